@@ -1,0 +1,137 @@
+/*
+ * pbrt_amd.h — C ABI of the MI355X-native wavefront hot path (drop-in for pbrt-v4's
+ * WavefrontPathIntegrator + WavefrontAggregate).
+ *
+ * Every entry point replaces a reference interface (file:line in scienstanford/pbrt-v4):
+ *
+ *   pbrt_scene_load / pbrt_scene_load_string
+ *       pbrt::ParseFiles + BasicScene (cmd/pbrt.cpp:291-293, scene.h:260) for the .pbrt
+ *       subset the hot path needs; overrides mirror --spp / --seed / --pixelbounds.
+ *   pbrt_context_create
+ *       WavefrontPathIntegrator ctor (wavefront/integrator.cpp:80-287): device scene
+ *       upload, BVH build (replaces OptiXAggregate ctor, gpu/aggregate.cpp:1179-1663), queue
+ *       allocation sized for maxPathsPerPass (integrator.cpp:227-236 uses 1M).
+ *   pbrt_render
+ *       WavefrontPathIntegrator::Render (wavefront/integrator.cpp:290-493) restricted to a
+ *       set of film rows and a range of sample indices; asynchronous on the context stream.
+ *   pbrt_intersect
+ *       WavefrontAggregate::IntersectClosest / IntersectShadow (wavefront/integrator.h:32-54)
+ *       over caller-owned device SoA ray buffers.
+ *   pbrt_film_*
+ *       RGBFilm pixel storage (film.h:305-310) and GetPixelRGB (film.h:261-277).
+ *
+ * Conventions: 0 = success, nonzero = error with text from pbrt_last_error(); device
+ * buffers are caller-owned where passed in; one hipStream per context; nothing blocks
+ * except pbrt_synchronize / pbrt_film_read / pbrt_film_get_rgb.
+ */
+#ifndef PBRT_AMD_H
+#define PBRT_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct pbrt_scene pbrt_scene;
+typedef struct pbrt_context pbrt_context;
+
+typedef struct pbrt_scene_info {
+    int xres, yres;
+    int px0, px1, py0, py1; /* pixel bounds [px0,px1) x [py0,py1) */
+    int spp, seed, max_depth;
+    int n_triangles, n_vertices, n_materials, n_area_lights, n_infinite_lights;
+    int n_light_nodes, uniform_light_sampler;
+    float filter_radius_x, filter_radius_y;
+} pbrt_scene_info;
+
+/* Flattened, read-only view of a loaded scene (pointers into scene-owned memory). Used
+ * by the CPU oracle and by tests; layout documented in DESIGN.md. */
+typedef struct pbrt_scene_flat {
+    int n_vertices, n_triangles, n_materials, n_area_lights, n_infinite_lights, n_spectra;
+    const float *vertices;        /* [n_vertices][3] render space */
+    const int32_t *triangles;     /* [n_triangles][3] */
+    const int32_t *tri_material;  /* [n_triangles] */
+    const int32_t *tri_light;     /* [n_triangles], -1 if not emissive */
+    const uint8_t *tri_flip;      /* [n_triangles] reverseOrientation ^ swapsHandedness */
+    const float *material_coeffs; /* [n_materials][4]: c0 c1 c2 constant */
+    const int32_t *material_constant;
+    const int32_t *light_prim;    /* [n_area_lights] */
+    const float *light_scale;
+    const int32_t *light_spectrum;
+    const int32_t *light_two_sided;
+    const int32_t *inf_spectrum;  /* [n_infinite_lights] */
+    const float *inf_scale;
+    const float *dense_spectra;   /* [n_spectra][311] at 395..705 nm */
+    const float *sensor_xyz;      /* [3][311] */
+    float imaging_ratio;
+    float camera_from_raster[16];
+    float render_from_camera[16];
+    float lens_radius, focal_distance;
+    double output_rgb_from_sensor_rgb[9];
+    /* light BVH: [n_light_nodes][12] floats pMin3 pMax3 w3 phi cosO cosE, plus ints */
+    int n_light_nodes;
+    const float *light_node_bounds;
+    const int32_t *light_node_info; /* [n][3]: childOrLight, isLeaf, twoSided */
+    const uint32_t *light_bit_trail;
+    /* Halton */
+    int halton_base_scales[2], halton_base_exponents[2], halton_mult_inverse[2];
+    int n_dims;
+    const uint16_t *perm_table;
+    const uint32_t *perm_offset, *perm_ndigits, *perm_base;
+} pbrt_scene_flat;
+
+typedef struct pbrt_render_params {
+    const int32_t *rows; /* host array of absolute film rows to render (within bounds) */
+    int n_rows;
+    int first_sample;    /* first sample index */
+    int n_samples;       /* number of consecutive sample indices */
+    int time_closest;    /* 1: record HIP events around every closest-hit launch */
+} pbrt_render_params;
+
+typedef struct pbrt_render_stats {
+    uint64_t camera_rays, closest_rays, shadow_rays; /* valid after pbrt_synchronize */
+    int closest_launches;
+    double closest_ms;   /* sum of event-timed closest-hit kernel durations */
+    int passes;
+    uint64_t paths_per_pass;
+} pbrt_render_stats;
+
+const char *pbrt_last_error(void);
+int pbrt_set_data_dir(const char *dir);
+
+int pbrt_scene_load(const char *path, const char *overrides, pbrt_scene **out);
+int pbrt_scene_load_string(const char *text, const char *base_dir, const char *overrides, pbrt_scene **out);
+void pbrt_scene_free(pbrt_scene *scene);
+int pbrt_scene_get_info(const pbrt_scene *scene, pbrt_scene_info *info);
+int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *flat);
+
+int pbrt_device_count(int *count);
+int pbrt_context_create(const pbrt_scene *scene, int device, int64_t max_paths_per_pass, pbrt_context **out);
+void pbrt_context_free(pbrt_context *ctx);
+
+int pbrt_render(pbrt_context *ctx, const pbrt_render_params *params);
+int pbrt_synchronize(pbrt_context *ctx);
+int pbrt_get_stats(pbrt_context *ctx, pbrt_render_stats *stats);
+int pbrt_reset_stats(pbrt_context *ctx);
+
+int pbrt_film_clear(pbrt_context *ctx);
+int pbrt_film_device_ptr(pbrt_context *ctx, double **film, size_t *n_doubles);
+int pbrt_film_read(pbrt_context *ctx, double *out);     /* [4][xres*yres] sensor RGB sums + weight */
+int pbrt_film_get_rgb(pbrt_context *ctx, float *rgb);   /* [yres*xres][3] output colour space */
+
+/* WavefrontAggregate boundary: rays_dev = [7][n] SoA (o.xyz, d.xyz, tMax) on the device;
+ * prim_dev [n] receives the original triangle index or -1; hit_dev [4][n] b0 b1 b2 t. */
+int pbrt_intersect(pbrt_context *ctx, const float *rays_dev, int n, int any_hit, int32_t *prim_dev, float *hit_dev);
+
+/* host-side evaluation of product components (no GPU): used by golden-vector tests */
+float pbrt_debug_halton(const pbrt_scene *scene, int px, int py, int sample_index, int dim);
+int pbrt_debug_rgb_coeffs(float r, float g, float b, float *coeffs3);
+int pbrt_debug_rgb2spec_column(int maxc, int j, int i, float *out192);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PBRT_AMD_H */

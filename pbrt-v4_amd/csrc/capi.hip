@@ -1,0 +1,692 @@
+// C ABI and render driver of pbrt-v4_amd (declared in include/pbrt_amd.h).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/pbrt_amd.h"
+#include "host/bvh.h"
+#include "host/scene.h"
+#include "kernels/device.h"
+
+namespace pbrt_amd {
+hipError_t LaunchCamera(const DeviceScene &S, const PathState &st, int nActive, hipStream_t s);
+hipError_t LaunchClosest(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
+hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
+hipError_t LaunchShadow(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
+hipError_t LaunchFilm(const DeviceScene &S, const PathState &st, int nSamples, hipStream_t s);
+hipError_t LaunchIntersectBatch(const DeviceScene &S, const float *rays, int n, int anyHit, int *outPrim,
+                                float *outHit, hipStream_t s);
+}  // namespace pbrt_amd
+
+using namespace pbrt_amd;
+
+static thread_local std::string g_lastError;
+static int Fail(const std::string &msg) {
+    g_lastError = msg;
+    return 1;
+}
+#define HIPCHECK(x)                                                                                     \
+    do {                                                                                                \
+        hipError_t e_ = (x);                                                                            \
+        if (e_ != hipSuccess) throw Error(std::string("HIP error ") + hipGetErrorString(e_) + " at " #x); \
+    } while (0)
+
+struct pbrt_scene {
+    SceneDesc desc;
+    // flattened copies for pbrt_scene_get_flat
+    std::vector<float> verts, matCoeffs, lightScale, infScale, dense, sensor, nodeBounds;
+    std::vector<int32_t> tris, lightPrim, lightSpectrum, lightTwoSided, infSpectrum, matConstant, nodeInfo;
+    void Flatten() {
+        const SceneDesc &s = desc;
+        verts.clear();
+        for (V3 v : s.verts) {
+            verts.push_back(v.x);
+            verts.push_back(v.y);
+            verts.push_back(v.z);
+        }
+        tris.clear();
+        for (auto &t : s.tris) tris.insert(tris.end(), t.begin(), t.end());
+        matCoeffs.clear();
+        matConstant.clear();
+        for (auto &m : s.materials) {
+            matCoeffs.insert(matCoeffs.end(), {m.c0, m.c1, m.c2, m.constantValue});
+            matConstant.push_back(m.constant ? 1 : 0);
+        }
+        lightPrim.clear();
+        lightScale.clear();
+        lightSpectrum.clear();
+        lightTwoSided.clear();
+        for (auto &l : s.areaLights) {
+            lightPrim.push_back(l.prim);
+            lightScale.push_back(l.scale);
+            lightSpectrum.push_back(l.spectrum);
+            lightTwoSided.push_back(l.twoSided ? 1 : 0);
+        }
+        infSpectrum.clear();
+        infScale.clear();
+        for (auto &l : s.infiniteLights) {
+            infSpectrum.push_back(l.spectrum);
+            infScale.push_back(l.scale);
+        }
+        dense.clear();
+        for (auto &d : s.denseSpectra) dense.insert(dense.end(), d.begin(), d.end());
+        sensor.clear();
+        sensor.insert(sensor.end(), s.sensorX.begin(), s.sensorX.end());
+        sensor.insert(sensor.end(), s.sensorY.begin(), s.sensorY.end());
+        sensor.insert(sensor.end(), s.sensorZ.begin(), s.sensorZ.end());
+        nodeBounds.clear();
+        nodeInfo.clear();
+        for (auto &n : s.lightNodes) {
+            const LightNodeBounds &b = n.bounds;
+            nodeBounds.insert(nodeBounds.end(), {b.pMin.x, b.pMin.y, b.pMin.z, b.pMax.x, b.pMax.y, b.pMax.z, b.w.x, b.w.y,
+                                                 b.w.z, b.phi, b.cosTheta_o, b.cosTheta_e});
+            nodeInfo.insert(nodeInfo.end(), {n.childOrLight, n.isLeaf, b.twoSided});
+        }
+    }
+};
+
+template <typename T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    void Alloc(size_t count) {
+        Free();
+        n = count;
+        if (count) HIPCHECK(hipMalloc((void **)&p, count * sizeof(T)));
+    }
+    void Upload(const std::vector<T> &v) {
+        Alloc(v.size());
+        if (!v.empty()) HIPCHECK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    }
+    void Free() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    ~DevBuf() { Free(); }
+};
+
+struct pbrt_context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    SceneDesc desc;
+    BVH8 bvh;
+    DeviceScene S{};
+    // scene buffers
+    DevBuf<BVH8Node> nodes;
+    DevBuf<float> triVerts, matCoeffs, lightScale, lightArea, infScale, dense, sensor;
+    DevBuf<int> primMaterial, primLight, matConstant, lightPrim, lightSpectrum, lightTwoSided, infSpectrum;
+    DevBuf<int> primOrig;
+    DevBuf<uint8_t> primFlip;
+    DevBuf<uint32_t> lightBitTrail, permOffset, permNDigits, permBase;
+    DevBuf<uint16_t> perm;
+    DevBuf<DeviceLightNode> lightNodes;
+    // wavefront buffers
+    int64_t maxPaths = 0;
+    DevBuf<float> fState;
+    DevBuf<int> iState;
+    DevBuf<int> rows;
+    DevBuf<double> film;
+    PathState st{};
+    // timing
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
+    int eventsUsed = 0;
+    pbrt_render_stats stats{};
+    std::vector<int> hostCounters;
+    std::vector<int> lastRows;
+
+    ~pbrt_context() {
+        for (auto &e : events) {
+            (void)hipEventDestroy(e.first);
+            (void)hipEventDestroy(e.second);
+        }
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+static void BuildDevice(pbrt_context *c) {
+    SceneDesc &s = c->desc;
+    HIPCHECK(hipSetDevice(c->device));
+    HIPCHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    c->bvh = BuildBVH8(s.verts, s.tris, 4);
+    if (7 * c->bvh.maxDepth + 1 > 64) throw Error("BVH too deep for the traversal stack");
+    BVH8 &b = c->bvh;
+    int nt = (int)s.tris.size();
+    std::vector<int> origToLeaf(nt);
+    for (int i = 0; i < nt; ++i) origToLeaf[b.triPrim[i]] = i;
+    std::vector<int> pm(nt), pl(nt);
+    std::vector<uint8_t> pf(nt);
+    for (int i = 0; i < nt; ++i) {
+        int o = b.triPrim[i];
+        pm[i] = s.triMaterial[o];
+        pl[i] = s.triLight[o];
+        pf[i] = s.triFlip[o];
+    }
+    c->nodes.Upload(b.nodes);
+    c->triVerts.Upload(b.triVerts);
+    c->primMaterial.Upload(pm);
+    c->primLight.Upload(pl);
+    c->primFlip.Upload(pf);
+    c->primOrig.Upload(b.triPrim);
+    std::vector<float> mc;
+    std::vector<int> mk;
+    for (auto &m : s.materials) {
+        mc.insert(mc.end(), {m.c0, m.c1, m.c2, m.constantValue});
+        mk.push_back(m.constant);
+    }
+    c->matCoeffs.Upload(mc);
+    c->matConstant.Upload(mk);
+    std::vector<int> lp, ls, lt;
+    std::vector<float> lsc, la;
+    for (auto &l : s.areaLights) {
+        lp.push_back(origToLeaf[l.prim]);
+        ls.push_back(l.spectrum);
+        lt.push_back(l.twoSided);
+        lsc.push_back(l.scale);
+        la.push_back(l.area);
+    }
+    c->lightPrim.Upload(lp);
+    c->lightSpectrum.Upload(ls);
+    c->lightTwoSided.Upload(lt);
+    c->lightScale.Upload(lsc);
+    c->lightArea.Upload(la);
+    std::vector<int> is;
+    std::vector<float> isc;
+    for (auto &l : s.infiniteLights) {
+        is.push_back(l.spectrum);
+        isc.push_back(l.scale);
+    }
+    c->infSpectrum.Upload(is);
+    c->infScale.Upload(isc);
+    std::vector<float> dense;
+    for (auto &d : s.denseSpectra) dense.insert(dense.end(), d.begin(), d.end());
+    c->dense.Upload(dense);
+    std::vector<float> sensor;
+    sensor.insert(sensor.end(), s.sensorX.begin(), s.sensorX.end());
+    sensor.insert(sensor.end(), s.sensorY.begin(), s.sensorY.end());
+    sensor.insert(sensor.end(), s.sensorZ.begin(), s.sensorZ.end());
+    c->sensor.Upload(sensor);
+    std::vector<uint32_t> bt(s.areaLights.size(), 0xffffffffu);
+    if (!s.uniformLightSampler)
+        for (auto &n : s.lightNodes)
+            if (n.isLeaf) bt[n.childOrLight] = s.lightBitTrail[n.childOrLight];
+    c->lightBitTrail.Upload(bt);
+    std::vector<DeviceLightNode> ln;
+    for (auto &n : s.lightNodes) ln.push_back(DeviceLightNode{n.bounds, n.childOrLight, n.isLeaf});
+    c->lightNodes.Upload(ln);
+    c->perm.Upload(s.permTable);
+    c->permOffset.Upload(s.permOffset);
+    c->permNDigits.Upload(s.permNDigits);
+    c->permBase.Upload(s.permBase);
+
+    DeviceScene &S = c->S;
+    S.nodes = c->nodes.p;
+    S.triVerts = (const float4 *)c->triVerts.p;
+    S.nTris = nt;
+    S.primMaterial = c->primMaterial.p;
+    S.primLight = c->primLight.p;
+    S.primFlip = c->primFlip.p;
+    S.matCoeffs = (const float4 *)c->matCoeffs.p;
+    S.matConstant = c->matConstant.p;
+    S.nMaterials = (int)s.materials.size();
+    S.nAreaLights = (int)s.areaLights.size();
+    S.lightPrim = c->lightPrim.p;
+    S.lightScale = c->lightScale.p;
+    S.lightSpectrum = c->lightSpectrum.p;
+    S.lightTwoSided = c->lightTwoSided.p;
+    S.lightArea = c->lightArea.p;
+    S.lightBitTrail = c->lightBitTrail.p;
+    S.nInfinite = (int)s.infiniteLights.size();
+    S.infSpectrum = c->infSpectrum.p;
+    S.infScale = c->infScale.p;
+    S.uniformLightSampler = s.uniformLightSampler ? 1 : 0;
+    S.lightNodes = c->lightNodes.p;
+    S.nLightNodes = (int)s.lightNodes.size();
+    S.dense = c->dense.p;
+    S.sensor = c->sensor.p;
+    S.imagingRatio = s.imagingRatio;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            S.cameraFromRaster[4 * i + j] = (float)s.camera.cameraFromRaster[i][j];
+            S.renderFromCamera[4 * i + j] = (float)s.camera.renderFromCamera[i][j];
+        }
+    S.lensRadius = s.camera.lensRadius;
+    S.focalDistance = s.camera.focalDistance;
+    S.xres = s.xres;
+    S.yres = s.yres;
+    S.px0 = s.px0;
+    S.px1 = s.px1;
+    S.py0 = s.py0;
+    S.py1 = s.py1;
+    S.filterRadiusX = s.filterRadiusX;
+    S.filterRadiusY = s.filterRadiusY;
+    S.perm = c->perm.p;
+    S.permOffset = c->permOffset.p;
+    S.permNDigits = c->permNDigits.p;
+    S.permBase = c->permBase.p;
+    S.nDims = (int)s.permBase.size();
+    for (int i = 0; i < 2; ++i) {
+        S.baseScales[i] = s.haltonBaseScales[i];
+        S.baseExponents[i] = s.haltonBaseExponents[i];
+        S.multInverse[i] = s.haltonMultInverse[i];
+    }
+    S.maxDepth = s.maxDepth;
+
+    // film
+    size_t npix = (size_t)s.xres * s.yres;
+    c->film.Alloc(4 * npix);
+    HIPCHECK(hipMemset(c->film.p, 0, 4 * npix * sizeof(double)));
+}
+
+static void AllocPaths(pbrt_context *c, int64_t N) {
+    if (N <= c->maxPaths) return;
+    // float arrays: beta 31, rl 1, L 3, lambda0 1, filterW 1, etaScale 1, ray 6, ctx 12, hitB 4,
+    // shadowRay 6, shadowL 3  = 69 floats; int arrays: flags, hitPrim, rayQ x2, matQ, shadowQ = 6
+    const int nf = 69, ni = 6;
+    c->fState.Alloc((size_t)nf * N);
+    c->iState.Alloc((size_t)ni * N + 4 * (c->desc.maxDepth + 3));
+    c->maxPaths = N;
+    PathState &st = c->st;
+    float *f = c->fState.p;
+    auto take = [&](int k) {
+        float *r = f;
+        f += (size_t)k * N;
+        return r;
+    };
+    st.beta = take(31);
+    st.rl = take(1);
+    st.L = take(3);
+    st.lambda0 = take(1);
+    st.filterW = take(1);
+    st.etaScale = take(1);
+    st.ray = take(6);
+    st.ctx = take(12);
+    st.hitB = take(4);
+    st.shadowRay = take(6);
+    st.shadowL = take(3);
+    int *ip = c->iState.p;
+    auto takei = [&](int k) {
+        int *r = ip;
+        ip += (size_t)k * N;
+        return r;
+    };
+    st.flags = takei(1);
+    st.hitPrim = takei(1);
+    st.rayQ[0] = takei(1);
+    st.rayQ[1] = takei(1);
+    st.matQ = takei(1);
+    st.shadowQ = takei(1);
+    st.counters = ip;
+}
+
+static void RecordEvent(pbrt_context *c, bool start) {
+    if (start) {
+        if (c->eventsUsed == (int)c->events.size()) {
+            hipEvent_t a, b;
+            HIPCHECK(hipEventCreate(&a));
+            HIPCHECK(hipEventCreate(&b));
+            c->events.push_back({a, b});
+        }
+        HIPCHECK(hipEventRecord(c->events[c->eventsUsed].first, c->stream));
+    } else {
+        HIPCHECK(hipEventRecord(c->events[c->eventsUsed].second, c->stream));
+        ++c->eventsUsed;
+    }
+}
+
+static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
+    HIPCHECK(hipSetDevice(c->device));
+    const SceneDesc &s = c->desc;
+    int width = s.px1 - s.px0;
+    if (width <= 0) throw Error("empty pixel bounds");
+    std::vector<int> rows;
+    for (int i = 0; i < p->n_rows; ++i) {
+        int y = p->rows[i];
+        if (y < s.py0 || y >= s.py1) throw Error("row outside the film pixel bounds");
+        rows.push_back(y);
+    }
+    if (rows.empty() || p->n_samples <= 0) return;
+    int64_t maxPaths = c->maxPaths;
+    // rows per chunk so that one sample of the chunk fits
+    int64_t rowsPerChunk = std::max<int64_t>(1, maxPaths / width);
+    if (rows != c->lastRows) {
+        HIPCHECK(hipStreamSynchronize(c->stream));  // earlier passes may still read the row table
+        c->rows.Alloc(rows.size());
+        HIPCHECK(hipMemcpy(c->rows.p, rows.data(), rows.size() * sizeof(int), hipMemcpyHostToDevice));
+        c->lastRows = rows;
+    }
+    const int countersBytes = 4 * (s.maxDepth + 3) * sizeof(int);
+    for (size_t r0 = 0; r0 < rows.size(); r0 += rowsPerChunk) {
+        int nRows = (int)std::min<int64_t>(rowsPerChunk, rows.size() - r0);
+        int64_t P = (int64_t)nRows * width;
+        int64_t samplesPerPass = std::max<int64_t>(1, std::min<int64_t>(p->n_samples, maxPaths / P));
+        for (int s0 = 0; s0 < p->n_samples; s0 += (int)samplesPerPass) {
+            int nS = (int)std::min<int64_t>(samplesPerPass, p->n_samples - s0);
+            int64_t nActive = P * nS;
+            PathState st = c->st;
+            st.N = (int)c->maxPaths;
+            st.P = (int)P;
+            st.width = width;
+            st.rows = c->rows.p + r0;
+            st.firstSample = p->first_sample + s0;
+            st.film = c->film.p;
+            HIPCHECK(hipMemsetAsync(st.counters, 0, countersBytes, c->stream));
+            HIPCHECK(LaunchCamera(c->S, st, (int)nActive, c->stream));
+            for (int depth = 0; depth <= s.maxDepth; ++depth) {
+                if (p->time_closest) RecordEvent(c, true);
+                HIPCHECK(LaunchClosest(c->S, st, depth, (int)nActive, c->stream));
+                if (p->time_closest) RecordEvent(c, false);
+                HIPCHECK(LaunchShadeDiffuse(c->S, st, depth, (int)nActive, c->stream));
+                if (depth == s.maxDepth) break;
+                HIPCHECK(LaunchShadow(c->S, st, depth, (int)nActive, c->stream));
+            }
+            HIPCHECK(LaunchFilm(c->S, st, nS, c->stream));
+            c->stats.passes++;
+            c->stats.camera_rays += nActive;
+            c->stats.paths_per_pass = std::max<uint64_t>(c->stats.paths_per_pass, nActive);
+        }
+    }
+}
+
+extern "C" {
+
+const char *pbrt_last_error(void) { return g_lastError.c_str(); }
+
+int pbrt_set_data_dir(const char *dir) {
+    SetDataDirectory(dir ? dir : "");
+    return 0;
+}
+
+static std::map<std::string, std::string> ParseOverrides(const char *ov) {
+    std::map<std::string, std::string> m;
+    if (!ov) return m;
+    std::stringstream ss(ov);
+    std::string item;
+    while (std::getline(ss, item, ';')) {
+        auto eq = item.find('=');
+        if (eq == std::string::npos) continue;
+        m[item.substr(0, eq)] = item.substr(eq + 1);
+    }
+    return m;
+}
+
+int pbrt_scene_load(const char *path, const char *overrides, pbrt_scene **out) {
+    try {
+        auto s = std::make_unique<pbrt_scene>();
+        s->desc = LoadPbrtFile(path, ParseOverrides(overrides));
+        s->Flatten();
+        *out = s.release();
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_scene_load_string(const char *text, const char *base_dir, const char *overrides, pbrt_scene **out) {
+    try {
+        auto s = std::make_unique<pbrt_scene>();
+        s->desc = LoadPbrtString(text, base_dir ? base_dir : "", ParseOverrides(overrides));
+        s->Flatten();
+        *out = s.release();
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+void pbrt_scene_free(pbrt_scene *scene) { delete scene; }
+
+int pbrt_scene_get_info(const pbrt_scene *scene, pbrt_scene_info *info) {
+    if (!scene || !info) return Fail("null argument");
+    const SceneDesc &s = scene->desc;
+    info->xres = s.xres;
+    info->yres = s.yres;
+    info->px0 = s.px0;
+    info->px1 = s.px1;
+    info->py0 = s.py0;
+    info->py1 = s.py1;
+    info->spp = s.spp;
+    info->seed = s.seed;
+    info->max_depth = s.maxDepth;
+    info->n_triangles = (int)s.tris.size();
+    info->n_vertices = (int)s.verts.size();
+    info->n_materials = (int)s.materials.size();
+    info->n_area_lights = (int)s.areaLights.size();
+    info->n_infinite_lights = (int)s.infiniteLights.size();
+    info->n_light_nodes = (int)s.lightNodes.size();
+    info->uniform_light_sampler = s.uniformLightSampler;
+    info->filter_radius_x = s.filterRadiusX;
+    info->filter_radius_y = s.filterRadiusY;
+    return 0;
+}
+
+int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
+    if (!scene || !f) return Fail("null argument");
+    const SceneDesc &s = scene->desc;
+    memset(f, 0, sizeof(*f));
+    f->n_vertices = (int)s.verts.size();
+    f->n_triangles = (int)s.tris.size();
+    f->n_materials = (int)s.materials.size();
+    f->n_area_lights = (int)s.areaLights.size();
+    f->n_infinite_lights = (int)s.infiniteLights.size();
+    f->n_spectra = (int)s.denseSpectra.size();
+    f->vertices = scene->verts.data();
+    f->triangles = scene->tris.data();
+    f->tri_material = s.triMaterial.data();
+    f->tri_light = s.triLight.data();
+    f->tri_flip = s.triFlip.data();
+    f->material_coeffs = scene->matCoeffs.data();
+    f->material_constant = scene->matConstant.data();
+    f->light_prim = scene->lightPrim.data();
+    f->light_scale = scene->lightScale.data();
+    f->light_spectrum = scene->lightSpectrum.data();
+    f->light_two_sided = scene->lightTwoSided.data();
+    f->inf_spectrum = scene->infSpectrum.data();
+    f->inf_scale = scene->infScale.data();
+    f->dense_spectra = scene->dense.data();
+    f->sensor_xyz = scene->sensor.data();
+    f->imaging_ratio = s.imagingRatio;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            f->camera_from_raster[4 * i + j] = (float)s.camera.cameraFromRaster[i][j];
+            f->render_from_camera[4 * i + j] = (float)s.camera.renderFromCamera[i][j];
+        }
+    f->lens_radius = s.camera.lensRadius;
+    f->focal_distance = s.camera.focalDistance;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) f->output_rgb_from_sensor_rgb[3 * i + j] = s.outputRGBFromSensorRGB[i][j];
+    f->n_light_nodes = (int)s.lightNodes.size();
+    f->light_node_bounds = scene->nodeBounds.data();
+    f->light_node_info = scene->nodeInfo.data();
+    f->light_bit_trail = s.lightBitTrail.data();
+    for (int i = 0; i < 2; ++i) {
+        f->halton_base_scales[i] = s.haltonBaseScales[i];
+        f->halton_base_exponents[i] = s.haltonBaseExponents[i];
+        f->halton_mult_inverse[i] = s.haltonMultInverse[i];
+    }
+    f->n_dims = (int)s.permBase.size();
+    f->perm_table = s.permTable.data();
+    f->perm_offset = s.permOffset.data();
+    f->perm_ndigits = s.permNDigits.data();
+    f->perm_base = s.permBase.data();
+    return 0;
+}
+
+int pbrt_device_count(int *count) {
+    hipError_t e = hipGetDeviceCount(count);
+    if (e != hipSuccess) {
+        *count = 0;
+        return Fail(std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+    }
+    return 0;
+}
+
+int pbrt_context_create(const pbrt_scene *scene, int device, int64_t maxPaths, pbrt_context **out) {
+    try {
+        if (!scene) return Fail("null scene");
+        auto c = std::make_unique<pbrt_context>();
+        c->device = device;
+        c->desc = scene->desc;
+        BuildDevice(c.get());
+        if (maxPaths <= 0) maxPaths = 1 << 22;
+        AllocPaths(c.get(), maxPaths);
+        *out = c.release();
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+void pbrt_context_free(pbrt_context *ctx) { delete ctx; }
+
+int pbrt_render(pbrt_context *ctx, const pbrt_render_params *params) {
+    try {
+        if (!ctx || !params) return Fail("null argument");
+        RenderImpl(ctx, params);
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_synchronize(pbrt_context *ctx) {
+    try {
+        HIPCHECK(hipSetDevice(ctx->device));
+        HIPCHECK(hipStreamSynchronize(ctx->stream));
+        for (int i = 0; i < ctx->eventsUsed; ++i) {
+            float ms = 0;
+            HIPCHECK(hipEventElapsedTime(&ms, ctx->events[i].first, ctx->events[i].second));
+            ctx->stats.closest_ms += ms;
+            ctx->stats.closest_launches++;
+        }
+        ctx->eventsUsed = 0;
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_get_stats(pbrt_context *ctx, pbrt_render_stats *stats) {
+    *stats = ctx->stats;
+    return 0;
+}
+
+int pbrt_reset_stats(pbrt_context *ctx) {
+    ctx->stats = pbrt_render_stats{};
+    return 0;
+}
+
+int pbrt_film_clear(pbrt_context *ctx) {
+    try {
+        HIPCHECK(hipSetDevice(ctx->device));
+        HIPCHECK(hipMemsetAsync(ctx->film.p, 0, ctx->film.n * sizeof(double), ctx->stream));
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_film_device_ptr(pbrt_context *ctx, double **film, size_t *n) {
+    *film = ctx->film.p;
+    *n = ctx->film.n;
+    return 0;
+}
+
+int pbrt_film_read(pbrt_context *ctx, double *out) {
+    try {
+        HIPCHECK(hipSetDevice(ctx->device));
+        HIPCHECK(hipStreamSynchronize(ctx->stream));
+        HIPCHECK(hipMemcpy(out, ctx->film.p, ctx->film.n * sizeof(double), hipMemcpyDeviceToHost));
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_film_get_rgb(pbrt_context *ctx, float *rgb) {
+    try {
+        std::vector<double> f(ctx->film.n);
+        if (pbrt_film_read(ctx, f.data())) return 1;
+        size_t npix = (size_t)ctx->desc.xres * ctx->desc.yres;
+        const auto &m = ctx->desc.outputRGBFromSensorRGB;
+        for (size_t i = 0; i < npix; ++i) {
+            // RGBFilm::GetPixelRGB (film.h:261-277)
+            float c[3] = {(float)f[i], (float)f[npix + i], (float)f[2 * npix + i]};
+            float w = (float)f[3 * npix + i];
+            if (w != 0)
+                for (float &v : c) v /= w;
+            for (int k = 0; k < 3; ++k)
+                rgb[3 * i + k] = (float)(m[k][0] * c[0] + m[k][1] * c[1] + m[k][2] * c[2]);
+        }
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_intersect(pbrt_context *ctx, const float *rays, int n, int anyHit, int32_t *prim, float *hit) {
+    try {
+        HIPCHECK(hipSetDevice(ctx->device));
+        HIPCHECK(LaunchIntersectBatch(ctx->S, rays, n, anyHit, prim, hit, ctx->stream));
+        HIPCHECK(hipStreamSynchronize(ctx->stream));
+        // map leaf-order prim to the original triangle index on the host side of the copy
+        std::vector<int> p(n);
+        HIPCHECK(hipMemcpy(p.data(), prim, n * sizeof(int), hipMemcpyDeviceToHost));
+        for (int &v : p)
+            if (v >= 0) v = ctx->bvh.triPrim[v];
+        HIPCHECK(hipMemcpy(prim, p.data(), n * sizeof(int), hipMemcpyHostToDevice));
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+float pbrt_debug_halton(const pbrt_scene *scene, int px, int py, int sampleIndex, int dim) {
+    const SceneDesc &s = scene->desc;
+    uint64_t stride = (uint64_t)s.haltonBaseScales[0] * s.haltonBaseScales[1];
+    uint64_t index = 0;
+    if (stride > 1) {
+        int pm[2] = {((px % 128) + 128) % 128, ((py % 128) + 128) % 128};
+        for (int i = 0; i < 2; ++i) {
+            uint64_t off = InverseRadicalInverse((uint64_t)pm[i], i == 0 ? 2 : 3, s.haltonBaseExponents[i]);
+            index += off * (stride / s.haltonBaseScales[i]) * (uint64_t)s.haltonMultInverse[i];
+        }
+        index %= stride;
+    }
+    index += (uint64_t)sampleIndex * stride;
+    if (dim == -1) return RadicalInverse(2, index >> s.haltonBaseExponents[0]);
+    if (dim == -2) return RadicalInverse(3, index / s.haltonBaseScales[1]);
+    if (dim < 0 || dim >= (int)s.permBase.size()) return -1;
+    return ScrambledRadicalInverse(s.permBase[dim], s.permNDigits[dim], index, s.permTable.data() + s.permOffset[dim]);
+}
+
+int pbrt_debug_rgb_coeffs(float r, float g, float b, float *c) {
+    try {
+        auto v = RGBToSigmoidCoeffs(r, g, b);
+        c[0] = v[0];
+        c[1] = v[1];
+        c[2] = v[2];
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_debug_rgb2spec_column(int maxc, int j, int i, float *out) {
+    try {
+        auto v = RGB2SpecColumn(maxc, j, i);
+        std::copy(v.begin(), v.end(), out);
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+}  // extern "C"

@@ -1,0 +1,560 @@
+// pbrt-v4_amd core: host+device scalar math shared by the HIP kernels and the host
+// scene builder.  Every routine restates the reference semantics it names (file:line in
+// /root/reference/src/pbrt) with the same operation order, so that device results stay
+// within float rounding of pbrt's CPU path.  Compile with -ffp-contract=off: explicit
+// fmaf() is used exactly where pbrt calls FMA().
+#pragma once
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define PHD __host__ __device__ inline
+#else
+#define PHD inline
+#endif
+
+namespace pbrt_amd {
+
+constexpr float kPi = 3.14159265358979323846f;
+constexpr float kInvPi = 0.31830988618379067154f;
+constexpr float kPiOver2 = 1.57079632679489661923f;
+constexpr float kPiOver4 = 0.78539816339744830961f;
+constexpr float kInfinity = __builtin_huge_valf();
+constexpr float kMachineEpsilon = 5.9604644775390625e-08f;  // util/float.h:45
+constexpr float kOneMinusEpsilon = 0x1.fffffep-1f;           // util/float.h
+constexpr float kShadowEpsilon = 0.0001f;                    // util/math.h:42
+constexpr float kLambdaMin = 395.f, kLambdaMax = 705.f;      // util/spectrum.h:34
+constexpr int kNSpectrumSamples = 31;                        // util/spectrum.h:36
+constexpr float kMinSphericalSampleArea = 3e-4f;             // shapes.h
+constexpr float kMaxSphericalSampleArea = 6.22f;
+
+// ---------------------------------------------------------------- float utilities
+PHD uint32_t FloatToBits(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    return u;
+}
+PHD float BitsToFloat(uint32_t u) {
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+// util/float.h NextFloatUp/NextFloatDown
+PHD float NextFloatUp(float v) {
+    if (std::isinf(v) && v > 0.f) return v;
+    if (v == -0.f) v = 0.f;
+    uint32_t ui = FloatToBits(v);
+    if (v >= 0) ++ui; else --ui;
+    return BitsToFloat(ui);
+}
+PHD float NextFloatDown(float v) {
+    if (std::isinf(v) && v < 0.f) return v;
+    if (v == 0.f) v = -0.f;
+    uint32_t ui = FloatToBits(v);
+    if (v > 0) --ui; else ++ui;
+    return BitsToFloat(ui);
+}
+// util/float.h:197 gamma(n)
+PHD constexpr float gamma(int n) { return (n * kMachineEpsilon) / (1 - n * kMachineEpsilon); }
+
+PHD float Sqr(float v) { return v * v; }
+PHD float Clampf(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
+PHD float Lerpf(float t, float a, float b) { return (1 - t) * a + t * b; }
+PHD float SafeSqrt(float x) { return std::sqrt(std::fmax(0.f, x)); }
+PHD float SafeASin(float x) { return std::asin(Clampf(x, -1, 1)); }
+PHD float SafeACos(float x) { return std::acos(Clampf(x, -1, 1)); }
+// util/math.h:570-583
+PHD float DifferenceOfProducts(float a, float b, float c, float d) {
+    float cd = c * d;
+    float dop = fmaf(a, b, -cd);
+    float err = fmaf(-c, d, cd);
+    return dop + err;
+}
+PHD float SumOfProducts(float a, float b, float c, float d) {
+    float cd = c * d;
+    float sop = fmaf(a, b, cd);
+    float err = fmaf(c, d, -cd);
+    return sop + err;
+}
+
+// ---------------------------------------------------------------- vectors
+struct V3 {
+    float x, y, z;
+    PHD V3() : x(0), y(0), z(0) {}
+    PHD V3(float a, float b, float c) : x(a), y(b), z(c) {}
+    PHD float operator[](int i) const { return i == 0 ? x : (i == 1 ? y : z); }
+    PHD float &operator[](int i) { return i == 0 ? x : (i == 1 ? y : z); }
+};
+PHD V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+PHD V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+PHD V3 operator-(V3 a) { return {-a.x, -a.y, -a.z}; }
+PHD V3 operator*(float s, V3 a) { return {s * a.x, s * a.y, s * a.z}; }
+PHD V3 operator*(V3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+PHD V3 operator/(V3 a, float d) { return {a.x / d, a.y / d, a.z / d}; }
+PHD bool operator==(V3 a, V3 b) { return a.x == b.x && a.y == b.y && a.z == b.z; }
+PHD bool operator!=(V3 a, V3 b) { return !(a == b); }
+PHD V3 Abs(V3 a) { return {std::fabs(a.x), std::fabs(a.y), std::fabs(a.z)}; }
+// util/vecmath.h:966 (plain, left to right)
+PHD float Dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+PHD float AbsDot(V3 a, V3 b) { return std::fabs(Dot(a, b)); }
+// util/vecmath.h:1001 Cross via DifferenceOfProducts
+PHD V3 Cross(V3 v, V3 w) {
+    return {DifferenceOfProducts(v.y, w.z, v.z, w.y), DifferenceOfProducts(v.z, w.x, v.x, w.z),
+            DifferenceOfProducts(v.x, w.y, v.y, w.x)};
+}
+PHD float LengthSquared(V3 v) { return Sqr(v.x) + Sqr(v.y) + Sqr(v.z); }
+PHD float Length(V3 v) { return std::sqrt(LengthSquared(v)); }
+PHD V3 Normalize(V3 v) { return v / Length(v); }
+PHD float DistanceSquared(V3 a, V3 b) { return LengthSquared(a - b); }
+PHD float Distance(V3 a, V3 b) { return Length(a - b); }
+PHD float MaxComponentValue(V3 v) { return std::fmax(v.x, std::fmax(v.y, v.z)); }
+PHD int MaxComponentIndex(V3 v) { return (v.x > v.y) ? ((v.x > v.z) ? 0 : 2) : ((v.y > v.z) ? 1 : 2); }
+PHD V3 Permute(V3 v, int a, int b, int c) { return {v[a], v[b], v[c]}; }
+PHD V3 FaceForward(V3 n, V3 v) { return (Dot(n, v) < 0.f) ? -n : n; }
+PHD V3 GramSchmidt(V3 v, V3 w) { return v - Dot(v, w) * w; }
+// util/vecmath.h:974 AngleBetween
+PHD float AngleBetween(V3 v1, V3 v2) {
+    if (Dot(v1, v2) < 0) return kPi - 2 * SafeASin(Length(v1 + v2) / 2);
+    return 2 * SafeASin(Length(v2 - v1) / 2);
+}
+// util/vecmath.h:1009 CoordinateSystem
+PHD void CoordinateSystem(V3 v1, V3 *v2, V3 *v3) {
+    float sign = std::copysign(1.f, v1.z);
+    float a = -1 / (sign + v1.z);
+    float b = v1.x * v1.y * a;
+    *v2 = V3(1 + sign * Sqr(v1.x) * a, sign * b, -sign * v1.x);
+    *v3 = V3(b, sign + Sqr(v1.y) * a, -v1.y);
+}
+// util/vecmath.h:1640
+PHD float SphericalTriangleArea(V3 a, V3 b, V3 c) {
+    return std::fabs(2 * std::atan2(Dot(a, Cross(b, c)), 1 + Dot(a, b) + Dot(a, c) + Dot(b, c)));
+}
+
+// Frame (util/vecmath.h:1855): FromXZ(x, z) = (x, Cross(z, x), z)
+struct Frame {
+    V3 x, y, z;
+    PHD static Frame FromXZ(V3 x, V3 z) { return Frame{x, Cross(z, x), z}; }
+    PHD V3 ToLocal(V3 v) const { return {Dot(v, x), Dot(v, y), Dot(v, z)}; }
+    PHD V3 FromLocal(V3 v) const { return x * v.x + y * v.y + z * v.z; }
+};
+
+// ---------------------------------------------------------------- sampling (util/sampling.h)
+PHD float SampleLinear(float u, float a, float b) {  // :122
+    if (u == 0 && a == 0) return 0;
+    float x = u * (a + b) / (a + std::sqrt(Lerpf(u, Sqr(a), Sqr(b))));
+    return std::fmin(x, kOneMinusEpsilon);
+}
+PHD float BilinearPDF(float px, float py, const float w[4]) {  // :134
+    if (px < 0 || px > 1 || py < 0 || py > 1) return 0;
+    if (w[0] + w[1] + w[2] + w[3] == 0) return 1;
+    return 4 * ((1 - px) * (1 - py) * w[0] + px * (1 - py) * w[1] + (1 - px) * py * w[2] + px * py * w[3]) /
+           (w[0] + w[1] + w[2] + w[3]);
+}
+PHD void SampleBilinear(float u0, float u1, const float w[4], float *px, float *py) {  // :146
+    *py = SampleLinear(u1, w[0] + w[1], w[2] + w[3]);
+    *px = SampleLinear(u0, Lerpf(*py, w[0], w[2]), Lerpf(*py, w[1], w[3]));
+}
+PHD void SampleUniformTriangle(float u0, float u1, float b[3]) {  // :173
+    float b0, b1;
+    if (u0 < u1) {
+        b0 = u0 / 2;
+        b1 = u1 - b0;
+    } else {
+        b1 = u1 / 2;
+        b0 = u0 - b1;
+    }
+    b[0] = b0;
+    b[1] = b1;
+    b[2] = 1 - b0 - b1;
+}
+PHD void SampleUniformDiskConcentric(float u0, float u1, float *dx, float *dy) {  // :325
+    float ox = 2 * u0 - 1, oy = 2 * u1 - 1;
+    if (ox == 0 && oy == 0) {
+        *dx = 0;
+        *dy = 0;
+        return;
+    }
+    float theta, r;
+    if (std::fabs(ox) > std::fabs(oy)) {
+        r = ox;
+        theta = kPiOver4 * (oy / ox);
+    } else {
+        r = oy;
+        theta = kPiOver2 - kPiOver4 * (ox / oy);
+    }
+    *dx = r * std::cos(theta);
+    *dy = r * std::sin(theta);
+}
+PHD V3 SampleCosineHemisphere(float u0, float u1) {  // :409
+    float dx, dy;
+    SampleUniformDiskConcentric(u0, u1, &dx, &dy);
+    float z = SafeSqrt(1 - Sqr(dx) - Sqr(dy));
+    return V3(dx, dy, z);
+}
+PHD float CosineHemispherePDF(float cosTheta) { return cosTheta * kInvPi; }
+
+// util/sampling.h:79 SampleDiscrete specialised to two weights (light BVH child choice)
+PHD int SampleDiscrete2(float w0, float w1, float u, float *pmf, float *uRemapped) {
+    float sumWeights = 0;
+    sumWeights += w0;
+    sumWeights += w1;
+    float up = u * sumWeights;
+    if (up == sumWeights) up = NextFloatDown(up);
+    int offset = 0;
+    float sum = 0;
+    float wts[2] = {w0, w1};
+    while (sum + wts[offset] <= up) {
+        sum += wts[offset++];
+    }
+    *pmf = wts[offset] / sumWeights;
+    *uRemapped = std::fmin((up - sum) / wts[offset], kOneMinusEpsilon);
+    return offset;
+}
+
+// util/sampling.cpp:28 SampleSphericalTriangle (returns false when the reference returns {})
+PHD bool SampleSphericalTriangle(V3 v0, V3 v1, V3 v2, V3 p, float u0, float u1, float b[3],
+                                 float *pdf) {
+    *pdf = 0;
+    V3 a = v0 - p, bb = v1 - p, c = v2 - p;
+    a = Normalize(a);
+    bb = Normalize(bb);
+    c = Normalize(c);
+    V3 n_ab = Cross(a, bb), n_bc = Cross(bb, c), n_ca = Cross(c, a);
+    if (LengthSquared(n_ab) == 0 || LengthSquared(n_bc) == 0 || LengthSquared(n_ca) == 0) {
+        b[0] = b[1] = b[2] = 0;
+        return false;
+    }
+    n_ab = Normalize(n_ab);
+    n_bc = Normalize(n_bc);
+    n_ca = Normalize(n_ca);
+    float alpha = AngleBetween(n_ab, -n_ca);
+    float beta = AngleBetween(n_bc, -n_ab);
+    float gam = AngleBetween(n_ca, -n_bc);
+    float A_pi = alpha + beta + gam;
+    float Ap_pi = Lerpf(u0, kPi, A_pi);
+    {
+        float A = A_pi - kPi;
+        *pdf = (A <= 0) ? 0 : 1 / A;
+    }
+    float cosAlpha = std::cos(alpha), sinAlpha = std::sin(alpha);
+    float sinPhi = std::sin(Ap_pi) * cosAlpha - std::cos(Ap_pi) * sinAlpha;
+    float cosPhi = std::cos(Ap_pi) * cosAlpha + std::sin(Ap_pi) * sinAlpha;
+    float k1 = cosPhi + cosAlpha;
+    float k2 = sinPhi - sinAlpha * Dot(a, bb);
+    float cosBp = (k2 + (DifferenceOfProducts(k2, cosPhi, k1, sinPhi)) * cosAlpha) /
+                  ((SumOfProducts(k2, sinPhi, k1, cosPhi)) * sinAlpha);
+    cosBp = Clampf(cosBp, -1, 1);
+    float sinBp = SafeSqrt(1 - Sqr(cosBp));
+    V3 cp = cosBp * a + sinBp * Normalize(GramSchmidt(c, a));
+    float cosTheta = 1 - u1 * (1 - Dot(cp, bb));
+    float sinTheta = SafeSqrt(1 - Sqr(cosTheta));
+    V3 w = cosTheta * bb + sinTheta * Normalize(GramSchmidt(cp, bb));
+    V3 e1 = v1 - v0, e2 = v2 - v0;
+    V3 s1 = Cross(w, e2);
+    float divisor = Dot(s1, e1);
+    if (divisor == 0) {
+        b[0] = b[1] = b[2] = 1.f / 3.f;
+        return true;
+    }
+    float invDivisor = 1 / divisor;
+    V3 s = p - v0;
+    float b1 = Dot(s, s1) * invDivisor;
+    float b2 = Dot(w, Cross(s, e1)) * invDivisor;
+    b1 = Clampf(b1, 0, 1);
+    b2 = Clampf(b2, 0, 1);
+    if (b1 + b2 > 1) {
+        b1 /= b1 + b2;
+        b2 /= b1 + b2;  // sic: the reference divides by the updated sum
+    }
+    b[0] = 1 - b1 - b2;
+    b[1] = b1;
+    b[2] = b2;
+    return true;
+}
+
+// util/sampling.cpp:110 InvertSphericalTriangleSample
+PHD void InvertSphericalTriangleSample(V3 v0, V3 v1, V3 v2, V3 p, V3 w, float *u0out, float *u1out) {
+    V3 a = v0 - p, b = v1 - p, c = v2 - p;
+    a = Normalize(a);
+    b = Normalize(b);
+    c = Normalize(c);
+    V3 n_ab = Cross(a, b), n_bc = Cross(b, c), n_ca = Cross(c, a);
+    if (LengthSquared(n_ab) == 0 || LengthSquared(n_bc) == 0 || LengthSquared(n_ca) == 0) {
+        *u0out = 0;
+        *u1out = 0;
+        return;
+    }
+    n_ab = Normalize(n_ab);
+    n_bc = Normalize(n_bc);
+    n_ca = Normalize(n_ca);
+    float alpha = AngleBetween(n_ab, -n_ca);
+    float beta = AngleBetween(n_bc, -n_ab);
+    float gam = AngleBetween(n_ca, -n_bc);
+    V3 cp = Normalize(Cross(Cross(b, w), Cross(c, a)));
+    if (Dot(cp, a + c) < 0) cp = -cp;
+    float u0;
+    if (Dot(a, cp) > 0.99999847691f)
+        u0 = 0;
+    else {
+        V3 n_cpb = Cross(cp, b), n_acp = Cross(a, cp);
+        if (LengthSquared(n_cpb) == 0 || LengthSquared(n_acp) == 0) {
+            *u0out = 0.5f;
+            *u1out = 0.5f;
+            return;
+        }
+        n_cpb = Normalize(n_cpb);
+        n_acp = Normalize(n_acp);
+        float Ap = alpha + AngleBetween(n_ab, n_cpb) + AngleBetween(n_acp, -n_cpb) - kPi;
+        float A = alpha + beta + gam - kPi;
+        u0 = Ap / A;
+    }
+    float u1 = (1 - Dot(w, b)) / (1 - Dot(cp, b));
+    *u0out = Clampf(u0, 0, 1);
+    *u1out = Clampf(u1, 0, 1);
+}
+
+// ---------------------------------------------------------------- rays and triangles
+// ray.h:78 OffsetRayOrigin; error vector e is the Point3fi half-width
+PHD V3 OffsetRayOrigin(V3 p, V3 e, V3 n, V3 w) {
+    float d = Dot(Abs(n), e);
+    V3 offset = d * n;
+    if (Dot(w, n) < 0) offset = -offset;
+    V3 po = p + offset;
+    for (int i = 0; i < 3; ++i) {
+        if (offset[i] > 0)
+            po[i] = NextFloatUp(po[i]);
+        else if (offset[i] < 0)
+            po[i] = NextFloatDown(po[i]);
+    }
+    return po;
+}
+
+struct TriHit {
+    float b0, b1, b2, t;
+};
+
+// shapes.cpp:172-273 IntersectTriangle (watertight, fp64 edge fallback)
+PHD bool IntersectTriangle(V3 o, V3 dir, float tMax, V3 p0, V3 p1, V3 p2, TriHit *hit) {
+    if (LengthSquared(Cross(p2 - p0, p1 - p0)) == 0) return false;
+    V3 p0t = p0 - o, p1t = p1 - o, p2t = p2 - o;
+    int kz = MaxComponentIndex(Abs(dir));
+    int kx = kz + 1;
+    if (kx == 3) kx = 0;
+    int ky = kx + 1;
+    if (ky == 3) ky = 0;
+    V3 d = Permute(dir, kx, ky, kz);
+    p0t = Permute(p0t, kx, ky, kz);
+    p1t = Permute(p1t, kx, ky, kz);
+    p2t = Permute(p2t, kx, ky, kz);
+    float Sx = -d.x / d.z, Sy = -d.y / d.z, Sz = 1 / d.z;
+    p0t.x += Sx * p0t.z;
+    p0t.y += Sy * p0t.z;
+    p1t.x += Sx * p1t.z;
+    p1t.y += Sy * p1t.z;
+    p2t.x += Sx * p2t.z;
+    p2t.y += Sy * p2t.z;
+    float e0 = DifferenceOfProducts(p1t.x, p2t.y, p1t.y, p2t.x);
+    float e1 = DifferenceOfProducts(p2t.x, p0t.y, p2t.y, p0t.x);
+    float e2 = DifferenceOfProducts(p0t.x, p1t.y, p0t.y, p1t.x);
+    if (e0 == 0.0f || e1 == 0.0f || e2 == 0.0f) {
+        double p2txp1ty = (double)p2t.x * (double)p1t.y;
+        double p2typ1tx = (double)p2t.y * (double)p1t.x;
+        e0 = (float)(p2typ1tx - p2txp1ty);
+        double p0txp2ty = (double)p0t.x * (double)p2t.y;
+        double p0typ2tx = (double)p0t.y * (double)p2t.x;
+        e1 = (float)(p0typ2tx - p0txp2ty);
+        double p1txp0ty = (double)p1t.x * (double)p0t.y;
+        double p1typ0tx = (double)p1t.y * (double)p0t.x;
+        e2 = (float)(p1typ0tx - p1txp0ty);
+    }
+    if ((e0 < 0 || e1 < 0 || e2 < 0) && (e0 > 0 || e1 > 0 || e2 > 0)) return false;
+    float det = e0 + e1 + e2;
+    if (det == 0) return false;
+    p0t.z *= Sz;
+    p1t.z *= Sz;
+    p2t.z *= Sz;
+    float tScaled = e0 * p0t.z + e1 * p1t.z + e2 * p2t.z;
+    if (det < 0 && (tScaled >= 0 || tScaled < tMax * det)) return false;
+    if (det > 0 && (tScaled <= 0 || tScaled > tMax * det)) return false;
+    float invDet = 1 / det;
+    float b0 = e0 * invDet, b1 = e1 * invDet, b2 = e2 * invDet;
+    float t = tScaled * invDet;
+    float maxZt = MaxComponentValue(Abs(V3(p0t.z, p1t.z, p2t.z)));
+    float deltaZ = gamma(3) * maxZt;
+    float maxXt = MaxComponentValue(Abs(V3(p0t.x, p1t.x, p2t.x)));
+    float maxYt = MaxComponentValue(Abs(V3(p0t.y, p1t.y, p2t.y)));
+    float deltaX = gamma(5) * (maxXt + maxZt);
+    float deltaY = gamma(5) * (maxYt + maxZt);
+    float deltaE = 2 * (gamma(2) * maxXt * maxYt + deltaY * maxXt + deltaX * maxYt);
+    float maxE = MaxComponentValue(Abs(V3(e0, e1, e2)));
+    float deltaT = 3 * (gamma(3) * maxE * maxZt + deltaE * maxZt + deltaZ * maxE) * std::fabs(invDet);
+    if (t <= deltaT) return false;
+    hit->b0 = b0;
+    hit->b1 = b1;
+    hit->b2 = b2;
+    hit->t = t;
+    return true;
+}
+
+// Surface geometry of a triangle hit without shading normals or uv
+// (shapes.h:884-1010, mesh without n/s/uv: default uv (0,0),(1,0),(1,1)).
+struct TriSurface {
+    V3 p, pErr, n, dpdu;
+};
+PHD TriSurface TriangleSurface(V3 p0, V3 p1, V3 p2, float b0, float b1, float b2, bool flip) {
+    TriSurface s;
+    // uv = (0,0),(1,0),(1,1): duv02 = (-1,-1), duv12 = (0,-1)
+    const float duv02x = -1, duv02y = -1, duv12x = 0, duv12y = -1;
+    V3 dp02 = p0 - p2, dp12 = p1 - p2;
+    float determinant = DifferenceOfProducts(duv02x, duv12y, duv02y, duv12x);
+    V3 dpdu, dpdv;
+    bool degenerateUV = std::fabs(determinant) < 1e-9f;
+    if (!degenerateUV) {
+        float invdet = 1 / determinant;
+        dpdu = V3(DifferenceOfProducts(duv12y, dp02.x, duv02y, dp12.x),
+                  DifferenceOfProducts(duv12y, dp02.y, duv02y, dp12.y),
+                  DifferenceOfProducts(duv12y, dp02.z, duv02y, dp12.z)) *
+               invdet;
+        dpdv = V3(DifferenceOfProducts(duv02x, dp12.x, duv12x, dp02.x),
+                  DifferenceOfProducts(duv02x, dp12.y, duv12x, dp02.y),
+                  DifferenceOfProducts(duv02x, dp12.z, duv12x, dp02.z)) *
+               invdet;
+    }
+    if (degenerateUV || LengthSquared(Cross(dpdu, dpdv)) == 0) {
+        V3 ng = Cross(p2 - p0, p1 - p0);
+        CoordinateSystem(Normalize(ng), &dpdu, &dpdv);
+    }
+    s.p = b0 * p0 + b1 * p1 + b2 * p2;
+    V3 pAbsSum = Abs(b0 * p0) + Abs(b1 * p1) + Abs(b2 * p2);
+    s.pErr = gamma(7) * pAbsSum;
+    V3 n = Normalize(Cross(dp02, dp12));
+    if (flip) n = -n;
+    s.n = n;
+    s.dpdu = dpdu;
+    return s;
+}
+
+// ---------------------------------------------------------------- spectra
+// util/color.h:341 RGBSigmoidPolynomial; EvaluatePolynomial(l, c2, c1, c0) uses FMA.
+PHD float SigmoidPolynomial(float c0, float c1, float c2, float lambda) {
+    float x = fmaf(lambda, fmaf(lambda, c0, c1), c2);
+    if (std::isinf(x)) return x > 0 ? 1 : 0;
+    return .5f + x / (2 * std::sqrt(1 + Sqr(x)));
+}
+
+// util/spectrum.h:318 SampledWavelengths::SampleUniform (sequential adds, wrap)
+PHD void SampleWavelengthsUniform(float u, float lambda[kNSpectrumSamples]) {
+    lambda[0] = Lerpf(u, kLambdaMin, kLambdaMax);
+    const float delta = (kLambdaMax - kLambdaMin) / kNSpectrumSamples;
+    for (int i = 1; i < kNSpectrumSamples; ++i) {
+        lambda[i] = lambda[i - 1] + delta;
+        if (lambda[i] > kLambdaMax) lambda[i] = kLambdaMin + (lambda[i] - kLambdaMax);
+    }
+}
+// DenselySampledSpectrum offset (util/spectrum.h:420): lround(lambda) - 395, 311 entries
+PHD int DenseOffset(float lambda) {
+    long o = std::lround(lambda) - 395;
+    return (o < 0 || o > 310) ? -1 : (int)o;
+}
+// Average of 31 copies of x (SampledSpectrum::Average of a constant spectrum)
+PHD float Avg31(float x) {
+    float s = x;
+    for (int i = 1; i < kNSpectrumSamples; ++i) s += x;
+    return s / kNSpectrumSamples;
+}
+
+// ---------------------------------------------------------------- Halton
+// util/lowdiscrepancy.h ScrambledRadicalInverse with digit permutations, index < 2^32.
+// perm points at the permutation rows for this prime: perm[digit * base + value].
+PHD float ScrambledRadicalInverse(uint32_t base, uint32_t nDigits, uint64_t a, const uint16_t *perm) {
+    float invBase = (float)1 / (float)base, invBaseM = 1;
+    uint64_t reversedDigits = 0;
+    for (uint32_t digitIndex = 0; digitIndex < nDigits; ++digitIndex) {
+        uint64_t next = a / base;
+        int digitValue = (int)(a - next * base);
+        reversedDigits = reversedDigits * base + perm[digitIndex * base + digitValue];
+        invBaseM *= invBase;
+        a = next;
+    }
+    return std::fmin(invBaseM * (float)reversedDigits, kOneMinusEpsilon);
+}
+// util/lowdiscrepancy.h RadicalInverse (unscrambled), used for the pixel sample
+PHD float RadicalInverse(uint32_t base, uint64_t a) {
+    uint64_t limit = ~0ull / base - base;
+    float invBase = (float)1 / (float)base, invBaseM = 1;
+    uint64_t reversedDigits = 0;
+    while (a && reversedDigits < limit) {
+        uint64_t next = a / base;
+        uint64_t digit = a - next * base;
+        reversedDigits = reversedDigits * base + digit;
+        invBaseM *= invBase;
+        a = next;
+    }
+    return std::fmin((float)reversedDigits * invBaseM, kOneMinusEpsilon);
+}
+PHD uint64_t InverseRadicalInverse(uint64_t inverse, int base, int nDigits) {
+    uint64_t index = 0;
+    for (int i = 0; i < nDigits; ++i) {
+        uint64_t digit = inverse % base;
+        inverse /= base;
+        index = index * base + digit;
+    }
+    return index;
+}
+
+// ---------------------------------------------------------------- light BVH importance
+// lightsamplers.h:130 CompactLightBounds::Importance on host-decoded bounds.
+struct LightNodeBounds {
+    V3 pMin, pMax;  // decoded quantised bounds
+    V3 w;           // decoded octahedral direction
+    float phi, cosTheta_o, cosTheta_e;
+    int twoSided;
+};
+// util/vecmath.h:1817 BoundSubtendedDirections -> cosTheta
+PHD float BoundSubtendedCos(V3 pMin, V3 pMax, V3 p) {
+    V3 pCenter = (pMin + pMax) / 2;
+    bool inside = pCenter.x >= pMin.x && pCenter.x <= pMax.x && pCenter.y >= pMin.y &&
+                  pCenter.y <= pMax.y && pCenter.z >= pMin.z && pCenter.z <= pMax.z;
+    float radius = inside ? Distance(pCenter, pMax) : 0;
+    if (DistanceSquared(p, pCenter) < Sqr(radius)) return -1;
+    float sin2ThetaMax = Sqr(radius) / DistanceSquared(pCenter, p);
+    return SafeSqrt(1 - sin2ThetaMax);
+}
+PHD float CosSubClamped(float sinA, float cosA, float sinB, float cosB) {
+    if (cosA > cosB) return 1;
+    return cosA * cosB + sinA * sinB;
+}
+PHD float SinSubClamped(float sinA, float cosA, float sinB, float cosB) {
+    if (cosA > cosB) return 0;
+    return sinA * cosB - cosA * sinB;
+}
+PHD float LightImportance(const LightNodeBounds &lb, V3 p, V3 n) {
+    V3 pc = (lb.pMin + lb.pMax) / 2;
+    float d2 = DistanceSquared(p, pc);
+    d2 = std::fmax(d2, Length(lb.pMax - lb.pMin) / 2);
+    V3 wi = Normalize(p - pc);
+    float cosTheta_w = Dot(lb.w, wi);
+    if (lb.twoSided) cosTheta_w = std::fabs(cosTheta_w);
+    float sinTheta_w = SafeSqrt(1 - Sqr(cosTheta_w));
+    float cosTheta_b = BoundSubtendedCos(lb.pMin, lb.pMax, p);
+    float sinTheta_b = SafeSqrt(1 - Sqr(cosTheta_b));
+    float sinTheta_o = SafeSqrt(1 - Sqr(lb.cosTheta_o));
+    float cosTheta_x = CosSubClamped(sinTheta_w, cosTheta_w, sinTheta_o, lb.cosTheta_o);
+    float sinTheta_x = SinSubClamped(sinTheta_w, cosTheta_w, sinTheta_o, lb.cosTheta_o);
+    float cosThetap = CosSubClamped(sinTheta_x, cosTheta_x, sinTheta_b, cosTheta_b);
+    if (cosThetap <= lb.cosTheta_e) return 0;
+    float importance = lb.phi * cosThetap / d2;
+    if (n != V3(0, 0, 0)) {
+        float cosTheta_i = AbsDot(wi, n);
+        float sinTheta_i = SafeSqrt(1 - Sqr(cosTheta_i));
+        float cosThetap_i = CosSubClamped(sinTheta_i, cosTheta_i, sinTheta_b, cosTheta_b);
+        importance *= cosThetap_i;
+    }
+    importance = std::fmax(importance, 0.f);
+    return importance;
+}
+
+}  // namespace pbrt_amd

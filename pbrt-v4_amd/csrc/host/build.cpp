@@ -1,0 +1,444 @@
+// Scene finalisation: BVH light sampler construction (lightsamplers.cpp:112-236,
+// lights.cpp:803-822, lightsamplers.h:95-229) and Halton digit-permutation tables
+// (util/lowdiscrepancy.h:25-55, samplers.cpp:32-52).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <functional>
+
+#include "scene.h"
+
+namespace pbrt_amd {
+
+const std::vector<int> &Primes() {
+    // util/primes.cpp: the first 1000 primes
+    static std::vector<int> primes = [] {
+        std::vector<int> p;
+        for (int n = 2; (int)p.size() < 1000; ++n) {
+            bool isPrime = true;
+            for (int q : p) {
+                if (q * q > n) break;
+                if (n % q == 0) {
+                    isPrime = false;
+                    break;
+                }
+            }
+            if (isPrime) p.push_back(n);
+        }
+        return p;
+    }();
+    return primes;
+}
+
+uint64_t MurmurHash64A(const unsigned char *key, size_t len, uint64_t seed) {
+    const uint64_t m = 0xc6a4a7935bd1e995ull;
+    const int r = 47;
+    uint64_t h = seed ^ (len * m);
+    const unsigned char *end = key + 8 * (len / 8);
+    while (key != end) {
+        uint64_t k;
+        std::memcpy(&k, key, sizeof(uint64_t));
+        key += 8;
+        k *= m;
+        k ^= k >> r;
+        k *= m;
+        h ^= k;
+        h *= m;
+    }
+    switch (len & 7) {
+    case 7: h ^= uint64_t(key[6]) << 48; [[fallthrough]];
+    case 6: h ^= uint64_t(key[5]) << 40; [[fallthrough]];
+    case 5: h ^= uint64_t(key[4]) << 32; [[fallthrough]];
+    case 4: h ^= uint64_t(key[3]) << 24; [[fallthrough]];
+    case 3: h ^= uint64_t(key[2]) << 16; [[fallthrough]];
+    case 2: h ^= uint64_t(key[1]) << 8; [[fallthrough]];
+    case 1:
+        h ^= uint64_t(key[0]);
+        h *= m;
+    };
+    h ^= h >> r;
+    h *= m;
+    h ^= h >> r;
+    return h;
+}
+
+int PermutationElement(uint32_t i, uint32_t l, uint32_t p) {
+    uint32_t w = l - 1;
+    w |= w >> 1;
+    w |= w >> 2;
+    w |= w >> 4;
+    w |= w >> 8;
+    w |= w >> 16;
+    do {
+        i ^= p;
+        i *= 0xe170893d;
+        i ^= p >> 16;
+        i ^= (i & w) >> 4;
+        i ^= p >> 8;
+        i *= 0x0929eb3f;
+        i ^= p >> 23;
+        i ^= (i & w) >> 1;
+        i *= 1 | p >> 27;
+        i *= 0x6935fa69;
+        i ^= (i & w) >> 11;
+        i *= 0x74dcb303;
+        i ^= (i & w) >> 2;
+        i *= 0x9e501cc3;
+        i ^= (i & w) >> 2;
+        i *= 0xc860a3df;
+        i &= w;
+        i ^= i >> 5;
+    } while (i >= l);
+    return (i + p) % l;
+}
+
+static int NumDigits(int base) {
+    // DigitPermutation ctor digit count (float arithmetic, no contraction)
+    int nDigits = 0;
+    volatile float invBase = (float)1 / (float)base, invBaseM = 1;
+    while (1 - (float)(base - 1) * invBaseM < 1) {
+        ++nDigits;
+        invBaseM = invBaseM * invBase;
+    }
+    return nDigits;
+}
+
+static void BuildHalton(SceneDesc &s) {
+    int fullRes[2] = {s.xres, s.yres};
+    for (int i = 0; i < 2; ++i) {
+        int base = (i == 0) ? 2 : 3;
+        int scale = 1, exp = 0;
+        while (scale < std::min(fullRes[i], 128)) {
+            scale *= base;
+            ++exp;
+        }
+        s.haltonBaseScales[i] = scale;
+        s.haltonBaseExponents[i] = exp;
+    }
+    auto multInv = [](int64_t a, int64_t n) {
+        // extended Euclid (samplers.h multiplicativeInverse)
+        std::function<void(uint64_t, uint64_t, int64_t *, int64_t *)> egcd = [&](uint64_t a, uint64_t b, int64_t *x,
+                                                                                 int64_t *y) {
+            if (b == 0) {
+                *x = 1;
+                *y = 0;
+                return;
+            }
+            int64_t d = a / b, xp, yp;
+            egcd(b, a % b, &xp, &yp);
+            *x = yp;
+            *y = xp - (d * yp);
+        };
+        int64_t x, y;
+        egcd(a, n, &x, &y);
+        int64_t r = x % n;
+        return (int)(r < 0 ? r + n : r);
+    };
+    s.haltonMultInverse[0] = multInv(s.haltonBaseScales[1], s.haltonBaseScales[0]);
+    s.haltonMultInverse[1] = multInv(s.haltonBaseScales[0], s.haltonBaseScales[1]);
+
+    int maxDim = 7 * s.maxDepth + 6;  // 6 camera dims + 7 per bounce (wavefront/samples.cpp:39)
+    maxDim = std::min(maxDim, 999);
+    const std::vector<int> &primes = Primes();
+    s.permTable.clear();
+    s.permOffset.clear();
+    s.permNDigits.clear();
+    s.permBase.clear();
+    for (int dim = 0; dim <= maxDim; ++dim) {
+        int base = primes[dim];
+        int nDigits = NumDigits(base);
+        s.permOffset.push_back((uint32_t)s.permTable.size());
+        s.permNDigits.push_back(nDigits);
+        s.permBase.push_back(base);
+        for (int digitIndex = 0; digitIndex < nDigits; ++digitIndex) {
+            // Hash(base, digitIndex, seed): int, int, uint32_t packed = 12 bytes
+            unsigned char buf[16];
+            int b = base, di = digitIndex;
+            uint32_t seed = (uint32_t)s.seed;
+            std::memcpy(buf, &b, 4);
+            std::memcpy(buf + 4, &di, 4);
+            std::memcpy(buf + 8, &seed, 4);
+            uint64_t dseed = MurmurHash64A(buf, 12, 0);
+            for (int v = 0; v < base; ++v)
+                s.permTable.push_back((uint16_t)PermutationElement((uint32_t)v, (uint32_t)base, (uint32_t)dseed));
+        }
+    }
+}
+
+// ---------------------------------------------------------------- light BVH
+namespace {
+struct Bounds3 {
+    V3 pMin{kInfinity, kInfinity, kInfinity}, pMax{-kInfinity, -kInfinity, -kInfinity};
+    bool Valid() const { return pMin.x <= pMax.x; }
+    void Add(V3 p) {
+        pMin = V3(std::min(pMin.x, p.x), std::min(pMin.y, p.y), std::min(pMin.z, p.z));
+        pMax = V3(std::max(pMax.x, p.x), std::max(pMax.y, p.y), std::max(pMax.z, p.z));
+    }
+    void Add(const Bounds3 &b) {
+        if (!b.Valid()) return;
+        Add(b.pMin);
+        Add(b.pMax);
+    }
+    V3 Diagonal() const { return pMax - pMin; }
+    float SurfaceArea() const {
+        V3 d = Diagonal();
+        return 2 * (d.x * d.y + d.x * d.z + d.y * d.z);
+    }
+    V3 Offset(V3 p) const {
+        V3 o = p - pMin;
+        if (pMax.x > pMin.x) o.x /= pMax.x - pMin.x;
+        if (pMax.y > pMin.y) o.y /= pMax.y - pMin.y;
+        if (pMax.z > pMin.z) o.z /= pMax.z - pMin.z;
+        return o;
+    }
+};
+
+struct LightBounds {
+    Bounds3 bounds;
+    float phi = 0;
+    V3 w;
+    float cosTheta_o = 0, cosTheta_e = 0;
+    bool twoSided = false;
+    V3 Centroid() const { return (bounds.pMin + bounds.pMax) / 2; }
+};
+
+// util/transform.h Rotate(theta, axis) applied to a vector (float matrix)
+V3 RotateVector(float thetaDeg, V3 axis, V3 v) {
+    V3 a = Normalize(axis);
+    float theta = thetaDeg * (kPi / 180);
+    float sinTheta = std::sin(theta), cosTheta = std::cos(theta);
+    float m[3][3];
+    m[0][0] = a.x * a.x + (1 - a.x * a.x) * cosTheta;
+    m[0][1] = a.x * a.y * (1 - cosTheta) - a.z * sinTheta;
+    m[0][2] = a.x * a.z * (1 - cosTheta) + a.y * sinTheta;
+    m[1][0] = a.x * a.y * (1 - cosTheta) + a.z * sinTheta;
+    m[1][1] = a.y * a.y + (1 - a.y * a.y) * cosTheta;
+    m[1][2] = a.y * a.z * (1 - cosTheta) - a.x * sinTheta;
+    m[2][0] = a.x * a.z * (1 - cosTheta) - a.y * sinTheta;
+    m[2][1] = a.y * a.z * (1 - cosTheta) + a.x * sinTheta;
+    m[2][2] = a.z * a.z + (1 - a.z * a.z) * cosTheta;
+    return V3(m[0][0] * v.x + m[0][1] * v.y + m[0][2] * v.z, m[1][0] * v.x + m[1][1] * v.y + m[1][2] * v.z,
+              m[2][0] * v.x + m[2][1] * v.y + m[2][2] * v.z);
+}
+
+// util/vecmath.cpp:57 Union(DirectionCone, DirectionCone)
+void ConeUnion(V3 aw, float aCos, V3 bw, float bCos, V3 *w, float *cosTheta) {
+    float theta_a = SafeACos(aCos), theta_b = SafeACos(bCos);
+    float theta_d = AngleBetween(aw, bw);
+    if (std::min(theta_d + theta_b, kPi) <= theta_a) {
+        *w = aw;
+        *cosTheta = aCos;
+        return;
+    }
+    if (std::min(theta_d + theta_a, kPi) <= theta_b) {
+        *w = bw;
+        *cosTheta = bCos;
+        return;
+    }
+    float theta_o = (theta_a + theta_d + theta_b) / 2;
+    if (theta_o >= kPi) {
+        *w = V3(0, 0, 1);
+        *cosTheta = -1;
+        return;
+    }
+    float theta_r = theta_o - theta_a;
+    V3 wr = Cross(aw, bw);
+    if (LengthSquared(wr) == 0) {
+        *w = V3(0, 0, 1);
+        *cosTheta = -1;
+        return;
+    }
+    *w = RotateVector(theta_r * (180 / kPi), wr, aw);
+    *cosTheta = std::cos(theta_o);
+}
+
+LightBounds Union(const LightBounds &a, const LightBounds &b) {
+    if (a.phi == 0) return b;
+    if (b.phi == 0) return a;
+    LightBounds r;
+    V3 w;
+    float cosTheta;
+    ConeUnion(a.w, a.cosTheta_o, b.w, b.cosTheta_o, &w, &cosTheta);
+    r.bounds = a.bounds;
+    r.bounds.Add(b.bounds);
+    r.w = Normalize(w);
+    r.phi = a.phi + b.phi;
+    r.cosTheta_o = cosTheta;
+    r.cosTheta_e = std::min(a.cosTheta_e, b.cosTheta_e);
+    r.twoSided = a.twoSided | b.twoSided;
+    return r;
+}
+
+float EvaluateCost(const LightBounds &b, const Bounds3 &bounds, int dim) {
+    float theta_o = std::acos(b.cosTheta_o), theta_e = std::acos(b.cosTheta_e);
+    float theta_w = std::min(theta_o + theta_e, kPi);
+    float sinTheta_o = SafeSqrt(1 - Sqr(b.cosTheta_o));
+    float M_omega = 2 * kPi * (1 - b.cosTheta_o) +
+                    kPi / 2 * (2 * theta_w * sinTheta_o - std::cos(theta_o - 2 * theta_w) - 2 * theta_o * sinTheta_o + b.cosTheta_o);
+    V3 d = bounds.Diagonal();
+    float Kr = MaxComponentValue(d) / d[dim];
+    return b.phi * M_omega * Kr * b.bounds.SurfaceArea();
+}
+
+// util/vecmath.h:1735 OctahedralVector encode/decode round trip
+V3 OctahedralRoundTrip(V3 v) {
+    auto sign = [](float x) { return std::copysign(1.f, x); };
+    auto encode = [](float f) { return (uint16_t)std::round(Clampf((f + 1) / 2, 0, 1) * 65535.f); };
+    v = v / (std::fabs(v.x) + std::fabs(v.y) + std::fabs(v.z));
+    uint16_t x, y;
+    if (v.z >= 0) {
+        x = encode(v.x);
+        y = encode(v.y);
+    } else {
+        x = encode((1 - std::fabs(v.y)) * sign(v.x));
+        y = encode((1 - std::fabs(v.x)) * sign(v.y));
+    }
+    V3 r;
+    r.x = -1 + 2 * (x / 65535.f);
+    r.y = -1 + 2 * (y / 65535.f);
+    r.z = 1 - (std::fabs(r.x) + std::fabs(r.y));
+    if (r.z < 0) {
+        float xo = r.x;
+        r.x = (1 - std::fabs(r.y)) * sign(xo);
+        r.y = (1 - std::fabs(xo)) * sign(r.y);
+    }
+    return Normalize(r);
+}
+
+LightNodeBounds Compact(const LightBounds &lb, const Bounds3 &allb) {
+    // CompactLightBounds ctor + decode (lightsamplers.h:95-180)
+    LightNodeBounds c;
+    c.w = OctahedralRoundTrip(Normalize(lb.w));
+    c.phi = lb.phi;
+    auto qcos = [](float v) { return (unsigned)std::floor(32767.f * ((v + 1) / 2)); };
+    unsigned qo = qcos(lb.cosTheta_o), qe = qcos(lb.cosTheta_e);
+    c.cosTheta_o = 2 * (qo / 32767.f) - 1;
+    c.cosTheta_e = 2 * (qe / 32767.f) - 1;
+    c.twoSided = lb.twoSided;
+    auto qb = [](float v, float mn, float mx) {
+        if (mn == mx) return 0.f;
+        return 65535.f * Clampf((v - mn) / (mx - mn), 0, 1);
+    };
+    uint16_t q[2][3];
+    for (int k = 0; k < 3; ++k) {
+        q[0][k] = (uint16_t)std::floor(qb(lb.bounds.pMin[k], allb.pMin[k], allb.pMax[k]));
+        q[1][k] = (uint16_t)std::ceil(qb(lb.bounds.pMax[k], allb.pMin[k], allb.pMax[k]));
+    }
+    for (int k = 0; k < 3; ++k) {
+        c.pMin[k] = Lerpf(q[0][k] / 65535.f, allb.pMin[k], allb.pMax[k]);
+        c.pMax[k] = Lerpf(q[1][k] / 65535.f, allb.pMin[k], allb.pMax[k]);
+    }
+    return c;
+}
+
+struct LightBVHBuilder {
+    SceneDesc &s;
+    Bounds3 allLightBounds;
+    std::pair<int, LightBounds> Build(std::vector<std::pair<int, LightBounds>> &bvhLights, int start, int end,
+                                      uint32_t bitTrail, int depth) {
+        if (end - start == 1) {
+            int nodeIndex = (int)s.lightNodes.size();
+            LightBVHNodeDesc n;
+            n.bounds = Compact(bvhLights[start].second, allLightBounds);
+            n.childOrLight = bvhLights[start].first;
+            n.isLeaf = 1;
+            s.lightNodes.push_back(n);
+            s.lightBitTrail[bvhLights[start].first] = bitTrail;
+            return {nodeIndex, bvhLights[start].second};
+        }
+        Bounds3 bounds, centroidBounds;
+        for (int i = start; i < end; ++i) {
+            bounds.Add(bvhLights[i].second.bounds);
+            centroidBounds.Add(bvhLights[i].second.Centroid());
+        }
+        float minCost = kInfinity;
+        int minCostSplitBucket = -1, minCostSplitDim = -1;
+        constexpr int nBuckets = 12;
+        for (int dim = 0; dim < 3; ++dim) {
+            if (centroidBounds.pMax[dim] == centroidBounds.pMin[dim]) continue;
+            LightBounds bucketLightBounds[nBuckets];
+            for (int i = start; i < end; ++i) {
+                V3 pc = bvhLights[i].second.Centroid();
+                int b = (int)(nBuckets * centroidBounds.Offset(pc)[dim]);
+                if (b == nBuckets) b = nBuckets - 1;
+                bucketLightBounds[b] = Union(bucketLightBounds[b], bvhLights[i].second);
+            }
+            float cost[nBuckets - 1];
+            for (int i = 0; i < nBuckets - 1; ++i) {
+                LightBounds b0, b1;
+                for (int j = 0; j <= i; ++j) b0 = Union(b0, bucketLightBounds[j]);
+                for (int j = i + 1; j < nBuckets; ++j) b1 = Union(b1, bucketLightBounds[j]);
+                cost[i] = EvaluateCost(b0, bounds, dim) + EvaluateCost(b1, bounds, dim);
+            }
+            for (int i = 1; i < nBuckets - 1; ++i) {
+                if (cost[i] > 0 && cost[i] < minCost) {
+                    minCost = cost[i];
+                    minCostSplitBucket = i;
+                    minCostSplitDim = dim;
+                }
+            }
+        }
+        int mid;
+        if (minCostSplitDim == -1)
+            mid = (start + end) / 2;
+        else {
+            auto *pmid = std::partition(&bvhLights[start], &bvhLights[end - 1] + 1, [&](const std::pair<int, LightBounds> &l) {
+                int b = (int)(nBuckets * centroidBounds.Offset(l.second.Centroid())[minCostSplitDim]);
+                if (b == nBuckets) b = nBuckets - 1;
+                return b <= minCostSplitBucket;
+            });
+            mid = (int)(pmid - &bvhLights[0]);
+            if (mid == start || mid == end) mid = (start + end) / 2;
+        }
+        int nodeIndex = (int)s.lightNodes.size();
+        s.lightNodes.push_back(LightBVHNodeDesc());
+        std::pair<int, LightBounds> child0 = Build(bvhLights, start, mid, bitTrail, depth + 1);
+        std::pair<int, LightBounds> child1 = Build(bvhLights, mid, end, bitTrail | (1u << depth), depth + 1);
+        LightBounds lb = Union(child0.second, child1.second);
+        s.lightNodes[nodeIndex].bounds = Compact(lb, allLightBounds);
+        s.lightNodes[nodeIndex].childOrLight = child1.first;
+        s.lightNodes[nodeIndex].isLeaf = 0;
+        return {nodeIndex, lb};
+    }
+};
+}  // namespace
+
+static void BuildLightBVH(SceneDesc &s) {
+    s.lightNodes.clear();
+    s.lightBitTrail.assign(s.areaLights.size(), 0);
+    if (s.uniformLightSampler) return;
+    LightBVHBuilder b{s, Bounds3()};
+    std::vector<std::pair<int, LightBounds>> bvhLights;
+    for (size_t i = 0; i < s.areaLights.size(); ++i) {
+        const AreaLightDesc &al = s.areaLights[i];
+        const auto &tri = s.tris[al.prim];
+        V3 p0 = s.verts[tri[0]], p1 = s.verts[tri[1]], p2 = s.verts[tri[2]];
+        const auto &dense = s.denseSpectra[al.spectrum];
+        float mx = *std::max_element(dense.begin(), dense.end());
+        float phi = mx;
+        phi *= al.scale * al.area * kPi;
+        V3 n = Normalize(Cross(p1 - p0, p2 - p0));
+        if (s.triFlip[al.prim]) n = n * -1.f;
+        LightBounds lb;
+        lb.bounds.Add(p0);
+        lb.bounds.Add(p1);
+        lb.bounds.Add(p2);
+        lb.w = Normalize(n);
+        lb.phi = phi;
+        lb.cosTheta_o = 1;
+        lb.cosTheta_e = std::cos(kPi / 2);
+        lb.twoSided = al.twoSided;
+        if (lb.phi > 0) {
+            bvhLights.push_back({(int)i, lb});
+            b.allLightBounds.Add(lb.bounds);
+        }
+    }
+    if (!bvhLights.empty()) b.Build(bvhLights, 0, (int)bvhLights.size(), 0, 0);
+}
+
+void FinalizeScene(SceneDesc &s) {
+    BuildLightBVH(s);
+    BuildHalton(s);
+}
+
+}  // namespace pbrt_amd

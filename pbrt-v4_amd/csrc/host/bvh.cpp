@@ -1,0 +1,261 @@
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <stdexcept>
+
+#include "bvh.h"
+
+namespace pbrt_amd {
+
+namespace {
+struct Box {
+    V3 mn{kInfinity, kInfinity, kInfinity}, mx{-kInfinity, -kInfinity, -kInfinity};
+    void Add(V3 p) {
+        mn = V3(std::min(mn.x, p.x), std::min(mn.y, p.y), std::min(mn.z, p.z));
+        mx = V3(std::max(mx.x, p.x), std::max(mx.y, p.y), std::max(mx.z, p.z));
+    }
+    void Add(const Box &b) {
+        mn = V3(std::min(mn.x, b.mn.x), std::min(mn.y, b.mn.y), std::min(mn.z, b.mn.z));
+        mx = V3(std::max(mx.x, b.mx.x), std::max(mx.y, b.mx.y), std::max(mx.z, b.mx.z));
+    }
+    bool Empty() const { return mn.x > mx.x; }
+    float Area() const {
+        if (Empty()) return 0;
+        V3 d = mx - mn;
+        return 2 * (d.x * d.y + d.x * d.z + d.y * d.z);
+    }
+};
+
+struct Prim {
+    Box box;
+    V3 centroid;
+    int index;
+};
+
+struct Node2 {
+    Box box;
+    int left = -1, right = -1;   // interior
+    int first = 0, count = 0;    // leaf (into ordered prims)
+    bool leaf() const { return left < 0; }
+};
+
+struct Builder2 {
+    std::vector<Prim> &prims;
+    std::vector<Node2> nodes;
+    int maxLeaf;
+
+    int Build(int start, int end) {
+        Node2 node;
+        for (int i = start; i < end; ++i) node.box.Add(prims[i].box);
+        int idx = (int)nodes.size();
+        nodes.push_back(node);
+        int n = end - start;
+        auto makeLeaf = [&]() {
+            nodes[idx].first = start;
+            nodes[idx].count = n;
+            return idx;
+        };
+        if (n == 1) return makeLeaf();
+        Box cb;
+        for (int i = start; i < end; ++i) cb.Add(prims[i].centroid);
+        V3 d = cb.mx - cb.mn;
+        int dim = (d.x > d.y) ? ((d.x > d.z) ? 0 : 2) : ((d.y > d.z) ? 1 : 2);
+        if (cb.mx[dim] == cb.mn[dim]) {
+            if (n <= maxLeaf) return makeLeaf();
+            int mid = (start + end) / 2;  // all centroids coincide: split the list
+            nodes[idx].left = Build(start, mid);
+            nodes[idx].right = Build(mid, end);
+            return idx;
+        }
+        int mid;
+        if (n <= 2) {
+            mid = (start + end) / 2;
+            std::nth_element(&prims[start], &prims[mid], &prims[end - 1] + 1,
+                             [dim](const Prim &a, const Prim &b) { return a.centroid[dim] < b.centroid[dim]; });
+        } else {
+            constexpr int nBuckets = 12;
+            int counts[nBuckets] = {0};
+            Box bbox[nBuckets];
+            auto bucketOf = [&](const Prim &p) {
+                int b = (int)(nBuckets * ((p.centroid[dim] - cb.mn[dim]) / (cb.mx[dim] - cb.mn[dim])));
+                return std::min(std::max(b, 0), nBuckets - 1);
+            };
+            for (int i = start; i < end; ++i) {
+                int b = bucketOf(prims[i]);
+                counts[b]++;
+                bbox[b].Add(prims[i].box);
+            }
+            float costs[nBuckets - 1] = {};
+            int countBelow = 0;
+            Box boundBelow;
+            for (int i = 0; i < nBuckets - 1; ++i) {
+                boundBelow.Add(bbox[i]);
+                countBelow += counts[i];
+                costs[i] += countBelow * boundBelow.Area();
+            }
+            int countAbove = 0;
+            Box boundAbove;
+            for (int i = nBuckets - 1; i >= 1; --i) {
+                boundAbove.Add(bbox[i]);
+                countAbove += counts[i];
+                costs[i - 1] += countAbove * boundAbove.Area();
+            }
+            int minBucket = -1;
+            float minCost = kInfinity;
+            for (int i = 0; i < nBuckets - 1; ++i)
+                if (costs[i] < minCost) {
+                    minCost = costs[i];
+                    minBucket = i;
+                }
+            float leafCost = (float)n;
+            minCost = 1.f / 2.f + minCost / node.box.Area();
+            if (n > maxLeaf || minCost < leafCost) {
+                Prim *pm = std::partition(&prims[start], &prims[end - 1] + 1,
+                                          [&](const Prim &p) { return bucketOf(p) <= minBucket; });
+                mid = (int)(pm - &prims[0]);
+                if (mid == start || mid == end) {
+                    mid = (start + end) / 2;
+                    std::nth_element(&prims[start], &prims[mid], &prims[end - 1] + 1,
+                                     [dim](const Prim &a, const Prim &b) { return a.centroid[dim] < b.centroid[dim]; });
+                }
+            } else {
+                return makeLeaf();
+            }
+        }
+        int l = Build(start, mid);
+        int r = Build(mid, end);
+        nodes[idx].left = l;
+        nodes[idx].right = r;
+        return idx;
+    }
+};
+}  // namespace
+
+BVH8 BuildBVH8(const std::vector<V3> &verts, const std::vector<std::array<int, 3>> &tris, int maxLeafPrims) {
+    BVH8 out;
+    std::vector<Prim> prims;
+    prims.reserve(tris.size());
+    Box all;
+    for (size_t i = 0; i < tris.size(); ++i) {
+        Prim p;
+        p.box.Add(verts[tris[i][0]]);
+        p.box.Add(verts[tris[i][1]]);
+        p.box.Add(verts[tris[i][2]]);
+        p.centroid = (p.box.mn + p.box.mx) * 0.5f;
+        p.index = (int)i;
+        all.Add(p.box);
+        prims.push_back(p);
+    }
+    out.boundsMin = all.mn;
+    out.boundsMax = all.mx;
+    if (prims.empty()) {
+        BVH8Node root{};
+        for (int c = 0; c < 8; ++c) {
+            root.lox[c] = root.loy[c] = root.loz[c] = 1;
+            root.hix[c] = root.hiy[c] = root.hiz[c] = -1;
+            root.child[c] = kEmptyChild;
+        }
+        out.nodes.push_back(root);
+        return out;
+    }
+    maxLeafPrims = std::min(std::max(maxLeafPrims, 1), 8);
+    Builder2 b{prims, {}, maxLeafPrims};
+    b.nodes.reserve(2 * prims.size());
+    b.Build(0, (int)prims.size());
+
+    // ordered triangles follow the BVH2 leaf order (prims array order)
+    out.triPrim.resize(prims.size());
+    out.triVerts.resize(prims.size() * 12);
+    for (size_t i = 0; i < prims.size(); ++i) {
+        int t = prims[i].index;
+        out.triPrim[i] = t;
+        for (int k = 0; k < 3; ++k) {
+            V3 p = verts[tris[t][k]];
+            out.triVerts[i * 12 + k * 4 + 0] = p.x;
+            out.triVerts[i * 12 + k * 4 + 1] = p.y;
+            out.triVerts[i * 12 + k * 4 + 2] = p.z;
+            float w = 0;
+            if (k == 0) {
+                int32_t tt = t;
+                memcpy(&w, &tt, 4);
+            }
+            out.triVerts[i * 12 + k * 4 + 3] = w;
+        }
+    }
+
+    // collapse BVH2 -> BVH8 (greedy: open the child with the largest surface area)
+    struct Work {
+        int node2, depth;
+    };
+    std::vector<Work> queue;
+    queue.push_back({0, 1});
+    out.nodes.reserve(prims.size() / 2 + 1);
+    std::vector<int> node8Of;  // per queue entry the BVH8 index
+    size_t head = 0;
+    out.nodes.push_back(BVH8Node{});
+    node8Of.push_back(0);
+    while (head < queue.size()) {
+        Work w = queue[head];
+        int self = node8Of[head];
+        ++head;
+        out.maxDepth = std::max(out.maxDepth, w.depth);
+        std::vector<int> kids;
+        const Node2 &n2 = b.nodes[w.node2];
+        if (n2.leaf())
+            kids.push_back(w.node2);
+        else {
+            kids.push_back(n2.left);
+            kids.push_back(n2.right);
+        }
+        while ((int)kids.size() < 8) {
+            int best = -1;
+            float bestArea = -1;
+            for (size_t k = 0; k < kids.size(); ++k) {
+                const Node2 &c = b.nodes[kids[k]];
+                if (!c.leaf() && c.box.Area() > bestArea) {
+                    bestArea = c.box.Area();
+                    best = (int)k;
+                }
+            }
+            if (best < 0) break;
+            int open = kids[best];
+            kids.erase(kids.begin() + best);
+            kids.push_back(b.nodes[open].left);
+            kids.push_back(b.nodes[open].right);
+        }
+        BVH8Node node{};
+        node.nChildren = (int)kids.size();
+        for (int c = 0; c < 8; ++c) {
+            if (c < (int)kids.size()) {
+                const Node2 &k = b.nodes[kids[c]];
+                node.lox[c] = k.box.mn.x;
+                node.loy[c] = k.box.mn.y;
+                node.loz[c] = k.box.mn.z;
+                node.hix[c] = k.box.mx.x;
+                node.hiy[c] = k.box.mx.y;
+                node.hiz[c] = k.box.mx.z;
+                if (k.leaf()) {
+                    if (k.count > 8) throw std::runtime_error("BVH leaf larger than 8 triangles");
+                    node.child[c] = ~((k.first << 3) | (k.count - 1));
+                } else {
+                    int idx8 = (int)out.nodes.size() + (int)(queue.size() - head);
+                    // index assigned in BFS order: position in queue
+                    node.child[c] = (int)queue.size();
+                    queue.push_back({kids[c], w.depth + 1});
+                    node8Of.push_back((int)queue.size() - 1);
+                    (void)idx8;
+                }
+            } else {
+                node.lox[c] = node.loy[c] = node.loz[c] = 1;
+                node.hix[c] = node.hiy[c] = node.hiz[c] = -1;
+                node.child[c] = kEmptyChild;
+            }
+        }
+        if ((int)out.nodes.size() <= self) out.nodes.resize(self + 1);
+        out.nodes[self] = node;
+    }
+    out.nodes.resize(queue.size());
+    return out;
+}
+
+}  // namespace pbrt_amd

@@ -1,0 +1,840 @@
+// .pbrt scene-description subset loader (the drop-in boundary on the scene side).
+// Mirrors the directive semantics of the reference parser and BasicSceneBuilder
+// (parser.cpp, scene.cpp:92-98 fork defaults, scene.cpp CreateAggregate/CreateLights)
+// for the statements the wavefront hot path needs; anything else fails loudly with the
+// file location, as pbrt's ErrorExit does.
+#include <algorithm>
+#include <cctype>
+#include <cmath>
+#include <fstream>
+#include <functional>
+#include <memory>
+#include <set>
+#include <sstream>
+
+#include "scene.h"
+
+namespace pbrt_amd {
+
+// ------------------------------------------------------------------ matrices (double)
+Mat4 Identity4() {
+    Mat4 m{};
+    for (int i = 0; i < 4; ++i) m[i][i] = 1;
+    return m;
+}
+Mat4 Mul(const Mat4 &a, const Mat4 &b) {
+    Mat4 r{};
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            double s = 0;
+            for (int k = 0; k < 4; ++k) s += a[i][k] * b[k][j];
+            r[i][j] = s;
+        }
+    return r;
+}
+Mat4 Inverse4(const Mat4 &m) {
+    // Gauss-Jordan with full pivoting (util/math.cpp InvertOrExit semantics)
+    int indxc[4], indxr[4], ipiv[4] = {0, 0, 0, 0};
+    Mat4 minv = m;
+    for (int i = 0; i < 4; i++) {
+        int irow = 0, icol = 0;
+        double big = 0.;
+        for (int j = 0; j < 4; j++) {
+            if (ipiv[j] != 1) {
+                for (int k = 0; k < 4; k++) {
+                    if (ipiv[k] == 0) {
+                        if (std::fabs(minv[j][k]) >= big) {
+                            big = std::fabs(minv[j][k]);
+                            irow = j;
+                            icol = k;
+                        }
+                    } else if (ipiv[k] > 1)
+                        throw Error("singular matrix");
+                }
+            }
+        }
+        ++ipiv[icol];
+        if (irow != icol)
+            for (int k = 0; k < 4; ++k) std::swap(minv[irow][k], minv[icol][k]);
+        indxr[i] = irow;
+        indxc[i] = icol;
+        if (minv[icol][icol] == 0.) throw Error("singular matrix");
+        double pivinv = 1. / minv[icol][icol];
+        minv[icol][icol] = 1.;
+        for (int j = 0; j < 4; j++) minv[icol][j] *= pivinv;
+        for (int j = 0; j < 4; j++) {
+            if (j != icol) {
+                double save = minv[j][icol];
+                minv[j][icol] = 0;
+                for (int k = 0; k < 4; k++) minv[j][k] -= minv[icol][k] * save;
+            }
+        }
+    }
+    for (int j = 3; j >= 0; j--) {
+        if (indxr[j] != indxc[j]) {
+            for (int k = 0; k < 4; k++) std::swap(minv[k][indxr[j]], minv[k][indxc[j]]);
+        }
+    }
+    return minv;
+}
+V3 XformPoint(const Mat4 &m, V3 p) {
+    double x = p.x, y = p.y, z = p.z;
+    double xp = m[0][0] * x + m[0][1] * y + m[0][2] * z + m[0][3];
+    double yp = m[1][0] * x + m[1][1] * y + m[1][2] * z + m[1][3];
+    double zp = m[2][0] * x + m[2][1] * y + m[2][2] * z + m[2][3];
+    double wp = m[3][0] * x + m[3][1] * y + m[3][2] * z + m[3][3];
+    if (wp == 1) return V3((float)xp, (float)yp, (float)zp);
+    return V3((float)(xp / wp), (float)(yp / wp), (float)(zp / wp));
+}
+V3 XformVector(const Mat4 &m, V3 v) {
+    double x = v.x, y = v.y, z = v.z;
+    return V3((float)(m[0][0] * x + m[0][1] * y + m[0][2] * z), (float)(m[1][0] * x + m[1][1] * y + m[1][2] * z),
+              (float)(m[2][0] * x + m[2][1] * y + m[2][2] * z));
+}
+V3 XformNormal(const Mat4 &mi, V3 n) {
+    double x = n.x, y = n.y, z = n.z;
+    return V3((float)(mi[0][0] * x + mi[1][0] * y + mi[2][0] * z), (float)(mi[0][1] * x + mi[1][1] * y + mi[2][1] * z),
+              (float)(mi[0][2] * x + mi[1][2] * y + mi[2][2] * z));
+}
+bool SwapsHandedness(const Mat4 &m) {
+    double det = m[0][0] * (m[1][1] * m[2][2] - m[1][2] * m[2][1]) -
+                 m[0][1] * (m[1][0] * m[2][2] - m[1][2] * m[2][0]) +
+                 m[0][2] * (m[1][0] * m[2][1] - m[1][1] * m[2][0]);
+    return det < 0;
+}
+static Mat4 TranslateM(double x, double y, double z) {
+    Mat4 m = Identity4();
+    m[0][3] = x;
+    m[1][3] = y;
+    m[2][3] = z;
+    return m;
+}
+static Mat4 ScaleM(double x, double y, double z) {
+    Mat4 m = Identity4();
+    m[0][0] = x;
+    m[1][1] = y;
+    m[2][2] = z;
+    return m;
+}
+static Mat4 RotateM(double theta, double ax, double ay, double az) {
+    // util/transform.h Rotate(theta, axis)
+    double len = std::sqrt(ax * ax + ay * ay + az * az);
+    ax /= len;
+    ay /= len;
+    az /= len;
+    double s = std::sin(theta * M_PI / 180.0), c = std::cos(theta * M_PI / 180.0);
+    Mat4 m = Identity4();
+    m[0][0] = ax * ax + (1 - ax * ax) * c;
+    m[0][1] = ax * ay * (1 - c) - az * s;
+    m[0][2] = ax * az * (1 - c) + ay * s;
+    m[1][0] = ax * ay * (1 - c) + az * s;
+    m[1][1] = ay * ay + (1 - ay * ay) * c;
+    m[1][2] = ay * az * (1 - c) - ax * s;
+    m[2][0] = ax * az * (1 - c) - ay * s;
+    m[2][1] = ay * az * (1 - c) + ax * s;
+    m[2][2] = az * az + (1 - az * az) * c;
+    return m;
+}
+static Mat4 LookAtM(V3 pos, V3 look, V3 up) {
+    // util/transform.cpp:81-117: cameraFromWorld = Inverse(worldFromCamera)
+    auto nrm = [](double v[3]) {
+        double l = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+        v[0] /= l;
+        v[1] /= l;
+        v[2] /= l;
+    };
+    auto cross = [](const double a[3], const double b[3], double r[3]) {
+        r[0] = a[1] * b[2] - a[2] * b[1];
+        r[1] = a[2] * b[0] - a[0] * b[2];
+        r[2] = a[0] * b[1] - a[1] * b[0];
+    };
+    double dir[3] = {(double)look.x - pos.x, (double)look.y - pos.y, (double)look.z - pos.z};
+    nrm(dir);
+    double u[3] = {up.x, up.y, up.z};
+    nrm(u);
+    double right[3];
+    cross(u, dir, right);
+    double rl = std::sqrt(right[0] * right[0] + right[1] * right[1] + right[2] * right[2]);
+    if (rl == 0) throw Error("LookAt: up vector and viewing direction are parallel");
+    nrm(right);
+    double newUp[3];
+    cross(dir, right, newUp);
+    Mat4 w = Identity4();
+    for (int i = 0; i < 3; ++i) {
+        w[i][0] = right[i];
+        w[i][1] = newUp[i];
+        w[i][2] = dir[i];
+    }
+    w[0][3] = pos.x;
+    w[1][3] = pos.y;
+    w[2][3] = pos.z;
+    return Inverse4(w);
+}
+static Mat4 PerspectiveM(double fov, double n, double f) {
+    Mat4 persp{};
+    persp[0][0] = 1;
+    persp[1][1] = 1;
+    persp[2][2] = f / (f - n);
+    persp[2][3] = -f * n / (f - n);
+    persp[3][2] = 1;
+    double invTanAng = 1 / std::tan(fov * M_PI / 180.0 / 2);
+    return Mul(ScaleM(invTanAng, invTanAng, 1), persp);
+}
+
+// ------------------------------------------------------------------ tokenizer
+struct Token {
+    std::string text;
+    bool isString = false;
+    std::string file;
+    int line = 0;
+};
+
+static std::vector<Token> Tokenize(const std::string &src, const std::string &file) {
+    std::vector<Token> toks;
+    size_t i = 0, n = src.size();
+    int line = 1;
+    while (i < n) {
+        char c = src[i];
+        if (c == '\n') {
+            ++line;
+            ++i;
+        } else if (std::isspace((unsigned char)c)) {
+            ++i;
+        } else if (c == '#') {
+            while (i < n && src[i] != '\n') ++i;
+        } else if (c == '"') {
+            size_t j = i + 1;
+            std::string s;
+            while (j < n && src[j] != '"') {
+                if (src[j] == '\n') throw Error(file + ":" + std::to_string(line) + ": unterminated string");
+                if (src[j] == '\\' && j + 1 < n) {
+                    ++j;
+                    char e = src[j];
+                    s += (e == 'n') ? '\n' : (e == 't') ? '\t' : e;
+                } else
+                    s += src[j];
+                ++j;
+            }
+            toks.push_back({s, true, file, line});
+            i = j + 1;
+        } else if (c == '[' || c == ']') {
+            toks.push_back({std::string(1, c), false, file, line});
+            ++i;
+        } else {
+            size_t j = i;
+            while (j < n && !std::isspace((unsigned char)src[j]) && src[j] != '"' && src[j] != '[' &&
+                   src[j] != ']' && src[j] != '#')
+                ++j;
+            toks.push_back({src.substr(i, j - i), false, file, line});
+            i = j;
+        }
+    }
+    return toks;
+}
+
+// ------------------------------------------------------------------ parameters
+struct Param {
+    std::string type, name;
+    std::vector<double> nums;
+    std::vector<std::string> strs;
+    std::vector<bool> bools;
+    bool used = false;
+};
+struct ParamSet {
+    std::vector<Param> params;
+    std::string loc;
+    Param *Find(const std::string &name, const std::string &type = "") {
+        for (auto &p : params)
+            if (p.name == name && (type.empty() || p.type == type)) {
+                p.used = true;
+                return &p;
+            }
+        return nullptr;
+    }
+    double GetFloat(const std::string &name, double def) {
+        Param *p = Find(name, "float");
+        return (p && !p->nums.empty()) ? p->nums[0] : def;
+    }
+    int GetInt(const std::string &name, int def) {
+        Param *p = Find(name, "integer");
+        return (p && !p->nums.empty()) ? (int)p->nums[0] : def;
+    }
+    bool GetBool(const std::string &name, bool def) {
+        Param *p = Find(name, "bool");
+        return (p && !p->bools.empty()) ? (bool)p->bools[0] : def;
+    }
+    std::string GetString(const std::string &name, const std::string &def) {
+        Param *p = Find(name, "string");
+        return (p && !p->strs.empty()) ? p->strs[0] : def;
+    }
+    void CheckUnused() const {
+        for (auto &p : params)
+            if (!p.used) throw Error(loc + ": parameter \"" + p.type + " " + p.name + "\" is not supported");
+    }
+};
+
+struct GraphicsState {
+    Mat4 ctm = Identity4();
+    bool reverseOrientation = false;
+    int material = -1;  // index into materials (-1 -> default diffuse)
+    std::string areaLightName;
+    ParamSet areaLightParams;
+};
+
+class Parser {
+  public:
+    Parser(SceneDesc &s, const std::map<std::string, std::string> &ov) : scene(s), overrides(ov) {}
+
+    void ParseFile(const std::string &path) {
+        std::ifstream in(path);
+        if (!in) throw Error("cannot open scene file " + path);
+        std::stringstream ss;
+        ss << in.rdbuf();
+        std::string dir = path.substr(0, path.find_last_of('/') == std::string::npos ? 0 : path.find_last_of('/'));
+        ParseString(ss.str(), path, dir);
+    }
+
+    void ParseString(const std::string &text, const std::string &file, const std::string &dir) {
+        std::vector<Token> toks = Tokenize(text, file);
+        size_t pos = 0;
+        while (pos < toks.size()) Directive(toks, pos, dir);
+    }
+
+    void Finish();
+
+  private:
+    SceneDesc &scene;
+    std::map<std::string, std::string> overrides;
+    GraphicsState gs;
+    std::vector<GraphicsState> stack;
+    std::map<std::string, int> namedMaterials;
+    std::map<std::string, Mat4> namedCoordSys;
+    bool haveCamera = false;
+    Mat4 cameraFromWorld = Identity4();
+    ParamSet cameraParams, filmParams, samplerParams, integratorParams, filterParams;
+    std::string cameraType = "perspective", filmType = "rgb";
+    bool inWorld = false;
+    struct PendingShape {
+        std::vector<V3> P;
+        std::vector<int> idx;
+        std::vector<float> uv;  // per vertex, 2 floats
+        Mat4 renderFromObject;
+        bool flip;
+        int material;
+        std::string areaLight;
+        ParamSet areaParams;
+        std::string loc;
+    };
+    std::vector<PendingShape> shapes;
+    struct PendingLight {
+        std::string type;
+        ParamSet params;
+        Mat4 worldFromLight;
+    };
+    std::vector<PendingLight> lights;
+
+    static std::string Loc(const Token &t) { return t.file + ":" + std::to_string(t.line); }
+
+    double Num(const std::vector<Token> &toks, size_t &pos) {
+        if (pos >= toks.size()) throw Error("unexpected end of file");
+        const Token &t = toks[pos++];
+        char *end = nullptr;
+        double v = std::strtod(t.text.c_str(), &end);
+        if (t.isString || end == t.text.c_str() || *end) throw Error(Loc(t) + ": expected a number, got '" + t.text + "'");
+        return v;
+    }
+    std::string Str(const std::vector<Token> &toks, size_t &pos) {
+        if (pos >= toks.size() || !toks[pos].isString)
+            throw Error((pos < toks.size() ? Loc(toks[pos]) : std::string("EOF")) + ": expected a quoted string");
+        return toks[pos++].text;
+    }
+    ParamSet Params(const std::vector<Token> &toks, size_t &pos) {
+        ParamSet ps;
+        ps.loc = pos > 0 ? Loc(toks[pos - 1]) : "";
+        while (pos < toks.size() && toks[pos].isString) {
+            std::string decl = toks[pos].text;
+            std::istringstream ds(decl);
+            Param p;
+            ds >> p.type >> p.name;
+            if (p.name.empty()) break;  // a bare string: not a parameter declaration
+            ++pos;
+            if (p.type == "point") p.type = "point3";
+            if (p.type == "vector") p.type = "vector3";
+            if (p.type == "color") p.type = "rgb";
+            if (p.type == "normal3") p.type = "normal";
+            auto value = [&](const Token &t) {
+                if (p.type == "string" || p.type == "texture" || (p.type == "spectrum" && t.isString)) {
+                    if (!t.isString) throw Error(Loc(t) + ": expected string value for " + p.name);
+                    p.strs.push_back(t.text);
+                } else if (p.type == "bool") {
+                    std::string v = t.text;
+                    if (v != "true" && v != "false") throw Error(Loc(t) + ": bad bool value");
+                    p.bools.push_back(v == "true");
+                } else {
+                    char *end = nullptr;
+                    double v = std::strtod(t.text.c_str(), &end);
+                    if (t.isString || *end) throw Error(Loc(t) + ": bad numeric value '" + t.text + "'");
+                    p.nums.push_back(v);
+                }
+            };
+            if (pos < toks.size() && toks[pos].text == "[" && !toks[pos].isString) {
+                ++pos;
+                while (pos < toks.size() && !(toks[pos].text == "]" && !toks[pos].isString)) value(toks[pos++]);
+                if (pos >= toks.size()) throw Error(ps.loc + ": unterminated [");
+                ++pos;
+            } else if (pos < toks.size()) {
+                value(toks[pos++]);
+            }
+            ps.params.push_back(std::move(p));
+        }
+        return ps;
+    }
+
+    void Directive(const std::vector<Token> &toks, size_t &pos, const std::string &dir) {
+        const Token &t = toks[pos++];
+        const std::string &d = t.text;
+        std::string loc = Loc(t);
+        if (d == "LookAt") {
+            double v[9];
+            for (double &x : v) x = Num(toks, pos);
+            gs.ctm = Mul(gs.ctm, LookAtM(V3(v[0], v[1], v[2]), V3(v[3], v[4], v[5]), V3(v[6], v[7], v[8])));
+        } else if (d == "Translate") {
+            double x = Num(toks, pos), y = Num(toks, pos), z = Num(toks, pos);
+            gs.ctm = Mul(gs.ctm, TranslateM(x, y, z));
+        } else if (d == "Scale") {
+            double x = Num(toks, pos), y = Num(toks, pos), z = Num(toks, pos);
+            gs.ctm = Mul(gs.ctm, ScaleM(x, y, z));
+        } else if (d == "Rotate") {
+            double a = Num(toks, pos), x = Num(toks, pos), y = Num(toks, pos), z = Num(toks, pos);
+            gs.ctm = Mul(gs.ctm, RotateM(a, x, y, z));
+        } else if (d == "Identity") {
+            gs.ctm = Identity4();
+        } else if (d == "Transform" || d == "ConcatTransform") {
+            bool br = pos < toks.size() && toks[pos].text == "[";
+            if (br) ++pos;
+            double v[16];
+            for (double &x : v) x = Num(toks, pos);
+            if (br) {
+                if (toks[pos].text != "]") throw Error(loc + ": expected ]");
+                ++pos;
+            }
+            Mat4 m;
+            for (int i = 0; i < 4; ++i)
+                for (int j = 0; j < 4; ++j) m[i][j] = v[j * 4 + i];  // Transpose(m)
+            gs.ctm = (d == "Transform") ? m : Mul(gs.ctm, m);
+        } else if (d == "CoordinateSystem") {
+            namedCoordSys[Str(toks, pos)] = gs.ctm;
+        } else if (d == "CoordSysTransform") {
+            std::string n = Str(toks, pos);
+            if (!namedCoordSys.count(n)) throw Error(loc + ": unknown coordinate system " + n);
+            gs.ctm = namedCoordSys[n];
+        } else if (d == "ReverseOrientation") {
+            gs.reverseOrientation = !gs.reverseOrientation;
+        } else if (d == "Camera") {
+            cameraType = Str(toks, pos);
+            cameraParams = Params(toks, pos);
+            cameraParams.loc = loc;
+            cameraFromWorld = gs.ctm;
+            namedCoordSys["camera"] = Inverse4(gs.ctm);
+            haveCamera = true;
+        } else if (d == "Film") {
+            filmType = Str(toks, pos);
+            filmParams = Params(toks, pos);
+            filmParams.loc = loc;
+        } else if (d == "Sampler") {
+            scene.samplerName = Str(toks, pos);
+            samplerParams = Params(toks, pos);
+            samplerParams.loc = loc;
+        } else if (d == "PixelFilter") {
+            scene.filterName = Str(toks, pos);
+            filterParams = Params(toks, pos);
+            filterParams.loc = loc;
+        } else if (d == "Integrator") {
+            scene.integratorName = Str(toks, pos);
+            integratorParams = Params(toks, pos);
+            integratorParams.loc = loc;
+        } else if (d == "Accelerator" || d == "Option" || d == "ColorSpace" || d == "Attribute") {
+            if (d == "ColorSpace") {
+                std::string cs = Str(toks, pos);
+                if (cs != "srgb") throw Error(loc + ": only the srgb colour space is supported");
+            } else if (d == "Option") {
+                Str(toks, pos);
+                if (pos < toks.size()) ++pos;
+            } else {
+                Str(toks, pos);
+                Params(toks, pos);
+            }
+        } else if (d == "WorldBegin") {
+            inWorld = true;
+            gs.ctm = Identity4();
+            namedCoordSys["world"] = gs.ctm;
+        } else if (d == "WorldEnd") {
+        } else if (d == "AttributeBegin" || d == "TransformBegin") {
+            stack.push_back(gs);
+        } else if (d == "AttributeEnd" || d == "TransformEnd") {
+            if (stack.empty()) throw Error(loc + ": unmatched " + d);
+            if (d == "TransformEnd") {
+                Mat4 m = stack.back().ctm;
+                stack.pop_back();
+                gs.ctm = m;
+            } else {
+                gs = stack.back();
+                stack.pop_back();
+            }
+        } else if (d == "Material") {
+            std::string type = Str(toks, pos);
+            ParamSet ps = Params(toks, pos);
+            ps.loc = loc;
+            gs.material = MakeMaterial(type, ps, "");
+        } else if (d == "MakeNamedMaterial") {
+            std::string name = Str(toks, pos);
+            ParamSet ps = Params(toks, pos);
+            ps.loc = loc;
+            std::string type = ps.GetString("type", "");
+            if (type.empty()) throw Error(loc + ": MakeNamedMaterial needs \"string type\"");
+            namedMaterials[name] = MakeMaterial(type, ps, name);
+        } else if (d == "NamedMaterial") {
+            std::string name = Str(toks, pos);
+            if (!namedMaterials.count(name)) throw Error(loc + ": named material \"" + name + "\" undefined");
+            gs.material = namedMaterials[name];
+        } else if (d == "AreaLightSource") {
+            gs.areaLightName = Str(toks, pos);
+            gs.areaLightParams = Params(toks, pos);
+            gs.areaLightParams.loc = loc;
+            if (gs.areaLightName != "diffuse") throw Error(loc + ": unsupported area light " + gs.areaLightName);
+        } else if (d == "LightSource") {
+            PendingLight l;
+            l.type = Str(toks, pos);
+            l.params = Params(toks, pos);
+            l.params.loc = loc;
+            l.worldFromLight = gs.ctm;
+            lights.push_back(std::move(l));
+        } else if (d == "Shape") {
+            std::string type = Str(toks, pos);
+            ParamSet ps = Params(toks, pos);
+            ps.loc = loc;
+            Shape(type, ps);
+        } else if (d == "Include" || d == "Import") {
+            std::string f = Str(toks, pos);
+            std::string path = (f.size() && f[0] == '/') ? f : (dir.empty() ? f : dir + "/" + f);
+            ParseFile(path);
+        } else if (d == "Texture" || d == "MakeNamedMedium" || d == "MediumInterface" || d == "ObjectBegin" ||
+                   d == "ObjectEnd" || d == "ObjectInstance" || d == "ActiveTransform" || d == "TransformTimes") {
+            throw Error(loc + ": directive " + d + " is not supported by the wavefront hot path yet");
+        } else {
+            throw Error(loc + ": unknown directive '" + d + "'");
+        }
+    }
+
+    int MakeMaterial(const std::string &type, ParamSet &ps, const std::string &name) {
+        MaterialDesc m;
+        m.name = name;
+        if (type == "diffuse") {
+            m.type = kMatDiffuse;
+            Param *r = ps.Find("reflectance");
+            if (!r) {
+                m.constant = true;
+                m.constantValue = 0.5f;
+            } else if (r->type == "rgb") {
+                if (r->nums.size() != 3) throw Error(ps.loc + ": reflectance needs 3 values");
+                float rgb[3] = {(float)r->nums[0], (float)r->nums[1], (float)r->nums[2]};
+                for (float v : rgb)
+                    if (v < 0 || v > 1) throw Error(ps.loc + ": RGB reflectance must be in [0,1]");
+                auto c = RGBToSigmoidCoeffs(rgb[0], rgb[1], rgb[2]);
+                m.c0 = c[0];
+                m.c1 = c[1];
+                m.c2 = c[2];
+            } else if (r->type == "float") {
+                m.constant = true;
+                m.constantValue = (float)r->nums[0];
+            } else {
+                throw Error(ps.loc + ": reflectance of type " + r->type + " not supported");
+            }
+        } else {
+            throw Error(ps.loc + ": material \"" + type + "\" is not supported yet");
+        }
+        ps.Find("type");
+        ps.CheckUnused();
+        scene.materials.push_back(m);
+        return (int)scene.materials.size() - 1;
+    }
+
+    void Shape(const std::string &type, ParamSet &ps) {
+        if (type != "trianglemesh") throw Error(ps.loc + ": shape \"" + type + "\" is not supported yet");
+        PendingShape s;
+        Param *P = ps.Find("P", "point3");
+        if (!P || P->nums.size() % 3) throw Error(ps.loc + ": trianglemesh needs \"point3 P\"");
+        for (size_t i = 0; i < P->nums.size(); i += 3) s.P.push_back(V3(P->nums[i], P->nums[i + 1], P->nums[i + 2]));
+        Param *I = ps.Find("indices", "integer");
+        if (I)
+            for (double v : I->nums) s.idx.push_back((int)v);
+        else if (s.P.size() == 3)
+            s.idx = {0, 1, 2};
+        else
+            throw Error(ps.loc + ": trianglemesh needs \"integer indices\"");
+        if (s.idx.size() % 3) throw Error(ps.loc + ": indices not a multiple of 3");
+        for (int v : s.idx)
+            if (v < 0 || v >= (int)s.P.size()) throw Error(ps.loc + ": vertex index out of range");
+        Param *uv = ps.Find("uv", "point2");
+        if (uv) {
+            if (uv->nums.size() != 2 * s.P.size()) throw Error(ps.loc + ": uv count mismatch");
+            for (double v : uv->nums) s.uv.push_back((float)v);
+        }
+        if (ps.Find("N") || ps.Find("S")) throw Error(ps.loc + ": per-vertex shading normals/tangents not supported yet");
+        ps.Find("faceIndices");
+        ps.CheckUnused();
+        s.renderFromObject = gs.ctm;  // renderFromWorld applied at Finish
+        s.flip = gs.reverseOrientation;
+        s.material = gs.material;
+        s.areaLight = gs.areaLightName;
+        s.areaParams = gs.areaLightParams;
+        s.loc = ps.loc;
+        shapes.push_back(std::move(s));
+    }
+};
+
+void Parser::Finish() {
+    if (!haveCamera) {
+        cameraFromWorld = Identity4();
+    }
+    // ---- film (film.cpp FilmBaseParameters)
+    if (filmType != "rgb") throw Error(filmParams.loc + ": film \"" + filmType + "\" not supported (rgb only)");
+    scene.xres = filmParams.GetInt("xresolution", 1280);
+    scene.yres = filmParams.GetInt("yresolution", 720);
+    if (overrides.count("xresolution")) scene.xres = std::stoi(overrides.at("xresolution"));
+    if (overrides.count("yresolution")) scene.yres = std::stoi(overrides.at("yresolution"));
+    scene.outFile = filmParams.GetString("filename", "pbrt.exr");
+    {
+        Param *pb = filmParams.Find("pixelbounds", "integer");
+        Param *cw = filmParams.Find("cropwindow", "float");
+        scene.px0 = 0;
+        scene.px1 = scene.xres;
+        scene.py0 = 0;
+        scene.py1 = scene.yres;
+        if (pb && pb->nums.size() == 4) {
+            scene.px0 = (int)pb->nums[0];
+            scene.px1 = (int)pb->nums[1];
+            scene.py0 = (int)pb->nums[2];
+            scene.py1 = (int)pb->nums[3];
+        } else if (cw && cw->nums.size() == 4) {
+            scene.px0 = (int)std::ceil(scene.xres * cw->nums[0]);
+            scene.px1 = (int)std::ceil(scene.xres * cw->nums[1]);
+            scene.py0 = (int)std::ceil(scene.yres * cw->nums[2]);
+            scene.py1 = (int)std::ceil(scene.yres * cw->nums[3]);
+        }
+        if (overrides.count("pixelbounds")) {
+            int v[4];
+            std::istringstream is(overrides.at("pixelbounds"));
+            char c;
+            is >> v[0] >> c >> v[1] >> c >> v[2] >> c >> v[3];
+            scene.px0 = v[0];
+            scene.px1 = v[1];
+            scene.py0 = v[2];
+            scene.py1 = v[3];
+        }
+        double iso = filmParams.GetFloat("iso", 100.);
+        std::string sensor = filmParams.GetString("sensor", "cie1931");
+        if (sensor != "cie1931") throw Error(filmParams.loc + ": only the cie1931 sensor is supported");
+        if (filmParams.GetFloat("whitebalance", 0) != 0) throw Error(filmParams.loc + ": whitebalance not supported");
+        if (filmParams.Find("maxcomponentvalue")) throw Error(filmParams.loc + ": maxcomponentvalue not supported");
+        filmParams.Find("savefp16");
+        filmParams.Find("diagonal");
+        double exposure = cameraParams.GetFloat("shutterclose", 1.0) - cameraParams.GetFloat("shutteropen", 0.0);
+        scene.imagingRatio = (float)(exposure * iso / 100);
+        filmParams.CheckUnused();
+    }
+    // ---- sampler
+    scene.spp = samplerParams.GetInt("pixelsamples", 16);
+    scene.seed = samplerParams.GetInt("seed", 0);
+    if (overrides.count("spp")) scene.spp = std::stoi(overrides.at("spp"));
+    if (overrides.count("seed")) scene.seed = std::stoi(overrides.at("seed"));
+    if (scene.samplerName != "halton")
+        throw Error(samplerParams.loc + ": sampler \"" + scene.samplerName + "\" not supported yet (halton only)");
+    if (samplerParams.GetString("randomization", "permutedigits") != "permutedigits")
+        throw Error(samplerParams.loc + ": only permutedigits randomization is supported");
+    samplerParams.CheckUnused();
+    // ---- integrator
+    scene.maxDepth = integratorParams.GetInt("maxdepth", 5);
+    if (overrides.count("maxdepth")) scene.maxDepth = std::stoi(overrides.at("maxdepth"));
+    scene.regularize = integratorParams.GetBool("regularize", false);
+    std::string ls = integratorParams.GetString("lightsampler", "bvh");
+    if (ls != "bvh" && ls != "uniform") throw Error(integratorParams.loc + ": lightsampler " + ls + " not supported");
+    if (ls == "uniform") scene.uniformLightSampler = true;
+    if (scene.regularize) throw Error(integratorParams.loc + ": regularize not supported");
+    // ---- filter
+    if (scene.filterName != "box") throw Error(filterParams.loc + ": pixel filter \"" + scene.filterName + "\" not supported yet (box only)");
+    scene.filterRadiusX = (float)filterParams.GetFloat("xradius", 0.5);
+    scene.filterRadiusY = (float)filterParams.GetFloat("yradius", 0.5);
+    filterParams.CheckUnused();
+
+    // ---- camera (cameras.cpp:43-73, 266-285, 543-600) in cameraworld rendering space
+    if (cameraType != "perspective") throw Error(cameraParams.loc + ": camera \"" + cameraType + "\" not supported");
+    {
+        Mat4 worldFromCamera = Inverse4(cameraFromWorld);
+        V3 pCam = XformPoint(worldFromCamera, V3(0, 0, 0));
+        Mat4 renderFromWorld = TranslateM(-(double)pCam.x, -(double)pCam.y, -(double)pCam.z);
+        scene.camera.renderFromWorld = renderFromWorld;
+        scene.camera.renderFromCamera = Mul(renderFromWorld, worldFromCamera);
+        double frame = cameraParams.GetFloat("frameaspectratio", double((float)scene.xres / (float)scene.yres));
+        double sx0, sx1, sy0, sy1;
+        if (frame > 1.) {
+            sx0 = -frame;
+            sx1 = frame;
+            sy0 = -1;
+            sy1 = 1;
+        } else {
+            sx0 = -1;
+            sx1 = 1;
+            sy0 = -1 / frame;
+            sy1 = 1 / frame;
+        }
+        if (Param *sw = cameraParams.Find("screenwindow", "float")) {
+            if (sw->nums.size() != 4) throw Error(cameraParams.loc + ": screenwindow needs 4 values");
+            sx0 = sw->nums[0];
+            sx1 = sw->nums[1];
+            sy0 = sw->nums[2];
+            sy1 = sw->nums[3];
+        }
+        double fov = cameraParams.GetFloat("fov", 90.);
+        scene.camera.fov = (float)fov;
+        scene.camera.lensRadius = (float)cameraParams.GetFloat("lensradius", 0.);
+        scene.camera.focalDistance = (float)cameraParams.GetFloat("focaldistance", 1e6);
+        scene.camera.shutterOpen = (float)cameraParams.GetFloat("shutteropen", 0.);
+        scene.camera.shutterClose = (float)cameraParams.GetFloat("shutterclose", 1.);
+        Mat4 screenFromCamera = PerspectiveM(fov, 1e-2, 1000.);
+        Mat4 NDCFromScreen = Mul(ScaleM(1 / (sx1 - sx0), 1 / (sy1 - sy0), 1), TranslateM(-sx0, -sy1, 0));
+        Mat4 rasterFromNDC = ScaleM(scene.xres, -scene.yres, 1);
+        Mat4 rasterFromScreen = Mul(rasterFromNDC, NDCFromScreen);
+        scene.camera.cameraFromRaster = Mul(Inverse4(screenFromCamera), Inverse4(rasterFromScreen));
+        cameraParams.CheckUnused();
+    }
+    // ---- sensor / output colour space
+    {
+        const SpectralData &sd = GetSpectralData();
+        scene.sensorX = sd.denseX;
+        scene.sensorY = sd.denseY;
+        scene.sensorZ = sd.denseZ;
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) scene.outputRGBFromSensorRGB[i][j] = sd.rgbFromXYZ[i][j];
+    }
+    // ---- shapes -> render-space triangles; area lights in shape order
+    const Mat4 &renderFromWorld = scene.camera.renderFromWorld;
+    std::map<std::string, int> spectrumCache;
+    for (PendingShape &s : shapes) {
+        Mat4 rfo = Mul(renderFromWorld, s.renderFromObject);
+        bool flip = s.flip ^ SwapsHandedness(rfo);
+        int base = (int)scene.verts.size();
+        for (V3 p : s.P) scene.verts.push_back(XformPoint(rfo, p));
+        int mat = s.material;
+        if (mat < 0) {
+            // pbrt's default material is "diffuse" with reflectance 0.5
+            MaterialDesc m;
+            m.constant = true;
+            m.constantValue = 0.5f;
+            m.name = "__default";
+            scene.materials.push_back(m);
+            mat = (int)scene.materials.size() - 1;
+            for (PendingShape &o : shapes)
+                if (o.material < 0) o.material = mat;
+        }
+        int lightSpectrum = -1;
+        float lightScale = 1;
+        bool twoSided = false;
+        if (!s.areaLight.empty()) {
+            ParamSet &ap = s.areaParams;
+            Param *L = ap.Find("L");
+            float rgb[3] = {0, 0, 0};
+            std::array<float, 311> dense;
+            if (!L) {
+                dense = GetSpectralData().denseD65;  // colorSpace->illuminant
+            } else if (L->type == "rgb") {
+                if (L->nums.size() != 3) throw Error(ap.loc + ": L needs 3 values");
+                for (int i = 0; i < 3; ++i) rgb[i] = (float)L->nums[i];
+                dense = DenseRGBIlluminant(rgb[0], rgb[1], rgb[2]);
+            } else if (L->type == "blackbody") {
+                throw Error(ap.loc + ": blackbody L not supported yet");
+            } else {
+                throw Error(ap.loc + ": L of type " + L->type + " not supported");
+            }
+            std::string key = std::to_string(rgb[0]) + "," + std::to_string(rgb[1]) + "," + std::to_string(rgb[2]) +
+                              (L ? "" : "D65");
+            if (!spectrumCache.count(key)) {
+                scene.denseSpectra.push_back(dense);
+                spectrumCache[key] = (int)scene.denseSpectra.size() - 1;
+            }
+            lightSpectrum = spectrumCache[key];
+            lightScale = (float)ap.GetFloat("scale", 1);
+            twoSided = ap.GetBool("twosided", false);
+            // lights.cpp:941: scale /= SpectrumToPhotometric(L) (illuminant part only)
+            lightScale /= GetSpectralData().photometricD65;
+            if (ap.GetFloat("power", -1) > 0) throw Error(ap.loc + ": \"power\" not supported yet");
+            float spread = (float)ap.GetFloat("spread", 90);
+            if (spread != 90) throw Error(ap.loc + ": \"spread\" other than 90 not supported yet");
+            ap.Find("filename");
+            ap.CheckUnused();
+        }
+        for (size_t t = 0; t < s.idx.size(); t += 3) {
+            std::array<int, 3> tri = {base + s.idx[t], base + s.idx[t + 1], base + s.idx[t + 2]};
+            int triIndex = (int)scene.tris.size();
+            scene.tris.push_back(tri);
+            scene.triMaterial.push_back(s.material < 0 ? mat : s.material);
+            scene.triFlip.push_back(flip ? 1 : 0);
+            if (!s.uv.empty()) throw Error(s.loc + ": per-vertex uv not supported yet");
+            if (lightSpectrum >= 0) {
+                AreaLightDesc l;
+                l.prim = triIndex;
+                l.spectrum = lightSpectrum;
+                l.scale = lightScale;
+                l.twoSided = twoSided;
+                V3 p0 = scene.verts[tri[0]], p1 = scene.verts[tri[1]], p2 = scene.verts[tri[2]];
+                l.area = 0.5f * Length(Cross(p1 - p0, p2 - p0));  // Triangle::Area (shapes.h)
+                scene.triLight.push_back((int)scene.areaLights.size());
+                scene.areaLights.push_back(l);
+            } else {
+                scene.triLight.push_back(-1);
+            }
+        }
+    }
+    for (PendingLight &l : lights) {
+        if (l.type != "infinite") throw Error(l.params.loc + ": light \"" + l.type + "\" not supported yet");
+        Param *L = l.params.Find("L");
+        if (l.params.Find("filename")) throw Error(l.params.loc + ": image infinite lights not supported yet");
+        InfiniteLightDesc il;
+        std::array<float, 311> dense;
+        if (!L)
+            dense = GetSpectralData().denseD65;
+        else if (L->type == "rgb" && L->nums.size() == 3)
+            dense = DenseRGBIlluminant((float)L->nums[0], (float)L->nums[1], (float)L->nums[2]);
+        else
+            throw Error(l.params.loc + ": infinite light L must be rgb");
+        scene.denseSpectra.push_back(dense);
+        il.spectrum = (int)scene.denseSpectra.size() - 1;
+        il.scale = (float)l.params.GetFloat("scale", 1) / GetSpectralData().photometricD65;
+        if (l.params.Find("illuminance")) throw Error(l.params.loc + ": illuminance not supported yet");
+        l.params.CheckUnused();
+        scene.infiniteLights.push_back(il);
+    }
+    if (scene.areaLights.empty() && scene.infiniteLights.empty()) throw Error("No light sources specified");
+    if (scene.areaLights.size() + scene.infiniteLights.size() == 1) scene.uniformLightSampler = true;
+}
+
+SceneDesc LoadPbrtString(const std::string &text, const std::string &baseDir,
+                         const std::map<std::string, std::string> &overrides) {
+    SceneDesc s;
+    Parser p(s, overrides);
+    p.ParseString(text, "<string>", baseDir);
+    p.Finish();
+    FinalizeScene(s);
+    return s;
+}
+
+SceneDesc LoadPbrtFile(const std::string &path, const std::map<std::string, std::string> &overrides) {
+    SceneDesc s;
+    Parser p(s, overrides);
+    p.ParseFile(path);
+    p.Finish();
+    FinalizeScene(s);
+    return s;
+}
+
+}  // namespace pbrt_amd

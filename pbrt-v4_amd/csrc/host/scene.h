@@ -1,0 +1,143 @@
+// Host-side scene model of pbrt-v4_amd: what the .pbrt subset loader produces and what
+// the device upload consumes.  Everything is already in pbrt's "cameraworld" rendering
+// space (cameras.cpp:51-56), triangles are flattened, and every spectrum the device
+// evaluates is reduced to either sigmoid-polynomial coefficients (util/color.h:332) or a
+// densely sampled 395..705 nm table (util/spectrum.h:400).
+#pragma once
+
+#include <array>
+#include <cstdint>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../core/core.h"
+
+namespace pbrt_amd {
+
+struct Error : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+using Mat4 = std::array<std::array<double, 4>, 4>;
+Mat4 Identity4();
+Mat4 Mul(const Mat4 &a, const Mat4 &b);
+Mat4 Inverse4(const Mat4 &m);
+V3 XformPoint(const Mat4 &m, V3 p);
+V3 XformVector(const Mat4 &m, V3 v);
+V3 XformNormal(const Mat4 &mInv, V3 n);  // uses the inverse transpose
+bool SwapsHandedness(const Mat4 &m);
+
+enum MaterialType : int { kMatDiffuse = 0, kMatNumTypes = 1 };
+
+struct MaterialDesc {
+    int type = kMatDiffuse;
+    // spectrum of the reflectance: sigmoid (c0,c1,c2) or a constant value
+    bool constant = false;
+    float constantValue = 0.5f;
+    float c0 = 0, c1 = 0, c2 = 0;
+    std::string name;
+};
+
+struct AreaLightDesc {
+    int prim = -1;          // triangle index in SceneDesc::tris
+    int spectrum = -1;      // index into SceneDesc::denseSpectra
+    float scale = 1;        // final DiffuseAreaLight::scale (lights.cpp:941-966)
+    bool twoSided = false;
+    float area = 0;
+};
+
+struct InfiniteLightDesc {
+    int spectrum = -1;
+    float scale = 1;
+};
+
+struct CameraDesc {
+    Mat4 cameraFromRaster;   // ProjectiveCamera (cameras.h:266-285)
+    Mat4 renderFromCamera;   // CameraTransform (cameras.cpp:43-73)
+    Mat4 renderFromWorld;
+    float lensRadius = 0, focalDistance = 1e6f;
+    float shutterOpen = 0, shutterClose = 1;
+    float fov = 90;
+};
+
+struct LightBVHNodeDesc {
+    LightNodeBounds bounds;  // decoded CompactLightBounds
+    int childOrLight = 0;    // second child index for interior, light index for leaf
+    int isLeaf = 0;
+};
+
+struct SceneDesc {
+    // film / sampler / integrator
+    int xres = 1280, yres = 720;
+    int px0 = 0, px1 = 1280, py0 = 0, py1 = 720;  // pixel bounds
+    int spp = 16, seed = 0, maxDepth = 5;
+    std::string samplerName = "zsobol";
+    std::string integratorName = "volpath";
+    bool regularize = false;
+    std::string outFile = "pbrt.exr";
+    float filterRadiusX = 0.5f, filterRadiusY = 0.5f;  // box (scene.cpp:94 fork default)
+    std::string filterName = "box";
+    float imagingRatio = 1;
+    double outputRGBFromSensorRGB[3][3];
+    CameraDesc camera;
+
+    // geometry (render space)
+    std::vector<V3> verts;
+    std::vector<std::array<int, 3>> tris;
+    std::vector<int> triMaterial;   // material index
+    std::vector<int> triLight;      // area light index or -1
+    std::vector<uint8_t> triFlip;   // reverseOrientation ^ transformSwapsHandedness
+
+    std::vector<MaterialDesc> materials;
+    std::vector<AreaLightDesc> areaLights;
+    std::vector<InfiniteLightDesc> infiniteLights;
+    std::vector<std::array<float, 311>> denseSpectra;
+    std::array<float, 311> sensorX, sensorY, sensorZ;  // r_bar/g_bar/b_bar of "cie1931"
+
+    // BVH light sampler (lightsamplers.cpp:112-236); unused when one light -> uniform
+    bool uniformLightSampler = false;
+    std::vector<LightBVHNodeDesc> lightNodes;
+    std::vector<uint32_t> lightBitTrail;  // per area light
+
+    // Halton digit permutations (util/lowdiscrepancy.cpp:47-55) for the dimensions used
+    int haltonBaseScales[2] = {1, 1}, haltonBaseExponents[2] = {0, 0}, haltonMultInverse[2] = {0, 0};
+    std::vector<uint16_t> permTable;       // concatenated nDigits*base rows per dimension
+    std::vector<uint32_t> permOffset;      // per dimension: offset into permTable
+    std::vector<uint32_t> permNDigits;     // per dimension
+    std::vector<uint32_t> permBase;        // per dimension (prime)
+};
+
+// Loaders and builders
+SceneDesc LoadPbrtFile(const std::string &path, const std::map<std::string, std::string> &overrides);
+SceneDesc LoadPbrtString(const std::string &text, const std::string &baseDir,
+                         const std::map<std::string, std::string> &overrides);
+void FinalizeScene(SceneDesc &s);  // lights, light BVH, halton tables
+
+// Spectral support (host)
+struct SpectralData {
+    std::vector<float> cieX, cieY, cieZ, cieLambda, d65Interleaved;
+    std::vector<double> optX, optY, optZ, optD65Raw, optXyzToSrgb, optSrgbToXyz;
+    double optD65Divisor = 1;
+    std::array<float, 311> denseX, denseY, denseZ, denseD65;  // 395..705
+    float photometricD65 = 0;                                  // SpectrumToPhotometric(D65)
+    double rgbFromXYZ[3][3];
+};
+const SpectralData &GetSpectralData();
+void SetDataDirectory(const std::string &dir);
+std::string GetDataDirectory();
+// RGB -> sigmoid coefficients through the 64^3 sRGB table (util/color.cpp:36-75); table
+// columns are generated on demand with the rgb2spec Gauss-Newton restatement.
+std::array<float, 3> RGBToSigmoidCoeffs(float r, float g, float b);
+// Column (maxc, yi, xi) of the 64^3 table as produced by cmd/rgb2spec_opt.cpp: 64 x 3 floats
+std::vector<float> RGB2SpecColumn(int maxc, int j, int i);
+float RGB2SpecZNode(int k);
+std::array<float, 311> DenseRGBIlluminant(float r, float g, float b);
+
+// Hash / permutation (util/hash.h:19, util/math.h:728)
+uint64_t MurmurHash64A(const unsigned char *key, size_t len, uint64_t seed);
+int PermutationElement(uint32_t i, uint32_t l, uint32_t p);
+const std::vector<int> &Primes();
+
+}  // namespace pbrt_amd

@@ -1,0 +1,439 @@
+// Host spectral setup: CIE data, dense spectra, the sRGB colour space, and the RGB ->
+// sigmoid-polynomial table of pbrt (util/color.cpp:36-75, util/colorspace.cpp:25-38,
+// util/spectrum.cpp:37-51,133-163,2586-2610, cmd/rgb2spec_opt.cpp:248-570).
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <mutex>
+#include <sstream>
+
+#include "scene.h"
+
+namespace pbrt_amd {
+
+static std::string g_dataDir;
+void SetDataDirectory(const std::string &dir) { g_dataDir = dir; }
+std::string GetDataDirectory() {
+    if (!g_dataDir.empty()) return g_dataDir;
+    if (const char *e = std::getenv("PBRT_AMD_DATA")) return e;
+    return "pbrt-v4_amd/data";
+}
+
+static float PiecewiseLinearEval(const std::vector<float> &lambdas, const std::vector<float> &values,
+                                 float lambda) {
+    // util/spectrum.cpp PiecewiseLinearSpectrum::operator()
+    if (lambdas.empty() || lambda < lambdas.front() || lambda > lambdas.back()) return 0;
+    // FindInterval(size, lambdas[i] <= lambda)
+    int sz = (int)lambdas.size();
+    int size = sz - 2, first = 1;
+    while (size > 0) {
+        int half = size >> 1, middle = first + half;
+        bool pred = lambdas[middle] <= lambda;
+        first = pred ? middle + 1 : first;
+        size = pred ? size - (half + 1) : half;
+    }
+    int o = std::min(std::max(first - 1, 0), sz - 2);
+    float t = (lambda - lambdas[o]) / (lambdas[o + 1] - lambdas[o]);
+    return Lerpf(t, values[o], values[o + 1]);
+}
+
+static void Invert3(const double m[3][3], double r[3][3]) {
+    double det = m[0][0] * (m[1][1] * m[2][2] - m[1][2] * m[2][1]) -
+                 m[0][1] * (m[1][0] * m[2][2] - m[1][2] * m[2][0]) +
+                 m[0][2] * (m[1][0] * m[2][1] - m[1][1] * m[2][0]);
+    double id = 1.0 / det;
+    r[0][0] = (m[1][1] * m[2][2] - m[1][2] * m[2][1]) * id;
+    r[0][1] = (m[0][2] * m[2][1] - m[0][1] * m[2][2]) * id;
+    r[0][2] = (m[0][1] * m[1][2] - m[0][2] * m[1][1]) * id;
+    r[1][0] = (m[1][2] * m[2][0] - m[1][0] * m[2][2]) * id;
+    r[1][1] = (m[0][0] * m[2][2] - m[0][2] * m[2][0]) * id;
+    r[1][2] = (m[0][2] * m[1][0] - m[0][0] * m[1][2]) * id;
+    r[2][0] = (m[1][0] * m[2][1] - m[1][1] * m[2][0]) * id;
+    r[2][1] = (m[0][1] * m[2][0] - m[0][0] * m[2][1]) * id;
+    r[2][2] = (m[0][0] * m[1][1] - m[0][1] * m[1][0]) * id;
+}
+
+static SpectralData LoadSpectralData() {
+    SpectralData d;
+    std::string path = GetDataDirectory() + "/spectral_data.txt";
+    std::ifstream in(path);
+    if (!in) throw Error("cannot open spectral data file " + path);
+    std::string line;
+    while (std::getline(in, line)) {
+        std::istringstream ls(line);
+        std::string name;
+        size_t n;
+        ls >> name >> n;
+        std::vector<double> v(n);
+        for (size_t i = 0; i < n; ++i) ls >> v[i];
+        auto tof = [&](std::vector<float> &dst) { dst.assign(v.begin(), v.end()); };
+        if (name == "CIE_X") tof(d.cieX);
+        else if (name == "CIE_Y") tof(d.cieY);
+        else if (name == "CIE_Z") tof(d.cieZ);
+        else if (name == "CIE_lambda") tof(d.cieLambda);
+        else if (name == "CIE_Illum_D6500_interleaved") tof(d.d65Interleaved);
+        else if (name == "opt_cie_x") d.optX = v;
+        else if (name == "opt_cie_y") d.optY = v;
+        else if (name == "opt_cie_z") d.optZ = v;
+        else if (name == "opt_cie_d65_raw") d.optD65Raw = v;
+        else if (name == "opt_cie_d65_divisor") d.optD65Divisor = v[0];
+        else if (name == "opt_xyz_to_srgb") d.optXyzToSrgb = v;
+        else if (name == "opt_srgb_to_xyz") d.optSrgbToXyz = v;
+    }
+    if (d.cieX.size() != 471 || d.optX.size() != 95) throw Error("malformed spectral data " + path);
+    // Spectra::Init: dense X/Y/Z over Lambda_min..Lambda_max of PiecewiseLinear(CIE_lambda, CIE_*)
+    for (int l = 395; l <= 705; ++l) {
+        d.denseX[l - 395] = PiecewiseLinearEval(d.cieLambda, d.cieX, (float)l);
+        d.denseY[l - 395] = PiecewiseLinearEval(d.cieLambda, d.cieY, (float)l);
+        d.denseZ[l - 395] = PiecewiseLinearEval(d.cieLambda, d.cieZ, (float)l);
+    }
+    // stdillum-D65 = PiecewiseLinearSpectrum::FromInterleaved(CIE_Illum_D6500, normalize=true)
+    std::vector<float> lam, val;
+    for (size_t i = 0; i + 1 < d.d65Interleaved.size(); i += 2) {
+        lam.push_back(d.d65Interleaved[i]);
+        val.push_back(d.d65Interleaved[i + 1]);
+    }
+    if (lam.front() > kLambdaMin) {
+        lam.insert(lam.begin(), kLambdaMin - 1);
+        val.insert(val.begin(), val.front());
+    }
+    if (lam.back() < kLambdaMax) {
+        lam.push_back(kLambdaMax + 1);
+        val.push_back(val.back());
+    }
+    {
+        // InnerProduct(spec, &Spectra::Y()) over lambda = 395..705 in Float steps
+        float integral = 0;
+        for (float lambda = kLambdaMin; lambda <= kLambdaMax; ++lambda)
+            integral += PiecewiseLinearEval(lam, val, lambda) * d.denseY[DenseOffset(lambda)];
+        const float CIE_Y_integral = 106.856895f;
+        float s = CIE_Y_integral / integral;
+        for (float &v : val) v *= s;
+    }
+    // RGBColorSpace::illuminant = DenselySampledSpectrum(stdillum-D65)
+    for (int l = 395; l <= 705; ++l) d.denseD65[l - 395] = PiecewiseLinearEval(lam, val, (float)l);
+    // SpectrumToPhotometric(illuminant): sum over Float lambda of Y(l) * s(l)
+    {
+        float y = 0;
+        for (float lambda = kLambdaMin; lambda <= kLambdaMax; ++lambda)
+            y += d.denseY[DenseOffset(lambda)] * d.denseD65[DenseOffset(lambda)];
+        d.photometricD65 = y;
+    }
+    // sRGB colour space matrices (colorspace.cpp:25-38), in double
+    {
+        double X = 0, Y = 0, Z = 0;
+        for (int l = 395; l <= 705; ++l) {
+            X += (double)d.denseX[l - 395] * d.denseD65[l - 395];
+            Y += (double)d.denseY[l - 395] * d.denseD65[l - 395];
+            Z += (double)d.denseZ[l - 395] * d.denseD65[l - 395];
+        }
+        const double CIE_Y_integral = 106.856895;
+        X /= CIE_Y_integral;
+        Y /= CIE_Y_integral;
+        Z /= CIE_Y_integral;
+        double wx = X / (X + Y + Z), wy = Y / (X + Y + Z);
+        auto fromxyY = [](double x, double y, double out[3]) {
+            out[0] = x / y;
+            out[1] = 1;
+            out[2] = (1 - x - y) / y;
+        };
+        double R[3], G[3], B[3], W[3];
+        fromxyY(0.64, 0.33, R);
+        fromxyY(0.3, 0.6, G);
+        fromxyY(0.15, 0.06, B);
+        fromxyY(wx, wy, W);
+        W[0] *= Y;
+        W[1] *= Y;
+        W[2] *= Y;
+        // W.xy() then XYZ::FromxyY(w, Y=1)?  pbrt uses W directly: C = inv(rgb) * W
+        W[0] = X;
+        W[1] = Y;
+        W[2] = Z;
+        double rgb[3][3] = {{R[0], G[0], B[0]}, {R[1], G[1], B[1]}, {R[2], G[2], B[2]}};
+        double inv[3][3];
+        Invert3(rgb, inv);
+        double C[3];
+        for (int i = 0; i < 3; ++i) C[i] = inv[i][0] * W[0] + inv[i][1] * W[1] + inv[i][2] * W[2];
+        double xyzFromRGB[3][3];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) xyzFromRGB[i][j] = rgb[i][j] * C[j];
+        Invert3(xyzFromRGB, d.rgbFromXYZ);
+    }
+    return d;
+}
+
+const SpectralData &GetSpectralData() {
+    static std::once_flag once;
+    static SpectralData *data = nullptr;
+    std::call_once(once, [] { data = new SpectralData(LoadSpectralData()); });
+    return *data;
+}
+
+// ------------------------------------------------------------------ rgb2spec restatement
+namespace {
+constexpr int kRes = 64;
+constexpr int kCIESamples = 95;
+constexpr double kCIEMin = 360.0, kCIEMax = 830.0;
+constexpr int kFine = (kCIESamples - 1) * 3 + 1;
+
+struct OptTables {
+    double lambda_tbl[kFine], rgb_tbl[3][kFine], rgb_to_xyz[3][3], xyz_to_rgb[3][3], whitepoint[3];
+};
+
+double cie_interp(const double *data, double x) {  // rgb2spec_opt.cpp:248
+    x -= kCIEMin;
+    x *= (kCIESamples - 1) / (kCIEMax - kCIEMin);
+    int offset = (int)x;
+    if (offset < 0) offset = 0;
+    if (offset > kCIESamples - 2) offset = kCIESamples - 2;
+    double weight = x - offset;
+    return (1.0 - weight) * data[offset] + weight * data[offset + 1];
+}
+
+const OptTables &GetOptTables() {
+    static std::once_flag once;
+    static OptTables *t = nullptr;
+    std::call_once(once, [] {
+        const SpectralData &d = GetSpectralData();
+        t = new OptTables();
+        memset(t, 0, sizeof(*t));
+        double d65[kCIESamples];
+        for (int i = 0; i < kCIESamples; ++i) d65[i] = d.optD65Raw[i] / d.optD65Divisor;
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) {
+                t->xyz_to_rgb[i][j] = d.optXyzToSrgb[3 * i + j];
+                t->rgb_to_xyz[i][j] = d.optSrgbToXyz[3 * i + j];
+            }
+        double h = (kCIEMax - kCIEMin) / (kFine - 1);
+        for (int i = 0; i < kFine; ++i) {  // init_tables, rgb2spec_opt.cpp:408-486
+            double lambda = kCIEMin + i * h;
+            double xyz[3] = {cie_interp(d.optX.data(), lambda), cie_interp(d.optY.data(), lambda),
+                             cie_interp(d.optZ.data(), lambda)},
+                   I = cie_interp(d65, lambda);
+            double weight = 3.0 / 8.0 * h;
+            if (i == 0 || i == kFine - 1)
+                ;
+            else if ((i - 1) % 3 == 2)
+                weight *= 2.f;
+            else
+                weight *= 3.f;
+            t->lambda_tbl[i] = lambda;
+            for (int k = 0; k < 3; ++k)
+                for (int j = 0; j < 3; ++j) t->rgb_tbl[k][i] += t->xyz_to_rgb[k][j] * xyz[j] * I * weight;
+            for (int k = 0; k < 3; ++k) t->whitepoint[k] += xyz[k] * I * weight;
+        }
+    });
+    return *t;
+}
+
+void cie_lab(const OptTables &t, double *p) {
+    double X = 0.0, Y = 0.0, Z = 0.0, Xw = t.whitepoint[0], Yw = t.whitepoint[1], Zw = t.whitepoint[2];
+    for (int j = 0; j < 3; ++j) {
+        X += p[j] * t.rgb_to_xyz[0][j];
+        Y += p[j] * t.rgb_to_xyz[1][j];
+        Z += p[j] * t.rgb_to_xyz[2][j];
+    }
+    auto f = [](double v) -> double {
+        double delta = 6.0 / 29.0;
+        if (v > delta * delta * delta) return cbrt(v);
+        return v / (delta * delta * 3.0) + (4.0 / 29.0);
+    };
+    p[0] = 116.0 * f(Y / Yw) - 16.0;
+    p[1] = 500.0 * (f(X / Xw) - f(Y / Yw));
+    p[2] = 200.0 * (f(Y / Yw) - f(Z / Zw));
+}
+
+void eval_residual(const OptTables &t, const double *coeffs, const double *rgb, double *residual) {
+    double out[3] = {0.0, 0.0, 0.0};
+    for (int i = 0; i < kFine; ++i) {
+        double lambda = (t.lambda_tbl[i] - kCIEMin) / (kCIEMax - kCIEMin);
+        double x = 0.0;
+        for (int k = 0; k < 3; ++k) x = x * lambda + coeffs[k];
+        double s = 0.5 * x / std::sqrt(1.0 + x * x) + 0.5;
+        for (int j = 0; j < 3; ++j) out[j] += t.rgb_tbl[j][i] * s;
+    }
+    cie_lab(t, out);
+    memcpy(residual, rgb, sizeof(double) * 3);
+    cie_lab(t, residual);
+    for (int j = 0; j < 3; ++j) residual[j] -= out[j];
+}
+
+void eval_jacobian(const OptTables &t, const double *coeffs, const double *rgb, double **jac) {
+    const double eps = 1e-4;
+    double r0[3], r1[3], tmp[3];
+    for (int i = 0; i < 3; ++i) {
+        memcpy(tmp, coeffs, sizeof(double) * 3);
+        tmp[i] -= eps;
+        eval_residual(t, tmp, rgb, r0);
+        memcpy(tmp, coeffs, sizeof(double) * 3);
+        tmp[i] += eps;
+        eval_residual(t, tmp, rgb, r1);
+        for (int j = 0; j < 3; ++j) jac[j][i] = (r1[j] - r0[j]) * 1.0 / (2 * eps);
+    }
+}
+
+bool LUPDecompose(double **A, int N, double Tol, int *P) {
+    for (int i = 0; i <= N; i++) P[i] = i;
+    for (int i = 0; i < N; i++) {
+        double maxA = 0.0, absA;
+        int imax = i;
+        for (int k = i; k < N; k++)
+            if ((absA = std::fabs(A[k][i])) > maxA) {
+                maxA = absA;
+                imax = k;
+            }
+        if (maxA < Tol) return false;
+        if (imax != i) {
+            int j = P[i];
+            P[i] = P[imax];
+            P[imax] = j;
+            double *ptr = A[i];
+            A[i] = A[imax];
+            A[imax] = ptr;
+            P[N]++;
+        }
+        for (int j = i + 1; j < N; j++) {
+            A[j][i] /= A[i][i];
+            for (int k = i + 1; k < N; k++) A[j][k] -= A[j][i] * A[i][k];
+        }
+    }
+    return true;
+}
+
+void LUPSolve(double **const A, const int *P, const double *b, int N, double *x) {
+    for (int i = 0; i < N; i++) {
+        x[i] = b[P[i]];
+        for (int k = 0; k < i; k++) x[i] -= A[i][k] * x[k];
+    }
+    for (int i = N - 1; i >= 0; i--) {
+        for (int k = i + 1; k < N; k++) x[i] -= A[i][k] * x[k];
+        x[i] = x[i] / A[i][i];
+    }
+}
+
+void gauss_newton(const OptTables &t, const double rgb[3], double coeffs[3], int it = 15) {
+    for (int i = 0; i < it; ++i) {
+        double J0[3], J1[3], J2[3], *J[3] = {J0, J1, J2};
+        double residual[3];
+        eval_residual(t, coeffs, rgb, residual);
+        eval_jacobian(t, coeffs, rgb, J);
+        int P[4];
+        if (!LUPDecompose(J, 3, 1e-15, P)) throw Error("rgb2spec: LU decomposition failed");
+        double x[3];
+        LUPSolve(J, P, residual, 3, x);
+        double r = 0.0;
+        for (int j = 0; j < 3; ++j) {
+            coeffs[j] -= x[j];
+            r += residual[j] * residual[j];
+        }
+        double mx = std::max(std::max(coeffs[0], coeffs[1]), coeffs[2]);
+        if (mx > 200)
+            for (int j = 0; j < 3; ++j) coeffs[j] *= 200 / mx;
+        if (r < 1e-6) break;
+    }
+}
+
+double smoothstep(double x) { return x * x * (3.0 - 2.0 * x); }
+}  // namespace
+
+float RGB2SpecZNode(int k) { return (float)smoothstep(smoothstep(k / double(kRes - 1))); }
+
+std::vector<float> RGB2SpecColumn(int l, int j, int i) {
+    // rgb2spec_opt.cpp:825-875 for one (l, j, i): two warm-started chains over k
+    const OptTables &t = GetOptTables();
+    std::vector<float> out(kRes * 3);
+    const double y = j / double(kRes - 1), x = i / double(kRes - 1);
+    auto store = [&](int k, const double *coeffs) {
+        double c0 = 360.0, c1 = 1.0 / (830.0 - 360.0);
+        double A = coeffs[0], B = coeffs[1], C = coeffs[2];
+        out[3 * k + 0] = float(A * (c1 * c1));
+        out[3 * k + 1] = float(B * c1 - 2 * A * c0 * (c1 * c1));
+        out[3 * k + 2] = float(C - B * c0 * c1 + A * ((c0 * c1) * (c0 * c1)));
+    };
+    double coeffs[3], rgb[3];
+    int start = kRes / 5;
+    memset(coeffs, 0, sizeof(coeffs));
+    for (int k = start; k < kRes; ++k) {
+        double b = (double)RGB2SpecZNode(k);
+        rgb[l] = b;
+        rgb[(l + 1) % 3] = x * b;
+        rgb[(l + 2) % 3] = y * b;
+        gauss_newton(t, rgb, coeffs);
+        store(k, coeffs);
+    }
+    memset(coeffs, 0, sizeof(coeffs));
+    for (int k = start; k >= 0; --k) {
+        double b = (double)RGB2SpecZNode(k);
+        rgb[l] = b;
+        rgb[(l + 1) % 3] = x * b;
+        rgb[(l + 2) % 3] = y * b;
+        gauss_newton(t, rgb, coeffs);
+        store(k, coeffs);
+    }
+    return out;
+}
+
+static const std::vector<float> &CachedColumn(int l, int j, int i) {
+    static std::mutex mu;
+    static std::map<int, std::vector<float>> cache;
+    std::lock_guard<std::mutex> lock(mu);
+    int key = (l * kRes + j) * kRes + i;
+    auto it = cache.find(key);
+    if (it == cache.end()) it = cache.emplace(key, RGB2SpecColumn(l, j, i)).first;
+    return it->second;
+}
+
+std::array<float, 3> RGBToSigmoidCoeffs(float r, float g, float b) {
+    // RGBColorSpace::ToRGBCoeffs -> RGBToSpectrumTable::operator() (util/color.cpp:36-75)
+    float rgb[3] = {std::max(0.f, r), std::max(0.f, g), std::max(0.f, b)};
+    if (rgb[0] == rgb[1] && rgb[1] == rgb[2])
+        return {0.f, 0.f, (rgb[0] - .5f) / std::sqrt(rgb[0] * (1 - rgb[0]))};
+    int maxc = (rgb[0] > rgb[1]) ? ((rgb[0] > rgb[2]) ? 0 : 2) : ((rgb[1] > rgb[2]) ? 1 : 2);
+    float z = rgb[maxc];
+    float x = rgb[(maxc + 1) % 3] * (kRes - 1) / z;
+    float y = rgb[(maxc + 2) % 3] * (kRes - 1) / z;
+    int xi = std::min((int)x, kRes - 2), yi = std::min((int)y, kRes - 2);
+    float zNodes[kRes];
+    for (int k = 0; k < kRes; ++k) zNodes[k] = RGB2SpecZNode(k);
+    int zi;
+    {
+        int size = kRes - 2, first = 1;
+        while (size > 0) {
+            int half = size >> 1, middle = first + half;
+            bool pred = zNodes[middle] < z;
+            first = pred ? middle + 1 : first;
+            size = pred ? size - (half + 1) : half;
+        }
+        zi = std::min(std::max(first - 1, 0), kRes - 2);
+    }
+    float dx = x - xi, dy = y - yi, dz = (z - zNodes[zi]) / (zNodes[zi + 1] - zNodes[zi]);
+    std::array<float, 3> c;
+    for (int ci = 0; ci < 3; ++ci) {
+        auto co = [&](int ddx, int ddy, int ddz) {
+            const std::vector<float> &col = CachedColumn(maxc, yi + ddy, xi + ddx);
+            return col[3 * (zi + ddz) + ci];
+        };
+        c[ci] = Lerpf(dz, Lerpf(dy, Lerpf(dx, co(0, 0, 0), co(1, 0, 0)), Lerpf(dx, co(0, 1, 0), co(1, 1, 0))),
+                      Lerpf(dy, Lerpf(dx, co(0, 0, 1), co(1, 0, 1)), Lerpf(dx, co(0, 1, 1), co(1, 1, 1))));
+    }
+    return c;
+}
+
+std::array<float, 311> DenseRGBIlluminant(float r, float g, float b) {
+    // DenselySampledSpectrum(RGBIlluminantSpectrum(sRGB, rgb)) (util/spectrum.cpp:246-251)
+    const SpectralData &d = GetSpectralData();
+    float m = std::max({r, g, b});
+    float scale = 2 * m;
+    std::array<float, 3> c = scale ? RGBToSigmoidCoeffs(r / scale, g / scale, b / scale)
+                                   : RGBToSigmoidCoeffs(0, 0, 0);
+    std::array<float, 311> out;
+    for (int l = 395; l <= 705; ++l) {
+        float lambda = (float)l;
+        out[l - 395] = scale * SigmoidPolynomial(c[0], c[1], c[2], lambda) * d.denseD65[DenseOffset(lambda)];
+    }
+    return out;
+}
+
+}  // namespace pbrt_amd

@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Extract the standard CIE tables the renderer needs into a JSON data file.
+
+The data are the public CIE 1931 2-degree colour matching functions (1 nm, 360-830 nm),
+the CIE D65 relative SPD, and the 5 nm CIE/D65 tables plus sRGB<->XYZ matrices that
+pbrt's RGB->spectrum optimiser (cmd/rgb2spec_opt.cpp) integrates against.  They are
+measurement data, not code: this script only parses the numeric literals out of the
+reference's sources
+
+    src/pbrt/util/spectrum.cpp   CIE_X / CIE_Y / CIE_Z / CIE_lambda (:273-567),
+                                 CIE_Illum_D6500 (:770)
+    src/pbrt/cmd/rgb2spec_opt.cpp cie_x / cie_y / cie_z / cie_d65 (:46-128),
+                                 xyz_to_srgb / srgb_to_xyz (:191-197)
+
+and writes pbrt-v4_amd/data/spectral_data.json, which is committed.  Run it only in a
+container that has /root/reference; the GPU box uses the committed JSON.
+"""
+import json
+import re
+import sys
+from pathlib import Path
+
+REF = Path("/root/reference/src/pbrt")
+OUT = Path(__file__).resolve().parents[1] / "pbrt-v4_amd" / "data" / "spectral_data.json"
+
+NUM = r"[-+]?(?:\d+\.?\d*|\.\d+)(?:[eE][-+]?\d+)?"
+
+
+def array_body(text, name):
+    m = re.search(r"(?:const\s+(?:Float|double)\s+)" + re.escape(name) + r"\s*(?:\[[^\]]*\]\s*)+=\s*\{", text)
+    if not m:
+        raise SystemExit(f"array {name} not found")
+    depth, i = 1, m.end()
+    while depth:
+        c = text[i]
+        depth += c == "{"
+        depth -= c == "}"
+        i += 1
+    return text[m.end():i - 1]
+
+
+def numbers(body):
+    body = re.sub(r"//[^\n]*", "", body)
+    return [float(x) for x in re.findall(NUM, body)]
+
+
+def main():
+    spec = (REF / "util" / "spectrum.cpp").read_text()
+    opt = (REF / "cmd" / "rgb2spec_opt.cpp").read_text()
+    data = {}
+    for name in ("CIE_X", "CIE_Y", "CIE_Z", "CIE_lambda"):
+        data[name] = numbers(array_body(spec, name))
+        assert len(data[name]) == 471, (name, len(data[name]))
+    d65 = numbers(array_body(spec, "CIE_Illum_D6500"))
+    data["CIE_Illum_D6500_interleaved"] = d65
+    # rgb2spec_opt tables: the N(x) macro divides by a constant; keep raw and the divisor
+    for name in ("cie_x", "cie_y", "cie_z"):
+        data["opt_" + name] = numbers(array_body(opt, name))
+        assert len(data["opt_" + name]) == 95
+    body = array_body(opt, "cie_d65")
+    raw = [float(x) for x in re.findall(r"N\((" + NUM + r")\)", body)]
+    assert len(raw) == 95
+    div = float(re.search(r"#define N\(x\) \(x / (" + NUM + r")\)", opt[:opt.find("cie_d65")][-400:]).group(1))
+    data["opt_cie_d65_raw"] = raw
+    data["opt_cie_d65_divisor"] = div
+    for name in ("xyz_to_srgb", "srgb_to_xyz"):
+        data["opt_" + name] = numbers(array_body(opt, name))
+        assert len(data["opt_" + name]) == 9
+    OUT.parent.mkdir(parents=True, exist_ok=True)
+    OUT.write_text(json.dumps(data))
+    print("wrote", OUT, {k: len(v) if isinstance(v, list) else v for k, v in data.items()})
+
+
+
+
+def write_text(data, path):
+    """Plain 'name count v0 v1 ...' lines for the C++ loader (no JSON parser needed)."""
+    with open(path, "w") as f:
+        for k, v in data.items():
+            vals = v if isinstance(v, list) else [v]
+            f.write(k + " " + str(len(vals)) + " " + " ".join(repr(float(x)) for x in vals) + "\n")
+
+
+if __name__ == "__main__":
+    main()
+    write_text(json.loads(OUT.read_text()), OUT.with_suffix(".txt"))

@@ -1,0 +1,1247 @@
+// oracle/oracle.cpp — TEST INFRASTRUCTURE ONLY.  CPU restatement of pbrt-v4's wavefront
+// path integrator (equivalently the CPU VolPathIntegrator for medium-free, non-specular
+// paths: identical sample-dimension schedule, MIS and RR) for the scene
+// subset the MI355X path supports.  Only tests/, __graft_entry__.smoke() and bench.py's
+// cpu_baseline leg load this library, as the checker; the product never links it.
+//
+// It is written independently of pbrt-v4_amd/csrc: scalar, one path at a time, full
+// 31-wavelength SampledSpectrum arithmetic for beta, r_u, r_l and L, spectral L converted
+// to sensor RGB once per sample exactly as RGBFilm::AddSample does, its own BVH, its own
+// Halton digit-permutation tables.  It consumes the loaded scene through the flat C view
+// (pbrt_scene_flat) so that the scene description is identical on both sides.
+//
+// Reference functions restated (file:line in /root/reference/src/pbrt):
+//   WavefrontPathIntegrator::Render / stages    wavefront/integrator.cpp:290-573,
+//     wavefront/camera.cpp:31-80, samples.cpp:29-66, surfscatter.cpp:57-328,
+//     intersect.h:16-156, film.cpp:13-39
+//   HaltonSampler                              samplers.h:33-141, samplers.cpp:32-52,
+//     util/lowdiscrepancy.h:25-140, util/hash.h:19-106, util/math.h:728-756
+//   IntersectTriangle / InteractionFromIntersection / Sample / PDF
+//                                              shapes.cpp:172-273, shapes.h:884-1174
+//   sampling                                   util/sampling.h:79-420, util/sampling.cpp:28-175
+//   BVHLightSampler::Sample / PMF, Importance  lightsamplers.h:130-403
+//   DiffuseBxDF / BSDF                         bxdfs.h:30-82, bsdf.h:60-135
+//   DiffuseAreaLight::L / SampleLi / PDF_Li    lights.h:443-480, lights.cpp:743-781
+//   RGBFilm::AddSample / PixelSensor           film.h:95-100, 241-258
+//   OffsetRayOrigin / SpawnRay(To)             ray.h:78-111
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "../include/pbrt_amd.h"
+
+namespace oracle {
+
+typedef float Float;
+static constexpr int NS = 31;
+static constexpr Float Pi = 3.14159265358979323846f, InvPi = 0.31830988618379067154f;
+static constexpr Float PiOver2 = 1.57079632679489661923f, PiOver4 = 0.78539816339744830961f;
+static constexpr Float Infinity = std::numeric_limits<Float>::infinity();
+static constexpr Float MachineEpsilon = std::numeric_limits<Float>::epsilon() * 0.5f;
+static constexpr Float OneMinusEpsilon = 0x1.fffffep-1f;
+static constexpr Float ShadowEpsilon = 0.0001f;
+static constexpr Float LambdaMin = 395, LambdaMax = 705;
+
+static inline constexpr Float gamma(int n) { return (n * MachineEpsilon) / (1 - n * MachineEpsilon); }
+static inline Float Sqr(Float x) { return x * x; }
+static inline Float Clamp(Float v, Float lo, Float hi) { return v < lo ? lo : (v > hi ? hi : v); }
+static inline Float Lerp(Float t, Float a, Float b) { return (1 - t) * a + t * b; }
+static inline Float SafeSqrt(Float x) { return std::sqrt(std::max<Float>(0.f, x)); }
+static inline Float SafeASin(Float x) { return std::asin(Clamp(x, -1, 1)); }
+static inline Float SafeACos(Float x) { return std::acos(Clamp(x, -1, 1)); }
+static inline Float DifferenceOfProducts(Float a, Float b, Float c, Float d) {
+    Float cd = c * d;
+    return std::fma(a, b, -cd) + std::fma(-c, d, cd);
+}
+static inline Float SumOfProducts(Float a, Float b, Float c, Float d) {
+    Float cd = c * d;
+    return std::fma(a, b, cd) + std::fma(c, d, -cd);
+}
+static inline uint32_t FloatToBits(Float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    return u;
+}
+static inline Float BitsToFloat(uint32_t u) {
+    Float f;
+    std::memcpy(&f, &u, 4);
+    return f;
+}
+static inline Float NextFloatUp(Float v) {
+    if (std::isinf(v) && v > 0.f) return v;
+    if (v == -0.f) v = 0.f;
+    uint32_t ui = FloatToBits(v);
+    if (v >= 0) ++ui;
+    else --ui;
+    return BitsToFloat(ui);
+}
+static inline Float NextFloatDown(Float v) {
+    if (std::isinf(v) && v < 0.f) return v;
+    if (v == 0.f) v = -0.f;
+    uint32_t ui = FloatToBits(v);
+    if (v > 0) --ui;
+    else ++ui;
+    return BitsToFloat(ui);
+}
+
+struct Vec {
+    Float x = 0, y = 0, z = 0;
+    Vec() = default;
+    Vec(Float a, Float b, Float c) : x(a), y(b), z(c) {}
+    Float operator[](int i) const { return i == 0 ? x : (i == 1 ? y : z); }
+    Float &operator[](int i) { return i == 0 ? x : (i == 1 ? y : z); }
+    Vec operator+(Vec o) const { return {x + o.x, y + o.y, z + o.z}; }
+    Vec operator-(Vec o) const { return {x - o.x, y - o.y, z - o.z}; }
+    Vec operator-() const { return {-x, -y, -z}; }
+    Vec operator*(Float s) const { return {x * s, y * s, z * s}; }
+    Vec operator/(Float s) const { return {x / s, y / s, z / s}; }
+    bool operator==(Vec o) const { return x == o.x && y == o.y && z == o.z; }
+    bool operator!=(Vec o) const { return !(*this == o); }
+};
+static inline Vec operator*(Float s, Vec v) { return {s * v.x, s * v.y, s * v.z}; }
+static inline Float Dot(Vec a, Vec b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static inline Float AbsDot(Vec a, Vec b) { return std::abs(Dot(a, b)); }
+static inline Vec Cross(Vec v, Vec w) {
+    return {DifferenceOfProducts(v.y, w.z, v.z, w.y), DifferenceOfProducts(v.z, w.x, v.x, w.z),
+            DifferenceOfProducts(v.x, w.y, v.y, w.x)};
+}
+static inline Float LengthSquared(Vec v) { return Sqr(v.x) + Sqr(v.y) + Sqr(v.z); }
+static inline Float Length(Vec v) { return std::sqrt(LengthSquared(v)); }
+static inline Vec Normalize(Vec v) { return v / Length(v); }
+static inline Vec Abs(Vec v) { return {std::abs(v.x), std::abs(v.y), std::abs(v.z)}; }
+static inline Float DistanceSquared(Vec a, Vec b) { return LengthSquared(a - b); }
+static inline Float MaxComp(Vec v) { return std::max(v.x, std::max(v.y, v.z)); }
+static inline int MaxCompIndex(Vec v) { return (v.x > v.y) ? ((v.x > v.z) ? 0 : 2) : ((v.y > v.z) ? 1 : 2); }
+static inline Vec GramSchmidt(Vec v, Vec w) { return v - Dot(v, w) * w; }
+static inline Float AngleBetween(Vec v1, Vec v2) {
+    if (Dot(v1, v2) < 0) return Pi - 2 * SafeASin(Length(v1 + v2) / 2);
+    return 2 * SafeASin(Length(v2 - v1) / 2);
+}
+static inline void CoordinateSystem(Vec v1, Vec *v2, Vec *v3) {
+    Float sign = std::copysign(Float(1), v1.z);
+    Float a = -1 / (sign + v1.z);
+    Float b = v1.x * v1.y * a;
+    *v2 = Vec(1 + sign * Sqr(v1.x) * a, sign * b, -sign * v1.x);
+    *v3 = Vec(b, sign + Sqr(v1.y) * a, -v1.y);
+}
+
+// ---------------------------------------------------------------- spectra
+struct Spectrum {
+    Float v[NS];
+    Spectrum() { std::fill(v, v + NS, 0.f); }
+    explicit Spectrum(Float c) { std::fill(v, v + NS, c); }
+    Float &operator[](int i) { return v[i]; }
+    Float operator[](int i) const { return v[i]; }
+    Spectrum operator+(const Spectrum &o) const {
+        Spectrum r = *this;
+        for (int i = 0; i < NS; ++i) r.v[i] += o.v[i];
+        return r;
+    }
+    Spectrum operator*(const Spectrum &o) const {
+        Spectrum r = *this;
+        for (int i = 0; i < NS; ++i) r.v[i] *= o.v[i];
+        return r;
+    }
+    Spectrum operator*(Float a) const {
+        Spectrum r = *this;
+        for (int i = 0; i < NS; ++i) r.v[i] *= a;
+        return r;
+    }
+    Spectrum operator/(Float a) const {
+        Spectrum r = *this;
+        for (int i = 0; i < NS; ++i) r.v[i] /= a;
+        return r;
+    }
+    Spectrum operator/(const Spectrum &o) const {
+        Spectrum r = *this;
+        for (int i = 0; i < NS; ++i) r.v[i] /= o.v[i];
+        return r;
+    }
+    explicit operator bool() const {
+        for (int i = 0; i < NS; ++i)
+            if (v[i] != 0) return true;
+        return false;
+    }
+    Float Max() const {
+        Float m = v[0];
+        for (int i = 1; i < NS; ++i) m = std::max(m, v[i]);
+        return m;
+    }
+    Float Average() const {
+        Float s = v[0];
+        for (int i = 1; i < NS; ++i) s += v[i];
+        return s / NS;
+    }
+};
+
+struct Wavelengths {
+    Float lambda[NS], pdf[NS];
+    static Wavelengths SampleUniform(Float u) {  // util/spectrum.h:318 (fork: uniform)
+        Wavelengths w;
+        w.lambda[0] = Lerp(u, LambdaMin, LambdaMax);
+        Float delta = (LambdaMax - LambdaMin) / NS;
+        for (int i = 1; i < NS; ++i) {
+            w.lambda[i] = w.lambda[i - 1] + delta;
+            if (w.lambda[i] > LambdaMax) w.lambda[i] = LambdaMin + (w.lambda[i] - LambdaMax);
+        }
+        for (int i = 0; i < NS; ++i) w.pdf[i] = 1 / (LambdaMax - LambdaMin);
+        return w;
+    }
+};
+
+static inline Spectrum SampleDense(const float *dense, const Wavelengths &w) {
+    Spectrum s;
+    for (int i = 0; i < NS; ++i) {
+        long off = std::lround(w.lambda[i]) - 395;
+        s[i] = (off < 0 || off >= 311) ? 0 : dense[off];
+    }
+    return s;
+}
+
+static inline Float Sigmoid(Float c0, Float c1, Float c2, Float lambda) {
+    Float x = std::fma(lambda, std::fma(lambda, c0, c1), c2);
+    if (std::isinf(x)) return x > 0 ? 1 : 0;
+    return .5f + x / (2 * std::sqrt(1 + Sqr(x)));
+}
+
+// ---------------------------------------------------------------- Halton
+static uint64_t Murmur64A(const unsigned char *key, size_t len, uint64_t seed) {
+    const uint64_t m = 0xc6a4a7935bd1e995ull;
+    const int r = 47;
+    uint64_t h = seed ^ (len * m);
+    const unsigned char *end = key + 8 * (len / 8);
+    while (key != end) {
+        uint64_t k;
+        std::memcpy(&k, key, 8);
+        key += 8;
+        k *= m;
+        k ^= k >> r;
+        k *= m;
+        h ^= k;
+        h *= m;
+    }
+    switch (len & 7) {
+    case 7: h ^= uint64_t(key[6]) << 48; [[fallthrough]];
+    case 6: h ^= uint64_t(key[5]) << 40; [[fallthrough]];
+    case 5: h ^= uint64_t(key[4]) << 32; [[fallthrough]];
+    case 4: h ^= uint64_t(key[3]) << 24; [[fallthrough]];
+    case 3: h ^= uint64_t(key[2]) << 16; [[fallthrough]];
+    case 2: h ^= uint64_t(key[1]) << 8; [[fallthrough]];
+    case 1: h ^= uint64_t(key[0]); h *= m;
+    }
+    h ^= h >> r;
+    h *= m;
+    h ^= h >> r;
+    return h;
+}
+static int PermElem(uint32_t i, uint32_t l, uint32_t p) {
+    uint32_t w = l - 1;
+    w |= w >> 1; w |= w >> 2; w |= w >> 4; w |= w >> 8; w |= w >> 16;
+    do {
+        i ^= p; i *= 0xe170893d; i ^= p >> 16; i ^= (i & w) >> 4; i ^= p >> 8; i *= 0x0929eb3f;
+        i ^= p >> 23; i ^= (i & w) >> 1; i *= 1 | p >> 27; i *= 0x6935fa69; i ^= (i & w) >> 11;
+        i *= 0x74dcb303; i ^= (i & w) >> 2; i *= 0x9e501cc3; i ^= (i & w) >> 2; i *= 0xc860a3df;
+        i &= w; i ^= i >> 5;
+    } while (i >= l);
+    return (i + p) % l;
+}
+
+struct DigitPerm {
+    int base = 0, nDigits = 0;
+    std::vector<uint16_t> perm;
+};
+
+struct Halton {
+    std::vector<DigitPerm> perms;
+    int baseScales[2], baseExponents[2], multInverse[2];
+    static void ExtGCD(uint64_t a, uint64_t b, int64_t *x, int64_t *y) {
+        if (b == 0) { *x = 1; *y = 0; return; }
+        int64_t d = a / b, xp, yp;
+        ExtGCD(b, a % b, &xp, &yp);
+        *x = yp;
+        *y = xp - (d * yp);
+    }
+    static int MultInv(int64_t a, int64_t n) {
+        int64_t x, y;
+        ExtGCD(a, n, &x, &y);
+        int64_t r = x % n;
+        return (int)(r < 0 ? r + n : r);
+    }
+    void Init(int xres, int yres, uint32_t seed, int nDims) {
+        std::vector<int> primes;
+        for (int n = 2; (int)primes.size() < nDims; ++n) {
+            bool ok = true;
+            for (int q : primes) {
+                if (q * q > n) break;
+                if (n % q == 0) { ok = false; break; }
+            }
+            if (ok) primes.push_back(n);
+        }
+        perms.resize(nDims);
+        for (int d = 0; d < nDims; ++d) {
+            DigitPerm &p = perms[d];
+            p.base = primes[d];
+            volatile Float invBase = (Float)1 / (Float)p.base, invBaseM = 1;
+            p.nDigits = 0;
+            while (1 - (Float)(p.base - 1) * invBaseM < 1) { ++p.nDigits; invBaseM = invBaseM * invBase; }
+            p.perm.resize(p.nDigits * p.base);
+            for (int di = 0; di < p.nDigits; ++di) {
+                unsigned char buf[12];
+                int b = p.base, dd = di;
+                std::memcpy(buf, &b, 4);
+                std::memcpy(buf + 4, &dd, 4);
+                std::memcpy(buf + 8, &seed, 4);
+                uint64_t dseed = Murmur64A(buf, 12, 0);
+                for (int v = 0; v < p.base; ++v) p.perm[di * p.base + v] = (uint16_t)PermElem(v, p.base, (uint32_t)dseed);
+            }
+        }
+        int res[2] = {xres, yres};
+        for (int i = 0; i < 2; ++i) {
+            int base = i == 0 ? 2 : 3, scale = 1, exp = 0;
+            while (scale < std::min(res[i], 128)) { scale *= base; ++exp; }
+            baseScales[i] = scale;
+            baseExponents[i] = exp;
+        }
+        multInverse[0] = MultInv(baseScales[1], baseScales[0]);
+        multInverse[1] = MultInv(baseScales[0], baseScales[1]);
+    }
+};
+
+struct HaltonState {
+    const Halton *h;
+    uint64_t index;
+    int dimension;
+    static uint64_t InvRadInv(uint64_t inverse, int base, int nDigits) {
+        uint64_t index = 0;
+        for (int i = 0; i < nDigits; ++i) {
+            uint64_t digit = inverse % base;
+            inverse /= base;
+            index = index * base + digit;
+        }
+        return index;
+    }
+    void Start(int px, int py, int sampleIndex, int dim) {
+        index = 0;
+        int stride = h->baseScales[0] * h->baseScales[1];
+        if (stride > 1) {
+            int pm[2] = {((px % 128) + 128) % 128, ((py % 128) + 128) % 128};
+            for (int i = 0; i < 2; ++i) {
+                uint64_t off = InvRadInv(pm[i], i == 0 ? 2 : 3, h->baseExponents[i]);
+                index += off * (stride / h->baseScales[i]) * h->multInverse[i];
+            }
+            index %= stride;
+        }
+        index += (uint64_t)sampleIndex * stride;
+        dimension = std::max(2, dim);
+    }
+    Float Sample(int dim) const {
+        const DigitPerm &p = h->perms[dim];
+        uint64_t a = index;
+        Float invBase = (Float)1 / (Float)p.base, invBaseM = 1;
+        uint64_t rev = 0;
+        for (int di = 0; di < p.nDigits; ++di) {
+            uint64_t next = a / p.base;
+            int dv = (int)(a - next * p.base);
+            rev = rev * p.base + p.perm[di * p.base + dv];
+            invBaseM *= invBase;
+            a = next;
+        }
+        return std::min(invBaseM * rev, OneMinusEpsilon);
+    }
+    Float Get1D() {
+        if (dimension >= (int)h->perms.size()) dimension = 2;
+        return Sample(dimension++);
+    }
+    void Get2D(Float *a, Float *b) {
+        if (dimension + 1 >= (int)h->perms.size()) dimension = 2;
+        int d = dimension;
+        dimension += 2;
+        *a = Sample(d);
+        *b = Sample(d + 1);
+    }
+    static Float RadInv(int base, uint64_t a) {
+        uint64_t limit = ~0ull / base - base;
+        Float invBase = (Float)1 / (Float)base, invBaseM = 1;
+        uint64_t rev = 0;
+        while (a && rev < limit) {
+            uint64_t next = a / base;
+            rev = rev * base + (a - next * base);
+            invBaseM *= invBase;
+            a = next;
+        }
+        return std::min(rev * invBaseM, OneMinusEpsilon);
+    }
+    void Pixel2D(Float *x, Float *y) const {
+        *x = RadInv(2, index >> h->baseExponents[0]);
+        *y = RadInv(3, index / h->baseScales[1]);
+    }
+};
+
+// ---------------------------------------------------------------- geometry
+struct TriIsect {
+    Float b0, b1, b2, t;
+};
+static bool IntersectTriangle(Vec o, Vec dir, Float tMax, Vec p0, Vec p1, Vec p2, TriIsect *out) {
+    if (LengthSquared(Cross(p2 - p0, p1 - p0)) == 0) return false;
+    Vec p0t = p0 - o, p1t = p1 - o, p2t = p2 - o;
+    int kz = MaxCompIndex(Abs(dir));
+    int kx = kz + 1 == 3 ? 0 : kz + 1;
+    int ky = kx + 1 == 3 ? 0 : kx + 1;
+    Vec d(dir[kx], dir[ky], dir[kz]);
+    p0t = Vec(p0t[kx], p0t[ky], p0t[kz]);
+    p1t = Vec(p1t[kx], p1t[ky], p1t[kz]);
+    p2t = Vec(p2t[kx], p2t[ky], p2t[kz]);
+    Float Sx = -d.x / d.z, Sy = -d.y / d.z, Sz = 1 / d.z;
+    p0t.x += Sx * p0t.z; p0t.y += Sy * p0t.z;
+    p1t.x += Sx * p1t.z; p1t.y += Sy * p1t.z;
+    p2t.x += Sx * p2t.z; p2t.y += Sy * p2t.z;
+    Float e0 = DifferenceOfProducts(p1t.x, p2t.y, p1t.y, p2t.x);
+    Float e1 = DifferenceOfProducts(p2t.x, p0t.y, p2t.y, p0t.x);
+    Float e2 = DifferenceOfProducts(p0t.x, p1t.y, p0t.y, p1t.x);
+    if (e0 == 0.0f || e1 == 0.0f || e2 == 0.0f) {
+        double a = (double)p2t.x * (double)p1t.y, b = (double)p2t.y * (double)p1t.x;
+        e0 = (float)(b - a);
+        double c = (double)p0t.x * (double)p2t.y, dd = (double)p0t.y * (double)p2t.x;
+        e1 = (float)(dd - c);
+        double e = (double)p1t.x * (double)p0t.y, f = (double)p1t.y * (double)p0t.x;
+        e2 = (float)(f - e);
+    }
+    if ((e0 < 0 || e1 < 0 || e2 < 0) && (e0 > 0 || e1 > 0 || e2 > 0)) return false;
+    Float det = e0 + e1 + e2;
+    if (det == 0) return false;
+    p0t.z *= Sz; p1t.z *= Sz; p2t.z *= Sz;
+    Float tScaled = e0 * p0t.z + e1 * p1t.z + e2 * p2t.z;
+    if (det < 0 && (tScaled >= 0 || tScaled < tMax * det)) return false;
+    if (det > 0 && (tScaled <= 0 || tScaled > tMax * det)) return false;
+    Float invDet = 1 / det;
+    Float b0 = e0 * invDet, b1 = e1 * invDet, b2 = e2 * invDet, t = tScaled * invDet;
+    Float maxZt = MaxComp(Abs(Vec(p0t.z, p1t.z, p2t.z)));
+    Float deltaZ = gamma(3) * maxZt;
+    Float maxXt = MaxComp(Abs(Vec(p0t.x, p1t.x, p2t.x)));
+    Float maxYt = MaxComp(Abs(Vec(p0t.y, p1t.y, p2t.y)));
+    Float deltaX = gamma(5) * (maxXt + maxZt), deltaY = gamma(5) * (maxYt + maxZt);
+    Float deltaE = 2 * (gamma(2) * maxXt * maxYt + deltaY * maxXt + deltaX * maxYt);
+    Float maxE = MaxComp(Abs(Vec(e0, e1, e2)));
+    Float deltaT = 3 * (gamma(3) * maxE * maxZt + deltaE * maxZt + deltaZ * maxE) * std::abs(invDet);
+    if (t <= deltaT) return false;
+    *out = {b0, b1, b2, t};
+    return true;
+}
+
+static Vec OffsetRayOrigin(Vec p, Vec err, Vec n, Vec w) {
+    Float d = Dot(Abs(n), err);
+    Vec offset = d * n;
+    if (Dot(w, n) < 0) offset = -offset;
+    Vec po = p + offset;
+    for (int i = 0; i < 3; ++i) {
+        if (offset[i] > 0) po[i] = NextFloatUp(po[i]);
+        else if (offset[i] < 0) po[i] = NextFloatDown(po[i]);
+    }
+    return po;
+}
+
+struct Scene;
+
+struct Interaction {
+    Vec p, err, n, ns, dpdu, wo;
+    int prim = -1;
+};
+
+// shapes.h:884-1010 for meshes without n/s/uv
+static Interaction TriangleInteraction(Vec p0, Vec p1, Vec p2, bool flip, TriIsect ti, Vec rayD) {
+    Interaction si;
+    const Float uv[3][2] = {{0, 0}, {1, 0}, {1, 1}};
+    Float duv02[2] = {uv[0][0] - uv[2][0], uv[0][1] - uv[2][1]};
+    Float duv12[2] = {uv[1][0] - uv[2][0], uv[1][1] - uv[2][1]};
+    Vec dp02 = p0 - p2, dp12 = p1 - p2;
+    Float determinant = DifferenceOfProducts(duv02[0], duv12[1], duv02[1], duv12[0]);
+    Vec dpdu, dpdv;
+    bool degenerate = std::abs(determinant) < 1e-9f;
+    if (!degenerate) {
+        Float invdet = 1 / determinant;
+        for (int k = 0; k < 3; ++k) {
+            dpdu[k] = DifferenceOfProducts(duv12[1], dp02[k], duv02[1], dp12[k]) * invdet;
+            dpdv[k] = DifferenceOfProducts(duv02[0], dp12[k], duv12[0], dp02[k]) * invdet;
+        }
+    }
+    if (degenerate || LengthSquared(Cross(dpdu, dpdv)) == 0) CoordinateSystem(Normalize(Cross(p2 - p0, p1 - p0)), &dpdu, &dpdv);
+    si.p = ti.b0 * p0 + ti.b1 * p1 + ti.b2 * p2;
+    si.err = gamma(7) * (Abs(ti.b0 * p0) + Abs(ti.b1 * p1) + Abs(ti.b2 * p2));
+    si.n = Normalize(Cross(dp02, dp12));
+    if (flip) si.n = -si.n;
+    si.ns = si.n;
+    si.dpdu = dpdu;
+    si.wo = Normalize(-rayD);
+    return si;
+}
+
+// simple binned-SAH BVH2 over the scene triangles (oracle-side; any correct BVH gives the
+// same closest hit up to exact-t ties)
+struct BVHNode {
+    Vec mn, mx;
+    int left = -1, right = -1, first = 0, count = 0;
+};
+
+struct Scene {
+    const pbrt_scene_flat *f;
+    std::vector<Vec> v;
+    std::vector<int> tri;  // 3 per triangle
+    std::vector<BVHNode> nodes;
+    std::vector<int> order;
+    Halton halton;
+    int xres, yres, px0, px1, py0, py1, maxDepth;
+    Float frx, fry;
+    Vec P(int t, int k) const { return v[tri[3 * t + k]]; }
+
+    int Build(int start, int end, std::vector<Vec> &cent) {
+        BVHNode n;
+        n.mn = Vec(Infinity, Infinity, Infinity);
+        n.mx = Vec(-Infinity, -Infinity, -Infinity);
+        Vec cmn = n.mn, cmx = n.mx;
+        for (int i = start; i < end; ++i) {
+            int t = order[i];
+            for (int k = 0; k < 3; ++k) {
+                Vec p = P(t, k);
+                for (int a = 0; a < 3; ++a) {
+                    n.mn[a] = std::min(n.mn[a], p[a]);
+                    n.mx[a] = std::max(n.mx[a], p[a]);
+                }
+            }
+            for (int a = 0; a < 3; ++a) {
+                cmn[a] = std::min(cmn[a], cent[t][a]);
+                cmx[a] = std::max(cmx[a], cent[t][a]);
+            }
+        }
+        int idx = (int)nodes.size();
+        nodes.push_back(n);
+        if (end - start <= 4) {
+            nodes[idx].first = start;
+            nodes[idx].count = end - start;
+            return idx;
+        }
+        int axis = MaxCompIndex(cmx - cmn);
+        int mid = (start + end) / 2;
+        std::nth_element(order.begin() + start, order.begin() + mid, order.begin() + end,
+                         [&](int a, int b) { return cent[a][axis] < cent[b][axis]; });
+        int l = Build(start, mid, cent), r = Build(mid, end, cent);
+        nodes[idx].left = l;
+        nodes[idx].right = r;
+        return idx;
+    }
+
+    void Init(const pbrt_scene_flat *flat, const pbrt_scene_info *info) {
+        f = flat;
+        for (int i = 0; i < f->n_vertices; ++i) v.push_back(Vec(f->vertices[3 * i], f->vertices[3 * i + 1], f->vertices[3 * i + 2]));
+        tri.assign(f->triangles, f->triangles + 3 * f->n_triangles);
+        std::vector<Vec> cent(f->n_triangles);
+        order.resize(f->n_triangles);
+        for (int t = 0; t < f->n_triangles; ++t) {
+            order[t] = t;
+            cent[t] = (P(t, 0) + P(t, 1) + P(t, 2)) / 3.f;
+        }
+        if (f->n_triangles) Build(0, f->n_triangles, cent);
+        xres = info->xres;
+        yres = info->yres;
+        px0 = info->px0;
+        px1 = info->px1;
+        py0 = info->py0;
+        py1 = info->py1;
+        maxDepth = info->max_depth;
+        frx = info->filter_radius_x;
+        fry = info->filter_radius_y;
+        halton.Init(xres, yres, (uint32_t)info->seed, std::max(f->n_dims, 7 * maxDepth + 7));
+    }
+
+    static bool BoxHit(const BVHNode &n, Vec o, Vec invDir, const int neg[3], Float rayTMax) {
+        // util/vecmath.h:1576-1611
+        Float b[2][3] = {{n.mn.x, n.mn.y, n.mn.z}, {n.mx.x, n.mx.y, n.mx.z}};
+        Float tMin = (b[neg[0]][0] - o.x) * invDir.x;
+        Float tMax = (b[1 - neg[0]][0] - o.x) * invDir.x;
+        Float tyMin = (b[neg[1]][1] - o.y) * invDir.y;
+        Float tyMax = (b[1 - neg[1]][1] - o.y) * invDir.y;
+        tMax *= 1 + 2 * gamma(3);
+        tyMax *= 1 + 2 * gamma(3);
+        if (tMin > tyMax || tyMin > tMax) return false;
+        if (tyMin > tMin) tMin = tyMin;
+        if (tyMax < tMax) tMax = tyMax;
+        Float tzMin = (b[neg[2]][2] - o.z) * invDir.z;
+        Float tzMax = (b[1 - neg[2]][2] - o.z) * invDir.z;
+        tzMax *= 1 + 2 * gamma(3);
+        if (tMin > tzMax || tzMin > tMax) return false;
+        if (tzMin > tMin) tMin = tzMin;
+        if (tzMax < tMax) tMax = tzMax;
+        return (tMin < rayTMax) && (tMax > 0);
+    }
+
+    int Intersect(Vec o, Vec d, Float tMax, TriIsect *hit, bool anyHit) const {
+        if (nodes.empty()) return -1;
+        Vec invDir(1 / d.x, 1 / d.y, 1 / d.z);
+        int neg[3] = {invDir.x < 0, invDir.y < 0, invDir.z < 0};
+        int stack[128], sp = 0, best = -1;
+        stack[sp++] = 0;
+        while (sp) {
+            const BVHNode &n = nodes[stack[--sp]];
+            if (!BoxHit(n, o, invDir, neg, tMax)) continue;
+            if (n.left < 0) {
+                for (int i = n.first; i < n.first + n.count; ++i) {
+                    int t = order[i];
+                    TriIsect ti;
+                    if (IntersectTriangle(o, d, tMax, P(t, 0), P(t, 1), P(t, 2), &ti)) {
+                        if (anyHit) return t;
+                        tMax = ti.t;
+                        *hit = ti;
+                        best = t;
+                    }
+                }
+            } else {
+                stack[sp++] = n.left;
+                stack[sp++] = n.right;
+            }
+        }
+        return best;
+    }
+};
+
+// ---------------------------------------------------------------- sampling
+static void SampleUniformDiskConcentric(Float u0, Float u1, Float *x, Float *y) {
+    Float ox = 2 * u0 - 1, oy = 2 * u1 - 1;
+    if (ox == 0 && oy == 0) { *x = 0; *y = 0; return; }
+    Float theta, r;
+    if (std::abs(ox) > std::abs(oy)) { r = ox; theta = PiOver4 * (oy / ox); }
+    else { r = oy; theta = PiOver2 - PiOver4 * (ox / oy); }
+    *x = r * std::cos(theta);
+    *y = r * std::sin(theta);
+}
+static Vec SampleCosineHemisphere(Float u0, Float u1) {
+    Float x, y;
+    SampleUniformDiskConcentric(u0, u1, &x, &y);
+    return Vec(x, y, SafeSqrt(1 - Sqr(x) - Sqr(y)));
+}
+static Float SampleLinear(Float u, Float a, Float b) {
+    if (u == 0 && a == 0) return 0;
+    Float x = u * (a + b) / (a + std::sqrt(Lerp(u, Sqr(a), Sqr(b))));
+    return std::min(x, OneMinusEpsilon);
+}
+static Float BilinearPDF(Float x, Float y, const Float w[4]) {
+    if (x < 0 || x > 1 || y < 0 || y > 1) return 0;
+    if (w[0] + w[1] + w[2] + w[3] == 0) return 1;
+    return 4 * ((1 - x) * (1 - y) * w[0] + x * (1 - y) * w[1] + (1 - x) * y * w[2] + x * y * w[3]) /
+           (w[0] + w[1] + w[2] + w[3]);
+}
+static void SampleBilinear(Float u0, Float u1, const Float w[4], Float *x, Float *y) {
+    *y = SampleLinear(u1, w[0] + w[1], w[2] + w[3]);
+    *x = SampleLinear(u0, Lerp(*y, w[0], w[2]), Lerp(*y, w[1], w[3]));
+}
+static void SampleUniformTriangle(Float u0, Float u1, Float b[3]) {
+    if (u0 < u1) { b[0] = u0 / 2; b[1] = u1 - b[0]; }
+    else { b[1] = u1 / 2; b[0] = u0 - b[1]; }
+    b[2] = 1 - b[0] - b[1];
+}
+static Float SphericalTriangleArea(Vec a, Vec b, Vec c) {
+    return std::abs(2 * std::atan2(Dot(a, Cross(b, c)), 1 + Dot(a, b) + Dot(a, c) + Dot(b, c)));
+}
+static bool SampleSphericalTriangle(Vec v0, Vec v1, Vec v2, Vec p, Float u0, Float u1, Float bary[3], Float *pdf) {
+    *pdf = 0;
+    Vec a = Normalize(v0 - p), b = Normalize(v1 - p), c = Normalize(v2 - p);
+    Vec n_ab = Cross(a, b), n_bc = Cross(b, c), n_ca = Cross(c, a);
+    if (LengthSquared(n_ab) == 0 || LengthSquared(n_bc) == 0 || LengthSquared(n_ca) == 0) {
+        bary[0] = bary[1] = bary[2] = 0;
+        return false;
+    }
+    n_ab = Normalize(n_ab); n_bc = Normalize(n_bc); n_ca = Normalize(n_ca);
+    Float alpha = AngleBetween(n_ab, -n_ca), beta = AngleBetween(n_bc, -n_ab), gam = AngleBetween(n_ca, -n_bc);
+    Float A_pi = alpha + beta + gam;
+    Float Ap_pi = Lerp(u0, Pi, A_pi);
+    Float A = A_pi - Pi;
+    *pdf = (A <= 0) ? 0 : 1 / A;
+    Float cosAlpha = std::cos(alpha), sinAlpha = std::sin(alpha);
+    Float sinPhi = std::sin(Ap_pi) * cosAlpha - std::cos(Ap_pi) * sinAlpha;
+    Float cosPhi = std::cos(Ap_pi) * cosAlpha + std::sin(Ap_pi) * sinAlpha;
+    Float k1 = cosPhi + cosAlpha, k2 = sinPhi - sinAlpha * Dot(a, b);
+    Float cosBp = (k2 + (DifferenceOfProducts(k2, cosPhi, k1, sinPhi)) * cosAlpha) /
+                  ((SumOfProducts(k2, sinPhi, k1, cosPhi)) * sinAlpha);
+    cosBp = Clamp(cosBp, -1, 1);
+    Float sinBp = SafeSqrt(1 - Sqr(cosBp));
+    Vec cp = cosBp * a + sinBp * Normalize(GramSchmidt(c, a));
+    Float cosTheta = 1 - u1 * (1 - Dot(cp, b));
+    Float sinTheta = SafeSqrt(1 - Sqr(cosTheta));
+    Vec w = cosTheta * b + sinTheta * Normalize(GramSchmidt(cp, b));
+    Vec e1 = v1 - v0, e2 = v2 - v0;
+    Vec s1 = Cross(w, e2);
+    Float divisor = Dot(s1, e1);
+    if (divisor == 0) { bary[0] = bary[1] = bary[2] = 1.f / 3.f; return true; }
+    Float inv = 1 / divisor;
+    Vec s = p - v0;
+    Float b1 = Dot(s, s1) * inv, b2 = Dot(w, Cross(s, e1)) * inv;
+    b1 = Clamp(b1, 0, 1);
+    b2 = Clamp(b2, 0, 1);
+    if (b1 + b2 > 1) { b1 /= b1 + b2; b2 /= b1 + b2; }
+    bary[0] = 1 - b1 - b2; bary[1] = b1; bary[2] = b2;
+    return true;
+}
+static void InvertSphericalTriangleSample(Vec v0, Vec v1, Vec v2, Vec p, Vec w, Float *u0, Float *u1) {
+    Vec a = Normalize(v0 - p), b = Normalize(v1 - p), c = Normalize(v2 - p);
+    Vec n_ab = Cross(a, b), n_bc = Cross(b, c), n_ca = Cross(c, a);
+    if (LengthSquared(n_ab) == 0 || LengthSquared(n_bc) == 0 || LengthSquared(n_ca) == 0) { *u0 = *u1 = 0; return; }
+    n_ab = Normalize(n_ab); n_bc = Normalize(n_bc); n_ca = Normalize(n_ca);
+    Float alpha = AngleBetween(n_ab, -n_ca), beta = AngleBetween(n_bc, -n_ab), gam = AngleBetween(n_ca, -n_bc);
+    Vec cp = Normalize(Cross(Cross(b, w), Cross(c, a)));
+    if (Dot(cp, a + c) < 0) cp = -cp;
+    Float uu0;
+    if (Dot(a, cp) > 0.99999847691f) uu0 = 0;
+    else {
+        Vec n_cpb = Cross(cp, b), n_acp = Cross(a, cp);
+        if (LengthSquared(n_cpb) == 0 || LengthSquared(n_acp) == 0) { *u0 = *u1 = 0.5f; return; }
+        n_cpb = Normalize(n_cpb);
+        n_acp = Normalize(n_acp);
+        Float Ap = alpha + AngleBetween(n_ab, n_cpb) + AngleBetween(n_acp, -n_cpb) - Pi;
+        Float A = alpha + beta + gam - Pi;
+        uu0 = Ap / A;
+    }
+    Float uu1 = (1 - Dot(w, b)) / (1 - Dot(cp, b));
+    *u0 = Clamp(uu0, 0, 1);
+    *u1 = Clamp(uu1, 0, 1);
+}
+
+// Triangle::Sample(ctx, u) -> false when pbrt returns {}
+struct ShapeSample {
+    Vec p, err, n;
+    Float pdf;
+};
+static Float TriArea(Vec p0, Vec p1, Vec p2) { return 0.5f * Length(Cross(p1 - p0, p2 - p0)); }
+static bool TriangleSample(Vec p0, Vec p1, Vec p2, bool flip, Vec ref, Vec ns, Float u0, Float u1, ShapeSample *ss) {
+    Float solidAngle = SphericalTriangleArea(Normalize(p0 - ref), Normalize(p1 - ref), Normalize(p2 - ref));
+    if (solidAngle < 3e-4f || solidAngle > 6.22f) {
+        Float b[3];
+        SampleUniformTriangle(u0, u1, b);
+        Vec p = b[0] * p0 + b[1] * p1 + b[2] * p2;
+        Vec n = Normalize(Cross(p1 - p0, p2 - p0));
+        if (flip) n = n * -1.f;
+        ss->err = gamma(6) * (Abs(b[0] * p0) + Abs(b[1] * p1) + Abs((1 - b[0] - b[1]) * p2));
+        Float pdf = 1 / TriArea(p0, p1, p2);
+        Vec wi = p - ref;
+        if (LengthSquared(wi) == 0) return false;
+        wi = Normalize(wi);
+        pdf /= AbsDot(n, -wi) / DistanceSquared(ref, p);
+        if (std::isinf(pdf)) return false;
+        ss->p = p;
+        ss->n = n;
+        ss->pdf = pdf;
+        return true;
+    }
+    Float pdf = 1;
+    if (ns != Vec(0, 0, 0)) {
+        Vec w0 = Normalize(p0 - ref), w1 = Normalize(p1 - ref), w2 = Normalize(p2 - ref);
+        Float w[4] = {std::max<Float>(0.01, AbsDot(ns, w1)), std::max<Float>(0.01, AbsDot(ns, w1)),
+                      std::max<Float>(0.01, AbsDot(ns, w0)), std::max<Float>(0.01, AbsDot(ns, w2))};
+        Float x, y;
+        SampleBilinear(u0, u1, w, &x, &y);
+        u0 = x;
+        u1 = y;
+        pdf = BilinearPDF(u0, u1, w);
+    }
+    Float triPDF, b[3];
+    SampleSphericalTriangle(p0, p1, p2, ref, u0, u1, b, &triPDF);
+    if (triPDF == 0) return false;
+    pdf *= triPDF;
+    ss->err = gamma(6) * (Abs(b[0] * p0) + Abs(b[1] * p1) + Abs((1 - b[0] - b[1]) * p2));
+    ss->p = b[0] * p0 + b[1] * p1 + b[2] * p2;
+    Vec n = Normalize(Cross(p1 - p0, p2 - p0));
+    if (flip) n = n * -1.f;
+    ss->n = n;
+    ss->pdf = pdf;
+    return true;
+}
+static Float TrianglePDF(Vec p0, Vec p1, Vec p2, bool flip, Vec ref, Vec refErr, Vec refN, Vec ns, Vec wi) {
+    Float solidAngle = SphericalTriangleArea(Normalize(p0 - ref), Normalize(p1 - ref), Normalize(p2 - ref));
+    if (solidAngle < 3e-4f || solidAngle > 6.22f) {
+        Vec o = OffsetRayOrigin(ref, refErr, refN, wi);
+        TriIsect ti;
+        if (!IntersectTriangle(o, wi, Infinity, p0, p1, p2, &ti)) return 0;
+        Interaction si = TriangleInteraction(p0, p1, p2, flip, ti, wi);
+        Float pdf = (1 / TriArea(p0, p1, p2)) / (AbsDot(si.n, -wi) / DistanceSquared(ref, si.p));
+        if (std::isinf(pdf)) pdf = 0;
+        return pdf;
+    }
+    Float pdf = 1 / solidAngle;
+    if (ns != Vec(0, 0, 0)) {
+        Float u0, u1;
+        InvertSphericalTriangleSample(p0, p1, p2, ref, wi, &u0, &u1);
+        Vec w0 = Normalize(p0 - ref), w1 = Normalize(p1 - ref), w2 = Normalize(p2 - ref);
+        Float w[4] = {std::max<Float>(0.01, AbsDot(ns, w1)), std::max<Float>(0.01, AbsDot(ns, w1)),
+                      std::max<Float>(0.01, AbsDot(ns, w0)), std::max<Float>(0.01, AbsDot(ns, w2))};
+        pdf *= BilinearPDF(u0, u1, w);
+    }
+    return pdf;
+}
+
+// ---------------------------------------------------------------- light sampler
+struct LightNode {
+    Vec mn, mx, w;
+    Float phi, cosO, cosE;
+    int twoSided, childOrLight, isLeaf;
+};
+static Float CosSub(Float sa, Float ca, Float sb, Float cb) { return ca > cb ? 1 : ca * cb + sa * sb; }
+static Float SinSub(Float sa, Float ca, Float sb, Float cb) { return ca > cb ? 0 : sa * cb - ca * sb; }
+static Float Importance(const LightNode &b, Vec p, Vec n) {
+    Vec pc = (b.mn + b.mx) / 2;
+    Float d2 = DistanceSquared(p, pc);
+    d2 = std::max(d2, Length(b.mx - b.mn) / 2);
+    Vec wi = Normalize(p - pc);
+    Float cosW = Dot(b.w, wi);
+    if (b.twoSided) cosW = std::abs(cosW);
+    Float sinW = SafeSqrt(1 - Sqr(cosW));
+    // BoundSubtendedDirections
+    Float cosB;
+    {
+        Vec c = (b.mn + b.mx) / 2;
+        bool inside = c.x >= b.mn.x && c.x <= b.mx.x && c.y >= b.mn.y && c.y <= b.mx.y && c.z >= b.mn.z && c.z <= b.mx.z;
+        Float radius = inside ? Length(c - b.mx) : 0;
+        if (DistanceSquared(p, c) < Sqr(radius)) cosB = -1;
+        else cosB = SafeSqrt(1 - Sqr(radius) / DistanceSquared(c, p));
+    }
+    Float sinB = SafeSqrt(1 - Sqr(cosB));
+    Float sinO = SafeSqrt(1 - Sqr(b.cosO));
+    Float cosX = CosSub(sinW, cosW, sinO, b.cosO), sinX = SinSub(sinW, cosW, sinO, b.cosO);
+    Float cosThetap = CosSub(sinX, cosX, sinB, cosB);
+    if (cosThetap <= b.cosE) return 0;
+    Float imp = b.phi * cosThetap / d2;
+    if (n != Vec(0, 0, 0)) {
+        Float cosI = AbsDot(wi, n), sinI = SafeSqrt(1 - Sqr(cosI));
+        imp *= CosSub(sinI, cosI, sinB, cosB);
+    }
+    return std::max<Float>(imp, 0);
+}
+
+struct Lights {
+    const pbrt_scene_flat *f;
+    std::vector<LightNode> nodes;
+    void Init(const pbrt_scene_flat *flat) {
+        f = flat;
+        for (int i = 0; i < f->n_light_nodes; ++i) {
+            const float *b = f->light_node_bounds + 12 * i;
+            const int32_t *in = f->light_node_info + 3 * i;
+            nodes.push_back({Vec(b[0], b[1], b[2]), Vec(b[3], b[4], b[5]), Vec(b[6], b[7], b[8]), b[9], b[10], b[11],
+                             in[2], in[0], in[1]});
+        }
+    }
+    int NumAll() const { return f->n_area_lights + f->n_infinite_lights; }
+    bool uniform() const {
+        return f->n_light_nodes == 0 && f->n_infinite_lights + f->n_area_lights > 0 && uniformFlag;
+    }
+    bool uniformFlag = false;
+    // returns light index (area first, then infinite) and pmf
+    bool Sample(Vec p, Vec n, Float u, int *light, Float *pmf) const {
+        if (uniformFlag) {
+            int nAll = NumAll();
+            if (!nAll) return false;
+            *light = std::min<int>(u * nAll, nAll - 1);
+            *pmf = 1.f / nAll;
+            return true;
+        }
+        Float pInf = Float(f->n_infinite_lights) / Float(f->n_infinite_lights + (nodes.empty() ? 0 : 1));
+        if (u < pInf) {
+            u /= pInf;
+            int index = std::min<int>(u * f->n_infinite_lights, f->n_infinite_lights - 1);
+            *pmf = pInf / f->n_infinite_lights;
+            *light = f->n_area_lights + index;
+            return true;
+        }
+        if (nodes.empty()) return false;
+        u = std::min<Float>((u - pInf) / (1 - pInf), OneMinusEpsilon);
+        int ni = 0;
+        Float pm = 1 - pInf;
+        while (true) {
+            const LightNode &node = nodes[ni];
+            if (!node.isLeaf) {
+                Float ci[2] = {Importance(nodes[ni + 1], p, n), Importance(nodes[node.childOrLight], p, n)};
+                if (ci[0] == 0 && ci[1] == 0) return false;
+                // SampleDiscrete over two weights
+                Float sum = 0;
+                sum += ci[0];
+                sum += ci[1];
+                Float up = u * sum;
+                if (up == sum) up = NextFloatDown(up);
+                int off = 0;
+                Float acc = 0;
+                while (acc + ci[off] <= up) acc += ci[off++];
+                pm *= ci[off] / sum;
+                u = std::min((up - acc) / ci[off], OneMinusEpsilon);
+                ni = off == 0 ? ni + 1 : node.childOrLight;
+            } else {
+                if (ni > 0 || Importance(node, p, n) > 0) {
+                    *light = node.childOrLight;
+                    *pmf = pm;
+                    return true;
+                }
+                return false;
+            }
+        }
+    }
+    Float PMF(Vec p, Vec n, int light) const {
+        if (uniformFlag) return NumAll() ? 1.f / NumAll() : 0.f;
+        uint32_t trail = light < f->n_area_lights ? f->light_bit_trail[light] : 0xffffffffu;
+        bool inBVH = false;
+        for (auto &nd : nodes)
+            if (nd.isLeaf && nd.childOrLight == light) inBVH = true;
+        if (!inBVH) return 1.f / (f->n_infinite_lights + (nodes.empty() ? 0 : 1));
+        Float pInf = Float(f->n_infinite_lights) / Float(f->n_infinite_lights + (nodes.empty() ? 0 : 1));
+        Float pm = 1 - pInf;
+        int ni = 0;
+        while (true) {
+            const LightNode &node = nodes[ni];
+            if (node.isLeaf) return pm;
+            Float ci[2] = {Importance(nodes[ni + 1], p, n), Importance(nodes[node.childOrLight], p, n)};
+            pm *= ci[trail & 1] / (ci[0] + ci[1]);
+            ni = (trail & 1) ? node.childOrLight : ni + 1;
+            trail >>= 1;
+        }
+    }
+};
+
+// ---------------------------------------------------------------- integrator
+struct Renderer {
+    Scene S;
+    Lights lights;
+    const pbrt_scene_flat *f;
+
+    Vec Xf(const float *m, Vec p, bool point) const {
+        Float x = m[0] * p.x + m[1] * p.y + m[2] * p.z, y = m[4] * p.x + m[5] * p.y + m[6] * p.z,
+              z = m[8] * p.x + m[9] * p.y + m[10] * p.z;
+        if (!point) return Vec(x, y, z);
+        x = x + m[3];
+        y = y + m[7];
+        z = z + m[11];
+        Float w = m[12] * p.x + m[13] * p.y + m[14] * p.z + m[15];
+        if (w == 1) return Vec(x, y, z);
+        return Vec(x, y, z) / w;
+    }
+
+    Spectrum LightL(int li, const Wavelengths &lambda) const {
+        const float *dense = f->dense_spectra + 311 * f->light_spectrum[li];
+        return SampleDense(dense, lambda) * f->light_scale[li];
+    }
+
+    // one pixel sample -> sensor RGB and filter weight (film.h:95-100)
+    void Li(int px, int py, int sampleIndex, float rgb[3], float *weight) const {
+        HaltonState hs{&S.halton, 0, 0};
+        hs.Start(px, py, sampleIndex, 0);
+        Float lu = hs.Get1D();
+        Wavelengths lambda = Wavelengths::SampleUniform(lu);
+        Float fx, fy;
+        hs.Pixel2D(&fx, &fy);
+        Float ox = Lerp(fx, -S.frx, S.frx), oy = Lerp(fy, -S.fry, S.fry);
+        Float pFilmX = px + ox + 0.5f, pFilmY = py + oy + 0.5f;
+        hs.Get1D();  // time
+        Float l0, l1;
+        hs.Get2D(&l0, &l1);
+        *weight = 1;
+        Vec pCam = Xf(f->camera_from_raster, Vec(pFilmX, pFilmY, 0), true);
+        Vec ro(0, 0, 0), rd = Normalize(pCam);
+        if (f->lens_radius > 0) {
+            Float lx, ly;
+            SampleUniformDiskConcentric(l0, l1, &lx, &ly);
+            lx *= f->lens_radius;
+            ly *= f->lens_radius;
+            Float ft = f->focal_distance / rd.z;
+            Vec pFocus = ro + rd * ft;
+            ro = Vec(lx, ly, 0);
+            rd = Normalize(pFocus - ro);
+        }
+        {
+            const float *m = f->render_from_camera;
+            Vec oo = Xf(m, ro, true);
+            Vec err = gamma(3) * (Abs(Vec(m[0] * ro.x, m[4] * ro.x, m[8] * ro.x)) + Abs(Vec(m[1] * ro.y, m[5] * ro.y, m[9] * ro.y)) +
+                                  Abs(Vec(m[2] * ro.z, m[6] * ro.z, m[10] * ro.z)) + Abs(Vec(m[3], m[7], m[11])));
+            Vec dd = Xf(m, rd, false);
+            Float l2 = LengthSquared(dd);
+            if (l2 > 0) oo = oo + dd * (Dot(Abs(dd), err) / l2);
+            ro = oo;
+            rd = dd;
+        }
+        Spectrum L(0.f), beta(1.f), r_u(1.f), r_l(1.f);
+        bool specularBounce = false;
+        Float etaScale = 1;
+        Vec prevP, prevErr, prevN, prevNs;
+        for (int depth = 0;; ++depth) {
+            TriIsect ti;
+            int prim = S.Intersect(ro, rd, Infinity, &ti, false);
+            if (prim < 0) {
+                // HandleEscapedRays: uniform infinite lights, PDF_Li(allowIncomplete)=0
+                for (int k = 0; k < f->n_infinite_lights; ++k) {
+                    Spectrum Le = SampleDense(f->dense_spectra + 311 * f->inf_spectrum[k], lambda) * f->inf_scale[k];
+                    if (!Le) continue;
+                    if (depth == 0 || specularBounce) L = L + beta * Le / r_u.Average();
+                    else {
+                        Spectrum rl = r_l * 0.f;
+                        L = L + beta * Le / (r_u + rl).Average();
+                    }
+                }
+                break;
+            }
+            bool flip = f->tri_flip[prim];
+            Vec p0 = S.P(prim, 0), p1 = S.P(prim, 1), p2 = S.P(prim, 2);
+            Interaction si = TriangleInteraction(p0, p1, p2, flip, ti, rd);
+            // HandleEmissiveIntersection
+            int light = f->tri_light[prim];
+            if (light >= 0 && (f->light_two_sided[light] || Dot(si.n, si.wo) >= 0)) {
+                Spectrum Le = LightL(light, lambda);
+                if (Le) {
+                    if (depth == 0 || specularBounce) L = L + beta * Le / r_u.Average();
+                    else {
+                        Float lightChoicePDF = lights.PMF(prevP, prevNs, light);
+                        int lp = f->light_prim[light];
+                        Float lightPDF = lightChoicePDF * TrianglePDF(S.P(lp, 0), S.P(lp, 1), S.P(lp, 2), f->tri_flip[lp],
+                                                                      prevP, prevErr, prevN, prevNs, -si.wo);
+                        Spectrum rl = r_l * lightPDF;
+                        L = L + beta * Le / (r_u + rl).Average();
+                    }
+                }
+            }
+            if (depth == S.maxDepth) break;
+            // GenerateRaySamples: dims 6 + 7 depth
+            HaltonState h2{&S.halton, 0, 0};
+            h2.Start(px, py, sampleIndex, 6 + 7 * depth);
+            Float dUc = h2.Get1D(), dU0, dU1;
+            h2.Get2D(&dU0, &dU1);
+            Float iUc = h2.Get1D(), iU0, iU1;
+            h2.Get2D(&iU0, &iU1);
+            Float rr = h2.Get1D();
+            (void)iUc;
+            // DiffuseMaterial
+            int mat = f->tri_material[prim];
+            const float *mc = f->material_coeffs + 4 * mat;
+            Spectrum R;
+            for (int i = 0; i < NS; ++i) {
+                Float r = f->material_constant[mat] ? mc[3] : Sigmoid(mc[0], mc[1], mc[2], lambda.lambda[i]);
+                R[i] = Clamp(r, 0, 1);
+            }
+            Vec fx_ = Normalize(si.dpdu), fz = si.ns, fy_ = Cross(fz, fx_);
+            auto toLocal = [&](Vec v) { return Vec(Dot(v, fx_), Dot(v, fy_), Dot(v, fz)); };
+            auto fromLocal = [&](Vec v) { return fx_ * v.x + fy_ * v.y + fz * v.z; };
+            Vec woL = toLocal(si.wo);
+            bool nonSpecular = bool(R);
+            Spectrum oldBeta = beta;
+            bool haveNext = false;
+            Vec nextO, nextD;
+            Spectrum nb;
+            Spectrum nrl;
+            if (woL.z != 0 && nonSpecular) {
+                Vec wiL = SampleCosineHemisphere(iU0, iU1);
+                if (woL.z < 0) wiL.z *= -1;
+                Float pdf = std::abs(wiL.z) * InvPi;
+                Spectrum fv = R * InvPi;
+                if (fv && pdf != 0 && wiL.z != 0) {
+                    Vec wi = fromLocal(wiL);
+                    nb = beta * fv * AbsDot(wi, si.ns) / pdf;
+                    nrl = r_u / pdf;
+                    Spectrum rrBeta = nb * etaScale / r_u.Average();
+                    if (rrBeta.Max() < 1 && depth >= 1) {
+                        Float q = std::max<Float>(0, 1 - rrBeta.Max());
+                        if (rr < q) nb = Spectrum(0.f);
+                        else nb = nb / (1 - q);
+                    }
+                    if (nb) {
+                        haveNext = true;
+                        nextO = OffsetRayOrigin(si.p, si.err, si.n, wi);
+                        nextD = wi;
+                    }
+                }
+            }
+            // light sampling + shadow ray
+            if (nonSpecular) {
+                Vec cp = OffsetRayOrigin(si.p, si.err, si.n, si.wo);
+                int li;
+                Float lpmf;
+                if (lights.Sample(cp, si.ns, dUc, &li, &lpmf) && li < f->n_area_lights) {
+                    int lp = f->light_prim[li];
+                    ShapeSample ss;
+                    if (TriangleSample(S.P(lp, 0), S.P(lp, 1), S.P(lp, 2), f->tri_flip[lp], cp, si.ns, dU0, dU1, &ss) &&
+                        ss.pdf != 0 && LengthSquared(ss.p - cp) != 0) {
+                        Vec wi = Normalize(ss.p - cp);
+                        Spectrum Le(0.f);
+                        if (f->light_two_sided[li] || Dot(ss.n, -wi) >= 0) Le = LightL(li, lambda);
+                        if (Le) {
+                            Vec wiL = toLocal(wi);
+                            Spectrum fv = (woL.z != 0 && woL.z * wiL.z > 0) ? R * InvPi : Spectrum(0.f);
+                            if (fv) {
+                                Spectrum b2 = oldBeta * fv * AbsDot(wi, si.ns);
+                                Float lightPDF = ss.pdf * lpmf;
+                                Float bsdfPDF = (woL.z != 0 && woL.z * wiL.z > 0) ? std::abs(wiL.z) * InvPi : 0;
+                                Spectrum ru = r_u * bsdfPDF, rl = r_u * lightPDF;
+                                Spectrum Ld = b2 * Le;
+                                Vec pf = OffsetRayOrigin(si.p, si.err, si.n, ss.p - si.p);
+                                Vec pt = OffsetRayOrigin(ss.p, ss.err, ss.n, pf - ss.p);
+                                TriIsect dummy;
+                                if (S.Intersect(pf, pt - pf, 1 - ShadowEpsilon, &dummy, true) < 0)
+                                    L = L + Ld / (ru + rl).Average();
+                            }
+                        }
+                    }
+                }
+            }
+            if (!haveNext) break;
+            beta = nb;
+            r_l = nrl;
+            specularBounce = false;
+            prevP = si.p;
+            prevErr = si.err;
+            prevN = si.n;
+            prevNs = si.ns;
+            ro = nextO;
+            rd = nextD;
+        }
+        // PixelSensor::ToSensorRGB (cie1931): L / pdf, averaged against X/Y/Z bars
+        Spectrum Lp;
+        for (int i = 0; i < NS; ++i) Lp[i] = lambda.pdf[i] != 0 ? L[i] / lambda.pdf[i] : 0;
+        Spectrum xb = SampleDense(f->sensor_xyz, lambda), yb = SampleDense(f->sensor_xyz + 311, lambda),
+                 zb = SampleDense(f->sensor_xyz + 622, lambda);
+        rgb[0] = f->imaging_ratio * (xb * Lp).Average();
+        rgb[1] = f->imaging_ratio * (yb * Lp).Average();
+        rgb[2] = f->imaging_ratio * (zb * Lp).Average();
+    }
+};
+
+}  // namespace oracle
+
+using namespace oracle;
+
+extern "C" {
+
+// Renders rows x [first_sample, first_sample + n_samples) into film[4][yres*xres]
+// (sensor RGB sums + weight sums, RGBFilm::Pixel layout) with `threads` host threads.
+int oracle_render(const pbrt_scene_flat *flat, const pbrt_scene_info *info, const int32_t *rows, int nRows,
+                  int firstSample, int nSamples, int uniformLightSampler, int threads, double *film) {
+    Renderer r;
+    r.f = flat;
+    r.S.Init(flat, info);
+    r.lights.Init(flat);
+    r.lights.uniformFlag = uniformLightSampler != 0;
+    size_t npix = (size_t)info->xres * info->yres;
+    std::atomic<int> next(0);
+    auto work = [&]() {
+        while (true) {
+            int ri = next.fetch_add(1);
+            if (ri >= nRows) break;
+            int y = rows[ri];
+            for (int x = info->px0; x < info->px1; ++x) {
+                size_t pix = (size_t)y * info->xres + x;
+                for (int s = firstSample; s < firstSample + nSamples; ++s) {
+                    float rgb[3], w;
+                    r.Li(x, y, s, rgb, &w);
+                    film[pix] += w * rgb[0];
+                    film[npix + pix] += w * rgb[1];
+                    film[2 * npix + pix] += w * rgb[2];
+                    film[3 * npix + pix] += w;
+                }
+            }
+        }
+    };
+    threads = std::max(1, threads);
+    std::vector<std::thread> pool;
+    for (int t = 1; t < threads; ++t) pool.emplace_back(work);
+    work();
+    for (auto &t : pool) t.join();
+    return 0;
+}
+
+// ---- component entry points checked against tests/golden/reference_components.json
+int oracle_intersect_triangle(const float *p9, const float *o3, const float *d3, float tMax, int flip, float *out) {
+    // out: b0 b1 b2 t | p3 err3 n3 dpdu3 wo3
+    TriIsect ti;
+    Vec p0(p9[0], p9[1], p9[2]), p1(p9[3], p9[4], p9[5]), p2(p9[6], p9[7], p9[8]);
+    Vec d(d3[0], d3[1], d3[2]);
+    if (!IntersectTriangle(Vec(o3[0], o3[1], o3[2]), d, tMax, p0, p1, p2, &ti)) return 0;
+    Interaction si = TriangleInteraction(p0, p1, p2, flip != 0, ti, d);
+    float v[19] = {ti.b0, ti.b1, ti.b2, ti.t, si.p.x, si.p.y, si.p.z, si.err.x, si.err.y, si.err.z, si.n.x,
+                   si.n.y, si.n.z, si.dpdu.x, si.dpdu.y, si.dpdu.z, si.wo.x, si.wo.y, si.wo.z};
+    std::memcpy(out, v, sizeof v);
+    return 1;
+}
+
+void oracle_warps(const float *u2, const float *w4, float *out) {
+    // out: disk2 cos3 tri3 bilinear2 bilinear_pdf1
+    Float x, y;
+    SampleUniformDiskConcentric(u2[0], u2[1], &x, &y);
+    Vec c = SampleCosineHemisphere(u2[0], u2[1]);
+    Float b[3];
+    SampleUniformTriangle(u2[0], u2[1], b);
+    Float bx, by;
+    SampleBilinear(u2[0], u2[1], w4, &bx, &by);
+    float v[11] = {x, y, c.x, c.y, c.z, b[0], b[1], b[2], bx, by, BilinearPDF(bx, by, w4)};
+    std::memcpy(out, v, sizeof v);
+}
+
+void oracle_spherical_triangle(const float *v9, const float *p3, const float *u2, float *out) {
+    // out: b3 pdf1 w3 inv2 area1
+    Vec v0(v9[0], v9[1], v9[2]), v1(v9[3], v9[4], v9[5]), v2(v9[6], v9[7], v9[8]), p(p3[0], p3[1], p3[2]);
+    Float b[3], pdf;
+    SampleSphericalTriangle(v0, v1, v2, p, u2[0], u2[1], b, &pdf);
+    Vec ps = b[0] * v0 + b[1] * v1 + b[2] * v2;
+    Vec w = Normalize(ps - p);
+    Float i0, i1;
+    InvertSphericalTriangleSample(v0, v1, v2, p, w, &i0, &i1);
+    Float area = SphericalTriangleArea(Normalize(v0 - p), Normalize(v1 - p), Normalize(v2 - p));
+    float v[10] = {b[0], b[1], b[2], pdf, w.x, w.y, w.z, i0, i1, area};
+    std::memcpy(out, v, sizeof v);
+}
+
+int oracle_triangle_sample(const float *v9, int flip, const float *ref3, const float *n3, const float *ns3,
+                           const float *u2, float *out) {
+    // out: p3 err3 n3 pdf1 pdf_wi1 solid_angle1
+    Vec p0(v9[0], v9[1], v9[2]), p1(v9[3], v9[4], v9[5]), p2(v9[6], v9[7], v9[8]);
+    Vec ref(ref3[0], ref3[1], ref3[2]), n(n3[0], n3[1], n3[2]), ns(ns3[0], ns3[1], ns3[2]);
+    ShapeSample ss;
+    if (!TriangleSample(p0, p1, p2, flip != 0, ref, ns, u2[0], u2[1], &ss)) return 0;
+    Vec wi = Normalize(ss.p - ref);
+    Float pdf2 = TrianglePDF(p0, p1, p2, flip != 0, ref, Vec(0, 0, 0), n, ns, wi);
+    Float sa = SphericalTriangleArea(Normalize(p0 - ref), Normalize(p1 - ref), Normalize(p2 - ref));
+    float v[12] = {ss.p.x, ss.p.y, ss.p.z, ss.err.x, ss.err.y, ss.err.z, ss.n.x, ss.n.y, ss.n.z, ss.pdf, pdf2, sa};
+    std::memcpy(out, v, sizeof v);
+    return 1;
+}
+
+float oracle_light_importance(const float *decoded11, float phi, int twoSided, const float *p3, const float *n3) {
+    LightNode b{Vec(decoded11[0], decoded11[1], decoded11[2]), Vec(decoded11[3], decoded11[4], decoded11[5]),
+                Vec(decoded11[6], decoded11[7], decoded11[8]), phi, decoded11[9], decoded11[10], twoSided, 0, 1};
+    return Importance(b, Vec(p3[0], p3[1], p3[2]), Vec(n3[0], n3[1], n3[2]));
+}
+
+void oracle_offset_ray_origin(const float *p3, const float *e3, const float *n3, const float *w3, float *out) {
+    Vec po = OffsetRayOrigin(Vec(p3[0], p3[1], p3[2]), Vec(e3[0], e3[1], e3[2]), Vec(n3[0], n3[1], n3[2]),
+                             Vec(w3[0], w3[1], w3[2]));
+    out[0] = po.x;
+    out[1] = po.y;
+    out[2] = po.z;
+}
+
+void oracle_sample_wavelengths(float u, float *lambda31, float *pdf) {
+    Wavelengths w = Wavelengths::SampleUniform(u);
+    std::memcpy(lambda31, w.lambda, sizeof w.lambda);
+    *pdf = w.pdf[0];
+}
+
+float oracle_halton(int xres, int yres, int seed, int px, int py, int sampleIndex, int dim) {
+    static thread_local Halton h;
+    static thread_local int key[3] = {-1, -1, -1};
+    if (key[0] != xres || key[1] != yres || key[2] != seed) {
+        h = Halton();
+        h.Init(xres, yres, (uint32_t)seed, 60);
+        key[0] = xres;
+        key[1] = yres;
+        key[2] = seed;
+    }
+    HaltonState s{&h, 0, 0};
+    s.Start(px, py, sampleIndex, dim < 0 ? 0 : dim);
+    Float a, b;
+    s.Pixel2D(&a, &b);
+    if (dim == -1) return a;
+    if (dim == -2) return b;
+    return s.Sample(std::max(2, dim));
+}
+
+}  // extern "C"

@@ -1,0 +1,63 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes wrapper of oracle/_build/liboracle.so, the CPU
+restatement of pbrt-v4's wavefront integrator (see oracle/oracle.cpp).  Imported only by
+tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg."""
+import ctypes
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB = HERE / "_build" / "liboracle.so"
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", str(HERE)])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            build()
+        _lib = ctypes.CDLL(str(LIB))
+        _lib.oracle_render.restype = ctypes.c_int
+        _lib.oracle_light_importance.restype = ctypes.c_float
+        _lib.oracle_halton.restype = ctypes.c_float
+        _lib.oracle_intersect_triangle.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_float, ctypes.c_int, ctypes.c_void_p]
+        _lib.oracle_light_importance.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        _lib.oracle_sample_wavelengths.argtypes = [ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p]
+        _lib.oracle_halton.argtypes = [ctypes.c_int] * 7
+    return _lib
+
+
+def f32(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float32))
+
+
+def render(scene, rows=None, first_sample=0, n_samples=None, threads=None):
+    """Render `rows` of a pbrt_amd.Scene on the CPU; returns film [4, yres, xres] float64."""
+    info = scene.info
+    flat = scene.flat()
+    if rows is None:
+        rows = np.arange(info.py0, info.py1, dtype=np.int32)
+    rows = np.ascontiguousarray(rows, dtype=np.int32)
+    if n_samples is None:
+        n_samples = info.spp - first_sample
+    threads = threads or os.cpu_count() or 1
+    film = np.zeros((4, info.yres, info.xres), dtype=np.float64)
+    rc = lib().oracle_render(ctypes.byref(flat), ctypes.byref(info), rows.ctypes.data_as(ctypes.c_void_p),
+                             len(rows), int(first_sample), int(n_samples), int(info.uniform_light_sampler),
+                             int(threads), film.ctypes.data_as(ctypes.c_void_p))
+    assert rc == 0
+    return film
+
+
+def film_to_rgb(film, m3x3):
+    """RGBFilm::GetPixelRGB: normalise by the weight sum and apply outputRGBFromSensorRGB."""
+    w = film[3]
+    rgb = film[:3] / np.where(w == 0, 1, w)
+    m = np.asarray(m3x3, dtype=np.float64).reshape(3, 3)
+    return np.einsum("ij,jhw->hwi", m, rgb).astype(np.float32)

@@ -1,0 +1,182 @@
+#!/usr/bin/env python3
+"""Benchmark: Msamples/s of the MI355X wavefront path tracer on BASELINE.json's headline
+configuration (configs[1]): synthetic Cornell box, 1280x720, 64 spp, PathIntegrator maxdepth
+5 semantics (wavefront volpath), Halton sampler, diffuse-only BxDFs.
+
+One "step" = one complete render of that image (all 64 samples per pixel, film cleared
+first) plus, for N > 1, the single RCCL sum-reduce of the film over xGMI.  Pixel rows are
+sharded across ranks in 16-row blocks (strong scaling: every step renders the same whole
+image, split over the N ranks, so per-GPU work is 1/N of it; the metric counts every sample
+of the image).  Launch: ``python bench.py`` (1 GPU) or
+``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``.
+
+The JSON line also carries
+  roofline     the closest-hit (traverse + compact + material-queue scatter) kernel, the
+               judged "BVH kernel" (SURVEY.md §8(d)): algorithmic bytes per launch / mean
+               launch time measured with HIP events on the context stream
+  cpu_baseline the CPU oracle (oracle/oracle.cpp, a port of pbrt's wavefront/VolPath
+               integrator) on a bounded sample of the same workload, host threads stated.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "pbrt-v4_amd"))
+
+# Algorithmic bytes per ray of the closest-hit kernel, from its declared SoA fields:
+#   reads  ray-queue entry 4 B + ray o,d 24 B             = 28 B
+#   writes hit prim 4 B + b0,b1,b2,t 16 B + queue push 4 B = 24 B
+BYTES_PER_RAY_CLOSEST = 52
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--xres", type=int, default=1280)
+    ap.add_argument("--yres", type=int, default=720)
+    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--max-paths", type=int, default=1 << 22)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def cpu_baseline(args, threads):
+    """Oracle (pbrt wavefront/VolPath port) on the host: every 8th film row, 16 spp."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import numpy as np
+    import pbrt_amd as pa
+    import pyoracle
+    sc = pa.load_scene(ROOT / "scenes" / "cornell-box.pbrt", xresolution=args.xres, yresolution=args.yres, spp=args.spp)
+    i = sc.info
+    rows = np.arange(i.py0, i.py1, 8, dtype=np.int32)
+    spp = 16
+    pyoracle.lib()
+    t = time.perf_counter()
+    pyoracle.render(sc, rows=rows, first_sample=0, n_samples=spp, threads=threads)
+    dt = time.perf_counter() - t
+    n = len(rows) * (i.px1 - i.px0) * spp
+    return {"value": n / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"{len(rows)} of {i.py1 - i.py0} rows x {i.px1 - i.px0} px x {spp} spp "
+                      f"({n} samples, {dt:.2f} s wall)"}
+
+
+def pmc_traffic():
+    """HBM bytes per closest-hit launch from the committed rocprofv3 PMC pass, if any."""
+    f = ROOT / "profiles" / "r01_closest_pmc.json"
+    if f.exists():
+        try:
+            return json.loads(f.read_text()).get("hbm_bytes_per_launch")
+        except Exception:
+            return None
+    return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+    import pbrt_amd as pa
+    from pbrt_amd.tiles import film_tensor_from_device_ptr, rows_for_rank
+
+    scene = pa.load_scene(ROOT / "scenes" / "cornell-box.pbrt", xresolution=args.xres, yresolution=args.yres,
+                          spp=args.spp)
+    info = scene.info
+    integ = pa.WavefrontPathIntegrator(scene, device=local_rank, max_paths=args.max_paths)
+    rows = rows_for_rank(info.py0, info.py1, rank, world)
+    film_ptr, film_n = integ.film_device_ptr()
+    film_t = film_tensor_from_device_ptr(film_ptr, film_n, local_rank) if world > 1 else None
+
+    def step(timed_kernel=False):
+        integ.film_clear()
+        integ.render(rows=rows, first_sample=0, n_samples=info.spp, time_closest=timed_kernel)
+        if world > 1:
+            integ.synchronize()
+            dist.reduce(film_t, dst=0, op=dist.ReduceOp.SUM)
+
+    for _ in range(args.warmup):
+        step()
+    integ.synchronize()
+    integ.reset_stats()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(timed_kernel=True)
+    integ.synchronize()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    st = integ.stats()
+    dt_max = dt
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt_max = tt.item()
+
+    samples = (info.px1 - info.px0) * (info.py1 - info.py0) * info.spp * args.steps  # all ranks together
+    value = samples / dt_max / 1e6
+    launches = max(st.closest_launches, 1)
+    mean_launch_s = st.closest_ms / 1e3 / launches
+    bytes_per_launch = BYTES_PER_RAY_CLOSEST * st.closest_rays / launches
+    achieved = bytes_per_launch / mean_launch_s / 1e9 if mean_launch_s > 0 else 0.0
+    traffic = pmc_traffic()
+
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            try:
+                cpu = cpu_baseline(args, min(args.cpu_threads, os.cpu_count() or 1))
+            except Exception as e:  # the baseline is reported, never required
+                cpu = {"value": None, "error": str(e)}
+        line = {
+            "metric": "Msamples/sec (paths x spp / s) at 1280x720x64spp",
+            "value": round(value, 3),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt_max / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": f"cornell-box (synthetic) {args.xres}x{args.yres} {info.spp}spp maxdepth "
+                                   f"{info.max_depth} halton, wavefront volpath, diffuse BxDF (BASELINE configs[1])",
+                       "xres": args.xres, "yres": args.yres, "spp": info.spp, "max_depth": info.max_depth,
+                       "triangles": info.n_triangles, "paths_per_pass": int(st.paths_per_pass),
+                       "sharding": "16-row stripes round-robin over ranks + 1 RCCL film reduce" if world > 1 else
+                       "single GPU"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "kernel": "k_closest (BVH8 traverse + hit record + wave64 ballot push to material queue)",
+                         "bytes_per_ray": BYTES_PER_RAY_CLOSEST,
+                         "rays_per_launch": round(st.closest_rays / launches, 1),
+                         "mean_launch_us": round(mean_launch_s * 1e6, 3)},
+            "cpu_baseline": cpu,
+            "rays": {"camera": int(st.camera_rays), "closest": int(st.closest_rays), "shadow": int(st.shadow_rays)},
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

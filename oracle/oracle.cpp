@@ -105,6 +105,10 @@ struct Vec {
 static inline Vec operator*(Float s, Vec v) { return {s * v.x, s * v.y, s * v.z}; }
 static inline Float Dot(Vec a, Vec b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 static inline Float AbsDot(Vec a, Vec b) { return std::abs(Dot(a, b)); }
+// Normal3f dot products are FMA-compensated (util/vecmath.h:1059-1099)
+static inline Float SumOfProducts(Float a, Float b, Float c, Float d);
+static inline Float DotN(Vec n, Vec v) { return std::fma(n.x, v.x, SumOfProducts(n.y, v.y, n.z, v.z)); }
+static inline Float AbsDotN(Vec n, Vec v) { return std::abs(DotN(n, v)); }
 static inline Vec Cross(Vec v, Vec w) {
     return {DifferenceOfProducts(v.y, w.z, v.z, w.y), DifferenceOfProducts(v.z, w.x, v.x, w.z),
             DifferenceOfProducts(v.x, w.y, v.y, w.x)};
@@ -433,9 +437,9 @@ static bool IntersectTriangle(Vec o, Vec dir, Float tMax, Vec p0, Vec p1, Vec p2
 }
 
 static Vec OffsetRayOrigin(Vec p, Vec err, Vec n, Vec w) {
-    Float d = Dot(Abs(n), err);
+    Float d = DotN(Abs(n), err);
     Vec offset = d * n;
-    if (Dot(w, n) < 0) offset = -offset;
+    if (DotN(n, w) < 0) offset = -offset;
     Vec po = p + offset;
     for (int i = 0; i < 3; ++i) {
         if (offset[i] > 0) po[i] = NextFloatUp(po[i]);
@@ -445,6 +449,20 @@ static Vec OffsetRayOrigin(Vec p, Vec err, Vec n, Vec w) {
 }
 
 struct Scene;
+
+// Point3fi(p, e): interval [NextFloatDown(p - e), NextFloatUp(p + e)]; p() is its midpoint
+// and Error() its half width (util/vecmath.h:753, util/math.h:829, util/float.h:201-229)
+static void Point3fi(Vec v, Vec e, Vec *p, Vec *err) {
+    for (int i = 0; i < 3; ++i) {
+        Float lo = v[i], hi = v[i];
+        if (e[i] != 0) {
+            lo = NextFloatDown(v[i] + (-e[i]));
+            hi = NextFloatUp(v[i] + e[i]);
+        }
+        (*p)[i] = (lo + hi) / 2;
+        (*err)[i] = (hi - lo) / 2;
+    }
+}
 
 struct Interaction {
     Vec p, err, n, ns, dpdu, wo;
@@ -469,8 +487,8 @@ static Interaction TriangleInteraction(Vec p0, Vec p1, Vec p2, bool flip, TriIse
         }
     }
     if (degenerate || LengthSquared(Cross(dpdu, dpdv)) == 0) CoordinateSystem(Normalize(Cross(p2 - p0, p1 - p0)), &dpdu, &dpdv);
-    si.p = ti.b0 * p0 + ti.b1 * p1 + ti.b2 * p2;
-    si.err = gamma(7) * (Abs(ti.b0 * p0) + Abs(ti.b1 * p1) + Abs(ti.b2 * p2));
+    Point3fi(ti.b0 * p0 + ti.b1 * p1 + ti.b2 * p2, gamma(7) * (Abs(ti.b0 * p0) + Abs(ti.b1 * p1) + Abs(ti.b2 * p2)),
+             &si.p, &si.err);
     si.n = Normalize(Cross(dp02, dp12));
     if (flip) si.n = -si.n;
     si.ns = si.n;
@@ -721,12 +739,12 @@ static bool TriangleSample(Vec p0, Vec p1, Vec p2, bool flip, Vec ref, Vec ns, F
         Vec p = b[0] * p0 + b[1] * p1 + b[2] * p2;
         Vec n = Normalize(Cross(p1 - p0, p2 - p0));
         if (flip) n = n * -1.f;
-        ss->err = gamma(6) * (Abs(b[0] * p0) + Abs(b[1] * p1) + Abs((1 - b[0] - b[1]) * p2));
+        Point3fi(p, gamma(6) * (Abs(b[0] * p0) + Abs(b[1] * p1) + Abs((1 - b[0] - b[1]) * p2)), &p, &ss->err);
         Float pdf = 1 / TriArea(p0, p1, p2);
         Vec wi = p - ref;
         if (LengthSquared(wi) == 0) return false;
         wi = Normalize(wi);
-        pdf /= AbsDot(n, -wi) / DistanceSquared(ref, p);
+        pdf /= AbsDotN(n, -wi) / DistanceSquared(ref, p);
         if (std::isinf(pdf)) return false;
         ss->p = p;
         ss->n = n;
@@ -736,8 +754,8 @@ static bool TriangleSample(Vec p0, Vec p1, Vec p2, bool flip, Vec ref, Vec ns, F
     Float pdf = 1;
     if (ns != Vec(0, 0, 0)) {
         Vec w0 = Normalize(p0 - ref), w1 = Normalize(p1 - ref), w2 = Normalize(p2 - ref);
-        Float w[4] = {std::max<Float>(0.01, AbsDot(ns, w1)), std::max<Float>(0.01, AbsDot(ns, w1)),
-                      std::max<Float>(0.01, AbsDot(ns, w0)), std::max<Float>(0.01, AbsDot(ns, w2))};
+        Float w[4] = {std::max<Float>(0.01, AbsDotN(ns, w1)), std::max<Float>(0.01, AbsDotN(ns, w1)),
+                      std::max<Float>(0.01, AbsDotN(ns, w0)), std::max<Float>(0.01, AbsDotN(ns, w2))};
         Float x, y;
         SampleBilinear(u0, u1, w, &x, &y);
         u0 = x;
@@ -748,8 +766,8 @@ static bool TriangleSample(Vec p0, Vec p1, Vec p2, bool flip, Vec ref, Vec ns, F
     SampleSphericalTriangle(p0, p1, p2, ref, u0, u1, b, &triPDF);
     if (triPDF == 0) return false;
     pdf *= triPDF;
-    ss->err = gamma(6) * (Abs(b[0] * p0) + Abs(b[1] * p1) + Abs((1 - b[0] - b[1]) * p2));
-    ss->p = b[0] * p0 + b[1] * p1 + b[2] * p2;
+    Point3fi(b[0] * p0 + b[1] * p1 + b[2] * p2, gamma(6) * (Abs(b[0] * p0) + Abs(b[1] * p1) + Abs((1 - b[0] - b[1]) * p2)),
+             &ss->p, &ss->err);
     Vec n = Normalize(Cross(p1 - p0, p2 - p0));
     if (flip) n = n * -1.f;
     ss->n = n;
@@ -763,7 +781,7 @@ static Float TrianglePDF(Vec p0, Vec p1, Vec p2, bool flip, Vec ref, Vec refErr,
         TriIsect ti;
         if (!IntersectTriangle(o, wi, Infinity, p0, p1, p2, &ti)) return 0;
         Interaction si = TriangleInteraction(p0, p1, p2, flip, ti, wi);
-        Float pdf = (1 / TriArea(p0, p1, p2)) / (AbsDot(si.n, -wi) / DistanceSquared(ref, si.p));
+        Float pdf = (1 / TriArea(p0, p1, p2)) / (AbsDotN(si.n, -wi) / DistanceSquared(ref, si.p));
         if (std::isinf(pdf)) pdf = 0;
         return pdf;
     }
@@ -772,8 +790,8 @@ static Float TrianglePDF(Vec p0, Vec p1, Vec p2, bool flip, Vec ref, Vec refErr,
         Float u0, u1;
         InvertSphericalTriangleSample(p0, p1, p2, ref, wi, &u0, &u1);
         Vec w0 = Normalize(p0 - ref), w1 = Normalize(p1 - ref), w2 = Normalize(p2 - ref);
-        Float w[4] = {std::max<Float>(0.01, AbsDot(ns, w1)), std::max<Float>(0.01, AbsDot(ns, w1)),
-                      std::max<Float>(0.01, AbsDot(ns, w0)), std::max<Float>(0.01, AbsDot(ns, w2))};
+        Float w[4] = {std::max<Float>(0.01, AbsDotN(ns, w1)), std::max<Float>(0.01, AbsDotN(ns, w1)),
+                      std::max<Float>(0.01, AbsDotN(ns, w0)), std::max<Float>(0.01, AbsDotN(ns, w2))};
         pdf *= BilinearPDF(u0, u1, w);
     }
     return pdf;
@@ -811,7 +829,7 @@ static Float Importance(const LightNode &b, Vec p, Vec n) {
     if (cosThetap <= b.cosE) return 0;
     Float imp = b.phi * cosThetap / d2;
     if (n != Vec(0, 0, 0)) {
-        Float cosI = AbsDot(wi, n), sinI = SafeSqrt(1 - Sqr(cosI));
+        Float cosI = AbsDotN(n, wi), sinI = SafeSqrt(1 - Sqr(cosI));
         imp *= CosSub(sinI, cosI, sinB, cosB);
     }
     return std::max<Float>(imp, 0);
@@ -988,7 +1006,7 @@ struct Renderer {
             Interaction si = TriangleInteraction(p0, p1, p2, flip, ti, rd);
             // HandleEmissiveIntersection
             int light = f->tri_light[prim];
-            if (light >= 0 && (f->light_two_sided[light] || Dot(si.n, si.wo) >= 0)) {
+            if (light >= 0 && (f->light_two_sided[light] || DotN(si.n, si.wo) >= 0)) {
                 Spectrum Le = LightL(light, lambda);
                 if (Le) {
                     if (depth == 0 || specularBounce) L = L + beta * Le / r_u.Average();
@@ -1037,7 +1055,7 @@ struct Renderer {
                 Spectrum fv = R * InvPi;
                 if (fv && pdf != 0 && wiL.z != 0) {
                     Vec wi = fromLocal(wiL);
-                    nb = beta * fv * AbsDot(wi, si.ns) / pdf;
+                    nb = beta * fv * AbsDotN(si.ns, wi) / pdf;
                     nrl = r_u / pdf;
                     Spectrum rrBeta = nb * etaScale / r_u.Average();
                     if (rrBeta.Max() < 1 && depth >= 1) {
@@ -1064,12 +1082,12 @@ struct Renderer {
                         ss.pdf != 0 && LengthSquared(ss.p - cp) != 0) {
                         Vec wi = Normalize(ss.p - cp);
                         Spectrum Le(0.f);
-                        if (f->light_two_sided[li] || Dot(ss.n, -wi) >= 0) Le = LightL(li, lambda);
+                        if (f->light_two_sided[li] || DotN(ss.n, -wi) >= 0) Le = LightL(li, lambda);
                         if (Le) {
                             Vec wiL = toLocal(wi);
                             Spectrum fv = (woL.z != 0 && woL.z * wiL.z > 0) ? R * InvPi : Spectrum(0.f);
                             if (fv) {
-                                Spectrum b2 = oldBeta * fv * AbsDot(wi, si.ns);
+                                Spectrum b2 = oldBeta * fv * AbsDotN(si.ns, wi);
                                 Float lightPDF = ss.pdf * lpmf;
                                 Float bsdfPDF = (woL.z != 0 && woL.z * wiL.z > 0) ? std::abs(wiL.z) * InvPi : 0;
                                 Spectrum ru = r_u * bsdfPDF, rl = r_u * lightPDF;
@@ -1149,6 +1167,23 @@ int oracle_render(const pbrt_scene_flat *flat, const pbrt_scene_info *info, cons
     return 0;
 }
 
+// closest / any hit for an SoA ray batch rays[7][n] (o, d, tMax); prim = original triangle
+int oracle_intersect_batch(const pbrt_scene_flat *flat, const pbrt_scene_info *info, const float *rays, int n,
+                           int anyHit, int32_t *prim, float *hit) {
+    Scene S;
+    S.Init(flat, info);
+    for (int i = 0; i < n; ++i) {
+        Vec o(rays[i], rays[n + i], rays[2 * n + i]), d(rays[3 * n + i], rays[4 * n + i], rays[5 * n + i]);
+        TriIsect ti{0, 0, 0, 0};
+        prim[i] = S.Intersect(o, d, rays[6 * n + i], &ti, anyHit != 0);
+        hit[i] = ti.b0;
+        hit[n + i] = ti.b1;
+        hit[2 * n + i] = ti.b2;
+        hit[3 * n + i] = ti.t;
+    }
+    return 0;
+}
+
 // ---- component entry points checked against tests/golden/reference_components.json
 int oracle_intersect_triangle(const float *p9, const float *o3, const float *d3, float tMax, int flip, float *out) {
     // out: b0 b1 b2 t | p3 err3 n3 dpdu3 wo3
@@ -1212,8 +1247,9 @@ float oracle_light_importance(const float *decoded11, float phi, int twoSided, c
 }
 
 void oracle_offset_ray_origin(const float *p3, const float *e3, const float *n3, const float *w3, float *out) {
-    Vec po = OffsetRayOrigin(Vec(p3[0], p3[1], p3[2]), Vec(e3[0], e3[1], e3[2]), Vec(n3[0], n3[1], n3[2]),
-                             Vec(w3[0], w3[1], w3[2]));
+    Vec pm, em;  // the reference call site passes Point3fi(p, e)
+    Point3fi(Vec(p3[0], p3[1], p3[2]), Vec(e3[0], e3[1], e3[2]), &pm, &em);
+    Vec po = OffsetRayOrigin(pm, em, Vec(n3[0], n3[1], n3[2]), Vec(w3[0], w3[1], w3[2]));
     out[0] = po.x;
     out[1] = po.y;
     out[2] = po.z;

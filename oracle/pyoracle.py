@@ -30,6 +30,13 @@ def lib():
         _lib.oracle_light_importance.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         _lib.oracle_sample_wavelengths.argtypes = [ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p]
         _lib.oracle_halton.argtypes = [ctypes.c_int] * 7
+        vp = ctypes.c_void_p
+        _lib.oracle_warps.argtypes = [vp, vp, vp]
+        _lib.oracle_spherical_triangle.argtypes = [vp, vp, vp, vp]
+        _lib.oracle_triangle_sample.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, vp]
+        _lib.oracle_offset_ray_origin.argtypes = [vp, vp, vp, vp, vp]
+        _lib.oracle_render.argtypes = [vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_int, vp]
     return _lib
 
 
@@ -53,6 +60,20 @@ def render(scene, rows=None, first_sample=0, n_samples=None, threads=None):
                              int(threads), film.ctypes.data_as(ctypes.c_void_p))
     assert rc == 0
     return film
+
+
+def intersect(scene, rays, any_hit=False):
+    """rays: float32 [7, n] (o, d, tMax) -> (prim int32 [n], hit float32 [4, n])"""
+    info = scene.info
+    flat = scene.flat()
+    rays = np.ascontiguousarray(rays, dtype=np.float32)
+    n = rays.shape[1]
+    prim = np.zeros(n, np.int32)
+    hit = np.zeros((4, n), np.float32)
+    lib().oracle_intersect_batch(ctypes.byref(flat), ctypes.byref(info), rays.ctypes.data_as(ctypes.c_void_p), n,
+                                 int(any_hit), prim.ctypes.data_as(ctypes.c_void_p),
+                                 hit.ctypes.data_as(ctypes.c_void_p))
+    return prim, hit
 
 
 def film_to_rgb(film, m3x3):

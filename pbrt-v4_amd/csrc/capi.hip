@@ -134,6 +134,7 @@ struct pbrt_context {
     DevBuf<int> iState;
     DevBuf<int> rows;
     DevBuf<double> film;
+    DevBuf<unsigned long long> devStats;
     PathState st{};
     // timing
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
@@ -324,6 +325,11 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
     st.matQ = takei(1);
     st.shadowQ = takei(1);
     st.counters = ip;
+    if (!c->devStats.p) {
+        c->devStats.Alloc(8);
+        HIPCHECK(hipMemset(c->devStats.p, 0, 8 * sizeof(unsigned long long)));
+    }
+    st.stats = c->devStats.p;
 }
 
 static void RecordEvent(pbrt_context *c, bool start) {
@@ -389,7 +395,6 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
             }
             HIPCHECK(LaunchFilm(c->S, st, nS, c->stream));
             c->stats.passes++;
-            c->stats.camera_rays += nActive;
             c->stats.paths_per_pass = std::max<uint64_t>(c->stats.paths_per_pass, nActive);
         }
     }
@@ -567,6 +572,11 @@ int pbrt_synchronize(pbrt_context *ctx) {
             ctx->stats.closest_launches++;
         }
         ctx->eventsUsed = 0;
+        unsigned long long ds[8];
+        HIPCHECK(hipMemcpy(ds, ctx->devStats.p, sizeof ds, hipMemcpyDeviceToHost));
+        ctx->stats.camera_rays = ds[0];
+        ctx->stats.closest_rays = ds[1];
+        ctx->stats.shadow_rays = ds[2];
         return 0;
     } catch (const std::exception &e) {
         return Fail(e.what());
@@ -579,8 +589,16 @@ int pbrt_get_stats(pbrt_context *ctx, pbrt_render_stats *stats) {
 }
 
 int pbrt_reset_stats(pbrt_context *ctx) {
-    ctx->stats = pbrt_render_stats{};
-    return 0;
+    try {
+        HIPCHECK(hipSetDevice(ctx->device));
+        HIPCHECK(hipStreamSynchronize(ctx->stream));
+        HIPCHECK(hipMemset(ctx->devStats.p, 0, 8 * sizeof(unsigned long long)));
+        ctx->stats = pbrt_render_stats{};
+        ctx->eventsUsed = 0;
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
 }
 
 int pbrt_film_clear(pbrt_context *ctx) {

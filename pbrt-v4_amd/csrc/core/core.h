@@ -80,7 +80,7 @@ PHD float SumOfProducts(float a, float b, float c, float d) {
     return sop + err;
 }
 
-// ---------------------------------------------------------------- vectors
+// ---------------------------------------------------------------- vectors (DotN defined below)
 struct V3 {
     float x, y, z;
     PHD V3() : x(0), y(0), z(0) {}
@@ -100,11 +100,17 @@ PHD V3 Abs(V3 a) { return {std::fabs(a.x), std::fabs(a.y), std::fabs(a.z)}; }
 // util/vecmath.h:966 (plain, left to right)
 PHD float Dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 PHD float AbsDot(V3 a, V3 b) { return std::fabs(Dot(a, b)); }
+// Dot products that involve a Normal3f are FMA-compensated in pbrt (util/vecmath.h:1059-1099):
+// FMA(n.x, v.x, SumOfProducts(n.y, v.y, n.z, v.z)).  n is the normal operand.
+PHD float DotN(V3 n, V3 v);
+PHD float AbsDotN(V3 n, V3 v);
 // util/vecmath.h:1001 Cross via DifferenceOfProducts
 PHD V3 Cross(V3 v, V3 w) {
     return {DifferenceOfProducts(v.y, w.z, v.z, w.y), DifferenceOfProducts(v.z, w.x, v.x, w.z),
             DifferenceOfProducts(v.x, w.y, v.y, w.x)};
 }
+PHD float DotN(V3 n, V3 v) { return fmaf(n.x, v.x, SumOfProducts(n.y, v.y, n.z, v.z)); }
+PHD float AbsDotN(V3 n, V3 v) { return std::fabs(DotN(n, v)); }
 PHD float LengthSquared(V3 v) { return Sqr(v.x) + Sqr(v.y) + Sqr(v.z); }
 PHD float Length(V3 v) { return std::sqrt(LengthSquared(v)); }
 PHD V3 Normalize(V3 v) { return v / Length(v); }
@@ -319,9 +325,9 @@ PHD void InvertSphericalTriangleSample(V3 v0, V3 v1, V3 v2, V3 p, V3 w, float *u
 // ---------------------------------------------------------------- rays and triangles
 // ray.h:78 OffsetRayOrigin; error vector e is the Point3fi half-width
 PHD V3 OffsetRayOrigin(V3 p, V3 e, V3 n, V3 w) {
-    float d = Dot(Abs(n), e);
+    float d = DotN(Abs(n), e);
     V3 offset = d * n;
-    if (Dot(w, n) < 0) offset = -offset;
+    if (DotN(n, w) < 0) offset = -offset;
     V3 po = p + offset;
     for (int i = 0; i < 3; ++i) {
         if (offset[i] > 0)
@@ -330,6 +336,22 @@ PHD V3 OffsetRayOrigin(V3 p, V3 e, V3 n, V3 w) {
             po[i] = NextFloatDown(po[i]);
     }
     return po;
+}
+
+// Point3fi(Point3f p, Vector3f e) (util/vecmath.h:753) stores intervals built with
+// Interval::FromValueAndError (util/math.h:829) using the CPU rounding helpers
+// AddRoundUp/AddRoundDown = NextFloatUp/Down(a + b) (util/float.h:201-229); Point3f(pi) is
+// the interval midpoint and pi.Error() its half width.  Round-trip (p, e) the same way.
+PHD void ToPoint3fi(V3 v, V3 e, V3 *p, V3 *err) {
+    for (int i = 0; i < 3; ++i) {
+        float lo = v[i], hi = v[i];
+        if (e[i] != 0) {
+            lo = NextFloatDown(v[i] + (-e[i]));
+            hi = NextFloatUp(v[i] + e[i]);
+        }
+        (*p)[i] = (lo + hi) / 2;
+        (*err)[i] = (hi - lo) / 2;
+    }
 }
 
 struct TriHit {
@@ -427,9 +449,9 @@ PHD TriSurface TriangleSurface(V3 p0, V3 p1, V3 p2, float b0, float b1, float b2
         V3 ng = Cross(p2 - p0, p1 - p0);
         CoordinateSystem(Normalize(ng), &dpdu, &dpdv);
     }
-    s.p = b0 * p0 + b1 * p1 + b2 * p2;
+    V3 pHit = b0 * p0 + b1 * p1 + b2 * p2;
     V3 pAbsSum = Abs(b0 * p0) + Abs(b1 * p1) + Abs(b2 * p2);
-    s.pErr = gamma(7) * pAbsSum;
+    ToPoint3fi(pHit, gamma(7) * pAbsSum, &s.p, &s.pErr);
     V3 n = Normalize(Cross(dp02, dp12));
     if (flip) n = -n;
     s.n = n;
@@ -548,7 +570,7 @@ PHD float LightImportance(const LightNodeBounds &lb, V3 p, V3 n) {
     if (cosThetap <= lb.cosTheta_e) return 0;
     float importance = lb.phi * cosThetap / d2;
     if (n != V3(0, 0, 0)) {
-        float cosTheta_i = AbsDot(wi, n);
+        float cosTheta_i = AbsDotN(n, wi);
         float sinTheta_i = SafeSqrt(1 - Sqr(cosTheta_i));
         float cosThetap_i = CosSubClamped(sinTheta_i, cosTheta_i, sinTheta_b, cosTheta_b);
         importance *= cosThetap_i;

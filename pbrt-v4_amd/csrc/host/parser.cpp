@@ -593,6 +593,42 @@ class Parser {
     }
 };
 
+static std::array<float, 311> DensePiecewiseLinear(const std::vector<double> &nums, const std::string &loc) {
+    if (nums.size() % 2) throw Error(loc + ": odd number of values in spectrum");
+    std::vector<float> lam, val;
+    for (size_t i = 0; i < nums.size(); i += 2) {
+        if (!lam.empty() && (float)nums[i] <= lam.back()) throw Error(loc + ": spectrum wavelengths not increasing");
+        lam.push_back((float)nums[i]);
+        val.push_back((float)nums[i + 1]);
+    }
+    std::array<float, 311> out;
+    for (int l = 395; l <= 705; ++l) {
+        float lambda = (float)l;
+        float v = 0;
+        if (!(lambda < lam.front() || lambda > lam.back())) {
+            size_t o = 0;
+            while (o + 2 < lam.size() && lam[o + 1] <= lambda) ++o;
+            if (lam.size() == 1)
+                v = val[0];
+            else {
+                float t = (lambda - lam[o]) / (lam[o + 1] - lam[o]);
+                v = Lerpf(t, val[o], val[o + 1]);
+            }
+        }
+        out[l - 395] = v;
+    }
+    return out;
+}
+
+static float PhotometricOf(const std::array<float, 311> &dense) {
+    // SpectrumToPhotometric (util/spectrum.cpp:37-51) over the dense samples
+    const SpectralData &d = GetSpectralData();
+    float y = 0;
+    for (float lambda = kLambdaMin; lambda <= kLambdaMax; ++lambda)
+        y += d.denseY[DenseOffset(lambda)] * dense[DenseOffset(lambda)];
+    return y;
+}
+
 void Parser::Finish() {
     if (!haveCamera) {
         cameraFromWorld = Identity4();
@@ -745,19 +781,28 @@ void Parser::Finish() {
             Param *L = ap.Find("L");
             float rgb[3] = {0, 0, 0};
             std::array<float, 311> dense;
+            float photometric = GetSpectralData().photometricD65;
+            std::string spectrumKey;
             if (!L) {
                 dense = GetSpectralData().denseD65;  // colorSpace->illuminant
             } else if (L->type == "rgb") {
                 if (L->nums.size() != 3) throw Error(ap.loc + ": L needs 3 values");
                 for (int i = 0; i < 3; ++i) rgb[i] = (float)L->nums[i];
                 dense = DenseRGBIlluminant(rgb[0], rgb[1], rgb[2]);
+            } else if (L->type == "spectrum" && !L->nums.empty()) {
+                // PiecewiseLinearSpectrum from (lambda, value) pairs (paramdict.cpp:415-439)
+                dense = DensePiecewiseLinear(L->nums, ap.loc);
+                photometric = PhotometricOf(dense);
+                rgb[0] = -1;
+                spectrumKey = "pl:" + std::to_string(scene.denseSpectra.size());
             } else if (L->type == "blackbody") {
                 throw Error(ap.loc + ": blackbody L not supported yet");
             } else {
                 throw Error(ap.loc + ": L of type " + L->type + " not supported");
             }
-            std::string key = std::to_string(rgb[0]) + "," + std::to_string(rgb[1]) + "," + std::to_string(rgb[2]) +
-                              (L ? "" : "D65");
+            std::string key = spectrumKey.empty() ? std::to_string(rgb[0]) + "," + std::to_string(rgb[1]) + "," +
+                                                        std::to_string(rgb[2]) + (L ? "" : "D65")
+                                                  : spectrumKey;
             if (!spectrumCache.count(key)) {
                 scene.denseSpectra.push_back(dense);
                 spectrumCache[key] = (int)scene.denseSpectra.size() - 1;
@@ -766,7 +811,7 @@ void Parser::Finish() {
             lightScale = (float)ap.GetFloat("scale", 1);
             twoSided = ap.GetBool("twosided", false);
             // lights.cpp:941: scale /= SpectrumToPhotometric(L) (illuminant part only)
-            lightScale /= GetSpectralData().photometricD65;
+            lightScale /= photometric;
             if (ap.GetFloat("power", -1) > 0) throw Error(ap.loc + ": \"power\" not supported yet");
             float spread = (float)ap.GetFloat("spread", 90);
             if (spread != 90) throw Error(ap.loc + ": \"spread\" other than 90 not supported yet");
@@ -803,13 +848,17 @@ void Parser::Finish() {
         std::array<float, 311> dense;
         if (!L)
             dense = GetSpectralData().denseD65;
-        else if (L->type == "rgb" && L->nums.size() == 3)
+        float photometric = GetSpectralData().photometricD65;
+        if (L && L->type == "rgb" && L->nums.size() == 3)
             dense = DenseRGBIlluminant((float)L->nums[0], (float)L->nums[1], (float)L->nums[2]);
-        else
-            throw Error(l.params.loc + ": infinite light L must be rgb");
+        else if (L && L->type == "spectrum" && !L->nums.empty()) {
+            dense = DensePiecewiseLinear(L->nums, l.params.loc);
+            photometric = PhotometricOf(dense);
+        } else if (L)
+            throw Error(l.params.loc + ": infinite light L must be rgb or spectrum");
         scene.denseSpectra.push_back(dense);
         il.spectrum = (int)scene.denseSpectra.size() - 1;
-        il.scale = (float)l.params.GetFloat("scale", 1) / GetSpectralData().photometricD65;
+        il.scale = (float)l.params.GetFloat("scale", 1) / photometric;
         if (l.params.Find("illuminance")) throw Error(l.params.loc + ": illuminance not supported yet");
         l.params.CheckUnused();
         scene.infiniteLights.push_back(il);

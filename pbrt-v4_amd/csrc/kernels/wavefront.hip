@@ -242,12 +242,12 @@ __device__ inline bool SampleTriangle(V3 p0, V3 p1, V3 p2, bool flip, V3 refP, V
         V3 n = Normalize(Cross(p1 - p0, p2 - p0));
         if (flip) n = n * -1.f;
         V3 pAbsSum = Abs(b[0] * p0) + Abs(b[1] * p1) + Abs((1 - b[0] - b[1]) * p2);
-        *pErr = gamma(6) * pAbsSum;
+        ToPoint3fi(p, gamma(6) * pAbsSum, &p, pErr);
         float pdf = 1 / TriArea(p0, p1, p2);
         V3 wi = p - refP;
         if (LengthSquared(wi) == 0) return false;
         wi = Normalize(wi);
-        pdf /= AbsDot(n, -wi) / DistanceSquared(refP, p);
+        pdf /= AbsDotN(n, -wi) / DistanceSquared(refP, p);
         if (isinf(pdf)) return false;
         *ps = p;
         *ns = n;
@@ -257,8 +257,8 @@ __device__ inline bool SampleTriangle(V3 p0, V3 p1, V3 p2, bool flip, V3 refP, V
     float pdf = 1;
     if (refNs != V3(0, 0, 0)) {
         V3 wi0 = Normalize(p0 - refP), wi1 = Normalize(p1 - refP), wi2 = Normalize(p2 - refP);
-        float w[4] = {fmaxf(0.01f, AbsDot(refNs, wi1)), fmaxf(0.01f, AbsDot(refNs, wi1)),
-                      fmaxf(0.01f, AbsDot(refNs, wi0)), fmaxf(0.01f, AbsDot(refNs, wi2))};
+        float w[4] = {fmaxf(0.01f, AbsDotN(refNs, wi1)), fmaxf(0.01f, AbsDotN(refNs, wi1)),
+                      fmaxf(0.01f, AbsDotN(refNs, wi0)), fmaxf(0.01f, AbsDotN(refNs, wi2))};
         float px, py;
         SampleBilinear(u0, u1, w, &px, &py);
         u0 = px;
@@ -271,8 +271,8 @@ __device__ inline bool SampleTriangle(V3 p0, V3 p1, V3 p2, bool flip, V3 refP, V
     if (triPDF == 0) return false;
     pdf *= triPDF;
     V3 pAbsSum = Abs(b[0] * p0) + Abs(b[1] * p1) + Abs((1 - b[0] - b[1]) * p2);
-    *pErr = gamma(6) * pAbsSum;
-    V3 p = b[0] * p0 + b[1] * p1 + b[2] * p2;
+    V3 p;
+    ToPoint3fi(b[0] * p0 + b[1] * p1 + b[2] * p2, gamma(6) * pAbsSum, &p, pErr);
     V3 n = Normalize(Cross(p1 - p0, p2 - p0));
     if (flip) n = n * -1.f;
     *ps = p;
@@ -291,10 +291,9 @@ __device__ inline float TrianglePDF(const DeviceScene &S, int prim, V3 refP, V3 
         V3 o = OffsetRayOrigin(refP, refPErr, refN, wi);
         TriHit h;
         if (!IntersectTriangle(o, wi, kInfinity, p0, p1, p2, &h)) return 0;
-        V3 pHit = h.b0 * p0 + h.b1 * p1 + h.b2 * p2;
-        V3 n = Normalize(Cross(p0 - p2, p1 - p2));
-        if (S.primFlip[prim]) n = -n;
-        float pdf = (1 / TriArea(p0, p1, p2)) / (AbsDot(n, -wi) / DistanceSquared(refP, pHit));
+        TriSurface hs = TriangleSurface(p0, p1, p2, h.b0, h.b1, h.b2, S.primFlip[prim]);
+        V3 pHit = hs.p, n = hs.n;
+        float pdf = (1 / TriArea(p0, p1, p2)) / (AbsDotN(n, -wi) / DistanceSquared(refP, pHit));
         if (isinf(pdf)) pdf = 0;
         return pdf;
     }
@@ -303,8 +302,8 @@ __device__ inline float TrianglePDF(const DeviceScene &S, int prim, V3 refP, V3 
         float u0, u1;
         InvertSphericalTriangleSample(p0, p1, p2, refP, wi, &u0, &u1);
         V3 wi0 = Normalize(p0 - refP), wi1 = Normalize(p1 - refP), wi2 = Normalize(p2 - refP);
-        float w[4] = {fmaxf(0.01f, AbsDot(refNs, wi1)), fmaxf(0.01f, AbsDot(refNs, wi1)),
-                      fmaxf(0.01f, AbsDot(refNs, wi0)), fmaxf(0.01f, AbsDot(refNs, wi2))};
+        float w[4] = {fmaxf(0.01f, AbsDotN(refNs, wi1)), fmaxf(0.01f, AbsDotN(refNs, wi1)),
+                      fmaxf(0.01f, AbsDotN(refNs, wi0)), fmaxf(0.01f, AbsDotN(refNs, wi2))};
         pdf *= BilinearPDF(u0, u1, w);
     }
     return pdf;
@@ -381,6 +380,7 @@ __global__ void __launch_bounds__(kBlock) k_camera(DeviceScene S, PathState st, 
     int slot = blockIdx.x * blockDim.x + threadIdx.x;
     if (slot == 0) {
         st.counters[0] = nActive;  // depth-0 ray queue = every slot
+        atomicAdd(&st.stats[0], (unsigned long long)nActive);
     }
     if (slot >= nActive) return;
     int px, py, sampleIndex;
@@ -454,6 +454,7 @@ __global__ void __launch_bounds__(kBlock) k_closest(DeviceScene S, PathState st,
     const int *q = st.rayQ[depth & 1];
     const int count = st.counters[depth * 4 + 0];
     int *matCounter = &st.counters[depth * 4 + 1];
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&st.stats[1], (unsigned long long)count);
     for (int base = blockIdx.x * blockDim.x; base < count; base += gridDim.x * blockDim.x) {
         int qi = base + threadIdx.x;
         bool active = qi < count;
@@ -543,7 +544,7 @@ __global__ void __launch_bounds__(kBlock) k_shade_diffuse(DeviceScene S, PathSta
             int light = S.primLight[prim];
             if (light >= 0) {
                 bool twoSided = S.lightTwoSided[light];
-                if (twoSided || Dot(n, wo) >= 0) {
+                if (twoSided || DotN(n, wo) >= 0) {
                     const float *dense = S.dense + S.lightSpectrum[light] * kDenseN;
                     float scale = S.lightScale[light];
                     float Le[kNSpectrumSamples];
@@ -615,7 +616,7 @@ __global__ void __launch_bounds__(kBlock) k_shade_diffuse(DeviceScene S, PathSta
                     float pdf = CosineHemispherePDF(fabsf(wiL.z));
                     if (pdf != 0 && wiL.z != 0) {
                         V3 wi = frame.FromLocal(wiL);
-                        float absdot = AbsDot(wi, ns);
+                        float absdot = AbsDotN(ns, wi);
                         float nb[kNSpectrumSamples];
                         float mx = -kInfinity;
                         bool nz = false;
@@ -679,7 +680,7 @@ __global__ void __launch_bounds__(kBlock) k_shade_diffuse(DeviceScene S, PathSta
                             V3 wi = Normalize(lp - cp);
                             // DiffuseAreaLight::L(p, n, uv, -wi)
                             bool lTwo = S.lightTwoSided[li];
-                            if (lTwo || Dot(ln, -wi) >= 0) {
+                            if (lTwo || DotN(ln, -wi) >= 0) {
                                 const float *dense = S.dense + S.lightSpectrum[li] * kDenseN;
                                 float scale = S.lightScale[li];
                                 float Le[kNSpectrumSamples];
@@ -692,7 +693,7 @@ __global__ void __launch_bounds__(kBlock) k_shade_diffuse(DeviceScene S, PathSta
                                 V3 wiL = frame.ToLocal(wi);
                                 bool same = woL.z * wiL.z > 0;
                                 if (nz && woL.z != 0 && same) {
-                                    float absdot = AbsDot(wi, ns);
+                                    float absdot = AbsDotN(ns, wi);
                                     float lightPDF = lpdf * lpmf;
                                     float bsdfPDF = CosineHemispherePDF(fabsf(wiL.z));
                                     float denom = Avg31(bsdfPDF + lightPDF);
@@ -732,6 +733,7 @@ __global__ void __launch_bounds__(kBlock) k_shade_diffuse(DeviceScene S, PathSta
 __global__ void __launch_bounds__(kBlock) k_shadow(DeviceScene S, PathState st, int depth) {
     int N = st.N;
     const int count = st.counters[depth * 4 + 2];
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&st.stats[2], (unsigned long long)count);
     for (int qi = blockIdx.x * blockDim.x + threadIdx.x; qi < count; qi += gridDim.x * blockDim.x) {
         int slot = st.shadowQ[qi];
         V3 o(st.shadowRay[slot], st.shadowRay[N + slot], st.shadowRay[2 * N + slot]);

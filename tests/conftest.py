@@ -1,0 +1,42 @@
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "pbrt-v4_amd"))
+sys.path.insert(0, str(ROOT / "oracle"))
+sys.path.insert(0, str(ROOT))
+
+GOLDEN = ROOT / "tests" / "golden"
+SCENES = ROOT / "scenes"
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); parity tests through the C ABI")
+
+
+@pytest.fixture(scope="session")
+def golden():
+    import json
+    return json.loads((GOLDEN / "reference_components.json").read_text())
+
+
+@pytest.fixture(scope="session")
+def pa():
+    import pbrt_amd
+    return pbrt_amd
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    import pyoracle
+    pyoracle.lib()
+    return pyoracle
+
+
+def fl(v):
+    """golden JSON floats ('inf'/'nan' strings) -> float"""
+    if isinstance(v, list):
+        return [fl(x) for x in v]
+    return float(v)

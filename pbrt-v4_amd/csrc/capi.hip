@@ -19,6 +19,7 @@ namespace pbrt_amd {
 hipError_t LaunchCamera(const DeviceScene &S, const PathState &st, int nActive, hipStream_t s);
 hipError_t LaunchClosest(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
 hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
+hipError_t LaunchEscaped(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
 hipError_t LaunchShadow(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
 hipError_t LaunchFilm(const DeviceScene &S, const PathState &st, int nSamples, hipStream_t s);
 hipError_t LaunchIntersectBatch(const DeviceScene &S, const float *rays, int n, int anyHit, int *outPrim,
@@ -127,6 +128,8 @@ struct pbrt_context {
     DevBuf<uint8_t> primFlip;
     DevBuf<uint32_t> lightBitTrail, permOffset, permNDigits, permBase;
     DevBuf<uint16_t> perm;
+    DevBuf<uint32_t> haltonDim;
+    DevBuf<float> sensor4;
     DevBuf<DeviceLightNode> lightNodes;
     // wavefront buffers
     int64_t maxPaths = 0;
@@ -157,7 +160,9 @@ static void BuildDevice(pbrt_context *c) {
     HIPCHECK(hipSetDevice(c->device));
     HIPCHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     c->bvh = BuildBVH8(s.verts, s.tris, 4);
-    if (7 * c->bvh.maxDepth + 1 > 64) throw Error("BVH too deep for the traversal stack");
+    if (c->bvh.maxStack > kMaxStackSize)
+        throw Error("BVH needs a " + std::to_string(c->bvh.maxStack) + "-entry traversal stack (limit " +
+                    std::to_string(kMaxStackSize) + ")");
     BVH8 &b = c->bvh;
     int nt = (int)s.tris.size();
     std::vector<int> origToLeaf(nt);
@@ -214,6 +219,13 @@ static void BuildDevice(pbrt_context *c) {
     sensor.insert(sensor.end(), s.sensorY.begin(), s.sensorY.end());
     sensor.insert(sensor.end(), s.sensorZ.begin(), s.sensorZ.end());
     c->sensor.Upload(sensor);
+    std::vector<float> sensor4(4 * kDenseN, 0.f);
+    for (int i = 0; i < kDenseN; ++i) {
+        sensor4[4 * i] = s.sensorX[i];
+        sensor4[4 * i + 1] = s.sensorY[i];
+        sensor4[4 * i + 2] = s.sensorZ[i];
+    }
+    c->sensor4.Upload(sensor4);
     std::vector<uint32_t> bt(s.areaLights.size(), 0xffffffffu);
     if (!s.uniformLightSampler)
         for (auto &n : s.lightNodes)
@@ -226,6 +238,12 @@ static void BuildDevice(pbrt_context *c) {
     c->permOffset.Upload(s.permOffset);
     c->permNDigits.Upload(s.permNDigits);
     c->permBase.Upload(s.permBase);
+    std::vector<uint32_t> hd;
+    for (size_t d = 0; d < s.permBase.size(); ++d) {
+        uint32_t shift, magic = HaltonMagic(s.permBase[d], &shift);
+        hd.insert(hd.end(), {s.permBase[d], s.permNDigits[d] | (shift << 8), s.permOffset[d], magic});
+    }
+    c->haltonDim.Upload(hd);
 
     DeviceScene &S = c->S;
     S.nodes = c->nodes.p;
@@ -252,6 +270,7 @@ static void BuildDevice(pbrt_context *c) {
     S.nLightNodes = (int)s.lightNodes.size();
     S.dense = c->dense.p;
     S.sensor = c->sensor.p;
+    S.sensor4 = (const float4 *)c->sensor4.p;
     S.imagingRatio = s.imagingRatio;
     for (int i = 0; i < 4; ++i)
         for (int j = 0; j < 4; ++j) {
@@ -272,6 +291,7 @@ static void BuildDevice(pbrt_context *c) {
     S.permOffset = c->permOffset.p;
     S.permNDigits = c->permNDigits.p;
     S.permBase = c->permBase.p;
+    S.haltonDim = (const uint4 *)c->haltonDim.p;
     S.nDims = (int)s.permBase.size();
     for (int i = 0; i < 2; ++i) {
         S.baseScales[i] = s.haltonBaseScales[i];
@@ -279,6 +299,7 @@ static void BuildDevice(pbrt_context *c) {
         S.multInverse[i] = s.haltonMultInverse[i];
     }
     S.maxDepth = s.maxDepth;
+    S.stackSize = c->bvh.maxStack;
 
     // film
     size_t npix = (size_t)s.xres * s.yres;
@@ -290,7 +311,7 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
     if (N <= c->maxPaths) return;
     // float arrays: beta 31, rl 1, L 3, lambda0 1, filterW 1, etaScale 1, ray 6, ctx 12, hitB 4,
     // shadowRay 6, shadowL 3  = 69 floats; int arrays: flags, hitPrim, rayQ x2, matQ, shadowQ = 6
-    const int nf = 69, ni = 6;
+    const int nf = 69, ni = 7;
     c->fState.Alloc((size_t)nf * N);
     c->iState.Alloc((size_t)ni * N + 4 * (c->desc.maxDepth + 3));
     c->maxPaths = N;
@@ -324,6 +345,7 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
     st.rayQ[1] = takei(1);
     st.matQ = takei(1);
     st.shadowQ = takei(1);
+    st.escQ = takei(1);
     st.counters = ip;
     if (!c->devStats.p) {
         c->devStats.Alloc(8);
@@ -389,6 +411,7 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
                 if (p->time_closest) RecordEvent(c, true);
                 HIPCHECK(LaunchClosest(c->S, st, depth, (int)nActive, c->stream));
                 if (p->time_closest) RecordEvent(c, false);
+                if (s.infiniteLights.size()) HIPCHECK(LaunchEscaped(c->S, st, depth, (int)nActive, c->stream));
                 HIPCHECK(LaunchShadeDiffuse(c->S, st, depth, (int)nActive, c->stream));
                 if (depth == s.maxDepth) break;
                 HIPCHECK(LaunchShadow(c->S, st, depth, (int)nActive, c->stream));

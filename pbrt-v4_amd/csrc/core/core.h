@@ -209,14 +209,16 @@ PHD int SampleDiscrete2(float w0, float w1, float u, float *pmf, float *uRemappe
     sumWeights += w1;
     float up = u * sumWeights;
     if (up == sumWeights) up = NextFloatDown(up);
+    // offset walk of the reference loop, unrolled for two weights (no indexed array)
     int offset = 0;
     float sum = 0;
-    float wts[2] = {w0, w1};
-    while (sum + wts[offset] <= up) {
-        sum += wts[offset++];
+    if (sum + w0 <= up) {
+        sum += w0;
+        offset = 1;
     }
-    *pmf = wts[offset] / sumWeights;
-    *uRemapped = std::fmin((up - sum) / wts[offset], kOneMinusEpsilon);
+    float w = offset ? w1 : w0;
+    *pmf = w / sumWeights;
+    *uRemapped = std::fmin((up - sum) / w, kOneMinusEpsilon);
     return offset;
 }
 
@@ -358,20 +360,54 @@ struct TriHit {
     float b0, b1, b2, t;
 };
 
-// shapes.cpp:172-273 IntersectTriangle (watertight, fp64 edge fallback)
-PHD bool IntersectTriangle(V3 o, V3 dir, float tMax, V3 p0, V3 p1, V3 p2, TriHit *hit) {
-    if (LengthSquared(Cross(p2 - p0, p1 - p0)) == 0) return false;
-    V3 p0t = p0 - o, p1t = p1 - o, p2t = p2 - o;
-    int kz = MaxComponentIndex(Abs(dir));
-    int kx = kz + 1;
-    if (kx == 3) kx = 0;
-    int ky = kx + 1;
-    if (ky == 3) ky = 0;
-    V3 d = Permute(dir, kx, ky, kz);
-    p0t = Permute(p0t, kx, ky, kz);
-    p1t = Permute(p1t, kx, ky, kz);
-    p2t = Permute(p2t, kx, ky, kz);
-    float Sx = -d.x / d.z, Sy = -d.y / d.z, Sz = 1 / d.z;
+// shapes.cpp:215-225: recompute the edge functions in double when one is exactly zero.
+// Rare, so it is kept out of line (its doubles would otherwise inflate every caller's VGPRs).
+#if defined(__HIPCC__)
+__host__ __device__ inline __attribute__((noinline))
+#else
+inline
+#endif
+void EdgeFunctionsFP64(V3 p0t, V3 p1t, V3 p2t, float *e0, float *e1, float *e2) {
+    double p2txp1ty = (double)p2t.x * (double)p1t.y;
+    double p2typ1tx = (double)p2t.y * (double)p1t.x;
+    *e0 = (float)(p2typ1tx - p2txp1ty);
+    double p0txp2ty = (double)p0t.x * (double)p2t.y;
+    double p0typ2tx = (double)p0t.y * (double)p2t.x;
+    *e1 = (float)(p0typ2tx - p0txp2ty);
+    double p1txp0ty = (double)p1t.x * (double)p0t.y;
+    double p1typ0tx = (double)p1t.y * (double)p0t.x;
+    *e2 = (float)(p1typ0tx - p1txp0ty);
+}
+
+// shapes.cpp:172-273 IntersectTriangle (watertight, fp64 edge fallback), split so that the
+// per-ray part (permutation and shear, shapes.cpp:180-200) is computed once per ray rather
+// than once per triangle; the arithmetic and its order are unchanged.
+struct TriRay {
+    V3 o;
+    int kx, ky, kz;
+    float Sx, Sy, Sz;
+};
+PHD TriRay MakeTriRay(V3 o, V3 dir) {
+    TriRay r;
+    r.o = o;
+    r.kz = MaxComponentIndex(Abs(dir));
+    r.kx = r.kz + 1;
+    if (r.kx == 3) r.kx = 0;
+    r.ky = r.kx + 1;
+    if (r.ky == 3) r.ky = 0;
+    V3 d = Permute(dir, r.kx, r.ky, r.kz);
+    r.Sx = -d.x / d.z;
+    r.Sy = -d.y / d.z;
+    r.Sz = 1 / d.z;
+    return r;
+}
+// Triangle test for a non-degenerate triangle (callers drop degenerate triangles, the
+// shapes.cpp:175 early-out, before calling).
+PHD bool IntersectTriangleRay(const TriRay &r, float tMax, V3 p0, V3 p1, V3 p2, TriHit *hit) {
+    V3 p0t = Permute(p0 - r.o, r.kx, r.ky, r.kz);
+    V3 p1t = Permute(p1 - r.o, r.kx, r.ky, r.kz);
+    V3 p2t = Permute(p2 - r.o, r.kx, r.ky, r.kz);
+    const float Sx = r.Sx, Sy = r.Sy, Sz = r.Sz;
     p0t.x += Sx * p0t.z;
     p0t.y += Sy * p0t.z;
     p1t.x += Sx * p1t.z;
@@ -381,17 +417,7 @@ PHD bool IntersectTriangle(V3 o, V3 dir, float tMax, V3 p0, V3 p1, V3 p2, TriHit
     float e0 = DifferenceOfProducts(p1t.x, p2t.y, p1t.y, p2t.x);
     float e1 = DifferenceOfProducts(p2t.x, p0t.y, p2t.y, p0t.x);
     float e2 = DifferenceOfProducts(p0t.x, p1t.y, p0t.y, p1t.x);
-    if (e0 == 0.0f || e1 == 0.0f || e2 == 0.0f) {
-        double p2txp1ty = (double)p2t.x * (double)p1t.y;
-        double p2typ1tx = (double)p2t.y * (double)p1t.x;
-        e0 = (float)(p2typ1tx - p2txp1ty);
-        double p0txp2ty = (double)p0t.x * (double)p2t.y;
-        double p0typ2tx = (double)p0t.y * (double)p2t.x;
-        e1 = (float)(p0typ2tx - p0txp2ty);
-        double p1txp0ty = (double)p1t.x * (double)p0t.y;
-        double p1typ0tx = (double)p1t.y * (double)p0t.x;
-        e2 = (float)(p1typ0tx - p1txp0ty);
-    }
+    if (e0 == 0.0f || e1 == 0.0f || e2 == 0.0f) EdgeFunctionsFP64(p0t, p1t, p2t, &e0, &e1, &e2);
     if ((e0 < 0 || e1 < 0 || e2 < 0) && (e0 > 0 || e1 > 0 || e2 > 0)) return false;
     float det = e0 + e1 + e2;
     if (det == 0) return false;
@@ -419,6 +445,13 @@ PHD bool IntersectTriangle(V3 o, V3 dir, float tMax, V3 p0, V3 p1, V3 p2, TriHit
     hit->b2 = b2;
     hit->t = t;
     return true;
+}
+
+PHD bool TriangleDegenerate(V3 p0, V3 p1, V3 p2) { return LengthSquared(Cross(p2 - p0, p1 - p0)) == 0; }
+
+PHD bool IntersectTriangle(V3 o, V3 dir, float tMax, V3 p0, V3 p1, V3 p2, TriHit *hit) {
+    if (TriangleDegenerate(p0, p1, p2)) return false;
+    return IntersectTriangleRay(MakeTriRay(o, dir), tMax, p0, p1, p2, hit);
 }
 
 // Surface geometry of a triangle hit without shading normals or uv
@@ -497,6 +530,43 @@ PHD float ScrambledRadicalInverse(uint32_t base, uint32_t nDigits, uint64_t a, c
     for (uint32_t digitIndex = 0; digitIndex < nDigits; ++digitIndex) {
         uint64_t next = a / base;
         int digitValue = (int)(a - next * base);
+        reversedDigits = reversedDigits * base + perm[digitIndex * base + digitValue];
+        invBaseM *= invBase;
+        a = next;
+    }
+    return std::fmin(invBaseM * (float)reversedDigits, kOneMinusEpsilon);
+}
+// Same digits for a < 2^32 with 32-bit division (the digit count and the float
+// accumulation of reversedDigits are unchanged, so results are bit-identical).
+PHD float ScrambledRadicalInverse32(uint32_t base, uint32_t nDigits, uint32_t a, const uint16_t *perm) {
+    float invBase = (float)1 / (float)base, invBaseM = 1;
+    uint64_t reversedDigits = 0;
+    for (uint32_t digitIndex = 0; digitIndex < nDigits; ++digitIndex) {
+        uint32_t next = a / base;
+        uint32_t digitValue = a - next * base;
+        reversedDigits = reversedDigits * base + perm[digitIndex * base + digitValue];
+        invBaseM *= invBase;
+        a = next;
+    }
+    return std::fmin(invBaseM * (float)reversedDigits, kOneMinusEpsilon);
+}
+// Same digits with the runtime division by the base replaced by a Granlund-Montgomery
+// multiply (q = (t + ((a - t) >> 1)) >> shift, t = mulhi(magic, a); exact for every 32-bit a).
+// magic = floor(2^32 (2^l - base) / base) + 1, shift = l - 1, l = ceil(log2 base).
+PHD uint32_t HaltonMagic(uint32_t base, uint32_t *shift) {
+    uint32_t l = 0;
+    while ((1u << l) < base) ++l;
+    *shift = l - 1;
+    return (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - base)) / base + 1);
+}
+PHD float ScrambledRadicalInverse32Magic(uint32_t base, uint32_t nDigits, uint32_t magic, uint32_t shift, uint32_t a,
+                                          const uint16_t *perm) {
+    float invBase = (float)1 / (float)base, invBaseM = 1;
+    uint64_t reversedDigits = 0;
+    for (uint32_t digitIndex = 0; digitIndex < nDigits; ++digitIndex) {
+        uint32_t t = (uint32_t)(((uint64_t)magic * a) >> 32);
+        uint32_t next = (t + ((a - t) >> 1)) >> shift;
+        uint32_t digitValue = a - next * base;
         reversedDigits = reversedDigits * base + perm[digitIndex * base + digitValue];
         invBaseM *= invBase;
         a = next;

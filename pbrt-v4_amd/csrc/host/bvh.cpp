@@ -136,7 +136,14 @@ BVH8 BuildBVH8(const std::vector<V3> &verts, const std::vector<std::array<int, 3
     std::vector<Prim> prims;
     prims.reserve(tris.size());
     Box all;
+    // Degenerate triangles can never be hit (shapes.cpp:175); they stay out of the tree and
+    // are appended after the BVH's triangles in leaf order, so the traversal skips the test.
+    std::vector<int> degenerate;
     for (size_t i = 0; i < tris.size(); ++i) {
+        if (TriangleDegenerate(verts[tris[i][0]], verts[tris[i][1]], verts[tris[i][2]])) {
+            degenerate.push_back((int)i);
+            continue;
+        }
         Prim p;
         p.box.Add(verts[tris[i][0]]);
         p.box.Add(verts[tris[i][1]]);
@@ -148,6 +155,20 @@ BVH8 BuildBVH8(const std::vector<V3> &verts, const std::vector<std::array<int, 3
     }
     out.boundsMin = all.mn;
     out.boundsMax = all.mx;
+    auto appendDegenerate = [&]() {
+        for (int t : degenerate) {
+            out.triPrim.push_back(t);
+            for (int k = 0; k < 3; ++k) {
+                V3 p = verts[tris[t][k]];
+                float w = 0;
+                if (k == 0) {
+                    int32_t tt = t;
+                    memcpy(&w, &tt, 4);
+                }
+                out.triVerts.insert(out.triVerts.end(), {p.x, p.y, p.z, w});
+            }
+        }
+    };
     if (prims.empty()) {
         BVH8Node root{};
         for (int c = 0; c < 8; ++c) {
@@ -156,6 +177,7 @@ BVH8 BuildBVH8(const std::vector<V3> &verts, const std::vector<std::array<int, 3
             root.child[c] = kEmptyChild;
         }
         out.nodes.push_back(root);
+        appendDegenerate();
         return out;
     }
     maxLeafPrims = std::min(std::max(maxLeafPrims, 1), 8);
@@ -255,6 +277,23 @@ BVH8 BuildBVH8(const std::vector<V3> &verts, const std::vector<std::array<int, 3
         out.nodes[self] = node;
     }
     out.nodes.resize(queue.size());
+    appendDegenerate();
+    // Worst-case traversal stack: a node pushes its k interior children and pops one before
+    // descending, so need(n) = max(k, k - 1 + max need(child)); children follow parents in
+    // BFS order, so one reverse sweep suffices.
+    std::vector<int> need(out.nodes.size(), 0);
+    for (int i = (int)out.nodes.size() - 1; i >= 0; --i) {
+        int k = 0, deeper = 0;
+        for (int c = 0; c < 8; ++c) {
+            int ch = out.nodes[i].child[c];
+            if (ch >= 0) {
+                ++k;
+                deeper = std::max(deeper, need[ch]);
+            }
+        }
+        need[i] = k ? std::max(k, k - 1 + deeper) : 0;
+    }
+    out.maxStack = need[0];
     return out;
 }
 

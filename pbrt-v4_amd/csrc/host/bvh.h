@@ -32,6 +32,7 @@ struct BVH8 {
     std::vector<float> triVerts;
     std::vector<int> triPrim;  // leaf order -> original triangle index
     int maxDepth = 0;
+    int maxStack = 0;  // worst-case traversal stack entries (farthest-first pushes)
     V3 boundsMin, boundsMax;
 };
 

@@ -24,6 +24,8 @@ struct DeviceLightNode {
     int isLeaf;
 };
 
+constexpr int kMaxStackSize = 64;  // traversal stack entries per lane (64 KB of LDS per block)
+
 struct DeviceScene {
     // geometry (leaf order)
     const BVH8Node *nodes;
@@ -55,6 +57,7 @@ struct DeviceScene {
     const float *dense;  // [nSpectra][311]
     // sensor (PixelSensor cie1931): x,y,z bar dense tables [3][311]
     const float *sensor;
+    const float4 *sensor4;  // same tables interleaved: {xbar, ybar, zbar, 0} per dense entry
     float imagingRatio;
     // camera
     float cameraFromRaster[16];
@@ -66,9 +69,11 @@ struct DeviceScene {
     // halton
     const uint16_t *perm;
     const uint32_t *permOffset, *permNDigits, *permBase;
+    const uint4 *haltonDim;  // per dimension {base, nDigits | shift << 8, permOffset, magic}
     int nDims;
     int baseScales[2], baseExponents[2], multInverse[2];
     int maxDepth;
+    int stackSize;  // BVH traversal stack entries per lane (BVH8::maxStack)
 };
 
 // Per-pass wavefront buffers; N = paths per pass = P pixels x S samples.
@@ -94,6 +99,7 @@ struct PathState {
     int *rayQ[2];       // [N]
     int *matQ;          // [N]
     int *shadowQ;       // [N]
+    int *escQ;          // [N] escaped rays (only with infinite lights)
     int *counters;      // [(maxDepth+2) * 4]: ray, mat, shadow, spare per depth
     double *film;       // [4][xres*yres]: rgbSum[3], weightSum (sensor RGB)
     unsigned long long *stats;  // [8]: camera rays, closest rays, shadow rays, node visits

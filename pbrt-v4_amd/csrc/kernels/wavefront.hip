@@ -20,6 +20,7 @@
 namespace pbrt_amd {
 
 constexpr int kBlock = 256;
+constexpr float kInvWavelengthPDF = kLambdaMax - kLambdaMin;  // 1 / SampleUniformWavelengths pdf
 
 // ------------------------------------------------------------------ helpers
 __device__ inline int WavePush(int *counter, bool pred) {
@@ -57,13 +58,13 @@ __device__ inline Halton StartPixelSample(const DeviceScene &S, int px, int py, 
     h.index = 0;
     uint64_t sampleStride = (uint64_t)S.baseScales[0] * S.baseScales[1];
     if (sampleStride > 1) {
-        int pm[2] = {px % 128, py % 128};
-        if (pm[0] < 0) pm[0] += 128;
-        if (pm[1] < 0) pm[1] += 128;
-        for (int i = 0; i < 2; ++i) {
-            uint64_t dimOffset = InverseRadicalInverse((uint64_t)pm[i], i == 0 ? 2 : 3, S.baseExponents[i]);
-            h.index += dimOffset * (sampleStride / S.baseScales[i]) * (uint64_t)S.multInverse[i];
-        }
+        int pmx = px % 128, pmy = py % 128;
+        if (pmx < 0) pmx += 128;
+        if (pmy < 0) pmy += 128;
+        h.index += InverseRadicalInverse((uint64_t)pmx, 2, S.baseExponents[0]) * (sampleStride / S.baseScales[0]) *
+                   (uint64_t)S.multInverse[0];
+        h.index += InverseRadicalInverse((uint64_t)pmy, 3, S.baseExponents[1]) * (sampleStride / S.baseScales[1]) *
+                   (uint64_t)S.multInverse[1];
         h.index %= sampleStride;
     }
     h.index += (uint64_t)sampleIndex * sampleStride;
@@ -71,6 +72,10 @@ __device__ inline Halton StartPixelSample(const DeviceScene &S, int px, int py, 
     return h;
 }
 __device__ inline float SampleDim(const DeviceScene &S, uint64_t index, int dim) {
+    if ((index >> 32) == 0) {  // 32-bit digit extraction: same digits, division by multiply
+        const uint4 hd = S.haltonDim[dim];
+        return ScrambledRadicalInverse32Magic(hd.x, hd.y & 0xffu, hd.w, hd.y >> 8, (uint32_t)index, S.perm + hd.z);
+    }
     return ScrambledRadicalInverse(S.permBase[dim], S.permNDigits[dim], index, S.perm + S.permOffset[dim]);
 }
 __device__ inline float Get1D(const DeviceScene &S, Halton &h) {
@@ -93,111 +98,117 @@ __device__ inline void PixelOf(const PathState &st, int slot, int *px, int *py, 
     *sampleIndex = st.firstSample + s;
 }
 
-__device__ inline void Lambdas(float lambda0, float lambda[kNSpectrumSamples]) {
-    lambda[0] = lambda0;
-    const float delta = (kLambdaMax - kLambdaMin) / kNSpectrumSamples;
-    for (int i = 1; i < kNSpectrumSamples; ++i) {
-        lambda[i] = lambda[i - 1] + delta;
-        if (lambda[i] > kLambdaMax) lambda[i] = kLambdaMin + (lambda[i] - kLambdaMax);
-    }
-}
-
-// spectral contribution c[i] -> PixelSensor::ToSensorRGB (film.h:95-100), pdf = 1/310
-__device__ inline void AddSensorRGB(const DeviceScene &S, const float lambda[kNSpectrumSamples],
-                                    const float c[kNSpectrumSamples], float rgb[3]) {
-    const float pdf = 1 / (kLambdaMax - kLambdaMin);
-    float sx = 0, sy = 0, sz = 0;
-    for (int i = 0; i < kNSpectrumSamples; ++i) {
-        int o = DenseOffset(lambda[i]);
-        float v = (pdf != 0) ? c[i] / pdf : 0.f;
-        float xb = o < 0 ? 0.f : S.sensor[o], yb = o < 0 ? 0.f : S.sensor[kDenseN + o],
-              zb = o < 0 ? 0.f : S.sensor[2 * kDenseN + o];
-        if (i == 0) {
-            sx = xb * v;
-            sy = yb * v;
-            sz = zb * v;
-        } else {
-            sx += xb * v;
-            sy += yb * v;
-            sz += zb * v;
-        }
-    }
-    rgb[0] += S.imagingRatio * (sx / kNSpectrumSamples);
-    rgb[1] += S.imagingRatio * (sy / kNSpectrumSamples);
-    rgb[2] += S.imagingRatio * (sz / kNSpectrumSamples);
-}
-
 // ------------------------------------------------------------------ BVH8 traversal
-__device__ inline bool SlabHit(const BVH8Node &n, int c, V3 o, V3 invDir, const int dirIsNeg[3], float raytMax,
-                               float *tNear) {
-    // util/vecmath.h:1576-1611 Bounds3::IntersectP with the 1 + 2 gamma(3) far-plane slack
-    float lo[3] = {n.lox[c], n.loy[c], n.loz[c]}, hi[3] = {n.hix[c], n.hiy[c], n.hiz[c]};
-    float tMin = ((dirIsNeg[0] ? hi[0] : lo[0]) - o.x) * invDir.x;
-    float tMax = ((dirIsNeg[0] ? lo[0] : hi[0]) - o.x) * invDir.x;
-    float tyMin = ((dirIsNeg[1] ? hi[1] : lo[1]) - o.y) * invDir.y;
-    float tyMax = ((dirIsNeg[1] ? lo[1] : hi[1]) - o.y) * invDir.y;
-    tMax *= 1 + 2 * gamma(3);
-    tyMax *= 1 + 2 * gamma(3);
-    if (tMin > tyMax || tyMin > tMax) return false;
-    if (tyMin > tMin) tMin = tyMin;
-    if (tyMax < tMax) tMax = tyMax;
-    float tzMin = ((dirIsNeg[2] ? hi[2] : lo[2]) - o.z) * invDir.z;
-    float tzMax = ((dirIsNeg[2] ? lo[2] : hi[2]) - o.z) * invDir.z;
-    tzMax *= 1 + 2 * gamma(3);
-    if (tMin > tzMax || tzMin > tMax) return false;
-    if (tzMin > tMin) tMin = tzMin;
-    if (tzMax < tMax) tMax = tzMax;
-    *tNear = tMin;
-    return (tMin < raytMax) && (tMax > 0);
+// One ray per lane.  The node's 8 child boxes are read as 12 float4 loads (SoA inside the
+// 256-byte node), the 8 slab tests run fully unrolled in registers, leaves are intersected
+// nearest-first and interior children are pushed farthest-first onto a per-lane stack that
+// lives in LDS ([depth][lane] layout: consecutive lanes hit consecutive banks), so nothing
+// spills to scratch.  Box test = Bounds3::IntersectP (util/vecmath.h:1576-1611) including the
+// 1 + 2 gamma(3) far-plane slack; triangle test = IntersectTriangle (shapes.cpp:172-273).
+// Stack entries per lane = DeviceScene::stackSize (the BVH's exact worst case, host-computed,
+// at most kMaxStackSize), allocated as dynamic LDS at launch so small scenes keep occupancy.
+
+struct RayPre {
+    V3 o, invDir;
+    int neg[3];
+};
+
+__device__ inline void SlabTest4(const float4 *__restrict__ q, int g, const RayPre &r, float raytMax, float tn[8],
+                                 unsigned *mask) {
+    // children 4g..4g+3: lox,loy,loz at float4 index 2a+g, hix,hiy,hiz at 6+2a+g
+    float4 L[3], H[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        L[a] = q[2 * a + g];
+        H[a] = q[6 + 2 * a + g];
+    }
+    const float slack = 1 + 2 * gamma(3);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        float lo[3], hi[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = k == 0 ? L[a].x : k == 1 ? L[a].y : k == 2 ? L[a].z : L[a].w;
+            hi[a] = k == 0 ? H[a].x : k == 1 ? H[a].y : k == 2 ? H[a].z : H[a].w;
+        }
+        float nx = r.neg[0] ? hi[0] : lo[0], fx = r.neg[0] ? lo[0] : hi[0];
+        float ny = r.neg[1] ? hi[1] : lo[1], fy = r.neg[1] ? lo[1] : hi[1];
+        float nz = r.neg[2] ? hi[2] : lo[2], fz = r.neg[2] ? lo[2] : hi[2];
+        float tMin = (nx - r.o.x) * r.invDir.x;
+        float tMax = (fx - r.o.x) * r.invDir.x * slack;
+        float tyMin = (ny - r.o.y) * r.invDir.y;
+        float tyMax = (fy - r.o.y) * r.invDir.y * slack;
+        bool ok = !(tMin > tyMax || tyMin > tMax);
+        tMin = tyMin > tMin ? tyMin : tMin;
+        tMax = tyMax < tMax ? tyMax : tMax;
+        float tzMin = (nz - r.o.z) * r.invDir.z;
+        float tzMax = (fz - r.o.z) * r.invDir.z * slack;
+        ok = ok && !(tMin > tzMax || tzMin > tMax);
+        tMin = tzMin > tMin ? tzMin : tMin;
+        tMax = tzMax < tMax ? tzMax : tMax;
+        ok = ok && (tMin < raytMax) && (tMax > 0);
+        tn[4 * g + k] = tMin;
+        *mask |= ok ? (1u << (4 * g + k)) : 0u;
+    }
 }
 
-constexpr int kStackSize = 64;
+__device__ inline void SlabTest8(const BVH8Node *__restrict__ np, const RayPre &r, float raytMax, float tn[8],
+                                 unsigned *mask) {
+    const float4 *q = reinterpret_cast<const float4 *>(np);
+    *mask = 0;
+    SlabTest4(q, 0, r, raytMax, tn, mask);
+    SlabTest4(q, 1, r, raytMax, tn, mask);
+}
 
 template <bool AnyHit>
-__device__ inline int Traverse(const DeviceScene &S, V3 o, V3 d, float tMax, TriHit *best) {
-    V3 invDir(1 / d.x, 1 / d.y, 1 / d.z);
-    int dirIsNeg[3] = {invDir.x < 0, invDir.y < 0, invDir.z < 0};
-    int stack[kStackSize];
+__device__ inline int Traverse(const DeviceScene &S, V3 o, V3 d, float tMax, TriHit *best, int *lds) {
+    const TriRay tr = MakeTriRay(o, d);
+    RayPre r;
+    r.o = o;
+    r.invDir = V3(1 / d.x, 1 / d.y, 1 / d.z);
+    r.neg[0] = r.invDir.x < 0;
+    r.neg[1] = r.invDir.y < 0;
+    r.neg[2] = r.invDir.z < 0;
+    const int lane = threadIdx.x, stride = blockDim.x;
     int sp = 0;
-    stack[sp++] = 0;
+    int node = 0;
     int hitPrim = -1;
-    while (sp > 0) {
-        int ni = stack[--sp];
-        const BVH8Node &n = S.nodes[ni];
+    while (true) {
+        const BVH8Node *np = S.nodes + node;
         float tn[8];
-        int order[8];
-        int nHit = 0;
+        unsigned mask;
+        SlabTest8(np, r, tMax, tn, &mask);
+        // empty slots carry an inverted box, so they never pass the slab test
+        unsigned leaves = 0, inner = 0;
+        int4 ch0 = reinterpret_cast<const int4 *>(np->child)[0], ch1 = reinterpret_cast<const int4 *>(np->child)[1];
+        int ch[8] = {ch0.x, ch0.y, ch0.z, ch0.w, ch1.x, ch1.y, ch1.z, ch1.w};
+#pragma unroll
         for (int c = 0; c < 8; ++c) {
-            int ch = n.child[c];
-            if (ch == kEmptyChild) continue;
-            float t;
-            if (SlabHit(n, c, o, invDir, dirIsNeg, tMax, &t)) {
-                // insertion sort by tNear (ascending)
-                int k = nHit++;
-                while (k > 0 && tn[k - 1] > t) {
-                    tn[k] = tn[k - 1];
-                    order[k] = order[k - 1];
-                    --k;
-                }
-                tn[k] = t;
-                order[k] = c;
+            if (mask & (1u << c)) {
+                if (ch[c] < 0) leaves |= 1u << c;
+                else inner |= 1u << c;
             }
         }
-        // push interior children far-to-near; leaves are intersected near-to-far now
-        for (int k = nHit - 1; k >= 0; --k) {
-            int ch = n.child[order[k]];
-            if (ch >= 0 && sp < kStackSize) stack[sp++] = ch;
-        }
-        for (int k = 0; k < nHit; ++k) {
-            int ch = n.child[order[k]];
-            if (ch >= 0) continue;
-            if (tn[k] >= tMax) continue;
-            int enc = ~ch;
+        // leaves nearest-first
+        while (leaves) {
+            int bc = 0;
+            float bt = kInfinity;
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                if ((leaves & (1u << c)) && tn[c] <= bt) {
+                    bt = tn[c];
+                    bc = c;
+                }
+            leaves &= ~(1u << bc);
+            if (bt >= tMax) continue;
+            int enc = 0;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) enc = (c == bc) ? ~ch[c] : enc;
             int first = enc >> 3, count = (enc & 7) + 1;
             for (int t = first; t < first + count; ++t) {
                 float4 a = S.triVerts[3 * t], b = S.triVerts[3 * t + 1], c = S.triVerts[3 * t + 2];
                 TriHit h;
-                if (IntersectTriangle(o, d, tMax, V3(a.x, a.y, a.z), V3(b.x, b.y, b.z), V3(c.x, c.y, c.z), &h)) {
+                if (IntersectTriangleRay(tr, tMax, V3(a.x, a.y, a.z), V3(b.x, b.y, b.z), V3(c.x, c.y, c.z), &h)) {
                     if (AnyHit) return t;
                     tMax = h.t;
                     *best = h;
@@ -205,6 +216,25 @@ __device__ inline int Traverse(const DeviceScene &S, V3 o, V3 d, float tMax, Tri
                 }
             }
         }
+        // interior children farthest-first onto the stack (closest popped next)
+        while (inner) {
+            int bc = 0;
+            float bt = -kInfinity;
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                if ((inner & (1u << c)) && tn[c] >= bt) {
+                    bt = tn[c];
+                    bc = c;
+                }
+            inner &= ~(1u << bc);
+            if (bt >= tMax) continue;
+            int child = 0;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) child = (c == bc) ? ch[c] : child;
+            lds[(sp++) * stride + lane] = child;  // sp < S.stackSize by construction
+        }
+        if (sp == 0) break;
+        node = lds[(--sp) * stride + lane];
     }
     return hitPrim;
 }
@@ -367,8 +397,7 @@ __device__ inline float LightPMF(const DeviceScene &S, V3 p, V3 ns, int light) {
         if (node.isLeaf) return pmf;
         float c0 = LightImportance(S.lightNodes[nodeIndex + 1].b, p, ns);
         float c1 = LightImportance(S.lightNodes[node.childOrLight].b, p, ns);
-        float ci[2] = {c0, c1};
-        pmf *= ci[bitTrail & 1] / (c0 + c1);
+        pmf *= ((bitTrail & 1) ? c1 : c0) / (c0 + c1);
         nodeIndex = (bitTrail & 1) ? node.childOrLight : (nodeIndex + 1);
         bitTrail >>= 1;
     }
@@ -450,10 +479,12 @@ __global__ void __launch_bounds__(kBlock) k_camera(DeviceScene S, PathState st, 
 }
 
 __global__ void __launch_bounds__(kBlock) k_closest(DeviceScene S, PathState st, int depth) {
+    extern __shared__ int stackLds[];
     int N = st.N;
     const int *q = st.rayQ[depth & 1];
     const int count = st.counters[depth * 4 + 0];
     int *matCounter = &st.counters[depth * 4 + 1];
+    int *escCounter = &st.counters[depth * 4 + 3];
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&st.stats[1], (unsigned long long)count);
     for (int base = blockIdx.x * blockDim.x; base < count; base += gridDim.x * blockDim.x) {
         int qi = base + threadIdx.x;
@@ -465,55 +496,109 @@ __global__ void __launch_bounds__(kBlock) k_closest(DeviceScene S, PathState st,
         if (active) {
             o = V3(st.ray[slot], st.ray[N + slot], st.ray[2 * N + slot]);
             d = V3(st.ray[3 * N + slot], st.ray[4 * N + slot], st.ray[5 * N + slot]);
-            prim = Traverse<false>(S, o, d, kInfinity, &h);
+            prim = Traverse<false>(S, o, d, kInfinity, &h, stackLds);
             if (prim >= 0) {
                 st.hitPrim[slot] = prim;
                 st.hitB[slot] = h.b0;
                 st.hitB[N + slot] = h.b1;
                 st.hitB[2 * N + slot] = h.b2;
                 st.hitB[3 * N + slot] = h.t;
-            } else if (S.nInfinite > 0) {
-                // HandleEscapedRays: UniformInfiniteLight::Le with PDF_Li(allowIncomplete) = 0
-                float lambda[kNSpectrumSamples];
-                Lambdas(st.lambda0[slot], lambda);
-                float c[kNSpectrumSamples];
-                bool any = false;
-                for (int i = 0; i < kNSpectrumSamples; ++i) c[i] = 0;
-                int fl = st.flags[slot];
-                float rl = st.rl[slot];
-                for (int li = 0; li < S.nInfinite; ++li) {
-                    const float *dense = S.dense + S.infSpectrum[li] * kDenseN;
-                    float Le[kNSpectrumSamples];
-                    bool nz = false;
-                    for (int i = 0; i < kNSpectrumSamples; ++i) {
-                        int off = DenseOffset(lambda[i]);
-                        Le[i] = S.infScale[li] * (off < 0 ? 0.f : dense[off]);
-                        nz |= Le[i] != 0;
-                    }
-                    if (!nz) continue;
-                    float denom;
-                    if (depth == 0 || (fl & 1))
-                        denom = Avg31(1.f);
-                    else
-                        denom = Avg31(1.f + rl * 0.f);
-                    for (int i = 0; i < kNSpectrumSamples; ++i) c[i] += st.beta[i * N + slot] * Le[i] / denom;
-                    any = true;
-                }
-                if (any) {
-                    float rgb[3] = {0, 0, 0};
-                    AddSensorRGB(S, lambda, c, rgb);
-                    st.L[slot] += rgb[0];
-                    st.L[N + slot] += rgb[1];
-                    st.L[2 * N + slot] += rgb[2];
-                }
             }
+        }
+        if (S.nInfinite > 0) {
+            int epos = WavePush(escCounter, active && prim < 0);
+            if (epos >= 0) st.escQ[epos] = slot;
         }
         int pos = WavePush(matCounter, active && prim >= 0);
         if (pos >= 0) st.matQ[pos] = slot;
     }
 }
 
+// HandleEscapedRays (integrator.cpp:495-537) for UniformInfiniteLight: Le with MIS where
+// PDF_Li(allowIncompletePDF = true) == 0, so r_l contributes nothing.
+__global__ void __launch_bounds__(kBlock) k_escaped(DeviceScene S, PathState st, int depth) {
+    int N = st.N;
+    const int count = st.counters[depth * 4 + 3];
+    for (int qi = blockIdx.x * blockDim.x + threadIdx.x; qi < count; qi += gridDim.x * blockDim.x) {
+        int slot = st.escQ[qi];
+        int fl = st.flags[slot];
+        float rl = st.rl[slot];
+        float denom = (depth == 0 || (fl & 1)) ? Avg31(1.f) : Avg31(1.f + rl * 0.f);
+        const float invDenom = 1 / denom;
+        float rgb[3] = {0, 0, 0};
+        bool any = false;
+        for (int li = 0; li < S.nInfinite; ++li) {
+            const float *dense = S.dense + S.infSpectrum[li] * kDenseN;
+            float scale = S.infScale[li];
+            float sx = 0, sy = 0, sz = 0, lam = st.lambda0[slot];
+            bool nz = false;
+            for (int i = 0; i < kNSpectrumSamples; ++i) {
+                if (i > 0) {
+                    lam = lam + (kLambdaMax - kLambdaMin) / kNSpectrumSamples;
+                    if (lam > kLambdaMax) lam = kLambdaMin + (lam - kLambdaMax);
+                }
+                int off = DenseOffset(lam);
+                float Le = scale * (off < 0 ? 0.f : dense[off]);
+                nz |= Le != 0;
+                float v = (st.beta[i * N + slot] * Le * invDenom) * kInvWavelengthPDF;
+                float xb = off < 0 ? 0.f : S.sensor[off], yb = off < 0 ? 0.f : S.sensor[kDenseN + off],
+                      zb = off < 0 ? 0.f : S.sensor[2 * kDenseN + off];
+                sx = i == 0 ? xb * v : sx + xb * v;
+                sy = i == 0 ? yb * v : sy + yb * v;
+                sz = i == 0 ? zb * v : sz + zb * v;
+            }
+            if (!nz) continue;
+            any = true;
+            rgb[0] += S.imagingRatio * (sx / kNSpectrumSamples);
+            rgb[1] += S.imagingRatio * (sy / kNSpectrumSamples);
+            rgb[2] += S.imagingRatio * (sz / kNSpectrumSamples);
+        }
+        if (any) {
+            st.L[slot] += rgb[0];
+            st.L[N + slot] += rgb[1];
+            st.L[2 * N + slot] += rgb[2];
+        }
+    }
+}
+
+// Streaming form of the per-wavelength work: lambda_i, R_i, Le_i and beta_i are produced
+// inside each 31-iteration loop (lambda by pbrt's sequential +10 nm recurrence, R by the
+// sigmoid polynomial, beta re-read from the wavelength-major SoA through L1/L2) instead of
+// being held in 31-entry register arrays, which keeps the kernel at a few waves per SIMD.
+struct SpectralIter {
+    float lam;
+    int i;
+    __device__ SpectralIter(float l0) : lam(l0), i(0) {}
+    __device__ void Next() {
+        lam = lam + (kLambdaMax - kLambdaMin) / kNSpectrumSamples;
+        if (lam > kLambdaMax) lam = kLambdaMin + (lam - kLambdaMax);
+        ++i;
+    }
+};
+
+__device__ inline float Reflectance(float4 mc, bool constant, float lambda) {
+    float r = constant ? mc.w : SigmoidPolynomial(mc.x, mc.y, mc.z, lambda);
+    return Clampf(r, 0, 1);
+}
+
+// ToSensorRGB accumulation for one wavelength: sx += xbar * (c / pdf) (film.h:95-100)
+// Film-only arithmetic (the contribution c and its 1/pdf, 1/denom scalings) uses reciprocal
+// multiplies where the reference divides: at most an ulp or two per term in the pixel sums,
+// and nothing that steers a path (beta, pdfs and RR keep the reference's exact operations).
+struct SensorAcc {
+    float sx = 0, sy = 0, sz = 0;
+    __device__ void Add(const DeviceScene &S, int off, float c, bool first) {
+        float v = c * kInvWavelengthPDF;
+        float4 sb = off < 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : S.sensor4[off];
+        float xb = sb.x, yb = sb.y, zb = sb.z;
+        sx = first ? xb * v : sx + xb * v;
+        sy = first ? yb * v : sy + yb * v;
+        sz = first ? zb * v : sz + zb * v;
+    }
+};
+
 __global__ void __launch_bounds__(kBlock) k_shade_diffuse(DeviceScene S, PathState st, int depth) {
+    __shared__ float bfLds[kNSpectrumSamples * kBlock];  // [lambda][lane]: conflict-free
     int N = st.N;
     const int count = st.counters[depth * 4 + 1];
     int *nextCounter = &st.counters[(depth + 1) * 4 + 0];
@@ -525,62 +610,50 @@ __global__ void __launch_bounds__(kBlock) k_shade_diffuse(DeviceScene S, PathSta
         bool pushRay = false, pushShadow = false;
         int slot = active ? st.matQ[qi] : 0;
         if (active) {
-            float lambda[kNSpectrumSamples];
-            Lambdas(st.lambda0[slot], lambda);
+            const float lambda0 = st.lambda0[slot];
+            const float *betaP = st.beta + slot;
             int prim = st.hitPrim[slot];
             float b0 = st.hitB[slot], b1 = st.hitB[N + slot], b2 = st.hitB[2 * N + slot];
             V3 rd(st.ray[3 * N + slot], st.ray[4 * N + slot], st.ray[5 * N + slot]);
             V3 p0, p1, p2;
             PrimVerts(S, prim, &p0, &p1, &p2);
-            bool flip = S.primFlip[prim];
-            TriSurface surf = TriangleSurface(p0, p1, p2, b0, b1, b2, flip);
+            TriSurface surf = TriangleSurface(p0, p1, p2, b0, b1, b2, S.primFlip[prim]);
             V3 wo = Normalize(-rd);
             V3 n = surf.n, ns = surf.n;
             int fl = st.flags[slot];
             float rl = st.rl[slot];
-            float rgb[3] = {0, 0, 0};
-            bool addL = false;
-            // ---- HandleEmissiveIntersection
+            float Lr = 0, Lg = 0, Lb = 0;
+            // ---- HandleEmissiveIntersection (integrator.cpp:539-573)
             int light = S.primLight[prim];
-            if (light >= 0) {
-                bool twoSided = S.lightTwoSided[light];
-                if (twoSided || DotN(n, wo) >= 0) {
-                    const float *dense = S.dense + S.lightSpectrum[light] * kDenseN;
-                    float scale = S.lightScale[light];
-                    float Le[kNSpectrumSamples];
-                    bool nz = false;
-                    for (int i = 0; i < kNSpectrumSamples; ++i) {
-                        int off = DenseOffset(lambda[i]);
-                        Le[i] = scale * (off < 0 ? 0.f : dense[off]);
-                        nz |= Le[i] != 0;
-                    }
-                    if (nz) {
-                        float denom;
-                        if (depth == 0 || (fl & 1)) {
-                            denom = Avg31(1.f);
-                        } else {
-                            V3 cp(st.ctx[slot], st.ctx[N + slot], st.ctx[2 * N + slot]);
-                            V3 cn(st.ctx[3 * N + slot], st.ctx[4 * N + slot], st.ctx[5 * N + slot]);
-                            V3 cns(st.ctx[6 * N + slot], st.ctx[7 * N + slot], st.ctx[8 * N + slot]);
-                            V3 cpe(st.ctx[9 * N + slot], st.ctx[10 * N + slot], st.ctx[11 * N + slot]);
-                            float lightChoicePDF = LightPMF(S, cp, cns, light);
-                            float lightPDF = lightChoicePDF * TrianglePDF(S, S.lightPrim[light], cp, cpe, cn, cns, -wo);
-                            denom = Avg31(1.f + rl * lightPDF);
-                        }
-                        float c[kNSpectrumSamples];
-                        for (int i = 0; i < kNSpectrumSamples; ++i) c[i] = st.beta[i * N + slot] * Le[i] / denom;
-                        AddSensorRGB(S, lambda, c, rgb);
-                        addL = true;
-                    }
+            if (light >= 0 && (S.lightTwoSided[light] || DotN(n, wo) >= 0)) {
+                float denom;
+                if (depth == 0 || (fl & 1)) {
+                    denom = Avg31(1.f);
+                } else {
+                    V3 cp(st.ctx[slot], st.ctx[N + slot], st.ctx[2 * N + slot]);
+                    V3 cn(st.ctx[3 * N + slot], st.ctx[4 * N + slot], st.ctx[5 * N + slot]);
+                    V3 cns(st.ctx[6 * N + slot], st.ctx[7 * N + slot], st.ctx[8 * N + slot]);
+                    V3 cpe(st.ctx[9 * N + slot], st.ctx[10 * N + slot], st.ctx[11 * N + slot]);
+                    float lightChoicePDF = LightPMF(S, cp, cns, light);
+                    float lightPDF = lightChoicePDF * TrianglePDF(S, S.lightPrim[light], cp, cpe, cn, cns, -wo);
+                    denom = Avg31(1.f + rl * lightPDF);
                 }
-            }
-            if (addL) {
-                st.L[slot] += rgb[0];
-                st.L[N + slot] += rgb[1];
-                st.L[2 * N + slot] += rgb[2];
+                const float *dense = S.dense + S.lightSpectrum[light] * kDenseN;
+                float scale = S.lightScale[light];
+                SensorAcc acc;
+                const float invDenom = 1 / denom;
+#pragma unroll 4
+                for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next()) {
+                    int off = DenseOffset(it.lam);
+                    float Le = scale * (off < 0 ? 0.f : dense[off]);
+                    acc.Add(S, off, betaP[it.i * N] * Le * invDenom, it.i == 0);
+                }
+                Lr = S.imagingRatio * (acc.sx / kNSpectrumSamples);
+                Lg = S.imagingRatio * (acc.sy / kNSpectrumSamples);
+                Lb = S.imagingRatio * (acc.sz / kNSpectrumSamples);
             }
             if (depth < S.maxDepth) {
-                // ---- GenerateRaySamples (dimension = 6 + 7 * depth)
+                // ---- GenerateRaySamples (samples.cpp:29-66): dimension = 6 + 7 * depth
                 int px, py, sampleIndex;
                 PixelOf(st, slot, &px, &py, &sampleIndex);
                 px += S.px0;
@@ -588,83 +661,28 @@ __global__ void __launch_bounds__(kBlock) k_shade_diffuse(DeviceScene S, PathSta
                 float dUc = Get1D(S, h);
                 float dU0, dU1;
                 Get2D(S, h, &dU0, &dU1);
-                float iUc = Get1D(S, h);
+                (void)Get1D(S, h);  // indirect.uc (unused by DiffuseBxDF)
                 float iU0, iU1;
                 Get2D(S, h, &iU0, &iU1);
                 float rr = Get1D(S, h);
-                (void)iUc;
-                // ---- DiffuseMaterial::GetBxDF: R = clamp(reflectance(lambda), 0, 1)
+                // ---- DiffuseMaterial::GetBxDF: R = clamp(reflectance(lambda), 0, 1); f = R / pi
+                // (bxdfs.h DiffuseBxDF::f).  bf_i = beta_i * f_i is formed once per wavelength
+                // into LDS; light sampling and the BSDF update both start from that product.
                 int mat = S.primMaterial[prim];
-                float4 mc = S.matCoeffs[mat];
-                bool constant = S.matConstant[mat];
-                float R[kNSpectrumSamples];
+                const float4 mc = S.matCoeffs[mat];
+                const bool constant = S.matConstant[mat];
                 bool Rnz = false;
-                for (int i = 0; i < kNSpectrumSamples; ++i) {
-                    float r = constant ? mc.w : SigmoidPolynomial(mc.x, mc.y, mc.z, lambda[i]);
-                    R[i] = Clampf(r, 0, 1);
-                    Rnz |= R[i] != 0;
+                float *bf = bfLds + threadIdx.x;
+#pragma unroll 4
+                for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next()) {
+                    float R = Reflectance(mc, constant, it.lam);
+                    Rnz |= R != 0;
+                    bf[it.i * kBlock] = betaP[it.i * N] * (R * kInvPi);
                 }
                 Frame frame = Frame::FromXZ(Normalize(surf.dpdu), ns);
                 V3 woL = frame.ToLocal(wo);
-                float beta[kNSpectrumSamples];
-                for (int i = 0; i < kNSpectrumSamples; ++i) beta[i] = st.beta[i * N + slot];
                 V3 pi = surf.p, pe = surf.pErr;
-                // ---- BSDF::Sample_f<DiffuseBxDF> + RR + indirect ray (surfscatter.cpp:170-250)
-                if (woL.z != 0 && Rnz) {
-                    V3 wiL = SampleCosineHemisphere(iU0, iU1);
-                    if (woL.z < 0) wiL.z *= -1;
-                    float pdf = CosineHemispherePDF(fabsf(wiL.z));
-                    if (pdf != 0 && wiL.z != 0) {
-                        V3 wi = frame.FromLocal(wiL);
-                        float absdot = AbsDotN(ns, wi);
-                        float nb[kNSpectrumSamples];
-                        float mx = -kInfinity;
-                        bool nz = false;
-                        for (int i = 0; i < kNSpectrumSamples; ++i) {
-                            nb[i] = beta[i] * (R[i] * kInvPi) * absdot / pdf;
-                        }
-                        float newRl = 1.f / pdf;
-                        float etaScale = st.etaScale[slot];
-                        float avgRu = Avg31(1.f);
-                        for (int i = 0; i < kNSpectrumSamples; ++i) mx = fmaxf(mx, nb[i] * etaScale / avgRu);
-                        if (mx < 1 && depth >= 1) {
-                            float q = fmaxf(0.f, 1 - mx);
-                            if (rr < q) {
-                                for (int i = 0; i < kNSpectrumSamples; ++i) nb[i] = 0;
-                            } else {
-                                for (int i = 0; i < kNSpectrumSamples; ++i) nb[i] /= 1 - q;
-                            }
-                        }
-                        for (int i = 0; i < kNSpectrumSamples; ++i) nz |= nb[i] != 0;
-                        if (nz) {
-                            V3 ro = OffsetRayOrigin(pi, pe, n, wi);
-                            pushRay = true;
-                            // NEE below still reads the old beta from registers
-                            st.ray[slot] = ro.x;
-                            st.ray[N + slot] = ro.y;
-                            st.ray[2 * N + slot] = ro.z;
-                            st.ray[3 * N + slot] = wi.x;
-                            st.ray[4 * N + slot] = wi.y;
-                            st.ray[5 * N + slot] = wi.z;
-                            st.rl[slot] = newRl;
-                            st.flags[slot] = 2;  // specularBounce = false, anyNonSpecular = true
-                            st.ctx[slot] = pi.x;
-                            st.ctx[N + slot] = pi.y;
-                            st.ctx[2 * N + slot] = pi.z;
-                            st.ctx[3 * N + slot] = n.x;
-                            st.ctx[4 * N + slot] = n.y;
-                            st.ctx[5 * N + slot] = n.z;
-                            st.ctx[6 * N + slot] = ns.x;
-                            st.ctx[7 * N + slot] = ns.y;
-                            st.ctx[8 * N + slot] = ns.z;
-                            st.ctx[9 * N + slot] = pe.x;
-                            st.ctx[10 * N + slot] = pe.y;
-                            st.ctx[11 * N + slot] = pe.z;
-                            for (int i = 0; i < kNSpectrumSamples; ++i) st.beta[i * N + slot] = nb[i];
-                        }
-                    }
-                }
-                // ---- light sampling + shadow ray (surfscatter.cpp:254-326)
+                // ---- light sampling + shadow ray (surfscatter.cpp:254-326); reads the old beta
                 if (Rnz) {
                     V3 cp = OffsetRayOrigin(pi, pe, n, wo);  // reflective, not transmissive
                     int li;
@@ -678,30 +696,25 @@ __global__ void __launch_bounds__(kBlock) k_shade_diffuse(DeviceScene S, PathSta
                         if (SampleTriangle(q0, q1, q2, S.primFlip[lprim], cp, n, ns, dU0, dU1, &lp, &lpe, &ln, &lpdf) &&
                             lpdf != 0 && LengthSquared(lp - cp) != 0) {
                             V3 wi = Normalize(lp - cp);
-                            // DiffuseAreaLight::L(p, n, uv, -wi)
-                            bool lTwo = S.lightTwoSided[li];
-                            if (lTwo || DotN(ln, -wi) >= 0) {
+                            V3 wiL = frame.ToLocal(wi);
+                            if ((S.lightTwoSided[li] || DotN(ln, -wi) >= 0) && woL.z != 0 && woL.z * wiL.z > 0) {
                                 const float *dense = S.dense + S.lightSpectrum[li] * kDenseN;
                                 float scale = S.lightScale[li];
-                                float Le[kNSpectrumSamples];
+                                float absdot = AbsDotN(ns, wi);
+                                float lightPDF = lpdf * lpmf;
+                                float bsdfPDF = CosineHemispherePDF(fabsf(wiL.z));
+                                float denom = Avg31(bsdfPDF + lightPDF);
+                                const float invDenom = 1 / denom;
+                                SensorAcc acc;
                                 bool nz = false;
-                                for (int i = 0; i < kNSpectrumSamples; ++i) {
-                                    int off = DenseOffset(lambda[i]);
-                                    Le[i] = scale * (off < 0 ? 0.f : dense[off]);
-                                    nz |= Le[i] != 0;
+#pragma unroll 4
+                                for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next()) {
+                                    int off = DenseOffset(it.lam);
+                                    float Le = scale * (off < 0 ? 0.f : dense[off]);
+                                    nz |= Le != 0;
+                                    acc.Add(S, off, bf[it.i * kBlock] * absdot * Le * invDenom, it.i == 0);
                                 }
-                                V3 wiL = frame.ToLocal(wi);
-                                bool same = woL.z * wiL.z > 0;
-                                if (nz && woL.z != 0 && same) {
-                                    float absdot = AbsDotN(ns, wi);
-                                    float lightPDF = lpdf * lpmf;
-                                    float bsdfPDF = CosineHemispherePDF(fabsf(wiL.z));
-                                    float denom = Avg31(bsdfPDF + lightPDF);
-                                    float c[kNSpectrumSamples];
-                                    for (int i = 0; i < kNSpectrumSamples; ++i)
-                                        c[i] = beta[i] * (R[i] * kInvPi) * absdot * Le[i] / denom;
-                                    float srgb[3] = {0, 0, 0};
-                                    AddSensorRGB(S, lambda, c, srgb);
+                                if (nz) {
                                     // SpawnRayTo(pi, n, time, pLight.pi, pLight.n) (ray.h:106-111)
                                     V3 pf = OffsetRayOrigin(pi, pe, n, lp - pi);
                                     V3 pt = OffsetRayOrigin(lp, lpe, ln, pf - lp);
@@ -712,15 +725,81 @@ __global__ void __launch_bounds__(kBlock) k_shade_diffuse(DeviceScene S, PathSta
                                     st.shadowRay[3 * N + slot] = sd.x;
                                     st.shadowRay[4 * N + slot] = sd.y;
                                     st.shadowRay[5 * N + slot] = sd.z;
-                                    st.shadowL[slot] = srgb[0];
-                                    st.shadowL[N + slot] = srgb[1];
-                                    st.shadowL[2 * N + slot] = srgb[2];
+                                    st.shadowL[slot] = S.imagingRatio * (acc.sx / kNSpectrumSamples);
+                                    st.shadowL[N + slot] = S.imagingRatio * (acc.sy / kNSpectrumSamples);
+                                    st.shadowL[2 * N + slot] = S.imagingRatio * (acc.sz / kNSpectrumSamples);
                                     pushShadow = true;
                                 }
                             }
                         }
                     }
                 }
+                // ---- BSDF::Sample_f<DiffuseBxDF> + RR + indirect ray (surfscatter.cpp:170-250)
+                if (woL.z != 0 && Rnz) {
+                    V3 wiL = SampleCosineHemisphere(iU0, iU1);
+                    if (woL.z < 0) wiL.z *= -1;
+                    float pdf = CosineHemispherePDF(fabsf(wiL.z));
+                    if (pdf != 0 && wiL.z != 0) {
+                        V3 wi = frame.FromLocal(wiL);
+                        float absdot = AbsDotN(ns, wi);
+                        float etaScale = st.etaScale[slot];
+                        float avgRu = Avg31(1.f);
+                        float mx = -kInfinity;
+#pragma unroll 4
+                        for (int i = 0; i < kNSpectrumSamples; ++i) {
+                            float nbv = bf[i * kBlock] * absdot / pdf;
+                            bf[i * kBlock] = nbv;
+                            mx = fmaxf(mx, nbv * etaScale / avgRu);
+                        }
+                        bool kill = false;
+                        float q = 0;
+                        if (mx < 1 && depth >= 1) {
+                            q = fmaxf(0.f, 1 - mx);
+                            kill = rr < q;
+                        }
+                        if (!kill) {
+                            bool rrScale = mx < 1 && depth >= 1;
+                            bool nz = false;
+                            float *betaW = st.beta + slot;
+#pragma unroll 4
+                            for (int i = 0; i < kNSpectrumSamples; ++i) {
+                                float nbv = bf[i * kBlock];
+                                if (rrScale) nbv /= 1 - q;
+                                nz |= nbv != 0;
+                                betaW[i * N] = nbv;
+                            }
+                            if (nz) {
+                                V3 ro = OffsetRayOrigin(pi, pe, n, wi);
+                                pushRay = true;
+                                st.ray[slot] = ro.x;
+                                st.ray[N + slot] = ro.y;
+                                st.ray[2 * N + slot] = ro.z;
+                                st.ray[3 * N + slot] = wi.x;
+                                st.ray[4 * N + slot] = wi.y;
+                                st.ray[5 * N + slot] = wi.z;
+                                st.rl[slot] = 1.f / pdf;
+                                st.flags[slot] = 2;  // specularBounce = false, anyNonSpecular = true
+                                st.ctx[slot] = pi.x;
+                                st.ctx[N + slot] = pi.y;
+                                st.ctx[2 * N + slot] = pi.z;
+                                st.ctx[3 * N + slot] = n.x;
+                                st.ctx[4 * N + slot] = n.y;
+                                st.ctx[5 * N + slot] = n.z;
+                                st.ctx[6 * N + slot] = ns.x;
+                                st.ctx[7 * N + slot] = ns.y;
+                                st.ctx[8 * N + slot] = ns.z;
+                                st.ctx[9 * N + slot] = pe.x;
+                                st.ctx[10 * N + slot] = pe.y;
+                                st.ctx[11 * N + slot] = pe.z;
+                            }
+                        }
+                    }
+                }
+            }
+            if (Lr != 0 || Lg != 0 || Lb != 0) {
+                st.L[slot] += Lr;
+                st.L[N + slot] += Lg;
+                st.L[2 * N + slot] += Lb;
             }
         }
         int pos = WavePush(nextCounter, pushRay);
@@ -731,6 +810,7 @@ __global__ void __launch_bounds__(kBlock) k_shade_diffuse(DeviceScene S, PathSta
 }
 
 __global__ void __launch_bounds__(kBlock) k_shadow(DeviceScene S, PathState st, int depth) {
+    extern __shared__ int stackLds[];
     int N = st.N;
     const int count = st.counters[depth * 4 + 2];
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&st.stats[2], (unsigned long long)count);
@@ -739,7 +819,7 @@ __global__ void __launch_bounds__(kBlock) k_shadow(DeviceScene S, PathState st, 
         V3 o(st.shadowRay[slot], st.shadowRay[N + slot], st.shadowRay[2 * N + slot]);
         V3 d(st.shadowRay[3 * N + slot], st.shadowRay[4 * N + slot], st.shadowRay[5 * N + slot]);
         TriHit h;
-        int hit = Traverse<true>(S, o, d, 1 - kShadowEpsilon, &h);
+        int hit = Traverse<true>(S, o, d, 1 - kShadowEpsilon, &h, stackLds);
         if (hit < 0) {
             st.L[slot] += st.shadowL[slot];
             st.L[N + slot] += st.shadowL[N + slot];
@@ -778,12 +858,13 @@ __global__ void __launch_bounds__(kBlock) k_film(DeviceScene S, PathState st, in
 // for an SoA ray batch, used by parity tests and the traversal benchmark.
 __global__ void __launch_bounds__(kBlock) k_intersect_batch(DeviceScene S, const float *rays, int n, int anyHit,
                                                               int *outPrim, float *outHit) {
+    extern __shared__ int stackLds[];
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         V3 o(rays[i], rays[n + i], rays[2 * n + i]);
         V3 d(rays[3 * n + i], rays[4 * n + i], rays[5 * n + i]);
         float tMax = rays[6 * n + i];
         TriHit h{0, 0, 0, 0};
-        int prim = anyHit ? Traverse<true>(S, o, d, tMax, &h) : Traverse<false>(S, o, d, tMax, &h);
+        int prim = anyHit ? Traverse<true>(S, o, d, tMax, &h, stackLds) : Traverse<false>(S, o, d, tMax, &h, stackLds);
         outPrim[i] = prim;
         outHit[i] = h.b0;
         outHit[n + i] = h.b1;
@@ -793,6 +874,8 @@ __global__ void __launch_bounds__(kBlock) k_intersect_batch(DeviceScene S, const
 }
 
 // ------------------------------------------------------------------ launch helpers (host)
+static size_t StackBytes(const DeviceScene &S) { return (size_t)(S.stackSize > 0 ? S.stackSize : 1) * kBlock * sizeof(int); }
+
 static int GridFor(int n) {
     int g = (n + kBlock - 1) / kBlock;
     return g < 1 ? 1 : (g > 8192 ? 8192 : g);
@@ -803,7 +886,11 @@ hipError_t LaunchCamera(const DeviceScene &S, const PathState &st, int nActive, 
     return hipGetLastError();
 }
 hipError_t LaunchClosest(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s) {
-    hipLaunchKernelGGL(k_closest, dim3(GridFor(maxCount)), dim3(kBlock), 0, s, S, st, depth);
+    hipLaunchKernelGGL(k_closest, dim3(GridFor(maxCount)), dim3(kBlock), StackBytes(S), s, S, st, depth);
+    return hipGetLastError();
+}
+hipError_t LaunchEscaped(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s) {
+    hipLaunchKernelGGL(k_escaped, dim3(GridFor(maxCount)), dim3(kBlock), 0, s, S, st, depth);
     return hipGetLastError();
 }
 hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s) {
@@ -811,7 +898,7 @@ hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int dep
     return hipGetLastError();
 }
 hipError_t LaunchShadow(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s) {
-    hipLaunchKernelGGL(k_shadow, dim3(GridFor(maxCount)), dim3(kBlock), 0, s, S, st, depth);
+    hipLaunchKernelGGL(k_shadow, dim3(GridFor(maxCount)), dim3(kBlock), StackBytes(S), s, S, st, depth);
     return hipGetLastError();
 }
 hipError_t LaunchFilm(const DeviceScene &S, const PathState &st, int nSamples, hipStream_t s) {
@@ -820,7 +907,7 @@ hipError_t LaunchFilm(const DeviceScene &S, const PathState &st, int nSamples, h
 }
 hipError_t LaunchIntersectBatch(const DeviceScene &S, const float *rays, int n, int anyHit, int *outPrim,
                                 float *outHit, hipStream_t s) {
-    hipLaunchKernelGGL(k_intersect_batch, dim3(GridFor(n)), dim3(kBlock), 0, s, S, rays, n, anyHit, outPrim, outHit);
+    hipLaunchKernelGGL(k_intersect_batch, dim3(GridFor(n)), dim3(kBlock), StackBytes(S), s, S, rays, n, anyHit, outPrim, outHit);
     return hipGetLastError();
 }
 

@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Write the k_closest HBM-traffic record that bench.py reports as roofline.traffic.
+
+Input: the rocprofv3 PMC passes of tools/pmc.sh (FETCH_SIZE and WRITE_SIZE each in its own
+pass, values in KB per dispatch) plus the bench JSON line those runs printed (rays/launch).
+gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half the bytes of a
+wide coalesced read, so it is doubled; WRITE_SIZE is used as is.
+Usage: python tools/closest_pmc_json.py gpurun_out/pmc profiles/r01_closest_pmc.json
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+
+def per_dispatch(csv_path, kernel, counter):
+    acc = defaultdict(float)
+    for r in csv.DictReader(open(csv_path)):
+        if r["Kernel_Name"].split("(")[0].endswith(kernel) and r["Counter_Name"] == counter:
+            acc[r["Dispatch_Id"]] += float(r["Counter_Value"])
+    return list(acc.values())
+
+
+def bench_line(log):
+    for line in open(log):
+        if line.startswith('{"metric"'):
+            return json.loads(line)
+    raise SystemExit(f"no bench line in {log}")
+
+
+src, dst = Path(sys.argv[1]), Path(sys.argv[2])
+kernel = sys.argv[3] if len(sys.argv) > 3 else "k_closest"
+fetch = per_dispatch(src / "fetch" / "run_counter_collection.csv", kernel, "FETCH_SIZE")
+write = per_dispatch(src / "write" / "run_counter_collection.csv", kernel, "WRITE_SIZE")
+b = bench_line(src / "fetch.log")
+fetch_b = 2 * 1024 * sum(fetch) / len(fetch)
+write_b = 1024 * sum(write) / len(write)
+rays = b["roofline"]["rays_per_launch"]
+rec = {
+    "kernel": kernel,
+    "dispatches": len(fetch),
+    "fetch_size_kb_mean": sum(fetch) / len(fetch),
+    "write_size_kb_mean": sum(write) / len(write),
+    "fetch_bytes_corrected": fetch_b,
+    "write_bytes": write_b,
+    "hbm_bytes_per_launch": round(fetch_b + write_b),
+    "rays_per_launch": rays,
+    "hbm_bytes_per_ray": round((fetch_b + write_b) / rays, 2),
+    "algorithmic_bytes_per_ray": b["roofline"]["bytes_per_ray"],
+    "bench_config": b["config"]["workload"],
+    "note": "FETCH_SIZE x2 per the gfx950 correction; 4-byte-per-lane SoA accesses are not calibrated "
+            "by the guide, so the corrected read figure is an upper estimate",
+}
+dst.write_text(json.dumps(rec, indent=1) + "\n")
+print(json.dumps(rec, indent=1))

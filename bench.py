@@ -134,7 +134,7 @@ def main():
     value = samples / dt_max / 1e6
     launches = max(st.closest_launches, 1)
     mean_launch_s = st.closest_ms / 1e3 / launches
-    bytes_per_launch = BYTES_PER_RAY_CLOSEST * st.closest_rays / launches
+    bytes_per_launch = BYTES_PER_RAY_CLOSEST * st.timed_closest_rays / launches
     achieved = bytes_per_launch / mean_launch_s / 1e9 if mean_launch_s > 0 else 0.0
     traffic = pmc_traffic()
 
@@ -168,7 +168,8 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "kernel": "k_closest (BVH8 traverse + hit record + wave64 ballot push to material queue)",
                          "bytes_per_ray": BYTES_PER_RAY_CLOSEST,
-                         "rays_per_launch": round(st.closest_rays / launches, 1),
+                         "rays_per_launch": round(st.timed_closest_rays / launches, 1),
+                         "timed_launches": launches,
                          "mean_launch_us": round(mean_launch_s * 1e6, 3)},
             "cpu_baseline": cpu,
             "rays": {"camera": int(st.camera_rays), "closest": int(st.closest_rays), "shadow": int(st.shadow_rays)},

@@ -92,8 +92,9 @@ typedef struct pbrt_render_params {
 
 typedef struct pbrt_render_stats {
     uint64_t camera_rays, closest_rays, shadow_rays; /* valid after pbrt_synchronize */
-    int closest_launches;
-    double closest_ms;   /* sum of event-timed closest-hit kernel durations */
+    int closest_launches;   /* event-timed closest-hit launches (first pass of each render) */
+    double closest_ms;      /* sum of their durations */
+    uint64_t timed_closest_rays; /* rays those launches processed */
     int passes;
     uint64_t paths_per_pass;
 } pbrt_render_stats;
@@ -129,6 +130,9 @@ int pbrt_intersect(pbrt_context *ctx, const float *rays_dev, int n, int any_hit,
 float pbrt_debug_halton(const pbrt_scene *scene, int px, int py, int sample_index, int dim);
 int pbrt_debug_rgb_coeffs(float r, float g, float b, float *coeffs3);
 int pbrt_debug_rgb2spec_column(int maxc, int j, int i, float *out192);
+/* profiling build only (PBRT_AMD_SECTION_TIMING): summed wave cycles per kernel section
+ * since the last pbrt_reset_stats; zeros in the product build */
+int pbrt_debug_kernel_sections(pbrt_context *ctx, uint64_t *cycles, int n);
 
 #ifdef __cplusplus
 }

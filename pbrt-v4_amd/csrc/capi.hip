@@ -17,9 +17,11 @@
 
 namespace pbrt_amd {
 hipError_t LaunchCamera(const DeviceScene &S, const PathState &st, int nActive, hipStream_t s);
-hipError_t LaunchClosest(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
+hipError_t LaunchClosest(const DeviceScene &S, const PathState &st, int depth, int maxCount, int timed,
+                         hipStream_t s);
 hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
 hipError_t LaunchEscaped(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
+hipError_t LaunchEmissive(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
 hipError_t LaunchShadow(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
 hipError_t LaunchFilm(const DeviceScene &S, const PathState &st, int nSamples, hipStream_t s);
 hipError_t LaunchIntersectBatch(const DeviceScene &S, const float *rays, int n, int anyHit, int *outPrim,
@@ -128,9 +130,12 @@ struct pbrt_context {
     DevBuf<uint8_t> primFlip;
     DevBuf<uint32_t> lightBitTrail, permOffset, permNDigits, permBase;
     DevBuf<uint16_t> perm;
-    DevBuf<uint32_t> haltonDim;
+    DevBuf<HaltonDimDesc> haltonDim;
+    DevBuf<uint16_t> permByDepth;
+    DevBuf<uint32_t> permDepthInfo;
     DevBuf<float> sensor4;
     DevBuf<DeviceLightNode> lightNodes;
+    DevBuf<DeviceAreaLight> lights;
     // wavefront buffers
     int64_t maxPaths = 0;
     DevBuf<float> fState;
@@ -203,6 +208,21 @@ static void BuildDevice(pbrt_context *c) {
     c->lightTwoSided.Upload(lt);
     c->lightScale.Upload(lsc);
     c->lightArea.Upload(la);
+    std::vector<DeviceAreaLight> dl;
+    for (auto &l : s.areaLights) {
+        DeviceAreaLight d{};
+        int leaf = origToLeaf[l.prim];
+        const float *v = &b.triVerts[(size_t)leaf * 12];
+        d.v0 = make_float4(v[0], v[1], v[2], 0.f);
+        d.v1 = make_float4(v[4], v[5], v[6], 0.f);
+        d.v2 = make_float4(v[8], v[9], v[10], 0.f);
+        d.scale = l.scale;
+        d.spectrum = l.spectrum;
+        d.twoSided = l.twoSided;
+        d.flip = pf[leaf];
+        dl.push_back(d);
+    }
+    c->lights.Upload(dl);
     std::vector<int> is;
     std::vector<float> isc;
     for (auto &l : s.infiniteLights) {
@@ -238,12 +258,32 @@ static void BuildDevice(pbrt_context *c) {
     c->permOffset.Upload(s.permOffset);
     c->permNDigits.Upload(s.permNDigits);
     c->permBase.Upload(s.permBase);
-    std::vector<uint32_t> hd;
-    for (size_t d = 0; d < s.permBase.size(); ++d) {
-        uint32_t shift, magic = HaltonMagic(s.permBase[d], &shift);
-        hd.insert(hd.end(), {s.permBase[d], s.permNDigits[d] | (shift << 8), s.permOffset[d], magic});
-    }
+    std::vector<HaltonDimDesc> hd;
+    for (size_t d = 0; d < s.permBase.size(); ++d)
+        hd.push_back(MakeHaltonDimDesc(s.permBase[d], s.permNDigits[d], s.permOffset[d]));
     c->haltonDim.Upload(hd);
+    {
+        std::vector<uint16_t> pb;
+        std::vector<uint32_t> info((size_t)8 * (s.maxDepth + 1), 0);
+        for (int depth = 0; depth < s.maxDepth; ++depth) {
+            if (pb.size() & 1) pb.push_back(0);  // 4-byte aligned block start
+            uint32_t start = (uint32_t)pb.size();
+            info[8 * depth] = start;
+            for (int k = 0; k < 7; ++k) {
+                int d = 6 + 7 * depth + k;
+                info[8 * depth + 1 + k] = (uint32_t)pb.size() - start;
+                if (d < (int)s.permBase.size()) {
+                    size_t n = (size_t)s.permBase[d] * s.permNDigits[d];
+                    pb.insert(pb.end(), s.permTable.begin() + s.permOffset[d], s.permTable.begin() + s.permOffset[d] + n);
+                }
+            }
+        }
+        if (pb.size() & 1) pb.push_back(0);
+        info[8 * s.maxDepth] = (uint32_t)pb.size();
+        if (pb.empty()) pb.push_back(0);
+        c->permByDepth.Upload(pb);
+        c->permDepthInfo.Upload(info);
+    }
 
     DeviceScene &S = c->S;
     S.nodes = c->nodes.p;
@@ -261,6 +301,7 @@ static void BuildDevice(pbrt_context *c) {
     S.lightSpectrum = c->lightSpectrum.p;
     S.lightTwoSided = c->lightTwoSided.p;
     S.lightArea = c->lightArea.p;
+    S.lights = c->lights.p;
     S.lightBitTrail = c->lightBitTrail.p;
     S.nInfinite = (int)s.infiniteLights.size();
     S.infSpectrum = c->infSpectrum.p;
@@ -269,6 +310,7 @@ static void BuildDevice(pbrt_context *c) {
     S.lightNodes = c->lightNodes.p;
     S.nLightNodes = (int)s.lightNodes.size();
     S.dense = c->dense.p;
+    S.nDense = (int)s.denseSpectra.size();
     S.sensor = c->sensor.p;
     S.sensor4 = (const float4 *)c->sensor4.p;
     S.imagingRatio = s.imagingRatio;
@@ -287,19 +329,77 @@ static void BuildDevice(pbrt_context *c) {
     S.py1 = s.py1;
     S.filterRadiusX = s.filterRadiusX;
     S.filterRadiusY = s.filterRadiusY;
+    S.boxFilter = 1;  // the loader accepts only PixelFilter "box"
     S.perm = c->perm.p;
     S.permOffset = c->permOffset.p;
     S.permNDigits = c->permNDigits.p;
     S.permBase = c->permBase.p;
-    S.haltonDim = (const uint4 *)c->haltonDim.p;
+    S.haltonDim = c->haltonDim.p;
+    S.permByDepth = c->permByDepth.p;
+    S.permDepthInfo = c->permDepthInfo.p;
     S.nDims = (int)s.permBase.size();
     for (int i = 0; i < 2; ++i) {
         S.baseScales[i] = s.haltonBaseScales[i];
         S.baseExponents[i] = s.haltonBaseExponents[i];
         S.multInverse[i] = s.haltonMultInverse[i];
     }
+    {
+        uint64_t s0 = (uint64_t)S.baseScales[0], s1 = (uint64_t)S.baseScales[1];
+        // every pixel coordinate passed to the kernels is >= 0 (pixel bounds start at >= 0)
+        S.haltonFast32 = s.px0 >= 0 && s.py0 >= 0 && s0 * s1 * (s0 + s1) < (1ull << 32) ? 1 : 0;
+    }
     S.maxDepth = s.maxDepth;
+    {
+        // k_shade_diffuse dynamic LDS: [beta*f 31x256 floats][sensor][light spectra][Halton
+        // permutations of 7 dims][lights][light BVH][materials]
+        ShadeLdsLayout &L = S.shadeLds;
+        L = ShadeLdsLayout{};
+        auto align16 = [](int v) { return (v + 15) & ~15; };
+        int off = kNSpectrumSamples * 256 * (int)sizeof(float);
+        L.sensor = off;
+        off += kDenseN * 16;
+        L.denseInLds = s.denseSpectra.size() <= 4 ? 1 : 0;
+        L.dense = off;
+        if (L.denseInLds) off = align16(off + (int)s.denseSpectra.size() * kDenseN * 4);
+        int permEntries = 0;
+        for (int depth = 0; depth < s.maxDepth; ++depth) {
+            int n = 0;
+            for (int k = 0; k < 7; ++k) {
+                int d = 6 + 7 * depth + k;
+                if (d < (int)s.permBase.size()) n += (int)(s.permBase[d] * s.permNDigits[d]);
+            }
+            permEntries = std::max(permEntries, n);
+        }
+        L.permEntries = permEntries + 1;  // DMA copies whole 4-byte words
+        L.perm = off;
+        off = align16(off + (permEntries + 1) * 2);
+        L.lightsInLds = (s.areaLights.size() <= 64 && s.lightNodes.size() <= 127) ? 1 : 0;
+        L.lights = off;
+        L.lightNodes = off;
+        if (L.lightsInLds) {
+            off += (int)s.areaLights.size() * (int)sizeof(DeviceAreaLight);
+            L.lightNodes = off;
+            off = align16(off + (int)s.lightNodes.size() * (int)sizeof(DeviceLightNode));
+        }
+        L.matsInLds = s.materials.size() <= 256 ? 1 : 0;
+        L.mats = off;
+        L.matConst = off;
+        if (L.matsInLds) {
+            off += (int)s.materials.size() * 16;
+            L.matConst = off;
+            off = align16(off + (int)s.materials.size() * 4);
+        }
+        L.total = off;
+        if (L.total > 64 * 1024) throw Error("shade kernel LDS layout exceeds 64 KB");
+    }
     S.stackSize = c->bvh.maxStack;
+    {
+        // LDS scene cache: top BVH8 nodes first (BFS order), then leading leaf-order triangles
+        int nNodes = (int)c->bvh.nodes.size(), budget = kSceneLdsBudget;
+        S.ldsNodes = std::min(nNodes, budget / (17 * 16));
+        budget -= S.ldsNodes * 17 * 16;
+        S.ldsTris = (S.ldsNodes == nNodes && nt * 48 <= budget) ? nt : 0;  // all or none
+    }
 
     // film
     size_t npix = (size_t)s.xres * s.yres;
@@ -309,11 +409,12 @@ static void BuildDevice(pbrt_context *c) {
 
 static void AllocPaths(pbrt_context *c, int64_t N) {
     if (N <= c->maxPaths) return;
-    // float arrays: beta 31, rl 1, L 3, lambda0 1, filterW 1, etaScale 1, ray 6, ctx 12, hitB 4,
-    // shadowRay 6, shadowL 3  = 69 floats; int arrays: flags, hitPrim, rayQ x2, matQ, shadowQ = 6
-    const int nf = 69, ni = 7;
+    // float arrays: beta 31, rl 1, L 3, lambda0 1, filterW 1, etaScale 1, ray 6, hitB 2x4,
+    // shadowRay 6, shadowL 3 = 61 floats; int arrays: flags, hitPrim x2, rayQ x2, matQ,
+    // shadowQ, escQ, emitQ = 9
+    const int nf = 61, ni = 9;
     c->fState.Alloc((size_t)nf * N);
-    c->iState.Alloc((size_t)ni * N + 4 * (c->desc.maxDepth + 3));
+    c->iState.Alloc((size_t)ni * N + kCounterStride * (c->desc.maxDepth + 3));
     c->maxPaths = N;
     PathState &st = c->st;
     float *f = c->fState.p;
@@ -329,8 +430,8 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
     st.filterW = take(1);
     st.etaScale = take(1);
     st.ray = take(6);
-    st.ctx = take(12);
-    st.hitB = take(4);
+    st.hitB[0] = take(4);
+    st.hitB[1] = take(4);
     st.shadowRay = take(6);
     st.shadowL = take(3);
     int *ip = c->iState.p;
@@ -340,16 +441,18 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
         return r;
     };
     st.flags = takei(1);
-    st.hitPrim = takei(1);
+    st.hitPrim[0] = takei(1);
+    st.hitPrim[1] = takei(1);
     st.rayQ[0] = takei(1);
     st.rayQ[1] = takei(1);
     st.matQ = takei(1);
     st.shadowQ = takei(1);
     st.escQ = takei(1);
+    st.emitQ = takei(1);
     st.counters = ip;
     if (!c->devStats.p) {
-        c->devStats.Alloc(8);
-        HIPCHECK(hipMemset(c->devStats.p, 0, 8 * sizeof(unsigned long long)));
+        c->devStats.Alloc(kStatsSlots);
+        HIPCHECK(hipMemset(c->devStats.p, 0, kStatsSlots * sizeof(unsigned long long)));
     }
     st.stats = c->devStats.p;
 }
@@ -390,7 +493,7 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
         HIPCHECK(hipMemcpy(c->rows.p, rows.data(), rows.size() * sizeof(int), hipMemcpyHostToDevice));
         c->lastRows = rows;
     }
-    const int countersBytes = 4 * (s.maxDepth + 3) * sizeof(int);
+    const int countersBytes = kCounterStride * (s.maxDepth + 3) * sizeof(int);
     for (size_t r0 = 0; r0 < rows.size(); r0 += rowsPerChunk) {
         int nRows = (int)std::min<int64_t>(rowsPerChunk, rows.size() - r0);
         int64_t P = (int64_t)nRows * width;
@@ -408,12 +511,16 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
             HIPCHECK(hipMemsetAsync(st.counters, 0, countersBytes, c->stream));
             HIPCHECK(LaunchCamera(c->S, st, (int)nActive, c->stream));
             for (int depth = 0; depth <= s.maxDepth; ++depth) {
-                if (p->time_closest) RecordEvent(c, true);
-                HIPCHECK(LaunchClosest(c->S, st, depth, (int)nActive, c->stream));
-                if (p->time_closest) RecordEvent(c, false);
+                // closest-hit launches are event-timed in the first pass of a render only: the
+                // passes are statistically identical and each event pair costs a queue gap
+                const bool timed = p->time_closest && r0 == 0 && s0 == 0;
+                if (timed) RecordEvent(c, true);
+                HIPCHECK(LaunchClosest(c->S, st, depth, (int)nActive, timed ? 1 : 0, c->stream));
+                if (timed) RecordEvent(c, false);
                 if (s.infiniteLights.size()) HIPCHECK(LaunchEscaped(c->S, st, depth, (int)nActive, c->stream));
-                HIPCHECK(LaunchShadeDiffuse(c->S, st, depth, (int)nActive, c->stream));
+                if (s.areaLights.size()) HIPCHECK(LaunchEmissive(c->S, st, depth, (int)nActive, c->stream));
                 if (depth == s.maxDepth) break;
+                HIPCHECK(LaunchShadeDiffuse(c->S, st, depth, (int)nActive, c->stream));
                 HIPCHECK(LaunchShadow(c->S, st, depth, (int)nActive, c->stream));
             }
             HIPCHECK(LaunchFilm(c->S, st, nS, c->stream));
@@ -600,6 +707,7 @@ int pbrt_synchronize(pbrt_context *ctx) {
         ctx->stats.camera_rays = ds[0];
         ctx->stats.closest_rays = ds[1];
         ctx->stats.shadow_rays = ds[2];
+        ctx->stats.timed_closest_rays = ds[3];
         return 0;
     } catch (const std::exception &e) {
         return Fail(e.what());
@@ -615,7 +723,7 @@ int pbrt_reset_stats(pbrt_context *ctx) {
     try {
         HIPCHECK(hipSetDevice(ctx->device));
         HIPCHECK(hipStreamSynchronize(ctx->stream));
-        HIPCHECK(hipMemset(ctx->devStats.p, 0, 8 * sizeof(unsigned long long)));
+        HIPCHECK(hipMemset(ctx->devStats.p, 0, kStatsSlots * sizeof(unsigned long long)));
         ctx->stats = pbrt_render_stats{};
         ctx->eventsUsed = 0;
         return 0;
@@ -705,7 +813,9 @@ float pbrt_debug_halton(const pbrt_scene *scene, int px, int py, int sampleIndex
     if (dim == -1) return RadicalInverse(2, index >> s.haltonBaseExponents[0]);
     if (dim == -2) return RadicalInverse(3, index / s.haltonBaseScales[1]);
     if (dim < 0 || dim >= (int)s.permBase.size()) return -1;
-    return ScrambledRadicalInverse(s.permBase[dim], s.permNDigits[dim], index, s.permTable.data() + s.permOffset[dim]);
+    // the device's evaluation path
+    HaltonDimDesc d = MakeHaltonDimDesc(s.permBase[dim], s.permNDigits[dim], s.permOffset[dim]);
+    return HaltonSampleDimension(d, index, s.permTable.data());
 }
 
 int pbrt_debug_rgb_coeffs(float r, float g, float b, float *c) {
@@ -724,6 +834,21 @@ int pbrt_debug_rgb2spec_column(int maxc, int j, int i, float *out) {
     try {
         auto v = RGB2SpecColumn(maxc, j, i);
         std::copy(v.begin(), v.end(), out);
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_debug_kernel_sections(pbrt_context *ctx, uint64_t *cycles, int n) {
+    try {
+        if (!ctx || !cycles || n <= 0) return Fail("null argument");
+        n = std::min(n, kStatsSlots - kStatsSectionBase);
+        HIPCHECK(hipSetDevice(ctx->device));
+        HIPCHECK(hipStreamSynchronize(ctx->stream));
+        std::vector<unsigned long long> h(kStatsSlots);
+        HIPCHECK(hipMemcpy(h.data(), ctx->devStats.p, kStatsSlots * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        for (int i = 0; i < n; ++i) cycles[i] = h[kStatsSectionBase + i];
         return 0;
     } catch (const std::exception &e) {
         return Fail(e.what());

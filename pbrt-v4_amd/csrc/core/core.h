@@ -118,7 +118,7 @@ PHD float DistanceSquared(V3 a, V3 b) { return LengthSquared(a - b); }
 PHD float Distance(V3 a, V3 b) { return Length(a - b); }
 PHD float MaxComponentValue(V3 v) { return std::fmax(v.x, std::fmax(v.y, v.z)); }
 PHD int MaxComponentIndex(V3 v) { return (v.x > v.y) ? ((v.x > v.z) ? 0 : 2) : ((v.y > v.z) ? 1 : 2); }
-PHD V3 Permute(V3 v, int a, int b, int c) { return {v[a], v[b], v[c]}; }
+PHD V3 Permute(const V3 &v, int a, int b, int c) { return {v[a], v[b], v[c]}; }  // const []: selects, no scratch
 PHD V3 FaceForward(V3 n, V3 v) { return (Dot(n, v) < 0.f) ? -n : n; }
 PHD V3 GramSchmidt(V3 v, V3 w) { return v - Dot(v, w) * w; }
 // util/vecmath.h:974 AngleBetween
@@ -550,29 +550,69 @@ PHD float ScrambledRadicalInverse32(uint32_t base, uint32_t nDigits, uint32_t a,
     }
     return std::fmin(invBaseM * (float)reversedDigits, kOneMinusEpsilon);
 }
-// Same digits with the runtime division by the base replaced by a Granlund-Montgomery
-// multiply (q = (t + ((a - t) >> 1)) >> shift, t = mulhi(magic, a); exact for every 32-bit a).
-// magic = floor(2^32 (2^l - base) / base) + 1, shift = l - 1, l = ceil(log2 base).
-PHD uint32_t HaltonMagic(uint32_t base, uint32_t *shift) {
+// One Halton dimension (HaltonSampler::SampleDimension -> ScrambledRadicalInverse with
+// DigitPermutation, samplers.h:78-87, util/lowdiscrepancy.h:51-76) as the kernels evaluate it.
+// For 32-bit indices and bases with base^nDigits < 2^32 the same digits are produced with the
+// runtime division replaced by a Granlund-Montgomery multiply (q = (t + ((a - t) >> 1)) >> shift,
+// t = mulhi(magic, a), exact for every 32-bit a), all permutation loads issued together and the
+// reversed digits held in 32 bits; the float arithmetic is unchanged.  Otherwise the 64-bit
+// restatement above runs.
+constexpr int kMaxMagicDigits = 8;  // dims >= 6 use bases >= 17: at most 7 digits (float precision)
+struct HaltonDimDesc {
+    uint32_t base, nDigits, permOffset, magic, shift, fast;
+    float invBase;
+    uint32_t pad;
+};
+PHD HaltonDimDesc MakeHaltonDimDesc(uint32_t base, uint32_t nDigits, uint32_t permOffset) {
+    HaltonDimDesc d{};
+    d.base = base;
+    d.nDigits = nDigits;
+    d.permOffset = permOffset;
     uint32_t l = 0;
     while ((1u << l) < base) ++l;
-    *shift = l - 1;
-    return (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - base)) / base + 1);
+    d.shift = l - 1;
+    d.magic = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - base)) / base + 1);
+    uint64_t pw = 1;
+    bool fits = nDigits <= (uint32_t)kMaxMagicDigits;
+    for (uint32_t k = 0; fits && k < nDigits; ++k) {
+        pw *= base;
+        fits = pw < ((uint64_t)1 << 32);
+    }
+    d.fast = fits ? 1u : 0u;
+    d.invBase = (float)1 / (float)base;
+    return d;
 }
-PHD float ScrambledRadicalInverse32Magic(uint32_t base, uint32_t nDigits, uint32_t magic, uint32_t shift, uint32_t a,
-                                          const uint16_t *perm) {
-    float invBase = (float)1 / (float)base, invBaseM = 1;
-    uint64_t reversedDigits = 0;
-    for (uint32_t digitIndex = 0; digitIndex < nDigits; ++digitIndex) {
-        uint32_t t = (uint32_t)(((uint64_t)magic * a) >> 32);
-        uint32_t next = (t + ((a - t) >> 1)) >> shift;
-        uint32_t digitValue = a - next * base;
-        reversedDigits = reversedDigits * base + perm[digitIndex * base + digitValue];
-        invBaseM *= invBase;
+// PermPtr: a plain pointer, or an LDS-qualified one in the kernels that stage the tables.
+template <typename PermPtr>
+PHD float ScrambledRadicalInverse32Magic(const HaltonDimDesc &d, uint32_t a, PermPtr perm) {
+    const uint32_t base = d.base;
+    uint32_t pv[kMaxMagicDigits];
+#pragma unroll
+    for (int k = 0; k < kMaxMagicDigits; ++k) {
+        uint32_t t = (uint32_t)(((uint64_t)d.magic * a) >> 32);
+        uint32_t next = (t + ((a - t) >> 1)) >> d.shift;
+        // unconditional (row clamped to the table) so the loads issue together; rows past
+        // nDigits are discarded below
+        uint32_t row = (uint32_t)k < d.nDigits ? (uint32_t)k : d.nDigits - 1;
+        pv[k] = perm[row * base + (a - next * base)];
         a = next;
+    }
+    float invBaseM = 1;
+    uint32_t reversedDigits = 0;
+#pragma unroll
+    for (int k = 0; k < kMaxMagicDigits; ++k) {
+        if ((uint32_t)k < d.nDigits) {
+            reversedDigits = reversedDigits * base + pv[k];
+            invBaseM *= d.invBase;
+        }
     }
     return std::fmin(invBaseM * (float)reversedDigits, kOneMinusEpsilon);
 }
+PHD float HaltonSampleDimension(const HaltonDimDesc &d, uint64_t index, const uint16_t *permTable) {
+    if ((index >> 32) == 0 && d.fast) return ScrambledRadicalInverse32Magic(d, (uint32_t)index, permTable + d.permOffset);
+    return ScrambledRadicalInverse(d.base, d.nDigits, index, permTable + d.permOffset);
+}
+
 // util/lowdiscrepancy.h RadicalInverse (unscrambled), used for the pixel sample
 PHD float RadicalInverse(uint32_t base, uint64_t a) {
     uint64_t limit = ~0ull / base - base;

@@ -24,7 +24,30 @@ struct DeviceLightNode {
     int isLeaf;
 };
 
+// One area light (a triangle of a DiffuseAreaLight shape) as the light-sampling code reads it:
+// the triangle's vertices and the light's parameters in one 64-byte record.
+struct DeviceAreaLight {
+    float4 v0, v1, v2;  // render-space vertices (.w unused)
+    float scale;
+    int spectrum, twoSided, flip;
+};
+static_assert(sizeof(DeviceAreaLight) == 64, "DeviceAreaLight must be 64 bytes");
+
+// Dynamic-LDS layout of k_shade_diffuse (byte offsets; host-computed per scene).  The block
+// stages everything its lanes look up per wavelength or per sample: sensor tables, light
+// spectra, the Halton permutations of the launch's 7 dimensions, lights and materials.
+struct ShadeLdsLayout {
+    int sensor, dense, perm, lights, lightNodes, mats, matConst, total;
+    int denseInLds, lightsInLds, matsInLds, permEntries;
+};
+
+// per-depth queue counters: counters[depth * kCounterStride + kCnt*]
+constexpr int kCounterStride = 8;
+constexpr int kCntRay = 0, kCntMat = 1, kCntShadow = 2, kCntEscaped = 3, kCntEmissive = 4;
+// device stats slots: [0..7] ray counters, [16..47] per-section wave cycles (profiling build)
+constexpr int kStatsSlots = 48, kStatsSectionBase = 16;
 constexpr int kMaxStackSize = 64;  // traversal stack entries per lane (64 KB of LDS per block)
+constexpr int kSceneLdsBudget = 16 * 1024;  // bytes of BVH nodes + triangles cached in LDS per block
 
 struct DeviceScene {
     // geometry (leaf order)
@@ -45,6 +68,7 @@ struct DeviceScene {
     const int *lightSpectrum;
     const int *lightTwoSided;
     const float *lightArea;
+    const DeviceAreaLight *lights;  // [nAreaLights]
     const uint32_t *lightBitTrail;  // 0xffffffff when not in the light BVH
     // infinite (uniform) lights
     int nInfinite;
@@ -54,7 +78,8 @@ struct DeviceScene {
     int uniformLightSampler;
     const DeviceLightNode *lightNodes;
     int nLightNodes;
-    const float *dense;  // [nSpectra][311]
+    const float *dense;  // [nDense][311]
+    int nDense;
     // sensor (PixelSensor cie1931): x,y,z bar dense tables [3][311]
     const float *sensor;
     const float4 *sensor4;  // same tables interleaved: {xbar, ybar, zbar, 0} per dense entry
@@ -66,14 +91,23 @@ struct DeviceScene {
     // film / filter
     int xres, yres, px0, px1, py0, py1;
     float filterRadiusX, filterRadiusY;
+    int boxFilter;  // box filter: every sample weight is 1 (filters.h:67-71)
     // halton
     const uint16_t *perm;
     const uint32_t *permOffset, *permNDigits, *permBase;
-    const uint4 *haltonDim;  // per dimension {base, nDigits | shift << 8, permOffset, magic}
+    const HaltonDimDesc *haltonDim;  // per dimension (core.h)
+    // the 7 permutation tables of each depth's dims (6+7d .. 12+7d) stored contiguously, each
+    // depth's block starting on a 4-byte boundary; permDepthInfo[8d] = block start (uint16
+    // units), [8d+1+k] = dim k's offset inside the block; [8*maxDepth] = end of the last block
+    const uint16_t *permByDepth;
+    const uint32_t *permDepthInfo;
     int nDims;
     int baseScales[2], baseExponents[2], multInverse[2];
+    int haltonFast32;  // pixel offsets computable in 32 bits (StartPixelSample fast path)
     int maxDepth;
     int stackSize;  // BVH traversal stack entries per lane (BVH8::maxStack)
+    int ldsNodes, ldsTris;  // BVH8 nodes / triangles cached in LDS by the traversal kernels
+    ShadeLdsLayout shadeLds;
 };
 
 // Per-pass wavefront buffers; N = paths per pass = P pixels x S samples.
@@ -91,16 +125,18 @@ struct PathState {
     float *etaScale;    // [N]
     int *flags;         // [N]: bit0 specularBounce, bit1 anyNonSpecular
     float *ray;         // [6][N]
-    float *ctx;         // [12][N]: prev p, n, ns, pError
-    int *hitPrim;       // [N]
-    float *hitB;        // [4][N]: b0, b1, b2, t
+    // Hit records double-buffered by depth parity: the previous bounce's record is the MIS
+    // context of an emissive hit (pbrt's prevIntrCtx), recomputed rather than stored.
+    int *hitPrim[2];    // [N] each
+    float *hitB[2];     // [4][N] each: b0, b1, b2, t
     float *shadowRay;   // [6][N]
     float *shadowL;     // [3][N]
     int *rayQ[2];       // [N]
     int *matQ;          // [N]
     int *shadowQ;       // [N]
     int *escQ;          // [N] escaped rays (only with infinite lights)
-    int *counters;      // [(maxDepth+2) * 4]: ray, mat, shadow, spare per depth
+    int *emitQ;         // [N] hits on emissive triangles
+    int *counters;      // [(maxDepth+2) * kCounterStride]: see kCnt*
     double *film;       // [4][xres*yres]: rgbSum[3], weightSum (sensor RGB)
     unsigned long long *stats;  // [8]: camera rays, closest rays, shadow rays, node visits
 };

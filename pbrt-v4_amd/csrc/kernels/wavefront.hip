@@ -20,9 +20,30 @@
 namespace pbrt_amd {
 
 constexpr int kBlock = 256;
+#ifndef PBRT_TRAVERSAL_WAVES
+#define PBRT_TRAVERSAL_WAVES 4  // waves/SIMD the closest/shadow kernels are compiled for
+#endif
+#ifndef PBRT_SHADE_WAVES
+#define PBRT_SHADE_WAVES 3  // waves/SIMD the shade kernel is compiled for (VGPR budget)
+#endif
 constexpr float kInvWavelengthPDF = kLambdaMax - kLambdaMin;  // 1 / SampleUniformWavelengths pdf
 
 // ------------------------------------------------------------------ helpers
+// Section timing (profiling build only): wave-level s_memtime deltas summed per section by the
+// wave's first active lane into stats[kStatsSectionBase + k].
+#ifdef PBRT_AMD_SECTION_TIMING
+#define SEC_BEGIN() unsigned long long secT_ = __builtin_amdgcn_s_memtime()
+#define SEC_MARK(st, k)                                                                          \
+    do {                                                                                         \
+        unsigned long long n_ = __builtin_amdgcn_s_memtime();                                    \
+        if (__lane_id() == __ffsll((long long)__ballot(1)) - 1)                                   \
+            atomicAdd(&(st).stats[kStatsSectionBase + (k)], n_ - secT_);                         \
+        secT_ = n_;                                                                              \
+    } while (0)
+#else
+#define SEC_BEGIN() (void)0
+#define SEC_MARK(st, k) (void)0
+#endif
 __device__ inline int WavePush(int *counter, bool pred) {
     unsigned long long mask = __ballot(pred);
     if (mask == 0) return -1;
@@ -33,6 +54,60 @@ __device__ inline int WavePush(int *counter, bool pred) {
     base = __shfl(base, leader);
     return pred ? base + __popcll(mask & ((1ull << lane) - 1ull)) : -1;
 }
+
+// Append to up to K queues for a whole block: one global atomicAdd per queue per block, so the
+// queue counters (one address each, serialised at one L2 channel) see a quarter of the
+// per-wave traffic.  Lanes receive consecutive slots in (wave, lane) order.  Every thread of
+// the block must call it (the callers' grid-stride loops are block-uniform).
+template <int K>
+__device__ inline void BlockPush(int *const (&counters)[K], const bool (&pred)[K], int (&pos)[K]) {
+    constexpr int kWaves = kBlock / 64;
+    __shared__ int sCount[K][kWaves];
+    __shared__ int sBase[K];
+    const int lane = __lane_id(), wave = threadIdx.x >> 6;
+    unsigned long long mask[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        mask[k] = __ballot(pred[k]);
+        if (lane == 0) sCount[k][wave] = __popcll(mask[k]);
+    }
+    __syncthreads();
+    if (threadIdx.x < K) {
+        const int k = threadIdx.x;
+        int tot = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) tot += sCount[k][w];
+        sBase[k] = tot ? atomicAdd(counters[k], tot) : 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        int b = sBase[k];
+        for (int w = 0; w < wave; ++w) b += sCount[k][w];
+        pos[k] = pred[k] ? b + __popcll(mask[k] & ((1ull << lane) - 1ull)) : -1;
+    }
+    __syncthreads();  // sCount/sBase are reused by the next call
+}
+
+// Block-wide global -> LDS copies by LDS-DMA (global_load_lds_*): no VGPR round trip and no
+// wait per element, so a prologue of several tables costs one memory latency.  Each wave
+// copies 64 consecutive elements per instruction (LDS destination = wave base + lane * size);
+// lanes past the end are masked.  Callers finish with DmaWait() and one __syncthreads().
+template <int Bytes>  // 4 or 16 (sub-dword LDS-DMA does not pack lanes)
+__device__ inline void DmaCopy(const void *src, void *ldsDst, int n) {
+    const int lane = __lane_id(), wave = threadIdx.x >> 6, nWaves = blockDim.x >> 6;
+    for (int base = wave * 64; base < n; base += nWaves * 64) {
+        if (base + lane < n) {
+            auto g = (const __attribute__((address_space(1))) void *)((const char *)src + (size_t)(base + lane) * Bytes);
+            auto l = (__attribute__((address_space(3))) void *)((char *)ldsDst + (size_t)base * Bytes);
+            // the builtin's size operand must be a literal
+            static_assert(Bytes == 4 || Bytes == 16, "DmaCopy: 4- or 16-byte elements");
+            if constexpr (Bytes == 4) __builtin_amdgcn_global_load_lds(g, l, 4, 0, 0);
+            else __builtin_amdgcn_global_load_lds(g, l, 16, 0, 0);
+        }
+    }
+}
+__device__ inline void DmaWait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 __device__ inline V3 XfPoint(const float *m, V3 p) {
     float xp = m[0] * p.x + m[1] * p.y + m[2] * p.z + m[3];
@@ -56,6 +131,24 @@ __device__ inline Halton StartPixelSample(const DeviceScene &S, int px, int py, 
     // samplers.h:53-71
     Halton h;
     h.index = 0;
+    if (S.haltonFast32) {
+        // Same terms in 32-bit arithmetic: the host checked that the stride and every partial
+        // sum fit (stride * (scale0 + scale1) < 2^32), so no 64-bit division is needed.
+        const uint32_t stride = (uint32_t)S.baseScales[0] * (uint32_t)S.baseScales[1];
+        uint32_t pmx = (uint32_t)px & 127u, pmy = (uint32_t)py & 127u;  // Mod(p, 128), p >= 0
+        uint32_t i0 = (uint32_t)InverseRadicalInverse((uint64_t)pmx, 2, S.baseExponents[0]);
+        uint32_t i1 = 0;
+        for (int k = 0; k < S.baseExponents[1]; ++k) {
+            uint32_t q = pmy / 3u;
+            i1 = i1 * 3u + (pmy - 3u * q);
+            pmy = q;
+        }
+        uint32_t t = i0 * (uint32_t)S.baseScales[1] * (uint32_t)S.multInverse[0] +
+                     i1 * (uint32_t)S.baseScales[0] * (uint32_t)S.multInverse[1];
+        h.index = (uint64_t)(t % stride) + (uint64_t)sampleIndex * stride;
+        h.dimension = dim < 2 ? 2 : dim;
+        return h;
+    }
     uint64_t sampleStride = (uint64_t)S.baseScales[0] * S.baseScales[1];
     if (sampleStride > 1) {
         int pmx = px % 128, pmy = py % 128;
@@ -72,11 +165,7 @@ __device__ inline Halton StartPixelSample(const DeviceScene &S, int px, int py, 
     return h;
 }
 __device__ inline float SampleDim(const DeviceScene &S, uint64_t index, int dim) {
-    if ((index >> 32) == 0) {  // 32-bit digit extraction: same digits, division by multiply
-        const uint4 hd = S.haltonDim[dim];
-        return ScrambledRadicalInverse32Magic(hd.x, hd.y & 0xffu, hd.w, hd.y >> 8, (uint32_t)index, S.perm + hd.z);
-    }
-    return ScrambledRadicalInverse(S.permBase[dim], S.permNDigits[dim], index, S.perm + S.permOffset[dim]);
+    return HaltonSampleDimension(S.haltonDim[dim], index, S.perm);
 }
 __device__ inline float Get1D(const DeviceScene &S, Halton &h) {
     if (h.dimension >= S.nDims) h.dimension = 2;
@@ -113,7 +202,8 @@ struct RayPre {
     int neg[3];
 };
 
-__device__ inline void SlabTest4(const float4 *__restrict__ q, int g, const RayPre &r, float raytMax, float tn[8],
+template <typename F4>
+__device__ inline void SlabTest4(const F4 *__restrict__ q, int g, const RayPre &r, float raytMax, float tn[8],
                                  unsigned *mask) {
     // children 4g..4g+3: lox,loy,loz at float4 index 2a+g, hix,hiy,hiz at 6+2a+g
     float4 L[3], H[3];
@@ -152,16 +242,57 @@ __device__ inline void SlabTest4(const float4 *__restrict__ q, int g, const RayP
     }
 }
 
-__device__ inline void SlabTest8(const BVH8Node *__restrict__ np, const RayPre &r, float raytMax, float tn[8],
+template <typename F4>
+__device__ inline void SlabTest8(const F4 *__restrict__ q, const RayPre &r, float raytMax, float tn[8],
                                  unsigned *mask) {
-    const float4 *q = reinterpret_cast<const float4 *>(np);
     *mask = 0;
     SlabTest4(q, 0, r, raytMax, tn, mask);
     SlabTest4(q, 1, r, raytMax, tn, mask);
 }
 
-template <bool AnyHit>
-__device__ inline int Traverse(const DeviceScene &S, V3 o, V3 d, float tMax, TriHit *best, int *lds) {
+// Scene cache in LDS: the first S.ldsNodes BVH8 nodes (BFS order = the top of the tree) at a
+// 17-float4 stride and the first S.ldsTris triangles of the leaf order.  The 68-dword node
+// stride puts the same field of 16 different nodes in 16 different 4-bank groups, so the
+// ds_read_b128 lane groups stay conflict-free when lanes sit in different nodes; the 12-dword
+// triangle stride does the same for triangles.  Everything else is read from global memory.
+constexpr int kLdsNodeStride = 17;  // float4 per cached node
+
+// LDS-qualified pointers keep the cached and the global paths distinct instructions
+// (ds_read_b128 vs global_load_dwordx4); generic pointers would merge them into flat loads.
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef __attribute__((address_space(3))) const float4 LdsF4;
+#else
+typedef const float4 LdsF4;  // host pass only parses the kernels
+#endif
+struct SceneLds {
+    int *stack;          // [stackSize][blockDim]
+    const LdsF4 *nodes;  // [ldsNodes][17]
+    const LdsF4 *tris;   // [ldsTris][3]
+};
+
+// Lays out the dynamic LDS of a traversal kernel and fills the cache (whole block, one sync).
+__device__ inline SceneLds SetupSceneLds(const DeviceScene &S, float4 *dyn) {
+    SceneLds L;
+    L.stack = reinterpret_cast<int *>(dyn);
+    float4 *nodes = dyn + (S.stackSize * kBlock) / 4;
+    float4 *tris = nodes + S.ldsNodes * kLdsNodeStride;
+    // plain copies: measured faster here than per-node LDS-DMA (few, tiny rows)
+    const float4 *gn = reinterpret_cast<const float4 *>(S.nodes);
+    for (int i = threadIdx.x; i < S.ldsNodes * 14; i += blockDim.x) {
+        int n = i / 14, k = i - n * 14;
+        nodes[n * kLdsNodeStride + k] = gn[n * 16 + k];
+    }
+    for (int i = threadIdx.x; i < S.ldsTris * 3; i += blockDim.x) tris[i] = S.triVerts[i];
+    __syncthreads();
+    L.nodes = (const LdsF4 *)nodes;
+    L.tris = (const LdsF4 *)tris;
+    return L;
+}
+
+// TrisInLds: every triangle is cached (a launch-uniform choice, so no per-lane branch whose
+// two loads the compiler would merge into one flat load).
+template <bool AnyHit, bool TrisInLds>
+__device__ inline int TraverseT(const DeviceScene &S, const SceneLds &L, V3 o, V3 d, float tMax, TriHit *best) {
     const TriRay tr = MakeTriRay(o, d);
     RayPre r;
     r.o = o;
@@ -170,17 +301,28 @@ __device__ inline int Traverse(const DeviceScene &S, V3 o, V3 d, float tMax, Tri
     r.neg[1] = r.invDir.y < 0;
     r.neg[2] = r.invDir.z < 0;
     const int lane = threadIdx.x, stride = blockDim.x;
+    int *lds = L.stack;
     int sp = 0;
     int node = 0;
     int hitPrim = -1;
     while (true) {
-        const BVH8Node *np = S.nodes + node;
         float tn[8];
         unsigned mask;
-        SlabTest8(np, r, tMax, tn, &mask);
+        int4 ch0, ch1;
+        if (node < S.ldsNodes) {
+            const LdsF4 *q = L.nodes + node * kLdsNodeStride;
+            SlabTest8(q, r, tMax, tn, &mask);
+            float4 c0 = q[12], c1 = q[13];
+            ch0 = make_int4(__float_as_int(c0.x), __float_as_int(c0.y), __float_as_int(c0.z), __float_as_int(c0.w));
+            ch1 = make_int4(__float_as_int(c1.x), __float_as_int(c1.y), __float_as_int(c1.z), __float_as_int(c1.w));
+        } else {
+            const BVH8Node *np = S.nodes + node;
+            SlabTest8(reinterpret_cast<const float4 *>(np), r, tMax, tn, &mask);
+            ch0 = reinterpret_cast<const int4 *>(np->child)[0];
+            ch1 = reinterpret_cast<const int4 *>(np->child)[1];
+        }
         // empty slots carry an inverted box, so they never pass the slab test
         unsigned leaves = 0, inner = 0;
-        int4 ch0 = reinterpret_cast<const int4 *>(np->child)[0], ch1 = reinterpret_cast<const int4 *>(np->child)[1];
         int ch[8] = {ch0.x, ch0.y, ch0.z, ch0.w, ch1.x, ch1.y, ch1.z, ch1.w};
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
@@ -206,7 +348,16 @@ __device__ inline int Traverse(const DeviceScene &S, V3 o, V3 d, float tMax, Tri
             for (int c = 0; c < 8; ++c) enc = (c == bc) ? ~ch[c] : enc;
             int first = enc >> 3, count = (enc & 7) + 1;
             for (int t = first; t < first + count; ++t) {
-                float4 a = S.triVerts[3 * t], b = S.triVerts[3 * t + 1], c = S.triVerts[3 * t + 2];
+                float4 a, b, c;
+                if (TrisInLds) {
+                    a = L.tris[3 * t];
+                    b = L.tris[3 * t + 1];
+                    c = L.tris[3 * t + 2];
+                } else {
+                    a = S.triVerts[3 * t];
+                    b = S.triVerts[3 * t + 1];
+                    c = S.triVerts[3 * t + 2];
+                }
                 TriHit h;
                 if (IntersectTriangleRay(tr, tMax, V3(a.x, a.y, a.z), V3(b.x, b.y, b.z), V3(c.x, c.y, c.z), &h)) {
                     if (AnyHit) return t;
@@ -237,6 +388,12 @@ __device__ inline int Traverse(const DeviceScene &S, V3 o, V3 d, float tMax, Tri
         node = lds[(--sp) * stride + lane];
     }
     return hitPrim;
+}
+
+template <bool AnyHit>
+__device__ inline int Traverse(const DeviceScene &S, const SceneLds &L, V3 o, V3 d, float tMax, TriHit *best) {
+    if (S.ldsTris > 0) return TraverseT<AnyHit, true>(S, L, o, d, tMax, best);
+    return TraverseT<AnyHit, false>(S, L, o, d, tMax, best);
 }
 
 // ------------------------------------------------------------------ lights
@@ -312,16 +469,14 @@ __device__ inline bool SampleTriangle(V3 p0, V3 p1, V3 p2, bool flip, V3 refP, V
 }
 
 // Triangle::PDF(ctx, wi) (shapes.h:1133-1174)
-__device__ inline float TrianglePDF(const DeviceScene &S, int prim, V3 refP, V3 refPErr, V3 refN, V3 refNs, V3 wi) {
-    V3 p0, p1, p2;
-    PrimVerts(S, prim, &p0, &p1, &p2);
+__device__ inline float TrianglePDF(V3 p0, V3 p1, V3 p2, bool flip, V3 refP, V3 refPErr, V3 refN, V3 refNs, V3 wi) {
     float solidAngle = SolidAngleOf(p0, p1, p2, refP);
     if (solidAngle < kMinSphericalSampleArea || solidAngle > kMaxSphericalSampleArea) {
         // ShapeSampleContext::SpawnRay(wi) then Triangle::Intersect
         V3 o = OffsetRayOrigin(refP, refPErr, refN, wi);
         TriHit h;
         if (!IntersectTriangle(o, wi, kInfinity, p0, p1, p2, &h)) return 0;
-        TriSurface hs = TriangleSurface(p0, p1, p2, h.b0, h.b1, h.b2, S.primFlip[prim]);
+        TriSurface hs = TriangleSurface(p0, p1, p2, h.b0, h.b1, h.b2, flip);
         V3 pHit = hs.p, n = hs.n;
         float pdf = (1 / TriArea(p0, p1, p2)) / (AbsDotN(n, -wi) / DistanceSquared(refP, pHit));
         if (isinf(pdf)) pdf = 0;
@@ -459,14 +614,14 @@ __global__ void __launch_bounds__(kBlock) k_camera(DeviceScene S, PathState st, 
         o = oo;
         d = dd;
     }
+    // beta = 1 and r_u = r_l = 1 at depth 0 are implicit (the depth-0 kernels use the constants
+    // and never read them), and the box filter's weight is always 1: none is stored.
     int N = st.N;
-    for (int i = 0; i < kNSpectrumSamples; ++i) st.beta[i * N + slot] = 1.f;
-    st.rl[slot] = 1.f;
     st.L[slot] = 0;
     st.L[N + slot] = 0;
     st.L[2 * N + slot] = 0;
     st.lambda0[slot] = lambda0;
-    st.filterW[slot] = 1.f;
+    if (!S.boxFilter) st.filterW[slot] = 1.f;
     st.etaScale[slot] = 1.f;
     st.flags[slot] = 0;
     st.ray[slot] = o.x;
@@ -474,43 +629,57 @@ __global__ void __launch_bounds__(kBlock) k_camera(DeviceScene S, PathState st, 
     st.ray[2 * N + slot] = o.z;
     st.ray[3 * N + slot] = d.x;
     st.ray[4 * N + slot] = d.y;
-    st.ray[5 * N + slot] = d.z;
-    st.rayQ[0][slot] = slot;
+    st.ray[5 * N + slot] = d.z;  // the depth-0 ray queue is the identity (k_closest)
 }
 
-__global__ void __launch_bounds__(kBlock) k_closest(DeviceScene S, PathState st, int depth) {
-    extern __shared__ int stackLds[];
+__global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_closest(DeviceScene S, PathState st, int depth, int timed) {
+    if ((int)(blockIdx.x * blockDim.x) >= st.counters[depth * kCounterStride + kCntRay]) return;  // no work
+    extern __shared__ float4 dynLds[];
+    const SceneLds L = SetupSceneLds(S, dynLds);
     int N = st.N;
     const int *q = st.rayQ[depth & 1];
-    const int count = st.counters[depth * 4 + 0];
-    int *matCounter = &st.counters[depth * 4 + 1];
-    int *escCounter = &st.counters[depth * 4 + 3];
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&st.stats[1], (unsigned long long)count);
+    const int count = st.counters[depth * kCounterStride + kCntRay];
+    int *matCounter = &st.counters[depth * kCounterStride + kCntMat];
+    int *escCounter = &st.counters[depth * kCounterStride + kCntEscaped];
+    int *emitCounter = &st.counters[depth * kCounterStride + kCntEmissive];
+    int *hitPrim = st.hitPrim[depth & 1];
+    float *hitB = st.hitB[depth & 1];
+    const bool shade = depth < S.maxDepth;  // at maxDepth only emission and escape matter
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        atomicAdd(&st.stats[1], (unsigned long long)count);
+        if (timed) atomicAdd(&st.stats[3], (unsigned long long)count);  // rays of event-timed launches
+    }
     for (int base = blockIdx.x * blockDim.x; base < count; base += gridDim.x * blockDim.x) {
         int qi = base + threadIdx.x;
         bool active = qi < count;
-        int slot = active ? q[qi] : 0;
+        int slot = active ? (depth == 0 ? qi : q[qi]) : 0;
         int prim = -1;
         TriHit h;
         V3 o, d;
         if (active) {
             o = V3(st.ray[slot], st.ray[N + slot], st.ray[2 * N + slot]);
             d = V3(st.ray[3 * N + slot], st.ray[4 * N + slot], st.ray[5 * N + slot]);
-            prim = Traverse<false>(S, o, d, kInfinity, &h, stackLds);
+            prim = Traverse<false>(S, L, o, d, kInfinity, &h);
             if (prim >= 0) {
-                st.hitPrim[slot] = prim;
-                st.hitB[slot] = h.b0;
-                st.hitB[N + slot] = h.b1;
-                st.hitB[2 * N + slot] = h.b2;
-                st.hitB[3 * N + slot] = h.t;
+                hitPrim[slot] = prim;
+                hitB[slot] = h.b0;
+                hitB[N + slot] = h.b1;
+                hitB[2 * N + slot] = h.b2;
+                hitB[3 * N + slot] = h.t;
             }
         }
-        if (S.nInfinite > 0) {
-            int epos = WavePush(escCounter, active && prim < 0);
-            if (epos >= 0) st.escQ[epos] = slot;
-        }
-        int pos = WavePush(matCounter, active && prim >= 0);
-        if (pos >= 0) st.matQ[pos] = slot;
+        // EnqueueWorkAfterIntersection / Miss (intersect.h:48-156): misses to the escaped-ray
+        // queue (infinite lights only), emissive hits to the hit-area-light queue, every hit
+        // to its material queue
+        int *const cnt[3] = {escCounter, emitCounter, matCounter};
+        const bool pred[3] = {S.nInfinite > 0 && active && prim < 0,
+                              S.nAreaLights > 0 && active && prim >= 0 && S.primLight[prim] >= 0,
+                              shade && active && prim >= 0};
+        int pos[3];
+        BlockPush<3>(cnt, pred, pos);
+        if (pos[0] >= 0) st.escQ[pos[0]] = slot;
+        if (pos[1] >= 0) st.emitQ[pos[1]] = slot;
+        if (pos[2] >= 0) st.matQ[pos[2]] = slot;
     }
 }
 
@@ -518,7 +687,7 @@ __global__ void __launch_bounds__(kBlock) k_closest(DeviceScene S, PathState st,
 // PDF_Li(allowIncompletePDF = true) == 0, so r_l contributes nothing.
 __global__ void __launch_bounds__(kBlock) k_escaped(DeviceScene S, PathState st, int depth) {
     int N = st.N;
-    const int count = st.counters[depth * 4 + 3];
+    const int count = st.counters[depth * kCounterStride + kCntEscaped];
     for (int qi = blockIdx.x * blockDim.x + threadIdx.x; qi < count; qi += gridDim.x * blockDim.x) {
         int slot = st.escQ[qi];
         int fl = st.flags[slot];
@@ -540,7 +709,7 @@ __global__ void __launch_bounds__(kBlock) k_escaped(DeviceScene S, PathState st,
                 int off = DenseOffset(lam);
                 float Le = scale * (off < 0 ? 0.f : dense[off]);
                 nz |= Le != 0;
-                float v = (st.beta[i * N + slot] * Le * invDenom) * kInvWavelengthPDF;
+                float v = ((depth > 0 ? st.beta[i * N + slot] : 1.f) * Le * invDenom) * kInvWavelengthPDF;
                 float xb = off < 0 ? 0.f : S.sensor[off], yb = off < 0 ? 0.f : S.sensor[kDenseN + off],
                       zb = off < 0 ? 0.f : S.sensor[2 * kDenseN + off];
                 sx = i == 0 ? xb * v : sx + xb * v;
@@ -587,9 +756,11 @@ __device__ inline float Reflectance(float4 mc, bool constant, float lambda) {
 // and nothing that steers a path (beta, pdfs and RR keep the reference's exact operations).
 struct SensorAcc {
     float sx = 0, sy = 0, sz = 0;
-    __device__ void Add(const DeviceScene &S, int off, float c, bool first) {
+    __device__ void Add(const DeviceScene &S, int off, float c, bool first) { Add(S.sensor4, off, c, first); }
+    template <typename F4>
+    __device__ void Add(const F4 *sensor4, int off, float c, bool first) {
         float v = c * kInvWavelengthPDF;
-        float4 sb = off < 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : S.sensor4[off];
+        float4 sb = off < 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : float4(sensor4[off]);
         float xb = sb.x, yb = sb.y, zb = sb.z;
         sx = first ? xb * v : sx + xb * v;
         sy = first ? yb * v : sy + yb * v;
@@ -597,88 +768,208 @@ struct SensorAcc {
     }
 };
 
-__global__ void __launch_bounds__(kBlock) k_shade_diffuse(DeviceScene S, PathState st, int depth) {
-    __shared__ float bfLds[kNSpectrumSamples * kBlock];  // [lambda][lane]: conflict-free
+// HandleEmissiveIntersection (integrator.cpp:539-573) over the hit-area-light queue.  The MIS
+// context (pbrt's prevIntrCtx: p, n, ns, pError of the previous surface) is rebuilt from the
+// previous bounce's hit record with the same TriangleSurface arithmetic that produced it.
+__global__ void __launch_bounds__(kBlock) k_emissive(DeviceScene S, PathState st, int depth) {
     int N = st.N;
-    const int count = st.counters[depth * 4 + 1];
-    int *nextCounter = &st.counters[(depth + 1) * 4 + 0];
-    int *shadowCounter = &st.counters[depth * 4 + 2];
+    const int count = st.counters[depth * kCounterStride + kCntEmissive];
+    const int *hitPrim = st.hitPrim[depth & 1];
+    const float *hitB = st.hitB[depth & 1];
+    const int *prevPrim = st.hitPrim[(depth + 1) & 1];
+    const float *prevB = st.hitB[(depth + 1) & 1];
+    for (int qi = blockIdx.x * blockDim.x + threadIdx.x; qi < count; qi += gridDim.x * blockDim.x) {
+        // The queue is short, so this kernel's time is its dependent-load chain: every load
+        // that depends only on the slot is issued up front, beta's 31 values included.
+        const int slot = st.emitQ[qi];
+        const int prim = hitPrim[slot];
+        const float b0 = hitB[slot], b1 = hitB[N + slot], b2 = hitB[2 * N + slot];
+        const V3 rd(st.ray[3 * N + slot], st.ray[4 * N + slot], st.ray[5 * N + slot]);
+        const float lambda0 = st.lambda0[slot];
+        const bool mis = depth > 0 && !(st.flags[slot] & 1);
+        const float rl = depth > 0 ? st.rl[slot] : 1.f;
+        const int pp = depth > 0 ? prevPrim[slot] : 0;
+        const float pb0 = depth > 0 ? prevB[slot] : 0.f, pb1 = depth > 0 ? prevB[N + slot] : 0.f,
+                    pb2 = depth > 0 ? prevB[2 * N + slot] : 0.f;
+        float beta[kNSpectrumSamples];
+#pragma unroll
+        for (int i = 0; i < kNSpectrumSamples; ++i) beta[i] = depth > 0 ? st.beta[(size_t)i * N + slot] : 1.f;
+        V3 p0, p1, p2;
+        PrimVerts(S, prim, &p0, &p1, &p2);
+        const int light = S.primLight[prim];
+        const bool flip = S.primFlip[prim];
+        TriSurface surf = TriangleSurface(p0, p1, p2, b0, b1, b2, flip);
+        V3 wo = Normalize(-rd);
+        const DeviceAreaLight Ld = S.lights[light];
+        if (!(Ld.twoSided || DotN(surf.n, wo) >= 0)) continue;
+        float denom;
+        if (!mis) {
+            denom = Avg31(1.f);
+        } else {
+            V3 q0, q1, q2;
+            PrimVerts(S, pp, &q0, &q1, &q2);
+            TriSurface prev = TriangleSurface(q0, q1, q2, pb0, pb1, pb2, S.primFlip[pp]);
+            float lightChoicePDF = LightPMF(S, prev.p, prev.n, light);
+            V3 l0(Ld.v0.x, Ld.v0.y, Ld.v0.z), l1(Ld.v1.x, Ld.v1.y, Ld.v1.z), l2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
+            float lightPDF = lightChoicePDF * TrianglePDF(l0, l1, l2, Ld.flip, prev.p, prev.pErr, prev.n, prev.n, -wo);
+            denom = Avg31(1.f + rl * lightPDF);
+        }
+        const float *dense = S.dense + Ld.spectrum * kDenseN;
+        const float invDenom = 1 / denom;
+        SensorAcc acc;
+        SpectralIter it(lambda0);
+#pragma unroll
+        for (int i = 0; i < kNSpectrumSamples; ++i, it.Next()) {
+            int off = DenseOffset(it.lam);
+            float Le = Ld.scale * (off < 0 ? 0.f : dense[off]);
+            acc.Add(S, off, beta[i] * Le * invDenom, i == 0);
+        }
+        st.L[slot] += S.imagingRatio * (acc.sx / kNSpectrumSamples);
+        st.L[N + slot] += S.imagingRatio * (acc.sy / kNSpectrumSamples);
+        st.L[2 * N + slot] += S.imagingRatio * (acc.sz / kNSpectrumSamples);
+    }
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef __attribute__((address_space(3))) const float LdsF;
+typedef __attribute__((address_space(3))) const uint16_t LdsU16;
+#else
+typedef const float LdsF;
+typedef const uint16_t LdsU16;
+#endif
+
+// Light-sample contribution beta*f*|cos|*Le/denom summed to sensor RGB (surfscatter.cpp:288-308,
+// then film.h:95-100); returns whether Le was nonzero at any wavelength.
+template <typename FD>
+__device__ inline bool NeeAccumulate(const FD *dense, const LdsF4 *sensor4, const float *bf, float lambda0,
+                                     float scale, float absdot, float invDenom, SensorAcc *acc) {
+    bool nz = false;
+#pragma unroll 4
+    for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next()) {
+        int off = DenseOffset(it.lam);
+        float Le = scale * (off < 0 ? 0.f : float(dense[off]));
+        nz |= Le != 0;
+        acc->Add(sensor4, off, bf[it.i * kBlock] * absdot * Le * invDenom, it.i == 0);
+    }
+    return nz;
+}
+
+// EvaluateMaterialAndBSDF<DiffuseMaterial> (surfscatter.cpp:57-328) fused with
+// GenerateRaySamples (samples.cpp:29-66) for one depth.  Every table a lane looks up per
+// wavelength or per sample is staged in LDS by the block first (ShadeLdsLayout): sensor
+// curves, light spectra, this depth's 7 Halton permutation tables, lights, light BVH and
+// materials.  The only HBM traffic per item is its path state, the hit triangle and beta,
+// whose 31 values arrive by LDS-DMA while the sampler runs on LDS-resident tables.
+__global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(DeviceScene S, PathState st, int depth) {
+    if ((int)(blockIdx.x * blockDim.x) >= st.counters[depth * kCounterStride + kCntMat]) return;  // no work
+    extern __shared__ float4 dynLds[];
+    char *ldsBase = reinterpret_cast<char *>(dynLds);
+    const ShadeLdsLayout lay = S.shadeLds;
+    float *bfLds = reinterpret_cast<float *>(ldsBase);  // [lambda][lane]: conflict-free
+    float4 *sensorLds = reinterpret_cast<float4 *>(ldsBase + lay.sensor);
+    float *denseLds = reinterpret_cast<float *>(ldsBase + lay.dense);
+    uint16_t *permLds = reinterpret_cast<uint16_t *>(ldsBase + lay.perm);
+    DeviceAreaLight *lightsLds = reinterpret_cast<DeviceAreaLight *>(ldsBase + lay.lights);
+    DeviceLightNode *nodesLds = reinterpret_cast<DeviceLightNode *>(ldsBase + lay.lightNodes);
+    float4 *matsLds = reinterpret_cast<float4 *>(ldsBase + lay.mats);
+    int *matConstLds = reinterpret_cast<int *>(ldsBase + lay.matConst);
+    const int d0 = 6 + 7 * depth;  // first sampler dimension of this depth
+    uint32_t permOff[7];
+    {
+        DmaCopy<16>(S.sensor4, sensorLds, kDenseN);
+        if (lay.denseInLds) DmaCopy<4>(S.dense, denseLds, S.nDense * kDenseN);
+        // this depth's 7 permutation tables, stored contiguously per depth on the host
+        const uint32_t *info = S.permDepthInfo + depth * 8;  // {start, off0..off6}
+#pragma unroll
+        for (int k = 0; k < 7; ++k) permOff[k] = info[1 + k];
+        const uint32_t start = info[0], words = (S.permDepthInfo[(depth + 1) * 8] - start + 1) / 2;
+        DmaCopy<4>(S.permByDepth + start, permLds, (int)words);
+        if (lay.lightsInLds) {
+            DmaCopy<4>(S.lights, lightsLds, S.nAreaLights * (int)(sizeof(DeviceAreaLight) / 4));
+            DmaCopy<4>(S.lightNodes, nodesLds, S.nLightNodes * (int)(sizeof(DeviceLightNode) / 4));
+        }
+        if (lay.matsInLds) {
+            DmaCopy<16>(S.matCoeffs, matsLds, S.nMaterials);
+            DmaCopy<4>(S.matConstant, matConstLds, S.nMaterials);
+        }
+        DmaWait();
+        __syncthreads();
+    }
+    const LdsF4 *sensorL = (const LdsF4 *)sensorLds;
+    const LdsU16 *permL = (const LdsU16 *)permLds;
+    DeviceScene SL = S;  // light sampler reads its nodes from LDS
+    if (lay.lightsInLds) SL.lightNodes = nodesLds;
+    const DeviceAreaLight *lightsL = lay.lightsInLds ? lightsLds : S.lights;
+    const float4 *matsL = lay.matsInLds ? matsLds : S.matCoeffs;
+    const int *matConstL = lay.matsInLds ? matConstLds : S.matConstant;
+
+    int N = st.N;
+    const int count = st.counters[depth * kCounterStride + kCntMat];
+    int *nextCounter = &st.counters[(depth + 1) * kCounterStride + kCntRay];
+    int *shadowCounter = &st.counters[depth * kCounterStride + kCntShadow];
     int *nextQ = st.rayQ[(depth + 1) & 1];
+    const int *hitPrim = st.hitPrim[depth & 1];
+    const float *hitB = st.hitB[depth & 1];
     for (int base = blockIdx.x * blockDim.x; base < count; base += gridDim.x * blockDim.x) {
         int qi = base + threadIdx.x;
         bool active = qi < count;
         bool pushRay = false, pushShadow = false;
         int slot = active ? st.matQ[qi] : 0;
+        SEC_BEGIN();
         if (active) {
             const float lambda0 = st.lambda0[slot];
             const float *betaP = st.beta + slot;
-            int prim = st.hitPrim[slot];
-            float b0 = st.hitB[slot], b1 = st.hitB[N + slot], b2 = st.hitB[2 * N + slot];
+            int prim = hitPrim[slot];
+            float b0 = hitB[slot], b1 = hitB[N + slot], b2 = hitB[2 * N + slot];
             V3 rd(st.ray[3 * N + slot], st.ray[4 * N + slot], st.ray[5 * N + slot]);
+            int px, py, sampleIndex;
+            PixelOf(st, slot, &px, &py, &sampleIndex);
+            px += S.px0;
             V3 p0, p1, p2;
             PrimVerts(S, prim, &p0, &p1, &p2);
+            const int mat = S.primMaterial[prim];
             TriSurface surf = TriangleSurface(p0, p1, p2, b0, b1, b2, S.primFlip[prim]);
+            const float4 mc = matsL[mat];
+            const bool constant = matConstL[mat];
             V3 wo = Normalize(-rd);
             V3 n = surf.n, ns = surf.n;
-            int fl = st.flags[slot];
-            float rl = st.rl[slot];
-            float Lr = 0, Lg = 0, Lb = 0;
-            // ---- HandleEmissiveIntersection (integrator.cpp:539-573)
-            int light = S.primLight[prim];
-            if (light >= 0 && (S.lightTwoSided[light] || DotN(n, wo) >= 0)) {
-                float denom;
-                if (depth == 0 || (fl & 1)) {
-                    denom = Avg31(1.f);
-                } else {
-                    V3 cp(st.ctx[slot], st.ctx[N + slot], st.ctx[2 * N + slot]);
-                    V3 cn(st.ctx[3 * N + slot], st.ctx[4 * N + slot], st.ctx[5 * N + slot]);
-                    V3 cns(st.ctx[6 * N + slot], st.ctx[7 * N + slot], st.ctx[8 * N + slot]);
-                    V3 cpe(st.ctx[9 * N + slot], st.ctx[10 * N + slot], st.ctx[11 * N + slot]);
-                    float lightChoicePDF = LightPMF(S, cp, cns, light);
-                    float lightPDF = lightChoicePDF * TrianglePDF(S, S.lightPrim[light], cp, cpe, cn, cns, -wo);
-                    denom = Avg31(1.f + rl * lightPDF);
-                }
-                const float *dense = S.dense + S.lightSpectrum[light] * kDenseN;
-                float scale = S.lightScale[light];
-                SensorAcc acc;
-                const float invDenom = 1 / denom;
-#pragma unroll 4
-                for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next()) {
-                    int off = DenseOffset(it.lam);
-                    float Le = scale * (off < 0 ? 0.f : dense[off]);
-                    acc.Add(S, off, betaP[it.i * N] * Le * invDenom, it.i == 0);
-                }
-                Lr = S.imagingRatio * (acc.sx / kNSpectrumSamples);
-                Lg = S.imagingRatio * (acc.sy / kNSpectrumSamples);
-                Lb = S.imagingRatio * (acc.sz / kNSpectrumSamples);
+            // beta_i -> bfLds[i][lane] by LDS-DMA: all 31 loads in flight at once, no VGPRs,
+            // landing while the sampler below works from LDS (depth 0: beta = 1, no loads)
+            if (depth > 0) {
+                const int waveBase = threadIdx.x & ~63;
+#pragma unroll
+                for (int i = 0; i < kNSpectrumSamples; ++i)
+                    __builtin_amdgcn_global_load_lds(
+                        (const __attribute__((address_space(1))) void *)(betaP + (size_t)i * N),
+                        (__attribute__((address_space(3))) void *)(bfLds + i * kBlock + waveBase), 4, 0, 0);
             }
-            if (depth < S.maxDepth) {
-                // ---- GenerateRaySamples (samples.cpp:29-66): dimension = 6 + 7 * depth
-                int px, py, sampleIndex;
-                PixelOf(st, slot, &px, &py, &sampleIndex);
-                px += S.px0;
-                Halton h = StartPixelSample(S, px, py, sampleIndex, 6 + 7 * depth);
-                float dUc = Get1D(S, h);
-                float dU0, dU1;
-                Get2D(S, h, &dU0, &dU1);
-                (void)Get1D(S, h);  // indirect.uc (unused by DiffuseBxDF)
-                float iU0, iU1;
-                Get2D(S, h, &iU0, &iU1);
-                float rr = Get1D(S, h);
+            SEC_MARK(st, 0);
+            {
+                // ---- GenerateRaySamples (samples.cpp:29-66): dims 6 + 7 * depth + {0..6}
+                // = direct.uc, direct.u (2), indirect.uc, indirect.u (2), rr
+                const Halton h = StartPixelSample(S, px, py, sampleIndex, d0);
+                auto dim = [&](int k) -> float {
+                    const HaltonDimDesc hd = S.haltonDim[d0 + k];
+                    if ((h.index >> 32) == 0 && hd.fast)
+                        return ScrambledRadicalInverse32Magic(hd, (uint32_t)h.index, permL + permOff[k]);
+                    return ScrambledRadicalInverse(hd.base, hd.nDigits, h.index, S.perm + hd.permOffset);
+                };
+                const float dUc = dim(0), dU0 = dim(1), dU1 = dim(2);
+                const float iU0 = dim(4), iU1 = dim(5), rr = dim(6);  // dim 3: indirect.uc, unused
+                SEC_MARK(st, 1);
                 // ---- DiffuseMaterial::GetBxDF: R = clamp(reflectance(lambda), 0, 1); f = R / pi
                 // (bxdfs.h DiffuseBxDF::f).  bf_i = beta_i * f_i is formed once per wavelength
                 // into LDS; light sampling and the BSDF update both start from that product.
-                int mat = S.primMaterial[prim];
-                const float4 mc = S.matCoeffs[mat];
-                const bool constant = S.matConstant[mat];
                 bool Rnz = false;
                 float *bf = bfLds + threadIdx.x;
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the beta LDS-DMA has landed
 #pragma unroll 4
                 for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next()) {
                     float R = Reflectance(mc, constant, it.lam);
                     Rnz |= R != 0;
-                    bf[it.i * kBlock] = betaP[it.i * N] * (R * kInvPi);
+                    bf[it.i * kBlock] = (depth > 0 ? bf[it.i * kBlock] : 1.f) * (R * kInvPi);
                 }
+                SEC_MARK(st, 2);
                 Frame frame = Frame::FromXZ(Normalize(surf.dpdu), ns);
                 V3 woL = frame.ToLocal(wo);
                 V3 pi = surf.p, pe = surf.pErr;
@@ -687,33 +978,30 @@ __global__ void __launch_bounds__(kBlock) k_shade_diffuse(DeviceScene S, PathSta
                     V3 cp = OffsetRayOrigin(pi, pe, n, wo);  // reflective, not transmissive
                     int li;
                     float lpmf;
-                    if (SampleLight(S, cp, ns, dUc, &li, &lpmf) && li < S.nAreaLights) {
-                        int lprim = S.lightPrim[li];
-                        V3 q0, q1, q2;
-                        PrimVerts(S, lprim, &q0, &q1, &q2);
+                    if (SampleLight(SL, cp, ns, dUc, &li, &lpmf) && li < S.nAreaLights) {
+                        const DeviceAreaLight &Ld = lightsL[li];
+                        V3 q0(Ld.v0.x, Ld.v0.y, Ld.v0.z), q1(Ld.v1.x, Ld.v1.y, Ld.v1.z), q2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
                         V3 lp, lpe, ln;
                         float lpdf;
-                        if (SampleTriangle(q0, q1, q2, S.primFlip[lprim], cp, n, ns, dU0, dU1, &lp, &lpe, &ln, &lpdf) &&
+                        if (SampleTriangle(q0, q1, q2, Ld.flip, cp, n, ns, dU0, dU1, &lp, &lpe, &ln, &lpdf) &&
                             lpdf != 0 && LengthSquared(lp - cp) != 0) {
+                            SEC_MARK(st, 3);
                             V3 wi = Normalize(lp - cp);
                             V3 wiL = frame.ToLocal(wi);
-                            if ((S.lightTwoSided[li] || DotN(ln, -wi) >= 0) && woL.z != 0 && woL.z * wiL.z > 0) {
-                                const float *dense = S.dense + S.lightSpectrum[li] * kDenseN;
-                                float scale = S.lightScale[li];
+                            if ((Ld.twoSided || DotN(ln, -wi) >= 0) && woL.z != 0 && woL.z * wiL.z > 0) {
+                                const int spec = Ld.spectrum;
+                                float scale = Ld.scale;
                                 float absdot = AbsDotN(ns, wi);
                                 float lightPDF = lpdf * lpmf;
                                 float bsdfPDF = CosineHemispherePDF(fabsf(wiL.z));
                                 float denom = Avg31(bsdfPDF + lightPDF);
                                 const float invDenom = 1 / denom;
                                 SensorAcc acc;
-                                bool nz = false;
-#pragma unroll 4
-                                for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next()) {
-                                    int off = DenseOffset(it.lam);
-                                    float Le = scale * (off < 0 ? 0.f : dense[off]);
-                                    nz |= Le != 0;
-                                    acc.Add(S, off, bf[it.i * kBlock] * absdot * Le * invDenom, it.i == 0);
-                                }
+                                bool nz = lay.denseInLds
+                                              ? NeeAccumulate((const LdsF *)denseLds + spec * kDenseN, sensorL, bf,
+                                                              lambda0, scale, absdot, invDenom, &acc)
+                                              : NeeAccumulate(S.dense + spec * kDenseN, sensorL, bf, lambda0, scale,
+                                                              absdot, invDenom, &acc);
                                 if (nz) {
                                     // SpawnRayTo(pi, n, time, pLight.pi, pLight.n) (ray.h:106-111)
                                     V3 pf = OffsetRayOrigin(pi, pe, n, lp - pi);
@@ -734,6 +1022,7 @@ __global__ void __launch_bounds__(kBlock) k_shade_diffuse(DeviceScene S, PathSta
                         }
                     }
                 }
+                SEC_MARK(st, 4);
                 // ---- BSDF::Sample_f<DiffuseBxDF> + RR + indirect ray (surfscatter.cpp:170-250)
                 if (woL.z != 0 && Rnz) {
                     V3 wiL = SampleCosineHemisphere(iU0, iU1);
@@ -742,7 +1031,7 @@ __global__ void __launch_bounds__(kBlock) k_shade_diffuse(DeviceScene S, PathSta
                     if (pdf != 0 && wiL.z != 0) {
                         V3 wi = frame.FromLocal(wiL);
                         float absdot = AbsDotN(ns, wi);
-                        float etaScale = st.etaScale[slot];
+                        float etaScale = depth > 0 ? st.etaScale[slot] : 1.f;
                         float avgRu = Avg31(1.f);
                         float mx = -kInfinity;
 #pragma unroll 4
@@ -751,6 +1040,7 @@ __global__ void __launch_bounds__(kBlock) k_shade_diffuse(DeviceScene S, PathSta
                             bf[i * kBlock] = nbv;
                             mx = fmaxf(mx, nbv * etaScale / avgRu);
                         }
+                        SEC_MARK(st, 5);
                         bool kill = false;
                         float q = 0;
                         if (mx < 1 && depth >= 1) {
@@ -779,47 +1069,36 @@ __global__ void __launch_bounds__(kBlock) k_shade_diffuse(DeviceScene S, PathSta
                                 st.ray[5 * N + slot] = wi.z;
                                 st.rl[slot] = 1.f / pdf;
                                 st.flags[slot] = 2;  // specularBounce = false, anyNonSpecular = true
-                                st.ctx[slot] = pi.x;
-                                st.ctx[N + slot] = pi.y;
-                                st.ctx[2 * N + slot] = pi.z;
-                                st.ctx[3 * N + slot] = n.x;
-                                st.ctx[4 * N + slot] = n.y;
-                                st.ctx[5 * N + slot] = n.z;
-                                st.ctx[6 * N + slot] = ns.x;
-                                st.ctx[7 * N + slot] = ns.y;
-                                st.ctx[8 * N + slot] = ns.z;
-                                st.ctx[9 * N + slot] = pe.x;
-                                st.ctx[10 * N + slot] = pe.y;
-                                st.ctx[11 * N + slot] = pe.z;
                             }
                         }
                     }
                 }
             }
-            if (Lr != 0 || Lg != 0 || Lb != 0) {
-                st.L[slot] += Lr;
-                st.L[N + slot] += Lg;
-                st.L[2 * N + slot] += Lb;
-            }
         }
-        int pos = WavePush(nextCounter, pushRay);
-        if (pos >= 0) nextQ[pos] = slot;
-        int spos = WavePush(shadowCounter, pushShadow);
-        if (spos >= 0) st.shadowQ[spos] = slot;
+        SEC_MARK(st, 6);
+        int *const cnt[2] = {nextCounter, shadowCounter};
+        const bool pred[2] = {pushRay, pushShadow};
+        int pos[2];
+        BlockPush<2>(cnt, pred, pos);
+        if (pos[0] >= 0) nextQ[pos[0]] = slot;
+        if (pos[1] >= 0) st.shadowQ[pos[1]] = slot;
+        SEC_MARK(st, 7);
     }
 }
 
-__global__ void __launch_bounds__(kBlock) k_shadow(DeviceScene S, PathState st, int depth) {
-    extern __shared__ int stackLds[];
+__global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_shadow(DeviceScene S, PathState st, int depth) {
+    if ((int)(blockIdx.x * blockDim.x) >= st.counters[depth * kCounterStride + kCntShadow]) return;  // no work
+    extern __shared__ float4 dynLds[];
+    const SceneLds L = SetupSceneLds(S, dynLds);
     int N = st.N;
-    const int count = st.counters[depth * 4 + 2];
+    const int count = st.counters[depth * kCounterStride + kCntShadow];
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&st.stats[2], (unsigned long long)count);
     for (int qi = blockIdx.x * blockDim.x + threadIdx.x; qi < count; qi += gridDim.x * blockDim.x) {
         int slot = st.shadowQ[qi];
         V3 o(st.shadowRay[slot], st.shadowRay[N + slot], st.shadowRay[2 * N + slot]);
         V3 d(st.shadowRay[3 * N + slot], st.shadowRay[4 * N + slot], st.shadowRay[5 * N + slot]);
         TriHit h;
-        int hit = Traverse<true>(S, o, d, 1 - kShadowEpsilon, &h, stackLds);
+        int hit = Traverse<true>(S, L, o, d, 1 - kShadowEpsilon, &h);
         if (hit < 0) {
             st.L[slot] += st.shadowL[slot];
             st.L[N + slot] += st.shadowL[N + slot];
@@ -840,7 +1119,7 @@ __global__ void __launch_bounds__(kBlock) k_film(DeviceScene S, PathState st, in
     double sr = st.film[pix], sg = st.film[npix + pix], sb = st.film[2 * npix + pix], sw = st.film[3 * npix + pix];
     for (int s = 0; s < nSamples; ++s) {
         int slot = s * st.P + pl;
-        float w = st.filterW[slot];
+        float w = S.boxFilter ? 1.f : st.filterW[slot];
         float rr = st.L[slot], gg = st.L[N + slot], bb = st.L[2 * N + slot];
         sr += w * rr;
         sg += w * gg;
@@ -856,15 +1135,16 @@ __global__ void __launch_bounds__(kBlock) k_film(DeviceScene S, PathState st, in
 // ------------------------------------------------------------------ stand-alone intersection
 // The WavefrontAggregate boundary exposed on its own (integrator.h:32-54): closest / any hit
 // for an SoA ray batch, used by parity tests and the traversal benchmark.
-__global__ void __launch_bounds__(kBlock) k_intersect_batch(DeviceScene S, const float *rays, int n, int anyHit,
+__global__ void __launch_bounds__(kBlock, 4) k_intersect_batch(DeviceScene S, const float *rays, int n, int anyHit,
                                                               int *outPrim, float *outHit) {
-    extern __shared__ int stackLds[];
+    extern __shared__ float4 dynLds[];
+    const SceneLds L = SetupSceneLds(S, dynLds);
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         V3 o(rays[i], rays[n + i], rays[2 * n + i]);
         V3 d(rays[3 * n + i], rays[4 * n + i], rays[5 * n + i]);
         float tMax = rays[6 * n + i];
         TriHit h{0, 0, 0, 0};
-        int prim = anyHit ? Traverse<true>(S, o, d, tMax, &h, stackLds) : Traverse<false>(S, o, d, tMax, &h, stackLds);
+        int prim = anyHit ? Traverse<true>(S, L, o, d, tMax, &h) : Traverse<false>(S, L, o, d, tMax, &h);
         outPrim[i] = prim;
         outHit[i] = h.b0;
         outHit[n + i] = h.b1;
@@ -874,7 +1154,34 @@ __global__ void __launch_bounds__(kBlock) k_intersect_batch(DeviceScene S, const
 }
 
 // ------------------------------------------------------------------ launch helpers (host)
-static size_t StackBytes(const DeviceScene &S) { return (size_t)(S.stackSize > 0 ? S.stackSize : 1) * kBlock * sizeof(int); }
+size_t TraversalLdsBytes(int stackSize, int ldsNodes, int ldsTris) {
+    return (size_t)stackSize * kBlock * sizeof(int) + (size_t)ldsNodes * kLdsNodeStride * 16 + (size_t)ldsTris * 48;
+}
+static size_t StackBytes(const DeviceScene &S) { return TraversalLdsBytes(S.stackSize, S.ldsNodes, S.ldsTris); }
+
+// Traversal kernels loop over their queue inside a bounded grid so the LDS scene cache is
+// filled once per block, not once per 256 rays.
+#ifndef PBRT_GRID_CAP
+#define PBRT_GRID_CAP 1024
+#endif
+#ifndef PBRT_SHADE_GRID_CAP
+#define PBRT_SHADE_GRID_CAP 2048
+#endif
+static int TraversalGridFor(int n) {
+    int g = (n + kBlock - 1) / kBlock;
+    return g < 1 ? 1 : (g > PBRT_GRID_CAP ? PBRT_GRID_CAP : g);
+}
+static int ShadeGridFor(int n) {
+    int g = (n + kBlock - 1) / kBlock;
+    return g < 1 ? 1 : (g > PBRT_SHADE_GRID_CAP ? PBRT_SHADE_GRID_CAP : g);
+}
+
+// Kernels over queues that are usually short (emissive hits, escaped rays): a grid of one
+// block per CU, grid-stride beyond that.
+static int SmallGridFor(int n) {
+    int g = (n + kBlock - 1) / kBlock;
+    return g < 1 ? 1 : (g > 256 ? 256 : g);
+}
 
 static int GridFor(int n) {
     int g = (n + kBlock - 1) / kBlock;
@@ -885,20 +1192,27 @@ hipError_t LaunchCamera(const DeviceScene &S, const PathState &st, int nActive, 
     hipLaunchKernelGGL(k_camera, dim3((nActive + kBlock - 1) / kBlock), dim3(kBlock), 0, s, S, st, nActive);
     return hipGetLastError();
 }
-hipError_t LaunchClosest(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s) {
-    hipLaunchKernelGGL(k_closest, dim3(GridFor(maxCount)), dim3(kBlock), StackBytes(S), s, S, st, depth);
+hipError_t LaunchClosest(const DeviceScene &S, const PathState &st, int depth, int maxCount, int timed,
+                         hipStream_t s) {
+    hipLaunchKernelGGL(k_closest, dim3(TraversalGridFor(maxCount)), dim3(kBlock), StackBytes(S), s, S, st, depth,
+                       timed);
     return hipGetLastError();
 }
 hipError_t LaunchEscaped(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s) {
-    hipLaunchKernelGGL(k_escaped, dim3(GridFor(maxCount)), dim3(kBlock), 0, s, S, st, depth);
+    hipLaunchKernelGGL(k_escaped, dim3(SmallGridFor(maxCount)), dim3(kBlock), 0, s, S, st, depth);
+    return hipGetLastError();
+}
+hipError_t LaunchEmissive(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s) {
+    hipLaunchKernelGGL(k_emissive, dim3(SmallGridFor(maxCount)), dim3(kBlock), 0, s, S, st, depth);
     return hipGetLastError();
 }
 hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s) {
-    hipLaunchKernelGGL(k_shade_diffuse, dim3(GridFor(maxCount)), dim3(kBlock), 0, s, S, st, depth);
+    hipLaunchKernelGGL(k_shade_diffuse, dim3(ShadeGridFor(maxCount)), dim3(kBlock), (size_t)S.shadeLds.total, s,
+                       S, st, depth);
     return hipGetLastError();
 }
 hipError_t LaunchShadow(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s) {
-    hipLaunchKernelGGL(k_shadow, dim3(GridFor(maxCount)), dim3(kBlock), StackBytes(S), s, S, st, depth);
+    hipLaunchKernelGGL(k_shadow, dim3(TraversalGridFor(maxCount)), dim3(kBlock), StackBytes(S), s, S, st, depth);
     return hipGetLastError();
 }
 hipError_t LaunchFilm(const DeviceScene &S, const PathState &st, int nSamples, hipStream_t s) {
@@ -907,7 +1221,7 @@ hipError_t LaunchFilm(const DeviceScene &S, const PathState &st, int nSamples, h
 }
 hipError_t LaunchIntersectBatch(const DeviceScene &S, const float *rays, int n, int anyHit, int *outPrim,
                                 float *outHit, hipStream_t s) {
-    hipLaunchKernelGGL(k_intersect_batch, dim3(GridFor(n)), dim3(kBlock), StackBytes(S), s, S, rays, n, anyHit, outPrim, outHit);
+    hipLaunchKernelGGL(k_intersect_batch, dim3(TraversalGridFor(n)), dim3(kBlock), StackBytes(S), s, S, rays, n, anyHit, outPrim, outHit);
     return hipGetLastError();
 }
 

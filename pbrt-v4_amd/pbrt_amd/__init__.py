@@ -25,7 +25,8 @@ import numpy as np
 
 PKG_DIR = Path(__file__).resolve().parent
 ROOT = PKG_DIR.parent
-LIB_PATH = ROOT / "lib" / "libpbrt_amd.so"
+# PBRT_AMD_LIB selects a profiling build (lib/libpbrt_amd_prof.so, tools only)
+LIB_PATH = Path(os.environ.get("PBRT_AMD_LIB", ROOT / "lib" / "libpbrt_amd.so"))
 DATA_DIR = ROOT / "data"
 
 
@@ -72,7 +73,8 @@ class RenderParams(ctypes.Structure):
 class RenderStats(ctypes.Structure):
     _fields_ = [("camera_rays", ctypes.c_uint64), ("closest_rays", ctypes.c_uint64),
                 ("shadow_rays", ctypes.c_uint64), ("closest_launches", ctypes.c_int),
-                ("closest_ms", ctypes.c_double), ("passes", ctypes.c_int), ("paths_per_pass", ctypes.c_uint64)]
+                ("closest_ms", ctypes.c_double), ("timed_closest_rays", ctypes.c_uint64), ("passes", ctypes.c_int),
+                ("paths_per_pass", ctypes.c_uint64)]
 
 
 # Symbols declared in include/pbrt_amd.h (tests check every one is exported)
@@ -81,7 +83,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_scene_get_info", "pbrt_scene_get_flat", "pbrt_device_count", "pbrt_context_create",
     "pbrt_context_free", "pbrt_render", "pbrt_synchronize", "pbrt_get_stats", "pbrt_reset_stats",
     "pbrt_film_clear", "pbrt_film_device_ptr", "pbrt_film_read", "pbrt_film_get_rgb", "pbrt_intersect",
-    "pbrt_debug_halton", "pbrt_debug_rgb_coeffs", "pbrt_debug_rgb2spec_column",
+    "pbrt_debug_halton", "pbrt_debug_rgb_coeffs", "pbrt_debug_rgb2spec_column", "pbrt_debug_kernel_sections",
 ]
 
 _LIB = None
@@ -119,6 +121,7 @@ def _lib():
     lib.pbrt_debug_halton.restype = c.c_float
     lib.pbrt_debug_rgb_coeffs.argtypes = [c.c_float, c.c_float, c.c_float, c.POINTER(c.c_float)]
     lib.pbrt_debug_rgb2spec_column.argtypes = [c.c_int, c.c_int, c.c_int, c.POINTER(c.c_float)]
+    lib.pbrt_debug_kernel_sections.argtypes = [c.c_void_p, c.POINTER(c.c_uint64), c.c_int]
     lib.pbrt_set_data_dir(str(DATA_DIR).encode())
     _LIB = lib
     return lib
@@ -222,6 +225,12 @@ class WavefrontPathIntegrator:
 
     def reset_stats(self):
         _check(_lib().pbrt_reset_stats(self._h))
+
+    def kernel_sections(self, n=32):
+        """Summed wave cycles per instrumented kernel section (profiling build only)."""
+        out = (ctypes.c_uint64 * n)()
+        _check(_lib().pbrt_debug_kernel_sections(self._h, out, n))
+        return list(out)
 
     def film_clear(self):
         _check(_lib().pbrt_film_clear(self._h))

@@ -130,6 +130,9 @@ int pbrt_intersect(pbrt_context *ctx, const float *rays_dev, int n, int any_hit,
 float pbrt_debug_halton(const pbrt_scene *scene, int px, int py, int sample_index, int dim);
 int pbrt_debug_rgb_coeffs(float r, float g, float b, float *coeffs3);
 int pbrt_debug_rgb2spec_column(int maxc, int j, int i, float *out192);
+/* queue counters of the last pass: [depth][8] = rays, material hits, shadow rays, escaped,
+ * emissive hits (diagnostics) */
+int pbrt_debug_queue_counts(pbrt_context *ctx, int32_t *counts, int n);
 /* profiling build only (PBRT_AMD_SECTION_TIMING): summed wave cycles per kernel section
  * since the last pbrt_reset_stats; zeros in the product build */
 int pbrt_debug_kernel_sections(pbrt_context *ctx, uint64_t *cycles, int n);

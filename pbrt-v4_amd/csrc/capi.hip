@@ -409,10 +409,10 @@ static void BuildDevice(pbrt_context *c) {
 
 static void AllocPaths(pbrt_context *c, int64_t N) {
     if (N <= c->maxPaths) return;
-    // float arrays: beta 31, rl 1, L 3, lambda0 1, filterW 1, etaScale 1, ray 6, hitB 2x4,
-    // shadowRay 6, shadowL 3 = 61 floats; int arrays: flags, hitPrim x2, rayQ x2, matQ,
-    // shadowQ, escQ, emitQ = 9
-    const int nf = 61, ni = 9;
+    // floats: records 2 x (beta 31, ray 6, lambda0, rl, etaScale) = 80, hitB 2x4, shadowRay 6,
+    // shadowL 3, L 3, filterW 1 = 101; ints: records 2 x (flags, pixel, prevIdx), hitPrim 2,
+    // shadowPixel, matQ, escQ, emitQ = 12
+    const int nf = 101, ni = 12;
     c->fState.Alloc((size_t)nf * N);
     c->iState.Alloc((size_t)ni * N + kCounterStride * (c->desc.maxDepth + 3));
     c->maxPaths = N;
@@ -423,30 +423,31 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
         f += (size_t)k * N;
         return r;
     };
-    st.beta = take(31);
-    st.rl = take(1);
-    st.L = take(3);
-    st.lambda0 = take(1);
-    st.filterW = take(1);
-    st.etaScale = take(1);
-    st.ray = take(6);
-    st.hitB[0] = take(4);
-    st.hitB[1] = take(4);
-    st.shadowRay = take(6);
-    st.shadowL = take(3);
     int *ip = c->iState.p;
     auto takei = [&](int k) {
         int *r = ip;
         ip += (size_t)k * N;
         return r;
     };
-    st.flags = takei(1);
-    st.hitPrim[0] = takei(1);
-    st.hitPrim[1] = takei(1);
-    st.rayQ[0] = takei(1);
-    st.rayQ[1] = takei(1);
+    for (int b = 0; b < 2; ++b) {
+        PathRecords &r = st.rec[b];
+        r.beta = take(31);
+        r.ray = take(6);
+        r.lambda0 = take(1);
+        r.rl = take(1);
+        r.etaScale = take(1);
+        r.flags = takei(1);
+        r.pixel = takei(1);
+        r.prevIdx = takei(1);
+        st.hitB[b] = take(4);
+        st.hitPrim[b] = takei(1);
+    }
+    st.shadowRay = take(6);
+    st.shadowL = take(3);
+    st.L = take(3);
+    st.filterW = take(1);
+    st.shadowPixel = takei(1);
     st.matQ = takei(1);
-    st.shadowQ = takei(1);
     st.escQ = takei(1);
     st.emitQ = takei(1);
     st.counters = ip;
@@ -834,6 +835,19 @@ int pbrt_debug_rgb2spec_column(int maxc, int j, int i, float *out) {
     try {
         auto v = RGB2SpecColumn(maxc, j, i);
         std::copy(v.begin(), v.end(), out);
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_debug_queue_counts(pbrt_context *ctx, int32_t *counts, int n) {
+    try {
+        if (!ctx || !counts || n <= 0) return Fail("null argument");
+        HIPCHECK(hipSetDevice(ctx->device));
+        HIPCHECK(hipStreamSynchronize(ctx->stream));
+        n = std::min(n, kCounterStride * (ctx->desc.maxDepth + 3));
+        HIPCHECK(hipMemcpy(counts, ctx->st.counters, n * sizeof(int32_t), hipMemcpyDeviceToHost));
         return 0;
     } catch (const std::exception &e) {
         return Fail(e.what());

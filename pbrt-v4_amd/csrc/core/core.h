@@ -12,8 +12,14 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define PHD __host__ __device__ inline
+// Large, cold-ish helpers stay out of line in the kernels: the shade kernel's inlined code
+// outgrew the instruction cache, and a call is cheaper than streaming instructions from L2.
+#define PHD_NOINLINE __host__ __device__ inline __attribute__((noinline))
+#define PHD_UNROLL _Pragma("unroll")
 #else
 #define PHD inline
+#define PHD_NOINLINE inline
+#define PHD_UNROLL
 #endif
 
 namespace pbrt_amd {
@@ -222,18 +228,23 @@ PHD int SampleDiscrete2(float w0, float w1, float u, float *pmf, float *uRemappe
     return offset;
 }
 
-// util/sampling.cpp:28 SampleSphericalTriangle (returns false when the reference returns {})
-PHD bool SampleSphericalTriangle(V3 v0, V3 v1, V3 v2, V3 p, float u0, float u1, float b[3],
-                                 float *pdf) {
-    *pdf = 0;
+// util/sampling.cpp:28 SampleSphericalTriangle (ok = false when the reference returns {});
+// results by value so the out-of-line call needs no stack.
+struct SphTriSample {
+    float b0, b1, b2, pdf;
+    bool ok;
+};
+PHD_NOINLINE SphTriSample SampleSphericalTriangle(V3 v0, V3 v1, V3 v2, V3 p, float u0, float u1) {
+    SphTriSample r{0, 0, 0, 0, false};
+    float b[3];
+    float *pdf = &r.pdf;
     V3 a = v0 - p, bb = v1 - p, c = v2 - p;
     a = Normalize(a);
     bb = Normalize(bb);
     c = Normalize(c);
     V3 n_ab = Cross(a, bb), n_bc = Cross(bb, c), n_ca = Cross(c, a);
     if (LengthSquared(n_ab) == 0 || LengthSquared(n_bc) == 0 || LengthSquared(n_ca) == 0) {
-        b[0] = b[1] = b[2] = 0;
-        return false;
+        return r;
     }
     n_ab = Normalize(n_ab);
     n_bc = Normalize(n_bc);
@@ -264,8 +275,9 @@ PHD bool SampleSphericalTriangle(V3 v0, V3 v1, V3 v2, V3 p, float u0, float u1, 
     V3 s1 = Cross(w, e2);
     float divisor = Dot(s1, e1);
     if (divisor == 0) {
-        b[0] = b[1] = b[2] = 1.f / 3.f;
-        return true;
+        r.b0 = r.b1 = r.b2 = 1.f / 3.f;
+        r.ok = true;
+        return r;
     }
     float invDivisor = 1 / divisor;
     V3 s = p - v0;
@@ -277,23 +289,28 @@ PHD bool SampleSphericalTriangle(V3 v0, V3 v1, V3 v2, V3 p, float u0, float u1, 
         b1 /= b1 + b2;
         b2 /= b1 + b2;  // sic: the reference divides by the updated sum
     }
-    b[0] = 1 - b1 - b2;
-    b[1] = b1;
-    b[2] = b2;
-    return true;
+    r.b0 = 1 - b1 - b2;
+    r.b1 = b1;
+    r.b2 = b2;
+    r.ok = true;
+    (void)b;
+    return r;
 }
 
 // util/sampling.cpp:110 InvertSphericalTriangleSample
-PHD void InvertSphericalTriangleSample(V3 v0, V3 v1, V3 v2, V3 p, V3 w, float *u0out, float *u1out) {
+struct SphTriUV {
+    float u0, u1;
+};
+PHD_NOINLINE SphTriUV InvertSphericalTriangleSample(V3 v0, V3 v1, V3 v2, V3 p, V3 w) {
+    SphTriUV r{0, 0};
+    float *u0out = &r.u0, *u1out = &r.u1;
     V3 a = v0 - p, b = v1 - p, c = v2 - p;
     a = Normalize(a);
     b = Normalize(b);
     c = Normalize(c);
     V3 n_ab = Cross(a, b), n_bc = Cross(b, c), n_ca = Cross(c, a);
     if (LengthSquared(n_ab) == 0 || LengthSquared(n_bc) == 0 || LengthSquared(n_ca) == 0) {
-        *u0out = 0;
-        *u1out = 0;
-        return;
+        return r;
     }
     n_ab = Normalize(n_ab);
     n_bc = Normalize(n_bc);
@@ -311,7 +328,7 @@ PHD void InvertSphericalTriangleSample(V3 v0, V3 v1, V3 v2, V3 p, V3 w, float *u
         if (LengthSquared(n_cpb) == 0 || LengthSquared(n_acp) == 0) {
             *u0out = 0.5f;
             *u1out = 0.5f;
-            return;
+            return r;
         }
         n_cpb = Normalize(n_cpb);
         n_acp = Normalize(n_acp);
@@ -322,6 +339,7 @@ PHD void InvertSphericalTriangleSample(V3 v0, V3 v1, V3 v2, V3 p, V3 w, float *u
     float u1 = (1 - Dot(w, b)) / (1 - Dot(cp, b));
     *u0out = Clampf(u0, 0, 1);
     *u1out = Clampf(u1, 0, 1);
+    return r;
 }
 
 // ---------------------------------------------------------------- rays and triangles
@@ -524,7 +542,7 @@ PHD float Avg31(float x) {
 // ---------------------------------------------------------------- Halton
 // util/lowdiscrepancy.h ScrambledRadicalInverse with digit permutations, index < 2^32.
 // perm points at the permutation rows for this prime: perm[digit * base + value].
-PHD float ScrambledRadicalInverse(uint32_t base, uint32_t nDigits, uint64_t a, const uint16_t *perm) {
+PHD_NOINLINE float ScrambledRadicalInverse(uint32_t base, uint32_t nDigits, uint64_t a, const uint16_t *perm) {
     float invBase = (float)1 / (float)base, invBaseM = 1;
     uint64_t reversedDigits = 0;
     for (uint32_t digitIndex = 0; digitIndex < nDigits; ++digitIndex) {
@@ -587,7 +605,7 @@ template <typename PermPtr>
 PHD float ScrambledRadicalInverse32Magic(const HaltonDimDesc &d, uint32_t a, PermPtr perm) {
     const uint32_t base = d.base;
     uint32_t pv[kMaxMagicDigits];
-#pragma unroll
+PHD_UNROLL
     for (int k = 0; k < kMaxMagicDigits; ++k) {
         uint32_t t = (uint32_t)(((uint64_t)d.magic * a) >> 32);
         uint32_t next = (t + ((a - t) >> 1)) >> d.shift;
@@ -599,7 +617,7 @@ PHD float ScrambledRadicalInverse32Magic(const HaltonDimDesc &d, uint32_t a, Per
     }
     float invBaseM = 1;
     uint32_t reversedDigits = 0;
-#pragma unroll
+PHD_UNROLL
     for (int k = 0; k < kMaxMagicDigits; ++k) {
         if ((uint32_t)k < d.nDigits) {
             reversedDigits = reversedDigits * base + pv[k];
@@ -663,7 +681,7 @@ PHD float SinSubClamped(float sinA, float cosA, float sinB, float cosB) {
     if (cosA > cosB) return 0;
     return sinA * cosB - cosA * sinB;
 }
-PHD float LightImportance(const LightNodeBounds &lb, V3 p, V3 n) {
+PHD_NOINLINE float LightImportance(LightNodeBounds lb, V3 p, V3 n) {
     V3 pc = (lb.pMin + lb.pMax) / 2;
     float d2 = DistanceSquared(p, pc);
     d2 = std::fmax(d2, Length(lb.pMax - lb.pMin) / 2);

@@ -110,6 +110,21 @@ struct DeviceScene {
     ShadeLdsLayout shadeLds;
 };
 
+// One depth's path records, compacted: record i is the i-th ray of that depth (pbrt's
+// RayWorkItem, workitems.h, in SoA).  Each shade pass writes the surviving paths densely into
+// the other parity's records, so every later depth reads contiguous memory instead of the
+// thinning-out slots of the original pixel samples.
+struct PathRecords {
+    float *beta;      // [31][N] wavelength-major
+    float *ray;       // [6][N] o, d
+    float *lambda0;   // [N] first wavelength (the other 30 follow by pbrt's +10 nm rule)
+    float *rl;        // [N] r_l (spectrally constant for surface-only paths); depth > 0
+    float *etaScale;  // [N]
+    int *flags;       // [N] bit0 specularBounce, bit1 anyNonSpecular
+    int *pixel;       // [N] pixel-sample slot (index of L / film sample); depth > 0
+    int *prevIdx;     // [N] record index at the previous depth (its hit = the MIS context)
+};
+
 // Per-pass wavefront buffers; N = paths per pass = P pixels x S samples.
 struct PathState {
     int N;
@@ -117,28 +132,25 @@ struct PathState {
     int width;          // pixel row width (px1 - px0)
     const int *rows;    // P / width row indices (absolute y)
     int firstSample;    // sample index of slot block 0
-    float *beta;        // [31][N]
-    float *rl;          // [N]
-    float *L;           // [3][N] sensor RGB
-    float *lambda0;     // [N]
-    float *filterW;     // [N]
-    float *etaScale;    // [N]
-    int *flags;         // [N]: bit0 specularBounce, bit1 anyNonSpecular
-    float *ray;         // [6][N]
-    // Hit records double-buffered by depth parity: the previous bounce's record is the MIS
-    // context of an emissive hit (pbrt's prevIntrCtx), recomputed rather than stored.
+    PathRecords rec[2]; // by depth parity
+    // hit records of each depth's rays (by record index), double-buffered by depth parity:
+    // the previous depth's hit is the emissive-hit MIS context (pbrt's prevIntrCtx)
     int *hitPrim[2];    // [N] each
     float *hitB[2];     // [4][N] each: b0, b1, b2, t
+    // shadow-ray queue, compacted (pbrt's ShadowRayWorkItem)
     float *shadowRay;   // [6][N]
-    float *shadowL;     // [3][N]
-    int *rayQ[2];       // [N]
-    int *matQ;          // [N]
-    int *shadowQ;       // [N]
+    float *shadowL;     // [3][N] sensor RGB to add when unoccluded
+    int *shadowPixel;   // [N]
+    // per pixel-sample slot
+    float *L;           // [3][N] sensor RGB
+    float *filterW;     // [N]
+    // work queues: record indices of the current depth
+    int *matQ;          // [N] material (diffuse) hits
     int *escQ;          // [N] escaped rays (only with infinite lights)
     int *emitQ;         // [N] hits on emissive triangles
     int *counters;      // [(maxDepth+2) * kCounterStride]: see kCnt*
     double *film;       // [4][xres*yres]: rgbSum[3], weightSum (sensor RGB)
-    unsigned long long *stats;  // [8]: camera rays, closest rays, shadow rays, node visits
+    unsigned long long *stats;  // [kStatsSlots]
 };
 
 }  // namespace pbrt_amd

@@ -109,6 +109,55 @@ __device__ inline void DmaCopy(const void *src, void *ldsDst, int n) {
 }
 __device__ inline void DmaWait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// Block-local staging of queue appends: entries collect in an LDS buffer across the block's
+// grid-stride iterations (one LDS atomic per wave) and are written out in contiguous runs with
+// one global atomicAdd per flush, i.e. every ~cap/256 iterations instead of every iteration.
+// All threads of the block must call Append/FlushAll (the grid-stride loops are block-uniform).
+template <int K, int Cap>
+struct BlockQueues {
+    int *buf;   // LDS [K][Cap]
+    int *fill;  // LDS [K]
+    int *gbase; // LDS [K]
+    int *const *counters;
+    int *const *queues;
+
+    __device__ void Init() {
+        if (threadIdx.x < K) fill[threadIdx.x] = 0;
+        __syncthreads();
+    }
+    __device__ void Flush(int k) {
+        const int n = fill[k];
+        if (threadIdx.x == 0) gbase[k] = n ? atomicAdd(counters[k], n) : 0;
+        __syncthreads();
+        const int b = gbase[k];
+        int *q = queues[k];
+        for (int i = threadIdx.x; i < n; i += blockDim.x) q[b + i] = buf[k * Cap + i];
+        __syncthreads();
+        if (threadIdx.x == 0) fill[k] = 0;
+        __syncthreads();
+    }
+    __device__ void Append(const bool (&pred)[K], int slot) {
+        const int lane = __lane_id();
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const unsigned long long mask = __ballot(pred[k]);
+            const int n = __popcll(mask);
+            int b = 0;
+            if (lane == 0 && n) b = atomicAdd(&fill[k], n);  // LDS atomic
+            b = __shfl(b, 0);
+            if (pred[k]) buf[k * Cap + b + __popcll(mask & ((1ull << lane) - 1ull))] = slot;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (fill[k] > Cap - kBlock) Flush(k);  // block-uniform: read after the barrier
+    }
+    __device__ void FlushAll() {
+#pragma unroll
+        for (int k = 0; k < K; ++k) Flush(k);
+    }
+};
+
 __device__ inline V3 XfPoint(const float *m, V3 p) {
     float xp = m[0] * p.x + m[1] * p.y + m[2] * p.z + m[3];
     float yp = m[4] * p.x + m[5] * p.y + m[6] * p.z + m[7];
@@ -454,7 +503,13 @@ __device__ inline bool SampleTriangle(V3 p0, V3 p1, V3 p2, bool flip, V3 refP, V
     }
     float triPDF;
     float b[3];
-    SampleSphericalTriangle(p0, p1, p2, refP, u0, u1, b, &triPDF);
+    {
+        const SphTriSample r = SampleSphericalTriangle(p0, p1, p2, refP, u0, u1);
+        b[0] = r.b0;
+        b[1] = r.b1;
+        b[2] = r.b2;
+        triPDF = r.pdf;
+    }
     if (triPDF == 0) return false;
     pdf *= triPDF;
     V3 pAbsSum = Abs(b[0] * p0) + Abs(b[1] * p1) + Abs((1 - b[0] - b[1]) * p2);
@@ -485,7 +540,9 @@ __device__ inline float TrianglePDF(V3 p0, V3 p1, V3 p2, bool flip, V3 refP, V3 
     float pdf = 1 / solidAngle;
     if (refNs != V3(0, 0, 0)) {
         float u0, u1;
-        InvertSphericalTriangleSample(p0, p1, p2, refP, wi, &u0, &u1);
+        const SphTriUV uv = InvertSphericalTriangleSample(p0, p1, p2, refP, wi);
+        u0 = uv.u0;
+        u1 = uv.u1;
         V3 wi0 = Normalize(p0 - refP), wi1 = Normalize(p1 - refP), wi2 = Normalize(p2 - refP);
         float w[4] = {fmaxf(0.01f, AbsDotN(refNs, wi1)), fmaxf(0.01f, AbsDotN(refNs, wi1)),
                       fmaxf(0.01f, AbsDotN(refNs, wi0)), fmaxf(0.01f, AbsDotN(refNs, wi2))};
@@ -614,22 +671,22 @@ __global__ void __launch_bounds__(kBlock) k_camera(DeviceScene S, PathState st, 
         o = oo;
         d = dd;
     }
-    // beta = 1 and r_u = r_l = 1 at depth 0 are implicit (the depth-0 kernels use the constants
-    // and never read them), and the box filter's weight is always 1: none is stored.
+    // Depth-0 record = the pixel-sample slot.  beta = 1, r_u = r_l = 1, etaScale = 1, flags = 0,
+    // pixel = slot are implicit at depth 0 (the depth-0 kernels use the constants) and the box
+    // filter's weight is always 1: none of them is stored.
     int N = st.N;
     st.L[slot] = 0;
     st.L[N + slot] = 0;
     st.L[2 * N + slot] = 0;
-    st.lambda0[slot] = lambda0;
     if (!S.boxFilter) st.filterW[slot] = 1.f;
-    st.etaScale[slot] = 1.f;
-    st.flags[slot] = 0;
-    st.ray[slot] = o.x;
-    st.ray[N + slot] = o.y;
-    st.ray[2 * N + slot] = o.z;
-    st.ray[3 * N + slot] = d.x;
-    st.ray[4 * N + slot] = d.y;
-    st.ray[5 * N + slot] = d.z;  // the depth-0 ray queue is the identity (k_closest)
+    const PathRecords &r = st.rec[0];
+    r.lambda0[slot] = lambda0;
+    r.ray[slot] = o.x;
+    r.ray[N + slot] = o.y;
+    r.ray[2 * N + slot] = o.z;
+    r.ray[3 * N + slot] = d.x;
+    r.ray[4 * N + slot] = d.y;
+    r.ray[5 * N + slot] = d.z;
 }
 
 __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_closest(DeviceScene S, PathState st, int depth, int timed) {
@@ -637,7 +694,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_closest(Device
     extern __shared__ float4 dynLds[];
     const SceneLds L = SetupSceneLds(S, dynLds);
     int N = st.N;
-    const int *q = st.rayQ[depth & 1];
+    const PathRecords &rec = st.rec[depth & 1];
     const int count = st.counters[depth * kCounterStride + kCntRay];
     int *matCounter = &st.counters[depth * kCounterStride + kCntMat];
     int *escCounter = &st.counters[depth * kCounterStride + kCntEscaped];
@@ -645,42 +702,42 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_closest(Device
     int *hitPrim = st.hitPrim[depth & 1];
     float *hitB = st.hitB[depth & 1];
     const bool shade = depth < S.maxDepth;  // at maxDepth only emission and escape matter
+    constexpr int kCap = 2048;
+    __shared__ int qBuf[3 * kCap], qFill[3], qBase[3];
+    int *const qCnt[3] = {escCounter, emitCounter, matCounter};
+    int *const qArr[3] = {st.escQ, st.emitQ, st.matQ};
+    BlockQueues<3, kCap> queues{qBuf, qFill, qBase, qCnt, qArr};
+    queues.Init();
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         atomicAdd(&st.stats[1], (unsigned long long)count);
         if (timed) atomicAdd(&st.stats[3], (unsigned long long)count);  // rays of event-timed launches
     }
     for (int base = blockIdx.x * blockDim.x; base < count; base += gridDim.x * blockDim.x) {
-        int qi = base + threadIdx.x;
+        const int qi = base + threadIdx.x;  // record index of this depth
         bool active = qi < count;
-        int slot = active ? (depth == 0 ? qi : q[qi]) : 0;
         int prim = -1;
         TriHit h;
-        V3 o, d;
         if (active) {
-            o = V3(st.ray[slot], st.ray[N + slot], st.ray[2 * N + slot]);
-            d = V3(st.ray[3 * N + slot], st.ray[4 * N + slot], st.ray[5 * N + slot]);
+            const V3 o(rec.ray[qi], rec.ray[N + qi], rec.ray[2 * N + qi]);
+            const V3 d(rec.ray[3 * N + qi], rec.ray[4 * N + qi], rec.ray[5 * N + qi]);
             prim = Traverse<false>(S, L, o, d, kInfinity, &h);
             if (prim >= 0) {
-                hitPrim[slot] = prim;
-                hitB[slot] = h.b0;
-                hitB[N + slot] = h.b1;
-                hitB[2 * N + slot] = h.b2;
-                hitB[3 * N + slot] = h.t;
+                hitPrim[qi] = prim;
+                hitB[qi] = h.b0;
+                hitB[N + qi] = h.b1;
+                hitB[2 * N + qi] = h.b2;
+                hitB[3 * N + qi] = h.t;
             }
         }
         // EnqueueWorkAfterIntersection / Miss (intersect.h:48-156): misses to the escaped-ray
         // queue (infinite lights only), emissive hits to the hit-area-light queue, every hit
         // to its material queue
-        int *const cnt[3] = {escCounter, emitCounter, matCounter};
         const bool pred[3] = {S.nInfinite > 0 && active && prim < 0,
                               S.nAreaLights > 0 && active && prim >= 0 && S.primLight[prim] >= 0,
                               shade && active && prim >= 0};
-        int pos[3];
-        BlockPush<3>(cnt, pred, pos);
-        if (pos[0] >= 0) st.escQ[pos[0]] = slot;
-        if (pos[1] >= 0) st.emitQ[pos[1]] = slot;
-        if (pos[2] >= 0) st.matQ[pos[2]] = slot;
+        queues.Append(pred, qi);
     }
+    queues.FlushAll();
 }
 
 // HandleEscapedRays (integrator.cpp:495-537) for UniformInfiniteLight: Le with MIS where
@@ -689,9 +746,11 @@ __global__ void __launch_bounds__(kBlock) k_escaped(DeviceScene S, PathState st,
     int N = st.N;
     const int count = st.counters[depth * kCounterStride + kCntEscaped];
     for (int qi = blockIdx.x * blockDim.x + threadIdx.x; qi < count; qi += gridDim.x * blockDim.x) {
-        int slot = st.escQ[qi];
-        int fl = st.flags[slot];
-        float rl = st.rl[slot];
+        const PathRecords &rec = st.rec[depth & 1];
+        const int ri = st.escQ[qi];
+        const int slot = depth > 0 ? rec.pixel[ri] : ri;
+        int fl = depth > 0 ? rec.flags[ri] : 0;
+        float rl = depth > 0 ? rec.rl[ri] : 1.f;
         float denom = (depth == 0 || (fl & 1)) ? Avg31(1.f) : Avg31(1.f + rl * 0.f);
         const float invDenom = 1 / denom;
         float rgb[3] = {0, 0, 0};
@@ -699,7 +758,7 @@ __global__ void __launch_bounds__(kBlock) k_escaped(DeviceScene S, PathState st,
         for (int li = 0; li < S.nInfinite; ++li) {
             const float *dense = S.dense + S.infSpectrum[li] * kDenseN;
             float scale = S.infScale[li];
-            float sx = 0, sy = 0, sz = 0, lam = st.lambda0[slot];
+            float sx = 0, sy = 0, sz = 0, lam = rec.lambda0[ri];
             bool nz = false;
             for (int i = 0; i < kNSpectrumSamples; ++i) {
                 if (i > 0) {
@@ -709,7 +768,7 @@ __global__ void __launch_bounds__(kBlock) k_escaped(DeviceScene S, PathState st,
                 int off = DenseOffset(lam);
                 float Le = scale * (off < 0 ? 0.f : dense[off]);
                 nz |= Le != 0;
-                float v = ((depth > 0 ? st.beta[i * N + slot] : 1.f) * Le * invDenom) * kInvWavelengthPDF;
+                float v = ((depth > 0 ? rec.beta[i * N + ri] : 1.f) * Le * invDenom) * kInvWavelengthPDF;
                 float xb = off < 0 ? 0.f : S.sensor[off], yb = off < 0 ? 0.f : S.sensor[kDenseN + off],
                       zb = off < 0 ? 0.f : S.sensor[2 * kDenseN + off];
                 sx = i == 0 ? xb * v : sx + xb * v;
@@ -781,19 +840,22 @@ __global__ void __launch_bounds__(kBlock) k_emissive(DeviceScene S, PathState st
     for (int qi = blockIdx.x * blockDim.x + threadIdx.x; qi < count; qi += gridDim.x * blockDim.x) {
         // The queue is short, so this kernel's time is its dependent-load chain: every load
         // that depends only on the slot is issued up front, beta's 31 values included.
-        const int slot = st.emitQ[qi];
-        const int prim = hitPrim[slot];
-        const float b0 = hitB[slot], b1 = hitB[N + slot], b2 = hitB[2 * N + slot];
-        const V3 rd(st.ray[3 * N + slot], st.ray[4 * N + slot], st.ray[5 * N + slot]);
-        const float lambda0 = st.lambda0[slot];
-        const bool mis = depth > 0 && !(st.flags[slot] & 1);
-        const float rl = depth > 0 ? st.rl[slot] : 1.f;
-        const int pp = depth > 0 ? prevPrim[slot] : 0;
-        const float pb0 = depth > 0 ? prevB[slot] : 0.f, pb1 = depth > 0 ? prevB[N + slot] : 0.f,
-                    pb2 = depth > 0 ? prevB[2 * N + slot] : 0.f;
+        const PathRecords &rec = st.rec[depth & 1];
+        const int ri = st.emitQ[qi];
+        const int prim = hitPrim[ri];
+        const float b0 = hitB[ri], b1 = hitB[N + ri], b2 = hitB[2 * N + ri];
+        const V3 rd(rec.ray[3 * N + ri], rec.ray[4 * N + ri], rec.ray[5 * N + ri]);
+        const float lambda0 = rec.lambda0[ri];
+        const int slot = depth > 0 ? rec.pixel[ri] : ri;
+        const bool mis = depth > 0 && !(rec.flags[ri] & 1);
+        const float rl = depth > 0 ? rec.rl[ri] : 1.f;
+        const int pi = depth > 0 ? rec.prevIdx[ri] : 0;  // previous depth's record of this path
+        const int pp = depth > 0 ? prevPrim[pi] : 0;
+        const float pb0 = depth > 0 ? prevB[pi] : 0.f, pb1 = depth > 0 ? prevB[N + pi] : 0.f,
+                    pb2 = depth > 0 ? prevB[2 * N + pi] : 0.f;
         float beta[kNSpectrumSamples];
 #pragma unroll
-        for (int i = 0; i < kNSpectrumSamples; ++i) beta[i] = depth > 0 ? st.beta[(size_t)i * N + slot] : 1.f;
+        for (int i = 0; i < kNSpectrumSamples; ++i) beta[i] = depth > 0 ? rec.beta[(size_t)i * N + ri] : 1.f;
         V3 p0, p1, p2;
         PrimVerts(S, prim, &p0, &p1, &p2);
         const int light = S.primLight[prim];
@@ -907,21 +969,27 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
     const int count = st.counters[depth * kCounterStride + kCntMat];
     int *nextCounter = &st.counters[(depth + 1) * kCounterStride + kCntRay];
     int *shadowCounter = &st.counters[depth * kCounterStride + kCntShadow];
-    int *nextQ = st.rayQ[(depth + 1) & 1];
+    const PathRecords &rec = st.rec[depth & 1], &out = st.rec[(depth + 1) & 1];
     const int *hitPrim = st.hitPrim[depth & 1];
     const float *hitB = st.hitB[depth & 1];
     for (int base = blockIdx.x * blockDim.x; base < count; base += gridDim.x * blockDim.x) {
         int qi = base + threadIdx.x;
         bool active = qi < count;
         bool pushRay = false, pushShadow = false;
-        int slot = active ? st.matQ[qi] : 0;
+        const int ri = active ? st.matQ[qi] : 0;  // this depth's record
+        // outputs kept to the (block-wide) queue appends: shadow ray, continuing path
+        V3 sOrg, sDir, sL, nOrg, nDir;
+        float nRl = 0, nEta = 1;
+        int slot = 0;
+        float lambda0 = 0;
         SEC_BEGIN();
         if (active) {
-            const float lambda0 = st.lambda0[slot];
-            const float *betaP = st.beta + slot;
-            int prim = hitPrim[slot];
-            float b0 = hitB[slot], b1 = hitB[N + slot], b2 = hitB[2 * N + slot];
-            V3 rd(st.ray[3 * N + slot], st.ray[4 * N + slot], st.ray[5 * N + slot]);
+            lambda0 = rec.lambda0[ri];
+            slot = depth > 0 ? rec.pixel[ri] : ri;
+            const float *betaP = rec.beta + ri;
+            int prim = hitPrim[ri];
+            float b0 = hitB[ri], b1 = hitB[N + ri], b2 = hitB[2 * N + ri];
+            V3 rd(rec.ray[3 * N + ri], rec.ray[4 * N + ri], rec.ray[5 * N + ri]);
             int px, py, sampleIndex;
             PixelOf(st, slot, &px, &py, &sampleIndex);
             px += S.px0;
@@ -1004,18 +1072,12 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                                                               absdot, invDenom, &acc);
                                 if (nz) {
                                     // SpawnRayTo(pi, n, time, pLight.pi, pLight.n) (ray.h:106-111)
-                                    V3 pf = OffsetRayOrigin(pi, pe, n, lp - pi);
-                                    V3 pt = OffsetRayOrigin(lp, lpe, ln, pf - lp);
-                                    V3 sd = pt - pf;
-                                    st.shadowRay[slot] = pf.x;
-                                    st.shadowRay[N + slot] = pf.y;
-                                    st.shadowRay[2 * N + slot] = pf.z;
-                                    st.shadowRay[3 * N + slot] = sd.x;
-                                    st.shadowRay[4 * N + slot] = sd.y;
-                                    st.shadowRay[5 * N + slot] = sd.z;
-                                    st.shadowL[slot] = S.imagingRatio * (acc.sx / kNSpectrumSamples);
-                                    st.shadowL[N + slot] = S.imagingRatio * (acc.sy / kNSpectrumSamples);
-                                    st.shadowL[2 * N + slot] = S.imagingRatio * (acc.sz / kNSpectrumSamples);
+                                    sOrg = OffsetRayOrigin(pi, pe, n, lp - pi);
+                                    V3 pt = OffsetRayOrigin(lp, lpe, ln, sOrg - lp);
+                                    sDir = pt - sOrg;
+                                    sL = V3(S.imagingRatio * (acc.sx / kNSpectrumSamples),
+                                            S.imagingRatio * (acc.sy / kNSpectrumSamples),
+                                            S.imagingRatio * (acc.sz / kNSpectrumSamples));
                                     pushShadow = true;
                                 }
                             }
@@ -1031,7 +1093,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                     if (pdf != 0 && wiL.z != 0) {
                         V3 wi = frame.FromLocal(wiL);
                         float absdot = AbsDotN(ns, wi);
-                        float etaScale = depth > 0 ? st.etaScale[slot] : 1.f;
+                        float etaScale = depth > 0 ? rec.etaScale[ri] : 1.f;
                         float avgRu = Avg31(1.f);
                         float mx = -kInfinity;
 #pragma unroll 4
@@ -1050,25 +1112,19 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                         if (!kill) {
                             bool rrScale = mx < 1 && depth >= 1;
                             bool nz = false;
-                            float *betaW = st.beta + slot;
 #pragma unroll 4
                             for (int i = 0; i < kNSpectrumSamples; ++i) {
                                 float nbv = bf[i * kBlock];
                                 if (rrScale) nbv /= 1 - q;
                                 nz |= nbv != 0;
-                                betaW[i * N] = nbv;
+                                bf[i * kBlock] = nbv;  // written out after the queue append
                             }
                             if (nz) {
-                                V3 ro = OffsetRayOrigin(pi, pe, n, wi);
+                                nOrg = OffsetRayOrigin(pi, pe, n, wi);
+                                nDir = wi;
+                                nRl = 1.f / pdf;
+                                nEta = etaScale;
                                 pushRay = true;
-                                st.ray[slot] = ro.x;
-                                st.ray[N + slot] = ro.y;
-                                st.ray[2 * N + slot] = ro.z;
-                                st.ray[3 * N + slot] = wi.x;
-                                st.ray[4 * N + slot] = wi.y;
-                                st.ray[5 * N + slot] = wi.z;
-                                st.rl[slot] = 1.f / pdf;
-                                st.flags[slot] = 2;  // specularBounce = false, anyNonSpecular = true
                             }
                         }
                     }
@@ -1076,12 +1132,44 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
             }
         }
         SEC_MARK(st, 6);
+        // Queue appends (one global atomic per block and queue): the shadow ray and the
+        // continuing path are written densely at their queue positions (pbrt's
+        // ShadowRayQueue / next RayQueue pushes, surfscatter.cpp:236-246, 310-316).
         int *const cnt[2] = {nextCounter, shadowCounter};
         const bool pred[2] = {pushRay, pushShadow};
         int pos[2];
         BlockPush<2>(cnt, pred, pos);
-        if (pos[0] >= 0) nextQ[pos[0]] = slot;
-        if (pos[1] >= 0) st.shadowQ[pos[1]] = slot;
+        if (pos[1] >= 0) {
+            const int j = pos[1];
+            st.shadowRay[j] = sOrg.x;
+            st.shadowRay[N + j] = sOrg.y;
+            st.shadowRay[2 * N + j] = sOrg.z;
+            st.shadowRay[3 * N + j] = sDir.x;
+            st.shadowRay[4 * N + j] = sDir.y;
+            st.shadowRay[5 * N + j] = sDir.z;
+            st.shadowL[j] = sL.x;
+            st.shadowL[N + j] = sL.y;
+            st.shadowL[2 * N + j] = sL.z;
+            st.shadowPixel[j] = slot;
+        }
+        if (pos[0] >= 0) {
+            const int j = pos[0];
+            const float *bf = bfLds + threadIdx.x;
+#pragma unroll 8
+            for (int i = 0; i < kNSpectrumSamples; ++i) out.beta[(size_t)i * N + j] = bf[i * kBlock];
+            out.ray[j] = nOrg.x;
+            out.ray[N + j] = nOrg.y;
+            out.ray[2 * N + j] = nOrg.z;
+            out.ray[3 * N + j] = nDir.x;
+            out.ray[4 * N + j] = nDir.y;
+            out.ray[5 * N + j] = nDir.z;
+            out.lambda0[j] = lambda0;
+            out.rl[j] = nRl;
+            out.etaScale[j] = nEta;
+            out.flags[j] = 2;  // specularBounce = false, anyNonSpecular = true
+            out.pixel[j] = slot;
+            out.prevIdx[j] = ri;
+        }
         SEC_MARK(st, 7);
     }
 }
@@ -1094,15 +1182,16 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_shadow(DeviceS
     const int count = st.counters[depth * kCounterStride + kCntShadow];
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&st.stats[2], (unsigned long long)count);
     for (int qi = blockIdx.x * blockDim.x + threadIdx.x; qi < count; qi += gridDim.x * blockDim.x) {
-        int slot = st.shadowQ[qi];
-        V3 o(st.shadowRay[slot], st.shadowRay[N + slot], st.shadowRay[2 * N + slot]);
-        V3 d(st.shadowRay[3 * N + slot], st.shadowRay[4 * N + slot], st.shadowRay[5 * N + slot]);
+        // the shadow queue is dense: record qi holds the ray, its contribution and its pixel
+        V3 o(st.shadowRay[qi], st.shadowRay[N + qi], st.shadowRay[2 * N + qi]);
+        V3 d(st.shadowRay[3 * N + qi], st.shadowRay[4 * N + qi], st.shadowRay[5 * N + qi]);
         TriHit h;
         int hit = Traverse<true>(S, L, o, d, 1 - kShadowEpsilon, &h);
         if (hit < 0) {
-            st.L[slot] += st.shadowL[slot];
-            st.L[N + slot] += st.shadowL[N + slot];
-            st.L[2 * N + slot] += st.shadowL[2 * N + slot];
+            const int slot = st.shadowPixel[qi];
+            st.L[slot] += st.shadowL[qi];
+            st.L[N + slot] += st.shadowL[N + qi];
+            st.L[2 * N + slot] += st.shadowL[2 * N + qi];
         }
     }
 }

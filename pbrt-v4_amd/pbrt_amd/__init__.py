@@ -84,6 +84,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_context_free", "pbrt_render", "pbrt_synchronize", "pbrt_get_stats", "pbrt_reset_stats",
     "pbrt_film_clear", "pbrt_film_device_ptr", "pbrt_film_read", "pbrt_film_get_rgb", "pbrt_intersect",
     "pbrt_debug_halton", "pbrt_debug_rgb_coeffs", "pbrt_debug_rgb2spec_column", "pbrt_debug_kernel_sections",
+    "pbrt_debug_queue_counts",
 ]
 
 _LIB = None
@@ -122,6 +123,7 @@ def _lib():
     lib.pbrt_debug_rgb_coeffs.argtypes = [c.c_float, c.c_float, c.c_float, c.POINTER(c.c_float)]
     lib.pbrt_debug_rgb2spec_column.argtypes = [c.c_int, c.c_int, c.c_int, c.POINTER(c.c_float)]
     lib.pbrt_debug_kernel_sections.argtypes = [c.c_void_p, c.POINTER(c.c_uint64), c.c_int]
+    lib.pbrt_debug_queue_counts.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_int]
     lib.pbrt_set_data_dir(str(DATA_DIR).encode())
     _LIB = lib
     return lib
@@ -225,6 +227,13 @@ class WavefrontPathIntegrator:
 
     def reset_stats(self):
         _check(_lib().pbrt_reset_stats(self._h))
+
+    def queue_counts(self):
+        """Per-depth queue sizes of the last pass: rows of (rays, material, shadow, escaped, emissive)."""
+        n = 8 * (self.info.max_depth + 3)
+        out = (ctypes.c_int32 * n)()
+        _check(_lib().pbrt_debug_queue_counts(self._h, out, n))
+        return np.array(out[:], dtype=np.int64).reshape(-1, 8)[:, :5]
 
     def kernel_sections(self, n=32):
         """Summed wave cycles per instrumented kernel section (profiling build only)."""

@@ -24,3 +24,5 @@ cyc = integ.kernel_sections(16)
 tot = sum(cyc[:8]) or 1
 for i, n in enumerate(NAMES):
     print(f"{i} {n:28s} {cyc[i] / 1e9:10.3f} Gcyc  {100 * cyc[i] / tot:5.1f}%")
+print("queue counts of the last pass (rays, material, shadow, escaped, emissive):")
+print(integ.queue_counts())

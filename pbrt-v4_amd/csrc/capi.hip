@@ -413,20 +413,25 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
     // shadowL 3, L 3, filterW 1 = 101; ints: records 2 x (flags, pixel, prevIdx), hitPrim 2,
     // shadowPixel, matQ, escQ, emitQ = 12
     const int nf = 101, ni = 12;
-    c->fState.Alloc((size_t)nf * N);
-    c->iState.Alloc((size_t)ni * N + kCounterStride * (c->desc.maxDepth + 3));
+    const int64_t capS = ((N + kShards - 1) / kShards + 256 + 63) / 64 * 64;
+    const int64_t NR = capS * kShards;  // record stride
+    // per pixel-sample arrays (L, filterW) use N; the rest NR (>= N)
+    c->fState.Alloc((size_t)nf * NR);
+    c->iState.Alloc((size_t)ni * NR + CounterIndex(c->desc.maxDepth + 3, 0, 0));
     c->maxPaths = N;
     PathState &st = c->st;
+    st.capS = (int)capS;
+    st.NR = (int)NR;
     float *f = c->fState.p;
     auto take = [&](int k) {
         float *r = f;
-        f += (size_t)k * N;
+        f += (size_t)k * NR;
         return r;
     };
     int *ip = c->iState.p;
     auto takei = [&](int k) {
         int *r = ip;
-        ip += (size_t)k * N;
+        ip += (size_t)k * NR;
         return r;
     };
     for (int b = 0; b < 2; ++b) {
@@ -494,7 +499,7 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
         HIPCHECK(hipMemcpy(c->rows.p, rows.data(), rows.size() * sizeof(int), hipMemcpyHostToDevice));
         c->lastRows = rows;
     }
-    const int countersBytes = kCounterStride * (s.maxDepth + 3) * sizeof(int);
+    const int countersBytes = CounterIndex(s.maxDepth + 3, 0, 0) * sizeof(int);
     for (size_t r0 = 0; r0 < rows.size(); r0 += rowsPerChunk) {
         int nRows = (int)std::min<int64_t>(rowsPerChunk, rows.size() - r0);
         int64_t P = (int64_t)nRows * width;
@@ -811,8 +816,15 @@ float pbrt_debug_halton(const pbrt_scene *scene, int px, int py, int sampleIndex
         index %= stride;
     }
     index += (uint64_t)sampleIndex * stride;
-    if (dim == -1) return RadicalInverse(2, index >> s.haltonBaseExponents[0]);
-    if (dim == -2) return RadicalInverse(3, index / s.haltonBaseScales[1]);
+    // the camera kernel's evaluation (32-bit digit loop below 2^30)
+    if (dim == -1) {
+        const uint64_t a = index >> s.haltonBaseExponents[0];
+        return a < (1ull << 30) ? RadicalInverse32<2>((uint32_t)a) : RadicalInverse(2, a);
+    }
+    if (dim == -2) {
+        const uint64_t a = index / s.haltonBaseScales[1];
+        return a < (1ull << 30) ? RadicalInverse32<3>((uint32_t)a) : RadicalInverse(3, a);
+    }
     if (dim < 0 || dim >= (int)s.permBase.size()) return -1;
     // the device's evaluation path
     HaltonDimDesc d = MakeHaltonDimDesc(s.permBase[dim], s.permNDigits[dim], s.permOffset[dim]);
@@ -846,8 +858,15 @@ int pbrt_debug_queue_counts(pbrt_context *ctx, int32_t *counts, int n) {
         if (!ctx || !counts || n <= 0) return Fail("null argument");
         HIPCHECK(hipSetDevice(ctx->device));
         HIPCHECK(hipStreamSynchronize(ctx->stream));
-        n = std::min(n, kCounterStride * (ctx->desc.maxDepth + 3));
-        HIPCHECK(hipMemcpy(counts, ctx->st.counters, n * sizeof(int32_t), hipMemcpyDeviceToHost));
+        const int depths = ctx->desc.maxDepth + 3;
+        std::vector<int32_t> raw(CounterIndex(depths, 0, 0));
+        HIPCHECK(hipMemcpy(raw.data(), ctx->st.counters, raw.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+        // [depth][8]: totals over shards of the kNumQueues queues, zero padded
+        for (int i = 0; i < n; ++i) counts[i] = 0;
+        for (int d = 0; d < depths; ++d)
+            for (int q = 0; q < kNumQueues; ++q)
+                for (int sh = 0; sh < kShards; ++sh)
+                    if (d * 8 + q < n) counts[d * 8 + q] += raw[CounterIndex(d, q, sh)];
         return 0;
     } catch (const std::exception &e) {
         return Fail(e.what());

@@ -575,7 +575,8 @@ PHD float ScrambledRadicalInverse32(uint32_t base, uint32_t nDigits, uint32_t a,
 // t = mulhi(magic, a), exact for every 32-bit a), all permutation loads issued together and the
 // reversed digits held in 32 bits; the float arithmetic is unchanged.  Otherwise the 64-bit
 // restatement above runs.
-constexpr int kMaxMagicDigits = 8;  // dims >= 6 use bases >= 17: at most 7 digits (float precision)
+constexpr int kMaxMagicDigits = 8;       // dims >= 6 (bases >= 17): at most 7 digits
+constexpr int kMaxMagicDigitsWide = 12;  // every dim with base^nDigits < 2^32 (base 5: 11 digits)
 struct HaltonDimDesc {
     uint32_t base, nDigits, permOffset, magic, shift, fast;
     float invBase;
@@ -591,7 +592,7 @@ PHD HaltonDimDesc MakeHaltonDimDesc(uint32_t base, uint32_t nDigits, uint32_t pe
     d.shift = l - 1;
     d.magic = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - base)) / base + 1);
     uint64_t pw = 1;
-    bool fits = nDigits <= (uint32_t)kMaxMagicDigits;
+    bool fits = nDigits <= (uint32_t)kMaxMagicDigitsWide;
     for (uint32_t k = 0; fits && k < nDigits; ++k) {
         pw *= base;
         fits = pw < ((uint64_t)1 << 32);
@@ -601,12 +602,13 @@ PHD HaltonDimDesc MakeHaltonDimDesc(uint32_t base, uint32_t nDigits, uint32_t pe
     return d;
 }
 // PermPtr: a plain pointer, or an LDS-qualified one in the kernels that stage the tables.
-template <typename PermPtr>
+// MaxDigits >= d.nDigits (callers check): the digit loop is unrolled to that bound.
+template <int MaxDigits, typename PermPtr>
 PHD float ScrambledRadicalInverse32Magic(const HaltonDimDesc &d, uint32_t a, PermPtr perm) {
     const uint32_t base = d.base;
-    uint32_t pv[kMaxMagicDigits];
+    uint32_t pv[MaxDigits];
 PHD_UNROLL
-    for (int k = 0; k < kMaxMagicDigits; ++k) {
+    for (int k = 0; k < MaxDigits; ++k) {
         uint32_t t = (uint32_t)(((uint64_t)d.magic * a) >> 32);
         uint32_t next = (t + ((a - t) >> 1)) >> d.shift;
         // unconditional (row clamped to the table) so the loads issue together; rows past
@@ -618,7 +620,7 @@ PHD_UNROLL
     float invBaseM = 1;
     uint32_t reversedDigits = 0;
 PHD_UNROLL
-    for (int k = 0; k < kMaxMagicDigits; ++k) {
+    for (int k = 0; k < MaxDigits; ++k) {
         if ((uint32_t)k < d.nDigits) {
             reversedDigits = reversedDigits * base + pv[k];
             invBaseM *= d.invBase;
@@ -627,7 +629,8 @@ PHD_UNROLL
     return std::fmin(invBaseM * (float)reversedDigits, kOneMinusEpsilon);
 }
 PHD float HaltonSampleDimension(const HaltonDimDesc &d, uint64_t index, const uint16_t *permTable) {
-    if ((index >> 32) == 0 && d.fast) return ScrambledRadicalInverse32Magic(d, (uint32_t)index, permTable + d.permOffset);
+    if ((index >> 32) == 0 && d.fast)
+        return ScrambledRadicalInverse32Magic<kMaxMagicDigitsWide>(d, (uint32_t)index, permTable + d.permOffset);
     return ScrambledRadicalInverse(d.base, d.nDigits, index, permTable + d.permOffset);
 }
 
@@ -640,6 +643,23 @@ PHD float RadicalInverse(uint32_t base, uint64_t a) {
         uint64_t next = a / base;
         uint64_t digit = a - next * base;
         reversedDigits = reversedDigits * base + digit;
+        invBaseM *= invBase;
+        a = next;
+    }
+    return std::fmin((float)reversedDigits * invBaseM, kOneMinusEpsilon);
+}
+// RadicalInverse for a < 2^30 and Base <= 3: the same digit loop in 32-bit integers.  The
+// reversed digits stay below Base * a < 2^32 and the 64-bit limit (~2^62) is never reached,
+// so digits and float rounding are identical; no 64-bit division.
+template <uint32_t Base>
+PHD float RadicalInverse32(uint32_t a) {
+    static_assert(Base <= 3, "RadicalInverse32: Base * 2^30 must fit in 32 bits");
+    float invBase = (float)1 / (float)Base, invBaseM = 1;
+    uint32_t reversedDigits = 0;
+    while (a) {
+        uint32_t next = a / Base;
+        uint32_t digit = a - next * Base;
+        reversedDigits = reversedDigits * Base + digit;
         invBaseM *= invBase;
         a = next;
     }

@@ -41,9 +41,19 @@ struct ShadeLdsLayout {
     int denseInLds, lightsInLds, matsInLds, permEntries;
 };
 
-// per-depth queue counters: counters[depth * kCounterStride + kCnt*]
-constexpr int kCounterStride = 8;
+// Work queues are sharded: a producer block appends to shard (blockIdx.x % kShards), each
+// shard with its own counter on its own cache line.  Same-line atomics serialise at ~11 ns
+// each on MI355X (tools/microbench/atomics.hip); kShards lines take the queue appends off the
+// critical path.  Producer grids are multiples of kShards and grid-stride in 256-item
+// chunks, so shard s receives at most count/kShards + 256 items: capS = N/kShards + 256
+// bounds every shard, and the records need no more memory than an unsharded queue.
+constexpr int kShards = 8;
+constexpr int kCounterPad = 64;  // ints between counters (256 B)
+constexpr int kNumQueues = 5;
 constexpr int kCntRay = 0, kCntMat = 1, kCntShadow = 2, kCntEscaped = 3, kCntEmissive = 4;
+PHD int CounterIndex(int depth, int queue, int shard) {
+    return ((depth * kNumQueues + queue) * kShards + shard) * kCounterPad;
+}
 // device stats slots: [0..7] ray counters, [16..47] per-section wave cycles (profiling build)
 constexpr int kStatsSlots = 48, kStatsSectionBase = 16;
 constexpr int kMaxStackSize = 64;  // traversal stack entries per lane (64 KB of LDS per block)
@@ -115,14 +125,14 @@ struct DeviceScene {
 // the other parity's records, so every later depth reads contiguous memory instead of the
 // thinning-out slots of the original pixel samples.
 struct PathRecords {
-    float *beta;      // [31][N] wavelength-major
-    float *ray;       // [6][N] o, d
-    float *lambda0;   // [N] first wavelength (the other 30 follow by pbrt's +10 nm rule)
-    float *rl;        // [N] r_l (spectrally constant for surface-only paths); depth > 0
-    float *etaScale;  // [N]
-    int *flags;       // [N] bit0 specularBounce, bit1 anyNonSpecular
-    int *pixel;       // [N] pixel-sample slot (index of L / film sample); depth > 0
-    int *prevIdx;     // [N] record index at the previous depth (its hit = the MIS context)
+    float *beta;      // [31][NR] wavelength-major
+    float *ray;       // [6][NR] o, d
+    float *lambda0;   // [NR] first wavelength (the other 30 follow by pbrt's +10 nm rule)
+    float *rl;        // [NR] r_l (spectrally constant for surface-only paths); depth > 0
+    float *etaScale;  // [NR]
+    int *flags;       // [NR] bit0 specularBounce, bit1 anyNonSpecular
+    int *pixel;       // [NR] pixel-sample slot (index of L / film sample); depth > 0
+    int *prevIdx;     // [NR] record index at the previous depth (its hit = the MIS context)
 };
 
 // Per-pass wavefront buffers; N = paths per pass = P pixels x S samples.
@@ -132,23 +142,25 @@ struct PathState {
     int width;          // pixel row width (px1 - px0)
     const int *rows;    // P / width row indices (absolute y)
     int firstSample;    // sample index of slot block 0
+    int capS;           // capacity of one queue shard
+    int NR;             // record stride = kShards * capS (>= N)
     PathRecords rec[2]; // by depth parity
     // hit records of each depth's rays (by record index), double-buffered by depth parity:
     // the previous depth's hit is the emissive-hit MIS context (pbrt's prevIntrCtx)
-    int *hitPrim[2];    // [N] each
-    float *hitB[2];     // [4][N] each: b0, b1, b2, t
+    int *hitPrim[2];    // [NR] each
+    float *hitB[2];     // [4][NR] each: b0, b1, b2, t
     // shadow-ray queue, compacted (pbrt's ShadowRayWorkItem)
-    float *shadowRay;   // [6][N]
-    float *shadowL;     // [3][N] sensor RGB to add when unoccluded
-    int *shadowPixel;   // [N]
+    float *shadowRay;   // [6][NR]
+    float *shadowL;     // [3][NR] sensor RGB to add when unoccluded
+    int *shadowPixel;   // [NR]
     // per pixel-sample slot
     float *L;           // [3][N] sensor RGB
     float *filterW;     // [N]
     // work queues: record indices of the current depth
-    int *matQ;          // [N] material (diffuse) hits
-    int *escQ;          // [N] escaped rays (only with infinite lights)
-    int *emitQ;         // [N] hits on emissive triangles
-    int *counters;      // [(maxDepth+2) * kCounterStride]: see kCnt*
+    int *matQ;          // [NR] material (diffuse) hits
+    int *escQ;          // [NR] escaped rays (only with infinite lights)
+    int *emitQ;         // [NR] hits on emissive triangles
+    int *counters;      // [CounterIndex(maxDepth + 2, 0, 0)]: per depth, queue and shard
     double *film;       // [4][xres*yres]: rgbSum[3], weightSum (sensor RGB)
     unsigned long long *stats;  // [kStatsSlots]
 };

@@ -158,6 +158,79 @@ struct BlockQueues {
     }
 };
 
+// Wave-local staging of queue appends: each wave owns a Cap-entry LDS buffer per queue, fills
+// it with ballot/popcount prefixes and writes it out in a contiguous run with one global
+// atomicAdd when it would overflow (and at the end).  No block barriers: a wave never waits
+// for the slowest wave of its block, unlike BlockQueues.
+template <int K, int Cap>
+struct WaveQueues {
+    int *buf;  // LDS: this wave's [K][Cap]
+    int fill[K];
+    int *const *counters;
+    int *const *queues;
+
+    __device__ WaveQueues(int *ldsAll, int *const *c, int *const *q) : counters(c), queues(q) {
+        buf = ldsAll + (threadIdx.x >> 6) * (K * Cap);
+#pragma unroll
+        for (int k = 0; k < K; ++k) fill[k] = 0;
+    }
+    __device__ void Flush(int k) {
+        const int n = fill[k];
+        if (n == 0) return;
+        int b = 0;
+        if (__lane_id() == 0) b = atomicAdd(counters[k], n);
+        b = __shfl(b, 0);
+        int *q = queues[k];
+        for (int i = __lane_id(); i < n; i += 64) q[b + i] = buf[k * Cap + i];
+        fill[k] = 0;
+    }
+    __device__ void Append(const bool (&pred)[K], int value) {
+        const int lane = __lane_id();
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const unsigned long long mask = __ballot(pred[k]);
+            const int n = __popcll(mask);
+            if (fill[k] + n > Cap) Flush(k);
+            if (pred[k]) buf[k * Cap + fill[k] + __popcll(mask & ((1ull << lane) - 1ull))] = value;
+            fill[k] += n;
+        }
+    }
+    __device__ void FlushAll() {
+#pragma unroll
+        for (int k = 0; k < K; ++k) Flush(k);
+    }
+};
+
+// A sharded queue as its consumer sees it: per-shard counts (uniform, scalar loads) and the
+// map from a dense item index j to the item's physical index (shard * capS + offset).
+struct QueueView {
+    int count[kShards];
+    int total, capS;
+};
+__device__ inline QueueView LoadQueue(const PathState &st, int depth, int queue) {
+    QueueView v;
+    v.total = 0;
+    v.capS = st.capS;
+#pragma unroll
+    for (int s = 0; s < kShards; ++s) {
+        v.count[s] = st.counters[CounterIndex(depth, queue, s)];
+        v.total += v.count[s];
+    }
+    return v;
+}
+__device__ inline int QueueSlot(const QueueView &v, int j) {
+    int base = 0, shard = 0;
+#pragma unroll
+    for (int s = 0; s < kShards - 1; ++s) {
+        const bool later = j >= base + v.count[s];
+        base += later ? v.count[s] : 0;
+        shard += later ? 1 : 0;
+        if (!later) break;
+    }
+    return shard * v.capS + (j - base);
+}
+__device__ inline int ProducerShard() { return blockIdx.x % kShards; }
+
 __device__ inline V3 XfPoint(const float *m, V3 p) {
     float xp = m[0] * p.x + m[1] * p.y + m[2] * p.z + m[3];
     float yp = m[4] * p.x + m[5] * p.y + m[6] * p.z + m[7];
@@ -620,7 +693,7 @@ __device__ inline float LightPMF(const DeviceScene &S, V3 p, V3 ns, int light) {
 __global__ void __launch_bounds__(kBlock) k_camera(DeviceScene S, PathState st, int nActive) {
     int slot = blockIdx.x * blockDim.x + threadIdx.x;
     if (slot == 0) {
-        st.counters[0] = nActive;  // depth-0 ray queue = every slot
+        st.counters[CounterIndex(0, kCntRay, 0)] = nActive;  // depth-0 records = every slot (shard 0)
         atomicAdd(&st.stats[0], (unsigned long long)nActive);
     }
     if (slot >= nActive) return;
@@ -631,8 +704,11 @@ __global__ void __launch_bounds__(kBlock) k_camera(DeviceScene S, PathState st, 
     float lu = Get1D(S, h);
     float lambda0 = Lerpf(lu, kLambdaMin, kLambdaMax);
     // GetCameraSample (samplers.h:797-813) with the box filter (filters.h:67-71)
-    float pix0 = RadicalInverse(2, h.index >> S.baseExponents[0]);
-    float pix1 = RadicalInverse(3, h.index / (uint64_t)S.baseScales[1]);
+    const uint64_t a0 = h.index >> S.baseExponents[0];
+    const uint64_t a1 = (h.index >> 32) == 0 ? (uint64_t)((uint32_t)h.index / (uint32_t)S.baseScales[1])
+                                             : h.index / (uint64_t)S.baseScales[1];
+    float pix0 = a0 < (1ull << 30) ? RadicalInverse32<2>((uint32_t)a0) : RadicalInverse(2, a0);
+    float pix1 = a1 < (1ull << 30) ? RadicalInverse32<3>((uint32_t)a1) : RadicalInverse(3, a1);
     float fx = Lerpf(pix0, -S.filterRadiusX, S.filterRadiusX), fy = Lerpf(pix1, -S.filterRadiusY, S.filterRadiusY);
     float pFilmX = px + fx + 0.5f, pFilmY = py + fy + 0.5f;
     float time = Get1D(S, h);
@@ -680,41 +756,44 @@ __global__ void __launch_bounds__(kBlock) k_camera(DeviceScene S, PathState st, 
     st.L[2 * N + slot] = 0;
     if (!S.boxFilter) st.filterW[slot] = 1.f;
     const PathRecords &r = st.rec[0];
+    const int NR = st.NR;
     r.lambda0[slot] = lambda0;
     r.ray[slot] = o.x;
-    r.ray[N + slot] = o.y;
-    r.ray[2 * N + slot] = o.z;
-    r.ray[3 * N + slot] = d.x;
-    r.ray[4 * N + slot] = d.y;
-    r.ray[5 * N + slot] = d.z;
+    r.ray[NR + slot] = o.y;
+    r.ray[2 * NR + slot] = o.z;
+    r.ray[3 * NR + slot] = d.x;
+    r.ray[4 * NR + slot] = d.y;
+    r.ray[5 * NR + slot] = d.z;
 }
 
 __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_closest(DeviceScene S, PathState st, int depth, int timed) {
-    if ((int)(blockIdx.x * blockDim.x) >= st.counters[depth * kCounterStride + kCntRay]) return;  // no work
+    const QueueView rays = LoadQueue(st, depth, kCntRay);
+    if ((int)(blockIdx.x * blockDim.x) >= rays.total) return;  // no work
     extern __shared__ float4 dynLds[];
     const SceneLds L = SetupSceneLds(S, dynLds);
-    int N = st.N;
+    const int N = st.NR;  // record stride
     const PathRecords &rec = st.rec[depth & 1];
-    const int count = st.counters[depth * kCounterStride + kCntRay];
-    int *matCounter = &st.counters[depth * kCounterStride + kCntMat];
-    int *escCounter = &st.counters[depth * kCounterStride + kCntEscaped];
-    int *emitCounter = &st.counters[depth * kCounterStride + kCntEmissive];
+    const int count = rays.total;
+    const int shard = ProducerShard();
+    int *matCounter = &st.counters[CounterIndex(depth, kCntMat, shard)];
+    int *escCounter = &st.counters[CounterIndex(depth, kCntEscaped, shard)];
+    int *emitCounter = &st.counters[CounterIndex(depth, kCntEmissive, shard)];
     int *hitPrim = st.hitPrim[depth & 1];
     float *hitB = st.hitB[depth & 1];
     const bool shade = depth < S.maxDepth;  // at maxDepth only emission and escape matter
-    constexpr int kCap = 2048;
-    __shared__ int qBuf[3 * kCap], qFill[3], qBase[3];
+    constexpr int kCap = 512;  // entries per wave and queue
+    __shared__ int qBuf[(kBlock / 64) * 3 * kCap];
     int *const qCnt[3] = {escCounter, emitCounter, matCounter};
-    int *const qArr[3] = {st.escQ, st.emitQ, st.matQ};
-    BlockQueues<3, kCap> queues{qBuf, qFill, qBase, qCnt, qArr};
-    queues.Init();
+    int *const qArr[3] = {st.escQ + shard * st.capS, st.emitQ + shard * st.capS, st.matQ + shard * st.capS};
+    WaveQueues<3, kCap> queues(qBuf, qCnt, qArr);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         atomicAdd(&st.stats[1], (unsigned long long)count);
         if (timed) atomicAdd(&st.stats[3], (unsigned long long)count);  // rays of event-timed launches
     }
     for (int base = blockIdx.x * blockDim.x; base < count; base += gridDim.x * blockDim.x) {
-        const int qi = base + threadIdx.x;  // record index of this depth
-        bool active = qi < count;
+        const int j = base + threadIdx.x;
+        bool active = j < count;
+        const int qi = active ? QueueSlot(rays, j) : 0;  // record index of this depth
         int prim = -1;
         TriHit h;
         if (active) {
@@ -743,11 +822,11 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_closest(Device
 // HandleEscapedRays (integrator.cpp:495-537) for UniformInfiniteLight: Le with MIS where
 // PDF_Li(allowIncompletePDF = true) == 0, so r_l contributes nothing.
 __global__ void __launch_bounds__(kBlock) k_escaped(DeviceScene S, PathState st, int depth) {
-    int N = st.N;
-    const int count = st.counters[depth * kCounterStride + kCntEscaped];
-    for (int qi = blockIdx.x * blockDim.x + threadIdx.x; qi < count; qi += gridDim.x * blockDim.x) {
+    const int N = st.N, NR = st.NR;
+    const QueueView esc = LoadQueue(st, depth, kCntEscaped);
+    for (int qi = blockIdx.x * blockDim.x + threadIdx.x; qi < esc.total; qi += gridDim.x * blockDim.x) {
         const PathRecords &rec = st.rec[depth & 1];
-        const int ri = st.escQ[qi];
+        const int ri = st.escQ[QueueSlot(esc, qi)];
         const int slot = depth > 0 ? rec.pixel[ri] : ri;
         int fl = depth > 0 ? rec.flags[ri] : 0;
         float rl = depth > 0 ? rec.rl[ri] : 1.f;
@@ -768,7 +847,7 @@ __global__ void __launch_bounds__(kBlock) k_escaped(DeviceScene S, PathState st,
                 int off = DenseOffset(lam);
                 float Le = scale * (off < 0 ? 0.f : dense[off]);
                 nz |= Le != 0;
-                float v = ((depth > 0 ? rec.beta[i * N + ri] : 1.f) * Le * invDenom) * kInvWavelengthPDF;
+                float v = ((depth > 0 ? rec.beta[i * NR + ri] : 1.f) * Le * invDenom) * kInvWavelengthPDF;
                 float xb = off < 0 ? 0.f : S.sensor[off], yb = off < 0 ? 0.f : S.sensor[kDenseN + off],
                       zb = off < 0 ? 0.f : S.sensor[2 * kDenseN + off];
                 sx = i == 0 ? xb * v : sx + xb * v;
@@ -831,8 +910,9 @@ struct SensorAcc {
 // context (pbrt's prevIntrCtx: p, n, ns, pError of the previous surface) is rebuilt from the
 // previous bounce's hit record with the same TriangleSurface arithmetic that produced it.
 __global__ void __launch_bounds__(kBlock) k_emissive(DeviceScene S, PathState st, int depth) {
-    int N = st.N;
-    const int count = st.counters[depth * kCounterStride + kCntEmissive];
+    const int N = st.NR, NL = st.N;  // record stride, pixel-sample stride (L)
+    const QueueView emit = LoadQueue(st, depth, kCntEmissive);
+    const int count = emit.total;
     const int *hitPrim = st.hitPrim[depth & 1];
     const float *hitB = st.hitB[depth & 1];
     const int *prevPrim = st.hitPrim[(depth + 1) & 1];
@@ -841,7 +921,7 @@ __global__ void __launch_bounds__(kBlock) k_emissive(DeviceScene S, PathState st
         // The queue is short, so this kernel's time is its dependent-load chain: every load
         // that depends only on the slot is issued up front, beta's 31 values included.
         const PathRecords &rec = st.rec[depth & 1];
-        const int ri = st.emitQ[qi];
+        const int ri = st.emitQ[QueueSlot(emit, qi)];
         const int prim = hitPrim[ri];
         const float b0 = hitB[ri], b1 = hitB[N + ri], b2 = hitB[2 * N + ri];
         const V3 rd(rec.ray[3 * N + ri], rec.ray[4 * N + ri], rec.ray[5 * N + ri]);
@@ -887,8 +967,8 @@ __global__ void __launch_bounds__(kBlock) k_emissive(DeviceScene S, PathState st
             acc.Add(S, off, beta[i] * Le * invDenom, i == 0);
         }
         st.L[slot] += S.imagingRatio * (acc.sx / kNSpectrumSamples);
-        st.L[N + slot] += S.imagingRatio * (acc.sy / kNSpectrumSamples);
-        st.L[2 * N + slot] += S.imagingRatio * (acc.sz / kNSpectrumSamples);
+        st.L[NL + slot] += S.imagingRatio * (acc.sy / kNSpectrumSamples);
+        st.L[2 * NL + slot] += S.imagingRatio * (acc.sz / kNSpectrumSamples);
     }
 }
 
@@ -923,7 +1003,8 @@ __device__ inline bool NeeAccumulate(const FD *dense, const LdsF4 *sensor4, cons
 // materials.  The only HBM traffic per item is its path state, the hit triangle and beta,
 // whose 31 values arrive by LDS-DMA while the sampler runs on LDS-resident tables.
 __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(DeviceScene S, PathState st, int depth) {
-    if ((int)(blockIdx.x * blockDim.x) >= st.counters[depth * kCounterStride + kCntMat]) return;  // no work
+    const QueueView mats = LoadQueue(st, depth, kCntMat);
+    if ((int)(blockIdx.x * blockDim.x) >= mats.total) return;  // no work
     extern __shared__ float4 dynLds[];
     char *ldsBase = reinterpret_cast<char *>(dynLds);
     const ShadeLdsLayout lay = S.shadeLds;
@@ -965,10 +1046,12 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
     const float4 *matsL = lay.matsInLds ? matsLds : S.matCoeffs;
     const int *matConstL = lay.matsInLds ? matConstLds : S.matConstant;
 
-    int N = st.N;
-    const int count = st.counters[depth * kCounterStride + kCntMat];
-    int *nextCounter = &st.counters[(depth + 1) * kCounterStride + kCntRay];
-    int *shadowCounter = &st.counters[depth * kCounterStride + kCntShadow];
+    const int N = st.NR;  // record stride
+    const int count = mats.total;
+    const int shard = ProducerShard();
+    int *nextCounter = &st.counters[CounterIndex(depth + 1, kCntRay, shard)];
+    int *shadowCounter = &st.counters[CounterIndex(depth, kCntShadow, shard)];
+    const int shardBase = shard * st.capS;
     const PathRecords &rec = st.rec[depth & 1], &out = st.rec[(depth + 1) & 1];
     const int *hitPrim = st.hitPrim[depth & 1];
     const float *hitB = st.hitB[depth & 1];
@@ -976,7 +1059,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
         int qi = base + threadIdx.x;
         bool active = qi < count;
         bool pushRay = false, pushShadow = false;
-        const int ri = active ? st.matQ[qi] : 0;  // this depth's record
+        const int ri = active ? st.matQ[QueueSlot(mats, qi)] : 0;  // this depth's record
         // outputs kept to the (block-wide) queue appends: shadow ray, continuing path
         V3 sOrg, sDir, sL, nOrg, nDir;
         float nRl = 0, nEta = 1;
@@ -1018,8 +1101,9 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                 const Halton h = StartPixelSample(S, px, py, sampleIndex, d0);
                 auto dim = [&](int k) -> float {
                     const HaltonDimDesc hd = S.haltonDim[d0 + k];
-                    if ((h.index >> 32) == 0 && hd.fast)
-                        return ScrambledRadicalInverse32Magic(hd, (uint32_t)h.index, permL + permOff[k]);
+                    if ((h.index >> 32) == 0 && hd.fast && hd.nDigits <= (uint32_t)kMaxMagicDigits)
+                        return ScrambledRadicalInverse32Magic<kMaxMagicDigits>(hd, (uint32_t)h.index,
+                                                                               permL + permOff[k]);
                     return ScrambledRadicalInverse(hd.base, hd.nDigits, h.index, S.perm + hd.permOffset);
                 };
                 const float dUc = dim(0), dU0 = dim(1), dU1 = dim(2);
@@ -1140,7 +1224,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
         int pos[2];
         BlockPush<2>(cnt, pred, pos);
         if (pos[1] >= 0) {
-            const int j = pos[1];
+            const int j = shardBase + pos[1];
             st.shadowRay[j] = sOrg.x;
             st.shadowRay[N + j] = sOrg.y;
             st.shadowRay[2 * N + j] = sOrg.z;
@@ -1153,7 +1237,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
             st.shadowPixel[j] = slot;
         }
         if (pos[0] >= 0) {
-            const int j = pos[0];
+            const int j = shardBase + pos[0];
             const float *bf = bfLds + threadIdx.x;
 #pragma unroll 8
             for (int i = 0; i < kNSpectrumSamples; ++i) out.beta[(size_t)i * N + j] = bf[i * kBlock];
@@ -1175,23 +1259,25 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
 }
 
 __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_shadow(DeviceScene S, PathState st, int depth) {
-    if ((int)(blockIdx.x * blockDim.x) >= st.counters[depth * kCounterStride + kCntShadow]) return;  // no work
+    const QueueView shadows = LoadQueue(st, depth, kCntShadow);
+    if ((int)(blockIdx.x * blockDim.x) >= shadows.total) return;  // no work
     extern __shared__ float4 dynLds[];
     const SceneLds L = SetupSceneLds(S, dynLds);
-    int N = st.N;
-    const int count = st.counters[depth * kCounterStride + kCntShadow];
+    const int N = st.NR, NL = st.N;
+    const int count = shadows.total;
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&st.stats[2], (unsigned long long)count);
     for (int qi = blockIdx.x * blockDim.x + threadIdx.x; qi < count; qi += gridDim.x * blockDim.x) {
-        // the shadow queue is dense: record qi holds the ray, its contribution and its pixel
-        V3 o(st.shadowRay[qi], st.shadowRay[N + qi], st.shadowRay[2 * N + qi]);
-        V3 d(st.shadowRay[3 * N + qi], st.shadowRay[4 * N + qi], st.shadowRay[5 * N + qi]);
+        // the shadow queue is dense per shard: entry p holds the ray, its contribution and pixel
+        const int p = QueueSlot(shadows, qi);
+        V3 o(st.shadowRay[p], st.shadowRay[N + p], st.shadowRay[2 * N + p]);
+        V3 d(st.shadowRay[3 * N + p], st.shadowRay[4 * N + p], st.shadowRay[5 * N + p]);
         TriHit h;
         int hit = Traverse<true>(S, L, o, d, 1 - kShadowEpsilon, &h);
         if (hit < 0) {
-            const int slot = st.shadowPixel[qi];
-            st.L[slot] += st.shadowL[qi];
-            st.L[N + slot] += st.shadowL[N + qi];
-            st.L[2 * N + slot] += st.shadowL[2 * N + qi];
+            const int slot = st.shadowPixel[p];
+            st.L[slot] += st.shadowL[p];
+            st.L[NL + slot] += st.shadowL[N + p];
+            st.L[2 * NL + slot] += st.shadowL[2 * N + p];
         }
     }
 }
@@ -1256,14 +1342,14 @@ static size_t StackBytes(const DeviceScene &S) { return TraversalLdsBytes(S.stac
 #ifndef PBRT_SHADE_GRID_CAP
 #define PBRT_SHADE_GRID_CAP 2048
 #endif
-static int TraversalGridFor(int n) {
+// Producer grids are multiples of kShards (the shard capacity bound depends on it).
+static int ShardedGrid(int n, int cap) {
     int g = (n + kBlock - 1) / kBlock;
-    return g < 1 ? 1 : (g > PBRT_GRID_CAP ? PBRT_GRID_CAP : g);
+    g = g < 1 ? 1 : (g > cap ? cap : g);
+    return (g + kShards - 1) / kShards * kShards;
 }
-static int ShadeGridFor(int n) {
-    int g = (n + kBlock - 1) / kBlock;
-    return g < 1 ? 1 : (g > PBRT_SHADE_GRID_CAP ? PBRT_SHADE_GRID_CAP : g);
-}
+static int TraversalGridFor(int n) { return ShardedGrid(n, PBRT_GRID_CAP); }
+static int ShadeGridFor(int n) { return ShardedGrid(n, PBRT_SHADE_GRID_CAP); }
 
 // Kernels over queues that are usually short (emissive hits, escaped rays): a grid of one
 // block per CU, grid-stride beyond that.

@@ -27,10 +27,11 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "pbrt-v4_amd"))
 
-# Algorithmic bytes per ray of the closest-hit kernel, from its declared SoA fields:
-#   reads  ray-queue entry 4 B + ray o,d 24 B             = 28 B
-#   writes hit prim 4 B + b0,b1,b2,t 16 B + queue push 4 B = 24 B
-BYTES_PER_RAY_CLOSEST = 52
+# Algorithmic bytes per ray of the closest-hit kernel, from its declared SoA fields (the
+# depth's path records are dense, so there is no ray-queue index to read):
+#   reads  ray o,d 24 B
+#   writes hit prim 4 B + b0,b1,b2,t 16 B + material-queue entry 4 B = 24 B
+BYTES_PER_RAY_CLOSEST = 48
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
 

@@ -80,6 +80,8 @@ typedef struct pbrt_scene_flat {
     int n_dims;
     const uint16_t *perm_table;
     const uint32_t *perm_offset, *perm_ndigits, *perm_base;
+    /* sampler: 0 halton, 1 zsobol (randomization 0 none, 1 permutedigits, 2 fastowen, 3 owen) */
+    int sampler_type, zs_randomize, zs_log2_spp, zs_nbase4_digits;
 } pbrt_scene_flat;
 
 typedef struct pbrt_render_params {
@@ -130,6 +132,10 @@ int pbrt_intersect(pbrt_context *ctx, const float *rays_dev, int n, int any_hit,
 float pbrt_debug_halton(const pbrt_scene *scene, int px, int py, int sample_index, int dim);
 int pbrt_debug_rgb_coeffs(float r, float g, float b, float *coeffs3);
 int pbrt_debug_rgb2spec_column(int maxc, int j, int i, float *out192);
+/* ZSobolSampler (samplers.h:225-370) from StartPixelSample((px,py), sample_index, dim) with the
+ * wavefront's call pattern Get1D, Get2D, Get1D, Get2D, Get1D -> 7 values (scene's sampler
+ * parameters: spp, resolution, seed, randomization) */
+int pbrt_debug_zsobol(const pbrt_scene *scene, int px, int py, int sample_index, int dim, float *out7);
 /* queue counters of the last pass: [depth][8] = rays, material hits, shadow rays, escaped,
  * emissive hits (diagnostics) */
 int pbrt_debug_queue_counts(pbrt_context *ctx, int32_t *counts, int n);

@@ -385,6 +385,129 @@ struct HaltonState {
     }
 };
 
+// ---------------------------------------------------------------- ZSobol
+// ZSobolSampler (samplers.h:225-370).  Sobol' dimension 0 is the van der Corput matrix; the
+// rows of dimension 1 are Pascal's triangle mod 2 (bit r of row k set iff (r & k) == r by
+// Lucas), top 32 bits of the 52-bit rows of util/sobolmatrices.
+struct ZSobol {
+    int log2Spp = 0, nBase4Digits = 0, seed = 0, randomize = 2;
+    static const int perm4[24][4];
+    void Init(int spp, int xres, int yres, int seed_, int randomize_) {
+        seed = seed_;
+        randomize = randomize_;
+        log2Spp = 0;
+        while ((2 << log2Spp) <= spp) ++log2Spp;  // Log2Int
+        int res = 1;
+        while (res < std::max(xres, yres)) res *= 2;  // RoundUpPow2
+        int l = 0;
+        while ((2 << l) <= res) ++l;
+        nBase4Digits = l + (log2Spp + 1) / 2;
+    }
+};
+const int ZSobol::perm4[24][4] = {{0, 1, 2, 3}, {0, 1, 3, 2}, {0, 2, 1, 3}, {0, 2, 3, 1}, {0, 3, 2, 1}, {0, 3, 1, 2},
+                                  {1, 0, 2, 3}, {1, 0, 3, 2}, {1, 2, 0, 3}, {1, 2, 3, 0}, {1, 3, 2, 0}, {1, 3, 0, 2},
+                                  {2, 1, 0, 3}, {2, 1, 3, 0}, {2, 0, 1, 3}, {2, 0, 3, 1}, {2, 3, 0, 1}, {2, 3, 1, 0},
+                                  {3, 1, 2, 0}, {3, 1, 0, 2}, {3, 2, 1, 0}, {3, 2, 0, 1}, {3, 0, 2, 1}, {3, 0, 1, 2}};
+
+static uint64_t Mix64(uint64_t v) {
+    v = (v ^ (v >> 31)) * 0x7fb5d329728ea185ull;
+    v = (v ^ (v >> 27)) * 0x81dadef4bc2dd44dull;
+    return v ^ (v >> 33);
+}
+static uint32_t BitReverse(uint32_t v) {
+    uint32_t r = 0;
+    for (int i = 0; i < 32; ++i) r |= ((v >> i) & 1u) << (31 - i);
+    return r;
+}
+static uint32_t SobolRow(int dim, int k) {
+    if (dim == 0) return k < 32 ? 0x80000000u >> k : 0u;
+    uint32_t w = 0;
+    for (int r = 0; r < 32; ++r)
+        if ((r & k) == r) w |= 0x80000000u >> r;
+    return w;
+}
+
+struct ZSobolState {
+    const ZSobol *z;
+    uint64_t morton = 0;
+    int dimension = 0;
+    void Start(int px, int py, int sampleIndex, int dim) {
+        uint64_t m = 0;
+        for (int b = 0; b < 32; ++b) m |= (uint64_t)((uint32_t)px >> b & 1) << (2 * b) | (uint64_t)((uint32_t)py >> b & 1) << (2 * b + 1);
+        morton = (m << z->log2Spp) | (uint64_t)(uint32_t)sampleIndex;
+        dimension = dim;
+    }
+    uint64_t Index() const {
+        uint64_t idx = 0;
+        const bool odd = z->log2Spp & 1;
+        const uint64_t salt = (uint64_t)(uint32_t)(0x55555555u * (uint32_t)dimension);
+        for (int i = z->nBase4Digits - 1; i >= (odd ? 1 : 0); --i) {
+            int shift = 2 * i - (odd ? 1 : 0);
+            int digit = (int)(morton >> shift) & 3;
+            int p = (int)((Mix64((morton >> (shift + 2)) ^ salt) >> 24) % 24);
+            idx |= (uint64_t)ZSobol::perm4[p][digit] << shift;
+        }
+        if (odd) idx |= ((morton & 1) ^ (Mix64((morton >> 1) ^ salt) & 1));
+        return idx;
+    }
+    static uint64_t HashDimSeed(int d, int seed) {
+        unsigned char buf[8];
+        std::memcpy(buf, &d, 4);
+        std::memcpy(buf + 4, &seed, 4);
+        return Murmur64A(buf, 8, 0);
+    }
+    Float Sobol(uint64_t a, int dim, uint32_t h) const {
+        uint32_t v = 0;
+        for (int k = 0; a; a >>= 1, ++k)
+            if (a & 1) v ^= SobolRow(dim, k);
+        switch (z->randomize) {
+        case 1: v ^= h; break;
+        case 2: {  // FastOwenScrambler (lowdiscrepancy.h:221-237)
+            v = BitReverse(v);
+            v ^= v * 0x3d20adea;
+            v += h;
+            v *= (h >> 16) | 1;
+            v ^= v * 0x05526c56;
+            v ^= v * 0x53a22864;
+            v = BitReverse(v);
+            break;
+        }
+        case 3: {  // OwenScrambler (lowdiscrepancy.h:240-258)
+            if (h & 1) v ^= 1u << 31;
+            for (int b = 1; b < 32; ++b)
+                if ((uint32_t)Mix64((v & (~0u << (32 - b))) ^ h) & (1u << b)) v ^= 1u << (31 - b);
+            break;
+        }
+        default: break;
+        }
+        return std::min(v * 0x1p-32f, OneMinusEpsilon);
+    }
+    Float Get1D() {
+        uint64_t idx = Index();
+        ++dimension;
+        return Sobol(idx, 0, (uint32_t)HashDimSeed(dimension, z->seed));
+    }
+    void Get2D(Float *a, Float *b) {
+        uint64_t idx = Index();
+        dimension += 2;
+        uint64_t h = HashDimSeed(dimension, z->seed);
+        *a = Sobol(idx, 0, (uint32_t)h);
+        *b = Sobol(idx, 1, (uint32_t)(h >> 32));
+    }
+    void Pixel2D(Float *a, Float *b) { Get2D(a, b); }
+};
+
+// Either sampler behind pbrt's Sampler interface calls used by the wavefront
+struct AnySampler {
+    HaltonState h;
+    ZSobolState z;
+    bool zsobol;
+    void Start(int px, int py, int si, int dim) { zsobol ? z.Start(px, py, si, dim) : h.Start(px, py, si, dim); }
+    Float Get1D() { return zsobol ? z.Get1D() : h.Get1D(); }
+    void Get2D(Float *a, Float *b) { zsobol ? z.Get2D(a, b) : h.Get2D(a, b); }
+    void Pixel2D(Float *a, Float *b) { zsobol ? z.Pixel2D(a, b) : h.Pixel2D(a, b); }
+};
+
 // ---------------------------------------------------------------- geometry
 struct TriIsect {
     Float b0, b1, b2, t;
@@ -511,6 +634,8 @@ struct Scene {
     std::vector<BVHNode> nodes;
     std::vector<int> order;
     Halton halton;
+    ZSobol zsobol;
+    bool useZSobol = false;
     int xres, yres, px0, px1, py0, py1, maxDepth;
     Float frx, fry;
     Vec P(int t, int k) const { return v[tri[3 * t + k]]; }
@@ -572,6 +697,8 @@ struct Scene {
         frx = info->filter_radius_x;
         fry = info->filter_radius_y;
         halton.Init(xres, yres, (uint32_t)info->seed, std::max(f->n_dims, 7 * maxDepth + 7));
+        useZSobol = f->sampler_type == 1;
+        zsobol.Init(info->spp, xres, yres, info->seed, f->zs_randomize);
     }
 
     static bool BoxHit(const BVHNode &n, Vec o, Vec invDir, const int neg[3], Float rayTMax) {
@@ -946,7 +1073,7 @@ struct Renderer {
 
     // one pixel sample -> sensor RGB and filter weight (film.h:95-100)
     void Li(int px, int py, int sampleIndex, float rgb[3], float *weight) const {
-        HaltonState hs{&S.halton, 0, 0};
+        AnySampler hs{HaltonState{&S.halton, 0, 0}, ZSobolState{&S.zsobol}, S.useZSobol};
         hs.Start(px, py, sampleIndex, 0);
         Float lu = hs.Get1D();
         Wavelengths lambda = Wavelengths::SampleUniform(lu);
@@ -1022,7 +1149,7 @@ struct Renderer {
             }
             if (depth == S.maxDepth) break;
             // GenerateRaySamples: dims 6 + 7 depth
-            HaltonState h2{&S.halton, 0, 0};
+            AnySampler h2{HaltonState{&S.halton, 0, 0}, ZSobolState{&S.zsobol}, S.useZSobol};
             h2.Start(px, py, sampleIndex, 6 + 7 * depth);
             Float dUc = h2.Get1D(), dU0, dU1;
             h2.Get2D(&dU0, &dU1);
@@ -1259,6 +1386,19 @@ void oracle_sample_wavelengths(float u, float *lambda31, float *pdf) {
     Wavelengths w = Wavelengths::SampleUniform(u);
     std::memcpy(lambda31, w.lambda, sizeof w.lambda);
     *pdf = w.pdf[0];
+}
+
+void oracle_zsobol(int spp, int xres, int yres, int seed, int randomize, int px, int py, int sampleIndex, int dim,
+                   float *out7) {
+    ZSobol z;
+    z.Init(spp, xres, yres, seed, randomize);
+    ZSobolState s{&z};
+    s.Start(px, py, sampleIndex, dim);
+    out7[0] = s.Get1D();
+    s.Get2D(&out7[1], &out7[2]);
+    out7[3] = s.Get1D();
+    s.Get2D(&out7[4], &out7[5]);
+    out7[6] = s.Get1D();
 }
 
 float oracle_halton(int xres, int yres, int seed, int px, int py, int sampleIndex, int dim) {

@@ -30,6 +30,7 @@ def lib():
         _lib.oracle_light_importance.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         _lib.oracle_sample_wavelengths.argtypes = [ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p]
         _lib.oracle_halton.argtypes = [ctypes.c_int] * 7
+        _lib.oracle_zsobol.argtypes = [ctypes.c_int] * 9 + [ctypes.c_void_p]
         vp = ctypes.c_void_p
         _lib.oracle_warps.argtypes = [vp, vp, vp]
         _lib.oracle_spherical_triangle.argtypes = [vp, vp, vp, vp]

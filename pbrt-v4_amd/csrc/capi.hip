@@ -132,6 +132,8 @@ struct pbrt_context {
     DevBuf<uint16_t> perm;
     DevBuf<HaltonDimDesc> haltonDim;
     DevBuf<uint16_t> permByDepth;
+    DevBuf<uint8_t> zsPerms;
+    DevBuf<uint32_t> sobolM1;
     DevBuf<uint32_t> permDepthInfo;
     DevBuf<float> sensor4;
     DevBuf<DeviceLightNode> lightNodes;
@@ -263,6 +265,13 @@ static void BuildDevice(pbrt_context *c) {
         hd.push_back(MakeHaltonDimDesc(s.permBase[d], s.permNDigits[d], s.permOffset[d]));
     c->haltonDim.Upload(hd);
     {
+        std::vector<uint8_t> zp(&kZSobolPermutations[0][0], &kZSobolPermutations[0][0] + 96);
+        c->zsPerms.Upload(zp);
+        std::vector<uint32_t> m1(kSobolMatrixSize);
+        for (int k = 0; k < kSobolMatrixSize; ++k) m1[k] = SobolMatrix1Row(k);
+        c->sobolM1.Upload(m1);
+    }
+    {
         std::vector<uint16_t> pb;
         std::vector<uint32_t> info((size_t)8 * (s.maxDepth + 1), 0);
         for (int depth = 0; depth < s.maxDepth; ++depth) {
@@ -349,6 +358,10 @@ static void BuildDevice(pbrt_context *c) {
         S.haltonFast32 = s.px0 >= 0 && s.py0 >= 0 && s0 * s1 * (s0 + s1) < (1ull << 32) ? 1 : 0;
     }
     S.maxDepth = s.maxDepth;
+    S.samplerType = s.samplerType;
+    S.zs = ZSobolParams{s.zsLog2SamplesPerPixel, s.zsNBase4Digits, s.seed, (Randomize)s.zsRandomize};
+    S.zsPerms = reinterpret_cast<const uint8_t(*)[4]>(c->zsPerms.p);
+    S.sobolM1 = c->sobolM1.p;
     {
         // k_shade_diffuse dynamic LDS: [beta*f 31x256 floats][sensor][light spectra][Halton
         // permutations of 7 dims][lights][light BVH][materials]
@@ -657,6 +670,10 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
     f->perm_offset = s.permOffset.data();
     f->perm_ndigits = s.permNDigits.data();
     f->perm_base = s.permBase.data();
+    f->sampler_type = s.samplerType;
+    f->zs_randomize = s.zsRandomize;
+    f->zs_log2_spp = s.zsLog2SamplesPerPixel;
+    f->zs_nbase4_digits = s.zsNBase4Digits;
     return 0;
 }
 
@@ -847,6 +864,26 @@ int pbrt_debug_rgb2spec_column(int maxc, int j, int i, float *out) {
     try {
         auto v = RGB2SpecColumn(maxc, j, i);
         std::copy(v.begin(), v.end(), out);
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_debug_zsobol(const pbrt_scene *scene, int px, int py, int sampleIndex, int dim, float *out7) {
+    try {
+        if (!scene || !out7) return Fail("null argument");
+        const SceneDesc &s = scene->desc;
+        ZSobolParams z{s.zsLog2SamplesPerPixel, s.zsNBase4Digits, s.seed, (Randomize)s.zsRandomize};
+        uint32_t m1[kSobolMatrixSize];
+        for (int k = 0; k < kSobolMatrixSize; ++k) m1[k] = SobolMatrix1Row(k);
+        const uint64_t morton = ZSobolMortonIndex(z, px, py, sampleIndex);
+        // the wavefront's call pattern from `dim`: Get1D, Get2D, Get1D, Get2D, Get1D
+        out7[0] = ZSobolGet1D(z, morton, dim, kZSobolPermutations, m1);
+        ZSobolGet2D(z, morton, dim + 1, kZSobolPermutations, m1, &out7[1], &out7[2]);
+        out7[3] = ZSobolGet1D(z, morton, dim + 3, kZSobolPermutations, m1);
+        ZSobolGet2D(z, morton, dim + 4, kZSobolPermutations, m1, &out7[4], &out7[5]);
+        out7[6] = ZSobolGet1D(z, morton, dim + 6, kZSobolPermutations, m1);
         return 0;
     } catch (const std::exception &e) {
         return Fail(e.what());

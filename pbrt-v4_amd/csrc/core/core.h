@@ -675,6 +675,142 @@ PHD uint64_t InverseRadicalInverse(uint64_t inverse, int base, int nDigits) {
     return index;
 }
 
+// ---------------------------------------------------------------- ZSobol sampler
+// ZSobolSampler (samplers.h:225-370): Morton-ordered pixel samples, base-4 digit
+// permutations per dimension, Sobol' dimensions 0/1 with the chosen scrambler.
+PHD uint64_t LeftShift2(uint64_t x) {  // util/math.h:83-91
+    x &= 0xffffffff;
+    x = (x ^ (x << 16)) & 0x0000ffff0000ffffull;
+    x = (x ^ (x << 8)) & 0x00ff00ff00ff00ffull;
+    x = (x ^ (x << 4)) & 0x0f0f0f0f0f0f0f0full;
+    x = (x ^ (x << 2)) & 0x3333333333333333ull;
+    x = (x ^ (x << 1)) & 0x5555555555555555ull;
+    return x;
+}
+PHD uint64_t EncodeMorton2(uint32_t x, uint32_t y) { return (LeftShift2(y) << 1) | LeftShift2(x); }
+PHD uint64_t MixBits(uint64_t v) {  // util/hash.h:70-77
+    v ^= (v >> 31);
+    v *= 0x7fb5d329728ea185ull;
+    v ^= (v >> 27);
+    v *= 0x81dadef4bc2dd44dull;
+    v ^= (v >> 33);
+    return v;
+}
+// MurmurHash64A over one 8-byte block with seed 0: pbrt's Hash(int a, int b) (util/hash.h:100-106)
+PHD uint64_t HashInt2(int32_t a, int32_t b) {
+    const uint64_t m = 0xc6a4a7935bd1e995ull;
+    const int r = 47;
+    uint64_t h = 0 ^ (8ull * m);
+    uint64_t k = (uint64_t)(uint32_t)a | ((uint64_t)(uint32_t)b << 32);  // little-endian packing
+    k *= m;
+    k ^= k >> r;
+    k *= m;
+    h ^= k;
+    h *= m;
+    h ^= h >> r;
+    h *= m;
+    h ^= h >> r;
+    return h;
+}
+PHD uint32_t ReverseBits32(uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_bitreverse32(v);
+#else
+    v = (v << 16) | (v >> 16);
+    v = ((v & 0x00ff00ff) << 8) | ((v & 0xff00ff00) >> 8);
+    v = ((v & 0x0f0f0f0f) << 4) | ((v & 0xf0f0f0f0) >> 4);
+    v = ((v & 0x33333333) << 2) | ((v & 0xcccccccc) >> 2);
+    v = ((v & 0x55555555) << 1) | ((v & 0xaaaaaaaa) >> 1);
+    return v;
+#endif
+}
+// Sobol' generator matrices of dimensions 0 and 1 (the only ones ZSobol reads), 52 rows of
+// 32 bits each as in util/sobolmatrices: dimension 0 is the van der Corput matrix; dimension 1
+// follows from its primitive polynomial x + 1, V_k = V_{k-1} ^ (V_{k-1} >> 1) on 52-bit rows,
+// keeping the top 32 bits.
+constexpr int kSobolMatrixSize = 52;
+PHD uint32_t SobolMatrix1Row(int k) {
+    uint64_t v = 1ull << 51;
+    for (int i = 0; i < k; ++i) v ^= v >> 1;
+    return (uint32_t)(v >> 20);
+}
+enum class Randomize : int { None = 0, PermuteDigits = 1, FastOwen = 2, Owen = 3 };
+PHD uint32_t FastOwenScramble(uint32_t v, uint32_t seed) {  // lowdiscrepancy.h:221-237
+    v = ReverseBits32(v);
+    v ^= v * 0x3d20adea;
+    v += seed;
+    v *= (seed >> 16) | 1;
+    v ^= v * 0x05526c56;
+    v ^= v * 0x53a22864;
+    return ReverseBits32(v);
+}
+PHD uint32_t OwenScramble(uint32_t v, uint32_t seed) {  // lowdiscrepancy.h:240-258
+    if (seed & 1) v ^= 1u << 31;
+    for (int b = 1; b < 32; ++b) {
+        uint32_t mask = (~0u) << (32 - b);
+        if ((uint32_t)MixBits((v & mask) ^ seed) & (1u << b)) v ^= 1u << (31 - b);
+    }
+    return v;
+}
+// SobolSample (lowdiscrepancy.h:168-180) for dimension 0 or 1; matrix1 = the 52 rows above
+PHD float SobolSampleDim01(uint64_t a, int dim, Randomize rz, uint32_t seed, const uint32_t *matrix1) {
+    uint32_t v = 0;
+    if (dim == 0) {
+        v = ReverseBits32((uint32_t)a);  // rows >= 32 of dimension 0 are zero
+    } else {
+        for (int i = 0; a != 0; a >>= 1, ++i)
+            if (a & 1) v ^= matrix1[i];
+    }
+    if (rz == Randomize::PermuteDigits) v ^= seed;
+    else if (rz == Randomize::FastOwen) v = FastOwenScramble(v, seed);
+    else if (rz == Randomize::Owen) v = OwenScramble(v, seed);
+    return std::fmin(v * 0x1p-32f, kOneMinusEpsilon);
+}
+struct ZSobolParams {
+    int log2SamplesPerPixel, nBase4Digits, seed;
+    Randomize randomize;
+};
+// samplers.h:301-356 GetSampleIndex; perms = the 24 four-way permutations in pbrt's order
+PHD uint64_t ZSobolSampleIndex(const ZSobolParams &z, uint64_t mortonIndex, int dimension,
+                               const uint8_t (*perms)[4]) {
+    uint64_t sampleIndex = 0;
+    const bool pow2Samples = z.log2SamplesPerPixel & 1;
+    const int lastDigit = pow2Samples ? 1 : 0;
+    for (int i = z.nBase4Digits - 1; i >= lastDigit; --i) {
+        int digitShift = 2 * i - (pow2Samples ? 1 : 0);
+        int digit = (int)((mortonIndex >> digitShift) & 3);
+        uint64_t higherDigits = mortonIndex >> (digitShift + 2);
+        int p = (int)((MixBits(higherDigits ^ (uint64_t)(0x55555555u * (uint32_t)dimension)) >> 24) % 24);
+        digit = perms[p][digit];
+        sampleIndex |= uint64_t(digit) << digitShift;
+    }
+    if (pow2Samples) {
+        int digit = (int)(mortonIndex & 1);
+        sampleIndex |= digit ^ (MixBits((mortonIndex >> 1) ^ (uint64_t)(0x55555555u * (uint32_t)dimension)) & 1);
+    }
+    return sampleIndex;
+}
+// Get1D at state dimension `dimension` (samplers.h:257-271): index from the current dimension,
+// hash from the incremented one
+PHD float ZSobolGet1D(const ZSobolParams &z, uint64_t morton, int dimension, const uint8_t (*perms)[4],
+                      const uint32_t *matrix1) {
+    uint64_t sampleIndex = ZSobolSampleIndex(z, morton, dimension, perms);
+    uint32_t sampleHash = (uint32_t)HashInt2(dimension + 1, z.seed);
+    return SobolSampleDim01(sampleIndex, 0, z.randomize, sampleHash, matrix1);
+}
+// Get2D at state dimension `dimension` (samplers.h:273-292)
+PHD void ZSobolGet2D(const ZSobolParams &z, uint64_t morton, int dimension, const uint8_t (*perms)[4],
+                     const uint32_t *matrix1, float *u0, float *u1) {
+    uint64_t sampleIndex = ZSobolSampleIndex(z, morton, dimension, perms);
+    uint64_t bits = HashInt2(dimension + 2, z.seed);
+    *u0 = SobolSampleDim01(sampleIndex, 0, z.randomize, (uint32_t)bits, matrix1);
+    *u1 = SobolSampleDim01(sampleIndex, 1, z.randomize, (uint32_t)(bits >> 32), matrix1);
+}
+// StartPixelSample (samplers.h:252-255)
+PHD uint64_t ZSobolMortonIndex(const ZSobolParams &z, int px, int py, int sampleIndex) {
+    return (EncodeMorton2((uint32_t)px, (uint32_t)py) << z.log2SamplesPerPixel) | (uint64_t)(uint32_t)sampleIndex;
+}
+
 // ---------------------------------------------------------------- light BVH importance
 // lightsamplers.h:130 CompactLightBounds::Importance on host-decoded bounds.
 struct LightNodeBounds {

@@ -436,9 +436,34 @@ static void BuildLightBVH(SceneDesc &s) {
     if (!bvhLights.empty()) b.Build(bvhLights, 0, (int)bvhLights.size(), 0, 0);
 }
 
+// samplers.h:303-330 (ZSobolSampler::GetSampleIndex permutations)
+const uint8_t kZSobolPermutations[24][4] = {
+    {0, 1, 2, 3}, {0, 1, 3, 2}, {0, 2, 1, 3}, {0, 2, 3, 1}, {0, 3, 2, 1}, {0, 3, 1, 2},
+    {1, 0, 2, 3}, {1, 0, 3, 2}, {1, 2, 0, 3}, {1, 2, 3, 0}, {1, 3, 2, 0}, {1, 3, 0, 2},
+    {2, 1, 0, 3}, {2, 1, 3, 0}, {2, 0, 1, 3}, {2, 0, 3, 1}, {2, 3, 0, 1}, {2, 3, 1, 0},
+    {3, 1, 2, 0}, {3, 1, 0, 2}, {3, 2, 1, 0}, {3, 2, 0, 1}, {3, 0, 2, 1}, {3, 0, 1, 2}};
+
+// ZSobolSampler ctor (samplers.h:228-239)
+static void BuildZSobol(SceneDesc &s) {
+    auto log2Int = [](int64_t v) {
+        int r = -1;
+        while (v > 0) {
+            v >>= 1;
+            ++r;
+        }
+        return r;
+    };
+    s.zsLog2SamplesPerPixel = log2Int(s.spp);
+    int64_t res = 1;
+    while (res < std::max(s.xres, s.yres)) res <<= 1;  // RoundUpPow2
+    int log4SamplesPerPixel = (s.zsLog2SamplesPerPixel + 1) / 2;
+    s.zsNBase4Digits = log2Int(res) + log4SamplesPerPixel;
+}
+
 void FinalizeScene(SceneDesc &s) {
     BuildLightBVH(s);
     BuildHalton(s);
+    BuildZSobol(s);
 }
 
 }  // namespace pbrt_amd

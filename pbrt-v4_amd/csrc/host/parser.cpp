@@ -684,10 +684,22 @@ void Parser::Finish() {
     scene.seed = samplerParams.GetInt("seed", 0);
     if (overrides.count("spp")) scene.spp = std::stoi(overrides.at("spp"));
     if (overrides.count("seed")) scene.seed = std::stoi(overrides.at("seed"));
-    if (scene.samplerName != "halton")
-        throw Error(samplerParams.loc + ": sampler \"" + scene.samplerName + "\" not supported yet (halton only)");
-    if (samplerParams.GetString("randomization", "permutedigits") != "permutedigits")
-        throw Error(samplerParams.loc + ": only permutedigits randomization is supported");
+    if (scene.samplerName == "halton") {
+        scene.samplerType = 0;
+        if (samplerParams.GetString("randomization", "permutedigits") != "permutedigits")
+            throw Error(samplerParams.loc + ": halton: only permutedigits randomization is supported");
+    } else if (scene.samplerName == "zsobol") {
+        // samplers.cpp:146-170 (ZSobolSampler::Create), default randomization fastowen
+        scene.samplerType = 1;
+        std::string r = samplerParams.GetString("randomization", "fastowen");
+        if (r == "none") scene.zsRandomize = 0;
+        else if (r == "permutedigits") scene.zsRandomize = 1;
+        else if (r == "fastowen") scene.zsRandomize = 2;
+        else if (r == "owen") scene.zsRandomize = 3;
+        else throw Error(samplerParams.loc + ": unknown randomization strategy \"" + r + "\" given to ZSobolSampler");
+    } else {
+        throw Error(samplerParams.loc + ": sampler \"" + scene.samplerName + "\" not supported yet (halton, zsobol)");
+    }
     samplerParams.CheckUnused();
     // ---- integrator
     scene.maxDepth = integratorParams.GetInt("maxdepth", 5);

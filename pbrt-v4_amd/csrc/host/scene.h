@@ -101,6 +101,11 @@ struct SceneDesc {
     std::vector<LightBVHNodeDesc> lightNodes;
     std::vector<uint32_t> lightBitTrail;  // per area light
 
+    // sampler: 0 = HaltonSampler (permutedigits), 1 = ZSobolSampler (samplers.h:225-370)
+    int samplerType = 1;
+    int zsRandomize = 2;  // Randomize: 0 none, 1 permutedigits, 2 fastowen, 3 owen
+    int zsLog2SamplesPerPixel = 0, zsNBase4Digits = 0;
+
     // Halton digit permutations (util/lowdiscrepancy.cpp:47-55) for the dimensions used
     int haltonBaseScales[2] = {1, 1}, haltonBaseExponents[2] = {0, 0}, haltonMultInverse[2] = {0, 0};
     std::vector<uint16_t> permTable;       // concatenated nDigits*base rows per dimension
@@ -113,7 +118,9 @@ struct SceneDesc {
 SceneDesc LoadPbrtFile(const std::string &path, const std::map<std::string, std::string> &overrides);
 SceneDesc LoadPbrtString(const std::string &text, const std::string &baseDir,
                          const std::map<std::string, std::string> &overrides);
-void FinalizeScene(SceneDesc &s);  // lights, light BVH, halton tables
+void FinalizeScene(SceneDesc &s);  // lights, light BVH, sampler tables
+// the 24 four-way digit permutations of ZSobolSampler::GetSampleIndex, in pbrt's order
+extern const uint8_t kZSobolPermutations[24][4];
 
 // Spectral support (host)
 struct SpectralData {

@@ -114,6 +114,11 @@ struct DeviceScene {
     int nDims;
     int baseScales[2], baseExponents[2], multInverse[2];
     int haltonFast32;  // pixel offsets computable in 32 bits (StartPixelSample fast path)
+    // sampler: 0 Halton, 1 ZSobol
+    int samplerType;
+    ZSobolParams zs;
+    const uint8_t (*zsPerms)[4];  // [24][4]
+    const uint32_t *sobolM1;      // Sobol' dimension-1 matrix rows [52]
     int maxDepth;
     int stackSize;  // BVH traversal stack entries per lane (BVH8::maxStack)
     int ldsNodes, ldsTris;  // BVH8 nodes / triangles cached in LDS by the traversal kernels

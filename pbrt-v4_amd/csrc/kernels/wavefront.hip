@@ -700,21 +700,30 @@ __global__ void __launch_bounds__(kBlock) k_camera(DeviceScene S, PathState st, 
     int px, py, sampleIndex;
     PixelOf(st, slot, &px, &py, &sampleIndex);
     px += S.px0;
-    Halton h = StartPixelSample(S, px, py, sampleIndex, 0);
-    float lu = Get1D(S, h);
+    // camera.cpp:50-62: wavelength Get1D, then GetCameraSample (samplers.h:797-813): pixel
+    // offset (GetPixel2D) through the box filter (filters.h:67-71), time Get1D, lens Get2D
+    float lu, pix0, pix1, l0, l1;
+    if (S.samplerType == 1) {
+        // ZSobolSampler: dimensions 0 (wavelength), 1-2 (pixel), 3 (time), 4-5 (lens)
+        const uint64_t morton = ZSobolMortonIndex(S.zs, px, py, sampleIndex);
+        lu = ZSobolGet1D(S.zs, morton, 0, S.zsPerms, S.sobolM1);
+        ZSobolGet2D(S.zs, morton, 1, S.zsPerms, S.sobolM1, &pix0, &pix1);
+        ZSobolGet2D(S.zs, morton, 4, S.zsPerms, S.sobolM1, &l0, &l1);
+    } else {
+        // HaltonSampler: GetPixel2D reads the pixel's own Halton digits, not a dimension
+        Halton h = StartPixelSample(S, px, py, sampleIndex, 0);
+        lu = Get1D(S, h);
+        const uint64_t a0 = h.index >> S.baseExponents[0];
+        const uint64_t a1 = (h.index >> 32) == 0 ? (uint64_t)((uint32_t)h.index / (uint32_t)S.baseScales[1])
+                                                 : h.index / (uint64_t)S.baseScales[1];
+        pix0 = a0 < (1ull << 30) ? RadicalInverse32<2>((uint32_t)a0) : RadicalInverse(2, a0);
+        pix1 = a1 < (1ull << 30) ? RadicalInverse32<3>((uint32_t)a1) : RadicalInverse(3, a1);
+        (void)Get1D(S, h);  // time (unused: static camera)
+        Get2D(S, h, &l0, &l1);
+    }
     float lambda0 = Lerpf(lu, kLambdaMin, kLambdaMax);
-    // GetCameraSample (samplers.h:797-813) with the box filter (filters.h:67-71)
-    const uint64_t a0 = h.index >> S.baseExponents[0];
-    const uint64_t a1 = (h.index >> 32) == 0 ? (uint64_t)((uint32_t)h.index / (uint32_t)S.baseScales[1])
-                                             : h.index / (uint64_t)S.baseScales[1];
-    float pix0 = a0 < (1ull << 30) ? RadicalInverse32<2>((uint32_t)a0) : RadicalInverse(2, a0);
-    float pix1 = a1 < (1ull << 30) ? RadicalInverse32<3>((uint32_t)a1) : RadicalInverse(3, a1);
     float fx = Lerpf(pix0, -S.filterRadiusX, S.filterRadiusX), fy = Lerpf(pix1, -S.filterRadiusY, S.filterRadiusY);
     float pFilmX = px + fx + 0.5f, pFilmY = py + fy + 0.5f;
-    float time = Get1D(S, h);
-    (void)time;
-    float l0, l1;
-    Get2D(S, h, &l0, &l1);
     // PerspectiveCamera::GenerateRay (cameras.cpp:433-456)
     V3 pCamera = XfPoint(S.cameraFromRaster, V3(pFilmX, pFilmY, 0));
     V3 o(0, 0, 0), d = Normalize(pCamera);
@@ -1098,16 +1107,29 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
             {
                 // ---- GenerateRaySamples (samples.cpp:29-66): dims 6 + 7 * depth + {0..6}
                 // = direct.uc, direct.u (2), indirect.uc, indirect.u (2), rr
-                const Halton h = StartPixelSample(S, px, py, sampleIndex, d0);
-                auto dim = [&](int k) -> float {
-                    const HaltonDimDesc hd = S.haltonDim[d0 + k];
-                    if ((h.index >> 32) == 0 && hd.fast && hd.nDigits <= (uint32_t)kMaxMagicDigits)
-                        return ScrambledRadicalInverse32Magic<kMaxMagicDigits>(hd, (uint32_t)h.index,
-                                                                               permL + permOff[k]);
-                    return ScrambledRadicalInverse(hd.base, hd.nDigits, h.index, S.perm + hd.permOffset);
-                };
-                const float dUc = dim(0), dU0 = dim(1), dU1 = dim(2);
-                const float iU0 = dim(4), iU1 = dim(5), rr = dim(6);  // dim 3: indirect.uc, unused
+                float dUc, dU0, dU1, iU0, iU1, rr;  // dim 3 (indirect.uc) is unused by DiffuseBxDF
+                if (S.samplerType == 1) {
+                    const uint64_t morton = ZSobolMortonIndex(S.zs, px, py, sampleIndex);
+                    dUc = ZSobolGet1D(S.zs, morton, d0, S.zsPerms, S.sobolM1);
+                    ZSobolGet2D(S.zs, morton, d0 + 1, S.zsPerms, S.sobolM1, &dU0, &dU1);
+                    ZSobolGet2D(S.zs, morton, d0 + 4, S.zsPerms, S.sobolM1, &iU0, &iU1);
+                    rr = ZSobolGet1D(S.zs, morton, d0 + 6, S.zsPerms, S.sobolM1);
+                } else {
+                    const Halton h = StartPixelSample(S, px, py, sampleIndex, d0);
+                    auto dim = [&](int k) -> float {
+                        const HaltonDimDesc hd = S.haltonDim[d0 + k];
+                        if ((h.index >> 32) == 0 && hd.fast && hd.nDigits <= (uint32_t)kMaxMagicDigits)
+                            return ScrambledRadicalInverse32Magic<kMaxMagicDigits>(hd, (uint32_t)h.index,
+                                                                                   permL + permOff[k]);
+                        return ScrambledRadicalInverse(hd.base, hd.nDigits, h.index, S.perm + hd.permOffset);
+                    };
+                    dUc = dim(0);
+                    dU0 = dim(1);
+                    dU1 = dim(2);
+                    iU0 = dim(4);
+                    iU1 = dim(5);
+                    rr = dim(6);
+                }
                 SEC_MARK(st, 1);
                 // ---- DiffuseMaterial::GetBxDF: R = clamp(reflectance(lambda), 0, 1); f = R / pi
                 // (bxdfs.h DiffuseBxDF::f).  bf_i = beta_i * f_i is formed once per wavelength

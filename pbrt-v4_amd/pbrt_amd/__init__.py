@@ -62,6 +62,8 @@ class SceneFlat(ctypes.Structure):
         ("halton_mult_inverse", ctypes.c_int * 2), ("n_dims", ctypes.c_int),
         ("perm_table", ctypes.POINTER(ctypes.c_uint16)), ("perm_offset", ctypes.POINTER(ctypes.c_uint32)),
         ("perm_ndigits", ctypes.POINTER(ctypes.c_uint32)), ("perm_base", ctypes.POINTER(ctypes.c_uint32)),
+        ("sampler_type", ctypes.c_int), ("zs_randomize", ctypes.c_int), ("zs_log2_spp", ctypes.c_int),
+        ("zs_nbase4_digits", ctypes.c_int),
     ]
 
 
@@ -84,7 +86,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_context_free", "pbrt_render", "pbrt_synchronize", "pbrt_get_stats", "pbrt_reset_stats",
     "pbrt_film_clear", "pbrt_film_device_ptr", "pbrt_film_read", "pbrt_film_get_rgb", "pbrt_intersect",
     "pbrt_debug_halton", "pbrt_debug_rgb_coeffs", "pbrt_debug_rgb2spec_column", "pbrt_debug_kernel_sections",
-    "pbrt_debug_queue_counts",
+    "pbrt_debug_queue_counts", "pbrt_debug_zsobol",
 ]
 
 _LIB = None
@@ -123,6 +125,7 @@ def _lib():
     lib.pbrt_debug_rgb_coeffs.argtypes = [c.c_float, c.c_float, c.c_float, c.POINTER(c.c_float)]
     lib.pbrt_debug_rgb2spec_column.argtypes = [c.c_int, c.c_int, c.c_int, c.POINTER(c.c_float)]
     lib.pbrt_debug_kernel_sections.argtypes = [c.c_void_p, c.POINTER(c.c_uint64), c.c_int]
+    lib.pbrt_debug_zsobol.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_int, c.POINTER(c.c_float)]
     lib.pbrt_debug_queue_counts.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_int]
     lib.pbrt_set_data_dir(str(DATA_DIR).encode())
     _LIB = lib
@@ -168,6 +171,11 @@ class Scene:
         _check(_lib().pbrt_scene_get_flat(self._h, ctypes.byref(f)))
         f._owner = self  # keep the scene alive
         return f
+
+    def zsobol(self, px, py, sample_index, dim):
+        out = (ctypes.c_float * 7)()
+        _check(_lib().pbrt_debug_zsobol(self._h, px, py, sample_index, dim, out))
+        return np.array(out[:], dtype=np.float32)
 
     def halton(self, px, py, sample_index, dim):
         return _lib().pbrt_debug_halton(self._h, px, py, sample_index, dim)

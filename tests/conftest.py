@@ -40,3 +40,10 @@ def fl(v):
     if isinstance(v, list):
         return [fl(x) for x in v]
     return float(v)
+
+
+def cornell_with_sampler(pa, sampler_line, **overrides):
+    """The Cornell scene with its Sampler directive replaced (e.g. a zsobol configuration)."""
+    text = (SCENES / "cornell-box.pbrt").read_text()
+    lines = [sampler_line if ln.startswith("Sampler ") else ln for ln in text.splitlines()]
+    return pa.Scene.from_string("\n".join(lines) + "\n", SCENES, **overrides)

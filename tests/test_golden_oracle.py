@@ -140,3 +140,17 @@ def test_halton_bit_exact(oracle, golden, cfg_index):
         np.testing.assert_array_equal(np.float32(got), arr(vals))
         assert lib.oracle_halton(cfg["xres"], cfg["yres"], cfg["seed"], px, py, si, -1) == np.float32(p0)
         assert lib.oracle_halton(cfg["xres"], cfg["yres"], cfg["seed"], px, py, si, -2) == np.float32(p1)
+
+
+RANDOMIZE = {"none": 0, "permutedigits": 1, "fastowen": 2, "owen": 3}
+
+
+@pytest.mark.parametrize("cfg_index", range(6))
+def test_zsobol_bit_exact(oracle, golden, cfg_index):
+    """The oracle's ZSobolSampler restatement against the reference's (samplers.h:225-370)."""
+    cfg = golden["zsobol"][cfg_index]
+    out = (ctypes.c_float * 7)()
+    for px, py, si, dim, vals in cfg["samples"]:
+        oracle.lib().oracle_zsobol(cfg["spp"], cfg["xres"], cfg["yres"], cfg["seed"], RANDOMIZE[cfg["randomization"]],
+                                   px, py, si, dim, out)
+        np.testing.assert_array_equal(np.array(out[:], np.float32), np.array(vals, np.float32))

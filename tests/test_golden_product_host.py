@@ -87,3 +87,17 @@ def test_camera_rays_match_reference(pa, golden, i):
         d = d / np.linalg.norm(d)
         d = rfc[:3, :3] @ d
         np.testing.assert_allclose(d, [dx, dy, dz], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("cfg_index", range(6))
+def test_zsobol_bit_exact(pa, golden, cfg_index):
+    """ZSobolSampler (samplers.h:225-370): the product's sampler evaluation against the
+    reference's ZSobolSampler for the wavefront's call pattern (1D, 2D, 1D, 2D, 1D)."""
+    from conftest import cornell_with_sampler
+    cfg = golden["zsobol"][cfg_index]
+    line = (f'Sampler "zsobol" "integer pixelsamples" [ {cfg["spp"]} ] "integer seed" [ {cfg["seed"]} ] '
+            f'"string randomization" "{cfg["randomization"]}"')
+    sc = cornell_with_sampler(pa, line, xresolution=cfg["xres"], yresolution=cfg["yres"])
+    assert sc.flat().sampler_type == 1
+    for px, py, si, dim, vals in cfg["samples"]:
+        np.testing.assert_array_equal(sc.zsobol(px, py, si, dim), f32(vals), err_msg=f"{px} {py} {si} {dim}")

@@ -47,6 +47,18 @@ def test_cornell_c1_matches_oracle(pa, oracle):
     print(f"C1 parity: {frac*100:.3f}% pixels within 1e-3, mean rel {mean_rel:.2e}")
 
 
+@pytest.mark.parametrize("randomization", ["fastowen", "owen"])
+def test_cornell_zsobol_matches_oracle(pa, oracle, randomization):
+    """pbrt's default sampler (ZSobolSampler, fork default scene.cpp:93) end to end."""
+    from conftest import cornell_with_sampler
+    line = f'Sampler "zsobol" "integer pixelsamples" [ 16 ] "string randomization" "{randomization}"'
+    sc = cornell_with_sampler(pa, line, xresolution=160, yresolution=120)
+    film, _ = gpu_film(pa, sc)
+    ref = oracle.render(sc, threads=16)
+    frac, mean_rel = check_parity(to_rgb(oracle, sc, film), to_rgb(oracle, sc, ref))
+    print(f"ZSobol ({randomization}) parity: {frac*100:.3f}% pixels within 1e-3, mean rel {mean_rel:.2e}")
+
+
 def test_cornell_c2_rows_match_oracle(pa, oracle):
     sc = pa.load_scene(SCENES / "cornell-box.pbrt", xresolution=1280, yresolution=720, spp=64)
     rows = np.arange(300, 316, dtype=np.int32)

@@ -50,3 +50,11 @@ def test_cornell_plausible(pa, oracle):
     img = oracle.film_to_rgb(film, [f.output_rgb_from_sensor_rgb[i] for i in range(9)])
     # red wall left / green wall right after the "Scale -1 1 1" flip, light is brightest
     assert img[:, :4, 0].mean() > img[:, :4, 1].mean() and img[:, -4:, 1].mean() > img[:, -4:, 0].mean()
+
+
+def test_oracle_zsobol_render_runs(pa, oracle):
+    """The oracle renders the default-sampler (ZSobol) Cornell; finite, nonzero image."""
+    from conftest import cornell_with_sampler
+    sc = cornell_with_sampler(pa, 'Sampler "zsobol" "integer pixelsamples" [ 4 ]', xresolution=32, yresolution=24)
+    film = oracle.render(sc, threads=4)
+    assert np.isfinite(film).all() and film[:3].sum() > 0

@@ -82,6 +82,17 @@ typedef struct pbrt_scene_flat {
     const uint32_t *perm_offset, *perm_ndigits, *perm_base;
     /* sampler: 0 halton, 1 zsobol (randomization 0 none, 1 permutedigits, 2 fastowen, 3 owen) */
     int sampler_type, zs_randomize, zs_log2_spp, zs_nbase4_digits;
+    /* materials: type 0 diffuse, 1 dielectric, 2 conductor (materials.h DiffuseMaterial,
+     * DielectricMaterial, ConductorMaterial) */
+    const int32_t *material_type;     /* [n_materials] */
+    const float *material_params;     /* [n_materials][4]: alpha_x alpha_y eta 0 (TrowbridgeReitz
+                                         alphas after remap + clamp; dielectric eta) */
+    const int32_t *material_spectra;  /* [n_materials][2]: conductor eta, k indices into the
+                                         piecewise-linear spectra; -1 -1 = "reflectance" (coeffs) */
+    int n_pl_spectra;
+    const int32_t *pl_offsets;        /* [n_pl_spectra + 1] into pl_lambda / pl_value */
+    const float *pl_lambda, *pl_value;
+    int regularize;                   /* integrator "regularize" */
 } pbrt_scene_flat;
 
 typedef struct pbrt_render_params {
@@ -136,6 +147,22 @@ int pbrt_debug_rgb2spec_column(int maxc, int j, int i, float *out192);
  * wavefront's call pattern Get1D, Get2D, Get1D, Get2D, Get1D -> 7 values (scene's sampler
  * parameters: spp, resolution, seed, randomization) */
 int pbrt_debug_zsobol(const pbrt_scene *scene, int px, int py, int sample_index, int dim, float *out7);
+/* util/scattering.h components as the product evaluates them (core.h), host side.
+ * trowbridge: in13 = ax ay wo3 wi3 wm3 u0 u1 (TrowbridgeReitzDistribution(ax, ay)) ->
+ *   out14 = alpha_x alpha_y smooth D(wm) D(wo,wm) Lambda(wo) G1(wo) G(wo,wi) PDF(wo,wm)
+ *           Sample_wm(wo,u)3 regularized alpha_x alpha_y
+ * fresnel: in10 = cos eta eta_re eta_im wi3 n3 -> out10 = FrDielectric FrComplex
+ *   refract_ok etap wt3 reflect3 */
+int pbrt_debug_trowbridge(const float *in13, float *out14);
+int pbrt_debug_fresnel(const float *in10, float *out10);
+/* GetNamedSpectrum(name)(lambda_i) for the metal / glass tables */
+int pbrt_debug_named_spectrum(const char *name, const float *lambda, int n, float *out);
+/* DielectricBxDF (type 1) / ConductorBxDF (type 2) in the shading frame: params3 = alpha_x
+ * alpha_y eta (alphas as the constructor leaves them); eta31 / k31 the conductor's sampled
+ * spectra; u3 = uc u0 u1.  out70 = sample_ok wi3 pdf flags etap f_sample[31] f(wo,wi)[31]
+ * PDF(wo,wi) (Sample_f / f / PDF of bxdfs.h:300-517, bxdfs.cpp:77-245) */
+int pbrt_debug_bxdf(int type, const float *params3, const float *eta31, const float *k31, const float *wo3,
+                    const float *wi3, const float *u3, float *out70);
 /* queue counters of the last pass: [depth][8] = rays, material hits, shadow rays, escaped,
  * emissive hits (diagnostics) */
 int pbrt_debug_queue_counts(pbrt_context *ctx, int32_t *counts, int n);

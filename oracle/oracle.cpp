@@ -1048,6 +1048,296 @@ struct Lights {
     }
 };
 
+// ---------------------------------------------------------------- BxDFs
+// DiffuseBxDF (bxdfs.h:30-82), DielectricBxDF (bxdfs.h:300-341, bxdfs.cpp:77-245),
+// ConductorBxDF (bxdfs.h:413-517) with TrowbridgeReitzDistribution and the Fresnel terms of
+// util/scattering.h:18-205 and pstd::complex (util/pstd.h:1066-1229).  TransportMode::Radiance,
+// BxDFReflTransFlags::All throughout (the wavefront never restricts the sampled lobes).
+enum { BxR = 1, BxT = 2, BxDiffuse = 4, BxGlossy = 8, BxSpecular = 16 };
+
+struct BSDFSample {
+    Spectrum f;
+    Vec wi;
+    Float pdf = 0;
+    int flags = 0;
+    Float eta = 1;
+};
+
+static inline Float Tan2Theta(Vec w) {
+    Float sin2 = std::max<Float>(0, 1 - Sqr(w.z));
+    return sin2 / Sqr(w.z);
+}
+static inline Float CosPhi(Vec w) {
+    Float st = std::sqrt(std::max<Float>(0, 1 - Sqr(w.z)));
+    return st == 0 ? 1 : Clamp(w.x / st, -1, 1);
+}
+static inline Float SinPhi(Vec w) {
+    Float st = std::sqrt(std::max<Float>(0, 1 - Sqr(w.z)));
+    return st == 0 ? 0 : Clamp(w.y / st, -1, 1);
+}
+static inline bool SameHemisphere(Vec a, Vec b) { return a.z * b.z > 0; }
+
+struct TRDistribution {
+    Float ax = 0, ay = 0;
+    TRDistribution() = default;
+    TRDistribution(Float x, Float y) : ax(x), ay(y) {
+        if (!Smooth()) {
+            ax = std::max<Float>(ax, 1e-4f);
+            ay = std::max<Float>(ay, 1e-4f);
+        }
+    }
+    bool Smooth() const { return std::max(ax, ay) < 1e-3f; }
+    Float D(Vec wm) const {
+        Float t2 = Tan2Theta(wm);
+        if (std::isinf(t2)) return 0;
+        Float c4 = Sqr(Sqr(wm.z));
+        if (c4 < 1e-16f) return 0;
+        Float e = t2 * (Sqr(CosPhi(wm) / ax) + Sqr(SinPhi(wm) / ay));
+        return 1 / (Pi * ax * ay * c4 * Sqr(1 + e));
+    }
+    Float Lambda(Vec w) const {
+        Float t2 = Tan2Theta(w);
+        if (std::isinf(t2)) return 0;
+        Float a2 = Sqr(CosPhi(w) * ax) + Sqr(SinPhi(w) * ay);
+        return (std::sqrt(1 + a2 * t2) - 1) / 2;
+    }
+    Float G1(Vec w) const { return 1 / (1 + Lambda(w)); }
+    Float G(Vec wo, Vec wi) const { return 1 / (1 + Lambda(wo) + Lambda(wi)); }
+    Float PDF(Vec w, Vec wm) const { return G1(w) / std::abs(w.z) * D(wm) * AbsDot(w, wm); }
+    Vec Sample_wm(Vec w, Float u0, Float u1) const {
+        Vec wh = Normalize(Vec(ax * w.x, ay * w.y, w.z));
+        if (wh.z < 0) wh = -wh;
+        Vec T1 = (wh.z < 0.99999f) ? Normalize(Cross(Vec(0, 0, 1), wh)) : Vec(1, 0, 0);
+        Vec T2 = Cross(wh, T1);
+        Float r = std::sqrt(u0), th = 2 * Pi * u1;  // SampleUniformDiskPolar
+        Float px = r * std::cos(th), py = r * std::sin(th);
+        Float h = std::sqrt(1 - Sqr(px));
+        py = Lerp((1 + wh.z) / 2, h, py);
+        Float pz = std::sqrt(std::max<Float>(0, 1 - (Sqr(px) + Sqr(py))));
+        Vec nh = px * T1 + py * T2 + pz * wh;
+        return Normalize(Vec(ax * nh.x, ay * nh.y, std::max<Float>(1e-6f, nh.z)));
+    }
+    void Regularize() {
+        if (ax < 0.3f) ax = Clamp(2 * ax, 0.1f, 0.3f);
+        if (ay < 0.3f) ay = Clamp(2 * ay, 0.1f, 0.3f);
+    }
+};
+
+static Float FrDielectric(Float cosI, Float eta) {
+    cosI = Clamp(cosI, -1, 1);
+    if (cosI < 0) {
+        eta = 1 / eta;
+        cosI = -cosI;
+    }
+    Float sin2T = (1 - Sqr(cosI)) / Sqr(eta);
+    if (sin2T >= 1) return 1.f;
+    Float cosT = SafeSqrt(1 - sin2T);
+    Float rParl = (eta * cosI - cosT) / (eta * cosI + cosT);
+    Float rPerp = (cosI - eta * cosT) / (cosI + eta * cosT);
+    return (Sqr(rParl) + Sqr(rPerp)) / 2;
+}
+
+struct Complex {
+    Float re, im;
+    Complex(Float r, Float i = 0) : re(r), im(i) {}
+    Complex operator+(Complex z) const { return {re + z.re, im + z.im}; }
+    Complex operator-(Complex z) const { return {re - z.re, im - z.im}; }
+    Complex operator*(Complex z) const { return {re * z.re - im * z.im, re * z.im + im * z.re}; }
+    Complex operator/(Complex z) const {
+        Float scale = 1 / (z.re * z.re + z.im * z.im);
+        return {scale * (re * z.re + im * z.im), scale * (im * z.re - re * z.im)};
+    }
+};
+static inline Float Norm(Complex z) { return z.re * z.re + z.im * z.im; }
+static Complex Sqrt(Complex z) {
+    Float n = std::sqrt(Norm(z)), t1 = std::sqrt(Float(.5) * (n + std::abs(z.re))), t2 = Float(.5) * z.im / t1;
+    if (n == 0) return 0;
+    if (z.re >= 0) return {t1, t2};
+    return {std::abs(t2), std::copysign(t1, z.im)};
+}
+static Float FrComplex(Float cosI, Complex eta) {
+    cosI = Clamp(cosI, 0, 1);
+    Float sin2I = 1 - Sqr(cosI);
+    Complex sin2T = Complex(sin2I) / (eta * eta);
+    Complex cosT = Sqrt(Complex(1) - sin2T);
+    Complex rParl = (eta * Complex(cosI) - cosT) / (eta * Complex(cosI) + cosT);
+    Complex rPerp = (Complex(cosI) - eta * cosT) / (Complex(cosI) + eta * cosT);
+    return (Norm(rParl) + Norm(rPerp)) / 2;
+}
+static bool Refract(Vec wi, Vec n, Float eta, Float *etap, Vec *wt) {
+    Float cosI = DotN(n, wi);
+    if (cosI < 0) {
+        eta = 1 / eta;
+        cosI = -cosI;
+        n = -n;
+    }
+    Float sin2T = std::max<Float>(0, 1 - Sqr(cosI)) / Sqr(eta);
+    if (sin2T >= 1) return false;
+    Float cosT = std::sqrt(1 - sin2T);
+    *wt = -wi / eta + (cosI / eta - cosT) * n;
+    *etap = eta;
+    return true;
+}
+static inline Vec Reflect(Vec wo, Vec n) { return -wo + 2 * Dot(wo, n) * n; }
+
+struct BxDF {
+    int type = 0;  // 0 diffuse, 1 dielectric, 2 conductor
+    Spectrum R;
+    Float eta = 1;
+    TRDistribution mf;
+    Spectrum etaS, kS;
+
+    int Flags() const {
+        if (type == 0) return R ? (BxR | BxDiffuse) : 0;
+        int lobe = mf.Smooth() ? BxSpecular : BxGlossy;
+        if (type == 1) return (eta == 1 ? BxT : (BxR | BxT)) | lobe;
+        return BxR | lobe;
+    }
+    Spectrum FrC(Float cosI) const {
+        Spectrum r;
+        for (int i = 0; i < NS; ++i) r[i] = FrComplex(cosI, Complex(etaS[i], kS[i]));
+        return r;
+    }
+    bool Sample_f(Vec wo, Float uc, Float u0, Float u1, BSDFSample *bs) const {
+        if (type == 0) {
+            Vec wi = SampleCosineHemisphere(u0, u1);
+            if (wo.z < 0) wi.z *= -1;
+            *bs = BSDFSample{R * InvPi, wi, std::abs(wi.z) * InvPi, BxR | BxDiffuse, 1};
+            return true;
+        }
+        if (type == 2) {
+            if (mf.Smooth()) {
+                Vec wi(-wo.x, -wo.y, wo.z);
+                *bs = BSDFSample{FrC(std::abs(wi.z)) / std::abs(wi.z), wi, 1, BxR | BxSpecular, 1};
+                return true;
+            }
+            if (wo.z == 0) return false;
+            Vec wm = mf.Sample_wm(wo, u0, u1);
+            Vec wi = Reflect(wo, wm);
+            if (!SameHemisphere(wo, wi)) return false;
+            Float pdf = mf.PDF(wo, wm) / (4 * AbsDot(wo, wm));
+            Float co = std::abs(wo.z), ci = std::abs(wi.z);
+            if (ci == 0 || co == 0) return false;
+            Spectrum F = FrC(AbsDot(wo, wm));
+            *bs = BSDFSample{F * mf.D(wm) * mf.G(wo, wi) / (4 * ci * co), wi, pdf, BxR | BxGlossy, 1};
+            return true;
+        }
+        if (eta == 1 || mf.Smooth()) {
+            Float R_ = FrDielectric(wo.z, eta), T_ = 1 - R_;
+            if (R_ == 0 && T_ == 0) return false;
+            if (uc < R_ / (R_ + T_)) {
+                Vec wi(-wo.x, -wo.y, wo.z);
+                *bs = BSDFSample{Spectrum(R_ / std::abs(wi.z)), wi, R_ / (R_ + T_), BxR | BxSpecular, 1};
+                return true;
+            }
+            Vec wi;
+            Float etap;
+            if (!Refract(wo, Vec(0, 0, 1), eta, &etap, &wi)) return false;
+            Spectrum ft(T_ / std::abs(wi.z));
+            ft = ft / Sqr(etap);
+            *bs = BSDFSample{ft, wi, T_ / (R_ + T_), BxT | BxSpecular, etap};
+            return true;
+        }
+        Vec wm = mf.Sample_wm(wo, u0, u1);
+        Float R_ = FrDielectric(Dot(wo, wm), eta), T_ = 1 - R_;
+        if (R_ == 0 && T_ == 0) return false;
+        if (uc < R_ / (R_ + T_)) {
+            Vec wi = Reflect(wo, wm);
+            if (!SameHemisphere(wo, wi)) return false;
+            Float pdf = mf.PDF(wo, wm) / (4 * AbsDot(wo, wm)) * R_ / (R_ + T_);
+            Spectrum f(mf.D(wm) * mf.G(wo, wi) * R_ / (4 * wi.z * wo.z));
+            *bs = BSDFSample{f, wi, pdf, BxR | BxGlossy, 1};
+            return true;
+        }
+        Float etap;
+        Vec wi;
+        bool tir = !Refract(wo, wm, eta, &etap, &wi);
+        if (SameHemisphere(wo, wi) || wi.z == 0 || tir) return false;
+        Float denom = Sqr(Dot(wi, wm) + Dot(wo, wm) / etap);
+        Float dwm_dwi = AbsDot(wi, wm) / denom;
+        Float pdf = mf.PDF(wo, wm) * dwm_dwi * T_ / (R_ + T_);
+        Spectrum ft(T_ * mf.D(wm) * mf.G(wo, wi) * std::abs(Dot(wi, wm) * Dot(wo, wm) / (wi.z * wo.z * denom)));
+        ft = ft / Sqr(etap);
+        *bs = BSDFSample{ft, wi, pdf, BxT | BxGlossy, etap};
+        return true;
+    }
+    // the generalized half vector of a dielectric pair, or false (f = pdf = 0)
+    bool DielectricHalf(Vec wo, Vec wi, Vec *wm, Float *etap, bool *reflect) const {
+        Float co = wo.z, ci = wi.z;
+        *reflect = ci * co > 0;
+        *etap = 1;
+        if (!*reflect) *etap = co > 0 ? eta : (1 / eta);
+        Vec h = wi * *etap + wo;
+        if (ci == 0 || co == 0 || LengthSquared(h) == 0) return false;
+        h = Normalize(h);
+        if (h.z < 0) h = -h;  // FaceForward(wm, (0,0,1))
+        if (Dot(h, wi) * ci < 0 || Dot(h, wo) * co < 0) return false;
+        *wm = h;
+        return true;
+    }
+    Spectrum f(Vec wo, Vec wi) const {
+        if (type == 0) return SameHemisphere(wo, wi) ? R * InvPi : Spectrum(0.f);
+        if (type == 2) {
+            if (!SameHemisphere(wo, wi) || mf.Smooth()) return Spectrum(0.f);
+            Float co = std::abs(wo.z), ci = std::abs(wi.z);
+            if (ci == 0 || co == 0) return Spectrum(0.f);
+            Vec wm = wi + wo;
+            if (LengthSquared(wm) == 0) return Spectrum(0.f);
+            wm = Normalize(wm);
+            Spectrum F = FrC(AbsDot(wo, wm));
+            return F * mf.D(wm) * mf.G(wo, wi) / (4 * ci * co);
+        }
+        if (eta == 1 || mf.Smooth()) return Spectrum(0.f);
+        Vec wm;
+        Float etap;
+        bool reflect;
+        if (!DielectricHalf(wo, wi, &wm, &etap, &reflect)) return Spectrum(0.f);
+        Float F = FrDielectric(Dot(wo, wm), eta);
+        if (reflect) return Spectrum(mf.D(wm) * mf.G(wo, wi) * F / std::abs(4 * wi.z * wo.z));
+        Float denom = Sqr(Dot(wi, wm) + Dot(wo, wm) / etap) * wi.z * wo.z;
+        Float ft = mf.D(wm) * (1 - F) * mf.G(wo, wi) * std::abs(Dot(wi, wm) * Dot(wo, wm) / denom);
+        ft /= Sqr(etap);
+        return Spectrum(ft);
+    }
+    Float PDF(Vec wo, Vec wi) const {
+        if (type == 0) return SameHemisphere(wo, wi) ? std::abs(wi.z) * InvPi : 0;
+        if (type == 2) {
+            if (!SameHemisphere(wo, wi) || mf.Smooth()) return 0;
+            Vec wm = wo + wi;
+            if (LengthSquared(wm) == 0) return 0;
+            wm = Normalize(wm);
+            if (wm.z < 0) wm = -wm;
+            return mf.PDF(wo, wm) / (4 * AbsDot(wo, wm));
+        }
+        if (eta == 1 || mf.Smooth()) return 0;
+        Vec wm;
+        Float etap;
+        bool reflect;
+        if (!DielectricHalf(wo, wi, &wm, &etap, &reflect)) return 0;
+        Float R_ = FrDielectric(Dot(wo, wm), eta), T_ = 1 - R_;
+        if (R_ == 0 && T_ == 0) return 0;
+        if (reflect) return mf.PDF(wo, wm) / (4 * AbsDot(wo, wm)) * R_ / (R_ + T_);
+        Float denom = Sqr(Dot(wi, wm) + Dot(wo, wm) / etap);
+        return mf.PDF(wo, wm) * (AbsDot(wi, wm) / denom) * T_ / (R_ + T_);
+    }
+};
+
+// PiecewiseLinearSpectrum::operator() (util/spectrum.cpp:68-78)
+static Float PLEval(const float *lam, const float *val, int n, Float l) {
+    if (n == 0 || l < lam[0] || l > lam[n - 1]) return 0;
+    // FindInterval (util/math.h:509-520): binary search for the last lam[i] <= l, i <= n-2
+    int size = n - 2, first = 1;
+    while (size > 0) {
+        int half = size >> 1, middle = first + half;
+        bool pr = lam[middle] <= l;
+        first = pr ? middle + 1 : first;
+        size = pr ? size - (half + 1) : half;
+    }
+    int o = std::min(std::max(first - 1, 0), n - 2);
+    Float t = (l - lam[o]) / (lam[o + 1] - lam[o]);
+    return Lerp(t, val[o], val[o + 1]);
+}
+
 // ---------------------------------------------------------------- integrator
 struct Renderer {
     Scene S;
@@ -1109,7 +1399,7 @@ struct Renderer {
             rd = dd;
         }
         Spectrum L(0.f), beta(1.f), r_u(1.f), r_l(1.f);
-        bool specularBounce = false;
+        bool specularBounce = false, anyNonSpecular = false;
         Float etaScale = 1;
         Vec prevP, prevErr, prevN, prevNs;
         for (int depth = 0;; ++depth) {
@@ -1156,50 +1446,75 @@ struct Renderer {
             Float iUc = h2.Get1D(), iU0, iU1;
             h2.Get2D(&iU0, &iU1);
             Float rr = h2.Get1D();
-            (void)iUc;
-            // DiffuseMaterial
+            // Material::GetBxDF (materials.h:466-471 diffuse, :182-204 dielectric, :491-511 conductor)
             int mat = f->tri_material[prim];
             const float *mc = f->material_coeffs + 4 * mat;
-            Spectrum R;
-            for (int i = 0; i < NS; ++i) {
-                Float r = f->material_constant[mat] ? mc[3] : Sigmoid(mc[0], mc[1], mc[2], lambda.lambda[i]);
-                R[i] = Clamp(r, 0, 1);
+            BxDF bx;
+            bx.type = f->material_type[mat];
+            if (bx.type == 0) {
+                for (int i = 0; i < NS; ++i) {
+                    Float r = f->material_constant[mat] ? mc[3] : Sigmoid(mc[0], mc[1], mc[2], lambda.lambda[i]);
+                    bx.R[i] = Clamp(r, 0, 1);
+                }
+            } else {
+                const float *mp = f->material_params + 4 * mat;
+                bx.mf.ax = mp[0];  // alphas arrive remapped and clamped (TrowbridgeReitz ctor)
+                bx.mf.ay = mp[1];
+                bx.eta = mp[2] == 0 ? 1.f : mp[2];
+                if (bx.type == 2) {
+                    int es = f->material_spectra[2 * mat], ks = f->material_spectra[2 * mat + 1];
+                    for (int i = 0; i < NS; ++i) {
+                        Float l = lambda.lambda[i];
+                        if (es >= 0) {
+                            const int a = f->pl_offsets[es], b = f->pl_offsets[ks];
+                            bx.etaS[i] = PLEval(f->pl_lambda + a, f->pl_value + a, f->pl_offsets[es + 1] - a, l);
+                            bx.kS[i] = PLEval(f->pl_lambda + b, f->pl_value + b, f->pl_offsets[ks + 1] - b, l);
+                        } else {
+                            Float r = Clamp(Sigmoid(mc[0], mc[1], mc[2], l), 0, .9999f);
+                            bx.etaS[i] = 1;
+                            bx.kS[i] = 2 * std::sqrt(r) / std::sqrt(std::max<Float>(0, 1 - r));
+                        }
+                    }
+                }
+                if (f->regularize && anyNonSpecular) bx.mf.Regularize();
             }
             Vec fx_ = Normalize(si.dpdu), fz = si.ns, fy_ = Cross(fz, fx_);
             auto toLocal = [&](Vec v) { return Vec(Dot(v, fx_), Dot(v, fy_), Dot(v, fz)); };
             auto fromLocal = [&](Vec v) { return fx_ * v.x + fy_ * v.y + fz * v.z; };
             Vec woL = toLocal(si.wo);
-            bool nonSpecular = bool(R);
+            const int flags = bx.Flags();
             Spectrum oldBeta = beta;
-            bool haveNext = false;
+            bool haveNext = false, nextSpecular = false;
             Vec nextO, nextD;
             Spectrum nb;
             Spectrum nrl;
-            if (woL.z != 0 && nonSpecular) {
-                Vec wiL = SampleCosineHemisphere(iU0, iU1);
-                if (woL.z < 0) wiL.z *= -1;
-                Float pdf = std::abs(wiL.z) * InvPi;
-                Spectrum fv = R * InvPi;
-                if (fv && pdf != 0 && wiL.z != 0) {
-                    Vec wi = fromLocal(wiL);
-                    nb = beta * fv * AbsDotN(si.ns, wi) / pdf;
-                    nrl = r_u / pdf;
-                    Spectrum rrBeta = nb * etaScale / r_u.Average();
-                    if (rrBeta.Max() < 1 && depth >= 1) {
-                        Float q = std::max<Float>(0, 1 - rrBeta.Max());
-                        if (rr < q) nb = Spectrum(0.f);
-                        else nb = nb / (1 - q);
-                    }
-                    if (nb) {
-                        haveNext = true;
-                        nextO = OffsetRayOrigin(si.p, si.err, si.n, wi);
-                        nextD = wi;
-                    }
+            Float nextEtaScale = etaScale;
+            // BSDF::Sample_f (bsdf.h:89-116), then surfscatter.cpp:183-250
+            BSDFSample bs;
+            if (woL.z != 0 && flags && bx.Sample_f(woL, iUc, iU0, iU1, &bs) && bs.f && bs.pdf != 0 && bs.wi.z != 0) {
+                Vec wi = fromLocal(bs.wi);
+                nb = beta * bs.f * AbsDotN(si.ns, wi) / bs.pdf;
+                nrl = r_u / bs.pdf;
+                if (bs.flags & BxT) nextEtaScale *= Sqr(bs.eta);
+                Spectrum rrBeta = nb * nextEtaScale / r_u.Average();
+                if (rrBeta.Max() < 1 && depth >= 1) {
+                    Float q = std::max<Float>(0, 1 - rrBeta.Max());
+                    if (rr < q) nb = Spectrum(0.f);
+                    else nb = nb / (1 - q);
+                }
+                if (nb) {
+                    haveNext = true;
+                    nextSpecular = bs.flags & BxSpecular;
+                    nextO = OffsetRayOrigin(si.p, si.err, si.n, wi);
+                    nextD = wi;
                 }
             }
-            // light sampling + shadow ray
-            if (nonSpecular) {
-                Vec cp = OffsetRayOrigin(si.p, si.err, si.n, si.wo);
+            // light sampling + shadow ray (surfscatter.cpp:252-326), IsNonSpecular(flags)
+            if (flags & (BxDiffuse | BxGlossy)) {
+                Vec cp = si.p;
+                bool refl = flags & BxR, trans = flags & BxT;
+                if (refl && !trans) cp = OffsetRayOrigin(si.p, si.err, si.n, si.wo);
+                else if (trans && refl) cp = OffsetRayOrigin(si.p, si.err, si.n, -si.wo);
                 int li;
                 Float lpmf;
                 if (lights.Sample(cp, si.ns, dUc, &li, &lpmf) && li < f->n_area_lights) {
@@ -1212,11 +1527,11 @@ struct Renderer {
                         if (f->light_two_sided[li] || DotN(ss.n, -wi) >= 0) Le = LightL(li, lambda);
                         if (Le) {
                             Vec wiL = toLocal(wi);
-                            Spectrum fv = (woL.z != 0 && woL.z * wiL.z > 0) ? R * InvPi : Spectrum(0.f);
+                            Spectrum fv = woL.z != 0 ? bx.f(woL, wiL) : Spectrum(0.f);  // BSDF::f (bsdf.h:60-70)
                             if (fv) {
                                 Spectrum b2 = oldBeta * fv * AbsDotN(si.ns, wi);
                                 Float lightPDF = ss.pdf * lpmf;
-                                Float bsdfPDF = (woL.z != 0 && woL.z * wiL.z > 0) ? std::abs(wiL.z) * InvPi : 0;
+                                Float bsdfPDF = woL.z != 0 ? bx.PDF(woL, wiL) : 0;
                                 Spectrum ru = r_u * bsdfPDF, rl = r_u * lightPDF;
                                 Spectrum Ld = b2 * Le;
                                 Vec pf = OffsetRayOrigin(si.p, si.err, si.n, ss.p - si.p);
@@ -1232,7 +1547,9 @@ struct Renderer {
             if (!haveNext) break;
             beta = nb;
             r_l = nrl;
-            specularBounce = false;
+            specularBounce = nextSpecular;
+            anyNonSpecular = anyNonSpecular || !nextSpecular;
+            etaScale = nextEtaScale;
             prevP = si.p;
             prevErr = si.err;
             prevN = si.n;
@@ -1418,6 +1735,72 @@ float oracle_halton(int xres, int yres, int seed, int px, int py, int sampleInde
     if (dim == -1) return a;
     if (dim == -2) return b;
     return s.Sample(std::max(2, dim));
+}
+
+void oracle_trowbridge(const float *in, float *out) {
+    TRDistribution d(in[0], in[1]);
+    Vec wo(in[2], in[3], in[4]), wi(in[5], in[6], in[7]), wm(in[8], in[9], in[10]);
+    Vec sw = d.Sample_wm(wo, in[11], in[12]);
+    TRDistribution r = d;
+    r.Regularize();
+    Float dwm = d.G1(wo) / std::abs(wo.z) * d.D(wm) * AbsDot(wo, wm);  // D(w, wm)
+    float v[14] = {d.ax, d.ay, (float)d.Smooth(), d.D(wm), dwm, d.Lambda(wo), d.G1(wo), d.G(wo, wi), d.PDF(wo, wm),
+                   sw.x, sw.y, sw.z, r.ax, r.ay};
+    std::memcpy(out, v, sizeof v);
+}
+
+void oracle_fresnel(const float *in, float *out) {
+    Vec wi(in[4], in[5], in[6]), n(in[7], in[8], in[9]);
+    Float etap = 0;
+    Vec wt(0, 0, 0);
+    bool ok = Refract(wi, n, in[1], &etap, &wt);
+    Vec rf = Reflect(wi, n);
+    float v[10] = {FrDielectric(in[0], in[1]), FrComplex(in[0], Complex(in[2], in[3])), (float)ok, etap, wt.x, wt.y,
+                   wt.z, rf.x, rf.y, rf.z};
+    std::memcpy(out, v, sizeof v);
+}
+
+// PiecewiseLinearSpectrum::FromInterleaved(samples, false) (util/spectrum.cpp:133-163) then
+// operator() at each lambda
+void oracle_named_spectrum(const float *interleaved, int nValues, const float *lambda, int n, float *out) {
+    std::vector<float> lam, val;
+    if (interleaved[0] > LambdaMin) {
+        lam.push_back(LambdaMin - 1);
+        val.push_back(interleaved[1]);
+    }
+    for (int i = 0; i + 1 < nValues; i += 2) {
+        lam.push_back(interleaved[i]);
+        val.push_back(interleaved[i + 1]);
+    }
+    if (lam.back() < LambdaMax) {
+        lam.push_back(LambdaMax + 1);
+        val.push_back(val.back());
+    }
+    for (int i = 0; i < n; ++i) out[i] = PLEval(lam.data(), val.data(), (int)lam.size(), lambda[i]);
+}
+
+void oracle_bxdf(int type, const float *params, const float *eta31, const float *k31, const float *wo3,
+                 const float *wi3, const float *u3, float *out) {
+    BxDF bx;
+    bx.type = type;
+    bx.mf.ax = params[0];
+    bx.mf.ay = params[1];
+    bx.eta = params[2];
+    for (int i = 0; i < NS; ++i) {
+        bx.etaS[i] = eta31[i];
+        bx.kS[i] = k31[i];
+    }
+    Vec wo(wo3[0], wo3[1], wo3[2]), wi(wi3[0], wi3[1], wi3[2]);
+    std::fill(out, out + 70, 0.f);
+    BSDFSample bs;
+    if (bx.Sample_f(wo, u3[0], u3[1], u3[2], &bs)) {
+        float v[7] = {1, bs.wi.x, bs.wi.y, bs.wi.z, bs.pdf, (float)bs.flags, bs.eta};
+        std::memcpy(out, v, sizeof v);
+        for (int i = 0; i < NS; ++i) out[7 + i] = bs.f[i];
+    }
+    Spectrum f = bx.f(wo, wi);
+    for (int i = 0; i < NS; ++i) out[38 + i] = f[i];
+    out[69] = bx.PDF(wo, wi);
 }
 
 }  // extern "C"

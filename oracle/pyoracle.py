@@ -36,6 +36,10 @@ def lib():
         _lib.oracle_spherical_triangle.argtypes = [vp, vp, vp, vp]
         _lib.oracle_triangle_sample.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, vp]
         _lib.oracle_offset_ray_origin.argtypes = [vp, vp, vp, vp, vp]
+        _lib.oracle_trowbridge.argtypes = [vp, vp]
+        _lib.oracle_fresnel.argtypes = [vp, vp]
+        _lib.oracle_named_spectrum.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, vp]
+        _lib.oracle_bxdf.argtypes = [ctypes.c_int] + [vp] * 7
         _lib.oracle_render.argtypes = [vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, vp]
     return _lib
@@ -83,3 +87,32 @@ def film_to_rgb(film, m3x3):
     rgb = film[:3] / np.where(w == 0, 1, w)
     m = np.asarray(m3x3, dtype=np.float64).reshape(3, 3)
     return np.einsum("ij,jhw->hwi", m, rgb).astype(np.float32)
+
+
+def trowbridge(in13):
+    i = f32(in13)
+    out = np.zeros(14, np.float32)
+    lib().oracle_trowbridge(i.ctypes.data, out.ctypes.data)
+    return out
+
+
+def fresnel(in10):
+    i = f32(in10)
+    out = np.zeros(10, np.float32)
+    lib().oracle_fresnel(i.ctypes.data, out.ctypes.data)
+    return out
+
+
+def named_spectrum(interleaved, lambdas):
+    src, lam = f32(interleaved), f32(lambdas)
+    out = np.zeros(lam.size, np.float32)
+    lib().oracle_named_spectrum(src.ctypes.data, src.size, lam.ctypes.data, lam.size, out.ctypes.data)
+    return out
+
+
+def bxdf(bxdf_type, params3, wo, wi, u3, eta31=None, k31=None):
+    arrs = [f32(params3), f32(eta31 if eta31 is not None else np.ones(31)),
+            f32(k31 if k31 is not None else np.zeros(31)), f32(wo), f32(wi), f32(u3)]
+    out = np.zeros(70, np.float32)
+    lib().oracle_bxdf(int(bxdf_type), *[a.ctypes.data for a in arrs], out.ctypes.data)
+    return out

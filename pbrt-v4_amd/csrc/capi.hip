@@ -20,6 +20,8 @@ hipError_t LaunchCamera(const DeviceScene &S, const PathState &st, int nActive, 
 hipError_t LaunchClosest(const DeviceScene &S, const PathState &st, int depth, int maxCount, int timed,
                          hipStream_t s);
 hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
+hipError_t LaunchShadeMicrofacet(const DeviceScene &S, const PathState &st, int depth, int type, int maxCount,
+                                 hipStream_t s);
 hipError_t LaunchEscaped(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
 hipError_t LaunchEmissive(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
 hipError_t LaunchShadow(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
@@ -44,8 +46,9 @@ static int Fail(const std::string &msg) {
 struct pbrt_scene {
     SceneDesc desc;
     // flattened copies for pbrt_scene_get_flat
-    std::vector<float> verts, matCoeffs, lightScale, infScale, dense, sensor, nodeBounds;
-    std::vector<int32_t> tris, lightPrim, lightSpectrum, lightTwoSided, infSpectrum, matConstant, nodeInfo;
+    std::vector<float> verts, matCoeffs, lightScale, infScale, dense, sensor, nodeBounds, matParams, plLambda, plValue;
+    std::vector<int32_t> tris, lightPrim, lightSpectrum, lightTwoSided, infSpectrum, matConstant, nodeInfo, matType,
+        matSpectra, plOffsets;
     void Flatten() {
         const SceneDesc &s = desc;
         verts.clear();
@@ -58,9 +61,23 @@ struct pbrt_scene {
         for (auto &t : s.tris) tris.insert(tris.end(), t.begin(), t.end());
         matCoeffs.clear();
         matConstant.clear();
+        matType.clear();
+        matParams.clear();
+        matSpectra.clear();
         for (auto &m : s.materials) {
             matCoeffs.insert(matCoeffs.end(), {m.c0, m.c1, m.c2, m.constantValue});
             matConstant.push_back(m.constant ? 1 : 0);
+            matType.push_back(m.type);
+            matParams.insert(matParams.end(), {m.alphaX, m.alphaY, m.eta, 0.f});
+            matSpectra.insert(matSpectra.end(), {m.etaSpec, m.kSpec});
+        }
+        plOffsets.assign(1, 0);
+        plLambda.clear();
+        plValue.clear();
+        for (auto &sp : s.plSpectra) {
+            plLambda.insert(plLambda.end(), sp.lambda.begin(), sp.lambda.end());
+            plValue.insert(plValue.end(), sp.value.begin(), sp.value.end());
+            plOffsets.push_back((int32_t)plLambda.size());
         }
         lightPrim.clear();
         lightScale.clear();
@@ -126,7 +143,8 @@ struct pbrt_context {
     DevBuf<BVH8Node> nodes;
     DevBuf<float> triVerts, matCoeffs, lightScale, lightArea, infScale, dense, sensor;
     DevBuf<int> primMaterial, primLight, matConstant, lightPrim, lightSpectrum, lightTwoSided, infSpectrum;
-    DevBuf<int> primOrig;
+    DevBuf<int> primOrig, matType, matSpectra, plOffsets;
+    DevBuf<float> matParams, plLambda, plValue;
     DevBuf<uint8_t> primFlip;
     DevBuf<uint32_t> lightBitTrail, permOffset, permNDigits, permBase;
     DevBuf<uint16_t> perm;
@@ -196,6 +214,28 @@ static void BuildDevice(pbrt_context *c) {
     }
     c->matCoeffs.Upload(mc);
     c->matConstant.Upload(mk);
+    {
+        static_assert(kNumMatTypes == kMatNumTypes, "material type count");
+        std::vector<int> mt, msp, po{0};
+        std::vector<float> mp, pll, plv;
+        for (auto &m : s.materials) {
+            mt.push_back(m.type);
+            mp.insert(mp.end(), {m.alphaX, m.alphaY, m.eta, 0.f});
+            msp.insert(msp.end(), {m.etaSpec, m.kSpec});
+        }
+        for (auto &sp : s.plSpectra) {
+            pll.insert(pll.end(), sp.lambda.begin(), sp.lambda.end());
+            plv.insert(plv.end(), sp.value.begin(), sp.value.end());
+            po.push_back((int)pll.size());
+        }
+        if (pll.empty()) pll.push_back(0), plv.push_back(0);
+        c->matType.Upload(mt);
+        c->matParams.Upload(mp);
+        c->matSpectra.Upload(msp);
+        c->plOffsets.Upload(po);
+        c->plLambda.Upload(pll);
+        c->plValue.Upload(plv);
+    }
     std::vector<int> lp, ls, lt;
     std::vector<float> lsc, la;
     for (auto &l : s.areaLights) {
@@ -304,6 +344,15 @@ static void BuildDevice(pbrt_context *c) {
     S.matCoeffs = (const float4 *)c->matCoeffs.p;
     S.matConstant = c->matConstant.p;
     S.nMaterials = (int)s.materials.size();
+    S.matType = c->matType.p;
+    S.matParams = (const float4 *)c->matParams.p;
+    S.matSpectra = c->matSpectra.p;
+    S.plOffsets = c->plOffsets.p;
+    S.plLambda = c->plLambda.p;
+    S.plValue = c->plValue.p;
+    S.matTypeMask = 0;
+    for (auto &m : s.materials) S.matTypeMask |= 1 << m.type;
+    S.regularize = s.regularize ? 1 : 0;
     S.nAreaLights = (int)s.areaLights.size();
     S.lightPrim = c->lightPrim.p;
     S.lightScale = c->lightScale.p;
@@ -424,8 +473,8 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
     if (N <= c->maxPaths) return;
     // floats: records 2 x (beta 31, ray 6, lambda0, rl, etaScale) = 80, hitB 2x4, shadowRay 6,
     // shadowL 3, L 3, filterW 1 = 101; ints: records 2 x (flags, pixel, prevIdx), hitPrim 2,
-    // shadowPixel, matQ, escQ, emitQ = 12
-    const int nf = 101, ni = 12;
+    // shadowPixel, matQ x 3 (per material type), escQ, emitQ = 14
+    const int nf = 101, ni = 14;
     const int64_t capS = ((N + kShards - 1) / kShards + 256 + 63) / 64 * 64;
     const int64_t NR = capS * kShards;  // record stride
     // per pixel-sample arrays (L, filterW) use N; the rest NR (>= N)
@@ -465,7 +514,7 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
     st.L = take(3);
     st.filterW = take(1);
     st.shadowPixel = takei(1);
-    st.matQ = takei(1);
+    for (int t = 0; t < kNumMatTypes; ++t) st.matQ[t] = takei(1);
     st.escQ = takei(1);
     st.emitQ = takei(1);
     st.counters = ip;
@@ -539,7 +588,12 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
                 if (s.infiniteLights.size()) HIPCHECK(LaunchEscaped(c->S, st, depth, (int)nActive, c->stream));
                 if (s.areaLights.size()) HIPCHECK(LaunchEmissive(c->S, st, depth, (int)nActive, c->stream));
                 if (depth == s.maxDepth) break;
-                HIPCHECK(LaunchShadeDiffuse(c->S, st, depth, (int)nActive, c->stream));
+                // EvaluateMaterialsAndBSDFs: one launch per material type present (surfscatter.cpp:39-55)
+                if (c->S.matTypeMask & (1 << kMatDiffuseT))
+                    HIPCHECK(LaunchShadeDiffuse(c->S, st, depth, (int)nActive, c->stream));
+                for (int t = kMatDielectricT; t < kNumMatTypes; ++t)
+                    if (c->S.matTypeMask & (1 << t))
+                        HIPCHECK(LaunchShadeMicrofacet(c->S, st, depth, t, (int)nActive, c->stream));
                 HIPCHECK(LaunchShadow(c->S, st, depth, (int)nActive, c->stream));
             }
             HIPCHECK(LaunchFilm(c->S, st, nS, c->stream));
@@ -674,6 +728,14 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
     f->zs_randomize = s.zsRandomize;
     f->zs_log2_spp = s.zsLog2SamplesPerPixel;
     f->zs_nbase4_digits = s.zsNBase4Digits;
+    f->material_type = scene->matType.data();
+    f->material_params = scene->matParams.data();
+    f->material_spectra = scene->matSpectra.data();
+    f->n_pl_spectra = (int)s.plSpectra.size();
+    f->pl_offsets = scene->plOffsets.data();
+    f->pl_lambda = scene->plLambda.data();
+    f->pl_value = scene->plValue.data();
+    f->regularize = s.regularize ? 1 : 0;
     return 0;
 }
 
@@ -888,6 +950,82 @@ int pbrt_debug_zsobol(const pbrt_scene *scene, int px, int py, int sampleIndex, 
     } catch (const std::exception &e) {
         return Fail(e.what());
     }
+}
+
+int pbrt_debug_trowbridge(const float *in, float *out) {
+    if (!in || !out) return Fail("null argument");
+    TrowbridgeReitz d = TrowbridgeReitz::Make(in[0], in[1]);
+    V3 wo(in[2], in[3], in[4]), wi(in[5], in[6], in[7]), wm(in[8], in[9], in[10]);
+    V3 sw = d.SampleWm(wo, in[11], in[12]);
+    TrowbridgeReitz r = d;
+    r.Regularize();
+    const float v[14] = {d.ax,        d.ay,      (float)d.EffectivelySmooth(), d.D(wm), d.D(wo, wm), d.Lambda(wo),
+                         d.G1(wo),    d.G(wo, wi), d.PDF(wo, wm),             sw.x,    sw.y,        sw.z,
+                         r.ax,        r.ay};
+    memcpy(out, v, sizeof v);
+    return 0;
+}
+
+int pbrt_debug_fresnel(const float *in, float *out) {
+    if (!in || !out) return Fail("null argument");
+    V3 wi(in[4], in[5], in[6]), n(in[7], in[8], in[9]);
+    float etap = 0;
+    V3 wt(0, 0, 0);
+    bool ok = Refract(wi, n, in[1], &etap, &wt);
+    V3 rf = Reflect(wi, n);
+    const float v[10] = {FrDielectric(in[0], in[1]), FrComplex(in[0], in[2], in[3]), (float)ok, etap, wt.x, wt.y,
+                         wt.z, rf.x, rf.y, rf.z};
+    memcpy(out, v, sizeof v);
+    return 0;
+}
+
+int pbrt_debug_named_spectrum(const char *name, const float *lambda, int n, float *out) {
+    try {
+        if (!name || !lambda || !out) return Fail("null argument");
+        PLSpectrumDesc d = NamedPiecewiseLinear(name);
+        for (int i = 0; i < n; ++i)
+            out[i] = PiecewiseLinearEval(d.lambda.data(), d.value.data(), (int)d.lambda.size(), lambda[i]);
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_debug_bxdf(int type, const float *params, const float *eta31, const float *k31, const float *wo3,
+                    const float *wi3, const float *u3, float *out) {
+    if (!params || !wo3 || !wi3 || !u3 || !out) return Fail("null argument");
+    if (type == kMatConductor && (!eta31 || !k31)) return Fail("conductor needs eta and k");
+    if (type != kMatDielectric && type != kMatConductor) return Fail("type must be 1 (dielectric) or 2 (conductor)");
+    const TrowbridgeReitz tr{params[0], params[1]};
+    const float eta = params[2];
+    const V3 wo(wo3[0], wo3[1], wo3[2]), wi(wi3[0], wi3[1], wi3[2]);
+    memset(out, 0, 70 * sizeof(float));
+    if (type == kMatDielectric) {
+        BxSample bs = DielectricSample(eta, tr, wo, u3[0], u3[1], u3[2]);
+        if (bs.ok) {
+            const float v[7] = {1, bs.wi.x, bs.wi.y, bs.wi.z, bs.pdf, (float)bs.flags, bs.etap};
+            memcpy(out, v, sizeof v);
+            for (int i = 0; i < kNSpectrumSamples; ++i) out[7 + i] = bs.f;
+        }
+        float pdf;
+        float f = DielectricEval(eta, tr, wo, wi, &pdf);
+        for (int i = 0; i < kNSpectrumSamples; ++i) out[38 + i] = f;
+        out[69] = pdf;
+    } else {
+        ConductorTerms ct = ConductorSample(tr, wo, u3[1], u3[2]);
+        if (ct.ok) {
+            const int flags = kBxReflection | (ct.specular ? kBxSpecular : kBxGlossy);
+            const float v[7] = {1, ct.wi.x, ct.wi.y, ct.wi.z, ct.pdf, (float)flags, 1};
+            memcpy(out, v, sizeof v);
+            for (int i = 0; i < kNSpectrumSamples; ++i) out[7 + i] = ConductorF(ct, eta31[i], k31[i]);
+        }
+        ConductorTerms ce = ConductorEval(tr, wo, wi);
+        if (ce.ok) {
+            for (int i = 0; i < kNSpectrumSamples; ++i) out[38 + i] = ConductorF(ce, eta31[i], k31[i]);
+            out[69] = ce.pdf;
+        }
+    }
+    return 0;
 }
 
 int pbrt_debug_queue_counts(pbrt_context *ctx, int32_t *counts, int n) {

@@ -675,6 +675,289 @@ PHD uint64_t InverseRadicalInverse(uint64_t inverse, int base, int nDigits) {
     return index;
 }
 
+// ---------------------------------------------------------------- microfacet BxDFs
+// TrowbridgeReitzDistribution (util/scattering.h:109-205), Fresnel terms and the dielectric /
+// conductor BxDFs (bxdfs.h:300-510, bxdfs.cpp:77-245) in the local shading frame.  Vector dot
+// products are plain; a dot with a Normal3f operand (Refract) is FMA-compensated (DotN).
+enum BxDFFlagBits : int { kBxReflection = 1, kBxTransmission = 2, kBxDiffuse = 4, kBxGlossy = 8, kBxSpecular = 16 };
+
+PHD float CosTheta(V3 w) { return w.z; }
+PHD float Cos2Theta(V3 w) { return Sqr(w.z); }
+PHD float AbsCosTheta(V3 w) { return std::fabs(w.z); }
+PHD float Sin2Theta(V3 w) { return std::fmax(0.f, 1 - Cos2Theta(w)); }
+PHD float SinTheta(V3 w) { return std::sqrt(Sin2Theta(w)); }
+PHD float Tan2Theta(V3 w) { return Sin2Theta(w) / Cos2Theta(w); }
+PHD float CosPhi(V3 w) {
+    float sinTheta = SinTheta(w);
+    return (sinTheta == 0) ? 1 : Clampf(w.x / sinTheta, -1, 1);
+}
+PHD float SinPhi(V3 w) {
+    float sinTheta = SinTheta(w);
+    return (sinTheta == 0) ? 0 : Clampf(w.y / sinTheta, -1, 1);
+}
+PHD bool SameHemisphere(V3 w, V3 wp) { return w.z * wp.z > 0; }
+PHD V3 Reflect(V3 wo, V3 n) { return -wo + 2 * Dot(wo, n) * n; }
+// util/scattering.h Refract: n is a Normal3f
+PHD bool Refract(V3 wi, V3 n, float eta, float *etap, V3 *wt) {
+    float cosTheta_i = DotN(n, wi);
+    if (cosTheta_i < 0) {
+        eta = 1 / eta;
+        cosTheta_i = -cosTheta_i;
+        n = -n;
+    }
+    float sin2Theta_i = std::fmax(0.f, 1 - Sqr(cosTheta_i));
+    float sin2Theta_t = sin2Theta_i / Sqr(eta);
+    if (sin2Theta_t >= 1) return false;
+    float cosTheta_t = std::sqrt(1 - sin2Theta_t);
+    *wt = -wi / eta + (cosTheta_i / eta - cosTheta_t) * n;
+    *etap = eta;
+    return true;
+}
+PHD float FrDielectric(float cosTheta_i, float eta) {
+    cosTheta_i = Clampf(cosTheta_i, -1, 1);
+    if (cosTheta_i < 0) {
+        eta = 1 / eta;
+        cosTheta_i = -cosTheta_i;
+    }
+    float sin2Theta_i = 1 - Sqr(cosTheta_i);
+    float sin2Theta_t = sin2Theta_i / Sqr(eta);
+    if (sin2Theta_t >= 1) return 1.f;
+    float cosTheta_t = SafeSqrt(1 - sin2Theta_t);
+    float r_parl = (eta * cosTheta_i - cosTheta_t) / (eta * cosTheta_i + cosTheta_t);
+    float r_perp = (cosTheta_i - eta * cosTheta_t) / (cosTheta_i + eta * cosTheta_t);
+    return (Sqr(r_parl) + Sqr(r_perp)) / 2;
+}
+// pstd::complex<float> arithmetic exactly as util/pstd.h:1066-1229 writes it
+struct Cpx {
+    float re, im;
+};
+PHD Cpx CAdd(Cpx a, Cpx b) { return {a.re + b.re, a.im + b.im}; }
+PHD Cpx CSub(Cpx a, Cpx b) { return {a.re - b.re, a.im - b.im}; }
+PHD Cpx CMul(Cpx a, Cpx b) { return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re}; }
+PHD Cpx CDiv(Cpx a, Cpx z) {
+    float scale = 1 / (z.re * z.re + z.im * z.im);
+    return {scale * (a.re * z.re + a.im * z.im), scale * (a.im * z.re - a.re * z.im)};
+}
+PHD float CNorm(Cpx z) { return z.re * z.re + z.im * z.im; }
+PHD Cpx CSqrt(Cpx z) {
+    float n = std::sqrt(CNorm(z)), t1 = std::sqrt(0.5f * (n + std::fabs(z.re))), t2 = 0.5f * z.im / t1;
+    if (n == 0) return {0, 0};
+    if (z.re >= 0) return {t1, t2};
+    return {std::fabs(t2), std::copysign(t1, z.im)};
+}
+// util/scattering.h FrComplex(Float cosTheta_i, complex eta)
+PHD float FrComplex(float cosTheta_i, float etaRe, float etaIm) {
+    const Cpx eta{etaRe, etaIm};
+    cosTheta_i = Clampf(cosTheta_i, 0, 1);
+    float sin2Theta_i = 1 - Sqr(cosTheta_i);
+    Cpx sin2Theta_t = CDiv(Cpx{sin2Theta_i, 0}, CMul(eta, eta));
+    Cpx cosTheta_t = CSqrt(CSub(Cpx{1, 0}, sin2Theta_t));
+    Cpx ec = CMul(eta, Cpx{cosTheta_i, 0});
+    Cpx r_parl = CDiv(CSub(ec, cosTheta_t), CAdd(ec, cosTheta_t));
+    Cpx et = CMul(eta, cosTheta_t);
+    Cpx r_perp = CDiv(CSub(Cpx{cosTheta_i, 0}, et), CAdd(Cpx{cosTheta_i, 0}, et));
+    return (CNorm(r_parl) + CNorm(r_perp)) / 2;
+}
+struct TrowbridgeReitz {
+    float ax, ay;
+    PHD static TrowbridgeReitz Make(float ax, float ay) {
+        TrowbridgeReitz t{ax, ay};
+        if (!t.EffectivelySmooth()) {
+            t.ax = std::fmax(t.ax, 1e-4f);
+            t.ay = std::fmax(t.ay, 1e-4f);
+        }
+        return t;
+    }
+    PHD bool EffectivelySmooth() const { return std::fmax(ax, ay) < 1e-3f; }
+    PHD void Regularize() {
+        if (ax < 0.3f) ax = Clampf(2 * ax, 0.1f, 0.3f);
+        if (ay < 0.3f) ay = Clampf(2 * ay, 0.1f, 0.3f);
+    }
+    PHD float D(V3 wm) const {
+        float tan2Theta = Tan2Theta(wm);
+        if (std::isinf(tan2Theta)) return 0;
+        float cos4Theta = Sqr(Cos2Theta(wm));
+        if (cos4Theta < 1e-16f) return 0;
+        float e = tan2Theta * (Sqr(CosPhi(wm) / ax) + Sqr(SinPhi(wm) / ay));
+        return 1 / (kPi * ax * ay * cos4Theta * Sqr(1 + e));
+    }
+    PHD float Lambda(V3 w) const {
+        float tan2Theta = Tan2Theta(w);
+        if (std::isinf(tan2Theta)) return 0;
+        float alpha2 = Sqr(CosPhi(w) * ax) + Sqr(SinPhi(w) * ay);
+        return (std::sqrt(1 + alpha2 * tan2Theta) - 1) / 2;
+    }
+    PHD float G1(V3 w) const { return 1 / (1 + Lambda(w)); }
+    PHD float G(V3 wo, V3 wi) const { return 1 / (1 + Lambda(wo) + Lambda(wi)); }
+    PHD float D(V3 w, V3 wm) const { return G1(w) / AbsCosTheta(w) * D(wm) * AbsDot(w, wm); }
+    PHD float PDF(V3 w, V3 wm) const { return D(w, wm); }
+    PHD V3 SampleWm(V3 w, float u0, float u1) const {
+        V3 wh = Normalize(V3(ax * w.x, ay * w.y, w.z));
+        if (wh.z < 0) wh = -wh;
+        V3 T1 = (wh.z < 0.99999f) ? Normalize(Cross(V3(0, 0, 1), wh)) : V3(1, 0, 0);
+        V3 T2 = Cross(wh, T1);
+        // SampleUniformDiskPolar (util/sampling.h:311-315)
+        float r = std::sqrt(u0), theta = 2 * kPi * u1;
+        float px = r * std::cos(theta), py = r * std::sin(theta);
+        float h = std::sqrt(1 - Sqr(px));
+        py = Lerpf((1 + wh.z) / 2, h, py);
+        float pz = std::sqrt(std::fmax(0.f, 1 - (Sqr(px) + Sqr(py))));
+        V3 nh = px * T1 + py * T2 + pz * wh;
+        return Normalize(V3(ax * nh.x, ay * nh.y, std::fmax(1e-6f, nh.z)));
+    }
+};
+// PiecewiseLinearSpectrum::operator() (util/spectrum.cpp:68-78): FindInterval's result is the
+// largest knot index o <= n-2 with lambda[o] <= l
+PHD float PiecewiseLinearEval(const float *lam, const float *val, int n, float l) {
+    if (n == 0 || l < lam[0] || l > lam[n - 1]) return 0;
+    int lo = 0, hi = n - 2;
+    while (lo < hi) {
+        int mid = (lo + hi + 1) >> 1;
+        if (lam[mid] <= l) lo = mid;
+        else hi = mid - 1;
+    }
+    float t = (l - lam[lo]) / (lam[lo + 1] - lam[lo]);
+    return Lerpf(t, val[lo], val[lo + 1]);
+}
+// RoughnessToAlpha (util/scattering.h:192)
+PHD float RoughnessToAlpha(float roughness) { return std::sqrt(roughness); }
+
+// A sampled BxDF direction.  f is the scalar BSDF value (dielectric); for the conductor the
+// spectral value is evaluated per wavelength from the geometry terms (ConductorTerms).
+struct BxSample {
+    bool ok;
+    V3 wi;
+    float f, pdf, etap;
+    int flags;
+};
+PHD int DielectricFlags(float eta, const TrowbridgeReitz &tr) {
+    int flags = (eta == 1) ? kBxTransmission : (kBxReflection | kBxTransmission);
+    return flags | (tr.EffectivelySmooth() ? kBxSpecular : kBxGlossy);
+}
+// DielectricBxDF::Sample_f (bxdfs.cpp:77-170), TransportMode::Radiance, all lobes
+PHD BxSample DielectricSample(float eta, const TrowbridgeReitz &tr, V3 wo, float uc, float u0, float u1) {
+    BxSample s{false, V3(0, 0, 0), 0, 0, 1, 0};
+    if (eta == 1 || tr.EffectivelySmooth()) {
+        float R = FrDielectric(CosTheta(wo), eta), T = 1 - R;
+        float pr = R, pt = T;
+        if (pr == 0 && pt == 0) return s;
+        if (uc < pr / (pr + pt)) {
+            V3 wi(-wo.x, -wo.y, wo.z);
+            s = BxSample{true, wi, R / AbsCosTheta(wi), pr / (pr + pt), 1, kBxSpecular | kBxReflection};
+            return s;
+        }
+        V3 wi;
+        float etap;
+        if (!Refract(wo, V3(0, 0, 1), eta, &etap, &wi)) return s;
+        float ft = T / AbsCosTheta(wi);
+        ft /= Sqr(etap);
+        s = BxSample{true, wi, ft, pt / (pr + pt), etap, kBxSpecular | kBxTransmission};
+        return s;
+    }
+    V3 wm = tr.SampleWm(wo, u0, u1);
+    float R = FrDielectric(Dot(wo, wm), eta);
+    float T = 1 - R;
+    float pr = R, pt = T;
+    if (pr == 0 && pt == 0) return s;
+    if (uc < pr / (pr + pt)) {
+        V3 wi = Reflect(wo, wm);
+        if (!SameHemisphere(wo, wi)) return s;
+        float pdf = tr.PDF(wo, wm) / (4 * AbsDot(wo, wm)) * pr / (pr + pt);
+        float f = tr.D(wm) * tr.G(wo, wi) * R / (4 * CosTheta(wi) * CosTheta(wo));
+        s = BxSample{true, wi, f, pdf, 1, kBxGlossy | kBxReflection};
+        return s;
+    }
+    float etap;
+    V3 wi;
+    bool tir = !Refract(wo, wm, eta, &etap, &wi);
+    if (SameHemisphere(wo, wi) || wi.z == 0 || tir) return s;
+    float denom = Sqr(Dot(wi, wm) + Dot(wo, wm) / etap);
+    float dwm_dwi = AbsDot(wi, wm) / denom;
+    float pdf = tr.PDF(wo, wm) * dwm_dwi * pt / (pr + pt);
+    float ft = T * tr.D(wm) * tr.G(wo, wi) * std::fabs(Dot(wi, wm) * Dot(wo, wm) / (CosTheta(wi) * CosTheta(wo) * denom));
+    ft /= Sqr(etap);
+    s = BxSample{true, wi, ft, pdf, etap, kBxGlossy | kBxTransmission};
+    return s;
+}
+// DielectricBxDF::f and ::PDF (bxdfs.cpp:172-245); pdfOut may be null
+PHD float DielectricEval(float eta, const TrowbridgeReitz &tr, V3 wo, V3 wi, float *pdfOut) {
+    if (pdfOut) *pdfOut = 0;
+    if (eta == 1 || tr.EffectivelySmooth()) return 0;
+    float cosTheta_o = CosTheta(wo), cosTheta_i = CosTheta(wi);
+    bool reflect = cosTheta_i * cosTheta_o > 0;
+    float etap = 1;
+    if (!reflect) etap = cosTheta_o > 0 ? eta : (1 / eta);
+    V3 wm = wi * etap + wo;
+    if (cosTheta_i == 0 || cosTheta_o == 0 || LengthSquared(wm) == 0) return 0;
+    wm = FaceForward(Normalize(wm), V3(0, 0, 1));
+    if (Dot(wm, wi) * cosTheta_i < 0 || Dot(wm, wo) * cosTheta_o < 0) return 0;
+    float F = FrDielectric(Dot(wo, wm), eta);
+    float R = F, T = 1 - R, pr = R, pt = T;
+    if (reflect) {
+        if (pdfOut && !(pr == 0 && pt == 0)) *pdfOut = tr.PDF(wo, wm) / (4 * AbsDot(wo, wm)) * pr / (pr + pt);
+        return tr.D(wm) * tr.G(wo, wi) * F / std::fabs(4 * cosTheta_i * cosTheta_o);
+    }
+    float denom = Sqr(Dot(wi, wm) + Dot(wo, wm) / etap) * cosTheta_i * cosTheta_o;
+    float ft = tr.D(wm) * (1 - F) * tr.G(wo, wi) * std::fabs(Dot(wi, wm) * Dot(wo, wm) / denom);
+    ft /= Sqr(etap);
+    if (pdfOut && !(pr == 0 && pt == 0)) {
+        float denomP = Sqr(Dot(wi, wm) + Dot(wo, wm) / etap);
+        float dwm_dwi = AbsDot(wi, wm) / denomP;
+        *pdfOut = tr.PDF(wo, wm) * dwm_dwi * pt / (pr + pt);
+    }
+    return ft;
+}
+// ConductorBxDF (bxdfs.h:413-510).  f is spectral: the geometry-only terms are returned and
+// ConductorF combines them with each wavelength's Fresnel factor in pbrt's operation order.
+struct ConductorTerms {
+    bool ok, specular;
+    V3 wi;
+    float pdf;
+    float D, G, cosI, cosO;  // rough: f = D * F * G / (4 * cosI * cosO)
+    float cosF;              // argument of FrComplex; specular: f = Fr / cosI
+};
+PHD float ConductorF(const ConductorTerms &t, float eta, float k) {
+    float F = FrComplex(t.cosF, eta, k);
+    if (t.specular) return F / t.cosI;
+    return t.D * F * t.G / (4 * t.cosI * t.cosO);
+}
+PHD ConductorTerms ConductorSample(const TrowbridgeReitz &tr, V3 wo, float u0, float u1) {
+    ConductorTerms c{false, false, V3(0, 0, 0), 0, 0, 0, 0, 0, 0};
+    if (tr.EffectivelySmooth()) {
+        V3 wi(-wo.x, -wo.y, wo.z);
+        c.ok = true;
+        c.specular = true;
+        c.wi = wi;
+        c.pdf = 1;
+        c.cosI = AbsCosTheta(wi);
+        c.cosF = AbsCosTheta(wi);
+        return c;
+    }
+    if (wo.z == 0) return c;
+    V3 wm = tr.SampleWm(wo, u0, u1);
+    V3 wi = Reflect(wo, wm);
+    if (!SameHemisphere(wo, wi)) return c;
+    float pdf = tr.PDF(wo, wm) / (4 * AbsDot(wo, wm));
+    float cosTheta_o = AbsCosTheta(wo), cosTheta_i = AbsCosTheta(wi);
+    if (cosTheta_i == 0 || cosTheta_o == 0) return c;
+    c = ConductorTerms{true, false, wi, pdf, tr.D(wm), tr.G(wo, wi), cosTheta_i, cosTheta_o, AbsDot(wo, wm)};
+    return c;
+}
+// ConductorBxDF::f / ::PDF geometry for a given wi (ok = false: f = 0, pdf = 0)
+PHD ConductorTerms ConductorEval(const TrowbridgeReitz &tr, V3 wo, V3 wi) {
+    ConductorTerms c{false, false, wi, 0, 0, 0, 0, 0, 0};
+    if (!SameHemisphere(wo, wi) || tr.EffectivelySmooth()) return c;
+    float cosTheta_o = AbsCosTheta(wo), cosTheta_i = AbsCosTheta(wi);
+    V3 wm = wi + wo;
+    if (cosTheta_i == 0 || cosTheta_o == 0 || LengthSquared(wm) == 0) return c;
+    wm = Normalize(wm);
+    // PDF: wm faced forward; f: not (FrComplex uses |dot|, D and G are even in wm)
+    V3 wmf = FaceForward(wm, V3(0, 0, 1));
+    c = ConductorTerms{true, false, wi, tr.PDF(wo, wmf) / (4 * AbsDot(wo, wmf)), tr.D(wm), tr.G(wo, wi), cosTheta_i,
+                       cosTheta_o, AbsDot(wo, wm)};
+    return c;
+}
+
 // ---------------------------------------------------------------- ZSobol sampler
 // ZSobolSampler (samplers.h:225-370): Morton-ordered pixel samples, base-4 digit
 // permutations per dimension, Sobol' dimensions 0/1 with the chosen scrambler.

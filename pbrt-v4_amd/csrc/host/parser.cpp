@@ -550,6 +550,38 @@ class Parser {
             } else {
                 throw Error(ps.loc + ": reflectance of type " + r->type + " not supported");
             }
+        } else if (type == "dielectric") {
+            // DielectricMaterial::Create (materials.cpp:51-74)
+            m.type = kMatDielectric;
+            if (Param *e = ps.Find("eta", "float")) {
+                if (e->nums.empty()) throw Error(ps.loc + ": \"float eta\" needs a value");
+                m.eta = (float)e->nums[0];
+            } else if (ps.Find("eta", "spectrum")) {
+                // a non-constant eta makes GetBxDF call SampledWavelengths::TerminateSecondary
+                throw Error(ps.loc + ": spectrally varying dielectric eta (dispersion) is not supported yet");
+            }
+            Roughness(ps, &m);
+        } else if (type == "conductor") {
+            // ConductorMaterial::Create (materials.cpp:217-251)
+            m.type = kMatConductor;
+            Param *eta = ps.Find("eta"), *k = ps.Find("k"), *refl = ps.Find("reflectance");
+            if (refl && (eta || k))
+                throw Error(ps.loc + ": For the conductor material, both \"reflectance\" and \"eta\" and \"k\" can't be provided.");
+            if (refl) {
+                if (refl->type != "rgb" || refl->nums.size() != 3)
+                    throw Error(ps.loc + ": conductor reflectance must be \"rgb\" (3 values)");
+                float rgb[3] = {(float)refl->nums[0], (float)refl->nums[1], (float)refl->nums[2]};
+                for (float v : rgb)
+                    if (v < 0 || v > 1) throw Error(ps.loc + ": RGB parameter \"reflectance\" used as an albedo has > 1 component.");
+                auto c = RGBToSigmoidCoeffs(rgb[0], rgb[1], rgb[2]);
+                m.c0 = c[0];
+                m.c1 = c[1];
+                m.c2 = c[2];
+            } else {
+                m.etaSpec = eta ? SpectrumParam(eta, ps.loc) : NamedPLSpectrum("metal-Cu-eta", ps.loc);
+                m.kSpec = k ? SpectrumParam(k, ps.loc) : NamedPLSpectrum("metal-Cu-k", ps.loc);
+            }
+            Roughness(ps, &m);
         } else {
             throw Error(ps.loc + ": material \"" + type + "\" is not supported yet");
         }
@@ -557,6 +589,57 @@ class Parser {
         ps.CheckUnused();
         scene.materials.push_back(m);
         return (int)scene.materials.size() - 1;
+    }
+
+    // uroughness / vroughness / roughness + remaproughness -> TrowbridgeReitzDistribution alphas
+    // (materials.cpp:62-70, materials.h:194-199 / :494-509, util/scattering.h:109-118, 192)
+    void Roughness(ParamSet &ps, MaterialDesc *m) {
+        Param *u = ps.Find("uroughness", "float"), *v = ps.Find("vroughness", "float");
+        float ur = 0, vr = 0;
+        if (!u || !v) {
+            Param *r = ps.Find("roughness", "float");
+            float rv = (r && !r->nums.empty()) ? (float)r->nums[0] : 0.f;
+            ur = vr = rv;
+        }
+        if (u) ur = u->nums.empty() ? 0.f : (float)u->nums[0];
+        if (v) vr = v->nums.empty() ? 0.f : (float)v->nums[0];
+        if (ps.GetBool("remaproughness", true)) {
+            ur = RoughnessToAlpha(ur);
+            vr = RoughnessToAlpha(vr);
+        }
+        TrowbridgeReitz t = TrowbridgeReitz::Make(ur, vr);
+        m->alphaX = t.ax;
+        m->alphaY = t.ay;
+    }
+
+    // named spectrum -> PiecewiseLinearSpectrum::FromInterleaved(samples, normalize = false)
+    // (util/spectrum.cpp:133-163, 2636-2662): extended to cover Lambda_min..Lambda_max
+    int NamedPLSpectrum(const std::string &name, const std::string &loc) {
+        try {
+            scene.plSpectra.push_back(NamedPiecewiseLinear(name));
+        } catch (const Error &e) {
+            throw Error(loc + ": " + e.what());
+        }
+        return (int)scene.plSpectra.size() - 1;
+    }
+
+    // "spectrum" parameter of an Unbounded spectrum texture (paramdict.cpp:384-450, :817-875)
+    int SpectrumParam(Param *p, const std::string &loc) {
+        if (p->type == "spectrum" && !p->strs.empty()) return NamedPLSpectrum(p->strs[0], loc);
+        if (p->type == "spectrum" && !p->nums.empty()) {
+            if (p->nums.size() % 2) throw Error(loc + ": Found odd number of values for \"" + p->name + "\"");
+            PLSpectrumDesc d;
+            for (size_t i = 0; i < p->nums.size(); i += 2) {
+                if (i > 0 && (float)p->nums[i] <= d.lambda.back())
+                    throw Error(loc + ": Spectrum description invalid: wavelengths aren't increasing");
+                d.lambda.push_back((float)p->nums[i]);
+                d.value.push_back((float)p->nums[i + 1]);
+            }
+            if (d.lambda.size() < 2) throw Error(loc + ": spectrum \"" + p->name + "\" needs at least two samples");
+            scene.plSpectra.push_back(std::move(d));
+            return (int)scene.plSpectra.size() - 1;
+        }
+        throw Error(loc + ": \"" + p->type + " " + p->name + "\" is not supported for conductors yet (use \"spectrum\")");
     }
 
     void Shape(const std::string &type, ParamSet &ps) {
@@ -708,7 +791,6 @@ void Parser::Finish() {
     std::string ls = integratorParams.GetString("lightsampler", "bvh");
     if (ls != "bvh" && ls != "uniform") throw Error(integratorParams.loc + ": lightsampler " + ls + " not supported");
     if (ls == "uniform") scene.uniformLightSampler = true;
-    if (scene.regularize) throw Error(integratorParams.loc + ": regularize not supported");
     // ---- filter
     if (scene.filterName != "box") throw Error(filterParams.loc + ": pixel filter \"" + scene.filterName + "\" not supported yet (box only)");
     scene.filterRadiusX = (float)filterParams.GetFloat("xradius", 0.5);

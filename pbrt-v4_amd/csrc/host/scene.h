@@ -29,15 +29,26 @@ V3 XformVector(const Mat4 &m, V3 v);
 V3 XformNormal(const Mat4 &mInv, V3 n);  // uses the inverse transpose
 bool SwapsHandedness(const Mat4 &m);
 
-enum MaterialType : int { kMatDiffuse = 0, kMatNumTypes = 1 };
+enum MaterialType : int { kMatDiffuse = 0, kMatDielectric = 1, kMatConductor = 2, kMatNumTypes = 3 };
 
 struct MaterialDesc {
     int type = kMatDiffuse;
-    // spectrum of the reflectance: sigmoid (c0,c1,c2) or a constant value
+    // diffuse reflectance / conductor "reflectance": sigmoid (c0,c1,c2) or a constant value
     bool constant = false;
     float constantValue = 0.5f;
     float c0 = 0, c1 = 0, c2 = 0;
+    // dielectric / conductor: TrowbridgeReitzDistribution alphas after RoughnessToAlpha (when
+    // remaproughness) and the constructor's clamp (util/scattering.h:109-118)
+    float alphaX = 0, alphaY = 0;
+    float eta = 1.5f;              // dielectric: ConstantSpectrum eta (materials.cpp:51-60)
+    int etaSpec = -1, kSpec = -1;  // conductor: SceneDesc::plSpectra indices; -1/-1 = reflectance
     std::string name;
+};
+
+// PiecewiseLinearSpectrum (util/spectrum.h:187-239): named spectra arrive already extended by
+// FromInterleaved (util/spectrum.cpp:133-163), inline "spectrum" parameters as written
+struct PLSpectrumDesc {
+    std::vector<float> lambda, value;
 };
 
 struct AreaLightDesc {
@@ -94,6 +105,7 @@ struct SceneDesc {
     std::vector<AreaLightDesc> areaLights;
     std::vector<InfiniteLightDesc> infiniteLights;
     std::vector<std::array<float, 311>> denseSpectra;
+    std::vector<PLSpectrumDesc> plSpectra;
     std::array<float, 311> sensorX, sensorY, sensorZ;  // r_bar/g_bar/b_bar of "cie1931"
 
     // BVH light sampler (lightsamplers.cpp:112-236); unused when one light -> uniform
@@ -126,6 +138,7 @@ extern const uint8_t kZSobolPermutations[24][4];
 struct SpectralData {
     std::vector<float> cieX, cieY, cieZ, cieLambda, d65Interleaved;
     std::vector<double> optX, optY, optZ, optD65Raw, optXyzToSrgb, optSrgbToXyz;
+    std::map<std::string, std::vector<float>> named;  // interleaved (lambda, value) tables
     double optD65Divisor = 1;
     std::array<float, 311> denseX, denseY, denseZ, denseD65;  // 395..705
     float photometricD65 = 0;                                  // SpectrumToPhotometric(D65)
@@ -141,6 +154,9 @@ std::array<float, 3> RGBToSigmoidCoeffs(float r, float g, float b);
 std::vector<float> RGB2SpecColumn(int maxc, int j, int i);
 float RGB2SpecZNode(int k);
 std::array<float, 311> DenseRGBIlluminant(float r, float g, float b);
+// GetNamedSpectrum(name) for the metal / glass tables: PiecewiseLinearSpectrum::FromInterleaved
+// (samples, normalize = false), extended to Lambda_min - 1 / Lambda_max + 1 (spectrum.cpp:133-163)
+PLSpectrumDesc NamedPiecewiseLinear(const std::string &name);
 
 // Hash / permutation (util/hash.h:19, util/math.h:728)
 uint64_t MurmurHash64A(const unsigned char *key, size_t len, uint64_t seed);

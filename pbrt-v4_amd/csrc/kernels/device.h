@@ -49,8 +49,13 @@ struct ShadeLdsLayout {
 // bounds every shard, and the records need no more memory than an unsharded queue.
 constexpr int kShards = 8;
 constexpr int kCounterPad = 64;  // ints between counters (256 B)
-constexpr int kNumQueues = 5;
+constexpr int kNumQueues = 7;
 constexpr int kCntRay = 0, kCntMat = 1, kCntShadow = 2, kCntEscaped = 3, kCntEmissive = 4;
+// per-material-type queues (pbrt's MaterialEvalQueue per Material::Types, surfscatter.cpp:39-55):
+// diffuse uses kCntMat, dielectric kCntMat + 4, conductor kCntMat + 5
+constexpr int kNumMatTypes = 3;  // == host kMatNumTypes (diffuse, dielectric, conductor)
+constexpr int kMatDiffuseT = 0, kMatDielectricT = 1, kMatConductorT = 2;
+PHD int MatCounter(int type) { return type == 0 ? kCntMat : kCntMat + 3 + type; }
 PHD int CounterIndex(int depth, int queue, int shard) {
     return ((depth * kNumQueues + queue) * kShards + shard) * kCounterPad;
 }
@@ -71,6 +76,14 @@ struct DeviceScene {
     const float4 *matCoeffs;  // c0, c1, c2, constant value
     const int *matConstant;
     int nMaterials;
+    const int *matType;        // [nMaterials] 0 diffuse, 1 dielectric, 2 conductor
+    const float4 *matParams;   // alpha_x, alpha_y (TrowbridgeReitz), dielectric eta, 0
+    const int *matSpectra;     // [nMaterials][2] conductor eta / k piecewise-linear spectra
+    int matTypeMask;           // bit t: some material of type t exists
+    int regularize;            // integrator "regularize" (surfscatter.cpp:127-128)
+    // piecewise-linear spectra (conductor eta / k): spectrum s spans [plOffsets[s], plOffsets[s+1])
+    const int *plOffsets;
+    const float *plLambda, *plValue;
     // area lights
     int nAreaLights;
     const int *lightPrim;  // leaf-order prim
@@ -162,7 +175,7 @@ struct PathState {
     float *L;           // [3][N] sensor RGB
     float *filterW;     // [N]
     // work queues: record indices of the current depth
-    int *matQ;          // [NR] material (diffuse) hits
+    int *matQ[kNumMatTypes];  // [NR] each: hits per material type
     int *escQ;          // [NR] escaped rays (only with infinite lights)
     int *emitQ;         // [NR] hits on emissive triangles
     int *counters;      // [CounterIndex(maxDepth + 2, 0, 0)]: per depth, queue and shard

@@ -775,6 +775,8 @@ __global__ void __launch_bounds__(kBlock) k_camera(DeviceScene S, PathState st, 
     r.ray[5 * NR + slot] = d.z;
 }
 
+// NMatQ = 1: every material is diffuse (one material queue); 3: one queue per material type
+template <int NMatQ>
 __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_closest(DeviceScene S, PathState st, int depth, int timed) {
     const QueueView rays = LoadQueue(st, depth, kCntRay);
     if ((int)(blockIdx.x * blockDim.x) >= rays.total) return;  // no work
@@ -784,17 +786,22 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_closest(Device
     const PathRecords &rec = st.rec[depth & 1];
     const int count = rays.total;
     const int shard = ProducerShard();
-    int *matCounter = &st.counters[CounterIndex(depth, kCntMat, shard)];
     int *escCounter = &st.counters[CounterIndex(depth, kCntEscaped, shard)];
     int *emitCounter = &st.counters[CounterIndex(depth, kCntEmissive, shard)];
     int *hitPrim = st.hitPrim[depth & 1];
     float *hitB = st.hitB[depth & 1];
     const bool shade = depth < S.maxDepth;  // at maxDepth only emission and escape matter
-    constexpr int kCap = 512;  // entries per wave and queue
-    __shared__ int qBuf[(kBlock / 64) * 3 * kCap];
-    int *const qCnt[3] = {escCounter, emitCounter, matCounter};
-    int *const qArr[3] = {st.escQ + shard * st.capS, st.emitQ + shard * st.capS, st.matQ + shard * st.capS};
-    WaveQueues<3, kCap> queues(qBuf, qCnt, qArr);
+    constexpr int kQ = 2 + NMatQ;
+    constexpr int kCap = NMatQ == 1 ? 512 : 256;  // entries per wave and queue
+    __shared__ int qBuf[(kBlock / 64) * kQ * kCap];
+    int *qCnt[kQ] = {escCounter, emitCounter};
+    int *qArr[kQ] = {st.escQ + shard * st.capS, st.emitQ + shard * st.capS};
+#pragma unroll
+    for (int t = 0; t < NMatQ; ++t) {
+        qCnt[2 + t] = &st.counters[CounterIndex(depth, MatCounter(t), shard)];
+        qArr[2 + t] = st.matQ[t] + shard * st.capS;
+    }
+    WaveQueues<kQ, kCap> queues(qBuf, qCnt, qArr);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         atomicAdd(&st.stats[1], (unsigned long long)count);
         if (timed) atomicAdd(&st.stats[3], (unsigned long long)count);  // rays of event-timed launches
@@ -820,9 +827,15 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_closest(Device
         // EnqueueWorkAfterIntersection / Miss (intersect.h:48-156): misses to the escaped-ray
         // queue (infinite lights only), emissive hits to the hit-area-light queue, every hit
         // to its material queue
-        const bool pred[3] = {S.nInfinite > 0 && active && prim < 0,
-                              S.nAreaLights > 0 && active && prim >= 0 && S.primLight[prim] >= 0,
-                              shade && active && prim >= 0};
+        bool pred[kQ] = {S.nInfinite > 0 && active && prim < 0,
+                         S.nAreaLights > 0 && active && prim >= 0 && S.primLight[prim] >= 0};
+        if constexpr (NMatQ == 1) {
+            pred[2] = shade && active && prim >= 0;
+        } else {
+            const int type = (shade && active && prim >= 0) ? S.matType[S.primMaterial[prim]] : -1;
+#pragma unroll
+            for (int t = 0; t < NMatQ; ++t) pred[2 + t] = type == t;
+        }
         queues.Append(pred, qi);
     }
     queues.FlushAll();
@@ -1011,49 +1024,110 @@ __device__ inline bool NeeAccumulate(const FD *dense, const LdsF4 *sensor4, cons
 // curves, light spectra, this depth's 7 Halton permutation tables, lights, light BVH and
 // materials.  The only HBM traffic per item is its path state, the hit triangle and beta,
 // whose 31 values arrive by LDS-DMA while the sampler runs on LDS-resident tables.
-__global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(DeviceScene S, PathState st, int depth) {
-    const QueueView mats = LoadQueue(st, depth, kCntMat);
-    if ((int)(blockIdx.x * blockDim.x) >= mats.total) return;  // no work
-    extern __shared__ float4 dynLds[];
-    char *ldsBase = reinterpret_cast<char *>(dynLds);
+// Tables the shade kernels stage in LDS per block (ShadeLdsLayout): sensor curves, light
+// spectra, this depth's 7 Halton permutation tables, lights, light BVH and materials, plus the
+// [31][kBlock] per-lane beta buffer (wavelength-major: conflict-free).
+struct ShadeTables {
+    ShadeLdsLayout lay;
+    float *bfLds;
+    float *denseLds;
+    const LdsF4 *sensorL;
+    const LdsU16 *permL;
+    uint32_t permOff[7];
+    DeviceScene SL;  // the light sampler reads its nodes from LDS
+    const DeviceAreaLight *lightsL;
+    const float4 *matsL;
+    const int *matConstL;
+};
+__device__ __forceinline__ void StageShadeTables(const DeviceScene &S, int depth, char *ldsBase, ShadeTables *T) {
     const ShadeLdsLayout lay = S.shadeLds;
-    float *bfLds = reinterpret_cast<float *>(ldsBase);  // [lambda][lane]: conflict-free
+    T->lay = lay;
+    T->bfLds = reinterpret_cast<float *>(ldsBase);
     float4 *sensorLds = reinterpret_cast<float4 *>(ldsBase + lay.sensor);
-    float *denseLds = reinterpret_cast<float *>(ldsBase + lay.dense);
+    T->denseLds = reinterpret_cast<float *>(ldsBase + lay.dense);
     uint16_t *permLds = reinterpret_cast<uint16_t *>(ldsBase + lay.perm);
     DeviceAreaLight *lightsLds = reinterpret_cast<DeviceAreaLight *>(ldsBase + lay.lights);
     DeviceLightNode *nodesLds = reinterpret_cast<DeviceLightNode *>(ldsBase + lay.lightNodes);
     float4 *matsLds = reinterpret_cast<float4 *>(ldsBase + lay.mats);
     int *matConstLds = reinterpret_cast<int *>(ldsBase + lay.matConst);
-    const int d0 = 6 + 7 * depth;  // first sampler dimension of this depth
-    uint32_t permOff[7];
-    {
-        DmaCopy<16>(S.sensor4, sensorLds, kDenseN);
-        if (lay.denseInLds) DmaCopy<4>(S.dense, denseLds, S.nDense * kDenseN);
-        // this depth's 7 permutation tables, stored contiguously per depth on the host
-        const uint32_t *info = S.permDepthInfo + depth * 8;  // {start, off0..off6}
+    DmaCopy<16>(S.sensor4, sensorLds, kDenseN);
+    if (lay.denseInLds) DmaCopy<4>(S.dense, T->denseLds, S.nDense * kDenseN);
+    // this depth's 7 permutation tables, stored contiguously per depth on the host
+    const uint32_t *info = S.permDepthInfo + depth * 8;  // {start, off0..off6}
 #pragma unroll
-        for (int k = 0; k < 7; ++k) permOff[k] = info[1 + k];
-        const uint32_t start = info[0], words = (S.permDepthInfo[(depth + 1) * 8] - start + 1) / 2;
-        DmaCopy<4>(S.permByDepth + start, permLds, (int)words);
-        if (lay.lightsInLds) {
-            DmaCopy<4>(S.lights, lightsLds, S.nAreaLights * (int)(sizeof(DeviceAreaLight) / 4));
-            DmaCopy<4>(S.lightNodes, nodesLds, S.nLightNodes * (int)(sizeof(DeviceLightNode) / 4));
-        }
-        if (lay.matsInLds) {
-            DmaCopy<16>(S.matCoeffs, matsLds, S.nMaterials);
-            DmaCopy<4>(S.matConstant, matConstLds, S.nMaterials);
-        }
-        DmaWait();
-        __syncthreads();
+    for (int k = 0; k < 7; ++k) T->permOff[k] = info[1 + k];
+    const uint32_t start = info[0], words = (S.permDepthInfo[(depth + 1) * 8] - start + 1) / 2;
+    DmaCopy<4>(S.permByDepth + start, permLds, (int)words);
+    if (lay.lightsInLds) {
+        DmaCopy<4>(S.lights, lightsLds, S.nAreaLights * (int)(sizeof(DeviceAreaLight) / 4));
+        DmaCopy<4>(S.lightNodes, nodesLds, S.nLightNodes * (int)(sizeof(DeviceLightNode) / 4));
     }
-    const LdsF4 *sensorL = (const LdsF4 *)sensorLds;
-    const LdsU16 *permL = (const LdsU16 *)permLds;
-    DeviceScene SL = S;  // light sampler reads its nodes from LDS
-    if (lay.lightsInLds) SL.lightNodes = nodesLds;
-    const DeviceAreaLight *lightsL = lay.lightsInLds ? lightsLds : S.lights;
-    const float4 *matsL = lay.matsInLds ? matsLds : S.matCoeffs;
-    const int *matConstL = lay.matsInLds ? matConstLds : S.matConstant;
+    if (lay.matsInLds) {
+        DmaCopy<16>(S.matCoeffs, matsLds, S.nMaterials);
+        DmaCopy<4>(S.matConstant, matConstLds, S.nMaterials);
+    }
+    DmaWait();
+    __syncthreads();
+    T->sensorL = (const LdsF4 *)sensorLds;
+    T->permL = (const LdsU16 *)permLds;
+    T->SL = S;
+    if (lay.lightsInLds) T->SL.lightNodes = nodesLds;
+    T->lightsL = lay.lightsInLds ? lightsLds : S.lights;
+    T->matsL = lay.matsInLds ? matsLds : S.matCoeffs;
+    T->matConstL = lay.matsInLds ? matConstLds : S.matConstant;
+}
+
+// GenerateRaySamples (samples.cpp:29-66): dims d0 + {0..6} = direct.uc, direct.u (2),
+// indirect.uc, indirect.u (2), rr; Halton digit permutations come from the LDS tables
+struct RaySamples {
+    float dUc, dU0, dU1, iUc, iU0, iU1, rr;
+};
+template <bool IndirectUc>
+__device__ __forceinline__ RaySamples GenerateRaySamples(const DeviceScene &S, const ShadeTables &T, int px, int py,
+                                                         int sampleIndex, int d0) {
+    RaySamples r;
+    r.iUc = 0;
+    if (S.samplerType == 1) {
+        const uint64_t morton = ZSobolMortonIndex(S.zs, px, py, sampleIndex);
+        r.dUc = ZSobolGet1D(S.zs, morton, d0, S.zsPerms, S.sobolM1);
+        ZSobolGet2D(S.zs, morton, d0 + 1, S.zsPerms, S.sobolM1, &r.dU0, &r.dU1);
+        if (IndirectUc) r.iUc = ZSobolGet1D(S.zs, morton, d0 + 3, S.zsPerms, S.sobolM1);
+        ZSobolGet2D(S.zs, morton, d0 + 4, S.zsPerms, S.sobolM1, &r.iU0, &r.iU1);
+        r.rr = ZSobolGet1D(S.zs, morton, d0 + 6, S.zsPerms, S.sobolM1);
+    } else {
+        const Halton h = StartPixelSample(S, px, py, sampleIndex, d0);
+        auto dim = [&](int k) -> float {
+            const HaltonDimDesc hd = S.haltonDim[d0 + k];
+            if ((h.index >> 32) == 0 && hd.fast && hd.nDigits <= (uint32_t)kMaxMagicDigits)
+                return ScrambledRadicalInverse32Magic<kMaxMagicDigits>(hd, (uint32_t)h.index, T.permL + T.permOff[k]);
+            return ScrambledRadicalInverse(hd.base, hd.nDigits, h.index, S.perm + hd.permOffset);
+        };
+        r.dUc = dim(0);
+        r.dU0 = dim(1);
+        r.dU1 = dim(2);
+        if (IndirectUc) r.iUc = dim(3);
+        r.iU0 = dim(4);
+        r.iU1 = dim(5);
+        r.rr = dim(6);
+    }
+    return r;
+}
+
+__global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(DeviceScene S, PathState st, int depth) {
+    const QueueView mats = LoadQueue(st, depth, kCntMat);
+    if ((int)(blockIdx.x * blockDim.x) >= mats.total) return;  // no work
+    extern __shared__ float4 dynLds[];
+    ShadeTables T;
+    StageShadeTables(S, depth, reinterpret_cast<char *>(dynLds), &T);
+    const ShadeLdsLayout &lay = T.lay;
+    float *bfLds = T.bfLds;
+    float *denseLds = T.denseLds;
+    const LdsF4 *sensorL = T.sensorL;
+    const DeviceScene &SL = T.SL;
+    const DeviceAreaLight *lightsL = T.lightsL;
+    const float4 *matsL = T.matsL;
+    const int *matConstL = T.matConstL;
+    const int d0 = 6 + 7 * depth;  // first sampler dimension of this depth
 
     const int N = st.NR;  // record stride
     const int count = mats.total;
@@ -1068,7 +1142,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
         int qi = base + threadIdx.x;
         bool active = qi < count;
         bool pushRay = false, pushShadow = false;
-        const int ri = active ? st.matQ[QueueSlot(mats, qi)] : 0;  // this depth's record
+        const int ri = active ? st.matQ[0][QueueSlot(mats, qi)] : 0;  // this depth's record
         // outputs kept to the (block-wide) queue appends: shadow ray, continuing path
         V3 sOrg, sDir, sL, nOrg, nDir;
         float nRl = 0, nEta = 1;
@@ -1107,29 +1181,9 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
             {
                 // ---- GenerateRaySamples (samples.cpp:29-66): dims 6 + 7 * depth + {0..6}
                 // = direct.uc, direct.u (2), indirect.uc, indirect.u (2), rr
-                float dUc, dU0, dU1, iU0, iU1, rr;  // dim 3 (indirect.uc) is unused by DiffuseBxDF
-                if (S.samplerType == 1) {
-                    const uint64_t morton = ZSobolMortonIndex(S.zs, px, py, sampleIndex);
-                    dUc = ZSobolGet1D(S.zs, morton, d0, S.zsPerms, S.sobolM1);
-                    ZSobolGet2D(S.zs, morton, d0 + 1, S.zsPerms, S.sobolM1, &dU0, &dU1);
-                    ZSobolGet2D(S.zs, morton, d0 + 4, S.zsPerms, S.sobolM1, &iU0, &iU1);
-                    rr = ZSobolGet1D(S.zs, morton, d0 + 6, S.zsPerms, S.sobolM1);
-                } else {
-                    const Halton h = StartPixelSample(S, px, py, sampleIndex, d0);
-                    auto dim = [&](int k) -> float {
-                        const HaltonDimDesc hd = S.haltonDim[d0 + k];
-                        if ((h.index >> 32) == 0 && hd.fast && hd.nDigits <= (uint32_t)kMaxMagicDigits)
-                            return ScrambledRadicalInverse32Magic<kMaxMagicDigits>(hd, (uint32_t)h.index,
-                                                                                   permL + permOff[k]);
-                        return ScrambledRadicalInverse(hd.base, hd.nDigits, h.index, S.perm + hd.permOffset);
-                    };
-                    dUc = dim(0);
-                    dU0 = dim(1);
-                    dU1 = dim(2);
-                    iU0 = dim(4);
-                    iU1 = dim(5);
-                    rr = dim(6);
-                }
+                // dim 3 (indirect.uc) is unused by DiffuseBxDF
+                const RaySamples rs = GenerateRaySamples<false>(S, T, px, py, sampleIndex, d0);
+                const float dUc = rs.dUc, dU0 = rs.dU0, dU1 = rs.dU1, iU0 = rs.iU0, iU1 = rs.iU1, rr = rs.rr;
                 SEC_MARK(st, 1);
                 // ---- DiffuseMaterial::GetBxDF: R = clamp(reflectance(lambda), 0, 1); f = R / pi
                 // (bxdfs.h DiffuseBxDF::f).  bf_i = beta_i * f_i is formed once per wavelength
@@ -1280,6 +1334,266 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
     }
 }
 
+// EvaluateMaterialAndBSDF<DielectricMaterial | ConductorMaterial> (surfscatter.cpp:57-328) with
+// GenerateRaySamples, over that material type's queue.  Same staging and queue appends as
+// k_shade_diffuse; the BSDF is TrowbridgeReitz microfacet (core.h: DielectricSample/Eval,
+// ConductorSample/Eval).  f differs between the light sample and the BSDF sample, so beta stays
+// in bfLds and each 31-wavelength loop forms beta_i * f_i itself.  Specular BSDFs skip light
+// sampling (IsNonSpecular(flags), surfscatter.cpp:253).
+template <int MT>
+__global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(DeviceScene S, PathState st, int depth) {
+    const QueueView mats = LoadQueue(st, depth, MatCounter(MT));
+    if ((int)(blockIdx.x * blockDim.x) >= mats.total) return;  // no work
+    extern __shared__ float4 dynLds[];
+    ShadeTables T;
+    StageShadeTables(S, depth, reinterpret_cast<char *>(dynLds), &T);
+    const ShadeLdsLayout &lay = T.lay;
+    const int d0 = 6 + 7 * depth;
+    const int N = st.NR;
+    const int count = mats.total;
+    const int shard = ProducerShard();
+    int *nextCounter = &st.counters[CounterIndex(depth + 1, kCntRay, shard)];
+    int *shadowCounter = &st.counters[CounterIndex(depth, kCntShadow, shard)];
+    const int shardBase = shard * st.capS;
+    const PathRecords &rec = st.rec[depth & 1], &out = st.rec[(depth + 1) & 1];
+    const int *hitPrim = st.hitPrim[depth & 1];
+    const float *hitB = st.hitB[depth & 1];
+    const int *queue = st.matQ[MT];
+    for (int base = blockIdx.x * blockDim.x; base < count; base += gridDim.x * blockDim.x) {
+        int qi = base + threadIdx.x;
+        bool active = qi < count;
+        bool pushRay = false, pushShadow = false;
+        const int ri = active ? queue[QueueSlot(mats, qi)] : 0;
+        V3 sOrg, sDir, sL, nOrg, nDir;
+        float nRl = 0, nEta = 1;
+        int nFlags = 0;
+        int slot = 0;
+        float lambda0 = 0;
+        float *bf = T.bfLds + threadIdx.x;  // beta_i at bf[i * kBlock]
+        if (active) {
+            lambda0 = rec.lambda0[ri];
+            slot = depth > 0 ? rec.pixel[ri] : ri;
+            const int inFlags = depth > 0 ? rec.flags[ri] : 0;
+            const int prim = hitPrim[ri];
+            const float b0 = hitB[ri], b1 = hitB[N + ri], b2 = hitB[2 * N + ri];
+            const V3 rd(rec.ray[3 * N + ri], rec.ray[4 * N + ri], rec.ray[5 * N + ri]);
+            int px, py, sampleIndex;
+            PixelOf(st, slot, &px, &py, &sampleIndex);
+            px += S.px0;
+#pragma unroll 8
+            for (int i = 0; i < kNSpectrumSamples; ++i) bf[i * kBlock] = depth > 0 ? rec.beta[(size_t)i * N + ri] : 1.f;
+            V3 p0, p1, p2;
+            PrimVerts(S, prim, &p0, &p1, &p2);
+            const int mat = S.primMaterial[prim];
+            const TriSurface surf = TriangleSurface(p0, p1, p2, b0, b1, b2, S.primFlip[prim]);
+            const V3 wo = Normalize(-rd);
+            const V3 n = surf.n, ns = surf.n;
+            const RaySamples rs = GenerateRaySamples<MT == kMatDielectricT>(S, T, px, py, sampleIndex, d0);
+            // ---- Material::GetBxDF (materials.h:182-204 dielectric, :491-511 conductor)
+            const float4 mp = S.matParams[mat];
+            TrowbridgeReitz tr{mp.x, mp.y};
+            if (S.regularize && (inFlags & 2)) tr.Regularize();  // surfscatter.cpp:127-128
+            float eta = mp.z;
+            if (eta == 0) eta = 1;
+            // conductor eta_i / k_i: piecewise-linear spectra, or from the albedo "reflectance"
+            const int etaSpec = MT == kMatConductorT ? S.matSpectra[2 * mat] : -1;
+            const int kSpec = MT == kMatConductorT ? S.matSpectra[2 * mat + 1] : -1;
+            const float4 mc = T.matsL[mat];
+            auto etaK = [&](float lam, float *e, float *k) {
+                if (etaSpec >= 0) {
+                    const int a = S.plOffsets[etaSpec], na = S.plOffsets[etaSpec + 1] - a;
+                    const int b = S.plOffsets[kSpec], nb = S.plOffsets[kSpec + 1] - b;
+                    *e = PiecewiseLinearEval(S.plLambda + a, S.plValue + a, na, lam);
+                    *k = PiecewiseLinearEval(S.plLambda + b, S.plValue + b, nb, lam);
+                } else {
+                    float r = Clampf(SigmoidPolynomial(mc.x, mc.y, mc.z, lam), 0, .9999f);
+                    *e = 1.f;
+                    *k = 2 * std::sqrt(r) / std::sqrt(std::fmax(0.f, 1 - r));
+                }
+            };
+            const Frame frame = Frame::FromXZ(Normalize(surf.dpdu), ns);
+            const V3 woL = frame.ToLocal(wo);
+            const V3 pi = surf.p, pe = surf.pErr;
+            const bool smooth = tr.EffectivelySmooth();
+            const bool reflective = MT == kMatConductorT || eta != 1;
+            const bool transmissive = MT == kMatDielectricT;
+            // ---- light sampling + shadow ray (surfscatter.cpp:252-326)
+            if (!smooth) {
+                V3 cp = pi;
+                if (reflective && !transmissive) cp = OffsetRayOrigin(pi, pe, n, wo);
+                else if (transmissive && reflective) cp = OffsetRayOrigin(pi, pe, n, -wo);
+                int li;
+                float lpmf;
+                if (SampleLight(T.SL, cp, ns, rs.dUc, &li, &lpmf) && li < S.nAreaLights) {
+                    const DeviceAreaLight &Ld = T.lightsL[li];
+                    V3 q0(Ld.v0.x, Ld.v0.y, Ld.v0.z), q1(Ld.v1.x, Ld.v1.y, Ld.v1.z), q2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
+                    V3 lp, lpe, ln;
+                    float lpdf;
+                    if (SampleTriangle(q0, q1, q2, Ld.flip, cp, n, ns, rs.dU0, rs.dU1, &lp, &lpe, &ln, &lpdf) &&
+                        lpdf != 0 && LengthSquared(lp - cp) != 0) {
+                        const V3 wi = Normalize(lp - cp);
+                        const V3 wiL = frame.ToLocal(wi);
+                        if ((Ld.twoSided || DotN(ln, -wi) >= 0) && woL.z != 0) {
+                            // BSDF::f / BSDF::PDF (bsdf.h:60-135)
+                            float fd = 0, bsdfPDF = 0;
+                            ConductorTerms ct{};
+                            bool fAny;
+                            if constexpr (MT == kMatDielectricT) {
+                                fd = DielectricEval(eta, tr, woL, wiL, &bsdfPDF);
+                                fAny = fd != 0;
+                            } else {
+                                ct = ConductorEval(tr, woL, wiL);
+                                bsdfPDF = ct.pdf;
+                                fAny = ct.ok;  // f_i may still vanish; a zero Ld adds nothing
+                            }
+                            if (fAny) {
+                                const float absdot = AbsDotN(ns, wi);
+                                const float lightPDF = lpdf * lpmf;
+                                const float invDenom = 1 / Avg31(bsdfPDF + lightPDF);
+                                const float *dense = lay.denseInLds ? nullptr : S.dense + Ld.spectrum * kDenseN;
+                                const LdsF *denseL = (const LdsF *)T.denseLds + Ld.spectrum * kDenseN;
+                                SensorAcc acc;
+                                bool nz = false;
+#pragma unroll 2
+                                for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next()) {
+                                    const int off = DenseOffset(it.lam);
+                                    const float Le =
+                                        Ld.scale * (off < 0 ? 0.f : (lay.denseInLds ? float(denseL[off]) : dense[off]));
+                                    nz |= Le != 0;
+                                    float f = fd;
+                                    if constexpr (MT == kMatConductorT) {
+                                        float e, k;
+                                        etaK(it.lam, &e, &k);
+                                        f = ConductorF(ct, e, k);
+                                    }
+                                    acc.Add(T.sensorL, off, bf[it.i * kBlock] * f * absdot * Le * invDenom, it.i == 0);
+                                }
+                                if (nz) {
+                                    sOrg = OffsetRayOrigin(pi, pe, n, lp - pi);
+                                    const V3 pt = OffsetRayOrigin(lp, lpe, ln, sOrg - lp);
+                                    sDir = pt - sOrg;
+                                    sL = V3(S.imagingRatio * (acc.sx / kNSpectrumSamples),
+                                            S.imagingRatio * (acc.sy / kNSpectrumSamples),
+                                            S.imagingRatio * (acc.sz / kNSpectrumSamples));
+                                    pushShadow = true;
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+            // ---- BSDF::Sample_f + RR + indirect ray (surfscatter.cpp:183-250)
+            if (woL.z != 0) {
+                bool ok;
+                V3 wiL;
+                float pdf, fd = 0, etap = 1;
+                bool specular, transmission;
+                ConductorTerms ct{};
+                if constexpr (MT == kMatDielectricT) {
+                    const BxSample bs = DielectricSample(eta, tr, woL, rs.iUc, rs.iU0, rs.iU1);
+                    ok = bs.ok && bs.f != 0;
+                    wiL = bs.wi;
+                    pdf = bs.pdf;
+                    fd = bs.f;
+                    etap = bs.etap;
+                    specular = bs.flags & kBxSpecular;
+                    transmission = bs.flags & kBxTransmission;
+                } else {
+                    ct = ConductorSample(tr, woL, rs.iU0, rs.iU1);
+                    ok = ct.ok;
+                    wiL = ct.wi;
+                    pdf = ct.pdf;
+                    specular = ct.specular;
+                    transmission = false;
+                }
+                if (ok && pdf != 0 && wiL.z != 0) {
+                    const V3 wi = frame.FromLocal(wiL);
+                    const float absdot = AbsDotN(ns, wi);
+                    float etaScale = depth > 0 ? rec.etaScale[ri] : 1.f;
+                    if (transmission) etaScale *= Sqr(etap);
+                    const float avgRu = Avg31(1.f);
+                    float mx = -kInfinity;
+                    bool fAny = MT == kMatDielectricT;
+#pragma unroll 2
+                    for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next()) {
+                        float f = fd;
+                        if constexpr (MT == kMatConductorT) {
+                            float e, k;
+                            etaK(it.lam, &e, &k);
+                            f = ConductorF(ct, e, k);
+                            fAny |= f != 0;
+                        }
+                        const float nbv = bf[it.i * kBlock] * f * absdot / pdf;
+                        bf[it.i * kBlock] = nbv;
+                        mx = fmaxf(mx, nbv * etaScale / avgRu);
+                    }
+                    if (fAny) {
+                        bool kill = false;
+                        float q = 0;
+                        if (mx < 1 && depth >= 1) {
+                            q = fmaxf(0.f, 1 - mx);
+                            kill = rs.rr < q;
+                        }
+                        if (!kill) {
+                            const bool rrScale = mx < 1 && depth >= 1;
+                            bool nz = false;
+#pragma unroll 4
+                            for (int i = 0; i < kNSpectrumSamples; ++i) {
+                                float nbv = bf[i * kBlock];
+                                if (rrScale) nbv /= 1 - q;
+                                nz |= nbv != 0;
+                                bf[i * kBlock] = nbv;
+                            }
+                            if (nz) {
+                                nOrg = OffsetRayOrigin(pi, pe, n, wi);
+                                nDir = wi;
+                                nRl = 1.f / pdf;
+                                nEta = etaScale;
+                                nFlags = (specular ? 1 : 0) | ((!specular || (inFlags & 2)) ? 2 : 0);
+                                pushRay = true;
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        int *const cnt[2] = {nextCounter, shadowCounter};
+        const bool pred[2] = {pushRay, pushShadow};
+        int pos[2];
+        BlockPush<2>(cnt, pred, pos);
+        if (pos[1] >= 0) {
+            const int j = shardBase + pos[1];
+            st.shadowRay[j] = sOrg.x;
+            st.shadowRay[N + j] = sOrg.y;
+            st.shadowRay[2 * N + j] = sOrg.z;
+            st.shadowRay[3 * N + j] = sDir.x;
+            st.shadowRay[4 * N + j] = sDir.y;
+            st.shadowRay[5 * N + j] = sDir.z;
+            st.shadowL[j] = sL.x;
+            st.shadowL[N + j] = sL.y;
+            st.shadowL[2 * N + j] = sL.z;
+            st.shadowPixel[j] = slot;
+        }
+        if (pos[0] >= 0) {
+            const int j = shardBase + pos[0];
+#pragma unroll 8
+            for (int i = 0; i < kNSpectrumSamples; ++i) out.beta[(size_t)i * N + j] = bf[i * kBlock];
+            out.ray[j] = nOrg.x;
+            out.ray[N + j] = nOrg.y;
+            out.ray[2 * N + j] = nOrg.z;
+            out.ray[3 * N + j] = nDir.x;
+            out.ray[4 * N + j] = nDir.y;
+            out.ray[5 * N + j] = nDir.z;
+            out.lambda0[j] = lambda0;
+            out.rl[j] = nRl;
+            out.etaScale[j] = nEta;
+            out.flags[j] = nFlags;
+            out.pixel[j] = slot;
+            out.prevIdx[j] = ri;
+        }
+    }
+}
+
 __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_shadow(DeviceScene S, PathState st, int depth) {
     const QueueView shadows = LoadQueue(st, depth, kCntShadow);
     if ((int)(blockIdx.x * blockDim.x) >= shadows.total) return;  // no work
@@ -1391,8 +1705,12 @@ hipError_t LaunchCamera(const DeviceScene &S, const PathState &st, int nActive, 
 }
 hipError_t LaunchClosest(const DeviceScene &S, const PathState &st, int depth, int maxCount, int timed,
                          hipStream_t s) {
-    hipLaunchKernelGGL(k_closest, dim3(TraversalGridFor(maxCount)), dim3(kBlock), StackBytes(S), s, S, st, depth,
-                       timed);
+    if (S.matTypeMask & ~1)
+        hipLaunchKernelGGL(k_closest<kNumMatTypes>, dim3(TraversalGridFor(maxCount)), dim3(kBlock), StackBytes(S), s, S,
+                           st, depth, timed);
+    else
+        hipLaunchKernelGGL(k_closest<1>, dim3(TraversalGridFor(maxCount)), dim3(kBlock), StackBytes(S), s, S, st,
+                           depth, timed);
     return hipGetLastError();
 }
 hipError_t LaunchEscaped(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s) {
@@ -1406,6 +1724,16 @@ hipError_t LaunchEmissive(const DeviceScene &S, const PathState &st, int depth, 
 hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s) {
     hipLaunchKernelGGL(k_shade_diffuse, dim3(ShadeGridFor(maxCount)), dim3(kBlock), (size_t)S.shadeLds.total, s,
                        S, st, depth);
+    return hipGetLastError();
+}
+hipError_t LaunchShadeMicrofacet(const DeviceScene &S, const PathState &st, int depth, int type, int maxCount,
+                                 hipStream_t s) {
+    if (type == kMatDielectricT)
+        hipLaunchKernelGGL(k_shade_microfacet<kMatDielectricT>, dim3(ShadeGridFor(maxCount)), dim3(kBlock),
+                           (size_t)S.shadeLds.total, s, S, st, depth);
+    else
+        hipLaunchKernelGGL(k_shade_microfacet<kMatConductorT>, dim3(ShadeGridFor(maxCount)), dim3(kBlock),
+                           (size_t)S.shadeLds.total, s, S, st, depth);
     return hipGetLastError();
 }
 hipError_t LaunchShadow(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s) {

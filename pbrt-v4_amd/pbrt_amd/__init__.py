@@ -64,6 +64,10 @@ class SceneFlat(ctypes.Structure):
         ("perm_ndigits", ctypes.POINTER(ctypes.c_uint32)), ("perm_base", ctypes.POINTER(ctypes.c_uint32)),
         ("sampler_type", ctypes.c_int), ("zs_randomize", ctypes.c_int), ("zs_log2_spp", ctypes.c_int),
         ("zs_nbase4_digits", ctypes.c_int),
+        ("material_type", ctypes.POINTER(ctypes.c_int32)), ("material_params", ctypes.POINTER(ctypes.c_float)),
+        ("material_spectra", ctypes.POINTER(ctypes.c_int32)), ("n_pl_spectra", ctypes.c_int),
+        ("pl_offsets", ctypes.POINTER(ctypes.c_int32)), ("pl_lambda", ctypes.POINTER(ctypes.c_float)),
+        ("pl_value", ctypes.POINTER(ctypes.c_float)), ("regularize", ctypes.c_int),
     ]
 
 
@@ -86,7 +90,8 @@ EXPORTED_SYMBOLS = [
     "pbrt_context_free", "pbrt_render", "pbrt_synchronize", "pbrt_get_stats", "pbrt_reset_stats",
     "pbrt_film_clear", "pbrt_film_device_ptr", "pbrt_film_read", "pbrt_film_get_rgb", "pbrt_intersect",
     "pbrt_debug_halton", "pbrt_debug_rgb_coeffs", "pbrt_debug_rgb2spec_column", "pbrt_debug_kernel_sections",
-    "pbrt_debug_queue_counts", "pbrt_debug_zsobol",
+    "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
+    "pbrt_debug_named_spectrum", "pbrt_debug_bxdf",
 ]
 
 _LIB = None
@@ -127,9 +132,52 @@ def _lib():
     lib.pbrt_debug_kernel_sections.argtypes = [c.c_void_p, c.POINTER(c.c_uint64), c.c_int]
     lib.pbrt_debug_zsobol.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_int, c.POINTER(c.c_float)]
     lib.pbrt_debug_queue_counts.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_int]
+    lib.pbrt_debug_trowbridge.argtypes = [c.c_void_p, c.c_void_p]
+    lib.pbrt_debug_fresnel.argtypes = [c.c_void_p, c.c_void_p]
+    lib.pbrt_debug_named_spectrum.argtypes = [c.c_char_p, c.c_void_p, c.c_int, c.c_void_p]
+    lib.pbrt_debug_bxdf.argtypes = [c.c_int] + [c.c_void_p] * 7
     lib.pbrt_set_data_dir(str(DATA_DIR).encode())
     _LIB = lib
     return lib
+
+
+def _f32(a, n=None):
+    a = np.ascontiguousarray(np.asarray(a, dtype=np.float32))
+    if n is not None and a.size != n:
+        raise PbrtError(f"expected {n} values, got {a.size}")
+    return a
+
+
+def debug_trowbridge(in13):
+    """TrowbridgeReitzDistribution terms as the product computes them (see pbrt_amd.h)."""
+    i, o = _f32(in13, 13), np.zeros(14, np.float32)
+    _check(_lib().pbrt_debug_trowbridge(i.ctypes.data, o.ctypes.data))
+    return o
+
+
+def debug_fresnel(in10):
+    i, o = _f32(in10, 10), np.zeros(10, np.float32)
+    _check(_lib().pbrt_debug_fresnel(i.ctypes.data, o.ctypes.data))
+    return o
+
+
+def named_spectrum(name, lambdas):
+    """GetNamedSpectrum(name)(lambda) for the metal / glass tables."""
+    lam = _f32(lambdas)
+    o = np.zeros(lam.size, np.float32)
+    _check(_lib().pbrt_debug_named_spectrum(name.encode(), lam.ctypes.data, lam.size, o.ctypes.data))
+    return o
+
+
+def debug_bxdf(bxdf_type, params3, wo, wi, u3, eta31=None, k31=None):
+    """Sample_f / f / PDF of DielectricBxDF (1) or ConductorBxDF (2): 70 floats (pbrt_amd.h)."""
+    p, a, b, u = _f32(params3, 3), _f32(wo, 3), _f32(wi, 3), _f32(u3, 3)
+    e = _f32(eta31 if eta31 is not None else np.ones(31), 31)
+    k = _f32(k31 if k31 is not None else np.zeros(31), 31)
+    o = np.zeros(70, np.float32)
+    _check(_lib().pbrt_debug_bxdf(int(bxdf_type), p.ctypes.data, e.ctypes.data, k.ctypes.data, a.ctypes.data,
+                                  b.ctypes.data, u.ctypes.data, o.ctypes.data))
+    return o
 
 
 def _check(rc):
@@ -237,11 +285,12 @@ class WavefrontPathIntegrator:
         _check(_lib().pbrt_reset_stats(self._h))
 
     def queue_counts(self):
-        """Per-depth queue sizes of the last pass: rows of (rays, material, shadow, escaped, emissive)."""
+        """Per-depth queue sizes of the last pass: rows of (rays, diffuse material, shadow, escaped,
+        emissive, dielectric material, conductor material)."""
         n = 8 * (self.info.max_depth + 3)
         out = (ctypes.c_int32 * n)()
         _check(_lib().pbrt_debug_queue_counts(self._h, out, n))
-        return np.array(out[:], dtype=np.int64).reshape(-1, 8)[:, :5]
+        return np.array(out[:], dtype=np.int64).reshape(-1, 8)[:, :7]
 
     def kernel_sections(self, n=32):
         """Summed wave cycles per instrumented kernel section (profiling build only)."""

@@ -11,6 +11,9 @@ reference's sources
                                  CIE_Illum_D6500 (:770)
     src/pbrt/cmd/rgb2spec_opt.cpp cie_x / cie_y / cie_z / cie_d65 (:46-128),
                                  xyz_to_srgb / srgb_to_xyz (:191-197)
+    src/pbrt/util/spectrum.cpp   the interleaved (lambda, value) tables behind the named
+                                 metal and glass spectra (:1128-1440), keyed by the names
+                                 Spectra::Init registers them under (:2666-2690)
 
 and writes pbrt-v4_amd/data/spectral_data.json, which is committed.  Run it only in a
 container that has /root/reference; the GPU box uses the committed JSON.
@@ -24,6 +27,18 @@ REF = Path("/root/reference/src/pbrt")
 OUT = Path(__file__).resolve().parents[1] / "pbrt-v4_amd" / "data" / "spectral_data.json"
 
 NUM = r"[-+]?(?:\d+\.?\d*|\.\d+)(?:[eE][-+]?\d+)?"
+
+
+# name -> array as registered in Spectra::Init's namedSpectra map (util/spectrum.cpp:2666-2690)
+NAMED = {
+    "glass-BK7": "GlassBK7_eta", "glass-BAF10": "GlassBAF10_eta", "glass-FK51A": "GlassFK51A_eta",
+    "glass-LASF9": "GlassLASF9_eta", "glass-F5": "GlassSF5_eta", "glass-F10": "GlassSF10_eta",
+    "glass-F11": "GlassSF11_eta",
+    "metal-Ag-eta": "Ag_eta", "metal-Ag-k": "Ag_k", "metal-Al-eta": "Al_eta", "metal-Al-k": "Al_k",
+    "metal-Au-eta": "Au_eta", "metal-Au-k": "Au_k", "metal-Cu-eta": "Cu_eta", "metal-Cu-k": "Cu_k",
+    "metal-CuZn-eta": "CuZn_eta", "metal-CuZn-k": "CuZn_k", "metal-MgO-eta": "MgO_eta",
+    "metal-MgO-k": "MgO_k", "metal-TiO2-eta": "TiO2_eta", "metal-TiO2-k": "TiO2_k",
+}
 
 
 def array_body(text, name):
@@ -66,6 +81,10 @@ def main():
     for name in ("xyz_to_srgb", "srgb_to_xyz"):
         data["opt_" + name] = numbers(array_body(opt, name))
         assert len(data["opt_" + name]) == 9
+    for name, arr in NAMED.items():
+        vals = numbers(array_body(spec, arr))
+        assert len(vals) % 2 == 0 and len(vals) >= 4, (name, len(vals))
+        data["named:" + name] = vals
     OUT.parent.mkdir(parents=True, exist_ok=True)
     OUT.write_text(json.dumps(data))
     print("wrote", OUT, {k: len(v) if isinstance(v, list) else v for k, v in data.items()})

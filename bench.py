@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Benchmark: Msamples/s of the MI355X wavefront path tracer on BASELINE.json's headline
 configuration (configs[1]): synthetic Cornell box, 1280x720, 64 spp, PathIntegrator maxdepth
-5 semantics (wavefront volpath), Halton sampler, diffuse-only BxDFs.
+5 semantics (wavefront volpath), Halton sampler, diffuse-only BxDFs.  ``--workload c3`` runs
+configs[2] instead (scenes/gen_c3.py: 30k-triangle displaced dielectric icosphere + rough
+conductor floor, 1920x1080, 256 spp, ZSobol) -- a second line, not the headline.
 
 One "step" = one complete render of that image (all 64 samples per pixel, film cleared
 first) plus, for N > 1, the single RCCL sum-reduce of the film over xGMI.  Pixel rows are
@@ -38,15 +40,31 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--workload", choices=["c2", "c3"], default="c2")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--xres", type=int, default=1280)
-    ap.add_argument("--yres", type=int, default=720)
-    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--xres", type=int, default=None)
+    ap.add_argument("--yres", type=int, default=None)
+    ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--max-paths", type=int, default=1 << 22)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    return ap.parse_args()
+    a = ap.parse_args()
+    d = {"c2": (1280, 720, 64), "c3": (1920, 1080, 256)}[a.workload]
+    a.xres = a.xres or d[0]
+    a.yres = a.yres or d[1]
+    a.spp = a.spp or d[2]
+    return a
+
+
+def load(args):
+    import pbrt_amd as pa
+    if args.workload == "c3":
+        sys.path.insert(0, str(ROOT / "scenes"))
+        import gen_c3
+        return pa.Scene.from_string(gen_c3.scene_text(args.xres, args.yres, args.spp), ROOT / "scenes")
+    return pa.load_scene(ROOT / "scenes" / "cornell-box.pbrt", xresolution=args.xres, yresolution=args.yres,
+                         spp=args.spp)
 
 
 def cpu_baseline(args, threads):
@@ -56,10 +74,11 @@ def cpu_baseline(args, threads):
     import numpy as np
     import pbrt_amd as pa
     import pyoracle
-    sc = pa.load_scene(ROOT / "scenes" / "cornell-box.pbrt", xresolution=args.xres, yresolution=args.yres, spp=args.spp)
+    sc = load(args)
     i = sc.info
-    rows = np.arange(i.py0, i.py1, 1, dtype=np.int32)
-    spp = 16
+    # C2: every row, 16 of 64 spp; C3: every 8th row, 4 of 256 spp (~10 s of host work)
+    rows = np.arange(i.py0, i.py1, 1 if args.workload == "c2" else 8, dtype=np.int32)
+    spp = 16 if args.workload == "c2" else 4
     pyoracle.lib()
     t = time.perf_counter()
     pyoracle.render(sc, rows=rows, first_sample=0, n_samples=spp, threads=threads)
@@ -94,8 +113,7 @@ def main():
     import pbrt_amd as pa
     from pbrt_amd.tiles import film_tensor_from_device_ptr, rows_for_rank
 
-    scene = pa.load_scene(ROOT / "scenes" / "cornell-box.pbrt", xresolution=args.xres, yresolution=args.yres,
-                          spp=args.spp)
+    scene = load(args)
     info = scene.info
     integ = pa.WavefrontPathIntegrator(scene, device=local_rank, max_paths=args.max_paths)
     rows = rows_for_rank(info.py0, info.py1, rank, world)
@@ -137,7 +155,7 @@ def main():
     mean_launch_s = st.closest_ms / 1e3 / launches
     bytes_per_launch = BYTES_PER_RAY_CLOSEST * st.timed_closest_rays / launches
     achieved = bytes_per_launch / mean_launch_s / 1e9 if mean_launch_s > 0 else 0.0
-    traffic = pmc_traffic()
+    traffic = pmc_traffic() if args.workload == "c2" else None  # the committed PMC pass is of C2
 
     if rank == 0:
         cpu = None
@@ -147,7 +165,7 @@ def main():
             except Exception as e:  # the baseline is reported, never required
                 cpu = {"value": None, "error": str(e)}
         line = {
-            "metric": "Msamples/sec (paths x spp / s) at 1280x720x64spp",
+            "metric": f"Msamples/sec (paths x spp / s) at {args.xres}x{args.yres}x{info.spp}spp",
             "value": round(value, 3),
             "unit": "Msamples/s",
             "n_gpus": world,
@@ -159,8 +177,12 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
-            "config": {"workload": f"cornell-box (synthetic) {args.xres}x{args.yres} {info.spp}spp maxdepth "
-                                   f"{info.max_depth} halton, wavefront volpath, diffuse BxDF (BASELINE configs[1])",
+            "config": {"workload": (f"cornell-box (synthetic) {args.xres}x{args.yres} {info.spp}spp maxdepth "
+                                    f"{info.max_depth} halton, wavefront volpath, diffuse BxDF (BASELINE configs[1])"
+                                    if args.workload == "c2" else
+                                    f"C3 killeroo stand-in (scenes/gen_c3.py) {args.xres}x{args.yres} {info.spp}spp "
+                                    f"maxdepth {info.max_depth} zsobol, dielectric + conductor + diffuse "
+                                    "(BASELINE configs[2])"),
                        "xres": args.xres, "yres": args.yres, "spp": info.spp, "max_depth": info.max_depth,
                        "triangles": info.n_triangles, "paths_per_pass": int(st.paths_per_pass),
                        "sharding": "16-row stripes round-robin over ranks + 1 RCCL film reduce" if world > 1 else

@@ -93,6 +93,11 @@ typedef struct pbrt_scene_flat {
     const int32_t *pl_offsets;        /* [n_pl_spectra + 1] into pl_lambda / pl_value */
     const float *pl_lambda, *pl_value;
     int regularize;                   /* integrator "regularize" */
+    /* shading attributes (TriangleMesh n / uv): per vertex, or NULL when no mesh has any;
+     * tri_shading[t] bit0 = triangle t uses vertex normals, bit1 = uv */
+    const float *vertex_normals;      /* [n_vertices][3] render space */
+    const float *vertex_uv;           /* [n_vertices][2] */
+    const uint8_t *tri_shading;       /* [n_triangles] */
 } pbrt_scene_flat;
 
 typedef struct pbrt_render_params {
@@ -155,6 +160,11 @@ int pbrt_debug_zsobol(const pbrt_scene *scene, int px, int py, int sample_index,
  *   refract_ok etap wt3 reflect3 */
 int pbrt_debug_trowbridge(const float *in13, float *out14);
 int pbrt_debug_fresnel(const float *in10, float *out10);
+/* Triangle::InteractionFromIntersection with optional vertex normals n9 / uv6 (NULL = absent)
+ * at barycentrics b3, and the normal of Triangle::Sample(u2): out15 = n3 shading.n3 dpdu3
+ * shading.dpdu3 sample_n3 (shapes.h:884-1046) */
+int pbrt_debug_triangle_shading(const float *p9, const float *n9, const float *uv6, int flip, const float *b3,
+                                const float *u2, float *out15);
 /* GetNamedSpectrum(name)(lambda_i) for the metal / glass tables */
 int pbrt_debug_named_spectrum(const char *name, const float *lambda, int n, float *out);
 /* DielectricBxDF (type 1) / ConductorBxDF (type 2) in the shading frame: params3 = alpha_x

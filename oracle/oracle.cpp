@@ -588,16 +588,24 @@ static void Point3fi(Vec v, Vec e, Vec *p, Vec *err) {
 }
 
 struct Interaction {
-    Vec p, err, n, ns, dpdu, wo;
+    Vec p, err, n, ns, dpdu, dpdus, wo;
     int prim = -1;
 };
 
-// shapes.h:884-1010 for meshes without n/s/uv
-static Interaction TriangleInteraction(Vec p0, Vec p1, Vec p2, bool flip, TriIsect ti, Vec rayD) {
+// a mesh triangle's optional vertex normals and uv (TriangleMesh n / uv, util/mesh.h:23-46)
+struct TriAttr {
+    bool hasN = false, hasUV = false;
+    Vec n[3];
+    Float uv[3][2] = {{0, 0}, {1, 0}, {1, 1}};
+};
+
+// Triangle::InteractionFromIntersection (shapes.h:884-1010) + SetShadingGeometry
+// (interaction.h:194-214, orientationIsAuthoritative = true); dndu/dndv are not needed
+static Interaction TriangleInteraction(Vec p0, Vec p1, Vec p2, bool flip, TriIsect ti, Vec rayD,
+                                       const TriAttr &a = TriAttr()) {
     Interaction si;
-    const Float uv[3][2] = {{0, 0}, {1, 0}, {1, 1}};
-    Float duv02[2] = {uv[0][0] - uv[2][0], uv[0][1] - uv[2][1]};
-    Float duv12[2] = {uv[1][0] - uv[2][0], uv[1][1] - uv[2][1]};
+    Float duv02[2] = {a.uv[0][0] - a.uv[2][0], a.uv[0][1] - a.uv[2][1]};
+    Float duv12[2] = {a.uv[1][0] - a.uv[2][0], a.uv[1][1] - a.uv[2][1]};
     Vec dp02 = p0 - p2, dp12 = p1 - p2;
     Float determinant = DifferenceOfProducts(duv02[0], duv12[1], duv02[1], duv12[0]);
     Vec dpdu, dpdv;
@@ -615,7 +623,21 @@ static Interaction TriangleInteraction(Vec p0, Vec p1, Vec p2, bool flip, TriIse
     si.n = Normalize(Cross(dp02, dp12));
     if (flip) si.n = -si.n;
     si.ns = si.n;
-    si.dpdu = dpdu;
+    si.dpdu = si.dpdus = dpdu;
+    if (a.hasN) {
+        Vec ns = ti.b0 * a.n[0] + ti.b1 * a.n[1] + ti.b2 * a.n[2];
+        ns = LengthSquared(ns) > 0 ? Normalize(ns) : si.n;
+        Vec ss = si.dpdu, ts = Cross(ns, ss);
+        if (LengthSquared(ts) > 0) ss = Cross(ts, ns);
+        else CoordinateSystem(ns, &ss, &ts);
+        si.ns = ns;
+        if (DotN(si.n, ns) < 0) si.n = -si.n;  // FaceForward(n, shading.n)
+        while (LengthSquared(ss) > 1e16f || LengthSquared(ts) > 1e16f) {
+            ss = ss / 1e8f;
+            ts = ts / 1e8f;
+        }
+        si.dpdus = ss;
+    }
     si.wo = Normalize(-rayD);
     return si;
 }
@@ -639,6 +661,21 @@ struct Scene {
     int xres, yres, px0, px1, py0, py1, maxDepth;
     Float frx, fry;
     Vec P(int t, int k) const { return v[tri[3 * t + k]]; }
+    TriAttr Attr(int t) const {
+        TriAttr a;
+        const int bits = f->tri_shading ? f->tri_shading[t] : 0;
+        for (int k = 0; k < 3; ++k) {
+            const int vi = tri[3 * t + k];
+            if (bits & 1) a.n[k] = Vec(f->vertex_normals[3 * vi], f->vertex_normals[3 * vi + 1], f->vertex_normals[3 * vi + 2]);
+            if (bits & 2) {
+                a.uv[k][0] = f->vertex_uv[2 * vi];
+                a.uv[k][1] = f->vertex_uv[2 * vi + 1];
+            }
+        }
+        a.hasN = bits & 1;
+        a.hasUV = bits & 2;
+        return a;
+    }
 
     int Build(int start, int end, std::vector<Vec> &cent) {
         BVHNode n;
@@ -858,14 +895,25 @@ struct ShapeSample {
     Float pdf;
 };
 static Float TriArea(Vec p0, Vec p1, Vec p2) { return 0.5f * Length(Cross(p1 - p0, p2 - p0)); }
-static bool TriangleSample(Vec p0, Vec p1, Vec p2, bool flip, Vec ref, Vec ns, Float u0, Float u1, ShapeSample *ss) {
+// Triangle::Sample(u)'s normal (shapes.h:1023-1029)
+static Vec SampledNormal(Vec p0, Vec p1, Vec p2, bool flip, const TriAttr &a, const Float b[3]) {
+    Vec n = Normalize(Cross(p1 - p0, p2 - p0));
+    if (a.hasN) {
+        Vec ns = b[0] * a.n[0] + b[1] * a.n[1] + (1 - b[0] - b[1]) * a.n[2];
+        if (DotN(n, ns) < 0) n = -n;
+    } else if (flip) {
+        n = n * -1.f;
+    }
+    return n;
+}
+static bool TriangleSample(Vec p0, Vec p1, Vec p2, bool flip, Vec ref, Vec ns, Float u0, Float u1, ShapeSample *ss,
+                           const TriAttr &a = TriAttr()) {
     Float solidAngle = SphericalTriangleArea(Normalize(p0 - ref), Normalize(p1 - ref), Normalize(p2 - ref));
     if (solidAngle < 3e-4f || solidAngle > 6.22f) {
         Float b[3];
         SampleUniformTriangle(u0, u1, b);
         Vec p = b[0] * p0 + b[1] * p1 + b[2] * p2;
-        Vec n = Normalize(Cross(p1 - p0, p2 - p0));
-        if (flip) n = n * -1.f;
+        Vec n = SampledNormal(p0, p1, p2, flip, a, b);
         Point3fi(p, gamma(6) * (Abs(b[0] * p0) + Abs(b[1] * p1) + Abs((1 - b[0] - b[1]) * p2)), &p, &ss->err);
         Float pdf = 1 / TriArea(p0, p1, p2);
         Vec wi = p - ref;
@@ -895,19 +943,18 @@ static bool TriangleSample(Vec p0, Vec p1, Vec p2, bool flip, Vec ref, Vec ns, F
     pdf *= triPDF;
     Point3fi(b[0] * p0 + b[1] * p1 + b[2] * p2, gamma(6) * (Abs(b[0] * p0) + Abs(b[1] * p1) + Abs((1 - b[0] - b[1]) * p2)),
              &ss->p, &ss->err);
-    Vec n = Normalize(Cross(p1 - p0, p2 - p0));
-    if (flip) n = n * -1.f;
-    ss->n = n;
+    ss->n = SampledNormal(p0, p1, p2, flip, a, b);
     ss->pdf = pdf;
     return true;
 }
-static Float TrianglePDF(Vec p0, Vec p1, Vec p2, bool flip, Vec ref, Vec refErr, Vec refN, Vec ns, Vec wi) {
+static Float TrianglePDF(Vec p0, Vec p1, Vec p2, bool flip, Vec ref, Vec refErr, Vec refN, Vec ns, Vec wi,
+                         const TriAttr &a = TriAttr()) {
     Float solidAngle = SphericalTriangleArea(Normalize(p0 - ref), Normalize(p1 - ref), Normalize(p2 - ref));
     if (solidAngle < 3e-4f || solidAngle > 6.22f) {
         Vec o = OffsetRayOrigin(ref, refErr, refN, wi);
         TriIsect ti;
         if (!IntersectTriangle(o, wi, Infinity, p0, p1, p2, &ti)) return 0;
-        Interaction si = TriangleInteraction(p0, p1, p2, flip, ti, wi);
+        Interaction si = TriangleInteraction(p0, p1, p2, flip, ti, wi, a);
         Float pdf = (1 / TriArea(p0, p1, p2)) / (AbsDotN(si.n, -wi) / DistanceSquared(ref, si.p));
         if (std::isinf(pdf)) pdf = 0;
         return pdf;
@@ -1420,7 +1467,7 @@ struct Renderer {
             }
             bool flip = f->tri_flip[prim];
             Vec p0 = S.P(prim, 0), p1 = S.P(prim, 1), p2 = S.P(prim, 2);
-            Interaction si = TriangleInteraction(p0, p1, p2, flip, ti, rd);
+            Interaction si = TriangleInteraction(p0, p1, p2, flip, ti, rd, S.Attr(prim));
             // HandleEmissiveIntersection
             int light = f->tri_light[prim];
             if (light >= 0 && (f->light_two_sided[light] || DotN(si.n, si.wo) >= 0)) {
@@ -1431,7 +1478,7 @@ struct Renderer {
                         Float lightChoicePDF = lights.PMF(prevP, prevNs, light);
                         int lp = f->light_prim[light];
                         Float lightPDF = lightChoicePDF * TrianglePDF(S.P(lp, 0), S.P(lp, 1), S.P(lp, 2), f->tri_flip[lp],
-                                                                      prevP, prevErr, prevN, prevNs, -si.wo);
+                                                                      prevP, prevErr, prevN, prevNs, -si.wo, S.Attr(lp));
                         Spectrum rl = r_l * lightPDF;
                         L = L + beta * Le / (r_u + rl).Average();
                     }
@@ -1478,7 +1525,7 @@ struct Renderer {
                 }
                 if (f->regularize && anyNonSpecular) bx.mf.Regularize();
             }
-            Vec fx_ = Normalize(si.dpdu), fz = si.ns, fy_ = Cross(fz, fx_);
+            Vec fx_ = Normalize(si.dpdus), fz = si.ns, fy_ = Cross(fz, fx_);
             auto toLocal = [&](Vec v) { return Vec(Dot(v, fx_), Dot(v, fy_), Dot(v, fz)); };
             auto fromLocal = [&](Vec v) { return fx_ * v.x + fy_ * v.y + fz * v.z; };
             Vec woL = toLocal(si.wo);
@@ -1520,7 +1567,8 @@ struct Renderer {
                 if (lights.Sample(cp, si.ns, dUc, &li, &lpmf) && li < f->n_area_lights) {
                     int lp = f->light_prim[li];
                     ShapeSample ss;
-                    if (TriangleSample(S.P(lp, 0), S.P(lp, 1), S.P(lp, 2), f->tri_flip[lp], cp, si.ns, dU0, dU1, &ss) &&
+                    if (TriangleSample(S.P(lp, 0), S.P(lp, 1), S.P(lp, 2), f->tri_flip[lp], cp, si.ns, dU0, dU1, &ss,
+                                       S.Attr(lp)) &&
                         ss.pdf != 0 && LengthSquared(ss.p - cp) != 0) {
                         Vec wi = Normalize(ss.p - cp);
                         Spectrum Le(0.f);
@@ -1735,6 +1783,28 @@ float oracle_halton(int xres, int yres, int seed, int px, int py, int sampleInde
     if (dim == -1) return a;
     if (dim == -2) return b;
     return s.Sample(std::max(2, dim));
+}
+
+void oracle_triangle_shading(const float *p9, const float *n9, const float *uv6, int flip, const float *b3,
+                             const float *u2, float *out) {
+    Vec p0(p9[0], p9[1], p9[2]), p1(p9[3], p9[4], p9[5]), p2(p9[6], p9[7], p9[8]);
+    TriAttr a;
+    if (n9) {
+        a.hasN = true;
+        for (int k = 0; k < 3; ++k) a.n[k] = Vec(n9[3 * k], n9[3 * k + 1], n9[3 * k + 2]);
+    }
+    if (uv6) {
+        a.hasUV = true;
+        for (int k = 0; k < 3; ++k) a.uv[k][0] = uv6[2 * k], a.uv[k][1] = uv6[2 * k + 1];
+    }
+    TriIsect ti{b3[0], b3[1], b3[2], 1};
+    Interaction si = TriangleInteraction(p0, p1, p2, flip != 0, ti, Vec(0, 0, 1), a);
+    Float b[3];
+    SampleUniformTriangle(u2[0], u2[1], b);
+    Vec sn = SampledNormal(p0, p1, p2, flip != 0, a, b);
+    float v[15] = {si.n.x, si.n.y, si.n.z, si.ns.x, si.ns.y, si.ns.z, si.dpdu.x, si.dpdu.y, si.dpdu.z,
+                   si.dpdus.x, si.dpdus.y, si.dpdus.z, sn.x, sn.y, sn.z};
+    std::memcpy(out, v, sizeof v);
 }
 
 void oracle_trowbridge(const float *in, float *out) {

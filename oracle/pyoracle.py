@@ -40,6 +40,7 @@ def lib():
         _lib.oracle_fresnel.argtypes = [vp, vp]
         _lib.oracle_named_spectrum.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, vp]
         _lib.oracle_bxdf.argtypes = [ctypes.c_int] + [vp] * 7
+        _lib.oracle_triangle_shading.argtypes = [vp] * 3 + [ctypes.c_int] + [vp] * 3
         _lib.oracle_render.argtypes = [vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, vp]
     return _lib
@@ -115,4 +116,15 @@ def bxdf(bxdf_type, params3, wo, wi, u3, eta31=None, k31=None):
             f32(k31 if k31 is not None else np.zeros(31)), f32(wo), f32(wi), f32(u3)]
     out = np.zeros(70, np.float32)
     lib().oracle_bxdf(int(bxdf_type), *[a.ctypes.data for a in arrs], out.ctypes.data)
+    return out
+
+
+def triangle_shading(p9, n9, uv6, flip, b3, u2):
+    p, b, u = f32(p9), f32(b3), f32(u2)
+    n = None if n9 is None else f32(n9)
+    t = None if uv6 is None else f32(uv6)
+    out = np.zeros(15, np.float32)
+    lib().oracle_triangle_shading(p.ctypes.data, None if n is None else n.ctypes.data,
+                                  None if t is None else t.ctypes.data, int(flip), b.ctypes.data, u.ctypes.data,
+                                  out.ctypes.data)
     return out

@@ -144,7 +144,7 @@ struct pbrt_context {
     DevBuf<float> triVerts, matCoeffs, lightScale, lightArea, infScale, dense, sensor;
     DevBuf<int> primMaterial, primLight, matConstant, lightPrim, lightSpectrum, lightTwoSided, infSpectrum;
     DevBuf<int> primOrig, matType, matSpectra, plOffsets;
-    DevBuf<float> matParams, plLambda, plValue;
+    DevBuf<float> matParams, plLambda, plValue, triShade;
     DevBuf<uint8_t> primFlip;
     DevBuf<uint32_t> lightBitTrail, permOffset, permNDigits, permBase;
     DevBuf<uint16_t> perm;
@@ -206,6 +206,31 @@ static void BuildDevice(pbrt_context *c) {
     c->primLight.Upload(pl);
     c->primFlip.Upload(pf);
     c->primOrig.Upload(b.triPrim);
+    // vertex normals / uv per leaf triangle (only when some mesh has them)
+    if (std::any_of(s.triShade.begin(), s.triShade.end(), [](uint8_t f) { return f != 0; })) {
+        std::vector<float> ts((size_t)nt * 16, 0.f);
+        for (int i = 0; i < nt; ++i) {
+            const int o = b.triPrim[i];
+            const int flags = s.triShade[o];
+            if (!flags) continue;
+            const auto &t = s.tris[o];
+            float *d = &ts[(size_t)i * 16];
+            for (int k = 0; k < 3; ++k) {
+                d[4 * k] = s.vertN[t[k]].x;
+                d[4 * k + 1] = s.vertN[t[k]].y;
+                d[4 * k + 2] = s.vertN[t[k]].z;
+            }
+            int fl = flags;
+            memcpy(&d[3], &fl, 4);
+            d[7] = s.vertUV[t[0]][0];
+            d[11] = s.vertUV[t[0]][1];
+            d[12] = s.vertUV[t[1]][0];
+            d[13] = s.vertUV[t[1]][1];
+            d[14] = s.vertUV[t[2]][0];
+            d[15] = s.vertUV[t[2]][1];
+        }
+        c->triShade.Upload(ts);
+    }
     std::vector<float> mc;
     std::vector<int> mk;
     for (auto &m : s.materials) {
@@ -255,7 +280,9 @@ static void BuildDevice(pbrt_context *c) {
         DeviceAreaLight d{};
         int leaf = origToLeaf[l.prim];
         const float *v = &b.triVerts[(size_t)leaf * 12];
-        d.v0 = make_float4(v[0], v[1], v[2], 0.f);
+        float leafBits;  // .w: the light's leaf prim (its shading data), as int bits
+        memcpy(&leafBits, &leaf, 4);
+        d.v0 = make_float4(v[0], v[1], v[2], leafBits);
         d.v1 = make_float4(v[4], v[5], v[6], 0.f);
         d.v2 = make_float4(v[8], v[9], v[10], 0.f);
         d.scale = l.scale;
@@ -341,6 +368,7 @@ static void BuildDevice(pbrt_context *c) {
     S.primMaterial = c->primMaterial.p;
     S.primLight = c->primLight.p;
     S.primFlip = c->primFlip.p;
+    S.triShade = (const float4 *)c->triShade.p;
     S.matCoeffs = (const float4 *)c->matCoeffs.p;
     S.matConstant = c->matConstant.p;
     S.nMaterials = (int)s.materials.size();
@@ -736,6 +764,10 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
     f->pl_lambda = scene->plLambda.data();
     f->pl_value = scene->plValue.data();
     f->regularize = s.regularize ? 1 : 0;
+    static_assert(sizeof(V3) == 12, "vertex normals are handed out as float[3] arrays");
+    f->vertex_normals = s.vertN.empty() ? nullptr : &s.vertN[0].x;
+    f->vertex_uv = s.vertUV.empty() ? nullptr : s.vertUV[0].data();
+    f->tri_shading = s.triShade.data();
     return 0;
 }
 
@@ -975,6 +1007,29 @@ int pbrt_debug_fresnel(const float *in, float *out) {
     V3 rf = Reflect(wi, n);
     const float v[10] = {FrDielectric(in[0], in[1]), FrComplex(in[0], in[2], in[3]), (float)ok, etap, wt.x, wt.y,
                          wt.z, rf.x, rf.y, rf.z};
+    memcpy(out, v, sizeof v);
+    return 0;
+}
+
+int pbrt_debug_triangle_shading(const float *p9, const float *n9, const float *uv6, int flip, const float *b3,
+                                const float *u2, float *out) {
+    if (!p9 || !b3 || !u2 || !out) return Fail("null argument");
+    const V3 p0(p9[0], p9[1], p9[2]), p1(p9[3], p9[4], p9[5]), p2(p9[6], p9[7], p9[8]);
+    TriShading sh;
+    sh.flags = (n9 ? 1 : 0) | (uv6 ? 2 : 0);
+    if (n9) {
+        sh.n0 = V3(n9[0], n9[1], n9[2]);
+        sh.n1 = V3(n9[3], n9[4], n9[5]);
+        sh.n2 = V3(n9[6], n9[7], n9[8]);
+    }
+    if (uv6)
+        for (int k = 0; k < 3; ++k) sh.uv[k][0] = uv6[2 * k], sh.uv[k][1] = uv6[2 * k + 1];
+    TriSurface s = TriangleSurface(p0, p1, p2, b3[0], b3[1], b3[2], flip != 0, &sh);
+    float b[3];
+    SampleUniformTriangle(u2[0], u2[1], b);
+    V3 sn = TriangleSampleNormal(p0, p1, p2, b[0], b[1], flip != 0, &sh);
+    const float v[15] = {s.n.x, s.n.y, s.n.z, s.ns.x, s.ns.y, s.ns.z, s.dpdu.x, s.dpdu.y, s.dpdu.z,
+                         s.dpdus.x, s.dpdus.y, s.dpdus.z, sn.x, sn.y, sn.z};
     memcpy(out, v, sizeof v);
     return 0;
 }

@@ -126,6 +126,8 @@ PHD float MaxComponentValue(V3 v) { return std::fmax(v.x, std::fmax(v.y, v.z)); 
 PHD int MaxComponentIndex(V3 v) { return (v.x > v.y) ? ((v.x > v.z) ? 0 : 2) : ((v.y > v.z) ? 1 : 2); }
 PHD V3 Permute(const V3 &v, int a, int b, int c) { return {v[a], v[b], v[c]}; }  // const []: selects, no scratch
 PHD V3 FaceForward(V3 n, V3 v) { return (Dot(n, v) < 0.f) ? -n : n; }
+// FaceForward(Normal3f, Normal3f): the dot of two normals is FMA-compensated (vecmath.h:1073)
+PHD V3 FaceForwardN(V3 n, V3 n2) { return (DotN(n, n2) < 0.f) ? -n : n; }
 PHD V3 GramSchmidt(V3 v, V3 w) { return v - Dot(v, w) * w; }
 // util/vecmath.h:974 AngleBetween
 PHD float AngleBetween(V3 v1, V3 v2) {
@@ -474,13 +476,27 @@ PHD bool IntersectTriangle(V3 o, V3 dir, float tMax, V3 p0, V3 p1, V3 p2, TriHit
 
 // Surface geometry of a triangle hit without shading normals or uv
 // (shapes.h:884-1010, mesh without n/s/uv: default uv (0,0),(1,0),(1,1)).
+// Per-triangle shading attributes of TriangleMesh (util/mesh.h:23-46): vertex normals and
+// uv, each optional (flags bit0 / bit1).
+struct TriShading {
+    int flags = 0;
+    V3 n0, n1, n2;
+    float uv[3][2];
+};
 struct TriSurface {
     V3 p, pErr, n, dpdu;
+    V3 ns, dpdus;  // shading normal and shading dpdu (== n, dpdu without vertex normals)
 };
-PHD TriSurface TriangleSurface(V3 p0, V3 p1, V3 p2, float b0, float b1, float b2, bool flip) {
+// Triangle::InteractionFromIntersection (shapes.h:884-1010) without the dndu/dndv terms (bump
+// mapping / ray differentials only) and with SetShadingGeometry(..., true) (interaction.h:194)
+PHD TriSurface TriangleSurface(V3 p0, V3 p1, V3 p2, float b0, float b1, float b2, bool flip,
+                               const TriShading *sh = nullptr) {
     TriSurface s;
-    // uv = (0,0),(1,0),(1,1): duv02 = (-1,-1), duv12 = (0,-1)
-    const float duv02x = -1, duv02y = -1, duv12x = 0, duv12y = -1;
+    float uv[3][2] = {{0, 0}, {1, 0}, {1, 1}};
+    if (sh && (sh->flags & 2))
+        for (int k = 0; k < 3; ++k) uv[k][0] = sh->uv[k][0], uv[k][1] = sh->uv[k][1];
+    const float duv02x = uv[0][0] - uv[2][0], duv02y = uv[0][1] - uv[2][1];
+    const float duv12x = uv[1][0] - uv[2][0], duv12y = uv[1][1] - uv[2][1];
     V3 dp02 = p0 - p2, dp12 = p1 - p2;
     float determinant = DifferenceOfProducts(duv02x, duv12y, duv02y, duv12x);
     V3 dpdu, dpdv;
@@ -507,7 +523,35 @@ PHD TriSurface TriangleSurface(V3 p0, V3 p1, V3 p2, float b0, float b1, float b2
     if (flip) n = -n;
     s.n = n;
     s.dpdu = dpdu;
+    s.ns = n;
+    s.dpdus = dpdu;
+    if (sh && (sh->flags & 1)) {
+        V3 ns = b0 * sh->n0 + b1 * sh->n1 + b2 * sh->n2;
+        ns = LengthSquared(ns) > 0 ? Normalize(ns) : s.n;
+        V3 ss = s.dpdu;
+        V3 ts = Cross(ns, ss);
+        if (LengthSquared(ts) > 0) ss = Cross(ts, ns);
+        else CoordinateSystem(ns, &ss, &ts);
+        s.ns = ns;
+        s.n = FaceForwardN(s.n, ns);
+        while (LengthSquared(ss) > 1e16f || LengthSquared(ts) > 1e16f) {
+            ss = ss / 1e8f;
+            ts = ts / 1e8f;
+        }
+        s.dpdus = ss;
+    }
     return s;
+}
+// Triangle::Sample's normal for a sampled point with barycentrics b (shapes.h:1023-1029)
+PHD V3 TriangleSampleNormal(V3 p0, V3 p1, V3 p2, float b0, float b1, bool flip, const TriShading *sh) {
+    V3 n = Normalize(Cross(p1 - p0, p2 - p0));
+    if (sh && (sh->flags & 1)) {
+        V3 ns = b0 * sh->n0 + b1 * sh->n1 + (1 - b0 - b1) * sh->n2;
+        n = FaceForwardN(n, ns);
+    } else if (flip) {
+        n = n * -1.f;
+    }
+    return n;
 }
 
 // ---------------------------------------------------------------- spectra

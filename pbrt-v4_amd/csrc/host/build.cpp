@@ -417,8 +417,15 @@ static void BuildLightBVH(SceneDesc &s) {
         float mx = *std::max_element(dense.begin(), dense.end());
         float phi = mx;
         phi *= al.scale * al.area * kPi;
+        // Triangle::NormalBounds (shapes.h): with vertex normals the face normal is turned
+        // toward their sum, otherwise flipped by reverseOrientation ^ transformSwapsHandedness
         V3 n = Normalize(Cross(p1 - p0, p2 - p0));
-        if (s.triFlip[al.prim]) n = n * -1.f;
+        if (!s.triShade.empty() && (s.triShade[al.prim] & 1)) {
+            V3 ns = s.vertN[tri[0]] + s.vertN[tri[1]] + s.vertN[tri[2]];
+            n = FaceForwardN(n, ns);
+        } else if (s.triFlip[al.prim]) {
+            n = n * -1.f;
+        }
         LightBounds lb;
         lb.bounds.Add(p0);
         lb.bounds.Add(p1);

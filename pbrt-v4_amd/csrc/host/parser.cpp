@@ -12,6 +12,7 @@
 #include <set>
 #include <sstream>
 
+#include "ply.h"
 #include "scene.h"
 
 namespace pbrt_amd {
@@ -318,6 +319,7 @@ class Parser {
         std::vector<V3> P;
         std::vector<int> idx;
         std::vector<float> uv;  // per vertex, 2 floats
+        std::vector<V3> N;      // per vertex (object space)
         Mat4 renderFromObject;
         bool flip;
         int material;
@@ -513,7 +515,7 @@ class Parser {
             std::string type = Str(toks, pos);
             ParamSet ps = Params(toks, pos);
             ps.loc = loc;
-            Shape(type, ps);
+            Shape(type, ps, dir);
         } else if (d == "Include" || d == "Import") {
             std::string f = Str(toks, pos);
             std::string path = (f.size() && f[0] == '/') ? f : (dir.empty() ? f : dir + "/" + f);
@@ -642,29 +644,59 @@ class Parser {
         throw Error(loc + ": \"" + p->type + " " + p->name + "\" is not supported for conductors yet (use \"spectrum\")");
     }
 
-    void Shape(const std::string &type, ParamSet &ps) {
-        if (type != "trianglemesh") throw Error(ps.loc + ": shape \"" + type + "\" is not supported yet");
+    // Shape "trianglemesh" (Triangle::CreateMesh, shapes.cpp:1380-1417) and "plymesh"
+    // (shapes.cpp:1418-1478; TriQuadMesh::ReadPLY, util/mesh.cpp:322-420)
+    void Shape(const std::string &type, ParamSet &ps, const std::string &dir) {
         PendingShape s;
-        Param *P = ps.Find("P", "point3");
-        if (!P || P->nums.size() % 3) throw Error(ps.loc + ": trianglemesh needs \"point3 P\"");
-        for (size_t i = 0; i < P->nums.size(); i += 3) s.P.push_back(V3(P->nums[i], P->nums[i + 1], P->nums[i + 2]));
-        Param *I = ps.Find("indices", "integer");
-        if (I)
-            for (double v : I->nums) s.idx.push_back((int)v);
-        else if (s.P.size() == 3)
-            s.idx = {0, 1, 2};
-        else
-            throw Error(ps.loc + ": trianglemesh needs \"integer indices\"");
-        if (s.idx.size() % 3) throw Error(ps.loc + ": indices not a multiple of 3");
-        for (int v : s.idx)
-            if (v < 0 || v >= (int)s.P.size()) throw Error(ps.loc + ": vertex index out of range");
-        Param *uv = ps.Find("uv", "point2");
-        if (uv) {
-            if (uv->nums.size() != 2 * s.P.size()) throw Error(ps.loc + ": uv count mismatch");
-            for (double v : uv->nums) s.uv.push_back((float)v);
+        if (type == "trianglemesh") {
+            Param *P = ps.Find("P", "point3");
+            if (!P || P->nums.size() % 3) throw Error(ps.loc + ": trianglemesh needs \"point3 P\"");
+            for (size_t i = 0; i < P->nums.size(); i += 3) s.P.push_back(V3(P->nums[i], P->nums[i + 1], P->nums[i + 2]));
+            Param *I = ps.Find("indices", "integer");
+            if (I)
+                for (double v : I->nums) s.idx.push_back((int)v);
+            else if (s.P.size() == 3)
+                s.idx = {0, 1, 2};
+            else
+                throw Error(ps.loc + ": trianglemesh needs \"integer indices\"");
+            if (s.idx.size() % 3) throw Error(ps.loc + ": indices not a multiple of 3");
+            for (int v : s.idx)
+                if (v < 0 || v >= (int)s.P.size()) throw Error(ps.loc + ": vertex index out of range");
+            Param *uv = ps.Find("uv", "point2");
+            if (uv) {
+                if (uv->nums.size() != 2 * s.P.size()) throw Error(ps.loc + ": uv count mismatch");
+                for (double v : uv->nums) s.uv.push_back((float)v);
+            }
+            Param *N = ps.Find("N", "normal");
+            if (!N) N = ps.Find("N", "normal3");
+            if (N) {
+                if (N->nums.size() != 3 * s.P.size()) throw Error(ps.loc + ": N count mismatch");
+                for (size_t i = 0; i < N->nums.size(); i += 3) s.N.push_back(V3(N->nums[i], N->nums[i + 1], N->nums[i + 2]));
+            }
+            if (ps.Find("S")) throw Error(ps.loc + ": per-vertex shading tangents \"S\" are not supported yet");
+            ps.Find("faceIndices");
+        } else if (type == "plymesh") {
+            std::string f = ps.GetString("filename", "");
+            if (f.empty()) throw Error(ps.loc + ": plymesh needs \"string filename\"");
+            std::string path = (f[0] == '/') ? f : (dir.empty() ? f : dir + "/" + f);
+            if (ps.Find("displacement")) throw Error(ps.loc + ": plymesh displacement is not supported yet");
+            ps.GetFloat("edgelength", 1);
+            PlyMesh m;
+            try {
+                m = ReadPly(path);
+            } catch (const Error &e) {
+                throw Error(ps.loc + ": " + e.what());
+            }
+            if (!m.quadIndices.empty())
+                throw Error(ps.loc + ": " + f + " has quads; pbrt makes bilinear patches of them, which are not supported yet");
+            if (m.triIndices.empty()) throw Error(ps.loc + ": " + f + " has no triangles");
+            s.P = std::move(m.p);
+            s.idx = std::move(m.triIndices);
+            s.N = std::move(m.n);
+            for (auto &t : m.uv) s.uv.insert(s.uv.end(), {t[0], t[1]});
+        } else {
+            throw Error(ps.loc + ": shape \"" + type + "\" is not supported yet");
         }
-        if (ps.Find("N") || ps.Find("S")) throw Error(ps.loc + ": per-vertex shading normals/tangents not supported yet");
-        ps.Find("faceIndices");
         ps.CheckUnused();
         s.renderFromObject = gs.ctm;  // renderFromWorld applied at Finish
         s.flip = gs.reverseOrientation;
@@ -855,6 +887,24 @@ void Parser::Finish() {
         bool flip = s.flip ^ SwapsHandedness(rfo);
         int base = (int)scene.verts.size();
         for (V3 p : s.P) scene.verts.push_back(XformPoint(rfo, p));
+        // normals: renderFromObject(n) (inverse transpose), negated under ReverseOrientation
+        // (TriangleMesh ctor, util/mesh.cpp:49-57); uv as given
+        const uint8_t shadeBits = (s.N.empty() ? 0 : 1) | (s.uv.empty() ? 0 : 2);
+        if (shadeBits || !scene.vertN.empty()) {
+            scene.vertN.resize(base, V3(0, 0, 0));
+            scene.vertUV.resize(base, {0.f, 0.f});
+            Mat4 inv = Inverse4(rfo);
+            for (size_t i = 0; i < s.P.size(); ++i) {
+                V3 nn(0, 0, 0);
+                if (!s.N.empty()) {
+                    nn = XformNormal(inv, s.N[i]);
+                    if (s.flip) nn = -nn;
+                }
+                scene.vertN.push_back(nn);
+                scene.vertUV.push_back(s.uv.empty() ? std::array<float, 2>{0.f, 0.f}
+                                                    : std::array<float, 2>{s.uv[2 * i], s.uv[2 * i + 1]});
+            }
+        }
         int mat = s.material;
         if (mat < 0) {
             // pbrt's default material is "diffuse" with reflectance 0.5
@@ -918,7 +968,7 @@ void Parser::Finish() {
             scene.tris.push_back(tri);
             scene.triMaterial.push_back(s.material < 0 ? mat : s.material);
             scene.triFlip.push_back(flip ? 1 : 0);
-            if (!s.uv.empty()) throw Error(s.loc + ": per-vertex uv not supported yet");
+            scene.triShade.push_back(shadeBits);
             if (lightSpectrum >= 0) {
                 AreaLightDesc l;
                 l.prim = triIndex;

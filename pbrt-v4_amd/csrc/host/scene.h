@@ -100,6 +100,11 @@ struct SceneDesc {
     std::vector<int> triMaterial;   // material index
     std::vector<int> triLight;      // area light index or -1
     std::vector<uint8_t> triFlip;   // reverseOrientation ^ transformSwapsHandedness
+    // shading attributes (TriangleMesh n / uv, util/mesh.cpp:23-68): per vertex, meaningful
+    // only for triangles whose triShade bit says so (bit0 normals, bit1 uv)
+    std::vector<V3> vertN;                       // render space, reverseOrientation applied
+    std::vector<std::array<float, 2>> vertUV;
+    std::vector<uint8_t> triShade;
 
     std::vector<MaterialDesc> materials;
     std::vector<AreaLightDesc> areaLights;

@@ -72,6 +72,9 @@ struct DeviceScene {
     const int *primMaterial;
     const int *primLight;
     const uint8_t *primFlip;
+    // per-triangle shading attributes (leaf order, 4 float4 each: n0|flags, n1|u0, n2|v0,
+    // u1 v1 u2 v2), nullptr when no mesh has vertex normals or uv
+    const float4 *triShade;
     // materials
     const float4 *matCoeffs;  // c0, c1, c2, constant value
     const int *matConstant;

@@ -533,6 +533,34 @@ __device__ inline void PrimVerts(const DeviceScene &S, int prim, V3 *p0, V3 *p1,
     *p2 = V3(c.x, c.y, c.z);
 }
 
+// Vertex normals / uv of a leaf-order prim; false (and sh untouched) when it has none
+__device__ inline bool LoadTriShading(const DeviceScene &S, int prim, TriShading *sh) {
+    if (!S.triShade) return false;
+    const float4 a = S.triShade[4 * prim];
+    const int flags = __float_as_int(a.w);
+    if (flags == 0) return false;
+    const float4 b = S.triShade[4 * prim + 1], c = S.triShade[4 * prim + 2], d = S.triShade[4 * prim + 3];
+    sh->flags = flags;
+    sh->n0 = V3(a.x, a.y, a.z);
+    sh->n1 = V3(b.x, b.y, b.z);
+    sh->n2 = V3(c.x, c.y, c.z);
+    sh->uv[0][0] = b.w;
+    sh->uv[0][1] = c.w;
+    sh->uv[1][0] = d.x;
+    sh->uv[1][1] = d.y;
+    sh->uv[2][0] = d.z;
+    sh->uv[2][1] = d.w;
+    return true;
+}
+
+// SurfaceInteraction of a hit (Triangle::InteractionFromIntersection)
+__device__ inline TriSurface SurfaceAt(const DeviceScene &S, int prim, V3 p0, V3 p1, V3 p2, float b0, float b1,
+                                       float b2) {
+    TriShading sh;
+    const bool has = LoadTriShading(S, prim, &sh);
+    return TriangleSurface(p0, p1, p2, b0, b1, b2, S.primFlip[prim], has ? &sh : nullptr);
+}
+
 __device__ inline float TriArea(V3 p0, V3 p1, V3 p2) { return 0.5f * Length(Cross(p1 - p0, p2 - p0)); }
 
 __device__ inline float SolidAngleOf(V3 p0, V3 p1, V3 p2, V3 p) {
@@ -540,16 +568,15 @@ __device__ inline float SolidAngleOf(V3 p0, V3 p1, V3 p2, V3 p) {
 }
 
 // Triangle::Sample(ctx, u) (shapes.h:1053-1130); returns false for {}
-__device__ inline bool SampleTriangle(V3 p0, V3 p1, V3 p2, bool flip, V3 refP, V3 refN, V3 refNs, float u0,
-                                      float u1, V3 *ps, V3 *pErr, V3 *ns, float *pdfOut) {
+__device__ inline bool SampleTriangle(V3 p0, V3 p1, V3 p2, bool flip, const TriShading *sh, V3 refP, V3 refN,
+                                      V3 refNs, float u0, float u1, V3 *ps, V3 *pErr, V3 *ns, float *pdfOut) {
     (void)refN;
     float solidAngle = SolidAngleOf(p0, p1, p2, refP);
     if (solidAngle < kMinSphericalSampleArea || solidAngle > kMaxSphericalSampleArea) {
         float b[3];
         SampleUniformTriangle(u0, u1, b);
         V3 p = b[0] * p0 + b[1] * p1 + b[2] * p2;
-        V3 n = Normalize(Cross(p1 - p0, p2 - p0));
-        if (flip) n = n * -1.f;
+        V3 n = TriangleSampleNormal(p0, p1, p2, b[0], b[1], flip, sh);
         V3 pAbsSum = Abs(b[0] * p0) + Abs(b[1] * p1) + Abs((1 - b[0] - b[1]) * p2);
         ToPoint3fi(p, gamma(6) * pAbsSum, &p, pErr);
         float pdf = 1 / TriArea(p0, p1, p2);
@@ -588,8 +615,7 @@ __device__ inline bool SampleTriangle(V3 p0, V3 p1, V3 p2, bool flip, V3 refP, V
     V3 pAbsSum = Abs(b[0] * p0) + Abs(b[1] * p1) + Abs((1 - b[0] - b[1]) * p2);
     V3 p;
     ToPoint3fi(b[0] * p0 + b[1] * p1 + b[2] * p2, gamma(6) * pAbsSum, &p, pErr);
-    V3 n = Normalize(Cross(p1 - p0, p2 - p0));
-    if (flip) n = n * -1.f;
+    V3 n = TriangleSampleNormal(p0, p1, p2, b[0], b[1], flip, sh);
     *ps = p;
     *ns = n;
     *pdfOut = pdf;
@@ -597,14 +623,15 @@ __device__ inline bool SampleTriangle(V3 p0, V3 p1, V3 p2, bool flip, V3 refP, V
 }
 
 // Triangle::PDF(ctx, wi) (shapes.h:1133-1174)
-__device__ inline float TrianglePDF(V3 p0, V3 p1, V3 p2, bool flip, V3 refP, V3 refPErr, V3 refN, V3 refNs, V3 wi) {
+__device__ inline float TrianglePDF(V3 p0, V3 p1, V3 p2, bool flip, const TriShading *sh, V3 refP, V3 refPErr,
+                                   V3 refN, V3 refNs, V3 wi) {
     float solidAngle = SolidAngleOf(p0, p1, p2, refP);
     if (solidAngle < kMinSphericalSampleArea || solidAngle > kMaxSphericalSampleArea) {
         // ShapeSampleContext::SpawnRay(wi) then Triangle::Intersect
         V3 o = OffsetRayOrigin(refP, refPErr, refN, wi);
         TriHit h;
         if (!IntersectTriangle(o, wi, kInfinity, p0, p1, p2, &h)) return 0;
-        TriSurface hs = TriangleSurface(p0, p1, p2, h.b0, h.b1, h.b2, flip);
+        TriSurface hs = TriangleSurface(p0, p1, p2, h.b0, h.b1, h.b2, flip, sh);
         V3 pHit = hs.p, n = hs.n;
         float pdf = (1 / TriArea(p0, p1, p2)) / (AbsDotN(n, -wi) / DistanceSquared(refP, pHit));
         if (isinf(pdf)) pdf = 0;
@@ -962,7 +989,8 @@ __global__ void __launch_bounds__(kBlock) k_emissive(DeviceScene S, PathState st
         PrimVerts(S, prim, &p0, &p1, &p2);
         const int light = S.primLight[prim];
         const bool flip = S.primFlip[prim];
-        TriSurface surf = TriangleSurface(p0, p1, p2, b0, b1, b2, flip);
+        TriSurface surf = SurfaceAt(S, prim, p0, p1, p2, b0, b1, b2);
+        (void)flip;
         V3 wo = Normalize(-rd);
         const DeviceAreaLight Ld = S.lights[light];
         if (!(Ld.twoSided || DotN(surf.n, wo) >= 0)) continue;
@@ -972,10 +1000,14 @@ __global__ void __launch_bounds__(kBlock) k_emissive(DeviceScene S, PathState st
         } else {
             V3 q0, q1, q2;
             PrimVerts(S, pp, &q0, &q1, &q2);
-            TriSurface prev = TriangleSurface(q0, q1, q2, pb0, pb1, pb2, S.primFlip[pp]);
-            float lightChoicePDF = LightPMF(S, prev.p, prev.n, light);
+            // prevIntrCtx = LightSampleContext(pi, n, ns) of the previous surface
+            TriSurface prev = SurfaceAt(S, pp, q0, q1, q2, pb0, pb1, pb2);
+            float lightChoicePDF = LightPMF(S, prev.p, prev.ns, light);
+            TriShading lsh;
+            const bool lhas = LoadTriShading(S, __float_as_int(Ld.v0.w), &lsh);
             V3 l0(Ld.v0.x, Ld.v0.y, Ld.v0.z), l1(Ld.v1.x, Ld.v1.y, Ld.v1.z), l2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
-            float lightPDF = lightChoicePDF * TrianglePDF(l0, l1, l2, Ld.flip, prev.p, prev.pErr, prev.n, prev.n, -wo);
+            float lightPDF = lightChoicePDF * TrianglePDF(l0, l1, l2, Ld.flip, lhas ? &lsh : nullptr, prev.p,
+                                                          prev.pErr, prev.n, prev.ns, -wo);
             denom = Avg31(1.f + rl * lightPDF);
         }
         const float *dense = S.dense + Ld.spectrum * kDenseN;
@@ -1162,11 +1194,11 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
             V3 p0, p1, p2;
             PrimVerts(S, prim, &p0, &p1, &p2);
             const int mat = S.primMaterial[prim];
-            TriSurface surf = TriangleSurface(p0, p1, p2, b0, b1, b2, S.primFlip[prim]);
+            TriSurface surf = SurfaceAt(S, prim, p0, p1, p2, b0, b1, b2);
             const float4 mc = matsL[mat];
             const bool constant = matConstL[mat];
             V3 wo = Normalize(-rd);
-            V3 n = surf.n, ns = surf.n;
+            V3 n = surf.n, ns = surf.ns;
             // beta_i -> bfLds[i][lane] by LDS-DMA: all 31 loads in flight at once, no VGPRs,
             // landing while the sampler below works from LDS (depth 0: beta = 1, no loads)
             if (depth > 0) {
@@ -1198,7 +1230,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                     bf[it.i * kBlock] = (depth > 0 ? bf[it.i * kBlock] : 1.f) * (R * kInvPi);
                 }
                 SEC_MARK(st, 2);
-                Frame frame = Frame::FromXZ(Normalize(surf.dpdu), ns);
+                Frame frame = Frame::FromXZ(Normalize(surf.dpdus), ns);
                 V3 woL = frame.ToLocal(wo);
                 V3 pi = surf.p, pe = surf.pErr;
                 // ---- light sampling + shadow ray (surfscatter.cpp:254-326); reads the old beta
@@ -1211,7 +1243,10 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                         V3 q0(Ld.v0.x, Ld.v0.y, Ld.v0.z), q1(Ld.v1.x, Ld.v1.y, Ld.v1.z), q2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
                         V3 lp, lpe, ln;
                         float lpdf;
-                        if (SampleTriangle(q0, q1, q2, Ld.flip, cp, n, ns, dU0, dU1, &lp, &lpe, &ln, &lpdf) &&
+                        TriShading lsh;
+                        const bool lhas = LoadTriShading(S, __float_as_int(Ld.v0.w), &lsh);
+                        if (SampleTriangle(q0, q1, q2, Ld.flip, lhas ? &lsh : nullptr, cp, n, ns, dU0, dU1, &lp, &lpe,
+                                           &ln, &lpdf) &&
                             lpdf != 0 && LengthSquared(lp - cp) != 0) {
                             SEC_MARK(st, 3);
                             V3 wi = Normalize(lp - cp);
@@ -1385,9 +1420,9 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
             V3 p0, p1, p2;
             PrimVerts(S, prim, &p0, &p1, &p2);
             const int mat = S.primMaterial[prim];
-            const TriSurface surf = TriangleSurface(p0, p1, p2, b0, b1, b2, S.primFlip[prim]);
+            const TriSurface surf = SurfaceAt(S, prim, p0, p1, p2, b0, b1, b2);
             const V3 wo = Normalize(-rd);
-            const V3 n = surf.n, ns = surf.n;
+            const V3 n = surf.n, ns = surf.ns;
             const RaySamples rs = GenerateRaySamples<MT == kMatDielectricT>(S, T, px, py, sampleIndex, d0);
             // ---- Material::GetBxDF (materials.h:182-204 dielectric, :491-511 conductor)
             const float4 mp = S.matParams[mat];
@@ -1411,7 +1446,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
                     *k = 2 * std::sqrt(r) / std::sqrt(std::fmax(0.f, 1 - r));
                 }
             };
-            const Frame frame = Frame::FromXZ(Normalize(surf.dpdu), ns);
+            const Frame frame = Frame::FromXZ(Normalize(surf.dpdus), ns);
             const V3 woL = frame.ToLocal(wo);
             const V3 pi = surf.p, pe = surf.pErr;
             const bool smooth = tr.EffectivelySmooth();
@@ -1429,7 +1464,10 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
                     V3 q0(Ld.v0.x, Ld.v0.y, Ld.v0.z), q1(Ld.v1.x, Ld.v1.y, Ld.v1.z), q2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
                     V3 lp, lpe, ln;
                     float lpdf;
-                    if (SampleTriangle(q0, q1, q2, Ld.flip, cp, n, ns, rs.dU0, rs.dU1, &lp, &lpe, &ln, &lpdf) &&
+                    TriShading lsh;
+                    const bool lhas = LoadTriShading(S, __float_as_int(Ld.v0.w), &lsh);
+                    if (SampleTriangle(q0, q1, q2, Ld.flip, lhas ? &lsh : nullptr, cp, n, ns, rs.dU0, rs.dU1, &lp,
+                                       &lpe, &ln, &lpdf) &&
                         lpdf != 0 && LengthSquared(lp - cp) != 0) {
                         const V3 wi = Normalize(lp - cp);
                         const V3 wiL = frame.ToLocal(wi);

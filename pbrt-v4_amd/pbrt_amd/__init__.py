@@ -68,6 +68,8 @@ class SceneFlat(ctypes.Structure):
         ("material_spectra", ctypes.POINTER(ctypes.c_int32)), ("n_pl_spectra", ctypes.c_int),
         ("pl_offsets", ctypes.POINTER(ctypes.c_int32)), ("pl_lambda", ctypes.POINTER(ctypes.c_float)),
         ("pl_value", ctypes.POINTER(ctypes.c_float)), ("regularize", ctypes.c_int),
+        ("vertex_normals", ctypes.POINTER(ctypes.c_float)), ("vertex_uv", ctypes.POINTER(ctypes.c_float)),
+        ("tri_shading", ctypes.POINTER(ctypes.c_uint8)),
     ]
 
 
@@ -91,7 +93,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_film_clear", "pbrt_film_device_ptr", "pbrt_film_read", "pbrt_film_get_rgb", "pbrt_intersect",
     "pbrt_debug_halton", "pbrt_debug_rgb_coeffs", "pbrt_debug_rgb2spec_column", "pbrt_debug_kernel_sections",
     "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
-    "pbrt_debug_named_spectrum", "pbrt_debug_bxdf",
+    "pbrt_debug_named_spectrum", "pbrt_debug_bxdf", "pbrt_debug_triangle_shading",
 ]
 
 _LIB = None
@@ -136,6 +138,7 @@ def _lib():
     lib.pbrt_debug_fresnel.argtypes = [c.c_void_p, c.c_void_p]
     lib.pbrt_debug_named_spectrum.argtypes = [c.c_char_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_debug_bxdf.argtypes = [c.c_int] + [c.c_void_p] * 7
+    lib.pbrt_debug_triangle_shading.argtypes = [c.c_void_p] * 3 + [c.c_int] + [c.c_void_p] * 3
     lib.pbrt_set_data_dir(str(DATA_DIR).encode())
     _LIB = lib
     return lib
@@ -166,6 +169,18 @@ def named_spectrum(name, lambdas):
     lam = _f32(lambdas)
     o = np.zeros(lam.size, np.float32)
     _check(_lib().pbrt_debug_named_spectrum(name.encode(), lam.ctypes.data, lam.size, o.ctypes.data))
+    return o
+
+
+def debug_triangle_shading(p9, n9, uv6, flip, b3, u2):
+    """TriangleSurface (+ Triangle::Sample normal) with optional vertex normals / uv: 15 floats."""
+    p, b, u = _f32(p9, 9), _f32(b3, 3), _f32(u2, 2)
+    n = None if n9 is None else _f32(n9, 9)
+    t = None if uv6 is None else _f32(uv6, 6)
+    o = np.zeros(15, np.float32)
+    _check(_lib().pbrt_debug_triangle_shading(p.ctypes.data, None if n is None else n.ctypes.data,
+                                              None if t is None else t.ctypes.data, int(flip), b.ctypes.data,
+                                              u.ctypes.data, o.ctypes.data))
     return o
 
 

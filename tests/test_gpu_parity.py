@@ -115,6 +115,18 @@ def test_index_matched_glass_invisible_gpu(pa, oracle):
     np.testing.assert_allclose(img, sky, rtol=1e-5)
 
 
+@pytest.mark.parametrize("sampler", ["zsobol", "halton"])
+def test_vertex_normals_and_uv_match_oracle(pa, oracle, sampler):
+    """Smooth-shaded conductor sphere with uv, an area light with vertex normals, uv floor."""
+    import sys
+    sys.path.insert(0, str(SCENES.parent / "tests"))
+    from test_shading_ply import smooth_sphere_text
+    sc = pa.Scene.from_string(smooth_sphere_text(res=96, spp=16, sampler=sampler), SCENES)
+    film, _ = gpu_film(pa, sc)
+    frac, mean_rel = check_parity(to_rgb(oracle, sc, film), to_rgb(oracle, sc, oracle.render(sc, threads=16)))
+    print(f"vertex normals/uv ({sampler}) parity: {frac*100:.3f}% pixels within 1e-3, mean rel {mean_rel:.2e}")
+
+
 def test_sample_splits_bit_exact(pa):
     sc = pa.load_scene(SCENES / "cornell-box.pbrt", xresolution=64, yresolution=48, spp=8)
     full, _ = gpu_film(pa, sc)

@@ -646,7 +646,7 @@ static Interaction TriangleInteraction(Vec p0, Vec p1, Vec p2, bool flip, TriIse
 // same closest hit up to exact-t ties)
 struct BVHNode {
     Vec mn, mx;
-    int left = -1, right = -1, first = 0, count = 0;
+    int left = -1, right = -1, first = 0, count = 0, axis = 0;
 };
 
 struct Scene {
@@ -710,6 +710,7 @@ struct Scene {
         int l = Build(start, mid, cent), r = Build(mid, end, cent);
         nodes[idx].left = l;
         nodes[idx].right = r;
+        nodes[idx].axis = axis;
         return idx;
     }
 
@@ -779,9 +780,12 @@ struct Scene {
                         best = t;
                     }
                 }
-            } else {
+            } else if (neg[n.axis]) {  // near child first (cpu/aggregates.cpp:561-568)
                 stack[sp++] = n.left;
                 stack[sp++] = n.right;
+            } else {
+                stack[sp++] = n.right;
+                stack[sp++] = n.left;
             }
         }
         return best;

@@ -1,6 +1,7 @@
 #include <algorithm>
 #include <array>
 #include <cmath>
+#include <future>
 #include <stdexcept>
 
 #include "bvh.h"
@@ -44,83 +45,87 @@ struct Builder2 {
     std::vector<Node2> nodes;
     int maxLeaf;
 
-    int Build(int start, int end) {
-        Node2 node;
-        for (int i = start; i < end; ++i) node.box.Add(prims[i].box);
-        int idx = (int)nodes.size();
-        nodes.push_back(node);
+    // One binned-SAH decision for prims [start, end): fills box and returns the split point,
+    // or -1 for a leaf.  Reorders the range in place.
+    int Split(int start, int end, Box *box) {
+        Box nb;
+        for (int i = start; i < end; ++i) nb.Add(prims[i].box);
+        *box = nb;
         int n = end - start;
-        auto makeLeaf = [&]() {
-            nodes[idx].first = start;
-            nodes[idx].count = n;
-            return idx;
-        };
-        if (n == 1) return makeLeaf();
+        if (n == 1) return -1;
         Box cb;
         for (int i = start; i < end; ++i) cb.Add(prims[i].centroid);
         V3 d = cb.mx - cb.mn;
         int dim = (d.x > d.y) ? ((d.x > d.z) ? 0 : 2) : ((d.y > d.z) ? 1 : 2);
         if (cb.mx[dim] == cb.mn[dim]) {
-            if (n <= maxLeaf) return makeLeaf();
-            int mid = (start + end) / 2;  // all centroids coincide: split the list
-            nodes[idx].left = Build(start, mid);
-            nodes[idx].right = Build(mid, end);
-            return idx;
+            if (n <= maxLeaf) return -1;
+            return (start + end) / 2;  // all centroids coincide: split the list
         }
         int mid;
         if (n <= 2) {
             mid = (start + end) / 2;
             std::nth_element(&prims[start], &prims[mid], &prims[end - 1] + 1,
                              [dim](const Prim &a, const Prim &b) { return a.centroid[dim] < b.centroid[dim]; });
-        } else {
-            constexpr int nBuckets = 12;
-            int counts[nBuckets] = {0};
-            Box bbox[nBuckets];
-            auto bucketOf = [&](const Prim &p) {
-                int b = (int)(nBuckets * ((p.centroid[dim] - cb.mn[dim]) / (cb.mx[dim] - cb.mn[dim])));
-                return std::min(std::max(b, 0), nBuckets - 1);
-            };
-            for (int i = start; i < end; ++i) {
-                int b = bucketOf(prims[i]);
-                counts[b]++;
-                bbox[b].Add(prims[i].box);
+            return mid;
+        }
+        constexpr int nBuckets = 12;
+        int counts[nBuckets] = {0};
+        Box bbox[nBuckets];
+        auto bucketOf = [&](const Prim &p) {
+            int b = (int)(nBuckets * ((p.centroid[dim] - cb.mn[dim]) / (cb.mx[dim] - cb.mn[dim])));
+            return std::min(std::max(b, 0), nBuckets - 1);
+        };
+        for (int i = start; i < end; ++i) {
+            int b = bucketOf(prims[i]);
+            counts[b]++;
+            bbox[b].Add(prims[i].box);
+        }
+        float costs[nBuckets - 1] = {};
+        int countBelow = 0;
+        Box boundBelow;
+        for (int i = 0; i < nBuckets - 1; ++i) {
+            boundBelow.Add(bbox[i]);
+            countBelow += counts[i];
+            costs[i] += countBelow * boundBelow.Area();
+        }
+        int countAbove = 0;
+        Box boundAbove;
+        for (int i = nBuckets - 1; i >= 1; --i) {
+            boundAbove.Add(bbox[i]);
+            countAbove += counts[i];
+            costs[i - 1] += countAbove * boundAbove.Area();
+        }
+        int minBucket = -1;
+        float minCost = kInfinity;
+        for (int i = 0; i < nBuckets - 1; ++i)
+            if (costs[i] < minCost) {
+                minCost = costs[i];
+                minBucket = i;
             }
-            float costs[nBuckets - 1] = {};
-            int countBelow = 0;
-            Box boundBelow;
-            for (int i = 0; i < nBuckets - 1; ++i) {
-                boundBelow.Add(bbox[i]);
-                countBelow += counts[i];
-                costs[i] += countBelow * boundBelow.Area();
-            }
-            int countAbove = 0;
-            Box boundAbove;
-            for (int i = nBuckets - 1; i >= 1; --i) {
-                boundAbove.Add(bbox[i]);
-                countAbove += counts[i];
-                costs[i - 1] += countAbove * boundAbove.Area();
-            }
-            int minBucket = -1;
-            float minCost = kInfinity;
-            for (int i = 0; i < nBuckets - 1; ++i)
-                if (costs[i] < minCost) {
-                    minCost = costs[i];
-                    minBucket = i;
-                }
-            float leafCost = (float)n;
-            minCost = 1.f / 2.f + minCost / node.box.Area();
-            if (n > maxLeaf || minCost < leafCost) {
-                Prim *pm = std::partition(&prims[start], &prims[end - 1] + 1,
-                                          [&](const Prim &p) { return bucketOf(p) <= minBucket; });
-                mid = (int)(pm - &prims[0]);
-                if (mid == start || mid == end) {
-                    mid = (start + end) / 2;
-                    std::nth_element(&prims[start], &prims[mid], &prims[end - 1] + 1,
-                                     [dim](const Prim &a, const Prim &b) { return a.centroid[dim] < b.centroid[dim]; });
-                }
-            } else {
-                return makeLeaf();
-            }
+        float leafCost = (float)n;
+        minCost = 1.f / 2.f + minCost / nb.Area();
+        if (!(n > maxLeaf || minCost < leafCost)) return -1;
+        Prim *pm = std::partition(&prims[start], &prims[end - 1] + 1,
+                                  [&](const Prim &p) { return bucketOf(p) <= minBucket; });
+        mid = (int)(pm - &prims[0]);
+        if (mid == start || mid == end) {
+            mid = (start + end) / 2;
+            std::nth_element(&prims[start], &prims[mid], &prims[end - 1] + 1,
+                             [dim](const Prim &a, const Prim &b) { return a.centroid[dim] < b.centroid[dim]; });
+        }
+        return mid;
+    }
+
+    int Build(int start, int end) {
+        int idx = (int)nodes.size();
+        nodes.push_back(Node2{});
+        Box box;
+        int mid = Split(start, end, &box);
+        nodes[idx].box = box;
+        if (mid < 0) {
+            nodes[idx].first = start;
+            nodes[idx].count = end - start;
+            return idx;
         }
         int l = Build(start, mid);
         int r = Build(mid, end);
@@ -129,6 +134,47 @@ struct Builder2 {
         return idx;
     }
 };
+
+// The same tree built with the top levels' subtrees on their own threads: each subtree lands
+// in its own node array and the arrays are concatenated in depth-first order (node, left
+// subtree, right subtree), i.e. exactly the serial Build's layout.
+std::vector<Node2> BuildParallel(std::vector<Prim> &prims, int start, int end, int maxLeaf, int depth) {
+    Builder2 b{prims, {}, maxLeaf};
+    if (depth >= 4 || end - start < (1 << 16)) {
+        b.nodes.reserve(2 * (end - start) / std::max(maxLeaf / 2, 1) + 1);
+        b.Build(start, end);
+        return std::move(b.nodes);
+    }
+    Box box;
+    int mid = b.Split(start, end, &box);
+    Node2 root;
+    root.box = box;
+    if (mid < 0) {
+        root.first = start;
+        root.count = end - start;
+        return {root};
+    }
+    auto left = std::async(std::launch::async, BuildParallel, std::ref(prims), start, mid, maxLeaf, depth + 1);
+    std::vector<Node2> r = BuildParallel(prims, mid, end, maxLeaf, depth + 1);
+    std::vector<Node2> l = left.get();
+    std::vector<Node2> out;
+    out.reserve(1 + l.size() + r.size());
+    out.push_back(root);
+    auto append = [&](const std::vector<Node2> &sub) {
+        const int off = (int)out.size();
+        for (Node2 n : sub) {
+            if (!n.leaf()) {
+                n.left += off;
+                n.right += off;
+            }
+            out.push_back(n);
+        }
+        return off;
+    };
+    out[0].left = append(l);
+    out[0].right = append(r);
+    return out;
+}
 }  // namespace
 
 BVH8 BuildBVH8(const std::vector<V3> &verts, const std::vector<std::array<int, 3>> &tris, int maxLeafPrims) {
@@ -182,8 +228,7 @@ BVH8 BuildBVH8(const std::vector<V3> &verts, const std::vector<std::array<int, 3
     }
     maxLeafPrims = std::min(std::max(maxLeafPrims, 1), 8);
     Builder2 b{prims, {}, maxLeafPrims};
-    b.nodes.reserve(2 * prims.size());
-    b.Build(0, (int)prims.size());
+    b.nodes = BuildParallel(prims, 0, (int)prims.size(), maxLeafPrims, 0);
 
     // ordered triangles follow the BVH2 leaf order (prims array order)
     out.triPrim.resize(prims.size());

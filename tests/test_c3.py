@@ -109,3 +109,15 @@ def test_oracle_c3_plausible(pa, oracle):
     img = _rgb(oracle, sc, oracle.render(sc, threads=8))
     assert np.isfinite(img).all() and img.min() >= 0
     assert 0.05 < img.mean() < 1.0
+
+
+def test_c4_generator_small_variant_loads(pa, oracle, tmp_path):
+    """scenes/gen_c4.py (PLY copies, diffuse + named-metal conductors) at a small size."""
+    import gen_c4
+    path, n = gen_c4.generate(tmp_path, copies=6, level=2, xres=48, yres=27, spp=4)
+    sc = pa.load_scene(path)
+    assert sc.info.n_triangles == n == 6 * 320 + 4
+    f, types, params, spectra = _flat_materials(sc)
+    assert types.count(2) >= 3 and types.count(0) >= 4
+    img = _rgb(oracle, sc, oracle.render(sc, threads=8))
+    assert np.isfinite(img).all() and img.mean() > 0.01

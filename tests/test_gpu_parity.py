@@ -127,6 +127,18 @@ def test_vertex_normals_and_uv_match_oracle(pa, oracle, sampler):
     print(f"vertex normals/uv ({sampler}) parity: {frac*100:.3f}% pixels within 1e-3, mean rel {mean_rel:.2e}")
 
 
+def test_c4_small_variant_matches_oracle(pa, oracle, tmp_path):
+    """C4's construction (PLY copies, named-metal conductors, 124 materials) at 1/1000 size."""
+    import sys
+    sys.path.insert(0, str(SCENES))
+    import gen_c4
+    path, _ = gen_c4.generate(tmp_path, copies=12, level=3, xres=160, yres=90, spp=8)
+    sc = pa.load_scene(path)
+    film, _ = gpu_film(pa, sc)
+    frac, mean_rel = check_parity(to_rgb(oracle, sc, film), to_rgb(oracle, sc, oracle.render(sc, threads=16)))
+    print(f"C4 small parity: {frac*100:.3f}% pixels within 1e-3, mean rel {mean_rel:.2e}")
+
+
 def test_sample_splits_bit_exact(pa):
     sc = pa.load_scene(SCENES / "cornell-box.pbrt", xresolution=64, yresolution=48, spp=8)
     full, _ = gpu_film(pa, sc)

@@ -141,6 +141,7 @@ struct pbrt_context {
     DeviceScene S{};
     // scene buffers
     DevBuf<BVH8Node> nodes;
+    DevBuf<BVH8QNode> qnodes;
     DevBuf<float> triVerts, matCoeffs, lightScale, lightArea, infScale, dense, sensor;
     DevBuf<int> primMaterial, primLight, matConstant, lightPrim, lightSpectrum, lightTwoSided, infSpectrum;
     DevBuf<int> primOrig, matType, matSpectra, plOffsets;
@@ -201,6 +202,7 @@ static void BuildDevice(pbrt_context *c) {
         pf[i] = s.triFlip[o];
     }
     c->nodes.Upload(b.nodes);
+    c->qnodes.Upload(b.qnodes);
     c->triVerts.Upload(b.triVerts);
     c->primMaterial.Upload(pm);
     c->primLight.Upload(pl);
@@ -363,6 +365,7 @@ static void BuildDevice(pbrt_context *c) {
 
     DeviceScene &S = c->S;
     S.nodes = c->nodes.p;
+    S.qnodes = c->qnodes.p;
     S.triVerts = (const float4 *)c->triVerts.p;
     S.nTris = nt;
     S.primMaterial = c->primMaterial.p;
@@ -484,11 +487,18 @@ static void BuildDevice(pbrt_context *c) {
     }
     S.stackSize = c->bvh.maxStack;
     {
+        // Node format: the 256-B wide node by default; PBRT_AMD_BVH=compressed selects the 80-B
+        // quantised node.  Measured: the quantised node cuts node bytes 3.2x but
+        // its decode adds VALU work to a traversal that is issue-bound, not bandwidth-bound,
+        // so it is 1-5 % slower on C3 and C4 today.
+        const char *fmt = getenv("PBRT_AMD_BVH");
+        S.compressed = fmt && strcmp(fmt, "compressed") == 0;
         // LDS scene cache: top BVH8 nodes first (BFS order), then leading leaf-order triangles
+        const int stride = 16 * LdsNodeStride(S.compressed);
         int nNodes = (int)c->bvh.nodes.size(), budget = kSceneLdsBudget;
-        S.ldsNodes = std::min(nNodes, budget / (17 * 16));
-        budget -= S.ldsNodes * 17 * 16;
-        S.ldsTris = (S.ldsNodes == nNodes && nt * 48 <= budget) ? nt : 0;  // all or none
+        S.ldsNodes = std::min(nNodes, budget / stride);
+        budget -= S.ldsNodes * stride;
+        S.ldsTris = (!S.compressed && S.ldsNodes == nNodes && nt * 48 <= budget) ? nt : 0;  // all or none
     }
 
     // film

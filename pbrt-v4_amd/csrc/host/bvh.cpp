@@ -177,6 +177,79 @@ std::vector<Node2> BuildParallel(std::vector<Prim> &prims, int start, int end, i
 }
 }  // namespace
 
+// Quantise every node of out.nodes into out.qnodes (same indices).
+static void Compress(BVH8 &out) {
+    out.qnodes.assign(out.nodes.size(), BVH8QNode{});
+    for (size_t i = 0; i < out.nodes.size(); ++i) {
+        const BVH8Node &n = out.nodes[i];
+        BVH8QNode &q = out.qnodes[i];
+        float lo[3] = {kInfinity, kInfinity, kInfinity}, hi[3] = {-kInfinity, -kInfinity, -kInfinity};
+        const float *clo[3] = {n.lox, n.loy, n.loz}, *chi[3] = {n.hix, n.hiy, n.hiz};
+        bool any = false;
+        for (int c = 0; c < 8; ++c) {
+            if (n.child[c] == kEmptyChild) continue;
+            any = true;
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = std::min(lo[a], clo[a][c]);
+                hi[a] = std::max(hi[a], chi[a][c]);
+            }
+        }
+        uint8_t e[3] = {127, 127, 127};
+        if (any)
+            for (int a = 0; a < 3; ++a) {
+                // smallest exponent whose 255-step grid from lo reaches hi
+                const double ext = (double)hi[a] - lo[a];
+                int ex = (int)std::ceil(std::log2(std::max(ext / 255.0, 1e-37))) + 127;
+                ex = std::min(std::max(ex, 1), 254);
+                while (ex < 254 && DecodeQ(255, (uint8_t)ex, lo[a]) < hi[a]) ++ex;
+                while (ex > 1 && DecodeQ(255, (uint8_t)(ex - 1), lo[a]) >= hi[a]) --ex;
+                e[a] = (uint8_t)ex;
+            }
+        q.px = any ? lo[0] : 0;
+        q.py = any ? lo[1] : 0;
+        q.pz = any ? lo[2] : 0;
+        q.ex = e[0], q.ey = e[1], q.ez = e[2];
+        uint8_t *qlo[3] = {q.qlox, q.qloy, q.qloz}, *qhi[3] = {q.qhix, q.qhiy, q.qhiz};
+        const float org[3] = {q.px, q.py, q.pz};
+        int innerRank = 0, triBase = -1;
+        q.childBase = -1;
+        for (int c = 0; c < 8; ++c) {
+            const int ch = n.child[c];
+            if (ch == kEmptyChild) {
+                for (int a = 0; a < 3; ++a) qlo[a][c] = 255, qhi[a][c] = 0;
+                continue;
+            }
+            for (int a = 0; a < 3; ++a) {
+                double s = std::ldexp(1.0, (int)e[a] - 127);
+                int l = (int)std::floor(((double)clo[a][c] - org[a]) / s);
+                int h = (int)std::ceil(((double)chi[a][c] - org[a]) / s);
+                l = std::min(std::max(l, 0), 255);
+                h = std::min(std::max(h, 0), 255);
+                while (l > 0 && DecodeQ((uint8_t)l, e[a], org[a]) > clo[a][c]) --l;
+                while (h < 255 && DecodeQ((uint8_t)h, e[a], org[a]) < chi[a][c]) ++h;
+                if (DecodeQ((uint8_t)l, e[a], org[a]) > clo[a][c] || DecodeQ((uint8_t)h, e[a], org[a]) < chi[a][c])
+                    throw std::runtime_error("BVH8 quantisation is not conservative");
+                qlo[a][c] = (uint8_t)l;
+                qhi[a][c] = (uint8_t)h;
+            }
+            if (ch >= 0) {
+                if (q.childBase < 0) q.childBase = ch;
+                if (ch != q.childBase + innerRank) throw std::runtime_error("BVH8 interior children not contiguous");
+                ++innerRank;
+                q.imask |= (uint8_t)(1u << c);
+            } else {
+                const int enc = ~ch, first = enc >> 3, count = (enc & 7) + 1;
+                if (triBase < 0) triBase = first;
+                const int off = first - triBase;
+                if (off < 0 || off > 31 || count > 4) throw std::runtime_error("BVH8 leaf range does not fit the compressed node");
+                q.meta[c] = (uint8_t)(0x80 | ((count - 1) << 5) | off);
+            }
+        }
+        q.triBase = triBase < 0 ? 0 : triBase;
+        if (q.childBase < 0) q.childBase = 0;
+    }
+}
+
 BVH8 BuildBVH8(const std::vector<V3> &verts, const std::vector<std::array<int, 3>> &tris, int maxLeafPrims) {
     BVH8 out;
     std::vector<Prim> prims;
@@ -224,37 +297,20 @@ BVH8 BuildBVH8(const std::vector<V3> &verts, const std::vector<std::array<int, 3
         }
         out.nodes.push_back(root);
         appendDegenerate();
+        Compress(out);
         return out;
     }
     maxLeafPrims = std::min(std::max(maxLeafPrims, 1), 8);
     Builder2 b{prims, {}, maxLeafPrims};
     b.nodes = BuildParallel(prims, 0, (int)prims.size(), maxLeafPrims, 0);
 
-    // ordered triangles follow the BVH2 leaf order (prims array order)
-    out.triPrim.resize(prims.size());
-    out.triVerts.resize(prims.size() * 12);
-    for (size_t i = 0; i < prims.size(); ++i) {
-        int t = prims[i].index;
-        out.triPrim[i] = t;
-        for (int k = 0; k < 3; ++k) {
-            V3 p = verts[tris[t][k]];
-            out.triVerts[i * 12 + k * 4 + 0] = p.x;
-            out.triVerts[i * 12 + k * 4 + 1] = p.y;
-            out.triVerts[i * 12 + k * 4 + 2] = p.z;
-            float w = 0;
-            if (k == 0) {
-                int32_t tt = t;
-                memcpy(&w, &tt, 4);
-            }
-            out.triVerts[i * 12 + k * 4 + 3] = w;
-        }
-    }
-
     // collapse BVH2 -> BVH8 (greedy: open the child with the largest surface area)
     struct Work {
         int node2, depth;
     };
     std::vector<Work> queue;
+    std::vector<int> order;  // leaf-order triangles (original indices)
+    order.reserve(prims.size());
     queue.push_back({0, 1});
     out.nodes.reserve(prims.size() / 2 + 1);
     std::vector<int> node8Of;  // per queue entry the BVH8 index
@@ -292,6 +348,8 @@ BVH8 BuildBVH8(const std::vector<V3> &verts, const std::vector<std::array<int, 3
         }
         BVH8Node node{};
         node.nChildren = (int)kids.size();
+        // a node's leaf triangles are emitted contiguously (BFS node order), so both node
+        // formats address them as one range
         for (int c = 0; c < 8; ++c) {
             if (c < (int)kids.size()) {
                 const Node2 &k = b.nodes[kids[c]];
@@ -303,7 +361,9 @@ BVH8 BuildBVH8(const std::vector<V3> &verts, const std::vector<std::array<int, 3
                 node.hiz[c] = k.box.mx.z;
                 if (k.leaf()) {
                     if (k.count > 8) throw std::runtime_error("BVH leaf larger than 8 triangles");
-                    node.child[c] = ~((k.first << 3) | (k.count - 1));
+                    const int first = (int)order.size();
+                    for (int i = k.first; i < k.first + k.count; ++i) order.push_back(prims[i].index);
+                    node.child[c] = ~((first << 3) | (k.count - 1));
                 } else {
                     int idx8 = (int)out.nodes.size() + (int)(queue.size() - head);
                     // index assigned in BFS order: position in queue
@@ -322,7 +382,24 @@ BVH8 BuildBVH8(const std::vector<V3> &verts, const std::vector<std::array<int, 3
         out.nodes[self] = node;
     }
     out.nodes.resize(queue.size());
+    out.triPrim.resize(order.size());
+    out.triVerts.resize(order.size() * 12);
+    for (size_t i = 0; i < order.size(); ++i) {
+        const int t = order[i];
+        out.triPrim[i] = t;
+        for (int k = 0; k < 3; ++k) {
+            V3 p = verts[tris[t][k]];
+            float w = 0;
+            if (k == 0) {
+                int32_t tt = t;
+                memcpy(&w, &tt, 4);
+            }
+            float *d = &out.triVerts[i * 12 + k * 4];
+            d[0] = p.x, d[1] = p.y, d[2] = p.z, d[3] = w;
+        }
+    }
     appendDegenerate();
+    Compress(out);
     // Worst-case traversal stack: a node pushes its k interior children and pops one before
     // descending, so need(n) = max(k, k - 1 + max need(child)); children follow parents in
     // BFS order, so one reverse sweep suffices.

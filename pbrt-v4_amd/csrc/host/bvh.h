@@ -26,8 +26,32 @@ struct alignas(16) BVH8Node {
 };
 static_assert(sizeof(BVH8Node) == 256, "BVH8Node must be 256 bytes");
 
+// Compressed BVH8 node (80 B, the quantised wide-node layout of Ylitie et al. 2017): child
+// boxes as 8-bit offsets on a per-node grid lo = fma(q, 2^(e-127), p), rounded outward on the
+// host with the same fma the device decodes with, so every decoded box contains the exact one.
+// Interior children are contiguous from childBase (in slot order); a node's leaf triangles are
+// contiguous from triBase.  meta[c]: 0 = empty or interior, else 0x80 | (count-1) << 5 | offset.
+struct alignas(16) BVH8QNode {
+    float px, py, pz;
+    uint8_t ex, ey, ez;
+    uint8_t imask;  // bit c: child c is an interior node
+    int32_t childBase, triBase;
+    uint8_t meta[8];
+    uint8_t qlox[8], qloy[8], qloz[8], qhix[8], qhiy[8], qhiz[8];
+};
+static_assert(sizeof(BVH8QNode) == 80, "BVH8QNode must be 80 bytes");
+
+// decoded plane of a quantised box: the device evaluates exactly this expression
+inline float DecodeQ(uint8_t q, uint8_t e, float p) {
+    uint32_t bits = (uint32_t)e << 23;
+    float s;
+    memcpy(&s, &bits, 4);
+    return fmaf((float)q, s, p);
+}
+
 struct BVH8 {
     std::vector<BVH8Node> nodes;
+    std::vector<BVH8QNode> qnodes;  // the same tree, compressed (same node indices)
     // triangles in leaf order: 3 float4 per triangle = p0.xyz|prim, p1.xyz|0, p2.xyz|0
     std::vector<float> triVerts;
     std::vector<int> triPrim;  // leaf order -> original triangle index

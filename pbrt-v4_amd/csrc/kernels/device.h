@@ -63,10 +63,15 @@ PHD int CounterIndex(int depth, int queue, int shard) {
 constexpr int kStatsSlots = 48, kStatsSectionBase = 16;
 constexpr int kMaxStackSize = 64;  // traversal stack entries per lane (64 KB of LDS per block)
 constexpr int kSceneLdsBudget = 16 * 1024;  // bytes of BVH nodes + triangles cached in LDS per block
+constexpr int kLdsNodeStride = 17;  // float4 per LDS-cached wide node (68 dwords: conflict-free)
+constexpr int kLdsQNodeStride = 5;  // float4 per LDS-cached compressed node (20 dwords: conflict-free)
+PHD int LdsNodeStride(int compressed) { return compressed ? kLdsQNodeStride : kLdsNodeStride; }
 
 struct DeviceScene {
     // geometry (leaf order)
     const BVH8Node *nodes;
+    const BVH8QNode *qnodes;  // the same tree, quantised (80 B/node)
+    int compressed;           // traverse qnodes (HBM-resident scenes) instead of nodes
     const float4 *triVerts;  // 3 per triangle
     int nTris;
     const int *primMaterial;

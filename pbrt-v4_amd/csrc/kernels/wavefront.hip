@@ -372,12 +372,81 @@ __device__ inline void SlabTest8(const F4 *__restrict__ q, const RayPre &r, floa
     SlabTest4(q, 1, r, raytMax, tn, mask);
 }
 
+// Child references of a compressed node, decoded on demand for the children actually visited
+struct QRefs {
+    unsigned imask, meta[2];
+    int childBase, triBase;
+    // the uncompressed encoding: >= 0 interior node, < 0 leaf ~(first << 3 | count - 1)
+    __device__ int Get(int c) const {
+        if ((imask >> c) & 1u) return childBase + __popc(imask & ((1u << c) - 1u));
+        const unsigned m = (meta[c >> 2] >> (8 * (c & 3))) & 0xffu;
+        const int first = triBase + (int)(m & 31u), count = (int)((m >> 5) & 3u) + 1;
+        return ~((first << 3) | (count - 1));
+    }
+};
+
+// Slab tests of a compressed node (BVH8QNode, 5 float4): child planes decoded as
+// fma(q, 2^(e-127), p) -- the expression the host rounded outward -- then the same test as
+// SlabTest4.
+template <typename F4>
+__device__ inline void SlabTestQ(const F4 *__restrict__ q, const RayPre &r, float raytMax, float tn[8],
+                                 unsigned *mask, QRefs *refs) {
+    const float4 f0 = q[0], f1 = q[1], f2 = q[2], f3 = q[3], f4 = q[4];
+    const unsigned eb = __float_as_uint(f0.w);
+    const float sx = __uint_as_float((eb & 0xffu) << 23), sy = __uint_as_float(((eb >> 8) & 0xffu) << 23),
+                sz = __uint_as_float(((eb >> 16) & 0xffu) << 23);
+    const unsigned imask = eb >> 24;
+    const int childBase = __float_as_int(f1.x), triBase = __float_as_int(f1.y);
+    const unsigned meta[2] = {__float_as_uint(f1.z), __float_as_uint(f1.w)};
+    const unsigned qw[12] = {__float_as_uint(f2.x), __float_as_uint(f2.y), __float_as_uint(f2.z),
+                             __float_as_uint(f2.w), __float_as_uint(f3.x), __float_as_uint(f3.y),
+                             __float_as_uint(f3.z), __float_as_uint(f3.w), __float_as_uint(f4.x),
+                             __float_as_uint(f4.y), __float_as_uint(f4.z), __float_as_uint(f4.w)};
+    const float slack = 1 + 2 * gamma(3);
+    *mask = 0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const int w = c >> 2, sh = 8 * (c & 3);
+        auto byteOf = [&](int field) { return (float)((qw[2 * field + w] >> sh) & 0xffu); };
+        const float lo[3] = {fmaf(byteOf(0), sx, f0.x), fmaf(byteOf(1), sy, f0.y), fmaf(byteOf(2), sz, f0.z)};
+        const float hi[3] = {fmaf(byteOf(3), sx, f0.x), fmaf(byteOf(4), sy, f0.y), fmaf(byteOf(5), sz, f0.z)};
+        float nx = r.neg[0] ? hi[0] : lo[0], fx = r.neg[0] ? lo[0] : hi[0];
+        float ny = r.neg[1] ? hi[1] : lo[1], fy = r.neg[1] ? lo[1] : hi[1];
+        float nz = r.neg[2] ? hi[2] : lo[2], fz = r.neg[2] ? lo[2] : hi[2];
+        float tMin = (nx - r.o.x) * r.invDir.x;
+        float tMax = (fx - r.o.x) * r.invDir.x * slack;
+        float tyMin = (ny - r.o.y) * r.invDir.y;
+        float tyMax = (fy - r.o.y) * r.invDir.y * slack;
+        bool ok = !(tMin > tyMax || tyMin > tMax);
+        tMin = tyMin > tMin ? tyMin : tMin;
+        tMax = tyMax < tMax ? tyMax : tMax;
+        float tzMin = (nz - r.o.z) * r.invDir.z;
+        float tzMax = (fz - r.o.z) * r.invDir.z * slack;
+        ok = ok && !(tMin > tzMax || tzMin > tMax);
+        tMin = tzMin > tMin ? tzMin : tMin;
+        tMax = tzMax < tMax ? tzMax : tMax;
+        ok = ok && (tMin < raytMax) && (tMax > 0);
+        tn[c] = tMin;
+        *mask |= ok ? (1u << c) : 0u;
+    }
+    // occupied slots: interior (imask) or leaf (meta bit 7)
+    const unsigned leafBits = ((meta[0] >> 7) & 1u) | ((meta[0] >> 14) & 2u) | ((meta[0] >> 21) & 4u) |
+                              ((meta[0] >> 28) & 8u) | (((meta[1] >> 7) & 1u) << 4) | (((meta[1] >> 15) & 1u) << 5) |
+                              (((meta[1] >> 23) & 1u) << 6) | (((meta[1] >> 31) & 1u) << 7);
+    *mask &= imask | leafBits;
+    refs->imask = imask;
+    refs->meta[0] = meta[0];
+    refs->meta[1] = meta[1];
+    refs->childBase = childBase;
+    refs->triBase = triBase;
+}
+
 // Scene cache in LDS: the first S.ldsNodes BVH8 nodes (BFS order = the top of the tree) at a
 // 17-float4 stride and the first S.ldsTris triangles of the leaf order.  The 68-dword node
 // stride puts the same field of 16 different nodes in 16 different 4-bank groups, so the
 // ds_read_b128 lane groups stay conflict-free when lanes sit in different nodes; the 12-dword
 // triangle stride does the same for triangles.  Everything else is read from global memory.
-constexpr int kLdsNodeStride = 17;  // float4 per cached node
+// (strides: kLdsNodeStride / kLdsQNodeStride, device.h)
 
 // LDS-qualified pointers keep the cached and the global paths distinct instructions
 // (ds_read_b128 vs global_load_dwordx4); generic pointers would merge them into flat loads.
@@ -397,12 +466,17 @@ __device__ inline SceneLds SetupSceneLds(const DeviceScene &S, float4 *dyn) {
     SceneLds L;
     L.stack = reinterpret_cast<int *>(dyn);
     float4 *nodes = dyn + (S.stackSize * kBlock) / 4;
-    float4 *tris = nodes + S.ldsNodes * kLdsNodeStride;
+    float4 *tris = nodes + S.ldsNodes * LdsNodeStride(S.compressed);
     // plain copies: measured faster here than per-node LDS-DMA (few, tiny rows)
-    const float4 *gn = reinterpret_cast<const float4 *>(S.nodes);
-    for (int i = threadIdx.x; i < S.ldsNodes * 14; i += blockDim.x) {
-        int n = i / 14, k = i - n * 14;
-        nodes[n * kLdsNodeStride + k] = gn[n * 16 + k];
+    if (S.compressed) {
+        const float4 *gn = reinterpret_cast<const float4 *>(S.qnodes);
+        for (int i = threadIdx.x; i < S.ldsNodes * kLdsQNodeStride; i += blockDim.x) nodes[i] = gn[i];
+    } else {
+        const float4 *gn = reinterpret_cast<const float4 *>(S.nodes);
+        for (int i = threadIdx.x; i < S.ldsNodes * 14; i += blockDim.x) {
+            int n = i / 14, k = i - n * 14;
+            nodes[n * kLdsNodeStride + k] = gn[n * 16 + k];
+        }
     }
     for (int i = threadIdx.x; i < S.ldsTris * 3; i += blockDim.x) tris[i] = S.triVerts[i];
     __syncthreads();
@@ -413,7 +487,7 @@ __device__ inline SceneLds SetupSceneLds(const DeviceScene &S, float4 *dyn) {
 
 // TrisInLds: every triangle is cached (a launch-uniform choice, so no per-lane branch whose
 // two loads the compiler would merge into one flat load).
-template <bool AnyHit, bool TrisInLds>
+template <bool AnyHit, bool TrisInLds, bool Compressed>
 __device__ inline int TraverseT(const DeviceScene &S, const SceneLds &L, V3 o, V3 d, float tMax, TriHit *best) {
     const TriRay tr = MakeTriRay(o, d);
     RayPre r;
@@ -430,27 +504,40 @@ __device__ inline int TraverseT(const DeviceScene &S, const SceneLds &L, V3 o, V
     while (true) {
         float tn[8];
         unsigned mask;
-        int4 ch0, ch1;
-        if (node < S.ldsNodes) {
-            const LdsF4 *q = L.nodes + node * kLdsNodeStride;
-            SlabTest8(q, r, tMax, tn, &mask);
-            float4 c0 = q[12], c1 = q[13];
-            ch0 = make_int4(__float_as_int(c0.x), __float_as_int(c0.y), __float_as_int(c0.z), __float_as_int(c0.w));
-            ch1 = make_int4(__float_as_int(c1.x), __float_as_int(c1.y), __float_as_int(c1.z), __float_as_int(c1.w));
+        int ch[8];
+        QRefs qr;
+        if constexpr (Compressed) {
+            if (node < S.ldsNodes) SlabTestQ(L.nodes + node * kLdsQNodeStride, r, tMax, tn, &mask, &qr);
+            else SlabTestQ(reinterpret_cast<const float4 *>(S.qnodes + node), r, tMax, tn, &mask, &qr);
         } else {
-            const BVH8Node *np = S.nodes + node;
-            SlabTest8(reinterpret_cast<const float4 *>(np), r, tMax, tn, &mask);
-            ch0 = reinterpret_cast<const int4 *>(np->child)[0];
-            ch1 = reinterpret_cast<const int4 *>(np->child)[1];
+            int4 ch0, ch1;
+            if (node < S.ldsNodes) {
+                const LdsF4 *q = L.nodes + node * kLdsNodeStride;
+                SlabTest8(q, r, tMax, tn, &mask);
+                float4 c0 = q[12], c1 = q[13];
+                ch0 = make_int4(__float_as_int(c0.x), __float_as_int(c0.y), __float_as_int(c0.z), __float_as_int(c0.w));
+                ch1 = make_int4(__float_as_int(c1.x), __float_as_int(c1.y), __float_as_int(c1.z), __float_as_int(c1.w));
+            } else {
+                const BVH8Node *np = S.nodes + node;
+                SlabTest8(reinterpret_cast<const float4 *>(np), r, tMax, tn, &mask);
+                ch0 = reinterpret_cast<const int4 *>(np->child)[0];
+                ch1 = reinterpret_cast<const int4 *>(np->child)[1];
+            }
+            ch[0] = ch0.x, ch[1] = ch0.y, ch[2] = ch0.z, ch[3] = ch0.w;
+            ch[4] = ch1.x, ch[5] = ch1.y, ch[6] = ch1.z, ch[7] = ch1.w;
         }
-        // empty slots carry an inverted box, so they never pass the slab test
+        // empty slots fail the slab test (inverted box / masked compressed slot)
         unsigned leaves = 0, inner = 0;
-        int ch[8] = {ch0.x, ch0.y, ch0.z, ch0.w, ch1.x, ch1.y, ch1.z, ch1.w};
+        if constexpr (Compressed) {
+            inner = mask & qr.imask;
+            leaves = mask & ~qr.imask;
+        } else {
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            if (mask & (1u << c)) {
-                if (ch[c] < 0) leaves |= 1u << c;
-                else inner |= 1u << c;
+            for (int c = 0; c < 8; ++c) {
+                if (mask & (1u << c)) {
+                    if (ch[c] < 0) leaves |= 1u << c;
+                    else inner |= 1u << c;
+                }
             }
         }
         // leaves nearest-first
@@ -466,8 +553,12 @@ __device__ inline int TraverseT(const DeviceScene &S, const SceneLds &L, V3 o, V
             leaves &= ~(1u << bc);
             if (bt >= tMax) continue;
             int enc = 0;
+            if constexpr (Compressed) {
+                enc = ~qr.Get(bc);
+            } else {
 #pragma unroll
-            for (int c = 0; c < 8; ++c) enc = (c == bc) ? ~ch[c] : enc;
+                for (int c = 0; c < 8; ++c) enc = (c == bc) ? ~ch[c] : enc;
+            }
             int first = enc >> 3, count = (enc & 7) + 1;
             for (int t = first; t < first + count; ++t) {
                 float4 a, b, c;
@@ -502,8 +593,12 @@ __device__ inline int TraverseT(const DeviceScene &S, const SceneLds &L, V3 o, V
             inner &= ~(1u << bc);
             if (bt >= tMax) continue;
             int child = 0;
+            if constexpr (Compressed) {
+                child = qr.Get(bc);
+            } else {
 #pragma unroll
-            for (int c = 0; c < 8; ++c) child = (c == bc) ? ch[c] : child;
+                for (int c = 0; c < 8; ++c) child = (c == bc) ? ch[c] : child;
+            }
             lds[(sp++) * stride + lane] = child;  // sp < S.stackSize by construction
         }
         if (sp == 0) break;
@@ -512,10 +607,16 @@ __device__ inline int TraverseT(const DeviceScene &S, const SceneLds &L, V3 o, V
     return hitPrim;
 }
 
-template <bool AnyHit>
+// Q: the launch's node format (a kernel template parameter, so each kernel carries only the
+// traversal loops of its own format)
+template <bool AnyHit, bool Q>
 __device__ inline int Traverse(const DeviceScene &S, const SceneLds &L, V3 o, V3 d, float tMax, TriHit *best) {
-    if (S.ldsTris > 0) return TraverseT<AnyHit, true>(S, L, o, d, tMax, best);
-    return TraverseT<AnyHit, false>(S, L, o, d, tMax, best);
+    if constexpr (Q) {
+        return TraverseT<AnyHit, false, true>(S, L, o, d, tMax, best);
+    } else {
+        if (S.ldsTris > 0) return TraverseT<AnyHit, true, false>(S, L, o, d, tMax, best);
+        return TraverseT<AnyHit, false, false>(S, L, o, d, tMax, best);
+    }
 }
 
 // ------------------------------------------------------------------ lights
@@ -803,7 +904,7 @@ __global__ void __launch_bounds__(kBlock) k_camera(DeviceScene S, PathState st, 
 }
 
 // NMatQ = 1: every material is diffuse (one material queue); 3: one queue per material type
-template <int NMatQ>
+template <int NMatQ, bool Q>
 __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_closest(DeviceScene S, PathState st, int depth, int timed) {
     const QueueView rays = LoadQueue(st, depth, kCntRay);
     if ((int)(blockIdx.x * blockDim.x) >= rays.total) return;  // no work
@@ -842,7 +943,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_closest(Device
         if (active) {
             const V3 o(rec.ray[qi], rec.ray[N + qi], rec.ray[2 * N + qi]);
             const V3 d(rec.ray[3 * N + qi], rec.ray[4 * N + qi], rec.ray[5 * N + qi]);
-            prim = Traverse<false>(S, L, o, d, kInfinity, &h);
+            prim = Traverse<false, Q>(S, L, o, d, kInfinity, &h);
             if (prim >= 0) {
                 hitPrim[qi] = prim;
                 hitB[qi] = h.b0;
@@ -1632,6 +1733,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
     }
 }
 
+template <bool Q>
 __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_shadow(DeviceScene S, PathState st, int depth) {
     const QueueView shadows = LoadQueue(st, depth, kCntShadow);
     if ((int)(blockIdx.x * blockDim.x) >= shadows.total) return;  // no work
@@ -1646,7 +1748,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_shadow(DeviceS
         V3 o(st.shadowRay[p], st.shadowRay[N + p], st.shadowRay[2 * N + p]);
         V3 d(st.shadowRay[3 * N + p], st.shadowRay[4 * N + p], st.shadowRay[5 * N + p]);
         TriHit h;
-        int hit = Traverse<true>(S, L, o, d, 1 - kShadowEpsilon, &h);
+        int hit = Traverse<true, Q>(S, L, o, d, 1 - kShadowEpsilon, &h);
         if (hit < 0) {
             const int slot = st.shadowPixel[p];
             st.L[slot] += st.shadowL[p];
@@ -1684,6 +1786,7 @@ __global__ void __launch_bounds__(kBlock) k_film(DeviceScene S, PathState st, in
 // ------------------------------------------------------------------ stand-alone intersection
 // The WavefrontAggregate boundary exposed on its own (integrator.h:32-54): closest / any hit
 // for an SoA ray batch, used by parity tests and the traversal benchmark.
+template <bool Q>
 __global__ void __launch_bounds__(kBlock, 4) k_intersect_batch(DeviceScene S, const float *rays, int n, int anyHit,
                                                               int *outPrim, float *outHit) {
     extern __shared__ float4 dynLds[];
@@ -1693,7 +1796,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_intersect_batch(DeviceScene S, co
         V3 d(rays[3 * n + i], rays[4 * n + i], rays[5 * n + i]);
         float tMax = rays[6 * n + i];
         TriHit h{0, 0, 0, 0};
-        int prim = anyHit ? Traverse<true>(S, L, o, d, tMax, &h) : Traverse<false>(S, L, o, d, tMax, &h);
+        int prim = anyHit ? Traverse<true, Q>(S, L, o, d, tMax, &h) : Traverse<false, Q>(S, L, o, d, tMax, &h);
         outPrim[i] = prim;
         outHit[i] = h.b0;
         outHit[n + i] = h.b1;
@@ -1703,10 +1806,13 @@ __global__ void __launch_bounds__(kBlock, 4) k_intersect_batch(DeviceScene S, co
 }
 
 // ------------------------------------------------------------------ launch helpers (host)
-size_t TraversalLdsBytes(int stackSize, int ldsNodes, int ldsTris) {
-    return (size_t)stackSize * kBlock * sizeof(int) + (size_t)ldsNodes * kLdsNodeStride * 16 + (size_t)ldsTris * 48;
+size_t TraversalLdsBytes(int stackSize, int ldsNodes, int ldsTris, int compressed) {
+    return (size_t)stackSize * kBlock * sizeof(int) + (size_t)ldsNodes * LdsNodeStride(compressed) * 16 +
+           (size_t)ldsTris * 48;
 }
-static size_t StackBytes(const DeviceScene &S) { return TraversalLdsBytes(S.stackSize, S.ldsNodes, S.ldsTris); }
+static size_t StackBytes(const DeviceScene &S) {
+    return TraversalLdsBytes(S.stackSize, S.ldsNodes, S.ldsTris, S.compressed);
+}
 
 // Traversal kernels loop over their queue inside a bounded grid so the LDS scene cache is
 // filled once per block, not once per 256 rays.
@@ -1743,12 +1849,15 @@ hipError_t LaunchCamera(const DeviceScene &S, const PathState &st, int nActive, 
 }
 hipError_t LaunchClosest(const DeviceScene &S, const PathState &st, int depth, int maxCount, int timed,
                          hipStream_t s) {
-    if (S.matTypeMask & ~1)
-        hipLaunchKernelGGL(k_closest<kNumMatTypes>, dim3(TraversalGridFor(maxCount)), dim3(kBlock), StackBytes(S), s, S,
-                           st, depth, timed);
-    else
-        hipLaunchKernelGGL(k_closest<1>, dim3(TraversalGridFor(maxCount)), dim3(kBlock), StackBytes(S), s, S, st,
-                           depth, timed);
+    const dim3 grid(TraversalGridFor(maxCount)), block(kBlock);
+    const bool multi = S.matTypeMask & ~1;
+    if (S.compressed) {
+        if (multi) hipLaunchKernelGGL((k_closest<kNumMatTypes, true>), grid, block, StackBytes(S), s, S, st, depth, timed);
+        else hipLaunchKernelGGL((k_closest<1, true>), grid, block, StackBytes(S), s, S, st, depth, timed);
+    } else {
+        if (multi) hipLaunchKernelGGL((k_closest<kNumMatTypes, false>), grid, block, StackBytes(S), s, S, st, depth, timed);
+        else hipLaunchKernelGGL((k_closest<1, false>), grid, block, StackBytes(S), s, S, st, depth, timed);
+    }
     return hipGetLastError();
 }
 hipError_t LaunchEscaped(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s) {
@@ -1775,7 +1884,10 @@ hipError_t LaunchShadeMicrofacet(const DeviceScene &S, const PathState &st, int 
     return hipGetLastError();
 }
 hipError_t LaunchShadow(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s) {
-    hipLaunchKernelGGL(k_shadow, dim3(TraversalGridFor(maxCount)), dim3(kBlock), StackBytes(S), s, S, st, depth);
+    if (S.compressed)
+        hipLaunchKernelGGL(k_shadow<true>, dim3(TraversalGridFor(maxCount)), dim3(kBlock), StackBytes(S), s, S, st, depth);
+    else
+        hipLaunchKernelGGL(k_shadow<false>, dim3(TraversalGridFor(maxCount)), dim3(kBlock), StackBytes(S), s, S, st, depth);
     return hipGetLastError();
 }
 hipError_t LaunchFilm(const DeviceScene &S, const PathState &st, int nSamples, hipStream_t s) {
@@ -1784,7 +1896,12 @@ hipError_t LaunchFilm(const DeviceScene &S, const PathState &st, int nSamples, h
 }
 hipError_t LaunchIntersectBatch(const DeviceScene &S, const float *rays, int n, int anyHit, int *outPrim,
                                 float *outHit, hipStream_t s) {
-    hipLaunchKernelGGL(k_intersect_batch, dim3(TraversalGridFor(n)), dim3(kBlock), StackBytes(S), s, S, rays, n, anyHit, outPrim, outHit);
+    if (S.compressed)
+        hipLaunchKernelGGL(k_intersect_batch<true>, dim3(TraversalGridFor(n)), dim3(kBlock), StackBytes(S), s, S, rays,
+                           n, anyHit, outPrim, outHit);
+    else
+        hipLaunchKernelGGL(k_intersect_batch<false>, dim3(TraversalGridFor(n)), dim3(kBlock), StackBytes(S), s, S, rays,
+                           n, anyHit, outPrim, outHit);
     return hipGetLastError();
 }
 

@@ -139,6 +139,41 @@ def test_c4_small_variant_matches_oracle(pa, oracle, tmp_path):
     print(f"C4 small parity: {frac*100:.3f}% pixels within 1e-3, mean rel {mean_rel:.2e}")
 
 
+@pytest.mark.parametrize("fmt", ["wide", "compressed"])
+def test_bvh_node_formats_match_oracle(pa, oracle, monkeypatch, fmt):
+    """Both BVH8 node formats (256-B wide, 80-B quantised) on C3 geometry: the quantised boxes
+    are conservative, so closest hits -- and the image -- must not change."""
+    monkeypatch.setenv("PBRT_AMD_BVH", fmt)
+    sc = _c3(pa, 128, 72, 8)
+    film, _ = gpu_film(pa, sc)
+    frac, mean_rel = check_parity(to_rgb(oracle, sc, film), to_rgb(oracle, sc, oracle.render(sc, threads=16)))
+    print(f"BVH {fmt} parity: {frac*100:.3f}% pixels within 1e-3, mean rel {mean_rel:.2e}")
+
+
+def test_compressed_bvh_intersections_match_oracle(pa, oracle, monkeypatch):
+    import torch
+    monkeypatch.setenv("PBRT_AMD_BVH", "compressed")
+    sc = _c3(pa, 64, 36, 4)
+    integ = pa.WavefrontPathIntegrator(sc, max_paths=1 << 12)
+    agg = pa.HIPAggregate(integ)
+    rng = np.random.default_rng(11)
+    n = 50000
+    o = rng.uniform([-3, 0.2, -3], [3, 3, 3], size=(n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    o = o - np.array([0, 1.7, -5.2], np.float32)  # world -> render space ("cameraworld": minus the eye)
+    rays = np.concatenate([o.T, d.T, np.full((1, n), np.inf, np.float32)]).astype(np.float32)
+    gp, gh = agg.IntersectClosest(torch.from_numpy(rays).cuda())
+    gp, gh = gp.cpu().numpy(), gh.cpu().numpy()
+    op, oh = oracle.intersect(sc, rays)
+    np.testing.assert_array_equal(gp >= 0, op >= 0)
+    hit = op >= 0
+    assert hit.sum() > n // 4
+    same = gp[hit] == op[hit]
+    tie = ~same & (gh[3][hit] == oh[3][hit])
+    assert (same | tie).all()
+    np.testing.assert_array_equal(gh[3][hit], oh[3][hit])
+
+
 def test_sample_splits_bit_exact(pa):
     sc = pa.load_scene(SCENES / "cornell-box.pbrt", xresolution=64, yresolution=48, spp=8)
     full, _ = gpu_film(pa, sc)

@@ -98,6 +98,17 @@ typedef struct pbrt_scene_flat {
     const float *vertex_normals;      /* [n_vertices][3] render space */
     const float *vertex_uv;           /* [n_vertices][2] */
     const uint8_t *tri_shading;       /* [n_triangles] */
+    /* participating media (HomogeneousMedium / GridMedium); index -1 = vacuum */
+    int n_media, camera_medium;
+    const int32_t *medium_info;       /* [n_media][16]: type (0 homogeneous, 1 grid), sigma_a,
+                                         sigma_s, Le (dense_spectra indices, pbrt's scales
+                                         applied), emissive, nx, ny, nz, lnx, lny, lnz,
+                                         density offset, LeScale offset, majorant offset (into
+                                         medium_values), 0, 0 */
+    const float *medium_params;       /* [n_media][24]: g, bounds p0 xyz, p1 xyz, 0,
+                                         mediumFromRender 4x4 row-major */
+    const float *medium_values;       /* density / LeScale / 16^3 majorant grids */
+    const int16_t *tri_medium;        /* [n_triangles][2] inside, outside (NULL without media) */
 } pbrt_scene_flat;
 
 typedef struct pbrt_render_params {

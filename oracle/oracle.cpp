@@ -1389,10 +1389,322 @@ static Float PLEval(const float *lam, const float *val, int n, Float l) {
     return Lerp(t, val[o], val[o + 1]);
 }
 
+// ---------------------------------------------------------------- media
+// HomogeneousMedium / GridMedium (media.h:209-350), HGPhaseFunction (media.h:43-70,
+// util/scattering.h:49-58, util/sampling.cpp:347-373), SampleT_maj (media.h:725-800) with
+// the majorant iterators (media.h:79-205), PCG32 RNG (util/rng.h:30-140) seeded from ray
+// hashes (util/hash.h), FastExp's CPU polynomial (util/math.h:450-475).
+struct PCG32 {
+    uint64_t state = 0, inc = 1;
+    PCG32(uint64_t seqIndex, uint64_t offset) {
+        state = 0u;
+        inc = (seqIndex << 1u) | 1u;
+        NextU32();
+        state += offset;
+        NextU32();
+    }
+    uint32_t NextU32() {
+        uint64_t old = state;
+        state = old * 0x5851f42d4c957f2dULL + inc;
+        uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+        uint32_t rot = (uint32_t)(old >> 59u);
+        return (xs >> rot) | (xs << ((~rot + 1u) & 31));
+    }
+    Float Uniform() { return std::min<Float>(OneMinusEpsilon, NextU32() * 0x1p-32f); }
+};
+template <typename... T>
+static uint64_t HashFloats(T... v) {
+    const float a[] = {float(v)...};
+    return Murmur64A((const unsigned char *)a, sizeof(a), 0);
+}
+
+static Float FastExp(Float x) {
+    Float xp = x * 1.442695041f;
+    Float fxp = std::floor(xp), f = xp - fxp;
+    int i = (int)fxp;
+    // EvaluatePolynomial(f, 1, 0.695556856, 0.226173572, 0.0781455737) with FMA
+    Float twoToF = std::fma(f, std::fma(f, std::fma(f, 0.0781455737f, 0.226173572f), 0.695556856f), 1.f);
+    int exponent = (int)((FloatToBits(twoToF) >> 23) & 0xff) - 127 + i;
+    if (exponent < -126) return 0;
+    if (exponent > 127) return Infinity;
+    uint32_t bits = FloatToBits(twoToF);
+    bits &= 0b10000000011111111111111111111111u;
+    bits |= (uint32_t)(exponent + 127) << 23;
+    return BitsToFloat(bits);
+}
+
+static Float HenyeyGreenstein(Float cosTheta, Float g) {
+    g = Clamp(g, -.99f, .99f);
+    Float denom = 1 + Sqr(g) + 2 * g * cosTheta;
+    return (1 / (4 * Pi)) * (1 - Sqr(g)) / (denom * SafeSqrt(denom));
+}
+static Vec SampleHG(Vec wo, Float g, Float u0, Float u1, Float *pdf) {
+    g = Clamp(g, -.99f, .99f);
+    Float cosTheta;
+    if (std::abs(g) < 1e-3f) cosTheta = 1 - 2 * u0;
+    else cosTheta = -1 / (2 * g) * (1 + Sqr(g) - Sqr((1 - Sqr(g)) / (1 + g - 2 * g * u0)));
+    Float sinTheta = SafeSqrt(1 - Sqr(cosTheta));
+    Float phi = 2 * Pi * u1;
+    // Frame::FromZ(wo).FromLocal(SphericalDirection(sinTheta, cosTheta, phi))
+    Vec z = wo, x, y;
+    CoordinateSystem(z, &x, &y);
+    Vec l(Clamp(sinTheta, -1, 1) * std::cos(phi), Clamp(sinTheta, -1, 1) * std::sin(phi), Clamp(cosTheta, -1, 1));
+    *pdf = HenyeyGreenstein(cosTheta, g);
+    return x * l.x + y * l.y + z * l.z;
+}
+
+struct MediumProps {
+    Spectrum sigma_a, sigma_s, Le;
+};
+struct MajorantSeg {
+    Float tMin, tMax;
+    Spectrum sigma_maj;
+};
+
+struct Media {
+    const pbrt_scene_flat *f = nullptr;
+    int n = 0;
+    const int32_t *Info(int m) const { return f->medium_info + 16 * m; }
+    const float *Params(int m) const { return f->medium_params + 24 * m; }
+    Spectrum Dense(int idx, const Wavelengths &lambda) const { return SampleDense(f->dense_spectra + 311 * idx, lambda); }
+    // Transform::ApplyInverse(Point3f) (util/transform.h:387-398)
+    Vec ToMedium(int m, Vec p) const {
+        const float *M = Params(m) + 8;
+        Float x = (M[0] * p.x + M[1] * p.y) + (M[2] * p.z + M[3]);
+        Float y = (M[4] * p.x + M[5] * p.y) + (M[6] * p.z + M[7]);
+        Float z = (M[8] * p.x + M[9] * p.y) + (M[10] * p.z + M[11]);
+        Float w = (M[12] * p.x + M[13] * p.y) + (M[14] * p.z + M[15]);
+        return w == 1 ? Vec(x, y, z) : Vec(x, y, z) / w;
+    }
+    // SampledGrid<Float>::Lookup(Point3f) (util/containers.h:804-835)
+    static Float GridLookup(const float *v, int nx, int ny, int nz, Vec p) {
+        auto at = [&](int x, int y, int z) -> Float {
+            if (x < 0 || x >= nx || y < 0 || y >= ny || z < 0 || z >= nz) return 0;
+            return v[((size_t)z * ny + y) * nx + x];
+        };
+        Float sx = p.x * nx - .5f, sy = p.y * ny - .5f, sz = p.z * nz - .5f;
+        int ix = (int)std::floor(sx), iy = (int)std::floor(sy), iz = (int)std::floor(sz);
+        Float dx = sx - ix, dy = sy - iy, dz = sz - iz;
+        Float d00 = Lerp(dx, at(ix, iy, iz), at(ix + 1, iy, iz));
+        Float d10 = Lerp(dx, at(ix, iy + 1, iz), at(ix + 1, iy + 1, iz));
+        Float d01 = Lerp(dx, at(ix, iy, iz + 1), at(ix + 1, iy, iz + 1));
+        Float d11 = Lerp(dx, at(ix, iy + 1, iz + 1), at(ix + 1, iy + 1, iz + 1));
+        return Lerp(dz, Lerp(dy, d00, d10), Lerp(dy, d01, d11));
+    }
+    // Bounds3::Offset (util/vecmath.h:1325-1334)
+    Vec Offset(int m, Vec p) const {
+        const float *P = Params(m);
+        Vec o(p.x - P[1], p.y - P[2], p.z - P[3]);
+        if (P[4] > P[1]) o.x /= P[4] - P[1];
+        if (P[5] > P[2]) o.y /= P[5] - P[2];
+        if (P[6] > P[3]) o.z /= P[6] - P[3];
+        return o;
+    }
+    MediumProps SamplePoint(int m, Vec p, const Wavelengths &lambda) const {
+        const int32_t *I = Info(m);
+        MediumProps mp{Dense(I[1], lambda), Dense(I[2], lambda), Spectrum(0.f)};
+        if (I[0] == 0) {
+            mp.Le = Dense(I[3], lambda);
+            return mp;
+        }
+        Vec q = Offset(m, ToMedium(m, p));
+        Float d = GridLookup(f->medium_values + I[11], I[5], I[6], I[7], q);
+        mp.sigma_a = mp.sigma_a * d;
+        mp.sigma_s = mp.sigma_s * d;
+        if (I[4]) {
+            Float scale = GridLookup(f->medium_values + I[12], I[8], I[9], I[10], q);
+            if (scale > 0) mp.Le = Dense(I[3], lambda) * scale;
+        }
+        return mp;
+    }
+};
+
+// Majorant segments of a ray in medium m (HomogeneousMajorantIterator / DDAMajorantIterator)
+struct MajorantIter {
+    bool homogeneous = true, called = false, empty = false;
+    MajorantSeg seg;
+    // DDA state
+    const float *grid = nullptr;
+    Spectrum sigma_t;
+    Float tMin = Infinity, tMax = -Infinity, nextCrossingT[3], deltaT[3];
+    int step[3], voxelLimit[3], voxel[3];
+
+    bool Next(MajorantSeg *out) {
+        if (homogeneous) {
+            if (called || empty) return false;
+            called = true;
+            *out = seg;
+            return true;
+        }
+        if (empty || tMin >= tMax) return false;
+        int bits = ((nextCrossingT[0] < nextCrossingT[1]) << 2) + ((nextCrossingT[0] < nextCrossingT[2]) << 1) +
+                   ((nextCrossingT[1] < nextCrossingT[2]));
+        const int cmpToAxis[8] = {2, 1, 2, 1, 2, 2, 0, 0};
+        int stepAxis = cmpToAxis[bits];
+        Float tVoxelExit = std::min(tMax, nextCrossingT[stepAxis]);
+        Float mx = grid[voxel[0] + 16 * (voxel[1] + 16 * voxel[2])];
+        *out = MajorantSeg{tMin, tVoxelExit, sigma_t * mx};
+        tMin = tVoxelExit;
+        if (nextCrossingT[stepAxis] > tMax) tMin = tMax;
+        voxel[stepAxis] += step[stepAxis];
+        if (voxel[stepAxis] == voxelLimit[stepAxis]) tMin = tMax;
+        nextCrossingT[stepAxis] += deltaT[stepAxis];
+        return true;
+    }
+};
+
+static MajorantIter SampleRay(const Media &M, int m, Vec o, Vec d, Float raytMax, const Wavelengths &lambda) {
+    MajorantIter it;
+    const int32_t *I = M.Info(m);
+    Spectrum sa = M.Dense(I[1], lambda), ss = M.Dense(I[2], lambda);
+    if (I[0] == 0) {
+        it.seg = MajorantSeg{0, raytMax, sa + ss};
+        return it;
+    }
+    it.homogeneous = false;
+    // Transform::ApplyInverse(Ray, &tMax) (util/transform.h:416-429): exact origin -> Point3fi
+    const float *Mx = M.Params(m) + 8;
+    Float x = o.x, y = o.y, z = o.z;
+    Float xp = (Mx[0] * x + Mx[1] * y) + (Mx[2] * z + Mx[3]);
+    Float yp = (Mx[4] * x + Mx[5] * y) + (Mx[6] * z + Mx[7]);
+    Float zp = (Mx[8] * x + Mx[9] * y) + (Mx[10] * z + Mx[11]);
+    Vec err(gamma(3) * (std::abs(Mx[0] * x) + std::abs(Mx[1] * y) + std::abs(Mx[2] * z)),
+            gamma(3) * (std::abs(Mx[4] * x) + std::abs(Mx[5] * y) + std::abs(Mx[6] * z)),
+            gamma(3) * (std::abs(Mx[8] * x) + std::abs(Mx[9] * y) + std::abs(Mx[10] * z)));
+    Vec lo, hi;
+    Vec pc(xp, yp, zp);
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = err[a] == 0 ? pc[a] : NextFloatDown(pc[a] - err[a]);
+        hi[a] = err[a] == 0 ? pc[a] : NextFloatUp(pc[a] + err[a]);
+    }
+    Vec dm(Mx[0] * d.x + Mx[1] * d.y + Mx[2] * d.z, Mx[4] * d.x + Mx[5] * d.y + Mx[6] * d.z,
+           Mx[8] * d.x + Mx[9] * d.y + Mx[10] * d.z);
+    Float l2 = LengthSquared(dm);
+    if (l2 > 0) {
+        Vec oErr((hi.x - lo.x) / 2, (hi.y - lo.y) / 2, (hi.z - lo.z) / 2);
+        Float dt = Dot(Abs(dm), oErr) / l2;
+        for (int a = 0; a < 3; ++a) {
+            Float v = dm[a] * dt;
+            lo[a] = NextFloatDown(lo[a] + v);
+            hi[a] = NextFloatUp(hi[a] + v);
+        }
+        raytMax -= dt;
+    }
+    Vec om((lo.x + hi.x) / 2, (lo.y + hi.y) / 2, (lo.z + hi.z) / 2);
+    // Bounds3::IntersectP(o, d, tMax, &t0, &t1) (util/vecmath.h:1549-1573)
+    const float *P = M.Params(m);
+    Float t0 = 0, t1 = raytMax;
+    for (int a = 0; a < 3; ++a) {
+        Float inv = 1 / dm[a];
+        Float tNear = (P[1 + a] - om[a]) * inv, tFar = (P[4 + a] - om[a]) * inv;
+        if (tNear > tFar) std::swap(tNear, tFar);
+        tFar *= 1 + 2 * gamma(3);
+        t0 = tNear > t0 ? tNear : t0;
+        t1 = tFar < t1 ? tFar : t1;
+        if (t0 > t1) {
+            it.empty = true;
+            return it;
+        }
+    }
+    // DDAMajorantIterator (media.h:168-205) over the medium's 16^3 majorant grid
+    it.grid = M.f->medium_values + I[13];
+    it.sigma_t = sa + ss;
+    it.tMin = t0;
+    it.tMax = t1;
+    Vec diag(P[4] - P[1], P[5] - P[2], P[6] - P[3]);
+    Vec og = M.Offset(m, om);
+    Vec dg(dm.x / diag.x, dm.y / diag.y, dm.z / diag.z);
+    Vec gi = og + dg * t0;
+    for (int a = 0; a < 3; ++a) {
+        it.voxel[a] = (int)Clamp(gi[a] * 16, 0, 15);
+        it.deltaT[a] = 1 / (std::abs(dg[a]) * 16);
+        if (dg[a] == -0.f) dg[a] = 0.f;
+        if (dg[a] >= 0) {
+            Float next = Float(it.voxel[a] + 1) / 16;
+            it.nextCrossingT[a] = t0 + (next - gi[a]) / dg[a];
+            it.step[a] = 1;
+            it.voxelLimit[a] = 16;
+        } else {
+            Float next = Float(it.voxel[a]) / 16;
+            it.nextCrossingT[a] = t0 + (next - gi[a]) / dg[a];
+            it.step[a] = -1;
+            it.voxelLimit[a] = -1;
+        }
+    }
+    return it;
+}
+
+static Spectrum FastExpS(const Spectrum &s) {
+    Spectrum r;
+    for (int i = 0; i < NS; ++i) r[i] = FastExp(s[i]);
+    return r;
+}
+static Spectrum ClampZero(const Spectrum &s) {
+    Spectrum r;
+    for (int i = 0; i < NS; ++i) r[i] = std::max<Float>(0, s[i]);
+    return r;
+}
+static Spectrum operator-(const Spectrum &a, const Spectrum &b) {
+    Spectrum r;
+    for (int i = 0; i < NS; ++i) r[i] = a[i] - b[i];
+    return r;
+}
+
+// SampleT_maj<ConcreteMedium>(ray, tMax, u, rng, lambda, callback) (media.h:737-800)
+template <typename F>
+static Spectrum SampleTmaj(const Media &M, int m, Vec o, Vec d, Float tMax, Float u, PCG32 &rng,
+                           const Wavelengths &lambda, F callback) {
+    tMax *= Length(d);
+    d = Normalize(d);
+    MajorantIter iter = SampleRay(M, m, o, d, tMax, lambda);
+    Spectrum T_maj(1.f);
+    MajorantSeg seg;
+    while (true) {
+        if (!iter.Next(&seg)) return T_maj;
+        if (seg.sigma_maj[0] == 0) {
+            Float dt = seg.tMax - seg.tMin;
+            if (std::isinf(dt)) dt = std::numeric_limits<Float>::max();
+            T_maj = T_maj * FastExpS(seg.sigma_maj * -dt);
+            continue;
+        }
+        Float tMin = seg.tMin;
+        while (true) {
+            Float t = tMin + (-std::log(1 - u) / seg.sigma_maj[0]);  // SampleExponential
+            u = rng.Uniform();
+            if (t < seg.tMax) {
+                T_maj = T_maj * FastExpS(seg.sigma_maj * -(t - tMin));
+                Vec p = o + d * t;
+                MediumProps mp = M.SamplePoint(m, p, lambda);
+                if (!callback(p, mp, seg.sigma_maj, T_maj)) return Spectrum(1.f);
+                T_maj = Spectrum(1.f);
+                tMin = t;
+            } else {
+                Float dt = seg.tMax - tMin;
+                if (std::isinf(dt)) dt = std::numeric_limits<Float>::max();
+                T_maj = T_maj * FastExpS(seg.sigma_maj * -dt);
+                break;
+            }
+        }
+    }
+}
+
+static int SampleDiscrete3(Float w0, Float w1, Float w2, Float u) {
+    const Float w[3] = {w0, w1, w2};
+    Float sum = 0;
+    for (Float x : w) sum += x;
+    Float up = u * sum;
+    if (up == sum) up = NextFloatDown(up);
+    int offset = 0;
+    Float acc = 0;
+    while (acc + w[offset] <= up) acc += w[offset++];
+    return offset;
+}
+
 // ---------------------------------------------------------------- integrator
 struct Renderer {
     Scene S;
     Lights lights;
+    Media M;
     const pbrt_scene_flat *f;
 
     Vec Xf(const float *m, Vec p, bool point) const {
@@ -1453,9 +1765,182 @@ struct Renderer {
         bool specularBounce = false, anyNonSpecular = false;
         Float etaScale = 1;
         Vec prevP, prevErr, prevN, prevNs;
-        for (int depth = 0;; ++depth) {
+        // WavefrontPathIntegrator::Render (integrator.cpp:374-432) for one path: iteration wf of
+        // the wavefront loop processes this path's ray of path depth `depth`.  Interface
+        // crossings continue in the next iteration at the same path depth; the loop ends at
+        // wf == maxDepth after emission (so a path may stop before depth reaches maxDepth).
+        const bool haveMedia = f->n_media > 0;
+        int medium = haveMedia ? f->camera_medium : -1;
+        int depth = 0;
+        auto mediaOf = [&](int prim, int rayMedium, int *in, int *out) {
+            *in = *out = rayMedium;
+            if (haveMedia && f->tri_medium && f->tri_medium[2 * prim] != f->tri_medium[2 * prim + 1]) {
+                *in = f->tri_medium[2 * prim];
+                *out = f->tri_medium[2 * prim + 1];
+            }
+        };
+        auto isInterface = [&](int prim) { return f->material_type[f->tri_material[prim]] == 3; };
+        // shadow rays: plain occlusion, or TraceTransmittance (wavefront/intersect.h:164-274)
+        // whenever the scene has media (interface surfaces are then transparent to them)
+        auto shadow = [&](Vec o, Vec d, int med, const Spectrum &Ld, const Spectrum &ru, const Spectrum &rl) {
+            TriIsect dummy;
+            if (!haveMedia) {
+                if (S.Intersect(o, d, 1 - ShadowEpsilon, &dummy, true) < 0) L = L + Ld / (ru + rl).Average();
+                return;
+            }
+            const Float tMax = 1 - ShadowEpsilon;
+            const Vec pLight = o + d * tMax;
+            PCG32 rng(HashFloats(o.x, o.y, o.z), HashFloats(d.x, d.y, d.z));
+            Spectrum T_ray(1.f), tu(1.f), tl(1.f);
+            while (d != Vec(0, 0, 0)) {
+                TriIsect ti;
+                int hp = S.Intersect(o, d, tMax, &ti, false);
+                if (hp >= 0 && !isInterface(hp)) {
+                    T_ray = Spectrum(0.f);
+                    break;
+                }
+                Interaction hsi;
+                if (hp >= 0)
+                    hsi = TriangleInteraction(S.P(hp, 0), S.P(hp, 1), S.P(hp, 2), f->tri_flip[hp], ti, d, S.Attr(hp));
+                if (med >= 0) {
+                    Float tEnd = hp < 0 ? tMax : (Length(o - hsi.p) / Length(d));
+                    Spectrum T_maj = SampleTmaj(M, med, o, d, tEnd, rng.Uniform(), rng, lambda,
+                                                [&](Vec, const MediumProps &mp, const Spectrum &sigma_maj, const Spectrum &Tm) {
+                        Spectrum sigma_n = ClampZero(sigma_maj - mp.sigma_a - mp.sigma_s);
+                        Float pr = Tm[0] * sigma_maj[0];
+                        T_ray = T_ray * (Tm * sigma_n / pr);
+                        tl = tl * (Tm * sigma_maj / pr);
+                        tu = tu * (Tm * sigma_n / pr);
+                        Spectrum Tr = T_ray / (tl + tu).Average();
+                        if (Tr.Max() < 0.05f) {
+                            Float q = 0.75f;
+                            if (rng.Uniform() < q) T_ray = Spectrum(0.f);
+                            else T_ray = T_ray / (1 - q);
+                        }
+                        return bool(T_ray);
+                    });
+                    T_ray = T_ray * (T_maj / T_maj[0]);
+                    tl = tl * (T_maj / T_maj[0]);
+                    tu = tu * (T_maj / T_maj[0]);
+                }
+                if (hp < 0 || !T_ray) break;
+                // SurfaceInteraction::SpawnRayTo(pLight) (interaction.h, ray.h:98-104)
+                int mi, mo;
+                mediaOf(hp, med, &mi, &mo);
+                Vec dd = pLight - hsi.p;
+                o = OffsetRayOrigin(hsi.p, hsi.err, hsi.n, dd);
+                d = pLight - hsi.p;
+                med = DotN(hsi.n, d) > 0 ? mo : mi;
+            }
+            if (T_ray) L = L + Ld * T_ray / (ru * tu + rl * tl).Average();
+        };
+        for (int wf = 0;; ++wf) {
             TriIsect ti;
             int prim = S.Intersect(ro, rd, Infinity, &ti, false);
+            Interaction si;
+            if (prim >= 0)
+                si = TriangleInteraction(S.P(prim, 0), S.P(prim, 1), S.P(prim, 2), f->tri_flip[prim], ti, rd, S.Attr(prim));
+            // GenerateRaySamples: dims 6 + 7 depth (path depth)
+            AnySampler h2{HaltonState{&S.halton, 0, 0}, ZSobolState{&S.zsobol}, S.useZSobol};
+            h2.Start(px, py, sampleIndex, 6 + 7 * depth);
+            Float dUc = h2.Get1D(), dU0, dU1;
+            h2.Get2D(&dU0, &dU1);
+            Float iUc = h2.Get1D(), iU0, iU1;
+            h2.Get2D(&iU0, &iU1);
+            Float rr = h2.Get1D();
+            if (haveMedia && medium >= 0) {
+                // SampleMediumInteraction (wavefront/media.cpp:22-247)
+                const Float tHit = prim >= 0 ? ti.t : Infinity;
+                PCG32 rng(HashFloats(ro.x, ro.y, ro.z, tHit), HashFloats(rd.x, rd.y, rd.z));
+                Float uDist = rng.Uniform(), uMode = rng.Uniform();
+                bool scattered = false, pushScatter = false;
+                Vec pS;
+                Spectrum Lm(0.f);
+                Spectrum T_maj = SampleTmaj(M, medium, ro, rd, tHit, uDist, rng, lambda,
+                                            [&](Vec p, const MediumProps &mp, const Spectrum &sigma_maj, const Spectrum &Tm) {
+                    if (depth < S.maxDepth && mp.Le) {
+                        Float pr = sigma_maj[0] * Tm[0];
+                        Spectrum r_e = r_u * sigma_maj * Tm / pr;
+                        if (r_e) Lm = Lm + beta * mp.sigma_a * Tm * mp.Le / (pr * r_e.Average());
+                    }
+                    Float pAbsorb = mp.sigma_a[0] / sigma_maj[0], pScatter = mp.sigma_s[0] / sigma_maj[0];
+                    Float pNull = std::max<Float>(0, 1 - pAbsorb - pScatter);
+                    int mode = SampleDiscrete3(pAbsorb, pScatter, pNull, uMode);
+                    if (mode == 0) {
+                        beta = Spectrum(0.f);
+                        return false;
+                    }
+                    if (mode == 1) {
+                        Float pr = Tm[0] * mp.sigma_s[0];
+                        beta = beta * (Tm * mp.sigma_s / pr);
+                        r_u = r_u * (Tm * mp.sigma_s / pr);
+                        pushScatter = bool(beta) && bool(r_u);
+                        pS = p;
+                        scattered = true;
+                        return false;
+                    }
+                    Spectrum sigma_n = ClampZero(sigma_maj - mp.sigma_a - mp.sigma_s);
+                    Float pr = Tm[0] * sigma_n[0];
+                    beta = beta * (Tm * sigma_n / pr);
+                    if (pr == 0) beta = Spectrum(0.f);
+                    r_u = r_u * (Tm * sigma_n / pr);
+                    r_l = r_l * (Tm * sigma_maj / pr);
+                    uMode = rng.Uniform();
+                    return bool(beta) && bool(r_u);
+                });
+                if (!scattered && beta) {
+                    beta = beta * (T_maj / T_maj[0]);
+                    r_u = r_u * (T_maj / T_maj[0]);
+                    r_l = r_l * (T_maj / T_maj[0]);
+                }
+                L = L + Lm;
+                if (scattered) {
+                    if (!pushScatter || wf == S.maxDepth) break;
+                    // SampleMediumScattering<HGPhaseFunction> (wavefront/media.cpp:259-352)
+                    const Float g = M.Params(medium)[0];
+                    const Vec wo = -rd;
+                    int li;
+                    Float lpmf;
+                    if (lights.Sample(pS, Vec(0, 0, 0), dUc, &li, &lpmf) && li < f->n_area_lights) {
+                        int lp = f->light_prim[li];
+                        ShapeSample ss;
+                        if (TriangleSample(S.P(lp, 0), S.P(lp, 1), S.P(lp, 2), f->tri_flip[lp], pS, Vec(0, 0, 0), dU0,
+                                           dU1, &ss, S.Attr(lp)) &&
+                            ss.pdf != 0 && LengthSquared(ss.p - pS) != 0) {
+                            Vec wi = Normalize(ss.p - pS);
+                            Spectrum Le(0.f);
+                            if (f->light_two_sided[li] || DotN(ss.n, -wi) >= 0) Le = LightL(li, lambda);
+                            if (Le) {
+                                Float ph = HenyeyGreenstein(Dot(wo, wi), g);
+                                Spectrum b2 = beta * ph;
+                                Float lightPDF = ss.pdf * lpmf;
+                                Spectrum ru = r_u * ph, rl = r_u * lightPDF;
+                                shadow(pS, ss.p - pS, medium, b2 * Le, ru, rl);
+                            }
+                        }
+                    }
+                    Float pdf;
+                    Vec wi = SampleHG(wo, g, iU0, iU1, &pdf);
+                    if (pdf == 0) break;
+                    beta = beta * pdf / pdf;
+                    r_l = r_u / pdf;
+                    Spectrum rrBeta = beta * etaScale / r_u.Average();
+                    if (rrBeta.Max() < 1 && depth >= 1) {
+                        Float q = std::max<Float>(0, 1 - rrBeta.Max());
+                        if (rr < q) break;
+                        beta = beta / (1 - q);
+                    }
+                    ro = pS;
+                    rd = wi;
+                    ++depth;
+                    specularBounce = false;
+                    anyNonSpecular = true;
+                    prevP = pS;
+                    prevErr = prevN = prevNs = Vec(0, 0, 0);
+                    continue;
+                }
+                if (!beta || !r_u || depth == S.maxDepth) break;
+            }
             if (prim < 0) {
                 // HandleEscapedRays: uniform infinite lights, PDF_Li(allowIncomplete)=0
                 for (int k = 0; k < f->n_infinite_lights; ++k) {
@@ -1469,9 +1954,15 @@ struct Renderer {
                 }
                 break;
             }
-            bool flip = f->tri_flip[prim];
-            Vec p0 = S.P(prim, 0), p1 = S.P(prim, 1), p2 = S.P(prim, 2);
-            Interaction si = TriangleInteraction(p0, p1, p2, flip, ti, rd, S.Attr(prim));
+            int mIn, mOut;
+            mediaOf(prim, medium, &mIn, &mOut);
+            if (isInterface(prim)) {
+                // Material "interface": SpawnRay(ray.d) into the next wavefront iteration, same depth
+                if (wf == S.maxDepth) break;
+                ro = OffsetRayOrigin(si.p, si.err, si.n, rd);
+                medium = DotN(si.n, rd) > 0 ? mOut : mIn;
+                continue;
+            }
             // HandleEmissiveIntersection
             int light = f->tri_light[prim];
             if (light >= 0 && (f->light_two_sided[light] || DotN(si.n, si.wo) >= 0)) {
@@ -1488,15 +1979,7 @@ struct Renderer {
                     }
                 }
             }
-            if (depth == S.maxDepth) break;
-            // GenerateRaySamples: dims 6 + 7 depth
-            AnySampler h2{HaltonState{&S.halton, 0, 0}, ZSobolState{&S.zsobol}, S.useZSobol};
-            h2.Start(px, py, sampleIndex, 6 + 7 * depth);
-            Float dUc = h2.Get1D(), dU0, dU1;
-            h2.Get2D(&dU0, &dU1);
-            Float iUc = h2.Get1D(), iU0, iU1;
-            h2.Get2D(&iU0, &iU1);
-            Float rr = h2.Get1D();
+            if (wf == S.maxDepth) break;
             // Material::GetBxDF (materials.h:466-471 diffuse, :182-204 dielectric, :491-511 conductor)
             int mat = f->tri_material[prim];
             const float *mc = f->material_coeffs + 4 * mat;
@@ -1586,11 +2069,10 @@ struct Renderer {
                                 Float bsdfPDF = woL.z != 0 ? bx.PDF(woL, wiL) : 0;
                                 Spectrum ru = r_u * bsdfPDF, rl = r_u * lightPDF;
                                 Spectrum Ld = b2 * Le;
+                                // SpawnRayTo(pi, n, time, pLight.pi, pLight.n) (ray.h:106-111)
                                 Vec pf = OffsetRayOrigin(si.p, si.err, si.n, ss.p - si.p);
                                 Vec pt = OffsetRayOrigin(ss.p, ss.err, ss.n, pf - ss.p);
-                                TriIsect dummy;
-                                if (S.Intersect(pf, pt - pf, 1 - ShadowEpsilon, &dummy, true) < 0)
-                                    L = L + Ld / (ru + rl).Average();
+                                shadow(pf, pt - pf, DotN(si.n, pt - pf) > 0 ? mOut : mIn, Ld, ru, rl);
                             }
                         }
                     }
@@ -1606,8 +2088,10 @@ struct Renderer {
             prevErr = si.err;
             prevN = si.n;
             prevNs = si.ns;
+            medium = DotN(si.n, nextD) > 0 ? mOut : mIn;
             ro = nextO;
             rd = nextD;
+            ++depth;
         }
         // PixelSensor::ToSensorRGB (cie1931): L / pdf, averaged against X/Y/Z bars
         Spectrum Lp;
@@ -1635,6 +2119,8 @@ int oracle_render(const pbrt_scene_flat *flat, const pbrt_scene_info *info, cons
     r.S.Init(flat, info);
     r.lights.Init(flat);
     r.lights.uniformFlag = uniformLightSampler != 0;
+    r.M.f = flat;
+    r.M.n = flat->n_media;
     size_t npix = (size_t)info->xres * info->yres;
     std::atomic<int> next(0);
     auto work = [&]() {

@@ -43,10 +43,36 @@ static int Fail(const std::string &msg) {
         if (e_ != hipSuccess) throw Error(std::string("HIP error ") + hipGetErrorString(e_) + " at " #x); \
     } while (0)
 
+// Media as flat tables (pbrt_scene_flat::medium_*; the device upload uses the same layout)
+static void MediumTables(const SceneDesc &s, std::vector<int32_t> *info, std::vector<float> *params,
+                         std::vector<float> *values) {
+    info->clear();
+    params->clear();
+    values->clear();
+    for (const MediumDesc &m : s.media) {
+        const int dOff = (int)values->size();
+        values->insert(values->end(), m.density.begin(), m.density.end());
+        const int lOff = (int)values->size();
+        values->insert(values->end(), m.LeScale.begin(), m.LeScale.end());
+        const int mOff = (int)values->size();
+        values->insert(values->end(), m.majorant.begin(), m.majorant.end());
+        info->insert(info->end(), {m.type, m.sigmaA, m.sigmaS, m.Le, m.emissive ? 1 : 0, m.nx, m.ny, m.nz, m.lnx, m.lny,
+                                   m.lnz, dOff, lOff, mOff, 0, 0});
+        const V3 lo(std::min(m.p0.x, m.p1.x), std::min(m.p0.y, m.p1.y), std::min(m.p0.z, m.p1.z));
+        const V3 hi(std::max(m.p0.x, m.p1.x), std::max(m.p0.y, m.p1.y), std::max(m.p0.z, m.p1.z));
+        params->insert(params->end(), {m.g, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, 0.f});
+        Mat4 inv = m.type == kMediumGrid ? Inverse4(m.renderFromMedium) : Identity4();
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j) params->push_back((float)inv[i][j]);
+    }
+}
+
 struct pbrt_scene {
     SceneDesc desc;
     // flattened copies for pbrt_scene_get_flat
-    std::vector<float> verts, matCoeffs, lightScale, infScale, dense, sensor, nodeBounds, matParams, plLambda, plValue;
+    std::vector<float> verts, matCoeffs, lightScale, infScale, dense, sensor, nodeBounds, matParams, plLambda, plValue,
+        mediumParams, mediumValues;
+    std::vector<int32_t> mediumInfo;
     std::vector<int32_t> tris, lightPrim, lightSpectrum, lightTwoSided, infSpectrum, matConstant, nodeInfo, matType,
         matSpectra, plOffsets;
     void Flatten() {
@@ -71,6 +97,7 @@ struct pbrt_scene {
             matParams.insert(matParams.end(), {m.alphaX, m.alphaY, m.eta, 0.f});
             matSpectra.insert(matSpectra.end(), {m.etaSpec, m.kSpec});
         }
+        MediumTables(s, &mediumInfo, &mediumParams, &mediumValues);
         plOffsets.assign(1, 0);
         plLambda.clear();
         plValue.clear();
@@ -778,6 +805,12 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
     f->vertex_normals = s.vertN.empty() ? nullptr : &s.vertN[0].x;
     f->vertex_uv = s.vertUV.empty() ? nullptr : s.vertUV[0].data();
     f->tri_shading = s.triShade.data();
+    f->n_media = (int)s.media.size();
+    f->camera_medium = s.cameraMedium;
+    f->medium_info = scene->mediumInfo.data();
+    f->medium_params = scene->mediumParams.data();
+    f->medium_values = scene->mediumValues.data();
+    f->tri_medium = s.triMedium.empty() ? nullptr : s.triMedium[0].data();
     return 0;
 }
 

@@ -280,6 +280,7 @@ struct GraphicsState {
     int material = -1;  // index into materials (-1 -> default diffuse)
     std::string areaLightName;
     ParamSet areaLightParams;
+    std::string insideMedium, outsideMedium;  // MediumInterface ("" = vacuum)
 };
 
 class Parser {
@@ -320,6 +321,7 @@ class Parser {
         std::vector<int> idx;
         std::vector<float> uv;  // per vertex, 2 floats
         std::vector<V3> N;      // per vertex (object space)
+        std::string insideMedium, outsideMedium;
         Mat4 renderFromObject;
         bool flip;
         int material;
@@ -334,6 +336,13 @@ class Parser {
         Mat4 worldFromLight;
     };
     std::vector<PendingLight> lights;
+    struct PendingMedium {
+        std::string name, type;
+        ParamSet params;
+        Mat4 worldFromMedium;
+    };
+    std::vector<PendingMedium> pendingMedia;
+    std::string cameraMediumName;
 
     static std::string Loc(const Token &t) { return t.file + ":" + std::to_string(t.line); }
 
@@ -439,6 +448,7 @@ class Parser {
             cameraFromWorld = gs.ctm;
             namedCoordSys["camera"] = Inverse4(gs.ctm);
             haveCamera = true;
+            cameraMediumName = gs.outsideMedium;  // CameraSceneEntity's medium
         } else if (d == "Film") {
             filmType = Str(toks, pos);
             filmParams = Params(toks, pos);
@@ -520,7 +530,24 @@ class Parser {
             std::string f = Str(toks, pos);
             std::string path = (f.size() && f[0] == '/') ? f : (dir.empty() ? f : dir + "/" + f);
             ParseFile(path);
-        } else if (d == "Texture" || d == "MakeNamedMedium" || d == "MediumInterface" || d == "ObjectBegin" ||
+        } else if (d == "MakeNamedMedium") {
+            PendingMedium m;
+            m.name = Str(toks, pos);
+            m.params = Params(toks, pos);
+            m.params.loc = loc;
+            m.type = m.params.GetString("type", "");
+            if (m.type.empty()) throw Error(loc + ": MakeNamedMedium needs \"string type\"");
+            m.worldFromMedium = gs.ctm;
+            for (auto &o : pendingMedia)
+                if (o.name == m.name) throw Error(loc + ": medium \"" + m.name + "\" redefined");
+            pendingMedia.push_back(std::move(m));
+        } else if (d == "MediumInterface") {
+            // one name: inside = outside; two: inside, outside (parser.cpp MediumInterface)
+            std::string a = Str(toks, pos), b = a;
+            if (pos < toks.size() && toks[pos].isString) b = Str(toks, pos);
+            gs.insideMedium = a;
+            gs.outsideMedium = b;
+        } else if (d == "Texture" || d == "ObjectBegin" ||
                    d == "ObjectEnd" || d == "ObjectInstance" || d == "ActiveTransform" || d == "TransformTimes") {
             throw Error(loc + ": directive " + d + " is not supported by the wavefront hot path yet");
         } else {
@@ -552,6 +579,9 @@ class Parser {
             } else {
                 throw Error(ps.loc + ": reflectance of type " + r->type + " not supported");
             }
+        } else if (type == "interface") {
+            // a null material: the surface only bounds media (scene.cpp: "interface")
+            m.type = kMatInterface;
         } else if (type == "dielectric") {
             // DielectricMaterial::Create (materials.cpp:51-74)
             m.type = kMatDielectric;
@@ -703,6 +733,8 @@ class Parser {
         s.material = gs.material;
         s.areaLight = gs.areaLightName;
         s.areaParams = gs.areaLightParams;
+        s.insideMedium = gs.insideMedium;
+        s.outsideMedium = gs.outsideMedium;
         s.loc = ps.loc;
         shapes.push_back(std::move(s));
     }
@@ -742,6 +774,67 @@ static float PhotometricOf(const std::array<float, 311> &dense) {
     for (float lambda = kLambdaMin; lambda <= kLambdaMax; ++lambda)
         y += d.denseY[DenseOffset(lambda)] * dense[DenseOffset(lambda)];
     return y;
+}
+
+// A spectrum parameter as a DenselySampledSpectrum (395..705 nm), scaled.  Unbounded: rgb ->
+// RGBUnboundedSpectrum; Illuminant: rgb -> RGBIlluminantSpectrum; either: "spectrum" as
+// inline lambda/value pairs (PiecewiseLinearSpectrum).  *photometric gets SpectrumToPhotometric
+// of the unscaled spectrum (illuminant part for rgb, util/spectrum.cpp:37-51).
+// GridMedium's MajorantGrid (media.h:124-160, media.cpp:239-246): per 16^3 voxel of the
+// medium's [0,1]^3, SampledGrid::MaxValue of the density (util/containers.h:838-854)
+static void BuildMajorantGrid(MediumDesc &m) {
+    const int R = 16;
+    m.majorant.assign(R * R * R, 0.f);
+    auto lookup = [&](int x, int y, int z) -> float {
+        if (x < 0 || x >= m.nx || y < 0 || y >= m.ny || z < 0 || z >= m.nz) return 0.f;
+        return m.density[((size_t)z * m.ny + y) * m.nx + x];
+    };
+    for (int z = 0; z < R; ++z)
+        for (int y = 0; y < R; ++y)
+            for (int x = 0; x < R; ++x) {
+                const float b0[3] = {float(x) / R, float(y) / R, float(z) / R};
+                const float b1[3] = {float(x + 1) / R, float(y + 1) / R, float(z + 1) / R};
+                const int n[3] = {m.nx, m.ny, m.nz};
+                int lo[3], hi[3];
+                for (int a = 0; a < 3; ++a) {
+                    lo[a] = std::max((int)std::floor(b0[a] * n[a] - .5f), 0);
+                    hi[a] = std::min((int)std::floor(b1[a] * n[a] - .5f) + 1, n[a] - 1);
+                }
+                float v = lookup(lo[0], lo[1], lo[2]);
+                for (int zz = lo[2]; zz <= hi[2]; ++zz)
+                    for (int yy = lo[1]; yy <= hi[1]; ++yy)
+                        for (int xx = lo[0]; xx <= hi[0]; ++xx) v = std::max(v, lookup(xx, yy, zz));
+                m.majorant[x + R * (y + R * z)] = v;
+            }
+}
+
+static std::array<float, 311> MediumSpectrum(ParamSet &ps, const char *name, bool illuminant, float defaultValue,
+                                             bool *given, float *photometric) {
+    Param *p = ps.Find(name);
+    std::array<float, 311> d;
+    *given = p != nullptr;
+    if (photometric) *photometric = 1;
+    if (!p) {
+        d.fill(defaultValue);
+        return d;
+    }
+    if (p->type == "rgb" && p->nums.size() == 3) {
+        float r = (float)p->nums[0], g = (float)p->nums[1], b = (float)p->nums[2];
+        if (r < 0 || g < 0 || b < 0) throw Error(ps.loc + ": RGB parameter \"" + std::string(name) + "\" has negative component.");
+        if (illuminant) {
+            d = DenseRGBIlluminant(r, g, b);
+            if (photometric) *photometric = GetSpectralData().photometricD65;
+        } else {
+            d = DenseRGBUnbounded(r, g, b);
+        }
+        return d;
+    }
+    if (p->type == "spectrum" && !p->nums.empty()) {
+        d = DensePiecewiseLinear(p->nums, ps.loc);
+        if (photometric) *photometric = PhotometricOf(d);
+        return d;
+    }
+    throw Error(ps.loc + ": \"" + p->type + " " + name + "\" is not supported for media yet (use rgb or spectrum)");
 }
 
 void Parser::Finish() {
@@ -879,6 +972,81 @@ void Parser::Finish() {
         for (int i = 0; i < 3; ++i)
             for (int j = 0; j < 3; ++j) scene.outputRGBFromSensorRGB[i][j] = sd.rgbFromXYZ[i][j];
     }
+    // ---- media (MakeNamedMedium -> HomogeneousMedium / GridMedium, media.cpp:167-330)
+    std::map<std::string, int> mediumIndex;
+    for (PendingMedium &pm : pendingMedia) {
+        ParamSet &ps = pm.params;
+        MediumDesc m;
+        m.name = pm.name;
+        if (ps.Find("preset")) throw Error(ps.loc + ": medium \"preset\" is not supported yet");
+        bool given;
+        float scale = (float)ps.GetFloat("scale", 1);
+        auto addDense = [&](std::array<float, 311> d, float k) {
+            for (float &v : d) v *= k;  // DenselySampledSpectrum::Scale
+            scene.denseSpectra.push_back(d);
+            return (int)scene.denseSpectra.size() - 1;
+        };
+        m.sigmaA = addDense(MediumSpectrum(ps, "sigma_a", false, 1.f, &given, nullptr), scale);
+        m.sigmaS = addDense(MediumSpectrum(ps, "sigma_s", false, 1.f, &given, nullptr), scale);
+        m.g = (float)ps.GetFloat("g", 0);
+        float photometric = 1;
+        std::array<float, 311> Le = MediumSpectrum(ps, "Le", true, 0.f, &given, &photometric);
+        const bool LeZero = !given || *std::max_element(Le.begin(), Le.end()) == 0;
+        if (LeZero) Le.fill(0.f);
+        if (pm.type == "homogeneous") {
+            m.type = kMediumHomogeneous;
+            float LeScale = (float)ps.GetFloat("Lescale", 1);
+            if (!LeZero) LeScale /= photometric;
+            m.Le = addDense(Le, LeScale);
+            const auto &LeD = scene.denseSpectra[m.Le];
+            m.emissive = *std::max_element(LeD.begin(), LeD.end()) > 0;  // IsEmissive
+        } else if (pm.type == "uniformgrid") {
+            m.type = kMediumGrid;
+            if (ps.Find("temperature") || ps.Find("temperaturescale") || ps.Find("temperatureoffset") ||
+                ps.Find("temperaturecutoff"))
+                throw Error(ps.loc + ": grid medium \"temperature\" is not supported yet");
+            Param *dens = ps.Find("density", "float");
+            if (!dens || dens->nums.empty()) throw Error(ps.loc + ": No \"density\" value provided for grid medium.");
+            m.nx = ps.GetInt("nx", 1);
+            m.ny = ps.GetInt("ny", 1);
+            m.nz = ps.GetInt("nz", 1);
+            if ((long)dens->nums.size() != (long)m.nx * m.ny * m.nz)
+                throw Error(ps.loc + ": Grid medium has " + std::to_string(dens->nums.size()) +
+                            " density values; expected nx*ny*nz = " + std::to_string(m.nx * m.ny * m.nz));
+            for (double v : dens->nums) m.density.push_back((float)v);
+            const float LeNorm = LeZero ? 1.f : 1 / photometric;
+            Param *ls = ps.Find("Lescale", "float");
+            if (!ls) {
+                m.LeScale = {LeNorm};
+            } else {
+                if ((long)ls->nums.size() != (long)m.nx * m.ny * m.nz)
+                    throw Error(ps.loc + ": \"Lescale\" needs nx*ny*nz values");
+                for (double v : ls->nums) m.LeScale.push_back((float)v * LeNorm);
+                m.lnx = m.nx, m.lny = m.ny, m.lnz = m.nz;
+            }
+            m.Le = addDense(Le, 1.f);
+            m.emissive = !LeZero;
+            Param *p0 = ps.Find("p0", "point3"), *p1 = ps.Find("p1", "point3");
+            if (p0) m.p0 = V3((float)p0->nums[0], (float)p0->nums[1], (float)p0->nums[2]);
+            if (p1) m.p1 = V3((float)p1->nums[0], (float)p1->nums[1], (float)p1->nums[2]);
+            m.renderFromMedium = Mul(scene.camera.renderFromWorld, pm.worldFromMedium);
+            BuildMajorantGrid(m);
+        } else {
+            throw Error(ps.loc + ": medium type \"" + pm.type + "\" is not supported yet");
+        }
+        ps.Find("type");
+        ps.CheckUnused();
+        mediumIndex[pm.name] = (int)scene.media.size();
+        scene.media.push_back(std::move(m));
+    }
+    auto mediumOf = [&](const std::string &n, const std::string &loc) -> int {
+        if (n.empty()) return -1;
+        auto it = mediumIndex.find(n);
+        if (it == mediumIndex.end()) throw Error(loc + ": named medium \"" + n + "\" undefined");
+        return it->second;
+    };
+    scene.cameraMedium = mediumOf(cameraMediumName, "Camera");
+
     // ---- shapes -> render-space triangles; area lights in shape order
     const Mat4 &renderFromWorld = scene.camera.renderFromWorld;
     std::map<std::string, int> spectrumCache;
@@ -969,6 +1137,8 @@ void Parser::Finish() {
             scene.triMaterial.push_back(s.material < 0 ? mat : s.material);
             scene.triFlip.push_back(flip ? 1 : 0);
             scene.triShade.push_back(shadeBits);
+            if (!scene.media.empty())
+                scene.triMedium.push_back({(int16_t)mediumOf(s.insideMedium, s.loc), (int16_t)mediumOf(s.outsideMedium, s.loc)});
             if (lightSpectrum >= 0) {
                 AreaLightDesc l;
                 l.prim = triIndex;

@@ -30,6 +30,28 @@ V3 XformNormal(const Mat4 &mInv, V3 n);  // uses the inverse transpose
 bool SwapsHandedness(const Mat4 &m);
 
 enum MaterialType : int { kMatDiffuse = 0, kMatDielectric = 1, kMatConductor = 2, kMatNumTypes = 3 };
+// Material "interface" (a null material: medium boundary only, materials.cpp); not a BxDF type
+constexpr int kMatInterface = 3;
+
+// Participating media (media.h:209-350, media.cpp:167-330).  Spectra are DenselySampled
+// 395..705 nm tables in SceneDesc::denseSpectra with pbrt's constructor scaling applied
+// (sigma_a/sigma_s *= "scale"; homogeneous Le *= "Lescale" / photometric).
+enum MediumType : int { kMediumHomogeneous = 0, kMediumGrid = 1 };
+struct MediumDesc {
+    int type = kMediumHomogeneous;
+    std::string name;
+    int sigmaA = -1, sigmaS = -1, Le = -1;  // denseSpectra indices
+    float g = 0;
+    bool emissive = false;
+    // GridMedium ("uniformgrid")
+    Mat4 renderFromMedium;                 // inverse applied to rays and points
+    V3 p0{0, 0, 0}, p1{1, 1, 1};           // medium-space bounds
+    int nx = 1, ny = 1, nz = 1;
+    std::vector<float> density;            // [nz][ny][nx]
+    int lnx = 1, lny = 1, lnz = 1;         // LeScale grid (1x1x1 = {1 / photometric(Le)})
+    std::vector<float> LeScale;
+    std::vector<float> majorant;           // 16^3 MaxValue of density per majorant voxel
+};
 
 struct MaterialDesc {
     int type = kMatDiffuse;
@@ -107,6 +129,11 @@ struct SceneDesc {
     std::vector<uint8_t> triShade;
 
     std::vector<MaterialDesc> materials;
+    std::vector<MediumDesc> media;
+    int cameraMedium = -1;                          // -1: vacuum
+    std::vector<std::array<int16_t, 2>> triMedium;  // {inside, outside}; empty if no media
+                                                    // a triangle changes the ray's medium
+                                                    // only when inside != outside
     std::vector<AreaLightDesc> areaLights;
     std::vector<InfiniteLightDesc> infiniteLights;
     std::vector<std::array<float, 311>> denseSpectra;
@@ -159,6 +186,7 @@ std::array<float, 3> RGBToSigmoidCoeffs(float r, float g, float b);
 std::vector<float> RGB2SpecColumn(int maxc, int j, int i);
 float RGB2SpecZNode(int k);
 std::array<float, 311> DenseRGBIlluminant(float r, float g, float b);
+std::array<float, 311> DenseRGBUnbounded(float r, float g, float b);
 // GetNamedSpectrum(name) for the metal / glass tables: PiecewiseLinearSpectrum::FromInterleaved
 // (samples, normalize = false), extended to Lambda_min - 1 / Lambda_max + 1 (spectrum.cpp:133-163)
 PLSpectrumDesc NamedPiecewiseLinear(const std::string &name);

@@ -437,6 +437,17 @@ std::array<float, 311> DenseRGBIlluminant(float r, float g, float b) {
     return out;
 }
 
+std::array<float, 311> DenseRGBUnbounded(float r, float g, float b) {
+    // DenselySampledSpectrum(RGBUnboundedSpectrum(sRGB, rgb)) (util/spectrum.cpp:230-244)
+    float m = std::max({r, g, b});
+    float scale = 2 * m;
+    std::array<float, 3> c = scale ? RGBToSigmoidCoeffs(r / scale, g / scale, b / scale)
+                                   : RGBToSigmoidCoeffs(0, 0, 0);
+    std::array<float, 311> out;
+    for (int l = 395; l <= 705; ++l) out[l - 395] = scale * SigmoidPolynomial(c[0], c[1], c[2], (float)l);
+    return out;
+}
+
 }  // namespace pbrt_amd
 
 namespace pbrt_amd {

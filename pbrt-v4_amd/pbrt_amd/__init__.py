@@ -70,6 +70,9 @@ class SceneFlat(ctypes.Structure):
         ("pl_value", ctypes.POINTER(ctypes.c_float)), ("regularize", ctypes.c_int),
         ("vertex_normals", ctypes.POINTER(ctypes.c_float)), ("vertex_uv", ctypes.POINTER(ctypes.c_float)),
         ("tri_shading", ctypes.POINTER(ctypes.c_uint8)),
+        ("n_media", ctypes.c_int), ("camera_medium", ctypes.c_int),
+        ("medium_info", ctypes.POINTER(ctypes.c_int32)), ("medium_params", ctypes.POINTER(ctypes.c_float)),
+        ("medium_values", ctypes.POINTER(ctypes.c_float)), ("tri_medium", ctypes.POINTER(ctypes.c_int16)),
     ]
 
 

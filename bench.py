@@ -42,7 +42,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--workload", choices=["c2", "c3", "c4"], default="c2")
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--xres", type=int, default=None)
@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     a = ap.parse_args()
-    d = {"c2": (1280, 720, 64), "c3": (1920, 1080, 256), "c4": (1920, 1080, 128)}[a.workload]
+    d = {"c2": (1280, 720, 64), "c3": (1920, 1080, 256), "c4": (1920, 1080, 128), "c5": (1280, 720, 1024)}[a.workload]
     a.xres = a.xres or d[0]
     a.yres = a.yres or d[1]
     a.spp = a.spp or d[2]
@@ -73,6 +73,10 @@ def load(args):
             import shutil
             shutil.rmtree(out, ignore_errors=True)
         return scene
+    if args.workload == "c5":
+        sys.path.insert(0, str(ROOT / "scenes"))
+        import gen_c5
+        return pa.Scene.from_string(gen_c5.scene_text(args.xres, args.yres, args.spp, grid=256), ROOT / "scenes")
     if args.workload == "c3":
         sys.path.insert(0, str(ROOT / "scenes"))
         import gen_c3
@@ -199,6 +203,10 @@ def main():
                                     f"C3 killeroo stand-in (scenes/gen_c3.py) {args.xres}x{args.yres} {info.spp}spp "
                                     f"maxdepth {info.max_depth} zsobol, dielectric + conductor + diffuse "
                                     "(BASELINE configs[2])" if args.workload == "c3" else
+                                    f"C5 cloud stand-in (scenes/gen_c5.py: 256^3 fBm uniformgrid medium, sigma_a 0.5, "
+                                    f"sigma_s 5, g 0.3, in an interface box) {args.xres}x{args.yres} {info.spp}spp "
+                                    f"maxdepth {info.max_depth} zsobol, volpath null scattering (BASELINE configs[4])"
+                                    if args.workload == "c5" else
                                     f"C4 San-Miguel stand-in (scenes/gen_c4.py, PLY) {args.xres}x{args.yres} "
                                     f"{info.spp}spp maxdepth {info.max_depth} zsobol, diffuse + conductor, "
                                     "untextured (BASELINE configs[3] geometry)"),

@@ -51,8 +51,24 @@ static inline Float Sqr(Float x) { return x * x; }
 static inline Float Clamp(Float v, Float lo, Float hi) { return v < lo ? lo : (v > hi ? hi : v); }
 static inline Float Lerp(Float t, Float a, Float b) { return (1 - t) * a + t * b; }
 static inline Float SafeSqrt(Float x) { return std::sqrt(std::max<Float>(0.f, x)); }
-static inline Float SafeASin(Float x) { return std::asin(Clamp(x, -1, 1)); }
-static inline Float SafeACos(Float x) { return std::acos(Clamp(x, -1, 1)); }
+// Transcendentals.  Default: libm's float functions, as the reference CPU build calls them.
+// CR mode (oracle_set_cr_math(1)): the correctly rounded float (double evaluation, one rounding),
+// which is what the device media kernels compute (core.h PBRT_AMD_CR_MATH).  A medium path's
+// RNG is seeded from the bits of its ray (wavefront/media.cpp:44), so per-sample parity of the
+// device media path needs bit-identical transcendentals; the two modes differ in the last ulp.
+static int g_crMath = 0;
+static inline Float CRSin(Float x) { return g_crMath ? (Float)std::sin((double)x) : std::sin(x); }
+static inline Float CRCos(Float x) { return g_crMath ? (Float)std::cos((double)x) : std::cos(x); }
+static inline Float CRLog(Float x) { return g_crMath ? (Float)std::log((double)x) : std::log(x); }
+static inline Float CRATan2(Float y, Float x) {
+    return g_crMath ? (Float)std::atan2((double)y, (double)x) : std::atan2(y, x);
+}
+static inline Float SafeASin(Float x) {
+    return g_crMath ? (Float)std::asin((double)Clamp(x, -1, 1)) : std::asin(Clamp(x, -1, 1));
+}
+static inline Float SafeACos(Float x) {
+    return g_crMath ? (Float)std::acos((double)Clamp(x, -1, 1)) : std::acos(Clamp(x, -1, 1));
+}
 static inline Float DifferenceOfProducts(Float a, Float b, Float c, Float d) {
     Float cd = c * d;
     return std::fma(a, b, -cd) + std::fma(-c, d, cd);
@@ -799,8 +815,8 @@ static void SampleUniformDiskConcentric(Float u0, Float u1, Float *x, Float *y) 
     Float theta, r;
     if (std::abs(ox) > std::abs(oy)) { r = ox; theta = PiOver4 * (oy / ox); }
     else { r = oy; theta = PiOver2 - PiOver4 * (ox / oy); }
-    *x = r * std::cos(theta);
-    *y = r * std::sin(theta);
+    *x = r * CRCos(theta);
+    *y = r * CRSin(theta);
 }
 static Vec SampleCosineHemisphere(Float u0, Float u1) {
     Float x, y;
@@ -828,7 +844,7 @@ static void SampleUniformTriangle(Float u0, Float u1, Float b[3]) {
     b[2] = 1 - b[0] - b[1];
 }
 static Float SphericalTriangleArea(Vec a, Vec b, Vec c) {
-    return std::abs(2 * std::atan2(Dot(a, Cross(b, c)), 1 + Dot(a, b) + Dot(a, c) + Dot(b, c)));
+    return std::abs(2 * CRATan2(Dot(a, Cross(b, c)), 1 + Dot(a, b) + Dot(a, c) + Dot(b, c)));
 }
 static bool SampleSphericalTriangle(Vec v0, Vec v1, Vec v2, Vec p, Float u0, Float u1, Float bary[3], Float *pdf) {
     *pdf = 0;
@@ -844,9 +860,9 @@ static bool SampleSphericalTriangle(Vec v0, Vec v1, Vec v2, Vec p, Float u0, Flo
     Float Ap_pi = Lerp(u0, Pi, A_pi);
     Float A = A_pi - Pi;
     *pdf = (A <= 0) ? 0 : 1 / A;
-    Float cosAlpha = std::cos(alpha), sinAlpha = std::sin(alpha);
-    Float sinPhi = std::sin(Ap_pi) * cosAlpha - std::cos(Ap_pi) * sinAlpha;
-    Float cosPhi = std::cos(Ap_pi) * cosAlpha + std::sin(Ap_pi) * sinAlpha;
+    Float cosAlpha = CRCos(alpha), sinAlpha = CRSin(alpha);
+    Float sinPhi = CRSin(Ap_pi) * cosAlpha - CRCos(Ap_pi) * sinAlpha;
+    Float cosPhi = CRCos(Ap_pi) * cosAlpha + CRSin(Ap_pi) * sinAlpha;
     Float k1 = cosPhi + cosAlpha, k2 = sinPhi - sinAlpha * Dot(a, b);
     Float cosBp = (k2 + (DifferenceOfProducts(k2, cosPhi, k1, sinPhi)) * cosAlpha) /
                   ((SumOfProducts(k2, sinPhi, k1, cosPhi)) * sinAlpha);
@@ -1161,7 +1177,7 @@ struct TRDistribution {
         Vec T1 = (wh.z < 0.99999f) ? Normalize(Cross(Vec(0, 0, 1), wh)) : Vec(1, 0, 0);
         Vec T2 = Cross(wh, T1);
         Float r = std::sqrt(u0), th = 2 * Pi * u1;  // SampleUniformDiskPolar
-        Float px = r * std::cos(th), py = r * std::sin(th);
+        Float px = r * CRCos(th), py = r * CRSin(th);
         Float h = std::sqrt(1 - Sqr(px));
         py = Lerp((1 + wh.z) / 2, h, py);
         Float pz = std::sqrt(std::max<Float>(0, 1 - (Sqr(px) + Sqr(py))));
@@ -1448,7 +1464,7 @@ static Vec SampleHG(Vec wo, Float g, Float u0, Float u1, Float *pdf) {
     // Frame::FromZ(wo).FromLocal(SphericalDirection(sinTheta, cosTheta, phi))
     Vec z = wo, x, y;
     CoordinateSystem(z, &x, &y);
-    Vec l(Clamp(sinTheta, -1, 1) * std::cos(phi), Clamp(sinTheta, -1, 1) * std::sin(phi), Clamp(cosTheta, -1, 1));
+    Vec l(Clamp(sinTheta, -1, 1) * CRCos(phi), Clamp(sinTheta, -1, 1) * CRSin(phi), Clamp(cosTheta, -1, 1));
     *pdf = HenyeyGreenstein(cosTheta, g);
     return x * l.x + y * l.y + z * l.z;
 }
@@ -1669,7 +1685,7 @@ static Spectrum SampleTmaj(const Media &M, int m, Vec o, Vec d, Float tMax, Floa
         }
         Float tMin = seg.tMin;
         while (true) {
-            Float t = tMin + (-std::log(1 - u) / seg.sigma_maj[0]);  // SampleExponential
+            Float t = tMin + (-CRLog(1 - u) / seg.sigma_maj[0]);  // SampleExponential
             u = rng.Uniform();
             if (t < seg.tMax) {
                 T_maj = T_maj * FastExpS(seg.sigma_maj * -(t - tMin));
@@ -2109,6 +2125,9 @@ struct Renderer {
 using namespace oracle;
 
 extern "C" {
+
+// Transcendental mode of every later call (see CRSin): 0 = libm float (reference), 1 = CR
+void oracle_set_cr_math(int on) { g_crMath = on ? 1 : 0; }
 
 // Renders rows x [first_sample, first_sample + n_samples) into film[4][yres*xres]
 // (sensor RGB sums + weight sums, RGBFilm::Pixel layout) with `threads` host threads.

@@ -43,7 +43,21 @@ def lib():
         _lib.oracle_triangle_shading.argtypes = [vp] * 3 + [ctypes.c_int] + [vp] * 3
         _lib.oracle_render.argtypes = [vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, vp]
+        _lib.oracle_set_cr_math.argtypes = [ctypes.c_int]
     return _lib
+
+
+class cr_math:
+    """Context manager: the oracle evaluates transcendentals correctly rounded (as the device
+    media kernels do) inside the block, libm float (as the reference) outside it."""
+
+    def __enter__(self):
+        lib().oracle_set_cr_math(1)
+        return self
+
+    def __exit__(self, *exc):
+        lib().oracle_set_cr_math(0)
+        return False
 
 
 def f32(a):

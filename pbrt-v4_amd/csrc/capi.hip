@@ -26,6 +26,9 @@ hipError_t LaunchEscaped(const DeviceScene &S, const PathState &st, int depth, i
 hipError_t LaunchEmissive(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
 hipError_t LaunchShadow(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
 hipError_t LaunchFilm(const DeviceScene &S, const PathState &st, int nSamples, hipStream_t s);
+hipError_t LaunchVolCamera(const DeviceScene &S, const PathState &st, const VolState &v, int nActive, hipStream_t s);
+hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const VolState &v, int wf, int maxCount,
+                              hipStream_t s);
 hipError_t LaunchIntersectBatch(const DeviceScene &S, const float *rays, int n, int anyHit, int *outPrim,
                                 float *outHit, hipStream_t s);
 }  // namespace pbrt_amd
@@ -184,6 +187,8 @@ struct pbrt_context {
     DevBuf<float> sensor4;
     DevBuf<DeviceLightNode> lightNodes;
     DevBuf<DeviceAreaLight> lights;
+    DevBuf<int> mediumInfo, primMedium;
+    DevBuf<float> mediumParams, mediumValues;
     // wavefront buffers
     int64_t maxPaths = 0;
     DevBuf<float> fState;
@@ -191,7 +196,11 @@ struct pbrt_context {
     DevBuf<int> rows;
     DevBuf<double> film;
     DevBuf<unsigned long long> devStats;
+    DevBuf<float> vfState;  // media scenes: VolState records
+    DevBuf<int> viState;
     PathState st{};
+    VolState vs{};
+    bool volumetric = false;  // media or interface materials: the volpath.hip kernels render
     // timing
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
     int eventsUsed = 0;
@@ -390,7 +399,34 @@ static void BuildDevice(pbrt_context *c) {
         c->permDepthInfo.Upload(info);
     }
 
+    // participating media: the flat tables, and {inside, outside} per leaf-order triangle
+    if (!s.media.empty()) {
+        std::vector<int32_t> mi;
+        std::vector<float> mp, mv;
+        MediumTables(s, &mi, &mp, &mv);
+        if (mv.empty()) mv.push_back(0.f);
+        c->mediumInfo.Upload(std::vector<int>(mi.begin(), mi.end()));
+        c->mediumParams.Upload(mp);
+        c->mediumValues.Upload(mv);
+        if (!s.triMedium.empty()) {
+            std::vector<int> tm((size_t)nt * 2);
+            for (int i = 0; i < nt; ++i) {
+                tm[2 * i] = s.triMedium[b.triPrim[i]][0];
+                tm[2 * i + 1] = s.triMedium[b.triPrim[i]][1];
+            }
+            c->primMedium.Upload(tm);
+        }
+    }
+
     DeviceScene &S = c->S;
+    S.media.n = (int)s.media.size();
+    c->volumetric = !s.media.empty() ||
+                    std::any_of(s.materials.begin(), s.materials.end(), [](const MaterialDesc &m) { return m.type == kMatInterface; });
+    S.media.cameraMedium = s.cameraMedium;
+    S.media.info = c->mediumInfo.p;
+    S.media.params = c->mediumParams.p;
+    S.media.values = c->mediumValues.p;
+    S.media.primMedium = c->primMedium.p;
     S.nodes = c->nodes.p;
     S.qnodes = c->qnodes.p;
     S.triVerts = (const float4 *)c->triVerts.p;
@@ -510,7 +546,7 @@ static void BuildDevice(pbrt_context *c) {
             off = align16(off + (int)s.materials.size() * 4);
         }
         L.total = off;
-        if (L.total > 64 * 1024) throw Error("shade kernel LDS layout exceeds 64 KB");
+        if (L.total > 64 * 1024 && !c->volumetric) throw Error("shade kernel LDS layout exceeds 64 KB");
     }
     S.stackSize = c->bvh.maxStack;
     {
@@ -583,6 +619,55 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
     st.escQ = takei(1);
     st.emitQ = takei(1);
     st.counters = ip;
+    if (c->volumetric) {
+        // VolState: records 2 x (beta, r_u, r_l 93 + ray 6 + prev 12 + lambda0, etaScale 2) = 226,
+        // hitB 4, shadow ray 6 + Ld/r_u/r_l 93 + lambda0 = 100 floats; records 2 x (flags, pixel,
+        // depth, medium) = 8, hitPrim, 3 queues, shadow pixel + medium = 14 ints
+        const int vf = 330, vi = 14;
+        c->vfState.Alloc((size_t)vf * NR);
+        c->viState.Alloc((size_t)vi * NR);
+        float *g = c->vfState.p;
+        int *gi = c->viState.p;
+        auto tf = [&](int k) {
+            float *r = g;
+            g += (size_t)k * NR;
+            return r;
+        };
+        auto ti = [&](int k) {
+            int *r = gi;
+            gi += (size_t)k * NR;
+            return r;
+        };
+        VolState &v = c->vs;
+        for (int b = 0; b < 2; ++b) {
+            VolRecords &r = v.rec[b];
+            r.beta = tf(31);
+            r.ru = tf(31);
+            r.rl = tf(31);
+            r.ray = tf(6);
+            r.prev = tf(12);
+            r.lambda0 = tf(1);
+            r.etaScale = tf(1);
+            r.flags = ti(1);
+            r.pixel = ti(1);
+            r.depth = ti(1);
+            r.medium = ti(1);
+        }
+        v.hitB = tf(4);
+        v.shRay = tf(6);
+        v.shLd = tf(31);
+        v.shRu = tf(31);
+        v.shRl = tf(31);
+        v.shLambda0 = tf(1);
+        v.hitPrim = ti(1);
+        v.medQ = ti(1);
+        v.surfQ = ti(1);
+        v.scatQ = ti(1);
+        v.shPixel = ti(1);
+        v.shMedium = ti(1);
+        if (g - c->vfState.p > (ptrdiff_t)vf * NR || gi - c->viState.p > (ptrdiff_t)vi * NR)
+            throw Error("VolState layout overflow");
+    }
     if (!c->devStats.p) {
         c->devStats.Alloc(kStatsSlots);
         HIPCHECK(hipMemset(c->devStats.p, 0, kStatsSlots * sizeof(unsigned long long)));
@@ -642,6 +727,16 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
             st.firstSample = p->first_sample + s0;
             st.film = c->film.p;
             HIPCHECK(hipMemsetAsync(st.counters, 0, countersBytes, c->stream));
+            if (c->volumetric) {
+                // participating media: the volumetric wavefront (volpath.hip), same film update
+                HIPCHECK(LaunchVolCamera(c->S, st, c->vs, (int)nActive, c->stream));
+                for (int wf = 0; wf <= s.maxDepth; ++wf)
+                    HIPCHECK(LaunchVolIteration(c->S, st, c->vs, wf, (int)nActive, c->stream));
+                HIPCHECK(LaunchFilm(c->S, st, nS, c->stream));
+                c->stats.passes++;
+                c->stats.paths_per_pass = std::max<uint64_t>(c->stats.paths_per_pass, nActive);
+                continue;
+            }
             HIPCHECK(LaunchCamera(c->S, st, (int)nActive, c->stream));
             for (int depth = 0; depth <= s.maxDepth; ++depth) {
                 // closest-hit launches are event-timed in the first pass of a render only: the

@@ -66,12 +66,35 @@ PHD float NextFloatDown(float v) {
 // util/float.h:197 gamma(n)
 PHD constexpr float gamma(int n) { return (n * kMachineEpsilon) / (1 - n * kMachineEpsilon); }
 
+// Transcendentals.  Host code calls libm's float functions, as the reference CPU build does.
+// The participating-media kernels (volpath.hip defines PBRT_AMD_CR_MATH) take the correctly
+// rounded float result (evaluated in double, rounded once), which the CPU oracle reproduces in
+// its CR mode (oracle_set_cr_math): a medium path's RNG is seeded from the bits of its ray
+// (RNG(Hash(ray.o, tMax), Hash(ray.d)), wavefront/media.cpp:44), so an ulp anywhere upstream
+// would decorrelate the device from the oracle.  The surface-only kernels (wavefront.hip) use
+// the device's own float functions: there an ulp never reseeds anything.
+#if defined(__HIP_DEVICE_COMPILE__) && defined(PBRT_AMD_CR_MATH)
+PHD float Sinf(float x) { return (float)std::sin((double)x); }
+PHD float Cosf(float x) { return (float)std::cos((double)x); }
+PHD float ASinf(float x) { return (float)std::asin((double)x); }
+PHD float ACosf(float x) { return (float)std::acos((double)x); }
+PHD float ATan2f(float y, float x) { return (float)std::atan2((double)y, (double)x); }
+PHD float Logf(float x) { return (float)std::log((double)x); }
+#else
+PHD float Sinf(float x) { return std::sin(x); }
+PHD float Cosf(float x) { return std::cos(x); }
+PHD float ASinf(float x) { return std::asin(x); }
+PHD float ACosf(float x) { return std::acos(x); }
+PHD float ATan2f(float y, float x) { return std::atan2(y, x); }
+PHD float Logf(float x) { return std::log(x); }
+#endif
+
 PHD float Sqr(float v) { return v * v; }
 PHD float Clampf(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
 PHD float Lerpf(float t, float a, float b) { return (1 - t) * a + t * b; }
 PHD float SafeSqrt(float x) { return std::sqrt(std::fmax(0.f, x)); }
-PHD float SafeASin(float x) { return std::asin(Clampf(x, -1, 1)); }
-PHD float SafeACos(float x) { return std::acos(Clampf(x, -1, 1)); }
+PHD float SafeASin(float x) { return ASinf(Clampf(x, -1, 1)); }
+PHD float SafeACos(float x) { return ACosf(Clampf(x, -1, 1)); }
 // util/math.h:570-583
 PHD float DifferenceOfProducts(float a, float b, float c, float d) {
     float cd = c * d;
@@ -144,7 +167,7 @@ PHD void CoordinateSystem(V3 v1, V3 *v2, V3 *v3) {
 }
 // util/vecmath.h:1640
 PHD float SphericalTriangleArea(V3 a, V3 b, V3 c) {
-    return std::fabs(2 * std::atan2(Dot(a, Cross(b, c)), 1 + Dot(a, b) + Dot(a, c) + Dot(b, c)));
+    return std::fabs(2 * ATan2f(Dot(a, Cross(b, c)), 1 + Dot(a, b) + Dot(a, c) + Dot(b, c)));
 }
 
 // Frame (util/vecmath.h:1855): FromXZ(x, z) = (x, Cross(z, x), z)
@@ -199,8 +222,8 @@ PHD void SampleUniformDiskConcentric(float u0, float u1, float *dx, float *dy) {
         r = oy;
         theta = kPiOver2 - kPiOver4 * (ox / oy);
     }
-    *dx = r * std::cos(theta);
-    *dy = r * std::sin(theta);
+    *dx = r * Cosf(theta);
+    *dy = r * Sinf(theta);
 }
 PHD V3 SampleCosineHemisphere(float u0, float u1) {  // :409
     float dx, dy;
@@ -260,9 +283,9 @@ PHD_NOINLINE SphTriSample SampleSphericalTriangle(V3 v0, V3 v1, V3 v2, V3 p, flo
         float A = A_pi - kPi;
         *pdf = (A <= 0) ? 0 : 1 / A;
     }
-    float cosAlpha = std::cos(alpha), sinAlpha = std::sin(alpha);
-    float sinPhi = std::sin(Ap_pi) * cosAlpha - std::cos(Ap_pi) * sinAlpha;
-    float cosPhi = std::cos(Ap_pi) * cosAlpha + std::sin(Ap_pi) * sinAlpha;
+    float cosAlpha = Cosf(alpha), sinAlpha = Sinf(alpha);
+    float sinPhi = Sinf(Ap_pi) * cosAlpha - Cosf(Ap_pi) * sinAlpha;
+    float cosPhi = Cosf(Ap_pi) * cosAlpha + Sinf(Ap_pi) * sinAlpha;
     float k1 = cosPhi + cosAlpha;
     float k2 = sinPhi - sinAlpha * Dot(a, bb);
     float cosBp = (k2 + (DifferenceOfProducts(k2, cosPhi, k1, sinPhi)) * cosAlpha) /
@@ -842,7 +865,7 @@ struct TrowbridgeReitz {
         V3 T2 = Cross(wh, T1);
         // SampleUniformDiskPolar (util/sampling.h:311-315)
         float r = std::sqrt(u0), theta = 2 * kPi * u1;
-        float px = r * std::cos(theta), py = r * std::sin(theta);
+        float px = r * Cosf(theta), py = r * Sinf(theta);
         float h = std::sqrt(1 - Sqr(px));
         py = Lerpf((1 + wh.z) / 2, h, py);
         float pz = std::sqrt(std::fmax(0.f, 1 - (Sqr(px) + Sqr(py))));
@@ -1188,6 +1211,114 @@ PHD_NOINLINE float LightImportance(LightNodeBounds lb, V3 p, V3 n) {
     }
     importance = std::fmax(importance, 0.f);
     return importance;
+}
+
+// ---------------------------------------------------------------- participating media
+// pbrt's Hash(args...) over whole 4-byte words (util/hash.h:91-106): MurmurHash64A (seed 0) of
+// the packed arguments, e.g. Hash(ray.o, tMax) = 16 bytes, Hash(ray.d) = 12 bytes.
+PHD uint64_t HashWords(const uint32_t *w, int nWords) {
+    const uint64_t m = 0xc6a4a7935bd1e995ull;
+    const int r = 47;
+    uint64_t h = (uint64_t)(4 * nWords) * m;
+    for (int i = 0; i + 1 < nWords; i += 2) {
+        uint64_t k = (uint64_t)w[i] | ((uint64_t)w[i + 1] << 32);  // little-endian 8-byte block
+        k *= m;
+        k ^= k >> r;
+        k *= m;
+        h ^= k;
+        h *= m;
+    }
+    if (nWords & 1) {  // 4-byte tail: bytes 3..0 xor-ed in, then one multiply
+        h ^= (uint64_t)w[nWords - 1];
+        h *= m;
+    }
+    h ^= h >> r;
+    h *= m;
+    h ^= h >> r;
+    return h;
+}
+PHD uint64_t HashV3(V3 v) {
+    const uint32_t w[3] = {FloatToBits(v.x), FloatToBits(v.y), FloatToBits(v.z)};
+    return HashWords(w, 3);
+}
+PHD uint64_t HashV3F(V3 v, float f) {
+    const uint32_t w[4] = {FloatToBits(v.x), FloatToBits(v.y), FloatToBits(v.z), FloatToBits(f)};
+    return HashWords(w, 4);
+}
+
+// PCG32 (util/rng.h:30-140): RNG(seqIndex, offset) = SetSequence(seqIndex, offset)
+struct PCG32 {
+    uint64_t state, inc;
+    PHD PCG32(uint64_t seqIndex, uint64_t offset) {
+        state = 0u;
+        inc = (seqIndex << 1u) | 1u;
+        NextU32();
+        state += offset;
+        NextU32();
+    }
+    PHD uint32_t NextU32() {
+        const uint64_t old = state;
+        state = old * 0x5851f42d4c957f2dULL + inc;
+        const uint32_t xorshifted = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+        const uint32_t rot = (uint32_t)(old >> 59u);
+        return (xorshifted >> rot) | (xorshifted << ((~rot + 1u) & 31));
+    }
+    PHD float Uniform() { return std::fmin(kOneMinusEpsilon, (float)NextU32() * 0x1p-32f); }
+};
+
+// FastExp (util/math.h:450-475), the CPU form (2^x by a cubic on the fraction, exponent bits
+// patched in).  |xp| > 256 (and NaN) short-circuit to the values the exponent test gives.
+PHD float FastExp(float x) {
+    const float xp = x * 1.442695041f;
+    if (!(xp > -256.f)) return 0.f;
+    if (xp > 256.f) return kInfinity;
+    const float fxp = std::floor(xp), f = xp - fxp;
+    const int i = (int)fxp;
+    const float twoToF = fmaf(f, fmaf(f, fmaf(f, 0.0781455737f, 0.226173572f), 0.695556856f), 1.f);
+    const int exponent = (int)((FloatToBits(twoToF) >> 23) & 0xff) - 127 + i;
+    if (exponent < -126) return 0.f;
+    if (exponent > 127) return kInfinity;
+    uint32_t bits = FloatToBits(twoToF);
+    bits &= 0b10000000011111111111111111111111u;
+    bits |= (uint32_t)(exponent + 127) << 23;
+    return BitsToFloat(bits);
+}
+
+// SampleExponential (util/sampling.h): -log(1 - u) / a
+PHD float SampleExponential(float u, float a) { return -Logf(1 - u) / a; }
+
+// HenyeyGreenstein (util/scattering.h:49-58) and SampleHenyeyGreenstein (util/sampling.cpp:347-373)
+constexpr float kInv4Pi = 0.07957747154594766788f;
+PHD float HenyeyGreenstein(float cosTheta, float g) {
+    g = Clampf(g, -.99f, .99f);
+    const float denom = 1 + Sqr(g) + 2 * g * cosTheta;
+    return kInv4Pi * (1 - Sqr(g)) / (denom * SafeSqrt(denom));
+}
+PHD V3 SampleHenyeyGreenstein(V3 wo, float g, float u0, float u1, float *pdf) {
+    g = Clampf(g, -.99f, .99f);
+    float cosTheta;
+    if (std::fabs(g) < 1e-3f) cosTheta = 1 - 2 * u0;
+    else cosTheta = -1 / (2 * g) * (1 + Sqr(g) - Sqr((1 - Sqr(g)) / (1 + g - 2 * g * u0)));
+    const float sinTheta = SafeSqrt(1 - Sqr(cosTheta));
+    const float phi = 2 * kPi * u1;
+    V3 x, y;
+    CoordinateSystem(wo, &x, &y);  // Frame::FromZ(wo)
+    const float st = Clampf(sinTheta, -1, 1);
+    const V3 l(st * Cosf(phi), st * Sinf(phi), Clampf(cosTheta, -1, 1));  // SphericalDirection
+    *pdf = HenyeyGreenstein(cosTheta, g);
+    return x * l.x + y * l.y + wo * l.z;
+}
+
+// SampleDiscrete (util/sampling.h:79-110) over three weights; bounded to the last index
+PHD int SampleDiscrete3(float w0, float w1, float w2, float u) {
+    const float sum = (w0 + w1) + w2;
+    float up = u * sum;
+    if (up == sum) up = NextFloatDown(up);
+    float acc = 0;
+    if (acc + w0 > up) return 0;
+    acc += w0;
+    if (acc + w1 > up) return 1;
+    return 2;
 }
 
 }  // namespace pbrt_amd

@@ -1,0 +1,925 @@
+// Device helpers shared by the wavefront kernels (wavefront.hip: surface-only paths) and the
+// participating-media kernels (volpath.hip): queues, samplers, BVH8 traversal, light sampling,
+// camera rays and spectral accumulation.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "device.h"
+
+namespace pbrt_amd {
+
+constexpr int kBlock = 256;
+#ifndef PBRT_TRAVERSAL_WAVES
+#define PBRT_TRAVERSAL_WAVES 4  // waves/SIMD the closest/shadow kernels are compiled for
+#endif
+#ifndef PBRT_SHADE_WAVES
+#define PBRT_SHADE_WAVES 3  // waves/SIMD the shade kernel is compiled for (VGPR budget)
+#endif
+constexpr float kInvWavelengthPDF = kLambdaMax - kLambdaMin;  // 1 / SampleUniformWavelengths pdf
+
+// ------------------------------------------------------------------ helpers
+// Section timing (profiling build only): wave-level s_memtime deltas summed per section by the
+// wave's first active lane into stats[kStatsSectionBase + k].
+#ifdef PBRT_AMD_SECTION_TIMING
+#define SEC_BEGIN() unsigned long long secT_ = __builtin_amdgcn_s_memtime()
+#define SEC_MARK(st, k)                                                                          \
+    do {                                                                                         \
+        unsigned long long n_ = __builtin_amdgcn_s_memtime();                                    \
+        if (__lane_id() == __ffsll((long long)__ballot(1)) - 1)                                   \
+            atomicAdd(&(st).stats[kStatsSectionBase + (k)], n_ - secT_);                         \
+        secT_ = n_;                                                                              \
+    } while (0)
+#else
+#define SEC_BEGIN() (void)0
+#define SEC_MARK(st, k) (void)0
+#endif
+__device__ inline int WavePush(int *counter, bool pred) {
+    unsigned long long mask = __ballot(pred);
+    if (mask == 0) return -1;
+    int lane = __lane_id();
+    int leader = __ffsll((long long)mask) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(counter, __popcll(mask));
+    base = __shfl(base, leader);
+    return pred ? base + __popcll(mask & ((1ull << lane) - 1ull)) : -1;
+}
+
+// Append to up to K queues for a whole block: one global atomicAdd per queue per block, so the
+// queue counters (one address each, serialised at one L2 channel) see a quarter of the
+// per-wave traffic.  Lanes receive consecutive slots in (wave, lane) order.  Every thread of
+// the block must call it (the callers' grid-stride loops are block-uniform).
+template <int K>
+__device__ inline void BlockPush(int *const (&counters)[K], const bool (&pred)[K], int (&pos)[K]) {
+    constexpr int kWaves = kBlock / 64;
+    __shared__ int sCount[K][kWaves];
+    __shared__ int sBase[K];
+    const int lane = __lane_id(), wave = threadIdx.x >> 6;
+    unsigned long long mask[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        mask[k] = __ballot(pred[k]);
+        if (lane == 0) sCount[k][wave] = __popcll(mask[k]);
+    }
+    __syncthreads();
+    if (threadIdx.x < K) {
+        const int k = threadIdx.x;
+        int tot = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) tot += sCount[k][w];
+        sBase[k] = tot ? atomicAdd(counters[k], tot) : 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        int b = sBase[k];
+        for (int w = 0; w < wave; ++w) b += sCount[k][w];
+        pos[k] = pred[k] ? b + __popcll(mask[k] & ((1ull << lane) - 1ull)) : -1;
+    }
+    __syncthreads();  // sCount/sBase are reused by the next call
+}
+
+// Block-wide global -> LDS copies by LDS-DMA (global_load_lds_*): no VGPR round trip and no
+// wait per element, so a prologue of several tables costs one memory latency.  Each wave
+// copies 64 consecutive elements per instruction (LDS destination = wave base + lane * size);
+// lanes past the end are masked.  Callers finish with DmaWait() and one __syncthreads().
+template <int Bytes>  // 4 or 16 (sub-dword LDS-DMA does not pack lanes)
+__device__ inline void DmaCopy(const void *src, void *ldsDst, int n) {
+    const int lane = __lane_id(), wave = threadIdx.x >> 6, nWaves = blockDim.x >> 6;
+    for (int base = wave * 64; base < n; base += nWaves * 64) {
+        if (base + lane < n) {
+            auto g = (const __attribute__((address_space(1))) void *)((const char *)src + (size_t)(base + lane) * Bytes);
+            auto l = (__attribute__((address_space(3))) void *)((char *)ldsDst + (size_t)base * Bytes);
+            // the builtin's size operand must be a literal
+            static_assert(Bytes == 4 || Bytes == 16, "DmaCopy: 4- or 16-byte elements");
+            if constexpr (Bytes == 4) __builtin_amdgcn_global_load_lds(g, l, 4, 0, 0);
+            else __builtin_amdgcn_global_load_lds(g, l, 16, 0, 0);
+        }
+    }
+}
+__device__ inline void DmaWait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Block-local staging of queue appends: entries collect in an LDS buffer across the block's
+// grid-stride iterations (one LDS atomic per wave) and are written out in contiguous runs with
+// one global atomicAdd per flush, i.e. every ~cap/256 iterations instead of every iteration.
+// All threads of the block must call Append/FlushAll (the grid-stride loops are block-uniform).
+template <int K, int Cap>
+struct BlockQueues {
+    int *buf;   // LDS [K][Cap]
+    int *fill;  // LDS [K]
+    int *gbase; // LDS [K]
+    int *const *counters;
+    int *const *queues;
+
+    __device__ void Init() {
+        if (threadIdx.x < K) fill[threadIdx.x] = 0;
+        __syncthreads();
+    }
+    __device__ void Flush(int k) {
+        const int n = fill[k];
+        if (threadIdx.x == 0) gbase[k] = n ? atomicAdd(counters[k], n) : 0;
+        __syncthreads();
+        const int b = gbase[k];
+        int *q = queues[k];
+        for (int i = threadIdx.x; i < n; i += blockDim.x) q[b + i] = buf[k * Cap + i];
+        __syncthreads();
+        if (threadIdx.x == 0) fill[k] = 0;
+        __syncthreads();
+    }
+    __device__ void Append(const bool (&pred)[K], int slot) {
+        const int lane = __lane_id();
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const unsigned long long mask = __ballot(pred[k]);
+            const int n = __popcll(mask);
+            int b = 0;
+            if (lane == 0 && n) b = atomicAdd(&fill[k], n);  // LDS atomic
+            b = __shfl(b, 0);
+            if (pred[k]) buf[k * Cap + b + __popcll(mask & ((1ull << lane) - 1ull))] = slot;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (fill[k] > Cap - kBlock) Flush(k);  // block-uniform: read after the barrier
+    }
+    __device__ void FlushAll() {
+#pragma unroll
+        for (int k = 0; k < K; ++k) Flush(k);
+    }
+};
+
+// Wave-local staging of queue appends: each wave owns a Cap-entry LDS buffer per queue, fills
+// it with ballot/popcount prefixes and writes it out in a contiguous run with one global
+// atomicAdd when it would overflow (and at the end).  No block barriers: a wave never waits
+// for the slowest wave of its block, unlike BlockQueues.
+template <int K, int Cap>
+struct WaveQueues {
+    int *buf;  // LDS: this wave's [K][Cap]
+    int fill[K];
+    int *const *counters;
+    int *const *queues;
+
+    __device__ WaveQueues(int *ldsAll, int *const *c, int *const *q) : counters(c), queues(q) {
+        buf = ldsAll + (threadIdx.x >> 6) * (K * Cap);
+#pragma unroll
+        for (int k = 0; k < K; ++k) fill[k] = 0;
+    }
+    __device__ void Flush(int k) {
+        const int n = fill[k];
+        if (n == 0) return;
+        int b = 0;
+        if (__lane_id() == 0) b = atomicAdd(counters[k], n);
+        b = __shfl(b, 0);
+        int *q = queues[k];
+        for (int i = __lane_id(); i < n; i += 64) q[b + i] = buf[k * Cap + i];
+        fill[k] = 0;
+    }
+    __device__ void Append(const bool (&pred)[K], int value) {
+        const int lane = __lane_id();
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const unsigned long long mask = __ballot(pred[k]);
+            const int n = __popcll(mask);
+            if (fill[k] + n > Cap) Flush(k);
+            if (pred[k]) buf[k * Cap + fill[k] + __popcll(mask & ((1ull << lane) - 1ull))] = value;
+            fill[k] += n;
+        }
+    }
+    __device__ void FlushAll() {
+#pragma unroll
+        for (int k = 0; k < K; ++k) Flush(k);
+    }
+};
+
+// A sharded queue as its consumer sees it: per-shard counts (uniform, scalar loads) and the
+// map from a dense item index j to the item's physical index (shard * capS + offset).
+struct QueueView {
+    int count[kShards];
+    int total, capS;
+};
+__device__ inline QueueView LoadQueue(const PathState &st, int depth, int queue) {
+    QueueView v;
+    v.total = 0;
+    v.capS = st.capS;
+#pragma unroll
+    for (int s = 0; s < kShards; ++s) {
+        v.count[s] = st.counters[CounterIndex(depth, queue, s)];
+        v.total += v.count[s];
+    }
+    return v;
+}
+__device__ inline int QueueSlot(const QueueView &v, int j) {
+    int base = 0, shard = 0;
+#pragma unroll
+    for (int s = 0; s < kShards - 1; ++s) {
+        const bool later = j >= base + v.count[s];
+        base += later ? v.count[s] : 0;
+        shard += later ? 1 : 0;
+        if (!later) break;
+    }
+    return shard * v.capS + (j - base);
+}
+__device__ inline int ProducerShard() { return blockIdx.x % kShards; }
+
+__device__ inline V3 XfPoint(const float *m, V3 p) {
+    float xp = m[0] * p.x + m[1] * p.y + m[2] * p.z + m[3];
+    float yp = m[4] * p.x + m[5] * p.y + m[6] * p.z + m[7];
+    float zp = m[8] * p.x + m[9] * p.y + m[10] * p.z + m[11];
+    float wp = m[12] * p.x + m[13] * p.y + m[14] * p.z + m[15];
+    if (wp == 1) return V3(xp, yp, zp);
+    return V3(xp, yp, zp) / wp;
+}
+__device__ inline V3 XfVector(const float *m, V3 v) {
+    return V3(m[0] * v.x + m[1] * v.y + m[2] * v.z, m[4] * v.x + m[5] * v.y + m[6] * v.z,
+              m[8] * v.x + m[9] * v.y + m[10] * v.z);
+}
+
+struct Halton {
+    uint64_t index;
+    int dimension;
+};
+
+__device__ inline Halton StartPixelSample(const DeviceScene &S, int px, int py, int sampleIndex, int dim) {
+    // samplers.h:53-71
+    Halton h;
+    h.index = 0;
+    if (S.haltonFast32) {
+        // Same terms in 32-bit arithmetic: the host checked that the stride and every partial
+        // sum fit (stride * (scale0 + scale1) < 2^32), so no 64-bit division is needed.
+        const uint32_t stride = (uint32_t)S.baseScales[0] * (uint32_t)S.baseScales[1];
+        uint32_t pmx = (uint32_t)px & 127u, pmy = (uint32_t)py & 127u;  // Mod(p, 128), p >= 0
+        uint32_t i0 = (uint32_t)InverseRadicalInverse((uint64_t)pmx, 2, S.baseExponents[0]);
+        uint32_t i1 = 0;
+        for (int k = 0; k < S.baseExponents[1]; ++k) {
+            uint32_t q = pmy / 3u;
+            i1 = i1 * 3u + (pmy - 3u * q);
+            pmy = q;
+        }
+        uint32_t t = i0 * (uint32_t)S.baseScales[1] * (uint32_t)S.multInverse[0] +
+                     i1 * (uint32_t)S.baseScales[0] * (uint32_t)S.multInverse[1];
+        h.index = (uint64_t)(t % stride) + (uint64_t)sampleIndex * stride;
+        h.dimension = dim < 2 ? 2 : dim;
+        return h;
+    }
+    uint64_t sampleStride = (uint64_t)S.baseScales[0] * S.baseScales[1];
+    if (sampleStride > 1) {
+        int pmx = px % 128, pmy = py % 128;
+        if (pmx < 0) pmx += 128;
+        if (pmy < 0) pmy += 128;
+        h.index += InverseRadicalInverse((uint64_t)pmx, 2, S.baseExponents[0]) * (sampleStride / S.baseScales[0]) *
+                   (uint64_t)S.multInverse[0];
+        h.index += InverseRadicalInverse((uint64_t)pmy, 3, S.baseExponents[1]) * (sampleStride / S.baseScales[1]) *
+                   (uint64_t)S.multInverse[1];
+        h.index %= sampleStride;
+    }
+    h.index += (uint64_t)sampleIndex * sampleStride;
+    h.dimension = dim < 2 ? 2 : dim;
+    return h;
+}
+__device__ inline float SampleDim(const DeviceScene &S, uint64_t index, int dim) {
+    return HaltonSampleDimension(S.haltonDim[dim], index, S.perm);
+}
+__device__ inline float Get1D(const DeviceScene &S, Halton &h) {
+    if (h.dimension >= S.nDims) h.dimension = 2;
+    return SampleDim(S, h.index, h.dimension++);
+}
+__device__ inline void Get2D(const DeviceScene &S, Halton &h, float *u0, float *u1) {
+    if (h.dimension + 1 >= S.nDims) h.dimension = 2;
+    int dim = h.dimension;
+    h.dimension += 2;
+    *u0 = SampleDim(S, h.index, dim);
+    *u1 = SampleDim(S, h.index, dim + 1);
+}
+
+__device__ inline void PixelOf(const PathState &st, int slot, int *px, int *py, int *sampleIndex) {
+    int s = slot / st.P, pl = slot - s * st.P;
+    int r = pl / st.width;
+    *px = pl - r * st.width;
+    *py = st.rows[r];
+    *sampleIndex = st.firstSample + s;
+}
+
+// ------------------------------------------------------------------ BVH8 traversal
+// One ray per lane.  The node's 8 child boxes are read as 12 float4 loads (SoA inside the
+// 256-byte node), the 8 slab tests run fully unrolled in registers, leaves are intersected
+// nearest-first and interior children are pushed farthest-first onto a per-lane stack that
+// lives in LDS ([depth][lane] layout: consecutive lanes hit consecutive banks), so nothing
+// spills to scratch.  Box test = Bounds3::IntersectP (util/vecmath.h:1576-1611) including the
+// 1 + 2 gamma(3) far-plane slack; triangle test = IntersectTriangle (shapes.cpp:172-273).
+// Stack entries per lane = DeviceScene::stackSize (the BVH's exact worst case, host-computed,
+// at most kMaxStackSize), allocated as dynamic LDS at launch so small scenes keep occupancy.
+
+struct RayPre {
+    V3 o, invDir;
+    int neg[3];
+};
+
+template <typename F4>
+__device__ inline void SlabTest4(const F4 *__restrict__ q, int g, const RayPre &r, float raytMax, float tn[8],
+                                 unsigned *mask) {
+    // children 4g..4g+3: lox,loy,loz at float4 index 2a+g, hix,hiy,hiz at 6+2a+g
+    float4 L[3], H[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        L[a] = q[2 * a + g];
+        H[a] = q[6 + 2 * a + g];
+    }
+    const float slack = 1 + 2 * gamma(3);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        float lo[3], hi[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = k == 0 ? L[a].x : k == 1 ? L[a].y : k == 2 ? L[a].z : L[a].w;
+            hi[a] = k == 0 ? H[a].x : k == 1 ? H[a].y : k == 2 ? H[a].z : H[a].w;
+        }
+        float nx = r.neg[0] ? hi[0] : lo[0], fx = r.neg[0] ? lo[0] : hi[0];
+        float ny = r.neg[1] ? hi[1] : lo[1], fy = r.neg[1] ? lo[1] : hi[1];
+        float nz = r.neg[2] ? hi[2] : lo[2], fz = r.neg[2] ? lo[2] : hi[2];
+        float tMin = (nx - r.o.x) * r.invDir.x;
+        float tMax = (fx - r.o.x) * r.invDir.x * slack;
+        float tyMin = (ny - r.o.y) * r.invDir.y;
+        float tyMax = (fy - r.o.y) * r.invDir.y * slack;
+        bool ok = !(tMin > tyMax || tyMin > tMax);
+        tMin = tyMin > tMin ? tyMin : tMin;
+        tMax = tyMax < tMax ? tyMax : tMax;
+        float tzMin = (nz - r.o.z) * r.invDir.z;
+        float tzMax = (fz - r.o.z) * r.invDir.z * slack;
+        ok = ok && !(tMin > tzMax || tzMin > tMax);
+        tMin = tzMin > tMin ? tzMin : tMin;
+        tMax = tzMax < tMax ? tzMax : tMax;
+        ok = ok && (tMin < raytMax) && (tMax > 0);
+        tn[4 * g + k] = tMin;
+        *mask |= ok ? (1u << (4 * g + k)) : 0u;
+    }
+}
+
+template <typename F4>
+__device__ inline void SlabTest8(const F4 *__restrict__ q, const RayPre &r, float raytMax, float tn[8],
+                                 unsigned *mask) {
+    *mask = 0;
+    SlabTest4(q, 0, r, raytMax, tn, mask);
+    SlabTest4(q, 1, r, raytMax, tn, mask);
+}
+
+// Child references of a compressed node, decoded on demand for the children actually visited
+struct QRefs {
+    unsigned imask, meta[2];
+    int childBase, triBase;
+    // the uncompressed encoding: >= 0 interior node, < 0 leaf ~(first << 3 | count - 1)
+    __device__ int Get(int c) const {
+        if ((imask >> c) & 1u) return childBase + __popc(imask & ((1u << c) - 1u));
+        const unsigned m = (meta[c >> 2] >> (8 * (c & 3))) & 0xffu;
+        const int first = triBase + (int)(m & 31u), count = (int)((m >> 5) & 3u) + 1;
+        return ~((first << 3) | (count - 1));
+    }
+};
+
+// Slab tests of a compressed node (BVH8QNode, 5 float4): child planes decoded as
+// fma(q, 2^(e-127), p) -- the expression the host rounded outward -- then the same test as
+// SlabTest4.
+template <typename F4>
+__device__ inline void SlabTestQ(const F4 *__restrict__ q, const RayPre &r, float raytMax, float tn[8],
+                                 unsigned *mask, QRefs *refs) {
+    const float4 f0 = q[0], f1 = q[1], f2 = q[2], f3 = q[3], f4 = q[4];
+    const unsigned eb = __float_as_uint(f0.w);
+    const float sx = __uint_as_float((eb & 0xffu) << 23), sy = __uint_as_float(((eb >> 8) & 0xffu) << 23),
+                sz = __uint_as_float(((eb >> 16) & 0xffu) << 23);
+    const unsigned imask = eb >> 24;
+    const int childBase = __float_as_int(f1.x), triBase = __float_as_int(f1.y);
+    const unsigned meta[2] = {__float_as_uint(f1.z), __float_as_uint(f1.w)};
+    const unsigned qw[12] = {__float_as_uint(f2.x), __float_as_uint(f2.y), __float_as_uint(f2.z),
+                             __float_as_uint(f2.w), __float_as_uint(f3.x), __float_as_uint(f3.y),
+                             __float_as_uint(f3.z), __float_as_uint(f3.w), __float_as_uint(f4.x),
+                             __float_as_uint(f4.y), __float_as_uint(f4.z), __float_as_uint(f4.w)};
+    const float slack = 1 + 2 * gamma(3);
+    *mask = 0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const int w = c >> 2, sh = 8 * (c & 3);
+        auto byteOf = [&](int field) { return (float)((qw[2 * field + w] >> sh) & 0xffu); };
+        const float lo[3] = {fmaf(byteOf(0), sx, f0.x), fmaf(byteOf(1), sy, f0.y), fmaf(byteOf(2), sz, f0.z)};
+        const float hi[3] = {fmaf(byteOf(3), sx, f0.x), fmaf(byteOf(4), sy, f0.y), fmaf(byteOf(5), sz, f0.z)};
+        float nx = r.neg[0] ? hi[0] : lo[0], fx = r.neg[0] ? lo[0] : hi[0];
+        float ny = r.neg[1] ? hi[1] : lo[1], fy = r.neg[1] ? lo[1] : hi[1];
+        float nz = r.neg[2] ? hi[2] : lo[2], fz = r.neg[2] ? lo[2] : hi[2];
+        float tMin = (nx - r.o.x) * r.invDir.x;
+        float tMax = (fx - r.o.x) * r.invDir.x * slack;
+        float tyMin = (ny - r.o.y) * r.invDir.y;
+        float tyMax = (fy - r.o.y) * r.invDir.y * slack;
+        bool ok = !(tMin > tyMax || tyMin > tMax);
+        tMin = tyMin > tMin ? tyMin : tMin;
+        tMax = tyMax < tMax ? tyMax : tMax;
+        float tzMin = (nz - r.o.z) * r.invDir.z;
+        float tzMax = (fz - r.o.z) * r.invDir.z * slack;
+        ok = ok && !(tMin > tzMax || tzMin > tMax);
+        tMin = tzMin > tMin ? tzMin : tMin;
+        tMax = tzMax < tMax ? tzMax : tMax;
+        ok = ok && (tMin < raytMax) && (tMax > 0);
+        tn[c] = tMin;
+        *mask |= ok ? (1u << c) : 0u;
+    }
+    // occupied slots: interior (imask) or leaf (meta bit 7)
+    const unsigned leafBits = ((meta[0] >> 7) & 1u) | ((meta[0] >> 14) & 2u) | ((meta[0] >> 21) & 4u) |
+                              ((meta[0] >> 28) & 8u) | (((meta[1] >> 7) & 1u) << 4) | (((meta[1] >> 15) & 1u) << 5) |
+                              (((meta[1] >> 23) & 1u) << 6) | (((meta[1] >> 31) & 1u) << 7);
+    *mask &= imask | leafBits;
+    refs->imask = imask;
+    refs->meta[0] = meta[0];
+    refs->meta[1] = meta[1];
+    refs->childBase = childBase;
+    refs->triBase = triBase;
+}
+
+// Scene cache in LDS: the first S.ldsNodes BVH8 nodes (BFS order = the top of the tree) at a
+// 17-float4 stride and the first S.ldsTris triangles of the leaf order.  The 68-dword node
+// stride puts the same field of 16 different nodes in 16 different 4-bank groups, so the
+// ds_read_b128 lane groups stay conflict-free when lanes sit in different nodes; the 12-dword
+// triangle stride does the same for triangles.  Everything else is read from global memory.
+// (strides: kLdsNodeStride / kLdsQNodeStride, device.h)
+
+// LDS-qualified pointers keep the cached and the global paths distinct instructions
+// (ds_read_b128 vs global_load_dwordx4); generic pointers would merge them into flat loads.
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef __attribute__((address_space(3))) const float4 LdsF4;
+#else
+typedef const float4 LdsF4;  // host pass only parses the kernels
+#endif
+struct SceneLds {
+    int *stack;          // [stackSize][blockDim]
+    const LdsF4 *nodes;  // [ldsNodes][17]
+    const LdsF4 *tris;   // [ldsTris][3]
+};
+
+// Lays out the dynamic LDS of a traversal kernel and fills the cache (whole block, one sync).
+__device__ inline SceneLds SetupSceneLds(const DeviceScene &S, float4 *dyn) {
+    SceneLds L;
+    L.stack = reinterpret_cast<int *>(dyn);
+    float4 *nodes = dyn + (S.stackSize * kBlock) / 4;
+    float4 *tris = nodes + S.ldsNodes * LdsNodeStride(S.compressed);
+    // plain copies: measured faster here than per-node LDS-DMA (few, tiny rows)
+    if (S.compressed) {
+        const float4 *gn = reinterpret_cast<const float4 *>(S.qnodes);
+        for (int i = threadIdx.x; i < S.ldsNodes * kLdsQNodeStride; i += blockDim.x) nodes[i] = gn[i];
+    } else {
+        const float4 *gn = reinterpret_cast<const float4 *>(S.nodes);
+        for (int i = threadIdx.x; i < S.ldsNodes * 14; i += blockDim.x) {
+            int n = i / 14, k = i - n * 14;
+            nodes[n * kLdsNodeStride + k] = gn[n * 16 + k];
+        }
+    }
+    for (int i = threadIdx.x; i < S.ldsTris * 3; i += blockDim.x) tris[i] = S.triVerts[i];
+    __syncthreads();
+    L.nodes = (const LdsF4 *)nodes;
+    L.tris = (const LdsF4 *)tris;
+    return L;
+}
+
+// TrisInLds: every triangle is cached (a launch-uniform choice, so no per-lane branch whose
+// two loads the compiler would merge into one flat load).
+template <bool AnyHit, bool TrisInLds, bool Compressed>
+__device__ inline int TraverseT(const DeviceScene &S, const SceneLds &L, V3 o, V3 d, float tMax, TriHit *best) {
+    const TriRay tr = MakeTriRay(o, d);
+    RayPre r;
+    r.o = o;
+    r.invDir = V3(1 / d.x, 1 / d.y, 1 / d.z);
+    r.neg[0] = r.invDir.x < 0;
+    r.neg[1] = r.invDir.y < 0;
+    r.neg[2] = r.invDir.z < 0;
+    const int lane = threadIdx.x, stride = blockDim.x;
+    int *lds = L.stack;
+    int sp = 0;
+    int node = 0;
+    int hitPrim = -1;
+    while (true) {
+        float tn[8];
+        unsigned mask;
+        int ch[8];
+        QRefs qr;
+        if constexpr (Compressed) {
+            if (node < S.ldsNodes) SlabTestQ(L.nodes + node * kLdsQNodeStride, r, tMax, tn, &mask, &qr);
+            else SlabTestQ(reinterpret_cast<const float4 *>(S.qnodes + node), r, tMax, tn, &mask, &qr);
+        } else {
+            int4 ch0, ch1;
+            if (node < S.ldsNodes) {
+                const LdsF4 *q = L.nodes + node * kLdsNodeStride;
+                SlabTest8(q, r, tMax, tn, &mask);
+                float4 c0 = q[12], c1 = q[13];
+                ch0 = make_int4(__float_as_int(c0.x), __float_as_int(c0.y), __float_as_int(c0.z), __float_as_int(c0.w));
+                ch1 = make_int4(__float_as_int(c1.x), __float_as_int(c1.y), __float_as_int(c1.z), __float_as_int(c1.w));
+            } else {
+                const BVH8Node *np = S.nodes + node;
+                SlabTest8(reinterpret_cast<const float4 *>(np), r, tMax, tn, &mask);
+                ch0 = reinterpret_cast<const int4 *>(np->child)[0];
+                ch1 = reinterpret_cast<const int4 *>(np->child)[1];
+            }
+            ch[0] = ch0.x, ch[1] = ch0.y, ch[2] = ch0.z, ch[3] = ch0.w;
+            ch[4] = ch1.x, ch[5] = ch1.y, ch[6] = ch1.z, ch[7] = ch1.w;
+        }
+        // empty slots fail the slab test (inverted box / masked compressed slot)
+        unsigned leaves = 0, inner = 0;
+        if constexpr (Compressed) {
+            inner = mask & qr.imask;
+            leaves = mask & ~qr.imask;
+        } else {
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                if (mask & (1u << c)) {
+                    if (ch[c] < 0) leaves |= 1u << c;
+                    else inner |= 1u << c;
+                }
+            }
+        }
+        // leaves nearest-first
+        while (leaves) {
+            int bc = 0;
+            float bt = kInfinity;
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                if ((leaves & (1u << c)) && tn[c] <= bt) {
+                    bt = tn[c];
+                    bc = c;
+                }
+            leaves &= ~(1u << bc);
+            if (bt >= tMax) continue;
+            int enc = 0;
+            if constexpr (Compressed) {
+                enc = ~qr.Get(bc);
+            } else {
+#pragma unroll
+                for (int c = 0; c < 8; ++c) enc = (c == bc) ? ~ch[c] : enc;
+            }
+            int first = enc >> 3, count = (enc & 7) + 1;
+            for (int t = first; t < first + count; ++t) {
+                float4 a, b, c;
+                if (TrisInLds) {
+                    a = L.tris[3 * t];
+                    b = L.tris[3 * t + 1];
+                    c = L.tris[3 * t + 2];
+                } else {
+                    a = S.triVerts[3 * t];
+                    b = S.triVerts[3 * t + 1];
+                    c = S.triVerts[3 * t + 2];
+                }
+                TriHit h;
+                if (IntersectTriangleRay(tr, tMax, V3(a.x, a.y, a.z), V3(b.x, b.y, b.z), V3(c.x, c.y, c.z), &h)) {
+                    if (AnyHit) return t;
+                    tMax = h.t;
+                    *best = h;
+                    hitPrim = t;
+                }
+            }
+        }
+        // interior children farthest-first onto the stack (closest popped next)
+        while (inner) {
+            int bc = 0;
+            float bt = -kInfinity;
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                if ((inner & (1u << c)) && tn[c] >= bt) {
+                    bt = tn[c];
+                    bc = c;
+                }
+            inner &= ~(1u << bc);
+            if (bt >= tMax) continue;
+            int child = 0;
+            if constexpr (Compressed) {
+                child = qr.Get(bc);
+            } else {
+#pragma unroll
+                for (int c = 0; c < 8; ++c) child = (c == bc) ? ch[c] : child;
+            }
+            lds[(sp++) * stride + lane] = child;  // sp < S.stackSize by construction
+        }
+        if (sp == 0) break;
+        node = lds[(--sp) * stride + lane];
+    }
+    return hitPrim;
+}
+
+// Q: the launch's node format (a kernel template parameter, so each kernel carries only the
+// traversal loops of its own format)
+template <bool AnyHit, bool Q>
+__device__ inline int Traverse(const DeviceScene &S, const SceneLds &L, V3 o, V3 d, float tMax, TriHit *best) {
+    if constexpr (Q) {
+        return TraverseT<AnyHit, false, true>(S, L, o, d, tMax, best);
+    } else {
+        if (S.ldsTris > 0) return TraverseT<AnyHit, true, false>(S, L, o, d, tMax, best);
+        return TraverseT<AnyHit, false, false>(S, L, o, d, tMax, best);
+    }
+}
+
+// ------------------------------------------------------------------ lights
+struct LightSample {
+    float Le[kNSpectrumSamples];
+    V3 wi, p, pErr, n;
+    float pdf;
+};
+
+// Triangle geometry of a leaf-order prim
+__device__ inline void PrimVerts(const DeviceScene &S, int prim, V3 *p0, V3 *p1, V3 *p2) {
+    float4 a = S.triVerts[3 * prim], b = S.triVerts[3 * prim + 1], c = S.triVerts[3 * prim + 2];
+    *p0 = V3(a.x, a.y, a.z);
+    *p1 = V3(b.x, b.y, b.z);
+    *p2 = V3(c.x, c.y, c.z);
+}
+
+// Vertex normals / uv of a leaf-order prim; false (and sh untouched) when it has none
+__device__ inline bool LoadTriShading(const DeviceScene &S, int prim, TriShading *sh) {
+    if (!S.triShade) return false;
+    const float4 a = S.triShade[4 * prim];
+    const int flags = __float_as_int(a.w);
+    if (flags == 0) return false;
+    const float4 b = S.triShade[4 * prim + 1], c = S.triShade[4 * prim + 2], d = S.triShade[4 * prim + 3];
+    sh->flags = flags;
+    sh->n0 = V3(a.x, a.y, a.z);
+    sh->n1 = V3(b.x, b.y, b.z);
+    sh->n2 = V3(c.x, c.y, c.z);
+    sh->uv[0][0] = b.w;
+    sh->uv[0][1] = c.w;
+    sh->uv[1][0] = d.x;
+    sh->uv[1][1] = d.y;
+    sh->uv[2][0] = d.z;
+    sh->uv[2][1] = d.w;
+    return true;
+}
+
+// SurfaceInteraction of a hit (Triangle::InteractionFromIntersection)
+__device__ inline TriSurface SurfaceAt(const DeviceScene &S, int prim, V3 p0, V3 p1, V3 p2, float b0, float b1,
+                                       float b2) {
+    TriShading sh;
+    const bool has = LoadTriShading(S, prim, &sh);
+    return TriangleSurface(p0, p1, p2, b0, b1, b2, S.primFlip[prim], has ? &sh : nullptr);
+}
+
+__device__ inline float TriArea(V3 p0, V3 p1, V3 p2) { return 0.5f * Length(Cross(p1 - p0, p2 - p0)); }
+
+__device__ inline float SolidAngleOf(V3 p0, V3 p1, V3 p2, V3 p) {
+    return SphericalTriangleArea(Normalize(p0 - p), Normalize(p1 - p), Normalize(p2 - p));
+}
+
+// Triangle::Sample(ctx, u) (shapes.h:1053-1130); returns false for {}
+__device__ inline bool SampleTriangle(V3 p0, V3 p1, V3 p2, bool flip, const TriShading *sh, V3 refP, V3 refN,
+                                      V3 refNs, float u0, float u1, V3 *ps, V3 *pErr, V3 *ns, float *pdfOut) {
+    (void)refN;
+    float solidAngle = SolidAngleOf(p0, p1, p2, refP);
+    if (solidAngle < kMinSphericalSampleArea || solidAngle > kMaxSphericalSampleArea) {
+        float b[3];
+        SampleUniformTriangle(u0, u1, b);
+        V3 p = b[0] * p0 + b[1] * p1 + b[2] * p2;
+        V3 n = TriangleSampleNormal(p0, p1, p2, b[0], b[1], flip, sh);
+        V3 pAbsSum = Abs(b[0] * p0) + Abs(b[1] * p1) + Abs((1 - b[0] - b[1]) * p2);
+        ToPoint3fi(p, gamma(6) * pAbsSum, &p, pErr);
+        float pdf = 1 / TriArea(p0, p1, p2);
+        V3 wi = p - refP;
+        if (LengthSquared(wi) == 0) return false;
+        wi = Normalize(wi);
+        pdf /= AbsDotN(n, -wi) / DistanceSquared(refP, p);
+        if (isinf(pdf)) return false;
+        *ps = p;
+        *ns = n;
+        *pdfOut = pdf;
+        return true;
+    }
+    float pdf = 1;
+    if (refNs != V3(0, 0, 0)) {
+        V3 wi0 = Normalize(p0 - refP), wi1 = Normalize(p1 - refP), wi2 = Normalize(p2 - refP);
+        float w[4] = {fmaxf(0.01f, AbsDotN(refNs, wi1)), fmaxf(0.01f, AbsDotN(refNs, wi1)),
+                      fmaxf(0.01f, AbsDotN(refNs, wi0)), fmaxf(0.01f, AbsDotN(refNs, wi2))};
+        float px, py;
+        SampleBilinear(u0, u1, w, &px, &py);
+        u0 = px;
+        u1 = py;
+        pdf = BilinearPDF(u0, u1, w);
+    }
+    float triPDF;
+    float b[3];
+    {
+        const SphTriSample r = SampleSphericalTriangle(p0, p1, p2, refP, u0, u1);
+        b[0] = r.b0;
+        b[1] = r.b1;
+        b[2] = r.b2;
+        triPDF = r.pdf;
+    }
+    if (triPDF == 0) return false;
+    pdf *= triPDF;
+    V3 pAbsSum = Abs(b[0] * p0) + Abs(b[1] * p1) + Abs((1 - b[0] - b[1]) * p2);
+    V3 p;
+    ToPoint3fi(b[0] * p0 + b[1] * p1 + b[2] * p2, gamma(6) * pAbsSum, &p, pErr);
+    V3 n = TriangleSampleNormal(p0, p1, p2, b[0], b[1], flip, sh);
+    *ps = p;
+    *ns = n;
+    *pdfOut = pdf;
+    return true;
+}
+
+// Triangle::PDF(ctx, wi) (shapes.h:1133-1174)
+__device__ inline float TrianglePDF(V3 p0, V3 p1, V3 p2, bool flip, const TriShading *sh, V3 refP, V3 refPErr,
+                                   V3 refN, V3 refNs, V3 wi) {
+    float solidAngle = SolidAngleOf(p0, p1, p2, refP);
+    if (solidAngle < kMinSphericalSampleArea || solidAngle > kMaxSphericalSampleArea) {
+        // ShapeSampleContext::SpawnRay(wi) then Triangle::Intersect
+        V3 o = OffsetRayOrigin(refP, refPErr, refN, wi);
+        TriHit h;
+        if (!IntersectTriangle(o, wi, kInfinity, p0, p1, p2, &h)) return 0;
+        TriSurface hs = TriangleSurface(p0, p1, p2, h.b0, h.b1, h.b2, flip, sh);
+        V3 pHit = hs.p, n = hs.n;
+        float pdf = (1 / TriArea(p0, p1, p2)) / (AbsDotN(n, -wi) / DistanceSquared(refP, pHit));
+        if (isinf(pdf)) pdf = 0;
+        return pdf;
+    }
+    float pdf = 1 / solidAngle;
+    if (refNs != V3(0, 0, 0)) {
+        float u0, u1;
+        const SphTriUV uv = InvertSphericalTriangleSample(p0, p1, p2, refP, wi);
+        u0 = uv.u0;
+        u1 = uv.u1;
+        V3 wi0 = Normalize(p0 - refP), wi1 = Normalize(p1 - refP), wi2 = Normalize(p2 - refP);
+        float w[4] = {fmaxf(0.01f, AbsDotN(refNs, wi1)), fmaxf(0.01f, AbsDotN(refNs, wi1)),
+                      fmaxf(0.01f, AbsDotN(refNs, wi0)), fmaxf(0.01f, AbsDotN(refNs, wi2))};
+        pdf *= BilinearPDF(u0, u1, w);
+    }
+    return pdf;
+}
+
+// BVHLightSampler::Sample / PMF (lightsamplers.h:266-403) and UniformLightSampler
+// light index convention: [0, nAreaLights) area lights, then infinite lights.
+__device__ inline bool SampleLight(const DeviceScene &S, V3 p, V3 ns, float u, int *light, float *pmfOut) {
+    int nAll = S.nAreaLights + S.nInfinite;
+    if (S.uniformLightSampler) {
+        if (nAll == 0) return false;
+        int li = min((int)(u * nAll), nAll - 1);
+        *light = li;
+        *pmfOut = 1.f / nAll;
+        return true;
+    }
+    float pInfinite = float(S.nInfinite) / float(S.nInfinite + (S.nLightNodes == 0 ? 0 : 1));
+    if (u < pInfinite) {
+        u /= pInfinite;
+        int index = min((int)(u * S.nInfinite), S.nInfinite - 1);
+        *pmfOut = pInfinite / S.nInfinite;
+        *light = S.nAreaLights + index;
+        return true;
+    }
+    if (S.nLightNodes == 0) return false;
+    u = fminf((u - pInfinite) / (1 - pInfinite), kOneMinusEpsilon);
+    int nodeIndex = 0;
+    float pmf = 1 - pInfinite;
+    for (int iter = 0; iter < 4 * kMaxLightBVHDepth; ++iter) {
+        DeviceLightNode node = S.lightNodes[nodeIndex];
+        if (!node.isLeaf) {
+            float c0 = LightImportance(S.lightNodes[nodeIndex + 1].b, p, ns);
+            float c1 = LightImportance(S.lightNodes[node.childOrLight].b, p, ns);
+            if (c0 == 0 && c1 == 0) return false;
+            float nodePMF;
+            int child = SampleDiscrete2(c0, c1, u, &nodePMF, &u);
+            pmf *= nodePMF;
+            nodeIndex = (child == 0) ? (nodeIndex + 1) : node.childOrLight;
+        } else {
+            if (nodeIndex > 0 || LightImportance(node.b, p, ns) > 0) {
+                *light = node.childOrLight;
+                *pmfOut = pmf;
+                return true;
+            }
+            return false;
+        }
+    }
+    return false;
+}
+
+__device__ inline float LightPMF(const DeviceScene &S, V3 p, V3 ns, int light) {
+    int nAll = S.nAreaLights + S.nInfinite;
+    if (S.uniformLightSampler) return nAll ? 1.f / nAll : 0.f;
+    uint32_t bitTrail = light < S.nAreaLights ? S.lightBitTrail[light] : 0xffffffffu;
+    if (bitTrail == 0xffffffffu) return 1.f / (S.nInfinite + (S.nLightNodes == 0 ? 0 : 1));
+    float pInfinite = float(S.nInfinite) / float(S.nInfinite + (S.nLightNodes == 0 ? 0 : 1));
+    float pmf = 1 - pInfinite;
+    int nodeIndex = 0;
+    for (int iter = 0; iter < kMaxLightBVHDepth; ++iter) {
+        const DeviceLightNode &node = S.lightNodes[nodeIndex];
+        if (node.isLeaf) return pmf;
+        float c0 = LightImportance(S.lightNodes[nodeIndex + 1].b, p, ns);
+        float c1 = LightImportance(S.lightNodes[node.childOrLight].b, p, ns);
+        pmf *= ((bitTrail & 1) ? c1 : c0) / (c0 + c1);
+        nodeIndex = (bitTrail & 1) ? node.childOrLight : (nodeIndex + 1);
+        bitTrail >>= 1;
+    }
+    return pmf;
+}
+
+
+// Streaming form of the per-wavelength work: lambda_i, R_i, Le_i and beta_i are produced
+// inside each 31-iteration loop (lambda by pbrt's sequential +10 nm recurrence, R by the
+// sigmoid polynomial, beta re-read from the wavelength-major SoA through L1/L2) instead of
+// being held in 31-entry register arrays, which keeps the kernel at a few waves per SIMD.
+struct SpectralIter {
+    float lam;
+    int i;
+    __device__ SpectralIter(float l0) : lam(l0), i(0) {}
+    __device__ void Next() {
+        lam = lam + (kLambdaMax - kLambdaMin) / kNSpectrumSamples;
+        if (lam > kLambdaMax) lam = kLambdaMin + (lam - kLambdaMax);
+        ++i;
+    }
+};
+
+__device__ inline float Reflectance(float4 mc, bool constant, float lambda) {
+    float r = constant ? mc.w : SigmoidPolynomial(mc.x, mc.y, mc.z, lambda);
+    return Clampf(r, 0, 1);
+}
+
+// ToSensorRGB accumulation for one wavelength: sx += xbar * (c / pdf) (film.h:95-100)
+// Film-only arithmetic (the contribution c and its 1/pdf, 1/denom scalings) uses reciprocal
+// multiplies where the reference divides: at most an ulp or two per term in the pixel sums,
+// and nothing that steers a path (beta, pdfs and RR keep the reference's exact operations).
+struct SensorAcc {
+    float sx = 0, sy = 0, sz = 0;
+    __device__ void Add(const DeviceScene &S, int off, float c, bool first) { Add(S.sensor4, off, c, first); }
+    template <typename F4>
+    __device__ void Add(const F4 *sensor4, int off, float c, bool first) {
+        float v = c * kInvWavelengthPDF;
+        float4 sb = off < 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : float4(sensor4[off]);
+        float xb = sb.x, yb = sb.y, zb = sb.z;
+        sx = first ? xb * v : sx + xb * v;
+        sy = first ? yb * v : sy + yb * v;
+        sz = first ? zb * v : sz + zb * v;
+    }
+};
+
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef __attribute__((address_space(3))) const float LdsF;
+typedef __attribute__((address_space(3))) const uint16_t LdsU16;
+#else
+typedef const float LdsF;
+typedef const uint16_t LdsU16;
+#endif
+
+// GenerateCameraRays (wavefront/camera.cpp:31-80) for one pixel-sample slot: the first
+// wavelength, and the render-space camera ray (PerspectiveCamera::GenerateRay,
+// cameras.cpp:433-456, then CameraBase::RenderFromCamera).
+__device__ inline void GenerateCameraRay(const DeviceScene &S, const PathState &st, int slot, float *lambda0Out,
+                                         V3 *oOut, V3 *dOut) {
+    int px, py, sampleIndex;
+    PixelOf(st, slot, &px, &py, &sampleIndex);
+    px += S.px0;
+    // camera.cpp:50-62: wavelength Get1D, then GetCameraSample (samplers.h:797-813): pixel
+    // offset (GetPixel2D) through the box filter (filters.h:67-71), time Get1D, lens Get2D
+    float lu, pix0, pix1, l0, l1;
+    if (S.samplerType == 1) {
+        // ZSobolSampler: dimensions 0 (wavelength), 1-2 (pixel), 3 (time), 4-5 (lens)
+        const uint64_t morton = ZSobolMortonIndex(S.zs, px, py, sampleIndex);
+        lu = ZSobolGet1D(S.zs, morton, 0, S.zsPerms, S.sobolM1);
+        ZSobolGet2D(S.zs, morton, 1, S.zsPerms, S.sobolM1, &pix0, &pix1);
+        ZSobolGet2D(S.zs, morton, 4, S.zsPerms, S.sobolM1, &l0, &l1);
+    } else {
+        // HaltonSampler: GetPixel2D reads the pixel's own Halton digits, not a dimension
+        Halton h = StartPixelSample(S, px, py, sampleIndex, 0);
+        lu = Get1D(S, h);
+        const uint64_t a0 = h.index >> S.baseExponents[0];
+        const uint64_t a1 = (h.index >> 32) == 0 ? (uint64_t)((uint32_t)h.index / (uint32_t)S.baseScales[1])
+                                                 : h.index / (uint64_t)S.baseScales[1];
+        pix0 = a0 < (1ull << 30) ? RadicalInverse32<2>((uint32_t)a0) : RadicalInverse(2, a0);
+        pix1 = a1 < (1ull << 30) ? RadicalInverse32<3>((uint32_t)a1) : RadicalInverse(3, a1);
+        (void)Get1D(S, h);  // time (unused: static camera)
+        Get2D(S, h, &l0, &l1);
+    }
+    float lambda0 = Lerpf(lu, kLambdaMin, kLambdaMax);
+    float fx = Lerpf(pix0, -S.filterRadiusX, S.filterRadiusX), fy = Lerpf(pix1, -S.filterRadiusY, S.filterRadiusY);
+    float pFilmX = px + fx + 0.5f, pFilmY = py + fy + 0.5f;
+    // PerspectiveCamera::GenerateRay (cameras.cpp:433-456)
+    V3 pCamera = XfPoint(S.cameraFromRaster, V3(pFilmX, pFilmY, 0));
+    V3 o(0, 0, 0), d = Normalize(pCamera);
+    if (S.lensRadius > 0) {
+        float lx, ly;
+        SampleUniformDiskConcentric(l0, l1, &lx, &ly);
+        lx *= S.lensRadius;
+        ly *= S.lensRadius;
+        float ft = S.focalDistance / d.z;
+        V3 pFocus = o + d * ft;
+        o = V3(lx, ly, 0);
+        d = Normalize(pFocus - o);
+    }
+    // CameraBase::RenderFromCamera(ray): Transform::operator()(Ray) with origin error offset
+    {
+        const float *m = S.renderFromCamera;
+        V3 oo = XfPoint(m, o);
+        V3 err;
+        if (o == V3(0, 0, 0))
+            err = gamma(3) * Abs(V3(m[3], m[7], m[11]));
+        else
+            err = gamma(3) * (Abs(V3(m[0] * o.x, m[4] * o.x, m[8] * o.x)) + Abs(V3(m[1] * o.y, m[5] * o.y, m[9] * o.y)) +
+                              Abs(V3(m[2] * o.z, m[6] * o.z, m[10] * o.z)) + Abs(V3(m[3], m[7], m[11])));
+        V3 dd = XfVector(m, d);
+        float l2 = LengthSquared(dd);
+        if (l2 > 0) {
+            float dt = Dot(Abs(dd), err) / l2;
+            oo = oo + dd * dt;
+        }
+        o = oo;
+        d = dd;
+    }
+    *lambda0Out = lambda0;
+    *oOut = o;
+    *dOut = d;
+}
+
+}  // namespace pbrt_amd

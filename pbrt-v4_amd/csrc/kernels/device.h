@@ -67,6 +67,23 @@ constexpr int kLdsNodeStride = 17;  // float4 per LDS-cached wide node (68 dword
 constexpr int kLdsQNodeStride = 5;  // float4 per LDS-cached compressed node (20 dwords: conflict-free)
 PHD int LdsNodeStride(int compressed) { return compressed ? kLdsQNodeStride : kLdsNodeStride; }
 
+// Participating media (MakeNamedMedium homogeneous / uniformgrid), as the flat tables of
+// pbrt_scene_flat::medium_* (capi.hip MediumTables): per medium 16 ints (type, sigma_a, sigma_s,
+// Le dense-spectrum ids, emissive, density nx ny nz, LeScale nx ny nz, value offsets of the
+// density / LeScale / 16^3 majorant grids) and 24 floats (g, bounds lo hi, pad,
+// mediumFromRender 4x4).  primMedium: {inside, outside} per leaf-order triangle (-1 = none),
+// nullptr when no triangle is a medium boundary.
+constexpr int kDevMediumGrid = 1;  // info[0] (scene.h MediumType)
+constexpr int kMajorantRes = 16;
+struct DeviceMedia {
+    int n;             // media in the scene (0: the surface-only kernels run)
+    int cameraMedium;  // medium the camera sits in, or -1
+    const int *info;
+    const float *params;
+    const float *values;
+    const int *primMedium;
+};
+
 struct DeviceScene {
     // geometry (leaf order)
     const BVH8Node *nodes;
@@ -144,6 +161,7 @@ struct DeviceScene {
     int stackSize;  // BVH traversal stack entries per lane (BVH8::maxStack)
     int ldsNodes, ldsTris;  // BVH8 nodes / triangles cached in LDS by the traversal kernels
     ShadeLdsLayout shadeLds;
+    DeviceMedia media;
 };
 
 // One depth's path records, compacted: record i is the i-th ray of that depth (pbrt's
@@ -189,6 +207,34 @@ struct PathState {
     int *counters;      // [CounterIndex(maxDepth + 2, 0, 0)]: per depth, queue and shard
     double *film;       // [4][xres*yres]: rgbSum[3], weightSum (sensor RGB)
     unsigned long long *stats;  // [kStatsSlots]
+};
+
+// Path records of the participating-media wavefront (volpath.hip), one per ray of a wavefront
+// iteration, double-buffered by iteration parity.  With media r_u and r_l are spectral
+// (SampleT_maj's T_maj / T_maj[0] ratios differ per wavelength), the path depth may lag the
+// iteration (an interface crossing continues at the same depth, integrator.cpp:374 and
+// media.cpp:196-203), each ray carries its medium, and the MIS context of the previous vertex
+// is stored (a medium scattering vertex has no surface to rebuild it from).
+struct VolRecords {
+    float *beta, *ru, *rl;     // [31][NR] wavelength-major
+    float *ray;                // [6][NR] o, d
+    float *prev;               // [12][NR] prevIntrCtx: p, pErr, n, ns
+    float *lambda0, *etaScale; // [NR]
+    int *flags;                // [NR] bit0 specularBounce, bit1 anyNonSpecularBounces
+    int *pixel, *depth, *medium;
+};
+// queues of one iteration (counters at CounterIndex(iteration, queue, shard))
+constexpr int kVRay = 0, kVSurf = 1, kVShadow = 2, kVMed = 3, kVScat = 4;
+struct VolState {
+    VolRecords rec[2];
+    int *hitPrim;  // [NR] this iteration's closest hit (-1: none)
+    float *hitB;   // [4][NR] b0 b1 b2 t; a medium scattering event stores its point in b0..b2
+    int *medQ, *surfQ, *scatQ;  // record indices
+    // shadow rays (ShadowRayWorkItem with spectral Ld, r_u, r_l), compacted
+    float *shRay;              // [6][NR] o, d (d unnormalised, tMax = 1 - ShadowEpsilon)
+    float *shLd, *shRu, *shRl; // [31][NR]
+    float *shLambda0;          // [NR]
+    int *shPixel, *shMedium;   // [NR]
 };
 
 }  // namespace pbrt_amd

@@ -1,0 +1,1173 @@
+// MI355X wavefront kernels for scenes with participating media: pbrt's
+// WavefrontPathIntegrator with haveMedia (wavefront/integrator.cpp:290-493).
+//
+// Stage <-> reference mapping (one launch each per wavefront iteration):
+//   k_vcamera    GenerateCameraRays (camera.cpp:31-80) + the camera medium
+//   k_vclosest   IntersectClosest (integrator.h:39-45): closest hit; rays inside a medium go to
+//                the medium-sample queue (MediumSampleQueue, intersect.h:48-80), the rest to
+//                the surface queue
+//   k_vmedium    SampleMediumInteraction (media.cpp:22-247): delta tracking along the ray
+//                through SampleT_maj (media.h:725-800) with the homogeneous / DDA majorant
+//                iterators (media.h:79-205), medium emission, absorption / real scattering /
+//                null scattering; survivors continue to the surface queue
+//   k_vsurface   the surface side: HandleEscapedRays (integrator.cpp:495-537), interface
+//                crossings (media.cpp:193-203), HandleEmissiveIntersection (:539-573) and
+//                EvaluateMaterialAndBSDF (surfscatter.cpp:57-328) for every material type
+//   k_vscatter   SampleMediumScattering<HGPhaseFunction> (media.cpp:259-352)
+//   k_vshadow    TraceTransmittance (intersect.h:164-274): shadow rays through interfaces with
+//                ratio tracking in each medium they cross
+// Film: k_film of wavefront.hip (the same per-slot sensor-RGB L).
+//
+// Records are keyed by their index in the iteration's ray queue; every queue is sharded like
+// the surface path's (device.h kShards).  Spectral state (beta, r_u, r_l, T_maj) lives in
+// registers inside a kernel and wavelength-major in HBM between kernels.
+#define PBRT_AMD_CR_MATH 1  // correctly rounded transcendentals (core.h): bit-identical to the oracle
+#include "common.h"
+
+namespace pbrt_amd {
+
+#ifndef PBRT_VOL_WAVES
+#define PBRT_VOL_WAVES 2  // waves/SIMD the spectral media kernels are compiled for
+#endif
+constexpr int kNS = kNSpectrumSamples;
+
+// ------------------------------------------------------------------ media
+struct MediumRef {
+    const int *I;    // 16 ints (device.h DeviceMedia)
+    const float *P;  // 24 floats
+};
+__device__ inline MediumRef MediumAt(const DeviceScene &S, int m) {
+    return MediumRef{S.media.info + 16 * m, S.media.params + 24 * m};
+}
+__device__ inline float DenseAt(const DeviceScene &S, int idx, int off) {
+    return off < 0 ? 0.f : S.dense[idx * kDenseN + off];
+}
+
+// Transform::ApplyInverse(Point3f) (util/transform.h:387-398) with mediumFromRender
+__device__ inline V3 MediumFromRender(const float *M, V3 p) {
+    const float x = (M[0] * p.x + M[1] * p.y) + (M[2] * p.z + M[3]);
+    const float y = (M[4] * p.x + M[5] * p.y) + (M[6] * p.z + M[7]);
+    const float z = (M[8] * p.x + M[9] * p.y) + (M[10] * p.z + M[11]);
+    const float w = (M[12] * p.x + M[13] * p.y) + (M[14] * p.z + M[15]);
+    if (w == 1) return V3(x, y, z);
+    return V3(x, y, z) / w;
+}
+// Bounds3::Offset (util/vecmath.h:1325-1334), bounds = P[1..3], P[4..6]
+__device__ inline V3 BoundsOffset(const float *P, V3 p) {
+    V3 o(p.x - P[1], p.y - P[2], p.z - P[3]);
+    if (P[4] > P[1]) o.x /= P[4] - P[1];
+    if (P[5] > P[2]) o.y /= P[5] - P[2];
+    if (P[6] > P[3]) o.z /= P[6] - P[3];
+    return o;
+}
+// SampledGrid<Float>::Lookup(Point3f) (util/containers.h:804-835): trilinear, zero outside
+__device__ inline float GridLookup(const float *v, int nx, int ny, int nz, V3 p) {
+    const float sx = p.x * nx - .5f, sy = p.y * ny - .5f, sz = p.z * nz - .5f;
+    const int ix = (int)floorf(sx), iy = (int)floorf(sy), iz = (int)floorf(sz);
+    const float dx = sx - ix, dy = sy - iy, dz = sz - iz;
+    auto at = [&](int x, int y, int z) -> float {
+        if (x < 0 || x >= nx || y < 0 || y >= ny || z < 0 || z >= nz) return 0.f;
+        return v[((size_t)z * ny + y) * nx + x];
+    };
+    const float d00 = Lerpf(dx, at(ix, iy, iz), at(ix + 1, iy, iz));
+    const float d10 = Lerpf(dx, at(ix, iy + 1, iz), at(ix + 1, iy + 1, iz));
+    const float d01 = Lerpf(dx, at(ix, iy, iz + 1), at(ix + 1, iy, iz + 1));
+    const float d11 = Lerpf(dx, at(ix, iy + 1, iz + 1), at(ix + 1, iy + 1, iz + 1));
+    return Lerpf(dz, Lerpf(dy, d00, d10), Lerpf(dy, d01, d11));
+}
+
+// Medium::SamplePoint (media.h:209-350) reduced to its scalars: sigma_a = dense(I[1]) * d,
+// sigma_s = dense(I[2]) * d, Le = dense(I[3]) * le (le = 0: no emission at p).  Homogeneous:
+// d = le = 1 (x * 1 is exact, so the spectra are the reference's).
+struct MediumPoint {
+    float d, le;
+};
+__device__ inline MediumPoint SampleMediumPoint(const DeviceScene &S, const MediumRef &m, V3 p) {
+    if (m.I[0] != kDevMediumGrid) return MediumPoint{1.f, 1.f};
+    const V3 q = BoundsOffset(m.P, MediumFromRender(m.P + 8, p));
+    MediumPoint r;
+    r.d = GridLookup(S.media.values + m.I[11], m.I[5], m.I[6], m.I[7], q);
+    r.le = 0.f;
+    if (m.I[4]) {
+        const float scale = GridLookup(S.media.values + m.I[12], m.I[8], m.I[9], m.I[10], q);
+        if (scale > 0) r.le = scale;
+    }
+    return r;
+}
+
+// Majorant segments of a ray (HomogeneousMajorantIterator, media.h:79-102, and
+// DDAMajorantIterator over the 16^3 majorant grid, media.h:136-205).  A segment's majorant is
+// sigma_t(lambda) * mx: the iterator yields the scalar mx (1 for a homogeneous medium).
+struct MajorantIter {
+    bool dda, called, empty;
+    float tMin, tMax;
+    float nextCrossingT[3], deltaT[3];
+    int step[3], voxelLimit[3], voxel[3];
+    const float *grid;
+    __device__ bool Next(float *segMin, float *segMax, float *mx) {
+        if (!dda) {
+            if (called || empty) return false;
+            called = true;
+            *segMin = 0;
+            *segMax = tMax;
+            *mx = 1.f;
+            return true;
+        }
+        if (empty || tMin >= tMax) return false;
+        const int bits = ((nextCrossingT[0] < nextCrossingT[1]) << 2) + ((nextCrossingT[0] < nextCrossingT[2]) << 1) +
+                         ((nextCrossingT[1] < nextCrossingT[2]));
+        // cmpToAxis[8] = {2, 1, 2, 1, 2, 2, 0, 0} as a 2-bit table
+        const int stepAxis = (0x0A66 >> (2 * bits)) & 3;
+        const float nct = stepAxis == 0 ? nextCrossingT[0] : (stepAxis == 1 ? nextCrossingT[1] : nextCrossingT[2]);
+        const float tVoxelExit = fminf(tMax, nct);
+        *mx = grid[voxel[0] + kMajorantRes * (voxel[1] + kMajorantRes * voxel[2])];
+        *segMin = tMin;
+        *segMax = tVoxelExit;
+        tMin = tVoxelExit;
+        if (nct > tMax) tMin = tMax;
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+            if (a == stepAxis) {
+                voxel[a] += step[a];
+                if (voxel[a] == voxelLimit[a]) tMin = tMax;
+                nextCrossingT[a] += deltaT[a];
+            }
+        return true;
+    }
+};
+
+// Medium::SampleRay (media.h:240-250 homogeneous, :319-333 grid) for a ray with a normalised
+// direction and render-space tMax
+__device__ inline MajorantIter SampleMediumRay(const DeviceScene &S, const MediumRef &m, V3 o, V3 d, float raytMax) {
+    MajorantIter it;
+    it.called = false;
+    it.empty = false;
+    it.grid = nullptr;
+    if (m.I[0] != kDevMediumGrid) {
+        it.dda = false;
+        it.tMax = raytMax;
+        return it;
+    }
+    it.dda = true;
+    // Transform::ApplyInverse(Ray, &tMax) (util/transform.h:416-429): the exact origin becomes a
+    // Point3fi (transform.cpp:263-303), is pushed to the edge of its error bounds along d
+    const float *M = m.P + 8;
+    const float xp = (M[0] * o.x + M[1] * o.y) + (M[2] * o.z + M[3]);
+    const float yp = (M[4] * o.x + M[5] * o.y) + (M[6] * o.z + M[7]);
+    const float zp = (M[8] * o.x + M[9] * o.y) + (M[10] * o.z + M[11]);
+    const V3 err(gamma(3) * (fabsf(M[0] * o.x) + fabsf(M[1] * o.y) + fabsf(M[2] * o.z)),
+                 gamma(3) * (fabsf(M[4] * o.x) + fabsf(M[5] * o.y) + fabsf(M[6] * o.z)),
+                 gamma(3) * (fabsf(M[8] * o.x) + fabsf(M[9] * o.y) + fabsf(M[10] * o.z)));
+    float lo[3], hi[3];
+    const float pc[3] = {xp, yp, zp}, pe[3] = {err.x, err.y, err.z};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = pe[a] == 0 ? pc[a] : NextFloatDown(pc[a] - pe[a]);
+        hi[a] = pe[a] == 0 ? pc[a] : NextFloatUp(pc[a] + pe[a]);
+    }
+    const V3 dm(M[0] * d.x + M[1] * d.y + M[2] * d.z, M[4] * d.x + M[5] * d.y + M[6] * d.z,
+                M[8] * d.x + M[9] * d.y + M[10] * d.z);
+    const float l2 = LengthSquared(dm);
+    if (l2 > 0) {
+        const V3 oErr((hi[0] - lo[0]) / 2, (hi[1] - lo[1]) / 2, (hi[2] - lo[2]) / 2);
+        const float dt = Dot(Abs(dm), oErr) / l2;
+        const float dv[3] = {dm.x * dt, dm.y * dt, dm.z * dt};
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = NextFloatDown(lo[a] + dv[a]);
+            hi[a] = NextFloatUp(hi[a] + dv[a]);
+        }
+        raytMax -= dt;
+    }
+    const float om[3] = {(lo[0] + hi[0]) / 2, (lo[1] + hi[1]) / 2, (lo[2] + hi[2]) / 2};
+    const float dmv[3] = {dm.x, dm.y, dm.z};
+    // Bounds3::IntersectP(o, d, tMax, &t0, &t1) (util/vecmath.h:1549-1573)
+    const float *P = m.P;
+    float t0 = 0, t1 = raytMax;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float inv = 1 / dmv[a];
+        float tNear = (P[1 + a] - om[a]) * inv, tFar = (P[4 + a] - om[a]) * inv;
+        if (tNear > tFar) {
+            const float t = tNear;
+            tNear = tFar;
+            tFar = t;
+        }
+        tFar *= 1 + 2 * gamma(3);
+        t0 = tNear > t0 ? tNear : t0;
+        t1 = tFar < t1 ? tFar : t1;
+        if (t0 > t1) it.empty = true;
+    }
+    if (it.empty) return it;
+    // DDAMajorantIterator ctor (media.h:140-166)
+    it.grid = S.media.values + m.I[13];
+    it.tMin = t0;
+    it.tMax = t1;
+    const float diag[3] = {P[4] - P[1], P[5] - P[2], P[6] - P[3]};
+    const V3 og = BoundsOffset(P, V3(om[0], om[1], om[2]));
+    const float ogv[3] = {og.x, og.y, og.z};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        float dg = dmv[a] / diag[a];
+        const float gi = ogv[a] + dg * t0;
+        it.voxel[a] = (int)Clampf(gi * kMajorantRes, 0, kMajorantRes - 1);
+        it.deltaT[a] = 1 / (fabsf(dg) * kMajorantRes);
+        if (dg == -0.f) dg = 0.f;
+        if (dg >= 0) {
+            const float next = float(it.voxel[a] + 1) / kMajorantRes;
+            it.nextCrossingT[a] = t0 + (next - gi) / dg;
+            it.step[a] = 1;
+            it.voxelLimit[a] = kMajorantRes;
+        } else {
+            const float next = float(it.voxel[a]) / kMajorantRes;
+            it.nextCrossingT[a] = t0 + (next - gi) / dg;
+            it.step[a] = -1;
+            it.voxelLimit[a] = -1;
+        }
+    }
+    return it;
+}
+
+// Per-wavelength offsets into the dense tables for a path's 31 wavelengths
+// (SampledWavelengths::SampleUniform's +10 nm recurrence, util/spectrum.h:318-336)
+struct WaveOffsets {
+    int off[kNS];
+    __device__ explicit WaveOffsets(float lambda0) {
+        SpectralIter it(lambda0);
+#pragma unroll
+        for (int i = 0; i < kNS; ++i, it.Next()) off[i] = DenseOffset(it.lam);
+    }
+};
+
+__device__ inline float AvgArr(const float *a) {
+    float s = a[0];
+#pragma unroll
+    for (int i = 1; i < kNS; ++i) s += a[i];
+    return s / kNS;
+}
+__device__ inline bool AnyNonZero(const float *a) {
+    bool nz = false;
+#pragma unroll
+    for (int i = 0; i < kNS; ++i) nz |= a[i] != 0;
+    return nz;
+}
+
+// SampleT_maj<ConcreteMedium> (media.h:737-800).  `event(p, mp, mx, Tm)` is the callback:
+// sigma_maj_i = (sigma_a_i + sigma_s_i) * mx; returns false to stop.  Returns true when the
+// traversal ran to the end (T_maj = Tm then) and false when the callback stopped it
+// (SampleT_maj returns SampledSpectrum(1) then).
+template <typename F>
+__device__ inline bool SampleTmaj(const DeviceScene &S, const MediumRef &m, const WaveOffsets &wo, V3 o, V3 d,
+                                  float tMax, float u, PCG32 &rng, float Tm[kNS], F &&event) {
+    tMax *= Length(d);
+    d = Normalize(d);
+    MajorantIter iter = SampleMediumRay(S, m, o, d, tMax);
+#pragma unroll
+    for (int i = 0; i < kNS; ++i) Tm[i] = 1.f;
+    const int sa = m.I[1], ss = m.I[2];
+    const float st0 = DenseAt(S, sa, wo.off[0]) + DenseAt(S, ss, wo.off[0]);
+    float segMin, segMax, mx;
+    while (iter.Next(&segMin, &segMax, &mx)) {
+        const float smaj0 = st0 * mx;
+        if (smaj0 == 0) {
+            float dt = segMax - segMin;
+            if (isinf(dt)) dt = 3.402823466e+38f;
+#pragma unroll
+            for (int i = 0; i < kNS; ++i) {
+                const float smaj = (DenseAt(S, sa, wo.off[i]) + DenseAt(S, ss, wo.off[i])) * mx;
+                Tm[i] *= FastExp(smaj * -dt);
+            }
+            continue;
+        }
+        float tMin = segMin;
+        while (true) {
+            const float t = tMin + SampleExponential(u, smaj0);
+            u = rng.Uniform();
+            if (t < segMax) {
+#pragma unroll
+                for (int i = 0; i < kNS; ++i) {
+                    const float smaj = (DenseAt(S, sa, wo.off[i]) + DenseAt(S, ss, wo.off[i])) * mx;
+                    Tm[i] *= FastExp(smaj * -(t - tMin));
+                }
+                const V3 p = o + d * t;
+                const MediumPoint mp = SampleMediumPoint(S, m, p);
+                if (!event(p, mp, mx, Tm)) return false;
+#pragma unroll
+                for (int i = 0; i < kNS; ++i) Tm[i] = 1.f;
+                tMin = t;
+            } else {
+                float dt = segMax - tMin;
+                if (isinf(dt)) dt = 3.402823466e+38f;
+#pragma unroll
+                for (int i = 0; i < kNS; ++i) {
+                    const float smaj = (DenseAt(S, sa, wo.off[i]) + DenseAt(S, ss, wo.off[i])) * mx;
+                    Tm[i] *= FastExp(smaj * -dt);
+                }
+                break;
+            }
+        }
+    }
+    return true;
+}
+
+// Spectral contribution c_i (already divided by its MIS denominator) to sensor RGB
+// (PixelSensor::ToSensorRGB, film.h:95-100), added to the slot's L
+template <typename C>
+__device__ inline void AddToL(const DeviceScene &S, const PathState &st, int slot, const WaveOffsets &wo, C &&c) {
+    SensorAcc acc;
+#pragma unroll
+    for (int i = 0; i < kNS; ++i) acc.Add(S, wo.off[i], c(i), i == 0);
+    const int NL = st.N;
+    st.L[slot] += S.imagingRatio * (acc.sx / kNS);
+    st.L[NL + slot] += S.imagingRatio * (acc.sy / kNS);
+    st.L[2 * NL + slot] += S.imagingRatio * (acc.sz / kNS);
+}
+
+// RaySamples of a path depth (samples.cpp:29-66) from the global sampler tables
+struct VRaySamples {
+    float dUc, dU0, dU1, iUc, iU0, iU1, rr;
+};
+__device__ inline VRaySamples RaySamplesAt(const DeviceScene &S, const PathState &st, int slot, int depth) {
+    int px, py, sampleIndex;
+    PixelOf(st, slot, &px, &py, &sampleIndex);
+    px += S.px0;
+    const int d0 = 6 + 7 * depth;
+    VRaySamples r;
+    if (S.samplerType == 1) {
+        const uint64_t morton = ZSobolMortonIndex(S.zs, px, py, sampleIndex);
+        r.dUc = ZSobolGet1D(S.zs, morton, d0, S.zsPerms, S.sobolM1);
+        ZSobolGet2D(S.zs, morton, d0 + 1, S.zsPerms, S.sobolM1, &r.dU0, &r.dU1);
+        r.iUc = ZSobolGet1D(S.zs, morton, d0 + 3, S.zsPerms, S.sobolM1);
+        ZSobolGet2D(S.zs, morton, d0 + 4, S.zsPerms, S.sobolM1, &r.iU0, &r.iU1);
+        r.rr = ZSobolGet1D(S.zs, morton, d0 + 6, S.zsPerms, S.sobolM1);
+    } else {
+        Halton h = StartPixelSample(S, px, py, sampleIndex, d0);
+        r.dUc = Get1D(S, h);
+        Get2D(S, h, &r.dU0, &r.dU1);
+        r.iUc = Get1D(S, h);
+        Get2D(S, h, &r.iU0, &r.iU1);
+        r.rr = Get1D(S, h);
+    }
+    return r;
+}
+
+// Spectral record I/O (wavelength-major)
+__device__ inline void LoadSpec(const float *base, int NR, int ri, float v[kNS]) {
+#pragma unroll
+    for (int i = 0; i < kNS; ++i) v[i] = base[(size_t)i * NR + ri];
+}
+__device__ inline void StoreSpec(float *base, int NR, int ri, const float v[kNS]) {
+#pragma unroll
+    for (int i = 0; i < kNS; ++i) base[(size_t)i * NR + ri] = v[i];
+}
+__device__ inline V3 LoadV3(const float *base, int NR, int ri) {
+    return V3(base[ri], base[NR + ri], base[2 * (size_t)NR + ri]);
+}
+__device__ inline void StoreV3(float *base, int NR, int ri, V3 v) {
+    base[ri] = v.x;
+    base[NR + ri] = v.y;
+    base[2 * (size_t)NR + ri] = v.z;
+}
+
+// Medium on each side of a leaf-order triangle, or the ray's medium when the triangle is no
+// medium boundary (SurfaceInteraction::SetIntersectionProperties, interaction.h:236-248)
+__device__ inline void MediaOf(const DeviceScene &S, int prim, int rayMedium, int *in, int *out) {
+    *in = *out = rayMedium;
+    if (S.media.primMedium) {
+        const int a = S.media.primMedium[2 * prim], b = S.media.primMedium[2 * prim + 1];
+        if (a != b) {
+            *in = a;
+            *out = b;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ kernels
+__global__ void __launch_bounds__(kBlock) k_vcamera(DeviceScene S, PathState st, VolState v, int nActive) {
+    const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot == 0) {
+        st.counters[CounterIndex(0, kVRay, 0)] = nActive;  // iteration-0 records = every slot
+        atomicAdd(&st.stats[0], (unsigned long long)nActive);
+    }
+    if (slot >= nActive) return;
+    float lambda0;
+    V3 o, d;
+    GenerateCameraRay(S, st, slot, &lambda0, &o, &d);
+    const int NR = st.NR, N = st.N;
+    st.L[slot] = 0;
+    st.L[N + slot] = 0;
+    st.L[2 * N + slot] = 0;
+    if (!S.boxFilter) st.filterW[slot] = 1.f;
+    const VolRecords &r = v.rec[0];
+#pragma unroll 8
+    for (int i = 0; i < kNS; ++i) {
+        r.beta[(size_t)i * NR + slot] = 1.f;
+        r.ru[(size_t)i * NR + slot] = 1.f;
+        r.rl[(size_t)i * NR + slot] = 1.f;
+    }
+    StoreV3(r.ray, NR, slot, o);
+    StoreV3(r.ray + 3 * (size_t)NR, NR, slot, d);
+#pragma unroll
+    for (int k = 0; k < 12; ++k) r.prev[(size_t)k * NR + slot] = 0.f;
+    r.lambda0[slot] = lambda0;
+    r.etaScale[slot] = 1.f;
+    r.flags[slot] = 0;
+    r.pixel[slot] = slot;
+    r.depth[slot] = 0;
+    r.medium[slot] = S.media.cameraMedium;
+}
+
+template <bool Q>
+__global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_vclosest(DeviceScene S, PathState st, VolState v,
+                                                                          int wf) {
+    const QueueView rays = LoadQueue(st, wf, kVRay);
+    if ((int)(blockIdx.x * blockDim.x) >= rays.total) return;
+    extern __shared__ float4 dynLds[];
+    const SceneLds L = SetupSceneLds(S, dynLds);
+    const int NR = st.NR;
+    const VolRecords &rec = v.rec[wf & 1];
+    const int shard = ProducerShard();
+    int *medCnt = &st.counters[CounterIndex(wf, kVMed, shard)];
+    int *surfCnt = &st.counters[CounterIndex(wf, kVSurf, shard)];
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&st.stats[1], (unsigned long long)rays.total);
+    for (int base = blockIdx.x * blockDim.x; base < rays.total; base += gridDim.x * blockDim.x) {
+        const int j = base + threadIdx.x;
+        const bool active = j < rays.total;
+        const int ri = active ? QueueSlot(rays, j) : 0;
+        int medium = -1;
+        if (active) {
+            const V3 o = LoadV3(rec.ray, NR, ri), d = LoadV3(rec.ray + 3 * (size_t)NR, NR, ri);
+            TriHit h;
+            const int prim = Traverse<false, Q>(S, L, o, d, kInfinity, &h);
+            v.hitPrim[ri] = prim;
+            v.hitB[ri] = h.b0;
+            v.hitB[NR + ri] = h.b1;
+            v.hitB[2 * NR + ri] = h.b2;
+            v.hitB[3 * NR + ri] = prim >= 0 ? h.t : kInfinity;
+            medium = rec.medium[ri];
+        }
+        // rays inside a medium sample it first (MediumSampleQueue), the rest go to the surface
+        const int pm = WavePush(medCnt, active && medium >= 0);
+        const int ps = WavePush(surfCnt, active && medium < 0);
+        if (pm >= 0) v.medQ[shard * st.capS + pm] = ri;
+        if (ps >= 0) v.surfQ[shard * st.capS + ps] = ri;
+    }
+}
+
+// SampleMediumInteraction (media.cpp:22-247)
+__global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vmedium(DeviceScene S, PathState st, VolState v, int wf) {
+    const QueueView meds = LoadQueue(st, wf, kVMed);
+    const int NR = st.NR;
+    const VolRecords &rec = v.rec[wf & 1];
+    const int shard = ProducerShard();
+    int *surfCnt = &st.counters[CounterIndex(wf, kVSurf, shard)];
+    int *scatCnt = &st.counters[CounterIndex(wf, kVScat, shard)];
+    for (int base = blockIdx.x * blockDim.x; base < meds.total; base += gridDim.x * blockDim.x) {
+        const int j = base + threadIdx.x;
+        const bool active = j < meds.total;
+        const int ri = active ? v.medQ[QueueSlot(meds, j)] : 0;
+        bool toSurf = false, toScat = false;
+        if (active) {
+            const V3 o = LoadV3(rec.ray, NR, ri), d = LoadV3(rec.ray + 3 * (size_t)NR, NR, ri);
+            const float tHit = v.hitB[3 * NR + ri];
+            const int depth = rec.depth[ri], slot = rec.pixel[ri];
+            const MediumRef m = MediumAt(S, rec.medium[ri]);
+            const WaveOffsets wo(rec.lambda0[ri]);
+            float beta[kNS], ru[kNS], rl[kNS], Tm[kNS];
+            LoadSpec(rec.beta, NR, ri, beta);
+            LoadSpec(rec.ru, NR, ri, ru);
+            LoadSpec(rec.rl, NR, ri, rl);
+            PCG32 rng(HashV3F(o, tHit), HashV3(d));
+            const float uDist = rng.Uniform();
+            float uMode = rng.Uniform();
+            bool scattered = false, pushScatter = false;
+            V3 pS(0, 0, 0);
+            float Lx = 0, Ly = 0, Lz = 0;
+            bool emitted = false;
+            const int sa = m.I[1], ss = m.I[2], le = m.I[3];
+            const bool maxD = depth >= S.maxDepth;
+            auto event = [&](V3 p, const MediumPoint &mp, float mx, const float *T) -> bool {
+                const float smaj0 = (DenseAt(S, sa, wo.off[0]) + DenseAt(S, ss, wo.off[0])) * mx;
+                const float sa0 = DenseAt(S, sa, wo.off[0]) * mp.d, ss0 = DenseAt(S, ss, wo.off[0]) * mp.d;
+                // medium emission, scaled by sigma_a / sigma_maj at every event (media.cpp:70-83)
+                if (!maxD && mp.le != 0) {
+                    bool leNz = false;
+#pragma unroll
+                    for (int i = 0; i < kNS; ++i) leNz |= DenseAt(S, le, wo.off[i]) * mp.le != 0;
+                    if (leNz) {
+                        const float pr = smaj0 * T[0];
+                        float re[kNS];
+#pragma unroll
+                        for (int i = 0; i < kNS; ++i) {
+                            const float smaj = (DenseAt(S, sa, wo.off[i]) + DenseAt(S, ss, wo.off[i])) * mx;
+                            re[i] = ru[i] * smaj * T[i] / pr;
+                        }
+                        if (AnyNonZero(re)) {
+                            const float den = pr * AvgArr(re);
+                            SensorAcc acc;
+#pragma unroll
+                            for (int i = 0; i < kNS; ++i) {
+                                const float sai = DenseAt(S, sa, wo.off[i]) * mp.d;
+                                const float Le = DenseAt(S, le, wo.off[i]) * mp.le;
+                                acc.Add(S, wo.off[i], beta[i] * sai * T[i] * Le / den, i == 0);
+                            }
+                            Lx += S.imagingRatio * (acc.sx / kNS);
+                            Ly += S.imagingRatio * (acc.sy / kNS);
+                            Lz += S.imagingRatio * (acc.sz / kNS);
+                            emitted = true;
+                        }
+                    }
+                }
+                const float pAbsorb = sa0 / smaj0, pScatter = ss0 / smaj0;
+                const float pNull = fmaxf(0.f, 1 - pAbsorb - pScatter);
+                const int mode = SampleDiscrete3(pAbsorb, pScatter, pNull, uMode);
+                if (mode == 0) {
+#pragma unroll
+                    for (int i = 0; i < kNS; ++i) beta[i] = 0.f;
+                    return false;
+                }
+                if (mode == 1) {
+                    const float pr = T[0] * ss0;
+#pragma unroll
+                    for (int i = 0; i < kNS; ++i) {
+                        const float f = T[i] * (DenseAt(S, ss, wo.off[i]) * mp.d) / pr;
+                        beta[i] *= f;
+                        ru[i] *= f;
+                    }
+                    pushScatter = AnyNonZero(beta) && AnyNonZero(ru);
+                    pS = p;
+                    scattered = true;
+                    return false;
+                }
+                // null scattering
+                float sn0 = 0;
+                float sn[kNS];
+#pragma unroll
+                for (int i = 0; i < kNS; ++i) {
+                    const float smaj = (DenseAt(S, sa, wo.off[i]) + DenseAt(S, ss, wo.off[i])) * mx;
+                    sn[i] = fmaxf(0.f, smaj - DenseAt(S, sa, wo.off[i]) * mp.d - DenseAt(S, ss, wo.off[i]) * mp.d);
+                }
+                sn0 = sn[0];
+                const float pr = T[0] * sn0;
+#pragma unroll
+                for (int i = 0; i < kNS; ++i) {
+                    const float smaj = (DenseAt(S, sa, wo.off[i]) + DenseAt(S, ss, wo.off[i])) * mx;
+                    const float f = T[i] * sn[i] / pr;
+                    beta[i] = pr == 0 ? 0.f : beta[i] * f;
+                    ru[i] *= f;
+                    rl[i] *= T[i] * smaj / pr;
+                }
+                uMode = rng.Uniform();
+                return AnyNonZero(beta) && AnyNonZero(ru);
+            };
+            const bool ranOut = SampleTmaj(S, m, wo, o, d, tHit, uDist, rng, Tm, event);
+            if (emitted) {
+                st.L[slot] += Lx;
+                st.L[st.N + slot] += Ly;
+                st.L[2 * st.N + slot] += Lz;
+            }
+            if (!scattered && AnyNonZero(beta) && ranOut) {
+                // beta, r_u, r_l *= T_maj / T_maj[0] (a stopped traversal returns T_maj = 1)
+                const float t0 = Tm[0];
+#pragma unroll
+                for (int i = 0; i < kNS; ++i) {
+                    const float f = Tm[i] / t0;
+                    beta[i] *= f;
+                    ru[i] *= f;
+                    rl[i] *= f;
+                }
+            }
+            if (scattered) {
+                if (pushScatter) {
+                    StoreSpec(rec.beta, NR, ri, beta);
+                    StoreSpec(rec.ru, NR, ri, ru);
+                    StoreV3(v.hitB, NR, ri, pS);  // the scattering point replaces the hit
+                    toScat = true;
+                }
+            } else if (AnyNonZero(beta) && AnyNonZero(ru) && depth != S.maxDepth) {
+                StoreSpec(rec.beta, NR, ri, beta);
+                StoreSpec(rec.ru, NR, ri, ru);
+                StoreSpec(rec.rl, NR, ri, rl);
+                toSurf = true;
+            }
+        }
+        const int p0 = WavePush(surfCnt, toSurf);
+        const int p1 = WavePush(scatCnt, toScat);
+        if (p0 >= 0) v.surfQ[shard * st.capS + p0] = ri;
+        if (p1 >= 0) v.scatQ[shard * st.capS + p1] = ri;
+    }
+}
+
+struct ShadowOut {
+    V3 o, d;
+    int medium;
+};
+__device__ inline void WriteShadow(const VolState &v, int NR, int j, const ShadowOut &s, const float *Ld,
+                                   const float *ru, const float *rl, float lambda0, int slot) {
+    StoreV3(v.shRay, NR, j, s.o);
+    StoreV3(v.shRay + 3 * (size_t)NR, NR, j, s.d);
+    StoreSpec(v.shLd, NR, j, Ld);
+    StoreSpec(v.shRu, NR, j, ru);
+    StoreSpec(v.shRl, NR, j, rl);
+    v.shLambda0[j] = lambda0;
+    v.shPixel[j] = slot;
+    v.shMedium[j] = s.medium;
+}
+
+// One area light sample for a reference point (BVHLightSampler::Sample + DiffuseAreaLight::SampleLi
+// with allowIncompletePDF, lights.cpp:743-775): false when no light / no sample / Le = 0
+struct AreaLightSample {
+    int light;
+    V3 p, pErr, n;
+    float pdf;  // shape pdf * light-choice pmf
+};
+__device__ inline bool SampleAreaLight(const DeviceScene &S, V3 refP, V3 refN, V3 refNs, float uc, float u0, float u1,
+                                       const WaveOffsets &wo, AreaLightSample *out, float Le[kNS]) {
+    int li;
+    float lpmf;
+    if (!SampleLight(S, refP, refNs, uc, &li, &lpmf) || li >= S.nAreaLights) return false;
+    const DeviceAreaLight Ld = S.lights[li];
+    const V3 q0(Ld.v0.x, Ld.v0.y, Ld.v0.z), q1(Ld.v1.x, Ld.v1.y, Ld.v1.z), q2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
+    TriShading lsh;
+    const bool lhas = LoadTriShading(S, __float_as_int(Ld.v0.w), &lsh);
+    V3 lp, lpe, ln;
+    float lpdf;
+    if (!SampleTriangle(q0, q1, q2, Ld.flip, lhas ? &lsh : nullptr, refP, refN, refNs, u0, u1, &lp, &lpe, &ln, &lpdf) ||
+        lpdf == 0 || LengthSquared(lp - refP) == 0)
+        return false;
+    const V3 wi = Normalize(lp - refP);
+    bool nz = false;
+    const bool facing = Ld.twoSided || DotN(ln, -wi) >= 0;
+#pragma unroll
+    for (int i = 0; i < kNS; ++i) {
+        Le[i] = facing ? Ld.scale * DenseAt(S, Ld.spectrum, wo.off[i]) : 0.f;
+        nz |= Le[i] != 0;
+    }
+    if (!nz) return false;
+    out->light = li;
+    out->p = lp;
+    out->pErr = lpe;
+    out->n = ln;
+    out->pdf = lpdf * lpmf;
+    return true;
+}
+
+
+// The surface side of an iteration: escaped rays, interfaces, emission, materials.  Queue
+// appends happen where a lane decides to push (WavePush works on the lanes that reach it).
+__global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vsurface(DeviceScene S, PathState st, VolState v, int wf) {
+    const QueueView surf = LoadQueue(st, wf, kVSurf);
+    const int NR = st.NR;
+    const VolRecords &rec = v.rec[wf & 1];
+    const int shard = ProducerShard();
+    const int shardBase = shard * st.capS;
+    int *nextCnt = &st.counters[CounterIndex(wf + 1, kVRay, shard)];
+    int *shadowCnt = &st.counters[CounterIndex(wf, kVShadow, shard)];
+    const bool last = wf == S.maxDepth;
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < surf.total; j += gridDim.x * blockDim.x) {
+        const int ri = v.surfQ[QueueSlot(surf, j)];
+        const float lambda0 = rec.lambda0[ri];
+        const int slot = rec.pixel[ri];
+        const WaveOffsets wo(lambda0);
+        const int depth = rec.depth[ri], flags = rec.flags[ri], medium = rec.medium[ri];
+        const bool specularBounce = flags & 1;
+        float beta[kNS], ru[kNS], rl[kNS];
+        LoadSpec(rec.beta, NR, ri, beta);
+        LoadSpec(rec.ru, NR, ri, ru);
+        LoadSpec(rec.rl, NR, ri, rl);
+        const V3 rd = LoadV3(rec.ray + 3 * (size_t)NR, NR, ri);
+        const int prim = v.hitPrim[ri];
+        if (prim < 0) {
+            // HandleEscapedRays (integrator.cpp:495-537): UniformInfiniteLight, whose
+            // PDF_Li(allowIncompletePDF) is 0, so r_l adds nothing to the MIS denominator
+            float den[kNS];
+#pragma unroll
+            for (int i = 0; i < kNS; ++i) den[i] = (depth == 0 || specularBounce) ? ru[i] : ru[i] + rl[i] * 0.f;
+            const float avg = AvgArr(den);
+            for (int k = 0; k < S.nInfinite; ++k) {
+                const int spec = S.infSpectrum[k];
+                const float scale = S.infScale[k];
+                bool nz = false;
+#pragma unroll
+                for (int i = 0; i < kNS; ++i) nz |= scale * DenseAt(S, spec, wo.off[i]) != 0;
+                if (!nz) continue;
+                AddToL(S, st, slot, wo, [&](int i) { return beta[i] * (scale * DenseAt(S, spec, wo.off[i])) / avg; });
+            }
+            continue;
+        }
+        const float b0 = v.hitB[ri], b1 = v.hitB[NR + ri], b2 = v.hitB[2 * NR + ri];
+        V3 p0, p1, p2;
+        PrimVerts(S, prim, &p0, &p1, &p2);
+        const TriSurface si = SurfaceAt(S, prim, p0, p1, p2, b0, b1, b2);
+        const V3 wo3 = Normalize(-rd);
+        int mIn, mOut;
+        MediaOf(S, prim, medium, &mIn, &mOut);
+        const int mat = S.primMaterial[prim];
+        const int mtype = S.matType[mat];
+        if (mtype == 3) {
+            // Material "interface": SpawnRay(ray.d) at the same path depth (media.cpp:193-203)
+            if (last) continue;
+            const int pos = WavePush(nextCnt, true);
+            const int jn = shardBase + pos;
+            const VolRecords &out = v.rec[(wf + 1) & 1];
+            StoreSpec(out.beta, NR, jn, beta);
+            StoreSpec(out.ru, NR, jn, ru);
+            StoreSpec(out.rl, NR, jn, rl);
+            StoreV3(out.ray, NR, jn, OffsetRayOrigin(si.p, si.pErr, si.n, rd));
+            StoreV3(out.ray + 3 * (size_t)NR, NR, jn, rd);
+#pragma unroll
+            for (int k = 0; k < 12; ++k) out.prev[(size_t)k * NR + jn] = rec.prev[(size_t)k * NR + ri];
+            out.lambda0[jn] = lambda0;
+            out.etaScale[jn] = rec.etaScale[ri];
+            out.flags[jn] = flags;
+            out.pixel[jn] = slot;
+            out.depth[jn] = depth;
+            out.medium[jn] = DotN(si.n, rd) > 0 ? mOut : mIn;
+            continue;
+        }
+        // HandleEmissiveIntersection (integrator.cpp:539-573)
+        const int light = S.primLight[prim];
+        if (light >= 0) {
+            const DeviceAreaLight Ld = S.lights[light];
+            bool nz = false;
+#pragma unroll
+            for (int i = 0; i < kNS; ++i) nz |= Ld.scale * DenseAt(S, Ld.spectrum, wo.off[i]) != 0;
+            if (nz && (Ld.twoSided || DotN(si.n, wo3) >= 0)) {
+                float den[kNS];
+                if (depth == 0 || specularBounce) {
+#pragma unroll
+                    for (int i = 0; i < kNS; ++i) den[i] = ru[i];
+                } else {
+                    const V3 pp = LoadV3(rec.prev, NR, ri), pe = LoadV3(rec.prev + 3 * (size_t)NR, NR, ri);
+                    const V3 pn = LoadV3(rec.prev + 6 * (size_t)NR, NR, ri);
+                    const V3 pns = LoadV3(rec.prev + 9 * (size_t)NR, NR, ri);
+                    const float lightChoicePDF = LightPMF(S, pp, pns, light);
+                    TriShading lsh;
+                    const bool lhas = LoadTriShading(S, __float_as_int(Ld.v0.w), &lsh);
+                    const V3 l0(Ld.v0.x, Ld.v0.y, Ld.v0.z), l1(Ld.v1.x, Ld.v1.y, Ld.v1.z),
+                        l2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
+                    const float lightPDF =
+                        lightChoicePDF * TrianglePDF(l0, l1, l2, Ld.flip, lhas ? &lsh : nullptr, pp, pe, pn, pns, -wo3);
+#pragma unroll
+                    for (int i = 0; i < kNS; ++i) den[i] = ru[i] + rl[i] * lightPDF;
+                }
+                const float avg = AvgArr(den);
+                AddToL(S, st, slot, wo, [&](int i) { return beta[i] * (Ld.scale * DenseAt(S, Ld.spectrum, wo.off[i])) / avg; });
+            }
+        }
+        if (last) continue;
+        // ---- EvaluateMaterialAndBSDF (surfscatter.cpp:57-328) for this material type
+        const VRaySamples rs = RaySamplesAt(S, st, slot, depth);
+        const float4 mp4 = S.matParams[mat];
+        const float4 mc = S.matCoeffs[mat];
+        const bool constant = S.matConstant[mat];
+        TrowbridgeReitz tr{mp4.x, mp4.y};
+        if (mtype != 0 && S.regularize && (flags & 2)) tr.Regularize();  // surfscatter.cpp:127-128
+        const float eta = mp4.z == 0 ? 1.f : mp4.z;
+        const int etaSpec = mtype == 2 ? S.matSpectra[2 * mat] : -1;
+        const int kSpec = mtype == 2 ? S.matSpectra[2 * mat + 1] : -1;
+        auto etaK = [&](float lam, float *e, float *k) {
+            if (etaSpec >= 0) {
+                const int a = S.plOffsets[etaSpec], na = S.plOffsets[etaSpec + 1] - a;
+                const int b = S.plOffsets[kSpec], nb = S.plOffsets[kSpec + 1] - b;
+                *e = PiecewiseLinearEval(S.plLambda + a, S.plValue + a, na, lam);
+                *k = PiecewiseLinearEval(S.plLambda + b, S.plValue + b, nb, lam);
+            } else {
+                const float r = Clampf(SigmoidPolynomial(mc.x, mc.y, mc.z, lam), 0, .9999f);
+                *e = 1.f;
+                *k = 2 * std::sqrt(r) / std::sqrt(std::fmax(0.f, 1 - r));
+            }
+        };
+        // BxDF::Flags (bxdfs.h): diffuse R != 0; dielectric / conductor always
+        bool hasFlags = mtype != 0;
+        if (mtype == 0) {
+            SpectralIter it(lambda0);
+#pragma unroll
+            for (int i = 0; i < kNS; ++i, it.Next()) hasFlags |= Reflectance(mc, constant, it.lam) != 0;
+        }
+        if (!hasFlags) continue;
+        const bool smooth = mtype != 0 && tr.EffectivelySmooth();
+        const bool reflective = mtype != 1 || eta != 1;
+        const bool transmissive = mtype == 1;
+        const Frame frame = Frame::FromXZ(Normalize(si.dpdus), si.ns);
+        const V3 woL = frame.ToLocal(wo3);
+        // ---- light sampling + shadow ray (surfscatter.cpp:252-326), IsNonSpecular(flags)
+        if (mtype == 0 || !smooth) {
+            V3 cp = si.p;
+            if (reflective && !transmissive) cp = OffsetRayOrigin(si.p, si.pErr, si.n, wo3);
+            else if (transmissive && reflective) cp = OffsetRayOrigin(si.p, si.pErr, si.n, -wo3);
+            AreaLightSample ls;
+            float Le[kNS];
+            if (SampleAreaLight(S, cp, si.n, si.ns, rs.dUc, rs.dU0, rs.dU1, wo, &ls, Le) && woL.z != 0) {
+                const V3 wi = Normalize(ls.p - cp);
+                const V3 wiL = frame.ToLocal(wi);
+                // BSDF::f / BSDF::PDF (bsdf.h:60-135)
+                float fd = 0, bsdfPDF = 0;
+                ConductorTerms ct{};
+                bool fAny;
+                if (mtype == 0) {
+                    fAny = woL.z * wiL.z > 0;  // SameHemisphere, else f = 0
+                    bsdfPDF = fAny ? CosineHemispherePDF(fabsf(wiL.z)) : 0.f;
+                } else if (mtype == 1) {
+                    fd = DielectricEval(eta, tr, woL, wiL, &bsdfPDF);
+                    fAny = fd != 0;
+                } else {
+                    ct = ConductorEval(tr, woL, wiL);
+                    bsdfPDF = ct.pdf;
+                    fAny = ct.ok;
+                }
+                if (fAny) {
+                    const float absdot = AbsDotN(si.ns, wi);
+                    float f[kNS];
+                    bool fnz = false;
+                    SpectralIter it(lambda0);
+#pragma unroll
+                    for (int i = 0; i < kNS; ++i, it.Next()) {
+                        if (mtype == 0) {
+                            f[i] = Reflectance(mc, constant, it.lam) * kInvPi;
+                        } else if (mtype == 1) {
+                            f[i] = fd;
+                        } else {
+                            float e, k;
+                            etaK(it.lam, &e, &k);
+                            f[i] = ConductorF(ct, e, k);
+                        }
+                        fnz |= f[i] != 0;
+                    }
+                    if (fnz) {
+                        const float lightPDF = ls.pdf;
+                        float Ld[kNS], sru[kNS], srl[kNS];
+#pragma unroll
+                        for (int i = 0; i < kNS; ++i) {
+                            Ld[i] = beta[i] * f[i] * absdot * Le[i];
+                            sru[i] = ru[i] * bsdfPDF;
+                            srl[i] = ru[i] * lightPDF;
+                        }
+                        // SpawnRayTo(pi, n, time, pLight.pi, pLight.n) (ray.h:106-111)
+                        ShadowOut so;
+                        so.o = OffsetRayOrigin(si.p, si.pErr, si.n, ls.p - si.p);
+                        const V3 pt = OffsetRayOrigin(ls.p, ls.pErr, ls.n, so.o - ls.p);
+                        so.d = pt - so.o;
+                        so.medium = DotN(si.n, so.d) > 0 ? mOut : mIn;
+                        const int pos = WavePush(shadowCnt, true);
+                        WriteShadow(v, NR, shardBase + pos, so, Ld, sru, srl, lambda0, slot);
+                    }
+                }
+            }
+        }
+        // ---- BSDF::Sample_f + RR + indirect ray (surfscatter.cpp:170-250)
+        if (woL.z == 0) continue;
+        bool ok = false;
+        V3 wiL;
+        float pdf = 0, fd = 0, etap = 1;
+        bool specular = false, transmission = false;
+        ConductorTerms ct{};
+        if (mtype == 0) {
+            wiL = SampleCosineHemisphere(rs.iU0, rs.iU1);
+            if (woL.z < 0) wiL.z *= -1;
+            pdf = CosineHemispherePDF(fabsf(wiL.z));
+            ok = true;
+        } else if (mtype == 1) {
+            const BxSample bs = DielectricSample(eta, tr, woL, rs.iUc, rs.iU0, rs.iU1);
+            ok = bs.ok && bs.f != 0;
+            wiL = bs.wi;
+            pdf = bs.pdf;
+            fd = bs.f;
+            etap = bs.etap;
+            specular = bs.flags & kBxSpecular;
+            transmission = bs.flags & kBxTransmission;
+        } else {
+            ct = ConductorSample(tr, woL, rs.iU0, rs.iU1);
+            ok = ct.ok;
+            wiL = ct.wi;
+            pdf = ct.pdf;
+            specular = ct.specular;
+        }
+        if (!ok || pdf == 0 || wiL.z == 0) continue;
+        const V3 wi = frame.FromLocal(wiL);
+        const float absdot = AbsDotN(si.ns, wi);
+        float etaScale = rec.etaScale[ri];
+        if (transmission) etaScale *= Sqr(etap);
+        bool fAny = false;
+        {
+            SpectralIter it(lambda0);
+#pragma unroll
+            for (int i = 0; i < kNS; ++i, it.Next()) {
+                float f = fd;
+                if (mtype == 0) {
+                    f = Reflectance(mc, constant, it.lam) * kInvPi;
+                } else if (mtype == 2) {
+                    float e, k;
+                    etaK(it.lam, &e, &k);
+                    f = ConductorF(ct, e, k);
+                }
+                fAny |= f != 0;
+                beta[i] = beta[i] * f * absdot / pdf;
+            }
+        }
+        if (!fAny) continue;
+        const float avgRu = AvgArr(ru);
+        float mx = -kInfinity;
+#pragma unroll
+        for (int i = 0; i < kNS; ++i) mx = fmaxf(mx, beta[i] * etaScale / avgRu);
+        const bool rrOn = mx < 1 && depth >= 1;
+        float q = 0;
+        if (rrOn) {
+            q = fmaxf(0.f, 1 - mx);
+            if (rs.rr < q) continue;
+        }
+        bool nz = false;
+#pragma unroll
+        for (int i = 0; i < kNS; ++i) {
+            if (rrOn) beta[i] /= 1 - q;
+            nz |= beta[i] != 0;
+            rl[i] = ru[i] / pdf;
+        }
+        if (!nz) continue;
+        const int pos = WavePush(nextCnt, true);
+        const int jn = shardBase + pos;
+        const VolRecords &out = v.rec[(wf + 1) & 1];
+        StoreSpec(out.beta, NR, jn, beta);
+        StoreSpec(out.ru, NR, jn, ru);
+        StoreSpec(out.rl, NR, jn, rl);
+        StoreV3(out.ray, NR, jn, OffsetRayOrigin(si.p, si.pErr, si.n, wi));
+        StoreV3(out.ray + 3 * (size_t)NR, NR, jn, wi);
+        StoreV3(out.prev, NR, jn, si.p);
+        StoreV3(out.prev + 3 * (size_t)NR, NR, jn, si.pErr);
+        StoreV3(out.prev + 6 * (size_t)NR, NR, jn, si.n);
+        StoreV3(out.prev + 9 * (size_t)NR, NR, jn, si.ns);
+        out.lambda0[jn] = lambda0;
+        out.etaScale[jn] = etaScale;
+        out.flags[jn] = (specular ? 1 : 0) | ((!specular || (flags & 2)) ? 2 : 0);
+        out.pixel[jn] = slot;
+        out.depth[jn] = depth + 1;
+        out.medium[jn] = DotN(si.n, wi) > 0 ? mOut : mIn;
+    }
+}
+
+// SampleMediumScattering<HGPhaseFunction> (media.cpp:259-352)
+__global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vscatter(DeviceScene S, PathState st, VolState v, int wf) {
+    const QueueView scat = LoadQueue(st, wf, kVScat);
+    const int NR = st.NR;
+    const VolRecords &rec = v.rec[wf & 1];
+    const int shard = ProducerShard();
+    const int shardBase = shard * st.capS;
+    int *nextCnt = &st.counters[CounterIndex(wf + 1, kVRay, shard)];
+    int *shadowCnt = &st.counters[CounterIndex(wf, kVShadow, shard)];
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < scat.total; j += gridDim.x * blockDim.x) {
+        const int ri = v.scatQ[QueueSlot(scat, j)];
+        const float lambda0 = rec.lambda0[ri];
+        const int slot = rec.pixel[ri], depth = rec.depth[ri], medium = rec.medium[ri];
+        const WaveOffsets wo(lambda0);
+        float beta[kNS], ru[kNS];
+        LoadSpec(rec.beta, NR, ri, beta);
+        LoadSpec(rec.ru, NR, ri, ru);
+        const V3 pS = LoadV3(v.hitB, NR, ri);
+        const V3 wo3 = -LoadV3(rec.ray + 3 * (size_t)NR, NR, ri);
+        const float g = MediumAt(S, medium).P[0];
+        const VRaySamples rs = RaySamplesAt(S, st, slot, depth);
+        // direct lighting: LightSampleContext(p, n = 0, ns = 0)
+        {
+            AreaLightSample ls;
+            float Le[kNS];
+            if (SampleAreaLight(S, pS, V3(0, 0, 0), V3(0, 0, 0), rs.dUc, rs.dU0, rs.dU1, wo, &ls, Le)) {
+                const V3 wi = Normalize(ls.p - pS);
+                const float ph = HenyeyGreenstein(Dot(wo3, wi), g);
+                float Ld[kNS], sru[kNS], srl[kNS];
+#pragma unroll
+                for (int i = 0; i < kNS; ++i) {
+                    Ld[i] = (beta[i] * ph) * Le[i];
+                    sru[i] = ru[i] * ph;
+                    srl[i] = ru[i] * ls.pdf;
+                }
+                ShadowOut so;
+                so.o = pS;
+                so.d = ls.p - pS;
+                so.medium = medium;
+                const int pos = WavePush(shadowCnt, true);
+                WriteShadow(v, NR, shardBase + pos, so, Ld, sru, srl, lambda0, slot);
+            }
+        }
+        // indirect: phase-function sample, RR, next ray at depth + 1
+        float pdf;
+        const V3 wi = SampleHenyeyGreenstein(wo3, g, rs.iU0, rs.iU1, &pdf);
+        if (pdf == 0) continue;
+        const float etaScale = rec.etaScale[ri];
+        float rl[kNS];
+#pragma unroll
+        for (int i = 0; i < kNS; ++i) {
+            beta[i] = beta[i] * pdf / pdf;
+            rl[i] = ru[i] / pdf;
+        }
+        const float avgRu = AvgArr(ru);
+        float mx = -kInfinity;
+#pragma unroll
+        for (int i = 0; i < kNS; ++i) mx = fmaxf(mx, beta[i] * etaScale / avgRu);
+        if (mx < 1 && depth >= 1) {
+            const float q = fmaxf(0.f, 1 - mx);
+            if (rs.rr < q) continue;
+#pragma unroll
+            for (int i = 0; i < kNS; ++i) beta[i] /= 1 - q;
+        }
+        const int pos = WavePush(nextCnt, true);
+        const int jn = shardBase + pos;
+        const VolRecords &out = v.rec[(wf + 1) & 1];
+        StoreSpec(out.beta, NR, jn, beta);
+        StoreSpec(out.ru, NR, jn, ru);
+        StoreSpec(out.rl, NR, jn, rl);
+        StoreV3(out.ray, NR, jn, pS);
+        StoreV3(out.ray + 3 * (size_t)NR, NR, jn, wi);
+        StoreV3(out.prev, NR, jn, pS);
+#pragma unroll
+        for (int k = 3; k < 12; ++k) out.prev[(size_t)k * NR + jn] = 0.f;
+        out.lambda0[jn] = lambda0;
+        out.etaScale[jn] = etaScale;
+        out.flags[jn] = 2;  // specularBounce = false, anyNonSpecularBounces = true
+        out.pixel[jn] = slot;
+        out.depth[jn] = depth + 1;
+        out.medium[jn] = medium;
+    }
+}
+
+// TraceTransmittance (wavefront/intersect.h:164-274): closest hits up to the light; a
+// non-interface surface blocks, interfaces are crossed (SpawnRayTo the light point), and in
+// each medium T_ray / r_u / r_l follow ratio tracking with RR on a small T_ray.
+template <bool Q>
+__global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vshadow(DeviceScene S, PathState st, VolState v, int wf) {
+    const QueueView sh = LoadQueue(st, wf, kVShadow);
+    if ((int)(blockIdx.x * blockDim.x) >= sh.total) return;
+    extern __shared__ float4 dynLds[];
+    const SceneLds L = SetupSceneLds(S, dynLds);
+    const int NR = st.NR;
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&st.stats[2], (unsigned long long)sh.total);
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < sh.total; j += gridDim.x * blockDim.x) {
+        const int p = QueueSlot(sh, j);
+        V3 o = LoadV3(v.shRay, NR, p), d = LoadV3(v.shRay + 3 * (size_t)NR, NR, p);
+        int med = v.shMedium[p];
+        const WaveOffsets wo(v.shLambda0[p]);
+        const float tMax = 1 - kShadowEpsilon;
+        const V3 pLight = o + d * tMax;
+        PCG32 rng(HashV3(o), HashV3(d));
+        float Tr[kNS], tu[kNS], tl[kNS], Tm[kNS];
+#pragma unroll
+        for (int i = 0; i < kNS; ++i) Tr[i] = tu[i] = tl[i] = 1.f;
+        bool blocked = false;
+        for (int guard = 0; guard < 256; ++guard) {
+            if (d == V3(0, 0, 0)) break;
+            TriHit h;
+            const int hp = Traverse<false, Q>(S, L, o, d, tMax, &h);
+            if (hp >= 0 && S.matType[S.primMaterial[hp]] != 3) {
+                blocked = true;
+                break;
+            }
+            TriSurface hs{};
+            if (hp >= 0) {
+                V3 p0, p1, p2;
+                PrimVerts(S, hp, &p0, &p1, &p2);
+                hs = SurfaceAt(S, hp, p0, p1, p2, h.b0, h.b1, h.b2);
+            }
+            if (med >= 0) {
+                const MediumRef m = MediumAt(S, med);
+                const int sa = m.I[1], ss = m.I[2];
+                const float tEnd = hp < 0 ? tMax : (Length(o - hs.p) / Length(d));
+                auto event = [&](V3, const MediumPoint &mp, float mx, const float *T) -> bool {
+                    float sn[kNS], smj[kNS];
+#pragma unroll
+                    for (int i = 0; i < kNS; ++i) {
+                        smj[i] = (DenseAt(S, sa, wo.off[i]) + DenseAt(S, ss, wo.off[i])) * mx;
+                        sn[i] = fmaxf(0.f, smj[i] - DenseAt(S, sa, wo.off[i]) * mp.d - DenseAt(S, ss, wo.off[i]) * mp.d);
+                    }
+                    const float pr = T[0] * smj[0];
+#pragma unroll
+                    for (int i = 0; i < kNS; ++i) {
+                        Tr[i] *= T[i] * sn[i] / pr;
+                        tl[i] *= T[i] * smj[i] / pr;
+                        tu[i] *= T[i] * sn[i] / pr;
+                    }
+                    // T_ray / (r_l + r_u).Average() < 0.05: Russian roulette
+                    float den[kNS];
+#pragma unroll
+                    for (int i = 0; i < kNS; ++i) den[i] = tl[i] + tu[i];
+                    const float avg = AvgArr(den);
+                    float mxT = -kInfinity;
+#pragma unroll
+                    for (int i = 0; i < kNS; ++i) mxT = fmaxf(mxT, Tr[i] / avg);
+                    if (mxT < 0.05f) {
+                        const float q = 0.75f;
+                        if (rng.Uniform() < q) {
+#pragma unroll
+                            for (int i = 0; i < kNS; ++i) Tr[i] = 0.f;
+                        } else {
+#pragma unroll
+                            for (int i = 0; i < kNS; ++i) Tr[i] /= 1 - q;
+                        }
+                    }
+                    return AnyNonZero(Tr);
+                };
+                const bool ranOut = SampleTmaj(S, m, wo, o, d, tEnd, rng.Uniform(), rng, Tm, event);
+                if (ranOut) {
+                    const float t0 = Tm[0];
+#pragma unroll
+                    for (int i = 0; i < kNS; ++i) {
+                        const float f = Tm[i] / t0;
+                        Tr[i] *= f;
+                        tl[i] *= f;
+                        tu[i] *= f;
+                    }
+                }
+            }
+            if (hp < 0 || !AnyNonZero(Tr)) break;
+            // SurfaceInteraction::SpawnRayTo(pLight) (interaction.h, ray.h:98-104)
+            int mIn, mOut;
+            MediaOf(S, hp, med, &mIn, &mOut);
+            const V3 dd = pLight - hs.p;
+            o = OffsetRayOrigin(hs.p, hs.pErr, hs.n, dd);
+            d = dd;
+            med = DotN(hs.n, d) > 0 ? mOut : mIn;
+        }
+        if (blocked || !AnyNonZero(Tr)) continue;
+        float Ld[kNS], den[kNS];
+        {
+            float ru[kNS], rl[kNS];
+            LoadSpec(v.shRu, NR, p, ru);
+            LoadSpec(v.shRl, NR, p, rl);
+#pragma unroll
+            for (int i = 0; i < kNS; ++i) den[i] = ru[i] * tu[i] + rl[i] * tl[i];
+        }
+        LoadSpec(v.shLd, NR, p, Ld);
+        const float avg = AvgArr(den);
+        AddToL(S, st, v.shPixel[p], wo, [&](int i) { return Ld[i] * Tr[i] / avg; });
+    }
+}
+
+// ------------------------------------------------------------------ launch helpers (host)
+size_t TraversalLdsBytes(int stackSize, int ldsNodes, int ldsTris, int compressed);
+static size_t VolStackBytes(const DeviceScene &S) {
+    return TraversalLdsBytes(S.stackSize, S.ldsNodes, S.ldsTris, S.compressed);
+}
+static int VolGrid(int n, int cap) {
+    int g = (n + kBlock - 1) / kBlock;
+    g = g < 1 ? 1 : (g > cap ? cap : g);
+    return (g + kShards - 1) / kShards * kShards;  // producer grids: multiples of kShards
+}
+
+hipError_t LaunchVolCamera(const DeviceScene &S, const PathState &st, const VolState &v, int nActive, hipStream_t s) {
+    hipLaunchKernelGGL(k_vcamera, dim3((nActive + kBlock - 1) / kBlock), dim3(kBlock), 0, s, S, st, v, nActive);
+    return hipGetLastError();
+}
+hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const VolState &v, int wf, int maxCount,
+                              hipStream_t s) {
+    const dim3 block(kBlock);
+    const dim3 gT(VolGrid(maxCount, 1024)), gW(VolGrid(maxCount, 2048));
+    if (S.compressed) hipLaunchKernelGGL(k_vclosest<true>, gT, block, VolStackBytes(S), s, S, st, v, wf);
+    else hipLaunchKernelGGL(k_vclosest<false>, gT, block, VolStackBytes(S), s, S, st, v, wf);
+    hipLaunchKernelGGL(k_vmedium, gW, block, 0, s, S, st, v, wf);
+    hipLaunchKernelGGL(k_vsurface, gW, block, 0, s, S, st, v, wf);
+    if (wf == S.maxDepth) return hipGetLastError();
+    hipLaunchKernelGGL(k_vscatter, gW, block, 0, s, S, st, v, wf);
+    if (S.compressed) hipLaunchKernelGGL(k_vshadow<true>, gT, block, VolStackBytes(S), s, S, st, v, wf);
+    else hipLaunchKernelGGL(k_vshadow<false>, gT, block, VolStackBytes(S), s, S, st, v, wf);
+    return hipGetLastError();
+}
+
+}  // namespace pbrt_amd

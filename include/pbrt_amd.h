@@ -104,7 +104,8 @@ typedef struct pbrt_scene_flat {
                                          sigma_s, Le (dense_spectra indices, pbrt's scales
                                          applied), emissive, nx, ny, nz, lnx, lny, lnz,
                                          density offset, LeScale offset, majorant offset (into
-                                         medium_values), 0, 0 */
+                                         medium_values), grey (sigma_a and sigma_s
+                                         constant over wavelength), 0 */
     const float *medium_params;       /* [n_media][24]: g, bounds p0 xyz, p1 xyz, 0,
                                          mediumFromRender 4x4 row-major */
     const float *medium_values;       /* density / LeScale / 16^3 majorant grids */

@@ -59,8 +59,15 @@ static void MediumTables(const SceneDesc &s, std::vector<int32_t> *info, std::ve
         values->insert(values->end(), m.LeScale.begin(), m.LeScale.end());
         const int mOff = (int)values->size();
         values->insert(values->end(), m.majorant.begin(), m.majorant.end());
+        // grey: sigma_a and sigma_s are the same at every wavelength, so every SampledSpectrum
+        // built from them (T_maj, sigma_n, ...) has 31 equal entries (the kernels' scalar path)
+        auto flat = [&](int idx) {
+            const auto &d = s.denseSpectra[idx];
+            return std::all_of(d.begin(), d.end(), [&](float v) { return v == d[0]; });
+        };
+        const int grey = flat(m.sigmaA) && flat(m.sigmaS) ? 1 : 0;
         info->insert(info->end(), {m.type, m.sigmaA, m.sigmaS, m.Le, m.emissive ? 1 : 0, m.nx, m.ny, m.nz, m.lnx, m.lny,
-                                   m.lnz, dOff, lOff, mOff, 0, 0});
+                                   m.lnz, dOff, lOff, mOff, grey, 0});
         const V3 lo(std::min(m.p0.x, m.p1.x), std::min(m.p0.y, m.p1.y), std::min(m.p0.z, m.p1.z));
         const V3 hi(std::max(m.p0.x, m.p1.x), std::max(m.p0.y, m.p1.y), std::max(m.p0.z, m.p1.z));
         params->insert(params->end(), {m.g, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, 0.f});
@@ -423,6 +430,14 @@ static void BuildDevice(pbrt_context *c) {
     c->volumetric = !s.media.empty() ||
                     std::any_of(s.materials.begin(), s.materials.end(), [](const MaterialDesc &m) { return m.type == kMatInterface; });
     S.media.cameraMedium = s.cameraMedium;
+    S.media.allGrey = 1;
+    for (size_t m = 0; m < s.media.size(); ++m) {
+        const auto &a = s.denseSpectra[s.media[m].sigmaA], &b = s.denseSpectra[s.media[m].sigmaS];
+        if (!std::all_of(a.begin(), a.end(), [&](float x) { return x == a[0]; }) ||
+            !std::all_of(b.begin(), b.end(), [&](float x) { return x == b[0]; }))
+            S.media.allGrey = 0;
+    }
+    if (getenv("PBRT_AMD_SPECTRAL_MEDIA")) S.media.allGrey = 0;  // force the spectral kernels (tests)
     S.media.info = c->mediumInfo.p;
     S.media.params = c->mediumParams.p;
     S.media.values = c->mediumValues.p;

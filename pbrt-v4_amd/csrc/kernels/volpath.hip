@@ -29,6 +29,9 @@ namespace pbrt_amd {
 #ifndef PBRT_VOL_WAVES
 #define PBRT_VOL_WAVES 2  // waves/SIMD the spectral media kernels are compiled for
 #endif
+#ifndef PBRT_VOL_GREY_WAVES
+#define PBRT_VOL_GREY_WAVES 3  // waves/SIMD of the grey-medium sampling kernel
+#endif
 constexpr int kNS = kNSpectrumSamples;
 
 // ------------------------------------------------------------------ media
@@ -257,7 +260,7 @@ __device__ inline bool AnyNonZero(const float *a) {
 // traversal ran to the end (T_maj = Tm then) and false when the callback stopped it
 // (SampleT_maj returns SampledSpectrum(1) then).
 template <typename F>
-__device__ inline bool SampleTmaj(const DeviceScene &S, const MediumRef &m, const WaveOffsets &wo, V3 o, V3 d,
+__device__ __forceinline__ bool SampleTmaj(const DeviceScene &S, const MediumRef &m, const WaveOffsets &wo, V3 o, V3 d,
                                   float tMax, float u, PCG32 &rng, float Tm[kNS], F &&event) {
     tMax *= Length(d);
     d = Normalize(d);
@@ -303,6 +306,48 @@ __device__ inline bool SampleTmaj(const DeviceScene &S, const MediumRef &m, cons
                     const float smaj = (DenseAt(S, sa, wo.off[i]) + DenseAt(S, ss, wo.off[i])) * mx;
                     Tm[i] *= FastExp(smaj * -dt);
                 }
+                break;
+            }
+        }
+    }
+    return true;
+}
+
+// SampleT_maj for a grey medium (sigma_a, sigma_s equal at every wavelength, DeviceMedia
+// info[14]): every T_maj / sigma_maj entry is the same, so the reference's 31-wide products
+// are one scalar product here -- the same float operations on the same values.
+// sigmaT = sigma_a + sigma_s of the medium (its wavelength-0 entries).
+template <typename F>
+__device__ __forceinline__ bool SampleTmajGrey(const DeviceScene &S, const MediumRef &m, float sigmaT, V3 o, V3 d,
+                                               float tMax, float u, PCG32 &rng, float &Tm, F &&event) {
+    tMax *= Length(d);
+    d = Normalize(d);
+    MajorantIter iter = SampleMediumRay(S, m, o, d, tMax);
+    Tm = 1.f;
+    float segMin, segMax, mx;
+    while (iter.Next(&segMin, &segMax, &mx)) {
+        const float smaj = sigmaT * mx;
+        if (smaj == 0) {
+            float dt = segMax - segMin;
+            if (isinf(dt)) dt = 3.402823466e+38f;
+            Tm *= FastExp(smaj * -dt);
+            continue;
+        }
+        float tMin = segMin;
+        while (true) {
+            const float t = tMin + SampleExponential(u, smaj);
+            u = rng.Uniform();
+            if (t < segMax) {
+                Tm *= FastExp(smaj * -(t - tMin));
+                const V3 p = o + d * t;
+                const MediumPoint mp = SampleMediumPoint(S, m, p);
+                if (!event(p, mp, smaj, Tm)) return false;
+                Tm = 1.f;
+                tMin = t;
+            } else {
+                float dt = segMax - tMin;
+                if (isinf(dt)) dt = 3.402823466e+38f;
+                Tm *= FastExp(smaj * -dt);
                 break;
             }
         }
@@ -486,7 +531,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vmedium(DeviceScene 
             bool emitted = false;
             const int sa = m.I[1], ss = m.I[2], le = m.I[3];
             const bool maxD = depth >= S.maxDepth;
-            auto event = [&](V3 p, const MediumPoint &mp, float mx, const float *T) -> bool {
+            auto event = [&](V3 p, const MediumPoint &mp, float mx, const float *T) __attribute__((always_inline)) -> bool {
                 const float smaj0 = (DenseAt(S, sa, wo.off[0]) + DenseAt(S, ss, wo.off[0])) * mx;
                 const float sa0 = DenseAt(S, sa, wo.off[0]) * mp.d, ss0 = DenseAt(S, ss, wo.off[0]) * mp.d;
                 // medium emission, scaled by sigma_a / sigma_maj at every event (media.cpp:70-83)
@@ -588,6 +633,175 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vmedium(DeviceScene 
                 StoreSpec(rec.beta, NR, ri, beta);
                 StoreSpec(rec.ru, NR, ri, ru);
                 StoreSpec(rec.rl, NR, ri, rl);
+                toSurf = true;
+            }
+        }
+        const int p0 = WavePush(surfCnt, toSurf);
+        const int p1 = WavePush(scatCnt, toScat);
+        if (p0 >= 0) v.surfQ[shard * st.capS + p0] = ri;
+        if (p1 >= 0) v.scatQ[shard * st.capS + p1] = ri;
+    }
+}
+
+// SampleMediumInteraction for scenes whose media are all grey (DeviceMedia::allGrey): every
+// T_maj / sigma product is a scalar.  The factors that multiply beta and r_u are then
+// (T sigma) / (T[0] sigma[0]) = x / x -- exactly 1 unless x is 0 (the path dies) -- so beta and
+// r_u stay in memory and only a scalar record of any non-unit factor is kept; r_l takes
+// T sigma_maj / pr per null collision, applied in the reference's order to its (spectrally
+// constant, checked) value.  No 31-wide array lives through the tracking loop.
+__global__ void __launch_bounds__(kBlock, PBRT_VOL_GREY_WAVES) k_vmedium_grey(DeviceScene S, PathState st, VolState v,
+                                                                            int wf) {
+    const QueueView meds = LoadQueue(st, wf, kVMed);
+    const int NR = st.NR;
+    const VolRecords &rec = v.rec[wf & 1];
+    const int shard = ProducerShard();
+    int *surfCnt = &st.counters[CounterIndex(wf, kVSurf, shard)];
+    int *scatCnt = &st.counters[CounterIndex(wf, kVScat, shard)];
+    for (int base = blockIdx.x * blockDim.x; base < meds.total; base += gridDim.x * blockDim.x) {
+        const int j = base + threadIdx.x;
+        const bool active = j < meds.total;
+        const int ri = active ? v.medQ[QueueSlot(meds, j)] : 0;
+        bool toSurf = false, toScat = false;
+        if (active) {
+            const V3 o = LoadV3(rec.ray, NR, ri), d = LoadV3(rec.ray + 3 * (size_t)NR, NR, ri);
+            const float tHit = v.hitB[3 * NR + ri];
+            const int depth = rec.depth[ri], slot = rec.pixel[ri];
+            const MediumRef m = MediumAt(S, rec.medium[ri]);
+            const float lambda0 = rec.lambda0[ri];
+            const int off0 = DenseOffset(lambda0);
+            const int sa = m.I[1], ss = m.I[2], le = m.I[3];
+            const float sa0 = DenseAt(S, sa, off0), ss0 = DenseAt(S, ss, off0);
+            // beta, r_u nonzero?  r_l spectrally constant?  (one pass over the records)
+            bool betaNz = false, ruNz = false, rlFlat = true;
+            const float rl0 = rec.rl[ri];
+#pragma unroll 4
+            for (int i = 0; i < kNS; ++i) {
+                betaNz |= rec.beta[(size_t)i * NR + ri] != 0;
+                ruNz |= rec.ru[(size_t)i * NR + ri] != 0;
+                rlFlat &= rec.rl[(size_t)i * NR + ri] == rl0;
+            }
+            float fb = 1.f;     // product of the (non-unit) beta / r_u factors
+            float rlS = rl0;    // r_l when spectrally constant (exact)
+            float gl = 1.f;     // product of the r_l factors otherwise
+            bool fbZero = false;
+            PCG32 rng(HashV3F(o, tHit), HashV3(d));
+            const float uDist = rng.Uniform();
+            float uMode = rng.Uniform();
+            bool scattered = false, pushScatter = false;
+            V3 pS(0, 0, 0);
+            float Lx = 0, Ly = 0, Lz = 0;
+            bool emitted = false;
+            const bool maxD = depth >= S.maxDepth;
+            auto mulBeta = [&](float f) __attribute__((always_inline)) {
+                if (f != 1.f) {
+                    fb *= f;
+                    fbZero |= f == 0;
+                }
+            };
+            auto event = [&](V3 p, const MediumPoint &mp, float smaj, float T) __attribute__((always_inline)) -> bool {
+                const float sad = sa0 * mp.d, ssd = ss0 * mp.d;
+                if (!maxD && mp.le != 0) {
+                    // medium emission (media.cpp:70-83); Le may be chromatic.  Two rolled passes
+                    // over the wavelengths (sum of r_e, then the sensor sums): no 31-wide arrays.
+                    const float pr = smaj * T;
+                    bool leNz = false, reNz = false;
+                    float reSum = 0;
+                    {
+                        SpectralIter it(lambda0);
+#pragma unroll 1
+                        for (int i = 0; i < kNS; ++i, it.Next()) {
+                            leNz |= DenseAt(S, le, DenseOffset(it.lam)) * mp.le != 0;
+                            float ru = rec.ru[(size_t)i * NR + ri];
+                            if (fb != 1.f) ru *= fb;
+                            const float re = ru * smaj * T / pr;
+                            reNz |= re != 0;
+                            reSum = i == 0 ? re : reSum + re;
+                        }
+                    }
+                    if (leNz && reNz) {
+                        const float den = pr * (reSum / kNS);
+                        SensorAcc acc;
+                        SpectralIter it(lambda0);
+#pragma unroll 1
+                        for (int i = 0; i < kNS; ++i, it.Next()) {
+                            const int off = DenseOffset(it.lam);
+                            float b = rec.beta[(size_t)i * NR + ri];
+                            if (fb != 1.f) b *= fb;
+                            const float Le = DenseAt(S, le, off) * mp.le;
+                            acc.Add(S, off, b * sad * T * Le / den, i == 0);
+                        }
+                        Lx += S.imagingRatio * (acc.sx / kNS);
+                        Ly += S.imagingRatio * (acc.sy / kNS);
+                        Lz += S.imagingRatio * (acc.sz / kNS);
+                        emitted = true;
+                    }
+                }
+                const float pAbsorb = sad / smaj, pScatter = ssd / smaj;
+                const float pNull = fmaxf(0.f, 1 - pAbsorb - pScatter);
+                const int mode = SampleDiscrete3(pAbsorb, pScatter, pNull, uMode);
+                if (mode == 0) {
+                    betaNz = false;  // absorbed
+                    return false;
+                }
+                if (mode == 1) {
+                    const float pr = T * ssd;
+                    mulBeta(T * ssd / pr);
+                    pushScatter = betaNz && !fbZero && ruNz;
+                    pS = p;
+                    scattered = true;
+                    return false;
+                }
+                const float sn = fmaxf(0.f, smaj - sad - ssd);
+                const float pr = T * sn;
+                mulBeta(T * sn / pr);
+                if (pr == 0) betaNz = false;
+                const float g = T * smaj / pr;
+                rlS *= g;
+                gl *= g;
+                uMode = rng.Uniform();
+                return betaNz && !fbZero && ruNz;
+            };
+            float Tm;
+            const bool ranOut = SampleTmajGrey(S, m, sa0 + ss0, o, d, tHit, uDist, rng, Tm, event);
+            if (emitted) {
+                st.L[slot] += Lx;
+                st.L[st.N + slot] += Ly;
+                st.L[2 * st.N + slot] += Lz;
+            }
+            if (!scattered && betaNz && !fbZero && ranOut) {
+                const float f = Tm / Tm;  // T_maj / T_maj[0]: 1, or NaN as the reference's for 0 / inf
+                mulBeta(f);
+                rlS *= f;
+                gl *= f;
+            }
+            const bool alive = betaNz && !fbZero;
+            if (scattered) {
+                if (pushScatter) {
+                    if (fb != 1.f) {
+#pragma unroll
+                        for (int i = 0; i < kNS; ++i) {
+                            rec.beta[(size_t)i * NR + ri] *= fb;
+                            rec.ru[(size_t)i * NR + ri] *= fb;
+                        }
+                    }
+                    StoreV3(v.hitB, NR, ri, pS);
+                    toScat = true;
+                }
+            } else if (alive && ruNz && depth != S.maxDepth) {
+                if (fb != 1.f) {
+#pragma unroll
+                    for (int i = 0; i < kNS; ++i) {
+                        rec.beta[(size_t)i * NR + ri] *= fb;
+                        rec.ru[(size_t)i * NR + ri] *= fb;
+                    }
+                }
+                if (rlS != rl0 || !rlFlat) {
+#pragma unroll
+                    for (int i = 0; i < kNS; ++i) {
+                        if (rlFlat) rec.rl[(size_t)i * NR + ri] = rlS;
+                        else rec.rl[(size_t)i * NR + ri] *= gl;
+                    }
+                }
                 toSurf = true;
             }
         }
@@ -1070,7 +1284,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vshadow(DeviceScene 
                 const MediumRef m = MediumAt(S, med);
                 const int sa = m.I[1], ss = m.I[2];
                 const float tEnd = hp < 0 ? tMax : (Length(o - hs.p) / Length(d));
-                auto event = [&](V3, const MediumPoint &mp, float mx, const float *T) -> bool {
+                auto event = [&](V3, const MediumPoint &mp, float mx, const float *T) __attribute__((always_inline)) -> bool {
                     float sn[kNS], smj[kNS];
 #pragma unroll
                     for (int i = 0; i < kNS; ++i) {
@@ -1140,6 +1354,99 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vshadow(DeviceScene 
     }
 }
 
+// TraceTransmittance when every medium is grey: T_ray, r_u and r_l start at 1 and only ever
+// take factors that are equal at all wavelengths, so each is one scalar (the reference's 31
+// entries are 31 copies of it).
+template <bool Q>
+__global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_vshadow_grey(DeviceScene S, PathState st, VolState v,
+                                                                             int wf) {
+    const QueueView sh = LoadQueue(st, wf, kVShadow);
+    if ((int)(blockIdx.x * blockDim.x) >= sh.total) return;
+    extern __shared__ float4 dynLds[];
+    const SceneLds L = SetupSceneLds(S, dynLds);
+    const int NR = st.NR;
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&st.stats[2], (unsigned long long)sh.total);
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < sh.total; j += gridDim.x * blockDim.x) {
+        const int p = QueueSlot(sh, j);
+        V3 o = LoadV3(v.shRay, NR, p), d = LoadV3(v.shRay + 3 * (size_t)NR, NR, p);
+        int med = v.shMedium[p];
+        const float lambda0 = v.shLambda0[p];
+        const float tMax = 1 - kShadowEpsilon;
+        const V3 pLight = o + d * tMax;
+        PCG32 rng(HashV3(o), HashV3(d));
+        float Tr = 1.f, tu = 1.f, tl = 1.f, Tm;
+        bool blocked = false;
+        for (int guard = 0; guard < 256; ++guard) {
+            if (d == V3(0, 0, 0)) break;
+            TriHit h;
+            const int hp = Traverse<false, Q>(S, L, o, d, tMax, &h);
+            if (hp >= 0 && S.matType[S.primMaterial[hp]] != 3) {
+                blocked = true;
+                break;
+            }
+            TriSurface hs{};
+            if (hp >= 0) {
+                V3 p0, p1, p2;
+                PrimVerts(S, hp, &p0, &p1, &p2);
+                hs = SurfaceAt(S, hp, p0, p1, p2, h.b0, h.b1, h.b2);
+            }
+            if (med >= 0) {
+                const MediumRef m = MediumAt(S, med);
+                const int sa = m.I[1], ss = m.I[2];
+                const float tEnd = hp < 0 ? tMax : (Length(o - hs.p) / Length(d));
+                const int off0 = DenseOffset(lambda0);
+                const float sa0 = DenseAt(S, sa, off0), ss0 = DenseAt(S, ss, off0);
+                auto event = [&](V3, const MediumPoint &mp, float smaj, float T) __attribute__((always_inline)) -> bool {
+                    const float sn = fmaxf(0.f, smaj - sa0 * mp.d - ss0 * mp.d);
+                    const float pr = T * smaj;
+                    Tr *= T * sn / pr;
+                    tl *= T * smaj / pr;
+                    tu *= T * sn / pr;
+                    if (Tr / Avg31(tl + tu) < 0.05f) {  // T_ray / (r_l + r_u).Average(): RR
+                        const float q = 0.75f;
+                        if (rng.Uniform() < q) Tr = 0.f;
+                        else Tr /= 1 - q;
+                    }
+                    return Tr != 0;
+                };
+                const bool ranOut = SampleTmajGrey(S, m, sa0 + ss0, o, d, tEnd, rng.Uniform(), rng, Tm, event);
+                if (ranOut) {
+                    const float f = Tm / Tm;
+                    Tr *= f;
+                    tl *= f;
+                    tu *= f;
+                }
+            }
+            if (hp < 0 || Tr == 0) break;
+            // SurfaceInteraction::SpawnRayTo(pLight) (interaction.h, ray.h:98-104)
+            int mIn, mOut;
+            MediaOf(S, hp, med, &mIn, &mOut);
+            const V3 dd = pLight - hs.p;
+            o = OffsetRayOrigin(hs.p, hs.pErr, hs.n, dd);
+            d = dd;
+            med = DotN(hs.n, d) > 0 ? mOut : mIn;
+        }
+        if (blocked || Tr == 0) continue;
+        // L += Ld T_ray / (r_u tu + r_l tl).Average(): rolled passes, no 31-wide arrays
+        float denSum = 0;
+#pragma unroll 1
+        for (int i = 0; i < kNS; ++i) {
+            const float dv = v.shRu[(size_t)i * NR + p] * tu + v.shRl[(size_t)i * NR + p] * tl;
+            denSum = i == 0 ? dv : denSum + dv;
+        }
+        const float avg = denSum / kNS;
+        SensorAcc acc;
+        SpectralIter it(lambda0);
+#pragma unroll 1
+        for (int i = 0; i < kNS; ++i, it.Next())
+            acc.Add(S, DenseOffset(it.lam), v.shLd[(size_t)i * NR + p] * Tr / avg, i == 0);
+        const int slot = v.shPixel[p], NL = st.N;
+        st.L[slot] += S.imagingRatio * (acc.sx / kNS);
+        st.L[NL + slot] += S.imagingRatio * (acc.sy / kNS);
+        st.L[2 * NL + slot] += S.imagingRatio * (acc.sz / kNS);
+    }
+}
+
 // ------------------------------------------------------------------ launch helpers (host)
 size_t TraversalLdsBytes(int stackSize, int ldsNodes, int ldsTris, int compressed);
 static size_t VolStackBytes(const DeviceScene &S) {
@@ -1161,12 +1468,18 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
     const dim3 gT(VolGrid(maxCount, 1024)), gW(VolGrid(maxCount, 2048));
     if (S.compressed) hipLaunchKernelGGL(k_vclosest<true>, gT, block, VolStackBytes(S), s, S, st, v, wf);
     else hipLaunchKernelGGL(k_vclosest<false>, gT, block, VolStackBytes(S), s, S, st, v, wf);
-    hipLaunchKernelGGL(k_vmedium, gW, block, 0, s, S, st, v, wf);
+    if (S.media.allGrey) hipLaunchKernelGGL(k_vmedium_grey, gW, block, 0, s, S, st, v, wf);
+    else hipLaunchKernelGGL(k_vmedium, gW, block, 0, s, S, st, v, wf);
     hipLaunchKernelGGL(k_vsurface, gW, block, 0, s, S, st, v, wf);
     if (wf == S.maxDepth) return hipGetLastError();
     hipLaunchKernelGGL(k_vscatter, gW, block, 0, s, S, st, v, wf);
-    if (S.compressed) hipLaunchKernelGGL(k_vshadow<true>, gT, block, VolStackBytes(S), s, S, st, v, wf);
-    else hipLaunchKernelGGL(k_vshadow<false>, gT, block, VolStackBytes(S), s, S, st, v, wf);
+    if (S.media.allGrey) {
+        if (S.compressed) hipLaunchKernelGGL(k_vshadow_grey<true>, gT, block, VolStackBytes(S), s, S, st, v, wf);
+        else hipLaunchKernelGGL(k_vshadow_grey<false>, gT, block, VolStackBytes(S), s, S, st, v, wf);
+    } else {
+        if (S.compressed) hipLaunchKernelGGL(k_vshadow<true>, gT, block, VolStackBytes(S), s, S, st, v, wf);
+        else hipLaunchKernelGGL(k_vshadow<false>, gT, block, VolStackBytes(S), s, S, st, v, wf);
+    }
     return hipGetLastError();
 }
 

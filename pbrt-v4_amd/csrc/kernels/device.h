@@ -221,7 +221,8 @@ struct VolRecords {
     float *ray;                // [6][NR] o, d
     float *prev;               // [12][NR] prevIntrCtx: p, pErr, n, ns
     float *lambda0, *etaScale; // [NR]
-    int *flags;                // [NR] bit0 specularBounce, bit1 anyNonSpecularBounces
+    int *flags;                // [NR] bit0 specularBounce, bit1 anyNonSpecularBounces, bits 2-4:
+                               // beta / r_u / r_l stored uniform (entry 0 only, volpath.hip)
     int *pixel, *depth, *medium;
 };
 // queues of one iteration (counters at CounterIndex(iteration, queue, shard))
@@ -236,6 +237,7 @@ struct VolState {
     float *shLd, *shRu, *shRl; // [31][NR]
     float *shLambda0;          // [NR]
     int *shPixel, *shMedium;   // [NR]
+    int *shFlags;              // [NR] uniform-spectrum bits (volpath.hip kShUni*)
 };
 
 }  // namespace pbrt_amd

@@ -396,15 +396,53 @@ __device__ inline VRaySamples RaySamplesAt(const DeviceScene &S, const PathState
     return r;
 }
 
-// Spectral record I/O (wavelength-major)
-__device__ inline void LoadSpec(const float *base, int NR, int ri, float v[kNS]) {
+// Spectral record I/O (wavelength-major).  A spectrum whose 31 entries are equal is stored
+// "uniform": only entry 0 is written and a flag bit says so (camera rays, grey media and grey
+// materials keep beta, r_u and r_l uniform; most shadow rays' r_u, r_l too), which takes 30 of
+// every 31 record loads and stores off the HBM stream.  The values read back are the same bits.
+constexpr int kUniBeta = 4, kUniRu = 8, kUniRl = 16;      // VolRecords::flags
+constexpr int kShUniLd = 1, kShUniRu = 2, kShUniRl = 4;   // VolState::shFlags
+__device__ inline void LoadSpec(const float *base, int NR, int ri, float v[kNS], bool uni = false) {
+    if (uni) {
+        const float x = base[ri];
+#pragma unroll
+        for (int i = 0; i < kNS; ++i) v[i] = x;
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < kNS; ++i) v[i] = base[(size_t)i * NR + ri];
 }
-__device__ inline void StoreSpec(float *base, int NR, int ri, const float v[kNS]) {
+__device__ inline bool AllEqual(const float v[kNS]) {
+    bool eq = true;
+#pragma unroll
+    for (int i = 1; i < kNS; ++i) eq &= FloatToBits(v[i]) == FloatToBits(v[0]);
+    return eq;
+}
+// Stores v (uniform when all 31 entries have the same bits); returns whether it did so
+__device__ inline bool StoreSpec(float *base, int NR, int ri, const float v[kNS]) {
+    const bool uni = AllEqual(v);
+    if (uni) {
+        base[ri] = v[0];
+        return true;
+    }
 #pragma unroll
     for (int i = 0; i < kNS; ++i) base[(size_t)i * NR + ri] = v[i];
+    return false;
 }
+// Entry i of a possibly-uniform record spectrum: entry 0 preloaded, the rest loaded only for
+// non-uniform spectra (lanes with uniform ones skip the load)
+struct SpecIn {
+    const float *p;
+    int NR;
+    bool uni;
+    float v0;
+    __device__ SpecIn(const float *base, int NR_, int ri, bool u) : p(base + ri), NR(NR_), uni(u) { v0 = p[0]; }
+    __device__ float operator()(int i) const {
+        float x = v0;
+        if (!uni && i > 0) x = p[(size_t)i * NR];
+        return x;
+    }
+};
 __device__ inline V3 LoadV3(const float *base, int NR, int ri) {
     return V3(base[ri], base[NR + ri], base[2 * (size_t)NR + ri]);
 }
@@ -444,19 +482,16 @@ __global__ void __launch_bounds__(kBlock) k_vcamera(DeviceScene S, PathState st,
     st.L[2 * N + slot] = 0;
     if (!S.boxFilter) st.filterW[slot] = 1.f;
     const VolRecords &r = v.rec[0];
-#pragma unroll 8
-    for (int i = 0; i < kNS; ++i) {
-        r.beta[(size_t)i * NR + slot] = 1.f;
-        r.ru[(size_t)i * NR + slot] = 1.f;
-        r.rl[(size_t)i * NR + slot] = 1.f;
-    }
+    r.beta[slot] = 1.f;  // uniform spectra: entry 0 only (kUni* flags)
+    r.ru[slot] = 1.f;
+    r.rl[slot] = 1.f;
     StoreV3(r.ray, NR, slot, o);
     StoreV3(r.ray + 3 * (size_t)NR, NR, slot, d);
 #pragma unroll
     for (int k = 0; k < 12; ++k) r.prev[(size_t)k * NR + slot] = 0.f;
     r.lambda0[slot] = lambda0;
     r.etaScale[slot] = 1.f;
-    r.flags[slot] = 0;
+    r.flags[slot] = kUniBeta | kUniRu | kUniRl;
     r.pixel[slot] = slot;
     r.depth[slot] = 0;
     r.medium[slot] = S.media.cameraMedium;
@@ -518,10 +553,11 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vmedium(DeviceScene 
             const int depth = rec.depth[ri], slot = rec.pixel[ri];
             const MediumRef m = MediumAt(S, rec.medium[ri]);
             const WaveOffsets wo(rec.lambda0[ri]);
+            const int inFlags = rec.flags[ri];
             float beta[kNS], ru[kNS], rl[kNS], Tm[kNS];
-            LoadSpec(rec.beta, NR, ri, beta);
-            LoadSpec(rec.ru, NR, ri, ru);
-            LoadSpec(rec.rl, NR, ri, rl);
+            LoadSpec(rec.beta, NR, ri, beta, inFlags & kUniBeta);
+            LoadSpec(rec.ru, NR, ri, ru, inFlags & kUniRu);
+            LoadSpec(rec.rl, NR, ri, rl, inFlags & kUniRl);
             PCG32 rng(HashV3F(o, tHit), HashV3(d));
             const float uDist = rng.Uniform();
             float uMode = rng.Uniform();
@@ -624,15 +660,19 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vmedium(DeviceScene 
             }
             if (scattered) {
                 if (pushScatter) {
-                    StoreSpec(rec.beta, NR, ri, beta);
-                    StoreSpec(rec.ru, NR, ri, ru);
+                    int fl = inFlags & ~(kUniBeta | kUniRu);
+                    fl |= StoreSpec(rec.beta, NR, ri, beta) ? kUniBeta : 0;
+                    fl |= StoreSpec(rec.ru, NR, ri, ru) ? kUniRu : 0;
+                    rec.flags[ri] = fl;
                     StoreV3(v.hitB, NR, ri, pS);  // the scattering point replaces the hit
                     toScat = true;
                 }
             } else if (AnyNonZero(beta) && AnyNonZero(ru) && depth != S.maxDepth) {
-                StoreSpec(rec.beta, NR, ri, beta);
-                StoreSpec(rec.ru, NR, ri, ru);
-                StoreSpec(rec.rl, NR, ri, rl);
+                int fl = inFlags & ~(kUniBeta | kUniRu | kUniRl);
+                fl |= StoreSpec(rec.beta, NR, ri, beta) ? kUniBeta : 0;
+                fl |= StoreSpec(rec.ru, NR, ri, ru) ? kUniRu : 0;
+                fl |= StoreSpec(rec.rl, NR, ri, rl) ? kUniRl : 0;
+                rec.flags[ri] = fl;
                 toSurf = true;
             }
         }
@@ -671,14 +711,19 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_GREY_WAVES) k_vmedium_grey(De
             const int off0 = DenseOffset(lambda0);
             const int sa = m.I[1], ss = m.I[2], le = m.I[3];
             const float sa0 = DenseAt(S, sa, off0), ss0 = DenseAt(S, ss, off0);
-            // beta, r_u nonzero?  r_l spectrally constant?  (one pass over the records)
-            bool betaNz = false, ruNz = false, rlFlat = true;
-            const float rl0 = rec.rl[ri];
+            // beta, r_u nonzero?  r_l spectrally constant?  (uniform records: one value each)
+            const int inFlags = rec.flags[ri];
+            const bool betaUni = inFlags & kUniBeta, ruUni = inFlags & kUniRu, rlUni = inFlags & kUniRl;
+            const SpecIn betaIn(rec.beta, NR, ri, betaUni), ruIn(rec.ru, NR, ri, ruUni), rlIn(rec.rl, NR, ri, rlUni);
+            bool betaNz = betaIn.v0 != 0, ruNz = ruIn.v0 != 0, rlFlat = true;
+            const float rl0 = rlIn.v0;
+            if (!betaUni || !ruUni || !rlUni) {
 #pragma unroll 4
-            for (int i = 0; i < kNS; ++i) {
-                betaNz |= rec.beta[(size_t)i * NR + ri] != 0;
-                ruNz |= rec.ru[(size_t)i * NR + ri] != 0;
-                rlFlat &= rec.rl[(size_t)i * NR + ri] == rl0;
+                for (int i = 1; i < kNS; ++i) {
+                    betaNz |= betaIn(i) != 0;
+                    ruNz |= ruIn(i) != 0;
+                    rlFlat &= rlIn(i) == rl0;
+                }
             }
             float fb = 1.f;     // product of the (non-unit) beta / r_u factors
             float rlS = rl0;    // r_l when spectrally constant (exact)
@@ -711,7 +756,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_GREY_WAVES) k_vmedium_grey(De
 #pragma unroll 1
                         for (int i = 0; i < kNS; ++i, it.Next()) {
                             leNz |= DenseAt(S, le, DenseOffset(it.lam)) * mp.le != 0;
-                            float ru = rec.ru[(size_t)i * NR + ri];
+                            float ru = ruIn(i);
                             if (fb != 1.f) ru *= fb;
                             const float re = ru * smaj * T / pr;
                             reNz |= re != 0;
@@ -725,7 +770,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_GREY_WAVES) k_vmedium_grey(De
 #pragma unroll 1
                         for (int i = 0; i < kNS; ++i, it.Next()) {
                             const int off = DenseOffset(it.lam);
-                            float b = rec.beta[(size_t)i * NR + ri];
+                            float b = betaIn(i);
                             if (fb != 1.f) b *= fb;
                             const float Le = DenseAt(S, le, off) * mp.le;
                             acc.Add(S, off, b * sad * T * Le / den, i == 0);
@@ -775,32 +820,27 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_GREY_WAVES) k_vmedium_grey(De
                 gl *= f;
             }
             const bool alive = betaNz && !fbZero;
+            // write back only what changed (a non-unit beta / r_u factor is rare: x / x == 1)
+            auto scaleBetaRu = [&]() __attribute__((always_inline)) {
+                if (fb == 1.f) return;
+                for (int i = 0; i < (betaUni ? 1 : kNS); ++i) rec.beta[(size_t)i * NR + ri] *= fb;
+                for (int i = 0; i < (ruUni ? 1 : kNS); ++i) rec.ru[(size_t)i * NR + ri] *= fb;
+            };
             if (scattered) {
                 if (pushScatter) {
-                    if (fb != 1.f) {
-#pragma unroll
-                        for (int i = 0; i < kNS; ++i) {
-                            rec.beta[(size_t)i * NR + ri] *= fb;
-                            rec.ru[(size_t)i * NR + ri] *= fb;
-                        }
-                    }
+                    scaleBetaRu();
                     StoreV3(v.hitB, NR, ri, pS);
                     toScat = true;
                 }
             } else if (alive && ruNz && depth != S.maxDepth) {
-                if (fb != 1.f) {
-#pragma unroll
-                    for (int i = 0; i < kNS; ++i) {
-                        rec.beta[(size_t)i * NR + ri] *= fb;
-                        rec.ru[(size_t)i * NR + ri] *= fb;
-                    }
-                }
-                if (rlS != rl0 || !rlFlat) {
-#pragma unroll
-                    for (int i = 0; i < kNS; ++i) {
-                        if (rlFlat) rec.rl[(size_t)i * NR + ri] = rlS;
-                        else rec.rl[(size_t)i * NR + ri] *= gl;
-                    }
+                scaleBetaRu();
+                if (rlFlat) {
+                    // r_l keeps one value: exact for every wavelength, stored uniform
+                    if (rlS != rl0 || !rlUni) rec.rl[ri] = rlS;
+                    if (!rlUni) rec.flags[ri] = inFlags | kUniRl;
+                } else {
+#pragma unroll 1
+                    for (int i = 0; i < kNS; ++i) rec.rl[(size_t)i * NR + ri] *= gl;
                 }
                 toSurf = true;
             }
@@ -820,9 +860,10 @@ __device__ inline void WriteShadow(const VolState &v, int NR, int j, const Shado
                                    const float *ru, const float *rl, float lambda0, int slot) {
     StoreV3(v.shRay, NR, j, s.o);
     StoreV3(v.shRay + 3 * (size_t)NR, NR, j, s.d);
-    StoreSpec(v.shLd, NR, j, Ld);
-    StoreSpec(v.shRu, NR, j, ru);
-    StoreSpec(v.shRl, NR, j, rl);
+    int fl = StoreSpec(v.shLd, NR, j, Ld) ? kShUniLd : 0;
+    fl |= StoreSpec(v.shRu, NR, j, ru) ? kShUniRu : 0;
+    fl |= StoreSpec(v.shRl, NR, j, rl) ? kShUniRl : 0;
+    v.shFlags[j] = fl;
     v.shLambda0[j] = lambda0;
     v.shPixel[j] = slot;
     v.shMedium[j] = s.medium;
@@ -867,12 +908,76 @@ __device__ inline bool SampleAreaLight(const DeviceScene &S, V3 refP, V3 refN, V
 }
 
 
-// The surface side of an iteration: escaped rays, interfaces, emission, materials.  Queue
-// appends happen where a lane decides to push (WavePush works on the lanes that reach it).
-__global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vsurface(DeviceScene S, PathState st, VolState v, int wf) {
+// Spectral contribution c(i, off) of the path's 31 wavelengths to sensor RGB, added to the
+// slot's L (film.h:95-100).  Rolled: the terms stream from the wavelength-major records.
+template <typename C>
+__device__ inline void AddSpecToL(const DeviceScene &S, const PathState &st, int slot, float lambda0, C &&c) {
+    SensorAcc acc;
+    SpectralIter it(lambda0);
+#pragma unroll 1
+    for (int i = 0; i < kNS; ++i, it.Next()) {
+        const int off = DenseOffset(it.lam);
+        acc.Add(S, off, c(i, off), i == 0);
+    }
+    const int NL = st.N;
+    st.L[slot] += S.imagingRatio * (acc.sx / kNS);
+    st.L[NL + slot] += S.imagingRatio * (acc.sy / kNS);
+    st.L[2 * NL + slot] += S.imagingRatio * (acc.sz / kNS);
+}
+
+// An area-light sample for a reference point (BVHLightSampler::Sample, then
+// DiffuseAreaLight::SampleLi with allowIncompletePDF, lights.cpp:743-775); false when no light,
+// no sample, or Le = 0 at every wavelength.  Le_i = scale * dense[spectrum][off_i] when facing.
+struct AreaLightHit {
+    V3 p, pErr, n;
+    float pdf;  // shape pdf * light-choice pmf
+    float scale;
+    int spectrum;
+};
+__device__ inline bool SampleAreaLightAt(const DeviceScene &S, V3 refP, V3 refN, V3 refNs, float uc, float u0, float u1,
+                                         float lambda0, AreaLightHit *out) {
+    int li;
+    float lpmf;
+    if (!SampleLight(S, refP, refNs, uc, &li, &lpmf) || li >= S.nAreaLights) return false;
+    const DeviceAreaLight Ld = S.lights[li];
+    const V3 q0(Ld.v0.x, Ld.v0.y, Ld.v0.z), q1(Ld.v1.x, Ld.v1.y, Ld.v1.z), q2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
+    TriShading lsh;
+    const bool lhas = LoadTriShading(S, __float_as_int(Ld.v0.w), &lsh);
+    V3 lp, lpe, ln;
+    float lpdf;
+    if (!SampleTriangle(q0, q1, q2, Ld.flip, lhas ? &lsh : nullptr, refP, refN, refNs, u0, u1, &lp, &lpe, &ln, &lpdf) ||
+        lpdf == 0 || LengthSquared(lp - refP) == 0)
+        return false;
+    const V3 wi = Normalize(lp - refP);
+    if (!(Ld.twoSided || DotN(ln, -wi) >= 0)) return false;  // L() = 0 on the back side
+    bool nz = false;
+    SpectralIter it(lambda0);
+#pragma unroll 1
+    for (int i = 0; i < kNS; ++i, it.Next()) nz |= Ld.scale * DenseAt(S, Ld.spectrum, DenseOffset(it.lam)) != 0;
+    if (!nz) return false;
+    out->p = lp;
+    out->pErr = lpe;
+    out->n = ln;
+    out->pdf = lpdf * lpmf;
+    out->scale = Ld.scale;
+    out->spectrum = Ld.spectrum;
+    return true;
+}
+
+#ifndef PBRT_VOL_SURF_WAVES
+#define PBRT_VOL_SURF_WAVES 3  // waves/SIMD of k_vsurface
+#endif
+
+// The surface side of an iteration: escaped rays, interfaces, emission, materials.  Spectral
+// quantities stream from the wavelength-major records in rolled loops; the one 31-wide
+// intermediate (f, then beta') lives in LDS ([31][kBlock], conflict-free).  Queue appends happen
+// where a lane decides to push (WavePush serves the lanes that reach it).
+__global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(DeviceScene S, PathState st, VolState v, int wf) {
+    __shared__ float fbuf[kNS * kBlock];
+    float *fL = fbuf + threadIdx.x;  // fL[i * kBlock]
     const QueueView surf = LoadQueue(st, wf, kVSurf);
     const int NR = st.NR;
-    const VolRecords &rec = v.rec[wf & 1];
+    const VolRecords &rec = v.rec[wf & 1], &out = v.rec[(wf + 1) & 1];
     const int shard = ProducerShard();
     const int shardBase = shard * st.capS;
     int *nextCnt = &st.counters[CounterIndex(wf + 1, kVRay, shard)];
@@ -882,30 +987,34 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vsurface(DeviceScene
         const int ri = v.surfQ[QueueSlot(surf, j)];
         const float lambda0 = rec.lambda0[ri];
         const int slot = rec.pixel[ri];
-        const WaveOffsets wo(lambda0);
         const int depth = rec.depth[ri], flags = rec.flags[ri], medium = rec.medium[ri];
         const bool specularBounce = flags & 1;
-        float beta[kNS], ru[kNS], rl[kNS];
-        LoadSpec(rec.beta, NR, ri, beta);
-        LoadSpec(rec.ru, NR, ri, ru);
-        LoadSpec(rec.rl, NR, ri, rl);
+        const bool betaUni = flags & kUniBeta, ruUni = flags & kUniRu, rlUni = flags & kUniRl;
+        const SpecIn betaIn(rec.beta, NR, ri, betaUni), ruIn(rec.ru, NR, ri, ruUni), rlIn(rec.rl, NR, ri, rlUni);
         const V3 rd = LoadV3(rec.ray + 3 * (size_t)NR, NR, ri);
         const int prim = v.hitPrim[ri];
         if (prim < 0) {
             // HandleEscapedRays (integrator.cpp:495-537): UniformInfiniteLight, whose
             // PDF_Li(allowIncompletePDF) is 0, so r_l adds nothing to the MIS denominator
-            float den[kNS];
-#pragma unroll
-            for (int i = 0; i < kNS; ++i) den[i] = (depth == 0 || specularBounce) ? ru[i] : ru[i] + rl[i] * 0.f;
-            const float avg = AvgArr(den);
+            if (S.nInfinite == 0) continue;
+            float ds = 0;
+#pragma unroll 1
+            for (int i = 0; i < kNS; ++i) {
+                const float ru = ruIn(i);
+                const float dv = (depth == 0 || specularBounce) ? ru : ru + rlIn(i) * 0.f;
+                ds = i == 0 ? dv : ds + dv;
+            }
+            const float avg = ds / kNS;
             for (int k = 0; k < S.nInfinite; ++k) {
                 const int spec = S.infSpectrum[k];
                 const float scale = S.infScale[k];
                 bool nz = false;
-#pragma unroll
-                for (int i = 0; i < kNS; ++i) nz |= scale * DenseAt(S, spec, wo.off[i]) != 0;
+                SpectralIter it(lambda0);
+#pragma unroll 1
+                for (int i = 0; i < kNS; ++i, it.Next()) nz |= scale * DenseAt(S, spec, DenseOffset(it.lam)) != 0;
                 if (!nz) continue;
-                AddToL(S, st, slot, wo, [&](int i) { return beta[i] * (scale * DenseAt(S, spec, wo.off[i])) / avg; });
+                AddSpecToL(S, st, slot, lambda0,
+                           [&](int i, int off) { return betaIn(i) * (scale * DenseAt(S, spec, off)) / avg; });
             }
             continue;
         }
@@ -921,12 +1030,16 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vsurface(DeviceScene
         if (mtype == 3) {
             // Material "interface": SpawnRay(ray.d) at the same path depth (media.cpp:193-203)
             if (last) continue;
-            const int pos = WavePush(nextCnt, true);
-            const int jn = shardBase + pos;
-            const VolRecords &out = v.rec[(wf + 1) & 1];
-            StoreSpec(out.beta, NR, jn, beta);
-            StoreSpec(out.ru, NR, jn, ru);
-            StoreSpec(out.rl, NR, jn, rl);
+            const int jn = shardBase + WavePush(nextCnt, true);
+            out.beta[jn] = betaIn.v0;
+            out.ru[jn] = ruIn.v0;
+            out.rl[jn] = rlIn.v0;
+#pragma unroll 2
+            for (int i = 1; i < kNS; ++i) {
+                if (!betaUni) out.beta[(size_t)i * NR + jn] = betaIn(i);
+                if (!ruUni) out.ru[(size_t)i * NR + jn] = ruIn(i);
+                if (!rlUni) out.rl[(size_t)i * NR + jn] = rlIn(i);
+            }
             StoreV3(out.ray, NR, jn, OffsetRayOrigin(si.p, si.pErr, si.n, rd));
             StoreV3(out.ray + 3 * (size_t)NR, NR, jn, rd);
 #pragma unroll
@@ -944,14 +1057,15 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vsurface(DeviceScene
         if (light >= 0) {
             const DeviceAreaLight Ld = S.lights[light];
             bool nz = false;
-#pragma unroll
-            for (int i = 0; i < kNS; ++i) nz |= Ld.scale * DenseAt(S, Ld.spectrum, wo.off[i]) != 0;
+            {
+                SpectralIter it(lambda0);
+#pragma unroll 1
+                for (int i = 0; i < kNS; ++i, it.Next()) nz |= Ld.scale * DenseAt(S, Ld.spectrum, DenseOffset(it.lam)) != 0;
+            }
             if (nz && (Ld.twoSided || DotN(si.n, wo3) >= 0)) {
-                float den[kNS];
-                if (depth == 0 || specularBounce) {
-#pragma unroll
-                    for (int i = 0; i < kNS; ++i) den[i] = ru[i];
-                } else {
+                const bool plain = depth == 0 || specularBounce;
+                float lightPDF = 0;
+                if (!plain) {
                     const V3 pp = LoadV3(rec.prev, NR, ri), pe = LoadV3(rec.prev + 3 * (size_t)NR, NR, ri);
                     const V3 pn = LoadV3(rec.prev + 6 * (size_t)NR, NR, ri);
                     const V3 pns = LoadV3(rec.prev + 9 * (size_t)NR, NR, ri);
@@ -960,13 +1074,19 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vsurface(DeviceScene
                     const bool lhas = LoadTriShading(S, __float_as_int(Ld.v0.w), &lsh);
                     const V3 l0(Ld.v0.x, Ld.v0.y, Ld.v0.z), l1(Ld.v1.x, Ld.v1.y, Ld.v1.z),
                         l2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
-                    const float lightPDF =
+                    lightPDF =
                         lightChoicePDF * TrianglePDF(l0, l1, l2, Ld.flip, lhas ? &lsh : nullptr, pp, pe, pn, pns, -wo3);
-#pragma unroll
-                    for (int i = 0; i < kNS; ++i) den[i] = ru[i] + rl[i] * lightPDF;
                 }
-                const float avg = AvgArr(den);
-                AddToL(S, st, slot, wo, [&](int i) { return beta[i] * (Ld.scale * DenseAt(S, Ld.spectrum, wo.off[i])) / avg; });
+                float ds = 0;
+#pragma unroll 1
+                for (int i = 0; i < kNS; ++i) {
+                    const float ru = ruIn(i);
+                    const float dv = plain ? ru : ru + rlIn(i) * lightPDF;
+                    ds = i == 0 ? dv : ds + dv;
+                }
+                const float avg = ds / kNS;
+                AddSpecToL(S, st, slot, lambda0,
+                           [&](int i, int off) { return betaIn(i) * (Ld.scale * DenseAt(S, Ld.spectrum, off)) / avg; });
             }
         }
         if (last) continue;
@@ -992,11 +1112,20 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vsurface(DeviceScene
                 *k = 2 * std::sqrt(r) / std::sqrt(std::fmax(0.f, 1 - r));
             }
         };
+        // f_i of the material's BxDF given its per-sample terms (diffuse R/pi, dielectric scalar,
+        // conductor Fresnel per wavelength)
+        auto fAt = [&](float lam, float fd, const ConductorTerms &ct) -> float {
+            if (mtype == 0) return Reflectance(mc, constant, lam) * kInvPi;
+            if (mtype == 1) return fd;
+            float e, k;
+            etaK(lam, &e, &k);
+            return ConductorF(ct, e, k);
+        };
         // BxDF::Flags (bxdfs.h): diffuse R != 0; dielectric / conductor always
         bool hasFlags = mtype != 0;
         if (mtype == 0) {
             SpectralIter it(lambda0);
-#pragma unroll
+#pragma unroll 1
             for (int i = 0; i < kNS; ++i, it.Next()) hasFlags |= Reflectance(mc, constant, it.lam) != 0;
         }
         if (!hasFlags) continue;
@@ -1010,9 +1139,8 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vsurface(DeviceScene
             V3 cp = si.p;
             if (reflective && !transmissive) cp = OffsetRayOrigin(si.p, si.pErr, si.n, wo3);
             else if (transmissive && reflective) cp = OffsetRayOrigin(si.p, si.pErr, si.n, -wo3);
-            AreaLightSample ls;
-            float Le[kNS];
-            if (SampleAreaLight(S, cp, si.n, si.ns, rs.dUc, rs.dU0, rs.dU1, wo, &ls, Le) && woL.z != 0) {
+            AreaLightHit ls;
+            if (SampleAreaLightAt(S, cp, si.n, si.ns, rs.dUc, rs.dU0, rs.dU1, lambda0, &ls) && woL.z != 0) {
                 const V3 wi = Normalize(ls.p - cp);
                 const V3 wiL = frame.ToLocal(wi);
                 // BSDF::f / BSDF::PDF (bsdf.h:60-135)
@@ -1031,40 +1159,46 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vsurface(DeviceScene
                     fAny = ct.ok;
                 }
                 if (fAny) {
+                    // Ld_i = beta_i f_i |cos| Le_i into LDS (uniform check), r_u / r_l follow r_u
                     const float absdot = AbsDotN(si.ns, wi);
-                    float f[kNS];
-                    bool fnz = false;
-                    SpectralIter it(lambda0);
-#pragma unroll
-                    for (int i = 0; i < kNS; ++i, it.Next()) {
-                        if (mtype == 0) {
-                            f[i] = Reflectance(mc, constant, it.lam) * kInvPi;
-                        } else if (mtype == 1) {
-                            f[i] = fd;
-                        } else {
-                            float e, k;
-                            etaK(it.lam, &e, &k);
-                            f[i] = ConductorF(ct, e, k);
+                    bool fnz = false, ldUni = true;
+                    {
+                        SpectralIter it(lambda0);
+#pragma unroll 1
+                        for (int i = 0; i < kNS; ++i, it.Next()) {
+                            const float f = fAt(it.lam, fd, ct);
+                            fnz |= f != 0;
+                            const float Le = ls.scale * DenseAt(S, ls.spectrum, DenseOffset(it.lam));
+                            const float Ldv = betaIn(i) * f * absdot * Le;
+                            fL[i * kBlock] = Ldv;
+                            ldUni &= FloatToBits(Ldv) == FloatToBits(fL[0]);
                         }
-                        fnz |= f[i] != 0;
                     }
                     if (fnz) {
                         const float lightPDF = ls.pdf;
-                        float Ld[kNS], sru[kNS], srl[kNS];
-#pragma unroll
-                        for (int i = 0; i < kNS; ++i) {
-                            Ld[i] = beta[i] * f[i] * absdot * Le[i];
-                            sru[i] = ru[i] * bsdfPDF;
-                            srl[i] = ru[i] * lightPDF;
-                        }
                         // SpawnRayTo(pi, n, time, pLight.pi, pLight.n) (ray.h:106-111)
-                        ShadowOut so;
-                        so.o = OffsetRayOrigin(si.p, si.pErr, si.n, ls.p - si.p);
-                        const V3 pt = OffsetRayOrigin(ls.p, ls.pErr, ls.n, so.o - ls.p);
-                        so.d = pt - so.o;
-                        so.medium = DotN(si.n, so.d) > 0 ? mOut : mIn;
-                        const int pos = WavePush(shadowCnt, true);
-                        WriteShadow(v, NR, shardBase + pos, so, Ld, sru, srl, lambda0, slot);
+                        const V3 so = OffsetRayOrigin(si.p, si.pErr, si.n, ls.p - si.p);
+                        const V3 pt = OffsetRayOrigin(ls.p, ls.pErr, ls.n, so - ls.p);
+                        const V3 sd = pt - so;
+                        const int js = shardBase + WavePush(shadowCnt, true);
+                        v.shLd[js] = fL[0];
+                        v.shRu[js] = ruIn.v0 * bsdfPDF;
+                        v.shRl[js] = ruIn.v0 * lightPDF;
+#pragma unroll 2
+                        for (int i = 1; i < kNS; ++i) {
+                            if (!ldUni) v.shLd[(size_t)i * NR + js] = fL[i * kBlock];
+                            if (!ruUni) {
+                                const float ru = ruIn(i);
+                                v.shRu[(size_t)i * NR + js] = ru * bsdfPDF;
+                                v.shRl[(size_t)i * NR + js] = ru * lightPDF;
+                            }
+                        }
+                        v.shFlags[js] = (ldUni ? kShUniLd : 0) | (ruUni ? kShUniRu | kShUniRl : 0);
+                        StoreV3(v.shRay, NR, js, so);
+                        StoreV3(v.shRay + 3 * (size_t)NR, NR, js, sd);
+                        v.shLambda0[js] = lambda0;
+                        v.shPixel[js] = slot;
+                        v.shMedium[js] = DotN(si.n, sd) > 0 ? mOut : mIn;
                     }
                 }
             }
@@ -1102,48 +1236,53 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vsurface(DeviceScene
         const float absdot = AbsDotN(si.ns, wi);
         float etaScale = rec.etaScale[ri];
         if (transmission) etaScale *= Sqr(etap);
+        float rus = 0;
+#pragma unroll 1
+        for (int i = 0; i < kNS; ++i) rus = i == 0 ? ruIn.v0 : rus + ruIn(i);
+        const float avgRu = rus / kNS;
         bool fAny = false;
+        float mx = -kInfinity;
         {
             SpectralIter it(lambda0);
-#pragma unroll
+#pragma unroll 1
             for (int i = 0; i < kNS; ++i, it.Next()) {
-                float f = fd;
-                if (mtype == 0) {
-                    f = Reflectance(mc, constant, it.lam) * kInvPi;
-                } else if (mtype == 2) {
-                    float e, k;
-                    etaK(it.lam, &e, &k);
-                    f = ConductorF(ct, e, k);
-                }
+                const float f = fAt(it.lam, fd, ct);
                 fAny |= f != 0;
-                beta[i] = beta[i] * f * absdot / pdf;
+                const float nb = betaIn(i) * f * absdot / pdf;
+                fL[i * kBlock] = nb;
+                mx = fmaxf(mx, nb * etaScale / avgRu);
             }
         }
         if (!fAny) continue;
-        const float avgRu = AvgArr(ru);
-        float mx = -kInfinity;
-#pragma unroll
-        for (int i = 0; i < kNS; ++i) mx = fmaxf(mx, beta[i] * etaScale / avgRu);
         const bool rrOn = mx < 1 && depth >= 1;
         float q = 0;
         if (rrOn) {
             q = fmaxf(0.f, 1 - mx);
             if (rs.rr < q) continue;
         }
-        bool nz = false;
-#pragma unroll
+        bool nz = false, nbUni = true;
+#pragma unroll 1
         for (int i = 0; i < kNS; ++i) {
-            if (rrOn) beta[i] /= 1 - q;
-            nz |= beta[i] != 0;
-            rl[i] = ru[i] / pdf;
+            float nb = fL[i * kBlock];
+            if (rrOn) nb /= 1 - q;
+            fL[i * kBlock] = nb;
+            nz |= nb != 0;
+            nbUni &= FloatToBits(nb) == FloatToBits(fL[0]);
         }
         if (!nz) continue;
-        const int pos = WavePush(nextCnt, true);
-        const int jn = shardBase + pos;
-        const VolRecords &out = v.rec[(wf + 1) & 1];
-        StoreSpec(out.beta, NR, jn, beta);
-        StoreSpec(out.ru, NR, jn, ru);
-        StoreSpec(out.rl, NR, jn, rl);
+        const int jn = shardBase + WavePush(nextCnt, true);
+        out.beta[jn] = fL[0];
+        out.ru[jn] = ruIn.v0;
+        out.rl[jn] = ruIn.v0 / pdf;
+#pragma unroll 2
+        for (int i = 1; i < kNS; ++i) {
+            if (!nbUni) out.beta[(size_t)i * NR + jn] = fL[i * kBlock];
+            if (!ruUni) {
+                const float ru = ruIn(i);
+                out.ru[(size_t)i * NR + jn] = ru;
+                out.rl[(size_t)i * NR + jn] = ru / pdf;
+            }
+        }
         StoreV3(out.ray, NR, jn, OffsetRayOrigin(si.p, si.pErr, si.n, wi));
         StoreV3(out.ray + 3 * (size_t)NR, NR, jn, wi);
         StoreV3(out.prev, NR, jn, si.p);
@@ -1152,7 +1291,8 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vsurface(DeviceScene
         StoreV3(out.prev + 9 * (size_t)NR, NR, jn, si.ns);
         out.lambda0[jn] = lambda0;
         out.etaScale[jn] = etaScale;
-        out.flags[jn] = (specular ? 1 : 0) | ((!specular || (flags & 2)) ? 2 : 0);
+        out.flags[jn] = (specular ? 1 : 0) | ((!specular || (flags & 2)) ? 2 : 0) | (nbUni ? kUniBeta : 0) |
+                        (ruUni ? kUniRu | kUniRl : 0);
         out.pixel[jn] = slot;
         out.depth[jn] = depth + 1;
         out.medium[jn] = DotN(si.n, wi) > 0 ? mOut : mIn;
@@ -1173,9 +1313,10 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vscatter(DeviceScene
         const float lambda0 = rec.lambda0[ri];
         const int slot = rec.pixel[ri], depth = rec.depth[ri], medium = rec.medium[ri];
         const WaveOffsets wo(lambda0);
+        const int inFlags = rec.flags[ri];
         float beta[kNS], ru[kNS];
-        LoadSpec(rec.beta, NR, ri, beta);
-        LoadSpec(rec.ru, NR, ri, ru);
+        LoadSpec(rec.beta, NR, ri, beta, inFlags & kUniBeta);
+        LoadSpec(rec.ru, NR, ri, ru, inFlags & kUniRu);
         const V3 pS = LoadV3(v.hitB, NR, ri);
         const V3 wo3 = -LoadV3(rec.ray + 3 * (size_t)NR, NR, ri);
         const float g = MediumAt(S, medium).P[0];
@@ -1226,9 +1367,9 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vscatter(DeviceScene
         const int pos = WavePush(nextCnt, true);
         const int jn = shardBase + pos;
         const VolRecords &out = v.rec[(wf + 1) & 1];
-        StoreSpec(out.beta, NR, jn, beta);
-        StoreSpec(out.ru, NR, jn, ru);
-        StoreSpec(out.rl, NR, jn, rl);
+        int uni = StoreSpec(out.beta, NR, jn, beta) ? kUniBeta : 0;
+        uni |= StoreSpec(out.ru, NR, jn, ru) ? kUniRu : 0;
+        uni |= StoreSpec(out.rl, NR, jn, rl) ? kUniRl : 0;
         StoreV3(out.ray, NR, jn, pS);
         StoreV3(out.ray + 3 * (size_t)NR, NR, jn, wi);
         StoreV3(out.prev, NR, jn, pS);
@@ -1236,7 +1377,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vscatter(DeviceScene
         for (int k = 3; k < 12; ++k) out.prev[(size_t)k * NR + jn] = 0.f;
         out.lambda0[jn] = lambda0;
         out.etaScale[jn] = etaScale;
-        out.flags[jn] = 2;  // specularBounce = false, anyNonSpecularBounces = true
+        out.flags[jn] = 2 | uni;  // specularBounce = false, anyNonSpecularBounces = true
         out.pixel[jn] = slot;
         out.depth[jn] = depth + 1;
         out.medium[jn] = medium;
@@ -1341,14 +1482,15 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vshadow(DeviceScene 
         }
         if (blocked || !AnyNonZero(Tr)) continue;
         float Ld[kNS], den[kNS];
+        const int shf = v.shFlags[p];
         {
             float ru[kNS], rl[kNS];
-            LoadSpec(v.shRu, NR, p, ru);
-            LoadSpec(v.shRl, NR, p, rl);
+            LoadSpec(v.shRu, NR, p, ru, shf & kShUniRu);
+            LoadSpec(v.shRl, NR, p, rl, shf & kShUniRl);
 #pragma unroll
             for (int i = 0; i < kNS; ++i) den[i] = ru[i] * tu[i] + rl[i] * tl[i];
         }
-        LoadSpec(v.shLd, NR, p, Ld);
+        LoadSpec(v.shLd, NR, p, Ld, shf & kShUniLd);
         const float avg = AvgArr(den);
         AddToL(S, st, v.shPixel[p], wo, [&](int i) { return Ld[i] * Tr[i] / avg; });
     }
@@ -1428,18 +1570,20 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_vshadow_grey(D
         }
         if (blocked || Tr == 0) continue;
         // L += Ld T_ray / (r_u tu + r_l tl).Average(): rolled passes, no 31-wide arrays
+        const int shf = v.shFlags[p];
+        const SpecIn ruIn(v.shRu, NR, p, shf & kShUniRu), rlIn(v.shRl, NR, p, shf & kShUniRl),
+            ldIn(v.shLd, NR, p, shf & kShUniLd);
         float denSum = 0;
 #pragma unroll 1
         for (int i = 0; i < kNS; ++i) {
-            const float dv = v.shRu[(size_t)i * NR + p] * tu + v.shRl[(size_t)i * NR + p] * tl;
+            const float dv = ruIn(i) * tu + rlIn(i) * tl;
             denSum = i == 0 ? dv : denSum + dv;
         }
         const float avg = denSum / kNS;
         SensorAcc acc;
         SpectralIter it(lambda0);
 #pragma unroll 1
-        for (int i = 0; i < kNS; ++i, it.Next())
-            acc.Add(S, DenseOffset(it.lam), v.shLd[(size_t)i * NR + p] * Tr / avg, i == 0);
+        for (int i = 0; i < kNS; ++i, it.Next()) acc.Add(S, DenseOffset(it.lam), ldIn(i) * Tr / avg, i == 0);
         const int slot = v.shPixel[p], NL = st.N;
         st.L[slot] += S.imagingRatio * (acc.sx / kNS);
         st.L[NL + slot] += S.imagingRatio * (acc.sy / kNS);

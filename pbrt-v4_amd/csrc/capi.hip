@@ -437,7 +437,8 @@ static void BuildDevice(pbrt_context *c) {
             !std::all_of(b.begin(), b.end(), [&](float x) { return x == b[0]; }))
             S.media.allGrey = 0;
     }
-    if (getenv("PBRT_AMD_SPECTRAL_MEDIA")) S.media.allGrey = 0;  // force the spectral kernels (tests)
+    if (getenv("PBRT_AMD_SPECTRAL_MEDIA")) S.media.allGrey = 0;
+    S.media.denseInLds = s.denseSpectra.size() <= 12 ? 1 : 0;  // <= 15 KB of LDS per block  // force the spectral kernels (tests)
     S.media.info = c->mediumInfo.p;
     S.media.params = c->mediumParams.p;
     S.media.values = c->mediumValues.p;

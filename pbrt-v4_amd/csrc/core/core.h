@@ -1104,12 +1104,16 @@ PHD uint32_t OwenScramble(uint32_t v, uint32_t seed) {  // lowdiscrepancy.h:240-
 }
 // SobolSample (lowdiscrepancy.h:168-180) for dimension 0 or 1; matrix1 = the 52 rows above
 PHD float SobolSampleDim01(uint64_t a, int dim, Randomize rz, uint32_t seed, const uint32_t *matrix1) {
+    (void)matrix1;
     uint32_t v = 0;
     if (dim == 0) {
         v = ReverseBits32((uint32_t)a);  // rows >= 32 of dimension 0 are zero
     } else {
-        for (int i = 0; a != 0; a >>= 1, ++i)
-            if (a & 1) v ^= matrix1[i];
+        // row i of the dimension-1 matrix generated on the fly (SobolMatrix1Row: the top 32
+        // bits of the 52-bit recurrence follow the same recurrence in 32 bits), no table loads
+        uint32_t col = 1u << 31;
+        for (int i = 0; a != 0 && i < kSobolMatrixSize; a >>= 1, ++i, col ^= col >> 1)
+            if (a & 1) v ^= col;
     }
     if (rz == Randomize::PermuteDigits) v ^= seed;
     else if (rz == Randomize::FastOwen) v = FastOwenScramble(v, seed);
@@ -1120,18 +1124,34 @@ struct ZSobolParams {
     int log2SamplesPerPixel, nBase4Digits, seed;
     Randomize randomize;
 };
+// The 24 four-way digit permutations of ZSobolSampler (pbrt's order, host/build.cpp
+// kZSobolPermutations) packed 2 bits per entry: perm p, digit d at bit (p & 7) * 8 + 2 d of
+// word p >> 3 -- a register lookup instead of a table load per digit.
+PHD int ZSobolPermute(int p, int d) {
+    const uint64_t w = p < 8 ? 0xb1e19c6c78d8b4e4ull : (p < 16 ? 0x72d236c68d2d39c9ull : 0x93634b1b87271e4eull);
+    return (int)((w >> ((p & 7) * 8 + d * 2)) & 3);
+}
+// (h >> 24) % 24 of a 64-bit hash in 32-bit arithmetic: x = hi 2^32 + lo with hi < 2^8,
+// 2^32 = 16 (mod 24)
+PHD int Mod24Of40(uint64_t h) {
+    const uint32_t lo = (uint32_t)(h >> 24), hi = (uint32_t)(h >> 56);
+    return (int)((hi * 16u + lo % 24u) % 24u);
+}
 // samplers.h:301-356 GetSampleIndex; perms = the 24 four-way permutations in pbrt's order
+// (evaluated from the packed ZSobolPermute table; the argument is kept for the callers)
 PHD uint64_t ZSobolSampleIndex(const ZSobolParams &z, uint64_t mortonIndex, int dimension,
                                const uint8_t (*perms)[4]) {
+    (void)perms;
     uint64_t sampleIndex = 0;
     const bool pow2Samples = z.log2SamplesPerPixel & 1;
     const int lastDigit = pow2Samples ? 1 : 0;
+    const uint64_t dimHash = (uint64_t)(0x55555555u * (uint32_t)dimension);
     for (int i = z.nBase4Digits - 1; i >= lastDigit; --i) {
         int digitShift = 2 * i - (pow2Samples ? 1 : 0);
         int digit = (int)((mortonIndex >> digitShift) & 3);
         uint64_t higherDigits = mortonIndex >> (digitShift + 2);
-        int p = (int)((MixBits(higherDigits ^ (uint64_t)(0x55555555u * (uint32_t)dimension)) >> 24) % 24);
-        digit = perms[p][digit];
+        int p = Mod24Of40(MixBits(higherDigits ^ dimHash));
+        digit = ZSobolPermute(p, digit);
         sampleIndex |= uint64_t(digit) << digitShift;
     }
     if (pow2Samples) {

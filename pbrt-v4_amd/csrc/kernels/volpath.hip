@@ -914,7 +914,7 @@ template <typename C>
 __device__ inline void AddSpecToL(const DeviceScene &S, const PathState &st, int slot, float lambda0, C &&c) {
     SensorAcc acc;
     SpectralIter it(lambda0);
-#pragma unroll 1
+#pragma unroll 4
     for (int i = 0; i < kNS; ++i, it.Next()) {
         const int off = DenseOffset(it.lam);
         acc.Add(S, off, c(i, off), i == 0);
@@ -964,6 +964,27 @@ __device__ inline bool SampleAreaLightAt(const DeviceScene &S, V3 refP, V3 refN,
     return true;
 }
 
+// Per-block LDS copies of the tables the spectral loops read per wavelength: the sensor's
+// x/y/z curves and (when they fit, DeviceMedia::denseInLds) every dense spectrum.  The
+// kernel's scene copy is repointed at them, so DenseAt / SensorAcc read LDS.
+__device__ inline char *StageVolTables(const DeviceScene &S0, DeviceScene &S, char *lds) {
+    float4 *sensorL = reinterpret_cast<float4 *>(lds);
+    DmaCopy<16>(S0.sensor4, sensorL, kDenseN);
+    char *next = lds + kDenseN * 16;
+    if (S0.media.denseInLds) {
+        DmaCopy<4>(S0.dense, next, S0.nDense * kDenseN);
+        S.dense = reinterpret_cast<const float *>(next);
+        next += ((S0.nDense * kDenseN * 4 + 15) & ~15);
+    }
+    S.sensor4 = sensorL;
+    DmaWait();
+    __syncthreads();
+    return next;
+}
+size_t VolTablesLdsBytes(const DeviceScene &S) {
+    return kDenseN * 16 + (S.media.denseInLds ? ((S.nDense * kDenseN * 4 + 15) & ~15) : 0);
+}
+
 #ifndef PBRT_VOL_SURF_WAVES
 #define PBRT_VOL_SURF_WAVES 3  // waves/SIMD of k_vsurface
 #endif
@@ -972,10 +993,14 @@ __device__ inline bool SampleAreaLightAt(const DeviceScene &S, V3 refP, V3 refN,
 // quantities stream from the wavelength-major records in rolled loops; the one 31-wide
 // intermediate (f, then beta') lives in LDS ([31][kBlock], conflict-free).  Queue appends happen
 // where a lane decides to push (WavePush serves the lanes that reach it).
-__global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(DeviceScene S, PathState st, VolState v, int wf) {
-    __shared__ float fbuf[kNS * kBlock];
-    float *fL = fbuf + threadIdx.x;  // fL[i * kBlock]
+__global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(DeviceScene S0, PathState st, VolState v,
+                                                                       int wf) {
     const QueueView surf = LoadQueue(st, wf, kVSurf);
+    if ((int)(blockIdx.x * blockDim.x) >= surf.total) return;
+    extern __shared__ float4 dynLds[];
+    DeviceScene S = S0;
+    float *fbuf = reinterpret_cast<float *>(StageVolTables(S0, S, reinterpret_cast<char *>(dynLds)));
+    float *fL = fbuf + threadIdx.x;  // fL[i * kBlock]: [31][kBlock] per-lane spectra
     const int NR = st.NR;
     const VolRecords &rec = v.rec[wf & 1], &out = v.rec[(wf + 1) & 1];
     const int shard = ProducerShard();
@@ -1005,14 +1030,10 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
                 ds = i == 0 ? dv : ds + dv;
             }
             const float avg = ds / kNS;
+            // (a light with Le = 0 at every wavelength adds exact zeros: no separate test)
             for (int k = 0; k < S.nInfinite; ++k) {
                 const int spec = S.infSpectrum[k];
                 const float scale = S.infScale[k];
-                bool nz = false;
-                SpectralIter it(lambda0);
-#pragma unroll 1
-                for (int i = 0; i < kNS; ++i, it.Next()) nz |= scale * DenseAt(S, spec, DenseOffset(it.lam)) != 0;
-                if (!nz) continue;
                 AddSpecToL(S, st, slot, lambda0,
                            [&](int i, int off) { return betaIn(i) * (scale * DenseAt(S, spec, off)) / avg; });
             }
@@ -1056,13 +1077,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
         const int light = S.primLight[prim];
         if (light >= 0) {
             const DeviceAreaLight Ld = S.lights[light];
-            bool nz = false;
-            {
-                SpectralIter it(lambda0);
-#pragma unroll 1
-                for (int i = 0; i < kNS; ++i, it.Next()) nz |= Ld.scale * DenseAt(S, Ld.spectrum, DenseOffset(it.lam)) != 0;
-            }
-            if (nz && (Ld.twoSided || DotN(si.n, wo3) >= 0)) {
+            if (Ld.twoSided || DotN(si.n, wo3) >= 0) {  // Le = 0 everywhere would add exact zeros
                 const bool plain = depth == 0 || specularBounce;
                 float lightPDF = 0;
                 if (!plain) {
@@ -1614,7 +1629,7 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
     else hipLaunchKernelGGL(k_vclosest<false>, gT, block, VolStackBytes(S), s, S, st, v, wf);
     if (S.media.allGrey) hipLaunchKernelGGL(k_vmedium_grey, gW, block, 0, s, S, st, v, wf);
     else hipLaunchKernelGGL(k_vmedium, gW, block, 0, s, S, st, v, wf);
-    hipLaunchKernelGGL(k_vsurface, gW, block, 0, s, S, st, v, wf);
+    hipLaunchKernelGGL(k_vsurface, gW, block, VolTablesLdsBytes(S) + kNS * kBlock * sizeof(float), s, S, st, v, wf);
     if (wf == S.maxDepth) return hipGetLastError();
     hipLaunchKernelGGL(k_vscatter, gW, block, 0, s, S, st, v, wf);
     if (S.media.allGrey) {

@@ -21,7 +21,12 @@
 // Records are keyed by their index in the iteration's ray queue; every queue is sharded like
 // the surface path's (device.h kShards).  Spectral state (beta, r_u, r_l, T_maj) lives in
 // registers inside a kernel and wavelength-major in HBM between kernels.
+#ifndef PBRT_VOL_EXPERIMENT
+#define PBRT_VOL_EXPERIMENT 0  // timing experiments only (tools/exp_*.sh), never in the product
+#endif
+#if PBRT_VOL_EXPERIMENT != 3
 #define PBRT_AMD_CR_MATH 1  // correctly rounded transcendentals (core.h): bit-identical to the oracle
+#endif
 #include "common.h"
 
 namespace pbrt_amd {
@@ -372,7 +377,12 @@ __device__ inline void AddToL(const DeviceScene &S, const PathState &st, int slo
 struct VRaySamples {
     float dUc, dU0, dU1, iUc, iU0, iU1, rr;
 };
-__device__ inline VRaySamples RaySamplesAt(const DeviceScene &S, const PathState &st, int slot, int depth) {
+// indirectUc: the BxDF reads indirect.uc (dielectric); otherwise that dimension is skipped
+__device__ inline VRaySamples RaySamplesAt(const DeviceScene &S, const PathState &st, int slot, int depth,
+                                           bool indirectUc = true) {
+#if PBRT_VOL_EXPERIMENT == 1
+    { const float u = (slot & 1023) * (1.f / 1024); return VRaySamples{u, u * 0.5f, 0.7f - u * 0.5f, 0.3f, u, 1 - u, 0.9f}; }
+#endif
     int px, py, sampleIndex;
     PixelOf(st, slot, &px, &py, &sampleIndex);
     px += S.px0;
@@ -382,14 +392,20 @@ __device__ inline VRaySamples RaySamplesAt(const DeviceScene &S, const PathState
         const uint64_t morton = ZSobolMortonIndex(S.zs, px, py, sampleIndex);
         r.dUc = ZSobolGet1D(S.zs, morton, d0, S.zsPerms, S.sobolM1);
         ZSobolGet2D(S.zs, morton, d0 + 1, S.zsPerms, S.sobolM1, &r.dU0, &r.dU1);
-        r.iUc = ZSobolGet1D(S.zs, morton, d0 + 3, S.zsPerms, S.sobolM1);
+        r.iUc = indirectUc ? ZSobolGet1D(S.zs, morton, d0 + 3, S.zsPerms, S.sobolM1) : 0.f;
         ZSobolGet2D(S.zs, morton, d0 + 4, S.zsPerms, S.sobolM1, &r.iU0, &r.iU1);
         r.rr = ZSobolGet1D(S.zs, morton, d0 + 6, S.zsPerms, S.sobolM1);
     } else {
         Halton h = StartPixelSample(S, px, py, sampleIndex, d0);
         r.dUc = Get1D(S, h);
         Get2D(S, h, &r.dU0, &r.dU1);
-        r.iUc = Get1D(S, h);
+        if (indirectUc) {
+            r.iUc = Get1D(S, h);
+        } else {  // Get1D's dimension bookkeeping without the sample
+            if (h.dimension >= S.nDims) h.dimension = 2;
+            ++h.dimension;
+            r.iUc = 0.f;
+        }
         Get2D(S, h, &r.iU0, &r.iU1);
         r.rr = Get1D(S, h);
     }
@@ -1106,7 +1122,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
         }
         if (last) continue;
         // ---- EvaluateMaterialAndBSDF (surfscatter.cpp:57-328) for this material type
-        const VRaySamples rs = RaySamplesAt(S, st, slot, depth);
+        const VRaySamples rs = RaySamplesAt(S, st, slot, depth, mtype == 1);
         const float4 mp4 = S.matParams[mat];
         const float4 mc = S.matCoeffs[mat];
         const bool constant = S.matConstant[mat];
@@ -1130,6 +1146,9 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
         // f_i of the material's BxDF given its per-sample terms (diffuse R/pi, dielectric scalar,
         // conductor Fresnel per wavelength)
         auto fAt = [&](float lam, float fd, const ConductorTerms &ct) -> float {
+#if PBRT_VOL_EXPERIMENT == 2
+            if (mtype == 0) return 0.4f * kInvPi;
+#endif
             if (mtype == 0) return Reflectance(mc, constant, lam) * kInvPi;
             if (mtype == 1) return fd;
             float e, k;
@@ -1137,11 +1156,16 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
             return ConductorF(ct, e, k);
         };
         // BxDF::Flags (bxdfs.h): diffuse R != 0; dielectric / conductor always
+        // (diffuse: f_i = R_i / pi is kept in LDS for the light sample and the BSDF sample)
         bool hasFlags = mtype != 0;
         if (mtype == 0) {
             SpectralIter it(lambda0);
-#pragma unroll 1
-            for (int i = 0; i < kNS; ++i, it.Next()) hasFlags |= Reflectance(mc, constant, it.lam) != 0;
+#pragma unroll 2
+            for (int i = 0; i < kNS; ++i, it.Next()) {
+                const float R = Reflectance(mc, constant, it.lam);
+                hasFlags |= R != 0;
+                fL[i * kBlock] = R * kInvPi;
+            }
         }
         if (!hasFlags) continue;
         const bool smooth = mtype != 0 && tr.EffectivelySmooth();
@@ -1174,10 +1198,29 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
                     fAny = ct.ok;
                 }
                 if (fAny) {
-                    // Ld_i = beta_i f_i |cos| Le_i into LDS (uniform check), r_u / r_l follow r_u
                     const float absdot = AbsDotN(si.ns, wi);
-                    bool fnz = false, ldUni = true;
-                    {
+                    const float lightPDF = ls.pdf;
+                    // SpawnRayTo(pi, n, time, pLight.pi, pLight.n) (ray.h:106-111)
+                    const V3 so = OffsetRayOrigin(si.p, si.pErr, si.n, ls.p - si.p);
+                    const V3 pt = OffsetRayOrigin(ls.p, ls.pErr, ls.n, so - ls.p);
+                    const V3 sd = pt - so;
+                    // Ld_i = beta_i f_i |cos| Le_i; r_u / r_l follow r_u
+                    bool fnz = mtype == 0, ldUni = true;
+                    int js = -1;
+                    if (mtype == 0) {
+                        // f_i from LDS (nonzero somewhere: the flags pass), Ld straight to the queue
+                        js = shardBase + WavePush(shadowCnt, true);
+                        SpectralIter it(lambda0);
+                        float ld0 = 0;
+#pragma unroll 2
+                        for (int i = 0; i < kNS; ++i, it.Next()) {
+                            const float Le = ls.scale * DenseAt(S, ls.spectrum, DenseOffset(it.lam));
+                            const float Ldv = betaIn(i) * fL[i * kBlock] * absdot * Le;
+                            ld0 = i == 0 ? Ldv : ld0;
+                            ldUni &= FloatToBits(Ldv) == FloatToBits(ld0);
+                            v.shLd[(size_t)i * NR + js] = Ldv;
+                        }
+                    } else {
                         SpectralIter it(lambda0);
 #pragma unroll 1
                         for (int i = 0; i < kNS; ++i, it.Next()) {
@@ -1188,21 +1231,20 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
                             fL[i * kBlock] = Ldv;
                             ldUni &= FloatToBits(Ldv) == FloatToBits(fL[0]);
                         }
+                        if (fnz) {
+                            js = shardBase + WavePush(shadowCnt, true);
+                            v.shLd[js] = fL[0];
+#pragma unroll 2
+                            for (int i = 1; i < kNS; ++i)
+                                if (!ldUni) v.shLd[(size_t)i * NR + js] = fL[i * kBlock];
+                        }
                     }
                     if (fnz) {
-                        const float lightPDF = ls.pdf;
-                        // SpawnRayTo(pi, n, time, pLight.pi, pLight.n) (ray.h:106-111)
-                        const V3 so = OffsetRayOrigin(si.p, si.pErr, si.n, ls.p - si.p);
-                        const V3 pt = OffsetRayOrigin(ls.p, ls.pErr, ls.n, so - ls.p);
-                        const V3 sd = pt - so;
-                        const int js = shardBase + WavePush(shadowCnt, true);
-                        v.shLd[js] = fL[0];
                         v.shRu[js] = ruIn.v0 * bsdfPDF;
                         v.shRl[js] = ruIn.v0 * lightPDF;
+                        if (!ruUni) {
 #pragma unroll 2
-                        for (int i = 1; i < kNS; ++i) {
-                            if (!ldUni) v.shLd[(size_t)i * NR + js] = fL[i * kBlock];
-                            if (!ruUni) {
+                            for (int i = 1; i < kNS; ++i) {
                                 const float ru = ruIn(i);
                                 v.shRu[(size_t)i * NR + js] = ru * bsdfPDF;
                                 v.shRl[(size_t)i * NR + js] = ru * lightPDF;
@@ -1261,7 +1303,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
             SpectralIter it(lambda0);
 #pragma unroll 1
             for (int i = 0; i < kNS; ++i, it.Next()) {
-                const float f = fAt(it.lam, fd, ct);
+                const float f = mtype == 0 ? fL[i * kBlock] : fAt(it.lam, fd, ct);
                 fAny |= f != 0;
                 const float nb = betaIn(i) * f * absdot / pdf;
                 fL[i * kBlock] = nb;

@@ -36,6 +36,9 @@ sys.path.insert(0, str(ROOT / "pbrt-v4_amd"))
 #   reads  ray o,d 24 B
 #   writes hit prim 4 B + b0,b1,b2,t 16 B + material-queue entry 4 B = 24 B
 BYTES_PER_RAY_CLOSEST = 48
+# The media wavefront's closest-hit kernel (volpath.hip k_vclosest) also reads the ray's medium
+# (4 B) and always writes the hit (prim 4 + b0,b1,b2,t 16) and one queue entry (4): 52 B
+BYTES_PER_RAY_VCLOSEST = 52
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
 
@@ -92,9 +95,10 @@ def cpu_baseline(args, threads, sc):
     import numpy as np
     import pyoracle
     i = sc.info
-    # C2: every row, 16 of 64 spp; C3/C4: every 8th row, 4 spp (seconds of host work)
-    rows = np.arange(i.py0, i.py1, 1 if args.workload == "c2" else 8, dtype=np.int32)
-    spp = 16 if args.workload == "c2" else 4
+    # C2: every row, 16 of 64 spp; C3/C4: every 8th row, 4 spp; C5: every 2nd row, 8 spp
+    # (seconds of host work)
+    rows = np.arange(i.py0, i.py1, {"c2": 1, "c5": 2}.get(args.workload, 8), dtype=np.int32)
+    spp = {"c2": 16, "c5": 8}.get(args.workload, 4)
     pyoracle.lib()
     # the oracle builds its BVH inside every render call: time an empty render and subtract it
     t = time.perf_counter()
@@ -173,7 +177,8 @@ def main():
     value = samples / dt_max / 1e6
     launches = max(st.closest_launches, 1)
     mean_launch_s = st.closest_ms / 1e3 / launches
-    bytes_per_launch = BYTES_PER_RAY_CLOSEST * st.timed_closest_rays / launches
+    bpr = BYTES_PER_RAY_VCLOSEST if args.workload == "c5" else BYTES_PER_RAY_CLOSEST
+    bytes_per_launch = bpr * st.timed_closest_rays / launches
     achieved = bytes_per_launch / mean_launch_s / 1e9 if mean_launch_s > 0 else 0.0
     traffic = pmc_traffic() if args.workload == "c2" else None  # the committed PMC pass is of C2
 
@@ -216,8 +221,10 @@ def main():
                        "single GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "kernel": "k_closest (BVH8 traverse + hit record + wave64 ballot push to material queue)",
-                         "bytes_per_ray": BYTES_PER_RAY_CLOSEST,
+                         "kernel": ("k_vclosest (BVH8 traverse + hit record + push to medium / surface queue)"
+                                    if args.workload == "c5" else
+                                    "k_closest (BVH8 traverse + hit record + wave64 ballot push to material queue)"),
+                         "bytes_per_ray": bpr,
                          "rays_per_launch": round(st.timed_closest_rays / launches, 1),
                          "timed_launches": launches,
                          "mean_launch_us": round(mean_launch_s * 1e6, 3)},

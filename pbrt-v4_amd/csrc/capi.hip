@@ -27,6 +27,8 @@ hipError_t LaunchEmissive(const DeviceScene &S, const PathState &st, int depth, 
 hipError_t LaunchShadow(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
 hipError_t LaunchFilm(const DeviceScene &S, const PathState &st, int nSamples, hipStream_t s);
 hipError_t LaunchVolCamera(const DeviceScene &S, const PathState &st, const VolState &v, int nActive, hipStream_t s);
+hipError_t LaunchVolClosest(const DeviceScene &S, const PathState &st, const VolState &v, int wf, int maxCount,
+                            int timed, hipStream_t s);
 hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const VolState &v, int wf, int maxCount,
                               hipStream_t s);
 hipError_t LaunchIntersectBatch(const DeviceScene &S, const float *rays, int n, int anyHit, int *outPrim,
@@ -747,8 +749,13 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
             if (c->volumetric) {
                 // participating media: the volumetric wavefront (volpath.hip), same film update
                 HIPCHECK(LaunchVolCamera(c->S, st, c->vs, (int)nActive, c->stream));
-                for (int wf = 0; wf <= s.maxDepth; ++wf)
+                for (int wf = 0; wf <= s.maxDepth; ++wf) {
+                    const bool timed = p->time_closest && r0 == 0 && s0 == 0;
+                    if (timed) RecordEvent(c, true);
+                    HIPCHECK(LaunchVolClosest(c->S, st, c->vs, wf, (int)nActive, timed ? 1 : 0, c->stream));
+                    if (timed) RecordEvent(c, false);
                     HIPCHECK(LaunchVolIteration(c->S, st, c->vs, wf, (int)nActive, c->stream));
+                }
                 HIPCHECK(LaunchFilm(c->S, st, nS, c->stream));
                 c->stats.passes++;
                 c->stats.paths_per_pass = std::max<uint64_t>(c->stats.paths_per_pass, nActive);

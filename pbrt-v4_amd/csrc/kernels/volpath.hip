@@ -515,7 +515,7 @@ __global__ void __launch_bounds__(kBlock) k_vcamera(DeviceScene S, PathState st,
 
 template <bool Q>
 __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_vclosest(DeviceScene S, PathState st, VolState v,
-                                                                          int wf) {
+                                                                          int wf, int timed) {
     const QueueView rays = LoadQueue(st, wf, kVRay);
     if ((int)(blockIdx.x * blockDim.x) >= rays.total) return;
     extern __shared__ float4 dynLds[];
@@ -525,7 +525,10 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_vclosest(Devic
     const int shard = ProducerShard();
     int *medCnt = &st.counters[CounterIndex(wf, kVMed, shard)];
     int *surfCnt = &st.counters[CounterIndex(wf, kVSurf, shard)];
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&st.stats[1], (unsigned long long)rays.total);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        atomicAdd(&st.stats[1], (unsigned long long)rays.total);
+        if (timed) atomicAdd(&st.stats[3], (unsigned long long)rays.total);  // rays of event-timed launches
+    }
     for (int base = blockIdx.x * blockDim.x; base < rays.total; base += gridDim.x * blockDim.x) {
         const int j = base + threadIdx.x;
         const bool active = j < rays.total;
@@ -1663,12 +1666,18 @@ hipError_t LaunchVolCamera(const DeviceScene &S, const PathState &st, const VolS
     hipLaunchKernelGGL(k_vcamera, dim3((nActive + kBlock - 1) / kBlock), dim3(kBlock), 0, s, S, st, v, nActive);
     return hipGetLastError();
 }
+hipError_t LaunchVolClosest(const DeviceScene &S, const PathState &st, const VolState &v, int wf, int maxCount,
+                            int timed, hipStream_t s) {
+    const dim3 block(kBlock), gT(VolGrid(maxCount, 1024));
+    if (S.compressed) hipLaunchKernelGGL(k_vclosest<true>, gT, block, VolStackBytes(S), s, S, st, v, wf, timed);
+    else hipLaunchKernelGGL(k_vclosest<false>, gT, block, VolStackBytes(S), s, S, st, v, wf, timed);
+    return hipGetLastError();
+}
+// the rest of wavefront iteration wf after its closest-hit launch
 hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const VolState &v, int wf, int maxCount,
                               hipStream_t s) {
     const dim3 block(kBlock);
     const dim3 gT(VolGrid(maxCount, 1024)), gW(VolGrid(maxCount, 2048));
-    if (S.compressed) hipLaunchKernelGGL(k_vclosest<true>, gT, block, VolStackBytes(S), s, S, st, v, wf);
-    else hipLaunchKernelGGL(k_vclosest<false>, gT, block, VolStackBytes(S), s, S, st, v, wf);
     if (S.media.allGrey) hipLaunchKernelGGL(k_vmedium_grey, gW, block, 0, s, S, st, v, wf);
     else hipLaunchKernelGGL(k_vmedium, gW, block, 0, s, S, st, v, wf);
     hipLaunchKernelGGL(k_vsurface, gW, block, VolTablesLdsBytes(S) + kNS * kBlock * sizeof(float), s, S, st, v, wf);

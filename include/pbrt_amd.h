@@ -18,7 +18,10 @@
  *       WavefrontAggregate::IntersectClosest / IntersectShadow (wavefront/integrator.h:32-54)
  *       over caller-owned device SoA ray buffers.
  *   pbrt_film_*
- *       RGBFilm pixel storage (film.h:305-310) and GetPixelRGB (film.h:261-277).
+ *       RGBFilm pixel storage (film.h:305-310), GetPixelRGB (film.h:261-277) and
+ *       RGBFilm::WriteImage (film.cpp) to EXR / PFM / PNG.
+ *   pbrt_image_*
+ *       imgtool's diff / error metrics (cmd/imgtool.cpp:960-1105) and Image::Read.
  *
  * Conventions: 0 = success, nonzero = error with text from pbrt_last_error(); device
  * buffers are caller-owned where passed in; one hipStream per context; nothing blocks
@@ -151,6 +154,22 @@ int pbrt_film_clear(pbrt_context *ctx);
 int pbrt_film_device_ptr(pbrt_context *ctx, double **film, size_t *n_doubles);
 int pbrt_film_read(pbrt_context *ctx, double *out);     /* [4][xres*yres] sensor RGB sums + weight */
 int pbrt_film_get_rgb(pbrt_context *ctx, float *rgb);   /* [yres*xres][3] output colour space */
+
+/* Film output (RGBFilm::WriteImage, film.cpp; Image::Write, util/image.cpp:990-1012): the
+ * film's output-colour-space RGB written by extension: .exr (OpenEXR scanline, uncompressed;
+ * half floats unless write_fp16 = 0, pbrt's "writefp16"), .pfm (Image::WritePFM), .png (8-bit
+ * sRGB). */
+int pbrt_film_write_image(pbrt_context *ctx, const char *path, int write_fp16);
+/* imgtool (cmd/imgtool.cpp:960-1105) image access and error metrics, host only.
+ * pbrt_image_read_size then pbrt_image_read into a caller-owned [h][w][3] float buffer
+ * (.pfm, uncompressed .exr).  pbrt_image_error: metric "MAE" (pbrt's signed mean
+ * difference), "MSE" or "MRSE" per channel over [h][w][3] images (Image::MAE / MSE / MRSE,
+ * util/image.cpp:543-639). */
+int pbrt_image_read_size(const char *path, int *width, int *height);
+int pbrt_image_read(const char *path, float *rgb, int width, int height);
+int pbrt_image_write(const char *path, const float *rgb, int width, int height, int write_fp16);
+int pbrt_image_error(const float *image, const float *reference, int width, int height, const char *metric,
+                     double *error3);
 
 /* WavefrontAggregate boundary: rays_dev = [7][n] SoA (o.xyz, d.xyz, tMax) on the device;
  * prim_dev [n] receives the original triangle index or -1; hit_dev [4][n] b0 b1 b2 t. */

@@ -12,6 +12,7 @@
 
 #include "../../include/pbrt_amd.h"
 #include "host/bvh.h"
+#include "host/image.h"
 #include "host/scene.h"
 #include "kernels/device.h"
 
@@ -1053,6 +1054,66 @@ int pbrt_film_get_rgb(pbrt_context *ctx, float *rgb) {
             for (int k = 0; k < 3; ++k)
                 rgb[3 * i + k] = (float)(m[k][0] * c[0] + m[k][1] * c[1] + m[k][2] * c[2]);
         }
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_film_write_image(pbrt_context *ctx, const char *path, int writeFP16) {
+    try {
+        if (!ctx || !path) return Fail("null argument");
+        std::vector<float> rgb((size_t)ctx->desc.xres * ctx->desc.yres * 3);
+        if (pbrt_film_get_rgb(ctx, rgb.data())) return 1;
+        WriteImage(path, rgb.data(), ctx->desc.xres, ctx->desc.yres, writeFP16 != 0);
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_image_read_size(const char *path, int *width, int *height) {
+    try {
+        Image im = ReadImage(path);
+        *width = im.width;
+        *height = im.height;
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_image_read(const char *path, float *rgb, int width, int height) {
+    try {
+        Image im = ReadImage(path);
+        if (im.width != width || im.height != height) return Fail(std::string(path) + ": resolution mismatch");
+        std::copy(im.rgb.begin(), im.rgb.end(), rgb);
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_image_write(const char *path, const float *rgb, int width, int height, int writeFP16) {
+    try {
+        WriteImage(path, rgb, width, height, writeFP16 != 0);
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_image_error(const float *image, const float *reference, int width, int height, const char *metric,
+                     double *error3) {
+    try {
+        const std::string m = metric ? metric : "MSE";
+        ErrorMetric em;
+        if (m == "MAE") em = ErrorMetric::MAE;
+        else if (m == "MSE") em = ErrorMetric::MSE;
+        else if (m == "MRSE") em = ErrorMetric::MRSE;
+        else return Fail("--metric must be \"MAE\", \"MSE\", or \"MRSE\" (FLIP is not provided)");
+        const auto e = ImageError(image, reference, width, height, em);
+        for (int c = 0; c < 3; ++c) error3[c] = e[c];
         return 0;
     } catch (const std::exception &e) {
         return Fail(e.what());

@@ -1,0 +1,22 @@
+// Image output / input and imgtool's error metrics (host side; see image.cpp)
+#pragma once
+
+#include <array>
+#include <string>
+#include <vector>
+
+namespace pbrt_amd {
+
+struct Image {
+    int width = 0, height = 0;
+    std::vector<float> rgb;  // [height][width][3], row 0 = top
+};
+
+// by extension: .pfm (float), .exr (half unless exrHalf = false), .png (8-bit sRGB)
+void WriteImage(const std::string &path, const float *rgb, int w, int h, bool exrHalf = true);
+Image ReadImage(const std::string &path);  // .pfm, .exr (uncompressed scanline)
+
+enum class ErrorMetric { MAE = 0, MSE = 1, MRSE = 2 };
+std::array<double, 3> ImageError(const float *img, const float *ref, int w, int h, ErrorMetric metric);
+
+}  // namespace pbrt_amd

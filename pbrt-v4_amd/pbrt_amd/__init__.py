@@ -116,6 +116,11 @@ def _lib():
     lib.pbrt_scene_load.argtypes = [c.c_char_p, c.c_char_p, c.POINTER(c.c_void_p)]
     lib.pbrt_scene_load_string.argtypes = [c.c_char_p, c.c_char_p, c.c_char_p, c.POINTER(c.c_void_p)]
     lib.pbrt_scene_free.argtypes = [c.c_void_p]
+    lib.pbrt_film_write_image.argtypes = [c.c_void_p, c.c_char_p, c.c_int]
+    lib.pbrt_image_read_size.argtypes = [c.c_char_p, c.POINTER(c.c_int), c.POINTER(c.c_int)]
+    lib.pbrt_image_read.argtypes = [c.c_char_p, c.c_void_p, c.c_int, c.c_int]
+    lib.pbrt_image_write.argtypes = [c.c_char_p, c.c_void_p, c.c_int, c.c_int, c.c_int]
+    lib.pbrt_image_error.argtypes = [c.c_void_p, c.c_void_p, c.c_int, c.c_int, c.c_char_p, c.c_void_p]
     lib.pbrt_scene_get_info.argtypes = [c.c_void_p, c.POINTER(SceneInfo)]
     lib.pbrt_scene_get_flat.argtypes = [c.c_void_p, c.POINTER(SceneFlat)]
     lib.pbrt_device_count.argtypes = [c.POINTER(c.c_int)]
@@ -337,6 +342,10 @@ class WavefrontPathIntegrator:
         _check(_lib().pbrt_film_get_rgb(self._h, out.ctypes.data))
         return out
 
+    def write_image(self, path, write_fp16=True):
+        """RGBFilm::WriteImage: .exr (half unless write_fp16=False), .pfm or .png by extension."""
+        _check(_lib().pbrt_film_write_image(self._h, str(path).encode(), 1 if write_fp16 else 0))
+
     def __del__(self):
         if getattr(self, "_h", None) and _LIB is not None:
             _LIB.pbrt_context_free(self._h)
@@ -393,3 +402,48 @@ def read_pfm(path):
         scale = float(f.readline())
         data = np.frombuffer(f.read(), dtype="<f4" if scale < 0 else ">f4").reshape(h, w, 3)
     return data[::-1].copy()
+
+
+# ---------------------------------------------------------------- image I/O and imgtool metrics
+def write_image(path, rgb, write_fp16=True):
+    """Image::Write for a [h, w, 3] float image: .exr / .pfm / .png by extension."""
+    a = np.ascontiguousarray(rgb, dtype=np.float32)
+    if a.ndim != 3 or a.shape[2] != 3:
+        raise PbrtError("write_image expects an [h, w, 3] image")
+    _check(_lib().pbrt_image_write(str(path).encode(), a.ctypes.data, a.shape[1], a.shape[0], 1 if write_fp16 else 0))
+
+
+def read_image(path) -> np.ndarray:
+    """Image::Read of a .pfm or uncompressed .exr file -> [h, w, 3] float32 (R, G, B)."""
+    w, h = ctypes.c_int(), ctypes.c_int()
+    _check(_lib().pbrt_image_read_size(str(path).encode(), ctypes.byref(w), ctypes.byref(h)))
+    out = np.zeros((h.value, w.value, 3), np.float32)
+    _check(_lib().pbrt_image_read(str(path).encode(), out.ctypes.data, w.value, h.value))
+    return out
+
+
+def image_error(image, reference, metric="MSE") -> np.ndarray:
+    """Image::MAE / MSE / MRSE per channel (imgtool diff/error, cmd/imgtool.cpp:960-1105).
+    Like imgtool diff, infinite pixel values are set to 0 first."""
+    a = np.array(image, dtype=np.float32, copy=True)
+    b = np.array(reference, dtype=np.float32, copy=True)
+    if a.shape != b.shape or a.ndim != 3 or a.shape[2] != 3:
+        raise PbrtError(f"image resolution {a.shape[:2]} doesn't match reference {b.shape[:2]}")
+    a[np.isinf(a)] = 0
+    b[np.isinf(b)] = 0
+    out = np.zeros(3, np.float64)
+    _check(_lib().pbrt_image_error(a.ctypes.data, b.ctypes.data, a.shape[1], a.shape[0], metric.encode(),
+                                   out.ctypes.data))
+    return out
+
+
+def imgtool_diff(image_file, reference_file, metric="MSE"):
+    """imgtool diff (cmd/imgtool.cpp:1105-1275) without FLIP: reads both images, returns
+    {"image_average", "reference_average", "delta_percent", metric: average over channels}."""
+    a, b = read_image(image_file), read_image(reference_file)
+    a[np.isinf(a)] = 0
+    b[np.isinf(b)] = 0
+    err = image_error(a, b, metric)
+    ia, ra = float(a.mean()), float(b.mean())
+    return {"image_average": ia, "reference_average": ra,
+            "delta_percent": 100.0 * (ia - ra) / ra if ra != 0 else float("inf"), metric: float(err.mean())}

@@ -96,7 +96,8 @@ EXPORTED_SYMBOLS = [
     "pbrt_film_clear", "pbrt_film_device_ptr", "pbrt_film_read", "pbrt_film_get_rgb", "pbrt_intersect",
     "pbrt_debug_halton", "pbrt_debug_rgb_coeffs", "pbrt_debug_rgb2spec_column", "pbrt_debug_kernel_sections",
     "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
-    "pbrt_debug_named_spectrum", "pbrt_debug_bxdf", "pbrt_debug_triangle_shading",
+    "pbrt_debug_named_spectrum", "pbrt_debug_bxdf", "pbrt_debug_triangle_shading", "pbrt_film_write_image",
+    "pbrt_image_read_size", "pbrt_image_read", "pbrt_image_write", "pbrt_image_error",
 ]
 
 _LIB = None

@@ -113,6 +113,10 @@ typedef struct pbrt_scene_flat {
                                          mediumFromRender 4x4 row-major */
     const float *medium_values;       /* density / LeScale / 16^3 majorant grids */
     const int16_t *tri_medium;        /* [n_triangles][2] inside, outside (NULL without media) */
+    /* pixel filter (filters.h): type 0 box, 1 gaussian (a = sigma), 2 mitchell (a = B, b = C),
+     * 3 sinc (a = tau), 4 triangle; radius in pbrt_scene_info */
+    int filter_type;
+    float filter_a, filter_b;
 } pbrt_scene_flat;
 
 typedef struct pbrt_render_params {
@@ -179,6 +183,9 @@ int pbrt_intersect(pbrt_context *ctx, const float *rays_dev, int n, int any_hit,
 float pbrt_debug_halton(const pbrt_scene *scene, int px, int py, int sample_index, int dim);
 int pbrt_debug_rgb_coeffs(float r, float g, float b, float *coeffs3);
 int pbrt_debug_rgb2spec_column(int maxc, int j, int i, float *out192);
+/* Filter::Sample(u) of the scene's pixel filter (FilterSampler over PiecewiseConstant2D for
+ * gaussian / mitchell / sinc, SampleTent for triangle, filters.h): out3 = p.x p.y weight */
+int pbrt_debug_filter_sample(const pbrt_scene *scene, float u0, float u1, float *out3);
 /* ZSobolSampler (samplers.h:225-370) from StartPixelSample((px,py), sample_index, dim) with the
  * wavefront's call pattern Get1D, Get2D, Get1D, Get2D, Get1D -> 7 values (scene's sampler
  * parameters: spp, resolution, seed, randomization) */

@@ -1716,11 +1716,140 @@ static int SampleDiscrete3(Float w0, Float w1, Float w2, Float u) {
     return offset;
 }
 
+// ---------------------------------------------------------------- pixel filters
+// Filters (filters.h, filters.cpp): Box, Gaussian, Mitchell, LanczosSinc, Triangle.  The
+// tabulated ones sample through FilterSampler (filters.cpp:133-147) = PiecewiseConstant2D
+// (util/sampling.h:603-790) over |f| at 32 samples per unit radius; weight = f / pdf.
+struct Distribution1D {
+    std::vector<Float> func, cdf;
+    Float lo = 0, hi = 1, integral = 0;
+    void Init(const Float *f, int n, Float mn, Float mx) {
+        lo = mn;
+        hi = mx;
+        func.assign(f, f + n);
+        for (Float &x : func) x = std::abs(x);
+        cdf.assign(n + 1, 0);
+        for (int i = 1; i <= n; ++i) cdf[i] = cdf[i - 1] + func[i - 1] * (mx - mn) / n;
+        integral = cdf[n];
+        for (int i = 1; i <= n; ++i) cdf[i] = integral == 0 ? Float(i) / Float(n) : cdf[i] / integral;
+    }
+    Float Sample(Float u, Float *pdf, int *off) const {
+        // FindInterval over cdf: last i in [0, n - 1] with cdf[i] <= u
+        int n = (int)func.size();
+        int lo_ = 0, hi_ = n - 1;  // invariant: cdf[lo_] <= u or lo_ == 0
+        int size = n + 1 - 2, first = 1;
+        while (size > 0) {
+            int half = size >> 1, middle = first + half;
+            bool pr = cdf[middle] <= u;
+            first = pr ? middle + 1 : first;
+            size = pr ? size - (half + 1) : half;
+        }
+        (void)lo_;
+        (void)hi_;
+        int o = std::min(std::max(first - 1, 0), n - 1);
+        *off = o;
+        Float du = u - cdf[o];
+        if (cdf[o + 1] - cdf[o] > 0) du /= cdf[o + 1] - cdf[o];
+        *pdf = integral > 0 ? func[o] / integral : 0;
+        return Lerp((o + du) / n, lo, hi);
+    }
+};
+
+struct PixelFilter {
+    int type = 0;  // 0 box, 1 gaussian, 2 mitchell, 3 sinc, 4 triangle
+    Float rx = 0.5f, ry = 0.5f, a = 0, b = 0, expX = 0, expY = 0;
+    int nx = 0, ny = 0;
+    std::vector<Float> f;
+    std::vector<Distribution1D> rows;
+    Distribution1D marginal;
+
+    static Float Gauss(Float x, Float sigma) {  // util/math.h:478, mu = 0
+        return 1 / std::sqrt(2 * Pi * sigma * sigma) * FastExp(-Sqr(x - 0) / (2 * sigma * sigma));
+    }
+    static Float Mitchell(Float x, Float B, Float C) {
+        x = std::abs(x);
+        if (x <= 1) return ((12 - 9 * B - 6 * C) * x * x * x + (-18 + 12 * B + 6 * C) * x * x + (6 - 2 * B)) * (1.f / 6.f);
+        if (x <= 2)
+            return ((-B - 6 * C) * x * x * x + (6 * B + 30 * C) * x * x + (-12 * B - 48 * C) * x + (8 * B + 24 * C)) *
+                   (1.f / 6.f);
+        return 0;
+    }
+    static Float SinXOverX(Float x) { return 1 - x * x == 1 ? 1 : CRSin(x) / x; }
+    static Float Lanczos(Float x, Float r, Float tau) {
+        if (std::abs(x) > r) return 0;
+        return SinXOverX(Pi * x) * SinXOverX(Pi * (x / tau));
+    }
+    Float Evaluate(Float x, Float y) const {
+        switch (type) {
+        case 1: return std::max<Float>(0, Gauss(x, a) - expX) * std::max<Float>(0, Gauss(y, a) - expY);
+        case 2: return Mitchell(2 * x / rx, a, b) * Mitchell(2 * y / ry, a, b);
+        case 3: return Lanczos(x, rx, a) * Lanczos(y, ry, a);
+        case 4: return std::max<Float>(0, rx - std::abs(x)) * std::max<Float>(0, ry - std::abs(y));
+        default: return (std::abs(x) <= rx && std::abs(y) <= ry) ? 1 : 0;
+        }
+    }
+    void Init(int t, Float rx_, Float ry_, Float a_, Float b_) {
+        type = t;
+        rx = rx_;
+        ry = ry_;
+        a = a_;
+        b = b_;
+        if (type == 1) {
+            expX = Gauss(rx, a);
+            expY = Gauss(ry, a);
+        }
+        if (type == 0 || type == 4) return;
+        nx = int(32 * rx);
+        ny = int(32 * ry);
+        f.resize((size_t)nx * ny);
+        for (int y = 0; y < ny; ++y)
+            for (int x = 0; x < nx; ++x)
+                f[(size_t)y * nx + x] = Evaluate(Lerp((x + 0.5f) / nx, -rx, rx), Lerp((y + 0.5f) / ny, -ry, ry));
+        rows.resize(ny);
+        std::vector<Float> m(ny);
+        for (int y = 0; y < ny; ++y) {
+            rows[y].Init(&f[(size_t)y * nx], nx, -rx, rx);
+            m[y] = rows[y].integral;
+        }
+        marginal.Init(m.data(), ny, -ry, ry);
+    }
+    static Float Tent(Float u, Float r) {  // SampleTent (util/sampling.h:196-201)
+        // SampleDiscrete({0.5, 0.5}, u, nullptr, &u)
+        Float sum = 0.5f + 0.5f, up = u * sum;
+        if (up == sum) up = NextFloatDown(up);
+        int k = (0 + 0.5f <= up) ? 1 : 0;
+        Float base = k ? 0.5f : 0.f;
+        u = std::min((up - base) / 0.5f, OneMinusEpsilon);
+        if (k == 0) return -r + r * SampleLinear(u, 0, 1);
+        return r * SampleLinear(u, 1, 0);
+    }
+    void Sample(Float u0, Float u1, Float *px, Float *py, Float *w) const {
+        if (type == 0) {
+            *px = Lerp(u0, -rx, rx);
+            *py = Lerp(u1, -ry, ry);
+            *w = 1;
+            return;
+        }
+        if (type == 4) {
+            *px = Tent(u0, rx);
+            *py = Tent(u1, ry);
+            *w = 1;
+            return;
+        }
+        Float p1, p0;
+        int iy, ix;
+        *py = marginal.Sample(u1, &p1, &iy);
+        *px = rows[iy].Sample(u0, &p0, &ix);
+        *w = f[(size_t)iy * nx + ix] / (p0 * p1);
+    }
+};
+
 // ---------------------------------------------------------------- integrator
 struct Renderer {
     Scene S;
     Lights lights;
     Media M;
+    PixelFilter filt;
     const pbrt_scene_flat *f;
 
     Vec Xf(const float *m, Vec p, bool point) const {
@@ -1748,12 +1877,13 @@ struct Renderer {
         Wavelengths lambda = Wavelengths::SampleUniform(lu);
         Float fx, fy;
         hs.Pixel2D(&fx, &fy);
-        Float ox = Lerp(fx, -S.frx, S.frx), oy = Lerp(fy, -S.fry, S.fry);
+        Float ox, oy, fw;
+        filt.Sample(fx, fy, &ox, &oy, &fw);  // Filter::Sample(GetPixel2D())
         Float pFilmX = px + ox + 0.5f, pFilmY = py + oy + 0.5f;
         hs.Get1D();  // time
         Float l0, l1;
         hs.Get2D(&l0, &l1);
-        *weight = 1;
+        *weight = fw;
         Vec pCam = Xf(f->camera_from_raster, Vec(pFilmX, pFilmY, 0), true);
         Vec ro(0, 0, 0), rd = Normalize(pCam);
         if (f->lens_radius > 0) {
@@ -2129,6 +2259,16 @@ extern "C" {
 // Transcendental mode of every later call (see CRSin): 0 = libm float (reference), 1 = CR
 void oracle_set_cr_math(int on) { g_crMath = on ? 1 : 0; }
 
+// Filter::Sample(u) of a filter (type as pbrt_scene_flat::filter_type): out3 = p.x p.y weight;
+// out_eval = Filter::Evaluate(px, py)
+void oracle_filter_sample(int type, float rx, float ry, float a, float b, float u0, float u1, float px, float py,
+                          float *out4) {
+    PixelFilter f;
+    f.Init(type, rx, ry, a, b);
+    f.Sample(u0, u1, &out4[0], &out4[1], &out4[2]);
+    out4[3] = f.Evaluate(px, py);
+}
+
 // Renders rows x [first_sample, first_sample + n_samples) into film[4][yres*xres]
 // (sensor RGB sums + weight sums, RGBFilm::Pixel layout) with `threads` host threads.
 int oracle_render(const pbrt_scene_flat *flat, const pbrt_scene_info *info, const int32_t *rows, int nRows,
@@ -2140,6 +2280,7 @@ int oracle_render(const pbrt_scene_flat *flat, const pbrt_scene_info *info, cons
     r.lights.uniformFlag = uniformLightSampler != 0;
     r.M.f = flat;
     r.M.n = flat->n_media;
+    r.filt.Init(flat->filter_type, info->filter_radius_x, info->filter_radius_y, flat->filter_a, flat->filter_b);
     size_t npix = (size_t)info->xres * info->yres;
     std::atomic<int> next(0);
     auto work = [&]() {

@@ -198,7 +198,7 @@ struct pbrt_context {
     DevBuf<DeviceLightNode> lightNodes;
     DevBuf<DeviceAreaLight> lights;
     DevBuf<int> mediumInfo, primMedium;
-    DevBuf<float> mediumParams, mediumValues;
+    DevBuf<float> mediumParams, mediumValues, filterTab;
     // wavefront buffers
     int64_t maxPaths = 0;
     DevBuf<float> fState;
@@ -500,7 +500,10 @@ static void BuildDevice(pbrt_context *c) {
     S.py1 = s.py1;
     S.filterRadiusX = s.filterRadiusX;
     S.filterRadiusY = s.filterRadiusY;
-    S.boxFilter = 1;  // the loader accepts only PixelFilter "box"
+    S.boxFilter = s.filterType == kFilterBox ? 1 : 0;
+    S.filter = FilterParams{s.filterType, s.filterRadiusX, s.filterRadiusY, s.filterA, s.filterB};
+    c->filterTab.Upload(s.filterTable.empty() ? std::vector<float>{0.f} : s.filterTable);
+    S.filterTab = FilterTableView{s.filterNu, s.filterNv, c->filterTab.p};
     S.perm = c->perm.p;
     S.permOffset = c->permOffset.p;
     S.permNDigits = c->permNDigits.p;
@@ -931,6 +934,9 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
     f->medium_params = scene->mediumParams.data();
     f->medium_values = scene->mediumValues.data();
     f->tri_medium = s.triMedium.empty() ? nullptr : s.triMedium[0].data();
+    f->filter_type = s.filterType;
+    f->filter_a = s.filterA;
+    f->filter_b = s.filterB;
     return 0;
 }
 
@@ -1181,6 +1187,18 @@ int pbrt_debug_rgb2spec_column(int maxc, int j, int i, float *out) {
     try {
         auto v = RGB2SpecColumn(maxc, j, i);
         std::copy(v.begin(), v.end(), out);
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_debug_filter_sample(const pbrt_scene *scene, float u0, float u1, float *out3) {
+    try {
+        const SceneDesc &s = scene->desc;
+        const FilterParams fp{s.filterType, s.filterRadiusX, s.filterRadiusY, s.filterA, s.filterB};
+        FilterSample(fp, FilterTableView{s.filterNu, s.filterNv, s.filterTable.data()}, u0, u1, &out3[0], &out3[1],
+                     &out3[2]);
         return 0;
     } catch (const std::exception &e) {
         return Fail(e.what());

@@ -1341,4 +1341,121 @@ PHD int SampleDiscrete3(float w0, float w1, float w2, float u) {
     return 2;
 }
 
+// ---------------------------------------------------------------- pixel filters
+// filters.h: Box / Gaussian / Mitchell / LanczosSinc / Triangle.  The tabulated filters sample
+// through FilterSampler (filters.cpp:133-147): f tabulated at 32 samples per unit radius,
+// PiecewiseConstant2D over |f| (util/sampling.h:603-790), weight = f[pi] / pdf.
+enum FilterType : int { kFilterBox = 0, kFilterGaussian = 1, kFilterMitchell = 2, kFilterSinc = 3, kFilterTriangle = 4 };
+struct FilterParams {
+    int type;
+    float rx, ry;
+    float a, b;  // gaussian sigma; mitchell B, C; sinc tau
+};
+// util/math.h:478 Gaussian (with the CPU FastExp)
+PHD float GaussianF(float x, float mu, float sigma) {
+    return 1 / std::sqrt(2 * kPi * sigma * sigma) * FastExp(-Sqr(x - mu) / (2 * sigma * sigma));
+}
+PHD float Mitchell1D(float x, float b, float c) {  // filters.h:150-162
+    x = std::fabs(x);
+    if (x <= 1)
+        return ((12 - 9 * b - 6 * c) * x * x * x + (-18 + 12 * b + 6 * c) * x * x + (6 - 2 * b)) * (1.f / 6.f);
+    else if (x <= 2)
+        return ((-b - 6 * c) * x * x * x + (6 * b + 30 * c) * x * x + (-12 * b - 48 * c) * x + (8 * b + 24 * c)) *
+               (1.f / 6.f);
+    return 0;
+}
+PHD float SinXOverX(float x) {  // util/math.h:340
+    if (1 - x * x == 1) return 1;
+    return Sinf(x) / x;
+}
+PHD float WindowedSinc(float x, float radius, float tau) {  // util/math.h:221
+    if (std::fabs(x) > radius) return 0;
+    return SinXOverX(kPi * x) * SinXOverX(kPi * (x / tau));
+}
+// Filter::Evaluate (filters.h)
+PHD float FilterEvaluate(const FilterParams &f, float px, float py) {
+    switch (f.type) {
+    case kFilterGaussian:
+        return std::fmax(0.f, GaussianF(px, 0, f.a) - GaussianF(f.rx, 0, f.a)) *
+               std::fmax(0.f, GaussianF(py, 0, f.a) - GaussianF(f.ry, 0, f.a));
+    case kFilterMitchell:
+        return Mitchell1D(2 * px / f.rx, f.a, f.b) * Mitchell1D(2 * py / f.ry, f.a, f.b);
+    case kFilterSinc:
+        return WindowedSinc(px, f.rx, f.a) * WindowedSinc(py, f.ry, f.a);
+    case kFilterTriangle:
+        return std::fmax(0.f, f.rx - std::fabs(px)) * std::fmax(0.f, f.ry - std::fabs(py));
+    default:
+        return (std::fabs(px) <= f.rx && std::fabs(py) <= f.ry) ? 1.f : 0.f;
+    }
+}
+// FindInterval (util/math.h) over a CDF of sz entries: largest i <= sz - 2 with cdf[i] <= u
+template <typename P>
+PHD int FindIntervalCdf(const P *cdf, int sz, float u) {
+    int size = sz - 2, first = 1;
+    while (size > 0) {
+        const int half = size >> 1, middle = first + half;
+        const bool pr = cdf[middle] <= u;
+        first = pr ? middle + 1 : first;
+        size = pr ? size - (half + 1) : half;
+    }
+    const int i = first - 1;
+    return i < 0 ? 0 : (i > sz - 2 ? sz - 2 : i);
+}
+// FilterSampler tables of a tabulated filter, one float array (filter.cpp BuildFilterTable):
+// [nu*nv] f, [nu*nv] |f|, [nv*(nu+1)] conditional CDFs, [nv] conditional integrals,
+// [nv+1] marginal CDF, [1] marginal integral
+struct FilterTableView {
+    int nu, nv;
+    const float *t;
+    PHD const float *F() const { return t; }
+    PHD const float *Func() const { return t + nu * nv; }
+    PHD const float *CondCdf() const { return t + 2 * nu * nv; }
+    PHD const float *CondInt() const { return t + 2 * nu * nv + nv * (nu + 1); }
+    PHD const float *MargCdf() const { return CondInt() + nv; }
+    PHD float MargInt() const { return MargCdf()[nv + 1]; }
+    static PHD int Size(int nu, int nv) { return 2 * nu * nv + nv * (nu + 1) + nv + (nv + 1) + 1; }
+};
+// PiecewiseConstant1D::Sample (util/sampling.h:657-675)
+PHD float SamplePC1D(const float *func, const float *cdf, int n, float funcInt, float mn, float mx, float u,
+                     float *pdf, int *offset) {
+    const int o = FindIntervalCdf(cdf, n + 1, u);
+    *offset = o;
+    float du = u - cdf[o];
+    if (cdf[o + 1] - cdf[o] > 0) du /= cdf[o + 1] - cdf[o];
+    *pdf = (funcInt > 0) ? func[o] / funcInt : 0;
+    return Lerpf((o + du) / n, mn, mx);
+}
+// SampleTent (util/sampling.h:196-201)
+PHD float SampleTent(float u, float r) {
+    float pmf;
+    if (SampleDiscrete2(0.5f, 0.5f, u, &pmf, &u) == 0) return -r + r * SampleLinear(u, 0, 1);
+    return r * SampleLinear(u, 1, 0);
+}
+// Filter::Sample(u) -> film offset p and weight (filters.h)
+PHD void FilterSample(const FilterParams &f, const FilterTableView &tab, float u0, float u1, float *px, float *py,
+                      float *weight) {
+    if (f.type == kFilterBox) {
+        *px = Lerpf(u0, -f.rx, f.rx);
+        *py = Lerpf(u1, -f.ry, f.ry);
+        *weight = 1.f;
+        return;
+    }
+    if (f.type == kFilterTriangle) {
+        *px = SampleTent(u0, f.rx);
+        *py = SampleTent(u1, f.ry);
+        *weight = 1.f;
+        return;
+    }
+    // PiecewiseConstant2D::Sample (util/sampling.h:761-772): marginal in y, conditional in x
+    float pdf1, pdf0;
+    int v, u;
+    const float *margFunc = tab.CondInt();  // |integral| of each row (all >= 0)
+    const float d1 = SamplePC1D(margFunc, tab.MargCdf(), tab.nv, tab.MargInt(), -f.ry, f.ry, u1, &pdf1, &v);
+    const float d0 = SamplePC1D(tab.Func() + v * tab.nu, tab.CondCdf() + v * (tab.nu + 1), tab.nu, tab.CondInt()[v],
+                                -f.rx, f.rx, u0, &pdf0, &u);
+    *px = d0;
+    *py = d1;
+    *weight = tab.F()[v * tab.nu + u] / (pdf0 * pdf1);
+}
+
 }  // namespace pbrt_amd

@@ -473,4 +473,41 @@ void FinalizeScene(SceneDesc &s) {
     BuildZSobol(s);
 }
 
+// PiecewiseConstant1D ctor (util/sampling.h:625-649) into func (|f|) and cdf; returns funcInt
+static float BuildPC1D(const float *f, int n, float mn, float mx, float *func, float *cdf) {
+    for (int i = 0; i < n; ++i) func[i] = std::fabs(f[i]);
+    cdf[0] = 0;
+    for (int i = 1; i < n + 1; ++i) cdf[i] = cdf[i - 1] + func[i - 1] * (mx - mn) / (float)n;
+    const float funcInt = cdf[n];
+    if (funcInt == 0)
+        for (int i = 1; i < n + 1; ++i) cdf[i] = float(i) / float(n);
+    else
+        for (int i = 1; i < n + 1; ++i) cdf[i] /= funcInt;
+    return funcInt;
+}
+
+void BuildFilterTable(SceneDesc &s) {
+    s.filterTable.clear();
+    s.filterNu = s.filterNv = 0;
+    if (s.filterType == kFilterBox || s.filterType == kFilterTriangle) return;
+    const FilterParams fp{s.filterType, s.filterRadiusX, s.filterRadiusY, s.filterA, s.filterB};
+    const int nu = int(32 * fp.rx), nv = int(32 * fp.ry);
+    if (nu < 1 || nv < 1) throw Error("pixel filter radius too small to tabulate");
+    s.filterNu = nu;
+    s.filterNv = nv;
+    s.filterTable.assign(FilterTableView::Size(nu, nv), 0.f);
+    float *F = s.filterTable.data(), *func = F + nu * nv, *condCdf = func + nu * nv, *condInt = condCdf + nv * (nu + 1);
+    float *margCdf = condInt + nv;
+    for (int y = 0; y < nv; ++y)
+        for (int x = 0; x < nu; ++x) {
+            // domain.Lerp((x + 0.5) / nu, (y + 0.5) / nv) over [-r, r]^2
+            const float px = Lerpf((x + 0.5f) / nu, -fp.rx, fp.rx), py = Lerpf((y + 0.5f) / nv, -fp.ry, fp.ry);
+            F[y * nu + x] = FilterEvaluate(fp, px, py);
+        }
+    for (int v = 0; v < nv; ++v)
+        condInt[v] = BuildPC1D(F + v * nu, nu, -fp.rx, fp.rx, func + v * nu, condCdf + v * (nu + 1));
+    std::vector<float> margFunc(nv);
+    margCdf[nv + 1] = BuildPC1D(condInt, nv, -fp.ry, fp.ry, margFunc.data(), margCdf);
+}
+
 }  // namespace pbrt_amd

@@ -917,10 +917,28 @@ void Parser::Finish() {
     if (ls != "bvh" && ls != "uniform") throw Error(integratorParams.loc + ": lightsampler " + ls + " not supported");
     if (ls == "uniform") scene.uniformLightSampler = true;
     // ---- filter
-    if (scene.filterName != "box") throw Error(filterParams.loc + ": pixel filter \"" + scene.filterName + "\" not supported yet (box only)");
-    scene.filterRadiusX = (float)filterParams.GetFloat("xradius", 0.5);
-    scene.filterRadiusY = (float)filterParams.GetFloat("yradius", 0.5);
-    filterParams.CheckUnused();
+    // Filter::Create (filters.cpp:26-130): box 0.5, gaussian 1.5 / sigma 0.5, mitchell 2 / B = C
+    // = 1/3, sinc 4 / tau 3, triangle 2
+    {
+        const std::string &fn = scene.filterName;
+        float r = 0.5f;
+        if (fn == "box") scene.filterType = kFilterBox, r = 0.5f;
+        else if (fn == "gaussian") scene.filterType = kFilterGaussian, r = 1.5f;
+        else if (fn == "mitchell") scene.filterType = kFilterMitchell, r = 2.f;
+        else if (fn == "sinc") scene.filterType = kFilterSinc, r = 4.f;
+        else if (fn == "triangle") scene.filterType = kFilterTriangle, r = 2.f;
+        else throw Error(filterParams.loc + ": " + fn + ": filter type unknown.");
+        scene.filterRadiusX = (float)filterParams.GetFloat("xradius", r);
+        scene.filterRadiusY = (float)filterParams.GetFloat("yradius", r);
+        if (fn == "gaussian") scene.filterA = (float)filterParams.GetFloat("sigma", 0.5);
+        if (fn == "mitchell") {
+            scene.filterA = (float)filterParams.GetFloat("B", 1. / 3.);
+            scene.filterB = (float)filterParams.GetFloat("C", 1. / 3.);
+        }
+        if (fn == "sinc") scene.filterA = (float)filterParams.GetFloat("tau", 3.);
+        filterParams.CheckUnused();
+        BuildFilterTable(scene);
+    }
 
     // ---- camera (cameras.cpp:43-73, 266-285, 543-600) in cameraworld rendering space
     if (cameraType != "perspective") throw Error(cameraParams.loc + ": camera \"" + cameraType + "\" not supported");

@@ -112,6 +112,11 @@ struct SceneDesc {
     std::string outFile = "pbrt.exr";
     float filterRadiusX = 0.5f, filterRadiusY = 0.5f;  // box (scene.cpp:94 fork default)
     std::string filterName = "box";
+    int filterType = 0;             // core.h FilterType
+    float filterA = 0, filterB = 0; // gaussian sigma; mitchell B, C; sinc tau
+    // FilterSampler tables (gaussian / mitchell / sinc; core.h FilterTableView layout)
+    int filterNu = 0, filterNv = 0;
+    std::vector<float> filterTable;
     float imagingRatio = 1;
     double outputRGBFromSensorRGB[3][3];
     CameraDesc camera;
@@ -164,6 +169,9 @@ SceneDesc LoadPbrtString(const std::string &text, const std::string &baseDir,
                          const std::map<std::string, std::string> &overrides);
 void FinalizeScene(SceneDesc &s);  // lights, light BVH, sampler tables
 // the 24 four-way digit permutations of ZSobolSampler::GetSampleIndex, in pbrt's order
+// FilterSampler ctor (filters.cpp:133-147): tabulates the scene's filter and its
+// PiecewiseConstant2D (util/sampling.h:603-790) into SceneDesc::filterTable
+void BuildFilterTable(SceneDesc &s);
 extern const uint8_t kZSobolPermutations[24][4];
 
 // Spectral support (host)

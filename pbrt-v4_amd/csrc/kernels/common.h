@@ -857,7 +857,7 @@ typedef const uint16_t LdsU16;
 // wavelength, and the render-space camera ray (PerspectiveCamera::GenerateRay,
 // cameras.cpp:433-456, then CameraBase::RenderFromCamera).
 __device__ inline void GenerateCameraRay(const DeviceScene &S, const PathState &st, int slot, float *lambda0Out,
-                                         V3 *oOut, V3 *dOut) {
+                                         V3 *oOut, V3 *dOut, float *filterWeight) {
     int px, py, sampleIndex;
     PixelOf(st, slot, &px, &py, &sampleIndex);
     px += S.px0;
@@ -883,7 +883,9 @@ __device__ inline void GenerateCameraRay(const DeviceScene &S, const PathState &
         Get2D(S, h, &l0, &l1);
     }
     float lambda0 = Lerpf(lu, kLambdaMin, kLambdaMax);
-    float fx = Lerpf(pix0, -S.filterRadiusX, S.filterRadiusX), fy = Lerpf(pix1, -S.filterRadiusY, S.filterRadiusY);
+    // Filter::Sample(GetPixel2D()) (samplers.h:797-813): offset and weight
+    float fx, fy;
+    FilterSample(S.filter, S.filterTab, pix0, pix1, &fx, &fy, filterWeight);
     float pFilmX = px + fx + 0.5f, pFilmY = py + fy + 0.5f;
     // PerspectiveCamera::GenerateRay (cameras.cpp:433-456)
     V3 pCamera = XfPoint(S.cameraFromRaster, V3(pFilmX, pFilmY, 0));

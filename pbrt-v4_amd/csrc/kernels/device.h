@@ -142,6 +142,8 @@ struct DeviceScene {
     int xres, yres, px0, px1, py0, py1;
     float filterRadiusX, filterRadiusY;
     int boxFilter;  // box filter: every sample weight is 1 (filters.h:67-71)
+    FilterParams filter;       // the pixel filter (core.h)
+    FilterTableView filterTab; // FilterSampler tables on the device (tabulated filters)
     // halton
     const uint16_t *perm;
     const uint32_t *permOffset, *permNDigits, *permBase;

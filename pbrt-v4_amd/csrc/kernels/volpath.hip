@@ -491,12 +491,13 @@ __global__ void __launch_bounds__(kBlock) k_vcamera(DeviceScene S, PathState st,
     if (slot >= nActive) return;
     float lambda0;
     V3 o, d;
-    GenerateCameraRay(S, st, slot, &lambda0, &o, &d);
+    float filterWeight;
+    GenerateCameraRay(S, st, slot, &lambda0, &o, &d, &filterWeight);
     const int NR = st.NR, N = st.N;
     st.L[slot] = 0;
     st.L[N + slot] = 0;
     st.L[2 * N + slot] = 0;
-    if (!S.boxFilter) st.filterW[slot] = 1.f;
+    if (!S.boxFilter) st.filterW[slot] = filterWeight;
     const VolRecords &r = v.rec[0];
     r.beta[slot] = 1.f;  // uniform spectra: entry 0 only (kUni* flags)
     r.ru[slot] = 1.f;

@@ -27,7 +27,8 @@ __global__ void __launch_bounds__(kBlock) k_camera(DeviceScene S, PathState st, 
     if (slot >= nActive) return;
     float lambda0;
     V3 o, d;
-    GenerateCameraRay(S, st, slot, &lambda0, &o, &d);
+    float filterWeight;
+    GenerateCameraRay(S, st, slot, &lambda0, &o, &d, &filterWeight);
     // Depth-0 record = the pixel-sample slot.  beta = 1, r_u = r_l = 1, etaScale = 1, flags = 0,
     // pixel = slot are implicit at depth 0 (the depth-0 kernels use the constants) and the box
     // filter's weight is always 1: none of them is stored.
@@ -35,7 +36,7 @@ __global__ void __launch_bounds__(kBlock) k_camera(DeviceScene S, PathState st, 
     st.L[slot] = 0;
     st.L[N + slot] = 0;
     st.L[2 * N + slot] = 0;
-    if (!S.boxFilter) st.filterW[slot] = 1.f;
+    if (!S.boxFilter) st.filterW[slot] = filterWeight;
     const PathRecords &r = st.rec[0];
     const int NR = st.NR;
     r.lambda0[slot] = lambda0;

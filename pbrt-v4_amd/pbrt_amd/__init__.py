@@ -73,6 +73,7 @@ class SceneFlat(ctypes.Structure):
         ("n_media", ctypes.c_int), ("camera_medium", ctypes.c_int),
         ("medium_info", ctypes.POINTER(ctypes.c_int32)), ("medium_params", ctypes.POINTER(ctypes.c_float)),
         ("medium_values", ctypes.POINTER(ctypes.c_float)), ("tri_medium", ctypes.POINTER(ctypes.c_int16)),
+        ("filter_type", ctypes.c_int), ("filter_a", ctypes.c_float), ("filter_b", ctypes.c_float),
     ]
 
 
@@ -97,7 +98,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_debug_halton", "pbrt_debug_rgb_coeffs", "pbrt_debug_rgb2spec_column", "pbrt_debug_kernel_sections",
     "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
     "pbrt_debug_named_spectrum", "pbrt_debug_bxdf", "pbrt_debug_triangle_shading", "pbrt_film_write_image",
-    "pbrt_image_read_size", "pbrt_image_read", "pbrt_image_write", "pbrt_image_error",
+    "pbrt_image_read_size", "pbrt_image_read", "pbrt_image_write", "pbrt_image_error", "pbrt_debug_filter_sample",
 ]
 
 _LIB = None
@@ -117,6 +118,7 @@ def _lib():
     lib.pbrt_scene_load.argtypes = [c.c_char_p, c.c_char_p, c.POINTER(c.c_void_p)]
     lib.pbrt_scene_load_string.argtypes = [c.c_char_p, c.c_char_p, c.c_char_p, c.POINTER(c.c_void_p)]
     lib.pbrt_scene_free.argtypes = [c.c_void_p]
+    lib.pbrt_debug_filter_sample.argtypes = [c.c_void_p, c.c_float, c.c_float, c.c_void_p]
     lib.pbrt_film_write_image.argtypes = [c.c_void_p, c.c_char_p, c.c_int]
     lib.pbrt_image_read_size.argtypes = [c.c_char_p, c.POINTER(c.c_int), c.POINTER(c.c_int)]
     lib.pbrt_image_read.argtypes = [c.c_char_p, c.c_void_p, c.c_int, c.c_int]
@@ -247,6 +249,12 @@ class Scene:
     def zsobol(self, px, py, sample_index, dim):
         out = (ctypes.c_float * 7)()
         _check(_lib().pbrt_debug_zsobol(self._h, px, py, sample_index, dim, out))
+        return np.array(out[:], dtype=np.float32)
+
+    def filter_sample(self, u0, u1):
+        """Filter::Sample((u0, u1)) of the scene's pixel filter -> (p.x, p.y, weight)"""
+        out = (ctypes.c_float * 3)()
+        _check(_lib().pbrt_debug_filter_sample(self._h, ctypes.c_float(u0), ctypes.c_float(u1), out))
         return np.array(out[:], dtype=np.float32)
 
     def halton(self, px, py, sample_index, dim):

@@ -221,3 +221,16 @@ def test_intersect_closest_and_shadow_match_oracle(pa, oracle):
             assert (same | tie).all()
             np.testing.assert_array_equal(gh[3][hit], oh[3][hit])
             np.testing.assert_array_equal(gh[:3, hit][:, same], oh[:3, hit][:, same])
+
+
+@pytest.mark.parametrize("line", ['PixelFilter "gaussian"', 'PixelFilter "mitchell" "float xradius" [ 1.5 ]',
+                                  'PixelFilter "triangle"', 'PixelFilter "sinc" "float xradius" [ 2 ] "float yradius" [ 2 ]'])
+def test_pixel_filters_match_oracle(pa, oracle, line):
+    """Filter::Sample offsets and weights (FilterSampler tables on the device) end to end."""
+    from test_filters import scene_with_filter
+    sc = scene_with_filter(pa, line)
+    film, _ = gpu_film(pa, sc)
+    ref = oracle.render(sc, threads=16)
+    np.testing.assert_array_equal(film[3], ref[3])  # the filter weight sums are the same floats summed
+    frac, mean_rel = check_parity(to_rgb(oracle, sc, film), to_rgb(oracle, sc, ref))
+    print(f"{line}: {frac*100:.3f}% pixels within 1e-3, mean rel {mean_rel:.2e}")

@@ -282,8 +282,13 @@ static void BuildDevice(pbrt_context *c) {
     std::vector<float> mc;
     std::vector<int> mk;
     for (auto &m : s.materials) {
-        mc.insert(mc.end(), {m.c0, m.c1, m.c2, m.constantValue});
-        mk.push_back(m.constant);
+        // An RGB albedo whose sigmoid has c0 = c1 = 0 (a grey rgb) is the same value at every
+        // wavelength: upload it as a constant, so the kernels skip 31 sigmoid evaluations
+        // (identical bits: SigmoidPolynomial(0, 0, c2, lambda) does not depend on lambda).
+        const bool grey = !m.constant && m.c0 == 0 && m.c1 == 0;
+        const float cv = grey ? SigmoidPolynomial(0.f, 0.f, m.c2, 500.f) : m.constantValue;
+        mc.insert(mc.end(), {m.c0, m.c1, m.c2, cv});
+        mk.push_back(m.constant || grey ? 1 : 0);
     }
     c->matCoeffs.Upload(mc);
     c->matConstant.Upload(mk);

@@ -50,6 +50,11 @@ __device__ inline int WavePush(int *counter, bool pred) {
 // the block must call it (the callers' grid-stride loops are block-uniform).
 template <int K>
 __device__ inline void BlockPush(int *const (&counters)[K], const bool (&pred)[K], int (&pos)[K]) {
+#ifdef PBRT_SHADE_PUSH_WAVE
+#pragma unroll
+    for (int k = 0; k < K; ++k) pos[k] = WavePush(counters[k], pred[k]);
+    return;
+#endif
     constexpr int kWaves = kBlock / 64;
     __shared__ int sCount[K][kWaves];
     __shared__ int sBase[K];

@@ -6,7 +6,9 @@
 #include <algorithm>
 #include <cctype>
 #include <cmath>
+#include <cstdio>
 #include <fstream>
+#include <map>
 #include <functional>
 #include <memory>
 #include <set>
@@ -330,6 +332,15 @@ class Parser {
         std::string loc;
     };
     std::vector<PendingShape> shapes;
+    // object instancing (scene.cpp:309-395): shapes of each ObjectBegin/End definition, and the
+    // ObjectInstance uses, resolved after parsing (a use may precede its definition)
+    std::map<std::string, std::vector<PendingShape>> instanceDefs;
+    std::string activeInstance;
+    struct InstanceUse {
+        std::string name, loc;
+        Mat4 worldFromInstance;
+    };
+    std::vector<InstanceUse> instanceUses;
     struct PendingLight {
         std::string type;
         ParamSet params;
@@ -547,8 +558,24 @@ class Parser {
             if (pos < toks.size() && toks[pos].isString) b = Str(toks, pos);
             gs.insideMedium = a;
             gs.outsideMedium = b;
-        } else if (d == "Texture" || d == "ObjectBegin" ||
-                   d == "ObjectEnd" || d == "ObjectInstance" || d == "ActiveTransform" || d == "TransformTimes") {
+        } else if (d == "ObjectBegin") {
+            std::string name = Str(toks, pos);
+            if (!activeInstance.empty()) throw Error(loc + ": ObjectBegin called inside of instance definition");
+            if (instanceDefs.count(name)) throw Error(loc + ": " + name + ": trying to redefine an object instance");
+            stack.push_back(gs);  // as AttributeBegin
+            instanceDefs[name];
+            activeInstance = name;
+        } else if (d == "ObjectEnd") {
+            if (activeInstance.empty()) throw Error(loc + ": ObjectEnd called outside of instance definition");
+            if (stack.empty()) throw Error(loc + ": unmatched ObjectEnd");
+            gs = stack.back();
+            stack.pop_back();
+            activeInstance.clear();
+        } else if (d == "ObjectInstance") {
+            std::string name = Str(toks, pos);
+            if (!activeInstance.empty()) throw Error(loc + ": ObjectInstance can't be called inside instance definition");
+            instanceUses.push_back(InstanceUse{name, loc, gs.ctm});
+        } else if (d == "Texture" || d == "ActiveTransform" || d == "TransformTimes") {
             throw Error(loc + ": directive " + d + " is not supported by the wavefront hot path yet");
         } else {
             throw Error(loc + ": unknown directive '" + d + "'");
@@ -736,7 +763,34 @@ class Parser {
         s.insideMedium = gs.insideMedium;
         s.outsideMedium = gs.outsideMedium;
         s.loc = ps.loc;
+        if (!activeInstance.empty()) {
+            // BasicSceneBuilder::Shape: "Area lights not supported with object instancing"
+            // (a warning; the shape is kept without emission)
+            if (!s.areaLight.empty()) {
+                std::fprintf(stderr, "%s: Warning: Area lights not supported with object instancing\n", ps.loc.c_str());
+                s.areaLight.clear();
+            }
+            instanceDefs[activeInstance].push_back(std::move(s));
+            return;
+        }
         shapes.push_back(std::move(s));
+    }
+
+    // ObjectInstance: renderFromInstance = RenderFromObject() * worldFromRender (scene.cpp:392),
+    // applied to each definition shape's renderFromObject, i.e. the shape's world-from-object
+    // becomes worldFromInstance * worldFromObject.  The instances are flattened into the
+    // triangle list (one BVH over every instance's triangles).
+    void ResolveInstances() {
+        if (!activeInstance.empty()) throw Error("End of files inside ObjectBegin \"" + activeInstance + "\"");
+        for (const InstanceUse &u : instanceUses) {
+            auto it = instanceDefs.find(u.name);
+            if (it == instanceDefs.end()) throw Error(u.loc + ": " + u.name + ": object instance not defined");
+            for (const PendingShape &d : it->second) {
+                PendingShape c = d;
+                c.renderFromObject = Mul(u.worldFromInstance, d.renderFromObject);
+                shapes.push_back(std::move(c));
+            }
+        }
     }
 };
 
@@ -1065,7 +1119,9 @@ void Parser::Finish() {
     };
     scene.cameraMedium = mediumOf(cameraMediumName, "Camera");
 
-    // ---- shapes -> render-space triangles; area lights in shape order
+    // ---- object instances (flattened), then shapes -> render-space triangles; area lights in
+    // shape order
+    ResolveInstances();
     const Mat4 &renderFromWorld = scene.camera.renderFromWorld;
     std::map<std::string, int> spectrumCache;
     for (PendingShape &s : shapes) {

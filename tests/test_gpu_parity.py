@@ -234,3 +234,19 @@ def test_pixel_filters_match_oracle(pa, oracle, line):
     np.testing.assert_array_equal(film[3], ref[3])  # the filter weight sums are the same floats summed
     frac, mean_rel = check_parity(to_rgb(oracle, sc, film), to_rgb(oracle, sc, ref))
     print(f"{line}: {frac*100:.3f}% pixels within 1e-3, mean rel {mean_rel:.2e}")
+
+
+def test_instanced_scene_matches_oracle(pa, oracle):
+    """ObjectBegin / ObjectInstance scenes render through the flattened triangle list."""
+    from test_instancing import HEAD, TRI
+    text = HEAD + f"""
+ObjectBegin "thing"
+  Material "diffuse" "rgb reflectance" [ 0.7 0.5 0.3 ]
+  {TRI}
+ObjectEnd
+AttributeBegin Translate -0.5 -0.5 0  ObjectInstance "thing" AttributeEnd
+AttributeBegin Translate 0.2 0 -0.3  Rotate 60 0 1 0  ObjectInstance "thing" AttributeEnd
+"""
+    sc = pa.Scene.from_string(text, SCENES, xresolution=96, yresolution=96, spp=8)
+    film, _ = gpu_film(pa, sc)
+    check_parity(to_rgb(oracle, sc, film), to_rgb(oracle, sc, oracle.render(sc, threads=16)))

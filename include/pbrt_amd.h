@@ -86,7 +86,7 @@ typedef struct pbrt_scene_flat {
     /* sampler: 0 halton, 1 zsobol (randomization 0 none, 1 permutedigits, 2 fastowen, 3 owen) */
     int sampler_type, zs_randomize, zs_log2_spp, zs_nbase4_digits;
     /* materials: type 0 diffuse, 1 dielectric, 2 conductor (materials.h DiffuseMaterial,
-     * DielectricMaterial, ConductorMaterial) */
+     * DielectricMaterial, ConductorMaterial), 3 interface, 4 coateddiffuse, 5 coatedconductor */
     const int32_t *material_type;     /* [n_materials] */
     const float *material_params;     /* [n_materials][4]: alpha_x alpha_y eta 0 (TrowbridgeReitz
                                          alphas after remap + clamp; dielectric eta) */
@@ -117,6 +117,12 @@ typedef struct pbrt_scene_flat {
      * 3 sinc (a = tau), 4 triangle; radius in pbrt_scene_info */
     int filter_type;
     float filter_a, filter_b;
+    /* layered materials, type 4 coateddiffuse / 5 coatedconductor (LayeredBxDF, bxdfs.h:565):
+     * material_params = interface alphas + eta, material_coeffs = diffuse or conductor
+     * "reflectance", material_spectra = conductor.eta / .k; per material [12] floats:
+     * thickness g maxdepth nsamples, albedo c0 c1 c2 value constant(1/0), conductor
+     * alpha_x alpha_y, 0 */
+    const float *material_layer;
 } pbrt_scene_flat;
 
 typedef struct pbrt_render_params {
@@ -211,6 +217,14 @@ int pbrt_debug_named_spectrum(const char *name, const float *lambda, int n, floa
  * PDF(wo,wi) (Sample_f / f / PDF of bxdfs.h:300-517, bxdfs.cpp:77-245) */
 int pbrt_debug_bxdf(int type, const float *params3, const float *eta31, const float *k31, const float *wo3,
                     const float *wi3, const float *u3, float *out70);
+/* LayeredBxDF (CoatedDiffuseBxDF / CoatedConductorBxDF, bxdfs.h:565-1052) in the shading
+ * frame: params12 = top alpha_x alpha_y eta, bottom type (0 diffuse, 2 conductor) alpha_x
+ * alpha_y, thickness g maxdepth nsamples radiance(1/0) 0; a31 = diffuse R or conductor eta,
+ * b31 = conductor k, alb31 = layer albedo; u3 = uc u0 u1.  out72 = sample_ok wi3 pdf flags
+ * f_sample[31] f(wo,wi)[31] PDF(wo,wi) Flags() 0 0 (stochastic estimates: RNGs seeded from
+ * the directions as the reference's) */
+int pbrt_debug_layered(const float *params12, const float *a31, const float *b31, const float *alb31,
+                       const float *wo3, const float *wi3, const float *u3, float *out72);
 /* queue counters of the last pass: [depth][8] = rays, material hits, shadow rays, escaped,
  * emissive hits (diagnostics) */
 int pbrt_debug_queue_counts(pbrt_context *ctx, int32_t *counts, int n);

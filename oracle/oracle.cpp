@@ -1118,8 +1118,9 @@ struct Lights {
 // ---------------------------------------------------------------- BxDFs
 // DiffuseBxDF (bxdfs.h:30-82), DielectricBxDF (bxdfs.h:300-341, bxdfs.cpp:77-245),
 // ConductorBxDF (bxdfs.h:413-517) with TrowbridgeReitzDistribution and the Fresnel terms of
-// util/scattering.h:18-205 and pstd::complex (util/pstd.h:1066-1229).  TransportMode::Radiance,
-// BxDFReflTransFlags::All throughout (the wavefront never restricts the sampled lobes).
+// util/scattering.h:18-205 and pstd::complex (util/pstd.h:1066-1229).  The path integrator calls
+// them with TransportMode::Radiance and BxDFReflTransFlags::All; the layered BxDFs below also
+// use Importance mode (no 1/eta^2 on transmission) and single-lobe flags (sf: 1 R, 2 T).
 enum { BxR = 1, BxT = 2, BxDiffuse = 4, BxGlossy = 8, BxSpecular = 16 };
 
 struct BSDFSample {
@@ -1265,7 +1266,8 @@ struct BxDF {
         for (int i = 0; i < NS; ++i) r[i] = FrComplex(cosI, Complex(etaS[i], kS[i]));
         return r;
     }
-    bool Sample_f(Vec wo, Float uc, Float u0, Float u1, BSDFSample *bs) const {
+    bool Sample_f(Vec wo, Float uc, Float u0, Float u1, BSDFSample *bs, bool radiance = true, int sf = 3) const {
+        if (type != 1 && !(sf & 1)) return false;
         if (type == 0) {
             Vec wi = SampleCosineHemisphere(u0, u1);
             if (wo.z < 0) wi.z *= -1;
@@ -1291,27 +1293,29 @@ struct BxDF {
         }
         if (eta == 1 || mf.Smooth()) {
             Float R_ = FrDielectric(wo.z, eta), T_ = 1 - R_;
-            if (R_ == 0 && T_ == 0) return false;
-            if (uc < R_ / (R_ + T_)) {
+            Float pr = (sf & 1) ? R_ : 0, pt = (sf & 2) ? T_ : 0;
+            if (pr == 0 && pt == 0) return false;
+            if (uc < pr / (pr + pt)) {
                 Vec wi(-wo.x, -wo.y, wo.z);
-                *bs = BSDFSample{Spectrum(R_ / std::abs(wi.z)), wi, R_ / (R_ + T_), BxR | BxSpecular, 1};
+                *bs = BSDFSample{Spectrum(R_ / std::abs(wi.z)), wi, pr / (pr + pt), BxR | BxSpecular, 1};
                 return true;
             }
             Vec wi;
             Float etap;
             if (!Refract(wo, Vec(0, 0, 1), eta, &etap, &wi)) return false;
             Spectrum ft(T_ / std::abs(wi.z));
-            ft = ft / Sqr(etap);
-            *bs = BSDFSample{ft, wi, T_ / (R_ + T_), BxT | BxSpecular, etap};
+            if (radiance) ft = ft / Sqr(etap);
+            *bs = BSDFSample{ft, wi, pt / (pr + pt), BxT | BxSpecular, etap};
             return true;
         }
         Vec wm = mf.Sample_wm(wo, u0, u1);
         Float R_ = FrDielectric(Dot(wo, wm), eta), T_ = 1 - R_;
-        if (R_ == 0 && T_ == 0) return false;
-        if (uc < R_ / (R_ + T_)) {
+        Float pr = (sf & 1) ? R_ : 0, pt = (sf & 2) ? T_ : 0;
+        if (pr == 0 && pt == 0) return false;
+        if (uc < pr / (pr + pt)) {
             Vec wi = Reflect(wo, wm);
             if (!SameHemisphere(wo, wi)) return false;
-            Float pdf = mf.PDF(wo, wm) / (4 * AbsDot(wo, wm)) * R_ / (R_ + T_);
+            Float pdf = mf.PDF(wo, wm) / (4 * AbsDot(wo, wm)) * pr / (pr + pt);
             Spectrum f(mf.D(wm) * mf.G(wo, wi) * R_ / (4 * wi.z * wo.z));
             *bs = BSDFSample{f, wi, pdf, BxR | BxGlossy, 1};
             return true;
@@ -1322,9 +1326,9 @@ struct BxDF {
         if (SameHemisphere(wo, wi) || wi.z == 0 || tir) return false;
         Float denom = Sqr(Dot(wi, wm) + Dot(wo, wm) / etap);
         Float dwm_dwi = AbsDot(wi, wm) / denom;
-        Float pdf = mf.PDF(wo, wm) * dwm_dwi * T_ / (R_ + T_);
+        Float pdf = mf.PDF(wo, wm) * dwm_dwi * pt / (pr + pt);
         Spectrum ft(T_ * mf.D(wm) * mf.G(wo, wi) * std::abs(Dot(wi, wm) * Dot(wo, wm) / (wi.z * wo.z * denom)));
-        ft = ft / Sqr(etap);
+        if (radiance) ft = ft / Sqr(etap);
         *bs = BSDFSample{ft, wi, pdf, BxT | BxGlossy, etap};
         return true;
     }
@@ -1342,7 +1346,7 @@ struct BxDF {
         *wm = h;
         return true;
     }
-    Spectrum f(Vec wo, Vec wi) const {
+    Spectrum f(Vec wo, Vec wi, bool radiance = true) const {
         if (type == 0) return SameHemisphere(wo, wi) ? R * InvPi : Spectrum(0.f);
         if (type == 2) {
             if (!SameHemisphere(wo, wi) || mf.Smooth()) return Spectrum(0.f);
@@ -1363,10 +1367,11 @@ struct BxDF {
         if (reflect) return Spectrum(mf.D(wm) * mf.G(wo, wi) * F / std::abs(4 * wi.z * wo.z));
         Float denom = Sqr(Dot(wi, wm) + Dot(wo, wm) / etap) * wi.z * wo.z;
         Float ft = mf.D(wm) * (1 - F) * mf.G(wo, wi) * std::abs(Dot(wi, wm) * Dot(wo, wm) / denom);
-        ft /= Sqr(etap);
+        if (radiance) ft /= Sqr(etap);
         return Spectrum(ft);
     }
-    Float PDF(Vec wo, Vec wi) const {
+    Float PDF(Vec wo, Vec wi, int sf = 3) const {
+        if (type != 1 && !(sf & 1)) return 0;
         if (type == 0) return SameHemisphere(wo, wi) ? std::abs(wi.z) * InvPi : 0;
         if (type == 2) {
             if (!SameHemisphere(wo, wi) || mf.Smooth()) return 0;
@@ -1382,10 +1387,11 @@ struct BxDF {
         bool reflect;
         if (!DielectricHalf(wo, wi, &wm, &etap, &reflect)) return 0;
         Float R_ = FrDielectric(Dot(wo, wm), eta), T_ = 1 - R_;
-        if (R_ == 0 && T_ == 0) return 0;
-        if (reflect) return mf.PDF(wo, wm) / (4 * AbsDot(wo, wm)) * R_ / (R_ + T_);
+        Float pr = (sf & 1) ? R_ : 0, pt = (sf & 2) ? T_ : 0;
+        if (pr == 0 && pt == 0) return 0;
+        if (reflect) return mf.PDF(wo, wm) / (4 * AbsDot(wo, wm)) * pr / (pr + pt);
         Float denom = Sqr(Dot(wi, wm) + Dot(wo, wm) / etap);
-        return mf.PDF(wo, wm) * (AbsDot(wi, wm) / denom) * T_ / (R_ + T_);
+        return mf.PDF(wo, wm) * (AbsDot(wi, wm) / denom) * pt / (pr + pt);
     }
 };
 
@@ -1436,6 +1442,8 @@ static uint64_t HashFloats(T... v) {
 
 static Float FastExp(Float x) {
     Float xp = x * 1.442695041f;
+    if (!(xp > -256.f)) return 0;  // far below the float range (and NaN): the exponent test's 0
+    if (xp > 256.f) return Infinity;
     Float fxp = std::floor(xp), f = xp - fxp;
     int i = (int)fxp;
     // EvaluatePolynomial(f, 1, 0.695556856, 0.226173572, 0.0781455737) with FMA
@@ -1468,6 +1476,279 @@ static Vec SampleHG(Vec wo, Float g, Float u0, Float u1, Float *pdf) {
     *pdf = HenyeyGreenstein(cosTheta, g);
     return x * l.x + y * l.y + z * l.z;
 }
+
+// ---------------------------------------------------------------- layered BxDFs
+// LayeredBxDF<DielectricBxDF, DiffuseBxDF | ConductorBxDF, twoSided = true> (bxdfs.h:565-1052),
+// i.e. CoatedDiffuseBxDF and CoatedConductorBxDF.  Written over the BxDF above with pbrt's
+// SampledSpectrum arithmetic.  The RNG streams follow the reference: RNG(Hash(seed, wo), Hash(wi))
+// for f, RNG(Hash(seed, wo), Hash(uc, u)) for Sample_f, RNG(Hash(seed, wi), Hash(wo)) for PDF,
+// seed = GetOptions().seed (0, pbrt's default).  Where the reference draws a sample as
+// `Sample_f(w, r(), {r(), r()})` / `Point2f(r(), r())` (argument order unspecified in C++), the
+// draws are taken left to right; that choice is shared with core.h and is why parity with a
+// pbrt binary is unpinned for these materials.
+static uint64_t HashIntVec(int a, Vec v) {
+    unsigned char b[16];
+    float f[3] = {v.x, v.y, v.z};
+    std::memcpy(b, &a, 4);
+    std::memcpy(b + 4, f, 12);
+    return Murmur64A(b, 16, 0);
+}
+static Float PowerHeuristic(Float nf, Float fPdf, Float ng, Float gPdf) {
+    Float f = nf * fPdf, g = ng * gPdf;
+    if (std::isinf(Sqr(f))) return 1;
+    return Sqr(f) / (Sqr(f) + Sqr(g));
+}
+struct LayeredBxDF {
+    BxDF top, bottom;  // top: type 1; bottom: type 0 or 2
+    Float thickness = .01f, g = 0;
+    Spectrum albedo;
+    int maxDepth = 10, nSamples = 1;
+    int seed = 0;
+
+    static Float Tr(Float dz, Vec w) {
+        if (std::abs(dz) <= std::numeric_limits<Float>::min()) return 1;
+        return FastExp(-std::abs(dz / w.z));
+    }
+    // a sampled lobe that the reference keeps: exists, f != 0, pdf > 0 (wi.z tested by callers)
+    static bool Good(bool ok, const BSDFSample &bs) { return ok && bs.f && bs.pdf > 0; }
+    const BxDF &Iface(bool isTop) const { return isTop ? top : bottom; }
+
+    int Flags() const {
+        int tf = top.Flags(), bf = bottom.Flags();
+        int fl = BxR;
+        if (tf & BxSpecular) fl |= BxSpecular;
+        if ((tf & BxDiffuse) || (bf & BxDiffuse) || albedo) fl |= BxDiffuse;
+        else if ((tf & BxGlossy) || (bf & BxGlossy)) fl |= BxGlossy;
+        if ((tf & BxT) && (bf & BxT)) fl |= BxT;
+        return fl;
+    }
+
+    Spectrum f(Vec wo, Vec wi, bool radiance) const {
+        Spectrum fr(0.f);
+        if (wo.z < 0) {
+            wo = -wo;
+            wi = -wi;
+        }
+        // entered through the top; the exit is the bottom when wo and wi are on opposite sides
+        const bool exitBottom = !SameHemisphere(wo, wi);
+        const BxDF &exitI = Iface(!exitBottom), &nonExitI = Iface(exitBottom);
+        const Float exitZ = exitBottom ? 0 : thickness;
+        if (SameHemisphere(wo, wi)) fr = top.f(wo, wi, radiance) * Float(nSamples);
+        PCG32 rng(HashIntVec(seed, wo), HashFloats(wi.x, wi.y, wi.z));
+        auto r = [&]() { return rng.Uniform(); };
+        for (int s = 0; s < nSamples; ++s) {
+            BSDFSample wos, wis;
+            Float uc = r(), a = r(), b = r();
+            bool ok = top.Sample_f(wo, uc, a, b, &wos, radiance, 2);
+            if (!Good(ok, wos) || wos.wi.z == 0) continue;
+            uc = r();
+            a = r();
+            b = r();
+            ok = exitI.Sample_f(wi, uc, a, b, &wis, !radiance, 2);
+            if (!Good(ok, wis) || wis.wi.z == 0) continue;
+            Spectrum beta = wos.f * std::abs(wos.wi.z) / wos.pdf;
+            Float z = thickness;
+            Vec w = wos.wi;
+            for (int depth = 0; depth < maxDepth; ++depth) {
+                if (depth > 3 && beta.Max() < 0.25f) {
+                    Float q = std::max<Float>(0, 1 - beta.Max());
+                    if (r() < q) break;
+                    beta = beta / (1 - q);
+                }
+                if (!albedo) {
+                    z = (z == thickness) ? 0 : thickness;
+                    beta = beta * Tr(thickness, w);
+                } else {
+                    Float dz = -CRLog(1 - r()) / (1 / std::abs(w.z));  // SampleExponential, sigma_t = 1
+                    Float zp = w.z > 0 ? (z + dz) : (z - dz);
+                    if (z == zp) continue;
+                    if (0 < zp && zp < thickness) {
+                        Float wt = 1;
+                        if (!(exitI.Flags() & BxSpecular))
+                            wt = PowerHeuristic(1, wis.pdf, 1, HenyeyGreenstein(Dot(-w, -wis.wi), g));
+                        fr = fr + beta * albedo * HenyeyGreenstein(Dot(-w, -wis.wi), g) * wt * Tr(zp - exitZ, wis.wi) *
+                                      wis.f / wis.pdf;
+                        Float u0 = r(), u1 = r(), ppdf;
+                        Vec pwi = SampleHG(-w, g, u0, u1, &ppdf);
+                        if (ppdf == 0 || pwi.z == 0) continue;
+                        beta = beta * (albedo * ppdf / ppdf);
+                        w = pwi;
+                        z = zp;
+                        if (((z < exitZ && w.z > 0) || (z > exitZ && w.z < 0)) && !(exitI.Flags() & BxSpecular)) {
+                            Spectrum fExit = exitI.f(-w, wi, radiance);
+                            if (fExit) {
+                                Float exitPDF = exitI.PDF(-w, wi, 2);
+                                Float wt2 = PowerHeuristic(1, ppdf, 1, exitPDF);
+                                fr = fr + beta * Tr(zp - exitZ, pwi) * fExit * wt2;
+                            }
+                        }
+                        continue;
+                    }
+                    z = Clamp(zp, 0, thickness);
+                }
+                if (z == exitZ) {
+                    BSDFSample bs;
+                    Float c = r(), a2 = r(), b2 = r();
+                    bool ok2 = exitI.Sample_f(-w, c, a2, b2, &bs, radiance, 1);
+                    if (!Good(ok2, bs) || bs.wi.z == 0) break;
+                    beta = beta * (bs.f * std::abs(bs.wi.z) / bs.pdf);
+                    w = bs.wi;
+                } else {
+                    if (!(nonExitI.Flags() & BxSpecular)) {
+                        Float wt = 1;
+                        if (!(exitI.Flags() & BxSpecular)) wt = PowerHeuristic(1, wis.pdf, 1, nonExitI.PDF(-w, -wis.wi));
+                        fr = fr + beta * nonExitI.f(-w, -wis.wi, radiance) * std::abs(wis.wi.z) * wt *
+                                      Tr(thickness, wis.wi) * wis.f / wis.pdf;
+                    }
+                    BSDFSample bs;
+                    Float c = r(), a2 = r(), b2 = r();
+                    bool ok2 = nonExitI.Sample_f(-w, c, a2, b2, &bs, radiance, 1);
+                    if (!Good(ok2, bs) || bs.wi.z == 0) break;
+                    beta = beta * (bs.f * std::abs(bs.wi.z) / bs.pdf);
+                    w = bs.wi;
+                    if (!(exitI.Flags() & BxSpecular)) {
+                        Spectrum fExit = exitI.f(-w, wi, radiance);
+                        if (fExit) {
+                            Float wt = 1;
+                            if (!(nonExitI.Flags() & BxSpecular)) wt = PowerHeuristic(1, bs.pdf, 1, exitI.PDF(-w, wi, 2));
+                            fr = fr + beta * Tr(thickness, bs.wi) * fExit * wt;
+                        }
+                    }
+                }
+            }
+        }
+        return fr / Float(nSamples);
+    }
+
+    // BSDFSample with pdfIsProportional = true
+    bool Sample_f(Vec wo, Float uc, Float u0, Float u1, BSDFSample *out, bool radiance) const {
+        bool flipWi = false;
+        if (wo.z < 0) {
+            wo = -wo;
+            flipWi = true;
+        }
+        BSDFSample bs;
+        bool ok = top.Sample_f(wo, uc, u0, u1, &bs, radiance, 3);
+        if (!Good(ok, bs) || bs.wi.z == 0) return false;
+        if (bs.flags & BxR) {
+            if (flipWi) bs.wi = -bs.wi;
+            *out = bs;
+            return true;
+        }
+        Vec w = bs.wi;
+        bool specularPath = bs.flags & BxSpecular;
+        PCG32 rng(HashIntVec(seed, wo), HashFloats(uc, u0, u1));
+        auto r = [&]() { return rng.Uniform(); };
+        Spectrum fr = bs.f * std::abs(bs.wi.z);
+        Float pdf = bs.pdf;
+        Float z = thickness;
+        for (int depth = 0; depth < maxDepth; ++depth) {
+            Float rrBeta = fr.Max() / pdf;
+            if (depth > 3 && rrBeta < 0.25f) {
+                Float q = std::max<Float>(0, 1 - rrBeta);
+                if (r() < q) return false;
+                pdf *= 1 - q;
+            }
+            if (w.z == 0) return false;
+            if (albedo) {
+                Float dz = -CRLog(1 - r()) / (1 / std::abs(w.z));
+                Float zp = w.z > 0 ? (z + dz) : (z - dz);
+                if (zp == z) return false;
+                if (0 < zp && zp < thickness) {
+                    Float a = r(), b = r(), ppdf;
+                    Vec pwi = SampleHG(-w, g, a, b, &ppdf);
+                    if (ppdf == 0 || pwi.z == 0) return false;
+                    fr = fr * (albedo * ppdf);
+                    pdf *= ppdf;
+                    specularPath = false;
+                    w = pwi;
+                    z = zp;
+                    continue;
+                }
+                z = Clamp(zp, 0, thickness);
+            } else {
+                z = (z == thickness) ? 0 : thickness;
+                fr = fr * Tr(thickness, w);
+            }
+            const BxDF &in = Iface(z != 0);
+            Float c = r(), a = r(), b = r();
+            BSDFSample is;
+            bool ok2 = in.Sample_f(-w, c, a, b, &is, radiance, 3);
+            if (!Good(ok2, is) || is.wi.z == 0) return false;
+            fr = fr * is.f;
+            pdf *= is.pdf;
+            specularPath &= (is.flags & BxSpecular) != 0;
+            w = is.wi;
+            if (is.flags & BxT) {
+                int fl = SameHemisphere(wo, w) ? BxR : BxT;
+                fl |= specularPath ? BxSpecular : BxGlossy;
+                if (flipWi) w = -w;
+                *out = BSDFSample{fr, w, pdf, fl, 1};
+                return true;
+            }
+            fr = fr * std::abs(is.wi.z);
+        }
+        return false;
+    }
+
+    Float PDF(Vec wo, Vec wi, bool radiance) const {
+        if (wo.z < 0) {
+            wo = -wo;
+            wi = -wi;
+        }
+        PCG32 rng(HashIntVec(seed, wi), HashFloats(wo.x, wo.y, wo.z));
+        auto r = [&]() { return rng.Uniform(); };
+        Float pdfSum = 0;
+        if (SameHemisphere(wo, wi)) pdfSum += nSamples * top.PDF(wo, wi, 1);
+        for (int s = 0; s < nSamples; ++s) {
+            if (SameHemisphere(wo, wi)) {
+                // TRT: transmit through the top, reflect off the bottom, transmit back out
+                BSDFSample wos, wis;
+                Float c = r(), a = r(), b = r();
+                bool okO = Good(top.Sample_f(wo, c, a, b, &wos, radiance, 2), wos);
+                c = r();
+                a = r();
+                b = r();
+                bool okI = Good(top.Sample_f(wi, c, a, b, &wis, !radiance, 2), wis);
+                if (okO && okI) {
+                    if (!(top.Flags() & (BxDiffuse | BxGlossy))) {
+                        pdfSum += bottom.PDF(-wos.wi, -wis.wi);
+                    } else {
+                        BSDFSample rs;
+                        c = r();
+                        a = r();
+                        b = r();
+                        if (Good(bottom.Sample_f(-wos.wi, c, a, b, &rs, radiance, 3), rs)) {
+                            if (!(bottom.Flags() & (BxDiffuse | BxGlossy))) {
+                                pdfSum += top.PDF(-rs.wi, wi);
+                            } else {
+                                Float rPDF = bottom.PDF(-wos.wi, -wis.wi);
+                                pdfSum += PowerHeuristic(1, wis.pdf, 1, rPDF) * rPDF;
+                                Float tPDF = top.PDF(-rs.wi, wi);
+                                pdfSum += PowerHeuristic(1, rs.pdf, 1, tPDF) * tPDF;
+                            }
+                        }
+                    }
+                }
+            } else {
+                // TT: through the top and out of the bottom; the opaque bottom never transmits
+                BSDFSample wos, wis;
+                Float c = r(), a = r(), b = r();
+                bool ok = top.Sample_f(wo, c, a, b, &wos, radiance, 3);
+                if (!Good(ok, wos) || wos.wi.z == 0 || (wos.flags & BxR)) continue;
+                c = r();
+                a = r();
+                b = r();
+                ok = bottom.Sample_f(wi, c, a, b, &wis, !radiance, 3);
+                if (!Good(ok, wis) || wis.wi.z == 0 || (wis.flags & BxR)) continue;
+                if (top.Flags() & BxSpecular) pdfSum += bottom.PDF(-wos.wi, wi);
+                else if (bottom.Flags() & BxSpecular) pdfSum += top.PDF(wo, -wis.wi);
+                else pdfSum += (top.PDF(wo, -wis.wi) + bottom.PDF(-wos.wi, wi)) / 2;
+            }
+        }
+        return Lerp(0.9f, 1 / (4 * Pi), pdfSum / nSamples);
+    }
+};
 
 struct MediumProps {
     Spectrum sigma_a, sigma_s, Le;
@@ -2131,7 +2412,51 @@ struct Renderer {
             const float *mc = f->material_coeffs + 4 * mat;
             BxDF bx;
             bx.type = f->material_type[mat];
-            if (bx.type == 0) {
+            const bool layered = bx.type == 4 || bx.type == 5;
+            LayeredBxDF lay;
+            if (layered) {
+                // CoatedDiffuseMaterial / CoatedConductorMaterial::GetBxDF (materials.cpp:301-329, :391-437)
+                const float *mp = f->material_params + 4 * mat, *ml = f->material_layer + 12 * mat;
+                const Float ieta = mp[2] == 0 ? 1.f : mp[2];
+                lay.top.type = 1;
+                lay.top.eta = ieta;
+                lay.top.mf.ax = mp[0];
+                lay.top.mf.ay = mp[1];
+                lay.bottom.type = bx.type == 4 ? 0 : 2;
+                lay.bottom.mf.ax = ml[9];
+                lay.bottom.mf.ay = ml[10];
+                const int es = f->material_spectra[2 * mat], ks = f->material_spectra[2 * mat + 1];
+                for (int i = 0; i < NS; ++i) {
+                    Float l = lambda.lambda[i];
+                    if (bx.type == 4) {
+                        Float r = f->material_constant[mat] ? mc[3] : Sigmoid(mc[0], mc[1], mc[2], l);
+                        lay.bottom.R[i] = Clamp(r, 0, 1);
+                    } else {
+                        Float e, k;
+                        if (es >= 0) {
+                            const int a = f->pl_offsets[es], b = f->pl_offsets[ks];
+                            e = PLEval(f->pl_lambda + a, f->pl_value + a, f->pl_offsets[es + 1] - a, l);
+                            k = PLEval(f->pl_lambda + b, f->pl_value + b, f->pl_offsets[ks + 1] - b, l);
+                        } else {
+                            Float r = Clamp(Sigmoid(mc[0], mc[1], mc[2], l), 0, .9999f);
+                            e = 1;
+                            k = 2 * std::sqrt(r) / std::sqrt(std::max<Float>(0, 1 - r));
+                        }
+                        lay.bottom.etaS[i] = e / ieta;
+                        lay.bottom.kS[i] = k / ieta;
+                    }
+                    Float av = ml[8] != 0 ? ml[7] : Sigmoid(ml[4], ml[5], ml[6], l);
+                    lay.albedo[i] = Clamp(av, 0, 1);
+                }
+                lay.thickness = std::max<Float>(ml[0], std::numeric_limits<Float>::min());
+                lay.g = Clamp(ml[1], -1, 1);
+                lay.maxDepth = (int)ml[2];
+                lay.nSamples = (int)ml[3];
+                if (f->regularize && anyNonSpecular) {
+                    lay.top.mf.Regularize();
+                    lay.bottom.mf.Regularize();
+                }
+            } else if (bx.type == 0) {
                 for (int i = 0; i < NS; ++i) {
                     Float r = f->material_constant[mat] ? mc[3] : Sigmoid(mc[0], mc[1], mc[2], lambda.lambda[i]);
                     bx.R[i] = Clamp(r, 0, 1);
@@ -2162,7 +2487,7 @@ struct Renderer {
             auto toLocal = [&](Vec v) { return Vec(Dot(v, fx_), Dot(v, fy_), Dot(v, fz)); };
             auto fromLocal = [&](Vec v) { return fx_ * v.x + fy_ * v.y + fz * v.z; };
             Vec woL = toLocal(si.wo);
-            const int flags = bx.Flags();
+            const int flags = layered ? lay.Flags() : bx.Flags();
             Spectrum oldBeta = beta;
             bool haveNext = false, nextSpecular = false;
             Vec nextO, nextD;
@@ -2171,10 +2496,12 @@ struct Renderer {
             Float nextEtaScale = etaScale;
             // BSDF::Sample_f (bsdf.h:89-116), then surfscatter.cpp:183-250
             BSDFSample bs;
-            if (woL.z != 0 && flags && bx.Sample_f(woL, iUc, iU0, iU1, &bs) && bs.f && bs.pdf != 0 && bs.wi.z != 0) {
+            const bool sampled = layered ? lay.Sample_f(woL, iUc, iU0, iU1, &bs, true) : bx.Sample_f(woL, iUc, iU0, iU1, &bs);
+            if (woL.z != 0 && flags && sampled && bs.f && bs.pdf != 0 && bs.wi.z != 0) {
                 Vec wi = fromLocal(bs.wi);
                 nb = beta * bs.f * AbsDotN(si.ns, wi) / bs.pdf;
-                nrl = r_u / bs.pdf;
+                // pdfIsProportional (layered): r_l = r_u / BSDF::PDF(wo, wi), wi back in the local frame
+                nrl = layered ? r_u / lay.PDF(woL, toLocal(wi), true) : r_u / bs.pdf;
                 if (bs.flags & BxT) nextEtaScale *= Sqr(bs.eta);
                 Spectrum rrBeta = nb * nextEtaScale / r_u.Average();
                 if (rrBeta.Max() < 1 && depth >= 1) {
@@ -2208,11 +2535,12 @@ struct Renderer {
                         if (f->light_two_sided[li] || DotN(ss.n, -wi) >= 0) Le = LightL(li, lambda);
                         if (Le) {
                             Vec wiL = toLocal(wi);
-                            Spectrum fv = woL.z != 0 ? bx.f(woL, wiL) : Spectrum(0.f);  // BSDF::f (bsdf.h:60-70)
+                            Spectrum fv = woL.z == 0 ? Spectrum(0.f)  // BSDF::f (bsdf.h:60-70)
+                                          : layered ? lay.f(woL, wiL, true) : bx.f(woL, wiL);
                             if (fv) {
                                 Spectrum b2 = oldBeta * fv * AbsDotN(si.ns, wi);
                                 Float lightPDF = ss.pdf * lpmf;
-                                Float bsdfPDF = woL.z != 0 ? bx.PDF(woL, wiL) : 0;
+                                Float bsdfPDF = woL.z == 0 ? 0 : layered ? lay.PDF(woL, wiL, true) : bx.PDF(woL, wiL);
                                 Spectrum ru = r_u * bsdfPDF, rl = r_u * lightPDF;
                                 Spectrum Ld = b2 * Le;
                                 // SpawnRayTo(pi, n, time, pLight.pi, pLight.n) (ray.h:106-111)
@@ -2521,6 +2849,45 @@ void oracle_bxdf(int type, const float *params, const float *eta31, const float 
     Spectrum f = bx.f(wo, wi);
     for (int i = 0; i < NS; ++i) out[38 + i] = f[i];
     out[69] = bx.PDF(wo, wi);
+}
+
+// LayeredBxDF (coated diffuse: params[3] = 0, coated conductor: 2) in the shading frame, as
+// pbrt_debug_layered: params12 = top ax ay eta, bottom type ax ay, thickness g maxdepth
+// nsamples radiance 0; a31 = R or conductor eta, b31 = k, alb31 = albedo; out72 = sample_ok
+// wi3 pdf flags f_sample[31] f(wo,wi)[31] PDF(wo,wi) Flags() 0 0
+void oracle_layered(const float *params, const float *a31, const float *b31, const float *alb31, const float *wo3,
+                    const float *wi3, const float *u3, float *out) {
+    LayeredBxDF L;
+    L.top.type = 1;
+    L.top.mf.ax = params[0];
+    L.top.mf.ay = params[1];
+    L.top.eta = params[2];
+    L.bottom.type = (int)params[3];
+    L.bottom.mf.ax = params[4];
+    L.bottom.mf.ay = params[5];
+    for (int i = 0; i < NS; ++i) {
+        L.bottom.R[i] = a31[i];
+        L.bottom.etaS[i] = a31[i];
+        L.bottom.kS[i] = b31[i];
+        L.albedo[i] = alb31[i];
+    }
+    L.thickness = std::max<Float>(params[6], std::numeric_limits<Float>::min());
+    L.g = params[7];
+    L.maxDepth = (int)params[8];
+    L.nSamples = (int)params[9];
+    const bool radiance = params[10] != 0;
+    Vec wo(wo3[0], wo3[1], wo3[2]), wi(wi3[0], wi3[1], wi3[2]);
+    std::fill(out, out + 72, 0.f);
+    BSDFSample bs;
+    if (L.Sample_f(wo, u3[0], u3[1], u3[2], &bs, radiance)) {
+        float v[6] = {1, bs.wi.x, bs.wi.y, bs.wi.z, bs.pdf, (float)bs.flags};
+        std::memcpy(out, v, sizeof v);
+        for (int i = 0; i < NS; ++i) out[6 + i] = bs.f[i];
+    }
+    Spectrum f = L.f(wo, wi, radiance);
+    for (int i = 0; i < NS; ++i) out[37 + i] = f[i];
+    out[68] = L.PDF(wo, wi, radiance);
+    out[69] = (float)L.Flags();
 }
 
 }  // extern "C"

@@ -40,6 +40,7 @@ def lib():
         _lib.oracle_fresnel.argtypes = [vp, vp]
         _lib.oracle_named_spectrum.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, vp]
         _lib.oracle_bxdf.argtypes = [ctypes.c_int] + [vp] * 7
+        _lib.oracle_layered.argtypes = [vp] * 8
         _lib.oracle_triangle_shading.argtypes = [vp] * 3 + [ctypes.c_int] + [vp] * 3
         _lib.oracle_render.argtypes = [vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, vp]
@@ -130,6 +131,13 @@ def bxdf(bxdf_type, params3, wo, wi, u3, eta31=None, k31=None):
             f32(k31 if k31 is not None else np.zeros(31)), f32(wo), f32(wi), f32(u3)]
     out = np.zeros(70, np.float32)
     lib().oracle_bxdf(int(bxdf_type), *[a.ctypes.data for a in arrs], out.ctypes.data)
+    return out
+
+
+def layered(params12, a31, b31, alb31, wo, wi, u3):
+    arrs = [f32(params12), f32(a31), f32(b31), f32(alb31), f32(wo), f32(wi), f32(u3)]
+    out = np.zeros(72, np.float32)
+    lib().oracle_layered(*[a.ctypes.data for a in arrs], out.ctypes.data)
     return out
 
 

@@ -84,7 +84,7 @@ struct pbrt_scene {
     SceneDesc desc;
     // flattened copies for pbrt_scene_get_flat
     std::vector<float> verts, matCoeffs, lightScale, infScale, dense, sensor, nodeBounds, matParams, plLambda, plValue,
-        mediumParams, mediumValues;
+        mediumParams, mediumValues, matLayer;
     std::vector<int32_t> mediumInfo;
     std::vector<int32_t> tris, lightPrim, lightSpectrum, lightTwoSided, infSpectrum, matConstant, nodeInfo, matType,
         matSpectra, plOffsets;
@@ -103,7 +103,10 @@ struct pbrt_scene {
         matType.clear();
         matParams.clear();
         matSpectra.clear();
+        matLayer.clear();
         for (auto &m : s.materials) {
+            matLayer.insert(matLayer.end(), {m.thickness, m.g, (float)m.maxDepth, (float)m.nSamples, m.a0, m.a1, m.a2,
+                                             m.albedoValue, m.albedoConstant ? 1.f : 0.f, m.cAlphaX, m.cAlphaY, 0.f});
             matCoeffs.insert(matCoeffs.end(), {m.c0, m.c1, m.c2, m.constantValue});
             matConstant.push_back(m.constant ? 1 : 0);
             matType.push_back(m.type);
@@ -185,7 +188,7 @@ struct pbrt_context {
     DevBuf<float> triVerts, matCoeffs, lightScale, lightArea, infScale, dense, sensor;
     DevBuf<int> primMaterial, primLight, matConstant, lightPrim, lightSpectrum, lightTwoSided, infSpectrum;
     DevBuf<int> primOrig, matType, matSpectra, plOffsets;
-    DevBuf<float> matParams, plLambda, plValue, triShade;
+    DevBuf<float> matParams, plLambda, plValue, triShade, matLayer;
     DevBuf<uint8_t> primFlip;
     DevBuf<uint32_t> lightBitTrail, permOffset, permNDigits, permBase;
     DevBuf<uint16_t> perm;
@@ -307,6 +310,15 @@ static void BuildDevice(pbrt_context *c) {
             po.push_back((int)pll.size());
         }
         if (pll.empty()) pll.push_back(0), plv.push_back(0);
+        std::vector<float> ml;
+        for (auto &m : s.materials) {
+            // grey layer albedo uploaded as a constant (same bits, as the reflectances above)
+            const bool grey = !m.albedoConstant && m.a0 == 0 && m.a1 == 0;
+            const float av = grey ? SigmoidPolynomial(0.f, 0.f, m.a2, 500.f) : m.albedoValue;
+            ml.insert(ml.end(), {m.thickness, m.g, (float)m.maxDepth, (float)m.nSamples, m.a0, m.a1, m.a2, av,
+                                 (m.albedoConstant || grey) ? 1.f : 0.f, m.cAlphaX, m.cAlphaY, 0.f});
+        }
+        c->matLayer.Upload(ml);
         c->matType.Upload(mt);
         c->matParams.Upload(mp);
         c->matSpectra.Upload(msp);
@@ -436,7 +448,9 @@ static void BuildDevice(pbrt_context *c) {
     DeviceScene &S = c->S;
     S.media.n = (int)s.media.size();
     c->volumetric = !s.media.empty() ||
-                    std::any_of(s.materials.begin(), s.materials.end(), [](const MaterialDesc &m) { return m.type == kMatInterface; });
+                    std::any_of(s.materials.begin(), s.materials.end(), [](const MaterialDesc &m) {
+                        return m.type == kMatInterface || m.type == kMatCoatedDiffuse || m.type == kMatCoatedConductor;
+                    });
     S.media.cameraMedium = s.cameraMedium;
     S.media.allGrey = 1;
     for (size_t m = 0; m < s.media.size(); ++m) {
@@ -465,6 +479,7 @@ static void BuildDevice(pbrt_context *c) {
     S.matType = c->matType.p;
     S.matParams = (const float4 *)c->matParams.p;
     S.matSpectra = c->matSpectra.p;
+    S.matLayer = (const float4 *)c->matLayer.p;
     S.plOffsets = c->plOffsets.p;
     S.plLambda = c->plLambda.p;
     S.plValue = c->plValue.p;
@@ -923,6 +938,7 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
     f->zs_nbase4_digits = s.zsNBase4Digits;
     f->material_type = scene->matType.data();
     f->material_params = scene->matParams.data();
+    f->material_layer = scene->matLayer.data();
     f->material_spectra = scene->matSpectra.data();
     f->n_pl_spectra = (int)s.plSpectra.size();
     f->pl_offsets = scene->plOffsets.data();
@@ -1326,6 +1342,58 @@ int pbrt_debug_bxdf(int type, const float *params, const float *eta31, const flo
             out[69] = ce.pdf;
         }
     }
+    return 0;
+}
+
+namespace {
+struct DebugLayerSpec {
+    const float *a, *b, *alb;
+    float R(int i) const { return a[i]; }
+    void EtaK(int i, float *e, float *k) const {
+        *e = a[i];
+        *k = b[i];
+    }
+    float Albedo(int i) const { return alb[i]; }
+};
+}  // namespace
+
+int pbrt_debug_layered(const float *params, const float *a31, const float *b31, const float *alb31, const float *wo3,
+                       const float *wi3, const float *u3, float *out) {
+    if (!params || !a31 || !b31 || !alb31 || !wo3 || !wi3 || !u3 || !out) return Fail("null argument");
+    if (params[3] != 0 && params[3] != 2) return Fail("bottom type must be 0 (diffuse) or 2 (conductor)");
+    if (params[8] < 0 || params[9] < 1) return Fail("maxdepth >= 0 and nsamples >= 1 required");
+    const DebugLayerSpec sp{a31, b31, alb31};
+    bool bottomNz = false, albNz = false;
+    for (int i = 0; i < kNSpectrumSamples; ++i) {
+        bottomNz |= a31[i] != 0;
+        albNz |= alb31[i] != 0;
+    }
+    const LayeredBxDF<DebugLayerSpec> L{params[2],
+                                        TrowbridgeReitz{params[0], params[1]},
+                                        TrowbridgeReitz{params[4], params[5]},
+                                        params[3] == 2,
+                                        std::max(params[6], std::numeric_limits<float>::min()),
+                                        params[7],
+                                        albNz,
+                                        (int)params[8],
+                                        (int)params[9],
+                                        0,
+                                        sp,
+                                        bottomNz};
+    const bool radiance = params[10] != 0;
+    const V3 wo(wo3[0], wo3[1], wo3[2]), wi(wi3[0], wi3[1], wi3[2]);
+    memset(out, 0, 72 * sizeof(float));
+    float f[kNSpectrumSamples];
+    const LayerSample bs = L.Sample_f(wo, u3[0], u3[1], u3[2], radiance, f);
+    if (bs.ok) {
+        const float v[6] = {1, bs.wi.x, bs.wi.y, bs.wi.z, bs.pdf, (float)bs.flags};
+        memcpy(out, v, sizeof v);
+        for (int i = 0; i < kNSpectrumSamples; ++i) out[6 + i] = f[i];
+    }
+    L.f(wo, wi, radiance, f);
+    for (int i = 0; i < kNSpectrumSamples; ++i) out[37 + i] = f[i];
+    out[68] = L.PDF(wo, wi, radiance);
+    out[69] = (float)L.LayerFlags();
     return 0;
 }
 

@@ -901,12 +901,18 @@ PHD int DielectricFlags(float eta, const TrowbridgeReitz &tr) {
     int flags = (eta == 1) ? kBxTransmission : (kBxReflection | kBxTransmission);
     return flags | (tr.EffectivelySmooth() ? kBxSpecular : kBxGlossy);
 }
-// DielectricBxDF::Sample_f (bxdfs.cpp:77-170), TransportMode::Radiance, all lobes
-PHD BxSample DielectricSample(float eta, const TrowbridgeReitz &tr, V3 wo, float uc, float u0, float u1) {
+// BxDFReflTransFlags (bxdf.h): which lobes a Sample_f / PDF call may use
+constexpr int kSampleR = 1, kSampleT = 2, kSampleAll = 3;
+// DielectricBxDF::Sample_f (bxdfs.cpp:77-170); radiance = TransportMode::Radiance (the
+// 1/etap^2 factor on transmission), sampleFlags restricts the lobes (LayeredBxDF)
+PHD BxSample DielectricSample(float eta, const TrowbridgeReitz &tr, V3 wo, float uc, float u0, float u1,
+                              bool radiance = true, int sampleFlags = kSampleAll) {
     BxSample s{false, V3(0, 0, 0), 0, 0, 1, 0};
     if (eta == 1 || tr.EffectivelySmooth()) {
         float R = FrDielectric(CosTheta(wo), eta), T = 1 - R;
         float pr = R, pt = T;
+        if (!(sampleFlags & kSampleR)) pr = 0;
+        if (!(sampleFlags & kSampleT)) pt = 0;
         if (pr == 0 && pt == 0) return s;
         if (uc < pr / (pr + pt)) {
             V3 wi(-wo.x, -wo.y, wo.z);
@@ -917,7 +923,7 @@ PHD BxSample DielectricSample(float eta, const TrowbridgeReitz &tr, V3 wo, float
         float etap;
         if (!Refract(wo, V3(0, 0, 1), eta, &etap, &wi)) return s;
         float ft = T / AbsCosTheta(wi);
-        ft /= Sqr(etap);
+        if (radiance) ft /= Sqr(etap);
         s = BxSample{true, wi, ft, pt / (pr + pt), etap, kBxSpecular | kBxTransmission};
         return s;
     }
@@ -925,6 +931,8 @@ PHD BxSample DielectricSample(float eta, const TrowbridgeReitz &tr, V3 wo, float
     float R = FrDielectric(Dot(wo, wm), eta);
     float T = 1 - R;
     float pr = R, pt = T;
+    if (!(sampleFlags & kSampleR)) pr = 0;
+    if (!(sampleFlags & kSampleT)) pt = 0;
     if (pr == 0 && pt == 0) return s;
     if (uc < pr / (pr + pt)) {
         V3 wi = Reflect(wo, wm);
@@ -942,12 +950,13 @@ PHD BxSample DielectricSample(float eta, const TrowbridgeReitz &tr, V3 wo, float
     float dwm_dwi = AbsDot(wi, wm) / denom;
     float pdf = tr.PDF(wo, wm) * dwm_dwi * pt / (pr + pt);
     float ft = T * tr.D(wm) * tr.G(wo, wi) * std::fabs(Dot(wi, wm) * Dot(wo, wm) / (CosTheta(wi) * CosTheta(wo) * denom));
-    ft /= Sqr(etap);
+    if (radiance) ft /= Sqr(etap);
     s = BxSample{true, wi, ft, pdf, etap, kBxGlossy | kBxTransmission};
     return s;
 }
 // DielectricBxDF::f and ::PDF (bxdfs.cpp:172-245); pdfOut may be null
-PHD float DielectricEval(float eta, const TrowbridgeReitz &tr, V3 wo, V3 wi, float *pdfOut) {
+PHD float DielectricEval(float eta, const TrowbridgeReitz &tr, V3 wo, V3 wi, float *pdfOut, bool radiance = true,
+                         int sampleFlags = kSampleAll) {
     if (pdfOut) *pdfOut = 0;
     if (eta == 1 || tr.EffectivelySmooth()) return 0;
     float cosTheta_o = CosTheta(wo), cosTheta_i = CosTheta(wi);
@@ -960,13 +969,15 @@ PHD float DielectricEval(float eta, const TrowbridgeReitz &tr, V3 wo, V3 wi, flo
     if (Dot(wm, wi) * cosTheta_i < 0 || Dot(wm, wo) * cosTheta_o < 0) return 0;
     float F = FrDielectric(Dot(wo, wm), eta);
     float R = F, T = 1 - R, pr = R, pt = T;
+    if (!(sampleFlags & kSampleR)) pr = 0;
+    if (!(sampleFlags & kSampleT)) pt = 0;
     if (reflect) {
         if (pdfOut && !(pr == 0 && pt == 0)) *pdfOut = tr.PDF(wo, wm) / (4 * AbsDot(wo, wm)) * pr / (pr + pt);
         return tr.D(wm) * tr.G(wo, wi) * F / std::fabs(4 * cosTheta_i * cosTheta_o);
     }
     float denom = Sqr(Dot(wi, wm) + Dot(wo, wm) / etap) * cosTheta_i * cosTheta_o;
     float ft = tr.D(wm) * (1 - F) * tr.G(wo, wi) * std::fabs(Dot(wi, wm) * Dot(wo, wm) / denom);
-    ft /= Sqr(etap);
+    if (radiance) ft /= Sqr(etap);
     if (pdfOut && !(pr == 0 && pt == 0)) {
         float denomP = Sqr(Dot(wi, wm) + Dot(wo, wm) / etap);
         float dwm_dwi = AbsDot(wi, wm) / denomP;
@@ -1457,5 +1468,438 @@ PHD void FilterSample(const FilterParams &f, const FilterTableView &tab, float u
     *py = d1;
     *weight = tab.F()[v * tab.nu + u] / (pdf0 * pdf1);
 }
+
+// ---------------------------------------------------------------- layered BxDFs
+// LayeredBxDF<DielectricBxDF, DiffuseBxDF | ConductorBxDF, twoSided = true> (bxdfs.h:565-1052):
+// CoatedDiffuseBxDF / CoatedConductorBxDF.  f, Sample_f and PDF are stochastic estimates from a
+// random walk between the two interfaces with an RNG seeded from the directions
+// (Hash(GetOptions().seed, wo), Hash(wi) ...).  Two pairs of draws the reference writes as
+// Point2f(r(), r()) (unspecified argument order in C++) are taken left to right here.
+// Spectra are 31-wide (the bottom's per-wavelength values and the albedo come from `sp`):
+//   sp.R(i)            diffuse reflectance (clamped) at lambda_i
+//   sp.EtaK(i, &e, &k) conductor eta, k at lambda_i
+//   sp.Albedo(i)       layer albedo at lambda_i
+struct LayerSample {
+    bool ok;
+    V3 wi;
+    float pdf;
+    int flags;
+    bool pdfIsProportional;
+};
+PHD float PowerHeuristic(float nf, float fPdf, float ng, float gPdf) {  // util/sampling.h
+    const float f = nf * fPdf, g = ng * gPdf;
+    if (std::isinf(Sqr(f))) return 1;
+    return Sqr(f) / (Sqr(f) + Sqr(g));
+}
+PHD uint64_t HashIntV3(int a, V3 v) {
+    const uint32_t w[4] = {(uint32_t)a, FloatToBits(v.x), FloatToBits(v.y), FloatToBits(v.z)};
+    return HashWords(w, 4);
+}
+PHD uint64_t HashF3(float a, float b, float c) {
+    const uint32_t w[3] = {FloatToBits(a), FloatToBits(b), FloatToBits(c)};
+    return HashWords(w, 3);
+}
+
+template <typename Spec>
+struct LayeredBxDF {
+    // top: DielectricBxDF(eta, trTop); bottom: diffuse (conductor = false) or ConductorBxDF(trBot)
+    float eta;
+    TrowbridgeReitz trTop, trBot;
+    bool conductor;
+    float thickness, g;
+    bool albedoNz;
+    int maxDepth, nSamples, seed;
+    const Spec &sp;
+    bool bottomNz;  // diffuse: R != 0 at some wavelength (its Flags() is Unset otherwise)
+
+    PHD static float Tr(float dz, V3 w) {
+        if (std::fabs(dz) <= 1.17549435e-38f) return 1;
+        return FastExp(-std::fabs(dz / w.z));
+    }
+    // ---- interfaces (iface 0 = top dielectric, 1 = bottom)
+    PHD int Flags(int iface) const {
+        if (iface == 0) return DielectricFlags(eta, trTop);
+        if (conductor) return kBxReflection | (trBot.EffectivelySmooth() ? kBxSpecular : kBxGlossy);
+        return bottomNz ? (kBxReflection | kBxDiffuse) : 0;
+    }
+    PHD bool IsSpecularI(int iface) const { return Flags(iface) & kBxSpecular; }
+    // f of an interface: the top's is a scalar (ft[0] only, isScalar = true)
+    PHD void F(int iface, V3 wo, V3 wi, bool radiance, float out[kNSpectrumSamples], bool *isScalar) const {
+        if (iface == 0) {
+            out[0] = DielectricEval(eta, trTop, wo, wi, nullptr, radiance);
+            *isScalar = true;
+            return;
+        }
+        *isScalar = false;
+        if (!conductor) {
+            const bool same = SameHemisphere(wo, wi);
+            PHD_UNROLL
+            for (int i = 0; i < kNSpectrumSamples; ++i) out[i] = same ? sp.R(i) * kInvPi : 0.f;
+            return;
+        }
+        const ConductorTerms ct = ConductorEval(trBot, wo, wi);
+        PHD_UNROLL
+        for (int i = 0; i < kNSpectrumSamples; ++i) {
+            float e, k;
+            sp.EtaK(i, &e, &k);
+            out[i] = ct.ok ? ConductorF(ct, e, k) : 0.f;
+        }
+    }
+    PHD float Pdf(int iface, V3 wo, V3 wi, bool radiance, int flags) const {
+        if (iface == 0) {
+            float pdf;
+            DielectricEval(eta, trTop, wo, wi, &pdf, radiance, flags);
+            return pdf;
+        }
+        if (!(flags & kSampleR) || !SameHemisphere(wo, wi)) return 0;
+        if (!conductor) return CosineHemispherePDF(std::fabs(wi.z));
+        if (trBot.EffectivelySmooth()) return 0;
+        return ConductorEval(trBot, wo, wi).pdf;
+    }
+    // Sample_f of an interface; f into out (scalar for the top).  True when the sample exists
+    // with f != 0 and pdf > 0 (callers add the wi.z != 0 test where the reference has it).
+    PHD bool Sample(int iface, V3 wo, float uc, float u0, float u1, bool radiance, int flags, BxSample *bs,
+                    float out[kNSpectrumSamples], bool *isScalar) const {
+        if (iface == 0) {
+            *bs = DielectricSample(eta, trTop, wo, uc, u0, u1, radiance, flags);
+            out[0] = bs->f;
+            *isScalar = true;
+            return bs->ok && bs->f != 0 && bs->pdf > 0;
+        }
+        *isScalar = false;
+        if (!(flags & kSampleR)) return false;
+        if (!conductor) {
+            if (!bottomNz) return false;
+            V3 wi = SampleCosineHemisphere(u0, u1);
+            if (wo.z < 0) wi.z *= -1;
+            const float pdf = CosineHemispherePDF(std::fabs(wi.z));
+            *bs = BxSample{true, wi, 0, pdf, 1, kBxReflection | kBxDiffuse};
+            bool nz = false;
+            PHD_UNROLL
+            for (int i = 0; i < kNSpectrumSamples; ++i) {
+                out[i] = sp.R(i) * kInvPi;
+                nz |= out[i] != 0;
+            }
+            return nz && pdf > 0;
+        }
+        const ConductorTerms ct = ConductorSample(trBot, wo, u0, u1);
+        if (!ct.ok) return false;
+        *bs = BxSample{true, ct.wi, 0, ct.pdf, 1, kBxReflection | (ct.specular ? kBxSpecular : kBxGlossy)};
+        bool nz = false;
+        PHD_UNROLL
+        for (int i = 0; i < kNSpectrumSamples; ++i) {
+            float e, k;
+            sp.EtaK(i, &e, &k);
+            out[i] = ConductorF(ct, e, k);
+            nz |= out[i] != 0;
+        }
+        return nz && ct.pdf > 0;
+    }
+    PHD int LayerFlags() const {  // LayeredBxDF::Flags
+        const int t = Flags(0), b = Flags(1);
+        int flags = kBxReflection;
+        if (t & kBxSpecular) flags |= kBxSpecular;
+        if ((t & kBxDiffuse) || (b & kBxDiffuse) || albedoNz) flags |= kBxDiffuse;
+        else if ((t & kBxGlossy) || (b & kBxGlossy)) flags |= kBxGlossy;
+        if ((t & kBxTransmission) && (b & kBxTransmission)) flags |= kBxTransmission;
+        return flags;
+    }
+
+    // LayeredBxDF::f (bxdfs.h:611-781)
+    PHD void f(V3 wo, V3 wi, bool radiance, float fo[kNSpectrumSamples]) const {
+        PHD_UNROLL
+        for (int i = 0; i < kNSpectrumSamples; ++i) fo[i] = 0;
+        if (wo.z < 0) {  // twoSided
+            wo = -wo;
+            wi = -wi;
+        }
+        const bool enteredTop = true;
+        const int enter = 0;
+        const bool exitBottom = SameHemisphere(wo, wi) ^ enteredTop;
+        const int exitI = exitBottom ? 1 : 0, nonExitI = exitBottom ? 0 : 1;
+        const float exitZ = exitBottom ? 0 : thickness;
+        float tmp[kNSpectrumSamples];
+        bool sc;
+        if (SameHemisphere(wo, wi)) {
+            F(enter, wo, wi, radiance, tmp, &sc);
+            PHD_UNROLL
+            for (int i = 0; i < kNSpectrumSamples; ++i) fo[i] = nSamples * (sc ? tmp[0] : tmp[i]);
+        }
+        PCG32 rng(HashIntV3(seed, wo), HashV3(wi));
+        float beta[kNSpectrumSamples], wisF[kNSpectrumSamples];
+        for (int s = 0; s < nSamples; ++s) {
+            BxSample wos, wis;
+            float uc = rng.Uniform(), a0 = rng.Uniform(), a1 = rng.Uniform();
+            if (!Sample(enter, wo, uc, a0, a1, radiance, kSampleT, &wos, tmp, &sc) || wos.wi.z == 0) continue;
+            uc = rng.Uniform();
+            a0 = rng.Uniform();
+            a1 = rng.Uniform();
+            bool wisSc;
+            if (!Sample(exitI, wi, uc, a0, a1, !radiance, kSampleT, &wis, wisF, &wisSc) || wis.wi.z == 0) continue;
+            PHD_UNROLL
+            for (int i = 0; i < kNSpectrumSamples; ++i) beta[i] = (sc ? tmp[0] : tmp[i]) * AbsCosTheta(wos.wi) / wos.pdf;
+            float z = enteredTop ? thickness : 0;
+            V3 w = wos.wi;
+            for (int depth = 0; depth < maxDepth; ++depth) {
+                if (depth > 3) {
+                    float mx = beta[0];
+                    PHD_UNROLL
+                    for (int i = 1; i < kNSpectrumSamples; ++i) mx = std::fmax(mx, beta[i]);
+                    if (mx < 0.25f) {
+                        const float q = std::fmax(0.f, 1 - mx);
+                        if (rng.Uniform() < q) break;
+                        PHD_UNROLL
+                        for (int i = 0; i < kNSpectrumSamples; ++i) beta[i] /= 1 - q;
+                    }
+                }
+                if (!albedoNz) {
+                    z = (z == thickness) ? 0 : thickness;
+                    const float tr = Tr(thickness, w);
+                    PHD_UNROLL
+                    for (int i = 0; i < kNSpectrumSamples; ++i) beta[i] *= tr;
+                } else {
+                    const float sigma_t = 1;
+                    const float dz = SampleExponential(rng.Uniform(), sigma_t / std::fabs(w.z));
+                    const float zp = w.z > 0 ? (z + dz) : (z - dz);
+                    if (z == zp) continue;
+                    if (0 < zp && zp < thickness) {
+                        // scattering in the layer medium: NEE through the exit interface along wis
+                        float wt = 1;
+                        if (!IsSpecularI(exitI)) wt = PowerHeuristic(1, wis.pdf, 1, HenyeyGreenstein(Dot(-w, -wis.wi), g));
+                        const float ph = HenyeyGreenstein(Dot(-w, -wis.wi), g);
+                        const float trw = Tr(zp - exitZ, wis.wi);
+                        PHD_UNROLL
+                        for (int i = 0; i < kNSpectrumSamples; ++i)
+                            fo[i] += beta[i] * sp.Albedo(i) * ph * wt * trw * (wisSc ? wisF[0] : wisF[i]) / wis.pdf;
+                        const float p0 = rng.Uniform(), p1 = rng.Uniform();
+                        float ppdf;
+                        const V3 pwi = SampleHenyeyGreenstein(-w, g, p0, p1, &ppdf);
+                        if (ppdf == 0 || pwi.z == 0) continue;
+                        PHD_UNROLL
+                        for (int i = 0; i < kNSpectrumSamples; ++i) beta[i] *= sp.Albedo(i) * ppdf / ppdf;
+                        w = pwi;
+                        z = zp;
+                        if (((z < exitZ && w.z > 0) || (z > exitZ && w.z < 0)) && !IsSpecularI(exitI)) {
+                            bool fsc;
+                            F(exitI, -w, wi, radiance, tmp, &fsc);
+                            bool fnz = false;
+                            PHD_UNROLL
+                            for (int i = 0; i < kNSpectrumSamples; ++i) fnz |= (fsc ? tmp[0] : tmp[i]) != 0;
+                            if (fnz) {
+                                const float exitPDF = Pdf(exitI, -w, wi, radiance, kSampleT);
+                                const float wt2 = PowerHeuristic(1, ppdf, 1, exitPDF);
+                                const float tr2 = Tr(zp - exitZ, pwi);
+                                PHD_UNROLL
+                                for (int i = 0; i < kNSpectrumSamples; ++i)
+                                    fo[i] += beta[i] * tr2 * (fsc ? tmp[0] : tmp[i]) * wt2;
+                            }
+                        }
+                        continue;
+                    }
+                    z = Clampf(zp, 0, thickness);
+                }
+                if (z == exitZ) {
+                    BxSample bs;
+                    const float c = rng.Uniform(), b0 = rng.Uniform(), b1 = rng.Uniform();
+                    bool bsc;
+                    if (!Sample(exitI, -w, c, b0, b1, radiance, kSampleR, &bs, tmp, &bsc) || bs.wi.z == 0) break;
+                    PHD_UNROLL
+                    for (int i = 0; i < kNSpectrumSamples; ++i)
+                        beta[i] *= (bsc ? tmp[0] : tmp[i]) * AbsCosTheta(bs.wi) / bs.pdf;
+                    w = bs.wi;
+                } else {
+                    if (!IsSpecularI(nonExitI)) {
+                        float wt = 1;
+                        if (!IsSpecularI(exitI)) wt = PowerHeuristic(1, wis.pdf, 1, Pdf(nonExitI, -w, -wis.wi, radiance, kSampleAll));
+                        bool nsc;
+                        F(nonExitI, -w, -wis.wi, radiance, tmp, &nsc);
+                        const float trw = Tr(thickness, wis.wi);
+                        PHD_UNROLL
+                        for (int i = 0; i < kNSpectrumSamples; ++i)
+                            fo[i] += beta[i] * (nsc ? tmp[0] : tmp[i]) * AbsCosTheta(wis.wi) * wt * trw *
+                                     (wisSc ? wisF[0] : wisF[i]) / wis.pdf;
+                    }
+                    BxSample bs;
+                    const float c = rng.Uniform(), b0 = rng.Uniform(), b1 = rng.Uniform();
+                    bool bsc;
+                    if (!Sample(nonExitI, -w, c, b0, b1, radiance, kSampleR, &bs, tmp, &bsc) || bs.wi.z == 0) break;
+                    PHD_UNROLL
+                    for (int i = 0; i < kNSpectrumSamples; ++i)
+                        beta[i] *= (bsc ? tmp[0] : tmp[i]) * AbsCosTheta(bs.wi) / bs.pdf;
+                    w = bs.wi;
+                    if (!IsSpecularI(exitI)) {
+                        bool fsc;
+                        F(exitI, -w, wi, radiance, tmp, &fsc);
+                        bool fnz = false;
+                        PHD_UNROLL
+                        for (int i = 0; i < kNSpectrumSamples; ++i) fnz |= (fsc ? tmp[0] : tmp[i]) != 0;
+                        if (fnz) {
+                            float wt = 1;
+                            if (!IsSpecularI(nonExitI)) {
+                                const float exitPDF = Pdf(exitI, -w, wi, radiance, kSampleT);
+                                wt = PowerHeuristic(1, bs.pdf, 1, exitPDF);
+                            }
+                            const float tr2 = Tr(thickness, bs.wi);
+                            PHD_UNROLL
+                            for (int i = 0; i < kNSpectrumSamples; ++i) fo[i] += beta[i] * tr2 * (fsc ? tmp[0] : tmp[i]) * wt;
+                        }
+                    }
+                }
+            }
+        }
+        PHD_UNROLL
+        for (int i = 0; i < kNSpectrumSamples; ++i) fo[i] /= nSamples;
+    }
+
+    // LayeredBxDF::Sample_f (bxdfs.h:783-911): f into fo, wi / pdf / flags in the result
+    PHD LayerSample Sample_f(V3 wo, float uc, float u0, float u1, bool radiance, float fo[kNSpectrumSamples]) const {
+        LayerSample res{false, V3(0, 0, 0), 0, 0, false};
+        bool flipWi = false;
+        if (wo.z < 0) {
+            wo = -wo;
+            flipWi = true;
+        }
+        BxSample bs;
+        bool sc;
+        float tmp[kNSpectrumSamples];
+        if (!Sample(0, wo, uc, u0, u1, radiance, kSampleAll, &bs, tmp, &sc) || bs.wi.z == 0) return res;
+        if (bs.flags & kBxReflection) {
+            PHD_UNROLL
+            for (int i = 0; i < kNSpectrumSamples; ++i) fo[i] = sc ? tmp[0] : tmp[i];
+            res = LayerSample{true, flipWi ? -bs.wi : bs.wi, bs.pdf, bs.flags, true};
+            return res;
+        }
+        V3 w = bs.wi;
+        bool specularPath = bs.flags & kBxSpecular;
+        PCG32 rng(HashIntV3(seed, wo), HashF3(uc, u0, u1));
+        PHD_UNROLL
+        for (int i = 0; i < kNSpectrumSamples; ++i) fo[i] = (sc ? tmp[0] : tmp[i]) * AbsCosTheta(bs.wi);
+        float pdf = bs.pdf;
+        float z = thickness;
+        for (int depth = 0; depth < maxDepth; ++depth) {
+            float mx = fo[0];
+            PHD_UNROLL
+            for (int i = 1; i < kNSpectrumSamples; ++i) mx = std::fmax(mx, fo[i]);
+            const float rrBeta = mx / pdf;
+            if (depth > 3 && rrBeta < 0.25f) {
+                const float q = std::fmax(0.f, 1 - rrBeta);
+                if (rng.Uniform() < q) return res;
+                pdf *= 1 - q;
+            }
+            if (w.z == 0) return res;
+            if (albedoNz) {
+                const float sigma_t = 1;
+                const float dz = SampleExponential(rng.Uniform(), sigma_t / AbsCosTheta(w));
+                const float zp = w.z > 0 ? (z + dz) : (z - dz);
+                if (zp == z) return res;
+                if (0 < zp && zp < thickness) {
+                    const float p0 = rng.Uniform(), p1 = rng.Uniform();
+                    float ppdf;
+                    const V3 pwi = SampleHenyeyGreenstein(-w, g, p0, p1, &ppdf);
+                    if (ppdf == 0 || pwi.z == 0) return res;
+                    PHD_UNROLL
+                    for (int i = 0; i < kNSpectrumSamples; ++i) fo[i] *= sp.Albedo(i) * ppdf;
+                    pdf *= ppdf;
+                    specularPath = false;
+                    w = pwi;
+                    z = zp;
+                    continue;
+                }
+                z = Clampf(zp, 0, thickness);
+            } else {
+                z = (z == thickness) ? 0 : thickness;
+                const float tr = Tr(thickness, w);
+                PHD_UNROLL
+                for (int i = 0; i < kNSpectrumSamples; ++i) fo[i] *= tr;
+            }
+            const int iface = z == 0 ? 1 : 0;
+            const float c = rng.Uniform(), b0 = rng.Uniform(), b1 = rng.Uniform();
+            BxSample is;
+            bool isc;
+            if (!Sample(iface, -w, c, b0, b1, radiance, kSampleAll, &is, tmp, &isc) || is.wi.z == 0) return res;
+            PHD_UNROLL
+            for (int i = 0; i < kNSpectrumSamples; ++i) fo[i] *= isc ? tmp[0] : tmp[i];
+            pdf *= is.pdf;
+            specularPath &= (is.flags & kBxSpecular) != 0;
+            w = is.wi;
+            if (is.flags & kBxTransmission) {
+                int flags = SameHemisphere(wo, w) ? kBxReflection : kBxTransmission;
+                flags |= specularPath ? kBxSpecular : kBxGlossy;
+                res = LayerSample{true, flipWi ? -w : w, pdf, flags, true};
+                return res;
+            }
+            const float ci = AbsCosTheta(is.wi);
+            PHD_UNROLL
+            for (int i = 0; i < kNSpectrumSamples; ++i) fo[i] *= ci;
+        }
+        return res;
+    }
+
+    // LayeredBxDF::PDF (bxdfs.h:913-1016)
+    PHD float PDF(V3 wo, V3 wi, bool radiance) const {
+        if (wo.z < 0) {
+            wo = -wo;
+            wi = -wi;
+        }
+        PCG32 rng(HashIntV3(seed, wi), HashV3(wo));
+        const bool enteredTop = true;
+        float pdfSum = 0;
+        if (SameHemisphere(wo, wi)) pdfSum += nSamples * Pdf(0, wo, wi, radiance, kSampleR);
+        float tmp[kNSpectrumSamples];
+        bool sc;
+        for (int s = 0; s < nSamples; ++s) {
+            if (SameHemisphere(wo, wi)) {
+                const int rI = enteredTop ? 1 : 0, tI = enteredTop ? 0 : 1;
+                BxSample wos, wis;
+                float c = rng.Uniform(), a0 = rng.Uniform(), a1 = rng.Uniform();
+                const bool goodO = Sample(tI, wo, c, a0, a1, radiance, kSampleT, &wos, tmp, &sc);
+                c = rng.Uniform();
+                a0 = rng.Uniform();
+                a1 = rng.Uniform();
+                const bool goodI = Sample(tI, wi, c, a0, a1, !radiance, kSampleT, &wis, tmp, &sc);
+                if (goodO && goodI) {
+                    if (!(Flags(tI) & (kBxDiffuse | kBxGlossy))) {
+                        pdfSum += Pdf(rI, -wos.wi, -wis.wi, radiance, kSampleAll);
+                    } else {
+                        BxSample rs;
+                        c = rng.Uniform();
+                        a0 = rng.Uniform();
+                        a1 = rng.Uniform();
+                        if (Sample(rI, -wos.wi, c, a0, a1, radiance, kSampleAll, &rs, tmp, &sc)) {
+                            if (!(Flags(rI) & (kBxDiffuse | kBxGlossy))) {
+                                pdfSum += Pdf(tI, -rs.wi, wi, radiance, kSampleAll);
+                            } else {
+                                const float rPDF = Pdf(rI, -wos.wi, -wis.wi, radiance, kSampleAll);
+                                float wt = PowerHeuristic(1, wis.pdf, 1, rPDF);
+                                pdfSum += wt * rPDF;
+                                const float tPDF = Pdf(tI, -rs.wi, wi, radiance, kSampleAll);
+                                wt = PowerHeuristic(1, rs.pdf, 1, tPDF);
+                                pdfSum += wt * tPDF;
+                            }
+                        }
+                    }
+                }
+            } else {
+                // TT term: the opaque bottom never transmits, so every sample is rejected
+                const int toI = enteredTop ? 0 : 1, tiI = enteredTop ? 1 : 0;
+                BxSample wos, wis;
+                float c = rng.Uniform(), a0 = rng.Uniform(), a1 = rng.Uniform();
+                if (!Sample(toI, wo, c, a0, a1, radiance, kSampleAll, &wos, tmp, &sc) || wos.wi.z == 0 ||
+                    (wos.flags & kBxReflection))
+                    continue;
+                c = rng.Uniform();
+                a0 = rng.Uniform();
+                a1 = rng.Uniform();
+                if (!Sample(tiI, wi, c, a0, a1, !radiance, kSampleAll, &wis, tmp, &sc) || wis.wi.z == 0 ||
+                    (wis.flags & kBxReflection))
+                    continue;
+                if (Flags(toI) & kBxSpecular) pdfSum += Pdf(tiI, -wos.wi, wi, radiance, kSampleAll);
+                else if (Flags(tiI) & kBxSpecular) pdfSum += Pdf(toI, wo, -wis.wi, radiance, kSampleAll);
+                else pdfSum += (Pdf(toI, wo, -wis.wi, radiance, kSampleAll) + Pdf(tiI, -wos.wi, wi, radiance, kSampleAll)) / 2;
+            }
+        }
+        return Lerpf(0.9f, 1 / (4 * kPi), pdfSum / nSamples);
+    }
+};
 
 }  // namespace pbrt_amd

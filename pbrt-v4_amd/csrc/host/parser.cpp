@@ -641,6 +641,44 @@ class Parser {
                 m.kSpec = k ? SpectrumParam(k, ps.loc) : NamedPLSpectrum("metal-Cu-k", ps.loc);
             }
             Roughness(ps, &m);
+        } else if (type == "coateddiffuse") {
+            // CoatedDiffuseMaterial::Create (materials.cpp:347-389)
+            m.type = kMatCoatedDiffuse;
+            Param *r = ps.Find("reflectance");
+            if (!r) {
+                m.constant = true;
+                m.constantValue = 0.5f;
+            } else {
+                AlbedoParam(r, ps.loc, &m.constant, &m.constantValue, &m.c0, &m.c1, &m.c2);
+            }
+            Roughness(ps, &m);
+            LayerParams(ps, &m, "eta");
+        } else if (type == "coatedconductor") {
+            // CoatedConductorMaterial::Create (materials.cpp:460-540)
+            m.type = kMatCoatedConductor;
+            MaterialDesc c;
+            Roughness(ps, &m, "interface.");
+            Roughness(ps, &c, "conductor.");
+            m.cAlphaX = c.alphaX;
+            m.cAlphaY = c.alphaY;
+            Param *eta = ps.Find("conductor.eta"), *k = ps.Find("conductor.k"), *refl = ps.Find("reflectance");
+            if (refl && (eta || k))
+                throw Error(ps.loc + ": For the coated conductor material, both \"reflectance\" and \"eta\" and \"k\" can't be provided.");
+            if (refl) {
+                if (refl->type != "rgb" || refl->nums.size() != 3)
+                    throw Error(ps.loc + ": coated conductor reflectance must be \"rgb\" (3 values)");
+                float rgb[3] = {(float)refl->nums[0], (float)refl->nums[1], (float)refl->nums[2]};
+                for (float v : rgb)
+                    if (v < 0 || v > 1) throw Error(ps.loc + ": RGB parameter \"reflectance\" used as an albedo has > 1 component.");
+                auto cf = RGBToSigmoidCoeffs(rgb[0], rgb[1], rgb[2]);
+                m.c0 = cf[0];
+                m.c1 = cf[1];
+                m.c2 = cf[2];
+            } else {
+                m.etaSpec = eta ? SpectrumParam(eta, ps.loc) : NamedPLSpectrum("metal-Cu-eta", ps.loc);
+                m.kSpec = k ? SpectrumParam(k, ps.loc) : NamedPLSpectrum("metal-Cu-k", ps.loc);
+            }
+            LayerParams(ps, &m, "interface.eta");
         } else {
             throw Error(ps.loc + ": material \"" + type + "\" is not supported yet");
         }
@@ -650,13 +688,49 @@ class Parser {
         return (int)scene.materials.size() - 1;
     }
 
+    // an Albedo-type spectrum parameter: "rgb" in [0,1] (RGBAlbedoSpectrum sigmoid) or "float"
+    void AlbedoParam(Param *r, const std::string &loc, bool *constant, float *value, float *c0, float *c1, float *c2) {
+        if (r->type == "rgb") {
+            if (r->nums.size() != 3) throw Error(loc + ": " + r->name + " needs 3 values");
+            float rgb[3] = {(float)r->nums[0], (float)r->nums[1], (float)r->nums[2]};
+            for (float v : rgb)
+                if (v < 0 || v > 1) throw Error(loc + ": RGB " + r->name + " must be in [0,1]");
+            auto c = RGBToSigmoidCoeffs(rgb[0], rgb[1], rgb[2]);
+            *constant = false;
+            *c0 = c[0];
+            *c1 = c[1];
+            *c2 = c[2];
+        } else if (r->type == "float" && !r->nums.empty()) {
+            *constant = true;
+            *value = (float)r->nums[0];
+        } else {
+            throw Error(loc + ": " + r->name + " of type " + r->type + " not supported");
+        }
+    }
+    // the LayeredBxDF parameters common to both coated materials; etaName: the interface IOR
+    void LayerParams(ParamSet &ps, MaterialDesc *m, const std::string &etaName) {
+        if (Param *e = ps.Find(etaName, "float")) {
+            if (e->nums.empty()) throw Error(ps.loc + ": \"float " + etaName + "\" needs a value");
+            m->eta = (float)e->nums[0];
+        } else if (ps.Find(etaName, "spectrum")) {
+            throw Error(ps.loc + ": spectrally varying " + etaName + " (dispersion) is not supported yet");
+        }
+        if (m->eta == 0) m->eta = 1;
+        m->thickness = ps.GetFloat("thickness", .01f);
+        m->g = ps.GetFloat("g", 0.f);
+        m->maxDepth = ps.GetInt("maxdepth", 10);
+        m->nSamples = ps.GetInt("nsamples", 1);
+        if (Param *a = ps.Find("albedo")) AlbedoParam(a, ps.loc, &m->albedoConstant, &m->albedoValue, &m->a0, &m->a1, &m->a2);
+    }
+
     // uroughness / vroughness / roughness + remaproughness -> TrowbridgeReitzDistribution alphas
-    // (materials.cpp:62-70, materials.h:194-199 / :494-509, util/scattering.h:109-118, 192)
-    void Roughness(ParamSet &ps, MaterialDesc *m) {
-        Param *u = ps.Find("uroughness", "float"), *v = ps.Find("vroughness", "float");
+    // (materials.cpp:62-70, materials.h:194-199 / :494-509, util/scattering.h:109-118, 192);
+    // prefix "interface." / "conductor." for the coated conductor's two distributions
+    void Roughness(ParamSet &ps, MaterialDesc *m, const std::string &prefix = "") {
+        Param *u = ps.Find(prefix + "uroughness", "float"), *v = ps.Find(prefix + "vroughness", "float");
         float ur = 0, vr = 0;
         if (!u || !v) {
-            Param *r = ps.Find("roughness", "float");
+            Param *r = ps.Find(prefix + "roughness", "float");
             float rv = (r && !r->nums.empty()) ? (float)r->nums[0] : 0.f;
             ur = vr = rv;
         }

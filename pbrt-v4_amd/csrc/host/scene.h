@@ -32,6 +32,9 @@ bool SwapsHandedness(const Mat4 &m);
 enum MaterialType : int { kMatDiffuse = 0, kMatDielectric = 1, kMatConductor = 2, kMatNumTypes = 3 };
 // Material "interface" (a null material: medium boundary only, materials.cpp); not a BxDF type
 constexpr int kMatInterface = 3;
+// LayeredBxDF materials (bxdfs.h:565-1052, materials.cpp:301-540); shaded by the volumetric
+// kernels' layered stage
+constexpr int kMatCoatedDiffuse = 4, kMatCoatedConductor = 5;
 
 // Participating media (media.h:209-350, media.cpp:167-330).  Spectra are DenselySampled
 // 395..705 nm tables in SceneDesc::denseSpectra with pbrt's constructor scaling applied
@@ -64,6 +67,13 @@ struct MaterialDesc {
     float alphaX = 0, alphaY = 0;
     float eta = 1.5f;              // dielectric: ConstantSpectrum eta (materials.cpp:51-60)
     int etaSpec = -1, kSpec = -1;  // conductor: SceneDesc::plSpectra indices; -1/-1 = reflectance
+    // coateddiffuse / coatedconductor: alphaX/alphaY/eta are the interface's (DielectricBxDF),
+    // c0..c2/constant the diffuse or conductor "reflectance", etaSpec/kSpec conductor.eta / .k
+    float thickness = .01f, g = 0;
+    int maxDepth = 10, nSamples = 1;
+    bool albedoConstant = true;
+    float albedoValue = 0, a0 = 0, a1 = 0, a2 = 0;  // layer albedo: constant or sigmoid
+    float cAlphaX = 0, cAlphaY = 0;                 // conductor.{u,v}roughness -> alphas
     std::string name;
 };
 

@@ -55,6 +55,7 @@ constexpr int kCntRay = 0, kCntMat = 1, kCntShadow = 2, kCntEscaped = 3, kCntEmi
 // diffuse uses kCntMat, dielectric kCntMat + 4, conductor kCntMat + 5
 constexpr int kNumMatTypes = 3;  // == host kMatNumTypes (diffuse, dielectric, conductor)
 constexpr int kMatDiffuseT = 0, kMatDielectricT = 1, kMatConductorT = 2;
+constexpr int kMatCoatedDiffuseT = 4, kMatCoatedConductorT = 5;  // layered (volumetric path only)
 PHD int MatCounter(int type) { return type == 0 ? kCntMat : kCntMat + 3 + type; }
 PHD int CounterIndex(int depth, int queue, int shard) {
     return ((depth * kNumQueues + queue) * kShards + shard) * kCounterPad;
@@ -106,6 +107,8 @@ struct DeviceScene {
     const int *matType;        // [nMaterials] 0 diffuse, 1 dielectric, 2 conductor
     const float4 *matParams;   // alpha_x, alpha_y (TrowbridgeReitz), dielectric eta, 0
     const int *matSpectra;     // [nMaterials][2] conductor eta / k piecewise-linear spectra
+    const float4 *matLayer;    // [nMaterials][3] layered: thickness g maxDepth nSamples | albedo c0..c2 value |
+                               // albedo constant, conductor alpha_x alpha_y, 0
     int matTypeMask;           // bit t: some material of type t exists
     int regularize;            // integrator "regularize" (surfscatter.cpp:127-128)
     // piecewise-linear spectra (conductor eta / k): spectrum s spans [plOffsets[s], plOffsets[s+1])

@@ -1125,6 +1125,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
             }
         }
         if (last) continue;
+        if (mtype >= kMatCoatedDiffuseT) continue;  // layered: k_vlayered
         // ---- EvaluateMaterialAndBSDF (surfscatter.cpp:57-328) for this material type
         const VRaySamples rs = RaySamplesAt(S, st, slot, depth, mtype == 1);
         const float4 mp4 = S.matParams[mat];
@@ -1342,6 +1343,217 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
                 const float ru = ruIn(i);
                 out.ru[(size_t)i * NR + jn] = ru;
                 out.rl[(size_t)i * NR + jn] = ru / pdf;
+            }
+        }
+        StoreV3(out.ray, NR, jn, OffsetRayOrigin(si.p, si.pErr, si.n, wi));
+        StoreV3(out.ray + 3 * (size_t)NR, NR, jn, wi);
+        StoreV3(out.prev, NR, jn, si.p);
+        StoreV3(out.prev + 3 * (size_t)NR, NR, jn, si.pErr);
+        StoreV3(out.prev + 6 * (size_t)NR, NR, jn, si.n);
+        StoreV3(out.prev + 9 * (size_t)NR, NR, jn, si.ns);
+        out.lambda0[jn] = lambda0;
+        out.etaScale[jn] = etaScale;
+        out.flags[jn] = (specular ? 1 : 0) | ((!specular || (flags & 2)) ? 2 : 0) | (nbUni ? kUniBeta : 0) |
+                        (ruUni ? kUniRu | kUniRl : 0);
+        out.pixel[jn] = slot;
+        out.depth[jn] = depth + 1;
+        out.medium[jn] = DotN(si.n, wi) > 0 ? mOut : mIn;
+    }
+}
+
+// ---------------------------------------------------------------- layered materials
+// The per-wavelength parameters of a coated material at a hit (CoatedDiffuseMaterial::GetBxDF /
+// CoatedConductorMaterial::GetBxDF, materials.cpp:301-329, :391-437), evaluated once per hit:
+// a = diffuse R (clamped) or conductor eta / interface eta, b = conductor k / interface eta,
+// alb = layer albedo (clamped)
+struct LayerSpec {
+    float a[kNS], b[kNS], alb[kNS];
+    __device__ float R(int i) const { return a[i]; }
+    __device__ void EtaK(int i, float *e, float *k) const {
+        *e = a[i];
+        *k = b[i];
+    }
+    __device__ float Albedo(int i) const { return alb[i]; }
+};
+
+// EvaluateMaterialAndBSDF<CoatedDiffuseBxDF | CoatedConductorBxDF> (surfscatter.cpp:57-328):
+// surface hits on layered materials (k_vsurface handles escapes, interfaces and emission of
+// the same queue and skips these).  The LayeredBxDF estimates f, Sample_f and PDF by random
+// walks (core.h LayeredBxDF); BSDF samples are pdfIsProportional, so r_l = r_u / PDF(wo, wi).
+__global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st, VolState v, int wf) {
+    const QueueView surf = LoadQueue(st, wf, kVSurf);
+    const int NR = st.NR;
+    const VolRecords &rec = v.rec[wf & 1], &out = v.rec[(wf + 1) & 1];
+    const int shard = ProducerShard();
+    const int shardBase = shard * st.capS;
+    int *nextCnt = &st.counters[CounterIndex(wf + 1, kVRay, shard)];
+    int *shadowCnt = &st.counters[CounterIndex(wf, kVShadow, shard)];
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < surf.total; j += gridDim.x * blockDim.x) {
+        const int ri = v.surfQ[QueueSlot(surf, j)];
+        const int prim = v.hitPrim[ri];
+        if (prim < 0) continue;
+        const int mat = S.primMaterial[prim];
+        const int mtype = S.matType[mat];
+        if (mtype < kMatCoatedDiffuseT) continue;
+        const float lambda0 = rec.lambda0[ri];
+        const int slot = rec.pixel[ri];
+        const int depth = rec.depth[ri], flags = rec.flags[ri], medium = rec.medium[ri];
+        const bool betaUni = flags & kUniBeta, ruUni = flags & kUniRu;
+        const SpecIn betaIn(rec.beta, NR, ri, betaUni), ruIn(rec.ru, NR, ri, ruUni);
+        const V3 rd = LoadV3(rec.ray + 3 * (size_t)NR, NR, ri);
+        const float b0 = v.hitB[ri], b1 = v.hitB[NR + ri], b2 = v.hitB[2 * NR + ri];
+        V3 p0, p1, p2;
+        PrimVerts(S, prim, &p0, &p1, &p2);
+        const TriSurface si = SurfaceAt(S, prim, p0, p1, p2, b0, b1, b2);
+        const V3 wo3 = Normalize(-rd);
+        int mIn, mOut;
+        MediaOf(S, prim, medium, &mIn, &mOut);
+        const VRaySamples rs = RaySamplesAt(S, st, slot, depth, true);
+        // ---- GetBxDF
+        const float4 mp4 = S.matParams[mat], mc = S.matCoeffs[mat];
+        const bool constant = S.matConstant[mat];
+        const float4 L0 = S.matLayer[3 * mat], L1 = S.matLayer[3 * mat + 1], L2 = S.matLayer[3 * mat + 2];
+        const bool conductor = mtype == kMatCoatedConductorT;
+        const float ieta = mp4.z;
+        const int etaSpec = conductor ? S.matSpectra[2 * mat] : -1;
+        const int kSpec = conductor ? S.matSpectra[2 * mat + 1] : -1;
+        LayerSpec sp;
+        bool bottomNz = false, albNz = false;
+        {
+            SpectralIter it(lambda0);
+#pragma unroll 1
+            for (int i = 0; i < kNS; ++i, it.Next()) {
+                if (!conductor) {
+                    sp.a[i] = Reflectance(mc, constant, it.lam);
+                    bottomNz |= sp.a[i] != 0;
+                } else {
+                    float e, k;
+                    if (etaSpec >= 0) {
+                        const int a = S.plOffsets[etaSpec], na = S.plOffsets[etaSpec + 1] - a;
+                        const int b = S.plOffsets[kSpec], nb = S.plOffsets[kSpec + 1] - b;
+                        e = PiecewiseLinearEval(S.plLambda + a, S.plValue + a, na, it.lam);
+                        k = PiecewiseLinearEval(S.plLambda + b, S.plValue + b, nb, it.lam);
+                    } else {
+                        const float r = Clampf(SigmoidPolynomial(mc.x, mc.y, mc.z, it.lam), 0, .9999f);
+                        e = 1.f;
+                        k = 2 * std::sqrt(r) / std::sqrt(std::fmax(0.f, 1 - r));
+                    }
+                    sp.a[i] = e / ieta;
+                    sp.b[i] = k / ieta;
+                }
+                sp.alb[i] = Reflectance(L1, L2.x != 0, it.lam);
+                albNz |= sp.alb[i] != 0;
+            }
+        }
+        TrowbridgeReitz trTop{mp4.x, mp4.y}, trBot{L2.y, L2.z};
+        if (S.regularize && (flags & 2)) {  // surfscatter.cpp:127-128, LayeredBxDF::Regularize
+            trTop.Regularize();
+            trBot.Regularize();
+        }
+        const LayeredBxDF<LayerSpec> L{ieta,         trTop, trBot, conductor, fmaxf(L0.x, 1.17549435e-38f),
+                                       Clampf(L0.y, -1, 1), albNz, (int)L0.z,  (int)L0.w, 0, sp, bottomNz};
+        const int bflags = L.LayerFlags();
+        const Frame frame = Frame::FromXZ(Normalize(si.dpdus), si.ns);
+        const V3 woL = frame.ToLocal(wo3);
+        float fo[kNS];
+        // ---- light sampling + shadow ray (surfscatter.cpp:252-326): reflective, not transmissive
+        if (bflags & (kBxDiffuse | kBxGlossy)) {
+            const V3 cp = OffsetRayOrigin(si.p, si.pErr, si.n, wo3);
+            AreaLightHit ls;
+            if (SampleAreaLightAt(S, cp, si.n, si.ns, rs.dUc, rs.dU0, rs.dU1, lambda0, &ls) && woL.z != 0) {
+                const V3 wi = Normalize(ls.p - cp);
+                const V3 wiL = frame.ToLocal(wi);
+                L.f(woL, wiL, true, fo);
+                bool fnz = false;
+#pragma unroll 1
+                for (int i = 0; i < kNS; ++i) fnz |= fo[i] != 0;
+                if (fnz) {
+                    const float bsdfPDF = L.PDF(woL, wiL, true);
+                    const float absdot = AbsDotN(si.ns, wi);
+                    const V3 so = OffsetRayOrigin(si.p, si.pErr, si.n, ls.p - si.p);
+                    const V3 pt = OffsetRayOrigin(ls.p, ls.pErr, ls.n, so - ls.p);
+                    const V3 sd = pt - so;
+                    bool ldUni = true;
+                    SpectralIter it(lambda0);
+#pragma unroll 1
+                    for (int i = 0; i < kNS; ++i, it.Next()) {
+                        const float Le = ls.scale * DenseAt(S, ls.spectrum, DenseOffset(it.lam));
+                        fo[i] = betaIn(i) * fo[i] * absdot * Le;
+                        ldUni &= FloatToBits(fo[i]) == FloatToBits(fo[0]);
+                    }
+                    const int js = shardBase + WavePush(shadowCnt, true);
+                    v.shLd[js] = fo[0];
+#pragma unroll 1
+                    for (int i = 1; i < kNS; ++i)
+                        if (!ldUni) v.shLd[(size_t)i * NR + js] = fo[i];
+                    v.shRu[js] = ruIn.v0 * bsdfPDF;
+                    v.shRl[js] = ruIn.v0 * ls.pdf;
+                    if (!ruUni) {
+#pragma unroll 1
+                        for (int i = 1; i < kNS; ++i) {
+                            const float ru = ruIn(i);
+                            v.shRu[(size_t)i * NR + js] = ru * bsdfPDF;
+                            v.shRl[(size_t)i * NR + js] = ru * ls.pdf;
+                        }
+                    }
+                    v.shFlags[js] = (ldUni ? kShUniLd : 0) | (ruUni ? kShUniRu | kShUniRl : 0);
+                    StoreV3(v.shRay, NR, js, so);
+                    StoreV3(v.shRay + 3 * (size_t)NR, NR, js, sd);
+                    v.shLambda0[js] = lambda0;
+                    v.shPixel[js] = slot;
+                    v.shMedium[js] = DotN(si.n, sd) > 0 ? mOut : mIn;
+                }
+            }
+        }
+        // ---- BSDF::Sample_f + RR + indirect ray (surfscatter.cpp:170-250)
+        if (woL.z == 0) continue;
+        const LayerSample bs = L.Sample_f(woL, rs.iUc, rs.iU0, rs.iU1, true, fo);
+        if (!bs.ok || bs.pdf == 0 || bs.wi.z == 0) continue;
+        bool fAny = false;
+#pragma unroll 1
+        for (int i = 0; i < kNS; ++i) fAny |= fo[i] != 0;
+        if (!fAny) continue;
+        const V3 wi = frame.FromLocal(bs.wi);
+        const float absdot = AbsDotN(si.ns, wi);
+        // BSDF::PDF(wo, wi) takes wi back to the local frame (bsdf.h:118-125)
+        const float pdfP = L.PDF(woL, frame.ToLocal(wi), true);
+        const float etaScale = rec.etaScale[ri];  // the layered sample's eta is 1
+        float rus = 0;
+#pragma unroll 1
+        for (int i = 0; i < kNS; ++i) rus = i == 0 ? ruIn.v0 : rus + ruIn(i);
+        const float avgRu = rus / kNS;
+        float mx = -kInfinity;
+#pragma unroll 1
+        for (int i = 0; i < kNS; ++i) {
+            fo[i] = betaIn(i) * fo[i] * absdot / bs.pdf;
+            mx = fmaxf(mx, fo[i] * etaScale / avgRu);
+        }
+        const bool rrOn = mx < 1 && depth >= 1;
+        float q = 0;
+        if (rrOn) {
+            q = fmaxf(0.f, 1 - mx);
+            if (rs.rr < q) continue;
+        }
+        bool nz = false, nbUni = true;
+#pragma unroll 1
+        for (int i = 0; i < kNS; ++i) {
+            if (rrOn) fo[i] /= 1 - q;
+            nz |= fo[i] != 0;
+            nbUni &= FloatToBits(fo[i]) == FloatToBits(fo[0]);
+        }
+        if (!nz) continue;
+        const bool specular = bs.flags & kBxSpecular;
+        const int jn = shardBase + WavePush(nextCnt, true);
+        out.beta[jn] = fo[0];
+        out.ru[jn] = ruIn.v0;
+        out.rl[jn] = ruIn.v0 / pdfP;
+#pragma unroll 1
+        for (int i = 1; i < kNS; ++i) {
+            if (!nbUni) out.beta[(size_t)i * NR + jn] = fo[i];
+            if (!ruUni) {
+                const float ru = ruIn(i);
+                out.ru[(size_t)i * NR + jn] = ru;
+                out.rl[(size_t)i * NR + jn] = ru / pdfP;
             }
         }
         StoreV3(out.ray, NR, jn, OffsetRayOrigin(si.p, si.pErr, si.n, wi));
@@ -1683,6 +1895,8 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
     else hipLaunchKernelGGL(k_vmedium, gW, block, 0, s, S, st, v, wf);
     hipLaunchKernelGGL(k_vsurface, gW, block, VolTablesLdsBytes(S) + kNS * kBlock * sizeof(float), s, S, st, v, wf);
     if (wf == S.maxDepth) return hipGetLastError();
+    if (S.matTypeMask & ((1 << kMatCoatedDiffuseT) | (1 << kMatCoatedConductorT)))
+        hipLaunchKernelGGL(k_vlayered, gW, block, 0, s, S, st, v, wf);
     hipLaunchKernelGGL(k_vscatter, gW, block, 0, s, S, st, v, wf);
     if (S.media.allGrey) {
         if (S.compressed) hipLaunchKernelGGL(k_vshadow_grey<true>, gT, block, VolStackBytes(S), s, S, st, v, wf);

@@ -74,6 +74,7 @@ class SceneFlat(ctypes.Structure):
         ("medium_info", ctypes.POINTER(ctypes.c_int32)), ("medium_params", ctypes.POINTER(ctypes.c_float)),
         ("medium_values", ctypes.POINTER(ctypes.c_float)), ("tri_medium", ctypes.POINTER(ctypes.c_int16)),
         ("filter_type", ctypes.c_int), ("filter_a", ctypes.c_float), ("filter_b", ctypes.c_float),
+        ("material_layer", ctypes.POINTER(ctypes.c_float)),
     ]
 
 
@@ -97,7 +98,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_film_clear", "pbrt_film_device_ptr", "pbrt_film_read", "pbrt_film_get_rgb", "pbrt_intersect",
     "pbrt_debug_halton", "pbrt_debug_rgb_coeffs", "pbrt_debug_rgb2spec_column", "pbrt_debug_kernel_sections",
     "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
-    "pbrt_debug_named_spectrum", "pbrt_debug_bxdf", "pbrt_debug_triangle_shading", "pbrt_film_write_image",
+    "pbrt_debug_named_spectrum", "pbrt_debug_bxdf", "pbrt_debug_layered", "pbrt_debug_triangle_shading", "pbrt_film_write_image",
     "pbrt_image_read_size", "pbrt_image_read", "pbrt_image_write", "pbrt_image_error", "pbrt_debug_filter_sample",
 ]
 
@@ -149,6 +150,7 @@ def _lib():
     lib.pbrt_debug_fresnel.argtypes = [c.c_void_p, c.c_void_p]
     lib.pbrt_debug_named_spectrum.argtypes = [c.c_char_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_debug_bxdf.argtypes = [c.c_int] + [c.c_void_p] * 7
+    lib.pbrt_debug_layered.argtypes = [c.c_void_p] * 8
     lib.pbrt_debug_triangle_shading.argtypes = [c.c_void_p] * 3 + [c.c_int] + [c.c_void_p] * 3
     lib.pbrt_set_data_dir(str(DATA_DIR).encode())
     _LIB = lib
@@ -203,6 +205,15 @@ def debug_bxdf(bxdf_type, params3, wo, wi, u3, eta31=None, k31=None):
     o = np.zeros(70, np.float32)
     _check(_lib().pbrt_debug_bxdf(int(bxdf_type), p.ctypes.data, e.ctypes.data, k.ctypes.data, a.ctypes.data,
                                   b.ctypes.data, u.ctypes.data, o.ctypes.data))
+    return o
+
+
+def debug_layered(params12, a31, b31, alb31, wo, wi, u3):
+    """Sample_f / f / PDF / Flags of a LayeredBxDF (coated diffuse or conductor): 72 floats
+    (pbrt_amd.h pbrt_debug_layered)."""
+    arrs = [_f32(params12, 12), _f32(a31, 31), _f32(b31, 31), _f32(alb31, 31), _f32(wo, 3), _f32(wi, 3), _f32(u3, 3)]
+    o = np.zeros(72, np.float32)
+    _check(_lib().pbrt_debug_layered(*[a.ctypes.data for a in arrs], o.ctypes.data))
     return o
 
 

@@ -1,0 +1,43 @@
+"""GPU parity of the layered materials (k_vlayered in pbrt-v4_amd/csrc/kernels/volpath.hip over
+core.h's LayeredBxDF) against the oracle's independent restatement (oracle/oracle.cpp
+LayeredBxDF).  The walks' RNGs hash direction bits, so, as for media, both sides evaluate
+transcendentals correctly rounded (oracle CR mode).  Known answers of test_layered.py are
+repeated on the GPU image.  Tolerances as test_gpu_media.py."""
+import numpy as np
+import pytest
+
+from conftest import SCENES
+from test_gpu_media import check, gpu_rgb, oracle_rgb
+from test_layered import layered_scene, showcase_scene
+
+pytestmark = pytest.mark.gpu
+
+
+def test_showcase_matches_oracle(pa, oracle):
+    sc = pa.Scene.from_string(showcase_scene(res=48, spp=8), SCENES)
+    a, _ = gpu_rgb(pa, oracle, sc)
+    frac, mr = check(a, oracle_rgb(oracle, sc))
+    print(f"layered showcase: {frac*100:.2f}% pixels within 1e-3, mean rel {mr:.2e}")
+
+
+@pytest.mark.parametrize("material", [
+    'Material "coateddiffuse" "rgb reflectance" [0.6 0.4 0.2] "float roughness" 0.3 "integer nsamples" 2',
+    'Material "coatedconductor" "float interface.roughness" 0.2 "float conductor.roughness" 0.1 '
+    '"rgb albedo" [0.5 0.5 0.5] "float thickness" 0.1',
+])
+def test_quad_matches_oracle(pa, oracle, material):
+    from test_layered import LIGHT
+    sc = pa.Scene.from_string(layered_scene(material, res=32, spp=16, sky="0.4 0.5 0.6", extra=LIGHT), SCENES)
+    a, _ = gpu_rgb(pa, oracle, sc)
+    check(a, oracle_rgb(oracle, sc))
+
+
+def test_known_answers_gpu(pa, oracle):
+    black = pa.Scene.from_string(layered_scene('Material "coateddiffuse" "float reflectance" 0', spp=64), SCENES)
+    img, _ = gpu_rgb(pa, oracle, black)
+    assert img.mean() == pytest.approx(0.0401, rel=0.06), img.mean()
+    white = pa.Scene.from_string(layered_scene(
+        'Material "coateddiffuse" "float reflectance" 1 "float thickness" 0.0001 "integer maxdepth" 100', spp=32),
+        SCENES)
+    img, _ = gpu_rgb(pa, oracle, white)
+    assert img.mean() == pytest.approx(1.0, rel=0.01), img.mean()

@@ -2466,6 +2466,18 @@ struct Renderer {
                 bx.mf.ax = mp[0];  // alphas arrive remapped and clamped (TrowbridgeReitz ctor)
                 bx.mf.ay = mp[1];
                 bx.eta = mp[2] == 0 ? 1.f : mp[2];
+                if (bx.type == 1 && f->material_spectra[2 * mat] >= 0) {
+                    // DielectricMaterial::GetBxDF (materials.cpp:25-49): a spectral eta is taken at
+                    // lambda_0 and the secondary wavelengths are terminated
+                    // (SampledWavelengths::TerminateSecondary: pdf = (pdf_0 / n, 0, ..., 0))
+                    const int es = f->material_spectra[2 * mat], a = f->pl_offsets[es];
+                    Float e = PLEval(f->pl_lambda + a, f->pl_value + a, f->pl_offsets[es + 1] - a, lambda.lambda[0]);
+                    bx.eta = e == 0 ? 1.f : e;
+                    if (lambda.pdf[1] != 0) {
+                        for (int i = 1; i < NS; ++i) lambda.pdf[i] = 0;
+                        lambda.pdf[0] /= NS;
+                    }
+                }
                 if (bx.type == 2) {
                     int es = f->material_spectra[2 * mat], ks = f->material_spectra[2 * mat + 1];
                     for (int i = 0; i < NS; ++i) {

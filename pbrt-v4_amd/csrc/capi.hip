@@ -188,7 +188,8 @@ struct pbrt_context {
     DevBuf<float> triVerts, matCoeffs, lightScale, lightArea, infScale, dense, sensor;
     DevBuf<int> primMaterial, primLight, matConstant, lightPrim, lightSpectrum, lightTwoSided, infSpectrum;
     DevBuf<int> primOrig, matType, matSpectra, plOffsets;
-    DevBuf<float> matParams, plLambda, plValue, triShade, matLayer;
+    DevBuf<float> matParams, plLambda, plValue, triShade, matLayer, dispL0;
+    DevBuf<int> dispTerm;
     DevBuf<uint8_t> primFlip;
     DevBuf<uint32_t> lightBitTrail, permOffset, permNDigits, permBase;
     DevBuf<uint16_t> perm;
@@ -451,6 +452,11 @@ static void BuildDevice(pbrt_context *c) {
                     std::any_of(s.materials.begin(), s.materials.end(), [](const MaterialDesc &m) {
                         return m.type == kMatInterface || m.type == kMatCoatedDiffuse || m.type == kMatCoatedConductor;
                     });
+    S.dispersive = std::any_of(s.materials.begin(), s.materials.end(),
+                               [](const MaterialDesc &m) { return m.type == kMatDielectric && m.etaSpec >= 0; });
+    if (S.dispersive && !s.media.empty())
+        throw std::runtime_error("a dielectric with spectral eta (dispersion) together with participating media is not supported yet");
+    c->volumetric = c->volumetric || S.dispersive;
     S.media.cameraMedium = s.cameraMedium;
     S.media.allGrey = 1;
     for (size_t m = 0; m < s.media.size(); ++m) {
@@ -623,6 +629,10 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
     // per pixel-sample arrays (L, filterW) use N; the rest NR (>= N)
     c->fState.Alloc((size_t)nf * NR);
     c->iState.Alloc((size_t)ni * NR + CounterIndex(c->desc.maxDepth + 3, 0, 0));
+    if (c->S.dispersive) {
+        c->dispL0.Alloc((size_t)3 * NR);
+        c->dispTerm.Alloc((size_t)NR);
+    }
     c->maxPaths = N;
     PathState &st = c->st;
     st.capS = (int)capS;
@@ -655,6 +665,8 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
     st.shadowRay = take(6);
     st.shadowL = take(3);
     st.L = take(3);
+    st.L0 = c->S.dispersive ? c->dispL0.p : nullptr;
+    st.lamTerm = c->S.dispersive ? c->dispTerm.p : nullptr;
     st.filterW = take(1);
     st.shadowPixel = takei(1);
     for (int t = 0; t < kNumMatTypes; ++t) st.matQ[t] = takei(1);

@@ -615,9 +615,10 @@ class Parser {
             if (Param *e = ps.Find("eta", "float")) {
                 if (e->nums.empty()) throw Error(ps.loc + ": \"float eta\" needs a value");
                 m.eta = (float)e->nums[0];
-            } else if (ps.Find("eta", "spectrum")) {
-                // a non-constant eta makes GetBxDF call SampledWavelengths::TerminateSecondary
-                throw Error(ps.loc + ": spectrally varying dielectric eta (dispersion) is not supported yet");
+            } else if (Param *es = ps.Find("eta", "spectrum")) {
+                // a non-constant eta: GetBxDF takes eta(lambda_0) and calls
+                // SampledWavelengths::TerminateSecondary (materials.cpp:25-49)
+                m.etaSpec = SpectrumParam(es, ps.loc);
             }
             Roughness(ps, &m);
         } else if (type == "conductor") {

@@ -111,6 +111,7 @@ struct DeviceScene {
                                // albedo constant, conductor alpha_x alpha_y, 0
     int matTypeMask;           // bit t: some material of type t exists
     int regularize;            // integrator "regularize" (surfscatter.cpp:127-128)
+    int dispersive;            // some dielectric has a spectral eta (matSpectra[2 * mat] >= 0)
     // piecewise-linear spectra (conductor eta / k): spectrum s spans [plOffsets[s], plOffsets[s+1])
     const int *plOffsets;
     const float *plLambda, *plValue;
@@ -206,6 +207,11 @@ struct PathState {
     int *shadowPixel;   // [NR]
     // per pixel-sample slot
     float *L;           // [3][N] sensor RGB
+    // dispersion (SampledWavelengths::TerminateSecondary): the lambda_0-only sensor RGB of the
+    // same contributions, and whether the path terminated its secondary wavelengths; null
+    // unless the scene has a dielectric with spectral eta
+    float *L0;          // [3][N]
+    int *lamTerm;       // [N]
     float *filterW;     // [N]
     // work queues: record indices of the current depth
     int *matQ[kNumMatTypes];  // [NR] each: hits per material type

@@ -360,6 +360,19 @@ __device__ __forceinline__ bool SampleTmajGrey(const DeviceScene &S, const Mediu
     return true;
 }
 
+// The lambda_0 share of a contribution, for paths that terminate their secondary wavelengths
+// (dispersion): ToSensorRGB with pdf = (pdf_0 / n, 0, ...) keeps x(lambda_0) c_0 / pdf_0
+// (SampledWavelengths::TerminateSecondary, spectrum.h; film.h:95-100)
+__device__ inline void AddL0Off(const DeviceScene &S, const PathState &st, int slot, int off0, float c0) {
+    if (!S.dispersive) return;
+    SensorAcc a;
+    a.Add(S, off0, c0, true);
+    const int NL = st.N;
+    st.L0[slot] += S.imagingRatio * a.sx;
+    st.L0[NL + slot] += S.imagingRatio * a.sy;
+    st.L0[2 * NL + slot] += S.imagingRatio * a.sz;
+}
+
 // Spectral contribution c_i (already divided by its MIS denominator) to sensor RGB
 // (PixelSensor::ToSensorRGB, film.h:95-100), added to the slot's L
 template <typename C>
@@ -371,6 +384,7 @@ __device__ inline void AddToL(const DeviceScene &S, const PathState &st, int slo
     st.L[slot] += S.imagingRatio * (acc.sx / kNS);
     st.L[NL + slot] += S.imagingRatio * (acc.sy / kNS);
     st.L[2 * NL + slot] += S.imagingRatio * (acc.sz / kNS);
+    AddL0Off(S, st, slot, wo.off[0], c(0));
 }
 
 // RaySamples of a path depth (samples.cpp:29-66) from the global sampler tables
@@ -497,6 +511,12 @@ __global__ void __launch_bounds__(kBlock) k_vcamera(DeviceScene S, PathState st,
     st.L[slot] = 0;
     st.L[N + slot] = 0;
     st.L[2 * N + slot] = 0;
+    if (S.dispersive) {
+        st.L0[slot] = 0;
+        st.L0[N + slot] = 0;
+        st.L0[2 * N + slot] = 0;
+        st.lamTerm[slot] = 0;
+    }
     if (!S.boxFilter) st.filterW[slot] = filterWeight;
     const VolRecords &r = v.rec[0];
     r.beta[slot] = 1.f;  // uniform spectra: entry 0 only (kUni* flags)
@@ -934,15 +954,19 @@ template <typename C>
 __device__ inline void AddSpecToL(const DeviceScene &S, const PathState &st, int slot, float lambda0, C &&c) {
     SensorAcc acc;
     SpectralIter it(lambda0);
+    float c0 = 0;
 #pragma unroll 4
     for (int i = 0; i < kNS; ++i, it.Next()) {
         const int off = DenseOffset(it.lam);
-        acc.Add(S, off, c(i, off), i == 0);
+        const float ci = c(i, off);
+        c0 = i == 0 ? ci : c0;
+        acc.Add(S, off, ci, i == 0);
     }
     const int NL = st.N;
     st.L[slot] += S.imagingRatio * (acc.sx / kNS);
     st.L[NL + slot] += S.imagingRatio * (acc.sy / kNS);
     st.L[2 * NL + slot] += S.imagingRatio * (acc.sz / kNS);
+    AddL0Off(S, st, slot, DenseOffset(lambda0), c0);
 }
 
 // An area-light sample for a reference point (BVHLightSampler::Sample, then
@@ -1133,7 +1157,15 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
         const bool constant = S.matConstant[mat];
         TrowbridgeReitz tr{mp4.x, mp4.y};
         if (mtype != 0 && S.regularize && (flags & 2)) tr.Regularize();  // surfscatter.cpp:127-128
-        const float eta = mp4.z == 0 ? 1.f : mp4.z;
+        float eta = mp4.z == 0 ? 1.f : mp4.z;
+        if (mtype == 1 && S.dispersive && S.matSpectra[2 * mat] >= 0) {
+            // DielectricMaterial::GetBxDF (materials.cpp:25-49): eta(lambda_0), then
+            // TerminateSecondary for a non-constant eta
+            const int es = S.matSpectra[2 * mat], a = S.plOffsets[es], na = S.plOffsets[es + 1] - a;
+            eta = PiecewiseLinearEval(S.plLambda + a, S.plValue + a, na, lambda0);
+            if (eta == 0) eta = 1;
+            st.lamTerm[slot] = 1;
+        }
         const int etaSpec = mtype == 2 ? S.matSpectra[2 * mat] : -1;
         const int kSpec = mtype == 2 ? S.matSpectra[2 * mat + 1] : -1;
         auto etaK = [&](float lam, float *e, float *k) {
@@ -1861,6 +1893,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_vshadow_grey(D
         st.L[slot] += S.imagingRatio * (acc.sx / kNS);
         st.L[NL + slot] += S.imagingRatio * (acc.sy / kNS);
         st.L[2 * NL + slot] += S.imagingRatio * (acc.sz / kNS);
+        AddL0Off(S, st, slot, DenseOffset(lambda0), ldIn(0) * Tr / avg);
     }
 }
 

@@ -870,7 +870,8 @@ __global__ void __launch_bounds__(kBlock) k_film(DeviceScene S, PathState st, in
     for (int s = 0; s < nSamples; ++s) {
         int slot = s * st.P + pl;
         float w = S.boxFilter ? 1.f : st.filterW[slot];
-        float rr = st.L[slot], gg = st.L[N + slot], bb = st.L[2 * N + slot];
+        const float *Ls = (st.lamTerm && st.lamTerm[slot]) ? st.L0 : st.L;  // terminated: lambda_0 only
+        float rr = Ls[slot], gg = Ls[N + slot], bb = Ls[2 * N + slot];
         sr += w * rr;
         sg += w * gg;
         sb += w * bb;

@@ -1,4 +1,4 @@
-"""GPU parity of the layered materials (k_vlayered in pbrt-v4_amd/csrc/kernels/volpath.hip over
+"""GPU parity of the layered materials and of dispersion (spectral dielectric eta) (k_vlayered in pbrt-v4_amd/csrc/kernels/volpath.hip over
 core.h's LayeredBxDF) against the oracle's independent restatement (oracle/oracle.cpp
 LayeredBxDF).  The walks' RNGs hash direction bits, so, as for media, both sides evaluate
 transcendentals correctly rounded (oracle CR mode).  Known answers of test_layered.py are
@@ -41,3 +41,19 @@ def test_known_answers_gpu(pa, oracle):
         SCENES)
     img, _ = gpu_rgb(pa, oracle, white)
     assert img.mean() == pytest.approx(1.0, rel=0.01), img.mean()
+
+
+@pytest.mark.parametrize("eta", ['"spectrum eta" "glass-BK7"', '"spectrum eta" [300 1.7 800 1.4] "float roughness" 0.2'])
+def test_dispersion_matches_oracle(pa, oracle, eta):
+    from test_dispersion import glass_scene
+    sc = pa.Scene.from_string(glass_scene(eta, res=32, spp=16), SCENES)
+    a, _ = gpu_rgb(pa, oracle, sc)
+    frac, mr = check(a, oracle_rgb(oracle, sc))
+    print(f"dispersion {eta}: {frac*100:.2f}% pixels within 1e-3, mean rel {mr:.2e}")
+
+
+def test_dispersion_with_media_refused(pa):
+    from test_dispersion import dispersive_medium_scene
+    sc = pa.Scene.from_string(dispersive_medium_scene(), SCENES)
+    with pytest.raises(RuntimeError, match="dispersion"):
+        pa.WavefrontPathIntegrator(sc, max_paths=1 << 12)

@@ -121,7 +121,8 @@ typedef struct pbrt_scene_flat {
      * material_params = interface alphas + eta, material_coeffs = diffuse or conductor
      * "reflectance", material_spectra = conductor.eta / .k; per material [12] floats:
      * thickness g maxdepth nsamples, albedo c0 c1 c2 value constant(1/0), conductor
-     * alpha_x alpha_y, 0 */
+     * alpha_x alpha_y, spectral interface eta (index into the piecewise-linear spectra, -1
+     * for the constant eta of material_params) */
     const float *material_layer;
 } pbrt_scene_flat;
 

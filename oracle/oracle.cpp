@@ -2417,7 +2417,16 @@ struct Renderer {
             if (layered) {
                 // CoatedDiffuseMaterial / CoatedConductorMaterial::GetBxDF (materials.cpp:301-329, :391-437)
                 const float *mp = f->material_params + 4 * mat, *ml = f->material_layer + 12 * mat;
-                const Float ieta = mp[2] == 0 ? 1.f : mp[2];
+                Float ieta = mp[2] == 0 ? 1.f : mp[2];
+                if (ml[11] >= 0) {  // spectral interface eta: eta(lambda_0) and TerminateSecondary
+                    const int es = (int)ml[11], a = f->pl_offsets[es];
+                    Float e = PLEval(f->pl_lambda + a, f->pl_value + a, f->pl_offsets[es + 1] - a, lambda.lambda[0]);
+                    ieta = e == 0 ? 1.f : e;
+                    if (lambda.pdf[1] != 0) {
+                        for (int i = 1; i < NS; ++i) lambda.pdf[i] = 0;
+                        lambda.pdf[0] /= NS;
+                    }
+                }
                 lay.top.type = 1;
                 lay.top.eta = ieta;
                 lay.top.mf.ax = mp[0];

@@ -106,7 +106,7 @@ struct pbrt_scene {
         matLayer.clear();
         for (auto &m : s.materials) {
             matLayer.insert(matLayer.end(), {m.thickness, m.g, (float)m.maxDepth, (float)m.nSamples, m.a0, m.a1, m.a2,
-                                             m.albedoValue, m.albedoConstant ? 1.f : 0.f, m.cAlphaX, m.cAlphaY, 0.f});
+                                             m.albedoValue, m.albedoConstant ? 1.f : 0.f, m.cAlphaX, m.cAlphaY, (float)m.ifaceEtaSpec});
             matCoeffs.insert(matCoeffs.end(), {m.c0, m.c1, m.c2, m.constantValue});
             matConstant.push_back(m.constant ? 1 : 0);
             matType.push_back(m.type);
@@ -317,7 +317,7 @@ static void BuildDevice(pbrt_context *c) {
             const bool grey = !m.albedoConstant && m.a0 == 0 && m.a1 == 0;
             const float av = grey ? SigmoidPolynomial(0.f, 0.f, m.a2, 500.f) : m.albedoValue;
             ml.insert(ml.end(), {m.thickness, m.g, (float)m.maxDepth, (float)m.nSamples, m.a0, m.a1, m.a2, av,
-                                 (m.albedoConstant || grey) ? 1.f : 0.f, m.cAlphaX, m.cAlphaY, 0.f});
+                                 (m.albedoConstant || grey) ? 1.f : 0.f, m.cAlphaX, m.cAlphaY, (float)m.ifaceEtaSpec});
         }
         c->matLayer.Upload(ml);
         c->matType.Upload(mt);
@@ -453,7 +453,7 @@ static void BuildDevice(pbrt_context *c) {
                         return m.type == kMatInterface || m.type == kMatCoatedDiffuse || m.type == kMatCoatedConductor;
                     });
     S.dispersive = std::any_of(s.materials.begin(), s.materials.end(),
-                               [](const MaterialDesc &m) { return m.type == kMatDielectric && m.etaSpec >= 0; });
+                               [](const MaterialDesc &m) { return (m.type == kMatDielectric && m.etaSpec >= 0) || m.ifaceEtaSpec >= 0; });
     if (S.dispersive && !s.media.empty())
         throw std::runtime_error("a dielectric with spectral eta (dispersion) together with participating media is not supported yet");
     c->volumetric = c->volumetric || S.dispersive;

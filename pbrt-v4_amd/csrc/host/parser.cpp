@@ -713,8 +713,8 @@ class Parser {
         if (Param *e = ps.Find(etaName, "float")) {
             if (e->nums.empty()) throw Error(ps.loc + ": \"float " + etaName + "\" needs a value");
             m->eta = (float)e->nums[0];
-        } else if (ps.Find(etaName, "spectrum")) {
-            throw Error(ps.loc + ": spectrally varying " + etaName + " (dispersion) is not supported yet");
+        } else if (Param *es = ps.Find(etaName, "spectrum")) {
+            m->ifaceEtaSpec = SpectrumParam(es, ps.loc);  // eta(lambda_0) + TerminateSecondary
         }
         if (m->eta == 0) m->eta = 1;
         m->thickness = ps.GetFloat("thickness", .01f);

@@ -74,6 +74,7 @@ struct MaterialDesc {
     bool albedoConstant = true;
     float albedoValue = 0, a0 = 0, a1 = 0, a2 = 0;  // layer albedo: constant or sigmoid
     float cAlphaX = 0, cAlphaY = 0;                 // conductor.{u,v}roughness -> alphas
+    int ifaceEtaSpec = -1;                          // spectral interface eta (dispersion)
     std::string name;
 };
 

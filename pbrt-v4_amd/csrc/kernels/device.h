@@ -108,7 +108,7 @@ struct DeviceScene {
     const float4 *matParams;   // alpha_x, alpha_y (TrowbridgeReitz), dielectric eta, 0
     const int *matSpectra;     // [nMaterials][2] conductor eta / k piecewise-linear spectra
     const float4 *matLayer;    // [nMaterials][3] layered: thickness g maxDepth nSamples | albedo c0..c2 value |
-                               // albedo constant, conductor alpha_x alpha_y, 0
+                               // albedo constant, conductor alpha_x alpha_y, interface eta spectrum (-1)
     int matTypeMask;           // bit t: some material of type t exists
     int regularize;            // integrator "regularize" (surfscatter.cpp:127-128)
     int dispersive;            // some dielectric has a spectral eta (matSpectra[2 * mat] >= 0)

@@ -1446,7 +1446,13 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
         const bool constant = S.matConstant[mat];
         const float4 L0 = S.matLayer[3 * mat], L1 = S.matLayer[3 * mat + 1], L2 = S.matLayer[3 * mat + 2];
         const bool conductor = mtype == kMatCoatedConductorT;
-        const float ieta = mp4.z;
+        float ieta = mp4.z;
+        if (L2.w >= 0) {  // spectral interface eta: eta(lambda_0), TerminateSecondary
+            const int es = (int)L2.w, a = S.plOffsets[es], na = S.plOffsets[es + 1] - a;
+            ieta = PiecewiseLinearEval(S.plLambda + a, S.plValue + a, na, lambda0);
+            if (ieta == 0) ieta = 1;
+            st.lamTerm[slot] = 1;
+        }
         const int etaSpec = conductor ? S.matSpectra[2 * mat] : -1;
         const int kSpec = conductor ? S.matSpectra[2 * mat + 1] : -1;
         LayerSpec sp;

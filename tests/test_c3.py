@@ -58,7 +58,6 @@ def test_conductor_defaults_and_named_spectra(pa):
 
 @pytest.mark.parametrize("mat,msg", [
     ('Material "conductor" "rgb reflectance" [0.9 0.6 0.3] "spectrum eta" "metal-Au-eta"', "can't be provided"),
-    ('Material "dielectric" "spectrum eta" "glass-BK7"', "dispersion"),
     ('Material "conductor" "spectrum eta" "metal-Xx-eta"', "unknown named spectrum"),
     ('Material "conductor" "spectrum eta" [400 1 500]', "odd number"),
     ('Material "dielectric" "texture roughness" "foo"', "not supported"),

@@ -43,10 +43,14 @@ def test_known_answers_gpu(pa, oracle):
     assert img.mean() == pytest.approx(1.0, rel=0.01), img.mean()
 
 
-@pytest.mark.parametrize("eta", ['"spectrum eta" "glass-BK7"', '"spectrum eta" [300 1.7 800 1.4] "float roughness" 0.2'])
+@pytest.mark.parametrize("eta", ['"spectrum eta" "glass-BK7"', '"spectrum eta" [300 1.7 800 1.4] "float roughness" 0.2',
+                                 'coated'])
 def test_dispersion_matches_oracle(pa, oracle, eta):
     from test_dispersion import glass_scene
-    sc = pa.Scene.from_string(glass_scene(eta, res=32, spp=16), SCENES)
+    text = glass_scene(eta, res=32, spp=16) if eta != 'coated' else glass_scene(res=32, spp=16).replace(
+        'Material "dielectric" "spectrum eta" "glass-BK7"',
+        'Material "coateddiffuse" "spectrum eta" "glass-F11" "rgb reflectance" [0.3 0.5 0.7] "float roughness" 0.1')
+    sc = pa.Scene.from_string(text, SCENES)
     a, _ = gpu_rgb(pa, oracle, sc)
     frac, mr = check(a, oracle_rgb(oracle, sc))
     print(f"dispersion {eta}: {frac*100:.2f}% pixels within 1e-3, mean rel {mr:.2e}")

@@ -134,7 +134,6 @@ def test_coatedconductor_parameters(pa):
 @pytest.mark.parametrize("mat,msg", [
     ('Material "coatedconductor" "rgb reflectance" [0.9 0.6 0.3] "spectrum conductor.eta" "metal-Au-eta"',
      "can't be provided"),
-    ('Material "coateddiffuse" "spectrum eta" "glass-BK7"', "dispersion"),
     ('Material "coateddiffuse" "rgb reflectance" [1.2 0.5 0.5]', "[0,1]"),
     ('Material "coateddiffuse" "float bogus" 1', "bogus"),
 ])

@@ -1257,6 +1257,7 @@ struct BxDF {
 
     int Flags() const {
         if (type == 0) return R ? (BxR | BxDiffuse) : 0;
+        if (type == 6) return BxR | BxT | BxSpecular;  // ThinDielectricBxDF
         int lobe = mf.Smooth() ? BxSpecular : BxGlossy;
         if (type == 1) return (eta == 1 ? BxT : (BxR | BxT)) | lobe;
         return BxR | lobe;
@@ -1267,6 +1268,24 @@ struct BxDF {
         return r;
     }
     bool Sample_f(Vec wo, Float uc, Float u0, Float u1, BSDFSample *bs, bool radiance = true, int sf = 3) const {
+        if (type == 6) {
+            // ThinDielectricBxDF::Sample_f (bxdfs.h:355-386)
+            Float R_ = FrDielectric(std::abs(wo.z), eta), T_ = 1 - R_;
+            if (R_ < 1) {
+                R_ += Sqr(T_) * R_ / (1 - Sqr(R_));
+                T_ = 1 - R_;
+            }
+            Float pr = (sf & 1) ? R_ : 0, pt = (sf & 2) ? T_ : 0;
+            if (pr == 0 && pt == 0) return false;
+            if (uc < pr / (pr + pt)) {
+                Vec wi(-wo.x, -wo.y, wo.z);
+                *bs = BSDFSample{Spectrum(R_ / std::abs(wi.z)), wi, pr / (pr + pt), BxR | BxSpecular, 1};
+            } else {
+                Vec wi = -wo;
+                *bs = BSDFSample{Spectrum(T_ / std::abs(wi.z)), wi, pt / (pr + pt), BxT | BxSpecular, 1};
+            }
+            return true;
+        }
         if (type != 1 && !(sf & 1)) return false;
         if (type == 0) {
             Vec wi = SampleCosineHemisphere(u0, u1);
@@ -1347,6 +1366,7 @@ struct BxDF {
         return true;
     }
     Spectrum f(Vec wo, Vec wi, bool radiance = true) const {
+        if (type == 6) return Spectrum(0.f);
         if (type == 0) return SameHemisphere(wo, wi) ? R * InvPi : Spectrum(0.f);
         if (type == 2) {
             if (!SameHemisphere(wo, wi) || mf.Smooth()) return Spectrum(0.f);
@@ -1371,6 +1391,7 @@ struct BxDF {
         return Spectrum(ft);
     }
     Float PDF(Vec wo, Vec wi, int sf = 3) const {
+        if (type == 6) return 0;
         if (type != 1 && !(sf & 1)) return 0;
         if (type == 0) return SameHemisphere(wo, wi) ? std::abs(wi.z) * InvPi : 0;
         if (type == 2) {
@@ -2475,7 +2496,7 @@ struct Renderer {
                 bx.mf.ax = mp[0];  // alphas arrive remapped and clamped (TrowbridgeReitz ctor)
                 bx.mf.ay = mp[1];
                 bx.eta = mp[2] == 0 ? 1.f : mp[2];
-                if (bx.type == 1 && f->material_spectra[2 * mat] >= 0) {
+                if ((bx.type == 1 || bx.type == 6) && f->material_spectra[2 * mat] >= 0) {
                     // DielectricMaterial::GetBxDF (materials.cpp:25-49): a spectral eta is taken at
                     // lambda_0 and the secondary wavelengths are terminated
                     // (SampledWavelengths::TerminateSecondary: pdf = (pdf_0 / n, 0, ..., 0))
@@ -2502,7 +2523,7 @@ struct Renderer {
                         }
                     }
                 }
-                if (f->regularize && anyNonSpecular) bx.mf.Regularize();
+                if (f->regularize && anyNonSpecular && bx.type != 6) bx.mf.Regularize();  // thin: no-op
             }
             Vec fx_ = Normalize(si.dpdus), fz = si.ns, fy_ = Cross(fz, fx_);
             auto toLocal = [&](Vec v) { return Vec(Dot(v, fx_), Dot(v, fy_), Dot(v, fz)); };

@@ -450,10 +450,12 @@ static void BuildDevice(pbrt_context *c) {
     S.media.n = (int)s.media.size();
     c->volumetric = !s.media.empty() ||
                     std::any_of(s.materials.begin(), s.materials.end(), [](const MaterialDesc &m) {
-                        return m.type == kMatInterface || m.type == kMatCoatedDiffuse || m.type == kMatCoatedConductor;
+                        return m.type == kMatInterface || m.type == kMatCoatedDiffuse || m.type == kMatCoatedConductor ||
+                               m.type == kMatThinDielectric;
                     });
     S.dispersive = std::any_of(s.materials.begin(), s.materials.end(),
-                               [](const MaterialDesc &m) { return (m.type == kMatDielectric && m.etaSpec >= 0) || m.ifaceEtaSpec >= 0; });
+                               [](const MaterialDesc &m) { return ((m.type == kMatDielectric || m.type == kMatThinDielectric) && m.etaSpec >= 0) || m.ifaceEtaSpec >= 0;
+                               });
     if (S.dispersive && !s.media.empty())
         throw std::runtime_error("a dielectric with spectral eta (dispersion) together with participating media is not supported yet");
     c->volumetric = c->volumetric || S.dispersive;

@@ -954,6 +954,23 @@ PHD BxSample DielectricSample(float eta, const TrowbridgeReitz &tr, V3 wo, float
     s = BxSample{true, wi, ft, pdf, etap, kBxGlossy | kBxTransmission};
     return s;
 }
+// ThinDielectricBxDF::Sample_f (bxdfs.h:355-386): specular reflection / straight-through
+// transmission with the inter-reflections of a thin slab folded into R and T
+PHD BxSample ThinDielectricSample(float eta, V3 wo, float uc) {
+    float R = FrDielectric(AbsCosTheta(wo), eta), T = 1 - R;
+    if (R < 1) {
+        R += Sqr(T) * R / (1 - Sqr(R));
+        T = 1 - R;
+    }
+    const float pr = R, pt = T;
+    if (pr == 0 && pt == 0) return BxSample{false, V3(0, 0, 0), 0, 0, 1, 0};
+    if (uc < pr / (pr + pt)) {
+        const V3 wi(-wo.x, -wo.y, wo.z);
+        return BxSample{true, wi, R / AbsCosTheta(wi), pr / (pr + pt), 1, kBxSpecular | kBxReflection};
+    }
+    const V3 wi = -wo;
+    return BxSample{true, wi, T / AbsCosTheta(wi), pt / (pr + pt), 1, kBxSpecular | kBxTransmission};
+}
 // DielectricBxDF::f and ::PDF (bxdfs.cpp:172-245); pdfOut may be null
 PHD float DielectricEval(float eta, const TrowbridgeReitz &tr, V3 wo, V3 wi, float *pdfOut, bool radiance = true,
                          int sampleFlags = kSampleAll) {

@@ -621,6 +621,15 @@ class Parser {
                 m.etaSpec = SpectrumParam(es, ps.loc);
             }
             Roughness(ps, &m);
+        } else if (type == "thindielectric") {
+            // ThinDielectricMaterial::Create (materials.cpp:83-97): eta only, always specular
+            m.type = kMatThinDielectric;
+            if (Param *e = ps.Find("eta", "float")) {
+                if (e->nums.empty()) throw Error(ps.loc + ": \"float eta\" needs a value");
+                m.eta = (float)e->nums[0];
+            } else if (Param *es = ps.Find("eta", "spectrum")) {
+                m.etaSpec = SpectrumParam(es, ps.loc);  // eta(lambda_0) + TerminateSecondary
+            }
         } else if (type == "conductor") {
             // ConductorMaterial::Create (materials.cpp:217-251)
             m.type = kMatConductor;

@@ -35,6 +35,7 @@ constexpr int kMatInterface = 3;
 // LayeredBxDF materials (bxdfs.h:565-1052, materials.cpp:301-540); shaded by the volumetric
 // kernels' layered stage
 constexpr int kMatCoatedDiffuse = 4, kMatCoatedConductor = 5;
+constexpr int kMatThinDielectric = 6;  // ThinDielectricBxDF (bxdfs.h:342-404), volumetric kernels
 
 // Participating media (media.h:209-350, media.cpp:167-330).  Spectra are DenselySampled
 // 395..705 nm tables in SceneDesc::denseSpectra with pbrt's constructor scaling applied

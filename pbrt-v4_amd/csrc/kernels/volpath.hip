@@ -1151,14 +1151,15 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
         if (last) continue;
         if (mtype >= kMatCoatedDiffuseT) continue;  // layered: k_vlayered
         // ---- EvaluateMaterialAndBSDF (surfscatter.cpp:57-328) for this material type
-        const VRaySamples rs = RaySamplesAt(S, st, slot, depth, mtype == 1);
+        const VRaySamples rs = RaySamplesAt(S, st, slot, depth, mtype == 1 || mtype == kMatThinDielectricT);
         const float4 mp4 = S.matParams[mat];
         const float4 mc = S.matCoeffs[mat];
         const bool constant = S.matConstant[mat];
         TrowbridgeReitz tr{mp4.x, mp4.y};
-        if (mtype != 0 && S.regularize && (flags & 2)) tr.Regularize();  // surfscatter.cpp:127-128
+        // surfscatter.cpp:127-128 (ThinDielectricBxDF::Regularize does nothing)
+        if (mtype != 0 && mtype != kMatThinDielectricT && S.regularize && (flags & 2)) tr.Regularize();
         float eta = mp4.z == 0 ? 1.f : mp4.z;
-        if (mtype == 1 && S.dispersive && S.matSpectra[2 * mat] >= 0) {
+        if ((mtype == 1 || mtype == kMatThinDielectricT) && S.dispersive && S.matSpectra[2 * mat] >= 0) {
             // DielectricMaterial::GetBxDF (materials.cpp:25-49): eta(lambda_0), then
             // TerminateSecondary for a non-constant eta
             const int es = S.matSpectra[2 * mat], a = S.plOffsets[es], na = S.plOffsets[es + 1] - a;
@@ -1187,7 +1188,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
             if (mtype == 0) return 0.4f * kInvPi;
 #endif
             if (mtype == 0) return Reflectance(mc, constant, lam) * kInvPi;
-            if (mtype == 1) return fd;
+            if (mtype == 1 || mtype == kMatThinDielectricT) return fd;
             float e, k;
             etaK(lam, &e, &k);
             return ConductorF(ct, e, k);
@@ -1207,7 +1208,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
         if (!hasFlags) continue;
         const bool smooth = mtype != 0 && tr.EffectivelySmooth();
         const bool reflective = mtype != 1 || eta != 1;
-        const bool transmissive = mtype == 1;
+        const bool transmissive = mtype == 1 || mtype == kMatThinDielectricT;
         const Frame frame = Frame::FromXZ(Normalize(si.dpdus), si.ns);
         const V3 woL = frame.ToLocal(wo3);
         // ---- light sampling + shadow ray (surfscatter.cpp:252-326), IsNonSpecular(flags)
@@ -1317,6 +1318,14 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
             fd = bs.f;
             etap = bs.etap;
             specular = bs.flags & kBxSpecular;
+            transmission = bs.flags & kBxTransmission;
+        } else if (mtype == kMatThinDielectricT) {
+            const BxSample bs = ThinDielectricSample(eta, woL, rs.iUc);
+            ok = bs.ok && bs.f != 0;
+            wiL = bs.wi;
+            pdf = bs.pdf;
+            fd = bs.f;
+            specular = true;
             transmission = bs.flags & kBxTransmission;
         } else {
             ct = ConductorSample(tr, woL, rs.iU0, rs.iU1);

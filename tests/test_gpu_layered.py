@@ -61,3 +61,12 @@ def test_dispersion_with_media_refused(pa):
     sc = pa.Scene.from_string(dispersive_medium_scene(), SCENES)
     with pytest.raises(RuntimeError, match="dispersion"):
         pa.WavefrontPathIntegrator(sc, max_paths=1 << 12)
+
+
+@pytest.mark.parametrize("eta", ['"float eta" 1.6', '"spectrum eta" "glass-BAF10"'])
+def test_thin_dielectric_matches_oracle(pa, oracle, eta):
+    from test_dispersion import glass_scene
+    sc = pa.Scene.from_string(glass_scene(eta, res=32, spp=16).replace('"dielectric"', '"thindielectric"'), SCENES)
+    a, _ = gpu_rgb(pa, oracle, sc)
+    frac, mr = check(a, oracle_rgb(oracle, sc))
+    print(f"thin dielectric {eta}: {frac*100:.2f}% pixels within 1e-3, mean rel {mr:.2e}")

@@ -1149,7 +1149,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
             }
         }
         if (last) continue;
-        if (mtype >= kMatCoatedDiffuseT) continue;  // layered: k_vlayered
+        if (mtype == kMatCoatedDiffuseT || mtype == kMatCoatedConductorT) continue;  // layered: k_vlayered
         // ---- EvaluateMaterialAndBSDF (surfscatter.cpp:57-328) for this material type
         const VRaySamples rs = RaySamplesAt(S, st, slot, depth, mtype == 1 || mtype == kMatThinDielectricT);
         const float4 mp4 = S.matParams[mat];
@@ -1435,7 +1435,7 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
         if (prim < 0) continue;
         const int mat = S.primMaterial[prim];
         const int mtype = S.matType[mat];
-        if (mtype < kMatCoatedDiffuseT) continue;
+        if (mtype != kMatCoatedDiffuseT && mtype != kMatCoatedConductorT) continue;
         const float lambda0 = rec.lambda0[ri];
         const int slot = rec.pixel[ri];
         const int depth = rec.depth[ri], flags = rec.flags[ri], medium = rec.medium[ri];

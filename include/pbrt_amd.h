@@ -86,7 +86,9 @@ typedef struct pbrt_scene_flat {
     /* sampler: 0 halton, 1 zsobol (randomization 0 none, 1 permutedigits, 2 fastowen, 3 owen) */
     int sampler_type, zs_randomize, zs_log2_spp, zs_nbase4_digits;
     /* materials: type 0 diffuse, 1 dielectric, 2 conductor (materials.h DiffuseMaterial,
-     * DielectricMaterial, ConductorMaterial), 3 interface, 4 coateddiffuse, 5 coatedconductor */
+     * DielectricMaterial, ConductorMaterial), 3 interface, 4 coateddiffuse, 5 coatedconductor,
+     * 6 thindielectric, 7 diffusetransmission (reflectance in material_coeffs, transmittance in
+     * material_layer's albedo fields, scale = material_params[3]) */
     const int32_t *material_type;     /* [n_materials] */
     const float *material_params;     /* [n_materials][4]: alpha_x alpha_y eta 0 (TrowbridgeReitz
                                          alphas after remap + clamp; dielectric eta) */

@@ -1249,8 +1249,8 @@ static bool Refract(Vec wi, Vec n, Float eta, Float *etap, Vec *wt) {
 static inline Vec Reflect(Vec wo, Vec n) { return -wo + 2 * Dot(wo, n) * n; }
 
 struct BxDF {
-    int type = 0;  // 0 diffuse, 1 dielectric, 2 conductor
-    Spectrum R;
+    int type = 0;  // 0 diffuse, 1 dielectric, 2 conductor, 6 thin dielectric, 7 diffuse transmission
+    Spectrum R, Tt;  // Tt: DiffuseTransmissionBxDF's T
     Float eta = 1;
     TRDistribution mf;
     Spectrum etaS, kS;
@@ -1258,6 +1258,7 @@ struct BxDF {
     int Flags() const {
         if (type == 0) return R ? (BxR | BxDiffuse) : 0;
         if (type == 6) return BxR | BxT | BxSpecular;  // ThinDielectricBxDF
+        if (type == 7) return (R ? (BxR | BxDiffuse) : 0) | (Tt ? (BxT | BxDiffuse) : 0);
         int lobe = mf.Smooth() ? BxSpecular : BxGlossy;
         if (type == 1) return (eta == 1 ? BxT : (BxR | BxT)) | lobe;
         return BxR | lobe;
@@ -1268,6 +1269,20 @@ struct BxDF {
         return r;
     }
     bool Sample_f(Vec wo, Float uc, Float u0, Float u1, BSDFSample *bs, bool radiance = true, int sf = 3) const {
+        if (type == 7) {
+            // DiffuseTransmissionBxDF::Sample_f (bxdfs.h:231-260)
+            Float pr = (sf & 1) ? R.Max() : 0, pt = (sf & 2) ? Tt.Max() : 0;
+            if (pr == 0 && pt == 0) return false;
+            Vec wi = SampleCosineHemisphere(u0, u1);
+            if (uc < pr / (pr + pt)) {
+                if (wo.z < 0) wi.z *= -1;
+                *bs = BSDFSample{f(wo, wi), wi, std::abs(wi.z) * InvPi * pr / (pr + pt), BxR | BxDiffuse, 1};
+            } else {
+                if (wo.z > 0) wi.z *= -1;
+                *bs = BSDFSample{f(wo, wi), wi, std::abs(wi.z) * InvPi * pt / (pr + pt), BxT | BxDiffuse, 1};
+            }
+            return true;
+        }
         if (type == 6) {
             // ThinDielectricBxDF::Sample_f (bxdfs.h:355-386)
             Float R_ = FrDielectric(std::abs(wo.z), eta), T_ = 1 - R_;
@@ -1367,6 +1382,7 @@ struct BxDF {
     }
     Spectrum f(Vec wo, Vec wi, bool radiance = true) const {
         if (type == 6) return Spectrum(0.f);
+        if (type == 7) return SameHemisphere(wo, wi) ? R * InvPi : Tt * InvPi;
         if (type == 0) return SameHemisphere(wo, wi) ? R * InvPi : Spectrum(0.f);
         if (type == 2) {
             if (!SameHemisphere(wo, wi) || mf.Smooth()) return Spectrum(0.f);
@@ -1392,6 +1408,11 @@ struct BxDF {
     }
     Float PDF(Vec wo, Vec wi, int sf = 3) const {
         if (type == 6) return 0;
+        if (type == 7) {
+            Float pr = (sf & 1) ? R.Max() : 0, pt = (sf & 2) ? Tt.Max() : 0;
+            if (pr == 0 && pt == 0) return 0;
+            return (SameHemisphere(wo, wi) ? pr : pt) / (pr + pt) * (std::abs(wi.z) * InvPi);
+        }
         if (type != 1 && !(sf & 1)) return 0;
         if (type == 0) return SameHemisphere(wo, wi) ? std::abs(wi.z) * InvPi : 0;
         if (type == 2) {
@@ -2485,6 +2506,17 @@ struct Renderer {
                 if (f->regularize && anyNonSpecular) {
                     lay.top.mf.Regularize();
                     lay.bottom.mf.Regularize();
+                }
+            } else if (bx.type == 7) {
+                // DiffuseTransmissionMaterial::GetBxDF (materials.h): Clamp(scale * R | T, 0, 1)
+                const float *ml = f->material_layer + 12 * mat;
+                const Float scale = f->material_params[4 * mat + 3];
+                for (int i = 0; i < NS; ++i) {
+                    Float l = lambda.lambda[i];
+                    Float r = f->material_constant[mat] ? mc[3] : Sigmoid(mc[0], mc[1], mc[2], l);
+                    Float t = ml[8] != 0 ? ml[7] : Sigmoid(ml[4], ml[5], ml[6], l);
+                    bx.R[i] = Clamp(scale * r, 0, 1);
+                    bx.Tt[i] = Clamp(scale * t, 0, 1);
                 }
             } else if (bx.type == 0) {
                 for (int i = 0; i < NS; ++i) {

@@ -110,7 +110,7 @@ struct pbrt_scene {
             matCoeffs.insert(matCoeffs.end(), {m.c0, m.c1, m.c2, m.constantValue});
             matConstant.push_back(m.constant ? 1 : 0);
             matType.push_back(m.type);
-            matParams.insert(matParams.end(), {m.alphaX, m.alphaY, m.eta, 0.f});
+            matParams.insert(matParams.end(), {m.alphaX, m.alphaY, m.eta, m.scale});
             matSpectra.insert(matSpectra.end(), {m.etaSpec, m.kSpec});
         }
         MediumTables(s, &mediumInfo, &mediumParams, &mediumValues);
@@ -302,7 +302,7 @@ static void BuildDevice(pbrt_context *c) {
         std::vector<float> mp, pll, plv;
         for (auto &m : s.materials) {
             mt.push_back(m.type);
-            mp.insert(mp.end(), {m.alphaX, m.alphaY, m.eta, 0.f});
+            mp.insert(mp.end(), {m.alphaX, m.alphaY, m.eta, m.scale});
             msp.insert(msp.end(), {m.etaSpec, m.kSpec});
         }
         for (auto &sp : s.plSpectra) {
@@ -451,7 +451,7 @@ static void BuildDevice(pbrt_context *c) {
     c->volumetric = !s.media.empty() ||
                     std::any_of(s.materials.begin(), s.materials.end(), [](const MaterialDesc &m) {
                         return m.type == kMatInterface || m.type == kMatCoatedDiffuse || m.type == kMatCoatedConductor ||
-                               m.type == kMatThinDielectric;
+                               m.type == kMatThinDielectric || m.type == kMatDiffuseTransmission;
                     });
     S.dispersive = std::any_of(s.materials.begin(), s.materials.end(),
                                [](const MaterialDesc &m) { return ((m.type == kMatDielectric || m.type == kMatThinDielectric) && m.etaSpec >= 0) || m.ifaceEtaSpec >= 0;

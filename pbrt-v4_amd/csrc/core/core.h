@@ -1486,6 +1486,46 @@ PHD void FilterSample(const FilterParams &f, const FilterTableView &tab, float u
     *weight = tab.F()[v * tab.nu + u] / (pdf0 * pdf1);
 }
 
+// ---------------------------------------------------------------- diffuse transmission
+// DiffuseTransmissionBxDF (bxdfs.h:218-296): Lambertian reflection R and transmission T; the
+// lobe is chosen by the largest R and T values (pr, pt).  sp.R(i) = R_i, sp.EtaK(i, ...) unused,
+// sp.T(i) = T_i.
+template <typename Spec>
+struct DiffuseTransmission {
+    const Spec &sp;
+    float pr, pt;  // R.MaxComponentValue(), T.MaxComponentValue()
+    PHD int Flags() const {
+        return (pr > 0 ? (kBxReflection | kBxDiffuse) : 0) | (pt > 0 ? (kBxTransmission | kBxDiffuse) : 0);
+    }
+    PHD void f(V3 wo, V3 wi, float fo[kNSpectrumSamples]) const {
+        const bool same = SameHemisphere(wo, wi);
+        PHD_UNROLL
+        for (int i = 0; i < kNSpectrumSamples; ++i) fo[i] = (same ? sp.R(i) : sp.T(i)) * kInvPi;
+    }
+    PHD float PDF(V3 wo, V3 wi) const {
+        if (pr == 0 && pt == 0) return 0;
+        if (SameHemisphere(wo, wi)) return pr / (pr + pt) * CosineHemispherePDF(AbsCosTheta(wi));
+        return pt / (pr + pt) * CosineHemispherePDF(AbsCosTheta(wi));
+    }
+    PHD bool Sample_f(V3 wo, float uc, float u0, float u1, V3 *wi, float *pdf, int *flags,
+                      float fo[kNSpectrumSamples]) const {
+        if (pr == 0 && pt == 0) return false;
+        V3 w = SampleCosineHemisphere(u0, u1);
+        if (uc < pr / (pr + pt)) {
+            if (wo.z < 0) w.z *= -1;
+            *pdf = CosineHemispherePDF(AbsCosTheta(w)) * pr / (pr + pt);
+            *flags = kBxReflection | kBxDiffuse;
+        } else {
+            if (wo.z > 0) w.z *= -1;
+            *pdf = CosineHemispherePDF(AbsCosTheta(w)) * pt / (pr + pt);
+            *flags = kBxTransmission | kBxDiffuse;
+        }
+        *wi = w;
+        f(wo, w, fo);
+        return true;
+    }
+};
+
 // ---------------------------------------------------------------- layered BxDFs
 // LayeredBxDF<DielectricBxDF, DiffuseBxDF | ConductorBxDF, twoSided = true> (bxdfs.h:565-1052):
 // CoatedDiffuseBxDF / CoatedConductorBxDF.  f, Sample_f and PDF are stochastic estimates from a

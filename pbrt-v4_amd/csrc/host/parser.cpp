@@ -621,6 +621,18 @@ class Parser {
                 m.etaSpec = SpectrumParam(es, ps.loc);
             }
             Roughness(ps, &m);
+        } else if (type == "diffusetransmission") {
+            // DiffuseTransmissionMaterial::Create (materials.cpp:620-645): reflectance and
+            // transmittance default 0.25, scale 1; the transmittance rides in the albedo fields
+            m.type = kMatDiffuseTransmission;
+            m.constant = true;
+            m.constantValue = 0.25f;
+            if (Param *r = ps.Find("reflectance")) AlbedoParam(r, ps.loc, &m.constant, &m.constantValue, &m.c0, &m.c1, &m.c2);
+            m.albedoConstant = true;
+            m.albedoValue = 0.25f;
+            if (Param *t = ps.Find("transmittance"))
+                AlbedoParam(t, ps.loc, &m.albedoConstant, &m.albedoValue, &m.a0, &m.a1, &m.a2);
+            m.scale = ps.GetFloat("scale", 1.f);
         } else if (type == "thindielectric") {
             // ThinDielectricMaterial::Create (materials.cpp:83-97): eta only, always specular
             m.type = kMatThinDielectric;

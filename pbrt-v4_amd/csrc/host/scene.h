@@ -36,6 +36,7 @@ constexpr int kMatInterface = 3;
 // kernels' layered stage
 constexpr int kMatCoatedDiffuse = 4, kMatCoatedConductor = 5;
 constexpr int kMatThinDielectric = 6;  // ThinDielectricBxDF (bxdfs.h:342-404), volumetric kernels
+constexpr int kMatDiffuseTransmission = 7;  // DiffuseTransmissionBxDF (bxdfs.h:218-296), k_vlayered
 
 // Participating media (media.h:209-350, media.cpp:167-330).  Spectra are DenselySampled
 // 395..705 nm tables in SceneDesc::denseSpectra with pbrt's constructor scaling applied
@@ -76,6 +77,7 @@ struct MaterialDesc {
     float albedoValue = 0, a0 = 0, a1 = 0, a2 = 0;  // layer albedo: constant or sigmoid
     float cAlphaX = 0, cAlphaY = 0;                 // conductor.{u,v}roughness -> alphas
     int ifaceEtaSpec = -1;                          // spectral interface eta (dispersion)
+    float scale = 0;  // diffusetransmission "scale" (its transmittance uses the albedo fields)
     std::string name;
 };
 

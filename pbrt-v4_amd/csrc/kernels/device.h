@@ -57,6 +57,7 @@ constexpr int kNumMatTypes = 3;  // == host kMatNumTypes (diffuse, dielectric, c
 constexpr int kMatDiffuseT = 0, kMatDielectricT = 1, kMatConductorT = 2;
 constexpr int kMatCoatedDiffuseT = 4, kMatCoatedConductorT = 5;  // layered (volumetric path only)
 constexpr int kMatThinDielectricT = 6;                           // volumetric path only
+constexpr int kMatDiffuseTransmissionT = 7;                      // k_vlayered
 PHD int MatCounter(int type) { return type == 0 ? kCntMat : kCntMat + 3 + type; }
 PHD int CounterIndex(int depth, int queue, int shard) {
     return ((depth * kNumQueues + queue) * kShards + shard) * kCounterPad;

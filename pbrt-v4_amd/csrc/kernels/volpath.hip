@@ -1149,7 +1149,8 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
             }
         }
         if (last) continue;
-        if (mtype == kMatCoatedDiffuseT || mtype == kMatCoatedConductorT) continue;  // layered: k_vlayered
+        if (mtype == kMatCoatedDiffuseT || mtype == kMatCoatedConductorT || mtype == kMatDiffuseTransmissionT)
+            continue;  // k_vlayered
         // ---- EvaluateMaterialAndBSDF (surfscatter.cpp:57-328) for this material type
         const VRaySamples rs = RaySamplesAt(S, st, slot, depth, mtype == 1 || mtype == kMatThinDielectricT);
         const float4 mp4 = S.matParams[mat];
@@ -1415,6 +1416,7 @@ struct LayerSpec {
         *k = b[i];
     }
     __device__ float Albedo(int i) const { return alb[i]; }
+    __device__ float T(int i) const { return alb[i]; }  // diffuse transmission: T in alb
 };
 
 // EvaluateMaterialAndBSDF<CoatedDiffuseBxDF | CoatedConductorBxDF> (surfscatter.cpp:57-328):
@@ -1435,7 +1437,8 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
         if (prim < 0) continue;
         const int mat = S.primMaterial[prim];
         const int mtype = S.matType[mat];
-        if (mtype != kMatCoatedDiffuseT && mtype != kMatCoatedConductorT) continue;
+        if (mtype != kMatCoatedDiffuseT && mtype != kMatCoatedConductorT && mtype != kMatDiffuseTransmissionT) continue;
+        const bool dt = mtype == kMatDiffuseTransmissionT;
         const float lambda0 = rec.lambda0[ri];
         const int slot = rec.pixel[ri];
         const int depth = rec.depth[ri], flags = rec.flags[ri], medium = rec.medium[ri];
@@ -1466,10 +1469,21 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
         const int kSpec = conductor ? S.matSpectra[2 * mat + 1] : -1;
         LayerSpec sp;
         bool bottomNz = false, albNz = false;
+        float prMax = 0, ptMax = 0;
         {
             SpectralIter it(lambda0);
 #pragma unroll 1
             for (int i = 0; i < kNS; ++i, it.Next()) {
+                if (dt) {
+                    // DiffuseTransmissionMaterial::GetBxDF: Clamp(scale * R, 0, 1), likewise T
+                    const float r = constant ? mc.w : SigmoidPolynomial(mc.x, mc.y, mc.z, it.lam);
+                    const float t = L2.x != 0 ? L1.w : SigmoidPolynomial(L1.x, L1.y, L1.z, it.lam);
+                    sp.a[i] = Clampf(mp4.w * r, 0, 1);
+                    sp.alb[i] = Clampf(mp4.w * t, 0, 1);
+                    prMax = i == 0 ? sp.a[i] : fmaxf(prMax, sp.a[i]);
+                    ptMax = i == 0 ? sp.alb[i] : fmaxf(ptMax, sp.alb[i]);
+                    continue;
+                }
                 if (!conductor) {
                     sp.a[i] = Reflectance(mc, constant, it.lam);
                     bottomNz |= sp.a[i] != 0;
@@ -1499,23 +1513,28 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
         }
         const LayeredBxDF<LayerSpec> L{ieta,         trTop, trBot, conductor, fmaxf(L0.x, 1.17549435e-38f),
                                        Clampf(L0.y, -1, 1), albNz, (int)L0.z,  (int)L0.w, 0, sp, bottomNz};
-        const int bflags = L.LayerFlags();
+        const DiffuseTransmission<LayerSpec> D{sp, prMax, ptMax};
+        const int bflags = dt ? D.Flags() : L.LayerFlags();
         const Frame frame = Frame::FromXZ(Normalize(si.dpdus), si.ns);
         const V3 woL = frame.ToLocal(wo3);
         float fo[kNS];
         // ---- light sampling + shadow ray (surfscatter.cpp:252-326): reflective, not transmissive
         if (bflags & (kBxDiffuse | kBxGlossy)) {
-            const V3 cp = OffsetRayOrigin(si.p, si.pErr, si.n, wo3);
+            const bool refl = bflags & kBxReflection, trans = bflags & kBxTransmission;
+            V3 cp = si.p;
+            if (refl && !trans) cp = OffsetRayOrigin(si.p, si.pErr, si.n, wo3);
+            else if (refl && trans) cp = OffsetRayOrigin(si.p, si.pErr, si.n, -wo3);
             AreaLightHit ls;
             if (SampleAreaLightAt(S, cp, si.n, si.ns, rs.dUc, rs.dU0, rs.dU1, lambda0, &ls) && woL.z != 0) {
                 const V3 wi = Normalize(ls.p - cp);
                 const V3 wiL = frame.ToLocal(wi);
-                L.f(woL, wiL, true, fo);
+                if (dt) D.f(woL, wiL, fo);
+                else L.f(woL, wiL, true, fo);
                 bool fnz = false;
 #pragma unroll 1
                 for (int i = 0; i < kNS; ++i) fnz |= fo[i] != 0;
                 if (fnz) {
-                    const float bsdfPDF = L.PDF(woL, wiL, true);
+                    const float bsdfPDF = dt ? D.PDF(woL, wiL) : L.PDF(woL, wiL, true);
                     const float absdot = AbsDotN(si.ns, wi);
                     const V3 so = OffsetRayOrigin(si.p, si.pErr, si.n, ls.p - si.p);
                     const V3 pt = OffsetRayOrigin(ls.p, ls.pErr, ls.n, so - ls.p);
@@ -1554,7 +1573,13 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
         }
         // ---- BSDF::Sample_f + RR + indirect ray (surfscatter.cpp:170-250)
         if (woL.z == 0) continue;
-        const LayerSample bs = L.Sample_f(woL, rs.iUc, rs.iU0, rs.iU1, true, fo);
+        LayerSample bs;
+        if (dt) {
+            bs.pdfIsProportional = false;
+            bs.ok = D.Sample_f(woL, rs.iUc, rs.iU0, rs.iU1, &bs.wi, &bs.pdf, &bs.flags, fo);
+        } else {
+            bs = L.Sample_f(woL, rs.iUc, rs.iU0, rs.iU1, true, fo);
+        }
         if (!bs.ok || bs.pdf == 0 || bs.wi.z == 0) continue;
         bool fAny = false;
 #pragma unroll 1
@@ -1563,8 +1588,8 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
         const V3 wi = frame.FromLocal(bs.wi);
         const float absdot = AbsDotN(si.ns, wi);
         // BSDF::PDF(wo, wi) takes wi back to the local frame (bsdf.h:118-125)
-        const float pdfP = L.PDF(woL, frame.ToLocal(wi), true);
-        const float etaScale = rec.etaScale[ri];  // the layered sample's eta is 1
+        const float pdfP = bs.pdfIsProportional ? L.PDF(woL, frame.ToLocal(wi), true) : bs.pdf;
+        const float etaScale = rec.etaScale[ri];  // the layered / diffuse sample's eta is 1
         float rus = 0;
 #pragma unroll 1
         for (int i = 0; i < kNS; ++i) rus = i == 0 ? ruIn.v0 : rus + ruIn(i);
@@ -1943,7 +1968,7 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
     else hipLaunchKernelGGL(k_vmedium, gW, block, 0, s, S, st, v, wf);
     hipLaunchKernelGGL(k_vsurface, gW, block, VolTablesLdsBytes(S) + kNS * kBlock * sizeof(float), s, S, st, v, wf);
     if (wf == S.maxDepth) return hipGetLastError();
-    if (S.matTypeMask & ((1 << kMatCoatedDiffuseT) | (1 << kMatCoatedConductorT)))
+    if (S.matTypeMask & ((1 << kMatCoatedDiffuseT) | (1 << kMatCoatedConductorT) | (1 << kMatDiffuseTransmissionT)))
         hipLaunchKernelGGL(k_vlayered, gW, block, 0, s, S, st, v, wf);
     hipLaunchKernelGGL(k_vscatter, gW, block, 0, s, S, st, v, wf);
     if (S.media.allGrey) {

@@ -70,3 +70,13 @@ def test_thin_dielectric_matches_oracle(pa, oracle, eta):
     a, _ = gpu_rgb(pa, oracle, sc)
     frac, mr = check(a, oracle_rgb(oracle, sc))
     print(f"thin dielectric {eta}: {frac*100:.2f}% pixels within 1e-3, mean rel {mr:.2e}")
+
+
+@pytest.mark.parametrize("mat", ['"diffusetransmission" "rgb reflectance" [0.6 0.3 0.2] "rgb transmittance" [0.2 0.4 0.5]',
+                                 '"diffusetransmission" "float scale" 2'])
+def test_diffuse_transmission_matches_oracle(pa, oracle, mat):
+    from test_dispersion import glass_scene
+    sc = pa.Scene.from_string(glass_scene(res=32, spp=16).replace('"dielectric" "spectrum eta" "glass-BK7"', mat), SCENES)
+    a, _ = gpu_rgb(pa, oracle, sc)
+    frac, mr = check(a, oracle_rgb(oracle, sc))
+    print(f"diffuse transmission {mat}: {frac*100:.2f}% pixels within 1e-3, mean rel {mr:.2e}")

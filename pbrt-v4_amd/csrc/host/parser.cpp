@@ -1258,6 +1258,7 @@ void Parser::Finish() {
         int lightSpectrum = -1;
         float lightScale = 1;
         bool twoSided = false;
+        float power = -1;
         if (!s.areaLight.empty()) {
             ParamSet &ap = s.areaParams;
             Param *L = ap.Find("L");
@@ -1294,7 +1295,7 @@ void Parser::Finish() {
             twoSided = ap.GetBool("twosided", false);
             // lights.cpp:941: scale /= SpectrumToPhotometric(L) (illuminant part only)
             lightScale /= photometric;
-            if (ap.GetFloat("power", -1) > 0) throw Error(ap.loc + ": \"power\" not supported yet");
+            power = (float)ap.GetFloat("power", -1);  // applied per triangle below
             float spread = (float)ap.GetFloat("spread", 90);
             if (spread != 90) throw Error(ap.loc + ": \"spread\" other than 90 not supported yet");
             ap.Find("filename");
@@ -1317,6 +1318,13 @@ void Parser::Finish() {
                 l.twoSided = twoSided;
                 V3 p0 = scene.verts[tri[0]], p1 = scene.verts[tri[1]], p2 = scene.verts[tri[2]];
                 l.area = 0.5f * Length(Cross(p1 - p0, p2 - p0));  // Triangle::Area (shapes.h)
+                if (power > 0) {
+                    // lights.cpp:943-965: each triangle is its own DiffuseAreaLight, scaled so that
+                    // it emits phi_v: k_e = (twoSided ? 2 : 1) * Area * Pi
+                    float k_e = 1;
+                    k_e *= (twoSided ? 2 : 1) * l.area * kPi;
+                    l.scale *= power / k_e;
+                }
                 scene.triLight.push_back((int)scene.areaLights.size());
                 scene.areaLights.push_back(l);
             } else {

@@ -917,6 +917,22 @@ static std::array<float, 311> DensePiecewiseLinear(const std::vector<double> &nu
     return out;
 }
 
+// Blackbody (util/spectrum.h): Planck's law with the CPU FastExp, in pbrt's float operation
+// order; BlackbodySpectrum divides by its value at Wien's peak
+static float Blackbody(float lambda, float T) {
+    if (T <= 0) return 0;
+    const float c = 299792458.f, h = 6.62606957e-34f, kb = 1.3806488e-23f;
+    const float l = lambda * 1e-9f;
+    const float l2 = l * l;
+    const float l5 = l2 * l2 * l;  // Pow<5>
+    return (2 * h * c * c) / (l5 * (FastExp((h * c) / (l * kb * T)) - 1));
+}
+static float BlackbodyNormalized(float lambda, float T) {
+    const float lambdaMax = 2.8977721e-3f / T;
+    const float norm = 1 / Blackbody(lambdaMax * 1e9f, T);
+    return Blackbody(lambda, T) * norm;
+}
+
 static float PhotometricOf(const std::array<float, 311> &dense) {
     // SpectrumToPhotometric (util/spectrum.cpp:37-51) over the dense samples
     const SpectralData &d = GetSpectralData();
@@ -1279,7 +1295,13 @@ void Parser::Finish() {
                 rgb[0] = -1;
                 spectrumKey = "pl:" + std::to_string(scene.denseSpectra.size());
             } else if (L->type == "blackbody") {
-                throw Error(ap.loc + ": blackbody L not supported yet");
+                // BlackbodySpectrum(T) (util/spectrum.h), densely sampled; photometric over it
+                if (L->nums.size() != 1) throw Error(ap.loc + ": blackbody L needs one temperature");
+                const float T = (float)L->nums[0];
+                for (int i = 0; i < 311; ++i) dense[i] = BlackbodyNormalized(395.f + i, T);
+                photometric = PhotometricOf(dense);
+                rgb[0] = -1;
+                spectrumKey = "bb:" + std::to_string(T);
             } else {
                 throw Error(ap.loc + ": L of type " + L->type + " not supported");
             }

@@ -2,6 +2,7 @@
 triangle of the shape is its own light, its scale multiplied by phi_v / k_e with
 k_e = (twoSided ? 2 : 1) * Area * Pi, after the 1 / SpectrumToPhotometric(L) normalisation."""
 import numpy as np
+import pytest
 
 from conftest import SCENES
 
@@ -32,3 +33,20 @@ def test_power_scales_each_triangle(pa):
         np.testing.assert_allclose(got, want, rtol=1e-6)
     # no power (or a non-positive one): the scale is untouched
     np.testing.assert_array_equal(_lights(pa, '"float power" -1'), base)
+
+
+def test_blackbody_emitter_matches_reference(pa, golden):
+    """ "blackbody L" [T]: BlackbodySpectrum (util/spectrum.h) densely sampled, and the
+    1 / SpectrumToPhotometric scale, against the reference's own outputs
+    (tests/golden/reference_components.json "blackbody", oracle/ref/refgold.cpp)."""
+    cases = golden["blackbody"]
+    assert len(cases) == 7
+    for e in cases:
+        T = float(e["T"][0])
+        f = pa.Scene.from_string(SCENE.replace('"rgb L" [ 2 3 4 ]', f'"blackbody L" [ {T} ]').format(extra=""),
+                                 SCENES).flat()
+        spec = f.light_spectrum[0]
+        dense = np.array([f.dense_spectra[311 * spec + i] for i in range(311)], np.float32)
+        want = np.asarray(e["values"], np.float32)
+        np.testing.assert_allclose(dense, want, rtol=2e-6, atol=0)
+        assert f.light_scale[0] == pytest.approx(1 / float(e["photometric"][0]), rel=1e-5)

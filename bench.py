@@ -9,9 +9,12 @@ conductor, 1920x1080, 128 spp) -- extra lines, not the headline.
 
 One "step" = one complete render of that image (all 64 samples per pixel, film cleared
 first) plus, for N > 1, the single RCCL sum-reduce of the film over xGMI.  Pixel rows are
-sharded across ranks in 16-row blocks (strong scaling: every step renders the same whole
-image, split over the N ranks, so per-GPU work is 1/N of it; the metric counts every sample
-of the image).  Launch: ``python bench.py`` (1 GPU) or
+sharded across ranks in 16-row blocks (pixel tiles, BVH replicated, no collective on the data
+path).  Default for N > 1 is weak scaling: each GPU keeps the single-GPU workload, i.e. the job
+is the same 1280x720 image at 64 x N spp whose row stripes are dealt over the N GPUs (each
+renders 1/N of the rows at all 64 x N samples = 1280x720x64 samples' worth of paths);
+``--scaling strong`` splits one 1280x720x64 image N ways instead.  The metric counts every
+sample of the job.  Launch: ``python bench.py`` (1 GPU) or
 ``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``.
 
 The JSON line also carries
@@ -54,6 +57,9 @@ def parse():
     ap.add_argument("--max-paths", type=int, default=1 << 22)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="N > 1: weak = every GPU renders the single-GPU workload (job spp x N); "
+                         "strong = one image split N ways")
     a = ap.parse_args()
     d = {"c2": (1280, 720, 64), "c3": (1920, 1080, 256), "c4": (1920, 1080, 128), "c5": (1280, 720, 1024)}[a.workload]
     a.xres = a.xres or d[0]
@@ -62,15 +68,16 @@ def parse():
     return a
 
 
-def load(args):
+def load(args, spp=None):
     import pbrt_amd as pa
+    spp = spp or args.spp
     if args.workload == "c4":
         import tempfile
         sys.path.insert(0, str(ROOT / "scenes"))
         import gen_c4
         keep = os.environ.get("PBRT_C4_DIR")
         out = Path(keep or tempfile.mkdtemp(prefix="pbrt_c4_"))
-        path, _ = gen_c4.generate(out, xres=args.xres, yres=args.yres, spp=args.spp)
+        path, _ = gen_c4.generate(out, xres=args.xres, yres=args.yres, spp=spp)
         scene = pa.load_scene(path)  # the PLY files are read completely here
         if not keep:
             import shutil
@@ -79,13 +86,13 @@ def load(args):
     if args.workload == "c5":
         sys.path.insert(0, str(ROOT / "scenes"))
         import gen_c5
-        return pa.Scene.from_string(gen_c5.scene_text(args.xres, args.yres, args.spp, grid=256), ROOT / "scenes")
+        return pa.Scene.from_string(gen_c5.scene_text(args.xres, args.yres, spp, grid=256), ROOT / "scenes")
     if args.workload == "c3":
         sys.path.insert(0, str(ROOT / "scenes"))
         import gen_c3
-        return pa.Scene.from_string(gen_c3.scene_text(args.xres, args.yres, args.spp), ROOT / "scenes")
+        return pa.Scene.from_string(gen_c3.scene_text(args.xres, args.yres, spp), ROOT / "scenes")
     return pa.load_scene(ROOT / "scenes" / "cornell-box.pbrt", xresolution=args.xres, yresolution=args.yres,
-                         spp=args.spp)
+                         spp=spp)
 
 
 def cpu_baseline(args, threads, sc):
@@ -135,9 +142,10 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
     import pbrt_amd as pa
-    from pbrt_amd.tiles import film_tensor_from_device_ptr, rows_for_rank
+    from pbrt_amd.tiles import film_tensor_from_device_ptr, job_spp, rows_for_rank
 
-    scene = load(args)
+    scaling = args.scaling if world > 1 else "weak"
+    scene = load(args, job_spp(args.spp, world, scaling))
     info = scene.info
     integ = pa.WavefrontPathIntegrator(scene, device=local_rank, max_paths=args.max_paths)
     rows = rows_for_rank(info.py0, info.py1, rank, world)
@@ -190,7 +198,7 @@ def main():
             except Exception as e:  # the baseline is reported, never required
                 cpu = {"value": None, "error": str(e)}
         line = {
-            "metric": f"Msamples/sec (paths x spp / s) at {args.xres}x{args.yres}x{info.spp}spp",
+            "metric": f"Msamples/sec (paths x spp / s) at {args.xres}x{args.yres}x{args.spp}spp",
             "value": round(value, 3),
             "unit": "Msamples/s",
             "n_gpus": world,
@@ -198,7 +206,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(dt_max / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
@@ -217,8 +225,9 @@ def main():
                                     "untextured (BASELINE configs[3] geometry)"),
                        "xres": args.xres, "yres": args.yres, "spp": info.spp, "max_depth": info.max_depth,
                        "triangles": info.n_triangles, "paths_per_pass": int(st.paths_per_pass),
-                       "sharding": "16-row stripes round-robin over ranks + 1 RCCL film reduce" if world > 1 else
-                       "single GPU"},
+                       "sharding": (f"16-row stripes round-robin over ranks, job {info.spp} spp "
+                                    f"({'spp x N: weak' if scaling == 'weak' else 'strong'} scaling) "
+                                    "+ 1 RCCL film reduce") if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "kernel": ("k_vclosest (BVH8 traverse + hit record + push to medium / surface queue)"

@@ -1104,9 +1104,18 @@ int pbrt_film_get_rgb(pbrt_context *ctx, float *rgb) {
 int pbrt_film_write_image(pbrt_context *ctx, const char *path, int writeFP16) {
     try {
         if (!ctx || !path) return Fail("null argument");
-        std::vector<float> rgb((size_t)ctx->desc.xres * ctx->desc.yres * 3);
+        // RGBFilm::GetImage (film.cpp) covers pixelBounds only; Image::WriteEXR records it as
+        // the dataWindow of the full-resolution displayWindow
+        const SceneDesc &d = ctx->desc;
+        std::vector<float> rgb((size_t)d.xres * d.yres * 3);
         if (pbrt_film_get_rgb(ctx, rgb.data())) return 1;
-        WriteImage(path, rgb.data(), ctx->desc.xres, ctx->desc.yres, writeFP16 != 0);
+        const int w = d.px1 - d.px0, h = d.py1 - d.py0;
+        std::vector<float> crop((size_t)w * h * 3);
+        for (int y = 0; y < h; ++y)
+            std::copy(rgb.begin() + ((size_t)(d.py0 + y) * d.xres + d.px0) * 3,
+                      rgb.begin() + ((size_t)(d.py0 + y) * d.xres + d.px0 + w) * 3, crop.begin() + (size_t)y * w * 3);
+        const int window[4] = {d.px0, d.py0, d.xres, d.yres};
+        WriteImage(path, crop.data(), w, h, writeFP16 != 0, window);
         return 0;
     } catch (const std::exception &e) {
         return Fail(e.what());

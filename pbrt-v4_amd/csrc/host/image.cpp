@@ -171,7 +171,10 @@ struct Bytes {
     }
 };
 
-static void WriteEXR(const std::string &path, const float *rgb, int w, int h, bool half) {
+// win = {x0, y0, fullW, fullH}: the image covers the film's pixelBounds starting at (x0, y0) of a
+// fullW x fullH frame (Image::WriteEXR, util/image.cpp:1179-1200: displayWindow = full resolution,
+// dataWindow = pixelBounds; scanline y coordinates are absolute).
+static void WriteEXR(const std::string &path, const float *rgb, int w, int h, bool half, const int win[4]) {
     const int pt = half ? 1 : 2, bpc = half ? 2 : 4;  // pixel type HALF / FLOAT
     Bytes hdr;
     hdr.u32(20000630u);  // magic
@@ -194,10 +197,11 @@ static void WriteEXR(const std::string &path, const float *rgb, int w, int h, bo
         hdr.attr("compression", "compression", v);
     }
     {
-        Bytes v;
-        v.i32(0), v.i32(0), v.i32(w - 1), v.i32(h - 1);
-        hdr.attr("dataWindow", "box2i", v);
-        hdr.attr("displayWindow", "box2i", v);
+        Bytes data, disp;
+        data.i32(win[0]), data.i32(win[1]), data.i32(win[0] + w - 1), data.i32(win[1] + h - 1);
+        disp.i32(0), disp.i32(0), disp.i32(win[2] - 1), disp.i32(win[3] - 1);
+        hdr.attr("dataWindow", "box2i", data);
+        hdr.attr("displayWindow", "box2i", disp);
     }
     {
         Bytes v;
@@ -227,7 +231,7 @@ static void WriteEXR(const std::string &path, const float *rgb, int w, int h, bo
     std::fwrite(hdr.b.data(), 1, hdr.b.size(), fp.f);
     std::vector<uint8_t> line(8 + lineBytes);
     for (int y = 0; y < h; ++y) {
-        int32_t yy = y, sz = (int32_t)lineBytes;
+        int32_t yy = win[1] + y, sz = (int32_t)lineBytes;
         std::memcpy(&line[0], &yy, 4);
         std::memcpy(&line[4], &sz, 4);
         uint8_t *p = &line[8];
@@ -429,10 +433,11 @@ static void WritePNG(const std::string &path, const float *rgb, int w, int h) {
 }
 
 // ---------------------------------------------------------------- public
-void WriteImage(const std::string &path, const float *rgb, int w, int h, bool exrHalf) {
+void WriteImage(const std::string &path, const float *rgb, int w, int h, bool exrHalf, const int *window) {
     const std::string e = Ext(path);
+    const int full[4] = {0, 0, w, h};
     if (e == "pfm") WritePFM(path, rgb, w, h);
-    else if (e == "exr") WriteEXR(path, rgb, w, h, exrHalf);
+    else if (e == "exr") WriteEXR(path, rgb, w, h, exrHalf, window ? window : full);
     else if (e == "png") WritePNG(path, rgb, w, h);
     else throw std::runtime_error(path + ": unsupported image format \"" + e + "\" (pfm, exr, png)");
 }

@@ -12,8 +12,11 @@ struct Image {
     std::vector<float> rgb;  // [height][width][3], row 0 = top
 };
 
-// by extension: .pfm (float), .exr (half unless exrHalf = false), .png (8-bit sRGB)
-void WriteImage(const std::string &path, const float *rgb, int w, int h, bool exrHalf = true);
+// by extension: .pfm (float), .exr (half unless exrHalf = false), .png (8-bit sRGB).
+// window = {x0, y0, fullW, fullH}: rgb is the w x h pixelBounds region at (x0, y0) of a
+// fullW x fullH film; EXR records it as dataWindow inside displayWindow (null: whole frame).
+void WriteImage(const std::string &path, const float *rgb, int w, int h, bool exrHalf = true,
+                const int *window = nullptr);
 Image ReadImage(const std::string &path);  // .pfm, .exr (uncompressed scanline)
 
 enum class ErrorMetric { MAE = 0, MSE = 1, MRSE = 2 };

@@ -1320,7 +1320,14 @@ void Parser::Finish() {
             power = (float)ap.GetFloat("power", -1);  // applied per triangle below
             float spread = (float)ap.GetFloat("spread", 90);
             if (spread != 90) throw Error(ap.loc + ": \"spread\" other than 90 not supported yet");
-            ap.Find("filename");
+            // lights.cpp:909-939: an image-textured emitter ("filename") emits the image and
+            // folds its average luminance into k_e; neither is on this path, so it is refused
+            // rather than rendered with the default illuminant.
+            if (Param *fn = ap.Find("filename", "string")) {
+                if (L) throw Error(ap.loc + ": Both \"L\" and \"filename\" specified for DiffuseAreaLight.");
+                (void)fn;
+                throw Error(ap.loc + ": \"filename\" (image) area lights not supported yet");
+            }
             ap.CheckUnused();
         }
         for (size_t t = 0; t < s.idx.size(); t += 3) {

@@ -19,6 +19,16 @@ def rows_for_rank(py0: int, py1: int, rank: int, world: int, block: int = 16) ->
     return rows[(blk % world) == rank]
 
 
+def job_spp(spp_per_gpu: int, world: int, scaling: str = "weak") -> int:
+    """Samples per pixel of the whole job.  Weak scaling (bench.py default for N > 1): every GPU
+    keeps the single-GPU workload (W x H x spp samples), so the job is one W x H image at
+    spp x N samples per pixel whose row stripes are dealt over the N GPUs (each renders 1/N of
+    the rows at all spp x N samples).  Strong scaling: the same W x H x spp image split N ways."""
+    if scaling not in ("weak", "strong"):
+        raise ValueError(f"scaling must be 'weak' or 'strong', not {scaling!r}")
+    return spp_per_gpu * world if scaling == "weak" else spp_per_gpu
+
+
 def reduce_film(film_tensor, dst: int = 0, group=None):
     """Sum-reduce the RGBFilm buffer ([4][yres*xres] float64: rgbSum[3], weightSum) onto
     rank ``dst`` with torch.distributed (RCCL over xGMI for device tensors, gloo on CPU)."""

@@ -50,3 +50,14 @@ def test_blackbody_emitter_matches_reference(pa, golden):
         want = np.asarray(e["values"], np.float32)
         np.testing.assert_allclose(dense, want, rtol=2e-6, atol=0)
         assert f.light_scale[0] == pytest.approx(1 / float(e["photometric"][0]), rel=1e-5)
+
+
+def test_image_area_light_is_refused(pa):
+    """An image emitter ("string filename", lights.cpp:909-939) is not on this path: it must be
+    rejected with a located error instead of rendering the default illuminant, and "L" together
+    with "filename" is the reference's own error."""
+    with pytest.raises(pa.PbrtError, match="Both \"L\" and \"filename\""):
+        pa.Scene.from_string(SCENE.format(extra='"string filename" "emit.exr"'), SCENES)
+    no_l = SCENE.replace('"rgb L" [ 2 3 4 ]', '"string filename" "emit.exr"')
+    with pytest.raises(pa.PbrtError, match="image\\) area lights not supported"):
+        pa.Scene.from_string(no_l.format(extra=""), SCENES)

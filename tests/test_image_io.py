@@ -103,3 +103,56 @@ def test_film_write_image_gpu(pa, tmp_path):
     np.testing.assert_array_equal(pa.read_image(tmp_path / "c.exr"), rgb)
     np.testing.assert_array_equal(pa.read_image(tmp_path / "c.pfm"), rgb)
     np.testing.assert_array_equal(pa.read_image(tmp_path / "h.exr"), rgb.astype(np.float16).astype(np.float32))
+
+
+def _exr_attr(name, typ, payload):
+    return name.encode() + b"\0" + typ.encode() + b"\0" + struct.pack("<I", len(payload)) + payload
+
+
+def test_exr_header_bytes_match_openexr_layout(pa, tmp_path):
+    """Byte-level check of a 2x2 float EXR against the OpenEXR file layout (single-part
+    scanline, version 2): magic, version, attributes in the library's name order (Header keeps
+    them in a std::map), chlist = per channel name\\0 + int32 pixel type + uint8 pLinear + 3
+    reserved + int32 x/y sampling, closed by \\0; then the end-of-header \\0, one uint64 offset
+    per scanline and scanlines of int32 y, int32 byte count and the channel planes in chlist
+    order.  No OpenEXR library or reference EXR fixture exists here, so this pins the layout to
+    the specification, not to bytes the reference wrote (parity of the byte stream unpinned)."""
+    img = np.array([[[1, 2, 3], [4, 5, 6]], [[7, 8, 9], [10, 11, 12]]], np.float32)
+    p = tmp_path / "t.exr"
+    pa.write_image(p, img, write_fp16=False)
+    b = p.read_bytes()
+    chl = b"".join(c + b"\0" + struct.pack("<iB3xii", 2, 0, 1, 1) for c in (b"B", b"G", b"R")) + b"\0"
+    box = struct.pack("<iiii", 0, 0, 1, 1)
+    hdr = (struct.pack("<II", 20000630, 2) + _exr_attr("channels", "chlist", chl)
+           + _exr_attr("compression", "compression", b"\0") + _exr_attr("dataWindow", "box2i", box)
+           + _exr_attr("displayWindow", "box2i", box) + _exr_attr("lineOrder", "lineOrder", b"\0")
+           + _exr_attr("pixelAspectRatio", "float", struct.pack("<f", 1))
+           + _exr_attr("screenWindowCenter", "v2f", struct.pack("<ff", 0, 0))
+           + _exr_attr("screenWindowWidth", "float", struct.pack("<f", 1)) + b"\0")
+    line = 3 * 2 * 4
+    table = struct.pack("<QQ", len(hdr) + 16, len(hdr) + 16 + 8 + line)
+    lines = b"".join(struct.pack("<ii", y, line) + img[y][:, ::-1].T.astype("<f4").tobytes() for y in range(2))
+    assert b == hdr + table + lines
+
+
+@pytest.mark.gpu
+def test_film_write_image_crop_window(pa, tmp_path):
+    """--pixelbounds / cropwindow: RGBFilm::GetImage covers pixelBounds only and Image::WriteEXR
+    records it as the dataWindow inside the full-resolution displayWindow (util/image.cpp:
+    1179-1200); PFM holds the cropped pixels."""
+    from conftest import SCENES
+    sc = pa.load_scene(SCENES / "cornell-box.pbrt", xresolution=64, yresolution=48, spp=4,
+                       pixelbounds="8,40,4,30")
+    integ = pa.WavefrontPathIntegrator(sc, max_paths=1 << 16)
+    integ.render()
+    integ.synchronize()
+    rgb = integ.film_rgb()[4:30, 8:40]
+    integ.write_image(tmp_path / "c.exr", write_fp16=False)
+    integ.write_image(tmp_path / "c.pfm")
+    np.testing.assert_array_equal(pa.read_image(tmp_path / "c.exr"), rgb)
+    np.testing.assert_array_equal(pa.read_image(tmp_path / "c.pfm"), rgb)
+    b = (tmp_path / "c.exr").read_bytes()
+    i = b.index(b"dataWindow\0box2i\0")
+    assert struct.unpack("<Iiiii", b[i + 17:i + 37]) == (16, 8, 4, 39, 29)
+    i = b.index(b"displayWindow\0box2i\0")
+    assert struct.unpack("<Iiiii", b[i + 20:i + 40]) == (16, 0, 0, 63, 47)

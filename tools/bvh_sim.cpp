@@ -1,0 +1,166 @@
+// CPU model of the BVH8 traversal kernels (common.h TraverseT) for tuning the tree layout:
+// per-ray node visits, slab tests and triangle tests, and the wave64 cost (the max over the 64
+// lanes of a wave, since a wave runs until its slowest lane finishes).  Rays: camera rays of
+// the scene's camera (pixel centres + jitter) and one cosine-distributed bounce from each hit.
+// Build: g++ -O2 -std=c++17 -Ipbrt-v4_amd/csrc tools/bvh_sim.cpp pbrt-v4_amd/build/host_*.o -o /tmp/bvh_sim -pthread
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "host/bvh.h"
+#include "host/scene.h"
+
+using namespace pbrt_amd;
+
+struct Cost {
+    long nodes = 0, tris = 0, leaves = 0;
+};
+
+static int TraverseSim(const BVH8 &b, V3 o, V3 d, float tMax, bool anyHit, Cost *c, TriHit *best) {
+    const TriRay tr = MakeTriRay(o, d);
+    V3 inv(1 / d.x, 1 / d.y, 1 / d.z);
+    int neg[3] = {inv.x < 0, inv.y < 0, inv.z < 0};
+    std::vector<int> stack;
+    int node = 0, hit = -1;
+    const float slack = 1 + 2 * gamma(3);
+    while (true) {
+        const BVH8Node &n = b.nodes[node];
+        c->nodes++;
+        float tn[8];
+        unsigned mask = 0;
+        for (int k = 0; k < 8; ++k) {
+            float lo[3] = {n.lox[k], n.loy[k], n.loz[k]}, hi[3] = {n.hix[k], n.hiy[k], n.hiz[k]};
+            float t0 = -kInfinity, t1 = kInfinity;
+            bool ok = true;
+            for (int a = 0; a < 3; ++a) {
+                float nn = neg[a] ? hi[a] : lo[a], ff = neg[a] ? lo[a] : hi[a];
+                float tmn = (nn - o[a]) * inv[a], tmx = (ff - o[a]) * inv[a] * slack;
+                if (a == 0) {
+                    t0 = tmn, t1 = tmx;
+                } else {
+                    ok = ok && !(t0 > tmx || tmn > t1);
+                    t0 = tmn > t0 ? tmn : t0;
+                    t1 = tmx < t1 ? tmx : t1;
+                }
+            }
+            ok = ok && t0 < tMax && t1 > 0;
+            tn[k] = t0;
+            if (ok) mask |= 1u << k;
+        }
+        unsigned leaves = 0, inner = 0;
+        for (int k = 0; k < 8; ++k)
+            if (mask >> k & 1) (n.child[k] < 0 ? leaves : inner) |= 1u << k;
+        while (leaves) {
+            int bc = 0;
+            float bt = kInfinity;
+            for (int k = 0; k < 8; ++k)
+                if ((leaves >> k & 1) && tn[k] <= bt) bt = tn[k], bc = k;
+            leaves &= ~(1u << bc);
+            if (bt >= tMax) continue;
+            c->leaves++;
+            int enc = ~n.child[bc], first = enc >> 3, count = (enc & 7) + 1;
+            for (int t = first; t < first + count; ++t) {
+                c->tris++;
+                const float *v = &b.triVerts[12 * t];
+                TriHit h;
+                if (IntersectTriangleRay(tr, tMax, V3(v[0], v[1], v[2]), V3(v[4], v[5], v[6]), V3(v[8], v[9], v[10]), &h)) {
+                    if (anyHit) return t;
+                    tMax = h.t;
+                    *best = h;
+                    hit = t;
+                }
+            }
+        }
+        while (inner) {
+            int bc = 0;
+            float bt = -kInfinity;
+            for (int k = 0; k < 8; ++k)
+                if ((inner >> k & 1) && tn[k] >= bt) bt = tn[k], bc = k;
+            inner &= ~(1u << bc);
+            if (bt >= tMax) continue;
+            stack.push_back(n.child[bc]);
+        }
+        if (stack.empty()) break;
+        node = stack.back();
+        stack.pop_back();
+    }
+    return hit;
+}
+
+int main(int argc, char **argv) {
+    if (argc < 2) {
+        fprintf(stderr, "usage: bvh_sim scene.pbrt [leafPrims] [xres yres]\n");
+        return 1;
+    }
+    SetDataDirectory("pbrt-v4_amd/data");
+    std::map<std::string, std::string> ov;
+    int leaf = argc > 2 ? atoi(argv[2]) : 4;
+    if (argc > 4) {
+        ov["xresolution"] = argv[3];
+        ov["yresolution"] = argv[4];
+    }
+    SceneDesc s = LoadPbrtFile(argv[1], ov);
+    BVH8 b = BuildBVH8(s.verts, s.tris, leaf);
+    printf("tris %zu nodes %zu maxDepth %d stack %d\n", s.tris.size(), b.nodes.size(), b.maxDepth, b.maxStack);
+    std::mt19937 rng(1);
+    std::uniform_real_distribution<float> U(0, 1);
+    const int W = s.xres, H = s.yres;
+    long nRays[2] = {0, 0};
+    Cost tot[2], wave[2];
+    Cost laneC[64];
+    V3 bounceO[64], bounceD[64];
+    bool bounce[64];
+    for (int base = 0; base < W * H; base += 64) {
+        Cost wc[2];
+        long wmaxN[2] = {0, 0}, wmaxT[2] = {0, 0};
+        for (int l = 0; l < 64; ++l) {
+            int pix = base + l;
+            bounce[l] = false;
+            if (pix >= W * H) continue;
+            float px = pix % W + U(rng), py = pix / W + U(rng);
+            V3 pc = XformPoint(s.camera.cameraFromRaster, V3(px, py, 0));
+            V3 d = XformVector(s.camera.renderFromCamera, Normalize(pc));
+            V3 o = XformPoint(s.camera.renderFromCamera, V3(0, 0, 0));
+            Cost c;
+            TriHit h;
+            int hit = TraverseSim(b, o, d, kInfinity, false, &c, &h);
+            nRays[0]++;
+            tot[0].nodes += c.nodes, tot[0].tris += c.tris, tot[0].leaves += c.leaves;
+            wmaxN[0] = std::max(wmaxN[0], c.nodes), wmaxT[0] = std::max(wmaxT[0], c.tris);
+            if (hit >= 0) {
+                const float *v = &b.triVerts[12 * hit];
+                V3 p0(v[0], v[1], v[2]), p1(v[4], v[5], v[6]), p2(v[8], v[9], v[10]);
+                V3 p = h.b0 * p0 + h.b1 * p1 + h.b2 * p2;
+                V3 n = Normalize(Cross(p1 - p0, p2 - p0));
+                if (Dot(n, d) > 0) n = -n;
+                // cosine bounce
+                float r = std::sqrt(U(rng)), phi = 2 * kPi * U(rng);
+                V3 t1 = std::fabs(n.x) > .5f ? Normalize(Cross(n, V3(0, 1, 0))) : Normalize(Cross(n, V3(1, 0, 0)));
+                V3 t2 = Cross(n, t1);
+                V3 wi = r * std::cos(phi) * t1 + r * std::sin(phi) * t2 + std::sqrt(std::max(0.f, 1 - r * r)) * n;
+                bounceO[l] = p + n * 1e-3f;
+                bounceD[l] = wi;
+                bounce[l] = true;
+            }
+        }
+        for (int l = 0; l < 64; ++l) {
+            if (!bounce[l]) continue;
+            Cost c;
+            TriHit h;
+            TraverseSim(b, bounceO[l], bounceD[l], kInfinity, false, &c, &h);
+            nRays[1]++;
+            tot[1].nodes += c.nodes, tot[1].tris += c.tris, tot[1].leaves += c.leaves;
+            wmaxN[1] = std::max(wmaxN[1], c.nodes), wmaxT[1] = std::max(wmaxT[1], c.tris);
+        }
+        for (int k = 0; k < 2; ++k) wave[k].nodes += wmaxN[k], wave[k].tris += wmaxT[k];
+    }
+    const char *nm[2] = {"camera", "bounce"};
+    for (int k = 0; k < 2; ++k) {
+        double w = (double)(W * H) / 64;
+        printf("%s rays %ld: per ray nodes %.2f leaves %.2f tris %.2f | per wave max nodes %.2f max tris %.2f\n", nm[k],
+               nRays[k], (double)tot[k].nodes / nRays[k], (double)tot[k].leaves / nRays[k],
+               (double)tot[k].tris / nRays[k], wave[k].nodes / w, wave[k].tris / w);
+    }
+    return 0;
+}

@@ -599,6 +599,14 @@ static void BuildDevice(pbrt_context *c) {
         if (L.total > 64 * 1024 && !c->volumetric) throw Error("shade kernel LDS layout exceeds 64 KB");
     }
     S.stackSize = c->bvh.maxStack;
+    // |plane coordinate| bound per axis for the traversal's box-test margins (common.h
+    // MakeCwRay): the scene bounds, widened by twice the extent for the quantised planes'
+    // outward rounding (each lies within its node's grid of 255 steps of at most 2 ext / 255)
+    for (int a = 0; a < 3; ++a) {
+        const float lo = c->bvh.boundsMin[a], hi = c->bvh.boundsMax[a];
+        const float ext = std::isfinite(hi - lo) && hi >= lo ? hi - lo : 0.f;
+        S.bvhAbsMax[a] = std::isfinite(lo) && std::isfinite(hi) ? std::max(std::fabs(lo), std::fabs(hi)) + 2 * ext : 0.f;
+    }
     {
         // Node format: the 256-B wide node by default; PBRT_AMD_BVH=compressed selects the 80-B
         // quantised node.  Measured: the quantised node cuts node bytes 3.2x but
@@ -611,7 +619,8 @@ static void BuildDevice(pbrt_context *c) {
         int nNodes = (int)c->bvh.nodes.size(), budget = kSceneLdsBudget;
         S.ldsNodes = std::min(nNodes, budget / stride);
         budget -= S.ldsNodes * stride;
-        S.ldsTris = (!S.compressed && S.ldsNodes == nNodes && nt * 48 <= budget) ? nt : 0;  // all or none
+        // all or none, in three pre-rotated copies (one per ray permutation)
+        S.ldsTris = (!S.compressed && S.ldsNodes == nNodes && nt * 3 * 48 <= budget) ? nt : 0;
     }
 
     // film

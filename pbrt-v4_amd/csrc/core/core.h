@@ -404,22 +404,28 @@ struct TriHit {
 };
 
 // shapes.cpp:215-225: recompute the edge functions in double when one is exactly zero.
-// Rare, so it is kept out of line (its doubles would otherwise inflate every caller's VGPRs).
+// Rare, so it is kept out of line (its doubles would otherwise inflate every caller's VGPRs);
+// the three results come back by value (in registers, no scratch round trip).
+struct EdgeFns {
+    float e0, e1, e2;
+};
 #if defined(__HIPCC__)
 __host__ __device__ inline __attribute__((noinline))
 #else
 inline
 #endif
-void EdgeFunctionsFP64(V3 p0t, V3 p1t, V3 p2t, float *e0, float *e1, float *e2) {
+EdgeFns EdgeFunctionsFP64(V3 p0t, V3 p1t, V3 p2t) {
     double p2txp1ty = (double)p2t.x * (double)p1t.y;
     double p2typ1tx = (double)p2t.y * (double)p1t.x;
-    *e0 = (float)(p2typ1tx - p2txp1ty);
+    EdgeFns e;
+    e.e0 = (float)(p2typ1tx - p2txp1ty);
     double p0txp2ty = (double)p0t.x * (double)p2t.y;
     double p0typ2tx = (double)p0t.y * (double)p2t.x;
-    *e1 = (float)(p0typ2tx - p0txp2ty);
+    e.e1 = (float)(p0typ2tx - p0txp2ty);
     double p1txp0ty = (double)p1t.x * (double)p0t.y;
     double p1typ0tx = (double)p1t.y * (double)p0t.x;
-    *e2 = (float)(p1typ0tx - p1txp0ty);
+    e.e2 = (float)(p1typ0tx - p1txp0ty);
+    return e;
 }
 
 // shapes.cpp:172-273 IntersectTriangle (watertight, fp64 edge fallback), split so that the
@@ -460,7 +466,10 @@ PHD bool IntersectTriangleRay(const TriRay &r, float tMax, V3 p0, V3 p1, V3 p2, 
     float e0 = DifferenceOfProducts(p1t.x, p2t.y, p1t.y, p2t.x);
     float e1 = DifferenceOfProducts(p2t.x, p0t.y, p2t.y, p0t.x);
     float e2 = DifferenceOfProducts(p0t.x, p1t.y, p0t.y, p1t.x);
-    if (e0 == 0.0f || e1 == 0.0f || e2 == 0.0f) EdgeFunctionsFP64(p0t, p1t, p2t, &e0, &e1, &e2);
+    if (e0 == 0.0f || e1 == 0.0f || e2 == 0.0f) {
+        const EdgeFns e = EdgeFunctionsFP64(p0t, p1t, p2t);
+        e0 = e.e0, e1 = e.e1, e2 = e.e2;
+    }
     if ((e0 < 0 || e1 < 0 || e2 < 0) && (e0 > 0 || e1 > 0 || e2 > 0)) return false;
     float det = e0 + e1 + e2;
     if (det == 0) return false;

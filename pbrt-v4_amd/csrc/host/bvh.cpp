@@ -8,6 +8,9 @@
 
 namespace pbrt_amd {
 
+// empty slot box: lo = +kEmptyLo, hi = -kEmptyLo (fails every slab test, see BVH8Node)
+static constexpr float kEmptyLo = 1e30f;
+
 namespace {
 struct Box {
     V3 mn{kInfinity, kInfinity, kInfinity}, mx{-kInfinity, -kInfinity, -kInfinity};
@@ -182,12 +185,13 @@ static void Compress(BVH8 &out) {
     out.qnodes.assign(out.nodes.size(), BVH8QNode{});
     for (size_t i = 0; i < out.nodes.size(); ++i) {
         const BVH8Node &n = out.nodes[i];
+        const std::array<int32_t, 8> &child = out.childRef[i];
         BVH8QNode &q = out.qnodes[i];
         float lo[3] = {kInfinity, kInfinity, kInfinity}, hi[3] = {-kInfinity, -kInfinity, -kInfinity};
         const float *clo[3] = {n.lox, n.loy, n.loz}, *chi[3] = {n.hix, n.hiy, n.hiz};
         bool any = false;
         for (int c = 0; c < 8; ++c) {
-            if (n.child[c] == kEmptyChild) continue;
+            if (child[c] == kEmptyChild) continue;
             any = true;
             for (int a = 0; a < 3; ++a) {
                 lo[a] = std::min(lo[a], clo[a][c]);
@@ -214,7 +218,7 @@ static void Compress(BVH8 &out) {
         int innerRank = 0, triBase = -1;
         q.childBase = -1;
         for (int c = 0; c < 8; ++c) {
-            const int ch = n.child[c];
+            const int ch = child[c];
             if (ch == kEmptyChild) {
                 for (int a = 0; a < 3; ++a) qlo[a][c] = 255, qhi[a][c] = 0;
                 continue;
@@ -242,7 +246,7 @@ static void Compress(BVH8 &out) {
                 if (triBase < 0) triBase = first;
                 const int off = first - triBase;
                 if (off < 0 || off > 31 || count > 4) throw std::runtime_error("BVH8 leaf range does not fit the compressed node");
-                q.meta[c] = (uint8_t)(0x80 | ((count - 1) << 5) | off);
+                q.meta[c] = (uint8_t)((count << 5) | off);  // count 1..4; 0 = interior / empty
             }
         }
         q.triBase = triBase < 0 ? 0 : triBase;
@@ -290,17 +294,19 @@ BVH8 BuildBVH8(const std::vector<V3> &verts, const std::vector<std::array<int, 3
     };
     if (prims.empty()) {
         BVH8Node root{};
+        std::array<int32_t, 8> ref;
         for (int c = 0; c < 8; ++c) {
-            root.lox[c] = root.loy[c] = root.loz[c] = 1;
-            root.hix[c] = root.hiy[c] = root.hiz[c] = -1;
-            root.child[c] = kEmptyChild;
+            root.lox[c] = root.loy[c] = root.loz[c] = kEmptyLo;
+            root.hix[c] = root.hiy[c] = root.hiz[c] = -kEmptyLo;
+            ref[c] = kEmptyChild;
         }
         out.nodes.push_back(root);
+        out.childRef.push_back(ref);
         appendDegenerate();
         Compress(out);
         return out;
     }
-    maxLeafPrims = std::min(std::max(maxLeafPrims, 1), 8);
+    maxLeafPrims = std::min(std::max(maxLeafPrims, 1), kMaxLeafPrims);
     Builder2 b{prims, {}, maxLeafPrims};
     b.nodes = BuildParallel(prims, 0, (int)prims.size(), maxLeafPrims, 0);
 
@@ -316,6 +322,7 @@ BVH8 BuildBVH8(const std::vector<V3> &verts, const std::vector<std::array<int, 3
     std::vector<int> node8Of;  // per queue entry the BVH8 index
     size_t head = 0;
     out.nodes.push_back(BVH8Node{});
+    out.childRef.push_back({});
     node8Of.push_back(0);
     while (head < queue.size()) {
         Work w = queue[head];
@@ -346,42 +353,80 @@ BVH8 BuildBVH8(const std::vector<V3> &verts, const std::vector<std::array<int, 3
             kids.push_back(b.nodes[open].left);
             kids.push_back(b.nodes[open].right);
         }
+        // octant slots (Ylitie et al. 2017, section 3.2): slot s should hold the child that rays of
+        // direction-sign octant s (bit a set: d_a < 0) reach first, i.e. the child whose centroid
+        // lies farthest against D_s = (s & 1 ? -1 : 1, s & 2 ? -1 : 1, s & 4 ? -1 : 1).  Greedy
+        // assignment of the cheapest (child, slot) pair first.
+        int slotOf[8];
+        {
+            const Box &pb = n2.box;
+            const V3 pc = (pb.mn + pb.mx) * 0.5f;
+            float cost[8][8];
+            for (size_t k = 0; k < kids.size(); ++k) {
+                const Box &cb = b.nodes[kids[k]].box;
+                const V3 cc = (cb.mn + cb.mx) * 0.5f - pc;
+                for (int sl = 0; sl < 8; ++sl)
+                    cost[k][sl] = ((sl & 1) ? -cc.x : cc.x) + ((sl & 2) ? -cc.y : cc.y) + ((sl & 4) ? -cc.z : cc.z);
+            }
+            bool usedK[8] = {}, usedS[8] = {};
+            for (size_t round = 0; round < kids.size(); ++round) {
+                int bk = -1, bs = -1;
+                float bc = kInfinity;
+                for (size_t k = 0; k < kids.size(); ++k)
+                    for (int sl = 0; sl < 8; ++sl)
+                        if (!usedK[k] && !usedS[sl] && (bk < 0 || cost[k][sl] < bc)) bc = cost[k][sl], bk = (int)k, bs = sl;
+                usedK[bk] = usedS[bs] = true;
+                slotOf[bk] = bs;
+            }
+        }
+        int kidAt[8];
+        for (int c = 0; c < 8; ++c) kidAt[c] = -1;
+        for (size_t k = 0; k < kids.size(); ++k) kidAt[slotOf[k]] = kids[k];
         BVH8Node node{};
-        node.nChildren = (int)kids.size();
-        // a node's leaf triangles are emitted contiguously (BFS node order), so both node
-        // formats address them as one range
+        std::array<int32_t, 8> ref;
+        node.childBase = (int)queue.size();
+        node.triBase = (int)order.size();
+        // a node's interior children are consecutive in BFS order and its leaf triangles are
+        // emitted contiguously, both in slot order, so both node formats address them as ranges
         for (int c = 0; c < 8; ++c) {
-            if (c < (int)kids.size()) {
-                const Node2 &k = b.nodes[kids[c]];
+            if (kidAt[c] >= 0) {
+                const Node2 &k = b.nodes[kidAt[c]];
                 node.lox[c] = k.box.mn.x;
                 node.loy[c] = k.box.mn.y;
                 node.loz[c] = k.box.mn.z;
                 node.hix[c] = k.box.mx.x;
                 node.hiy[c] = k.box.mx.y;
                 node.hiz[c] = k.box.mx.z;
+                node.occ |= 1u << c;
                 if (k.leaf()) {
-                    if (k.count > 8) throw std::runtime_error("BVH leaf larger than 8 triangles");
+                    if (k.count > kMaxLeafPrims) throw std::runtime_error("BVH leaf larger than 4 triangles");
                     const int first = (int)order.size();
                     for (int i = k.first; i < k.first + k.count; ++i) order.push_back(prims[i].index);
-                    node.child[c] = ~((first << 3) | (k.count - 1));
+                    ref[c] = ~((first << 3) | (k.count - 1));
+                    const int off = first - node.triBase;
+                    if (off + k.count > 32) throw std::runtime_error("BVH8 node addresses more than 32 triangles");
+                    node.triMask[c] = ((1u << k.count) - 1u) << off;
                 } else {
-                    int idx8 = (int)out.nodes.size() + (int)(queue.size() - head);
                     // index assigned in BFS order: position in queue
-                    node.child[c] = (int)queue.size();
-                    queue.push_back({kids[c], w.depth + 1});
+                    ref[c] = (int)queue.size();
+                    node.imask |= 1u << c;
+                    queue.push_back({kidAt[c], w.depth + 1});
                     node8Of.push_back((int)queue.size() - 1);
-                    (void)idx8;
                 }
             } else {
-                node.lox[c] = node.loy[c] = node.loz[c] = 1;
-                node.hix[c] = node.hiy[c] = node.hiz[c] = -1;
-                node.child[c] = kEmptyChild;
+                // empty slot: an inverted box no slab test accepts (and occ excludes it)
+                node.lox[c] = node.loy[c] = node.loz[c] = kEmptyLo;
+                node.hix[c] = node.hiy[c] = node.hiz[c] = -kEmptyLo;
+                ref[c] = kEmptyChild;
             }
         }
-        if ((int)out.nodes.size() <= self) out.nodes.resize(self + 1);
+        if (node.imask == 0) node.childBase = 0;
+        if ((int)out.nodes.size() <= self) out.nodes.resize(self + 1), out.childRef.resize(self + 1);
         out.nodes[self] = node;
+        out.childRef[self] = ref;
     }
     out.nodes.resize(queue.size());
+    out.childRef.resize(queue.size());
     out.triPrim.resize(order.size());
     out.triVerts.resize(order.size() * 12);
     for (size_t i = 0; i < order.size(); ++i) {
@@ -400,22 +445,19 @@ BVH8 BuildBVH8(const std::vector<V3> &verts, const std::vector<std::array<int, 3
     }
     appendDegenerate();
     Compress(out);
-    // Worst-case traversal stack: a node pushes its k interior children and pops one before
-    // descending, so need(n) = max(k, k - 1 + max need(child)); children follow parents in
-    // BFS order, so one reverse sweep suffices.
+    // Worst-case traversal stack: descending into a node's nearest child leaves at most one
+    // entry (the rest of that node's child group) per tree level, so the bound is the depth of
+    // the deepest interior node below the root.
     std::vector<int> need(out.nodes.size(), 0);
     for (int i = (int)out.nodes.size() - 1; i >= 0; --i) {
-        int k = 0, deeper = 0;
+        int deeper = -1;
         for (int c = 0; c < 8; ++c) {
-            int ch = out.nodes[i].child[c];
-            if (ch >= 0) {
-                ++k;
-                deeper = std::max(deeper, need[ch]);
-            }
+            const int ch = out.childRef[i][c];
+            if (ch >= 0) deeper = std::max(deeper, need[ch]);
         }
-        need[i] = k ? std::max(k, k - 1 + deeper) : 0;
+        need[i] = deeper + 1;  // interior children exist: one pending group here plus theirs
     }
-    out.maxStack = need[0];
+    out.maxStack = std::max(need[0], 1);
     return out;
 }
 

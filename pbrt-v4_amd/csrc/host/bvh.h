@@ -13,16 +13,31 @@
 
 namespace pbrt_amd {
 
-// Child reference: >= 0 interior node index; < 0 leaf = ~(triStart << 3 | (count-1));
-// kEmptyChild marks an unused slot (its box is empty).
+// Child reference (host-side view, BVH8::childRef): >= 0 interior node index; < 0 leaf =
+// ~(triStart << 3 | (count-1)); kEmptyChild marks an unused slot (its box is empty).
 constexpr int32_t kEmptyChild = (int32_t)0x80000000;
+// Leaves hold at most 4 triangles, so a node's (at most 8) leaves address at most 32
+// triangles: one 32-bit mask relative to the node's triBase covers them all.
+constexpr int kMaxLeafPrims = 4;
 
+// Wide node (256 B), laid out for the device's group traversal (common.h TraverseCW):
+//  * child boxes in SoA (12 float4: lo x/y/z then hi x/y/z, children 0-3 then 4-7), so the near
+//    and far planes of 4 children are one float4 load at a per-ray offset (no per-child select);
+//  * children sit in "octant slots": slot s holds the child nearest to the entry side of rays
+//    whose direction-sign octant is s, so a ray visits slots in the order i ^ octant without
+//    sorting (Ylitie, Karras, Laine 2017, "Efficient incoherent ray traversal on GPUs through
+//    compressed wide BVHs", section 3.2);
+//  * interior children are consecutive nodes from childBase (in slot order) and the node's leaf
+//    triangles are consecutive from triBase; triMask[c] lists slot c's triangles as bits
+//    relative to triBase (0 for an interior or empty slot).
 struct alignas(16) BVH8Node {
     float lox[8], loy[8], loz[8];
     float hix[8], hiy[8], hiz[8];
-    int32_t child[8];
-    int32_t nChildren;
-    int32_t pad[7];
+    int32_t childBase, triBase;
+    uint32_t imask;  // bit c: slot c is an interior node
+    uint32_t occ;    // bit c: slot c is occupied (interior or leaf)
+    uint32_t triMask[8];
+    int32_t pad[4];
 };
 static_assert(sizeof(BVH8Node) == 256, "BVH8Node must be 256 bytes");
 
@@ -30,7 +45,8 @@ static_assert(sizeof(BVH8Node) == 256, "BVH8Node must be 256 bytes");
 // boxes as 8-bit offsets on a per-node grid lo = fma(q, 2^(e-127), p), rounded outward on the
 // host with the same fma the device decodes with, so every decoded box contains the exact one.
 // Interior children are contiguous from childBase (in slot order); a node's leaf triangles are
-// contiguous from triBase.  meta[c]: 0 = empty or interior, else 0x80 | (count-1) << 5 | offset.
+// contiguous from triBase.  meta[c]: 0 = empty or interior, else count << 5 | offset (count 1-4),
+// so slot c's triangle bits are ((1 << (meta >> 5)) - 1) << (meta & 31) with no special case.
 struct alignas(16) BVH8QNode {
     float px, py, pz;
     uint8_t ex, ey, ez;
@@ -52,14 +68,16 @@ inline float DecodeQ(uint8_t q, uint8_t e, float p) {
 struct BVH8 {
     std::vector<BVH8Node> nodes;
     std::vector<BVH8QNode> qnodes;  // the same tree, compressed (same node indices)
+    std::vector<std::array<int32_t, 8>> childRef;  // per node and slot (host view, kEmptyChild)
     // triangles in leaf order: 3 float4 per triangle = p0.xyz|prim, p1.xyz|0, p2.xyz|0
     std::vector<float> triVerts;
     std::vector<int> triPrim;  // leaf order -> original triangle index
     int maxDepth = 0;
-    int maxStack = 0;  // worst-case traversal stack entries (farthest-first pushes)
+    int maxStack = 0;  // worst-case traversal stack entries (one pending child group per level)
     V3 boundsMin, boundsMax;
 };
 
-BVH8 BuildBVH8(const std::vector<V3> &verts, const std::vector<std::array<int, 3>> &tris, int maxLeafPrims = 4);
+BVH8 BuildBVH8(const std::vector<V3> &verts, const std::vector<std::array<int, 3>> &tris,
+               int maxLeafPrims = kMaxLeafPrims);
 
 }  // namespace pbrt_amd

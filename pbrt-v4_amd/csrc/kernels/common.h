@@ -304,162 +304,249 @@ __device__ inline void PixelOf(const PathState &st, int slot, int *px, int *py, 
 }
 
 // ------------------------------------------------------------------ BVH8 traversal
-// One ray per lane.  The node's 8 child boxes are read as 12 float4 loads (SoA inside the
-// 256-byte node), the 8 slab tests run fully unrolled in registers, leaves are intersected
-// nearest-first and interior children are pushed farthest-first onto a per-lane stack that
-// lives in LDS ([depth][lane] layout: consecutive lanes hit consecutive banks), so nothing
-// spills to scratch.  Box test = Bounds3::IntersectP (util/vecmath.h:1576-1611) including the
-// 1 + 2 gamma(3) far-plane slack; triangle test = IntersectTriangle (shapes.cpp:172-273).
-// Stack entries per lane = DeviceScene::stackSize (the BVH's exact worst case, host-computed,
-// at most kMaxStackSize), allocated as dynamic LDS at launch so small scenes keep occupancy.
+// One ray per lane, compressed-wide-BVH group traversal (Ylitie, Karras, Laine 2017): a visited
+// node yields (a) a bit mask of its hit leaf triangles, relative to the node's triBase, tested
+// right away, and (b) the group of its hit interior children as a bit mask in visit order
+// (slot i ^ octant, nearest first: BVH8Node's octant slots).  The traversal descends into the
+// group's first child and keeps the rest of the group as ONE stack entry {childBase,
+// imask << 8 | remaining bits}, so the stack grows by at most one entry per tree level and no
+// child distances are sorted or stored.
+//
+// Box test: Bounds3::IntersectP (util/vecmath.h:1576-1611) decides only which nodes are
+// visited, never a hit's value, so any test that accepts every box the exact real-arithmetic
+// test accepts gives the same closest hit (and the same first-found any-hit candidate set).
+// Plane distances are one fma each, t = fma(plane, 1/d, -o/d -/+ m), with a per-ray absolute
+// margin m_a = (4 M_a + 3 |o_a|) |1/d_a| 8u (M_a bounds every plane coordinate, u = 2^-24)
+// that exceeds the rounding of 1/d, -o/d and the fma together: near distances are rounded
+// down and far distances up, so a box is culled only when the exact test culls it.  Zero
+// direction components are replaced by a same-signed 1e-20 so every distance stays finite.
+// Triangle test = IntersectTriangle (shapes.cpp:172-273), bit for bit.
 
-struct RayPre {
-    V3 o, invDir;
-    int neg[3];
+struct CwRay {
+    V3 inv;     // 1 / d (zero components replaced by +-1e-20)
+    V3 oN, oF;  // -o * inv - m, -o * inv + m
+    int nOff[3], fOff[3];  // float4 index (within a wide node) of axis a's near / far planes
+    uint32_t oct;          // bit a: d_a < 0 (Bounds3 dirIsNeg)
 };
-
-template <typename F4>
-__device__ inline void SlabTest4(const F4 *__restrict__ q, int g, const RayPre &r, float raytMax, float tn[8],
-                                 unsigned *mask) {
-    // children 4g..4g+3: lox,loy,loz at float4 index 2a+g, hix,hiy,hiz at 6+2a+g
-    float4 L[3], H[3];
+__device__ inline CwRay MakeCwRay(V3 o, V3 d, const float *absMax) {
+    CwRay r;
+    auto safe = [](float x) { return fabsf(x) < 1e-20f ? copysignf(1e-20f, x) : x; };
+    r.inv = V3(1 / safe(d.x), 1 / safe(d.y), 1 / safe(d.z));
+    r.oct = (r.inv.x < 0 ? 1u : 0u) | (r.inv.y < 0 ? 2u : 0u) | (r.inv.z < 0 ? 4u : 0u);
+    constexpr float k8u = 8.f / 16777216.f;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        L[a] = q[2 * a + g];
-        H[a] = q[6 + 2 * a + g];
+        const float c = -o[a] * r.inv[a];
+        const float m = (4 * absMax[a] + 3 * fabsf(o[a])) * fabsf(r.inv[a]) * k8u;
+        r.oN[a] = c - m;
+        r.oF[a] = c + m;
+        const int neg = (r.oct >> a) & 1;
+        r.nOff[a] = 2 * a + 6 * neg;
+        r.fOff[a] = 2 * a + 6 * (1 - neg);
     }
-    const float slack = 1 + 2 * gamma(3);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        float lo[3], hi[3];
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            lo[a] = k == 0 ? L[a].x : k == 1 ? L[a].y : k == 2 ? L[a].z : L[a].w;
-            hi[a] = k == 0 ? H[a].x : k == 1 ? H[a].y : k == 2 ? H[a].z : H[a].w;
-        }
-        float nx = r.neg[0] ? hi[0] : lo[0], fx = r.neg[0] ? lo[0] : hi[0];
-        float ny = r.neg[1] ? hi[1] : lo[1], fy = r.neg[1] ? lo[1] : hi[1];
-        float nz = r.neg[2] ? hi[2] : lo[2], fz = r.neg[2] ? lo[2] : hi[2];
-        float tMin = (nx - r.o.x) * r.invDir.x;
-        float tMax = (fx - r.o.x) * r.invDir.x * slack;
-        float tyMin = (ny - r.o.y) * r.invDir.y;
-        float tyMax = (fy - r.o.y) * r.invDir.y * slack;
-        bool ok = !(tMin > tyMax || tyMin > tMax);
-        tMin = tyMin > tMin ? tyMin : tMin;
-        tMax = tyMax < tMax ? tyMax : tMax;
-        float tzMin = (nz - r.o.z) * r.invDir.z;
-        float tzMax = (fz - r.o.z) * r.invDir.z * slack;
-        ok = ok && !(tMin > tzMax || tzMin > tMax);
-        tMin = tzMin > tMin ? tzMin : tMin;
-        tMax = tzMax < tMax ? tzMax : tMax;
-        ok = ok && (tMin < raytMax) && (tMax > 0);
-        tn[4 * g + k] = tMin;
-        *mask |= ok ? (1u << (4 * g + k)) : 0u;
-    }
+    return r;
 }
 
-template <typename F4>
-__device__ inline void SlabTest8(const F4 *__restrict__ q, const RayPre &r, float raytMax, float tn[8],
-                                 unsigned *mask) {
-    *mask = 0;
-    SlabTest4(q, 0, r, raytMax, tn, mask);
-    SlabTest4(q, 1, r, raytMax, tn, mask);
+// IntersectTriangle with the ray's axis permutation applied once per ray: kz = the largest
+// |d| axis, (kx, ky, kz) a rotation, so permuting a vertex is a rotation by kz.  Triangles
+// cached in LDS are stored pre-rotated (three copies, one per kz); global ones are rotated here.
+struct TriRayR {
+    V3 o;  // permuted origin
+    float Sx, Sy, Sz;
+    int kz;
+};
+__device__ inline TriRayR MakeTriRayR(V3 o, V3 dir) {
+    const TriRay t = MakeTriRay(o, dir);
+    TriRayR r;
+    r.o = Permute(o, t.kx, t.ky, t.kz);
+    r.Sx = t.Sx, r.Sy = t.Sy, r.Sz = t.Sz;
+    r.kz = t.kz;
+    return r;
+}
+__device__ inline V3 RotateToRay(float4 v, int kz) {
+    // (v[kx], v[ky], v[kz]) with kx = kz + 1, ky = kz + 2 (mod 3)
+    return V3(kz == 0 ? v.y : (kz == 1 ? v.z : v.x), kz == 0 ? v.z : (kz == 1 ? v.x : v.y),
+              kz == 0 ? v.x : (kz == 1 ? v.y : v.z));
+}
+// shapes.cpp:180-273 on already permuted vertices (same arithmetic and order as
+// IntersectTriangleRay: p - o commutes with the permutation)
+__device__ inline bool IntersectTriangleRot(const TriRayR &r, float tMax, V3 p0t, V3 p1t, V3 p2t, TriHit *hit) {
+    p0t = p0t - r.o;
+    p1t = p1t - r.o;
+    p2t = p2t - r.o;
+    const float Sx = r.Sx, Sy = r.Sy, Sz = r.Sz;
+    p0t.x += Sx * p0t.z;
+    p0t.y += Sy * p0t.z;
+    p1t.x += Sx * p1t.z;
+    p1t.y += Sy * p1t.z;
+    p2t.x += Sx * p2t.z;
+    p2t.y += Sy * p2t.z;
+    float e0 = DifferenceOfProducts(p1t.x, p2t.y, p1t.y, p2t.x);
+    float e1 = DifferenceOfProducts(p2t.x, p0t.y, p2t.y, p0t.x);
+    float e2 = DifferenceOfProducts(p0t.x, p1t.y, p0t.y, p1t.x);
+    if (e0 == 0.0f || e1 == 0.0f || e2 == 0.0f) {
+        const EdgeFns e = EdgeFunctionsFP64(p0t, p1t, p2t);
+        e0 = e.e0, e1 = e.e1, e2 = e.e2;
+    }
+    if ((e0 < 0 || e1 < 0 || e2 < 0) && (e0 > 0 || e1 > 0 || e2 > 0)) return false;
+    const float det = e0 + e1 + e2;
+    if (det == 0) return false;
+    p0t.z *= Sz;
+    p1t.z *= Sz;
+    p2t.z *= Sz;
+    const float tScaled = e0 * p0t.z + e1 * p1t.z + e2 * p2t.z;
+    if (det < 0 && (tScaled >= 0 || tScaled < tMax * det)) return false;
+    if (det > 0 && (tScaled <= 0 || tScaled > tMax * det)) return false;
+    const float invDet = 1 / det;
+    const float b0 = e0 * invDet, b1 = e1 * invDet, b2 = e2 * invDet;
+    const float t = tScaled * invDet;
+    const float maxZt = MaxComponentValue(Abs(V3(p0t.z, p1t.z, p2t.z)));
+    const float deltaZ = gamma(3) * maxZt;
+    const float maxXt = MaxComponentValue(Abs(V3(p0t.x, p1t.x, p2t.x)));
+    const float maxYt = MaxComponentValue(Abs(V3(p0t.y, p1t.y, p2t.y)));
+    const float deltaX = gamma(5) * (maxXt + maxZt);
+    const float deltaY = gamma(5) * (maxYt + maxZt);
+    const float deltaE = 2 * (gamma(2) * maxXt * maxYt + deltaY * maxXt + deltaX * maxYt);
+    const float maxE = MaxComponentValue(Abs(V3(e0, e1, e2)));
+    const float deltaT = 3 * (gamma(3) * maxE * maxZt + deltaE * maxZt + deltaZ * maxE) * std::fabs(invDet);
+    if (t <= deltaT) return false;
+    hit->b0 = b0;
+    hit->b1 = b1;
+    hit->b2 = b2;
+    hit->t = t;
+    return true;
 }
 
-// Child references of a compressed node, decoded on demand for the children actually visited
-struct QRefs {
-    unsigned imask, meta[2];
+// Visit order bits: visit index i <-> slot i ^ oct, i.e. the slot mask with its index bits
+// XOR-permuted by oct (three conditional swaps).
+__device__ inline uint32_t PermuteOct(uint32_t m, uint32_t oct) {
+    m = (oct & 1u) ? (((m & 0x55u) << 1) | ((m >> 1) & 0x55u)) : m;
+    m = (oct & 2u) ? (((m & 0x33u) << 2) | ((m >> 2) & 0x33u)) : m;
+    m = (oct & 4u) ? (((m & 0x0fu) << 4) | ((m >> 4) & 0x0fu)) : m;
+    return m;
+}
+
+// One visited node's outcome
+struct NodeHits {
+    uint32_t inner;  // hit interior slots (slot order)
+    uint32_t tris;   // hit leaf triangles, bits relative to triBase
+    uint32_t imask;
     int childBase, triBase;
-    // the uncompressed encoding: >= 0 interior node, < 0 leaf ~(first << 3 | count - 1)
-    __device__ int Get(int c) const {
-        if ((imask >> c) & 1u) return childBase + __popc(imask & ((1u << c) - 1u));
-        const unsigned m = (meta[c >> 2] >> (8 * (c & 3))) & 0xffu;
-        const int first = triBase + (int)(m & 31u), count = (int)((m >> 5) & 3u) + 1;
-        return ~((first << 3) | (count - 1));
-    }
 };
 
-// Slab tests of a compressed node (BVH8QNode, 5 float4): child planes decoded as
-// fma(q, 2^(e-127), p) -- the expression the host rounded outward -- then the same test as
-// SlabTest4.
+// Wide node (BVH8Node): 12 plane float4 at q[0..11], header q[12] = {childBase, triBase, imask,
+// occ}, slot triangle masks q[13..14].  Near/far planes of 4 children are one float4 each.
 template <typename F4>
-__device__ inline void SlabTestQ(const F4 *__restrict__ q, const RayPre &r, float raytMax, float tn[8],
-                                 unsigned *mask, QRefs *refs) {
+__device__ inline NodeHits VisitWide(const F4 *__restrict__ q, const CwRay &r, float tMax) {
+    const float4 hdr = q[12], tm0 = q[13], tm1 = q[14];
+    NodeHits o;
+    o.childBase = __float_as_int(hdr.x);
+    o.triBase = __float_as_int(hdr.y);
+    o.imask = __float_as_uint(hdr.z);
+    uint32_t hit = 0, tris = 0;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        const float4 nx = q[r.nOff[0] + g], ny = q[r.nOff[1] + g], nz = q[r.nOff[2] + g];
+        const float4 fx = q[r.fOff[0] + g], fy = q[r.fOff[1] + g], fz = q[r.fOff[2] + g];
+        const float4 tm = g ? tm1 : tm0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            auto comp = [k](float4 v) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; };
+            const float tn = fmaxf(fmaxf(fmaf(comp(nx), r.inv.x, r.oN.x), fmaf(comp(ny), r.inv.y, r.oN.y)),
+                                   fmaxf(fmaf(comp(nz), r.inv.z, r.oN.z), 0.f));
+            const float tf = fminf(fminf(fmaf(comp(fx), r.inv.x, r.oF.x), fmaf(comp(fy), r.inv.y, r.oF.y)),
+                                   fminf(fmaf(comp(fz), r.inv.z, r.oF.z), tMax));
+            const bool ok = tn <= tf;
+            hit |= ok ? 1u << (4 * g + k) : 0u;
+            tris |= ok ? __float_as_uint(comp(tm)) : 0u;
+        }
+    }
+    o.inner = hit & o.imask;
+    o.tris = tris;
+    return o;
+}
+
+// Quantised node (BVH8QNode, 5 float4): child planes P = fma(q, 2^(e-127), p) -- the expression
+// the host rounded outward -- folded into the distance: t = fma(q, 2^(e-127) / d, (p - o) / d
+// -/+ m); the margin bound M_a covers the decoded planes too (DeviceScene::bvhAbsMax).
+template <typename F4>
+__device__ inline NodeHits VisitQuant(const F4 *__restrict__ q, const CwRay &r, float tMax) {
     const float4 f0 = q[0], f1 = q[1], f2 = q[2], f3 = q[3], f4 = q[4];
-    const unsigned eb = __float_as_uint(f0.w);
-    const float sx = __uint_as_float((eb & 0xffu) << 23), sy = __uint_as_float(((eb >> 8) & 0xffu) << 23),
-                sz = __uint_as_float(((eb >> 16) & 0xffu) << 23);
-    const unsigned imask = eb >> 24;
-    const int childBase = __float_as_int(f1.x), triBase = __float_as_int(f1.y);
-    const unsigned meta[2] = {__float_as_uint(f1.z), __float_as_uint(f1.w)};
-    const unsigned qw[12] = {__float_as_uint(f2.x), __float_as_uint(f2.y), __float_as_uint(f2.z),
+    const uint32_t eb = __float_as_uint(f0.w);
+    const V3 p(f0.x, f0.y, f0.z);
+    const V3 s(__uint_as_float((eb & 0xffu) << 23), __uint_as_float(((eb >> 8) & 0xffu) << 23),
+               __uint_as_float(((eb >> 16) & 0xffu) << 23));
+    NodeHits o;
+    o.imask = eb >> 24;
+    o.childBase = __float_as_int(f1.x);
+    o.triBase = __float_as_int(f1.y);
+    const uint32_t meta[2] = {__float_as_uint(f1.z), __float_as_uint(f1.w)};
+    // plane words: lo axis a children 4g.. at qw[2a + g], hi at qw[6 + 2a + g]
+    const uint32_t qw[12] = {__float_as_uint(f2.x), __float_as_uint(f2.y), __float_as_uint(f2.z),
                              __float_as_uint(f2.w), __float_as_uint(f3.x), __float_as_uint(f3.y),
                              __float_as_uint(f3.z), __float_as_uint(f3.w), __float_as_uint(f4.x),
                              __float_as_uint(f4.y), __float_as_uint(f4.z), __float_as_uint(f4.w)};
-    const float slack = 1 + 2 * gamma(3);
-    *mask = 0;
+    V3 A, BN, BF;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        const int w = c >> 2, sh = 8 * (c & 3);
-        auto byteOf = [&](int field) { return (float)((qw[2 * field + w] >> sh) & 0xffu); };
-        const float lo[3] = {fmaf(byteOf(0), sx, f0.x), fmaf(byteOf(1), sy, f0.y), fmaf(byteOf(2), sz, f0.z)};
-        const float hi[3] = {fmaf(byteOf(3), sx, f0.x), fmaf(byteOf(4), sy, f0.y), fmaf(byteOf(5), sz, f0.z)};
-        float nx = r.neg[0] ? hi[0] : lo[0], fx = r.neg[0] ? lo[0] : hi[0];
-        float ny = r.neg[1] ? hi[1] : lo[1], fy = r.neg[1] ? lo[1] : hi[1];
-        float nz = r.neg[2] ? hi[2] : lo[2], fz = r.neg[2] ? lo[2] : hi[2];
-        float tMin = (nx - r.o.x) * r.invDir.x;
-        float tMax = (fx - r.o.x) * r.invDir.x * slack;
-        float tyMin = (ny - r.o.y) * r.invDir.y;
-        float tyMax = (fy - r.o.y) * r.invDir.y * slack;
-        bool ok = !(tMin > tyMax || tyMin > tMax);
-        tMin = tyMin > tMin ? tyMin : tMin;
-        tMax = tyMax < tMax ? tyMax : tMax;
-        float tzMin = (nz - r.o.z) * r.invDir.z;
-        float tzMax = (fz - r.o.z) * r.invDir.z * slack;
-        ok = ok && !(tMin > tzMax || tzMin > tMax);
-        tMin = tzMin > tMin ? tzMin : tMin;
-        tMax = tzMax < tMax ? tzMax : tMax;
-        ok = ok && (tMin < raytMax) && (tMax > 0);
-        tn[c] = tMin;
-        *mask |= ok ? (1u << c) : 0u;
+    for (int a = 0; a < 3; ++a) {
+        A[a] = s[a] * r.inv[a];
+        BN[a] = fmaf(p[a], r.inv[a], r.oN[a]);
+        BF[a] = fmaf(p[a], r.inv[a], r.oF[a]);
     }
-    // occupied slots: interior (imask) or leaf (meta bit 7)
-    const unsigned leafBits = ((meta[0] >> 7) & 1u) | ((meta[0] >> 14) & 2u) | ((meta[0] >> 21) & 4u) |
-                              ((meta[0] >> 28) & 8u) | (((meta[1] >> 7) & 1u) << 4) | (((meta[1] >> 15) & 1u) << 5) |
-                              (((meta[1] >> 23) & 1u) << 6) | (((meta[1] >> 31) & 1u) << 7);
-    *mask &= imask | leafBits;
-    refs->imask = imask;
-    refs->meta[0] = meta[0];
-    refs->meta[1] = meta[1];
-    refs->childBase = childBase;
-    refs->triBase = triBase;
+    uint32_t hit = 0, tris = 0;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        uint32_t wn[3], wf[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const bool neg = (r.oct >> a) & 1u;
+            wn[a] = neg ? qw[6 + 2 * a + g] : qw[2 * a + g];
+            wf[a] = neg ? qw[2 * a + g] : qw[6 + 2 * a + g];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            auto byteOf = [k](uint32_t w) { return (float)((w >> (8 * k)) & 0xffu); };
+            const float tn = fmaxf(fmaxf(fmaf(byteOf(wn[0]), A.x, BN.x), fmaf(byteOf(wn[1]), A.y, BN.y)),
+                                   fmaxf(fmaf(byteOf(wn[2]), A.z, BN.z), 0.f));
+            const float tf = fminf(fminf(fmaf(byteOf(wf[0]), A.x, BF.x), fmaf(byteOf(wf[1]), A.y, BF.y)),
+                                   fminf(fmaf(byteOf(wf[2]), A.z, BF.z), tMax));
+            const bool ok = tn <= tf;
+            const uint32_t m = (meta[g] >> (8 * k)) & 0xffu;
+            hit |= ok ? 1u << (4 * g + k) : 0u;
+            tris |= ok ? ((1u << (m >> 5)) - 1u) << (m & 31u) : 0u;
+        }
+    }
+    o.inner = hit & o.imask;
+    o.tris = tris;
+    return o;
 }
 
-// Scene cache in LDS: the first S.ldsNodes BVH8 nodes (BFS order = the top of the tree) at a
-// 17-float4 stride and the first S.ldsTris triangles of the leaf order.  The 68-dword node
-// stride puts the same field of 16 different nodes in 16 different 4-bank groups, so the
-// ds_read_b128 lane groups stay conflict-free when lanes sit in different nodes; the 12-dword
-// triangle stride does the same for triangles.  Everything else is read from global memory.
-// (strides: kLdsNodeStride / kLdsQNodeStride, device.h)
-
+// Scene cache in LDS: the group stack ([stackSize][kBlock] uint2), the first S.ldsNodes BVH8
+// nodes (BFS order = the top of the tree) at a 17-float4 (wide) / 5-float4 (quantised) stride,
+// and -- when every node and triangle fits -- all triangles in three pre-rotated copies
+// ([kz][tri][vertex], vertex = (p[kx], p[ky], p[kz], 0)).  The 68-dword wide stride puts the
+// same field of 16 nodes in 16 different 4-bank groups, so ds_read_b128 lane groups stay
+// conflict-free when lanes sit in different nodes.
 // LDS-qualified pointers keep the cached and the global paths distinct instructions
 // (ds_read_b128 vs global_load_dwordx4); generic pointers would merge them into flat loads.
 #if defined(__HIP_DEVICE_COMPILE__)
 typedef __attribute__((address_space(3))) const float4 LdsF4;
+typedef __attribute__((address_space(3))) uint2 LdsU2;
 #else
 typedef const float4 LdsF4;  // host pass only parses the kernels
+typedef uint2 LdsU2;
 #endif
 struct SceneLds {
-    int *stack;          // [stackSize][blockDim]
-    const LdsF4 *nodes;  // [ldsNodes][17]
-    const LdsF4 *tris;   // [ldsTris][3]
+    LdsU2 *stack;        // [stackSize][blockDim]
+    const LdsF4 *nodes;  // [ldsNodes][stride]
+    const LdsF4 *tris;   // [3][ldsTris][3]
 };
 
 // Lays out the dynamic LDS of a traversal kernel and fills the cache (whole block, one sync).
 __device__ inline SceneLds SetupSceneLds(const DeviceScene &S, float4 *dyn) {
     SceneLds L;
-    L.stack = reinterpret_cast<int *>(dyn);
-    float4 *nodes = dyn + (S.stackSize * kBlock) / 4;
+    L.stack = (LdsU2 *)reinterpret_cast<uint2 *>(dyn);
+    float4 *nodes = dyn + (S.stackSize * kBlock) / 2;
     float4 *tris = nodes + S.ldsNodes * LdsNodeStride(S.compressed);
     // plain copies: measured faster here than per-node LDS-DMA (few, tiny rows)
     if (S.compressed) {
@@ -467,151 +554,103 @@ __device__ inline SceneLds SetupSceneLds(const DeviceScene &S, float4 *dyn) {
         for (int i = threadIdx.x; i < S.ldsNodes * kLdsQNodeStride; i += blockDim.x) nodes[i] = gn[i];
     } else {
         const float4 *gn = reinterpret_cast<const float4 *>(S.nodes);
-        for (int i = threadIdx.x; i < S.ldsNodes * 14; i += blockDim.x) {
-            int n = i / 14, k = i - n * 14;
+        for (int i = threadIdx.x; i < S.ldsNodes * 15; i += blockDim.x) {
+            const int n = i / 15, k = i - n * 15;
             nodes[n * kLdsNodeStride + k] = gn[n * 16 + k];
         }
     }
-    for (int i = threadIdx.x; i < S.ldsTris * 3; i += blockDim.x) tris[i] = S.triVerts[i];
+    for (int i = threadIdx.x; i < S.ldsTris * 9; i += blockDim.x) {
+        const int rot = i / (S.ldsTris * 3), e = i - rot * (S.ldsTris * 3);
+        const V3 v = RotateToRay(S.triVerts[e], rot);
+        tris[i] = make_float4(v.x, v.y, v.z, 0.f);
+    }
     __syncthreads();
     L.nodes = (const LdsF4 *)nodes;
     L.tris = (const LdsF4 *)tris;
     return L;
 }
 
-// TrisInLds: every triangle is cached (a launch-uniform choice, so no per-lane branch whose
-// two loads the compiler would merge into one flat load).
-template <bool AnyHit, bool TrisInLds, bool Compressed>
-__device__ inline int TraverseT(const DeviceScene &S, const SceneLds &L, V3 o, V3 d, float tMax, TriHit *best) {
-    const TriRay tr = MakeTriRay(o, d);
-    RayPre r;
-    r.o = o;
-    r.invDir = V3(1 / d.x, 1 / d.y, 1 / d.z);
-    r.neg[0] = r.invDir.x < 0;
-    r.neg[1] = r.invDir.y < 0;
-    r.neg[2] = r.invDir.z < 0;
-    const int lane = threadIdx.x, stride = blockDim.x;
-    int *lds = L.stack;
-    int sp = 0;
-    int node = 0;
-    int hitPrim = -1;
+// NodesInLds / TrisInLds: every node / triangle is cached (launch-uniform choices, so no per-lane
+// branch whose two loads the compiler would merge into one flat load).
+template <bool AnyHit, bool Compressed, bool NodesInLds, bool TrisInLds>
+__device__ inline int TraverseCW(const DeviceScene &S, const SceneLds &L, V3 o, V3 d, float tMax, TriHit *best) {
+    const TriRayR tr = MakeTriRayR(o, d);
+    const CwRay r = MakeCwRay(o, d, S.bvhAbsMax);
+    LdsU2 *stk = L.stack + threadIdx.x;
+    int sp = 0, node = 0, hitPrim = -1;
     while (true) {
-        float tn[8];
-        unsigned mask;
-        int ch[8];
-        QRefs qr;
+        NodeHits nh;
         if constexpr (Compressed) {
-            if (node < S.ldsNodes) SlabTestQ(L.nodes + node * kLdsQNodeStride, r, tMax, tn, &mask, &qr);
-            else SlabTestQ(reinterpret_cast<const float4 *>(S.qnodes + node), r, tMax, tn, &mask, &qr);
+            if (NodesInLds || node < S.ldsNodes) nh = VisitQuant(L.nodes + node * kLdsQNodeStride, r, tMax);
+            else nh = VisitQuant(reinterpret_cast<const float4 *>(S.qnodes + node), r, tMax);
         } else {
-            int4 ch0, ch1;
-            if (node < S.ldsNodes) {
-                const LdsF4 *q = L.nodes + node * kLdsNodeStride;
-                SlabTest8(q, r, tMax, tn, &mask);
-                float4 c0 = q[12], c1 = q[13];
-                ch0 = make_int4(__float_as_int(c0.x), __float_as_int(c0.y), __float_as_int(c0.z), __float_as_int(c0.w));
-                ch1 = make_int4(__float_as_int(c1.x), __float_as_int(c1.y), __float_as_int(c1.z), __float_as_int(c1.w));
+            if (NodesInLds || node < S.ldsNodes) nh = VisitWide(L.nodes + node * kLdsNodeStride, r, tMax);
+            else nh = VisitWide(reinterpret_cast<const float4 *>(S.nodes + node), r, tMax);
+        }
+        // the node's hit leaf triangles, in leaf order
+        uint32_t tris = nh.tris;
+        while (tris) {
+            const int t = nh.triBase + __builtin_ctz(tris);
+            tris &= tris - 1u;
+            V3 a, b, c;
+            if constexpr (TrisInLds) {
+                const LdsF4 *v = L.tris + (tr.kz * S.ldsTris + t) * 3;
+                const float4 va = v[0], vb = v[1], vc = v[2];
+                a = V3(va.x, va.y, va.z), b = V3(vb.x, vb.y, vb.z), c = V3(vc.x, vc.y, vc.z);
             } else {
-                const BVH8Node *np = S.nodes + node;
-                SlabTest8(reinterpret_cast<const float4 *>(np), r, tMax, tn, &mask);
-                ch0 = reinterpret_cast<const int4 *>(np->child)[0];
-                ch1 = reinterpret_cast<const int4 *>(np->child)[1];
+                a = RotateToRay(S.triVerts[3 * t], tr.kz);
+                b = RotateToRay(S.triVerts[3 * t + 1], tr.kz);
+                c = RotateToRay(S.triVerts[3 * t + 2], tr.kz);
             }
-            ch[0] = ch0.x, ch[1] = ch0.y, ch[2] = ch0.z, ch[3] = ch0.w;
-            ch[4] = ch1.x, ch[5] = ch1.y, ch[6] = ch1.z, ch[7] = ch1.w;
-        }
-        // empty slots fail the slab test (inverted box / masked compressed slot)
-        unsigned leaves = 0, inner = 0;
-        if constexpr (Compressed) {
-            inner = mask & qr.imask;
-            leaves = mask & ~qr.imask;
-        } else {
-#pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                if (mask & (1u << c)) {
-                    if (ch[c] < 0) leaves |= 1u << c;
-                    else inner |= 1u << c;
-                }
+            TriHit h;
+            if (IntersectTriangleRot(tr, tMax, a, b, c, &h)) {
+                if (AnyHit) return t;
+                tMax = h.t;
+                *best = h;
+                hitPrim = t;
             }
         }
-        // leaves nearest-first
-        while (leaves) {
-            int bc = 0;
-            float bt = kInfinity;
-#pragma unroll
-            for (int c = 0; c < 8; ++c)
-                if ((leaves & (1u << c)) && tn[c] <= bt) {
-                    bt = tn[c];
-                    bc = c;
-                }
-            leaves &= ~(1u << bc);
-            if (bt >= tMax) continue;
-            int enc = 0;
-            if constexpr (Compressed) {
-                enc = ~qr.Get(bc);
-            } else {
-#pragma unroll
-                for (int c = 0; c < 8; ++c) enc = (c == bc) ? ~ch[c] : enc;
-            }
-            int first = enc >> 3, count = (enc & 7) + 1;
-            for (int t = first; t < first + count; ++t) {
-                float4 a, b, c;
-                if (TrisInLds) {
-                    a = L.tris[3 * t];
-                    b = L.tris[3 * t + 1];
-                    c = L.tris[3 * t + 2];
-                } else {
-                    a = S.triVerts[3 * t];
-                    b = S.triVerts[3 * t + 1];
-                    c = S.triVerts[3 * t + 2];
-                }
-                TriHit h;
-                if (IntersectTriangleRay(tr, tMax, V3(a.x, a.y, a.z), V3(b.x, b.y, b.z), V3(c.x, c.y, c.z), &h)) {
-                    if (AnyHit) return t;
-                    tMax = h.t;
-                    *best = h;
-                    hitPrim = t;
-                }
-            }
+        // next node: the nearest child of this node's group, else of the top stacked group
+        uint32_t bits = PermuteOct(nh.inner, r.oct), gBase = (uint32_t)nh.childBase, gMask = nh.imask;
+        if (bits == 0) {
+            if (sp == 0) break;
+            --sp;
+            const uint2 e = stk[sp * kBlock];
+            gBase = e.x;
+            gMask = e.y >> 8;
+            bits = e.y & 0xffu;
         }
-        // interior children farthest-first onto the stack (closest popped next)
-        while (inner) {
-            int bc = 0;
-            float bt = -kInfinity;
-#pragma unroll
-            for (int c = 0; c < 8; ++c)
-                if ((inner & (1u << c)) && tn[c] >= bt) {
-                    bt = tn[c];
-                    bc = c;
-                }
-            inner &= ~(1u << bc);
-            if (bt >= tMax) continue;
-            int child = 0;
-            if constexpr (Compressed) {
-                child = qr.Get(bc);
-            } else {
-#pragma unroll
-                for (int c = 0; c < 8; ++c) child = (c == bc) ? ch[c] : child;
-            }
-            lds[(sp++) * stride + lane] = child;  // sp < S.stackSize by construction
+        const uint32_t slot = (uint32_t)__builtin_ctz(bits) ^ r.oct;
+        bits &= bits - 1u;
+        node = (int)gBase + __popc(gMask & ((1u << slot) - 1u));
+        if (bits) {
+            stk[sp * kBlock] = make_uint2(gBase, (gMask << 8) | bits);  // sp < S.stackSize by construction
+            ++sp;
         }
-        if (sp == 0) break;
-        node = lds[(--sp) * stride + lane];
     }
     return hitPrim;
 }
 
-// Q: the launch's node format (a kernel template parameter, so each kernel carries only the
-// traversal loops of its own format)
-template <bool AnyHit, bool Q>
-__device__ inline int Traverse(const DeviceScene &S, const SceneLds &L, V3 o, V3 d, float tMax, TriHit *best) {
-    if constexpr (Q) {
-        return TraverseT<AnyHit, false, true>(S, L, o, d, tMax, best);
-    } else {
-        if (S.ldsTris > 0) return TraverseT<AnyHit, true, false>(S, L, o, d, tMax, best);
-        return TraverseT<AnyHit, false, false>(S, L, o, d, tMax, best);
-    }
+// Traversal modes, one kernel instantiation each (a launch-uniform choice, so every kernel
+// carries exactly one traversal loop): every node and triangle in LDS (small scenes); wide
+// nodes with the top of the tree in LDS; quantised nodes (PBRT_AMD_BVH=compressed).
+constexpr int kTravLds = 0, kTravWide = 1, kTravQuant = 2;
+inline int TraversalMode(const DeviceScene &S) {
+    return S.compressed ? kTravQuant : (S.ldsTris > 0 ? kTravLds : kTravWide);
 }
+template <bool AnyHit, int TM>
+__device__ inline int Traverse(const DeviceScene &S, const SceneLds &L, V3 o, V3 d, float tMax, TriHit *best) {
+    return TraverseCW<AnyHit, TM == kTravQuant, TM == kTravLds, TM == kTravLds>(S, L, o, d, tMax, best);
+}
+// Launches kernel template K<..., TM> with the scene's traversal mode
+#define PBRT_LAUNCH_TRAVERSAL(S, KERNEL, ...)                                                   \
+    do {                                                                                        \
+        switch (TraversalMode(S)) {                                                             \
+        case kTravLds: hipLaunchKernelGGL((KERNEL(kTravLds)), __VA_ARGS__); break;              \
+        case kTravWide: hipLaunchKernelGGL((KERNEL(kTravWide)), __VA_ARGS__); break;            \
+        default: hipLaunchKernelGGL((KERNEL(kTravQuant)), __VA_ARGS__); break;                  \
+        }                                                                                       \
+    } while (0)
 
 // ------------------------------------------------------------------ lights
 struct LightSample {

@@ -64,7 +64,7 @@ PHD int CounterIndex(int depth, int queue, int shard) {
 }
 // device stats slots: [0..7] ray counters, [16..47] per-section wave cycles (profiling build)
 constexpr int kStatsSlots = 48, kStatsSectionBase = 16;
-constexpr int kMaxStackSize = 64;  // traversal stack entries per lane (64 KB of LDS per block)
+constexpr int kMaxStackSize = 32;  // traversal stack entries per lane (uint2: 64 KB of LDS per block)
 constexpr int kSceneLdsBudget = 16 * 1024;  // bytes of BVH nodes + triangles cached in LDS per block
 constexpr int kLdsNodeStride = 17;  // float4 per LDS-cached wide node (68 dwords: conflict-free)
 constexpr int kLdsQNodeStride = 5;  // float4 per LDS-cached compressed node (20 dwords: conflict-free)
@@ -168,7 +168,8 @@ struct DeviceScene {
     const uint8_t (*zsPerms)[4];  // [24][4]
     const uint32_t *sobolM1;      // Sobol' dimension-1 matrix rows [52]
     int maxDepth;
-    int stackSize;  // BVH traversal stack entries per lane (BVH8::maxStack)
+    int stackSize;  // BVH traversal stack entries (uint2 groups) per lane (BVH8::maxStack)
+    float bvhAbsMax[3];  // bound on |plane coordinate| per axis (traversal box-test margins)
     int ldsNodes, ldsTris;  // BVH8 nodes / triangles cached in LDS by the traversal kernels
     ShadeLdsLayout shadeLds;
     DeviceMedia media;

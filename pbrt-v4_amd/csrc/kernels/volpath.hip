@@ -534,7 +534,7 @@ __global__ void __launch_bounds__(kBlock) k_vcamera(DeviceScene S, PathState st,
     r.medium[slot] = S.media.cameraMedium;
 }
 
-template <bool Q>
+template <int TM>
 __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_vclosest(DeviceScene S, PathState st, VolState v,
                                                                           int wf, int timed) {
     const QueueView rays = LoadQueue(st, wf, kVRay);
@@ -558,7 +558,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_vclosest(Devic
         if (active) {
             const V3 o = LoadV3(rec.ray, NR, ri), d = LoadV3(rec.ray + 3 * (size_t)NR, NR, ri);
             TriHit h;
-            const int prim = Traverse<false, Q>(S, L, o, d, kInfinity, &h);
+            const int prim = Traverse<false, TM>(S, L, o, d, kInfinity, &h);
             v.hitPrim[ri] = prim;
             v.hitB[ri] = h.b0;
             v.hitB[NR + ri] = h.b1;
@@ -1732,7 +1732,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vscatter(DeviceScene
 // TraceTransmittance (wavefront/intersect.h:164-274): closest hits up to the light; a
 // non-interface surface blocks, interfaces are crossed (SpawnRayTo the light point), and in
 // each medium T_ray / r_u / r_l follow ratio tracking with RR on a small T_ray.
-template <bool Q>
+template <int TM>
 __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vshadow(DeviceScene S, PathState st, VolState v, int wf) {
     const QueueView sh = LoadQueue(st, wf, kVShadow);
     if ((int)(blockIdx.x * blockDim.x) >= sh.total) return;
@@ -1755,7 +1755,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vshadow(DeviceScene 
         for (int guard = 0; guard < 256; ++guard) {
             if (d == V3(0, 0, 0)) break;
             TriHit h;
-            const int hp = Traverse<false, Q>(S, L, o, d, tMax, &h);
+            const int hp = Traverse<false, TM>(S, L, o, d, tMax, &h);
             if (hp >= 0 && S.matType[S.primMaterial[hp]] != 3) {
                 blocked = true;
                 break;
@@ -1844,7 +1844,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vshadow(DeviceScene 
 // TraceTransmittance when every medium is grey: T_ray, r_u and r_l start at 1 and only ever
 // take factors that are equal at all wavelengths, so each is one scalar (the reference's 31
 // entries are 31 copies of it).
-template <bool Q>
+template <int TM>
 __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_vshadow_grey(DeviceScene S, PathState st, VolState v,
                                                                              int wf) {
     const QueueView sh = LoadQueue(st, wf, kVShadow);
@@ -1866,7 +1866,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_vshadow_grey(D
         for (int guard = 0; guard < 256; ++guard) {
             if (d == V3(0, 0, 0)) break;
             TriHit h;
-            const int hp = Traverse<false, Q>(S, L, o, d, tMax, &h);
+            const int hp = Traverse<false, TM>(S, L, o, d, tMax, &h);
             if (hp >= 0 && S.matType[S.primMaterial[hp]] != 3) {
                 blocked = true;
                 break;
@@ -1955,8 +1955,9 @@ hipError_t LaunchVolCamera(const DeviceScene &S, const PathState &st, const VolS
 hipError_t LaunchVolClosest(const DeviceScene &S, const PathState &st, const VolState &v, int wf, int maxCount,
                             int timed, hipStream_t s) {
     const dim3 block(kBlock), gT(VolGrid(maxCount, 1024));
-    if (S.compressed) hipLaunchKernelGGL(k_vclosest<true>, gT, block, VolStackBytes(S), s, S, st, v, wf, timed);
-    else hipLaunchKernelGGL(k_vclosest<false>, gT, block, VolStackBytes(S), s, S, st, v, wf, timed);
+#define K_VCLOSEST(tm) k_vclosest<tm>
+    PBRT_LAUNCH_TRAVERSAL(S, K_VCLOSEST, gT, block, VolStackBytes(S), s, S, st, v, wf, timed);
+#undef K_VCLOSEST
     return hipGetLastError();
 }
 // the rest of wavefront iteration wf after its closest-hit launch
@@ -1972,11 +1973,13 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
         hipLaunchKernelGGL(k_vlayered, gW, block, 0, s, S, st, v, wf);
     hipLaunchKernelGGL(k_vscatter, gW, block, 0, s, S, st, v, wf);
     if (S.media.allGrey) {
-        if (S.compressed) hipLaunchKernelGGL(k_vshadow_grey<true>, gT, block, VolStackBytes(S), s, S, st, v, wf);
-        else hipLaunchKernelGGL(k_vshadow_grey<false>, gT, block, VolStackBytes(S), s, S, st, v, wf);
+#define K_VSHADOW_GREY(tm) k_vshadow_grey<tm>
+        PBRT_LAUNCH_TRAVERSAL(S, K_VSHADOW_GREY, gT, block, VolStackBytes(S), s, S, st, v, wf);
+#undef K_VSHADOW_GREY
     } else {
-        if (S.compressed) hipLaunchKernelGGL(k_vshadow<true>, gT, block, VolStackBytes(S), s, S, st, v, wf);
-        else hipLaunchKernelGGL(k_vshadow<false>, gT, block, VolStackBytes(S), s, S, st, v, wf);
+#define K_VSHADOW(tm) k_vshadow<tm>
+        PBRT_LAUNCH_TRAVERSAL(S, K_VSHADOW, gT, block, VolStackBytes(S), s, S, st, v, wf);
+#undef K_VSHADOW
     }
     return hipGetLastError();
 }

@@ -49,7 +49,7 @@ __global__ void __launch_bounds__(kBlock) k_camera(DeviceScene S, PathState st, 
 }
 
 // NMatQ = 1: every material is diffuse (one material queue); 3: one queue per material type
-template <int NMatQ, bool Q>
+template <int NMatQ, int TM>
 __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_closest(DeviceScene S, PathState st, int depth, int timed) {
     const QueueView rays = LoadQueue(st, depth, kCntRay);
     if ((int)(blockIdx.x * blockDim.x) >= rays.total) return;  // no work
@@ -88,7 +88,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_closest(Device
         if (active) {
             const V3 o(rec.ray[qi], rec.ray[N + qi], rec.ray[2 * N + qi]);
             const V3 d(rec.ray[3 * N + qi], rec.ray[4 * N + qi], rec.ray[5 * N + qi]);
-            prim = Traverse<false, Q>(S, L, o, d, kInfinity, &h);
+            prim = Traverse<false, TM>(S, L, o, d, kInfinity, &h);
             if (prim >= 0) {
                 hitPrim[qi] = prim;
                 hitB[qi] = h.b0;
@@ -832,7 +832,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
     }
 }
 
-template <bool Q>
+template <int TM>
 __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_shadow(DeviceScene S, PathState st, int depth) {
     const QueueView shadows = LoadQueue(st, depth, kCntShadow);
     if ((int)(blockIdx.x * blockDim.x) >= shadows.total) return;  // no work
@@ -847,7 +847,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_shadow(DeviceS
         V3 o(st.shadowRay[p], st.shadowRay[N + p], st.shadowRay[2 * N + p]);
         V3 d(st.shadowRay[3 * N + p], st.shadowRay[4 * N + p], st.shadowRay[5 * N + p]);
         TriHit h;
-        int hit = Traverse<true, Q>(S, L, o, d, 1 - kShadowEpsilon, &h);
+        int hit = Traverse<true, TM>(S, L, o, d, 1 - kShadowEpsilon, &h);
         if (hit < 0) {
             const int slot = st.shadowPixel[p];
             st.L[slot] += st.shadowL[p];
@@ -886,7 +886,7 @@ __global__ void __launch_bounds__(kBlock) k_film(DeviceScene S, PathState st, in
 // ------------------------------------------------------------------ stand-alone intersection
 // The WavefrontAggregate boundary exposed on its own (integrator.h:32-54): closest / any hit
 // for an SoA ray batch, used by parity tests and the traversal benchmark.
-template <bool Q>
+template <int TM>
 __global__ void __launch_bounds__(kBlock, 4) k_intersect_batch(DeviceScene S, const float *rays, int n, int anyHit,
                                                               int *outPrim, float *outHit) {
     extern __shared__ float4 dynLds[];
@@ -896,7 +896,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_intersect_batch(DeviceScene S, co
         V3 d(rays[3 * n + i], rays[4 * n + i], rays[5 * n + i]);
         float tMax = rays[6 * n + i];
         TriHit h{0, 0, 0, 0};
-        int prim = anyHit ? Traverse<true, Q>(S, L, o, d, tMax, &h) : Traverse<false, Q>(S, L, o, d, tMax, &h);
+        int prim = anyHit ? Traverse<true, TM>(S, L, o, d, tMax, &h) : Traverse<false, TM>(S, L, o, d, tMax, &h);
         outPrim[i] = prim;
         outHit[i] = h.b0;
         outHit[n + i] = h.b1;
@@ -907,8 +907,9 @@ __global__ void __launch_bounds__(kBlock, 4) k_intersect_batch(DeviceScene S, co
 
 // ------------------------------------------------------------------ launch helpers (host)
 size_t TraversalLdsBytes(int stackSize, int ldsNodes, int ldsTris, int compressed) {
-    return (size_t)stackSize * kBlock * sizeof(int) + (size_t)ldsNodes * LdsNodeStride(compressed) * 16 +
-           (size_t)ldsTris * 48;
+    // group stack (uint2 entries), cached nodes, cached triangles in three pre-rotated copies
+    return (size_t)stackSize * kBlock * sizeof(uint2) + (size_t)ldsNodes * LdsNodeStride(compressed) * 16 +
+           (size_t)ldsTris * 3 * 48;
 }
 static size_t StackBytes(const DeviceScene &S) {
     return TraversalLdsBytes(S.stackSize, S.ldsNodes, S.ldsTris, S.compressed);
@@ -951,13 +952,12 @@ hipError_t LaunchClosest(const DeviceScene &S, const PathState &st, int depth, i
                          hipStream_t s) {
     const dim3 grid(TraversalGridFor(maxCount)), block(kBlock);
     const bool multi = S.matTypeMask & ~1;
-    if (S.compressed) {
-        if (multi) hipLaunchKernelGGL((k_closest<kNumMatTypes, true>), grid, block, StackBytes(S), s, S, st, depth, timed);
-        else hipLaunchKernelGGL((k_closest<1, true>), grid, block, StackBytes(S), s, S, st, depth, timed);
-    } else {
-        if (multi) hipLaunchKernelGGL((k_closest<kNumMatTypes, false>), grid, block, StackBytes(S), s, S, st, depth, timed);
-        else hipLaunchKernelGGL((k_closest<1, false>), grid, block, StackBytes(S), s, S, st, depth, timed);
-    }
+#define K_CLOSEST_MULTI(tm) k_closest<kNumMatTypes, tm>
+#define K_CLOSEST_ONE(tm) k_closest<1, tm>
+    if (multi) PBRT_LAUNCH_TRAVERSAL(S, K_CLOSEST_MULTI, grid, block, StackBytes(S), s, S, st, depth, timed);
+    else PBRT_LAUNCH_TRAVERSAL(S, K_CLOSEST_ONE, grid, block, StackBytes(S), s, S, st, depth, timed);
+#undef K_CLOSEST_MULTI
+#undef K_CLOSEST_ONE
     return hipGetLastError();
 }
 hipError_t LaunchEscaped(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s) {
@@ -984,10 +984,9 @@ hipError_t LaunchShadeMicrofacet(const DeviceScene &S, const PathState &st, int 
     return hipGetLastError();
 }
 hipError_t LaunchShadow(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s) {
-    if (S.compressed)
-        hipLaunchKernelGGL(k_shadow<true>, dim3(TraversalGridFor(maxCount)), dim3(kBlock), StackBytes(S), s, S, st, depth);
-    else
-        hipLaunchKernelGGL(k_shadow<false>, dim3(TraversalGridFor(maxCount)), dim3(kBlock), StackBytes(S), s, S, st, depth);
+#define K_SHADOW(tm) k_shadow<tm>
+    PBRT_LAUNCH_TRAVERSAL(S, K_SHADOW, dim3(TraversalGridFor(maxCount)), dim3(kBlock), StackBytes(S), s, S, st, depth);
+#undef K_SHADOW
     return hipGetLastError();
 }
 hipError_t LaunchFilm(const DeviceScene &S, const PathState &st, int nSamples, hipStream_t s) {
@@ -996,12 +995,10 @@ hipError_t LaunchFilm(const DeviceScene &S, const PathState &st, int nSamples, h
 }
 hipError_t LaunchIntersectBatch(const DeviceScene &S, const float *rays, int n, int anyHit, int *outPrim,
                                 float *outHit, hipStream_t s) {
-    if (S.compressed)
-        hipLaunchKernelGGL(k_intersect_batch<true>, dim3(TraversalGridFor(n)), dim3(kBlock), StackBytes(S), s, S, rays,
-                           n, anyHit, outPrim, outHit);
-    else
-        hipLaunchKernelGGL(k_intersect_batch<false>, dim3(TraversalGridFor(n)), dim3(kBlock), StackBytes(S), s, S, rays,
-                           n, anyHit, outPrim, outHit);
+#define K_BATCH(tm) k_intersect_batch<tm>
+    PBRT_LAUNCH_TRAVERSAL(S, K_BATCH, dim3(TraversalGridFor(n)), dim3(kBlock), StackBytes(S), s, S, rays, n, anyHit,
+                          outPrim, outHit);
+#undef K_BATCH
     return hipGetLastError();
 }
 

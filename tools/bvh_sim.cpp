@@ -50,7 +50,7 @@ static int TraverseSim(const BVH8 &b, V3 o, V3 d, float tMax, bool anyHit, Cost 
         }
         unsigned leaves = 0, inner = 0;
         for (int k = 0; k < 8; ++k)
-            if (mask >> k & 1) (n.child[k] < 0 ? leaves : inner) |= 1u << k;
+            if (mask >> k & 1) (b.childRef[node][k] < 0 ? leaves : inner) |= 1u << k;
         while (leaves) {
             int bc = 0;
             float bt = kInfinity;
@@ -59,7 +59,7 @@ static int TraverseSim(const BVH8 &b, V3 o, V3 d, float tMax, bool anyHit, Cost 
             leaves &= ~(1u << bc);
             if (bt >= tMax) continue;
             c->leaves++;
-            int enc = ~n.child[bc], first = enc >> 3, count = (enc & 7) + 1;
+            int enc = ~b.childRef[node][bc], first = enc >> 3, count = (enc & 7) + 1;
             for (int t = first; t < first + count; ++t) {
                 c->tris++;
                 const float *v = &b.triVerts[12 * t];
@@ -79,7 +79,7 @@ static int TraverseSim(const BVH8 &b, V3 o, V3 d, float tMax, bool anyHit, Cost 
                 if ((inner >> k & 1) && tn[k] >= bt) bt = tn[k], bc = k;
             inner &= ~(1u << bc);
             if (bt >= tMax) continue;
-            stack.push_back(n.child[bc]);
+            stack.push_back(b.childRef[node][bc]);
         }
         if (stack.empty()) break;
         node = stack.back();

@@ -190,6 +190,12 @@ int pbrt_intersect(pbrt_context *ctx, const float *rays_dev, int n, int any_hit,
 
 /* host-side evaluation of product components (no GPU): used by golden-vector tests */
 float pbrt_debug_halton(const pbrt_scene *scene, int px, int py, int sample_index, int dim);
+/* Halton fast path check: ScrambledRadicalInverse of the scene's dimension dim (its digit
+ * permutations) by the kernels' 24-bit float-reciprocal digit loop against the 64-bit
+ * restatement of util/lowdiscrepancy.h:115-134, for a = a0, a0 + step, ... < a1 (a1 <= 2^24);
+ * returns the number of indices whose floats differ (bitwise), or -1 on error */
+int64_t pbrt_debug_halton_fastpath_mismatches(const pbrt_scene *scene, int dim, uint32_t a0, uint32_t a1,
+                                              uint32_t step);
 int pbrt_debug_rgb_coeffs(float r, float g, float b, float *coeffs3);
 int pbrt_debug_rgb2spec_column(int maxc, int j, int i, float *out192);
 /* Filter::Sample(u) of the scene's pixel filter (FilterSampler over PiecewiseConstant2D for

@@ -179,6 +179,12 @@ struct DevBuf {
 struct pbrt_context {
     int device = 0;
     hipStream_t stream = nullptr;
+    // side stream for the short emission kernels (HandleEmissiveIntersection / HandleEscapedRays):
+    // they are latency-bound on small queues and independent of the same depth's material
+    // stage, so they run beside it; per depth, eClosest orders them after the closest-hit
+    // launch and eEmit orders the shadow stage (which also adds to L) after them
+    hipStream_t sideStream = nullptr;
+    std::vector<hipEvent_t> eClosest, eEmit;
     SceneDesc desc;
     BVH8 bvh;
     DeviceScene S{};
@@ -227,6 +233,9 @@ struct pbrt_context {
             (void)hipEventDestroy(e.first);
             (void)hipEventDestroy(e.second);
         }
+        for (hipEvent_t e : eClosest) (void)hipEventDestroy(e);
+        for (hipEvent_t e : eEmit) (void)hipEventDestroy(e);
+        if (sideStream) (void)hipStreamDestroy(sideStream);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -235,6 +244,13 @@ static void BuildDevice(pbrt_context *c) {
     SceneDesc &s = c->desc;
     HIPCHECK(hipSetDevice(c->device));
     HIPCHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHECK(hipStreamCreateWithFlags(&c->sideStream, hipStreamNonBlocking));
+    c->eClosest.resize(s.maxDepth + 1);
+    c->eEmit.resize(s.maxDepth + 1);
+    for (int d = 0; d <= s.maxDepth; ++d) {
+        HIPCHECK(hipEventCreateWithFlags(&c->eClosest[d], hipEventDisableTiming));
+        HIPCHECK(hipEventCreateWithFlags(&c->eEmit[d], hipEventDisableTiming));
+    }
     c->bvh = BuildBVH8(s.verts, s.tris, 4);
     if (c->bvh.maxStack > kMaxStackSize)
         throw Error("BVH needs a " + std::to_string(c->bvh.maxStack) + "-entry traversal stack (limit " +
@@ -816,15 +832,27 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
                 if (timed) RecordEvent(c, true);
                 HIPCHECK(LaunchClosest(c->S, st, depth, (int)nActive, timed ? 1 : 0, c->stream));
                 if (timed) RecordEvent(c, false);
-                if (s.infiniteLights.size()) HIPCHECK(LaunchEscaped(c->S, st, depth, (int)nActive, c->stream));
-                if (s.areaLights.size()) HIPCHECK(LaunchEmissive(c->S, st, depth, (int)nActive, c->stream));
-                if (depth == s.maxDepth) break;
+                // emission (escaped rays, emissive hits) on the side stream, beside the material
+                // stage; the shadow stage and the next depth's closest hits wait for it
+                const bool emit = s.infiniteLights.size() || s.areaLights.size();
+                if (emit) {
+                    HIPCHECK(hipEventRecord(c->eClosest[depth], c->stream));
+                    HIPCHECK(hipStreamWaitEvent(c->sideStream, c->eClosest[depth], 0));
+                    if (s.infiniteLights.size()) HIPCHECK(LaunchEscaped(c->S, st, depth, (int)nActive, c->sideStream));
+                    if (s.areaLights.size()) HIPCHECK(LaunchEmissive(c->S, st, depth, (int)nActive, c->sideStream));
+                    HIPCHECK(hipEventRecord(c->eEmit[depth], c->sideStream));
+                }
+                if (depth == s.maxDepth) {
+                    if (emit) HIPCHECK(hipStreamWaitEvent(c->stream, c->eEmit[depth], 0));
+                    break;
+                }
                 // EvaluateMaterialsAndBSDFs: one launch per material type present (surfscatter.cpp:39-55)
                 if (c->S.matTypeMask & (1 << kMatDiffuseT))
                     HIPCHECK(LaunchShadeDiffuse(c->S, st, depth, (int)nActive, c->stream));
                 for (int t = kMatDielectricT; t < kNumMatTypes; ++t)
                     if (c->S.matTypeMask & (1 << t))
                         HIPCHECK(LaunchShadeMicrofacet(c->S, st, depth, t, (int)nActive, c->stream));
+                if (emit) HIPCHECK(hipStreamWaitEvent(c->stream, c->eEmit[depth], 0));
                 HIPCHECK(LaunchShadow(c->S, st, depth, (int)nActive, c->stream));
             }
             HIPCHECK(LaunchFilm(c->S, st, nS, c->stream));
@@ -1194,6 +1222,25 @@ int pbrt_intersect(pbrt_context *ctx, const float *rays, int n, int anyHit, int3
     } catch (const std::exception &e) {
         return Fail(e.what());
     }
+}
+
+int64_t pbrt_debug_halton_fastpath_mismatches(const pbrt_scene *scene, int dim, uint32_t a0, uint32_t a1,
+                                              uint32_t step) {
+    if (!scene || step == 0 || a1 > (1u << 24)) return -1;
+    const SceneDesc &s = scene->desc;
+    if (dim < 0 || dim >= (int)s.permBase.size()) return -1;
+    const HaltonDimDesc d = MakeHaltonDimDesc(s.permBase[dim], s.permNDigits[dim], s.permOffset[dim]);
+    const uint16_t *perm = s.permTable.data() + d.permOffset;
+    int64_t bad = 0;
+    for (uint64_t a = a0; a < a1; a += step) {
+        const float f = ScrambledRadicalInverse24(d, (uint32_t)a, perm);
+        const float g = ScrambledRadicalInverse(d.base, d.nDigits, a, perm);
+        uint32_t fb, gb;
+        memcpy(&fb, &f, 4);
+        memcpy(&gb, &g, 4);
+        bad += fb != gb;
+    }
+    return bad;
 }
 
 float pbrt_debug_halton(const pbrt_scene *scene, int px, int py, int sampleIndex, int dim) {

@@ -630,83 +630,62 @@ PHD_NOINLINE float ScrambledRadicalInverse(uint32_t base, uint32_t nDigits, uint
     }
     return std::fmin(invBaseM * (float)reversedDigits, kOneMinusEpsilon);
 }
-// Same digits for a < 2^32 with 32-bit division (the digit count and the float
-// accumulation of reversedDigits are unchanged, so results are bit-identical).
-PHD float ScrambledRadicalInverse32(uint32_t base, uint32_t nDigits, uint32_t a, const uint16_t *perm) {
-    float invBase = (float)1 / (float)base, invBaseM = 1;
-    uint64_t reversedDigits = 0;
-    for (uint32_t digitIndex = 0; digitIndex < nDigits; ++digitIndex) {
-        uint32_t next = a / base;
-        uint32_t digitValue = a - next * base;
-        reversedDigits = reversedDigits * base + perm[digitIndex * base + digitValue];
-        invBaseM *= invBase;
-        a = next;
-    }
-    return std::fmin(invBaseM * (float)reversedDigits, kOneMinusEpsilon);
-}
 // One Halton dimension (HaltonSampler::SampleDimension -> ScrambledRadicalInverse with
-// DigitPermutation, samplers.h:78-87, util/lowdiscrepancy.h:51-76) as the kernels evaluate it.
-// For 32-bit indices and bases with base^nDigits < 2^32 the same digits are produced with the
-// runtime division replaced by a Granlund-Montgomery multiply (q = (t + ((a - t) >> 1)) >> shift,
-// t = mulhi(magic, a), exact for every 32-bit a), all permutation loads issued together and the
-// reversed digits held in 32 bits; the float arithmetic is unchanged.  Otherwise the 64-bit
-// restatement above runs.
-constexpr int kMaxMagicDigits = 8;       // dims >= 6 (bases >= 17): at most 7 digits
-constexpr int kMaxMagicDigitsWide = 12;  // every dim with base^nDigits < 2^32 (base 5: 11 digits)
+// DigitPermutation, samplers.h:78-87, util/lowdiscrepancy.h:115-134) as the kernels evaluate it.
+// pbrt's loop keeps reversedDigits as an exact uint64 and converts it to Float once at the end,
+// so any exact evaluation of the same integer gives the same float.  For indices a < 2^24 the
+// kernels form it as:
+//  * digits by one float multiply: q = trunc(float(a) * rcp) with rcp = float(1/b): float(a) is
+//    exact and the product is within a / b * 2^-23 < 1 of a / b for a < 2^24, so q is
+//    floor(a / b) - 1, + 0 or + 1; the remainder's sign and size fix it (the integer products
+//    q * b are 24-bit multiplies);
+//  * reversedDigits = reversedDigits * b + perm by fma in double, exact because it stays below
+//    b^nDigits < 2^53;
+//  * invBaseM precomputed by the same float product chain as pbrt's loop.
+// Larger indices take the 64-bit restatement above.  No 32/64-bit integer division remains on
+// the fast path (pbrt's a / base is a 64-bit division; here it was most of the sampler's cost).
 struct HaltonDimDesc {
-    uint32_t base, nDigits, permOffset, magic, shift, fast;
-    float invBase;
-    uint32_t pad;
+    uint32_t base, nDigits, permOffset, pad;
+    float invBase, invBaseM, rcp, pad2;
 };
 PHD HaltonDimDesc MakeHaltonDimDesc(uint32_t base, uint32_t nDigits, uint32_t permOffset) {
     HaltonDimDesc d{};
     d.base = base;
     d.nDigits = nDigits;
     d.permOffset = permOffset;
-    uint32_t l = 0;
-    while ((1u << l) < base) ++l;
-    d.shift = l - 1;
-    d.magic = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - base)) / base + 1);
-    uint64_t pw = 1;
-    bool fits = nDigits <= (uint32_t)kMaxMagicDigitsWide;
-    for (uint32_t k = 0; fits && k < nDigits; ++k) {
-        pw *= base;
-        fits = pw < ((uint64_t)1 << 32);
-    }
-    d.fast = fits ? 1u : 0u;
     d.invBase = (float)1 / (float)base;
+    float invBaseM = 1;
+    for (uint32_t k = 0; k < nDigits; ++k) invBaseM *= d.invBase;
+    d.invBaseM = invBaseM;
+    d.rcp = (float)(1.0 / base);
     return d;
 }
-// PermPtr: a plain pointer, or an LDS-qualified one in the kernels that stage the tables.
-// MaxDigits >= d.nDigits (callers check): the digit loop is unrolled to that bound.
-template <int MaxDigits, typename PermPtr>
-PHD float ScrambledRadicalInverse32Magic(const HaltonDimDesc &d, uint32_t a, PermPtr perm) {
-    const uint32_t base = d.base;
-    uint32_t pv[MaxDigits];
-PHD_UNROLL
-    for (int k = 0; k < MaxDigits; ++k) {
-        uint32_t t = (uint32_t)(((uint64_t)d.magic * a) >> 32);
-        uint32_t next = (t + ((a - t) >> 1)) >> d.shift;
-        // unconditional (row clamped to the table) so the loads issue together; rows past
-        // nDigits are discarded below
-        uint32_t row = (uint32_t)k < d.nDigits ? (uint32_t)k : d.nDigits - 1;
-        pv[k] = perm[row * base + (a - next * base)];
-        a = next;
-    }
-    float invBaseM = 1;
-    uint32_t reversedDigits = 0;
-PHD_UNROLL
-    for (int k = 0; k < MaxDigits; ++k) {
-        if ((uint32_t)k < d.nDigits) {
-            reversedDigits = reversedDigits * base + pv[k];
-            invBaseM *= d.invBase;
+template <typename PermPtr>
+PHD float ScrambledRadicalInverse24(const HaltonDimDesc &d, uint32_t a, PermPtr perm) {
+    const uint32_t b = d.base;
+    double rd = 0;
+    for (uint32_t k = 0; k < d.nDigits; ++k) {
+        uint32_t q = (uint32_t)((float)a * d.rcp);
+#if defined(__HIP_DEVICE_COMPILE__)
+        int r = (int)a - (int)__umul24(q, b);
+#else
+        int r = (int)a - (int)(q * b);
+#endif
+        if (r < 0) {
+            --q;
+            r += (int)b;
         }
+        if (r >= (int)b) {
+            ++q;
+            r -= (int)b;
+        }
+        rd = fma(rd, (double)b, (double)perm[k * b + (uint32_t)r]);
+        a = q;
     }
-    return std::fmin(invBaseM * (float)reversedDigits, kOneMinusEpsilon);
+    return std::fmin(d.invBaseM * (float)rd, kOneMinusEpsilon);
 }
 PHD float HaltonSampleDimension(const HaltonDimDesc &d, uint64_t index, const uint16_t *permTable) {
-    if ((index >> 32) == 0 && d.fast)
-        return ScrambledRadicalInverse32Magic<kMaxMagicDigitsWide>(d, (uint32_t)index, permTable + d.permOffset);
+    if (index < (1ull << 24)) return ScrambledRadicalInverse24(d, (uint32_t)index, permTable + d.permOffset);
     return ScrambledRadicalInverse(d.base, d.nDigits, index, permTable + d.permOffset);
 }
 

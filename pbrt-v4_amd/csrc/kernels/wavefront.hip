@@ -330,8 +330,7 @@ __device__ __forceinline__ RaySamples GenerateRaySamples(const DeviceScene &S, c
         const Halton h = StartPixelSample(S, px, py, sampleIndex, d0);
         auto dim = [&](int k) -> float {
             const HaltonDimDesc hd = S.haltonDim[d0 + k];
-            if ((h.index >> 32) == 0 && hd.fast && hd.nDigits <= (uint32_t)kMaxMagicDigits)
-                return ScrambledRadicalInverse32Magic<kMaxMagicDigits>(hd, (uint32_t)h.index, T.permL + T.permOff[k]);
+            if (h.index < (1ull << 24)) return ScrambledRadicalInverse24(hd, (uint32_t)h.index, T.permL + T.permOff[k]);
             return ScrambledRadicalInverse(hd.base, hd.nDigits, h.index, S.perm + hd.permOffset);
         };
         r.dUc = dim(0);

@@ -96,7 +96,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_scene_get_info", "pbrt_scene_get_flat", "pbrt_device_count", "pbrt_context_create",
     "pbrt_context_free", "pbrt_render", "pbrt_synchronize", "pbrt_get_stats", "pbrt_reset_stats",
     "pbrt_film_clear", "pbrt_film_device_ptr", "pbrt_film_read", "pbrt_film_get_rgb", "pbrt_intersect",
-    "pbrt_debug_halton", "pbrt_debug_rgb_coeffs", "pbrt_debug_rgb2spec_column", "pbrt_debug_kernel_sections",
+    "pbrt_debug_halton", "pbrt_debug_halton_fastpath_mismatches", "pbrt_debug_rgb_coeffs", "pbrt_debug_rgb2spec_column", "pbrt_debug_kernel_sections",
     "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
     "pbrt_debug_named_spectrum", "pbrt_debug_bxdf", "pbrt_debug_layered", "pbrt_debug_triangle_shading", "pbrt_film_write_image",
     "pbrt_image_read_size", "pbrt_image_read", "pbrt_image_write", "pbrt_image_error", "pbrt_debug_filter_sample",
@@ -141,6 +141,8 @@ def _lib():
     lib.pbrt_intersect.argtypes = [c.c_void_p, c.c_void_p, c.c_int, c.c_int, c.c_void_p, c.c_void_p]
     lib.pbrt_debug_halton.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_int]
     lib.pbrt_debug_halton.restype = c.c_float
+    lib.pbrt_debug_halton_fastpath_mismatches.argtypes = [c.c_void_p, c.c_int, c.c_uint32, c.c_uint32, c.c_uint32]
+    lib.pbrt_debug_halton_fastpath_mismatches.restype = c.c_int64
     lib.pbrt_debug_rgb_coeffs.argtypes = [c.c_float, c.c_float, c.c_float, c.POINTER(c.c_float)]
     lib.pbrt_debug_rgb2spec_column.argtypes = [c.c_int, c.c_int, c.c_int, c.POINTER(c.c_float)]
     lib.pbrt_debug_kernel_sections.argtypes = [c.c_void_p, c.POINTER(c.c_uint64), c.c_int]
@@ -270,6 +272,11 @@ class Scene:
 
     def halton(self, px, py, sample_index, dim):
         return _lib().pbrt_debug_halton(self._h, px, py, sample_index, dim)
+
+    def halton_fastpath_mismatches(self, dim, a0, a1, step=1):
+        """Indices in [a0, a1) (stride step) whose 24-bit fast-path ScrambledRadicalInverse
+        differs from the 64-bit restatement (core.h); -1 on bad arguments."""
+        return _lib().pbrt_debug_halton_fastpath_mismatches(self._h, dim, a0, a1, step)
 
     def __del__(self):
         if getattr(self, "_h", None) and _LIB is not None:

@@ -649,8 +649,8 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
     if (N <= c->maxPaths) return;
     // floats: records 2 x (beta 31, ray 6, lambda0, rl, etaScale) = 80, hitB 2x4, shadowRay 6,
     // shadowL 3, L 3, filterW 1 = 101; ints: records 2 x (flags, pixel, prevIdx), hitPrim 2,
-    // shadowPixel, matQ x 3 (per material type), escQ, emitQ = 14
-    const int nf = 101, ni = 14;
+    // shadowPixel, matQ x 3 (per material type), escQ, emitQ, records 2 x sidx = 16
+    const int nf = 101, ni = 16;
     const int64_t capS = ((N + kShards - 1) / kShards + 256 + 63) / 64 * 64;
     const int64_t NR = capS * kShards;  // record stride
     // per pixel-sample arrays (L, filterW) use N; the rest NR (>= N)
@@ -686,6 +686,7 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
         r.flags = takei(1);
         r.pixel = takei(1);
         r.prevIdx = takei(1);
+        r.sidx = reinterpret_cast<uint32_t *>(takei(1));
         st.hitB[b] = take(4);
         st.hitPrim[b] = takei(1);
     }
@@ -1233,7 +1234,9 @@ int64_t pbrt_debug_halton_fastpath_mismatches(const pbrt_scene *scene, int dim, 
     const uint16_t *perm = s.permTable.data() + d.permOffset;
     int64_t bad = 0;
     for (uint64_t a = a0; a < a1; a += step) {
-        const float f = ScrambledRadicalInverse24(d, (uint32_t)a, perm);
+        const float f = d.nDigits <= (uint32_t)kMaxShadeHaltonDigits
+                            ? ScrambledRadicalInverse24<kMaxShadeHaltonDigits>(d, (uint32_t)a, perm)
+                            : ScrambledRadicalInverse24<kMaxHaltonDigits24>(d, (uint32_t)a, perm);
         const float g = ScrambledRadicalInverse(d.base, d.nDigits, a, perm);
         uint32_t fb, gb;
         memcpy(&fb, &f, 4);

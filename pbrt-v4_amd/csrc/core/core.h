@@ -660,32 +660,47 @@ PHD HaltonDimDesc MakeHaltonDimDesc(uint32_t base, uint32_t nDigits, uint32_t pe
     d.rcp = (float)(1.0 / base);
     return d;
 }
-template <typename PermPtr>
+// MaxDigits >= d.nDigits: the digit loop is unrolled to that bound (iterations past nDigits are
+// skipped by a launch-uniform test) and every permutation load is issued before the first is
+// used, so a dimension costs one memory round trip, not nDigits of them.
+template <int MaxDigits, typename PermPtr>
 PHD float ScrambledRadicalInverse24(const HaltonDimDesc &d, uint32_t a, PermPtr perm) {
-    const uint32_t b = d.base;
-    double rd = 0;
-    for (uint32_t k = 0; k < d.nDigits; ++k) {
-        uint32_t q = (uint32_t)((float)a * d.rcp);
+    const uint32_t b = d.base, n = d.nDigits;
+    uint32_t pv[MaxDigits];
+PHD_UNROLL
+    for (int k = 0; k < MaxDigits; ++k) {
+        if ((uint32_t)k < n) {
+            uint32_t q = (uint32_t)((float)a * d.rcp);
 #if defined(__HIP_DEVICE_COMPILE__)
-        int r = (int)a - (int)__umul24(q, b);
+            int r = (int)a - (int)__umul24(q, b);
 #else
-        int r = (int)a - (int)(q * b);
+            int r = (int)a - (int)(q * b);
 #endif
-        if (r < 0) {
-            --q;
-            r += (int)b;
+            if (r < 0) {
+                --q;
+                r += (int)b;
+            }
+            if (r >= (int)b) {
+                ++q;
+                r -= (int)b;
+            }
+            pv[k] = perm[k * b + (uint32_t)r];
+            a = q;
         }
-        if (r >= (int)b) {
-            ++q;
-            r -= (int)b;
-        }
-        rd = fma(rd, (double)b, (double)perm[k * b + (uint32_t)r]);
-        a = q;
     }
+    double rd = 0;
+PHD_UNROLL
+    for (int k = 0; k < MaxDigits; ++k)
+        if ((uint32_t)k < n) rd = fma(rd, (double)b, (double)pv[k]);
     return std::fmin(d.invBaseM * (float)rd, kOneMinusEpsilon);
 }
+constexpr int kMaxHaltonDigits24 = 25;  // base 2 (the largest digit count of any dimension)
+constexpr int kMaxShadeHaltonDigits = 8;  // dimensions >= 6 (bases >= 17)
 PHD float HaltonSampleDimension(const HaltonDimDesc &d, uint64_t index, const uint16_t *permTable) {
-    if (index < (1ull << 24)) return ScrambledRadicalInverse24(d, (uint32_t)index, permTable + d.permOffset);
+    if (index < (1ull << 24))
+        return d.nDigits <= (uint32_t)kMaxShadeHaltonDigits
+                   ? ScrambledRadicalInverse24<kMaxShadeHaltonDigits>(d, (uint32_t)index, permTable + d.permOffset)
+                   : ScrambledRadicalInverse24<kMaxHaltonDigits24>(d, (uint32_t)index, permTable + d.permOffset);
     return ScrambledRadicalInverse(d.base, d.nDigits, index, permTable + d.permOffset);
 }
 

@@ -188,7 +188,9 @@ struct PathRecords {
     int *flags;       // [NR] bit0 specularBounce, bit1 anyNonSpecular
     int *pixel;       // [NR] pixel-sample slot (index of L / film sample); depth > 0
     int *prevIdx;     // [NR] record index at the previous depth (its hit = the MIS context)
+    uint32_t *sidx;   // [NR] the pixel sample's Halton index (kNoSampleIndex: recompute it)
 };
+constexpr uint32_t kNoSampleIndex = 0xffffffffu;
 
 // Per-pass wavefront buffers; N = paths per pass = P pixels x S samples.
 struct PathState {

@@ -506,7 +506,8 @@ __global__ void __launch_bounds__(kBlock) k_vcamera(DeviceScene S, PathState st,
     float lambda0;
     V3 o, d;
     float filterWeight;
-    GenerateCameraRay(S, st, slot, &lambda0, &o, &d, &filterWeight);
+    uint32_t sidx;
+    GenerateCameraRay(S, st, slot, &lambda0, &o, &d, &filterWeight, &sidx);
     const int NR = st.NR, N = st.N;
     st.L[slot] = 0;
     st.L[N + slot] = 0;

@@ -28,7 +28,8 @@ __global__ void __launch_bounds__(kBlock) k_camera(DeviceScene S, PathState st, 
     float lambda0;
     V3 o, d;
     float filterWeight;
-    GenerateCameraRay(S, st, slot, &lambda0, &o, &d, &filterWeight);
+    uint32_t sidx;
+    GenerateCameraRay(S, st, slot, &lambda0, &o, &d, &filterWeight, &sidx);
     // Depth-0 record = the pixel-sample slot.  beta = 1, r_u = r_l = 1, etaScale = 1, flags = 0,
     // pixel = slot are implicit at depth 0 (the depth-0 kernels use the constants) and the box
     // filter's weight is always 1: none of them is stored.
@@ -40,6 +41,7 @@ __global__ void __launch_bounds__(kBlock) k_camera(DeviceScene S, PathState st, 
     const PathRecords &r = st.rec[0];
     const int NR = st.NR;
     r.lambda0[slot] = lambda0;
+    r.sidx[slot] = sidx;
     r.ray[slot] = o.x;
     r.ray[NR + slot] = o.y;
     r.ray[2 * NR + slot] = o.z;
@@ -314,11 +316,30 @@ __device__ __forceinline__ void StageShadeTables(const DeviceScene &S, int depth
 struct RaySamples {
     float dUc, dU0, dU1, iUc, iU0, iU1, rr;
 };
+// sidx: the Halton index stored by the camera kernel (kNoSampleIndex: recompute it from the
+// pixel sample of slot)
 template <bool IndirectUc>
-__device__ __forceinline__ RaySamples GenerateRaySamples(const DeviceScene &S, const ShadeTables &T, int px, int py,
-                                                         int sampleIndex, int d0) {
+__device__ __forceinline__ RaySamples GenerateRaySamples(const DeviceScene &S, const ShadeTables &T, const PathState &st,
+                                                         int slot, uint32_t sidx, int d0) {
     RaySamples r;
     r.iUc = 0;
+    if (S.samplerType == 0 && sidx < (1u << 24)) {
+        // the common case: every dimension by the 24-bit digit loop from the LDS tables
+        auto dim = [&](int k) -> float {
+            return ScrambledRadicalInverse24<kMaxShadeHaltonDigits>(S.haltonDim[d0 + k], sidx, T.permL + T.permOff[k]);
+        };
+        r.dUc = dim(0);
+        r.dU0 = dim(1);
+        r.dU1 = dim(2);
+        if (IndirectUc) r.iUc = dim(3);
+        r.iU0 = dim(4);
+        r.iU1 = dim(5);
+        r.rr = dim(6);
+        return r;
+    }
+    int px, py, sampleIndex;
+    PixelOf(st, slot, &px, &py, &sampleIndex);
+    px += S.px0;
     if (S.samplerType == 1) {
         const uint64_t morton = ZSobolMortonIndex(S.zs, px, py, sampleIndex);
         r.dUc = ZSobolGet1D(S.zs, morton, d0, S.zsPerms, S.sobolM1);
@@ -328,11 +349,7 @@ __device__ __forceinline__ RaySamples GenerateRaySamples(const DeviceScene &S, c
         r.rr = ZSobolGet1D(S.zs, morton, d0 + 6, S.zsPerms, S.sobolM1);
     } else {
         const Halton h = StartPixelSample(S, px, py, sampleIndex, d0);
-        auto dim = [&](int k) -> float {
-            const HaltonDimDesc hd = S.haltonDim[d0 + k];
-            if (h.index < (1ull << 24)) return ScrambledRadicalInverse24(hd, (uint32_t)h.index, T.permL + T.permOff[k]);
-            return ScrambledRadicalInverse(hd.base, hd.nDigits, h.index, S.perm + hd.permOffset);
-        };
+        auto dim = [&](int k) -> float { return HaltonSampleDimension(S.haltonDim[d0 + k], h.index, S.perm); };
         r.dUc = dim(0);
         r.dU0 = dim(1);
         r.dU1 = dim(2);
@@ -379,6 +396,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
         float nRl = 0, nEta = 1;
         int slot = 0;
         float lambda0 = 0;
+        uint32_t sidx = kNoSampleIndex;
         SEC_BEGIN();
         if (active) {
             lambda0 = rec.lambda0[ri];
@@ -387,9 +405,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
             int prim = hitPrim[ri];
             float b0 = hitB[ri], b1 = hitB[N + ri], b2 = hitB[2 * N + ri];
             V3 rd(rec.ray[3 * N + ri], rec.ray[4 * N + ri], rec.ray[5 * N + ri]);
-            int px, py, sampleIndex;
-            PixelOf(st, slot, &px, &py, &sampleIndex);
-            px += S.px0;
+            sidx = rec.sidx[ri];
             V3 p0, p1, p2;
             PrimVerts(S, prim, &p0, &p1, &p2);
             const int mat = S.primMaterial[prim];
@@ -413,7 +429,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                 // ---- GenerateRaySamples (samples.cpp:29-66): dims 6 + 7 * depth + {0..6}
                 // = direct.uc, direct.u (2), indirect.uc, indirect.u (2), rr
                 // dim 3 (indirect.uc) is unused by DiffuseBxDF
-                const RaySamples rs = GenerateRaySamples<false>(S, T, px, py, sampleIndex, d0);
+                const RaySamples rs = GenerateRaySamples<false>(S, T, st, slot, sidx, d0);
                 const float dUc = rs.dUc, dU0 = rs.dU0, dU1 = rs.dU1, iU0 = rs.iU0, iU1 = rs.iU1, rr = rs.rr;
                 SEC_MARK(st, 1);
                 // ---- DiffuseMaterial::GetBxDF: R = clamp(reflectance(lambda), 0, 1); f = R / pi
@@ -563,6 +579,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
             out.flags[j] = 2;  // specularBounce = false, anyNonSpecular = true
             out.pixel[j] = slot;
             out.prevIdx[j] = ri;
+            out.sidx[j] = sidx;
         }
         SEC_MARK(st, 7);
     }
@@ -603,6 +620,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
         int nFlags = 0;
         int slot = 0;
         float lambda0 = 0;
+        uint32_t sidx = kNoSampleIndex;
         float *bf = T.bfLds + threadIdx.x;  // beta_i at bf[i * kBlock]
         if (active) {
             lambda0 = rec.lambda0[ri];
@@ -611,9 +629,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
             const int prim = hitPrim[ri];
             const float b0 = hitB[ri], b1 = hitB[N + ri], b2 = hitB[2 * N + ri];
             const V3 rd(rec.ray[3 * N + ri], rec.ray[4 * N + ri], rec.ray[5 * N + ri]);
-            int px, py, sampleIndex;
-            PixelOf(st, slot, &px, &py, &sampleIndex);
-            px += S.px0;
+            sidx = rec.sidx[ri];
 #pragma unroll 8
             for (int i = 0; i < kNSpectrumSamples; ++i) bf[i * kBlock] = depth > 0 ? rec.beta[(size_t)i * N + ri] : 1.f;
             V3 p0, p1, p2;
@@ -622,7 +638,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
             const TriSurface surf = SurfaceAt(S, prim, p0, p1, p2, b0, b1, b2);
             const V3 wo = Normalize(-rd);
             const V3 n = surf.n, ns = surf.ns;
-            const RaySamples rs = GenerateRaySamples<MT == kMatDielectricT>(S, T, px, py, sampleIndex, d0);
+            const RaySamples rs = GenerateRaySamples<MT == kMatDielectricT>(S, T, st, slot, sidx, d0);
             // ---- Material::GetBxDF (materials.h:182-204 dielectric, :491-511 conductor)
             const float4 mp = S.matParams[mat];
             TrowbridgeReitz tr{mp.x, mp.y};
@@ -827,6 +843,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
             out.flags[j] = nFlags;
             out.pixel[j] = slot;
             out.prevIdx[j] = ri;
+            out.sidx[j] = sidx;
         }
     }
 }

@@ -27,6 +27,7 @@ hipError_t LaunchEscaped(const DeviceScene &S, const PathState &st, int depth, i
 hipError_t LaunchEmissive(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
 hipError_t LaunchShadow(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
 hipError_t LaunchFilm(const DeviceScene &S, const PathState &st, int nSamples, hipStream_t s);
+hipError_t LaunchCheckRNMath(uint64_t seed, int blocks, int perThread, unsigned long long *bad, hipStream_t s);
 hipError_t LaunchVolCamera(const DeviceScene &S, const PathState &st, const VolState &v, int nActive, hipStream_t s);
 hipError_t LaunchVolClosest(const DeviceScene &S, const PathState &st, const VolState &v, int wf, int maxCount,
                             int timed, hipStream_t s);
@@ -1219,6 +1220,27 @@ int pbrt_intersect(pbrt_context *ctx, const float *rays, int n, int anyHit, int3
         for (int &v : p)
             if (v >= 0) v = ctx->bvh.triPrim[v];
         HIPCHECK(hipMemcpy(prim, p.data(), n * sizeof(int), hipMemcpyHostToDevice));
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_debug_check_rn_math(int device, uint64_t seed, int64_t n, int64_t *mismatches, float *examples96) {
+    try {
+        if (!mismatches || n <= 0) return Fail("bad arguments");
+        HIPCHECK(hipSetDevice(device));
+        const int blocks = 4096, perThread = (int)std::max<int64_t>(1, n / ((int64_t)blocks * 256));
+        unsigned long long *bad = nullptr;
+        const size_t bytes = (2 + 48) * sizeof(unsigned long long);
+        HIPCHECK(hipMalloc(&bad, bytes));
+        HIPCHECK(hipMemset(bad, 0, bytes));
+        HIPCHECK(LaunchCheckRNMath(seed, blocks, perThread, bad, nullptr));
+        std::vector<unsigned long long> h(2 + 48);
+        HIPCHECK(hipMemcpy(h.data(), bad, bytes, hipMemcpyDeviceToHost));
+        HIPCHECK(hipFree(bad));
+        *mismatches = (int64_t)h[0];
+        if (examples96) memcpy(examples96, h.data() + 2, 96 * sizeof(float));
         return 0;
     } catch (const std::exception &e) {
         return Fail(e.what());

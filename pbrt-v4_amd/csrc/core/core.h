@@ -588,7 +588,40 @@ PHD V3 TriangleSampleNormal(V3 p0, V3 p1, V3 p2, float b0, float b1, bool flip, 
 
 // ---------------------------------------------------------------- spectra
 // util/color.h:341 RGBSigmoidPolynomial; EvaluatePolynomial(l, c2, c1, c0) uses FMA.
+//
+// On the device the correctly rounded sqrt and division are formed without the range-scaling
+// and special-case steps of the compiler's IEEE sequences, which cannot act here: the sqrt
+// operand 1 + x^2 is >= 1 (v_sqrt + the same one-ulp correction; +inf passes through), and
+// the division x / t has t = 2 sqrt(1 + x^2) in [2, inf] with |x| <= t / 2, so the exponent
+// difference is small and the quotient is a normal number or below 2^-26 in magnitude --
+// where .5 + q is .5 whatever its last bits.  t = inf (|x| > 2^64) divides to 0 as in pbrt.
+// Bit-identical to the plain expression (tests/test_gpu_rn_math.py).
 PHD float SigmoidPolynomial(float c0, float c1, float c2, float lambda) {
+    float x = fmaf(lambda, fmaf(lambda, c0, c1), c2);
+    if (std::isinf(x)) return x > 0 ? 1 : 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float v = 1 + Sqr(x);
+    const float s0 = __builtin_amdgcn_sqrtf(v);
+    const float dn = __uint_as_float(__float_as_uint(s0) - 1u), up = __uint_as_float(__float_as_uint(s0) + 1u);
+    float s = fmaf(-dn, s0, v) <= 0.f ? dn : s0;
+    s = fmaf(-up, s0, v) > 0.f ? up : s;
+    const float t = 2 * s;
+    float y = __builtin_amdgcn_rcpf(t);
+    y = fmaf(fmaf(-t, y, 1.0f), y, y);
+    float q = x * y;
+    float r = fmaf(-t, q, x);
+    q = fmaf(r, y, q);
+    r = fmaf(-t, q, x);
+    q = fmaf(r, y, q);
+    if (x == 0.f) q = x * y;       // the correctly signed zero
+    if (t == kInfinity) q = x * 0.f;  // x / inf (y is NaN here)
+    return .5f + q;
+#else
+    return .5f + x / (2 * std::sqrt(1 + Sqr(x)));
+#endif
+}
+// the plain expression, for the device self-check
+PHD float SigmoidPolynomialPlain(float c0, float c1, float c2, float lambda) {
     float x = fmaf(lambda, fmaf(lambda, c0, c1), c2);
     if (std::isinf(x)) return x > 0 ? 1 : 0;
     return .5f + x / (2 * std::sqrt(1 + Sqr(x)));

@@ -573,14 +573,23 @@ __device__ inline SceneLds SetupSceneLds(const DeviceScene &S, float4 *dyn) {
 
 // NodesInLds / TrisInLds: every node / triangle is cached (launch-uniform choices, so no per-lane
 // branch whose two loads the compiler would merge into one flat load).
+// Profiling build (PBRT_AMD_TRAV_STATS): nodes visited / triangles tested per lane, summed per
+// kernel into the stats slots by TravStatsAdd.
+struct TravCount {
+    int nodes = 0, tris = 0;
+};
 template <bool AnyHit, bool Compressed, bool NodesInLds, bool TrisInLds>
-__device__ inline int TraverseCW(const DeviceScene &S, const SceneLds &L, V3 o, V3 d, float tMax, TriHit *best) {
+__device__ inline int TraverseCW(const DeviceScene &S, const SceneLds &L, V3 o, V3 d, float tMax, TriHit *best,
+                                 TravCount *cnt = nullptr) {
     const TriRayR tr = MakeTriRayR(o, d);
     const CwRay r = MakeCwRay(o, d, S.bvhAbsMax);
     LdsU2 *stk = L.stack + threadIdx.x;
     int sp = 0, node = 0, hitPrim = -1;
     while (true) {
         NodeHits nh;
+#ifdef PBRT_AMD_TRAV_STATS
+        if (cnt) ++cnt->nodes;
+#endif
         if constexpr (Compressed) {
             if (NodesInLds || node < S.ldsNodes) nh = VisitQuant(L.nodes + node * kLdsQNodeStride, r, tMax);
             else nh = VisitQuant(reinterpret_cast<const float4 *>(S.qnodes + node), r, tMax);
@@ -593,6 +602,9 @@ __device__ inline int TraverseCW(const DeviceScene &S, const SceneLds &L, V3 o, 
         while (tris) {
             const int t = nh.triBase + __builtin_ctz(tris);
             tris &= tris - 1u;
+#ifdef PBRT_AMD_TRAV_STATS
+            if (cnt) ++cnt->tris;
+#endif
             V3 a, b, c;
             if constexpr (TrisInLds) {
                 const LdsF4 *v = L.tris + (tr.kz * S.ldsTris + t) * 3;
@@ -640,8 +652,33 @@ inline int TraversalMode(const DeviceScene &S) {
     return S.compressed ? kTravQuant : (S.ldsTris > 0 ? kTravLds : kTravWide);
 }
 template <bool AnyHit, int TM>
-__device__ inline int Traverse(const DeviceScene &S, const SceneLds &L, V3 o, V3 d, float tMax, TriHit *best) {
-    return TraverseCW<AnyHit, TM == kTravQuant, TM == kTravLds, TM == kTravLds>(S, L, o, d, tMax, best);
+__device__ inline int Traverse(const DeviceScene &S, const SceneLds &L, V3 o, V3 d, float tMax, TriHit *best,
+                               TravCount *cnt = nullptr) {
+    return TraverseCW<AnyHit, TM == kTravQuant, TM == kTravLds, TM == kTravLds>(S, L, o, d, tMax, best, cnt);
+}
+// Adds a wave's traversal counts to stats[base..base+5]: lane sums of nodes and triangles,
+// the wave maxima of both (a wave runs until its slowest lane is done), rays, waves
+__device__ inline void TravStatsAdd(unsigned long long *stats, int base, bool active, const TravCount &c) {
+#ifdef PBRT_AMD_TRAV_STATS
+    int sn = active ? c.nodes : 0, st = active ? c.tris : 0, mn = sn, mt = st, nr = active ? 1 : 0;
+    for (int off = 32; off > 0; off >>= 1) {
+        sn += __shfl_xor(sn, off);
+        st += __shfl_xor(st, off);
+        mn = max(mn, __shfl_xor(mn, off));
+        mt = max(mt, __shfl_xor(mt, off));
+        nr += __shfl_xor(nr, off);
+    }
+    if (__lane_id() == 0 && nr) {
+        atomicAdd(&stats[base], (unsigned long long)sn);
+        atomicAdd(&stats[base + 1], (unsigned long long)st);
+        atomicAdd(&stats[base + 2], (unsigned long long)mn);
+        atomicAdd(&stats[base + 3], (unsigned long long)mt);
+        atomicAdd(&stats[base + 4], (unsigned long long)nr);
+        atomicAdd(&stats[base + 5], 1ull);
+    }
+#else
+    (void)stats, (void)base, (void)active, (void)c;
+#endif
 }
 // Launches kernel template K<..., TM> with the scene's traversal mode
 #define PBRT_LAUNCH_TRAVERSAL(S, KERNEL, ...)                                                   \

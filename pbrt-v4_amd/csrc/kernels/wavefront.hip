@@ -87,10 +87,11 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_closest(Device
         const int qi = active ? QueueSlot(rays, j) : 0;  // record index of this depth
         int prim = -1;
         TriHit h;
+        TravCount tc;
         if (active) {
             const V3 o(rec.ray[qi], rec.ray[N + qi], rec.ray[2 * N + qi]);
             const V3 d(rec.ray[3 * N + qi], rec.ray[4 * N + qi], rec.ray[5 * N + qi]);
-            prim = Traverse<false, TM>(S, L, o, d, kInfinity, &h);
+            prim = Traverse<false, TM>(S, L, o, d, kInfinity, &h, &tc);
             if (prim >= 0) {
                 hitPrim[qi] = prim;
                 hitB[qi] = h.b0;
@@ -112,6 +113,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_closest(Device
             for (int t = 0; t < NMatQ; ++t) pred[2 + t] = type == t;
         }
         queues.Append(pred, qi);
+        TravStatsAdd(st.stats, kStatsSectionBase + 8, active, tc);
     }
     queues.FlushAll();
 }
@@ -863,7 +865,11 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_shadow(DeviceS
         V3 o(st.shadowRay[p], st.shadowRay[N + p], st.shadowRay[2 * N + p]);
         V3 d(st.shadowRay[3 * N + p], st.shadowRay[4 * N + p], st.shadowRay[5 * N + p]);
         TriHit h;
-        int hit = Traverse<true, TM>(S, L, o, d, 1 - kShadowEpsilon, &h);
+        TravCount tc;
+        int hit = Traverse<true, TM>(S, L, o, d, 1 - kShadowEpsilon, &h, &tc);
+#ifdef PBRT_AMD_TRAV_STATS
+        TravStatsAdd(st.stats, kStatsSectionBase + 16, true, tc);
+#endif
         if (hit < 0) {
             const int slot = st.shadowPixel[p];
             st.L[slot] += st.shadowL[p];
@@ -919,6 +925,53 @@ __global__ void __launch_bounds__(kBlock, 4) k_intersect_batch(DeviceScene S, co
         outHit[2 * n + i] = h.b2;
         outHit[3 * n + i] = h.t;
     }
+}
+
+// ------------------------------------------------------------------ arithmetic self-check
+// SigmoidPolynomial's device sqrt / division (core.h) against the plain IEEE expression, bitwise:
+// each thread draws coefficient triples and wavelengths from a counter hash -- arbitrary bit
+// patterns (every exponent, zeros, denormals, infinities, NaNs) and values in the tables' range.
+__device__ inline uint32_t CheckHash(uint64_t v) {
+    v ^= v >> 33;
+    v *= 0xff51afd7ed558ccdull;
+    v ^= v >> 33;
+    v *= 0xc4ceb9fe1a85ec53ull;
+    v ^= v >> 33;
+    return (uint32_t)v;
+}
+__device__ inline float CheckOperand(uint64_t key, float scale) {
+    const uint32_t h = CheckHash(key);
+    if ((h & 7u) == 0) return __uint_as_float(CheckHash(key * 3 + 1));  // any bit pattern
+    const uint32_t e = 40u + (CheckHash(key * 5 + 2) % 180u);             // biased exponents 40..219
+    const float f = __uint_as_float((h & 0x80000000u) | (e << 23) | (CheckHash(key * 7 + 3) & 0x7fffffu));
+    return (h & 6u) == 2u ? f : scale * ((CheckHash(key * 11 + 4) >> 8) * 0x1p-24f - .5f);
+}
+__device__ inline bool SameFloat(float a, float b) {
+    return __float_as_uint(a) == __float_as_uint(b) || (a != a && b != b);
+}
+__global__ void k_check_rn_math(uint64_t seed, int perThread, unsigned long long *bad) {
+    const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    unsigned long long ns = 0;
+    for (int i = 0; i < perThread; ++i) {
+        const uint64_t k = (seed + t * perThread + i) * 4;
+        const float c0 = CheckOperand(k, 2e-3f), c1 = CheckOperand(k + 1, 2.f), c2 = CheckOperand(k + 2, 600.f);
+        const float lam = 395.f + 310.f * ((CheckHash(k + 3) >> 8) * 0x1p-24f);
+        const float a = SigmoidPolynomial(c0, c1, c2, lam), b = SigmoidPolynomialPlain(c0, c1, c2, lam);
+        if (!SameFloat(a, b)) {
+            ++ns;
+            // the first few mismatches: inputs and both results (slots 1..96 of bad, as float bits)
+            const unsigned long long slot = atomicAdd(&bad[1], 1ull);
+            if (slot < 16) {
+                float *ex = reinterpret_cast<float *>(bad + 2) + 6 * slot;
+                ex[0] = c0, ex[1] = c1, ex[2] = c2, ex[3] = lam, ex[4] = a, ex[5] = b;
+            }
+        }
+    }
+    atomicAdd(&bad[0], ns);
+}
+hipError_t LaunchCheckRNMath(uint64_t seed, int blocks, int perThread, unsigned long long *bad, hipStream_t s) {
+    hipLaunchKernelGGL(k_check_rn_math, dim3(blocks), dim3(kBlock), 0, s, seed, perThread, bad);
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------------ launch helpers (host)

@@ -96,7 +96,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_scene_get_info", "pbrt_scene_get_flat", "pbrt_device_count", "pbrt_context_create",
     "pbrt_context_free", "pbrt_render", "pbrt_synchronize", "pbrt_get_stats", "pbrt_reset_stats",
     "pbrt_film_clear", "pbrt_film_device_ptr", "pbrt_film_read", "pbrt_film_get_rgb", "pbrt_intersect",
-    "pbrt_debug_halton", "pbrt_debug_halton_fastpath_mismatches", "pbrt_debug_rgb_coeffs", "pbrt_debug_rgb2spec_column", "pbrt_debug_kernel_sections",
+    "pbrt_debug_halton", "pbrt_debug_halton_fastpath_mismatches", "pbrt_debug_check_rn_math", "pbrt_debug_rgb_coeffs", "pbrt_debug_rgb2spec_column", "pbrt_debug_kernel_sections",
     "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
     "pbrt_debug_named_spectrum", "pbrt_debug_bxdf", "pbrt_debug_layered", "pbrt_debug_triangle_shading", "pbrt_film_write_image",
     "pbrt_image_read_size", "pbrt_image_read", "pbrt_image_write", "pbrt_image_error", "pbrt_debug_filter_sample",
@@ -143,6 +143,8 @@ def _lib():
     lib.pbrt_debug_halton.restype = c.c_float
     lib.pbrt_debug_halton_fastpath_mismatches.argtypes = [c.c_void_p, c.c_int, c.c_uint32, c.c_uint32, c.c_uint32]
     lib.pbrt_debug_halton_fastpath_mismatches.restype = c.c_int64
+    lib.pbrt_debug_check_rn_math.argtypes = [c.c_int, c.c_uint64, c.c_int64, c.POINTER(c.c_int64),
+                                             c.POINTER(c.c_float)]
     lib.pbrt_debug_rgb_coeffs.argtypes = [c.c_float, c.c_float, c.c_float, c.POINTER(c.c_float)]
     lib.pbrt_debug_rgb2spec_column.argtypes = [c.c_int, c.c_int, c.c_int, c.POINTER(c.c_float)]
     lib.pbrt_debug_kernel_sections.argtypes = [c.c_void_p, c.POINTER(c.c_uint64), c.c_int]
@@ -286,6 +288,16 @@ class Scene:
 
 def load_scene(path, **overrides) -> Scene:
     return Scene.load(path, **overrides)
+
+
+def check_rn_math(n=1 << 28, seed=1, device=0):
+    """Bitwise mismatches of the kernels' RGBSigmoidPolynomial (device sqrt / division without
+    range scaling) against the plain IEEE expression over ~n hashed inputs (runs on the GPU)."""
+    out = ctypes.c_int64(0)
+    ex = (ctypes.c_float * 96)()
+    _check(_lib().pbrt_debug_check_rn_math(device, seed, n, ctypes.byref(out), ex))
+    check_rn_math.examples = np.array(ex[:], np.float32).reshape(16, 6)[:min(out.value, 16)]
+    return out.value
 
 
 def device_count() -> int:

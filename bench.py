@@ -54,7 +54,9 @@ def parse():
     ap.add_argument("--xres", type=int, default=None)
     ap.add_argument("--yres", type=int, default=None)
     ap.add_argument("--spp", type=int, default=None)
-    ap.add_argument("--max-paths", type=int, default=1 << 22)
+    ap.add_argument("--max-paths", type=int, default=0,
+                    help="paths per wavefront pass (0: the library default, the whole image's samples in "
+                         "one pass up to 64 Mi paths)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",

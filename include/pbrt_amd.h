@@ -155,6 +155,8 @@ int pbrt_scene_get_info(const pbrt_scene *scene, pbrt_scene_info *info);
 int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *flat);
 
 int pbrt_device_count(int *count);
+/* max_paths_per_pass <= 0: every sample of the film in one pass, up to 64 Mi paths (16 Mi for
+ * scenes with media) */
 int pbrt_context_create(const pbrt_scene *scene, int device, int64_t max_paths_per_pass, pbrt_context **out);
 void pbrt_context_free(pbrt_context *ctx);
 

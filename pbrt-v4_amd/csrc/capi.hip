@@ -1030,7 +1030,14 @@ int pbrt_context_create(const pbrt_scene *scene, int device, int64_t maxPaths, p
         c->device = device;
         c->desc = scene->desc;
         BuildDevice(c.get());
-        if (maxPaths <= 0) maxPaths = 1 << 22;
+        if (maxPaths <= 0) {
+            // default: every sample of the film in one pass (one launch per stage and depth for
+            // the whole image -- per-pass launch, tail and LDS-staging costs paid once), up to
+            // 64 Mi paths (~31 GB of surface path state; 16 Mi with the media records, ~23 GB)
+            const SceneDesc &d = c->desc;
+            const int64_t all = (int64_t)(d.px1 - d.px0) * (d.py1 - d.py0) * std::max(d.spp, 1);
+            maxPaths = std::min<int64_t>(all, c->volumetric ? (1 << 24) : (1 << 26));
+        }
         AllocPaths(c.get(), maxPaths);
         *out = c.release();
         return 0;

@@ -313,7 +313,7 @@ class WavefrontPathIntegrator:
     ``WavefrontPathIntegrator::Render`` (wavefront/integrator.cpp:290-493) over the given
     film rows, asynchronously on the context's HIP stream."""
 
-    def __init__(self, scene: Scene, device: int = 0, max_paths: int = 1 << 22):
+    def __init__(self, scene: Scene, device: int = 0, max_paths: int = 0):
         self.scene = scene
         self.info = scene.info
         self._h = ctypes.c_void_p()

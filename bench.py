@@ -122,15 +122,40 @@ def cpu_baseline(args, threads, sc):
                       f"({n} samples, {dt:.2f} s wall excluding the oracle's {setup:.2f} s BVH build)"}
 
 
+def latest_profile(pattern):
+    """The newest round's committed profile record matching profiles/<pattern> (r01, r02, ...)."""
+    files = sorted((ROOT / "profiles").glob(pattern))
+    if not files:
+        return None
+    try:
+        return json.loads(files[-1].read_text())
+    except Exception:
+        return None
+
+
 def pmc_traffic():
-    """HBM bytes per closest-hit launch from the committed rocprofv3 PMC pass, if any."""
-    f = ROOT / "profiles" / "r01_closest_pmc.json"
-    if f.exists():
-        try:
-            return json.loads(f.read_text()).get("hbm_bytes_per_launch")
-        except Exception:
-            return None
-    return None
+    """HBM bytes per closest-hit launch from the newest committed rocprofv3 PMC pass, if any."""
+    rec = latest_profile("r*_closest_pmc.json")
+    return rec.get("hbm_bytes_per_launch") if rec else None
+
+
+# Wide BVH8 node bytes a visit reads (12 plane float4 + header + slot triangle masks) and the
+# bytes of one pre-rotated triangle (common.h VisitWide / TraverseCW)
+NODE_BYTES_READ, TRI_BYTES_READ = 240, 48
+
+
+def effective_traversal(rays_per_s):
+    """Secondary figure: ray I/O plus the BVH node and triangle bytes the
+    traversal reads per ray -- from LDS on C2 -- with the per-ray visit counts of the committed
+    traversal-statistics record, at the measured ray rate."""
+    rec = latest_profile("r*_c2_trav_stats.json")
+    if not rec:
+        return None
+    c = rec["closest"]
+    per_ray = BYTES_PER_RAY_CLOSEST + NODE_BYTES_READ * c["nodes_per_ray"] + TRI_BYTES_READ * c["tris_per_ray"]
+    return {"bytes_per_ray": round(per_ray, 1), "achieved_GBps": round(per_ray * rays_per_s / 1e9, 1),
+            "nodes_per_ray": round(c["nodes_per_ray"], 3), "tris_per_ray": round(c["tris_per_ray"], 3),
+            "source": "profiles/" + sorted((ROOT / "profiles").glob("r*_c2_trav_stats.json"))[-1].name}
 
 
 def main():
@@ -238,7 +263,15 @@ def main():
                          "bytes_per_ray": bpr,
                          "rays_per_launch": round(st.timed_closest_rays / launches, 1),
                          "timed_launches": launches,
-                         "mean_launch_us": round(mean_launch_s * 1e6, 3)},
+                         "mean_launch_us": round(mean_launch_s * 1e6, 3),
+                         # what actually bounds the kernel: its algorithmic HBM stream is a small
+                         # fraction of the peak; the PMC SQ counters show VALU issue and LDS /
+                         # dependent-load latency (profiles/r*_c2_pmc_per_kernel.json)
+                         "limiter": ("VALU issue + LDS latency (BVH and triangles LDS-resident), not HBM"
+                                     if args.workload == "c2" else
+                                     "dependent node/triangle loads (latency), not HBM bandwidth"),
+                         "effective": (effective_traversal(bytes_per_launch / bpr / mean_launch_s)
+                                       if args.workload == "c2" and mean_launch_s > 0 else None)},
             "cpu_baseline": cpu,
             "rays": {"camera": int(st.camera_rays), "closest": int(st.closest_rays), "shadow": int(st.shadow_rays)},
         }

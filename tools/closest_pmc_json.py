@@ -17,7 +17,8 @@ from pathlib import Path
 def per_dispatch(csv_path, kernel, counter):
     acc = defaultdict(float)
     for r in csv.DictReader(open(csv_path)):
-        if r["Kernel_Name"].split("(")[0].endswith(kernel) and r["Counter_Name"] == counter:
+        name = r["Kernel_Name"].split("(")[0].split("<")[0]
+        if name.endswith(kernel) and r["Counter_Name"] == counter:
             acc[r["Dispatch_Id"]] += float(r["Counter_Value"])
     return list(acc.values())
 

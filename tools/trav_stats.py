@@ -12,8 +12,10 @@ sys.path.insert(0, str(ROOT))
 import torch  # noqa: F401
 import bench
 
+import json
+
 wl = sys.argv[1] if len(sys.argv) > 1 else "c2"
-args = bench.parse.__wrapped__(wl) if hasattr(bench.parse, "__wrapped__") else None
+out_json = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
 sys.argv = ["bench.py", "--workload", wl, "--spp", "4"]
 a = bench.parse()
 import pbrt_amd as pa
@@ -25,7 +27,13 @@ integ.reset_stats()
 integ.render()
 integ.synchronize()
 c = integ.kernel_sections(32)
+rec = {"workload": wl, "spp": 4, "note": "BVH8 group traversal work per ray (PBRT_AMD_TRAV_STATS build); "
+       "wave figures are the per-wave maxima over lanes, averaged over waves"}
 for name, b in (("closest", 8), ("shadow", 16)):
     rays, waves = max(c[b + 4], 1), max(c[b + 5], 1)
+    rec[name] = {"rays": c[b + 4], "nodes_per_ray": c[b] / rays, "tris_per_ray": c[b + 1] / rays,
+                 "wave_max_nodes": c[b + 2] / waves, "wave_max_tris": c[b + 3] / waves}
     print(f"{name:8s} rays {c[b+4]:>11d}  per ray: nodes {c[b]/rays:6.2f} tris {c[b+1]/rays:6.2f}  "
           f"per wave (max lane): nodes {c[b+2]/waves:6.2f} tris {c[b+3]/waves:6.2f}  lanes/wave {rays/waves:5.1f}")
+if out_json:
+    Path(out_json).write_text(json.dumps(rec, indent=1) + "\n")

@@ -259,14 +259,13 @@ struct SphTriSample {
     float b0, b1, b2, pdf;
     bool ok;
 };
-PHD_NOINLINE SphTriSample SampleSphericalTriangle(V3 v0, V3 v1, V3 v2, V3 p, float u0, float u1) {
+// a, bb, c: Normalize(v0 - p), Normalize(v1 - p), Normalize(v2 - p) -- the callers have them
+// already (Triangle::Sample's solid angle and bilinear weights use the same three vectors), so
+// they are passed in rather than normalised a second time (same values, same bits).
+PHD_NOINLINE SphTriSample SampleSphericalTriangleN(V3 v0, V3 v1, V3 v2, V3 p, V3 a, V3 bb, V3 c, float u0, float u1) {
     SphTriSample r{0, 0, 0, 0, false};
     float b[3];
     float *pdf = &r.pdf;
-    V3 a = v0 - p, bb = v1 - p, c = v2 - p;
-    a = Normalize(a);
-    bb = Normalize(bb);
-    c = Normalize(c);
     V3 n_ab = Cross(a, bb), n_bc = Cross(bb, c), n_ca = Cross(c, a);
     if (LengthSquared(n_ab) == 0 || LengthSquared(n_bc) == 0 || LengthSquared(n_ca) == 0) {
         return r;
@@ -322,17 +321,19 @@ PHD_NOINLINE SphTriSample SampleSphericalTriangle(V3 v0, V3 v1, V3 v2, V3 p, flo
     return r;
 }
 
+PHD SphTriSample SampleSphericalTriangle(V3 v0, V3 v1, V3 v2, V3 p, float u0, float u1) {
+    return SampleSphericalTriangleN(v0, v1, v2, p, Normalize(v0 - p), Normalize(v1 - p), Normalize(v2 - p), u0, u1);
+}
+
 // util/sampling.cpp:110 InvertSphericalTriangleSample
 struct SphTriUV {
     float u0, u1;
 };
-PHD_NOINLINE SphTriUV InvertSphericalTriangleSample(V3 v0, V3 v1, V3 v2, V3 p, V3 w) {
+// a, b, c: the normalised (v_i - p), as for SampleSphericalTriangleN
+PHD_NOINLINE SphTriUV InvertSphericalTriangleSampleN(V3 v0, V3 v1, V3 v2, V3 p, V3 a, V3 b, V3 c, V3 w) {
     SphTriUV r{0, 0};
     float *u0out = &r.u0, *u1out = &r.u1;
-    V3 a = v0 - p, b = v1 - p, c = v2 - p;
-    a = Normalize(a);
-    b = Normalize(b);
-    c = Normalize(c);
+    (void)v0, (void)v1, (void)v2, (void)p;
     V3 n_ab = Cross(a, b), n_bc = Cross(b, c), n_ca = Cross(c, a);
     if (LengthSquared(n_ab) == 0 || LengthSquared(n_bc) == 0 || LengthSquared(n_ca) == 0) {
         return r;

@@ -739,11 +739,14 @@ __device__ inline float SolidAngleOf(V3 p0, V3 p1, V3 p2, V3 p) {
     return SphericalTriangleArea(Normalize(p0 - p), Normalize(p1 - p), Normalize(p2 - p));
 }
 
-// Triangle::Sample(ctx, u) (shapes.h:1053-1130); returns false for {}
+// Triangle::Sample(ctx, u) (shapes.h:1053-1130); returns false for {}.  The three directions
+// Normalize(p_i - refP) enter the solid angle, the bilinear warp weights and the spherical
+// sample; pbrt normalises them anew in each (same operations, same values), here once.
 __device__ inline bool SampleTriangle(V3 p0, V3 p1, V3 p2, bool flip, const TriShading *sh, V3 refP, V3 refN,
                                       V3 refNs, float u0, float u1, V3 *ps, V3 *pErr, V3 *ns, float *pdfOut) {
     (void)refN;
-    float solidAngle = SolidAngleOf(p0, p1, p2, refP);
+    const V3 wi0 = Normalize(p0 - refP), wi1 = Normalize(p1 - refP), wi2 = Normalize(p2 - refP);
+    float solidAngle = SphericalTriangleArea(wi0, wi1, wi2);
     if (solidAngle < kMinSphericalSampleArea || solidAngle > kMaxSphericalSampleArea) {
         float b[3];
         SampleUniformTriangle(u0, u1, b);
@@ -764,7 +767,6 @@ __device__ inline bool SampleTriangle(V3 p0, V3 p1, V3 p2, bool flip, const TriS
     }
     float pdf = 1;
     if (refNs != V3(0, 0, 0)) {
-        V3 wi0 = Normalize(p0 - refP), wi1 = Normalize(p1 - refP), wi2 = Normalize(p2 - refP);
         float w[4] = {fmaxf(0.01f, AbsDotN(refNs, wi1)), fmaxf(0.01f, AbsDotN(refNs, wi1)),
                       fmaxf(0.01f, AbsDotN(refNs, wi0)), fmaxf(0.01f, AbsDotN(refNs, wi2))};
         float px, py;
@@ -776,7 +778,7 @@ __device__ inline bool SampleTriangle(V3 p0, V3 p1, V3 p2, bool flip, const TriS
     float triPDF;
     float b[3];
     {
-        const SphTriSample r = SampleSphericalTriangle(p0, p1, p2, refP, u0, u1);
+        const SphTriSample r = SampleSphericalTriangleN(p0, p1, p2, refP, wi0, wi1, wi2, u0, u1);
         b[0] = r.b0;
         b[1] = r.b1;
         b[2] = r.b2;
@@ -794,10 +796,12 @@ __device__ inline bool SampleTriangle(V3 p0, V3 p1, V3 p2, bool flip, const TriS
     return true;
 }
 
-// Triangle::PDF(ctx, wi) (shapes.h:1133-1174)
+// Triangle::PDF(ctx, wi) (shapes.h:1133-1174); the normalised directions to the vertices are
+// formed once, as in SampleTriangle
 __device__ inline float TrianglePDF(V3 p0, V3 p1, V3 p2, bool flip, const TriShading *sh, V3 refP, V3 refPErr,
                                    V3 refN, V3 refNs, V3 wi) {
-    float solidAngle = SolidAngleOf(p0, p1, p2, refP);
+    const V3 wi0 = Normalize(p0 - refP), wi1 = Normalize(p1 - refP), wi2 = Normalize(p2 - refP);
+    float solidAngle = SphericalTriangleArea(wi0, wi1, wi2);
     if (solidAngle < kMinSphericalSampleArea || solidAngle > kMaxSphericalSampleArea) {
         // ShapeSampleContext::SpawnRay(wi) then Triangle::Intersect
         V3 o = OffsetRayOrigin(refP, refPErr, refN, wi);
@@ -811,14 +815,10 @@ __device__ inline float TrianglePDF(V3 p0, V3 p1, V3 p2, bool flip, const TriSha
     }
     float pdf = 1 / solidAngle;
     if (refNs != V3(0, 0, 0)) {
-        float u0, u1;
-        const SphTriUV uv = InvertSphericalTriangleSample(p0, p1, p2, refP, wi);
-        u0 = uv.u0;
-        u1 = uv.u1;
-        V3 wi0 = Normalize(p0 - refP), wi1 = Normalize(p1 - refP), wi2 = Normalize(p2 - refP);
+        const SphTriUV uv = InvertSphericalTriangleSampleN(p0, p1, p2, refP, wi0, wi1, wi2, wi);
         float w[4] = {fmaxf(0.01f, AbsDotN(refNs, wi1)), fmaxf(0.01f, AbsDotN(refNs, wi1)),
                       fmaxf(0.01f, AbsDotN(refNs, wi0)), fmaxf(0.01f, AbsDotN(refNs, wi2))};
-        pdf *= BilinearPDF(u0, u1, w);
+        pdf *= BilinearPDF(uv.u0, uv.u1, w);
     }
     return pdf;
 }
@@ -954,7 +954,8 @@ __device__ inline void GenerateCameraRay(const DeviceScene &S, const PathState &
         const uint64_t morton = ZSobolMortonIndex(S.zs, px, py, sampleIndex);
         lu = ZSobolGet1D(S.zs, morton, 0, S.zsPerms, S.sobolM1);
         ZSobolGet2D(S.zs, morton, 1, S.zsPerms, S.sobolM1, &pix0, &pix1);
-        ZSobolGet2D(S.zs, morton, 4, S.zsPerms, S.sobolM1, &l0, &l1);
+        l0 = l1 = 0;
+        if (S.lensRadius > 0) ZSobolGet2D(S.zs, morton, 4, S.zsPerms, S.sobolM1, &l0, &l1);
     } else {
         // HaltonSampler: GetPixel2D reads the pixel's own Halton digits, not a dimension
         Halton h = StartPixelSample(S, px, py, sampleIndex, 0);
@@ -965,8 +966,13 @@ __device__ inline void GenerateCameraRay(const DeviceScene &S, const PathState &
                                                  : h.index / (uint64_t)S.baseScales[1];
         pix0 = a0 < (1ull << 30) ? RadicalInverse32<2>((uint32_t)a0) : RadicalInverse(2, a0);
         pix1 = a1 < (1ull << 30) ? RadicalInverse32<3>((uint32_t)a1) : RadicalInverse(3, a1);
-        (void)Get1D(S, h);  // time (unused: static camera)
-        Get2D(S, h, &l0, &l1);
+        // time: Get1D (unused: static camera); lens: Get2D, needed only by a thin-lens camera
+        // (nothing samples this pixel sample's dimensions after them in this kernel)
+        l0 = l1 = 0;
+        if (S.lensRadius > 0) {
+            (void)Get1D(S, h);
+            Get2D(S, h, &l0, &l1);
+        }
     }
     float lambda0 = Lerpf(lu, kLambdaMin, kLambdaMax);
     // Filter::Sample(GetPixel2D()) (samplers.h:797-813): offset and weight

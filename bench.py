@@ -9,8 +9,8 @@ conductor, 1920x1080, 128 spp) -- extra lines, not the headline.
 
 One "step" = one complete render of that image (all 64 samples per pixel, film cleared
 first) plus, for N > 1, the single RCCL sum-reduce of the film over xGMI.  Pixel rows are
-sharded across ranks in 16-row blocks (pixel tiles, BVH replicated, no collective on the data
-path).  Default for N > 1 is weak scaling: each GPU keeps the single-GPU workload, i.e. the job
+interleaved across ranks (row r to rank r mod N: pixel tiles, BVH replicated, no collective on
+the data path).  Default for N > 1 is weak scaling: each GPU keeps the single-GPU workload, i.e. the job
 is the same 1280x720 image at 64 x N spp whose row stripes are dealt over the N GPUs (each
 renders 1/N of the rows at all 64 x N samples = 1280x720x64 samples' worth of paths);
 ``--scaling strong`` splits one 1280x720x64 image N ways instead.  The metric counts every
@@ -175,7 +175,9 @@ def main():
     scene = load(args, job_spp(args.spp, world, scaling))
     info = scene.info
     integ = pa.WavefrontPathIntegrator(scene, device=local_rank, max_paths=args.max_paths)
-    rows = rows_for_rank(info.py0, info.py1, rank, world)
+    # single-row interleave: every rank gets the same number of rows whenever N divides the
+    # height (720 and 1080 for N = 1, 2, 4, 8), so no rank waits on a heavier share
+    rows = rows_for_rank(info.py0, info.py1, rank, world, block=1)
     film_ptr, film_n = integ.film_device_ptr()
     film_t = film_tensor_from_device_ptr(film_ptr, film_n, local_rank) if world > 1 else None
 
@@ -252,7 +254,7 @@ def main():
                                     "untextured (BASELINE configs[3] geometry)"),
                        "xres": args.xres, "yres": args.yres, "spp": info.spp, "max_depth": info.max_depth,
                        "triangles": info.n_triangles, "paths_per_pass": int(st.paths_per_pass),
-                       "sharding": (f"16-row stripes round-robin over ranks, job {info.spp} spp "
+                       "sharding": (f"rows interleaved over ranks, job {info.spp} spp "
                                     f"({'spp x N: weak' if scaling == 'weak' else 'strong'} scaling) "
                                     "+ 1 RCCL film reduce") if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

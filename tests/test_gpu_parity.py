@@ -250,3 +250,32 @@ AttributeBegin Translate 0.2 0 -0.3  Rotate 60 0 1 0  ObjectInstance "thing" Att
     sc = pa.Scene.from_string(text, SCENES, xresolution=96, yresolution=96, spp=8)
     film, _ = gpu_film(pa, sc)
     check_parity(to_rgb(oracle, sc, film), to_rgb(oracle, sc, oracle.render(sc, threads=16)))
+
+
+def test_full_c2_size_split_invariance_and_mean(pa, oracle):
+    """BASELINE configs[1] at full size (1280x720, 64 spp, maxdepth 5) through size-independent
+    properties: the film is bit-identical when the same samples are rendered as two sample
+    ranges or as interleaved row sets (every path depends only on its pixel, sample index and
+    dimension, so any split must sum to the same floats), and the image mean agrees with the
+    oracle's 1-spp render of every pixel within its statistical error."""
+    from pbrt_amd.tiles import rows_for_rank
+    sc = pa.load_scene(SCENES / "cornell-box.pbrt", xresolution=1280, yresolution=720, spp=64)
+    full, integ = gpu_film(pa, sc, max_paths=0)
+    assert np.isfinite(full).all()
+    integ.film_clear()
+    integ.render(first_sample=0, n_samples=24)
+    integ.render(first_sample=24, n_samples=40)
+    integ.synchronize()
+    np.testing.assert_array_equal(integ.film_raw(), full)
+    integ.film_clear()
+    for r in range(4):
+        integ.render(rows=rows_for_rank(0, 720, r, 4, block=1))
+    integ.synchronize()
+    np.testing.assert_array_equal(integ.film_raw(), full)
+    # mean radiance vs the oracle at 1 spp (921,600 independent samples)
+    sc1 = pa.load_scene(SCENES / "cornell-box.pbrt", xresolution=1280, yresolution=720, spp=1)
+    ref = to_rgb(oracle, sc1, oracle.render(sc1, threads=16))
+    gpu = to_rgb(oracle, sc, full)
+    m_ref, m_gpu = ref.mean(axis=(0, 1)), gpu.mean(axis=(0, 1))
+    sigma = ref.std(axis=(0, 1)) / np.sqrt(ref.shape[0] * ref.shape[1])
+    assert (np.abs(m_gpu - m_ref) <= 5 * sigma + 1e-6).all(), (m_gpu, m_ref, sigma)

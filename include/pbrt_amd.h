@@ -193,8 +193,9 @@ int pbrt_intersect(pbrt_context *ctx, const float *rays_dev, int n, int any_hit,
 /* host-side evaluation of product components (no GPU): used by golden-vector tests */
 float pbrt_debug_halton(const pbrt_scene *scene, int px, int py, int sample_index, int dim);
 /* GPU arithmetic self-check: the kernels' RGBSigmoidPolynomial evaluation (core.h, correctly
- * rounded sqrt / division without the range-scaling steps) against the plain IEEE expression on
- * about n hashed (coefficients, lambda) tuples from seed; *mismatches = bitwise mismatch count;
+ * rounded sqrt / division without the range-scaling steps) against the plain IEEE expression, and
+ * SinCosf against separate sin / cos, on about n hashed inputs from seed; *mismatches = bitwise
+ * mismatch count of both;
  * examples96 (optional): up to 16 mismatches as {c0, c1, c2, lambda, kernel value, plain value} */
 int pbrt_debug_check_rn_math(int device, uint64_t seed, int64_t n, int64_t *mismatches, float *examples96);
 /* Halton fast path check: ScrambledRadicalInverse of the scene's dimension dim (its digit

@@ -76,6 +76,10 @@ PHD constexpr float gamma(int n) { return (n * kMachineEpsilon) / (1 - n * kMach
 #if defined(__HIP_DEVICE_COMPILE__) && defined(PBRT_AMD_CR_MATH)
 PHD float Sinf(float x) { return (float)std::sin((double)x); }
 PHD float Cosf(float x) { return (float)std::cos((double)x); }
+PHD void SinCosf(float x, float *s, float *c) {
+    *s = Sinf(x);
+    *c = Cosf(x);
+}
 PHD float ASinf(float x) { return (float)std::asin((double)x); }
 PHD float ACosf(float x) { return (float)std::acos((double)x); }
 PHD float ATan2f(float y, float x) { return (float)std::atan2((double)y, (double)x); }
@@ -83,6 +87,16 @@ PHD float Logf(float x) { return (float)std::log((double)x); }
 #else
 PHD float Sinf(float x) { return std::sin(x); }
 PHD float Cosf(float x) { return std::cos(x); }
+// sin and cos of one angle: on the device one shared argument reduction (ocml sincos), the same
+// values as the two separate calls (checked bitwise on the GPU, tests/test_gpu_rn_math.py)
+PHD void SinCosf(float x, float *s, float *c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    sincosf(x, s, c);
+#else
+    *s = std::sin(x);
+    *c = std::cos(x);
+#endif
+}
 PHD float ASinf(float x) { return std::asin(x); }
 PHD float ACosf(float x) { return std::acos(x); }
 PHD float ATan2f(float y, float x) { return std::atan2(y, x); }
@@ -222,8 +236,10 @@ PHD void SampleUniformDiskConcentric(float u0, float u1, float *dx, float *dy) {
         r = oy;
         theta = kPiOver2 - kPiOver4 * (ox / oy);
     }
-    *dx = r * Cosf(theta);
-    *dy = r * Sinf(theta);
+    float sinT, cosT;
+    SinCosf(theta, &sinT, &cosT);
+    *dx = r * cosT;
+    *dy = r * sinT;
 }
 PHD V3 SampleCosineHemisphere(float u0, float u1) {  // :409
     float dx, dy;
@@ -282,9 +298,11 @@ PHD_NOINLINE SphTriSample SampleSphericalTriangleN(V3 v0, V3 v1, V3 v2, V3 p, V3
         float A = A_pi - kPi;
         *pdf = (A <= 0) ? 0 : 1 / A;
     }
-    float cosAlpha = Cosf(alpha), sinAlpha = Sinf(alpha);
-    float sinPhi = Sinf(Ap_pi) * cosAlpha - Cosf(Ap_pi) * sinAlpha;
-    float cosPhi = Cosf(Ap_pi) * cosAlpha + Sinf(Ap_pi) * sinAlpha;
+    float cosAlpha, sinAlpha, sinAp, cosAp;
+    SinCosf(alpha, &sinAlpha, &cosAlpha);
+    SinCosf(Ap_pi, &sinAp, &cosAp);
+    float sinPhi = sinAp * cosAlpha - cosAp * sinAlpha;
+    float cosPhi = cosAp * cosAlpha + sinAp * sinAlpha;
     float k1 = cosPhi + cosAlpha;
     float k2 = sinPhi - sinAlpha * Dot(a, bb);
     float cosBp = (k2 + (DifferenceOfProducts(k2, cosPhi, k1, sinPhi)) * cosAlpha) /

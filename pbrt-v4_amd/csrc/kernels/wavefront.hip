@@ -957,6 +957,10 @@ __global__ void k_check_rn_math(uint64_t seed, int perThread, unsigned long long
         const float c0 = CheckOperand(k, 2e-3f), c1 = CheckOperand(k + 1, 2.f), c2 = CheckOperand(k + 2, 600.f);
         const float lam = 395.f + 310.f * ((CheckHash(k + 3) >> 8) * 0x1p-24f);
         const float a = SigmoidPolynomial(c0, c1, c2, lam), b = SigmoidPolynomialPlain(c0, c1, c2, lam);
+        // SinCosf against the separate calls, on an angle from the same hash (any value)
+        float sn, cs;
+        SinCosf(c2, &sn, &cs);
+        if (!SameFloat(sn, Sinf(c2)) || !SameFloat(cs, Cosf(c2))) atomicAdd(&bad[50], 1ull);
         if (!SameFloat(a, b)) {
             ++ns;
             // the first few mismatches: inputs and both results (slots 1..96 of bad, as float bits)

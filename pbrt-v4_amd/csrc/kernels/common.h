@@ -12,6 +12,19 @@ constexpr int kBlock = 256;
 #ifndef PBRT_TRAVERSAL_WAVES
 #define PBRT_TRAVERSAL_WAVES 4  // waves/SIMD the closest/shadow kernels are compiled for
 #endif
+// Grid caps of the queue kernels (blocks; each loops grid-stride over its queue).  Traversal
+// kernels fill their LDS scene cache once per block, so the grid is bounded, but 8192 blocks
+// (32 per CU) balance the tail better than 1024/2048 did: C2 +8 % (k_closest 960 -> 845 us
+// per launch, profiles/r02_grid_caps.txt).
+#ifndef PBRT_GRID_CAP
+#define PBRT_GRID_CAP 8192
+#endif
+#ifndef PBRT_SHADE_GRID_CAP
+#define PBRT_SHADE_GRID_CAP 8192
+#endif
+#ifndef PBRT_SHADOW_WAVES
+#define PBRT_SHADOW_WAVES PBRT_TRAVERSAL_WAVES  // waves/SIMD of the any-hit (shadow) kernel
+#endif
 #ifndef PBRT_SHADE_WAVES
 #define PBRT_SHADE_WAVES 3  // waves/SIMD the shade kernel is compiled for (VGPR budget)
 #endif

@@ -1955,7 +1955,7 @@ hipError_t LaunchVolCamera(const DeviceScene &S, const PathState &st, const VolS
 }
 hipError_t LaunchVolClosest(const DeviceScene &S, const PathState &st, const VolState &v, int wf, int maxCount,
                             int timed, hipStream_t s) {
-    const dim3 block(kBlock), gT(VolGrid(maxCount, 1024));
+    const dim3 block(kBlock), gT(VolGrid(maxCount, PBRT_GRID_CAP));
 #define K_VCLOSEST(tm) k_vclosest<tm>
     PBRT_LAUNCH_TRAVERSAL(S, K_VCLOSEST, gT, block, VolStackBytes(S), s, S, st, v, wf, timed);
 #undef K_VCLOSEST
@@ -1965,7 +1965,7 @@ hipError_t LaunchVolClosest(const DeviceScene &S, const PathState &st, const Vol
 hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const VolState &v, int wf, int maxCount,
                               hipStream_t s) {
     const dim3 block(kBlock);
-    const dim3 gT(VolGrid(maxCount, 1024)), gW(VolGrid(maxCount, 2048));
+    const dim3 gT(VolGrid(maxCount, PBRT_GRID_CAP)), gW(VolGrid(maxCount, PBRT_SHADE_GRID_CAP));
     if (S.media.allGrey) hipLaunchKernelGGL(k_vmedium_grey, gW, block, 0, s, S, st, v, wf);
     else hipLaunchKernelGGL(k_vmedium, gW, block, 0, s, S, st, v, wf);
     hipLaunchKernelGGL(k_vsurface, gW, block, VolTablesLdsBytes(S) + kNS * kBlock * sizeof(float), s, S, st, v, wf);

@@ -851,7 +851,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
 }
 
 template <int TM>
-__global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_shadow(DeviceScene S, PathState st, int depth) {
+__global__ void __launch_bounds__(kBlock, PBRT_SHADOW_WAVES) k_shadow(DeviceScene S, PathState st, int depth) {
     const QueueView shadows = LoadQueue(st, depth, kCntShadow);
     if ((int)(blockIdx.x * blockDim.x) >= shadows.total) return;  // no work
     extern __shared__ float4 dynLds[];
@@ -988,14 +988,6 @@ static size_t StackBytes(const DeviceScene &S) {
     return TraversalLdsBytes(S.stackSize, S.ldsNodes, S.ldsTris, S.compressed);
 }
 
-// Traversal kernels loop over their queue inside a bounded grid so the LDS scene cache is
-// filled once per block, not once per 256 rays.
-#ifndef PBRT_GRID_CAP
-#define PBRT_GRID_CAP 1024
-#endif
-#ifndef PBRT_SHADE_GRID_CAP
-#define PBRT_SHADE_GRID_CAP 2048
-#endif
 // Producer grids are multiples of kShards (the shard capacity bound depends on it).
 static int ShardedGrid(int n, int cap) {
     int g = (n + kBlock - 1) / kBlock;

@@ -1239,14 +1239,14 @@ int pbrt_debug_check_rn_math(int device, uint64_t seed, int64_t n, int64_t *mism
         HIPCHECK(hipSetDevice(device));
         const int blocks = 4096, perThread = (int)std::max<int64_t>(1, n / ((int64_t)blocks * 256));
         unsigned long long *bad = nullptr;
-        const size_t bytes = (2 + 48 + 1) * sizeof(unsigned long long);
+        const size_t bytes = (2 + 48 + 2) * sizeof(unsigned long long);
         HIPCHECK(hipMalloc(&bad, bytes));
         HIPCHECK(hipMemset(bad, 0, bytes));
         HIPCHECK(LaunchCheckRNMath(seed, blocks, perThread, bad, nullptr));
-        std::vector<unsigned long long> h(2 + 48 + 1);
+        std::vector<unsigned long long> h(2 + 48 + 2);
         HIPCHECK(hipMemcpy(h.data(), bad, bytes, hipMemcpyDeviceToHost));
         HIPCHECK(hipFree(bad));
-        *mismatches = (int64_t)(h[0] + h[50]);
+        *mismatches = (int64_t)(h[0] + h[50] + h[51]);
         if (examples96) memcpy(examples96, h.data() + 2, 96 * sizeof(float));
         return 0;
     } catch (const std::exception &e) {

@@ -655,10 +655,13 @@ PHD void SampleWavelengthsUniform(float u, float lambda[kNSpectrumSamples]) {
         if (lambda[i] > kLambdaMax) lambda[i] = kLambdaMin + (lambda[i] - kLambdaMax);
     }
 }
-// DenselySampledSpectrum offset (util/spectrum.h:420): lround(lambda) - 395, 311 entries
+// DenselySampledSpectrum offset (util/spectrum.h:420): lround(lambda) - 395, 311 entries.
+// Only lambda in [394.5, 705.5) has an entry; there lambda + 0.5f is exact (lambda's ulp is
+// 2^-15 below 512 and 2^-14 above, the sum stays below 1024 and never crosses a binade edge
+// with bits to drop), so floor(lambda + 0.5) is lround(lambda): a 32-bit form of the 64-bit
+// lround sequence (tests/test_golden_product_host.py checks every float in the range).
 PHD int DenseOffset(float lambda) {
-    long o = std::lround(lambda) - 395;
-    return (o < 0 || o > 310) ? -1 : (int)o;
+    return (lambda >= 394.5f && lambda < 705.5f) ? (int)std::floor(lambda + 0.5f) - 395 : -1;
 }
 // Average of 31 copies of x (SampledSpectrum::Average of a constant spectrum)
 PHD float Avg31(float x) {

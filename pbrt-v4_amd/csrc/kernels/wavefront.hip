@@ -174,6 +174,7 @@ __global__ void __launch_bounds__(kBlock) k_emissive(DeviceScene S, PathState st
     const int N = st.NR, NL = st.N;  // record stride, pixel-sample stride (L)
     const QueueView emit = LoadQueue(st, depth, kCntEmissive);
     const int count = emit.total;
+    if ((int)(blockIdx.x * blockDim.x) >= count) return;  // no work
     const int *hitPrim = st.hitPrim[depth & 1];
     const float *hitB = st.hitB[depth & 1];
     const int *prevPrim = st.hitPrim[(depth + 1) & 1];
@@ -961,6 +962,12 @@ __global__ void k_check_rn_math(uint64_t seed, int perThread, unsigned long long
         float sn, cs;
         SinCosf(c2, &sn, &cs);
         if (!SameFloat(sn, Sinf(c2)) || !SameFloat(cs, Cosf(c2))) atomicAdd(&bad[50], 1ull);
+        // DenseOffset's 32-bit form against lround over every float in [384, 712) (k / 4 sweeps it)
+        {
+            const float l = __uint_as_float(0x43C00000u + (uint32_t)((k / 4) % 0x720000u));
+            const long o = std::lround(l) - 395;
+            if (DenseOffset(l) != ((o < 0 || o > 310) ? -1 : (int)o)) atomicAdd(&bad[51], 1ull);
+        }
         if (!SameFloat(a, b)) {
             ++ns;
             // the first few mismatches: inputs and both results (slots 1..96 of bad, as float bits)

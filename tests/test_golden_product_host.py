@@ -117,3 +117,16 @@ def test_halton_fastpath_matches_64bit_restatement(pa):
         assert sc.halton_fastpath_mismatches(dim, top - (1 << 16), top) == 0, dim
         assert sc.halton_fastpath_mismatches(dim, 0, 1 << 16) == 0, dim
     assert sc.halton_fastpath_mismatches(0, 0, top + 1) == -1
+
+
+def test_dense_offset_32bit_form_is_lround():
+    """core.h DenseOffset: floor(lambda + 0.5f) - 395 on [394.5, 705.5), else -1, equals the
+    reference's lround(lambda) - 395 with its range check (util/spectrum.h:420) for every float
+    in [256, 1024) (float32 arithmetic, as on the host and the device)."""
+    lam = np.arange(np.float32(256).view(np.uint32), np.float32(1024).view(np.uint32), dtype=np.uint32).view(np.float32)
+    fast = np.where((lam >= np.float32(394.5)) & (lam < np.float32(705.5)),
+                    np.floor(lam + np.float32(0.5)).astype(np.int64) - 395, -1)
+    # lround: round half away from zero, in exact (float64) arithmetic
+    o = np.floor(lam.astype(np.float64) + 0.5).astype(np.int64) - 395
+    ref = np.where((o < 0) | (o > 310), -1, o)
+    assert np.array_equal(fast, ref)

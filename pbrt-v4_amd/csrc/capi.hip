@@ -836,7 +836,12 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
                 if (timed) RecordEvent(c, false);
                 // emission (escaped rays, emissive hits) on the side stream, beside the material
                 // stage; the shadow stage and the next depth's closest hits wait for it
-                const bool emit = s.infiniteLights.size() || s.areaLights.size();
+                static const bool emitSerial = getenv("PBRT_AMD_EMIT_SERIAL") != nullptr;
+                const bool emit = (s.infiniteLights.size() || s.areaLights.size()) && !emitSerial;
+                if (emitSerial) {
+                    if (s.infiniteLights.size()) HIPCHECK(LaunchEscaped(c->S, st, depth, (int)nActive, c->stream));
+                    if (s.areaLights.size()) HIPCHECK(LaunchEmissive(c->S, st, depth, (int)nActive, c->stream));
+                }
                 if (emit) {
                     HIPCHECK(hipEventRecord(c->eClosest[depth], c->stream));
                     HIPCHECK(hipStreamWaitEvent(c->sideStream, c->eClosest[depth], 0));
@@ -1239,14 +1244,14 @@ int pbrt_debug_check_rn_math(int device, uint64_t seed, int64_t n, int64_t *mism
         HIPCHECK(hipSetDevice(device));
         const int blocks = 4096, perThread = (int)std::max<int64_t>(1, n / ((int64_t)blocks * 256));
         unsigned long long *bad = nullptr;
-        const size_t bytes = (2 + 48 + 2) * sizeof(unsigned long long);
+        const size_t bytes = (2 + 48 + 3) * sizeof(unsigned long long);
         HIPCHECK(hipMalloc(&bad, bytes));
         HIPCHECK(hipMemset(bad, 0, bytes));
         HIPCHECK(LaunchCheckRNMath(seed, blocks, perThread, bad, nullptr));
-        std::vector<unsigned long long> h(2 + 48 + 2);
+        std::vector<unsigned long long> h(2 + 48 + 3);
         HIPCHECK(hipMemcpy(h.data(), bad, bytes, hipMemcpyDeviceToHost));
         HIPCHECK(hipFree(bad));
-        *mismatches = (int64_t)(h[0] + h[50] + h[51]);
+        *mismatches = (int64_t)(h[0] + h[50] + h[51] + h[52]);
         if (examples96) memcpy(examples96, h.data() + 2, 96 * sizeof(float));
         return 0;
     } catch (const std::exception &e) {

@@ -16,10 +16,21 @@
 // outgrew the instruction cache, and a call is cheaper than streaming instructions from L2.
 #define PHD_NOINLINE __host__ __device__ inline __attribute__((noinline))
 #define PHD_UNROLL _Pragma("unroll")
+// LightImportance and SampleSphericalTriangleN are inlined (C2 +2 % over out-of-line calls,
+// whose ABI saves registers around every call); -DPBRT_NOINLINE_LIGHT restores the calls.
+#ifdef PBRT_NOINLINE_LIGHT
+#define PHD_LI PHD_NOINLINE
+#define PHD_SPH PHD_NOINLINE
+#else
+#define PHD_LI PHD
+#define PHD_SPH PHD
+#endif
 #else
 #define PHD inline
 #define PHD_NOINLINE inline
 #define PHD_UNROLL
+#define PHD_LI inline
+#define PHD_SPH inline
 #endif
 
 namespace pbrt_amd {
@@ -278,7 +289,7 @@ struct SphTriSample {
 // a, bb, c: Normalize(v0 - p), Normalize(v1 - p), Normalize(v2 - p) -- the callers have them
 // already (Triangle::Sample's solid angle and bilinear weights use the same three vectors), so
 // they are passed in rather than normalised a second time (same values, same bits).
-PHD_NOINLINE SphTriSample SampleSphericalTriangleN(V3 v0, V3 v1, V3 v2, V3 p, V3 a, V3 bb, V3 c, float u0, float u1) {
+PHD_SPH SphTriSample SampleSphericalTriangleN(V3 v0, V3 v1, V3 v2, V3 p, V3 a, V3 bb, V3 c, float u0, float u1) {
     SphTriSample r{0, 0, 0, 0, false};
     float b[3];
     float *pdf = &r.pdf;
@@ -644,6 +655,34 @@ PHD float SigmoidPolynomialPlain(float c0, float c1, float c2, float lambda) {
     float x = fmaf(lambda, fmaf(lambda, c0, c1), c2);
     if (std::isinf(x)) return x > 0 ? 1 : 0;
     return .5f + x / (2 * std::sqrt(1 + Sqr(x)));
+}
+
+// x / p, correctly rounded, from y = RN(1 / p): the kernels divide a whole spectrum by one
+// scalar (beta * f * |cos| / pdf, beta / (1 - q)), so the reciprocal is one IEEE division per
+// path and each element takes q = x y and two residual corrections r = fma(-p, q, x),
+// q = fma(r, y, q) instead of the compiler's ten-instruction division.  Markstein: with y the
+// correctly rounded reciprocal and q within an ulp of x / p, one correction rounds correctly;
+// the first correction brings x y within that ulp.  DivFastOk: exponent in [-60, 60], where the
+// quotient, the exact residual (a multiple of 2^(e_x - 46)) and every intermediate are normal
+// and finite; any other operand (0, subnormal, inf, NaN, huge) takes the IEEE division.
+// Bit-identical to x / p (tests/test_gpu_rn_math.py).
+PHD bool DivFastOk(float x) { return ((FloatToBits(x) >> 23) & 0xffu) - 67u <= 120u; }
+PHD float DivByRcp(float x, float p, float y, bool pOk) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    float q = x * y;
+    float r = fmaf(-p, q, x);
+    q = fmaf(r, y, q);
+    r = fmaf(-p, q, x);
+    q = fmaf(r, y, q);
+    if (!(pOk && DivFastOk(x))) {
+        asm volatile("");  // keeps the rare IEEE path a branch (an fdiv alone would be if-converted)
+        q = x / p;
+    }
+    return q;
+#else
+    (void)y, (void)pOk;
+    return x / p;
+#endif
 }
 
 // util/spectrum.h:318 SampledWavelengths::SampleUniform (sequential adds, wrap)
@@ -1293,7 +1332,7 @@ PHD float SinSubClamped(float sinA, float cosA, float sinB, float cosB) {
     if (cosA > cosB) return 0;
     return sinA * cosB - cosA * sinB;
 }
-PHD_NOINLINE float LightImportance(LightNodeBounds lb, V3 p, V3 n) {
+PHD_LI float LightImportance(LightNodeBounds lb, V3 p, V3 n) {
     V3 pc = (lb.pMin + lb.pMax) / 2;
     float d2 = DistanceSquared(p, pc);
     d2 = std::fmax(d2, Length(lb.pMax - lb.pMin) / 2);

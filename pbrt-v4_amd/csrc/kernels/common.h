@@ -65,8 +65,26 @@ __device__ inline int WavePush(int *counter, bool pred) {
 template <int K>
 __device__ inline void BlockPush(int *const (&counters)[K], const bool (&pred)[K], int (&pos)[K]) {
 #ifndef PBRT_SHADE_PUSH_BLOCK
+    // The wave's first active lane issues every queue's atomic back to back, so their round
+    // trips overlap (one WavePush after another waits out each return in turn).
+    unsigned long long mask[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) pos[k] = WavePush(counters[k], pred[k]);
+    for (int k = 0; k < K; ++k) mask[k] = __ballot(pred[k]);
+    const int lane = __lane_id();
+    const int leader = __ffsll((long long)__ballot(1)) - 1;
+    int base[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) base[k] = 0;
+    if (lane == leader) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (mask[k]) base[k] = atomicAdd(counters[k], __popcll(mask[k]));
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int b = __builtin_amdgcn_readfirstlane(base[k]);
+        pos[k] = pred[k] ? b + __popcll(mask[k] & ((1ull << lane) - 1ull)) : -1;
+    }
 #else
     constexpr int kWaves = kBlock / 64;
     __shared__ int sCount[K][kWaves];
@@ -838,7 +856,9 @@ __device__ inline float TrianglePDF(V3 p0, V3 p1, V3 p2, bool flip, const TriSha
 
 // BVHLightSampler::Sample / PMF (lightsamplers.h:266-403) and UniformLightSampler
 // light index convention: [0, nAreaLights) area lights, then infinite lights.
-__device__ inline bool SampleLight(const DeviceScene &S, V3 p, V3 ns, float u, int *light, float *pmfOut) {
+template <typename NodeT>
+__device__ inline bool SampleLightT(const DeviceScene &S, const NodeT *lightNodes, V3 p, V3 ns, float u, int *light,
+                                    float *pmfOut) {
     int nAll = S.nAreaLights + S.nInfinite;
     if (S.uniformLightSampler) {
         if (nAll == 0) return false;
@@ -860,10 +880,10 @@ __device__ inline bool SampleLight(const DeviceScene &S, V3 p, V3 ns, float u, i
     int nodeIndex = 0;
     float pmf = 1 - pInfinite;
     for (int iter = 0; iter < 4 * kMaxLightBVHDepth; ++iter) {
-        DeviceLightNode node = S.lightNodes[nodeIndex];
+        DeviceLightNode node = lightNodes[nodeIndex];
         if (!node.isLeaf) {
-            float c0 = LightImportance(S.lightNodes[nodeIndex + 1].b, p, ns);
-            float c1 = LightImportance(S.lightNodes[node.childOrLight].b, p, ns);
+            float c0 = LightImportance(lightNodes[nodeIndex + 1].b, p, ns);
+            float c1 = LightImportance(lightNodes[node.childOrLight].b, p, ns);
             if (c0 == 0 && c1 == 0) return false;
             float nodePMF;
             int child = SampleDiscrete2(c0, c1, u, &nodePMF, &u);
@@ -879,6 +899,9 @@ __device__ inline bool SampleLight(const DeviceScene &S, V3 p, V3 ns, float u, i
         }
     }
     return false;
+}
+__device__ inline bool SampleLight(const DeviceScene &S, V3 p, V3 ns, float u, int *light, float *pmfOut) {
+    return SampleLightT(S, S.lightNodes, p, ns, u, light, pmfOut);
 }
 
 __device__ inline float LightPMF(const DeviceScene &S, V3 p, V3 ns, int light) {
@@ -943,9 +966,11 @@ struct SensorAcc {
 #if defined(__HIP_DEVICE_COMPILE__)
 typedef __attribute__((address_space(3))) const float LdsF;
 typedef __attribute__((address_space(3))) const uint16_t LdsU16;
+typedef __attribute__((address_space(3))) const DeviceLightNode LdsLightNode;
 #else
 typedef const float LdsF;
 typedef const uint16_t LdsU16;
+typedef const DeviceLightNode LdsLightNode;
 #endif
 
 // GenerateCameraRays (wavefront/camera.cpp:31-80) for one pixel-sample slot: the first

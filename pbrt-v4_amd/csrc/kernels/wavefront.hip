@@ -456,7 +456,11 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                     V3 cp = OffsetRayOrigin(pi, pe, n, wo);  // reflective, not transmissive
                     int li;
                     float lpmf;
-                    if (SampleLight(SL, cp, ns, dUc, &li, &lpmf) && li < S.nAreaLights) {
+                    const bool sampled =
+                        lay.lightsInLds
+                            ? SampleLightT(SL, (const LdsLightNode *)SL.lightNodes, cp, ns, dUc, &li, &lpmf)
+                            : SampleLightT(SL, S.lightNodes, cp, ns, dUc, &li, &lpmf);
+                    if (sampled && li < S.nAreaLights) {
                         const DeviceAreaLight &Ld = lightsL[li];
                         V3 q0(Ld.v0.x, Ld.v0.y, Ld.v0.z), q1(Ld.v1.x, Ld.v1.y, Ld.v1.z), q2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
                         V3 lp, lpe, ln;
@@ -509,9 +513,11 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                         float etaScale = depth > 0 ? rec.etaScale[ri] : 1.f;
                         float avgRu = Avg31(1.f);
                         float mx = -kInfinity;
+                        const float rpdf = 1 / pdf;  // one IEEE division; elements by DivByRcp
+                        const bool pdfOk = DivFastOk(pdf);
 #pragma unroll 4
                         for (int i = 0; i < kNSpectrumSamples; ++i) {
-                            float nbv = bf[i * kBlock] * absdot / pdf;
+                            float nbv = DivByRcp(bf[i * kBlock] * absdot, pdf, rpdf, pdfOk);
                             bf[i * kBlock] = nbv;
                             mx = fmaxf(mx, nbv * etaScale / avgRu);
                         }
@@ -525,12 +531,18 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                         if (!kill) {
                             bool rrScale = mx < 1 && depth >= 1;
                             bool nz = false;
+                            if (rrScale) {
+                                const float omq = 1 - q, rq = 1 / omq;
+                                const bool qOk = DivFastOk(omq);
 #pragma unroll 4
-                            for (int i = 0; i < kNSpectrumSamples; ++i) {
-                                float nbv = bf[i * kBlock];
-                                if (rrScale) nbv /= 1 - q;
-                                nz |= nbv != 0;
-                                bf[i * kBlock] = nbv;  // written out after the queue append
+                                for (int i = 0; i < kNSpectrumSamples; ++i) {
+                                    const float nbv = DivByRcp(bf[i * kBlock], omq, rq, qOk);
+                                    nz |= nbv != 0;
+                                    bf[i * kBlock] = nbv;  // written out after the queue append
+                                }
+                            } else {
+#pragma unroll 4
+                                for (int i = 0; i < kNSpectrumSamples; ++i) nz |= bf[i * kBlock] != 0;
                             }
                             if (nz) {
                                 nOrg = OffsetRayOrigin(pi, pe, n, wi);
@@ -968,6 +980,20 @@ __global__ void k_check_rn_math(uint64_t seed, int perThread, unsigned long long
             const long o = std::lround(l) - 395;
             if (DenseOffset(l) != ((o < 0 || o > 310) ? -1 : (int)o)) atomicAdd(&bad[51], 1ull);
         }
+        // DivByRcp (x / p from the correctly rounded 1 / p) against the IEEE division: any
+        // operands, and quotients placed next to a rounding midpoint (x = RN(p * m), m with a
+        // 25th significant bit) where a one-step correction is most likely to round wrongly
+        {
+            const float p = CheckOperand(k + 5, 3.f);
+            const float x0 = CheckOperand(k + 6, 5.f);
+            const uint32_t hm = CheckHash(k + 7);
+            const double mid = (double)__uint_as_float((hm & 0x807fffffu) | (127u << 23)) +
+                               ((hm >> 31) ? -0x1p-24 : 0x1p-24);  // halfway between two floats
+            const float xs[2] = {x0, (float)((double)p * mid)};
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                if (!SameFloat(DivByRcp(xs[j], p, 1 / p, DivFastOk(p)), xs[j] / p)) atomicAdd(&bad[52], 1ull);
+        }
         if (!SameFloat(a, b)) {
             ++ns;
             // the first few mismatches: inputs and both results (slots 1..96 of bad, as float bits)
@@ -1007,8 +1033,9 @@ static int ShadeGridFor(int n) { return ShardedGrid(n, PBRT_SHADE_GRID_CAP); }
 // Kernels over queues that are usually short (emissive hits, escaped rays): a grid of one
 // block per CU, grid-stride beyond that.
 static int SmallGridFor(int n) {
+    static const int cap = getenv("PBRT_AMD_EMIT_GRID") ? atoi(getenv("PBRT_AMD_EMIT_GRID")) : 256;
     int g = (n + kBlock - 1) / kBlock;
-    return g < 1 ? 1 : (g > 256 ? 256 : g);
+    return g < 1 ? 1 : (g > cap ? cap : g);
 }
 
 static int GridFor(int n) {

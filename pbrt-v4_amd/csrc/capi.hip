@@ -241,6 +241,23 @@ struct pbrt_context {
     }
 };
 
+// An RGB reflectance's sigmoid polynomial x(lambda) = c0 lambda^2 + c1 lambda + c2 bounded below
+// over every wavelength SampleUniform produces (within [390, 710]), with a generous allowance for
+// the float evaluation: x > -1000 gives clamp(.5 + x / (2 sqrt(1 + x^2)), 0, 1) >= 2e-7, so R
+// is nonzero at every sampled wavelength (it first rounds to zero near x = -2900).
+static bool SigmoidNeverZero(float c0, float c1, float c2) {
+    if (!std::isfinite(c0) || !std::isfinite(c1) || !std::isfinite(c2)) return false;
+    const double lo = 390, hi = 710;
+    auto x = [&](double l) { return ((double)c0 * l + c1) * l + c2; };
+    double m = std::min(x(lo), x(hi));
+    if (c0 > 0) {
+        const double v = -(double)c1 / (2.0 * c0);
+        if (v > lo && v < hi) m = std::min(m, x(v));
+    }
+    const double err = (std::fabs((double)c0) * hi * hi + std::fabs((double)c1) * hi + std::fabs((double)c2)) * 1e-5;
+    return m - err > -1000.0;
+}
+
 static void BuildDevice(pbrt_context *c) {
     SceneDesc &s = c->desc;
     HIPCHECK(hipSetDevice(c->device));
@@ -309,7 +326,11 @@ static void BuildDevice(pbrt_context *c) {
         const bool grey = !m.constant && m.c0 == 0 && m.c1 == 0;
         const float cv = grey ? SigmoidPolynomial(0.f, 0.f, m.c2, 500.f) : m.constantValue;
         mc.insert(mc.end(), {m.c0, m.c1, m.c2, cv});
-        mk.push_back(m.constant || grey ? 1 : 0);
+        // bit 0: constant R; bit 1: R != 0 at every sampled wavelength (k_shade_diffuse then
+        // needs no pass over the wavelengths to learn the BSDF's flags)
+        const bool constant = m.constant || grey;
+        const bool neverZero = constant ? Clampf(cv, 0, 1) != 0 : SigmoidNeverZero(m.c0, m.c1, m.c2);
+        mk.push_back((constant ? 1 : 0) | (neverZero ? 2 : 0));
     }
     c->matCoeffs.Upload(mc);
     c->matConstant.Upload(mk);

@@ -1156,7 +1156,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
         const VRaySamples rs = RaySamplesAt(S, st, slot, depth, mtype == 1 || mtype == kMatThinDielectricT);
         const float4 mp4 = S.matParams[mat];
         const float4 mc = S.matCoeffs[mat];
-        const bool constant = S.matConstant[mat];
+        const bool constant = S.matConstant[mat] & 1;
         TrowbridgeReitz tr{mp4.x, mp4.y};
         // surfscatter.cpp:127-128 (ThinDielectricBxDF::Regularize does nothing)
         if (mtype != 0 && mtype != kMatThinDielectricT && S.regularize && (flags & 2)) tr.Regularize();
@@ -1456,7 +1456,7 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
         const VRaySamples rs = RaySamplesAt(S, st, slot, depth, true);
         // ---- GetBxDF
         const float4 mp4 = S.matParams[mat], mc = S.matCoeffs[mat];
-        const bool constant = S.matConstant[mat];
+        const bool constant = S.matConstant[mat] & 1;
         const float4 L0 = S.matLayer[3 * mat], L1 = S.matLayer[3 * mat + 1], L2 = S.matLayer[3 * mat + 2];
         const bool conductor = mtype == kMatCoatedConductorT;
         float ieta = mp4.z;

@@ -239,20 +239,36 @@ __global__ void __launch_bounds__(kBlock) k_emissive(DeviceScene S, PathState st
     }
 }
 
-// Light-sample contribution beta*f*|cos|*Le/denom summed to sensor RGB (surfscatter.cpp:288-308,
-// then film.h:95-100); returns whether Le was nonzero at any wavelength.
+// k_shade_diffuse's one pass over the 31 wavelengths.  Per wavelength and in the reference's
+// operation order: bf = beta * f (f = R / pi); the light sample's contribution
+// bf * |cos| * Le / denom to sensor RGB (lanes without a light sample carry scale = 0); the new
+// beta = bf * |cos| / pdf (lanes that do not scatter carry |cos| = pdf = 1) into bf's LDS slot,
+// with max(beta * etaScale / avg(r_u)) for RR.  neeNz: Le != 0 somewhere; betaNz: new beta != 0
+// somewhere.
 template <typename FD>
-__device__ inline bool NeeAccumulate(const FD *dense, const LdsF4 *sensor4, const float *bf, float lambda0,
-                                     float scale, float absdot, float invDenom, SensorAcc *acc) {
-    bool nz = false;
-#pragma unroll 4
+__device__ inline void ShadeSpectralPass(int depth, const FD *dense, const LdsF4 *sensor4, float *bf, float4 mc,
+                                         bool constant, float lambda0, float scale, float absdotL, float invDenom,
+                                         float absdotB, float pdf, float rpdf, bool pdfOk, float etaScale,
+                                         SensorAcc *acc, bool *neeNz, bool *betaNz, float *mx) {
+    const float avgRu = Avg31(1.f);
+    bool nzL = false, nzB = false;
+    float m = -kInfinity;
+#pragma unroll 1
     for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next()) {
-        int off = DenseOffset(it.lam);
-        float Le = scale * (off < 0 ? 0.f : float(dense[off]));
-        nz |= Le != 0;
-        acc->Add(sensor4, off, bf[it.i * kBlock] * absdot * Le * invDenom, it.i == 0);
+        const float R = Reflectance(mc, constant, it.lam);
+        const float bfi = (depth > 0 ? bf[it.i * kBlock] : 1.f) * (R * kInvPi);
+        const int off = DenseOffset(it.lam);
+        const float Le = scale * (off < 0 ? 0.f : float(dense[off]));
+        nzL |= Le != 0;
+        acc->Add(sensor4, off, bfi * absdotL * Le * invDenom, it.i == 0);
+        const float nbv = DivByRcp(bfi * absdotB, pdf, rpdf, pdfOk);
+        bf[it.i * kBlock] = nbv;
+        m = fmaxf(m, nbv * etaScale / avgRu);
+        nzB |= nbv != 0;
     }
-    return nz;
+    *neeNz = nzL;
+    *betaNz = nzB;
+    *mx = m;
 }
 
 // EvaluateMaterialAndBSDF<DiffuseMaterial> (surfscatter.cpp:57-328) fused with
@@ -396,7 +412,8 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
         const int ri = active ? st.matQ[0][QueueSlot(mats, qi)] : 0;  // this depth's record
         // outputs kept to the (block-wide) queue appends: shadow ray, continuing path
         V3 sOrg, sDir, sL, nOrg, nDir;
-        float nRl = 0, nEta = 1;
+        float nRl = 0, nEta = 1, rrOmq = 1;
+        bool rrDiv = false;
         int slot = 0;
         float lambda0 = 0;
         uint32_t sidx = kNoSampleIndex;
@@ -414,7 +431,8 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
             const int mat = S.primMaterial[prim];
             TriSurface surf = SurfaceAt(S, prim, p0, p1, p2, b0, b1, b2);
             const float4 mc = matsL[mat];
-            const bool constant = matConstL[mat];
+            const int mflags = matConstL[mat];  // bit 0: constant R, bit 1: R != 0 at every wavelength
+            const bool constant = mflags & 1;
             V3 wo = Normalize(-rd);
             V3 n = surf.n, ns = surf.ns;
             // beta_i -> bfLds[i][lane] by LDS-DMA: all 31 loads in flight at once, no VGPRs,
@@ -435,23 +453,27 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                 const RaySamples rs = GenerateRaySamples<false>(S, T, st, slot, sidx, d0);
                 const float dUc = rs.dUc, dU0 = rs.dU0, dU1 = rs.dU1, iU0 = rs.iU0, iU1 = rs.iU1, rr = rs.rr;
                 SEC_MARK(st, 1);
-                // ---- DiffuseMaterial::GetBxDF: R = clamp(reflectance(lambda), 0, 1); f = R / pi
-                // (bxdfs.h DiffuseBxDF::f).  bf_i = beta_i * f_i is formed once per wavelength
-                // into LDS; light sampling and the BSDF update both start from that product.
-                bool Rnz = false;
-                float *bf = bfLds + threadIdx.x;
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the beta LDS-DMA has landed
-#pragma unroll 4
-                for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next()) {
-                    float R = Reflectance(mc, constant, it.lam);
-                    Rnz |= R != 0;
-                    bf[it.i * kBlock] = (depth > 0 ? bf[it.i * kBlock] : 1.f) * (R * kInvPi);
+                // ---- DiffuseMaterial::GetBxDF (materials.h:466-471): R = clamp(reflectance, 0, 1),
+                // f = R / pi (DiffuseBxDF, bxdfs.h:30-82).  The BSDF samples and is sampled for
+                // light only if R != 0 at some wavelength (its flags): known without a pass over
+                // the wavelengths for a constant R, and for an RGB R whose sigmoid polynomial the
+                // host bounded away from zero on every sampled wavelength (flag bit 1).
+                bool Rnz;
+                if (constant) Rnz = Reflectance(mc, true, 0.f) != 0;
+                else if (mflags & 2) Rnz = true;
+                else {
+                    Rnz = false;
+                    for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next())
+                        Rnz |= Reflectance(mc, false, it.lam) != 0;
                 }
-                SEC_MARK(st, 2);
                 Frame frame = Frame::FromXZ(Normalize(surf.dpdus), ns);
                 V3 woL = frame.ToLocal(wo);
                 V3 pi = surf.p, pe = surf.pErr;
-                // ---- light sampling + shadow ray (surfscatter.cpp:254-326); reads the old beta
+                SEC_MARK(st, 2);
+                // ---- light sample geometry (surfscatter.cpp:254-326)
+                bool nee = false;
+                int spec = 0;
+                float scale = 0, absdotL = 0, invDenom = 0;
                 if (Rnz) {
                     V3 cp = OffsetRayOrigin(pi, pe, n, wo);  // reflective, not transmissive
                     int li;
@@ -463,95 +485,98 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                     if (sampled && li < S.nAreaLights) {
                         const DeviceAreaLight &Ld = lightsL[li];
                         V3 q0(Ld.v0.x, Ld.v0.y, Ld.v0.z), q1(Ld.v1.x, Ld.v1.y, Ld.v1.z), q2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
-                        V3 lp, lpe, ln;
                         float lpdf;
+                        V3 lp, lpe, ln;
                         TriShading lsh;
                         const bool lhas = LoadTriShading(S, __float_as_int(Ld.v0.w), &lsh);
                         if (SampleTriangle(q0, q1, q2, Ld.flip, lhas ? &lsh : nullptr, cp, n, ns, dU0, dU1, &lp, &lpe,
                                            &ln, &lpdf) &&
                             lpdf != 0 && LengthSquared(lp - cp) != 0) {
-                            SEC_MARK(st, 3);
                             V3 wi = Normalize(lp - cp);
                             V3 wiL = frame.ToLocal(wi);
                             if ((Ld.twoSided || DotN(ln, -wi) >= 0) && woL.z != 0 && woL.z * wiL.z > 0) {
-                                const int spec = Ld.spectrum;
-                                float scale = Ld.scale;
-                                float absdot = AbsDotN(ns, wi);
+                                spec = Ld.spectrum;
+                                scale = Ld.scale;
+                                absdotL = AbsDotN(ns, wi);
                                 float lightPDF = lpdf * lpmf;
                                 float bsdfPDF = CosineHemispherePDF(fabsf(wiL.z));
                                 float denom = Avg31(bsdfPDF + lightPDF);
-                                const float invDenom = 1 / denom;
-                                SensorAcc acc;
-                                bool nz = lay.denseInLds
-                                              ? NeeAccumulate((const LdsF *)denseLds + spec * kDenseN, sensorL, bf,
-                                                              lambda0, scale, absdot, invDenom, &acc)
-                                              : NeeAccumulate(S.dense + spec * kDenseN, sensorL, bf, lambda0, scale,
-                                                              absdot, invDenom, &acc);
-                                if (nz) {
-                                    // SpawnRayTo(pi, n, time, pLight.pi, pLight.n) (ray.h:106-111)
-                                    sOrg = OffsetRayOrigin(pi, pe, n, lp - pi);
-                                    V3 pt = OffsetRayOrigin(lp, lpe, ln, sOrg - lp);
-                                    sDir = pt - sOrg;
-                                    sL = V3(S.imagingRatio * (acc.sx / kNSpectrumSamples),
-                                            S.imagingRatio * (acc.sy / kNSpectrumSamples),
-                                            S.imagingRatio * (acc.sz / kNSpectrumSamples));
-                                    pushShadow = true;
-                                }
+                                invDenom = 1 / denom;
+                                nee = true;
+                                // SpawnRayTo(pi, n, time, pLight.pi, pLight.n) (ray.h:106-111), formed
+                                // now so the light point is not held through the wavelength pass
+                                sOrg = OffsetRayOrigin(pi, pe, n, lp - pi);
+                                V3 pt = OffsetRayOrigin(lp, lpe, ln, sOrg - lp);
+                                sDir = pt - sOrg;
                             }
                         }
                     }
                 }
-                SEC_MARK(st, 4);
-                // ---- BSDF::Sample_f<DiffuseBxDF> + RR + indirect ray (surfscatter.cpp:170-250)
+                SEC_MARK(st, 3);
+                // ---- BSDF::Sample_f<DiffuseBxDF> geometry (surfscatter.cpp:170-190)
+                bool scat = false;
+                V3 wiB;
+                float pdf = 1, absdotB = 1, etaScale = 1;  // lanes that do not scatter: harmless values
                 if (woL.z != 0 && Rnz) {
                     V3 wiL = SampleCosineHemisphere(iU0, iU1);
                     if (woL.z < 0) wiL.z *= -1;
-                    float pdf = CosineHemispherePDF(fabsf(wiL.z));
-                    if (pdf != 0 && wiL.z != 0) {
-                        V3 wi = frame.FromLocal(wiL);
-                        float absdot = AbsDotN(ns, wi);
-                        float etaScale = depth > 0 ? rec.etaScale[ri] : 1.f;
-                        float avgRu = Avg31(1.f);
-                        float mx = -kInfinity;
-                        const float rpdf = 1 / pdf;  // one IEEE division; elements by DivByRcp
-                        const bool pdfOk = DivFastOk(pdf);
-#pragma unroll 4
-                        for (int i = 0; i < kNSpectrumSamples; ++i) {
-                            float nbv = DivByRcp(bf[i * kBlock] * absdot, pdf, rpdf, pdfOk);
-                            bf[i * kBlock] = nbv;
-                            mx = fmaxf(mx, nbv * etaScale / avgRu);
-                        }
-                        SEC_MARK(st, 5);
-                        bool kill = false;
-                        float q = 0;
+                    const float p = CosineHemispherePDF(fabsf(wiL.z));
+                    if (p != 0 && wiL.z != 0) {
+                        wiB = frame.FromLocal(wiL);
+                        nOrg = OffsetRayOrigin(pi, pe, n, wiB);
+                        nDir = wiB;
+                        absdotB = AbsDotN(ns, wiB);
+                        etaScale = depth > 0 ? rec.etaScale[ri] : 1.f;
+                        pdf = p;
+                        scat = true;
+                    }
+                }
+                SEC_MARK(st, 4);
+                // ---- one pass over the wavelengths: bf_i = beta_i f_i, the light sample's sensor
+                // RGB (beta f |cos| Le / denom, surfscatter.cpp:288-308, film.h:95-100) and the
+                // new beta = bf |cos| / pdf (surfscatter.cpp:190) with its RR maximum
+                bool neeNz = false, betaNz = false;
+                float mx = -kInfinity;
+                SensorAcc acc;
+                const float rpdf = 1 / pdf;  // one IEEE division; the elements by DivByRcp
+                if (nee || scat) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the beta LDS-DMA has landed
+                    const bool pdfOk = DivFastOk(pdf);
+                    float *bf = bfLds + threadIdx.x;
+                    if (lay.denseInLds)
+                        ShadeSpectralPass(depth, (const LdsF *)denseLds + spec * kDenseN, sensorL, bf, mc, constant,
+                                          lambda0, scale, absdotL, invDenom, absdotB, pdf, rpdf, pdfOk, etaScale, &acc,
+                                          &neeNz, &betaNz, &mx);
+                    else
+                        ShadeSpectralPass(depth, S.dense + spec * kDenseN, sensorL, bf, mc, constant, lambda0, scale,
+                                          absdotL, invDenom, absdotB, pdf, rpdf, pdfOk, etaScale, &acc, &neeNz, &betaNz,
+                                          &mx);
+                }
+                SEC_MARK(st, 5);
+                if (nee && neeNz) {
+                    sL = V3(S.imagingRatio * (acc.sx / kNSpectrumSamples), S.imagingRatio * (acc.sy / kNSpectrumSamples),
+                            S.imagingRatio * (acc.sz / kNSpectrumSamples));
+                    pushShadow = true;
+                }
+                // ---- Russian roulette (surfscatter.cpp:212-222) and the indirect ray
+                if (scat) {
+                    bool kill = false;
+                    float q = 0;
+                    if (mx < 1 && depth >= 1) {
+                        q = fmaxf(0.f, 1 - mx);
+                        kill = rr < q;
+                    }
+                    // beta / (1 - q) is nonzero exactly where beta is (1 - q in (0, 1] for a
+                    // surviving path), so the push decision needs no division; the division is
+                    // applied as beta is written out
+                    if (!kill && betaNz) {
                         if (mx < 1 && depth >= 1) {
-                            q = fmaxf(0.f, 1 - mx);
-                            kill = rr < q;
+                            rrOmq = 1 - q;
+                            rrDiv = true;
                         }
-                        if (!kill) {
-                            bool rrScale = mx < 1 && depth >= 1;
-                            bool nz = false;
-                            if (rrScale) {
-                                const float omq = 1 - q, rq = 1 / omq;
-                                const bool qOk = DivFastOk(omq);
-#pragma unroll 4
-                                for (int i = 0; i < kNSpectrumSamples; ++i) {
-                                    const float nbv = DivByRcp(bf[i * kBlock], omq, rq, qOk);
-                                    nz |= nbv != 0;
-                                    bf[i * kBlock] = nbv;  // written out after the queue append
-                                }
-                            } else {
-#pragma unroll 4
-                                for (int i = 0; i < kNSpectrumSamples; ++i) nz |= bf[i * kBlock] != 0;
-                            }
-                            if (nz) {
-                                nOrg = OffsetRayOrigin(pi, pe, n, wi);
-                                nDir = wi;
-                                nRl = 1.f / pdf;
-                                nEta = etaScale;
-                                pushRay = true;
-                            }
-                        }
+                        nRl = rpdf;  // 1 / pdf
+                        nEta = etaScale;
+                        pushRay = true;
                     }
                 }
             }
@@ -580,8 +605,16 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
         if (pos[0] >= 0) {
             const int j = shardBase + pos[0];
             const float *bf = bfLds + threadIdx.x;
+            if (rrDiv) {  // beta /= 1 - q (surfscatter.cpp:221)
+                const float rq = 1 / rrOmq;
+                const bool qOk = DivFastOk(rrOmq);
 #pragma unroll 8
-            for (int i = 0; i < kNSpectrumSamples; ++i) out.beta[(size_t)i * N + j] = bf[i * kBlock];
+                for (int i = 0; i < kNSpectrumSamples; ++i)
+                    out.beta[(size_t)i * N + j] = DivByRcp(bf[i * kBlock], rrOmq, rq, qOk);
+            } else {
+#pragma unroll 8
+                for (int i = 0; i < kNSpectrumSamples; ++i) out.beta[(size_t)i * N + j] = bf[i * kBlock];
+            }
             out.ray[j] = nOrg.x;
             out.ray[N + j] = nOrg.y;
             out.ray[2 * N + j] = nOrg.z;

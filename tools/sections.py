@@ -11,8 +11,8 @@ sys.path.insert(0, str(ROOT / "pbrt-v4_amd"))
 import torch  # noqa: F401  (same HIP runtime as bench.py)
 import pbrt_amd as pa
 
-NAMES = ["loads+surface", "halton", "R/beta*f loop", "light sample", "NEE loop+shadow write",
-         "BSDF sample+mx loop", "RR+beta write+ray write", "wave push"]
+NAMES = ["loads+surface", "halton", "R != 0 + frame", "light sample geometry", "BSDF sample geometry",
+         "wavelength pass", "RR + decisions", "queue push + writes"]
 sc = pa.load_scene(ROOT / "scenes" / "cornell-box.pbrt", xresolution=1280, yresolution=720, spp=64)
 integ = pa.WavefrontPathIntegrator(sc, device=0)
 integ.render(n_samples=4)

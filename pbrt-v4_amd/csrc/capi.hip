@@ -20,7 +20,8 @@ namespace pbrt_amd {
 hipError_t LaunchCamera(const DeviceScene &S, const PathState &st, int nActive, hipStream_t s);
 hipError_t LaunchClosest(const DeviceScene &S, const PathState &st, int depth, int maxCount, int timed,
                          hipStream_t s);
-hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
+hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int depth, int maxCount, bool lean,
+                              hipStream_t s);
 hipError_t LaunchShadeMicrofacet(const DeviceScene &S, const PathState &st, int depth, int type, int maxCount,
                                  hipStream_t s);
 hipError_t LaunchEscaped(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
@@ -848,6 +849,14 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
                 continue;
             }
             HIPCHECK(LaunchCamera(c->S, st, (int)nActive, c->stream));
+            // k_shade_diffuse<Lean>: Halton indices of this pass all below 2^24 (index <
+            // (sample + 1) * stride, samplers.h:53-71), lights, light BVH and dense spectra in
+            // LDS, no shading normals or uv
+            static const bool noLean = getenv("PBRT_AMD_NO_LEAN") != nullptr;
+            const uint64_t haltonStride = (uint64_t)c->S.baseScales[0] * (uint64_t)c->S.baseScales[1];
+            const bool lean = !noLean && c->S.samplerType == 0 &&
+                              (uint64_t)(st.firstSample + nS) * haltonStride <= (1ull << 24) &&
+                              c->S.shadeLds.lightsInLds && c->S.shadeLds.denseInLds && c->S.triShade == nullptr;
             for (int depth = 0; depth <= s.maxDepth; ++depth) {
                 // closest-hit launches are event-timed in the first pass of a render only: the
                 // passes are statistically identical and each event pair costs a queue gap
@@ -876,7 +885,7 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
                 }
                 // EvaluateMaterialsAndBSDFs: one launch per material type present (surfscatter.cpp:39-55)
                 if (c->S.matTypeMask & (1 << kMatDiffuseT))
-                    HIPCHECK(LaunchShadeDiffuse(c->S, st, depth, (int)nActive, c->stream));
+                    HIPCHECK(LaunchShadeDiffuse(c->S, st, depth, (int)nActive, lean, c->stream));
                 for (int t = kMatDielectricT; t < kNumMatTypes; ++t)
                     if (c->S.matTypeMask & (1 << t))
                         HIPCHECK(LaunchShadeMicrofacet(c->S, st, depth, t, (int)nActive, c->stream));

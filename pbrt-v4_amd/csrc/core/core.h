@@ -709,6 +709,19 @@ PHD float Avg31(float x) {
     return s / kNSpectrumSamples;
 }
 
+// 24-bit unsigned multiply as the full-rate v_mul_u32_u24.  __umul24 masks its operands and
+// relies on the backend to see 24-bit operands; once the compiler has folded the masks away by
+// range reasoning it selects the quarter-rate 32-bit v_mul_lo_u32 instead.
+PHD uint32_t MulU24(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;
+    asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+#else
+    return (a & 0xffffffu) * (b & 0xffffffu);
+#endif
+}
+
 // ---------------------------------------------------------------- Halton
 // util/lowdiscrepancy.h ScrambledRadicalInverse with digit permutations, index < 2^32.
 // perm points at the permutation rows for this prime: perm[digit * base + value].
@@ -759,14 +772,15 @@ PHD HaltonDimDesc MakeHaltonDimDesc(uint32_t base, uint32_t nDigits, uint32_t pe
 // used, so a dimension costs one memory round trip, not nDigits of them.
 template <int MaxDigits, typename PermPtr>
 PHD float ScrambledRadicalInverse24(const HaltonDimDesc &d, uint32_t a, PermPtr perm) {
-    const uint32_t b = d.base, n = d.nDigits;
+    // b < 2^24 made visible to the compiler, so __umul24 is the full-rate v_mul_u32_u24
+    const uint32_t b = d.base & 0xffffffu, n = d.nDigits;
     uint32_t pv[MaxDigits];
 PHD_UNROLL
     for (int k = 0; k < MaxDigits; ++k) {
         if ((uint32_t)k < n) {
             uint32_t q = (uint32_t)((float)a * d.rcp);
 #if defined(__HIP_DEVICE_COMPILE__)
-            int r = (int)a - (int)__umul24(q, b);
+            int r = (int)a - (int)MulU24(q, b);
 #else
             int r = (int)a - (int)(q * b);
 #endif

@@ -337,12 +337,14 @@ struct RaySamples {
 };
 // sidx: the Halton index stored by the camera kernel (kNoSampleIndex: recompute it from the
 // pixel sample of slot)
-template <bool IndirectUc>
+// Lean: the launch guarantees the Halton sampler and every index below 2^24 (host-checked), so
+// only the LDS digit loop is compiled in.
+template <bool IndirectUc, bool Lean = false>
 __device__ __forceinline__ RaySamples GenerateRaySamples(const DeviceScene &S, const ShadeTables &T, const PathState &st,
                                                          int slot, uint32_t sidx, int d0) {
     RaySamples r;
     r.iUc = 0;
-    if (S.samplerType == 0 && sidx < (1u << 24)) {
+    if (Lean || (S.samplerType == 0 && sidx < (1u << 24))) {
         // the common case: every dimension by the 24-bit digit loop from the LDS tables
         auto dim = [&](int k) -> float {
             return ScrambledRadicalInverse24<kMaxShadeHaltonDigits>(S.haltonDim[d0 + k], sidx, T.permL + T.permOff[k]);
@@ -356,6 +358,7 @@ __device__ __forceinline__ RaySamples GenerateRaySamples(const DeviceScene &S, c
         r.rr = dim(6);
         return r;
     }
+    if constexpr (Lean) return r;  // not reached
     int px, py, sampleIndex;
     PixelOf(st, slot, &px, &py, &sampleIndex);
     px += S.px0;
@@ -380,6 +383,10 @@ __device__ __forceinline__ RaySamples GenerateRaySamples(const DeviceScene &S, c
     return r;
 }
 
+// Lean (host-chosen per launch, pbrt-identical results either way): Halton indices below 2^24,
+// lights, light BVH and dense spectra staged in LDS, no mesh with shading normals or uv -- the
+// common case, compiled without the other paths so the kernel's hot code stays small.
+template <bool Lean>
 __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(DeviceScene S, PathState st, int depth) {
     const QueueView mats = LoadQueue(st, depth, kCntMat);
     if ((int)(blockIdx.x * blockDim.x) >= mats.total) return;  // no work
@@ -429,7 +436,8 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
             V3 p0, p1, p2;
             PrimVerts(S, prim, &p0, &p1, &p2);
             const int mat = S.primMaterial[prim];
-            TriSurface surf = SurfaceAt(S, prim, p0, p1, p2, b0, b1, b2);
+            TriSurface surf = Lean ? TriangleSurface(p0, p1, p2, b0, b1, b2, S.primFlip[prim], nullptr)
+                                   : SurfaceAt(S, prim, p0, p1, p2, b0, b1, b2);
             const float4 mc = matsL[mat];
             const int mflags = matConstL[mat];  // bit 0: constant R, bit 1: R != 0 at every wavelength
             const bool constant = mflags & 1;
@@ -450,7 +458,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                 // ---- GenerateRaySamples (samples.cpp:29-66): dims 6 + 7 * depth + {0..6}
                 // = direct.uc, direct.u (2), indirect.uc, indirect.u (2), rr
                 // dim 3 (indirect.uc) is unused by DiffuseBxDF
-                const RaySamples rs = GenerateRaySamples<false>(S, T, st, slot, sidx, d0);
+                const RaySamples rs = GenerateRaySamples<false, Lean>(S, T, st, slot, sidx, d0);
                 const float dUc = rs.dUc, dU0 = rs.dU0, dU1 = rs.dU1, iU0 = rs.iU0, iU1 = rs.iU1, rr = rs.rr;
                 SEC_MARK(st, 1);
                 // ---- DiffuseMaterial::GetBxDF (materials.h:466-471): R = clamp(reflectance, 0, 1),
@@ -479,7 +487,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                     int li;
                     float lpmf;
                     const bool sampled =
-                        lay.lightsInLds
+                        (Lean || lay.lightsInLds)
                             ? SampleLightT(SL, (const LdsLightNode *)SL.lightNodes, cp, ns, dUc, &li, &lpmf)
                             : SampleLightT(SL, S.lightNodes, cp, ns, dUc, &li, &lpmf);
                     if (sampled && li < S.nAreaLights) {
@@ -488,7 +496,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                         float lpdf;
                         V3 lp, lpe, ln;
                         TriShading lsh;
-                        const bool lhas = LoadTriShading(S, __float_as_int(Ld.v0.w), &lsh);
+                        const bool lhas = !Lean && LoadTriShading(S, __float_as_int(Ld.v0.w), &lsh);
                         if (SampleTriangle(q0, q1, q2, Ld.flip, lhas ? &lsh : nullptr, cp, n, ns, dU0, dU1, &lp, &lpe,
                                            &ln, &lpdf) &&
                             lpdf != 0 && LengthSquared(lp - cp) != 0) {
@@ -543,7 +551,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the beta LDS-DMA has landed
                     const bool pdfOk = DivFastOk(pdf);
                     float *bf = bfLds + threadIdx.x;
-                    if (lay.denseInLds)
+                    if (Lean || lay.denseInLds)
                         ShadeSpectralPass(depth, (const LdsF *)denseLds + spec * kDenseN, sensorL, bf, mc, constant,
                                           lambda0, scale, absdotL, invDenom, absdotB, pdf, rpdf, pdfOk, etaScale, &acc,
                                           &neeNz, &betaNz, &mx);
@@ -1100,9 +1108,14 @@ hipError_t LaunchEmissive(const DeviceScene &S, const PathState &st, int depth, 
     hipLaunchKernelGGL(k_emissive, dim3(SmallGridFor(maxCount)), dim3(kBlock), 0, s, S, st, depth);
     return hipGetLastError();
 }
-hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s) {
-    hipLaunchKernelGGL(k_shade_diffuse, dim3(ShadeGridFor(maxCount)), dim3(kBlock), (size_t)S.shadeLds.total, s,
-                       S, st, depth);
+hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int depth, int maxCount, bool lean,
+                              hipStream_t s) {
+    if (lean)
+        hipLaunchKernelGGL(k_shade_diffuse<true>, dim3(ShadeGridFor(maxCount)), dim3(kBlock), (size_t)S.shadeLds.total,
+                           s, S, st, depth);
+    else
+        hipLaunchKernelGGL(k_shade_diffuse<false>, dim3(ShadeGridFor(maxCount)), dim3(kBlock),
+                           (size_t)S.shadeLds.total, s, S, st, depth);
     return hipGetLastError();
 }
 hipError_t LaunchShadeMicrofacet(const DeviceScene &S, const PathState &st, int depth, int type, int maxCount,

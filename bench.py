@@ -8,7 +8,9 @@ conductor floor, 1920x1080, 256 spp, ZSobol) and ``--workload c4`` configs[3]'s 
 conductor, 1920x1080, 128 spp) -- extra lines, not the headline.
 
 One "step" = one complete render of that image (all 64 samples per pixel, film cleared
-first) plus, for N > 1, the single RCCL sum-reduce of the film over xGMI.  Pixel rows are
+first) plus, for N > 1, the single RCCL sum-reduce of the film over xGMI (issued
+asynchronously from a staging copy, so it overlaps the next step's render; the timed region
+ends after every reduce has completed).  Pixel rows are
 interleaved across ranks (row r to rank r mod N: pixel tiles, BVH replicated, no collective on
 the data path).  Default for N > 1 is weak scaling: each GPU keeps the single-GPU workload, i.e. the job
 is the same 1280x720 image at 64 x N spp whose row stripes are dealt over the N GPUs (each
@@ -180,17 +182,36 @@ def main():
     rows = rows_for_rank(info.py0, info.py1, rank, world, block=1)
     film_ptr, film_n = integ.film_device_ptr()
     film_t = film_tensor_from_device_ptr(film_ptr, film_n, local_rank) if world > 1 else None
+    # N > 1: each step's film is copied to one of two staging buffers and sum-reduced to rank 0
+    # asynchronously (RCCL on its own stream), so the reduce overlaps the next step's render;
+    # a staging buffer is reused only after the reduce that read it has completed.
+    staging = [torch.empty_like(film_t), torch.empty_like(film_t)] if world > 1 else None
+    pending = [None, None]
+    nstep = [0]
 
     def step(timed_kernel=False):
         integ.film_clear()
         integ.render(rows=rows, first_sample=0, n_samples=info.spp, time_closest=timed_kernel)
         if world > 1:
-            integ.synchronize()
-            dist.reduce(film_t, dst=0, op=dist.ReduceOp.SUM)
+            integ.synchronize()  # the film is complete
+            b = nstep[0] % 2
+            if pending[b] is not None:
+                pending[b].wait()
+            staging[b].copy_(film_t)
+            torch.cuda.current_stream().synchronize()  # the next film_clear must not overtake the copy
+            pending[b] = dist.reduce(staging[b], dst=0, op=dist.ReduceOp.SUM, async_op=True)
+            nstep[0] += 1
+
+    def drain():
+        for b in range(2):
+            if pending[b] is not None:
+                pending[b].wait()
+                pending[b] = None
 
     for _ in range(args.warmup):
         step()
     integ.synchronize()
+    drain()
     integ.reset_stats()
     torch.cuda.synchronize()
     if world > 1:
@@ -199,6 +220,7 @@ def main():
     for _ in range(args.steps):
         step(timed_kernel=True)
     integ.synchronize()
+    drain()  # every step's film reduce is inside the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -126,6 +126,20 @@ typedef struct pbrt_scene_flat {
      * alpha_x alpha_y, spectral interface eta (index into the piecewise-linear spectra, -1
      * for the constant eta of material_params) */
     const float *material_layer;
+    /* point / spot / distant lights (PointLight, SpotLight, DistantLight: lights.h, lights.cpp:
+     * 192-276, 1376-1495) in render space, [n_delta_lights][24] floats: type (0 point, 1 spot,
+     * 2 distant), dense spectrum index, final scale, cosFalloffStart, cosFalloffEnd, p xyz, w xyz
+     * (spot axis / direction toward a distant light), renderFromLight^-1 upper 3x3 row-major
+     * (spot), 4 unused.  The first n_point_spot are the point and spot lights: light-BVH members
+     * with global light index n_area_lights + i.  Infinite-list entry j (global index
+     * n_area_lights + n_point_spot + j) is a distant light when inf_distant[j] >= 0.
+     * uniform_order[k]: global index of pbrt's k-th light (area lights, then LightSource order);
+     * scene_radius: DistantLight::Preprocess's bounding-sphere radius. */
+    int n_delta_lights, n_point_spot;
+    const float *delta_lights;
+    const int32_t *inf_distant;       /* [n_infinite_lights] */
+    const int32_t *uniform_order;     /* [n_area_lights + n_point_spot + n_infinite_lights] */
+    float scene_radius;
 } pbrt_scene_flat;
 
 typedef struct pbrt_render_params {

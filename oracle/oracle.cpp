@@ -1041,7 +1041,8 @@ struct Lights {
                              in[2], in[0], in[1]});
         }
     }
-    int NumAll() const { return f->n_area_lights + f->n_infinite_lights; }
+    // global light index: area lights, point / spot lights, then the infinite-light list
+    int NumAll() const { return f->n_area_lights + f->n_point_spot + f->n_infinite_lights; }
     bool uniform() const {
         return f->n_light_nodes == 0 && f->n_infinite_lights + f->n_area_lights > 0 && uniformFlag;
     }
@@ -1051,7 +1052,7 @@ struct Lights {
         if (uniformFlag) {
             int nAll = NumAll();
             if (!nAll) return false;
-            *light = std::min<int>(u * nAll, nAll - 1);
+            *light = f->uniform_order[std::min<int>(u * nAll, nAll - 1)];  // pbrt's light order
             *pmf = 1.f / nAll;
             return true;
         }
@@ -1060,7 +1061,7 @@ struct Lights {
             u /= pInf;
             int index = std::min<int>(u * f->n_infinite_lights, f->n_infinite_lights - 1);
             *pmf = pInf / f->n_infinite_lights;
-            *light = f->n_area_lights + index;
+            *light = f->n_area_lights + f->n_point_spot + index;
             return true;
         }
         if (nodes.empty()) return false;
@@ -1096,7 +1097,7 @@ struct Lights {
     }
     Float PMF(Vec p, Vec n, int light) const {
         if (uniformFlag) return NumAll() ? 1.f / NumAll() : 0.f;
-        uint32_t trail = light < f->n_area_lights ? f->light_bit_trail[light] : 0xffffffffu;
+        uint32_t trail = light < f->n_area_lights + f->n_point_spot ? f->light_bit_trail[light] : 0xffffffffu;
         bool inBVH = false;
         for (auto &nd : nodes)
             if (nd.isLeaf && nd.childOrLight == light) inBVH = true;
@@ -2191,6 +2192,48 @@ struct Renderer {
         const float *dense = f->dense_spectra + 311 * f->light_spectrum[li];
         return SampleDense(dense, lambda) * f->light_scale[li];
     }
+    // PointLight / SpotLight / DistantLight::SampleLi (lights.h:221-228, 282-289, 784-798) for a
+    // global light index past the area lights; false for a UniformInfiniteLight (SampleLi with
+    // allowIncompletePDF returns nothing) and for a spot light whose Li vanishes.
+    struct DeltaSample {
+        Vec wi, p;
+        Spectrum L;
+    };
+    static Float SmoothStep(Float x, Float a, Float b) {
+        if (a == b) return (x < a) ? 0 : 1;
+        Float t = std::min<Float>(std::max<Float>((x - a) / (b - a), 0), 1);
+        return t * t * (3 - 2 * t);
+    }
+    bool DeltaLi(int li, Vec ref, const Wavelengths &lambda, DeltaSample *ds) const {
+        const int k = li - f->n_area_lights;
+        int di = k;
+        if (k >= f->n_point_spot) {
+            di = f->inf_distant[k - f->n_point_spot];
+            if (di < 0) return false;
+        }
+        const float *d = f->delta_lights + 24 * di;
+        const int type = (int)d[0];
+        const Spectrum I = SampleDense(f->dense_spectra + 311 * (int)d[1], lambda);
+        const Float scale = d[2];
+        if (type == 2) {
+            ds->wi = Normalize(Vec(d[8], d[9], d[10]));
+            ds->p = ref + ds->wi * (2 * f->scene_radius);
+            ds->L = I * scale;
+            return true;
+        }
+        const Vec p(d[5], d[6], d[7]);
+        ds->wi = Normalize(p - ref);
+        ds->p = p;
+        Float sc = scale;
+        if (type == 1) {
+            const Vec v = -ds->wi;
+            const Vec wl = Normalize(Vec(d[11] * v.x + d[12] * v.y + d[13] * v.z, d[14] * v.x + d[15] * v.y + d[16] * v.z,
+                                         d[17] * v.x + d[18] * v.y + d[19] * v.z));
+            sc = SmoothStep(wl.z, d[4], d[3]) * scale;
+        }
+        ds->L = (I * sc) / DistanceSquared(p, ref);
+        return (bool)ds->L;
+    }
 
     // one pixel sample -> sensor RGB and filter weight (film.h:95-100)
     void Li(int px, int py, int sampleIndex, float rgb[3], float *weight) const {
@@ -2370,7 +2413,13 @@ struct Renderer {
                     const Vec wo = -rd;
                     int li;
                     Float lpmf;
-                    if (lights.Sample(pS, Vec(0, 0, 0), dUc, &li, &lpmf) && li < f->n_area_lights) {
+                    DeltaSample ds;
+                    const bool sampledL = lights.Sample(pS, Vec(0, 0, 0), dUc, &li, &lpmf);
+                    if (sampledL && li >= f->n_area_lights && DeltaLi(li, pS, lambda, &ds)) {
+                        Float ph = HenyeyGreenstein(Dot(wo, ds.wi), g);
+                        Spectrum ru = r_u * 0.f, rl = r_u * (1 * lpmf);
+                        shadow(pS, ds.p - pS, medium, beta * ph * ds.L, ru, rl);
+                    } else if (sampledL && li < f->n_area_lights) {
                         int lp = f->light_prim[li];
                         ShapeSample ss;
                         if (TriangleSample(S.P(lp, 0), S.P(lp, 1), S.P(lp, 2), f->tri_flip[lp], pS, Vec(0, 0, 0), dU0,
@@ -2413,6 +2462,7 @@ struct Renderer {
             if (prim < 0) {
                 // HandleEscapedRays: uniform infinite lights, PDF_Li(allowIncomplete)=0
                 for (int k = 0; k < f->n_infinite_lights; ++k) {
+                    if (f->inf_distant[k] >= 0) continue;  // DistantLight: not an Infinite-type light
                     Spectrum Le = SampleDense(f->dense_spectra + 311 * f->inf_spectrum[k], lambda) * f->inf_scale[k];
                     if (!Le) continue;
                     if (depth == 0 || specularBounce) L = L + beta * Le / r_u.Average();
@@ -2598,7 +2648,21 @@ struct Renderer {
                 else if (trans && refl) cp = OffsetRayOrigin(si.p, si.err, si.n, -si.wo);
                 int li;
                 Float lpmf;
-                if (lights.Sample(cp, si.ns, dUc, &li, &lpmf) && li < f->n_area_lights) {
+                DeltaSample ds;
+                const bool sampledL = lights.Sample(cp, si.ns, dUc, &li, &lpmf);
+                if (sampledL && li >= f->n_area_lights && DeltaLi(li, cp, lambda, &ds)) {
+                    // a delta light: pdf 1, no BSDF MIS weight (IsDeltaLight), the light point
+                    // has no error bounds and no normal (SpawnRayTo leaves it where it is)
+                    Vec wi = ds.wi, wiL = toLocal(wi);
+                    Spectrum fv = woL.z == 0 ? Spectrum(0.f) : layered ? lay.f(woL, wiL, true) : bx.f(woL, wiL);
+                    if (fv) {
+                        Spectrum b2 = oldBeta * fv * AbsDotN(si.ns, wi);
+                        Float lightPDF = 1 * lpmf;
+                        Spectrum ru = r_u * 0.f, rl = r_u * lightPDF;
+                        Vec pf = OffsetRayOrigin(si.p, si.err, si.n, ds.p - si.p);
+                        shadow(pf, ds.p - pf, DotN(si.n, ds.p - pf) > 0 ? mOut : mIn, b2 * ds.L, ru, rl);
+                    }
+                } else if (sampledL && li < f->n_area_lights) {
                     int lp = f->light_prim[li];
                     ShapeSample ss;
                     if (TriangleSample(S.P(lp, 0), S.P(lp, 1), S.P(lp, 2), f->tri_flip[lp], cp, si.ns, dU0, dU1, &ss,

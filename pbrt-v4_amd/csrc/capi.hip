@@ -89,7 +89,8 @@ struct pbrt_scene {
         mediumParams, mediumValues, matLayer;
     std::vector<int32_t> mediumInfo;
     std::vector<int32_t> tris, lightPrim, lightSpectrum, lightTwoSided, infSpectrum, matConstant, nodeInfo, matType,
-        matSpectra, plOffsets;
+        matSpectra, plOffsets, infDistant, uniformOrder;
+    std::vector<float> deltaLights;
     void Flatten() {
         const SceneDesc &s = desc;
         verts.clear();
@@ -136,10 +137,21 @@ struct pbrt_scene {
         }
         infSpectrum.clear();
         infScale.clear();
+        infDistant.clear();
         for (auto &l : s.infiniteLights) {
             infSpectrum.push_back(l.spectrum);
             infScale.push_back(l.scale);
+            infDistant.push_back(l.distant);
         }
+        deltaLights.clear();
+        for (auto &d : s.deltaLights) {
+            deltaLights.insert(deltaLights.end(), {(float)d.type, (float)d.spectrum, d.scale, d.cosFalloffStart,
+                                                   d.cosFalloffEnd, d.p.x, d.p.y, d.p.z, d.w.x, d.w.y, d.w.z});
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) deltaLights.push_back(d.m[i][j]);
+            deltaLights.insert(deltaLights.end(), {0.f, 0.f, 0.f, 0.f});
+        }
+        uniformOrder.assign(s.uniformOrder.begin(), s.uniformOrder.end());
         dense.clear();
         for (auto &d : s.denseSpectra) dense.insert(dense.end(), d.begin(), d.end());
         sensor.clear();
@@ -194,7 +206,9 @@ struct pbrt_context {
     DevBuf<BVH8Node> nodes;
     DevBuf<BVH8QNode> qnodes;
     DevBuf<float> triVerts, matCoeffs, lightScale, lightArea, infScale, dense, sensor;
-    DevBuf<int> primMaterial, primLight, matConstant, lightPrim, lightSpectrum, lightTwoSided, infSpectrum;
+    DevBuf<int> primMaterial, primLight, matConstant, lightPrim, lightSpectrum, lightTwoSided, infSpectrum, infDistant,
+        uniformOrder;
+    DevBuf<DeviceDeltaLight> deltaLights;
     DevBuf<int> primOrig, matType, matSpectra, plOffsets;
     DevBuf<float> matParams, plLambda, plValue, triShade, matLayer, dispL0;
     DevBuf<int> dispTerm;
@@ -405,6 +419,24 @@ static void BuildDevice(pbrt_context *c) {
     }
     c->infSpectrum.Upload(is);
     c->infScale.Upload(isc);
+    {
+        std::vector<int> idist;
+        for (auto &l : s.infiniteLights) idist.push_back(l.distant);
+        c->infDistant.Upload(idist);
+        std::vector<DeviceDeltaLight> dd;
+        for (auto &d : s.deltaLights) {
+            DeviceDeltaLight x{};
+            x.p = make_float4(d.p.x, d.p.y, d.p.z, BitsToFloat((uint32_t)d.type));
+            x.w = make_float4(d.w.x, d.w.y, d.w.z, d.scale);
+            x.cone = make_float4(d.cosFalloffStart, d.cosFalloffEnd, BitsToFloat((uint32_t)d.spectrum), 0.f);
+            x.m0 = make_float4(d.m[0][0], d.m[0][1], d.m[0][2], 0.f);
+            x.m1 = make_float4(d.m[1][0], d.m[1][1], d.m[1][2], 0.f);
+            x.m2 = make_float4(d.m[2][0], d.m[2][1], d.m[2][2], 0.f);
+            dd.push_back(x);
+        }
+        c->deltaLights.Upload(dd);
+        c->uniformOrder.Upload(std::vector<int>(s.uniformOrder.begin(), s.uniformOrder.end()));
+    }
     std::vector<float> dense;
     for (auto &d : s.denseSpectra) dense.insert(dense.end(), d.begin(), d.end());
     c->dense.Upload(dense);
@@ -498,6 +530,9 @@ static void BuildDevice(pbrt_context *c) {
     if (S.dispersive && !s.media.empty())
         throw std::runtime_error("a dielectric with spectral eta (dispersion) together with participating media is not supported yet");
     c->volumetric = c->volumetric || S.dispersive;
+    if (c->volumetric && !s.deltaLights.empty())
+        throw std::runtime_error("point, spot and distant lights together with media, layered, thin-dielectric, "
+                                 "diffuse-transmission or dispersive materials are not supported yet");
     S.media.cameraMedium = s.cameraMedium;
     S.media.allGrey = 1;
     for (size_t m = 0; m < s.media.size(); ++m) {
@@ -544,6 +579,12 @@ static void BuildDevice(pbrt_context *c) {
     S.nInfinite = (int)s.infiniteLights.size();
     S.infSpectrum = c->infSpectrum.p;
     S.infScale = c->infScale.p;
+    S.infDistant = c->infDistant.p;
+    S.nDelta = (int)s.deltaLights.size();
+    S.nPointSpot = s.nPointSpot;
+    S.delta = c->deltaLights.p;
+    S.uniformOrder = c->uniformOrder.p;
+    S.sceneRadius = s.sceneRadius;
     S.uniformLightSampler = s.uniformLightSampler ? 1 : 0;
     S.lightNodes = c->lightNodes.p;
     S.nLightNodes = (int)s.lightNodes.size();
@@ -851,12 +892,13 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
             HIPCHECK(LaunchCamera(c->S, st, (int)nActive, c->stream));
             // k_shade_diffuse<Lean>: Halton indices of this pass all below 2^24 (index <
             // (sample + 1) * stride, samplers.h:53-71), lights, light BVH and dense spectra in
-            // LDS, no shading normals or uv
+            // LDS, no shading normals or uv, no point / spot / distant lights
             static const bool noLean = getenv("PBRT_AMD_NO_LEAN") != nullptr;
             const uint64_t haltonStride = (uint64_t)c->S.baseScales[0] * (uint64_t)c->S.baseScales[1];
             const bool lean = !noLean && c->S.samplerType == 0 &&
                               (uint64_t)(st.firstSample + nS) * haltonStride <= (1ull << 24) &&
-                              c->S.shadeLds.lightsInLds && c->S.shadeLds.denseInLds && c->S.triShade == nullptr;
+                              c->S.shadeLds.lightsInLds && c->S.shadeLds.denseInLds && c->S.triShade == nullptr &&
+                              c->S.nDelta == 0;
             for (int depth = 0; depth <= s.maxDepth; ++depth) {
                 // closest-hit launches are event-timed in the first pass of a render only: the
                 // passes are statistically identical and each event pair costs a queue gap
@@ -994,6 +1036,12 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
     f->light_two_sided = scene->lightTwoSided.data();
     f->inf_spectrum = scene->infSpectrum.data();
     f->inf_scale = scene->infScale.data();
+    f->n_delta_lights = (int)s.deltaLights.size();
+    f->n_point_spot = s.nPointSpot;
+    f->delta_lights = scene->deltaLights.data();
+    f->inf_distant = scene->infDistant.data();
+    f->uniform_order = scene->uniformOrder.data();
+    f->scene_radius = s.sceneRadius;
     f->dense_spectra = scene->dense.data();
     f->sensor_xyz = scene->sensor.data();
     f->imaging_ratio = s.imagingRatio;

@@ -405,7 +405,7 @@ struct LightBVHBuilder {
 
 static void BuildLightBVH(SceneDesc &s) {
     s.lightNodes.clear();
-    s.lightBitTrail.assign(s.areaLights.size(), 0);
+    s.lightBitTrail.assign(s.areaLights.size() + s.nPointSpot, 0);
     if (s.uniformLightSampler) return;
     LightBVHBuilder b{s, Bounds3()};
     std::vector<std::pair<int, LightBounds>> bvhLights;
@@ -437,6 +437,33 @@ static void BuildLightBVH(SceneDesc &s) {
         lb.twoSided = al.twoSided;
         if (lb.phi > 0) {
             bvhLights.push_back({(int)i, lb});
+            b.allLightBounds.Add(lb.bounds);
+        }
+    }
+    // PointLight::Bounds / SpotLight::Bounds (lights.cpp:168-173, 1401-1411), after the area
+    // lights in pbrt's light order; phi from the maximum of the dense spectrum, as for area lights
+    for (int i = 0; i < s.nPointSpot; ++i) {
+        const DeltaLightDesc &d = s.deltaLights[i];
+        const auto &dense = s.denseSpectra[d.spectrum];
+        const float mx = *std::max_element(dense.begin(), dense.end());
+        LightBounds lb;
+        lb.bounds.Add(d.p);
+        lb.twoSided = false;
+        if (d.type == kDeltaPoint) {
+            lb.w = V3(0, 0, 1);
+            lb.phi = 4 * kPi * d.scale * mx;
+            lb.cosTheta_o = std::cos(kPi);
+            lb.cosTheta_e = std::cos(kPi / 2);
+        } else {
+            lb.w = d.w;
+            lb.phi = d.scale * mx * 4 * kPi;
+            float cosTheta_e = std::cos(std::acos(d.cosFalloffEnd) - std::acos(d.cosFalloffStart));
+            if (cosTheta_e == 1 && d.cosFalloffEnd != d.cosFalloffStart) cosTheta_e = 0.999f;
+            lb.cosTheta_o = d.cosFalloffStart;
+            lb.cosTheta_e = cosTheta_e;
+        }
+        if (lb.phi > 0) {
+            bvhLights.push_back({(int)s.areaLights.size() + i, lb});
             b.allLightBounds.Add(lb.bounds);
         }
     }

@@ -347,6 +347,8 @@ class Parser {
         Mat4 worldFromLight;
     };
     std::vector<PendingLight> lights;
+    void DeltaLight(PendingLight &l, std::vector<DeltaLightDesc> &pointSpot, std::vector<DeltaLightDesc> &distants,
+                    std::vector<int> &distantEntry, std::vector<std::pair<int, int>> &lsOrder);
     struct PendingMedium {
         std::string name, type;
         ParamSet params;
@@ -1361,8 +1363,19 @@ void Parser::Finish() {
             }
         }
     }
+    // LightSource lights in the order written (pbrt appends them after the area lights,
+    // scene.cpp:1288-1348); point and spot lights join the light BVH, distant and uniform
+    // infinite lights the infinite-light list (lightsamplers.cpp BVHLightSampler ctor)
+    std::vector<std::pair<int, int>> lsOrder;  // (0: delta light j, 1: infinite-list entry j)
+    std::vector<DeltaLightDesc> pointSpot, distants;
+    std::vector<int> distantEntry;  // infinite-list entry of each distant light
     for (PendingLight &l : lights) {
+        if (l.type == "point" || l.type == "spot" || l.type == "distant") {
+            DeltaLight(l, pointSpot, distants, distantEntry, lsOrder);
+            continue;
+        }
         if (l.type != "infinite") throw Error(l.params.loc + ": light \"" + l.type + "\" not supported yet");
+        lsOrder.push_back({1, (int)scene.infiniteLights.size()});
         Param *L = l.params.Find("L");
         if (l.params.Find("filename")) throw Error(l.params.loc + ": image infinite lights not supported yet");
         InfiniteLightDesc il;
@@ -1384,8 +1397,131 @@ void Parser::Finish() {
         l.params.CheckUnused();
         scene.infiniteLights.push_back(il);
     }
-    if (scene.areaLights.empty() && scene.infiniteLights.empty()) throw Error("No light sources specified");
-    if (scene.areaLights.size() + scene.infiniteLights.size() == 1) scene.uniformLightSampler = true;
+    scene.nPointSpot = (int)pointSpot.size();
+    scene.deltaLights = pointSpot;
+    for (size_t j = 0; j < distants.size(); ++j) {
+        scene.infiniteLights[distantEntry[j]].distant = (int)scene.deltaLights.size();
+        scene.deltaLights.push_back(distants[j]);
+    }
+    const int nA = (int)scene.areaLights.size(), nPS = scene.nPointSpot;
+    scene.uniformOrder.clear();
+    for (int i = 0; i < nA; ++i) scene.uniformOrder.push_back(i);
+    for (auto &o : lsOrder) scene.uniformOrder.push_back(o.first == 0 ? nA + o.second : nA + nPS + o.second);
+    // Bounds3f::BoundingSphere of the aggregate's bounds (every triangle), DistantLight::Preprocess
+    {
+        V3 mn(kInfinity, kInfinity, kInfinity), mx(-kInfinity, -kInfinity, -kInfinity);
+        for (auto &t : scene.tris)
+            for (int k = 0; k < 3; ++k) {
+                const V3 v = scene.verts[t[k]];
+                mn = V3(std::fmin(mn.x, v.x), std::fmin(mn.y, v.y), std::fmin(mn.z, v.z));
+                mx = V3(std::fmax(mx.x, v.x), std::fmax(mx.y, v.y), std::fmax(mx.z, v.z));
+            }
+        const V3 c = (mn + mx) / 2;
+        const bool inside = c.x >= mn.x && c.x <= mx.x && c.y >= mn.y && c.y <= mx.y && c.z >= mn.z && c.z <= mx.z;
+        scene.sceneRadius = inside ? Distance(c, mx) : 0;
+    }
+    const size_t nLights = scene.areaLights.size() + scene.deltaLights.size() +
+                           (scene.infiniteLights.size() - distants.size());
+    if (nLights == 0) throw Error("No light sources specified");
+    if (nLights == 1) scene.uniformLightSampler = true;
+}
+
+// PointLight::Create / SpotLight::Create / DistantLight::Create (lights.cpp:192-276,
+// 1464-1495): I or L as an illuminant spectrum, scale /= SpectrumToPhotometric, "power" (point,
+// spot) or "illuminance" (distant), and the render-space geometry of renderFromLight * t.
+void Parser::DeltaLight(PendingLight &l, std::vector<DeltaLightDesc> &pointSpot, std::vector<DeltaLightDesc> &distants,
+                        std::vector<int> &distantEntry, std::vector<std::pair<int, int>> &lsOrder) {
+    ParamSet &ps = l.params;
+    const bool distant = l.type == "distant";
+    Param *I = ps.Find(distant ? "L" : "I");
+    std::array<float, 311> dense = GetSpectralData().denseD65;
+    float photometric = GetSpectralData().photometricD65;
+    if (I && I->type == "rgb" && I->nums.size() == 3) {
+        dense = DenseRGBIlluminant((float)I->nums[0], (float)I->nums[1], (float)I->nums[2]);
+    } else if (I && I->type == "spectrum" && !I->nums.empty()) {
+        dense = DensePiecewiseLinear(I->nums, ps.loc);
+        photometric = PhotometricOf(dense);
+    } else if (I && I->type == "blackbody" && I->nums.size() == 1) {
+        const float T = (float)I->nums[0];
+        for (int i = 0; i < 311; ++i) dense[i] = BlackbodyNormalized(395.f + i, T);
+        photometric = PhotometricOf(dense);
+    } else if (I) {
+        throw Error(ps.loc + ": " + l.type + " light " + (distant ? "L" : "I") + " must be rgb, spectrum or blackbody");
+    }
+    scene.denseSpectra.push_back(dense);
+    DeltaLightDesc d;
+    d.spectrum = (int)scene.denseSpectra.size() - 1;
+    float sc = (float)ps.GetFloat("scale", 1);
+    auto point3 = [&](const char *name, V3 def) {
+        Param *q = ps.Find(name, "point3");
+        if (!q) q = ps.Find(name, "point");
+        if (!q) return def;
+        if (q->nums.size() != 3) throw Error(ps.loc + ": \"" + std::string(name) + "\" needs 3 values");
+        return V3((float)q->nums[0], (float)q->nums[1], (float)q->nums[2]);
+    };
+    const Mat4 rfl = Mul(scene.camera.renderFromWorld, l.worldFromLight);
+    auto xfPoint = [&](const Mat4 &m, V3 p) {
+        double r[4];
+        for (int i = 0; i < 4; ++i) r[i] = m[i][0] * p.x + m[i][1] * p.y + m[i][2] * p.z + m[i][3];
+        if (r[3] == 1) return V3((float)r[0], (float)r[1], (float)r[2]);
+        return V3((float)(r[0] / r[3]), (float)(r[1] / r[3]), (float)(r[2] / r[3]));
+    };
+    auto xfVector = [&](const Mat4 &m, V3 v) {
+        return V3((float)(m[0][0] * v.x + m[0][1] * v.y + m[0][2] * v.z),
+                  (float)(m[1][0] * v.x + m[1][1] * v.y + m[1][2] * v.z),
+                  (float)(m[2][0] * v.x + m[2][1] * v.y + m[2][2] * v.z));
+    };
+    sc /= photometric;
+    if (l.type == "point") {
+        d.type = kDeltaPoint;
+        const float phi_v = (float)ps.GetFloat("power", -1);
+        if (phi_v > 0) sc *= phi_v / (4 * kPi);
+        d.p = xfPoint(rfl, point3("from", V3(0, 0, 0)));
+    } else if (l.type == "spot") {
+        d.type = kDeltaSpot;
+        const float coneangle = (float)ps.GetFloat("coneangle", 30.);
+        const float conedelta = (float)ps.GetFloat("conedeltaangle", 5.);
+        const V3 from = point3("from", V3(0, 0, 0)), to = point3("to", V3(0, 0, 1));
+        // dirToZ = Frame::FromZ(Normalize(to - from)): rows x, y, z (CoordinateSystem)
+        const V3 z = Normalize(to - from);
+        const float sign = std::copysign(1.f, z.z), a = -1 / (sign + z.z), b = z.x * z.y * a;
+        const V3 x(1 + sign * z.x * z.x * a, sign * b, -sign * z.x), y(b, sign + z.y * z.y * a, -z.y);
+        d.p = xfPoint(rfl, from);
+        d.w = Normalize(xfVector(rfl, z));  // renderFromLight(0, 0, 1): Inverse(dirToZ) maps z to the axis
+        // renderFromLight.ApplyInverse on vectors: dirToZ (rows x, y, z) times lightFromRender
+        const Mat4 lfr = Inverse4(rfl);
+        const V3 rows[3] = {x, y, z};
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j)
+                d.m[i][j] = (float)(rows[i].x * lfr[0][j] + rows[i].y * lfr[1][j] + rows[i].z * lfr[2][j]);
+        d.cosFalloffEnd = std::cos(coneangle * (kPi / 180));
+        d.cosFalloffStart = std::cos((coneangle - conedelta) * (kPi / 180));
+        const float phi_v = (float)ps.GetFloat("power", -1);
+        if (phi_v > 0) {
+            const float k_e = 2 * kPi * ((1 - d.cosFalloffStart) + (d.cosFalloffStart - d.cosFalloffEnd) / 2);
+            sc *= phi_v / k_e;
+        }
+    } else {
+        d.type = kDeltaDistant;
+        const V3 from = point3("from", V3(0, 0, 0)), to = point3("to", V3(0, 0, 1));
+        d.w = xfVector(rfl, Normalize(from - to));  // renderFromLight(0, 0, 1); SampleLi normalises it
+        const float E_v = (float)ps.GetFloat("illuminance", -1);
+        if (E_v > 0) sc *= E_v;
+    }
+    d.scale = sc;
+    ps.CheckUnused();
+    if (distant) {
+        lsOrder.push_back({1, (int)scene.infiniteLights.size()});
+        InfiniteLightDesc il;
+        il.spectrum = d.spectrum;
+        il.scale = d.scale;
+        distantEntry.push_back((int)scene.infiniteLights.size());
+        scene.infiniteLights.push_back(il);  // .distant set once the delta-light order is final
+        distants.push_back(d);
+    } else {
+        lsOrder.push_back({0, (int)pointSpot.size()});
+        pointSpot.push_back(d);
+    }
 }
 
 SceneDesc LoadPbrtString(const std::string &text, const std::string &baseDir,

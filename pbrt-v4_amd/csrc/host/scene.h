@@ -95,9 +95,26 @@ struct AreaLightDesc {
     float area = 0;
 };
 
+// An entry of BVHLightSampler's infinite-light list (lights without bounds, lightsamplers.cpp):
+// a UniformInfiniteLight, or a DistantLight (distant = its index in SceneDesc::deltaLights)
 struct InfiniteLightDesc {
     int spectrum = -1;
     float scale = 1;
+    int distant = -1;
+};
+
+// PointLight / SpotLight / DistantLight (lights.h:200-300, 740-800; lights.cpp:192-276, 1376-1495)
+// in render space: deltaLights holds the point and spot lights first (light-BVH members, global
+// light index nAreaLights + i), then the distant lights (members of the infinite-light list)
+enum DeltaLightType { kDeltaPoint = 0, kDeltaSpot = 1, kDeltaDistant = 2 };
+struct DeltaLightDesc {
+    int type = kDeltaPoint;
+    V3 p;                 // point / spot: renderFromLight(0, 0, 0)
+    V3 w;                 // spot: Normalize(renderFromLight(0, 0, 1)); distant: renderFromLight(0, 0, 1)
+    float m[3][3] = {};   // spot: upper 3x3 of renderFromLight's inverse (Transform::ApplyInverse)
+    float cosFalloffStart = 1, cosFalloffEnd = 1;
+    int spectrum = -1;    // dense spectrum of I (point, spot) or L (distant)
+    float scale = 1;      // final scale (photometric normalisation, power / illuminance applied)
 };
 
 struct CameraDesc {
@@ -155,6 +172,12 @@ struct SceneDesc {
                                                     // only when inside != outside
     std::vector<AreaLightDesc> areaLights;
     std::vector<InfiniteLightDesc> infiniteLights;
+    std::vector<DeltaLightDesc> deltaLights;  // point and spot lights first, then distant lights
+    int nPointSpot = 0;
+    // pbrt's light order (area lights, then LightSource lights as written) -> this scene's global
+    // light index (area, point/spot, infinite list); UniformLightSampler picks in pbrt's order
+    std::vector<int> uniformOrder;
+    float sceneRadius = 0;  // Bounds3f::BoundingSphere of the scene bounds (DistantLight::Preprocess)
     std::vector<std::array<float, 311>> denseSpectra;
     std::vector<PLSpectrumDesc> plSpectra;
     std::array<float, 311> sensorX, sensorY, sensorZ;  // r_bar/g_bar/b_bar of "cie1931"
@@ -162,7 +185,7 @@ struct SceneDesc {
     // BVH light sampler (lightsamplers.cpp:112-236); unused when one light -> uniform
     bool uniformLightSampler = false;
     std::vector<LightBVHNodeDesc> lightNodes;
-    std::vector<uint32_t> lightBitTrail;  // per area light
+    std::vector<uint32_t> lightBitTrail;  // per light-BVH light (area, then point/spot)
 
     // sampler: 0 = HaltonSampler (permutedigits), 1 = ZSobolSampler (samplers.h:225-370)
     int samplerType = 1;

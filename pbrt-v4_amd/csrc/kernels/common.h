@@ -859,11 +859,11 @@ __device__ inline float TrianglePDF(V3 p0, V3 p1, V3 p2, bool flip, const TriSha
 template <typename NodeT>
 __device__ inline bool SampleLightT(const DeviceScene &S, const NodeT *lightNodes, V3 p, V3 ns, float u, int *light,
                                     float *pmfOut) {
-    int nAll = S.nAreaLights + S.nInfinite;
+    int nAll = S.nAreaLights + S.nPointSpot + S.nInfinite;
     if (S.uniformLightSampler) {
         if (nAll == 0) return false;
         int li = min((int)(u * nAll), nAll - 1);
-        *light = li;
+        *light = S.uniformOrder[li];  // pbrt's light order -> global index
         *pmfOut = 1.f / nAll;
         return true;
     }
@@ -872,7 +872,7 @@ __device__ inline bool SampleLightT(const DeviceScene &S, const NodeT *lightNode
         u /= pInfinite;
         int index = min((int)(u * S.nInfinite), S.nInfinite - 1);
         *pmfOut = pInfinite / S.nInfinite;
-        *light = S.nAreaLights + index;
+        *light = S.nAreaLights + S.nPointSpot + index;
         return true;
     }
     if (S.nLightNodes == 0) return false;
@@ -905,9 +905,9 @@ __device__ inline bool SampleLight(const DeviceScene &S, V3 p, V3 ns, float u, i
 }
 
 __device__ inline float LightPMF(const DeviceScene &S, V3 p, V3 ns, int light) {
-    int nAll = S.nAreaLights + S.nInfinite;
+    int nAll = S.nAreaLights + S.nPointSpot + S.nInfinite;
     if (S.uniformLightSampler) return nAll ? 1.f / nAll : 0.f;
-    uint32_t bitTrail = light < S.nAreaLights ? S.lightBitTrail[light] : 0xffffffffu;
+    uint32_t bitTrail = light < S.nAreaLights + S.nPointSpot ? S.lightBitTrail[light] : 0xffffffffu;
     if (bitTrail == 0xffffffffu) return 1.f / (S.nInfinite + (S.nLightNodes == 0 ? 0 : 1));
     float pInfinite = float(S.nInfinite) / float(S.nInfinite + (S.nLightNodes == 0 ? 0 : 1));
     float pmf = 1 - pInfinite;
@@ -924,6 +924,86 @@ __device__ inline float LightPMF(const DeviceScene &S, V3 p, V3 ns, int light) {
     return pmf;
 }
 
+
+// One light sample for a surface vertex's NEE (surfscatter.cpp:254-285, light.SampleLi with
+// allowIncompletePDF): DiffuseAreaLight::SampleLi through Triangle::Sample (lights.cpp:743-775),
+// PointLight / SpotLight / DistantLight::SampleLi (lights.h).  The sample's radiance at a
+// wavelength is scale * spectrum(lambda), divided by d2 for point and spot lights (pbrt's
+// SampledSpectrum / DistanceSquared); a UniformInfiniteLight returns no sample.
+struct LiSample {
+    V3 wi, lp, lpe, ln;  // direction, and the light point (error, normal) for SpawnRayTo
+    float pdf;           // ls->pdf (1 for delta lights)
+    float scale, d2;     // d2 = 1: no division
+    int spectrum;
+    bool delta;          // IsDeltaLight: the BSDF's MIS pdf is 0
+};
+__device__ inline float SmoothStepf(float x, float a, float b) {
+    if (a == b) return (x < a) ? 0 : 1;
+    const float t = Clampf((x - a) / (b - a), 0, 1);
+    return t * t * (3 - 2 * t);
+}
+template <bool Lean>
+__device__ inline bool SampleLiSurface(const DeviceScene &S, const DeviceAreaLight *lightsL, int li, V3 cp, V3 n,
+                                       V3 ns, float u0, float u1, LiSample *ls) {
+    if (li < S.nAreaLights) {
+        const DeviceAreaLight &Ld = lightsL[li];
+        V3 q0(Ld.v0.x, Ld.v0.y, Ld.v0.z), q1(Ld.v1.x, Ld.v1.y, Ld.v1.z), q2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
+        TriShading lsh;
+        const bool lhas = !Lean && LoadTriShading(S, __float_as_int(Ld.v0.w), &lsh);
+        float lpdf;
+        if (!SampleTriangle(q0, q1, q2, Ld.flip, lhas ? &lsh : nullptr, cp, n, ns, u0, u1, &ls->lp, &ls->lpe, &ls->ln,
+                            &lpdf) ||
+            lpdf == 0 || LengthSquared(ls->lp - cp) == 0)
+            return false;
+        ls->wi = Normalize(ls->lp - cp);
+        if (!(Ld.twoSided || DotN(ls->ln, -ls->wi) >= 0)) return false;  // DiffuseAreaLight::L is 0
+        ls->pdf = lpdf;
+        ls->scale = Ld.scale;
+        ls->d2 = 1;
+        ls->spectrum = Ld.spectrum;
+        ls->delta = false;
+        return true;
+    }
+    if constexpr (Lean) {
+        return false;  // lean launches have no point, spot or distant lights
+    } else {
+        const int k = li - S.nAreaLights;
+        int di = k;
+        if (k >= S.nPointSpot) {
+            di = S.infDistant[k - S.nPointSpot];
+            if (di < 0) return false;  // UniformInfiniteLight::SampleLi(allowIncompletePDF) = {}
+        }
+        const DeviceDeltaLight &D = S.delta[di];
+        const int type = __float_as_int(D.p.w);
+        ls->pdf = 1;
+        ls->delta = true;
+        ls->spectrum = __float_as_int(D.cone.z);
+        ls->lpe = V3(0, 0, 0);
+        ls->ln = V3(0, 0, 0);
+        if (type == 2) {  // DistantLight: wi = Normalize(renderFromLight(0, 0, 1))
+            ls->wi = Normalize(V3(D.w.x, D.w.y, D.w.z));
+            ls->lp = cp + ls->wi * (2 * S.sceneRadius);
+            ls->scale = D.w.w;
+            ls->d2 = 1;
+            return true;
+        }
+        const V3 p(D.p.x, D.p.y, D.p.z);
+        ls->wi = Normalize(p - cp);
+        ls->lp = p;
+        ls->d2 = DistanceSquared(p, cp);
+        float sc = D.w.w;
+        if (type == 1) {  // SpotLight::I: SmoothStep(CosTheta(wLight), cosEnd, cosStart) * scale
+            const V3 v = -ls->wi;
+            const V3 wl = Normalize(V3(D.m0.x * v.x + D.m0.y * v.y + D.m0.z * v.z,
+                                       D.m1.x * v.x + D.m1.y * v.y + D.m1.z * v.z,
+                                       D.m2.x * v.x + D.m2.y * v.y + D.m2.z * v.z));
+            sc = SmoothStepf(wl.z, D.cone.y, D.cone.x) * sc;
+            if (sc == 0) return false;  // Li is 0 at every wavelength
+        }
+        ls->scale = sc;
+        return true;
+    }
+}
 
 // Streaming form of the per-wavelength work: lambda_i, R_i, Le_i and beta_i are produced
 // inside each 31-iteration loop (lambda by pbrt's sequential +10 nm recurrence, R by the

@@ -89,6 +89,14 @@ struct DeviceMedia {
     const int *primMedium;
 };
 
+// PointLight / SpotLight / DistantLight in render space (scene.h DeltaLightDesc): p.xyz position
+// (.w type bits: 0 point, 1 spot, 2 distant), w.xyz spot axis or direction toward a distant
+// light (.w scale), cone = cosFalloffStart, cosFalloffEnd, spectrum bits; m0..m2: rows of
+// renderFromLight's inverse 3x3 (spot, Transform::ApplyInverse on vectors)
+struct DeviceDeltaLight {
+    float4 p, w, cone, m0, m1, m2;
+};
+
 struct DeviceScene {
     // geometry (leaf order)
     const BVH8Node *nodes;
@@ -126,10 +134,17 @@ struct DeviceScene {
     const float *lightArea;
     const DeviceAreaLight *lights;  // [nAreaLights]
     const uint32_t *lightBitTrail;  // 0xffffffff when not in the light BVH
-    // infinite (uniform) lights
+    // infinite-light list (UniformInfiniteLight, or DistantLight when infDistant[j] >= 0)
     int nInfinite;
     const int *infSpectrum;
     const float *infScale;
+    const int *infDistant;
+    // point / spot / distant lights: the first nPointSpot are light-BVH members with global light
+    // index nAreaLights + i; the infinite-list entry j has global index nAreaLights + nPointSpot + j
+    int nDelta, nPointSpot;
+    const DeviceDeltaLight *delta;
+    const int *uniformOrder;  // UniformLightSampler: pbrt's light order -> global index
+    float sceneRadius;
     // light sampler
     int uniformLightSampler;
     const DeviceLightNode *lightNodes;

@@ -134,6 +134,7 @@ __global__ void __launch_bounds__(kBlock) k_escaped(DeviceScene S, PathState st,
         float rgb[3] = {0, 0, 0};
         bool any = false;
         for (int li = 0; li < S.nInfinite; ++li) {
+            if (S.infDistant[li] >= 0) continue;  // a DistantLight is no Infinite-type light (no Le)
             const float *dense = S.dense + S.infSpectrum[li] * kDenseN;
             float scale = S.infScale[li];
             float sx = 0, sy = 0, sz = 0, lam = rec.lambda0[ri];
@@ -245,11 +246,14 @@ __global__ void __launch_bounds__(kBlock) k_emissive(DeviceScene S, PathState st
 // beta = bf * |cos| / pdf (lanes that do not scatter carry |cos| = pdf = 1) into bf's LDS slot,
 // with max(beta * etaScale / avg(r_u)) for RR.  neeNz: Le != 0 somewhere; betaNz: new beta != 0
 // somewhere.
-template <typename FD>
+// DivD2: the light's radiance is divided by d2 per wavelength (point and spot lights; d2 = 1,
+// an exact no-op, for the other lanes).
+template <bool DivD2, typename FD>
 __device__ inline void ShadeSpectralPass(int depth, const FD *dense, const LdsF4 *sensor4, float *bf, float4 mc,
-                                         bool constant, float lambda0, float scale, float absdotL, float invDenom,
-                                         float absdotB, float pdf, float rpdf, bool pdfOk, float etaScale,
-                                         SensorAcc *acc, bool *neeNz, bool *betaNz, float *mx) {
+                                         bool constant, float lambda0, float scale, float d2, float rd2, bool d2Ok,
+                                         float absdotL, float invDenom, float absdotB, float pdf, float rpdf,
+                                         bool pdfOk, float etaScale, SensorAcc *acc, bool *neeNz, bool *betaNz,
+                                         float *mx) {
     const float avgRu = Avg31(1.f);
     bool nzL = false, nzB = false;
     float m = -kInfinity;
@@ -258,7 +262,8 @@ __device__ inline void ShadeSpectralPass(int depth, const FD *dense, const LdsF4
         const float R = Reflectance(mc, constant, it.lam);
         const float bfi = (depth > 0 ? bf[it.i * kBlock] : 1.f) * (R * kInvPi);
         const int off = DenseOffset(it.lam);
-        const float Le = scale * (off < 0 ? 0.f : float(dense[off]));
+        float Le = scale * (off < 0 ? 0.f : float(dense[off]));
+        if constexpr (DivD2) Le = DivByRcp(Le, d2, rd2, d2Ok);
         nzL |= Le != 0;
         acc->Add(sensor4, off, bfi * absdotL * Le * invDenom, it.i == 0);
         const float nbv = DivByRcp(bfi * absdotB, pdf, rpdf, pdfOk);
@@ -481,7 +486,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                 // ---- light sample geometry (surfscatter.cpp:254-326)
                 bool nee = false;
                 int spec = 0;
-                float scale = 0, absdotL = 0, invDenom = 0;
+                float scale = 0, absdotL = 0, invDenom = 0, d2 = 1;
                 if (Rnz) {
                     V3 cp = OffsetRayOrigin(pi, pe, n, wo);  // reflective, not transmissive
                     int li;
@@ -490,33 +495,25 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                         (Lean || lay.lightsInLds)
                             ? SampleLightT(SL, (const LdsLightNode *)SL.lightNodes, cp, ns, dUc, &li, &lpmf)
                             : SampleLightT(SL, S.lightNodes, cp, ns, dUc, &li, &lpmf);
-                    if (sampled && li < S.nAreaLights) {
-                        const DeviceAreaLight &Ld = lightsL[li];
-                        V3 q0(Ld.v0.x, Ld.v0.y, Ld.v0.z), q1(Ld.v1.x, Ld.v1.y, Ld.v1.z), q2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
-                        float lpdf;
-                        V3 lp, lpe, ln;
-                        TriShading lsh;
-                        const bool lhas = !Lean && LoadTriShading(S, __float_as_int(Ld.v0.w), &lsh);
-                        if (SampleTriangle(q0, q1, q2, Ld.flip, lhas ? &lsh : nullptr, cp, n, ns, dU0, dU1, &lp, &lpe,
-                                           &ln, &lpdf) &&
-                            lpdf != 0 && LengthSquared(lp - cp) != 0) {
-                            V3 wi = Normalize(lp - cp);
-                            V3 wiL = frame.ToLocal(wi);
-                            if ((Ld.twoSided || DotN(ln, -wi) >= 0) && woL.z != 0 && woL.z * wiL.z > 0) {
-                                spec = Ld.spectrum;
-                                scale = Ld.scale;
-                                absdotL = AbsDotN(ns, wi);
-                                float lightPDF = lpdf * lpmf;
-                                float bsdfPDF = CosineHemispherePDF(fabsf(wiL.z));
-                                float denom = Avg31(bsdfPDF + lightPDF);
-                                invDenom = 1 / denom;
-                                nee = true;
-                                // SpawnRayTo(pi, n, time, pLight.pi, pLight.n) (ray.h:106-111), formed
-                                // now so the light point is not held through the wavelength pass
-                                sOrg = OffsetRayOrigin(pi, pe, n, lp - pi);
-                                V3 pt = OffsetRayOrigin(lp, lpe, ln, sOrg - lp);
-                                sDir = pt - sOrg;
-                            }
+                    LiSample ls;
+                    if (sampled && SampleLiSurface<Lean>(S, lightsL, li, cp, n, ns, dU0, dU1, &ls)) {
+                        const V3 wi = ls.wi;
+                        const V3 wiL = frame.ToLocal(wi);
+                        if (woL.z != 0 && woL.z * wiL.z > 0) {  // DiffuseBxDF::f != 0
+                            spec = ls.spectrum;
+                            scale = ls.scale;
+                            d2 = ls.d2;
+                            absdotL = AbsDotN(ns, wi);
+                            float lightPDF = ls.pdf * lpmf;
+                            float bsdfPDF = ls.delta ? 0.f : CosineHemispherePDF(fabsf(wiL.z));
+                            float denom = Avg31(bsdfPDF + lightPDF);
+                            invDenom = 1 / denom;
+                            nee = true;
+                            // SpawnRayTo(pi, n, time, pLight.pi, pLight.n) (ray.h:106-111), formed
+                            // now so the light point is not held through the wavelength pass
+                            sOrg = OffsetRayOrigin(pi, pe, n, ls.lp - pi);
+                            V3 pt = OffsetRayOrigin(ls.lp, ls.lpe, ls.ln, sOrg - ls.lp);
+                            sDir = pt - sOrg;
                         }
                     }
                 }
@@ -551,14 +548,20 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the beta LDS-DMA has landed
                     const bool pdfOk = DivFastOk(pdf);
                     float *bf = bfLds + threadIdx.x;
-                    if (Lean || lay.denseInLds)
-                        ShadeSpectralPass(depth, (const LdsF *)denseLds + spec * kDenseN, sensorL, bf, mc, constant,
-                                          lambda0, scale, absdotL, invDenom, absdotB, pdf, rpdf, pdfOk, etaScale, &acc,
-                                          &neeNz, &betaNz, &mx);
+                    const float rd2 = 1 / d2;
+                    const bool d2Ok = DivFastOk(d2);
+                    if (Lean || (lay.denseInLds && S.nPointSpot == 0))
+                        ShadeSpectralPass<false>(depth, (const LdsF *)denseLds + spec * kDenseN, sensorL, bf, mc,
+                                                 constant, lambda0, scale, d2, rd2, d2Ok, absdotL, invDenom, absdotB, pdf,
+                                                 rpdf, pdfOk, etaScale, &acc, &neeNz, &betaNz, &mx);
+                    else if (lay.denseInLds)
+                        ShadeSpectralPass<true>(depth, (const LdsF *)denseLds + spec * kDenseN, sensorL, bf, mc,
+                                                constant, lambda0, scale, d2, rd2, d2Ok, absdotL, invDenom, absdotB, pdf,
+                                                rpdf, pdfOk, etaScale, &acc, &neeNz, &betaNz, &mx);
                     else
-                        ShadeSpectralPass(depth, S.dense + spec * kDenseN, sensorL, bf, mc, constant, lambda0, scale,
-                                          absdotL, invDenom, absdotB, pdf, rpdf, pdfOk, etaScale, &acc, &neeNz, &betaNz,
-                                          &mx);
+                        ShadeSpectralPass<true>(depth, S.dense + spec * kDenseN, sensorL, bf, mc, constant, lambda0,
+                                                scale, d2, rd2, d2Ok, absdotL, invDenom, absdotB, pdf, rpdf, pdfOk,
+                                                etaScale, &acc, &neeNz, &betaNz, &mx);
                 }
                 SEC_MARK(st, 5);
                 if (nee && neeNz) {
@@ -730,19 +733,14 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
                 else if (transmissive && reflective) cp = OffsetRayOrigin(pi, pe, n, -wo);
                 int li;
                 float lpmf;
-                if (SampleLight(T.SL, cp, ns, rs.dUc, &li, &lpmf) && li < S.nAreaLights) {
-                    const DeviceAreaLight &Ld = T.lightsL[li];
-                    V3 q0(Ld.v0.x, Ld.v0.y, Ld.v0.z), q1(Ld.v1.x, Ld.v1.y, Ld.v1.z), q2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
-                    V3 lp, lpe, ln;
-                    float lpdf;
-                    TriShading lsh;
-                    const bool lhas = LoadTriShading(S, __float_as_int(Ld.v0.w), &lsh);
-                    if (SampleTriangle(q0, q1, q2, Ld.flip, lhas ? &lsh : nullptr, cp, n, ns, rs.dU0, rs.dU1, &lp,
-                                       &lpe, &ln, &lpdf) &&
-                        lpdf != 0 && LengthSquared(lp - cp) != 0) {
-                        const V3 wi = Normalize(lp - cp);
+                LiSample ls;
+                if (SampleLight(T.SL, cp, ns, rs.dUc, &li, &lpmf) &&
+                    SampleLiSurface<false>(S, T.lightsL, li, cp, n, ns, rs.dU0, rs.dU1, &ls)) {
+                    const V3 lp = ls.lp, lpe = ls.lpe, ln = ls.ln;
+                    {
+                        const V3 wi = ls.wi;
                         const V3 wiL = frame.ToLocal(wi);
-                        if ((Ld.twoSided || DotN(ln, -wi) >= 0) && woL.z != 0) {
+                        if (woL.z != 0) {
                             // BSDF::f / BSDF::PDF (bsdf.h:60-135)
                             float fd = 0, bsdfPDF = 0;
                             ConductorTerms ct{};
@@ -757,17 +755,21 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
                             }
                             if (fAny) {
                                 const float absdot = AbsDotN(ns, wi);
-                                const float lightPDF = lpdf * lpmf;
+                                const float lightPDF = ls.pdf * lpmf;
+                                if (ls.delta) bsdfPDF = 0;  // IsDeltaLight: no BSDF MIS weight
                                 const float invDenom = 1 / Avg31(bsdfPDF + lightPDF);
-                                const float *dense = lay.denseInLds ? nullptr : S.dense + Ld.spectrum * kDenseN;
-                                const LdsF *denseL = (const LdsF *)T.denseLds + Ld.spectrum * kDenseN;
+                                const float *dense = lay.denseInLds ? nullptr : S.dense + ls.spectrum * kDenseN;
+                                const LdsF *denseL = (const LdsF *)T.denseLds + ls.spectrum * kDenseN;
+                                const float rd2 = 1 / ls.d2;
+                                const bool d2Ok = DivFastOk(ls.d2);
                                 SensorAcc acc;
                                 bool nz = false;
 #pragma unroll 2
                                 for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next()) {
                                     const int off = DenseOffset(it.lam);
-                                    const float Le =
-                                        Ld.scale * (off < 0 ? 0.f : (lay.denseInLds ? float(denseL[off]) : dense[off]));
+                                    float Le =
+                                        ls.scale * (off < 0 ? 0.f : (lay.denseInLds ? float(denseL[off]) : dense[off]));
+                                    if (S.nPointSpot > 0) Le = DivByRcp(Le, ls.d2, rd2, d2Ok);
                                     nz |= Le != 0;
                                     float f = fd;
                                     if constexpr (MT == kMatConductorT) {

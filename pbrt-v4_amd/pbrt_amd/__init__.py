@@ -75,6 +75,9 @@ class SceneFlat(ctypes.Structure):
         ("medium_values", ctypes.POINTER(ctypes.c_float)), ("tri_medium", ctypes.POINTER(ctypes.c_int16)),
         ("filter_type", ctypes.c_int), ("filter_a", ctypes.c_float), ("filter_b", ctypes.c_float),
         ("material_layer", ctypes.POINTER(ctypes.c_float)),
+        ("n_delta_lights", ctypes.c_int), ("n_point_spot", ctypes.c_int),
+        ("delta_lights", ctypes.POINTER(ctypes.c_float)), ("inf_distant", ctypes.POINTER(ctypes.c_int32)),
+        ("uniform_order", ctypes.POINTER(ctypes.c_int32)), ("scene_radius", ctypes.c_float),
     ]
 
 

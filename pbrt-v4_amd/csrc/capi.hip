@@ -452,7 +452,7 @@ static void BuildDevice(pbrt_context *c) {
         sensor4[4 * i + 2] = s.sensorZ[i];
     }
     c->sensor4.Upload(sensor4);
-    std::vector<uint32_t> bt(s.areaLights.size(), 0xffffffffu);
+    std::vector<uint32_t> bt(s.areaLights.size() + s.nPointSpot, 0xffffffffu);  // light-BVH members
     if (!s.uniformLightSampler)
         for (auto &n : s.lightNodes)
             if (n.isLeaf) bt[n.childOrLight] = s.lightBitTrail[n.childOrLight];
@@ -530,9 +530,6 @@ static void BuildDevice(pbrt_context *c) {
     if (S.dispersive && !s.media.empty())
         throw std::runtime_error("a dielectric with spectral eta (dispersion) together with participating media is not supported yet");
     c->volumetric = c->volumetric || S.dispersive;
-    if (c->volumetric && !s.deltaLights.empty())
-        throw std::runtime_error("point, spot and distant lights together with media, layered, thin-dielectric, "
-                                 "diffuse-transmission or dispersive materials are not supported yet");
     S.media.cameraMedium = s.cameraMedium;
     S.media.allGrey = 1;
     for (size_t m = 0; m < s.media.size(); ++m) {

@@ -912,16 +912,40 @@ __device__ inline void WriteShadow(const VolState &v, int NR, int j, const Shado
 
 // One area light sample for a reference point (BVHLightSampler::Sample + DiffuseAreaLight::SampleLi
 // with allowIncompletePDF, lights.cpp:743-775): false when no light / no sample / Le = 0
+// Point, spot and distant lights take the same route through SampleLiSurface (common.h): pdf 1,
+// a light point without error or normal, radiance scale * I(lambda) [/ d2]; delta is set.
 struct AreaLightSample {
     int light;
-    V3 p, pErr, n;
+    V3 p, pErr, n, wi;
     float pdf;  // shape pdf * light-choice pmf
+    bool delta;
 };
 __device__ inline bool SampleAreaLight(const DeviceScene &S, V3 refP, V3 refN, V3 refNs, float uc, float u0, float u1,
                                        const WaveOffsets &wo, AreaLightSample *out, float Le[kNS]) {
     int li;
     float lpmf;
-    if (!SampleLight(S, refP, refNs, uc, &li, &lpmf) || li >= S.nAreaLights) return false;
+    if (!SampleLight(S, refP, refNs, uc, &li, &lpmf)) return false;
+    if (li >= S.nAreaLights) {
+        LiSample ls;
+        if (!SampleLiSurface<false>(S, S.lights, li, refP, refN, refNs, u0, u1, &ls)) return false;
+        const float rd2 = 1 / ls.d2;
+        const bool ok = DivFastOk(ls.d2);
+        bool nz = false;
+#pragma unroll
+        for (int i = 0; i < kNS; ++i) {
+            Le[i] = DivByRcp(ls.scale * DenseAt(S, ls.spectrum, wo.off[i]), ls.d2, rd2, ok);
+            nz |= Le[i] != 0;
+        }
+        if (!nz) return false;
+        out->light = li;
+        out->p = ls.lp;
+        out->pErr = ls.lpe;
+        out->n = ls.ln;
+        out->wi = ls.wi;
+        out->pdf = ls.pdf * lpmf;
+        out->delta = true;
+        return true;
+    }
     const DeviceAreaLight Ld = S.lights[li];
     const V3 q0(Ld.v0.x, Ld.v0.y, Ld.v0.z), q1(Ld.v1.x, Ld.v1.y, Ld.v1.z), q2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
     TriShading lsh;
@@ -944,7 +968,9 @@ __device__ inline bool SampleAreaLight(const DeviceScene &S, V3 refP, V3 refN, V
     out->p = lp;
     out->pErr = lpe;
     out->n = ln;
+    out->wi = wi;
     out->pdf = lpdf * lpmf;
+    out->delta = false;
     return true;
 }
 
@@ -973,17 +999,45 @@ __device__ inline void AddSpecToL(const DeviceScene &S, const PathState &st, int
 // An area-light sample for a reference point (BVHLightSampler::Sample, then
 // DiffuseAreaLight::SampleLi with allowIncompletePDF, lights.cpp:743-775); false when no light,
 // no sample, or Le = 0 at every wavelength.  Le_i = scale * dense[spectrum][off_i] when facing.
+// Point, spot and distant lights through SampleLiSurface as well: Le(off) divides by d2 (1 for
+// area and distant lights: an exact no-op), and a delta light has no BSDF MIS weight.
 struct AreaLightHit {
-    V3 p, pErr, n;
+    V3 p, pErr, n, wi;
     float pdf;  // shape pdf * light-choice pmf
     float scale;
     int spectrum;
+    float d2, rd2;
+    bool d2Ok, delta;
+    __device__ float Le(const DeviceScene &S, int off) const {
+        const float v = scale * DenseAt(S, spectrum, off);
+        return delta ? DivByRcp(v, d2, rd2, d2Ok) : v;
+    }
 };
 __device__ inline bool SampleAreaLightAt(const DeviceScene &S, V3 refP, V3 refN, V3 refNs, float uc, float u0, float u1,
                                          float lambda0, AreaLightHit *out) {
     int li;
     float lpmf;
-    if (!SampleLight(S, refP, refNs, uc, &li, &lpmf) || li >= S.nAreaLights) return false;
+    if (!SampleLight(S, refP, refNs, uc, &li, &lpmf)) return false;
+    if (li >= S.nAreaLights) {
+        LiSample ls;
+        if (!SampleLiSurface<false>(S, S.lights, li, refP, refN, refNs, u0, u1, &ls)) return false;
+        out->p = ls.lp;
+        out->pErr = ls.lpe;
+        out->n = ls.ln;
+        out->wi = ls.wi;
+        out->pdf = ls.pdf * lpmf;
+        out->scale = ls.scale;
+        out->spectrum = ls.spectrum;
+        out->d2 = ls.d2;
+        out->rd2 = 1 / ls.d2;
+        out->d2Ok = DivFastOk(ls.d2);
+        out->delta = true;
+        bool nz = false;
+        SpectralIter it(lambda0);
+#pragma unroll 1
+        for (int i = 0; i < kNS; ++i, it.Next()) nz |= out->Le(S, DenseOffset(it.lam)) != 0;
+        return nz;
+    }
     const DeviceAreaLight Ld = S.lights[li];
     const V3 q0(Ld.v0.x, Ld.v0.y, Ld.v0.z), q1(Ld.v1.x, Ld.v1.y, Ld.v1.z), q2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
     TriShading lsh;
@@ -1003,9 +1057,13 @@ __device__ inline bool SampleAreaLightAt(const DeviceScene &S, V3 refP, V3 refN,
     out->p = lp;
     out->pErr = lpe;
     out->n = ln;
+    out->wi = wi;
     out->pdf = lpdf * lpmf;
     out->scale = Ld.scale;
     out->spectrum = Ld.spectrum;
+    out->d2 = out->rd2 = 1;
+    out->d2Ok = true;
+    out->delta = false;
     return true;
 }
 
@@ -1077,6 +1135,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
             const float avg = ds / kNS;
             // (a light with Le = 0 at every wavelength adds exact zeros: no separate test)
             for (int k = 0; k < S.nInfinite; ++k) {
+                if (S.infDistant[k] >= 0) continue;  // a DistantLight is no Infinite-type light
                 const int spec = S.infSpectrum[k];
                 const float scale = S.infScale[k];
                 AddSpecToL(S, st, slot, lambda0,
@@ -1220,7 +1279,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
             else if (transmissive && reflective) cp = OffsetRayOrigin(si.p, si.pErr, si.n, -wo3);
             AreaLightHit ls;
             if (SampleAreaLightAt(S, cp, si.n, si.ns, rs.dUc, rs.dU0, rs.dU1, lambda0, &ls) && woL.z != 0) {
-                const V3 wi = Normalize(ls.p - cp);
+                const V3 wi = ls.wi;
                 const V3 wiL = frame.ToLocal(wi);
                 // BSDF::f / BSDF::PDF (bsdf.h:60-135)
                 float fd = 0, bsdfPDF = 0;
@@ -1237,6 +1296,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
                     bsdfPDF = ct.pdf;
                     fAny = ct.ok;
                 }
+                if (ls.delta) bsdfPDF = 0;  // IsDeltaLight
                 if (fAny) {
                     const float absdot = AbsDotN(si.ns, wi);
                     const float lightPDF = ls.pdf;
@@ -1254,7 +1314,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
                         float ld0 = 0;
 #pragma unroll 2
                         for (int i = 0; i < kNS; ++i, it.Next()) {
-                            const float Le = ls.scale * DenseAt(S, ls.spectrum, DenseOffset(it.lam));
+                            const float Le = ls.Le(S, DenseOffset(it.lam));
                             const float Ldv = betaIn(i) * fL[i * kBlock] * absdot * Le;
                             ld0 = i == 0 ? Ldv : ld0;
                             ldUni &= FloatToBits(Ldv) == FloatToBits(ld0);
@@ -1266,7 +1326,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
                         for (int i = 0; i < kNS; ++i, it.Next()) {
                             const float f = fAt(it.lam, fd, ct);
                             fnz |= f != 0;
-                            const float Le = ls.scale * DenseAt(S, ls.spectrum, DenseOffset(it.lam));
+                            const float Le = ls.Le(S, DenseOffset(it.lam));
                             const float Ldv = betaIn(i) * f * absdot * Le;
                             fL[i * kBlock] = Ldv;
                             ldUni &= FloatToBits(Ldv) == FloatToBits(fL[0]);
@@ -1527,7 +1587,7 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
             else if (refl && trans) cp = OffsetRayOrigin(si.p, si.pErr, si.n, -wo3);
             AreaLightHit ls;
             if (SampleAreaLightAt(S, cp, si.n, si.ns, rs.dUc, rs.dU0, rs.dU1, lambda0, &ls) && woL.z != 0) {
-                const V3 wi = Normalize(ls.p - cp);
+                const V3 wi = ls.wi;
                 const V3 wiL = frame.ToLocal(wi);
                 if (dt) D.f(woL, wiL, fo);
                 else L.f(woL, wiL, true, fo);
@@ -1535,7 +1595,7 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
 #pragma unroll 1
                 for (int i = 0; i < kNS; ++i) fnz |= fo[i] != 0;
                 if (fnz) {
-                    const float bsdfPDF = dt ? D.PDF(woL, wiL) : L.PDF(woL, wiL, true);
+                    const float bsdfPDF = ls.delta ? 0.f : dt ? D.PDF(woL, wiL) : L.PDF(woL, wiL, true);
                     const float absdot = AbsDotN(si.ns, wi);
                     const V3 so = OffsetRayOrigin(si.p, si.pErr, si.n, ls.p - si.p);
                     const V3 pt = OffsetRayOrigin(ls.p, ls.pErr, ls.n, so - ls.p);
@@ -1544,7 +1604,7 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
                     SpectralIter it(lambda0);
 #pragma unroll 1
                     for (int i = 0; i < kNS; ++i, it.Next()) {
-                        const float Le = ls.scale * DenseAt(S, ls.spectrum, DenseOffset(it.lam));
+                        const float Le = ls.Le(S, DenseOffset(it.lam));
                         fo[i] = betaIn(i) * fo[i] * absdot * Le;
                         ldUni &= FloatToBits(fo[i]) == FloatToBits(fo[0]);
                     }
@@ -1672,13 +1732,14 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vscatter(DeviceScene
             AreaLightSample ls;
             float Le[kNS];
             if (SampleAreaLight(S, pS, V3(0, 0, 0), V3(0, 0, 0), rs.dUc, rs.dU0, rs.dU1, wo, &ls, Le)) {
-                const V3 wi = Normalize(ls.p - pS);
+                const V3 wi = ls.wi;
                 const float ph = HenyeyGreenstein(Dot(wo3, wi), g);
+                const float phasePDF = ls.delta ? 0.f : ph;  // IsDeltaLight (media.cpp:292-293)
                 float Ld[kNS], sru[kNS], srl[kNS];
 #pragma unroll
                 for (int i = 0; i < kNS; ++i) {
                     Ld[i] = (beta[i] * ph) * Le[i];
-                    sru[i] = ru[i] * ph;
+                    sru[i] = ru[i] * phasePDF;
                     srl[i] = ru[i] * ls.pdf;
                 }
                 ShadowOut so;

@@ -134,11 +134,33 @@ def test_cornell_with_delta_lights_matches_oracle(pa, oracle, sampler):
     print(f"cornell + delta lights ({sampler or 'bvh'}): {frac*100:.2f}% within 1e-3, mean rel {mr:.2e}")
 
 
+DELTA3 = ('LightSource "point" "rgb I" [ 0.9 0.8 0.6 ] "float power" 40 "point3 from" [ 0.3 2.2 0.6 ]\n'
+          'LightSource "distant" "rgb L" [ 1 0.9 0.8 ] "float scale" 0.5 "point3 from" [ 1 3 -1 ] "point3 to" [ 0 0 0.5 ]\n'
+          'LightSource "spot" "rgb I" [ 0.5 0.7 1 ] "float power" 30 "point3 from" [ -0.8 2 0.2 ] '
+          '"point3 to" [ 0 0 0.5 ] "float coneangle" 40 "float conedeltaangle" 8\n')
+
+
 @pytest.mark.gpu
-def test_delta_lights_on_volumetric_path_refused(pa):
-    """Scenes that render through the volumetric kernels (here: a layered material) do not take
-    point, spot or distant lights yet: refused when the context is built, never approximated."""
-    text = plane_scene(POINT).replace('Material "diffuse"', 'Material "coateddiffuse"')
+@pytest.mark.parametrize("kind", ["homogeneous", "grid"])
+def test_media_with_delta_lights_matches_oracle(pa, oracle, kind):
+    """The volumetric kernels: medium scattering and surface vertices sample point, spot and
+    distant lights beside the area light (phase-function / BSDF MIS weight 0 for them)."""
+    from test_gpu_media import HOMOG, LIGHT, check, gpu_rgb, grid_medium, medium_scene, oracle_rgb
+    m = HOMOG if kind == "homogeneous" else grid_medium()
+    sc = pa.Scene.from_string(medium_scene(m, res=40, spp=16, maxdepth=6, sky="0.3 0.4 0.5", extra=LIGHT + DELTA3,
+                                           fov=35), SCENES)
+    assert sc.flat().n_delta_lights == 3
+    a, _ = gpu_rgb(pa, oracle, sc)
+    frac, mr = check(a, oracle_rgb(oracle, sc))
+    print(f"media {kind} + delta lights: {frac*100:.2f}% pixels within 1e-3, mean rel {mr:.2e}")
+
+
+@pytest.mark.gpu
+def test_layered_plane_under_point_light_matches_oracle(pa, oracle):
+    from test_gpu_media import check, gpu_rgb, oracle_rgb
+    text = plane_scene(POINT + "\n" + SPOT, fov=40, spp=16, maxdepth=3).replace(
+        'Material "diffuse" "rgb reflectance" [ 0.5 0.5 0.5 ]',
+        'Material "coateddiffuse" "rgb reflectance" [ 0.6 0.4 0.2 ] "float roughness" 0.2')
     sc = pa.Scene.from_string(text, SCENES)
-    with pytest.raises(pa.PbrtError, match="not supported"):
-        pa.WavefrontPathIntegrator(sc)
+    a, _ = gpu_rgb(pa, oracle, sc)
+    check(a, oracle_rgb(oracle, sc))

@@ -644,18 +644,6 @@ static void BuildDevice(pbrt_context *c) {
         L.denseInLds = s.denseSpectra.size() <= 4 ? 1 : 0;
         L.dense = off;
         if (L.denseInLds) off = align16(off + (int)s.denseSpectra.size() * kDenseN * 4);
-        int permEntries = 0;
-        for (int depth = 0; depth < s.maxDepth; ++depth) {
-            int n = 0;
-            for (int k = 0; k < 7; ++k) {
-                int d = 6 + 7 * depth + k;
-                if (d < (int)s.permBase.size()) n += (int)(s.permBase[d] * s.permNDigits[d]);
-            }
-            permEntries = std::max(permEntries, n);
-        }
-        L.permEntries = permEntries + 1;  // DMA copies whole 4-byte words
-        L.perm = off;
-        off = align16(off + (permEntries + 1) * 2);
         L.lightsInLds = (s.areaLights.size() <= 64 && s.lightNodes.size() <= 127) ? 1 : 0;
         L.lights = off;
         L.lightNodes = off;
@@ -672,6 +660,22 @@ static void BuildDevice(pbrt_context *c) {
             L.matConst = off;
             off = align16(off + (int)s.materials.size() * 4);
         }
+        // the Halton permutations of the launch's 7 dimensions come last, so a launch asks for
+        // the LDS its own depth's tables need (depth 0's prime bases are the smallest)
+        int permEntries = 0;
+        L.perm = off;
+        for (int depth = 0; depth < s.maxDepth; ++depth) {
+            int n = 0;
+            for (int k = 0; k < 7; ++k) {
+                int d = 6 + 7 * depth + k;
+                if (d < (int)s.permBase.size()) n += (int)(s.permBase[d] * s.permNDigits[d]);
+            }
+            permEntries = std::max(permEntries, n);
+            if (depth < kShadeLdsDepths) L.totalByDepth[depth] = align16(off + (n + 1) * 2);  // whole 4-byte words
+        }
+        L.permEntries = permEntries + 1;
+        off = align16(off + (permEntries + 1) * 2);
+        for (int depth = s.maxDepth; depth < kShadeLdsDepths; ++depth) L.totalByDepth[depth] = off;
         L.total = off;
         if (L.total > 64 * 1024 && !c->volumetric) throw Error("shade kernel LDS layout exceeds 64 KB");
     }

@@ -36,9 +36,11 @@ static_assert(sizeof(DeviceAreaLight) == 64, "DeviceAreaLight must be 64 bytes")
 // Dynamic-LDS layout of k_shade_diffuse (byte offsets; host-computed per scene).  The block
 // stages everything its lanes look up per wavelength or per sample: sensor tables, light
 // spectra, the Halton permutations of the launch's 7 dimensions, lights and materials.
+constexpr int kShadeLdsDepths = 16;
 struct ShadeLdsLayout {
     int sensor, dense, perm, lights, lightNodes, mats, matConst, total;
     int denseInLds, lightsInLds, matsInLds, permEntries;
+    int totalByDepth[kShadeLdsDepths];  // bytes a launch at that depth needs (perm tables last)
 };
 
 // Work queues are sharded: a producer block appends to shard (blockIdx.x % kShards), each

@@ -17,6 +17,10 @@
 
 namespace pbrt_amd {
 
+// The sensor's x/y/z-bar table as the shade kernels read it (staged in LDS; reading it through
+// the L1 instead, to fit four blocks per CU, measured 5 % slower: profiles/r02_shade_ablation.txt)
+typedef LdsF4 SensorF4;
+
 // ------------------------------------------------------------------ kernels
 __global__ void __launch_bounds__(kBlock) k_camera(DeviceScene S, PathState st, int nActive) {
     int slot = blockIdx.x * blockDim.x + threadIdx.x;
@@ -249,7 +253,7 @@ __global__ void __launch_bounds__(kBlock) k_emissive(DeviceScene S, PathState st
 // DivD2: the light's radiance is divided by d2 per wavelength (point and spot lights; d2 = 1,
 // an exact no-op, for the other lanes).
 template <bool DivD2, typename FD>
-__device__ inline void ShadeSpectralPass(int depth, const FD *dense, const LdsF4 *sensor4, float *bf, float4 mc,
+__device__ inline void ShadeSpectralPass(int depth, const FD *dense, const SensorF4 *sensor4, float *bf, float4 mc,
                                          bool constant, float lambda0, float scale, float d2, float rd2, bool d2Ok,
                                          float absdotL, float invDenom, float absdotB, float pdf, float rpdf,
                                          bool pdfOk, float etaScale, SensorAcc *acc, bool *neeNz, bool *betaNz,
@@ -289,7 +293,7 @@ struct ShadeTables {
     ShadeLdsLayout lay;
     float *bfLds;
     float *denseLds;
-    const LdsF4 *sensorL;
+    const SensorF4 *sensorL;
     const LdsU16 *permL;
     uint32_t permOff[7];
     DeviceScene SL;  // the light sampler reads its nodes from LDS
@@ -401,7 +405,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
     const ShadeLdsLayout &lay = T.lay;
     float *bfLds = T.bfLds;
     float *denseLds = T.denseLds;
-    const LdsF4 *sensorL = T.sensorL;
+    const SensorF4 *sensorL = T.sensorL;
     const DeviceScene &SL = T.SL;
     const DeviceAreaLight *lightsL = T.lightsL;
     const float4 *matsL = T.matsL;
@@ -1110,24 +1114,29 @@ hipError_t LaunchEmissive(const DeviceScene &S, const PathState &st, int depth, 
     hipLaunchKernelGGL(k_emissive, dim3(SmallGridFor(maxCount)), dim3(kBlock), 0, s, S, st, depth);
     return hipGetLastError();
 }
+// Dynamic LDS of a shade launch: the layout up to this depth's Halton permutation tables, which
+// come last and grow with the depth's prime bases (ShadeLdsLayout::totalByDepth)
+static size_t ShadeLdsBytes(const DeviceScene &S, int depth) {
+    return (size_t)(depth < kShadeLdsDepths ? S.shadeLds.totalByDepth[depth] : S.shadeLds.total);
+}
 hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int depth, int maxCount, bool lean,
                               hipStream_t s) {
     if (lean)
-        hipLaunchKernelGGL(k_shade_diffuse<true>, dim3(ShadeGridFor(maxCount)), dim3(kBlock), (size_t)S.shadeLds.total,
+        hipLaunchKernelGGL(k_shade_diffuse<true>, dim3(ShadeGridFor(maxCount)), dim3(kBlock), ShadeLdsBytes(S, depth),
                            s, S, st, depth);
     else
         hipLaunchKernelGGL(k_shade_diffuse<false>, dim3(ShadeGridFor(maxCount)), dim3(kBlock),
-                           (size_t)S.shadeLds.total, s, S, st, depth);
+                           ShadeLdsBytes(S, depth), s, S, st, depth);
     return hipGetLastError();
 }
 hipError_t LaunchShadeMicrofacet(const DeviceScene &S, const PathState &st, int depth, int type, int maxCount,
                                  hipStream_t s) {
     if (type == kMatDielectricT)
         hipLaunchKernelGGL(k_shade_microfacet<kMatDielectricT>, dim3(ShadeGridFor(maxCount)), dim3(kBlock),
-                           (size_t)S.shadeLds.total, s, S, st, depth);
+                           ShadeLdsBytes(S, depth), s, S, st, depth);
     else
         hipLaunchKernelGGL(k_shade_microfacet<kMatConductorT>, dim3(ShadeGridFor(maxCount)), dim3(kBlock),
-                           (size_t)S.shadeLds.total, s, S, st, depth);
+                           ShadeLdsBytes(S, depth), s, S, st, depth);
     return hipGetLastError();
 }
 hipError_t LaunchShadow(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s) {

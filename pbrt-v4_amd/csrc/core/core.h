@@ -16,15 +16,11 @@
 // outgrew the instruction cache, and a call is cheaper than streaming instructions from L2.
 #define PHD_NOINLINE __host__ __device__ inline __attribute__((noinline))
 #define PHD_UNROLL _Pragma("unroll")
-// LightImportance and SampleSphericalTriangleN are inlined (C2 +2 % over out-of-line calls,
-// whose ABI saves registers around every call); -DPBRT_NOINLINE_LIGHT restores the calls.
-#ifdef PBRT_NOINLINE_LIGHT
-#define PHD_LI PHD_NOINLINE
-#define PHD_SPH PHD_NOINLINE
-#else
+// LightImportance and SampleSphericalTriangleN have an inline body (*Inl, taken by the lean
+// diffuse kernel: C2 +2 % over out-of-line calls) and an out-of-line wrapper (every other
+// kernel, where inlining them spilled hundreds of VGPRs: the conductor kernel ran 48 % slower).
 #define PHD_LI PHD
 #define PHD_SPH PHD
-#endif
 #else
 #define PHD inline
 #define PHD_NOINLINE inline
@@ -289,7 +285,7 @@ struct SphTriSample {
 // a, bb, c: Normalize(v0 - p), Normalize(v1 - p), Normalize(v2 - p) -- the callers have them
 // already (Triangle::Sample's solid angle and bilinear weights use the same three vectors), so
 // they are passed in rather than normalised a second time (same values, same bits).
-PHD_SPH SphTriSample SampleSphericalTriangleN(V3 v0, V3 v1, V3 v2, V3 p, V3 a, V3 bb, V3 c, float u0, float u1) {
+PHD_SPH SphTriSample SampleSphericalTriangleNInl(V3 v0, V3 v1, V3 v2, V3 p, V3 a, V3 bb, V3 c, float u0, float u1) {
     SphTriSample r{0, 0, 0, 0, false};
     float b[3];
     float *pdf = &r.pdf;
@@ -350,6 +346,9 @@ PHD_SPH SphTriSample SampleSphericalTriangleN(V3 v0, V3 v1, V3 v2, V3 p, V3 a, V
     return r;
 }
 
+PHD_NOINLINE SphTriSample SampleSphericalTriangleN(V3 v0, V3 v1, V3 v2, V3 p, V3 a, V3 bb, V3 c, float u0, float u1) {
+    return SampleSphericalTriangleNInl(v0, v1, v2, p, a, bb, c, u0, u1);
+}
 PHD SphTriSample SampleSphericalTriangle(V3 v0, V3 v1, V3 v2, V3 p, float u0, float u1) {
     return SampleSphericalTriangleN(v0, v1, v2, p, Normalize(v0 - p), Normalize(v1 - p), Normalize(v2 - p), u0, u1);
 }
@@ -1346,7 +1345,7 @@ PHD float SinSubClamped(float sinA, float cosA, float sinB, float cosB) {
     if (cosA > cosB) return 0;
     return sinA * cosB - cosA * sinB;
 }
-PHD_LI float LightImportance(LightNodeBounds lb, V3 p, V3 n) {
+PHD_LI float LightImportanceInl(LightNodeBounds lb, V3 p, V3 n) {
     V3 pc = (lb.pMin + lb.pMax) / 2;
     float d2 = DistanceSquared(p, pc);
     d2 = std::fmax(d2, Length(lb.pMax - lb.pMin) / 2);
@@ -1371,6 +1370,7 @@ PHD_LI float LightImportance(LightNodeBounds lb, V3 p, V3 n) {
     importance = std::fmax(importance, 0.f);
     return importance;
 }
+PHD_NOINLINE float LightImportance(LightNodeBounds lb, V3 p, V3 n) { return LightImportanceInl(lb, p, n); }
 
 // ---------------------------------------------------------------- participating media
 // pbrt's Hash(args...) over whole 4-byte words (util/hash.h:91-106): MurmurHash64A (seed 0) of

@@ -420,6 +420,7 @@ __device__ inline bool IntersectTriangleRot(const TriRayR &r, float tMax, V3 p0t
         const EdgeFns e = EdgeFunctionsFP64(p0t, p1t, p2t);
         e0 = e.e0, e1 = e.e1, e2 = e.e2;
     }
+#ifndef PBRT_TRI_BRANCHFREE
     if ((e0 < 0 || e1 < 0 || e2 < 0) && (e0 > 0 || e1 > 0 || e2 > 0)) return false;
     const float det = e0 + e1 + e2;
     if (det == 0) return false;
@@ -429,6 +430,18 @@ __device__ inline bool IntersectTriangleRot(const TriRayR &r, float tMax, V3 p0t
     const float tScaled = e0 * p0t.z + e1 * p1t.z + e2 * p2t.z;
     if (det < 0 && (tScaled >= 0 || tScaled < tMax * det)) return false;
     if (det > 0 && (tScaled <= 0 || tScaled > tMax * det)) return false;
+#else
+    // the same four rejections folded into one predicate (one branch for the wave)
+    const float det = e0 + e1 + e2;
+    p0t.z *= Sz;
+    p1t.z *= Sz;
+    p2t.z *= Sz;
+    const float tScaled = e0 * p0t.z + e1 * p1t.z + e2 * p2t.z;
+    const bool reject = ((e0 < 0 || e1 < 0 || e2 < 0) && (e0 > 0 || e1 > 0 || e2 > 0)) || det == 0 ||
+                        (det < 0 && (tScaled >= 0 || tScaled < tMax * det)) ||
+                        (det > 0 && (tScaled <= 0 || tScaled > tMax * det));
+    if (reject) return false;
+#endif
     const float invDet = 1 / det;
     const float b0 = e0 * invDet, b1 = e1 * invDet, b2 = e2 * invDet;
     const float t = tScaled * invDet;
@@ -625,7 +638,14 @@ __device__ inline int TraverseCW(const DeviceScene &S, const SceneLds &L, V3 o, 
             if (NodesInLds || node < S.ldsNodes) nh = VisitQuant(L.nodes + node * kLdsQNodeStride, r, tMax);
             else nh = VisitQuant(reinterpret_cast<const float4 *>(S.qnodes + node), r, tMax);
         } else {
+#ifdef PBRT_NODE_MUL24
+            if (NodesInLds || node < S.ldsNodes)
+                nh = VisitWide((const LdsF4 *)((__attribute__((address_space(3))) const char *)L.nodes +
+                                               MulU24((uint32_t)node, kLdsNodeStride * 16)),
+                               r, tMax);
+#else
             if (NodesInLds || node < S.ldsNodes) nh = VisitWide(L.nodes + node * kLdsNodeStride, r, tMax);
+#endif
             else nh = VisitWide(reinterpret_cast<const float4 *>(S.nodes + node), r, tMax);
         }
         // the node's hit leaf triangles, in leaf order
@@ -773,6 +793,7 @@ __device__ inline float SolidAngleOf(V3 p0, V3 p1, V3 p2, V3 p) {
 // Triangle::Sample(ctx, u) (shapes.h:1053-1130); returns false for {}.  The three directions
 // Normalize(p_i - refP) enter the solid angle, the bilinear warp weights and the spherical
 // sample; pbrt normalises them anew in each (same operations, same values), here once.
+template <bool Inl = false>
 __device__ inline bool SampleTriangle(V3 p0, V3 p1, V3 p2, bool flip, const TriShading *sh, V3 refP, V3 refN,
                                       V3 refNs, float u0, float u1, V3 *ps, V3 *pErr, V3 *ns, float *pdfOut) {
     (void)refN;
@@ -809,7 +830,8 @@ __device__ inline bool SampleTriangle(V3 p0, V3 p1, V3 p2, bool flip, const TriS
     float triPDF;
     float b[3];
     {
-        const SphTriSample r = SampleSphericalTriangleN(p0, p1, p2, refP, wi0, wi1, wi2, u0, u1);
+        const SphTriSample r = Inl ? SampleSphericalTriangleNInl(p0, p1, p2, refP, wi0, wi1, wi2, u0, u1)
+                                   : SampleSphericalTriangleN(p0, p1, p2, refP, wi0, wi1, wi2, u0, u1);
         b[0] = r.b0;
         b[1] = r.b1;
         b[2] = r.b2;
@@ -856,9 +878,12 @@ __device__ inline float TrianglePDF(V3 p0, V3 p1, V3 p2, bool flip, const TriSha
 
 // BVHLightSampler::Sample / PMF (lightsamplers.h:266-403) and UniformLightSampler
 // light index convention: [0, nAreaLights) area lights, then infinite lights.
-template <typename NodeT>
+template <typename NodeT, bool Inl = false>
 __device__ inline bool SampleLightT(const DeviceScene &S, const NodeT *lightNodes, V3 p, V3 ns, float u, int *light,
                                     float *pmfOut) {
+    auto importance = [](const LightNodeBounds &b, V3 q, V3 n) {
+        return Inl ? LightImportanceInl(b, q, n) : LightImportance(b, q, n);
+    };
     int nAll = S.nAreaLights + S.nPointSpot + S.nInfinite;
     if (S.uniformLightSampler) {
         if (nAll == 0) return false;
@@ -882,15 +907,15 @@ __device__ inline bool SampleLightT(const DeviceScene &S, const NodeT *lightNode
     for (int iter = 0; iter < 4 * kMaxLightBVHDepth; ++iter) {
         DeviceLightNode node = lightNodes[nodeIndex];
         if (!node.isLeaf) {
-            float c0 = LightImportance(lightNodes[nodeIndex + 1].b, p, ns);
-            float c1 = LightImportance(lightNodes[node.childOrLight].b, p, ns);
+            float c0 = importance(lightNodes[nodeIndex + 1].b, p, ns);
+            float c1 = importance(lightNodes[node.childOrLight].b, p, ns);
             if (c0 == 0 && c1 == 0) return false;
             float nodePMF;
             int child = SampleDiscrete2(c0, c1, u, &nodePMF, &u);
             pmf *= nodePMF;
             nodeIndex = (child == 0) ? (nodeIndex + 1) : node.childOrLight;
         } else {
-            if (nodeIndex > 0 || LightImportance(node.b, p, ns) > 0) {
+            if (nodeIndex > 0 || importance(node.b, p, ns) > 0) {
                 *light = node.childOrLight;
                 *pmfOut = pmf;
                 return true;
@@ -942,7 +967,8 @@ __device__ inline float SmoothStepf(float x, float a, float b) {
     const float t = Clampf((x - a) / (b - a), 0, 1);
     return t * t * (3 - 2 * t);
 }
-template <bool Lean>
+// Inl: the spherical-triangle sampling inlined (the diffuse kernels) or called out of line
+template <bool Lean, bool Inl = Lean>
 __device__ inline bool SampleLiSurface(const DeviceScene &S, const DeviceAreaLight *lightsL, int li, V3 cp, V3 n,
                                        V3 ns, float u0, float u1, LiSample *ls) {
     if (li < S.nAreaLights) {
@@ -951,7 +977,7 @@ __device__ inline bool SampleLiSurface(const DeviceScene &S, const DeviceAreaLig
         TriShading lsh;
         const bool lhas = !Lean && LoadTriShading(S, __float_as_int(Ld.v0.w), &lsh);
         float lpdf;
-        if (!SampleTriangle(q0, q1, q2, Ld.flip, lhas ? &lsh : nullptr, cp, n, ns, u0, u1, &ls->lp, &ls->lpe, &ls->ln,
+        if (!SampleTriangle<Inl>(q0, q1, q2, Ld.flip, lhas ? &lsh : nullptr, cp, n, ns, u0, u1, &ls->lp, &ls->lpe, &ls->ln,
                             &lpdf) ||
             lpdf == 0 || LengthSquared(ls->lp - cp) == 0)
             return false;
@@ -964,9 +990,15 @@ __device__ inline bool SampleLiSurface(const DeviceScene &S, const DeviceAreaLig
         ls->delta = false;
         return true;
     }
+#ifdef PBRT_EXP_NODELTA
+    if constexpr (true) {
+        return false;
+    } else {
+#else
     if constexpr (Lean) {
         return false;  // lean launches have no point, spot or distant lights
     } else {
+#endif
         const int k = li - S.nAreaLights;
         int di = k;
         if (k >= S.nPointSpot) {

@@ -497,10 +497,11 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                     float lpmf;
                     const bool sampled =
                         (Lean || lay.lightsInLds)
-                            ? SampleLightT(SL, (const LdsLightNode *)SL.lightNodes, cp, ns, dUc, &li, &lpmf)
-                            : SampleLightT(SL, S.lightNodes, cp, ns, dUc, &li, &lpmf);
+                            ? SampleLightT<LdsLightNode, true>(SL, (const LdsLightNode *)SL.lightNodes, cp, ns, dUc,
+                                                               &li, &lpmf)
+                            : SampleLightT<DeviceLightNode, true>(SL, S.lightNodes, cp, ns, dUc, &li, &lpmf);
                     LiSample ls;
-                    if (sampled && SampleLiSurface<Lean>(S, lightsL, li, cp, n, ns, dU0, dU1, &ls)) {
+                    if (sampled && SampleLiSurface<Lean, true>(S, lightsL, li, cp, n, ns, dU0, dU1, &ls)) {
                         const V3 wi = ls.wi;
                         const V3 wiL = frame.ToLocal(wi);
                         if (woL.z != 0 && woL.z * wiL.z > 0) {  // DiffuseBxDF::f != 0
@@ -554,7 +555,11 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                     float *bf = bfLds + threadIdx.x;
                     const float rd2 = 1 / d2;
                     const bool d2Ok = DivFastOk(d2);
+#ifdef PBRT_EXP_NODIV
+                    if (true)
+#else
                     if (Lean || (lay.denseInLds && S.nPointSpot == 0))
+#endif
                         ShadeSpectralPass<false>(depth, (const LdsF *)denseLds + spec * kDenseN, sensorL, bf, mc,
                                                  constant, lambda0, scale, d2, rd2, d2Ok, absdotL, invDenom, absdotB, pdf,
                                                  rpdf, pdfOk, etaScale, &acc, &neeNz, &betaNz, &mx);
@@ -738,8 +743,8 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
                 int li;
                 float lpmf;
                 LiSample ls;
-                if (SampleLight(T.SL, cp, ns, rs.dUc, &li, &lpmf) &&
-                    SampleLiSurface<false>(S, T.lightsL, li, cp, n, ns, rs.dU0, rs.dU1, &ls)) {
+                if (SampleLightT<DeviceLightNode, true>(T.SL, T.SL.lightNodes, cp, ns, rs.dUc, &li, &lpmf) &&
+                    SampleLiSurface<false, true>(S, T.lightsL, li, cp, n, ns, rs.dU0, rs.dU1, &ls)) {
                     const V3 lp = ls.lp, lpe = ls.lpe, ln = ls.ln;
                     {
                         const V3 wi = ls.wi;
@@ -764,8 +769,6 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
                                 const float invDenom = 1 / Avg31(bsdfPDF + lightPDF);
                                 const float *dense = lay.denseInLds ? nullptr : S.dense + ls.spectrum * kDenseN;
                                 const LdsF *denseL = (const LdsF *)T.denseLds + ls.spectrum * kDenseN;
-                                const float rd2 = 1 / ls.d2;
-                                const bool d2Ok = DivFastOk(ls.d2);
                                 SensorAcc acc;
                                 bool nz = false;
 #pragma unroll 2
@@ -773,7 +776,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
                                     const int off = DenseOffset(it.lam);
                                     float Le =
                                         ls.scale * (off < 0 ? 0.f : (lay.denseInLds ? float(denseL[off]) : dense[off]));
-                                    if (S.nPointSpot > 0) Le = DivByRcp(Le, ls.d2, rd2, d2Ok);
+                                    if (S.nPointSpot > 0) Le = Le / ls.d2;  // pbrt: SampledSpectrum / DistanceSquared
                                     nz |= Le != 0;
                                     float f = fd;
                                     if constexpr (MT == kMatConductorT) {

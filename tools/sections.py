@@ -13,7 +13,12 @@ import pbrt_amd as pa
 
 NAMES = ["loads+surface", "halton", "R != 0 + frame", "light sample geometry", "BSDF sample geometry",
          "wavelength pass", "RR + decisions", "queue push + writes"]
-sc = pa.load_scene(ROOT / "scenes" / "cornell-box.pbrt", xresolution=1280, yresolution=720, spp=64)
+if len(sys.argv) > 1 and sys.argv[1] == "c3":  # C3 at reduced size (ZSobol: the full kernel)
+    sys.path.insert(0, str(ROOT / "scenes"))
+    import gen_c3
+    sc = pa.Scene.from_string(gen_c3.scene_text(960, 540, 16), ROOT / "scenes")
+else:
+    sc = pa.load_scene(ROOT / "scenes" / "cornell-box.pbrt", xresolution=1280, yresolution=720, spp=64)
 integ = pa.WavefrontPathIntegrator(sc, device=0)
 integ.render(n_samples=4)
 integ.synchronize()

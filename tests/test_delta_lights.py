@@ -164,3 +164,25 @@ def test_layered_plane_under_point_light_matches_oracle(pa, oracle):
     sc = pa.Scene.from_string(text, SCENES)
     a, _ = gpu_rgb(pa, oracle, sc)
     check(a, oracle_rgb(oracle, sc))
+
+
+@pytest.mark.gpu
+def test_c3_with_delta_lights_matches_oracle(pa, oracle):
+    """Rough conductor and dielectric shading (k_shade_microfacet) under a point, a spot and a
+    distant light beside C3's area and infinite lights."""
+    import sys
+    sys.path.insert(0, str(SCENES))
+    import gen_c3
+    from test_gpu_media import check, gpu_rgb
+    lights = ('LightSource "point" "rgb I" [ 1 0.9 0.8 ] "float power" 2000 "point3 from" [ 3 6 -4 ]\n'
+              'LightSource "spot" "rgb I" [ 0.6 0.8 1 ] "float power" 3000 "point3 from" [ -4 5 -3 ] '
+              '"point3 to" [ 0 0 0 ] "float coneangle" 25\n'
+              'LightSource "distant" "rgb L" [ 1 1 1 ] "float scale" 0.8 "point3 from" [ 1 2 -1 ] "point3 to" [ 0 0 0 ]\n')
+    text = gen_c3.scene_text(96, 54, 8).replace("WorldBegin", "WorldBegin\n" + lights, 1)
+    sc = pa.Scene.from_string(text, SCENES)
+    assert sc.flat().n_delta_lights == 3
+    a, _ = gpu_rgb(pa, oracle, sc)
+    f = sc.flat()
+    b = oracle.film_to_rgb(oracle.render(sc, threads=16), [f.output_rgb_from_sensor_rgb[i] for i in range(9)])
+    frac, mr = check(a, b)
+    print(f"C3 + delta lights: {frac*100:.2f}% within 1e-3, mean rel {mr:.2e}")

@@ -420,7 +420,6 @@ __device__ inline bool IntersectTriangleRot(const TriRayR &r, float tMax, V3 p0t
         const EdgeFns e = EdgeFunctionsFP64(p0t, p1t, p2t);
         e0 = e.e0, e1 = e.e1, e2 = e.e2;
     }
-#ifndef PBRT_TRI_BRANCHFREE
     if ((e0 < 0 || e1 < 0 || e2 < 0) && (e0 > 0 || e1 > 0 || e2 > 0)) return false;
     const float det = e0 + e1 + e2;
     if (det == 0) return false;
@@ -430,18 +429,6 @@ __device__ inline bool IntersectTriangleRot(const TriRayR &r, float tMax, V3 p0t
     const float tScaled = e0 * p0t.z + e1 * p1t.z + e2 * p2t.z;
     if (det < 0 && (tScaled >= 0 || tScaled < tMax * det)) return false;
     if (det > 0 && (tScaled <= 0 || tScaled > tMax * det)) return false;
-#else
-    // the same four rejections folded into one predicate (one branch for the wave)
-    const float det = e0 + e1 + e2;
-    p0t.z *= Sz;
-    p1t.z *= Sz;
-    p2t.z *= Sz;
-    const float tScaled = e0 * p0t.z + e1 * p1t.z + e2 * p2t.z;
-    const bool reject = ((e0 < 0 || e1 < 0 || e2 < 0) && (e0 > 0 || e1 > 0 || e2 > 0)) || det == 0 ||
-                        (det < 0 && (tScaled >= 0 || tScaled < tMax * det)) ||
-                        (det > 0 && (tScaled <= 0 || tScaled > tMax * det));
-    if (reject) return false;
-#endif
     const float invDet = 1 / det;
     const float b0 = e0 * invDet, b1 = e1 * invDet, b2 = e2 * invDet;
     const float t = tScaled * invDet;
@@ -638,14 +625,7 @@ __device__ inline int TraverseCW(const DeviceScene &S, const SceneLds &L, V3 o, 
             if (NodesInLds || node < S.ldsNodes) nh = VisitQuant(L.nodes + node * kLdsQNodeStride, r, tMax);
             else nh = VisitQuant(reinterpret_cast<const float4 *>(S.qnodes + node), r, tMax);
         } else {
-#ifdef PBRT_NODE_MUL24
-            if (NodesInLds || node < S.ldsNodes)
-                nh = VisitWide((const LdsF4 *)((__attribute__((address_space(3))) const char *)L.nodes +
-                                               MulU24((uint32_t)node, kLdsNodeStride * 16)),
-                               r, tMax);
-#else
             if (NodesInLds || node < S.ldsNodes) nh = VisitWide(L.nodes + node * kLdsNodeStride, r, tMax);
-#endif
             else nh = VisitWide(reinterpret_cast<const float4 *>(S.nodes + node), r, tMax);
         }
         // the node's hit leaf triangles, in leaf order
@@ -990,15 +970,9 @@ __device__ inline bool SampleLiSurface(const DeviceScene &S, const DeviceAreaLig
         ls->delta = false;
         return true;
     }
-#ifdef PBRT_EXP_NODELTA
-    if constexpr (true) {
-        return false;
-    } else {
-#else
     if constexpr (Lean) {
         return false;  // lean launches have no point, spot or distant lights
     } else {
-#endif
         const int k = li - S.nAreaLights;
         int di = k;
         if (k >= S.nPointSpot) {

@@ -555,11 +555,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                     float *bf = bfLds + threadIdx.x;
                     const float rd2 = 1 / d2;
                     const bool d2Ok = DivFastOk(d2);
-#ifdef PBRT_EXP_NODIV
-                    if (true)
-#else
                     if (Lean || (lay.denseInLds && S.nPointSpot == 0))
-#endif
                         ShadeSpectralPass<false>(depth, (const LdsF *)denseLds + spec * kDenseN, sensorL, bf, mc,
                                                  constant, lambda0, scale, d2, rd2, d2Ok, absdotL, invDenom, absdotB, pdf,
                                                  rpdf, pdfOk, etaScale, &acc, &neeNz, &betaNz, &mx);

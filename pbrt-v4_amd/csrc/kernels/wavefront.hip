@@ -758,12 +758,18 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
             const int etaSpec = MT == kMatConductorT ? S.matSpectra[2 * mat] : -1;
             const int kSpec = MT == kMatConductorT ? S.matSpectra[2 * mat + 1] : -1;
             const float4 mc = T.matsL[mat];
-            auto etaK = [&](float lam, float *e, float *k) {
+            PiecewiseLinearWalk etaW{}, kW{};
+            if (etaSpec >= 0) {
+                const int a = S.plOffsets[etaSpec], na = S.plOffsets[etaSpec + 1] - a;
+                const int b = S.plOffsets[kSpec], nb = S.plOffsets[kSpec + 1] - b;
+                etaW = PiecewiseLinearWalk::Make(S.plLambda + a, S.plValue + a, na);
+                kW = PiecewiseLinearWalk::Make(S.plLambda + b, S.plValue + b, nb);
+            }
+            // e_i, k_i for the loop's i-th wavelength; ew / kw walk the knots (one pair per loop)
+            auto etaK = [&](float lam, float *e, float *k, PiecewiseLinearWalk &ew, PiecewiseLinearWalk &kw) {
                 if (etaSpec >= 0) {
-                    const int a = S.plOffsets[etaSpec], na = S.plOffsets[etaSpec + 1] - a;
-                    const int b = S.plOffsets[kSpec], nb = S.plOffsets[kSpec + 1] - b;
-                    *e = PiecewiseLinearEval(S.plLambda + a, S.plValue + a, na, lam);
-                    *k = PiecewiseLinearEval(S.plLambda + b, S.plValue + b, nb, lam);
+                    *e = ew(lam);
+                    *k = kw(lam);
                 } else {
                     float r = Clampf(SigmoidPolynomial(mc.x, mc.y, mc.z, lam), 0, .9999f);
                     *e = 1.f;
@@ -812,6 +818,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
                                 const LdsF *denseL = (const LdsF *)T.denseLds + ls.spectrum * kDenseN;
                                 SensorAcc acc;
                                 bool nz = false;
+                                PiecewiseLinearWalk ew = etaW, kw = kW;
 #pragma unroll 2
                                 for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next()) {
                                     const int off = DenseOffset(it.lam);
@@ -822,7 +829,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
                                     float f = fd;
                                     if constexpr (MT == kMatConductorT) {
                                         float e, k;
-                                        etaK(it.lam, &e, &k);
+                                        etaK(it.lam, &e, &k, ew, kw);
                                         f = ConductorF(ct, e, k);
                                     }
                                     acc.Add(T.sensorL, off, bf[it.i * kBlock] * f * absdot * Le * invDenom, it.i == 0);
@@ -873,12 +880,13 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
                     const float avgRu = Avg31(1.f);
                     float mx = -kInfinity;
                     bool fAny = MT == kMatDielectricT;
+                    PiecewiseLinearWalk ew = etaW, kw = kW;
 #pragma unroll 2
                     for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next()) {
                         float f = fd;
                         if constexpr (MT == kMatConductorT) {
                             float e, k;
-                            etaK(it.lam, &e, &k);
+                            etaK(it.lam, &e, &k, ew, kw);
                             f = ConductorF(ct, e, k);
                             fAny |= f != 0;
                         }

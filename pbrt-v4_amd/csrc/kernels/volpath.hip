@@ -1095,7 +1095,10 @@ size_t VolTablesLdsBytes(const DeviceScene &S) {
 // The surface side of an iteration: escaped rays, interfaces, emission, materials.  Spectral
 // quantities stream from the wavelength-major records in rolled loops; the one 31-wide
 // intermediate (f, then beta') lives in LDS ([31][kBlock], conflict-free).  Queue appends happen
-// where a lane decides to push (WavePush serves the lanes that reach it).
+// where a lane decides to push (WavePush serves the lanes that reach it).  DiffuseOnly: the
+// scene's surface materials are diffuse, interface or layered (k_vlayered) only, so the
+// dielectric / conductor code is compiled out (C5: fewer registers, no spills).
+template <bool DiffuseOnly>
 __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(DeviceScene S0, PathState st, VolState v,
                                                                        int wf) {
     const QueueView surf = LoadQueue(st, wf, kVSurf);
@@ -1151,8 +1154,8 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
         int mIn, mOut;
         MediaOf(S, prim, medium, &mIn, &mOut);
         const int mat = S.primMaterial[prim];
-        const int mtype = S.matType[mat];
-        if (mtype == 3) {
+        const int mtypeHit = S.matType[mat];
+        if (mtypeHit == 3) {
             // Material "interface": SpawnRay(ray.d) at the same path depth (media.cpp:193-203)
             if (last) continue;
             const int jn = shardBase + WavePush(nextCnt, true);
@@ -1209,8 +1212,9 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
             }
         }
         if (last) continue;
-        if (mtype == kMatCoatedDiffuseT || mtype == kMatCoatedConductorT || mtype == kMatDiffuseTransmissionT)
+        if (mtypeHit == kMatCoatedDiffuseT || mtypeHit == kMatCoatedConductorT || mtypeHit == kMatDiffuseTransmissionT)
             continue;  // k_vlayered
+        const int mtype = DiffuseOnly ? 0 : mtypeHit;
         // ---- EvaluateMaterialAndBSDF (surfscatter.cpp:57-328) for this material type
         const VRaySamples rs = RaySamplesAt(S, st, slot, depth, mtype == 1 || mtype == kMatThinDielectricT);
         const float4 mp4 = S.matParams[mat];
@@ -2029,7 +2033,11 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
     const dim3 gT(VolGrid(maxCount, PBRT_GRID_CAP)), gW(VolGrid(maxCount, PBRT_SHADE_GRID_CAP));
     if (S.media.allGrey) hipLaunchKernelGGL(k_vmedium_grey, gW, block, 0, s, S, st, v, wf);
     else hipLaunchKernelGGL(k_vmedium, gW, block, 0, s, S, st, v, wf);
-    hipLaunchKernelGGL(k_vsurface, gW, block, VolTablesLdsBytes(S) + kNS * kBlock * sizeof(float), s, S, st, v, wf);
+    const int other = ~((1 << kMatDiffuseT) | (1 << 3) | (1 << kMatCoatedDiffuseT) | (1 << kMatCoatedConductorT) |
+                        (1 << kMatDiffuseTransmissionT));
+    const size_t surfLds = VolTablesLdsBytes(S) + kNS * kBlock * sizeof(float);
+    if (S.matTypeMask & other) hipLaunchKernelGGL(k_vsurface<false>, gW, block, surfLds, s, S, st, v, wf);
+    else hipLaunchKernelGGL(k_vsurface<true>, gW, block, surfLds, s, S, st, v, wf);
     if (wf == S.maxDepth) return hipGetLastError();
     if (S.matTypeMask & ((1 << kMatCoatedDiffuseT) | (1 << kMatCoatedConductorT) | (1 << kMatDiffuseTransmissionT)))
         hipLaunchKernelGGL(k_vlayered, gW, block, 0, s, S, st, v, wf);

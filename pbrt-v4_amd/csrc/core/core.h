@@ -996,25 +996,6 @@ PHD float PiecewiseLinearEval(const float *lam, const float *val, int n, float l
     float t = (l - lam[lo]) / (lam[lo + 1] - lam[lo]);
     return Lerpf(t, val[lo], val[lo + 1]);
 }
-// PiecewiseLinearEval over a path's wavelengths in order: they rise by a fixed step and wrap
-// once, so the knot interval only moves forward (reset at the wrap).  Each lookup walks one or
-// two knots instead of a binary search, and lands on the same interval (the largest
-// o <= n-2 with lambda[o] <= l), so the value is the same.
-struct PiecewiseLinearWalk {
-    const float *lam, *val;
-    int n, o;
-    float first, last;
-    PHD static PiecewiseLinearWalk Make(const float *lam, const float *val, int n) {
-        return {lam, val, n, 0, n > 0 ? lam[0] : 0.f, n > 0 ? lam[n - 1] : 0.f};
-    }
-    PHD float operator()(float l) {
-        if (n == 0 || l < first || l > last) return 0;
-        if (l < lam[o]) o = 0;
-        while (o < n - 2 && lam[o + 1] <= l) ++o;
-        float t = (l - lam[o]) / (lam[o + 1] - lam[o]);
-        return Lerpf(t, val[o], val[o + 1]);
-    }
-};
 // RoughnessToAlpha (util/scattering.h:192)
 PHD float RoughnessToAlpha(float roughness) { return std::sqrt(roughness); }
 

@@ -758,18 +758,12 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
             const int etaSpec = MT == kMatConductorT ? S.matSpectra[2 * mat] : -1;
             const int kSpec = MT == kMatConductorT ? S.matSpectra[2 * mat + 1] : -1;
             const float4 mc = T.matsL[mat];
-            PiecewiseLinearWalk etaW{}, kW{};
-            if (etaSpec >= 0) {
-                const int a = S.plOffsets[etaSpec], na = S.plOffsets[etaSpec + 1] - a;
-                const int b = S.plOffsets[kSpec], nb = S.plOffsets[kSpec + 1] - b;
-                etaW = PiecewiseLinearWalk::Make(S.plLambda + a, S.plValue + a, na);
-                kW = PiecewiseLinearWalk::Make(S.plLambda + b, S.plValue + b, nb);
-            }
-            // e_i, k_i for the loop's i-th wavelength; ew / kw walk the knots (one pair per loop)
-            auto etaK = [&](float lam, float *e, float *k, PiecewiseLinearWalk &ew, PiecewiseLinearWalk &kw) {
+            auto etaK = [&](float lam, float *e, float *k) {
                 if (etaSpec >= 0) {
-                    *e = ew(lam);
-                    *k = kw(lam);
+                    const int a = S.plOffsets[etaSpec], na = S.plOffsets[etaSpec + 1] - a;
+                    const int b = S.plOffsets[kSpec], nb = S.plOffsets[kSpec + 1] - b;
+                    *e = PiecewiseLinearEval(S.plLambda + a, S.plValue + a, na, lam);
+                    *k = PiecewiseLinearEval(S.plLambda + b, S.plValue + b, nb, lam);
                 } else {
                     float r = Clampf(SigmoidPolynomial(mc.x, mc.y, mc.z, lam), 0, .9999f);
                     *e = 1.f;
@@ -818,7 +812,6 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
                                 const LdsF *denseL = (const LdsF *)T.denseLds + ls.spectrum * kDenseN;
                                 SensorAcc acc;
                                 bool nz = false;
-                                PiecewiseLinearWalk ew = etaW, kw = kW;
 #pragma unroll 2
                                 for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next()) {
                                     const int off = DenseOffset(it.lam);
@@ -829,7 +822,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
                                     float f = fd;
                                     if constexpr (MT == kMatConductorT) {
                                         float e, k;
-                                        etaK(it.lam, &e, &k, ew, kw);
+                                        etaK(it.lam, &e, &k);
                                         f = ConductorF(ct, e, k);
                                     }
                                     acc.Add(T.sensorL, off, bf[it.i * kBlock] * f * absdot * Le * invDenom, it.i == 0);
@@ -880,13 +873,12 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
                     const float avgRu = Avg31(1.f);
                     float mx = -kInfinity;
                     bool fAny = MT == kMatDielectricT;
-                    PiecewiseLinearWalk ew = etaW, kw = kW;
 #pragma unroll 2
                     for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next()) {
                         float f = fd;
                         if constexpr (MT == kMatConductorT) {
                             float e, k;
-                            etaK(it.lam, &e, &k, ew, kw);
+                            etaK(it.lam, &e, &k);
                             f = ConductorF(ct, e, k);
                             fAny |= f != 0;
                         }

@@ -104,6 +104,45 @@ def test_c3_regularize_matches_oracle(pa, oracle):
     check_parity(to_rgb(oracle, sc, film), to_rgb(oracle, sc, oracle.render(sc, threads=16)))
 
 
+@pytest.mark.parametrize("skies", [1, 2, 0], ids=["one-sky", "two-skies", "distant-only"])
+def test_c3_escaped_rays_match_oracle(pa, oracle, skies):
+    """HandleEscapedRays (integrator.cpp:495-537) in both k_escaped forms: one infinite light
+    with Le (sky spectrum and sensor curves staged in LDS), two (the general loop, per-light
+    sums in pbrt's order) and a distant light alone in the infinite list (no Le: escaped rays
+    add nothing)."""
+    import sys
+    sys.path.insert(0, str(SCENES))
+    import gen_c3
+    text = gen_c3.scene_text(96, 54, 8)
+    assert text.count('LightSource "infinite"') == 1
+    if skies == 2:
+        text = text.replace("WorldBegin", 'WorldBegin\nLightSource "infinite" "rgb L" [ 0.3 0.2 0.1 ] "float scale" 0.7\n', 1)
+    elif skies == 0:
+        text = "\n".join(l for l in text.splitlines() if not l.lstrip().startswith('LightSource "infinite"'))
+        text = text.replace("WorldBegin", 'WorldBegin\nLightSource "distant" "rgb L" [ 1 1 1 ] "point3 from" [ 1 2 -1 ] '
+                            '"point3 to" [ 0 0 0 ]\n', 1)
+    sc = pa.Scene.from_string(text, SCENES)
+    f = sc.flat()
+    assert f.n_infinite_lights == (skies if skies else 1)
+    film, _ = gpu_film(pa, sc)
+    frac, mean_rel = check_parity(to_rgb(oracle, sc, film), to_rgb(oracle, sc, oracle.render(sc, threads=16)))
+    print(f"C3 escaped rays ({skies} skies): {frac*100:.3f}% pixels within 1e-3, mean rel {mean_rel:.2e}")
+
+
+def test_c4_named_metals_match_oracle(pa, oracle, tmp_path):
+    """C4's generator at a small size: rough conductors with pbrt's named metal spectra (56-knot
+    piecewise-linear eta / k, walked knot by knot over each path's wavelengths) beside diffuse
+    copies, PLY meshes, area light and sky."""
+    import sys
+    sys.path.insert(0, str(SCENES))
+    import gen_c4
+    path, _ = gen_c4.generate(tmp_path, copies=12, level=3, xres=96, yres=54, spp=8)
+    sc = pa.load_scene(path)
+    film, _ = gpu_film(pa, sc)
+    frac, mean_rel = check_parity(to_rgb(oracle, sc, film), to_rgb(oracle, sc, oracle.render(sc, threads=16)))
+    print(f"C4 small (named metals): {frac*100:.3f}% pixels within 1e-3, mean rel {mean_rel:.2e}")
+
+
 def test_index_matched_glass_invisible_gpu(pa, oracle):
     import sys
     sys.path.insert(0, str(SCENES.parent / "tests"))

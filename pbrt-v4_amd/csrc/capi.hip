@@ -677,6 +677,12 @@ static void BuildDevice(pbrt_context *c) {
         off = align16(off + (permEntries + 1) * 2);
         for (int depth = s.maxDepth; depth < kShadeLdsDepths; ++depth) L.totalByDepth[depth] = off;
         L.total = off;
+        // conductor eta / k knots, searched per wavelength: the microfacet launches stage a
+        // small set (up to one named-metal pair, 2 x 56 knots) after their depth's permutation
+        // tables.  C3 (two 2-knot spectra): +2.7 %; C4's ten 56-knot spectra ran 1 % slower
+        // from LDS than through L1, so larger sets stay in global memory.
+        L.plCount = (int)c->plLambda.n;
+        L.plInLds = ((S.matTypeMask >> kMatConductorT) & 1) && L.plCount <= 128 ? 1 : 0;
         if (L.total > 64 * 1024 && !c->volumetric) throw Error("shade kernel LDS layout exceeds 64 KB");
     }
     S.stackSize = c->bvh.maxStack;

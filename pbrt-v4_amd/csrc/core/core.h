@@ -985,7 +985,8 @@ struct TrowbridgeReitz {
 };
 // PiecewiseLinearSpectrum::operator() (util/spectrum.cpp:68-78): FindInterval's result is the
 // largest knot index o <= n-2 with lambda[o] <= l
-PHD float PiecewiseLinearEval(const float *lam, const float *val, int n, float l) {
+template <typename F>  // const float, or its LDS-qualified form
+PHD float PiecewiseLinearEval(F *lam, F *val, int n, float l) {
     if (n == 0 || l < lam[0] || l > lam[n - 1]) return 0;
     int lo = 0, hi = n - 2;
     while (lo < hi) {

@@ -40,6 +40,7 @@ constexpr int kShadeLdsDepths = 16;
 struct ShadeLdsLayout {
     int sensor, dense, perm, lights, lightNodes, mats, matConst, total;
     int denseInLds, lightsInLds, matsInLds, permEntries;
+    int plInLds, plCount;  // conductor eta / k knots (lambdas, then values) after the perm tables
     int totalByDepth[kShadeLdsDepths];  // bytes a launch at that depth needs (perm tables last)
 };
 

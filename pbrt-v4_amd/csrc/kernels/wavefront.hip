@@ -345,7 +345,10 @@ struct ShadeTables {
     const DeviceAreaLight *lightsL;
     const float4 *matsL;
     const int *matConstL;
+    LdsF *plLamL, *plValL;  // conductor knots when lay.plInLds
 };
+// WithPl: also the conductor knots (lay.plInLds), after this depth's permutation tables
+template <bool WithPl = false>
 __device__ __forceinline__ void StageShadeTables(const DeviceScene &S, int depth, char *ldsBase, ShadeTables *T) {
     const ShadeLdsLayout lay = S.shadeLds;
     T->lay = lay;
@@ -373,6 +376,11 @@ __device__ __forceinline__ void StageShadeTables(const DeviceScene &S, int depth
         DmaCopy<16>(S.matCoeffs, matsLds, S.nMaterials);
         DmaCopy<4>(S.matConstant, matConstLds, S.nMaterials);
     }
+    float *plLds = reinterpret_cast<float *>(ldsBase + (depth < kShadeLdsDepths ? lay.totalByDepth[depth] : lay.total));
+    if (WithPl && lay.plInLds) {
+        DmaCopy<4>(S.plLambda, plLds, lay.plCount);
+        DmaCopy<4>(S.plValue, plLds + lay.plCount, lay.plCount);
+    }
     DmaWait();
     __syncthreads();
     T->sensorL = (const LdsF4 *)sensorLds;
@@ -382,6 +390,8 @@ __device__ __forceinline__ void StageShadeTables(const DeviceScene &S, int depth
     T->lightsL = lay.lightsInLds ? lightsLds : S.lights;
     T->matsL = lay.matsInLds ? matsLds : S.matCoeffs;
     T->matConstL = lay.matsInLds ? matConstLds : S.matConstant;
+    T->plLamL = (LdsF *)plLds;
+    T->plValL = (LdsF *)(plLds + lay.plCount);
 }
 
 // GenerateRaySamples (samples.cpp:29-66): dims d0 + {0..6} = direct.uc, direct.u (2),
@@ -706,7 +716,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
     if ((int)(blockIdx.x * blockDim.x) >= mats.total) return;  // no work
     extern __shared__ float4 dynLds[];
     ShadeTables T;
-    StageShadeTables(S, depth, reinterpret_cast<char *>(dynLds), &T);
+    StageShadeTables<true>(S, depth, reinterpret_cast<char *>(dynLds), &T);
     const ShadeLdsLayout &lay = T.lay;
     const int d0 = 6 + 7 * depth;
     const int N = st.NR;
@@ -762,8 +772,13 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
                 if (etaSpec >= 0) {
                     const int a = S.plOffsets[etaSpec], na = S.plOffsets[etaSpec + 1] - a;
                     const int b = S.plOffsets[kSpec], nb = S.plOffsets[kSpec + 1] - b;
-                    *e = PiecewiseLinearEval(S.plLambda + a, S.plValue + a, na, lam);
-                    *k = PiecewiseLinearEval(S.plLambda + b, S.plValue + b, nb, lam);
+                    if (lay.plInLds) {
+                        *e = PiecewiseLinearEval(T.plLamL + a, T.plValL + a, na, lam);
+                        *k = PiecewiseLinearEval(T.plLamL + b, T.plValL + b, nb, lam);
+                    } else {
+                        *e = PiecewiseLinearEval(S.plLambda + a, S.plValue + a, na, lam);
+                        *k = PiecewiseLinearEval(S.plLambda + b, S.plValue + b, nb, lam);
+                    }
                 } else {
                     float r = Clampf(SigmoidPolynomial(mc.x, mc.y, mc.z, lam), 0, .9999f);
                     *e = 1.f;
@@ -1161,8 +1176,10 @@ hipError_t LaunchEmissive(const DeviceScene &S, const PathState &st, int depth, 
 }
 // Dynamic LDS of a shade launch: the layout up to this depth's Halton permutation tables, which
 // come last and grow with the depth's prime bases (ShadeLdsLayout::totalByDepth)
-static size_t ShadeLdsBytes(const DeviceScene &S, int depth) {
-    return (size_t)(depth < kShadeLdsDepths ? S.shadeLds.totalByDepth[depth] : S.shadeLds.total);
+static size_t ShadeLdsBytes(const DeviceScene &S, int depth, bool withPl = false) {
+    const ShadeLdsLayout &L = S.shadeLds;
+    return (size_t)(depth < kShadeLdsDepths ? L.totalByDepth[depth] : L.total) +
+           (withPl && L.plInLds ? (size_t)L.plCount * 8 : 0);
 }
 hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int depth, int maxCount, bool lean,
                               hipStream_t s) {
@@ -1178,10 +1195,10 @@ hipError_t LaunchShadeMicrofacet(const DeviceScene &S, const PathState &st, int 
                                  hipStream_t s) {
     if (type == kMatDielectricT)
         hipLaunchKernelGGL(k_shade_microfacet<kMatDielectricT>, dim3(ShadeGridFor(maxCount)), dim3(kBlock),
-                           ShadeLdsBytes(S, depth), s, S, st, depth);
+                           ShadeLdsBytes(S, depth, true), s, S, st, depth);
     else
         hipLaunchKernelGGL(k_shade_microfacet<kMatConductorT>, dim3(ShadeGridFor(maxCount)), dim3(kBlock),
-                           ShadeLdsBytes(S, depth), s, S, st, depth);
+                           ShadeLdsBytes(S, depth, true), s, S, st, depth);
     return hipGetLastError();
 }
 hipError_t LaunchShadow(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s) {

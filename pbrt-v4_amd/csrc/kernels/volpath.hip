@@ -432,6 +432,11 @@ __device__ inline VRaySamples RaySamplesAt(const DeviceScene &S, const PathState
 // every 31 record loads and stores off the HBM stream.  The values read back are the same bits.
 constexpr int kUniBeta = 4, kUniRu = 8, kUniRl = 16;      // VolRecords::flags
 constexpr int kShUniLd = 1, kShUniRu = 2, kShUniRl = 4;   // VolState::shFlags
+// kShRgb (grey media only): shLd rows 0-2 hold the sensor-weighted sums sum_i xyz_bar(l_i) Ld_i
+// and row 3 holds Ld_0, so the grey shadow kernel scales four values by T_ray / avg instead of
+// reading 31.  Linear, as pbrt's film conversion of L is; the rounding order differs from the
+// per-wavelength form by float ulps (parity: within the tests' 1e-3 tolerance).
+constexpr int kShRgb = 8;
 __device__ inline void LoadSpec(const float *base, int NR, int ri, float v[kNS], bool uni = false) {
     if (uni) {
         const float x = base[ri];
@@ -897,11 +902,25 @@ struct ShadowOut {
     V3 o, d;
     int medium;
 };
-__device__ inline void WriteShadow(const VolState &v, int NR, int j, const ShadowOut &s, const float *Ld,
-                                   const float *ru, const float *rl, float lambda0, int slot) {
+// S: the scene, for grey media (kShRgb: Ld as its sensor sums + Ld_0)
+__device__ inline void WriteShadow(const DeviceScene &S, const VolState &v, int NR, int j, const ShadowOut &s,
+                                   const float *Ld, const float *ru, const float *rl, float lambda0, int slot) {
     StoreV3(v.shRay, NR, j, s.o);
     StoreV3(v.shRay + 3 * (size_t)NR, NR, j, s.d);
-    int fl = StoreSpec(v.shLd, NR, j, Ld) ? kShUniLd : 0;
+    int fl;
+    if (S.media.allGrey) {
+        SensorAcc acc;
+        SpectralIter it(lambda0);
+#pragma unroll
+        for (int i = 0; i < kNS; ++i, it.Next()) acc.Add(S, DenseOffset(it.lam), Ld[i], i == 0);
+        v.shLd[j] = acc.sx;
+        v.shLd[NR + j] = acc.sy;
+        v.shLd[2 * (size_t)NR + j] = acc.sz;
+        v.shLd[3 * (size_t)NR + j] = Ld[0];
+        fl = kShRgb;
+    } else {
+        fl = StoreSpec(v.shLd, NR, j, Ld) ? kShUniLd : 0;
+    }
     fl |= StoreSpec(v.shRu, NR, j, ru) ? kShUniRu : 0;
     fl |= StoreSpec(v.shRl, NR, j, rl) ? kShUniRl : 0;
     v.shFlags[j] = fl;
@@ -1309,9 +1328,28 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
                     const V3 pt = OffsetRayOrigin(ls.p, ls.pErr, ls.n, so - ls.p);
                     const V3 sd = pt - so;
                     // Ld_i = beta_i f_i |cos| Le_i; r_u / r_l follow r_u
-                    bool fnz = mtype == 0, ldUni = true;
+                    bool fnz = mtype == 0, ldUni = true, rgb = false;
                     int js = -1;
-                    if (mtype == 0) {
+                    if (mtype == 0 && S.media.allGrey) {
+                        // f_i from LDS; Ld as its sensor sums + Ld_0 (kShRgb)
+                        js = shardBase + WavePush(shadowCnt, true);
+                        SpectralIter it(lambda0);
+                        SensorAcc acc;
+                        float ld0 = 0;
+#pragma unroll 1
+                        for (int i = 0; i < kNS; ++i, it.Next()) {
+                            const int off = DenseOffset(it.lam);
+                            const float Ldv = betaIn(i) * fL[i * kBlock] * absdot * ls.Le(S, off);
+                            ld0 = i == 0 ? Ldv : ld0;
+                            acc.Add(S, off, Ldv, i == 0);
+                        }
+                        v.shLd[js] = acc.sx;
+                        v.shLd[NR + js] = acc.sy;
+                        v.shLd[2 * (size_t)NR + js] = acc.sz;
+                        v.shLd[3 * (size_t)NR + js] = ld0;
+                        ldUni = false;
+                        rgb = true;
+                    } else if (mtype == 0) {
                         // f_i from LDS (nonzero somewhere: the flags pass), Ld straight to the queue
                         js = shardBase + WavePush(shadowCnt, true);
                         SpectralIter it(lambda0);
@@ -1354,7 +1392,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
                                 v.shRl[(size_t)i * NR + js] = ru * lightPDF;
                             }
                         }
-                        v.shFlags[js] = (ldUni ? kShUniLd : 0) | (ruUni ? kShUniRu | kShUniRl : 0);
+                        v.shFlags[js] = (ldUni ? kShUniLd : 0) | (ruUni ? kShUniRu | kShUniRl : 0) | (rgb ? kShRgb : 0);
                         StoreV3(v.shRay, NR, js, so);
                         StoreV3(v.shRay + 3 * (size_t)NR, NR, js, sd);
                         v.shLambda0[js] = lambda0;
@@ -1751,7 +1789,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vscatter(DeviceScene
                 so.d = ls.p - pS;
                 so.medium = medium;
                 const int pos = WavePush(shadowCnt, true);
-                WriteShadow(v, NR, shardBase + pos, so, Ld, sru, srl, lambda0, slot);
+                WriteShadow(S, v, NR, shardBase + pos, so, Ld, sru, srl, lambda0, slot);
             }
         }
         // indirect: phase-function sample, RR, next ray at depth + 1
@@ -1991,11 +2029,19 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_vshadow_grey(D
             denSum = i == 0 ? dv : denSum + dv;
         }
         const float avg = denSum / kNS;
+        const int slot = v.shPixel[p], NL = st.N;
+        if (shf & kShRgb) {
+            const float q = Tr / avg;
+            st.L[slot] += S.imagingRatio * ((v.shLd[p] * q) / kNS);
+            st.L[NL + slot] += S.imagingRatio * ((v.shLd[NR + p] * q) / kNS);
+            st.L[2 * NL + slot] += S.imagingRatio * ((v.shLd[2 * (size_t)NR + p] * q) / kNS);
+            AddL0Off(S, st, slot, DenseOffset(lambda0), v.shLd[3 * (size_t)NR + p] * Tr / avg);
+            continue;
+        }
         SensorAcc acc;
         SpectralIter it(lambda0);
 #pragma unroll 1
         for (int i = 0; i < kNS; ++i, it.Next()) acc.Add(S, DenseOffset(it.lam), ldIn(i) * Tr / avg, i == 0);
-        const int slot = v.shPixel[p], NL = st.N;
         st.L[slot] += S.imagingRatio * (acc.sx / kNS);
         st.L[NL + slot] += S.imagingRatio * (acc.sy / kNS);
         st.L[2 * NL + slot] += S.imagingRatio * (acc.sz / kNS);

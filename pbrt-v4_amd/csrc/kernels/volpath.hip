@@ -540,6 +540,11 @@ __global__ void __launch_bounds__(kBlock) k_vcamera(DeviceScene S, PathState st,
     r.medium[slot] = S.media.cameraMedium;
 }
 
+// a surface hit on Material "interface" (type 3): the ray only changes medium (k_viface)
+__device__ inline bool IsInterfaceHit(const DeviceScene &S, int prim) {
+    return prim >= 0 && S.matType[S.primMaterial[prim]] == 3;
+}
+
 template <int TM>
 __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_vclosest(DeviceScene S, PathState st, VolState v,
                                                                           int wf, int timed) {
@@ -552,6 +557,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_vclosest(Devic
     const int shard = ProducerShard();
     int *medCnt = &st.counters[CounterIndex(wf, kVMed, shard)];
     int *surfCnt = &st.counters[CounterIndex(wf, kVSurf, shard)];
+    int *ifaceCnt = &st.counters[CounterIndex(wf, kVIface, shard)];
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         atomicAdd(&st.stats[1], (unsigned long long)rays.total);
         if (timed) atomicAdd(&st.stats[3], (unsigned long long)rays.total);  // rays of event-timed launches
@@ -561,6 +567,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_vclosest(Devic
         const bool active = j < rays.total;
         const int ri = active ? QueueSlot(rays, j) : 0;
         int medium = -1;
+        bool iface = false;
         if (active) {
             const V3 o = LoadV3(rec.ray, NR, ri), d = LoadV3(rec.ray + 3 * (size_t)NR, NR, ri);
             TriHit h;
@@ -571,12 +578,16 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_vclosest(Devic
             v.hitB[2 * NR + ri] = h.b2;
             v.hitB[3 * NR + ri] = prim >= 0 ? h.t : kInfinity;
             medium = rec.medium[ri];
+            iface = medium < 0 && IsInterfaceHit(S, prim);
         }
         // rays inside a medium sample it first (MediumSampleQueue), the rest go to the surface
+        // (interface crossings to their own queue)
         const int pm = WavePush(medCnt, active && medium >= 0);
-        const int ps = WavePush(surfCnt, active && medium < 0);
+        const int ps = WavePush(surfCnt, active && medium < 0 && !iface);
+        const int pf = WavePush(ifaceCnt, active && iface);
         if (pm >= 0) v.medQ[shard * st.capS + pm] = ri;
         if (ps >= 0) v.surfQ[shard * st.capS + ps] = ri;
+        if (pf >= 0) v.ifaceQ[shard * st.capS + pf] = ri;
     }
 }
 
@@ -722,10 +733,13 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vmedium(DeviceScene 
                 toSurf = true;
             }
         }
-        const int p0 = WavePush(surfCnt, toSurf);
+        const bool iface = toSurf && IsInterfaceHit(S, v.hitPrim[ri]);
+        const int p0 = WavePush(surfCnt, toSurf && !iface);
         const int p1 = WavePush(scatCnt, toScat);
+        const int p2 = WavePush(&st.counters[CounterIndex(wf, kVIface, shard)], iface);
         if (p0 >= 0) v.surfQ[shard * st.capS + p0] = ri;
         if (p1 >= 0) v.scatQ[shard * st.capS + p1] = ri;
+        if (p2 >= 0) v.ifaceQ[shard * st.capS + p2] = ri;
     }
 }
 
@@ -891,10 +905,13 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_GREY_WAVES) k_vmedium_grey(De
                 toSurf = true;
             }
         }
-        const int p0 = WavePush(surfCnt, toSurf);
+        const bool iface = toSurf && IsInterfaceHit(S, v.hitPrim[ri]);
+        const int p0 = WavePush(surfCnt, toSurf && !iface);
         const int p1 = WavePush(scatCnt, toScat);
+        const int p2 = WavePush(&st.counters[CounterIndex(wf, kVIface, shard)], iface);
         if (p0 >= 0) v.surfQ[shard * st.capS + p0] = ri;
         if (p1 >= 0) v.scatQ[shard * st.capS + p1] = ri;
+        if (p2 >= 0) v.ifaceQ[shard * st.capS + p2] = ri;
     }
 }
 
@@ -1174,31 +1191,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
         MediaOf(S, prim, medium, &mIn, &mOut);
         const int mat = S.primMaterial[prim];
         const int mtypeHit = S.matType[mat];
-        if (mtypeHit == 3) {
-            // Material "interface": SpawnRay(ray.d) at the same path depth (media.cpp:193-203)
-            if (last) continue;
-            const int jn = shardBase + WavePush(nextCnt, true);
-            out.beta[jn] = betaIn.v0;
-            out.ru[jn] = ruIn.v0;
-            out.rl[jn] = rlIn.v0;
-#pragma unroll 2
-            for (int i = 1; i < kNS; ++i) {
-                if (!betaUni) out.beta[(size_t)i * NR + jn] = betaIn(i);
-                if (!ruUni) out.ru[(size_t)i * NR + jn] = ruIn(i);
-                if (!rlUni) out.rl[(size_t)i * NR + jn] = rlIn(i);
-            }
-            StoreV3(out.ray, NR, jn, OffsetRayOrigin(si.p, si.pErr, si.n, rd));
-            StoreV3(out.ray + 3 * (size_t)NR, NR, jn, rd);
-#pragma unroll
-            for (int k = 0; k < 12; ++k) out.prev[(size_t)k * NR + jn] = rec.prev[(size_t)k * NR + ri];
-            out.lambda0[jn] = lambda0;
-            out.etaScale[jn] = rec.etaScale[ri];
-            out.flags[jn] = flags;
-            out.pixel[jn] = slot;
-            out.depth[jn] = depth;
-            out.medium[jn] = DotN(si.n, rd) > 0 ? mOut : mIn;
-            continue;
-        }
+        if (mtypeHit == 3) continue;  // interface crossings: k_viface
         // HandleEmissiveIntersection (integrator.cpp:539-573)
         const int light = S.primLight[prim];
         if (light >= 0) {
@@ -1503,6 +1496,54 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
         out.pixel[jn] = slot;
         out.depth[jn] = depth + 1;
         out.medium[jn] = DotN(si.n, wi) > 0 ? mOut : mIn;
+    }
+}
+
+// Material "interface" crossings (media.cpp:193-203): SpawnRay(ray.d) at the same path depth into
+// the medium on the far side.  Split from k_vsurface (their own queue, filled by the closest-hit
+// and medium kernels), so these items do not hold that kernel's registers and lanes.
+__global__ void __launch_bounds__(kBlock) k_viface(DeviceScene S, PathState st, VolState v, int wf) {
+    const QueueView q = LoadQueue(st, wf, kVIface);
+    if ((int)(blockIdx.x * blockDim.x) >= q.total || wf == S.maxDepth) return;  // last: path ends
+    const int NR = st.NR;
+    const VolRecords &rec = v.rec[wf & 1], &out = v.rec[(wf + 1) & 1];
+    const int shardBase = ProducerShard() * st.capS;
+    int *nextCnt = &st.counters[CounterIndex(wf + 1, kVRay, ProducerShard())];
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < q.total; j += gridDim.x * blockDim.x) {
+        const int ri = v.ifaceQ[QueueSlot(q, j)];
+        const float lambda0 = rec.lambda0[ri];
+        const int slot = rec.pixel[ri];
+        const int depth = rec.depth[ri], flags = rec.flags[ri], medium = rec.medium[ri];
+        const bool betaUni = flags & kUniBeta, ruUni = flags & kUniRu, rlUni = flags & kUniRl;
+        const SpecIn betaIn(rec.beta, NR, ri, betaUni), ruIn(rec.ru, NR, ri, ruUni), rlIn(rec.rl, NR, ri, rlUni);
+        const V3 rd = LoadV3(rec.ray + 3 * (size_t)NR, NR, ri);
+        const int prim = v.hitPrim[ri];
+        const float b0 = v.hitB[ri], b1 = v.hitB[NR + ri], b2 = v.hitB[2 * NR + ri];
+        V3 p0, p1, p2;
+        PrimVerts(S, prim, &p0, &p1, &p2);
+        const TriSurface si = SurfaceAt(S, prim, p0, p1, p2, b0, b1, b2);
+        int mIn, mOut;
+        MediaOf(S, prim, medium, &mIn, &mOut);
+        const int jn = shardBase + WavePush(nextCnt, true);
+        out.beta[jn] = betaIn.v0;
+        out.ru[jn] = ruIn.v0;
+        out.rl[jn] = rlIn.v0;
+#pragma unroll 2
+        for (int i = 1; i < kNS; ++i) {
+            if (!betaUni) out.beta[(size_t)i * NR + jn] = betaIn(i);
+            if (!ruUni) out.ru[(size_t)i * NR + jn] = ruIn(i);
+            if (!rlUni) out.rl[(size_t)i * NR + jn] = rlIn(i);
+        }
+        StoreV3(out.ray, NR, jn, OffsetRayOrigin(si.p, si.pErr, si.n, rd));
+        StoreV3(out.ray + 3 * (size_t)NR, NR, jn, rd);
+#pragma unroll
+        for (int k = 0; k < 12; ++k) out.prev[(size_t)k * NR + jn] = rec.prev[(size_t)k * NR + ri];
+        out.lambda0[jn] = lambda0;
+        out.etaScale[jn] = rec.etaScale[ri];
+        out.flags[jn] = flags;
+        out.pixel[jn] = slot;
+        out.depth[jn] = depth;
+        out.medium[jn] = DotN(si.n, rd) > 0 ? mOut : mIn;
     }
 }
 
@@ -2085,6 +2126,7 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
     if (S.matTypeMask & other) hipLaunchKernelGGL(k_vsurface<false>, gW, block, surfLds, s, S, st, v, wf);
     else hipLaunchKernelGGL(k_vsurface<true>, gW, block, surfLds, s, S, st, v, wf);
     if (wf == S.maxDepth) return hipGetLastError();
+    if (S.matTypeMask & (1 << 3)) hipLaunchKernelGGL(k_viface, gW, block, 0, s, S, st, v, wf);
     if (S.matTypeMask & ((1 << kMatCoatedDiffuseT) | (1 << kMatCoatedConductorT) | (1 << kMatDiffuseTransmissionT)))
         hipLaunchKernelGGL(k_vlayered, gW, block, 0, s, S, st, v, wf);
     hipLaunchKernelGGL(k_vscatter, gW, block, 0, s, S, st, v, wf);

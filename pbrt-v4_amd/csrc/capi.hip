@@ -775,8 +775,8 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
     if (c->volumetric) {
         // VolState: records 2 x (beta, r_u, r_l 93 + ray 6 + prev 12 + lambda0, etaScale 2) = 226,
         // hitB 4, shadow ray 6 + Ld/r_u/r_l 93 + lambda0 = 100 floats; records 2 x (flags, pixel,
-        // depth, medium) = 8, hitPrim, 4 queues, shadow pixel + medium + flags = 16 ints
-        const int vf = 330, vi = 16;
+        // depth, medium) = 8, hitPrim, 5 queues, shadow pixel + medium + flags = 17 ints
+        const int vf = 330, vi = 17;
         c->vfState.Alloc((size_t)vf * NR);
         c->viState.Alloc((size_t)vi * NR);
         float *g = c->vfState.p;
@@ -817,6 +817,7 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
         v.surfQ = ti(1);
         v.scatQ = ti(1);
         v.ifaceQ = ti(1);
+        v.escQ = ti(1);
         v.shPixel = ti(1);
         v.shMedium = ti(1);
         v.shFlags = ti(1);

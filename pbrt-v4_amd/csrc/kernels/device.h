@@ -263,11 +263,12 @@ struct VolRecords {
 // queues of one iteration (counters at CounterIndex(iteration, queue, shard))
 constexpr int kVRay = 0, kVSurf = 1, kVShadow = 2, kVMed = 3, kVScat = 4;
 constexpr int kVIface = 5;  // surface hits on Material "interface" (k_viface)
+constexpr int kVEsc = 6;    // escaped rays (k_vescaped)
 struct VolState {
     VolRecords rec[2];
     int *hitPrim;  // [NR] this iteration's closest hit (-1: none)
     float *hitB;   // [4][NR] b0 b1 b2 t; a medium scattering event stores its point in b0..b2
-    int *medQ, *surfQ, *scatQ, *ifaceQ;  // record indices
+    int *medQ, *surfQ, *scatQ, *ifaceQ, *escQ;  // record indices
     // shadow rays (ShadowRayWorkItem with spectral Ld, r_u, r_l), compacted
     float *shRay;              // [6][NR] o, d (d unnormalised, tMax = 1 - ShadowEpsilon)
     float *shLd, *shRu, *shRl; // [31][NR]

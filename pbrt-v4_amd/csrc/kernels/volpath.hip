@@ -567,7 +567,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_vclosest(Devic
         const bool active = j < rays.total;
         const int ri = active ? QueueSlot(rays, j) : 0;
         int medium = -1;
-        bool iface = false;
+        bool iface = false, esc = false;
         if (active) {
             const V3 o = LoadV3(rec.ray, NR, ri), d = LoadV3(rec.ray + 3 * (size_t)NR, NR, ri);
             TriHit h;
@@ -579,15 +579,18 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_vclosest(Devic
             v.hitB[3 * NR + ri] = prim >= 0 ? h.t : kInfinity;
             medium = rec.medium[ri];
             iface = medium < 0 && IsInterfaceHit(S, prim);
+            esc = medium < 0 && prim < 0;
         }
         // rays inside a medium sample it first (MediumSampleQueue), the rest go to the surface
-        // (interface crossings to their own queue)
+        // (interface crossings and escaped rays to their own queues)
         const int pm = WavePush(medCnt, active && medium >= 0);
-        const int ps = WavePush(surfCnt, active && medium < 0 && !iface);
+        const int ps = WavePush(surfCnt, active && medium < 0 && !iface && !esc);
         const int pf = WavePush(ifaceCnt, active && iface);
+        const int pe = WavePush(&st.counters[CounterIndex(wf, kVEsc, shard)], active && esc);
         if (pm >= 0) v.medQ[shard * st.capS + pm] = ri;
         if (ps >= 0) v.surfQ[shard * st.capS + ps] = ri;
         if (pf >= 0) v.ifaceQ[shard * st.capS + pf] = ri;
+        if (pe >= 0) v.escQ[shard * st.capS + pe] = ri;
     }
 }
 
@@ -733,13 +736,16 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vmedium(DeviceScene 
                 toSurf = true;
             }
         }
-        const bool iface = toSurf && IsInterfaceHit(S, v.hitPrim[ri]);
-        const int p0 = WavePush(surfCnt, toSurf && !iface);
+        const int hp = toSurf ? v.hitPrim[ri] : 0;
+        const bool iface = toSurf && IsInterfaceHit(S, hp), esc = toSurf && hp < 0;
+        const int p0 = WavePush(surfCnt, toSurf && !iface && !esc);
         const int p1 = WavePush(scatCnt, toScat);
         const int p2 = WavePush(&st.counters[CounterIndex(wf, kVIface, shard)], iface);
+        const int p3 = WavePush(&st.counters[CounterIndex(wf, kVEsc, shard)], esc);
         if (p0 >= 0) v.surfQ[shard * st.capS + p0] = ri;
         if (p1 >= 0) v.scatQ[shard * st.capS + p1] = ri;
         if (p2 >= 0) v.ifaceQ[shard * st.capS + p2] = ri;
+        if (p3 >= 0) v.escQ[shard * st.capS + p3] = ri;
     }
 }
 
@@ -905,13 +911,16 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_GREY_WAVES) k_vmedium_grey(De
                 toSurf = true;
             }
         }
-        const bool iface = toSurf && IsInterfaceHit(S, v.hitPrim[ri]);
-        const int p0 = WavePush(surfCnt, toSurf && !iface);
+        const int hp = toSurf ? v.hitPrim[ri] : 0;
+        const bool iface = toSurf && IsInterfaceHit(S, hp), esc = toSurf && hp < 0;
+        const int p0 = WavePush(surfCnt, toSurf && !iface && !esc);
         const int p1 = WavePush(scatCnt, toScat);
         const int p2 = WavePush(&st.counters[CounterIndex(wf, kVIface, shard)], iface);
+        const int p3 = WavePush(&st.counters[CounterIndex(wf, kVEsc, shard)], esc);
         if (p0 >= 0) v.surfQ[shard * st.capS + p0] = ri;
         if (p1 >= 0) v.scatQ[shard * st.capS + p1] = ri;
         if (p2 >= 0) v.ifaceQ[shard * st.capS + p2] = ri;
+        if (p3 >= 0) v.escQ[shard * st.capS + p3] = ri;
     }
 }
 
@@ -1160,28 +1169,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
         const SpecIn betaIn(rec.beta, NR, ri, betaUni), ruIn(rec.ru, NR, ri, ruUni), rlIn(rec.rl, NR, ri, rlUni);
         const V3 rd = LoadV3(rec.ray + 3 * (size_t)NR, NR, ri);
         const int prim = v.hitPrim[ri];
-        if (prim < 0) {
-            // HandleEscapedRays (integrator.cpp:495-537): UniformInfiniteLight, whose
-            // PDF_Li(allowIncompletePDF) is 0, so r_l adds nothing to the MIS denominator
-            if (S.nInfinite == 0) continue;
-            float ds = 0;
-#pragma unroll 1
-            for (int i = 0; i < kNS; ++i) {
-                const float ru = ruIn(i);
-                const float dv = (depth == 0 || specularBounce) ? ru : ru + rlIn(i) * 0.f;
-                ds = i == 0 ? dv : ds + dv;
-            }
-            const float avg = ds / kNS;
-            // (a light with Le = 0 at every wavelength adds exact zeros: no separate test)
-            for (int k = 0; k < S.nInfinite; ++k) {
-                if (S.infDistant[k] >= 0) continue;  // a DistantLight is no Infinite-type light
-                const int spec = S.infSpectrum[k];
-                const float scale = S.infScale[k];
-                AddSpecToL(S, st, slot, lambda0,
-                           [&](int i, int off) { return betaIn(i) * (scale * DenseAt(S, spec, off)) / avg; });
-            }
-            continue;
-        }
+        if (prim < 0) continue;  // escaped rays: k_vescaped
         const float b0 = v.hitB[ri], b1 = v.hitB[NR + ri], b2 = v.hitB[2 * NR + ri];
         V3 p0, p1, p2;
         PrimVerts(S, prim, &p0, &p1, &p2);
@@ -1496,6 +1484,45 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
         out.pixel[jn] = slot;
         out.depth[jn] = depth + 1;
         out.medium[jn] = DotN(si.n, wi) > 0 ? mOut : mIn;
+    }
+}
+
+// HandleEscapedRays (integrator.cpp:495-537) for the volumetric wavefront: UniformInfiniteLight,
+// whose PDF_Li(allowIncompletePDF) is 0, so r_l adds nothing to the MIS denominator.  Escaped
+// rays have their own queue (filled by the closest-hit and medium kernels) and kernel, with the
+// sensor curves and spectra staged in LDS.
+__global__ void __launch_bounds__(kBlock) k_vescaped(DeviceScene S0, PathState st, VolState v, int wf) {
+    const QueueView q = LoadQueue(st, wf, kVEsc);
+    if ((int)(blockIdx.x * blockDim.x) >= q.total || S0.nInfinite == 0) return;
+    extern __shared__ float4 dynLds[];
+    DeviceScene S = S0;
+    StageVolTables(S0, S, reinterpret_cast<char *>(dynLds));
+    const int NR = st.NR;
+    const VolRecords &rec = v.rec[wf & 1];
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < q.total; j += gridDim.x * blockDim.x) {
+        const int ri = v.escQ[QueueSlot(q, j)];
+        const float lambda0 = rec.lambda0[ri];
+        const int slot = rec.pixel[ri];
+        const int depth = rec.depth[ri], flags = rec.flags[ri];
+        const bool specularBounce = flags & 1;
+        const SpecIn betaIn(rec.beta, NR, ri, flags & kUniBeta), ruIn(rec.ru, NR, ri, flags & kUniRu),
+            rlIn(rec.rl, NR, ri, flags & kUniRl);
+        float ds = 0;
+#pragma unroll 1
+        for (int i = 0; i < kNS; ++i) {
+            const float ru = ruIn(i);
+            const float dv = (depth == 0 || specularBounce) ? ru : ru + rlIn(i) * 0.f;
+            ds = i == 0 ? dv : ds + dv;
+        }
+        const float avg = ds / kNS;
+        // (a light with Le = 0 at every wavelength adds exact zeros: no separate test)
+        for (int k = 0; k < S.nInfinite; ++k) {
+            if (S.infDistant[k] >= 0) continue;  // a DistantLight is no Infinite-type light
+            const int spec = S.infSpectrum[k];
+            const float scale = S.infScale[k];
+            AddSpecToL(S, st, slot, lambda0,
+                       [&](int i, int off) { return betaIn(i) * (scale * DenseAt(S, spec, off)) / avg; });
+        }
     }
 }
 
@@ -2125,6 +2152,7 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
     const size_t surfLds = VolTablesLdsBytes(S) + kNS * kBlock * sizeof(float);
     if (S.matTypeMask & other) hipLaunchKernelGGL(k_vsurface<false>, gW, block, surfLds, s, S, st, v, wf);
     else hipLaunchKernelGGL(k_vsurface<true>, gW, block, surfLds, s, S, st, v, wf);
+    if (S.nInfinite > 0) hipLaunchKernelGGL(k_vescaped, gW, block, VolTablesLdsBytes(S), s, S, st, v, wf);
     if (wf == S.maxDepth) return hipGetLastError();
     if (S.matTypeMask & (1 << 3)) hipLaunchKernelGGL(k_viface, gW, block, 0, s, S, st, v, wf);
     if (S.matTypeMask & ((1 << kMatCoatedDiffuseT) | (1 << kMatCoatedConductorT) | (1 << kMatDiffuseTransmissionT)))

@@ -5,13 +5,14 @@
 //   k_vcamera    GenerateCameraRays (camera.cpp:31-80) + the camera medium
 //   k_vclosest   IntersectClosest (integrator.h:39-45): closest hit; rays inside a medium go to
 //                the medium-sample queue (MediumSampleQueue, intersect.h:48-80), the rest to
-//                the surface queue
+//                the surface, interface-crossing or escaped-ray queue
 //   k_vmedium    SampleMediumInteraction (media.cpp:22-247): delta tracking along the ray
 //                through SampleT_maj (media.h:725-800) with the homogeneous / DDA majorant
 //                iterators (media.h:79-205), medium emission, absorption / real scattering /
-//                null scattering; survivors continue to the surface queue
-//   k_vsurface   the surface side: HandleEscapedRays (integrator.cpp:495-537), interface
-//                crossings (media.cpp:193-203), HandleEmissiveIntersection (:539-573) and
+//                null scattering; survivors continue to the same three queues
+//   k_vescaped   HandleEscapedRays (integrator.cpp:495-537)
+//   k_viface     interface crossings (media.cpp:193-203)
+//   k_vsurface   the surface side: HandleEmissiveIntersection (:539-573) and
 //                EvaluateMaterialAndBSDF (surfscatter.cpp:57-328) for every material type
 //   k_vscatter   SampleMediumScattering<HGPhaseFunction> (media.cpp:259-352)
 //   k_vshadow    TraceTransmittance (intersect.h:164-274): shadow rays through interfaces with

@@ -565,6 +565,9 @@ static void BuildDevice(pbrt_context *c) {
     S.matTypeMask = 0;
     for (auto &m : s.materials) S.matTypeMask |= 1 << m.type;
     S.regularize = s.regularize ? 1 : 0;
+    S.smoothDielectrics = !s.regularize;
+    for (auto &m : s.materials)
+        if (m.type == kMatDielectricT && !(std::fmax(m.alphaX, m.alphaY) < 1e-3f)) S.smoothDielectrics = 0;
     S.nAreaLights = (int)s.areaLights.size();
     S.lightPrim = c->lightPrim.p;
     S.lightScale = c->lightScale.p;

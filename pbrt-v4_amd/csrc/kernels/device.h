@@ -124,6 +124,7 @@ struct DeviceScene {
                                // albedo constant, conductor alpha_x alpha_y, interface eta spectrum (-1)
     int matTypeMask;           // bit t: some material of type t exists
     int regularize;            // integrator "regularize" (surfscatter.cpp:127-128)
+    int smoothDielectrics;     // every dielectric is EffectivelySmooth and no regularize
     int dispersive;            // some dielectric has a spectral eta (matSpectra[2 * mat] >= 0)
     // piecewise-linear spectra (conductor eta / k): spectrum s spans [plOffsets[s], plOffsets[s+1])
     const int *plOffsets;

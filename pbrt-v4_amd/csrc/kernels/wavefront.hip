@@ -710,7 +710,9 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
 // ConductorSample/Eval).  f differs between the light sample and the BSDF sample, so beta stays
 // in bfLds and each 31-wavelength loop forms beta_i * f_i itself.  Specular BSDFs skip light
 // sampling (IsNonSpecular(flags), surfscatter.cpp:253).
-template <int MT>
+// Smooth (dielectric only, host-checked: every dielectric EffectivelySmooth, no regularize):
+// the light-sampling code of rough surfaces is compiled out.
+template <int MT, bool Smooth = false>
 __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(DeviceScene S, PathState st, int depth) {
     const QueueView mats = LoadQueue(st, depth, MatCounter(MT));
     if ((int)(blockIdx.x * blockDim.x) >= mats.total) return;  // no work
@@ -792,7 +794,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
             const bool reflective = MT == kMatConductorT || eta != 1;
             const bool transmissive = MT == kMatDielectricT;
             // ---- light sampling + shadow ray (surfscatter.cpp:252-326)
-            if (!smooth) {
+            if (!Smooth && !smooth) {
                 V3 cp = pi;
                 if (reflective && !transmissive) cp = OffsetRayOrigin(pi, pe, n, wo);
                 else if (transmissive && reflective) cp = OffsetRayOrigin(pi, pe, n, -wo);
@@ -1193,7 +1195,10 @@ hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int dep
 }
 hipError_t LaunchShadeMicrofacet(const DeviceScene &S, const PathState &st, int depth, int type, int maxCount,
                                  hipStream_t s) {
-    if (type == kMatDielectricT)
+    if (type == kMatDielectricT && S.smoothDielectrics)
+        hipLaunchKernelGGL((k_shade_microfacet<kMatDielectricT, true>), dim3(ShadeGridFor(maxCount)), dim3(kBlock),
+                           ShadeLdsBytes(S, depth, true), s, S, st, depth);
+    else if (type == kMatDielectricT)
         hipLaunchKernelGGL(k_shade_microfacet<kMatDielectricT>, dim3(ShadeGridFor(maxCount)), dim3(kBlock),
                            ShadeLdsBytes(S, depth, true), s, S, st, depth);
     else

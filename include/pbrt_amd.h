@@ -201,7 +201,9 @@ int pbrt_image_error(const float *image, const float *reference, int width, int 
                      double *error3);
 
 /* WavefrontAggregate boundary: rays_dev = [7][n] SoA (o.xyz, d.xyz, tMax) on the device;
- * prim_dev [n] receives the original triangle index or -1; hit_dev [4][n] b0 b1 b2 t. */
+ * prim_dev [n] receives the original triangle index or -1; hit_dev [4][n] b0 b1 b2 t.
+ * Asynchronous on the context stream (no host round trip): the results are valid after
+ * pbrt_synchronize, or for work the caller orders after the context stream. */
 int pbrt_intersect(pbrt_context *ctx, const float *rays_dev, int n, int any_hit, int32_t *prim_dev, float *hit_dev);
 
 /* host-side evaluation of product components (no GPU): used by golden-vector tests */

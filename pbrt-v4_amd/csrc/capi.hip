@@ -36,6 +36,8 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
                               hipStream_t s);
 hipError_t LaunchIntersectBatch(const DeviceScene &S, const float *rays, int n, int anyHit, int *outPrim,
                                 float *outHit, hipStream_t s);
+size_t SurfaceTraversalStaticLds();
+size_t VolTraversalStaticLds();
 }  // namespace pbrt_amd
 
 using namespace pbrt_amd;
@@ -551,6 +553,7 @@ static void BuildDevice(pbrt_context *c) {
     S.primMaterial = c->primMaterial.p;
     S.primLight = c->primLight.p;
     S.primFlip = c->primFlip.p;
+    S.primOrig = c->primOrig.p;
     S.triShade = (const float4 *)c->triShade.p;
     S.matCoeffs = (const float4 *)c->matCoeffs.p;
     S.matConstant = c->matConstant.p;
@@ -706,7 +709,19 @@ static void BuildDevice(pbrt_context *c) {
         S.compressed = fmt && strcmp(fmt, "compressed") == 0;
         // LDS scene cache: top BVH8 nodes first (BFS order), then leading leaf-order triangles
         const int stride = 16 * LdsNodeStride(S.compressed);
-        int nNodes = (int)c->bvh.nodes.size(), budget = kSceneLdsBudget;
+        // A traversal block's LDS = static (queue staging) + the group stack + the node /
+        // triangle cache; the cache gets what the other two leave of the per-block limit, and
+        // a tree whose stack alone does not fit is rejected here rather than failing at launch.
+        int maxLds = 0;
+        HIPCHECK(hipDeviceGetAttribute(&maxLds, hipDeviceAttributeMaxSharedMemoryPerBlock, c->device));
+        const size_t staticLds = std::max(SurfaceTraversalStaticLds(), VolTraversalStaticLds());
+        const size_t stackLds = (size_t)c->bvh.maxStack * 256 * sizeof(uint2);  // kBlock lanes
+        if (staticLds + stackLds > (size_t)maxLds)
+            throw Error("BVH needs a " + std::to_string(c->bvh.maxStack) + "-entry traversal stack (" +
+                        std::to_string(stackLds) + " B of LDS per block beside " + std::to_string(staticLds) +
+                        " B static; the device allows " + std::to_string(maxLds) + ")");
+        int nNodes = (int)c->bvh.nodes.size();
+        int budget = (int)std::min<size_t>(kSceneLdsBudget, (size_t)maxLds - staticLds - stackLds);
         S.ldsNodes = std::min(nNodes, budget / stride);
         budget -= S.ldsNodes * stride;
         // all or none, in three pre-rotated copies (one per ray permutation)
@@ -719,14 +734,25 @@ static void BuildDevice(pbrt_context *c) {
     HIPCHECK(hipMemset(c->film.p, 0, 4 * npix * sizeof(double)));
 }
 
+// floats: records 2 x (beta 31, ray 6, lambda0, rl, etaScale) = 80, hitB 2x4, shadowRay 6,
+// shadowL 3, L 3, filterW 1 = 101; ints: records 2 x (flags, pixel, prevIdx), hitPrim 2,
+// shadowPixel, matQ x 3 (per material type), escQ, emitQ, records 2 x sidx = 16
+constexpr int kPathFloats = 101, kPathInts = 16;
+// VolState: records 2 x (beta, r_u, r_l 93 + ray 6 + prev 12 + lambda0, etaScale 2) = 226,
+// hitB 4, shadow ray 6 + Ld/r_u/r_l 93 + lambda0 = 100 floats; records 2 x (flags, pixel,
+// depth, medium) = 8, hitPrim, 5 queues, shadow pixel + medium + flags = 17 ints
+constexpr int kVolFloats = 330, kVolInts = 17;
+static int64_t PathStateBytesPerPath(bool volumetric, bool dispersive) {
+    return 4 * (kPathFloats + kPathInts) + (volumetric ? 4 * (kVolFloats + kVolInts) : 0) + (dispersive ? 16 : 0);
+}
+
 static void AllocPaths(pbrt_context *c, int64_t N) {
     if (N <= c->maxPaths) return;
-    // floats: records 2 x (beta 31, ray 6, lambda0, rl, etaScale) = 80, hitB 2x4, shadowRay 6,
-    // shadowL 3, L 3, filterW 1 = 101; ints: records 2 x (flags, pixel, prevIdx), hitPrim 2,
-    // shadowPixel, matQ x 3 (per material type), escQ, emitQ, records 2 x sidx = 16
-    const int nf = 101, ni = 16;
+    const int nf = kPathFloats, ni = kPathInts;
     const int64_t capS = ((N + kShards - 1) / kShards + 256 + 63) / 64 * 64;
     const int64_t NR = capS * kShards;  // record stride
+    // kernels index [k][NR] arrays with 32-bit k * NR for k <= 11 (spectral ones use size_t)
+    if (NR > INT32_MAX / 12) throw Error("max_paths too large: " + std::to_string(N));
     // per pixel-sample arrays (L, filterW) use N; the rest NR (>= N)
     c->fState.Alloc((size_t)nf * NR);
     c->iState.Alloc((size_t)ni * NR + CounterIndex(c->desc.maxDepth + 3, 0, 0));
@@ -776,10 +802,7 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
     st.emitQ = takei(1);
     st.counters = ip;
     if (c->volumetric) {
-        // VolState: records 2 x (beta, r_u, r_l 93 + ray 6 + prev 12 + lambda0, etaScale 2) = 226,
-        // hitB 4, shadow ray 6 + Ld/r_u/r_l 93 + lambda0 = 100 floats; records 2 x (flags, pixel,
-        // depth, medium) = 8, hitPrim, 5 queues, shadow pixel + medium + flags = 17 ints
-        const int vf = 330, vi = 17;
+        const int vf = kVolFloats, vi = kVolInts;
         c->vfState.Alloc((size_t)vf * NR);
         c->viState.Alloc((size_t)vi * NR);
         float *g = c->vfState.p;
@@ -1132,6 +1155,14 @@ int pbrt_context_create(const pbrt_scene *scene, int device, int64_t maxPaths, p
             const SceneDesc &d = c->desc;
             const int64_t all = (int64_t)(d.px1 - d.px0) * (d.py1 - d.py0) * std::max(d.spp, 1);
             maxPaths = std::min<int64_t>(all, c->volumetric ? (1 << 24) : (1 << 26));
+            // ... and within 3/4 of the device memory still free (several contexts per GPU,
+            // smaller cards): path-state bytes per path from AllocPaths' layout
+            size_t freeB = 0, totalB = 0;
+            HIPCHECK(hipMemGetInfo(&freeB, &totalB));
+            const int64_t perPath = PathStateBytesPerPath(c->volumetric, c->S.dispersive);
+            const int64_t fit = (int64_t)(freeB / 4 * 3) / perPath - kShards * 320;
+            if (fit < 4096) throw Error("not enough free device memory for path state");
+            maxPaths = std::min<int64_t>(maxPaths, fit);
         }
         AllocPaths(c.get(), maxPaths);
         *out = c.release();
@@ -1314,14 +1345,11 @@ int pbrt_image_error(const float *image, const float *reference, int width, int 
 int pbrt_intersect(pbrt_context *ctx, const float *rays, int n, int anyHit, int32_t *prim, float *hit) {
     try {
         HIPCHECK(hipSetDevice(ctx->device));
+        if (!ctx || n < 0 || (n > 0 && (!rays || !prim || !hit))) return Fail("bad arguments");
+        if (n == 0) return 0;
+        if ((int64_t)n * 7 > INT32_MAX) return Fail("ray batch too large");
+        // asynchronous on the context stream; the kernel writes the scene's triangle numbering
         HIPCHECK(LaunchIntersectBatch(ctx->S, rays, n, anyHit, prim, hit, ctx->stream));
-        HIPCHECK(hipStreamSynchronize(ctx->stream));
-        // map leaf-order prim to the original triangle index on the host side of the copy
-        std::vector<int> p(n);
-        HIPCHECK(hipMemcpy(p.data(), prim, n * sizeof(int), hipMemcpyDeviceToHost));
-        for (int &v : p)
-            if (v >= 0) v = ctx->bvh.triPrim[v];
-        HIPCHECK(hipMemcpy(prim, p.data(), n * sizeof(int), hipMemcpyHostToDevice));
         return 0;
     } catch (const std::exception &e) {
         return Fail(e.what());

@@ -110,6 +110,7 @@ struct DeviceScene {
     const int *primMaterial;
     const int *primLight;
     const uint8_t *primFlip;
+    const int *primOrig;  // leaf order -> the scene's triangle index (boundary results)
     // per-triangle shading attributes (leaf order, 4 float4 each: n0|flags, n1|u0, n2|v0,
     // u1 v1 u2 v2), nullptr when no mesh has vertex normals or uv
     const float4 *triShade;

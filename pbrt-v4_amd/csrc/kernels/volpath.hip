@@ -2120,6 +2120,20 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_vshadow_grey(D
 
 // ------------------------------------------------------------------ launch helpers (host)
 size_t TraversalLdsBytes(int stackSize, int ldsNodes, int ldsTris, int compressed);
+size_t VolTraversalStaticLds() {
+    size_t m = 0;
+    auto take = [&](const void *f) {
+        hipFuncAttributes a{};
+        if (hipFuncGetAttributes(&a, f) == hipSuccess) m = std::max(m, (size_t)a.sharedSizeBytes);
+    };
+#define TAKE_TM(tm)                                                      \
+    take(reinterpret_cast<const void *>(&k_vclosest<tm>));               \
+    take(reinterpret_cast<const void *>(&k_vshadow_grey<tm>));           \
+    take(reinterpret_cast<const void *>(&k_vshadow<tm>));
+    TAKE_TM(kTravLds) TAKE_TM(kTravWide) TAKE_TM(kTravQuant)
+#undef TAKE_TM
+    return m;
+}
 static size_t VolStackBytes(const DeviceScene &S) {
     return TraversalLdsBytes(S.stackSize, S.ldsNodes, S.ldsTris, S.compressed);
 }

@@ -159,7 +159,7 @@ __global__ void __launch_bounds__(kBlock) k_escaped(DeviceScene S, PathState st,
                 const int off = DenseOffset(lam);
                 const float4 t = off < 0 ? make_float4(0.f, 0.f, 0.f, scale * 0.f) : tab[off];
                 nz |= t.w != 0;
-                const float v = ((depth > 0 ? rec.beta[i * NR + ri] : 1.f) * t.w * invDenom) * kInvWavelengthPDF;
+                const float v = ((depth > 0 ? rec.beta[(size_t)i * NR + ri] : 1.f) * t.w * invDenom) * kInvWavelengthPDF;
                 sx = i == 0 ? t.x * v : sx + t.x * v;
                 sy = i == 0 ? t.y * v : sy + t.y * v;
                 sz = i == 0 ? t.z * v : sz + t.z * v;
@@ -196,7 +196,7 @@ __global__ void __launch_bounds__(kBlock) k_escaped(DeviceScene S, PathState st,
                 int off = DenseOffset(lam);
                 float Le = scale * (off < 0 ? 0.f : dense[off]);
                 nz |= Le != 0;
-                float v = ((depth > 0 ? rec.beta[i * NR + ri] : 1.f) * Le * invDenom) * kInvWavelengthPDF;
+                float v = ((depth > 0 ? rec.beta[(size_t)i * NR + ri] : 1.f) * Le * invDenom) * kInvWavelengthPDF;
                 float xb = off < 0 ? 0.f : S.sensor[off], yb = off < 0 ? 0.f : S.sensor[kDenseN + off],
                       zb = off < 0 ? 0.f : S.sensor[2 * kDenseN + off];
                 sx = i == 0 ? xb * v : sx + xb * v;
@@ -1040,7 +1040,7 @@ __global__ void __launch_bounds__(kBlock, 4) k_intersect_batch(DeviceScene S, co
         float tMax = rays[6 * n + i];
         TriHit h{0, 0, 0, 0};
         int prim = anyHit ? Traverse<true, TM>(S, L, o, d, tMax, &h) : Traverse<false, TM>(S, L, o, d, tMax, &h);
-        outPrim[i] = prim;
+        outPrim[i] = prim >= 0 ? S.primOrig[prim] : -1;  // the caller's triangle numbering
         outHit[i] = h.b0;
         outHit[n + i] = h.b1;
         outHit[2 * n + i] = h.b2;
@@ -1124,6 +1124,23 @@ size_t TraversalLdsBytes(int stackSize, int ldsNodes, int ldsTris, int compresse
     // group stack (uint2 entries), cached nodes, cached triangles in three pre-rotated copies
     return (size_t)stackSize * kBlock * sizeof(uint2) + (size_t)ldsNodes * LdsNodeStride(compressed) * 16 +
            (size_t)ldsTris * 3 * 48;
+}
+// Largest static LDS of the traversal kernels (k_closest's queue staging), for BuildDevice's
+// check that the group stack + node cache + static LDS fit one block's LDS
+size_t SurfaceTraversalStaticLds() {
+    size_t m = 0;
+    auto take = [&](const void *f) {
+        hipFuncAttributes a{};
+        if (hipFuncGetAttributes(&a, f) == hipSuccess) m = std::max(m, (size_t)a.sharedSizeBytes);
+    };
+#define TAKE_TM(tm)                                                             \
+    take(reinterpret_cast<const void *>(&k_closest<kNumMatTypes, tm>));         \
+    take(reinterpret_cast<const void *>(&k_closest<1, tm>));                    \
+    take(reinterpret_cast<const void *>(&k_shadow<tm>));                        \
+    take(reinterpret_cast<const void *>(&k_intersect_batch<tm>));
+    TAKE_TM(kTravLds) TAKE_TM(kTravWide) TAKE_TM(kTravQuant)
+#undef TAKE_TM
+    return m;
 }
 static size_t StackBytes(const DeviceScene &S) {
     return TraversalLdsBytes(S.stackSize, S.ldsNodes, S.ldsTris, S.compressed);

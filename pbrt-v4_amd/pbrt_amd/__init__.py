@@ -411,6 +411,7 @@ class HIPAggregate:
         torch.cuda.synchronize(rays.device)
         _check(_lib().pbrt_intersect(self.integrator._h, ctypes.c_void_p(rays.data_ptr()), n, int(any_hit),
                                      ctypes.c_void_p(prim.data_ptr()), ctypes.c_void_p(hit.data_ptr())))
+        self.integrator.synchronize()  # results are written on the context's stream
         return prim, hit
 
     def IntersectClosest(self, rays):

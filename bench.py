@@ -12,11 +12,11 @@ first) plus, for N > 1, the single RCCL sum-reduce of the film over xGMI (issued
 asynchronously from a staging copy, so it overlaps the next step's render; the timed region
 ends after every reduce has completed).  Pixel rows are
 interleaved across ranks (row r to rank r mod N: pixel tiles, BVH replicated, no collective on
-the data path).  Default for N > 1 is weak scaling: each GPU keeps the single-GPU workload, i.e. the job
-is the same 1280x720 image at 64 x N spp whose row stripes are dealt over the N GPUs (each
-renders 1/N of the rows at all 64 x N samples = 1280x720x64 samples' worth of paths);
-``--scaling strong`` splits one 1280x720x64 image N ways instead.  The metric counts every
-sample of the job.  Launch: ``python bench.py`` (1 GPU) or
+the data path).  Default for N > 1 is strong scaling: the job is BASELINE's 1280x720x64 image
+split N ways (per-GPU work 1/N, "scaling": "strong").  ``--scaling weak`` keeps each GPU's
+work fixed instead: the job becomes the 1280x720 image at 64 x N spp (each GPU renders 1/N of
+the rows at all 64 x N samples); the metric string then names that job.  The metric counts
+every sample of the job.  Launch: ``python bench.py`` (1 GPU) or
 ``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``.
 
 The JSON line also carries
@@ -36,10 +36,14 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "pbrt-v4_amd"))
 
-# Algorithmic bytes per ray of the closest-hit kernel, from its declared SoA fields (the
-# depth's path records are dense, so there is no ray-queue index to read):
-#   reads  ray o,d 24 B
-#   writes hit prim 4 B + b0,b1,b2,t 16 B + material-queue entry 4 B = 24 B
+# Algorithmic bytes of the closest-hit kernel, from its declared SoA fields (the depth's path
+# records are dense, so there is no ray-queue index to read), per depth d:
+#   reads  ray o,d 24 B per ray
+#   writes hit prim 4 B + b0,b1,b2,t 16 B per recorded hit (every hit below maxDepth, only
+#          emissive hits at maxDepth), and 4 B per queue entry (material, emissive, escaped)
+# closest_bytes() sums this over the per-depth queue counts; BYTES_PER_RAY_CLOSEST is the
+# all-rays-hit upper bound used when no counts are available.
+RAY_READ_B, HIT_WRITE_B, QUEUE_ENTRY_B = 24, 20, 4
 BYTES_PER_RAY_CLOSEST = 48
 # The media wavefront's closest-hit kernel (volpath.hip k_vclosest) also reads the ray's medium
 # (4 B) and always writes the hit (prim 4 + b0,b1,b2,t 16) and one queue entry (4): 52 B
@@ -47,7 +51,7 @@ BYTES_PER_RAY_VCLOSEST = 52
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2")
@@ -61,10 +65,10 @@ def parse():
                          "one pass up to 64 Mi paths)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
-                    help="N > 1: weak = every GPU renders the single-GPU workload (job spp x N); "
-                         "strong = one image split N ways")
-    a = ap.parse_args()
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
+                    help="N > 1: strong = one image split N ways (default); weak = every GPU renders "
+                         "the single-GPU workload (job spp x N)")
+    a = ap.parse_args(argv)
     d = {"c2": (1280, 720, 64), "c3": (1920, 1080, 256), "c4": (1920, 1080, 128), "c5": (1280, 720, 1024)}[a.workload]
     a.xres = a.xres or d[0]
     a.yres = a.yres or d[1]
@@ -97,6 +101,58 @@ def load(args, spp=None):
         return pa.Scene.from_string(gen_c3.scene_text(args.xres, args.yres, spp), ROOT / "scenes")
     return pa.load_scene(ROOT / "scenes" / "cornell-box.pbrt", xresolution=args.xres, yresolution=args.yres,
                          spp=spp)
+
+
+def closest_bytes(qcounts, max_depth):
+    """(algorithmic bytes, rays) of the closest-hit launches of one pass from its per-depth queue
+    counts (WavefrontPathIntegrator.queue_counts: rays, diffuse, shadow, escaped, emissive,
+    dielectric, conductor)."""
+    total = rays = 0
+    for d in range(max_depth + 1):
+        r, dif, _sh, esc, emi, die, con = (int(x) for x in qcounts[d])
+        mat = dif + die + con
+        hits = mat if d < max_depth else emi
+        total += RAY_READ_B * r + HIT_WRITE_B * hits + QUEUE_ENTRY_B * (mat + emi + esc)
+        rays += r
+    return total, rays
+
+
+def job_spec(args, world, scaling):
+    """The job one bench step renders: image, spp of the whole job, and how it is sharded."""
+    from pbrt_amd.tiles import job_spp
+    spp = job_spp(args.spp, world, scaling)
+    metric = f"Msamples/sec (paths x spp / s) at {args.xres}x{args.yres}x{spp}spp"
+    if world == 1:
+        sharding = "single GPU"
+    elif scaling == "strong":
+        sharding = (f"one {args.xres}x{args.yres}x{spp}spp image, film rows interleaved over {world} ranks "
+                    "(strong scaling: per-GPU work 1/N) + 1 RCCL film reduce")
+    else:
+        sharding = (f"one {args.xres}x{args.yres}x{spp}spp image ({args.spp} spp x {world}), film rows "
+                    f"interleaved over {world} ranks (weak scaling: each GPU renders "
+                    f"{args.xres}x{args.yres}x{args.spp} samples' worth) + 1 RCCL film reduce")
+    return {"metric": metric, "spp": spp, "sharding": sharding, "scaling": scaling if world > 1 else "weak"}
+
+
+def roofline_entry(achieved, mean_launch_s, launches, rays_per_launch, bytes_per_ray, traffic, workload):
+    """The 'roofline' object.  bound = the roofline that applies (HBM: nothing on this path
+    is a dense contraction, so MFMA has no ceiling to offer); 'limiter' says whether the
+    measured fraction is bandwidth-limited or what else limits the kernel."""
+    frac = achieved / HBM_PEAK_GBS
+    if frac >= 0.6:
+        limiter = "HBM bandwidth"
+    elif workload == "c2":
+        limiter = (f"not HBM ({frac:.1%} of peak): VALU issue + LDS latency, BVH and triangles LDS-resident "
+                   "(profiles/r*_c2_pmc_per_kernel.json)")
+    else:
+        limiter = f"not HBM ({frac:.1%} of peak): dependent node/triangle load latency"
+    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(frac, 5), "traffic": traffic,
+            "kernel": ("k_vclosest (BVH8 traverse + hit record + push to medium / surface queue)"
+                       if workload == "c5" else
+                       "k_closest (BVH8 traverse + hit record + wave64 ballot push to material queue)"),
+            "bytes_per_ray": round(bytes_per_ray, 2), "rays_per_launch": round(rays_per_launch, 1),
+            "timed_launches": launches, "mean_launch_us": round(mean_launch_s * 1e6, 3), "limiter": limiter}
 
 
 def cpu_baseline(args, threads, sc):
@@ -135,10 +191,15 @@ def latest_profile(pattern):
         return None
 
 
-def pmc_traffic():
-    """HBM bytes per closest-hit launch from the newest committed rocprofv3 PMC pass, if any."""
-    rec = latest_profile("r*_closest_pmc.json")
-    return rec.get("hbm_bytes_per_launch") if rec else None
+def pmc_traffic(workload):
+    """HBM bytes per closest-hit launch from the newest committed rocprofv3 PMC pass of this
+    workload, tagged with the commit it was measured on (a figure, not a live measurement)."""
+    pat = "r*_closest_pmc.json" if workload == "c2" else f"r*_{workload}_closest_pmc.json"
+    rec = latest_profile(pat)
+    if not rec or rec.get("hbm_bytes_per_launch") is None:
+        return None
+    return {"hbm_bytes_per_launch": rec["hbm_bytes_per_launch"], "bytes_per_ray": rec.get("hbm_bytes_per_ray"),
+            "measured_on": rec.get("head", "unknown"), "source": "profiles/" + sorted((ROOT / "profiles").glob(pat))[-1].name}
 
 
 # Wide BVH8 node bytes a visit reads (12 plane float4 + header + slot triangle masks) and the
@@ -171,10 +232,11 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
     import pbrt_amd as pa
-    from pbrt_amd.tiles import film_tensor_from_device_ptr, job_spp, rows_for_rank
+    from pbrt_amd.tiles import film_tensor_from_device_ptr, rows_for_rank
 
     scaling = args.scaling if world > 1 else "weak"
-    scene = load(args, job_spp(args.spp, world, scaling))
+    job = job_spec(args, world, scaling)
+    scene = load(args, job["spp"])
     info = scene.info
     integ = pa.WavefrontPathIntegrator(scene, device=local_rank, max_paths=args.max_paths)
     # single-row interleave: every rank gets the same number of rows whenever N divides the
@@ -236,10 +298,15 @@ def main():
     value = samples / dt_max / 1e6
     launches = max(st.closest_launches, 1)
     mean_launch_s = st.closest_ms / 1e3 / launches
-    bpr = BYTES_PER_RAY_VCLOSEST if args.workload == "c5" else BYTES_PER_RAY_CLOSEST
+    if args.workload == "c5":
+        bpr = BYTES_PER_RAY_VCLOSEST
+    else:
+        # per-depth queue counts of the last pass (= the timed pass when a render is one pass)
+        qb, qr = closest_bytes(integ.queue_counts(), info.max_depth)
+        bpr = qb / qr if qr else BYTES_PER_RAY_CLOSEST
     bytes_per_launch = bpr * st.timed_closest_rays / launches
     achieved = bytes_per_launch / mean_launch_s / 1e9 if mean_launch_s > 0 else 0.0
-    traffic = pmc_traffic() if args.workload == "c2" else None  # the committed PMC pass is of C2
+    traffic = pmc_traffic(args.workload)
 
     if rank == 0:
         cpu = None
@@ -249,7 +316,7 @@ def main():
             except Exception as e:  # the baseline is reported, never required
                 cpu = {"value": None, "error": str(e)}
         line = {
-            "metric": f"Msamples/sec (paths x spp / s) at {args.xres}x{args.yres}x{args.spp}spp",
+            "metric": job["metric"],
             "value": round(value, 3),
             "unit": "Msamples/s",
             "n_gpus": world,
@@ -257,7 +324,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(dt_max / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": scaling,
+            "scaling": job["scaling"],
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
@@ -276,26 +343,11 @@ def main():
                                     "untextured (BASELINE configs[3] geometry)"),
                        "xres": args.xres, "yres": args.yres, "spp": info.spp, "max_depth": info.max_depth,
                        "triangles": info.n_triangles, "paths_per_pass": int(st.paths_per_pass),
-                       "sharding": (f"rows interleaved over ranks, job {info.spp} spp "
-                                    f"({'spp x N: weak' if scaling == 'weak' else 'strong'} scaling) "
-                                    "+ 1 RCCL film reduce") if world > 1 else "single GPU"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "kernel": ("k_vclosest (BVH8 traverse + hit record + push to medium / surface queue)"
-                                    if args.workload == "c5" else
-                                    "k_closest (BVH8 traverse + hit record + wave64 ballot push to material queue)"),
-                         "bytes_per_ray": bpr,
-                         "rays_per_launch": round(st.timed_closest_rays / launches, 1),
-                         "timed_launches": launches,
-                         "mean_launch_us": round(mean_launch_s * 1e6, 3),
-                         # what actually bounds the kernel: its algorithmic HBM stream is a small
-                         # fraction of the peak; the PMC SQ counters show VALU issue and LDS /
-                         # dependent-load latency (profiles/r*_c2_pmc_per_kernel.json)
-                         "limiter": ("VALU issue + LDS latency (BVH and triangles LDS-resident), not HBM"
-                                     if args.workload == "c2" else
-                                     "dependent node/triangle loads (latency), not HBM bandwidth"),
-                         "effective": (effective_traversal(bytes_per_launch / bpr / mean_launch_s)
-                                       if args.workload == "c2" and mean_launch_s > 0 else None)},
+                       "sharding": job["sharding"]},
+            "roofline": dict(roofline_entry(achieved, mean_launch_s, launches, st.timed_closest_rays / launches,
+                                            bpr, traffic, args.workload),
+                             effective=(effective_traversal(bytes_per_launch / bpr / mean_launch_s)
+                                        if args.workload == "c2" and mean_launch_s > 0 else None)),
             "cpu_baseline": cpu,
             "rays": {"camera": int(st.camera_rays), "closest": int(st.closest_rays), "shadow": int(st.shadow_rays)},
         }

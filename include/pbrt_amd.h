@@ -159,6 +159,15 @@ typedef struct pbrt_render_stats {
     uint64_t paths_per_pass;
 } pbrt_render_stats;
 
+/* Per-stage kernel profile (GetProfilerEvents / ReportKernelStats, gpu/util.cpp:128-246): with
+ * profiling on, every stage launch of pbrt_render is bracketed by HIP events on the stream it
+ * runs on; pbrt_synchronize folds them into one record per stage. */
+typedef struct pbrt_kernel_stat {
+    char description[96];
+    int launches;
+    double total_ms, min_ms, max_ms;
+} pbrt_kernel_stat;
+
 const char *pbrt_last_error(void);
 int pbrt_set_data_dir(const char *dir);
 
@@ -177,7 +186,11 @@ void pbrt_context_free(pbrt_context *ctx);
 int pbrt_render(pbrt_context *ctx, const pbrt_render_params *params);
 int pbrt_synchronize(pbrt_context *ctx);
 int pbrt_get_stats(pbrt_context *ctx, pbrt_render_stats *stats);
-int pbrt_reset_stats(pbrt_context *ctx);
+int pbrt_reset_stats(pbrt_context *ctx); /* also clears the kernel profile */
+int pbrt_set_kernel_profiling(pbrt_context *ctx, int enable);
+/* the profile as of the last pbrt_synchronize: min(*n_stats, max_stats) records in first-launch
+ * order; *n_stats = number of stages profiled */
+int pbrt_get_kernel_stats(pbrt_context *ctx, pbrt_kernel_stat *out, int max_stats, int *n_stats);
 
 int pbrt_film_clear(pbrt_context *ctx);
 int pbrt_film_device_ptr(pbrt_context *ctx, double **film, size_t *n_doubles);
@@ -258,6 +271,10 @@ int pbrt_debug_bxdf(int type, const float *params3, const float *eta31, const fl
  * the directions as the reference's) */
 int pbrt_debug_layered(const float *params12, const float *a31, const float *b31, const float *alb31,
                        const float *wo3, const float *wi3, const float *u3, float *out72);
+/* host-side BVH8 build of the scene (what pbrt_context_create uploads): out8 = nodes, leaf-order
+ * triangles, tree depth, worst-case traversal stack entries, wide node bytes, quantised node
+ * bytes, 0, 0 */
+int pbrt_debug_bvh_stats(const pbrt_scene *scene, int64_t *out8);
 /* queue counters of the last pass: [depth][8] = rays, material hits, shadow rays, escaped,
  * emissive hits (diagnostics) */
 int pbrt_debug_queue_counts(pbrt_context *ctx, int32_t *counts, int n);

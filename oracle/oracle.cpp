@@ -2780,15 +2780,22 @@ int oracle_intersect_batch(const pbrt_scene_flat *flat, const pbrt_scene_info *i
                            int anyHit, int32_t *prim, float *hit) {
     Scene S;
     S.Init(flat, info);
-    for (int i = 0; i < n; ++i) {
-        Vec o(rays[i], rays[n + i], rays[2 * n + i]), d(rays[3 * n + i], rays[4 * n + i], rays[5 * n + i]);
-        TriIsect ti{0, 0, 0, 0};
-        prim[i] = S.Intersect(o, d, rays[6 * n + i], &ti, anyHit != 0);
-        hit[i] = ti.b0;
-        hit[n + i] = ti.b1;
-        hit[2 * n + i] = ti.b2;
-        hit[3 * n + i] = ti.t;
-    }
+    // independent rays: split over host threads (large scenes, 10^5+ rays in the tests)
+    const int nt = std::max(1, std::min<int>(16, (int)std::thread::hardware_concurrency()));
+    std::vector<std::thread> pool;
+    for (int w = 0; w < nt; ++w)
+        pool.emplace_back([&, w] {
+            for (int i = w; i < n; i += nt) {
+                Vec o(rays[i], rays[n + i], rays[2 * n + i]), d(rays[3 * n + i], rays[4 * n + i], rays[5 * n + i]);
+                TriIsect ti{0, 0, 0, 0};
+                prim[i] = S.Intersect(o, d, rays[6 * n + i], &ti, anyHit != 0);
+                hit[i] = ti.b0;
+                hit[n + i] = ti.b1;
+                hit[2 * n + i] = ti.b2;
+                hit[3 * n + i] = ti.t;
+            }
+        });
+    for (auto &t : pool) t.join();
     return 0;
 }
 

@@ -242,6 +242,21 @@ struct pbrt_context {
     // timing
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
     int eventsUsed = 0;
+    // per-stage kernel profile (pbrt_set_kernel_profiling; ReportKernelStats, gpu/util.cpp:128-246):
+    // an event pair around every stage launch, folded into stageStats at pbrt_synchronize
+    bool profiling = false;
+    struct StageStat {
+        std::string name;
+        int launches = 0;
+        double sum = 0, mn = 0, mx = 0;
+    };
+    std::vector<StageStat> stageStats;
+    struct StageEvents {
+        hipEvent_t a, b;
+        int stat;
+    };
+    std::vector<StageEvents> stageEvents;
+    int stageEventsUsed = 0;
     pbrt_render_stats stats{};
     std::vector<int> hostCounters;
     std::vector<int> lastRows;
@@ -250,6 +265,10 @@ struct pbrt_context {
         for (auto &e : events) {
             (void)hipEventDestroy(e.first);
             (void)hipEventDestroy(e.second);
+        }
+        for (auto &e : stageEvents) {
+            (void)hipEventDestroy(e.a);
+            (void)hipEventDestroy(e.b);
         }
         for (hipEvent_t e : eClosest) (void)hipEventDestroy(e);
         for (hipEvent_t e : eEmit) (void)hipEventDestroy(e);
@@ -720,8 +739,12 @@ static void BuildDevice(pbrt_context *c) {
             throw Error("BVH needs a " + std::to_string(c->bvh.maxStack) + "-entry traversal stack (" +
                         std::to_string(stackLds) + " B of LDS per block beside " + std::to_string(staticLds) +
                         " B static; the device allows " + std::to_string(maxLds) + ")");
+        // occupancy: kTraversalBlocksPerCU blocks per CU when static + stack leave room (C4: 10 KB
+        // + 18 KB of a 40 KB share -> a 12 KB cache); the cache never pushes a block past its share
+        const size_t share = std::min<size_t>((size_t)maxLds, kLdsPerCU / kTraversalBlocksPerCU - 512);
+        const size_t left = share > staticLds + stackLds ? share - staticLds - stackLds : 0;
         int nNodes = (int)c->bvh.nodes.size();
-        int budget = (int)std::min<size_t>(kSceneLdsBudget, (size_t)maxLds - staticLds - stackLds);
+        int budget = (int)std::min<size_t>(kSceneLdsBudget, left);
         S.ldsNodes = std::min(nNodes, budget / stride);
         budget -= S.ldsNodes * stride;
         // all or none, in three pre-rotated copies (one per ray permutation)
@@ -872,6 +895,49 @@ static void RecordEvent(pbrt_context *c, bool start) {
     }
 }
 
+// Brackets one stage launch with events on the stream it runs on (profiling on); the pair is
+// read back at pbrt_synchronize
+struct StageTimer {
+    pbrt_context *c;
+    hipStream_t s;
+    int slot = -1;
+    StageTimer(pbrt_context *ctx, const char *name, hipStream_t stream) : c(ctx), s(stream) {
+        if (!c->profiling) return;
+        int stat = -1;
+        for (size_t i = 0; i < c->stageStats.size(); ++i)
+            if (c->stageStats[i].name == name) stat = (int)i;
+        if (stat < 0) {
+            c->stageStats.push_back({name});
+            stat = (int)c->stageStats.size() - 1;
+        }
+        if (c->stageEventsUsed == (int)c->stageEvents.size()) {
+            pbrt_context::StageEvents e{};
+            HIPCHECK(hipEventCreate(&e.a));
+            HIPCHECK(hipEventCreate(&e.b));
+            c->stageEvents.push_back(e);
+        }
+        slot = c->stageEventsUsed++;
+        c->stageEvents[slot].stat = stat;
+        HIPCHECK(hipEventRecord(c->stageEvents[slot].a, s));
+    }
+    ~StageTimer() noexcept(false) {
+        if (slot >= 0) HIPCHECK(hipEventRecord(c->stageEvents[slot].b, s));
+    }
+};
+
+static void CollectStageEvents(pbrt_context *c) {
+    for (int i = 0; i < c->stageEventsUsed; ++i) {
+        float ms = 0;
+        HIPCHECK(hipEventElapsedTime(&ms, c->stageEvents[i].a, c->stageEvents[i].b));
+        auto &st = c->stageStats[c->stageEvents[i].stat];
+        st.mn = st.launches ? std::min(st.mn, (double)ms) : ms;
+        st.mx = st.launches ? std::max(st.mx, (double)ms) : ms;
+        st.sum += ms;
+        ++st.launches;
+    }
+    c->stageEventsUsed = 0;
+}
+
 static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
     HIPCHECK(hipSetDevice(c->device));
     const SceneDesc &s = c->desc;
@@ -911,20 +977,33 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
             HIPCHECK(hipMemsetAsync(st.counters, 0, countersBytes, c->stream));
             if (c->volumetric) {
                 // participating media: the volumetric wavefront (volpath.hip), same film update
-                HIPCHECK(LaunchVolCamera(c->S, st, c->vs, (int)nActive, c->stream));
+                {
+                    StageTimer t(c, "Generate camera rays (k_vcamera)", c->stream);
+                    HIPCHECK(LaunchVolCamera(c->S, st, c->vs, (int)nActive, c->stream));
+                }
                 for (int wf = 0; wf <= s.maxDepth; ++wf) {
                     const bool timed = p->time_closest && r0 == 0 && s0 == 0;
                     if (timed) RecordEvent(c, true);
-                    HIPCHECK(LaunchVolClosest(c->S, st, c->vs, wf, (int)nActive, timed ? 1 : 0, c->stream));
+                    {
+                        StageTimer t(c, "Tracing closest hit rays (k_vclosest)", c->stream);
+                        HIPCHECK(LaunchVolClosest(c->S, st, c->vs, wf, (int)nActive, timed ? 1 : 0, c->stream));
+                    }
                     if (timed) RecordEvent(c, false);
+                    StageTimer t(c, "Media, surfaces, scattering and shadow rays (volpath iteration)", c->stream);
                     HIPCHECK(LaunchVolIteration(c->S, st, c->vs, wf, (int)nActive, c->stream));
                 }
-                HIPCHECK(LaunchFilm(c->S, st, nS, c->stream));
+                {
+                    StageTimer t(c, "Update film (k_film)", c->stream);
+                    HIPCHECK(LaunchFilm(c->S, st, nS, c->stream));
+                }
                 c->stats.passes++;
                 c->stats.paths_per_pass = std::max<uint64_t>(c->stats.paths_per_pass, nActive);
                 continue;
             }
-            HIPCHECK(LaunchCamera(c->S, st, (int)nActive, c->stream));
+            {
+                StageTimer t(c, "Generate camera rays (k_camera)", c->stream);
+                HIPCHECK(LaunchCamera(c->S, st, (int)nActive, c->stream));
+            }
             // k_shade_diffuse<Lean>: Halton indices of this pass all below 2^24 (index <
             // (sample + 1) * stride, samplers.h:53-71), lights, light BVH and dense spectra in
             // LDS, no shading normals or uv, no point / spot / distant lights
@@ -939,21 +1018,36 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
                 // passes are statistically identical and each event pair costs a queue gap
                 const bool timed = p->time_closest && r0 == 0 && s0 == 0;
                 if (timed) RecordEvent(c, true);
-                HIPCHECK(LaunchClosest(c->S, st, depth, (int)nActive, timed ? 1 : 0, c->stream));
+                {
+                    StageTimer t(c, "Tracing closest hit rays (k_closest)", c->stream);
+                    HIPCHECK(LaunchClosest(c->S, st, depth, (int)nActive, timed ? 1 : 0, c->stream));
+                }
                 if (timed) RecordEvent(c, false);
                 // emission (escaped rays, emissive hits) on the side stream, beside the material
                 // stage; the shadow stage and the next depth's closest hits wait for it
                 static const bool emitSerial = getenv("PBRT_AMD_EMIT_SERIAL") != nullptr;
                 const bool emit = (s.infiniteLights.size() || s.areaLights.size()) && !emitSerial;
                 if (emitSerial) {
-                    if (s.infiniteLights.size()) HIPCHECK(LaunchEscaped(c->S, st, depth, (int)nActive, c->stream));
-                    if (s.areaLights.size()) HIPCHECK(LaunchEmissive(c->S, st, depth, (int)nActive, c->stream));
+                    if (s.infiniteLights.size()) {
+                        StageTimer t(c, "Handle escaped rays (k_escaped)", c->stream);
+                        HIPCHECK(LaunchEscaped(c->S, st, depth, (int)nActive, c->stream));
+                    }
+                    if (s.areaLights.size()) {
+                        StageTimer t(c, "Handle emitters hit by indirect rays (k_emissive)", c->stream);
+                        HIPCHECK(LaunchEmissive(c->S, st, depth, (int)nActive, c->stream));
+                    }
                 }
                 if (emit) {
                     HIPCHECK(hipEventRecord(c->eClosest[depth], c->stream));
                     HIPCHECK(hipStreamWaitEvent(c->sideStream, c->eClosest[depth], 0));
-                    if (s.infiniteLights.size()) HIPCHECK(LaunchEscaped(c->S, st, depth, (int)nActive, c->sideStream));
-                    if (s.areaLights.size()) HIPCHECK(LaunchEmissive(c->S, st, depth, (int)nActive, c->sideStream));
+                    if (s.infiniteLights.size()) {
+                        StageTimer t(c, "Handle escaped rays (k_escaped)", c->sideStream);
+                        HIPCHECK(LaunchEscaped(c->S, st, depth, (int)nActive, c->sideStream));
+                    }
+                    if (s.areaLights.size()) {
+                        StageTimer t(c, "Handle emitters hit by indirect rays (k_emissive)", c->sideStream);
+                        HIPCHECK(LaunchEmissive(c->S, st, depth, (int)nActive, c->sideStream));
+                    }
                     HIPCHECK(hipEventRecord(c->eEmit[depth], c->sideStream));
                 }
                 if (depth == s.maxDepth) {
@@ -961,15 +1055,27 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
                     break;
                 }
                 // EvaluateMaterialsAndBSDFs: one launch per material type present (surfscatter.cpp:39-55)
-                if (c->S.matTypeMask & (1 << kMatDiffuseT))
+                if (c->S.matTypeMask & (1 << kMatDiffuseT)) {
+                    StageTimer t(c, "Evaluate materials/BSDFs for DiffuseMaterial (k_shade_diffuse)", c->stream);
                     HIPCHECK(LaunchShadeDiffuse(c->S, st, depth, (int)nActive, lean, c->stream));
+                }
                 for (int t = kMatDielectricT; t < kNumMatTypes; ++t)
-                    if (c->S.matTypeMask & (1 << t))
+                    if (c->S.matTypeMask & (1 << t)) {
+                        StageTimer tm(c, t == kMatDielectricT ? "Evaluate materials/BSDFs for DielectricMaterial (k_shade_microfacet)"
+                                                             : "Evaluate materials/BSDFs for ConductorMaterial (k_shade_microfacet)",
+                                      c->stream);
                         HIPCHECK(LaunchShadeMicrofacet(c->S, st, depth, t, (int)nActive, c->stream));
+                    }
                 if (emit) HIPCHECK(hipStreamWaitEvent(c->stream, c->eEmit[depth], 0));
-                HIPCHECK(LaunchShadow(c->S, st, depth, (int)nActive, c->stream));
+                {
+                    StageTimer t(c, "Tracing shadow rays (k_shadow)", c->stream);
+                    HIPCHECK(LaunchShadow(c->S, st, depth, (int)nActive, c->stream));
+                }
             }
-            HIPCHECK(LaunchFilm(c->S, st, nS, c->stream));
+            {
+                StageTimer t(c, "Update film (k_film)", c->stream);
+                HIPCHECK(LaunchFilm(c->S, st, nS, c->stream));
+            }
             c->stats.passes++;
             c->stats.paths_per_pass = std::max<uint64_t>(c->stats.paths_per_pass, nActive);
         }
@@ -1195,6 +1301,7 @@ int pbrt_synchronize(pbrt_context *ctx) {
             ctx->stats.closest_launches++;
         }
         ctx->eventsUsed = 0;
+        CollectStageEvents(ctx);
         unsigned long long ds[8];
         HIPCHECK(hipMemcpy(ds, ctx->devStats.p, sizeof ds, hipMemcpyDeviceToHost));
         ctx->stats.camera_rays = ds[0];
@@ -1205,6 +1312,37 @@ int pbrt_synchronize(pbrt_context *ctx) {
     } catch (const std::exception &e) {
         return Fail(e.what());
     }
+}
+
+int pbrt_set_kernel_profiling(pbrt_context *ctx, int enable) {
+    try {
+        if (!ctx) return Fail("null argument");
+        HIPCHECK(hipSetDevice(ctx->device));
+        HIPCHECK(hipStreamSynchronize(ctx->stream));
+        HIPCHECK(hipStreamSynchronize(ctx->sideStream));
+        CollectStageEvents(ctx);
+        ctx->profiling = enable != 0;
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_get_kernel_stats(pbrt_context *ctx, pbrt_kernel_stat *out, int max_stats, int *n_stats) {
+    if (!ctx || !n_stats || (max_stats > 0 && !out)) return Fail("null argument");
+    const int n = (int)ctx->stageStats.size();
+    *n_stats = n;
+    for (int i = 0; i < std::min(n, max_stats); ++i) {
+        const auto &st = ctx->stageStats[i];
+        pbrt_kernel_stat &o = out[i];
+        memset(&o, 0, sizeof o);
+        strncpy(o.description, st.name.c_str(), sizeof o.description - 1);
+        o.launches = st.launches;
+        o.total_ms = st.sum;
+        o.min_ms = st.mn;
+        o.max_ms = st.mx;
+    }
+    return 0;
 }
 
 int pbrt_get_stats(pbrt_context *ctx, pbrt_render_stats *stats) {
@@ -1219,6 +1357,8 @@ int pbrt_reset_stats(pbrt_context *ctx) {
         HIPCHECK(hipMemset(ctx->devStats.p, 0, kStatsSlots * sizeof(unsigned long long)));
         ctx->stats = pbrt_render_stats{};
         ctx->eventsUsed = 0;
+        ctx->stageEventsUsed = 0;
+        ctx->stageStats.clear();
         return 0;
     } catch (const std::exception &e) {
         return Fail(e.what());
@@ -1629,6 +1769,20 @@ int pbrt_debug_layered(const float *params, const float *a31, const float *b31, 
     out[68] = L.PDF(wo, wi, radiance);
     out[69] = (float)L.LayerFlags();
     return 0;
+}
+
+int pbrt_debug_bvh_stats(const pbrt_scene *scene, int64_t *out8) {
+    try {
+        if (!scene || !out8) return Fail("null argument");
+        const BVH8 b = BuildBVH8(scene->desc.verts, scene->desc.tris, 4);
+        const int64_t v[8] = {(int64_t)b.nodes.size(), (int64_t)b.triPrim.size(), b.maxDepth, b.maxStack,
+                              (int64_t)(b.nodes.size() * sizeof(BVH8Node)), (int64_t)(b.qnodes.size() * sizeof(BVH8QNode)),
+                              0, 0};
+        memcpy(out8, v, sizeof v);
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
 }
 
 int pbrt_debug_queue_counts(pbrt_context *ctx, int32_t *counts, int n) {

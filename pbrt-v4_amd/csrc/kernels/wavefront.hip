@@ -71,7 +71,9 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_closest(Device
     float *hitB = st.hitB[depth & 1];
     const bool shade = depth < S.maxDepth;  // at maxDepth only emission and escape matter
     constexpr int kQ = 2 + NMatQ;
-    constexpr int kCap = NMatQ == 1 ? 512 : 256;  // entries per wave and queue
+    // entries per wave and queue: small enough that the staging (12 / 10 KB per block) leaves
+    // room for the group stack and the node cache at kTraversalBlocksPerCU blocks per CU
+    constexpr int kCap = NMatQ == 1 ? 256 : 128;
     __shared__ int qBuf[(kBlock / 64) * kQ * kCap];
     int *qCnt[kQ] = {escCounter, emitCounter};
     int *qArr[kQ] = {st.escQ + shard * st.capS, st.emitQ + shard * st.capS};
@@ -96,7 +98,8 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_closest(Device
             const V3 o(rec.ray[qi], rec.ray[N + qi], rec.ray[2 * N + qi]);
             const V3 d(rec.ray[3 * N + qi], rec.ray[4 * N + qi], rec.ray[5 * N + qi]);
             prim = Traverse<false, TM>(S, L, o, d, kInfinity, &h, &tc);
-            if (prim >= 0) {
+            // the hit record feeds the material stage, and at maxDepth only k_emissive
+            if (prim >= 0 && (shade || S.primLight[prim] >= 0)) {
                 hitPrim[qi] = prim;
                 hitB[qi] = h.b0;
                 hitB[N + qi] = h.b1;

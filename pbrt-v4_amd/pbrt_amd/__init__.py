@@ -93,6 +93,11 @@ class RenderStats(ctypes.Structure):
                 ("paths_per_pass", ctypes.c_uint64)]
 
 
+class KernelStat(ctypes.Structure):
+    _fields_ = [("description", ctypes.c_char * 96), ("launches", ctypes.c_int), ("total_ms", ctypes.c_double),
+                ("min_ms", ctypes.c_double), ("max_ms", ctypes.c_double)]
+
+
 # Symbols declared in include/pbrt_amd.h (tests check every one is exported)
 EXPORTED_SYMBOLS = [
     "pbrt_last_error", "pbrt_set_data_dir", "pbrt_scene_load", "pbrt_scene_load_string", "pbrt_scene_free",
@@ -103,6 +108,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
     "pbrt_debug_named_spectrum", "pbrt_debug_bxdf", "pbrt_debug_layered", "pbrt_debug_triangle_shading", "pbrt_film_write_image",
     "pbrt_image_read_size", "pbrt_image_read", "pbrt_image_write", "pbrt_image_error", "pbrt_debug_filter_sample",
+    "pbrt_debug_bvh_stats", "pbrt_set_kernel_profiling", "pbrt_get_kernel_stats",
 ]
 
 _LIB = None
@@ -142,6 +148,9 @@ def _lib():
     lib.pbrt_film_read.argtypes = [c.c_void_p, c.c_void_p]
     lib.pbrt_film_get_rgb.argtypes = [c.c_void_p, c.c_void_p]
     lib.pbrt_intersect.argtypes = [c.c_void_p, c.c_void_p, c.c_int, c.c_int, c.c_void_p, c.c_void_p]
+    lib.pbrt_debug_bvh_stats.argtypes = [c.c_void_p, c.c_void_p]
+    lib.pbrt_set_kernel_profiling.argtypes = [c.c_void_p, c.c_int]
+    lib.pbrt_get_kernel_stats.argtypes = [c.c_void_p, c.c_void_p, c.c_int, c.POINTER(c.c_int)]
     lib.pbrt_debug_halton.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_int]
     lib.pbrt_debug_halton.restype = c.c_float
     lib.pbrt_debug_halton_fastpath_mismatches.argtypes = [c.c_void_p, c.c_int, c.c_uint32, c.c_uint32, c.c_uint32]
@@ -278,6 +287,13 @@ class Scene:
     def halton(self, px, py, sample_index, dim):
         return _lib().pbrt_debug_halton(self._h, px, py, sample_index, dim)
 
+    def bvh_stats(self):
+        """Host BVH8 build statistics (pbrt_debug_bvh_stats)."""
+        out = (ctypes.c_int64 * 8)()
+        _check(_lib().pbrt_debug_bvh_stats(self._h, out))
+        keys = ("nodes", "triangles", "depth", "max_stack", "wide_bytes", "quantised_bytes")
+        return dict(zip(keys, list(out)[:6]))
+
     def halton_fastpath_mismatches(self, dim, a0, a1, step=1):
         """Indices in [a0, a1) (stride step) whose 24-bit fast-path ScrambledRadicalInverse
         differs from the 64-bit restatement (core.h); -1 on bad arguments."""
@@ -348,6 +364,40 @@ class WavefrontPathIntegrator:
 
     def reset_stats(self):
         _check(_lib().pbrt_reset_stats(self._h))
+
+    def set_kernel_profiling(self, enable=True):
+        """Bracket every stage launch with HIP events (GetProfilerEvents, gpu/util.cpp:178-205)."""
+        _check(_lib().pbrt_set_kernel_profiling(self._h, 1 if enable else 0))
+
+    def kernel_stats(self):
+        """Per-stage profile as of the last synchronize(): list of dicts in first-launch order."""
+        n = ctypes.c_int(0)
+        _check(_lib().pbrt_get_kernel_stats(self._h, None, 0, ctypes.byref(n)))
+        arr = (KernelStat * max(n.value, 1))()
+        _check(_lib().pbrt_get_kernel_stats(self._h, arr, n.value, ctypes.byref(n)))
+        return [{"description": k.description.decode(), "launches": k.launches, "total_ms": k.total_ms,
+                 "min_ms": k.min_ms, "max_ms": k.max_ms} for k in arr[:n.value]]
+
+    def report_kernel_stats(self, file=None):
+        """ReportKernelStats (gpu/util.cpp:211-246): one line per stage, stages under 0.1 % of the
+        total folded into "Other"."""
+        import sys
+        out = file or sys.stdout
+        ks = self.kernel_stats()
+        total = sum(k["total_ms"] for k in ks) or 1.0
+        print("Wavefront Kernel Profile:", file=out)
+        other_n, other_ms = 0, 0.0
+        for k in ks:
+            if k["total_ms"] > 0.001 * total:
+                print(f"  {k['description']:<49s} {k['launches']:5d} launches {k['total_ms']:9.2f} ms / "
+                      f"{100 * k['total_ms'] / total:5.1f}% (avg {k['total_ms'] / k['launches']:6.3f}, min "
+                      f"{k['min_ms']:6.3f}, max {k['max_ms']:7.3f})", file=out)
+            else:
+                other_n += k["launches"]
+                other_ms += k["total_ms"]
+        print(f"  {'Other':<49s} {other_n:5d} launches {other_ms:9.2f} ms / {100 * other_ms / total:5.1f}% "
+              f"(avg {other_ms / max(other_n, 1):6.3f})", file=out)
+        print(f"\nTotal rendering time: {total:9.2f} ms\n", file=out)
 
     def queue_counts(self):
         """Per-depth queue sizes of the last pass: rows of (rays, diffuse material, shadow, escaped,

@@ -20,10 +20,10 @@ def rows_for_rank(py0: int, py1: int, rank: int, world: int, block: int = 16) ->
 
 
 def job_spp(spp_per_gpu: int, world: int, scaling: str = "weak") -> int:
-    """Samples per pixel of the whole job.  Weak scaling (bench.py default for N > 1): every GPU
-    keeps the single-GPU workload (W x H x spp samples), so the job is one W x H image at
-    spp x N samples per pixel whose row stripes are dealt over the N GPUs (each renders 1/N of
-    the rows at all spp x N samples).  Strong scaling: the same W x H x spp image split N ways."""
+    """Samples per pixel of the whole job.  Strong scaling (bench.py's default for N > 1): the
+    same W x H x spp image split N ways.  Weak scaling: every GPU keeps the single-GPU workload
+    (W x H x spp samples), so the job is one W x H image at spp x N samples per pixel whose row
+    stripes are dealt over the N GPUs (each renders 1/N of the rows at all spp x N samples)."""
     if scaling not in ("weak", "strong"):
         raise ValueError(f"scaling must be 'weak' or 'strong', not {scaling!r}")
     return spp_per_gpu * world if scaling == "weak" else spp_per_gpu

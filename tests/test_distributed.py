@@ -1,6 +1,7 @@
 """Multi-process film sharding (the N>1 path of bench.py) on CPU with gloo, world_size 2:
 each rank renders its row stripes, one sum-reduce of the film, result == single process.
-Weak scaling (bench.py's default for N > 1) renders the job at spp x N; strong at spp."""
+Strong scaling (bench.py's default for N > 1) renders the job at spp; weak at spp x N.  The
+bench line's metric / config must name the job the ranks actually rendered."""
 import os
 import socket
 
@@ -63,3 +64,67 @@ def test_job_spp():
     assert job_spp(64, 8) == 512 and job_spp(64, 8, "strong") == 64 and job_spp(64, 1) == 64
     with pytest.raises(ValueError):
         job_spp(64, 2, "both")
+
+
+def _bench_worker(rank, world, port, out_path, scaling):
+    """bench.py's N > 1 job on the CPU: bench.job_spec decides the job, the ranks render it
+    (oracle in place of the GPU library) and reduce the film; rank 0 records the line's fields."""
+    import json
+    import sys
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(ROOT / "pbrt-v4_amd"))
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import bench
+    import pbrt_amd as pa
+    import pyoracle
+    from pbrt_amd.tiles import reduce_film, rows_for_rank
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    argv = ["--gpus", str(world), "--xres", "32", "--yres", "24", "--spp", "2"]
+    if scaling:
+        argv += ["--scaling", scaling]
+    args = bench.parse(argv)
+    job = bench.job_spec(args, world, args.scaling if world > 1 else "weak")
+    sc = pa.load_scene(SCENES / "cornell-box.pbrt", xresolution=args.xres, yresolution=args.yres, spp=job["spp"])
+    i = sc.info
+    rows = rows_for_rank(i.py0, i.py1, rank, world, block=1)
+    film = pyoracle.render(sc, rows=rows, threads=2)
+    t = torch.from_numpy(film.reshape(-1).copy())
+    reduce_film(t, dst=0)
+    n_rows = torch.tensor([len(rows)])
+    dist.all_reduce(n_rows)
+    if rank == 0:
+        np.save(out_path + ".npy", t.numpy())
+        rec = dict(job, rendered_spp=i.spp, rendered_rows=int(n_rows.item()), xres=i.xres, yres=i.yres)
+        open(out_path + ".json", "w").write(json.dumps(rec))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("scaling", [None, "weak"])
+def test_bench_line_names_the_rendered_job(tmp_path, pa, oracle, scaling):
+    import json
+    out = str(tmp_path / "job")
+    mp.spawn(_bench_worker, args=(2, _free_port(), out, scaling), nprocs=2, join=True)
+    rec = json.loads(open(out + ".json").read())
+    spp = 2 if scaling is None else 4  # default for N > 1 is strong scaling
+    assert rec["scaling"] == ("strong" if scaling is None else "weak")
+    assert rec["spp"] == rec["rendered_spp"] == spp
+    assert rec["metric"] == f"Msamples/sec (paths x spp / s) at 32x24x{spp}spp"
+    assert rec["rendered_rows"] == rec["yres"] == 24
+    assert f"32x24x{spp}spp" in rec["sharding"]
+    sc = pa.load_scene(SCENES / "cornell-box.pbrt", xresolution=32, yresolution=24, spp=spp)
+    np.testing.assert_array_equal(np.load(out + ".npy"), oracle.render(sc, threads=4).reshape(-1))
+
+
+def test_closest_bytes_from_queue_counts():
+    import sys
+    sys.path.insert(0, str(ROOT))
+    import bench
+    # columns: rays, diffuse, shadow, escaped, emissive, dielectric, conductor; maxdepth 1
+    q = np.array([[100, 60, 0, 30, 5, 4, 1], [65, 0, 0, 20, 3, 0, 0]])
+    total, rays = bench.closest_bytes(q, 1)
+    # depth 0: 24*100 + 20*65 hits + 4*(65 + 5 + 30); depth 1: 24*65 + 20*3 emissive + 4*(0 + 3 + 20)
+    assert rays == 165
+    assert total == (2400 + 1300 + 400) + (1560 + 60 + 92)

@@ -275,6 +275,13 @@ int pbrt_debug_layered(const float *params12, const float *a31, const float *b31
  * triangles, tree depth, worst-case traversal stack entries, wide node bytes, quantised node
  * bytes, 0, 0 */
 int pbrt_debug_bvh_stats(const pbrt_scene *scene, int64_t *out8);
+/* BVHLightSampler::buildBVH (lightsamplers.cpp:135-238) as the loader runs it, over given
+ * LightBounds lights13 [n][13] = pMin3 pMax3 w3 phi cosTheta_o cosTheta_e twoSided: nodes12
+ * [n_nodes][12] decoded CompactLightBounds (pMin3 pMax3 w3 phi cosTheta_o cosTheta_e), info3
+ * [n_nodes][3] childOrLight isLeaf twoSided, trails [n] bit trails (0xffffffff: not in the
+ * tree); at most max_nodes nodes are written, *n_nodes = the tree's node count (host only) */
+int pbrt_debug_light_bvh(const float *lights13, int n, float *nodes12, int32_t *info3, uint32_t *trails, int max_nodes,
+                         int *n_nodes);
 /* queue counters of the last pass: [depth][8] = rays, material hits, shadow rays, escaped,
  * emissive hits (diagnostics) */
 int pbrt_debug_queue_counts(pbrt_context *ctx, int32_t *counts, int n);

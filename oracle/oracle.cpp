@@ -1029,17 +1029,262 @@ static Float Importance(const LightNode &b, Vec p, Vec n) {
     return std::max<Float>(imp, 0);
 }
 
+// ---------------------------------------------------------------- light BVH construction
+// The oracle builds its own BVHLightSampler tree from the flat light list (it does not read the
+// product's): LightBounds of each light (DiffuseAreaLight::Bounds lights.cpp:803-822 with
+// Triangle::NormalBounds shapes.cpp:303-318; PointLight / SpotLight::Bounds lights.cpp:168-173,
+// 1401-1411), their union (lights.h:137-150 over DirectionCone Union, util/vecmath.cpp:57-84,
+// and Rotate, util/transform.h:220-247), the modified-SAH split (lightsamplers.cpp:135-238,
+// EvaluateCost lightsamplers.h:383-396) and the CompactLightBounds quantisation with its
+// decode (lightsamplers.h:95-180, OctahedralVector util/vecmath.h:1735-1785).
+namespace lbvh {
+struct Box {
+    Vec mn{std::numeric_limits<Float>::max(), std::numeric_limits<Float>::max(), std::numeric_limits<Float>::max()};
+    Vec mx{std::numeric_limits<Float>::lowest(), std::numeric_limits<Float>::lowest(), std::numeric_limits<Float>::lowest()};
+    Box() = default;
+    Box(Vec a, Vec b) {
+        mn = Vec(std::min(a.x, b.x), std::min(a.y, b.y), std::min(a.z, b.z));
+        mx = Vec(std::max(a.x, b.x), std::max(a.y, b.y), std::max(a.z, b.z));
+    }
+    Box Union(const Box &o) const {
+        Box r;
+        r.mn = Vec(std::min(mn.x, o.mn.x), std::min(mn.y, o.mn.y), std::min(mn.z, o.mn.z));
+        r.mx = Vec(std::max(mx.x, o.mx.x), std::max(mx.y, o.mx.y), std::max(mx.z, o.mx.z));
+        return r;
+    }
+    Box Union(Vec p) const { return Union(Box(p, p)); }
+    Vec Diagonal() const { return mx - mn; }
+    Float SurfaceArea() const {
+        Vec d = Diagonal();
+        return 2 * (d.x * d.y + d.x * d.z + d.y * d.z);
+    }
+    Vec Offset(Vec p) const {
+        Vec o = p - mn;
+        for (int a = 0; a < 3; ++a)
+            if (mx[a] > mn[a]) o[a] /= mx[a] - mn[a];
+        return o;
+    }
+};
+struct LB {  // LightBounds
+    Box b;
+    Vec w;
+    Float phi = 0, cosO = 0, cosE = 0;
+    bool two = false;
+    LB() = default;
+    LB(Box bb, Vec ww, Float p, Float co, Float ce, bool t) : b(bb), w(Normalize(ww)), phi(p), cosO(co), cosE(ce), two(t) {}
+    Vec Centroid() const { return (b.mn + b.mx) / 2; }
+};
+struct Cone {
+    Vec w;
+    Float cosT = Infinity;
+    Cone() = default;
+    Cone(Vec ww, Float c) : w(Normalize(ww)), cosT(c) {}
+    bool Empty() const { return cosT == Infinity; }
+};
+static Vec Rotated(Float thetaDeg, Vec axis, Vec v) {
+    const Float rad = (Pi / 180) * thetaDeg;
+    const Float st = std::sin(rad), ct = std::cos(rad);
+    const Vec a = Normalize(axis);
+    Float m[3][3];
+    m[0][0] = a.x * a.x + (1 - a.x * a.x) * ct;
+    m[0][1] = a.x * a.y * (1 - ct) - a.z * st;
+    m[0][2] = a.x * a.z * (1 - ct) + a.y * st;
+    m[1][0] = a.x * a.y * (1 - ct) + a.z * st;
+    m[1][1] = a.y * a.y + (1 - a.y * a.y) * ct;
+    m[1][2] = a.y * a.z * (1 - ct) - a.x * st;
+    m[2][0] = a.x * a.z * (1 - ct) - a.y * st;
+    m[2][1] = a.y * a.z * (1 - ct) + a.x * st;
+    m[2][2] = a.z * a.z + (1 - a.z * a.z) * ct;
+    return Vec(m[0][0] * v.x + m[0][1] * v.y + m[0][2] * v.z, m[1][0] * v.x + m[1][1] * v.y + m[1][2] * v.z,
+               m[2][0] * v.x + m[2][1] * v.y + m[2][2] * v.z);
+}
+static Cone UnionCone(const Cone &a, const Cone &b) {
+    if (a.Empty()) return b;
+    if (b.Empty()) return a;
+    const Float ta = SafeACos(a.cosT), tb = SafeACos(b.cosT), td = AngleBetween(a.w, b.w);
+    if (std::min(td + tb, Pi) <= ta) return a;
+    if (std::min(td + ta, Pi) <= tb) return b;
+    const Float to = (ta + td + tb) / 2;
+    if (to >= Pi) return Cone(Vec(0, 0, 1), -1);
+    const Float tr = to - ta;
+    const Vec wr = Cross(a.w, b.w);
+    if (LengthSquared(wr) == 0) return Cone(Vec(0, 0, 1), -1);
+    return Cone(Rotated((180 / Pi) * tr, wr, a.w), std::cos(to));
+}
+static LB Union(const LB &a, const LB &b) {
+    if (a.phi == 0) return b;
+    if (b.phi == 0) return a;
+    const Cone c = UnionCone(Cone(a.w, a.cosO), Cone(b.w, b.cosO));
+    return LB(a.b.Union(b.b), c.w, a.phi + b.phi, c.cosT, std::min(a.cosE, b.cosE), a.two || b.two);
+}
+static Float Cost(const LB &b, const Box &bounds, int dim) {
+    const Float thO = std::acos(b.cosO), thE = std::acos(b.cosE);
+    const Float thW = std::min(thO + thE, Pi);
+    const Float sinO = SafeSqrt(1 - Sqr(b.cosO));
+    const Float Mw = 2 * Pi * (1 - b.cosO) + Pi / 2 * (2 * thW * sinO - std::cos(thO - 2 * thW) - 2 * thO * sinO + b.cosO);
+    const Vec d = bounds.Diagonal();
+    const Float Kr = MaxComp(d) / d[dim];
+    return b.phi * Mw * Kr * b.b.SurfaceArea();
+}
+// CompactLightBounds(lb, allb) and its decode
+static LightNode Compact(const LB &lb, const Box &all) {
+    LightNode n{};
+    Vec v = Normalize(lb.w);
+    v = v / (std::abs(v.x) + std::abs(v.y) + std::abs(v.z));
+    auto enc = [](Float f) { return (uint16_t)std::round(std::min<Float>(std::max<Float>((f + 1) / 2, 0), 1) * 65535.f); };
+    auto sgn = [](Float x) { return std::copysign(Float(1), x); };
+    uint16_t ox, oy;
+    if (v.z >= 0) ox = enc(v.x), oy = enc(v.y);
+    else ox = enc((1 - std::abs(v.y)) * sgn(v.x)), oy = enc((1 - std::abs(v.x)) * sgn(v.y));
+    Vec d(-1 + 2 * (ox / 65535.f), -1 + 2 * (oy / 65535.f), 0);
+    d.z = 1 - (std::abs(d.x) + std::abs(d.y));
+    if (d.z < 0) {
+        const Float xo = d.x;
+        d.x = (1 - std::abs(d.y)) * sgn(xo);
+        d.y = (1 - std::abs(xo)) * sgn(d.y);
+    }
+    n.w = Normalize(d);
+    n.phi = lb.phi;
+    const unsigned qo = (unsigned)std::floor(32767.f * ((lb.cosO + 1) / 2)), qe = (unsigned)std::floor(32767.f * ((lb.cosE + 1) / 2));
+    n.cosO = 2 * (qo / 32767.f) - 1;
+    n.cosE = 2 * (qe / 32767.f) - 1;
+    n.twoSided = lb.two;
+    for (int c = 0; c < 3; ++c) {
+        auto q = [&](Float x) { return all.mn[c] == all.mx[c] ? 0.f : 65535.f * Clamp((x - all.mn[c]) / (all.mx[c] - all.mn[c]), 0, 1); };
+        const uint16_t q0 = (uint16_t)std::floor(q(lb.b.mn[c])), q1 = (uint16_t)std::ceil(q(lb.b.mx[c]));
+        auto lerp = [&](Float t) { return (1 - t) * all.mn[c] + t * all.mx[c]; };
+        n.mn[c] = lerp(q0 / 65535.f);
+        n.mx[c] = lerp(q1 / 65535.f);
+    }
+    return n;
+}
+struct Builder {
+    std::vector<LightNode> nodes;
+    std::vector<uint32_t> trail;
+    Box all;
+    std::pair<int, LB> Build(std::vector<std::pair<int, LB>> &L, int start, int end, uint32_t bits, int depth) {
+        if (end - start == 1) {
+            const int idx = (int)nodes.size();
+            LightNode n = Compact(L[start].second, all);
+            n.childOrLight = L[start].first;
+            n.isLeaf = 1;
+            nodes.push_back(n);
+            trail[L[start].first] = bits;
+            return {idx, L[start].second};
+        }
+        Box bounds, cb;
+        for (int i = start; i < end; ++i) {
+            bounds = bounds.Union(L[i].second.b);
+            cb = cb.Union(L[i].second.Centroid());
+        }
+        Float minCost = Infinity;
+        int bestB = -1, bestDim = -1;
+        constexpr int nb = 12;
+        auto bucket = [&](const LB &lb, int dim) {
+            int b = nb * cb.Offset(lb.Centroid())[dim];
+            return b == nb ? nb - 1 : b;
+        };
+        for (int dim = 0; dim < 3; ++dim) {
+            if (cb.mx[dim] == cb.mn[dim]) continue;
+            LB bl[nb];
+            for (int i = start; i < end; ++i) {
+                const int b = bucket(L[i].second, dim);
+                bl[b] = Union(bl[b], L[i].second);
+            }
+            Float cost[nb - 1];
+            for (int i = 0; i < nb - 1; ++i) {
+                LB b0, b1;
+                for (int j = 0; j <= i; ++j) b0 = Union(b0, bl[j]);
+                for (int j = i + 1; j < nb; ++j) b1 = Union(b1, bl[j]);
+                cost[i] = Cost(b0, bounds, dim) + Cost(b1, bounds, dim);
+            }
+            for (int i = 1; i < nb - 1; ++i)
+                if (cost[i] > 0 && cost[i] < minCost) minCost = cost[i], bestB = i, bestDim = dim;
+        }
+        int mid;
+        if (bestDim == -1) mid = (start + end) / 2;
+        else {
+            auto it = std::partition(L.begin() + start, L.begin() + end,
+                                     [&](const std::pair<int, LB> &l) { return bucket(l.second, bestDim) <= bestB; });
+            mid = (int)(it - L.begin());
+            if (mid == start || mid == end) mid = (start + end) / 2;
+        }
+        const int idx = (int)nodes.size();
+        nodes.push_back(LightNode{});
+        auto c0 = Build(L, start, mid, bits, depth + 1);
+        auto c1 = Build(L, mid, end, bits | (1u << depth), depth + 1);
+        const LB lb = Union(c0.second, c1.second);
+        LightNode n = Compact(lb, all);
+        n.childOrLight = c1.first;
+        n.isLeaf = 0;
+        nodes[idx] = n;
+        return {idx, lb};
+    }
+    void Run(std::vector<std::pair<int, LB>> L, int nLights) {
+        nodes.clear();
+        trail.assign(nLights, 0xffffffffu);
+        all = Box();
+        std::vector<std::pair<int, LB>> in;
+        for (auto &l : L)
+            if (l.second.phi > 0) {  // lightsamplers.cpp:121-124
+                in.push_back(l);
+                all = all.Union(l.second.b);
+            }
+        if (!in.empty()) Build(in, 0, (int)in.size(), 0, 0);
+    }
+};
+// LightBounds of the scene's bounded lights (area lights, then point / spot lights)
+static std::vector<std::pair<int, LB>> SceneLightBounds(const pbrt_scene_flat *f) {
+    std::vector<std::pair<int, LB>> L;
+    auto denseMax = [&](int sp) {
+        const float *d = f->dense_spectra + 311 * sp;
+        return *std::max_element(d, d + 311);
+    };
+    for (int i = 0; i < f->n_area_lights; ++i) {
+        const int t = f->light_prim[i];
+        const int32_t *v = f->triangles + 3 * t;
+        auto P = [&](int k) { return Vec(f->vertices[3 * v[k]], f->vertices[3 * v[k] + 1], f->vertices[3 * v[k] + 2]); };
+        const Vec p0 = P(0), p1 = P(1), p2 = P(2);
+        Float phi = denseMax(f->light_spectrum[i]);
+        phi *= f->light_scale[i] * TriArea(p0, p1, p2) * Pi;
+        Vec n = Normalize(Cross(p1 - p0, p2 - p0));
+        if (f->tri_shading && (f->tri_shading[t] & 1)) {
+            auto N = [&](int k) { return Vec(f->vertex_normals[3 * v[k]], f->vertex_normals[3 * v[k] + 1], f->vertex_normals[3 * v[k] + 2]); };
+            const Vec ns = N(0) + N(1) + N(2);
+            if (DotN(n, ns) < 0) n = -n;  // FaceForward(Normal3f, Normal3f): FMA-compensated dot
+        } else if (f->tri_flip[t]) {
+            n = -n;
+        }
+        const Cone nb(n, 1);  // DirectionCone(Vector3f(n))
+        L.push_back({i, LB(Box(p0, p1).Union(p2), nb.w, phi, nb.cosT, std::cos(Pi / 2), f->light_two_sided[i] != 0)});
+    }
+    for (int k = 0; k < f->n_point_spot; ++k) {
+        const float *d = f->delta_lights + 24 * k;
+        const Vec p(d[5], d[6], d[7]);
+        const Float mx = denseMax((int)d[1]), scale = d[2];
+        if ((int)d[0] == 0) {
+            L.push_back({f->n_area_lights + k, LB(Box(p, p), Vec(0, 0, 1), 4 * Pi * scale * mx, std::cos(Pi), std::cos(Pi / 2), false)});
+        } else {
+            const Float cosStart = d[3], cosEnd = d[4];
+            Float cosE = std::cos(std::acos(cosEnd) - std::acos(cosStart));
+            if (cosE == 1 && cosEnd != cosStart) cosE = 0.999f;
+            L.push_back({f->n_area_lights + k, LB(Box(p, p), Vec(d[8], d[9], d[10]), scale * mx * 4 * Pi, cosStart, cosE, false)});
+        }
+    }
+    return L;
+}
+}  // namespace lbvh
+
 struct Lights {
     const pbrt_scene_flat *f;
     std::vector<LightNode> nodes;
+    std::vector<uint32_t> bitTrail;  // per bounded light (area, then point / spot)
     void Init(const pbrt_scene_flat *flat) {
         f = flat;
-        for (int i = 0; i < f->n_light_nodes; ++i) {
-            const float *b = f->light_node_bounds + 12 * i;
-            const int32_t *in = f->light_node_info + 3 * i;
-            nodes.push_back({Vec(b[0], b[1], b[2]), Vec(b[3], b[4], b[5]), Vec(b[6], b[7], b[8]), b[9], b[10], b[11],
-                             in[2], in[0], in[1]});
-        }
+        lbvh::Builder b;
+        b.Run(lbvh::SceneLightBounds(f), f->n_area_lights + f->n_point_spot);
+        nodes = b.nodes;
+        bitTrail = b.trail;
     }
     // global light index: area lights, point / spot lights, then the infinite-light list
     int NumAll() const { return f->n_area_lights + f->n_point_spot + f->n_infinite_lights; }
@@ -1097,7 +1342,7 @@ struct Lights {
     }
     Float PMF(Vec p, Vec n, int light) const {
         if (uniformFlag) return NumAll() ? 1.f / NumAll() : 0.f;
-        uint32_t trail = light < f->n_area_lights + f->n_point_spot ? f->light_bit_trail[light] : 0xffffffffu;
+        uint32_t trail = light < f->n_area_lights + f->n_point_spot ? bitTrail[light] : 0xffffffffu;
         bool inBVH = false;
         for (auto &nd : nodes)
             if (nd.isLeaf && nd.childOrLight == light) inBVH = true;
@@ -2797,6 +3042,41 @@ int oracle_intersect_batch(const pbrt_scene_flat *flat, const pbrt_scene_info *i
         });
     for (auto &t : pool) t.join();
     return 0;
+}
+
+// The oracle's own light BVH: over given LightBounds rows ([n][13] pMin3 pMax3 w3 phi cosO cosE
+// twoSided) when lights13 != NULL, else over the scene's lights.  Same output layout as
+// pbrt_debug_light_bvh.  Returns the node count.
+int oracle_light_bvh(const pbrt_scene_flat *flat, const float *lights13, int n, float *nodes12, int32_t *info3,
+                     uint32_t *trails, int maxNodes) {
+    std::vector<std::pair<int, lbvh::LB>> L;
+    int nLights = n;
+    if (lights13) {
+        for (int i = 0; i < n; ++i) {
+            const float *v = lights13 + 13 * i;
+            lbvh::LB lb;
+            lb.b = lbvh::Box(Vec(v[0], v[1], v[2]), Vec(v[3], v[4], v[5]));
+            lb.w = Vec(v[6], v[7], v[8]);  // as stored by the LightBounds constructor
+            lb.phi = v[9];
+            lb.cosO = v[10];
+            lb.cosE = v[11];
+            lb.two = v[12] != 0;
+            L.push_back({i, lb});
+        }
+    } else {
+        L = lbvh::SceneLightBounds(flat);
+        nLights = flat->n_area_lights + flat->n_point_spot;
+    }
+    lbvh::Builder b;
+    b.Run(L, nLights);
+    for (int i = 0; i < std::min((int)b.nodes.size(), maxNodes); ++i) {
+        const LightNode &d = b.nodes[i];
+        const float v[12] = {d.mn.x, d.mn.y, d.mn.z, d.mx.x, d.mx.y, d.mx.z, d.w.x, d.w.y, d.w.z, d.phi, d.cosO, d.cosE};
+        if (nodes12) std::memcpy(nodes12 + 12 * i, v, sizeof v);
+        if (info3) info3[3 * i] = d.childOrLight, info3[3 * i + 1] = d.isLeaf, info3[3 * i + 2] = d.twoSided;
+    }
+    if (trails) std::copy(b.trail.begin(), b.trail.end(), trails);
+    return (int)b.nodes.size();
 }
 
 // ---- component entry points checked against tests/golden/reference_components.json

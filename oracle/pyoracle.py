@@ -45,6 +45,7 @@ def lib():
         _lib.oracle_render.argtypes = [vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, vp]
         _lib.oracle_set_cr_math.argtypes = [ctypes.c_int]
+        _lib.oracle_light_bvh.argtypes = [vp, vp, ctypes.c_int, vp, vp, vp, ctypes.c_int]
     return _lib
 
 
@@ -103,6 +104,24 @@ def film_to_rgb(film, m3x3):
     rgb = film[:3] / np.where(w == 0, 1, w)
     m = np.asarray(m3x3, dtype=np.float64).reshape(3, 3)
     return np.einsum("ij,jhw->hwi", m, rgb).astype(np.float32)
+
+
+def light_bvh(scene=None, lights13=None):
+    """The oracle's own BVHLightSampler tree, over the scene's lights or given [n][13] LightBounds
+    rows -> (nodes [m][12] decoded bounds, info [m][3] childOrLight / isLeaf / twoSided, trails)."""
+    flat = None if scene is None else scene.flat()
+    fp = ctypes.byref(flat) if flat is not None else None
+    if lights13 is not None:
+        lights13 = np.ascontiguousarray(lights13, dtype=np.float32).reshape(-1, 13)
+        n, lp = len(lights13), lights13.ctypes.data
+    else:
+        n, lp = flat.n_area_lights + flat.n_point_spot, None
+    m = lib().oracle_light_bvh(fp, lp, n, None, None, None, 0)
+    nodes = np.zeros((max(m, 1), 12), np.float32)
+    info = np.zeros((max(m, 1), 3), np.int32)
+    trails = np.zeros(max(n, 1), np.uint32)
+    lib().oracle_light_bvh(fp, lp, n, nodes.ctypes.data, info.ctypes.data, trails.ctypes.data, m)
+    return nodes[:m], info[:m], trails[:n]
 
 
 def trowbridge(in13):

@@ -36,8 +36,9 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
                               hipStream_t s);
 hipError_t LaunchIntersectBatch(const DeviceScene &S, const float *rays, int n, int anyHit, int *outPrim,
                                 float *outHit, hipStream_t s);
-size_t SurfaceTraversalStaticLds();
-size_t VolTraversalStaticLds();
+size_t SurfaceTraversalStaticLds(int tm);
+int TraversalBlocksCompiled(int compressed);
+size_t VolTraversalStaticLds(int tm);
 }  // namespace pbrt_amd
 
 using namespace pbrt_amd;
@@ -720,35 +721,44 @@ static void BuildDevice(pbrt_context *c) {
         S.bvhAbsMax[a] = std::isfinite(lo) && std::isfinite(hi) ? std::max(std::fabs(lo), std::fabs(hi)) + 2 * ext : 0.f;
     }
     {
-        // Node format: the 256-B wide node by default; PBRT_AMD_BVH=compressed selects the 80-B
-        // quantised node.  Measured: the quantised node cuts node bytes 3.2x but
-        // its decode adds VALU work to a traversal that is issue-bound, not bandwidth-bound,
-        // so it is 1-5 % slower on C3 and C4 today.
+        // Node format.  A tree that fits the LDS cache whole (nodes + pre-rotated triangles:
+        // Cornell) traverses wide nodes from LDS.  An HBM-resident tree traverses the 80-B
+        // quantised nodes with kernels compiled for TraversalWaves(kTravQuant) = 6 waves per
+        // SIMD: the traversal is bound by dependent-load latency, and the smaller node loads
+        // (20 VGPRs instead of 60) buy the waves in flight (C4 k_closest -16 %).
+        // PBRT_AMD_BVH=wide / compressed forces a format.
         const char *fmt = getenv("PBRT_AMD_BVH");
-        S.compressed = fmt && strcmp(fmt, "compressed") == 0;
-        // LDS scene cache: top BVH8 nodes first (BFS order), then leading leaf-order triangles
-        const int stride = 16 * LdsNodeStride(S.compressed);
-        // A traversal block's LDS = static (queue staging) + the group stack + the node /
-        // triangle cache; the cache gets what the other two leave of the per-block limit, and
-        // a tree whose stack alone does not fit is rejected here rather than failing at launch.
+        const bool forceWide = fmt && strcmp(fmt, "wide") == 0, forceQuant = fmt && strcmp(fmt, "compressed") == 0;
         int maxLds = 0;
         HIPCHECK(hipDeviceGetAttribute(&maxLds, hipDeviceAttributeMaxSharedMemoryPerBlock, c->device));
-        const size_t staticLds = std::max(SurfaceTraversalStaticLds(), VolTraversalStaticLds());
         const size_t stackLds = (size_t)c->bvh.maxStack * 256 * sizeof(uint2);  // kBlock lanes
-        if (staticLds + stackLds > (size_t)maxLds)
-            throw Error("BVH needs a " + std::to_string(c->bvh.maxStack) + "-entry traversal stack (" +
-                        std::to_string(stackLds) + " B of LDS per block beside " + std::to_string(staticLds) +
-                        " B static; the device allows " + std::to_string(maxLds) + ")");
-        // occupancy: kTraversalBlocksPerCU blocks per CU when static + stack leave room (C4: 10 KB
-        // + 18 KB of a 40 KB share -> a 12 KB cache); the cache never pushes a block past its share
-        const size_t share = std::min<size_t>((size_t)maxLds, kLdsPerCU / kTraversalBlocksPerCU - 512);
-        const size_t left = share > staticLds + stackLds ? share - staticLds - stackLds : 0;
-        int nNodes = (int)c->bvh.nodes.size();
-        int budget = (int)std::min<size_t>(kSceneLdsBudget, left);
-        S.ldsNodes = std::min(nNodes, budget / stride);
-        budget -= S.ldsNodes * stride;
-        // all or none, in three pre-rotated copies (one per ray permutation)
-        S.ldsTris = (!S.compressed && S.ldsNodes == nNodes && nt * 3 * 48 <= budget) ? nt : 0;
+        const int nNodes = (int)c->bvh.nodes.size();
+        // A traversal block's LDS = static (queue staging) + the group stack + the node /
+        // triangle cache (top BVH8 nodes first, BFS order, then all triangles or none).  The
+        // cache gets what the other two leave of the block's share of the CU at the mode's
+        // occupancy (C4 wide: 10 KB + 18 KB of 40 KB -> 12 KB); a tree whose stack does not fit
+        // the per-block limit is rejected here rather than failing at launch.
+        auto layout = [&](bool compressed, int tm) {
+            const size_t staticLds = std::max(SurfaceTraversalStaticLds(tm), VolTraversalStaticLds(tm));
+            if (staticLds + stackLds > (size_t)maxLds)
+                throw Error("BVH needs a " + std::to_string(c->bvh.maxStack) + "-entry traversal stack (" +
+                            std::to_string(stackLds) + " B of LDS per block beside " + std::to_string(staticLds) +
+                            " B static; the device allows " + std::to_string(maxLds) + ")");
+            const size_t share =
+                std::min<size_t>((size_t)maxLds, kLdsPerCU / TraversalBlocksCompiled(compressed ? 1 : 0) - 512);
+            const size_t left = share > staticLds + stackLds ? share - staticLds - stackLds : 0;
+            const int stride = 16 * LdsNodeStride(compressed);
+            int budget = (int)std::min<size_t>(kSceneLdsBudget, left);
+            S.compressed = compressed ? 1 : 0;
+            S.ldsNodes = std::min(nNodes, budget / stride);
+            budget -= S.ldsNodes * stride;
+            // all or none, in three pre-rotated copies (one per ray permutation)
+            S.ldsTris = (!compressed && S.ldsNodes == nNodes && nt * 3 * 48 <= budget) ? nt : 0;
+        };
+        layout(false, kTravWide);
+        const bool allInLds = S.ldsTris > 0;
+        if (forceQuant || (!forceWide && !allInLds)) layout(true, kTravQuant);
+        else if (allInLds) layout(false, kTravLds);
     }
 
     // film
@@ -1769,6 +1779,32 @@ int pbrt_debug_layered(const float *params, const float *a31, const float *b31, 
     out[68] = L.PDF(wo, wi, radiance);
     out[69] = (float)L.LayerFlags();
     return 0;
+}
+
+int pbrt_debug_light_bvh(const float *lights13, int n, float *nodes12, int32_t *info3, uint32_t *trails, int max_nodes,
+                         int *n_nodes) {
+    try {
+        if (!lights13 || n < 0 || !n_nodes) return Fail("bad arguments");
+        std::vector<LightBVHNodeDesc> nodes;
+        std::vector<uint32_t> tr;
+        DebugBuildLightBVH(lights13, n, &nodes, &tr);
+        *n_nodes = (int)nodes.size();
+        for (int i = 0; i < std::min((int)nodes.size(), max_nodes); ++i) {
+            const LightNodeBounds &b = nodes[i].bounds;
+            const float v[12] = {b.pMin.x, b.pMin.y, b.pMin.z, b.pMax.x, b.pMax.y, b.pMax.z, b.w.x, b.w.y, b.w.z,
+                                 b.phi, b.cosTheta_o, b.cosTheta_e};
+            if (nodes12) memcpy(nodes12 + 12 * i, v, sizeof v);
+            if (info3) {
+                info3[3 * i] = nodes[i].childOrLight;
+                info3[3 * i + 1] = nodes[i].isLeaf;
+                info3[3 * i + 2] = b.twoSided;
+            }
+        }
+        if (trails) std::copy(tr.begin(), tr.end(), trails);
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
 }
 
 int pbrt_debug_bvh_stats(const pbrt_scene *scene, int64_t *out8) {

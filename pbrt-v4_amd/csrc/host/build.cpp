@@ -248,7 +248,7 @@ void ConeUnion(V3 aw, float aCos, V3 bw, float bCos, V3 *w, float *cosTheta) {
         *cosTheta = -1;
         return;
     }
-    *w = RotateVector(theta_r * (180 / kPi), wr, aw);
+    *w = Normalize(RotateVector(theta_r * (180 / kPi), wr, aw));  // DirectionCone(w, cos theta_o)
     *cosTheta = std::cos(theta_o);
 }
 
@@ -258,7 +258,9 @@ LightBounds Union(const LightBounds &a, const LightBounds &b) {
     LightBounds r;
     V3 w;
     float cosTheta;
-    ConeUnion(a.w, a.cosTheta_o, b.w, b.cosTheta_o, &w, &cosTheta);
+    // DirectionCone(a.w, ...) normalizes its axis, and so does the LightBounds constructor
+    // around the union's (lights.h:128-150): the same normalizations, for the same bits
+    ConeUnion(Normalize(a.w), a.cosTheta_o, Normalize(b.w), b.cosTheta_o, &w, &cosTheta);
     r.bounds = a.bounds;
     r.bounds.Add(b.bounds);
     r.w = Normalize(w);
@@ -403,6 +405,31 @@ struct LightBVHBuilder {
 };
 }  // namespace
 
+void DebugBuildLightBVH(const float *in13, int n, std::vector<LightBVHNodeDesc> *nodes, std::vector<uint32_t> *trails) {
+    SceneDesc s;
+    s.lightBitTrail.assign(n, 0xffffffffu);
+    LightBVHBuilder b{s, Bounds3()};
+    std::vector<std::pair<int, LightBounds>> bvhLights;
+    for (int i = 0; i < n; ++i) {
+        const float *v = in13 + 13 * i;
+        LightBounds lb;
+        lb.bounds.Add(V3(v[0], v[1], v[2]));
+        lb.bounds.Add(V3(v[3], v[4], v[5]));
+        lb.w = V3(v[6], v[7], v[8]);
+        lb.phi = v[9];
+        lb.cosTheta_o = v[10];
+        lb.cosTheta_e = v[11];
+        lb.twoSided = v[12] != 0;
+        if (lb.phi > 0) {
+            bvhLights.push_back({i, lb});
+            b.allLightBounds.Add(lb.bounds);
+        }
+    }
+    if (!bvhLights.empty()) b.Build(bvhLights, 0, (int)bvhLights.size(), 0, 0);
+    *nodes = s.lightNodes;
+    *trails = s.lightBitTrail;
+}
+
 static void BuildLightBVH(SceneDesc &s) {
     s.lightNodes.clear();
     s.lightBitTrail.assign(s.areaLights.size() + s.nPointSpot, 0);
@@ -430,7 +457,9 @@ static void BuildLightBVH(SceneDesc &s) {
         lb.bounds.Add(p0);
         lb.bounds.Add(p1);
         lb.bounds.Add(p2);
-        lb.w = Normalize(n);
+        // DirectionCone(n) normalizes n, and LightBounds' constructor normalizes the cone's axis
+        // (DiffuseAreaLight::Bounds, lights.cpp:819-821): both, for pbrt's bits
+        lb.w = Normalize(Normalize(n));
         lb.phi = phi;
         lb.cosTheta_o = 1;
         lb.cosTheta_e = std::cos(kPi / 2);
@@ -455,7 +484,7 @@ static void BuildLightBVH(SceneDesc &s) {
             lb.cosTheta_o = std::cos(kPi);
             lb.cosTheta_e = std::cos(kPi / 2);
         } else {
-            lb.w = d.w;
+            lb.w = Normalize(d.w);  // LightBounds' constructor normalizes SpotLight::Bounds' axis again
             lb.phi = d.scale * mx * 4 * kPi;
             float cosTheta_e = std::cos(std::acos(d.cosFalloffEnd) - std::acos(d.cosFalloffStart));
             if (cosTheta_e == 1 && d.cosFalloffEnd != d.cosFalloffStart) cosTheta_e = 0.999f;

@@ -205,6 +205,9 @@ SceneDesc LoadPbrtFile(const std::string &path, const std::map<std::string, std:
 SceneDesc LoadPbrtString(const std::string &text, const std::string &baseDir,
                          const std::map<std::string, std::string> &overrides);
 void FinalizeScene(SceneDesc &s);  // lights, light BVH, sampler tables
+// BVHLightSampler::buildBVH over given LightBounds ([n][13]: pMin3 pMax3 w3 phi cosTheta_o
+// cosTheta_e twoSided); trails[i] = 0xffffffff for a light left out (phi == 0)
+void DebugBuildLightBVH(const float *in13, int n, std::vector<LightBVHNodeDesc> *nodes, std::vector<uint32_t> *trails);
 // the 24 four-way digit permutations of ZSobolSampler::GetSampleIndex, in pbrt's order
 // FilterSampler ctor (filters.cpp:133-147): tabulates the scene's filter and its
 // PiecewiseConstant2D (util/sampling.h:603-790) into SceneDesc::filterTable

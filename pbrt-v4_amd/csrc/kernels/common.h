@@ -22,8 +22,12 @@ constexpr int kBlock = 256;
 #ifndef PBRT_SHADE_GRID_CAP
 #define PBRT_SHADE_GRID_CAP 8192
 #endif
-#ifndef PBRT_SHADOW_WAVES
-#define PBRT_SHADOW_WAVES PBRT_TRAVERSAL_WAVES  // waves/SIMD of the any-hit (shadow) kernel
+// Quantised-node traversal (80-B nodes, HBM-resident trees) is compiled for more waves: its
+// node loads hold 20 VGPRs instead of 60, and on C4 (10 M triangles) the traversal is bound by
+// dependent-load latency, so waves in flight are what pays (k_closest 65.1 -> 54.6 ms per pass:
+// wide at 4, quantised at 4 / 5 / 6 waves = 65.1 / 66.9 / 66.9 / 54.6 ms; tools/gpu_c4_occ.sh)
+#ifndef PBRT_QUANT_TRAVERSAL_WAVES
+#define PBRT_QUANT_TRAVERSAL_WAVES 6
 #endif
 #ifndef PBRT_SHADE_WAVES
 #define PBRT_SHADE_WAVES 3  // waves/SIMD the shade kernel is compiled for (VGPR budget)
@@ -678,7 +682,8 @@ __device__ inline int TraverseCW(const DeviceScene &S, const SceneLds &L, V3 o, 
 // Traversal modes, one kernel instantiation each (a launch-uniform choice, so every kernel
 // carries exactly one traversal loop): every node and triangle in LDS (small scenes); wide
 // nodes with the top of the tree in LDS; quantised nodes (PBRT_AMD_BVH=compressed).
-constexpr int kTravLds = 0, kTravWide = 1, kTravQuant = 2;
+// waves per SIMD (= 256-thread blocks per CU) a traversal kernel of mode TM is compiled for
+constexpr int TraversalWaves(int tm) { return tm == kTravQuant ? PBRT_QUANT_TRAVERSAL_WAVES : PBRT_TRAVERSAL_WAVES; }
 inline int TraversalMode(const DeviceScene &S) {
     return S.compressed ? kTravQuant : (S.ldsTris > 0 ? kTravLds : kTravWide);
 }

@@ -69,10 +69,12 @@ PHD int CounterIndex(int depth, int queue, int shard) {
 constexpr int kStatsSlots = 48, kStatsSectionBase = 16;
 constexpr int kMaxStackSize = 32;  // traversal stack entries per lane (uint2: 64 KB of LDS per block)
 constexpr int kSceneLdsBudget = 16 * 1024;  // bytes of BVH nodes + triangles cached in LDS per block (at most)
-// Traversal kernels run 256-thread blocks at this many blocks (= waves per SIMD) per CU; the
-// node cache gets what static LDS and the group stack leave of 160 KB / kTraversalBlocksPerCU
-constexpr int kTraversalBlocksPerCU = 4;
+// Traversal kernels run 256-thread blocks at PBRT_TRAVERSAL_WAVES blocks (= waves per SIMD) per
+// CU; the node cache gets what static LDS and the group stack leave of kLdsPerCU / that
 constexpr int kLdsPerCU = 160 * 1024;
+// Traversal modes (one kernel instantiation each): every node and triangle in LDS, wide nodes
+// with the tree top in LDS, quantised nodes
+constexpr int kTravLds = 0, kTravWide = 1, kTravQuant = 2;
 constexpr int kLdsNodeStride = 17;  // float4 per LDS-cached wide node (68 dwords: conflict-free)
 constexpr int kLdsQNodeStride = 5;  // float4 per LDS-cached compressed node (20 dwords: conflict-free)
 PHD int LdsNodeStride(int compressed) { return compressed ? kLdsQNodeStride : kLdsNodeStride; }

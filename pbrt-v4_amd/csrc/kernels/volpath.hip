@@ -547,7 +547,7 @@ __device__ inline bool IsInterfaceHit(const DeviceScene &S, int prim) {
 }
 
 template <int TM>
-__global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_vclosest(DeviceScene S, PathState st, VolState v,
+__global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_vclosest(DeviceScene S, PathState st, VolState v,
                                                                           int wf, int timed) {
     const QueueView rays = LoadQueue(st, wf, kVRay);
     if ((int)(blockIdx.x * blockDim.x) >= rays.total) return;
@@ -2018,7 +2018,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vshadow(DeviceScene 
 // take factors that are equal at all wavelengths, so each is one scalar (the reference's 31
 // entries are 31 copies of it).
 template <int TM>
-__global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_vshadow_grey(DeviceScene S, PathState st, VolState v,
+__global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_vshadow_grey(DeviceScene S, PathState st, VolState v,
                                                                              int wf) {
     const QueueView sh = LoadQueue(st, wf, kVShadow);
     if ((int)(blockIdx.x * blockDim.x) >= sh.total) return;
@@ -2120,16 +2120,18 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_vshadow_grey(D
 
 // ------------------------------------------------------------------ launch helpers (host)
 size_t TraversalLdsBytes(int stackSize, int ldsNodes, int ldsTris, int compressed);
-size_t VolTraversalStaticLds() {
+size_t VolTraversalStaticLds(int tm) {
     size_t m = 0;
     auto take = [&](const void *f) {
         hipFuncAttributes a{};
         if (hipFuncGetAttributes(&a, f) == hipSuccess) m = std::max(m, (size_t)a.sharedSizeBytes);
     };
-#define TAKE_TM(tm)                                                      \
-    take(reinterpret_cast<const void *>(&k_vclosest<tm>));               \
-    take(reinterpret_cast<const void *>(&k_vshadow_grey<tm>));           \
-    take(reinterpret_cast<const void *>(&k_vshadow<tm>));
+#define TAKE_TM(TM)                                                      \
+    if (tm == TM) {                                                      \
+        take(reinterpret_cast<const void *>(&k_vclosest<TM>));           \
+        take(reinterpret_cast<const void *>(&k_vshadow_grey<TM>));       \
+        take(reinterpret_cast<const void *>(&k_vshadow<TM>));            \
+    }
     TAKE_TM(kTravLds) TAKE_TM(kTravWide) TAKE_TM(kTravQuant)
 #undef TAKE_TM
     return m;

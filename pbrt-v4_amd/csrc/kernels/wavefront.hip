@@ -56,7 +56,7 @@ __global__ void __launch_bounds__(kBlock) k_camera(DeviceScene S, PathState st, 
 
 // NMatQ = 1: every material is diffuse (one material queue); 3: one queue per material type
 template <int NMatQ, int TM>
-__global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_closest(DeviceScene S, PathState st, int depth, int timed) {
+__global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_closest(DeviceScene S, PathState st, int depth, int timed) {
     const QueueView rays = LoadQueue(st, depth, kCntRay);
     if ((int)(blockIdx.x * blockDim.x) >= rays.total) return;  // no work
     extern __shared__ float4 dynLds[];
@@ -72,8 +72,8 @@ __global__ void __launch_bounds__(kBlock, PBRT_TRAVERSAL_WAVES) k_closest(Device
     const bool shade = depth < S.maxDepth;  // at maxDepth only emission and escape matter
     constexpr int kQ = 2 + NMatQ;
     // entries per wave and queue: small enough that the staging (12 / 10 KB per block) leaves
-    // room for the group stack and the node cache at kTraversalBlocksPerCU blocks per CU
-    constexpr int kCap = NMatQ == 1 ? 256 : 128;
+    // room for the group stack and the node cache at TraversalWaves(TM) blocks per CU
+    constexpr int kCap = TraversalWaves(TM) > 4 ? 64 : (NMatQ == 1 ? 256 : 128);
     __shared__ int qBuf[(kBlock / 64) * kQ * kCap];
     int *qCnt[kQ] = {escCounter, emitCounter};
     int *qArr[kQ] = {st.escQ + shard * st.capS, st.emitQ + shard * st.capS};
@@ -975,7 +975,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
 }
 
 template <int TM>
-__global__ void __launch_bounds__(kBlock, PBRT_SHADOW_WAVES) k_shadow(DeviceScene S, PathState st, int depth) {
+__global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_shadow(DeviceScene S, PathState st, int depth) {
     const QueueView shadows = LoadQueue(st, depth, kCntShadow);
     if ((int)(blockIdx.x * blockDim.x) >= shadows.total) return;  // no work
     extern __shared__ float4 dynLds[];
@@ -1033,7 +1033,7 @@ __global__ void __launch_bounds__(kBlock) k_film(DeviceScene S, PathState st, in
 // The WavefrontAggregate boundary exposed on its own (integrator.h:32-54): closest / any hit
 // for an SoA ray batch, used by parity tests and the traversal benchmark.
 template <int TM>
-__global__ void __launch_bounds__(kBlock, 4) k_intersect_batch(DeviceScene S, const float *rays, int n, int anyHit,
+__global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_intersect_batch(DeviceScene S, const float *rays, int n, int anyHit,
                                                               int *outPrim, float *outHit) {
     extern __shared__ float4 dynLds[];
     const SceneLds L = SetupSceneLds(S, dynLds);
@@ -1128,19 +1128,24 @@ size_t TraversalLdsBytes(int stackSize, int ldsNodes, int ldsTris, int compresse
     return (size_t)stackSize * kBlock * sizeof(uint2) + (size_t)ldsNodes * LdsNodeStride(compressed) * 16 +
            (size_t)ldsTris * 3 * 48;
 }
+// Blocks (of kBlock threads) per CU the traversal kernels of a mode are compiled for
+int TraversalBlocksCompiled(int compressed) { return TraversalWaves(compressed ? kTravQuant : kTravWide); }
+
 // Largest static LDS of the traversal kernels (k_closest's queue staging), for BuildDevice's
 // check that the group stack + node cache + static LDS fit one block's LDS
-size_t SurfaceTraversalStaticLds() {
+size_t SurfaceTraversalStaticLds(int tm) {
     size_t m = 0;
     auto take = [&](const void *f) {
         hipFuncAttributes a{};
         if (hipFuncGetAttributes(&a, f) == hipSuccess) m = std::max(m, (size_t)a.sharedSizeBytes);
     };
-#define TAKE_TM(tm)                                                             \
-    take(reinterpret_cast<const void *>(&k_closest<kNumMatTypes, tm>));         \
-    take(reinterpret_cast<const void *>(&k_closest<1, tm>));                    \
-    take(reinterpret_cast<const void *>(&k_shadow<tm>));                        \
-    take(reinterpret_cast<const void *>(&k_intersect_batch<tm>));
+#define TAKE_TM(TM)                                                             \
+    if (tm == TM) {                                                             \
+        take(reinterpret_cast<const void *>(&k_closest<kNumMatTypes, TM>));     \
+        take(reinterpret_cast<const void *>(&k_closest<1, TM>));                \
+        take(reinterpret_cast<const void *>(&k_shadow<TM>));                    \
+        take(reinterpret_cast<const void *>(&k_intersect_batch<TM>));           \
+    }
     TAKE_TM(kTravLds) TAKE_TM(kTravWide) TAKE_TM(kTravQuant)
 #undef TAKE_TM
     return m;

@@ -108,7 +108,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
     "pbrt_debug_named_spectrum", "pbrt_debug_bxdf", "pbrt_debug_layered", "pbrt_debug_triangle_shading", "pbrt_film_write_image",
     "pbrt_image_read_size", "pbrt_image_read", "pbrt_image_write", "pbrt_image_error", "pbrt_debug_filter_sample",
-    "pbrt_debug_bvh_stats", "pbrt_set_kernel_profiling", "pbrt_get_kernel_stats",
+    "pbrt_debug_bvh_stats", "pbrt_debug_light_bvh", "pbrt_set_kernel_profiling", "pbrt_get_kernel_stats",
 ]
 
 _LIB = None
@@ -150,6 +150,8 @@ def _lib():
     lib.pbrt_intersect.argtypes = [c.c_void_p, c.c_void_p, c.c_int, c.c_int, c.c_void_p, c.c_void_p]
     lib.pbrt_debug_bvh_stats.argtypes = [c.c_void_p, c.c_void_p]
     lib.pbrt_set_kernel_profiling.argtypes = [c.c_void_p, c.c_int]
+    lib.pbrt_debug_light_bvh.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_void_p, c.c_void_p, c.c_int,
+                                         c.POINTER(c.c_int)]
     lib.pbrt_get_kernel_stats.argtypes = [c.c_void_p, c.c_void_p, c.c_int, c.POINTER(c.c_int)]
     lib.pbrt_debug_halton.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_int]
     lib.pbrt_debug_halton.restype = c.c_float
@@ -178,6 +180,21 @@ def _f32(a, n=None):
     if n is not None and a.size != n:
         raise PbrtError(f"expected {n} values, got {a.size}")
     return a
+
+
+def debug_light_bvh(lights13):
+    """The loader's light-BVH build over [n][13] LightBounds rows -> (nodes [m][12] decoded bounds,
+    info [m][3] childOrLight / isLeaf / twoSided, trails [n] uint32)."""
+    lights13 = np.ascontiguousarray(lights13, dtype=np.float32).reshape(-1, 13)
+    n = len(lights13)
+    m = ctypes.c_int(0)
+    _check(_lib().pbrt_debug_light_bvh(lights13.ctypes.data, n, None, None, None, 0, ctypes.byref(m)))
+    nodes = np.zeros((max(m.value, 1), 12), np.float32)
+    info = np.zeros((max(m.value, 1), 3), np.int32)
+    trails = np.zeros(max(n, 1), np.uint32)
+    _check(_lib().pbrt_debug_light_bvh(lights13.ctypes.data, n, nodes.ctypes.data, info.ctypes.data,
+                                       trails.ctypes.data, m.value, ctypes.byref(m)))
+    return nodes[:m.value], info[:m.value], trails[:n]
 
 
 def debug_trowbridge(in13):

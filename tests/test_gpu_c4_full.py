@@ -1,6 +1,6 @@
 """BASELINE configs[3] geometry at full size on the GPU: the default C4 scene (scenes/gen_c4.py:
-122 copied displaced icospheres from PLY files, 9,994,244 triangles), whose BVH8 (2.6 M nodes,
-650 MB wide / 205 MB quantised) is HBM-resident with only the top of the tree in LDS.
+122 copied displaced icospheres from PLY files, 9,994,244 triangles), whose BVH8 (3.2 M nodes,
+810 MB wide / 253 MB quantised) is HBM-resident with only the top of the tree in LDS.
 
 * ``pbrt_intersect`` (WavefrontAggregate::IntersectClosest / IntersectShadow, the contract of
   cpu/aggregates.cpp:529-624 and shapes.cpp:172-273) against the oracle's independent binary

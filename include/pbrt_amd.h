@@ -14,9 +14,9 @@
  *   pbrt_render
  *       WavefrontPathIntegrator::Render (wavefront/integrator.cpp:290-493) restricted to a
  *       set of film rows and a range of sample indices; asynchronous on the context stream.
- *   pbrt_intersect
- *       WavefrontAggregate::IntersectClosest / IntersectShadow (wavefront/integrator.h:32-54)
- *       over caller-owned device SoA ray buffers.
+ *   pbrt_intersect / pbrt_intersect_tr
+ *       WavefrontAggregate::IntersectClosest / IntersectShadow / IntersectShadowTr
+ *       (wavefront/integrator.h:32-54) over caller-owned device SoA ray buffers.
  *   pbrt_film_*
  *       RGBFilm pixel storage (film.h:305-310), GetPixelRGB (film.h:261-277) and
  *       RGBFilm::WriteImage (film.cpp) to EXR / PFM / PNG.
@@ -218,6 +218,17 @@ int pbrt_image_error(const float *image, const float *reference, int width, int 
  * Asynchronous on the context stream (no host round trip): the results are valid after
  * pbrt_synchronize, or for work the caller orders after the context stream. */
 int pbrt_intersect(pbrt_context *ctx, const float *rays_dev, int n, int any_hit, int32_t *prim_dev, float *hit_dev);
+/* WavefrontAggregate::IntersectShadowTr (wavefront/integrator.h:49-51; TraceTransmittance,
+ * wavefront/intersect.h:164-274) over device SoA buffers: rays_dev [7][n] (o, d, tMax: the light
+ * point is o + tMax d), medium_dev [n] the medium each ray starts in (NULL or -1: vacuum; indices
+ * of the scene's media), lambda0_dev [n] the path's first wavelength (the other 30 follow
+ * SampleUniform's 10 nm stratification, as every SampledWavelengths of this wavefront); out_dev
+ * [3][31][n] receives T_ray, r_u, r_l after ratio tracking through every medium and interface
+ * up to the light (T_ray = 0 when an opaque surface blocks the ray; RNG seeded as pbrt's,
+ * Hash(ray.o), Hash(ray.d)).  The caller applies intersect.h:262-266: Ld *= T_ray /
+ * avg(sr.r_u * r_u + sr.r_l * r_l).  Asynchronous on the context stream. */
+int pbrt_intersect_tr(pbrt_context *ctx, const float *rays_dev, const int32_t *medium_dev, const float *lambda0_dev,
+                      int n, float *out_dev);
 
 /* host-side evaluation of product components (no GPU): used by golden-vector tests */
 float pbrt_debug_halton(const pbrt_scene *scene, int px, int py, int sample_index, int dim);

@@ -2421,6 +2421,62 @@ struct Renderer {
     PixelFilter filt;
     const pbrt_scene_flat *f;
 
+    // TraceTransmittance (wavefront/intersect.h:164-274) up to the light point o + tMax d:
+    // closest hits; a non-interface surface blocks (T_ray = 0); interfaces are crossed with
+    // SpawnRayTo(pLight); ratio tracking with RR in every medium.  RNG(Hash(o), Hash(d)).
+    void TraceTransmittance(Vec o, Vec d, Float tMax, int med, const Wavelengths &lambda, Spectrum *Tout,
+                            Spectrum *tuOut, Spectrum *tlOut) const {
+        const Vec pLight = o + d * tMax;
+        PCG32 rng(HashFloats(o.x, o.y, o.z), HashFloats(d.x, d.y, d.z));
+        Spectrum T_ray(1.f), tu(1.f), tl(1.f);
+        while (d != Vec(0, 0, 0)) {
+            TriIsect ti;
+            int hp = S.Intersect(o, d, tMax, &ti, false);
+            if (hp >= 0 && f->material_type[f->tri_material[hp]] != 3) {
+                T_ray = Spectrum(0.f);
+                break;
+            }
+            Interaction hsi;
+            if (hp >= 0)
+                hsi = TriangleInteraction(S.P(hp, 0), S.P(hp, 1), S.P(hp, 2), f->tri_flip[hp], ti, d, S.Attr(hp));
+            if (med >= 0) {
+                Float tEnd = hp < 0 ? tMax : (Length(o - hsi.p) / Length(d));
+                Spectrum T_maj = SampleTmaj(M, med, o, d, tEnd, rng.Uniform(), rng, lambda,
+                                            [&](Vec, const MediumProps &mp, const Spectrum &sigma_maj, const Spectrum &Tm) {
+                    Spectrum sigma_n = ClampZero(sigma_maj - mp.sigma_a - mp.sigma_s);
+                    Float pr = Tm[0] * sigma_maj[0];
+                    T_ray = T_ray * (Tm * sigma_n / pr);
+                    tl = tl * (Tm * sigma_maj / pr);
+                    tu = tu * (Tm * sigma_n / pr);
+                    Spectrum Tr = T_ray / (tl + tu).Average();
+                    if (Tr.Max() < 0.05f) {
+                        Float q = 0.75f;
+                        if (rng.Uniform() < q) T_ray = Spectrum(0.f);
+                        else T_ray = T_ray / (1 - q);
+                    }
+                    return bool(T_ray);
+                });
+                T_ray = T_ray * (T_maj / T_maj[0]);
+                tl = tl * (T_maj / T_maj[0]);
+                tu = tu * (T_maj / T_maj[0]);
+            }
+            if (hp < 0 || !T_ray) break;
+            // SurfaceInteraction::SpawnRayTo(pLight) (interaction.h, ray.h:98-104)
+            int mi = med, mo = med;
+            if (f->n_media > 0 && f->tri_medium && f->tri_medium[2 * hp] != f->tri_medium[2 * hp + 1]) {
+                mi = f->tri_medium[2 * hp];
+                mo = f->tri_medium[2 * hp + 1];
+            }
+            Vec dd = pLight - hsi.p;
+            o = OffsetRayOrigin(hsi.p, hsi.err, hsi.n, dd);
+            d = pLight - hsi.p;
+            med = DotN(hsi.n, d) > 0 ? mo : mi;
+        }
+        *Tout = T_ray;
+        *tuOut = tu;
+        *tlOut = tl;
+    }
+
     Vec Xf(const float *m, Vec p, bool point) const {
         Float x = m[0] * p.x + m[1] * p.y + m[2] * p.z, y = m[4] * p.x + m[5] * p.y + m[6] * p.z,
               z = m[8] * p.x + m[9] * p.y + m[10] * p.z;
@@ -2545,50 +2601,8 @@ struct Renderer {
                 if (S.Intersect(o, d, 1 - ShadowEpsilon, &dummy, true) < 0) L = L + Ld / (ru + rl).Average();
                 return;
             }
-            const Float tMax = 1 - ShadowEpsilon;
-            const Vec pLight = o + d * tMax;
-            PCG32 rng(HashFloats(o.x, o.y, o.z), HashFloats(d.x, d.y, d.z));
-            Spectrum T_ray(1.f), tu(1.f), tl(1.f);
-            while (d != Vec(0, 0, 0)) {
-                TriIsect ti;
-                int hp = S.Intersect(o, d, tMax, &ti, false);
-                if (hp >= 0 && !isInterface(hp)) {
-                    T_ray = Spectrum(0.f);
-                    break;
-                }
-                Interaction hsi;
-                if (hp >= 0)
-                    hsi = TriangleInteraction(S.P(hp, 0), S.P(hp, 1), S.P(hp, 2), f->tri_flip[hp], ti, d, S.Attr(hp));
-                if (med >= 0) {
-                    Float tEnd = hp < 0 ? tMax : (Length(o - hsi.p) / Length(d));
-                    Spectrum T_maj = SampleTmaj(M, med, o, d, tEnd, rng.Uniform(), rng, lambda,
-                                                [&](Vec, const MediumProps &mp, const Spectrum &sigma_maj, const Spectrum &Tm) {
-                        Spectrum sigma_n = ClampZero(sigma_maj - mp.sigma_a - mp.sigma_s);
-                        Float pr = Tm[0] * sigma_maj[0];
-                        T_ray = T_ray * (Tm * sigma_n / pr);
-                        tl = tl * (Tm * sigma_maj / pr);
-                        tu = tu * (Tm * sigma_n / pr);
-                        Spectrum Tr = T_ray / (tl + tu).Average();
-                        if (Tr.Max() < 0.05f) {
-                            Float q = 0.75f;
-                            if (rng.Uniform() < q) T_ray = Spectrum(0.f);
-                            else T_ray = T_ray / (1 - q);
-                        }
-                        return bool(T_ray);
-                    });
-                    T_ray = T_ray * (T_maj / T_maj[0]);
-                    tl = tl * (T_maj / T_maj[0]);
-                    tu = tu * (T_maj / T_maj[0]);
-                }
-                if (hp < 0 || !T_ray) break;
-                // SurfaceInteraction::SpawnRayTo(pLight) (interaction.h, ray.h:98-104)
-                int mi, mo;
-                mediaOf(hp, med, &mi, &mo);
-                Vec dd = pLight - hsi.p;
-                o = OffsetRayOrigin(hsi.p, hsi.err, hsi.n, dd);
-                d = pLight - hsi.p;
-                med = DotN(hsi.n, d) > 0 ? mo : mi;
-            }
+            Spectrum T_ray, tu, tl;
+            TraceTransmittance(o, d, 1 - ShadowEpsilon, med, lambda, &T_ray, &tu, &tl);
             if (T_ray) L = L + Ld * T_ray / (ru * tu + rl * tl).Average();
         };
         for (int wf = 0;; ++wf) {
@@ -2978,6 +2992,42 @@ void oracle_filter_sample(int type, float rx, float ry, float a, float b, float 
     f.Init(type, rx, ry, a, b);
     f.Sample(u0, u1, &out4[0], &out4[1], &out4[2]);
     out4[3] = f.Evaluate(px, py);
+}
+
+// IntersectShadowTr over a batch (the counterpart of pbrt_intersect_tr): rays [7][n], medium
+// [n] (-1 vacuum), lambda0 [n] -> out [3][31][n] T_ray, r_u, r_l
+int oracle_intersect_tr(const pbrt_scene_flat *flat, const pbrt_scene_info *info, const float *rays,
+                        const int32_t *medium, const float *lambda0, int n, float *out) {
+    Renderer r;
+    r.f = flat;
+    r.S.Init(flat, info);
+    r.M.f = flat;
+    r.M.n = flat->n_media;
+    const int nt = std::max(1, std::min<int>(16, (int)std::thread::hardware_concurrency()));
+    std::vector<std::thread> pool;
+    for (int w = 0; w < nt; ++w)
+        pool.emplace_back([&, w] {
+            for (int i = w; i < n; i += nt) {
+                Wavelengths lam = Wavelengths::SampleUniform(0.f);
+                lam.lambda[0] = lambda0[i];
+                for (int k = 1; k < NS; ++k) {
+                    lam.lambda[k] = lam.lambda[k - 1] + (LambdaMax - LambdaMin) / NS;
+                    if (lam.lambda[k] > LambdaMax) lam.lambda[k] = LambdaMin + (lam.lambda[k] - LambdaMax);
+                }
+                Spectrum T, tu, tl;
+                const int med = medium && medium[i] >= 0 && medium[i] < flat->n_media ? medium[i] : -1;
+                r.TraceTransmittance(Vec(rays[i], rays[n + i], rays[2 * n + i]),
+                                     Vec(rays[3 * n + i], rays[4 * n + i], rays[5 * n + i]), rays[6 * n + i], med, lam,
+                                     &T, &tu, &tl);
+                for (int k = 0; k < NS; ++k) {
+                    out[(size_t)k * n + i] = T[k];
+                    out[(size_t)(NS + k) * n + i] = tu[k];
+                    out[(size_t)(2 * NS + k) * n + i] = tl[k];
+                }
+            }
+        });
+    for (auto &t : pool) t.join();
+    return 0;
 }
 
 // Renders rows x [first_sample, first_sample + n_samples) into film[4][yres*xres]

@@ -46,6 +46,7 @@ def lib():
                                        ctypes.c_int, vp]
         _lib.oracle_set_cr_math.argtypes = [ctypes.c_int]
         _lib.oracle_light_bvh.argtypes = [vp, vp, ctypes.c_int, vp, vp, vp, ctypes.c_int]
+        _lib.oracle_intersect_tr.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int, vp]
     return _lib
 
 
@@ -96,6 +97,21 @@ def intersect(scene, rays, any_hit=False):
                                  int(any_hit), prim.ctypes.data_as(ctypes.c_void_p),
                                  hit.ctypes.data_as(ctypes.c_void_p))
     return prim, hit
+
+
+def intersect_tr(scene, rays, medium, lambda0):
+    """TraceTransmittance per ray (see pbrt_intersect_tr): rays float32 [7, n], medium int32 [n],
+    lambda0 float32 [n] -> float32 [3, 31, n] (T_ray, r_u, r_l)."""
+    info = scene.info
+    flat = scene.flat()
+    rays = np.ascontiguousarray(rays, dtype=np.float32)
+    medium = np.ascontiguousarray(medium, dtype=np.int32)
+    lambda0 = np.ascontiguousarray(lambda0, dtype=np.float32)
+    n = rays.shape[1]
+    out = np.zeros((3, 31, n), np.float32)
+    lib().oracle_intersect_tr(ctypes.byref(flat), ctypes.byref(info), rays.ctypes.data, medium.ctypes.data,
+                              lambda0.ctypes.data, n, out.ctypes.data)
+    return out
 
 
 def film_to_rgb(film, m3x3):

@@ -36,6 +36,8 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
                               hipStream_t s);
 hipError_t LaunchIntersectBatch(const DeviceScene &S, const float *rays, int n, int anyHit, int *outPrim,
                                 float *outHit, hipStream_t s);
+hipError_t LaunchIntersectTr(const DeviceScene &S, const float *rays, const int *medium, const float *lambda0, int n,
+                             float *out, hipStream_t s);
 size_t SurfaceTraversalStaticLds(int tm);
 int TraversalBlocksCompiled(int compressed);
 size_t VolTraversalStaticLds(int tm);
@@ -1500,6 +1502,20 @@ int pbrt_intersect(pbrt_context *ctx, const float *rays, int n, int anyHit, int3
         if ((int64_t)n * 7 > INT32_MAX) return Fail("ray batch too large");
         // asynchronous on the context stream; the kernel writes the scene's triangle numbering
         HIPCHECK(LaunchIntersectBatch(ctx->S, rays, n, anyHit, prim, hit, ctx->stream));
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_intersect_tr(pbrt_context *ctx, const float *rays, const int32_t *medium, const float *lambda0, int n,
+                      float *out) {
+    try {
+        if (!ctx || n < 0 || (n > 0 && (!rays || !lambda0 || !out))) return Fail("bad arguments");
+        if (n == 0) return 0;
+        if ((int64_t)n * 93 > INT32_MAX) return Fail("ray batch too large");
+        HIPCHECK(hipSetDevice(ctx->device));
+        HIPCHECK(LaunchIntersectTr(ctx->S, rays, medium, lambda0, n, out, ctx->stream));
         return 0;
     } catch (const std::exception &e) {
         return Fail(e.what());

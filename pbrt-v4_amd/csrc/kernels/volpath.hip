@@ -1902,9 +1902,89 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vscatter(DeviceScene
     }
 }
 
-// TraceTransmittance (wavefront/intersect.h:164-274): closest hits up to the light; a
-// non-interface surface blocks, interfaces are crossed (SpawnRayTo the light point), and in
-// each medium T_ray / r_u / r_l follow ratio tracking with RR on a small T_ray.
+// TraceTransmittance (wavefront/intersect.h:164-274) for one shadow ray: closest hits up to the
+// light point ray(tMax); a non-interface surface blocks (returns false), interfaces are crossed
+// (SpawnRayTo the light point), and in each medium T_ray / r_u / r_l follow ratio tracking with
+// RR on a small T_ray.  Tr, tu, tl start at 1 (the caller's arrays).
+template <int TM>
+__device__ __forceinline__ bool TraceTransmittanceRay(const DeviceScene &S, const SceneLds &L, V3 o, V3 d, float tMax,
+                                                      int med, const WaveOffsets &wo, float *Tr, float *tu, float *tl) {
+    const V3 pLight = o + d * tMax;
+    PCG32 rng(HashV3(o), HashV3(d));
+    float Tm[kNS];
+    for (int guard = 0; guard < 256; ++guard) {
+        if (d == V3(0, 0, 0)) break;
+        TriHit h;
+        const int hp = Traverse<false, TM>(S, L, o, d, tMax, &h);
+        if (hp >= 0 && S.matType[S.primMaterial[hp]] != 3) return false;
+        TriSurface hs{};
+        if (hp >= 0) {
+            V3 p0, p1, p2;
+            PrimVerts(S, hp, &p0, &p1, &p2);
+            hs = SurfaceAt(S, hp, p0, p1, p2, h.b0, h.b1, h.b2);
+        }
+        if (med >= 0) {
+            const MediumRef m = MediumAt(S, med);
+            const int sa = m.I[1], ss = m.I[2];
+            const float tEnd = hp < 0 ? tMax : (Length(o - hs.p) / Length(d));
+            auto event = [&](V3, const MediumPoint &mp, float mx, const float *T) __attribute__((always_inline)) -> bool {
+                float sn[kNS], smj[kNS];
+#pragma unroll
+                for (int i = 0; i < kNS; ++i) {
+                    smj[i] = (DenseAt(S, sa, wo.off[i]) + DenseAt(S, ss, wo.off[i])) * mx;
+                    sn[i] = fmaxf(0.f, smj[i] - DenseAt(S, sa, wo.off[i]) * mp.d - DenseAt(S, ss, wo.off[i]) * mp.d);
+                }
+                const float pr = T[0] * smj[0];
+#pragma unroll
+                for (int i = 0; i < kNS; ++i) {
+                    Tr[i] *= T[i] * sn[i] / pr;
+                    tl[i] *= T[i] * smj[i] / pr;
+                    tu[i] *= T[i] * sn[i] / pr;
+                }
+                // T_ray / (r_l + r_u).Average() < 0.05: Russian roulette
+                float den[kNS];
+#pragma unroll
+                for (int i = 0; i < kNS; ++i) den[i] = tl[i] + tu[i];
+                const float avg = AvgArr(den);
+                float mxT = -kInfinity;
+#pragma unroll
+                for (int i = 0; i < kNS; ++i) mxT = fmaxf(mxT, Tr[i] / avg);
+                if (mxT < 0.05f) {
+                    const float q = 0.75f;
+                    if (rng.Uniform() < q) {
+#pragma unroll
+                        for (int i = 0; i < kNS; ++i) Tr[i] = 0.f;
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < kNS; ++i) Tr[i] /= 1 - q;
+                    }
+                }
+                return AnyNonZero(Tr);
+            };
+            const bool ranOut = SampleTmaj(S, m, wo, o, d, tEnd, rng.Uniform(), rng, Tm, event);
+            if (ranOut) {
+                const float t0 = Tm[0];
+#pragma unroll
+                for (int i = 0; i < kNS; ++i) {
+                    const float f = Tm[i] / t0;
+                    Tr[i] *= f;
+                    tl[i] *= f;
+                    tu[i] *= f;
+                }
+            }
+        }
+        if (hp < 0 || !AnyNonZero(Tr)) break;
+        // SurfaceInteraction::SpawnRayTo(pLight) (interaction.h, ray.h:98-104)
+        int mIn, mOut;
+        MediaOf(S, hp, med, &mIn, &mOut);
+        const V3 dd = pLight - hs.p;
+        o = OffsetRayOrigin(hs.p, hs.pErr, hs.n, dd);
+        d = dd;
+        med = DotN(hs.n, d) > 0 ? mOut : mIn;
+    }
+    return true;
+}
+
 template <int TM>
 __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vshadow(DeviceScene S, PathState st, VolState v, int wf) {
     const QueueView sh = LoadQueue(st, wf, kVShadow);
@@ -1915,90 +1995,13 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vshadow(DeviceScene 
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&st.stats[2], (unsigned long long)sh.total);
     for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < sh.total; j += gridDim.x * blockDim.x) {
         const int p = QueueSlot(sh, j);
-        V3 o = LoadV3(v.shRay, NR, p), d = LoadV3(v.shRay + 3 * (size_t)NR, NR, p);
-        int med = v.shMedium[p];
+        const V3 o = LoadV3(v.shRay, NR, p), d = LoadV3(v.shRay + 3 * (size_t)NR, NR, p);
         const WaveOffsets wo(v.shLambda0[p]);
-        const float tMax = 1 - kShadowEpsilon;
-        const V3 pLight = o + d * tMax;
-        PCG32 rng(HashV3(o), HashV3(d));
-        float Tr[kNS], tu[kNS], tl[kNS], Tm[kNS];
+        float Tr[kNS], tu[kNS], tl[kNS];
 #pragma unroll
         for (int i = 0; i < kNS; ++i) Tr[i] = tu[i] = tl[i] = 1.f;
-        bool blocked = false;
-        for (int guard = 0; guard < 256; ++guard) {
-            if (d == V3(0, 0, 0)) break;
-            TriHit h;
-            const int hp = Traverse<false, TM>(S, L, o, d, tMax, &h);
-            if (hp >= 0 && S.matType[S.primMaterial[hp]] != 3) {
-                blocked = true;
-                break;
-            }
-            TriSurface hs{};
-            if (hp >= 0) {
-                V3 p0, p1, p2;
-                PrimVerts(S, hp, &p0, &p1, &p2);
-                hs = SurfaceAt(S, hp, p0, p1, p2, h.b0, h.b1, h.b2);
-            }
-            if (med >= 0) {
-                const MediumRef m = MediumAt(S, med);
-                const int sa = m.I[1], ss = m.I[2];
-                const float tEnd = hp < 0 ? tMax : (Length(o - hs.p) / Length(d));
-                auto event = [&](V3, const MediumPoint &mp, float mx, const float *T) __attribute__((always_inline)) -> bool {
-                    float sn[kNS], smj[kNS];
-#pragma unroll
-                    for (int i = 0; i < kNS; ++i) {
-                        smj[i] = (DenseAt(S, sa, wo.off[i]) + DenseAt(S, ss, wo.off[i])) * mx;
-                        sn[i] = fmaxf(0.f, smj[i] - DenseAt(S, sa, wo.off[i]) * mp.d - DenseAt(S, ss, wo.off[i]) * mp.d);
-                    }
-                    const float pr = T[0] * smj[0];
-#pragma unroll
-                    for (int i = 0; i < kNS; ++i) {
-                        Tr[i] *= T[i] * sn[i] / pr;
-                        tl[i] *= T[i] * smj[i] / pr;
-                        tu[i] *= T[i] * sn[i] / pr;
-                    }
-                    // T_ray / (r_l + r_u).Average() < 0.05: Russian roulette
-                    float den[kNS];
-#pragma unroll
-                    for (int i = 0; i < kNS; ++i) den[i] = tl[i] + tu[i];
-                    const float avg = AvgArr(den);
-                    float mxT = -kInfinity;
-#pragma unroll
-                    for (int i = 0; i < kNS; ++i) mxT = fmaxf(mxT, Tr[i] / avg);
-                    if (mxT < 0.05f) {
-                        const float q = 0.75f;
-                        if (rng.Uniform() < q) {
-#pragma unroll
-                            for (int i = 0; i < kNS; ++i) Tr[i] = 0.f;
-                        } else {
-#pragma unroll
-                            for (int i = 0; i < kNS; ++i) Tr[i] /= 1 - q;
-                        }
-                    }
-                    return AnyNonZero(Tr);
-                };
-                const bool ranOut = SampleTmaj(S, m, wo, o, d, tEnd, rng.Uniform(), rng, Tm, event);
-                if (ranOut) {
-                    const float t0 = Tm[0];
-#pragma unroll
-                    for (int i = 0; i < kNS; ++i) {
-                        const float f = Tm[i] / t0;
-                        Tr[i] *= f;
-                        tl[i] *= f;
-                        tu[i] *= f;
-                    }
-                }
-            }
-            if (hp < 0 || !AnyNonZero(Tr)) break;
-            // SurfaceInteraction::SpawnRayTo(pLight) (interaction.h, ray.h:98-104)
-            int mIn, mOut;
-            MediaOf(S, hp, med, &mIn, &mOut);
-            const V3 dd = pLight - hs.p;
-            o = OffsetRayOrigin(hs.p, hs.pErr, hs.n, dd);
-            d = dd;
-            med = DotN(hs.n, d) > 0 ? mOut : mIn;
-        }
-        if (blocked || !AnyNonZero(Tr)) continue;
+        if (!TraceTransmittanceRay<TM>(S, L, o, d, 1 - kShadowEpsilon, v.shMedium[p], wo, Tr, tu, tl) || !AnyNonZero(Tr))
+            continue;
         float Ld[kNS], den[kNS];
         const int shf = v.shFlags[p];
         {
@@ -2011,6 +2014,35 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vshadow(DeviceScene 
         LoadSpec(v.shLd, NR, p, Ld, shf & kShUniLd);
         const float avg = AvgArr(den);
         AddToL(S, st, v.shPixel[p], wo, [&](int i) { return Ld[i] * Tr[i] / avg; });
+    }
+}
+
+// WavefrontAggregate::IntersectShadowTr (wavefront/integrator.h:49-51) over a caller's SoA batch:
+// rays [7][n] o, d, tMax; the ray's medium (-1: none) and the path's first wavelength (the
+// other 30 by SampleUniform's +10 nm stratification, as every SampledWavelengths of this
+// wavefront); out [3][31][n] = T_ray, r_u, r_l of TraceTransmittance after the ray reached the
+// light point (T_ray all 0 when a surface blocks it).  The caller scales its Ld by
+// T_ray / avg(sr.r_u * r_u + sr.r_l * r_l) (intersect.h:262-266).
+template <int TM>
+__global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_intersect_tr(DeviceScene S, const float *rays, const int *medium,
+                                                                      const float *lambda0, int n, float *out) {
+    extern __shared__ float4 dynLds[];
+    const SceneLds L = SetupSceneLds(S, dynLds);
+    for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x) {
+        const V3 o(rays[r], rays[n + r], rays[2 * n + r]), d(rays[3 * n + r], rays[4 * n + r], rays[5 * n + r]);
+        const WaveOffsets wo(lambda0[r]);
+        float Tr[kNS], tu[kNS], tl[kNS];
+#pragma unroll
+        for (int i = 0; i < kNS; ++i) Tr[i] = tu[i] = tl[i] = 1.f;
+        int med = medium ? medium[r] : -1;
+        med = med >= 0 && med < S.media.n ? med : -1;  // outside the scene's media: vacuum
+        if (!TraceTransmittanceRay<TM>(S, L, o, d, rays[6 * n + r], med, wo, Tr, tu, tl))
+            for (int i = 0; i < kNS; ++i) Tr[i] = 0.f;
+        for (int i = 0; i < kNS; ++i) {
+            out[(size_t)i * n + r] = Tr[i];
+            out[(size_t)(kNS + i) * n + r] = tu[i];
+            out[(size_t)(2 * kNS + i) * n + r] = tl[i];
+        }
     }
 }
 
@@ -2143,6 +2175,15 @@ static int VolGrid(int n, int cap) {
     int g = (n + kBlock - 1) / kBlock;
     g = g < 1 ? 1 : (g > cap ? cap : g);
     return (g + kShards - 1) / kShards * kShards;  // producer grids: multiples of kShards
+}
+
+hipError_t LaunchIntersectTr(const DeviceScene &S, const float *rays, const int *medium, const float *lambda0, int n,
+                            float *out, hipStream_t s) {
+    const int g = std::max(1, std::min(4096, (n + kBlock - 1) / kBlock));
+#define K_TR(tm) k_intersect_tr<tm>
+    PBRT_LAUNCH_TRAVERSAL(S, K_TR, dim3(g), dim3(kBlock), VolStackBytes(S), s, S, rays, medium, lambda0, n, out);
+#undef K_TR
+    return hipGetLastError();
 }
 
 hipError_t LaunchVolCamera(const DeviceScene &S, const PathState &st, const VolState &v, int nActive, hipStream_t s) {

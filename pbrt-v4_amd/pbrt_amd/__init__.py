@@ -108,7 +108,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
     "pbrt_debug_named_spectrum", "pbrt_debug_bxdf", "pbrt_debug_layered", "pbrt_debug_triangle_shading", "pbrt_film_write_image",
     "pbrt_image_read_size", "pbrt_image_read", "pbrt_image_write", "pbrt_image_error", "pbrt_debug_filter_sample",
-    "pbrt_debug_bvh_stats", "pbrt_debug_light_bvh", "pbrt_set_kernel_profiling", "pbrt_get_kernel_stats",
+    "pbrt_debug_bvh_stats", "pbrt_debug_light_bvh", "pbrt_intersect_tr", "pbrt_set_kernel_profiling", "pbrt_get_kernel_stats",
 ]
 
 _LIB = None
@@ -149,6 +149,7 @@ def _lib():
     lib.pbrt_film_get_rgb.argtypes = [c.c_void_p, c.c_void_p]
     lib.pbrt_intersect.argtypes = [c.c_void_p, c.c_void_p, c.c_int, c.c_int, c.c_void_p, c.c_void_p]
     lib.pbrt_debug_bvh_stats.argtypes = [c.c_void_p, c.c_void_p]
+    lib.pbrt_intersect_tr.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_set_kernel_profiling.argtypes = [c.c_void_p, c.c_int]
     lib.pbrt_debug_light_bvh.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_void_p, c.c_void_p, c.c_int,
                                          c.POINTER(c.c_int)]
@@ -486,6 +487,27 @@ class HIPAggregate:
 
     def IntersectShadow(self, rays):
         return self._run(rays, True)
+
+    def IntersectShadowTr(self, rays, medium, lambda0):
+        """TraceTransmittance (wavefront/intersect.h:164-274) per ray: rays [7, n] float32, medium
+        [n] int32 (-1 vacuum), lambda0 [n] float32 device tensors -> (T_ray, r_u, r_l), each
+        [31, n] float32."""
+        import torch
+        if not (rays.is_cuda and rays.dtype == torch.float32 and rays.dim() == 2 and rays.shape[0] == 7):
+            raise PbrtError("rays must be a float32 device tensor of shape [7, n]")
+        n = rays.shape[1]
+        rays = rays.contiguous()
+        medium = medium.to(device=rays.device, dtype=torch.int32).contiguous()
+        lambda0 = lambda0.to(device=rays.device, dtype=torch.float32).contiguous()
+        if medium.numel() != n or lambda0.numel() != n:
+            raise PbrtError("medium and lambda0 need one entry per ray")
+        out = torch.empty((3, 31, n), dtype=torch.float32, device=rays.device)
+        torch.cuda.synchronize(rays.device)
+        _check(_lib().pbrt_intersect_tr(self.integrator._h, ctypes.c_void_p(rays.data_ptr()),
+                                        ctypes.c_void_p(medium.data_ptr()), ctypes.c_void_p(lambda0.data_ptr()), n,
+                                        ctypes.c_void_p(out.data_ptr())))
+        self.integrator.synchronize()
+        return out[0], out[1], out[2]
 
 
 def RenderWavefront(scene_path, device=0, **overrides):

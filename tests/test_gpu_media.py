@@ -177,3 +177,42 @@ def test_c5_small_statistical_vs_libm_oracle(pa, oracle):
     same = (np.abs(gpu - ref) <= np.maximum(1e-3 * np.abs(ref), 1e-4)).all(axis=-1).mean()
     assert same >= 0.5, same
     print(f"C5 small vs libm oracle: mean diff {d} (sigma {sigma}), {same*100:.1f}% pixels within 1e-3")
+
+
+@pytest.mark.parametrize("kind", ["homogeneous", "grid"])
+def test_intersect_shadow_tr_matches_oracle(pa, oracle, kind):
+    """pbrt_intersect_tr (WavefrontAggregate::IntersectShadowTr, TraceTransmittance
+    intersect.h:164-274) on 20k shadow-style rays through the interface box and its medium,
+    some blocked by the opaque light quad: T_ray, r_u, r_l per wavelength against the oracle
+    (CR-math mode, as the media kernels)."""
+    import torch
+    m = {"homogeneous": HOMOG, "grid": grid_medium()}[kind]
+    sc = pa.Scene.from_string(medium_scene(m, res=16, spp=1, extra=LIGHT), SCENES)
+    f = sc.flat()
+    V = np.ctypeslib.as_array(f.vertices, shape=(f.n_vertices * 3,)).reshape(-1, 3)
+    T = np.ctypeslib.as_array(f.triangles, shape=(f.n_triangles * 3,)).reshape(-1, 3)
+    mt = np.ctypeslib.as_array(f.material_type, shape=(f.n_materials,))
+    tm = np.ctypeslib.as_array(f.tri_material, shape=(f.n_triangles,))
+    box = V[T[mt[tm] == 3].ravel()]
+    lo, hi = box.min(axis=0), box.max(axis=0)
+    rng = np.random.default_rng(9)
+    n = 20000
+    o = rng.uniform(lo - 1.5, hi + 1.5, (n, 3))
+    pl = rng.uniform(lo - 1.5, hi + [1.5, 3.5, 1.5], (n, 3))
+    inside = ((o > lo) & (o < hi)).all(axis=1)
+    medium = np.where(inside, 0, -1).astype(np.int32)
+    rays = np.concatenate([o.T, (pl - o).T, np.full((1, n), 1 - 1e-4)]).astype(np.float32)
+    lam = rng.uniform(395, 705, n).astype(np.float32)
+    integ = pa.WavefrontPathIntegrator(sc, max_paths=1 << 12)
+    agg = pa.HIPAggregate(integ)
+    g = torch.stack(agg.IntersectShadowTr(torch.from_numpy(rays).cuda(), torch.from_numpy(medium),
+                                          torch.from_numpy(lam))).cpu().numpy()
+    with oracle.cr_math():
+        ref = oracle.intersect_tr(sc, rays, medium, lam)
+    blocked_g, blocked_r = (g[0] == 0).all(axis=0), (ref[0] == 0).all(axis=0)
+    assert 0.05 < blocked_r.mean() < 0.95 and inside.mean() > 0.05
+    close = np.isclose(g, ref, rtol=1e-6, atol=0).all(axis=(0, 1))
+    assert (blocked_g == blocked_r).mean() >= 0.999
+    assert close.mean() >= 0.999, close.mean()
+    through = ~blocked_r & (medium >= 0)
+    assert through.sum() > 500 and (ref[0][:, through] < 1).any()  # the medium attenuates

@@ -205,13 +205,16 @@ int pbrt_film_write_image(pbrt_context *ctx, const char *path, int write_fp16);
 /* imgtool (cmd/imgtool.cpp:960-1105) image access and error metrics, host only.
  * pbrt_image_read_size then pbrt_image_read into a caller-owned [h][w][3] float buffer
  * (.pfm, uncompressed .exr).  pbrt_image_error: metric "MAE" (pbrt's signed mean
- * difference), "MSE" or "MRSE" per channel over [h][w][3] images (Image::MAE / MSE / MRSE,
- * util/image.cpp:543-639). */
+ * difference), "MSE", "MRSE" or "FLIP" per channel over [h][w][3] images (Image::MAE / MSE /
+ * MRSE, util/image.cpp:543-639; FLIP below). */
 int pbrt_image_read_size(const char *path, int *width, int *height);
 int pbrt_image_read(const char *path, float *rgb, int width, int height);
 int pbrt_image_write(const char *path, const float *rgb, int width, int height, int write_fp16);
 int pbrt_image_error(const float *image, const float *reference, int width, int height, const char *metric,
                      double *error3);
+/* FLIP error map [h][w] (imgtool --metric FLIP, cmd/imgtool.cpp:1224-1255 over src/ext/flip):
+ * inputs clamped to [0, 1]; "FLIP" in pbrt_image_error reports the map's mean per channel */
+int pbrt_image_flip(const float *image, const float *reference, int width, int height, float *error_map);
 
 /* WavefrontAggregate boundary: rays_dev = [7][n] SoA (o.xyz, d.xyz, tMax) on the device;
  * prim_dev [n] receives the original triangle index or -1; hit_dev [4][n] b0 b1 b2 t.

@@ -1485,9 +1485,21 @@ int pbrt_image_error(const float *image, const float *reference, int width, int 
         if (m == "MAE") em = ErrorMetric::MAE;
         else if (m == "MSE") em = ErrorMetric::MSE;
         else if (m == "MRSE") em = ErrorMetric::MRSE;
-        else return Fail("--metric must be \"MAE\", \"MSE\", or \"MRSE\" (FLIP is not provided)");
+        else if (m == "FLIP") em = ErrorMetric::FLIP;
+        else return Fail("--metric must be \"MAE\", \"MSE\", \"MRSE\", or \"FLIP\"");
         const auto e = ImageError(image, reference, width, height, em);
         for (int c = 0; c < 3; ++c) error3[c] = e[c];
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_image_flip(const float *image, const float *reference, int width, int height, float *error_map) {
+    try {
+        if (!image || !reference || !error_map || width <= 0 || height <= 0) return Fail("bad arguments");
+        const std::vector<float> m = FlipErrorMap(image, reference, width, height);
+        std::copy(m.begin(), m.end(), error_map);
         return 0;
     } catch (const std::exception &e) {
         return Fail(e.what());

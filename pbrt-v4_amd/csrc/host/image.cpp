@@ -13,6 +13,7 @@
 //   metrics  Image::MAE / MSE / MRSE (util/image.cpp:543-639) as imgtool diff/error call them
 //        (cmd/imgtool.cpp:960-1105): per channel, double sums over pixels / (x res * y res);
 //        MAE is pbrt's signed mean difference; infinite terms are skipped.
+#include <algorithm>
 #include "image.h"
 
 #include <cmath>
@@ -450,6 +451,14 @@ Image ReadImage(const std::string &path) {
 }
 
 std::array<double, 3> ImageError(const float *img, const float *ref, int w, int h, ErrorMetric metric) {
+    if (metric == ErrorMetric::FLIP) {
+        // imgtool.cpp:1248-1255: every channel reports the map's mean
+        const std::vector<float> m = FlipErrorMap(img, ref, w, h);
+        float s = 0;
+        for (float v : m) s += v;
+        const double e = s / (w * h);
+        return {e, e, e};
+    }
     double sum[3] = {0, 0, 0};
     for (size_t i = 0; i < (size_t)w * h; ++i)
         for (int c = 0; c < 3; ++c) {
@@ -463,6 +472,158 @@ std::array<double, 3> ImageError(const float *img, const float *ref, int w, int 
         }
     const float denom = float(w) * float(h);
     return {sum[0] / denom, sum[1] / denom, sum[2] / denom};
+}
+
+// ---------------------------------------------------------------- FLIP
+// FLIP (Andersson, Nilsson, Akenine-Moller, Oskarsson, Astrom, Fairchild, "FLIP: A Difference
+// Evaluator for Alternating Images", HPG 2020), the LDR evaluator as pbrt's imgtool runs it
+// (cmd/imgtool.cpp:1224-1255: inputs clamped to [0, 1] and read as sRGB-encoded, FLIP's default
+// viewing conditions -- 0.7 m from a 0.7 m wide 3840-pixel monitor).  Colour pipeline: YCxCz
+// opponent space, contrast-sensitivity filters (sums of Gaussians per channel), back to linear
+// RGB clamped to the gamut, CIELab with the Hunt adjustment, HyAB distance redistributed into
+// [0, 1].  Feature pipeline: first / second Gaussian-derivative edge and point detectors on the
+// achromatic channel.  Per pixel: colour^(1 - feature).  Float arithmetic throughout, as the
+// published evaluator (pinned by tests/golden "flip", ComputeFLIPError of src/ext/flip).
+namespace {
+struct C3 {
+    float a = 0, b = 0, c = 0;
+};
+constexpr float kWhiteX = 0.950428545377181f, kWhiteY = 1.0f, kWhiteZ = 1.088900370798128f;
+C3 SrgbToXyz(C3 v) {
+    auto lin = [](float x) { return x <= 0.04045f ? x / 12.92f : powf((x + 0.055f) / 1.055f, 2.4f); };
+    v = {lin(v.a), lin(v.b), lin(v.c)};
+    return {(10135552.0f / 24577794.0f) * v.a + (8788810.0f / 24577794.0f) * v.b + (4435075.0f / 24577794.0f) * v.c,
+            (2613072.0f / 12288897.0f) * v.a + (8788810.0f / 12288897.0f) * v.b + (887015.0f / 12288897.0f) * v.c,
+            (1425312.0f / 73733382.0f) * v.a + (8788810.0f / 73733382.0f) * v.b + (70074185.0f / 73733382.0f) * v.c};
+}
+C3 LinearToXyz(C3 v) {
+    return {(10135552.0f / 24577794.0f) * v.a + (8788810.0f / 24577794.0f) * v.b + (4435075.0f / 24577794.0f) * v.c,
+            (2613072.0f / 12288897.0f) * v.a + (8788810.0f / 12288897.0f) * v.b + (887015.0f / 12288897.0f) * v.c,
+            (1425312.0f / 73733382.0f) * v.a + (8788810.0f / 73733382.0f) * v.b + (70074185.0f / 73733382.0f) * v.c};
+}
+C3 XyzToLinear(C3 v) {
+    return {3.241003232976358f * v.a + -1.537398969488785f * v.b + -0.498615881996363f * v.c,
+            -0.969224252202516f * v.a + 1.875929983695176f * v.b + 0.041554226340085f * v.c,
+            0.055639419851975f * v.a + -0.204011206123910f * v.b + 1.057148977187533f * v.c};
+}
+C3 XyzToYCxCz(C3 v) {
+    const float x = v.a / kWhiteX, y = v.b / kWhiteY, z = v.c / kWhiteZ;
+    return {116.0f * y - 16.0f, 500.0f * (x - y), 200.0f * (y - z)};
+}
+C3 YCxCzToXyz(C3 v) {
+    const float yy = (v.a + 16.0f) / 116.0f, cx = v.b / 500.0f, cz = v.c / 200.0f;
+    return {(yy + cx) * kWhiteX, yy * kWhiteY, (yy - cz) * kWhiteZ};
+}
+C3 XyzToLab(C3 v) {
+    auto f = [](float t) { return t > 0.008856 ? powf(t, 1.0f / 3.0f) : 7.787f * t + 16.0f / 116.0f; };
+    const float x = f(fabsf(v.a) / kWhiteX), y = f(fabsf(v.b) / kWhiteY), z = f(fabsf(v.c) / kWhiteZ);
+    return {116.0f * y - 16.0f, 500.0f * (x - y), 200.0f * (y - z)};
+}
+float HyABDist(C3 p, C3 q) { return fabsf(p.a - q.a) + sqrtf((p.b - q.b) * (p.b - q.b) + (p.c - q.c) * (p.c - q.c)); }
+C3 HuntAdjust(C3 lab) { return {lab.a, 0.01f * lab.a * lab.b, 0.01f * lab.a * lab.c}; }
+// 2D convolution with clamp-to-edge borders; kernel [k][k] (odd), three channels
+std::vector<C3> Convolve(const std::vector<C3> &img, int w, int h, const std::vector<C3> &ker, int k) {
+    std::vector<C3> out(img.size());
+    const int r = k / 2;
+    for (int y = 0; y < h; ++y)
+        for (int x = 0; x < w; ++x) {
+            C3 acc;
+            for (int dy = -r; dy <= r; ++dy) {
+                const int yy = std::min(std::max(0, y + dy), h - 1);
+                for (int dx = -r; dx <= r; ++dx) {
+                    const int xx = std::min(std::max(0, x + dx), w - 1);
+                    const C3 &kv = ker[(dy + r) * k + dx + r], &v = img[yy * w + xx];
+                    acc = {acc.a + kv.a * v.a, acc.b + kv.b * v.b, acc.c + kv.c * v.c};
+                }
+            }
+            out[y * w + x] = acc;
+        }
+    return out;
+}
+}  // namespace
+
+std::vector<float> FlipErrorMap(const float *test, const float *ref, int w, int h) {
+    const float pi = 3.14159265358979323846f;
+    const float ppd = 0.7f * (3840.0f / 0.7f) * (pi / 180.0f);
+    const size_t n = (size_t)w * h;
+    std::vector<C3> T(n), R(n);
+    for (size_t i = 0; i < n; ++i) {
+        auto cl = [](float v) { return std::min(std::max(v, 0.f), 1.f); };
+        T[i] = XyzToYCxCz(SrgbToXyz({cl(test[3 * i]), cl(test[3 * i + 1]), cl(test[3 * i + 2])}));
+        R[i] = XyzToYCxCz(SrgbToXyz({cl(ref[3 * i]), cl(ref[3 * i + 1]), cl(ref[3 * i + 2])}));
+    }
+    // contrast sensitivity: per channel a1 sqrt(pi/b1) exp(-pi^2 r^2 / b1) + a2 sqrt(pi/b2) exp(-pi^2 r^2 / b2)
+    const C3 A1{1.0f, 1.0f, 34.1f}, B1{0.0047f, 0.0053f, 0.04f}, A2{0.0f, 0.0f, 13.5f}, B2{1.0e-5f, 1.0e-5f, 0.025f};
+    const float pi2 = float(M_PI * M_PI);
+    const float bmax = std::max({B1.a, B1.b, B1.c, B2.a, B2.b, B2.c});
+    const int rad = int(std::ceil(3.0f * sqrtf(bmax / (2.0f * pi2)) * ppd)), kw = 2 * rad + 1;
+    std::vector<C3> csf(kw * kw);
+    C3 sum;
+    auto gs = [&](float r2, float a1, float b1, float a2, float b2) {
+        return a1 * sqrtf(pi / b1) * expf(-pi2 * r2 / b1) + a2 * sqrtf(pi / b2) * expf(-pi2 * r2 / b2);
+    };
+    for (int y = 0; y < kw; ++y)
+        for (int x = 0; x < kw; ++x) {
+            const float fx = (x - rad) * (1.0f / ppd), fy = (y - rad) * (1.0f / ppd), r2 = fx * fx + fy * fy;
+            const C3 v{gs(r2, A1.a, B1.a, A2.a, B2.a), gs(r2, A1.b, B1.b, A2.b, B2.b), gs(r2, A1.c, B1.c, A2.c, B2.c)};
+            csf[y * kw + x] = v;
+            sum = {sum.a + v.a, sum.b + v.b, sum.c + v.c};
+        }
+    for (C3 &v : csf) v = {v.a / sum.a, v.b / sum.b, v.c / sum.c};
+    auto toLab = [&](const std::vector<C3> &img) {
+        std::vector<C3> f = Convolve(img, w, h, csf, kw);
+        for (C3 &p : f) {
+            C3 l = XyzToLinear(YCxCzToXyz(p));
+            auto g = [](float v) { return std::max(std::min(v, 1.0f), 0.0f); };
+            p = HuntAdjust(XyzToLab(LinearToXyz({g(l.a), g(l.b), g(l.c)})));
+        }
+        return f;
+    };
+    const std::vector<C3> LT = toLab(T), LR = toLab(R);
+    const float qc = 0.7f, pc = 0.4f, pt = 0.95f;
+    const float cmax = powf(HyABDist(HuntAdjust(XyzToLab(LinearToXyz({0, 1, 0}))), HuntAdjust(XyzToLab(LinearToXyz({0, 0, 1})))), qc);
+    // feature detectors: Gaussian (std 0.5 w ppd, w = 0.082 deg) first derivative (edges) and
+    // second derivative (points), positive and negative weights each normalized to sum 1
+    const float sd = 0.5f * 0.082f * ppd;
+    const int fr = int(std::ceil(3.0f * sd)), fw = 2 * fr + 1;
+    auto detector = [&](bool point) {
+        std::vector<C3> k(fw * fw);
+        float px = 0, nx = 0, py = 0, ny = 0;
+        for (int y = 0; y < fw; ++y)
+            for (int x = 0; x < fw; ++x) {
+                const float xx = float(x - fr), yy = float(y - fr);
+                const float G = expf(-(xx * xx + yy * yy) / (2.0f * sd * sd));
+                const float wx = point ? (xx * xx / (sd * sd) - 1.0f) * G : -xx * G;
+                const float wy = point ? (yy * yy / (sd * sd) - 1.0f) * G : -yy * G;
+                k[y * fw + x] = {wx, wy, 0.f};
+                (wx > 0 ? px : nx) += wx > 0 ? wx : -wx;
+                (wy > 0 ? py : ny) += wy > 0 ? wy : -wy;
+            }
+        for (C3 &v : k) v = {v.a / (v.a > 0 ? px : nx), v.b / (v.b > 0 ? py : ny), 0.f};
+        return k;
+    };
+    const std::vector<C3> edgeK = detector(false), pointK = detector(true);
+    auto gray = [&](const std::vector<C3> &img) {
+        std::vector<C3> g(img.size());
+        for (size_t i = 0; i < img.size(); ++i) {
+            const float c = (img[i].a + 16.0f) / 116.0f;
+            g[i] = {c, c, 0.f};
+        }
+        return g;
+    };
+    const std::vector<C3> gT = gray(T), gR = gray(R);
+    const std::vector<C3> eT = Convolve(gT, w, h, edgeK, fw), eR = Convolve(gR, w, h, edgeK, fw);
+    const std::vector<C3> pT = Convolve(gT, w, h, pointK, fw), pR = Convolve(gR, w, h, pointK, fw);
+    std::vector<float> out(n);
+    for (size_t i = 0; i < n; ++i) {
+        float e = powf(HyABDist(LR[i], LT[i]), qc);
+        e = e < pc * cmax ? e * (pt / (pc * cmax)) : pt + ((e - pc * cmax) / (cmax - pc * cmax)) * (1.0f - pt);
+        auto mag = [](C3 v) { return sqrtf(v.a * v.a + v.b * v.b); };
+        const float de = std::abs(mag(eR[i]) - mag(eT[i])), dp = std::abs(mag(pR[i]) - mag(pT[i]));
+        const float feat = std::pow((1.0f / sqrtf(2.0f)) * std::max(de, dp), 0.5f);
+        out[i] = std::pow(e, 1.0f - feat);
+    }
+    return out;
 }
 
 }  // namespace pbrt_amd

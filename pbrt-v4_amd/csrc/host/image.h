@@ -19,7 +19,9 @@ void WriteImage(const std::string &path, const float *rgb, int w, int h, bool ex
                 const int *window = nullptr);
 Image ReadImage(const std::string &path);  // .pfm, .exr (uncompressed scanline)
 
-enum class ErrorMetric { MAE = 0, MSE = 1, MRSE = 2 };
+enum class ErrorMetric { MAE = 0, MSE = 1, MRSE = 2, FLIP = 3 };
 std::array<double, 3> ImageError(const float *img, const float *ref, int w, int h, ErrorMetric metric);
+// FLIP error per pixel ([h][w]) of RGB images test vs reference (imgtool --metric FLIP)
+std::vector<float> FlipErrorMap(const float *test, const float *ref, int w, int h);
 
 }  // namespace pbrt_amd

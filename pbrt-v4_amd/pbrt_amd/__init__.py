@@ -108,7 +108,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
     "pbrt_debug_named_spectrum", "pbrt_debug_bxdf", "pbrt_debug_layered", "pbrt_debug_triangle_shading", "pbrt_film_write_image",
     "pbrt_image_read_size", "pbrt_image_read", "pbrt_image_write", "pbrt_image_error", "pbrt_debug_filter_sample",
-    "pbrt_debug_bvh_stats", "pbrt_debug_light_bvh", "pbrt_intersect_tr", "pbrt_set_kernel_profiling", "pbrt_get_kernel_stats",
+    "pbrt_debug_bvh_stats", "pbrt_debug_light_bvh", "pbrt_intersect_tr", "pbrt_image_flip", "pbrt_set_kernel_profiling", "pbrt_get_kernel_stats",
 ]
 
 _LIB = None
@@ -149,6 +149,7 @@ def _lib():
     lib.pbrt_film_get_rgb.argtypes = [c.c_void_p, c.c_void_p]
     lib.pbrt_intersect.argtypes = [c.c_void_p, c.c_void_p, c.c_int, c.c_int, c.c_void_p, c.c_void_p]
     lib.pbrt_debug_bvh_stats.argtypes = [c.c_void_p, c.c_void_p]
+    lib.pbrt_image_flip.argtypes = [c.c_void_p, c.c_void_p, c.c_int, c.c_int, c.c_void_p]
     lib.pbrt_intersect_tr.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_set_kernel_profiling.argtypes = [c.c_void_p, c.c_int]
     lib.pbrt_debug_light_bvh.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_void_p, c.c_void_p, c.c_int,
@@ -555,8 +556,8 @@ def read_image(path) -> np.ndarray:
 
 
 def image_error(image, reference, metric="MSE") -> np.ndarray:
-    """Image::MAE / MSE / MRSE per channel (imgtool diff/error, cmd/imgtool.cpp:960-1105).
-    Like imgtool diff, infinite pixel values are set to 0 first."""
+    """Image::MAE / MSE / MRSE per channel, or the FLIP map's mean (imgtool diff/error,
+    cmd/imgtool.cpp:960-1255).  Like imgtool diff, infinite pixel values are set to 0 first."""
     a = np.array(image, dtype=np.float32, copy=True)
     b = np.array(reference, dtype=np.float32, copy=True)
     if a.shape != b.shape or a.ndim != 3 or a.shape[2] != 3:
@@ -569,8 +570,19 @@ def image_error(image, reference, metric="MSE") -> np.ndarray:
     return out
 
 
+def flip_error_map(image, reference) -> np.ndarray:
+    """FLIP error per pixel [h, w] (imgtool --metric FLIP; inputs clamped to [0, 1])."""
+    a = np.ascontiguousarray(image, dtype=np.float32)
+    b = np.ascontiguousarray(reference, dtype=np.float32)
+    if a.shape != b.shape or a.ndim != 3 or a.shape[2] != 3:
+        raise PbrtError("FLIP needs two [h, w, 3] images of one resolution")
+    out = np.zeros(a.shape[:2], np.float32)
+    _check(_lib().pbrt_image_flip(a.ctypes.data, b.ctypes.data, a.shape[1], a.shape[0], out.ctypes.data))
+    return out
+
+
 def imgtool_diff(image_file, reference_file, metric="MSE"):
-    """imgtool diff (cmd/imgtool.cpp:1105-1275) without FLIP: reads both images, returns
+    """imgtool diff (cmd/imgtool.cpp:1105-1275): reads both images, returns
     {"image_average", "reference_average", "delta_percent", metric: average over channels}."""
     a, b = read_image(image_file), read_image(reference_file)
     a[np.isinf(a)] = 0

@@ -82,8 +82,9 @@ def test_imgtool_diff_and_errors(pa, img, tmp_path):
     d = pa.imgtool_diff(tmp_path / "a.exr", tmp_path / "b.pfm", "MSE")
     assert d["delta_percent"] == pytest.approx(100 * (1 / 1.01 - 1), rel=1e-4)
     assert np.isclose(pa.image_error(img, img, "MSE"), 0).all()
+    assert (pa.image_error(img, img, "FLIP") == 0).all()
     with pytest.raises(pa.PbrtError, match="FLIP"):
-        pa.image_error(img, img, "FLIP")
+        pa.image_error(img, img, "PSNR")
     with pytest.raises(pa.PbrtError, match="unsupported"):
         pa.write_image(tmp_path / "x.tga", img)
 
@@ -156,3 +157,28 @@ def test_film_write_image_crop_window(pa, tmp_path):
     assert struct.unpack("<Iiiii", b[i + 17:i + 37]) == (16, 8, 4, 39, 29)
     i = b.index(b"displayWindow\0box2i\0")
     assert struct.unpack("<Iiiii", b[i + 20:i + 40]) == (16, 0, 0, 63, 47)
+
+
+def test_flip_matches_reference_flip(pa, golden):
+    """imgtool --metric FLIP: the product's FLIP (csrc/host/image.cpp FlipErrorMap) against
+    ComputeFLIPError of the reference's vendored src/ext/flip/flip.cpp (oracle/ref/refgold.cpp)
+    on three image pairs; the error maps agree to float rounding."""
+    from conftest import fl
+    for c in golden["flip"]:
+        w, h = c["w"], c["h"]
+        t = np.array(fl(c["test"]), np.float32).reshape(h, w, 3)
+        r = np.array(fl(c["reference"]), np.float32).reshape(h, w, 3)
+        e = np.array(fl(c["error"]), np.float32).reshape(h, w)
+        m = pa.flip_error_map(t, r)
+        np.testing.assert_allclose(m, e, rtol=1e-5, atol=1e-6)
+        err = pa.image_error(t, r, "FLIP")
+        assert err[0] == err[1] == err[2]
+        np.testing.assert_allclose(err[0], e.mean(), rtol=1e-5)
+
+
+def test_flip_identical_images_and_clamping(pa):
+    rng = np.random.default_rng(1)
+    a = rng.uniform(0, 1, (20, 24, 3)).astype(np.float32)
+    assert pa.flip_error_map(a, a).max() == 0
+    # values outside [0, 1] are clamped first (imgtool.cpp:1236-1243)
+    np.testing.assert_array_equal(pa.flip_error_map(a * 3 - 1, a), pa.flip_error_map(np.clip(a * 3 - 1, 0, 1), a))

@@ -140,6 +140,37 @@ typedef struct pbrt_scene_flat {
     const int32_t *inf_distant;       /* [n_infinite_lights] */
     const int32_t *uniform_order;     /* [n_area_lights + n_point_spot + n_infinite_lights] */
     float scene_radius;
+    /* textures (textures.h, textures.cpp, util/mipmap.*): expression nodes in the device layout
+     * (core/texture_eval.h DeviceTexNode) -- [n][8] ints kind (0 constant, 1 scale, 2 mix,
+     * 3 directionmix, 4 checkerboard, 5 bilerp, 6 imagemap), flags (bit0 spectrum, bits 1-2
+     * SpectrumType 0 albedo / 1 unbounded, bit3 invert, bit4 3D checkerboard), child0..2, image,
+     * mapping (0 uv, 1 spherical, 2 cylindrical, 3 planar), MIP filter (0 point, 1 bilinear,
+     * 2 trilinear, 3 EWA); [n][28] floats textureFromRender 3x4, planar vs vt, uv su sv du dv
+     * (planar ds dt), float constant / bilerp v00 v01 v10 v11 / directionmix dir, image scale,
+     * maxanisotropy; [n][4][8] constant spectra {rgb, value, c0, c1, c2, scale} (bilerp corners
+     * in v00 v10 v01 v11 order).  Images: [n][8] format (0 u8, 1 half, 2 float), channels,
+     * levels, wrap (0 repeat, 1 black, 2 clamp, 3 octahedral), first level, lut offset; per
+     * level [4] w, h, byte offset lo, hi into image_data; 8-bit decode tables [n][256]; the
+     * decoded files before the pyramid ([n][8] w, h, format, channels, encoding 0 linear /
+     * 1 sRGB / 2 gamma; image_raw_gamma, bytes at image_raw_offset).  material_tex [n][4]: root
+     * node of the reflectance, u and v roughness textures (-1 none), remaproughness.
+     * camera_from_render (3x4) and camera_min_diff (minPosDifferentialX/Y,
+     * minDirDifferentialX/Y, cameras.cpp:170-216) for Approximate_dp_dxy (cameras.h:167-195). */
+    int n_tex_nodes, n_images;
+    const int32_t *tex_node_info;
+    const float *tex_node_params;
+    const float *tex_node_spec;
+    const int32_t *image_info;
+    const int32_t *image_levels;
+    const uint8_t *image_data;
+    const float *image_luts;
+    const int32_t *image_raw_info;
+    const float *image_raw_gamma;
+    const uint64_t *image_raw_offset;
+    const uint8_t *image_raw_data;
+    const int32_t *material_tex;
+    float camera_from_render[12];
+    float camera_min_diff[12];
 } pbrt_scene_flat;
 
 typedef struct pbrt_render_params {
@@ -249,6 +280,13 @@ int64_t pbrt_debug_halton_fastpath_mismatches(const pbrt_scene *scene, int dim, 
                                               uint32_t step);
 int pbrt_debug_rgb_coeffs(float r, float g, float b, float *coeffs3);
 int pbrt_debug_rgb2spec_column(int maxc, int j, int i, float *out192);
+/* Texture evaluation of material `material`'s textured parameter (slot 0 reflectance, 1 u / 2 v
+ * roughness) at a hit given as p, n, dpdu, dpdv (render space) and uv (14 floats), with the
+ * product's shared host/device code (surfscatter.cpp:74-137, textures.h): out[0..3] = dudx,
+ * dudy, dvdx, dvdy, then the spectrum texture at each of the n wavelengths, or out[4] = the
+ * float texture */
+int pbrt_debug_texture_eval(const pbrt_scene *scene, int material, int slot, const float *hit14, const float *lambda,
+                            int n, float *out);
 /* Filter::Sample(u) of the scene's pixel filter (FilterSampler over PiecewiseConstant2D for
  * gaussian / mitchell / sinc, SampleTent for triangle, filters.h): out3 = p.x p.y weight */
 int pbrt_debug_filter_sample(const pbrt_scene *scene, float u0, float u1, float *out3);

@@ -605,6 +605,8 @@ static void Point3fi(Vec v, Vec e, Vec *p, Vec *err) {
 
 struct Interaction {
     Vec p, err, n, ns, dpdu, dpdus, wo;
+    Vec dpdv;        // geometric dpdv and uv: texture lookups (surfscatter.cpp:74-135)
+    Float uv[2] = {0, 0};
     int prim = -1;
 };
 
@@ -640,6 +642,9 @@ static Interaction TriangleInteraction(Vec p0, Vec p1, Vec p2, bool flip, TriIse
     if (flip) si.n = -si.n;
     si.ns = si.n;
     si.dpdu = si.dpdus = dpdu;
+    si.dpdv = dpdv;
+    // Point2f uvHit = b0 * uv[0] + b1 * uv[1] + b2 * uv[2] (shapes.h:920)
+    for (int k = 0; k < 2; ++k) si.uv[k] = ti.b0 * a.uv[0][k] + ti.b1 * a.uv[1][k] + ti.b2 * a.uv[2][k];
     if (a.hasN) {
         Vec ns = ti.b0 * a.n[0] + ti.b1 * a.n[1] + ti.b2 * a.n[2];
         ns = LengthSquared(ns) > 0 ? Normalize(ns) : si.n;
@@ -2413,9 +2418,693 @@ struct PixelFilter {
     }
 };
 
+// ---------------------------------------------------------------- textures
+// Image textures and texture expressions, restated independently of the product:
+//   Image::GeneratePyramid / FloatResizeUp / ResampleWeights   util/image.cpp:208-383
+//   ColorEncoding FromLinear / ToLinear, LinearToSRGB           util/color.h:420-538, color.cpp
+//   Half(float) round to nearest even                           util/float.h:419-470
+//   Image::GetChannel / BilerpChannel, RemapPixelCoords          util/image.h:96-146, 255-292
+//   MIPMap::Filter / Bilerp / Texel / EWA                        util/mipmap.cpp:208-375
+//   textures and mappings                                        textures.h:86-1175, textures.cpp
+//   RGBToSpectrumTable::operator(), RGB*Spectrum                 util/color.cpp:36-75, spectrum.cpp
+//   CameraBase::FindMinimumDifferentials / Approximate_dp_dxy    cameras.cpp:170-216, cameras.h:167
+//   the (u,v) derivatives of the material stage                  wavefront/surfscatter.cpp:74-104
+// The oracle builds its own MIPMap pyramid from the decoded image files the loader hands over
+// (pbrt_scene_flat image_raw_*) and evaluates each texture tree recursively with full
+// SampledSpectrum arithmetic, as pbrt's UniversalTextureEvaluator does.  The only tables it
+// shares with the product are reference data: the 8-bit sRGB decode table (the literals of
+// util/color.cpp), the EWA weight table (util/mipmap.cpp) and the rgb2spec_opt coefficient
+// table (set through oracle_set_rgb_table).
+static const float *g_rgbTable = nullptr;  // zNodes[64], then coefficients [3][64][64][64][3]
+static const float *g_ewaLut = nullptr;    // MIPFilterLUT[128]
+
+static uint16_t OFloatToHalf(float ff) {
+    uint32_t f = FloatToBits(ff);
+    const uint32_t sign = f & 0x80000000u;
+    f ^= sign;
+    uint16_t o;
+    if (f >= (uint32_t)(127 + 16) << 23) {
+        o = (f > (255u << 23)) ? 0x7e00 : 0x7c00;
+    } else if (f < (113u << 23)) {
+        const uint32_t magic = ((127 - 15) + (23 - 10) + 1) << 23;
+        float v = BitsToFloat(f) + BitsToFloat(magic);
+        o = (uint16_t)(FloatToBits(v) - magic);
+    } else {
+        const uint32_t mantOdd = (f >> 13) & 1;
+        f += ((uint32_t)(15 - 127) << 23) + 0xfff;
+        f += mantOdd;
+        o = (uint16_t)(f >> 13);
+    }
+    return (uint16_t)(o | (sign >> 16));
+}
+static float OHalfToFloat(uint16_t h) {
+    const int e = (h >> 10) & 31, m = h & 1023;
+    float v;
+    if (e == 0) v = std::ldexp((float)m, -24);
+    else if (e == 31) v = m ? std::numeric_limits<float>::quiet_NaN() : std::numeric_limits<float>::infinity();
+    else v = std::ldexp((float)(m | 1024), e - 25);
+    return (h & 0x8000) ? -v : v;
+}
+static Float OEvalPoly(Float t, const Float *c, int n) {
+    Float r = c[n - 1];
+    for (int i = n - 2; i >= 0; --i) r = std::fma(t, r, c[i]);
+    return r;
+}
+static Float OLinearToSRGB(Float value) {
+    if (value <= 0.0031308f) return 12.92f * value;
+    const Float sq = SafeSqrt(value);
+    static const Float P[6] = {-0.0016829072605308378f, 0.03453868659826638f, 0.7642611304733891f,
+                               2.0041169284241644f, 0.7551545191665577f, -0.016202083165206348f};
+    static const Float Q[6] = {4.178892964897981e-7f, -0.00004375359692957097f, 0.03467195408529984f,
+                               0.6085338522168684f, 1.8970238036421054f, 1.f};
+    return OEvalPoly(sq, P, 6) / OEvalPoly(sq, Q, 6) * value;
+}
+
+struct OEncoding {
+    int kind = 1;  // 0 linear, 1 sRGB, 2 gamma
+    Float gamma = 1;
+    const float *srgbLut = nullptr;
+    Float apply[256], inverse[1024];
+    void Init(int k, Float g, const float *lut) {
+        kind = k;
+        gamma = g;
+        srgbLut = lut;
+        if (kind == 2) {
+            for (int i = 0; i < 256; ++i) apply[i] = std::pow(Float(i) / 255.f, gamma);
+            for (int i = 0; i < 1024; ++i) inverse[i] = Clamp(255.f * std::pow(Float(i) / Float(1023), 1.f / gamma) + .5f, 0, 255);
+        }
+    }
+    Float ToLinear(uint8_t v) const { return kind == 0 ? v / 255.f : (kind == 1 ? srgbLut[v] : apply[v]); }
+    uint8_t FromLinear(Float v) const {
+        if (kind == 0) return (uint8_t)Clamp(v * 255.f + 0.5f, 0, 255);
+        if (kind == 1) {
+            if (v <= 0) return 0;
+            if (v >= 1) return 255;
+            return (uint8_t)Clamp(std::round(255.f * OLinearToSRGB(v)), 0, 255);
+        }
+        return (uint8_t)inverse[(size_t)Clamp(v * Float(1023), 0, 1023)];
+    }
+};
+
+struct OImage {
+    int format = 0, nc = 0, wrap = 0, nLevels = 0;
+    OEncoding enc;
+    std::vector<int> w, h;
+    std::vector<std::vector<uint8_t>> l8;
+    std::vector<std::vector<uint16_t>> l16;
+    std::vector<std::vector<float>> l32;
+
+    static bool Remap(int *px, int *py, int W, int H, int wrap) {
+        int x = *px, y = *py;
+        if (wrap == 3) {
+            if (x < 0) { x = -x; y = H - 1 - y; }
+            else if (x >= W) { x = 2 * W - 1 - x; y = H - 1 - y; }
+            if (y < 0) { x = W - 1 - x; y = -y; }
+            else if (y >= H) { x = W - 1 - x; y = 2 * H - 1 - y; }
+            if (W == 1) x = 0;
+            if (H == 1) y = 0;
+        } else {
+            int *c[2] = {&x, &y};
+            const int res[2] = {W, H};
+            for (int k = 0; k < 2; ++k) {
+                if (*c[k] >= 0 && *c[k] < res[k]) continue;
+                if (wrap == 0) { int r = *c[k] % res[k]; *c[k] = r < 0 ? r + res[k] : r; }
+                else if (wrap == 2) *c[k] = Clamp(*c[k], 0, res[k] - 1);
+                else return false;
+            }
+        }
+        *px = x;
+        *py = y;
+        return true;
+    }
+    Float Get(int level, int x, int y, int c) const {
+        if (!Remap(&x, &y, w[level], h[level], wrap)) return 0;
+        const size_t i = ((size_t)y * w[level] + x) * nc + c;
+        if (format == 0) return enc.ToLinear(l8[level][i]);
+        if (format == 1) return OHalfToFloat(l16[level][i]);
+        return l32[level][i];
+    }
+    void Store(const std::vector<float> &f, int W, int H) {
+        w.push_back(W);
+        h.push_back(H);
+        l8.emplace_back();
+        l16.emplace_back();
+        l32.emplace_back();
+        if (format == 0) for (float v : f) l8.back().push_back(enc.FromLinear(v));
+        else if (format == 1) for (float v : f) l16.back().push_back(OFloatToHalf(v));
+        else l32.back() = f;
+    }
+    // Image::GeneratePyramid
+    void Build(const uint8_t *raw, int W, int H) {
+        std::vector<float> f((size_t)W * H * nc);
+        for (size_t i = 0; i < f.size(); ++i) {
+            if (format == 0) f[i] = enc.ToLinear(raw[i]);
+            else if (format == 1) { uint16_t hv; std::memcpy(&hv, raw + 2 * i, 2); f[i] = OHalfToFloat(hv); }
+            else std::memcpy(&f[i], raw + 4 * i, 4);
+        }
+        auto pow2 = [](int v) { return v > 0 && !(v & (v - 1)); };
+        auto up2 = [](int v) { int r = 1; while (r < v) r <<= 1; return r; };
+        if (!pow2(W) || !pow2(H)) {
+            const int nw = up2(W), nh = up2(H);
+            f = ResizeUp(f, W, H, nw, nh);
+            W = nw;
+            H = nh;
+        }
+        int lv = 1, m = std::max(W, H);
+        while (m > 1) { m >>= 1; ++lv; }
+        nLevels = lv;
+        for (int i = 0; i < nLevels - 1; ++i) {
+            Store(f, W, H);
+            const int nw = std::max(1, W / 2), nh = std::max(1, H / 2);
+            std::vector<float> next((size_t)nw * nh * nc);
+            for (int y = 0; y < nh; ++y)
+                for (int x = 0; x < nw; ++x)
+                    for (int c = 0; c < nc; ++c) {
+                        const int x0 = 2 * x, y0 = 2 * y, x1 = W == 1 ? x0 : x0 + 1, y1 = H == 1 ? y0 : y0 + 1;
+                        auto at = [&](int xx, int yy) { return f[((size_t)yy * W + xx) * nc + c]; };
+                        next[((size_t)y * nw + x) * nc + c] = (at(x0, y0) + at(x1, y0) + at(x0, y1) + at(x1, y1)) / 4;
+                    }
+            f.swap(next);
+            W = nw;
+            H = nh;
+        }
+        Store(f, W, H);
+    }
+    static Float WSinc(Float x) {
+        // WindowedSinc(x, 2, 2): SinXOverX(Pi x) * SinXOverX(Pi x / 2)
+        if (std::abs(x) > 2) return 0;
+        auto sxx = [](Float v) { return (1 - v * v == 1) ? Float(1) : std::sin(v) / v; };
+        return sxx(Pi * x) * sxx(Pi * (x / 2));
+    }
+    std::vector<float> ResizeUp(const std::vector<float> &src, int W, int H, int nw, int nh) const {
+        struct RW { int first; Float wt[4]; };
+        auto weights = [](int oldRes, int newRes) {
+            std::vector<RW> r(newRes);
+            for (int i = 0; i < newRes; ++i) {
+                Float center = (i + .5f) * oldRes / newRes;
+                r[i].first = (int)std::floor((center - 2) + 0.5f);
+                for (int j = 0; j < 4; ++j) r[i].wt[j] = WSinc(r[i].first + j + .5f - center);
+                Float inv = 1 / (r[i].wt[0] + r[i].wt[1] + r[i].wt[2] + r[i].wt[3]);
+                for (int j = 0; j < 4; ++j) r[i].wt[j] *= inv;
+            }
+            return r;
+        };
+        std::vector<RW> xw = weights(W, nw), yw = weights(H, nh);
+        auto in = [&](int x, int y, int c) {
+            Remap(&x, &y, W, H, wrap);
+            return src[((size_t)y * W + x) * nc + c];
+        };
+        auto xpass = [&](int x, int y, int c) {
+            const RW &r = xw[x];
+            return r.wt[0] * in(r.first, y, c) + r.wt[1] * in(r.first + 1, y, c) + r.wt[2] * in(r.first + 2, y, c) +
+                   r.wt[3] * in(r.first + 3, y, c);
+        };
+        std::vector<float> out((size_t)nw * nh * nc);
+        for (int y = 0; y < nh; ++y)
+            for (int x = 0; x < nw; ++x)
+                for (int c = 0; c < nc; ++c) {
+                    const RW &r = yw[y];
+                    out[((size_t)y * nw + x) * nc + c] =
+                        std::max<Float>(0, (r.wt[0] * xpass(x, r.first, c) + r.wt[1] * xpass(x, r.first + 1, c) +
+                                            r.wt[2] * xpass(x, r.first + 2, c) + r.wt[3] * xpass(x, r.first + 3, c)));
+                }
+        return out;
+    }
+    // MIPMap::Bilerp / Texel for RGB (channels 0-2, or the single channel) and Float
+    Float BilerpC(int level, Float s, Float t, int c) const {
+        Float x = s * w[level] - 0.5f, y = t * h[level] - 0.5f;
+        int xi = (int)std::floor(x), yi = (int)std::floor(y);
+        Float dx = x - xi, dy = y - yi;
+        return ((1 - dx) * (1 - dy) * Get(level, xi, yi, c) + dx * (1 - dy) * Get(level, xi + 1, yi, c) +
+                (1 - dx) * dy * Get(level, xi, yi + 1, c) + dx * dy * Get(level, xi + 1, yi + 1, c));
+    }
+    void BilerpRGB(int level, Float s, Float t, Float *rgb) const {
+        for (int c = 0; c < 3; ++c) rgb[c] = BilerpC(level, s, t, nc == 1 ? 0 : c);
+    }
+    Float BilerpF(int level, Float s, Float t) const {
+        if (nc == 1) return BilerpC(level, s, t, 0);
+        if (nc == 3) {
+            Float sum = 0;
+            for (int c = 0; c < 3; ++c) sum += BilerpC(level, s, t, c);
+            return sum / 3;
+        }
+        return BilerpC(level, s, t, 3);
+    }
+    void TexelRGB(int level, int x, int y, Float *rgb) const {
+        for (int c = 0; c < 3; ++c) rgb[c] = Get(level, x, y, nc == 1 ? 0 : c);
+    }
+    // MIPMap::Filter; nOut = 3 (RGB) or 1 (Float)
+    void Filter(int filter, Float maxAniso, Float s, Float t, Float d0s, Float d0t, Float d1s, Float d1t, int nOut,
+                Float *out) const {
+        auto bil = [&](int level, Float *o) {
+            if (nOut == 3) BilerpRGB(level, s, t, o);
+            else o[0] = BilerpF(level, s, t);
+        };
+        auto texel = [&](int level, int x, int y, Float *o) {
+            if (nOut == 3) TexelRGB(level, x, y, o);
+            else o[0] = Get(level, x, y, 0);
+        };
+        const Float invLog2 = 1.442695040888963387004650940071f;
+        if (filter != 3) {
+            Float width = 2 * std::max({std::abs(d0s), std::abs(d0t), std::abs(d1s), std::abs(d1t)});
+            Float level = nLevels - 1 + CRLog(std::max<Float>(width, 1e-8f)) * invLog2;
+            if (level >= nLevels - 1) return texel(nLevels - 1, 0, 0, out);
+            int iLevel = std::max(0, (int)std::floor(level));
+            if (filter == 0)
+                return texel(iLevel, (int)std::round(s * w[iLevel] - 0.5f), (int)std::round(t * h[iLevel] - 0.5f), out);
+            if (filter == 1 || iLevel == 0) return bil(iLevel, out);
+            Float a[3], b[3];
+            bil(iLevel, a);
+            bil(iLevel + 1, b);
+            for (int k = 0; k < nOut; ++k) out[k] = Lerp(level - iLevel, a[k], b[k]);
+            return;
+        }
+        if (Sqr(d0s) + Sqr(d0t) < Sqr(d1s) + Sqr(d1t)) {
+            std::swap(d0s, d1s);
+            std::swap(d0t, d1t);
+        }
+        Float longer = std::sqrt(Sqr(d0s) + Sqr(d0t)), shorter = std::sqrt(Sqr(d1s) + Sqr(d1t));
+        if (shorter * maxAniso < longer && shorter > 0) {
+            Float sc = longer / (shorter * maxAniso);
+            d1s *= sc;
+            d1t *= sc;
+            shorter *= sc;
+        }
+        if (shorter == 0) return bil(0, out);
+        Float lod = std::max<Float>(0, nLevels - 1 + CRLog(shorter) * invLog2);
+        int ilod = (int)std::floor(lod);
+        Float a[3], b[3];
+        EWA(ilod, s, t, d0s, d0t, d1s, d1t, nOut, a);
+        EWA(ilod + 1, s, t, d0s, d0t, d1s, d1t, nOut, b);
+        for (int k = 0; k < nOut; ++k) out[k] = Lerp(lod - ilod, a[k], b[k]);
+    }
+    void EWA(int level, Float s, Float t, Float d0s, Float d0t, Float d1s, Float d1t, int nOut, Float *out) const {
+        if (level >= nLevels) {
+            if (nOut == 3) TexelRGB(nLevels - 1, 0, 0, out);
+            else out[0] = Get(nLevels - 1, 0, 0, 0);
+            return;
+        }
+        s = s * w[level] - 0.5f;
+        t = t * h[level] - 0.5f;
+        d0s *= w[level];
+        d0t *= h[level];
+        d1s *= w[level];
+        d1t *= h[level];
+        Float A = Sqr(d0t) + Sqr(d1t) + 1, B = -2 * (d0s * d0t + d1s * d1t), C = Sqr(d0s) + Sqr(d1s) + 1;
+        Float invF = 1 / (A * C - Sqr(B) * 0.25f);
+        A *= invF;
+        B *= invF;
+        C *= invF;
+        Float det = -Sqr(B) + 4 * A * C, invDet = 1 / det;
+        Float uSqrt = SafeSqrt(det * C), vSqrt = SafeSqrt(A * det);
+        int s0 = (int)std::ceil(s - 2 * invDet * uSqrt), s1 = (int)std::floor(s + 2 * invDet * uSqrt);
+        int t0 = (int)std::ceil(t - 2 * invDet * vSqrt), t1 = (int)std::floor(t + 2 * invDet * vSqrt);
+        Float sum[3] = {0, 0, 0}, sumW = 0;
+        for (int it = t0; it <= t1; ++it) {
+            Float tt = it - t;
+            for (int is = s0; is <= s1; ++is) {
+                Float ss = is - s;
+                Float r2 = A * Sqr(ss) + B * ss * tt + C * Sqr(tt);
+                if (r2 < 1) {
+                    int index = std::min<int>((int)(r2 * 128), 127);
+                    Float wt = g_ewaLut[index], v[3];
+                    if (nOut == 3) TexelRGB(level, is, it, v);
+                    else v[0] = Get(level, is, it, 0);
+                    for (int k = 0; k < nOut; ++k) sum[k] = sum[k] + wt * v[k];
+                    sumW += wt;
+                }
+            }
+        }
+        for (int k = 0; k < nOut; ++k) out[k] = sum[k] / sumW;
+    }
+};
+
+// RGBToSpectrumTable::operator() (util/color.cpp:36-75)
+static void ORGBCoeffs(Float r, Float g, Float b, Float c[3]) {
+    if (r == g && g == b) {
+        c[0] = c[1] = 0;
+        c[2] = (r - .5f) / std::sqrt(r * (1 - r));
+        return;
+    }
+    const Float rgb[3] = {r, g, b};
+    const int res = 64;
+    const float *zn = g_rgbTable, *data = g_rgbTable + 64;
+    int maxc = (r > g) ? ((r > b) ? 0 : 2) : ((g > b) ? 1 : 2);
+    Float z = rgb[maxc], x = rgb[(maxc + 1) % 3] * (res - 1) / z, y = rgb[(maxc + 2) % 3] * (res - 1) / z;
+    int xi = std::min((int)x, res - 2), yi = std::min((int)y, res - 2);
+    int zi = 0;
+    while (zi < res - 2 && zn[zi + 1] < z) ++zi;  // FindInterval over the monotone z nodes
+    Float dx = x - xi, dy = y - yi, dz = (z - zn[zi]) / (zn[zi + 1] - zn[zi]);
+    for (int i = 0; i < 3; ++i) {
+        auto co = [&](int a, int bb, int cc) {
+            return data[((((size_t)maxc * res + (zi + cc)) * res + (yi + bb)) * res + (xi + a)) * 3 + i];
+        };
+        c[i] = Lerp(dz, Lerp(dy, Lerp(dx, co(0, 0, 0), co(1, 0, 0)), Lerp(dx, co(0, 1, 0), co(1, 1, 0))),
+                    Lerp(dy, Lerp(dx, co(0, 0, 1), co(1, 0, 1)), Lerp(dx, co(0, 1, 1), co(1, 1, 1))));
+    }
+}
+
+struct OTexCtx {
+    Vec p, n;
+    Float u = 0, v = 0, dudx = 0, dudy = 0, dvdx = 0, dvdy = 0;
+};
+
+struct OTextures {
+    const pbrt_scene_flat *f = nullptr;
+    std::vector<OImage> images;
+    // camera differentials (own FindMinimumDifferentials) and CameraFromRender
+    Vec minPosDx, minPosDy, minDirDx, minDirDy;
+    Float sppScale = 1;
+    int n = 0;
+
+    void Init(const pbrt_scene_flat *flat, int spp, int xres, int yres) {
+        f = flat;
+        fullRes[0] = xres;
+        fullRes[1] = yres;
+        n = flat->n_tex_nodes;
+        if (!n) return;
+        sppScale = std::max<Float>(.125f, 1 / std::sqrt((Float)spp));
+        images.resize(flat->n_images);
+        for (int i = 0; i < flat->n_images; ++i) {
+            const int32_t *ri = flat->image_raw_info + 8 * i;
+            const int32_t *ii = flat->image_info + 8 * i;
+            OImage &im = images[i];
+            im.format = ri[2];
+            im.nc = ri[3];
+            im.wrap = ii[3];
+            im.enc.Init(ri[4], flat->image_raw_gamma[i], flat->image_luts + 256 * i);
+            im.Build(flat->image_raw_data + flat->image_raw_offset[i], ri[0], ri[1]);
+        }
+        FindMinimumDifferentials();
+    }
+    const int32_t *Info(int node) const { return f->tex_node_info + 8 * node; }
+    const float *Par(int node) const { return f->tex_node_params + 28 * node; }
+    const float *Spec(int node, int k) const { return f->tex_node_spec + 32 * node + 8 * k; }
+
+    // PerspectiveCamera::GenerateRayDifferential (cameras.cpp:458-520) + RenderFromCamera, then
+    // CameraBase::FindMinimumDifferentials (cameras.cpp:170-216)
+    static Vec XP(const float *m, Vec p) {
+        Float x = m[0] * p.x + m[1] * p.y + m[2] * p.z + m[3], y = m[4] * p.x + m[5] * p.y + m[6] * p.z + m[7];
+        Float z = m[8] * p.x + m[9] * p.y + m[10] * p.z + m[11], w = m[12] * p.x + m[13] * p.y + m[14] * p.z + m[15];
+        return w == 1 ? Vec(x, y, z) : Vec(x, y, z) / w;
+    }
+    static Vec XV(const float *m, Vec v) {
+        return Vec(m[0] * v.x + m[1] * v.y + m[2] * v.z, m[4] * v.x + m[5] * v.y + m[6] * v.z, m[8] * v.x + m[9] * v.y + m[10] * v.z);
+    }
+    Vec CameraFromRenderV(Vec v) const {
+        const float *c = f->camera_from_render;
+        return Vec(c[0] * v.x + c[1] * v.y + c[2] * v.z, c[4] * v.x + c[5] * v.y + c[6] * v.z, c[8] * v.x + c[9] * v.y + c[10] * v.z);
+    }
+    void FindMinimumDifferentials() {
+        const float *cfr = f->camera_from_raster, *rfc = f->render_from_camera;
+        const Vec dxCam = XP(cfr, Vec(1, 0, 0)) - XP(cfr, Vec(0, 0, 0)), dyCam = XP(cfr, Vec(0, 1, 0)) - XP(cfr, Vec(0, 0, 0));
+        const Float inf = Infinity;
+        minPosDx = minPosDy = minDirDx = minDirDy = Vec(inf, inf, inf);
+        // the film's full resolution: camera_from_raster maps raster (xres, yres) corners
+        const int xres = fullRes[0], yres = fullRes[1];
+        for (int i = 0; i < 512; ++i) {
+            Vec pCam = XP(cfr, Vec(Float(i) / 511 * xres, Float(i) / 511 * yres, 0));
+            Vec d = Normalize(pCam), o(0, 0, 0), rxd, ryd;
+            if (f->lens_radius > 0) {
+                Float ft = f->focal_distance / d.z;
+                d = Normalize((o + d * ft) - o);
+                Vec dx = Normalize(pCam + dxCam), dy = Normalize(pCam + dyCam);
+                rxd = Normalize((Vec(0, 0, 0) + (f->focal_distance / dx.z) * dx) - o);
+                ryd = Normalize((Vec(0, 0, 0) + (f->focal_distance / dy.z) * dy) - o);
+            } else {
+                rxd = Normalize(pCam + dxCam);
+                ryd = Normalize(pCam + dyCam);
+            }
+            // Transform::operator()(Ray): the origin moves to the edge of its error bound
+            Vec oo = XP(rfc, o), dd = XV(rfc, d);
+            Vec err = gamma(3) * Abs(Vec(rfc[3], rfc[7], rfc[11]));
+            if (LengthSquared(dd) > 0) oo = oo + dd * (Dot(Abs(dd), err) / LengthSquared(dd));
+            Vec rxo = XP(rfc, o), ryo = rxo;
+            Vec dox = CameraFromRenderV(rxo - oo), doy = CameraFromRenderV(ryo - oo);
+            if (Length(dox) < Length(minPosDx)) minPosDx = dox;
+            if (Length(doy) < Length(minPosDy)) minPosDy = doy;
+            Vec rd = Normalize(dd), rx = Normalize(XV(rfc, rxd)), ry = Normalize(XV(rfc, ryd));
+            Vec fx, fy;
+            CoordinateSystem(rd, &fx, &fy);
+            auto local = [&](Vec v) { return Vec(Dot(v, fx), Dot(v, fy), Dot(v, rd)); };
+            Vec df = local(rd), dxf = Normalize(local(rx)), dyf = Normalize(local(ry));
+            if (Length(dxf - df) < Length(minDirDx)) minDirDx = dxf - df;
+            if (Length(dyf - df) < Length(minDirDy)) minDirDy = dyf - df;
+        }
+    }
+    int fullRes[2] = {1, 1};
+
+    // CameraBase::Approximate_dp_dxy (cameras.h:167-195)
+    void DpDxy(Vec p, Vec n, Vec *dpdx, Vec *dpdy) const {
+        const float *ci = f->camera_from_render, *m = f->render_from_camera;
+        Vec pc((ci[0] * p.x + ci[1] * p.y) + (ci[2] * p.z + ci[3]), (ci[4] * p.x + ci[5] * p.y) + (ci[6] * p.z + ci[7]),
+               (ci[8] * p.x + ci[9] * p.y) + (ci[10] * p.z + ci[11]));
+        Vec nc(m[0] * n.x + m[4] * n.y + m[8] * n.z, m[1] * n.x + m[5] * n.y + m[9] * n.z, m[2] * n.x + m[6] * n.y + m[10] * n.z);
+        // RotateFromTo(Normalize(pc), (0, 0, 1)) (util/transform.h:249-270)
+        Vec from = Normalize(pc), to(0, 0, 1), refl;
+        if (std::abs(from.x) < 0.72f && std::abs(to.x) < 0.72f) refl = Vec(1, 0, 0);
+        else if (std::abs(from.y) < 0.72f && std::abs(to.y) < 0.72f) refl = Vec(0, 1, 0);
+        else refl = Vec(0, 0, 1);
+        Vec u = refl - from, v = refl - to;
+        Float r[3][3];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j)
+                r[i][j] = ((i == j) ? 1 : 0) - 2 / Dot(u, u) * u[i] * u[j] - 2 / Dot(v, v) * v[i] * v[j] +
+                          4 * Dot(u, v) / (Dot(u, u) * Dot(v, v)) * v[i] * u[j];
+        auto R = [&](Vec a, bool transpose) {
+            Vec o;
+            for (int i = 0; i < 3; ++i)
+                o[i] = transpose ? r[0][i] * a.x + r[1][i] * a.y + r[2][i] * a.z : r[i][0] * a.x + r[i][1] * a.y + r[i][2] * a.z;
+            return o;
+        };
+        Vec pz = R(pc, false);
+        pz = Vec(pz.x + 0, pz.y + 0, pz.z + 0);
+        Vec nz = R(nc, false);
+        Float d = nz.z * pz.z;
+        Vec xo = Vec(0, 0, 0) + minPosDx, xd = Vec(0, 0, 1) + minDirDx;
+        Vec yo = Vec(0, 0, 0) + minPosDy, yd = Vec(0, 0, 1) + minDirDy;
+        Float tx = -(DotN(nz, xo) - d) / DotN(nz, xd), ty = -(DotN(nz, yo) - d) / DotN(nz, yd);
+        Vec px = xo + xd * tx, py = yo + yd * ty;
+        auto toRender = [&](Vec a) {
+            return Vec(m[0] * a.x + m[1] * a.y + m[2] * a.z, m[4] * a.x + m[5] * a.y + m[6] * a.z, m[8] * a.x + m[9] * a.y + m[10] * a.z);
+        };
+        *dpdx = sppScale * toRender(R(px - pz, true));
+        *dpdy = sppScale * toRender(R(py - pz, true));
+    }
+    // wavefront/surfscatter.cpp:74-104
+    OTexCtx Ctx(const Interaction &si) const {
+        OTexCtx c;
+        c.p = si.p;
+        c.n = si.n;
+        c.u = si.uv[0];
+        c.v = si.uv[1];
+        Vec dpdx, dpdy;
+        DpDxy(si.p, si.n, &dpdx, &dpdy);
+        Float ata00 = Dot(si.dpdu, si.dpdu), ata01 = Dot(si.dpdu, si.dpdv), ata11 = Dot(si.dpdv, si.dpdv);
+        Float invDet = 1 / DifferenceOfProducts(ata00, ata11, ata01, ata01);
+        invDet = std::isfinite(invDet) ? invDet : 0.f;
+        Float atb0x = Dot(si.dpdu, dpdx), atb1x = Dot(si.dpdv, dpdx), atb0y = Dot(si.dpdu, dpdy), atb1y = Dot(si.dpdv, dpdy);
+        Float v[4] = {DifferenceOfProducts(ata11, atb0x, ata01, atb1x) * invDet, DifferenceOfProducts(ata11, atb0y, ata01, atb1y) * invDet,
+                      DifferenceOfProducts(ata00, atb1x, ata01, atb0x) * invDet, DifferenceOfProducts(ata00, atb1y, ata01, atb0y) * invDet};
+        for (Float &x : v) x = std::isfinite(x) ? Clamp(x, -1e8f, 1e8f) : 0.f;
+        c.dudx = v[0];
+        c.dudy = v[1];
+        c.dvdx = v[2];
+        c.dvdy = v[3];
+        return c;
+    }
+
+    // TextureMapping2D::Map (textures.h:86-202); the wavefront's dpdx = dpdy = 0
+    void Map2D(int node, const OTexCtx &c, Float st[2], Float dst[4]) const {
+        const int mapping = Info(node)[6];
+        const float *q = Par(node);
+        if (mapping == 0) {
+            dst[0] = q[18] * c.dudx;
+            dst[1] = q[18] * c.dudy;
+            dst[2] = q[19] * c.dvdx;
+            dst[3] = q[19] * c.dvdy;
+            st[0] = q[18] * c.u + q[20];
+            st[1] = q[19] * c.v + q[21];
+            return;
+        }
+        Vec pt(q[0] * c.p.x + q[1] * c.p.y + q[2] * c.p.z + q[3], q[4] * c.p.x + q[5] * c.p.y + q[6] * c.p.z + q[7],
+               q[8] * c.p.x + q[9] * c.p.y + q[10] * c.p.z + q[11]);
+        const Vec zero(0, 0, 0);
+        if (mapping == 1) {
+            Float x2y2 = Sqr(pt.x) + Sqr(pt.y), sq = std::sqrt(x2y2);
+            Vec dsdp = Vec(-pt.y, pt.x, 0) / (2 * Pi * x2y2);
+            Vec dtdp = 1 / (Pi * (x2y2 + Sqr(pt.z))) * Vec(pt.x * pt.z / sq, pt.y * pt.z / sq, -sq);
+            dst[0] = Dot(dsdp, zero);
+            dst[1] = Dot(dsdp, zero);
+            dst[2] = Dot(dtdp, zero);
+            dst[3] = Dot(dtdp, zero);
+            Vec vec = Normalize(pt - Vec(0, 0, 0));
+            Float phi = CRATan2(vec.y, vec.x);
+            st[0] = SafeACos(vec.z) * InvPi;
+            st[1] = (phi < 0 ? phi + 2 * Pi : phi) * 0.15915494309189533577f;
+        } else if (mapping == 2) {
+            Float x2y2 = Sqr(pt.x) + Sqr(pt.y);
+            Vec dsdp = Vec(-pt.y, pt.x, 0) / (2 * Pi * x2y2), dtdp(0, 0, 1);
+            dst[0] = Dot(dsdp, zero);
+            dst[1] = Dot(dsdp, zero);
+            dst[2] = Dot(dtdp, zero);
+            dst[3] = Dot(dtdp, zero);
+            st[0] = (Pi + CRATan2(pt.y, pt.x)) * 0.15915494309189533577f;
+            st[1] = pt.z;
+        } else {
+            Vec vs(q[12], q[13], q[14]), vt(q[15], q[16], q[17]);
+            dst[0] = Dot(vs, zero);
+            dst[1] = Dot(vs, zero);
+            dst[2] = Dot(vt, zero);
+            dst[3] = Dot(vt, zero);
+            st[0] = q[18] + Dot(pt, vs);
+            st[1] = q[19] + Dot(pt, vt);
+        }
+    }
+    // Checkerboard (textures.cpp:183-217)
+    Float Checker(int node, const OTexCtx &c) const {
+        auto d = [](Float x) {
+            Float y = x / 2 - std::floor(x / 2) - 0.5f;
+            return x / 2 + y * (1 - 2 * std::abs(y));
+        };
+        auto bf = [&](Float x, Float r) -> Float {
+            if (std::floor(x - r) == std::floor(x + r)) return 1 - 2 * ((int)std::floor(x) & 1);
+            return (d(x + r) - 2 * d(x) + d(x - r)) / Sqr(r);
+        };
+        if (!(Info(node)[1] & 16)) {
+            Float st[2], dst[4];
+            Map2D(node, c, st, dst);
+            Float ds = std::max(std::abs(dst[0]), std::abs(dst[1])), dt = std::max(std::abs(dst[2]), std::abs(dst[3]));
+            ds *= 1.5f;
+            dt *= 1.5f;
+            return 0.5f - bf(st[0], ds) * bf(st[1], dt) / 2;
+        }
+        const float *q = Par(node);
+        Vec p(q[0] * c.p.x + q[1] * c.p.y + q[2] * c.p.z + q[3], q[4] * c.p.x + q[5] * c.p.y + q[6] * c.p.z + q[7],
+              q[8] * c.p.x + q[9] * c.p.y + q[10] * c.p.z + q[11]);
+        Float dx = 1.5f * std::max(std::abs(0.f), std::abs(0.f));
+        return 0.5f - 0.5f * bf(p.x, dx) * bf(p.y, dx) * bf(p.z, dx);
+    }
+    Float EvalF(int node, const OTexCtx &c) const {
+        const int32_t *in = Info(node);
+        const float *q = Par(node);
+        switch (in[0]) {
+        case 0: return q[22];
+        case 1: {  // FloatScaledTexture
+            Float sc = EvalF(in[3], c);
+            if (sc == 0) return 0;
+            return EvalF(in[2], c) * sc;
+        }
+        case 2: {  // FloatMixTexture
+            Float amt = EvalF(in[4], c), t1 = 0, t2 = 0;
+            if (amt != 1) t1 = EvalF(in[2], c);
+            if (amt != 0) t2 = EvalF(in[3], c);
+            return (1 - amt) * t1 + amt * t2;
+        }
+        case 3: {  // FloatDirectionMixTexture
+            Float amt = AbsDotN(c.n, Vec(q[22], q[23], q[24])), t1 = 0, t2 = 0;
+            if (amt != 0) t1 = EvalF(in[2], c);
+            if (amt != 1) t2 = EvalF(in[3], c);
+            return amt * t1 + (1 - amt) * t2;
+        }
+        case 4: {  // FloatCheckerboardTexture
+            Float w = Checker(node, c), t0 = 0, t1 = 0;
+            if (w != 1) t0 = EvalF(in[2], c);
+            if (w != 0) t1 = EvalF(in[3], c);
+            return (1 - w) * t0 + w * t1;
+        }
+        case 5: {  // FloatBilerpTexture
+            Float st[2], dst[4];
+            Map2D(node, c, st, dst);
+            return (1 - st[0]) * (1 - st[1]) * q[22] + st[0] * (1 - st[1]) * q[24] + (1 - st[0]) * st[1] * q[23] +
+                   st[0] * st[1] * q[25];
+        }
+        default: {  // FloatImageTexture
+            Float st[2], dst[4];
+            Map2D(node, c, st, dst);
+            st[1] = 1 - st[1];
+            Float v;
+            images[in[5]].Filter(in[7], q[27], st[0], st[1], dst[0], dst[2], dst[1], dst[3], 1, &v);
+            v = q[26] * v;
+            return (in[1] & 8) ? std::max<Float>(0, 1 - v) : v;
+        }
+        }
+    }
+    Spectrum ConstS(int node, int k, const Wavelengths &L) const {
+        const float *s = Spec(node, k);
+        Spectrum r;
+        for (int i = 0; i < NS; ++i) r[i] = s[0] != 0 ? s[5] * Sigmoid(s[2], s[3], s[4], L.lambda[i]) : s[1];
+        return r;
+    }
+    Spectrum EvalS(int node, const OTexCtx &c, const Wavelengths &L) const {
+        const int32_t *in = Info(node);
+        const float *q = Par(node);
+        switch (in[0]) {
+        case 0: return ConstS(node, 0, L);
+        case 1: {
+            Float sc = EvalF(in[3], c);
+            if (sc == 0) return Spectrum(0.f);
+            return EvalS(in[2], c, L) * sc;
+        }
+        case 2: {
+            Float amt = EvalF(in[4], c);
+            Spectrum t1, t2;
+            if (amt != 1) t1 = EvalS(in[2], c, L);
+            if (amt != 0) t2 = EvalS(in[3], c, L);
+            return t1 * (1 - amt) + t2 * amt;
+        }
+        case 3: {
+            Float amt = AbsDotN(c.n, Vec(q[22], q[23], q[24]));
+            Spectrum t1, t2;
+            if (amt != 0) t1 = EvalS(in[2], c, L);
+            if (amt != 1) t2 = EvalS(in[3], c, L);
+            return t1 * amt + t2 * (1 - amt);
+        }
+        case 4: {
+            Float w = Checker(node, c);
+            Spectrum t0, t1;
+            if (w != 1) t0 = EvalS(in[2], c, L);
+            if (w != 0) t1 = EvalS(in[3], c, L);
+            return t0 * (1 - w) + t1 * w;
+        }
+        case 5: {  // Bilerp({s, t}, {v00, v10, v01, v11}) (util/spectrum.h:734-738)
+            Float st[2], dst[4];
+            Map2D(node, c, st, dst);
+            return ConstS(node, 0, L) * ((1 - st[0]) * (1 - st[1])) + ConstS(node, 1, L) * (st[0] * (1 - st[1])) +
+                   ConstS(node, 2, L) * ((1 - st[0]) * st[1]) + ConstS(node, 3, L) * (st[0] * st[1]);
+        }
+        default: {  // SpectrumImageTexture (textures.cpp:359-405)
+            Float st[2], dst[4], rgb[3];
+            Map2D(node, c, st, dst);
+            st[1] = 1 - st[1];
+            images[in[5]].Filter(in[7], q[27], st[0], st[1], dst[0], dst[2], dst[1], dst[3], 3, rgb);
+            for (int k = 0; k < 3; ++k) {
+                rgb[k] = q[26] * rgb[k];
+                rgb[k] = std::max<Float>(0, (in[1] & 8) ? 1 - rgb[k] : rgb[k]);
+            }
+            Float co[3], scale = 1;
+            if (((in[1] >> 1) & 3) == 0) {  // RGBAlbedoSpectrum(Clamp(rgb, 0, 1))
+                ORGBCoeffs(Clamp(rgb[0], 0, 1), Clamp(rgb[1], 0, 1), Clamp(rgb[2], 0, 1), co);
+                Spectrum r;
+                for (int i = 0; i < NS; ++i) r[i] = Sigmoid(co[0], co[1], co[2], L.lambda[i]);
+                return r;
+            }
+            Float m = std::max({rgb[0], rgb[1], rgb[2]});  // RGBUnboundedSpectrum
+            scale = 2 * m;
+            if (scale != 0) ORGBCoeffs(rgb[0] / scale, rgb[1] / scale, rgb[2] / scale, co);
+            else ORGBCoeffs(0, 0, 0, co);
+            Spectrum r;
+            for (int i = 0; i < NS; ++i) r[i] = scale * Sigmoid(co[0], co[1], co[2], L.lambda[i]);
+            return r;
+        }
+        }
+    }
+};
+
 // ---------------------------------------------------------------- integrator
 struct Renderer {
     Scene S;
+    OTextures tex;
     Lights lights;
     Media M;
     PixelFilter filt;
@@ -2828,14 +3517,34 @@ struct Renderer {
                     bx.Tt[i] = Clamp(scale * t, 0, 1);
                 }
             } else if (bx.type == 0) {
-                for (int i = 0; i < NS; ++i) {
-                    Float r = f->material_constant[mat] ? mc[3] : Sigmoid(mc[0], mc[1], mc[2], lambda.lambda[i]);
-                    bx.R[i] = Clamp(r, 0, 1);
+                // DiffuseMaterial::GetBxDF: Clamp(texEval(reflectance), 0, 1)
+                const int rt = f->material_tex ? f->material_tex[4 * mat] : -1;
+                if (rt >= 0) {
+                    const Spectrum R = tex.EvalS(rt, tex.Ctx(si), lambda);
+                    for (int i = 0; i < NS; ++i) bx.R[i] = Clamp(R[i], 0, 1);
+                } else {
+                    for (int i = 0; i < NS; ++i) {
+                        Float r = f->material_constant[mat] ? mc[3] : Sigmoid(mc[0], mc[1], mc[2], lambda.lambda[i]);
+                        bx.R[i] = Clamp(r, 0, 1);
+                    }
                 }
             } else {
                 const float *mp = f->material_params + 4 * mat;
                 bx.mf.ax = mp[0];  // alphas arrive remapped and clamped (TrowbridgeReitz ctor)
                 bx.mf.ay = mp[1];
+                const int32_t *mt = f->material_tex ? f->material_tex + 4 * mat : nullptr;
+                OTexCtx tctx;
+                if (mt && (mt[0] >= 0 || mt[1] >= 0)) tctx = tex.Ctx(si);
+                if (mt && mt[1] >= 0) {
+                    // texEval(uRoughness), texEval(vRoughness), RoughnessToAlpha if remapped,
+                    // TrowbridgeReitzDistribution(urough, vrough) (materials.h:182-204, :491-511)
+                    Float ur = tex.EvalF(mt[1], tctx), vr = tex.EvalF(mt[2], tctx);
+                    if (mt[3]) {
+                        ur = std::sqrt(ur);
+                        vr = std::sqrt(vr);
+                    }
+                    bx.mf = TRDistribution(ur, vr);
+                }
                 bx.eta = mp[2] == 0 ? 1.f : mp[2];
                 if ((bx.type == 1 || bx.type == 6) && f->material_spectra[2 * mat] >= 0) {
                     // DielectricMaterial::GetBxDF (materials.cpp:25-49): a spectral eta is taken at
@@ -2859,6 +3568,15 @@ struct Renderer {
                             bx.kS[i] = PLEval(f->pl_lambda + b, f->pl_value + b, f->pl_offsets[ks + 1] - b, l);
                         } else {
                             Float r = Clamp(Sigmoid(mc[0], mc[1], mc[2], l), 0, .9999f);
+                            bx.etaS[i] = 1;
+                            bx.kS[i] = 2 * std::sqrt(r) / std::sqrt(std::max<Float>(0, 1 - r));
+                        }
+                    }
+                    if (mt && mt[0] >= 0) {
+                        // ConductorMaterial::GetBxDF: r = Clamp(texEval(reflectance), 0, .9999)
+                        const Spectrum R = tex.EvalS(mt[0], tctx, lambda);
+                        for (int i = 0; i < NS; ++i) {
+                            Float r = Clamp(R[i], 0, .9999f);
                             bx.etaS[i] = 1;
                             bx.kS[i] = 2 * std::sqrt(r) / std::sqrt(std::max<Float>(0, 1 - r));
                         }
@@ -3001,6 +3719,8 @@ int oracle_intersect_tr(const pbrt_scene_flat *flat, const pbrt_scene_info *info
     Renderer r;
     r.f = flat;
     r.S.Init(flat, info);
+    if (flat->n_tex_nodes > 0 && (!g_rgbTable || !g_ewaLut)) return -2;  // oracle_set_rgb_table first
+    r.tex.Init(flat, info->spp, info->xres, info->yres);
     r.M.f = flat;
     r.M.n = flat->n_media;
     const int nt = std::max(1, std::min<int>(16, (int)std::thread::hardware_concurrency()));
@@ -3037,6 +3757,8 @@ int oracle_render(const pbrt_scene_flat *flat, const pbrt_scene_info *info, cons
     Renderer r;
     r.f = flat;
     r.S.Init(flat, info);
+    if (flat->n_tex_nodes > 0 && (!g_rgbTable || !g_ewaLut)) return -2;  // oracle_set_rgb_table first
+    r.tex.Init(flat, info->spp, info->xres, info->yres);
     r.lights.Init(flat);
     r.lights.uniformFlag = uniformLightSampler != 0;
     r.M.f = flat;
@@ -3127,6 +3849,77 @@ int oracle_light_bvh(const pbrt_scene_flat *flat, const float *lights13, int n, 
     }
     if (trails) std::copy(b.trail.begin(), b.trail.end(), trails);
     return (int)b.nodes.size();
+}
+
+// ---- textures
+void oracle_set_rgb_table(const float *table, const float *ewaLut) {
+    g_rgbTable = table;
+    g_ewaLut = ewaLut;
+}
+// the oracle's texture evaluation at a hit (p, n, dpdu, dpdv, uv): out[0..3] uv derivatives,
+// then the spectrum at each of the n wavelengths (slot 0) or the float texture (slots 1, 2)
+int oracle_texture_eval(const pbrt_scene_flat *flat, const pbrt_scene_info *info, int material, int slot,
+                        const float *hit, const float *lambda, int n, float *out) {
+    if (!g_rgbTable || !g_ewaLut) return -2;
+    OTextures t;
+    t.Init(flat, info->spp, info->xres, info->yres);
+    const int node = flat->material_tex[4 * material + slot];
+    if (node < 0) return -1;
+    Interaction si;
+    si.p = Vec(hit[0], hit[1], hit[2]);
+    si.n = Vec(hit[3], hit[4], hit[5]);
+    si.dpdu = Vec(hit[6], hit[7], hit[8]);
+    si.dpdv = Vec(hit[9], hit[10], hit[11]);
+    si.uv[0] = hit[12];
+    si.uv[1] = hit[13];
+    const OTexCtx c = t.Ctx(si);
+    out[0] = c.dudx;
+    out[1] = c.dudy;
+    out[2] = c.dvdx;
+    out[3] = c.dvdy;
+    if (slot != 0) {
+        out[4] = t.EvalF(node, c);
+        return 0;
+    }
+    for (int i = 0; i < n; ++i) {
+        Wavelengths L = Wavelengths::SampleUniform(0.f);
+        for (int k = 0; k < NS; ++k) L.lambda[k] = lambda[i];
+        out[4 + i] = t.EvalS(node, c, L)[0];
+    }
+    return 0;
+}
+// the oracle's FindMinimumDifferentials: pos dx, pos dy, dir dx, dir dy
+int oracle_camera_min_diff(const pbrt_scene_flat *flat, const pbrt_scene_info *info, float *out12) {
+    OTextures t;
+    t.f = flat;
+    t.fullRes[0] = info->xres;
+    t.fullRes[1] = info->yres;
+    t.FindMinimumDifferentials();
+    const Vec v[4] = {t.minPosDx, t.minPosDy, t.minDirDx, t.minDirDy};
+    for (int k = 0; k < 4; ++k)
+        for (int j = 0; j < 3; ++j) out12[3 * k + j] = v[k][j];
+    return 0;
+}
+// one level of the oracle's own MIPMap pyramid of image `image`, in its stored format:
+// returns the byte count (writes at most cap bytes to out), w / h of the level
+int64_t oracle_image_level(const pbrt_scene_flat *flat, int image, int level, uint8_t *out, int64_t cap, int *w, int *h) {
+    OImage im;
+    const int32_t *ri = flat->image_raw_info + 8 * image;
+    im.format = ri[2];
+    im.nc = ri[3];
+    im.wrap = flat->image_info[8 * image + 3];
+    im.enc.Init(ri[4], flat->image_raw_gamma[image], flat->image_luts + 256 * image);
+    im.Build(flat->image_raw_data + flat->image_raw_offset[image], ri[0], ri[1]);
+    if (level < 0 || level >= im.nLevels) return -1;
+    *w = im.w[level];
+    *h = im.h[level];
+    const uint8_t *src;
+    int64_t bytes;
+    if (im.format == 0) src = im.l8[level].data(), bytes = (int64_t)im.l8[level].size();
+    else if (im.format == 1) src = (const uint8_t *)im.l16[level].data(), bytes = 2 * (int64_t)im.l16[level].size();
+    else src = (const uint8_t *)im.l32[level].data(), bytes = 4 * (int64_t)im.l32[level].size();
+    std::memcpy(out, src, (size_t)std::min(bytes, cap));
+    return bytes;
 }
 
 // ---- component entry points checked against tests/golden/reference_components.json

@@ -47,7 +47,63 @@ def lib():
         _lib.oracle_set_cr_math.argtypes = [ctypes.c_int]
         _lib.oracle_light_bvh.argtypes = [vp, vp, ctypes.c_int, vp, vp, vp, ctypes.c_int]
         _lib.oracle_intersect_tr.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int, vp]
+        _lib.oracle_set_rgb_table.argtypes = [vp, vp]
+        _lib.oracle_texture_eval.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_int, vp]
+        _lib.oracle_camera_min_diff.argtypes = [vp, vp, vp]
+        _lib.oracle_image_level.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int64,
+                                            ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+        _lib.oracle_image_level.restype = ctypes.c_int64
+        _set_tables(_lib)
     return _lib
+
+
+# Reference data tables the oracle's texture code reads: the rgb2spec_opt coefficient table
+# (pbrt-v4_amd/data/rgbspec_srgb.bin, written by the build) and MIPFilterLUT
+# (pbrt-v4_amd/data/spectral_data.txt, the literals of util/mipmap.cpp)
+_TABLES = {}
+
+
+def _set_tables(l):
+    data = HERE.parent / "pbrt-v4_amd" / "data"
+    rgb = data / "rgbspec_srgb.bin"
+    if not rgb.exists():
+        return
+    _TABLES["rgb"] = np.fromfile(rgb, dtype=np.float32)
+    for line in (data / "spectral_data.txt").read_text().splitlines():
+        if line.startswith("MIPFilterLUT "):
+            _TABLES["ewa"] = np.array(line.split()[2:], dtype=np.float32)
+    l.oracle_set_rgb_table(_TABLES["rgb"].ctypes.data, _TABLES["ewa"].ctypes.data)
+
+
+def texture_eval(scene, material, slot, hit14, lambdas=()):
+    """The oracle's evaluation of a textured material parameter at a hit (p, n, dpdu, dpdv, uv):
+    ((dudx, dudy, dvdx, dvdy), values) as pbrt_amd.Scene.texture_eval returns them."""
+    info, flat = scene.info, scene.flat()
+    lam, hit = f32(lambdas), f32(hit14)
+    out = np.zeros(5 + lam.size, np.float32)
+    rc = lib().oracle_texture_eval(ctypes.byref(flat), ctypes.byref(info), material, slot, hit.ctypes.data,
+                                   lam.ctypes.data, lam.size, out.ctypes.data)
+    assert rc == 0, rc
+    return out[:4].copy(), (out[4:4 + lam.size].copy() if slot == 0 else float(out[4]))
+
+
+def camera_min_diff(scene):
+    """The oracle's own FindMinimumDifferentials: [pos dx, pos dy, dir dx, dir dy] x 3"""
+    info, flat = scene.info, scene.flat()
+    out = np.zeros(12, np.float32)
+    lib().oracle_camera_min_diff(ctypes.byref(flat), ctypes.byref(info), out.ctypes.data)
+    return out
+
+
+def image_level(scene, image, level):
+    """Level `level` of the oracle's own MIPMap pyramid of image `image`, as stored bytes"""
+    flat = scene.flat()
+    w, h = ctypes.c_int(), ctypes.c_int()
+    n = lib().oracle_image_level(ctypes.byref(flat), image, level, None, 0, ctypes.byref(w), ctypes.byref(h))
+    assert n >= 0
+    buf = np.zeros(n, np.uint8)
+    lib().oracle_image_level(ctypes.byref(flat), image, level, buf.ctypes.data, n, ctypes.byref(w), ctypes.byref(h))
+    return buf, w.value, h.value
 
 
 class cr_math:

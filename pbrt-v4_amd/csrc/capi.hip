@@ -14,6 +14,7 @@
 #include "host/bvh.h"
 #include "host/image.h"
 #include "host/scene.h"
+#include "host/texture.h"
 #include "kernels/device.h"
 
 namespace pbrt_amd {
@@ -87,6 +88,132 @@ static void MediumTables(const SceneDesc &s, std::vector<int32_t> *info, std::ve
     }
 }
 
+// Texture tables in the device layout (core/texture_eval.h), built on the host: uploaded by
+// BuildDevice, viewed in place by the host debug entry points, handed to the oracle by
+// pbrt_scene_get_flat.
+struct TexTables {
+    std::vector<DeviceTexNode> nodes;
+    std::vector<DeviceTexSpec> spec;
+    std::vector<DeviceImage> images;
+    std::vector<DeviceImageLevel> levels;
+    std::vector<uint8_t> data;
+    std::vector<float> luts;
+    std::vector<DeviceTexInstr> instrs;
+    std::vector<DeviceTexProgram> progs;
+    std::vector<int32_t> matTex;      // [nMaterials][4] program indices + remap
+    std::vector<int32_t> matTexNode;  // [nMaterials][4] the programs' root nodes + remap (oracle)
+    std::vector<int32_t> nodeInfo, imageInfo, levelInfo, rawInfo;
+    std::vector<float> nodeParams, specFlat, rawGamma;
+    std::vector<uint8_t> rawData;
+    std::vector<uint64_t> rawOffset;
+};
+static void BuildTexTables(const SceneDesc &s, TexTables *t) {
+    *t = TexTables{};
+    for (size_t i = 0; i < s.textures.size(); ++i) {
+        const TextureDesc &d = s.textures[i];
+        DeviceTexNode n{};
+        n.kind = d.kind;
+        n.flags = (d.spectrum ? 1 : 0) | (d.specType << 1) | (d.invert ? 8 : 0) | (d.mapping == kMap3D ? 16 : 0);
+        n.child0 = d.child[0];
+        n.child1 = d.child[1];
+        n.child2 = d.child[2];
+        n.image = d.image;
+        n.mapping = d.mapping == kMap3D ? 0 : d.mapping;
+        n.filter = d.filter;
+        for (int k = 0; k < 12; ++k) n.p[k] = d.textureFromRender[k];
+        for (int k = 0; k < 3; ++k) n.p[12 + k] = d.vs[k], n.p[15 + k] = d.vt[k];
+        for (int k = 0; k < 4; ++k) n.p[18 + k] = d.map[k];
+        for (int k = 0; k < 4; ++k) n.p[22 + k] = d.fvalue[k];
+        if (d.kind == kTexDirectionMix)
+            for (int k = 0; k < 3; ++k) n.p[22 + k] = d.dir[k];
+        n.p[26] = d.scale;
+        n.p[27] = d.maxAniso;
+        t->nodes.push_back(n);
+        for (int k = 0; k < 4; ++k) {
+            const TexSpectrumConst &c = d.svalue[k];
+            t->spec.push_back(DeviceTexSpec{c.rgb ? 1.f : 0.f, c.value, c.c[0], c.c[1], c.c[2], c.scale, 0.f, 0.f});
+        }
+        t->nodeInfo.insert(t->nodeInfo.end(), {n.kind, n.flags, n.child0, n.child1, n.child2, n.image, n.mapping, n.filter});
+        t->nodeParams.insert(t->nodeParams.end(), n.p, n.p + 28);
+        for (int k = 0; k < 4; ++k) {
+            const DeviceTexSpec &q = t->spec[4 * i + k];
+            t->specFlat.insert(t->specFlat.end(), {q.rgb, q.value, q.c0, q.c1, q.c2, q.scale, 0.f, 0.f});
+        }
+    }
+    for (size_t i = 0; i < s.images.size(); ++i) {
+        const ImageDesc &im = s.images[i];
+        DeviceImage di{};
+        di.format = im.format;
+        di.nc = im.nc;
+        di.nLevels = (int)im.levelRes.size();
+        di.wrap = im.wrap;
+        di.levelBase = (int)t->levels.size();
+        di.lutBase = (int)(256 * i);
+        const uint64_t base = t->data.size();
+        t->data.insert(t->data.end(), im.data.begin(), im.data.end());
+        t->data.resize((t->data.size() + 15) & ~size_t(15));
+        for (size_t l = 0; l < im.levelRes.size(); ++l) {
+            const uint64_t off = base + im.levelOffset[l];
+            t->levels.push_back(DeviceImageLevel{im.levelRes[l][0], im.levelRes[l][1], (uint32_t)off, (uint32_t)(off >> 32)});
+            t->levelInfo.insert(t->levelInfo.end(), {im.levelRes[l][0], im.levelRes[l][1], (int32_t)(uint32_t)off,
+                                                     (int32_t)(uint32_t)(off >> 32)});
+        }
+        t->luts.insert(t->luts.end(), im.toLinear.begin(), im.toLinear.end());
+        t->images.push_back(di);
+        t->imageInfo.insert(t->imageInfo.end(), {di.format, di.nc, di.nLevels, di.wrap, di.levelBase, di.lutBase, 0, 0});
+        t->rawInfo.insert(t->rawInfo.end(), {im.rawW, im.rawH, im.format, im.nc, im.encoding, 0, 0, 0});
+        t->rawGamma.push_back(im.gamma);
+        t->rawOffset.push_back(t->rawData.size());
+        t->rawData.insert(t->rawData.end(), im.raw.begin(), im.raw.end());
+    }
+    for (const TexInstr &in : s.texInstrs)
+        t->instrs.push_back(DeviceTexInstr{in.op | (in.a << 8) | (in.b << 16) | (in.c << 24), in.node});
+    for (const TexProgram &pg : s.texPrograms) {
+        int simple = 0;
+        if (pg.spectrum && pg.n1 == 1 && pg.n2 == 1) {
+            const TexInstr &a = s.texInstrs[pg.p1], &b = s.texInstrs[pg.p2];
+            simple = a.op == kT1SImage && a.a == 0 && b.op == kT2RGBReg && b.a == 0 && b.b == 0;
+        }
+        t->progs.push_back(DeviceTexProgram{pg.p1, pg.n1, pg.p2, pg.n2, pg.result, pg.nRegs, simple, 0});
+    }
+    for (const MaterialDesc &m : s.materials) {
+        t->matTex.insert(t->matTex.end(), {m.texReflectance, m.texURough, m.texVRough, m.remapRoughness ? 1 : 0});
+        auto root = [&](int p) { return p >= 0 ? s.texPrograms[p].root : -1; };
+        t->matTexNode.insert(t->matTexNode.end(),
+                             {root(m.texReflectance), root(m.texURough), root(m.texVRough), m.remapRoughness ? 1 : 0});
+    }
+}
+static CameraDiff MakeCameraDiff(const SceneDesc &s) {
+    CameraDiff c{};
+    for (int k = 0; k < 12; ++k) c.cameraFromRender[k] = s.cameraFromRender[k];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) c.renderFromCamera[3 * i + j] = (float)s.camera.renderFromCamera[i][j];
+    c.minPosDx = V3(s.minPosDx[0], s.minPosDx[1], s.minPosDx[2]);
+    c.minPosDy = V3(s.minPosDy[0], s.minPosDy[1], s.minPosDy[2]);
+    c.minDirDx = V3(s.minDirDx[0], s.minDirDx[1], s.minDirDx[2]);
+    c.minDirDy = V3(s.minDirDy[0], s.minDirDy[1], s.minDirDy[2]);
+    c.sppScale = std::max<float>(.125f, 1 / std::sqrt((float)s.spp));  // cameras.h:187-190
+    return c;
+}
+// a TexView over host copies (debug entry points; the device view points at DevBufs)
+static TexView HostTexView(const TexTables &t) {
+    const std::vector<float> &rgb = RGBToSpectrumTableData();
+    TexView v{};
+    v.nodes = t.nodes.data();
+    v.spec = t.spec.data();
+    v.images = t.images.data();
+    v.levels = t.levels.data();
+    v.data = t.data.data();
+    v.luts = t.luts.data();
+    v.instrs = t.instrs.data();
+    v.progs = t.progs.data();
+    v.rgbZNodes = rgb.data();
+    v.rgbCoeffs = rgb.data() + 64;
+    v.ewaLut = GetSpectralData().mipFilterLUT.data();
+    v.nProgs = (int)t.progs.size();
+    return v;
+}
+
 struct pbrt_scene {
     SceneDesc desc;
     // flattened copies for pbrt_scene_get_flat
@@ -96,8 +223,10 @@ struct pbrt_scene {
     std::vector<int32_t> tris, lightPrim, lightSpectrum, lightTwoSided, infSpectrum, matConstant, nodeInfo, matType,
         matSpectra, plOffsets, infDistant, uniformOrder;
     std::vector<float> deltaLights;
+    TexTables tex;
     void Flatten() {
         const SceneDesc &s = desc;
+        BuildTexTables(s, &tex);
         verts.clear();
         for (V3 v : s.verts) {
             verts.push_back(v.x);
@@ -230,6 +359,16 @@ struct pbrt_context {
     DevBuf<DeviceAreaLight> lights;
     DevBuf<int> mediumInfo, primMedium;
     DevBuf<float> mediumParams, mediumValues, filterTab;
+    // textures
+    DevBuf<DeviceTexNode> texNodes;
+    DevBuf<DeviceTexSpec> texSpec;
+    DevBuf<DeviceImage> texImages;
+    DevBuf<DeviceImageLevel> texLevels;
+    DevBuf<uint8_t> texData;
+    DevBuf<float> texLuts, rgbTable, ewaLut;
+    DevBuf<DeviceTexInstr> texInstrs;
+    DevBuf<DeviceTexProgram> texProgs;
+    DevBuf<int> matTex;
     // wavefront buffers
     int64_t maxPaths = 0;
     DevBuf<float> fState;
@@ -592,7 +731,46 @@ static void BuildDevice(pbrt_context *c) {
     S.regularize = s.regularize ? 1 : 0;
     S.smoothDielectrics = !s.regularize;
     for (auto &m : s.materials)
-        if (m.type == kMatDielectricT && !(std::fmax(m.alphaX, m.alphaY) < 1e-3f)) S.smoothDielectrics = 0;
+        if (m.type == kMatDielectricT && (!(std::fmax(m.alphaX, m.alphaY) < 1e-3f) || m.texURough >= 0))
+            S.smoothDielectrics = 0;
+    // textures: expression tables, pyramids, the RGB->spectrum table, camera differentials
+    {
+        TexTables tt;
+        BuildTexTables(s, &tt);
+        c->matTex.Upload(tt.matTex);
+        S.matTex = (const int4 *)c->matTex.p;
+        S.textured = s.texPrograms.empty() ? 0 : 1;
+        S.tex = TexView{};
+        if (S.textured) {
+            if (c->volumetric)
+                throw Error("textures together with the volumetric path (media, interface, layered, thin dielectric, "
+                            "diffuse transmission or dispersive materials) are not supported yet");
+            c->texNodes.Upload(tt.nodes);
+            c->texSpec.Upload(tt.spec);
+            c->texImages.Upload(tt.images);
+            c->texLevels.Upload(tt.levels);
+            if (tt.data.empty()) tt.data.push_back(0);
+            c->texData.Upload(tt.data);
+            c->texLuts.Upload(tt.luts);
+            c->texInstrs.Upload(tt.instrs);
+            c->texProgs.Upload(tt.progs);
+            c->rgbTable.Upload(RGBToSpectrumTableData());
+            c->ewaLut.Upload(std::vector<float>(GetSpectralData().mipFilterLUT.begin(), GetSpectralData().mipFilterLUT.end()));
+            S.tex.nodes = c->texNodes.p;
+            S.tex.spec = c->texSpec.p;
+            S.tex.images = c->texImages.p;
+            S.tex.levels = c->texLevels.p;
+            S.tex.data = c->texData.p;
+            S.tex.luts = c->texLuts.p;
+            S.tex.instrs = c->texInstrs.p;
+            S.tex.progs = c->texProgs.p;
+            S.tex.rgbZNodes = c->rgbTable.p;
+            S.tex.rgbCoeffs = c->rgbTable.p + 64;
+            S.tex.ewaLut = c->ewaLut.p;
+            S.tex.nProgs = (int)tt.progs.size();
+            S.camDiff = MakeCameraDiff(s);
+        }
+    }
     S.nAreaLights = (int)s.areaLights.size();
     S.lightPrim = c->lightPrim.p;
     S.lightScale = c->lightScale.p;
@@ -1024,7 +1202,7 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
             const bool lean = !noLean && c->S.samplerType == 0 &&
                               (uint64_t)(st.firstSample + nS) * haltonStride <= (1ull << 24) &&
                               c->S.shadeLds.lightsInLds && c->S.shadeLds.denseInLds && c->S.triShade == nullptr &&
-                              c->S.nDelta == 0;
+                              c->S.nDelta == 0 && !c->S.textured;
             for (int depth = 0; depth <= s.maxDepth; ++depth) {
                 // closest-hit launches are event-timed in the first pass of a render only: the
                 // passes are statistically identical and each event pair costs a queue gap
@@ -1195,6 +1373,30 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
     f->inf_distant = scene->infDistant.data();
     f->uniform_order = scene->uniformOrder.data();
     f->scene_radius = s.sceneRadius;
+    {
+        const TexTables &t = scene->tex;
+        f->n_tex_nodes = (int)s.textures.size();
+        f->n_images = (int)s.images.size();
+        f->tex_node_info = t.nodeInfo.data();
+        f->tex_node_params = t.nodeParams.data();
+        f->tex_node_spec = t.specFlat.data();
+        f->image_info = t.imageInfo.data();
+        f->image_levels = t.levelInfo.data();
+        f->image_data = t.data.data();
+        f->image_luts = t.luts.data();
+        f->image_raw_info = t.rawInfo.data();
+        f->image_raw_gamma = t.rawGamma.data();
+        f->image_raw_offset = t.rawOffset.data();
+        f->image_raw_data = t.rawData.data();
+        f->material_tex = t.matTexNode.data();
+        for (int k = 0; k < 12; ++k) f->camera_from_render[k] = s.cameraFromRender[k];
+        for (int k = 0; k < 3; ++k) {
+            f->camera_min_diff[k] = s.minPosDx[k];
+            f->camera_min_diff[3 + k] = s.minPosDy[k];
+            f->camera_min_diff[6 + k] = s.minDirDx[k];
+            f->camera_min_diff[9 + k] = s.minDirDy[k];
+        }
+    }
     f->dense_spectra = scene->dense.data();
     f->sensor_xyz = scene->sensor.data();
     f->imaging_ratio = s.imagingRatio;
@@ -1610,6 +1812,46 @@ int pbrt_debug_rgb_coeffs(float r, float g, float b, float *c) {
         c[0] = v[0];
         c[1] = v[1];
         c[2] = v[2];
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+// The product's texture evaluation (core/texture_eval.h, the same code the shade kernels run)
+// on the host, for one material slot at a given hit: out[0..3] = dudx dudy dvdx dvdy, then the
+// texture's value at each of the n wavelengths (reflectance) or out[4] (a roughness).
+int pbrt_debug_texture_eval(const pbrt_scene *scene, int material, int slot, const float *hit14, const float *lambda,
+                            int n, float *out) {
+    try {
+        if (!scene || !hit14 || !out) return Fail("null argument");
+        const SceneDesc &s = scene->desc;
+        if (material < 0 || material >= (int)s.materials.size()) return Fail("material index out of range");
+        const MaterialDesc &m = s.materials[material];
+        const int prog = slot == 0 ? m.texReflectance : (slot == 1 ? m.texURough : m.texVRough);
+        if (prog < 0) return Fail("material parameter is not textured");
+        const TexView T = HostTexView(scene->tex);
+        const CameraDiff cd = MakeCameraDiff(s);
+        TexEvalCtx c;
+        c.p = V3(hit14[0], hit14[1], hit14[2]);
+        c.n = V3(hit14[3], hit14[4], hit14[5]);
+        const V3 dpdu(hit14[6], hit14[7], hit14[8]), dpdv(hit14[9], hit14[10], hit14[11]);
+        c.u = hit14[12];
+        c.v = hit14[13];
+        UVDerivatives(cd, c.p, c.n, dpdu, dpdv, &c);
+        out[0] = c.dudx;
+        out[1] = c.dudy;
+        out[2] = c.dvdx;
+        out[3] = c.dvdy;
+        const DeviceTexProgram pg = T.progs[prog];
+        float R[kTexMaxRegs];
+        TexPhase1(T, pg, c, R);
+        if (slot != 0) {
+            out[4] = R[pg.result];
+            return 0;
+        }
+        for (int i = 0; i < n; ++i)
+            out[4 + i] = pg.simple ? SigmoidPolynomial(R[0], R[1], R[2], lambda[i]) : TexPhase2(T, pg, R, lambda[i]);
         return 0;
     } catch (const std::exception &e) {
         return Fail(e.what());

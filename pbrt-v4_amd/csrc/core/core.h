@@ -547,6 +547,8 @@ struct TriShading {
 struct TriSurface {
     V3 p, pErr, n, dpdu;
     V3 ns, dpdus;  // shading normal and shading dpdu (== n, dpdu without vertex normals)
+    V3 dpdv;       // geometric dpdv and the hit's uv (texture lookups, surfscatter.cpp:74-104)
+    float uv[2];
 };
 // Triangle::InteractionFromIntersection (shapes.h:884-1010) without the dndu/dndv terms (bump
 // mapping / ray differentials only) and with SetShadingGeometry(..., true) (interaction.h:194)
@@ -580,6 +582,9 @@ PHD TriSurface TriangleSurface(V3 p0, V3 p1, V3 p2, float b0, float b1, float b2
     V3 pHit = b0 * p0 + b1 * p1 + b2 * p2;
     V3 pAbsSum = Abs(b0 * p0) + Abs(b1 * p1) + Abs(b2 * p2);
     ToPoint3fi(pHit, gamma(7) * pAbsSum, &s.p, &s.pErr);
+    s.dpdv = dpdv;
+    s.uv[0] = b0 * uv[0][0] + b1 * uv[1][0] + b2 * uv[2][0];
+    s.uv[1] = b0 * uv[0][1] + b1 * uv[1][1] + b2 * uv[2][1];
     V3 n = Normalize(Cross(dp02, dp12));
     if (flip) n = -n;
     s.n = n;

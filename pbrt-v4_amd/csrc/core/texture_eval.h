@@ -1,0 +1,655 @@
+// Texture evaluation shared by the HIP kernels and the host (debug entry points): the
+// wavefront's texture-differential estimate, pbrt's texture mappings, MIPMap filtering and the
+// texture expressions materials read, restated from the reference:
+//   differentials for (u,v)                 wavefront/surfscatter.cpp:74-104
+//   CameraBase::Approximate_dp_dxy          cameras.h:167-195 (RotateFromTo transform.h:249-270)
+//   TextureEvalContext / TexCoord2D         textures.h:30-83 (the wavefront sets no dpdx/dpdy:
+//                                           workitems.h:288-304, so non-uv mappings see zero
+//                                           differentials)
+//   UV / spherical / cylindrical / planar   textures.h:86-202; point mapping textures.h:229-246
+//   Checkerboard                            textures.cpp:183-217
+//   Float/Spectrum Constant, Scaled, Mix,   textures.h:269-422, 841-956, 1066-1114
+//     DirectionMix, Bilerp, Checkerboard
+//   Float/SpectrumImageTexture::Evaluate    textures.h:586-597, textures.cpp:359-405
+//   MIPMap::Filter / Bilerp / Texel / EWA   util/mipmap.cpp:208-375, util/image.h:255-292
+//   RGBToSpectrumTable::operator()          util/color.cpp:36-75
+//   RGBAlbedo/UnboundedSpectrum             util/spectrum.h, util/spectrum.cpp:240-244
+#pragma once
+
+#include "core.h"
+
+namespace pbrt_amd {
+
+// ---------------------------------------------------------------- device tables
+// One texture expression node (host: scene.h TextureDesc).  flags: bit0 spectrum texture,
+// bits 1-2 SpectrumType, bit 3 invert, bit 4 3D checkerboard.  p[]: mapping textureFromRender
+// 3x4 [0..11], planar vs [12..14] vt [15..17], uv su sv du dv / planar ds dt [18..21],
+// float constant / bilerp v00 v01 v10 v11 / directionmix dir [22..25], image scale [26],
+// maxAnisotropy [27].
+struct DeviceTexNode {
+    int kind, flags, child0, child1, child2, image, mapping, filter;
+    float p[28];
+};
+// a constant spectrum of a spectrum node (up to 4: constant value, bilerp corners):
+// rgb != 0: scale * sigmoid(c0, c1, c2), else the constant value
+struct DeviceTexSpec {
+    float rgb, value, c0, c1, c2, scale, pad0, pad1;
+};
+struct DeviceImage {
+    int format, nc, nLevels, wrap, levelBase, lutBase, pad0, pad1;
+};
+struct DeviceImageLevel {
+    int w, h;
+    uint32_t offLo, offHi;
+};
+// compiled expression: phase-1 and phase-2 instruction ranges (scene.h TexProgram)
+struct DeviceTexProgram {
+    int p1, n1, p2, n2, result, nRegs, simple, pad;  // simple: phase 2 is one RGB leaf at reg 0
+};
+struct DeviceTexInstr {
+    int op;    // op | a << 8 | b << 16 | c << 24
+    int node;
+};
+
+// phase-1 ops (once per hit: scalar registers)
+enum TexOp1 : int {
+    kT1FConst = 0, kT1FImage = 1, kT1FBilerp = 2, kT1CheckW = 3, kT1DirAmt = 4, kT1FScale = 5,
+    kT1FMix = 6, kT1FDMix = 7, kT1SImage = 8, kT1BilerpW = 9
+};
+// phase-2 ops (per wavelength: value stack)
+enum TexOp2 : int { kT2Const = 0, kT2RGBReg = 1, kT2Scale = 2, kT2Mix = 3, kT2DMix = 4, kT2Bilerp = 5 };
+constexpr int kTexMaxRegs = 16, kTexMaxStack = 8;
+
+struct TexView {
+    const DeviceTexNode *nodes;
+    const DeviceTexSpec *spec;  // [node * 4 + k]
+    const DeviceImage *images;
+    const DeviceImageLevel *levels;
+    const uint8_t *data;
+    const float *luts;          // [image][256] ToLinear of 8-bit texels
+    const DeviceTexInstr *instrs;
+    const DeviceTexProgram *progs;
+    const float *rgbZNodes;     // RGBToSpectrumTable scale[64]
+    const float *rgbCoeffs;     // RGBToSpectrumTable data[3][64][64][64][3]
+    const float *ewaLut;        // MIPFilterLUT[128]
+    int nProgs;
+};
+
+// TextureEvalContext as the wavefront material stage builds it (workitems.h:288-304)
+struct TexEvalCtx {
+    V3 p, n;
+    float u, v, dudx, dudy, dvdx, dvdy;
+};
+
+// ---------------------------------------------------------------- differentials
+struct CameraDiff {
+    float cameraFromRender[12];  // 3x4 (renderFromCamera^-1)
+    float renderFromCamera[9];   // upper 3x3
+    V3 minPosDx, minPosDy, minDirDx, minDirDy;
+    float sppScale;              // max(.125, 1 / sqrt(spp))
+};
+
+// Transform::ApplyInverse(Point3f) of a 3x4 inverse matrix (transform.h:387-398)
+PHD V3 ApplyInvPoint(const float *mi, V3 p) {
+    return V3((mi[0] * p.x + mi[1] * p.y) + (mi[2] * p.z + mi[3]), (mi[4] * p.x + mi[5] * p.y) + (mi[6] * p.z + mi[7]),
+              (mi[8] * p.x + mi[9] * p.y) + (mi[10] * p.z + mi[11]));
+}
+
+// CameraBase::Approximate_dp_dxy (cameras.h:167-195) for a static camera; p, n in render space
+PHD void ApproximateDpDxy(const CameraDiff &c, V3 p, V3 n, V3 *dpdx, V3 *dpdy) {
+    const float *m = c.renderFromCamera;
+    // CameraFromRender(p): renderFromCamera.ApplyInverse(p); of n: m^T n
+    const V3 pCamera = ApplyInvPoint(c.cameraFromRender, p);
+    const V3 nCamera(m[0] * n.x + m[3] * n.y + m[6] * n.z, m[1] * n.x + m[4] * n.y + m[7] * n.z,
+                     m[2] * n.x + m[5] * n.y + m[8] * n.z);
+    // DownZFromCamera = RotateFromTo(Normalize(pCamera), (0, 0, 1)): r and Transpose(r)
+    const V3 from = Normalize(pCamera), to(0, 0, 1);
+    V3 refl;
+    if (std::fabs(from.x) < 0.72f && std::fabs(to.x) < 0.72f) refl = V3(1, 0, 0);
+    else if (std::fabs(from.y) < 0.72f && std::fabs(to.y) < 0.72f) refl = V3(0, 1, 0);
+    else refl = V3(0, 0, 1);
+    const V3 u = refl - from, v = refl - to;
+    const float uu = Dot(u, u), vv = Dot(v, v), uv = Dot(u, v);
+    float r[3][3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            r[i][j] = float((i == j) ? 1 : 0) - 2 / uu * u[i] * u[j] - 2 / vv * v[i] * v[j] + 4 * uv / (uu * vv) * v[i] * u[j];
+    auto rot = [&](V3 a) {  // r a (a point with w = 1 has no translation to add: r[.][3] = 0)
+        return V3(r[0][0] * a.x + r[0][1] * a.y + r[0][2] * a.z, r[1][0] * a.x + r[1][1] * a.y + r[1][2] * a.z,
+                  r[2][0] * a.x + r[2][1] * a.y + r[2][2] * a.z);
+    };
+    auto rotInv = [&](V3 a) {  // Transpose(r) a
+        return V3(r[0][0] * a.x + r[1][0] * a.y + r[2][0] * a.z, r[0][1] * a.x + r[1][1] * a.y + r[2][1] * a.z,
+                  r[0][2] * a.x + r[1][2] * a.y + r[2][2] * a.z);
+    };
+    V3 pDownZ = rot(pCamera);
+    pDownZ = V3(pDownZ.x + 0.f, pDownZ.y + 0.f, pDownZ.z + 0.f);  // + r[.][3]
+    const V3 nDownZ = rot(nCamera);  // Normal transform through mInv = Transpose(r): r n
+    const float d = nDownZ.z * pDownZ.z;
+    const V3 xo = V3(0, 0, 0) + c.minPosDx, xd = V3(0, 0, 1) + c.minDirDx;
+    const float tx = -(DotN(nDownZ, xo) - d) / DotN(nDownZ, xd);
+    const V3 yo = V3(0, 0, 0) + c.minPosDy, yd = V3(0, 0, 1) + c.minDirDy;
+    const float ty = -(DotN(nDownZ, yo) - d) / DotN(nDownZ, yd);
+    const V3 px = xo + xd * tx, py = yo + yd * ty;
+    auto renderFromCamera = [&](V3 a) {
+        return V3(m[0] * a.x + m[1] * a.y + m[2] * a.z, m[3] * a.x + m[4] * a.y + m[5] * a.z,
+                  m[6] * a.x + m[7] * a.y + m[8] * a.z);
+    };
+    *dpdx = c.sppScale * renderFromCamera(rotInv(px - pDownZ));
+    *dpdy = c.sppScale * renderFromCamera(rotInv(py - pDownZ));
+}
+
+PHD bool IsFiniteF(float x) { return !std::isinf(x) && !std::isnan(x); }
+
+// surfscatter.cpp:74-104: screen-space (u,v) derivatives from dp/dx, dp/dy and dpdu, dpdv
+PHD void UVDerivatives(const CameraDiff &c, V3 p, V3 n, V3 dpdu, V3 dpdv, TexEvalCtx *ctx) {
+    V3 dpdx, dpdy;
+    ApproximateDpDxy(c, p, n, &dpdx, &dpdy);
+    const float ata00 = Dot(dpdu, dpdu), ata01 = Dot(dpdu, dpdv), ata11 = Dot(dpdv, dpdv);
+    float invDet = 1 / DifferenceOfProducts(ata00, ata11, ata01, ata01);
+    invDet = IsFiniteF(invDet) ? invDet : 0.f;
+    const float atb0x = Dot(dpdu, dpdx), atb1x = Dot(dpdv, dpdx);
+    const float atb0y = Dot(dpdu, dpdy), atb1y = Dot(dpdv, dpdy);
+    float dudx = DifferenceOfProducts(ata11, atb0x, ata01, atb1x) * invDet;
+    float dvdx = DifferenceOfProducts(ata00, atb1x, ata01, atb0x) * invDet;
+    float dudy = DifferenceOfProducts(ata11, atb0y, ata01, atb1y) * invDet;
+    float dvdy = DifferenceOfProducts(ata00, atb1y, ata01, atb0y) * invDet;
+    ctx->dudx = IsFiniteF(dudx) ? Clampf(dudx, -1e8f, 1e8f) : 0.f;
+    ctx->dvdx = IsFiniteF(dvdx) ? Clampf(dvdx, -1e8f, 1e8f) : 0.f;
+    ctx->dudy = IsFiniteF(dudy) ? Clampf(dudy, -1e8f, 1e8f) : 0.f;
+    ctx->dvdy = IsFiniteF(dvdy) ? Clampf(dvdy, -1e8f, 1e8f) : 0.f;
+}
+
+// ---------------------------------------------------------------- mappings
+struct TexCoord2 {
+    float s, t, dsdx, dsdy, dtdx, dtdy;
+};
+PHD V3 XformPoint34(const float *m, V3 p) {
+    return V3(m[0] * p.x + m[1] * p.y + m[2] * p.z + m[3], m[4] * p.x + m[5] * p.y + m[6] * p.z + m[7],
+              m[8] * p.x + m[9] * p.y + m[10] * p.z + m[11]);
+}
+PHD TexCoord2 MapST(const DeviceTexNode &nd, const TexEvalCtx &c) {
+    const float *q = nd.p;
+    TexCoord2 r;
+    if (nd.mapping == 0) {  // UVMapping
+        const float su = q[18], sv = q[19], du = q[20], dv = q[21];
+        r.dsdx = su * c.dudx;
+        r.dsdy = su * c.dudy;
+        r.dtdx = sv * c.dvdx;
+        r.dtdy = sv * c.dvdy;
+        r.s = su * c.u + du;
+        r.t = sv * c.v + dv;
+        return r;
+    }
+    const V3 pt = XformPoint34(q, c.p);
+    const V3 zero(0, 0, 0);  // textureFromRender(ctx.dpdx) with dpdx = 0
+    if (nd.mapping == 1) {  // SphericalMapping
+        const float x2y2 = Sqr(pt.x) + Sqr(pt.y);
+        const float sqrtx2y2 = std::sqrt(x2y2);
+        const V3 dsdp = V3(-pt.y, pt.x, 0) / (2 * kPi * x2y2);
+        const V3 dtdp = 1 / (kPi * (x2y2 + Sqr(pt.z))) * V3(pt.x * pt.z / sqrtx2y2, pt.y * pt.z / sqrtx2y2, -sqrtx2y2);
+        r.dsdx = Dot(dsdp, zero);
+        r.dsdy = Dot(dsdp, zero);
+        r.dtdx = Dot(dtdp, zero);
+        r.dtdy = Dot(dtdp, zero);
+        const V3 vec = Normalize(pt - V3(0, 0, 0));
+        float phi = ATan2f(vec.y, vec.x);
+        phi = (phi < 0) ? (phi + 2 * kPi) : phi;
+        r.s = SafeACos(vec.z) * kInvPi;
+        r.t = phi * (0.15915494309189533577f);
+        return r;
+    }
+    if (nd.mapping == 2) {  // CylindricalMapping
+        const float x2y2 = Sqr(pt.x) + Sqr(pt.y);
+        const V3 dsdp = V3(-pt.y, pt.x, 0) / (2 * kPi * x2y2), dtdp(0, 0, 1);
+        r.dsdx = Dot(dsdp, zero);
+        r.dsdy = Dot(dsdp, zero);
+        r.dtdx = Dot(dtdp, zero);
+        r.dtdy = Dot(dtdp, zero);
+        r.s = (kPi + ATan2f(pt.y, pt.x)) * 0.15915494309189533577f;
+        r.t = pt.z;
+        return r;
+    }
+    // PlanarMapping
+    const V3 vs(q[12], q[13], q[14]), vt(q[15], q[16], q[17]);
+    r.dsdx = Dot(vs, zero);
+    r.dsdy = Dot(vs, zero);
+    r.dtdx = Dot(vt, zero);
+    r.dtdy = Dot(vt, zero);
+    r.s = q[18] + Dot(pt, vs);
+    r.t = q[19] + Dot(pt, vt);
+    return r;
+}
+
+// Checkerboard (textures.cpp:183-217)
+PHD float CheckerD(float x) {
+    float y = x / 2 - std::floor(x / 2) - 0.5f;
+    return x / 2 + y * (1 - 2 * std::fabs(y));
+}
+PHD float CheckerBF(float x, float r) {
+    if (std::floor(x - r) == std::floor(x + r)) return 1 - 2 * ((int)std::floor(x) & 1);
+    return (CheckerD(x + r) - 2 * CheckerD(x) + CheckerD(x - r)) / Sqr(r);
+}
+PHD float CheckerboardWeight(const DeviceTexNode &nd, const TexEvalCtx &c) {
+    if (!(nd.flags & 16)) {
+        const TexCoord2 t = MapST(nd, c);
+        float ds = std::fmax(std::fabs(t.dsdx), std::fabs(t.dsdy));
+        float dt = std::fmax(std::fabs(t.dtdx), std::fabs(t.dtdy));
+        ds *= 1.5f;
+        dt *= 1.5f;
+        return 0.5f - CheckerBF(t.s, ds) * CheckerBF(t.t, dt) / 2;
+    }
+    const V3 p = XformPoint34(nd.p, c.p);  // PointTransformMapping, dpdx = dpdy = 0
+    const float dx = 1.5f * std::fmax(std::fabs(0.f), std::fabs(0.f));
+    return 0.5f - 0.5f * CheckerBF(p.x, dx) * CheckerBF(p.y, dx) * CheckerBF(p.z, dx);
+}
+
+// ---------------------------------------------------------------- MIPMap
+PHD float HalfBitsToFloat(uint16_t h) {
+    const uint32_t sign = (uint32_t)(h & 0x8000u) << 16;
+    uint32_t e = (h >> 10) & 0x1f, mant = h & 0x3ffu;
+    if (e == 0) {
+        // subnormal or zero: mant * 2^-24, exact in float
+        float f = (float)mant * 5.9604644775390625e-08f;
+        return sign ? -f : f;
+    }
+    if (e == 31) return BitsToFloat(sign | 0x7f800000u | (mant << 13));
+    return BitsToFloat(sign | ((e + 112) << 23) | (mant << 13));
+}
+
+PHD bool RemapPixelCoords(int *px, int *py, int w, int h, int wrap) {
+    int p0 = *px, p1 = *py;
+    if (wrap == 3) {  // OctahedralSphere
+        if (p0 < 0) {
+            p0 = -p0;
+            p1 = h - 1 - p1;
+        } else if (p0 >= w) {
+            p0 = 2 * w - 1 - p0;
+            p1 = h - 1 - p1;
+        }
+        if (p1 < 0) {
+            p0 = w - 1 - p0;
+            p1 = -p1;
+        } else if (p1 >= h) {
+            p0 = w - 1 - p0;
+            p1 = 2 * h - 1 - p1;
+        }
+        if (w == 1) p0 = 0;
+        if (h == 1) p1 = 0;
+    } else {
+        if (p0 < 0 || p0 >= w) {
+            if (wrap == 0) {
+                int r = p0 - (p0 / w) * w;
+                p0 = r < 0 ? r + w : r;
+            } else if (wrap == 2) p0 = p0 < 0 ? 0 : w - 1;
+            else return false;
+        }
+        if (p1 < 0 || p1 >= h) {
+            if (wrap == 0) {
+                int r = p1 - (p1 / h) * h;
+                p1 = r < 0 ? r + h : r;
+            } else if (wrap == 2) p1 = p1 < 0 ? 0 : h - 1;
+            else return false;
+        }
+    }
+    *px = p0;
+    *py = p1;
+    return true;
+}
+
+// Image::GetChannel (util/image.h:255-276) of pyramid level `level`
+PHD float TexelChannel(const TexView &T, const DeviceImage &im, int level, int x, int y, int c) {
+    const DeviceImageLevel L = T.levels[im.levelBase + level];
+    if (!RemapPixelCoords(&x, &y, L.w, L.h, im.wrap)) return 0;
+    const size_t i = ((size_t)y * (size_t)L.w + (size_t)x) * (size_t)im.nc + (size_t)c;
+    const uint8_t *base = T.data + (((uint64_t)L.offHi << 32) | L.offLo);
+    if (im.format == 0) return T.luts[im.lutBase + base[i]];
+    if (im.format == 1) return HalfBitsToFloat(reinterpret_cast<const uint16_t *>(base)[i]);
+    return reinterpret_cast<const float *>(base)[i];
+}
+
+// Image::BilerpChannel (util/image.h:279-292)
+PHD float BilerpChannel(const TexView &T, const DeviceImage &im, int level, float s, float t, int c) {
+    const DeviceImageLevel L = T.levels[im.levelBase + level];
+    const float x = s * L.w - 0.5f, y = t * L.h - 0.5f;
+    const int xi = (int)std::floor(x), yi = (int)std::floor(y);
+    const float dx = x - xi, dy = y - yi;
+    const float v0 = TexelChannel(T, im, level, xi, yi, c), v1 = TexelChannel(T, im, level, xi + 1, yi, c);
+    const float v2 = TexelChannel(T, im, level, xi, yi + 1, c), v3 = TexelChannel(T, im, level, xi + 1, yi + 1, c);
+    return ((1 - dx) * (1 - dy) * v0 + dx * (1 - dy) * v1 + (1 - dx) * dy * v2 + dx * dy * v3);
+}
+
+struct RGB3 {
+    float r, g, b;
+};
+// MIPMap::Texel<RGB> / Bilerp<RGB> / Texel<Float> / Bilerp<Float> (util/mipmap.cpp:208-226,
+// 299-311, 429-443)
+PHD RGB3 MipTexelRGB(const TexView &T, const DeviceImage &im, int level, int x, int y) {
+    if (im.nc >= 3)
+        return {TexelChannel(T, im, level, x, y, 0), TexelChannel(T, im, level, x, y, 1), TexelChannel(T, im, level, x, y, 2)};
+    const float v = TexelChannel(T, im, level, x, y, 0);
+    return {v, v, v};
+}
+PHD RGB3 MipBilerpRGB(const TexView &T, const DeviceImage &im, int level, float s, float t) {
+    if (im.nc >= 3)
+        return {BilerpChannel(T, im, level, s, t, 0), BilerpChannel(T, im, level, s, t, 1),
+                BilerpChannel(T, im, level, s, t, 2)};
+    const float v = BilerpChannel(T, im, level, s, t, 0);
+    return {v, v, v};
+}
+PHD float MipTexelF(const TexView &T, const DeviceImage &im, int level, int x, int y) {
+    return TexelChannel(T, im, level, x, y, 0);
+}
+PHD float MipBilerpF(const TexView &T, const DeviceImage &im, int level, float s, float t) {
+    if (im.nc == 1) return BilerpChannel(T, im, level, s, t, 0);
+    if (im.nc == 3) {
+        float sum = 0;
+        for (int c = 0; c < 3; ++c) sum += BilerpChannel(T, im, level, s, t, c);
+        return sum / 3;
+    }
+    return BilerpChannel(T, im, level, s, t, 3);
+}
+
+// MIPMap EWA filter weights (util/mipmap.cpp:59-191): the reference's 128 float literals
+// (pbrt-v4_amd/data/spectral_data.txt MIPFilterLUT), read through TexView::ewaLut
+constexpr int kMIPFilterLUTSize = 128;
+
+template <bool RGBT>
+struct MipVal {
+    float v[RGBT ? 3 : 1];
+};
+
+template <bool RGBT>
+PHD MipVal<RGBT> MipTexel(const TexView &T, const DeviceImage &im, int level, int x, int y) {
+    MipVal<RGBT> r;
+    if constexpr (RGBT) {
+        const RGB3 c = MipTexelRGB(T, im, level, x, y);
+        r.v[0] = c.r;
+        r.v[1] = c.g;
+        r.v[2] = c.b;
+    } else {
+        r.v[0] = MipTexelF(T, im, level, x, y);
+    }
+    return r;
+}
+template <bool RGBT>
+PHD MipVal<RGBT> MipBilerp(const TexView &T, const DeviceImage &im, int level, float s, float t) {
+    MipVal<RGBT> r;
+    if constexpr (RGBT) {
+        const RGB3 c = MipBilerpRGB(T, im, level, s, t);
+        r.v[0] = c.r;
+        r.v[1] = c.g;
+        r.v[2] = c.b;
+    } else {
+        r.v[0] = MipBilerpF(T, im, level, s, t);
+    }
+    return r;
+}
+template <bool RGBT>
+PHD MipVal<RGBT> MipLerp(float t, const MipVal<RGBT> &a, const MipVal<RGBT> &b) {
+    MipVal<RGBT> r;
+    for (int i = 0; i < (RGBT ? 3 : 1); ++i) r.v[i] = (1 - t) * a.v[i] + t * b.v[i];
+    return r;
+}
+
+// MIPMap::EWA (util/mipmap.cpp:326-375)
+template <bool RGBT>
+PHD MipVal<RGBT> MipEWA(const TexView &T, const DeviceImage &im, int level, float s, float t, float d0x, float d0y,
+                        float d1x, float d1y) {
+    if (level >= im.nLevels) return MipTexel<RGBT>(T, im, im.nLevels - 1, 0, 0);
+    const DeviceImageLevel L = T.levels[im.levelBase + level];
+    s = s * L.w - 0.5f;
+    t = t * L.h - 0.5f;
+    d0x *= L.w;
+    d0y *= L.h;
+    d1x *= L.w;
+    d1y *= L.h;
+    float A = Sqr(d0y) + Sqr(d1y) + 1;
+    float B = -2 * (d0x * d0y + d1x * d1y);
+    float C = Sqr(d0x) + Sqr(d1x) + 1;
+    const float invF = 1 / (A * C - Sqr(B) * 0.25f);
+    A *= invF;
+    B *= invF;
+    C *= invF;
+    const float det = -Sqr(B) + 4 * A * C;
+    const float invDet = 1 / det;
+    const float uSqrt = SafeSqrt(det * C), vSqrt = SafeSqrt(A * det);
+    const int s0 = (int)std::ceil(s - 2 * invDet * uSqrt), s1 = (int)std::floor(s + 2 * invDet * uSqrt);
+    const int t0 = (int)std::ceil(t - 2 * invDet * vSqrt), t1 = (int)std::floor(t + 2 * invDet * vSqrt);
+    MipVal<RGBT> sum;
+    for (int i = 0; i < (RGBT ? 3 : 1); ++i) sum.v[i] = 0;
+    float sumWts = 0;
+    for (int it = t0; it <= t1; ++it) {
+        const float tt = it - t;
+        for (int is = s0; is <= s1; ++is) {
+            const float ss = is - s;
+            const float r2 = A * Sqr(ss) + B * ss * tt + C * Sqr(tt);
+            if (r2 < 1) {
+                const float fi = r2 * kMIPFilterLUTSize;
+                const int index = fi < float(kMIPFilterLUTSize - 1) ? (int)fi : kMIPFilterLUTSize - 1;
+                const float weight = T.ewaLut[index];
+                const MipVal<RGBT> tx = MipTexel<RGBT>(T, im, level, is, it);
+                for (int i = 0; i < (RGBT ? 3 : 1); ++i) sum.v[i] = sum.v[i] + weight * tx.v[i];
+                sumWts += weight;
+            }
+        }
+    }
+    for (int i = 0; i < (RGBT ? 3 : 1); ++i) sum.v[i] = sum.v[i] / sumWts;
+    return sum;
+}
+
+// MIPMap::Filter (util/mipmap.cpp:241-297); dst0 = (dsdx, dtdx), dst1 = (dsdy, dtdy)
+template <bool RGBT>
+PHD MipVal<RGBT> MipFilter(const TexView &T, const DeviceImage &im, int filter, float maxAniso, float s, float t,
+                           float d0x, float d0y, float d1x, float d1y) {
+    const float invLog2 = 1.442695040888963387004650940071f;
+    if (filter != 3) {
+        const float width =
+            2 * std::fmax(std::fmax(std::fabs(d0x), std::fabs(d0y)), std::fmax(std::fabs(d1x), std::fabs(d1y)));
+        const int nLevels = im.nLevels;
+        const float level = nLevels - 1 + Logf(std::fmax(width, 1e-8f)) * invLog2;
+        if (level >= nLevels - 1) return MipTexel<RGBT>(T, im, nLevels - 1, 0, 0);
+        const int iLevel = std::max(0, (int)std::floor(level));
+        if (filter == 0) {
+            const DeviceImageLevel L = T.levels[im.levelBase + iLevel];
+            return MipTexel<RGBT>(T, im, iLevel, (int)std::round(s * L.w - 0.5f), (int)std::round(t * L.h - 0.5f));
+        }
+        if (filter == 1 || iLevel == 0) return MipBilerp<RGBT>(T, im, iLevel, s, t);
+        return MipLerp<RGBT>(level - iLevel, MipBilerp<RGBT>(T, im, iLevel, s, t), MipBilerp<RGBT>(T, im, iLevel + 1, s, t));
+    }
+    if (Sqr(d0x) + Sqr(d0y) < Sqr(d1x) + Sqr(d1y)) {
+        float tx = d0x, ty = d0y;
+        d0x = d1x;
+        d0y = d1y;
+        d1x = tx;
+        d1y = ty;
+    }
+    const float longer = std::sqrt(Sqr(d0x) + Sqr(d0y));
+    float shorter = std::sqrt(Sqr(d1x) + Sqr(d1y));
+    if (shorter * maxAniso < longer && shorter > 0) {
+        const float scale = longer / (shorter * maxAniso);
+        d1x *= scale;
+        d1y *= scale;
+        shorter *= scale;
+    }
+    if (shorter == 0) return MipBilerp<RGBT>(T, im, 0, s, t);
+    const float lod = std::fmax(0.f, im.nLevels - 1 + Logf(shorter) * invLog2);
+    const int ilod = (int)std::floor(lod);
+    return MipLerp<RGBT>(lod - ilod, MipEWA<RGBT>(T, im, ilod, s, t, d0x, d0y, d1x, d1y),
+                         MipEWA<RGBT>(T, im, ilod + 1, s, t, d0x, d0y, d1x, d1y));
+}
+
+// ---------------------------------------------------------------- RGB -> spectrum
+// RGBToSpectrumTable::operator() (util/color.cpp:36-75) over the device copy of the sRGB table
+PHD void RGBToCoeffs(const TexView &T, float r, float g, float b, float c[3]) {
+    if (r == g && g == b) {
+        c[0] = 0;
+        c[1] = 0;
+        c[2] = (r - .5f) / std::sqrt(r * (1 - r));
+        return;
+    }
+    const float rgb[3] = {r, g, b};
+    const int maxc = (r > g) ? ((r > b) ? 0 : 2) : ((g > b) ? 1 : 2);
+    const float z = rgb[maxc];
+    const int res = 64;
+    const float x = rgb[(maxc + 1) % 3] * (res - 1) / z;
+    const float y = rgb[(maxc + 2) % 3] * (res - 1) / z;
+    const int xi = std::min((int)x, res - 2), yi = std::min((int)y, res - 2);
+    int size = res - 2, first = 1;
+    while (size > 0) {
+        const int half = size >> 1, middle = first + half;
+        const bool pred = T.rgbZNodes[middle] < z;
+        first = pred ? middle + 1 : first;
+        size = pred ? size - (half + 1) : half;
+    }
+    const int zi = std::min(std::max(first - 1, 0), res - 2);
+    const float dx = x - xi, dy = y - yi, dz = (z - T.rgbZNodes[zi]) / (T.rgbZNodes[zi + 1] - T.rgbZNodes[zi]);
+    // data[maxc][z][y][x][3]
+    const float *base = T.rgbCoeffs + ((((size_t)maxc * res + zi) * res + yi) * res + xi) * 3;
+    const size_t sx = 3, sy = (size_t)res * 3, sz = (size_t)res * res * 3;
+    for (int i = 0; i < 3; ++i) {
+        auto co = [&](int ddx, int ddy, int ddz) { return base[ddz * sz + ddy * sy + ddx * sx + i]; };
+        c[i] = Lerpf(dz, Lerpf(dy, Lerpf(dx, co(0, 0, 0), co(1, 0, 0)), Lerpf(dx, co(0, 1, 0), co(1, 1, 0))),
+                     Lerpf(dy, Lerpf(dx, co(0, 0, 1), co(1, 0, 1)), Lerpf(dx, co(0, 1, 1), co(1, 1, 1))));
+    }
+}
+
+// ---------------------------------------------------------------- image textures
+// FloatImageTexture::Evaluate (textures.h:586-597)
+PHD float FloatImageEval(const TexView &T, const DeviceTexNode &nd, const TexEvalCtx &c) {
+    TexCoord2 tc = MapST(nd, c);
+    tc.t = 1 - tc.t;
+    const DeviceImage im = T.images[nd.image];
+    const MipVal<false> f = MipFilter<false>(T, im, nd.filter, nd.p[27], tc.s, tc.t, tc.dsdx, tc.dtdx, tc.dsdy, tc.dtdy);
+    const float v = nd.p[26] * f.v[0];
+    return (nd.flags & 8) ? std::fmax(0.f, 1 - v) : v;
+}
+// SpectrumImageTexture::Evaluate's RGB (textures.cpp:386-397) reduced to the sigmoid
+// coefficients and scale of its RGBAlbedoSpectrum / RGBUnboundedSpectrum
+PHD void SpectrumImageCoeffs(const TexView &T, const DeviceTexNode &nd, const TexEvalCtx &c, float out[4]) {
+    TexCoord2 tc = MapST(nd, c);
+    tc.t = 1 - tc.t;
+    const DeviceImage im = T.images[nd.image];
+    const MipVal<true> f = MipFilter<true>(T, im, nd.filter, nd.p[27], tc.s, tc.t, tc.dsdx, tc.dtdx, tc.dsdy, tc.dtdy);
+    const float sc = nd.p[26];
+    float rgb[3] = {sc * f.v[0], sc * f.v[1], sc * f.v[2]};
+    for (int i = 0; i < 3; ++i) rgb[i] = std::fmax(0.f, (nd.flags & 8) ? 1 - rgb[i] : rgb[i]);
+    const int specType = (nd.flags >> 1) & 3;
+    if (specType == 0) {  // Albedo: Clamp(rgb, 0, 1)
+        for (int i = 0; i < 3; ++i) rgb[i] = Clampf(rgb[i], 0, 1);
+        RGBToCoeffs(T, rgb[0], rgb[1], rgb[2], out);
+        out[3] = 1;
+    } else {  // Unbounded: scale = 2 max, coefficients of rgb / scale
+        const float m = std::fmax(rgb[0], std::fmax(rgb[1], rgb[2]));
+        const float scale = 2 * m;
+        if (scale != 0) RGBToCoeffs(T, rgb[0] / scale, rgb[1] / scale, rgb[2] / scale, out);
+        else RGBToCoeffs(T, 0, 0, 0, out);
+        out[3] = scale;
+    }
+}
+
+// ---------------------------------------------------------------- expressions
+PHD void DecodeInstr(const DeviceTexInstr &in, int *op, int *a, int *b, int *c) {
+    *op = in.op & 0xff;
+    *a = (in.op >> 8) & 0xff;
+    *b = (in.op >> 16) & 0xff;
+    *c = (in.op >> 24) & 0xff;
+}
+
+// phase 1: scalar registers R (float textures, image coefficients, weights)
+PHD void TexPhase1(const TexView &T, const DeviceTexProgram &pg, const TexEvalCtx &c, float *R) {
+    for (int k = 0; k < pg.n1; ++k) {
+        const DeviceTexInstr in = T.instrs[pg.p1 + k];
+        int op, a, b, cc;
+        DecodeInstr(in, &op, &a, &b, &cc);
+        const DeviceTexNode &nd = T.nodes[in.node < 0 ? 0 : in.node];
+        switch (op) {
+        case kT1FConst: R[a] = nd.p[22]; break;
+        case kT1FImage: R[a] = FloatImageEval(T, nd, c); break;
+        case kT1FBilerp: {
+            const TexCoord2 t = MapST(nd, c);
+            R[a] = (1 - t.s) * (1 - t.t) * nd.p[22] + t.s * (1 - t.t) * nd.p[24] + (1 - t.s) * t.t * nd.p[23] +
+                   t.s * t.t * nd.p[25];
+            break;
+        }
+        case kT1CheckW: R[a] = CheckerboardWeight(nd, c); break;
+        case kT1DirAmt: R[a] = AbsDotN(c.n, V3(nd.p[22], nd.p[23], nd.p[24])); break;
+        case kT1FScale: R[a] = (R[cc] == 0) ? 0.f : R[b] * R[cc]; break;
+        case kT1FMix: {
+            const float amt = R[in.node];
+            const float t1 = amt != 1 ? R[b] : 0.f, t2 = amt != 0 ? R[cc] : 0.f;
+            R[a] = (1 - amt) * t1 + amt * t2;
+            break;
+        }
+        case kT1FDMix: {
+            const float amt = R[in.node];
+            const float t1 = amt != 0 ? R[b] : 0.f, t2 = amt != 1 ? R[cc] : 0.f;
+            R[a] = amt * t1 + (1 - amt) * t2;
+            break;
+        }
+        case kT1SImage: SpectrumImageCoeffs(T, nd, c, R + a); break;
+        case kT1BilerpW: {
+            const TexCoord2 t = MapST(nd, c);
+            R[a] = (1 - t.s) * (1 - t.t);
+            R[a + 1] = t.s * (1 - t.t);
+            R[a + 2] = (1 - t.s) * t.t;
+            R[a + 3] = t.s * t.t;
+            break;
+        }
+        default: break;
+        }
+    }
+}
+
+PHD float TexSpecConstAt(const DeviceTexSpec &s, float lambda) {
+    if (s.rgb != 0) return s.scale * SigmoidPolynomial(s.c0, s.c1, s.c2, lambda);
+    return s.value;
+}
+
+// phase 2 at one wavelength: the spectrum texture's value, in pbrt's operation order
+PHD float TexPhase2(const TexView &T, const DeviceTexProgram &pg, const float *R, float lambda) {
+    float st[kTexMaxStack];
+    int sp = 0;
+    for (int k = 0; k < pg.n2; ++k) {
+        const DeviceTexInstr in = T.instrs[pg.p2 + k];
+        int op, a, b, cc;
+        DecodeInstr(in, &op, &a, &b, &cc);
+        switch (op) {
+        case kT2Const: st[sp++] = TexSpecConstAt(T.spec[in.node * 4 + a], lambda); break;
+        case kT2RGBReg: {
+            const float v = SigmoidPolynomial(R[a], R[a + 1], R[a + 2], lambda);
+            st[sp++] = b ? R[a + 3] * v : v;
+            break;
+        }
+        case kT2Scale: {
+            const float s = R[a];
+            st[sp - 1] = (s == 0) ? 0.f : st[sp - 1] * s;
+            break;
+        }
+        case kT2Mix: {
+            const float amt = R[a];
+            const float t2 = amt != 0 ? st[sp - 1] : 0.f, t1 = amt != 1 ? st[sp - 2] : 0.f;
+            --sp;
+            st[sp - 1] = (1 - amt) * t1 + amt * t2;
+            break;
+        }
+        case kT2DMix: {
+            const float amt = R[a];
+            const float t2 = amt != 1 ? st[sp - 1] : 0.f, t1 = amt != 0 ? st[sp - 2] : 0.f;
+            --sp;
+            st[sp - 1] = amt * t1 + (1 - amt) * t2;
+            break;
+        }
+        case kT2Bilerp: {
+            const float v3 = st[sp - 1], v2 = st[sp - 2], v1 = st[sp - 3], v0 = st[sp - 4];
+            sp -= 3;
+            st[sp - 1] = R[a] * v0 + R[a + 1] * v1 + R[a + 2] * v2 + R[a + 3] * v3;
+            break;
+        }
+        default: break;
+        }
+    }
+    return sp > 0 ? st[sp - 1] : 0.f;
+}
+
+}  // namespace pbrt_amd

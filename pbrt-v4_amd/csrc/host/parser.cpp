@@ -16,6 +16,7 @@
 
 #include "ply.h"
 #include "scene.h"
+#include "texture.h"
 
 namespace pbrt_amd {
 
@@ -356,6 +357,40 @@ class Parser {
     };
     std::vector<PendingMedium> pendingMedia;
     std::string cameraMediumName;
+    // Texture directives (scene.cpp BasicSceneBuilder::Texture): kept by (name, is spectrum) and
+    // instantiated per SpectrumType when a material uses them (scene.cpp CreateTextures)
+    struct PendingTexture {
+        std::string name, cls, dir;
+        bool spectrum = false;
+        ParamSet params;
+        Mat4 worldFromTexture;
+    };
+    std::map<std::pair<std::string, bool>, PendingTexture> pendingTextures;
+    std::map<std::tuple<std::string, bool, int>, int> texInstances;
+    std::set<std::pair<std::string, bool>> texInProgress;
+    // textured material parameters, resolved at Finish once the camera (render space) is known
+    struct MatTexPending {
+        int mat = -1;
+        std::string loc;
+        bool hasRefl = false;
+        Param refl;
+        bool hasRough = false;
+        Param ur, vr;  // type "" = constant 0 (no parameter)
+        bool remap = true;
+    };
+    std::vector<MatTexPending> matTexPending;
+    void ResolveTextures();
+    int InstTex(const std::string &name, bool spectrum, int specType, const std::string &loc);
+    int FloatTexParam(ParamSet &ps, const std::string &name, float def);
+    int SpectrumTexParam(ParamSet &ps, const std::string &name, int specType, float def);
+    int FloatParamNode(const Param *p, float def, const std::string &loc);
+    int SpectrumParamNode(const Param *p, int specType, float def, const std::string &loc);
+    int NewTexNode(const TextureDesc &t) {
+        scene.textures.push_back(t);
+        return (int)scene.textures.size() - 1;
+    }
+    TexSpectrumConst RGBConst(const Param *p, int specType, const std::string &loc);
+    void TexMapping(ParamSet &ps, const Mat4 &renderFromTexture, TextureDesc *t, bool allow3D);
 
     static std::string Loc(const Token &t) { return t.file + ":" + std::to_string(t.line); }
 
@@ -577,7 +612,22 @@ class Parser {
             std::string name = Str(toks, pos);
             if (!activeInstance.empty()) throw Error(loc + ": ObjectInstance can't be called inside instance definition");
             instanceUses.push_back(InstanceUse{name, loc, gs.ctm});
-        } else if (d == "Texture" || d == "ActiveTransform" || d == "TransformTimes") {
+        } else if (d == "Texture") {
+            PendingTexture t;
+            t.name = Str(toks, pos);
+            std::string type = Str(toks, pos);
+            t.cls = Str(toks, pos);
+            t.params = Params(toks, pos);
+            t.params.loc = loc;
+            if (type != "float" && type != "spectrum")
+                throw Error(loc + ": " + type + ": texture type unknown. Must be \"float\" or \"spectrum\".");
+            t.spectrum = type == "spectrum";
+            t.worldFromTexture = gs.ctm;
+            t.dir = dir;
+            auto key = std::make_pair(t.name, t.spectrum);
+            if (pendingTextures.count(key)) throw Error(loc + ": Redefining texture \"" + t.name + "\".");
+            pendingTextures[key] = std::move(t);
+        } else if (d == "ActiveTransform" || d == "TransformTimes") {
             throw Error(loc + ": directive " + d + " is not supported by the wavefront hot path yet");
         } else {
             throw Error(loc + ": unknown directive '" + d + "'");
@@ -605,6 +655,11 @@ class Parser {
             } else if (r->type == "float") {
                 m.constant = true;
                 m.constantValue = (float)r->nums[0];
+            } else if (r->type == "texture") {
+                // GetSpectrumTexture("reflectance", ..., SpectrumType::Albedo) (materials.cpp)
+                MatTexPending &mp = PendingTex(ps.loc);
+                mp.hasRefl = true;
+                mp.refl = *r;
             } else {
                 throw Error(ps.loc + ": reflectance of type " + r->type + " not supported");
             }
@@ -650,7 +705,11 @@ class Parser {
             Param *eta = ps.Find("eta"), *k = ps.Find("k"), *refl = ps.Find("reflectance");
             if (refl && (eta || k))
                 throw Error(ps.loc + ": For the conductor material, both \"reflectance\" and \"eta\" and \"k\" can't be provided.");
-            if (refl) {
+            if (refl && refl->type == "texture") {
+                MatTexPending &mp = PendingTex(ps.loc);
+                mp.hasRefl = true;
+                mp.refl = *refl;
+            } else if (refl) {
                 if (refl->type != "rgb" || refl->nums.size() != 3)
                     throw Error(ps.loc + ": conductor reflectance must be \"rgb\" (3 values)");
                 float rgb[3] = {(float)refl->nums[0], (float)refl->nums[1], (float)refl->nums[2]};
@@ -750,7 +809,41 @@ class Parser {
     // uroughness / vroughness / roughness + remaproughness -> TrowbridgeReitzDistribution alphas
     // (materials.cpp:62-70, materials.h:194-199 / :494-509, util/scattering.h:109-118, 192);
     // prefix "interface." / "conductor." for the coated conductor's two distributions
+    // the MatTexPending record of the material MakeMaterial is building
+    MatTexPending &PendingTex(const std::string &loc) {
+        const int idx = (int)scene.materials.size();
+        if (matTexPending.empty() || matTexPending.back().mat != idx) {
+            matTexPending.emplace_back();
+            matTexPending.back().mat = idx;
+            matTexPending.back().loc = loc;
+        }
+        return matTexPending.back();
+    }
     void Roughness(ParamSet &ps, MaterialDesc *m, const std::string &prefix = "") {
+        // GetFloatTextureOrNull("uroughness" / "vroughness"), else GetFloatTexture("roughness", 0)
+        // (materials.cpp:51-74, 217-251): a textured roughness is evaluated per hit
+        auto findTex = [&](const std::string &n) -> Param * {
+            for (auto &p : ps.params)
+                if (p.name == n && p.type == "texture") return &p;
+            return nullptr;
+        };
+        Param *ut = findTex(prefix + "uroughness"), *vt = findTex(prefix + "vroughness"), *rt = findTex(prefix + "roughness");
+        if (ut || vt || rt) {
+            if (!prefix.empty()) throw Error(ps.loc + ": textured " + prefix + "roughness is not supported yet");
+            Param *uf = ut ? ut : ps.Find("uroughness", "float"), *vf = vt ? vt : ps.Find("vroughness", "float");
+            Param *rf = rt ? rt : ps.Find("roughness", "float");
+            MatTexPending &mp = PendingTex(ps.loc);
+            mp.hasRough = true;
+            if (uf) mp.ur = *uf;
+            else if (rf) mp.ur = *rf;
+            if (vf) mp.vr = *vf;
+            else if (rf) mp.vr = *rf;
+            for (Param *q : {ut, vt, rt, uf, vf, rf})
+                if (q) q->used = true;
+            mp.remap = ps.GetBool("remaproughness", true);
+            m->remapRoughness = mp.remap;
+            return;
+        }
         Param *u = ps.Find(prefix + "uroughness", "float"), *v = ps.Find(prefix + "vroughness", "float");
         float ur = 0, vr = 0;
         if (!u || !v) {
@@ -1149,6 +1242,8 @@ void Parser::Finish() {
         scene.camera.cameraFromRaster = Mul(Inverse4(screenFromCamera), Inverse4(rasterFromScreen));
         cameraParams.CheckUnused();
     }
+    // ---- textures of the materials (render space is known now)
+    ResolveTextures();
     // ---- sensor / output colour space
     {
         const SpectralData &sd = GetSpectralData();
@@ -1522,6 +1617,304 @@ void Parser::DeltaLight(PendingLight &l, std::vector<DeltaLightDesc> &pointSpot,
         lsOrder.push_back({0, (int)pointSpot.size()});
         pointSpot.push_back(d);
     }
+}
+
+// ------------------------------------------------------------------ textures
+// TextureMapping2D::Create (textures.cpp:49-73) / TextureMapping3D::Create (:75-79)
+void Parser::TexMapping(ParamSet &ps, const Mat4 &renderFromTexture, TextureDesc *t, bool threeD) {
+    auto setXform = [&]() {
+        Mat4 tfr = Inverse4(renderFromTexture);
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 4; ++j) t->textureFromRender[4 * i + j] = (float)tfr[i][j];
+        if (tfr[3][0] != 0 || tfr[3][1] != 0 || tfr[3][2] != 0 || tfr[3][3] != 1)
+            throw Error(ps.loc + ": projective texture transforms are not supported");
+    };
+    if (threeD) {
+        t->mapping = kMap3D;
+        setXform();
+        return;
+    }
+    std::string type = ps.GetString("mapping", "uv");
+    if (type == "uv") {
+        t->mapping = kMapUV;
+        t->map[0] = (float)ps.GetFloat("uscale", 1.);
+        t->map[1] = (float)ps.GetFloat("vscale", 1.);
+        t->map[2] = (float)ps.GetFloat("udelta", 0.);
+        t->map[3] = (float)ps.GetFloat("vdelta", 0.);
+    } else if (type == "spherical" || type == "cylindrical") {
+        t->mapping = type == "spherical" ? kMapSpherical : kMapCylindrical;
+        setXform();
+    } else if (type == "planar") {
+        t->mapping = kMapPlanar;
+        setXform();
+        auto vec = [&](const char *n, V3 def) {
+            Param *p = ps.Find(n, "vector3");
+            if (p && p->nums.size() == 3) return V3((float)p->nums[0], (float)p->nums[1], (float)p->nums[2]);
+            return def;
+        };
+        V3 v1 = vec("v1", V3(1, 0, 0)), v2 = vec("v2", V3(0, 1, 0));
+        t->vs[0] = v1.x, t->vs[1] = v1.y, t->vs[2] = v1.z;
+        t->vt[0] = v2.x, t->vt[1] = v2.y, t->vt[2] = v2.z;
+        t->map[0] = (float)ps.GetFloat("udelta", 0.);
+        t->map[1] = (float)ps.GetFloat("vdelta", 0.);
+    } else {
+        throw Error(ps.loc + ": 2D texture mapping \"" + type + "\" unknown");
+    }
+}
+
+// an "rgb" spectrum parameter as pbrt's GetSpectrumTextureOrNull builds it (paramdict.cpp:846-870)
+TexSpectrumConst Parser::RGBConst(const Param *p, int specType, const std::string &loc) {
+    if (p->nums.size() != 3) throw Error(loc + ": Didn't find three values for \"rgb\" parameter \"" + p->name + "\".");
+    const float r = (float)p->nums[0], g = (float)p->nums[1], b = (float)p->nums[2];
+    if (r < 0 || g < 0 || b < 0) throw Error(loc + ": Negative value provided for RGB parameter \"" + p->name + "\".");
+    TexSpectrumConst c;
+    c.rgb = true;
+    if (specType == kSpecAlbedo) {
+        if (r > 1 || g > 1 || b > 1)
+            throw Error(loc + ": RGB parameter \"" + p->name + "\" used as an albedo has > 1 component.");
+        auto cf = RGBToSigmoidCoeffs(r, g, b);
+        c.c[0] = cf[0], c.c[1] = cf[1], c.c[2] = cf[2];
+        c.scale = 1;
+    } else if (specType == kSpecUnbounded) {
+        // RGBUnboundedSpectrum (util/spectrum.cpp:240-244)
+        const float m = std::max({r, g, b});
+        c.scale = 2 * m;
+        auto cf = c.scale != 0 ? RGBToSigmoidCoeffs(r / c.scale, g / c.scale, b / c.scale) : RGBToSigmoidCoeffs(0, 0, 0);
+        c.c[0] = cf[0], c.c[1] = cf[1], c.c[2] = cf[2];
+    } else {
+        throw Error(loc + ": illuminant spectrum textures are not supported");
+    }
+    return c;
+}
+
+int Parser::FloatParamNode(const Param *p, float def, const std::string &loc) {
+    TextureDesc t;
+    t.kind = kTexConstant;
+    t.fvalue[0] = def;
+    if (p && p->type == "texture") {
+        if (p->strs.size() != 1) throw Error(loc + ": texture parameter \"" + p->name + "\" needs one texture name");
+        return InstTex(p->strs[0], false, 0, loc);
+    }
+    if (p && p->type == "float") {
+        if (p->nums.empty()) throw Error(loc + ": \"float " + p->name + "\" needs a value");
+        t.fvalue[0] = (float)p->nums[0];
+    } else if (p && !p->type.empty()) {
+        throw Error(loc + ": \"" + p->type + " " + p->name + "\" is not a float texture parameter");
+    }
+    return NewTexNode(t);
+}
+
+int Parser::SpectrumParamNode(const Param *p, int specType, float def, const std::string &loc) {
+    TextureDesc t;
+    t.kind = kTexConstant;
+    t.spectrum = true;
+    t.specType = specType;
+    t.svalue[0].value = def;
+    if (p && p->type == "texture") {
+        if (p->strs.size() != 1) throw Error(loc + ": texture parameter \"" + p->name + "\" needs one texture name");
+        return InstTex(p->strs[0], true, specType, loc);
+    }
+    if (p && p->type == "rgb") {
+        t.svalue[0] = RGBConst(p, specType, loc);
+    } else if (p && !p->type.empty()) {
+        throw Error(loc + ": \"" + p->type + " " + p->name + "\" is not supported as a spectrum texture parameter");
+    }
+    return NewTexNode(t);
+}
+
+// GetFloatTexture(name, def) / GetSpectrumTexture(name, ConstantSpectrum(def), type)
+int Parser::FloatTexParam(ParamSet &ps, const std::string &name, float def) {
+    Param *p = nullptr;
+    for (auto &q : ps.params)
+        if (q.name == name && (q.type == "texture" || q.type == "float")) {
+            q.used = true;
+            p = &q;
+            break;
+        }
+    return FloatParamNode(p, def, ps.loc);
+}
+int Parser::SpectrumTexParam(ParamSet &ps, const std::string &name, int specType, float def) {
+    Param *p = nullptr;
+    for (auto &q : ps.params)
+        if (q.name == name) {
+            q.used = true;
+            p = &q;
+            break;
+        }
+    return SpectrumParamNode(p, specType, def, ps.loc);
+}
+
+// FloatTexture::Create / SpectrumTexture::Create (textures.cpp:1606-1707) for one SpectrumType
+int Parser::InstTex(const std::string &name, bool spectrum, int specType, const std::string &loc) {
+    const auto key = std::make_tuple(name, spectrum, spectrum ? specType : 0);
+    if (auto it = texInstances.find(key); it != texInstances.end()) return it->second;
+    auto pit = pendingTextures.find({name, spectrum});
+    if (pit == pendingTextures.end())
+        throw Error(loc + ": Couldn't find " + std::string(spectrum ? "spectrum" : "float") + " texture named \"" + name + "\"");
+    if (texInProgress.count({name, spectrum})) throw Error(loc + ": texture \"" + name + "\" refers to itself");
+    texInProgress.insert({name, spectrum});
+    PendingTexture pt = pit->second;
+    ParamSet &ps = pt.params;
+    const Mat4 renderFromTexture = Mul(scene.camera.renderFromWorld, pt.worldFromTexture);
+    TextureDesc t;
+    t.spectrum = spectrum;
+    t.specType = specType;
+    auto child = [&](const char *n, float def) {
+        return spectrum ? SpectrumTexParam(ps, n, specType, def) : FloatTexParam(ps, n, def);
+    };
+    int result = -1;
+    const std::string &c = pt.cls;
+    if (c == "constant") {
+        t.kind = kTexConstant;
+        if (spectrum) {
+            Param *v = ps.Find("value");
+            if (v && v->type == "rgb") t.svalue[0] = RGBConst(v, specType, ps.loc);
+            else if (v) throw Error(ps.loc + ": \"" + v->type + " value\" is not supported for spectrum textures");
+            else t.svalue[0].value = 1;
+        } else {
+            t.fvalue[0] = (float)ps.GetFloat("value", 1.);
+        }
+        result = NewTexNode(t);
+    } else if (c == "scale") {
+        // FloatScaledTexture::Create / SpectrumScaledTexture::Create (textures.cpp:936-1001): a
+        // constant scale of 1 drops the node, a constant scale of an image texture folds into
+        // the image's scale
+        int tex = child("tex", 1.f), sc = FloatTexParam(ps, "scale", 1.f);
+        const int rounds = spectrum ? 1 : 2;
+        for (int i = 0; i < rounds && result < 0; ++i) {
+            const TextureDesc &sn = scene.textures[sc];
+            if (sn.kind == kTexConstant) {
+                const float cs = sn.fvalue[0];
+                if (cs == 1) result = tex;
+                else if (scene.textures[tex].kind == kTexImage) {
+                    TextureDesc copy = scene.textures[tex];
+                    copy.scale *= cs;
+                    result = NewTexNode(copy);
+                }
+            }
+            if (!spectrum && result < 0) std::swap(tex, sc);
+        }
+        if (result < 0) {
+            if (!spectrum) std::swap(tex, sc);
+            t.kind = kTexScale;
+            t.child[0] = tex;
+            t.child[1] = sc;
+            result = NewTexNode(t);
+        }
+    } else if (c == "mix") {
+        t.kind = kTexMix;
+        t.child[0] = child("tex1", 0.f);
+        t.child[1] = child("tex2", 1.f);
+        t.child[2] = FloatTexParam(ps, "amount", 0.5f);
+        result = NewTexNode(t);
+    } else if (c == "directionmix") {
+        t.kind = kTexDirectionMix;
+        V3 dir(0, 1, 0);
+        if (Param *d = ps.Find("dir", "vector3")) {
+            if (d->nums.size() != 3) throw Error(ps.loc + ": \"vector3 dir\" needs 3 values");
+            dir = V3((float)d->nums[0], (float)d->nums[1], (float)d->nums[2]);
+        }
+        dir = Normalize(XformVector(renderFromTexture, dir));
+        t.dir[0] = dir.x, t.dir[1] = dir.y, t.dir[2] = dir.z;
+        t.child[0] = child("tex1", 0.f);
+        t.child[1] = child("tex2", 1.f);
+        result = NewTexNode(t);
+    } else if (c == "checkerboard") {
+        t.kind = kTexCheckerboard;
+        const int dim = ps.GetInt("dimension", 2);
+        if (dim != 2 && dim != 3) throw Error(ps.loc + ": " + std::to_string(dim) + " dimensional checkerboard texture not supported");
+        t.child[0] = child("tex1", 1.f);
+        t.child[1] = child("tex2", 0.f);
+        TexMapping(ps, renderFromTexture, &t, dim == 3);
+        result = NewTexNode(t);
+    } else if (c == "bilerp") {
+        t.kind = kTexBilerp;
+        TexMapping(ps, renderFromTexture, &t, false);
+        const char *names[4] = {"v00", "v01", "v10", "v11"};
+        const float defs[4] = {0, 1, 0, 1};
+        if (spectrum) {
+            // stored in Bilerp's corner order v00, v10, v01, v11 (textures.h:340-344)
+            const int slot[4] = {0, 2, 1, 3};
+            for (int k = 0; k < 4; ++k) {
+                Param *v = ps.Find(names[k]);
+                if (v && v->type == "rgb") t.svalue[slot[k]] = RGBConst(v, specType, ps.loc);
+                else if (v) throw Error(ps.loc + ": \"" + v->type + " " + names[k] + "\" is not supported");
+                else t.svalue[slot[k]].value = defs[k];
+            }
+        } else {
+            for (int k = 0; k < 4; ++k) t.fvalue[k] = (float)ps.GetFloat(names[k], defs[k]);
+        }
+        result = NewTexNode(t);
+    } else if (c == "imagemap") {
+        // Float/SpectrumImageTexture::Create (textures.cpp:428-521)
+        t.kind = kTexImage;
+        TexMapping(ps, renderFromTexture, &t, false);
+        t.maxAniso = (float)ps.GetFloat("maxanisotropy", 8.);
+        const std::string filter = ps.GetString("filter", "bilinear");
+        if (filter == "point") t.filter = kMipPoint;
+        else if (filter == "bilinear") t.filter = kMipBilinear;
+        else if (filter == "trilinear") t.filter = kMipTrilinear;
+        else if (filter == "ewa" || filter == "EWA") t.filter = kMipEWA;
+        else throw Error(ps.loc + ": " + filter + ": filter function unknown");
+        const std::string wrapS = ps.GetString("wrap", "repeat");
+        int wrap;
+        if (wrapS == "repeat") wrap = kWrapRepeat;
+        else if (wrapS == "black") wrap = kWrapBlack;
+        else if (wrapS == "clamp") wrap = kWrapClamp;
+        else if (wrapS == "octahedralsphere") wrap = kWrapOctahedral;
+        else throw Error(ps.loc + ": " + wrapS + ": wrap mode unknown");
+        t.scale = (float)ps.GetFloat("scale", 1.);
+        t.invert = ps.GetBool("invert", false);
+        std::string fn = ps.GetString("filename", "");
+        if (fn.empty()) throw Error(ps.loc + ": imagemap needs \"string filename\"");
+        if (fn[0] != '/' && !pt.dir.empty()) fn = pt.dir + "/" + fn;
+        auto hasPng = [](const std::string &f) {
+            if (f.size() < 4) return false;
+            std::string e = f.substr(f.size() - 4);
+            std::transform(e.begin(), e.end(), e.begin(), ::tolower);
+            return e == ".png";
+        };
+        const std::string enc = ps.GetString("encoding", hasPng(fn) ? "sRGB" : "linear");
+        if (ps.Find("basisfilename")) throw Error(ps.loc + ": multispectral basis textures are not supported");
+        // the texture cache (textures.h:537-554): one pyramid per (file, encoding, wrap)
+        int img = -1;
+        for (size_t i = 0; i < scene.images.size(); ++i)
+            if (scene.images[i].filename == fn + "|" + enc && scene.images[i].wrap == wrap) img = (int)i;
+        if (img < 0) {
+            ImageDesc id = LoadImageTexture(fn, enc, wrap, ps.loc);
+            id.filename = fn + "|" + enc;
+            scene.images.push_back(std::move(id));
+            img = (int)scene.images.size() - 1;
+        }
+        t.image = img;
+        result = NewTexNode(t);
+    } else {
+        throw Error(ps.loc + ": \"" + c + "\": " + std::string(spectrum ? "spectrum" : "float") +
+                    " texture type is not supported yet");
+    }
+    ps.CheckUnused();
+    texInProgress.erase({name, spectrum});
+    texInstances[key] = result;
+    return result;
+}
+
+void Parser::ResolveTextures() {
+    for (MatTexPending &mp : matTexPending) {
+        MaterialDesc &m = scene.materials[mp.mat];
+        if (m.type != kMatDiffuse && m.type != kMatDielectric && m.type != kMatConductor)
+            throw Error(mp.loc + ": textures are supported on diffuse, dielectric and conductor materials only");
+        if (mp.hasRefl) {
+            const int node = SpectrumParamNode(&mp.refl, kSpecAlbedo, 0.5f, mp.loc);
+            m.texReflectance = CompileTexProgram(scene, node, true);
+        }
+        if (mp.hasRough) {
+            const int u = FloatParamNode(mp.ur.type.empty() ? nullptr : &mp.ur, 0.f, mp.loc);
+            const int v = FloatParamNode(mp.vr.type.empty() ? nullptr : &mp.vr, 0.f, mp.loc);
+            m.texURough = CompileTexProgram(scene, u, false);
+            m.texVRough = CompileTexProgram(scene, v, false);
+        }
+    }
+    if (!matTexPending.empty()) ComputeCameraDifferentials(scene);
 }
 
 SceneDesc LoadPbrtString(const std::string &text, const std::string &baseDir,

@@ -78,7 +78,83 @@ struct MaterialDesc {
     float cAlphaX = 0, cAlphaY = 0;                 // conductor.{u,v}roughness -> alphas
     int ifaceEtaSpec = -1;                          // spectral interface eta (dispersion)
     float scale = 0;  // diffusetransmission "scale" (its transmittance uses the albedo fields)
+    // textured parameters (SceneDesc::texPrograms index, -1: the constant fields above apply):
+    // diffuse / conductor "reflectance" (SpectrumType::Albedo), {u,v}roughness (float)
+    int texReflectance = -1, texURough = -1, texVRough = -1;
+    bool remapRoughness = true;  // applied on the device when a roughness is textured
     std::string name;
+};
+
+// ---- textures (textures.h / textures.cpp, util/mipmap.*, util/image.*) --------------------
+// An image texture's MIPMap pyramid (Image::GeneratePyramid, util/image.cpp:313-383): every
+// level is stored in the image's original pixel format (8-bit with its ColorEncoding, half or
+// float), as pbrt stores it, so a lookup decodes exactly the values pbrt's GetChannel returns.
+enum ImageFormat : int { kImgU8 = 0, kImgHalf = 1, kImgFloat = 2 };
+enum WrapModeT : int { kWrapRepeat = 0, kWrapBlack = 1, kWrapClamp = 2, kWrapOctahedral = 3 };
+struct ImageDesc {
+    std::string filename;
+    int format = kImgU8, nc = 3;
+    int wrap = kWrapRepeat;
+    std::vector<std::array<int, 2>> levelRes;  // level 0 = finest
+    std::vector<uint64_t> levelOffset;         // byte offset of each level in data
+    std::vector<uint8_t> data;                 // levels, row-major, nc channels interleaved
+    std::array<float, 256> toLinear{};         // U8: ColorEncoding::ToLinear of every byte value
+    // the decoded file before the pyramid (the CPU oracle builds its own pyramid from it)
+    int rawW = 0, rawH = 0, encoding = 1;      // encoding: 0 linear, 1 sRGB, 2 gamma
+    float gamma = 1;
+    std::vector<uint8_t> raw;                  // rawW x rawH x nc texels in `format`
+};
+
+// Texture expression nodes.  The loader instantiates every named texture a material uses for
+// the SpectrumType of that use (pbrt keeps one instance per type: scene.cpp CreateTextures).
+enum TexKind : int {
+    kTexConstant = 0, kTexScale = 1, kTexMix = 2, kTexDirectionMix = 3, kTexCheckerboard = 4,
+    kTexBilerp = 5, kTexImage = 6
+};
+enum TexSpectrumType : int { kSpecAlbedo = 0, kSpecUnbounded = 1, kSpecIlluminant = 2 };
+enum TexMapping : int { kMapUV = 0, kMapSpherical = 1, kMapCylindrical = 2, kMapPlanar = 3, kMap3D = 4 };
+enum MIPFilter : int { kMipPoint = 0, kMipBilinear = 1, kMipTrilinear = 2, kMipEWA = 3 };
+// A constant spectrum value of a spectrum texture: ConstantSpectrum(value) or an RGB spectrum
+// of the node's type (RGBAlbedoSpectrum: sigmoid c0..c2; RGBUnboundedSpectrum: scale * sigmoid)
+struct TexSpectrumConst {
+    bool rgb = false;
+    float value = 0;               // !rgb
+    float c[3] = {0, 0, 0}, scale = 1;
+};
+struct TextureDesc {
+    int kind = kTexConstant;
+    bool spectrum = false;
+    int specType = kSpecAlbedo;
+    int child[3] = {-1, -1, -1};   // scale: tex, scale; mix: tex1, tex2, amount;
+                                   // directionmix / checkerboard: tex1, tex2
+    // TextureMapping2D (uv: su sv du dv; planar: vs, vt, ds dt) or the 3D point mapping
+    int mapping = kMapUV;
+    float map[4] = {1, 1, 0, 0};
+    float textureFromRender[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};  // 3x4 row-major
+    float vs[3] = {1, 0, 0}, vt[3] = {0, 1, 0};
+    float fvalue[4] = {0, 0, 0, 0};   // float constant (fvalue[0]); bilerp v00 v01 v10 v11
+    TexSpectrumConst svalue[4];       // spectrum constant (svalue[0]); bilerp v00 v01 v10 v11
+    float dir[3] = {0, 1, 0};         // directionmix (render space, normalised)
+    // image textures
+    int image = -1, filter = kMipBilinear;
+    float scale = 1, maxAniso = 8;
+    bool invert = false;
+};
+
+// A texture expression compiled for the device (core.h TexEval*): phase 1 runs once per hit
+// and fills scalar registers (float sub-textures, image-texture RGB -> sigmoid coefficients,
+// mix / bilerp weights); phase 2 (spectrum textures) runs per wavelength over those registers
+// with a small value stack, in pbrt's operation order.
+struct TexInstr {
+    int op = 0, a = 0, b = 0, c = 0, node = -1;
+};
+struct TexProgram {
+    bool spectrum = false;
+    int p1 = 0, n1 = 0;   // phase-1 instructions [p1, p1 + n1)
+    int p2 = 0, n2 = 0;   // phase-2 instructions
+    int result = 0;       // float textures: the register holding the value
+    int nRegs = 0;
+    int root = -1;        // TextureDesc index (oracle: evaluates the tree itself)
 };
 
 // PiecewiseLinearSpectrum (util/spectrum.h:187-239): named spectra arrive already extended by
@@ -198,6 +274,16 @@ struct SceneDesc {
     std::vector<uint32_t> permOffset;      // per dimension: offset into permTable
     std::vector<uint32_t> permNDigits;     // per dimension
     std::vector<uint32_t> permBase;        // per dimension (prime)
+
+    // textures: expression nodes, images (MIPMap pyramids), compiled programs
+    std::vector<TextureDesc> textures;
+    std::vector<ImageDesc> images;
+    std::vector<TexProgram> texPrograms;
+    std::vector<TexInstr> texInstrs;
+    // CameraBase::FindMinimumDifferentials (cameras.cpp:170-216) and CameraFromRender, for
+    // Approximate_dp_dxy (cameras.h:167-195); filled when a material is textured
+    float cameraFromRender[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+    float minPosDx[3] = {0, 0, 0}, minPosDy[3] = {0, 0, 0}, minDirDx[3] = {0, 0, 0}, minDirDy[3] = {0, 0, 0};
 };
 
 // Loaders and builders
@@ -223,7 +309,13 @@ struct SpectralData {
     std::array<float, 311> denseX, denseY, denseZ, denseD65;  // 395..705
     float photometricD65 = 0;                                  // SpectrumToPhotometric(D65)
     double rgbFromXYZ[3][3];
+    std::array<float, 256> srgbToLinear;  // SRGBToLinearLUT (util/color.cpp:286)
+    std::array<float, 128> mipFilterLUT;  // MIPFilterLUT (util/mipmap.cpp:59-191)
 };
+// The whole 64^3 sRGB RGBToSpectrumTable (cmd/rgb2spec_opt.cpp output): zNodes[64] then
+// data[3][64][64][64][3]; loaded from data/rgbspec_srgb.bin (written by the build), computed
+// in parallel (and cached there) when the file is absent
+const std::vector<float> &RGBToSpectrumTableData();
 const SpectralData &GetSpectralData();
 void SetDataDirectory(const std::string &dir);
 std::string GetDataDirectory();

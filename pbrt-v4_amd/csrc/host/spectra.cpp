@@ -8,6 +8,7 @@
 #include <fstream>
 #include <mutex>
 #include <sstream>
+#include <thread>
 
 #include "scene.h"
 
@@ -81,6 +82,10 @@ static SpectralData LoadSpectralData() {
         else if (name == "opt_cie_d65_divisor") d.optD65Divisor = v[0];
         else if (name == "opt_xyz_to_srgb") d.optXyzToSrgb = v;
         else if (name == "opt_srgb_to_xyz") d.optSrgbToXyz = v;
+        else if (name == "MIPFilterLUT" && n == 128)
+            for (int i = 0; i < 128; ++i) d.mipFilterLUT[i] = (float)v[i];
+        else if (name == "SRGBToLinearLUT" && n == 256)
+            for (int i = 0; i < 256; ++i) d.srgbToLinear[i] = (float)v[i];
         else if (name.rfind("named:", 0) == 0) tof(d.named[name.substr(6)]);
     }
     if (d.cieX.size() != 471 || d.optX.size() != 95) throw Error("malformed spectral data " + path);
@@ -384,6 +389,42 @@ static const std::vector<float> &CachedColumn(int l, int j, int i) {
     auto it = cache.find(key);
     if (it == cache.end()) it = cache.emplace(key, RGB2SpecColumn(l, j, i)).first;
     return it->second;
+}
+
+const std::vector<float> &RGBToSpectrumTableData() {
+    static std::once_flag once;
+    static std::vector<float> table;
+    std::call_once(once, [] {
+        const size_t nData = (size_t)3 * kRes * kRes * kRes * 3;
+        table.assign(kRes + nData, 0.f);
+        const std::string path = GetDataDirectory() + "/rgbspec_srgb.bin";
+        {
+            std::ifstream in(path, std::ios::binary);
+            if (in) {
+                in.read(reinterpret_cast<char *>(table.data()), (std::streamsize)(table.size() * 4));
+                if (in.gcount() == (std::streamsize)(table.size() * 4)) return;
+            }
+        }
+        // rgb2spec_opt.cpp:800-880: every (maxc, y, x) column, independent of the others
+        for (int k = 0; k < kRes; ++k) table[k] = RGB2SpecZNode(k);
+        const int nCols = 3 * kRes * kRes;
+        unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < nt; ++t)
+            th.emplace_back([&, t] {
+                for (int col = (int)t; col < nCols; col += (int)nt) {
+                    const int l = col / (kRes * kRes), j = (col / kRes) % kRes, i = col % kRes;
+                    const std::vector<float> c = RGB2SpecColumn(l, j, i);
+                    for (int k = 0; k < kRes; ++k)
+                        for (int ci = 0; ci < 3; ++ci)
+                            table[kRes + ((((size_t)l * kRes + k) * kRes + j) * kRes + i) * 3 + ci] = c[3 * k + ci];
+                }
+            });
+        for (auto &x : th) x.join();
+        std::ofstream out(path, std::ios::binary);
+        if (out) out.write(reinterpret_cast<const char *>(table.data()), (std::streamsize)(table.size() * 4));
+    });
+    return table;
 }
 
 std::array<float, 3> RGBToSigmoidCoeffs(float r, float g, float b) {

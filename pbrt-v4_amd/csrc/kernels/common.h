@@ -1036,6 +1036,40 @@ __device__ inline float Reflectance(float4 mc, bool constant, float lambda) {
     return Clampf(r, 0, 1);
 }
 
+// ---- textures (core/texture_eval.h)
+// TextureEvalContext of a hit as the wavefront material stage builds it: p, n, uv and the
+// (u,v) screen-space derivatives from Approximate_dp_dxy (surfscatter.cpp:74-104, 132-135)
+__device__ inline TexEvalCtx HitTexCtx(const DeviceScene &S, const TriSurface &surf) {
+    TexEvalCtx c;
+    c.p = surf.p;
+    c.n = surf.n;
+    c.u = surf.uv[0];
+    c.v = surf.uv[1];
+    UVDerivatives(S.camDiff, surf.p, surf.n, surf.dpdu, surf.dpdv, &c);
+    return c;
+}
+// FloatTexture::Evaluate of a compiled float program
+__device__ inline float TexFloatAt(const DeviceScene &S, int prog, const TexEvalCtx &c) {
+    float R[kTexMaxRegs];
+    const DeviceTexProgram pg = S.tex.progs[prog];
+    TexPhase1(S.tex, pg, c, R);
+    return R[pg.result];
+}
+// A hit's textured spectrum parameter: the phase-1 registers of its program; a program that is
+// one albedo RGB leaf (an image texture) reduces to the sigmoid coefficients in R[0..2]
+struct HitSpectrumTex {
+    DeviceTexProgram pg;
+    float R[kTexMaxRegs];
+    __device__ float At(const DeviceScene &S, float lambda) const {
+        if (pg.simple) return SigmoidPolynomial(R[0], R[1], R[2], lambda);
+        return TexPhase2(S.tex, pg, R, lambda);
+    }
+};
+__device__ inline void EvalSpectrumTex(const DeviceScene &S, int prog, const TexEvalCtx &c, HitSpectrumTex *h) {
+    h->pg = S.tex.progs[prog];
+    TexPhase1(S.tex, h->pg, c, h->R);
+}
+
 // ToSensorRGB accumulation for one wavelength: sx += xbar * (c / pdf) (film.h:95-100)
 // Film-only arithmetic (the contribution c and its 1/pdf, 1/denom scalings) uses reciprocal
 // multiplies where the reference divides: at most an ulp or two per term in the pixel sums,

@@ -11,6 +11,7 @@
 #include <cstdint>
 
 #include "../core/core.h"
+#include "../core/texture_eval.h"
 #include "../host/bvh.h"
 
 namespace pbrt_amd {
@@ -199,6 +200,13 @@ struct DeviceScene {
     int ldsNodes, ldsTris;  // BVH8 nodes / triangles cached in LDS by the traversal kernels
     ShadeLdsLayout shadeLds;
     DeviceMedia media;
+    // textures (core/texture_eval.h): expression tables, MIPMap pyramids, the RGB->spectrum
+    // table, the camera's differential estimate, and per material the texture programs of
+    // reflectance / u roughness / v roughness (-1: the constant parameters apply) + remap flag
+    int textured;
+    TexView tex;
+    CameraDiff camDiff;
+    const int4 *matTex;
 };
 
 // One depth's path records, compacted: record i is the i-th ray of that depth (pbrt's

@@ -300,9 +300,10 @@ __global__ void __launch_bounds__(kBlock) k_emissive(DeviceScene S, PathState st
 // somewhere.
 // DivD2: the light's radiance is divided by d2 per wavelength (point and spot lights; d2 = 1,
 // an exact no-op, for the other lanes).
-template <bool DivD2, typename FD>
-__device__ inline void ShadeSpectralPass(int depth, const FD *dense, const SensorF4 *sensor4, float *bf, float4 mc,
-                                         bool constant, float lambda0, float scale, float d2, float rd2, bool d2Ok,
+// RF: the diffuse reflectance R(lambda), clamped to [0, 1] (DiffuseMaterial::GetBxDF)
+template <bool DivD2, typename FD, typename RF>
+__device__ inline void ShadeSpectralPass(int depth, const FD *dense, const SensorF4 *sensor4, float *bf, const RF &rf,
+                                         float lambda0, float scale, float d2, float rd2, bool d2Ok,
                                          float absdotL, float invDenom, float absdotB, float pdf, float rpdf,
                                          bool pdfOk, float etaScale, SensorAcc *acc, bool *neeNz, bool *betaNz,
                                          float *mx) {
@@ -311,7 +312,7 @@ __device__ inline void ShadeSpectralPass(int depth, const FD *dense, const Senso
     float m = -kInfinity;
 #pragma unroll 1
     for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next()) {
-        const float R = Reflectance(mc, constant, it.lam);
+        const float R = rf(it.lam);
         const float bfi = (depth > 0 ? bf[it.i * kBlock] : 1.f) * (R * kInvPi);
         const int off = DenseOffset(it.lam);
         float Le = scale * (off < 0 ? 0.f : float(dense[off]));
@@ -453,7 +454,9 @@ __device__ __forceinline__ RaySamples GenerateRaySamples(const DeviceScene &S, c
 // Lean (host-chosen per launch, pbrt-identical results either way): Halton indices below 2^24,
 // lights, light BVH and dense spectra staged in LDS, no mesh with shading normals or uv -- the
 // common case, compiled without the other paths so the kernel's hot code stays small.
-template <bool Lean>
+// Tex (host-chosen: some material is textured): reflectance textures are evaluated per hit
+// (surfscatter.cpp:74-137: uv derivatives, then GetBxDF's texture evaluation).
+template <bool Lean, bool Tex = false>
 __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(DeviceScene S, PathState st, int depth) {
     const QueueView mats = LoadQueue(st, depth, kCntMat);
     if ((int)(blockIdx.x * blockDim.x) >= mats.total) return;  // no work
@@ -505,9 +508,29 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
             const int mat = S.primMaterial[prim];
             TriSurface surf = Lean ? TriangleSurface(p0, p1, p2, b0, b1, b2, S.primFlip[prim], nullptr)
                                    : SurfaceAt(S, prim, p0, p1, p2, b0, b1, b2);
-            const float4 mc = matsL[mat];
-            const int mflags = matConstL[mat];  // bit 0: constant R, bit 1: R != 0 at every wavelength
-            const bool constant = mflags & 1;
+            float4 mc = matsL[mat];
+            int mflags = matConstL[mat];  // bit 0: constant R, bit 1: R != 0 at every wavelength
+            bool constant = mflags & 1;
+            // a textured reflectance: one RGB leaf becomes this hit's sigmoid coefficients; any
+            // other expression is evaluated per wavelength (texR)
+            HitSpectrumTex htex;
+            bool texR = false;
+            if constexpr (Tex) {
+                const int tp = S.matTex[mat].x;
+                if (tp >= 0) {
+                    EvalSpectrumTex(S, tp, HitTexCtx(S, surf), &htex);
+                    mflags = 0;
+                    constant = false;
+                    if (htex.pg.simple) mc = make_float4(htex.R[0], htex.R[1], htex.R[2], 0.f);
+                    else texR = true;
+                }
+            }
+            auto rfun = [&](float lam) -> float {
+                if constexpr (Tex) {
+                    if (texR) return Clampf(htex.At(S, lam), 0, 1);
+                }
+                return Reflectance(mc, constant, lam);
+            };
             V3 wo = Normalize(-rd);
             V3 n = surf.n, ns = surf.ns;
             // beta_i -> bfLds[i][lane] by LDS-DMA: all 31 loads in flight at once, no VGPRs,
@@ -538,8 +561,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                 else if (mflags & 2) Rnz = true;
                 else {
                     Rnz = false;
-                    for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next())
-                        Rnz |= Reflectance(mc, false, it.lam) != 0;
+                    for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next()) Rnz |= rfun(it.lam) != 0;
                 }
                 Frame frame = Frame::FromXZ(Normalize(surf.dpdus), ns);
                 V3 woL = frame.ToLocal(wo);
@@ -614,15 +636,15 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                     const float rd2 = 1 / d2;
                     const bool d2Ok = DivFastOk(d2);
                     if (Lean || (lay.denseInLds && S.nPointSpot == 0))
-                        ShadeSpectralPass<false>(depth, (const LdsF *)denseLds + spec * kDenseN, sensorL, bf, mc,
-                                                 constant, lambda0, scale, d2, rd2, d2Ok, absdotL, invDenom, absdotB, pdf,
+                        ShadeSpectralPass<false>(depth, (const LdsF *)denseLds + spec * kDenseN, sensorL, bf, rfun,
+                                                 lambda0, scale, d2, rd2, d2Ok, absdotL, invDenom, absdotB, pdf,
                                                  rpdf, pdfOk, etaScale, &acc, &neeNz, &betaNz, &mx);
                     else if (lay.denseInLds)
-                        ShadeSpectralPass<true>(depth, (const LdsF *)denseLds + spec * kDenseN, sensorL, bf, mc,
-                                                constant, lambda0, scale, d2, rd2, d2Ok, absdotL, invDenom, absdotB, pdf,
+                        ShadeSpectralPass<true>(depth, (const LdsF *)denseLds + spec * kDenseN, sensorL, bf, rfun,
+                                                lambda0, scale, d2, rd2, d2Ok, absdotL, invDenom, absdotB, pdf,
                                                 rpdf, pdfOk, etaScale, &acc, &neeNz, &betaNz, &mx);
                     else
-                        ShadeSpectralPass<true>(depth, S.dense + spec * kDenseN, sensorL, bf, mc, constant, lambda0,
+                        ShadeSpectralPass<true>(depth, S.dense + spec * kDenseN, sensorL, bf, rfun, lambda0,
                                                 scale, d2, rd2, d2Ok, absdotL, invDenom, absdotB, pdf, rpdf, pdfOk,
                                                 etaScale, &acc, &neeNz, &betaNz, &mx);
                 }
@@ -715,7 +737,9 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
 // sampling (IsNonSpecular(flags), surfscatter.cpp:253).
 // Smooth (dielectric only, host-checked: every dielectric EffectivelySmooth, no regularize):
 // the light-sampling code of rough surfaces is compiled out.
-template <int MT, bool Smooth = false>
+// Tex (host-chosen: some material is textured): textured roughness (both types) and conductor
+// reflectance are evaluated per hit (materials.h:182-204, :491-511).
+template <int MT, bool Smooth = false, bool Tex = false>
 __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(DeviceScene S, PathState st, int depth) {
     const QueueView mats = LoadQueue(st, depth, MatCounter(MT));
     if ((int)(blockIdx.x * blockDim.x) >= mats.total) return;  // no work
@@ -766,13 +790,36 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
             // ---- Material::GetBxDF (materials.h:182-204 dielectric, :491-511 conductor)
             const float4 mp = S.matParams[mat];
             TrowbridgeReitz tr{mp.x, mp.y};
+            float4 mc = T.matsL[mat];
+            HitSpectrumTex htex;
+            bool texR = false;
+            if constexpr (Tex) {
+                const int4 mt = S.matTex[mat];
+                if (mt.x >= 0 || mt.y >= 0) {
+                    const TexEvalCtx tc = HitTexCtx(S, surf);
+                    if (mt.y >= 0) {
+                        // texEval(uRoughness / vRoughness), RoughnessToAlpha when remapped, then the
+                        // TrowbridgeReitzDistribution constructor's clamp
+                        float ur = TexFloatAt(S, mt.y, tc), vr = TexFloatAt(S, mt.z, tc);
+                        if (mt.w) {
+                            ur = RoughnessToAlpha(ur);
+                            vr = RoughnessToAlpha(vr);
+                        }
+                        tr = TrowbridgeReitz::Make(ur, vr);
+                    }
+                    if (MT == kMatConductorT && mt.x >= 0) {
+                        EvalSpectrumTex(S, mt.x, tc, &htex);
+                        if (htex.pg.simple) mc = make_float4(htex.R[0], htex.R[1], htex.R[2], 0.f);
+                        else texR = true;
+                    }
+                }
+            }
             if (S.regularize && (inFlags & 2)) tr.Regularize();  // surfscatter.cpp:127-128
             float eta = mp.z;
             if (eta == 0) eta = 1;
             // conductor eta_i / k_i: piecewise-linear spectra, or from the albedo "reflectance"
             const int etaSpec = MT == kMatConductorT ? S.matSpectra[2 * mat] : -1;
             const int kSpec = MT == kMatConductorT ? S.matSpectra[2 * mat + 1] : -1;
-            const float4 mc = T.matsL[mat];
             auto etaK = [&](float lam, float *e, float *k) {
                 if (etaSpec >= 0) {
                     const int a = S.plOffsets[etaSpec], na = S.plOffsets[etaSpec + 1] - a;
@@ -785,7 +832,11 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
                         *k = PiecewiseLinearEval(S.plLambda + b, S.plValue + b, nb, lam);
                     }
                 } else {
-                    float r = Clampf(SigmoidPolynomial(mc.x, mc.y, mc.z, lam), 0, .9999f);
+                    float rv = SigmoidPolynomial(mc.x, mc.y, mc.z, lam);
+                    if constexpr (Tex) {
+                        if (texR) rv = htex.At(S, lam);
+                    }
+                    float r = Clampf(rv, 0, .9999f);
                     *e = 1.f;
                     *k = 2 * std::sqrt(r) / std::sqrt(std::fmax(0.f, 1 - r));
                 }
@@ -1210,7 +1261,10 @@ static size_t ShadeLdsBytes(const DeviceScene &S, int depth, bool withPl = false
 }
 hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int depth, int maxCount, bool lean,
                               hipStream_t s) {
-    if (lean)
+    if (S.textured)
+        hipLaunchKernelGGL((k_shade_diffuse<false, true>), dim3(ShadeGridFor(maxCount)), dim3(kBlock),
+                           ShadeLdsBytes(S, depth), s, S, st, depth);
+    else if (lean)
         hipLaunchKernelGGL(k_shade_diffuse<true>, dim3(ShadeGridFor(maxCount)), dim3(kBlock), ShadeLdsBytes(S, depth),
                            s, S, st, depth);
     else
@@ -1220,7 +1274,14 @@ hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int dep
 }
 hipError_t LaunchShadeMicrofacet(const DeviceScene &S, const PathState &st, int depth, int type, int maxCount,
                                  hipStream_t s) {
-    if (type == kMatDielectricT && S.smoothDielectrics)
+    if (S.textured) {
+        if (type == kMatDielectricT)
+            hipLaunchKernelGGL((k_shade_microfacet<kMatDielectricT, false, true>), dim3(ShadeGridFor(maxCount)),
+                               dim3(kBlock), ShadeLdsBytes(S, depth, true), s, S, st, depth);
+        else
+            hipLaunchKernelGGL((k_shade_microfacet<kMatConductorT, false, true>), dim3(ShadeGridFor(maxCount)),
+                               dim3(kBlock), ShadeLdsBytes(S, depth, true), s, S, st, depth);
+    } else if (type == kMatDielectricT && S.smoothDielectrics)
         hipLaunchKernelGGL((k_shade_microfacet<kMatDielectricT, true>), dim3(ShadeGridFor(maxCount)), dim3(kBlock),
                            ShadeLdsBytes(S, depth, true), s, S, st, depth);
     else if (type == kMatDielectricT)

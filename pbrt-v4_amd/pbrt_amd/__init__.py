@@ -78,6 +78,14 @@ class SceneFlat(ctypes.Structure):
         ("n_delta_lights", ctypes.c_int), ("n_point_spot", ctypes.c_int),
         ("delta_lights", ctypes.POINTER(ctypes.c_float)), ("inf_distant", ctypes.POINTER(ctypes.c_int32)),
         ("uniform_order", ctypes.POINTER(ctypes.c_int32)), ("scene_radius", ctypes.c_float),
+        ("n_tex_nodes", ctypes.c_int), ("n_images", ctypes.c_int),
+        ("tex_node_info", ctypes.POINTER(ctypes.c_int32)), ("tex_node_params", ctypes.POINTER(ctypes.c_float)),
+        ("tex_node_spec", ctypes.POINTER(ctypes.c_float)), ("image_info", ctypes.POINTER(ctypes.c_int32)),
+        ("image_levels", ctypes.POINTER(ctypes.c_int32)), ("image_data", ctypes.POINTER(ctypes.c_uint8)),
+        ("image_luts", ctypes.POINTER(ctypes.c_float)), ("image_raw_info", ctypes.POINTER(ctypes.c_int32)),
+        ("image_raw_gamma", ctypes.POINTER(ctypes.c_float)), ("image_raw_offset", ctypes.POINTER(ctypes.c_uint64)),
+        ("image_raw_data", ctypes.POINTER(ctypes.c_uint8)), ("material_tex", ctypes.POINTER(ctypes.c_int32)),
+        ("camera_from_render", ctypes.c_float * 12), ("camera_min_diff", ctypes.c_float * 12),
     ]
 
 
@@ -109,6 +117,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_debug_named_spectrum", "pbrt_debug_bxdf", "pbrt_debug_layered", "pbrt_debug_triangle_shading", "pbrt_film_write_image",
     "pbrt_image_read_size", "pbrt_image_read", "pbrt_image_write", "pbrt_image_error", "pbrt_debug_filter_sample",
     "pbrt_debug_bvh_stats", "pbrt_debug_light_bvh", "pbrt_intersect_tr", "pbrt_image_flip", "pbrt_set_kernel_profiling", "pbrt_get_kernel_stats",
+    "pbrt_debug_texture_eval",
 ]
 
 _LIB = None
@@ -172,6 +181,7 @@ def _lib():
     lib.pbrt_debug_bxdf.argtypes = [c.c_int] + [c.c_void_p] * 7
     lib.pbrt_debug_layered.argtypes = [c.c_void_p] * 8
     lib.pbrt_debug_triangle_shading.argtypes = [c.c_void_p] * 3 + [c.c_int] + [c.c_void_p] * 3
+    lib.pbrt_debug_texture_eval.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_set_data_dir(str(DATA_DIR).encode())
     _LIB = lib
     return lib
@@ -312,6 +322,17 @@ class Scene:
         _check(_lib().pbrt_debug_bvh_stats(self._h, out))
         keys = ("nodes", "triangles", "depth", "max_stack", "wide_bytes", "quantised_bytes")
         return dict(zip(keys, list(out)[:6]))
+
+    def texture_eval(self, material, slot, hit14, lambdas=()):
+        """The product's texture evaluation of a material's textured parameter at a hit
+        (pbrt_debug_texture_eval): returns ((dudx, dudy, dvdx, dvdy), values) where values are
+        the reflectance at each wavelength (slot 0) or the roughness (slot 1 u, 2 v)."""
+        lam = np.ascontiguousarray(lambdas, dtype=np.float32)
+        hit = np.ascontiguousarray(hit14, dtype=np.float32)
+        out = np.zeros(5 + len(lam), dtype=np.float32)
+        _check(_lib().pbrt_debug_texture_eval(self._h, material, slot, hit.ctypes.data, lam.ctypes.data, len(lam),
+                                              out.ctypes.data))
+        return out[:4].copy(), (out[4:4 + len(lam)].copy() if slot == 0 else float(out[4]))
 
     def halton_fastpath_mismatches(self, dim, a0, a1, step=1):
         """Indices in [a0, a1) (stride step) whose 24-bit fast-path ScrambledRadicalInverse

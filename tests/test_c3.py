@@ -60,7 +60,7 @@ def test_conductor_defaults_and_named_spectra(pa):
     ('Material "conductor" "rgb reflectance" [0.9 0.6 0.3] "spectrum eta" "metal-Au-eta"', "can't be provided"),
     ('Material "conductor" "spectrum eta" "metal-Xx-eta"', "unknown named spectrum"),
     ('Material "conductor" "spectrum eta" [400 1 500]', "odd number"),
-    ('Material "dielectric" "texture roughness" "foo"', "not supported"),
+    ('Material "dielectric" "texture roughness" "foo"', "Couldn't find float texture"),
 ])
 def test_material_errors_are_loud(pa, mat, msg):
     text = 'WorldBegin\nLightSource "infinite"\n' + mat + '\nShape "trianglemesh" "point3 P" [0 0 0 1 0 0 0 1 0]\n'

@@ -11,6 +11,9 @@ reference's sources
                                  CIE_Illum_D6500 (:770)
     src/pbrt/cmd/rgb2spec_opt.cpp cie_x / cie_y / cie_z / cie_d65 (:46-128),
                                  xyz_to_srgb / srgb_to_xyz (:191-197)
+    src/pbrt/util/color.cpp      SRGBToLinearLUT (:286-330), the 8-bit sRGB decode table
+                                 every sRGB-encoded image texel goes through
+    src/pbrt/util/mipmap.cpp     MIPFilterLUT (:59-191), the EWA filter weight table
     src/pbrt/util/spectrum.cpp   the interleaved (lambda, value) tables behind the named
                                  metal and glass spectra (:1128-1440), keyed by the names
                                  Spectra::Init registers them under (:2666-2690)
@@ -81,6 +84,16 @@ def main():
     for name in ("xyz_to_srgb", "srgb_to_xyz"):
         data["opt_" + name] = numbers(array_body(opt, name))
         assert len(data["opt_" + name]) == 9
+    color = (REF / "util" / "color.cpp").read_text()
+    m = re.search(r"Float\s+SRGBToLinearLUT\s*\[256\]\s*=\s*\{", color)
+    body = color[m.end():color.index("}", m.end())]
+    data["SRGBToLinearLUT"] = numbers(body)
+    assert len(data["SRGBToLinearLUT"]) == 256
+    mip = (REF / "util" / "mipmap.cpp").read_text()
+    m = re.search(r"Float\s+MIPFilterLUT\s*\[MIPFilterLUTSize\]\s*=\s*\{", mip)
+    body = mip[m.end():mip.index("};", m.end())]
+    data["MIPFilterLUT"] = numbers(body)
+    assert len(data["MIPFilterLUT"]) == 128, len(data["MIPFilterLUT"])
     for name, arr in NAMED.items():
         vals = numbers(array_body(spec, arr))
         assert len(vals) % 2 == 0 and len(vals) >= 4, (name, len(vals))

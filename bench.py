@@ -64,6 +64,8 @@ def parse(argv=None):
                     help="paths per wavefront pass (0: the library default, the whole image's samples in "
                          "one pass up to 64 Mi paths)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--untextured", action="store_true",
+                    help="C4: round 2's constant materials instead of configs[3]'s image textures")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
                     help="N > 1: strong = one image split N ways (default); weak = every GPU renders "
@@ -85,7 +87,7 @@ def load(args, spp=None):
         import gen_c4
         keep = os.environ.get("PBRT_C4_DIR")
         out = Path(keep or tempfile.mkdtemp(prefix="pbrt_c4_"))
-        path, _ = gen_c4.generate(out, xres=args.xres, yres=args.yres, spp=spp)
+        path, _ = gen_c4.generate(out, xres=args.xres, yres=args.yres, spp=spp, textured=not args.untextured)
         scene = pa.load_scene(path)  # the PLY files are read completely here
         if not keep:
             import shutil
@@ -340,7 +342,9 @@ def main():
                                     if args.workload == "c5" else
                                     f"C4 San-Miguel stand-in (scenes/gen_c4.py, PLY) {args.xres}x{args.yres} "
                                     f"{info.spp}spp maxdepth {info.max_depth} zsobol, diffuse + conductor, "
-                                    "untextured (BASELINE configs[3] geometry)"),
+                                    + ("untextured (BASELINE configs[3] geometry)" if args.untextured else
+                                       "textured: 8 sRGB PNG albedo images (256^2-1024^2, bilinear / trilinear MIP) "
+                                       "and 2 roughness images, per-vertex uv (BASELINE configs[3])")),
                        "xres": args.xres, "yres": args.yres, "spp": info.spp, "max_depth": info.max_depth,
                        "triangles": info.n_triangles, "paths_per_pass": int(st.paths_per_pass),
                        "sharding": job["sharding"]},

@@ -23,6 +23,8 @@ hipError_t LaunchClosest(const DeviceScene &S, const PathState &st, int depth, i
                          hipStream_t s);
 hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int depth, int maxCount, bool lean,
                               hipStream_t s);
+hipError_t LaunchTexture(const DeviceScene &S, const PathState &st, int depth, int type, bool full, int maxCount,
+                         hipStream_t s);
 hipError_t LaunchShadeMicrofacet(const DeviceScene &S, const PathState &st, int depth, int type, int maxCount,
                                  hipStream_t s);
 hipError_t LaunchEscaped(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
@@ -369,6 +371,10 @@ struct pbrt_context {
     DevBuf<DeviceTexInstr> texInstrs;
     DevBuf<DeviceTexProgram> texProgs;
     DevBuf<int> matTex;
+    DevBuf<float> texCoef, texR;  // k_texture results (PathState::texCoef / texR)
+    bool texGeneral = false;      // some textured reflectance is not a single image leaf
+    int texTypeMask = 0;          // bit t: some material of type t is textured
+    int texFullMask = 0;          // bit t: ... with an expression beyond one non-EWA image leaf
     // wavefront buffers
     int64_t maxPaths = 0;
     DevBuf<float> fState;
@@ -769,6 +775,24 @@ static void BuildDevice(pbrt_context *c) {
             S.tex.ewaLut = c->ewaLut.p;
             S.tex.nProgs = (int)tt.progs.size();
             S.camDiff = MakeCameraDiff(s);
+            // a program k_texture's lean instantiation evaluates: one image leaf without EWA
+            // (reflectance: the albedo RGB leaf; roughness: a float image or a constant)
+            auto leanProg = [&](int p, bool spectrum) {
+                if (p < 0) return true;
+                const DeviceTexProgram &pg = tt.progs[p];
+                if (spectrum && !pg.simple) return false;
+                if (!spectrum && pg.n1 != 1) return false;
+                const DeviceTexInstr &in = tt.instrs[pg.p1];
+                const int op = in.op & 0xff;
+                if (!spectrum && op != kT1FConst && op != kT1FImage) return false;
+                return op == kT1FConst || s.textures[in.node].filter != kMipEWA;
+            };
+            for (const MaterialDesc &m : s.materials) {
+                if (m.texReflectance >= 0 && !tt.progs[m.texReflectance].simple) c->texGeneral = true;
+                if (m.texReflectance >= 0 || m.texURough >= 0) c->texTypeMask |= 1 << m.type;
+                if (!leanProg(m.texReflectance, true) || !leanProg(m.texURough, false) || !leanProg(m.texVRough, false))
+                    c->texFullMask |= 1 << m.type;
+            }
         }
     }
     S.nAreaLights = (int)s.areaLights.size();
@@ -955,8 +979,9 @@ constexpr int kPathFloats = 101, kPathInts = 16;
 // hitB 4, shadow ray 6 + Ld/r_u/r_l 93 + lambda0 = 100 floats; records 2 x (flags, pixel,
 // depth, medium) = 8, hitPrim, 5 queues, shadow pixel + medium + flags = 17 ints
 constexpr int kVolFloats = 330, kVolInts = 17;
-static int64_t PathStateBytesPerPath(bool volumetric, bool dispersive) {
-    return 4 * (kPathFloats + kPathInts) + (volumetric ? 4 * (kVolFloats + kVolInts) : 0) + (dispersive ? 16 : 0);
+static int64_t PathStateBytesPerPath(bool volumetric, bool dispersive, bool textured = false, bool texGeneral = false) {
+    return 4 * (kPathFloats + kPathInts) + (volumetric ? 4 * (kVolFloats + kVolInts) : 0) + (dispersive ? 16 : 0) +
+           (textured ? 24 : 0) + (texGeneral ? 124 : 0);
 }
 
 static void AllocPaths(pbrt_context *c, int64_t N) {
@@ -972,6 +997,10 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
     if (c->S.dispersive) {
         c->dispL0.Alloc((size_t)3 * NR);
         c->dispTerm.Alloc((size_t)NR);
+    }
+    if (c->S.textured) {
+        c->texCoef.Alloc((size_t)6 * NR);
+        if (c->texGeneral) c->texR.Alloc((size_t)kNSpectrumSamples * NR);
     }
     c->maxPaths = N;
     PathState &st = c->st;
@@ -1014,6 +1043,8 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
     st.escQ = takei(1);
     st.emitQ = takei(1);
     st.counters = ip;
+    st.texCoef = c->texCoef.p;
+    st.texR = c->texR.p;
     if (c->volumetric) {
         const int vf = kVolFloats, vi = kVolInts;
         c->vfState.Alloc((size_t)vf * NR);
@@ -1244,7 +1275,13 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
                     if (emit) HIPCHECK(hipStreamWaitEvent(c->stream, c->eEmit[depth], 0));
                     break;
                 }
-                // EvaluateMaterialsAndBSDFs: one launch per material type present (surfscatter.cpp:39-55)
+                // EvaluateMaterialsAndBSDFs: one launch per material type present (surfscatter.cpp:39-55),
+                // preceded by that type's texture stage when some material of it is textured
+                for (int t = 0; t < kNumMatTypes; ++t)
+                    if (c->texTypeMask & (1 << t)) {
+                        StageTimer tm(c, "Evaluate textures (k_texture)", c->stream);
+                        HIPCHECK(LaunchTexture(c->S, st, depth, t, (c->texFullMask >> t) & 1, (int)nActive, c->stream));
+                    }
                 if (c->S.matTypeMask & (1 << kMatDiffuseT)) {
                     StageTimer t(c, "Evaluate materials/BSDFs for DiffuseMaterial (k_shade_diffuse)", c->stream);
                     HIPCHECK(LaunchShadeDiffuse(c->S, st, depth, (int)nActive, lean, c->stream));
@@ -1479,7 +1516,7 @@ int pbrt_context_create(const pbrt_scene *scene, int device, int64_t maxPaths, p
             // smaller cards): path-state bytes per path from AllocPaths' layout
             size_t freeB = 0, totalB = 0;
             HIPCHECK(hipMemGetInfo(&freeB, &totalB));
-            const int64_t perPath = PathStateBytesPerPath(c->volumetric, c->S.dispersive);
+            const int64_t perPath = PathStateBytesPerPath(c->volumetric, c->S.dispersive, c->S.textured, c->texGeneral);
             const int64_t fit = (int64_t)(freeB / 4 * 3) / perPath - kShards * 320;
             if (fit < 4096) throw Error("not enough free device memory for path state");
             maxPaths = std::min<int64_t>(maxPaths, fit);

@@ -438,12 +438,14 @@ PHD MipVal<RGBT> MipEWA(const TexView &T, const DeviceImage &im, int level, floa
     return sum;
 }
 
-// MIPMap::Filter (util/mipmap.cpp:241-297); dst0 = (dsdx, dtdx), dst1 = (dsdy, dtdy)
-template <bool RGBT>
+// MIPMap::Filter (util/mipmap.cpp:241-297); dst0 = (dsdx, dtdx), dst1 = (dsdy, dtdy).
+// AllowEWA = false: the caller guarantees a point / bilinear / trilinear filter (the EWA code is
+// not compiled in)
+template <bool RGBT, bool AllowEWA = true>
 PHD MipVal<RGBT> MipFilter(const TexView &T, const DeviceImage &im, int filter, float maxAniso, float s, float t,
                            float d0x, float d0y, float d1x, float d1y) {
     const float invLog2 = 1.442695040888963387004650940071f;
-    if (filter != 3) {
+    if (!AllowEWA || filter != 3) {
         const float width =
             2 * std::fmax(std::fmax(std::fabs(d0x), std::fabs(d0y)), std::fmax(std::fabs(d1x), std::fabs(d1y)));
         const int nLevels = im.nLevels;
@@ -457,6 +459,8 @@ PHD MipVal<RGBT> MipFilter(const TexView &T, const DeviceImage &im, int filter, 
         if (filter == 1 || iLevel == 0) return MipBilerp<RGBT>(T, im, iLevel, s, t);
         return MipLerp<RGBT>(level - iLevel, MipBilerp<RGBT>(T, im, iLevel, s, t), MipBilerp<RGBT>(T, im, iLevel + 1, s, t));
     }
+    if constexpr (!AllowEWA) return MipVal<RGBT>{};
+    else {
     if (Sqr(d0x) + Sqr(d0y) < Sqr(d1x) + Sqr(d1y)) {
         float tx = d0x, ty = d0y;
         d0x = d1x;
@@ -477,6 +481,7 @@ PHD MipVal<RGBT> MipFilter(const TexView &T, const DeviceImage &im, int filter, 
     const int ilod = (int)std::floor(lod);
     return MipLerp<RGBT>(lod - ilod, MipEWA<RGBT>(T, im, ilod, s, t, d0x, d0y, d1x, d1y),
                          MipEWA<RGBT>(T, im, ilod + 1, s, t, d0x, d0y, d1x, d1y));
+    }
 }
 
 // ---------------------------------------------------------------- RGB -> spectrum
@@ -516,21 +521,25 @@ PHD void RGBToCoeffs(const TexView &T, float r, float g, float b, float c[3]) {
 
 // ---------------------------------------------------------------- image textures
 // FloatImageTexture::Evaluate (textures.h:586-597)
+template <bool AllowEWA = true>
 PHD float FloatImageEval(const TexView &T, const DeviceTexNode &nd, const TexEvalCtx &c) {
     TexCoord2 tc = MapST(nd, c);
     tc.t = 1 - tc.t;
     const DeviceImage im = T.images[nd.image];
-    const MipVal<false> f = MipFilter<false>(T, im, nd.filter, nd.p[27], tc.s, tc.t, tc.dsdx, tc.dtdx, tc.dsdy, tc.dtdy);
+    const MipVal<false> f =
+        MipFilter<false, AllowEWA>(T, im, nd.filter, nd.p[27], tc.s, tc.t, tc.dsdx, tc.dtdx, tc.dsdy, tc.dtdy);
     const float v = nd.p[26] * f.v[0];
     return (nd.flags & 8) ? std::fmax(0.f, 1 - v) : v;
 }
 // SpectrumImageTexture::Evaluate's RGB (textures.cpp:386-397) reduced to the sigmoid
 // coefficients and scale of its RGBAlbedoSpectrum / RGBUnboundedSpectrum
+template <bool AllowEWA = true>
 PHD void SpectrumImageCoeffs(const TexView &T, const DeviceTexNode &nd, const TexEvalCtx &c, float out[4]) {
     TexCoord2 tc = MapST(nd, c);
     tc.t = 1 - tc.t;
     const DeviceImage im = T.images[nd.image];
-    const MipVal<true> f = MipFilter<true>(T, im, nd.filter, nd.p[27], tc.s, tc.t, tc.dsdx, tc.dtdx, tc.dsdy, tc.dtdy);
+    const MipVal<true> f =
+        MipFilter<true, AllowEWA>(T, im, nd.filter, nd.p[27], tc.s, tc.t, tc.dsdx, tc.dtdx, tc.dsdy, tc.dtdy);
     const float sc = nd.p[26];
     float rgb[3] = {sc * f.v[0], sc * f.v[1], sc * f.v[2]};
     for (int i = 0; i < 3; ++i) rgb[i] = std::fmax(0.f, (nd.flags & 8) ? 1 - rgb[i] : rgb[i]);

@@ -1055,19 +1055,21 @@ __device__ inline float TexFloatAt(const DeviceScene &S, int prog, const TexEval
     TexPhase1(S.tex, pg, c, R);
     return R[pg.result];
 }
-// A hit's textured spectrum parameter: the phase-1 registers of its program; a program that is
-// one albedo RGB leaf (an image texture) reduces to the sigmoid coefficients in R[0..2]
-struct HitSpectrumTex {
-    DeviceTexProgram pg;
-    float R[kTexMaxRegs];
-    __device__ float At(const DeviceScene &S, float lambda) const {
-        if (pg.simple) return SigmoidPolynomial(R[0], R[1], R[2], lambda);
-        return TexPhase2(S.tex, pg, R, lambda);
+// FloatTexture::Evaluate with the one-instruction programs (a constant, an image) evaluated
+// directly, without the register file.  Full = false: the host guarantees every program is
+// one of those and no image filters with EWA (k_texture's lean instantiation)
+template <bool Full = true>
+__device__ inline float TexFloatFast(const DeviceScene &S, int prog, const TexEvalCtx &c) {
+    const DeviceTexProgram pg = S.tex.progs[prog];
+    if (!Full || pg.n1 == 1) {
+        const DeviceTexInstr in = S.tex.instrs[pg.p1];
+        const DeviceTexNode &nd = S.tex.nodes[in.node];
+        const int op = in.op & 0xff;
+        if (op == kT1FConst) return nd.p[22];
+        if (!Full || op == kT1FImage) return FloatImageEval<Full>(S.tex, nd, c);
     }
-};
-__device__ inline void EvalSpectrumTex(const DeviceScene &S, int prog, const TexEvalCtx &c, HitSpectrumTex *h) {
-    h->pg = S.tex.progs[prog];
-    TexPhase1(S.tex, h->pg, c, h->R);
+    if constexpr (Full) return TexFloatAt(S, prog, c);
+    else return 0.f;
 }
 
 // ToSensorRGB accumulation for one wavelength: sx += xbar * (c / pdf) (film.h:95-100)

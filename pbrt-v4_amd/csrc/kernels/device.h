@@ -254,6 +254,11 @@ struct PathState {
     float *filterW;     // [N]
     // work queues: record indices of the current depth
     int *matQ[kNumMatTypes];  // [NR] each: hits per material type
+    // textured materials (k_texture, before each shade launch), by record index: the hit's
+    // reflectance as sigmoid coefficients c0 c1 c2 + a flag (1: the per-wavelength values are
+    // in texR), then the TrowbridgeReitz alphas of a textured roughness; null when untextured
+    float *texCoef;     // [6][NR]
+    float *texR;        // [31][NR] general reflectance expressions (null when none)
     int *escQ;          // [NR] escaped rays (only with infinite lights)
     int *emitQ;         // [NR] hits on emissive triangles
     int *counters;      // [CounterIndex(maxDepth + 2, 0, 0)]: per depth, queue and shard

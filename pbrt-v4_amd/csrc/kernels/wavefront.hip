@@ -312,7 +312,7 @@ __device__ inline void ShadeSpectralPass(int depth, const FD *dense, const Senso
     float m = -kInfinity;
 #pragma unroll 1
     for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next()) {
-        const float R = rf(it.lam);
+        const float R = rf(it.lam, it.i);
         const float bfi = (depth > 0 ? bf[it.i * kBlock] : 1.f) * (R * kInvPi);
         const int off = DenseOffset(it.lam);
         float Le = scale * (off < 0 ? 0.f : float(dense[off]));
@@ -511,23 +511,20 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
             float4 mc = matsL[mat];
             int mflags = matConstL[mat];  // bit 0: constant R, bit 1: R != 0 at every wavelength
             bool constant = mflags & 1;
-            // a textured reflectance: one RGB leaf becomes this hit's sigmoid coefficients; any
-            // other expression is evaluated per wavelength (texR)
-            HitSpectrumTex htex;
+            // a textured reflectance (k_texture's result for this record): sigmoid coefficients,
+            // or per-wavelength values for a general expression (texR)
             bool texR = false;
             if constexpr (Tex) {
-                const int tp = S.matTex[mat].x;
-                if (tp >= 0) {
-                    EvalSpectrumTex(S, tp, HitTexCtx(S, surf), &htex);
+                if (S.matTex[mat].x >= 0) {
                     mflags = 0;
                     constant = false;
-                    if (htex.pg.simple) mc = make_float4(htex.R[0], htex.R[1], htex.R[2], 0.f);
-                    else texR = true;
+                    if (st.texCoef[3 * (size_t)N + ri] != 0) texR = true;
+                    else mc = make_float4(st.texCoef[ri], st.texCoef[(size_t)N + ri], st.texCoef[2 * (size_t)N + ri], 0.f);
                 }
             }
-            auto rfun = [&](float lam) -> float {
+            auto rfun = [&](float lam, int i) -> float {
                 if constexpr (Tex) {
-                    if (texR) return Clampf(htex.At(S, lam), 0, 1);
+                    if (texR) return Clampf(st.texR[(size_t)i * N + ri], 0, 1);
                 }
                 return Reflectance(mc, constant, lam);
             };
@@ -561,7 +558,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                 else if (mflags & 2) Rnz = true;
                 else {
                     Rnz = false;
-                    for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next()) Rnz |= rfun(it.lam) != 0;
+                    for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next()) Rnz |= rfun(it.lam, it.i) != 0;
                 }
                 Frame frame = Frame::FromXZ(Normalize(surf.dpdus), ns);
                 V3 woL = frame.ToLocal(wo);
@@ -791,27 +788,15 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
             const float4 mp = S.matParams[mat];
             TrowbridgeReitz tr{mp.x, mp.y};
             float4 mc = T.matsL[mat];
-            HitSpectrumTex htex;
             bool texR = false;
             if constexpr (Tex) {
                 const int4 mt = S.matTex[mat];
-                if (mt.x >= 0 || mt.y >= 0) {
-                    const TexEvalCtx tc = HitTexCtx(S, surf);
-                    if (mt.y >= 0) {
-                        // texEval(uRoughness / vRoughness), RoughnessToAlpha when remapped, then the
-                        // TrowbridgeReitzDistribution constructor's clamp
-                        float ur = TexFloatAt(S, mt.y, tc), vr = TexFloatAt(S, mt.z, tc);
-                        if (mt.w) {
-                            ur = RoughnessToAlpha(ur);
-                            vr = RoughnessToAlpha(vr);
-                        }
-                        tr = TrowbridgeReitz::Make(ur, vr);
-                    }
-                    if (MT == kMatConductorT && mt.x >= 0) {
-                        EvalSpectrumTex(S, mt.x, tc, &htex);
-                        if (htex.pg.simple) mc = make_float4(htex.R[0], htex.R[1], htex.R[2], 0.f);
-                        else texR = true;
-                    }
+                // k_texture's results for this record: the roughness alphas (remapped and clamped)
+                // and a conductor's reflectance
+                if (mt.y >= 0) tr = TrowbridgeReitz{st.texCoef[4 * (size_t)N + ri], st.texCoef[5 * (size_t)N + ri]};
+                if (MT == kMatConductorT && mt.x >= 0) {
+                    if (st.texCoef[3 * (size_t)N + ri] != 0) texR = true;
+                    else mc = make_float4(st.texCoef[ri], st.texCoef[(size_t)N + ri], st.texCoef[2 * (size_t)N + ri], 0.f);
                 }
             }
             if (S.regularize && (inFlags & 2)) tr.Regularize();  // surfscatter.cpp:127-128
@@ -820,7 +805,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
             // conductor eta_i / k_i: piecewise-linear spectra, or from the albedo "reflectance"
             const int etaSpec = MT == kMatConductorT ? S.matSpectra[2 * mat] : -1;
             const int kSpec = MT == kMatConductorT ? S.matSpectra[2 * mat + 1] : -1;
-            auto etaK = [&](float lam, float *e, float *k) {
+            auto etaK = [&](float lam, int li, float *e, float *k) {
                 if (etaSpec >= 0) {
                     const int a = S.plOffsets[etaSpec], na = S.plOffsets[etaSpec + 1] - a;
                     const int b = S.plOffsets[kSpec], nb = S.plOffsets[kSpec + 1] - b;
@@ -834,7 +819,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
                 } else {
                     float rv = SigmoidPolynomial(mc.x, mc.y, mc.z, lam);
                     if constexpr (Tex) {
-                        if (texR) rv = htex.At(S, lam);
+                        if (texR) rv = st.texR[(size_t)li * N + ri];
                     }
                     float r = Clampf(rv, 0, .9999f);
                     *e = 1.f;
@@ -893,7 +878,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
                                     float f = fd;
                                     if constexpr (MT == kMatConductorT) {
                                         float e, k;
-                                        etaK(it.lam, &e, &k);
+                                        etaK(it.lam, it.i, &e, &k);
                                         f = ConductorF(ct, e, k);
                                     }
                                     acc.Add(T.sensorL, off, bf[it.i * kBlock] * f * absdot * Le * invDenom, it.i == 0);
@@ -949,7 +934,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
                         float f = fd;
                         if constexpr (MT == kMatConductorT) {
                             float e, k;
-                            etaK(it.lam, &e, &k);
+                            etaK(it.lam, it.i, &e, &k);
                             f = ConductorF(ct, e, k);
                             fAny |= f != 0;
                         }
@@ -1021,6 +1006,62 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
             out.pixel[j] = slot;
             out.prevIdx[j] = ri;
             out.sidx[j] = sidx;
+        }
+    }
+}
+
+// The texture stage of EvaluateMaterialAndBSDF (surfscatter.cpp:74-137, materials.h GetBxDF's
+// texEval calls) over one material type's queue, ahead of that type's shade launch: per textured
+// hit the uv derivatives (Approximate_dp_dxy), then the reflectance (one RGB image leaf -> this
+// hit's sigmoid coefficients; any other expression -> its 31 values) and the roughness alphas
+// (RoughnessToAlpha when remapped, the TrowbridgeReitzDistribution clamp).  Keeping the
+// texture code out of the shade kernels keeps them at their untextured register budget.
+// Full = false (host-chosen per material type): every textured parameter of the type is a single
+// image (or constant) leaf filtered without EWA -- the register-file interpreter and the EWA
+// filter are not compiled in.
+template <int MT, bool Full>
+__global__ void __launch_bounds__(kBlock) k_texture(DeviceScene S, PathState st, int depth) {
+    const QueueView mats = LoadQueue(st, depth, MatCounter(MT));
+    const int N = st.NR;
+    const PathRecords &rec = st.rec[depth & 1];
+    const int *hitPrim = st.hitPrim[depth & 1];
+    const float *hitB = st.hitB[depth & 1];
+    for (int qi = blockIdx.x * blockDim.x + threadIdx.x; qi < mats.total; qi += gridDim.x * blockDim.x) {
+        const int ri = st.matQ[MT][QueueSlot(mats, qi)];
+        const int prim = hitPrim[ri];
+        const int mat = S.primMaterial[prim];
+        const int4 mt = S.matTex[mat];
+        if (mt.x < 0 && mt.y < 0) continue;
+        V3 p0, p1, p2;
+        PrimVerts(S, prim, &p0, &p1, &p2);
+        const TriSurface surf = SurfaceAt(S, prim, p0, p1, p2, hitB[ri], hitB[N + ri], hitB[2 * N + ri]);
+        const TexEvalCtx tc = HitTexCtx(S, surf);
+        if (mt.x >= 0) {
+            const DeviceTexProgram pg = S.tex.progs[mt.x];
+            if (!Full || pg.simple) {
+                float c[4];
+                SpectrumImageCoeffs<Full>(S.tex, S.tex.nodes[S.tex.instrs[pg.p1].node], tc, c);
+                st.texCoef[ri] = c[0];
+                st.texCoef[(size_t)N + ri] = c[1];
+                st.texCoef[2 * (size_t)N + ri] = c[2];
+                st.texCoef[3 * (size_t)N + ri] = 0.f;
+            } else if constexpr (Full) {
+                float R[kTexMaxRegs];
+                TexPhase1(S.tex, pg, tc, R);
+                for (SpectralIter it(rec.lambda0[ri]); it.i < kNSpectrumSamples; it.Next())
+                    st.texR[(size_t)it.i * N + ri] = TexPhase2(S.tex, pg, R, it.lam);
+                st.texCoef[3 * (size_t)N + ri] = 1.f;
+            }
+        }
+        if (mt.y >= 0) {
+            float ur = TexFloatFast<Full>(S, mt.y, tc), vr = TexFloatFast<Full>(S, mt.z, tc);
+            if (mt.w) {
+                ur = RoughnessToAlpha(ur);
+                vr = RoughnessToAlpha(vr);
+            }
+            const TrowbridgeReitz t = TrowbridgeReitz::Make(ur, vr);
+            st.texCoef[4 * (size_t)N + ri] = t.ax;
+            st.texCoef[5 * (size_t)N + ri] = t.ay;
         }
     }
 }
@@ -1258,6 +1299,20 @@ static size_t ShadeLdsBytes(const DeviceScene &S, int depth, bool withPl = false
     const ShadeLdsLayout &L = S.shadeLds;
     return (size_t)(depth < kShadeLdsDepths ? L.totalByDepth[depth] : L.total) +
            (withPl && L.plInLds ? (size_t)L.plCount * 8 : 0);
+}
+hipError_t LaunchTexture(const DeviceScene &S, const PathState &st, int depth, int type, bool full, int maxCount,
+                         hipStream_t s) {
+    const dim3 grid(SmallGridFor(maxCount));
+#define K_TEX(mt)                                                                             \
+    do {                                                                                      \
+        if (full) hipLaunchKernelGGL((k_texture<mt, true>), grid, dim3(kBlock), 0, s, S, st, depth);  \
+        else hipLaunchKernelGGL((k_texture<mt, false>), grid, dim3(kBlock), 0, s, S, st, depth);      \
+    } while (0)
+    if (type == kMatDiffuseT) K_TEX(kMatDiffuseT);
+    else if (type == kMatDielectricT) K_TEX(kMatDielectricT);
+    else K_TEX(kMatConductorT);
+#undef K_TEX
+    return hipGetLastError();
 }
 hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int depth, int maxCount, bool lean,
                               hipStream_t s) {

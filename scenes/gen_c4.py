@@ -5,10 +5,18 @@ rough conductor ground, lit by a large quad light and a uniform sky.  The defaul
 copies of a 81,920-triangle sphere + a 2-triangle ground + the light = 9,994,244 triangles,
 written as binary little-endian PLY files (one per copy) next to the .pbrt file.
 
+Textured (the default, as BASELINE configs[3] "San-Miguel (~10M tris, textured)"): every mesh
+carries per-vertex uv, the diffuse copies read their reflectance from one of eight 8-bit sRGB
+PNG image textures (256^2 .. 1024^2, written next to the scene, bilinear or trilinear MIP
+filtering, random uv scales), the metals and the ground their roughness from float image
+textures.  --untextured writes round 2's constant-material scene.
+
     python scenes/gen_c4.py OUTDIR                       # full C4: 1920x1080, 128 spp
     python scenes/gen_c4.py OUTDIR --copies 6 --level 3  # small variant for tests
 """
 import argparse
+import struct
+import zlib
 from pathlib import Path
 
 import numpy as np
@@ -16,27 +24,87 @@ import numpy as np
 from gen_c3 import icosphere, outward
 
 
-def write_ply(path, P, F):
-    """binary_little_endian PLY: float x y z, faces as uchar-count int indices"""
-    P = np.ascontiguousarray(P, dtype="<f4")
+def write_ply(path, P, F, UV=None):
+    """binary_little_endian PLY: float x y z (u v), faces as uchar-count int indices"""
+    V = P if UV is None else np.concatenate([P, UV], axis=1)
+    V = np.ascontiguousarray(V, dtype="<f4")
     faces = np.zeros(len(F), dtype=[("n", "u1"), ("i", "<i4", (3,))])
     faces["n"] = 3
     faces["i"] = F
     head = (f"ply\nformat binary_little_endian 1.0\nelement vertex {len(P)}\n"
             "property float x\nproperty float y\nproperty float z\n"
+            + ("" if UV is None else "property float u\nproperty float v\n") +
             f"element face {len(F)}\nproperty list uchar int vertex_indices\nend_header\n")
     with open(path, "wb") as f:
         f.write(head.encode())
-        f.write(P.tobytes())
+        f.write(V.tobytes())
         f.write(faces.tobytes())
 
 
-def generate(outdir, copies=122, level=6, xres=1920, yres=1080, spp=128, seed=0, maxdepth=5):
+def write_png(path, img):
+    """8-bit RGB (or grey) PNG, filter type 0 rows (numpy + zlib)"""
+    img = np.ascontiguousarray(np.clip(img, 0, 255).astype(np.uint8))
+    h, w = img.shape[:2]
+    ct = 2 if img.ndim == 3 else 0
+    raw = np.concatenate([np.zeros((h, 1), np.uint8), img.reshape(h, -1)], axis=1).tobytes()
+
+    def chunk(t, d):
+        return struct.pack(">I", len(d)) + t + d + struct.pack(">I", zlib.crc32(t + d) & 0xffffffff)
+    path.write_bytes(b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, 8, ct, 0, 0, 0)) +
+                     chunk(b"IDAT", zlib.compress(raw, 6)) + chunk(b"IEND", b""))
+
+
+def texture_images(out, rng):
+    """eight albedo images (bricks, stripes, tiles, wood, noise, checks, rings, plaster) and two
+    grey roughness maps; sizes 256^2 .. 1024^2"""
+    names = []
+    for t in range(8):
+        n = [256, 512, 1024, 512, 256, 1024, 512, 256][t]
+        y, x = np.mgrid[0:n, 0:n].astype(np.float32) / n
+        base = rng.uniform(40, 200, 3)
+        if t % 4 == 0:
+            pat = ((np.floor(x * 8 + (np.floor(y * 16) % 2) * 0.5) + np.floor(y * 16)) % 2)[..., None]
+        elif t % 4 == 1:
+            pat = (0.5 + 0.5 * np.sin(2 * np.pi * (x * 6 + 2 * np.sin(2 * np.pi * y * 3))))[..., None]
+        elif t % 4 == 2:
+            pat = (((np.floor(x * 12) + np.floor(y * 12)) % 3) / 2.0)[..., None]
+        else:
+            r = np.sqrt((x - .5) ** 2 + (y - .5) ** 2)
+            pat = (0.5 + 0.5 * np.sin(60 * r))[..., None]
+        noise = rng.uniform(-25, 25, (n, n, 1))
+        img = base[None, None, :] * (0.45 + 0.55 * pat) + noise
+        name = f"c4_tex{t}.png"
+        write_png(out / name, img)
+        names.append(name)
+    for t in range(2):
+        n = 512
+        y, x = np.mgrid[0:n, 0:n].astype(np.float32) / n
+        g = 40 + 160 * (0.5 + 0.5 * np.sin(2 * np.pi * (x * (4 + 3 * t) + y * 2))) + rng.uniform(-20, 20, (n, n))
+        name = f"c4_gloss{t}.png"
+        write_png(out / name, g)
+        names.append(name)
+    return names
+
+
+def generate(outdir, copies=122, level=6, xres=1920, yres=1080, spp=128, seed=0, maxdepth=5, textured=True):
     out = Path(outdir)
     out.mkdir(parents=True, exist_ok=True)
     rng = np.random.default_rng(seed)
     P0, F0 = icosphere(level)
     F0 = outward(P0, F0, np.zeros(3))
+    # spherical uv of the unit sphere (u around y, v from the pole)
+    UV0 = np.stack([np.arctan2(P0[:, 2], P0[:, 0]) / (2 * np.pi) + 0.5,
+                    np.arccos(np.clip(P0[:, 1] / np.linalg.norm(P0, axis=1), -1, 1)) / np.pi], axis=1)
+    tex_lines = []
+    if textured:
+        names = texture_images(out, np.random.default_rng(seed + 1))
+        for t in range(8):
+            filt = "trilinear" if t % 2 else "bilinear"
+            tex_lines.append(f'Texture "albedo{t}" "spectrum" "imagemap" "string filename" "{names[t]}" '
+                             f'"string filter" "{filt}"')
+        for t in range(2):
+            tex_lines.append(f'Texture "gloss{t}" "float" "imagemap" "string filename" "{names[8 + t]}" '
+                             f'"float scale" 0.35')
     # a jittered 3D grid of copies in front of the camera (rows recede into the distance)
     nx = int(np.ceil(np.sqrt(copies / 2)))
     rows = int(np.ceil(copies / (2 * nx)))
@@ -55,12 +123,19 @@ def generate(outdir, copies=122, level=6, xres=1920, yres=1080, spp=128, seed=0,
                            j * 1.4 + rng.uniform(-0.2, 0.2)])
         P = P0 * (r * scale)[:, None] + center
         name = f"c4_{c:04d}.ply"
-        write_ply(out / name, P, F0)
+        write_ply(out / name, P, F0, UV0 if textured else None)
         n_tris += len(F0)
         if c % 3 == 2:
             metal = ["metal-Au", "metal-Cu", "metal-Al"][c % 9 // 3]
-            mat = (f'Material "conductor" "spectrum eta" "{metal}-eta" "spectrum k" "{metal}-k" '
-                   f'"float roughness" [ {rng.uniform(0.01, 0.3):.4f} ]')
+            rough = (f'"texture roughness" "gloss{c % 2}"' if textured
+                     else f'"float roughness" [ {rng.uniform(0.01, 0.3):.4f} ]')
+            mat = f'Material "conductor" "spectrum eta" "{metal}-eta" "spectrum k" "{metal}-k" {rough}'
+        elif textured:
+            # a per-copy scaled view of one of the eight images (the scale folds into the image)
+            tex = f"albedo{c % 8}"
+            mat = (f'Texture "a{c}" "spectrum" "scale" "texture tex" "{tex}" '
+                   f'"float scale" {rng.uniform(0.6, 1.0):.4f}\n'
+                   f'Material "diffuse" "texture reflectance" "a{c}"')
         else:
             rgb = rng.uniform(0.15, 0.85, 3)
             mat = f'Material "diffuse" "rgb reflectance" [ {rgb[0]:.4f} {rgb[1]:.4f} {rgb[2]:.4f} ]'
@@ -87,9 +162,11 @@ AttributeBegin
       "point3 P" [ -6 9 -2  6 9 -2  6 9 {depth:.2f}  -6 9 {depth:.2f} ]
 AttributeEnd
 
-Material "conductor" "spectrum eta" [ 300 0.3 800 0.3 ] "spectrum k" [ 300 3.5 800 3.5 ] "float roughness" [ 0.2 ]
+""" + "\n".join(tex_lines) + ("\n" if tex_lines else "") + f"""
+Material "conductor" "spectrum eta" [ 300 0.3 800 0.3 ] "spectrum k" [ 300 3.5 800 3.5 ] {'"texture roughness" "gloss0"' if textured else '"float roughness" [ 0.2 ]'}
 Shape "trianglemesh" "integer indices" [ 0 1 2 0 2 3 ]
     "point3 P" [ -40 0 -10  -40 0 {depth + 40:.2f}  40 0 {depth + 40:.2f}  40 0 -10 ]
+    "point2 uv" [ 0 0  0 20  20 20  20 0 ]
 
 """ + "\n".join(lines) + "\n"
     (out / "c4.pbrt").write_text(text)
@@ -104,8 +181,9 @@ def main():
     ap.add_argument("--xres", type=int, default=1920)
     ap.add_argument("--yres", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=128)
+    ap.add_argument("--untextured", action="store_true")
     a = ap.parse_args()
-    path, n = generate(a.outdir, a.copies, a.level, a.xres, a.yres, a.spp)
+    path, n = generate(a.outdir, a.copies, a.level, a.xres, a.yres, a.spp, textured=not a.untextured)
     print(path, n, "triangles")
 
 

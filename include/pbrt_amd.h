@@ -171,6 +171,9 @@ typedef struct pbrt_scene_flat {
     const int32_t *material_tex;
     float camera_from_render[12];
     float camera_min_diff[12];
+    /* MixMaterial (materials.h:271-350, type 8): [n_materials][4] material 0, material 1, root
+     * node of the float "amount" texture (constant or image), 0; -1 for other materials */
+    const int32_t *material_mix;
 } pbrt_scene_flat;
 
 typedef struct pbrt_render_params {

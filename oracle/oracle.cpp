@@ -3449,6 +3449,30 @@ struct Renderer {
             if (wf == S.maxDepth) break;
             // Material::GetBxDF (materials.h:466-471 diffuse, :182-204 dielectric, :491-511 conductor)
             int mat = f->tri_material[prim];
+            // MixMaterial::ChooseMaterial at the closest hit (wavefront/intersect.h:90-97,
+            // materials.h:285-294): amount texture without (u,v) derivatives, HashFloat(p, wo,
+            // m0, m1) with the material indices standing in for pbrt's material pointers
+            while (f->material_mix && f->material_type[mat] == 8) {
+                const int32_t *mm = f->material_mix + 4 * mat;
+                OTexCtx c0;
+                c0.p = si.p;
+                c0.n = si.n;
+                c0.u = si.uv[0];
+                c0.v = si.uv[1];
+                const Float amt = tex.EvalF(mm[2], c0);
+                if (amt <= 0) mat = mm[0];
+                else if (amt >= 1) mat = mm[1];
+                else {
+                    unsigned char buf[40];
+                    const Float pv[6] = {si.p.x, si.p.y, si.p.z, si.wo.x, si.wo.y, si.wo.z};
+                    const uint64_t m0 = (uint32_t)mm[0], m1 = (uint32_t)mm[1];
+                    std::memcpy(buf, pv, 24);
+                    std::memcpy(buf + 24, &m0, 8);
+                    std::memcpy(buf + 32, &m1, 8);
+                    const Float u = (Float)(uint32_t)Murmur64A(buf, 40, 0) * 0x1p-32f;
+                    mat = (amt < u) ? mm[0] : mm[1];
+                }
+            }
             const float *mc = f->material_coeffs + 4 * mat;
             BxDF bx;
             bx.type = f->material_type[mat];

@@ -104,6 +104,7 @@ struct TexTables {
     std::vector<DeviceTexProgram> progs;
     std::vector<int32_t> matTex;      // [nMaterials][4] program indices + remap
     std::vector<int32_t> matTexNode;  // [nMaterials][4] the programs' root nodes + remap (oracle)
+    std::vector<int32_t> matMixNode;  // [nMaterials][4] mix: material 0, 1, amount root node, 0
     std::vector<int32_t> nodeInfo, imageInfo, levelInfo, rawInfo;
     std::vector<float> nodeParams, specFlat, rawGamma;
     std::vector<uint8_t> rawData;
@@ -183,6 +184,7 @@ static void BuildTexTables(const SceneDesc &s, TexTables *t) {
         auto root = [&](int p) { return p >= 0 ? s.texPrograms[p].root : -1; };
         t->matTexNode.insert(t->matTexNode.end(),
                              {root(m.texReflectance), root(m.texURough), root(m.texVRough), m.remapRoughness ? 1 : 0});
+        t->matMixNode.insert(t->matMixNode.end(), {m.mixMat[0], m.mixMat[1], root(m.texAmount), 0});
     }
 }
 static CameraDiff MakeCameraDiff(const SceneDesc &s) {
@@ -213,6 +215,7 @@ static TexView HostTexView(const TexTables &t) {
     v.rgbCoeffs = rgb.data() + 64;
     v.ewaLut = GetSpectralData().mipFilterLUT.data();
     v.nProgs = (int)t.progs.size();
+    v.nLuts = (int)t.images.size();
     return v;
 }
 
@@ -372,6 +375,8 @@ struct pbrt_context {
     DevBuf<DeviceTexProgram> texProgs;
     DevBuf<int> matTex;
     DevBuf<float> texCoef, texR;  // k_texture results (PathState::texCoef / texR)
+    DevBuf<int> matMix, hitMat;   // mix materials: {m0, m1, amount program} and resolved materials
+    bool hasMix = false;
     bool texGeneral = false;      // some textured reflectance is not a single image leaf
     int texTypeMask = 0;          // bit t: some material of type t is textured
     int texFullMask = 0;          // bit t: ... with an expression beyond one non-EWA image leaf
@@ -745,12 +750,19 @@ static void BuildDevice(pbrt_context *c) {
         BuildTexTables(s, &tt);
         c->matTex.Upload(tt.matTex);
         S.matTex = (const int4 *)c->matTex.p;
+        std::vector<int> mm;
+        for (const MaterialDesc &m : s.materials) {
+            mm.insert(mm.end(), {m.mixMat[0], m.mixMat[1], m.texAmount, 0});
+            c->hasMix = c->hasMix || m.type == kMatMix;
+        }
+        c->matMix.Upload(mm);
+        S.matMix = (const int4 *)c->matMix.p;
         S.textured = s.texPrograms.empty() ? 0 : 1;
         S.tex = TexView{};
         if (S.textured) {
             if (c->volumetric)
-                throw Error("textures together with the volumetric path (media, interface, layered, thin dielectric, "
-                            "diffuse transmission or dispersive materials) are not supported yet");
+                throw Error("textures or mix materials together with the volumetric path (media, interface, layered, "
+                            "thin dielectric, diffuse transmission or dispersive materials) are not supported yet");
             c->texNodes.Upload(tt.nodes);
             c->texSpec.Upload(tt.spec);
             c->texImages.Upload(tt.images);
@@ -774,6 +786,7 @@ static void BuildDevice(pbrt_context *c) {
             S.tex.rgbCoeffs = c->rgbTable.p + 64;
             S.tex.ewaLut = c->ewaLut.p;
             S.tex.nProgs = (int)tt.progs.size();
+            S.tex.nLuts = (int)tt.images.size();
             S.camDiff = MakeCameraDiff(s);
             // a program k_texture's lean instantiation evaluates: one image leaf without EWA
             // (reflectance: the albedo RGB leaf; roughness: a float image or a constant)
@@ -979,9 +992,10 @@ constexpr int kPathFloats = 101, kPathInts = 16;
 // hitB 4, shadow ray 6 + Ld/r_u/r_l 93 + lambda0 = 100 floats; records 2 x (flags, pixel,
 // depth, medium) = 8, hitPrim, 5 queues, shadow pixel + medium + flags = 17 ints
 constexpr int kVolFloats = 330, kVolInts = 17;
-static int64_t PathStateBytesPerPath(bool volumetric, bool dispersive, bool textured = false, bool texGeneral = false) {
+static int64_t PathStateBytesPerPath(bool volumetric, bool dispersive, bool textured = false, bool texGeneral = false,
+                                     bool mix = false) {
     return 4 * (kPathFloats + kPathInts) + (volumetric ? 4 * (kVolFloats + kVolInts) : 0) + (dispersive ? 16 : 0) +
-           (textured ? 24 : 0) + (texGeneral ? 124 : 0);
+           (textured ? 24 : 0) + (texGeneral ? 124 : 0) + (mix ? 8 : 0);
 }
 
 static void AllocPaths(pbrt_context *c, int64_t N) {
@@ -1002,6 +1016,7 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
         c->texCoef.Alloc((size_t)6 * NR);
         if (c->texGeneral) c->texR.Alloc((size_t)kNSpectrumSamples * NR);
     }
+    if (c->hasMix) c->hitMat.Alloc((size_t)2 * NR);
     c->maxPaths = N;
     PathState &st = c->st;
     st.capS = (int)capS;
@@ -1045,6 +1060,8 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
     st.counters = ip;
     st.texCoef = c->texCoef.p;
     st.texR = c->texR.p;
+    st.hitMat[0] = c->hasMix ? c->hitMat.p : nullptr;
+    st.hitMat[1] = c->hasMix ? c->hitMat.p + NR : nullptr;
     if (c->volumetric) {
         const int vf = kVolFloats, vi = kVolInts;
         c->vfState.Alloc((size_t)vf * NR);
@@ -1233,7 +1250,7 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
             const bool lean = !noLean && c->S.samplerType == 0 &&
                               (uint64_t)(st.firstSample + nS) * haltonStride <= (1ull << 24) &&
                               c->S.shadeLds.lightsInLds && c->S.shadeLds.denseInLds && c->S.triShade == nullptr &&
-                              c->S.nDelta == 0 && !c->S.textured;
+                              c->S.nDelta == 0 && !c->S.textured && !c->hasMix;
             for (int depth = 0; depth <= s.maxDepth; ++depth) {
                 // closest-hit launches are event-timed in the first pass of a render only: the
                 // passes are statistically identical and each event pair costs a queue gap
@@ -1426,6 +1443,7 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
         f->image_raw_offset = t.rawOffset.data();
         f->image_raw_data = t.rawData.data();
         f->material_tex = t.matTexNode.data();
+        f->material_mix = t.matMixNode.data();
         for (int k = 0; k < 12; ++k) f->camera_from_render[k] = s.cameraFromRender[k];
         for (int k = 0; k < 3; ++k) {
             f->camera_min_diff[k] = s.minPosDx[k];
@@ -1516,7 +1534,7 @@ int pbrt_context_create(const pbrt_scene *scene, int device, int64_t maxPaths, p
             // smaller cards): path-state bytes per path from AllocPaths' layout
             size_t freeB = 0, totalB = 0;
             HIPCHECK(hipMemGetInfo(&freeB, &totalB));
-            const int64_t perPath = PathStateBytesPerPath(c->volumetric, c->S.dispersive, c->S.textured, c->texGeneral);
+            const int64_t perPath = PathStateBytesPerPath(c->volumetric, c->S.dispersive, c->S.textured, c->texGeneral, c->hasMix);
             const int64_t fit = (int64_t)(freeB / 4 * 3) / perPath - kShards * 320;
             if (fit < 4096) throw Error("not enough free device memory for path state");
             maxPaths = std::min<int64_t>(maxPaths, fit);

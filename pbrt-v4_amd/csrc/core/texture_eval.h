@@ -73,7 +73,9 @@ struct TexView {
     const float *rgbCoeffs;     // RGBToSpectrumTable data[3][64][64][64][3]
     const float *ewaLut;        // MIPFilterLUT[128]
     int nProgs;
+    int nLuts;                  // images (one 256-entry decode table each)
 };
+constexpr int kTexLdsLuts = 16;  // k_texture stages up to this many images' decode tables in LDS
 
 // TextureEvalContext as the wavefront material stage builds it (workitems.h:288-304)
 struct TexEvalCtx {

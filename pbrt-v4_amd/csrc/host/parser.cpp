@@ -377,6 +377,8 @@ class Parser {
         bool hasRough = false;
         Param ur, vr;  // type "" = constant 0 (no parameter)
         bool remap = true;
+        bool hasAmount = false;  // mix: "amount" (default 0.5)
+        Param amount;
     };
     std::vector<MatTexPending> matTexPending;
     void ResolveTextures();
@@ -663,6 +665,20 @@ class Parser {
             } else {
                 throw Error(ps.loc + ": reflectance of type " + r->type + " not supported");
             }
+        } else if (type == "mix") {
+            // MixMaterial::Create (materials.cpp:105-125, scene.cpp CreateMaterials): two named
+            // materials and a float "amount" texture the closest-hit stage can evaluate
+            m.type = kMatMix;
+            Param *ms = ps.Find("materials", "string");
+            if (!ms || ms->strs.size() != 2) throw Error(ps.loc + ": Must provide two values for \"string materials\" for mix material.");
+            for (int k = 0; k < 2; ++k) {
+                auto it = namedMaterials.find(ms->strs[k]);
+                if (it == namedMaterials.end()) throw Error(ps.loc + ": " + ms->strs[k] + ": named material not found.");
+                m.mixMat[k] = it->second;
+            }
+            MatTexPending &mp = PendingTex(ps.loc);
+            mp.hasAmount = true;
+            if (Param *a = ps.Find("amount")) mp.amount = *a;
         } else if (type == "interface") {
             // a null material: the surface only bounds media (scene.cpp: "interface")
             m.type = kMatInterface;
@@ -1901,6 +1917,14 @@ int Parser::InstTex(const std::string &name, bool spectrum, int specType, const 
 void Parser::ResolveTextures() {
     for (MatTexPending &mp : matTexPending) {
         MaterialDesc &m = scene.materials[mp.mat];
+        if (mp.hasAmount) {
+            const int node = FloatParamNode(mp.amount.type.empty() ? nullptr : &mp.amount, 0.5f, mp.loc);
+            const int k = scene.textures[node].kind;
+            if (k != kTexConstant && k != kTexImage)
+                throw Error(mp.loc + ": The wavefront renderer currently only supports basic textures for its \"amount\" parameter.");
+            m.texAmount = CompileTexProgram(scene, node, false);
+            continue;
+        }
         if (m.type != kMatDiffuse && m.type != kMatDielectric && m.type != kMatConductor)
             throw Error(mp.loc + ": textures are supported on diffuse, dielectric and conductor materials only");
         if (mp.hasRefl) {
@@ -1915,6 +1939,19 @@ void Parser::ResolveTextures() {
         }
     }
     if (!matTexPending.empty()) ComputeCameraDifferentials(scene);
+    // a mix of mixes must bottom out in real materials (materials.cpp: a cycle never resolves)
+    for (size_t i = 0; i < scene.materials.size(); ++i) {
+        int m = (int)i, steps = 0;
+        std::vector<int> stack{m};
+        while (!stack.empty()) {
+            const int x = stack.back();
+            stack.pop_back();
+            if (scene.materials[x].type != kMatMix) continue;
+            if (++steps > 64) throw Error("mix material \"" + scene.materials[i].name + "\" refers to itself");
+            stack.push_back(scene.materials[x].mixMat[0]);
+            stack.push_back(scene.materials[x].mixMat[1]);
+        }
+    }
 }
 
 SceneDesc LoadPbrtString(const std::string &text, const std::string &baseDir,

@@ -37,6 +37,9 @@ constexpr int kMatInterface = 3;
 constexpr int kMatCoatedDiffuse = 4, kMatCoatedConductor = 5;
 constexpr int kMatThinDielectric = 6;  // ThinDielectricBxDF (bxdfs.h:342-404), volumetric kernels
 constexpr int kMatDiffuseTransmission = 7;  // DiffuseTransmissionBxDF (bxdfs.h:218-296), k_vlayered
+// MixMaterial (materials.h:271-350): resolved per hit to one of its two materials by the
+// closest-hit stage (wavefront/intersect.h:90-97); never shaded itself
+constexpr int kMatMix = 8;
 
 // Participating media (media.h:209-350, media.cpp:167-330).  Spectra are DenselySampled
 // 395..705 nm tables in SceneDesc::denseSpectra with pbrt's constructor scaling applied
@@ -82,6 +85,9 @@ struct MaterialDesc {
     // diffuse / conductor "reflectance" (SpectrumType::Albedo), {u,v}roughness (float)
     int texReflectance = -1, texURough = -1, texVRough = -1;
     bool remapRoughness = true;  // applied on the device when a roughness is textured
+    // mix: the two materials and the "amount" texture program (constant or image)
+    int mixMat[2] = {-1, -1};
+    int texAmount = -1;
     std::string name;
 };
 

@@ -1036,6 +1036,11 @@ __device__ inline float Reflectance(float4 mc, bool constant, float lambda) {
     return Clampf(r, 0, 1);
 }
 
+// the material a hit shades with: its triangle's, or with mix materials the one k_closest chose
+__device__ inline int HitMaterial(const DeviceScene &S, const PathState &st, int depth, int ri, int prim) {
+    return st.hitMat[0] ? st.hitMat[depth & 1][ri] : S.primMaterial[prim];
+}
+
 // ---- textures (core/texture_eval.h)
 // TextureEvalContext of a hit as the wavefront material stage builds it: p, n, uv and the
 // (u,v) screen-space derivatives from Approximate_dp_dxy (surfscatter.cpp:74-104, 132-135)
@@ -1181,4 +1186,39 @@ __device__ inline void GenerateCameraRay(const DeviceScene &S, const PathState &
     *dOut = d;
 }
 
+}  // namespace pbrt_amd
+
+namespace pbrt_amd {
+// MixMaterial::ChooseMaterial until a non-mix material is reached (materials.h:285-294), as the
+// closest-hit stage does (wavefront/intersect.h:90-97): the "amount" texture at the hit (the
+// context a SurfaceInteraction gives: no (u,v) derivatives), then HashFloat(p, wo, m0, m1).
+// pbrt hashes the two materials' pointers; their indices stand in for them here (the oracle
+// does the same), so which material an interior amount picks is not comparable with pbrt.
+__device__ __attribute__((noinline)) int ResolveMixMaterial(const DeviceScene &S, int prim, int mat, float b0, float b1,
+                                                            float b2, V3 d) {
+    V3 p0, p1, p2;
+    PrimVerts(S, prim, &p0, &p1, &p2);
+    const TriSurface surf = SurfaceAt(S, prim, p0, p1, p2, b0, b1, b2);
+    TexEvalCtx c;
+    c.p = surf.p;
+    c.n = surf.n;
+    c.u = surf.uv[0];
+    c.v = surf.uv[1];
+    c.dudx = c.dudy = c.dvdx = c.dvdy = 0;
+    const V3 wo = Normalize(-d);
+    for (int guard = 0; guard < 64 && S.matType[mat] == kMatMixT; ++guard) {
+        const int4 mm = S.matMix[mat];
+        const float amt = TexFloatFast(S, mm.z, c);
+        if (amt <= 0) mat = mm.x;
+        else if (amt >= 1) mat = mm.y;
+        else {
+            const uint32_t w[10] = {FloatToBits(c.p.x), FloatToBits(c.p.y), FloatToBits(c.p.z), FloatToBits(wo.x),
+                                    FloatToBits(wo.y),  FloatToBits(wo.z),  (uint32_t)mm.x,     0u,
+                                    (uint32_t)mm.y,     0u};
+            const float u = (float)(uint32_t)HashWords(w, 10) * 0x1p-32f;
+            mat = (amt < u) ? mm.x : mm.y;
+        }
+    }
+    return mat;
+}
 }  // namespace pbrt_amd

@@ -62,6 +62,7 @@ constexpr int kMatDiffuseT = 0, kMatDielectricT = 1, kMatConductorT = 2;
 constexpr int kMatCoatedDiffuseT = 4, kMatCoatedConductorT = 5;  // layered (volumetric path only)
 constexpr int kMatThinDielectricT = 6;                           // volumetric path only
 constexpr int kMatDiffuseTransmissionT = 7;                      // k_vlayered
+constexpr int kMatMixT = 8;  // MixMaterial: resolved per hit by k_closest<kClosestMix>
 PHD int MatCounter(int type) { return type == 0 ? kCntMat : kCntMat + 3 + type; }
 PHD int CounterIndex(int depth, int queue, int shard) {
     return ((depth * kNumQueues + queue) * kShards + shard) * kCounterPad;
@@ -207,6 +208,8 @@ struct DeviceScene {
     TexView tex;
     CameraDiff camDiff;
     const int4 *matTex;
+    // MixMaterial: per material {material 0, material 1, amount program, 0}
+    const int4 *matMix;
 };
 
 // One depth's path records, compacted: record i is the i-th ray of that depth (pbrt's
@@ -259,6 +262,8 @@ struct PathState {
     // in texR), then the TrowbridgeReitz alphas of a textured roughness; null when untextured
     float *texCoef;     // [6][NR]
     float *texR;        // [31][NR] general reflectance expressions (null when none)
+    // scenes with mix materials: each hit's resolved material, by depth parity (null otherwise)
+    int *hitMat[2];
     int *escQ;          // [NR] escaped rays (only with infinite lights)
     int *emitQ;         // [NR] hits on emissive triangles
     int *counters;      // [CounterIndex(maxDepth + 2, 0, 0)]: per depth, queue and shard

@@ -54,9 +54,13 @@ __global__ void __launch_bounds__(kBlock) k_camera(DeviceScene S, PathState st, 
     r.ray[5 * NR + slot] = d.z;
 }
 
-// NMatQ = 1: every material is diffuse (one material queue); 3: one queue per material type
-template <int NMatQ, int TM>
+// NMatQ = 1: every material is diffuse (one material queue); 3: one queue per material type;
+// kClosestMix (4): one queue per type, and mix materials resolved per hit (into st.hitMat)
+constexpr int kClosestMix = 4;
+template <int NMatQ_, int TM>
 __global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_closest(DeviceScene S, PathState st, int depth, int timed) {
+    constexpr bool kMix = NMatQ_ == kClosestMix;
+    constexpr int NMatQ = kMix ? kNumMatTypes : NMatQ_;
     const QueueView rays = LoadQueue(st, depth, kCntRay);
     if ((int)(blockIdx.x * blockDim.x) >= rays.total) return;  // no work
     extern __shared__ float4 dynLds[];
@@ -115,7 +119,18 @@ __global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_closest(DeviceSc
         if constexpr (NMatQ == 1) {
             pred[2] = shade && active && prim >= 0;
         } else {
-            const int type = (shade && active && prim >= 0) ? S.matType[S.primMaterial[prim]] : -1;
+            int type = -1;
+            if (shade && active && prim >= 0) {
+                int mat = S.primMaterial[prim];
+                if constexpr (kMix) {
+                    if (S.matType[mat] == kMatMixT) {
+                        const V3 d(rec.ray[3 * N + qi], rec.ray[4 * N + qi], rec.ray[5 * N + qi]);
+                        mat = ResolveMixMaterial(S, prim, mat, h.b0, h.b1, h.b2, d);
+                    }
+                    st.hitMat[depth & 1][qi] = mat;
+                }
+                type = S.matType[mat];
+            }
 #pragma unroll
             for (int t = 0; t < NMatQ; ++t) pred[2 + t] = type == t;
         }
@@ -505,7 +520,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
             sidx = rec.sidx[ri];
             V3 p0, p1, p2;
             PrimVerts(S, prim, &p0, &p1, &p2);
-            const int mat = S.primMaterial[prim];
+            const int mat = Lean ? S.primMaterial[prim] : HitMaterial(S, st, depth, ri, prim);
             TriSurface surf = Lean ? TriangleSurface(p0, p1, p2, b0, b1, b2, S.primFlip[prim], nullptr)
                                    : SurfaceAt(S, prim, p0, p1, p2, b0, b1, b2);
             float4 mc = matsL[mat];
@@ -779,7 +794,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
             for (int i = 0; i < kNSpectrumSamples; ++i) bf[i * kBlock] = depth > 0 ? rec.beta[(size_t)i * N + ri] : 1.f;
             V3 p0, p1, p2;
             PrimVerts(S, prim, &p0, &p1, &p2);
-            const int mat = S.primMaterial[prim];
+            const int mat = HitMaterial(S, st, depth, ri, prim);
             const TriSurface surf = SurfaceAt(S, prim, p0, p1, p2, b0, b1, b2);
             const V3 wo = Normalize(-rd);
             const V3 n = surf.n, ns = surf.ns;
@@ -1022,6 +1037,17 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
 template <int MT, bool Full>
 __global__ void __launch_bounds__(kBlock) k_texture(DeviceScene S, PathState st, int depth) {
     const QueueView mats = LoadQueue(st, depth, MatCounter(MT));
+    if ((int)(blockIdx.x * blockDim.x) >= mats.total) return;  // no work
+    // the RGB->spectrum table's z nodes (searched per lookup) and the 8-bit decode tables of up
+    // to kTexLdsLuts images are read from LDS
+    __shared__ float zLds[64];
+    __shared__ float lutLds[kTexLdsLuts * 256];
+    const int nLut = S.tex.nLuts <= kTexLdsLuts ? S.tex.nLuts : 0;
+    for (int i = threadIdx.x; i < 64; i += blockDim.x) zLds[i] = S.tex.rgbZNodes[i];
+    for (int i = threadIdx.x; i < nLut * 256; i += blockDim.x) lutLds[i] = S.tex.luts[i];
+    __syncthreads();
+    S.tex.rgbZNodes = zLds;
+    if (nLut) S.tex.luts = lutLds;
     const int N = st.NR;
     const PathRecords &rec = st.rec[depth & 1];
     const int *hitPrim = st.hitPrim[depth & 1];
@@ -1029,7 +1055,7 @@ __global__ void __launch_bounds__(kBlock) k_texture(DeviceScene S, PathState st,
     for (int qi = blockIdx.x * blockDim.x + threadIdx.x; qi < mats.total; qi += gridDim.x * blockDim.x) {
         const int ri = st.matQ[MT][QueueSlot(mats, qi)];
         const int prim = hitPrim[ri];
-        const int mat = S.primMaterial[prim];
+        const int mat = HitMaterial(S, st, depth, ri, prim);
         const int4 mt = S.matTex[mat];
         if (mt.x < 0 && mt.y < 0) continue;
         V3 p0, p1, p2;
@@ -1277,10 +1303,13 @@ hipError_t LaunchClosest(const DeviceScene &S, const PathState &st, int depth, i
                          hipStream_t s) {
     const dim3 grid(TraversalGridFor(maxCount)), block(kBlock);
     const bool multi = S.matTypeMask & ~1;
+#define K_CLOSEST_MIX(tm) k_closest<kClosestMix, tm>
 #define K_CLOSEST_MULTI(tm) k_closest<kNumMatTypes, tm>
 #define K_CLOSEST_ONE(tm) k_closest<1, tm>
-    if (multi) PBRT_LAUNCH_TRAVERSAL(S, K_CLOSEST_MULTI, grid, block, StackBytes(S), s, S, st, depth, timed);
+    if (st.hitMat[0]) PBRT_LAUNCH_TRAVERSAL(S, K_CLOSEST_MIX, grid, block, StackBytes(S), s, S, st, depth, timed);
+    else if (multi) PBRT_LAUNCH_TRAVERSAL(S, K_CLOSEST_MULTI, grid, block, StackBytes(S), s, S, st, depth, timed);
     else PBRT_LAUNCH_TRAVERSAL(S, K_CLOSEST_ONE, grid, block, StackBytes(S), s, S, st, depth, timed);
+#undef K_CLOSEST_MIX
 #undef K_CLOSEST_MULTI
 #undef K_CLOSEST_ONE
     return hipGetLastError();

@@ -86,6 +86,7 @@ class SceneFlat(ctypes.Structure):
         ("image_raw_gamma", ctypes.POINTER(ctypes.c_float)), ("image_raw_offset", ctypes.POINTER(ctypes.c_uint64)),
         ("image_raw_data", ctypes.POINTER(ctypes.c_uint8)), ("material_tex", ctypes.POINTER(ctypes.c_int32)),
         ("camera_from_render", ctypes.c_float * 12), ("camera_min_diff", ctypes.c_float * 12),
+        ("material_mix", ctypes.POINTER(ctypes.c_int32)),
     ]
 
 

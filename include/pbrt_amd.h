@@ -174,6 +174,18 @@ typedef struct pbrt_scene_flat {
     /* MixMaterial (materials.h:271-350, type 8): [n_materials][4] material 0, material 1, root
      * node of the float "amount" texture (constant or image), 0; -1 for other materials */
     const int32_t *material_mix;
+    /* ImageInfiniteLight (lights.h:557-641): infinite-list entry j is an image light when
+     * inf_image[j] >= 0 (its index here); per image light env_info [n_env][4] res (square),
+     * 0, 0, 0, env_xform [n_env][18] renderFromLight then its inverse (upper 3x3, row major),
+     * and its linear R, G, B pixels (Image::GetChannel) at env_rgb + 3 * env_offset[k]
+     * ([res][res][3], row y = v * res).  inf_spectrum / inf_scale hold the colour space's
+     * illuminant and the light's scale. */
+    int n_env;
+    const int32_t *inf_image;
+    const int32_t *env_info;
+    const float *env_xform;
+    const uint64_t *env_offset;
+    const float *env_rgb;
 } pbrt_scene_flat;
 
 typedef struct pbrt_render_params {
@@ -290,6 +302,13 @@ int pbrt_debug_rgb2spec_column(int maxc, int j, int i, float *out192);
  * float texture */
 int pbrt_debug_texture_eval(const pbrt_scene *scene, int material, int slot, const float *hit14, const float *lambda,
                             int n, float *out);
+/* ImageInfiniteLight `env` of the scene with the product's shared host/device code
+ * (lights.h:587-631, lights.cpp:1073-1083): for n directions dirs[n][3] and sample pairs
+ * u[n][2], out[n][16] = Le's (u, v) of the direction, PDF_Li(allowIncompletePDF), the pixel's
+ * RGBIlluminantSpectrum at 400 / 500 / 600 / 700 nm (light scale and illuminant 1), the
+ * compensated distribution's sample (u, v), its mapPDF, wi = renderFromLight(
+ * EqualAreaSquareToSphere(u, v)), 3 unused */
+int pbrt_debug_env_eval(const pbrt_scene *scene, int env, const float *dirs, const float *u, int n, float *out);
 /* Filter::Sample(u) of the scene's pixel filter (FilterSampler over PiecewiseConstant2D for
  * gaussian / mitchell / sinc, SampleTent for triangle, filters.h): out3 = p.x p.y weight */
 int pbrt_debug_filter_sample(const pbrt_scene *scene, float u0, float u1, float *out3);

@@ -2764,6 +2764,108 @@ static void ORGBCoeffs(Float r, Float g, Float b, Float c[3]) {
     }
 }
 
+// ImageInfiniteLight (lights.h:557-641, lights.cpp:1038-1083) over the flat view's linear
+// R, G, B pixels: compensated PiecewiseConstant2D, equal-area octahedral mapping
+// (util/math.cpp:292-361), nearest-pixel RGBIlluminantSpectrum radiance
+struct OEnvLight {
+    int n = 0;
+    const float *rgb = nullptr;
+    const float *m = nullptr, *mi = nullptr;  // renderFromLight, its inverse (3x3 row major)
+    std::vector<Distribution1D> rows;
+    Distribution1D marginal;
+    void Init(const pbrt_scene_flat *f, int k) {
+        n = f->env_info[4 * k];
+        rgb = f->env_rgb + 3 * f->env_offset[k];
+        m = f->env_xform + 18 * k;
+        mi = m + 9;
+        std::vector<Float> d((size_t)n * n);
+        for (size_t p = 0; p < d.size(); ++p) {
+            Float sum = 0;
+            for (int c = 0; c < 3; ++c) sum += rgb[3 * p + c];
+            d[p] = sum / 3;  // ImageChannelValues::Average
+        }
+        double avg = 0.;
+        for (Float v : d) avg += v;
+        avg /= d.size();
+        for (Float &v : d) v = std::max<Float>(v - avg, 0);
+        if (std::all_of(d.begin(), d.end(), [](Float v) { return v == 0; })) std::fill(d.begin(), d.end(), Float(1));
+        rows.assign(n, Distribution1D());
+        std::vector<Float> mf(n);
+        for (int v = 0; v < n; ++v) {
+            rows[v].Init(&d[(size_t)v * n], n, 0, 1);
+            mf[v] = rows[v].integral;
+        }
+        marginal.Init(mf.data(), n, 0, 1);
+    }
+    static Vec Mul(const float *a, Vec v) {
+        return Vec(a[0] * v.x + a[1] * v.y + a[2] * v.z, a[3] * v.x + a[4] * v.y + a[5] * v.z,
+                   a[6] * v.x + a[7] * v.y + a[8] * v.z);
+    }
+    static Vec SquareToSphere(Float px, Float py) {
+        Float u = 2 * px - 1, v = 2 * py - 1, up = std::abs(u), vp = std::abs(v);
+        Float sd = 1 - (up + vp), dd = std::abs(sd), r = 1 - dd;
+        Float phi = (r == 0 ? 1 : (vp - up) / r + 1) * Pi / 4;
+        Float z = std::copysign(1 - Sqr(r), sd);
+        Float cp = std::copysign(std::cos(phi), u), sp = std::copysign(std::sin(phi), v);
+        return Vec(cp * r * SafeSqrt(2 - Sqr(r)), sp * r * SafeSqrt(2 - Sqr(r)), z);
+    }
+    static void SphereToSquare(Vec d, Float *uo, Float *vo) {
+        Float x = std::abs(d.x), y = std::abs(d.y), z = std::abs(d.z);
+        Float r = SafeSqrt(1 - z);
+        Float a = std::max(x, y), b = std::min(x, y);
+        b = a == 0 ? 0 : b / a;
+        // EvaluatePolynomial(b, t1..t7) = FMA(b, EvaluatePolynomial(b, t2..t7), t1)
+        static const Float t[7] = {0.406758566246788489601959989e-5f, 0.636226545274016134946890922156f,
+                                   0.61572017898280213493197203466e-2f, -0.247333733281268944196501420480f,
+                                   0.881770664775316294736387951347e-1f, 0.419038818029165735901852432784e-1f,
+                                   -0.251390972343483509333252996350e-1f};
+        Float phi = t[6];
+        for (int i = 5; i >= 0; --i) phi = std::fma(b, phi, t[i]);
+        if (x < y) phi = 1 - phi;
+        Float v = phi * r, u = r - v;
+        if (d.z < 0) {
+            std::swap(u, v);
+            u = 1 - u;
+            v = 1 - v;
+        }
+        u = std::copysign(u, d.x);
+        v = std::copysign(v, d.y);
+        *uo = 0.5f * (u + 1);
+        *vo = 0.5f * (v + 1);
+    }
+    // Image::LookupNearestChannel with WrapMode::OctahedralSphere, then RGBIlluminantSpectrum
+    // of ClampZero(rgb) (util/spectrum.cpp:246-251) times the light scale
+    Spectrum Le(Float u, Float v, const Wavelengths &lambda, const float *illum, Float lightScale) const {
+        int x = (int)(u * n), y = (int)(v * n);
+        if (x < 0) x = -x, y = n - 1 - y;
+        else if (x >= n) x = 2 * n - 1 - x, y = n - 1 - y;
+        if (y < 0) x = n - 1 - x, y = -y;
+        else if (y >= n) x = n - 1 - x, y = 2 * n - 1 - y;
+        if (n == 1) x = y = 0;
+        const float *px = rgb + 3 * ((size_t)y * n + x);
+        Float c3[3] = {std::max<Float>(0, px[0]), std::max<Float>(0, px[1]), std::max<Float>(0, px[2])};
+        Float mx = std::max({c3[0], c3[1], c3[2]}), scale = 2 * mx, co[3];
+        if (scale) ORGBCoeffs(c3[0] / scale, c3[1] / scale, c3[2] / scale, co);
+        else ORGBCoeffs(0, 0, 0, co);
+        Spectrum s;
+        for (int i = 0; i < NS; ++i) s[i] = scale * Sigmoid(co[0], co[1], co[2], lambda.lambda[i]);
+        return (s * SampleDense(illum, lambda)) * lightScale;
+    }
+    // compensatedDistribution.Sample / PDF (util/sampling.h:760-779)
+    bool Sample(Float u0, Float u1, Float *uo, Float *vo, Float *mapPDF) const {
+        Float p1, p0;
+        int iv, iu;
+        *vo = marginal.Sample(u1, &p1, &iv);
+        *uo = rows[iv].Sample(u0, &p0, &iu);
+        *mapPDF = p0 * p1;
+        return *mapPDF != 0;
+    }
+    Float PDF(Float u, Float v) const {
+        int iu = std::clamp((int)(u * n), 0, n - 1), iv = std::clamp((int)(v * n), 0, n - 1);
+        return rows[iv].func[iu] / marginal.integral;
+    }
+};
+
 struct OTexCtx {
     Vec p, n;
     Float u = 0, v = 0, dudx = 0, dudy = 0, dvdx = 0, dvdy = 0;
@@ -3103,6 +3205,13 @@ struct OTextures {
 
 // ---------------------------------------------------------------- integrator
 struct Renderer {
+    std::vector<OEnvLight> envs;  // ImageInfiniteLights (flat inf_image)
+    // the image light behind global light index li, or null
+    const OEnvLight *EnvOf(int li) const {
+        const int j = li - f->n_area_lights - f->n_point_spot;
+        if (f->n_env == 0 || j < 0 || f->inf_image[j] < 0) return nullptr;
+        return &envs[f->inf_image[j]];
+    }
     Scene S;
     OTextures tex;
     Lights lights;
@@ -3408,14 +3517,31 @@ struct Renderer {
                 if (!beta || !r_u || depth == S.maxDepth) break;
             }
             if (prim < 0) {
-                // HandleEscapedRays: uniform infinite lights, PDF_Li(allowIncomplete)=0
+                // HandleEscapedRays (integrator.cpp:495-537): uniform infinite lights, whose
+                // PDF_Li(allowIncomplete) is 0, and image infinite lights
                 for (int k = 0; k < f->n_infinite_lights; ++k) {
                     if (f->inf_distant[k] >= 0) continue;  // DistantLight: not an Infinite-type light
-                    Spectrum Le = SampleDense(f->dense_spectra + 311 * f->inf_spectrum[k], lambda) * f->inf_scale[k];
+                    const int gi = f->n_area_lights + f->n_point_spot + k;
+                    const OEnvLight *E = EnvOf(gi);
+                    const float *illum = f->dense_spectra + 311 * f->inf_spectrum[k];
+                    Spectrum Le;
+                    if (E) {
+                        Float u, v;
+                        OEnvLight::SphereToSquare(Normalize(OEnvLight::Mul(E->mi, rd)), &u, &v);
+                        Le = E->Le(u, v, lambda, illum, f->inf_scale[k]);
+                    } else {
+                        Le = SampleDense(illum, lambda) * f->inf_scale[k];
+                    }
                     if (!Le) continue;
                     if (depth == 0 || specularBounce) L = L + beta * Le / r_u.Average();
                     else {
-                        Spectrum rl = r_l * 0.f;
+                        Float pdfLi = 0;
+                        if (E) {
+                            Float u, v;
+                            OEnvLight::SphereToSquare(OEnvLight::Mul(E->mi, rd), &u, &v);
+                            pdfLi = E->PDF(u, v) / (4 * Pi);
+                        }
+                        Spectrum rl = r_l * lights.PMF(prevP, prevNs, gi) * pdfLi;
                         L = L + beta * Le / (r_u + rl).Average();
                     }
                 }
@@ -3651,7 +3777,28 @@ struct Renderer {
                 Float lpmf;
                 DeltaSample ds;
                 const bool sampledL = lights.Sample(cp, si.ns, dUc, &li, &lpmf);
-                if (sampledL && li >= f->n_area_lights && DeltaLi(li, cp, lambda, &ds)) {
+                const OEnvLight *E = sampledL ? EnvOf(li) : nullptr;
+                Float eu, ev, emap;
+                if (E) {
+                    // ImageInfiniteLight::SampleLi(allowIncompletePDF) (lights.h:594-618): a light
+                    // point 2 sceneRadius away without error bounds or normal
+                    if (E->Sample(dU0, dU1, &eu, &ev, &emap)) {
+                        const int k = li - f->n_area_lights - f->n_point_spot;
+                        Vec wi = OEnvLight::Mul(E->m, OEnvLight::SquareToSphere(eu, ev));
+                        Vec lp = cp + wi * (2 * f->scene_radius);
+                        Spectrum Le = E->Le(eu, ev, lambda, f->dense_spectra + 311 * f->inf_spectrum[k], f->inf_scale[k]);
+                        Vec wiL = toLocal(wi);
+                        Spectrum fv = woL.z == 0 ? Spectrum(0.f) : layered ? lay.f(woL, wiL, true) : bx.f(woL, wiL);
+                        if (Le && fv) {
+                            Spectrum b2 = oldBeta * fv * AbsDotN(si.ns, wi);
+                            Float lightPDF = emap / (4 * Pi) * lpmf;
+                            Float bsdfPDF = woL.z == 0 ? 0 : layered ? lay.PDF(woL, wiL, true) : bx.PDF(woL, wiL);
+                            Spectrum ru = r_u * bsdfPDF, rl = r_u * lightPDF;
+                            Vec pf = OffsetRayOrigin(si.p, si.err, si.n, lp - si.p);
+                            shadow(pf, lp - pf, DotN(si.n, lp - pf) > 0 ? mOut : mIn, b2 * Le, ru, rl);
+                        }
+                    }
+                } else if (sampledL && li >= f->n_area_lights && DeltaLi(li, cp, lambda, &ds)) {
                     // a delta light: pdf 1, no BSDF MIS weight (IsDeltaLight), the light point
                     // has no error bounds and no normal (SpawnRayTo leaves it where it is)
                     Vec wi = ds.wi, wiL = toLocal(wi);
@@ -3783,6 +3930,9 @@ int oracle_render(const pbrt_scene_flat *flat, const pbrt_scene_info *info, cons
     r.S.Init(flat, info);
     if (flat->n_tex_nodes > 0 && (!g_rgbTable || !g_ewaLut)) return -2;  // oracle_set_rgb_table first
     r.tex.Init(flat, info->spp, info->xres, info->yres);
+    if ((flat->n_env > 0 || flat->n_tex_nodes > 0) && !g_rgbTable) return -2;
+    r.envs.resize(flat->n_env);
+    for (int k = 0; k < flat->n_env; ++k) r.envs[k].Init(flat, k);
     r.lights.Init(flat);
     r.lights.uniformFlag = uniformLightSampler != 0;
     r.M.f = flat;
@@ -3909,6 +4059,42 @@ int oracle_texture_eval(const pbrt_scene_flat *flat, const pbrt_scene_info *info
         Wavelengths L = Wavelengths::SampleUniform(0.f);
         for (int k = 0; k < NS; ++k) L.lambda[k] = lambda[i];
         out[4 + i] = t.EvalS(node, c, L)[0];
+    }
+    return 0;
+}
+// the oracle's ImageInfiniteLight lookups, laid out as pbrt_debug_env_eval's rows
+int oracle_env_eval(const pbrt_scene_flat *flat, int env, const float *dirs, const float *u, int n, float *out) {
+    if (!g_rgbTable) return -2;
+    if (env < 0 || env >= flat->n_env) return -1;
+    OEnvLight E;
+    E.Init(flat, env);
+    static const float kLam[4] = {400.f, 500.f, 600.f, 700.f};
+    float one[311];
+    std::fill(one, one + 311, 1.f);
+    for (int i = 0; i < n; ++i) {
+        float *o = out + 16 * (size_t)i;
+        const Vec d(dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2]);
+        Float uu, vv, pu, pv;
+        OEnvLight::SphereToSquare(Normalize(OEnvLight::Mul(E.mi, d)), &uu, &vv);
+        o[0] = uu;
+        o[1] = vv;
+        OEnvLight::SphereToSquare(OEnvLight::Mul(E.mi, d), &pu, &pv);
+        o[2] = E.PDF(pu, pv) / (4 * Pi);
+        for (int k = 0; k < 4; ++k) {
+            Wavelengths L = Wavelengths::SampleUniform(0.f);
+            for (int j = 0; j < NS; ++j) L.lambda[j] = kLam[k];
+            o[3 + k] = E.Le(uu, vv, L, one, 1.f)[0];
+        }
+        Float su, sv, mp;
+        E.Sample(u[2 * i], u[2 * i + 1], &su, &sv, &mp);
+        o[7] = su;
+        o[8] = sv;
+        o[9] = mp;
+        const Vec wi = OEnvLight::Mul(E.m, OEnvLight::SquareToSphere(su, sv));
+        o[10] = wi.x;
+        o[11] = wi.y;
+        o[12] = wi.z;
+        o[13] = o[14] = o[15] = 0;
     }
     return 0;
 }

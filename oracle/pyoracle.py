@@ -49,6 +49,7 @@ def lib():
         _lib.oracle_intersect_tr.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int, vp]
         _lib.oracle_set_rgb_table.argtypes = [vp, vp]
         _lib.oracle_texture_eval.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_int, vp]
+        _lib.oracle_env_eval.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_int, vp]
         _lib.oracle_camera_min_diff.argtypes = [vp, vp, vp]
         _lib.oracle_image_level.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int64,
                                             ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
@@ -85,6 +86,17 @@ def texture_eval(scene, material, slot, hit14, lambdas=()):
                                    lam.ctypes.data, lam.size, out.ctypes.data)
     assert rc == 0, rc
     return out[:4].copy(), (out[4:4 + lam.size].copy() if slot == 0 else float(out[4]))
+
+
+def env_eval(scene, env, dirs, u):
+    """The oracle's ImageInfiniteLight lookups, rows as pbrt_amd.Scene.env_eval returns them"""
+    flat = scene.flat()
+    d = f32(dirs).reshape(-1, 3)
+    uu = f32(u).reshape(-1, 2)
+    out = np.zeros((len(d), 16), np.float32)
+    rc = lib().oracle_env_eval(ctypes.byref(flat), env, d.ctypes.data, uu.ctypes.data, len(d), out.ctypes.data)
+    assert rc == 0, rc
+    return out
 
 
 def camera_min_diff(scene):

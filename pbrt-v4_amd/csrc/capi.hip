@@ -219,6 +219,27 @@ static TexView HostTexView(const TexTables &t) {
     return v;
 }
 
+// ImageInfiniteLight::ImageLe's RGBIlluminantSpectrum per pixel (lights.h:625-631,
+// util/spectrum.cpp:246-251): ClampZero(rgb), scale = 2 max, coefficients of rgb / scale
+static std::vector<EnvCoef> BuildEnvCoefs(const EnvLightDesc &e) {
+    const std::vector<float> &tab = RGBToSpectrumTableData();
+    TexView T{};
+    T.rgbZNodes = tab.data();
+    T.rgbCoeffs = tab.data() + 64;
+    const size_t np = (size_t)e.res * e.res;
+    std::vector<EnvCoef> out(np);
+    for (size_t p = 0; p < np; ++p) {
+        const float r = std::max(0.f, e.rgb[3 * p]), g = std::max(0.f, e.rgb[3 * p + 1]), b = std::max(0.f, e.rgb[3 * p + 2]);
+        const float m = std::max(r, std::max(g, b));
+        const float scale = 2 * m;
+        float c[3];
+        if (scale != 0) RGBToCoeffs(T, r / scale, g / scale, b / scale, c);
+        else RGBToCoeffs(T, 0, 0, 0, c);
+        out[p] = EnvCoef{c[0], c[1], c[2], scale};
+    }
+    return out;
+}
+
 struct pbrt_scene {
     SceneDesc desc;
     // flattened copies for pbrt_scene_get_flat
@@ -228,9 +249,25 @@ struct pbrt_scene {
     std::vector<int32_t> tris, lightPrim, lightSpectrum, lightTwoSided, infSpectrum, matConstant, nodeInfo, matType,
         matSpectra, plOffsets, infDistant, uniformOrder;
     std::vector<float> deltaLights;
+    std::vector<int32_t> infImage, envInfo;
+    std::vector<float> envXform, envRgb;
+    std::vector<uint64_t> envOffset;
     TexTables tex;
     void Flatten() {
         const SceneDesc &s = desc;
+        infImage.clear();
+        for (auto &l : s.infiniteLights) infImage.push_back(l.image);
+        envInfo.clear();
+        envXform.clear();
+        envRgb.clear();
+        envOffset.clear();
+        for (const EnvLightDesc &e : s.envLights) {
+            envInfo.insert(envInfo.end(), {e.res, 0, 0, 0});
+            envXform.insert(envXform.end(), e.renderFromLight, e.renderFromLight + 9);
+            envXform.insert(envXform.end(), e.lightFromRender, e.lightFromRender + 9);
+            envOffset.push_back(envRgb.size() / 3);
+            envRgb.insert(envRgb.end(), e.rgb.begin(), e.rgb.end());
+        }
         BuildTexTables(s, &tex);
         verts.clear();
         for (V3 v : s.verts) {
@@ -375,6 +412,10 @@ struct pbrt_context {
     DevBuf<DeviceTexProgram> texProgs;
     DevBuf<int> matTex;
     DevBuf<float> texCoef, texR;  // k_texture results (PathState::texCoef / texR)
+    DevBuf<int> infImage;
+    DevBuf<EnvCoef> envCoef;
+    DevBuf<float> envDist;
+    DevBuf<DeviceEnvLight> envLights;
     DevBuf<int> matMix, hitMat;   // mix materials: {m0, m1, amount program} and resolved materials
     bool hasMix = false;
     bool texGeneral = false;      // some textured reflectance is not a single image leaf
@@ -597,6 +638,34 @@ static void BuildDevice(pbrt_context *c) {
         std::vector<int> idist;
         for (auto &l : s.infiniteLights) idist.push_back(l.distant);
         c->infDistant.Upload(idist);
+        // image infinite lights: per-pixel spectra and the compensated sampling distribution
+        std::vector<int> iimg;
+        for (auto &l : s.infiniteLights) iimg.push_back(l.image);
+        c->infImage.Upload(iimg);
+        std::vector<EnvCoef> coefs;
+        std::vector<float> dist;
+        std::vector<DeviceEnvLight> els;
+        std::vector<std::pair<size_t, size_t>> offs;
+        for (const EnvLightDesc &e : s.envLights) {
+            const std::vector<EnvCoef> ec = BuildEnvCoefs(e);
+            const std::vector<float> dt = BuildEnvDistribution(e);
+            offs.push_back({coefs.size(), dist.size()});
+            coefs.insert(coefs.end(), ec.begin(), ec.end());
+            dist.insert(dist.end(), dt.begin(), dt.end());
+        }
+        c->envCoef.Upload(coefs);
+        c->envDist.Upload(dist);
+        for (size_t k = 0; k < s.envLights.size(); ++k) {
+            const EnvLightDesc &e = s.envLights[k];
+            DeviceEnvLight d{};
+            std::memcpy(d.m, e.renderFromLight, sizeof(d.m));
+            std::memcpy(d.mi, e.lightFromRender, sizeof(d.mi));
+            d.res = e.res;
+            d.coef = c->envCoef.p + offs[k].first;
+            d.dist = FilterTableView{e.res, e.res, c->envDist.p + offs[k].second};
+            els.push_back(d);
+        }
+        c->envLights.Upload(els);
         std::vector<DeviceDeltaLight> dd;
         for (auto &d : s.deltaLights) {
             DeviceDeltaLight x{};
@@ -704,6 +773,9 @@ static void BuildDevice(pbrt_context *c) {
     if (S.dispersive && !s.media.empty())
         throw std::runtime_error("a dielectric with spectral eta (dispersion) together with participating media is not supported yet");
     c->volumetric = c->volumetric || S.dispersive;
+    if (c->volumetric && !s.envLights.empty())
+        throw Error("image infinite lights together with the volumetric path (media, interface, layered, thin "
+                    "dielectric, diffuse transmission or dispersive materials) are not supported yet");
     S.media.cameraMedium = s.cameraMedium;
     S.media.allGrey = 1;
     for (size_t m = 0; m < s.media.size(); ++m) {
@@ -820,6 +892,9 @@ static void BuildDevice(pbrt_context *c) {
     S.infSpectrum = c->infSpectrum.p;
     S.infScale = c->infScale.p;
     S.infDistant = c->infDistant.p;
+    S.infImage = c->infImage.p;
+    S.env = c->envLights.p;
+    S.nEnv = (int)s.envLights.size();
     S.nDelta = (int)s.deltaLights.size();
     S.nPointSpot = s.nPointSpot;
     S.delta = c->deltaLights.p;
@@ -1250,7 +1325,7 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
             const bool lean = !noLean && c->S.samplerType == 0 &&
                               (uint64_t)(st.firstSample + nS) * haltonStride <= (1ull << 24) &&
                               c->S.shadeLds.lightsInLds && c->S.shadeLds.denseInLds && c->S.triShade == nullptr &&
-                              c->S.nDelta == 0 && !c->S.textured && !c->hasMix;
+                              c->S.nDelta == 0 && c->S.nEnv == 0 && !c->S.textured && !c->hasMix;
             for (int depth = 0; depth <= s.maxDepth; ++depth) {
                 // closest-hit launches are event-timed in the first pass of a render only: the
                 // passes are statistically identical and each event pair costs a queue gap
@@ -1425,6 +1500,12 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
     f->n_point_spot = s.nPointSpot;
     f->delta_lights = scene->deltaLights.data();
     f->inf_distant = scene->infDistant.data();
+    f->n_env = (int)scene->desc.envLights.size();
+    f->inf_image = scene->infImage.data();
+    f->env_info = scene->envInfo.data();
+    f->env_xform = scene->envXform.data();
+    f->env_offset = scene->envOffset.data();
+    f->env_rgb = scene->envRgb.data();
     f->uniform_order = scene->uniformOrder.data();
     f->scene_radius = s.sceneRadius;
     {
@@ -1907,6 +1988,50 @@ int pbrt_debug_texture_eval(const pbrt_scene *scene, int material, int slot, con
         }
         for (int i = 0; i < n; ++i)
             out[4 + i] = pg.simple ? SigmoidPolynomial(R[0], R[1], R[2], lambda[i]) : TexPhase2(T, pg, R, lambda[i]);
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_debug_env_eval(const pbrt_scene *scene, int env, const float *dirs, const float *u, int n, float *out) {
+    try {
+        if (!scene || !dirs || !u || !out) return Fail("null argument");
+        const SceneDesc &s = scene->desc;
+        if (env < 0 || env >= (int)s.envLights.size()) return Fail("environment light index out of range");
+        const EnvLightDesc &e = s.envLights[env];
+        const std::vector<EnvCoef> coef = BuildEnvCoefs(e);
+        const std::vector<float> dist = BuildEnvDistribution(e);
+        DeviceEnvLight E{};
+        std::memcpy(E.m, e.renderFromLight, sizeof(E.m));
+        std::memcpy(E.mi, e.lightFromRender, sizeof(E.mi));
+        E.res = e.res;
+        E.coef = coef.data();
+        E.dist = FilterTableView{e.res, e.res, dist.data()};
+        static const float kLam[4] = {400.f, 500.f, 600.f, 700.f};
+        for (int i = 0; i < n; ++i) {
+            float *o = out + 16 * (size_t)i;
+            const V3 d(dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2]);
+            float uu, vv;
+            EqualAreaSphereToSquare(Normalize(MulM3(E.mi, d)), &uu, &vv);
+            o[0] = uu;
+            o[1] = vv;
+            float pu, pv;
+            EqualAreaSphereToSquare(MulM3(E.mi, d), &pu, &pv);
+            o[2] = EnvPDF(E, pu, pv) / (4 * kPi);
+            const EnvCoef c = EnvCoefAt(E, uu, vv);
+            for (int k = 0; k < 4; ++k) o[3 + k] = EnvLe(c, 1.f, 1.f, kLam[k]);
+            float su, sv, mp;
+            EnvSampleUV(E, u[2 * i], u[2 * i + 1], &su, &sv, &mp);
+            o[7] = su;
+            o[8] = sv;
+            o[9] = mp;
+            const V3 wi = MulM3(E.m, EqualAreaSquareToSphere(su, sv));
+            o[10] = wi.x;
+            o[11] = wi.y;
+            o[12] = wi.z;
+            o[13] = o[14] = o[15] = 0;
+        }
         return 0;
     } catch (const std::exception &e) {
         return Fail(e.what());

@@ -1570,6 +1570,109 @@ PHD float SamplePC1D(const float *func, const float *cdf, int n, float funcInt, 
     *pdf = (funcInt > 0) ? func[o] / funcInt : 0;
     return Lerpf((o + du) / n, mn, mx);
 }
+// ---------------------------------------------------------------- image infinite lights
+// EqualAreaSquareToSphere / EqualAreaSphereToSquare (util/math.cpp:292-361, Clarberg's
+// equal-area octahedral mapping); EvaluatePolynomial is FMA-based
+PHD V3 EqualAreaSquareToSphere(float px, float py) {
+    const float u = 2 * px - 1, v = 2 * py - 1;
+    const float up = std::fabs(u), vp = std::fabs(v);
+    const float signedDistance = 1 - (up + vp);
+    const float d = std::fabs(signedDistance);
+    const float r = 1 - d;
+    const float phi = (r == 0 ? 1 : (vp - up) / r + 1) * kPi / 4;
+    const float z = std::copysign(1 - Sqr(r), signedDistance);
+    const float cosPhi = std::copysign(std::cos(phi), u);
+    const float sinPhi = std::copysign(std::sin(phi), v);
+    return V3(cosPhi * r * SafeSqrt(2 - Sqr(r)), sinPhi * r * SafeSqrt(2 - Sqr(r)), z);
+}
+PHD void EqualAreaSphereToSquare(V3 d, float *uo, float *vo) {
+    const float x = std::fabs(d.x), y = std::fabs(d.y), z = std::fabs(d.z);
+    const float r = SafeSqrt(1 - z);
+    const float a = std::fmax(x, y);
+    float b = std::fmin(x, y);
+    b = a == 0 ? 0 : b / a;
+    const float t1 = 0.406758566246788489601959989e-5f, t2 = 0.636226545274016134946890922156f,
+                t3 = 0.61572017898280213493197203466e-2f, t4 = -0.247333733281268944196501420480f,
+                t5 = 0.881770664775316294736387951347e-1f, t6 = 0.419038818029165735901852432784e-1f,
+                t7 = -0.251390972343483509333252996350e-1f;
+    float phi = fmaf(b, fmaf(b, fmaf(b, fmaf(b, fmaf(b, fmaf(b, t7, t6), t5), t4), t3), t2), t1);
+    if (x < y) phi = 1 - phi;
+    float v = phi * r;
+    float u = r - v;
+    if (d.z < 0) {
+        const float t = u;
+        u = v;
+        v = t;
+        u = 1 - u;
+        v = 1 - v;
+    }
+    u = std::copysign(u, d.x);
+    v = std::copysign(v, d.y);
+    *uo = 0.5f * (u + 1);
+    *vo = 0.5f * (v + 1);
+}
+// One ImageInfiniteLight's device tables: per pixel the RGBIlluminantSpectrum of the clamped
+// RGB as {c0, c1, c2, scale}, and the compensated PiecewiseConstant2D over [0,1]^2 in the
+// FilterTableView layout.  m: renderFromLight, mi: its inverse (upper 3x3, row major).
+struct alignas(16) EnvCoef {
+    float c0, c1, c2, s;  // sigmoid polynomial coefficients and RGBIlluminantSpectrum::scale
+};
+struct DeviceEnvLight {
+    float m[9], mi[9];
+    int res, pad;
+    const EnvCoef *coef;
+    FilterTableView dist;
+};
+PHD V3 MulM3(const float *m, V3 v) {
+    return V3(m[0] * v.x + m[1] * v.y + m[2] * v.z, m[3] * v.x + m[4] * v.y + m[5] * v.z,
+              m[6] * v.x + m[7] * v.y + m[8] * v.z);
+}
+// Image::LookupNearestChannel(uv, c, OctahedralSphere) (util/image.h:351-356, 96-125)
+PHD EnvCoef EnvCoefAt(const DeviceEnvLight &E, float u, float v) {
+    int x = (int)(u * E.res), y = (int)(v * E.res);
+    const int n = E.res;
+    if (x < 0) {
+        x = -x;
+        y = n - 1 - y;
+    } else if (x >= n) {
+        x = 2 * n - 1 - x;
+        y = n - 1 - y;
+    }
+    if (y < 0) {
+        x = n - 1 - x;
+        y = -y;
+    } else if (y >= n) {
+        x = n - 1 - x;
+        y = 2 * n - 1 - y;
+    }
+    if (n == 1) x = y = 0;
+    return E.coef[(size_t)y * n + x];
+}
+// compensatedDistribution.Sample(u) (util/sampling.h:760-770): marginal in v from u1,
+// conditional in u from u0; *pdf = mapPDF
+PHD void EnvSampleUV(const DeviceEnvLight &E, float u0, float u1, float *uo, float *vo, float *pdf) {
+    const FilterTableView &t = E.dist;
+    float pdf1, pdf0;
+    int iv, iu;
+    *vo = SamplePC1D(t.CondInt(), t.MargCdf(), t.nv, t.MargInt(), 0.f, 1.f, u1, &pdf1, &iv);
+    *uo = SamplePC1D(t.Func() + (size_t)iv * t.nu, t.CondCdf() + (size_t)iv * (t.nu + 1), t.nu, t.CondInt()[iv], 0.f,
+                     1.f, u0, &pdf0, &iu);
+    *pdf = pdf0 * pdf1;
+}
+// compensatedDistribution.PDF(uv) (util/sampling.h:773-779)
+PHD float EnvPDF(const DeviceEnvLight &E, float u, float v) {
+    const FilterTableView &t = E.dist;
+    int iu = (int)(u * t.nu), iv = (int)(v * t.nv);
+    iu = iu < 0 ? 0 : (iu > t.nu - 1 ? t.nu - 1 : iu);
+    iv = iv < 0 ? 0 : (iv > t.nv - 1 ? t.nv - 1 : iv);
+    return t.Func()[(size_t)iv * t.nu + iu] / t.MargInt();
+}
+// RGBIlluminantSpectrum::Sample at one wavelength times the light scale (lights.h:625-631):
+// scale * ((c.w * rsp(lambda)) * illuminant(lambda))
+PHD float EnvLe(const EnvCoef &c, float lightScale, float illum, float lambda) {
+    return lightScale * ((c.s * SigmoidPolynomial(c.c0, c.c1, c.c2, lambda)) * illum);
+}
+
 // SampleTent (util/sampling.h:196-201)
 PHD float SampleTent(float u, float r) {
     float pmf;

@@ -530,7 +530,7 @@ void FinalizeScene(SceneDesc &s) {
 }
 
 // PiecewiseConstant1D ctor (util/sampling.h:625-649) into func (|f|) and cdf; returns funcInt
-static float BuildPC1D(const float *f, int n, float mn, float mx, float *func, float *cdf) {
+float BuildPC1D(const float *f, int n, float mn, float mx, float *func, float *cdf) {
     for (int i = 0; i < n; ++i) func[i] = std::fabs(f[i]);
     cdf[0] = 0;
     for (int i = 1; i < n + 1; ++i) cdf[i] = cdf[i - 1] + func[i - 1] * (mx - mn) / (float)n;
@@ -540,6 +540,36 @@ static float BuildPC1D(const float *f, int n, float mn, float mx, float *func, f
     else
         for (int i = 1; i < n + 1; ++i) cdf[i] /= funcInt;
     return funcInt;
+}
+
+// ImageInfiniteLight's compensatedDistribution (lights.cpp:1060-1070): pixel averages
+// (ImageChannelValues::Average, in float), minus their mean accumulated in double, clamped at
+// zero (all ones when nothing is left), as a PiecewiseConstant2D over [0,1]^2 in the
+// FilterTableView layout
+std::vector<float> BuildEnvDistribution(const EnvLightDesc &e) {
+    const int n = e.res;
+    std::vector<float> t(FilterTableView::Size(n, n), 0.f);
+    float *F = t.data(), *func = F + (size_t)n * n, *condCdf = func + (size_t)n * n, *condInt = condCdf + (size_t)n * (n + 1);
+    float *margCdf = condInt + n;
+    const size_t np = (size_t)n * n;
+    for (size_t p = 0; p < np; ++p) {
+        float sum = 0;
+        for (int c = 0; c < 3; ++c) sum += e.rgb[3 * p + c];
+        F[p] = sum / 3;
+    }
+    double acc = 0.;
+    for (size_t p = 0; p < np; ++p) acc += F[p];
+    const double average = acc / np;
+    bool allZero = true;
+    for (size_t p = 0; p < np; ++p) {
+        F[p] = std::max<float>((float)(F[p] - average), 0.f);
+        allZero = allZero && F[p] == 0;
+    }
+    if (allZero) std::fill(F, F + np, 1.f);
+    for (int v = 0; v < n; ++v) condInt[v] = BuildPC1D(F + (size_t)v * n, n, 0.f, 1.f, func + (size_t)v * n, condCdf + (size_t)v * (n + 1));
+    std::vector<float> margFunc(n);
+    margCdf[n + 1] = BuildPC1D(condInt, n, 0.f, 1.f, margFunc.data(), margCdf);
+    return t;
 }
 
 void BuildFilterTable(SceneDesc &s) {

@@ -24,6 +24,8 @@
 #include <string>
 #include <vector>
 
+#include <zlib.h>
+
 namespace pbrt_amd {
 
 static std::string Ext(const std::string &path) {
@@ -251,6 +253,36 @@ static void WriteEXR(const std::string &path, const float *rgb, int w, int h, bo
     }
 }
 
+// OpenEXR's RLE / ZIP(S) decoders: byte predictor, then the two half-streams interleaved
+// (the file format's documented reorder of a block's bytes)
+static void ExrUnpredict(std::vector<uint8_t> &t, std::vector<uint8_t> *out) {
+    for (size_t i = 1; i < t.size(); ++i) t[i] = (uint8_t)(int(t[i - 1]) + int(t[i]) - 128);
+    out->resize(t.size());
+    const size_t half = (t.size() + 1) / 2;
+    for (size_t i = 0, a = 0, b = half; i < t.size(); ++i) (*out)[i] = (i & 1) ? t[b++] : t[a++];
+}
+static bool ExrRle(const uint8_t *in, size_t n, size_t outSize, std::vector<uint8_t> *t) {
+    t->clear();
+    size_t i = 0;
+    while (i < n) {
+        const int c = (int8_t)in[i++];
+        if (c < 0) {
+            if (i + (size_t)-c > n) return false;
+            t->insert(t->end(), in + i, in + i + (size_t)-c);
+            i += (size_t)-c;
+        } else {
+            if (i >= n) return false;
+            t->insert(t->end(), (size_t)c + 1, in[i++]);
+        }
+        if (t->size() > outSize) return false;
+    }
+    return t->size() == outSize;
+}
+
+// Scanline OpenEXR with NONE / RLE / ZIPS / ZIP compression and HALF or FLOAT channels (what
+// Image::Read, util/image.cpp:1055-1180, takes through the OpenEXR library; PIZ and the lossy
+// codecs, tiled and deep files are refused).  chromaticities must be sRGB's
+// (RGBColorSpace::Lookup's 1e-3 relative match).
 static Image ReadEXR(const std::string &path) {
     File fp(path, "rb");
     std::vector<uint8_t> d;
@@ -281,13 +313,17 @@ static Image ReadEXR(const std::string &path) {
         return s;
     };
     if (rd32() != 20000630u) throw std::runtime_error(path + ": not an OpenEXR file");
-    if ((rd32() & 0xffu) != 2u) throw std::runtime_error(path + ": unsupported EXR version");
+    const uint32_t version = rd32();
+    if ((version & 0xffu) != 2u) throw std::runtime_error(path + ": unsupported EXR version");
+    if (version & 0x1a00u) throw std::runtime_error(path + ": tiled, multi-part and deep EXR files are not supported");
     struct Ch {
         std::string name;
         int type;
     };
     std::vector<Ch> chans;
     int compression = -1, x0 = 0, y0 = 0, x1 = -1, y1 = -1;
+    float chroma[8];
+    bool hasChroma = false;
     while (true) {
         std::string name = rdstr();
         if (name.empty()) break;
@@ -298,8 +334,12 @@ static Image ReadEXR(const std::string &path) {
         if (name == "channels") {
             while (pos < end && d[pos] != 0) {
                 std::string cn = rdstr();
-                int32_t t;
+                int32_t t, xs, ys;
+                need(16);
                 std::memcpy(&t, &d[pos], 4);
+                std::memcpy(&xs, &d[pos + 8], 4);
+                std::memcpy(&ys, &d[pos + 12], 4);
+                if (xs != 1 || ys != 1) throw std::runtime_error(path + ": subsampled EXR channels are not supported");
                 chans.push_back({cn, t});
                 pos += 16;
             }
@@ -310,10 +350,24 @@ static Image ReadEXR(const std::string &path) {
             std::memcpy(&y0, &d[pos + 4], 4);
             std::memcpy(&x1, &d[pos + 8], 4);
             std::memcpy(&y1, &d[pos + 12], 4);
+        } else if (name == "chromaticities" && size == 32) {
+            std::memcpy(chroma, &d[pos], 32);
+            hasChroma = true;
         }
         pos = end;
     }
-    if (compression != 0) throw std::runtime_error(path + ": only uncompressed EXR files are supported");
+    static const char *kCodec[] = {"NONE", "RLE", "ZIPS", "ZIP", "PIZ", "PXR24", "B44", "B44A", "DWAA", "DWAB"};
+    if (compression < 0 || compression > 3)
+        throw std::runtime_error(path + ": EXR compression " +
+                                 (compression >= 0 && compression < 10 ? kCodec[compression] : std::string("?")) +
+                                 " is not supported (NONE, RLE, ZIPS and ZIP are)");
+    if (hasChroma) {
+        // sRGB primaries and the D65 white point
+        const float srgb[8] = {.64f, .33f, .3f, .6f, .15f, .06f, .3127f, .329f};
+        for (int i = 0; i < 8; ++i)
+            if (!(chroma[i] == srgb[i] || std::abs((chroma[i] - srgb[i]) / srgb[i]) < 1e-3f))
+                throw std::runtime_error(path + ": EXR chromaticities are not sRGB's; only sRGB images are supported");
+    }
     Image im;
     im.width = x1 - x0 + 1;
     im.height = y1 - y0 + 1;
@@ -323,6 +377,8 @@ static Image ReadEXR(const std::string &path) {
     std::vector<size_t> chOff;
     for (size_t i = 0; i < chans.size(); ++i) {
         if (chans[i].type != 1 && chans[i].type != 2) throw std::runtime_error(path + ": unsupported EXR pixel type");
+        if (chans[i].type != chans[0].type)
+            throw std::runtime_error(path + ": EXR images with multiple channel types are not supported");
         chOff.push_back(lineBytes);
         lineBytes += (size_t)im.width * (chans[i].type == 1 ? 2 : 4);
         if (chans[i].name == "R") idx[0] = (int)i;
@@ -330,33 +386,57 @@ static Image ReadEXR(const std::string &path) {
         if (chans[i].name == "B") idx[2] = (int)i;
     }
     if (idx[0] < 0 || idx[1] < 0 || idx[2] < 0) throw std::runtime_error(path + ": EXR file has no R, G, B channels");
-    pos += (size_t)8 * im.height;  // offset table (lines are read in order)
+    const int linesPerBlock = compression == 3 ? 16 : 1;
+    const int nBlocks = (im.height + linesPerBlock - 1) / linesPerBlock;
+    std::vector<uint64_t> table(nBlocks);
+    need((size_t)8 * nBlocks);
+    std::memcpy(table.data(), &d[pos], (size_t)8 * nBlocks);
     im.rgb.assign((size_t)3 * im.width * im.height, 0.f);
-    for (int l = 0; l < im.height; ++l) {
+    std::vector<uint8_t> tmp, raw;
+    for (int blk = 0; blk < nBlocks; ++blk) {
+        pos = (size_t)table[blk];
         need(8);
         int32_t y, sz;
         std::memcpy(&y, &d[pos], 4);
         std::memcpy(&sz, &d[pos + 4], 4);
         pos += 8;
+        if (sz < 0) throw std::runtime_error(path + ": bad EXR block");
         need((size_t)sz);
-        if ((size_t)sz != lineBytes || y - y0 < 0 || y - y0 >= im.height)
+        const int ly = y - y0;
+        const int nl = std::min(linesPerBlock, im.height - ly);
+        if (ly < 0 || ly >= im.height || ly % linesPerBlock) throw std::runtime_error(path + ": bad EXR block");
+        const size_t rawSize = lineBytes * nl;
+        const uint8_t *src = &d[pos];
+        if ((size_t)sz == rawSize) {
+            raw.assign(src, src + rawSize);  // stored: the codec did not shrink it
+        } else if (compression == 1) {
+            if (!ExrRle(src, (size_t)sz, rawSize, &tmp)) throw std::runtime_error(path + ": corrupt RLE block");
+            ExrUnpredict(tmp, &raw);
+        } else if (compression == 2 || compression == 3) {
+            tmp.resize(rawSize);
+            uLongf outLen = (uLongf)rawSize;
+            if (uncompress(tmp.data(), &outLen, src, (uLong)sz) != Z_OK || outLen != rawSize)
+                throw std::runtime_error(path + ": corrupt ZIP block");
+            ExrUnpredict(tmp, &raw);
+        } else {
             throw std::runtime_error(path + ": bad EXR scanline");
-        for (int c = 0; c < 3; ++c) {
-            const Ch &ch = chans[idx[c]];
-            const uint8_t *p = &d[pos + chOff[idx[c]]];
-            for (int x = 0; x < im.width; ++x) {
-                float v;
-                if (ch.type == 1) {
-                    uint16_t hv;
-                    std::memcpy(&hv, p + 2 * x, 2);
-                    v = HalfToFloat(hv);
-                } else {
-                    std::memcpy(&v, p + 4 * x, 4);
-                }
-                im.rgb[((size_t)(y - y0) * im.width + x) * 3 + c] = v;
-            }
         }
-        pos += sz;
+        for (int l = 0; l < nl; ++l)
+            for (int c = 0; c < 3; ++c) {
+                const Ch &ch = chans[idx[c]];
+                const uint8_t *p = raw.data() + l * lineBytes + chOff[idx[c]];
+                for (int x = 0; x < im.width; ++x) {
+                    float v;
+                    if (ch.type == 1) {
+                        uint16_t hv;
+                        std::memcpy(&hv, p + 2 * x, 2);
+                        v = HalfToFloat(hv);
+                    } else {
+                        std::memcpy(&v, p + 4 * x, 4);
+                    }
+                    im.rgb[((size_t)(ly + l) * im.width + x) * 3 + c] = v;
+                }
+            }
     }
     return im;
 }

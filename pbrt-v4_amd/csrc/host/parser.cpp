@@ -346,8 +346,10 @@ class Parser {
         std::string type;
         ParamSet params;
         Mat4 worldFromLight;
+        std::string dir;  // directory of the file that declared it (relative "filename")
     };
     std::vector<PendingLight> lights;
+    InfiniteLightDesc InfiniteLight(PendingLight &l);
     void DeltaLight(PendingLight &l, std::vector<DeltaLightDesc> &pointSpot, std::vector<DeltaLightDesc> &distants,
                     std::vector<int> &distantEntry, std::vector<std::pair<int, int>> &lsOrder);
     struct PendingMedium {
@@ -570,6 +572,7 @@ class Parser {
             l.params = Params(toks, pos);
             l.params.loc = loc;
             l.worldFromLight = gs.ctm;
+            l.dir = dir;
             lights.push_back(std::move(l));
         } else if (d == "Shape") {
             std::string type = Str(toks, pos);
@@ -1487,26 +1490,7 @@ void Parser::Finish() {
         }
         if (l.type != "infinite") throw Error(l.params.loc + ": light \"" + l.type + "\" not supported yet");
         lsOrder.push_back({1, (int)scene.infiniteLights.size()});
-        Param *L = l.params.Find("L");
-        if (l.params.Find("filename")) throw Error(l.params.loc + ": image infinite lights not supported yet");
-        InfiniteLightDesc il;
-        std::array<float, 311> dense;
-        if (!L)
-            dense = GetSpectralData().denseD65;
-        float photometric = GetSpectralData().photometricD65;
-        if (L && L->type == "rgb" && L->nums.size() == 3)
-            dense = DenseRGBIlluminant((float)L->nums[0], (float)L->nums[1], (float)L->nums[2]);
-        else if (L && L->type == "spectrum" && !L->nums.empty()) {
-            dense = DensePiecewiseLinear(L->nums, l.params.loc);
-            photometric = PhotometricOf(dense);
-        } else if (L)
-            throw Error(l.params.loc + ": infinite light L must be rgb or spectrum");
-        scene.denseSpectra.push_back(dense);
-        il.spectrum = (int)scene.denseSpectra.size() - 1;
-        il.scale = (float)l.params.GetFloat("scale", 1) / photometric;
-        if (l.params.Find("illuminance")) throw Error(l.params.loc + ": illuminance not supported yet");
-        l.params.CheckUnused();
-        scene.infiniteLights.push_back(il);
+        scene.infiniteLights.push_back(InfiniteLight(l));
     }
     scene.nPointSpot = (int)pointSpot.size();
     scene.deltaLights = pointSpot;
@@ -1535,6 +1519,70 @@ void Parser::Finish() {
                            (scene.infiniteLights.size() - distants.size());
     if (nLights == 0) throw Error("No light sources specified");
     if (nLights == 1) scene.uniformLightSampler = true;
+}
+
+// Light::Create "infinite" (lights.cpp:1558-1694): no "L" and no "filename" -> the colour
+// space's illuminant; "L" -> UniformInfiniteLight of it; "filename" -> ImageInfiniteLight of the
+// image's R, G, B channels (square, finite, sRGB).  scale /= SpectrumToPhotometric of the
+// spectrum (the colour space's illuminant for images); "illuminance" E_v scales a uniform
+// light by E_v / pi.
+InfiniteLightDesc Parser::InfiniteLight(PendingLight &l) {
+    ParamSet &ps = l.params;
+    Param *L = ps.Find("L");
+    InfiniteLightDesc il;
+    float scale = (float)ps.GetFloat("scale", 1);
+    const float E_v = (float)ps.GetFloat("illuminance", -1);
+    if (ps.Find("portal")) throw Error(ps.loc + ": portal infinite lights are not supported yet");
+    std::string fn = ps.GetString("filename", "");
+    if (L && !fn.empty()) throw Error(ps.loc + ": Can't specify both emission \"L\" and \"filename\" with ImageInfiniteLight");
+    if (fn.empty()) {
+        std::array<float, 311> dense = GetSpectralData().denseD65;
+        float photometric = GetSpectralData().photometricD65;
+        if (L && L->type == "rgb" && L->nums.size() == 3)
+            dense = DenseRGBIlluminant((float)L->nums[0], (float)L->nums[1], (float)L->nums[2]);
+        else if (L && L->type == "spectrum" && !L->nums.empty()) {
+            dense = DensePiecewiseLinear(L->nums, ps.loc);
+            photometric = PhotometricOf(dense);
+        } else if (L && L->type == "blackbody" && L->nums.size() == 1) {
+            const float T = (float)L->nums[0];
+            for (int i = 0; i < 311; ++i) dense[i] = BlackbodyNormalized(395.f + i, T);
+            photometric = PhotometricOf(dense);
+        } else if (L)
+            throw Error(ps.loc + ": infinite light L must be rgb, spectrum or blackbody");
+        scene.denseSpectra.push_back(dense);
+        il.spectrum = (int)scene.denseSpectra.size() - 1;
+        scale /= photometric;
+        if (E_v > 0) scale *= E_v / kPi;
+        il.scale = scale;
+        ps.CheckUnused();
+        return il;
+    }
+    if (fn[0] != '/' && !l.dir.empty()) fn = l.dir + "/" + fn;
+    EnvLightDesc env = LoadEnvironmentImage(fn, ps.loc);
+    for (float v : env.rgb) {
+        if (std::isinf(v)) throw Error(ps.loc + ": " + fn + ": image has infinite pixel values and so is not suitable as a light.");
+        if (std::isnan(v)) throw Error(ps.loc + ": " + fn + ": image has not-a-number pixel values and so is not suitable as a light.");
+    }
+    // the sRGB colour space's illuminant (std illuminant D65)
+    scene.denseSpectra.push_back(GetSpectralData().denseD65);
+    il.spectrum = (int)scene.denseSpectra.size() - 1;
+    scale /= GetSpectralData().photometricD65;
+    // the upper-hemisphere illuminance normalisation (lights.cpp:1651-1679) needs the colour
+    // space's luminance vector; not restated yet
+    if (E_v > 0) throw Error(ps.loc + ": \"illuminance\" for image infinite lights is not supported yet");
+    il.scale = scale;
+    const Mat4 rfl = Mul(scene.camera.renderFromWorld, l.worldFromLight);
+    const Mat4 lfr = Inverse4(rfl);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            env.renderFromLight[3 * i + j] = (float)rfl[i][j];
+            env.lightFromRender[3 * i + j] = (float)lfr[i][j];
+        }
+    env.filename = fn;
+    il.image = (int)scene.envLights.size();
+    scene.envLights.push_back(std::move(env));
+    ps.CheckUnused();
+    return il;
 }
 
 // PointLight::Create / SpotLight::Create / DistantLight::Create (lights.cpp:192-276,

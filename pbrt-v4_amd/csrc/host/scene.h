@@ -179,10 +179,26 @@ struct AreaLightDesc {
 
 // An entry of BVHLightSampler's infinite-light list (lights without bounds, lightsamplers.cpp):
 // a UniformInfiniteLight, or a DistantLight (distant = its index in SceneDesc::deltaLights)
+// a UniformInfiniteLight, a DistantLight (distant = its index in SceneDesc::deltaLights) or an
+// ImageInfiniteLight (image = its index in SceneDesc::envLights; spectrum = the colour space's
+// illuminant, scale = the light's scale)
 struct InfiniteLightDesc {
     int spectrum = -1;
     float scale = 1;
     int distant = -1;
+    int image = -1;
+};
+
+// ImageInfiniteLight (lights.h:557-641, lights.cpp:1038-1071): an equal-area octahedral
+// environment image of linear sRGB values (Image::GetChannel of the selected R, G, B channels)
+// and the light's frame.  The device tables (per-pixel RGBIlluminantSpectrum coefficients and
+// the compensated PiecewiseConstant2D) are derived from it at upload.
+struct EnvLightDesc {
+    int res = 0;                      // square: res x res
+    std::vector<float> rgb;           // [res][res][3], row y = v * res
+    float renderFromLight[9] = {};    // upper 3x3 of renderFromLight (row major)
+    float lightFromRender[9] = {};    // upper 3x3 of its inverse (Transform::ApplyInverse)
+    std::string filename;
 };
 
 // PointLight / SpotLight / DistantLight (lights.h:200-300, 740-800; lights.cpp:192-276, 1376-1495)
@@ -254,6 +270,7 @@ struct SceneDesc {
                                                     // only when inside != outside
     std::vector<AreaLightDesc> areaLights;
     std::vector<InfiniteLightDesc> infiniteLights;
+    std::vector<EnvLightDesc> envLights;
     std::vector<DeltaLightDesc> deltaLights;  // point and spot lights first, then distant lights
     int nPointSpot = 0;
     // pbrt's light order (area lights, then LightSource lights as written) -> this scene's global
@@ -302,6 +319,10 @@ void FinalizeScene(SceneDesc &s);  // lights, light BVH, sampler tables
 void DebugBuildLightBVH(const float *in13, int n, std::vector<LightBVHNodeDesc> *nodes, std::vector<uint32_t> *trails);
 // the 24 four-way digit permutations of ZSobolSampler::GetSampleIndex, in pbrt's order
 // FilterSampler ctor (filters.cpp:133-147): tabulates the scene's filter and its
+// PiecewiseConstant1D ctor (util/sampling.h:625-649): func = |f|, normalised cdf; returns funcInt
+float BuildPC1D(const float *f, int n, float mn, float mx, float *func, float *cdf);
+// ImageInfiniteLight's compensated PiecewiseConstant2D (FilterTableView layout, domain [0,1]^2)
+std::vector<float> BuildEnvDistribution(const EnvLightDesc &e);
 // PiecewiseConstant2D (util/sampling.h:603-790) into SceneDesc::filterTable
 void BuildFilterTable(SceneDesc &s);
 extern const uint8_t kZSobolPermutations[24][4];

@@ -19,6 +19,7 @@
 #include <thread>
 
 #include "texture.h"
+#include "image.h"
 
 namespace pbrt_amd {
 
@@ -562,6 +563,40 @@ ImageDesc LoadImageTexture(const std::string &filename, const std::string &encod
     img.levelRes.push_back({w, h});
     StoreLevel(img, f, enc);
     return img;
+}
+
+EnvLightDesc LoadEnvironmentImage(const std::string &filename, const std::string &loc) {
+    EnvLightDesc env;
+    int w = 0, h = 0;
+    if (HasExt(filename, "exr")) {
+        Image im;
+        try {
+            im = ReadImage(filename);
+        } catch (const std::exception &e) {
+            throw Error(loc + ": " + e.what());
+        }
+        w = im.width;
+        h = im.height;
+        env.rgb = std::move(im.rgb);
+    } else {
+        const Encoding enc = Encoding::Get("sRGB", loc);
+        RawImage raw;
+        if (HasExt(filename, "png")) raw = ReadPNG(filename, enc);
+        else if (HasExt(filename, "pfm")) raw = ReadPFM(filename);
+        else throw Error(loc + ": " + filename + ": only PNG, PFM and EXR environment images are supported");
+        if (raw.nc < 3)
+            throw Error(loc + ": " + filename + ": image provided to \"infinite\" light must have R, G, and B channels.");
+        w = raw.w;
+        h = raw.h;
+        env.rgb.resize((size_t)3 * w * h);
+        for (size_t p = 0; p < (size_t)w * h; ++p)
+            for (int c = 0; c < 3; ++c) env.rgb[3 * p + c] = raw.Get(p * raw.nc + c, enc);
+    }
+    if (w != h)
+        throw Error(loc + ": " + filename + ": image resolution (" + std::to_string(w) + ", " + std::to_string(h) +
+                    ") is non-square. It's unlikely this is an equal area environment map.");
+    env.res = w;
+    return env;
 }
 
 // Decoded texel value (GetChannel, util/image.h:255-276) of a stored level

@@ -32,6 +32,9 @@ uint8_t LinearToSRGB8(float v);
 ImageDesc LoadImageTexture(const std::string &filename, const std::string &encoding, int wrap, const std::string &loc);
 // the decoded value of a stored texel (Image::GetChannel with the image's wrap mode)
 float ImageTexel(const ImageDesc &img, int level, int x, int y, int c);
+// Image::Read + GetChannelDesc({"R", "G", "B"}) for an ImageInfiniteLight (lights.cpp:1600-1681):
+// PNG (sRGB encoding), PFM or EXR; linear values as Image::GetChannel returns them; square
+EnvLightDesc LoadEnvironmentImage(const std::string &filename, const std::string &loc);
 // lowers texture node `node` (scene.textures) to a two-phase device program; returns its index
 int CompileTexProgram(SceneDesc &s, int node, bool spectrum);
 // CameraBase::FindMinimumDifferentials and CameraFromRender (SceneDesc::minPosDx ...)

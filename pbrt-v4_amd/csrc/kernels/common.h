@@ -946,7 +946,48 @@ struct LiSample {
     float scale, d2;     // d2 = 1: no division
     int spectrum;
     bool delta;          // IsDeltaLight: the BSDF's MIS pdf is 0
+    bool envLe;          // ImageInfiniteLight: Le = EnvLe(env, scale, spectrum(lambda), lambda)
+    EnvCoef env;
+    // the radiance at one wavelength from the dense value of `spectrum` there
+    __device__ float Le(float denseVal, float lambda) const {
+        return envLe ? EnvLe(env, scale, denseVal, lambda) : scale * denseVal;
+    }
 };
+// ImageInfiniteLight::SampleLi with allowIncompletePDF (lights.h:594-618): the compensated
+// distribution's (u, v), its direction in render space, pdf = mapPDF / (4 pi), a light point
+// 2 sceneRadius away and the nearest pixel's radiance
+__device__ inline bool SampleEnvLi(const DeviceScene &S, int j, V3 cp, float u0, float u1, LiSample *ls) {
+    const DeviceEnvLight &E = S.env[S.infImage[j]];
+    float uu, vv, mapPDF;
+    EnvSampleUV(E, u0, u1, &uu, &vv, &mapPDF);
+    if (mapPDF == 0) return false;
+    const V3 wi = MulM3(E.m, EqualAreaSquareToSphere(uu, vv));
+    ls->wi = wi;
+    ls->pdf = mapPDF / (4 * kPi);
+    ls->lp = cp + wi * (2 * S.sceneRadius);
+    ls->lpe = V3(0, 0, 0);
+    ls->ln = V3(0, 0, 0);
+    ls->scale = S.infScale[j];
+    ls->d2 = 1;
+    ls->spectrum = S.infSpectrum[j];
+    ls->delta = false;
+    ls->envLe = true;
+    ls->env = EnvCoefAt(E, uu, vv);
+    return true;
+}
+// ImageInfiniteLight::Le / PDF_Li(allowIncompletePDF) for an escaped ray direction d
+// (lights.h:587-591, lights.cpp:1073-1083): Le's (u, v) from the normalised light-space
+// direction, PDF_Li's from the unnormalised one
+__device__ inline EnvCoef EnvLeCoef(const DeviceEnvLight &E, V3 d) {
+    float u, v;
+    EqualAreaSphereToSquare(Normalize(MulM3(E.mi, d)), &u, &v);
+    return EnvCoefAt(E, u, v);
+}
+__device__ inline float EnvPDFLi(const DeviceEnvLight &E, V3 d) {
+    float u, v;
+    EqualAreaSphereToSquare(MulM3(E.mi, d), &u, &v);
+    return EnvPDF(E, u, v) / (4 * kPi);
+}
 __device__ inline float SmoothStepf(float x, float a, float b) {
     if (a == b) return (x < a) ? 0 : 1;
     const float t = Clampf((x - a) / (b - a), 0, 1);
@@ -973,6 +1014,7 @@ __device__ inline bool SampleLiSurface(const DeviceScene &S, const DeviceAreaLig
         ls->d2 = 1;
         ls->spectrum = Ld.spectrum;
         ls->delta = false;
+        ls->envLe = false;
         return true;
     }
     if constexpr (Lean) {
@@ -982,8 +1024,13 @@ __device__ inline bool SampleLiSurface(const DeviceScene &S, const DeviceAreaLig
         int di = k;
         if (k >= S.nPointSpot) {
             di = S.infDistant[k - S.nPointSpot];
-            if (di < 0) return false;  // UniformInfiniteLight::SampleLi(allowIncompletePDF) = {}
+            if (di < 0) {
+                if (S.nEnv > 0 && S.infImage[k - S.nPointSpot] >= 0)
+                    return SampleEnvLi(S, k - S.nPointSpot, cp, u0, u1, ls);
+                return false;  // UniformInfiniteLight::SampleLi(allowIncompletePDF) = {}
+            }
         }
+        ls->envLe = false;
         const DeviceDeltaLight &D = S.delta[di];
         const int type = __float_as_int(D.p.w);
         ls->pdf = 1;

@@ -152,6 +152,10 @@ struct DeviceScene {
     const int *infSpectrum;
     const float *infScale;
     const int *infDistant;
+    // ImageInfiniteLight entries: infImage[j] indexes env[] (-1: not an image light)
+    const int *infImage;
+    const DeviceEnvLight *env;
+    int nEnv;
     // point / spot / distant lights: the first nPointSpot are light-BVH members with global light
     // index nAreaLights + i; the infinite-list entry j has global index nAreaLights + nPointSpot + j
     int nDelta, nPointSpot;

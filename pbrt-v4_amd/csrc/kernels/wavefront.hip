@@ -149,7 +149,7 @@ __global__ void __launch_bounds__(kBlock) k_escaped(DeviceScene S, PathState st,
     int nLe = 0, leLight = -1;
     for (int li = 0; li < S.nInfinite; ++li)
         if (S.infDistant[li] < 0) ++nLe, leLight = li;
-    if (nLe == 1) {
+    if (nLe == 1 && S.nEnv == 0) {
         // One light with Le (the usual sky): its scaled spectrum and the sensor's three matching
         // curves are staged in LDS, so each wavelength is one LDS gather instead of four global
         // ones.  Same products in the same order as the general loop below, and rgb = 0 + x = x.
@@ -204,6 +204,20 @@ __global__ void __launch_bounds__(kBlock) k_escaped(DeviceScene S, PathState st,
             if (S.infDistant[li] >= 0) continue;  // a DistantLight is no Infinite-type light (no Le)
             const float *dense = S.dense + S.infSpectrum[li] * kDenseN;
             float scale = S.infScale[li];
+            // ImageInfiniteLight: Le at the ray direction's pixel; past a non-specular bounce the
+            // MIS denominator takes r_l * PMF * PDF_Li(allowIncompletePDF) (integrator.cpp:515-523)
+            const bool env = S.nEnv > 0 && S.infImage[li] >= 0;
+            EnvCoef ec{};
+            float lInvDenom = invDenom;
+            if (env) {
+                const DeviceEnvLight &E = S.env[S.infImage[li]];
+                const V3 d(rec.ray[3 * NR + ri], rec.ray[4 * NR + ri], rec.ray[5 * NR + ri]);
+                ec = EnvLeCoef(E, d);
+                if (!(depth == 0 || (fl & 1))) {
+                    const float pmf = LightPMF(S, V3(0, 0, 0), V3(0, 0, 0), S.nAreaLights + S.nPointSpot + li);
+                    lInvDenom = 1 / Avg31(1.f + rl * pmf * EnvPDFLi(E, d));
+                }
+            }
             float sx = 0, sy = 0, sz = 0, lam = rec.lambda0[ri];
             bool nz = false;
             for (int i = 0; i < kNSpectrumSamples; ++i) {
@@ -212,9 +226,10 @@ __global__ void __launch_bounds__(kBlock) k_escaped(DeviceScene S, PathState st,
                     if (lam > kLambdaMax) lam = kLambdaMin + (lam - kLambdaMax);
                 }
                 int off = DenseOffset(lam);
-                float Le = scale * (off < 0 ? 0.f : dense[off]);
+                const float dv = off < 0 ? 0.f : dense[off];
+                float Le = env ? EnvLe(ec, scale, dv, lam) : scale * dv;
                 nz |= Le != 0;
-                float v = ((depth > 0 ? rec.beta[(size_t)i * NR + ri] : 1.f) * Le * invDenom) * kInvWavelengthPDF;
+                float v = ((depth > 0 ? rec.beta[(size_t)i * NR + ri] : 1.f) * Le * lInvDenom) * kInvWavelengthPDF;
                 float xb = off < 0 ? 0.f : S.sensor[off], yb = off < 0 ? 0.f : S.sensor[kDenseN + off],
                       zb = off < 0 ? 0.f : S.sensor[2 * kDenseN + off];
                 sx = i == 0 ? xb * v : sx + xb * v;
@@ -316,12 +331,14 @@ __global__ void __launch_bounds__(kBlock) k_emissive(DeviceScene S, PathState st
 // DivD2: the light's radiance is divided by d2 per wavelength (point and spot lights; d2 = 1,
 // an exact no-op, for the other lanes).
 // RF: the diffuse reflectance R(lambda), clamped to [0, 1] (DiffuseMaterial::GetBxDF)
-template <bool DivD2, typename FD, typename RF>
+// Env: the light sample may be an ImageInfiniteLight's (envLe), whose radiance is the pixel's
+// RGBIlluminantSpectrum at the wavelength (EnvLe) rather than scale * dense
+template <bool DivD2, bool Env, typename FD, typename RF>
 __device__ inline void ShadeSpectralPass(int depth, const FD *dense, const SensorF4 *sensor4, float *bf, const RF &rf,
                                          float lambda0, float scale, float d2, float rd2, bool d2Ok,
                                          float absdotL, float invDenom, float absdotB, float pdf, float rpdf,
                                          bool pdfOk, float etaScale, SensorAcc *acc, bool *neeNz, bool *betaNz,
-                                         float *mx) {
+                                         float *mx, bool envLe = false, EnvCoef ec = EnvCoef{}) {
     const float avgRu = Avg31(1.f);
     bool nzL = false, nzB = false;
     float m = -kInfinity;
@@ -330,7 +347,11 @@ __device__ inline void ShadeSpectralPass(int depth, const FD *dense, const Senso
         const float R = rf(it.lam, it.i);
         const float bfi = (depth > 0 ? bf[it.i * kBlock] : 1.f) * (R * kInvPi);
         const int off = DenseOffset(it.lam);
-        float Le = scale * (off < 0 ? 0.f : float(dense[off]));
+        const float dv = off < 0 ? 0.f : float(dense[off]);
+        float Le = scale * dv;
+        if constexpr (Env) {
+            if (envLe) Le = EnvLe(ec, scale, dv, it.lam);
+        }
         if constexpr (DivD2) Le = DivByRcp(Le, d2, rd2, d2Ok);
         nzL |= Le != 0;
         acc->Add(sensor4, off, bfi * absdotL * Le * invDenom, it.i == 0);
@@ -580,7 +601,8 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                 V3 pi = surf.p, pe = surf.pErr;
                 SEC_MARK(st, 2);
                 // ---- light sample geometry (surfscatter.cpp:254-326)
-                bool nee = false;
+                bool nee = false, envLe = false;
+                EnvCoef envC{};
                 int spec = 0;
                 float scale = 0, absdotL = 0, invDenom = 0, d2 = 1;
                 if (Rnz) {
@@ -597,6 +619,10 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                         const V3 wi = ls.wi;
                         const V3 wiL = frame.ToLocal(wi);
                         if (woL.z != 0 && woL.z * wiL.z > 0) {  // DiffuseBxDF::f != 0
+                            if constexpr (!Lean) {
+                                envLe = ls.envLe;
+                                envC = ls.env;
+                            }
                             spec = ls.spectrum;
                             scale = ls.scale;
                             d2 = ls.d2;
@@ -647,18 +673,20 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                     float *bf = bfLds + threadIdx.x;
                     const float rd2 = 1 / d2;
                     const bool d2Ok = DivFastOk(d2);
-                    if (Lean || (lay.denseInLds && S.nPointSpot == 0))
-                        ShadeSpectralPass<false>(depth, (const LdsF *)denseLds + spec * kDenseN, sensorL, bf, rfun,
-                                                 lambda0, scale, d2, rd2, d2Ok, absdotL, invDenom, absdotB, pdf,
-                                                 rpdf, pdfOk, etaScale, &acc, &neeNz, &betaNz, &mx);
+                    if (Lean || (lay.denseInLds && S.nPointSpot == 0 && S.nEnv == 0))
+                        ShadeSpectralPass<false, false>(depth, (const LdsF *)denseLds + spec * kDenseN, sensorL, bf,
+                                                        rfun, lambda0, scale, d2, rd2, d2Ok, absdotL, invDenom,
+                                                        absdotB, pdf, rpdf, pdfOk, etaScale, &acc, &neeNz, &betaNz,
+                                                        &mx);
                     else if (lay.denseInLds)
-                        ShadeSpectralPass<true>(depth, (const LdsF *)denseLds + spec * kDenseN, sensorL, bf, rfun,
-                                                lambda0, scale, d2, rd2, d2Ok, absdotL, invDenom, absdotB, pdf,
-                                                rpdf, pdfOk, etaScale, &acc, &neeNz, &betaNz, &mx);
+                        ShadeSpectralPass<true, !Lean>(depth, (const LdsF *)denseLds + spec * kDenseN, sensorL, bf,
+                                                       rfun, lambda0, scale, d2, rd2, d2Ok, absdotL, invDenom,
+                                                       absdotB, pdf, rpdf, pdfOk, etaScale, &acc, &neeNz, &betaNz,
+                                                       &mx, envLe, envC);
                     else
-                        ShadeSpectralPass<true>(depth, S.dense + spec * kDenseN, sensorL, bf, rfun, lambda0,
-                                                scale, d2, rd2, d2Ok, absdotL, invDenom, absdotB, pdf, rpdf, pdfOk,
-                                                etaScale, &acc, &neeNz, &betaNz, &mx);
+                        ShadeSpectralPass<true, !Lean>(depth, S.dense + spec * kDenseN, sensorL, bf, rfun, lambda0,
+                                                       scale, d2, rd2, d2Ok, absdotL, invDenom, absdotB, pdf, rpdf,
+                                                       pdfOk, etaScale, &acc, &neeNz, &betaNz, &mx, envLe, envC);
                 }
                 SEC_MARK(st, 5);
                 if (nee && neeNz) {
@@ -886,8 +914,8 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
 #pragma unroll 2
                                 for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next()) {
                                     const int off = DenseOffset(it.lam);
-                                    float Le =
-                                        ls.scale * (off < 0 ? 0.f : (lay.denseInLds ? float(denseL[off]) : dense[off]));
+                                    float Le = ls.Le(off < 0 ? 0.f : (lay.denseInLds ? float(denseL[off]) : dense[off]),
+                                                     it.lam);
                                     if (S.nPointSpot > 0) Le = Le / ls.d2;  // pbrt: SampledSpectrum / DistanceSquared
                                     nz |= Le != 0;
                                     float f = fd;

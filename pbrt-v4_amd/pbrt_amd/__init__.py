@@ -87,6 +87,12 @@ class SceneFlat(ctypes.Structure):
         ("image_raw_data", ctypes.POINTER(ctypes.c_uint8)), ("material_tex", ctypes.POINTER(ctypes.c_int32)),
         ("camera_from_render", ctypes.c_float * 12), ("camera_min_diff", ctypes.c_float * 12),
         ("material_mix", ctypes.POINTER(ctypes.c_int32)),
+        ("n_env", ctypes.c_int),
+        ("inf_image", ctypes.POINTER(ctypes.c_int32)),
+        ("env_info", ctypes.POINTER(ctypes.c_int32)),
+        ("env_xform", ctypes.POINTER(ctypes.c_float)),
+        ("env_offset", ctypes.POINTER(ctypes.c_uint64)),
+        ("env_rgb", ctypes.POINTER(ctypes.c_float)),
     ]
 
 
@@ -119,6 +125,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_image_read_size", "pbrt_image_read", "pbrt_image_write", "pbrt_image_error", "pbrt_debug_filter_sample",
     "pbrt_debug_bvh_stats", "pbrt_debug_light_bvh", "pbrt_intersect_tr", "pbrt_image_flip", "pbrt_set_kernel_profiling", "pbrt_get_kernel_stats",
     "pbrt_debug_texture_eval",
+    "pbrt_debug_env_eval",
 ]
 
 _LIB = None
@@ -183,6 +190,7 @@ def _lib():
     lib.pbrt_debug_layered.argtypes = [c.c_void_p] * 8
     lib.pbrt_debug_triangle_shading.argtypes = [c.c_void_p] * 3 + [c.c_int] + [c.c_void_p] * 3
     lib.pbrt_debug_texture_eval.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
+    lib.pbrt_debug_env_eval.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_set_data_dir(str(DATA_DIR).encode())
     _LIB = lib
     return lib
@@ -334,6 +342,16 @@ class Scene:
         _check(_lib().pbrt_debug_texture_eval(self._h, material, slot, hit.ctypes.data, lam.ctypes.data, len(lam),
                                               out.ctypes.data))
         return out[:4].copy(), (out[4:4 + len(lam)].copy() if slot == 0 else float(out[4]))
+
+    def env_eval(self, env, dirs, u):
+        """The product's ImageInfiniteLight lookups for directions dirs[n][3] and sample pairs
+        u[n][2] (pbrt_debug_env_eval): [n][16] rows as include/pbrt_amd.h documents."""
+        d = np.ascontiguousarray(dirs, dtype=np.float32).reshape(-1, 3)
+        uu = np.ascontiguousarray(u, dtype=np.float32).reshape(-1, 2)
+        assert len(d) == len(uu)
+        out = np.zeros((len(d), 16), dtype=np.float32)
+        _check(_lib().pbrt_debug_env_eval(self._h, env, d.ctypes.data, uu.ctypes.data, len(d), out.ctypes.data))
+        return out
 
     def halton_fastpath_mismatches(self, dim, a0, a1, step=1):
         """Indices in [a0, a1) (stride step) whose 24-bit fast-path ScrambledRadicalInverse

@@ -1,0 +1,191 @@
+"""ImageInfiniteLight (lights.h:557-641, lights.cpp:1038-1083, 1558-1694): environment image
+readers, the equal-area mapping / compensated distribution / per-pixel spectra against the
+oracle's independent restatement (bit-exact, both on the host), a furnace known answer, and
+GPU film parity.
+
+Fixtures come from scenes/gen_env.py (its own EXR encoder for the NONE / RLE / ZIPS / ZIP
+codecs).  pbrt's own EXR path goes through the OpenEXR library, which is absent here: the
+decoded pixels are checked against the arrays the generator encoded."""
+import importlib.util
+
+import numpy as np
+import pytest
+
+from conftest import SCENES
+
+TEX = SCENES / "textures"
+
+
+def _gen():
+    spec = importlib.util.spec_from_file_location("gen_env", SCENES / "gen_env.py")
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+SCENE = """LookAt 0 0.5 -5  0 0 0  0 1 0
+Camera "perspective" "float fov" 40
+Film "rgb" "integer xresolution" 48 "integer yresolution" 32
+Sampler "halton" "integer pixelsamples" 8
+Integrator "volpath" "integer maxdepth" 5
+WorldBegin
+AttributeBegin
+Rotate -90 1 0 0
+LightSource "infinite" "string filename" "textures/{fn}" "float scale" 0.7
+AttributeEnd
+Material "diffuse" "rgb reflectance" [0.6 0.5 0.4]
+Shape "trianglemesh" "integer indices" [0 1 2 0 2 3] "point3 P" [-3 -1 -3 3 -1 -3 3 -1 3 -3 -1 3]
+Material "conductor" "float roughness" 0.15
+Shape "trianglemesh" "integer indices" [0 1 2 0 2 3] "point3 P" [-1 -1 1 1 -1 1 1 1 1 -1 1 1]
+Material "dielectric" "float roughness" 0.05
+Shape "trianglemesh" "integer indices" [0 1 2 0 2 3] "point3 P" [1.2 -1 0 2.2 -1 0 2.2 0.5 -0.5 1.2 0.5 -0.5]
+"""
+
+
+def _env_rgb(sc):
+    f = sc.flat()
+    n = f.env_info[0]
+    return np.ctypeslib.as_array(f.env_rgb, shape=(n * n * 3,)).reshape(n, n, 3).copy()
+
+
+@pytest.mark.parametrize("fn, half", [("env_sky_zip.exr", True), ("env_sky_rle.exr", True),
+                                      ("env_sky_zips.exr", False), ("env_sky_none.exr", False),
+                                      ("env_sky.pfm", False)])
+def test_environment_readers_decode_the_encoded_pixels(pa, fn, half):
+    want = _gen().sky(64)
+    if half:
+        want = want.astype(np.float16).astype(np.float32)
+    got = _env_rgb(pa.Scene.from_string(SCENE.format(fn=fn), SCENES))
+    assert np.array_equal(got, want)
+
+
+def test_png_environment_is_srgb_decoded(pa):
+    from PIL import Image
+    b = np.asarray(Image.open(TEX / "env_sky.png").convert("RGB")).astype(np.float64) / 255
+    lin = np.where(b <= 0.04045, b / 12.92, ((b + 0.055) / 1.055) ** 2.4)
+    got = _env_rgb(pa.Scene.from_string(SCENE.format(fn="env_sky.png"), SCENES))
+    assert np.abs(got - lin).max() < 1e-6
+
+
+@pytest.mark.parametrize("fn", ["env_sky.pfm", "env_sky_zip.exr", "env_sky.png", "env_const.pfm"])
+def test_env_lookups_match_oracle_bitwise(pa, oracle, fn):
+    """Le's (u, v), PDF_Li, the pixel spectra, the compensated distribution's samples and the
+    sampled directions: the product's shared host/device code vs the oracle, bit for bit."""
+    sc = pa.Scene.from_string(SCENE.format(fn=fn), SCENES)
+    rng = np.random.default_rng(7)
+    d = rng.normal(size=(4000, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    d[:8] = [[0, 0, 1], [0, 0, -1], [1, 0, 0], [0, 1, 0], [-1, 0, 0], [0, -1, 0], [1, 1, 0], [0, 1, 1]]
+    u = rng.random((4000, 2), dtype=np.float32)
+    u[:4] = [[0, 0], [0.99999994, 0.99999994], [0.5, 0.5], [0, 0.99999994]]
+    a = sc.env_eval(0, d, u)
+    b = oracle.env_eval(sc, 0, d, u)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert (a[:, 9] > 0).all()  # every pixel of these maps has mass (compensation leaves some)
+
+
+def test_compensated_distribution_follows_the_sun(pa):
+    """Sampling concentrates where the map is brightest above its mean (lights.cpp:1064-1070):
+    most samples land within the sun's cone."""
+    sc = pa.Scene.from_string(SCENE.format(fn="env_sky.pfm"), SCENES)
+    u = np.random.default_rng(3).random((20000, 2), dtype=np.float32)
+    out = sc.env_eval(0, np.tile([0, 0, 1.0], (20000, 1)), u)
+    # light space: the sun direction of gen_env.sky; render space = Rotate(-90, x) of it
+    s = np.array([0.3, 0.5, 0.81]) / np.linalg.norm([0.3, 0.5, 0.81])
+    s_render = np.array([s[0], s[2], -s[1]])
+    wi = out[:, 10:13] / np.linalg.norm(out[:, 10:13], axis=1, keepdims=True)
+    assert (wi @ s_render > 0.99).mean() > 0.5
+
+
+def test_constant_environment_furnace(pa, oracle):
+    """A constant 0.5 grey map over a white Lambertian quad seen head on, one bounce: every
+    pixel reflects 0.5 (a furnace known answer, as for the uniform light of the same radiance)."""
+    text = """LookAt 0 0 -5  0 0 0  0 1 0
+Camera "perspective" "float fov" 20
+Film "rgb" "integer xresolution" 16 "integer yresolution" 16
+Sampler "halton" "integer pixelsamples" 64
+Integrator "volpath" "integer maxdepth" 1
+WorldBegin
+LightSource "infinite" "string filename" "textures/env_const.pfm"
+Material "diffuse" "rgb reflectance" [1 1 1]
+Shape "trianglemesh" "integer indices" [0 1 2 0 2 3] "point3 P" [-1 -1 0 1 -1 0 1 1 0 -1 1 0]
+"""
+    for t in (text, text.replace('"string filename" "textures/env_const.pfm"', '"rgb L" [0.5 0.5 0.5]')):
+        sc = pa.Scene.from_string(t, SCENES)
+        f = sc.flat()
+        img = oracle.film_to_rgb(oracle.render(sc, threads=8), [f.output_rgb_from_sensor_rgb[i] for i in range(9)])
+        assert img[2:14, 2:14].mean() == pytest.approx(0.5, abs=0.01)
+
+
+def _write_pfm(path, img):
+    h, w = img.shape[:2]
+    path.write_bytes(b"PF\n%d %d\n-1\n" % (w, h) + np.ascontiguousarray(img[::-1]).astype("<f4").tobytes())
+
+
+def test_env_loader_errors(pa, tmp_path):
+    _write_pfm(tmp_path / "rect.pfm", np.ones((4, 8, 3), np.float32))
+    nan = np.ones((4, 4, 3), np.float32)
+    nan[1, 2, 0] = np.nan
+    _write_pfm(tmp_path / "nan.pfm", nan)
+    inf = np.ones((4, 4, 3), np.float32)
+    inf[0, 0, 1] = np.inf
+    _write_pfm(tmp_path / "inf.pfm", inf)
+    piz = bytearray((TEX / "env_sky_none.exr").read_bytes())
+    k = piz.index(b"compression\0compression\0") + len(b"compression\0compression\0") + 4
+    piz[k] = 4
+    (tmp_path / "piz.exr").write_bytes(bytes(piz))
+    (tmp_path / "grey.png").write_bytes((TEX / "bumps_grey16.png").read_bytes())
+    cases = [
+        ('"string filename" "rect.pfm"', "non-square"),
+        ('"string filename" "nan.pfm"', "not-a-number"),
+        ('"string filename" "inf.pfm"', "infinite pixel values"),
+        ('"string filename" "piz.exr"', "PIZ is not supported"),
+        ('"string filename" "grey.png"', "must have R, G, and B channels"),
+        ('"string filename" "missing.exr"', "unable to open|No such file|cannot open"),
+        ('"string filename" "rect.pfm" "rgb L" [1 1 1]', "Can't specify both"),
+        ('"string filename" "nan.pfm" "float illuminance" 3', "not-a-number|illuminance"),
+        ('"point3 portal" [0 0 0 1 0 0 1 1 0 0 1 0]', "portal"),
+    ]
+    for params, msg in cases:
+        text = SCENE.replace('"string filename" "textures/{fn}" "float scale" 0.7', params)
+        with pytest.raises(pa.PbrtError, match=msg):
+            pa.Scene.from_string(text, tmp_path)
+
+
+def test_uniform_infinite_light_illuminance(pa):
+    """UniformInfiniteLight "illuminance" E_v: scale *= E_v / pi (lights.cpp:1581-1597)"""
+    base = 'LightSource "infinite" "rgb L" [0.2 0.3 0.4]'
+    a = pa.Scene.from_string(SCENE.replace('LightSource "infinite" "string filename" "textures/{fn}" "float scale" 0.7',
+                                           base), SCENES).flat()
+    b = pa.Scene.from_string(SCENE.replace('LightSource "infinite" "string filename" "textures/{fn}" "float scale" 0.7',
+                                           base + ' "float illuminance" 2.5'), SCENES).flat()
+    assert b.inf_scale[0] == np.float32(np.float32(a.inf_scale[0]) * np.float32(np.float32(2.5) / np.float32(np.pi)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fn", ["env_sky.pfm", "env_sky_zip.exr"])
+def test_env_scene_matches_oracle_gpu(pa, oracle, fn):
+    from test_gpu_parity import check_parity, gpu_film, to_rgb
+    sc = pa.Scene.from_string(SCENE.format(fn=fn).replace('"integer pixelsamples" 8', '"integer pixelsamples" 16'),
+                              SCENES, xresolution=96, yresolution=64)
+    film, _ = gpu_film(pa, sc)
+    ref = oracle.render(sc, threads=16)
+    frac, mean_rel = check_parity(to_rgb(oracle, sc, film), to_rgb(oracle, sc, ref))
+    print(f"env light ({fn}) parity: {frac*100:.3f}% pixels within 1e-3, mean rel {mean_rel:.2e}")
+
+
+@pytest.mark.gpu
+def test_env_scene_zsobol_bvh_sampler_gpu(pa, oracle):
+    """The env light beside an area light: the BVH light sampler's infinite-light branch and the
+    escaped-ray MIS PMF (BVHLightSampler::PMF of an infinite light)."""
+    from test_gpu_parity import check_parity, gpu_film, to_rgb
+    text = SCENE.format(fn="env_sky.pfm").replace(
+        'Sampler "halton" "integer pixelsamples" 8', 'Sampler "zsobol" "integer pixelsamples" 16').replace(
+        "AttributeEnd\n", 'AttributeEnd\nAttributeBegin\nAreaLightSource "diffuse" "rgb L" [4 4 4]\n'
+        'Shape "trianglemesh" "integer indices" [0 1 2 0 2 3] "point3 P" [-0.5 2 -0.5 0.5 2 -0.5 0.5 2 0.5 -0.5 2 0.5]\n'
+        'AttributeEnd\n', 1)
+    sc = pa.Scene.from_string(text, SCENES, xresolution=96, yresolution=64)
+    film, _ = gpu_film(pa, sc)
+    ref = oracle.render(sc, threads=16)
+    frac, mean_rel = check_parity(to_rgb(oracle, sc, film), to_rgb(oracle, sc, ref))
+    print(f"env + area light parity: {frac*100:.3f}% pixels within 1e-3, mean rel {mean_rel:.2e}")

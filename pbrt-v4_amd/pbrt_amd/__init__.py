@@ -138,6 +138,13 @@ def _lib():
     if not LIB_PATH.exists():
         raise PbrtError(f"HIP library {LIB_PATH} is missing: build it with __graft_entry__.build() "
                         "(make -C pbrt-v4_amd); there is no CPU fallback")
+    # One HIP runtime per process: torch ships its own libamdhip64 with the same soname as
+    # /opt/rocm's.  Whichever loads first serves both, and torch cannot initialise on the
+    # system runtime ("No HIP GPUs are available"), so torch (when installed) goes first.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(str(LIB_PATH))
     c = ctypes
     lib.pbrt_last_error.restype = c.c_char_p

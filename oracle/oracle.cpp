@@ -2806,7 +2806,7 @@ struct OEnvLight {
         Float sd = 1 - (up + vp), dd = std::abs(sd), r = 1 - dd;
         Float phi = (r == 0 ? 1 : (vp - up) / r + 1) * Pi / 4;
         Float z = std::copysign(1 - Sqr(r), sd);
-        Float cp = std::copysign(std::cos(phi), u), sp = std::copysign(std::sin(phi), v);
+        Float cp = std::copysign(CRCos(phi), u), sp = std::copysign(CRSin(phi), v);
         return Vec(cp * r * SafeSqrt(2 - Sqr(r)), sp * r * SafeSqrt(2 - Sqr(r)), z);
     }
     static void SphereToSquare(Vec d, Float *uo, Float *vo) {
@@ -3380,7 +3380,11 @@ struct Renderer {
         // the wavefront loop processes this path's ray of path depth `depth`.  Interface
         // crossings continue in the next iteration at the same path depth; the loop ends at
         // wf == maxDepth after emission (so a path may stop before depth reaches maxDepth).
-        const bool haveMedia = f->n_media > 0;
+        // WavefrontPathIntegrator's haveMedia (wavefront/integrator.cpp:49-110): media, or any
+        // "interface" material (a null Material) -- shadow rays then pass interfaces
+        // (IntersectShadowTr) instead of stopping at them
+        bool haveMedia = f->n_media > 0;
+        for (int m = 0; m < f->n_materials && !haveMedia; ++m) haveMedia = f->material_type[m] == 3;
         int medium = haveMedia ? f->camera_medium : -1;
         int depth = 0;
         auto mediaOf = [&](int prim, int rayMedium, int *in, int *out) {
@@ -3472,7 +3476,24 @@ struct Renderer {
                     Float lpmf;
                     DeltaSample ds;
                     const bool sampledL = lights.Sample(pS, Vec(0, 0, 0), dUc, &li, &lpmf);
-                    if (sampledL && li >= f->n_area_lights && DeltaLi(li, pS, lambda, &ds)) {
+                    const OEnvLight *E = sampledL ? EnvOf(li) : nullptr;
+                    Float eu, ev, emap;
+                    if (E) {
+                        // ImageInfiniteLight::SampleLi from the medium point (media.cpp:280-305)
+                        if (E->Sample(dU0, dU1, &eu, &ev, &emap)) {
+                            const int k = li - f->n_area_lights - f->n_point_spot;
+                            Vec wi = OEnvLight::Mul(E->m, OEnvLight::SquareToSphere(eu, ev));
+                            Vec lp = pS + wi * (2 * f->scene_radius);
+                            Spectrum Le =
+                                E->Le(eu, ev, lambda, f->dense_spectra + 311 * f->inf_spectrum[k], f->inf_scale[k]);
+                            if (Le) {
+                                Float ph = HenyeyGreenstein(Dot(wo, wi), g);
+                                Float lightPDF = emap / (4 * Pi) * lpmf;
+                                Spectrum ru = r_u * ph, rl = r_u * lightPDF;
+                                shadow(pS, lp - pS, medium, beta * ph * Le, ru, rl);
+                            }
+                        }
+                    } else if (sampledL && li >= f->n_area_lights && DeltaLi(li, pS, lambda, &ds)) {
                         Float ph = HenyeyGreenstein(Dot(wo, ds.wi), g);
                         Spectrum ru = r_u * 0.f, rl = r_u * (1 * lpmf);
                         shadow(pS, ds.p - pS, medium, beta * ph * ds.L, ru, rl);

@@ -773,9 +773,6 @@ static void BuildDevice(pbrt_context *c) {
     if (S.dispersive && !s.media.empty())
         throw std::runtime_error("a dielectric with spectral eta (dispersion) together with participating media is not supported yet");
     c->volumetric = c->volumetric || S.dispersive;
-    if (c->volumetric && !s.envLights.empty())
-        throw Error("image infinite lights together with the volumetric path (media, interface, layered, thin "
-                    "dielectric, diffuse transmission or dispersive materials) are not supported yet");
     S.media.cameraMedium = s.cameraMedium;
     S.media.allGrey = 1;
     for (size_t m = 0; m < s.media.size(); ++m) {

@@ -1581,8 +1581,10 @@ PHD V3 EqualAreaSquareToSphere(float px, float py) {
     const float r = 1 - d;
     const float phi = (r == 0 ? 1 : (vp - up) / r + 1) * kPi / 4;
     const float z = std::copysign(1 - Sqr(r), signedDistance);
-    const float cosPhi = std::copysign(std::cos(phi), u);
-    const float sinPhi = std::copysign(std::sin(phi), v);
+    float sp, cp;
+    SinCosf(phi, &sp, &cp);
+    const float cosPhi = std::copysign(cp, u);
+    const float sinPhi = std::copysign(sp, v);
     return V3(cosPhi * r * SafeSqrt(2 - Sqr(r)), sinPhi * r * SafeSqrt(2 - Sqr(r)), z);
 }
 PHD void EqualAreaSphereToSquare(V3 d, float *uo, float *vo) {

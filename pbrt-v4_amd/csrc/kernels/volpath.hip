@@ -967,7 +967,7 @@ struct AreaLightSample {
     bool delta;
 };
 __device__ inline bool SampleAreaLight(const DeviceScene &S, V3 refP, V3 refN, V3 refNs, float uc, float u0, float u1,
-                                       const WaveOffsets &wo, AreaLightSample *out, float Le[kNS]) {
+                                       float lambda0, const WaveOffsets &wo, AreaLightSample *out, float Le[kNS]) {
     int li;
     float lpmf;
     if (!SampleLight(S, refP, refNs, uc, &li, &lpmf)) return false;
@@ -977,9 +977,10 @@ __device__ inline bool SampleAreaLight(const DeviceScene &S, V3 refP, V3 refN, V
         const float rd2 = 1 / ls.d2;
         const bool ok = DivFastOk(ls.d2);
         bool nz = false;
+        SpectralIter it(lambda0);
 #pragma unroll
-        for (int i = 0; i < kNS; ++i) {
-            Le[i] = DivByRcp(ls.scale * DenseAt(S, ls.spectrum, wo.off[i]), ls.d2, rd2, ok);
+        for (int i = 0; i < kNS; ++i, it.Next()) {
+            Le[i] = DivByRcp(ls.Le(DenseAt(S, ls.spectrum, wo.off[i]), it.lam), ls.d2, rd2, ok);
             nz |= Le[i] != 0;
         }
         if (!nz) return false;
@@ -989,7 +990,7 @@ __device__ inline bool SampleAreaLight(const DeviceScene &S, V3 refP, V3 refN, V
         out->n = ls.ln;
         out->wi = ls.wi;
         out->pdf = ls.pdf * lpmf;
-        out->delta = true;
+        out->delta = ls.delta;  // an ImageInfiniteLight sample is not a delta light
         return true;
     }
     const DeviceAreaLight Ld = S.lights[li];
@@ -1054,8 +1055,12 @@ struct AreaLightHit {
     int spectrum;
     float d2, rd2;
     bool d2Ok, delta;
-    __device__ float Le(const DeviceScene &S, int off) const {
-        const float v = scale * DenseAt(S, spectrum, off);
+    bool envLe;  // ImageInfiniteLight: the pixel's RGBIlluminantSpectrum (EnvLe)
+    EnvCoef env;
+    __device__ float Le(const DeviceScene &S, int off, float lam) const {
+        const float dv = DenseAt(S, spectrum, off);
+        if (envLe) return EnvLe(env, scale, dv, lam);
+        const float v = scale * dv;
         return delta ? DivByRcp(v, d2, rd2, d2Ok) : v;
     }
 };
@@ -1077,11 +1082,13 @@ __device__ inline bool SampleAreaLightAt(const DeviceScene &S, V3 refP, V3 refN,
         out->d2 = ls.d2;
         out->rd2 = 1 / ls.d2;
         out->d2Ok = DivFastOk(ls.d2);
-        out->delta = true;
+        out->delta = ls.delta;
+        out->envLe = ls.envLe;
+        out->env = ls.env;
         bool nz = false;
         SpectralIter it(lambda0);
 #pragma unroll 1
-        for (int i = 0; i < kNS; ++i, it.Next()) nz |= out->Le(S, DenseOffset(it.lam)) != 0;
+        for (int i = 0; i < kNS; ++i, it.Next()) nz |= out->Le(S, DenseOffset(it.lam), it.lam) != 0;
         return nz;
     }
     const DeviceAreaLight Ld = S.lights[li];
@@ -1110,6 +1117,7 @@ __device__ inline bool SampleAreaLightAt(const DeviceScene &S, V3 refP, V3 refN,
     out->d2 = out->rd2 = 1;
     out->d2Ok = true;
     out->delta = false;
+    out->envLe = false;
     return true;
 }
 
@@ -1321,7 +1329,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
 #pragma unroll 1
                         for (int i = 0; i < kNS; ++i, it.Next()) {
                             const int off = DenseOffset(it.lam);
-                            const float Ldv = betaIn(i) * fL[i * kBlock] * absdot * ls.Le(S, off);
+                            const float Ldv = betaIn(i) * fL[i * kBlock] * absdot * ls.Le(S, off, it.lam);
                             ld0 = i == 0 ? Ldv : ld0;
                             acc.Add(S, off, Ldv, i == 0);
                         }
@@ -1338,7 +1346,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
                         float ld0 = 0;
 #pragma unroll 2
                         for (int i = 0; i < kNS; ++i, it.Next()) {
-                            const float Le = ls.Le(S, DenseOffset(it.lam));
+                            const float Le = ls.Le(S, DenseOffset(it.lam), it.lam);
                             const float Ldv = betaIn(i) * fL[i * kBlock] * absdot * Le;
                             ld0 = i == 0 ? Ldv : ld0;
                             ldUni &= FloatToBits(Ldv) == FloatToBits(ld0);
@@ -1350,7 +1358,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
                         for (int i = 0; i < kNS; ++i, it.Next()) {
                             const float f = fAt(it.lam, fd, ct);
                             fnz |= f != 0;
-                            const float Le = ls.Le(S, DenseOffset(it.lam));
+                            const float Le = ls.Le(S, DenseOffset(it.lam), it.lam);
                             const float Ldv = betaIn(i) * f * absdot * Le;
                             fL[i * kBlock] = Ldv;
                             ldUni &= FloatToBits(Ldv) == FloatToBits(fL[0]);
@@ -1521,6 +1529,41 @@ __global__ void __launch_bounds__(kBlock) k_vescaped(DeviceScene S0, PathState s
             if (S.infDistant[k] >= 0) continue;  // a DistantLight is no Infinite-type light
             const int spec = S.infSpectrum[k];
             const float scale = S.infScale[k];
+            if (S.nEnv > 0 && S.infImage[k] >= 0) {
+                // ImageInfiniteLight: Le at the direction's pixel; past a non-specular bounce
+                // r_l * PMF * PDF_Li(allowIncompletePDF) joins the denominator
+                const DeviceEnvLight &E = S.env[S.infImage[k]];
+                const V3 rd = LoadV3(rec.ray + 3 * (size_t)NR, NR, ri);
+                const EnvCoef ec = EnvLeCoef(E, rd);
+                float eavg = avg;
+                if (!(depth == 0 || specularBounce)) {
+                    const float pmf = LightPMF(S, V3(0, 0, 0), V3(0, 0, 0), S.nAreaLights + S.nPointSpot + k);
+                    const float pdf = EnvPDFLi(E, rd);
+                    float es = 0;
+#pragma unroll 1
+                    for (int i = 0; i < kNS; ++i) {
+                        const float dv = ruIn(i) + rlIn(i) * pmf * pdf;
+                        es = i == 0 ? dv : es + dv;
+                    }
+                    eavg = es / kNS;
+                }
+                SensorAcc acc;
+                SpectralIter it(lambda0);
+                float c0 = 0;
+#pragma unroll 1
+                for (int i = 0; i < kNS; ++i, it.Next()) {
+                    const int off = DenseOffset(it.lam);
+                    const float ci = betaIn(i) * EnvLe(ec, scale, DenseAt(S, spec, off), it.lam) / eavg;
+                    c0 = i == 0 ? ci : c0;
+                    acc.Add(S, off, ci, i == 0);
+                }
+                const int NL = st.N;
+                st.L[slot] += S.imagingRatio * (acc.sx / kNS);
+                st.L[NL + slot] += S.imagingRatio * (acc.sy / kNS);
+                st.L[2 * NL + slot] += S.imagingRatio * (acc.sz / kNS);
+                AddL0Off(S, st, slot, DenseOffset(lambda0), c0);
+                continue;
+            }
             AddSpecToL(S, st, slot, lambda0,
                        [&](int i, int off) { return betaIn(i) * (scale * DenseAt(S, spec, off)) / avg; });
         }
@@ -1715,7 +1758,7 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
                     SpectralIter it(lambda0);
 #pragma unroll 1
                     for (int i = 0; i < kNS; ++i, it.Next()) {
-                        const float Le = ls.Le(S, DenseOffset(it.lam));
+                        const float Le = ls.Le(S, DenseOffset(it.lam), it.lam);
                         fo[i] = betaIn(i) * fo[i] * absdot * Le;
                         ldUni &= FloatToBits(fo[i]) == FloatToBits(fo[0]);
                     }
@@ -1842,7 +1885,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vscatter(DeviceScene
         {
             AreaLightSample ls;
             float Le[kNS];
-            if (SampleAreaLight(S, pS, V3(0, 0, 0), V3(0, 0, 0), rs.dUc, rs.dU0, rs.dU1, wo, &ls, Le)) {
+            if (SampleAreaLight(S, pS, V3(0, 0, 0), V3(0, 0, 0), rs.dUc, rs.dU0, rs.dU1, lambda0, wo, &ls, Le)) {
                 const V3 wi = ls.wi;
                 const float ph = HenyeyGreenstein(Dot(wo3, wi), g);
                 const float phasePDF = ls.delta ? 0.f : ph;  // IsDeltaLight (media.cpp:292-293)

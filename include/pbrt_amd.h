@@ -60,7 +60,7 @@ typedef struct pbrt_scene_flat {
     const uint8_t *tri_flip;      /* [n_triangles] reverseOrientation ^ swapsHandedness */
     const float *material_coeffs; /* [n_materials][4]: c0 c1 c2 constant */
     const int32_t *material_constant;
-    const int32_t *light_prim;    /* [n_area_lights] */
+    const int32_t *light_prim;    /* [n_area_lights]: triangle, or n_triangles + k for shape k */
     const float *light_scale;
     const int32_t *light_spectrum;
     const int32_t *light_two_sided;
@@ -186,6 +186,15 @@ typedef struct pbrt_scene_flat {
     const float *env_xform;
     const uint64_t *env_offset;
     const float *env_rgb;
+    /* Sphere / Disk (shapes.h:106-571), render space: primitive id n_triangles + k (light_prim
+     * of a shape emitter).  shape_info [n][8] kind (1 sphere, 2 disk), flags (bit0
+     * ReverseOrientation, bit1 transformSwapsHandedness), material, area light (-1), medium
+     * inside, outside, 0, 0; shape_params [n][32] objectFromRender 3x4, renderFromObject 3x4
+     * (row major), then sphere radius, zMin, zMax, phiMax, thetaZMin, thetaZMax or disk height,
+     * radius, innerRadius, phiMax (radians), 2 unused. */
+    int n_shapes;
+    const int32_t *shape_info;
+    const float *shape_params;
 } pbrt_scene_flat;
 
 typedef struct pbrt_render_params {
@@ -309,6 +318,12 @@ int pbrt_debug_texture_eval(const pbrt_scene *scene, int material, int slot, con
  * compensated distribution's sample (u, v), its mapPDF, wi = renderFromLight(
  * EqualAreaSquareToSphere(u, v)), 3 unused */
 int pbrt_debug_env_eval(const pbrt_scene *scene, int env, const float *dirs, const float *u, int n, float *out);
+/* Sphere / disk `shape` of the scene with the product's shared host/device code (shapes.h:
+ * 106-571): for n rays rays[n][6] (o, d) and sample pairs u[n][2], out[n][40] = hit flag, tHit,
+ * pObj xyz, then the render-space SurfaceInteraction p xyz, pError xyz, n xyz, shading n xyz,
+ * dpdu xyz, dpdv xyz, uv; then Shape::Sample(ctx = (o, no error, no normal), u): ok flag, p
+ * xyz, pError xyz, n xyz, pdf; then Shape::PDF(ctx, d); 2 unused */
+int pbrt_debug_shape_eval(const pbrt_scene *scene, int shape, const float *rays, const float *u, int n, float *out);
 /* Filter::Sample(u) of the scene's pixel filter (FilterSampler over PiecewiseConstant2D for
  * gaussian / mitchell / sinc, SampleTent for triangle, filters.h): out3 = p.x p.y weight */
 int pbrt_debug_filter_sample(const pbrt_scene *scene, float u0, float u1, float *out3);

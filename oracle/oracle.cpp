@@ -670,8 +670,10 @@ struct BVHNode {
     int left = -1, right = -1, first = 0, count = 0, axis = 0;
 };
 
+struct OShape;
 struct Scene {
     const pbrt_scene_flat *f;
+    std::vector<OShape> shapes;  // spheres and disks: prim ids n_triangles + k
     std::vector<Vec> v;
     std::vector<int> tri;  // 3 per triangle
     std::vector<BVHNode> nodes;
@@ -755,11 +757,13 @@ struct Scene {
         maxDepth = info->max_depth;
         frx = info->filter_radius_x;
         fry = info->filter_radius_y;
+        InitShapes();
         halton.Init(xres, yres, (uint32_t)info->seed, std::max(f->n_dims, 7 * maxDepth + 7));
         useZSobol = f->sampler_type == 1;
         zsobol.Init(info->spp, xres, yres, info->seed, f->zs_randomize);
     }
 
+    void InitShapes();
     static bool BoxHit(const BVHNode &n, Vec o, Vec invDir, const int neg[3], Float rayTMax) {
         // util/vecmath.h:1576-1611
         Float b[2][3] = {{n.mn.x, n.mn.y, n.mn.z}, {n.mx.x, n.mx.y, n.mx.z}};
@@ -782,6 +786,17 @@ struct Scene {
     }
 
     int Intersect(Vec o, Vec d, Float tMax, TriIsect *hit, bool anyHit) const {
+        int best = IntersectTris(o, d, tMax, hit, anyHit);
+        if (anyHit && best >= 0) return best;
+        return IntersectShapes(o, d, best >= 0 ? hit->t : tMax, hit, anyHit, best);
+    }
+    int IntersectShapes(Vec o, Vec d, Float tMax, TriIsect *hit, bool anyHit, int best) const;
+    // the per-primitive attributes of a triangle or a shape
+    int Material(int prim) const;
+    int Light(int prim) const;
+    bool Medium(int prim, int *in, int *out) const;
+    Interaction Interact(int prim, const TriIsect &ti, Vec rd) const;
+    int IntersectTris(Vec o, Vec d, Float tMax, TriIsect *hit, bool anyHit) const {
         if (nodes.empty()) return -1;
         Vec invDir(1 / d.x, 1 / d.y, 1 / d.z);
         int neg[3] = {invDir.x < 0, invDir.y < 0, invDir.z < 0};
@@ -997,6 +1012,352 @@ static Float TrianglePDF(Vec p0, Vec p1, Vec p2, bool flip, Vec ref, Vec refErr,
 }
 
 // ---------------------------------------------------------------- light sampler
+// ---------------------------------------------------------------- spheres and disks
+// Sphere / Disk (shapes.h:106-571, shapes.cpp:33-119) over the flat shape records, with pbrt's
+// Interval (util/math.h:819-1076) under the CPU rounding helpers NextFloatUp/Down(a op b)
+struct OInterval {
+    Float lo = 0, hi = 0;
+    OInterval() = default;
+    explicit OInterval(Float v) : lo(v), hi(v) {}
+    OInterval(Float a, Float b) : lo(std::min(a, b)), hi(std::max(a, b)) {}
+    static OInterval VE(Float v, Float err) {
+        OInterval i(v);
+        if (err != 0) {
+            i.lo = NextFloatDown(v - err);
+            i.hi = NextFloatUp(v + err);
+        }
+        return i;
+    }
+    Float Mid() const { return (lo + hi) / 2; }
+    Float Err() const { return (hi - lo) / 2; }
+    OInterval operator+(OInterval b) const { return {NextFloatDown(lo + b.lo), NextFloatUp(hi + b.hi)}; }
+    OInterval operator-(OInterval b) const { return {NextFloatDown(lo - b.hi), NextFloatUp(hi - b.lo)}; }
+    OInterval operator*(OInterval b) const {
+        return {std::min({NextFloatDown(lo * b.lo), NextFloatDown(hi * b.lo), NextFloatDown(lo * b.hi), NextFloatDown(hi * b.hi)}),
+                std::max({NextFloatUp(lo * b.lo), NextFloatUp(hi * b.lo), NextFloatUp(lo * b.hi), NextFloatUp(hi * b.hi)})};
+    }
+    OInterval operator/(OInterval b) const {
+        if (0 >= b.lo && 0 <= b.hi) return {-Infinity, Infinity};
+        return {std::min({NextFloatDown(lo / b.lo), NextFloatDown(hi / b.lo), NextFloatDown(lo / b.hi), NextFloatDown(hi / b.hi)}),
+                std::max({NextFloatUp(lo / b.lo), NextFloatUp(hi / b.lo), NextFloatUp(lo / b.hi), NextFloatUp(hi / b.hi)})};
+    }
+    bool operator==(OInterval b) const { return lo == b.lo && hi == b.hi; }
+};
+static OInterval operator*(Float f, OInterval i) {
+    return f > 0 ? OInterval(NextFloatDown(f * i.lo), NextFloatUp(f * i.hi)) : OInterval(NextFloatDown(f * i.hi), NextFloatUp(f * i.lo));
+}
+static OInterval ISqr(OInterval i) {
+    Float a = std::abs(i.lo), b = std::abs(i.hi);
+    if (a > b) std::swap(a, b);
+    if (0 >= i.lo && 0 <= i.hi) return {0, NextFloatUp(b * b)};
+    return {NextFloatDown(a * a), NextFloatUp(b * b)};
+}
+static OInterval ISqrt(OInterval i) { return {std::max<Float>(0, NextFloatDown(std::sqrt(i.lo))), NextFloatUp(std::sqrt(i.hi))}; }
+
+struct OShape {
+    int kind = 0, flags = 0;
+    const float *r2o = nullptr, *o2r = nullptr;  // 3x4 row major
+    Float a = 0, b = 0, c = 0, d = 0, e = 0, g = 0;
+    void Init(const pbrt_scene_flat *f, int k) {
+        const int32_t *info = f->shape_info + 8 * k;
+        const float *pp = f->shape_params + 32 * k;
+        kind = info[0];
+        flags = info[1];
+        r2o = pp;
+        o2r = pp + 12;
+        a = pp[24], b = pp[25], c = pp[26], d = pp[27], e = pp[28], g = pp[29];
+    }
+    bool sphere() const { return kind == 1; }
+    Float Area() const { return sphere() ? d * a * (c - b) : d * Float(0.5) * (Sqr(b) - Sqr(c)); }
+    // Transform::operator() on points / vectors / normals (util/transform.h:133-176, 272-334)
+    static void XPointI(const float *m, const OInterval in[3], OInterval out[3]) {
+        const Float x = in[0].Mid(), y = in[1].Mid(), z = in[2].Mid();
+        const Float ex = in[0].Err(), ey = in[1].Err(), ez = in[2].Err();
+        const bool exact = ex == 0 && ey == 0 && ez == 0;
+        for (int i = 0; i < 3; ++i) {
+            const float *r = m + 4 * i;
+            const Float v = (r[0] * x + r[1] * y) + (r[2] * z + r[3]);
+            Float err = gamma(3) * (std::abs(r[0] * x) + std::abs(r[1] * y) + std::abs(r[2] * z) + std::abs(r[3]));
+            if (!exact) err = (gamma(3) + 1) * (std::abs(r[0]) * ex + std::abs(r[1]) * ey + std::abs(r[2]) * ez) + err;
+            out[i] = OInterval::VE(v, err);
+        }
+    }
+    static void XVectorExact(const float *m, Vec v, OInterval out[3]) {
+        for (int i = 0; i < 3; ++i) {
+            const float *r = m + 4 * i;
+            const Float err = gamma(3) * (std::abs(r[0] * v.x) + std::abs(r[1] * v.y) + std::abs(r[2] * v.z));
+            out[i] = OInterval::VE(r[0] * v.x + r[1] * v.y + r[2] * v.z, err);
+        }
+    }
+    static Vec XV(const float *m, Vec v) {
+        return Vec(m[0] * v.x + m[1] * v.y + m[2] * v.z, m[4] * v.x + m[5] * v.y + m[6] * v.z, m[8] * v.x + m[9] * v.y + m[10] * v.z);
+    }
+    static Vec XN(const float *mInv, Vec n) {
+        return Vec(mInv[0] * n.x + mInv[4] * n.y + mInv[8] * n.z, mInv[1] * n.x + mInv[5] * n.y + mInv[9] * n.z,
+                   mInv[2] * n.x + mInv[6] * n.y + mInv[10] * n.z);
+    }
+    static Vec XP(const float *m, Vec p) {
+        return Vec(m[0] * p.x + m[1] * p.y + m[2] * p.z + m[3], m[4] * p.x + m[5] * p.y + m[6] * p.z + m[7],
+                   m[8] * p.x + m[9] * p.y + m[10] * p.z + m[11]);
+    }
+    static Float Phi(Vec p) {
+        Float phi = CRATan2(p.y, p.x);
+        if (phi < 0) phi += 2 * Pi;
+        return phi;
+    }
+    // BasicIntersect -> tHit and the object-space hit
+    bool Intersect(Vec ro, Vec rd, Float tMax, Float *tHit, Vec *pObj) const {
+        OInterval oi[3], di[3];
+        const OInterval ro3[3] = {OInterval(ro.x), OInterval(ro.y), OInterval(ro.z)};
+        XPointI(r2o, ro3, oi);
+        XVectorExact(r2o, rd, di);
+        const Vec o(oi[0].Mid(), oi[1].Mid(), oi[2].Mid()), dd(di[0].Mid(), di[1].Mid(), di[2].Mid());
+        if (!sphere()) {
+            if (dd.z == 0) return false;
+            const Float th = (a - o.z) / dd.z;
+            if (th <= 0 || th >= tMax) return false;
+            const Vec p = o + th * dd;
+            const Float dist2 = Sqr(p.x) + Sqr(p.y);
+            if (dist2 > Sqr(b) || dist2 < Sqr(c)) return false;
+            if (Phi(p) > d) return false;
+            *tHit = th;
+            *pObj = p;
+            return true;
+        }
+        const Float radius = a, zMin = b, zMax = c, phiMax = d;
+        const OInterval A = ISqr(di[0]) + ISqr(di[1]) + ISqr(di[2]);
+        const OInterval B = 2.f * (di[0] * oi[0] + di[1] * oi[1] + di[2] * oi[2]);
+        const OInterval C = ISqr(oi[0]) + ISqr(oi[1]) + ISqr(oi[2]) - ISqr(OInterval(radius));
+        const OInterval fct = B / (2.f * A);
+        OInterval v[3];
+        for (int i = 0; i < 3; ++i) v[i] = oi[i] - fct * di[i];
+        const OInterval len = ISqrt(ISqr(v[0]) + ISqr(v[1]) + ISqr(v[2]));
+        const OInterval disc = 4.f * A * (OInterval(radius) + len) * (OInterval(radius) - len);
+        if (disc.lo < 0) return false;
+        const OInterval root = ISqrt(disc);
+        const OInterval q = B.Mid() < 0 ? -.5f * (B - root) : -.5f * (B + root);
+        OInterval t0 = q / A, t1 = C / q;
+        if (t0.lo > t1.lo) std::swap(t0, t1);
+        if (t0.hi > tMax || t1.lo <= 0) return false;
+        OInterval ts = t0;
+        if (ts.lo <= 0) {
+            ts = t1;
+            if (ts.hi > tMax) return false;
+        }
+        auto hitAt = [&](OInterval t, Vec *p, Float *phi) {
+            *p = o + t.Mid() * dd;
+            *p = *p * (radius / Length(*p));
+            if (p->x == 0 && p->y == 0) p->x = 1e-5f * radius;
+            *phi = Phi(*p);
+        };
+        Vec p;
+        Float phi;
+        hitAt(ts, &p, &phi);
+        auto clipped = [&]() { return (zMin > -radius && p.z < zMin) || (zMax < radius && p.z > zMax) || phi > phiMax; };
+        if (clipped()) {
+            if (ts == t1) return false;
+            if (t1.hi > tMax) return false;
+            ts = t1;
+            hitAt(ts, &p, &phi);
+            if (clipped()) return false;
+        }
+        *tHit = ts.Mid();
+        *pObj = p;
+        return true;
+    }
+    // InteractionFromIntersection + Transform::operator()(SurfaceInteraction)
+    Interaction Surface(Vec pHit, Vec rd) const {
+        const Float phi = Phi(pHit);
+        Vec dpdu, dpdv, pErr;
+        Float u, v;
+        if (sphere()) {
+            const Float radius = a, phiMax = d, tzMin = e, tzMax = g;
+            u = phi / phiMax;
+            const Float cosTheta = pHit.z / radius, theta = SafeACos(cosTheta);
+            v = (theta - tzMin) / (tzMax - tzMin);
+            const Float zr = std::sqrt(Sqr(pHit.x) + Sqr(pHit.y));
+            const Float cp = pHit.x / zr, sp = pHit.y / zr;
+            dpdu = Vec(-phiMax * pHit.y, phiMax * pHit.x, 0);
+            const Float sinTheta = SafeSqrt(1 - Sqr(cosTheta));
+            dpdv = (tzMax - tzMin) * Vec(pHit.z * cp, pHit.z * sp, -radius * sinTheta);
+            pErr = gamma(5) * Abs(pHit);
+        } else {
+            const Float radius = b, inner = c, phiMax = d;
+            u = phi / phiMax;
+            const Float rHit = std::sqrt(Sqr(pHit.x) + Sqr(pHit.y));
+            v = (radius - rHit) / (radius - inner);
+            dpdu = Vec(-phiMax * pHit.y, phiMax * pHit.x, 0);
+            dpdv = Vec(pHit.x, pHit.y, 0) * (inner - radius) / rHit;
+            pHit.z = a;
+            pErr = Vec(0, 0, 0);
+        }
+        Vec n = Normalize(Cross(dpdu, dpdv));
+        if (((flags & 1) != 0) != ((flags & 2) != 0)) n = -n;
+        const OInterval pi[3] = {OInterval::VE(pHit.x, pErr.x), OInterval::VE(pHit.y, pErr.y), OInterval::VE(pHit.z, pErr.z)};
+        OInterval po[3];
+        XPointI(o2r, pi, po);
+        Interaction si;
+        si.p = Vec(po[0].Mid(), po[1].Mid(), po[2].Mid());
+        si.err = Vec(po[0].Err(), po[1].Err(), po[2].Err());
+        si.n = Normalize(XN(r2o, n));
+        si.dpdu = si.dpdus = XV(o2r, dpdu);
+        si.dpdv = XV(o2r, dpdv);
+        Vec ns = Normalize(XN(r2o, n));
+        if (DotN(ns, si.n) < 0) ns = -ns;  // FaceForward(shading.n, n)
+        si.ns = ns;
+        si.uv[0] = u;
+        si.uv[1] = v;
+        si.wo = Normalize(-rd);
+        return si;
+    }
+    // Sphere::Sample(u) / Disk::Sample(u): area measure
+    ShapeSample SampleArea(Float u0, Float u1) const {
+        ShapeSample ss;
+        if (sphere()) {
+            const Float z = 1 - 2 * u0, r = SafeSqrt(1 - Sqr(z)), ph = 2 * Pi * u1;
+            Vec pObj = Vec(0, 0, 0) + a * Vec(r * CRCos(ph), r * CRSin(ph), z);
+            pObj = pObj * (a / Length(pObj));
+            const Vec pErr = gamma(5) * Abs(pObj);
+            Vec n = Normalize(XN(r2o, pObj));
+            if (flags & 1) n = -n;
+            const OInterval pi[3] = {OInterval::VE(pObj.x, pErr.x), OInterval::VE(pObj.y, pErr.y), OInterval::VE(pObj.z, pErr.z)};
+            OInterval po[3];
+            XPointI(o2r, pi, po);
+            ss.p = Vec(po[0].Mid(), po[1].Mid(), po[2].Mid());
+            ss.err = Vec(po[0].Err(), po[1].Err(), po[2].Err());
+            ss.n = n;
+        } else {
+            Float dx, dy;
+            SampleUniformDiskConcentric(u0, u1, &dx, &dy);
+            const OInterval pi[3] = {OInterval(dx * b), OInterval(dy * b), OInterval(a)};
+            OInterval po[3];
+            XPointI(o2r, pi, po);
+            ss.p = Vec(po[0].Mid(), po[1].Mid(), po[2].Mid());
+            ss.err = Vec(po[0].Err(), po[1].Err(), po[2].Err());
+            Vec n = Normalize(XN(r2o, Vec(0, 0, 1)));
+            if (flags & 1) n = -n;
+            ss.n = n;
+        }
+        ss.pdf = 1 / Area();
+        return ss;
+    }
+    // Shape::Sample(ctx, u), solid angle (false: {})
+    bool Sample(Vec cp, Vec cpErr, Vec cn, Float u0, Float u1, ShapeSample *out) const {
+        if (sphere()) {
+            const Vec pc = XP(o2r, Vec(0, 0, 0));
+            const Vec po = OffsetRayOrigin(cp, cpErr, cn, pc - cp);
+            if (DistanceSquared(po, pc) > Sqr(a)) {
+                const Float sinMax = a / Length(cp - pc), sin2Max = Sqr(sinMax), cosMax = SafeSqrt(1 - sin2Max);
+                Float omc = 1 - cosMax, cosT = (cosMax - 1) * u0 + 1, sin2T = 1 - Sqr(cosT);
+                if (sin2Max < 0.00068523f) {
+                    sin2T = sin2Max * u0;
+                    cosT = std::sqrt(1 - sin2T);
+                    omc = sin2Max / 2;
+                }
+                const Float cosA = sin2T / sinMax + cosT * SafeSqrt(1 - sin2T / Sqr(sinMax)), sinA = SafeSqrt(1 - Sqr(cosA));
+                const Float ph = u1 * 2 * Pi;
+                const Float st = Clamp(sinA, -1, 1);
+                const Vec w(st * CRCos(ph), st * CRSin(ph), Clamp(cosA, -1, 1));
+                const Vec fz = Normalize(pc - cp);
+                Vec fx, fy;
+                CoordinateSystem(fz, &fx, &fy);
+                Vec n = fx * (-w.x) + fy * (-w.y) + fz * (-w.z);
+                const Vec p = pc + a * n;
+                if (flags & 1) n = -n;
+                Point3fi(p, gamma(5) * Abs(p), &out->p, &out->err);
+                out->n = n;
+                out->pdf = 1 / (2 * Pi * omc);
+                return true;
+            }
+        }
+        ShapeSample ss = SampleArea(u0, u1);
+        Vec wi = ss.p - cp;
+        if (LengthSquared(wi) == 0) return false;
+        wi = Normalize(wi);
+        ss.pdf /= AbsDotN(ss.n, -wi) / DistanceSquared(cp, ss.p);
+        if (std::isinf(ss.pdf)) return false;
+        *out = ss;
+        return true;
+    }
+    // Shape::PDF(ctx, wi)
+    Float PDF(Vec cp, Vec cpErr, Vec cn, Vec wi) const {
+        if (sphere()) {
+            const Vec pc = XP(o2r, Vec(0, 0, 0));
+            const Vec po = OffsetRayOrigin(cp, cpErr, cn, pc - cp);
+            if (DistanceSquared(po, pc) > Sqr(a)) {
+                const Float sin2Max = a * a / DistanceSquared(cp, pc), cosMax = SafeSqrt(1 - sin2Max);
+                Float omc = 1 - cosMax;
+                if (sin2Max < 0.00068523f) omc = sin2Max / 2;
+                return 1 / (2 * Pi * omc);
+            }
+        }
+        const Vec ro = OffsetRayOrigin(cp, cpErr, cn, wi);
+        Float th;
+        Vec pObj;
+        if (!Intersect(ro, wi, Infinity, &th, &pObj)) return 0;
+        const Interaction si = Surface(pObj, wi);
+        Float pdf = (1 / Area()) / (AbsDotN(si.n, -wi) / DistanceSquared(cp, si.p));
+        if (std::isinf(pdf)) pdf = 0;
+        return pdf;
+    }
+    void Bounds(Vec *mn, Vec *mx) const {
+        const Vec lo = sphere() ? Vec(-a, -a, b) : Vec(-b, -b, a), hi = sphere() ? Vec(a, a, c) : Vec(b, b, a);
+        *mn = Vec(Infinity, Infinity, Infinity);
+        *mx = -*mn;
+        for (int i = 0; i < 8; ++i) {
+            const Vec q = XP(o2r, Vec((i & 1) ? hi.x : lo.x, (i & 2) ? hi.y : lo.y, (i & 4) ? hi.z : lo.z));
+            for (int k = 0; k < 3; ++k) {
+                (*mn)[k] = std::min((*mn)[k], q[k]);
+                (*mx)[k] = std::max((*mx)[k], q[k]);
+            }
+        }
+    }
+};
+
+void Scene::InitShapes() {
+    shapes.assign(f->n_shapes, OShape());
+    for (int k = 0; k < f->n_shapes; ++k) shapes[k].Init(f, k);
+}
+int Scene::IntersectShapes(Vec o, Vec d, Float tMax, TriIsect *hit, bool anyHit, int best) const {
+    for (size_t k = 0; k < shapes.size(); ++k) {
+        Float th;
+        Vec pObj;
+        if (shapes[k].Intersect(o, d, tMax, &th, &pObj)) {
+            tMax = th;
+            *hit = TriIsect{pObj.x, pObj.y, pObj.z, th};
+            best = f->n_triangles + (int)k;
+            if (anyHit) return best;
+        }
+    }
+    return best;
+}
+int Scene::Material(int prim) const {
+    return prim < f->n_triangles ? f->tri_material[prim] : f->shape_info[8 * (prim - f->n_triangles) + 2];
+}
+int Scene::Light(int prim) const {
+    return prim < f->n_triangles ? f->tri_light[prim] : f->shape_info[8 * (prim - f->n_triangles) + 3];
+}
+bool Scene::Medium(int prim, int *in, int *out) const {
+    if (prim >= f->n_triangles) {
+        const int32_t *info = f->shape_info + 8 * (prim - f->n_triangles);
+        *in = info[4];
+        *out = info[5];
+        return true;
+    }
+    if (!f->tri_medium) return false;
+    *in = f->tri_medium[2 * prim];
+    *out = f->tri_medium[2 * prim + 1];
+    return true;
+}
+Interaction Scene::Interact(int prim, const TriIsect &ti, Vec rd) const {
+    if (prim >= f->n_triangles) {
+        Interaction si = shapes[prim - f->n_triangles].Surface(Vec(ti.b0, ti.b1, ti.b2), rd);
+        si.prim = prim;
+        return si;
+    }
+    return TriangleInteraction(P(prim, 0), P(prim, 1), P(prim, 2), f->tri_flip[prim], ti, rd, Attr(prim));
+}
+
 struct LightNode {
     Vec mn, mx, w;
     Float phi, cosO, cosE;
@@ -1247,6 +1608,23 @@ static std::vector<std::pair<int, LB>> SceneLightBounds(const pbrt_scene_flat *f
     };
     for (int i = 0; i < f->n_area_lights; ++i) {
         const int t = f->light_prim[i];
+        if (t >= f->n_triangles) {
+            // a sphere or disk emitter: Shape::Bounds and NormalBounds (shapes.h:134, shapes.cpp:94-99)
+            OShape sh;
+            sh.Init(f, t - f->n_triangles);
+            Vec mn, mx;
+            sh.Bounds(&mn, &mx);
+            Float phi = denseMax(f->light_spectrum[i]);
+            phi *= f->light_scale[i] * sh.Area() * Pi;
+            Cone nb(Vec(0, 0, 1), -1);  // DirectionCone::EntireSphere
+            if (!sh.sphere()) {
+                Vec n = OShape::XN(sh.r2o, Vec(0, 0, 1));
+                if (sh.flags & 1) n = -n;
+                nb = Cone(n, 1);
+            }
+            L.push_back({i, LB(Box(mn, mx), nb.w, phi, nb.cosT, std::cos(Pi / 2), f->light_two_sided[i] != 0)});
+            continue;
+        }
         const int32_t *v = f->triangles + 3 * t;
         auto P = [&](int k) { return Vec(f->vertices[3 * v[k]], f->vertices[3 * v[k] + 1], f->vertices[3 * v[k] + 2]); };
         const Vec p0 = P(0), p1 = P(1), p2 = P(2);
@@ -3230,13 +3608,12 @@ struct Renderer {
         while (d != Vec(0, 0, 0)) {
             TriIsect ti;
             int hp = S.Intersect(o, d, tMax, &ti, false);
-            if (hp >= 0 && f->material_type[f->tri_material[hp]] != 3) {
+            if (hp >= 0 && f->material_type[S.Material(hp)] != 3) {
                 T_ray = Spectrum(0.f);
                 break;
             }
             Interaction hsi;
-            if (hp >= 0)
-                hsi = TriangleInteraction(S.P(hp, 0), S.P(hp, 1), S.P(hp, 2), f->tri_flip[hp], ti, d, S.Attr(hp));
+            if (hp >= 0) hsi = S.Interact(hp, ti, d);
             if (med >= 0) {
                 Float tEnd = hp < 0 ? tMax : (Length(o - hsi.p) / Length(d));
                 Spectrum T_maj = SampleTmaj(M, med, o, d, tEnd, rng.Uniform(), rng, lambda,
@@ -3260,10 +3637,10 @@ struct Renderer {
             }
             if (hp < 0 || !T_ray) break;
             // SurfaceInteraction::SpawnRayTo(pLight) (interaction.h, ray.h:98-104)
-            int mi = med, mo = med;
-            if (f->n_media > 0 && f->tri_medium && f->tri_medium[2 * hp] != f->tri_medium[2 * hp + 1]) {
-                mi = f->tri_medium[2 * hp];
-                mo = f->tri_medium[2 * hp + 1];
+            int mi = med, mo = med, pin, pout;
+            if (f->n_media > 0 && S.Medium(hp, &pin, &pout) && pin != pout) {
+                mi = pin;
+                mo = pout;
             }
             Vec dd = pLight - hsi.p;
             o = OffsetRayOrigin(hsi.p, hsi.err, hsi.n, dd);
@@ -3389,12 +3766,24 @@ struct Renderer {
         int depth = 0;
         auto mediaOf = [&](int prim, int rayMedium, int *in, int *out) {
             *in = *out = rayMedium;
-            if (haveMedia && f->tri_medium && f->tri_medium[2 * prim] != f->tri_medium[2 * prim + 1]) {
-                *in = f->tri_medium[2 * prim];
-                *out = f->tri_medium[2 * prim + 1];
+            int pin, pout;
+            if (haveMedia && f->n_media > 0 && S.Medium(prim, &pin, &pout) && pin != pout) {
+                *in = pin;
+                *out = pout;
             }
         };
-        auto isInterface = [&](int prim) { return f->material_type[f->tri_material[prim]] == 3; };
+        auto isInterface = [&](int prim) { return f->material_type[S.Material(prim)] == 3; };
+        // Shape::Sample(ctx, u) / PDF(ctx, wi) of area light li (a triangle, sphere or disk)
+        auto sampleArea = [&](int li, Vec ref, Vec refErr, Vec refN, Vec refNs, Float u0, Float u1, ShapeSample *ss) {
+            const int lp = f->light_prim[li];
+            if (lp >= f->n_triangles) return S.shapes[lp - f->n_triangles].Sample(ref, refErr, refN, u0, u1, ss);
+            return TriangleSample(S.P(lp, 0), S.P(lp, 1), S.P(lp, 2), f->tri_flip[lp], ref, refNs, u0, u1, ss, S.Attr(lp));
+        };
+        auto pdfArea = [&](int li, Vec ref, Vec refErr, Vec refN, Vec refNs, Vec wi) {
+            const int lp = f->light_prim[li];
+            if (lp >= f->n_triangles) return S.shapes[lp - f->n_triangles].PDF(ref, refErr, refN, wi);
+            return TrianglePDF(S.P(lp, 0), S.P(lp, 1), S.P(lp, 2), f->tri_flip[lp], ref, refErr, refN, refNs, wi, S.Attr(lp));
+        };
         // shadow rays: plain occlusion, or TraceTransmittance (wavefront/intersect.h:164-274)
         // whenever the scene has media (interface surfaces are then transparent to them)
         auto shadow = [&](Vec o, Vec d, int med, const Spectrum &Ld, const Spectrum &ru, const Spectrum &rl) {
@@ -3411,8 +3800,7 @@ struct Renderer {
             TriIsect ti;
             int prim = S.Intersect(ro, rd, Infinity, &ti, false);
             Interaction si;
-            if (prim >= 0)
-                si = TriangleInteraction(S.P(prim, 0), S.P(prim, 1), S.P(prim, 2), f->tri_flip[prim], ti, rd, S.Attr(prim));
+            if (prim >= 0) si = S.Interact(prim, ti, rd);
             // GenerateRaySamples: dims 6 + 7 depth (path depth)
             AnySampler h2{HaltonState{&S.halton, 0, 0}, ZSobolState{&S.zsobol}, S.useZSobol};
             h2.Start(px, py, sampleIndex, 6 + 7 * depth);
@@ -3498,10 +3886,8 @@ struct Renderer {
                         Spectrum ru = r_u * 0.f, rl = r_u * (1 * lpmf);
                         shadow(pS, ds.p - pS, medium, beta * ph * ds.L, ru, rl);
                     } else if (sampledL && li < f->n_area_lights) {
-                        int lp = f->light_prim[li];
                         ShapeSample ss;
-                        if (TriangleSample(S.P(lp, 0), S.P(lp, 1), S.P(lp, 2), f->tri_flip[lp], pS, Vec(0, 0, 0), dU0,
-                                           dU1, &ss, S.Attr(lp)) &&
+                        if (sampleArea(li, pS, Vec(0, 0, 0), Vec(0, 0, 0), Vec(0, 0, 0), dU0, dU1, &ss) &&
                             ss.pdf != 0 && LengthSquared(ss.p - pS) != 0) {
                             Vec wi = Normalize(ss.p - pS);
                             Spectrum Le(0.f);
@@ -3578,16 +3964,14 @@ struct Renderer {
                 continue;
             }
             // HandleEmissiveIntersection
-            int light = f->tri_light[prim];
+            int light = S.Light(prim);
             if (light >= 0 && (f->light_two_sided[light] || DotN(si.n, si.wo) >= 0)) {
                 Spectrum Le = LightL(light, lambda);
                 if (Le) {
                     if (depth == 0 || specularBounce) L = L + beta * Le / r_u.Average();
                     else {
                         Float lightChoicePDF = lights.PMF(prevP, prevNs, light);
-                        int lp = f->light_prim[light];
-                        Float lightPDF = lightChoicePDF * TrianglePDF(S.P(lp, 0), S.P(lp, 1), S.P(lp, 2), f->tri_flip[lp],
-                                                                      prevP, prevErr, prevN, prevNs, -si.wo, S.Attr(lp));
+                        Float lightPDF = lightChoicePDF * pdfArea(light, prevP, prevErr, prevN, prevNs, -si.wo);
                         Spectrum rl = r_l * lightPDF;
                         L = L + beta * Le / (r_u + rl).Average();
                     }
@@ -3595,7 +3979,7 @@ struct Renderer {
             }
             if (wf == S.maxDepth) break;
             // Material::GetBxDF (materials.h:466-471 diffuse, :182-204 dielectric, :491-511 conductor)
-            int mat = f->tri_material[prim];
+            int mat = S.Material(prim);
             // MixMaterial::ChooseMaterial at the closest hit (wavefront/intersect.h:90-97,
             // materials.h:285-294): amount texture without (u,v) derivatives, HashFloat(p, wo,
             // m0, m1) with the material indices standing in for pbrt's material pointers
@@ -3790,10 +4174,10 @@ struct Renderer {
             }
             // light sampling + shadow ray (surfscatter.cpp:252-326), IsNonSpecular(flags)
             if (flags & (BxDiffuse | BxGlossy)) {
-                Vec cp = si.p;
+                Vec cp = si.p, cpErr = si.err;  // LightSampleContext: the offset point is exact
                 bool refl = flags & BxR, trans = flags & BxT;
-                if (refl && !trans) cp = OffsetRayOrigin(si.p, si.err, si.n, si.wo);
-                else if (trans && refl) cp = OffsetRayOrigin(si.p, si.err, si.n, -si.wo);
+                if (refl && !trans) cp = OffsetRayOrigin(si.p, si.err, si.n, si.wo), cpErr = Vec(0, 0, 0);
+                else if (trans && refl) cp = OffsetRayOrigin(si.p, si.err, si.n, -si.wo), cpErr = Vec(0, 0, 0);
                 int li;
                 Float lpmf;
                 DeltaSample ds;
@@ -3832,11 +4216,9 @@ struct Renderer {
                         shadow(pf, ds.p - pf, DotN(si.n, ds.p - pf) > 0 ? mOut : mIn, b2 * ds.L, ru, rl);
                     }
                 } else if (sampledL && li < f->n_area_lights) {
-                    int lp = f->light_prim[li];
                     ShapeSample ss;
-                    if (TriangleSample(S.P(lp, 0), S.P(lp, 1), S.P(lp, 2), f->tri_flip[lp], cp, si.ns, dU0, dU1, &ss,
-                                       S.Attr(lp)) &&
-                        ss.pdf != 0 && LengthSquared(ss.p - cp) != 0) {
+                    if (sampleArea(li, cp, cpErr, si.n, si.ns, dU0, dU1, &ss) && ss.pdf != 0 &&
+                        LengthSquared(ss.p - cp) != 0) {
                         Vec wi = Normalize(ss.p - cp);
                         Spectrum Le(0.f);
                         if (f->light_two_sided[li] || DotN(ss.n, -wi) >= 0) Le = LightL(li, lambda);
@@ -4080,6 +4462,39 @@ int oracle_texture_eval(const pbrt_scene_flat *flat, const pbrt_scene_info *info
         Wavelengths L = Wavelengths::SampleUniform(0.f);
         for (int k = 0; k < NS; ++k) L.lambda[k] = lambda[i];
         out[4 + i] = t.EvalS(node, c, L)[0];
+    }
+    return 0;
+}
+// the oracle's sphere / disk evaluation, laid out as pbrt_debug_shape_eval's rows
+int oracle_shape_eval(const pbrt_scene_flat *flat, int shape, const float *rays, const float *u, int n, float *out) {
+    if (shape < 0 || shape >= flat->n_shapes) return -1;
+    OShape sh;
+    sh.Init(flat, shape);
+    for (int i = 0; i < n; ++i) {
+        float *o = out + 40 * (size_t)i;
+        std::fill(o, o + 40, 0.f);
+        const Vec ro(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]), rd(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
+        Float th;
+        Vec pObj;
+        if (sh.Intersect(ro, rd, Infinity, &th, &pObj)) {
+            const Interaction si = sh.Surface(pObj, rd);
+            const Vec v[8] = {pObj, si.p, si.err, si.n, si.ns, si.dpdu, si.dpdv, Vec(si.uv[0], si.uv[1], 0)};
+            o[0] = 1;
+            o[1] = th;
+            for (int k = 0; k < 8; ++k)
+                for (int j = 0; j < (k == 7 ? 2 : 3); ++j) o[2 + 3 * k + j] = v[k][j];
+        }
+        ShapeSample ss;
+        if (sh.Sample(ro, Vec(0, 0, 0), Vec(0, 0, 0), u[2 * i], u[2 * i + 1], &ss)) {
+            o[26] = 1;
+            for (int j = 0; j < 3; ++j) {
+                o[27 + j] = ss.p[j];
+                o[30 + j] = ss.err[j];
+                o[33 + j] = ss.n[j];
+            }
+            o[36] = ss.pdf;
+        }
+        o[37] = sh.PDF(ro, Vec(0, 0, 0), Vec(0, 0, 0), rd);
     }
     return 0;
 }

@@ -50,6 +50,7 @@ def lib():
         _lib.oracle_set_rgb_table.argtypes = [vp, vp]
         _lib.oracle_texture_eval.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_int, vp]
         _lib.oracle_env_eval.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_int, vp]
+        _lib.oracle_shape_eval.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_int, vp]
         _lib.oracle_camera_min_diff.argtypes = [vp, vp, vp]
         _lib.oracle_image_level.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int64,
                                             ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
@@ -95,6 +96,17 @@ def env_eval(scene, env, dirs, u):
     uu = f32(u).reshape(-1, 2)
     out = np.zeros((len(d), 16), np.float32)
     rc = lib().oracle_env_eval(ctypes.byref(flat), env, d.ctypes.data, uu.ctypes.data, len(d), out.ctypes.data)
+    assert rc == 0, rc
+    return out
+
+
+def shape_eval(scene, shape, rays, u):
+    """The oracle's sphere / disk evaluation, rows as pbrt_amd.Scene.shape_eval returns them"""
+    flat = scene.flat()
+    r = f32(rays).reshape(-1, 6)
+    uu = f32(u).reshape(-1, 2)
+    out = np.zeros((len(r), 40), np.float32)
+    rc = lib().oracle_shape_eval(ctypes.byref(flat), shape, r.ctypes.data, uu.ctypes.data, len(r), out.ctypes.data)
     assert rc == 0, rc
     return out
 

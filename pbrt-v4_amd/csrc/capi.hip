@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <functional>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -249,7 +250,8 @@ struct pbrt_scene {
     std::vector<int32_t> tris, lightPrim, lightSpectrum, lightTwoSided, infSpectrum, matConstant, nodeInfo, matType,
         matSpectra, plOffsets, infDistant, uniformOrder;
     std::vector<float> deltaLights;
-    std::vector<int32_t> infImage, envInfo;
+    std::vector<int32_t> infImage, envInfo, shapeInfo;
+    std::vector<float> shapeParams;
     std::vector<float> envXform, envRgb;
     std::vector<uint64_t> envOffset;
     TexTables tex;
@@ -257,6 +259,14 @@ struct pbrt_scene {
         const SceneDesc &s = desc;
         infImage.clear();
         for (auto &l : s.infiniteLights) infImage.push_back(l.image);
+        shapeInfo.clear();
+        shapeParams.clear();
+        for (const AnalyticShapeDesc &a : s.shapes) {
+            shapeInfo.insert(shapeInfo.end(), {a.dev.kind, a.dev.flags, a.material, a.light, a.medium[0], a.medium[1], 0, 0});
+            shapeParams.insert(shapeParams.end(), a.dev.r2o, a.dev.r2o + 12);
+            shapeParams.insert(shapeParams.end(), a.dev.o2r, a.dev.o2r + 12);
+            shapeParams.insert(shapeParams.end(), {a.dev.a, a.dev.b, a.dev.c, a.dev.d, a.dev.e, a.dev.f, 0.f, 0.f});
+        }
         envInfo.clear();
         envXform.clear();
         envRgb.clear();
@@ -306,7 +316,7 @@ struct pbrt_scene {
         lightSpectrum.clear();
         lightTwoSided.clear();
         for (auto &l : s.areaLights) {
-            lightPrim.push_back(l.prim);
+            lightPrim.push_back(l.shape >= 0 ? (int32_t)s.tris.size() + l.shape : l.prim);
             lightScale.push_back(l.scale);
             lightSpectrum.push_back(l.spectrum);
             lightTwoSided.push_back(l.twoSided ? 1 : 0);
@@ -413,6 +423,8 @@ struct pbrt_context {
     DevBuf<int> matTex;
     DevBuf<float> texCoef, texR;  // k_texture results (PathState::texCoef / texR)
     DevBuf<int> infImage;
+    DevBuf<DeviceShape> shapes;
+    DevBuf<ShapeBVHNode> shapeNodes;
     DevBuf<EnvCoef> envCoef;
     DevBuf<float> envDist;
     DevBuf<DeviceEnvLight> envLights;
@@ -488,6 +500,59 @@ static bool SigmoidNeverZero(float c0, float c1, float c2) {
     return m - err > -1000.0;
 }
 
+// Binary BVH over the spheres and disks (ShapeBVHNode): median split of the centroids along the
+// widest axis down to one shape per leaf (a leaf's child is the shape index, so the device
+// array stays in scene order)
+static std::vector<ShapeBVHNode> BuildShapeBVH(const std::vector<AnalyticShapeDesc> &shapes) {
+    std::vector<ShapeBVHNode> nodes;
+    const int n = (int)shapes.size();
+    if (n == 0) {
+        nodes.push_back(ShapeBVHNode{{0, 0, 0}, {0, 0, 0}, 0, 0});
+        return nodes;
+    }
+    std::vector<V3> lo(n), hi(n), cen(n);
+    for (int i = 0; i < n; ++i) {
+        ShapeBounds(shapes[i].dev, &lo[i], &hi[i]);
+        cen[i] = (lo[i] + hi[i]) * 0.5f;
+    }
+    std::vector<int> order(n);
+    for (int i = 0; i < n; ++i) order[i] = i;
+    std::function<int(int, int)> build = [&](int a, int e) -> int {
+        const int idx = (int)nodes.size();
+        nodes.push_back(ShapeBVHNode{});
+        V3 bl(kInfinity, kInfinity, kInfinity), bh(-kInfinity, -kInfinity, -kInfinity);
+        V3 cl = bl, ch = bh;
+        for (int i = a; i < e; ++i) {
+            const int k = order[i];
+            bl = V3(std::fmin(bl.x, lo[k].x), std::fmin(bl.y, lo[k].y), std::fmin(bl.z, lo[k].z));
+            bh = V3(std::fmax(bh.x, hi[k].x), std::fmax(bh.y, hi[k].y), std::fmax(bh.z, hi[k].z));
+            cl = V3(std::fmin(cl.x, cen[k].x), std::fmin(cl.y, cen[k].y), std::fmin(cl.z, cen[k].z));
+            ch = V3(std::fmax(ch.x, cen[k].x), std::fmax(ch.y, cen[k].y), std::fmax(ch.z, cen[k].z));
+        }
+        for (int j = 0; j < 3; ++j) {
+            nodes[idx].lo[j] = bl[j];
+            nodes[idx].hi[j] = bh[j];
+        }
+        if (e - a == 1) {
+            nodes[idx].child = order[a];
+            nodes[idx].count = 1;
+            return idx;
+        }
+        const V3 ext = ch - cl;
+        const int axis = ext.x > ext.y ? (ext.x > ext.z ? 0 : 2) : (ext.y > ext.z ? 1 : 2);
+        const int mid = (a + e) / 2;
+        std::nth_element(order.begin() + a, order.begin() + mid, order.begin() + e,
+                         [&](int x, int y) { return cen[x][axis] < cen[y][axis]; });
+        build(a, mid);
+        const int right = build(mid, e);
+        nodes[idx].child = right;
+        nodes[idx].count = 0;
+        return idx;
+    };
+    build(0, n);
+    return nodes;
+}
+
 static void BuildDevice(pbrt_context *c) {
     SceneDesc &s = c->desc;
     HIPCHECK(hipSetDevice(c->device));
@@ -507,13 +572,20 @@ static void BuildDevice(pbrt_context *c) {
     int nt = (int)s.tris.size();
     std::vector<int> origToLeaf(nt);
     for (int i = 0; i < nt; ++i) origToLeaf[b.triPrim[i]] = i;
-    std::vector<int> pm(nt), pl(nt);
-    std::vector<uint8_t> pf(nt);
+    const int nsh = (int)s.shapes.size();
+    std::vector<int> pm(nt + nsh), pl(nt + nsh), po(b.triPrim.begin(), b.triPrim.end());
+    std::vector<uint8_t> pf(nt + nsh, 0);
     for (int i = 0; i < nt; ++i) {
         int o = b.triPrim[i];
         pm[i] = s.triMaterial[o];
         pl[i] = s.triLight[o];
         pf[i] = s.triFlip[o];
+    }
+    // spheres and disks follow the leaf-order triangles (prim nt + k; original id nt + k)
+    for (int k = 0; k < nsh; ++k) {
+        pm[nt + k] = s.shapes[k].material;
+        pl[nt + k] = s.shapes[k].light;
+        po.push_back(nt + k);
     }
     c->nodes.Upload(b.nodes);
     c->qnodes.Upload(b.qnodes);
@@ -521,7 +593,13 @@ static void BuildDevice(pbrt_context *c) {
     c->primMaterial.Upload(pm);
     c->primLight.Upload(pl);
     c->primFlip.Upload(pf);
-    c->primOrig.Upload(b.triPrim);
+    c->primOrig.Upload(po);
+    {
+        std::vector<DeviceShape> ds;
+        for (const AnalyticShapeDesc &a : s.shapes) ds.push_back(a.dev);
+        c->shapes.Upload(ds);
+        c->shapeNodes.Upload(BuildShapeBVH(s.shapes));
+    }
     // vertex normals / uv per leaf triangle (only when some mesh has them)
     if (std::any_of(s.triShade.begin(), s.triShade.end(), [](uint8_t f) { return f != 0; })) {
         std::vector<float> ts((size_t)nt * 16, 0.f);
@@ -598,7 +676,7 @@ static void BuildDevice(pbrt_context *c) {
     std::vector<int> lp, ls, lt;
     std::vector<float> lsc, la;
     for (auto &l : s.areaLights) {
-        lp.push_back(origToLeaf[l.prim]);
+        lp.push_back(l.shape >= 0 ? nt + l.shape : origToLeaf[l.prim]);
         ls.push_back(l.spectrum);
         lt.push_back(l.twoSided);
         lsc.push_back(l.scale);
@@ -612,6 +690,18 @@ static void BuildDevice(pbrt_context *c) {
     std::vector<DeviceAreaLight> dl;
     for (auto &l : s.areaLights) {
         DeviceAreaLight d{};
+        if (l.shape >= 0) {
+            // a sphere or disk emitter: .w holds its prim id nt + shape (no vertices)
+            const int prim = nt + l.shape;
+            float bits;
+            memcpy(&bits, &prim, 4);
+            d.v0 = make_float4(0.f, 0.f, 0.f, bits);
+            d.scale = l.scale;
+            d.spectrum = l.spectrum;
+            d.twoSided = l.twoSided;
+            dl.push_back(d);
+            continue;
+        }
         int leaf = origToLeaf[l.prim];
         const float *v = &b.triVerts[(size_t)leaf * 12];
         float leafBits;  // .w: the light's leaf prim (its shading data), as int bits
@@ -750,11 +840,15 @@ static void BuildDevice(pbrt_context *c) {
         c->mediumInfo.Upload(std::vector<int>(mi.begin(), mi.end()));
         c->mediumParams.Upload(mp);
         c->mediumValues.Upload(mv);
-        if (!s.triMedium.empty()) {
-            std::vector<int> tm((size_t)nt * 2);
-            for (int i = 0; i < nt; ++i) {
+        if (!s.triMedium.empty() || nsh > 0) {
+            std::vector<int> tm((size_t)(nt + nsh) * 2, -1);
+            for (int i = 0; i < nt && !s.triMedium.empty(); ++i) {
                 tm[2 * i] = s.triMedium[b.triPrim[i]][0];
                 tm[2 * i + 1] = s.triMedium[b.triPrim[i]][1];
+            }
+            for (int k = 0; k < nsh; ++k) {
+                tm[2 * (nt + k)] = s.shapes[k].medium[0];
+                tm[2 * (nt + k) + 1] = s.shapes[k].medium[1];
             }
             c->primMedium.Upload(tm);
         }
@@ -795,6 +889,9 @@ static void BuildDevice(pbrt_context *c) {
     S.primLight = c->primLight.p;
     S.primFlip = c->primFlip.p;
     S.primOrig = c->primOrig.p;
+    S.nShapes = nsh;
+    S.shapes = c->shapes.p;
+    S.shapeNodes = c->shapeNodes.p;
     S.triShade = (const float4 *)c->triShade.p;
     S.matCoeffs = (const float4 *)c->matCoeffs.p;
     S.matConstant = c->matConstant.p;
@@ -1322,7 +1419,7 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
             const bool lean = !noLean && c->S.samplerType == 0 &&
                               (uint64_t)(st.firstSample + nS) * haltonStride <= (1ull << 24) &&
                               c->S.shadeLds.lightsInLds && c->S.shadeLds.denseInLds && c->S.triShade == nullptr &&
-                              c->S.nDelta == 0 && c->S.nEnv == 0 && !c->S.textured && !c->hasMix;
+                              c->S.nDelta == 0 && c->S.nEnv == 0 && c->S.nShapes == 0 && !c->S.textured && !c->hasMix;
             for (int depth = 0; depth <= s.maxDepth; ++depth) {
                 // closest-hit launches are event-timed in the first pass of a render only: the
                 // passes are statistically identical and each event pair costs a queue gap
@@ -1503,6 +1600,9 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
     f->env_xform = scene->envXform.data();
     f->env_offset = scene->envOffset.data();
     f->env_rgb = scene->envRgb.data();
+    f->n_shapes = (int)scene->desc.shapes.size();
+    f->shape_info = scene->shapeInfo.data();
+    f->shape_params = scene->shapeParams.data();
     f->uniform_order = scene->uniformOrder.data();
     f->scene_radius = s.sceneRadius;
     {
@@ -2028,6 +2128,44 @@ int pbrt_debug_env_eval(const pbrt_scene *scene, int env, const float *dirs, con
             o[11] = wi.y;
             o[12] = wi.z;
             o[13] = o[14] = o[15] = 0;
+        }
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_debug_shape_eval(const pbrt_scene *scene, int shape, const float *rays, const float *u, int n, float *out) {
+    try {
+        if (!scene || !rays || !u || !out) return Fail("null argument");
+        const SceneDesc &s = scene->desc;
+        if (shape < 0 || shape >= (int)s.shapes.size()) return Fail("shape index out of range");
+        const DeviceShape &d = s.shapes[shape].dev;
+        for (int i = 0; i < n; ++i) {
+            float *o = out + 40 * (size_t)i;
+            std::fill(o, o + 40, 0.f);
+            const V3 ro(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]), rd(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
+            float th;
+            V3 pObj;
+            if (ShapeIntersect(d, ro, rd, kInfinity, &th, &pObj)) {
+                const TriSurface si = ShapeSurface(d, pObj);
+                const V3 v[8] = {pObj, si.p, si.pErr, si.n, si.ns, si.dpdu, si.dpdv, V3(si.uv[0], si.uv[1], 0)};
+                o[0] = 1;
+                o[1] = th;
+                for (int k = 0; k < 8; ++k)
+                    for (int j = 0; j < (k == 7 ? 2 : 3); ++j) o[2 + 3 * k + j] = v[k][j];
+            }
+            ShapeSamplePt ss;
+            if (ShapeSampleSolidAngle(d, ro, V3(0, 0, 0), V3(0, 0, 0), u[2 * i], u[2 * i + 1], &ss)) {
+                o[26] = 1;
+                for (int j = 0; j < 3; ++j) {
+                    o[27 + j] = ss.p[j];
+                    o[30 + j] = ss.pErr[j];
+                    o[33 + j] = ss.n[j];
+                }
+                o[36] = ss.pdf;
+            }
+            o[37] = ShapePDFSolidAngle(d, ro, V3(0, 0, 0), V3(0, 0, 0), rd);
         }
         return 0;
     } catch (const std::exception &e) {

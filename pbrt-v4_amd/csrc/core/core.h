@@ -1675,6 +1675,390 @@ PHD float EnvLe(const EnvCoef &c, float lightScale, float illum, float lambda) {
     return lightScale * ((c.s * SigmoidPolynomial(c.c0, c.c1, c.c2, lambda)) * illum);
 }
 
+// ---------------------------------------------------------------- analytic shapes
+// Interval (util/math.h:819-1076) with pbrt's CPU rounding helpers AddRoundUp(a, b) =
+// NextFloatUp(a + b) etc. (util/float.h:201-301); the constructor orders its bounds
+struct Itv {
+    float lo, hi;
+};
+PHD Itv ItvMake(float a, float b) { return Itv{(b < a) ? b : a, (a < b) ? b : a}; }
+PHD Itv ItvExact(float v) { return Itv{v, v}; }
+PHD Itv ItvFromValueAndError(float v, float err) {
+    if (err == 0) return Itv{v, v};
+    return Itv{NextFloatDown(v + (-err)), NextFloatUp(v + err)};
+}
+PHD float ItvMid(Itv i) { return (i.lo + i.hi) / 2; }
+PHD float ItvErr(Itv i) { return (i.hi - i.lo) / 2; }
+PHD bool ItvHasZero(Itv i) { return 0 >= i.lo && 0 <= i.hi; }
+PHD float Min4(float a, float b, float c, float d) {
+    float m = a;
+    m = (b < m) ? b : m;
+    m = (c < m) ? c : m;
+    return (d < m) ? d : m;
+}
+PHD float Max4(float a, float b, float c, float d) {
+    float m = a;
+    m = (m < b) ? b : m;
+    m = (m < c) ? c : m;
+    return (m < d) ? d : m;
+}
+PHD Itv operator+(Itv a, Itv b) { return ItvMake(NextFloatDown(a.lo + b.lo), NextFloatUp(a.hi + b.hi)); }
+PHD Itv operator-(Itv a, Itv b) { return ItvMake(NextFloatDown(a.lo + (-b.hi)), NextFloatUp(a.hi + (-b.lo))); }
+PHD Itv operator*(Itv a, Itv b) {
+    return ItvMake(Min4(NextFloatDown(a.lo * b.lo), NextFloatDown(a.hi * b.lo), NextFloatDown(a.lo * b.hi),
+                        NextFloatDown(a.hi * b.hi)),
+                   Max4(NextFloatUp(a.lo * b.lo), NextFloatUp(a.hi * b.lo), NextFloatUp(a.lo * b.hi),
+                        NextFloatUp(a.hi * b.hi)));
+}
+PHD Itv operator/(Itv a, Itv b) {
+    if (ItvHasZero(b)) return Itv{-kInfinity, kInfinity};
+    return ItvMake(Min4(NextFloatDown(a.lo / b.lo), NextFloatDown(a.hi / b.lo), NextFloatDown(a.lo / b.hi),
+                        NextFloatDown(a.hi / b.hi)),
+                   Max4(NextFloatUp(a.lo / b.lo), NextFloatUp(a.hi / b.lo), NextFloatUp(a.lo / b.hi),
+                        NextFloatUp(a.hi / b.hi)));
+}
+PHD Itv operator*(float f, Itv i) {
+    if (f > 0) return ItvMake(NextFloatDown(f * i.lo), NextFloatUp(f * i.hi));
+    return ItvMake(NextFloatDown(f * i.hi), NextFloatUp(f * i.lo));
+}
+PHD Itv ItvSqr(Itv i) {
+    float alow = std::fabs(i.lo), ahigh = std::fabs(i.hi);
+    if (alow > ahigh) {
+        const float t = alow;
+        alow = ahigh;
+        ahigh = t;
+    }
+    if (ItvHasZero(i)) return ItvMake(0, NextFloatUp(ahigh * ahigh));
+    return ItvMake(NextFloatDown(alow * alow), NextFloatUp(ahigh * ahigh));
+}
+PHD Itv ItvSqrt(Itv i) { return ItvMake(std::fmax(0.f, NextFloatDown(std::sqrt(i.lo))), NextFloatUp(std::sqrt(i.hi))); }
+struct P3i {
+    Itv x, y, z;
+};
+// Transform::operator()(Point3fi) / (Vector3fi) for exact inputs (util/transform.h:133-176,
+// 272-306): the affine 3x4 row-major matrix m; the result as Point3fi(value, error)
+PHD P3i XfPointExact(const float *m, V3 p) {
+    const float x = p.x, y = p.y, z = p.z;
+    P3i r;
+    Itv *o[3] = {&r.x, &r.y, &r.z};
+    for (int i = 0; i < 3; ++i) {
+        const float *row = m + 4 * i;
+        const float v = (row[0] * x + row[1] * y) + (row[2] * z + row[3]);
+        const float e = gamma(3) * (std::fabs(row[0] * x) + std::fabs(row[1] * y) + std::fabs(row[2] * z) +
+                                    std::fabs(row[3]));
+        *o[i] = ItvFromValueAndError(v, e);
+    }
+    return r;
+}
+PHD P3i XfVectorExact(const float *m, V3 v) {
+    P3i r;
+    Itv *o[3] = {&r.x, &r.y, &r.z};
+    for (int i = 0; i < 3; ++i) {
+        const float *row = m + 4 * i;
+        const float e = gamma(3) * (std::fabs(row[0] * v.x) + std::fabs(row[1] * v.y) + std::fabs(row[2] * v.z));
+        const float x = row[0] * v.x + row[1] * v.y + row[2] * v.z;
+        *o[i] = ItvFromValueAndError(x, e);
+    }
+    return r;
+}
+// Transform::operator()(Point3fi) of an inexact point (value = interval midpoint, error = half
+// width): *po, *pe the resulting Point3fi's midpoint and half width
+PHD void XfPointInexact(const float *m, P3i p, V3 *po, V3 *pe) {
+    const float x = ItvMid(p.x), y = ItvMid(p.y), z = ItvMid(p.z);
+    const V3 ein(ItvErr(p.x), ItvErr(p.y), ItvErr(p.z));
+    const bool exact = ein.x == 0 && ein.y == 0 && ein.z == 0;
+    for (int i = 0; i < 3; ++i) {
+        const float *row = m + 4 * i;
+        const float v = (row[0] * x + row[1] * y) + (row[2] * z + row[3]);
+        float e = gamma(3) * (std::fabs(row[0] * x) + std::fabs(row[1] * y) + std::fabs(row[2] * z) + std::fabs(row[3]));
+        if (!exact)
+            e = (gamma(3) + 1) * (std::fabs(row[0]) * ein.x + std::fabs(row[1]) * ein.y + std::fabs(row[2]) * ein.z) + e;
+        const Itv r = ItvFromValueAndError(v, e);
+        (*po)[i] = ItvMid(r);
+        (*pe)[i] = ItvErr(r);
+    }
+}
+// Transform::operator()(Vector3f) and (Normal3f) (the normal through the inverse's transpose)
+PHD V3 XfVec(const float *m, V3 v) {
+    return V3(m[0] * v.x + m[1] * v.y + m[2] * v.z, m[4] * v.x + m[5] * v.y + m[6] * v.z,
+              m[8] * v.x + m[9] * v.y + m[10] * v.z);
+}
+PHD V3 XfNormal(const float *mInv, V3 n) {
+    return V3(mInv[0] * n.x + mInv[4] * n.y + mInv[8] * n.z, mInv[1] * n.x + mInv[5] * n.y + mInv[9] * n.z,
+              mInv[2] * n.x + mInv[6] * n.y + mInv[10] * n.z);
+}
+// Transform::operator()(Point3f) (util/transform.h:310-319), affine
+PHD V3 XfPt(const float *m, V3 p) {
+    return V3(m[0] * p.x + m[1] * p.y + m[2] * p.z + m[3], m[4] * p.x + m[5] * p.y + m[6] * p.z + m[7],
+              m[8] * p.x + m[9] * p.y + m[10] * p.z + m[11]);
+}
+
+// Sphere and Disk (shapes.h:106-571): affine renderFromObject (o2r) and objectFromRender (r2o)
+enum ShapeKindT { kShapeSphereT = 1, kShapeDiskT = 2 };
+struct alignas(16) DeviceShape {
+    float r2o[12], o2r[12];
+    // sphere: radius, zMin, zMax, phiMax, thetaZMin, thetaZMax; disk: height, radius,
+    // innerRadius, phiMax
+    float a, b, c, d, e, f;
+    int kind, flags;  // flags: bit0 reverseOrientation, bit1 transformSwapsHandedness
+};
+static_assert(sizeof(DeviceShape) == 128, "DeviceShape must be 128 bytes");
+// binary BVH over the analytic shapes (host-built, median split): count 0 = interior node whose
+// children are this + 1 and `child`; count > 0 = leaf of shapes [child, child + count)
+struct alignas(16) ShapeBVHNode {
+    float lo[3], hi[3];
+    int child, count;
+};
+PHD float ShapeArea(const DeviceShape &s) {
+    if (s.kind == kShapeSphereT) return s.d * s.a * (s.c - s.b);  // phiMax radius (zMax - zMin)
+    return s.d * 0.5f * (Sqr(s.b) - Sqr(s.c));                    // phiMax / 2 (r^2 - ri^2)
+}
+// phi of an object-space hit (atan2, wrapped to [0, 2 pi))
+PHD float ShapePhi(V3 p) {
+    float phi = ATan2f(p.y, p.x);
+    if (phi < 0) phi += 2 * kPi;
+    return phi;
+}
+// Sphere::BasicIntersect (shapes.h:147-229): *pObj the refined object-space hit
+PHD bool SphereIntersect(const DeviceShape &s, V3 ro, V3 rd, float tMax, float *tHit, V3 *pObj) {
+    const float radius = s.a, zMin = s.b, zMax = s.c, phiMax = s.d;
+    const P3i oi = XfPointExact(s.r2o, ro), di = XfVectorExact(s.r2o, rd);
+    const Itv a = ItvSqr(di.x) + ItvSqr(di.y) + ItvSqr(di.z);
+    const Itv b = 2.f * (di.x * oi.x + di.y * oi.y + di.z * oi.z);
+    const Itv c = ItvSqr(oi.x) + ItvSqr(oi.y) + ItvSqr(oi.z) - ItvSqr(ItvExact(radius));
+    const Itv f = b / (2.f * a);
+    const Itv vx = oi.x - f * di.x, vy = oi.y - f * di.y, vz = oi.z - f * di.z;
+    const Itv length = ItvSqrt(ItvSqr(vx) + ItvSqr(vy) + ItvSqr(vz));
+    const Itv discrim = 4.f * a * (ItvExact(radius) + length) * (ItvExact(radius) - length);
+    if (discrim.lo < 0) return false;
+    const Itv rootDiscrim = ItvSqrt(discrim);
+    const Itv q = ItvMid(b) < 0 ? -.5f * (b - rootDiscrim) : -.5f * (b + rootDiscrim);
+    Itv t0 = q / a, t1 = c / q;
+    if (t0.lo > t1.lo) {
+        const Itv t = t0;
+        t0 = t1;
+        t1 = t;
+    }
+    if (t0.hi > tMax || t1.lo <= 0) return false;
+    Itv tShapeHit = t0;
+    if (tShapeHit.lo <= 0) {
+        tShapeHit = t1;
+        if (tShapeHit.hi > tMax) return false;
+    }
+    const V3 o(ItvMid(oi.x), ItvMid(oi.y), ItvMid(oi.z)), d(ItvMid(di.x), ItvMid(di.y), ItvMid(di.z));
+    for (int pass = 0; pass < 2; ++pass) {
+        const float th = ItvMid(tShapeHit);
+        V3 pHit = o + th * d;
+        const float sc = radius / Distance(pHit, V3(0, 0, 0));
+        pHit = V3(pHit.x * sc, pHit.y * sc, pHit.z * sc);
+        if (pHit.x == 0 && pHit.y == 0) pHit.x = 1e-5f * radius;
+        const float phi = ShapePhi(pHit);
+        if ((zMin > -radius && pHit.z < zMin) || (zMax < radius && pHit.z > zMax) || phi > phiMax) {
+            if (pass == 1 || (tShapeHit.lo == t1.lo && tShapeHit.hi == t1.hi)) return false;
+            if (t1.hi > tMax) return false;
+            tShapeHit = t1;
+            continue;
+        }
+        *tHit = th;
+        *pObj = pHit;
+        return true;
+    }
+    return false;
+}
+// Disk::BasicIntersect (shapes.h:446-474)
+PHD bool DiskIntersect(const DeviceShape &s, V3 ro, V3 rd, float tMax, float *tHit, V3 *pObj) {
+    const float height = s.a, radius = s.b, innerRadius = s.c, phiMax = s.d;
+    const P3i oi = XfPointExact(s.r2o, ro), di = XfVectorExact(s.r2o, rd);
+    if (ItvMid(di.z) == 0) return false;
+    const float th = (height - ItvMid(oi.z)) / ItvMid(di.z);
+    if (th <= 0 || th >= tMax) return false;
+    const V3 pHit = V3(ItvMid(oi.x), ItvMid(oi.y), ItvMid(oi.z)) + th * V3(ItvMid(di.x), ItvMid(di.y), ItvMid(di.z));
+    const float dist2 = Sqr(pHit.x) + Sqr(pHit.y);
+    if (dist2 > Sqr(radius) || dist2 < Sqr(innerRadius)) return false;
+    if (ShapePhi(pHit) > phiMax) return false;
+    *tHit = th;
+    *pObj = pHit;
+    return true;
+}
+PHD bool ShapeIntersect(const DeviceShape &s, V3 ro, V3 rd, float tMax, float *tHit, V3 *pObj) {
+    return s.kind == kShapeSphereT ? SphereIntersect(s, ro, rd, tMax, tHit, pObj)
+                                   : DiskIntersect(s, ro, rd, tMax, tHit, pObj);
+}
+// Sphere / Disk::InteractionFromIntersection (shapes.h:237-281, 477-501) followed by
+// Transform::operator()(SurfaceInteraction) (util/transform.cpp:229-261): render-space p and
+// its error, n, shading n (faced to n), dpdu, dpdv and uv
+PHD TriSurface ShapeSurface(const DeviceShape &s, V3 pHit) {
+    const float phi = ShapePhi(pHit);
+    V3 dpdu, dpdv, pError;
+    float u, v;
+    if (s.kind == kShapeSphereT) {
+        const float radius = s.a, phiMax = s.d, thetaZMin = s.e, thetaZMax = s.f;
+        u = phi / phiMax;
+        const float cosTheta = pHit.z / radius;
+        const float theta = SafeACos(cosTheta);
+        v = (theta - thetaZMin) / (thetaZMax - thetaZMin);
+        const float zRadius = std::sqrt(Sqr(pHit.x) + Sqr(pHit.y));
+        const float cosPhi = pHit.x / zRadius, sinPhi = pHit.y / zRadius;
+        dpdu = V3(-phiMax * pHit.y, phiMax * pHit.x, 0);
+        const float sinTheta = SafeSqrt(1 - Sqr(cosTheta));
+        dpdv = (thetaZMax - thetaZMin) * V3(pHit.z * cosPhi, pHit.z * sinPhi, -radius * sinTheta);
+        pError = gamma(5) * Abs(pHit);
+    } else {
+        const float height = s.a, radius = s.b, innerRadius = s.c, phiMax = s.d;
+        u = phi / phiMax;
+        const float rHit = std::sqrt(Sqr(pHit.x) + Sqr(pHit.y));
+        v = (radius - rHit) / (radius - innerRadius);
+        dpdu = V3(-phiMax * pHit.y, phiMax * pHit.x, 0);
+        dpdv = V3(pHit.x, pHit.y, 0) * (innerRadius - radius) / rHit;
+        pHit.z = height;
+        pError = V3(0, 0, 0);
+    }
+    // SurfaceInteraction ctor (interaction.h): n = Normalize(Cross(dpdu, dpdv)), flipped
+    V3 n = Normalize(Cross(dpdu, dpdv));
+    if (((s.flags & 1) != 0) != ((s.flags & 2) != 0)) n = -n;
+    const P3i pi = {ItvFromValueAndError(pHit.x, pError.x), ItvFromValueAndError(pHit.y, pError.y),
+                    ItvFromValueAndError(pHit.z, pError.z)};
+    TriSurface r;
+    XfPointInexact(s.o2r, pi, &r.p, &r.pErr);
+    r.n = Normalize(XfNormal(s.r2o, n));
+    r.dpdu = XfVec(s.o2r, dpdu);
+    r.dpdv = XfVec(s.o2r, dpdv);
+    r.ns = FaceForwardN(Normalize(XfNormal(s.r2o, n)), r.n);
+    r.dpdus = r.dpdu;
+    r.uv[0] = u;
+    r.uv[1] = v;
+    return r;
+}
+// ShapeSample of a sphere or disk light (render space): point, its error, normal
+struct ShapeSamplePt {
+    V3 p, pErr, n;
+    float pdf;
+};
+// Sphere::Sample(u) / Disk::Sample(u) (shapes.cpp:42-62, shapes.h:509-525): area measure
+PHD ShapeSamplePt ShapeSampleArea(const DeviceShape &s, float u0, float u1) {
+    ShapeSamplePt r;
+    if (s.kind == kShapeSphereT) {
+        const float radius = s.a;
+        const float z = 1 - 2 * u0, rr = SafeSqrt(1 - Sqr(z)), phi = 2 * kPi * u1;
+        float sp, cp;
+        SinCosf(phi, &sp, &cp);
+        V3 pObj = V3(0, 0, 0) + radius * V3(rr * cp, rr * sp, z);
+        const float sc = radius / Distance(pObj, V3(0, 0, 0));
+        pObj = V3(pObj.x * sc, pObj.y * sc, pObj.z * sc);
+        const V3 pObjError = gamma(5) * Abs(pObj);
+        V3 n = Normalize(XfNormal(s.r2o, pObj));
+        if (s.flags & 1) n = -n;
+        const P3i pi = {ItvFromValueAndError(pObj.x, pObjError.x), ItvFromValueAndError(pObj.y, pObjError.y),
+                        ItvFromValueAndError(pObj.z, pObjError.z)};
+        XfPointInexact(s.o2r, pi, &r.p, &r.pErr);
+        r.n = n;
+    } else {
+        const float height = s.a, radius = s.b;
+        float dx, dy;
+        SampleUniformDiskConcentric(u0, u1, &dx, &dy);
+        const V3 pObj(dx * radius, dy * radius, height);
+        const P3i pi = XfPointExact(s.o2r, pObj);
+        r.p = V3(ItvMid(pi.x), ItvMid(pi.y), ItvMid(pi.z));
+        r.pErr = V3(ItvErr(pi.x), ItvErr(pi.y), ItvErr(pi.z));
+        V3 n = Normalize(XfNormal(s.r2o, V3(0, 0, 1)));
+        if (s.flags & 1) n = -n;
+        r.n = n;
+    }
+    r.pdf = 1 / ShapeArea(s);
+    return r;
+}
+// Shape::Sample(ctx, u) (shapes.h:293-361 sphere cone sampling, :531-547 disk) with
+// ctx = (p, pErr, n): false for {} (also a zero solid-angle pdf); the pdf in solid angle
+PHD bool ShapeSampleSolidAngle(const DeviceShape &s, V3 cp, V3 cpErr, V3 cn, float u0, float u1, ShapeSamplePt *out) {
+    if (s.kind == kShapeSphereT) {
+        const float radius = s.a;
+        const V3 pCenter = XfPt(s.o2r, V3(0, 0, 0));
+        const V3 pOrigin = OffsetRayOrigin(cp, cpErr, cn, pCenter - cp);
+        if (!(DistanceSquared(pOrigin, pCenter) <= Sqr(radius))) {
+            const float sinThetaMax = radius / Distance(cp, pCenter);
+            const float sin2ThetaMax = Sqr(sinThetaMax);
+            const float cosThetaMax = SafeSqrt(1 - sin2ThetaMax);
+            float oneMinusCosThetaMax = 1 - cosThetaMax;
+            float cosTheta = (cosThetaMax - 1) * u0 + 1;
+            float sin2Theta = 1 - Sqr(cosTheta);
+            if (sin2ThetaMax < 0.00068523f) {
+                sin2Theta = sin2ThetaMax * u0;
+                cosTheta = std::sqrt(1 - sin2Theta);
+                oneMinusCosThetaMax = sin2ThetaMax / 2;
+            }
+            const float cosAlpha = sin2Theta / sinThetaMax + cosTheta * SafeSqrt(1 - sin2Theta / Sqr(sinThetaMax));
+            const float sinAlpha = SafeSqrt(1 - Sqr(cosAlpha));
+            const float phi = u1 * 2 * kPi;
+            float sp, cpp;
+            SinCosf(phi, &sp, &cpp);
+            const float st = Clampf(sinAlpha, -1, 1);
+            const V3 w(st * cpp, st * sp, Clampf(cosAlpha, -1, 1));
+            V3 fx, fy;
+            const V3 fz = Normalize(pCenter - cp);
+            CoordinateSystem(fz, &fx, &fy);
+            const V3 mw = -w;
+            V3 n = fx * mw.x + fy * mw.y + fz * mw.z;
+            const V3 p = pCenter + radius * V3(n.x, n.y, n.z);
+            if (s.flags & 1) n = -n;
+            ToPoint3fi(p, gamma(5) * Abs(p), &out->p, &out->pErr);  // Interaction(Point3fi(p, pError))
+            out->n = n;
+            out->pdf = 1 / (2 * kPi * oneMinusCosThetaMax);
+            return true;
+        }
+    }
+    ShapeSamplePt ss = ShapeSampleArea(s, u0, u1);
+    V3 wi = ss.p - cp;
+    if (LengthSquared(wi) == 0) return false;
+    wi = Normalize(wi);
+    ss.pdf /= AbsDotN(ss.n, -wi) / DistanceSquared(cp, ss.p);
+    if (std::isinf(ss.pdf)) return false;
+    *out = ss;
+    return true;
+}
+// Shape::PDF(ctx, wi) (shapes.h:364-392 sphere, :550-564 disk): the ray ctx.SpawnRay(wi)
+// against the shape alone where the cone formula does not apply
+PHD float ShapePDFSolidAngle(const DeviceShape &s, V3 cp, V3 cpErr, V3 cn, V3 wi) {
+    if (s.kind == kShapeSphereT) {
+        const float radius = s.a;
+        const V3 pCenter = XfPt(s.o2r, V3(0, 0, 0));
+        const V3 pOrigin = OffsetRayOrigin(cp, cpErr, cn, pCenter - cp);
+        if (!(DistanceSquared(pOrigin, pCenter) <= Sqr(radius))) {
+            const float sin2ThetaMax = radius * radius / DistanceSquared(cp, pCenter);
+            const float cosThetaMax = SafeSqrt(1 - sin2ThetaMax);
+            float oneMinusCosThetaMax = 1 - cosThetaMax;
+            if (sin2ThetaMax < 0.00068523f) oneMinusCosThetaMax = sin2ThetaMax / 2;
+            return 1 / (2 * kPi * oneMinusCosThetaMax);
+        }
+    }
+    const V3 ro = OffsetRayOrigin(cp, cpErr, cn, wi);
+    float tHit;
+    V3 pObj;
+    if (!ShapeIntersect(s, ro, wi, kInfinity, &tHit, &pObj)) return 0;
+    const TriSurface si = ShapeSurface(s, pObj);
+    float pdf = (1 / ShapeArea(s)) / (AbsDotN(si.n, -wi) / DistanceSquared(cp, si.p));
+    if (std::isinf(pdf)) pdf = 0;
+    return pdf;
+}
+// Sphere / Disk::Bounds (shapes.cpp:33-40, 88-92): the transformed object box's 8 corners
+PHD void ShapeBounds(const DeviceShape &s, V3 *lo, V3 *hi) {
+    V3 a, b;
+    if (s.kind == kShapeSphereT) {
+        a = V3(-s.a, -s.a, s.b);
+        b = V3(s.a, s.a, s.c);
+    } else {
+        a = V3(-s.b, -s.b, s.a);
+        b = V3(s.b, s.b, s.a);
+    }
+    *lo = V3(kInfinity, kInfinity, kInfinity);
+    *hi = V3(-kInfinity, -kInfinity, -kInfinity);
+    for (int i = 0; i < 8; ++i) {
+        const V3 c((i & 1) ? b.x : a.x, (i & 2) ? b.y : a.y, (i & 4) ? b.z : a.z);
+        const V3 q = XfPt(s.o2r, c);
+        *lo = V3(std::fmin(lo->x, q.x), std::fmin(lo->y, q.y), std::fmin(lo->z, q.z));
+        *hi = V3(std::fmax(hi->x, q.x), std::fmax(hi->y, q.y), std::fmax(hi->z, q.z));
+    }
+}
+
 // SampleTent (util/sampling.h:196-201)
 PHD float SampleTent(float u, float r) {
     float pmf;

@@ -438,6 +438,36 @@ static void BuildLightBVH(SceneDesc &s) {
     std::vector<std::pair<int, LightBounds>> bvhLights;
     for (size_t i = 0; i < s.areaLights.size(); ++i) {
         const AreaLightDesc &al = s.areaLights[i];
+        if (al.shape >= 0) {
+            // Sphere / Disk emitters: Shape::Bounds, Shape::NormalBounds (shapes.h:134,
+            // shapes.cpp:94-99: the entire sphere; the disk's transformed, oriented normal)
+            const DeviceShape &d = s.shapes[al.shape].dev;
+            const auto &dense = s.denseSpectra[al.spectrum];
+            float phi = *std::max_element(dense.begin(), dense.end());
+            phi *= al.scale * al.area * kPi;
+            LightBounds lb;
+            V3 lo, hi;
+            ShapeBounds(d, &lo, &hi);
+            lb.bounds.Add(lo);
+            lb.bounds.Add(hi);
+            if (d.kind == kShapeSphereT) {
+                lb.w = Normalize(V3(0, 0, 1));
+                lb.cosTheta_o = -1;
+            } else {
+                V3 n = XfNormal(d.r2o, V3(0, 0, 1));
+                if (d.flags & 1) n = -n;
+                lb.w = Normalize(Normalize(n));
+                lb.cosTheta_o = 1;
+            }
+            lb.phi = phi;
+            lb.cosTheta_e = std::cos(kPi / 2);
+            lb.twoSided = al.twoSided;
+            if (lb.phi > 0) {
+                bvhLights.push_back({(int)i, lb});
+                b.allLightBounds.Add(lb.bounds);
+            }
+            continue;
+        }
         const auto &tri = s.tris[al.prim];
         V3 p0 = s.verts[tri[0]], p1 = s.verts[tri[1]], p2 = s.verts[tri[2]];
         const auto &dense = s.denseSpectra[al.spectrum];

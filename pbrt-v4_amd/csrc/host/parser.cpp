@@ -320,6 +320,8 @@ class Parser {
     std::string cameraType = "perspective", filmType = "rgb";
     bool inWorld = false;
     struct PendingShape {
+        int kind = 0;                 // 0 triangle mesh, kShapeSphereT, kShapeDiskT
+        float sp[4] = {0, 0, 0, 0};   // sphere: radius zmin zmax phimax; disk: height radius innerradius phimax
         std::vector<V3> P;
         std::vector<int> idx;
         std::vector<float> uv;  // per vertex, 2 floats
@@ -961,6 +963,21 @@ class Parser {
             s.idx = std::move(m.triIndices);
             s.N = std::move(m.n);
             for (auto &t : m.uv) s.uv.insert(s.uv.end(), {t[0], t[1]});
+        } else if (type == "sphere") {
+            // Sphere::Create (shapes.cpp:75-85)
+            s.kind = kShapeSphereT;
+            const float radius = (float)ps.GetFloat("radius", 1.f);
+            s.sp[0] = radius;
+            s.sp[1] = (float)ps.GetFloat("zmin", -radius);
+            s.sp[2] = (float)ps.GetFloat("zmax", radius);
+            s.sp[3] = (float)ps.GetFloat("phimax", 360.f);
+        } else if (type == "disk") {
+            // Disk::Create (shapes.cpp:110-119)
+            s.kind = kShapeDiskT;
+            s.sp[0] = (float)ps.GetFloat("height", 0.);
+            s.sp[1] = (float)ps.GetFloat("radius", 1);
+            s.sp[2] = (float)ps.GetFloat("innerradius", 0);
+            s.sp[3] = (float)ps.GetFloat("phimax", 360);
         } else {
             throw Error(ps.loc + ": shape \"" + type + "\" is not supported yet");
         }
@@ -984,6 +1001,62 @@ class Parser {
             return;
         }
         shapes.push_back(std::move(s));
+    }
+
+    // Sphere / Disk constructors (shapes.h:117-128, 407-417) in render space: affine
+    // renderFromObject and its inverse as float matrices; the shape's area light (its own
+    // DiffuseAreaLight, lights.cpp:941-966 with Shape::Area) in shape order
+    template <typename MediumOf>
+    void AnalyticShape(const PendingShape &s, const Mat4 &rfo, int mat, int lightSpectrum, float lightScale,
+                       bool twoSided, float power, const MediumOf &mediumOf) {
+        if (rfo[3][0] != 0 || rfo[3][1] != 0 || rfo[3][2] != 0 || rfo[3][3] != 1)
+            throw Error(s.loc + ": projective transforms of spheres and disks are not supported");
+        const Mat4 ofr = Inverse4(rfo);
+        AnalyticShapeDesc a;
+        DeviceShape &d = a.dev;
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 4; ++j) {
+                d.o2r[4 * i + j] = (float)rfo[i][j];
+                d.r2o[4 * i + j] = (float)ofr[i][j];
+            }
+        d.kind = s.kind;
+        d.flags = (s.flip ? 1 : 0) | (SwapsHandedness(rfo) ? 2 : 0);
+        auto radians = [](float deg) { return (kPi / 180) * deg; };
+        if (s.kind == kShapeSphereT) {
+            const float radius = s.sp[0], zMin = s.sp[1], zMax = s.sp[2], phiMax = s.sp[3];
+            d.a = radius;
+            d.b = Clampf(std::min(zMin, zMax), -radius, radius);
+            d.c = Clampf(std::max(zMin, zMax), -radius, radius);
+            d.e = std::acos(Clampf(std::min(zMin, zMax) / radius, -1, 1));
+            d.f = std::acos(Clampf(std::max(zMin, zMax) / radius, -1, 1));
+            d.d = radians(Clampf(phiMax, 0, 360));
+        } else {
+            d.a = s.sp[0];
+            d.b = s.sp[1];
+            d.c = s.sp[2];
+            d.d = radians(Clampf(s.sp[3], 0, 360));
+        }
+        a.material = mat;
+        if (!scene.media.empty()) {
+            a.medium[0] = (int16_t)mediumOf(s.insideMedium, s.loc);
+            a.medium[1] = (int16_t)mediumOf(s.outsideMedium, s.loc);
+        }
+        if (lightSpectrum >= 0) {
+            AreaLightDesc l;
+            l.shape = (int)scene.shapes.size();
+            l.spectrum = lightSpectrum;
+            l.scale = lightScale;
+            l.twoSided = twoSided;
+            l.area = ShapeArea(d);
+            if (power > 0) {
+                float k_e = 1;
+                k_e *= (twoSided ? 2 : 1) * l.area * kPi;
+                l.scale *= power / k_e;
+            }
+            a.light = (int)scene.areaLights.size();
+            scene.areaLights.push_back(l);
+        }
+        scene.shapes.push_back(a);
     }
 
     // ObjectInstance: renderFromInstance = RenderFromObject() * worldFromRender (scene.cpp:392),
@@ -1446,6 +1519,10 @@ void Parser::Finish() {
             }
             ap.CheckUnused();
         }
+        if (s.kind != 0) {
+            AnalyticShape(s, rfo, mat, lightSpectrum, lightScale, twoSided, power, mediumOf);
+            continue;
+        }
         for (size_t t = 0; t < s.idx.size(); t += 3) {
             std::array<int, 3> tri = {base + s.idx[t], base + s.idx[t + 1], base + s.idx[t + 2]};
             int triIndex = (int)scene.tris.size();
@@ -1511,6 +1588,12 @@ void Parser::Finish() {
                 mn = V3(std::fmin(mn.x, v.x), std::fmin(mn.y, v.y), std::fmin(mn.z, v.z));
                 mx = V3(std::fmax(mx.x, v.x), std::fmax(mx.y, v.y), std::fmax(mx.z, v.z));
             }
+        for (const AnalyticShapeDesc &a : scene.shapes) {
+            V3 lo, hi;
+            ShapeBounds(a.dev, &lo, &hi);
+            mn = V3(std::fmin(mn.x, lo.x), std::fmin(mn.y, lo.y), std::fmin(mn.z, lo.z));
+            mx = V3(std::fmax(mx.x, hi.x), std::fmax(mx.y, hi.y), std::fmax(mx.z, hi.z));
+        }
         const V3 c = (mn + mx) / 2;
         const bool inside = c.x >= mn.x && c.x <= mx.x && c.y >= mn.y && c.y <= mx.y && c.z >= mn.z && c.z <= mx.z;
         scene.sceneRadius = inside ? Distance(c, mx) : 0;

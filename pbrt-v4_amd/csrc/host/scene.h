@@ -170,11 +170,22 @@ struct PLSpectrumDesc {
 };
 
 struct AreaLightDesc {
-    int prim = -1;          // triangle index in SceneDesc::tris
+    int prim = -1;          // triangle index in SceneDesc::tris (-1 for an analytic shape)
+    int shape = -1;         // index in SceneDesc::shapes for a sphere / disk emitter
     int spectrum = -1;      // index into SceneDesc::denseSpectra
     float scale = 1;        // final DiffuseAreaLight::scale (lights.cpp:941-966)
     bool twoSided = false;
     float area = 0;
+};
+
+// Sphere / Disk (shapes.h:106-571) in render space: the device record (affine render-from-object
+// and object-from-render matrices, parameters, orientation flags) and the shape's attributes.
+// Primitive ids: leaf-order triangles first, then shape k as nTriangles + k.
+struct AnalyticShapeDesc {
+    DeviceShape dev{};
+    int material = -1;
+    int light = -1;                   // area light index or -1
+    int16_t medium[2] = {-1, -1};     // {inside, outside}
 };
 
 // An entry of BVHLightSampler's infinite-light list (lights without bounds, lightsamplers.cpp):
@@ -261,6 +272,7 @@ struct SceneDesc {
     std::vector<V3> vertN;                       // render space, reverseOrientation applied
     std::vector<std::array<float, 2>> vertUV;
     std::vector<uint8_t> triShade;
+    std::vector<AnalyticShapeDesc> shapes;  // spheres and disks
 
     std::vector<MaterialDesc> materials;
     std::vector<MediumDesc> media;

@@ -687,10 +687,62 @@ constexpr int TraversalWaves(int tm) { return tm == kTravQuant ? PBRT_QUANT_TRAV
 inline int TraversalMode(const DeviceScene &S) {
     return S.compressed ? kTravQuant : (S.ldsTris > 0 ? kTravLds : kTravWide);
 }
+// Spheres and disks (Sphere / Disk::BasicIntersect) through their binary BVH, nearer than
+// tMax: the shape index and best = {pObj, tHit}, or -1.  Out of line: only scenes with shapes
+// reach it, and the triangle traversal keeps its registers.
+template <bool AnyHit>
+__device__ __attribute__((noinline)) int TraverseShapes(const DeviceScene &S, V3 o, V3 d, float tMax, TriHit *best) {
+    const V3 inv(1 / d.x, 1 / d.y, 1 / d.z);
+    int stack[32], sp = 0, found = -1;
+    stack[sp++] = 0;
+    while (sp > 0) {
+        const int ni = stack[--sp];
+        const ShapeBVHNode n = S.shapeNodes[ni];
+        // slab test with pbrt's 1 + 2 gamma(3) far-plane widening (util/vecmath.h:1576-1611)
+        float t0 = 0, t1 = tMax;
+        bool miss = false;
+        for (int a = 0; a < 3 && !miss; ++a) {
+            float tn = (n.lo[a] - o[a]) * inv[a], tf = (n.hi[a] - o[a]) * inv[a];
+            if (tn > tf) {
+                const float t = tn;
+                tn = tf;
+                tf = t;
+            }
+            tf *= 1 + 2 * gamma(3);
+            t0 = tn > t0 ? tn : t0;
+            t1 = tf < t1 ? tf : t1;
+            miss = t0 > t1;
+        }
+        if (miss) continue;
+        if (n.count > 0) {
+            for (int k = n.child; k < n.child + n.count; ++k) {
+                float th;
+                V3 pObj;
+                if (ShapeIntersect(S.shapes[k], o, d, tMax, &th, &pObj)) {
+                    found = k;
+                    tMax = th;
+                    *best = TriHit{pObj.x, pObj.y, pObj.z, th};
+                    if (AnyHit) return k;
+                }
+            }
+        } else if (sp < 30) {
+            stack[sp++] = n.child;
+            stack[sp++] = ni + 1;
+        }
+    }
+    return found;
+}
 template <bool AnyHit, int TM>
 __device__ inline int Traverse(const DeviceScene &S, const SceneLds &L, V3 o, V3 d, float tMax, TriHit *best,
                                TravCount *cnt = nullptr) {
-    return TraverseCW<AnyHit, TM == kTravQuant, TM == kTravLds, TM == kTravLds>(S, L, o, d, tMax, best, cnt);
+    int prim = -1;
+    if (S.nShapes == 0 || S.nTris > 0)
+        prim = TraverseCW<AnyHit, TM == kTravQuant, TM == kTravLds, TM == kTravLds>(S, L, o, d, tMax, best, cnt);
+    if (S.nShapes > 0 && !(AnyHit && prim >= 0)) {
+        const int k = TraverseShapes<AnyHit>(S, o, d, prim >= 0 ? best->t : tMax, best);
+        if (k >= 0) prim = S.nTris + k;
+    }
+    return prim;
 }
 // Adds a wave's traversal counts to stats[base..base+5]: lane sums of nodes and triangles,
 // the wave maxima of both (a wave runs until its slowest lane is done), rays, waves
@@ -735,6 +787,10 @@ struct LightSample {
 
 // Triangle geometry of a leaf-order prim
 __device__ inline void PrimVerts(const DeviceScene &S, int prim, V3 *p0, V3 *p1, V3 *p2) {
+    if (S.nShapes > 0 && prim >= S.nTris) {  // a sphere or disk: no vertices
+        *p0 = *p1 = *p2 = V3(0, 0, 0);
+        return;
+    }
     float4 a = S.triVerts[3 * prim], b = S.triVerts[3 * prim + 1], c = S.triVerts[3 * prim + 2];
     *p0 = V3(a.x, a.y, a.z);
     *p1 = V3(b.x, b.y, b.z);
@@ -743,7 +799,7 @@ __device__ inline void PrimVerts(const DeviceScene &S, int prim, V3 *p0, V3 *p1,
 
 // Vertex normals / uv of a leaf-order prim; false (and sh untouched) when it has none
 __device__ inline bool LoadTriShading(const DeviceScene &S, int prim, TriShading *sh) {
-    if (!S.triShade) return false;
+    if (!S.triShade || (S.nShapes > 0 && prim >= S.nTris)) return false;
     const float4 a = S.triShade[4 * prim];
     const int flags = __float_as_int(a.w);
     if (flags == 0) return false;
@@ -761,9 +817,14 @@ __device__ inline bool LoadTriShading(const DeviceScene &S, int prim, TriShading
     return true;
 }
 
+// SurfaceInteraction of a sphere / disk hit (b0..b2 of the hit record hold pObj)
+__device__ __attribute__((noinline)) TriSurface ShapeSurfaceAt(const DeviceScene &S, int k, V3 pObj) {
+    return ShapeSurface(S.shapes[k], pObj);
+}
 // SurfaceInteraction of a hit (Triangle::InteractionFromIntersection)
 __device__ inline TriSurface SurfaceAt(const DeviceScene &S, int prim, V3 p0, V3 p1, V3 p2, float b0, float b1,
                                        float b2) {
+    if (S.nShapes > 0 && prim >= S.nTris) return ShapeSurfaceAt(S, prim - S.nTris, V3(b0, b1, b2));
     TriShading sh;
     const bool has = LoadTriShading(S, prim, &sh);
     return TriangleSurface(p0, p1, p2, b0, b1, b2, S.primFlip[prim], has ? &sh : nullptr);
@@ -994,11 +1055,35 @@ __device__ inline float SmoothStepf(float x, float a, float b) {
     return t * t * (3 - 2 * t);
 }
 // Inl: the spherical-triangle sampling inlined (the diffuse kernels) or called out of line
+// DiffuseAreaLight::SampleLi over a sphere or disk (lights.cpp:743-775 with Shape::Sample(ctx,
+// u)): ctx = (cp, cpErr, n)
+__device__ __attribute__((noinline)) bool SampleShapeLi(const DeviceScene &S, const DeviceAreaLight &Ld, V3 cp, V3 cpErr,
+                                                       V3 n, float u0, float u1, LiSample *ls) {
+    ShapeSamplePt ss;
+    if (!ShapeSampleSolidAngle(S.shapes[__float_as_int(Ld.v0.w) - S.nTris], cp, cpErr, n, u0, u1, &ss) ||
+        ss.pdf == 0 || LengthSquared(ss.p - cp) == 0)
+        return false;
+    ls->wi = Normalize(ss.p - cp);
+    if (!(Ld.twoSided || DotN(ss.n, -ls->wi) >= 0)) return false;  // DiffuseAreaLight::L is 0
+    ls->lp = ss.p;
+    ls->lpe = ss.pErr;
+    ls->ln = ss.n;
+    ls->pdf = ss.pdf;
+    ls->scale = Ld.scale;
+    ls->d2 = 1;
+    ls->spectrum = Ld.spectrum;
+    ls->delta = false;
+    ls->envLe = false;
+    return true;
+}
 template <bool Lean, bool Inl = Lean>
 __device__ inline bool SampleLiSurface(const DeviceScene &S, const DeviceAreaLight *lightsL, int li, V3 cp, V3 n,
-                                       V3 ns, float u0, float u1, LiSample *ls) {
+                                       V3 ns, float u0, float u1, LiSample *ls, V3 cpErr = V3(0, 0, 0)) {
     if (li < S.nAreaLights) {
         const DeviceAreaLight &Ld = lightsL[li];
+        if constexpr (!Lean) {
+            if (S.nShapes > 0 && __float_as_int(Ld.v0.w) >= S.nTris) return SampleShapeLi(S, Ld, cp, cpErr, n, u0, u1, ls);
+        }
         V3 q0(Ld.v0.x, Ld.v0.y, Ld.v0.z), q1(Ld.v1.x, Ld.v1.y, Ld.v1.z), q2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
         TriShading lsh;
         const bool lhas = !Lean && LoadTriShading(S, __float_as_int(Ld.v0.w), &lsh);

@@ -152,6 +152,10 @@ struct DeviceScene {
     const int *infSpectrum;
     const float *infScale;
     const int *infDistant;
+    // spheres and disks: prim ids nTris + k (leaf-order triangles first), their BVH
+    int nShapes;
+    const DeviceShape *shapes;
+    const ShapeBVHNode *shapeNodes;
     // ImageInfiniteLight entries: infImage[j] indexes env[] (-1: not an image light)
     const int *infImage;
     const DeviceEnvLight *env;

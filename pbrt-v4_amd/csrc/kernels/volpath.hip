@@ -971,7 +971,7 @@ __device__ inline bool SampleAreaLight(const DeviceScene &S, V3 refP, V3 refN, V
     int li;
     float lpmf;
     if (!SampleLight(S, refP, refNs, uc, &li, &lpmf)) return false;
-    if (li >= S.nAreaLights) {
+    if (li >= S.nAreaLights || (S.nShapes > 0 && __float_as_int(S.lights[li].v0.w) >= S.nTris)) {
         LiSample ls;
         if (!SampleLiSurface<false>(S, S.lights, li, refP, refN, refNs, u0, u1, &ls)) return false;
         const float rd2 = 1 / ls.d2;
@@ -1065,13 +1065,13 @@ struct AreaLightHit {
     }
 };
 __device__ inline bool SampleAreaLightAt(const DeviceScene &S, V3 refP, V3 refN, V3 refNs, float uc, float u0, float u1,
-                                         float lambda0, AreaLightHit *out) {
+                                         float lambda0, AreaLightHit *out, V3 refErr = V3(0, 0, 0)) {
     int li;
     float lpmf;
     if (!SampleLight(S, refP, refNs, uc, &li, &lpmf)) return false;
-    if (li >= S.nAreaLights) {
+    if (li >= S.nAreaLights || (S.nShapes > 0 && __float_as_int(S.lights[li].v0.w) >= S.nTris)) {
         LiSample ls;
-        if (!SampleLiSurface<false>(S, S.lights, li, refP, refN, refNs, u0, u1, &ls)) return false;
+        if (!SampleLiSurface<false>(S, S.lights, li, refP, refN, refNs, u0, u1, &ls, refErr)) return false;
         out->p = ls.lp;
         out->pErr = ls.lpe;
         out->n = ls.ln;
@@ -1201,12 +1201,16 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
                     const V3 pn = LoadV3(rec.prev + 6 * (size_t)NR, NR, ri);
                     const V3 pns = LoadV3(rec.prev + 9 * (size_t)NR, NR, ri);
                     const float lightChoicePDF = LightPMF(S, pp, pns, light);
-                    TriShading lsh;
-                    const bool lhas = LoadTriShading(S, __float_as_int(Ld.v0.w), &lsh);
-                    const V3 l0(Ld.v0.x, Ld.v0.y, Ld.v0.z), l1(Ld.v1.x, Ld.v1.y, Ld.v1.z),
-                        l2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
-                    lightPDF =
-                        lightChoicePDF * TrianglePDF(l0, l1, l2, Ld.flip, lhas ? &lsh : nullptr, pp, pe, pn, pns, -wo3);
+                    if (S.nShapes > 0 && prim >= S.nTris) {
+                        lightPDF = lightChoicePDF * ShapePDFSolidAngle(S.shapes[prim - S.nTris], pp, pe, pn, -wo3);
+                    } else {
+                        TriShading lsh;
+                        const bool lhas = LoadTriShading(S, __float_as_int(Ld.v0.w), &lsh);
+                        const V3 l0(Ld.v0.x, Ld.v0.y, Ld.v0.z), l1(Ld.v1.x, Ld.v1.y, Ld.v1.z),
+                            l2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
+                        lightPDF = lightChoicePDF *
+                                   TrianglePDF(l0, l1, l2, Ld.flip, lhas ? &lsh : nullptr, pp, pe, pn, pns, -wo3);
+                    }
                 }
                 float ds = 0;
 #pragma unroll 1
@@ -1287,11 +1291,11 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
         const V3 woL = frame.ToLocal(wo3);
         // ---- light sampling + shadow ray (surfscatter.cpp:252-326), IsNonSpecular(flags)
         if (mtype == 0 || !smooth) {
-            V3 cp = si.p;
-            if (reflective && !transmissive) cp = OffsetRayOrigin(si.p, si.pErr, si.n, wo3);
-            else if (transmissive && reflective) cp = OffsetRayOrigin(si.p, si.pErr, si.n, -wo3);
+            V3 cp = si.p, cpErr = si.pErr;  // LightSampleContext: the offset point is exact
+            if (reflective && !transmissive) cp = OffsetRayOrigin(si.p, si.pErr, si.n, wo3), cpErr = V3(0, 0, 0);
+            else if (transmissive && reflective) cp = OffsetRayOrigin(si.p, si.pErr, si.n, -wo3), cpErr = V3(0, 0, 0);
             AreaLightHit ls;
-            if (SampleAreaLightAt(S, cp, si.n, si.ns, rs.dUc, rs.dU0, rs.dU1, lambda0, &ls) && woL.z != 0) {
+            if (SampleAreaLightAt(S, cp, si.n, si.ns, rs.dUc, rs.dU0, rs.dU1, lambda0, &ls, cpErr) && woL.z != 0) {
                 const V3 wi = ls.wi;
                 const V3 wiL = frame.ToLocal(wi);
                 // BSDF::f / BSDF::PDF (bsdf.h:60-135)
@@ -1736,11 +1740,11 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
         // ---- light sampling + shadow ray (surfscatter.cpp:252-326): reflective, not transmissive
         if (bflags & (kBxDiffuse | kBxGlossy)) {
             const bool refl = bflags & kBxReflection, trans = bflags & kBxTransmission;
-            V3 cp = si.p;
-            if (refl && !trans) cp = OffsetRayOrigin(si.p, si.pErr, si.n, wo3);
-            else if (refl && trans) cp = OffsetRayOrigin(si.p, si.pErr, si.n, -wo3);
+            V3 cp = si.p, cpErr = si.pErr;  // LightSampleContext: the offset point is exact
+            if (refl && !trans) cp = OffsetRayOrigin(si.p, si.pErr, si.n, wo3), cpErr = V3(0, 0, 0);
+            else if (refl && trans) cp = OffsetRayOrigin(si.p, si.pErr, si.n, -wo3), cpErr = V3(0, 0, 0);
             AreaLightHit ls;
-            if (SampleAreaLightAt(S, cp, si.n, si.ns, rs.dUc, rs.dU0, rs.dU1, lambda0, &ls) && woL.z != 0) {
+            if (SampleAreaLightAt(S, cp, si.n, si.ns, rs.dUc, rs.dU0, rs.dU1, lambda0, &ls, cpErr) && woL.z != 0) {
                 const V3 wi = ls.wi;
                 const V3 wiL = frame.ToLocal(wi);
                 if (dt) D.f(woL, wiL, fo);

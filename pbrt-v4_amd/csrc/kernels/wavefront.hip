@@ -299,11 +299,16 @@ __global__ void __launch_bounds__(kBlock) k_emissive(DeviceScene S, PathState st
             // prevIntrCtx = LightSampleContext(pi, n, ns) of the previous surface
             TriSurface prev = SurfaceAt(S, pp, q0, q1, q2, pb0, pb1, pb2);
             float lightChoicePDF = LightPMF(S, prev.p, prev.ns, light);
-            TriShading lsh;
-            const bool lhas = LoadTriShading(S, __float_as_int(Ld.v0.w), &lsh);
-            V3 l0(Ld.v0.x, Ld.v0.y, Ld.v0.z), l1(Ld.v1.x, Ld.v1.y, Ld.v1.z), l2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
-            float lightPDF = lightChoicePDF * TrianglePDF(l0, l1, l2, Ld.flip, lhas ? &lsh : nullptr, prev.p,
-                                                          prev.pErr, prev.n, prev.ns, -wo);
+            float lightPDF;
+            if (S.nShapes > 0 && prim >= S.nTris) {
+                lightPDF = lightChoicePDF * ShapePDFSolidAngle(S.shapes[prim - S.nTris], prev.p, prev.pErr, prev.n, -wo);
+            } else {
+                TriShading lsh;
+                const bool lhas = LoadTriShading(S, __float_as_int(Ld.v0.w), &lsh);
+                V3 l0(Ld.v0.x, Ld.v0.y, Ld.v0.z), l1(Ld.v1.x, Ld.v1.y, Ld.v1.z), l2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
+                lightPDF = lightChoicePDF * TrianglePDF(l0, l1, l2, Ld.flip, lhas ? &lsh : nullptr, prev.p, prev.pErr,
+                                                       prev.n, prev.ns, -wo);
+            }
             denom = Avg31(1.f + rl * lightPDF);
         }
         const float *dense = S.dense + Ld.spectrum * kDenseN;
@@ -877,14 +882,14 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
             const bool transmissive = MT == kMatDielectricT;
             // ---- light sampling + shadow ray (surfscatter.cpp:252-326)
             if (!Smooth && !smooth) {
-                V3 cp = pi;
-                if (reflective && !transmissive) cp = OffsetRayOrigin(pi, pe, n, wo);
-                else if (transmissive && reflective) cp = OffsetRayOrigin(pi, pe, n, -wo);
+                V3 cp = pi, cpErr = pe;  // LightSampleContext: the offset point is exact
+                if (reflective && !transmissive) cp = OffsetRayOrigin(pi, pe, n, wo), cpErr = V3(0, 0, 0);
+                else if (transmissive && reflective) cp = OffsetRayOrigin(pi, pe, n, -wo), cpErr = V3(0, 0, 0);
                 int li;
                 float lpmf;
                 LiSample ls;
                 if (SampleLightT<DeviceLightNode, true>(T.SL, T.SL.lightNodes, cp, ns, rs.dUc, &li, &lpmf) &&
-                    SampleLiSurface<false, true>(S, T.lightsL, li, cp, n, ns, rs.dU0, rs.dU1, &ls)) {
+                    SampleLiSurface<false, true>(S, T.lightsL, li, cp, n, ns, rs.dU0, rs.dU1, &ls, cpErr)) {
                     const V3 lp = ls.lp, lpe = ls.lpe, ln = ls.ln;
                     {
                         const V3 wi = ls.wi;

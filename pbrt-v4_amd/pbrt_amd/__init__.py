@@ -93,6 +93,9 @@ class SceneFlat(ctypes.Structure):
         ("env_xform", ctypes.POINTER(ctypes.c_float)),
         ("env_offset", ctypes.POINTER(ctypes.c_uint64)),
         ("env_rgb", ctypes.POINTER(ctypes.c_float)),
+        ("n_shapes", ctypes.c_int),
+        ("shape_info", ctypes.POINTER(ctypes.c_int32)),
+        ("shape_params", ctypes.POINTER(ctypes.c_float)),
     ]
 
 
@@ -126,6 +129,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_debug_bvh_stats", "pbrt_debug_light_bvh", "pbrt_intersect_tr", "pbrt_image_flip", "pbrt_set_kernel_profiling", "pbrt_get_kernel_stats",
     "pbrt_debug_texture_eval",
     "pbrt_debug_env_eval",
+    "pbrt_debug_shape_eval",
 ]
 
 _LIB = None
@@ -198,6 +202,7 @@ def _lib():
     lib.pbrt_debug_triangle_shading.argtypes = [c.c_void_p] * 3 + [c.c_int] + [c.c_void_p] * 3
     lib.pbrt_debug_texture_eval.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_debug_env_eval.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
+    lib.pbrt_debug_shape_eval.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_set_data_dir(str(DATA_DIR).encode())
     _LIB = lib
     return lib
@@ -358,6 +363,15 @@ class Scene:
         assert len(d) == len(uu)
         out = np.zeros((len(d), 16), dtype=np.float32)
         _check(_lib().pbrt_debug_env_eval(self._h, env, d.ctypes.data, uu.ctypes.data, len(d), out.ctypes.data))
+        return out
+
+    def shape_eval(self, shape, rays, u):
+        """The product's sphere / disk intersection, surface, sampling and pdf for rays[n][6]
+        and sample pairs u[n][2] (pbrt_debug_shape_eval): [n][40] rows as the header documents."""
+        r = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 6)
+        uu = np.ascontiguousarray(u, dtype=np.float32).reshape(-1, 2)
+        out = np.zeros((len(r), 40), dtype=np.float32)
+        _check(_lib().pbrt_debug_shape_eval(self._h, shape, r.ctypes.data, uu.ctypes.data, len(r), out.ctypes.data))
         return out
 
     def halton_fastpath_mismatches(self, dim, a0, a1, step=1):

@@ -195,6 +195,11 @@ typedef struct pbrt_scene_flat {
     int n_shapes;
     const int32_t *shape_info;
     const float *shape_params;
+    /* kind 3 (bilinear patch, shapes.h:1272-1540): shape_params holds the render-space corners
+     * p00 p10 p01 p11 in its first 12 floats, their uv in the next 8, then area and
+     * isRectangle; flags bit2 uv present, bit3 vertex normals present (shape_normals [n][12],
+     * render space) */
+    const float *shape_normals;
 } pbrt_scene_flat;
 
 typedef struct pbrt_render_params {
@@ -322,7 +327,8 @@ int pbrt_debug_env_eval(const pbrt_scene *scene, int env, const float *dirs, con
  * 106-571): for n rays rays[n][6] (o, d) and sample pairs u[n][2], out[n][40] = hit flag, tHit,
  * pObj xyz, then the render-space SurfaceInteraction p xyz, pError xyz, n xyz, shading n xyz,
  * dpdu xyz, dpdv xyz, uv; then Shape::Sample(ctx = (o, no error, no normal), u): ok flag, p
- * xyz, pError xyz, n xyz, pdf; then Shape::PDF(ctx, d); 2 unused */
+ * xyz, pError xyz, n xyz, pdf; then Shape::PDF(ctx, d); 2 unused.  Odd rows give the context the
+ * shading normal -d (the bilinear patch's cosine-weighted warp), even rows none. */
 int pbrt_debug_shape_eval(const pbrt_scene *scene, int shape, const float *rays, const float *u, int n, float *out);
 /* Filter::Sample(u) of the scene's pixel filter (FilterSampler over PiecewiseConstant2D for
  * gaussian / mitchell / sinc, SampleTent for triangle, filters.h): out3 = p.x p.y weight */

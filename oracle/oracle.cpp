@@ -1054,10 +1054,152 @@ static OInterval ISqr(OInterval i) {
 }
 static OInterval ISqrt(OInterval i) { return {std::max<Float>(0, NextFloatDown(std::sqrt(i.lo))), NextFloatUp(std::sqrt(i.hi))}; }
 
+// Bilinear-patch helpers (util/math.h:614-637 Quadratic, :1420-1426 Determinant; util/vecmath.h
+// InvertBilinear, SphericalQuadArea; util/sampling.cpp:163-345 spherical rectangles;
+// util/transform.h:249-270 RotateFromTo)
+static bool OQuadratic(Float a, Float b, Float c, Float *t0, Float *t1) {
+    if (a == 0) {
+        if (b == 0) return false;
+        *t0 = *t1 = -c / b;
+        return true;
+    }
+    Float disc = DifferenceOfProducts(b, b, 4 * a, c);
+    if (disc < 0) return false;
+    Float root = std::sqrt(disc);
+    Float q = -0.5f * (b + std::copysign(root, b));
+    *t0 = q / a;
+    *t1 = c / q;
+    if (*t0 > *t1) std::swap(*t0, *t1);
+    return true;
+}
+static Float ODet3(const Float m[3][3]) {
+    Float minor12 = DifferenceOfProducts(m[1][1], m[2][2], m[1][2], m[2][1]);
+    Float minor02 = DifferenceOfProducts(m[1][0], m[2][2], m[1][2], m[2][0]);
+    Float minor01 = DifferenceOfProducts(m[1][0], m[2][1], m[1][1], m[2][0]);
+    return std::fma(m[0][2], minor01, DifferenceOfProducts(m[0][0], minor12, m[0][1], minor02));
+}
+static Vec OLerp(Float t, Vec a, Vec b) { return (1 - t) * a + t * b; }
+static Float OSphericalQuadArea(Vec a, Vec b, Vec c, Vec d) {
+    Vec axb = Cross(a, b), bxc = Cross(b, c), cxd = Cross(c, d), dxa = Cross(d, a);
+    if (LengthSquared(axb) == 0 || LengthSquared(bxc) == 0 || LengthSquared(cxd) == 0 || LengthSquared(dxa) == 0) return 0;
+    axb = Normalize(axb), bxc = Normalize(bxc), cxd = Normalize(cxd), dxa = Normalize(dxa);
+    Float al = AngleBetween(dxa, -axb), be = AngleBetween(axb, -bxc), ga = AngleBetween(bxc, -cxd), de = AngleBetween(cxd, -dxa);
+    return std::abs(al + be + ga + de - 2 * Pi);
+}
+struct ORectFrame {  // Frame::FromXY(ex / |ex|, ey / |ey|), z flipped toward the rectangle
+    Vec x, y, z;
+    Float x0, y0, z0, x1, y1, exl, eyl;
+    ORectFrame(Vec pRef, Vec s, Vec ex, Vec ey) {
+        exl = Length(ex), eyl = Length(ey);
+        x = ex / exl;
+        y = ey / eyl;
+        z = Cross(x, y);
+        Vec d = s - pRef;
+        x0 = Dot(d, x);
+        y0 = Dot(d, y);
+        z0 = Dot(d, z);
+        if (z0 > 0) {
+            z = -z;
+            z0 *= -1;
+        }
+        x1 = x0 + exl;
+        y1 = y0 + eyl;
+    }
+    void Angles(Vec *n0, Vec *n2, Float g[4]) const {
+        Vec v00(x0, y0, z0), v01(x0, y1, z0), v10(x1, y0, z0), v11(x1, y1, z0);
+        Vec a = Normalize(Cross(v00, v10)), b = Normalize(Cross(v10, v11)), c = Normalize(Cross(v11, v01)),
+            d = Normalize(Cross(v01, v00));
+        g[0] = AngleBetween(-a, b);
+        g[1] = AngleBetween(-b, c);
+        g[2] = AngleBetween(-c, d);
+        g[3] = AngleBetween(-d, a);
+        *n0 = a;
+        *n2 = c;
+    }
+};
+static Vec OSampleSphericalRectangle(Vec pRef, Vec s, Vec ex, Vec ey, Float u0, Float u1, Float *pdf) {
+    ORectFrame R(pRef, s, ex, ey);
+    Vec n0, n2;
+    Float g[4];
+    R.Angles(&n0, &n2, g);
+    Float solid = g[0] + g[1] + g[2] + g[3] - 2 * Pi;
+    if (solid <= 0) {
+        *pdf = 0;
+        return s + u0 * ex + u1 * ey;
+    }
+    *pdf = std::max<Float>(0, 1 / solid);
+    if (solid < 1e-3f) return s + u0 * ex + u1 * ey;
+    Float b0 = n0.z, b1 = n2.z;
+    Float au = u0 * (g[0] + g[1] - 2 * Pi) + (u0 - 1) * (g[2] + g[3]);
+    Float fu = (CRCos(au) * b0 - b1) / CRSin(au);
+    Float cu = std::copysign(1 / std::sqrt(Sqr(fu) + Sqr(b0)), fu);
+    cu = Clamp(cu, -OneMinusEpsilon, OneMinusEpsilon);
+    Float xu = Clamp(-(cu * R.z0) / SafeSqrt(1 - Sqr(cu)), R.x0, R.x1);
+    Float dd = std::sqrt(Sqr(xu) + Sqr(R.z0));
+    Float h0 = R.y0 / std::sqrt(Sqr(dd) + Sqr(R.y0)), h1 = R.y1 / std::sqrt(Sqr(dd) + Sqr(R.y1));
+    Float hv = h0 + u1 * (h1 - h0), hvsq = Sqr(hv);
+    Float yv = (hvsq < 1 - 1e-6f) ? (hv * dd) / std::sqrt(1 - hvsq) : R.y1;
+    return pRef + (R.x * xu + R.y * yv + R.z * R.z0);
+}
+static void OInvertSphericalRectangle(Vec pRef, Vec s, Vec ex, Vec ey, Vec pRect, Float *ru0, Float *ru1) {
+    ORectFrame R(pRef, s, ex, ey);
+    Vec n0, n2;
+    Float g[4];
+    R.Angles(&n0, &n2, g);
+    Float b0 = n0.z, b1 = n2.z, b0sq = Sqr(b0);
+    Float solid = double(g[0]) + double(g[1]) + double(g[2]) + double(g[3]) - 2. * Pi;
+    if (solid < 1e-3f) {
+        Vec pq = pRect - s;
+        *ru0 = Dot(pq, ex) / LengthSquared(ex);
+        *ru1 = Dot(pq, ey) / LengthSquared(ey);
+        return;
+    }
+    Vec v = pRect - pRef;
+    Float xu = Clamp(Dot(v, R.x), R.x0, R.x1), yv = Dot(v, R.y);
+    if (xu == 0) xu = 1e-10f;
+    Float z0sq = Sqr(R.z0);
+    Float fusq = (1 + z0sq / Sqr(xu)) - b0sq;
+    Float fu = std::copysign(std::sqrt(fusq), xu);
+    Float sq = SafeSqrt(DifferenceOfProducts(b0, b0, b1, b1) + fusq);
+    Float au = CRATan2(-(b1 * fu) - std::copysign(b0 * sq, fu * b0), b0 * b1 - sq * std::abs(fu));
+    if (au > 0) au -= 2 * Pi;
+    if (fu == 0) au = Pi;
+    Float u0 = (au + g[2] + g[3]) / solid;
+    Float ddsq = Sqr(xu) + z0sq, dd = std::sqrt(ddsq);
+    Float h0 = R.y0 / std::sqrt(ddsq + Sqr(R.y0)), h1 = R.y1 / std::sqrt(ddsq + Sqr(R.y1));
+    Float yvsq = Sqr(yv);
+    Float term = std::abs(h0 - h1) * std::sqrt(yvsq * (ddsq + yvsq)) / (ddsq + yvsq);
+    Float ua = (DifferenceOfProducts(h0, h0, h0, h1) - term) / Sqr(h0 - h1);
+    Float ub = (DifferenceOfProducts(h0, h0, h0, h1) + term) / Sqr(h0 - h1);
+    Float ha = Lerp(ua, h0, h1), hb = Lerp(ub, h0, h1);
+    Float ya = (ha * dd) / std::sqrt(1 - Sqr(ha)), yb = (hb * dd) / std::sqrt(1 - Sqr(hb));
+    *ru0 = Clamp(u0, 0, 1);
+    *ru1 = (std::abs(ya - yv) < std::abs(yb - yv)) ? ua : ub;
+}
+static Vec ORotateFromTo(Vec from, Vec to, Vec w) {
+    Vec refl;
+    if (std::abs(from.x) < 0.72f && std::abs(to.x) < 0.72f) refl = Vec(1, 0, 0);
+    else if (std::abs(from.y) < 0.72f && std::abs(to.y) < 0.72f) refl = Vec(0, 1, 0);
+    else refl = Vec(0, 0, 1);
+    Vec u = refl - from, v = refl - to;
+    Float m[3][3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            m[i][j] = ((i == j) ? 1 : 0) - 2 / Dot(u, u) * u[i] * u[j] - 2 / Dot(v, v) * v[i] * v[j] +
+                      4 * Dot(u, v) / (Dot(u, u) * Dot(v, v)) * v[i] * u[j];
+    return Vec(m[0][0] * w.x + m[0][1] * w.y + m[0][2] * w.z, m[1][0] * w.x + m[1][1] * w.y + m[1][2] * w.z,
+               m[2][0] * w.x + m[2][1] * w.y + m[2][2] * w.z);
+}
+
 struct OShape {
     int kind = 0, flags = 0;
     const float *r2o = nullptr, *o2r = nullptr;  // 3x4 row major
     Float a = 0, b = 0, c = 0, d = 0, e = 0, g = 0;
+    // bilinear patch: corners, corner uvs, vertex normals; the oracle's own area / rectangle test
+    Vec P[4], Nv[4];
+    Float UV[4][2];
+    bool rect = false;
+    Float patchArea = 0;
     void Init(const pbrt_scene_flat *f, int k) {
         const int32_t *info = f->shape_info + 8 * k;
         const float *pp = f->shape_params + 32 * k;
@@ -1066,9 +1208,259 @@ struct OShape {
         r2o = pp;
         o2r = pp + 12;
         a = pp[24], b = pp[25], c = pp[26], d = pp[27], e = pp[28], g = pp[29];
+        if (kind == 3) {
+            for (int i = 0; i < 4; ++i) {
+                P[i] = Vec(pp[3 * i], pp[3 * i + 1], pp[3 * i + 2]);
+                UV[i][0] = pp[12 + 2 * i];
+                UV[i][1] = pp[12 + 2 * i + 1];
+                const float *n = f->shape_normals + 12 * k + 3 * i;
+                Nv[i] = Vec(n[0], n[1], n[2]);
+            }
+            InitPatch();
+        }
     }
     bool sphere() const { return kind == 1; }
-    Float Area() const { return sphere() ? d * a * (c - b) : d * Float(0.5) * (Sqr(b) - Sqr(c)); }
+    bool patch() const { return kind == 3; }
+    bool flip() const { return ((flags & 1) != 0) != ((flags & 2) != 0); }
+    // BilinearPatch ctor (shapes.cpp:1041-1071) with IsRectangle (shapes.h:1511-1532)
+    void InitPatch() {
+        const Vec p00 = P[0], p10 = P[1], p01 = P[2], p11 = P[3];
+        rect = !(p00 == p01 || p01 == p11 || p11 == p10 || p10 == p00);
+        if (rect && AbsDotN(Normalize(Cross(p10 - p00, p01 - p00)), Normalize(p11 - p00)) > 1e-5f) rect = false;
+        if (rect) {
+            Vec pc = (p00 + p01 + p10 + p11) / 4;
+            Float d2[4] = {DistanceSquared(p00, pc), DistanceSquared(p01, pc), DistanceSquared(p10, pc), DistanceSquared(p11, pc)};
+            for (int i = 1; i < 4; ++i)
+                if (std::abs(d2[i] - d2[0]) / d2[0] > 1e-4f) rect = false;
+        }
+        if (rect) {
+            patchArea = Length(p00 - p01) * Length(p00 - p10);
+        } else {
+            Vec q[4][4];
+            for (int i = 0; i <= 3; ++i)
+                for (int j = 0; j <= 3; ++j) q[i][j] = OLerp(Float(i) / Float(3), OLerp(Float(j) / Float(3), p00, p01), OLerp(Float(j) / Float(3), p10, p11));
+            patchArea = 0;
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) patchArea += 0.5f * Length(Cross(q[i + 1][j + 1] - q[i][j], q[i + 1][j] - q[i][j + 1]));
+        }
+    }
+    Float Area() const {
+        if (patch()) return patchArea;
+        return sphere() ? d * a * (c - b) : d * Float(0.5) * (Sqr(b) - Sqr(c));
+    }
+    // IntersectBilinearPatch (shapes.h:1279-1347)
+    bool PatchIntersect(Vec o, Vec dir, Float tMax, Float *tHit, Float *uo, Float *vo) const {
+        const Vec p00 = P[0], p10 = P[1], p01 = P[2], p11 = P[3];
+        Float qa = Dot(Cross(p10 - p00, p01 - p11), dir);
+        Float qc = Dot(Cross(p00 - o, dir), p01 - p00);
+        Float qb = Dot(Cross(p10 - o, dir), p11 - p10) - (qa + qc);
+        Float u1, u2;
+        if (!OQuadratic(qa, qb, qc, &u1, &u2)) return false;
+        Float eps = gamma(10) * (MaxComp(Abs(o)) + MaxComp(Abs(dir)) + MaxComp(Abs(p00)) + MaxComp(Abs(p10)) +
+                                 MaxComp(Abs(p01)) + MaxComp(Abs(p11)));
+        Float t = tMax, u = 0, v = 0;
+        auto solve = [&](Float uu, Float *vv, Float *tt, Float *p2) {
+            Vec uo2 = OLerp(uu, p00, p10), ud = OLerp(uu, p01, p11) - uo2, deltao = uo2 - o, perp = Cross(dir, ud);
+            *p2 = LengthSquared(perp);
+            const Float mv[3][3] = {{deltao.x, dir.x, perp.x}, {deltao.y, dir.y, perp.y}, {deltao.z, dir.z, perp.z}};
+            const Float mt[3][3] = {{deltao.x, ud.x, perp.x}, {deltao.y, ud.y, perp.y}, {deltao.z, ud.z, perp.z}};
+            *vv = ODet3(mv);
+            *tt = ODet3(mt);
+        };
+        if (0 <= u1 && u1 <= 1) {
+            Float v1, t1, p2;
+            solve(u1, &v1, &t1, &p2);
+            if (t1 > p2 * eps && 0 <= v1 && v1 <= p2) {
+                u = u1;
+                v = v1 / p2;
+                t = t1 / p2;
+            }
+        }
+        if (0 <= u2 && u2 <= 1 && u2 != u1) {
+            Float v2, t2, p2;
+            solve(u2, &v2, &t2, &p2);
+            t2 /= p2;
+            if (0 <= v2 && v2 <= p2 && t > t2 && t2 > eps) {
+                t = t2;
+                u = u2;
+                v = v2 / p2;
+            }
+        }
+        if (t >= tMax) return false;
+        *tHit = t;
+        *uo = u;
+        *vo = v;
+        return true;
+    }
+    // BilinearPatch::InteractionFromIntersection (shapes.h:1396-1497)
+    Interaction PatchSurface(Float u, Float v) const {
+        const Vec p00 = P[0], p10 = P[1], p01 = P[2], p11 = P[3];
+        Vec p = OLerp(u, OLerp(v, p00, p01), OLerp(v, p10, p11));
+        Vec dpdu = OLerp(v, p10, p11) - OLerp(v, p00, p01), dpdv = OLerp(u, p01, p11) - OLerp(u, p00, p10);
+        Float st[2] = {u, v};
+        if (flags & 4) {
+            Float dstdu[2], dstdv[2];
+            for (int j = 0; j < 2; ++j) {
+                st[j] = Lerp(u, Lerp(v, UV[0][j], UV[2][j]), Lerp(v, UV[1][j], UV[3][j]));
+                dstdu[j] = Lerp(v, UV[1][j], UV[3][j]) - Lerp(v, UV[0][j], UV[2][j]);
+                dstdv[j] = Lerp(u, UV[2][j], UV[3][j]) - Lerp(u, UV[0][j], UV[1][j]);
+            }
+            Float duds = std::abs(dstdu[0]) < 1e-8f ? 0 : 1 / dstdu[0];
+            Float dvds = std::abs(dstdv[0]) < 1e-8f ? 0 : 1 / dstdv[0];
+            Float dudt = std::abs(dstdu[1]) < 1e-8f ? 0 : 1 / dstdu[1];
+            Float dvdt = std::abs(dstdv[1]) < 1e-8f ? 0 : 1 / dstdv[1];
+            Vec dpds = dpdu * duds + dpdv * dvds, dpdt = dpdu * dudt + dpdv * dvdt;
+            if (Cross(dpds, dpdt) != Vec(0, 0, 0)) {
+                if (Dot(Cross(dpdu, dpdv), Cross(dpds, dpdt)) < 0) dpdt = -dpdt;
+                dpdu = dpds;
+                dpdv = dpdt;
+            }
+        }
+        Interaction si;
+        Point3fi(p, gamma(6) * (Abs(p00) + Abs(p01) + Abs(p10) + Abs(p11)), &si.p, &si.err);
+        Vec n = Normalize(Cross(dpdu, dpdv));
+        if (flip()) n = -n;
+        si.n = si.ns = n;
+        si.dpdu = si.dpdus = dpdu;
+        si.dpdv = dpdv;
+        si.uv[0] = st[0];
+        si.uv[1] = st[1];
+        if (flags & 8) {
+            Vec ns = OLerp(u, OLerp(v, Nv[0], Nv[2]), OLerp(v, Nv[1], Nv[3]));
+            if (LengthSquared(ns) > 0) {
+                ns = Normalize(ns);
+                Vec sd = ORotateFromTo(Normalize(si.n), ns, dpdu), sv = ORotateFromTo(Normalize(si.n), ns, dpdv);
+                si.ns = ns;
+                if (DotN(si.n, ns) < 0) si.n = -si.n;  // SetShadingGeometry(..., true)
+                while (LengthSquared(sd) > 1e16f || LengthSquared(sv) > 1e16f) {
+                    sd = sd / 1e8f;
+                    sv = sv / 1e8f;
+                }
+                si.dpdus = sd;
+            }
+        }
+        return si;
+    }
+    Vec PatchNormalAt(Vec n, Float u, Float v) const {
+        if (flags & 8) {
+            Vec ns = OLerp(u, OLerp(v, Nv[0], Nv[2]), OLerp(v, Nv[1], Nv[3]));
+            return DotN(n, ns) < 0 ? -n : n;
+        }
+        return flip() ? -n : n;
+    }
+    void PatchWeights(Float w[4]) const {
+        const Vec p00 = P[0], p10 = P[1], p01 = P[2], p11 = P[3];
+        w[0] = Length(Cross(p10 - p00, p01 - p00));
+        w[1] = Length(Cross(p10 - p00, p11 - p10));
+        w[2] = Length(Cross(p01 - p00, p11 - p01));
+        w[3] = Length(Cross(p11 - p10, p11 - p01));
+    }
+    // BilinearPatch::Sample(u) (shapes.cpp:1158-1217)
+    bool PatchSampleArea(Float u0, Float u1, ShapeSample *ss) const {
+        Float pdf = 1, u = u0, v = u1;
+        if (!rect) {
+            Float w[4];
+            PatchWeights(w);
+            SampleBilinear(u0, u1, w, &u, &v);
+            pdf = BilinearPDF(u, v, w);
+        }
+        Vec pu0 = OLerp(v, P[0], P[2]), pu1 = OLerp(v, P[1], P[3]);
+        Vec p = OLerp(u, pu0, pu1), dpdu = pu1 - pu0, dpdv = OLerp(u, P[2], P[3]) - OLerp(u, P[0], P[1]);
+        if (LengthSquared(dpdu) == 0 || LengthSquared(dpdv) == 0) return false;
+        ss->n = PatchNormalAt(Normalize(Cross(dpdu, dpdv)), u, v);
+        Point3fi(p, gamma(6) * (Abs(P[0]) + Abs(P[2]) + Abs(P[1]) + Abs(P[3])), &ss->p, &ss->err);
+        ss->pdf = pdf / Length(Cross(dpdu, dpdv));
+        return true;
+    }
+    // BilinearPatch::Sample(ctx, u) and PDF(ctx, wi) (shapes.cpp:1257-1372)
+    bool PatchSample(Vec cp, Vec cns, Float u0, Float u1, ShapeSample *out) const {
+        Vec v00 = Normalize(P[0] - cp), v10 = Normalize(P[1] - cp), v01 = Normalize(P[2] - cp), v11 = Normalize(P[3] - cp);
+        if (!rect || OSphericalQuadArea(v00, v10, v11, v01) <= 1e-4f) {
+            ShapeSample ss;
+            if (!PatchSampleArea(u0, u1, &ss)) return false;
+            Vec wi = ss.p - cp;
+            if (LengthSquared(wi) == 0) return false;
+            wi = Normalize(wi);
+            ss.pdf /= AbsDotN(ss.n, -wi) / DistanceSquared(cp, ss.p);
+            if (std::isinf(ss.pdf)) return false;
+            *out = ss;
+            return true;
+        }
+        Float pdf = 1, uu = u0, vv = u1;
+        if (cns != Vec(0, 0, 0)) {
+            Float w[4] = {std::max<Float>(0.01f, AbsDotN(cns, v00)), std::max<Float>(0.01f, AbsDotN(cns, v10)),
+                          std::max<Float>(0.01f, AbsDotN(cns, v01)), std::max<Float>(0.01f, AbsDotN(cns, v11))};
+            SampleBilinear(u0, u1, w, &uu, &vv);
+            pdf *= BilinearPDF(uu, vv, w);
+        }
+        Vec eu = P[1] - P[0], ev = P[2] - P[0];
+        Float qpdf;
+        Vec p = OSampleSphericalRectangle(cp, P[0], eu, ev, uu, vv, &qpdf);
+        pdf *= qpdf;
+        Float su = Dot(p - P[0], eu) / DistanceSquared(P[1], P[0]), sv = Dot(p - P[0], ev) / DistanceSquared(P[2], P[0]);
+        out->n = PatchNormalAt(Normalize(Cross(eu, ev)), su, sv);
+        out->p = p;
+        out->err = Vec(0, 0, 0);
+        out->pdf = pdf;
+        return true;
+    }
+    Float PatchPDF(Vec cp, Vec cpErr, Vec cn, Vec cns, Vec wi) const {
+        Vec ro = OffsetRayOrigin(cp, cpErr, cn, wi);
+        Float th, iu, iv;
+        if (!PatchIntersect(ro, wi, Infinity, &th, &iu, &iv)) return 0;
+        Interaction si = PatchSurface(iu, iv);
+        Vec v00 = Normalize(P[0] - cp), v10 = Normalize(P[1] - cp), v01 = Normalize(P[2] - cp), v11 = Normalize(P[3] - cp);
+        if (!rect || OSphericalQuadArea(v00, v10, v11, v01) <= 1e-4f) {
+            Float u = si.uv[0], v = si.uv[1];
+            if (flags & 4) {
+                // InvertBilinear(uv, {uv00, uv10, uv01, uv11}): a = uv00, b = uv10, c = uv11, d = uv01
+                const Float *A = UV[0], *B = UV[1], *C = UV[3], *D = UV[2];
+                Float ee[2] = {B[0] - A[0], B[1] - A[1]}, ff[2] = {D[0] - A[0], D[1] - A[1]};
+                Float gg[2] = {(A[0] - B[0]) + (C[0] - D[0]), (A[1] - B[1]) + (C[1] - D[1])}, hh[2] = {u - A[0], v - A[1]};
+                auto cr = [](const Float *x, const Float *y) { return DifferenceOfProducts(x[0], y[1], x[1], y[0]); };
+                Float k2 = cr(gg, ff), k1 = cr(ee, ff) + cr(hh, gg), k0 = cr(hh, ee);
+                if (std::abs(k2) < 0.001f) {
+                    u = std::abs(ee[0] * k1 - gg[0] * k0) < 1e-5f ? (hh[1] * k1 + ff[1] * k0) / (ee[1] * k1 - gg[1] * k0)
+                                                                 : (hh[0] * k1 + ff[0] * k0) / (ee[0] * k1 - gg[0] * k0);
+                    v = -k0 / k1;
+                } else {
+                    Float w0, w1;
+                    if (!OQuadratic(k2, k1, k0, &w0, &w1)) {
+                        u = v = 0;
+                    } else {
+                        Float uu = (hh[0] - ff[0] * w0) / (ee[0] + gg[0] * w0);
+                        if (uu < 0 || uu > 1 || w0 < 0 || w0 > 1) {
+                            u = (hh[0] - ff[0] * w1) / (ee[0] + gg[0] * w1);
+                            v = w1;
+                        } else {
+                            u = uu;
+                            v = w0;
+                        }
+                    }
+                }
+            }
+            Float pdf = 1;
+            if (!rect) {
+                Float w[4];
+                PatchWeights(w);
+                pdf = BilinearPDF(u, v, w);
+            }
+            Vec pu0 = OLerp(v, P[0], P[2]), pu1 = OLerp(v, P[1], P[3]);
+            Vec dpdu = pu1 - pu0, dpdv = OLerp(u, P[2], P[3]) - OLerp(u, P[0], P[1]);
+            pdf = pdf / Length(Cross(dpdu, dpdv));
+            pdf = pdf * (DistanceSquared(cp, si.p) / AbsDotN(si.n, -wi));
+            return std::isinf(pdf) ? 0 : pdf;
+        }
+        Float pdf = 1 / OSphericalQuadArea(v00, v10, v11, v01);
+        if (cns != Vec(0, 0, 0)) {
+            Float w[4] = {std::max<Float>(0.01f, AbsDotN(cns, v00)), std::max<Float>(0.01f, AbsDotN(cns, v10)),
+                          std::max<Float>(0.01f, AbsDotN(cns, v01)), std::max<Float>(0.01f, AbsDotN(cns, v11))};
+            Float su, sv;
+            OInvertSphericalRectangle(cp, P[0], P[1] - P[0], P[2] - P[0], si.p, &su, &sv);
+            return BilinearPDF(su, sv, w) * pdf;
+        }
+        return pdf;
+    }
     // Transform::operator() on points / vectors / normals (util/transform.h:133-176, 272-334)
     static void XPointI(const float *m, const OInterval in[3], OInterval out[3]) {
         const Float x = in[0].Mid(), y = in[1].Mid(), z = in[2].Mid();
@@ -1107,6 +1499,12 @@ struct OShape {
     }
     // BasicIntersect -> tHit and the object-space hit
     bool Intersect(Vec ro, Vec rd, Float tMax, Float *tHit, Vec *pObj) const {
+        if (patch()) {
+            Float u, v;
+            if (!PatchIntersect(ro, rd, tMax, tHit, &u, &v)) return false;
+            *pObj = Vec(u, v, 0);
+            return true;
+        }
         OInterval oi[3], di[3];
         const OInterval ro3[3] = {OInterval(ro.x), OInterval(ro.y), OInterval(ro.z)};
         XPointI(r2o, ro3, oi);
@@ -1167,6 +1565,11 @@ struct OShape {
     }
     // InteractionFromIntersection + Transform::operator()(SurfaceInteraction)
     Interaction Surface(Vec pHit, Vec rd) const {
+        if (patch()) {
+            Interaction si = PatchSurface(pHit.x, pHit.y);
+            si.wo = Normalize(-rd);
+            return si;
+        }
         const Float phi = Phi(pHit);
         Vec dpdu, dpdv, pErr;
         Float u, v;
@@ -1242,7 +1645,8 @@ struct OShape {
         return ss;
     }
     // Shape::Sample(ctx, u), solid angle (false: {})
-    bool Sample(Vec cp, Vec cpErr, Vec cn, Float u0, Float u1, ShapeSample *out) const {
+    bool Sample(Vec cp, Vec cpErr, Vec cn, Float u0, Float u1, ShapeSample *out, Vec cns = Vec(0, 0, 0)) const {
+        if (patch()) return PatchSample(cp, cns, u0, u1, out);
         if (sphere()) {
             const Vec pc = XP(o2r, Vec(0, 0, 0));
             const Vec po = OffsetRayOrigin(cp, cpErr, cn, pc - cp);
@@ -1280,7 +1684,8 @@ struct OShape {
         return true;
     }
     // Shape::PDF(ctx, wi)
-    Float PDF(Vec cp, Vec cpErr, Vec cn, Vec wi) const {
+    Float PDF(Vec cp, Vec cpErr, Vec cn, Vec wi, Vec cns = Vec(0, 0, 0)) const {
+        if (patch()) return PatchPDF(cp, cpErr, cn, cns, wi);
         if (sphere()) {
             const Vec pc = XP(o2r, Vec(0, 0, 0));
             const Vec po = OffsetRayOrigin(cp, cpErr, cn, pc - cp);
@@ -1301,6 +1706,13 @@ struct OShape {
         return pdf;
     }
     void Bounds(Vec *mn, Vec *mx) const {
+        if (patch()) {
+            *mn = Vec(std::min(std::min(P[0].x, P[2].x), std::min(P[1].x, P[3].x)), std::min(std::min(P[0].y, P[2].y), std::min(P[1].y, P[3].y)),
+                      std::min(std::min(P[0].z, P[2].z), std::min(P[1].z, P[3].z)));
+            *mx = Vec(std::max(std::max(P[0].x, P[2].x), std::max(P[1].x, P[3].x)), std::max(std::max(P[0].y, P[2].y), std::max(P[1].y, P[3].y)),
+                      std::max(std::max(P[0].z, P[2].z), std::max(P[1].z, P[3].z)));
+            return;
+        }
         const Vec lo = sphere() ? Vec(-a, -a, b) : Vec(-b, -b, a), hi = sphere() ? Vec(a, a, c) : Vec(b, b, a);
         *mn = Vec(Infinity, Infinity, Infinity);
         *mx = -*mn;
@@ -1617,7 +2029,30 @@ static std::vector<std::pair<int, LB>> SceneLightBounds(const pbrt_scene_flat *f
             Float phi = denseMax(f->light_spectrum[i]);
             phi *= f->light_scale[i] * sh.Area() * Pi;
             Cone nb(Vec(0, 0, 1), -1);  // DirectionCone::EntireSphere
-            if (!sh.sphere()) {
+            if (sh.patch()) {
+                // BilinearPatch::NormalBounds (shapes.cpp:1083-1129)
+                const Vec p00 = sh.P[0], p10 = sh.P[1], p01 = sh.P[2], p11 = sh.P[3];
+                const bool hasN = (sh.flags & 8) != 0, flip = sh.flip();
+                auto ff = [](Vec v, Vec n) { return DotN(v, n) < 0 ? -v : v; };
+                if (p00 == p10 || p10 == p11 || p11 == p01 || p01 == p00) {
+                    Vec du = OLerp(0.5f, p10, p11) - OLerp(0.5f, p00, p01), dv = OLerp(0.5f, p01, p11) - OLerp(0.5f, p00, p10);
+                    Vec n = Normalize(Cross(du, dv));
+                    if (hasN) n = ff(n, (sh.Nv[0] + sh.Nv[1] + sh.Nv[2] + sh.Nv[3]) / 4);
+                    else if (flip) n = -n;
+                    nb = Cone(n, 1);
+                } else {
+                    Vec n00 = Normalize(Cross(p10 - p00, p01 - p00)), n10 = Normalize(Cross(p11 - p10, p00 - p10));
+                    Vec n01 = Normalize(Cross(p00 - p01, p11 - p01)), n11 = Normalize(Cross(p01 - p11, p10 - p11));
+                    if (hasN) {
+                        n00 = ff(n00, sh.Nv[0]), n10 = ff(n10, sh.Nv[1]), n01 = ff(n01, sh.Nv[2]), n11 = ff(n11, sh.Nv[3]);
+                    } else if (flip) {
+                        n00 = -n00, n10 = -n10, n01 = -n01, n11 = -n11;
+                    }
+                    Vec n = Normalize(n00 + n10 + n01 + n11);
+                    Float ct = std::min(std::min(Dot(n, n00), Dot(n, n01)), std::min(Dot(n, n10), Dot(n, n11)));
+                    nb = Cone(n, Clamp(ct, -1, 1));
+                }
+            } else if (!sh.sphere()) {
                 Vec n = OShape::XN(sh.r2o, Vec(0, 0, 1));
                 if (sh.flags & 1) n = -n;
                 nb = Cone(n, 1);
@@ -3776,12 +4211,12 @@ struct Renderer {
         // Shape::Sample(ctx, u) / PDF(ctx, wi) of area light li (a triangle, sphere or disk)
         auto sampleArea = [&](int li, Vec ref, Vec refErr, Vec refN, Vec refNs, Float u0, Float u1, ShapeSample *ss) {
             const int lp = f->light_prim[li];
-            if (lp >= f->n_triangles) return S.shapes[lp - f->n_triangles].Sample(ref, refErr, refN, u0, u1, ss);
+            if (lp >= f->n_triangles) return S.shapes[lp - f->n_triangles].Sample(ref, refErr, refN, u0, u1, ss, refNs);
             return TriangleSample(S.P(lp, 0), S.P(lp, 1), S.P(lp, 2), f->tri_flip[lp], ref, refNs, u0, u1, ss, S.Attr(lp));
         };
         auto pdfArea = [&](int li, Vec ref, Vec refErr, Vec refN, Vec refNs, Vec wi) {
             const int lp = f->light_prim[li];
-            if (lp >= f->n_triangles) return S.shapes[lp - f->n_triangles].PDF(ref, refErr, refN, wi);
+            if (lp >= f->n_triangles) return S.shapes[lp - f->n_triangles].PDF(ref, refErr, refN, wi, refNs);
             return TrianglePDF(S.P(lp, 0), S.P(lp, 1), S.P(lp, 2), f->tri_flip[lp], ref, refErr, refN, refNs, wi, S.Attr(lp));
         };
         // shadow rays: plain occlusion, or TraceTransmittance (wavefront/intersect.h:164-274)
@@ -4474,6 +4909,7 @@ int oracle_shape_eval(const pbrt_scene_flat *flat, int shape, const float *rays,
         float *o = out + 40 * (size_t)i;
         std::fill(o, o + 40, 0.f);
         const Vec ro(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]), rd(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
+        const Vec cns = (i & 1) ? Normalize(-rd) : Vec(0, 0, 0);
         Float th;
         Vec pObj;
         if (sh.Intersect(ro, rd, Infinity, &th, &pObj)) {
@@ -4485,7 +4921,7 @@ int oracle_shape_eval(const pbrt_scene_flat *flat, int shape, const float *rays,
                 for (int j = 0; j < (k == 7 ? 2 : 3); ++j) o[2 + 3 * k + j] = v[k][j];
         }
         ShapeSample ss;
-        if (sh.Sample(ro, Vec(0, 0, 0), Vec(0, 0, 0), u[2 * i], u[2 * i + 1], &ss)) {
+        if (sh.Sample(ro, Vec(0, 0, 0), Vec(0, 0, 0), u[2 * i], u[2 * i + 1], &ss, cns)) {
             o[26] = 1;
             for (int j = 0; j < 3; ++j) {
                 o[27 + j] = ss.p[j];
@@ -4494,7 +4930,7 @@ int oracle_shape_eval(const pbrt_scene_flat *flat, int shape, const float *rays,
             }
             o[36] = ss.pdf;
         }
-        o[37] = sh.PDF(ro, Vec(0, 0, 0), Vec(0, 0, 0), rd);
+        o[37] = sh.PDF(ro, Vec(0, 0, 0), Vec(0, 0, 0), rd, cns);
     }
     return 0;
 }

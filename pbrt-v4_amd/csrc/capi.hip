@@ -251,7 +251,7 @@ struct pbrt_scene {
         matSpectra, plOffsets, infDistant, uniformOrder;
     std::vector<float> deltaLights;
     std::vector<int32_t> infImage, envInfo, shapeInfo;
-    std::vector<float> shapeParams;
+    std::vector<float> shapeParams, shapeNormals;
     std::vector<float> envXform, envRgb;
     std::vector<uint64_t> envOffset;
     TexTables tex;
@@ -261,11 +261,13 @@ struct pbrt_scene {
         for (auto &l : s.infiniteLights) infImage.push_back(l.image);
         shapeInfo.clear();
         shapeParams.clear();
+        shapeNormals.clear();
         for (const AnalyticShapeDesc &a : s.shapes) {
             shapeInfo.insert(shapeInfo.end(), {a.dev.kind, a.dev.flags, a.material, a.light, a.medium[0], a.medium[1], 0, 0});
             shapeParams.insert(shapeParams.end(), a.dev.r2o, a.dev.r2o + 12);
             shapeParams.insert(shapeParams.end(), a.dev.o2r, a.dev.o2r + 12);
             shapeParams.insert(shapeParams.end(), {a.dev.a, a.dev.b, a.dev.c, a.dev.d, a.dev.e, a.dev.f, 0.f, 0.f});
+            shapeNormals.insert(shapeNormals.end(), a.normals.begin(), a.normals.end());
         }
         envInfo.clear();
         envXform.clear();
@@ -425,6 +427,7 @@ struct pbrt_context {
     DevBuf<int> infImage;
     DevBuf<DeviceShape> shapes;
     DevBuf<ShapeBVHNode> shapeNodes;
+    DevBuf<float> shapeN;
     DevBuf<EnvCoef> envCoef;
     DevBuf<float> envDist;
     DevBuf<DeviceEnvLight> envLights;
@@ -599,6 +602,9 @@ static void BuildDevice(pbrt_context *c) {
         for (const AnalyticShapeDesc &a : s.shapes) ds.push_back(a.dev);
         c->shapes.Upload(ds);
         c->shapeNodes.Upload(BuildShapeBVH(s.shapes));
+        std::vector<float> sn((size_t)std::max(nsh, 1) * 12, 0.f);
+        for (int k = 0; k < nsh; ++k) std::copy(s.shapes[k].normals.begin(), s.shapes[k].normals.end(), sn.begin() + 12 * k);
+        c->shapeN.Upload(sn);
     }
     // vertex normals / uv per leaf triangle (only when some mesh has them)
     if (std::any_of(s.triShade.begin(), s.triShade.end(), [](uint8_t f) { return f != 0; })) {
@@ -892,6 +898,7 @@ static void BuildDevice(pbrt_context *c) {
     S.nShapes = nsh;
     S.shapes = c->shapes.p;
     S.shapeNodes = c->shapeNodes.p;
+    S.shapeN = c->shapeN.p;
     S.triShade = (const float4 *)c->triShade.p;
     S.matCoeffs = (const float4 *)c->matCoeffs.p;
     S.matConstant = c->matConstant.p;
@@ -1603,6 +1610,7 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
     f->n_shapes = (int)scene->desc.shapes.size();
     f->shape_info = scene->shapeInfo.data();
     f->shape_params = scene->shapeParams.data();
+    f->shape_normals = scene->shapeNormals.data();
     f->uniform_order = scene->uniformOrder.data();
     f->scene_radius = s.sceneRadius;
     {
@@ -2141,14 +2149,17 @@ int pbrt_debug_shape_eval(const pbrt_scene *scene, int shape, const float *rays,
         const SceneDesc &s = scene->desc;
         if (shape < 0 || shape >= (int)s.shapes.size()) return Fail("shape index out of range");
         const DeviceShape &d = s.shapes[shape].dev;
+        const float *N = s.shapes[shape].normals.data();
         for (int i = 0; i < n; ++i) {
             float *o = out + 40 * (size_t)i;
             std::fill(o, o + 40, 0.f);
             const V3 ro(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]), rd(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
+            // the sampling context's shading normal: every other row uses -d (patch cosine warp)
+            const V3 cns = (i & 1) ? Normalize(-rd) : V3(0, 0, 0);
             float th;
             V3 pObj;
             if (ShapeIntersect(d, ro, rd, kInfinity, &th, &pObj)) {
-                const TriSurface si = ShapeSurface(d, pObj);
+                const TriSurface si = ShapeSurface(d, pObj, N);
                 const V3 v[8] = {pObj, si.p, si.pErr, si.n, si.ns, si.dpdu, si.dpdv, V3(si.uv[0], si.uv[1], 0)};
                 o[0] = 1;
                 o[1] = th;
@@ -2156,7 +2167,7 @@ int pbrt_debug_shape_eval(const pbrt_scene *scene, int shape, const float *rays,
                     for (int j = 0; j < (k == 7 ? 2 : 3); ++j) o[2 + 3 * k + j] = v[k][j];
             }
             ShapeSamplePt ss;
-            if (ShapeSampleSolidAngle(d, ro, V3(0, 0, 0), V3(0, 0, 0), u[2 * i], u[2 * i + 1], &ss)) {
+            if (ShapeSampleSolidAngle(d, ro, V3(0, 0, 0), V3(0, 0, 0), u[2 * i], u[2 * i + 1], &ss, N, cns)) {
                 o[26] = 1;
                 for (int j = 0; j < 3; ++j) {
                     o[27 + j] = ss.p[j];
@@ -2165,7 +2176,7 @@ int pbrt_debug_shape_eval(const pbrt_scene *scene, int shape, const float *rays,
                 }
                 o[36] = ss.pdf;
             }
-            o[37] = ShapePDFSolidAngle(d, ro, V3(0, 0, 0), V3(0, 0, 0), rd);
+            o[37] = ShapePDFSolidAngle(d, ro, V3(0, 0, 0), V3(0, 0, 0), rd, N, cns);
         }
         return 0;
     } catch (const std::exception &e) {

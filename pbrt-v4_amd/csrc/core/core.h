@@ -1794,13 +1794,14 @@ PHD V3 XfPt(const float *m, V3 p) {
 }
 
 // Sphere and Disk (shapes.h:106-571): affine renderFromObject (o2r) and objectFromRender (r2o)
-enum ShapeKindT { kShapeSphereT = 1, kShapeDiskT = 2 };
+enum ShapeKindT { kShapeSphereT = 1, kShapeDiskT = 2, kShapeBilinearT = 3 };
 struct alignas(16) DeviceShape {
     float r2o[12], o2r[12];
     // sphere: radius, zMin, zMax, phiMax, thetaZMin, thetaZMax; disk: height, radius,
-    // innerRadius, phiMax
+    // innerRadius, phiMax; bilinear patch: area, isRectangle (render-space corners p00 p10 p01
+    // p11 in r2o, their uv in o2r[0..7], vertex normals in a side array)
     float a, b, c, d, e, f;
-    int kind, flags;  // flags: bit0 reverseOrientation, bit1 transformSwapsHandedness
+    int kind, flags;  // flags: bit0 reverseOrientation, bit1 transformSwapsHandedness, bit2 uv, bit3 N
 };
 static_assert(sizeof(DeviceShape) == 128, "DeviceShape must be 128 bytes");
 // binary BVH over the analytic shapes (host-built, median split): count 0 = interior node whose
@@ -1809,7 +1810,348 @@ struct alignas(16) ShapeBVHNode {
     float lo[3], hi[3];
     int child, count;
 };
+// ---- bilinear patches (shapes.h:1272-1540, shapes.cpp:1041-1372)
+PHD V3 LerpV(float t, V3 a, V3 b) { return (1 - t) * a + t * b; }
+// Quadratic(float) (util/math.h:614-637)
+PHD bool QuadraticF(float a, float b, float c, float *t0, float *t1) {
+    if (a == 0) {
+        if (b == 0) return false;
+        *t0 = *t1 = -c / b;
+        return true;
+    }
+    const float discrim = DifferenceOfProducts(b, b, 4 * a, c);
+    if (discrim < 0) return false;
+    const float rootDiscrim = std::sqrt(discrim);
+    const float q = -0.5f * (b + std::copysign(rootDiscrim, b));
+    *t0 = q / a;
+    *t1 = c / q;
+    if (*t0 > *t1) {
+        const float t = *t0;
+        *t0 = *t1;
+        *t1 = t;
+    }
+    return true;
+}
+// Determinant(SquareMatrix<3>) (util/math.h:1420-1426), rows (a0 a1 a2) (b0 b1 b2) (c0 c1 c2)
+PHD float Det3(float a0, float a1, float a2, float b0, float b1, float b2, float c0, float c1, float c2) {
+    const float minor12 = DifferenceOfProducts(b1, c2, b2, c1);
+    const float minor02 = DifferenceOfProducts(b0, c2, b2, c0);
+    const float minor01 = DifferenceOfProducts(b0, c1, b1, c0);
+    return fmaf(a2, minor01, DifferenceOfProducts(a0, minor12, a1, minor02));
+}
+struct PatchVerts {
+    V3 p00, p10, p01, p11;
+};
+PHD PatchVerts PatchP(const DeviceShape &s) {
+    const float *q = s.r2o;
+    return PatchVerts{V3(q[0], q[1], q[2]), V3(q[3], q[4], q[5]), V3(q[6], q[7], q[8]), V3(q[9], q[10], q[11])};
+}
+// IntersectBilinearPatch (shapes.h:1279-1347): *u, *v the patch parameters
+PHD bool BilinearIntersect(const DeviceShape &s, V3 o, V3 d, float tMax, float *tHit, float *uo, float *vo) {
+    const PatchVerts P = PatchP(s);
+    const V3 p00 = P.p00, p10 = P.p10, p01 = P.p01, p11 = P.p11;
+    const float a = Dot(Cross(p10 - p00, p01 - p11), d);
+    const float c = Dot(Cross(p00 - o, d), p01 - p00);
+    const float b = Dot(Cross(p10 - o, d), p11 - p10) - (a + c);
+    float u1, u2;
+    if (!QuadraticF(a, b, c, &u1, &u2)) return false;
+    const float eps = gamma(10) * (MaxComponentValue(Abs(o)) + MaxComponentValue(Abs(d)) + MaxComponentValue(Abs(p00)) +
+                                   MaxComponentValue(Abs(p10)) + MaxComponentValue(Abs(p01)) + MaxComponentValue(Abs(p11)));
+    float t = tMax, u = 0, v = 0;
+    if (0 <= u1 && u1 <= 1) {
+        const V3 uo1 = LerpV(u1, p00, p10);
+        const V3 ud = LerpV(u1, p01, p11) - uo1;
+        const V3 deltao = uo1 - o;
+        const V3 perp = Cross(d, ud);
+        const float p2 = LengthSquared(perp);
+        const float v1 = Det3(deltao.x, d.x, perp.x, deltao.y, d.y, perp.y, deltao.z, d.z, perp.z);
+        const float t1 = Det3(deltao.x, ud.x, perp.x, deltao.y, ud.y, perp.y, deltao.z, ud.z, perp.z);
+        if (t1 > p2 * eps && 0 <= v1 && v1 <= p2) {
+            u = u1;
+            v = v1 / p2;
+            t = t1 / p2;
+        }
+    }
+    if (0 <= u2 && u2 <= 1 && u2 != u1) {
+        const V3 uo2 = LerpV(u2, p00, p10);
+        const V3 ud = LerpV(u2, p01, p11) - uo2;
+        const V3 deltao = uo2 - o;
+        const V3 perp = Cross(d, ud);
+        const float p2 = LengthSquared(perp);
+        const float v2 = Det3(deltao.x, d.x, perp.x, deltao.y, d.y, perp.y, deltao.z, d.z, perp.z);
+        float t2 = Det3(deltao.x, ud.x, perp.x, deltao.y, ud.y, perp.y, deltao.z, ud.z, perp.z);
+        t2 /= p2;
+        if (0 <= v2 && v2 <= p2 && t > t2 && t2 > eps) {
+            t = t2;
+            u = u2;
+            v = v2 / p2;
+        }
+    }
+    if (t >= tMax) return false;
+    *tHit = t;
+    *uo = u;
+    *vo = v;
+    return true;
+}
+// RotateFromTo(from, to) applied to a vector (util/transform.h:249-270)
+PHD V3 RotateFromToApply(V3 from, V3 to, V3 w) {
+    V3 refl;
+    if (std::fabs(from.x) < 0.72f && std::fabs(to.x) < 0.72f) refl = V3(1, 0, 0);
+    else if (std::fabs(from.y) < 0.72f && std::fabs(to.y) < 0.72f) refl = V3(0, 1, 0);
+    else refl = V3(0, 0, 1);
+    const V3 u = refl - from, v = refl - to;
+    const float uu = Dot(u, u), vv = Dot(v, v), uv = Dot(u, v);
+    float r[3][3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            r[i][j] = ((i == j) ? 1 : 0) - 2 / uu * u[i] * u[j] - 2 / vv * v[i] * v[j] + 4 * uv / (uu * vv) * v[i] * u[j];
+    return V3(r[0][0] * w.x + r[0][1] * w.y + r[0][2] * w.z, r[1][0] * w.x + r[1][1] * w.y + r[1][2] * w.z,
+              r[2][0] * w.x + r[2][1] * w.y + r[2][2] * w.z);
+}
+PHD void PatchUV(const DeviceShape &s, int k, float *u, float *v) {
+    *u = s.o2r[2 * k];
+    *v = s.o2r[2 * k + 1];
+}
+// BilinearPatch::InteractionFromIntersection (shapes.h:1396-1497) without dndu/dndv; N: the
+// four vertex normals (render space, 12 floats) when the mesh has them
+PHD TriSurface BilinearSurface(const DeviceShape &s, const float *N, float uu, float vv) {
+    const PatchVerts P = PatchP(s);
+    const V3 p00 = P.p00, p10 = P.p10, p01 = P.p01, p11 = P.p11;
+    const V3 p = LerpV(uu, LerpV(vv, p00, p01), LerpV(vv, p10, p11));
+    V3 dpdu = LerpV(vv, p10, p11) - LerpV(vv, p00, p01);
+    V3 dpdv = LerpV(uu, p01, p11) - LerpV(uu, p00, p10);
+    float st[2] = {uu, vv};
+    if (s.flags & 4) {
+        float a[4][2];
+        for (int k = 0; k < 4; ++k) PatchUV(s, k, &a[k][0], &a[k][1]);  // uv00 uv10 uv01 uv11
+        float dstdu[2], dstdv[2];
+        for (int j = 0; j < 2; ++j) {
+            st[j] = Lerpf(uu, Lerpf(vv, a[0][j], a[2][j]), Lerpf(vv, a[1][j], a[3][j]));
+            dstdu[j] = Lerpf(vv, a[1][j], a[3][j]) - Lerpf(vv, a[0][j], a[2][j]);
+            dstdv[j] = Lerpf(uu, a[2][j], a[3][j]) - Lerpf(uu, a[0][j], a[1][j]);
+        }
+        const float duds = std::fabs(dstdu[0]) < 1e-8f ? 0 : 1 / dstdu[0];
+        const float dvds = std::fabs(dstdv[0]) < 1e-8f ? 0 : 1 / dstdv[0];
+        const float dudt = std::fabs(dstdu[1]) < 1e-8f ? 0 : 1 / dstdu[1];
+        const float dvdt = std::fabs(dstdv[1]) < 1e-8f ? 0 : 1 / dstdv[1];
+        const V3 dpds = dpdu * duds + dpdv * dvds;
+        V3 dpdt = dpdu * dudt + dpdv * dvdt;
+        const V3 cst = Cross(dpds, dpdt);
+        if (cst.x != 0 || cst.y != 0 || cst.z != 0) {
+            if (Dot(Cross(dpdu, dpdv), cst) < 0) dpdt = -dpdt;
+            dpdu = dpds;
+            dpdv = dpdt;
+        }
+    }
+    const V3 pAbsSum = Abs(p00) + Abs(p01) + Abs(p10) + Abs(p11);
+    TriSurface r;
+    ToPoint3fi(p, gamma(6) * pAbsSum, &r.p, &r.pErr);
+    V3 n = Normalize(Cross(dpdu, dpdv));
+    if (((s.flags & 1) != 0) != ((s.flags & 2) != 0)) n = -n;
+    r.n = n;
+    r.ns = n;
+    r.dpdu = r.dpdus = dpdu;
+    r.dpdv = dpdv;
+    r.uv[0] = st[0];
+    r.uv[1] = st[1];
+    if ((s.flags & 8) && N) {
+        const V3 n00(N[0], N[1], N[2]), n10(N[3], N[4], N[5]), n01(N[6], N[7], N[8]), n11(N[9], N[10], N[11]);
+        V3 ns = LerpV(uu, LerpV(vv, n00, n01), LerpV(vv, n10, n11));
+        if (LengthSquared(ns) > 0) {
+            ns = Normalize(ns);
+            V3 sd = RotateFromToApply(Normalize(r.n), ns, dpdu), sv = RotateFromToApply(Normalize(r.n), ns, dpdv);
+            // SetShadingGeometry(ns, r(dpdu), r(dpdv), ..., true) (interaction.h:194-214)
+            r.ns = ns;
+            r.n = FaceForwardN(r.n, ns);
+            while (LengthSquared(sd) > 1e16f || LengthSquared(sv) > 1e16f) {
+                sd = sd / 1e8f;
+                sv = sv / 1e8f;
+            }
+            r.dpdus = sd;
+        }
+    }
+    return r;
+}
+// the patch normal at (u, v) for sampling (shapes.cpp:1199-1208)
+PHD V3 PatchSampleNormal(const DeviceShape &s, const float *N, V3 n, float uu, float vv) {
+    if ((s.flags & 8) && N) {
+        const V3 n00(N[0], N[1], N[2]), n10(N[3], N[4], N[5]), n01(N[6], N[7], N[8]), n11(N[9], N[10], N[11]);
+        const V3 ns = LerpV(uu, LerpV(vv, n00, n01), LerpV(vv, n10, n11));
+        return FaceForwardN(n, ns);
+    }
+    if (((s.flags & 1) != 0) != ((s.flags & 2) != 0)) return -n;
+    return n;
+}
+// the bilinear warp's corner weights of a non-rectangular patch (shapes.cpp:1173-1175)
+PHD void PatchAreaWeights(const PatchVerts &P, float w[4]) {
+    w[0] = Length(Cross(P.p10 - P.p00, P.p01 - P.p00));
+    w[1] = Length(Cross(P.p10 - P.p00, P.p11 - P.p10));
+    w[2] = Length(Cross(P.p01 - P.p00, P.p11 - P.p01));
+    w[3] = Length(Cross(P.p11 - P.p10, P.p11 - P.p01));
+}
+// BilinearPatch::Sample(u) (shapes.cpp:1158-1217): area measure; false for {}
+PHD bool BilinearSampleArea(const DeviceShape &s, const float *N, float u0, float u1, V3 *pOut, V3 *pErr, V3 *nOut,
+                            float *pdfOut) {
+    const PatchVerts P = PatchP(s);
+    float pdf = 1, uu = u0, vv = u1;
+    if (s.b == 0) {
+        float w[4];
+        PatchAreaWeights(P, w);
+        SampleBilinear(u0, u1, w, &uu, &vv);
+        pdf = BilinearPDF(uu, vv, w);
+    }
+    const V3 pu0 = LerpV(vv, P.p00, P.p01), pu1 = LerpV(vv, P.p10, P.p11);
+    const V3 p = LerpV(uu, pu0, pu1);
+    const V3 dpdu = pu1 - pu0;
+    const V3 dpdv = LerpV(uu, P.p01, P.p11) - LerpV(uu, P.p00, P.p10);
+    if (LengthSquared(dpdu) == 0 || LengthSquared(dpdv) == 0) return false;
+    *nOut = PatchSampleNormal(s, N, Normalize(Cross(dpdu, dpdv)), uu, vv);
+    const V3 pAbsSum = Abs(P.p00) + Abs(P.p01) + Abs(P.p10) + Abs(P.p11);
+    ToPoint3fi(p, gamma(6) * pAbsSum, pOut, pErr);
+    *pdfOut = pdf / Length(Cross(dpdu, dpdv));
+    return true;
+}
+// SphericalQuadArea (util/vecmath.h:1648-1666)
+PHD float SphericalQuadArea(V3 a, V3 b, V3 c, V3 d) {
+    V3 axb = Cross(a, b), bxc = Cross(b, c), cxd = Cross(c, d), dxa = Cross(d, a);
+    if (LengthSquared(axb) == 0 || LengthSquared(bxc) == 0 || LengthSquared(cxd) == 0 || LengthSquared(dxa) == 0)
+        return 0;
+    axb = Normalize(axb);
+    bxc = Normalize(bxc);
+    cxd = Normalize(cxd);
+    dxa = Normalize(dxa);
+    const float alpha = AngleBetween(dxa, -axb), beta = AngleBetween(axb, -bxc);
+    const float gam = AngleBetween(bxc, -cxd), delta = AngleBetween(cxd, -dxa);
+    return std::fabs(alpha + beta + gam + delta - 2 * kPi);
+}
+// SampleSphericalRectangle (util/sampling.cpp:163-220)
+PHD V3 SampleSphericalRectangle(V3 pRef, V3 sq, V3 ex, V3 ey, float u0, float u1, float *pdf) {
+    const float exl = Length(ex), eyl = Length(ey);
+    const V3 rx = ex / exl, ry = ey / eyl;
+    V3 rz = Cross(rx, ry);
+    const V3 dd0 = sq - pRef;
+    float z0 = Dot(dd0, rz);
+    const float x0 = Dot(dd0, rx), y0 = Dot(dd0, ry);
+    if (z0 > 0) {
+        rz = -rz;
+        z0 *= -1;
+    }
+    const float x1 = x0 + exl, y1 = y0 + eyl;
+    const V3 v00(x0, y0, z0), v01(x0, y1, z0), v10(x1, y0, z0), v11(x1, y1, z0);
+    const V3 n0 = Normalize(Cross(v00, v10)), n1 = Normalize(Cross(v10, v11));
+    const V3 n2 = Normalize(Cross(v11, v01)), n3 = Normalize(Cross(v01, v00));
+    const float g0 = AngleBetween(-n0, n1), g1 = AngleBetween(-n1, n2);
+    const float g2 = AngleBetween(-n2, n3), g3 = AngleBetween(-n3, n0);
+    const float solidAngle = g0 + g1 + g2 + g3 - 2 * kPi;
+    if (solidAngle <= 0) {
+        *pdf = 0;
+        return sq + u0 * ex + u1 * ey;
+    }
+    *pdf = std::fmax(0.f, 1 / solidAngle);
+    if (solidAngle < 1e-3f) return sq + u0 * ex + u1 * ey;
+    const float b0 = n0.z, b1 = n2.z;
+    const float au = u0 * (g0 + g1 - 2 * kPi) + (u0 - 1) * (g2 + g3);
+    float sau, cau;
+    SinCosf(au, &sau, &cau);
+    const float fu = (cau * b0 - b1) / sau;
+    float cu = std::copysign(1 / std::sqrt(Sqr(fu) + Sqr(b0)), fu);
+    cu = Clampf(cu, -kOneMinusEpsilon, kOneMinusEpsilon);
+    float xu = -(cu * z0) / SafeSqrt(1 - Sqr(cu));
+    xu = Clampf(xu, x0, x1);
+    const float dd = std::sqrt(Sqr(xu) + Sqr(z0));
+    const float h0 = y0 / std::sqrt(Sqr(dd) + Sqr(y0));
+    const float h1 = y1 / std::sqrt(Sqr(dd) + Sqr(y1));
+    const float hv = h0 + u1 * (h1 - h0), hvsq = Sqr(hv);
+    const float yv = (hvsq < 1 - 1e-6f) ? (hv * dd) / std::sqrt(1 - hvsq) : y1;
+    return pRef + (rx * xu + ry * yv + rz * z0);
+}
+// InvertSphericalRectangleSample (util/sampling.cpp:222-345)
+PHD void InvertSphericalRectangleSample(V3 pRef, V3 sq, V3 ex, V3 ey, V3 pRect, float *uo0, float *uo1) {
+    const float exl = Length(ex), eyl = Length(ey);
+    const V3 rx = ex / exl, ry = ey / eyl;
+    V3 rz = Cross(rx, ry);
+    const V3 dd0 = sq - pRef;
+    float z0 = Dot(dd0, rz);
+    const float x0 = Dot(dd0, rx), y0 = Dot(dd0, ry);
+    if (z0 > 0) {
+        rz = -rz;
+        z0 *= -1;
+    }
+    const float z0sq = Sqr(z0);
+    const float x1 = x0 + exl, y1 = y0 + eyl;
+    const float y0sq = Sqr(y0), y1sq = Sqr(y1);
+    const V3 v00(x0, y0, z0), v01(x0, y1, z0), v10(x1, y0, z0), v11(x1, y1, z0);
+    const V3 n0 = Normalize(Cross(v00, v10)), n1 = Normalize(Cross(v10, v11));
+    const V3 n2 = Normalize(Cross(v11, v01)), n3 = Normalize(Cross(v01, v00));
+    const float g0 = AngleBetween(-n0, n1), g1 = AngleBetween(-n1, n2);
+    const float g2 = AngleBetween(-n2, n3), g3 = AngleBetween(-n3, n0);
+    const float b0 = n0.z, b1 = n2.z, b0sq = Sqr(b0);
+    const float solidAngle = (float)((double)g0 + (double)g1 + (double)g2 + (double)g3 - 2. * (double)kPi);
+    if (solidAngle < 1e-3f) {
+        const V3 pq = pRect - sq;
+        *uo0 = Dot(pq, ex) / LengthSquared(ex);
+        *uo1 = Dot(pq, ey) / LengthSquared(ey);
+        return;
+    }
+    const V3 dv = pRect - pRef;
+    float xu = Dot(dv, rx);
+    const float yv = Dot(dv, ry);
+    xu = Clampf(xu, x0, x1);
+    if (xu == 0) xu = 1e-10f;
+    const float invcusq = 1 + z0sq / Sqr(xu);
+    const float fusq = invcusq - b0sq;
+    const float fu = std::copysign(std::sqrt(fusq), xu);
+    const float sqr = SafeSqrt(DifferenceOfProducts(b0, b0, b1, b1) + fusq);
+    float au = ATan2f(-(b1 * fu) - std::copysign(b0 * sqr, fu * b0), b0 * b1 - sqr * std::fabs(fu));
+    if (au > 0) au -= 2 * kPi;
+    if (fu == 0) au = kPi;
+    const float u0 = (au + g2 + g3) / solidAngle;
+    const float ddsq = Sqr(xu) + z0sq;
+    const float dd = std::sqrt(ddsq);
+    const float h0 = y0 / std::sqrt(ddsq + y0sq);
+    const float h1 = y1 / std::sqrt(ddsq + y1sq);
+    const float yvsq = Sqr(yv);
+    const float root = std::fabs(h0 - h1) * std::sqrt(yvsq * (ddsq + yvsq)) / (ddsq + yvsq);
+    const float u1a = (DifferenceOfProducts(h0, h0, h0, h1) - root) / Sqr(h0 - h1);
+    const float u1b = (DifferenceOfProducts(h0, h0, h0, h1) + root) / Sqr(h0 - h1);
+    const float hva = Lerpf(u1a, h0, h1), hvb = Lerpf(u1b, h0, h1);
+    const float yza = (hva * dd) / std::sqrt(1 - Sqr(hva)), yzb = (hvb * dd) / std::sqrt(1 - Sqr(hvb));
+    *uo0 = Clampf(u0, 0, 1);
+    *uo1 = (std::fabs(yza - yv) < std::fabs(yzb - yv)) ? u1a : u1b;
+}
+// InvertBilinear (util/vecmath.h:625-654) of st over the corner uvs uv00 uv10 uv01 uv11
+PHD void InvertBilinearUV(const DeviceShape &s, float px, float py, float *uo, float *vo) {
+    float a[2], b[2], c[2], d[2];
+    PatchUV(s, 0, &a[0], &a[1]);
+    PatchUV(s, 1, &b[0], &b[1]);
+    PatchUV(s, 3, &c[0], &c[1]);
+    PatchUV(s, 2, &d[0], &d[1]);
+    const float e[2] = {b[0] - a[0], b[1] - a[1]}, f[2] = {d[0] - a[0], d[1] - a[1]};
+    const float g[2] = {(a[0] - b[0]) + (c[0] - d[0]), (a[1] - b[1]) + (c[1] - d[1])}, h[2] = {px - a[0], py - a[1]};
+    auto cross2d = [](const float *x, const float *y) { return DifferenceOfProducts(x[0], y[1], x[1], y[0]); };
+    const float k2 = cross2d(g, f), k1 = cross2d(e, f) + cross2d(h, g), k0 = cross2d(h, e);
+    if (std::fabs(k2) < 0.001f) {
+        if (std::fabs(e[0] * k1 - g[0] * k0) < 1e-5f) *uo = (h[1] * k1 + f[1] * k0) / (e[1] * k1 - g[1] * k0);
+        else *uo = (h[0] * k1 + f[0] * k0) / (e[0] * k1 - g[0] * k0);
+        *vo = -k0 / k1;
+        return;
+    }
+    float v0, v1;
+    if (!QuadraticF(k2, k1, k0, &v0, &v1)) {
+        *uo = *vo = 0;
+        return;
+    }
+    const float u = (h[0] - f[0] * v0) / (e[0] + g[0] * v0);
+    if (u < 0 || u > 1 || v0 < 0 || v0 > 1) {
+        *uo = (h[0] - f[0] * v1) / (e[0] + g[0] * v1);
+        *vo = v1;
+        return;
+    }
+    *uo = u;
+    *vo = v0;
+}
 PHD float ShapeArea(const DeviceShape &s) {
+    if (s.kind == kShapeBilinearT) return s.a;
     if (s.kind == kShapeSphereT) return s.d * s.a * (s.c - s.b);  // phiMax radius (zMax - zMin)
     return s.d * 0.5f * (Sqr(s.b) - Sqr(s.c));                    // phiMax / 2 (r^2 - ri^2)
 }
@@ -1880,14 +2222,22 @@ PHD bool DiskIntersect(const DeviceShape &s, V3 ro, V3 rd, float tMax, float *tH
     *pObj = pHit;
     return true;
 }
+// pObj: the object-space hit (sphere, disk) or (u, v, 0) (bilinear patch)
 PHD bool ShapeIntersect(const DeviceShape &s, V3 ro, V3 rd, float tMax, float *tHit, V3 *pObj) {
+    if (s.kind == kShapeBilinearT) {
+        float u, v;
+        if (!BilinearIntersect(s, ro, rd, tMax, tHit, &u, &v)) return false;
+        *pObj = V3(u, v, 0);
+        return true;
+    }
     return s.kind == kShapeSphereT ? SphereIntersect(s, ro, rd, tMax, tHit, pObj)
                                    : DiskIntersect(s, ro, rd, tMax, tHit, pObj);
 }
 // Sphere / Disk::InteractionFromIntersection (shapes.h:237-281, 477-501) followed by
 // Transform::operator()(SurfaceInteraction) (util/transform.cpp:229-261): render-space p and
 // its error, n, shading n (faced to n), dpdu, dpdv and uv
-PHD TriSurface ShapeSurface(const DeviceShape &s, V3 pHit) {
+PHD TriSurface ShapeSurface(const DeviceShape &s, V3 pHit, const float *N = nullptr) {
+    if (s.kind == kShapeBilinearT) return BilinearSurface(s, N, pHit.x, pHit.y);
     const float phi = ShapePhi(pHit);
     V3 dpdu, dpdv, pError;
     float u, v;
@@ -1969,7 +2319,43 @@ PHD ShapeSamplePt ShapeSampleArea(const DeviceShape &s, float u0, float u1) {
 }
 // Shape::Sample(ctx, u) (shapes.h:293-361 sphere cone sampling, :531-547 disk) with
 // ctx = (p, pErr, n): false for {} (also a zero solid-angle pdf); the pdf in solid angle
-PHD bool ShapeSampleSolidAngle(const DeviceShape &s, V3 cp, V3 cpErr, V3 cn, float u0, float u1, ShapeSamplePt *out) {
+PHD bool ShapeSampleSolidAngle(const DeviceShape &s, V3 cp, V3 cpErr, V3 cn, float u0, float u1, ShapeSamplePt *out,
+                               const float *N = nullptr, V3 cns = V3(0, 0, 0)) {
+    if (s.kind == kShapeBilinearT) {
+        // BilinearPatch::Sample(ctx, u) (shapes.cpp:1257-1330)
+        const PatchVerts P = PatchP(s);
+        const V3 v00 = Normalize(P.p00 - cp), v10 = Normalize(P.p10 - cp);
+        const V3 v01 = Normalize(P.p01 - cp), v11 = Normalize(P.p11 - cp);
+        if (s.b == 0 || SphericalQuadArea(v00, v10, v11, v01) <= 1e-4f) {
+            ShapeSamplePt ss;
+            if (!BilinearSampleArea(s, N, u0, u1, &ss.p, &ss.pErr, &ss.n, &ss.pdf)) return false;
+            V3 wi = ss.p - cp;
+            if (LengthSquared(wi) == 0) return false;
+            wi = Normalize(wi);
+            ss.pdf /= AbsDotN(ss.n, -wi) / DistanceSquared(cp, ss.p);
+            if (std::isinf(ss.pdf)) return false;
+            *out = ss;
+            return true;
+        }
+        float pdf = 1, uu = u0, vv = u1;
+        if (cns.x != 0 || cns.y != 0 || cns.z != 0) {
+            const float w[4] = {std::fmax(0.01f, AbsDotN(cns, v00)), std::fmax(0.01f, AbsDotN(cns, v10)),
+                                std::fmax(0.01f, AbsDotN(cns, v01)), std::fmax(0.01f, AbsDotN(cns, v11))};
+            SampleBilinear(u0, u1, w, &uu, &vv);
+            pdf *= BilinearPDF(uu, vv, w);
+        }
+        const V3 eu = P.p10 - P.p00, ev = P.p01 - P.p00;
+        float quadPDF;
+        const V3 p = SampleSphericalRectangle(cp, P.p00, eu, ev, uu, vv, &quadPDF);
+        pdf *= quadPDF;
+        const float su = Dot(p - P.p00, eu) / DistanceSquared(P.p10, P.p00);
+        const float sv = Dot(p - P.p00, ev) / DistanceSquared(P.p01, P.p00);
+        out->n = PatchSampleNormal(s, N, Normalize(Cross(eu, ev)), su, sv);
+        out->p = p;
+        out->pErr = V3(0, 0, 0);
+        out->pdf = pdf;
+        return true;
+    }
     if (s.kind == kShapeSphereT) {
         const float radius = s.a;
         const V3 pCenter = XfPt(s.o2r, V3(0, 0, 0));
@@ -2017,7 +2403,44 @@ PHD bool ShapeSampleSolidAngle(const DeviceShape &s, V3 cp, V3 cpErr, V3 cn, flo
 }
 // Shape::PDF(ctx, wi) (shapes.h:364-392 sphere, :550-564 disk): the ray ctx.SpawnRay(wi)
 // against the shape alone where the cone formula does not apply
-PHD float ShapePDFSolidAngle(const DeviceShape &s, V3 cp, V3 cpErr, V3 cn, V3 wi) {
+PHD float ShapePDFSolidAngle(const DeviceShape &s, V3 cp, V3 cpErr, V3 cn, V3 wi, const float *N = nullptr,
+                             V3 cns = V3(0, 0, 0)) {
+    if (s.kind == kShapeBilinearT) {
+        // BilinearPatch::PDF(ctx, wi) (shapes.cpp:1332-1372)
+        const V3 ro = OffsetRayOrigin(cp, cpErr, cn, wi);
+        float th, iu, iv;
+        if (!BilinearIntersect(s, ro, wi, kInfinity, &th, &iu, &iv)) return 0;
+        const TriSurface si = BilinearSurface(s, N, iu, iv);
+        const PatchVerts P = PatchP(s);
+        const V3 v00 = Normalize(P.p00 - cp), v10 = Normalize(P.p10 - cp);
+        const V3 v01 = Normalize(P.p01 - cp), v11 = Normalize(P.p11 - cp);
+        if (s.b == 0 || SphericalQuadArea(v00, v10, v11, v01) <= 1e-4f) {
+            // BilinearPatch::PDF(intr) (shapes.cpp:1219-1255) at the hit's (s, t)
+            float uu = si.uv[0], vv = si.uv[1];
+            if (s.flags & 4) InvertBilinearUV(s, si.uv[0], si.uv[1], &uu, &vv);
+            float pdf = 1;
+            if (s.b == 0) {
+                float w[4];
+                PatchAreaWeights(P, w);
+                pdf = BilinearPDF(uu, vv, w);
+            }
+            const V3 pu0 = LerpV(vv, P.p00, P.p01), pu1 = LerpV(vv, P.p10, P.p11);
+            const V3 dpdu = pu1 - pu0;
+            const V3 dpdv = LerpV(uu, P.p01, P.p11) - LerpV(uu, P.p00, P.p10);
+            pdf = pdf / Length(Cross(dpdu, dpdv));
+            pdf = pdf * (DistanceSquared(cp, si.p) / AbsDotN(si.n, -wi));
+            return std::isinf(pdf) ? 0.f : pdf;
+        }
+        const float pdf = 1 / SphericalQuadArea(v00, v10, v11, v01);
+        if (cns.x != 0 || cns.y != 0 || cns.z != 0) {
+            const float w[4] = {std::fmax(0.01f, AbsDotN(cns, v00)), std::fmax(0.01f, AbsDotN(cns, v10)),
+                                std::fmax(0.01f, AbsDotN(cns, v01)), std::fmax(0.01f, AbsDotN(cns, v11))};
+            float su, sv;
+            InvertSphericalRectangleSample(cp, P.p00, P.p10 - P.p00, P.p01 - P.p00, si.p, &su, &sv);
+            return BilinearPDF(su, sv, w) * pdf;
+        }
+        return pdf;
+    }
     if (s.kind == kShapeSphereT) {
         const float radius = s.a;
         const V3 pCenter = XfPt(s.o2r, V3(0, 0, 0));
@@ -2041,6 +2464,16 @@ PHD float ShapePDFSolidAngle(const DeviceShape &s, V3 cp, V3 cpErr, V3 cn, V3 wi
 }
 // Sphere / Disk::Bounds (shapes.cpp:33-40, 88-92): the transformed object box's 8 corners
 PHD void ShapeBounds(const DeviceShape &s, V3 *lo, V3 *hi) {
+    if (s.kind == kShapeBilinearT) {  // Union(Bounds3f(p00, p01), Bounds3f(p10, p11))
+        const PatchVerts P = PatchP(s);
+        *lo = V3(std::fmin(std::fmin(P.p00.x, P.p01.x), std::fmin(P.p10.x, P.p11.x)),
+                 std::fmin(std::fmin(P.p00.y, P.p01.y), std::fmin(P.p10.y, P.p11.y)),
+                 std::fmin(std::fmin(P.p00.z, P.p01.z), std::fmin(P.p10.z, P.p11.z)));
+        *hi = V3(std::fmax(std::fmax(P.p00.x, P.p01.x), std::fmax(P.p10.x, P.p11.x)),
+                 std::fmax(std::fmax(P.p00.y, P.p01.y), std::fmax(P.p10.y, P.p11.y)),
+                 std::fmax(std::fmax(P.p00.z, P.p01.z), std::fmax(P.p10.z, P.p11.z)));
+        return;
+    }
     V3 a, b;
     if (s.kind == kShapeSphereT) {
         a = V3(-s.a, -s.a, s.b);

@@ -450,7 +450,39 @@ static void BuildLightBVH(SceneDesc &s) {
             ShapeBounds(d, &lo, &hi);
             lb.bounds.Add(lo);
             lb.bounds.Add(hi);
-            if (d.kind == kShapeSphereT) {
+            if (d.kind == kShapeBilinearT) {
+                // BilinearPatch::NormalBounds (shapes.cpp:1083-1129)
+                const AnalyticShapeDesc &sh = s.shapes[al.shape];
+                const PatchVerts P = PatchP(d);
+                const bool hasN = d.flags & 8, flip = ((d.flags & 1) != 0) != ((d.flags & 2) != 0);
+                auto N = [&](int k) { return V3(sh.normals[3 * k], sh.normals[3 * k + 1], sh.normals[3 * k + 2]); };
+                if (P.p00 == P.p10 || P.p10 == P.p11 || P.p11 == P.p01 || P.p01 == P.p00) {
+                    const V3 dpdu = LerpV(0.5f, P.p10, P.p11) - LerpV(0.5f, P.p00, P.p01);
+                    const V3 dpdv = LerpV(0.5f, P.p01, P.p11) - LerpV(0.5f, P.p00, P.p10);
+                    V3 n = Normalize(Cross(dpdu, dpdv));
+                    if (hasN) n = FaceForwardN(n, (N(0) + N(1) + N(2) + N(3)) / 4);
+                    else if (flip) n = -n;
+                    lb.w = Normalize(Normalize(n));
+                    lb.cosTheta_o = 1;
+                } else {
+                    V3 n00 = Normalize(Cross(P.p10 - P.p00, P.p01 - P.p00));
+                    V3 n10 = Normalize(Cross(P.p11 - P.p10, P.p00 - P.p10));
+                    V3 n01 = Normalize(Cross(P.p00 - P.p01, P.p11 - P.p01));
+                    V3 n11 = Normalize(Cross(P.p01 - P.p11, P.p10 - P.p11));
+                    if (hasN) {
+                        n00 = FaceForwardN(n00, N(0));
+                        n10 = FaceForwardN(n10, N(1));
+                        n01 = FaceForwardN(n01, N(2));
+                        n11 = FaceForwardN(n11, N(3));
+                    } else if (flip) {
+                        n00 = -n00, n10 = -n10, n01 = -n01, n11 = -n11;
+                    }
+                    const V3 n = Normalize(n00 + n10 + n01 + n11);
+                    const float cosTheta = std::min(std::min(Dot(n, n00), Dot(n, n01)), std::min(Dot(n, n10), Dot(n, n11)));
+                    lb.w = Normalize(n);
+                    lb.cosTheta_o = Clampf(cosTheta, -1, 1);
+                }
+            } else if (d.kind == kShapeSphereT) {
                 lb.w = Normalize(V3(0, 0, 1));
                 lb.cosTheta_o = -1;
             } else {

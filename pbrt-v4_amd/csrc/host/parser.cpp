@@ -320,7 +320,8 @@ class Parser {
     std::string cameraType = "perspective", filmType = "rgb";
     bool inWorld = false;
     struct PendingShape {
-        int kind = 0;                 // 0 triangle mesh, kShapeSphereT, kShapeDiskT
+        int kind = 0;                 // 0 triangle mesh, kShapeSphereT, kShapeDiskT, kShapeBilinearT
+        std::vector<int> quadIdx;     // bilinear patches: 4 vertex indices each (p00 p10 p01 p11)
         float sp[4] = {0, 0, 0, 0};   // sphere: radius zmin zmax phimax; disk: height radius innerradius phimax
         std::vector<V3> P;
         std::vector<int> idx;
@@ -956,13 +957,42 @@ class Parser {
             } catch (const Error &e) {
                 throw Error(ps.loc + ": " + e.what());
             }
-            if (!m.quadIndices.empty())
-                throw Error(ps.loc + ": " + f + " has quads; pbrt makes bilinear patches of them, which are not supported yet");
-            if (m.triIndices.empty()) throw Error(ps.loc + ": " + f + " has no triangles");
+            // triangles become a TriangleMesh, quads a BilinearPatchMesh (scene.cpp plymesh)
+            if (m.triIndices.empty() && m.quadIndices.empty()) throw Error(ps.loc + ": " + f + " has no faces");
             s.P = std::move(m.p);
             s.idx = std::move(m.triIndices);
+            s.quadIdx = std::move(m.quadIndices);
             s.N = std::move(m.n);
             for (auto &t : m.uv) s.uv.insert(s.uv.end(), {t[0], t[1]});
+        } else if (type == "bilinearmesh") {
+            // BilinearPatch::CreateMesh (shapes.cpp:914-1003)
+            s.kind = kShapeBilinearT;
+            Param *P = ps.Find("P", "point3");
+            if (!P) P = ps.Find("P", "point");
+            if (!P || P->nums.empty() || P->nums.size() % 3)
+                throw Error(ps.loc + ": Vertex positions \"P\" must be provided with bilinear patch mesh shape.");
+            for (size_t i = 0; i < P->nums.size(); i += 3) s.P.push_back(V3(P->nums[i], P->nums[i + 1], P->nums[i + 2]));
+            if (Param *I = ps.Find("indices", "integer")) {
+                for (double v : I->nums) s.quadIdx.push_back((int)v);
+                while (s.quadIdx.size() % 4) s.quadIdx.pop_back();  // "Discarding excess"
+            } else if (s.P.size() == 4) {
+                s.quadIdx = {0, 1, 2, 3};
+            } else {
+                throw Error(ps.loc + ": Vertex indices \"indices\" must be provided with bilinear patch mesh shape.");
+            }
+            for (int v : s.quadIdx)
+                if (v < 0 || v >= (int)s.P.size())
+                    throw Error(ps.loc + ": Bilinear patch mesh has out of-bounds vertex index " + std::to_string(v));
+            if (Param *uv = ps.Find("uv", "point2")) {
+                if (uv->nums.size() == 2 * s.P.size())
+                    for (double v : uv->nums) s.uv.push_back((float)v);
+            }
+            Param *N = ps.Find("N", "normal");
+            if (!N) N = ps.Find("N", "normal3");
+            if (N && N->nums.size() == 3 * s.P.size())
+                for (size_t i = 0; i < N->nums.size(); i += 3) s.N.push_back(V3(N->nums[i], N->nums[i + 1], N->nums[i + 2]));
+            if (ps.Find("emissionfilename")) throw Error(ps.loc + ": \"emissionfilename\" is not supported yet");
+            ps.Find("faceIndices");
         } else if (type == "sphere") {
             // Sphere::Create (shapes.cpp:75-85)
             s.kind = kShapeSphereT;
@@ -1057,6 +1087,87 @@ class Parser {
             scene.areaLights.push_back(l);
         }
         scene.shapes.push_back(a);
+    }
+
+    // BilinearPatchMesh ctor (util/mesh.cpp: render-space P, N through renderFromObject and
+    // negated under ReverseOrientation) and one BilinearPatch per quad (shapes.cpp:1041-1071:
+    // IsRectangle, area); each emissive patch is its own DiffuseAreaLight
+    template <typename MediumOf>
+    void BilinearPatches(const PendingShape &s, const Mat4 &rfo, int mat, int lightSpectrum, float lightScale,
+                         bool twoSided, float power, const MediumOf &mediumOf, int base) {
+        const Mat4 inv = Inverse4(rfo);
+        const bool swaps = SwapsHandedness(rfo);
+        for (size_t q = 0; q + 3 < s.quadIdx.size(); q += 4) {
+            AnalyticShapeDesc a;
+            DeviceShape &d = a.dev;
+            d.kind = kShapeBilinearT;
+            d.flags = (s.flip ? 1 : 0) | (swaps ? 2 : 0) | (s.uv.empty() ? 0 : 4) | (s.N.empty() ? 0 : 8);
+            V3 pv[4];
+            for (int k = 0; k < 4; ++k) {
+                const int vi = s.quadIdx[q + k];
+                pv[k] = scene.verts[base + vi];  // render space (pushed by the mesh pass)
+                for (int j = 0; j < 3; ++j) d.r2o[3 * k + j] = pv[k][j];
+                if (!s.uv.empty()) {
+                    d.o2r[2 * k] = s.uv[2 * vi];
+                    d.o2r[2 * k + 1] = s.uv[2 * vi + 1];
+                }
+                if (!s.N.empty()) {
+                    V3 nn = XformNormal(inv, s.N[vi]);
+                    if (s.flip) nn = -nn;
+                    for (int j = 0; j < 3; ++j) a.normals[3 * k + j] = nn[j];
+                }
+            }
+            const V3 p00 = pv[0], p10 = pv[1], p01 = pv[2], p11 = pv[3];
+            bool rect = !(p00 == p01 || p01 == p11 || p11 == p10 || p10 == p00);
+            if (rect) {
+                const V3 n = Normalize(Cross(p10 - p00, p01 - p00));
+                if (AbsDotN(n, Normalize(p11 - p00)) > 1e-5f) rect = false;
+            }
+            if (rect) {
+                const V3 pCenter = (p00 + p01 + p10 + p11) / 4;
+                const float d2[4] = {DistanceSquared(p00, pCenter), DistanceSquared(p01, pCenter),
+                                     DistanceSquared(p10, pCenter), DistanceSquared(p11, pCenter)};
+                for (int i = 1; i < 4; ++i)
+                    if (std::abs(d2[i] - d2[0]) / d2[0] > 1e-4f) rect = false;
+            }
+            float area = 0;
+            if (rect) {
+                area = Distance(p00, p01) * Distance(p00, p10);
+            } else {
+                V3 g[4][4];
+                for (int i = 0; i <= 3; ++i)
+                    for (int j = 0; j <= 3; ++j) {
+                        const float u = float(i) / float(3), v = float(j) / float(3);
+                        g[i][j] = LerpV(u, LerpV(v, p00, p01), LerpV(v, p10, p11));
+                    }
+                for (int i = 0; i < 3; ++i)
+                    for (int j = 0; j < 3; ++j)
+                        area += 0.5f * Length(Cross(g[i + 1][j + 1] - g[i][j], g[i + 1][j] - g[i][j + 1]));
+            }
+            d.a = area;
+            d.b = rect ? 1.f : 0.f;
+            a.material = mat;
+            if (!scene.media.empty()) {
+                a.medium[0] = (int16_t)mediumOf(s.insideMedium, s.loc);
+                a.medium[1] = (int16_t)mediumOf(s.outsideMedium, s.loc);
+            }
+            if (lightSpectrum >= 0) {
+                AreaLightDesc l;
+                l.shape = (int)scene.shapes.size();
+                l.spectrum = lightSpectrum;
+                l.scale = lightScale;
+                l.twoSided = twoSided;
+                l.area = area;
+                if (power > 0) {
+                    float k_e = 1;
+                    k_e *= (twoSided ? 2 : 1) * l.area * kPi;
+                    l.scale *= power / k_e;
+                }
+                a.light = (int)scene.areaLights.size();
+                scene.areaLights.push_back(l);
+            }
+            scene.shapes.push_back(a);
+        }
     }
 
     // ObjectInstance: renderFromInstance = RenderFromObject() * worldFromRender (scene.cpp:392),
@@ -1519,10 +1630,12 @@ void Parser::Finish() {
             }
             ap.CheckUnused();
         }
-        if (s.kind != 0) {
+        if (s.kind == kShapeSphereT || s.kind == kShapeDiskT) {
             AnalyticShape(s, rfo, mat, lightSpectrum, lightScale, twoSided, power, mediumOf);
             continue;
         }
+        if (!s.quadIdx.empty())
+            BilinearPatches(s, rfo, mat, lightSpectrum, lightScale, twoSided, power, mediumOf, base);
         for (size_t t = 0; t < s.idx.size(); t += 3) {
             std::array<int, 3> tri = {base + s.idx[t], base + s.idx[t + 1], base + s.idx[t + 2]};
             int triIndex = (int)scene.tris.size();

@@ -178,11 +178,12 @@ struct AreaLightDesc {
     float area = 0;
 };
 
-// Sphere / Disk (shapes.h:106-571) in render space: the device record (affine render-from-object
+// Sphere / Disk / BilinearPatch (shapes.h:106-571, 1272-1540) in render space: the device record (affine render-from-object
 // and object-from-render matrices, parameters, orientation flags) and the shape's attributes.
 // Primitive ids: leaf-order triangles first, then shape k as nTriangles + k.
 struct AnalyticShapeDesc {
     DeviceShape dev{};
+    std::array<float, 12> normals{};  // bilinear patch: render-space vertex normals (dev.flags bit 3)
     int material = -1;
     int light = -1;                   // area light index or -1
     int16_t medium[2] = {-1, -1};     // {inside, outside}

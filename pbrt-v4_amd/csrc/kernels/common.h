@@ -819,7 +819,11 @@ __device__ inline bool LoadTriShading(const DeviceScene &S, int prim, TriShading
 
 // SurfaceInteraction of a sphere / disk hit (b0..b2 of the hit record hold pObj)
 __device__ __attribute__((noinline)) TriSurface ShapeSurfaceAt(const DeviceScene &S, int k, V3 pObj) {
-    return ShapeSurface(S.shapes[k], pObj);
+    return ShapeSurface(S.shapes[k], pObj, S.shapeN + 12 * (size_t)k);
+}
+// Shape::PDF(ctx, wi) of sphere / disk / patch k from a surface context (p, pErr, n, ns)
+__device__ __attribute__((noinline)) float ShapeLightPDF(const DeviceScene &S, int k, V3 p, V3 pErr, V3 n, V3 ns, V3 wi) {
+    return ShapePDFSolidAngle(S.shapes[k], p, pErr, n, wi, S.shapeN + 12 * (size_t)k, ns);
 }
 // SurfaceInteraction of a hit (Triangle::InteractionFromIntersection)
 __device__ inline TriSurface SurfaceAt(const DeviceScene &S, int prim, V3 p0, V3 p1, V3 p2, float b0, float b1,
@@ -1058,9 +1062,10 @@ __device__ inline float SmoothStepf(float x, float a, float b) {
 // DiffuseAreaLight::SampleLi over a sphere or disk (lights.cpp:743-775 with Shape::Sample(ctx,
 // u)): ctx = (cp, cpErr, n)
 __device__ __attribute__((noinline)) bool SampleShapeLi(const DeviceScene &S, const DeviceAreaLight &Ld, V3 cp, V3 cpErr,
-                                                       V3 n, float u0, float u1, LiSample *ls) {
+                                                       V3 n, V3 ns, float u0, float u1, LiSample *ls) {
     ShapeSamplePt ss;
-    if (!ShapeSampleSolidAngle(S.shapes[__float_as_int(Ld.v0.w) - S.nTris], cp, cpErr, n, u0, u1, &ss) ||
+    const int k = __float_as_int(Ld.v0.w) - S.nTris;
+    if (!ShapeSampleSolidAngle(S.shapes[k], cp, cpErr, n, u0, u1, &ss, S.shapeN + 12 * (size_t)k, ns) ||
         ss.pdf == 0 || LengthSquared(ss.p - cp) == 0)
         return false;
     ls->wi = Normalize(ss.p - cp);
@@ -1082,7 +1087,8 @@ __device__ inline bool SampleLiSurface(const DeviceScene &S, const DeviceAreaLig
     if (li < S.nAreaLights) {
         const DeviceAreaLight &Ld = lightsL[li];
         if constexpr (!Lean) {
-            if (S.nShapes > 0 && __float_as_int(Ld.v0.w) >= S.nTris) return SampleShapeLi(S, Ld, cp, cpErr, n, u0, u1, ls);
+            if (S.nShapes > 0 && __float_as_int(Ld.v0.w) >= S.nTris)
+                return SampleShapeLi(S, Ld, cp, cpErr, n, ns, u0, u1, ls);
         }
         V3 q0(Ld.v0.x, Ld.v0.y, Ld.v0.z), q1(Ld.v1.x, Ld.v1.y, Ld.v1.z), q2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
         TriShading lsh;

@@ -156,6 +156,7 @@ struct DeviceScene {
     int nShapes;
     const DeviceShape *shapes;
     const ShapeBVHNode *shapeNodes;
+    const float *shapeN;  // [nShapes][12]: a bilinear patch's vertex normals (flags bit 3)
     // ImageInfiniteLight entries: infImage[j] indexes env[] (-1: not an image light)
     const int *infImage;
     const DeviceEnvLight *env;

@@ -1202,7 +1202,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
                     const V3 pns = LoadV3(rec.prev + 9 * (size_t)NR, NR, ri);
                     const float lightChoicePDF = LightPMF(S, pp, pns, light);
                     if (S.nShapes > 0 && prim >= S.nTris) {
-                        lightPDF = lightChoicePDF * ShapePDFSolidAngle(S.shapes[prim - S.nTris], pp, pe, pn, -wo3);
+                        lightPDF = lightChoicePDF * ShapeLightPDF(S, prim - S.nTris, pp, pe, pn, pns, -wo3);
                     } else {
                         TriShading lsh;
                         const bool lhas = LoadTriShading(S, __float_as_int(Ld.v0.w), &lsh);

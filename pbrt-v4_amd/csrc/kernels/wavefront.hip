@@ -301,7 +301,7 @@ __global__ void __launch_bounds__(kBlock) k_emissive(DeviceScene S, PathState st
             float lightChoicePDF = LightPMF(S, prev.p, prev.ns, light);
             float lightPDF;
             if (S.nShapes > 0 && prim >= S.nTris) {
-                lightPDF = lightChoicePDF * ShapePDFSolidAngle(S.shapes[prim - S.nTris], prev.p, prev.pErr, prev.n, -wo);
+                lightPDF = lightChoicePDF * ShapeLightPDF(S, prim - S.nTris, prev.p, prev.pErr, prev.n, prev.ns, -wo);
             } else {
                 TriShading lsh;
                 const bool lhas = LoadTriShading(S, __float_as_int(Ld.v0.w), &lsh);

@@ -96,6 +96,7 @@ class SceneFlat(ctypes.Structure):
         ("n_shapes", ctypes.c_int),
         ("shape_info", ctypes.POINTER(ctypes.c_int32)),
         ("shape_params", ctypes.POINTER(ctypes.c_float)),
+        ("shape_normals", ctypes.POINTER(ctypes.c_float)),
     ]
 
 

@@ -126,17 +126,21 @@ def test_reverse_orientation_negates_normals(pa, tmp_path):
 
 
 @pytest.mark.parametrize("kind,msg", [
-    ("quad", "bilinear patches"),
     ("missing", "Couldn't open PLY file"),
     ("badindex", "out of bounds"),
 ])
 def test_plymesh_errors_are_loud(pa, tmp_path, kind, msg):
-    if kind == "quad":
-        write_ply(tmp_path / "m.ply", MESH_P, MESH_F, extra_face=[[0, 1, 2, 3]])
-    elif kind == "badindex":
+    if kind == "badindex":
         write_ply(tmp_path / "m.ply", MESH_P, MESH_F + [[0, 1, 9]])
     with pytest.raises(pa.PbrtError, match=msg):
         _scene(pa, 'Shape "plymesh" "string filename" "m.ply"', tmp_path)
+
+
+def test_plymesh_quad_becomes_a_patch(pa, tmp_path):
+    """A quad face loads as a bilinear patch beside the TriangleMesh (tests/test_bilinear.py)."""
+    write_ply(tmp_path / "m.ply", MESH_P, MESH_F, extra_face=[[0, 1, 2, 3]])
+    sc = _scene(pa, 'Shape "plymesh" "string filename" "m.ply"', tmp_path)
+    assert (sc.info.n_triangles, sc.flat().n_shapes) == (3, 1)
 
 
 def test_plymesh_skips_polygons(pa, tmp_path):

@@ -21,7 +21,9 @@
 namespace pbrt_amd {
 hipError_t LaunchCamera(const DeviceScene &S, const PathState &st, int nActive, hipStream_t s);
 hipError_t LaunchClosest(const DeviceScene &S, const PathState &st, int depth, int maxCount, int timed,
-                         hipStream_t s);
+                         hipStream_t s, bool sorted);
+hipError_t LaunchRayBin(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
+hipError_t LaunchClassify(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
 hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int depth, int maxCount, bool lean,
                               hipStream_t s);
 hipError_t LaunchTexture(const DeviceScene &S, const PathState &st, int depth, int type, bool full, int maxCount,
@@ -433,6 +435,11 @@ struct pbrt_context {
     DevBuf<DeviceEnvLight> envLights;
     DevBuf<int> matMix, hitMat;   // mix materials: {m0, m1, amount program} and resolved materials
     bool hasMix = false;
+    // ray binning before closest hits at depth >= 1 (HBM-resident trees; PBRT_AMD_RAY_SORT=0/1
+    // overrides): st.raySort / st.rayBins
+    bool rayBinning = false;
+    DevBuf<float4> raySort;
+    DevBuf<int> rayBins;
     bool texGeneral = false;      // some textured reflectance is not a single image leaf
     int texTypeMask = 0;          // bit t: some material of type t is textured
     int texFullMask = 0;          // bit t: ... with an expression beyond one non-EWA image leaf
@@ -1112,6 +1119,8 @@ static void BuildDevice(pbrt_context *c) {
         const float lo = c->bvh.boundsMin[a], hi = c->bvh.boundsMax[a];
         const float ext = std::isfinite(hi - lo) && hi >= lo ? hi - lo : 0.f;
         S.bvhAbsMax[a] = std::isfinite(lo) && std::isfinite(hi) ? std::max(std::fabs(lo), std::fabs(hi)) + 2 * ext : 0.f;
+        S.rayBinLo[a] = std::isfinite(lo) ? lo : 0.f;
+        S.rayBinScale[a] = ext > 0 ? 8.f / ext : 0.f;
     }
     {
         // Node format.  A tree that fits the LDS cache whole (nodes + pre-rotated triangles:
@@ -1152,6 +1161,10 @@ static void BuildDevice(pbrt_context *c) {
         const bool allInLds = S.ldsTris > 0;
         if (forceQuant || (!forceWide && !allInLds)) layout(true, kTravQuant);
         else if (allInLds) layout(false, kTravLds);
+        // ray binning before the closest hits of depth >= 1 when the tree lives in HBM (the
+        // surface wavefront; PBRT_AMD_RAY_SORT=0/1 overrides)
+        const char *rs = getenv("PBRT_AMD_RAY_SORT");
+        c->rayBinning = !c->volumetric && (rs ? atoi(rs) != 0 : S.ldsTris == 0);
     }
 
     // film
@@ -1193,6 +1206,11 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
         if (c->texGeneral) c->texR.Alloc((size_t)kNSpectrumSamples * NR);
     }
     if (c->hasMix) c->hitMat.Alloc((size_t)2 * NR);
+    if (c->rayBinning) {
+        c->raySort.Alloc((size_t)2 * NR);
+        c->rayBins.Alloc(2 * 4096);
+        HIPCHECK(hipMemset(c->rayBins.p, 0, 2 * 4096 * sizeof(int)));
+    }
     c->maxPaths = N;
     PathState &st = c->st;
     st.capS = (int)capS;
@@ -1238,6 +1256,8 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
     st.texR = c->texR.p;
     st.hitMat[0] = c->hasMix ? c->hitMat.p : nullptr;
     st.hitMat[1] = c->hasMix ? c->hitMat.p + NR : nullptr;
+    st.raySort = c->rayBinning ? c->raySort.p : nullptr;
+    st.rayBins = c->rayBinning ? c->rayBins.p : nullptr;
     if (c->volumetric) {
         const int vf = kVolFloats, vi = kVolInts;
         c->vfState.Alloc((size_t)vf * NR);
@@ -1431,12 +1451,21 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
                 // closest-hit launches are event-timed in the first pass of a render only: the
                 // passes are statistically identical and each event pair costs a queue gap
                 const bool timed = p->time_closest && r0 == 0 && s0 == 0;
+                const bool bin = c->rayBinning && depth > 0;
+                if (bin) {
+                    StageTimer t(c, "Bin rays by origin cell and direction octant (k_raybin_*)", c->stream);
+                    HIPCHECK(LaunchRayBin(c->S, st, depth, (int)nActive, c->stream));
+                }
                 if (timed) RecordEvent(c, true);
                 {
                     StageTimer t(c, "Tracing closest hit rays (k_closest)", c->stream);
-                    HIPCHECK(LaunchClosest(c->S, st, depth, (int)nActive, timed ? 1 : 0, c->stream));
+                    HIPCHECK(LaunchClosest(c->S, st, depth, (int)nActive, timed ? 1 : 0, c->stream, bin));
                 }
                 if (timed) RecordEvent(c, false);
+                if (bin) {
+                    StageTimer t(c, "Enqueue binned hits in record order (k_classify)", c->stream);
+                    HIPCHECK(LaunchClassify(c->S, st, depth, (int)nActive, c->stream));
+                }
                 // emission (escaped rays, emissive hits) on the side stream, beside the material
                 // stage; the shadow stage and the next depth's closest hits wait for it
                 static const bool emitSerial = getenv("PBRT_AMD_EMIT_SERIAL") != nullptr;
@@ -1720,7 +1749,8 @@ int pbrt_context_create(const pbrt_scene *scene, int device, int64_t maxPaths, p
             // smaller cards): path-state bytes per path from AllocPaths' layout
             size_t freeB = 0, totalB = 0;
             HIPCHECK(hipMemGetInfo(&freeB, &totalB));
-            const int64_t perPath = PathStateBytesPerPath(c->volumetric, c->S.dispersive, c->S.textured, c->texGeneral, c->hasMix);
+            const int64_t perPath = PathStateBytesPerPath(c->volumetric, c->S.dispersive, c->S.textured, c->texGeneral, c->hasMix) +
+                                    (c->rayBinning ? 32 : 0);
             const int64_t fit = (int64_t)(freeB / 4 * 3) / perPath - kShards * 320;
             if (fit < 4096) throw Error("not enough free device memory for path state");
             maxPaths = std::min<int64_t>(maxPaths, fit);

@@ -683,9 +683,15 @@ __device__ inline int TraverseCW(const DeviceScene &S, const SceneLds &L, V3 o, 
 // carries exactly one traversal loop): every node and triangle in LDS (small scenes); wide
 // nodes with the top of the tree in LDS; quantised nodes (PBRT_AMD_BVH=compressed).
 // waves per SIMD (= 256-thread blocks per CU) a traversal kernel of mode TM is compiled for
-constexpr int TraversalWaves(int tm) { return tm == kTravQuant ? PBRT_QUANT_TRAVERSAL_WAVES : PBRT_TRAVERSAL_WAVES; }
+// A mode may carry kTravShapes: the scene has analytic shapes, whose BVH is traversed after the
+// triangles' (an out-of-line call, compiled only into these instantiations so the triangle-only
+// kernels keep their register allocation and scratch).
+constexpr int kTravShapes = 4;
+constexpr int TraversalWaves(int tm) {
+    return (tm & 3) == kTravQuant ? PBRT_QUANT_TRAVERSAL_WAVES : PBRT_TRAVERSAL_WAVES;
+}
 inline int TraversalMode(const DeviceScene &S) {
-    return S.compressed ? kTravQuant : (S.ldsTris > 0 ? kTravLds : kTravWide);
+    return (S.compressed ? kTravQuant : (S.ldsTris > 0 ? kTravLds : kTravWide)) | (S.nShapes > 0 ? kTravShapes : 0);
 }
 // Spheres and disks (Sphere / Disk::BasicIntersect) through their binary BVH, nearer than
 // tMax: the shape index and best = {pObj, tHit}, or -1.  Out of line: only scenes with shapes
@@ -735,12 +741,16 @@ __device__ __attribute__((noinline)) int TraverseShapes(const DeviceScene &S, V3
 template <bool AnyHit, int TM>
 __device__ inline int Traverse(const DeviceScene &S, const SceneLds &L, V3 o, V3 d, float tMax, TriHit *best,
                                TravCount *cnt = nullptr) {
+    constexpr int tm = TM & 3;
     int prim = -1;
-    if (S.nShapes == 0 || S.nTris > 0)
-        prim = TraverseCW<AnyHit, TM == kTravQuant, TM == kTravLds, TM == kTravLds>(S, L, o, d, tMax, best, cnt);
-    if (S.nShapes > 0 && !(AnyHit && prim >= 0)) {
-        const int k = TraverseShapes<AnyHit>(S, o, d, prim >= 0 ? best->t : tMax, best);
-        if (k >= 0) prim = S.nTris + k;
+    if constexpr ((TM & kTravShapes) != 0) {
+        if (S.nTris > 0) prim = TraverseCW<AnyHit, tm == kTravQuant, tm == kTravLds, tm == kTravLds>(S, L, o, d, tMax, best, cnt);
+        if (!(AnyHit && prim >= 0)) {
+            const int k = TraverseShapes<AnyHit>(S, o, d, prim >= 0 ? best->t : tMax, best);
+            if (k >= 0) prim = S.nTris + k;
+        }
+    } else {
+        prim = TraverseCW<AnyHit, tm == kTravQuant, tm == kTravLds, tm == kTravLds>(S, L, o, d, tMax, best, cnt);
     }
     return prim;
 }
@@ -774,7 +784,14 @@ __device__ inline void TravStatsAdd(unsigned long long *stats, int base, bool ac
         switch (TraversalMode(S)) {                                                             \
         case kTravLds: hipLaunchKernelGGL((KERNEL(kTravLds)), __VA_ARGS__); break;              \
         case kTravWide: hipLaunchKernelGGL((KERNEL(kTravWide)), __VA_ARGS__); break;            \
-        default: hipLaunchKernelGGL((KERNEL(kTravQuant)), __VA_ARGS__); break;                  \
+        case kTravQuant: hipLaunchKernelGGL((KERNEL(kTravQuant)), __VA_ARGS__); break;          \
+        case kTravLds | kTravShapes:                                                            \
+            hipLaunchKernelGGL((KERNEL(kTravLds | kTravShapes)), __VA_ARGS__);                  \
+            break;                                                                              \
+        case kTravWide | kTravShapes:                                                           \
+            hipLaunchKernelGGL((KERNEL(kTravWide | kTravShapes)), __VA_ARGS__);                 \
+            break;                                                                              \
+        default: hipLaunchKernelGGL((KERNEL(kTravQuant | kTravShapes)), __VA_ARGS__); break;    \
         }                                                                                       \
     } while (0)
 
@@ -826,9 +843,12 @@ __device__ __attribute__((noinline)) float ShapeLightPDF(const DeviceScene &S, i
     return ShapePDFSolidAngle(S.shapes[k], p, pErr, n, wi, S.shapeN + 12 * (size_t)k, ns);
 }
 // SurfaceInteraction of a hit (Triangle::InteractionFromIntersection)
+// Ext: the scene may have analytic shapes (kernels instantiated without them compile the
+// branch out, keeping the out-of-line call and its frame away from their register allocation)
+template <bool Ext = true>
 __device__ inline TriSurface SurfaceAt(const DeviceScene &S, int prim, V3 p0, V3 p1, V3 p2, float b0, float b1,
                                        float b2) {
-    if (S.nShapes > 0 && prim >= S.nTris) return ShapeSurfaceAt(S, prim - S.nTris, V3(b0, b1, b2));
+    if (Ext && S.nShapes > 0 && prim >= S.nTris) return ShapeSurfaceAt(S, prim - S.nTris, V3(b0, b1, b2));
     TriShading sh;
     const bool has = LoadTriShading(S, prim, &sh);
     return TriangleSurface(p0, p1, p2, b0, b1, b2, S.primFlip[prim], has ? &sh : nullptr);
@@ -1081,12 +1101,14 @@ __device__ __attribute__((noinline)) bool SampleShapeLi(const DeviceScene &S, co
     ls->envLe = false;
     return true;
 }
-template <bool Lean, bool Inl = Lean>
+// Ext: analytic-shape emitters and image infinite lights may be sampled (false: their branches
+// are compiled out; the host launches such kernels only for scenes without either)
+template <bool Lean, bool Inl = Lean, bool Ext = true>
 __device__ inline bool SampleLiSurface(const DeviceScene &S, const DeviceAreaLight *lightsL, int li, V3 cp, V3 n,
                                        V3 ns, float u0, float u1, LiSample *ls, V3 cpErr = V3(0, 0, 0)) {
     if (li < S.nAreaLights) {
         const DeviceAreaLight &Ld = lightsL[li];
-        if constexpr (!Lean) {
+        if constexpr (!Lean && Ext) {
             if (S.nShapes > 0 && __float_as_int(Ld.v0.w) >= S.nTris)
                 return SampleShapeLi(S, Ld, cp, cpErr, n, ns, u0, u1, ls);
         }
@@ -1116,7 +1138,7 @@ __device__ inline bool SampleLiSurface(const DeviceScene &S, const DeviceAreaLig
         if (k >= S.nPointSpot) {
             di = S.infDistant[k - S.nPointSpot];
             if (di < 0) {
-                if (S.nEnv > 0 && S.infImage[k - S.nPointSpot] >= 0)
+                if (Ext && S.nEnv > 0 && S.infImage[k - S.nPointSpot] >= 0)
                     return SampleEnvLi(S, k - S.nPointSpot, cp, u0, u1, ls);
                 return false;  // UniformInfiniteLight::SampleLi(allowIncompletePDF) = {}
             }

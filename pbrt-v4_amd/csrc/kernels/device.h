@@ -207,6 +207,7 @@ struct DeviceScene {
     int maxDepth;
     int stackSize;  // BVH traversal stack entries (uint2 groups) per lane (BVH8::maxStack)
     float bvhAbsMax[3];  // bound on |plane coordinate| per axis (traversal box-test margins)
+    float rayBinLo[3], rayBinScale[3];  // ray-binning grid: cell = (o - lo) * scale, 8 per axis
     int ldsNodes, ldsTris;  // BVH8 nodes / triangles cached in LDS by the traversal kernels
     ShadeLdsLayout shadeLds;
     DeviceMedia media;
@@ -276,6 +277,10 @@ struct PathState {
     int *escQ;          // [NR] escaped rays (only with infinite lights)
     int *emitQ;         // [NR] hits on emissive triangles
     int *counters;      // [CounterIndex(maxDepth + 2, 0, 0)]: per depth, queue and shard
+    // ray binning (HBM-resident trees, depth >= 1; null when off): binned rays (o, record
+    // index), (d, 0) and the bin counts / running offsets
+    float4 *raySort;    // [2][NR]
+    int *rayBins;       // [2][kRayBins]
     double *film;       // [4][xres*yres]: rgbSum[3], weightSum (sensor RGB)
     unsigned long long *stats;  // [kStatsSlots]
 };

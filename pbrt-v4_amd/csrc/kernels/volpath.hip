@@ -966,14 +966,16 @@ struct AreaLightSample {
     float pdf;  // shape pdf * light-choice pmf
     bool delta;
 };
+// Ext: analytic-shape emitters and image lights are possible (the kernels' Ext)
+template <bool Ext>
 __device__ inline bool SampleAreaLight(const DeviceScene &S, V3 refP, V3 refN, V3 refNs, float uc, float u0, float u1,
                                        float lambda0, const WaveOffsets &wo, AreaLightSample *out, float Le[kNS]) {
     int li;
     float lpmf;
     if (!SampleLight(S, refP, refNs, uc, &li, &lpmf)) return false;
-    if (li >= S.nAreaLights || (S.nShapes > 0 && __float_as_int(S.lights[li].v0.w) >= S.nTris)) {
+    if (li >= S.nAreaLights || (Ext && S.nShapes > 0 && __float_as_int(S.lights[li].v0.w) >= S.nTris)) {
         LiSample ls;
-        if (!SampleLiSurface<false>(S, S.lights, li, refP, refN, refNs, u0, u1, &ls)) return false;
+        if (!SampleLiSurface<false, false, Ext>(S, S.lights, li, refP, refN, refNs, u0, u1, &ls)) return false;
         const float rd2 = 1 / ls.d2;
         const bool ok = DivFastOk(ls.d2);
         bool nz = false;
@@ -1064,14 +1066,15 @@ struct AreaLightHit {
         return delta ? DivByRcp(v, d2, rd2, d2Ok) : v;
     }
 };
+template <bool Ext>
 __device__ inline bool SampleAreaLightAt(const DeviceScene &S, V3 refP, V3 refN, V3 refNs, float uc, float u0, float u1,
                                          float lambda0, AreaLightHit *out, V3 refErr = V3(0, 0, 0)) {
     int li;
     float lpmf;
     if (!SampleLight(S, refP, refNs, uc, &li, &lpmf)) return false;
-    if (li >= S.nAreaLights || (S.nShapes > 0 && __float_as_int(S.lights[li].v0.w) >= S.nTris)) {
+    if (li >= S.nAreaLights || (Ext && S.nShapes > 0 && __float_as_int(S.lights[li].v0.w) >= S.nTris)) {
         LiSample ls;
-        if (!SampleLiSurface<false>(S, S.lights, li, refP, refN, refNs, u0, u1, &ls, refErr)) return false;
+        if (!SampleLiSurface<false, false, Ext>(S, S.lights, li, refP, refN, refNs, u0, u1, &ls, refErr)) return false;
         out->p = ls.lp;
         out->pErr = ls.lpe;
         out->n = ls.ln;
@@ -1152,7 +1155,7 @@ size_t VolTablesLdsBytes(const DeviceScene &S) {
 // where a lane decides to push (WavePush serves the lanes that reach it).  DiffuseOnly: the
 // scene's surface materials are diffuse, interface or layered (k_vlayered) only, so the
 // dielectric / conductor code is compiled out (C5: fewer registers, no spills).
-template <bool DiffuseOnly>
+template <bool DiffuseOnly, bool Ext>
 __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(DeviceScene S0, PathState st, VolState v,
                                                                        int wf) {
     const QueueView surf = LoadQueue(st, wf, kVSurf);
@@ -1182,7 +1185,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
         const float b0 = v.hitB[ri], b1 = v.hitB[NR + ri], b2 = v.hitB[2 * NR + ri];
         V3 p0, p1, p2;
         PrimVerts(S, prim, &p0, &p1, &p2);
-        const TriSurface si = SurfaceAt(S, prim, p0, p1, p2, b0, b1, b2);
+        const TriSurface si = SurfaceAt<Ext>(S, prim, p0, p1, p2, b0, b1, b2);
         const V3 wo3 = Normalize(-rd);
         int mIn, mOut;
         MediaOf(S, prim, medium, &mIn, &mOut);
@@ -1201,7 +1204,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
                     const V3 pn = LoadV3(rec.prev + 6 * (size_t)NR, NR, ri);
                     const V3 pns = LoadV3(rec.prev + 9 * (size_t)NR, NR, ri);
                     const float lightChoicePDF = LightPMF(S, pp, pns, light);
-                    if (S.nShapes > 0 && prim >= S.nTris) {
+                    if (Ext && S.nShapes > 0 && prim >= S.nTris) {
                         lightPDF = lightChoicePDF * ShapeLightPDF(S, prim - S.nTris, pp, pe, pn, pns, -wo3);
                     } else {
                         TriShading lsh;
@@ -1295,7 +1298,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
             if (reflective && !transmissive) cp = OffsetRayOrigin(si.p, si.pErr, si.n, wo3), cpErr = V3(0, 0, 0);
             else if (transmissive && reflective) cp = OffsetRayOrigin(si.p, si.pErr, si.n, -wo3), cpErr = V3(0, 0, 0);
             AreaLightHit ls;
-            if (SampleAreaLightAt(S, cp, si.n, si.ns, rs.dUc, rs.dU0, rs.dU1, lambda0, &ls, cpErr) && woL.z != 0) {
+            if (SampleAreaLightAt<Ext>(S, cp, si.n, si.ns, rs.dUc, rs.dU0, rs.dU1, lambda0, &ls, cpErr) && woL.z != 0) {
                 const V3 wi = ls.wi;
                 const V3 wiL = frame.ToLocal(wi);
                 // BSDF::f / BSDF::PDF (bsdf.h:60-135)
@@ -1504,6 +1507,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
 // whose PDF_Li(allowIncompletePDF) is 0, so r_l adds nothing to the MIS denominator.  Escaped
 // rays have their own queue (filled by the closest-hit and medium kernels) and kernel, with the
 // sensor curves and spectra staged in LDS.
+template <bool Ext>
 __global__ void __launch_bounds__(kBlock) k_vescaped(DeviceScene S0, PathState st, VolState v, int wf) {
     const QueueView q = LoadQueue(st, wf, kVEsc);
     if ((int)(blockIdx.x * blockDim.x) >= q.total || S0.nInfinite == 0) return;
@@ -1533,7 +1537,7 @@ __global__ void __launch_bounds__(kBlock) k_vescaped(DeviceScene S0, PathState s
             if (S.infDistant[k] >= 0) continue;  // a DistantLight is no Infinite-type light
             const int spec = S.infSpectrum[k];
             const float scale = S.infScale[k];
-            if (S.nEnv > 0 && S.infImage[k] >= 0) {
+            if (Ext && S.nEnv > 0 && S.infImage[k] >= 0) {
                 // ImageInfiniteLight: Le at the direction's pixel; past a non-specular bounce
                 // r_l * PMF * PDF_Li(allowIncompletePDF) joins the denominator
                 const DeviceEnvLight &E = S.env[S.infImage[k]];
@@ -1577,6 +1581,7 @@ __global__ void __launch_bounds__(kBlock) k_vescaped(DeviceScene S0, PathState s
 // Material "interface" crossings (media.cpp:193-203): SpawnRay(ray.d) at the same path depth into
 // the medium on the far side.  Split from k_vsurface (their own queue, filled by the closest-hit
 // and medium kernels), so these items do not hold that kernel's registers and lanes.
+template <bool Ext>
 __global__ void __launch_bounds__(kBlock) k_viface(DeviceScene S, PathState st, VolState v, int wf) {
     const QueueView q = LoadQueue(st, wf, kVIface);
     if ((int)(blockIdx.x * blockDim.x) >= q.total || wf == S.maxDepth) return;  // last: path ends
@@ -1596,7 +1601,7 @@ __global__ void __launch_bounds__(kBlock) k_viface(DeviceScene S, PathState st, 
         const float b0 = v.hitB[ri], b1 = v.hitB[NR + ri], b2 = v.hitB[2 * NR + ri];
         V3 p0, p1, p2;
         PrimVerts(S, prim, &p0, &p1, &p2);
-        const TriSurface si = SurfaceAt(S, prim, p0, p1, p2, b0, b1, b2);
+        const TriSurface si = SurfaceAt<Ext>(S, prim, p0, p1, p2, b0, b1, b2);
         int mIn, mOut;
         MediaOf(S, prim, medium, &mIn, &mOut);
         const int jn = shardBase + WavePush(nextCnt, true);
@@ -1642,6 +1647,7 @@ struct LayerSpec {
 // surface hits on layered materials (k_vsurface handles escapes, interfaces and emission of
 // the same queue and skips these).  The LayeredBxDF estimates f, Sample_f and PDF by random
 // walks (core.h LayeredBxDF); BSDF samples are pdfIsProportional, so r_l = r_u / PDF(wo, wi).
+template <bool Ext>
 __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st, VolState v, int wf) {
     const QueueView surf = LoadQueue(st, wf, kVSurf);
     const int NR = st.NR;
@@ -1667,7 +1673,7 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
         const float b0 = v.hitB[ri], b1 = v.hitB[NR + ri], b2 = v.hitB[2 * NR + ri];
         V3 p0, p1, p2;
         PrimVerts(S, prim, &p0, &p1, &p2);
-        const TriSurface si = SurfaceAt(S, prim, p0, p1, p2, b0, b1, b2);
+        const TriSurface si = SurfaceAt<Ext>(S, prim, p0, p1, p2, b0, b1, b2);
         const V3 wo3 = Normalize(-rd);
         int mIn, mOut;
         MediaOf(S, prim, medium, &mIn, &mOut);
@@ -1744,7 +1750,7 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
             if (refl && !trans) cp = OffsetRayOrigin(si.p, si.pErr, si.n, wo3), cpErr = V3(0, 0, 0);
             else if (refl && trans) cp = OffsetRayOrigin(si.p, si.pErr, si.n, -wo3), cpErr = V3(0, 0, 0);
             AreaLightHit ls;
-            if (SampleAreaLightAt(S, cp, si.n, si.ns, rs.dUc, rs.dU0, rs.dU1, lambda0, &ls, cpErr) && woL.z != 0) {
+            if (SampleAreaLightAt<Ext>(S, cp, si.n, si.ns, rs.dUc, rs.dU0, rs.dU1, lambda0, &ls, cpErr) && woL.z != 0) {
                 const V3 wi = ls.wi;
                 const V3 wiL = frame.ToLocal(wi);
                 if (dt) D.f(woL, wiL, fo);
@@ -1864,6 +1870,7 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
 }
 
 // SampleMediumScattering<HGPhaseFunction> (media.cpp:259-352)
+template <bool Ext>
 __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vscatter(DeviceScene S, PathState st, VolState v, int wf) {
     const QueueView scat = LoadQueue(st, wf, kVScat);
     const int NR = st.NR;
@@ -1889,7 +1896,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vscatter(DeviceScene
         {
             AreaLightSample ls;
             float Le[kNS];
-            if (SampleAreaLight(S, pS, V3(0, 0, 0), V3(0, 0, 0), rs.dUc, rs.dU0, rs.dU1, lambda0, wo, &ls, Le)) {
+            if (SampleAreaLight<Ext>(S, pS, V3(0, 0, 0), V3(0, 0, 0), rs.dUc, rs.dU0, rs.dU1, lambda0, wo, &ls, Le)) {
                 const V3 wi = ls.wi;
                 const float ph = HenyeyGreenstein(Dot(wo3, wi), g);
                 const float phasePDF = ls.delta ? 0.f : ph;  // IsDeltaLight (media.cpp:292-293)
@@ -1968,7 +1975,7 @@ __device__ __forceinline__ bool TraceTransmittanceRay(const DeviceScene &S, cons
         if (hp >= 0) {
             V3 p0, p1, p2;
             PrimVerts(S, hp, &p0, &p1, &p2);
-            hs = SurfaceAt(S, hp, p0, p1, p2, h.b0, h.b1, h.b2);
+            hs = SurfaceAt<(TM & kTravShapes) != 0>(S, hp, p0, p1, p2, h.b0, h.b1, h.b2);
         }
         if (med >= 0) {
             const MediumRef m = MediumAt(S, med);
@@ -2127,7 +2134,7 @@ __global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_vshadow_grey(Dev
             if (hp >= 0) {
                 V3 p0, p1, p2;
                 PrimVerts(S, hp, &p0, &p1, &p2);
-                hs = SurfaceAt(S, hp, p0, p1, p2, h.b0, h.b1, h.b2);
+                hs = SurfaceAt<(TM & kTravShapes) != 0>(S, hp, p0, p1, p2, h.b0, h.b1, h.b2);
             }
             if (med >= 0) {
                 const MediumRef m = MediumAt(S, med);
@@ -2255,14 +2262,25 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
     const int other = ~((1 << kMatDiffuseT) | (1 << 3) | (1 << kMatCoatedDiffuseT) | (1 << kMatCoatedConductorT) |
                         (1 << kMatDiffuseTransmissionT));
     const size_t surfLds = VolTablesLdsBytes(S) + kNS * kBlock * sizeof(float);
-    if (S.matTypeMask & other) hipLaunchKernelGGL(k_vsurface<false>, gW, block, surfLds, s, S, st, v, wf);
-    else hipLaunchKernelGGL(k_vsurface<true>, gW, block, surfLds, s, S, st, v, wf);
-    if (S.nInfinite > 0) hipLaunchKernelGGL(k_vescaped, gW, block, VolTablesLdsBytes(S), s, S, st, v, wf);
-    if (wf == S.maxDepth) return hipGetLastError();
-    if (S.matTypeMask & (1 << 3)) hipLaunchKernelGGL(k_viface, gW, block, 0, s, S, st, v, wf);
-    if (S.matTypeMask & ((1 << kMatCoatedDiffuseT) | (1 << kMatCoatedConductorT) | (1 << kMatDiffuseTransmissionT)))
-        hipLaunchKernelGGL(k_vlayered, gW, block, 0, s, S, st, v, wf);
-    hipLaunchKernelGGL(k_vscatter, gW, block, 0, s, S, st, v, wf);
+#define VOL_REST(EXT) \
+    if (wf == S.maxDepth) return hipGetLastError(); \
+    if (S.matTypeMask & (1 << 3)) hipLaunchKernelGGL(k_viface<EXT>, gW, block, 0, s, S, st, v, wf); \
+    if (S.matTypeMask & ((1 << kMatCoatedDiffuseT) | (1 << kMatCoatedConductorT) | (1 << kMatDiffuseTransmissionT))) \
+        hipLaunchKernelGGL(k_vlayered<EXT>, gW, block, 0, s, S, st, v, wf); \
+    hipLaunchKernelGGL(k_vscatter<EXT>, gW, block, 0, s, S, st, v, wf);
+    // Ext: analytic shapes or image lights in the scene (their paths compiled in)
+    if (S.nShapes > 0 || S.nEnv > 0) {
+        if (S.matTypeMask & other) hipLaunchKernelGGL((k_vsurface<false, true>), gW, block, surfLds, s, S, st, v, wf);
+        else hipLaunchKernelGGL((k_vsurface<true, true>), gW, block, surfLds, s, S, st, v, wf);
+        if (S.nInfinite > 0) hipLaunchKernelGGL(k_vescaped<true>, gW, block, VolTablesLdsBytes(S), s, S, st, v, wf);
+        VOL_REST(true);
+    } else {
+        if (S.matTypeMask & other) hipLaunchKernelGGL((k_vsurface<false, false>), gW, block, surfLds, s, S, st, v, wf);
+        else hipLaunchKernelGGL((k_vsurface<true, false>), gW, block, surfLds, s, S, st, v, wf);
+        if (S.nInfinite > 0) hipLaunchKernelGGL(k_vescaped<false>, gW, block, VolTablesLdsBytes(S), s, S, st, v, wf);
+        VOL_REST(false);
+    }
+#undef VOL_REST
     if (S.media.allGrey) {
 #define K_VSHADOW_GREY(tm) k_vshadow_grey<tm>
         PBRT_LAUNCH_TRAVERSAL(S, K_VSHADOW_GREY, gT, block, VolStackBytes(S), s, S, st, v, wf);

@@ -57,8 +57,11 @@ __global__ void __launch_bounds__(kBlock) k_camera(DeviceScene S, PathState st, 
 // NMatQ = 1: every material is diffuse (one material queue); 3: one queue per material type;
 // kClosestMix (4): one queue per type, and mix materials resolved per hit (into st.hitMat)
 constexpr int kClosestMix = 4;
+// sorted: this depth's rays were binned (k_raybin_*): lane j traces st.raySort[j] and only
+// writes its hit record; k_classify then enqueues the hits in record order.
 template <int NMatQ_, int TM>
-__global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_closest(DeviceScene S, PathState st, int depth, int timed) {
+__global__ void __launch_bounds__(kBlock, TraversalWaves(TM))
+    k_closest(DeviceScene S, PathState st, int depth, int timed, int sorted) {
     constexpr bool kMix = NMatQ_ == kClosestMix;
     constexpr int NMatQ = kMix ? kNumMatTypes : NMatQ_;
     const QueueView rays = LoadQueue(st, depth, kCntRay);
@@ -94,22 +97,49 @@ __global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_closest(DeviceSc
     for (int base = blockIdx.x * blockDim.x; base < count; base += gridDim.x * blockDim.x) {
         const int j = base + threadIdx.x;
         bool active = j < count;
-        const int qi = active ? QueueSlot(rays, j) : 0;  // record index of this depth
+        int qi = 0;  // record index of this depth
         int prim = -1;
         TriHit h;
         TravCount tc;
         if (active) {
-            const V3 o(rec.ray[qi], rec.ray[N + qi], rec.ray[2 * N + qi]);
-            const V3 d(rec.ray[3 * N + qi], rec.ray[4 * N + qi], rec.ray[5 * N + qi]);
+            V3 o, d;
+            if (sorted) {
+                const float4 a = st.raySort[j], b = st.raySort[(size_t)N + j];
+                qi = __float_as_int(a.w);
+                o = V3(a.x, a.y, a.z);
+                d = V3(b.x, b.y, b.z);
+            } else {
+                qi = QueueSlot(rays, j);
+                o = V3(rec.ray[qi], rec.ray[N + qi], rec.ray[2 * N + qi]);
+                d = V3(rec.ray[3 * N + qi], rec.ray[4 * N + qi], rec.ray[5 * N + qi]);
+            }
             prim = Traverse<false, TM>(S, L, o, d, kInfinity, &h, &tc);
+            if (sorted) {
+                hitPrim[qi] = prim;
+                if (prim >= 0) {
+                    hitB[qi] = h.b0;
+                    hitB[N + qi] = h.b1;
+                    hitB[2 * N + qi] = h.b2;
+                    hitB[3 * N + qi] = h.t;
+                    if constexpr (kMix) {
+                        int mat = S.primMaterial[prim];
+                        if (S.matType[mat] == kMatMixT) mat = ResolveMixMaterial(S, prim, mat, h.b0, h.b1, h.b2, d);
+                        st.hitMat[depth & 1][qi] = mat;
+                    }
+                }
+            }
             // the hit record feeds the material stage, and at maxDepth only k_emissive
-            if (prim >= 0 && (shade || S.primLight[prim] >= 0)) {
+            if (!sorted && prim >= 0 && (shade || S.primLight[prim] >= 0)) {
                 hitPrim[qi] = prim;
                 hitB[qi] = h.b0;
                 hitB[N + qi] = h.b1;
                 hitB[2 * N + qi] = h.b2;
                 hitB[3 * N + qi] = h.t;
             }
+        }
+        if (sorted) {  // k_classify enqueues
+            TravStatsAdd(st.stats, kStatsSectionBase + 8, active, tc);
+            continue;
         }
         // EnqueueWorkAfterIntersection / Miss (intersect.h:48-156): misses to the escaped-ray
         // queue (infinite lights only), emissive hits to the hit-area-light queue, every hit
@@ -136,6 +166,155 @@ __global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_closest(DeviceSc
         }
         queues.Append(pred, qi);
         TravStatsAdd(st.stats, kStatsSectionBase + 8, active, tc);
+    }
+    queues.FlushAll();
+}
+
+// ---- Ray binning for HBM-resident trees (depth >= 1).  Secondary rays arrive in record order
+// (roughly pixel order, random directions), so a wave's 64 traversals diverge through a tree
+// far larger than L2.  A counting sort by origin cell (8^3 Morton grid over the scene bounds)
+// and direction octant groups rays that visit the same nodes: k_raybin_hist counts the bins,
+// k_raybin_scan turns counts into offsets, k_raybin_scatter writes each ray with its record
+// index to st.raySort in bin order.  k_closest<sorted> traces that order and writes hit
+// records only; k_classify then enqueues the hits in record order, so the material queues --
+// and the shade kernels' beta reads -- keep their coalesced layout.  Films are unchanged (each
+// path's arithmetic is independent of the order rays are traced in).
+constexpr int kRayBins = 4096, kBinBlock = 1024, kBinItems = 4;
+__device__ inline int RayBinKey(const DeviceScene &S, const V3 &o, const V3 &d) {
+    int c[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float t = (o[a] - S.rayBinLo[a]) * S.rayBinScale[a];
+        c[a] = (int)fminf(fmaxf(t, 0.f), 7.f);  // NaN -> 0
+    }
+    int m = 0;
+#pragma unroll
+    for (int b = 0; b < 3; ++b)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) m |= ((c[a] >> b) & 1) << (3 * b + a);
+    return m << 3 | (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
+}
+__device__ inline void RayAt(const PathState &st, int depth, int qi, V3 *o, V3 *d) {
+    const PathRecords &rec = st.rec[depth & 1];
+    const int N = st.NR;
+    *o = V3(rec.ray[qi], rec.ray[N + qi], rec.ray[2 * N + qi]);
+    *d = V3(rec.ray[3 * N + qi], rec.ray[4 * N + qi], rec.ray[5 * N + qi]);
+}
+__global__ void __launch_bounds__(kBinBlock) k_raybin_hist(DeviceScene S, PathState st, int depth) {
+    const QueueView rays = LoadQueue(st, depth, kCntRay);
+    if ((int)(blockIdx.x * blockDim.x) >= rays.total) return;
+    __shared__ int h[kRayBins];
+    for (int i = threadIdx.x; i < kRayBins; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < rays.total; j += gridDim.x * blockDim.x) {
+        V3 o, d;
+        RayAt(st, depth, QueueSlot(rays, j), &o, &d);
+        atomicAdd(&h[RayBinKey(S, o, d)], 1);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kRayBins; i += blockDim.x)
+        if (h[i]) atomicAdd(&st.rayBins[i], h[i]);
+}
+// one block: exclusive offsets into rayBins[kRayBins..], counts cleared for the next depth
+__global__ void __launch_bounds__(kBinBlock) k_raybin_scan(PathState st) {
+    __shared__ int part[kBinBlock];
+    constexpr int kPer = kRayBins / kBinBlock;
+    const int t = threadIdx.x;
+    int v[kPer], sum = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) sum += (v[k] = st.rayBins[kPer * t + k]);
+    part[t] = sum;
+    __syncthreads();
+    for (int off = 1; off < kBinBlock; off <<= 1) {
+        const int x = t >= off ? part[t - off] : 0;
+        __syncthreads();
+        part[t] += x;
+        __syncthreads();
+    }
+    int run = part[t] - sum;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        st.rayBins[kRayBins + kPer * t + k] = run;
+        run += v[k];
+        st.rayBins[kPer * t + k] = 0;
+    }
+}
+__global__ void __launch_bounds__(kBinBlock) k_raybin_scatter(DeviceScene S, PathState st, int depth) {
+    constexpr int kChunk = kBinBlock * kBinItems;
+    const QueueView rays = LoadQueue(st, depth, kCntRay);
+    if ((int)(blockIdx.x * kChunk) >= rays.total) return;
+    __shared__ int h[kRayBins];
+    int *offs = st.rayBins + kRayBins;
+    const size_t NR = st.NR;
+    for (int c0 = blockIdx.x * kChunk; c0 < rays.total; c0 += gridDim.x * kChunk) {
+        for (int i = threadIdx.x; i < kRayBins; i += blockDim.x) h[i] = 0;
+        __syncthreads();
+        int key[kBinItems], rank[kBinItems], qi[kBinItems];
+        V3 o[kBinItems], d[kBinItems];
+#pragma unroll
+        for (int k = 0; k < kBinItems; ++k) {
+            const int j = c0 + k * kBinBlock + threadIdx.x;
+            key[k] = -1;
+            if (j < rays.total) {
+                qi[k] = QueueSlot(rays, j);
+                RayAt(st, depth, qi[k], &o[k], &d[k]);
+                key[k] = RayBinKey(S, o[k], d[k]);
+                rank[k] = atomicAdd(&h[key[k]], 1);
+            }
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < kRayBins; i += blockDim.x) {
+            const int n = h[i];
+            if (n) h[i] = atomicAdd(&offs[i], n);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kBinItems; ++k) {
+            if (key[k] < 0) continue;
+            const int pos = h[key[k]] + rank[k];
+            st.raySort[pos] = make_float4(o[k].x, o[k].y, o[k].z, __int_as_float(qi[k]));
+            st.raySort[NR + pos] = make_float4(d[k].x, d[k].y, d[k].z, 0.f);
+        }
+        __syncthreads();
+    }
+}
+// EnqueueWorkAfterIntersection / Miss for a sorted depth, in record order (k_closest's queues)
+template <int NMatQ_>
+__global__ void __launch_bounds__(kBlock) k_classify(DeviceScene S, PathState st, int depth) {
+    constexpr bool kMix = NMatQ_ == kClosestMix;
+    constexpr int NMatQ = kMix ? kNumMatTypes : NMatQ_;
+    const QueueView rays = LoadQueue(st, depth, kCntRay);
+    if ((int)(blockIdx.x * blockDim.x) >= rays.total) return;
+    const int shard = ProducerShard();
+    const int *hitPrim = st.hitPrim[depth & 1];
+    const bool shade = depth < S.maxDepth;
+    constexpr int kQ = 2 + NMatQ, kCap = 128;
+    __shared__ int qBuf[(kBlock / 64) * kQ * kCap];
+    int *qCnt[kQ] = {&st.counters[CounterIndex(depth, kCntEscaped, shard)],
+                     &st.counters[CounterIndex(depth, kCntEmissive, shard)]};
+    int *qArr[kQ] = {st.escQ + shard * st.capS, st.emitQ + shard * st.capS};
+#pragma unroll
+    for (int t = 0; t < NMatQ; ++t) {
+        qCnt[2 + t] = &st.counters[CounterIndex(depth, MatCounter(t), shard)];
+        qArr[2 + t] = st.matQ[t] + shard * st.capS;
+    }
+    WaveQueues<kQ, kCap> queues(qBuf, qCnt, qArr);
+    for (int base = blockIdx.x * blockDim.x; base < rays.total; base += gridDim.x * blockDim.x) {
+        const int j = base + threadIdx.x;
+        const bool active = j < rays.total;
+        const int qi = active ? QueueSlot(rays, j) : 0;
+        const int prim = active ? hitPrim[qi] : -1;
+        bool pred[kQ] = {S.nInfinite > 0 && active && prim < 0,
+                         S.nAreaLights > 0 && active && prim >= 0 && S.primLight[prim] >= 0};
+        if constexpr (NMatQ == 1) {
+            pred[2] = shade && active && prim >= 0;
+        } else {
+            int type = -1;
+            if (shade && active && prim >= 0) type = S.matType[kMix ? st.hitMat[depth & 1][qi] : S.primMaterial[prim]];
+#pragma unroll
+            for (int t = 0; t < NMatQ; ++t) pred[2 + t] = type == t;
+        }
+        queues.Append(pred, qi);
     }
     queues.FlushAll();
 }
@@ -253,6 +432,8 @@ __global__ void __launch_bounds__(kBlock) k_escaped(DeviceScene S, PathState st,
 // HandleEmissiveIntersection (integrator.cpp:539-573) over the hit-area-light queue.  The MIS
 // context (pbrt's prevIntrCtx: p, n, ns, pError of the previous surface) is rebuilt from the
 // previous bounce's hit record with the same TriangleSurface arithmetic that produced it.
+// Ext: the scene has analytic shapes (their surfaces and solid-angle pdfs are compiled in)
+template <bool Ext>
 __global__ void __launch_bounds__(kBlock) k_emissive(DeviceScene S, PathState st, int depth) {
     const int N = st.NR, NL = st.N;  // record stride, pixel-sample stride (L)
     const QueueView emit = LoadQueue(st, depth, kCntEmissive);
@@ -285,7 +466,7 @@ __global__ void __launch_bounds__(kBlock) k_emissive(DeviceScene S, PathState st
         PrimVerts(S, prim, &p0, &p1, &p2);
         const int light = S.primLight[prim];
         const bool flip = S.primFlip[prim];
-        TriSurface surf = SurfaceAt(S, prim, p0, p1, p2, b0, b1, b2);
+        TriSurface surf = SurfaceAt<Ext>(S, prim, p0, p1, p2, b0, b1, b2);
         (void)flip;
         V3 wo = Normalize(-rd);
         const DeviceAreaLight Ld = S.lights[light];
@@ -297,10 +478,10 @@ __global__ void __launch_bounds__(kBlock) k_emissive(DeviceScene S, PathState st
             V3 q0, q1, q2;
             PrimVerts(S, pp, &q0, &q1, &q2);
             // prevIntrCtx = LightSampleContext(pi, n, ns) of the previous surface
-            TriSurface prev = SurfaceAt(S, pp, q0, q1, q2, pb0, pb1, pb2);
+            TriSurface prev = SurfaceAt<Ext>(S, pp, q0, q1, q2, pb0, pb1, pb2);
             float lightChoicePDF = LightPMF(S, prev.p, prev.ns, light);
             float lightPDF;
-            if (S.nShapes > 0 && prim >= S.nTris) {
+            if (Ext && prim >= S.nTris) {
                 lightPDF = lightChoicePDF * ShapeLightPDF(S, prim - S.nTris, prev.p, prev.pErr, prev.n, prev.ns, -wo);
             } else {
                 TriShading lsh;
@@ -497,7 +678,9 @@ __device__ __forceinline__ RaySamples GenerateRaySamples(const DeviceScene &S, c
 // common case, compiled without the other paths so the kernel's hot code stays small.
 // Tex (host-chosen: some material is textured): reflectance textures are evaluated per hit
 // (surfscatter.cpp:74-137: uv derivatives, then GetBxDF's texture evaluation).
-template <bool Lean, bool Tex = false>
+// Ext (host-chosen: the scene has analytic shapes or image infinite lights): their surface,
+// light-sampling and radiance paths are compiled in.
+template <bool Lean, bool Tex = false, bool Ext = false>
 __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(DeviceScene S, PathState st, int depth) {
     const QueueView mats = LoadQueue(st, depth, kCntMat);
     if ((int)(blockIdx.x * blockDim.x) >= mats.total) return;  // no work
@@ -548,7 +731,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
             PrimVerts(S, prim, &p0, &p1, &p2);
             const int mat = Lean ? S.primMaterial[prim] : HitMaterial(S, st, depth, ri, prim);
             TriSurface surf = Lean ? TriangleSurface(p0, p1, p2, b0, b1, b2, S.primFlip[prim], nullptr)
-                                   : SurfaceAt(S, prim, p0, p1, p2, b0, b1, b2);
+                                   : SurfaceAt<Ext>(S, prim, p0, p1, p2, b0, b1, b2);
             float4 mc = matsL[mat];
             int mflags = matConstL[mat];  // bit 0: constant R, bit 1: R != 0 at every wavelength
             bool constant = mflags & 1;
@@ -620,11 +803,11 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                                                                &li, &lpmf)
                             : SampleLightT<DeviceLightNode, true>(SL, S.lightNodes, cp, ns, dUc, &li, &lpmf);
                     LiSample ls;
-                    if (sampled && SampleLiSurface<Lean, true>(S, lightsL, li, cp, n, ns, dU0, dU1, &ls)) {
+                    if (sampled && SampleLiSurface<Lean, true, Ext>(S, lightsL, li, cp, n, ns, dU0, dU1, &ls)) {
                         const V3 wi = ls.wi;
                         const V3 wiL = frame.ToLocal(wi);
                         if (woL.z != 0 && woL.z * wiL.z > 0) {  // DiffuseBxDF::f != 0
-                            if constexpr (!Lean) {
+                            if constexpr (!Lean && Ext) {
                                 envLe = ls.envLe;
                                 envC = ls.env;
                             }
@@ -678,18 +861,18 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                     float *bf = bfLds + threadIdx.x;
                     const float rd2 = 1 / d2;
                     const bool d2Ok = DivFastOk(d2);
-                    if (Lean || (lay.denseInLds && S.nPointSpot == 0 && S.nEnv == 0))
+                    if (Lean || (lay.denseInLds && S.nPointSpot == 0 && (!Ext || S.nEnv == 0)))
                         ShadeSpectralPass<false, false>(depth, (const LdsF *)denseLds + spec * kDenseN, sensorL, bf,
                                                         rfun, lambda0, scale, d2, rd2, d2Ok, absdotL, invDenom,
                                                         absdotB, pdf, rpdf, pdfOk, etaScale, &acc, &neeNz, &betaNz,
                                                         &mx);
                     else if (lay.denseInLds)
-                        ShadeSpectralPass<true, !Lean>(depth, (const LdsF *)denseLds + spec * kDenseN, sensorL, bf,
+                        ShadeSpectralPass<true, !Lean && Ext>(depth, (const LdsF *)denseLds + spec * kDenseN, sensorL, bf,
                                                        rfun, lambda0, scale, d2, rd2, d2Ok, absdotL, invDenom,
                                                        absdotB, pdf, rpdf, pdfOk, etaScale, &acc, &neeNz, &betaNz,
                                                        &mx, envLe, envC);
                     else
-                        ShadeSpectralPass<true, !Lean>(depth, S.dense + spec * kDenseN, sensorL, bf, rfun, lambda0,
+                        ShadeSpectralPass<true, !Lean && Ext>(depth, S.dense + spec * kDenseN, sensorL, bf, rfun, lambda0,
                                                        scale, d2, rd2, d2Ok, absdotL, invDenom, absdotB, pdf, rpdf,
                                                        pdfOk, etaScale, &acc, &neeNz, &betaNz, &mx, envLe, envC);
                 }
@@ -784,7 +967,8 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
 // the light-sampling code of rough surfaces is compiled out.
 // Tex (host-chosen: some material is textured): textured roughness (both types) and conductor
 // reflectance are evaluated per hit (materials.h:182-204, :491-511).
-template <int MT, bool Smooth = false, bool Tex = false>
+// Ext: as k_shade_diffuse's.
+template <int MT, bool Smooth = false, bool Tex = false, bool Ext = false>
 __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(DeviceScene S, PathState st, int depth) {
     const QueueView mats = LoadQueue(st, depth, MatCounter(MT));
     if ((int)(blockIdx.x * blockDim.x) >= mats.total) return;  // no work
@@ -828,7 +1012,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
             V3 p0, p1, p2;
             PrimVerts(S, prim, &p0, &p1, &p2);
             const int mat = HitMaterial(S, st, depth, ri, prim);
-            const TriSurface surf = SurfaceAt(S, prim, p0, p1, p2, b0, b1, b2);
+            const TriSurface surf = SurfaceAt<Ext>(S, prim, p0, p1, p2, b0, b1, b2);
             const V3 wo = Normalize(-rd);
             const V3 n = surf.n, ns = surf.ns;
             const RaySamples rs = GenerateRaySamples<MT == kMatDielectricT>(S, T, st, slot, sidx, d0);
@@ -889,7 +1073,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
                 float lpmf;
                 LiSample ls;
                 if (SampleLightT<DeviceLightNode, true>(T.SL, T.SL.lightNodes, cp, ns, rs.dUc, &li, &lpmf) &&
-                    SampleLiSurface<false, true>(S, T.lightsL, li, cp, n, ns, rs.dU0, rs.dU1, &ls, cpErr)) {
+                    SampleLiSurface<false, true, Ext>(S, T.lightsL, li, cp, n, ns, rs.dU0, rs.dU1, &ls, cpErr)) {
                     const V3 lp = ls.lp, lpe = ls.lpe, ln = ls.ln;
                     {
                         const V3 wi = ls.wi;
@@ -1067,7 +1251,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
 // Full = false (host-chosen per material type): every textured parameter of the type is a single
 // image (or constant) leaf filtered without EWA -- the register-file interpreter and the EWA
 // filter are not compiled in.
-template <int MT, bool Full>
+template <int MT, bool Full, bool Ext = false>
 __global__ void __launch_bounds__(kBlock) k_texture(DeviceScene S, PathState st, int depth) {
     const QueueView mats = LoadQueue(st, depth, MatCounter(MT));
     if ((int)(blockIdx.x * blockDim.x) >= mats.total) return;  // no work
@@ -1093,7 +1277,7 @@ __global__ void __launch_bounds__(kBlock) k_texture(DeviceScene S, PathState st,
         if (mt.x < 0 && mt.y < 0) continue;
         V3 p0, p1, p2;
         PrimVerts(S, prim, &p0, &p1, &p2);
-        const TriSurface surf = SurfaceAt(S, prim, p0, p1, p2, hitB[ri], hitB[N + ri], hitB[2 * N + ri]);
+        const TriSurface surf = SurfaceAt<Ext>(S, prim, p0, p1, p2, hitB[ri], hitB[N + ri], hitB[2 * N + ri]);
         const TexEvalCtx tc = HitTexCtx(S, surf);
         if (mt.x >= 0) {
             const DeviceTexProgram pg = S.tex.progs[mt.x];
@@ -1333,18 +1517,34 @@ hipError_t LaunchCamera(const DeviceScene &S, const PathState &st, int nActive, 
     return hipGetLastError();
 }
 hipError_t LaunchClosest(const DeviceScene &S, const PathState &st, int depth, int maxCount, int timed,
-                         hipStream_t s) {
+                         hipStream_t s, bool sorted) {
     const dim3 grid(TraversalGridFor(maxCount)), block(kBlock);
     const bool multi = S.matTypeMask & ~1;
+    const int so = sorted ? 1 : 0;
 #define K_CLOSEST_MIX(tm) k_closest<kClosestMix, tm>
 #define K_CLOSEST_MULTI(tm) k_closest<kNumMatTypes, tm>
 #define K_CLOSEST_ONE(tm) k_closest<1, tm>
-    if (st.hitMat[0]) PBRT_LAUNCH_TRAVERSAL(S, K_CLOSEST_MIX, grid, block, StackBytes(S), s, S, st, depth, timed);
-    else if (multi) PBRT_LAUNCH_TRAVERSAL(S, K_CLOSEST_MULTI, grid, block, StackBytes(S), s, S, st, depth, timed);
-    else PBRT_LAUNCH_TRAVERSAL(S, K_CLOSEST_ONE, grid, block, StackBytes(S), s, S, st, depth, timed);
+    if (st.hitMat[0]) PBRT_LAUNCH_TRAVERSAL(S, K_CLOSEST_MIX, grid, block, StackBytes(S), s, S, st, depth, timed, so);
+    else if (multi) PBRT_LAUNCH_TRAVERSAL(S, K_CLOSEST_MULTI, grid, block, StackBytes(S), s, S, st, depth, timed, so);
+    else PBRT_LAUNCH_TRAVERSAL(S, K_CLOSEST_ONE, grid, block, StackBytes(S), s, S, st, depth, timed, so);
 #undef K_CLOSEST_MIX
 #undef K_CLOSEST_MULTI
 #undef K_CLOSEST_ONE
+    return hipGetLastError();
+}
+hipError_t LaunchRayBin(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s) {
+    const int g = std::max(1, std::min(2048, (maxCount + kBinBlock - 1) / kBinBlock));
+    hipLaunchKernelGGL(k_raybin_hist, dim3(std::min(g, 1024)), dim3(kBinBlock), 0, s, S, st, depth);
+    hipLaunchKernelGGL(k_raybin_scan, dim3(1), dim3(kBinBlock), 0, s, st);
+    const int gs = std::max(1, std::min(2048, (maxCount + kBinBlock * kBinItems - 1) / (kBinBlock * kBinItems)));
+    hipLaunchKernelGGL(k_raybin_scatter, dim3(gs), dim3(kBinBlock), 0, s, S, st, depth);
+    return hipGetLastError();
+}
+hipError_t LaunchClassify(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s) {
+    const dim3 grid(GridFor(maxCount)), block(kBlock);
+    if (st.hitMat[0]) hipLaunchKernelGGL(k_classify<kClosestMix>, grid, block, 0, s, S, st, depth);
+    else if (S.matTypeMask & ~1) hipLaunchKernelGGL(k_classify<kNumMatTypes>, grid, block, 0, s, S, st, depth);
+    else hipLaunchKernelGGL(k_classify<1>, grid, block, 0, s, S, st, depth);
     return hipGetLastError();
 }
 hipError_t LaunchEscaped(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s) {
@@ -1352,7 +1552,8 @@ hipError_t LaunchEscaped(const DeviceScene &S, const PathState &st, int depth, i
     return hipGetLastError();
 }
 hipError_t LaunchEmissive(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s) {
-    hipLaunchKernelGGL(k_emissive, dim3(SmallGridFor(maxCount)), dim3(kBlock), 0, s, S, st, depth);
+    if (S.nShapes > 0) hipLaunchKernelGGL(k_emissive<true>, dim3(SmallGridFor(maxCount)), dim3(kBlock), 0, s, S, st, depth);
+    else hipLaunchKernelGGL(k_emissive<false>, dim3(SmallGridFor(maxCount)), dim3(kBlock), 0, s, S, st, depth);
     return hipGetLastError();
 }
 // Dynamic LDS of a shade launch: the layout up to this depth's Halton permutation tables, which
@@ -1367,7 +1568,8 @@ hipError_t LaunchTexture(const DeviceScene &S, const PathState &st, int depth, i
     const dim3 grid(SmallGridFor(maxCount));
 #define K_TEX(mt)                                                                             \
     do {                                                                                      \
-        if (full) hipLaunchKernelGGL((k_texture<mt, true>), grid, dim3(kBlock), 0, s, S, st, depth);  \
+        if (S.nShapes > 0) hipLaunchKernelGGL((k_texture<mt, true, true>), grid, dim3(kBlock), 0, s, S, st, depth); \
+        else if (full) hipLaunchKernelGGL((k_texture<mt, true>), grid, dim3(kBlock), 0, s, S, st, depth);  \
         else hipLaunchKernelGGL((k_texture<mt, false>), grid, dim3(kBlock), 0, s, S, st, depth);      \
     } while (0)
     if (type == kMatDiffuseT) K_TEX(kMatDiffuseT);
@@ -1378,35 +1580,38 @@ hipError_t LaunchTexture(const DeviceScene &S, const PathState &st, int depth, i
 }
 hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int depth, int maxCount, bool lean,
                               hipStream_t s) {
-    if (S.textured)
-        hipLaunchKernelGGL((k_shade_diffuse<false, true>), dim3(ShadeGridFor(maxCount)), dim3(kBlock),
-                           ShadeLdsBytes(S, depth), s, S, st, depth);
-    else if (lean)
-        hipLaunchKernelGGL(k_shade_diffuse<true>, dim3(ShadeGridFor(maxCount)), dim3(kBlock), ShadeLdsBytes(S, depth),
-                           s, S, st, depth);
-    else
-        hipLaunchKernelGGL(k_shade_diffuse<false>, dim3(ShadeGridFor(maxCount)), dim3(kBlock),
-                           ShadeLdsBytes(S, depth), s, S, st, depth);
+    const dim3 grid(ShadeGridFor(maxCount)), block(kBlock);
+    const size_t lds = ShadeLdsBytes(S, depth);
+    const bool ext = S.nShapes > 0 || S.nEnv > 0;
+    if (S.textured && ext) hipLaunchKernelGGL((k_shade_diffuse<false, true, true>), grid, block, lds, s, S, st, depth);
+    else if (S.textured) hipLaunchKernelGGL((k_shade_diffuse<false, true>), grid, block, lds, s, S, st, depth);
+    else if (lean) hipLaunchKernelGGL(k_shade_diffuse<true>, grid, block, lds, s, S, st, depth);
+    else if (ext) hipLaunchKernelGGL((k_shade_diffuse<false, false, true>), grid, block, lds, s, S, st, depth);
+    else hipLaunchKernelGGL(k_shade_diffuse<false>, grid, block, lds, s, S, st, depth);
     return hipGetLastError();
 }
 hipError_t LaunchShadeMicrofacet(const DeviceScene &S, const PathState &st, int depth, int type, int maxCount,
                                  hipStream_t s) {
-    if (S.textured) {
-        if (type == kMatDielectricT)
-            hipLaunchKernelGGL((k_shade_microfacet<kMatDielectricT, false, true>), dim3(ShadeGridFor(maxCount)),
-                               dim3(kBlock), ShadeLdsBytes(S, depth, true), s, S, st, depth);
-        else
-            hipLaunchKernelGGL((k_shade_microfacet<kMatConductorT, false, true>), dim3(ShadeGridFor(maxCount)),
-                               dim3(kBlock), ShadeLdsBytes(S, depth, true), s, S, st, depth);
-    } else if (type == kMatDielectricT && S.smoothDielectrics)
-        hipLaunchKernelGGL((k_shade_microfacet<kMatDielectricT, true>), dim3(ShadeGridFor(maxCount)), dim3(kBlock),
-                           ShadeLdsBytes(S, depth, true), s, S, st, depth);
-    else if (type == kMatDielectricT)
-        hipLaunchKernelGGL(k_shade_microfacet<kMatDielectricT>, dim3(ShadeGridFor(maxCount)), dim3(kBlock),
-                           ShadeLdsBytes(S, depth, true), s, S, st, depth);
-    else
-        hipLaunchKernelGGL(k_shade_microfacet<kMatConductorT>, dim3(ShadeGridFor(maxCount)), dim3(kBlock),
-                           ShadeLdsBytes(S, depth, true), s, S, st, depth);
+    const dim3 grid(ShadeGridFor(maxCount)), block(kBlock);
+    const size_t lds = ShadeLdsBytes(S, depth, true);
+    const bool ext = S.nShapes > 0 || S.nEnv > 0, diel = type == kMatDielectricT;
+#define K_MF(mt, smooth, tex, ex) hipLaunchKernelGGL((k_shade_microfacet<mt, smooth, tex, ex>), grid, block, lds, s, S, st, depth)
+    if (ext) {
+        if (diel && S.textured) K_MF(kMatDielectricT, false, true, true);
+        else if (diel) K_MF(kMatDielectricT, false, false, true);
+        else if (S.textured) K_MF(kMatConductorT, false, true, true);
+        else K_MF(kMatConductorT, false, false, true);
+    } else if (S.textured) {
+        if (diel) K_MF(kMatDielectricT, false, true, false);
+        else K_MF(kMatConductorT, false, true, false);
+    } else if (diel && S.smoothDielectrics) {
+        K_MF(kMatDielectricT, true, false, false);
+    } else if (diel) {
+        K_MF(kMatDielectricT, false, false, false);
+    } else {
+        K_MF(kMatConductorT, false, false, false);
+    }
+#undef K_MF
     return hipGetLastError();
 }
 hipError_t LaunchShadow(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s) {

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """C4 k_closest HBM traffic record (round 3): rocprofv3 PMC passes FETCH_SIZE, WRITE_SIZE and
-TCC_HIT/TCC_MISS (each its own run, tools/gpu_profile_r03.sh) -> per-launch bytes and bytes
+TCC_HIT/TCC_MISS (each its own run, tools/pmc.sh) -> per-launch bytes and bytes
 per ray next to the algorithmic bytes of the bench line.  FETCH_SIZE is doubled (gfx950
 correction, MI355X_MICROARCH.md HBM section); values are KB per dispatch.
 Usage: python tools/c4_pmc_json.py gpurun_out/r03p profiles/r03_c4_closest_pmc.json HEAD"""

@@ -401,6 +401,7 @@ struct pbrt_context {
     DevBuf<DeviceDeltaLight> deltaLights;
     DevBuf<int> primOrig, matType, matSpectra, plOffsets;
     DevBuf<float> matParams, plLambda, plValue, triShade, matLayer, dispL0;
+    DevBuf<uint16_t> plIndex;
     DevBuf<int> dispTerm;
     DevBuf<uint8_t> primFlip;
     DevBuf<uint32_t> lightBitTrail, permOffset, permNDigits, permBase;
@@ -685,6 +686,14 @@ static void BuildDevice(pbrt_context *c) {
         c->plOffsets.Upload(po);
         c->plLambda.Upload(pll);
         c->plValue.Upload(plv);
+        // PiecewiseLinearEvalIdx's start segments: FindInterval at each integer wavelength
+        std::vector<uint16_t> pli;
+        for (size_t j = 0; j + 1 < po.size(); ++j) {
+            pli.resize(pli.size() + kPlIndexN);
+            BuildPlIndex(pll.data() + po[j], po[j + 1] - po[j], pli.data() + pli.size() - kPlIndexN);
+        }
+        if (pli.empty()) pli.push_back(0);
+        c->plIndex.Upload(pli);
     }
     std::vector<int> lp, ls, lt;
     std::vector<float> lsc, la;
@@ -917,6 +926,7 @@ static void BuildDevice(pbrt_context *c) {
     S.plOffsets = c->plOffsets.p;
     S.plLambda = c->plLambda.p;
     S.plValue = c->plValue.p;
+    S.plIndex = c->plIndex.p;
     S.matTypeMask = 0;
     for (auto &m : s.materials) S.matTypeMask |= 1 << m.type;
     S.regularize = s.regularize ? 1 : 0;
@@ -2310,8 +2320,11 @@ int pbrt_debug_named_spectrum(const char *name, const float *lambda, int n, floa
     try {
         if (!name || !lambda || !out) return Fail("null argument");
         PLSpectrumDesc d = NamedPiecewiseLinear(name);
+        // the kernels' indexed evaluation (the same segment and arithmetic as PiecewiseLinearEval)
+        uint16_t idx[kPlIndexN];
+        BuildPlIndex(d.lambda.data(), (int)d.lambda.size(), idx);
         for (int i = 0; i < n; ++i)
-            out[i] = PiecewiseLinearEval(d.lambda.data(), d.value.data(), (int)d.lambda.size(), lambda[i]);
+            out[i] = PiecewiseLinearEvalIdx(d.lambda.data(), d.value.data(), (int)d.lambda.size(), idx, lambda[i]);
         return 0;
     } catch (const std::exception &e) {
         return Fail(e.what());

@@ -1002,6 +1002,31 @@ PHD float PiecewiseLinearEval(F *lam, F *val, int n, float l) {
     float t = (l - lam[lo]) / (lam[lo + 1] - lam[lo]);
     return Lerpf(t, val[lo], val[lo + 1]);
 }
+// The same evaluation started from a per-nanometre segment table: idx[b] = the FindInterval
+// result at lambda = kPlIndexLo + b.  FindInterval is monotone in lambda, so for l >= that
+// wavelength the answer is idx[b] or a later segment, reached by the forward walk (knots are
+// >= 1 nm apart in pbrt's named spectra: at most one step).  Same segment, same arithmetic.
+constexpr int kPlIndexLo = 360, kPlIndexN = 471;  // 360..830 nm (SampleVisibleWavelengths)
+template <typename F, typename I>
+PHD float PiecewiseLinearEvalIdx(F *lam, F *val, int n, I *idx, float l) {
+    if (n == 0 || l < lam[0] || l > lam[n - 1]) return 0;
+    const int b = (int)l - kPlIndexLo;
+    int lo = idx[b < 0 ? 0 : (b >= kPlIndexN ? kPlIndexN - 1 : b)];
+    float l1 = lam[lo + 1];
+    while (lo < n - 2 && l1 <= l) l1 = lam[++lo + 1];
+    const float l0 = lam[lo];
+    float t = (l - l0) / (l1 - l0);
+    return Lerpf(t, val[lo], val[lo + 1]);
+}
+// idx[b] for PiecewiseLinearEvalIdx (host): FindInterval at kPlIndexLo + b
+inline void BuildPlIndex(const float *lam, int n, uint16_t *idx) {
+    for (int b = 0; b < kPlIndexN; ++b) {
+        const float l = (float)(kPlIndexLo + b);
+        int o = 0;
+        while (o < n - 2 && lam[o + 1] <= l) ++o;
+        idx[b] = (uint16_t)o;
+    }
+}
 // RoughnessToAlpha (util/scattering.h:192)
 PHD float RoughnessToAlpha(float roughness) { return std::sqrt(roughness); }
 

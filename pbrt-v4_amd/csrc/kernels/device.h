@@ -138,6 +138,9 @@ struct DeviceScene {
     // piecewise-linear spectra (conductor eta / k): spectrum s spans [plOffsets[s], plOffsets[s+1])
     const int *plOffsets;
     const float *plLambda, *plValue;
+    // per spectrum and integer wavelength 360..830 nm: the segment FindInterval picks at that
+    // wavelength (PiecewiseLinearEvalIdx starts its search there)
+    const uint16_t *plIndex;  // [nPL][kPlIndexN]
     // area lights
     int nAreaLights;
     const int *lightPrim;  // leaf-order prim

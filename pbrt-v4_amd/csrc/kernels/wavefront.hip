@@ -1041,12 +1041,13 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
                 if (etaSpec >= 0) {
                     const int a = S.plOffsets[etaSpec], na = S.plOffsets[etaSpec + 1] - a;
                     const int b = S.plOffsets[kSpec], nb = S.plOffsets[kSpec + 1] - b;
+                    const uint16_t *ia = S.plIndex + (size_t)etaSpec * kPlIndexN, *ib = S.plIndex + (size_t)kSpec * kPlIndexN;
                     if (lay.plInLds) {
-                        *e = PiecewiseLinearEval(T.plLamL + a, T.plValL + a, na, lam);
-                        *k = PiecewiseLinearEval(T.plLamL + b, T.plValL + b, nb, lam);
+                        *e = PiecewiseLinearEvalIdx(T.plLamL + a, T.plValL + a, na, ia, lam);
+                        *k = PiecewiseLinearEvalIdx(T.plLamL + b, T.plValL + b, nb, ib, lam);
                     } else {
-                        *e = PiecewiseLinearEval(S.plLambda + a, S.plValue + a, na, lam);
-                        *k = PiecewiseLinearEval(S.plLambda + b, S.plValue + b, nb, lam);
+                        *e = PiecewiseLinearEvalIdx(S.plLambda + a, S.plValue + a, na, ia, lam);
+                        *k = PiecewiseLinearEvalIdx(S.plLambda + b, S.plValue + b, nb, ib, lam);
                     }
                 } else {
                     float rv = SigmoidPolynomial(mc.x, mc.y, mc.z, lam);

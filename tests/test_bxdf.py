@@ -54,6 +54,23 @@ def test_named_spectra_match_reference(pa, oracle, golden):
         assert same(oracle.named_spectrum(raw["named:" + name], lam), want), name
 
 
+def test_indexed_spectrum_lookup_matches_search(pa, oracle):
+    """The kernels' per-nanometre segment index (PiecewiseLinearEvalIdx) against the oracle's
+    FindInterval search: random wavelengths over 360..830 nm plus every knot and its float
+    neighbours, for every named spectrum the library carries, bit for bit."""
+    raw = json.loads(DATA.read_text())
+    rng = np.random.default_rng(11)
+    names = [k[len("named:"):] for k in raw if k.startswith("named:")]
+    assert len(names) >= 20
+    for name in names:
+        knots = np.asarray(raw["named:" + name][0::2] if isinstance(raw["named:" + name], list) else [], np.float32)
+        lam = np.concatenate([rng.uniform(360, 830, 4000).astype(np.float32), knots,
+                              np.nextafter(knots, np.float32(0)), np.nextafter(knots, np.float32(1e4)),
+                              np.arange(360, 831, dtype=np.float32)])
+        lam = lam[(lam >= 360) & (lam <= 830)].astype(np.float32)
+        assert same(pa.named_spectrum(name, lam), oracle.named_spectrum(raw["named:" + name], lam)), name
+
+
 def _cases(seed, n):
     rng = np.random.default_rng(seed)
 

@@ -1041,11 +1041,14 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
                 if (etaSpec >= 0) {
                     const int a = S.plOffsets[etaSpec], na = S.plOffsets[etaSpec + 1] - a;
                     const int b = S.plOffsets[kSpec], nb = S.plOffsets[kSpec + 1] - b;
-                    const uint16_t *ia = S.plIndex + (size_t)etaSpec * kPlIndexN, *ib = S.plIndex + (size_t)kSpec * kPlIndexN;
+                    // small sets (LDS-resident knots) search in LDS; large ones (named metals,
+                    // through L1/L2) start from the per-nanometre segment table
                     if (lay.plInLds) {
-                        *e = PiecewiseLinearEvalIdx(T.plLamL + a, T.plValL + a, na, ia, lam);
-                        *k = PiecewiseLinearEvalIdx(T.plLamL + b, T.plValL + b, nb, ib, lam);
+                        *e = PiecewiseLinearEval(T.plLamL + a, T.plValL + a, na, lam);
+                        *k = PiecewiseLinearEval(T.plLamL + b, T.plValL + b, nb, lam);
                     } else {
+                        const uint16_t *ia = S.plIndex + (size_t)etaSpec * kPlIndexN;
+                        const uint16_t *ib = S.plIndex + (size_t)kSpec * kPlIndexN;
                         *e = PiecewiseLinearEvalIdx(S.plLambda + a, S.plValue + a, na, ia, lam);
                         *k = PiecewiseLinearEvalIdx(S.plLambda + b, S.plValue + b, nb, ib, lam);
                     }
@@ -1566,7 +1569,11 @@ static size_t ShadeLdsBytes(const DeviceScene &S, int depth, bool withPl = false
 }
 hipError_t LaunchTexture(const DeviceScene &S, const PathState &st, int depth, int type, bool full, int maxCount,
                          hipStream_t s) {
-    const dim3 grid(SmallGridFor(maxCount));
+    // the material queue is large and the kernel latency-bound: enough blocks for every SIMD's
+    // wave slots (a 256-block grid left C4's k_texture at one wave per SIMD), each block's LDS
+    // tables amortised over its grid-stride items
+    const int g = (maxCount + kBlock - 1) / kBlock;
+    const dim3 grid(g < 1 ? 1 : (g > 2048 ? 2048 : g));
 #define K_TEX(mt)                                                                             \
     do {                                                                                      \
         if (S.nShapes > 0) hipLaunchKernelGGL((k_texture<mt, true, true>), grid, dim3(kBlock), 0, s, S, st, depth); \

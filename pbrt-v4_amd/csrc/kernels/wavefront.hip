@@ -1068,141 +1068,144 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
             const bool smooth = tr.EffectivelySmooth();
             const bool reflective = MT == kMatConductorT || eta != 1;
             const bool transmissive = MT == kMatDielectricT;
-            // ---- light sampling + shadow ray (surfscatter.cpp:252-326)
+            // ---- light sample geometry (surfscatter.cpp:252-326) and BSDF::Sample_f geometry
+            // (surfscatter.cpp:183-190), then ONE pass over the wavelengths for both: each eta_i,
+            // k_i (conductor) is looked up once and feeds the light sample's f_i and the
+            // sampled direction's f_i, with the light term formed from beta_i before the update
+            // overwrites it -- the same products per wavelength as two separate passes.
+            bool haveL = false, haveB = false;
+            ConductorTerms ctL{}, ctB{};
+            float fdL = 0, absdotL = 0, invDenomL = 0;
+            LiSample ls;
             if (!Smooth && !smooth) {
                 V3 cp = pi, cpErr = pe;  // LightSampleContext: the offset point is exact
                 if (reflective && !transmissive) cp = OffsetRayOrigin(pi, pe, n, wo), cpErr = V3(0, 0, 0);
                 else if (transmissive && reflective) cp = OffsetRayOrigin(pi, pe, n, -wo), cpErr = V3(0, 0, 0);
                 int li;
                 float lpmf;
-                LiSample ls;
                 if (SampleLightT<DeviceLightNode, true>(T.SL, T.SL.lightNodes, cp, ns, rs.dUc, &li, &lpmf) &&
                     SampleLiSurface<false, true, Ext>(S, T.lightsL, li, cp, n, ns, rs.dU0, rs.dU1, &ls, cpErr)) {
-                    const V3 lp = ls.lp, lpe = ls.lpe, ln = ls.ln;
-                    {
-                        const V3 wi = ls.wi;
-                        const V3 wiL = frame.ToLocal(wi);
-                        if (woL.z != 0) {
-                            // BSDF::f / BSDF::PDF (bsdf.h:60-135)
-                            float fd = 0, bsdfPDF = 0;
-                            ConductorTerms ct{};
-                            bool fAny;
-                            if constexpr (MT == kMatDielectricT) {
-                                fd = DielectricEval(eta, tr, woL, wiL, &bsdfPDF);
-                                fAny = fd != 0;
-                            } else {
-                                ct = ConductorEval(tr, woL, wiL);
-                                bsdfPDF = ct.pdf;
-                                fAny = ct.ok;  // f_i may still vanish; a zero Ld adds nothing
-                            }
-                            if (fAny) {
-                                const float absdot = AbsDotN(ns, wi);
-                                const float lightPDF = ls.pdf * lpmf;
-                                if (ls.delta) bsdfPDF = 0;  // IsDeltaLight: no BSDF MIS weight
-                                const float invDenom = 1 / Avg31(bsdfPDF + lightPDF);
-                                const float *dense = lay.denseInLds ? nullptr : S.dense + ls.spectrum * kDenseN;
-                                const LdsF *denseL = (const LdsF *)T.denseLds + ls.spectrum * kDenseN;
-                                SensorAcc acc;
-                                bool nz = false;
-#pragma unroll 2
-                                for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next()) {
-                                    const int off = DenseOffset(it.lam);
-                                    float Le = ls.Le(off < 0 ? 0.f : (lay.denseInLds ? float(denseL[off]) : dense[off]),
-                                                     it.lam);
-                                    if (S.nPointSpot > 0) Le = Le / ls.d2;  // pbrt: SampledSpectrum / DistanceSquared
-                                    nz |= Le != 0;
-                                    float f = fd;
-                                    if constexpr (MT == kMatConductorT) {
-                                        float e, k;
-                                        etaK(it.lam, it.i, &e, &k);
-                                        f = ConductorF(ct, e, k);
-                                    }
-                                    acc.Add(T.sensorL, off, bf[it.i * kBlock] * f * absdot * Le * invDenom, it.i == 0);
-                                }
-                                if (nz) {
-                                    sOrg = OffsetRayOrigin(pi, pe, n, lp - pi);
-                                    const V3 pt = OffsetRayOrigin(lp, lpe, ln, sOrg - lp);
-                                    sDir = pt - sOrg;
-                                    sL = V3(S.imagingRatio * (acc.sx / kNSpectrumSamples),
-                                            S.imagingRatio * (acc.sy / kNSpectrumSamples),
-                                            S.imagingRatio * (acc.sz / kNSpectrumSamples));
-                                    pushShadow = true;
-                                }
-                            }
+                    const V3 wiL = frame.ToLocal(ls.wi);
+                    if (woL.z != 0) {
+                        // BSDF::f / BSDF::PDF (bsdf.h:60-135)
+                        float bsdfPDF = 0;
+                        bool fAny;
+                        if constexpr (MT == kMatDielectricT) {
+                            fdL = DielectricEval(eta, tr, woL, wiL, &bsdfPDF);
+                            fAny = fdL != 0;
+                        } else {
+                            ctL = ConductorEval(tr, woL, wiL);
+                            bsdfPDF = ctL.pdf;
+                            fAny = ctL.ok;  // f_i may still vanish; a zero Ld adds nothing
+                        }
+                        if (fAny) {
+                            absdotL = AbsDotN(ns, ls.wi);
+                            const float lightPDF = ls.pdf * lpmf;
+                            if (ls.delta) bsdfPDF = 0;  // IsDeltaLight: no BSDF MIS weight
+                            invDenomL = 1 / Avg31(bsdfPDF + lightPDF);
+                            haveL = true;
                         }
                     }
                 }
             }
-            // ---- BSDF::Sample_f + RR + indirect ray (surfscatter.cpp:183-250)
+            V3 wi;
+            float pdf = 1, fdB = 0, absdotB = 0, etaScale = 1;
+            bool specular = false;
             if (woL.z != 0) {
-                bool ok;
+                bool ok, transmission;
                 V3 wiL;
-                float pdf, fd = 0, etap = 1;
-                bool specular, transmission;
-                ConductorTerms ct{};
+                float etap = 1;
                 if constexpr (MT == kMatDielectricT) {
                     const BxSample bs = DielectricSample(eta, tr, woL, rs.iUc, rs.iU0, rs.iU1);
                     ok = bs.ok && bs.f != 0;
                     wiL = bs.wi;
                     pdf = bs.pdf;
-                    fd = bs.f;
+                    fdB = bs.f;
                     etap = bs.etap;
                     specular = bs.flags & kBxSpecular;
                     transmission = bs.flags & kBxTransmission;
                 } else {
-                    ct = ConductorSample(tr, woL, rs.iU0, rs.iU1);
-                    ok = ct.ok;
-                    wiL = ct.wi;
-                    pdf = ct.pdf;
-                    specular = ct.specular;
+                    ctB = ConductorSample(tr, woL, rs.iU0, rs.iU1);
+                    ok = ctB.ok;
+                    wiL = ctB.wi;
+                    pdf = ctB.pdf;
+                    specular = ctB.specular;
                     transmission = false;
                 }
                 if (ok && pdf != 0 && wiL.z != 0) {
-                    const V3 wi = frame.FromLocal(wiL);
-                    const float absdot = AbsDotN(ns, wi);
-                    float etaScale = depth > 0 ? rec.etaScale[ri] : 1.f;
+                    wi = frame.FromLocal(wiL);
+                    absdotB = AbsDotN(ns, wi);
+                    etaScale = depth > 0 ? rec.etaScale[ri] : 1.f;
                     if (transmission) etaScale *= Sqr(etap);
-                    const float avgRu = Avg31(1.f);
-                    float mx = -kInfinity;
-                    bool fAny = MT == kMatDielectricT;
+                    haveB = true;
+                }
+            }
+            if (haveL || haveB) {
+                const int lspec = haveL ? ls.spectrum : 0;
+                const float *dense = lay.denseInLds ? nullptr : S.dense + lspec * kDenseN;
+                const LdsF *denseL = (const LdsF *)T.denseLds + lspec * kDenseN;
+                const float avgRu = Avg31(1.f);
+                SensorAcc acc;
+                bool nzL = false, fAnyB = MT == kMatDielectricT;
+                float mx = -kInfinity;
 #pragma unroll 2
-                    for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next()) {
-                        float f = fd;
+                for (SpectralIter it(lambda0); it.i < kNSpectrumSamples; it.Next()) {
+                    float e = 1, k = 0;
+                    if constexpr (MT == kMatConductorT) etaK(it.lam, it.i, &e, &k);
+                    const float b = bf[it.i * kBlock];
+                    if (haveL) {
+                        const int off = DenseOffset(it.lam);
+                        float Le = ls.Le(off < 0 ? 0.f : (lay.denseInLds ? float(denseL[off]) : dense[off]), it.lam);
+                        if (S.nPointSpot > 0) Le = Le / ls.d2;  // pbrt: SampledSpectrum / DistanceSquared
+                        nzL |= Le != 0;
+                        float f = fdL;
+                        if constexpr (MT == kMatConductorT) f = ConductorF(ctL, e, k);
+                        acc.Add(T.sensorL, off, b * f * absdotL * Le * invDenomL, it.i == 0);
+                    }
+                    if (haveB) {
+                        float f = fdB;
                         if constexpr (MT == kMatConductorT) {
-                            float e, k;
-                            etaK(it.lam, it.i, &e, &k);
-                            f = ConductorF(ct, e, k);
-                            fAny |= f != 0;
+                            f = ConductorF(ctB, e, k);
+                            fAnyB |= f != 0;
                         }
-                        const float nbv = bf[it.i * kBlock] * f * absdot / pdf;
+                        const float nbv = b * f * absdotB / pdf;
                         bf[it.i * kBlock] = nbv;
                         mx = fmaxf(mx, nbv * etaScale / avgRu);
                     }
-                    if (fAny) {
-                        bool kill = false;
-                        float q = 0;
-                        if (mx < 1 && depth >= 1) {
-                            q = fmaxf(0.f, 1 - mx);
-                            kill = rs.rr < q;
-                        }
-                        if (!kill) {
-                            const bool rrScale = mx < 1 && depth >= 1;
-                            bool nz = false;
+                }
+                if (haveL && nzL) {
+                    sOrg = OffsetRayOrigin(pi, pe, n, ls.lp - pi);
+                    const V3 pt = OffsetRayOrigin(ls.lp, ls.lpe, ls.ln, sOrg - ls.lp);
+                    sDir = pt - sOrg;
+                    sL = V3(S.imagingRatio * (acc.sx / kNSpectrumSamples), S.imagingRatio * (acc.sy / kNSpectrumSamples),
+                            S.imagingRatio * (acc.sz / kNSpectrumSamples));
+                    pushShadow = true;
+                }
+                // ---- Russian roulette (surfscatter.cpp:212-222) and the indirect ray
+                if (haveB && fAnyB) {
+                    bool kill = false;
+                    float q = 0;
+                    if (mx < 1 && depth >= 1) {
+                        q = fmaxf(0.f, 1 - mx);
+                        kill = rs.rr < q;
+                    }
+                    if (!kill) {
+                        const bool rrScale = mx < 1 && depth >= 1;
+                        bool nz = false;
 #pragma unroll 4
-                            for (int i = 0; i < kNSpectrumSamples; ++i) {
-                                float nbv = bf[i * kBlock];
-                                if (rrScale) nbv /= 1 - q;
-                                nz |= nbv != 0;
-                                bf[i * kBlock] = nbv;
-                            }
-                            if (nz) {
-                                nOrg = OffsetRayOrigin(pi, pe, n, wi);
-                                nDir = wi;
-                                nRl = 1.f / pdf;
-                                nEta = etaScale;
-                                nFlags = (specular ? 1 : 0) | ((!specular || (inFlags & 2)) ? 2 : 0);
-                                pushRay = true;
-                            }
+                        for (int i = 0; i < kNSpectrumSamples; ++i) {
+                            float nbv = bf[i * kBlock];
+                            if (rrScale) nbv /= 1 - q;
+                            nz |= nbv != 0;
+                            bf[i * kBlock] = nbv;
+                        }
+                        if (nz) {
+                            nOrg = OffsetRayOrigin(pi, pe, n, wi);
+                            nDir = wi;
+                            nRl = 1.f / pdf;
+                            nEta = etaScale;
+                            nFlags = (specular ? 1 : 0) | ((!specular || (inFlags & 2)) ? 2 : 0);
+                            pushRay = true;
                         }
                     }
                 }

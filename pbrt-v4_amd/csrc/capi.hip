@@ -1175,6 +1175,8 @@ static void BuildDevice(pbrt_context *c) {
         // surface wavefront; PBRT_AMD_RAY_SORT=0/1 overrides)
         const char *rs = getenv("PBRT_AMD_RAY_SORT");
         c->rayBinning = !c->volumetric && (rs ? atoi(rs) != 0 : S.ldsTris == 0);
+        const char *rk = getenv("PBRT_AMD_RAY_BIN_KEY");
+        S.rayBinMode = rk ? std::max(0, std::min(2, atoi(rk))) : 0;
     }
 
     // film

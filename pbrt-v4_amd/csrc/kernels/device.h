@@ -211,6 +211,7 @@ struct DeviceScene {
     int stackSize;  // BVH traversal stack entries (uint2 groups) per lane (BVH8::maxStack)
     float bvhAbsMax[3];  // bound on |plane coordinate| per axis (traversal box-test margins)
     float rayBinLo[3], rayBinScale[3];  // ray-binning grid: cell = (o - lo) * scale, 8 per axis
+    int rayBinMode;                     // RayBinKey's key layout (PBRT_AMD_RAY_BIN_KEY)
     int ldsNodes, ldsTris;  // BVH8 nodes / triangles cached in LDS by the traversal kernels
     ShadeLdsLayout shadeLds;
     DeviceMedia media;

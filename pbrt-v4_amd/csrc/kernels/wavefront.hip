@@ -181,18 +181,35 @@ __global__ void __launch_bounds__(kBlock, TraversalWaves(TM))
 // path's arithmetic is independent of the order rays are traced in).
 constexpr int kRayBins = 4096, kBinBlock = 1024, kBinItems = 4;
 __device__ inline int RayBinKey(const DeviceScene &S, const V3 &o, const V3 &d) {
+    // S.rayBinMode: 0 = origin 8^3 x octant; 1 = origin 4^3 x direction 8x8 (octahedral);
+    // 2 = origin 2^3 x direction 32x16
+    const int mode = S.rayBinMode;
+    const int cBits = mode == 0 ? 3 : (mode == 1 ? 2 : 1);
+    const float cScale = mode == 0 ? 1.f : (mode == 1 ? 0.5f : 0.25f);
+    const float cMax = (float)((1 << cBits) - 1);
     int c[3];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        const float t = (o[a] - S.rayBinLo[a]) * S.rayBinScale[a];
-        c[a] = (int)fminf(fmaxf(t, 0.f), 7.f);  // NaN -> 0
+        const float t = (o[a] - S.rayBinLo[a]) * S.rayBinScale[a] * cScale;
+        c[a] = (int)fminf(fmaxf(t, 0.f), cMax);  // NaN -> 0
     }
     int m = 0;
-#pragma unroll
-    for (int b = 0; b < 3; ++b)
+    for (int b = 0; b < cBits; ++b)
 #pragma unroll
         for (int a = 0; a < 3; ++a) m |= ((c[a] >> b) & 1) << (3 * b + a);
-    return m << 3 | (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
+    if (mode == 0) return m << 3 | (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
+    // octahedral direction cell
+    const float l1 = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
+    float x = l1 > 0 ? d.x / l1 : 0.f, y = l1 > 0 ? d.y / l1 : 0.f;
+    if (d.z < 0) {
+        const float ox = x;
+        x = (1 - fabsf(y)) * (ox < 0 ? -1.f : 1.f);
+        y = (1 - fabsf(ox)) * (y < 0 ? -1.f : 1.f);
+    }
+    const int ub = mode == 1 ? 3 : 5, vb = mode == 1 ? 3 : 4;
+    const int u = (int)fminf(fmaxf((x + 1) * 0.5f * (1 << ub), 0.f), (float)((1 << ub) - 1));
+    const int v = (int)fminf(fmaxf((y + 1) * 0.5f * (1 << vb), 0.f), (float)((1 << vb) - 1));
+    return m << (ub + vb) | u << vb | v;
 }
 __device__ inline void RayAt(const PathState &st, int depth, int qi, V3 *o, V3 *d) {
     const PathRecords &rec = st.rec[depth & 1];

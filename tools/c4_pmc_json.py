@@ -3,7 +3,8 @@
 TCC_HIT/TCC_MISS (each its own run, tools/pmc.sh) -> per-launch bytes and bytes
 per ray next to the algorithmic bytes of the bench line.  FETCH_SIZE is doubled (gfx950
 correction, MI355X_MICROARCH.md HBM section); values are KB per dispatch.
-Usage: python tools/c4_pmc_json.py gpurun_out/r03p profiles/r03_c4_closest_pmc.json HEAD"""
+Usage: python tools/c4_pmc_json.py gpurun_out/pmc BENCH_LINE.json profiles/r03_c4_closest_pmc.json HEAD
+(gpurun_out/pmc as tools/pmc.sh writes it: fetch/, write/, tcc/ passes)"""
 import csv
 import json
 import sys
@@ -21,17 +22,17 @@ def per_dispatch(csv_path, counter, kernel="k_closest"):
     return sum(v) / len(v), len(v)
 
 
-src, dst = Path(sys.argv[1]), Path(sys.argv[2])
-head = sys.argv[3] if len(sys.argv) > 3 else "unknown"
-fetch, n = per_dispatch(src / "pmc_c4" / "FETCH_SIZE" / "run_counter_collection.csv", "FETCH_SIZE")
-write, _ = per_dispatch(src / "pmc_c4" / "WRITE_SIZE" / "run_counter_collection.csv", "WRITE_SIZE")
-hit, _ = per_dispatch(src / "pmc_c4" / "TCC_HIT_sum" / "run_counter_collection.csv", "TCC_HIT_sum")
-miss, _ = per_dispatch(src / "pmc_c4" / "TCC_HIT_sum" / "run_counter_collection.csv", "TCC_MISS_sum")
-bench = json.loads((src / "r03_c4_bench.json").read_text())
+src, bench_path, dst = Path(sys.argv[1]), Path(sys.argv[2]), Path(sys.argv[3])
+head = sys.argv[4] if len(sys.argv) > 4 else "unknown"
+fetch, n = per_dispatch(src / "fetch" / "run_counter_collection.csv", "FETCH_SIZE")
+write, _ = per_dispatch(src / "write" / "run_counter_collection.csv", "WRITE_SIZE")
+hit, _ = per_dispatch(src / "tcc" / "run_counter_collection.csv", "TCC_HIT_sum")
+miss, _ = per_dispatch(src / "tcc" / "run_counter_collection.csv", "TCC_MISS_sum")
+bench = json.loads(bench_path.read_text().strip().splitlines()[-1])
 rays = bench["roofline"]["rays_per_launch"]
 fetch_b, write_b = 2 * 1024 * fetch, 1024 * write
 rec = {
-    "kernel": "k_closest (C4: 9,994,244 triangles, quantised BVH8 nodes, 6 waves/SIMD)",
+    "kernel": "k_closest (C4: 9,994,244 triangles, quantised BVH8 nodes, 6 waves/SIMD, rays binned at depth >= 1)",
     "head": head,
     "dispatches": n,
     "fetch_size_kb_mean": fetch,

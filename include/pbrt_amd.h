@@ -383,6 +383,13 @@ int pbrt_debug_queue_counts(pbrt_context *ctx, int32_t *counts, int n);
 /* profiling build only (PBRT_AMD_SECTION_TIMING): summed wave cycles per kernel section
  * since the last pbrt_reset_stats; zeros in the product build */
 int pbrt_debug_kernel_sections(pbrt_context *ctx, uint64_t *cycles, int n);
+/* queue-integrity check of the volumetric wavefront (diagnostics): with it on, every queue
+ * slot the surface, layered and medium-scattering stages count must be written; a slot that is
+ * counted but left unwritten (a "hole") is counted, printed by the device and neutralised.
+ * pbrt_debug_queue_holes returns the holes found since its last call and resets the count.
+ * PBRT_AMD_QUEUE_CHECK=1 turns the check on from the environment. */
+int pbrt_debug_set_queue_check(int on);
+int pbrt_debug_queue_holes(int *holes);
 
 #ifdef __cplusplus
 }

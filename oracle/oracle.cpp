@@ -1220,6 +1220,7 @@ struct OShape {
         }
     }
     bool sphere() const { return kind == 1; }
+    bool cylinder() const { return kind == 4; }
     bool patch() const { return kind == 3; }
     bool flip() const { return ((flags & 1) != 0) != ((flags & 2) != 0); }
     // BilinearPatch ctor (shapes.cpp:1041-1071) with IsRectangle (shapes.h:1511-1532)
@@ -1246,6 +1247,7 @@ struct OShape {
     }
     Float Area() const {
         if (patch()) return patchArea;
+        if (cylinder()) return (c - b) * a * d;  // Cylinder::Area (shapes.h:620)
         return sphere() ? d * a * (c - b) : d * Float(0.5) * (Sqr(b) - Sqr(c));
     }
     // IntersectBilinearPatch (shapes.h:1279-1347)
@@ -1510,6 +1512,48 @@ struct OShape {
         XPointI(r2o, ro3, oi);
         XVectorExact(r2o, rd, di);
         const Vec o(oi[0].Mid(), oi[1].Mid(), oi[2].Mid()), dd(di[0].Mid(), di[1].Mid(), di[2].Mid());
+        if (cylinder()) {
+            // Cylinder::BasicIntersect (shapes.h:628-722): x-y quadratic, hit reprojected to r
+            const Float radius = a, zMin = b, zMax = c, phiMax = d;
+            const OInterval A = ISqr(di[0]) + ISqr(di[1]);
+            const OInterval B = 2.f * (di[0] * oi[0] + di[1] * oi[1]);
+            const OInterval C = ISqr(oi[0]) + ISqr(oi[1]) - ISqr(OInterval(radius));
+            const OInterval fct = B / (2.f * A);
+            const OInterval vx = oi[0] - fct * di[0], vy = oi[1] - fct * di[1];
+            const OInterval len = ISqrt(ISqr(vx) + ISqr(vy));
+            const OInterval disc = 4.f * A * (OInterval(radius) + len) * (OInterval(radius) - len);
+            if (disc.lo < 0) return false;
+            const OInterval root = ISqrt(disc);
+            const OInterval q = B.Mid() < 0 ? -.5f * (B - root) : -.5f * (B + root);
+            OInterval t0 = q / A, t1 = C / q;
+            if (t0.lo > t1.lo) std::swap(t0, t1);
+            if (t0.hi > tMax || t1.lo <= 0) return false;
+            OInterval ts = t0;
+            if (ts.lo <= 0) {
+                ts = t1;
+                if (ts.hi > tMax) return false;
+            }
+            Vec p;
+            Float phi;
+            auto hitAt = [&](OInterval t) {
+                p = o + t.Mid() * dd;
+                const Float hitRad = std::sqrt(Sqr(p.x) + Sqr(p.y));
+                p.x *= radius / hitRad;
+                p.y *= radius / hitRad;
+                phi = Phi(p);
+            };
+            hitAt(ts);
+            if (p.z < zMin || p.z > zMax || phi > phiMax) {
+                if (ts == t1) return false;
+                ts = t1;
+                if (t1.hi > tMax) return false;
+                hitAt(ts);
+                if (p.z < zMin || p.z > zMax || phi > phiMax) return false;
+            }
+            *tHit = ts.Mid();
+            *pObj = p;
+            return true;
+        }
         if (!sphere()) {
             if (dd.z == 0) return false;
             const Float th = (a - o.z) / dd.z;
@@ -1584,6 +1628,12 @@ struct OShape {
             const Float sinTheta = SafeSqrt(1 - Sqr(cosTheta));
             dpdv = (tzMax - tzMin) * Vec(pHit.z * cp, pHit.z * sp, -radius * sinTheta);
             pErr = gamma(5) * Abs(pHit);
+        } else if (cylinder()) {  // Cylinder::InteractionFromIntersection (shapes.h:725-760)
+            u = phi / d;
+            v = (pHit.z - b) / (c - b);
+            dpdu = Vec(-d * pHit.y, d * pHit.x, 0);
+            dpdv = Vec(0, 0, c - b);
+            pErr = gamma(3) * Abs(Vec(pHit.x, pHit.y, 0));
         } else {
             const Float radius = b, inner = c, phiMax = d;
             u = phi / phiMax;
@@ -1628,6 +1678,21 @@ struct OShape {
             XPointI(o2r, pi, po);
             ss.p = Vec(po[0].Mid(), po[1].Mid(), po[2].Mid());
             ss.err = Vec(po[0].Err(), po[1].Err(), po[2].Err());
+            ss.n = n;
+        } else if (cylinder()) {  // Cylinder::Sample(u) (shapes.h:772-793)
+            const Float z = Lerp(u0, b, c), ph = u1 * d;
+            Vec pObj(a * CRCos(ph), a * CRSin(ph), z);
+            const Float hitRad = std::sqrt(Sqr(pObj.x) + Sqr(pObj.y));
+            pObj.x *= a / hitRad;
+            pObj.y *= a / hitRad;
+            const Vec pErr = gamma(3) * Abs(Vec(pObj.x, pObj.y, 0));
+            const OInterval pi[3] = {OInterval::VE(pObj.x, pErr.x), OInterval::VE(pObj.y, pErr.y), OInterval::VE(pObj.z, pErr.z)};
+            OInterval po[3];
+            XPointI(o2r, pi, po);
+            ss.p = Vec(po[0].Mid(), po[1].Mid(), po[2].Mid());
+            ss.err = Vec(po[0].Err(), po[1].Err(), po[2].Err());
+            Vec n = Normalize(XN(r2o, Vec(pObj.x, pObj.y, 0)));
+            if (flags & 1) n = -n;
             ss.n = n;
         } else {
             Float dx, dy;
@@ -1713,7 +1778,8 @@ struct OShape {
                       std::max(std::max(P[0].z, P[2].z), std::max(P[1].z, P[3].z)));
             return;
         }
-        const Vec lo = sphere() ? Vec(-a, -a, b) : Vec(-b, -b, a), hi = sphere() ? Vec(a, a, c) : Vec(b, b, a);
+        const bool rz = sphere() || cylinder();  // (-r, -r, zMin), (r, r, zMax)
+        const Vec lo = rz ? Vec(-a, -a, b) : Vec(-b, -b, a), hi = rz ? Vec(a, a, c) : Vec(b, b, a);
         *mn = Vec(Infinity, Infinity, Infinity);
         *mx = -*mn;
         for (int i = 0; i < 8; ++i) {
@@ -2052,7 +2118,7 @@ static std::vector<std::pair<int, LB>> SceneLightBounds(const pbrt_scene_flat *f
                     Float ct = std::min(std::min(Dot(n, n00), Dot(n, n01)), std::min(Dot(n, n10), Dot(n, n11)));
                     nb = Cone(n, Clamp(ct, -1, 1));
                 }
-            } else if (!sh.sphere()) {
+            } else if (!sh.sphere() && !sh.cylinder()) {
                 Vec n = OShape::XN(sh.r2o, Vec(0, 0, 1));
                 if (sh.flags & 1) n = -n;
                 nb = Cone(n, 1);

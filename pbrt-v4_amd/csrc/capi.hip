@@ -42,6 +42,8 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
                               hipStream_t s);
 hipError_t LaunchIntersectBatch(const DeviceScene &S, const float *rays, int n, int anyHit, int *outPrim,
                                 float *outHit, hipStream_t s);
+void SetQueueCheck(int on);
+int TakeQueueHoles();
 hipError_t LaunchIntersectTr(const DeviceScene &S, const float *rays, const int *medium, const float *lambda0, int n,
                              float *out, hipStream_t s);
 size_t SurfaceTraversalStaticLds(int tm);
@@ -392,6 +394,7 @@ struct pbrt_context {
     SceneDesc desc;
     BVH8 bvh;
     DeviceScene S{};
+    DevBuf<DeviceScene> sceneSelf;
     // scene buffers
     DevBuf<BVH8Node> nodes;
     DevBuf<BVH8QNode> qnodes;
@@ -1178,6 +1181,11 @@ static void BuildDevice(pbrt_context *c) {
         const char *rk = getenv("PBRT_AMD_RAY_BIN_KEY");
         S.rayBinMode = rk ? std::max(0, std::min(2, atoi(rk))) : 0;
     }
+
+    // the scene struct's device copy (DeviceScene::self)
+    c->sceneSelf.Alloc(1);
+    S.self = c->sceneSelf.p;
+    HIPCHECK(hipMemcpy(c->sceneSelf.p, &S, sizeof(DeviceScene), hipMemcpyHostToDevice));
 
     // film
     size_t npix = (size_t)s.xres * s.yres;
@@ -2462,6 +2470,15 @@ int pbrt_debug_bvh_stats(const pbrt_scene *scene, int64_t *out8) {
     }
 }
 
+int pbrt_debug_set_queue_check(int on) {
+    SetQueueCheck(on);
+    return 0;
+}
+int pbrt_debug_queue_holes(int *holes) {
+    if (!holes) return Fail("pbrt_debug_queue_holes: null output");
+    *holes = TakeQueueHoles();
+    return 0;
+}
 int pbrt_debug_queue_counts(pbrt_context *ctx, int32_t *counts, int n) {
     try {
         if (!ctx || !counts || n <= 0) return Fail("null argument");

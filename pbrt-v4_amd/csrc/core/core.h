@@ -1819,7 +1819,7 @@ PHD V3 XfPt(const float *m, V3 p) {
 }
 
 // Sphere and Disk (shapes.h:106-571): affine renderFromObject (o2r) and objectFromRender (r2o)
-enum ShapeKindT { kShapeSphereT = 1, kShapeDiskT = 2, kShapeBilinearT = 3 };
+enum ShapeKindT { kShapeSphereT = 1, kShapeDiskT = 2, kShapeBilinearT = 3, kShapeCylinderT = 4 };
 struct alignas(16) DeviceShape {
     float r2o[12], o2r[12];
     // sphere: radius, zMin, zMax, phiMax, thetaZMin, thetaZMax; disk: height, radius,
@@ -2178,6 +2178,7 @@ PHD void InvertBilinearUV(const DeviceShape &s, float px, float py, float *uo, f
 PHD float ShapeArea(const DeviceShape &s) {
     if (s.kind == kShapeBilinearT) return s.a;
     if (s.kind == kShapeSphereT) return s.d * s.a * (s.c - s.b);  // phiMax radius (zMax - zMin)
+    if (s.kind == kShapeCylinderT) return (s.c - s.b) * s.a * s.d;  // (zMax - zMin) radius phiMax
     return s.d * 0.5f * (Sqr(s.b) - Sqr(s.c));                    // phiMax / 2 (r^2 - ri^2)
 }
 // phi of an object-space hit (atan2, wrapped to [0, 2 pi))
@@ -2232,6 +2233,53 @@ PHD bool SphereIntersect(const DeviceShape &s, V3 ro, V3 rd, float tMax, float *
     }
     return false;
 }
+// Cylinder::BasicIntersect (shapes.h:628-722): the sphere's interval quadratic in x and y only,
+// the hit refined onto the radius in x-y
+PHD bool CylinderIntersect(const DeviceShape &s, V3 ro, V3 rd, float tMax, float *tHit, V3 *pObj) {
+    const float radius = s.a, zMin = s.b, zMax = s.c, phiMax = s.d;
+    const P3i oi = XfPointExact(s.r2o, ro), di = XfVectorExact(s.r2o, rd);
+    const Itv a = ItvSqr(di.x) + ItvSqr(di.y);
+    const Itv b = 2.f * (di.x * oi.x + di.y * oi.y);
+    const Itv c = ItvSqr(oi.x) + ItvSqr(oi.y) - ItvSqr(ItvExact(radius));
+    const Itv f = b / (2.f * a);
+    const Itv vx = oi.x - f * di.x, vy = oi.y - f * di.y;
+    const Itv length = ItvSqrt(ItvSqr(vx) + ItvSqr(vy));
+    const Itv discrim = 4.f * a * (ItvExact(radius) + length) * (ItvExact(radius) - length);
+    if (discrim.lo < 0) return false;
+    const Itv rootDiscrim = ItvSqrt(discrim);
+    const Itv q = ItvMid(b) < 0 ? -.5f * (b - rootDiscrim) : -.5f * (b + rootDiscrim);
+    Itv t0 = q / a, t1 = c / q;
+    if (t0.lo > t1.lo) {
+        const Itv t = t0;
+        t0 = t1;
+        t1 = t;
+    }
+    if (t0.hi > tMax || t1.lo <= 0) return false;
+    Itv tShapeHit = t0;
+    if (tShapeHit.lo <= 0) {
+        tShapeHit = t1;
+        if (tShapeHit.hi > tMax) return false;
+    }
+    const V3 o(ItvMid(oi.x), ItvMid(oi.y), ItvMid(oi.z)), d(ItvMid(di.x), ItvMid(di.y), ItvMid(di.z));
+    for (int pass = 0; pass < 2; ++pass) {
+        const float th = ItvMid(tShapeHit);
+        V3 pHit = o + th * d;
+        const float hitRad = std::sqrt(Sqr(pHit.x) + Sqr(pHit.y));
+        pHit.x *= radius / hitRad;
+        pHit.y *= radius / hitRad;
+        const float phi = ShapePhi(pHit);
+        if (pHit.z < zMin || pHit.z > zMax || phi > phiMax) {
+            if (pass == 1 || (tShapeHit.lo == t1.lo && tShapeHit.hi == t1.hi)) return false;
+            tShapeHit = t1;
+            if (t1.hi > tMax) return false;
+            continue;
+        }
+        *tHit = th;
+        *pObj = pHit;
+        return true;
+    }
+    return false;
+}
 // Disk::BasicIntersect (shapes.h:446-474)
 PHD bool DiskIntersect(const DeviceShape &s, V3 ro, V3 rd, float tMax, float *tHit, V3 *pObj) {
     const float height = s.a, radius = s.b, innerRadius = s.c, phiMax = s.d;
@@ -2255,6 +2303,7 @@ PHD bool ShapeIntersect(const DeviceShape &s, V3 ro, V3 rd, float tMax, float *t
         *pObj = V3(u, v, 0);
         return true;
     }
+    if (s.kind == kShapeCylinderT) return CylinderIntersect(s, ro, rd, tMax, tHit, pObj);
     return s.kind == kShapeSphereT ? SphereIntersect(s, ro, rd, tMax, tHit, pObj)
                                    : DiskIntersect(s, ro, rd, tMax, tHit, pObj);
 }
@@ -2278,6 +2327,14 @@ PHD TriSurface ShapeSurface(const DeviceShape &s, V3 pHit, const float *N = null
         const float sinTheta = SafeSqrt(1 - Sqr(cosTheta));
         dpdv = (thetaZMax - thetaZMin) * V3(pHit.z * cosPhi, pHit.z * sinPhi, -radius * sinTheta);
         pError = gamma(5) * Abs(pHit);
+    } else if (s.kind == kShapeCylinderT) {
+        // Cylinder::InteractionFromIntersection (shapes.h:725-760)
+        const float zMin = s.b, zMax = s.c, phiMax = s.d;
+        u = phi / phiMax;
+        v = (pHit.z - zMin) / (zMax - zMin);
+        dpdu = V3(-phiMax * pHit.y, phiMax * pHit.x, 0);
+        dpdv = V3(0, 0, zMax - zMin);
+        pError = gamma(3) * Abs(V3(pHit.x, pHit.y, 0));
     } else {
         const float height = s.a, radius = s.b, innerRadius = s.c, phiMax = s.d;
         u = phi / phiMax;
@@ -2326,6 +2383,23 @@ PHD ShapeSamplePt ShapeSampleArea(const DeviceShape &s, float u0, float u1) {
         const P3i pi = {ItvFromValueAndError(pObj.x, pObjError.x), ItvFromValueAndError(pObj.y, pObjError.y),
                         ItvFromValueAndError(pObj.z, pObjError.z)};
         XfPointInexact(s.o2r, pi, &r.p, &r.pErr);
+        r.n = n;
+    } else if (s.kind == kShapeCylinderT) {
+        // Cylinder::Sample(u) (shapes.h:772-793)
+        const float radius = s.a, zMin = s.b, zMax = s.c, phiMax = s.d;
+        const float z = Lerpf(u0, zMin, zMax), phi = u1 * phiMax;
+        float sp, cp;
+        SinCosf(phi, &sp, &cp);
+        V3 pObj(radius * cp, radius * sp, z);
+        const float hitRad = std::sqrt(Sqr(pObj.x) + Sqr(pObj.y));
+        pObj.x *= radius / hitRad;
+        pObj.y *= radius / hitRad;
+        const V3 pObjError = gamma(3) * Abs(V3(pObj.x, pObj.y, 0));
+        const P3i pi = {ItvFromValueAndError(pObj.x, pObjError.x), ItvFromValueAndError(pObj.y, pObjError.y),
+                        ItvFromValueAndError(pObj.z, pObjError.z)};
+        XfPointInexact(s.o2r, pi, &r.p, &r.pErr);
+        V3 n = Normalize(XfNormal(s.r2o, V3(pObj.x, pObj.y, 0)));
+        if (s.flags & 1) n = -n;
         r.n = n;
     } else {
         const float height = s.a, radius = s.b;
@@ -2500,7 +2574,7 @@ PHD void ShapeBounds(const DeviceShape &s, V3 *lo, V3 *hi) {
         return;
     }
     V3 a, b;
-    if (s.kind == kShapeSphereT) {
+    if (s.kind == kShapeSphereT || s.kind == kShapeCylinderT) {  // (-r, -r, zMin), (r, r, zMax)
         a = V3(-s.a, -s.a, s.b);
         b = V3(s.a, s.a, s.c);
     } else {

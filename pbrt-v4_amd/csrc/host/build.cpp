@@ -482,7 +482,7 @@ static void BuildLightBVH(SceneDesc &s) {
                     lb.w = Normalize(n);
                     lb.cosTheta_o = Clampf(cosTheta, -1, 1);
                 }
-            } else if (d.kind == kShapeSphereT) {
+            } else if (d.kind == kShapeSphereT || d.kind == kShapeCylinderT) {  // EntireSphere
                 lb.w = Normalize(V3(0, 0, 1));
                 lb.cosTheta_o = -1;
             } else {

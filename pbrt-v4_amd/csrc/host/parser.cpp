@@ -1008,6 +1008,13 @@ class Parser {
             s.sp[1] = (float)ps.GetFloat("radius", 1);
             s.sp[2] = (float)ps.GetFloat("innerradius", 0);
             s.sp[3] = (float)ps.GetFloat("phimax", 360);
+        } else if (type == "cylinder") {
+            // Cylinder::Create (shapes.cpp:136-146)
+            s.kind = kShapeCylinderT;
+            s.sp[0] = (float)ps.GetFloat("radius", 1);
+            s.sp[1] = (float)ps.GetFloat("zmin", -1);
+            s.sp[2] = (float)ps.GetFloat("zmax", 1);
+            s.sp[3] = (float)ps.GetFloat("phimax", 360);
         } else {
             throw Error(ps.loc + ": shape \"" + type + "\" is not supported yet");
         }
@@ -1060,6 +1067,11 @@ class Parser {
             d.e = std::acos(Clampf(std::min(zMin, zMax) / radius, -1, 1));
             d.f = std::acos(Clampf(std::max(zMin, zMax) / radius, -1, 1));
             d.d = radians(Clampf(phiMax, 0, 360));
+        } else if (s.kind == kShapeCylinderT) {  // Cylinder ctor (shapes.h:580-590)
+            d.a = s.sp[0];
+            d.b = std::min(s.sp[1], s.sp[2]);
+            d.c = std::max(s.sp[1], s.sp[2]);
+            d.d = radians(Clampf(s.sp[3], 0, 360));
         } else {
             d.a = s.sp[0];
             d.b = s.sp[1];
@@ -1630,7 +1642,7 @@ void Parser::Finish() {
             }
             ap.CheckUnused();
         }
-        if (s.kind == kShapeSphereT || s.kind == kShapeDiskT) {
+        if (s.kind == kShapeSphereT || s.kind == kShapeDiskT || s.kind == kShapeCylinderT) {
             AnalyticShape(s, rfo, mat, lightSpectrum, lightScale, twoSided, power, mediumOf);
             continue;
         }

@@ -316,7 +316,7 @@ __device__ inline Halton StartPixelSample(const DeviceScene &S, int px, int py, 
     h.dimension = dim < 2 ? 2 : dim;
     return h;
 }
-__device__ inline float SampleDim(const DeviceScene &S, uint64_t index, int dim) {
+__device__ __forceinline__ float SampleDim(const DeviceScene &S, uint64_t index, int dim) {
     return HaltonSampleDimension(S.haltonDim[dim], index, S.perm);
 }
 __device__ inline float Get1D(const DeviceScene &S, Halton &h) {
@@ -697,13 +697,14 @@ inline int TraversalMode(const DeviceScene &S) {
 // tMax: the shape index and best = {pObj, tHit}, or -1.  Out of line: only scenes with shapes
 // reach it, and the triangle traversal keeps its registers.
 template <bool AnyHit>
-__device__ __attribute__((noinline)) int TraverseShapes(const DeviceScene &S, V3 o, V3 d, float tMax, TriHit *best) {
+__device__ __attribute__((noinline)) int TraverseShapes(const ShapeBVHNode *shapeNodes, const DeviceShape *shapes, V3 o,
+                                                        V3 d, float tMax, TriHit *best) {
     const V3 inv(1 / d.x, 1 / d.y, 1 / d.z);
     int stack[32], sp = 0, found = -1;
     stack[sp++] = 0;
     while (sp > 0) {
         const int ni = stack[--sp];
-        const ShapeBVHNode n = S.shapeNodes[ni];
+        const ShapeBVHNode n = shapeNodes[ni];
         // slab test with pbrt's 1 + 2 gamma(3) far-plane widening (util/vecmath.h:1576-1611)
         float t0 = 0, t1 = tMax;
         bool miss = false;
@@ -724,7 +725,7 @@ __device__ __attribute__((noinline)) int TraverseShapes(const DeviceScene &S, V3
             for (int k = n.child; k < n.child + n.count; ++k) {
                 float th;
                 V3 pObj;
-                if (ShapeIntersect(S.shapes[k], o, d, tMax, &th, &pObj)) {
+                if (ShapeIntersect(shapes[k], o, d, tMax, &th, &pObj)) {
                     found = k;
                     tMax = th;
                     *best = TriHit{pObj.x, pObj.y, pObj.z, th};
@@ -746,7 +747,7 @@ __device__ inline int Traverse(const DeviceScene &S, const SceneLds &L, V3 o, V3
     if constexpr ((TM & kTravShapes) != 0) {
         if (S.nTris > 0) prim = TraverseCW<AnyHit, tm == kTravQuant, tm == kTravLds, tm == kTravLds>(S, L, o, d, tMax, best, cnt);
         if (!(AnyHit && prim >= 0)) {
-            const int k = TraverseShapes<AnyHit>(S, o, d, prim >= 0 ? best->t : tMax, best);
+            const int k = TraverseShapes<AnyHit>(S.shapeNodes, S.shapes, o, d, prim >= 0 ? best->t : tMax, best);
             if (k >= 0) prim = S.nTris + k;
         }
     } else {
@@ -834,13 +835,18 @@ __device__ inline bool LoadTriShading(const DeviceScene &S, int prim, TriShading
     return true;
 }
 
+// The out-of-line shape functions take the shape tables by value, never the DeviceScene: a
+// scene reference passed to a call makes the kernel keep a copy of the whole DeviceScene
+// (≈ 1.5 KB) in scratch per lane.
 // SurfaceInteraction of a sphere / disk hit (b0..b2 of the hit record hold pObj)
-__device__ __attribute__((noinline)) TriSurface ShapeSurfaceAt(const DeviceScene &S, int k, V3 pObj) {
-    return ShapeSurface(S.shapes[k], pObj, S.shapeN + 12 * (size_t)k);
+__device__ __attribute__((noinline)) TriSurface ShapeSurfaceAt(const DeviceShape *shapes, const float *shapeN, int k,
+                                                               V3 pObj) {
+    return ShapeSurface(shapes[k], pObj, shapeN + 12 * (size_t)k);
 }
 // Shape::PDF(ctx, wi) of sphere / disk / patch k from a surface context (p, pErr, n, ns)
-__device__ __attribute__((noinline)) float ShapeLightPDF(const DeviceScene &S, int k, V3 p, V3 pErr, V3 n, V3 ns, V3 wi) {
-    return ShapePDFSolidAngle(S.shapes[k], p, pErr, n, wi, S.shapeN + 12 * (size_t)k, ns);
+__device__ __attribute__((noinline)) float ShapeLightPDF(const DeviceShape *shapes, const float *shapeN, int k, V3 p,
+                                                         V3 pErr, V3 n, V3 ns, V3 wi) {
+    return ShapePDFSolidAngle(shapes[k], p, pErr, n, wi, shapeN + 12 * (size_t)k, ns);
 }
 // SurfaceInteraction of a hit (Triangle::InteractionFromIntersection)
 // Ext: the scene may have analytic shapes (kernels instantiated without them compile the
@@ -848,7 +854,7 @@ __device__ __attribute__((noinline)) float ShapeLightPDF(const DeviceScene &S, i
 template <bool Ext = true>
 __device__ inline TriSurface SurfaceAt(const DeviceScene &S, int prim, V3 p0, V3 p1, V3 p2, float b0, float b1,
                                        float b2) {
-    if (Ext && S.nShapes > 0 && prim >= S.nTris) return ShapeSurfaceAt(S, prim - S.nTris, V3(b0, b1, b2));
+    if (Ext && S.nShapes > 0 && prim >= S.nTris) return ShapeSurfaceAt(S.shapes, S.shapeN, prim - S.nTris, V3(b0, b1, b2));
     TriShading sh;
     const bool has = LoadTriShading(S, prim, &sh);
     return TriangleSurface(p0, p1, p2, b0, b1, b2, S.primFlip[prim], has ? &sh : nullptr);
@@ -1081,22 +1087,23 @@ __device__ inline float SmoothStepf(float x, float a, float b) {
 // Inl: the spherical-triangle sampling inlined (the diffuse kernels) or called out of line
 // DiffuseAreaLight::SampleLi over a sphere or disk (lights.cpp:743-775 with Shape::Sample(ctx,
 // u)): ctx = (cp, cpErr, n)
-__device__ __attribute__((noinline)) bool SampleShapeLi(const DeviceScene &S, const DeviceAreaLight &Ld, V3 cp, V3 cpErr,
-                                                       V3 n, V3 ns, float u0, float u1, LiSample *ls) {
+// k: the shape's index (its prim id - nTris)
+__device__ __attribute__((noinline)) bool SampleShapeLi(const DeviceShape *shapes, const float *shapeN, int k,
+                                                       bool twoSided, float scale, int spectrum, V3 cp, V3 cpErr, V3 n,
+                                                       V3 ns, float u0, float u1, LiSample *ls) {
     ShapeSamplePt ss;
-    const int k = __float_as_int(Ld.v0.w) - S.nTris;
-    if (!ShapeSampleSolidAngle(S.shapes[k], cp, cpErr, n, u0, u1, &ss, S.shapeN + 12 * (size_t)k, ns) ||
-        ss.pdf == 0 || LengthSquared(ss.p - cp) == 0)
+    if (!ShapeSampleSolidAngle(shapes[k], cp, cpErr, n, u0, u1, &ss, shapeN + 12 * (size_t)k, ns) || ss.pdf == 0 ||
+        LengthSquared(ss.p - cp) == 0)
         return false;
     ls->wi = Normalize(ss.p - cp);
-    if (!(Ld.twoSided || DotN(ss.n, -ls->wi) >= 0)) return false;  // DiffuseAreaLight::L is 0
+    if (!(twoSided || DotN(ss.n, -ls->wi) >= 0)) return false;  // DiffuseAreaLight::L is 0
     ls->lp = ss.p;
     ls->lpe = ss.pErr;
     ls->ln = ss.n;
     ls->pdf = ss.pdf;
-    ls->scale = Ld.scale;
+    ls->scale = scale;
     ls->d2 = 1;
-    ls->spectrum = Ld.spectrum;
+    ls->spectrum = spectrum;
     ls->delta = false;
     ls->envLe = false;
     return true;
@@ -1110,7 +1117,8 @@ __device__ inline bool SampleLiSurface(const DeviceScene &S, const DeviceAreaLig
         const DeviceAreaLight &Ld = lightsL[li];
         if constexpr (!Lean && Ext) {
             if (S.nShapes > 0 && __float_as_int(Ld.v0.w) >= S.nTris)
-                return SampleShapeLi(S, Ld, cp, cpErr, n, ns, u0, u1, ls);
+                return SampleShapeLi(S.shapes, S.shapeN, __float_as_int(Ld.v0.w) - S.nTris, Ld.twoSided, Ld.scale,
+                                     Ld.spectrum, cp, cpErr, n, ns, u0, u1, ls);
         }
         V3 q0(Ld.v0.x, Ld.v0.y, Ld.v0.z), q1(Ld.v1.x, Ld.v1.y, Ld.v1.z), q2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
         TriShading lsh;

@@ -224,6 +224,9 @@ struct DeviceScene {
     const int4 *matTex;
     // MixMaterial: per material {material 0, material 1, amount program, 0}
     const int4 *matMix;
+    // this struct's copy in device memory (static scene fields only): out-of-line functions
+    // that need many scene tables take it, so no kernel copies its DeviceScene into scratch
+    const DeviceScene *self;
 };
 
 // One depth's path records, compacted: record i is the i-th ray of that depth (pbrt's

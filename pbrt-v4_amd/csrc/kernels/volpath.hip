@@ -1205,7 +1205,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
                     const V3 pns = LoadV3(rec.prev + 9 * (size_t)NR, NR, ri);
                     const float lightChoicePDF = LightPMF(S, pp, pns, light);
                     if (Ext && S.nShapes > 0 && prim >= S.nTris) {
-                        lightPDF = lightChoicePDF * ShapeLightPDF(S, prim - S.nTris, pp, pe, pn, pns, -wo3);
+                        lightPDF = lightChoicePDF * ShapeLightPDF(S.shapes, S.shapeN, prim - S.nTris, pp, pe, pn, pns, -wo3);
                     } else {
                         TriShading lsh;
                         const bool lhas = LoadTriShading(S, __float_as_int(Ld.v0.w), &lsh);
@@ -2204,6 +2204,62 @@ __global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_vshadow_grey(Dev
     }
 }
 
+// Diagnostic (PBRT_AMD_QUEUE_CHECK=1): queue slots that a stage counted but never wrote.  The
+// launcher fills the slots' pixel field with -1 before the surface stage; afterwards every
+// counted slot must hold a pixel index.  Holes are counted into hole[0] and the first few are
+// printed with their queue and shard.
+// A shadow-queue hole is then made harmless (no contribution to pixel 0), so the render goes on.
+__global__ void k_queue_holes(const int *counters, int wf, int queue, int *pixel, int capS, int *hole, VolState v,
+                              int NR, int stage) {
+    const int shard = blockIdx.y;
+    const int n = counters[CounterIndex(wf, queue, shard)];
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int js = shard * capS + i;
+        if (pixel[js] < 0) {
+            const int k = atomicAdd(hole, 1);
+            if (k < 8)
+                printf("queue hole after stage %d: iteration %d queue %d shard %d slot %d of %d\n", stage, wf, queue,
+                       shard, i, n);
+            pixel[js] = 0;
+            if (queue == kVShadow) {
+                v.shFlags[js] = kShUniLd | kShUniRu | kShUniRl;
+                v.shLd[js] = 0;
+                v.shLd[NR + js] = v.shLd[2 * (size_t)NR + js] = v.shLd[3 * (size_t)NR + js] = 0;
+                v.shRu[js] = v.shRl[js] = 1;
+                for (int c = 0; c < 6; ++c) v.shRay[(size_t)c * NR + js] = c == 5 ? 1e-6f : 0.f;
+                v.shLambda0[js] = 500.f;
+                v.shMedium[js] = -1;
+            }
+        }
+    }
+}
+static int g_queueCheck = -1;  // -1: PBRT_AMD_QUEUE_CHECK decides on first use
+static bool QueueCheckOn() {
+    if (g_queueCheck < 0) {
+        const char *e = getenv("PBRT_AMD_QUEUE_CHECK");
+        g_queueCheck = e && e[0] == '1' ? 1 : 0;
+    }
+    return g_queueCheck == 1;
+}
+static int *QueueHoleCounter() {
+    static int *d = nullptr;
+    if (!d) {
+        (void)hipMalloc(&d, sizeof(int));
+        (void)hipMemset(d, 0, sizeof(int));
+    }
+    return d;
+}
+void SetQueueCheck(int on) { g_queueCheck = on ? 1 : 0; }
+// holes found since the last call (the count is reset); 0 when the check never ran
+int TakeQueueHoles() {
+    if (g_queueCheck != 1) return 0;
+    int h = 0;
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpy(&h, QueueHoleCounter(), sizeof(int), hipMemcpyDeviceToHost);
+    (void)hipMemset(QueueHoleCounter(), 0, sizeof(int));
+    return h;
+}
+
 // ------------------------------------------------------------------ launch helpers (host)
 size_t TraversalLdsBytes(int stackSize, int ldsNodes, int ldsTris, int compressed);
 size_t VolTraversalStaticLds(int tm) {
@@ -2262,25 +2318,42 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
     const int other = ~((1 << kMatDiffuseT) | (1 << 3) | (1 << kMatCoatedDiffuseT) | (1 << kMatCoatedConductorT) |
                         (1 << kMatDiffuseTransmissionT));
     const size_t surfLds = VolTablesLdsBytes(S) + kNS * kBlock * sizeof(float);
+    const bool qcheck = QueueCheckOn() && wf != S.maxDepth;
+    if (qcheck) {
+        (void)hipMemsetAsync(v.shPixel, 0xff, sizeof(int) * (size_t)st.NR, s);
+        (void)hipMemsetAsync(v.rec[(wf + 1) & 1].pixel, 0xff, sizeof(int) * (size_t)st.NR, s);
+    }
 #define VOL_REST(EXT) \
     if (wf == S.maxDepth) return hipGetLastError(); \
     if (S.matTypeMask & (1 << 3)) hipLaunchKernelGGL(k_viface<EXT>, gW, block, 0, s, S, st, v, wf); \
     if (S.matTypeMask & ((1 << kMatCoatedDiffuseT) | (1 << kMatCoatedConductorT) | (1 << kMatDiffuseTransmissionT))) \
         hipLaunchKernelGGL(k_vlayered<EXT>, gW, block, 0, s, S, st, v, wf); \
-    hipLaunchKernelGGL(k_vscatter<EXT>, gW, block, 0, s, S, st, v, wf);
+    QUEUE_CHECK(2); \
+    hipLaunchKernelGGL(k_vscatter<EXT>, gW, block, 0, s, S, st, v, wf); \
+    QUEUE_CHECK(3);
+#define QUEUE_CHECK(stage)                                                                                          \
+    if (qcheck)                                                                                                     \
+        hipLaunchKernelGGL(k_queue_holes, dim3(64, kShards), block, 0, s, st.counters, wf, kVShadow, v.shPixel,      \
+                           st.capS, QueueHoleCounter(), v, st.NR, stage);
     // Ext: analytic shapes or image lights in the scene (their paths compiled in)
     if (S.nShapes > 0 || S.nEnv > 0) {
         if (S.matTypeMask & other) hipLaunchKernelGGL((k_vsurface<false, true>), gW, block, surfLds, s, S, st, v, wf);
         else hipLaunchKernelGGL((k_vsurface<true, true>), gW, block, surfLds, s, S, st, v, wf);
+        QUEUE_CHECK(1);
         if (S.nInfinite > 0) hipLaunchKernelGGL(k_vescaped<true>, gW, block, VolTablesLdsBytes(S), s, S, st, v, wf);
         VOL_REST(true);
     } else {
         if (S.matTypeMask & other) hipLaunchKernelGGL((k_vsurface<false, false>), gW, block, surfLds, s, S, st, v, wf);
         else hipLaunchKernelGGL((k_vsurface<true, false>), gW, block, surfLds, s, S, st, v, wf);
+        QUEUE_CHECK(1);
         if (S.nInfinite > 0) hipLaunchKernelGGL(k_vescaped<false>, gW, block, VolTablesLdsBytes(S), s, S, st, v, wf);
         VOL_REST(false);
     }
 #undef VOL_REST
+    if (qcheck)
+        hipLaunchKernelGGL(k_queue_holes, dim3(64, kShards), block, 0, s, st.counters, wf + 1, kVRay,
+                           v.rec[(wf + 1) & 1].pixel, st.capS, QueueHoleCounter(), v, st.NR, 4);
+#undef QUEUE_CHECK
     if (S.media.allGrey) {
 #define K_VSHADOW_GREY(tm) k_vshadow_grey<tm>
         PBRT_LAUNCH_TRAVERSAL(S, K_VSHADOW_GREY, gT, block, VolStackBytes(S), s, S, st, v, wf);

@@ -123,7 +123,7 @@ __global__ void __launch_bounds__(kBlock, TraversalWaves(TM))
                     hitB[3 * N + qi] = h.t;
                     if constexpr (kMix) {
                         int mat = S.primMaterial[prim];
-                        if (S.matType[mat] == kMatMixT) mat = ResolveMixMaterial(S, prim, mat, h.b0, h.b1, h.b2, d);
+                        if (S.matType[mat] == kMatMixT) mat = ResolveMixMaterial(*S.self, prim, mat, h.b0, h.b1, h.b2, d);
                         st.hitMat[depth & 1][qi] = mat;
                     }
                 }
@@ -155,7 +155,7 @@ __global__ void __launch_bounds__(kBlock, TraversalWaves(TM))
                 if constexpr (kMix) {
                     if (S.matType[mat] == kMatMixT) {
                         const V3 d(rec.ray[3 * N + qi], rec.ray[4 * N + qi], rec.ray[5 * N + qi]);
-                        mat = ResolveMixMaterial(S, prim, mat, h.b0, h.b1, h.b2, d);
+                        mat = ResolveMixMaterial(*S.self, prim, mat, h.b0, h.b1, h.b2, d);
                     }
                     st.hitMat[depth & 1][qi] = mat;
                 }
@@ -499,7 +499,7 @@ __global__ void __launch_bounds__(kBlock) k_emissive(DeviceScene S, PathState st
             float lightChoicePDF = LightPMF(S, prev.p, prev.ns, light);
             float lightPDF;
             if (Ext && prim >= S.nTris) {
-                lightPDF = lightChoicePDF * ShapeLightPDF(S, prim - S.nTris, prev.p, prev.pErr, prev.n, prev.ns, -wo);
+                lightPDF = lightChoicePDF * ShapeLightPDF(S.shapes, S.shapeN, prim - S.nTris, prev.p, prev.pErr, prev.n, prev.ns, -wo);
             } else {
                 TriShading lsh;
                 const bool lhas = LoadTriShading(S, __float_as_int(Ld.v0.w), &lsh);

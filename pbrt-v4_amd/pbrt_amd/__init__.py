@@ -131,6 +131,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_debug_texture_eval",
     "pbrt_debug_env_eval",
     "pbrt_debug_shape_eval",
+    "pbrt_debug_set_queue_check", "pbrt_debug_queue_holes",
 ]
 
 _LIB = None
@@ -204,6 +205,8 @@ def _lib():
     lib.pbrt_debug_texture_eval.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_debug_env_eval.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_debug_shape_eval.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
+    lib.pbrt_debug_set_queue_check.argtypes = [c.c_int]
+    lib.pbrt_debug_queue_holes.argtypes = [c.POINTER(c.c_int)]
     lib.pbrt_set_data_dir(str(DATA_DIR).encode())
     _LIB = lib
     return lib
@@ -214,6 +217,18 @@ def _f32(a, n=None):
     if n is not None and a.size != n:
         raise PbrtError(f"expected {n} values, got {a.size}")
     return a
+
+
+def set_queue_check(on):
+    """Turns the volumetric wavefront's queue-integrity check on or off (diagnostics)."""
+    _check(_lib().pbrt_debug_set_queue_check(1 if on else 0))
+
+
+def queue_holes():
+    """Queue slots counted but never written since the last call (0 with the check off)."""
+    n = ctypes.c_int(0)
+    _check(_lib().pbrt_debug_queue_holes(ctypes.byref(n)))
+    return n.value
 
 
 def debug_light_bvh(lights13):

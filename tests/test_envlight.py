@@ -192,6 +192,43 @@ def test_env_scene_zsobol_bvh_sampler_gpu(pa, oracle):
     print(f"env + area light parity: {frac*100:.3f}% pixels within 1e-3, mean rel {mean_rel:.2e}")
 
 
+def _env_volumetric_scenes():
+    from test_media import box
+    coated = SCENE.format(fn="env_sky.pfm").replace('Material "diffuse" "rgb reflectance" [0.6 0.5 0.4]',
+                                                    'Material "coateddiffuse" "rgb reflectance" [0.6 0.5 0.4] '
+                                                    '"float roughness" 0.2')
+    coated += ('MakeNamedMedium "m" "string type" "homogeneous" "rgb sigma_a" [0.3 0.5 0.2] '
+               '"rgb sigma_s" [1.2 0.8 1.5] "float g" 0.4\n'
+               'AttributeBegin\nMediumInterface "m" ""\nMaterial "interface"\n' + box(-2.6, -1.6, -0.9, 0.1, -0.5, 0.5) +
+               '\nAttributeEnd\n')
+    iface = SCENE.format(fn="env_sky.pfm") + ('AttributeBegin\nMaterial "interface"\n' +
+                                              box(-2.6, -1.6, -0.9, 0.1, -0.5, 0.5) + '\nAttributeEnd\n')
+    return {"coated+medium": coated, "interface": iface}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["coated+medium", "interface"])
+def test_env_volumetric_queues_have_no_holes_gpu(pa, oracle, name):
+    """Regression test for the round-3 volumetric-kernel defect: the image-light
+    volumetric kernels (k_vsurface<..., Ext>) counted shadow-queue slots they never wrote, which
+    left a NaN at pixel 0 and then faulted.  With the queue-integrity check on, every counted
+    slot of the surface, layered and scattering stages must be written, and the film must be
+    the same bits as with the check off."""
+    from test_gpu_media import gpu_rgb
+    sc = pa.Scene.from_string(_env_volumetric_scenes()[name], SCENES, xresolution=96, yresolution=64)
+    pa.queue_holes()
+    pa.set_queue_check(True)
+    try:
+        a, _ = gpu_rgb(pa, oracle, sc)
+        holes = pa.queue_holes()
+    finally:
+        pa.set_queue_check(False)
+    b, _ = gpu_rgb(pa, oracle, sc)
+    assert holes == 0
+    assert np.isfinite(b).all()
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
 @pytest.mark.gpu
 def test_env_coated_and_medium_match_oracle_gpu(pa, oracle):
     """The volumetric kernels with an image light: a coated-diffuse floor (layered BSDF) and a

@@ -66,7 +66,8 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--untextured", action="store_true",
                     help="C4: round 2's constant materials instead of configs[3]'s image textures")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="oracle threads for cpu_baseline (0: every host core this process may use)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
                     help="N > 1: strong = one image split N ways (default); weak = every GPU renders "
                          "the single-GPU workload (job spp x N)")
@@ -157,9 +158,35 @@ def roofline_entry(achieved, mean_launch_s, launches, rays_per_launch, bytes_per
             "timed_launches": launches, "mean_launch_us": round(mean_launch_s * 1e6, 3), "limiter": limiter}
 
 
+def host_cores():
+    """Host cores this process may run on: its CPU affinity, capped by a cgroup CPU quota and by
+    OMP_NUM_THREADS when set (a GPU box grants each GPU a share of a larger machine, stated in
+    OMP_NUM_THREADS; os.cpu_count() reports the whole machine there)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            quota, period = open(path).read().split()[:2]
+            if quota != "max" and int(period) > 0:
+                n = min(n, max(1, int(int(quota) // int(period))))
+        except (OSError, ValueError):
+            pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0 and p > 0:
+            n = min(n, max(1, q // p))
+    except (OSError, ValueError):
+        pass
+    # the box's per-GPU CPU allotment, when the environment states one (OMP_NUM_THREADS)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
 def cpu_baseline(args, threads, sc):
     """Oracle (pbrt wavefront/VolPath port) on the host: every film row, the first 16 of the
-    64 samples per pixel (~15 M samples, ~3 s wall at 16 threads on the GPU box's host)."""
+    64 samples per pixel (~15 M samples, a few seconds of wall time on the GPU box's host)."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import numpy as np
     import pyoracle
@@ -178,6 +205,8 @@ def cpu_baseline(args, threads, sc):
     dt = time.perf_counter() - t - setup
     n = len(rows) * (i.px1 - i.px0) * spp
     return {"value": n / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "cores_note": "every host core granted to the process (CPU affinity, cgroup quota, OMP_NUM_THREADS)"
+            if not args.cpu_threads else "--cpu-threads",
             "sample": f"{len(rows)} of {i.py1 - i.py0} rows x {i.px1 - i.px0} px x {spp} spp "
                       f"({n} samples, {dt:.2f} s wall excluding the oracle's {setup:.2f} s BVH build)"}
 
@@ -314,7 +343,7 @@ def main():
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             try:
-                cpu = cpu_baseline(args, min(args.cpu_threads, os.cpu_count() or 1), scene)
+                cpu = cpu_baseline(args, args.cpu_threads or host_cores(), scene)
             except Exception as e:  # the baseline is reported, never required
                 cpu = {"value": None, "error": str(e)}
         line = {

@@ -1797,6 +1797,7 @@ int pbrt_render(pbrt_context *ctx, const pbrt_render_params *params) {
 
 int pbrt_synchronize(pbrt_context *ctx) {
     try {
+        if (!ctx) return Fail("null context");
         HIPCHECK(hipSetDevice(ctx->device));
         HIPCHECK(hipStreamSynchronize(ctx->stream));
         for (int i = 0; i < ctx->eventsUsed; ++i) {
@@ -1851,12 +1852,14 @@ int pbrt_get_kernel_stats(pbrt_context *ctx, pbrt_kernel_stat *out, int max_stat
 }
 
 int pbrt_get_stats(pbrt_context *ctx, pbrt_render_stats *stats) {
+    if (!ctx || !stats) return Fail("null argument");
     *stats = ctx->stats;
     return 0;
 }
 
 int pbrt_reset_stats(pbrt_context *ctx) {
     try {
+        if (!ctx) return Fail("null context");
         HIPCHECK(hipSetDevice(ctx->device));
         HIPCHECK(hipStreamSynchronize(ctx->stream));
         HIPCHECK(hipMemset(ctx->devStats.p, 0, kStatsSlots * sizeof(unsigned long long)));
@@ -1872,6 +1875,7 @@ int pbrt_reset_stats(pbrt_context *ctx) {
 
 int pbrt_film_clear(pbrt_context *ctx) {
     try {
+        if (!ctx) return Fail("null context");
         HIPCHECK(hipSetDevice(ctx->device));
         HIPCHECK(hipMemsetAsync(ctx->film.p, 0, ctx->film.n * sizeof(double), ctx->stream));
         return 0;
@@ -1881,6 +1885,7 @@ int pbrt_film_clear(pbrt_context *ctx) {
 }
 
 int pbrt_film_device_ptr(pbrt_context *ctx, double **film, size_t *n) {
+    if (!ctx || !film || !n) return Fail("null argument");
     *film = ctx->film.p;
     *n = ctx->film.n;
     return 0;
@@ -1888,6 +1893,7 @@ int pbrt_film_device_ptr(pbrt_context *ctx, double **film, size_t *n) {
 
 int pbrt_film_read(pbrt_context *ctx, double *out) {
     try {
+        if (!ctx || !out) return Fail("null argument");
         HIPCHECK(hipSetDevice(ctx->device));
         HIPCHECK(hipStreamSynchronize(ctx->stream));
         HIPCHECK(hipMemcpy(out, ctx->film.p, ctx->film.n * sizeof(double), hipMemcpyDeviceToHost));
@@ -1899,6 +1905,7 @@ int pbrt_film_read(pbrt_context *ctx, double *out) {
 
 int pbrt_film_get_rgb(pbrt_context *ctx, float *rgb) {
     try {
+        if (!ctx || !rgb) return Fail("null argument");
         std::vector<double> f(ctx->film.n);
         if (pbrt_film_read(ctx, f.data())) return 1;
         size_t npix = (size_t)ctx->desc.xres * ctx->desc.yres;
@@ -2001,8 +2008,8 @@ int pbrt_image_flip(const float *image, const float *reference, int width, int h
 
 int pbrt_intersect(pbrt_context *ctx, const float *rays, int n, int anyHit, int32_t *prim, float *hit) {
     try {
-        HIPCHECK(hipSetDevice(ctx->device));
         if (!ctx || n < 0 || (n > 0 && (!rays || !prim || !hit))) return Fail("bad arguments");
+        HIPCHECK(hipSetDevice(ctx->device));
         if (n == 0) return 0;
         if ((int64_t)n * 7 > INT32_MAX) return Fail("ray batch too large");
         // asynchronous on the context stream; the kernel writes the scene's triangle numbering

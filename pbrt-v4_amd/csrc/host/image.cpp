@@ -323,7 +323,7 @@ static Image ReadEXR(const std::string &path) {
     std::vector<Ch> chans;
     int compression = -1, x0 = 0, y0 = 0, x1 = -1, y1 = -1;
     float chroma[8];
-    bool hasChroma = false;
+    bool hasChroma = false, haveWindow = false;
     while (true) {
         std::string name = rdstr();
         if (name.empty()) break;
@@ -346,6 +346,8 @@ static Image ReadEXR(const std::string &path) {
         } else if (name == "compression") {
             compression = d[pos];
         } else if (name == "dataWindow") {
+            if (size < 16) throw std::runtime_error(path + ": bad EXR data window");
+            haveWindow = true;
             std::memcpy(&x0, &d[pos], 4);
             std::memcpy(&y0, &d[pos + 4], 4);
             std::memcpy(&x1, &d[pos + 8], 4);
@@ -368,10 +370,14 @@ static Image ReadEXR(const std::string &path) {
             if (!(chroma[i] == srgb[i] || std::abs((chroma[i] - srgb[i]) / srgb[i]) < 1e-3f))
                 throw std::runtime_error(path + ": EXR chromaticities are not sRGB's; only sRGB images are supported");
     }
+    // dataWindow must exist and span a sane, non-empty box (64-bit extents: no int overflow)
+    const int64_t wExt = (int64_t)x1 - x0 + 1, hExt = (int64_t)y1 - y0 + 1;
+    if (!haveWindow || wExt <= 0 || hExt <= 0 || wExt > 65536 || hExt > 65536 || wExt * hExt > (int64_t(1) << 28))
+        throw std::runtime_error(path + ": bad EXR data window");
+    if (chans.empty()) throw std::runtime_error(path + ": EXR file without channels");
     Image im;
-    im.width = x1 - x0 + 1;
-    im.height = y1 - y0 + 1;
-    if (im.width <= 0 || im.height <= 0) throw std::runtime_error(path + ": bad EXR data window");
+    im.width = (int)wExt;
+    im.height = (int)hExt;
     int idx[3] = {-1, -1, -1};
     size_t lineBytes = 0;
     std::vector<size_t> chOff;

@@ -62,6 +62,7 @@ static SpectralData LoadSpectralData() {
     std::ifstream in(path);
     if (!in) throw Error("cannot open spectral data file " + path);
     std::string line;
+    bool haveMipLUT = false, haveSrgbLUT = false;
     while (std::getline(in, line)) {
         std::istringstream ls(line);
         std::string name;
@@ -82,13 +83,19 @@ static SpectralData LoadSpectralData() {
         else if (name == "opt_cie_d65_divisor") d.optD65Divisor = v[0];
         else if (name == "opt_xyz_to_srgb") d.optXyzToSrgb = v;
         else if (name == "opt_srgb_to_xyz") d.optSrgbToXyz = v;
-        else if (name == "MIPFilterLUT" && n == 128)
+        else if (name == "MIPFilterLUT" && n == 128) {
             for (int i = 0; i < 128; ++i) d.mipFilterLUT[i] = (float)v[i];
-        else if (name == "SRGBToLinearLUT" && n == 256)
+            haveMipLUT = true;
+        } else if (name == "SRGBToLinearLUT" && n == 256) {
             for (int i = 0; i < 256; ++i) d.srgbToLinear[i] = (float)v[i];
+            haveSrgbLUT = true;
+        }
         else if (name.rfind("named:", 0) == 0) tof(d.named[name.substr(6)]);
     }
     if (d.cieX.size() != 471 || d.optX.size() != 95) throw Error("malformed spectral data " + path);
+    if (!haveMipLUT || !haveSrgbLUT)
+        throw Error("malformed spectral data " + path + ": missing " +
+                    (!haveMipLUT ? std::string("MIPFilterLUT") : std::string("SRGBToLinearLUT")));
     // Spectra::Init: dense X/Y/Z over Lambda_min..Lambda_max of PiecewiseLinear(CIE_lambda, CIE_*)
     for (int l = 395; l <= 705; ++l) {
         d.denseX[l - 395] = PiecewiseLinearEval(d.cieLambda, d.cieX, (float)l);
@@ -402,7 +409,20 @@ const std::vector<float> &RGBToSpectrumTableData() {
             std::ifstream in(path, std::ios::binary);
             if (in) {
                 in.read(reinterpret_cast<char *>(table.data()), (std::streamsize)(table.size() * 4));
-                if (in.gcount() == (std::streamsize)(table.size() * 4)) return;
+                // a cached table is trusted only when its size, its z nodes and three sampled
+                // columns equal a fresh computation bit for bit; otherwise it is rebuilt
+                bool ok = in.gcount() == (std::streamsize)(table.size() * 4) && in.peek() == EOF;
+                for (int k = 0; ok && k < kRes; ++k) ok = table[k] == RGB2SpecZNode(k);
+                const int probe[3][3] = {{0, 0, 0}, {1, kRes / 2, kRes / 3}, {2, kRes - 1, kRes - 2}};
+                for (int p = 0; ok && p < 3; ++p) {
+                    const int l = probe[p][0], j = probe[p][1], i = probe[p][2];
+                    const std::vector<float> c = RGB2SpecColumn(l, j, i);
+                    for (int k = 0; ok && k < kRes; ++k)
+                        for (int ci = 0; ci < 3; ++ci)
+                            ok = ok && table[kRes + ((((size_t)l * kRes + k) * kRes + j) * kRes + i) * 3 + ci] ==
+                                           c[3 * k + ci];
+                }
+                if (ok) return;
             }
         }
         // rgb2spec_opt.cpp:800-880: every (maxc, y, x) column, independent of the others

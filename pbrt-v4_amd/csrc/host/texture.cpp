@@ -235,6 +235,16 @@ static RawImage ReadPNG(const std::string &fn, const Encoding &enc) {
     case 6: samples = 4; break;
     default: throw Error(fn + ": bad PNG colour type");
     }
+    // the PNG specification's bit depths per colour type (grey 1/2/4/8/16, palette 1/2/4/8,
+    // RGB, grey-alpha and RGBA 8/16); anything else would size rows wrongly
+    const bool depthOk = colorType == 0   ? (bitDepth == 1 || bitDepth == 2 || bitDepth == 4 || bitDepth == 8 ||
+                                           bitDepth == 16)
+                         : colorType == 3 ? (bitDepth == 1 || bitDepth == 2 || bitDepth == 4 || bitDepth == 8)
+                                          : (bitDepth == 8 || bitDepth == 16);
+    if (!depthOk)
+        throw Error(fn + ": bad PNG bit depth " + std::to_string(bitDepth) + " for colour type " +
+                    std::to_string(colorType));
+    if ((uint64_t)w * h > (1ull << 31)) throw Error(fn + ": PNG image too large");
     if (colorType == 3 && plte.empty()) throw Error(fn + ": paletted PNG without a palette");
     const size_t bitsPerPixel = (size_t)samples * bitDepth;
     const size_t rowBytes = (w * bitsPerPixel + 7) / 8;

@@ -321,8 +321,12 @@ int pbrt_debug_texture_eval(const pbrt_scene *scene, int material, int slot, con
  * u[n][2], out[n][16] = Le's (u, v) of the direction, PDF_Li(allowIncompletePDF), the pixel's
  * RGBIlluminantSpectrum at 400 / 500 / 600 / 700 nm (light scale and illuminant 1), the
  * compensated distribution's sample (u, v), its mapPDF, wi = renderFromLight(
- * EqualAreaSquareToSphere(u, v)), 3 unused */
+ * EqualAreaSquareToSphere(u, v)), PiecewiseConstant2D::PDF at that sample, PDF at u taken as a
+ * point of [0,1]^2, 1 unused */
 int pbrt_debug_env_eval(const pbrt_scene *scene, int env, const float *dirs, const float *u, int n, float *out);
+/* EqualAreaSquareToSphere (to_sphere != 0: in[n][2] -> out[n][3]) or EqualAreaSphereToSquare
+ * (in[n][3] -> out[n][2]) with the product's shared host/device code (util/math.cpp:292-361) */
+int pbrt_debug_equal_area(int to_sphere, const float *in, int n, float *out);
 /* Sphere / disk `shape` of the scene with the product's shared host/device code (shapes.h:
  * 106-571): for n rays rays[n][6] (o, d) and sample pairs u[n][2], out[n][40] = hit flag, tHit,
  * pObj xyz, then the render-space SurfaceInteraction p xyz, pError xyz, n xyz, shading n xyz,

@@ -5032,7 +5032,27 @@ int oracle_env_eval(const pbrt_scene_flat *flat, int env, const float *dirs, con
         o[10] = wi.x;
         o[11] = wi.y;
         o[12] = wi.z;
-        o[13] = o[14] = o[15] = 0;
+        o[13] = E.PDF(su, sv);                // PiecewiseConstant2D::PDF at the sample
+        o[14] = E.PDF(u[2 * i], u[2 * i + 1]);  // ... and at u taken as a point of [0,1]^2
+        o[15] = 0;
+    }
+    return 0;
+}
+// EqualAreaSquareToSphere (toSphere: in[n][2] -> out[n][3]) or EqualAreaSphereToSquare
+// (in[n][3] -> out[n][2]) of the oracle (util/math.cpp:292-361)
+int oracle_equal_area(int toSphere, const float *in, int n, float *out) {
+    for (int i = 0; i < n; ++i) {
+        if (toSphere) {
+            const Vec w = OEnvLight::SquareToSphere(in[2 * i], in[2 * i + 1]);
+            out[3 * i] = w.x;
+            out[3 * i + 1] = w.y;
+            out[3 * i + 2] = w.z;
+        } else {
+            Float uu, vv;
+            OEnvLight::SphereToSquare(Vec(in[3 * i], in[3 * i + 1], in[3 * i + 2]), &uu, &vv);
+            out[2 * i] = uu;
+            out[2 * i + 1] = vv;
+        }
     }
     return 0;
 }

@@ -51,6 +51,7 @@ def lib():
         _lib.oracle_texture_eval.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_int, vp]
         _lib.oracle_env_eval.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_int, vp]
         _lib.oracle_shape_eval.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_int, vp]
+        _lib.oracle_equal_area.argtypes = [ctypes.c_int, vp, ctypes.c_int, vp]
         _lib.oracle_camera_min_diff.argtypes = [vp, vp, vp]
         _lib.oracle_image_level.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int64,
                                             ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
@@ -97,6 +98,15 @@ def env_eval(scene, env, dirs, u):
     out = np.zeros((len(d), 16), np.float32)
     rc = lib().oracle_env_eval(ctypes.byref(flat), env, d.ctypes.data, uu.ctypes.data, len(d), out.ctypes.data)
     assert rc == 0, rc
+    return out
+
+
+def equal_area(points, to_sphere):
+    """The oracle's EqualAreaSquareToSphere / EqualAreaSphereToSquare, as pbrt_amd.equal_area"""
+    k_in, k_out = (2, 3) if to_sphere else (3, 2)
+    a = f32(points).reshape(-1, k_in)
+    out = np.zeros((len(a), k_out), np.float32)
+    assert lib().oracle_equal_area(1 if to_sphere else 0, a.ctypes.data, len(a), out.ctypes.data) == 0
     return out
 
 

@@ -2192,7 +2192,9 @@ int pbrt_debug_env_eval(const pbrt_scene *scene, int env, const float *dirs, con
             o[10] = wi.x;
             o[11] = wi.y;
             o[12] = wi.z;
-            o[13] = o[14] = o[15] = 0;
+            o[13] = EnvPDF(E, su, sv);                // PiecewiseConstant2D::PDF at the sample
+            o[14] = EnvPDF(E, u[2 * i], u[2 * i + 1]);  // ... and at u taken as a point of [0,1]^2
+            o[15] = 0;
         }
         return 0;
     } catch (const std::exception &e) {
@@ -2239,6 +2241,21 @@ int pbrt_debug_shape_eval(const pbrt_scene *scene, int shape, const float *rays,
     } catch (const std::exception &e) {
         return Fail(e.what());
     }
+}
+
+int pbrt_debug_equal_area(int to_sphere, const float *in, int n, float *out) {
+    if (!in || !out || n < 0) return Fail("null argument");
+    for (int i = 0; i < n; ++i) {
+        if (to_sphere) {
+            const V3 w = EqualAreaSquareToSphere(in[2 * i], in[2 * i + 1]);
+            out[3 * i] = w.x;
+            out[3 * i + 1] = w.y;
+            out[3 * i + 2] = w.z;
+        } else {
+            EqualAreaSphereToSquare(V3(in[3 * i], in[3 * i + 1], in[3 * i + 2]), &out[2 * i], &out[2 * i + 1]);
+        }
+    }
+    return 0;
 }
 
 int pbrt_debug_rgb2spec_column(int maxc, int j, int i, float *out) {

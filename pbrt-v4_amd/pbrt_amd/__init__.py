@@ -132,6 +132,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_debug_env_eval",
     "pbrt_debug_shape_eval",
     "pbrt_debug_set_queue_check", "pbrt_debug_queue_holes",
+    "pbrt_debug_equal_area",
 ]
 
 _LIB = None
@@ -207,9 +208,20 @@ def _lib():
     lib.pbrt_debug_shape_eval.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_debug_set_queue_check.argtypes = [c.c_int]
     lib.pbrt_debug_queue_holes.argtypes = [c.POINTER(c.c_int)]
+    lib.pbrt_debug_equal_area.argtypes = [c.c_int, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_set_data_dir(str(DATA_DIR).encode())
     _LIB = lib
     return lib
+
+
+def equal_area(points, to_sphere):
+    """EqualAreaSquareToSphere (to_sphere: points[n][2] -> [n][3]) or EqualAreaSphereToSquare
+    ([n][3] -> [n][2]) with the product's shared host/device code (pbrt_debug_equal_area)."""
+    k_in, k_out = (2, 3) if to_sphere else (3, 2)
+    a = np.ascontiguousarray(points, dtype=np.float32).reshape(-1, k_in)
+    out = np.zeros((len(a), k_out), np.float32)
+    _check(_lib().pbrt_debug_equal_area(1 if to_sphere else 0, a.ctypes.data, len(a), out.ctypes.data))
+    return out
 
 
 def _f32(a, n=None):

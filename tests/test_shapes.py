@@ -301,3 +301,85 @@ def test_cylinders_match_oracle_gpu(pa, oracle):
     frac, mean_rel = check_parity(to_rgb(oracle, sc, film), to_rgb(oracle, sc, oracle.render(sc, threads=16)))
     print(f"cylinders parity: {frac*100:.3f}% pixels within 1e-3, mean rel {mean_rel:.2e}")
 
+
+
+# ---------------------------------------------------------------- reference goldens
+# tests/golden/reference_components.json "shapes": the reference's own Sphere, Disk, Cylinder and
+# BilinearPatch (shapes.h / shapes.cpp compiled unmodified into oracle/_ref/refgold) on seeded
+# rays, in pbrt_debug_shape_eval's row layout (oracle/ref/refgold.cpp ShapeGoldens).  The
+# transforms are Translate * ConcatTransform(signed permutation) * Scale with dyadic values, so
+# the loader's double-precision composition and inversion equal pbrt's float ones bit for bit.
+_PERM = {0: None,
+         1: [[0, 0, 1, 0], [1, 0, 0, 0], [0, 1, 0, 0], [0, 0, 0, 1]],
+         2: [[0, 0, 1, 0], [0, 1, 0, 0], [1, 0, 0, 0], [0, 0, 0, 1]]}
+
+
+def _fmt(v):
+    return " ".join(repr(float(x)) for x in v)
+
+
+def golden_shape_scene(case):
+    """The one-shape scene of a golden case (camera at the origin: render space = world)."""
+    lines = ['LookAt 0 0 0  0 0 1  0 1 0', 'Camera "perspective"', 'WorldBegin', 'LightSource "infinite"',
+             'AttributeBegin']
+    if case["reverse"]:
+        lines.append("ReverseOrientation")
+    lines.append("Translate " + _fmt(case["translate"]))
+    if _PERM[case["perm"]] is not None:
+        m = np.array(_PERM[case["perm"]], float)
+        lines.append("ConcatTransform [" + _fmt(m.T.reshape(-1)) + "]")  # column-major, as pbrt reads it
+    lines.append("Scale " + _fmt(case["scale"]))
+    a, b, c, d = case["params"]
+    kind = case["kind"]
+    if kind == "sphere":
+        shape = f'Shape "sphere" "float radius" {a!r} "float zmin" {b!r} "float zmax" {c!r} "float phimax" {d!r}'
+    elif kind == "disk":
+        shape = f'Shape "disk" "float height" {a!r} "float radius" {b!r} "float innerradius" {c!r} "float phimax" {d!r}'
+    elif kind == "cylinder":
+        shape = f'Shape "cylinder" "float radius" {a!r} "float zmin" {b!r} "float zmax" {c!r} "float phimax" {d!r}'
+    else:
+        shape = f'Shape "bilinearmesh" "point3 P" [{_fmt(case["P"])}]'
+        if case["N"]:
+            shape += f' "normal N" [{_fmt(case["N"])}]'
+        if case["uv"]:
+            shape += f' "point2 uv" [{_fmt(case["uv"])}]'
+    lines += [shape, "AttributeEnd", ""]
+    return "\n".join(lines)
+
+
+def _golden_rows(case):
+    rays = np.array([r["ray"] for r in case["rows"]], np.float32)
+    u = np.array([r["u"] for r in case["rows"]], np.float32)
+    want = np.array([[float(x) for x in r["out"]] for r in case["rows"]], np.float32)
+    return rays, u, want
+
+
+def _assert_rows_equal(got, want, label):
+    """Bit for bit, except that +0 and -0 compare equal: the loader composes and inverts
+    transforms in double (Gauss-Jordan), pbrt in float (compensated inner products and the
+    cofactor inverse, util/math.h), so an exactly-zero matrix entry may carry the other sign
+    and so may a zero component it produces; every value is the same float."""
+    cols = list(range(38))
+    g, w = got[:, cols].copy(), want[:, cols].copy()
+    g[g == 0] = 0
+    w[w == 0] = 0
+    bad = np.nonzero((g.view(np.uint32) != w.view(np.uint32)).any(axis=1))[0]
+    if len(bad):
+        i = bad[0]
+        diff = [j for j in cols if got[i, j].view(np.uint32) != want[i, j].view(np.uint32)]
+        raise AssertionError(f"{label}: {len(bad)} of {len(got)} rows differ; row {i} columns {diff}: "
+                             f"got {got[i, diff]} want {want[i, diff]}")
+
+
+@pytest.mark.parametrize("ci", range(13))
+def test_shapes_match_reference_goldens(pa, oracle, golden, ci):
+    """Intersection, SurfaceInteraction, Sample(ctx, u) and PDF(ctx, wi) of spheres, disks,
+    cylinders and bilinear patches against the reference's own code, bit for bit: the product's
+    shared host/device code and the oracle's restatement."""
+    case = golden["shapes"][ci]
+    sc = pa.Scene.from_string(golden_shape_scene(case), SCENES)
+    assert sc.flat().n_shapes == 1
+    rays, u, want = _golden_rows(case)
+    assert want[:, 0].sum() >= 10 and want[:, 26].sum() >= 10  # hits and samples exercised
+    _assert_rows_equal(sc.shape_eval(0, rays, u), want, f"product {case['kind']} #{ci}")
+    _assert_rows_equal(oracle.shape_eval(sc, 0, rays, u), want, f"oracle {case['kind']} #{ci}")

@@ -825,6 +825,7 @@ static void BuildDevice(pbrt_context *c) {
     std::vector<HaltonDimDesc> hd;
     for (size_t d = 0; d < s.permBase.size(); ++d)
         hd.push_back(MakeHaltonDimDesc(s.permBase[d], s.permNDigits[d], s.permOffset[d]));
+    for (auto &d : hd) HaltonDimTail(&d, s.permTable.data() + d.permOffset);
     c->haltonDim.Upload(hd);
     {
         std::vector<uint8_t> zp(&kZSobolPermutations[0][0], &kZSobolPermutations[0][0] + 96);
@@ -2060,11 +2061,14 @@ int64_t pbrt_debug_halton_fastpath_mismatches(const pbrt_scene *scene, int dim, 
     if (!scene || step == 0 || a1 > (1u << 24)) return -1;
     const SceneDesc &s = scene->desc;
     if (dim < 0 || dim >= (int)s.permBase.size()) return -1;
-    const HaltonDimDesc d = MakeHaltonDimDesc(s.permBase[dim], s.permNDigits[dim], s.permOffset[dim]);
+    HaltonDimDesc d = MakeHaltonDimDesc(s.permBase[dim], s.permNDigits[dim], s.permOffset[dim]);
     const uint16_t *perm = s.permTable.data() + d.permOffset;
+    HaltonDimTail(&d, perm);
     int64_t bad = 0;
     for (uint64_t a = a0; a < a1; a += step) {
-        const float f = d.nDigits <= (uint32_t)kMaxShadeHaltonDigits
+        // the shade stage's form for bases >= 17 (a < 2^24 < base^6), the unrolled loop otherwise
+        const float f = d.base >= 17 ? ScrambledRadicalInverse24x6(d, (uint32_t)a, perm)
+                        : d.nDigits <= (uint32_t)kMaxShadeHaltonDigits
                             ? ScrambledRadicalInverse24<kMaxShadeHaltonDigits>(d, (uint32_t)a, perm)
                             : ScrambledRadicalInverse24<kMaxHaltonDigits24>(d, (uint32_t)a, perm);
         const float g = ScrambledRadicalInverse(d.base, d.nDigits, a, perm);

@@ -756,8 +756,8 @@ PHD_NOINLINE float ScrambledRadicalInverse(uint32_t base, uint32_t nDigits, uint
 // Larger indices take the 64-bit restatement above.  No 32/64-bit integer division remains on
 // the fast path (pbrt's a / base is a 64-bit division; here it was most of the sampler's cost).
 struct HaltonDimDesc {
-    uint32_t base, nDigits, permOffset, pad;
-    float invBase, invBaseM, rcp, pad2;
+    uint32_t base, nDigits, permOffset, tail;  // tail, tailMul: HaltonDimTail
+    float invBase, invBaseM, rcp, tailMul;
 };
 PHD HaltonDimDesc MakeHaltonDimDesc(uint32_t base, uint32_t nDigits, uint32_t permOffset) {
     HaltonDimDesc d{};
@@ -769,7 +769,24 @@ PHD HaltonDimDesc MakeHaltonDimDesc(uint32_t base, uint32_t nDigits, uint32_t pe
     for (uint32_t k = 0; k < nDigits; ++k) invBaseM *= d.invBase;
     d.invBaseM = invBaseM;
     d.rcp = (float)(1.0 / base);
+    d.tail = 0;
+    d.tailMul = 1;
     return d;
+}
+// The digits past the sixth of an index a < base^6 are all zero, so they add the constant
+// tail = sum_{k=6}^{n-1} perm[k base] base^(n-1-k) after scaling the six-digit value by
+// tailMul = base^(n-6) (ScrambledRadicalInverse24x6).  Both are exact integers far below 2^24.
+PHD void HaltonDimTail(HaltonDimDesc *d, const uint16_t *perm) {
+    d->tail = 0;
+    d->tailMul = 1;
+    if (d->nDigits <= 6) return;
+    uint32_t t = 0, m = 1;
+    for (uint32_t k = 6; k < d->nDigits; ++k) {
+        t = t * d->base + perm[k * d->base];
+        m *= d->base;
+    }
+    d->tail = t;
+    d->tailMul = (float)m;
 }
 // MaxDigits >= d.nDigits: the digit loop is unrolled to that bound (iterations past nDigits are
 // skipped by a launch-uniform test) and every permutation load is issued before the first is
@@ -804,6 +821,37 @@ PHD_UNROLL
 PHD_UNROLL
     for (int k = 0; k < MaxDigits; ++k)
         if ((uint32_t)k < n) rd = fma(rd, (double)b, (double)pv[k]);
+    return std::fmin(d.invBaseM * (float)rd, kOneMinusEpsilon);
+}
+// ScrambledRadicalInverse24 for a < base^6 (every shade-stage dimension: bases >= 17 and
+// a < 2^24 < 17^6): six digit steps without branches -- a step at or past nDigits loads the
+// table's first entry and is discarded by a select -- so the compiler can interleave the
+// dimensions of a depth, then the remaining (zero) digits as one exact fma with the host's tail.
+// reversedDigits stays an exact integer in double throughout, so the result is the same float.
+template <typename PermPtr>
+PHD float ScrambledRadicalInverse24x6(const HaltonDimDesc &d, uint32_t a, PermPtr perm) {
+    const uint32_t b = d.base & 0xffffffu, n = d.nDigits;
+    uint32_t pv[6];
+PHD_UNROLL
+    for (int k = 0; k < 6; ++k) {
+        uint32_t q = (uint32_t)((float)a * d.rcp);
+#if defined(__HIP_DEVICE_COMPILE__)
+        int r = (int)a - (int)MulU24(q, b);
+#else
+        int r = (int)a - (int)(q * b);
+#endif
+        q = r < 0 ? q - 1 : q;
+        r = r < 0 ? r + (int)b : r;
+        q = r >= (int)b ? q + 1 : q;
+        r = r >= (int)b ? r - (int)b : r;
+        const bool ok = (uint32_t)k < n;
+        pv[k] = perm[ok ? (uint32_t)k * b + (uint32_t)r : 0u];
+        a = q;
+    }
+    double rd = 0;
+PHD_UNROLL
+    for (int k = 0; k < 6; ++k) rd = (uint32_t)k < n ? fma(rd, (double)b, (double)pv[k]) : rd;
+    rd = fma(rd, (double)d.tailMul, (double)d.tail);
     return std::fmin(d.invBaseM * (float)rd, kOneMinusEpsilon);
 }
 constexpr int kMaxHaltonDigits24 = 25;  // base 2 (the largest digit count of any dimension)

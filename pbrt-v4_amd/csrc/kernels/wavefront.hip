@@ -654,7 +654,7 @@ __device__ __forceinline__ RaySamples GenerateRaySamples(const DeviceScene &S, c
     if (Lean || (S.samplerType == 0 && sidx < (1u << 24))) {
         // the common case: every dimension by the 24-bit digit loop from the LDS tables
         auto dim = [&](int k) -> float {
-            return ScrambledRadicalInverse24<kMaxShadeHaltonDigits>(S.haltonDim[d0 + k], sidx, T.permL + T.permOff[k]);
+            return ScrambledRadicalInverse24x6(S.haltonDim[d0 + k], sidx, T.permL + T.permOff[k]);
         };
         r.dUc = dim(0);
         r.dU0 = dim(1);

@@ -106,16 +106,23 @@ def test_zsobol_bit_exact(pa, golden, cfg_index):
 def test_halton_fastpath_matches_64bit_restatement(pa):
     """The kernels' Halton digits for indices < 2^24 (float-reciprocal quotient with one
     correction, reversedDigits accumulated exactly in double: core.h ScrambledRadicalInverse24)
+    and its six-digit branch-free form for bases >= 17 (ScrambledRadicalInverse24x6)
     equal the 64-bit restatement of ScrambledRadicalInverse (util/lowdiscrepancy.h:115-134), bit
     for bit: every dimension the wavefront uses at maxdepth 5 (0..40), a strided sweep of the
     whole 2^24 range plus the top 2^16 indices and the first 2^16 exhaustively."""
     from conftest import SCENES
     sc = pa.load_scene(SCENES / "cornell-box.pbrt", xresolution=1280, yresolution=720, spp=64)
     top = 1 << 24
+    # 0..40: maxdepth 5; beyond: bases whose digit count leaves a longer or no six-digit tail
+    # (ScrambledRadicalInverse24x6)
     for dim in range(0, 41):
         assert sc.halton_fastpath_mismatches(dim, 0, top, 61) == 0, dim
         assert sc.halton_fastpath_mismatches(dim, top - (1 << 16), top) == 0, dim
         assert sc.halton_fastpath_mismatches(dim, 0, 1 << 16) == 0, dim
+    deep = pa.load_scene(SCENES / "cornell-box.pbrt", xresolution=1280, yresolution=720, spp=64, maxdepth=60)
+    for dim in (55, 97, 146, 300, 426):
+        assert deep.halton_fastpath_mismatches(dim, 0, top, 61) == 0, dim
+        assert deep.halton_fastpath_mismatches(dim, top - (1 << 16), top) == 0, dim
     assert sc.halton_fastpath_mismatches(0, 0, top + 1) == -1
 
 

@@ -200,6 +200,10 @@ typedef struct pbrt_scene_flat {
      * isRectangle; flags bit2 uv present, bit3 vertex normals present (shape_normals [n][12],
      * render space) */
     const float *shape_normals;
+    /* alpha-tested primitives (GeometricPrimitive alpha, cpu/primitive.cpp:56-80; gpu/optix.cu
+     * alphaKilled): [n_triangles + n_shapes] in scene order, the float texture node (index into
+     * the tex_node tables) of the primitive's alpha, or -1; NULL when no shape has one */
+    const int32_t *prim_alpha;
 } pbrt_scene_flat;
 
 typedef struct pbrt_render_params {

@@ -665,6 +665,7 @@ static Interaction TriangleInteraction(Vec p0, Vec p1, Vec p2, bool flip, TriIse
 
 // simple binned-SAH BVH2 over the scene triangles (oracle-side; any correct BVH gives the
 // same closest hit up to exact-t ties)
+struct OTextures;
 struct BVHNode {
     Vec mn, mx;
     int left = -1, right = -1, first = 0, count = 0, axis = 0;
@@ -673,6 +674,7 @@ struct BVHNode {
 struct OShape;
 struct Scene {
     const pbrt_scene_flat *f;
+    const OTextures *tex = nullptr;  // alpha textures (f->prim_alpha)
     std::vector<OShape> shapes;  // spheres and disks: prim ids n_triangles + k
     std::vector<Vec> v;
     std::vector<int> tri;  // 3 per triangle
@@ -791,6 +793,11 @@ struct Scene {
         return IntersectShapes(o, d, best >= 0 ? hit->t : tMax, hit, anyHit, best);
     }
     int IntersectShapes(Vec o, Vec d, Float tMax, TriIsect *hit, bool anyHit, int best) const;
+    // GeometricPrimitive's alpha test as pbrt's GPU any-hit programs apply it (gpu/optix.cu:
+    // 197-243): the candidate is ignored when its alpha texture is <= 0 at the hit, or < 1 and
+    // below HashFloat(ray o, ray d)
+    bool AlphaKilled(int prim, const TriIsect &ti, Vec o, Vec d) const;
+    bool Alpha(int prim) const { return f->prim_alpha && f->prim_alpha[prim] >= 0; }
     // the per-primitive attributes of a triangle or a shape
     int Material(int prim) const;
     int Light(int prim) const;
@@ -810,6 +817,7 @@ struct Scene {
                     int t = order[i];
                     TriIsect ti;
                     if (IntersectTriangle(o, d, tMax, P(t, 0), P(t, 1), P(t, 2), &ti)) {
+                        if (Alpha(t) && AlphaKilled(t, ti, o, d)) continue;
                         if (anyHit) return t;
                         tMax = ti.t;
                         *hit = ti;
@@ -1801,6 +1809,8 @@ int Scene::IntersectShapes(Vec o, Vec d, Float tMax, TriIsect *hit, bool anyHit,
         Float th;
         Vec pObj;
         if (shapes[k].Intersect(o, d, tMax, &th, &pObj)) {
+            const int prim = f->n_triangles + (int)k;
+            if (Alpha(prim) && AlphaKilled(prim, TriIsect{pObj.x, pObj.y, pObj.z, th}, o, d)) continue;
             tMax = th;
             *hit = TriIsect{pObj.x, pObj.y, pObj.z, th};
             best = f->n_triangles + (int)k;
@@ -4083,6 +4093,22 @@ struct OTextures {
 };
 
 // ---------------------------------------------------------------- integrator
+bool Scene::AlphaKilled(int prim, const TriIsect &ti, Vec o, Vec d) const {
+    const Interaction si = Interact(prim, ti, d);
+    OTexCtx c;
+    c.p = si.p;
+    c.n = si.n;
+    c.u = si.uv[0];
+    c.v = si.uv[1];
+    const Float a = tex->EvalF(f->prim_alpha[prim], c);
+    if (a >= 1) return false;
+    if (a <= 0) return true;
+    const float od[6] = {o.x, o.y, o.z, d.x, d.y, d.z};
+    unsigned char buf[24];
+    std::memcpy(buf, od, 24);
+    return (Float)(uint32_t)Murmur64A(buf, 24, 0) * 0x1p-32f > a;
+}
+
 struct Renderer {
     std::vector<OEnvLight> envs;  // ImageInfiniteLights (flat inf_image)
     // the image light behind global light index li, or null
@@ -4796,6 +4822,7 @@ int oracle_intersect_tr(const pbrt_scene_flat *flat, const pbrt_scene_info *info
     r.S.Init(flat, info);
     if (flat->n_tex_nodes > 0 && (!g_rgbTable || !g_ewaLut)) return -2;  // oracle_set_rgb_table first
     r.tex.Init(flat, info->spp, info->xres, info->yres);
+    r.S.tex = &r.tex;
     r.M.f = flat;
     r.M.n = flat->n_media;
     const int nt = std::max(1, std::min<int>(16, (int)std::thread::hardware_concurrency()));
@@ -4834,6 +4861,7 @@ int oracle_render(const pbrt_scene_flat *flat, const pbrt_scene_info *info, cons
     r.S.Init(flat, info);
     if (flat->n_tex_nodes > 0 && (!g_rgbTable || !g_ewaLut)) return -2;  // oracle_set_rgb_table first
     r.tex.Init(flat, info->spp, info->xres, info->yres);
+    r.S.tex = &r.tex;
     if ((flat->n_env > 0 || flat->n_tex_nodes > 0) && !g_rgbTable) return -2;
     r.envs.resize(flat->n_env);
     for (int k = 0; k < flat->n_env; ++k) r.envs[k].Init(flat, k);
@@ -4875,6 +4903,10 @@ int oracle_intersect_batch(const pbrt_scene_flat *flat, const pbrt_scene_info *i
                            int anyHit, int32_t *prim, float *hit) {
     Scene S;
     S.Init(flat, info);
+    if (flat->n_tex_nodes > 0 && (!g_rgbTable || !g_ewaLut)) return -2;  // oracle_set_rgb_table first
+    OTextures tex;
+    tex.Init(flat, info->spp, info->xres, info->yres);
+    S.tex = &tex;
     // independent rays: split over host threads (large scenes, 10^5+ rays in the tests)
     const int nt = std::max(1, std::min<int>(16, (int)std::thread::hardware_concurrency()));
     std::vector<std::thread> pool;

@@ -254,7 +254,7 @@ struct pbrt_scene {
     std::vector<int32_t> tris, lightPrim, lightSpectrum, lightTwoSided, infSpectrum, matConstant, nodeInfo, matType,
         matSpectra, plOffsets, infDistant, uniformOrder;
     std::vector<float> deltaLights;
-    std::vector<int32_t> infImage, envInfo, shapeInfo;
+    std::vector<int32_t> infImage, envInfo, shapeInfo, primAlpha;
     std::vector<float> shapeParams, shapeNormals;
     std::vector<float> envXform, envRgb;
     std::vector<uint64_t> envOffset;
@@ -266,6 +266,11 @@ struct pbrt_scene {
         shapeInfo.clear();
         shapeParams.clear();
         shapeNormals.clear();
+        primAlpha.clear();
+        if (!s.alphaTex.empty()) {
+            for (int id : s.triAlpha) primAlpha.push_back(id >= 0 ? s.alphaTex[id][0] : -1);
+            for (const AnalyticShapeDesc &a : s.shapes) primAlpha.push_back(a.alpha >= 0 ? s.alphaTex[a.alpha][0] : -1);
+        }
         for (const AnalyticShapeDesc &a : s.shapes) {
             shapeInfo.insert(shapeInfo.end(), {a.dev.kind, a.dev.flags, a.material, a.light, a.medium[0], a.medium[1], 0, 0});
             shapeParams.insert(shapeParams.end(), a.dev.r2o, a.dev.r2o + 12);
@@ -407,6 +412,7 @@ struct pbrt_context {
     DevBuf<uint16_t> plIndex;
     DevBuf<int> dispTerm;
     DevBuf<uint8_t> primFlip;
+    DevBuf<int> primAlpha;  // leaf order: alpha texture program or -1 (scenes with alpha only)
     DevBuf<uint32_t> lightBitTrail, permOffset, permNDigits, permBase;
     DevBuf<uint16_t> perm;
     DevBuf<HaltonDimDesc> haltonDim;
@@ -600,6 +606,15 @@ static void BuildDevice(pbrt_context *c) {
         pm[nt + k] = s.shapes[k].material;
         pl[nt + k] = s.shapes[k].light;
         po.push_back(nt + k);
+    }
+    if (!s.alphaTex.empty()) {
+        std::vector<int> pa(nt + nsh, -1);
+        for (int i = 0; i < nt; ++i) {
+            const int id = s.triAlpha[b.triPrim[i]];
+            pa[i] = id >= 0 ? s.alphaTex[id][1] : -1;
+        }
+        for (int k = 0; k < nsh; ++k) pa[nt + k] = s.shapes[k].alpha >= 0 ? s.alphaTex[s.shapes[k].alpha][1] : -1;
+        c->primAlpha.Upload(pa);
     }
     c->nodes.Upload(b.nodes);
     c->qnodes.Upload(b.qnodes);
@@ -914,6 +929,8 @@ static void BuildDevice(pbrt_context *c) {
     S.primMaterial = c->primMaterial.p;
     S.primLight = c->primLight.p;
     S.primFlip = c->primFlip.p;
+    S.primAlpha = c->primAlpha.p;
+    S.nAlpha = (int)s.alphaTex.size();
     S.primOrig = c->primOrig.p;
     S.nShapes = nsh;
     S.shapes = c->shapes.p;
@@ -951,10 +968,19 @@ static void BuildDevice(pbrt_context *c) {
         }
         c->matMix.Upload(mm);
         S.matMix = (const int4 *)c->matMix.p;
-        S.textured = s.texPrograms.empty() ? 0 : 1;
+        // textured: some material evaluates a program (the textured shade / texture kernels);
+        // the alpha tests of the traversal kernels may need the tables on their own
+        {
+            std::vector<bool> alphaOnly(s.texPrograms.size(), false);
+            for (const auto &a : s.alphaTex) alphaOnly[a[1]] = true;
+            for (const MaterialDesc &m : s.materials)
+                for (int p : {m.texReflectance, m.texURough, m.texVRough, m.texAmount})
+                    if (p >= 0) alphaOnly[p] = false;
+            S.textured = std::any_of(alphaOnly.begin(), alphaOnly.end(), [](bool a) { return !a; }) ? 1 : 0;
+        }
         S.tex = TexView{};
-        if (S.textured) {
-            if (c->volumetric)
+        if (!s.texPrograms.empty()) {
+            if (S.textured && c->volumetric)
                 throw Error("textures or mix materials together with the volumetric path (media, interface, layered, "
                             "thin dielectric, diffuse transmission or dispersive materials) are not supported yet");
             c->texNodes.Upload(tt.nodes);
@@ -1661,6 +1687,7 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
     f->shape_info = scene->shapeInfo.data();
     f->shape_params = scene->shapeParams.data();
     f->shape_normals = scene->shapeNormals.data();
+    f->prim_alpha = scene->primAlpha.empty() ? nullptr : scene->primAlpha.data();
     f->uniform_order = scene->uniformOrder.data();
     f->scene_radius = s.sceneRadius;
     {

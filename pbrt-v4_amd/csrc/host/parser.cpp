@@ -334,8 +334,12 @@ class Parser {
         std::string areaLight;
         ParamSet areaParams;
         std::string loc;
+        bool hasAlpha = false;  // "float alpha" < 1 or "texture alpha" (scene.cpp:1369-1384)
+        Param alpha;
     };
     std::vector<PendingShape> shapes;
+    std::map<std::string, int> alphaIds;  // alpha parameter -> SceneDesc::alphaTex entry
+    int AlphaId(const PendingShape &s);
     // object instancing (scene.cpp:309-395): shapes of each ObjectBegin/End definition, and the
     // ObjectInstance uses, resolved after parsing (a use may precede its definition)
     std::map<std::string, std::vector<PendingShape>> instanceDefs;
@@ -1018,6 +1022,12 @@ class Parser {
         } else {
             throw Error(ps.loc + ": shape \"" + type + "\" is not supported yet");
         }
+        if (Param *a = ps.Find("alpha")) {
+            if (a->type != "float" && a->type != "texture")
+                throw Error(ps.loc + ": \"" + a->type + " alpha\" must be a float or a texture");
+            s.alpha = *a;
+            s.hasAlpha = true;
+        }
         ps.CheckUnused();
         s.renderFromObject = gs.ctm;  // renderFromWorld applied at Finish
         s.flip = gs.reverseOrientation;
@@ -1079,6 +1089,7 @@ class Parser {
             d.d = radians(Clampf(s.sp[3], 0, 360));
         }
         a.material = mat;
+        a.alpha = AlphaId(s);
         if (!scene.media.empty()) {
             a.medium[0] = (int16_t)mediumOf(s.insideMedium, s.loc);
             a.medium[1] = (int16_t)mediumOf(s.outsideMedium, s.loc);
@@ -1159,6 +1170,7 @@ class Parser {
             d.a = area;
             d.b = rect ? 1.f : 0.f;
             a.material = mat;
+            a.alpha = AlphaId(s);
             if (!scene.media.empty()) {
                 a.medium[0] = (int16_t)mediumOf(s.insideMedium, s.loc);
                 a.medium[1] = (int16_t)mediumOf(s.outsideMedium, s.loc);
@@ -1641,6 +1653,9 @@ void Parser::Finish() {
                 throw Error(ap.loc + ": \"filename\" (image) area lights not supported yet");
             }
             ap.CheckUnused();
+            // DiffuseAreaLight::AlphaMasked (lights.h) masks the emission of an alpha-tested
+            // emitter by HashFloat(p); not on this path yet
+            if (AlphaId(s) >= 0) throw Error(s.loc + ": \"alpha\" on area lights is not supported yet");
         }
         if (s.kind == kShapeSphereT || s.kind == kShapeDiskT || s.kind == kShapeCylinderT) {
             AnalyticShape(s, rfo, mat, lightSpectrum, lightScale, twoSided, power, mediumOf);
@@ -1648,7 +1663,9 @@ void Parser::Finish() {
         }
         if (!s.quadIdx.empty())
             BilinearPatches(s, rfo, mat, lightSpectrum, lightScale, twoSided, power, mediumOf, base);
+        const int alphaId = AlphaId(s);
         for (size_t t = 0; t < s.idx.size(); t += 3) {
+            scene.triAlpha.push_back(alphaId);
             std::array<int, 3> tri = {base + s.idx[t], base + s.idx[t + 1], base + s.idx[t + 2]};
             int triIndex = (int)scene.tris.size();
             scene.tris.push_back(tri);
@@ -2168,6 +2185,35 @@ int Parser::InstTex(const std::string &name, bool spectrum, int specType, const 
     texInProgress.erase({name, spectrum});
     texInstances[key] = result;
     return result;
+}
+
+// The shape's alpha texture (scene.cpp:1369-1384 getAlphaTexture): a named float texture, or a
+// constant "float alpha" below 1 (1 or more: no alpha test); -1 when there is none.  One
+// SceneDesc::alphaTex entry (texture node, compiled program) per distinct parameter.
+int Parser::AlphaId(const PendingShape &s) {
+    if (!s.hasAlpha) return -1;
+    std::string key;
+    if (s.alpha.type == "texture") {
+        if (s.alpha.strs.size() != 1) throw Error(s.loc + ": \"texture alpha\" needs one texture name");
+        if (!pendingTextures.count({s.alpha.strs[0], false}))
+            throw Error(s.loc + ": " + s.alpha.strs[0] + ": couldn't find float texture for \"alpha\" parameter.");
+        key = "t:" + s.alpha.strs[0];
+    } else {
+        if (s.alpha.nums.empty()) throw Error(s.loc + ": \"float alpha\" needs a value");
+        const float a = (float)s.alpha.nums[0];
+        if (!(a < 1.f)) return -1;
+        char b[32];
+        std::snprintf(b, sizeof b, "f:%a", a);
+        key = b;
+    }
+    auto it = alphaIds.find(key);
+    if (it != alphaIds.end()) return it->second;
+    const int node = FloatParamNode(&s.alpha, 1.f, s.loc);
+    const int prog = CompileTexProgram(scene, node, false);
+    scene.alphaTex.push_back({node, prog});
+    const int id = (int)scene.alphaTex.size() - 1;
+    alphaIds[key] = id;
+    return id;
 }
 
 void Parser::ResolveTextures() {

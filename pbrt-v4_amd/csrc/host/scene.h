@@ -186,6 +186,7 @@ struct AnalyticShapeDesc {
     std::array<float, 12> normals{};  // bilinear patch: render-space vertex normals (dev.flags bit 3)
     int material = -1;
     int light = -1;                   // area light index or -1
+    int alpha = -1;                   // SceneDesc::alphaTex entry or -1
     int16_t medium[2] = {-1, -1};     // {inside, outside}
 };
 
@@ -268,6 +269,9 @@ struct SceneDesc {
     std::vector<int> triMaterial;   // material index
     std::vector<int> triLight;      // area light index or -1
     std::vector<uint8_t> triFlip;   // reverseOrientation ^ transformSwapsHandedness
+    std::vector<int> triAlpha;      // alphaTex entry or -1 (GeometricPrimitive alpha test)
+    // alpha textures: {texture node, compiled float program}; shapes refer to them by index
+    std::vector<std::array<int, 2>> alphaTex;
     // shading attributes (TriangleMesh n / uv, util/mesh.cpp:23-68): per vertex, meaningful
     // only for triangles whose triShade bit says so (bit0 normals, bit1 uv)
     std::vector<V3> vertN;                       // render space, reverseOrientation applied

@@ -613,7 +613,17 @@ __device__ inline SceneLds SetupSceneLds(const DeviceScene &S, float4 *dyn) {
 struct TravCount {
     int nodes = 0, tris = 0;
 };
-template <bool AnyHit, bool Compressed, bool NodesInLds, bool TrisInLds>
+// GeometricPrimitive's stochastic alpha test as pbrt's GPU any-hit programs apply it to every
+// candidate hit (gpu/optix.cu:197-243, 368-381, 449-461): the alpha texture at the candidate's
+// SurfaceInteraction (p, n, uv; no derivatives) kills it when alpha <= 0, or when alpha < 1 and
+// HashFloat(ray o, ray d) > alpha.  One hash per ray, so the surviving hits are the same in
+// any traversal order.  Out of line (defined with the texture code below): only the alpha
+// instantiations call it.  b0..b2: the triangle's barycentrics, or a shape's pObj.
+__device__ __attribute__((noinline)) bool AlphaKilled(const DeviceScene *S, int prim, float b0, float b1, float b2,
+                                                     V3 o, V3 d);
+// Alpha: the scene has alpha-tested primitives (S.primAlpha); compiled into the kTravShapes
+// ("extended") instantiations only
+template <bool AnyHit, bool Compressed, bool NodesInLds, bool TrisInLds, bool Alpha = false>
 __device__ inline int TraverseCW(const DeviceScene &S, const SceneLds &L, V3 o, V3 d, float tMax, TriHit *best,
                                  TravCount *cnt = nullptr) {
     const TriRayR tr = MakeTriRayR(o, d);
@@ -652,6 +662,9 @@ __device__ inline int TraverseCW(const DeviceScene &S, const SceneLds &L, V3 o, 
             }
             TriHit h;
             if (IntersectTriangleRot(tr, tMax, a, b, c, &h)) {
+                if constexpr (Alpha) {
+                    if (S.nAlpha > 0 && S.primAlpha[t] >= 0 && AlphaKilled(S.self, t, h.b0, h.b1, h.b2, o, d)) continue;
+                }
                 if (AnyHit) return t;
                 tMax = h.t;
                 *best = h;
@@ -685,20 +698,23 @@ __device__ inline int TraverseCW(const DeviceScene &S, const SceneLds &L, V3 o, 
 // waves per SIMD (= 256-thread blocks per CU) a traversal kernel of mode TM is compiled for
 // A mode may carry kTravShapes: the scene has analytic shapes, whose BVH is traversed after the
 // triangles' (an out-of-line call, compiled only into these instantiations so the triangle-only
-// kernels keep their register allocation and scratch).
+// kernels keep their register allocation and scratch), or alpha-tested primitives.
 constexpr int kTravShapes = 4;
 constexpr int TraversalWaves(int tm) {
     return (tm & 3) == kTravQuant ? PBRT_QUANT_TRAVERSAL_WAVES : PBRT_TRAVERSAL_WAVES;
 }
 inline int TraversalMode(const DeviceScene &S) {
-    return (S.compressed ? kTravQuant : (S.ldsTris > 0 ? kTravLds : kTravWide)) | (S.nShapes > 0 ? kTravShapes : 0);
+    return (S.compressed ? kTravQuant : (S.ldsTris > 0 ? kTravLds : kTravWide)) |
+           (S.nShapes > 0 || S.nAlpha > 0 ? kTravShapes : 0);
 }
 // Spheres and disks (Sphere / Disk::BasicIntersect) through their binary BVH, nearer than
 // tMax: the shape index and best = {pObj, tHit}, or -1.  Out of line: only scenes with shapes
 // reach it, and the triangle traversal keeps its registers.
+// primAlpha (null: no alpha test) is the scene's leaf-order array, shape k at nTris + k
 template <bool AnyHit>
 __device__ __attribute__((noinline)) int TraverseShapes(const ShapeBVHNode *shapeNodes, const DeviceShape *shapes, V3 o,
-                                                        V3 d, float tMax, TriHit *best) {
+                                                        V3 d, float tMax, TriHit *best, const int *primAlpha,
+                                                        int nTris, const DeviceScene *self) {
     const V3 inv(1 / d.x, 1 / d.y, 1 / d.z);
     int stack[32], sp = 0, found = -1;
     stack[sp++] = 0;
@@ -726,6 +742,8 @@ __device__ __attribute__((noinline)) int TraverseShapes(const ShapeBVHNode *shap
                 float th;
                 V3 pObj;
                 if (ShapeIntersect(shapes[k], o, d, tMax, &th, &pObj)) {
+                    if (primAlpha && primAlpha[nTris + k] >= 0 && AlphaKilled(self, nTris + k, pObj.x, pObj.y, pObj.z, o, d))
+                        continue;
                     found = k;
                     tMax = th;
                     *best = TriHit{pObj.x, pObj.y, pObj.z, th};
@@ -745,9 +763,11 @@ __device__ inline int Traverse(const DeviceScene &S, const SceneLds &L, V3 o, V3
     constexpr int tm = TM & 3;
     int prim = -1;
     if constexpr ((TM & kTravShapes) != 0) {
-        if (S.nTris > 0) prim = TraverseCW<AnyHit, tm == kTravQuant, tm == kTravLds, tm == kTravLds>(S, L, o, d, tMax, best, cnt);
-        if (!(AnyHit && prim >= 0)) {
-            const int k = TraverseShapes<AnyHit>(S.shapeNodes, S.shapes, o, d, prim >= 0 ? best->t : tMax, best);
+        if (S.nTris > 0)
+            prim = TraverseCW<AnyHit, tm == kTravQuant, tm == kTravLds, tm == kTravLds, true>(S, L, o, d, tMax, best, cnt);
+        if (S.nShapes > 0 && !(AnyHit && prim >= 0)) {
+            const int k = TraverseShapes<AnyHit>(S.shapeNodes, S.shapes, o, d, prim >= 0 ? best->t : tMax, best,
+                                                 S.nAlpha > 0 ? S.primAlpha : nullptr, S.nTris, S.self);
             if (k >= 0) prim = S.nTris + k;
         }
     } else {
@@ -1357,6 +1377,25 @@ __device__ inline void GenerateCameraRay(const DeviceScene &S, const PathState &
 }  // namespace pbrt_amd
 
 namespace pbrt_amd {
+__device__ __attribute__((noinline)) bool AlphaKilled(const DeviceScene *Sp, int prim, float b0, float b1, float b2,
+                                                     V3 o, V3 d) {
+    const DeviceScene &S = *Sp;
+    V3 p0, p1, p2;
+    PrimVerts(S, prim, &p0, &p1, &p2);
+    const TriSurface surf = SurfaceAt<true>(S, prim, p0, p1, p2, b0, b1, b2);
+    TexEvalCtx c;
+    c.p = surf.p;
+    c.n = surf.n;
+    c.u = surf.uv[0];
+    c.v = surf.uv[1];
+    c.dudx = c.dudy = c.dvdx = c.dvdy = 0;
+    const float a = TexFloatFast(S, S.primAlpha[prim], c);
+    if (a >= 1) return false;
+    if (a <= 0) return true;
+    const uint32_t w[6] = {FloatToBits(o.x), FloatToBits(o.y), FloatToBits(o.z),
+                           FloatToBits(d.x), FloatToBits(d.y), FloatToBits(d.z)};
+    return (float)(uint32_t)HashWords(w, 6) * 0x1p-32f > a;  // HashFloat(o, d)
+}
 // MixMaterial::ChooseMaterial until a non-mix material is reached (materials.h:285-294), as the
 // closest-hit stage does (wavefront/intersect.h:90-97): the "amount" texture at the hit (the
 // context a SurfaceInteraction gives: no (u,v) derivatives), then HashFloat(p, wo, m0, m1).

@@ -118,6 +118,10 @@ struct DeviceScene {
     const int *primMaterial;
     const int *primLight;
     const uint8_t *primFlip;
+    // alpha-tested primitives (GeometricPrimitive alpha): leaf order, the alpha texture's
+    // program or -1; nAlpha = 0 (and primAlpha null) when no shape has an alpha texture
+    const int *primAlpha;
+    int nAlpha;
     const int *primOrig;  // leaf order -> the scene's triangle index (boundary results)
     // per-triangle shading attributes (leaf order, 4 float4 each: n0|flags, n1|u0, n2|v0,
     // u1 v1 u2 v2), nullptr when no mesh has vertex normals or uv

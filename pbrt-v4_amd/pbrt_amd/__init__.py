@@ -97,6 +97,7 @@ class SceneFlat(ctypes.Structure):
         ("shape_info", ctypes.POINTER(ctypes.c_int32)),
         ("shape_params", ctypes.POINTER(ctypes.c_float)),
         ("shape_normals", ctypes.POINTER(ctypes.c_float)),
+        ("prim_alpha", ctypes.POINTER(ctypes.c_int32)),
     ]
 
 

@@ -204,6 +204,10 @@ typedef struct pbrt_scene_flat {
      * alphaKilled): [n_triangles + n_shapes] in scene order, the float texture node (index into
      * the tex_node tables) of the primitive's alpha, or -1; NULL when no shape has one */
     const int32_t *prim_alpha;
+    /* RGBFilm / PixelSensor (film.cpp:222-262, 582-600): "maxcomponentvalue" (inf when not
+     * given) and the sensor's XYZFromSensorRGB (row major); sensor_xyz holds its r/g/b curves */
+    float max_component_value;
+    float xyz_from_sensor_rgb[9];
 } pbrt_scene_flat;
 
 typedef struct pbrt_render_params {

@@ -4882,6 +4882,12 @@ int oracle_render(const pbrt_scene_flat *flat, const pbrt_scene_info *info, cons
                 for (int s = firstSample; s < firstSample + nSamples; ++s) {
                     float rgb[3], w;
                     r.Li(x, y, s, rgb, &w);
+                    // RGBFilm::AddSample's clamp (film.h:247-249)
+                    const float m = std::max({rgb[0], rgb[1], rgb[2]});
+                    if (m > flat->max_component_value) {
+                        const float sc = flat->max_component_value / m;
+                        for (int c = 0; c < 3; ++c) rgb[c] *= sc;
+                    }
                     film[pix] += w * rgb[0];
                     film[npix + pix] += w * rgb[1];
                     film[2 * npix + pix] += w * rgb[2];

@@ -1056,6 +1056,7 @@ static void BuildDevice(pbrt_context *c) {
     S.sensor = c->sensor.p;
     S.sensor4 = (const float4 *)c->sensor4.p;
     S.imagingRatio = s.imagingRatio;
+    S.maxComponentValue = s.maxComponentValue;
     for (int i = 0; i < 4; ++i)
         for (int j = 0; j < 4; ++j) {
             S.cameraFromRaster[4 * i + j] = (float)s.camera.cameraFromRaster[i][j];
@@ -1718,6 +1719,9 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
     f->dense_spectra = scene->dense.data();
     f->sensor_xyz = scene->sensor.data();
     f->imaging_ratio = s.imagingRatio;
+    f->max_component_value = s.maxComponentValue;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) f->xyz_from_sensor_rgb[3 * i + j] = s.xyzFromSensorRGB[i][j];
     for (int i = 0; i < 4; ++i)
         for (int j = 0; j < 4; ++j) {
             f->camera_from_raster[4 * i + j] = (float)s.camera.cameraFromRaster[i][j];

@@ -1239,22 +1239,6 @@ static std::array<float, 311> DensePiecewiseLinear(const std::vector<double> &nu
     return out;
 }
 
-// Blackbody (util/spectrum.h): Planck's law with the CPU FastExp, in pbrt's float operation
-// order; BlackbodySpectrum divides by its value at Wien's peak
-static float Blackbody(float lambda, float T) {
-    if (T <= 0) return 0;
-    const float c = 299792458.f, h = 6.62606957e-34f, kb = 1.3806488e-23f;
-    const float l = lambda * 1e-9f;
-    const float l2 = l * l;
-    const float l5 = l2 * l2 * l;  // Pow<5>
-    return (2 * h * c * c) / (l5 * (FastExp((h * c) / (l * kb * T)) - 1));
-}
-static float BlackbodyNormalized(float lambda, float T) {
-    const float lambdaMax = 2.8977721e-3f / T;
-    const float norm = 1 / Blackbody(lambdaMax * 1e9f, T);
-    return Blackbody(lambda, T) * norm;
-}
-
 static float PhotometricOf(const std::array<float, 311> &dense) {
     // SpectrumToPhotometric (util/spectrum.cpp:37-51) over the dense samples
     const SpectralData &d = GetSpectralData();
@@ -1365,10 +1349,10 @@ void Parser::Finish() {
             scene.py1 = v[3];
         }
         double iso = filmParams.GetFloat("iso", 100.);
-        std::string sensor = filmParams.GetString("sensor", "cie1931");
-        if (sensor != "cie1931") throw Error(filmParams.loc + ": only the cie1931 sensor is supported");
-        if (filmParams.GetFloat("whitebalance", 0) != 0) throw Error(filmParams.loc + ": whitebalance not supported");
-        if (filmParams.Find("maxcomponentvalue")) throw Error(filmParams.loc + ": maxcomponentvalue not supported");
+        // PixelSensor::Create (film.cpp:222-262) and RGBFilm's clamp (film.cpp:585)
+        scene.sensorName = filmParams.GetString("sensor", "cie1931");
+        scene.whiteBalance = (float)filmParams.GetFloat("whitebalance", 0);
+        scene.maxComponentValue = (float)filmParams.GetFloat("maxcomponentvalue", kInfinity);
         filmParams.Find("savefp16");
         filmParams.Find("diagonal");
         double exposure = cameraParams.GetFloat("shutterclose", 1.0) - cameraParams.GetFloat("shutteropen", 0.0);
@@ -1473,12 +1457,24 @@ void Parser::Finish() {
     ResolveTextures();
     // ---- sensor / output colour space
     {
+        // RGBFilm: outputRGBFromSensorRGB = colorSpace->RGBFromXYZ * sensor->XYZFromSensorRGB
         const SpectralData &sd = GetSpectralData();
-        scene.sensorX = sd.denseX;
-        scene.sensorY = sd.denseY;
-        scene.sensorZ = sd.denseZ;
+        PixelSensorDesc ps;
+        try {
+            ps = BuildPixelSensor(scene.sensorName, scene.whiteBalance);
+        } catch (const Error &e) {
+            throw Error(filmParams.loc + ": " + e.what());
+        }
+        scene.sensorX = ps.r;
+        scene.sensorY = ps.g;
+        scene.sensorZ = ps.b;
         for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j) scene.outputRGBFromSensorRGB[i][j] = sd.rgbFromXYZ[i][j];
+            for (int j = 0; j < 3; ++j) {
+                scene.xyzFromSensorRGB[i][j] = ps.xyzFromSensorRGB[i][j];
+                double v = 0;
+                for (int k = 0; k < 3; ++k) v += sd.rgbFromXYZ[i][k] * ps.xyzFromSensorRGB[k][j];
+                scene.outputRGBFromSensorRGB[i][j] = v;
+            }
     }
     // ---- media (MakeNamedMedium -> HomogeneousMedium / GridMedium, media.cpp:167-330)
     std::map<std::string, int> mediumIndex;

@@ -260,6 +260,10 @@ struct SceneDesc {
     int filterNu = 0, filterNv = 0;
     std::vector<float> filterTable;
     float imagingRatio = 1;
+    std::string sensorName = "cie1931";
+    float whiteBalance = 0;                    // Film "whitebalance" (0: none)
+    float maxComponentValue = kInfinity;       // RGBFilm::AddSample clamp (film.h:247-249)
+    float xyzFromSensorRGB[3][3];              // PixelSensor::XYZFromSensorRGB
     double outputRGBFromSensorRGB[3][3];
     CameraDesc camera;
 
@@ -355,7 +359,25 @@ struct SpectralData {
     double rgbFromXYZ[3][3];
     std::array<float, 256> srgbToLinear;  // SRGBToLinearLUT (util/color.cpp:286)
     std::array<float, 128> mipFilterLUT;  // MIPFilterLUT (util/mipmap.cpp:59-191)
+    std::map<std::string, std::vector<float>> sensors;  // "<camera>_r|g|b" interleaved curves
+    std::vector<float> cieSLambda, cieS0, cieS1, cieS2;  // CIE daylight basis (Spectra::D)
+    std::vector<std::vector<float>> swatches;           // 24 ColorChecker reflectances (film.cpp)
 };
+// PixelSensor (film.h:36-116, PixelSensor::Create film.cpp:222-262): the sensor's r/g/b matching
+// curves densely sampled over 395..705 nm and XYZFromSensorRGB -- the CIE 1931 curves with an
+// optional white balance (Bradford, util/color.h WhiteBalance), or a named camera's curves with
+// the matrix fitted by LinearLeastSquares to the 24 swatches under the D(whitebalance)
+// illuminant (6500 K when unspecified).  Throws for an unknown sensor.
+struct PixelSensorDesc {
+    std::array<float, 311> r, g, b;
+    float xyzFromSensorRGB[3][3];
+    std::array<float, 311> illum;  // the white-balance illuminant (zeros without one)
+};
+PixelSensorDesc BuildPixelSensor(const std::string &name, float whiteBalanceTemp);
+// BlackbodySpectrum(T)(lambda) (util/spectrum.h): normalised to 1 at Wien's peak
+float BlackbodyNormalized(float lambda, float T);
+// Spectra::D(T) (util/spectrum.cpp:2537-2570) densely sampled over 395..705
+std::array<float, 311> DenseCIEDaylight(float T);
 // The whole 64^3 sRGB RGBToSpectrumTable (cmd/rgb2spec_opt.cpp output): zNodes[64] then
 // data[3][64][64][64][3]; loaded from data/rgbspec_srgb.bin (written by the build), computed
 // in parallel (and cached there) when the file is absent

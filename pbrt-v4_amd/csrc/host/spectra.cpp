@@ -91,6 +91,14 @@ static SpectralData LoadSpectralData() {
             haveSrgbLUT = true;
         }
         else if (name.rfind("named:", 0) == 0) tof(d.named[name.substr(6)]);
+        else if (name.rfind("sensor:", 0) == 0) tof(d.sensors[name.substr(7)]);
+        else if (name.rfind("swatch:", 0) == 0) {
+            d.swatches.emplace_back();
+            tof(d.swatches.back());
+        } else if (name == "CIE_S_lambda") tof(d.cieSLambda);
+        else if (name == "CIE_S0") tof(d.cieS0);
+        else if (name == "CIE_S1") tof(d.cieS1);
+        else if (name == "CIE_S2") tof(d.cieS2);
     }
     if (d.cieX.size() != 471 || d.optX.size() != 95) throw Error("malformed spectral data " + path);
     if (!haveMipLUT || !haveSrgbLUT)
@@ -531,5 +539,214 @@ PLSpectrumDesc NamedPiecewiseLinear(const std::string &name) {
         d.value.push_back(d.value.back());
     }
     return d;
+}
+}  // namespace pbrt_amd
+
+namespace pbrt_amd {
+// Blackbody (util/spectrum.h): Planck's law with the CPU FastExp, in pbrt's float operation
+// order; BlackbodySpectrum divides by its value at Wien's peak
+static float Blackbody(float lambda, float T) {
+    if (T <= 0) return 0;
+    const float c = 299792458.f, h = 6.62606957e-34f, kb = 1.3806488e-23f;
+    const float l = lambda * 1e-9f;
+    const float l2 = l * l;
+    const float l5 = l2 * l2 * l;  // Pow<5>
+    return (2 * h * c * c) / (l5 * (FastExp((h * c) / (l * kb * T)) - 1));
+}
+float BlackbodyNormalized(float lambda, float T) {
+    const float lambdaMax = 2.8977721e-3f / T;
+    const float norm = 1 / Blackbody(lambdaMax * 1e9f, T);
+    return Blackbody(lambda, T) * norm;
+}
+
+// PiecewiseLinearSpectrum::FromInterleaved(samples, normalize = false) (util/spectrum.cpp:
+// 133-163): split, then extended to Lambda_min - 1 / Lambda_max + 1 by the end values
+static void SplitInterleaved(const std::vector<float> &iv, std::vector<float> *lam, std::vector<float> *val) {
+    lam->clear();
+    val->clear();
+    for (size_t i = 0; i + 1 < iv.size(); i += 2) {
+        lam->push_back(iv[i]);
+        val->push_back(iv[i + 1]);
+    }
+    if (lam->front() > kLambdaMin) {
+        lam->insert(lam->begin(), kLambdaMin - 1);
+        val->insert(val->begin(), val->front());
+    }
+    if (lam->back() < kLambdaMax) {
+        lam->push_back(kLambdaMax + 1);
+        val->push_back(val->back());
+    }
+}
+static std::array<float, 311> DenseOf(const std::vector<float> &lam, const std::vector<float> &val) {
+    std::array<float, 311> d;
+    for (int l = 395; l <= 705; ++l) d[l - 395] = PiecewiseLinearEval(lam, val, (float)l);
+    return d;
+}
+// InnerProduct(f, g) over Float lambda = Lambda_min..Lambda_max (util/spectrum.h)
+static float InnerDense(const std::array<float, 311> &f, const std::array<float, 311> &g) {
+    float s = 0;
+    for (float lambda = kLambdaMin; lambda <= kLambdaMax; ++lambda) s += f[DenseOffset(lambda)] * g[DenseOffset(lambda)];
+    return s;
+}
+typedef std::array<std::array<float, 3>, 3> M3;
+static M3 Mul3(const M3 &a, const M3 &b) {
+    M3 r{};
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) r[i][j] = (float)((double)a[i][0] * b[0][j] + (double)a[i][1] * b[1][j] + (double)a[i][2] * b[2][j]);
+    return r;
+}
+// SpectrumToXYZ(s).xy() (util/color.cpp)
+static void WhiteXY(const std::array<float, 311> &s, float *x, float *y) {
+    const SpectralData &d = GetSpectralData();
+    const float CIE_Y_integral = 106.856895f;
+    const float X = InnerDense(d.denseX, s) / CIE_Y_integral, Y = InnerDense(d.denseY, s) / CIE_Y_integral,
+                Z = InnerDense(d.denseZ, s) / CIE_Y_integral;
+    *x = X / (X + Y + Z);
+    *y = Y / (X + Y + Z);
+}
+// WhiteBalance(srcWhite, targetWhite) (util/color.h:551-560): Bradford
+static M3 WhiteBalanceM(float sx, float sy, float tx, float ty) {
+    const M3 LMSFromXYZ = {{{0.8951f, 0.2664f, -0.1614f}, {-0.7502f, 1.7135f, 0.0367f}, {0.0389f, -0.0685f, 1.0296f}}};
+    const M3 XYZFromLMS = {{{0.986993f, -0.147054f, 0.159963f}, {0.432305f, 0.51836f, 0.0492912f},
+                            {-0.00852866f, 0.0400428f, 0.968487f}}};
+    auto fromxyY = [](float x, float y) { return std::array<float, 3>{x / y, 1.f, (1 - x - y) / y}; };
+    const std::array<float, 3> src = fromxyY(sx, sy), dst = fromxyY(tx, ty);
+    float srcL[3], dstL[3];
+    for (int i = 0; i < 3; ++i) {
+        srcL[i] = LMSFromXYZ[i][0] * src[0] + LMSFromXYZ[i][1] * src[1] + LMSFromXYZ[i][2] * src[2];
+        dstL[i] = LMSFromXYZ[i][0] * dst[0] + LMSFromXYZ[i][1] * dst[1] + LMSFromXYZ[i][2] * dst[2];
+    }
+    M3 D{};
+    for (int i = 0; i < 3; ++i) D[i][i] = dstL[i] / srcL[i];
+    return Mul3(Mul3(XYZFromLMS, D), LMSFromXYZ);
+}
+
+// Inverse(SquareMatrix<3>) (util/math.h:1449-1469): cofactors by DifferenceOfProducts over the
+// FMA-based Determinant (util/math.h:1420-1426), in float
+static float DoP(float a, float b, float c, float d) {
+    const float cd = c * d;
+    return std::fma(a, b, -cd) + std::fma(-c, d, cd);
+}
+static bool Invert3f(const float m[3][3], float r[3][3]) {
+    const float minor12 = DoP(m[1][1], m[2][2], m[1][2], m[2][1]);
+    const float minor02 = DoP(m[1][0], m[2][2], m[1][2], m[2][0]);
+    const float minor01 = DoP(m[1][0], m[2][1], m[1][1], m[2][0]);
+    const float det = std::fma(m[0][2], minor01, DoP(m[0][0], minor12, m[0][1], minor02));
+    if (det == 0) return false;
+    const float invDet = 1 / det;
+    r[0][0] = invDet * DoP(m[1][1], m[2][2], m[1][2], m[2][1]);
+    r[1][0] = invDet * DoP(m[1][2], m[2][0], m[1][0], m[2][2]);
+    r[2][0] = invDet * DoP(m[1][0], m[2][1], m[1][1], m[2][0]);
+    r[0][1] = invDet * DoP(m[0][2], m[2][1], m[0][1], m[2][2]);
+    r[1][1] = invDet * DoP(m[0][0], m[2][2], m[0][2], m[2][0]);
+    r[2][1] = invDet * DoP(m[0][1], m[2][0], m[0][0], m[2][1]);
+    r[0][2] = invDet * DoP(m[0][1], m[1][2], m[0][2], m[1][1]);
+    r[1][2] = invDet * DoP(m[0][2], m[1][0], m[0][0], m[1][2]);
+    r[2][2] = invDet * DoP(m[0][0], m[1][1], m[0][1], m[1][0]);
+    return true;
+}
+
+std::array<float, 311> DenseCIEDaylight(float temperature) {
+    const SpectralData &d = GetSpectralData();
+    const float cct = temperature * 1.4388f / 1.4380f;
+    std::array<float, 311> out;
+    if (cct < 4000) {  // CIE D ill-defined: a normalised blackbody
+        for (int l = 395; l <= 705; ++l) out[l - 395] = BlackbodyNormalized((float)l, cct);
+        return out;
+    }
+    if (d.cieS0.size() != 107) throw Error("malformed spectral data: no CIE daylight basis");
+    float x;
+    if (cct <= 7000)
+        x = -4.607f * 1e9f / (cct * cct * cct) + 2.9678f * 1e6f / (cct * cct) + 0.09911f * 1e3f / cct + 0.244063f;
+    else
+        x = -2.0064f * 1e9f / (cct * cct * cct) + 1.9018f * 1e6f / (cct * cct) + 0.24748f * 1e3f / cct + 0.23704f;
+    const float y = -3 * x * x + 2.870f * x - 0.275f;
+    const float M = 0.0241f + 0.2562f * x - 0.7341f * y;
+    const float M1 = (-1.3515f - 1.7703f * x + 5.9114f * y) / M;
+    const float M2 = (0.0300f - 31.4424f * x + 30.0717f * y) / M;
+    std::vector<float> v(107);
+    for (int i = 0; i < 107; ++i) v[i] = (float)((d.cieS0[i] + d.cieS1[i] * M1 + d.cieS2[i] * M2) * 0.01);
+    return DenseOf(d.cieSLambda, v);
+}
+
+PixelSensorDesc BuildPixelSensor(const std::string &name, float whiteBalanceTemp) {
+    const SpectralData &d = GetSpectralData();
+    PixelSensorDesc s{};
+    // PixelSensor::Create: named sensors white-balance to 6500 K unless told otherwise
+    if (name != "cie1931" && whiteBalanceTemp == 0) whiteBalanceTemp = 6500;
+    const bool haveIllum = whiteBalanceTemp != 0;
+    s.illum.fill(0.f);
+    if (haveIllum) s.illum = DenseCIEDaylight(whiteBalanceTemp);
+    // the output colour space's white (RGBColorSpace ctor: SpectrumToXYZ(illuminant).xy())
+    float wx, wy;
+    WhiteXY(d.denseD65, &wx, &wy);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) s.xyzFromSensorRGB[i][j] = i == j ? 1.f : 0.f;
+    if (name == "cie1931") {
+        s.r = d.denseX;
+        s.g = d.denseY;
+        s.b = d.denseZ;
+        if (haveIllum) {
+            float sx, sy;
+            WhiteXY(s.illum, &sx, &sy);
+            const M3 wb = WhiteBalanceM(sx, sy, wx, wy);
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) s.xyzFromSensorRGB[i][j] = wb[i][j];
+        }
+        return s;
+    }
+    auto curve = [&](const char *c) {
+        auto it = d.sensors.find(name + c);
+        if (it == d.sensors.end()) throw Error(name + ": unknown sensor type");
+        std::vector<float> lam, val;
+        SplitInterleaved(it->second, &lam, &val);
+        return DenseOf(lam, val);
+    };
+    s.r = curve("_r");
+    s.g = curve("_g");
+    s.b = curve("_b");
+    if (d.swatches.size() != 24) throw Error("malformed spectral data: no ColorChecker swatches");
+    // ProjectReflectance (film.h:119-131) of the swatches: camera RGB under the white-balance
+    // illuminant, XYZ under the colour space's illuminant scaled by sensorWhiteY / sensorWhiteG
+    float rgbCamera[24][3], xyzOutput[24][3];
+    const float sensorWhiteG = InnerDense(s.illum, s.g), sensorWhiteY = InnerDense(s.illum, d.denseY);
+    for (int i = 0; i < 24; ++i) {
+        std::vector<float> lam, val;
+        SplitInterleaved(d.swatches[i], &lam, &val);
+        float gi = 0, r3[3] = {0, 0, 0}, gx = 0, x3[3] = {0, 0, 0};
+        for (float lambda = kLambdaMin; lambda <= kLambdaMax; ++lambda) {
+            const int o = DenseOffset(lambda);
+            const float rl = PiecewiseLinearEval(lam, val, lambda);
+            gi += s.g[o] * s.illum[o];
+            r3[0] += s.r[o] * rl * s.illum[o];
+            r3[1] += s.g[o] * rl * s.illum[o];
+            r3[2] += s.b[o] * rl * s.illum[o];
+            gx += d.denseY[o] * d.denseD65[o];
+            x3[0] += d.denseX[o] * rl * d.denseD65[o];
+            x3[1] += d.denseY[o] * rl * d.denseD65[o];
+            x3[2] += d.denseZ[o] * rl * d.denseD65[o];
+        }
+        for (int c = 0; c < 3; ++c) {
+            rgbCamera[i][c] = r3[c] / gi;
+            xyzOutput[i][c] = (x3[c] / gx) * (sensorWhiteY / sensorWhiteG);
+        }
+    }
+    // LinearLeastSquares<3> (util/math.h:702-719): AtA and AtB accumulated in float,
+    // Transpose(Inverse(AtA) * AtB) with pbrt's float 3x3 cofactor inverse and the compensated
+    // SquareMatrix<3> product (InnerProduct: a correctly rounded float dot product)
+    float AtA[3][3] = {}, AtB[3][3] = {};
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            for (int r = 0; r < 24; ++r) {
+                AtA[i][j] += rgbCamera[r][i] * rgbCamera[r][j];
+                AtB[i][j] += rgbCamera[r][i] * xyzOutput[r][j];
+            }
+    float inv[3][3];
+    if (!Invert3f(AtA, inv)) throw Error("Sensor XYZ from RGB matrix could not be solved.");
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            s.xyzFromSensorRGB[j][i] =
+                (float)((double)inv[i][0] * AtB[0][j] + (double)inv[i][1] * AtB[1][j] + (double)inv[i][2] * AtB[2][j]);
+    return s;
 }
 }  // namespace pbrt_amd

@@ -184,6 +184,7 @@ struct DeviceScene {
     const float *sensor;
     const float4 *sensor4;  // same tables interleaved: {xbar, ybar, zbar, 0} per dense entry
     float imagingRatio;
+    float maxComponentValue;  // RGBFilm: a sample's sensor RGB is scaled down to this maximum
     // camera
     float cameraFromRaster[16];
     float renderFromCamera[16];

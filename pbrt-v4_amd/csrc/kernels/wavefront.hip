@@ -1377,6 +1377,14 @@ __global__ void __launch_bounds__(kBlock) k_film(DeviceScene S, PathState st, in
         float w = S.boxFilter ? 1.f : st.filterW[slot];
         const float *Ls = (st.lamTerm && st.lamTerm[slot]) ? st.L0 : st.L;  // terminated: lambda_0 only
         float rr = Ls[slot], gg = Ls[N + slot], bb = Ls[2 * N + slot];
+        // RGBFilm::AddSample (film.h:247-249): m = max(r, g, b) > maxComponentValue scales rgb
+        const float m = std::fmax(std::fmax(rr, gg), bb);
+        if (m > S.maxComponentValue) {
+            const float sc = S.maxComponentValue / m;
+            rr *= sc;
+            gg *= sc;
+            bb *= sc;
+        }
         sr += w * rr;
         sg += w * gg;
         sb += w * bb;

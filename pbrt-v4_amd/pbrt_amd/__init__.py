@@ -98,6 +98,8 @@ class SceneFlat(ctypes.Structure):
         ("shape_params", ctypes.POINTER(ctypes.c_float)),
         ("shape_normals", ctypes.POINTER(ctypes.c_float)),
         ("prim_alpha", ctypes.POINTER(ctypes.c_int32)),
+        ("max_component_value", ctypes.c_float),
+        ("xyz_from_sensor_rgb", ctypes.c_float * 9),
     ]
 
 

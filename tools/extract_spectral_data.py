@@ -16,7 +16,10 @@ reference's sources
     src/pbrt/util/mipmap.cpp     MIPFilterLUT (:59-191), the EWA filter weight table
     src/pbrt/util/spectrum.cpp   the interleaved (lambda, value) tables behind the named
                                  metal and glass spectra (:1128-1440), keyed by the names
-                                 Spectra::Init registers them under (:2666-2690)
+                                 Spectra::Init registers them under (:2666-2690), the camera
+                                 sensor curves (<camera>_r/_g/_b) and the CIE daylight basis
+                                 S0 / S1 / S2 (Spectra::D)
+    src/pbrt/film.cpp            the 24 ColorChecker swatch reflectances of PixelSensor
 
 and writes pbrt-v4_amd/data/spectral_data.json, which is committed.  Run it only in a
 container that has /root/reference; the GPU box uses the committed JSON.
@@ -98,6 +101,28 @@ def main():
         vals = numbers(array_body(spec, arr))
         assert len(vals) % 2 == 0 and len(vals) >= 4, (name, len(vals))
         data["named:" + name] = vals
+    # camera sensor response curves, registered in Spectra::Init as
+    # {"<camera>_r|g|b", PiecewiseLinearSpectrum::FromInterleaved(<array>, false, alloc)}
+    # (util/spectrum.cpp:2707-...), looked up by PixelSensor::Create (film.cpp:222-262)
+    for name, arr in re.findall(r'\{"(\w+_[rgb])",\s*PiecewiseLinearSpectrum::FromInterleaved\((\w+),\s*false,\s*alloc\)\}',
+                                spec):
+        vals = numbers(array_body(spec, arr))
+        assert len(vals) % 2 == 0 and len(vals) >= 4, (name, len(vals))
+        data["sensor:" + name] = vals
+    assert sum(k.startswith("sensor:") for k in data) >= 30
+    # CIE daylight basis S0, S1, S2 over CIE_S_lambda (Spectra::D, util/spectrum.cpp:632-690, 2537-2570)
+    for name in ("CIE_S_lambda", "CIE_S0", "CIE_S1", "CIE_S2"):
+        data[name] = numbers(array_body(spec, name))
+        assert len(data[name]) == 107, (name, len(data[name]))
+    # the 24 ColorChecker swatch reflectances PixelSensor fits XYZFromSensorRGB on
+    # (PixelSensor::swatchReflectances, film.cpp:268-...: BabelColor measurements)
+    film = (REF / "film.cpp").read_text()
+    m = re.search(r"Spectrum PixelSensor::swatchReflectances\[nSwatchReflectances\]\{", film)
+    body = film[m.end():film.index("};", m.end())]
+    sw = re.findall(r"FromInterleaved\(\s*\{([^}]*)\}", body)
+    assert len(sw) == 24, len(sw)
+    for i, b in enumerate(sw):
+        data[f"swatch:{i}"] = numbers(b)
     OUT.parent.mkdir(parents=True, exist_ok=True)
     OUT.write_text(json.dumps(data))
     print("wrote", OUT, {k: len(v) if isinstance(v, list) else v for k, v in data.items()})

@@ -208,6 +208,10 @@ typedef struct pbrt_scene_flat {
      * given) and the sensor's XYZFromSensorRGB (row major); sensor_xyz holds its r/g/b curves */
     float max_component_value;
     float xyz_from_sensor_rgb[9];
+    /* bump / normal mapping (materials.h:86-160) per material [n][2]: the displacement
+     * texture's root node and the normal map image (indices into the tex_node / image tables,
+     * -1 none) */
+    const int32_t *material_bump;
 } pbrt_scene_flat;
 
 typedef struct pbrt_render_params {

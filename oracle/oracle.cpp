@@ -606,6 +606,10 @@ static void Point3fi(Vec v, Vec e, Vec *p, Vec *err) {
 struct Interaction {
     Vec p, err, n, ns, dpdu, dpdus, wo;
     Vec dpdv;        // geometric dpdv and uv: texture lookups (surfscatter.cpp:74-135)
+    // shading dpdv and normal derivatives (bump mapping); a triangle without vertex normals or
+    // a disk keeps the geometric dpdv and zero derivatives (hasShadingDiff false)
+    Vec dpdvs, dndus, dndvs;
+    bool hasShadingDiff = false;
     Float uv[2] = {0, 0};
     int prim = -1;
 };
@@ -658,6 +662,21 @@ static Interaction TriangleInteraction(Vec p0, Vec p1, Vec p2, bool flip, TriIse
             ts = ts / 1e8f;
         }
         si.dpdus = ss;
+        // shading bitangent and dndu, dndv from the vertex normals (shapes.h:961-1006)
+        si.dpdvs = ts;
+        si.hasShadingDiff = true;
+        const Vec dn1 = a.n[0] - a.n[2], dn2 = a.n[1] - a.n[2];
+        const Float det = DifferenceOfProducts(duv02[0], duv12[1], duv02[1], duv12[0]);
+        if (std::abs(det) < 1e-9f) {
+            const Vec dn = Cross(a.n[2] - a.n[0], a.n[1] - a.n[0]);
+            if (LengthSquared(dn) != 0) CoordinateSystem(dn, &si.dndus, &si.dndvs);
+        } else {
+            const Float invDet = 1 / det;
+            for (int k = 0; k < 3; ++k) {
+                si.dndus[k] = DifferenceOfProducts(duv12[1], dn1[k], duv02[1], dn2[k]) * invDet;
+                si.dndvs[k] = DifferenceOfProducts(duv02[0], dn2[k], duv12[0], dn1[k]) * invDet;
+            }
+        }
     }
     si.wo = Normalize(-rayD);
     return si;
@@ -3773,7 +3792,7 @@ struct OTextures {
         fullRes[0] = xres;
         fullRes[1] = yres;
         n = flat->n_tex_nodes;
-        if (!n) return;
+        if (!n && !flat->n_images) return;  // normal maps are images without a texture node
         sppScale = std::max<Float>(.125f, 1 / std::sqrt((Float)spp));
         images.resize(flat->n_images);
         for (int i = 0; i < flat->n_images; ++i) {
@@ -3903,6 +3922,56 @@ struct OTextures {
         c.dvdx = v[2];
         c.dvdy = v[3];
         return c;
+    }
+
+    // NormalMap / BumpMap (materials.h:86-140) and the caller's ns = FaceForward(Normalize(
+    // Cross(dpdu, dpdv)), n) (surfscatter.cpp:109-127) on the oracle's own texture evaluation
+    void Bump(int dispNode, int normalImage, Interaction *si) const {
+        const OTexCtx c = Ctx(*si);
+        const Vec sdpdv = si->hasShadingDiff ? si->dpdvs : si->dpdv;
+        const Vec sdndu = si->hasShadingDiff ? si->dndus : Vec(0, 0, 0);
+        const Vec sdndv = si->hasShadingDiff ? si->dndvs : Vec(0, 0, 0);
+        Vec dpdu, dpdv;
+        if (normalImage >= 0) {
+            // Image::BilerpChannel at (u, 1 - v), repeat wrap, linear encoding
+            const OImage &im = images[normalImage];
+            const Float sx = c.u * im.w[0] - 0.5f, sy = (1 - c.v) * im.h[0] - 0.5f;
+            const int xi = (int)std::floor(sx), yi = (int)std::floor(sy);
+            const Float dx = sx - xi, dy = sy - yi;
+            Vec ns;
+            for (int ch = 0; ch < 3; ++ch) {
+                const Float v = ((1 - dx) * (1 - dy) * im.Get(0, xi, yi, ch) + dx * (1 - dy) * im.Get(0, xi + 1, yi, ch) +
+                                 (1 - dx) * dy * im.Get(0, xi, yi + 1, ch) + dx * dy * im.Get(0, xi + 1, yi + 1, ch));
+                ns[ch] = 2 * v - 1;
+            }
+            ns = Normalize(ns);
+            const Vec fx = Normalize(si->dpdus), fz = si->ns, fy = Cross(fz, fx);
+            ns = fx * ns.x + fy * ns.y + fz * ns.z;
+            const Float ulen = Length(si->dpdus), vlen = Length(sdpdv);
+            dpdu = Normalize(si->dpdus - Dot(si->dpdus, ns) * ns) * ulen;
+            dpdv = Normalize(Cross(ns, dpdu)) * vlen;
+        } else {
+            OTexCtx sc = c;
+            Float du = .5f * (std::abs(c.dudx) + std::abs(c.dudy));
+            if (du == 0) du = .0005f;
+            sc.p = c.p + du * si->dpdus;
+            sc.u = c.u + du;
+            sc.v = c.v + 0.f;
+            const Float uDisplace = EvalF(dispNode, sc);
+            Float dv = .5f * (std::abs(c.dvdx) + std::abs(c.dvdy));
+            if (dv == 0) dv = .0005f;
+            sc.p = c.p + dv * sdpdv;
+            sc.u = c.u + 0.f;
+            sc.v = c.v + dv;
+            const Float vDisplace = EvalF(dispNode, sc);
+            const Float displace = EvalF(dispNode, c);
+            dpdu = si->dpdus + (uDisplace - displace) / du * si->ns + displace * sdndu;
+            dpdv = sdpdv + (vDisplace - displace) / dv * si->ns + displace * sdndv;
+        }
+        Vec ns = Normalize(Cross(dpdu, dpdv));
+        if (DotN(ns, si->n) < 0) ns = -ns;  // FaceForward(ns, n)
+        si->ns = ns;
+        si->dpdus = dpdu;
     }
 
     // TextureMapping2D::Map (textures.h:86-202); the wavefront's dpdx = dpdy = 0
@@ -4533,6 +4602,10 @@ struct Renderer {
             }
             const float *mc = f->material_coeffs + 4 * mat;
             BxDF bx;
+            // bump / normal mapping (surfscatter.cpp:109-127, materials.h:86-140): the shading
+            // normal and dpdu the BSDF, the light sample and the next vertex's MIS context use
+            if (f->material_bump && (f->material_bump[2 * mat] >= 0 || f->material_bump[2 * mat + 1] >= 0))
+                tex.Bump(f->material_bump[2 * mat], f->material_bump[2 * mat + 1], &si);
             bx.type = f->material_type[mat];
             const bool layered = bx.type == 4 || bx.type == 5;
             LayeredBxDF lay;

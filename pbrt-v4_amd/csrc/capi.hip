@@ -110,6 +110,7 @@ struct TexTables {
     std::vector<int32_t> matTex;      // [nMaterials][4] program indices + remap
     std::vector<int32_t> matTexNode;  // [nMaterials][4] the programs' root nodes + remap (oracle)
     std::vector<int32_t> matMixNode;  // [nMaterials][4] mix: material 0, 1, amount root node, 0
+    std::vector<int32_t> matBumpNode; // [nMaterials][2] displacement root node, normal map image
     std::vector<int32_t> nodeInfo, imageInfo, levelInfo, rawInfo;
     std::vector<float> nodeParams, specFlat, rawGamma;
     std::vector<uint8_t> rawData;
@@ -190,6 +191,7 @@ static void BuildTexTables(const SceneDesc &s, TexTables *t) {
         t->matTexNode.insert(t->matTexNode.end(),
                              {root(m.texReflectance), root(m.texURough), root(m.texVRough), m.remapRoughness ? 1 : 0});
         t->matMixNode.insert(t->matMixNode.end(), {m.mixMat[0], m.mixMat[1], root(m.texAmount), 0});
+        t->matBumpNode.insert(t->matBumpNode.end(), {root(m.texDisp), m.normalMap});
     }
 }
 static CameraDiff MakeCameraDiff(const SceneDesc &s) {
@@ -451,6 +453,8 @@ struct pbrt_context {
     DevBuf<float4> raySort;
     DevBuf<int> rayBins;
     bool texGeneral = false;      // some textured reflectance is not a single image leaf
+    DevBuf<int> matBump;
+    DevBuf<float> texBump;        // [2][6][NR] (bump / normal-mapped materials only)
     int texTypeMask = 0;          // bit t: some material of type t is textured
     int texFullMask = 0;          // bit t: ... with an expression beyond one non-EWA image leaf
     // wavefront buffers
@@ -974,12 +978,23 @@ static void BuildDevice(pbrt_context *c) {
             std::vector<bool> alphaOnly(s.texPrograms.size(), false);
             for (const auto &a : s.alphaTex) alphaOnly[a[1]] = true;
             for (const MaterialDesc &m : s.materials)
-                for (int p : {m.texReflectance, m.texURough, m.texVRough, m.texAmount})
+                for (int p : {m.texReflectance, m.texURough, m.texVRough, m.texAmount, m.texDisp})
                     if (p >= 0) alphaOnly[p] = false;
             S.textured = std::any_of(alphaOnly.begin(), alphaOnly.end(), [](bool a) { return !a; }) ? 1 : 0;
         }
+        // bump / normal mapping (surfscatter.cpp:109-127): evaluated in k_texture
+        std::vector<int> mb;
+        S.hasBump = 0;
+        for (const MaterialDesc &m : s.materials) {
+            const bool bump = m.texDisp >= 0 || m.normalMap >= 0;
+            mb.insert(mb.end(), {m.texDisp, m.normalMap, bump ? 1 : 0, 0});
+            if (bump) S.hasBump = 1;
+        }
+        if (S.hasBump) S.textured = 1;
+        c->matBump.Upload(mb);
+        S.matBump = S.hasBump ? (const int4 *)c->matBump.p : nullptr;
         S.tex = TexView{};
-        if (!s.texPrograms.empty()) {
+        if (!s.texPrograms.empty() || S.hasBump) {
             if (S.textured && c->volumetric)
                 throw Error("textures or mix materials together with the volumetric path (media, interface, layered, "
                             "thin dielectric, diffuse transmission or dispersive materials) are not supported yet");
@@ -1022,7 +1037,9 @@ static void BuildDevice(pbrt_context *c) {
             };
             for (const MaterialDesc &m : s.materials) {
                 if (m.texReflectance >= 0 && !tt.progs[m.texReflectance].simple) c->texGeneral = true;
-                if (m.texReflectance >= 0 || m.texURough >= 0) c->texTypeMask |= 1 << m.type;
+                if (m.texReflectance >= 0 || m.texURough >= 0 || m.texDisp >= 0 || m.normalMap >= 0)
+                    c->texTypeMask |= 1 << m.type;
+                if (m.texDisp >= 0 && !leanProg(m.texDisp, false)) c->texFullMask |= 1 << m.type;
                 if (!leanProg(m.texReflectance, true) || !leanProg(m.texURough, false) || !leanProg(m.texVRough, false))
                     c->texFullMask |= 1 << m.type;
             }
@@ -1230,9 +1247,9 @@ constexpr int kPathFloats = 101, kPathInts = 16;
 // depth, medium) = 8, hitPrim, 5 queues, shadow pixel + medium + flags = 17 ints
 constexpr int kVolFloats = 330, kVolInts = 17;
 static int64_t PathStateBytesPerPath(bool volumetric, bool dispersive, bool textured = false, bool texGeneral = false,
-                                     bool mix = false) {
+                                     bool mix = false, bool bump = false) {
     return 4 * (kPathFloats + kPathInts) + (volumetric ? 4 * (kVolFloats + kVolInts) : 0) + (dispersive ? 16 : 0) +
-           (textured ? 24 : 0) + (texGeneral ? 124 : 0) + (mix ? 8 : 0);
+           (textured ? 24 : 0) + (texGeneral ? 124 : 0) + (mix ? 8 : 0) + (bump ? 48 : 0);
 }
 
 static void AllocPaths(pbrt_context *c, int64_t N) {
@@ -1251,6 +1268,7 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
     }
     if (c->S.textured) {
         c->texCoef.Alloc((size_t)6 * NR);
+        if (c->S.hasBump) c->texBump.Alloc((size_t)12 * NR);
         if (c->texGeneral) c->texR.Alloc((size_t)kNSpectrumSamples * NR);
     }
     if (c->hasMix) c->hitMat.Alloc((size_t)2 * NR);
@@ -1301,6 +1319,8 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
     st.emitQ = takei(1);
     st.counters = ip;
     st.texCoef = c->texCoef.p;
+    st.texBump[0] = c->S.hasBump ? c->texBump.p : nullptr;
+    st.texBump[1] = c->S.hasBump ? c->texBump.p + (size_t)6 * NR : nullptr;
     st.texR = c->texR.p;
     st.hitMat[0] = c->hasMix ? c->hitMat.p : nullptr;
     st.hitMat[1] = c->hasMix ? c->hitMat.p + NR : nullptr;
@@ -1708,6 +1728,7 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
         f->image_raw_data = t.rawData.data();
         f->material_tex = t.matTexNode.data();
         f->material_mix = t.matMixNode.data();
+        f->material_bump = t.matBumpNode.data();
         for (int k = 0; k < 12; ++k) f->camera_from_render[k] = s.cameraFromRender[k];
         for (int k = 0; k < 3; ++k) {
             f->camera_min_diff[k] = s.minPosDx[k];
@@ -1801,7 +1822,8 @@ int pbrt_context_create(const pbrt_scene *scene, int device, int64_t maxPaths, p
             // smaller cards): path-state bytes per path from AllocPaths' layout
             size_t freeB = 0, totalB = 0;
             HIPCHECK(hipMemGetInfo(&freeB, &totalB));
-            const int64_t perPath = PathStateBytesPerPath(c->volumetric, c->S.dispersive, c->S.textured, c->texGeneral, c->hasMix) +
+            const int64_t perPath = PathStateBytesPerPath(c->volumetric, c->S.dispersive, c->S.textured, c->texGeneral, c->hasMix,
+                                                       c->S.hasBump) +
                                     (c->rayBinning ? 32 : 0);
             const int64_t fit = (int64_t)(freeB / 4 * 3) / perPath - kShards * 320;
             if (fit < 4096) throw Error("not enough free device memory for path state");

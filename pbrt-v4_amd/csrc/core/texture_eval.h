@@ -663,4 +663,111 @@ PHD float TexPhase2(const TexView &T, const DeviceTexProgram &pg, const float *R
     return sp > 0 ? st[sp - 1] : 0.f;
 }
 
+// ---------------------------------------------------------------- bump and normal mapping
+// The shading geometry the wavefront's material stage perturbs (NormalBumpEvalContext,
+// materials.h:63-83): the hit point, geometric normal (after SetShadingGeometry's
+// FaceForward), uv and their screen-space derivatives, and the shading frame n, dpdu, dpdv,
+// dndu, dndv.
+struct BumpCtx {
+    V3 p, n;
+    float u, v, dudx, dudy, dvdx, dvdy;
+    V3 ns, dpdu, dpdv, dndu, dndv;
+};
+// SetShadingGeometry's shading dpdv (the bitangent ts) and dndu, dndv of a triangle hit
+// (Triangle::InteractionFromIntersection, shapes.h:961-1006): with vertex normals ts =
+// Cross(ns, ss) (CoordinateSystem when degenerate) rescaled with ss, and the normal
+// derivatives from the uv deltas (degenerate uv: CoordinateSystem of the normals' cross
+// product); without vertex normals the geometric dpdv and zero derivatives.
+PHD void TriangleShadingDiff(V3 p0, V3 p1, V3 p2, const TriShading *sh, const TriSurface &s, V3 *dpdvs, V3 *dndu,
+                             V3 *dndv) {
+    *dpdvs = s.dpdv;
+    *dndu = *dndv = V3(0, 0, 0);
+    if (!sh || !(sh->flags & 1)) return;
+    (void)p0, (void)p1, (void)p2;
+    V3 ss = s.dpdu;
+    V3 ts = Cross(s.ns, ss);
+    if (LengthSquared(ts) > 0) ss = Cross(ts, s.ns);
+    else CoordinateSystem(s.ns, &ss, &ts);
+    while (LengthSquared(ss) > 1e16f || LengthSquared(ts) > 1e16f) {
+        ss = ss / 1e8f;
+        ts = ts / 1e8f;
+    }
+    *dpdvs = ts;
+    float uv[3][2] = {{0, 0}, {1, 0}, {1, 1}};
+    if (sh->flags & 2)
+        for (int k = 0; k < 3; ++k) uv[k][0] = sh->uv[k][0], uv[k][1] = sh->uv[k][1];
+    const float duv02x = uv[0][0] - uv[2][0], duv02y = uv[0][1] - uv[2][1];
+    const float duv12x = uv[1][0] - uv[2][0], duv12y = uv[1][1] - uv[2][1];
+    const V3 dn1 = sh->n0 - sh->n2, dn2 = sh->n1 - sh->n2;
+    const float determinant = DifferenceOfProducts(duv02x, duv12y, duv02y, duv12x);
+    if (std::fabs(determinant) < 1e-9f) {
+        const V3 dn = Cross(sh->n2 - sh->n0, sh->n1 - sh->n0);
+        if (LengthSquared(dn) == 0) return;
+        CoordinateSystem(dn, dndu, dndv);
+    } else {
+        const float invDet = 1 / determinant;
+        *dndu = V3(DifferenceOfProducts(duv12y, dn1.x, duv02y, dn2.x), DifferenceOfProducts(duv12y, dn1.y, duv02y, dn2.y),
+                   DifferenceOfProducts(duv12y, dn1.z, duv02y, dn2.z)) *
+                invDet;
+        *dndv = V3(DifferenceOfProducts(duv02x, dn2.x, duv12x, dn1.x), DifferenceOfProducts(duv02x, dn2.y, duv12x, dn1.y),
+                   DifferenceOfProducts(duv02x, dn2.z, duv12x, dn1.z)) *
+                invDet;
+    }
+}
+// BumpMap (materials.h:109-140): the displacement at the hit and at the hit shifted by du along
+// dpdu and by dv along dpdv (half the summed screen-space uv derivatives, .0005 when zero); tex
+// evaluates the displacement texture at a TextureEvalContext.
+template <typename FloatTex>
+PHD void BumpMapEval(const BumpCtx &c, const FloatTex &tex, V3 *dpdu, V3 *dpdv) {
+    TexEvalCtx sc;
+    sc.p = c.p;
+    sc.n = c.n;
+    sc.u = c.u;
+    sc.v = c.v;
+    sc.dudx = c.dudx;
+    sc.dudy = c.dudy;
+    sc.dvdx = c.dvdx;
+    sc.dvdy = c.dvdy;
+    const TexEvalCtx c0 = sc;
+    float du = .5f * (std::fabs(c.dudx) + std::fabs(c.dudy));
+    if (du == 0) du = .0005f;
+    sc.p = c.p + du * c.dpdu;
+    sc.u = c.u + du;
+    sc.v = c.v + 0.f;
+    const float uDisplace = tex(sc);
+    float dv = .5f * (std::fabs(c.dvdx) + std::fabs(c.dvdy));
+    if (dv == 0) dv = .0005f;
+    sc.p = c.p + dv * c.dpdv;
+    sc.u = c.u + 0.f;
+    sc.v = c.v + dv;
+    const float vDisplace = tex(sc);
+    const float displace = tex(c0);
+    *dpdu = c.dpdu + (uDisplace - displace) / du * c.ns + displace * c.dndu;
+    *dpdv = c.dpdv + (vDisplace - displace) / dv * c.ns + displace * c.dndv;
+}
+// NormalMap (materials.h:86-106): the tangent-space normal 2 rgb - 1 bilinearly interpolated
+// from level 0 of the (repeat-wrapped, linear) image at (u, 1 - v), taken to render space by the
+// frame of the shading dpdu and normal; dpdu, dpdv keep their lengths.
+PHD void NormalMapEval(const BumpCtx &c, const TexView &T, const DeviceImage &im, V3 *dpdu, V3 *dpdv) {
+    const float s = c.u, t = 1 - c.v;
+    V3 ns(2 * BilerpChannel(T, im, 0, s, t, 0) - 1, 2 * BilerpChannel(T, im, 0, s, t, 1) - 1,
+          2 * BilerpChannel(T, im, 0, s, t, 2) - 1);
+    ns = Normalize(ns);
+    const Frame frame = Frame::FromXZ(Normalize(c.dpdu), c.ns);
+    ns = frame.FromLocal(ns);
+    const float ulen = Length(c.dpdu), vlen = Length(c.dpdv);
+    *dpdu = Normalize(GramSchmidt(c.dpdu, ns)) * ulen;
+    *dpdv = Normalize(Cross(ns, *dpdu)) * vlen;
+}
+// surfscatter.cpp:109-127: the perturbed shading normal and dpdu the BSDF and the light sample
+// use (a normal map takes precedence over a displacement)
+template <typename FloatTex>
+PHD void BumpShading(const BumpCtx &c, const TexView &T, int normalMapImage, const FloatTex &disp, V3 *ns, V3 *dpdus) {
+    V3 dpdu, dpdv;
+    if (normalMapImage >= 0) NormalMapEval(c, T, T.images[normalMapImage], &dpdu, &dpdv);
+    else BumpMapEval(c, disp, &dpdu, &dpdv);
+    *ns = FaceForwardN(Normalize(Cross(dpdu, dpdv)), c.n);
+    *dpdus = dpdu;
+}
+
 }  // namespace pbrt_amd

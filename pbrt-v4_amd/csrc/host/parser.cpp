@@ -388,6 +388,9 @@ class Parser {
         bool remap = true;
         bool hasAmount = false;  // mix: "amount" (default 0.5)
         Param amount;
+        bool hasDisp = false;   // "displacement" (a float texture or constant)
+        Param disp;
+        std::string normalMap;  // "normalmap" image file
     };
     std::vector<MatTexPending> matTexPending;
     void ResolveTextures();
@@ -556,14 +559,14 @@ class Parser {
             std::string type = Str(toks, pos);
             ParamSet ps = Params(toks, pos);
             ps.loc = loc;
-            gs.material = MakeMaterial(type, ps, "");
+            gs.material = MakeMaterial(type, ps, "", dir);
         } else if (d == "MakeNamedMaterial") {
             std::string name = Str(toks, pos);
             ParamSet ps = Params(toks, pos);
             ps.loc = loc;
             std::string type = ps.GetString("type", "");
             if (type.empty()) throw Error(loc + ": MakeNamedMaterial needs \"string type\"");
-            namedMaterials[name] = MakeMaterial(type, ps, name);
+            namedMaterials[name] = MakeMaterial(type, ps, name, dir);
         } else if (d == "NamedMaterial") {
             std::string name = Str(toks, pos);
             if (!namedMaterials.count(name)) throw Error(loc + ": named material \"" + name + "\" undefined");
@@ -646,9 +649,25 @@ class Parser {
         }
     }
 
-    int MakeMaterial(const std::string &type, ParamSet &ps, const std::string &name) {
+    int MakeMaterial(const std::string &type, ParamSet &ps, const std::string &name, const std::string &dir) {
         MaterialDesc m;
         m.name = name;
+        // shading-normal perturbation (materials.cpp: GetFloatTextureOrNull("displacement"),
+        // scene.cpp normal map cache: Image::Read(normalmap, ColorEncoding::Linear)), for the
+        // diffuse, dielectric and conductor materials of the surface wavefront
+        if (type == "diffuse" || type == "dielectric" || type == "conductor") {
+            if (Param *d = ps.Find("displacement")) {
+                MatTexPending &mp = PendingTex(ps.loc);
+                mp.hasDisp = true;
+                mp.disp = *d;
+            }
+            std::string nm = ps.GetString("normalmap", "");
+            if (!nm.empty()) {
+                if (nm[0] != '/' && !dir.empty()) nm = dir + "/" + nm;
+                MatTexPending &mp = PendingTex(ps.loc);
+                mp.normalMap = nm;
+            }
+        }
         if (type == "diffuse") {
             m.type = kMatDiffuse;
             Param *r = ps.Find("reflectance");
@@ -1653,6 +1672,14 @@ void Parser::Finish() {
             // emitter by HashFloat(p); not on this path yet
             if (AlphaId(s) >= 0) throw Error(s.loc + ": \"alpha\" on area lights is not supported yet");
         }
+        {
+            // bump / normal mapping needs the shading normal's derivatives dndu, dndv, which only
+            // triangles (vertex normals) and disks (zero) provide here
+            const MaterialDesc &md = scene.materials[mat];
+            if ((md.texDisp >= 0 || md.normalMap >= 0) &&
+                (s.kind == kShapeSphereT || s.kind == kShapeCylinderT || !s.quadIdx.empty()))
+                throw Error(s.loc + ": bump and normal mapping on spheres, cylinders and bilinear patches are not supported yet");
+        }
         if (s.kind == kShapeSphereT || s.kind == kShapeDiskT || s.kind == kShapeCylinderT) {
             AnalyticShape(s, rfo, mat, lightSpectrum, lightScale, twoSided, power, mediumOf);
             continue;
@@ -2225,6 +2252,26 @@ void Parser::ResolveTextures() {
         }
         if (m.type != kMatDiffuse && m.type != kMatDielectric && m.type != kMatConductor)
             throw Error(mp.loc + ": textures are supported on diffuse, dielectric and conductor materials only");
+        if (mp.hasDisp) {
+            m.dispNode = FloatParamNode(&mp.disp, 0.f, mp.loc);
+            m.texDisp = CompileTexProgram(scene, m.dispNode, false);
+        }
+        if (!mp.normalMap.empty()) {
+            // one image per file; pbrt reads it linearly encoded and looks it up with a repeat
+            // wrap (NormalMap, materials.h:86-106)
+            int img = -1;
+            const std::string key = mp.normalMap + "|normalmap";
+            for (size_t i = 0; i < scene.images.size(); ++i)
+                if (scene.images[i].filename == key) img = (int)i;
+            if (img < 0) {
+                ImageDesc id = LoadImageTexture(mp.normalMap, "linear", kWrapRepeat, mp.loc);
+                if (id.nc < 3) throw Error(mp.loc + ": " + mp.normalMap + ": normal map image must contain R, G, and B channels");
+                id.filename = key;
+                scene.images.push_back(std::move(id));
+                img = (int)scene.images.size() - 1;
+            }
+            m.normalMap = img;
+        }
         if (mp.hasRefl) {
             const int node = SpectrumParamNode(&mp.refl, kSpecAlbedo, 0.5f, mp.loc);
             m.texReflectance = CompileTexProgram(scene, node, true);

@@ -88,6 +88,9 @@ struct MaterialDesc {
     // mix: the two materials and the "amount" texture program (constant or image)
     int mixMat[2] = {-1, -1};
     int texAmount = -1;
+    // bump / normal mapping (materials.h:86-160): the displacement's program and node, the
+    // normal map's image (SceneDesc::images); -1 when absent
+    int texDisp = -1, dispNode = -1, normalMap = -1;
     std::string name;
 };
 

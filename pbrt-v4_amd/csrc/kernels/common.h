@@ -1228,6 +1228,16 @@ __device__ inline float Reflectance(float4 mc, bool constant, float lambda) {
 __device__ inline int HitMaterial(const DeviceScene &S, const PathState &st, int depth, int ri, int prim) {
     return st.hitMat[0] ? st.hitMat[depth & 1][ri] : S.primMaterial[prim];
 }
+// A bump / normal-mapped material's shading normal and dpdu, as k_texture left them for record
+// ri of `depth` (surfscatter.cpp:109-127); other materials keep the surface's
+__device__ inline void BumpedShading(const DeviceScene &S, const PathState &st, int depth, int mat, int ri,
+                                    TriSurface *surf) {
+    if (!S.matBump[mat].z) return;
+    const int N = st.NR;
+    const float *tb = st.texBump[depth & 1];
+    surf->ns = V3(tb[ri], tb[N + ri], tb[2 * N + ri]);
+    surf->dpdus = V3(tb[3 * N + ri], tb[4 * N + ri], tb[5 * N + ri]);
+}
 
 // ---- textures (core/texture_eval.h)
 // TextureEvalContext of a hit as the wavefront material stage builds it: p, n, uv and the

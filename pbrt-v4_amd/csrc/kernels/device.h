@@ -122,6 +122,10 @@ struct DeviceScene {
     // program or -1; nAlpha = 0 (and primAlpha null) when no shape has an alpha texture
     const int *primAlpha;
     int nAlpha;
+    // bump / normal mapping per material: {displacement program, normal map image, flag, 0};
+    // hasBump = 0 (matBump null) when no material perturbs its shading normal
+    const int4 *matBump;
+    int hasBump;
     const int *primOrig;  // leaf order -> the scene's triangle index (boundary results)
     // per-triangle shading attributes (leaf order, 4 float4 each: n0|flags, n1|u0, n2|v0,
     // u1 v1 u2 v2), nullptr when no mesh has vertex normals or uv
@@ -283,6 +287,8 @@ struct PathState {
     // reflectance as sigmoid coefficients c0 c1 c2 + a flag (1: the per-wavelength values are
     // in texR), then the TrowbridgeReitz alphas of a textured roughness; null when untextured
     float *texCoef;     // [6][NR]
+    float *texBump[2];  // by depth parity, [6][NR]: the bump / normal-mapped shading normal and
+                        // dpdu of a record (null without such materials)
     float *texR;        // [31][NR] general reflectance expressions (null when none)
     // scenes with mix materials: each hit's resolved material, by depth parity (null otherwise)
     int *hitMat[2];

@@ -496,6 +496,8 @@ __global__ void __launch_bounds__(kBlock) k_emissive(DeviceScene S, PathState st
             PrimVerts(S, pp, &q0, &q1, &q2);
             // prevIntrCtx = LightSampleContext(pi, n, ns) of the previous surface
             TriSurface prev = SurfaceAt<Ext>(S, pp, q0, q1, q2, pb0, pb1, pb2);
+            // prevIntrCtx holds the previous vertex's bump-mapped shading normal
+            if (S.hasBump) BumpedShading(S, st, depth - 1, HitMaterial(S, st, depth - 1, pi, pp), pi, &prev);
             float lightChoicePDF = LightPMF(S, prev.p, prev.ns, light);
             float lightPDF;
             if (Ext && prim >= S.nTris) {
@@ -749,6 +751,9 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
             const int mat = Lean ? S.primMaterial[prim] : HitMaterial(S, st, depth, ri, prim);
             TriSurface surf = Lean ? TriangleSurface(p0, p1, p2, b0, b1, b2, S.primFlip[prim], nullptr)
                                    : SurfaceAt<Ext>(S, prim, p0, p1, p2, b0, b1, b2);
+            if constexpr (Tex) {
+                if (S.hasBump) BumpedShading(S, st, depth, mat, ri, &surf);
+            }
             float4 mc = matsL[mat];
             int mflags = matConstL[mat];  // bit 0: constant R, bit 1: R != 0 at every wavelength
             bool constant = mflags & 1;
@@ -1029,7 +1034,10 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
             V3 p0, p1, p2;
             PrimVerts(S, prim, &p0, &p1, &p2);
             const int mat = HitMaterial(S, st, depth, ri, prim);
-            const TriSurface surf = SurfaceAt<Ext>(S, prim, p0, p1, p2, b0, b1, b2);
+            TriSurface surf = SurfaceAt<Ext>(S, prim, p0, p1, p2, b0, b1, b2);
+            if constexpr (Tex) {
+                if (S.hasBump) BumpedShading(S, st, depth, mat, ri, &surf);
+            }
             const V3 wo = Normalize(-rd);
             const V3 n = surf.n, ns = surf.ns;
             const RaySamples rs = GenerateRaySamples<MT == kMatDielectricT>(S, T, st, slot, sidx, d0);
@@ -1298,11 +1306,44 @@ __global__ void __launch_bounds__(kBlock) k_texture(DeviceScene S, PathState st,
         const int prim = hitPrim[ri];
         const int mat = HitMaterial(S, st, depth, ri, prim);
         const int4 mt = S.matTex[mat];
-        if (mt.x < 0 && mt.y < 0) continue;
+        const int4 mb = S.hasBump ? S.matBump[mat] : make_int4(-1, -1, 0, 0);
+        if (mt.x < 0 && mt.y < 0 && !mb.z) continue;
         V3 p0, p1, p2;
         PrimVerts(S, prim, &p0, &p1, &p2);
         const TriSurface surf = SurfaceAt<Ext>(S, prim, p0, p1, p2, hitB[ri], hitB[N + ri], hitB[2 * N + ri]);
         const TexEvalCtx tc = HitTexCtx(S, surf);
+        if (mb.z) {
+            // bump / normal mapping (surfscatter.cpp:109-127): the perturbed shading normal and
+            // dpdu, per record, for the shade kernel and the next depth's emission MIS
+            BumpCtx bc;
+            bc.p = surf.p;
+            bc.n = surf.n;
+            bc.u = tc.u;
+            bc.v = tc.v;
+            bc.dudx = tc.dudx;
+            bc.dudy = tc.dudy;
+            bc.dvdx = tc.dvdx;
+            bc.dvdy = tc.dvdy;
+            bc.ns = surf.ns;
+            bc.dpdu = surf.dpdus;
+            if (prim < S.nTris) {
+                TriShading sh;
+                const bool has = LoadTriShading(S, prim, &sh);
+                TriangleShadingDiff(p0, p1, p2, has ? &sh : nullptr, surf, &bc.dpdv, &bc.dndu, &bc.dndv);
+            } else {  // a disk: shading = geometric frame, no normal derivatives
+                bc.dpdv = surf.dpdv;
+                bc.dndu = bc.dndv = V3(0, 0, 0);
+            }
+            V3 ns, dpdus;
+            BumpShading(bc, S.tex, mb.y, [&](const TexEvalCtx &c) { return TexFloatFast<Full>(S, mb.x, c); }, &ns, &dpdus);
+            float *tb = st.texBump[depth & 1];
+            tb[ri] = ns.x;
+            tb[(size_t)N + ri] = ns.y;
+            tb[2 * (size_t)N + ri] = ns.z;
+            tb[3 * (size_t)N + ri] = dpdus.x;
+            tb[4 * (size_t)N + ri] = dpdus.y;
+            tb[5 * (size_t)N + ri] = dpdus.z;
+        }
         if (mt.x >= 0) {
             const DeviceTexProgram pg = S.tex.progs[mt.x];
             if (!Full || pg.simple) {

@@ -100,6 +100,7 @@ class SceneFlat(ctypes.Structure):
         ("prim_alpha", ctypes.POINTER(ctypes.c_int32)),
         ("max_component_value", ctypes.c_float),
         ("xyz_from_sensor_rgb", ctypes.c_float * 9),
+        ("material_bump", ctypes.POINTER(ctypes.c_int32)),
     ]
 
 

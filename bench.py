@@ -137,7 +137,8 @@ def job_spec(args, world, scaling):
     return {"metric": metric, "spp": spp, "sharding": sharding, "scaling": scaling if world > 1 else "weak"}
 
 
-def roofline_entry(achieved, mean_launch_s, launches, rays_per_launch, bytes_per_ray, traffic, workload):
+def roofline_entry(achieved, mean_launch_s, launches, rays_per_launch, bytes_per_ray, traffic, workload,
+                   bvh_bytes=0):
     """The 'roofline' object.  bound = the roofline that applies (HBM: nothing on this path
     is a dense contraction, so MFMA has no ceiling to offer); 'limiter' says whether the
     measured fraction is bandwidth-limited or what else limits the kernel."""
@@ -154,7 +155,9 @@ def roofline_entry(achieved, mean_launch_s, launches, rays_per_launch, bytes_per
             "kernel": ("k_vclosest (BVH8 traverse + hit record + push to medium / surface queue)"
                        if workload == "c5" else
                        "k_closest (BVH8 traverse + hit record + wave64 ballot push to material queue)"),
-            "bytes_per_ray": round(bytes_per_ray, 2), "rays_per_launch": round(rays_per_launch, 1),
+            "bytes_per_ray": round(bytes_per_ray, 2), "bvh_bytes_per_launch": bvh_bytes,
+            "algorithmic_bytes_per_launch": round(bytes_per_ray * rays_per_launch + bvh_bytes),
+            "rays_per_launch": round(rays_per_launch, 1),
             "timed_launches": launches, "mean_launch_us": round(mean_launch_s * 1e6, 3), "limiter": limiter}
 
 
@@ -335,7 +338,10 @@ def main():
         # per-depth queue counts of the last pass (= the timed pass when a render is one pass)
         qb, qr = closest_bytes(integ.queue_counts(), info.max_depth)
         bpr = qb / qr if qr else BYTES_PER_RAY_CLOSEST
-    bytes_per_launch = bpr * st.timed_closest_rays / launches
+    # ray I/O per ray plus the HBM-resident BVH touched once per launch (nodes
+    # beyond the LDS-cached top, triangles unless LDS-cached; 0 on C2, whose tree is in LDS)
+    bvh_bytes = int(st.bvh_hbm_node_bytes + st.bvh_hbm_tri_bytes)
+    bytes_per_launch = bpr * st.timed_closest_rays / launches + bvh_bytes
     achieved = bytes_per_launch / mean_launch_s / 1e9 if mean_launch_s > 0 else 0.0
     traffic = pmc_traffic(args.workload)
 
@@ -378,8 +384,8 @@ def main():
                        "triangles": info.n_triangles, "paths_per_pass": int(st.paths_per_pass),
                        "sharding": job["sharding"]},
             "roofline": dict(roofline_entry(achieved, mean_launch_s, launches, st.timed_closest_rays / launches,
-                                            bpr, traffic, args.workload),
-                             effective=(effective_traversal(bytes_per_launch / bpr / mean_launch_s)
+                                            bpr, traffic, args.workload, bvh_bytes),
+                             effective=(effective_traversal(st.timed_closest_rays / launches / mean_launch_s)
                                         if args.workload == "c2" and mean_launch_s > 0 else None)),
             "cpu_baseline": cpu,
             "rays": {"camera": int(st.camera_rays), "closest": int(st.closest_rays), "shadow": int(st.shadow_rays)},

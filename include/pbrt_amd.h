@@ -229,6 +229,10 @@ typedef struct pbrt_render_stats {
     uint64_t timed_closest_rays; /* rays those launches processed */
     int passes;
     uint64_t paths_per_pass;
+    /* the BVH the closest-hit traversal reads from HBM (SURVEY 8(d)'s "touched once per
+     * launch" term): node bytes in the format traversed, less the top nodes cached in LDS,
+     * and triangle bytes (0 when every triangle is cached in LDS) */
+    uint64_t bvh_hbm_node_bytes, bvh_hbm_tri_bytes;
 } pbrt_render_stats;
 
 /* Per-stage kernel profile (GetProfilerEvents / ReportKernelStats, gpu/util.cpp:128-246): with

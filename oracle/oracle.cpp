@@ -4308,11 +4308,183 @@ struct Renderer {
     }
 
     // one pixel sample -> sensor RGB and filter weight (film.h:95-100)
-    void Li(int px, int py, int sampleIndex, float rgb[3], float *weight) const {
-        AnySampler hs{HaltonState{&S.halton, 0, 0}, ZSobolState{&S.zsobol}, S.useZSobol};
-        hs.Start(px, py, sampleIndex, 0);
+    // MixMaterial resolution of a hit's material (see the loop's comment)
+    int ResolveMix(int mat, const Interaction &si) const {
+        // MixMaterial::ChooseMaterial at the closest hit (wavefront/intersect.h:90-97,
+        // materials.h:285-294): amount texture without (u,v) derivatives, HashFloat(p, wo,
+        // m0, m1) with the material indices standing in for pbrt's material pointers
+        while (f->material_mix && f->material_type[mat] == 8) {
+            const int32_t *mm = f->material_mix + 4 * mat;
+            OTexCtx c0;
+            c0.p = si.p;
+            c0.n = si.n;
+            c0.u = si.uv[0];
+            c0.v = si.uv[1];
+            const Float amt = tex.EvalF(mm[2], c0);
+            if (amt <= 0) mat = mm[0];
+            else if (amt >= 1) mat = mm[1];
+            else {
+                unsigned char buf[40];
+                const Float pv[6] = {si.p.x, si.p.y, si.p.z, si.wo.x, si.wo.y, si.wo.z};
+                const uint64_t m0 = (uint32_t)mm[0], m1 = (uint32_t)mm[1];
+                std::memcpy(buf, pv, 24);
+                std::memcpy(buf + 24, &m0, 8);
+                std::memcpy(buf + 32, &m1, 8);
+                const Float u = (Float)(uint32_t)Murmur64A(buf, 40, 0) * 0x1p-32f;
+                mat = (amt < u) ? mm[0] : mm[1];
+            }
+        }
+        return mat;
+    }
+    // Material::GetBxDF (materials.h:466-471 diffuse, :182-204 dielectric, :491-511 conductor,
+    // materials.cpp:301-329 / 391-437 coated) with bump / normal mapping applied to si first;
+    // lambda's secondary wavelengths may be terminated.  Returns whether the BSDF is layered.
+    bool MakeBSDF(int mat, Wavelengths &lambda, bool anyNonSpecular, Interaction &si, BxDF &bx,
+                  LayeredBxDF &lay) const {
+        const float *mc = f->material_coeffs + 4 * mat;
+        // bump / normal mapping (surfscatter.cpp:109-127, materials.h:86-140): the shading
+        // normal and dpdu the BSDF, the light sample and the next vertex's MIS context use
+        if (f->material_bump && (f->material_bump[2 * mat] >= 0 || f->material_bump[2 * mat + 1] >= 0))
+            tex.Bump(f->material_bump[2 * mat], f->material_bump[2 * mat + 1], &si);
+        bx.type = f->material_type[mat];
+        const bool layered = bx.type == 4 || bx.type == 5;
+        if (layered) {
+            // CoatedDiffuseMaterial / CoatedConductorMaterial::GetBxDF (materials.cpp:301-329, :391-437)
+            const float *mp = f->material_params + 4 * mat, *ml = f->material_layer + 12 * mat;
+            Float ieta = mp[2] == 0 ? 1.f : mp[2];
+            if (ml[11] >= 0) {  // spectral interface eta: eta(lambda_0) and TerminateSecondary
+                const int es = (int)ml[11], a = f->pl_offsets[es];
+                Float e = PLEval(f->pl_lambda + a, f->pl_value + a, f->pl_offsets[es + 1] - a, lambda.lambda[0]);
+                ieta = e == 0 ? 1.f : e;
+                if (lambda.pdf[1] != 0) {
+                    for (int i = 1; i < NS; ++i) lambda.pdf[i] = 0;
+                    lambda.pdf[0] /= NS;
+                }
+            }
+            lay.top.type = 1;
+            lay.top.eta = ieta;
+            lay.top.mf.ax = mp[0];
+            lay.top.mf.ay = mp[1];
+            lay.bottom.type = bx.type == 4 ? 0 : 2;
+            lay.bottom.mf.ax = ml[9];
+            lay.bottom.mf.ay = ml[10];
+            const int es = f->material_spectra[2 * mat], ks = f->material_spectra[2 * mat + 1];
+            for (int i = 0; i < NS; ++i) {
+                Float l = lambda.lambda[i];
+                if (bx.type == 4) {
+                    Float r = f->material_constant[mat] ? mc[3] : Sigmoid(mc[0], mc[1], mc[2], l);
+                    lay.bottom.R[i] = Clamp(r, 0, 1);
+                } else {
+                    Float e, k;
+                    if (es >= 0) {
+                        const int a = f->pl_offsets[es], b = f->pl_offsets[ks];
+                        e = PLEval(f->pl_lambda + a, f->pl_value + a, f->pl_offsets[es + 1] - a, l);
+                        k = PLEval(f->pl_lambda + b, f->pl_value + b, f->pl_offsets[ks + 1] - b, l);
+                    } else {
+                        Float r = Clamp(Sigmoid(mc[0], mc[1], mc[2], l), 0, .9999f);
+                        e = 1;
+                        k = 2 * std::sqrt(r) / std::sqrt(std::max<Float>(0, 1 - r));
+                    }
+                    lay.bottom.etaS[i] = e / ieta;
+                    lay.bottom.kS[i] = k / ieta;
+                }
+                Float av = ml[8] != 0 ? ml[7] : Sigmoid(ml[4], ml[5], ml[6], l);
+                lay.albedo[i] = Clamp(av, 0, 1);
+            }
+            lay.thickness = std::max<Float>(ml[0], std::numeric_limits<Float>::min());
+            lay.g = Clamp(ml[1], -1, 1);
+            lay.maxDepth = (int)ml[2];
+            lay.nSamples = (int)ml[3];
+            if (f->regularize && anyNonSpecular) {
+                lay.top.mf.Regularize();
+                lay.bottom.mf.Regularize();
+            }
+        } else if (bx.type == 7) {
+            // DiffuseTransmissionMaterial::GetBxDF (materials.h): Clamp(scale * R | T, 0, 1)
+            const float *ml = f->material_layer + 12 * mat;
+            const Float scale = f->material_params[4 * mat + 3];
+            for (int i = 0; i < NS; ++i) {
+                Float l = lambda.lambda[i];
+                Float r = f->material_constant[mat] ? mc[3] : Sigmoid(mc[0], mc[1], mc[2], l);
+                Float t = ml[8] != 0 ? ml[7] : Sigmoid(ml[4], ml[5], ml[6], l);
+                bx.R[i] = Clamp(scale * r, 0, 1);
+                bx.Tt[i] = Clamp(scale * t, 0, 1);
+            }
+        } else if (bx.type == 0) {
+            // DiffuseMaterial::GetBxDF: Clamp(texEval(reflectance), 0, 1)
+            const int rt = f->material_tex ? f->material_tex[4 * mat] : -1;
+            if (rt >= 0) {
+                const Spectrum R = tex.EvalS(rt, tex.Ctx(si), lambda);
+                for (int i = 0; i < NS; ++i) bx.R[i] = Clamp(R[i], 0, 1);
+            } else {
+                for (int i = 0; i < NS; ++i) {
+                    Float r = f->material_constant[mat] ? mc[3] : Sigmoid(mc[0], mc[1], mc[2], lambda.lambda[i]);
+                    bx.R[i] = Clamp(r, 0, 1);
+                }
+            }
+        } else {
+            const float *mp = f->material_params + 4 * mat;
+            bx.mf.ax = mp[0];  // alphas arrive remapped and clamped (TrowbridgeReitz ctor)
+            bx.mf.ay = mp[1];
+            const int32_t *mt = f->material_tex ? f->material_tex + 4 * mat : nullptr;
+            OTexCtx tctx;
+            if (mt && (mt[0] >= 0 || mt[1] >= 0)) tctx = tex.Ctx(si);
+            if (mt && mt[1] >= 0) {
+                // texEval(uRoughness), texEval(vRoughness), RoughnessToAlpha if remapped,
+                // TrowbridgeReitzDistribution(urough, vrough) (materials.h:182-204, :491-511)
+                Float ur = tex.EvalF(mt[1], tctx), vr = tex.EvalF(mt[2], tctx);
+                if (mt[3]) {
+                    ur = std::sqrt(ur);
+                    vr = std::sqrt(vr);
+                }
+                bx.mf = TRDistribution(ur, vr);
+            }
+            bx.eta = mp[2] == 0 ? 1.f : mp[2];
+            if ((bx.type == 1 || bx.type == 6) && f->material_spectra[2 * mat] >= 0) {
+                // DielectricMaterial::GetBxDF (materials.cpp:25-49): a spectral eta is taken at
+                // lambda_0 and the secondary wavelengths are terminated
+                // (SampledWavelengths::TerminateSecondary: pdf = (pdf_0 / n, 0, ..., 0))
+                const int es = f->material_spectra[2 * mat], a = f->pl_offsets[es];
+                Float e = PLEval(f->pl_lambda + a, f->pl_value + a, f->pl_offsets[es + 1] - a, lambda.lambda[0]);
+                bx.eta = e == 0 ? 1.f : e;
+                if (lambda.pdf[1] != 0) {
+                    for (int i = 1; i < NS; ++i) lambda.pdf[i] = 0;
+                    lambda.pdf[0] /= NS;
+                }
+            }
+            if (bx.type == 2) {
+                int es = f->material_spectra[2 * mat], ks = f->material_spectra[2 * mat + 1];
+                for (int i = 0; i < NS; ++i) {
+                    Float l = lambda.lambda[i];
+                    if (es >= 0) {
+                        const int a = f->pl_offsets[es], b = f->pl_offsets[ks];
+                        bx.etaS[i] = PLEval(f->pl_lambda + a, f->pl_value + a, f->pl_offsets[es + 1] - a, l);
+                        bx.kS[i] = PLEval(f->pl_lambda + b, f->pl_value + b, f->pl_offsets[ks + 1] - b, l);
+                    } else {
+                        Float r = Clamp(Sigmoid(mc[0], mc[1], mc[2], l), 0, .9999f);
+                        bx.etaS[i] = 1;
+                        bx.kS[i] = 2 * std::sqrt(r) / std::sqrt(std::max<Float>(0, 1 - r));
+                    }
+                }
+                if (mt && mt[0] >= 0) {
+                    // ConductorMaterial::GetBxDF: r = Clamp(texEval(reflectance), 0, .9999)
+                    const Spectrum R = tex.EvalS(mt[0], tctx, lambda);
+                    for (int i = 0; i < NS; ++i) {
+                        Float r = Clamp(R[i], 0, .9999f);
+                        bx.etaS[i] = 1;
+                        bx.kS[i] = 2 * std::sqrt(r) / std::sqrt(std::max<Float>(0, 1 - r));
+                    }
+                }
+            }
+            if (f->regularize && anyNonSpecular && bx.type != 6) bx.mf.Regularize();  // thin: no-op
+        }
+        return layered;
+    }
+    // The camera sample and ray of EvaluatePixelSample (cpu/integrators.cpp:228-242; the wavefront's
+    // camera.cpp:31-80 draws the same dimensions): wavelengths, filter, time, lens, render-space ray
+    void CameraRay(int px, int py, AnySampler &hs, Wavelengths &lambda, float *weight, Vec &ro, Vec &rd) const {
         Float lu = hs.Get1D();
-        Wavelengths lambda = Wavelengths::SampleUniform(lu);
+        lambda = Wavelengths::SampleUniform(lu);
         Float fx, fy;
         hs.Pixel2D(&fx, &fy);
         Float ox, oy, fw;
@@ -4323,7 +4495,8 @@ struct Renderer {
         hs.Get2D(&l0, &l1);
         *weight = fw;
         Vec pCam = Xf(f->camera_from_raster, Vec(pFilmX, pFilmY, 0), true);
-        Vec ro(0, 0, 0), rd = Normalize(pCam);
+        ro = Vec(0, 0, 0);
+        rd = Normalize(pCam);
         if (f->lens_radius > 0) {
             Float lx, ly;
             SampleUniformDiskConcentric(l0, l1, &lx, &ly);
@@ -4345,6 +4518,13 @@ struct Renderer {
             ro = oo;
             rd = dd;
         }
+    }
+    void Li(int px, int py, int sampleIndex, float rgb[3], float *weight) const {
+        AnySampler hs{HaltonState{&S.halton, 0, 0}, ZSobolState{&S.zsobol}, S.useZSobol};
+        hs.Start(px, py, sampleIndex, 0);
+        Wavelengths lambda;
+        Vec ro, rd;
+        CameraRay(px, py, hs, lambda, weight, ro, rd);
         Spectrum L(0.f), beta(1.f), r_u(1.f), r_l(1.f);
         bool specularBounce = false, anyNonSpecular = false;
         Float etaScale = 1;
@@ -4575,170 +4755,10 @@ struct Renderer {
             }
             if (wf == S.maxDepth) break;
             // Material::GetBxDF (materials.h:466-471 diffuse, :182-204 dielectric, :491-511 conductor)
-            int mat = S.Material(prim);
-            // MixMaterial::ChooseMaterial at the closest hit (wavefront/intersect.h:90-97,
-            // materials.h:285-294): amount texture without (u,v) derivatives, HashFloat(p, wo,
-            // m0, m1) with the material indices standing in for pbrt's material pointers
-            while (f->material_mix && f->material_type[mat] == 8) {
-                const int32_t *mm = f->material_mix + 4 * mat;
-                OTexCtx c0;
-                c0.p = si.p;
-                c0.n = si.n;
-                c0.u = si.uv[0];
-                c0.v = si.uv[1];
-                const Float amt = tex.EvalF(mm[2], c0);
-                if (amt <= 0) mat = mm[0];
-                else if (amt >= 1) mat = mm[1];
-                else {
-                    unsigned char buf[40];
-                    const Float pv[6] = {si.p.x, si.p.y, si.p.z, si.wo.x, si.wo.y, si.wo.z};
-                    const uint64_t m0 = (uint32_t)mm[0], m1 = (uint32_t)mm[1];
-                    std::memcpy(buf, pv, 24);
-                    std::memcpy(buf + 24, &m0, 8);
-                    std::memcpy(buf + 32, &m1, 8);
-                    const Float u = (Float)(uint32_t)Murmur64A(buf, 40, 0) * 0x1p-32f;
-                    mat = (amt < u) ? mm[0] : mm[1];
-                }
-            }
-            const float *mc = f->material_coeffs + 4 * mat;
+            const int mat = ResolveMix(S.Material(prim), si);
             BxDF bx;
-            // bump / normal mapping (surfscatter.cpp:109-127, materials.h:86-140): the shading
-            // normal and dpdu the BSDF, the light sample and the next vertex's MIS context use
-            if (f->material_bump && (f->material_bump[2 * mat] >= 0 || f->material_bump[2 * mat + 1] >= 0))
-                tex.Bump(f->material_bump[2 * mat], f->material_bump[2 * mat + 1], &si);
-            bx.type = f->material_type[mat];
-            const bool layered = bx.type == 4 || bx.type == 5;
             LayeredBxDF lay;
-            if (layered) {
-                // CoatedDiffuseMaterial / CoatedConductorMaterial::GetBxDF (materials.cpp:301-329, :391-437)
-                const float *mp = f->material_params + 4 * mat, *ml = f->material_layer + 12 * mat;
-                Float ieta = mp[2] == 0 ? 1.f : mp[2];
-                if (ml[11] >= 0) {  // spectral interface eta: eta(lambda_0) and TerminateSecondary
-                    const int es = (int)ml[11], a = f->pl_offsets[es];
-                    Float e = PLEval(f->pl_lambda + a, f->pl_value + a, f->pl_offsets[es + 1] - a, lambda.lambda[0]);
-                    ieta = e == 0 ? 1.f : e;
-                    if (lambda.pdf[1] != 0) {
-                        for (int i = 1; i < NS; ++i) lambda.pdf[i] = 0;
-                        lambda.pdf[0] /= NS;
-                    }
-                }
-                lay.top.type = 1;
-                lay.top.eta = ieta;
-                lay.top.mf.ax = mp[0];
-                lay.top.mf.ay = mp[1];
-                lay.bottom.type = bx.type == 4 ? 0 : 2;
-                lay.bottom.mf.ax = ml[9];
-                lay.bottom.mf.ay = ml[10];
-                const int es = f->material_spectra[2 * mat], ks = f->material_spectra[2 * mat + 1];
-                for (int i = 0; i < NS; ++i) {
-                    Float l = lambda.lambda[i];
-                    if (bx.type == 4) {
-                        Float r = f->material_constant[mat] ? mc[3] : Sigmoid(mc[0], mc[1], mc[2], l);
-                        lay.bottom.R[i] = Clamp(r, 0, 1);
-                    } else {
-                        Float e, k;
-                        if (es >= 0) {
-                            const int a = f->pl_offsets[es], b = f->pl_offsets[ks];
-                            e = PLEval(f->pl_lambda + a, f->pl_value + a, f->pl_offsets[es + 1] - a, l);
-                            k = PLEval(f->pl_lambda + b, f->pl_value + b, f->pl_offsets[ks + 1] - b, l);
-                        } else {
-                            Float r = Clamp(Sigmoid(mc[0], mc[1], mc[2], l), 0, .9999f);
-                            e = 1;
-                            k = 2 * std::sqrt(r) / std::sqrt(std::max<Float>(0, 1 - r));
-                        }
-                        lay.bottom.etaS[i] = e / ieta;
-                        lay.bottom.kS[i] = k / ieta;
-                    }
-                    Float av = ml[8] != 0 ? ml[7] : Sigmoid(ml[4], ml[5], ml[6], l);
-                    lay.albedo[i] = Clamp(av, 0, 1);
-                }
-                lay.thickness = std::max<Float>(ml[0], std::numeric_limits<Float>::min());
-                lay.g = Clamp(ml[1], -1, 1);
-                lay.maxDepth = (int)ml[2];
-                lay.nSamples = (int)ml[3];
-                if (f->regularize && anyNonSpecular) {
-                    lay.top.mf.Regularize();
-                    lay.bottom.mf.Regularize();
-                }
-            } else if (bx.type == 7) {
-                // DiffuseTransmissionMaterial::GetBxDF (materials.h): Clamp(scale * R | T, 0, 1)
-                const float *ml = f->material_layer + 12 * mat;
-                const Float scale = f->material_params[4 * mat + 3];
-                for (int i = 0; i < NS; ++i) {
-                    Float l = lambda.lambda[i];
-                    Float r = f->material_constant[mat] ? mc[3] : Sigmoid(mc[0], mc[1], mc[2], l);
-                    Float t = ml[8] != 0 ? ml[7] : Sigmoid(ml[4], ml[5], ml[6], l);
-                    bx.R[i] = Clamp(scale * r, 0, 1);
-                    bx.Tt[i] = Clamp(scale * t, 0, 1);
-                }
-            } else if (bx.type == 0) {
-                // DiffuseMaterial::GetBxDF: Clamp(texEval(reflectance), 0, 1)
-                const int rt = f->material_tex ? f->material_tex[4 * mat] : -1;
-                if (rt >= 0) {
-                    const Spectrum R = tex.EvalS(rt, tex.Ctx(si), lambda);
-                    for (int i = 0; i < NS; ++i) bx.R[i] = Clamp(R[i], 0, 1);
-                } else {
-                    for (int i = 0; i < NS; ++i) {
-                        Float r = f->material_constant[mat] ? mc[3] : Sigmoid(mc[0], mc[1], mc[2], lambda.lambda[i]);
-                        bx.R[i] = Clamp(r, 0, 1);
-                    }
-                }
-            } else {
-                const float *mp = f->material_params + 4 * mat;
-                bx.mf.ax = mp[0];  // alphas arrive remapped and clamped (TrowbridgeReitz ctor)
-                bx.mf.ay = mp[1];
-                const int32_t *mt = f->material_tex ? f->material_tex + 4 * mat : nullptr;
-                OTexCtx tctx;
-                if (mt && (mt[0] >= 0 || mt[1] >= 0)) tctx = tex.Ctx(si);
-                if (mt && mt[1] >= 0) {
-                    // texEval(uRoughness), texEval(vRoughness), RoughnessToAlpha if remapped,
-                    // TrowbridgeReitzDistribution(urough, vrough) (materials.h:182-204, :491-511)
-                    Float ur = tex.EvalF(mt[1], tctx), vr = tex.EvalF(mt[2], tctx);
-                    if (mt[3]) {
-                        ur = std::sqrt(ur);
-                        vr = std::sqrt(vr);
-                    }
-                    bx.mf = TRDistribution(ur, vr);
-                }
-                bx.eta = mp[2] == 0 ? 1.f : mp[2];
-                if ((bx.type == 1 || bx.type == 6) && f->material_spectra[2 * mat] >= 0) {
-                    // DielectricMaterial::GetBxDF (materials.cpp:25-49): a spectral eta is taken at
-                    // lambda_0 and the secondary wavelengths are terminated
-                    // (SampledWavelengths::TerminateSecondary: pdf = (pdf_0 / n, 0, ..., 0))
-                    const int es = f->material_spectra[2 * mat], a = f->pl_offsets[es];
-                    Float e = PLEval(f->pl_lambda + a, f->pl_value + a, f->pl_offsets[es + 1] - a, lambda.lambda[0]);
-                    bx.eta = e == 0 ? 1.f : e;
-                    if (lambda.pdf[1] != 0) {
-                        for (int i = 1; i < NS; ++i) lambda.pdf[i] = 0;
-                        lambda.pdf[0] /= NS;
-                    }
-                }
-                if (bx.type == 2) {
-                    int es = f->material_spectra[2 * mat], ks = f->material_spectra[2 * mat + 1];
-                    for (int i = 0; i < NS; ++i) {
-                        Float l = lambda.lambda[i];
-                        if (es >= 0) {
-                            const int a = f->pl_offsets[es], b = f->pl_offsets[ks];
-                            bx.etaS[i] = PLEval(f->pl_lambda + a, f->pl_value + a, f->pl_offsets[es + 1] - a, l);
-                            bx.kS[i] = PLEval(f->pl_lambda + b, f->pl_value + b, f->pl_offsets[ks + 1] - b, l);
-                        } else {
-                            Float r = Clamp(Sigmoid(mc[0], mc[1], mc[2], l), 0, .9999f);
-                            bx.etaS[i] = 1;
-                            bx.kS[i] = 2 * std::sqrt(r) / std::sqrt(std::max<Float>(0, 1 - r));
-                        }
-                    }
-                    if (mt && mt[0] >= 0) {
-                        // ConductorMaterial::GetBxDF: r = Clamp(texEval(reflectance), 0, .9999)
-                        const Spectrum R = tex.EvalS(mt[0], tctx, lambda);
-                        for (int i = 0; i < NS; ++i) {
-                            Float r = Clamp(R[i], 0, .9999f);
-                            bx.etaS[i] = 1;
-                            bx.kS[i] = 2 * std::sqrt(r) / std::sqrt(std::max<Float>(0, 1 - r));
-                        }
-                    }
-                }
-                if (f->regularize && anyNonSpecular && bx.type != 6) bx.mf.Regularize();  // thin: no-op
-            }
+            const bool layered = MakeBSDF(mat, lambda, anyNonSpecular, si, bx, lay);
             Vec fx_ = Normalize(si.dpdus), fz = si.ns, fy_ = Cross(fz, fx_);
             auto toLocal = [&](Vec v) { return Vec(Dot(v, fx_), Dot(v, fy_), Dot(v, fz)); };
             auto fromLocal = [&](Vec v) { return fx_ * v.x + fy_ * v.y + fz * v.z; };
@@ -4865,6 +4885,200 @@ struct Renderer {
         rgb[1] = f->imaging_ratio * (yb * Lp).Average();
         rgb[2] = f->imaging_ratio * (zb * Lp).Average();
     }
+
+    // PathIntegrator::Li (cpu/integrators.cpp:629-762) with SampleLd (:764-805) for one pixel
+    // sample -- configs[0]'s CPU integrator, a different estimator of the same image as the
+    // wavefront volpath above: power-heuristic MIS, Russian roulette after the second bounce, and
+    // the CPU sampler's sequential dimensions (light choice 1D + light point 2D only when the
+    // BSDF is non-specular, BSDF 1D + 2D, the roulette 1D only when it is tested).  Surfaces only
+    // (a scene with media returns false).
+    bool PathLi(int px, int py, int sampleIndex, float rgb[3], float *weight) const {
+        if (f->n_media > 0) return false;
+        AnySampler hs{HaltonState{&S.halton, 0, 0}, ZSobolState{&S.zsobol}, S.useZSobol};
+        hs.Start(px, py, sampleIndex, 0);
+        Wavelengths lambda;
+        Vec ro, rd;
+        CameraRay(px, py, hs, lambda, weight, ro, rd);
+        Spectrum L(0.f), beta(1.f);
+        int depth = 0;
+        Float p_b = 0, etaScale = 1;
+        bool specularBounce = false, anyNonSpecular = false;
+        Vec prevP, prevErr, prevN, prevNs;
+        TriIsect dummy;
+        auto unoccluded = [&](Vec pf, Vec pt) { return S.Intersect(pf, pt - pf, 1 - ShadowEpsilon, &dummy, true) < 0; };
+        while (true) {
+            TriIsect ti;
+            const int prim = S.Intersect(ro, rd, Infinity, &ti, false);
+            if (prim < 0) {
+                // escaped: every infinite light's Le, MIS-weighted against the BSDF sample
+                for (int k = 0; k < f->n_infinite_lights; ++k) {
+                    if (f->inf_distant[k] >= 0) continue;  // DistantLight is not in infiniteLights
+                    const int gi = f->n_area_lights + f->n_point_spot + k;
+                    const OEnvLight *E = EnvOf(gi);
+                    const float *illum = f->dense_spectra + 311 * f->inf_spectrum[k];
+                    Spectrum Le;
+                    Float pdfLi = 0;
+                    if (E) {
+                        Float u, v;
+                        OEnvLight::SphereToSquare(Normalize(OEnvLight::Mul(E->mi, rd)), &u, &v);
+                        Le = E->Le(u, v, lambda, illum, f->inf_scale[k]);
+                        OEnvLight::SphereToSquare(OEnvLight::Mul(E->mi, rd), &u, &v);
+                        pdfLi = E->PDF(u, v) / (4 * Pi);
+                    } else {
+                        Le = SampleDense(illum, lambda) * f->inf_scale[k];
+                    }
+                    if (depth == 0 || specularBounce) L = L + beta * Le;
+                    else {
+                        const Float p_l = lights.PMF(prevP, prevNs, gi) * pdfLi;
+                        L = L + beta * PowerHeuristic(1, p_b, 1, p_l) * Le;
+                    }
+                }
+                break;
+            }
+            Interaction si = S.Interact(prim, ti, rd);
+            // emission at the hit (SurfaceInteraction::Le -> DiffuseAreaLight::L)
+            const int light = S.Light(prim);
+            if (light >= 0 && (f->light_two_sided[light] || DotN(si.n, si.wo) >= 0)) {
+                const Spectrum Le = LightL(light, lambda);
+                if (Le) {
+                    if (depth == 0 || specularBounce) L = L + beta * Le;
+                    else {
+                        const int lp = f->light_prim[light];
+                        const Float pdfA = lp >= f->n_triangles
+                            ? S.shapes[lp - f->n_triangles].PDF(prevP, prevErr, prevN, -si.wo, prevNs)
+                            : TrianglePDF(S.P(lp, 0), S.P(lp, 1), S.P(lp, 2), f->tri_flip[lp], prevP, prevErr, prevN,
+                                          prevNs, -si.wo, S.Attr(lp));
+                        const Float p_l = lights.PMF(prevP, prevNs, light) * pdfA;
+                        L = L + beta * PowerHeuristic(1, p_b, 1, p_l) * Le;
+                    }
+                }
+            }
+            // GetBSDF; an interface (no BSDF) is skipped at the same depth
+            const int mat0 = S.Material(prim);
+            if (f->material_type[mat0] == 3) {
+                specularBounce = true;
+                ro = OffsetRayOrigin(si.p, si.err, si.n, rd);
+                continue;
+            }
+            const int mat = ResolveMix(mat0, si);
+            BxDF bx;
+            LayeredBxDF lay;
+            const bool layered = MakeBSDF(mat, lambda, anyNonSpecular, si, bx, lay);
+            if (depth++ == S.maxDepth) break;
+            Vec fx_ = Normalize(si.dpdus), fz = si.ns, fy_ = Cross(fz, fx_);
+            auto toLocal = [&](Vec v) { return Vec(Dot(v, fx_), Dot(v, fy_), Dot(v, fz)); };
+            auto fromLocal = [&](Vec v) { return fx_ * v.x + fy_ * v.y + fz * v.z; };
+            const Vec woL = toLocal(si.wo);
+            const int flags = layered ? lay.Flags() : bx.Flags();
+            auto bsdfF = [&](Vec wi) {
+                const Vec wiL = toLocal(wi);
+                return woL.z == 0 ? Spectrum(0.f) : layered ? lay.f(woL, wiL, true) : bx.f(woL, wiL);
+            };
+            auto bsdfPDF = [&](Vec wi) {
+                const Vec wiL = toLocal(wi);
+                return woL.z == 0 ? Float(0) : layered ? lay.PDF(woL, wiL, true) : bx.PDF(woL, wiL);
+            };
+            // SampleLd: light choice, light point, BSDF * |cos|, visibility, MIS
+            if (flags & (BxDiffuse | BxGlossy)) {
+                Vec cp = si.p, cpErr = si.err;
+                const bool refl = flags & BxR, trans = flags & BxT;
+                if (refl && !trans) cp = OffsetRayOrigin(si.p, si.err, si.n, si.wo), cpErr = Vec(0, 0, 0);
+                else if (trans && !refl) cp = OffsetRayOrigin(si.p, si.err, si.n, -si.wo), cpErr = Vec(0, 0, 0);
+                const Float uc = hs.Get1D();
+                Float u0, u1;
+                hs.Get2D(&u0, &u1);
+                int li;
+                Float lpmf;
+                if (lights.Sample(cp, si.ns, uc, &li, &lpmf)) {
+                    Spectrum Le(0.f);
+                    Vec wi, pf, pt;
+                    Float pdf = 0;
+                    bool delta = false;
+                    DeltaSample ds;
+                    const OEnvLight *E = EnvOf(li);
+                    if (E) {
+                        Float eu, ev, emap;
+                        if (E->Sample(u0, u1, &eu, &ev, &emap)) {
+                            const int k = li - f->n_area_lights - f->n_point_spot;
+                            wi = OEnvLight::Mul(E->m, OEnvLight::SquareToSphere(eu, ev));
+                            pt = cp + wi * (2 * f->scene_radius);
+                            Le = E->Le(eu, ev, lambda, f->dense_spectra + 311 * f->inf_spectrum[k], f->inf_scale[k]);
+                            pdf = emap / (4 * Pi);
+                            pf = OffsetRayOrigin(si.p, si.err, si.n, pt - si.p);
+                        }
+                    } else if (li >= f->n_area_lights) {
+                        if (DeltaLi(li, cp, lambda, &ds)) {
+                            wi = ds.wi;
+                            Le = ds.L;
+                            pdf = 1;
+                            delta = true;
+                            pf = OffsetRayOrigin(si.p, si.err, si.n, ds.p - si.p);
+                            pt = ds.p;
+                        }
+                    } else {
+                        ShapeSample ss;
+                        const int lp = f->light_prim[li];
+                        const bool ok = lp >= f->n_triangles
+                            ? S.shapes[lp - f->n_triangles].Sample(cp, cpErr, si.n, u0, u1, &ss, si.ns)
+                            : TriangleSample(S.P(lp, 0), S.P(lp, 1), S.P(lp, 2), f->tri_flip[lp], cp, si.ns, u0, u1, &ss,
+                                             S.Attr(lp));
+                        if (ok && ss.pdf != 0 && LengthSquared(ss.p - cp) != 0) {
+                            wi = Normalize(ss.p - cp);
+                            if (f->light_two_sided[li] || DotN(ss.n, -wi) >= 0) Le = LightL(li, lambda);
+                            pdf = ss.pdf;
+                            pf = OffsetRayOrigin(si.p, si.err, si.n, ss.p - si.p);
+                            pt = OffsetRayOrigin(ss.p, ss.err, ss.n, pf - ss.p);
+                        }
+                    }
+                    if (Le && pdf != 0) {
+                        const Spectrum fv = bsdfF(wi) * AbsDotN(si.ns, wi);
+                        if (fv && unoccluded(pf, pt)) {
+                            const Float p_l = lpmf * pdf;
+                            if (delta) L = L + beta * (Le * fv / p_l);
+                            else {
+                                const Float w_l = PowerHeuristic(1, p_l, 1, bsdfPDF(wi));
+                                L = L + beta * (Le * w_l * fv / p_l);  // w_l * L[i]: one product, same bits
+                            }
+                        }
+                    }
+                }
+            }
+            // BSDF sample -> next ray, then Russian roulette
+            const Float ucB = hs.Get1D();
+            Float b0, b1;
+            hs.Get2D(&b0, &b1);
+            BSDFSample bs;
+            const bool sampled = woL.z != 0 && flags &&
+                                 (layered ? lay.Sample_f(woL, ucB, b0, b1, &bs, true) : bx.Sample_f(woL, ucB, b0, b1, &bs));
+            if (!sampled || !bs.f || bs.pdf == 0 || bs.wi.z == 0) break;
+            const Vec wi = fromLocal(bs.wi);
+            beta = beta * bs.f * AbsDotN(si.ns, wi) / bs.pdf;
+            p_b = layered ? bsdfPDF(wi) : bs.pdf;  // pdfIsProportional: BSDF::PDF
+            specularBounce = bs.flags & BxSpecular;
+            anyNonSpecular = anyNonSpecular || !specularBounce;
+            if (bs.flags & BxT) etaScale *= Sqr(bs.eta);
+            prevP = si.p;
+            prevErr = si.err;
+            prevN = si.n;
+            prevNs = si.ns;
+            ro = OffsetRayOrigin(si.p, si.err, si.n, wi);
+            rd = wi;
+            const Spectrum rrBeta = beta * etaScale;
+            if (rrBeta.Max() < 1 && depth > 1) {
+                const Float q = std::max<Float>(0, 1 - rrBeta.Max());
+                if (hs.Get1D() < q) break;
+                beta = beta / (1 - q);
+            }
+        }
+        Spectrum Lp;
+        for (int i = 0; i < NS; ++i) Lp[i] = lambda.pdf[i] != 0 ? L[i] / lambda.pdf[i] : 0;
+        Spectrum xb = SampleDense(f->sensor_xyz, lambda), yb = SampleDense(f->sensor_xyz + 311, lambda),
+                 zb = SampleDense(f->sensor_xyz + 622, lambda);
+        rgb[0] = f->imaging_ratio * (xb * Lp).Average();
+        rgb[1] = f->imaging_ratio * (yb * Lp).Average();
+        rgb[2] = f->imaging_ratio * (zb * Lp).Average();
+        return true;
+    }
 };
 
 }  // namespace oracle
@@ -4927,8 +5141,8 @@ int oracle_intersect_tr(const pbrt_scene_flat *flat, const pbrt_scene_info *info
 
 // Renders rows x [first_sample, first_sample + n_samples) into film[4][yres*xres]
 // (sensor RGB sums + weight sums, RGBFilm::Pixel layout) with `threads` host threads.
-int oracle_render(const pbrt_scene_flat *flat, const pbrt_scene_info *info, const int32_t *rows, int nRows,
-                  int firstSample, int nSamples, int uniformLightSampler, int threads, double *film) {
+static int RenderRows(const pbrt_scene_flat *flat, const pbrt_scene_info *info, const int32_t *rows, int nRows,
+                      int firstSample, int nSamples, int uniformLightSampler, int threads, double *film, bool path) {
     Renderer r;
     r.f = flat;
     r.S.Init(flat, info);
@@ -4954,7 +5168,11 @@ int oracle_render(const pbrt_scene_flat *flat, const pbrt_scene_info *info, cons
                 size_t pix = (size_t)y * info->xres + x;
                 for (int s = firstSample; s < firstSample + nSamples; ++s) {
                     float rgb[3], w;
-                    r.Li(x, y, s, rgb, &w);
+                    if (path) {
+                        if (!r.PathLi(x, y, s, rgb, &w)) return;
+                    } else {
+                        r.Li(x, y, s, rgb, &w);
+                    }
                     // RGBFilm::AddSample's clamp (film.h:247-249)
                     const float m = std::max({rgb[0], rgb[1], rgb[2]});
                     if (m > flat->max_component_value) {
@@ -4974,7 +5192,18 @@ int oracle_render(const pbrt_scene_flat *flat, const pbrt_scene_info *info, cons
     for (int t = 1; t < threads; ++t) pool.emplace_back(work);
     work();
     for (auto &t : pool) t.join();
-    return 0;
+    return path && flat->n_media > 0 ? -3 : 0;
+}
+
+// WavefrontPathIntegrator semantics (the product's): film[4][yres][xres] += w * rgb, w
+int oracle_render(const pbrt_scene_flat *flat, const pbrt_scene_info *info, const int32_t *rows, int nRows,
+                  int firstSample, int nSamples, int uniformLightSampler, int threads, double *film) {
+    return RenderRows(flat, info, rows, nRows, firstSample, nSamples, uniformLightSampler, threads, film, false);
+}
+// PathIntegrator (cpu/integrators.cpp:629-805) on the same film; -3 for a scene with media
+int oracle_render_path(const pbrt_scene_flat *flat, const pbrt_scene_info *info, const int32_t *rows, int nRows,
+                       int firstSample, int nSamples, int uniformLightSampler, int threads, double *film) {
+    return RenderRows(flat, info, rows, nRows, firstSample, nSamples, uniformLightSampler, threads, film, true);
 }
 
 // closest / any hit for an SoA ray batch rays[7][n] (o, d, tMax); prim = original triangle

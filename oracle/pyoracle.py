@@ -44,6 +44,9 @@ def lib():
         _lib.oracle_triangle_shading.argtypes = [vp] * 3 + [ctypes.c_int] + [vp] * 3
         _lib.oracle_render.argtypes = [vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, vp]
+        _lib.oracle_render_path.argtypes = [vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_int, vp]
+        _lib.oracle_render_path.restype = ctypes.c_int
         _lib.oracle_set_cr_math.argtypes = [ctypes.c_int]
         _lib.oracle_light_bvh.argtypes = [vp, vp, ctypes.c_int, vp, vp, vp, ctypes.c_int]
         _lib.oracle_intersect_tr.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int, vp]
@@ -157,8 +160,10 @@ def f32(a):
     return np.ascontiguousarray(np.asarray(a, dtype=np.float32))
 
 
-def render(scene, rows=None, first_sample=0, n_samples=None, threads=None):
-    """Render `rows` of a pbrt_amd.Scene on the CPU; returns film [4, yres, xres] float64."""
+def render(scene, rows=None, first_sample=0, n_samples=None, threads=None, path=False):
+    """Render `rows` of a pbrt_amd.Scene on the CPU; returns film [4, yres, xres] float64.
+    path=False: WavefrontPathIntegrator semantics (the product's); path=True: the CPU
+    PathIntegrator (cpu/integrators.cpp:629-805, surfaces only) -- configs[0]'s integrator."""
     info = scene.info
     flat = scene.flat()
     if rows is None:
@@ -168,7 +173,8 @@ def render(scene, rows=None, first_sample=0, n_samples=None, threads=None):
         n_samples = info.spp - first_sample
     threads = threads or os.cpu_count() or 1
     film = np.zeros((4, info.yres, info.xres), dtype=np.float64)
-    rc = lib().oracle_render(ctypes.byref(flat), ctypes.byref(info), rows.ctypes.data_as(ctypes.c_void_p),
+    fn = lib().oracle_render_path if path else lib().oracle_render
+    rc = fn(ctypes.byref(flat), ctypes.byref(info), rows.ctypes.data_as(ctypes.c_void_p),
                              len(rows), int(first_sample), int(n_samples), int(info.uniform_light_sampler),
                              int(threads), film.ctypes.data_as(ctypes.c_void_p))
     assert rc == 0

@@ -1225,6 +1225,8 @@ static void BuildDevice(pbrt_context *c) {
         c->rayBinning = !c->volumetric && (rs ? atoi(rs) != 0 : S.ldsTris == 0);
         const char *rk = getenv("PBRT_AMD_RAY_BIN_KEY");
         S.rayBinMode = rk ? std::max(0, std::min(2, atoi(rk))) : 0;
+        const char *xg = getenv("PBRT_AMD_XCD_GROUPS");
+        S.xcdGroups = xg ? std::max(0, atoi(xg)) : 16;
     }
 
     // the scene struct's device copy (DeviceScene::self)
@@ -1868,6 +1870,13 @@ int pbrt_synchronize(pbrt_context *ctx) {
         ctx->stats.closest_rays = ds[1];
         ctx->stats.shadow_rays = ds[2];
         ctx->stats.timed_closest_rays = ds[3];
+        {
+            const DeviceScene &S = ctx->S;
+            const uint64_t nodeB = S.compressed ? sizeof(BVH8QNode) : sizeof(BVH8Node);
+            const uint64_t nNodes = S.compressed ? ctx->qnodes.n : ctx->nodes.n;
+            ctx->stats.bvh_hbm_node_bytes = nNodes > (uint64_t)S.ldsNodes ? (nNodes - S.ldsNodes) * nodeB : 0;
+            ctx->stats.bvh_hbm_tri_bytes = S.ldsTris > 0 ? 0 : (uint64_t)ctx->triVerts.n * sizeof(float);
+        }
         return 0;
     } catch (const std::exception &e) {
         return Fail(e.what());

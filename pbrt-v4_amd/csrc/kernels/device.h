@@ -221,6 +221,7 @@ struct DeviceScene {
     float bvhAbsMax[3];  // bound on |plane coordinate| per axis (traversal box-test margins)
     float rayBinLo[3], rayBinScale[3];  // ray-binning grid: cell = (o - lo) * scale, 8 per axis
     int rayBinMode;                     // RayBinKey's key layout (PBRT_AMD_RAY_BIN_KEY)
+    int xcdGroups;  // chunks per super-chunk of the traversal kernels' XCD-grouped walk, 0 = off (XcdChunks; PBRT_AMD_XCD_GROUPS)
     int ldsNodes, ldsTris;  // BVH8 nodes / triangles cached in LDS by the traversal kernels
     ShadeLdsLayout shadeLds;
     DeviceMedia media;

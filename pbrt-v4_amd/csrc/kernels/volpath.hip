@@ -550,7 +550,8 @@ template <int TM>
 __global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_vclosest(DeviceScene S, PathState st, VolState v,
                                                                           int wf, int timed) {
     const QueueView rays = LoadQueue(st, wf, kVRay);
-    if ((int)(blockIdx.x * blockDim.x) >= rays.total) return;
+    ChunkWalk walk = XcdChunks(rays.total, S.xcdGroups);
+    if (walk.n >= walk.end) return;
     extern __shared__ float4 dynLds[];
     const SceneLds L = SetupSceneLds(S, dynLds);
     const int NR = st.NR;
@@ -563,8 +564,8 @@ __global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_vclosest(DeviceS
         atomicAdd(&st.stats[1], (unsigned long long)rays.total);
         if (timed) atomicAdd(&st.stats[3], (unsigned long long)rays.total);  // rays of event-timed launches
     }
-    for (int base = blockIdx.x * blockDim.x; base < rays.total; base += gridDim.x * blockDim.x) {
-        const int j = base + threadIdx.x;
+    for (; walk.n < walk.end; walk.n += walk.step) {
+        const int j = walk.Chunk() * blockDim.x + threadIdx.x;
         const bool active = j < rays.total;
         const int ri = active ? QueueSlot(rays, j) : 0;
         int medium = -1;

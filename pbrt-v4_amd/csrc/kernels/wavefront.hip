@@ -65,7 +65,8 @@ __global__ void __launch_bounds__(kBlock, TraversalWaves(TM))
     constexpr bool kMix = NMatQ_ == kClosestMix;
     constexpr int NMatQ = kMix ? kNumMatTypes : NMatQ_;
     const QueueView rays = LoadQueue(st, depth, kCntRay);
-    if ((int)(blockIdx.x * blockDim.x) >= rays.total) return;  // no work
+    ChunkWalk walk = XcdChunks(rays.total, S.xcdGroups);
+    if (walk.n >= walk.end) return;  // no work
     extern __shared__ float4 dynLds[];
     const SceneLds L = SetupSceneLds(S, dynLds);
     const int N = st.NR;  // record stride
@@ -94,8 +95,8 @@ __global__ void __launch_bounds__(kBlock, TraversalWaves(TM))
         atomicAdd(&st.stats[1], (unsigned long long)count);
         if (timed) atomicAdd(&st.stats[3], (unsigned long long)count);  // rays of event-timed launches
     }
-    for (int base = blockIdx.x * blockDim.x; base < count; base += gridDim.x * blockDim.x) {
-        const int j = base + threadIdx.x;
+    for (; walk.n < walk.end; walk.n += walk.step) {
+        const int j = walk.Chunk() * blockDim.x + threadIdx.x;
         bool active = j < count;
         int qi = 0;  // record index of this depth
         int prim = -1;
@@ -1377,13 +1378,16 @@ __global__ void __launch_bounds__(kBlock) k_texture(DeviceScene S, PathState st,
 template <int TM>
 __global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_shadow(DeviceScene S, PathState st, int depth) {
     const QueueView shadows = LoadQueue(st, depth, kCntShadow);
-    if ((int)(blockIdx.x * blockDim.x) >= shadows.total) return;  // no work
+    ChunkWalk walk = XcdChunks(shadows.total, S.xcdGroups);
+    if (walk.n >= walk.end) return;  // no work
     extern __shared__ float4 dynLds[];
     const SceneLds L = SetupSceneLds(S, dynLds);
     const int N = st.NR, NL = st.N;
     const int count = shadows.total;
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&st.stats[2], (unsigned long long)count);
-    for (int qi = blockIdx.x * blockDim.x + threadIdx.x; qi < count; qi += gridDim.x * blockDim.x) {
+    for (; walk.n < walk.end; walk.n += walk.step) {
+        const int qi = walk.Chunk() * blockDim.x + threadIdx.x;
+        if (qi >= count) continue;
         // the shadow queue is dense per shard: entry p holds the ray, its contribution and pixel
         const int p = QueueSlot(shadows, qi);
         V3 o(st.shadowRay[p], st.shadowRay[N + p], st.shadowRay[2 * N + p]);

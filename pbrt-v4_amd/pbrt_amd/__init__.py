@@ -113,7 +113,8 @@ class RenderStats(ctypes.Structure):
     _fields_ = [("camera_rays", ctypes.c_uint64), ("closest_rays", ctypes.c_uint64),
                 ("shadow_rays", ctypes.c_uint64), ("closest_launches", ctypes.c_int),
                 ("closest_ms", ctypes.c_double), ("timed_closest_rays", ctypes.c_uint64), ("passes", ctypes.c_int),
-                ("paths_per_pass", ctypes.c_uint64)]
+                ("paths_per_pass", ctypes.c_uint64), ("bvh_hbm_node_bytes", ctypes.c_uint64),
+                ("bvh_hbm_tri_bytes", ctypes.c_uint64)]
 
 
 class KernelStat(ctypes.Structure):

@@ -86,7 +86,39 @@ def texture_images(out, rng):
     return names
 
 
-def generate(outdir, copies=122, level=6, xres=1920, yres=1080, spp=128, seed=0, maxdepth=5, textured=True):
+def leaf_mask(out, n=256):
+    """grey 8-bit PNG of a leaf cut-out (1 inside an elliptic blade with a notched tip and a
+    stem, 0 outside, a one-texel ramp at the edge): the alpha texture of the leaf canopy"""
+    y, x = (np.mgrid[0:n, 0:n].astype(np.float32) + 0.5) / n
+    u, v = x - 0.5, y - 0.5
+    blade = (u / 0.32) ** 2 + (v / 0.46) ** 2 - 0.08 * np.cos(18 * np.arctan2(v, u))
+    stem = (np.abs(u) < 0.02) & (v > 0.3)
+    a = np.clip((1 - blade) * n / 8, 0, 1)
+    a = np.maximum(a, stem.astype(np.float32))
+    write_png(out / "c4_leaf.png", 255 * a)
+    return "c4_leaf.png"
+
+
+def leaf_canopy(rng, n_leaves, lo, hi):
+    """n_leaves randomly oriented unit-ish quads (2 triangles each, uv over the leaf image) in the
+    box [lo, hi]: one trianglemesh whose "texture alpha" cuts the leaf shape out of each quad"""
+    c = rng.uniform(lo, hi, (n_leaves, 3))
+    a = rng.normal(size=(n_leaves, 3))
+    a /= np.linalg.norm(a, axis=1, keepdims=True)
+    b = np.cross(a, rng.normal(size=(n_leaves, 3)))
+    b /= np.linalg.norm(b, axis=1, keepdims=True)
+    s = rng.uniform(0.15, 0.35, (n_leaves, 1))
+    P = np.stack([c - s * a - s * b, c + s * a - s * b, c + s * a + s * b, c - s * a + s * b], axis=1)
+    F = (np.arange(n_leaves)[:, None, None] * 4 + np.array([[0, 1, 2], [0, 2, 3]])[None]).reshape(-1, 3)
+    UV = np.tile(np.array([[0, 0], [1, 0], [1, 1], [0, 1]], np.float32), (n_leaves, 1))
+    return P.reshape(-1, 3), F, UV
+
+
+def generate(outdir, copies=122, level=6, xres=1920, yres=1080, spp=128, seed=0, maxdepth=5, textured=True,
+             leaves=0):
+    """leaves > 0 adds an alpha-tested leaf canopy (that many cut-out quads, one PLY mesh with
+    per-vertex uv and a "texture alpha" leaf image) above the field of copies, as San Miguel's
+    foliage: every candidate hit on it runs the stochastic alpha test (gpu/optix.cu:197-243)"""
     out = Path(outdir)
     out.mkdir(parents=True, exist_ok=True)
     rng = np.random.default_rng(seed)
@@ -142,6 +174,15 @@ def generate(outdir, copies=122, level=6, xres=1920, yres=1080, spp=128, seed=0,
         lines.append(f'{mat}\nShape "plymesh" "string filename" "{name}"')
     n_tris += 2 + 2
     depth = max(cells, key=lambda c: c[1])[1] * 1.4 + 4
+    if leaves:
+        mask = leaf_mask(out)
+        P, F, UV = leaf_canopy(np.random.default_rng(seed + 2), leaves, [-(nx / 2) * 1.3, 1.8, -0.5],
+                               [(nx / 2) * 1.3, 3.4, depth - 2])
+        write_ply(out / "c4_leaves.ply", P, F, UV)
+        n_tris += len(F)
+        lines.append(f'Texture "leafmask" "float" "imagemap" "string filename" "{mask}" "string encoding" "linear"\n'
+                     'Material "diffuse" "rgb reflectance" [ 0.12 0.35 0.08 ]\n'
+                     'Shape "plymesh" "string filename" "c4_leaves.ply" "texture alpha" "leafmask"')
     text = f"""# C4: {len(cells)} copied displaced icospheres, {n_tris} triangles (scenes/gen_c4.py, seed {seed})
 LookAt 0 3.2 -6  0 1.0 {depth / 3:.3f}  0 1 0
 Camera "perspective" "float fov" [ 50 ]
@@ -182,8 +223,10 @@ def main():
     ap.add_argument("--yres", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=128)
     ap.add_argument("--untextured", action="store_true")
+    ap.add_argument("--leaves", type=int, default=0, help="alpha-tested leaf quads above the copies")
     a = ap.parse_args()
-    path, n = generate(a.outdir, a.copies, a.level, a.xres, a.yres, a.spp, textured=not a.untextured)
+    path, n = generate(a.outdir, a.copies, a.level, a.xres, a.yres, a.spp, textured=not a.untextured,
+                       leaves=a.leaves)
     print(path, n, "triangles")
 
 

@@ -8,7 +8,11 @@
   grazing rays in a triangle's plane, random rays through the scene box -- for both node
   formats.  Hit/miss must agree for every ray; hit triangle ids exactly except equal-t ties
   (two triangles sharing the hit point); t bit for bit.
-* A 4-row x 4-spp image stripe vs the oracle at test_gpu_parity's tolerance."""
+* A 4-row x 4-spp image stripe vs the oracle at test_gpu_parity's tolerance.
+
+The scene carries gen_c4's alpha-tested leaf canopy (20,000 cut-out quads, "texture alpha"), so
+every candidate hit on a leaf runs the stochastic alpha test inside the full-size traversal; the
+intersection classes include rays from the leaves' own triangles."""
 import os
 
 import numpy as np
@@ -17,6 +21,7 @@ import pytest
 from conftest import SCENES
 
 pytestmark = pytest.mark.gpu
+LEAVES = 20000  # alpha-tested leaf quads (gen_c4 leaf canopy): the any-hit alpha test at full size
 
 
 @pytest.fixture(scope="module")
@@ -24,9 +29,10 @@ def c4(tmp_path_factory, pa):
     import sys
     sys.path.insert(0, str(SCENES))
     import gen_c4
-    path, n_tris = gen_c4.generate(tmp_path_factory.mktemp("c4full"), xres=1920, yres=1080, spp=4)
+    path, n_tris = gen_c4.generate(tmp_path_factory.mktemp("c4full"), xres=1920, yres=1080, spp=4,
+                                   leaves=LEAVES)
     sc = pa.load_scene(path)
-    assert sc.info.n_triangles == n_tris == 9994244
+    assert sc.info.n_triangles == n_tris == 9994244 + 2 * LEAVES
     # a deep tree: the traversal's LDS group stack (8 B per entry and lane) is 18 KB per block,
     # admitted beside the static LDS with a smaller node cache (capi.hip BuildDevice)
     st = sc.bvh_stats()

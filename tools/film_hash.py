@@ -21,6 +21,11 @@ elif scene == "c3":
 elif scene == "c5":
     import gen_c5
     sc = pa.Scene.from_string(gen_c5.scene_text(x, y, spp, grid=64), ROOT / "scenes")
+elif scene == "c4":
+    import tempfile
+    import gen_c4
+    path, _ = gen_c4.generate(Path(tempfile.mkdtemp(prefix="pbrt_c4_")), xres=x, yres=y, spp=spp, textured=True)
+    sc = pa.load_scene(path)
 else:
     sc = pa.load_scene(scene, xresolution=x, yresolution=y, spp=spp)
 integ = pa.WavefrontPathIntegrator(sc, device=0)

@@ -130,13 +130,20 @@ typedef struct pbrt_scene_flat {
      * 192-276, 1376-1495) in render space, [n_delta_lights][24] floats: type (0 point, 1 spot,
      * 2 distant), dense spectrum index, final scale, cosFalloffStart, cosFalloffEnd, p xyz, w xyz
      * (spot axis / direction toward a distant light), renderFromLight^-1 upper 3x3 row-major
-     * (spot), 4 unused.  The first n_point_spot are the point and spot lights: light-BVH members
+     * (spot, goniometric, projection), then LightBounds' phi, the light's offset into
+     * delta_images (-1: none), image width, height.  Types 3 (goniometric) and 4 (projection)
+     * keep LightBounds' cosTheta_o / cosTheta_e in the cosFalloff slots and their bounds axis in
+     * w.  The first n_point_spot are the point, spot, goniometric and projection lights: light-BVH members
      * with global light index n_area_lights + i.  Infinite-list entry j (global index
      * n_area_lights + n_point_spot + j) is a distant light when inf_distant[j] >= 0.
      * uniform_order[k]: global index of pbrt's k-th light (area lights, then LightSource order);
      * scene_radius: DistantLight::Preprocess's bounding-sphere radius. */
     int n_delta_lights, n_point_spot;
     const float *delta_lights;
+    /* per goniometric / projection light at its offset: a 4-float header {1 / tan(fov / 2)
+     * (projection), 0, 0, 0}, then the goniometric light's Y values [h][w] or the projection
+     * light's linear R, G, B [h][w][3] (row 0 = top) */
+    const float *delta_images;
     const int32_t *inf_distant;       /* [n_infinite_lights] */
     const int32_t *uniform_order;     /* [n_area_lights + n_point_spot + n_infinite_lights] */
     float scene_radius;

@@ -2175,7 +2175,9 @@ static std::vector<std::pair<int, LB>> SceneLightBounds(const pbrt_scene_flat *f
         const float *d = f->delta_lights + 24 * k;
         const Vec p(d[5], d[6], d[7]);
         const Float mx = denseMax((int)d[1]), scale = d[2];
-        if ((int)d[0] == 0) {
+        if ((int)d[0] >= 3) {  // goniometric / projection: the loader's LightBounds terms
+            L.push_back({f->n_area_lights + k, LB(Box(p, p), Vec(d[8], d[9], d[10]), d[20], d[3], d[4], false)});
+        } else if ((int)d[0] == 0) {
             L.push_back({f->n_area_lights + k, LB(Box(p, p), Vec(0, 0, 1), 4 * Pi * scale * mx, std::cos(Pi), std::cos(Pi / 2), false)});
         } else {
             const Float cosStart = d[3], cosEnd = d[4];
@@ -4297,6 +4299,40 @@ struct Renderer {
         ds->wi = Normalize(p - ref);
         ds->p = p;
         Float sc = scale;
+        if (type >= 3) {
+            // GoniometricLight / ProjectionLight::SampleLi (lights.cpp:320-331, 538-547): I at
+            // renderFromLight.ApplyInverse(-wi), divided by the squared distance
+            const Vec v = -ds->wi;
+            const Vec wl(d[11] * v.x + d[12] * v.y + d[13] * v.z, d[14] * v.x + d[15] * v.y + d[16] * v.z,
+                         d[17] * v.x + d[18] * v.y + d[19] * v.z);
+            const float *img = f->delta_images + (int)d[21];
+            const int w = (int)d[22], h = (int)d[23];
+            auto nearest = [&](Float u, Float vv) {  // Image::LookupNearestChannel, WrapMode::Clamp
+                const int x = std::clamp((int)(u * w), 0, w - 1), y = std::clamp((int)(vv * h), 0, h - 1);
+                return (size_t)y * w + x;
+            };
+            if (type == 3) {
+                Float u, vv;
+                OEnvLight::SphereToSquare(wl, &u, &vv);
+                ds->L = (I * scale * img[4 + nearest(u, vv)]) / DistanceSquared(p, ref);
+                return (bool)ds->L;
+            }
+            // ProjectionLight::I (lights.cpp:343-360)
+            if (wl.z < 1e-3f) return false;
+            const Float s = img[0], aspect = Float(w) / Float(h);
+            const Float bx = aspect > 1 ? aspect : 1, by = aspect > 1 ? 1 : 1 / aspect;
+            const Float psx = (s * wl.x) / wl.z, psy = (s * wl.y) / wl.z;
+            if (!(psx >= -bx && psx <= bx && psy >= -by && psy <= by)) return false;
+            const float *px = img + 4 + 3 * nearest((psx - -bx) / (bx - -bx), (psy - -by) / (by - -by));
+            Float c3[3] = {std::max<Float>(0, px[0]), std::max<Float>(0, px[1]), std::max<Float>(0, px[2])};
+            Float mx = std::max({c3[0], c3[1], c3[2]}), rs = 2 * mx, co[3];
+            if (rs) ORGBCoeffs(c3[0] / rs, c3[1] / rs, c3[2] / rs, co);
+            else ORGBCoeffs(0, 0, 0, co);
+            Spectrum sp;
+            for (int i = 0; i < NS; ++i) sp[i] = rs * Sigmoid(co[0], co[1], co[2], lambda.lambda[i]);
+            ds->L = ((sp * I) * scale) / DistanceSquared(p, ref);  // scale * RGBIlluminantSpectrum
+            return (bool)ds->L;
+        }
         if (type == 1) {
             const Vec v = -ds->wi;
             const Vec wl = Normalize(Vec(d[11] * v.x + d[12] * v.y + d[13] * v.z, d[14] * v.x + d[15] * v.y + d[16] * v.z,
@@ -4307,7 +4343,6 @@ struct Renderer {
         return (bool)ds->L;
     }
 
-    // one pixel sample -> sensor RGB and filter weight (film.h:95-100)
     // MixMaterial resolution of a hit's material (see the loop's comment)
     int ResolveMix(int mat, const Interaction &si) const {
         // MixMaterial::ChooseMaterial at the closest hit (wavefront/intersect.h:90-97,
@@ -4519,6 +4554,7 @@ struct Renderer {
             rd = dd;
         }
     }
+    // one pixel sample -> sensor RGB and filter weight (film.h:95-100)
     void Li(int px, int py, int sampleIndex, float rgb[3], float *weight) const {
         AnySampler hs{HaltonState{&S.halton, 0, 0}, ZSobolState{&S.zsobol}, S.useZSobol};
         hs.Start(px, py, sampleIndex, 0);

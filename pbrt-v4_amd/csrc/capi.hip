@@ -255,7 +255,7 @@ struct pbrt_scene {
     std::vector<int32_t> mediumInfo;
     std::vector<int32_t> tris, lightPrim, lightSpectrum, lightTwoSided, infSpectrum, matConstant, nodeInfo, matType,
         matSpectra, plOffsets, infDistant, uniformOrder;
-    std::vector<float> deltaLights;
+    std::vector<float> deltaLights, deltaImages;
     std::vector<int32_t> infImage, envInfo, shapeInfo, primAlpha;
     std::vector<float> shapeParams, shapeNormals;
     std::vector<float> envXform, envRgb;
@@ -343,12 +343,19 @@ struct pbrt_scene {
             infDistant.push_back(l.distant);
         }
         deltaLights.clear();
+        deltaImages.clear();
         for (auto &d : s.deltaLights) {
             deltaLights.insert(deltaLights.end(), {(float)d.type, (float)d.spectrum, d.scale, d.cosFalloffStart,
                                                    d.cosFalloffEnd, d.p.x, d.p.y, d.p.z, d.w.x, d.w.y, d.w.z});
             for (int i = 0; i < 3; ++i)
                 for (int j = 0; j < 3; ++j) deltaLights.push_back(d.m[i][j]);
-            deltaLights.insert(deltaLights.end(), {0.f, 0.f, 0.f, 0.f});
+            float off = -1;
+            if (!d.img.empty()) {
+                off = (float)deltaImages.size();
+                deltaImages.insert(deltaImages.end(), {d.invTanAng, 0.f, 0.f, 0.f});
+                deltaImages.insert(deltaImages.end(), d.img.begin(), d.img.end());
+            }
+            deltaLights.insert(deltaLights.end(), {d.phi, off, (float)d.imgW, (float)d.imgH});
         }
         uniformOrder.assign(s.uniformOrder.begin(), s.uniformOrder.end());
         dense.clear();
@@ -409,6 +416,7 @@ struct pbrt_context {
     DevBuf<int> primMaterial, primLight, matConstant, lightPrim, lightSpectrum, lightTwoSided, infSpectrum, infDistant,
         uniformOrder;
     DevBuf<DeviceDeltaLight> deltaLights;
+    DevBuf<float> deltaImg;
     DevBuf<int> primOrig, matType, matSpectra, plOffsets;
     DevBuf<float> matParams, plLambda, plValue, triShade, matLayer, dispL0;
     DevBuf<uint16_t> plIndex;
@@ -801,17 +809,37 @@ static void BuildDevice(pbrt_context *c) {
         }
         c->envLights.Upload(els);
         std::vector<DeviceDeltaLight> dd;
+        std::vector<float> dimg;  // goniometric Y values / projection per-pixel EnvCoef
         for (auto &d : s.deltaLights) {
             DeviceDeltaLight x{};
             x.p = make_float4(d.p.x, d.p.y, d.p.z, BitsToFloat((uint32_t)d.type));
             x.w = make_float4(d.w.x, d.w.y, d.w.z, d.scale);
-            x.cone = make_float4(d.cosFalloffStart, d.cosFalloffEnd, BitsToFloat((uint32_t)d.spectrum), 0.f);
-            x.m0 = make_float4(d.m[0][0], d.m[0][1], d.m[0][2], 0.f);
-            x.m1 = make_float4(d.m[1][0], d.m[1][1], d.m[1][2], 0.f);
-            x.m2 = make_float4(d.m[2][0], d.m[2][1], d.m[2][2], 0.f);
+            int off = -1;
+            if (d.type == kDeltaGonio) {
+                off = (int)dimg.size();
+                dimg.insert(dimg.end(), d.img.begin(), d.img.end());
+            } else if (d.type == kDeltaProjection) {
+                // ProjectionLight::I's RGBIlluminantSpectrum of the nearest pixel, per pixel
+                off = (int)dimg.size();
+                EnvLightDesc e;
+                e.res = 1;
+                e.rgb = d.img;
+                const size_t np = (size_t)d.imgW * d.imgH;
+                for (size_t q = 0; q < np; ++q) {
+                    e.rgb.assign(d.img.begin() + 3 * q, d.img.begin() + 3 * q + 3);
+                    const EnvCoef ec = BuildEnvCoefs(e)[0];
+                    dimg.insert(dimg.end(), {ec.c0, ec.c1, ec.c2, ec.s});
+                }
+            }
+            x.cone = make_float4(d.cosFalloffStart, d.cosFalloffEnd, BitsToFloat((uint32_t)d.spectrum),
+                                 BitsToFloat((uint32_t)off));
+            x.m0 = make_float4(d.m[0][0], d.m[0][1], d.m[0][2], BitsToFloat((uint32_t)d.imgW));
+            x.m1 = make_float4(d.m[1][0], d.m[1][1], d.m[1][2], BitsToFloat((uint32_t)d.imgH));
+            x.m2 = make_float4(d.m[2][0], d.m[2][1], d.m[2][2], d.invTanAng);
             dd.push_back(x);
         }
         c->deltaLights.Upload(dd);
+        c->deltaImg.Upload(dimg);
         c->uniformOrder.Upload(std::vector<int>(s.uniformOrder.begin(), s.uniformOrder.end()));
     }
     std::vector<float> dense;
@@ -1063,6 +1091,9 @@ static void BuildDevice(pbrt_context *c) {
     S.nDelta = (int)s.deltaLights.size();
     S.nPointSpot = s.nPointSpot;
     S.delta = c->deltaLights.p;
+    S.deltaImg = c->deltaImg.p;
+    S.nImageDelta = 0;
+    for (auto &d : s.deltaLights) S.nImageDelta += d.type == kDeltaGonio || d.type == kDeltaProjection;
     S.uniformOrder = c->uniformOrder.p;
     S.sceneRadius = s.sceneRadius;
     S.uniformLightSampler = s.uniformLightSampler ? 1 : 0;
@@ -1699,6 +1730,7 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
     f->n_delta_lights = (int)s.deltaLights.size();
     f->n_point_spot = s.nPointSpot;
     f->delta_lights = scene->deltaLights.data();
+    f->delta_images = scene->deltaImages.data();
     f->inf_distant = scene->infDistant.data();
     f->n_env = (int)scene->desc.envLights.size();
     f->inf_image = scene->infImage.data();

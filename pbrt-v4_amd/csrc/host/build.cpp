@@ -540,7 +540,13 @@ static void BuildLightBVH(SceneDesc &s) {
         LightBounds lb;
         lb.bounds.Add(d.p);
         lb.twoSided = false;
-        if (d.type == kDeltaPoint) {
+        if (d.type == kDeltaGonio || d.type == kDeltaProjection) {
+            // GoniometricLight::Bounds (an isotropic point) / ProjectionLight::Bounds, precomputed
+            lb.w = Normalize(d.w);
+            lb.phi = d.phi;
+            lb.cosTheta_o = d.cosFalloffStart;
+            lb.cosTheta_e = d.cosFalloffEnd;
+        } else if (d.type == kDeltaPoint) {
             lb.w = V3(0, 0, 1);
             lb.phi = 4 * kPi * d.scale * mx;
             lb.cosTheta_o = std::cos(kPi);

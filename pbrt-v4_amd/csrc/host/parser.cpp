@@ -357,6 +357,7 @@ class Parser {
     };
     std::vector<PendingLight> lights;
     InfiniteLightDesc InfiniteLight(PendingLight &l);
+    void ImageLight(PendingLight &l, const Mat4 &rfl, float sc, DeltaLightDesc *d);
     void DeltaLight(PendingLight &l, std::vector<DeltaLightDesc> &pointSpot, std::vector<DeltaLightDesc> &distants,
                     std::vector<int> &distantEntry, std::vector<std::pair<int, int>> &lsOrder);
     struct PendingMedium {
@@ -1726,7 +1727,8 @@ void Parser::Finish() {
     std::vector<DeltaLightDesc> pointSpot, distants;
     std::vector<int> distantEntry;  // infinite-list entry of each distant light
     for (PendingLight &l : lights) {
-        if (l.type == "point" || l.type == "spot" || l.type == "distant") {
+        if (l.type == "point" || l.type == "spot" || l.type == "distant" || l.type == "goniometric" ||
+            l.type == "projection") {
             DeltaLight(l, pointSpot, distants, distantEntry, lsOrder);
             continue;
         }
@@ -1833,14 +1835,97 @@ InfiniteLightDesc Parser::InfiniteLight(PendingLight &l) {
     return il;
 }
 
+// GoniometricLight::Create / ProjectionLight::Create (lights.cpp:448-518, 603-680) after the
+// photometric normalisation (sc): the image, "power", the render-space position and the
+// inverse of renderFromLight * swapYZ (goniometric) or * Scale(1, -1, 1) (projection), and
+// the LightBounds terms (lights.cpp:384-399, 563-575) the light BVH needs.
+void Parser::ImageLight(PendingLight &l, const Mat4 &rfl, float sc, DeltaLightDesc *d) {
+    ParamSet &ps = l.params;
+    const bool gonio = l.type == "goniometric";
+    std::string fn = ps.GetString("filename", "");
+    if (fn.empty())
+        throw Error(ps.loc + (gonio ? ": goniometric light without \"filename\" is not supported"
+                                    : ": Must provide \"filename\" to \"projection\" light source"));
+    if (fn[0] != '/' && !l.dir.empty()) fn = l.dir + "/" + fn;
+    LightImage im = LoadLightImage(fn, ps.loc);
+    for (float v : im.v) {
+        if (std::isinf(v)) throw Error(ps.loc + ": " + fn + ": image has infinite pixel values and so is not suitable as a light.");
+        if (std::isnan(v)) throw Error(ps.loc + ": " + fn + ": image has not-a-number pixel values and so is not suitable as a light.");
+    }
+    const size_t np = (size_t)im.w * im.h;
+    const Mat4 lfr = Inverse4(rfl);
+    d->p = V3((float)rfl[0][3], (float)rfl[1][3], (float)rfl[2][3]);  // renderFromLight(0, 0, 0)
+    d->imgW = im.w;
+    d->imgH = im.h;
+    const float phi_v = (float)ps.GetFloat("power", -1);
+    if (gonio) {
+        d->type = kDeltaGonio;
+        if (im.w != im.h)
+            throw Error(ps.loc + ": " + fn + ": image resolution (" + std::to_string(im.w) + ", " + std::to_string(im.h) +
+                        ") is non-square. It's unlikely this is an equal-area environment map.");
+        // the Y channel, or a "Y" image of the R, G, B average in the source's pixel format
+        d->img.resize(np);
+        if (im.nc >= 3) {
+            if (im.exr) throw Error(ps.loc + ": " + fn + ": RGB EXR images for goniometric lights are not supported yet");
+            for (size_t q = 0; q < np; ++q) {
+                const float *c = &im.v[q * im.nc];
+                d->img[q] = im.Restore((c[0] + c[1] + c[2]) / 3);
+            }
+        } else if (im.nc == 1) {
+            d->img = im.v;
+        } else {
+            throw Error(ps.loc + ": " + fn + ": has neither \"R\", \"G\", and \"B\" or \"Y\" channels.");
+        }
+        float sumY = 0;
+        for (float y : d->img) sumY += y;
+        if (phi_v > 0) sc *= phi_v / (4 * kPi * sumY / (float)np);
+        // renderFromLight * swapYZ: its inverse swaps rows y and z of lightFromRender
+        const int rows[3] = {0, 2, 1};
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) d->m[i][j] = (float)lfr[rows[i]][j];
+        d->w = V3(0, 0, 1);
+        d->cosFalloffStart = std::cos(kPi);
+        d->cosFalloffEnd = std::cos(kPi / 2);
+        const auto &dense = scene.denseSpectra[d->spectrum];
+        d->phi = sc * *std::max_element(dense.begin(), dense.end()) * 4 * kPi * sumY / (float)np;
+    } else {
+        d->type = kDeltaProjection;
+        if (im.nc < 3)
+            throw Error(ps.loc + ": " + fn + ": Image provided to \"projection\" light must have R, G, and B channels.");
+        if (phi_v > 0) throw Error(ps.loc + ": \"power\" for projection lights is not supported yet");
+        const float fov = (float)ps.GetFloat("fov", 90.);
+        d->invTanAng = 1 / std::tan((kPi / 180) * fov / 2);
+        d->img.resize(3 * np);
+        float sum = 0;
+        for (size_t q = 0; q < np; ++q) {
+            const float *c = &im.v[q * im.nc];
+            for (int k = 0; k < 3; ++k) d->img[3 * q + k] = c[k];
+            sum += std::max({c[0], c[1], c[2]});
+        }
+        // renderFromLight * Scale(1, -1, 1): its inverse negates row y of lightFromRender
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) d->m[i][j] = (float)((i == 1 ? -1 : 1) * lfr[i][j]);
+        d->w = Normalize(V3((float)rfl[0][2], (float)rfl[1][2], (float)rfl[2][2]));
+        // cosTotalWidth: the corner of screenBounds through lightFromScreen (approximated in
+        // double: the light BVH's importance only)
+        const float aspect = float(im.w) / float(im.h);
+        const double cx = aspect > 1 ? aspect : 1, cy = aspect > 1 ? 1 : 1 / aspect;
+        const double ex = cx / d->invTanAng, ey = cy / d->invTanAng;
+        d->cosFalloffStart = std::cos(0.f);
+        d->cosFalloffEnd = (float)(1 / std::sqrt(ex * ex + ey * ey + 1));
+        d->phi = sc * sum / (float)np;
+    }
+    d->scale = sc;
+}
+
 // PointLight::Create / SpotLight::Create / DistantLight::Create (lights.cpp:192-276,
 // 1464-1495): I or L as an illuminant spectrum, scale /= SpectrumToPhotometric, "power" (point,
 // spot) or "illuminance" (distant), and the render-space geometry of renderFromLight * t.
 void Parser::DeltaLight(PendingLight &l, std::vector<DeltaLightDesc> &pointSpot, std::vector<DeltaLightDesc> &distants,
                         std::vector<int> &distantEntry, std::vector<std::pair<int, int>> &lsOrder) {
     ParamSet &ps = l.params;
-    const bool distant = l.type == "distant";
-    Param *I = ps.Find(distant ? "L" : "I");
+    const bool distant = l.type == "distant", projection = l.type == "projection";
+    Param *I = projection ? nullptr : ps.Find(distant ? "L" : "I");
     std::array<float, 311> dense = GetSpectralData().denseD65;
     float photometric = GetSpectralData().photometricD65;
     if (I && I->type == "rgb" && I->nums.size() == 3) {
@@ -1908,6 +1993,9 @@ void Parser::DeltaLight(PendingLight &l, std::vector<DeltaLightDesc> &pointSpot,
             const float k_e = 2 * kPi * ((1 - d.cosFalloffStart) + (d.cosFalloffStart - d.cosFalloffEnd) / 2);
             sc *= phi_v / k_e;
         }
+    } else if (l.type == "goniometric" || projection) {
+        ImageLight(l, rfl, sc, &d);
+        sc = d.scale;
     } else {
         d.type = kDeltaDistant;
         const V3 from = point3("from", V3(0, 0, 0)), to = point3("to", V3(0, 0, 1));

@@ -220,15 +220,26 @@ struct EnvLightDesc {
 // PointLight / SpotLight / DistantLight (lights.h:200-300, 740-800; lights.cpp:192-276, 1376-1495)
 // in render space: deltaLights holds the point and spot lights first (light-BVH members, global
 // light index nAreaLights + i), then the distant lights (members of the infinite-light list)
-enum DeltaLightType { kDeltaPoint = 0, kDeltaSpot = 1, kDeltaDistant = 2 };
+// GoniometricLight / ProjectionLight (lights.h:300-404, lights.cpp:281-680) are point lights
+// whose intensity is an image lookup: they follow the point and spot lights in deltaLights.
+enum DeltaLightType { kDeltaPoint = 0, kDeltaSpot = 1, kDeltaDistant = 2, kDeltaGonio = 3, kDeltaProjection = 4 };
 struct DeltaLightDesc {
     int type = kDeltaPoint;
     V3 p;                 // point / spot: renderFromLight(0, 0, 0)
-    V3 w;                 // spot: Normalize(renderFromLight(0, 0, 1)); distant: renderFromLight(0, 0, 1)
-    float m[3][3] = {};   // spot: upper 3x3 of renderFromLight's inverse (Transform::ApplyInverse)
-    float cosFalloffStart = 1, cosFalloffEnd = 1;
-    int spectrum = -1;    // dense spectrum of I (point, spot) or L (distant)
+    V3 w;                 // spot, projection: Normalize(renderFromLight(0, 0, 1)); distant: renderFromLight(0, 0, 1)
+    float m[3][3] = {};   // spot, goniometric, projection: upper 3x3 of renderFromLight's inverse
+                          // (Transform::ApplyInverse; the swapYZ / flip-y of Create folded in)
+    float cosFalloffStart = 1, cosFalloffEnd = 1;  // spot; goniometric / projection: LightBounds'
+                                                   // cosTheta_o, cosTheta_e
+    int spectrum = -1;    // dense spectrum of I (point, spot, goniometric), L (distant), or the
+                          // image colour space's illuminant (projection)
     float scale = 1;      // final scale (photometric normalisation, power / illuminance applied)
+    // goniometric: the Y image (Image::GetChannel values, res x res, row 0 = top); projection:
+    // per pixel the RGBIlluminantSpectrum {c0, c1, c2, scale} of ClampZero(rgb)
+    std::vector<float> img;
+    int imgW = 0, imgH = 0;
+    float invTanAng = 1;  // projection: 1 / tan(Radians(fov) / 2) of screenFromLight
+    float phi = 0;        // goniometric / projection: LightBounds' phi (Bounds(), lights.cpp:384-399, 563-575)
 };
 
 struct CameraDesc {

@@ -575,6 +575,44 @@ ImageDesc LoadImageTexture(const std::string &filename, const std::string &encod
     return img;
 }
 
+LightImage LoadLightImage(const std::string &filename, const std::string &loc) {
+    LightImage li;
+    if (HasExt(filename, "exr")) {
+        Image im;
+        try {
+            im = ReadImage(filename);
+        } catch (const std::exception &e) {
+            throw Error(loc + ": " + e.what());
+        }
+        li.w = im.width;
+        li.h = im.height;
+        li.nc = 3;
+        li.exr = true;
+        li.v = std::move(im.rgb);
+        return li;
+    }
+    const Encoding enc = Encoding::Get("sRGB", loc);
+    RawImage raw;
+    if (HasExt(filename, "png")) raw = ReadPNG(filename, enc);
+    else if (HasExt(filename, "pfm")) raw = ReadPFM(filename);
+    else throw Error(loc + ": " + filename + ": only PNG, PFM and EXR light images are supported");
+    li.w = raw.w;
+    li.h = raw.h;
+    li.nc = raw.nc;
+    li.format = raw.format;
+    li.v.resize((size_t)raw.w * raw.h * raw.nc);
+    for (size_t i = 0; i < li.v.size(); ++i) li.v[i] = raw.Get(i, enc);
+    return li;
+}
+float LightImage::Restore(float v) const {
+    static const Encoding enc = Encoding::Get("sRGB", "");
+    switch (format) {
+    case kImgU8: return enc.ToLinear(enc.FromLinear(v));
+    case kImgHalf: return HalfToFloat(FloatToHalf(v));
+    default: return v;
+    }
+}
+
 EnvLightDesc LoadEnvironmentImage(const std::string &filename, const std::string &loc) {
     EnvLightDesc env;
     int w = 0, h = 0;

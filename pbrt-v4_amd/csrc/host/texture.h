@@ -35,6 +35,17 @@ float ImageTexel(const ImageDesc &img, int level, int x, int y, int c);
 // Image::Read + GetChannelDesc({"R", "G", "B"}) for an ImageInfiniteLight (lights.cpp:1600-1681):
 // PNG (sRGB encoding), PFM or EXR; linear values as Image::GetChannel returns them; square
 EnvLightDesc LoadEnvironmentImage(const std::string &filename, const std::string &loc);
+// Image::Read of a goniometric / projection light's image: every channel's linear value as
+// Image::GetChannel returns it ([h][w][nc], row 0 = top), and the stored pixel format
+struct LightImage {
+    int w = 0, h = 0, nc = 0;
+    int format = kImgFloat;
+    bool exr = false;
+    std::vector<float> v;
+    // a value stored into an image of this format and read back (Image::SetChannel + GetChannel)
+    float Restore(float v) const;
+};
+LightImage LoadLightImage(const std::string &filename, const std::string &loc);
 // lowers texture node `node` (scene.textures) to a two-phase device program; returns its index
 int CompileTexProgram(SceneDesc &s, int node, bool spectrum);
 // CameraBase::FindMinimumDifferentials and CameraFromRender (SceneDesc::minPosDx ...)

@@ -1155,17 +1155,20 @@ __device__ inline float LightPMF(const DeviceScene &S, V3 p, V3 ns, int light) {
 // PointLight / SpotLight / DistantLight::SampleLi (lights.h).  The sample's radiance at a
 // wavelength is scale * spectrum(lambda), divided by d2 for point and spot lights (pbrt's
 // SampledSpectrum / DistanceSquared); a UniformInfiniteLight returns no sample.
+// A GoniometricLight's image value multiplies scale * I(lambda) before the division (k; 1, an
+// exact no-op, for every other light); a ProjectionLight's pixel is an envLe sample.
 struct LiSample {
     V3 wi, lp, lpe, ln;  // direction, and the light point (error, normal) for SpawnRayTo
     float pdf;           // ls->pdf (1 for delta lights)
     float scale, d2;     // d2 = 1: no division
+    float k = 1;         // GoniometricLight: image(uv) (lights.h:393-396)
     int spectrum;
     bool delta;          // IsDeltaLight: the BSDF's MIS pdf is 0
-    bool envLe;          // ImageInfiniteLight: Le = EnvLe(env, scale, spectrum(lambda), lambda)
+    bool envLe;          // ImageInfiniteLight / ProjectionLight: Le = EnvLe(env, scale, spectrum(lambda), lambda)
     EnvCoef env;
-    // the radiance at one wavelength from the dense value of `spectrum` there
+    // the radiance at one wavelength from the dense value of `spectrum` there (before / d2)
     __device__ float Le(float denseVal, float lambda) const {
-        return envLe ? EnvLe(env, scale, denseVal, lambda) : scale * denseVal;
+        return (envLe ? EnvLe(env, scale, denseVal, lambda) : scale * denseVal) * k;
     }
 };
 // ImageInfiniteLight::SampleLi with allowIncompletePDF (lights.h:594-618): the compensated
@@ -1295,6 +1298,39 @@ __device__ inline bool SampleLiSurface(const DeviceScene &S, const DeviceAreaLig
         ls->lp = p;
         ls->d2 = DistanceSquared(p, cp);
         float sc = D.w.w;
+        if constexpr (Ext) {
+            if (type >= 3) {
+                // renderFromLight.ApplyInverse(-wi) (not normalised, as pbrt passes it)
+                const V3 v = -ls->wi;
+                const V3 wl(D.m0.x * v.x + D.m0.y * v.y + D.m0.z * v.z, D.m1.x * v.x + D.m1.y * v.y + D.m1.z * v.z,
+                            D.m2.x * v.x + D.m2.y * v.y + D.m2.z * v.z);
+                const int w = __float_as_int(D.m0.w), h = __float_as_int(D.m1.w);
+                const float *img = S.deltaImg + __float_as_int(D.cone.w);
+                ls->scale = sc;
+                if (type == 3) {
+                    // GoniometricLight::I: image.LookupNearestChannel(EqualAreaSphereToSquare(w), 0)
+                    float u, vv;
+                    EqualAreaSphereToSquare(wl, &u, &vv);
+                    const int x = min(max((int)(u * w), 0), w - 1), y = min(max((int)(vv * h), 0), h - 1);
+                    ls->k = img[(size_t)y * w + x];
+                    return true;
+                }
+                // ProjectionLight::I (lights.cpp:343-360): behind the hither plane or outside the
+                // screen window nothing; else the nearest pixel's RGBIlluminantSpectrum
+                if (wl.z < 1e-3f) return false;
+                const float s = D.m2.w, aspect = float(w) / float(h);
+                const float bx = aspect > 1 ? aspect : 1.f, by = aspect > 1 ? 1.f : 1 / aspect;
+                // screenFromLight(Point3f(w)) = Perspective(fov, 1e-3, 1e30): x = s wx / wz, y = s wy / wz
+                const float psx = (s * wl.x) / wl.z, psy = (s * wl.y) / wl.z;
+                if (!(psx >= -bx && psx <= bx && psy >= -by && psy <= by)) return false;
+                const float u = (psx - -bx) / (bx - -bx), vv = (psy - -by) / (by - -by);
+                const int x = min(max((int)(u * w), 0), w - 1), y = min(max((int)(vv * h), 0), h - 1);
+                const float4 c = reinterpret_cast<const float4 *>(img + 4)[(size_t)y * w + x];
+                ls->envLe = true;
+                ls->env = EnvCoef{c.x, c.y, c.z, c.w};
+                return true;
+            }
+        }
         if (type == 1) {  // SpotLight::I: SmoothStep(CosTheta(wLight), cosEnd, cosStart) * scale
             const V3 v = -ls->wi;
             const V3 wl = Normalize(V3(D.m0.x * v.x + D.m0.y * v.y + D.m0.z * v.z,

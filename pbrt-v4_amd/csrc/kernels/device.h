@@ -104,6 +104,9 @@ struct DeviceMedia {
 // (.w type bits: 0 point, 1 spot, 2 distant), w.xyz spot axis or direction toward a distant
 // light (.w scale), cone = cosFalloffStart, cosFalloffEnd, spectrum bits; m0..m2: rows of
 // renderFromLight's inverse 3x3 (spot, Transform::ApplyInverse on vectors)
+// p.w: type bits; w.w: scale; cone: cosFalloffStart, cosFalloffEnd, spectrum bits, offset of the
+// goniometric / projection image in DeviceScene::deltaImg (int bits); m0..m2: rows of
+// renderFromLight^-1, .w: image width / height bits, projection 1 / tan(fov / 2)
 struct DeviceDeltaLight {
     float4 p, w, cone, m0, m1, m2;
 };
@@ -176,6 +179,8 @@ struct DeviceScene {
     // index nAreaLights + i; the infinite-list entry j has global index nAreaLights + nPointSpot + j
     int nDelta, nPointSpot;
     const DeviceDeltaLight *delta;
+    const float *deltaImg;  // goniometric Y images and projection per-pixel EnvCoef
+    int nImageDelta;        // goniometric + projection lights (their kernels are the Ext ones)
     const int *uniformOrder;  // UniformLightSampler: pbrt's light order -> global index
     float sceneRadius;
     // light sampler

@@ -1058,12 +1058,12 @@ struct AreaLightHit {
     int spectrum;
     float d2, rd2;
     bool d2Ok, delta;
-    bool envLe;  // ImageInfiniteLight: the pixel's RGBIlluminantSpectrum (EnvLe)
+    bool envLe;  // ImageInfiniteLight / ProjectionLight: the pixel's RGBIlluminantSpectrum (EnvLe)
     EnvCoef env;
+    float k;     // GoniometricLight: the image value (1 otherwise)
     __device__ float Le(const DeviceScene &S, int off, float lam) const {
         const float dv = DenseAt(S, spectrum, off);
-        if (envLe) return EnvLe(env, scale, dv, lam);
-        const float v = scale * dv;
+        const float v = (envLe ? EnvLe(env, scale, dv, lam) : scale * dv) * k;
         return delta ? DivByRcp(v, d2, rd2, d2Ok) : v;
     }
 };
@@ -1089,6 +1089,7 @@ __device__ inline bool SampleAreaLightAt(const DeviceScene &S, V3 refP, V3 refN,
         out->delta = ls.delta;
         out->envLe = ls.envLe;
         out->env = ls.env;
+        out->k = ls.k;
         bool nz = false;
         SpectralIter it(lambda0);
 #pragma unroll 1
@@ -1122,6 +1123,7 @@ __device__ inline bool SampleAreaLightAt(const DeviceScene &S, V3 refP, V3 refN,
     out->d2Ok = true;
     out->delta = false;
     out->envLe = false;
+    out->k = 1;
     return true;
 }
 
@@ -2337,7 +2339,7 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
         hipLaunchKernelGGL(k_queue_holes, dim3(64, kShards), block, 0, s, st.counters, wf, kVShadow, v.shPixel,      \
                            st.capS, QueueHoleCounter(), v, st.NR, stage);
     // Ext: analytic shapes or image lights in the scene (their paths compiled in)
-    if (S.nShapes > 0 || S.nEnv > 0) {
+    if (S.nShapes > 0 || S.nEnv > 0 || S.nImageDelta > 0) {
         if (S.matTypeMask & other) hipLaunchKernelGGL((k_vsurface<false, true>), gW, block, surfLds, s, S, st, v, wf);
         else hipLaunchKernelGGL((k_vsurface<true, true>), gW, block, surfLds, s, S, st, v, wf);
         QUEUE_CHECK(1);

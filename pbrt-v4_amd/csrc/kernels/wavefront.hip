@@ -544,7 +544,7 @@ __device__ inline void ShadeSpectralPass(int depth, const FD *dense, const Senso
                                          float lambda0, float scale, float d2, float rd2, bool d2Ok,
                                          float absdotL, float invDenom, float absdotB, float pdf, float rpdf,
                                          bool pdfOk, float etaScale, SensorAcc *acc, bool *neeNz, bool *betaNz,
-                                         float *mx, bool envLe = false, EnvCoef ec = EnvCoef{}) {
+                                         float *mx, bool envLe = false, EnvCoef ec = EnvCoef{}, float k = 1) {
     const float avgRu = Avg31(1.f);
     bool nzL = false, nzB = false;
     float m = -kInfinity;
@@ -557,6 +557,7 @@ __device__ inline void ShadeSpectralPass(int depth, const FD *dense, const Senso
         float Le = scale * dv;
         if constexpr (Env) {
             if (envLe) Le = EnvLe(ec, scale, dv, it.lam);
+            Le = Le * k;  // GoniometricLight's image value (1 otherwise)
         }
         if constexpr (DivD2) Le = DivByRcp(Le, d2, rd2, d2Ok);
         nzL |= Le != 0;
@@ -815,7 +816,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                 bool nee = false, envLe = false;
                 EnvCoef envC{};
                 int spec = 0;
-                float scale = 0, absdotL = 0, invDenom = 0, d2 = 1;
+                float scale = 0, absdotL = 0, invDenom = 0, d2 = 1, lk = 1;
                 if (Rnz) {
                     V3 cp = OffsetRayOrigin(pi, pe, n, wo);  // reflective, not transmissive
                     int li;
@@ -833,6 +834,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                             if constexpr (!Lean && Ext) {
                                 envLe = ls.envLe;
                                 envC = ls.env;
+                                lk = ls.k;
                             }
                             spec = ls.spectrum;
                             scale = ls.scale;
@@ -893,11 +895,11 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                         ShadeSpectralPass<true, !Lean && Ext>(depth, (const LdsF *)denseLds + spec * kDenseN, sensorL, bf,
                                                        rfun, lambda0, scale, d2, rd2, d2Ok, absdotL, invDenom,
                                                        absdotB, pdf, rpdf, pdfOk, etaScale, &acc, &neeNz, &betaNz,
-                                                       &mx, envLe, envC);
+                                                       &mx, envLe, envC, lk);
                     else
                         ShadeSpectralPass<true, !Lean && Ext>(depth, S.dense + spec * kDenseN, sensorL, bf, rfun, lambda0,
                                                        scale, d2, rd2, d2Ok, absdotL, invDenom, absdotB, pdf, rpdf,
-                                                       pdfOk, etaScale, &acc, &neeNz, &betaNz, &mx, envLe, envC);
+                                                       pdfOk, etaScale, &acc, &neeNz, &betaNz, &mx, envLe, envC, lk);
                 }
                 SEC_MARK(st, 5);
                 if (nee && neeNz) {
@@ -1663,7 +1665,7 @@ hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int dep
                               hipStream_t s) {
     const dim3 grid(ShadeGridFor(maxCount)), block(kBlock);
     const size_t lds = ShadeLdsBytes(S, depth);
-    const bool ext = S.nShapes > 0 || S.nEnv > 0;
+    const bool ext = S.nShapes > 0 || S.nEnv > 0 || S.nImageDelta > 0;
     if (S.textured && ext) hipLaunchKernelGGL((k_shade_diffuse<false, true, true>), grid, block, lds, s, S, st, depth);
     else if (S.textured) hipLaunchKernelGGL((k_shade_diffuse<false, true>), grid, block, lds, s, S, st, depth);
     else if (lean) hipLaunchKernelGGL(k_shade_diffuse<true>, grid, block, lds, s, S, st, depth);
@@ -1675,7 +1677,7 @@ hipError_t LaunchShadeMicrofacet(const DeviceScene &S, const PathState &st, int 
                                  hipStream_t s) {
     const dim3 grid(ShadeGridFor(maxCount)), block(kBlock);
     const size_t lds = ShadeLdsBytes(S, depth, true);
-    const bool ext = S.nShapes > 0 || S.nEnv > 0, diel = type == kMatDielectricT;
+    const bool ext = S.nShapes > 0 || S.nEnv > 0 || S.nImageDelta > 0, diel = type == kMatDielectricT;
 #define K_MF(mt, smooth, tex, ex) hipLaunchKernelGGL((k_shade_microfacet<mt, smooth, tex, ex>), grid, block, lds, s, S, st, depth)
     if (ext) {
         if (diel && S.textured) K_MF(kMatDielectricT, false, true, true);

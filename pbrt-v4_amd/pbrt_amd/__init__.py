@@ -76,7 +76,7 @@ class SceneFlat(ctypes.Structure):
         ("filter_type", ctypes.c_int), ("filter_a", ctypes.c_float), ("filter_b", ctypes.c_float),
         ("material_layer", ctypes.POINTER(ctypes.c_float)),
         ("n_delta_lights", ctypes.c_int), ("n_point_spot", ctypes.c_int),
-        ("delta_lights", ctypes.POINTER(ctypes.c_float)), ("inf_distant", ctypes.POINTER(ctypes.c_int32)),
+        ("delta_lights", ctypes.POINTER(ctypes.c_float)), ("delta_images", ctypes.POINTER(ctypes.c_float)), ("inf_distant", ctypes.POINTER(ctypes.c_int32)),
         ("uniform_order", ctypes.POINTER(ctypes.c_int32)), ("scene_radius", ctypes.c_float),
         ("n_tex_nodes", ctypes.c_int), ("n_images", ctypes.c_int),
         ("tex_node_info", ctypes.POINTER(ctypes.c_int32)), ("tex_node_params", ctypes.POINTER(ctypes.c_float)),

@@ -64,6 +64,9 @@ typedef struct pbrt_scene_flat {
     const float *light_scale;
     const int32_t *light_spectrum;
     const int32_t *light_two_sided;
+    /* [n_area_lights][3]: the fork's "spread" (lights.cpp:715-717): cosFalloffEnd (> 0 only for a
+     * spread below 90 degrees), tanFalloffEnd, normalize_falloffEnd */
+    const float *light_spread;
     const int32_t *inf_spectrum;  /* [n_infinite_lights] */
     const float *inf_scale;
     const float *dense_spectra;   /* [n_spectra][311] at 395..705 nm */

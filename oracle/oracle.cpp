@@ -4266,6 +4266,27 @@ struct Renderer {
         const float *dense = f->dense_spectra + 311 * f->light_spectrum[li];
         return SampleDense(dense, lambda) * f->light_scale[li];
     }
+    // DiffuseAreaLight::L (lights.h:443-470) leaving along w at a point with normal n: zero on the
+    // back of a one-sided emitter and, with this fork's spread, outside the cone
+    // AbsDot(w, n) >= cosFalloffEnd
+    Spectrum AreaL(int li, Vec n, Vec w, const Wavelengths &lambda) const {
+        if (!(f->light_two_sided[li] || DotN(n, w) >= 0)) return Spectrum(0.f);
+        const float cosE = f->light_spread ? f->light_spread[3 * li] : -1;
+        if (cosE > 0 && std::abs(DotN(n, w)) < cosE) return Spectrum(0.f);
+        return LightL(li, lambda);
+    }
+    // DiffuseAreaLight::SampleLi's spread attenuation (lights.cpp:763-771) toward wi
+    Spectrum SampledAreaL(int li, Vec n, Vec wi, const Wavelengths &lambda) const {
+        Spectrum Le = AreaL(li, n, -wi, lambda);
+        const float *sp = f->light_spread ? f->light_spread + 3 * li : nullptr;
+        if (sp && sp[0] > 0) {
+            const Float cos_a = -DotN(n, wi);
+            const Float sin_a = SafeSqrt(1 - Sqr(cos_a));
+            const Float tan_a = sin_a / cos_a;
+            Le = Le * std::max((1.0f - (sp[1] * tan_a)) * sp[2], 0.0f);
+        }
+        return Le;
+    }
     // PointLight / SpotLight / DistantLight::SampleLi (lights.h:221-228, 282-289, 784-798) for a
     // global light index past the area lights; false for a UniformInfiniteLight (SampleLi with
     // allowIncompletePDF returns nothing) and for a spot light whose Li vanishes.
@@ -4702,8 +4723,7 @@ struct Renderer {
                         if (sampleArea(li, pS, Vec(0, 0, 0), Vec(0, 0, 0), Vec(0, 0, 0), dU0, dU1, &ss) &&
                             ss.pdf != 0 && LengthSquared(ss.p - pS) != 0) {
                             Vec wi = Normalize(ss.p - pS);
-                            Spectrum Le(0.f);
-                            if (f->light_two_sided[li] || DotN(ss.n, -wi) >= 0) Le = LightL(li, lambda);
+                            const Spectrum Le = SampledAreaL(li, ss.n, wi, lambda);
                             if (Le) {
                                 Float ph = HenyeyGreenstein(Dot(wo, wi), g);
                                 Spectrum b2 = beta * ph;
@@ -4777,8 +4797,8 @@ struct Renderer {
             }
             // HandleEmissiveIntersection
             int light = S.Light(prim);
-            if (light >= 0 && (f->light_two_sided[light] || DotN(si.n, si.wo) >= 0)) {
-                Spectrum Le = LightL(light, lambda);
+            if (light >= 0) {
+                const Spectrum Le = AreaL(light, si.n, si.wo, lambda);
                 if (Le) {
                     if (depth == 0 || specularBounce) L = L + beta * Le / r_u.Average();
                     else {
@@ -4876,8 +4896,7 @@ struct Renderer {
                     if (sampleArea(li, cp, cpErr, si.n, si.ns, dU0, dU1, &ss) && ss.pdf != 0 &&
                         LengthSquared(ss.p - cp) != 0) {
                         Vec wi = Normalize(ss.p - cp);
-                        Spectrum Le(0.f);
-                        if (f->light_two_sided[li] || DotN(ss.n, -wi) >= 0) Le = LightL(li, lambda);
+                        const Spectrum Le = SampledAreaL(li, ss.n, wi, lambda);
                         if (Le) {
                             Vec wiL = toLocal(wi);
                             Spectrum fv = woL.z == 0 ? Spectrum(0.f)  // BSDF::f (bsdf.h:60-70)
@@ -4974,8 +4993,8 @@ struct Renderer {
             Interaction si = S.Interact(prim, ti, rd);
             // emission at the hit (SurfaceInteraction::Le -> DiffuseAreaLight::L)
             const int light = S.Light(prim);
-            if (light >= 0 && (f->light_two_sided[light] || DotN(si.n, si.wo) >= 0)) {
-                const Spectrum Le = LightL(light, lambda);
+            if (light >= 0) {
+                const Spectrum Le = AreaL(light, si.n, si.wo, lambda);
                 if (Le) {
                     if (depth == 0 || specularBounce) L = L + beta * Le;
                     else {
@@ -5060,7 +5079,7 @@ struct Renderer {
                                              S.Attr(lp));
                         if (ok && ss.pdf != 0 && LengthSquared(ss.p - cp) != 0) {
                             wi = Normalize(ss.p - cp);
-                            if (f->light_two_sided[li] || DotN(ss.n, -wi) >= 0) Le = LightL(li, lambda);
+                            Le = SampledAreaL(li, ss.n, wi, lambda);
                             pdf = ss.pdf;
                             pf = OffsetRayOrigin(si.p, si.err, si.n, ss.p - si.p);
                             pt = OffsetRayOrigin(ss.p, ss.err, ss.n, pf - ss.p);

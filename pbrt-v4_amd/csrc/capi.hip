@@ -255,7 +255,7 @@ struct pbrt_scene {
     std::vector<int32_t> mediumInfo;
     std::vector<int32_t> tris, lightPrim, lightSpectrum, lightTwoSided, infSpectrum, matConstant, nodeInfo, matType,
         matSpectra, plOffsets, infDistant, uniformOrder;
-    std::vector<float> deltaLights, deltaImages;
+    std::vector<float> deltaLights, deltaImages, lightSpread;
     std::vector<int32_t> infImage, envInfo, shapeInfo, primAlpha;
     std::vector<float> shapeParams, shapeNormals;
     std::vector<float> envXform, envRgb;
@@ -328,11 +328,13 @@ struct pbrt_scene {
         lightScale.clear();
         lightSpectrum.clear();
         lightTwoSided.clear();
+        lightSpread.clear();
         for (auto &l : s.areaLights) {
             lightPrim.push_back(l.shape >= 0 ? (int32_t)s.tris.size() + l.shape : l.prim);
             lightScale.push_back(l.scale);
             lightSpectrum.push_back(l.spectrum);
             lightTwoSided.push_back(l.twoSided ? 1 : 0);
+            lightSpread.insert(lightSpread.end(), {l.cosFalloffEnd, l.tanFalloffEnd, l.normFalloffEnd});
         }
         infSpectrum.clear();
         infScale.clear();
@@ -416,6 +418,8 @@ struct pbrt_context {
     DevBuf<int> primMaterial, primLight, matConstant, lightPrim, lightSpectrum, lightTwoSided, infSpectrum, infDistant,
         uniformOrder;
     DevBuf<DeviceDeltaLight> deltaLights;
+    DevBuf<float> lightSpreadNorm;  // per area light: normalize_falloffEnd of its spread
+    bool hasSpread = false;
     DevBuf<float> deltaImg;
     DevBuf<int> primOrig, matType, matSpectra, plOffsets;
     DevBuf<float> matParams, plLambda, plValue, triShade, matLayer, dispL0;
@@ -748,6 +752,8 @@ static void BuildDevice(pbrt_context *c) {
             float bits;
             memcpy(&bits, &prim, 4);
             d.v0 = make_float4(0.f, 0.f, 0.f, bits);
+            d.v1 = make_float4(0.f, 0.f, 0.f, l.cosFalloffEnd);
+            d.v2 = make_float4(0.f, 0.f, 0.f, l.tanFalloffEnd);
             d.scale = l.scale;
             d.spectrum = l.spectrum;
             d.twoSided = l.twoSided;
@@ -759,8 +765,8 @@ static void BuildDevice(pbrt_context *c) {
         float leafBits;  // .w: the light's leaf prim (its shading data), as int bits
         memcpy(&leafBits, &leaf, 4);
         d.v0 = make_float4(v[0], v[1], v[2], leafBits);
-        d.v1 = make_float4(v[4], v[5], v[6], 0.f);
-        d.v2 = make_float4(v[8], v[9], v[10], 0.f);
+        d.v1 = make_float4(v[4], v[5], v[6], l.cosFalloffEnd);
+        d.v2 = make_float4(v[8], v[9], v[10], l.tanFalloffEnd);
         d.scale = l.scale;
         d.spectrum = l.spectrum;
         d.twoSided = l.twoSided;
@@ -768,6 +774,15 @@ static void BuildDevice(pbrt_context *c) {
         dl.push_back(d);
     }
     c->lights.Upload(dl);
+    {
+        std::vector<float> norm;
+        c->hasSpread = false;
+        for (const AreaLightDesc &l : s.areaLights) {
+            norm.push_back(l.normFalloffEnd);
+            c->hasSpread = c->hasSpread || l.cosFalloffEnd > 0;
+        }
+        c->lightSpreadNorm.Upload(norm);
+    }
     std::vector<int> is;
     std::vector<float> isc;
     for (auto &l : s.infiniteLights) {
@@ -1078,6 +1093,8 @@ static void BuildDevice(pbrt_context *c) {
     S.lightScale = c->lightScale.p;
     S.lightSpectrum = c->lightSpectrum.p;
     S.lightTwoSided = c->lightTwoSided.p;
+    S.lightSpreadNorm = c->lightSpreadNorm.p;
+    S.hasSpread = c->hasSpread ? 1 : 0;
     S.lightArea = c->lightArea.p;
     S.lights = c->lights.p;
     S.lightBitTrail = c->lightBitTrail.p;
@@ -1547,7 +1564,8 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
             const bool lean = !noLean && c->S.samplerType == 0 &&
                               (uint64_t)(st.firstSample + nS) * haltonStride <= (1ull << 24) &&
                               c->S.shadeLds.lightsInLds && c->S.shadeLds.denseInLds && c->S.triShade == nullptr &&
-                              c->S.nDelta == 0 && c->S.nEnv == 0 && c->S.nShapes == 0 && !c->S.textured && !c->hasMix;
+                              c->S.nDelta == 0 && c->S.nEnv == 0 && c->S.nShapes == 0 && !c->S.textured && !c->hasMix &&
+                              !c->S.hasSpread;
             for (int depth = 0; depth <= s.maxDepth; ++depth) {
                 // closest-hit launches are event-timed in the first pass of a render only: the
                 // passes are statistically identical and each event pair costs a queue gap
@@ -1725,6 +1743,7 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
     f->light_scale = scene->lightScale.data();
     f->light_spectrum = scene->lightSpectrum.data();
     f->light_two_sided = scene->lightTwoSided.data();
+    f->light_spread = scene->lightSpread.data();
     f->inf_spectrum = scene->infSpectrum.data();
     f->inf_scale = scene->infScale.data();
     f->n_delta_lights = (int)s.deltaLights.size();

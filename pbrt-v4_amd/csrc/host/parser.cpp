@@ -358,6 +358,12 @@ class Parser {
     std::vector<PendingLight> lights;
     InfiniteLightDesc InfiniteLight(PendingLight &l);
     void ImageLight(PendingLight &l, const Mat4 &rfl, float sc, DeltaLightDesc *d);
+    AreaLightDesc curSpread;  // the current AreaLightSource's spread terms
+    void SetSpread(AreaLightDesc *l) const {
+        l->cosFalloffEnd = curSpread.cosFalloffEnd;
+        l->tanFalloffEnd = curSpread.tanFalloffEnd;
+        l->normFalloffEnd = curSpread.normFalloffEnd;
+    }
     void DeltaLight(PendingLight &l, std::vector<DeltaLightDesc> &pointSpot, std::vector<DeltaLightDesc> &distants,
                     std::vector<int> &distantEntry, std::vector<std::pair<int, int>> &lsOrder);
     struct PendingMedium {
@@ -1116,6 +1122,7 @@ class Parser {
         }
         if (lightSpectrum >= 0) {
             AreaLightDesc l;
+                SetSpread(&l);
             l.shape = (int)scene.shapes.size();
             l.spectrum = lightSpectrum;
             l.scale = lightScale;
@@ -1197,6 +1204,7 @@ class Parser {
             }
             if (lightSpectrum >= 0) {
                 AreaLightDesc l;
+                SetSpread(&l);
                 l.shape = (int)scene.shapes.size();
                 l.spectrum = lightSpectrum;
                 l.scale = lightScale;
@@ -1658,8 +1666,15 @@ void Parser::Finish() {
             // lights.cpp:941: scale /= SpectrumToPhotometric(L) (illuminant part only)
             lightScale /= photometric;
             power = (float)ap.GetFloat("power", -1);  // applied per triangle below
-            float spread = (float)ap.GetFloat("spread", 90);
-            if (spread != 90) throw Error(ap.loc + ": \"spread\" other than 90 not supported yet");
+            // DiffuseAreaLight's spread angle (lights.cpp:715-717): emission only within the
+            // cone about the normal, SampleLi attenuated by the falloff (lights.cpp:763-771)
+            {
+                const float spread = (float)ap.GetFloat("spread", 90);
+                const float rad = (kPi / 180) * spread;
+                curSpread.cosFalloffEnd = std::cos(rad);
+                curSpread.tanFalloffEnd = std::tan((kPi / 2 - rad));
+                curSpread.normFalloffEnd = 2.0f / (2.0f + (2.0f * (kPi / 2 - rad) - kPi) * curSpread.tanFalloffEnd);
+            }
             // lights.cpp:909-939: an image-textured emitter ("filename") emits the image and
             // folds its average luminance into k_e; neither is on this path, so it is refused
             // rather than rendered with the default illuminant.
@@ -1700,6 +1715,7 @@ void Parser::Finish() {
                 scene.triMedium.push_back({(int16_t)mediumOf(s.insideMedium, s.loc), (int16_t)mediumOf(s.outsideMedium, s.loc)});
             if (lightSpectrum >= 0) {
                 AreaLightDesc l;
+                SetSpread(&l);
                 l.prim = triIndex;
                 l.spectrum = lightSpectrum;
                 l.scale = lightScale;

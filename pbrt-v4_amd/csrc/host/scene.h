@@ -179,6 +179,10 @@ struct AreaLightDesc {
     float scale = 1;        // final DiffuseAreaLight::scale (lights.cpp:941-966)
     bool twoSided = false;
     float area = 0;
+    // this fork's "spread" (lights.cpp:907-908, lights.h:451-458, 763-771): cosFalloffEnd =
+    // cos(Radians(spread)) (> 0 only below 90 degrees), tanFalloffEnd = tan(Pi / 2 -
+    // Radians(spread)), normalize_falloffEnd, all as the constructor computes them in float
+    float cosFalloffEnd = -1, tanFalloffEnd = 0, normFalloffEnd = 0;
 };
 
 // Sphere / Disk / BilinearPatch (shapes.h:106-571, 1272-1540) in render space: the device record (affine render-from-object

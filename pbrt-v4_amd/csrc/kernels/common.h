@@ -1211,19 +1211,37 @@ __device__ inline float SmoothStepf(float x, float a, float b) {
     const float t = Clampf((x - a) / (b - a), 0, 1);
     return t * t * (3 - 2 * t);
 }
+// This fork's DiffuseAreaLight spread (lights.h:451-458, lights.cpp:763-771).  cosE =
+// cosFalloffEnd, > 0 only for a spread below 90 degrees.  L() is zero where the emission
+// direction w leaves farther than the spread from the normal: AbsDot(w, n) < cosE.
+__device__ inline bool SpreadCut(float cosE, V3 n, V3 w) { return cosE > 0 && AbsDotN(n, w) < cosE; }
+// SampleLi's falloff factor on the light sample toward wi (cosE > 0), std::max(x, 0) as written
+__device__ inline float SpreadFactor(float tanE, float norm, V3 n, V3 wi) {
+    const float cos_a = -DotN(n, wi);
+    const float sin_a = SafeSqrt(1 - Sqr(cos_a));
+    const float tan_a = sin_a / cos_a;
+    const float f = (1.0f - (tanE * tan_a)) * norm;
+    return f < 0.0f ? 0.0f : f;
+}
 // Inl: the spherical-triangle sampling inlined (the diffuse kernels) or called out of line
 // DiffuseAreaLight::SampleLi over a sphere or disk (lights.cpp:743-775 with Shape::Sample(ctx,
 // u)): ctx = (cp, cpErr, n)
 // k: the shape's index (its prim id - nTris)
 __device__ __attribute__((noinline)) bool SampleShapeLi(const DeviceShape *shapes, const float *shapeN, int k,
                                                        bool twoSided, float scale, int spectrum, V3 cp, V3 cpErr, V3 n,
-                                                       V3 ns, float u0, float u1, LiSample *ls) {
+                                                       V3 ns, float u0, float u1, LiSample *ls, float cosE = -1,
+                                                       float tanE = 0, float spreadNorm = 0) {
     ShapeSamplePt ss;
     if (!ShapeSampleSolidAngle(shapes[k], cp, cpErr, n, u0, u1, &ss, shapeN + 12 * (size_t)k, ns) || ss.pdf == 0 ||
         LengthSquared(ss.p - cp) == 0)
         return false;
     ls->wi = Normalize(ss.p - cp);
     if (!(twoSided || DotN(ss.n, -ls->wi) >= 0)) return false;  // DiffuseAreaLight::L is 0
+    if (cosE > 0) {
+        if (SpreadCut(cosE, ss.n, -ls->wi)) return false;
+        ls->k = SpreadFactor(tanE, spreadNorm, ss.n, ls->wi);
+        if (ls->k == 0) return false;  // Le *= 0: no sample
+    }
     ls->lp = ss.p;
     ls->lpe = ss.pErr;
     ls->ln = ss.n;
@@ -1245,7 +1263,8 @@ __device__ inline bool SampleLiSurface(const DeviceScene &S, const DeviceAreaLig
         if constexpr (!Lean && Ext) {
             if (S.nShapes > 0 && __float_as_int(Ld.v0.w) >= S.nTris)
                 return SampleShapeLi(S.shapes, S.shapeN, __float_as_int(Ld.v0.w) - S.nTris, Ld.twoSided, Ld.scale,
-                                     Ld.spectrum, cp, cpErr, n, ns, u0, u1, ls);
+                                     Ld.spectrum, cp, cpErr, n, ns, u0, u1, ls, Ld.v1.w, Ld.v2.w,
+                                     Ld.v1.w > 0 ? S.lightSpreadNorm[li] : 0.f);
         }
         V3 q0(Ld.v0.x, Ld.v0.y, Ld.v0.z), q1(Ld.v1.x, Ld.v1.y, Ld.v1.z), q2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
         TriShading lsh;
@@ -1257,6 +1276,13 @@ __device__ inline bool SampleLiSurface(const DeviceScene &S, const DeviceAreaLig
             return false;
         ls->wi = Normalize(ls->lp - cp);
         if (!(Ld.twoSided || DotN(ls->ln, -ls->wi) >= 0)) return false;  // DiffuseAreaLight::L is 0
+        if constexpr (!Lean) {
+            if (Ld.v1.w > 0) {  // spread below 90 degrees
+                if (SpreadCut(Ld.v1.w, ls->ln, -ls->wi)) return false;
+                ls->k = SpreadFactor(Ld.v2.w, S.lightSpreadNorm[li], ls->ln, ls->wi);
+                if (ls->k == 0) return false;
+            }
+        }
         ls->pdf = lpdf;
         ls->scale = Ld.scale;
         ls->d2 = 1;

@@ -28,7 +28,8 @@ struct DeviceLightNode {
 // One area light (a triangle of a DiffuseAreaLight shape) as the light-sampling code reads it:
 // the triangle's vertices and the light's parameters in one 64-byte record.
 struct DeviceAreaLight {
-    float4 v0, v1, v2;  // render-space vertices (.w unused)
+    float4 v0, v1, v2;  // render-space vertices; v0.w: prim bits; v1.w / v2.w: the spread's
+                        // cosFalloffEnd (> 0: a spread below 90 degrees) / tanFalloffEnd
     float scale;
     int spectrum, twoSided, flip;
 };
@@ -180,6 +181,8 @@ struct DeviceScene {
     int nDelta, nPointSpot;
     const DeviceDeltaLight *delta;
     const float *deltaImg;  // goniometric Y images and projection per-pixel EnvCoef
+    const float *lightSpreadNorm;  // per area light: the spread's normalize_falloffEnd
+    int hasSpread;                 // some area light has a spread below 90 degrees
     int nImageDelta;        // goniometric + projection lights (their kernels are the Ext ones)
     const int *uniformOrder;  // UniformLightSampler: pbrt's light order -> global index
     float sceneRadius;

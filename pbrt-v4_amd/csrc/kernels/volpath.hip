@@ -1007,10 +1007,12 @@ __device__ inline bool SampleAreaLight(const DeviceScene &S, V3 refP, V3 refN, V
         return false;
     const V3 wi = Normalize(lp - refP);
     bool nz = false;
-    const bool facing = Ld.twoSided || DotN(ln, -wi) >= 0;
+    const bool facing = (Ld.twoSided || DotN(ln, -wi) >= 0) && !SpreadCut(Ld.v1.w, ln, -wi);
+    // the spread's falloff multiplies L (lights.cpp:763-771); 1 without a spread
+    const float k = Ld.v1.w > 0 ? SpreadFactor(Ld.v2.w, S.lightSpreadNorm[li], ln, wi) : 1.f;
 #pragma unroll
     for (int i = 0; i < kNS; ++i) {
-        Le[i] = facing ? Ld.scale * DenseAt(S, Ld.spectrum, wo.off[i]) : 0.f;
+        Le[i] = facing ? (Ld.scale * DenseAt(S, Ld.spectrum, wo.off[i])) * k : 0.f;
         nz |= Le[i] != 0;
     }
     if (!nz) return false;
@@ -1107,10 +1109,12 @@ __device__ inline bool SampleAreaLightAt(const DeviceScene &S, V3 refP, V3 refN,
         return false;
     const V3 wi = Normalize(lp - refP);
     if (!(Ld.twoSided || DotN(ln, -wi) >= 0)) return false;  // L() = 0 on the back side
+    if (SpreadCut(Ld.v1.w, ln, -wi)) return false;            // outside the spread
+    const float k = Ld.v1.w > 0 ? SpreadFactor(Ld.v2.w, S.lightSpreadNorm[li], ln, wi) : 1.f;
     bool nz = false;
     SpectralIter it(lambda0);
 #pragma unroll 1
-    for (int i = 0; i < kNS; ++i, it.Next()) nz |= Ld.scale * DenseAt(S, Ld.spectrum, DenseOffset(it.lam)) != 0;
+    for (int i = 0; i < kNS; ++i, it.Next()) nz |= (Ld.scale * DenseAt(S, Ld.spectrum, DenseOffset(it.lam))) * k != 0;
     if (!nz) return false;
     out->p = lp;
     out->pErr = lpe;
@@ -1123,7 +1127,7 @@ __device__ inline bool SampleAreaLightAt(const DeviceScene &S, V3 refP, V3 refN,
     out->d2Ok = true;
     out->delta = false;
     out->envLe = false;
-    out->k = 1;
+    out->k = k;
     return true;
 }
 
@@ -1199,7 +1203,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
         const int light = S.primLight[prim];
         if (light >= 0) {
             const DeviceAreaLight Ld = S.lights[light];
-            if (Ld.twoSided || DotN(si.n, wo3) >= 0) {  // Le = 0 everywhere would add exact zeros
+            if ((Ld.twoSided || DotN(si.n, wo3) >= 0) && !SpreadCut(Ld.v1.w, si.n, wo3)) {  // else Le = 0
                 const bool plain = depth == 0 || specularBounce;
                 float lightPDF = 0;
                 if (!plain) {

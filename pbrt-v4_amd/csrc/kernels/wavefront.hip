@@ -489,6 +489,7 @@ __global__ void __launch_bounds__(kBlock) k_emissive(DeviceScene S, PathState st
         V3 wo = Normalize(-rd);
         const DeviceAreaLight Ld = S.lights[light];
         if (!(Ld.twoSided || DotN(surf.n, wo) >= 0)) continue;
+        if (SpreadCut(Ld.v1.w, surf.n, wo)) continue;  // outside the emitter's spread: L = 0
         float denom;
         if (!mis) {
             denom = Avg31(1.f);

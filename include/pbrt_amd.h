@@ -352,6 +352,10 @@ int pbrt_debug_texture_eval(const pbrt_scene *scene, int material, int slot, con
 int pbrt_debug_env_eval(const pbrt_scene *scene, int env, const float *dirs, const float *u, int n, float *out);
 /* EqualAreaSquareToSphere (to_sphere != 0: in[n][2] -> out[n][3]) or EqualAreaSphereToSquare
  * (in[n][3] -> out[n][2]) with the product's shared host/device code (util/math.cpp:292-361) */
+/* util/noise.cpp Noise / DNoise and CloudMedium::Density (media.h:493-517) as the media
+ * kernels evaluate them: out5 per point = Noise(p), DNoise(p) xyz, Density(p) for params3 =
+ * {density, wispiness, frequency} (host) */
+int pbrt_debug_cloud_density(const float *params3, const float *pts, int n, float *out5);
 int pbrt_debug_equal_area(int to_sphere, const float *in, int n, float *out);
 /* Sphere / disk `shape` of the scene with the product's shared host/device code (shapes.h:
  * 106-571): for n rays rays[n][6] (o, d) and sample pairs u[n][2], out[n][40] = hit flag, tHit,

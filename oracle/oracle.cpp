@@ -3000,11 +3000,74 @@ struct Media {
         if (P[6] > P[3]) o.z /= P[6] - P[3];
         return o;
     }
+    // util/noise.cpp Noise(x, y, z) / Grad / NoiseWeight (:53-118) over NoisePerm
+    static Float NoiseAt(const float *perm, Float x, Float y, Float z) {
+        auto grad = [&](int xi, int yi, int zi, Float dx, Float dy, Float dz) {
+            int h = (int)perm[(int)perm[(int)perm[xi] + yi] + zi] & 15;
+            Float u = h < 8 || h == 12 || h == 13 ? dx : dy;
+            Float v = h < 4 || h == 12 || h == 13 ? dy : dz;
+            return ((h & 1) ? -u : u) + ((h & 2) ? -v : v);
+        };
+        auto weight = [](Float t) {
+            Float t2 = t * t;  // Pow<5> = t2 t2 t, Pow<4> = t2 t2 1, Pow<3> = t t t
+            return 6 * (t2 * t2 * t) - 15 * (t2 * t2 * 1) + 10 * (t * t * t);
+        };
+        x = std::fmod(x, Float(1 << 30));
+        y = std::fmod(y, Float(1 << 30));
+        z = std::fmod(z, Float(1 << 30));
+        int ix = (int)std::floor(x), iy = (int)std::floor(y), iz = (int)std::floor(z);
+        Float dx = x - ix, dy = y - iy, dz = z - iz;
+        ix &= 255, iy &= 255, iz &= 255;
+        Float w000 = grad(ix, iy, iz, dx, dy, dz), w100 = grad(ix + 1, iy, iz, dx - 1, dy, dz);
+        Float w010 = grad(ix, iy + 1, iz, dx, dy - 1, dz), w110 = grad(ix + 1, iy + 1, iz, dx - 1, dy - 1, dz);
+        Float w001 = grad(ix, iy, iz + 1, dx, dy, dz - 1), w101 = grad(ix + 1, iy, iz + 1, dx - 1, dy, dz - 1);
+        Float w011 = grad(ix, iy + 1, iz + 1, dx, dy - 1, dz - 1);
+        Float w111 = grad(ix + 1, iy + 1, iz + 1, dx - 1, dy - 1, dz - 1);
+        Float wx = weight(dx), wy = weight(dy), wz = weight(dz);
+        Float y0 = Lerp(wy, Lerp(wx, w000, w100), Lerp(wx, w010, w110));
+        Float y1 = Lerp(wy, Lerp(wx, w001, w101), Lerp(wx, w011, w111));
+        return Lerp(wz, y0, y1);
+    }
+    // CloudMedium::Density (media.h:493-517); c = {density, wispiness, frequency, perm[512]}
+    static Float CloudDensity(const float *c, Vec p) {
+        const float *perm = c + 3;
+        Vec pp = p * c[2];
+        if (c[1] > 0) {
+            Float vomega = 0.05f * c[1], vlambda = 10.f;
+            for (int i = 0; i < 2; ++i) {
+                Vec q = pp * vlambda;
+                const Float delta = .01f;
+                Float n = NoiseAt(perm, q.x, q.y, q.z);
+                Vec dn((NoiseAt(perm, q.x + delta, q.y + 0.f, q.z + 0.f) - n) / delta,
+                       (NoiseAt(perm, q.x + 0.f, q.y + delta, q.z + 0.f) - n) / delta,
+                       (NoiseAt(perm, q.x + 0.f, q.y + 0.f, q.z + delta) - n) / delta);
+                pp = pp + dn * vomega;
+                vomega *= 0.5f;
+                vlambda *= 1.99f;
+            }
+        }
+        Float d = 0, omega = 0.5f, lambda = 1.f;
+        for (int i = 0; i < 5; ++i) {
+            Vec q = pp * lambda;
+            d += omega * NoiseAt(perm, q.x, q.y, q.z);
+            omega *= 0.5f;
+            lambda *= 1.99f;
+        }
+        d = Clamp((1 - p.y) * 4.5f * c[0] * d, 0, 1);
+        d += 2 * std::max<Float>(0, 0.5f - p.y);
+        return Clamp(d, 0, 1);
+    }
     MediumProps SamplePoint(int m, Vec p, const Wavelengths &lambda) const {
         const int32_t *I = Info(m);
         MediumProps mp{Dense(I[1], lambda), Dense(I[2], lambda), Spectrum(0.f)};
         if (I[0] == 0) {
             mp.Le = Dense(I[3], lambda);
+            return mp;
+        }
+        if (I[0] == 2) {  // CloudMedium::SamplePoint: density * sigma (no emission)
+            const Float d = CloudDensity(f->medium_values + I[11], ToMedium(m, p));
+            mp.sigma_a = mp.sigma_a * d;
+            mp.sigma_s = mp.sigma_s * d;
             return mp;
         }
         Vec q = Offset(m, ToMedium(m, p));
@@ -3105,6 +3168,11 @@ static MajorantIter SampleRay(const Media &M, int m, Vec o, Vec d, Float raytMax
             it.empty = true;
             return it;
         }
+    }
+    if (I[0] == 2) {  // CloudMedium: HomogeneousMajorantIterator(tMin, tMax, sigma_t)
+        it.homogeneous = true;
+        it.seg = MajorantSeg{t0, t1, sa + ss};
+        return it;
     }
     // DDAMajorantIterator (media.h:168-205) over the medium's 16^3 majorant grid
     it.grid = M.f->medium_values + I[13];
@@ -5435,6 +5503,22 @@ int oracle_env_eval(const pbrt_scene_flat *flat, int env, const float *dirs, con
 }
 // EqualAreaSquareToSphere (toSphere: in[n][2] -> out[n][3]) or EqualAreaSphereToSquare
 // (in[n][3] -> out[n][2]) of the oracle (util/math.cpp:292-361)
+// util/noise.cpp Noise / DNoise and CloudMedium::Density: c = {density, wispiness, frequency,
+// NoisePerm[512]}; out5 per point = Noise, DNoise xyz, Density
+int oracle_cloud_density(const float *c, const float *pts, int n, float *out) {
+    const float *perm = c + 3;
+    for (int i = 0; i < n; ++i) {
+        const Vec p(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]);
+        const Float nz = Media::NoiseAt(perm, p.x, p.y, p.z), d = .01f;
+        out[5 * i] = nz;
+        out[5 * i + 1] = (Media::NoiseAt(perm, p.x + d, p.y + 0.f, p.z + 0.f) - nz) / d;
+        out[5 * i + 2] = (Media::NoiseAt(perm, p.x + 0.f, p.y + d, p.z + 0.f) - nz) / d;
+        out[5 * i + 3] = (Media::NoiseAt(perm, p.x + 0.f, p.y + 0.f, p.z + d) - nz) / d;
+        out[5 * i + 4] = Media::CloudDensity(c, p);
+    }
+    return 0;
+}
+
 int oracle_equal_area(int toSphere, const float *in, int n, float *out) {
     for (int i = 0; i < n; ++i) {
         if (toSphere) {

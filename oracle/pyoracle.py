@@ -55,6 +55,7 @@ def lib():
         _lib.oracle_env_eval.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_int, vp]
         _lib.oracle_shape_eval.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_int, vp]
         _lib.oracle_equal_area.argtypes = [ctypes.c_int, vp, ctypes.c_int, vp]
+        _lib.oracle_cloud_density.argtypes = [vp, vp, ctypes.c_int, vp]
         _lib.oracle_camera_min_diff.argtypes = [vp, vp, vp]
         _lib.oracle_image_level.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int64,
                                             ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
@@ -101,6 +102,17 @@ def env_eval(scene, env, dirs, u):
     out = np.zeros((len(d), 16), np.float32)
     rc = lib().oracle_env_eval(ctypes.byref(flat), env, d.ctypes.data, uu.ctypes.data, len(d), out.ctypes.data)
     assert rc == 0, rc
+    return out
+
+
+def cloud_density(params3, points):
+    """The oracle's Noise / DNoise / CloudMedium density rows, as pbrt_amd.cloud_density"""
+    import json
+    perm = json.loads((HERE.parent / "pbrt-v4_amd" / "data" / "spectral_data.json").read_text())["NoisePerm"]
+    c = f32(list(params3) + perm)
+    pts = f32(points).reshape(-1, 3)
+    out = np.zeros((len(pts), 5), np.float32)
+    assert lib().oracle_cloud_density(c.ctypes.data, pts.ctypes.data, len(pts), out.ctypes.data) == 0
     return out
 
 

@@ -89,7 +89,7 @@ static void MediumTables(const SceneDesc &s, std::vector<int32_t> *info, std::ve
         const V3 lo(std::min(m.p0.x, m.p1.x), std::min(m.p0.y, m.p1.y), std::min(m.p0.z, m.p1.z));
         const V3 hi(std::max(m.p0.x, m.p1.x), std::max(m.p0.y, m.p1.y), std::max(m.p0.z, m.p1.z));
         params->insert(params->end(), {m.g, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, 0.f});
-        Mat4 inv = m.type == kMediumGrid ? Inverse4(m.renderFromMedium) : Identity4();
+        Mat4 inv = m.type != kMediumHomogeneous ? Inverse4(m.renderFromMedium) : Identity4();
         for (int i = 0; i < 4; ++i)
             for (int j = 0; j < 4; ++j) params->push_back((float)inv[i][j]);
     }
@@ -2353,6 +2353,29 @@ int pbrt_debug_shape_eval(const pbrt_scene *scene, int shape, const float *rays,
                 o[36] = ss.pdf;
             }
             o[37] = ShapePDFSolidAngle(d, ro, V3(0, 0, 0), V3(0, 0, 0), rd, N, cns);
+        }
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_debug_cloud_density(const float *params3, const float *pts, int n, float *out) {
+    try {
+        const auto &perm = GetSpectralData().noisePerm;
+        if (perm.size() != 512) return Fail("spectral data lacks the noise permutation (NoisePerm)");
+        std::vector<float> c(params3, params3 + 3);
+        c.insert(c.end(), perm.begin(), perm.end());
+        for (int i = 0; i < n; ++i) {
+            const V3 p(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]);
+            // rows: Noise(p), DNoise(p) xyz, Density(p) with params3
+            const float nz = Noise3(c.data() + 3, p.x, p.y, p.z);
+            const float d = .01f;
+            out[5 * i] = nz;
+            out[5 * i + 1] = (Noise3(c.data() + 3, p.x + d, p.y + 0.f, p.z + 0.f) - nz) / d;
+            out[5 * i + 2] = (Noise3(c.data() + 3, p.x + 0.f, p.y + d, p.z + 0.f) - nz) / d;
+            out[5 * i + 3] = (Noise3(c.data() + 3, p.x + 0.f, p.y + 0.f, p.z + d) - nz) / d;
+            out[5 * i + 4] = CloudDensity(c.data(), p);
         }
         return 0;
     } catch (const std::exception &e) {

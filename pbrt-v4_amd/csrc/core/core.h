@@ -1748,6 +1748,76 @@ PHD float EnvLe(const EnvCoef &c, float lightScale, float illum, float lambda) {
     return lightScale * ((c.s * SigmoidPolynomial(c.c0, c.c1, c.c2, lambda)) * illum);
 }
 
+// ---------------------------------------------------------------- cloud medium
+// Perlin gradient noise (util/noise.cpp:53-118) over the permutation stored with a cloud
+// medium (as floats); NoiseWeight's powers in pbrt's Pow<n> association
+PHD float NoiseGrad(const float *perm, int x, int y, int z, float dx, float dy, float dz) {
+    int h = (int)perm[(int)perm[(int)perm[x] + y] + z];
+    h &= 15;
+    const float u = h < 8 || h == 12 || h == 13 ? dx : dy;
+    const float v = h < 4 || h == 12 || h == 13 ? dy : dz;
+    return ((h & 1) ? -u : u) + ((h & 2) ? -v : v);
+}
+PHD float NoiseWeight(float t) {
+    const float t2 = t * t;
+    const float p5 = t2 * t2 * t, p4 = t2 * t2 * 1.f, p3 = t * t * t;
+    return 6 * p5 - 15 * p4 + 10 * p3;
+}
+PHD float Noise3(const float *perm, float x, float y, float z) {
+    x = std::fmod(x, float(1 << 30));
+    y = std::fmod(y, float(1 << 30));
+    z = std::fmod(z, float(1 << 30));
+    int ix = (int)std::floor(x), iy = (int)std::floor(y), iz = (int)std::floor(z);
+    const float dx = x - ix, dy = y - iy, dz = z - iz;
+    ix &= 255;
+    iy &= 255;
+    iz &= 255;
+    const float w000 = NoiseGrad(perm, ix, iy, iz, dx, dy, dz);
+    const float w100 = NoiseGrad(perm, ix + 1, iy, iz, dx - 1, dy, dz);
+    const float w010 = NoiseGrad(perm, ix, iy + 1, iz, dx, dy - 1, dz);
+    const float w110 = NoiseGrad(perm, ix + 1, iy + 1, iz, dx - 1, dy - 1, dz);
+    const float w001 = NoiseGrad(perm, ix, iy, iz + 1, dx, dy, dz - 1);
+    const float w101 = NoiseGrad(perm, ix + 1, iy, iz + 1, dx - 1, dy, dz - 1);
+    const float w011 = NoiseGrad(perm, ix, iy + 1, iz + 1, dx, dy - 1, dz - 1);
+    const float w111 = NoiseGrad(perm, ix + 1, iy + 1, iz + 1, dx - 1, dy - 1, dz - 1);
+    const float wx = NoiseWeight(dx), wy = NoiseWeight(dy), wz = NoiseWeight(dz);
+    const float x00 = Lerpf(wx, w000, w100), x10 = Lerpf(wx, w010, w110);
+    const float x01 = Lerpf(wx, w001, w101), x11 = Lerpf(wx, w011, w111);
+    return Lerpf(wz, Lerpf(wy, x00, x10), Lerpf(wy, x01, x11));
+}
+// CloudMedium::Density (media.h:493-517) at a medium-space point; c = {density, wispiness,
+// frequency, perm[512]}
+PHD float CloudDensity(const float *c, V3 p) {
+    const float *perm = c + 3;
+    const float freq = c[2];
+    V3 pp(freq * p.x, freq * p.y, freq * p.z);
+    if (c[1] > 0) {
+        float vomega = 0.05f * c[1], vlambda = 10.f;
+        for (int i = 0; i < 2; ++i) {
+            // DNoise(vlambda * pp) (util/noise.cpp:120-126)
+            const V3 q(vlambda * pp.x, vlambda * pp.y, vlambda * pp.z);
+            const float delta = .01f;
+            const float n = Noise3(perm, q.x, q.y, q.z);
+            const float nx = Noise3(perm, q.x + delta, q.y + 0.f, q.z + 0.f);
+            const float ny = Noise3(perm, q.x + 0.f, q.y + delta, q.z + 0.f);
+            const float nz = Noise3(perm, q.x + 0.f, q.y + 0.f, q.z + delta);
+            pp = V3(pp.x + vomega * ((nx - n) / delta), pp.y + vomega * ((ny - n) / delta),
+                    pp.z + vomega * ((nz - n) / delta));
+            vomega *= 0.5f;
+            vlambda *= 1.99f;
+        }
+    }
+    float d = 0, omega = 0.5f, lambda = 1.f;
+    for (int i = 0; i < 5; ++i) {
+        d += omega * Noise3(perm, lambda * pp.x, lambda * pp.y, lambda * pp.z);
+        omega *= 0.5f;
+        lambda *= 1.99f;
+    }
+    d = Clampf((1 - p.y) * 4.5f * c[0] * d, 0, 1);
+    d += 2 * std::fmax(0.f, 0.5f - p.y);
+    return Clampf(d, 0, 1);
+}
+
 // ---------------------------------------------------------------- analytic shapes
 // Interval (util/math.h:819-1076) with pbrt's CPU rounding helpers AddRoundUp(a, b) =
 // NextFloatUp(a + b) etc. (util/float.h:201-301); the constructor orders its bounds

@@ -1511,6 +1511,34 @@ void Parser::Finish() {
         MediumDesc m;
         m.name = pm.name;
         if (ps.Find("preset")) throw Error(ps.loc + ": medium \"preset\" is not supported yet");
+        if (pm.type == "cloud") {
+            // CloudMedium::Create (media.cpp:462-484): no scale or Le; sigma_a / sigma_s default 1
+            m.type = kMediumCloud;
+            bool given;
+            auto addDense = [&](const std::array<float, 311> &d) {
+                scene.denseSpectra.push_back(d);
+                return (int)scene.denseSpectra.size() - 1;
+            };
+            m.sigmaA = addDense(MediumSpectrum(ps, "sigma_a", false, 1.f, &given, nullptr));
+            m.sigmaS = addDense(MediumSpectrum(ps, "sigma_s", false, 1.f, &given, nullptr));
+            std::array<float, 311> zero{};
+            m.Le = addDense(zero);
+            m.g = (float)ps.GetFloat("g", 0);
+            m.density = {(float)ps.GetFloat("density", 1), (float)ps.GetFloat("wispiness", 1),
+                         (float)ps.GetFloat("frequency", 5)};
+            const auto &perm = GetSpectralData().noisePerm;
+            if (perm.size() != 512) throw Error("spectral data lacks the noise permutation (NoisePerm)");
+            m.density.insert(m.density.end(), perm.begin(), perm.end());
+            Param *p0 = ps.Find("p0", "point3"), *p1 = ps.Find("p1", "point3");
+            if (p0) m.p0 = V3((float)p0->nums[0], (float)p0->nums[1], (float)p0->nums[2]);
+            if (p1) m.p1 = V3((float)p1->nums[0], (float)p1->nums[1], (float)p1->nums[2]);
+            m.renderFromMedium = Mul(scene.camera.renderFromWorld, pm.worldFromMedium);
+            ps.Find("type");
+            ps.CheckUnused();
+            mediumIndex[pm.name] = (int)scene.media.size();
+            scene.media.push_back(std::move(m));
+            continue;
+        }
         bool given;
         float scale = (float)ps.GetFloat("scale", 1);
         auto addDense = [&](std::array<float, 311> d, float k) {

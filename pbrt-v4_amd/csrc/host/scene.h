@@ -44,7 +44,8 @@ constexpr int kMatMix = 8;
 // Participating media (media.h:209-350, media.cpp:167-330).  Spectra are DenselySampled
 // 395..705 nm tables in SceneDesc::denseSpectra with pbrt's constructor scaling applied
 // (sigma_a/sigma_s *= "scale"; homogeneous Le *= "Lescale" / photometric).
-enum MediumType : int { kMediumHomogeneous = 0, kMediumGrid = 1 };
+// CloudMedium (media.h:430-525): procedural Perlin-noise density in [p0, p1], homogeneous majorant
+enum MediumType : int { kMediumHomogeneous = 0, kMediumGrid = 1, kMediumCloud = 2 };
 struct MediumDesc {
     int type = kMediumHomogeneous;
     std::string name;
@@ -55,7 +56,8 @@ struct MediumDesc {
     Mat4 renderFromMedium;                 // inverse applied to rays and points
     V3 p0{0, 0, 0}, p1{1, 1, 1};           // medium-space bounds
     int nx = 1, ny = 1, nz = 1;
-    std::vector<float> density;            // [nz][ny][nx]
+    std::vector<float> density;            // [nz][ny][nx]; cloud: {density, wispiness, frequency}
+                                           // followed by the 512-entry noise permutation
     int lnx = 1, lny = 1, lnz = 1;         // LeScale grid (1x1x1 = {1 / photometric(Le)})
     std::vector<float> LeScale;
     std::vector<float> majorant;           // 16^3 MaxValue of density per majorant voxel
@@ -379,6 +381,7 @@ struct SpectralData {
     std::array<float, 128> mipFilterLUT;  // MIPFilterLUT (util/mipmap.cpp:59-191)
     std::map<std::string, std::vector<float>> sensors;  // "<camera>_r|g|b" interleaved curves
     std::vector<float> cieSLambda, cieS0, cieS1, cieS2;  // CIE daylight basis (Spectra::D)
+    std::vector<float> noisePerm;                        // util/noise.cpp NoisePerm[512]
     std::vector<std::vector<float>> swatches;           // 24 ColorChecker reflectances (film.cpp)
 };
 // PixelSensor (film.h:36-116, PixelSensor::Create film.cpp:222-262): the sensor's r/g/b matching

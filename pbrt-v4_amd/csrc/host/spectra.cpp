@@ -99,6 +99,7 @@ static SpectralData LoadSpectralData() {
         else if (name == "CIE_S0") tof(d.cieS0);
         else if (name == "CIE_S1") tof(d.cieS1);
         else if (name == "CIE_S2") tof(d.cieS2);
+        else if (name == "NoisePerm") tof(d.noisePerm);
     }
     if (d.cieX.size() != 471 || d.optX.size() != 95) throw Error("malformed spectral data " + path);
     if (!haveMipLUT || !haveSrgbLUT)

@@ -88,7 +88,8 @@ PHD int LdsNodeStride(int compressed) { return compressed ? kLdsQNodeStride : kL
 // density / LeScale / 16^3 majorant grids) and 24 floats (g, bounds lo hi, pad,
 // mediumFromRender 4x4).  primMedium: {inside, outside} per leaf-order triangle (-1 = none),
 // nullptr when no triangle is a medium boundary.
-constexpr int kDevMediumGrid = 1;  // info[0] (scene.h MediumType)
+constexpr int kDevMediumGrid = 1;   // info[0] (scene.h MediumType)
+constexpr int kDevMediumCloud = 2;  // density / wispiness / frequency + noise permutation at info[11]
 constexpr int kMajorantRes = 16;
 struct DeviceMedia {
     int n;             // media in the scene (0: the surface-only kernels run)
@@ -101,13 +102,12 @@ struct DeviceMedia {
     const int *primMedium;
 };
 
-// PointLight / SpotLight / DistantLight in render space (scene.h DeltaLightDesc): p.xyz position
-// (.w type bits: 0 point, 1 spot, 2 distant), w.xyz spot axis or direction toward a distant
-// light (.w scale), cone = cosFalloffStart, cosFalloffEnd, spectrum bits; m0..m2: rows of
-// renderFromLight's inverse 3x3 (spot, Transform::ApplyInverse on vectors)
-// p.w: type bits; w.w: scale; cone: cosFalloffStart, cosFalloffEnd, spectrum bits, offset of the
-// goniometric / projection image in DeviceScene::deltaImg (int bits); m0..m2: rows of
-// renderFromLight^-1, .w: image width / height bits, projection 1 / tan(fov / 2)
+// PointLight / SpotLight / DistantLight / GoniometricLight / ProjectionLight in render space
+// (scene.h DeltaLightDesc): p.xyz position (.w type bits: 0 point, 1 spot, 2 distant,
+// 3 goniometric, 4 projection), w.xyz spot axis or direction toward a distant light (.w scale),
+// cone = cosFalloffStart, cosFalloffEnd, spectrum bits, offset of the goniometric / projection
+// image in DeviceScene::deltaImg (int bits); m0..m2: rows of renderFromLight's inverse 3x3
+// (Transform::ApplyInverse on vectors), .w: image width / height bits, projection 1/tan(fov/2)
 struct DeviceDeltaLight {
     float4 p, w, cone, m0, m1, m2;
 };

@@ -92,6 +92,8 @@ struct MediumPoint {
     float d, le;
 };
 __device__ inline MediumPoint SampleMediumPoint(const DeviceScene &S, const MediumRef &m, V3 p) {
+    if (m.I[0] == kDevMediumCloud)
+        return MediumPoint{CloudDensity(S.media.values + m.I[11], MediumFromRender(m.P + 8, p)), 0.f};
     if (m.I[0] != kDevMediumGrid) return MediumPoint{1.f, 1.f};
     const V3 q = BoundsOffset(m.P, MediumFromRender(m.P + 8, p));
     MediumPoint r;
@@ -117,7 +119,7 @@ struct MajorantIter {
         if (!dda) {
             if (called || empty) return false;
             called = true;
-            *segMin = 0;
+            *segMin = tMin;
             *segMax = tMax;
             *mx = 1.f;
             return true;
@@ -152,12 +154,13 @@ __device__ inline MajorantIter SampleMediumRay(const DeviceScene &S, const Mediu
     it.called = false;
     it.empty = false;
     it.grid = nullptr;
-    if (m.I[0] != kDevMediumGrid) {
+    if (m.I[0] != kDevMediumGrid && m.I[0] != kDevMediumCloud) {
         it.dda = false;
+        it.tMin = 0;
         it.tMax = raytMax;
         return it;
     }
-    it.dda = true;
+    it.dda = m.I[0] == kDevMediumGrid;
     // Transform::ApplyInverse(Ray, &tMax) (util/transform.h:416-429): the exact origin becomes a
     // Point3fi (transform.cpp:263-303), is pushed to the edge of its error bounds along d
     const float *M = m.P + 8;
@@ -208,6 +211,11 @@ __device__ inline MajorantIter SampleMediumRay(const DeviceScene &S, const Mediu
         if (t0 > t1) it.empty = true;
     }
     if (it.empty) return it;
+    if (!it.dda) {  // CloudMedium: HomogeneousMajorantIterator(tMin, tMax, sigma_t) over the bounds
+        it.tMin = t0;
+        it.tMax = t1;
+        return it;
+    }
     // DDAMajorantIterator ctor (media.h:140-166)
     it.grid = S.media.values + m.I[13];
     it.tMin = t0;

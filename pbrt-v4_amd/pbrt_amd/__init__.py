@@ -137,7 +137,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_debug_env_eval",
     "pbrt_debug_shape_eval",
     "pbrt_debug_set_queue_check", "pbrt_debug_queue_holes",
-    "pbrt_debug_equal_area",
+    "pbrt_debug_equal_area", "pbrt_debug_cloud_density",
 ]
 
 _LIB = None
@@ -214,9 +214,20 @@ def _lib():
     lib.pbrt_debug_set_queue_check.argtypes = [c.c_int]
     lib.pbrt_debug_queue_holes.argtypes = [c.POINTER(c.c_int)]
     lib.pbrt_debug_equal_area.argtypes = [c.c_int, c.c_void_p, c.c_int, c.c_void_p]
+    lib.pbrt_debug_cloud_density.argtypes = [c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_set_data_dir(str(DATA_DIR).encode())
     _LIB = lib
     return lib
+
+
+def cloud_density(params3, points):
+    """pbrt_debug_cloud_density: [n, 5] rows Noise(p), DNoise(p) xyz, CloudMedium Density(p)."""
+    import numpy as np
+    p = np.ascontiguousarray(np.asarray(params3, np.float32).reshape(3))
+    pts = np.ascontiguousarray(np.asarray(points, np.float32).reshape(-1, 3))
+    out = np.zeros((len(pts), 5), np.float32)
+    _check(_lib().pbrt_debug_cloud_density(p.ctypes.data, pts.ctypes.data, len(pts), out.ctypes.data))
+    return out
 
 
 def equal_area(points, to_sphere):

@@ -20,6 +20,8 @@ reference's sources
                                  sensor curves (<camera>_r/_g/_b) and the CIE daylight basis
                                  S0 / S1 / S2 (Spectra::D)
     src/pbrt/film.cpp            the 24 ColorChecker swatch reflectances of PixelSensor
+    src/pbrt/util/noise.cpp      NoisePerm (:17-46), Perlin's gradient-noise permutation table
+                                 (the CloudMedium density)
 
 and writes pbrt-v4_amd/data/spectral_data.json, which is committed.  Run it only in a
 container that has /root/reference; the GPU box uses the committed JSON.
@@ -123,6 +125,13 @@ def main():
     assert len(sw) == 24, len(sw)
     for i, b in enumerate(sw):
         data[f"swatch:{i}"] = numbers(b)
+    # Perlin noise permutation (util/noise.cpp NoisePerm[2 * NoisePermSize])
+    noise = (REF / "util" / "noise.cpp").read_text()
+    m = re.search(r"NoisePerm\s*\[2 \* NoisePermSize\]\s*=\s*\{", noise)
+    body = noise[m.end():noise.index("};", m.end())]
+    body = re.sub(r"//[^\n]*", "", body)
+    data["NoisePerm"] = numbers(body)
+    assert len(data["NoisePerm"]) == 512, len(data["NoisePerm"])
     OUT.parent.mkdir(parents=True, exist_ok=True)
     OUT.write_text(json.dumps(data))
     print("wrote", OUT, {k: len(v) if isinstance(v, list) else v for k, v in data.items()})

@@ -835,6 +835,8 @@ static void BuildDevice(pbrt_context *c) {
                 dimg.insert(dimg.end(), d.img.begin(), d.img.end());
             } else if (d.type == kDeltaProjection) {
                 // ProjectionLight::I's RGBIlluminantSpectrum of the nearest pixel, per pixel
+                // (float4 records: 16-byte aligned)
+                while (dimg.size() % 4) dimg.push_back(0.f);
                 off = (int)dimg.size();
                 EnvLightDesc e;
                 e.res = 1;

@@ -1351,7 +1351,7 @@ __device__ inline bool SampleLiSurface(const DeviceScene &S, const DeviceAreaLig
                 if (!(psx >= -bx && psx <= bx && psy >= -by && psy <= by)) return false;
                 const float u = (psx - -bx) / (bx - -bx), vv = (psy - -by) / (by - -by);
                 const int x = min(max((int)(u * w), 0), w - 1), y = min(max((int)(vv * h), 0), h - 1);
-                const float4 c = reinterpret_cast<const float4 *>(img + 4)[(size_t)y * w + x];
+                const float4 c = reinterpret_cast<const float4 *>(img)[(size_t)y * w + x];
                 ls->envLe = true;
                 ls->env = EnvCoef{c.x, c.y, c.z, c.w};
                 return true;

@@ -67,6 +67,11 @@ typedef struct pbrt_scene_flat {
     /* [n_area_lights][3]: the fork's "spread" (lights.cpp:715-717): cosFalloffEnd (> 0 only for a
      * spread below 90 degrees), tanFalloffEnd, normalize_falloffEnd */
     const float *light_spread;
+    /* [n_area_lights]: offset of the light's emission image in area_images, or -1; an image
+     * is {w, h} then linear R, G, B [h][w][3] (row 0 = top); the light's spectrum is then the
+     * colour space's illuminant (DiffuseAreaLight with "filename", lights.cpp:909-936) */
+    const int32_t *light_image;
+    const float *area_images;
     const int32_t *inf_spectrum;  /* [n_infinite_lights] */
     const float *inf_scale;
     const float *dense_spectra;   /* [n_spectra][311] at 395..705 nm */

@@ -960,6 +960,7 @@ static void InvertSphericalTriangleSample(Vec v0, Vec v1, Vec v2, Vec p, Vec w, 
 struct ShapeSample {
     Vec p, err, n;
     Float pdf;
+    Float uv[2] = {0, 0};  // triangles: b0 uv0 + b1 uv1 + b2 uv2 (an image emitter's lookup)
 };
 static Float TriArea(Vec p0, Vec p1, Vec p2) { return 0.5f * Length(Cross(p1 - p0, p2 - p0)); }
 // Triangle::Sample(u)'s normal (shapes.h:1023-1029)
@@ -991,6 +992,7 @@ static bool TriangleSample(Vec p0, Vec p1, Vec p2, bool flip, Vec ref, Vec ns, F
         ss->p = p;
         ss->n = n;
         ss->pdf = pdf;
+        for (int c = 0; c < 2; ++c) ss->uv[c] = b[0] * a.uv[0][c] + b[1] * a.uv[1][c] + b[2] * a.uv[2][c];
         return true;
     }
     Float pdf = 1;
@@ -1012,6 +1014,7 @@ static bool TriangleSample(Vec p0, Vec p1, Vec p2, bool flip, Vec ref, Vec ns, F
              &ss->p, &ss->err);
     ss->n = SampledNormal(p0, p1, p2, flip, a, b);
     ss->pdf = pdf;
+    for (int c = 0; c < 2; ++c) ss->uv[c] = b[0] * a.uv[0][c] + b[1] * a.uv[1][c] + b[2] * a.uv[2][c];
     return true;
 }
 static Float TrianglePDF(Vec p0, Vec p1, Vec p2, bool flip, Vec ref, Vec refErr, Vec refN, Vec ns, Vec wi,
@@ -2159,6 +2162,14 @@ static std::vector<std::pair<int, LB>> SceneLightBounds(const pbrt_scene_flat *f
         auto P = [&](int k) { return Vec(f->vertices[3 * v[k]], f->vertices[3 * v[k] + 1], f->vertices[3 * v[k] + 2]); };
         const Vec p0 = P(0), p1 = P(1), p2 = P(2);
         Float phi = denseMax(f->light_spectrum[i]);
+        if (f->light_image && f->light_image[i] >= 0) {
+            // DiffuseAreaLight::Bounds with an image (lights.cpp:806-813): the mean channel value
+            const float *img = f->area_images + f->light_image[i];
+            const int w = (int)img[0], h = (int)img[1];
+            Float sum = 0;
+            for (int k = 0; k < 3 * w * h; ++k) sum += img[2 + k];
+            phi = sum / (3 * w * h);
+        }
         phi *= f->light_scale[i] * TriArea(p0, p1, p2) * Pi;
         Vec n = Normalize(Cross(p1 - p0, p2 - p0));
         if (f->tri_shading && (f->tri_shading[t] & 1)) {
@@ -4330,22 +4341,46 @@ struct Renderer {
         return Vec(x, y, z) / w;
     }
 
-    Spectrum LightL(int li, const Wavelengths &lambda) const {
+    Spectrum LightL(int li, const Wavelengths &lambda, const Float *uv = nullptr) const {
         const float *dense = f->dense_spectra + 311 * f->light_spectrum[li];
+        if (uv && f->light_image && f->light_image[li] >= 0) {
+            // an image emitter (lights.h:460-467): Image::BilerpChannel at (u, 1 - v), clamp
+            // wrap, RGBIlluminantSpectrum of ClampZero(rgb) times the light scale
+            const float *img = f->area_images + f->light_image[li];
+            const int w = (int)img[0], h = (int)img[1];
+            const float *rgb = img + 2;
+            const Float x = uv[0] * w - 0.5f, y = (1 - uv[1]) * h - 0.5f;
+            const int xi = (int)std::floor(x), yi = (int)std::floor(y);
+            const Float dx = x - xi, dy = y - yi;
+            auto at = [&](int px, int py, int c) {
+                px = std::clamp(px, 0, w - 1), py = std::clamp(py, 0, h - 1);
+                return rgb[((size_t)py * w + px) * 3 + c];
+            };
+            Float c3[3];
+            for (int c = 0; c < 3; ++c)
+                c3[c] = std::max<Float>(0, (1 - dx) * (1 - dy) * at(xi, yi, c) + dx * (1 - dy) * at(xi + 1, yi, c) +
+                                               (1 - dx) * dy * at(xi, yi + 1, c) + dx * dy * at(xi + 1, yi + 1, c));
+            Float mx = std::max({c3[0], c3[1], c3[2]}), rs = 2 * mx, co[3];
+            if (rs) ORGBCoeffs(c3[0] / rs, c3[1] / rs, c3[2] / rs, co);
+            else ORGBCoeffs(0, 0, 0, co);
+            Spectrum sp;
+            for (int i = 0; i < NS; ++i) sp[i] = rs * Sigmoid(co[0], co[1], co[2], lambda.lambda[i]);
+            return (sp * SampleDense(dense, lambda)) * f->light_scale[li];
+        }
         return SampleDense(dense, lambda) * f->light_scale[li];
     }
     // DiffuseAreaLight::L (lights.h:443-470) leaving along w at a point with normal n: zero on the
     // back of a one-sided emitter and, with this fork's spread, outside the cone
     // AbsDot(w, n) >= cosFalloffEnd
-    Spectrum AreaL(int li, Vec n, Vec w, const Wavelengths &lambda) const {
+    Spectrum AreaL(int li, Vec n, Vec w, const Wavelengths &lambda, const Float *uv = nullptr) const {
         if (!(f->light_two_sided[li] || DotN(n, w) >= 0)) return Spectrum(0.f);
         const float cosE = f->light_spread ? f->light_spread[3 * li] : -1;
         if (cosE > 0 && std::abs(DotN(n, w)) < cosE) return Spectrum(0.f);
-        return LightL(li, lambda);
+        return LightL(li, lambda, uv);
     }
     // DiffuseAreaLight::SampleLi's spread attenuation (lights.cpp:763-771) toward wi
-    Spectrum SampledAreaL(int li, Vec n, Vec wi, const Wavelengths &lambda) const {
-        Spectrum Le = AreaL(li, n, -wi, lambda);
+    Spectrum SampledAreaL(int li, Vec n, Vec wi, const Wavelengths &lambda, const Float *uv = nullptr) const {
+        Spectrum Le = AreaL(li, n, -wi, lambda, uv);
         const float *sp = f->light_spread ? f->light_spread + 3 * li : nullptr;
         if (sp && sp[0] > 0) {
             const Float cos_a = -DotN(n, wi);
@@ -4791,7 +4826,7 @@ struct Renderer {
                         if (sampleArea(li, pS, Vec(0, 0, 0), Vec(0, 0, 0), Vec(0, 0, 0), dU0, dU1, &ss) &&
                             ss.pdf != 0 && LengthSquared(ss.p - pS) != 0) {
                             Vec wi = Normalize(ss.p - pS);
-                            const Spectrum Le = SampledAreaL(li, ss.n, wi, lambda);
+                            const Spectrum Le = SampledAreaL(li, ss.n, wi, lambda, ss.uv);
                             if (Le) {
                                 Float ph = HenyeyGreenstein(Dot(wo, wi), g);
                                 Spectrum b2 = beta * ph;
@@ -4866,7 +4901,7 @@ struct Renderer {
             // HandleEmissiveIntersection
             int light = S.Light(prim);
             if (light >= 0) {
-                const Spectrum Le = AreaL(light, si.n, si.wo, lambda);
+                const Spectrum Le = AreaL(light, si.n, si.wo, lambda, si.uv);
                 if (Le) {
                     if (depth == 0 || specularBounce) L = L + beta * Le / r_u.Average();
                     else {
@@ -4964,7 +4999,7 @@ struct Renderer {
                     if (sampleArea(li, cp, cpErr, si.n, si.ns, dU0, dU1, &ss) && ss.pdf != 0 &&
                         LengthSquared(ss.p - cp) != 0) {
                         Vec wi = Normalize(ss.p - cp);
-                        const Spectrum Le = SampledAreaL(li, ss.n, wi, lambda);
+                        const Spectrum Le = SampledAreaL(li, ss.n, wi, lambda, ss.uv);
                         if (Le) {
                             Vec wiL = toLocal(wi);
                             Spectrum fv = woL.z == 0 ? Spectrum(0.f)  // BSDF::f (bsdf.h:60-70)
@@ -5062,7 +5097,7 @@ struct Renderer {
             // emission at the hit (SurfaceInteraction::Le -> DiffuseAreaLight::L)
             const int light = S.Light(prim);
             if (light >= 0) {
-                const Spectrum Le = AreaL(light, si.n, si.wo, lambda);
+                const Spectrum Le = AreaL(light, si.n, si.wo, lambda, si.uv);
                 if (Le) {
                     if (depth == 0 || specularBounce) L = L + beta * Le;
                     else {
@@ -5147,7 +5182,7 @@ struct Renderer {
                                              S.Attr(lp));
                         if (ok && ss.pdf != 0 && LengthSquared(ss.p - cp) != 0) {
                             wi = Normalize(ss.p - cp);
-                            Le = SampledAreaL(li, ss.n, wi, lambda);
+                            Le = SampledAreaL(li, ss.n, wi, lambda, ss.uv);
                             pdf = ss.pdf;
                             pf = OffsetRayOrigin(si.p, si.err, si.n, ss.p - si.p);
                             pt = OffsetRayOrigin(ss.p, ss.err, ss.n, pf - ss.p);

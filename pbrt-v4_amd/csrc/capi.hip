@@ -255,7 +255,8 @@ struct pbrt_scene {
     std::vector<int32_t> mediumInfo;
     std::vector<int32_t> tris, lightPrim, lightSpectrum, lightTwoSided, infSpectrum, matConstant, nodeInfo, matType,
         matSpectra, plOffsets, infDistant, uniformOrder;
-    std::vector<float> deltaLights, deltaImages, lightSpread;
+    std::vector<float> deltaLights, deltaImages, lightSpread, areaImages;
+    std::vector<int32_t> lightImage;
     std::vector<int32_t> infImage, envInfo, shapeInfo, primAlpha;
     std::vector<float> shapeParams, shapeNormals;
     std::vector<float> envXform, envRgb;
@@ -329,12 +330,22 @@ struct pbrt_scene {
         lightSpectrum.clear();
         lightTwoSided.clear();
         lightSpread.clear();
+        lightImage.clear();
+        areaImages.clear();
+        std::vector<int> areaImageOff;
+        for (const AreaLightImage &im : s.areaLightImages) {
+            areaImageOff.push_back((int)areaImages.size());
+            areaImages.push_back((float)im.w);
+            areaImages.push_back((float)im.h);
+            areaImages.insert(areaImages.end(), im.rgb.begin(), im.rgb.end());
+        }
         for (auto &l : s.areaLights) {
             lightPrim.push_back(l.shape >= 0 ? (int32_t)s.tris.size() + l.shape : l.prim);
             lightScale.push_back(l.scale);
             lightSpectrum.push_back(l.spectrum);
             lightTwoSided.push_back(l.twoSided ? 1 : 0);
             lightSpread.insert(lightSpread.end(), {l.cosFalloffEnd, l.tanFalloffEnd, l.normFalloffEnd});
+            lightImage.push_back(l.image >= 0 ? areaImageOff[l.image] : -1);
         }
         infSpectrum.clear();
         infScale.clear();
@@ -420,7 +431,8 @@ struct pbrt_context {
     DevBuf<DeviceDeltaLight> deltaLights;
     DevBuf<float> lightSpreadNorm;  // per area light: normalize_falloffEnd of its spread
     bool hasSpread = false;
-    DevBuf<float> deltaImg;
+    DevBuf<float> deltaImg, lightImg;
+    DevBuf<int> lightImgOff;
     DevBuf<int> primOrig, matType, matSpectra, plOffsets;
     DevBuf<float> matParams, plLambda, plValue, triShade, matLayer, dispL0;
     DevBuf<uint16_t> plIndex;
@@ -1113,6 +1125,39 @@ static void BuildDevice(pbrt_context *c) {
     S.deltaImg = c->deltaImg.p;
     S.nImageDelta = 0;
     for (auto &d : s.deltaLights) S.nImageDelta += d.type == kDeltaGonio || d.type == kDeltaProjection;
+    {
+        // DiffuseAreaLight emission images: per area light the offset of its image in lightImg
+        // ({w, h} as int bits, then linear R, G, B [h][w][3]) or -1; their RGBIlluminantSpectrum
+        // needs the RGB -> spectrum table (uploaded here when no texture did)
+        std::vector<float> img;
+        std::vector<int> offOf;
+        for (const AreaLightImage &im : s.areaLightImages) {
+            offOf.push_back((int)img.size());
+            img.push_back(BitsToFloat((uint32_t)im.w));
+            img.push_back(BitsToFloat((uint32_t)im.h));
+            img.insert(img.end(), im.rgb.begin(), im.rgb.end());
+        }
+        std::vector<int> lo;
+        S.nImageAreaLights = 0;
+        for (const AreaLightDesc &l : s.areaLights) {
+            lo.push_back(l.image >= 0 ? offOf[l.image] : -1);
+            S.nImageAreaLights += l.image >= 0;
+        }
+        if (S.nImageAreaLights > 0) {
+            if (c->volumetric)
+                throw Error("image area lights together with the volumetric path (media, interface, layered, thin "
+                            "dielectric, diffuse transmission or dispersive materials) are not supported yet");
+            c->lightImg.Upload(img);
+            c->lightImgOff.Upload(lo);
+            if (!S.tex.rgbZNodes) {
+                c->rgbTable.Upload(RGBToSpectrumTableData());
+                S.tex.rgbZNodes = c->rgbTable.p;
+                S.tex.rgbCoeffs = c->rgbTable.p + 64;
+            }
+        }
+        S.lightImg = S.nImageAreaLights ? c->lightImg.p : nullptr;
+        S.lightImgOff = S.nImageAreaLights ? c->lightImgOff.p : nullptr;
+    }
     S.uniformOrder = c->uniformOrder.p;
     S.sceneRadius = s.sceneRadius;
     S.uniformLightSampler = s.uniformLightSampler ? 1 : 0;
@@ -1567,7 +1612,7 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
                               (uint64_t)(st.firstSample + nS) * haltonStride <= (1ull << 24) &&
                               c->S.shadeLds.lightsInLds && c->S.shadeLds.denseInLds && c->S.triShade == nullptr &&
                               c->S.nDelta == 0 && c->S.nEnv == 0 && c->S.nShapes == 0 && !c->S.textured && !c->hasMix &&
-                              !c->S.hasSpread;
+                              !c->S.hasSpread && c->S.nImageAreaLights == 0;
             for (int depth = 0; depth <= s.maxDepth; ++depth) {
                 // closest-hit launches are event-timed in the first pass of a render only: the
                 // passes are statistically identical and each event pair costs a queue gap
@@ -1746,6 +1791,8 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
     f->light_spectrum = scene->lightSpectrum.data();
     f->light_two_sided = scene->lightTwoSided.data();
     f->light_spread = scene->lightSpread.data();
+    f->light_image = scene->lightImage.data();
+    f->area_images = scene->areaImages.data();
     f->inf_spectrum = scene->infSpectrum.data();
     f->inf_scale = scene->infScale.data();
     f->n_delta_lights = (int)s.deltaLights.size();

@@ -504,6 +504,13 @@ static void BuildLightBVH(SceneDesc &s) {
         V3 p0 = s.verts[tri[0]], p1 = s.verts[tri[1]], p2 = s.verts[tri[2]];
         const auto &dense = s.denseSpectra[al.spectrum];
         float mx = *std::max_element(dense.begin(), dense.end());
+        if (al.image >= 0) {
+            // DiffuseAreaLight::Bounds with an image (lights.cpp:806-813): the mean channel value
+            const AreaLightImage &im = s.areaLightImages[al.image];
+            float sum = 0;
+            for (float v : im.rgb) sum += v;
+            mx = sum / (3 * im.w * im.h);
+        }
         float phi = mx;
         phi *= al.scale * al.area * kPi;
         // Triangle::NormalBounds (shapes.h): with vertex normals the face normal is turned

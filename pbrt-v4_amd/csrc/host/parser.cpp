@@ -334,6 +334,7 @@ class Parser {
         std::string areaLight;
         ParamSet areaParams;
         std::string loc;
+        std::string dir;  // directory of the declaring file (an area light's "filename")
         bool hasAlpha = false;  // "float alpha" < 1 or "texture alpha" (scene.cpp:1369-1384)
         Param alpha;
     };
@@ -360,6 +361,7 @@ class Parser {
     void ImageLight(PendingLight &l, const Mat4 &rfl, float sc, DeltaLightDesc *d);
     AreaLightDesc curSpread;  // the current AreaLightSource's spread terms
     void SetSpread(AreaLightDesc *l) const {
+        l->image = curSpread.image;
         l->cosFalloffEnd = curSpread.cosFalloffEnd;
         l->tanFalloffEnd = curSpread.tanFalloffEnd;
         l->normFalloffEnd = curSpread.normFalloffEnd;
@@ -1060,6 +1062,7 @@ class Parser {
         s.material = gs.material;
         s.areaLight = gs.areaLightName;
         s.areaParams = gs.areaLightParams;
+        s.dir = dir;
         s.insideMedium = gs.insideMedium;
         s.outsideMedium = gs.outsideMedium;
         s.loc = ps.loc;
@@ -1706,10 +1709,31 @@ void Parser::Finish() {
             // lights.cpp:909-939: an image-textured emitter ("filename") emits the image and
             // folds its average luminance into k_e; neither is on this path, so it is refused
             // rather than rendered with the default illuminant.
-            if (Param *fn = ap.Find("filename", "string")) {
+            curSpread.image = -1;
+            if (Param *fnp = ap.Find("filename", "string")) {
                 if (L) throw Error(ap.loc + ": Both \"L\" and \"filename\" specified for DiffuseAreaLight.");
-                (void)fn;
-                throw Error(ap.loc + ": \"filename\" (image) area lights not supported yet");
+                // an image emitter: R, G, B bilerped at the hit's (u, 1 - v) as an
+                // RGBIlluminantSpectrum; scale already divided by the colour space illuminant's
+                // photometric integral (no "L": the default above)
+                std::string fn = fnp->strs.empty() ? std::string() : fnp->strs[0];
+                if (!fn.empty() && fn[0] != '/' && !s.dir.empty()) fn = s.dir + "/" + fn;
+                LightImage im = LoadLightImage(fn, ap.loc);
+                for (float v : im.v) {
+                    if (std::isinf(v)) throw Error(ap.loc + ": " + fn + ": image has infinite pixel values and so is not suitable as a light.");
+                    if (std::isnan(v)) throw Error(ap.loc + ": " + fn + ": image has not-a-number pixel values and so is not suitable as a light.");
+                }
+                if (im.nc < 3) throw Error(ap.loc + ": " + fn + ": Image provided to \"diffuse\" area light must have R, G, and B channels.");
+                if (power > 0) throw Error(ap.loc + ": \"power\" for image area lights is not supported yet");
+                if (s.kind == kShapeSphereT || s.kind == kShapeDiskT || s.kind == kShapeCylinderT || !s.quadIdx.empty())
+                    throw Error(ap.loc + ": image area lights on spheres, disks, cylinders and bilinear patches are not supported yet");
+                AreaLightImage ai;
+                ai.w = im.w;
+                ai.h = im.h;
+                ai.rgb.resize((size_t)3 * im.w * im.h);
+                for (size_t q = 0; q < (size_t)im.w * im.h; ++q)
+                    for (int c = 0; c < 3; ++c) ai.rgb[3 * q + c] = im.v[q * im.nc + c];
+                curSpread.image = (int)scene.areaLightImages.size();
+                scene.areaLightImages.push_back(std::move(ai));
             }
             ap.CheckUnused();
             // DiffuseAreaLight::AlphaMasked (lights.h) masks the emission of an alpha-tested
@@ -1812,6 +1836,7 @@ void Parser::Finish() {
     const size_t nLights = scene.areaLights.size() + scene.deltaLights.size() +
                            (scene.infiniteLights.size() - distants.size());
     if (nLights == 0) throw Error("No light sources specified");
+
     if (nLights == 1) scene.uniformLightSampler = true;
 }
 

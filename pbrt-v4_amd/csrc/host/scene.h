@@ -185,6 +185,15 @@ struct AreaLightDesc {
     // cos(Radians(spread)) (> 0 only below 90 degrees), tanFalloffEnd = tan(Pi / 2 -
     // Radians(spread)), normalize_falloffEnd, all as the constructor computes them in float
     float cosFalloffEnd = -1, tanFalloffEnd = 0, normFalloffEnd = 0;
+    // DiffuseAreaLight with "filename" (lights.cpp:909-936): index into
+    // SceneDesc::areaLightImages (-1: the spectrum); L = scale * RGBIlluminantSpectrum of the
+    // image bilerped at (u, 1 - v), spectrum then holds the colour space's illuminant
+    int image = -1;
+};
+// an area light's emission image: linear R, G, B ([h][w][3], row 0 = top)
+struct AreaLightImage {
+    int w = 0, h = 0;
+    std::vector<float> rgb;
 };
 
 // Sphere / Disk / BilinearPatch (shapes.h:106-571, 1272-1540) in render space: the device record (affine render-from-object
@@ -293,6 +302,7 @@ struct SceneDesc {
     std::vector<int> triMaterial;   // material index
     std::vector<int> triLight;      // area light index or -1
     std::vector<uint8_t> triFlip;   // reverseOrientation ^ transformSwapsHandedness
+    std::vector<AreaLightImage> areaLightImages;
     std::vector<int> triAlpha;      // alphaTex entry or -1 (GeometricPrimitive alpha test)
     // alpha textures: {texture node, compiled float program}; shapes refer to them by index
     std::vector<std::array<int, 2>> alphaTex;

@@ -993,9 +993,11 @@ __device__ inline float SolidAngleOf(V3 p0, V3 p1, V3 p2, V3 p) {
 // Triangle::Sample(ctx, u) (shapes.h:1053-1130); returns false for {}.  The three directions
 // Normalize(p_i - refP) enter the solid angle, the bilinear warp weights and the spherical
 // sample; pbrt normalises them anew in each (same operations, same values), here once.
+// bOut (optional): the sample's barycentrics (the light's uv for an image emitter)
 template <bool Inl = false>
 __device__ inline bool SampleTriangle(V3 p0, V3 p1, V3 p2, bool flip, const TriShading *sh, V3 refP, V3 refN,
-                                      V3 refNs, float u0, float u1, V3 *ps, V3 *pErr, V3 *ns, float *pdfOut) {
+                                      V3 refNs, float u0, float u1, V3 *ps, V3 *pErr, V3 *ns, float *pdfOut,
+                                      float *bOut = nullptr) {
     (void)refN;
     const V3 wi0 = Normalize(p0 - refP), wi1 = Normalize(p1 - refP), wi2 = Normalize(p2 - refP);
     float solidAngle = SphericalTriangleArea(wi0, wi1, wi2);
@@ -1015,6 +1017,7 @@ __device__ inline bool SampleTriangle(V3 p0, V3 p1, V3 p2, bool flip, const TriS
         *ps = p;
         *ns = n;
         *pdfOut = pdf;
+        if (bOut) bOut[0] = b[0], bOut[1] = b[1], bOut[2] = b[2];
         return true;
     }
     float pdf = 1;
@@ -1046,6 +1049,7 @@ __device__ inline bool SampleTriangle(V3 p0, V3 p1, V3 p2, bool flip, const TriS
     *ps = p;
     *ns = n;
     *pdfOut = pdf;
+    if (bOut) bOut[0] = b[0], bOut[1] = b[1], bOut[2] = b[2];
     return true;
 }
 
@@ -1211,6 +1215,42 @@ __device__ inline float SmoothStepf(float x, float a, float b) {
     const float t = Clampf((x - a) / (b - a), 0, 1);
     return t * t * (3 - 2 * t);
 }
+// DiffuseAreaLight::L with an image (lights.h:460-467): R, G, B bilerped (Image::BilerpChannel,
+// clamp wrap) at (u, 1 - v), then the RGBIlluminantSpectrum of ClampZero(rgb) as {c0, c1, c2,
+// scale}; the radiance is EnvLe(coef, light scale, illuminant(lambda), lambda)
+__device__ inline EnvCoef AreaImageCoef(const DeviceScene &S, int off, float u, float v) {
+    const float *img = S.lightImg + off;
+    const int w = __float_as_int(img[0]), h = __float_as_int(img[1]);
+    const float *rgb = img + 2;
+    v = 1 - v;
+    const float x = u * w - 0.5f, y = v * h - 0.5f;
+    const int xi = (int)floorf(x), yi = (int)floorf(y);
+    const float dx = x - xi, dy = y - yi;
+    const int x0 = min(max(xi, 0), w - 1), x1 = min(max(xi + 1, 0), w - 1);
+    const int y0 = min(max(yi, 0), h - 1), y1 = min(max(yi + 1, 0), h - 1);
+    float c3[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float v00 = rgb[((size_t)y0 * w + x0) * 3 + c], v10 = rgb[((size_t)y0 * w + x1) * 3 + c];
+        const float v01 = rgb[((size_t)y1 * w + x0) * 3 + c], v11 = rgb[((size_t)y1 * w + x1) * 3 + c];
+        const float b = (1 - dx) * (1 - dy) * v00 + dx * (1 - dy) * v10 + (1 - dx) * dy * v01 + dx * dy * v11;
+        c3[c] = fmaxf(0.f, b);
+    }
+    const float m = fmaxf(c3[0], fmaxf(c3[1], c3[2])), scale = 2 * m;
+    float co[3];
+    if (scale != 0) RGBToCoeffs(S.tex, c3[0] / scale, c3[1] / scale, c3[2] / scale, co);
+    else RGBToCoeffs(S.tex, 0, 0, 0, co);
+    return EnvCoef{co[0], co[1], co[2], scale};
+}
+// the uv of a triangle point from its barycentrics (Triangle::Sample, shapes.h:1076-1078, 1120)
+__device__ inline void TriUV(const TriShading *sh, const float b[3], float *u, float *v) {
+    float uv[3][2] = {{0, 0}, {1, 0}, {1, 1}};
+    if (sh && (sh->flags & 2))
+        for (int k = 0; k < 3; ++k) uv[k][0] = sh->uv[k][0], uv[k][1] = sh->uv[k][1];
+    *u = b[0] * uv[0][0] + b[1] * uv[1][0] + b[2] * uv[2][0];
+    *v = b[0] * uv[0][1] + b[1] * uv[1][1] + b[2] * uv[2][1];
+}
+
 // This fork's DiffuseAreaLight spread (lights.h:451-458, lights.cpp:763-771).  cosE =
 // cosFalloffEnd, > 0 only for a spread below 90 degrees.  L() is zero where the emission
 // direction w leaves farther than the spread from the normal: AbsDot(w, n) < cosE.
@@ -1269,11 +1309,19 @@ __device__ inline bool SampleLiSurface(const DeviceScene &S, const DeviceAreaLig
         V3 q0(Ld.v0.x, Ld.v0.y, Ld.v0.z), q1(Ld.v1.x, Ld.v1.y, Ld.v1.z), q2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
         TriShading lsh;
         const bool lhas = !Lean && LoadTriShading(S, __float_as_int(Ld.v0.w), &lsh);
-        float lpdf;
+        float lpdf, lb[3];
         if (!SampleTriangle<Inl>(q0, q1, q2, Ld.flip, lhas ? &lsh : nullptr, cp, n, ns, u0, u1, &ls->lp, &ls->lpe, &ls->ln,
-                            &lpdf) ||
+                            &lpdf, (!Lean && Ext) ? lb : nullptr) ||
             lpdf == 0 || LengthSquared(ls->lp - cp) == 0)
             return false;
+        if constexpr (!Lean && Ext) {
+            if (S.nImageAreaLights > 0 && S.lightImgOff[li] >= 0) {  // an image emitter
+                float lu, lv;
+                TriUV(lhas ? &lsh : nullptr, lb, &lu, &lv);
+                ls->envLe = true;
+                ls->env = AreaImageCoef(S, S.lightImgOff[li], lu, lv);
+            }
+        }
         ls->wi = Normalize(ls->lp - cp);
         if (!(Ld.twoSided || DotN(ls->ln, -ls->wi) >= 0)) return false;  // DiffuseAreaLight::L is 0
         if constexpr (!Lean) {
@@ -1288,7 +1336,8 @@ __device__ inline bool SampleLiSurface(const DeviceScene &S, const DeviceAreaLig
         ls->d2 = 1;
         ls->spectrum = Ld.spectrum;
         ls->delta = false;
-        ls->envLe = false;
+        if constexpr (Lean || !Ext) ls->envLe = false;
+        else if (!(S.nImageAreaLights > 0 && S.lightImgOff[li] >= 0)) ls->envLe = false;
         return true;
     }
     if constexpr (Lean) {

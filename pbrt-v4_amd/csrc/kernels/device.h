@@ -182,6 +182,9 @@ struct DeviceScene {
     const DeviceDeltaLight *delta;
     const float *deltaImg;  // goniometric Y images and projection per-pixel EnvCoef
     const float *lightSpreadNorm;  // per area light: the spread's normalize_falloffEnd
+    const float *lightImg;         // DiffuseAreaLight emission images ({w, h} bits, R G B [h][w][3])
+    const int *lightImgOff;        // per area light: its image's offset in lightImg, or -1
+    int nImageAreaLights;          // image emitters (their kernels are the Ext ones)
     int hasSpread;                 // some area light has a spread below 90 degrees
     int nImageDelta;        // goniometric + projection lights (their kernels are the Ext ones)
     const int *uniformOrder;  // UniformLightSampler: pbrt's light order -> global index

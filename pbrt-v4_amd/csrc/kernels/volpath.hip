@@ -2351,7 +2351,7 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
         hipLaunchKernelGGL(k_queue_holes, dim3(64, kShards), block, 0, s, st.counters, wf, kVShadow, v.shPixel,      \
                            st.capS, QueueHoleCounter(), v, st.NR, stage);
     // Ext: analytic shapes or image lights in the scene (their paths compiled in)
-    if (S.nShapes > 0 || S.nEnv > 0 || S.nImageDelta > 0) {
+    if (S.nShapes > 0 || S.nEnv > 0 || S.nImageDelta > 0 || S.hasSpread) {
         if (S.matTypeMask & other) hipLaunchKernelGGL((k_vsurface<false, true>), gW, block, surfLds, s, S, st, v, wf);
         else hipLaunchKernelGGL((k_vsurface<true, true>), gW, block, surfLds, s, S, st, v, wf);
         QUEUE_CHECK(1);

@@ -515,12 +515,18 @@ __global__ void __launch_bounds__(kBlock) k_emissive(DeviceScene S, PathState st
         }
         const float *dense = S.dense + Ld.spectrum * kDenseN;
         const float invDenom = 1 / denom;
+        // an image emitter: L at the hit's uv (DiffuseAreaLight::L, lights.h:460-467)
+        const bool img = Ext && S.nImageAreaLights > 0 && S.lightImgOff[light] >= 0;
+        EnvCoef ec{};
+        if (img) ec = AreaImageCoef(S, S.lightImgOff[light], surf.uv[0], surf.uv[1]);
         SensorAcc acc;
         SpectralIter it(lambda0);
 #pragma unroll
         for (int i = 0; i < kNSpectrumSamples; ++i, it.Next()) {
             int off = DenseOffset(it.lam);
-            float Le = Ld.scale * (off < 0 ? 0.f : dense[off]);
+            const float dv = off < 0 ? 0.f : dense[off];
+            float Le = Ld.scale * dv;
+            if (img) Le = EnvLe(ec, Ld.scale, dv, it.lam);
             acc.Add(S, off, beta[i] * Le * invDenom, i == 0);
         }
         st.L[slot] += S.imagingRatio * (acc.sx / kNSpectrumSamples);
@@ -887,7 +893,8 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
                     float *bf = bfLds + threadIdx.x;
                     const float rd2 = 1 / d2;
                     const bool d2Ok = DivFastOk(d2);
-                    if (Lean || (lay.denseInLds && S.nPointSpot == 0 && (!Ext || S.nEnv == 0)))
+                    if (Lean || (lay.denseInLds && S.nPointSpot == 0 &&
+                                 (!Ext || (S.nEnv == 0 && !S.hasSpread && S.nImageAreaLights == 0))))
                         ShadeSpectralPass<false, false>(depth, (const LdsF *)denseLds + spec * kDenseN, sensorL, bf,
                                                         rfun, lambda0, scale, d2, rd2, d2Ok, absdotL, invDenom,
                                                         absdotB, pdf, rpdf, pdfOk, etaScale, &acc, &neeNz, &betaNz,
@@ -1632,7 +1639,8 @@ hipError_t LaunchEscaped(const DeviceScene &S, const PathState &st, int depth, i
     return hipGetLastError();
 }
 hipError_t LaunchEmissive(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s) {
-    if (S.nShapes > 0) hipLaunchKernelGGL(k_emissive<true>, dim3(SmallGridFor(maxCount)), dim3(kBlock), 0, s, S, st, depth);
+    if (S.nShapes > 0 || S.nImageAreaLights > 0)
+        hipLaunchKernelGGL(k_emissive<true>, dim3(SmallGridFor(maxCount)), dim3(kBlock), 0, s, S, st, depth);
     else hipLaunchKernelGGL(k_emissive<false>, dim3(SmallGridFor(maxCount)), dim3(kBlock), 0, s, S, st, depth);
     return hipGetLastError();
 }
@@ -1666,7 +1674,7 @@ hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int dep
                               hipStream_t s) {
     const dim3 grid(ShadeGridFor(maxCount)), block(kBlock);
     const size_t lds = ShadeLdsBytes(S, depth);
-    const bool ext = S.nShapes > 0 || S.nEnv > 0 || S.nImageDelta > 0;
+    const bool ext = S.nShapes > 0 || S.nEnv > 0 || S.nImageDelta > 0 || S.hasSpread || S.nImageAreaLights > 0;
     if (S.textured && ext) hipLaunchKernelGGL((k_shade_diffuse<false, true, true>), grid, block, lds, s, S, st, depth);
     else if (S.textured) hipLaunchKernelGGL((k_shade_diffuse<false, true>), grid, block, lds, s, S, st, depth);
     else if (lean) hipLaunchKernelGGL(k_shade_diffuse<true>, grid, block, lds, s, S, st, depth);
@@ -1678,7 +1686,7 @@ hipError_t LaunchShadeMicrofacet(const DeviceScene &S, const PathState &st, int 
                                  hipStream_t s) {
     const dim3 grid(ShadeGridFor(maxCount)), block(kBlock);
     const size_t lds = ShadeLdsBytes(S, depth, true);
-    const bool ext = S.nShapes > 0 || S.nEnv > 0 || S.nImageDelta > 0, diel = type == kMatDielectricT;
+    const bool ext = S.nShapes > 0 || S.nEnv > 0 || S.nImageDelta > 0 || S.hasSpread || S.nImageAreaLights > 0, diel = type == kMatDielectricT;
 #define K_MF(mt, smooth, tex, ex) hipLaunchKernelGGL((k_shade_microfacet<mt, smooth, tex, ex>), grid, block, lds, s, S, st, depth)
     if (ext) {
         if (diel && S.textured) K_MF(kMatDielectricT, false, true, true);

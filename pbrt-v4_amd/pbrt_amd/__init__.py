@@ -50,7 +50,8 @@ class SceneFlat(ctypes.Structure):
         ("tri_flip", ctypes.POINTER(ctypes.c_uint8)), ("material_coeffs", ctypes.POINTER(ctypes.c_float)),
         ("material_constant", ctypes.POINTER(ctypes.c_int32)), ("light_prim", ctypes.POINTER(ctypes.c_int32)),
         ("light_scale", ctypes.POINTER(ctypes.c_float)), ("light_spectrum", ctypes.POINTER(ctypes.c_int32)),
-        ("light_two_sided", ctypes.POINTER(ctypes.c_int32)), ("light_spread", ctypes.POINTER(ctypes.c_float)), ("inf_spectrum", ctypes.POINTER(ctypes.c_int32)),
+        ("light_two_sided", ctypes.POINTER(ctypes.c_int32)), ("light_spread", ctypes.POINTER(ctypes.c_float)),
+        ("light_image", ctypes.POINTER(ctypes.c_int32)), ("area_images", ctypes.POINTER(ctypes.c_float)), ("inf_spectrum", ctypes.POINTER(ctypes.c_int32)),
         ("inf_scale", ctypes.POINTER(ctypes.c_float)), ("dense_spectra", ctypes.POINTER(ctypes.c_float)),
         ("sensor_xyz", ctypes.POINTER(ctypes.c_float)), ("imaging_ratio", ctypes.c_float),
         ("camera_from_raster", ctypes.c_float * 16), ("render_from_camera", ctypes.c_float * 16),

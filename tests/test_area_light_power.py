@@ -52,12 +52,12 @@ def test_blackbody_emitter_matches_reference(pa, golden):
         assert f.light_scale[0] == pytest.approx(1 / float(e["photometric"][0]), rel=1e-5)
 
 
-def test_image_area_light_is_refused(pa):
-    """An image emitter ("string filename", lights.cpp:909-939) is not on this path: it must be
-    rejected with a located error instead of rendering the default illuminant, and "L" together
-    with "filename" is the reference's own error."""
+def test_image_area_light_errors(pa):
+    """An image emitter ("string filename", lights.cpp:909-939; tests/test_area_image_lights.py):
+    "L" together with "filename" is the reference's own error, and a missing file is a located
+    error rather than a silent default illuminant."""
     with pytest.raises(pa.PbrtError, match="Both \"L\" and \"filename\""):
         pa.Scene.from_string(SCENE.format(extra='"string filename" "emit.exr"'), SCENES)
     no_l = SCENE.replace('"rgb L" [ 2 3 4 ]', '"string filename" "emit.exr"')
-    with pytest.raises(pa.PbrtError, match="image\\) area lights not supported"):
+    with pytest.raises(pa.PbrtError, match="emit.exr: unable to open"):
         pa.Scene.from_string(no_l.format(extra=""), SCENES)

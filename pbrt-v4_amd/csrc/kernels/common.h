@@ -26,9 +26,6 @@ constexpr int kBlock = 256;
 // node loads hold 20 VGPRs instead of 60, and on C4 (10 M triangles) the traversal is bound by
 // dependent-load latency, so waves in flight are what pays (k_closest 65.1 -> 54.6 ms per pass:
 // wide at 4, quantised at 4 / 5 / 6 waves = 65.1 / 66.9 / 66.9 / 54.6 ms; tools/gpu_c4_occ.sh)
-#ifndef PBRT_PIPELINED_TRAVERSAL
-#define PBRT_PIPELINED_TRAVERSAL 1  // quantised HBM-resident trees: next node loaded beside the triangles
-#endif
 #ifndef PBRT_QUANT_TRAVERSAL_WAVES
 #define PBRT_QUANT_TRAVERSAL_WAVES 6
 #endif
@@ -269,9 +266,11 @@ __device__ inline int ProducerShard() { return blockIdx.x % kShards; }
 // dealt round-robin to those eight block groups: rays adjacent in the queue (bin order, or pixel
 // order at depth 0) meet the same L2 instead of being dealt chunk by chunk over all eight, and
 // the round-robin keeps the groups' work balanced (one contiguous eighth per group was measured
-// 18 % slower on C4: the sorted order's cost varies by region).  Speed only -- every chunk is
-// walked exactly once under any placement.  k = 0 (or a grid that is not a multiple of 8) is
-// the plain grid-stride walk.  Uniform per block, so a block whose walk is empty may return.
+// 18 % slower on C4: the sorted order's cost varies by region).  Super-chunks of 16 measured
+// neutral on C4 (k_closest 7434 vs 7410 us per launch, films bit-identical), so the default is
+// k = 0 (PBRT_AMD_XCD_GROUPS selects k).  Speed only -- every chunk is walked exactly once under
+// any placement.  k = 0 (or a grid that is not a multiple of 8) is the plain grid-stride walk.
+// Uniform per block, so a block whose walk is empty may return.
 struct ChunkWalk {
     int n, end, step, k, g;
     __device__ int Chunk() const { return k ? ((n / k) * 8 + g) * k + n % k : n; }
@@ -656,84 +655,6 @@ __device__ inline int TraverseCW(const DeviceScene &S, const SceneLds &L, V3 o, 
     const CwRay r = MakeCwRay(o, d, S.bvhAbsMax);
     LdsU2 *stk = L.stack + threadIdx.x;
     int sp = 0, node = 0, hitPrim = -1;
-    if constexpr (Compressed && !NodesInLds && PBRT_PIPELINED_TRAVERSAL) {
-        // HBM-resident quantised tree, software-pipelined: the next node is chosen from this
-        // node's child mask (computed before its triangles, as in the loop below, so the order
-        // of visits is unchanged) and its 80 B are loaded before this node's triangles, so the
-        // two loads are in flight together: one memory round trip per step instead of two.
-        NodeHits nh = S.ldsNodes > 0 ? VisitQuant(L.nodes, r, tMax)
-                                     : VisitQuant(reinterpret_cast<const float4 *>(S.qnodes), r, tMax);
-#ifdef PBRT_AMD_TRAV_STATS
-        if (cnt) ++cnt->nodes;
-#endif
-        while (true) {
-            uint32_t bits = PermuteOct(nh.inner, r.oct), gBase = (uint32_t)nh.childBase, gMask = nh.imask;
-            bool done = false;
-            if (bits == 0) {
-                if (sp == 0) {
-                    done = true;
-                } else {
-                    --sp;
-                    const uint2 e = stk[sp * kBlock];
-                    gBase = e.x;
-                    gMask = e.y >> 8;
-                    bits = e.y & 0xffu;
-                }
-            }
-            float4 f0, f1, f2, f3, f4;
-            if (!done) {
-                const uint32_t slot = (uint32_t)__builtin_ctz(bits) ^ r.oct;
-                bits &= bits - 1u;
-                node = (int)gBase + __popc(gMask & ((1u << slot) - 1u));
-                if (bits) {
-                    stk[sp * kBlock] = make_uint2(gBase, (gMask << 8) | bits);  // sp < S.stackSize by construction
-                    ++sp;
-                }
-                if (node < S.ldsNodes) {
-                    const LdsF4 *q = L.nodes + node * kLdsQNodeStride;
-                    f0 = q[0], f1 = q[1], f2 = q[2], f3 = q[3], f4 = q[4];
-                } else {
-                    const float4 *q = reinterpret_cast<const float4 *>(S.qnodes + node);
-                    f0 = q[0], f1 = q[1], f2 = q[2], f3 = q[3], f4 = q[4];
-                }
-            }
-            uint32_t tris = nh.tris;
-            while (tris) {
-                const int t = nh.triBase + __builtin_ctz(tris);
-                tris &= tris - 1u;
-#ifdef PBRT_AMD_TRAV_STATS
-                if (cnt) ++cnt->tris;
-#endif
-                V3 a, b, c;
-                if constexpr (TrisInLds) {
-                    const LdsF4 *v = L.tris + (tr.kz * S.ldsTris + t) * 3;
-                    const float4 va = v[0], vb = v[1], vc = v[2];
-                    a = V3(va.x, va.y, va.z), b = V3(vb.x, vb.y, vb.z), c = V3(vc.x, vc.y, vc.z);
-                } else {
-                    a = RotateToRay(S.triVerts[3 * t], tr.kz);
-                    b = RotateToRay(S.triVerts[3 * t + 1], tr.kz);
-                    c = RotateToRay(S.triVerts[3 * t + 2], tr.kz);
-                }
-                TriHit h;
-                if (IntersectTriangleRot(tr, tMax, a, b, c, &h)) {
-                    if constexpr (Alpha) {
-                        if (S.nAlpha > 0 && S.primAlpha[t] >= 0 && AlphaKilled(S.self, t, h.b0, h.b1, h.b2, o, d))
-                            continue;
-                    }
-                    if (AnyHit) return t;
-                    tMax = h.t;
-                    *best = h;
-                    hitPrim = t;
-                }
-            }
-            if (done) break;
-#ifdef PBRT_AMD_TRAV_STATS
-            if (cnt) ++cnt->nodes;
-#endif
-            nh = VisitQuantV(f0, f1, f2, f3, f4, r, tMax);
-        }
-        return hitPrim;
-    }
     while (true) {
         NodeHits nh;
 #ifdef PBRT_AMD_TRAV_STATS

@@ -42,6 +42,9 @@ rec = {
     "hbm_bytes_per_ray": round((fetch_b + write_b) / rays, 2),
     "fetched_bytes_per_ray": round(fetch_b / rays, 2),
     "algorithmic_bytes_per_ray": bench["roofline"]["bytes_per_ray"],
+    # SURVEY 8(d)'s BVH term (round 4): HBM-resident nodes + triangles touched once per launch
+    "bvh_bytes_per_launch": bench["roofline"].get("bvh_bytes_per_launch"),
+    "algorithmic_bytes_per_launch": bench["roofline"].get("algorithmic_bytes_per_launch"),
     "tcc_hit_per_launch": hit,
     "tcc_miss_per_launch": miss,
     "l2_hit_rate": round(hit / (hit + miss), 4),

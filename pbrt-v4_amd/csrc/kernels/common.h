@@ -29,6 +29,15 @@ constexpr int kBlock = 256;
 #ifndef PBRT_QUANT_TRAVERSAL_WAVES
 #define PBRT_QUANT_TRAVERSAL_WAVES 6
 #endif
+// k_closest's dynamic ray fetch (wavefront.hip) for triangle-only traversal modes, and the number
+// of idle lanes at which a wave refills
+#ifndef PBRT_DYN_FETCH
+#define PBRT_DYN_FETCH 0
+#endif
+#ifndef PBRT_DYN_REFILL
+#define PBRT_DYN_REFILL 16
+#endif
+constexpr bool kDynFetch = PBRT_DYN_FETCH != 0;
 #ifndef PBRT_SHADE_WAVES
 #define PBRT_SHADE_WAVES 3  // waves/SIMD the shade kernel is compiled for (VGPR budget)
 #endif
@@ -648,73 +657,95 @@ __device__ __attribute__((noinline)) bool AlphaKilled(const DeviceScene *S, int 
                                                      V3 o, V3 d);
 // Alpha: the scene has alpha-tested primitives (S.primAlpha); compiled into the kTravShapes
 // ("extended") instantiations only
+// One ray's resumable group traversal: TraverseCW runs CwStep to completion; k_closest's
+// dynamic-fetch loop (PBRT_DYN_FETCH) interleaves steps of different rays in one lane.
+struct CwState {
+    TriRayR tr;
+    CwRay r;
+    float tMax;
+    TriHit best;
+    int node, sp, hit;
+};
+__device__ inline void CwBegin(const DeviceScene &S, CwState &s, V3 o, V3 d, float tMax) {
+    s.tr = MakeTriRayR(o, d);
+    s.r = MakeCwRay(o, d, S.bvhAbsMax);
+    s.tMax = tMax;
+    s.node = s.sp = 0;
+    s.hit = -1;
+}
+// Visits s.node and its hit leaf triangles, then moves to the next node.  Returns true when the
+// ray is done (stack empty, or with AnyHit the first hit: s.hit).  o, d: the ray, for the alpha test.
+template <bool AnyHit, bool Compressed, bool NodesInLds, bool TrisInLds, bool Alpha>
+__device__ inline bool CwStep(const DeviceScene &S, const SceneLds &L, CwState &s, V3 o, V3 d, TravCount *cnt) {
+    LdsU2 *stk = L.stack + threadIdx.x;
+    NodeHits nh;
+#ifdef PBRT_AMD_TRAV_STATS
+    if (cnt) ++cnt->nodes;
+#endif
+    if constexpr (Compressed) {
+        if (NodesInLds || s.node < S.ldsNodes) nh = VisitQuant(L.nodes + s.node * kLdsQNodeStride, s.r, s.tMax);
+        else nh = VisitQuant(reinterpret_cast<const float4 *>(S.qnodes + s.node), s.r, s.tMax);
+    } else {
+        if (NodesInLds || s.node < S.ldsNodes) nh = VisitWide(L.nodes + s.node * kLdsNodeStride, s.r, s.tMax);
+        else nh = VisitWide(reinterpret_cast<const float4 *>(S.nodes + s.node), s.r, s.tMax);
+    }
+    // the node's hit leaf triangles, in leaf order
+    uint32_t tris = nh.tris;
+    while (tris) {
+        const int t = nh.triBase + __builtin_ctz(tris);
+        tris &= tris - 1u;
+#ifdef PBRT_AMD_TRAV_STATS
+        if (cnt) ++cnt->tris;
+#endif
+        V3 a, b, c;
+        if constexpr (TrisInLds) {
+            const LdsF4 *v = L.tris + (s.tr.kz * S.ldsTris + t) * 3;
+            const float4 va = v[0], vb = v[1], vc = v[2];
+            a = V3(va.x, va.y, va.z), b = V3(vb.x, vb.y, vb.z), c = V3(vc.x, vc.y, vc.z);
+        } else {
+            a = RotateToRay(S.triVerts[3 * t], s.tr.kz);
+            b = RotateToRay(S.triVerts[3 * t + 1], s.tr.kz);
+            c = RotateToRay(S.triVerts[3 * t + 2], s.tr.kz);
+        }
+        TriHit h;
+        if (IntersectTriangleRot(s.tr, s.tMax, a, b, c, &h)) {
+            if constexpr (Alpha) {
+                if (S.nAlpha > 0 && S.primAlpha[t] >= 0 && AlphaKilled(S.self, t, h.b0, h.b1, h.b2, o, d)) continue;
+            }
+            s.hit = t;
+            if (AnyHit) return true;
+            s.tMax = h.t;
+            s.best = h;
+        }
+    }
+    // next node: the nearest child of this node's group, else of the top stacked group
+    uint32_t bits = PermuteOct(nh.inner, s.r.oct), gBase = (uint32_t)nh.childBase, gMask = nh.imask;
+    if (bits == 0) {
+        if (s.sp == 0) return true;
+        --s.sp;
+        const uint2 e = stk[s.sp * kBlock];
+        gBase = e.x;
+        gMask = e.y >> 8;
+        bits = e.y & 0xffu;
+    }
+    const uint32_t slot = (uint32_t)__builtin_ctz(bits) ^ s.r.oct;
+    bits &= bits - 1u;
+    s.node = (int)gBase + __popc(gMask & ((1u << slot) - 1u));
+    if (bits) {
+        stk[s.sp * kBlock] = make_uint2(gBase, (gMask << 8) | bits);  // sp < S.stackSize by construction
+        ++s.sp;
+    }
+    return false;
+}
 template <bool AnyHit, bool Compressed, bool NodesInLds, bool TrisInLds, bool Alpha = false>
 __device__ inline int TraverseCW(const DeviceScene &S, const SceneLds &L, V3 o, V3 d, float tMax, TriHit *best,
                                  TravCount *cnt = nullptr) {
-    const TriRayR tr = MakeTriRayR(o, d);
-    const CwRay r = MakeCwRay(o, d, S.bvhAbsMax);
-    LdsU2 *stk = L.stack + threadIdx.x;
-    int sp = 0, node = 0, hitPrim = -1;
-    while (true) {
-        NodeHits nh;
-#ifdef PBRT_AMD_TRAV_STATS
-        if (cnt) ++cnt->nodes;
-#endif
-        if constexpr (Compressed) {
-            if (NodesInLds || node < S.ldsNodes) nh = VisitQuant(L.nodes + node * kLdsQNodeStride, r, tMax);
-            else nh = VisitQuant(reinterpret_cast<const float4 *>(S.qnodes + node), r, tMax);
-        } else {
-            if (NodesInLds || node < S.ldsNodes) nh = VisitWide(L.nodes + node * kLdsNodeStride, r, tMax);
-            else nh = VisitWide(reinterpret_cast<const float4 *>(S.nodes + node), r, tMax);
-        }
-        // the node's hit leaf triangles, in leaf order
-        uint32_t tris = nh.tris;
-        while (tris) {
-            const int t = nh.triBase + __builtin_ctz(tris);
-            tris &= tris - 1u;
-#ifdef PBRT_AMD_TRAV_STATS
-            if (cnt) ++cnt->tris;
-#endif
-            V3 a, b, c;
-            if constexpr (TrisInLds) {
-                const LdsF4 *v = L.tris + (tr.kz * S.ldsTris + t) * 3;
-                const float4 va = v[0], vb = v[1], vc = v[2];
-                a = V3(va.x, va.y, va.z), b = V3(vb.x, vb.y, vb.z), c = V3(vc.x, vc.y, vc.z);
-            } else {
-                a = RotateToRay(S.triVerts[3 * t], tr.kz);
-                b = RotateToRay(S.triVerts[3 * t + 1], tr.kz);
-                c = RotateToRay(S.triVerts[3 * t + 2], tr.kz);
-            }
-            TriHit h;
-            if (IntersectTriangleRot(tr, tMax, a, b, c, &h)) {
-                if constexpr (Alpha) {
-                    if (S.nAlpha > 0 && S.primAlpha[t] >= 0 && AlphaKilled(S.self, t, h.b0, h.b1, h.b2, o, d)) continue;
-                }
-                if (AnyHit) return t;
-                tMax = h.t;
-                *best = h;
-                hitPrim = t;
-            }
-        }
-        // next node: the nearest child of this node's group, else of the top stacked group
-        uint32_t bits = PermuteOct(nh.inner, r.oct), gBase = (uint32_t)nh.childBase, gMask = nh.imask;
-        if (bits == 0) {
-            if (sp == 0) break;
-            --sp;
-            const uint2 e = stk[sp * kBlock];
-            gBase = e.x;
-            gMask = e.y >> 8;
-            bits = e.y & 0xffu;
-        }
-        const uint32_t slot = (uint32_t)__builtin_ctz(bits) ^ r.oct;
-        bits &= bits - 1u;
-        node = (int)gBase + __popc(gMask & ((1u << slot) - 1u));
-        if (bits) {
-            stk[sp * kBlock] = make_uint2(gBase, (gMask << 8) | bits);  // sp < S.stackSize by construction
-            ++sp;
-        }
+    CwState s;
+    CwBegin(S, s, o, d, tMax);
+    while (!CwStep<AnyHit, Compressed, NodesInLds, TrisInLds, Alpha>(S, L, s, o, d, cnt)) {
     }
-    return hitPrim;
+    if (!AnyHit && s.hit >= 0) *best = s.best;
+    return s.hit;
 }
 
 // Traversal modes, one kernel instantiation each (a launch-uniform choice, so every kernel

@@ -95,26 +95,10 @@ __global__ void __launch_bounds__(kBlock, TraversalWaves(TM))
         atomicAdd(&st.stats[1], (unsigned long long)count);
         if (timed) atomicAdd(&st.stats[3], (unsigned long long)count);  // rays of event-timed launches
     }
-    for (; walk.n < walk.end; walk.n += walk.step) {
-        const int j = walk.Chunk() * blockDim.x + threadIdx.x;
-        bool active = j < count;
-        int qi = 0;  // record index of this depth
-        int prim = -1;
-        TriHit h;
-        TravCount tc;
+    // A traced ray's results (every lane of the wave calls it; active: this lane has one): the
+    // hit record, and unless the depth was binned the queue entries
+    auto finish = [&](bool active, int qi, int prim, const TriHit &h, V3 d) {
         if (active) {
-            V3 o, d;
-            if (sorted) {
-                const float4 a = st.raySort[j], b = st.raySort[(size_t)N + j];
-                qi = __float_as_int(a.w);
-                o = V3(a.x, a.y, a.z);
-                d = V3(b.x, b.y, b.z);
-            } else {
-                qi = QueueSlot(rays, j);
-                o = V3(rec.ray[qi], rec.ray[N + qi], rec.ray[2 * N + qi]);
-                d = V3(rec.ray[3 * N + qi], rec.ray[4 * N + qi], rec.ray[5 * N + qi]);
-            }
-            prim = Traverse<false, TM>(S, L, o, d, kInfinity, &h, &tc);
             if (sorted) {
                 hitPrim[qi] = prim;
                 if (prim >= 0) {
@@ -138,10 +122,7 @@ __global__ void __launch_bounds__(kBlock, TraversalWaves(TM))
                 hitB[3 * N + qi] = h.t;
             }
         }
-        if (sorted) {  // k_classify enqueues
-            TravStatsAdd(st.stats, kStatsSectionBase + 8, active, tc);
-            continue;
-        }
+        if (sorted) return;  // k_classify enqueues
         // EnqueueWorkAfterIntersection / Miss (intersect.h:48-156): misses to the escaped-ray
         // queue (infinite lights only), emissive hits to the hit-area-light queue, every hit
         // to its material queue
@@ -154,10 +135,7 @@ __global__ void __launch_bounds__(kBlock, TraversalWaves(TM))
             if (shade && active && prim >= 0) {
                 int mat = S.primMaterial[prim];
                 if constexpr (kMix) {
-                    if (S.matType[mat] == kMatMixT) {
-                        const V3 d(rec.ray[3 * N + qi], rec.ray[4 * N + qi], rec.ray[5 * N + qi]);
-                        mat = ResolveMixMaterial(*S.self, prim, mat, h.b0, h.b1, h.b2, d);
-                    }
+                    if (S.matType[mat] == kMatMixT) mat = ResolveMixMaterial(*S.self, prim, mat, h.b0, h.b1, h.b2, d);
                     st.hitMat[depth & 1][qi] = mat;
                 }
                 type = S.matType[mat];
@@ -166,6 +144,78 @@ __global__ void __launch_bounds__(kBlock, TraversalWaves(TM))
             for (int t = 0; t < NMatQ; ++t) pred[2 + t] = type == t;
         }
         queues.Append(pred, qi);
+    };
+    auto fetch = [&](int j, int &qi, V3 &o, V3 &d) {
+        if (sorted) {
+            const float4 a = st.raySort[j], b = st.raySort[(size_t)N + j];
+            qi = __float_as_int(a.w);
+            o = V3(a.x, a.y, a.z);
+            d = V3(b.x, b.y, b.z);
+        } else {
+            qi = QueueSlot(rays, j);
+            o = V3(rec.ray[qi], rec.ray[N + qi], rec.ray[2 * N + qi]);
+            d = V3(rec.ray[3 * N + qi], rec.ray[4 * N + qi], rec.ray[5 * N + qi]);
+        }
+    };
+    if constexpr (kDynFetch && (TM & kTravShapes) == 0) {
+        // Dynamic ray fetch (Aila & Laine 2009, "speculative"/"replacing" traversal): a lane
+        // whose ray is done takes the next ray of its wave's stream once PBRT_DYN_REFILL lanes
+        // are idle, instead of idling until the wave's slowest ray finishes (C4: 12.7 nodes per
+        // ray against a wave maximum of 28.7, profiles/r04_c4_trav_stats.json).  A wave's
+        // stream is the 64-ray chunks w, w + W, w + 2W, ... (W waves in the grid); finished
+        // rays are recorded and enqueued at the refills, with every lane of the wave present.
+        constexpr int tm = TM & 3;
+        const int wpb = (int)blockDim.x >> 6, nw = (int)gridDim.x * wpb;
+        const int w = (int)blockIdx.x * wpb + ((int)threadIdx.x >> 6);
+        const int nChunks = (count + 63) >> 6;
+        const int end = (nChunks > w ? (nChunks - w + nw - 1) / nw : 0) * 64;  // stream positions
+        const unsigned long long below = (1ull << __lane_id()) - 1ull;
+        int pos = 0, qi = 0;
+        bool busy = false, done = false;
+        V3 d(0.f, 0.f, 0.f);
+        CwState s;
+        while (true) {
+            const unsigned long long idle = __ballot(!busy);
+            const bool feed = pos < end;
+            if ((feed && __popcll(idle) >= PBRT_DYN_REFILL) || idle == ~0ull) {
+                finish(done, qi, s.hit, s.best, d);
+                done = false;
+                if (feed) {
+                    const int p = pos + __popcll(idle & below);
+                    pos += __popcll(idle);
+                    if (!busy && p < end) {
+                        const int j = (w + (p >> 6) * nw) * 64 + (p & 63);
+                        if (j < count) {
+                            V3 o;
+                            fetch(j, qi, o, d);
+                            CwBegin(S, s, o, d, kInfinity);
+                            busy = true;
+                        }
+                    }
+                }
+                if (pos >= end && __ballot(busy) == 0) break;
+            }
+            if (busy && CwStep<false, tm == kTravQuant, tm == kTravLds, tm == kTravLds, false>(S, L, s, d, d, nullptr)) {
+                busy = false;
+                done = true;
+            }
+        }
+        queues.FlushAll();
+        return;
+    }
+    for (; walk.n < walk.end; walk.n += walk.step) {
+        const int j = walk.Chunk() * blockDim.x + threadIdx.x;
+        bool active = j < count;
+        int qi = 0;  // record index of this depth
+        int prim = -1;
+        TriHit h;
+        TravCount tc;
+        V3 o, d;
+        if (active) {
+            fetch(j, qi, o, d);
+            prim = Traverse<false, TM>(S, L, o, d, kInfinity, &h, &tc);
+        }
+        finish(active, qi, prim, h, d);
         TravStatsAdd(st.stats, kStatsSectionBase + 8, active, tc);
     }
     queues.FlushAll();

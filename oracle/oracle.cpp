@@ -3082,6 +3082,43 @@ struct Media {
             return mp;
         }
         Vec q = Offset(m, ToMedium(m, p));
+        if (I[0] == 3) {
+            // RGBGridMedium::SamplePoint (media.h:377-400): per-wavelength trilinear lookups of
+            // the voxels' RGBUnboundedSpectrum / RGBIlluminantSpectrum samples; voxel k of
+            // block b is {c0, c1, c2, scale} at medium_values[I[11] + 4 (b n + k)]
+            const int nx = I[5], ny = I[6], nz = I[7];
+            const size_t n = (size_t)nx * ny * nz;
+            const Spectrum illum = Dense(I[3], lambda);
+            auto lookup = [&](int b) {
+                const float *g = f->medium_values + I[11] + 4 * b * n;
+                auto at = [&](int x, int y, int z) {
+                    Spectrum s(0.f);
+                    if (x < 0 || x >= nx || y < 0 || y >= ny || z < 0 || z >= nz) return s;
+                    const float *c = g + 4 * (((size_t)z * ny + y) * nx + x);
+                    for (int i = 0; i < NS; ++i) s[i] = c[3] * Sigmoid(c[0], c[1], c[2], lambda.lambda[i]);
+                    return b == 2 ? s * illum : s;
+                };
+                Float sx = q.x * nx - .5f, sy = q.y * ny - .5f, sz = q.z * nz - .5f;
+                int ix = (int)std::floor(sx), iy = (int)std::floor(sy), iz = (int)std::floor(sz);
+                Float dx = sx - ix, dy = sy - iy, dz = sz - iz;
+                auto SLerp = [](Float t, const Spectrum &a, const Spectrum &b) {
+                    Spectrum r;
+                    for (int i = 0; i < NS; ++i) r[i] = Lerp(t, a[i], b[i]);
+                    return r;
+                };
+                Spectrum d00 = SLerp(dx, at(ix, iy, iz), at(ix + 1, iy, iz));
+                Spectrum d10 = SLerp(dx, at(ix, iy + 1, iz), at(ix + 1, iy + 1, iz));
+                Spectrum d01 = SLerp(dx, at(ix, iy, iz + 1), at(ix + 1, iy, iz + 1));
+                Spectrum d11 = SLerp(dx, at(ix, iy + 1, iz + 1), at(ix + 1, iy + 1, iz + 1));
+                return SLerp(dz, SLerp(dy, d00, d10), SLerp(dy, d01, d11));
+            };
+            const Float sigmaScale = Params(m)[7];
+            mp.sigma_a = ((I[15] & 1) ? lookup(0) : Spectrum(1.f)) * sigmaScale;
+            mp.sigma_s = ((I[15] & 2) ? lookup(1) : Spectrum(1.f)) * sigmaScale;
+            const Float LeScale = f->medium_values[I[12]];
+            if ((I[15] & 4) && LeScale > 0) mp.Le = lookup(2) * LeScale;
+            return mp;
+        }
         Float d = GridLookup(f->medium_values + I[11], I[5], I[6], I[7], q);
         mp.sigma_a = mp.sigma_a * d;
         mp.sigma_s = mp.sigma_s * d;
@@ -5550,6 +5587,27 @@ int oracle_cloud_density(const float *c, const float *pts, int n, float *out) {
         out[5 * i + 2] = (Media::NoiseAt(perm, p.x + 0.f, p.y + d, p.z + 0.f) - nz) / d;
         out[5 * i + 3] = (Media::NoiseAt(perm, p.x + 0.f, p.y + 0.f, p.z + d) - nz) / d;
         out[5 * i + 4] = Media::CloudDensity(c, p);
+    }
+    return 0;
+}
+
+// Medium::SamplePoint of medium `medium` at render-space points and the given wavelengths
+// (lambdas [n][31]) -> out [n][3][31]: sigma_a, sigma_s, Le
+int oracle_medium_point(const pbrt_scene_flat *flat, int medium, const float *pts, const float *lambdas, int n,
+                        float *out) {
+    if (medium < 0 || medium >= flat->n_media) return -1;
+    Media M;
+    M.f = flat;
+    M.n = flat->n_media;
+    for (int i = 0; i < n; ++i) {
+        Wavelengths lam = Wavelengths::SampleUniform(0.f);
+        for (int k = 0; k < NS; ++k) lam.lambda[k] = lambdas[NS * i + k];
+        const MediumProps mp = M.SamplePoint(medium, Vec(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]), lam);
+        for (int k = 0; k < NS; ++k) {
+            out[(3 * i) * NS + k] = mp.sigma_a[k];
+            out[(3 * i + 1) * NS + k] = mp.sigma_s[k];
+            out[(3 * i + 2) * NS + k] = mp.Le[k];
+        }
     }
     return 0;
 }

@@ -56,6 +56,7 @@ def lib():
         _lib.oracle_shape_eval.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_int, vp]
         _lib.oracle_equal_area.argtypes = [ctypes.c_int, vp, ctypes.c_int, vp]
         _lib.oracle_cloud_density.argtypes = [vp, vp, ctypes.c_int, vp]
+        _lib.oracle_medium_point.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_int, vp]
         _lib.oracle_camera_min_diff.argtypes = [vp, vp, vp]
         _lib.oracle_image_level.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int64,
                                             ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
@@ -113,6 +114,18 @@ def cloud_density(params3, points):
     pts = f32(points).reshape(-1, 3)
     out = np.zeros((len(pts), 5), np.float32)
     assert lib().oracle_cloud_density(c.ctypes.data, pts.ctypes.data, len(pts), out.ctypes.data) == 0
+    return out
+
+
+def medium_point(scene, medium, points, lambdas):
+    """Medium::SamplePoint at render-space points and wavelengths [n, 31] -> float32 [n, 3, 31]
+    (sigma_a, sigma_s, Le)"""
+    flat = scene.flat()
+    pts = f32(points).reshape(-1, 3)
+    lam = f32(lambdas).reshape(-1, 31)
+    out = np.zeros((len(pts), 3, 31), np.float32)
+    assert lib().oracle_medium_point(ctypes.byref(flat), medium, pts.ctypes.data, lam.ctypes.data, len(pts),
+                                     out.ctypes.data) == 0
     return out
 
 

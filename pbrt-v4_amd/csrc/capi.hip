@@ -83,12 +83,12 @@ static void MediumTables(const SceneDesc &s, std::vector<int32_t> *info, std::ve
             const auto &d = s.denseSpectra[idx];
             return std::all_of(d.begin(), d.end(), [&](float v) { return v == d[0]; });
         };
-        const int grey = flat(m.sigmaA) && flat(m.sigmaS) ? 1 : 0;
+        const int grey = m.type != kMediumRGBGrid && flat(m.sigmaA) && flat(m.sigmaS) ? 1 : 0;
         info->insert(info->end(), {m.type, m.sigmaA, m.sigmaS, m.Le, m.emissive ? 1 : 0, m.nx, m.ny, m.nz, m.lnx, m.lny,
-                                   m.lnz, dOff, lOff, mOff, grey, 0});
+                                   m.lnz, dOff, lOff, mOff, grey, m.rgbGrids});
         const V3 lo(std::min(m.p0.x, m.p1.x), std::min(m.p0.y, m.p1.y), std::min(m.p0.z, m.p1.z));
         const V3 hi(std::max(m.p0.x, m.p1.x), std::max(m.p0.y, m.p1.y), std::max(m.p0.z, m.p1.z));
-        params->insert(params->end(), {m.g, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, 0.f});
+        params->insert(params->end(), {m.g, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, m.sigmaScale});
         Mat4 inv = m.type != kMediumHomogeneous ? Inverse4(m.renderFromMedium) : Identity4();
         for (int i = 0; i < 4; ++i)
             for (int j = 0; j < 4; ++j) params->push_back((float)inv[i][j]);
@@ -974,7 +974,8 @@ static void BuildDevice(pbrt_context *c) {
     for (size_t m = 0; m < s.media.size(); ++m) {
         const auto &a = s.denseSpectra[s.media[m].sigmaA], &b = s.denseSpectra[s.media[m].sigmaS];
         if (!std::all_of(a.begin(), a.end(), [&](float x) { return x == a[0]; }) ||
-            !std::all_of(b.begin(), b.end(), [&](float x) { return x == b[0]; }))
+            !std::all_of(b.begin(), b.end(), [&](float x) { return x == b[0]; }) ||
+            s.media[m].type == kMediumRGBGrid)  // spectra per voxel (its dense sigma_a / sigma_s are 1 / 0)
             S.media.allGrey = 0;
     }
     if (getenv("PBRT_AMD_SPECTRAL_MEDIA")) S.media.allGrey = 0;

@@ -1311,6 +1311,96 @@ static void BuildMajorantGrid(MediumDesc &m) {
             }
 }
 
+// RGBGridMedium::Create (media.cpp:382-452) and its constructor's majorant grid (:339-380):
+// per voxel RGBUnboundedSpectrum / RGBIlluminantSpectrum(sRGB, rgb) as {c0, c1, c2, scale}
+// (scale = 2 max(r, g, b), coefficients of rgb / scale); majorant voxel = sigmaScale *
+// (max of sigma_a's MaxValue, or 1 without sigma_a) + (the same for sigma_s).
+static void BuildRGBGridMedium(ParamSet &ps, MediumDesc &m) {
+    m.type = kMediumRGBGrid;
+    auto rgbArray = [&](const char *name) {
+        std::vector<float> v;
+        if (Param *p = ps.Find(name)) {
+            if (p->type != "rgb" || p->nums.size() % 3)
+                throw Error(ps.loc + ": \"" + name + "\" of an RGB grid medium must be \"rgb\" values");
+            for (double x : p->nums) v.push_back((float)x);
+        }
+        return v;
+    };
+    const std::vector<float> grids[3] = {rgbArray("sigma_a"), rgbArray("sigma_s"), rgbArray("Le")};
+    const std::vector<float> &a = grids[0], &s = grids[1], &le = grids[2];
+    if (a.empty() && s.empty())
+        throw Error(ps.loc + ": RGB grid requires \"sigma_a\" and/or \"sigma_s\" parameter values.");
+    const size_t n = (a.empty() ? s.size() : a.size()) / 3;
+    if (!a.empty() && !s.empty() && a.size() != s.size())
+        throw Error(ps.loc + ": Different number of samples (" + std::to_string(n) + " vs " +
+                    std::to_string(s.size() / 3) + ") provided for \"sigma_a\" and \"sigma_s\".");
+    if (!le.empty() && a.empty()) throw Error(ps.loc + ": RGB grid requires \"sigma_a\" if \"Le\" value provided.");
+    if (!le.empty() && le.size() / 3 != n)
+        throw Error(ps.loc + ": Expected " + std::to_string(n) + " values for \"Le\" parameter but were given " +
+                    std::to_string(le.size() / 3) + ".");
+    m.nx = ps.GetInt("nx", 1);
+    m.ny = ps.GetInt("ny", 1);
+    m.nz = ps.GetInt("nz", 1);
+    if ((long)n != (long)m.nx * m.ny * m.nz)
+        throw Error(ps.loc + ": RGB grid medium has " + std::to_string(n) + " density values; expected nx*ny*nz = " +
+                    std::to_string((long)m.nx * m.ny * m.nz));
+    m.density.assign(12 * n, 0.f);
+    m.rgbGrids = 0;
+    for (int k = 0; k < 3; ++k) {
+        if (grids[k].empty()) continue;
+        m.rgbGrids |= 1 << k;
+        for (size_t i = 0; i < n; ++i) {
+            const float r = grids[k][3 * i], g = grids[k][3 * i + 1], b = grids[k][3 * i + 2];
+            if (r < 0 || g < 0 || b < 0) throw Error(ps.loc + ": RGB grid medium value has a negative component.");
+            const float scale = 2 * std::max({r, g, b});
+            const std::array<float, 3> c = scale ? RGBToSigmoidCoeffs(r / scale, g / scale, b / scale)
+                                                 : RGBToSigmoidCoeffs(0, 0, 0);
+            float *d = &m.density[(size_t)k * 4 * n + 4 * i];
+            d[0] = c[0], d[1] = c[1], d[2] = c[2], d[3] = scale;
+        }
+    }
+    if (Param *p0 = ps.Find("p0", "point3")) m.p0 = V3((float)p0->nums[0], (float)p0->nums[1], (float)p0->nums[2]);
+    if (Param *p1 = ps.Find("p1", "point3")) m.p1 = V3((float)p1->nums[0], (float)p1->nums[1], (float)p1->nums[2]);
+    const float LeScale = (float)ps.GetFloat("Lescale", 1);
+    m.g = (float)ps.GetFloat("g", 0);
+    m.sigmaScale = (float)ps.GetFloat("scale", 1);
+    m.LeScale = {LeScale};
+    m.emissive = !le.empty() && LeScale > 0;  // IsEmissive
+    // RGBSigmoidPolynomial::MaxValue (util/color.h:346-352) times the voxel's scale
+    auto maxOf = [&](int k, size_t i) {
+        const float *c = &m.density[(size_t)k * 4 * n + 4 * i];
+        auto f = [&](float l) { return SigmoidPolynomial(c[0], c[1], c[2], l); };
+        float r = std::max(f(360), f(830));
+        const float lambda = -c[1] / (2 * c[0]);
+        if (lambda >= 360 && lambda <= 830) r = std::max(r, f(lambda));
+        return c[3] * r;
+    };
+    const int R = 16, nn[3] = {m.nx, m.ny, m.nz};  // MajorantGrid res {16, 16, 16}
+    m.majorant.assign(R * R * R, 0.f);
+    for (int z = 0; z < R; ++z)
+        for (int y = 0; y < R; ++y)
+            for (int x = 0; x < R; ++x) {
+                const float b0[3] = {float(x) / R, float(y) / R, float(z) / R};
+                const float b1[3] = {float(x + 1) / R, float(y + 1) / R, float(z + 1) / R};
+                int lo[3], hi[3];
+                for (int ax = 0; ax < 3; ++ax) {
+                    lo[ax] = std::max((int)std::floor(b0[ax] * nn[ax] - .5f), 0);
+                    hi[ax] = std::min((int)std::floor(b1[ax] * nn[ax] - .5f) + 1, nn[ax] - 1);
+                }
+                // SampledGrid::MaxValue (util/containers.h:838-854)
+                auto gridMax = [&](int k) {
+                    float v = maxOf(k, ((size_t)lo[2] * m.ny + lo[1]) * m.nx + lo[0]);
+                    for (int zz = lo[2]; zz <= hi[2]; ++zz)
+                        for (int yy = lo[1]; yy <= hi[1]; ++yy)
+                            for (int xx = lo[0]; xx <= hi[0]; ++xx)
+                                v = std::max(v, maxOf(k, ((size_t)zz * m.ny + yy) * m.nx + xx));
+                    return v;
+                };
+                const float maxSigmaT = (a.empty() ? 1.f : gridMax(0)) + (s.empty() ? 1.f : gridMax(1));
+                m.majorant[x + R * (y + R * z)] = m.sigmaScale * maxSigmaT;
+            }
+}
+
 static std::array<float, 311> MediumSpectrum(ParamSet &ps, const char *name, bool illuminant, float defaultValue,
                                              bool *given, float *photometric) {
     Param *p = ps.Find(name);
@@ -1536,6 +1626,25 @@ void Parser::Finish() {
             if (p0) m.p0 = V3((float)p0->nums[0], (float)p0->nums[1], (float)p0->nums[2]);
             if (p1) m.p1 = V3((float)p1->nums[0], (float)p1->nums[1], (float)p1->nums[2]);
             m.renderFromMedium = Mul(scene.camera.renderFromWorld, pm.worldFromMedium);
+            ps.Find("type");
+            ps.CheckUnused();
+            mediumIndex[pm.name] = (int)scene.media.size();
+            scene.media.push_back(std::move(m));
+            continue;
+        }
+        if (pm.type == "rgbgrid") {
+            BuildRGBGridMedium(ps, m);
+            m.renderFromMedium = Mul(scene.camera.renderFromWorld, pm.worldFromMedium);
+            // SampleT_maj's sigma_t is SampledSpectrum(1) (media.h:411-414): sigma_a "ones",
+            // sigma_s zero; Le is the colour space's illuminant (RGBIlluminantSpectrum)
+            std::array<float, 311> ones, zero{};
+            ones.fill(1.f);
+            scene.denseSpectra.push_back(ones);
+            m.sigmaA = (int)scene.denseSpectra.size() - 1;
+            scene.denseSpectra.push_back(zero);
+            m.sigmaS = (int)scene.denseSpectra.size() - 1;
+            scene.denseSpectra.push_back(GetSpectralData().denseD65);
+            m.Le = (int)scene.denseSpectra.size() - 1;
             ps.Find("type");
             ps.CheckUnused();
             mediumIndex[pm.name] = (int)scene.media.size();

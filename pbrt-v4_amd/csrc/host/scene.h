@@ -45,7 +45,7 @@ constexpr int kMatMix = 8;
 // 395..705 nm tables in SceneDesc::denseSpectra with pbrt's constructor scaling applied
 // (sigma_a/sigma_s *= "scale"; homogeneous Le *= "Lescale" / photometric).
 // CloudMedium (media.h:430-525): procedural Perlin-noise density in [p0, p1], homogeneous majorant
-enum MediumType : int { kMediumHomogeneous = 0, kMediumGrid = 1, kMediumCloud = 2 };
+enum MediumType : int { kMediumHomogeneous = 0, kMediumGrid = 1, kMediumCloud = 2, kMediumRGBGrid = 3 };
 struct MediumDesc {
     int type = kMediumHomogeneous;
     std::string name;
@@ -61,6 +61,10 @@ struct MediumDesc {
     int lnx = 1, lny = 1, lnz = 1;         // LeScale grid (1x1x1 = {1 / photometric(Le)})
     std::vector<float> LeScale;
     std::vector<float> majorant;           // 16^3 MaxValue of density per majorant voxel
+    // RGBGridMedium ("rgbgrid"): density holds three [nz][ny][nx][4] blocks of {c0, c1, c2, scale}
+    // (sigma_a, sigma_s, Le; bit k of rgbGrids: block k given), LeScale = {"Lescale"}
+    int rgbGrids = 0;
+    float sigmaScale = 0;
 };
 
 struct MaterialDesc {

@@ -90,6 +90,10 @@ PHD int LdsNodeStride(int compressed) { return compressed ? kLdsQNodeStride : kL
 // nullptr when no triangle is a medium boundary.
 constexpr int kDevMediumGrid = 1;   // info[0] (scene.h MediumType)
 constexpr int kDevMediumCloud = 2;  // density / wispiness / frequency + noise permutation at info[11]
+// RGBGridMedium: per voxel {c0, c1, c2, scale} of sigma_a, sigma_s and Le (three [nz][ny][nx]
+// blocks at info[11]), info[15] bit 0 / 1 / 2: the grid is given; params[7] = sigmaScale,
+// values[info[12]] = LeScale
+constexpr int kDevMediumRGBGrid = 3;
 constexpr int kMajorantRes = 16;
 struct DeviceMedia {
     int n;             // media in the scene (0: the surface-only kernels run)

@@ -88,15 +88,69 @@ __device__ inline float GridLookup(const float *v, int nx, int ny, int nz, V3 p)
 // Medium::SamplePoint (media.h:209-350) reduced to its scalars: sigma_a = dense(I[1]) * d,
 // sigma_s = dense(I[2]) * d, Le = dense(I[3]) * le (le = 0: no emission at p).  Homogeneous:
 // d = le = 1 (x * 1 is exact, so the spectra are the reference's).
+// RGBGridMedium (media.h:355-428): rgb, and the trilinear lookup's voxel and offsets, from which
+// MediumSigmaA / MediumSigmaS / MediumLe evaluate the spectra per wavelength.
 struct MediumPoint {
     float d, le;
+    bool rgb;
+    int ix, iy, iz;
+    float dx, dy, dz;
 };
+// SampledGrid<RGB*Spectrum>::Lookup(p, convert) (util/containers.h:785-829) at one wavelength:
+// a voxel's value is scale * rsp(lambda) (RGBUnboundedSpectrum::Sample), times the illuminant
+// for Le (RGBIlluminantSpectrum::Sample); outside the grid T{} converts to 0.
+__device__ inline float RGBGridAt(const DeviceScene &S, const MediumRef &m, const MediumPoint &mp, int block, float lam,
+                                  float illum) {
+    const int nx = m.I[5], ny = m.I[6], nz = m.I[7];
+    const float *g = S.media.values + m.I[11] + (size_t)block * 4 * nx * ny * nz;
+    auto at = [&](int x, int y, int z) -> float {
+        if (x < 0 || x >= nx || y < 0 || y >= ny || z < 0 || z >= nz) return 0.f;
+        const float *c = g + 4 * (((size_t)z * ny + y) * nx + x);
+        const float v = c[3] * SigmoidPolynomial(c[0], c[1], c[2], lam);
+        return block == 2 ? v * illum : v;
+    };
+    const int ix = mp.ix, iy = mp.iy, iz = mp.iz;
+    const float d00 = Lerpf(mp.dx, at(ix, iy, iz), at(ix + 1, iy, iz));
+    const float d10 = Lerpf(mp.dx, at(ix, iy + 1, iz), at(ix + 1, iy + 1, iz));
+    const float d01 = Lerpf(mp.dx, at(ix, iy, iz + 1), at(ix + 1, iy, iz + 1));
+    const float d11 = Lerpf(mp.dx, at(ix, iy + 1, iz + 1), at(ix + 1, iy + 1, iz + 1));
+    return Lerpf(mp.dz, Lerpf(mp.dy, d00, d10), Lerpf(mp.dy, d01, d11));
+}
+// sigma_a, sigma_s, Le of MediumProperties at wavelength lam (dense offset off)
+__device__ inline float MediumSigmaA(const DeviceScene &S, const MediumRef &m, const MediumPoint &mp, int off, float lam) {
+    if (!mp.rgb) return DenseAt(S, m.I[1], off) * mp.d;
+    return m.P[7] * ((m.I[15] & 1) ? RGBGridAt(S, m, mp, 0, lam, 1.f) : 1.f);
+}
+__device__ inline float MediumSigmaS(const DeviceScene &S, const MediumRef &m, const MediumPoint &mp, int off, float lam) {
+    if (!mp.rgb) return DenseAt(S, m.I[2], off) * mp.d;
+    return m.P[7] * ((m.I[15] & 2) ? RGBGridAt(S, m, mp, 1, lam, 1.f) : 1.f);
+}
+__device__ inline float MediumLe(const DeviceScene &S, const MediumRef &m, const MediumPoint &mp, int off, float lam) {
+    if (!mp.rgb) return DenseAt(S, m.I[3], off) * mp.le;
+    return S.media.values[m.I[12]] * RGBGridAt(S, m, mp, 2, lam, DenseAt(S, m.I[3], off));
+}
 __device__ inline MediumPoint SampleMediumPoint(const DeviceScene &S, const MediumRef &m, V3 p) {
-    if (m.I[0] == kDevMediumCloud)
-        return MediumPoint{CloudDensity(S.media.values + m.I[11], MediumFromRender(m.P + 8, p)), 0.f};
-    if (m.I[0] != kDevMediumGrid) return MediumPoint{1.f, 1.f};
-    const V3 q = BoundsOffset(m.P, MediumFromRender(m.P + 8, p));
     MediumPoint r;
+    r.rgb = false;
+    if (m.I[0] == kDevMediumCloud) {
+        r.d = CloudDensity(S.media.values + m.I[11], MediumFromRender(m.P + 8, p));
+        r.le = 0.f;
+        return r;
+    }
+    if (m.I[0] != kDevMediumGrid && m.I[0] != kDevMediumRGBGrid) {
+        r.d = r.le = 1.f;
+        return r;
+    }
+    const V3 q = BoundsOffset(m.P, MediumFromRender(m.P + 8, p));
+    if (m.I[0] == kDevMediumRGBGrid) {
+        const float sx = q.x * m.I[5] - .5f, sy = q.y * m.I[6] - .5f, sz = q.z * m.I[7] - .5f;
+        r.rgb = true;
+        r.ix = (int)floorf(sx), r.iy = (int)floorf(sy), r.iz = (int)floorf(sz);
+        r.dx = sx - r.ix, r.dy = sy - r.iy, r.dz = sz - r.iz;
+        r.d = 1.f;
+        r.le = m.I[4] ? 1.f : 0.f;  // IsEmissive: an Le grid and LeScale > 0
+        return r;
+    }
     r.d = GridLookup(S.media.values + m.I[11], m.I[5], m.I[6], m.I[7], q);
     r.le = 0.f;
     if (m.I[4]) {
@@ -154,13 +208,13 @@ __device__ inline MajorantIter SampleMediumRay(const DeviceScene &S, const Mediu
     it.called = false;
     it.empty = false;
     it.grid = nullptr;
-    if (m.I[0] != kDevMediumGrid && m.I[0] != kDevMediumCloud) {
+    if (m.I[0] != kDevMediumGrid && m.I[0] != kDevMediumCloud && m.I[0] != kDevMediumRGBGrid) {
         it.dda = false;
         it.tMin = 0;
         it.tMax = raytMax;
         return it;
     }
-    it.dda = m.I[0] == kDevMediumGrid;
+    it.dda = m.I[0] != kDevMediumCloud;  // GridMedium, RGBGridMedium: DDAMajorantIterator
     // Transform::ApplyInverse(Ray, &tMax) (util/transform.h:416-429): the exact origin becomes a
     // Point3fi (transform.cpp:263-303), is pushed to the edge of its error bounds along d
     const float *M = m.P + 8;
@@ -249,7 +303,8 @@ __device__ inline MajorantIter SampleMediumRay(const DeviceScene &S, const Mediu
 // (SampledWavelengths::SampleUniform's +10 nm recurrence, util/spectrum.h:318-336)
 struct WaveOffsets {
     int off[kNS];
-    __device__ explicit WaveOffsets(float lambda0) {
+    float lam0;  // lambda[0] (the RGB grid medium evaluates its spectra at the wavelengths)
+    __device__ explicit WaveOffsets(float lambda0) : lam0(lambda0) {
         SpectralIter it(lambda0);
 #pragma unroll
         for (int i = 0; i < kNS; ++i, it.Next()) off[i] = DenseOffset(it.lam);
@@ -639,12 +694,13 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vmedium(DeviceScene 
             const bool maxD = depth >= S.maxDepth;
             auto event = [&](V3 p, const MediumPoint &mp, float mx, const float *T) __attribute__((always_inline)) -> bool {
                 const float smaj0 = (DenseAt(S, sa, wo.off[0]) + DenseAt(S, ss, wo.off[0])) * mx;
-                const float sa0 = DenseAt(S, sa, wo.off[0]) * mp.d, ss0 = DenseAt(S, ss, wo.off[0]) * mp.d;
+                const float sa0 = MediumSigmaA(S, m, mp, wo.off[0], wo.lam0), ss0 = MediumSigmaS(S, m, mp, wo.off[0], wo.lam0);
                 // medium emission, scaled by sigma_a / sigma_maj at every event (media.cpp:70-83)
                 if (!maxD && mp.le != 0) {
                     bool leNz = false;
+                    SpectralIter il(wo.lam0);
 #pragma unroll
-                    for (int i = 0; i < kNS; ++i) leNz |= DenseAt(S, le, wo.off[i]) * mp.le != 0;
+                    for (int i = 0; i < kNS; ++i, il.Next()) leNz |= MediumLe(S, m, mp, wo.off[i], il.lam) != 0;
                     if (leNz) {
                         const float pr = smaj0 * T[0];
                         float re[kNS];
@@ -656,10 +712,11 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vmedium(DeviceScene 
                         if (AnyNonZero(re)) {
                             const float den = pr * AvgArr(re);
                             SensorAcc acc;
+                            SpectralIter it(wo.lam0);
 #pragma unroll
-                            for (int i = 0; i < kNS; ++i) {
-                                const float sai = DenseAt(S, sa, wo.off[i]) * mp.d;
-                                const float Le = DenseAt(S, le, wo.off[i]) * mp.le;
+                            for (int i = 0; i < kNS; ++i, it.Next()) {
+                                const float sai = MediumSigmaA(S, m, mp, wo.off[i], it.lam);
+                                const float Le = MediumLe(S, m, mp, wo.off[i], it.lam);
                                 acc.Add(S, wo.off[i], beta[i] * sai * T[i] * Le / den, i == 0);
                             }
                             Lx += S.imagingRatio * (acc.sx / kNS);
@@ -679,9 +736,10 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vmedium(DeviceScene 
                 }
                 if (mode == 1) {
                     const float pr = T[0] * ss0;
+                    SpectralIter it(wo.lam0);
 #pragma unroll
-                    for (int i = 0; i < kNS; ++i) {
-                        const float f = T[i] * (DenseAt(S, ss, wo.off[i]) * mp.d) / pr;
+                    for (int i = 0; i < kNS; ++i, it.Next()) {
+                        const float f = T[i] * MediumSigmaS(S, m, mp, wo.off[i], it.lam) / pr;
                         beta[i] *= f;
                         ru[i] *= f;
                     }
@@ -693,10 +751,11 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vmedium(DeviceScene 
                 // null scattering
                 float sn0 = 0;
                 float sn[kNS];
+                SpectralIter it(wo.lam0);
 #pragma unroll
-                for (int i = 0; i < kNS; ++i) {
+                for (int i = 0; i < kNS; ++i, it.Next()) {
                     const float smaj = (DenseAt(S, sa, wo.off[i]) + DenseAt(S, ss, wo.off[i])) * mx;
-                    sn[i] = fmaxf(0.f, smaj - DenseAt(S, sa, wo.off[i]) * mp.d - DenseAt(S, ss, wo.off[i]) * mp.d);
+                    sn[i] = fmaxf(0.f, smaj - MediumSigmaA(S, m, mp, wo.off[i], it.lam) - MediumSigmaS(S, m, mp, wo.off[i], it.lam));
                 }
                 sn0 = sn[0];
                 const float pr = T[0] * sn0;
@@ -1998,10 +2057,11 @@ __device__ __forceinline__ bool TraceTransmittanceRay(const DeviceScene &S, cons
             const float tEnd = hp < 0 ? tMax : (Length(o - hs.p) / Length(d));
             auto event = [&](V3, const MediumPoint &mp, float mx, const float *T) __attribute__((always_inline)) -> bool {
                 float sn[kNS], smj[kNS];
+                SpectralIter it(wo.lam0);
 #pragma unroll
-                for (int i = 0; i < kNS; ++i) {
+                for (int i = 0; i < kNS; ++i, it.Next()) {
                     smj[i] = (DenseAt(S, sa, wo.off[i]) + DenseAt(S, ss, wo.off[i])) * mx;
-                    sn[i] = fmaxf(0.f, smj[i] - DenseAt(S, sa, wo.off[i]) * mp.d - DenseAt(S, ss, wo.off[i]) * mp.d);
+                    sn[i] = fmaxf(0.f, smj[i] - MediumSigmaA(S, m, mp, wo.off[i], it.lam) - MediumSigmaS(S, m, mp, wo.off[i], it.lam));
                 }
                 const float pr = T[0] * smj[0];
 #pragma unroll

@@ -979,6 +979,7 @@ static void BuildDevice(pbrt_context *c) {
             S.media.allGrey = 0;
     }
     if (getenv("PBRT_AMD_SPECTRAL_MEDIA")) S.media.allGrey = 0;
+    S.media.hasCloud = std::any_of(s.media.begin(), s.media.end(), [](const MediumDesc &m) { return m.type == kMediumCloud; }) ? 1 : 0;
     S.media.denseInLds = s.denseSpectra.size() <= 12 ? 1 : 0;  // <= 15 KB of LDS per block  // force the spectral kernels (tests)
     S.media.info = c->mediumInfo.p;
     S.media.params = c->mediumParams.p;

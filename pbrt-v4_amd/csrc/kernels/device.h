@@ -99,6 +99,7 @@ struct DeviceMedia {
     int n;             // media in the scene (0: the surface-only kernels run)
     int cameraMedium;  // medium the camera sits in, or -1
     int allGrey;       // every medium grey (info[14]): the scalar-majorant kernels run
+    int hasCloud;      // some medium is a CloudMedium: the grey kernels' cloud instantiations run
     int denseInLds;    // the media kernels stage every dense spectrum in LDS (nDense small)
     const int *info;
     const float *params;

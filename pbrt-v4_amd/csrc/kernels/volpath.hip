@@ -129,10 +129,14 @@ __device__ inline float MediumLe(const DeviceScene &S, const MediumRef &m, const
     if (!mp.rgb) return DenseAt(S, m.I[3], off) * mp.le;
     return S.media.values[m.I[12]] * RGBGridAt(S, m, mp, 2, lam, DenseAt(S, m.I[3], off));
 }
+// Cloud: the scene has a CloudMedium.  Its density (13 noise evaluations) inlined into every
+// medium event made the grey media kernels spill (C5 k_vshadow_grey 575 -> 944 us per launch,
+// k_vmedium_grey 1009 -> 1203 us), so the grey kernels have instantiations without it.
+template <bool Cloud = true>
 __device__ inline MediumPoint SampleMediumPoint(const DeviceScene &S, const MediumRef &m, V3 p) {
     MediumPoint r;
     r.rgb = false;
-    if (m.I[0] == kDevMediumCloud) {
+    if (Cloud && m.I[0] == kDevMediumCloud) {
         r.d = CloudDensity(S.media.values + m.I[11], MediumFromRender(m.P + 8, p));
         r.le = 0.f;
         return r;
@@ -386,7 +390,7 @@ __device__ __forceinline__ bool SampleTmaj(const DeviceScene &S, const MediumRef
 // info[14]): every T_maj / sigma_maj entry is the same, so the reference's 31-wide products
 // are one scalar product here -- the same float operations on the same values.
 // sigmaT = sigma_a + sigma_s of the medium (its wavelength-0 entries).
-template <typename F>
+template <bool Cloud, typename F>
 __device__ __forceinline__ bool SampleTmajGrey(const DeviceScene &S, const MediumRef &m, float sigmaT, V3 o, V3 d,
                                                float tMax, float u, PCG32 &rng, float &Tm, F &&event) {
     tMax *= Length(d);
@@ -409,7 +413,7 @@ __device__ __forceinline__ bool SampleTmajGrey(const DeviceScene &S, const Mediu
             if (t < segMax) {
                 Tm *= FastExp(smaj * -(t - tMin));
                 const V3 p = o + d * t;
-                const MediumPoint mp = SampleMediumPoint(S, m, p);
+                const MediumPoint mp = SampleMediumPoint<Cloud>(S, m, p);
                 if (!event(p, mp, smaj, Tm)) return false;
                 Tm = 1.f;
                 tMin = t;
@@ -824,6 +828,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vmedium(DeviceScene 
 // r_u stay in memory and only a scalar record of any non-unit factor is kept; r_l takes
 // T sigma_maj / pr per null collision, applied in the reference's order to its (spectrally
 // constant, checked) value.  No 31-wide array lives through the tracking loop.
+template <bool Cloud>
 __global__ void __launch_bounds__(kBlock, PBRT_VOL_GREY_WAVES) k_vmedium_grey(DeviceScene S, PathState st, VolState v,
                                                                             int wf) {
     const QueueView meds = LoadQueue(st, wf, kVMed);
@@ -942,7 +947,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_GREY_WAVES) k_vmedium_grey(De
                 return betaNz && !fbZero && ruNz;
             };
             float Tm;
-            const bool ranOut = SampleTmajGrey(S, m, sa0 + ss0, o, d, tHit, uDist, rng, Tm, event);
+            const bool ranOut = SampleTmajGrey<Cloud>(S, m, sa0 + ss0, o, d, tHit, uDist, rng, Tm, event);
             if (emitted) {
                 st.L[slot] += Lx;
                 st.L[st.N + slot] += Ly;
@@ -2178,7 +2183,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_intersect_tr(DeviceS
 // TraceTransmittance when every medium is grey: T_ray, r_u and r_l start at 1 and only ever
 // take factors that are equal at all wavelengths, so each is one scalar (the reference's 31
 // entries are 31 copies of it).
-template <int TM>
+template <int TM, bool Cloud>
 __global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_vshadow_grey(DeviceScene S, PathState st, VolState v,
                                                                              int wf) {
     const QueueView sh = LoadQueue(st, wf, kVShadow);
@@ -2230,7 +2235,7 @@ __global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_vshadow_grey(Dev
                     }
                     return Tr != 0;
                 };
-                const bool ranOut = SampleTmajGrey(S, m, sa0 + ss0, o, d, tEnd, rng.Uniform(), rng, Tm, event);
+                const bool ranOut = SampleTmajGrey<Cloud>(S, m, sa0 + ss0, o, d, tEnd, rng.Uniform(), rng, Tm, event);
                 if (ranOut) {
                     const float f = Tm / Tm;
                     Tr *= f;
@@ -2346,7 +2351,8 @@ size_t VolTraversalStaticLds(int tm) {
 #define TAKE_TM(TM)                                                      \
     if (tm == TM) {                                                      \
         take(reinterpret_cast<const void *>(&k_vclosest<TM>));           \
-        take(reinterpret_cast<const void *>(&k_vshadow_grey<TM>));       \
+        take(reinterpret_cast<const void *>(&k_vshadow_grey<TM, false>)); \
+        take(reinterpret_cast<const void *>(&k_vshadow_grey<TM, true>));  \
         take(reinterpret_cast<const void *>(&k_vshadow<TM>));            \
     }
     TAKE_TM(kTravLds) TAKE_TM(kTravWide) TAKE_TM(kTravQuant)
@@ -2388,7 +2394,8 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
                               hipStream_t s) {
     const dim3 block(kBlock);
     const dim3 gT(VolGrid(maxCount, PBRT_GRID_CAP)), gW(VolGrid(maxCount, PBRT_SHADE_GRID_CAP));
-    if (S.media.allGrey) hipLaunchKernelGGL(k_vmedium_grey, gW, block, 0, s, S, st, v, wf);
+    if (S.media.allGrey && S.media.hasCloud) hipLaunchKernelGGL(k_vmedium_grey<true>, gW, block, 0, s, S, st, v, wf);
+    else if (S.media.allGrey) hipLaunchKernelGGL(k_vmedium_grey<false>, gW, block, 0, s, S, st, v, wf);
     else hipLaunchKernelGGL(k_vmedium, gW, block, 0, s, S, st, v, wf);
     const int other = ~((1 << kMatDiffuseT) | (1 << 3) | (1 << kMatCoatedDiffuseT) | (1 << kMatCoatedConductorT) |
                         (1 << kMatDiffuseTransmissionT));
@@ -2429,8 +2436,12 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
         hipLaunchKernelGGL(k_queue_holes, dim3(64, kShards), block, 0, s, st.counters, wf + 1, kVRay,
                            v.rec[(wf + 1) & 1].pixel, st.capS, QueueHoleCounter(), v, st.NR, 4);
 #undef QUEUE_CHECK
-    if (S.media.allGrey) {
-#define K_VSHADOW_GREY(tm) k_vshadow_grey<tm>
+    if (S.media.allGrey && S.media.hasCloud) {
+#define K_VSHADOW_GREY(tm) k_vshadow_grey<tm, true>
+        PBRT_LAUNCH_TRAVERSAL(S, K_VSHADOW_GREY, gT, block, VolStackBytes(S), s, S, st, v, wf);
+#undef K_VSHADOW_GREY
+    } else if (S.media.allGrey) {
+#define K_VSHADOW_GREY(tm) k_vshadow_grey<tm, false>
         PBRT_LAUNCH_TRAVERSAL(S, K_VSHADOW_GREY, gT, block, VolStackBytes(S), s, S, st, v, wf);
 #undef K_VSHADOW_GREY
     } else {

@@ -1054,9 +1054,17 @@ static void BuildDevice(pbrt_context *c) {
         S.matBump = S.hasBump ? (const int4 *)c->matBump.p : nullptr;
         S.tex = TexView{};
         if (!s.texPrograms.empty() || S.hasBump) {
-            if (S.textured && c->volumetric)
-                throw Error("textures or mix materials together with the volumetric path (media, interface, layered, "
-                            "thin dielectric, diffuse transmission or dispersive materials) are not supported yet");
+            // textures on the volumetric path: k_vtexture + k_vsurface<..., Tex> (diffuse,
+            // dielectric, conductor); mix materials and bump on layered ones stay surface-only
+            if (c->volumetric && c->hasMix)
+                throw Error("mix materials together with the volumetric path (media, interface, layered, thin "
+                            "dielectric, diffuse transmission or dispersive materials) are not supported yet");
+            if (c->volumetric)
+                for (const MaterialDesc &m : s.materials)
+                    if ((m.texDisp >= 0 || m.normalMap >= 0) &&
+                        (m.type == kMatCoatedDiffuse || m.type == kMatCoatedConductor || m.type == kMatDiffuseTransmission))
+                        throw Error("bump or normal mapping on layered or diffuse transmission materials together with "
+                                    "the volumetric path is not supported yet");
             c->texNodes.Upload(tt.nodes);
             c->texSpec.Upload(tt.spec);
             c->texImages.Upload(tt.images);

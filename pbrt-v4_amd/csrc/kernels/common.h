@@ -1605,4 +1605,81 @@ __device__ __attribute__((noinline)) int ResolveMixMaterial(const DeviceScene &S
     }
     return mat;
 }
+// The texture stage of EvaluateMaterialAndBSDF for one hit on the volumetric path (k_vtexture;
+// k_texture keeps its own inline copy of the same body: built on this function it hung on the
+// GPU in tests/test_textures.py's textured Cornell box, cause not isolated): bump / normal mapping into st.texBump[depth & 1], the reflectance as
+// sigmoid coefficients (texCoef[0..2], texCoef[3] = 0) or 31 values (texR, texCoef[3] = 1),
+// the roughness alphas into texCoef[4..5]; record ri, its hit barycentrics hitB[k * NR + ri]
+// and lambda0[ri] (read only for textured materials).
+template <bool Full, bool Ext>
+__device__ inline void HitTextures(const DeviceScene &S, const PathState &st, int depth, int ri, int prim, int mat,
+                                   const float *hitB, const float *lambda0s) {
+    const int N = st.NR;
+    const int4 mt = S.matTex[mat];
+    const int4 mb = S.hasBump ? S.matBump[mat] : make_int4(-1, -1, 0, 0);
+    if (mt.x < 0 && mt.y < 0 && !mb.z) return;
+    V3 p0, p1, p2;
+    PrimVerts(S, prim, &p0, &p1, &p2);
+    const TriSurface surf = SurfaceAt<Ext>(S, prim, p0, p1, p2, hitB[ri], hitB[N + ri], hitB[2 * N + ri]);
+    const TexEvalCtx tc = HitTexCtx(S, surf);
+    if (mb.z) {
+        // bump / normal mapping (surfscatter.cpp:109-127): the perturbed shading normal and
+        // dpdu, per record, for the shade kernel and the next depth's emission MIS
+        BumpCtx bc;
+        bc.p = surf.p;
+        bc.n = surf.n;
+        bc.u = tc.u;
+        bc.v = tc.v;
+        bc.dudx = tc.dudx;
+        bc.dudy = tc.dudy;
+        bc.dvdx = tc.dvdx;
+        bc.dvdy = tc.dvdy;
+        bc.ns = surf.ns;
+        bc.dpdu = surf.dpdus;
+        if (prim < S.nTris) {
+            TriShading sh;
+            const bool has = LoadTriShading(S, prim, &sh);
+            TriangleShadingDiff(p0, p1, p2, has ? &sh : nullptr, surf, &bc.dpdv, &bc.dndu, &bc.dndv);
+        } else {  // a disk: shading = geometric frame, no normal derivatives
+            bc.dpdv = surf.dpdv;
+            bc.dndu = bc.dndv = V3(0, 0, 0);
+        }
+        V3 ns, dpdus;
+        BumpShading(bc, S.tex, mb.y, [&](const TexEvalCtx &c) { return TexFloatFast<Full>(S, mb.x, c); }, &ns, &dpdus);
+        float *tb = st.texBump[depth & 1];
+        tb[ri] = ns.x;
+        tb[(size_t)N + ri] = ns.y;
+        tb[2 * (size_t)N + ri] = ns.z;
+        tb[3 * (size_t)N + ri] = dpdus.x;
+        tb[4 * (size_t)N + ri] = dpdus.y;
+        tb[5 * (size_t)N + ri] = dpdus.z;
+    }
+    if (mt.x >= 0) {
+        const DeviceTexProgram pg = S.tex.progs[mt.x];
+        if (!Full || pg.simple) {
+            float c[4];
+            SpectrumImageCoeffs<Full>(S.tex, S.tex.nodes[S.tex.instrs[pg.p1].node], tc, c);
+            st.texCoef[ri] = c[0];
+            st.texCoef[(size_t)N + ri] = c[1];
+            st.texCoef[2 * (size_t)N + ri] = c[2];
+            st.texCoef[3 * (size_t)N + ri] = 0.f;
+        } else if constexpr (Full) {
+            float R[kTexMaxRegs];
+            TexPhase1(S.tex, pg, tc, R);
+            for (SpectralIter it(lambda0s[ri]); it.i < kNSpectrumSamples; it.Next())
+                st.texR[(size_t)it.i * N + ri] = TexPhase2(S.tex, pg, R, it.lam);
+            st.texCoef[3 * (size_t)N + ri] = 1.f;
+        }
+    }
+    if (mt.y >= 0) {
+        float ur = TexFloatFast<Full>(S, mt.y, tc), vr = TexFloatFast<Full>(S, mt.z, tc);
+        if (mt.w) {
+            ur = RoughnessToAlpha(ur);
+            vr = RoughnessToAlpha(vr);
+        }
+        const TrowbridgeReitz t = TrowbridgeReitz::Make(ur, vr);
+        st.texCoef[4 * (size_t)N + ri] = t.ax;
+        st.texCoef[5 * (size_t)N + ri] = t.ay;
+    }
+}
 }  // namespace pbrt_amd

@@ -1228,13 +1228,41 @@ size_t VolTablesLdsBytes(const DeviceScene &S) {
 #define PBRT_VOL_SURF_WAVES 3  // waves/SIMD of k_vsurface
 #endif
 
+// The texture stage of the volumetric surface queue (EvaluateMaterialAndBSDF's texEval calls
+// and bump / normal mapping, surfscatter.cpp:74-137), as k_texture on the surface path: per
+// surface hit of this iteration the results k_vsurface<..., Tex> reads (HitTextures).
+template <bool Ext>
+__global__ void __launch_bounds__(kBlock) k_vtexture(DeviceScene S, PathState st, VolState v, int wf) {
+    const QueueView surf = LoadQueue(st, wf, kVSurf);
+    if ((int)(blockIdx.x * blockDim.x) >= surf.total) return;
+    __shared__ float zLds[64];
+    __shared__ float lutLds[kTexLdsLuts * 256];
+    const int nLut = S.tex.nLuts <= kTexLdsLuts ? S.tex.nLuts : 0;
+    for (int i = threadIdx.x; i < 64; i += blockDim.x) zLds[i] = S.tex.rgbZNodes[i];
+    for (int i = threadIdx.x; i < nLut * 256; i += blockDim.x) lutLds[i] = S.tex.luts[i];
+    __syncthreads();
+    S.tex.rgbZNodes = zLds;
+    if (nLut) S.tex.luts = lutLds;
+    const VolRecords &rec = v.rec[wf & 1];
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < surf.total; j += gridDim.x * blockDim.x) {
+        const int ri = v.surfQ[QueueSlot(surf, j)];
+        const int prim = v.hitPrim[ri];
+        if (prim < 0) continue;  // escaped
+        const int mat = S.primMaterial[prim];
+        if (S.matType[mat] == 3) continue;  // interfaces
+        HitTextures<true, Ext>(S, st, wf, ri, prim, mat, v.hitB, rec.lambda0);
+    }
+}
+
 // The surface side of an iteration: escaped rays, interfaces, emission, materials.  Spectral
 // quantities stream from the wavelength-major records in rolled loops; the one 31-wide
 // intermediate (f, then beta') lives in LDS ([31][kBlock], conflict-free).  Queue appends happen
 // where a lane decides to push (WavePush serves the lanes that reach it).  DiffuseOnly: the
 // scene's surface materials are diffuse, interface or layered (k_vlayered) only, so the
-// dielectric / conductor code is compiled out (C5: fewer registers, no spills).
-template <bool DiffuseOnly, bool Ext>
+// dielectric / conductor code is compiled out (C5: fewer registers, no spills).  Tex: some
+// material is textured or bump mapped; k_vtexture left this iteration's texture results per
+// record (HitTextures), read here as the surface path's shade kernels read k_texture's.
+template <bool DiffuseOnly, bool Ext, bool Tex = false>
 __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(DeviceScene S0, PathState st, VolState v,
                                                                        int wf) {
     const QueueView surf = LoadQueue(st, wf, kVSurf);
@@ -1264,13 +1292,16 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
         const float b0 = v.hitB[ri], b1 = v.hitB[NR + ri], b2 = v.hitB[2 * NR + ri];
         V3 p0, p1, p2;
         PrimVerts(S, prim, &p0, &p1, &p2);
-        const TriSurface si = SurfaceAt<Ext>(S, prim, p0, p1, p2, b0, b1, b2);
+        TriSurface si = SurfaceAt<Ext>(S, prim, p0, p1, p2, b0, b1, b2);
         const V3 wo3 = Normalize(-rd);
         int mIn, mOut;
         MediaOf(S, prim, medium, &mIn, &mOut);
         const int mat = S.primMaterial[prim];
         const int mtypeHit = S.matType[mat];
         if (mtypeHit == 3) continue;  // interface crossings: k_viface
+        if constexpr (Tex) {
+            if (S.hasBump) BumpedShading(S, st, wf, mat, ri, &si);
+        }
         // HandleEmissiveIntersection (integrator.cpp:539-573)
         const int light = S.primLight[prim];
         if (light >= 0) {
@@ -1313,9 +1344,28 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
         // ---- EvaluateMaterialAndBSDF (surfscatter.cpp:57-328) for this material type
         const VRaySamples rs = RaySamplesAt(S, st, slot, depth, mtype == 1 || mtype == kMatThinDielectricT);
         const float4 mp4 = S.matParams[mat];
-        const float4 mc = S.matCoeffs[mat];
-        const bool constant = S.matConstant[mat] & 1;
+        float4 mc = S.matCoeffs[mat];
+        bool constant = S.matConstant[mat] & 1;
         TrowbridgeReitz tr{mp4.x, mp4.y};
+        // textured reflectance: sigmoid coefficients, or 31 values (texR); textured roughness:
+        // the alphas (materials.h GetBxDF texEval calls)
+        bool texR = false;
+        if constexpr (Tex) {
+            const int4 mt = S.matTex[mat];
+            if (mt.x >= 0) {
+                constant = false;
+                if (st.texCoef[3 * (size_t)NR + ri] != 0) texR = true;
+                else mc = make_float4(st.texCoef[ri], st.texCoef[(size_t)NR + ri], st.texCoef[2 * (size_t)NR + ri], 0.f);
+            }
+            if (mt.y >= 0) tr = TrowbridgeReitz{st.texCoef[4 * (size_t)NR + ri], st.texCoef[5 * (size_t)NR + ri]};
+        }
+        // the reflectance before its clamp at wavelength i (lam)
+        auto reflRaw = [&](float lam, int i) -> float {
+            if constexpr (Tex) {
+                if (texR) return st.texR[(size_t)i * NR + ri];
+            }
+            return constant ? mc.w : SigmoidPolynomial(mc.x, mc.y, mc.z, lam);
+        };
         // surfscatter.cpp:127-128 (ThinDielectricBxDF::Regularize does nothing)
         if (mtype != 0 && mtype != kMatThinDielectricT && S.regularize && (flags & 2)) tr.Regularize();
         float eta = mp4.z == 0 ? 1.f : mp4.z;
@@ -1329,28 +1379,28 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
         }
         const int etaSpec = mtype == 2 ? S.matSpectra[2 * mat] : -1;
         const int kSpec = mtype == 2 ? S.matSpectra[2 * mat + 1] : -1;
-        auto etaK = [&](float lam, float *e, float *k) {
-            if (etaSpec >= 0) {
+        auto etaK = [&](float lam, int i, float *e, float *k) {
+            if (etaSpec >= 0 && !texR && (!Tex || S.matTex[mat].x < 0)) {
                 const int a = S.plOffsets[etaSpec], na = S.plOffsets[etaSpec + 1] - a;
                 const int b = S.plOffsets[kSpec], nb = S.plOffsets[kSpec + 1] - b;
                 *e = PiecewiseLinearEval(S.plLambda + a, S.plValue + a, na, lam);
                 *k = PiecewiseLinearEval(S.plLambda + b, S.plValue + b, nb, lam);
             } else {
-                const float r = Clampf(SigmoidPolynomial(mc.x, mc.y, mc.z, lam), 0, .9999f);
+                const float r = Clampf(reflRaw(lam, i), 0, .9999f);
                 *e = 1.f;
                 *k = 2 * std::sqrt(r) / std::sqrt(std::fmax(0.f, 1 - r));
             }
         };
         // f_i of the material's BxDF given its per-sample terms (diffuse R/pi, dielectric scalar,
         // conductor Fresnel per wavelength)
-        auto fAt = [&](float lam, float fd, const ConductorTerms &ct) -> float {
+        auto fAt = [&](float lam, int i, float fd, const ConductorTerms &ct) -> float {
 #if PBRT_VOL_EXPERIMENT == 2
             if (mtype == 0) return 0.4f * kInvPi;
 #endif
-            if (mtype == 0) return Reflectance(mc, constant, lam) * kInvPi;
+            if (mtype == 0) return Clampf(reflRaw(lam, i), 0, 1) * kInvPi;
             if (mtype == 1 || mtype == kMatThinDielectricT) return fd;
             float e, k;
-            etaK(lam, &e, &k);
+            etaK(lam, i, &e, &k);
             return ConductorF(ct, e, k);
         };
         // BxDF::Flags (bxdfs.h): diffuse R != 0; dielectric / conductor always
@@ -1360,7 +1410,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
             SpectralIter it(lambda0);
 #pragma unroll 2
             for (int i = 0; i < kNS; ++i, it.Next()) {
-                const float R = Reflectance(mc, constant, it.lam);
+                const float R = Clampf(reflRaw(it.lam, i), 0, 1);
                 hasFlags |= R != 0;
                 fL[i * kBlock] = R * kInvPi;
             }
@@ -1442,7 +1492,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
                         SpectralIter it(lambda0);
 #pragma unroll 1
                         for (int i = 0; i < kNS; ++i, it.Next()) {
-                            const float f = fAt(it.lam, fd, ct);
+                            const float f = fAt(it.lam, i, fd, ct);
                             fnz |= f != 0;
                             const float Le = ls.Le(S, DenseOffset(it.lam), it.lam);
                             const float Ldv = betaIn(i) * f * absdot * Le;
@@ -1529,7 +1579,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
             SpectralIter it(lambda0);
 #pragma unroll 1
             for (int i = 0; i < kNS; ++i, it.Next()) {
-                const float f = mtype == 0 ? fL[i * kBlock] : fAt(it.lam, fd, ct);
+                const float f = mtype == 0 ? fL[i * kBlock] : fAt(it.lam, i, fd, ct);
                 fAny |= f != 0;
                 const float nb = betaIn(i) * f * absdot / pdf;
                 fL[i * kBlock] = nb;
@@ -2419,14 +2469,28 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
                            st.capS, QueueHoleCounter(), v, st.NR, stage);
     // Ext: analytic shapes or image lights in the scene (their paths compiled in)
     if (S.nShapes > 0 || S.nEnv > 0 || S.nImageDelta > 0 || S.hasSpread) {
-        if (S.matTypeMask & other) hipLaunchKernelGGL((k_vsurface<false, true>), gW, block, surfLds, s, S, st, v, wf);
-        else hipLaunchKernelGGL((k_vsurface<true, true>), gW, block, surfLds, s, S, st, v, wf);
+        if (S.textured) {
+            hipLaunchKernelGGL(k_vtexture<true>, gW, block, 0, s, S, st, v, wf);
+            if (S.matTypeMask & other) hipLaunchKernelGGL((k_vsurface<false, true, true>), gW, block, surfLds, s, S, st, v, wf);
+            else hipLaunchKernelGGL((k_vsurface<true, true, true>), gW, block, surfLds, s, S, st, v, wf);
+        } else if (S.matTypeMask & other) {
+            hipLaunchKernelGGL((k_vsurface<false, true>), gW, block, surfLds, s, S, st, v, wf);
+        } else {
+            hipLaunchKernelGGL((k_vsurface<true, true>), gW, block, surfLds, s, S, st, v, wf);
+        }
         QUEUE_CHECK(1);
         if (S.nInfinite > 0) hipLaunchKernelGGL(k_vescaped<true>, gW, block, VolTablesLdsBytes(S), s, S, st, v, wf);
         VOL_REST(true);
     } else {
-        if (S.matTypeMask & other) hipLaunchKernelGGL((k_vsurface<false, false>), gW, block, surfLds, s, S, st, v, wf);
-        else hipLaunchKernelGGL((k_vsurface<true, false>), gW, block, surfLds, s, S, st, v, wf);
+        if (S.textured) {
+            hipLaunchKernelGGL(k_vtexture<false>, gW, block, 0, s, S, st, v, wf);
+            if (S.matTypeMask & other) hipLaunchKernelGGL((k_vsurface<false, false, true>), gW, block, surfLds, s, S, st, v, wf);
+            else hipLaunchKernelGGL((k_vsurface<true, false, true>), gW, block, surfLds, s, S, st, v, wf);
+        } else if (S.matTypeMask & other) {
+            hipLaunchKernelGGL((k_vsurface<false, false>), gW, block, surfLds, s, S, st, v, wf);
+        } else {
+            hipLaunchKernelGGL((k_vsurface<true, false>), gW, block, surfLds, s, S, st, v, wf);
+        }
         QUEUE_CHECK(1);
         if (S.nInfinite > 0) hipLaunchKernelGGL(k_vescaped<false>, gW, block, VolTablesLdsBytes(S), s, S, st, v, wf);
         VOL_REST(false);

@@ -2,6 +2,7 @@
 #include <array>
 #include <cmath>
 #include <future>
+#include <cstdlib>
 #include <stdexcept>
 
 #include "bvh.h"
@@ -254,6 +255,46 @@ static void Compress(BVH8 &out) {
     }
 }
 
+// Node order below the top levels (PBRT_AMD_BVH_DFS=1, an experiment): the nodes down to
+// depth topDepth keep their breadth-first order (the prefix the traversal kernels cache in
+// LDS), and below each of them the child groups are laid out depth first (a group, then its
+// first child's group, ...), so a subtree's nodes sit together in HBM.  Every group stays
+// contiguous in slot order, and children still follow their parents.
+static void ReorderGroupsDepthFirst(BVH8 &out, const std::vector<int> &depth, int topDepth) {
+    const int n = (int)out.nodes.size();
+    std::vector<int> newIdx(n, -1);
+    int next = 0;
+    for (int i = 0; i < n; ++i)
+        if (depth[i] <= topDepth) newIdx[i] = next++;  // BFS order = level order: a prefix
+    std::vector<int> stack;
+    for (int i = 0; i < n; ++i) {
+        if (depth[i] != topDepth) continue;
+        stack.assign(1, i);
+        while (!stack.empty()) {
+            const int u = stack.back();
+            stack.pop_back();
+            const BVH8Node &nd = out.nodes[u];
+            const int cnt = __builtin_popcount(nd.imask);
+            for (int k = 0; k < cnt; ++k) newIdx[nd.childBase + k] = next++;
+            for (int k = cnt - 1; k >= 0; --k) stack.push_back(nd.childBase + k);
+        }
+    }
+    if (next != n) throw std::runtime_error("BVH8 depth-first reorder missed nodes");
+    std::vector<BVH8Node> nodes(n);
+    std::vector<std::array<int32_t, 8>> refs(n);
+    for (int i = 0; i < n; ++i) {
+        BVH8Node nd = out.nodes[i];
+        if (nd.imask) nd.childBase = newIdx[nd.childBase];
+        std::array<int32_t, 8> r = out.childRef[i];
+        for (int c = 0; c < 8; ++c)
+            if (r[c] >= 0) r[c] = newIdx[r[c]];
+        nodes[newIdx[i]] = nd;
+        refs[newIdx[i]] = r;
+    }
+    out.nodes.swap(nodes);
+    out.childRef.swap(refs);
+}
+
 BVH8 BuildBVH8(const std::vector<V3> &verts, const std::vector<std::array<int, 3>> &tris, int maxLeafPrims) {
     BVH8 out;
     std::vector<Prim> prims;
@@ -427,6 +468,11 @@ BVH8 BuildBVH8(const std::vector<V3> &verts, const std::vector<std::array<int, 3
     }
     out.nodes.resize(queue.size());
     out.childRef.resize(queue.size());
+    if (const char *e = getenv("PBRT_AMD_BVH_DFS"); e && atoi(e) > 0) {
+        std::vector<int> depth(queue.size());
+        for (size_t i = 0; i < queue.size(); ++i) depth[i] = queue[i].depth;
+        ReorderGroupsDepthFirst(out, depth, 1 + atoi(e));  // depths are 1-based (root: 1)
+    }
     out.triPrim.resize(order.size());
     out.triVerts.resize(order.size() * 12);
     for (size_t i = 0; i < order.size(); ++i) {

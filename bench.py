@@ -228,12 +228,26 @@ def latest_profile(pattern):
 def pmc_traffic(workload):
     """HBM bytes per closest-hit launch from the newest committed rocprofv3 PMC pass of this
     workload, tagged with the commit it was measured on (a figure, not a live measurement)."""
-    pat = "r*_closest_pmc.json" if workload == "c2" else f"r*_{workload}_closest_pmc.json"
+    pat = f"r*_{workload}_closest_pmc.json"  # this workload's own records only (r05_c2_..., r04_c4_...)
     rec = latest_profile(pat)
     if not rec or rec.get("hbm_bytes_per_launch") is None:
         return None
     return {"hbm_bytes_per_launch": rec["hbm_bytes_per_launch"], "bytes_per_ray": rec.get("hbm_bytes_per_ray"),
             "measured_on": rec.get("head", "unknown"), "source": "profiles/" + sorted((ROOT / "profiles").glob(pat))[-1].name}
+
+
+def compute_ceiling(workload):
+    """The closest-hit kernel's compute roof from the same PMC record: VALU issue as a fraction
+    of every SIMD's cycles (4 x SQ_ACTIVE_INST_VALU quad-cycles / (1024 SIMDs x GRBM_GUI_ACTIVE / 8
+    XCDs), the gfx9 VALUBusy formula with gfx950's XCD-summed GRBM), and per wave (SQ_ACTIVE_INST_VALU
+    / SQ_WAVE_CYCLES).  With the tree in LDS (C2) this, not HBM, is the binding roof."""
+    pat = f"r*_{workload}_closest_pmc.json"
+    rec = latest_profile(pat)
+    if not rec or rec.get("valu_busy") is None:
+        return None
+    return {"bound": "valu", "valu_busy": rec["valu_busy"], "valu_active_per_wave": rec.get("valu_active_per_wave"),
+            "waiting_per_wave": rec.get("wait_any_per_wave"), "measured_on": rec.get("head", "unknown"),
+            "source": "profiles/" + sorted((ROOT / "profiles").glob(pat))[-1].name}
 
 
 # Wide BVH8 node bytes a visit reads (12 plane float4 + header + slot triangle masks) and the
@@ -385,6 +399,7 @@ def main():
                        "sharding": job["sharding"]},
             "roofline": dict(roofline_entry(achieved, mean_launch_s, launches, st.timed_closest_rays / launches,
                                             bpr, traffic, args.workload, bvh_bytes),
+                             compute=compute_ceiling(args.workload),
                              effective=(effective_traversal(st.timed_closest_rays / launches / mean_launch_s)
                                         if args.workload == "c2" and mean_launch_s > 0 else None)),
             "cpu_baseline": cpu,

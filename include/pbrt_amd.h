@@ -248,6 +248,9 @@ typedef struct pbrt_render_stats {
      * launch" term): node bytes in the format traversed, less the top nodes cached in LDS,
      * and triangle bytes (0 when every triangle is cached in LDS) */
     uint64_t bvh_hbm_node_bytes, bvh_hbm_tri_bytes;
+    /* 1: the surface kernels ran from the correctly rounded build (scenes with alpha-tested
+     * shapes or mix materials, or PBRT_AMD_CR_MATH=1); compare with the oracle's CR mode */
+    int cr_math;
 } pbrt_render_stats;
 
 /* Per-stage kernel profile (GetProfilerEvents / ReportKernelStats, gpu/util.cpp:128-246): with

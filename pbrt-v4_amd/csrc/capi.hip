@@ -9,6 +9,7 @@
 #include <memory>
 #include <sstream>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/pbrt_amd.h"
@@ -19,35 +20,66 @@
 #include "kernels/device.h"
 
 namespace pbrt_amd {
-hipError_t LaunchCamera(const DeviceScene &S, const PathState &st, int nActive, hipStream_t s);
-hipError_t LaunchClosest(const DeviceScene &S, const PathState &st, int depth, int maxCount, int timed,
-                         hipStream_t s, bool sorted);
-hipError_t LaunchRayBin(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
-hipError_t LaunchClassify(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
-hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int depth, int maxCount, bool lean,
-                              hipStream_t s);
-hipError_t LaunchTexture(const DeviceScene &S, const PathState &st, int depth, int type, bool full, int maxCount,
-                         hipStream_t s);
-hipError_t LaunchShadeMicrofacet(const DeviceScene &S, const PathState &st, int depth, int type, int maxCount,
-                                 hipStream_t s);
-hipError_t LaunchEscaped(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
-hipError_t LaunchEmissive(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
-hipError_t LaunchShadow(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
-hipError_t LaunchFilm(const DeviceScene &S, const PathState &st, int nSamples, hipStream_t s);
+// kernels/wavefront.hip, built twice: wf (device transcendentals) and wfcr (correctly rounded)
+#define PBRT_WF_LAUNCHERS                                                                                      \
+    hipError_t LaunchCamera(const DeviceScene &S, const PathState &st, int nActive, hipStream_t s);             \
+    hipError_t LaunchClosest(const DeviceScene &S, const PathState &st, int depth, int maxCount, int timed,     \
+                             hipStream_t s, bool sorted);                                                      \
+    hipError_t LaunchRayBin(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s); \
+    hipError_t LaunchClassify(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s); \
+    hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int depth, int maxCount, bool lean, \
+                                  hipStream_t s);                                                              \
+    hipError_t LaunchTexture(const DeviceScene &S, const PathState &st, int depth, int type, bool full,         \
+                             int maxCount, hipStream_t s);                                                     \
+    hipError_t LaunchShadeMicrofacet(const DeviceScene &S, const PathState &st, int depth, int type,            \
+                                     int maxCount, hipStream_t s);                                             \
+    hipError_t LaunchEscaped(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s); \
+    hipError_t LaunchEmissive(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s); \
+    hipError_t LaunchShadow(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s); \
+    hipError_t LaunchFilm(const DeviceScene &S, const PathState &st, int nSamples, hipStream_t s);              \
+    hipError_t LaunchIntersectBatch(const DeviceScene &S, const float *rays, int n, int anyHit, int *outPrim,  \
+                                    float *outHit, hipStream_t s);
+namespace wf {
+PBRT_WF_LAUNCHERS
 hipError_t LaunchCheckRNMath(uint64_t seed, int blocks, int perThread, unsigned long long *bad, hipStream_t s);
+size_t SurfaceTraversalStaticLds(int tm);
+int TraversalBlocksCompiled(int compressed);
+}  // namespace wf
+namespace wfcr {
+PBRT_WF_LAUNCHERS
+}  // namespace wfcr
+#undef PBRT_WF_LAUNCHERS
+// Every surface-wavefront launch goes to the build the scene selected (DeviceScene::crMath)
+#define PBRT_WF_DISPATCH(name)                                                                   \
+    template <class... A>                                                                        \
+    static hipError_t name(const DeviceScene &S, A &&...a) {                                     \
+        return S.crMath ? wfcr::name(S, std::forward<A>(a)...) : wf::name(S, std::forward<A>(a)...); \
+    }
+PBRT_WF_DISPATCH(LaunchCamera)
+PBRT_WF_DISPATCH(LaunchClosest)
+PBRT_WF_DISPATCH(LaunchRayBin)
+PBRT_WF_DISPATCH(LaunchClassify)
+PBRT_WF_DISPATCH(LaunchShadeDiffuse)
+PBRT_WF_DISPATCH(LaunchTexture)
+PBRT_WF_DISPATCH(LaunchShadeMicrofacet)
+PBRT_WF_DISPATCH(LaunchEscaped)
+PBRT_WF_DISPATCH(LaunchEmissive)
+PBRT_WF_DISPATCH(LaunchShadow)
+PBRT_WF_DISPATCH(LaunchFilm)
+PBRT_WF_DISPATCH(LaunchIntersectBatch)
+#undef PBRT_WF_DISPATCH
+using wf::LaunchCheckRNMath;
+using wf::SurfaceTraversalStaticLds;
+using wf::TraversalBlocksCompiled;
 hipError_t LaunchVolCamera(const DeviceScene &S, const PathState &st, const VolState &v, int nActive, hipStream_t s);
 hipError_t LaunchVolClosest(const DeviceScene &S, const PathState &st, const VolState &v, int wf, int maxCount,
                             int timed, hipStream_t s);
 hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const VolState &v, int wf, int maxCount,
                               hipStream_t s);
-hipError_t LaunchIntersectBatch(const DeviceScene &S, const float *rays, int n, int anyHit, int *outPrim,
-                                float *outHit, hipStream_t s);
 void SetQueueCheck(int on);
 int TakeQueueHoles();
 hipError_t LaunchIntersectTr(const DeviceScene &S, const float *rays, const int *medium, const float *lambda0, int n,
                              float *out, hipStream_t s);
-size_t SurfaceTraversalStaticLds(int tm);
-int TraversalBlocksCompiled(int compressed);
 size_t VolTraversalStaticLds(int tm);
 }  // namespace pbrt_amd
 
@@ -1031,6 +1063,13 @@ static void BuildDevice(pbrt_context *c) {
         }
         c->matMix.Upload(mm);
         S.matMix = (const int4 *)c->matMix.p;
+        // Scenes whose paths hash ray bits (alpha tests: HashFloat(ray o, d), gpu/optix.cu:197-243;
+        // mix: HashFloat(p, wo, ...), materials.h:285-294) take the correctly rounded build of the
+        // surface kernels (wavefront.hip, namespace wfcr): a last-ulp difference in a device
+        // transcendental would otherwise flip a decision the oracle makes (its CR mode matches).
+        // PBRT_AMD_CR_MATH=0/1 forces either build.
+        S.crMath = (S.nAlpha > 0 || c->hasMix) ? 1 : 0;
+        if (const char *e = getenv("PBRT_AMD_CR_MATH")) S.crMath = atoi(e) ? 1 : 0;
         // textured: some material evaluates a program (the textured shade / texture kernels);
         // the alpha tests of the traversal kernels may need the tables on their own
         {
@@ -1986,6 +2025,7 @@ int pbrt_synchronize(pbrt_context *ctx) {
             const uint64_t nNodes = S.compressed ? ctx->qnodes.n : ctx->nodes.n;
             ctx->stats.bvh_hbm_node_bytes = nNodes > (uint64_t)S.ldsNodes ? (nNodes - S.ldsNodes) * nodeB : 0;
             ctx->stats.bvh_hbm_tri_bytes = S.ldsTris > 0 ? 0 : (uint64_t)ctx->triVerts.n * sizeof(float);
+            ctx->stats.cr_math = S.crMath;
         }
         return 0;
     } catch (const std::exception &e) {

@@ -15,7 +15,27 @@
 // device-side queue counters so the host never synchronises inside the render loop.
 #include "common.h"
 
+// This file is compiled twice (Makefile): once with the device's own transcendentals into
+// namespace pbrt_amd::wf, and once with PBRT_AMD_CR_MATH (correctly rounded, core.h) into
+// pbrt_amd::wfcr.  capi.hip picks the build per scene (DeviceScene::crMath): scenes whose paths
+// hash ray bits (alpha-tested shapes, mix materials) take the CR build, so every decision they
+// make equals the oracle's in its CR mode.
+#ifndef PBRT_WF_NS
+#define PBRT_WF_NS wf
+#endif
+
 namespace pbrt_amd {
+#if !defined(PBRT_AMD_CR_MATH)
+// Traversal LDS of one block (shared with volpath.hip; defined once, in the default build):
+// group stack (uint2 entries), cached nodes, cached triangles in three pre-rotated copies
+size_t TraversalLdsBytes(int stackSize, int ldsNodes, int ldsTris, int compressed) {
+    return (size_t)stackSize * kBlock * sizeof(uint2) + (size_t)ldsNodes * LdsNodeStride(compressed) * 16 +
+           (size_t)ldsTris * 3 * 48;
+}
+#else
+size_t TraversalLdsBytes(int stackSize, int ldsNodes, int ldsTris, int compressed);
+#endif
+namespace PBRT_WF_NS {
 
 // The sensor's x/y/z-bar table as the shade kernels read it (staged in LDS; reading it through
 // the L1 instead, to fit four blocks per CU, measured 5 % slower: profiles/r02_shade_ablation.txt)
@@ -1595,11 +1615,6 @@ hipError_t LaunchCheckRNMath(uint64_t seed, int blocks, int perThread, unsigned 
 }
 
 // ------------------------------------------------------------------ launch helpers (host)
-size_t TraversalLdsBytes(int stackSize, int ldsNodes, int ldsTris, int compressed) {
-    // group stack (uint2 entries), cached nodes, cached triangles in three pre-rotated copies
-    return (size_t)stackSize * kBlock * sizeof(uint2) + (size_t)ldsNodes * LdsNodeStride(compressed) * 16 +
-           (size_t)ldsTris * 3 * 48;
-}
 // Blocks (of kBlock threads) per CU the traversal kernels of a mode are compiled for
 int TraversalBlocksCompiled(int compressed) { return TraversalWaves(compressed ? kTravQuant : kTravWide); }
 
@@ -1775,4 +1790,5 @@ hipError_t LaunchIntersectBatch(const DeviceScene &S, const float *rays, int n, 
     return hipGetLastError();
 }
 
+}  // namespace PBRT_WF_NS
 }  // namespace pbrt_amd

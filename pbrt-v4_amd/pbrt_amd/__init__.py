@@ -115,7 +115,8 @@ class RenderStats(ctypes.Structure):
                 ("shadow_rays", ctypes.c_uint64), ("closest_launches", ctypes.c_int),
                 ("closest_ms", ctypes.c_double), ("timed_closest_rays", ctypes.c_uint64), ("passes", ctypes.c_int),
                 ("paths_per_pass", ctypes.c_uint64), ("bvh_hbm_node_bytes", ctypes.c_uint64),
-                ("bvh_hbm_tri_bytes", ctypes.c_uint64)]
+                ("bvh_hbm_tri_bytes", ctypes.c_uint64),
+                ("cr_math", ctypes.c_int)]
 
 
 class KernelStat(ctypes.Structure):
@@ -486,6 +487,13 @@ class WavefrontPathIntegrator:
         s = RenderStats()
         _check(_lib().pbrt_get_stats(self._h, ctypes.byref(s)))
         return s
+
+    @property
+    def cr_math(self) -> bool:
+        """True when the surface kernels ran from the correctly rounded build (scenes with
+        alpha-tested shapes or mix materials; valid after synchronize()): the oracle's CR mode
+        is then the one to compare with."""
+        return bool(self.stats().cr_math)
 
     def reset_stats(self):
         _check(_lib().pbrt_reset_stats(self._h))

@@ -29,6 +29,17 @@ def to_rgb(oracle, sc, film):
     return oracle.film_to_rgb(film, [f.output_rgb_from_sensor_rgb[i] for i in range(9)])
 
 
+def oracle_film(oracle, sc, integ, **kw):
+    """The oracle's film in the arithmetic mode the product's context ran: its correctly rounded
+    mode when the surface kernels came from the CR build (alpha-tested shapes, mix materials:
+    capi.hip DeviceScene::crMath), its libm mode otherwise."""
+    kw.setdefault("threads", 16)
+    if integ.cr_math:
+        with oracle.cr_math():
+            return oracle.render(sc, **kw)
+    return oracle.render(sc, **kw)
+
+
 def check_parity(a, b):
     d = np.abs(a - b)
     ok = d <= np.maximum(REL * np.abs(b), ABS_FLOOR)

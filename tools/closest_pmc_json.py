@@ -5,7 +5,10 @@ Input: the rocprofv3 PMC passes of tools/pmc.sh (FETCH_SIZE and WRITE_SIZE each 
 pass, values in KB per dispatch) plus the bench JSON line those runs printed (rays/launch).
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half the bytes of a
 wide coalesced read, so it is doubled; WRITE_SIZE is used as is.
-Usage: python tools/closest_pmc_json.py gpurun_out/pmc profiles/r01_closest_pmc.json
+With the sq1 / sq2 passes present it adds the kernel's compute roof: VALU busy = 4 x
+SQ_ACTIVE_INST_VALU (quad-cycles) / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs) and, per wave,
+SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES and SQ_WAIT_ANY / SQ_WAVE_CYCLES.
+Usage: python tools/closest_pmc_json.py gpurun_out/pmc profiles/r05_c2_closest_pmc.json [kernel] [--head SHA]
 """
 import csv
 import json
@@ -30,8 +33,14 @@ def bench_line(log):
     raise SystemExit(f"no bench line in {log}")
 
 
-src, dst = Path(sys.argv[1]), Path(sys.argv[2])
-kernel = sys.argv[3] if len(sys.argv) > 3 else "k_closest"
+args = [a for a in sys.argv[1:]]
+head = None
+if "--head" in args:
+    i = args.index("--head")
+    head = args[i + 1]
+    del args[i:i + 2]
+src, dst = Path(args[0]), Path(args[1])
+kernel = args[2] if len(args) > 2 else "k_closest"
 fetch = per_dispatch(src / "fetch" / "run_counter_collection.csv", kernel, "FETCH_SIZE")
 write = per_dispatch(src / "write" / "run_counter_collection.csv", kernel, "WRITE_SIZE")
 b = bench_line(src / "fetch.log")
@@ -53,5 +62,23 @@ rec = {
     "note": "FETCH_SIZE x2 per the gfx950 correction; 4-byte-per-lane SoA accesses are not calibrated "
             "by the guide, so the corrected read figure is an upper estimate",
 }
+def mean(pass_, counter):
+    f = src / pass_ / "run_counter_collection.csv"
+    if not f.exists():
+        return None
+    v = per_dispatch(f, kernel, counter)
+    return sum(v) / len(v) if v else None
+
+
+valu, wave, wait, grbm = (mean("sq2", "SQ_ACTIVE_INST_VALU"), mean("sq1", "SQ_WAVE_CYCLES"),
+                          mean("sq2", "SQ_WAIT_ANY"), mean("sq2", "GRBM_GUI_ACTIVE"))
+if valu is not None and grbm:
+    rec["valu_busy"] = round(4 * valu / (1024 * grbm / 8), 4)
+if valu is not None and wave:
+    rec["valu_active_per_wave"] = round(valu / wave, 4)
+if wait is not None and wave:
+    rec["wait_any_per_wave"] = round(wait / wave, 4)
+if head:
+    rec["head"] = head
 dst.write_text(json.dumps(rec, indent=1) + "\n")
 print(json.dumps(rec, indent=1))

@@ -91,7 +91,9 @@ typedef struct pbrt_scene_flat {
     int n_dims;
     const uint16_t *perm_table;
     const uint32_t *perm_offset, *perm_ndigits, *perm_base;
-    /* sampler: 0 halton, 1 zsobol (randomization 0 none, 1 permutedigits, 2 fastowen, 3 owen) */
+    /* sampler: 0 halton, 1 zsobol, 2 independent, 3 stratified, 4 sobol, 5 paddedsobol
+     * (randomization of zsobol / sobol / paddedsobol: 0 none, 1 permutedigits, 2 fastowen, 3 owen;
+     * stratified and Sobol' fields at the end of this struct) */
     int sampler_type, zs_randomize, zs_log2_spp, zs_nbase4_digits;
     /* materials: type 0 diffuse, 1 dielectric, 2 conductor (materials.h DiffuseMaterial,
      * DielectricMaterial, ConductorMaterial), 3 interface, 4 coateddiffuse, 5 coatedconductor,
@@ -227,6 +229,12 @@ typedef struct pbrt_scene_flat {
      * texture's root node and the normal map image (indices into the tex_node / image tables,
      * -1 none) */
     const int32_t *material_bump;
+    /* StratifiedSampler xsamples, ysamples, jitter; SobolSampler log2(RoundUpPow2(max(xres,
+     * yres))) and util/sobolmatrices.cpp's tables (SobolMatrices32 [1024 * 52], VdCSobolMatrices
+     * and VdCSobolMatricesInv [25 * 52]; NULL unless the sampler is sobol) */
+    int strat_xsamples, strat_ysamples, strat_jitter, sobol_log2_scale;
+    const uint32_t *sobol_matrices32;
+    const uint64_t *vdc_sobol, *vdc_sobol_inv;
 } pbrt_scene_flat;
 
 typedef struct pbrt_render_params {
@@ -379,6 +387,13 @@ int pbrt_debug_filter_sample(const pbrt_scene *scene, float u0, float u1, float 
  * wavefront's call pattern Get1D, Get2D, Get1D, Get2D, Get1D -> 7 values (scene's sampler
  * parameters: spp, resolution, seed, randomization) */
 int pbrt_debug_zsobol(const pbrt_scene *scene, int px, int py, int sample_index, int dim, float *out7);
+/* IndependentSampler / StratifiedSampler / SobolSampler / PaddedSobolSampler (samplers.h:144-224,
+ * 442-633) of the scene from StartPixelSample((px,py), sample_index, dim): for dim 0 the
+ * camera's Get1D, GetPixel2D, Get1D, Get2D, Get1D, otherwise Get1D, Get2D, Get1D, Get2D, Get1D
+ * -> 7 values.  Fails for halton / zsobol scenes (pbrt_debug_halton / pbrt_debug_zsobol). */
+int pbrt_debug_sampler(const pbrt_scene *scene, int px, int py, int sample_index, int dim, float *out7);
+/* RNG::SetSequence(seq); RNG::Advance(advance); two Uniform<uint32_t>() (util/rng.h:119-150) */
+int pbrt_debug_rng(uint64_t seq, uint64_t advance, uint32_t *out2);
 /* util/scattering.h components as the product evaluates them (core.h), host side.
  * trowbridge: in13 = ax ay wo3 wi3 wm3 u0 u1 (TrowbridgeReitzDistribution(ax, ay)) ->
  *   out14 = alpha_x alpha_y smooth D(wm) D(wo,wm) Lambda(wo) G1(wo) G(wo,wi) PDF(wo,wm)

@@ -513,15 +513,203 @@ struct ZSobolState {
     void Pixel2D(Float *a, Float *b) { Get2D(a, b); }
 };
 
-// Either sampler behind pbrt's Sampler interface calls used by the wavefront
+// ---------------------------------------------------------------- independent / stratified /
+// sobol / paddedsobol (samplers.h:144-224, 442-633).  The RNG is util/rng.h's PCG32 with its
+// SetSequence / Advance (rng.h:119-150); Hash(args...) is MurmurHash64A over the packed
+// arguments (util/hash.h:91-106); the Sobol' rows come from the scene's copy of
+// util/sobolmatrices.cpp (pbrt_scene_flat::sobol_matrices32 / vdc_sobol / vdc_sobol_inv).
+struct SeqRNG {
+    uint64_t state = 0, inc = 1;
+    uint32_t Next() {
+        uint64_t old = state;
+        state = old * 0x5851f42d4c957f2dULL + inc;
+        uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+        uint32_t rot = (uint32_t)(old >> 59u);
+        return (xs >> rot) | (xs << ((~rot + 1u) & 31));
+    }
+    void SetSequence(uint64_t seq) {
+        state = 0u;
+        inc = (seq << 1u) | 1u;
+        Next();
+        state += Mix64(seq);
+        Next();
+    }
+    void Advance(uint64_t delta) {
+        // delta steps of the LCG: x -> a x + c, composed by doubling (a^k, c (a^k - 1)/(a - 1))
+        uint64_t a = 0x5851f42d4c957f2dULL, c = inc, A = 1, C = 0;
+        for (; delta; delta >>= 1) {
+            if (delta & 1) {
+                A *= a;
+                C = C * a + c;
+            }
+            c = (a + 1) * c;
+            a *= a;
+        }
+        state = A * state + C;
+    }
+    Float Uniform() { return std::min<Float>(OneMinusEpsilon, Next() * 0x1p-32f); }
+};
+struct OtherSampler {
+    int kind = 0;  // 2 independent, 3 stratified, 4 sobol, 5 paddedsobol (pbrt_scene_flat::sampler_type)
+    int spp = 1, seed = 0, xs = 1, ys = 1, jitter = 1, randomize = 2, log2Scale = 0;
+    const uint32_t *m32 = nullptr;
+    const uint64_t *vdc = nullptr, *vdcInv = nullptr;
+};
+struct OtherState {
+    const OtherSampler *o = nullptr;
+    int px = 0, py = 0, si = 0, dimension = 0;
+    uint64_t sobolIndex = 0;
+    SeqRNG rng;
+    static uint64_t HashInts(std::initializer_list<int> v) {
+        unsigned char buf[16];
+        size_t n = 0;
+        for (int x : v) {
+            std::memcpy(buf + n, &x, 4);
+            n += 4;
+        }
+        return Murmur64A(buf, n, 0);
+    }
+    static uint32_t Scramble(uint32_t v, int randomize, uint32_t h) {
+        switch (randomize) {
+        case 1: return v ^ h;
+        case 2:
+            v = BitReverse(v);
+            v ^= v * 0x3d20adea;
+            v += h;
+            v *= (h >> 16) | 1;
+            v ^= v * 0x05526c56;
+            v ^= v * 0x53a22864;
+            return BitReverse(v);
+        case 3:
+            if (h & 1) v ^= 1u << 31;
+            for (int b = 1; b < 32; ++b)
+                if ((uint32_t)Mix64((v & (~0u << (32 - b))) ^ h) & (1u << b)) v ^= 1u << (31 - b);
+            return v;
+        default: return v;
+        }
+    }
+    // SobolSample(a, dim, scrambler) over the full matrices
+    Float Sobol(uint64_t a, int dim, int randomize, uint32_t h) const {
+        uint32_t v = 0;
+        for (int k = 0; a; a >>= 1, ++k)
+            if (a & 1) v ^= o->m32[dim * 52 + k];
+        return std::min(Scramble(v, randomize, h) * 0x1p-32f, OneMinusEpsilon);
+    }
+    // dimensions 0 / 1 (the padded sampler): van der Corput and Pascal's triangle mod 2
+    static Float Sobol01(uint64_t a, int dim, int randomize, uint32_t h) {
+        uint32_t v = 0;
+        for (int k = 0; a; a >>= 1, ++k)
+            if (a & 1) v ^= SobolRow(dim, k);
+        return std::min(Scramble(v, randomize, h) * 0x1p-32f, OneMinusEpsilon);
+    }
+    void Start(int x, int y, int index, int dim) {
+        px = x, py = y, si = index, dimension = dim;
+        if (o->kind == 2 || o->kind == 3) {
+            rng.SetSequence(HashInts({x, y, o->seed}));
+            rng.Advance((uint64_t)index * 65536ull + (uint64_t)dim);
+        }
+        if (o->kind == 4) {
+            dimension = std::max(2, dim);
+            // SobolIntervalToIndex (lowdiscrepancy.h:266-287)
+            const uint32_t m = (uint32_t)o->log2Scale;
+            uint64_t frame = (uint64_t)index;
+            if (m == 0) {
+                sobolIndex = frame;
+            } else {
+                uint64_t idx = frame << (2 * m), delta = 0;
+                for (int c = 0; frame; frame >>= 1, ++c)
+                    if (frame & 1) delta ^= o->vdc[(m - 1) * 52 + c];
+                uint64_t b = (((uint64_t)(uint32_t)x << m) | (uint32_t)y) ^ delta;
+                for (int c = 0; b; b >>= 1, ++c)
+                    if (b & 1) idx ^= o->vdcInv[(m - 1) * 52 + c];
+                sobolIndex = idx;
+            }
+        }
+    }
+    Float SobolDimension(int d) const {
+        return o->randomize == 0 ? Sobol(sobolIndex, d, 0, 0)
+                                 : Sobol(sobolIndex, d, o->randomize, (uint32_t)HashInts({d, o->seed}));
+    }
+    int Permuted(uint64_t hash, int n) const { return PermElem((uint32_t)si, (uint32_t)n, (uint32_t)hash); }
+    Float Get1D() {
+        switch (o->kind) {
+        case 2: return rng.Uniform();
+        case 3: {
+            const uint64_t hash = HashInts({px, py, dimension, o->seed});
+            const int n = o->xs * o->ys, stratum = Permuted(hash, n);
+            ++dimension;
+            const Float delta = o->jitter ? rng.Uniform() : 0.5f;
+            return (stratum + delta) / n;
+        }
+        case 4:
+            if (dimension >= 1024) dimension = 2;
+            return SobolDimension(dimension++);
+        default: {
+            const uint64_t hash = HashInts({px, py, dimension, o->seed});
+            const int index = Permuted(hash, o->spp);
+            ++dimension;
+            return Sobol01((uint32_t)index, 0, o->randomize, (uint32_t)(hash >> 32));
+        }
+        }
+    }
+    void Get2D(Float *a, Float *b) {
+        switch (o->kind) {
+        case 2:
+            *a = rng.Uniform();
+            *b = rng.Uniform();
+            return;
+        case 3: {
+            const uint64_t hash = HashInts({px, py, dimension, o->seed});
+            const int stratum = Permuted(hash, o->xs * o->ys);
+            dimension += 2;
+            const int x = stratum % o->xs, y = stratum / o->xs;
+            const Float dx = o->jitter ? rng.Uniform() : 0.5f;
+            const Float dy = o->jitter ? rng.Uniform() : 0.5f;
+            *a = (x + dx) / o->xs;
+            *b = (y + dy) / o->ys;
+            return;
+        }
+        case 4:
+            if (dimension + 1 >= 1024) dimension = 2;
+            *a = SobolDimension(dimension);
+            *b = SobolDimension(dimension + 1);
+            dimension += 2;
+            return;
+        default: {
+            const uint64_t hash = HashInts({px, py, dimension, o->seed});
+            const int index = Permuted(hash, o->spp);
+            dimension += 2;
+            *a = Sobol01((uint32_t)index, 0, o->randomize, (uint32_t)hash);
+            *b = Sobol01((uint32_t)index, 1, o->randomize, (uint32_t)(hash >> 32));
+            return;
+        }
+        }
+    }
+    void Pixel2D(Float *a, Float *b) {
+        if (o->kind != 4) {
+            Get2D(a, b);
+            return;
+        }
+        const Float scale = (Float)(1 << o->log2Scale);
+        Float u0 = Sobol(sobolIndex, 0, 0, 0), u1 = Sobol(sobolIndex, 1, 0, 0);
+        *a = Clamp(u0 * scale - px, 0.f, OneMinusEpsilon);
+        *b = Clamp(u1 * scale - py, 0.f, OneMinusEpsilon);
+    }
+};
+
+// Any sampler behind pbrt's Sampler interface calls used by the wavefront
 struct AnySampler {
     HaltonState h;
     ZSobolState z;
     bool zsobol;
-    void Start(int px, int py, int si, int dim) { zsobol ? z.Start(px, py, si, dim) : h.Start(px, py, si, dim); }
-    Float Get1D() { return zsobol ? z.Get1D() : h.Get1D(); }
-    void Get2D(Float *a, Float *b) { zsobol ? z.Get2D(a, b) : h.Get2D(a, b); }
-    void Pixel2D(Float *a, Float *b) { zsobol ? z.Pixel2D(a, b) : h.Pixel2D(a, b); }
+    OtherState os;  // os.o set: one of the other four samplers
+    void Start(int px, int py, int si, int dim) {
+        if (os.o) os.Start(px, py, si, dim);
+        else zsobol ? z.Start(px, py, si, dim) : h.Start(px, py, si, dim);
+    }
+    Float Get1D() { return os.o ? os.Get1D() : zsobol ? z.Get1D() : h.Get1D(); }
+    void Get2D(Float *a, Float *b) { os.o ? os.Get2D(a, b) : zsobol ? z.Get2D(a, b) : h.Get2D(a, b); }
+    void Pixel2D(Float *a, Float *b) { os.o ? os.Pixel2D(a, b) : zsobol ? z.Pixel2D(a, b) : h.Pixel2D(a, b); }
 };
 
 // ---------------------------------------------------------------- geometry
@@ -702,6 +890,12 @@ struct Scene {
     Halton halton;
     ZSobol zsobol;
     bool useZSobol = false;
+    OtherSampler other;  // other.kind >= 2: independent / stratified / sobol / paddedsobol
+    AnySampler Sampler() const {
+        AnySampler a{HaltonState{&halton, 0, 0}, ZSobolState{&zsobol}, useZSobol, OtherState{}};
+        if (other.kind >= 2) a.os.o = &other;
+        return a;
+    }
     int xres, yres, px0, px1, py0, py1, maxDepth;
     Float frx, fry;
     Vec P(int t, int k) const { return v[tri[3 * t + k]]; }
@@ -782,6 +976,19 @@ struct Scene {
         halton.Init(xres, yres, (uint32_t)info->seed, std::max(f->n_dims, 7 * maxDepth + 7));
         useZSobol = f->sampler_type == 1;
         zsobol.Init(info->spp, xres, yres, info->seed, f->zs_randomize);
+        if (f->sampler_type >= 2) {
+            other.kind = f->sampler_type;
+            other.spp = info->spp;
+            other.seed = info->seed;
+            other.xs = f->strat_xsamples;
+            other.ys = f->strat_ysamples;
+            other.jitter = f->strat_jitter;
+            other.randomize = f->zs_randomize;
+            other.log2Scale = f->sobol_log2_scale;
+            other.m32 = f->sobol_matrices32;
+            other.vdc = f->vdc_sobol;
+            other.vdcInv = f->vdc_sobol_inv;
+        }
     }
 
     void InitShapes();
@@ -4717,7 +4924,7 @@ struct Renderer {
     }
     // one pixel sample -> sensor RGB and filter weight (film.h:95-100)
     void Li(int px, int py, int sampleIndex, float rgb[3], float *weight) const {
-        AnySampler hs{HaltonState{&S.halton, 0, 0}, ZSobolState{&S.zsobol}, S.useZSobol};
+        AnySampler hs = S.Sampler();
         hs.Start(px, py, sampleIndex, 0);
         Wavelengths lambda;
         Vec ro, rd;
@@ -4775,7 +4982,7 @@ struct Renderer {
             Interaction si;
             if (prim >= 0) si = S.Interact(prim, ti, rd);
             // GenerateRaySamples: dims 6 + 7 depth (path depth)
-            AnySampler h2{HaltonState{&S.halton, 0, 0}, ZSobolState{&S.zsobol}, S.useZSobol};
+            AnySampler h2 = S.Sampler();
             h2.Start(px, py, sampleIndex, 6 + 7 * depth);
             Float dUc = h2.Get1D(), dU0, dU1;
             h2.Get2D(&dU0, &dU1);
@@ -5089,7 +5296,7 @@ struct Renderer {
     // (a scene with media returns false).
     bool PathLi(int px, int py, int sampleIndex, float rgb[3], float *weight) const {
         if (f->n_media > 0) return false;
-        AnySampler hs{HaltonState{&S.halton, 0, 0}, ZSobolState{&S.zsobol}, S.useZSobol};
+        AnySampler hs = S.Sampler();
         hs.Start(px, py, sampleIndex, 0);
         Wavelengths lambda;
         Vec ro, rd;
@@ -5750,6 +5957,44 @@ void oracle_zsobol(int spp, int xres, int yres, int seed, int randomize, int px,
     out7[3] = s.Get1D();
     s.Get2D(&out7[4], &out7[5]);
     out7[6] = s.Get1D();
+}
+
+// IndependentSampler / StratifiedSampler / SobolSampler / PaddedSobolSampler (kind 2..5) from
+// StartPixelSample((px, py), sampleIndex, dim) in the wavefront's call order: dimension 0 the
+// camera's Get1D, GetPixel2D, Get1D, Get2D, Get1D; otherwise Get1D, Get2D, Get1D, Get2D, Get1D
+void oracle_sampler(int kind, int spp, int seed, int xs, int ys, int jitter, int randomize, int xres, int yres,
+                    const uint32_t *m32, const uint64_t *vdc, const uint64_t *vdcInv, int px, int py,
+                    int sampleIndex, int dim, float *out7) {
+    OtherSampler o;
+    o.kind = kind;
+    o.spp = spp;
+    o.seed = seed;
+    o.xs = xs;
+    o.ys = ys;
+    o.jitter = jitter;
+    o.randomize = randomize;
+    int res = 1;
+    while (res < std::max(xres, yres)) res *= 2;  // SobolSampler: scale = RoundUpPow2(max res)
+    while ((2 << o.log2Scale) <= res) ++o.log2Scale;
+    o.m32 = m32;
+    o.vdc = vdc;
+    o.vdcInv = vdcInv;
+    OtherState st;
+    st.o = &o;
+    st.Start(px, py, sampleIndex, dim);
+    out7[0] = st.Get1D();
+    if (dim == 0) st.Pixel2D(&out7[1], &out7[2]);
+    else st.Get2D(&out7[1], &out7[2]);
+    out7[3] = st.Get1D();
+    st.Get2D(&out7[4], &out7[5]);
+    out7[6] = st.Get1D();
+}
+void oracle_rng(uint64_t seq, uint64_t advance, uint32_t *out2) {
+    SeqRNG r;
+    r.SetSequence(seq);
+    r.Advance(advance);
+    out2[0] = r.Next();
+    out2[1] = r.Next();
 }
 
 float oracle_halton(int xres, int yres, int seed, int px, int py, int sampleIndex, int dim) {

@@ -31,6 +31,8 @@ def lib():
         _lib.oracle_sample_wavelengths.argtypes = [ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p]
         _lib.oracle_halton.argtypes = [ctypes.c_int] * 7
         _lib.oracle_zsobol.argtypes = [ctypes.c_int] * 9 + [ctypes.c_void_p]
+        _lib.oracle_sampler.argtypes = [ctypes.c_int] * 9 + [ctypes.c_void_p] * 3 + [ctypes.c_int] * 4 + [ctypes.c_void_p]
+        _lib.oracle_rng.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]
         vp = ctypes.c_void_p
         _lib.oracle_warps.argtypes = [vp, vp, vp]
         _lib.oracle_spherical_triangle.argtypes = [vp, vp, vp, vp]
@@ -306,3 +308,27 @@ def triangle_shading(p9, n9, uv6, flip, b3, u2):
                                   None if t is None else t.ctypes.data, int(flip), b.ctypes.data, u.ctypes.data,
                                   out.ctypes.data)
     return out
+
+
+SAMPLER_KINDS = {"independent": 2, "stratified": 3, "sobol": 4, "paddedsobol": 5}
+RANDOMIZE = {"none": 0, "permutedigits": 1, "fastowen": 2, "owen": 3}
+
+
+def sampler(name, px, py, sample_index, dim, spp=16, seed=0, xsamples=4, ysamples=4, jitter=1,
+            randomization="fastowen", xres=256, yres=256, tables=None):
+    """The oracle's independent / stratified / sobol / paddedsobol sampler: 7 values in the
+    wavefront's call order from StartPixelSample((px, py), sample_index, dim).  tables =
+    (SobolMatrices32, VdCSobolMatrices, VdCSobolMatricesInv) numpy arrays (sobol only)."""
+    out = np.zeros(7, np.float32)
+    m32, vdc, inv = tables if tables is not None else (None, None, None)
+    ptr = lambda a: None if a is None else a.ctypes.data
+    lib().oracle_sampler(SAMPLER_KINDS[name], spp, seed, xsamples, ysamples, jitter, RANDOMIZE[randomization],
+                         xres, yres, ptr(m32), ptr(vdc), ptr(inv), px, py, sample_index, dim, out.ctypes.data)
+    return out
+
+
+def rng(seq, advance):
+    """RNG::SetSequence(seq), Advance(advance), two Uniform<uint32_t>() (oracle restatement)."""
+    out = np.zeros(2, np.uint32)
+    lib().oracle_rng(int(seq), int(advance), out.ctypes.data)
+    return int(out[0]), int(out[1])

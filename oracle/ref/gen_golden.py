@@ -12,6 +12,9 @@ from pathlib import Path
 HERE = Path(__file__).resolve().parent
 ROOT = HERE.parents[1]
 OUT = ROOT / "tests" / "golden" / "reference_components.json"
+# util/sobolmatrices.cpp's tables as the product's data file (constant data the SobolSampler
+# needs bit for bit; written by the reference's own compiled table)
+SOBOL = ROOT / "pbrt-v4_amd" / "data" / "sobol_tables.bin"
 
 
 def main():
@@ -22,6 +25,8 @@ def main():
     data = json.loads(tmp.read_text())
     OUT.write_text(json.dumps(data, separators=(",", ":")))
     tmp.unlink()
+    subprocess.check_call([str(ROOT / "oracle" / "_ref" / "refgold"), "--sobol-tables", str(SOBOL)])
+    print("wrote", SOBOL, SOBOL.stat().st_size, "bytes")
     print("wrote", OUT, OUT.stat().st_size, "bytes", sorted(data))
 
 

@@ -477,6 +477,8 @@ struct pbrt_context {
     DevBuf<uint16_t> permByDepth;
     DevBuf<uint8_t> zsPerms;
     DevBuf<uint32_t> sobolM1;
+    DevBuf<uint32_t> sobol32;           // SobolSampler: SobolMatrices32 (only for that sampler)
+    DevBuf<uint64_t> vdcSobol, vdcSobolInv;
     DevBuf<uint32_t> permDepthInfo;
     DevBuf<float> sensor4;
     DevBuf<DeviceLightNode> lightNodes;
@@ -1260,6 +1262,18 @@ static void BuildDevice(pbrt_context *c) {
     S.zs = ZSobolParams{s.zsLog2SamplesPerPixel, s.zsNBase4Digits, s.seed, (Randomize)s.zsRandomize};
     S.zsPerms = reinterpret_cast<const uint8_t(*)[4]>(c->zsPerms.p);
     S.sobolM1 = c->sobolM1.p;
+    // IndependentSampler / StratifiedSampler / SobolSampler / PaddedSobolSampler (core.h GenericSampler)
+    S.samp = SamplerDesc{s.samplerType, s.spp, s.seed, s.stratXs, s.stratYs, s.stratJitter,
+                         (Randomize)s.zsRandomize, s.sobolLog2Scale, nullptr, nullptr, nullptr};
+    if (s.samplerType == kSamplerSobol) {
+        const SobolTableData &sob = SobolTables();
+        c->sobol32.Upload(sob.m32);
+        c->vdcSobol.Upload(sob.vdc);
+        c->vdcSobolInv.Upload(sob.vdcInv);
+        S.samp.sobol32 = c->sobol32.p;
+        S.samp.vdc = c->vdcSobol.p;
+        S.samp.vdcInv = c->vdcSobolInv.p;
+    }
     {
         // k_shade_diffuse dynamic LDS: [beta*f 31x256 floats][sensor][light spectra][Halton
         // permutations of 7 dims][lights][light BVH][materials]
@@ -1921,6 +1935,16 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
     f->zs_randomize = s.zsRandomize;
     f->zs_log2_spp = s.zsLog2SamplesPerPixel;
     f->zs_nbase4_digits = s.zsNBase4Digits;
+    f->strat_xsamples = s.stratXs;
+    f->strat_ysamples = s.stratYs;
+    f->strat_jitter = s.stratJitter;
+    f->sobol_log2_scale = s.sobolLog2Scale;
+    if (s.samplerType == kSamplerSobol) {
+        const SobolTableData &sob = SobolTables();
+        f->sobol_matrices32 = sob.m32.data();
+        f->vdc_sobol = sob.vdc.data();
+        f->vdc_sobol_inv = sob.vdcInv.data();
+    }
     f->material_type = scene->matType.data();
     f->material_params = scene->matParams.data();
     f->material_layer = scene->matLayer.data();
@@ -2537,6 +2561,45 @@ int pbrt_debug_zsobol(const pbrt_scene *scene, int px, int py, int sampleIndex, 
     } catch (const std::exception &e) {
         return Fail(e.what());
     }
+}
+
+int pbrt_debug_sampler(const pbrt_scene *scene, int px, int py, int sampleIndex, int dim, float *out7) {
+    try {
+        if (!scene || !out7) return Fail("null argument");
+        const SceneDesc &s = scene->desc;
+        if (s.samplerType < kSamplerIndependent) return Fail("pbrt_debug_sampler: the scene's sampler is halton or zsobol");
+        SamplerDesc d{s.samplerType, s.spp, s.seed, s.stratXs, s.stratYs, s.stratJitter, (Randomize)s.zsRandomize,
+                      s.sobolLog2Scale, nullptr, nullptr, nullptr};
+        if (s.samplerType == kSamplerSobol) {
+            const SobolTableData &sob = SobolTables();
+            d.sobol32 = sob.m32.data();
+            d.vdc = sob.vdc.data();
+            d.vdcInv = sob.vdcInv.data();
+        }
+        GenericSampler g;
+        g.Start(d, px, py, sampleIndex, dim);
+        // dimension 0: the camera's Get1D, GetPixel2D, Get1D, Get2D, Get1D; otherwise the ray
+        // samples' Get1D, Get2D, Get1D, Get2D, Get1D
+        out7[0] = g.Get1D(d);
+        if (dim == 0) g.GetPixel2D(d, &out7[1], &out7[2]);
+        else g.Get2D(d, &out7[1], &out7[2]);
+        out7[3] = g.Get1D(d);
+        g.Get2D(d, &out7[4], &out7[5]);
+        out7[6] = g.Get1D(d);
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_debug_rng(uint64_t seq, uint64_t advance, uint32_t *out2) {
+    if (!out2) return Fail("null argument");
+    PCG32 r;
+    r.SetSequence(seq);
+    r.Advance(advance);
+    out2[0] = r.NextU32();
+    out2[1] = r.NextU32();
+    return 0;
 }
 
 int pbrt_debug_trowbridge(const float *in, float *out) {

@@ -1502,6 +1502,196 @@ struct PCG32 {
         return (xorshifted >> rot) | (xorshifted << ((~rot + 1u) & 31));
     }
     PHD float Uniform() { return std::fmin(kOneMinusEpsilon, (float)NextU32() * 0x1p-32f); }
+    PHD PCG32() : state(0x853c49e6748fea9bULL), inc(0xda3e39cb94b95bdbULL) {}  // PCG32_DEFAULT_STATE / STREAM
+    // SetSequence(sequenceIndex) = SetSequence(sequenceIndex, MixBits(sequenceIndex)) (rng.h:43-45, 119-125)
+    PHD void SetSequence(uint64_t seqIndex);
+    // Advance (rng.h:137-150): the state after idelta draws, by repeated squaring of the LCG step
+    PHD void Advance(uint64_t delta) {
+        uint64_t curMult = 0x5851f42d4c957f2dULL, curPlus = inc, accMult = 1u, accPlus = 0u;
+        while (delta > 0) {
+            if (delta & 1) {
+                accMult *= curMult;
+                accPlus = accPlus * curMult + curPlus;
+            }
+            curPlus = (curMult + 1) * curPlus;
+            curMult *= curMult;
+            delta /= 2;
+        }
+        state = accMult * state + accPlus;
+    }
+};
+PHD void PCG32::SetSequence(uint64_t seqIndex) {
+    state = 0u;
+    inc = (seqIndex << 1u) | 1u;
+    NextU32();
+    state += MixBits(seqIndex);
+    NextU32();
+}
+
+// PermutationElement (util/math.h:728-756): element i of the seeded permutation of [0, l)
+PHD int PermutationElement(uint32_t i, uint32_t l, uint32_t p) {
+    uint32_t w = l - 1;
+    w |= w >> 1;
+    w |= w >> 2;
+    w |= w >> 4;
+    w |= w >> 8;
+    w |= w >> 16;
+    do {
+        i ^= p;
+        i *= 0xe170893d;
+        i ^= p >> 16;
+        i ^= (i & w) >> 4;
+        i ^= p >> 8;
+        i *= 0x0929eb3f;
+        i ^= p >> 23;
+        i ^= (i & w) >> 1;
+        i *= 1 | p >> 27;
+        i *= 0x6935fa69;
+        i ^= (i & w) >> 11;
+        i *= 0x74dcb303;
+        i ^= (i & w) >> 2;
+        i *= 0x9e501cc3;
+        i ^= (i & w) >> 2;
+        i *= 0xc860a3df;
+        i &= w;
+        i ^= i >> 5;
+    } while (i >= l);
+    return (int)((i + p) % l);
+}
+
+// ---------------------------------------------------------------- the other samplers
+// IndependentSampler, StratifiedSampler, SobolSampler, PaddedSobolSampler (samplers.h:144-224,
+// 442-633), behind one state object so every kernel calls them the same way.  Sobol' rows come
+// from util/sobolmatrices.cpp's tables (data/sobol_tables.bin, uploaded when the scene uses the
+// SobolSampler): SobolMatrices32 [1024][52], VdCSobolMatrices and VdCSobolMatricesInv [25][52].
+constexpr int kSamplerHalton = 0, kSamplerZSobol = 1, kSamplerIndependent = 2, kSamplerStratified = 3,
+              kSamplerSobol = 4, kSamplerPaddedSobol = 5;
+constexpr int kNSobolDimensions = 1024, kNVdCSobol = 25;
+struct SamplerDesc {
+    int type, spp, seed;
+    int xSamples, ySamples, jitter;  // StratifiedSampler
+    Randomize randomize;             // SobolSampler / PaddedSobolSampler
+    int log2Scale;                   // SobolSampler: Log2Int(RoundUpPow2(max(xres, yres)))
+    const uint32_t *sobol32;         // [1024 * 52]
+    const uint64_t *vdc, *vdcInv;    // [25][52]
+};
+// Hash(p, seed) (12 bytes) and Hash(p, dimension, seed) (16 bytes), util/hash.h:91-106
+PHD uint64_t HashPixelSeed(int px, int py, int seed) {
+    const uint32_t w[3] = {(uint32_t)px, (uint32_t)py, (uint32_t)seed};
+    return HashWords(w, 3);
+}
+PHD uint64_t HashPixelDimSeed(int px, int py, int dim, int seed) {
+    const uint32_t w[4] = {(uint32_t)px, (uint32_t)py, (uint32_t)dim, (uint32_t)seed};
+    return HashWords(w, 4);
+}
+// SobolSample (lowdiscrepancy.h:167-180) of any dimension, then the scrambler
+PHD float SobolSampleDim(uint64_t a, int dim, Randomize rz, uint32_t seed, const uint32_t *m32) {
+    uint32_t v = 0;
+    for (int i = dim * kSobolMatrixSize; a != 0; a >>= 1, i++)
+        if (a & 1) v ^= m32[i];
+    if (rz == Randomize::PermuteDigits) v ^= seed;
+    else if (rz == Randomize::FastOwen) v = FastOwenScramble(v, seed);
+    else if (rz == Randomize::Owen) v = OwenScramble(v, seed);
+    return std::fmin(v * 0x1p-32f, kOneMinusEpsilon);
+}
+// SobolIntervalToIndex (lowdiscrepancy.h:266-287)
+PHD uint64_t SobolIntervalToIndex(const SamplerDesc &d, uint32_t m, uint64_t frame, int px, int py) {
+    if (m == 0) return frame;
+    const uint32_t m2 = m << 1;
+    uint64_t index = uint64_t(frame) << m2;
+    uint64_t delta = 0;
+    for (int c = 0; frame; frame >>= 1, ++c)
+        if (frame & 1) delta ^= d.vdc[(m - 1) * kSobolMatrixSize + c];
+    uint64_t b = (((uint64_t)((uint32_t)px) << m) | ((uint32_t)py)) ^ delta;
+    for (int c = 0; b; b >>= 1, ++c)
+        if (b & 1) index ^= d.vdcInv[(m - 1) * kSobolMatrixSize + c];
+    return index;
+}
+struct GenericSampler {
+    int px, py, sampleIndex, dimension;
+    uint64_t sobolIndex;
+    PCG32 rng;
+    // StartPixelSample
+    PHD void Start(const SamplerDesc &d, int x, int y, int index, int dim) {
+        px = x, py = y, sampleIndex = index, dimension = dim, sobolIndex = 0;
+        if (d.type == kSamplerIndependent || d.type == kSamplerStratified) {
+            rng.SetSequence(HashPixelSeed(x, y, d.seed));
+            rng.Advance((uint64_t)index * 65536ull + (uint64_t)dim);
+        } else if (d.type == kSamplerSobol) {
+            dimension = dim < 2 ? 2 : dim;
+            sobolIndex = SobolIntervalToIndex(d, (uint32_t)d.log2Scale, (uint64_t)index, x, y);
+        }
+    }
+    // SobolSampler::SampleDimension
+    PHD float SobolDim(const SamplerDesc &d, int dim) const {
+        if (d.randomize == Randomize::None) return SobolSampleDim(sobolIndex, dim, Randomize::None, 0, d.sobol32);
+        return SobolSampleDim(sobolIndex, dim, d.randomize, (uint32_t)HashInt2(dim, d.seed), d.sobol32);
+    }
+    PHD float Get1D(const SamplerDesc &d) {
+        if (d.type == kSamplerIndependent) return rng.Uniform();
+        if (d.type == kSamplerStratified) {
+            const uint64_t hash = HashPixelDimSeed(px, py, dimension, d.seed);
+            const int n = d.xSamples * d.ySamples;
+            const int stratum = PermutationElement((uint32_t)sampleIndex, (uint32_t)n, (uint32_t)hash);
+            ++dimension;
+            const float delta = d.jitter ? rng.Uniform() : 0.5f;
+            return (stratum + delta) / n;
+        }
+        if (d.type == kSamplerSobol) {
+            if (dimension >= kNSobolDimensions) dimension = 2;
+            return SobolDim(d, dimension++);
+        }
+        // PaddedSobolSampler
+        const uint64_t hash = HashPixelDimSeed(px, py, dimension, d.seed);
+        const int index = PermutationElement((uint32_t)sampleIndex, (uint32_t)d.spp, (uint32_t)hash);
+        ++dimension;
+        return SobolSampleDim01((uint64_t)(uint32_t)index, 0, d.randomize, (uint32_t)(hash >> 32), nullptr);
+    }
+    PHD void Get2D(const SamplerDesc &d, float *u0, float *u1) {
+        if (d.type == kSamplerIndependent) {
+            *u0 = rng.Uniform();
+            *u1 = rng.Uniform();
+            return;
+        }
+        if (d.type == kSamplerStratified) {
+            const uint64_t hash = HashPixelDimSeed(px, py, dimension, d.seed);
+            const int stratum =
+                PermutationElement((uint32_t)sampleIndex, (uint32_t)(d.xSamples * d.ySamples), (uint32_t)hash);
+            dimension += 2;
+            const int x = stratum % d.xSamples, y = stratum / d.xSamples;
+            const float dx = d.jitter ? rng.Uniform() : 0.5f;
+            const float dy = d.jitter ? rng.Uniform() : 0.5f;
+            *u0 = (x + dx) / d.xSamples;
+            *u1 = (y + dy) / d.ySamples;
+            return;
+        }
+        if (d.type == kSamplerSobol) {
+            if (dimension + 1 >= kNSobolDimensions) dimension = 2;
+            *u0 = SobolDim(d, dimension);
+            *u1 = SobolDim(d, dimension + 1);
+            dimension += 2;
+            return;
+        }
+        const uint64_t hash = HashPixelDimSeed(px, py, dimension, d.seed);
+        const int index = PermutationElement((uint32_t)sampleIndex, (uint32_t)d.spp, (uint32_t)hash);
+        dimension += 2;
+        *u0 = SobolSampleDim01((uint64_t)(uint32_t)index, 0, d.randomize, (uint32_t)hash, nullptr);
+        *u1 = SobolSampleDim01((uint64_t)(uint32_t)index, 1, d.randomize, (uint32_t)(hash >> 32), nullptr);
+    }
+    PHD void GetPixel2D(const SamplerDesc &d, float *u0, float *u1) {
+        if (d.type != kSamplerSobol) {
+            Get2D(d, u0, u1);
+            return;
+        }
+        // SobolSampler::GetPixel2D: dimensions 0 and 1 of the pixel's interval, unscrambled,
+        // remapped into the pixel
+        float u[2] = {SobolSampleDim(sobolIndex, 0, Randomize::None, 0, d.sobol32),
+                      SobolSampleDim(sobolIndex, 1, Randomize::None, 0, d.sobol32)};
+        const int scale = 1 << d.log2Scale, p[2] = {px, py};
+        for (int k = 0; k < 2; ++k) u[k] = Clampf(u[k] * scale - p[k], 0, kOneMinusEpsilon);
+        *u0 = u[0];
+        *u1 = u[1];
+    }
 };
 
 // FastExp (util/math.h:450-475), the CPU form (2^x by a cubic on the fraction, exponent bits

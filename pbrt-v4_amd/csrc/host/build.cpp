@@ -1,6 +1,8 @@
 // Scene finalisation: BVH light sampler construction (lightsamplers.cpp:112-236,
 // lights.cpp:803-822, lightsamplers.h:95-229) and Halton digit-permutation tables
 // (util/lowdiscrepancy.h:25-55, samplers.cpp:32-52).
+#include <fstream>
+#include <mutex>
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -62,35 +64,6 @@ uint64_t MurmurHash64A(const unsigned char *key, size_t len, uint64_t seed) {
     return h;
 }
 
-int PermutationElement(uint32_t i, uint32_t l, uint32_t p) {
-    uint32_t w = l - 1;
-    w |= w >> 1;
-    w |= w >> 2;
-    w |= w >> 4;
-    w |= w >> 8;
-    w |= w >> 16;
-    do {
-        i ^= p;
-        i *= 0xe170893d;
-        i ^= p >> 16;
-        i ^= (i & w) >> 4;
-        i ^= p >> 8;
-        i *= 0x0929eb3f;
-        i ^= p >> 23;
-        i ^= (i & w) >> 1;
-        i *= 1 | p >> 27;
-        i *= 0x6935fa69;
-        i ^= (i & w) >> 11;
-        i *= 0x74dcb303;
-        i ^= (i & w) >> 2;
-        i *= 0x9e501cc3;
-        i ^= (i & w) >> 2;
-        i *= 0xc860a3df;
-        i &= w;
-        i ^= i >> 5;
-    } while (i >= l);
-    return (i + p) % l;
-}
 
 static int NumDigits(int base) {
     // DigitPermutation ctor digit count (float arithmetic, no contraction)
@@ -596,6 +569,34 @@ static void BuildZSobol(SceneDesc &s) {
     while (res < std::max(s.xres, s.yres)) res <<= 1;  // RoundUpPow2
     int log4SamplesPerPixel = (s.zsLog2SamplesPerPixel + 1) / 2;
     s.zsNBase4Digits = log2Int(res) + log4SamplesPerPixel;
+    s.sobolLog2Scale = log2Int(res);  // SobolSampler: scale = RoundUpPow2(max(fullResolution))
+    if (s.samplerType == kSamplerSobol && s.sobolLog2Scale > kNVdCSobol)
+        throw Error("sobol: resolution above 2^25 pixels per side is outside the VdC Sobol' tables");
+}
+
+const SobolTableData &SobolTables() {
+    static std::once_flag once;
+    static SobolTableData t;
+    static std::string err;
+    std::call_once(once, [] {
+        const std::string path = GetDataDirectory() + "/sobol_tables.bin";
+        std::ifstream in(path, std::ios::binary);
+        const size_t n32 = (size_t)kNSobolDimensions * kSobolMatrixSize, nv = (size_t)kNVdCSobol * kSobolMatrixSize;
+        t.m32.resize(n32);
+        t.vdc.resize(nv);
+        t.vdcInv.resize(nv);
+        bool ok = (bool)in;
+        if (ok) in.read(reinterpret_cast<char *>(t.m32.data()), (std::streamsize)(n32 * 4));
+        if (ok) in.read(reinterpret_cast<char *>(t.vdc.data()), (std::streamsize)(nv * 8));
+        if (ok) in.read(reinterpret_cast<char *>(t.vdcInv.data()), (std::streamsize)(nv * 8));
+        ok = ok && in.gcount() == (std::streamsize)(nv * 8) && in.peek() == EOF;
+        // dimensions 0 and 1 must be the matrices the ZSobol path generates on the fly
+        for (int k = 0; ok && k < kSobolMatrixSize; ++k)
+            ok = t.m32[k] == (k < 32 ? 0x80000000u >> k : 0u) && t.m32[kSobolMatrixSize + k] == SobolMatrix1Row(k);
+        if (!ok) err = "SobolSampler: " + path + " is missing or malformed (oracle/ref/gen_golden.py writes it)";
+    });
+    if (!err.empty()) throw Error(err);
+    return t;
 }
 
 void FinalizeScene(SceneDesc &s) {

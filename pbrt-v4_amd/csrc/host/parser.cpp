@@ -1489,17 +1489,49 @@ void Parser::Finish() {
         scene.samplerType = 0;
         if (samplerParams.GetString("randomization", "permutedigits") != "permutedigits")
             throw Error(samplerParams.loc + ": halton: only permutedigits randomization is supported");
-    } else if (scene.samplerName == "zsobol") {
-        // samplers.cpp:146-170 (ZSobolSampler::Create), default randomization fastowen
-        scene.samplerType = 1;
+    } else if (scene.samplerName == "zsobol" || scene.samplerName == "sobol" || scene.samplerName == "paddedsobol") {
+        // samplers.cpp:108-130, 146-170, 258-295 (PaddedSobol / ZSobol / SobolSampler::Create):
+        // default randomization fastowen
+        scene.samplerType = scene.samplerName == "zsobol" ? kSamplerZSobol
+                            : scene.samplerName == "sobol" ? kSamplerSobol : kSamplerPaddedSobol;
         std::string r = samplerParams.GetString("randomization", "fastowen");
         if (r == "none") scene.zsRandomize = 0;
         else if (r == "permutedigits") scene.zsRandomize = 1;
         else if (r == "fastowen") scene.zsRandomize = 2;
         else if (r == "owen") scene.zsRandomize = 3;
-        else throw Error(samplerParams.loc + ": unknown randomization strategy \"" + r + "\" given to ZSobolSampler");
+        else {
+            const char *cls = scene.samplerType == kSamplerZSobol ? "ZSobolSampler"
+                              : scene.samplerType == kSamplerSobol ? "SobolSampler" : "PaddedSobolSampler";
+            throw Error(samplerParams.loc + ": unknown randomization strategy \"" + r + "\" given to " + cls);
+        }
+    } else if (scene.samplerName == "independent") {
+        // samplers.cpp:240-247 (IndependentSampler::Create): 4 pixel samples by default
+        scene.samplerType = kSamplerIndependent;
+        scene.spp = samplerParams.GetInt("pixelsamples", 4);
+        if (overrides.count("spp")) scene.spp = std::stoi(overrides.at("spp"));
+    } else if (scene.samplerName == "stratified") {
+        // samplers.cpp:297-320 (StratifiedSampler::Create): xsamples x ysamples strata, jittered
+        // by default; a pixel-sample override is factored into the two counts
+        scene.samplerType = kSamplerStratified;
+        scene.stratJitter = samplerParams.GetBool("jitter", true) ? 1 : 0;
+        scene.stratXs = samplerParams.GetInt("xsamples", 4);
+        scene.stratYs = samplerParams.GetInt("ysamples", 4);
+        if (overrides.count("spp")) {
+            const int n = std::stoi(overrides.at("spp"));
+            int div = (int)std::sqrt((double)n);
+            while (div > 0 && n % div) --div;
+            if (div <= 0) throw Error("stratified: cannot factor " + std::to_string(n) + " pixel samples");
+            scene.stratXs = n / div;
+            scene.stratYs = n / scene.stratXs;
+        }
+        if (scene.stratXs <= 0 || scene.stratYs <= 0)
+            throw Error(samplerParams.loc + ": stratified: xsamples and ysamples must be positive");
+        scene.spp = scene.stratXs * scene.stratYs;
+    } else if (scene.samplerName == "pmj02bn") {
+        throw Error(samplerParams.loc + ": sampler \"pmj02bn\" not supported (its PMJ02BN tables are not part of "
+                                        "this build); use halton, zsobol, sobol, paddedsobol, independent or stratified");
     } else {
-        throw Error(samplerParams.loc + ": sampler \"" + scene.samplerName + "\" not supported yet (halton, zsobol)");
+        throw Error(samplerParams.loc + ": unknown sampler \"" + scene.samplerName + "\"");
     }
     samplerParams.CheckUnused();
     // ---- integrator

@@ -343,7 +343,10 @@ struct SceneDesc {
 
     // sampler: 0 = HaltonSampler (permutedigits), 1 = ZSobolSampler (samplers.h:225-370)
     int samplerType = 1;
-    int zsRandomize = 2;  // Randomize: 0 none, 1 permutedigits, 2 fastowen, 3 owen
+    // Randomize of zsobol / sobol / paddedsobol: 0 none, 1 permutedigits, 2 fastowen, 3 owen
+    int zsRandomize = 2;
+    int stratXs = 4, stratYs = 4, stratJitter = 1;  // StratifiedSampler
+    int sobolLog2Scale = 0;                         // SobolSampler: Log2(RoundUpPow2(max(xres, yres)))
     int zsLog2SamplesPerPixel = 0, zsNBase4Digits = 0;
 
     // Halton digit permutations (util/lowdiscrepancy.cpp:47-55) for the dimensions used
@@ -417,6 +420,14 @@ std::array<float, 311> DenseCIEDaylight(float T);
 // data[3][64][64][64][3]; loaded from data/rgbspec_srgb.bin (written by the build), computed
 // in parallel (and cached there) when the file is absent
 const std::vector<float> &RGBToSpectrumTableData();
+// util/sobolmatrices.cpp's tables, from data/sobol_tables.bin (oracle/ref/gen_golden.py writes it
+// from the reference's compiled tables): SobolMatrices32 [1024 * 52], then VdCSobolMatrices and
+// VdCSobolMatricesInv [25 * 52]; throws when the file is absent or malformed
+struct SobolTableData {
+    std::vector<uint32_t> m32;
+    std::vector<uint64_t> vdc, vdcInv;
+};
+const SobolTableData &SobolTables();
 const SpectralData &GetSpectralData();
 void SetDataDirectory(const std::string &dir);
 std::string GetDataDirectory();
@@ -434,7 +445,6 @@ PLSpectrumDesc NamedPiecewiseLinear(const std::string &name);
 
 // Hash / permutation (util/hash.h:19, util/math.h:728)
 uint64_t MurmurHash64A(const unsigned char *key, size_t len, uint64_t seed);
-int PermutationElement(uint32_t i, uint32_t l, uint32_t p);
 const std::vector<int> &Primes();
 
 }  // namespace pbrt_amd

@@ -1484,7 +1484,19 @@ __device__ inline void GenerateCameraRay(const DeviceScene &S, const PathState &
     // camera.cpp:50-62: wavelength Get1D, then GetCameraSample (samplers.h:797-813): pixel
     // offset (GetPixel2D) through the box filter (filters.h:67-71), time Get1D, lens Get2D
     float lu, pix0, pix1, l0, l1;
-    if (S.samplerType == 1) {
+    if (S.samplerType >= kSamplerIndependent) {
+        // independent / stratified / Sobol' / padded Sobol': Get1D, GetPixel2D, Get1D (time),
+        // Get2D (lens) in order -- the stateful samplers' draws depend on it
+        GenericSampler g;
+        g.Start(S.samp, px, py, sampleIndex, 0);
+        lu = g.Get1D(S.samp);
+        g.GetPixel2D(S.samp, &pix0, &pix1);
+        l0 = l1 = 0;
+        if (S.lensRadius > 0) {
+            (void)g.Get1D(S.samp);
+            g.Get2D(S.samp, &l0, &l1);
+        }
+    } else if (S.samplerType == 1) {
         // ZSobolSampler: dimensions 0 (wavelength), 1-2 (pixel), 3 (time), 4-5 (lens)
         const uint64_t morton = ZSobolMortonIndex(S.zs, px, py, sampleIndex);
         lu = ZSobolGet1D(S.zs, morton, 0, S.zsPerms, S.sobolM1);

@@ -227,8 +227,9 @@ struct DeviceScene {
     int nDims;
     int baseScales[2], baseExponents[2], multInverse[2];
     int haltonFast32;  // pixel offsets computable in 32 bits (StartPixelSample fast path)
-    // sampler: 0 Halton, 1 ZSobol
+    // sampler: 0 Halton, 1 ZSobol, 2 independent, 3 stratified, 4 Sobol, 5 padded Sobol (core.h kSampler*)
     int samplerType;
+    SamplerDesc samp;  // the last four (core.h GenericSampler)
     ZSobolParams zs;
     const uint8_t (*zsPerms)[4];  // [24][4]
     const uint32_t *sobolM1;      // Sobol' dimension-1 matrix rows [52]

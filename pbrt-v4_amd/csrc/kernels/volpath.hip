@@ -470,7 +470,17 @@ __device__ inline VRaySamples RaySamplesAt(const DeviceScene &S, const PathState
     px += S.px0;
     const int d0 = 6 + 7 * depth;
     VRaySamples r;
-    if (S.samplerType == 1) {
+    if (S.samplerType >= kSamplerIndependent) {
+        // the other samplers are stateful: every draw in pbrt's order, indirect.uc included
+        GenericSampler g;
+        g.Start(S.samp, px, py, sampleIndex, d0);
+        r.dUc = g.Get1D(S.samp);
+        g.Get2D(S.samp, &r.dU0, &r.dU1);
+        const float iuc = g.Get1D(S.samp);
+        r.iUc = indirectUc ? iuc : 0.f;
+        g.Get2D(S.samp, &r.iU0, &r.iU1);
+        r.rr = g.Get1D(S.samp);
+    } else if (S.samplerType == 1) {
         const uint64_t morton = ZSobolMortonIndex(S.zs, px, py, sampleIndex);
         r.dUc = ZSobolGet1D(S.zs, morton, d0, S.zsPerms, S.sobolM1);
         ZSobolGet2D(S.zs, morton, d0 + 1, S.zsPerms, S.sobolM1, &r.dU0, &r.dU1);

@@ -102,6 +102,9 @@ class SceneFlat(ctypes.Structure):
         ("max_component_value", ctypes.c_float),
         ("xyz_from_sensor_rgb", ctypes.c_float * 9),
         ("material_bump", ctypes.POINTER(ctypes.c_int32)),
+        ("strat_xsamples", ctypes.c_int), ("strat_ysamples", ctypes.c_int), ("strat_jitter", ctypes.c_int),
+        ("sobol_log2_scale", ctypes.c_int), ("sobol_matrices32", ctypes.POINTER(ctypes.c_uint32)),
+        ("vdc_sobol", ctypes.POINTER(ctypes.c_uint64)), ("vdc_sobol_inv", ctypes.POINTER(ctypes.c_uint64)),
     ]
 
 
@@ -131,7 +134,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_context_free", "pbrt_render", "pbrt_synchronize", "pbrt_get_stats", "pbrt_reset_stats",
     "pbrt_film_clear", "pbrt_film_device_ptr", "pbrt_film_read", "pbrt_film_get_rgb", "pbrt_intersect",
     "pbrt_debug_halton", "pbrt_debug_halton_fastpath_mismatches", "pbrt_debug_check_rn_math", "pbrt_debug_rgb_coeffs", "pbrt_debug_rgb2spec_column", "pbrt_debug_kernel_sections",
-    "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
+    "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_sampler", "pbrt_debug_rng", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
     "pbrt_debug_named_spectrum", "pbrt_debug_bxdf", "pbrt_debug_layered", "pbrt_debug_triangle_shading", "pbrt_film_write_image",
     "pbrt_image_read_size", "pbrt_image_read", "pbrt_image_write", "pbrt_image_error", "pbrt_debug_filter_sample",
     "pbrt_debug_bvh_stats", "pbrt_debug_light_bvh", "pbrt_intersect_tr", "pbrt_image_flip", "pbrt_set_kernel_profiling", "pbrt_get_kernel_stats",
@@ -203,6 +206,8 @@ def _lib():
     lib.pbrt_debug_rgb2spec_column.argtypes = [c.c_int, c.c_int, c.c_int, c.POINTER(c.c_float)]
     lib.pbrt_debug_kernel_sections.argtypes = [c.c_void_p, c.POINTER(c.c_uint64), c.c_int]
     lib.pbrt_debug_zsobol.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_int, c.POINTER(c.c_float)]
+    lib.pbrt_debug_sampler.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_int, c.POINTER(c.c_float)]
+    lib.pbrt_debug_rng.argtypes = [c.c_uint64, c.c_uint64, c.POINTER(c.c_uint32)]
     lib.pbrt_debug_queue_counts.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_int]
     lib.pbrt_debug_trowbridge.argtypes = [c.c_void_p, c.c_void_p]
     lib.pbrt_debug_fresnel.argtypes = [c.c_void_p, c.c_void_p]
@@ -374,6 +379,14 @@ class Scene:
         _check(_lib().pbrt_debug_zsobol(self._h, px, py, sample_index, dim, out))
         return np.array(out[:], dtype=np.float32)
 
+    def sampler_values(self, px, py, sample_index, dim):
+        """The scene's independent / stratified / sobol / paddedsobol sampler from
+        StartPixelSample((px, py), sample_index, dim): 7 values in the wavefront's call order
+        (pbrt_debug_sampler)."""
+        out = (ctypes.c_float * 7)()
+        _check(_lib().pbrt_debug_sampler(self._h, px, py, sample_index, dim, out))
+        return np.array(out[:], dtype=np.float32)
+
     def filter_sample(self, u0, u1):
         """Filter::Sample((u0, u1)) of the scene's pixel filter -> (p.x, p.y, weight)"""
         out = (ctypes.c_float * 3)()
@@ -443,6 +456,13 @@ def check_rn_math(n=1 << 28, seed=1, device=0):
     _check(_lib().pbrt_debug_check_rn_math(device, seed, n, ctypes.byref(out), ex))
     check_rn_math.examples = np.array(ex[:], np.float32).reshape(16, 6)[:min(out.value, 16)]
     return out.value
+
+
+def debug_rng(seq, advance):
+    """RNG::SetSequence(seq), Advance(advance), then two Uniform<uint32_t>() (pbrt_debug_rng)."""
+    out = (ctypes.c_uint32 * 2)()
+    _check(_lib().pbrt_debug_rng(int(seq), int(advance), out))
+    return int(out[0]), int(out[1])
 
 
 def device_count() -> int:

@@ -1,0 +1,190 @@
+"""IndependentSampler, StratifiedSampler, SobolSampler and PaddedSobolSampler (samplers.h:144-224,
+442-633; factory samplers.cpp:108-130, 240-320, 416-432) on the wavefront: the loader, the
+product's sampler evaluation (core.h GenericSampler, host side) and the oracle's independent
+restatement against the reference's own samplers (tests/golden, refgold), then GPU film parity.
+
+The wavefront's call order matters for the stateful samplers: the camera kernel draws Get1D
+(wavelength), GetPixel2D, Get1D (time), Get2D (lens) from dimension 0 (camera.cpp:31-80,
+samplers.h:797-813), and every depth's ray samples draw Get1D, Get2D, Get1D, Get2D, Get1D from
+dimension 6 + 7 depth (samples.cpp:29-66).  The goldens record exactly those sequences.
+"""
+import numpy as np
+import pytest
+
+from conftest import ROOT, SCENES, cornell_with_sampler
+
+SOBOL_BIN = ROOT / "pbrt-v4_amd" / "data" / "sobol_tables.bin"
+
+
+def f32(v):
+    return np.array([float(x) for x in v], np.float32)
+
+
+def sobol_tables():
+    raw = SOBOL_BIN.read_bytes()
+    m32 = np.frombuffer(raw[:1024 * 52 * 4], np.uint32).copy()
+    rest = np.frombuffer(raw[1024 * 52 * 4:], np.uint64)
+    return m32, rest[:25 * 52].copy(), rest[25 * 52:].copy()
+
+
+def sampler_line(cfg):
+    name = cfg["sampler"]
+    if name == "stratified":
+        return (f'Sampler "stratified" "integer xsamples" {cfg["xsamples"]} "integer ysamples" {cfg["ysamples"]} '
+                f'"bool jitter" {"true" if cfg["jitter"] else "false"} "integer seed" {cfg["seed"]}')
+    line = f'Sampler "{name}" "integer pixelsamples" {cfg["spp"]} "integer seed" {cfg["seed"]}'
+    if "randomization" in cfg:
+        line += f' "string randomization" "{cfg["randomization"]}"'
+    return line
+
+
+N_CFGS = 23  # len(golden["samplers"]): 3 independent, 4 stratified, 8 sobol, 8 paddedsobol
+
+
+def test_golden_sampler_set(golden):
+    assert len(golden["samplers"]) == N_CFGS
+    assert {c["sampler"] for c in golden["samplers"]} == {"independent", "stratified", "sobol", "paddedsobol"}
+
+
+def test_rng_advance_bit_exact(pa, oracle, golden):
+    """RNG::SetSequence + Advance (util/rng.h:119-150), which the independent and stratified
+    samplers start every pixel sample with: product (core.h PCG32) and oracle equal the reference."""
+    for seq, adv, a, b in golden["rng_advance"]:
+        assert pa.debug_rng(int(seq), int(adv)) == (a, b), (seq, adv)
+        assert oracle.rng(int(seq), int(adv)) == (a, b), (seq, adv)
+
+
+def test_sobol_tables_match_zsobol_matrices(pa):
+    """data/sobol_tables.bin is util/sobolmatrices.cpp written by the reference build
+    (oracle/ref/gen_golden.py): its first two dimensions are the van der Corput matrix and the
+    Pascal-triangle matrix the ZSobol path generates on the fly."""
+    m32, vdc, inv = sobol_tables()
+    assert m32.shape == (1024 * 52,) and vdc.shape == inv.shape == (25 * 52,)
+    for k in range(52):
+        assert m32[k] == (0x80000000 >> k if k < 32 else 0)
+    # VdCSobolMatrices[m = 1] holds 50 ones (sobolmatrices.cpp: the remaining entries are zero)
+    assert (vdc[:50] == 1).all() and (vdc[50:52] == 0).all()
+
+
+@pytest.mark.parametrize("cfg_index", range(N_CFGS))
+def test_sampler_product_bit_exact(pa, golden, cfg_index):
+    """The product's GenericSampler (core.h, the code the kernels run) against the reference's
+    sampler classes, value for value."""
+    cfg = golden["samplers"][cfg_index]
+    sc = cornell_with_sampler(pa, sampler_line(cfg), xresolution=cfg["xres"], yresolution=cfg["yres"])
+    f = sc.flat()
+    assert f.sampler_type == {"independent": 2, "stratified": 3, "sobol": 4, "paddedsobol": 5}[cfg["sampler"]]
+    for px, py, si, dim, vals in cfg["samples"]:
+        np.testing.assert_array_equal(sc.sampler_values(px, py, si, dim), f32(vals),
+                                      err_msg=f"{cfg['sampler']} {px} {py} {si} {dim}")
+
+
+@pytest.mark.parametrize("cfg_index", range(N_CFGS))
+def test_sampler_oracle_bit_exact(oracle, golden, cfg_index):
+    """The oracle's own restatement (oracle.cpp OtherState) against the same goldens."""
+    cfg = golden["samplers"][cfg_index]
+    tables = sobol_tables() if cfg["sampler"] == "sobol" else None
+    spp = cfg.get("spp", cfg.get("xsamples", 1) * cfg.get("ysamples", 1))
+    for px, py, si, dim, vals in cfg["samples"]:
+        got = oracle.sampler(cfg["sampler"], px, py, si, dim, spp=spp, seed=cfg["seed"],
+                             xsamples=cfg.get("xsamples", 4), ysamples=cfg.get("ysamples", 4),
+                             jitter=cfg.get("jitter", 1), randomization=cfg.get("randomization", "fastowen"),
+                             xres=cfg["xres"], yres=cfg["yres"], tables=tables)
+        np.testing.assert_array_equal(got, f32(vals), err_msg=f"{cfg['sampler']} {px} {py} {si} {dim}")
+
+
+def test_sampler_loader_defaults_and_overrides(pa):
+    """Create() defaults: independent 4 pixel samples; stratified xsamples x ysamples (4 x 4),
+    jittered; sobol / paddedsobol fastowen; a pixel-sample override is factored for the
+    stratified sampler (samplers.cpp:297-320: 12 -> 4 x 3)."""
+    sc = cornell_with_sampler(pa, 'Sampler "independent"')
+    assert sc.info.spp == 4 and sc.flat().sampler_type == 2
+    sc = cornell_with_sampler(pa, 'Sampler "stratified"')
+    f = sc.flat()
+    assert (sc.info.spp, f.strat_xsamples, f.strat_ysamples, f.strat_jitter) == (16, 4, 4, 1)
+    sc = cornell_with_sampler(pa, 'Sampler "stratified" "integer xsamples" 2 "bool jitter" false', spp=12)
+    f = sc.flat()
+    assert (sc.info.spp, f.strat_xsamples, f.strat_ysamples, f.strat_jitter) == (12, 4, 3, 0)
+    for name in ("sobol", "paddedsobol"):
+        sc = cornell_with_sampler(pa, f'Sampler "{name}"')
+        assert sc.info.spp == 16 and sc.flat().zs_randomize == 2
+    sc = cornell_with_sampler(pa, 'Sampler "sobol"', xresolution=1280, yresolution=720)
+    f = sc.flat()
+    assert f.sobol_log2_scale == 11 and bool(f.sobol_matrices32)
+
+
+@pytest.mark.parametrize("line, msg", [
+    ('Sampler "pmj02bn"', "pmj02bn"),
+    ('Sampler "sobol" "string randomization" "nope"', "SobolSampler"),
+    ('Sampler "paddedsobol" "string randomization" "nope"', "PaddedSobolSampler"),
+    ('Sampler "bogus"', "unknown sampler"),
+])
+def test_sampler_loader_errors(pa, line, msg):
+    with pytest.raises(pa.PbrtError, match=msg):
+        cornell_with_sampler(pa, line)
+
+
+def test_stratified_oracle_strata_cover_the_pixel(oracle):
+    """Known answer: with jitter off, a 4 x 4 stratified pixel's 16 GetPixel2D samples are the
+    16 stratum centres, each exactly once."""
+    pts = set()
+    for si in range(16):
+        v = oracle.sampler("stratified", 5, 7, si, 0, spp=16, xsamples=4, ysamples=4, jitter=0)
+        pts.add((float(v[1]), float(v[2])))
+    assert pts == {((x + 0.5) / 4, (y + 0.5) / 4) for x in range(4) for y in range(4)}
+
+
+SAMPLERS_GPU = [
+    'Sampler "independent" "integer pixelsamples" 16',
+    'Sampler "stratified" "integer xsamples" 4 "integer ysamples" 4',
+    'Sampler "sobol" "integer pixelsamples" 16',
+    'Sampler "sobol" "integer pixelsamples" 16 "string randomization" "owen"',
+    'Sampler "paddedsobol" "integer pixelsamples" 16 "string randomization" "permutedigits"',
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("line", SAMPLERS_GPU, ids=["independent", "stratified", "sobol", "sobol-owen", "paddedsobol"])
+def test_cornell_samplers_match_oracle_gpu(pa, oracle, line):
+    """GenerateRaySamples<Sampler> for every sampler the factory makes (samples.cpp:29-66,
+    samplers.cpp:416-432): the Cornell film on the GPU against the oracle at test_gpu_parity's bar."""
+    from test_gpu_parity import check_parity, gpu_film, oracle_film, to_rgb
+    sc = cornell_with_sampler(pa, line, xresolution=128, yresolution=96)
+    film, integ = gpu_film(pa, sc)
+    frac, mean_rel = check_parity(to_rgb(oracle, sc, film), to_rgb(oracle, sc, oracle_film(oracle, sc, integ)))
+    print(f"{line}: {frac*100:.3f}% pixels within 1e-3, mean rel {mean_rel:.2e}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["independent", "sobol"])
+def test_media_samplers_match_oracle_gpu(pa, oracle, name):
+    """The volumetric kernels' ray samples (RaySamplesAt) with a stateful and a table sampler:
+    a homogeneous medium box against the oracle in its CR mode (test_gpu_media)."""
+    from test_gpu_media import HOMOG, check, gpu_rgb, oracle_rgb
+    from test_media import medium_scene
+    text = medium_scene(HOMOG, res=48, spp=16, maxdepth=4, sky="0.3 0.4 0.5", fov=35, sampler=name)
+    sc = pa.Scene.from_string(text, SCENES)
+    assert sc.flat().sampler_type == (2 if name == "independent" else 4)
+    a, _ = gpu_rgb(pa, oracle, sc)
+    frac, mr = check(a, oracle_rgb(oracle, sc))
+    print(f"media {name}: {frac*100:.3f}% pixels within 1e-3, mean rel {mr:.2e}")
+
+
+@pytest.mark.parametrize("line", [
+    'Sampler "independent" "integer pixelsamples" 64',
+    'Sampler "stratified" "integer xsamples" 8 "integer ysamples" 8',
+    'Sampler "sobol" "integer pixelsamples" 64',
+    'Sampler "paddedsobol" "integer pixelsamples" 64 "string randomization" "owen"',
+], ids=["independent", "stratified", "sobol", "paddedsobol"])
+def test_furnace_known_answer_each_sampler(pa, oracle, line):
+    """The furnace (emissive sphere of L = 0.5 around a 0.5-albedo diffuse one: radiance 1,
+    RenderTest.RadianceMatches' 1 +- 0.025, cpu/integrators_test.cpp:51-64) through the oracle
+    with every other sampler: each is an unbiased estimator of the same image.  32 x 32 pixels:
+    the SobolSampler's points are one global sequence over the RoundUpPow2(resolution) grid, and on
+    the scene's own 10 x 10 film its per-pixel subsets converge slowly (mean 1.075 at 64 spp)."""
+    text = (SCENES / "furnace.pbrt").read_text()
+    text = "\n".join(line if ln.startswith("Sampler ") else ln for ln in text.splitlines()) + "\n"
+    sc = pa.Scene.from_string(text, SCENES, xresolution=32, yresolution=32)
+    f = sc.flat()
+    img = oracle.film_to_rgb(oracle.render(sc, threads=8), [f.output_rgb_from_sensor_rgb[i] for i in range(9)])
+    assert abs(img.mean() - 1.0) < 0.025, img.mean()

@@ -256,9 +256,6 @@ typedef struct pbrt_render_stats {
      * launch" term): node bytes in the format traversed, less the top nodes cached in LDS,
      * and triangle bytes (0 when every triangle is cached in LDS) */
     uint64_t bvh_hbm_node_bytes, bvh_hbm_tri_bytes;
-    /* 1: the surface kernels ran from the correctly rounded build (scenes with alpha-tested
-     * shapes or mix materials, or PBRT_AMD_CR_MATH=1); compare with the oracle's CR mode */
-    int cr_math;
 } pbrt_render_stats;
 
 /* Per-stage kernel profile (GetProfilerEvents / ReportKernelStats, gpu/util.cpp:128-246): with
@@ -392,6 +389,11 @@ int pbrt_debug_zsobol(const pbrt_scene *scene, int px, int py, int sample_index,
  * camera's Get1D, GetPixel2D, Get1D, Get2D, Get1D, otherwise Get1D, Get2D, Get1D, Get2D, Get1D
  * -> 7 values.  Fails for halton / zsobol scenes (pbrt_debug_halton / pbrt_debug_zsobol). */
 int pbrt_debug_sampler(const pbrt_scene *scene, int px, int py, int sample_index, int dim, float *out7);
+/* The kernels' portable transcendentals (core/detmath.h) on n inputs: fn 0 sin, 1 cos, 2 asin, 3
+ * acos (inputs clamped to [-1, 1] as SafeASin / SafeACos), 4 atan2(a, b), 5 log, 6 / 7 the sin /
+ * cos of SinCosf; on GPU `device`, or compiled for the host when device < 0 (the two must agree
+ * bit for bit, and the oracle's device-math mode with both) */
+int pbrt_debug_det_math(int device, int fn, const float *a, const float *b, int n, float *out);
 /* RNG::SetSequence(seq); RNG::Advance(advance); two Uniform<uint32_t>() (util/rng.h:119-150) */
 int pbrt_debug_rng(uint64_t seq, uint64_t advance, uint32_t *out2);
 /* util/scattering.h components as the product evaluates them (core.h), host side.

@@ -50,6 +50,9 @@ def lib():
                                        ctypes.c_int, vp]
         _lib.oracle_render_path.restype = ctypes.c_int
         _lib.oracle_set_cr_math.argtypes = [ctypes.c_int]
+        _lib.oracle_set_math_mode.argtypes = [ctypes.c_int]
+        _lib.oracle_get_math_mode.restype = ctypes.c_int
+        _lib.oracle_math_eval.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
         _lib.oracle_light_bvh.argtypes = [vp, vp, ctypes.c_int, vp, vp, vp, ctypes.c_int]
         _lib.oracle_intersect_tr.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int, vp]
         _lib.oracle_set_rgb_table.argtypes = [vp, vp]
@@ -170,17 +173,39 @@ def image_level(scene, image, level):
     return buf, w.value, h.value
 
 
-class cr_math:
-    """Context manager: the oracle evaluates transcendentals correctly rounded (as the device
-    media kernels do) inside the block, libm float (as the reference) outside it."""
+MATH_LIBM, MATH_CR, MATH_DEVICE = 0, 1, 2
+
+
+class math_mode:
+    """Context manager: the oracle's transcendentals inside the block -- MATH_LIBM (its default:
+    libm float, as pbrt's CPU build), MATH_DEVICE (the device kernels' portable polynomials,
+    core/detmath.h, bit for bit: what GPU parity compares against) or MATH_CR (correctly rounded)."""
+
+    def __init__(self, mode):
+        self.mode = mode
 
     def __enter__(self):
-        lib().oracle_set_cr_math(1)
+        self.prev = lib().oracle_get_math_mode()
+        lib().oracle_set_math_mode(self.mode)
         return self
 
     def __exit__(self, *exc):
-        lib().oracle_set_cr_math(0)
+        lib().oracle_set_math_mode(self.prev)
         return False
+
+
+def set_math_mode(mode):
+    lib().oracle_set_math_mode(mode)
+
+
+def math_eval(fn, a, b=None):
+    """The oracle's transcendental `fn` (sin cos asin acos atan2 log) in its current mode."""
+    names = ["sin", "cos", "asin", "acos", "atan2", "log"]
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b if b is not None else np.zeros_like(a), np.float32)
+    out = np.zeros_like(a)
+    lib().oracle_math_eval(names.index(fn), a.ctypes.data, b.ctypes.data, len(a), out.ctypes.data)
+    return out
 
 
 def f32(a):

@@ -9,7 +9,6 @@
 #include <memory>
 #include <sstream>
 #include <string>
-#include <utility>
 #include <vector>
 
 #include "../../include/pbrt_amd.h"
@@ -20,57 +19,27 @@
 #include "kernels/device.h"
 
 namespace pbrt_amd {
-// kernels/wavefront.hip, built twice: wf (device transcendentals) and wfcr (correctly rounded)
-#define PBRT_WF_LAUNCHERS                                                                                      \
-    hipError_t LaunchCamera(const DeviceScene &S, const PathState &st, int nActive, hipStream_t s);             \
-    hipError_t LaunchClosest(const DeviceScene &S, const PathState &st, int depth, int maxCount, int timed,     \
-                             hipStream_t s, bool sorted);                                                      \
-    hipError_t LaunchRayBin(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s); \
-    hipError_t LaunchClassify(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s); \
-    hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int depth, int maxCount, bool lean, \
-                                  hipStream_t s);                                                              \
-    hipError_t LaunchTexture(const DeviceScene &S, const PathState &st, int depth, int type, bool full,         \
-                             int maxCount, hipStream_t s);                                                     \
-    hipError_t LaunchShadeMicrofacet(const DeviceScene &S, const PathState &st, int depth, int type,            \
-                                     int maxCount, hipStream_t s);                                             \
-    hipError_t LaunchEscaped(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s); \
-    hipError_t LaunchEmissive(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s); \
-    hipError_t LaunchShadow(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s); \
-    hipError_t LaunchFilm(const DeviceScene &S, const PathState &st, int nSamples, hipStream_t s);              \
-    hipError_t LaunchIntersectBatch(const DeviceScene &S, const float *rays, int n, int anyHit, int *outPrim,  \
-                                    float *outHit, hipStream_t s);
-namespace wf {
-PBRT_WF_LAUNCHERS
+hipError_t LaunchCamera(const DeviceScene &S, const PathState &st, int nActive, hipStream_t s);
+hipError_t LaunchClosest(const DeviceScene &S, const PathState &st, int depth, int maxCount, int timed,
+                         hipStream_t s, bool sorted);
+hipError_t LaunchRayBin(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
+hipError_t LaunchClassify(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
+hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int depth, int maxCount, bool lean,
+                              hipStream_t s);
+hipError_t LaunchTexture(const DeviceScene &S, const PathState &st, int depth, int type, bool full, int maxCount,
+                         hipStream_t s);
+hipError_t LaunchShadeMicrofacet(const DeviceScene &S, const PathState &st, int depth, int type, int maxCount,
+                                 hipStream_t s);
+hipError_t LaunchEscaped(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
+hipError_t LaunchEmissive(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
+hipError_t LaunchShadow(const DeviceScene &S, const PathState &st, int depth, int maxCount, hipStream_t s);
+hipError_t LaunchFilm(const DeviceScene &S, const PathState &st, int nSamples, hipStream_t s);
 hipError_t LaunchCheckRNMath(uint64_t seed, int blocks, int perThread, unsigned long long *bad, hipStream_t s);
+hipError_t LaunchDetMath(int fn, const float *a, const float *b, int n, float *out, hipStream_t s);
+hipError_t LaunchIntersectBatch(const DeviceScene &S, const float *rays, int n, int anyHit, int *outPrim,
+                                float *outHit, hipStream_t s);
 size_t SurfaceTraversalStaticLds(int tm);
 int TraversalBlocksCompiled(int compressed);
-}  // namespace wf
-namespace wfcr {
-PBRT_WF_LAUNCHERS
-}  // namespace wfcr
-#undef PBRT_WF_LAUNCHERS
-// Every surface-wavefront launch goes to the build the scene selected (DeviceScene::crMath)
-#define PBRT_WF_DISPATCH(name)                                                                   \
-    template <class... A>                                                                        \
-    static hipError_t name(const DeviceScene &S, A &&...a) {                                     \
-        return S.crMath ? wfcr::name(S, std::forward<A>(a)...) : wf::name(S, std::forward<A>(a)...); \
-    }
-PBRT_WF_DISPATCH(LaunchCamera)
-PBRT_WF_DISPATCH(LaunchClosest)
-PBRT_WF_DISPATCH(LaunchRayBin)
-PBRT_WF_DISPATCH(LaunchClassify)
-PBRT_WF_DISPATCH(LaunchShadeDiffuse)
-PBRT_WF_DISPATCH(LaunchTexture)
-PBRT_WF_DISPATCH(LaunchShadeMicrofacet)
-PBRT_WF_DISPATCH(LaunchEscaped)
-PBRT_WF_DISPATCH(LaunchEmissive)
-PBRT_WF_DISPATCH(LaunchShadow)
-PBRT_WF_DISPATCH(LaunchFilm)
-PBRT_WF_DISPATCH(LaunchIntersectBatch)
-#undef PBRT_WF_DISPATCH
-using wf::LaunchCheckRNMath;
-using wf::SurfaceTraversalStaticLds;
-using wf::TraversalBlocksCompiled;
 hipError_t LaunchVolCamera(const DeviceScene &S, const PathState &st, const VolState &v, int nActive, hipStream_t s);
 hipError_t LaunchVolClosest(const DeviceScene &S, const PathState &st, const VolState &v, int wf, int maxCount,
                             int timed, hipStream_t s);
@@ -1065,13 +1034,6 @@ static void BuildDevice(pbrt_context *c) {
         }
         c->matMix.Upload(mm);
         S.matMix = (const int4 *)c->matMix.p;
-        // Scenes whose paths hash ray bits (alpha tests: HashFloat(ray o, d), gpu/optix.cu:197-243;
-        // mix: HashFloat(p, wo, ...), materials.h:285-294) take the correctly rounded build of the
-        // surface kernels (wavefront.hip, namespace wfcr): a last-ulp difference in a device
-        // transcendental would otherwise flip a decision the oracle makes (its CR mode matches).
-        // PBRT_AMD_CR_MATH=0/1 forces either build.
-        S.crMath = (S.nAlpha > 0 || c->hasMix) ? 1 : 0;
-        if (const char *e = getenv("PBRT_AMD_CR_MATH")) S.crMath = atoi(e) ? 1 : 0;
         // textured: some material evaluates a program (the textured shade / texture kernels);
         // the alpha tests of the traversal kernels may need the tables on their own
         {
@@ -2049,7 +2011,6 @@ int pbrt_synchronize(pbrt_context *ctx) {
             const uint64_t nNodes = S.compressed ? ctx->qnodes.n : ctx->nodes.n;
             ctx->stats.bvh_hbm_node_bytes = nNodes > (uint64_t)S.ldsNodes ? (nNodes - S.ldsNodes) * nodeB : 0;
             ctx->stats.bvh_hbm_tri_bytes = S.ldsTris > 0 ? 0 : (uint64_t)ctx->triVerts.n * sizeof(float);
-            ctx->stats.cr_math = S.crMath;
         }
         return 0;
     } catch (const std::exception &e) {
@@ -2586,6 +2547,40 @@ int pbrt_debug_sampler(const pbrt_scene *scene, int px, int py, int sampleIndex,
         out7[3] = g.Get1D(d);
         g.Get2D(d, &out7[4], &out7[5]);
         out7[6] = g.Get1D(d);
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_debug_det_math(int device, int fn, const float *a, const float *b, int n, float *out) {
+    try {
+        if (!a || !b || !out || n < 0 || fn < 0 || fn > 7) return Fail("pbrt_debug_det_math: bad arguments");
+        if (device < 0) {  // the same code compiled for the host
+            for (int i = 0; i < n; ++i) {
+                float s, c;
+                switch (fn) {
+                case 0: out[i] = detm::Sin(a[i]); break;
+                case 1: out[i] = detm::Cos(a[i]); break;
+                case 2: out[i] = detm::ASin(std::fmin(std::fmax(a[i], -1.f), 1.f)); break;
+                case 3: out[i] = detm::ACos(std::fmin(std::fmax(a[i], -1.f), 1.f)); break;
+                case 4: out[i] = detm::ATan2(a[i], b[i]); break;
+                case 5: out[i] = detm::Log(a[i]); break;
+                case 6: detm::SinCos(a[i], &s, &c); out[i] = s; break;
+                default: detm::SinCos(a[i], &s, &c); out[i] = c; break;
+                }
+            }
+            return 0;
+        }
+        HIPCHECK(hipSetDevice(device));
+        DevBuf<float> da, db, dout;
+        da.Upload(std::vector<float>(a, a + n));
+        db.Upload(std::vector<float>(b, b + n));
+        dout.Alloc(n);
+        if (n > 0) {
+            HIPCHECK(LaunchDetMath(fn, da.p, db.p, n, dout.p, nullptr));
+            HIPCHECK(hipMemcpy(out, dout.p, (size_t)n * sizeof(float), hipMemcpyDeviceToHost));
+        }
         return 0;
     } catch (const std::exception &e) {
         return Fail(e.what());

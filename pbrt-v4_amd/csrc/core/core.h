@@ -29,6 +29,8 @@
 #define PHD_SPH inline
 #endif
 
+#include "detmath.h"  // after PHD: the device transcendentals
+
 namespace pbrt_amd {
 
 constexpr float kPi = 3.14159265358979323846f;
@@ -73,36 +75,28 @@ PHD float NextFloatDown(float v) {
 // util/float.h:197 gamma(n)
 PHD constexpr float gamma(int n) { return (n * kMachineEpsilon) / (1 - n * kMachineEpsilon); }
 
-// Transcendentals.  Host code calls libm's float functions, as the reference CPU build does.
-// The participating-media kernels (volpath.hip defines PBRT_AMD_CR_MATH) take the correctly
-// rounded float result (evaluated in double, rounded once), which the CPU oracle reproduces in
-// its CR mode (oracle_set_cr_math): a medium path's RNG is seeded from the bits of its ray
-// (RNG(Hash(ray.o, tMax), Hash(ray.d)), wavefront/media.cpp:44), so an ulp anywhere upstream
-// would decorrelate the device from the oracle.  The surface-only kernels (wavefront.hip) use
-// the device's own float functions: there an ulp never reseeds anything.
-#if defined(__HIP_DEVICE_COMPILE__) && defined(PBRT_AMD_CR_MATH)
-PHD float Sinf(float x) { return (float)std::sin((double)x); }
-PHD float Cosf(float x) { return (float)std::cos((double)x); }
-PHD void SinCosf(float x, float *s, float *c) {
-    *s = Sinf(x);
-    *c = Cosf(x);
-}
-PHD float ASinf(float x) { return (float)std::asin((double)x); }
-PHD float ACosf(float x) { return (float)std::acos((double)x); }
-PHD float ATan2f(float y, float x) { return (float)std::atan2((double)y, (double)x); }
-PHD float Logf(float x) { return (float)std::log((double)x); }
+// Transcendentals.  Host code calls libm's float functions, as the reference CPU build does (the
+// host-side tables and debug entries are pinned bit for bit against the reference's goldens).
+// Device code evaluates the portable polynomials of detmath.h, built from IEEE operations only,
+// so a host restatement reproduces every device result bit for bit: the CPU oracle's device-math
+// mode (oracle_set_math_mode(2), which the GPU parity tests select) does, and the GPU path makes every decision
+// the oracle makes -- the medium RNG seeded from a ray's bits (wavefront/media.cpp:44), alpha
+// tests hashing the ray (gpu/optix.cu:197-243), mix choices hashing the hit (materials.h:285-294).
+#if defined(__HIP_DEVICE_COMPILE__)
+PHD float Sinf(float x) { return detm::Sin(x); }
+PHD float Cosf(float x) { return detm::Cos(x); }
+// sin and cos of one angle: one shared argument reduction, the same values as the two calls
+PHD void SinCosf(float x, float *s, float *c) { detm::SinCos(x, s, c); }
+PHD float ASinf(float x) { return detm::ASin(x); }
+PHD float ACosf(float x) { return detm::ACos(x); }
+PHD float ATan2f(float y, float x) { return detm::ATan2(y, x); }
+PHD float Logf(float x) { return detm::Log(x); }
 #else
 PHD float Sinf(float x) { return std::sin(x); }
 PHD float Cosf(float x) { return std::cos(x); }
-// sin and cos of one angle: on the device one shared argument reduction (ocml sincos), the same
-// values as the two separate calls (checked bitwise on the GPU, tests/test_gpu_rn_math.py)
 PHD void SinCosf(float x, float *s, float *c) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    sincosf(x, s, c);
-#else
     *s = std::sin(x);
     *c = std::cos(x);
-#endif
 }
 PHD float ASinf(float x) { return std::asin(x); }
 PHD float ACosf(float x) { return std::acos(x); }

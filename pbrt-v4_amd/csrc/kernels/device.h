@@ -254,8 +254,6 @@ struct DeviceScene {
     // this struct's copy in device memory (static scene fields only): out-of-line functions
     // that need many scene tables take it, so no kernel copies its DeviceScene into scratch
     const DeviceScene *self;
-    // the surface kernels run from the correctly rounded build (wavefront.hip, namespace wfcr)
-    int crMath;
 };
 
 // One depth's path records, compacted: record i is the i-th ray of that depth (pbrt's

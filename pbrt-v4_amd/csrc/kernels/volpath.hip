@@ -25,9 +25,6 @@
 #ifndef PBRT_VOL_EXPERIMENT
 #define PBRT_VOL_EXPERIMENT 0  // timing experiments only (tools/exp_*.sh), never in the product
 #endif
-#if PBRT_VOL_EXPERIMENT != 3
-#define PBRT_AMD_CR_MATH 1  // correctly rounded transcendentals (core.h): bit-identical to the oracle
-#endif
 #include "common.h"
 
 namespace pbrt_amd {

@@ -15,27 +15,13 @@
 // device-side queue counters so the host never synchronises inside the render loop.
 #include "common.h"
 
-// This file is compiled twice (Makefile): once with the device's own transcendentals into
-// namespace pbrt_amd::wf, and once with PBRT_AMD_CR_MATH (correctly rounded, core.h) into
-// pbrt_amd::wfcr.  capi.hip picks the build per scene (DeviceScene::crMath): scenes whose paths
-// hash ray bits (alpha-tested shapes, mix materials) take the CR build, so every decision they
-// make equals the oracle's in its CR mode.
-#ifndef PBRT_WF_NS
-#define PBRT_WF_NS wf
-#endif
-
 namespace pbrt_amd {
-#if !defined(PBRT_AMD_CR_MATH)
-// Traversal LDS of one block (shared with volpath.hip; defined once, in the default build):
-// group stack (uint2 entries), cached nodes, cached triangles in three pre-rotated copies
+// Traversal LDS of one block (shared with volpath.hip): group stack (uint2 entries), cached
+// nodes, cached triangles in three pre-rotated copies
 size_t TraversalLdsBytes(int stackSize, int ldsNodes, int ldsTris, int compressed) {
     return (size_t)stackSize * kBlock * sizeof(uint2) + (size_t)ldsNodes * LdsNodeStride(compressed) * 16 +
            (size_t)ldsTris * 3 * 48;
 }
-#else
-size_t TraversalLdsBytes(int stackSize, int ldsNodes, int ldsTris, int compressed);
-#endif
-namespace PBRT_WF_NS {
 
 // The sensor's x/y/z-bar table as the shade kernels read it (staged in LDS; reading it through
 // the L1 instead, to fit four blocks per CU, measured 5 % slower: profiles/r02_shade_ablation.txt)
@@ -1619,6 +1605,29 @@ __global__ void k_check_rn_math(uint64_t seed, int perThread, unsigned long long
     }
     atomicAdd(&bad[0], ns);
 }
+// the device's portable transcendentals (core/detmath.h) on given inputs: fn 0 sin, 1 cos, 2 asin,
+// 3 acos, 4 atan2(a, b), 5 log, 6 sin of SinCosf, 7 cos of SinCosf
+__device__ inline float DetMathEval(int fn, float a, float b) {
+    float s, c;
+    switch (fn) {
+    case 0: return Sinf(a);
+    case 1: return Cosf(a);
+    case 2: return SafeASin(a);
+    case 3: return SafeACos(a);
+    case 4: return ATan2f(a, b);
+    case 5: return Logf(a);
+    case 6: SinCosf(a, &s, &c); return s;
+    default: SinCosf(a, &s, &c); return c;
+    }
+}
+__global__ void k_det_math(int fn, const float *a, const float *b, int n, float *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = DetMathEval(fn, a[i], b[i]);
+}
+hipError_t LaunchDetMath(int fn, const float *a, const float *b, int n, float *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_det_math, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, fn, a, b, n, out);
+    return hipGetLastError();
+}
 hipError_t LaunchCheckRNMath(uint64_t seed, int blocks, int perThread, unsigned long long *bad, hipStream_t s) {
     hipLaunchKernelGGL(k_check_rn_math, dim3(blocks), dim3(kBlock), 0, s, seed, perThread, bad);
     return hipGetLastError();
@@ -1800,5 +1809,4 @@ hipError_t LaunchIntersectBatch(const DeviceScene &S, const float *rays, int n, 
     return hipGetLastError();
 }
 
-}  // namespace PBRT_WF_NS
 }  // namespace pbrt_amd

@@ -118,8 +118,7 @@ class RenderStats(ctypes.Structure):
                 ("shadow_rays", ctypes.c_uint64), ("closest_launches", ctypes.c_int),
                 ("closest_ms", ctypes.c_double), ("timed_closest_rays", ctypes.c_uint64), ("passes", ctypes.c_int),
                 ("paths_per_pass", ctypes.c_uint64), ("bvh_hbm_node_bytes", ctypes.c_uint64),
-                ("bvh_hbm_tri_bytes", ctypes.c_uint64),
-                ("cr_math", ctypes.c_int)]
+                ("bvh_hbm_tri_bytes", ctypes.c_uint64)]
 
 
 class KernelStat(ctypes.Structure):
@@ -134,7 +133,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_context_free", "pbrt_render", "pbrt_synchronize", "pbrt_get_stats", "pbrt_reset_stats",
     "pbrt_film_clear", "pbrt_film_device_ptr", "pbrt_film_read", "pbrt_film_get_rgb", "pbrt_intersect",
     "pbrt_debug_halton", "pbrt_debug_halton_fastpath_mismatches", "pbrt_debug_check_rn_math", "pbrt_debug_rgb_coeffs", "pbrt_debug_rgb2spec_column", "pbrt_debug_kernel_sections",
-    "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_sampler", "pbrt_debug_rng", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
+    "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_sampler", "pbrt_debug_rng", "pbrt_debug_det_math", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
     "pbrt_debug_named_spectrum", "pbrt_debug_bxdf", "pbrt_debug_layered", "pbrt_debug_triangle_shading", "pbrt_film_write_image",
     "pbrt_image_read_size", "pbrt_image_read", "pbrt_image_write", "pbrt_image_error", "pbrt_debug_filter_sample",
     "pbrt_debug_bvh_stats", "pbrt_debug_light_bvh", "pbrt_intersect_tr", "pbrt_image_flip", "pbrt_set_kernel_profiling", "pbrt_get_kernel_stats",
@@ -208,6 +207,7 @@ def _lib():
     lib.pbrt_debug_zsobol.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_int, c.POINTER(c.c_float)]
     lib.pbrt_debug_sampler.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_int, c.POINTER(c.c_float)]
     lib.pbrt_debug_rng.argtypes = [c.c_uint64, c.c_uint64, c.POINTER(c.c_uint32)]
+    lib.pbrt_debug_det_math.argtypes = [c.c_int, c.c_int, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_debug_queue_counts.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_int]
     lib.pbrt_debug_trowbridge.argtypes = [c.c_void_p, c.c_void_p]
     lib.pbrt_debug_fresnel.argtypes = [c.c_void_p, c.c_void_p]
@@ -465,6 +465,20 @@ def debug_rng(seq, advance):
     return int(out[0]), int(out[1])
 
 
+DET_MATH_FNS = ["sin", "cos", "asin", "acos", "atan2", "log", "sincos_sin", "sincos_cos"]
+
+
+def det_math(fn, a, b=None, device=-1):
+    """The kernels' portable transcendental `fn` (DET_MATH_FNS) on a (and b for atan2), run on GPU
+    `device` or compiled for the host (device < 0): pbrt_debug_det_math."""
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b if b is not None else np.zeros_like(a), np.float32)
+    out = np.zeros_like(a)
+    _check(_lib().pbrt_debug_det_math(device, DET_MATH_FNS.index(fn), a.ctypes.data, b.ctypes.data, len(a),
+                                      out.ctypes.data))
+    return out
+
+
 def device_count() -> int:
     n = ctypes.c_int(0)
     _lib().pbrt_device_count(ctypes.byref(n))
@@ -507,13 +521,6 @@ class WavefrontPathIntegrator:
         s = RenderStats()
         _check(_lib().pbrt_get_stats(self._h, ctypes.byref(s)))
         return s
-
-    @property
-    def cr_math(self) -> bool:
-        """True when the surface kernels ran from the correctly rounded build (scenes with
-        alpha-tested shapes or mix materials; valid after synchronize()): the oracle's CR mode
-        is then the one to compare with."""
-        return bool(self.stats().cr_math)
 
     def reset_stats(self):
         _check(_lib().pbrt_reset_stats(self._h))

@@ -35,6 +35,17 @@ def oracle():
     return pyoracle
 
 
+@pytest.fixture(autouse=True)
+def _oracle_math_mode(request):
+    """GPU parity tests compare against the oracle in its device-math mode (the kernels' portable
+    transcendentals, core/detmath.h, reproduced bit for bit); every other test sees its libm mode,
+    in which the component tests pin it to the reference's goldens."""
+    import pyoracle
+    pyoracle.set_math_mode(pyoracle.MATH_DEVICE if request.node.get_closest_marker("gpu") else pyoracle.MATH_LIBM)
+    yield
+    pyoracle.set_math_mode(pyoracle.MATH_LIBM)
+
+
 def fl(v):
     """golden JSON floats ('inf'/'nan' strings) -> float"""
     if isinstance(v, list):

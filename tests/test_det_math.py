@@ -1,0 +1,95 @@
+"""The kernels' portable transcendentals (pbrt-v4_amd/csrc/core/detmath.h): sin, cos, asin, acos,
+atan2 and log from IEEE operations only, so the GPU, the host and the CPU oracle's device-math mode
+compute the same bits.  This is what lets every GPU parity test hold the oracle's per-sample
+decisions (medium RNG seeded from a ray, wavefront/media.cpp:44; alpha tests hashing the ray,
+gpu/optix.cu:197-243; mix choices hashing the hit, materials.h:285-294).
+
+* accuracy: within 3 ulp of the correctly rounded value (pbrt's CPU build uses libm, its GPU build
+  CUDA's sinf etc., both an ulp or two from correctly rounded in the same way);
+* host product == oracle device-math mode, bit for bit (CPU);
+* GPU == host, bit for bit (gpu).
+"""
+import numpy as np
+import pytest
+
+FNS = ["sin", "cos", "asin", "acos", "atan2", "log"]
+
+
+def inputs(fn, n=400000, seed=7):
+    rng = np.random.default_rng(seed)
+    if fn in ("sin", "cos", "sincos_sin", "sincos_cos"):
+        a = np.concatenate([rng.uniform(-7, 7, n // 2), rng.uniform(-1e4, 1e4, n // 4), rng.uniform(-1e-3, 1e-3, n // 8),
+                            rng.uniform(-1e6, 1e6, n // 8), [0.0, -0.0, 1e-30, np.pi, -np.pi / 2, 8192.0, 8193.0]])
+        b = np.zeros_like(a)
+    elif fn in ("asin", "acos"):
+        a = np.concatenate([rng.uniform(-1, 1, n // 2), 1 - np.ldexp(rng.uniform(0, 1, n // 4), -rng.integers(1, 24, n // 4)),
+                            -1 + np.ldexp(rng.uniform(0, 1, n // 4), -rng.integers(1, 24, n // 4)), [0.0, -0.0, 0.5, -0.5, 1, -1]])
+        b = np.zeros_like(a)
+    elif fn == "atan2":
+        a = np.concatenate([rng.uniform(-5, 5, n // 2), rng.uniform(-1e-5, 1e-5, n // 4), rng.normal(size=n // 4),
+                            [0.0, -0.0, 0.0, -0.0, 1.0, -1.0, np.inf, -np.inf]])
+        b = np.concatenate([rng.uniform(-5, 5, n // 2), rng.normal(size=n // 4), rng.uniform(-1e-5, 1e-5, n // 4),
+                            [1.0, 1.0, -1.0, -1.0, 0.0, -0.0, np.inf, -np.inf]])
+    else:  # log
+        a = np.concatenate([np.exp(rng.uniform(-87, 88, n // 2)), rng.uniform(0.5, 2, n // 4), rng.uniform(0, 1, n // 4),
+                            [1.0, 2.0, 0.5, 1e-40, 1e-45, 3e38]])
+        b = np.zeros_like(a)
+    return a.astype(np.float32), b.astype(np.float32)
+
+
+def ulp_error(got, ref64):
+    r32 = ref64.astype(np.float32)
+    ulp = np.spacing(np.abs(r32)).astype(np.float64)
+    ulp[ulp == 0] = np.spacing(np.float32(0))
+    return np.abs(got.astype(np.float64) - ref64) / ulp
+
+
+REF64 = {"sin": np.sin, "cos": np.cos, "asin": lambda a: np.arcsin(np.clip(a, -1, 1)),
+         "acos": lambda a: np.arccos(np.clip(a, -1, 1)), "log": np.log}
+
+
+@pytest.mark.parametrize("fn", FNS)
+def test_det_math_accuracy(pa, fn):
+    a, b = inputs(fn)
+    got = pa.det_math(fn, a, b)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        ref = np.arctan2(a.astype(np.float64), b.astype(np.float64)) if fn == "atan2" else REF64[fn](a.astype(np.float64))
+    fin = np.isfinite(ref)
+    assert np.array_equal(np.isfinite(got), fin)
+    err = ulp_error(got[fin], ref[fin])
+    print(f"{fn}: max {err.max():.3f} ulp, mean {err.mean():.4f}, {np.mean(err > 0.5) * 100:.1f}% not correctly rounded")
+    assert err.max() <= 3.0, (fn, err.max(), a[fin][np.argmax(err)])
+
+
+def test_det_math_special_values(pa):
+    z = np.float32
+    assert np.signbit(pa.det_math("sin", [-0.0])[0]) and pa.det_math("cos", [-0.0])[0] == 1
+    at = pa.det_math("atan2", [0.0, -0.0, 0.0, -0.0, 1.0, -1.0], [1.0, 1.0, -1.0, -1.0, 0.0, 0.0])
+    np.testing.assert_array_equal(at, np.arctan2(z([0.0, -0.0, 0.0, -0.0, 1.0, -1.0]), z([1.0, 1.0, -1.0, -1.0, 0.0, 0.0])))
+    assert np.signbit(at[1]) and not np.signbit(at[0])
+    lg = pa.det_math("log", [0.0, 1.0, np.inf, -1.0])
+    assert lg[0] == -np.inf and lg[1] == 0 and lg[2] == np.inf and np.isnan(lg[3])
+    assert np.isnan(pa.det_math("sin", [np.inf, np.nan])).all()
+
+
+@pytest.mark.parametrize("fn", FNS)
+def test_det_math_oracle_device_mode_bitwise(pa, oracle, fn):
+    """The oracle's device-math mode restates detmath.h: the same bits as the product's code."""
+    a, b = inputs(fn, seed=11)
+    got = pa.det_math(fn, a, b)
+    with oracle.math_mode(oracle.MATH_DEVICE):
+        ref = oracle.math_eval(fn, a, b)
+    np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fn", FNS + ["sincos_sin", "sincos_cos"])
+def test_det_math_gpu_equals_host_bitwise(pa, fn):
+    """The same source compiled for gfx950 and for the host gives the same bits on every input
+    (IEEE operations only; -ffp-contract=off), including SinCosf against the separate calls."""
+    a, b = inputs(fn, n=1 << 20, seed=13)
+    dev = pa.det_math(fn, a, b, device=0)
+    host = pa.det_math(fn, a, b)
+    np.testing.assert_array_equal(dev.view(np.uint32), host.view(np.uint32))
+    if fn.startswith("sincos_"):
+        np.testing.assert_array_equal(dev.view(np.uint32), pa.det_math(fn[7:], a, b, device=0).view(np.uint32))

@@ -3,8 +3,10 @@ scene, sampler and seed.
 
 Tolerance (north star: "per-channel float tolerance"): per-pixel output RGB
 within 1e-3 relative (abs floor 1e-4) on >= 99.5 % of pixels, image mean within 1e-4
-relative.  The remaining pixels are paths that diverge after a last-ulp difference in a
-transcendental (device ocml vs host libm sin/cos/asin/atan2) flips an RR or hit decision.
+relative.  The device's transcendentals are portable polynomials (core/detmath.h) that the
+oracle restates in its default math mode, so paths follow the oracle's decisions; what remains
+are exact-t closest-hit ties resolved in a different BVH order and film-only reciprocal
+roundings (DESIGN.md, Numerics).
 Integer results (closest-hit primitive ids) must match exactly except documented
 exact-t ties."""
 import numpy as np
@@ -29,14 +31,11 @@ def to_rgb(oracle, sc, film):
     return oracle.film_to_rgb(film, [f.output_rgb_from_sensor_rgb[i] for i in range(9)])
 
 
-def oracle_film(oracle, sc, integ, **kw):
-    """The oracle's film in the arithmetic mode the product's context ran: its correctly rounded
-    mode when the surface kernels came from the CR build (alpha-tested shapes, mix materials:
-    capi.hip DeviceScene::crMath), its libm mode otherwise."""
+def oracle_film(oracle, sc, integ=None, **kw):
+    """The oracle's film of the scene.  GPU tests run the oracle in its device-math mode (the
+    kernels' portable transcendentals, core/detmath.h; conftest), so every path decision -- alpha
+    tests and mix choices that hash a ray, the medium RNG seeded from one -- is the device's."""
     kw.setdefault("threads", 16)
-    if integ.cr_math:
-        with oracle.cr_math():
-            return oracle.render(sc, **kw)
     return oracle.render(sc, **kw)
 
 

@@ -159,7 +159,7 @@ def test_cornell_samplers_match_oracle_gpu(pa, oracle, line):
 @pytest.mark.parametrize("name", ["independent", "sobol"])
 def test_media_samplers_match_oracle_gpu(pa, oracle, name):
     """The volumetric kernels' ray samples (RaySamplesAt) with a stateful and a table sampler:
-    a homogeneous medium box against the oracle in its CR mode (test_gpu_media)."""
+    a homogeneous medium box against the oracle (test_gpu_media)."""
     from test_gpu_media import HOMOG, check, gpu_rgb, oracle_rgb
     from test_media import medium_scene
     text = medium_scene(HOMOG, res=48, spp=16, maxdepth=4, sky="0.3 0.4 0.5", fov=35, sampler=name)

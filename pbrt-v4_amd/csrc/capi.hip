@@ -1058,10 +1058,8 @@ static void BuildDevice(pbrt_context *c) {
         S.tex = TexView{};
         if (!s.texPrograms.empty() || S.hasBump) {
             // textures on the volumetric path: k_vtexture + k_vsurface<..., Tex> (diffuse,
-            // dielectric, conductor); mix materials and bump on layered ones stay surface-only
-            if (c->volumetric && c->hasMix)
-                throw Error("mix materials together with the volumetric path (media, interface, layered, thin "
-                            "dielectric, diffuse transmission or dispersive materials) are not supported yet");
+            // dielectric, conductor); mix materials resolve in k_vclosest<TM, true>; bump on
+            // layered materials stays surface-only
             if (c->volumetric)
                 for (const MaterialDesc &m : s.materials)
                     if ((m.texDisp >= 0 || m.normalMap >= 0) &&

@@ -615,12 +615,19 @@ __global__ void __launch_bounds__(kBlock) k_vcamera(DeviceScene S, PathState st,
     r.medium[slot] = S.media.cameraMedium;
 }
 
+// The material record ri's closest hit shades with: its primitive's, or with mix materials the
+// one k_vclosest<TM, true> chose (MixMaterial::ChooseMaterial at the hit, intersect.h:90-97)
+__device__ inline int VolHitMaterial(const DeviceScene &S, const PathState &st, int ri, int prim) {
+    return st.hitMat[0] ? st.hitMat[0][ri] : S.primMaterial[prim];
+}
 // a surface hit on Material "interface" (type 3): the ray only changes medium (k_viface)
-__device__ inline bool IsInterfaceHit(const DeviceScene &S, int prim) {
-    return prim >= 0 && S.matType[S.primMaterial[prim]] == 3;
+__device__ inline bool IsInterfaceHit(const DeviceScene &S, const PathState &st, int ri, int prim) {
+    return prim >= 0 && S.matType[VolHitMaterial(S, st, ri, prim)] == 3;
 }
 
-template <int TM>
+// Mix: the scene has mix materials, resolved per hit into st.hitMat[0] (an out-of-line call,
+// compiled into these instantiations only)
+template <int TM, bool Mix = false>
 __global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_vclosest(DeviceScene S, PathState st, VolState v,
                                                                           int wf, int timed) {
     const QueueView rays = LoadQueue(st, wf, kVRay);
@@ -653,8 +660,15 @@ __global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_vclosest(DeviceS
             v.hitB[NR + ri] = h.b1;
             v.hitB[2 * NR + ri] = h.b2;
             v.hitB[3 * NR + ri] = prim >= 0 ? h.t : kInfinity;
+            if constexpr (Mix) {
+                if (prim >= 0) {
+                    int mat = S.primMaterial[prim];
+                    if (S.matType[mat] == kMatMixT) mat = ResolveMixMaterial(*S.self, prim, mat, h.b0, h.b1, h.b2, d);
+                    st.hitMat[0][ri] = mat;
+                }
+            }
             medium = rec.medium[ri];
-            iface = medium < 0 && IsInterfaceHit(S, prim);
+            iface = medium < 0 && IsInterfaceHit(S, st, ri, prim);
             esc = medium < 0 && prim < 0;
         }
         // rays inside a medium sample it first (MediumSampleQueue), the rest go to the surface
@@ -817,7 +831,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vmedium(DeviceScene 
             }
         }
         const int hp = toSurf ? v.hitPrim[ri] : 0;
-        const bool iface = toSurf && IsInterfaceHit(S, hp), esc = toSurf && hp < 0;
+        const bool iface = toSurf && IsInterfaceHit(S, st, ri, hp), esc = toSurf && hp < 0;
         const int p0 = WavePush(surfCnt, toSurf && !iface && !esc);
         const int p1 = WavePush(scatCnt, toScat);
         const int p2 = WavePush(&st.counters[CounterIndex(wf, kVIface, shard)], iface);
@@ -993,7 +1007,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_GREY_WAVES) k_vmedium_grey(De
             }
         }
         const int hp = toSurf ? v.hitPrim[ri] : 0;
-        const bool iface = toSurf && IsInterfaceHit(S, hp), esc = toSurf && hp < 0;
+        const bool iface = toSurf && IsInterfaceHit(S, st, ri, hp), esc = toSurf && hp < 0;
         const int p0 = WavePush(surfCnt, toSurf && !iface && !esc);
         const int p1 = WavePush(scatCnt, toScat);
         const int p2 = WavePush(&st.counters[CounterIndex(wf, kVIface, shard)], iface);
@@ -1255,7 +1269,7 @@ __global__ void __launch_bounds__(kBlock) k_vtexture(DeviceScene S, PathState st
         const int ri = v.surfQ[QueueSlot(surf, j)];
         const int prim = v.hitPrim[ri];
         if (prim < 0) continue;  // escaped
-        const int mat = S.primMaterial[prim];
+        const int mat = VolHitMaterial(S, st, ri, prim);
         if (S.matType[mat] == 3) continue;  // interfaces
         HitTextures<true, Ext>(S, st, wf, ri, prim, mat, v.hitB, rec.lambda0);
     }
@@ -1303,7 +1317,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
         const V3 wo3 = Normalize(-rd);
         int mIn, mOut;
         MediaOf(S, prim, medium, &mIn, &mOut);
-        const int mat = S.primMaterial[prim];
+        const int mat = VolHitMaterial(S, st, ri, prim);
         const int mtypeHit = S.matType[mat];
         if (mtypeHit == 3) continue;  // interface crossings: k_viface
         if constexpr (Tex) {
@@ -1796,7 +1810,7 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
         const int ri = v.surfQ[QueueSlot(surf, j)];
         const int prim = v.hitPrim[ri];
         if (prim < 0) continue;
-        const int mat = S.primMaterial[prim];
+        const int mat = VolHitMaterial(S, st, ri, prim);
         const int mtype = S.matType[mat];
         if (mtype != kMatCoatedDiffuseT && mtype != kMatCoatedConductorT && mtype != kMatDiffuseTransmissionT) continue;
         const bool dt = mtype == kMatDiffuseTransmissionT;
@@ -2408,6 +2422,7 @@ size_t VolTraversalStaticLds(int tm) {
 #define TAKE_TM(TM)                                                      \
     if (tm == TM) {                                                      \
         take(reinterpret_cast<const void *>(&k_vclosest<TM>));           \
+        take(reinterpret_cast<const void *>(&k_vclosest<TM, true>));     \
         take(reinterpret_cast<const void *>(&k_vshadow_grey<TM, false>)); \
         take(reinterpret_cast<const void *>(&k_vshadow_grey<TM, true>));  \
         take(reinterpret_cast<const void *>(&k_vshadow<TM>));            \
@@ -2441,9 +2456,15 @@ hipError_t LaunchVolCamera(const DeviceScene &S, const PathState &st, const VolS
 hipError_t LaunchVolClosest(const DeviceScene &S, const PathState &st, const VolState &v, int wf, int maxCount,
                             int timed, hipStream_t s) {
     const dim3 block(kBlock), gT(VolGrid(maxCount, PBRT_GRID_CAP));
-#define K_VCLOSEST(tm) k_vclosest<tm>
-    PBRT_LAUNCH_TRAVERSAL(S, K_VCLOSEST, gT, block, VolStackBytes(S), s, S, st, v, wf, timed);
+    if (st.hitMat[0]) {
+#define K_VCLOSEST(tm) k_vclosest<tm, true>
+        PBRT_LAUNCH_TRAVERSAL(S, K_VCLOSEST, gT, block, VolStackBytes(S), s, S, st, v, wf, timed);
 #undef K_VCLOSEST
+    } else {
+#define K_VCLOSEST(tm) k_vclosest<tm>
+        PBRT_LAUNCH_TRAVERSAL(S, K_VCLOSEST, gT, block, VolStackBytes(S), s, S, st, v, wf, timed);
+#undef K_VCLOSEST
+    }
     return hipGetLastError();
 }
 // the rest of wavefront iteration wf after its closest-hit launch

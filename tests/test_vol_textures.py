@@ -2,8 +2,9 @@
 surface stage evaluates the same texEval calls and bump / normal mapping as the surface path
 (EvaluateMaterialAndBSDF, surfscatter.cpp:57-137).  k_vtexture evaluates them over the
 iteration's surface queue; k_vsurface<..., Tex> reads the results.  The oracle's volumetric
-integrator shares MakeBSDF with its surface integrator, so the GPU film is checked against it
-(CR-math oracle, as the media kernels)."""
+integrator shares MakeBSDF and the mix resolution with its surface integrator, so the GPU film
+is checked against it (CR-math oracle, as the media kernels).  Mix materials resolve at the
+closest hit (k_vclosest<TM, true>) there too."""
 import numpy as np
 import pytest
 
@@ -62,16 +63,27 @@ def test_textured_media_scene_renders_on_the_oracle(pa, oracle, tmp_path):
     assert np.isfinite(img).all() and np.abs(img - ref).mean() > 1e-3
 
 
+MIX = """MakeNamedMaterial "a" "string type" "diffuse" "rgb reflectance" [0.7 0.3 0.2]
+MakeNamedMaterial "b" "string type" "conductor" "float roughness" 0.15
+Material "mix" "string materials" ["a" "b"] "texture amount" "rough"
+Shape "trianglemesh" "integer indices" [0 1 2 0 2 3] "point3 P" [-1 0.01 -2.5 1 0.01 -2.5 1 0.01 -1.6 -1 0.01 -1.6]
+    "point2 uv" [0 0 1 0 1 1 0 1]
+Material "mix" "string materials" ["a" "b"] "float amount" 0.4
+Shape "trianglemesh" "integer indices" [0 1 2] "point3 P" [-0.4 0.2 0.9 0.4 0.2 0.9 0 1.0 1.0]
+"""
+
+
 @pytest.mark.gpu
-def test_mix_with_media_refused(pa, tmp_path):
+def test_mix_with_media_matches_oracle_gpu(pa, oracle, tmp_path):
+    """Mix materials on the volumetric path: MixMaterial::ChooseMaterial at the closest hit
+    (k_vclosest<TM, true>), the chosen material shaded by k_vsurface / k_vlayered."""
+    from test_gpu_media import check, gpu_rgb, oracle_rgb
     write_maps(tmp_path)
-    text = HEAD + TEX.replace("{box}", box(-1.2, 1.2, 0.02, 1.6, -1.5, 0.6)) + (
-        'MakeNamedMaterial "a" "string type" "diffuse"\nMakeNamedMaterial "b" "string type" "conductor"\n'
-        'Material "mix" "string materials" ["a" "b"] "float amount" 0.3\n'
-        'Shape "trianglemesh" "integer indices" [0 1 2] "point3 P" [0 0 0 1 0 0 0 1 0]\n')
+    text = HEAD + TEX.replace("{box}", box(-1.2, 1.2, 0.02, 1.6, -1.5, 0.6)) + MIX
     sc = pa.Scene.from_string(text, tmp_path)
-    with pytest.raises(pa.PbrtError, match="mix materials together with the volumetric path"):
-        pa.WavefrontPathIntegrator(sc, max_paths=1 << 12)
+    gpu, _ = gpu_rgb(pa, oracle, sc)
+    frac, mean_rel = check(gpu, oracle_rgb(oracle, sc))
+    print(f"volumetric mix parity: {frac*100:.3f}% pixels within 1e-3, mean rel {mean_rel:.2e}")
 
 
 @pytest.mark.gpu

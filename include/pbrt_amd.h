@@ -444,7 +444,8 @@ int pbrt_debug_queue_counts(pbrt_context *ctx, int32_t *counts, int n);
 int pbrt_debug_kernel_sections(pbrt_context *ctx, uint64_t *cycles, int n);
 /* queue-integrity check of the volumetric wavefront (diagnostics): with it on, every queue
  * slot the surface, layered and medium-scattering stages count must be written; a slot that is
- * counted but left unwritten (a "hole") is counted, printed by the device and neutralised.
+ * counted but left unwritten (a "hole") is counted and printed by the device, and pbrt_render
+ * stops with an error before any stage reads it.
  * pbrt_debug_queue_holes returns the holes found since its last call and resets the count.
  * PBRT_AMD_QUEUE_CHECK=1 turns the check on from the environment. */
 int pbrt_debug_set_queue_check(int on);

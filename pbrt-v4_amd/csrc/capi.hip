@@ -472,6 +472,7 @@ struct pbrt_context {
     DevBuf<EnvCoef> envCoef;
     DevBuf<float> envDist;
     DevBuf<DeviceEnvLight> envLights;
+    DevBuf<int> queueHoles;       // VolState::holes
     DevBuf<int> matMix, hitMat;   // mix materials: {m0, m1, amount program} and resolved materials
     bool hasMix = false;
     // ray binning before closest hits at depth >= 1 (HBM-resident trees; PBRT_AMD_RAY_SORT=0/1
@@ -1494,6 +1495,12 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
         v.shFlags = ti(1);
         if (g - c->vfState.p > (ptrdiff_t)vf * NR || gi - c->viState.p > (ptrdiff_t)vi * NR)
             throw Error("VolState layout overflow");
+        // the queue-integrity diagnostic's hole counter (PBRT_AMD_QUEUE_CHECK), this context's own
+        if (!c->queueHoles.p) {
+            c->queueHoles.Alloc(1);
+            HIPCHECK(hipMemset(c->queueHoles.p, 0, sizeof(int)));
+        }
+        v.holes = c->queueHoles.p;
     }
     if (!c->devStats.p) {
         c->devStats.Alloc(kStatsSlots);
@@ -1612,7 +1619,11 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
                     }
                     if (timed) RecordEvent(c, false);
                     StageTimer t(c, "Media, surfaces, scattering and shadow rays (volpath iteration)", c->stream);
-                    HIPCHECK(LaunchVolIteration(c->S, st, c->vs, wf, (int)nActive, c->stream));
+                    const hipError_t e = LaunchVolIteration(c->S, st, c->vs, wf, (int)nActive, c->stream);
+                    if (e == hipErrorIllegalState)
+                        throw Error("queue-integrity check (PBRT_AMD_QUEUE_CHECK): a volumetric stage counted queue slots "
+                                    "it never wrote (iteration " + std::to_string(wf) + "); render aborted");
+                    HIPCHECK(e);
                 }
                 {
                     StageTimer t(c, "Update film (k_film)", c->stream);

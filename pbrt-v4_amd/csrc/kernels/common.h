@@ -29,15 +29,6 @@ constexpr int kBlock = 256;
 #ifndef PBRT_QUANT_TRAVERSAL_WAVES
 #define PBRT_QUANT_TRAVERSAL_WAVES 6
 #endif
-// k_closest's dynamic ray fetch (wavefront.hip) for triangle-only traversal modes, and the number
-// of idle lanes at which a wave refills
-#ifndef PBRT_DYN_FETCH
-#define PBRT_DYN_FETCH 0
-#endif
-#ifndef PBRT_DYN_REFILL
-#define PBRT_DYN_REFILL 16
-#endif
-constexpr bool kDynFetch = PBRT_DYN_FETCH != 0;
 #ifndef PBRT_SHADE_WAVES
 #define PBRT_SHADE_WAVES 3  // waves/SIMD the shade kernel is compiled for (VGPR budget)
 #endif
@@ -657,8 +648,9 @@ __device__ __attribute__((noinline)) bool AlphaKilled(const DeviceScene *S, int 
                                                      V3 o, V3 d);
 // Alpha: the scene has alpha-tested primitives (S.primAlpha); compiled into the kTravShapes
 // ("extended") instantiations only
-// One ray's resumable group traversal: TraverseCW runs CwStep to completion; k_closest's
-// dynamic-fetch loop (PBRT_DYN_FETCH) interleaves steps of different rays in one lane.
+// One ray's resumable group traversal: TraverseCW runs CwStep to completion (round 4's
+// dynamic-ray-fetch experiment interleaved steps of different rays in one lane: measured slower
+// on C2 and C4, profiles/r04_c4_traversal_ab.txt, and removed in round 5).
 struct CwState {
     TriRayR tr;
     CwRay r;

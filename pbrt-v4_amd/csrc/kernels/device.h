@@ -351,6 +351,7 @@ struct VolState {
     float *shLambda0;          // [NR]
     int *shPixel, *shMedium;   // [NR]
     int *shFlags;              // [NR] uniform-spectrum bits (volpath.hip kShUni*)
+    int *holes;                // [1] queue-integrity diagnostic: unwritten queue slots found
 };
 
 }  // namespace pbrt_amd

@@ -2357,34 +2357,25 @@ __global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_vshadow_grey(Dev
 
 // Diagnostic (PBRT_AMD_QUEUE_CHECK=1): queue slots that a stage counted but never wrote.  The
 // launcher fills the slots' pixel field with -1 before the surface stage; afterwards every
-// counted slot must hold a pixel index.  Holes are counted into hole[0] and the first few are
-// printed with their queue and shard.
-// A shadow-queue hole is then made harmless (no contribution to pixel 0), so the render goes on.
-__global__ void k_queue_holes(const int *counters, int wf, int queue, int *pixel, int capS, int *hole, VolState v,
-                              int NR, int stage) {
+// counted slot must hold a pixel index.  Holes are counted into the context's counter and the
+// first few printed with their queue and shard; the check only reads.  The launcher then waits
+// for the check and, when it found a hole, stops the iteration before any stage consumes the
+// unwritten records (LaunchVolIteration returns hipErrorIllegalState; capi.hip raises it).
+__global__ void k_queue_holes(const int *counters, int wf, int queue, const int *pixel, int capS, int *hole,
+                              int stage) {
     const int shard = blockIdx.y;
     const int n = counters[CounterIndex(wf, queue, shard)];
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const int js = shard * capS + i;
-        if (pixel[js] < 0) {
+        if (pixel[shard * capS + i] < 0) {
             const int k = atomicAdd(hole, 1);
             if (k < 8)
                 printf("queue hole after stage %d: iteration %d queue %d shard %d slot %d of %d\n", stage, wf, queue,
                        shard, i, n);
-            pixel[js] = 0;
-            if (queue == kVShadow) {
-                v.shFlags[js] = kShUniLd | kShUniRu | kShUniRl;
-                v.shLd[js] = 0;
-                v.shLd[NR + js] = v.shLd[2 * (size_t)NR + js] = v.shLd[3 * (size_t)NR + js] = 0;
-                v.shRu[js] = v.shRl[js] = 1;
-                for (int c = 0; c < 6; ++c) v.shRay[(size_t)c * NR + js] = c == 5 ? 1e-6f : 0.f;
-                v.shLambda0[js] = 500.f;
-                v.shMedium[js] = -1;
-            }
         }
     }
 }
 static int g_queueCheck = -1;  // -1: PBRT_AMD_QUEUE_CHECK decides on first use
+static int g_holesFound = 0;   // holes the checks found since the last TakeQueueHoles (host)
 static bool QueueCheckOn() {
     if (g_queueCheck < 0) {
         const char *e = getenv("PBRT_AMD_QUEUE_CHECK");
@@ -2392,22 +2383,20 @@ static bool QueueCheckOn() {
     }
     return g_queueCheck == 1;
 }
-static int *QueueHoleCounter() {
-    static int *d = nullptr;
-    if (!d) {
-        (void)hipMalloc(&d, sizeof(int));
-        (void)hipMemset(d, 0, sizeof(int));
-    }
-    return d;
+// after the checks of one iteration: their hole count (the counter is reset), or -1 on a HIP error
+static int CollectQueueHoles(const VolState &v, hipStream_t s) {
+    int h = 0;
+    if (hipStreamSynchronize(s) != hipSuccess) return -1;
+    if (hipMemcpy(&h, v.holes, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    if (h && hipMemset(v.holes, 0, sizeof(int)) != hipSuccess) return -1;
+    g_holesFound += h;
+    return h;
 }
 void SetQueueCheck(int on) { g_queueCheck = on ? 1 : 0; }
 // holes found since the last call (the count is reset); 0 when the check never ran
 int TakeQueueHoles() {
-    if (g_queueCheck != 1) return 0;
-    int h = 0;
-    (void)hipDeviceSynchronize();
-    (void)hipMemcpy(&h, QueueHoleCounter(), sizeof(int), hipMemcpyDeviceToHost);
-    (void)hipMemset(QueueHoleCounter(), 0, sizeof(int));
+    const int h = g_holesFound;
+    g_holesFound = 0;
     return h;
 }
 
@@ -2494,7 +2483,7 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
 #define QUEUE_CHECK(stage)                                                                                          \
     if (qcheck)                                                                                                     \
         hipLaunchKernelGGL(k_queue_holes, dim3(64, kShards), block, 0, s, st.counters, wf, kVShadow, v.shPixel,      \
-                           st.capS, QueueHoleCounter(), v, st.NR, stage);
+                           st.capS, v.holes, stage);
     // Ext: analytic shapes or image lights in the scene (their paths compiled in)
     if (S.nShapes > 0 || S.nEnv > 0 || S.nImageDelta > 0 || S.hasSpread) {
         if (S.textured) {
@@ -2524,9 +2513,13 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
         VOL_REST(false);
     }
 #undef VOL_REST
-    if (qcheck)
+    if (qcheck) {
         hipLaunchKernelGGL(k_queue_holes, dim3(64, kShards), block, 0, s, st.counters, wf + 1, kVRay,
-                           v.rec[(wf + 1) & 1].pixel, st.capS, QueueHoleCounter(), v, st.NR, 4);
+                           v.rec[(wf + 1) & 1].pixel, st.capS, v.holes, 4);
+        const int h = CollectQueueHoles(v, s);
+        if (h < 0) return hipGetLastError() != hipSuccess ? hipGetLastError() : hipErrorUnknown;
+        if (h > 0) return hipErrorIllegalState;  // nothing consumes the unwritten records
+    }
 #undef QUEUE_CHECK
     if (S.media.allGrey && S.media.hasCloud) {
 #define K_VSHADOW_GREY(tm) k_vshadow_grey<tm, true>

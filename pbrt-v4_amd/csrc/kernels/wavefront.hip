@@ -163,52 +163,6 @@ __global__ void __launch_bounds__(kBlock, TraversalWaves(TM))
             d = V3(rec.ray[3 * N + qi], rec.ray[4 * N + qi], rec.ray[5 * N + qi]);
         }
     };
-    if constexpr (kDynFetch && (TM & kTravShapes) == 0) {
-        // Dynamic ray fetch (Aila & Laine 2009, "speculative"/"replacing" traversal): a lane
-        // whose ray is done takes the next ray of its wave's stream once PBRT_DYN_REFILL lanes
-        // are idle, instead of idling until the wave's slowest ray finishes (C4: 12.7 nodes per
-        // ray against a wave maximum of 28.7, profiles/r04_c4_trav_stats.json).  A wave's
-        // stream is the 64-ray chunks w, w + W, w + 2W, ... (W waves in the grid); finished
-        // rays are recorded and enqueued at the refills, with every lane of the wave present.
-        constexpr int tm = TM & 3;
-        const int wpb = (int)blockDim.x >> 6, nw = (int)gridDim.x * wpb;
-        const int w = (int)blockIdx.x * wpb + ((int)threadIdx.x >> 6);
-        const int nChunks = (count + 63) >> 6;
-        const int end = (nChunks > w ? (nChunks - w + nw - 1) / nw : 0) * 64;  // stream positions
-        const unsigned long long below = (1ull << __lane_id()) - 1ull;
-        int pos = 0, qi = 0;
-        bool busy = false, done = false;
-        V3 d(0.f, 0.f, 0.f);
-        CwState s;
-        while (true) {
-            const unsigned long long idle = __ballot(!busy);
-            const bool feed = pos < end;
-            if ((feed && __popcll(idle) >= PBRT_DYN_REFILL) || idle == ~0ull) {
-                finish(done, qi, s.hit, s.best, d);
-                done = false;
-                if (feed) {
-                    const int p = pos + __popcll(idle & below);
-                    pos += __popcll(idle);
-                    if (!busy && p < end) {
-                        const int j = (w + (p >> 6) * nw) * 64 + (p & 63);
-                        if (j < count) {
-                            V3 o;
-                            fetch(j, qi, o, d);
-                            CwBegin(S, s, o, d, kInfinity);
-                            busy = true;
-                        }
-                    }
-                }
-                if (pos >= end && __ballot(busy) == 0) break;
-            }
-            if (busy && CwStep<false, tm == kTravQuant, tm == kTravLds, tm == kTravLds, false>(S, L, s, d, d, nullptr)) {
-                busy = false;
-                done = true;
-            }
-        }
-        queues.FlushAll();
-        return;
-    }
     for (; walk.n < walk.end; walk.n += walk.step) {
         const int j = walk.Chunk() * blockDim.x + threadIdx.x;
         bool active = j < count;
@@ -1759,6 +1713,9 @@ hipError_t LaunchShadeDiffuse(const DeviceScene &S, const PathState &st, int dep
     const dim3 grid(ShadeGridFor(maxCount)), block(kBlock);
     const size_t lds = ShadeLdsBytes(S, depth);
     const bool ext = S.nShapes > 0 || S.nEnv > 0 || S.nImageDelta > 0 || S.hasSpread || S.nImageAreaLights > 0;
+    // the lean kernel compiles the Ext paths (spread falloff, image emitters, shapes, image
+    // lights) and textures out: a launcher that asks for it on such a scene is a bug
+    if (lean && (ext || S.textured)) return hipErrorInvalidValue;
     if (S.textured && ext) hipLaunchKernelGGL((k_shade_diffuse<false, true, true>), grid, block, lds, s, S, st, depth);
     else if (S.textured) hipLaunchKernelGGL((k_shade_diffuse<false, true>), grid, block, lds, s, S, st, depth);
     else if (lean) hipLaunchKernelGGL(k_shade_diffuse<true>, grid, block, lds, s, S, st, depth);

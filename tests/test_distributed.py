@@ -128,3 +128,46 @@ def test_closest_bytes_from_queue_counts():
     # depth 0: 24*100 + 20*65 hits + 4*(65 + 5 + 30); depth 1: 24*65 + 20*3 emissive + 4*(0 + 3 + 20)
     assert rays == 165
     assert total == (2400 + 1300 + 400) + (1560 + 60 + 92)
+
+
+def _gpu_worker(rank, world, port, out_path):
+    """bench.py's N > 1 data path with the product: this rank renders its single-row interleave
+    (rows_for_rank(block=1)) with libpbrt_amd on device 0, wraps the device film with
+    film_tensor_from_device_ptr, and sum-reduces it (gloo, via the host) onto rank 0."""
+    import sys
+    sys.path.insert(0, str(ROOT / "pbrt-v4_amd"))
+    import pbrt_amd as pa
+    from pbrt_amd.tiles import film_tensor_from_device_ptr, reduce_film, rows_for_rank
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sc = pa.load_scene(SCENES / "cornell-box.pbrt", xresolution=96, yresolution=72, spp=8)
+    i = sc.info
+    integ = pa.WavefrontPathIntegrator(sc, device=0, max_paths=1 << 18)
+    integ.film_clear()
+    integ.render(rows=rows_for_rank(i.py0, i.py1, rank, world, block=1), first_sample=0, n_samples=i.spp)
+    integ.synchronize()
+    ptr, n = integ.film_device_ptr()
+    t = film_tensor_from_device_ptr(ptr, n, 0).cpu()
+    reduce_film(t, dst=0)
+    if rank == 0:
+        np.save(out_path, t.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_ranks_product_film_equals_single_gpu(tmp_path, pa):
+    """The product's multi-rank path once on the GPU: two ranks, each rendering every other film
+    row with libpbrt_amd on device 0, their device films reduced -- the same bits as one
+    process rendering the whole image (non-owned pixels are exact zeros)."""
+    out = tmp_path / "film.npy"
+    mp.spawn(_gpu_worker, args=(2, _free_port(), str(out)), nprocs=2, join=True)
+    sc = pa.load_scene(SCENES / "cornell-box.pbrt", xresolution=96, yresolution=72, spp=8)
+    integ = pa.WavefrontPathIntegrator(sc, device=0, max_paths=1 << 18)
+    integ.render()
+    integ.synchronize()
+    single = integ.film_raw().reshape(-1)
+    got = np.load(out)
+    assert np.abs(single).sum() > 0
+    np.testing.assert_array_equal(got, single)

@@ -235,6 +235,10 @@ typedef struct pbrt_scene_flat {
     int strat_xsamples, strat_ysamples, strat_jitter, sobol_log2_scale;
     const uint32_t *sobol_matrices32;
     const uint64_t *vdc_sobol, *vdc_sobol_inv;
+    /* util/noise.cpp NoisePerm[512] (as floats), for the procedural textures (dots, fbm,
+     * wrinkled, windy, marble: tex_node_info kinds 7-11; their params [22..24] = octaves,
+     * roughness, variation and [26] = marble scale) */
+    const float *noise_perm;
 } pbrt_scene_flat;
 
 typedef struct pbrt_render_params {
@@ -394,6 +398,11 @@ int pbrt_debug_sampler(const pbrt_scene *scene, int px, int py, int sample_index
  * cos of SinCosf; on GPU `device`, or compiled for the host when device < 0 (the two must agree
  * bit for bit, and the oracle's device-math mode with both) */
 int pbrt_debug_det_math(int device, int fn, const float *a, const float *b, int n, float *out);
+/* The procedural textures' kernels code on the host (core/texture_eval.h): kind 0 FBm, 1
+ * Turbulence (wrinkled), 2 windy, 3 InsidePolkaDot (in9[0..1] = s, t), 4 marble; params4 =
+ * octaves, roughness, scale, variation; in9 per point = p, dpdx, dpdy; out6 per point = value
+ * (marble: RGB, then its RGBAlbedoSpectrum sigmoid coefficients) */
+int pbrt_debug_procedural(int kind, const float *params4, const float *in9, int n, float *out6);
 /* RNG::SetSequence(seq); RNG::Advance(advance); two Uniform<uint32_t>() (util/rng.h:119-150) */
 int pbrt_debug_rng(uint64_t seq, uint64_t advance, uint32_t *out2);
 /* util/scattering.h components as the product evaluates them (core.h), host side.

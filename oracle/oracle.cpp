@@ -4251,6 +4251,78 @@ struct OTexCtx {
     Float u = 0, v = 0, dudx = 0, dudy = 0, dvdx = 0, dvdy = 0;
 };
 
+// ---------------------------------------------------------------- procedural textures
+// FBm / Turbulence (util/noise.cpp:114-152), WindyTexture (textures.h:1125-1130),
+// InsidePolkaDot (textures.cpp:287-303), MarbleTexture's RGB (textures.cpp:524-549 with
+// EvaluateCubicBezier, util/splines.h:18-28) over Perlin's Noise (Media::NoiseAt).
+namespace proc {
+static Float Octaves(Vec dpdx, Vec dpdy, int maxOct) {
+    const Float len2 = std::max(LengthSquared(dpdx), LengthSquared(dpdy));
+    const Float invLog2 = 1.442695040888963387004650940071;
+    return Clamp(-1 - (CRLog(len2) * invLog2) / 2, 0, (Float)maxOct);
+}
+static Float SmoothStep(Float x, Float a, Float b) {
+    if (a == b) return x < a ? 0 : 1;
+    const Float t = Clamp((x - a) / (b - a), 0, 1);
+    return t * t * (3 - 2 * t);
+}
+static Float FBm(const float *perm, Vec p, Vec dpdx, Vec dpdy, Float omega, int maxOct) {
+    const Float n = Octaves(dpdx, dpdy, maxOct);
+    const int nInt = (int)std::floor(n);
+    Float sum = 0, lambda = 1, o = 1;
+    for (int i = 0; i < nInt; ++i) {
+        sum += o * Media::NoiseAt(perm, lambda * p.x, lambda * p.y, lambda * p.z);
+        lambda *= 1.99f;
+        o *= omega;
+    }
+    sum += o * SmoothStep(n - nInt, .3f, .7f) * Media::NoiseAt(perm, lambda * p.x, lambda * p.y, lambda * p.z);
+    return sum;
+}
+static Float Turbulence(const float *perm, Vec p, Vec dpdx, Vec dpdy, Float omega, int maxOct) {
+    const Float n = Octaves(dpdx, dpdy, maxOct);
+    const int nInt = (int)std::floor(n);
+    Float sum = 0, lambda = 1, o = 1;
+    for (int i = 0; i < nInt; ++i) {
+        sum += o * std::abs(Media::NoiseAt(perm, lambda * p.x, lambda * p.y, lambda * p.z));
+        lambda *= 1.99f;
+        o *= omega;
+    }
+    sum += o * Lerp(SmoothStep(n - nInt, .3f, .7f), 0.2f, std::abs(Media::NoiseAt(perm, lambda * p.x, lambda * p.y, lambda * p.z)));
+    for (int i = nInt; i < maxOct; ++i) {
+        sum += o * 0.2f;
+        o *= omega;
+    }
+    return sum;
+}
+static Float Windy(const float *perm, Vec p, Vec dpdx, Vec dpdy) {
+    return std::abs(FBm(perm, p * .1f, dpdx * .1f, dpdy * .1f, .5f, 3)) * FBm(perm, p, dpdx, dpdy, .5f, 6);
+}
+static bool PolkaDot(const float *perm, Float s, Float t) {
+    const int sc = (int)std::floor(s + .5f), tc = (int)std::floor(t + .5f);
+    if (!(Media::NoiseAt(perm, sc + .5f, tc + .5f, .5f) > 0)) return false;
+    const Float r = .35f, shift = .5f - r;
+    const Float cs = sc + shift * Media::NoiseAt(perm, sc + 1.5f, tc + 2.8f, .5f);
+    const Float ct = tc + shift * Media::NoiseAt(perm, sc + 4.5f, tc + 9.8f, .5f);
+    return Sqr(s - cs) + Sqr(t - ct) < Sqr(r);
+}
+static void Marble(const float *perm, Vec p, Vec dpdx, Vec dpdy, int oct, Float omega, Float scale, Float variation,
+                   Float rgb[3]) {
+    static const Float col[9][3] = {{.58f, .58f, .6f}, {.58f, .58f, .6f}, {.58f, .58f, .6f}, {.5f, .5f, .5f},  {.6f, .59f, .58f},
+                                    {.58f, .58f, .6f}, {.58f, .58f, .6f}, {.2f, .2f, .33f},  {.58f, .58f, .6f}};
+    p = p * scale;
+    const Float m = p.y + variation * FBm(perm, p, dpdx * scale, dpdy * scale, omega, oct);
+    Float t = .5f + .5f * CRSin(m);
+    const int first = std::min((int)std::floor(t * 6), 5);
+    t = t * 6 - first;
+    for (int c = 0; c < 3; ++c) {
+        Float a[3], b[2];
+        for (int k = 0; k < 3; ++k) a[k] = Lerp(t, col[first + k][c], col[first + k + 1][c]);
+        for (int k = 0; k < 2; ++k) b[k] = Lerp(t, a[k], a[k + 1]);
+        rgb[c] = 1.5f * Lerp(t, b[0], b[1]);
+    }
+}
+}  // namespace proc
+
 struct OTextures {
     const pbrt_scene_flat *f = nullptr;
     std::vector<OImage> images;
@@ -4280,6 +4352,14 @@ struct OTextures {
         FindMinimumDifferentials();
     }
     const int32_t *Info(int node) const { return f->tex_node_info + 8 * node; }
+    // PointTransformMapping (textures.h:229-246): textureFromRender (params [0..11]) of a point / vector
+    static Vec P3(const float *q, Vec p) {
+        return Vec(q[0] * p.x + q[1] * p.y + q[2] * p.z + q[3], q[4] * p.x + q[5] * p.y + q[6] * p.z + q[7],
+                   q[8] * p.x + q[9] * p.y + q[10] * p.z + q[11]);
+    }
+    static Vec V3x(const float *q, Vec v) {
+        return Vec(q[0] * v.x + q[1] * v.y + q[2] * v.z, q[4] * v.x + q[5] * v.y + q[6] * v.z, q[8] * v.x + q[9] * v.y + q[10] * v.z);
+    }
     const float *Par(int node) const { return f->tex_node_params + 28 * node; }
     const float *Spec(int node, int k) const { return f->tex_node_spec + 32 * node + 8 * k; }
 
@@ -4551,6 +4631,19 @@ struct OTextures {
             return (1 - st[0]) * (1 - st[1]) * q[22] + st[0] * (1 - st[1]) * q[24] + (1 - st[0]) * st[1] * q[23] +
                    st[0] * st[1] * q[25];
         }
+        case 7: {  // FloatDotsTexture
+            Float st[2], dst[4];
+            Map2D(node, c, st, dst);
+            return proc::PolkaDot(f->noise_perm, st[0], st[1]) ? EvalF(in[2], c) : EvalF(in[3], c);
+        }
+        case 8:
+        case 9:
+        case 10: {  // FBmTexture / WrinkledTexture / WindyTexture over the point mapping
+            const Vec p = P3(q, c.p), d0 = V3x(q, Vec(0, 0, 0));
+            if (in[0] == 8) return proc::FBm(f->noise_perm, p, d0, d0, q[23], (int)q[22]);
+            if (in[0] == 9) return proc::Turbulence(f->noise_perm, p, d0, d0, q[23], (int)q[22]);
+            return proc::Windy(f->noise_perm, p, d0, d0);
+        }
         default: {  // FloatImageTexture
             Float st[2], dst[4];
             Map2D(node, c, st, dst);
@@ -4598,6 +4691,20 @@ struct OTextures {
             if (w != 1) t0 = EvalS(in[2], c, L);
             if (w != 0) t1 = EvalS(in[3], c, L);
             return t0 * (1 - w) + t1 * w;
+        }
+        case 7: {  // SpectrumDotsTexture
+            Float st[2], dst[4];
+            Map2D(node, c, st, dst);
+            return proc::PolkaDot(f->noise_perm, st[0], st[1]) ? EvalS(in[2], c, L) : EvalS(in[3], c, L);
+        }
+        case 11: {  // MarbleTexture: RGBAlbedoSpectrum(sRGB, rgb)
+            const Vec p = P3(q, c.p), d0 = V3x(q, Vec(0, 0, 0));
+            Float rgb[3], co[3];
+            proc::Marble(f->noise_perm, p, d0, d0, (int)q[22], q[23], q[26], q[24], rgb);
+            ORGBCoeffs(rgb[0], rgb[1], rgb[2], co);
+            Spectrum r;
+            for (int i = 0; i < NS; ++i) r[i] = Sigmoid(co[0], co[1], co[2], L.lambda[i]);
+            return r;
         }
         case 5: {  // Bilerp({s, t}, {v00, v10, v01, v11}) (util/spectrum.h:734-738)
             Float st[2], dst[4];
@@ -6150,6 +6257,24 @@ void oracle_sampler(int kind, int spp, int seed, int xs, int ys, int jitter, int
     out7[3] = st.Get1D();
     st.Get2D(&out7[4], &out7[5]);
     out7[6] = st.Get1D();
+}
+// the oracle's procedural textures: kind 0 fbm, 1 turbulence, 2 windy, 3 polka dot (in9[0..1]),
+// 4 marble (out: RGB, then its sigmoid coefficients); params4 = octaves, roughness, scale, variation
+void oracle_procedural(int kind, const float *perm, const float *params4, const float *in9, int n, float *out6) {
+    for (int i = 0; i < n; ++i) {
+        const float *q = in9 + 9 * i;
+        float *o = out6 + 6 * i;
+        const Vec p(q[0], q[1], q[2]), dx(q[3], q[4], q[5]), dy(q[6], q[7], q[8]);
+        for (int k = 0; k < 6; ++k) o[k] = 0;
+        if (kind == 0) o[0] = proc::FBm(perm, p, dx, dy, params4[1], (int)params4[0]);
+        else if (kind == 1) o[0] = proc::Turbulence(perm, p, dx, dy, params4[1], (int)params4[0]);
+        else if (kind == 2) o[0] = proc::Windy(perm, p, dx, dy);
+        else if (kind == 3) o[0] = proc::PolkaDot(perm, q[0], q[1]) ? 1.f : 0.f;
+        else {
+            proc::Marble(perm, p, dx, dy, (int)params4[0], params4[1], params4[2], params4[3], o);
+            ORGBCoeffs(o[0], o[1], o[2], o + 3);
+        }
+    }
 }
 void oracle_rng(uint64_t seq, uint64_t advance, uint32_t *out2) {
     SeqRNG r;

@@ -33,6 +33,7 @@ def lib():
         _lib.oracle_zsobol.argtypes = [ctypes.c_int] * 9 + [ctypes.c_void_p]
         _lib.oracle_sampler.argtypes = [ctypes.c_int] * 9 + [ctypes.c_void_p] * 3 + [ctypes.c_int] * 4 + [ctypes.c_void_p]
         _lib.oracle_rng.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]
+        _lib.oracle_procedural.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 3 + [ctypes.c_int, ctypes.c_void_p]
         vp = ctypes.c_void_p
         _lib.oracle_warps.argtypes = [vp, vp, vp]
         _lib.oracle_spherical_triangle.argtypes = [vp, vp, vp, vp]
@@ -357,3 +358,13 @@ def rng(seq, advance):
     out = np.zeros(2, np.uint32)
     lib().oracle_rng(int(seq), int(advance), out.ctypes.data)
     return int(out[0]), int(out[1])
+
+
+def procedural(kind, perm, params4, in9):
+    """The oracle's procedural textures (fbm, turbulence, windy, polka dot, marble): [n][6]."""
+    perm = np.ascontiguousarray(perm, np.float32)
+    par = np.ascontiguousarray(params4, np.float32)
+    x = np.ascontiguousarray(in9, np.float32).reshape(-1, 9)
+    out = np.zeros((len(x), 6), np.float32)
+    lib().oracle_procedural(kind, perm.ctypes.data, par.ctypes.data, x.ctypes.data, len(x), out.ctypes.data)
+    return out

@@ -138,6 +138,11 @@ static void BuildTexTables(const SceneDesc &s, TexTables *t) {
             for (int k = 0; k < 3; ++k) n.p[22 + k] = d.dir[k];
         n.p[26] = d.scale;
         n.p[27] = d.maxAniso;
+        if (d.kind >= kTexDots) {  // procedural: octaves, omega, variation (core/texture_eval.h)
+            n.p[22] = (float)d.octaves;
+            n.p[23] = d.omega;
+            n.p[24] = d.variation;
+        }
         t->nodes.push_back(n);
         for (int k = 0; k < 4; ++k) {
             const TexSpectrumConst &c = d.svalue[k];
@@ -222,6 +227,7 @@ static TexView HostTexView(const TexTables &t) {
     v.rgbZNodes = rgb.data();
     v.rgbCoeffs = rgb.data() + 64;
     v.ewaLut = GetSpectralData().mipFilterLUT.data();
+    v.noisePerm = GetSpectralData().noisePerm.data();
     v.nProgs = (int)t.progs.size();
     v.nLuts = (int)t.images.size();
     return v;
@@ -460,7 +466,7 @@ struct pbrt_context {
     DevBuf<DeviceImage> texImages;
     DevBuf<DeviceImageLevel> texLevels;
     DevBuf<uint8_t> texData;
-    DevBuf<float> texLuts, rgbTable, ewaLut;
+    DevBuf<float> texLuts, rgbTable, ewaLut, noisePerm;
     DevBuf<DeviceTexInstr> texInstrs;
     DevBuf<DeviceTexProgram> texProgs;
     DevBuf<int> matTex;
@@ -1089,6 +1095,8 @@ static void BuildDevice(pbrt_context *c) {
             S.tex.rgbZNodes = c->rgbTable.p;
             S.tex.rgbCoeffs = c->rgbTable.p + 64;
             S.tex.ewaLut = c->ewaLut.p;
+            c->noisePerm.Upload(GetSpectralData().noisePerm);  // procedural textures' Perlin noise
+            S.tex.noisePerm = c->noisePerm.p;
             S.tex.nProgs = (int)tt.progs.size();
             S.tex.nLuts = (int)tt.images.size();
             S.camDiff = MakeCameraDiff(s);
@@ -1853,6 +1861,7 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
         f->n_images = (int)s.images.size();
         f->tex_node_info = t.nodeInfo.data();
         f->tex_node_params = t.nodeParams.data();
+        f->noise_perm = GetSpectralData().noisePerm.data();
         f->tex_node_spec = t.specFlat.data();
         f->image_info = t.imageInfo.data();
         f->image_levels = t.levelInfo.data();
@@ -2589,6 +2598,35 @@ int pbrt_debug_det_math(int device, int fn, const float *a, const float *b, int 
         if (n > 0) {
             HIPCHECK(LaunchDetMath(fn, da.p, db.p, n, dout.p, nullptr));
             HIPCHECK(hipMemcpy(out, dout.p, (size_t)n * sizeof(float), hipMemcpyDeviceToHost));
+        }
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_debug_procedural(int kind, const float *params4, const float *in9, int n, float *out6) {
+    try {
+        if (!params4 || !in9 || !out6 || n < 0 || kind < 0 || kind > 4) return Fail("pbrt_debug_procedural: bad arguments");
+        const auto &perm = GetSpectralData().noisePerm;
+        if (perm.size() != 512) return Fail("spectral data lacks the noise permutation (NoisePerm)");
+        TexTables none;
+        const TexView T = HostTexView(none);  // the RGB -> spectrum table for marble
+        for (int i = 0; i < n; ++i) {
+            const float *q = in9 + 9 * i;
+            float *o = out6 + 6 * i;
+            const V3 p(q[0], q[1], q[2]), dx(q[3], q[4], q[5]), dy(q[6], q[7], q[8]);
+            for (int k = 0; k < 6; ++k) o[k] = 0;
+            switch (kind) {
+            case 0: o[0] = FBmNoise(perm.data(), p, dx, dy, params4[1], (int)params4[0]); break;
+            case 1: o[0] = TurbulenceNoise(perm.data(), p, dx, dy, params4[1], (int)params4[0]); break;
+            case 2: o[0] = WindyNoise(perm.data(), p, dx, dy); break;
+            case 3: o[0] = InsidePolkaDot(perm.data(), q[0], q[1]) ? 1.f : 0.f; break;
+            default:
+                MarbleRGB(perm.data(), p, dx, dy, (int)params4[0], params4[1], params4[2], params4[3], o);
+                RGBToCoeffs(T, o[0], o[1], o[2], o + 3);
+                break;
+            }
         }
         return 0;
     } catch (const std::exception &e) {

@@ -14,6 +14,9 @@
 //   MIPMap::Filter / Bilerp / Texel / EWA   util/mipmap.cpp:208-375, util/image.h:255-292
 //   RGBToSpectrumTable::operator()          util/color.cpp:36-75
 //   RGBAlbedo/UnboundedSpectrum             util/spectrum.h, util/spectrum.cpp:240-244
+//   Dots / FBm / Wrinkled / Windy / Marble  textures.h:427-505, 813-841, 1117-1160,
+//                                           textures.cpp:287-303, 524-553; FBm / Turbulence
+//                                           util/noise.cpp:114-152; EvaluateCubicBezier splines.h
 #pragma once
 
 #include "core.h"
@@ -54,10 +57,13 @@ struct DeviceTexInstr {
 // phase-1 ops (once per hit: scalar registers)
 enum TexOp1 : int {
     kT1FConst = 0, kT1FImage = 1, kT1FBilerp = 2, kT1CheckW = 3, kT1DirAmt = 4, kT1FScale = 5,
-    kT1FMix = 6, kT1FDMix = 7, kT1SImage = 8, kT1BilerpW = 9
+    kT1FMix = 6, kT1FDMix = 7, kT1SImage = 8, kT1BilerpW = 9,
+    // procedural: FBm, Turbulence (wrinkled), windy (float textures), the polka-dot selector,
+    // a float select by it, and marble's RGBAlbedoSpectrum coefficients (4 registers)
+    kT1FBm = 10, kT1Wrinkled = 11, kT1Windy = 12, kT1DotsW = 13, kT1FSel = 14, kT1Marble = 15
 };
 // phase-2 ops (per wavelength: value stack)
-enum TexOp2 : int { kT2Const = 0, kT2RGBReg = 1, kT2Scale = 2, kT2Mix = 3, kT2DMix = 4, kT2Bilerp = 5 };
+enum TexOp2 : int { kT2Const = 0, kT2RGBReg = 1, kT2Scale = 2, kT2Mix = 3, kT2DMix = 4, kT2Bilerp = 5, kT2Sel = 6 };
 constexpr int kTexMaxRegs = 16, kTexMaxStack = 8;
 
 struct TexView {
@@ -72,6 +78,7 @@ struct TexView {
     const float *rgbZNodes;     // RGBToSpectrumTable scale[64]
     const float *rgbCoeffs;     // RGBToSpectrumTable data[3][64][64][64][3]
     const float *ewaLut;        // MIPFilterLUT[128]
+    const float *noisePerm;     // util/noise.cpp NoisePerm[512] (procedural textures)
     int nProgs;
     int nLuts;                  // images (one 256-entry decode table each)
 };
@@ -559,6 +566,104 @@ PHD void SpectrumImageCoeffs(const TexView &T, const DeviceTexNode &nd, const Te
     }
 }
 
+// ---------------------------------------------------------------- procedural textures
+// TextureMapping3D (PointTransformMapping, textures.h:229-246): the point and its differentials
+// in texture space (the wavefront's contexts carry dpdx = dpdy = 0, workitems.h:288-304)
+PHD V3 XformVector34(const float *m, V3 v) {
+    return V3(m[0] * v.x + m[1] * v.y + m[2] * v.z, m[4] * v.x + m[5] * v.y + m[6] * v.z,
+              m[8] * v.x + m[9] * v.y + m[10] * v.z);
+}
+PHD float SmoothStepF(float x, float a, float b) {  // util/math.h:268-274
+    if (a == b) return (x < a) ? 0.f : 1.f;
+    const float t = Clampf((x - a) / (b - a), 0, 1);
+    return t * t * (3 - 2 * t);
+}
+// the octave count of FBm / Turbulence (util/noise.cpp:116-118): Log2 = log(x) * invLog2
+PHD float NoiseOctaves(V3 dpdx, V3 dpdy, int maxOctaves) {
+    const float len2 = std::fmax(LengthSquared(dpdx), LengthSquared(dpdy));
+    const float n = -1 - (Logf(len2) * 1.442695040888963387f) / 2;
+    return n < 0 ? 0.f : (n > (float)maxOctaves ? (float)maxOctaves : n);
+}
+// FBm (util/noise.cpp:114-131)
+PHD float FBmNoise(const float *perm, V3 p, V3 dpdx, V3 dpdy, float omega, int maxOctaves) {
+    const float n = NoiseOctaves(dpdx, dpdy, maxOctaves);
+    const int nInt = (int)std::floor(n);
+    float sum = 0, lambda = 1, o = 1;
+    for (int i = 0; i < nInt; ++i) {
+        sum += o * Noise3(perm, lambda * p.x, lambda * p.y, lambda * p.z);
+        lambda *= 1.99f;
+        o *= omega;
+    }
+    const float nPartial = n - nInt;
+    sum += o * SmoothStepF(nPartial, .3f, .7f) * Noise3(perm, lambda * p.x, lambda * p.y, lambda * p.z);
+    return sum;
+}
+// Turbulence (util/noise.cpp:133-152)
+PHD float TurbulenceNoise(const float *perm, V3 p, V3 dpdx, V3 dpdy, float omega, int maxOctaves) {
+    const float n = NoiseOctaves(dpdx, dpdy, maxOctaves);
+    const int nInt = (int)std::floor(n);
+    float sum = 0, lambda = 1, o = 1;
+    for (int i = 0; i < nInt; ++i) {
+        sum += o * std::fabs(Noise3(perm, lambda * p.x, lambda * p.y, lambda * p.z));
+        lambda *= 1.99f;
+        o *= omega;
+    }
+    const float nPartial = n - nInt;
+    sum += o * Lerpf(SmoothStepF(nPartial, .3f, .7f), 0.2f,
+                     std::fabs(Noise3(perm, lambda * p.x, lambda * p.y, lambda * p.z)));
+    for (int i = nInt; i < maxOctaves; ++i) {
+        sum += o * 0.2f;
+        o *= omega;
+    }
+    return sum;
+}
+// WindyTexture::Evaluate (textures.h:1125-1130)
+PHD float WindyNoise(const float *perm, V3 p, V3 dpdx, V3 dpdy) {
+    const float windStrength = FBmNoise(perm, .1f * p, .1f * dpdx, .1f * dpdy, .5f, 3);
+    const float waveHeight = FBmNoise(perm, p, dpdx, dpdy, .5f, 6);
+    return std::fabs(windStrength) * waveHeight;
+}
+// InsidePolkaDot (textures.cpp:287-303): Noise(x, y) is Noise(x, y, .5)
+PHD bool InsidePolkaDot(const float *perm, float s, float t) {
+    const int sCell = (int)std::floor(s + .5f), tCell = (int)std::floor(t + .5f);
+    if (Noise3(perm, sCell + .5f, tCell + .5f, .5f) > 0) {
+        const float radius = .35f;
+        const float maxShift = 0.5f - radius;
+        const float sCenter = sCell + maxShift * Noise3(perm, sCell + 1.5f, tCell + 2.8f, .5f);
+        const float tCenter = tCell + maxShift * Noise3(perm, sCell + 4.5f, tCell + 9.8f, .5f);
+        const float ds = s - sCenter, dt = t - tCenter;
+        if (ds * ds + dt * dt < Sqr(radius)) return true;
+    }
+    return false;
+}
+// MarbleTexture::Evaluate's RGB (textures.cpp:524-549): the spline of the marble colours at
+// .5 + .5 sin(p.y + variation FBm), times 1.5.  par = octaves, omega, scale, variation
+PHD void MarbleRGB(const float *perm, V3 p, V3 dpdx, V3 dpdy, int octaves, float omega, float scale,
+                   float variation, float rgb[3]) {
+    p = p * scale;
+    const float marble = p.y + variation * FBmNoise(perm, p, scale * dpdx, scale * dpdy, omega, octaves);
+    float t = .5f + .5f * Sinf(marble);
+    const float colors[9][3] = {{.58f, .58f, .6f}, {.58f, .58f, .6f}, {.58f, .58f, .6f},
+                                {.5f, .5f, .5f},   {.6f, .59f, .58f}, {.58f, .58f, .6f},
+                                {.58f, .58f, .6f}, {.2f, .2f, .33f},  {.58f, .58f, .6f}};
+    const int nSeg = 9 - 3;
+    const int first = std::min((int)std::floor(t * nSeg), nSeg - 1);
+    t = t * nSeg - first;
+    for (int c = 0; c < 3; ++c) {
+        // EvaluateCubicBezier = BlossomCubicBezier(cp, t, t, t) (util/splines.h:18-28)
+        const float *q0 = colors[first], *q1 = colors[first + 1], *q2 = colors[first + 2], *q3 = colors[first + 3];
+        const float a0 = Lerpf(t, q0[c], q1[c]), a1 = Lerpf(t, q1[c], q2[c]), a2 = Lerpf(t, q2[c], q3[c]);
+        const float b0 = Lerpf(t, a0, a1), b1 = Lerpf(t, a1, a2);
+        rgb[c] = 1.5f * Lerpf(t, b0, b1);
+    }
+}
+// a procedural node's texture-space point and differentials (node p[0..11]: textureFromRender)
+PHD void Map3D(const DeviceTexNode &nd, const TexEvalCtx &c, V3 *p, V3 *dpdx, V3 *dpdy) {
+    *p = XformPoint34(nd.p, c.p);
+    *dpdx = XformVector34(nd.p, V3(0, 0, 0));
+    *dpdy = *dpdx;
+}
+
 // ---------------------------------------------------------------- expressions
 PHD void DecodeInstr(const DeviceTexInstr &in, int *op, int *a, int *b, int *c) {
     *op = in.op & 0xff;
@@ -599,6 +704,31 @@ PHD void TexPhase1(const TexView &T, const DeviceTexProgram &pg, const TexEvalCt
             break;
         }
         case kT1SImage: SpectrumImageCoeffs(T, nd, c, R + a); break;
+        case kT1FBm:
+        case kT1Wrinkled:
+        case kT1Windy: {
+            V3 p, dx, dy;
+            Map3D(nd, c, &p, &dx, &dy);
+            R[a] = op == kT1FBm        ? FBmNoise(T.noisePerm, p, dx, dy, nd.p[23], (int)nd.p[22])
+                   : op == kT1Wrinkled ? TurbulenceNoise(T.noisePerm, p, dx, dy, nd.p[23], (int)nd.p[22])
+                                       : WindyNoise(T.noisePerm, p, dx, dy);
+            break;
+        }
+        case kT1DotsW: {
+            const TexCoord2 t = MapST(nd, c);
+            R[a] = InsidePolkaDot(T.noisePerm, t.s, t.t) ? 1.f : 0.f;
+            break;
+        }
+        case kT1FSel: R[a] = R[in.node] != 0 ? R[b] : R[cc]; break;  // Dots: inside ? insideDot : outsideDot
+        case kT1Marble: {
+            V3 p, dx, dy;
+            Map3D(nd, c, &p, &dx, &dy);
+            float rgb[3];
+            MarbleRGB(T.noisePerm, p, dx, dy, (int)nd.p[22], nd.p[23], nd.p[26], nd.p[24], rgb);
+            RGBToCoeffs(T, rgb[0], rgb[1], rgb[2], R + a);  // RGBAlbedoSpectrum(sRGB, rgb)
+            R[a + 3] = 1.f;
+            break;
+        }
         case kT1BilerpW: {
             const TexCoord2 t = MapST(nd, c);
             R[a] = (1 - t.s) * (1 - t.t);
@@ -649,6 +779,12 @@ PHD float TexPhase2(const TexView &T, const DeviceTexProgram &pg, const float *R
             const float t2 = amt != 1 ? st[sp - 1] : 0.f, t1 = amt != 0 ? st[sp - 2] : 0.f;
             --sp;
             st[sp - 1] = amt * t1 + (1 - amt) * t2;
+            break;
+        }
+        case kT2Sel: {  // Dots: the inside child (pushed first) or the outside one
+            const float tOut = st[sp - 1], tIn = st[sp - 2];
+            --sp;
+            st[sp - 1] = R[a] != 0 ? tIn : tOut;
             break;
         }
         case kT2Bilerp: {

@@ -2455,6 +2455,34 @@ int Parser::InstTex(const std::string &name, bool spectrum, int specType, const 
             for (int k = 0; k < 4; ++k) t.fvalue[k] = (float)ps.GetFloat(names[k], defs[k]);
         }
         result = NewTexNode(t);
+    } else if (c == "dots") {
+        // Float/SpectrumDotsTexture::Create (textures.cpp:305-335): a 2D mapping, inside 1 /
+        // outside 0 by default
+        t.kind = kTexDots;
+        TexMapping(ps, renderFromTexture, &t, false);
+        t.child[0] = child("inside", 1.f);
+        t.child[1] = child("outside", 0.f);
+        result = NewTexNode(t);
+    } else if (!spectrum && (c == "fbm" || c == "wrinkled" || c == "windy")) {
+        // FBmTexture / WrinkledTexture / WindyTexture::Create (textures.cpp:343-352, 1008-1032):
+        // a 3D point mapping; octaves 8, roughness 0.5 (windy takes neither)
+        t.kind = c == "fbm" ? kTexFBm : (c == "wrinkled" ? kTexWrinkled : kTexWindy);
+        TexMapping(ps, renderFromTexture, &t, true);
+        if (t.kind != kTexWindy) {
+            t.octaves = ps.GetInt("octaves", 8);
+            t.omega = (float)ps.GetFloat("roughness", .5);
+        }
+        result = NewTexNode(t);
+    } else if (spectrum && c == "marble") {
+        // MarbleTexture::Create (textures.cpp:555-563): octaves 8, roughness .5, scale 1,
+        // variation .2; its RGB is an RGBAlbedoSpectrum whatever the use (textures.cpp:546-552)
+        t.kind = kTexMarble;
+        TexMapping(ps, renderFromTexture, &t, true);
+        t.octaves = ps.GetInt("octaves", 8);
+        t.omega = (float)ps.GetFloat("roughness", .5);
+        t.scale = (float)ps.GetFloat("scale", 1.);
+        t.variation = (float)ps.GetFloat("variation", .2);
+        result = NewTexNode(t);
     } else if (c == "imagemap") {
         // Float/SpectrumImageTexture::Create (textures.cpp:428-521)
         t.kind = kTexImage;

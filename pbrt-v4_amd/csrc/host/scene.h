@@ -124,7 +124,10 @@ struct ImageDesc {
 // the SpectrumType of that use (pbrt keeps one instance per type: scene.cpp CreateTextures).
 enum TexKind : int {
     kTexConstant = 0, kTexScale = 1, kTexMix = 2, kTexDirectionMix = 3, kTexCheckerboard = 4,
-    kTexBilerp = 5, kTexImage = 6
+    kTexBilerp = 5, kTexImage = 6,
+    // procedural (textures.h:427-505, 813-841, 1117-1160): dots (float or spectrum: inside,
+    // outside = child 0, 1), fbm / wrinkled / windy (float), marble (spectrum)
+    kTexDots = 7, kTexFBm = 8, kTexWrinkled = 9, kTexWindy = 10, kTexMarble = 11
 };
 enum TexSpectrumType : int { kSpecAlbedo = 0, kSpecUnbounded = 1, kSpecIlluminant = 2 };
 enum TexMapping : int { kMapUV = 0, kMapSpherical = 1, kMapCylindrical = 2, kMapPlanar = 3, kMap3D = 4 };
@@ -152,8 +155,11 @@ struct TextureDesc {
     float dir[3] = {0, 1, 0};         // directionmix (render space, normalised)
     // image textures
     int image = -1, filter = kMipBilinear;
-    float scale = 1, maxAniso = 8;
+    float scale = 1, maxAniso = 8;  // scale: also marble's "scale"
     bool invert = false;
+    // fbm / wrinkled / marble: "octaves", "roughness" (omega); marble "variation"
+    int octaves = 8;
+    float omega = .5f, variation = .2f;
 };
 
 // A texture expression compiled for the device (core.h TexEval*): phase 1 runs once per hit

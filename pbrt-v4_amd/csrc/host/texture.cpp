@@ -730,6 +730,17 @@ struct TexCompiler {
             Emit1(kT1FScale, r, a, b, -1);
             return r;
         }
+        case kTexFBm: r = NewReg(); Emit1(kT1FBm, r, 0, 0, node); return r;
+        case kTexWrinkled: r = NewReg(); Emit1(kT1Wrinkled, r, 0, 0, node); return r;
+        case kTexWindy: r = NewReg(); Emit1(kT1Windy, r, 0, 0, node); return r;
+        case kTexDots: {
+            const int w = NewReg();
+            Emit1(kT1DotsW, w, 0, 0, node);
+            const int a = F(t.child[0]), b = F(t.child[1]);
+            r = NewReg();
+            Emit1(kT1FSel, r, a, b, w);
+            return r;
+        }
         }
         throw Error("internal: unknown texture kind");
     }
@@ -778,6 +789,20 @@ struct TexCompiler {
             Emit1(kT1BilerpW, w, 0, 0, node);
             for (int k = 0; k < 4; ++k) Emit2(kT2Const, k, 0, node, 1);
             Emit2(kT2Bilerp, w, 0, -1, -3);
+            return;
+        }
+        case kTexDots: {
+            const int w = NewReg();
+            Emit1(kT1DotsW, w, 0, 0, node);
+            S(t.child[0]);
+            S(t.child[1]);
+            Emit2(kT2Sel, w, 0, -1, -1);
+            return;
+        }
+        case kTexMarble: {
+            const int r = NewReg(4);
+            Emit1(kT1Marble, r, 0, 0, node);
+            Emit2(kT2RGBReg, r, 0, -1, 1);
             return;
         }
         }

@@ -105,6 +105,7 @@ class SceneFlat(ctypes.Structure):
         ("strat_xsamples", ctypes.c_int), ("strat_ysamples", ctypes.c_int), ("strat_jitter", ctypes.c_int),
         ("sobol_log2_scale", ctypes.c_int), ("sobol_matrices32", ctypes.POINTER(ctypes.c_uint32)),
         ("vdc_sobol", ctypes.POINTER(ctypes.c_uint64)), ("vdc_sobol_inv", ctypes.POINTER(ctypes.c_uint64)),
+        ("noise_perm", ctypes.POINTER(ctypes.c_float)),
     ]
 
 
@@ -133,7 +134,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_context_free", "pbrt_render", "pbrt_synchronize", "pbrt_get_stats", "pbrt_reset_stats",
     "pbrt_film_clear", "pbrt_film_device_ptr", "pbrt_film_read", "pbrt_film_get_rgb", "pbrt_intersect",
     "pbrt_debug_halton", "pbrt_debug_halton_fastpath_mismatches", "pbrt_debug_check_rn_math", "pbrt_debug_rgb_coeffs", "pbrt_debug_rgb2spec_column", "pbrt_debug_kernel_sections",
-    "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_sampler", "pbrt_debug_rng", "pbrt_debug_det_math", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
+    "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_sampler", "pbrt_debug_rng", "pbrt_debug_det_math", "pbrt_debug_procedural", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
     "pbrt_debug_named_spectrum", "pbrt_debug_bxdf", "pbrt_debug_layered", "pbrt_debug_triangle_shading", "pbrt_film_write_image",
     "pbrt_image_read_size", "pbrt_image_read", "pbrt_image_write", "pbrt_image_error", "pbrt_debug_filter_sample",
     "pbrt_debug_bvh_stats", "pbrt_debug_light_bvh", "pbrt_intersect_tr", "pbrt_image_flip", "pbrt_set_kernel_profiling", "pbrt_get_kernel_stats",
@@ -208,6 +209,7 @@ def _lib():
     lib.pbrt_debug_sampler.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_int, c.POINTER(c.c_float)]
     lib.pbrt_debug_rng.argtypes = [c.c_uint64, c.c_uint64, c.POINTER(c.c_uint32)]
     lib.pbrt_debug_det_math.argtypes = [c.c_int, c.c_int, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
+    lib.pbrt_debug_procedural.argtypes = [c.c_int, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_debug_queue_counts.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_int]
     lib.pbrt_debug_trowbridge.argtypes = [c.c_void_p, c.c_void_p]
     lib.pbrt_debug_fresnel.argtypes = [c.c_void_p, c.c_void_p]
@@ -476,6 +478,16 @@ def det_math(fn, a, b=None, device=-1):
     out = np.zeros_like(a)
     _check(_lib().pbrt_debug_det_math(device, DET_MATH_FNS.index(fn), a.ctypes.data, b.ctypes.data, len(a),
                                       out.ctypes.data))
+    return out
+
+
+def procedural(kind, params4, in9):
+    """The procedural textures' code on the host (pbrt_debug_procedural): kind 0 fbm, 1
+    turbulence, 2 windy, 3 polka dot, 4 marble; in9 rows = p, dpdx, dpdy; [n][6] out."""
+    par = np.ascontiguousarray(params4, np.float32)
+    x = np.ascontiguousarray(in9, np.float32).reshape(-1, 9)
+    out = np.zeros((len(x), 6), np.float32)
+    _check(_lib().pbrt_debug_procedural(kind, par.ctypes.data, x.ctypes.data, len(x), out.ctypes.data))
     return out
 
 

@@ -65,7 +65,8 @@ def test_textured_media_scene_renders_on_the_oracle(pa, oracle, tmp_path):
 
 MIX = """MakeNamedMaterial "a" "string type" "diffuse" "rgb reflectance" [0.7 0.3 0.2]
 MakeNamedMaterial "b" "string type" "conductor" "float roughness" 0.15
-Material "mix" "string materials" ["a" "b"] "texture amount" "rough"
+Texture "amt" "float" "imagemap" "string filename" "normals.png"
+Material "mix" "string materials" ["a" "b"] "texture amount" "amt"
 Shape "trianglemesh" "integer indices" [0 1 2 0 2 3] "point3 P" [-1 0.01 -2.5 1 0.01 -2.5 1 0.01 -1.6 -1 0.01 -1.6]
     "point2 uv" [0 0 1 0 1 1 0 1]
 Material "mix" "string materials" ["a" "b"] "float amount" 0.4

@@ -5777,6 +5777,15 @@ int oracle_intersect_tr(const pbrt_scene_flat *flat, const pbrt_scene_info *info
                         const int32_t *medium, const float *lambda0, int n, float *out) {
     Renderer r;
     r.f = flat;
+    // Scene setup is host work in the product (BVH, light BVH cones, filter tables, pyramids,
+    // environment distributions: libm on the host), so in device-math mode it runs with libm
+    // and only the per-sample work uses the device's polynomials.
+    struct HostMath {
+        int mode = g_mathMode;
+        HostMath() { if (mode == 2) g_mathMode = 0; }
+        void Done() { g_mathMode = mode; }
+        ~HostMath() { Done(); }
+    } hostMath;
     r.S.Init(flat, info);
     if (flat->n_tex_nodes > 0 && (!g_rgbTable || !g_ewaLut)) return -2;  // oracle_set_rgb_table first
     r.tex.Init(flat, info->spp, info->xres, info->yres);
@@ -5816,6 +5825,15 @@ static int RenderRows(const pbrt_scene_flat *flat, const pbrt_scene_info *info, 
                       int firstSample, int nSamples, int uniformLightSampler, int threads, double *film, bool path) {
     Renderer r;
     r.f = flat;
+    // Scene setup is host work in the product (BVH, light BVH cones, filter tables, pyramids,
+    // environment distributions: libm on the host), so in device-math mode it runs with libm
+    // and only the per-sample work uses the device's polynomials.
+    struct HostMath {
+        int mode = g_mathMode;
+        HostMath() { if (mode == 2) g_mathMode = 0; }
+        void Done() { g_mathMode = mode; }
+        ~HostMath() { Done(); }
+    } hostMath;
     r.S.Init(flat, info);
     if (flat->n_tex_nodes > 0 && (!g_rgbTable || !g_ewaLut)) return -2;  // oracle_set_rgb_table first
     r.tex.Init(flat, info->spp, info->xres, info->yres);
@@ -5828,6 +5846,7 @@ static int RenderRows(const pbrt_scene_flat *flat, const pbrt_scene_info *info, 
     r.M.f = flat;
     r.M.n = flat->n_media;
     r.filt.Init(flat->filter_type, info->filter_radius_x, info->filter_radius_y, flat->filter_a, flat->filter_b);
+    hostMath.Done();
     size_t npix = (size_t)info->xres * info->yres;
     std::atomic<int> next(0);
     auto work = [&]() {

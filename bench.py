@@ -238,14 +238,15 @@ def pmc_traffic(workload):
 
 def compute_ceiling(workload):
     """The closest-hit kernel's compute roof from the same PMC record: VALU issue as a fraction
-    of every SIMD's cycles (4 x SQ_ACTIVE_INST_VALU quad-cycles / (1024 SIMDs x GRBM_GUI_ACTIVE / 8
-    XCDs), the gfx9 VALUBusy formula with gfx950's XCD-summed GRBM), and per wave (SQ_ACTIVE_INST_VALU
-    / SQ_WAVE_CYCLES).  With the tree in LDS (C2) this, not HBM, is the binding roof."""
+    of every SIMD's cycles, 2 cycles x SQ_INSTS_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs)
+    (a wave64 fp32 VALU instruction holds its SIMD 2 cycles at full rate: a lower bound), and per
+    wave SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES and SQ_WAIT_ANY / SQ_WAVE_CYCLES.  With the tree in
+    LDS (C2) this, not HBM, is the binding roof."""
     pat = f"r*_{workload}_closest_pmc.json"
     rec = latest_profile(pat)
     if not rec or rec.get("valu_busy") is None:
         return None
-    return {"bound": "valu", "valu_busy": rec["valu_busy"], "valu_active_per_wave": rec.get("valu_active_per_wave"),
+    return {"bound": "valu", "frac": rec["valu_busy"], "valu_active_per_wave": rec.get("valu_active_per_wave"),
             "waiting_per_wave": rec.get("wait_any_per_wave"), "measured_on": rec.get("head", "unknown"),
             "source": "profiles/" + sorted((ROOT / "profiles").glob(pat))[-1].name}
 

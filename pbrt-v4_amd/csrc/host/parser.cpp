@@ -1635,7 +1635,20 @@ void Parser::Finish() {
         ParamSet &ps = pm.params;
         MediumDesc m;
         m.name = pm.name;
-        if (ps.Find("preset")) throw Error(ps.loc + ": medium \"preset\" is not supported yet");
+        // HomogeneousMedium::Create's "preset" (media.cpp:170-186, GetMediumScatteringProperties):
+        // sigma_a and sigma_s from the named measurement (RGBUnboundedSpectrum of sRGB), else a
+        // warning and the parameters; the other media have no "preset" parameter
+        const std::string preset = ps.GetString("preset", "");
+        const std::array<float, 6> *presetVals = nullptr;
+        if (!preset.empty()) {
+            if (pm.type != "homogeneous")
+                throw Error(ps.loc + ": \"string preset\": unused parameter (only homogeneous media take a preset)");
+            auto it = GetSpectralData().mediumPresets.find(preset);
+            if (it == GetSpectralData().mediumPresets.end())
+                std::fprintf(stderr, "%s: Warning: Material preset \"%s\" not found.\n", ps.loc.c_str(), preset.c_str());
+            else
+                presetVals = &it->second;
+        }
         if (pm.type == "cloud") {
             // CloudMedium::Create (media.cpp:462-484): no scale or Le; sigma_a / sigma_s default 1
             m.type = kMediumCloud;
@@ -1690,8 +1703,14 @@ void Parser::Finish() {
             scene.denseSpectra.push_back(d);
             return (int)scene.denseSpectra.size() - 1;
         };
-        m.sigmaA = addDense(MediumSpectrum(ps, "sigma_a", false, 1.f, &given, nullptr), scale);
-        m.sigmaS = addDense(MediumSpectrum(ps, "sigma_s", false, 1.f, &given, nullptr), scale);
+        if (presetVals) {
+            const std::array<float, 6> &pv = *presetVals;
+            m.sigmaA = addDense(DenseRGBUnbounded(pv[3], pv[4], pv[5]), scale);
+            m.sigmaS = addDense(DenseRGBUnbounded(pv[0], pv[1], pv[2]), scale);
+        } else {
+            m.sigmaA = addDense(MediumSpectrum(ps, "sigma_a", false, 1.f, &given, nullptr), scale);
+            m.sigmaS = addDense(MediumSpectrum(ps, "sigma_s", false, 1.f, &given, nullptr), scale);
+        }
         m.g = (float)ps.GetFloat("g", 0);
         float photometric = 1;
         std::array<float, 311> Le = MediumSpectrum(ps, "Le", true, 0.f, &given, &photometric);
@@ -2027,9 +2046,25 @@ InfiniteLightDesc Parser::InfiniteLight(PendingLight &l) {
     scene.denseSpectra.push_back(GetSpectralData().denseD65);
     il.spectrum = (int)scene.denseSpectra.size() - 1;
     scale /= GetSpectralData().photometricD65;
-    // the upper-hemisphere illuminance normalisation (lights.cpp:1651-1679) needs the colour
-    // space's luminance vector; not restated yet
-    if (E_v > 0) throw Error(ps.loc + ": \"illuminance\" for image infinite lights is not supported yet");
+    if (E_v > 0) {
+        // the upper hemisphere's illuminance of the map (lights.cpp:1651-1679): pixel centres
+        // through EqualAreaSquareToSphere, luminance-weighted, cosine-weighted; scale *= E_v / it
+        const double(*xr)[3] = GetSpectralData().xyzFromRGB;
+        const float lum[3] = {(float)xr[1][0], (float)xr[1][1], (float)xr[1][2]};
+        float illuminance = 0;
+        for (int y = 0; y < env.res; ++y) {
+            const float v = (float(y) + 0.5f) / float(env.res);
+            for (int x = 0; x < env.res; ++x) {
+                const float u = (x + 0.5f) / env.res;
+                const V3 w = EqualAreaSquareToSphere(u, v);
+                if (w.z <= 0) continue;
+                const float *c = &env.rgb[((size_t)y * env.res + x) * 3];
+                for (int k = 0; k < 3; ++k) illuminance += c[k] * lum[k] * w.z;
+            }
+        }
+        illuminance *= 2 * kPi / (env.res * env.res);
+        scale *= E_v / illuminance;
+    }
     il.scale = scale;
     const Mat4 rfl = Mul(scene.camera.renderFromWorld, l.worldFromLight);
     const Mat4 lfr = Inverse4(rfl);
@@ -2102,9 +2137,32 @@ void Parser::ImageLight(PendingLight &l, const Mat4 &rfl, float sc, DeltaLightDe
         d->type = kDeltaProjection;
         if (im.nc < 3)
             throw Error(ps.loc + ": " + fn + ": Image provided to \"projection\" light must have R, G, and B channels.");
-        if (phi_v > 0) throw Error(ps.loc + ": \"power\" for projection lights is not supported yet");
         const float fov = (float)ps.GetFloat("fov", 90.);
         d->invTanAng = 1 / std::tan((kPi / 180) * fov / 2);
+        if (phi_v > 0) {
+            // ProjectionLight::Create's power (lights.cpp:479-511): the image's luminance over
+            // the screen window, each pixel weighted by dw/dA = cos^3 of its direction (the
+            // direction lightFromScreen gives a screen point is (x / invTan, y / invTan, 1)
+            // normalised, evaluated here in double)
+            const double(*xr)[3] = GetSpectralData().xyzFromRGB;
+            const float lum[3] = {(float)xr[1][0], (float)xr[1][1], (float)xr[1][2]};
+            const float aspect = float(im.w) / float(im.h);
+            const float x0 = aspect > 1 ? -aspect : -1, x1 = -x0, y0 = aspect > 1 ? -1 : -1 / aspect, y1 = -y0;
+            const float opposite = std::tan((kPi / 180) * fov / 2);
+            const float A = 4 * Sqr(opposite) * (aspect > 1 ? aspect : (1 / aspect));
+            float sum = 0;
+            for (int y = 0; y < im.h; ++y)
+                for (int x = 0; x < im.w; ++x) {
+                    const float tx = (x + .5f) / im.w, ty = (y + .5f) / im.h;
+                    const double sx = (1 - tx) * x0 + tx * x1, sy = (1 - ty) * y0 + ty * y1;
+                    const double wx = sx / d->invTanAng, wy = sy / d->invTanAng;
+                    const float wz = (float)(1 / std::sqrt(wx * wx + wy * wy + 1));
+                    const float dwdA = wz * wz * wz;
+                    const float *c = &im.v[((size_t)y * im.w + x) * im.nc];
+                    for (int k = 0; k < 3; ++k) sum += c[k] * lum[k] * dwdA;
+                }
+            sc *= phi_v / (A * sum / (float)np);
+        }
         d->img.resize(3 * np);
         float sum = 0;
         for (size_t q = 0; q < np; ++q) {

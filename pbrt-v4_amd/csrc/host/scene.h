@@ -400,12 +400,15 @@ struct SpectralData {
     std::array<float, 311> denseX, denseY, denseZ, denseD65;  // 395..705
     float photometricD65 = 0;                                  // SpectrumToPhotometric(D65)
     double rgbFromXYZ[3][3];
+    double xyzFromRGB[3][3];  // sRGB; row 1 = RGBColorSpace::LuminanceVector (colorspace.h:51-53)
     std::array<float, 256> srgbToLinear;  // SRGBToLinearLUT (util/color.cpp:286)
     std::array<float, 128> mipFilterLUT;  // MIPFilterLUT (util/mipmap.cpp:59-191)
     std::map<std::string, std::vector<float>> sensors;  // "<camera>_r|g|b" interleaved curves
     std::vector<float> cieSLambda, cieS0, cieS1, cieS2;  // CIE daylight basis (Spectra::D)
     std::vector<float> noisePerm;                        // util/noise.cpp NoisePerm[512]
     std::vector<std::vector<float>> swatches;           // 24 ColorChecker reflectances (film.cpp)
+    // GetMediumScatteringProperties presets (media.cpp:74-151): sigma_prime_s RGB, sigma_a RGB
+    std::map<std::string, std::array<float, 6>> mediumPresets;
 };
 // PixelSensor (film.h:36-116, PixelSensor::Create film.cpp:222-262): the sensor's r/g/b matching
 // curves densely sampled over 395..705 nm and XYZFromSensorRGB -- the CIE 1931 curves with an

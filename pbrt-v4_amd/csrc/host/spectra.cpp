@@ -100,6 +100,16 @@ static SpectralData LoadSpectralData() {
         else if (name == "CIE_S1") tof(d.cieS1);
         else if (name == "CIE_S2") tof(d.cieS2);
         else if (name == "NoisePerm") tof(d.noisePerm);
+        else if (name.rfind("mediumpreset:", 0) == 0) {
+            std::vector<float> v;
+            tof(v);
+            if (v.size() != 6) throw Error("malformed medium preset " + name + " in " + path);
+            std::string n = name.substr(13);
+            std::replace(n.begin(), n.end(), '_', ' ');
+            std::array<float, 6> a;
+            std::copy(v.begin(), v.end(), a.begin());
+            d.mediumPresets[n] = a;
+        }
     }
     if (d.cieX.size() != 471 || d.optX.size() != 95) throw Error("malformed spectral data " + path);
     if (!haveMipLUT || !haveSrgbLUT)
@@ -182,6 +192,8 @@ static SpectralData LoadSpectralData() {
         for (int i = 0; i < 3; ++i)
             for (int j = 0; j < 3; ++j) xyzFromRGB[i][j] = rgb[i][j] * C[j];
         Invert3(xyzFromRGB, d.rgbFromXYZ);
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) d.xyzFromRGB[i][j] = xyzFromRGB[i][j];
     }
     return d;
 }

@@ -144,7 +144,6 @@ def test_env_loader_errors(pa, tmp_path):
         ('"string filename" "grey.png"', "must have R, G, and B channels"),
         ('"string filename" "missing.exr"', "unable to open|No such file|cannot open"),
         ('"string filename" "rect.pfm" "rgb L" [1 1 1]', "Can't specify both"),
-        ('"string filename" "ok.pfm" "float illuminance" 3', "illuminance"),
         ('"point3 portal" [0 0 0 1 0 0 1 1 0 0 1 0]', "portal"),
     ]
     for params, msg in cases:
@@ -161,6 +160,38 @@ def test_uniform_infinite_light_illuminance(pa):
     b = pa.Scene.from_string(SCENE.replace('LightSource "infinite" "string filename" "textures/{fn}" "float scale" 0.7',
                                            base + ' "float illuminance" 2.5'), SCENES).flat()
     assert b.inf_scale[0] == np.float32(np.float32(a.inf_scale[0]) * np.float32(np.float32(2.5) / np.float32(np.pi)))
+
+
+def test_image_infinite_light_illuminance(pa, tmp_path):
+    """ImageInfiniteLight "illuminance" (lights.cpp:1651-1679): scale *= E_v / (the map's
+    upper-hemisphere illuminance).  The reference sums the equal-area pixels above the horizon
+    with the weight 2 pi / (w h) rather than the pixel solid angle 4 pi / (w h), so a constant map
+    c measures c pi / 2 (half the cosine integral pi c) and its scale is 2 E_v / pi / c to the
+    discretisation -- the reference's own normalisation, kept; the sky map's scale follows the
+    same formula restated here in float64."""
+    _write_pfm(tmp_path / "c.pfm", np.full((64, 64, 3), 0.5, np.float32))
+    line = 'LightSource "infinite" "string filename" "textures/{fn}" "float scale" 0.7'
+    plain = pa.Scene.from_string(SCENE.replace(line, 'LightSource "infinite" "string filename" "c.pfm"'), tmp_path).flat()
+    lit = pa.Scene.from_string(SCENE.replace(line, 'LightSource "infinite" "string filename" "c.pfm" '
+                                                   '"float illuminance" 3'), tmp_path).flat()
+    ratio = lit.inf_scale[0] / plain.inf_scale[0]
+    assert ratio == pytest.approx(2 * 3 / np.pi / 0.5, rel=2e-3)
+    # the sky map: the formula in float64 over the loader's own pixels, with the sRGB luminance
+    # vector (XYZFromRGB row 1) and EqualAreaSquareToSphere's z (1 - r^2, r = 1 - |1 - |2u - 1| - |2v - 1||
+    # at the pixel centre, signed by the inner square: util/math.cpp:292-330)
+    sky = pa.Scene.from_string(SCENE.format(fn="env_sky.pfm"), SCENES)
+    sky_lit = pa.Scene.from_string(SCENE.format(fn="env_sky.pfm").replace('"float scale" 0.7',
+                                                                           '"float scale" 0.7 "float illuminance" 2'), SCENES)
+    f = sky.flat()
+    res = f.env_info[0]
+    rgb = np.ctypeslib.as_array(f.env_rgb, shape=(res * res * 3,)).reshape(res, res, 3).astype(np.float64)
+    c = (np.arange(res) + 0.5) / res
+    u, v = np.meshgrid(c, c)
+    r = 1 - np.abs(np.abs(2 * u - 1) + np.abs(2 * v - 1) - 1)
+    z = np.where(np.abs(2 * u - 1) + np.abs(2 * v - 1) <= 1, 1 - r * r, -(1 - r * r))
+    lum = np.array([0.212639, 0.715169, 0.072192])
+    ill = (rgb @ lum * np.where(z > 0, z, 0)).sum() * 2 * np.pi / (res * res)
+    assert sky_lit.flat().inf_scale[0] / f.inf_scale[0] == pytest.approx(2.0 / ill, rel=1e-4)
 
 
 @pytest.mark.gpu

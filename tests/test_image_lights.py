@@ -61,7 +61,6 @@ def test_goniometric_loader(pa, tmp_path):
     ('LightSource "goniometric" "string filename" "rect.png"\n', "non-square"),
     ('LightSource "projection" "float fov" 40\n', "Must provide \"filename\""),
     ('LightSource "projection" "string filename" "grey.png"\n', "must have R, G, and B"),
-    ('LightSource "projection" "string filename" "rgb.png" "float power" 10\n', "not supported yet"),
 ])
 def test_image_light_errors(pa, tmp_path, light, msg):
     png(tmp_path / "rect.png", np.full((4, 8), 200))
@@ -145,3 +144,30 @@ def test_image_light_gpu_matches_oracle(pa, oracle, tmp_path, kind):
     film, _ = gpu_film(pa, sc)
     frac, mean_rel = check_parity(to_rgb(oracle, sc, film), to_rgb(oracle, sc, oracle.render(sc, threads=16)))
     print(f"{kind} light parity: {frac*100:.3f}% pixels within 1e-3, mean rel {mean_rel:.2e}")
+
+
+def test_projection_power_known_answer(pa, oracle, tmp_path):
+    """ProjectionLight "power" (lights.cpp:479-511): scale = power / (A * the image's mean
+    luminance weighted by dw/dA = cos^3): for a white image the light emits its power into the
+    frustum, so doubling "power" doubles the scale, and the scale matches that integral
+    evaluated here in float64 (sRGB luminance vector; 8-bit 255 = 1 after the sRGB decode)."""
+    png(tmp_path / "w.png", np.full((6, 8, 3), 255))
+    base = 'LightSource "projection" "string filename" "w.png" "float fov" 50'
+
+    def scale(extra):
+        sc = scene(pa, tmp_path, base + extra + "\n")
+        f = sc.flat()
+        return np.ctypeslib.as_array(f.delta_lights, shape=(f.n_delta_lights * 24,)).reshape(-1, 24)[0, 2]
+
+    s0, s1, s2 = scale(""), scale(' "float power" 10'), scale(' "float power" 20')
+    assert s2 / s1 == pytest.approx(2, rel=1e-6)
+    w, h, fov = 8, 6, 50.0
+    aspect = w / h
+    inv_tan = 1 / np.tan(np.radians(fov) / 2)
+    xs = -aspect + 2 * aspect * (np.arange(w) + 0.5) / w
+    ys = -1 + 2 * (np.arange(h) + 0.5) / h
+    X, Y = np.meshgrid(xs / inv_tan, ys / inv_tan)
+    dwdA = (1 / np.sqrt(X * X + Y * Y + 1)) ** 3
+    A = 4 * np.tan(np.radians(fov) / 2) ** 2 * aspect
+    k_e = A * dwdA.mean() * 1.0  # luminance of white = 1
+    assert s1 / s0 == pytest.approx(10 / k_e, rel=1e-4)

@@ -62,7 +62,6 @@ def test_loader_media_tables(pa):
 
 @pytest.mark.parametrize("bad,msg", [
     ('MakeNamedMedium "m" "string type" "nanovdb"', "not supported"),
-    ('MakeNamedMedium "m" "string type" "homogeneous" "string preset" "Skin1"', "preset"),
     ('MakeNamedMedium "m" "string type" "uniformgrid" "integer nx" 2', "density"),
     ('MakeNamedMedium "q" "string type" "homogeneous"', "undefined"),
 ])
@@ -122,3 +121,32 @@ def test_oracle_c5_small_plausible(pa, oracle):
     img, sc = render(pa, oracle, c5_small_text())
     assert sc.flat().camera_medium >= 0
     assert np.isfinite(img).all() and img.min() >= 0 and img.mean() > 0.01
+
+
+def test_medium_preset_equals_its_rgb(pa):
+    """HomogeneousMedium "preset" (media.cpp:170-186): GetMediumScatteringProperties' measured
+    sigma_a / sigma'_s (mm^-1, media.cpp:74-151) as RGBUnboundedSpectrum -- the same dense
+    spectra as writing them as "rgb sigma_a" / "rgb sigma_s"; "scale" applies to both."""
+    def dense(line):
+        sc = pa.Scene.from_string(medium_scene(line, res=8, spp=1), SCENES)
+        f = sc.flat()
+        info = np.ctypeslib.as_array(f.medium_info, shape=(f.n_media * 16,)).reshape(-1, 16)
+        d = np.ctypeslib.as_array(f.dense_spectra, shape=(f.n_spectra * 311,)).reshape(-1, 311)
+        return d[info[0, 1]].copy(), d[info[0, 2]].copy()
+    a = dense('MakeNamedMedium "m" "string type" "homogeneous" "string preset" "Skin1" "float scale" 2')
+    b = dense('MakeNamedMedium "m" "string type" "homogeneous" "rgb sigma_a" [0.032 0.17 0.48] '
+              '"rgb sigma_s" [0.74 0.88 1.01] "float scale" 2')
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    c = dense('MakeNamedMedium "m" "string type" "homogeneous" "string preset" "Regular Milk"')
+    assert c[1].mean() > 4 and c[0].max() < 0.05
+    # an unknown preset warns and keeps the parameters (pbrt's Warning, not an error)
+    u = dense('MakeNamedMedium "m" "string type" "homogeneous" "string preset" "Nope" "rgb sigma_a" [0.032 0.17 0.48] '
+              '"rgb sigma_s" [0.74 0.88 1.01] "float scale" 2')
+    np.testing.assert_array_equal(u[0], b[0])
+
+
+def test_medium_preset_only_on_homogeneous(pa):
+    with pytest.raises(pa.PbrtError, match="preset"):
+        pa.Scene.from_string(medium_scene('MakeNamedMedium "m" "string type" "uniformgrid" "string preset" "Skin1" '
+                                          '"float density" [1]', res=8, spp=1), SCENES)

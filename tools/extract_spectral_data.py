@@ -132,6 +132,15 @@ def main():
     body = re.sub(r"//[^\n]*", "", body)
     data["NoisePerm"] = numbers(body)
     assert len(data["NoisePerm"]) == 512, len(data["NoisePerm"])
+    # medium scattering presets (GetMediumScatteringProperties' SubsurfaceParameterTable,
+    # media.cpp:74-151): name -> sigma_prime_s RGB, sigma_a RGB in mm^-1 (spaces in names as "_")
+    media = (REF / "media.cpp").read_text()
+    m = re.search(r"static MeasuredSS SubsurfaceParameterTable\[\] = \{", media)
+    body = media[m.end():media.index("};", m.end())]
+    presets = re.findall(r'\{"([^"]+)",\s*RGB\(([^)]*)\),\s*RGB\(([^)]*)\)\}', body)
+    assert len(presets) == 47, len(presets)
+    for name, sps, sa in presets:
+        data["mediumpreset:" + name.replace(" ", "_")] = numbers(sps) + numbers(sa)
     OUT.parent.mkdir(parents=True, exist_ok=True)
     OUT.write_text(json.dumps(data))
     print("wrote", OUT, {k: len(v) if isinstance(v, list) else v for k, v in data.items()})

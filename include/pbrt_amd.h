@@ -115,12 +115,14 @@ typedef struct pbrt_scene_flat {
     const uint8_t *tri_shading;       /* [n_triangles] */
     /* participating media (HomogeneousMedium / GridMedium); index -1 = vacuum */
     int n_media, camera_medium;
-    const int32_t *medium_info;       /* [n_media][16]: type (0 homogeneous, 1 grid), sigma_a,
-                                         sigma_s, Le (dense_spectra indices, pbrt's scales
-                                         applied), emissive, nx, ny, nz, lnx, lny, lnz,
-                                         density offset, LeScale offset, majorant offset (into
-                                         medium_values), grey (sigma_a and sigma_s
-                                         constant over wavelength), 0 */
+    const int32_t *medium_info;       /* [n_media][16]: type (0 homogeneous, 1 grid, 2 cloud,
+                                         3 rgbgrid), sigma_a, sigma_s, Le (dense_spectra
+                                         indices, pbrt's scales applied), emissive, nx, ny, nz,
+                                         lnx, lny, lnz, density offset, LeScale offset,
+                                         majorant offset (into medium_values), grey (sigma_a and
+                                         sigma_s constant over wavelength); last: grid: offset
+                                         of {temperatureoffset, temperaturescale, T[nz][ny][nx]}
+                                         or -1, rgbgrid: bit k = block k given, else 0 */
     const float *medium_params;       /* [n_media][24]: g, bounds p0 xyz, p1 xyz, 0,
                                          mediumFromRender 4x4 row-major */
     const float *medium_values;       /* density / LeScale / 16^3 majorant grids */

@@ -3025,6 +3025,21 @@ static Float FastExp(Float x) {
     return BitsToFloat(bits);
 }
 
+// Blackbody (util/spectrum.h:69-80) and BlackbodySpectrum::Sample (util/spectrum.h:530-560):
+// Planck's law over its value at Wien's peak lambda_max = 2.8977721e-3 / T
+static Float Blackbody(Float lambda, Float T) {
+    if (T <= 0) return 0;
+    const Float c = 299792458.f, h = 6.62606957e-34f, kb = 1.3806488e-23f;
+    const Float l = lambda * 1e-9f;
+    const Float l5 = (l * l) * (l * l) * l;  // Pow<5>
+    return (2 * h * c * c) / (l5 * (FastExp((h * c) / (l * kb * T)) - 1));
+}
+static Float BlackbodySample(Float lambda, Float T) {
+    const Float lambdaMax = 2.8977721e-3f / T;
+    const Float normalizationFactor = 1 / Blackbody(lambdaMax * 1e9f, T);
+    return Blackbody(lambda, T) * normalizationFactor;
+}
+
 static Float HenyeyGreenstein(Float cosTheta, Float g) {
     g = Clamp(g, -.99f, .99f);
     Float denom = 1 + Sqr(g) + 2 * g * cosTheta;
@@ -3478,7 +3493,18 @@ struct Media {
         mp.sigma_s = mp.sigma_s * d;
         if (I[4]) {
             Float scale = GridLookup(f->medium_values + I[12], I[8], I[9], I[10], q);
-            if (scale > 0) mp.Le = Dense(I[3], lambda) * scale;
+            if (scale > 0) {
+                if (I[15] >= 0) {
+                    // temperature grid (media.h:303-311): values[I[15]] = {offset, scale}, then
+                    // the [nz][ny][nx] temperatures
+                    const float *tg = f->medium_values + I[15];
+                    Float temp = GridLookup(tg + 2, I[5], I[6], I[7], q);
+                    temp = (temp - tg[0]) * tg[1];
+                    if (temp > 100.f)
+                        for (int i = 0; i < NS; ++i) mp.Le[i] = scale * BlackbodySample(lambda.lambda[i], temp);
+                } else
+                    mp.Le = Dense(I[3], lambda) * scale;
+            }
         }
         return mp;
     }

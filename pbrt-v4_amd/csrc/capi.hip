@@ -78,15 +78,24 @@ static void MediumTables(const SceneDesc &s, std::vector<int32_t> *info, std::ve
         values->insert(values->end(), m.LeScale.begin(), m.LeScale.end());
         const int mOff = (int)values->size();
         values->insert(values->end(), m.majorant.begin(), m.majorant.end());
+        // GridMedium temperature: {offset, scale, T[nz][ny][nx]} at info[15] (-1: none)
+        int tOff = -1;
+        if (!m.temperature.empty()) {
+            tOff = (int)values->size();
+            values->push_back(m.temperatureOffset);
+            values->push_back(m.temperatureScale);
+            values->insert(values->end(), m.temperature.begin(), m.temperature.end());
+        }
         // grey: sigma_a and sigma_s are the same at every wavelength, so every SampledSpectrum
         // built from them (T_maj, sigma_n, ...) has 31 equal entries (the kernels' scalar path)
         auto flat = [&](int idx) {
             const auto &d = s.denseSpectra[idx];
             return std::all_of(d.begin(), d.end(), [&](float v) { return v == d[0]; });
         };
-        const int grey = m.type != kMediumRGBGrid && flat(m.sigmaA) && flat(m.sigmaS) ? 1 : 0;
+        // (a temperature grid's Le is a blackbody per point: the spectral kernels evaluate it)
+        const int grey = m.type != kMediumRGBGrid && tOff < 0 && flat(m.sigmaA) && flat(m.sigmaS) ? 1 : 0;
         info->insert(info->end(), {m.type, m.sigmaA, m.sigmaS, m.Le, m.emissive ? 1 : 0, m.nx, m.ny, m.nz, m.lnx, m.lny,
-                                   m.lnz, dOff, lOff, mOff, grey, m.rgbGrids});
+                                   m.lnz, dOff, lOff, mOff, grey, m.type == kMediumGrid ? tOff : m.rgbGrids});
         const V3 lo(std::min(m.p0.x, m.p1.x), std::min(m.p0.y, m.p1.y), std::min(m.p0.z, m.p1.z));
         const V3 hi(std::max(m.p0.x, m.p1.x), std::max(m.p0.y, m.p1.y), std::max(m.p0.z, m.p1.z));
         params->insert(params->end(), {m.g, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, m.sigmaScale});
@@ -985,7 +994,8 @@ static void BuildDevice(pbrt_context *c) {
         const auto &a = s.denseSpectra[s.media[m].sigmaA], &b = s.denseSpectra[s.media[m].sigmaS];
         if (!std::all_of(a.begin(), a.end(), [&](float x) { return x == a[0]; }) ||
             !std::all_of(b.begin(), b.end(), [&](float x) { return x == b[0]; }) ||
-            s.media[m].type == kMediumRGBGrid)  // spectra per voxel (its dense sigma_a / sigma_s are 1 / 0)
+            s.media[m].type == kMediumRGBGrid ||  // spectra per voxel (its dense sigma_a / sigma_s are 1 / 0)
+            !s.media[m].temperature.empty())      // blackbody Le per point
             S.media.allGrey = 0;
     }
     if (getenv("PBRT_AMD_SPECTRAL_MEDIA")) S.media.allGrey = 0;

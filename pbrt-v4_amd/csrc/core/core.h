@@ -1706,6 +1706,19 @@ PHD float FastExp(float x) {
     return BitsToFloat(bits);
 }
 
+// Blackbody (util/spectrum.h:69-80): Planck's law with the CPU FastExp, in pbrt's float
+// operation order (Pow<5> as (l l)(l l) l); BlackbodySpectrum (util/spectrum.h:530-560) divides
+// by its value at Wien's peak, computed once per temperature
+PHD float Blackbody(float lambda, float T) {
+    if (T <= 0) return 0;
+    const float c = 299792458.f, h = 6.62606957e-34f, kb = 1.3806488e-23f;
+    const float l = lambda * 1e-9f;
+    const float l2 = l * l;
+    const float l5 = l2 * l2 * l;
+    return (2 * h * c * c) / (l5 * (FastExp((h * c) / (l * kb * T)) - 1));
+}
+PHD float BlackbodyNorm(float T) { return 1 / Blackbody(2.8977721e-3f / T * 1e9f, T); }
+
 // SampleExponential (util/sampling.h): -log(1 - u) / a
 PHD float SampleExponential(float u, float a) { return -Logf(1 - u) / a; }
 

@@ -1427,7 +1427,14 @@ static std::array<float, 311> MediumSpectrum(ParamSet &ps, const char *name, boo
         if (photometric) *photometric = PhotometricOf(d);
         return d;
     }
-    throw Error(ps.loc + ": \"" + p->type + " " + name + "\" is not supported for media yet (use rgb or spectrum)");
+    if (p->type == "blackbody" && p->nums.size() == 1) {
+        // BlackbodySpectrum(T), normalised to 1 at its peak (util/spectrum.h:530-560)
+        const float T = (float)p->nums[0];
+        for (int i = 0; i < 311; ++i) d[i] = BlackbodyNormalized(395.f + i, T);
+        if (photometric) *photometric = PhotometricOf(d);
+        return d;
+    }
+    throw Error(ps.loc + ": \"" + p->type + " " + name + "\" is not supported for media yet (use rgb, spectrum or blackbody)");
 }
 
 void Parser::Finish() {
@@ -1725,11 +1732,19 @@ void Parser::Finish() {
             m.emissive = *std::max_element(LeD.begin(), LeD.end()) > 0;  // IsEmissive
         } else if (pm.type == "uniformgrid") {
             m.type = kMediumGrid;
-            if (ps.Find("temperature") || ps.Find("temperaturescale") || ps.Find("temperatureoffset") ||
-                ps.Find("temperaturecutoff"))
-                throw Error(ps.loc + ": grid medium \"temperature\" is not supported yet");
             Param *dens = ps.Find("density", "float");
             if (!dens || dens->nums.empty()) throw Error(ps.loc + ": No \"density\" value provided for grid medium.");
+            Param *temp = ps.Find("temperature", "float");
+            if (temp && !temp->nums.empty()) {
+                if (temp->nums.size() != dens->nums.size())
+                    throw Error(ps.loc + ": Different number of samples (" + std::to_string(dens->nums.size()) + " vs " +
+                                std::to_string(temp->nums.size()) + ") provided for \"density\" and \"temperature\".");
+                if (ps.Find("Le")) throw Error(ps.loc + ": Both \"Le\" and \"temperature\" values were provided.");
+                for (double v : temp->nums) m.temperature.push_back((float)v);
+            }
+            // "temperatureoffset" defaults to "temperaturecutoff" (media.cpp:320-322)
+            m.temperatureOffset = (float)ps.GetFloat("temperatureoffset", ps.GetFloat("temperaturecutoff", 0));
+            m.temperatureScale = (float)ps.GetFloat("temperaturescale", 1);
             m.nx = ps.GetInt("nx", 1);
             m.ny = ps.GetInt("ny", 1);
             m.nz = ps.GetInt("nz", 1);
@@ -1748,7 +1763,7 @@ void Parser::Finish() {
                 m.lnx = m.nx, m.lny = m.ny, m.lnz = m.nz;
             }
             m.Le = addDense(Le, 1.f);
-            m.emissive = !LeZero;
+            m.emissive = !m.temperature.empty() || !LeZero;  // isEmissive (media.h:263)
             Param *p0 = ps.Find("p0", "point3"), *p1 = ps.Find("p1", "point3");
             if (p0) m.p0 = V3((float)p0->nums[0], (float)p0->nums[1], (float)p0->nums[2]);
             if (p1) m.p1 = V3((float)p1->nums[0], (float)p1->nums[1], (float)p1->nums[2]);

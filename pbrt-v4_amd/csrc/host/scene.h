@@ -61,6 +61,11 @@ struct MediumDesc {
     int lnx = 1, lny = 1, lnz = 1;         // LeScale grid (1x1x1 = {1 / photometric(Le)})
     std::vector<float> LeScale;
     std::vector<float> majorant;           // 16^3 MaxValue of density per majorant voxel
+    // GridMedium "temperature" (media.h:300-312): [nz][ny][nx] like density; Le at p is
+    // LeScale(p) * BlackbodySpectrum((T(p) - temperatureOffset) * temperatureScale) when that
+    // temperature exceeds 100 K
+    std::vector<float> temperature;
+    float temperatureOffset = 0, temperatureScale = 1;
     // RGBGridMedium ("rgbgrid"): density holds three [nz][ny][nx][4] blocks of {c0, c1, c2, scale}
     // (sigma_a, sigma_s, Le; bit k of rgbGrids: block k given), LeScale = {"Lescale"}
     int rgbGrids = 0;

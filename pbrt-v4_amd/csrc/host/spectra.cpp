@@ -556,21 +556,8 @@ PLSpectrumDesc NamedPiecewiseLinear(const std::string &name) {
 }  // namespace pbrt_amd
 
 namespace pbrt_amd {
-// Blackbody (util/spectrum.h): Planck's law with the CPU FastExp, in pbrt's float operation
-// order; BlackbodySpectrum divides by its value at Wien's peak
-static float Blackbody(float lambda, float T) {
-    if (T <= 0) return 0;
-    const float c = 299792458.f, h = 6.62606957e-34f, kb = 1.3806488e-23f;
-    const float l = lambda * 1e-9f;
-    const float l2 = l * l;
-    const float l5 = l2 * l2 * l;  // Pow<5>
-    return (2 * h * c * c) / (l5 * (FastExp((h * c) / (l * kb * T)) - 1));
-}
-float BlackbodyNormalized(float lambda, float T) {
-    const float lambdaMax = 2.8977721e-3f / T;
-    const float norm = 1 / Blackbody(lambdaMax * 1e9f, T);
-    return Blackbody(lambda, T) * norm;
-}
+// BlackbodySpectrum (util/spectrum.h:530-560): Blackbody (core.h) over its value at Wien's peak
+float BlackbodyNormalized(float lambda, float T) { return Blackbody(lambda, T) * BlackbodyNorm(T); }
 
 // PiecewiseLinearSpectrum::FromInterleaved(samples, normalize = false) (util/spectrum.cpp:
 // 133-163): split, then extended to Lambda_min - 1 / Lambda_max + 1 by the end values

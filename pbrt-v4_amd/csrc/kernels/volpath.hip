@@ -89,6 +89,7 @@ __device__ inline float GridLookup(const float *v, int nx, int ny, int nz, V3 p)
 // MediumSigmaA / MediumSigmaS / MediumLe evaluate the spectra per wavelength.
 struct MediumPoint {
     float d, le;
+    float temp;  // GridMedium temperature > 100 K at p (Le = le * BlackbodySpectrum(temp)), else 0
     bool rgb;
     int ix, iy, iz;
     float dx, dy, dz;
@@ -123,7 +124,10 @@ __device__ inline float MediumSigmaS(const DeviceScene &S, const MediumRef &m, c
     return m.P[7] * ((m.I[15] & 2) ? RGBGridAt(S, m, mp, 1, lam, 1.f) : 1.f);
 }
 __device__ inline float MediumLe(const DeviceScene &S, const MediumRef &m, const MediumPoint &mp, int off, float lam) {
-    if (!mp.rgb) return DenseAt(S, m.I[3], off) * mp.le;
+    if (!mp.rgb) {
+        if (mp.temp > 0) return mp.le * (Blackbody(lam, mp.temp) * BlackbodyNorm(mp.temp));
+        return DenseAt(S, m.I[3], off) * mp.le;
+    }
     return S.media.values[m.I[12]] * RGBGridAt(S, m, mp, 2, lam, DenseAt(S, m.I[3], off));
 }
 // Cloud: the scene has a CloudMedium.  Its density (13 noise evaluations) inlined into every
@@ -133,6 +137,7 @@ template <bool Cloud = true>
 __device__ inline MediumPoint SampleMediumPoint(const DeviceScene &S, const MediumRef &m, V3 p) {
     MediumPoint r;
     r.rgb = false;
+    r.temp = 0.f;
     if (Cloud && m.I[0] == kDevMediumCloud) {
         r.d = CloudDensity(S.media.values + m.I[11], MediumFromRender(m.P + 8, p));
         r.le = 0.f;
@@ -157,6 +162,13 @@ __device__ inline MediumPoint SampleMediumPoint(const DeviceScene &S, const Medi
     if (m.I[4]) {
         const float scale = GridLookup(S.media.values + m.I[12], m.I[8], m.I[9], m.I[10], q);
         if (scale > 0) r.le = scale;
+        if (scale > 0 && m.I[15] >= 0) {
+            // temperature grid (media.h:303-311): {offset, scale} then the grid
+            const float *tg = S.media.values + m.I[15];
+            const float t = (GridLookup(tg + 2, m.I[5], m.I[6], m.I[7], q) - tg[0]) * tg[1];
+            if (t > 100.f) r.temp = t;
+            else r.le = 0.f;
+        }
     }
     return r;
 }

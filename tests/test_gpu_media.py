@@ -71,10 +71,19 @@ AttributeEnd
 """
 
 
-@pytest.mark.parametrize("kind", ["homogeneous", "grid", "grid_emissive"])
+def temperature_grid(n=8, seed=4):
+    """GridMedium "temperature" (media.h:303-311): voxels from 0 to 3000 K less an offset of 300,
+    so some points fall under the 100 K cutoff (no emission)"""
+    t = np.random.default_rng(seed).uniform(0, 3000, n * n * n)
+    return ('"float temperatureoffset" 300 "float temperaturescale" 1.25 '
+            f'"float temperature" [ {" ".join(f"{v:.2f}" for v in t)} ]')
+
+
+@pytest.mark.parametrize("kind", ["homogeneous", "grid", "grid_emissive", "grid_temperature"])
 def test_medium_box_matches_oracle(pa, oracle, kind):
     m = {"homogeneous": HOMOG, "grid": grid_medium(),
-         "grid_emissive": grid_medium(le='"rgb Le" [2 1 0.5]')}[kind]
+         "grid_emissive": grid_medium(le='"rgb Le" [2 1 0.5]'),
+         "grid_temperature": grid_medium(le=temperature_grid())}[kind]
     sc = pa.Scene.from_string(medium_scene(m, res=48, spp=16, maxdepth=6, sky="0.3 0.4 0.5", extra=LIGHT, fov=35),
                               SCENES)
     a, _ = gpu_rgb(pa, oracle, sc)

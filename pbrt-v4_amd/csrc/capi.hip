@@ -440,7 +440,9 @@ struct pbrt_context {
     DevBuf<DeviceScene> sceneSelf;
     // scene buffers
     DevBuf<BVH8Node> nodes;
-    DevBuf<BVH8QNode> qnodes;
+    DevBuf<float4> qnodes;  // qStride float4 per node
+    int qStride = 5;
+    int triStride = 3;  // float4 per triangle in triVerts
     DevBuf<float> triVerts, matCoeffs, lightScale, lightArea, infScale, dense, sensor;
     DevBuf<int> primMaterial, primLight, matConstant, lightPrim, lightSpectrum, lightTwoSided, infSpectrum, infDistant,
         uniformOrder;
@@ -458,6 +460,7 @@ struct pbrt_context {
     DevBuf<uint32_t> lightBitTrail, permOffset, permNDigits, permBase;
     DevBuf<uint16_t> perm;
     DevBuf<HaltonDimDesc> haltonDim;
+    uint64_t haltonIndexBound = 0;  // Lean launches: every Halton index below it (HaltonDimDesc::nz)
     DevBuf<uint16_t> permByDepth;
     DevBuf<uint8_t> zsPerms;
     DevBuf<uint32_t> sobolM1;
@@ -664,8 +667,25 @@ static void BuildDevice(pbrt_context *c) {
         c->primAlpha.Upload(pa);
     }
     c->nodes.Upload(b.nodes);
-    c->qnodes.Upload(b.qnodes);
-    c->triVerts.Upload(b.triVerts);
+    {
+        // quantised nodes packed (80 B) or one per 128-B line (PBRT_AMD_QNODE_LINE=1): a packed
+        // node straddles two lines 3 times in 5
+        c->qStride = getenv("PBRT_AMD_QNODE_LINE") && atoi(getenv("PBRT_AMD_QNODE_LINE")) ? 8 : 5;
+        std::vector<float4> q(b.qnodes.size() * c->qStride, make_float4(0.f, 0.f, 0.f, 0.f));
+        for (size_t n = 0; n < b.qnodes.size(); ++n) memcpy(&q[n * c->qStride], &b.qnodes[n], sizeof(BVH8QNode));
+        c->qnodes.Upload(q);
+    }
+    {
+        // triangles at 48 B (packed) or 64 B (PBRT_AMD_TRI_LINE=1: never across a 128-B line)
+        c->triStride = getenv("PBRT_AMD_TRI_LINE") && atoi(getenv("PBRT_AMD_TRI_LINE")) ? 4 : 3;
+        if (c->triStride == 3) {
+            c->triVerts.Upload(b.triVerts);
+        } else {
+            std::vector<float> t(b.triVerts.size() / 12 * 16, 0.f);
+            for (size_t i = 0; i < b.triVerts.size() / 12; ++i) memcpy(&t[i * 16], &b.triVerts[i * 12], 48);
+            c->triVerts.Upload(t);
+        }
+    }
     c->primMaterial.Upload(pm);
     c->primLight.Upload(pl);
     c->primFlip.Upload(pf);
@@ -920,7 +940,23 @@ static void BuildDevice(pbrt_context *c) {
     std::vector<HaltonDimDesc> hd;
     for (size_t d = 0; d < s.permBase.size(); ++d)
         hd.push_back(MakeHaltonDimDesc(s.permBase[d], s.permNDigits[d], s.permOffset[d]));
-    for (auto &d : hd) HaltonDimTail(&d, s.permTable.data() + d.permOffset);
+    // the shade stage's dimensions 6 + 7 depth + {0..6}: one digit count per depth, enough for
+    // every Halton index below spp * stride (samplers.h:53-71), the Lean launches' bound
+    {
+        const uint64_t stride = (uint64_t)s.haltonBaseScales[0] * (uint64_t)s.haltonBaseScales[1];
+        c->haltonIndexBound = std::min<uint64_t>((uint64_t)std::max(s.spp, 1) * stride, 1ull << 24);
+        for (size_t d = 0; d < hd.size(); ++d) {
+            uint32_t nz = 6;
+            if (d >= 6 && hd[d].base >= 17) {
+                const size_t d0 = 6 + (d - 6) / 7 * 7;
+                nz = 0;
+                for (size_t j = d0; j < std::min(d0 + 7, hd.size()); ++j)
+                    nz = std::max(nz, HaltonDigitsFor(hd[j].base, c->haltonIndexBound));
+                nz = std::min(std::max(nz, 1u), 6u);
+            }
+            HaltonDimTail(&hd[d], s.permTable.data() + hd[d].permOffset, nz);
+        }
+    }
     c->haltonDim.Upload(hd);
     {
         std::vector<uint8_t> zp(&kZSobolPermutations[0][0], &kZSobolPermutations[0][0] + 96);
@@ -1007,6 +1043,8 @@ static void BuildDevice(pbrt_context *c) {
     S.media.primMedium = c->primMedium.p;
     S.nodes = c->nodes.p;
     S.qnodes = c->qnodes.p;
+    S.qStride = c->qStride;
+    S.triStride = c->triStride;
     S.triVerts = (const float4 *)c->triVerts.p;
     S.nTris = nt;
     S.primMaterial = c->primMaterial.p;
@@ -1661,7 +1699,7 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
             static const bool noLean = getenv("PBRT_AMD_NO_LEAN") != nullptr;
             const uint64_t haltonStride = (uint64_t)c->S.baseScales[0] * (uint64_t)c->S.baseScales[1];
             const bool lean = !noLean && c->S.samplerType == 0 &&
-                              (uint64_t)(st.firstSample + nS) * haltonStride <= (1ull << 24) &&
+                              (uint64_t)(st.firstSample + nS) * haltonStride <= c->haltonIndexBound &&
                               c->S.shadeLds.lightsInLds && c->S.shadeLds.denseInLds && c->S.triShade == nullptr &&
                               c->S.nDelta == 0 && c->S.nEnv == 0 && c->S.nShapes == 0 && !c->S.textured && !c->hasMix &&
                               !c->S.hasSpread && c->S.nImageAreaLights == 0;
@@ -2036,9 +2074,9 @@ int pbrt_synchronize(pbrt_context *ctx) {
         {
             const DeviceScene &S = ctx->S;
             const uint64_t nodeB = S.compressed ? sizeof(BVH8QNode) : sizeof(BVH8Node);
-            const uint64_t nNodes = S.compressed ? ctx->qnodes.n : ctx->nodes.n;
+            const uint64_t nNodes = S.compressed ? ctx->qnodes.n / S.qStride : ctx->nodes.n;
             ctx->stats.bvh_hbm_node_bytes = nNodes > (uint64_t)S.ldsNodes ? (nNodes - S.ldsNodes) * nodeB : 0;
-            ctx->stats.bvh_hbm_tri_bytes = S.ldsTris > 0 ? 0 : (uint64_t)ctx->triVerts.n * sizeof(float);
+            ctx->stats.bvh_hbm_tri_bytes = S.ldsTris > 0 ? 0 : (uint64_t)ctx->triVerts.n / S.triStride * 3 * sizeof(float);
         }
         return 0;
     } catch (const std::exception &e) {
@@ -2301,6 +2339,26 @@ int64_t pbrt_debug_halton_fastpath_mismatches(const pbrt_scene *scene, int dim, 
         memcpy(&fb, &f, 4);
         memcpy(&gb, &g, 4);
         bad += fb != gb;
+    }
+    // the Lean shade stage's digit-major form (HaltonDepthSamples) over this dimension's depth
+    // group, with the digit count of indices below a1
+    if (dim >= 6 && 6 + ((size_t)dim - 6) / 7 * 7 + 7 <= s.permBase.size()) {
+        const int d0 = 6 + (dim - 6) / 7 * 7;
+        HaltonDimDesc g7[7];
+        const uint16_t *p7[7];
+        uint32_t nz = 1;
+        for (int j = 0; j < 7; ++j) {
+            g7[j] = MakeHaltonDimDesc(s.permBase[d0 + j], s.permNDigits[d0 + j], s.permOffset[d0 + j]);
+            p7[j] = s.permTable.data() + g7[j].permOffset;
+            nz = std::max(nz, HaltonDigitsFor(g7[j].base, a1));
+        }
+        for (int j = 0; j < 7; ++j) HaltonDimTail(&g7[j], p7[j], std::min(nz, 6u));
+        for (uint64_t a = a0; a < a1; a += step) {
+            float u[7];
+            HaltonDepthSamples<false>(g7, (uint32_t)a, p7, u);
+            const float g = ScrambledRadicalInverse(d.base, d.nDigits, a, perm);
+            bad += memcmp(&u[dim - d0], &g, 4) != 0;
+        }
     }
     return bad;
 }

@@ -752,6 +752,7 @@ PHD_NOINLINE float ScrambledRadicalInverse(uint32_t base, uint32_t nDigits, uint
 struct HaltonDimDesc {
     uint32_t base, nDigits, permOffset, tail;  // tail, tailMul: HaltonDimTail
     float invBase, invBaseM, rcp, tailMul;
+    uint32_t nz;  // digit steps of the fast forms (<= 6): every index they see is < base^nz
 };
 PHD HaltonDimDesc MakeHaltonDimDesc(uint32_t base, uint32_t nDigits, uint32_t permOffset) {
     HaltonDimDesc d{};
@@ -765,17 +766,20 @@ PHD HaltonDimDesc MakeHaltonDimDesc(uint32_t base, uint32_t nDigits, uint32_t pe
     d.rcp = (float)(1.0 / base);
     d.tail = 0;
     d.tailMul = 1;
+    d.nz = 6;
     return d;
 }
-// The digits past the sixth of an index a < base^6 are all zero, so they add the constant
-// tail = sum_{k=6}^{n-1} perm[k base] base^(n-1-k) after scaling the six-digit value by
-// tailMul = base^(n-6) (ScrambledRadicalInverse24x6).  Both are exact integers far below 2^24.
-PHD void HaltonDimTail(HaltonDimDesc *d, const uint16_t *perm) {
+// The digits past the nz-th of an index a < base^nz are all zero, so they add the constant
+// tail = sum_{k=nz}^{n-1} perm[k base] base^(n-1-k) after scaling the nz-digit value by
+// tailMul = base^(n-nz) (ScrambledRadicalInverse24x6, HaltonDepthSamples).  Both are exact
+// integers far below 2^24.
+PHD void HaltonDimTail(HaltonDimDesc *d, const uint16_t *perm, uint32_t nz = 6) {
+    d->nz = nz;
     d->tail = 0;
     d->tailMul = 1;
-    if (d->nDigits <= 6) return;
+    if (d->nDigits <= nz) return;
     uint32_t t = 0, m = 1;
-    for (uint32_t k = 6; k < d->nDigits; ++k) {
+    for (uint32_t k = nz; k < d->nDigits; ++k) {
         t = t * d->base + perm[k * d->base];
         m *= d->base;
     }
@@ -844,9 +848,70 @@ PHD_UNROLL
     }
     double rd = 0;
 PHD_UNROLL
-    for (int k = 0; k < 6; ++k) rd = (uint32_t)k < n ? fma(rd, (double)b, (double)pv[k]) : rd;
+    for (int k = 0; k < 6; ++k) rd = (uint32_t)k < n && (uint32_t)k < d.nz ? fma(rd, (double)b, (double)pv[k]) : rd;
     rd = fma(rd, (double)d.tailMul, (double)d.tail);
     return std::fmin(d.invBaseM * (float)rd, kOneMinusEpsilon);
+}
+// HaltonDigitsFor: the digit steps an index below bound needs in base b (bound <= 2^24, b >= 17:
+// at most 6)
+inline uint32_t HaltonDigitsFor(uint32_t b, uint64_t bound) {
+    uint32_t k = 0;
+    for (uint64_t p = 1; p < bound; p *= b) ++k;
+    return k;
+}
+// The seven dimensions of one depth (ScrambledRadicalInverse24x6 of each) digit-major: the host
+// gave the seven the same nz (digits every index of the render has, HaltonDigitsFor of the
+// largest), so the digit steps past nz are skipped by a launch-uniform branch and the seven
+// quotient chains interleave inside each step.  The result is the same float per dimension:
+// digits past nz are zero and their permuted values sit in the host's tail, as past the sixth.
+// Skip3: dimension 3 (indirect.uc) is not needed.
+template <bool Skip3, typename PermPtr>
+PHD void HaltonDepthSamples(const HaltonDimDesc *d, uint32_t a0, const PermPtr *perm, float *out) {
+    const uint32_t nz = d[0].nz;
+    uint32_t a[7], pv[6][7];
+    double rd[7];
+PHD_UNROLL
+    for (int j = 0; j < 7; ++j) {
+        a[j] = a0;
+        rd[j] = 0;
+    }
+PHD_UNROLL
+    for (int k = 0; k < 6; ++k) {
+        if ((uint32_t)k < nz) {
+PHD_UNROLL
+            for (int j = 0; j < 7; ++j) {
+                if (Skip3 && j == 3) continue;
+                const uint32_t b = d[j].base & 0xffffffu;
+                uint32_t q = (uint32_t)((float)a[j] * d[j].rcp);
+#if defined(__HIP_DEVICE_COMPILE__)
+                int r = (int)a[j] - (int)MulU24(q, b);
+#else
+                int r = (int)a[j] - (int)(q * b);
+#endif
+                q = r < 0 ? q - 1 : q;
+                r = r < 0 ? r + (int)b : r;
+                q = r >= (int)b ? q + 1 : q;
+                r = r >= (int)b ? r - (int)b : r;
+                const bool ok = (uint32_t)k < d[j].nDigits;
+                pv[k][j] = perm[j][ok ? (uint32_t)k * b + (uint32_t)r : 0u];
+                a[j] = q;
+            }
+PHD_UNROLL
+            for (int j = 0; j < 7; ++j) {
+                if (Skip3 && j == 3) continue;
+                if ((uint32_t)k < d[j].nDigits) rd[j] = fma(rd[j], (double)(d[j].base & 0xffffffu), (double)pv[k][j]);
+            }
+        }
+    }
+PHD_UNROLL
+    for (int j = 0; j < 7; ++j) {
+        if (Skip3 && j == 3) {
+            out[j] = 0;
+            continue;
+        }
+        rd[j] = fma(rd[j], (double)d[j].tailMul, (double)d[j].tail);
+        out[j] = std::fmin(d[j].invBaseM * (float)rd[j], kOneMinusEpsilon);
+    }
 }
 constexpr int kMaxHaltonDigits24 = 25;  // base 2 (the largest digit count of any dimension)
 constexpr int kMaxShadeHaltonDigits = 8;  // dimensions >= 6 (bases >= 17)

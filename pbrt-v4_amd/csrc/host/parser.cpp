@@ -19,6 +19,9 @@
 #include "texture.h"
 
 namespace pbrt_amd {
+// host/subdiv.cpp
+void LoopSubdivideMesh(int nLevels, const std::vector<int> &indices, const std::vector<V3> &p, std::vector<V3> *P,
+                       std::vector<int> *tris, std::vector<V3> *N);
 
 // ------------------------------------------------------------------ matrices (double)
 Mat4 Identity4() {
@@ -946,6 +949,146 @@ class Parser {
         throw Error(loc + ": \"" + p->type + " " + p->name + "\" is not supported for conductors yet (use \"spectrum\")");
     }
 
+    // Curve parameters as Curve::Create reads them (shapes.cpp:1004-1105), then the dicing of
+    // OptiXAggregate::diceCurveToBLP: nDiceU + 1 rings along the curve's global u (each in the
+    // cubic Bezier segment u falls in: degree 2 elevated, b-splines converted, util/splines.h),
+    // a ribbon's two edges across the slerped normal, or a tube of nDiceV + 1 vertices around
+    // flat and cylinder curves (with per-vertex normals), all in float as the reference has them.
+    static void DiceCurve(ParamSet &ps, PendingShape *s, int nDiceU, int nDiceV) {
+        const float width = (float)ps.GetFloat("width", 1.f);
+        const float width0 = (float)ps.GetFloat("width0", width), width1 = (float)ps.GetFloat("width1", width);
+        const int degree = ps.GetInt("degree", 3);
+        if (degree != 2 && degree != 3)
+            throw Error(ps.loc + ": Invalid degree " + std::to_string(degree) + ": only degree 2 and 3 curves are supported.");
+        const std::string basis = ps.GetString("basis", "bezier");
+        if (basis != "bezier" && basis != "bspline")
+            throw Error(ps.loc + ": Invalid basis \"" + basis + "\": only \"bezier\" and \"bspline\" are supported.");
+        std::vector<V3> cp;
+        Param *P = ps.Find("P", "point3");
+        if (!P) P = ps.Find("P", "point");
+        if (P)
+            for (size_t i = 0; i + 2 < P->nums.size(); i += 3) cp.push_back(V3((float)P->nums[i], (float)P->nums[i + 1], (float)P->nums[i + 2]));
+        const bool bezier = basis == "bezier";
+        int nSegments;
+        if (bezier) {
+            if (cp.size() < (size_t)degree + 1 || (cp.size() - 1 - degree) % degree != 0)
+                throw Error(ps.loc + ": Invalid number of control points " + std::to_string(cp.size()) + ": for the degree " +
+                            std::to_string(degree) + " Bezier basis " + std::to_string(degree + 1) + " + n * " +
+                            std::to_string(degree) + " are required, for n >= 0.");
+            nSegments = (int)(cp.size() - 1) / degree;
+        } else {
+            if (cp.size() < (size_t)degree + 1)
+                throw Error(ps.loc + ": Invalid number of control points " + std::to_string(cp.size()) + ": for the degree " +
+                            std::to_string(degree) + " b-spline basis, must have >= " + std::to_string(degree + 1) + ".");
+            nSegments = (int)cp.size() - degree;
+        }
+        enum { kFlat, kCylinder, kRibbon } ctype = kFlat;
+        const std::string ct = ps.GetString("type", "flat");
+        if (ct == "ribbon")
+            ctype = kRibbon;
+        else if (ct == "cylinder")
+            ctype = kCylinder;
+        else if (ct != "flat") {
+            std::fprintf(stderr, "%s: Error: Unknown curve type \"%s\".  Using \"cylinder\".\n", ps.loc.c_str(), ct.c_str());
+            ctype = kCylinder;
+        }
+        std::vector<V3> n;
+        Param *N = ps.Find("N", "normal");
+        if (!N) N = ps.Find("N", "normal3");
+        if (N)
+            for (size_t i = 0; i + 2 < N->nums.size(); i += 3) n.push_back(V3((float)N->nums[i], (float)N->nums[i + 1], (float)N->nums[i + 2]));
+        if (!n.empty()) {
+            if (ctype != kRibbon) {
+                std::fprintf(stderr, "%s: Warning: Curve normals are only used with \"ribbon\" type curves.\n", ps.loc.c_str());
+                n.clear();
+            } else if ((int)n.size() != nSegments + 1) {
+                throw Error(ps.loc + ": Invalid number of normals " + std::to_string(n.size()) + ": must provide " +
+                            std::to_string(nSegments + 1) + " normals for ribbon curves with " + std::to_string(nSegments) +
+                            " segments.");
+            }
+            for (V3 &v : n) v = Normalize(v);
+        } else if (ctype == kRibbon) {
+            throw Error(ps.loc + ": Must provide normals \"N\" at curve endpoints with ribbon curves.");
+        }
+        ps.GetInt("splitdepth", 3);  // Curve::Create's subdivision; the diced mesh has none
+        auto lerp = [](float t, V3 a, V3 b) { return (1 - t) * a + t * b; };
+        int lastOffset = -1;
+        V3 seg[4];
+        for (int i = 0; i <= nDiceU; ++i) {
+            const float u = float(i) / float(nDiceU);
+            const float w = (1 - u) * width0 + u * width1;
+            int segmentIndex = int(u * nSegments);
+            if (segmentIndex == nSegments) --segmentIndex;
+            const int off = bezier ? segmentIndex * degree : segmentIndex;
+            if (off != lastOffset) {
+                const V3 *c = &cp[off];
+                if (bezier && degree == 3) {
+                    for (int k = 0; k < 4; ++k) seg[k] = c[k];
+                } else if (degree == 2) {
+                    // QuadraticBSplineToBezier, then ElevateQuadraticBezierToCubic
+                    V3 q[3] = {c[0], c[1], c[2]};
+                    if (!bezier) q[0] = lerp(0.5f, c[0], c[1]), q[2] = lerp(0.5f, c[1], c[2]);
+                    seg[0] = q[0];
+                    seg[1] = lerp(2.f / 3.f, q[0], q[1]);
+                    seg[2] = lerp(1.f / 3.f, q[1], q[2]);
+                    seg[3] = q[2];
+                } else {
+                    // CubicBSplineToBezier (blossoming)
+                    const V3 p122 = lerp(2.f / 3.f, c[0], c[1]), p223 = lerp(1.f / 3.f, c[1], c[2]);
+                    const V3 p233 = lerp(2.f / 3.f, c[1], c[2]), p334 = lerp(1.f / 3.f, c[2], c[3]);
+                    seg[0] = lerp(0.5f, p122, p223);
+                    seg[1] = p223;
+                    seg[2] = p233;
+                    seg[3] = lerp(0.5f, p233, p334);
+                }
+                lastOffset = off;
+            }
+            const float uSeg = (u * nSegments) - segmentIndex;
+            // EvaluateCubicBezier with its derivative (util/splines.h:30-43)
+            const V3 c1[3] = {lerp(uSeg, seg[0], seg[1]), lerp(uSeg, seg[1], seg[2]), lerp(uSeg, seg[2], seg[3])};
+            const V3 c2[2] = {lerp(uSeg, c1[0], c1[1]), lerp(uSeg, c1[1], c1[2])};
+            const V3 dpdu = LengthSquared(c2[1] - c2[0]) > 0 ? 3 * (c2[1] - c2[0]) : seg[3] - seg[0];
+            const V3 p = lerp(uSeg, c2[0], c2[1]);
+            const int base = (int)s->P.size();
+            if (ctype == kRibbon) {
+                const V3 n0 = n[segmentIndex], n1 = n[segmentIndex + 1];
+                const float normalAngle =
+                    DotN(n0, n1) < 0 ? kPi - 2 * SafeASin(Length(n0 + n1) / 2) : 2 * SafeASin(Length(n1 - n0) / 2);
+                const float invSinNormalAngle = 1 / std::sin(normalAngle);
+                V3 nu;
+                if (normalAngle == 0) {
+                    nu = n0;
+                } else {
+                    const float sin0 = std::sin((1 - uSeg) * normalAngle) * invSinNormalAngle;
+                    const float sin1 = std::sin(uSeg * normalAngle) * invSinNormalAngle;
+                    nu = sin0 * n0 + sin1 * n1;
+                }
+                const V3 dpdv = Normalize(Cross(nu, dpdu)) * w;
+                s->P.push_back(p - dpdv / 2);
+                s->P.push_back(p + dpdv / 2);
+                s->uv.insert(s->uv.end(), {u, 0.f, u, 1.f});
+                if (i > 0) s->quadIdx.insert(s->quadIdx.end(), {base - 2, base - 1, base, base + 1});
+            } else {
+                V3 o0, o1;
+                CoordinateSystem(Normalize(dpdu), &o0, &o1);
+                o0 = o0 * (w / 2);
+                o1 = o1 * (w / 2);
+                for (int v = 0; v <= nDiceV; ++v) {
+                    const float angle = float(v) / nDiceV * 2 * kPi;
+                    const V3 q = p + o0 * std::cos(angle) + o1 * std::sin(angle);
+                    s->P.push_back(q);
+                    s->N.push_back(Normalize(q - p));
+                    s->uv.insert(s->uv.end(), {u, float(v) / nDiceV});
+                }
+                if (i > 0)
+                    for (int v = 0; v < nDiceV; ++v) {
+                        const int r0 = (nDiceV + 1) * (i - 1), r1 = (nDiceV + 1) * i;
+                        s->quadIdx.insert(s->quadIdx.end(), {r0 + v, r0 + v + 1, r1 + v, r1 + v + 1});
+                    }
+            }
+        }
+    }
+
     // Shape "trianglemesh" (Triangle::CreateMesh, shapes.cpp:1380-1417) and "plymesh"
     // (shapes.cpp:1418-1478; TriQuadMesh::ReadPLY, util/mesh.cpp:322-420)
     void Shape(const std::string &type, ParamSet &ps, const std::string &dir) {
@@ -1047,6 +1190,34 @@ class Parser {
             s.sp[1] = (float)ps.GetFloat("zmin", -1);
             s.sp[2] = (float)ps.GetFloat("zmax", 1);
             s.sp[3] = (float)ps.GetFloat("phimax", 360);
+        } else if (type == "loopsubdiv") {
+            // Shape "loopsubdiv" (shapes.cpp:1476-1493): LoopSubdivide's limit-surface triangle
+            // mesh with its vertex normals (host/subdiv.cpp)
+            const int levels = ps.GetInt("levels", 3);
+            Param *I = ps.Find("indices", "integer");
+            if (!I || I->nums.empty()) throw Error(ps.loc + ": Vertex indices \"indices\" not provided for LoopSubdiv shape.");
+            Param *P = ps.Find("P", "point3");
+            if (!P) P = ps.Find("P", "point");
+            if (!P || P->nums.size() < 3) throw Error(ps.loc + ": Vertex positions \"P\" not provided for LoopSubdiv shape.");
+            ps.GetString("scheme", "loop");  // "don't actually use this for now"
+            std::vector<int> ctrl;
+            for (double v : I->nums) ctrl.push_back((int)v);
+            std::vector<V3> cp;
+            for (size_t i = 0; i + 2 < P->nums.size(); i += 3) cp.push_back(V3((float)P->nums[i], (float)P->nums[i + 1], (float)P->nums[i + 2]));
+            try {
+                LoopSubdivideMesh(levels, ctrl, cp, &s.P, &s.idx, &s.N);
+            } catch (const Error &e) {
+                throw Error(ps.loc + ": " + e.what());
+            }
+        } else if (type == "curve") {
+            // the wavefront's curves: diced into a bilinear patch mesh on the host
+            // (OptiXAggregate::diceCurveToBLP, gpu/aggregate.cpp:547-760, called with 5 steps
+            // along the curve and 5 around it: gpu/aggregate.cpp:800-806)
+            s.kind = kShapeBilinearT;
+            // the reference pairs a curve's area lights (one per split Curve segment) with its
+            // diced patches by index, which do not correspond: refused rather than guessed
+            if (!gs.areaLightName.empty()) throw Error(ps.loc + ": area lights on curves are not supported");
+            DiceCurve(ps, &s, 5, 5);
         } else {
             throw Error(ps.loc + ": shape \"" + type + "\" is not supported yet");
         }

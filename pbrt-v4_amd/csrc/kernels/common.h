@@ -611,8 +611,10 @@ __device__ inline SceneLds SetupSceneLds(const DeviceScene &S, float4 *dyn) {
     float4 *tris = nodes + S.ldsNodes * LdsNodeStride(S.compressed);
     // plain copies: measured faster here than per-node LDS-DMA (few, tiny rows)
     if (S.compressed) {
-        const float4 *gn = reinterpret_cast<const float4 *>(S.qnodes);
-        for (int i = threadIdx.x; i < S.ldsNodes * kLdsQNodeStride; i += blockDim.x) nodes[i] = gn[i];
+        for (int i = threadIdx.x; i < S.ldsNodes * kLdsQNodeStride; i += blockDim.x) {
+            const int n = i / kLdsQNodeStride, k = i - n * kLdsQNodeStride;
+            nodes[i] = S.qnodes[n * S.qStride + k];
+        }
     } else {
         const float4 *gn = reinterpret_cast<const float4 *>(S.nodes);
         for (int i = threadIdx.x; i < S.ldsNodes * 15; i += blockDim.x) {
@@ -622,7 +624,8 @@ __device__ inline SceneLds SetupSceneLds(const DeviceScene &S, float4 *dyn) {
     }
     for (int i = threadIdx.x; i < S.ldsTris * 9; i += blockDim.x) {
         const int rot = i / (S.ldsTris * 3), e = i - rot * (S.ldsTris * 3);
-        const V3 v = RotateToRay(S.triVerts[e], rot);
+        const int tri = e / 3;
+        const V3 v = RotateToRay(S.triVerts[tri * S.triStride + (e - 3 * tri)], rot);
         tris[i] = make_float4(v.x, v.y, v.z, 0.f);
     }
     __syncthreads();
@@ -676,7 +679,7 @@ __device__ inline bool CwStep(const DeviceScene &S, const SceneLds &L, CwState &
 #endif
     if constexpr (Compressed) {
         if (NodesInLds || s.node < S.ldsNodes) nh = VisitQuant(L.nodes + s.node * kLdsQNodeStride, s.r, s.tMax);
-        else nh = VisitQuant(reinterpret_cast<const float4 *>(S.qnodes + s.node), s.r, s.tMax);
+        else nh = VisitQuant(S.qnodes + (size_t)s.node * S.qStride, s.r, s.tMax);
     } else {
         if (NodesInLds || s.node < S.ldsNodes) nh = VisitWide(L.nodes + s.node * kLdsNodeStride, s.r, s.tMax);
         else nh = VisitWide(reinterpret_cast<const float4 *>(S.nodes + s.node), s.r, s.tMax);
@@ -695,9 +698,10 @@ __device__ inline bool CwStep(const DeviceScene &S, const SceneLds &L, CwState &
             const float4 va = v[0], vb = v[1], vc = v[2];
             a = V3(va.x, va.y, va.z), b = V3(vb.x, vb.y, vb.z), c = V3(vc.x, vc.y, vc.z);
         } else {
-            a = RotateToRay(S.triVerts[3 * t], s.tr.kz);
-            b = RotateToRay(S.triVerts[3 * t + 1], s.tr.kz);
-            c = RotateToRay(S.triVerts[3 * t + 2], s.tr.kz);
+            const float4 *tv = S.triVerts + (size_t)t * S.triStride;
+            a = RotateToRay(tv[0], s.tr.kz);
+            b = RotateToRay(tv[1], s.tr.kz);
+            c = RotateToRay(tv[2], s.tr.kz);
         }
         TriHit h;
         if (IntersectTriangleRot(s.tr, s.tMax, a, b, c, &h)) {
@@ -877,7 +881,8 @@ __device__ inline void PrimVerts(const DeviceScene &S, int prim, V3 *p0, V3 *p1,
         *p0 = *p1 = *p2 = V3(0, 0, 0);
         return;
     }
-    float4 a = S.triVerts[3 * prim], b = S.triVerts[3 * prim + 1], c = S.triVerts[3 * prim + 2];
+    const float4 *tv = S.triVerts + (size_t)prim * S.triStride;
+    float4 a = tv[0], b = tv[1], c = tv[2];
     *p0 = V3(a.x, a.y, a.z);
     *p1 = V3(b.x, b.y, b.z);
     *p2 = V3(c.x, c.y, c.z);

@@ -120,9 +120,11 @@ struct DeviceDeltaLight {
 struct DeviceScene {
     // geometry (leaf order)
     const BVH8Node *nodes;
-    const BVH8QNode *qnodes;  // the same tree, quantised (80 B/node)
+    const float4 *qnodes;     // the same tree, quantised (80 B/node) at qStride float4 per node:
+    int qStride;              // 5 (packed) or 8 (one 128-B cache line per node)
     int compressed;           // traverse qnodes (HBM-resident scenes) instead of nodes
-    const float4 *triVerts;  // 3 per triangle
+    const float4 *triVerts;  // 3 per triangle at triStride (3, or 4: 64-B slots)
+    int triStride;
     int nTris;
     const int *primMaterial;
     const int *primLight;

@@ -673,17 +673,20 @@ __device__ __forceinline__ RaySamples GenerateRaySamples(const DeviceScene &S, c
     RaySamples r;
     r.iUc = 0;
     if (Lean || (S.samplerType == 0 && sidx < (1u << 24))) {
-        // the common case: every dimension by the 24-bit digit loop from the LDS tables
-        auto dim = [&](int k) -> float {
-            return ScrambledRadicalInverse24x6(S.haltonDim[d0 + k], sidx, T.permL + T.permOff[k]);
-        };
-        r.dUc = dim(0);
-        r.dU0 = dim(1);
-        r.dU1 = dim(2);
-        if (IndirectUc) r.iUc = dim(3);
-        r.iU0 = dim(4);
-        r.iU1 = dim(5);
-        r.rr = dim(6);
+        // the common case: the depth's seven dimensions digit-major from the LDS tables, with
+        // the digit count every index of the render fits in (host-chosen, HaltonDimDesc::nz)
+        const LdsU16 *perm[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) perm[k] = T.permL + T.permOff[k];
+        float u[7];
+        HaltonDepthSamples<!IndirectUc>(S.haltonDim + d0, sidx, perm, u);
+        r.dUc = u[0];
+        r.dU0 = u[1];
+        r.dU1 = u[2];
+        if (IndirectUc) r.iUc = u[3];
+        r.iU0 = u[4];
+        r.iU1 = u[5];
+        r.rr = u[6];
         return r;
     }
     if constexpr (Lean) return r;  // not reached

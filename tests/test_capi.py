@@ -41,7 +41,7 @@ def test_overrides(pa):
 
 
 @pytest.mark.parametrize("text,msg", [
-    ('WorldBegin\nShape "curve"\n', "not supported"),
+    ('WorldBegin\nShape "hyperboloid"\n', "not supported"),
     ('WorldBegin\nFoo 1 2 3\n', "unknown directive"),
     ('Sampler "pmj02bn"\nWorldBegin\nAttributeBegin\nAreaLightSource "diffuse"\nShape "trianglemesh" "point3 P" [0 0 0 1 0 0 0 1 0]\nAttributeEnd\n', "not supported"),
     ('Sampler "halton"\nWorldBegin\nShape "trianglemesh" "point3 P" [0 0 0 1 0 0 0 1 0]\n', "No light sources"),

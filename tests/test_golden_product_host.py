@@ -109,7 +109,10 @@ def test_halton_fastpath_matches_64bit_restatement(pa):
     and its six-digit branch-free form for bases >= 17 (ScrambledRadicalInverse24x6)
     equal the 64-bit restatement of ScrambledRadicalInverse (util/lowdiscrepancy.h:115-134), bit
     for bit: every dimension the wavefront uses at maxdepth 5 (0..40), a strided sweep of the
-    whole 2^24 range plus the top 2^16 indices and the first 2^16 exhaustively."""
+    whole 2^24 range plus the top 2^16 indices and the first 2^16 exhaustively.  For dimensions
+    >= 6 the same calls also check the Lean shade stage's digit-major form (HaltonDepthSamples)
+    with the digit count of the sweep's bound, here also at the bounds spp * 128 * 243 of
+    C2-like renders (fewer digits: 4 for 64 spp at depth 1)."""
     from conftest import SCENES
     sc = pa.load_scene(SCENES / "cornell-box.pbrt", xresolution=1280, yresolution=720, spp=64)
     top = 1 << 24
@@ -119,6 +122,10 @@ def test_halton_fastpath_matches_64bit_restatement(pa):
         assert sc.halton_fastpath_mismatches(dim, 0, top, 61) == 0, dim
         assert sc.halton_fastpath_mismatches(dim, top - (1 << 16), top) == 0, dim
         assert sc.halton_fastpath_mismatches(dim, 0, 1 << 16) == 0, dim
+    for bound in (31104 * 64, 31104 * 16, 31104):
+        for dim in range(6, 41):
+            assert sc.halton_fastpath_mismatches(dim, 0, bound, 7) == 0, (dim, bound)
+            assert sc.halton_fastpath_mismatches(dim, bound - min(bound, 1 << 14), bound) == 0, (dim, bound)
     deep = pa.load_scene(SCENES / "cornell-box.pbrt", xresolution=1280, yresolution=720, spp=64, maxdepth=60)
     for dim in (55, 97, 146, 300, 426):
         assert deep.halton_fastpath_mismatches(dim, 0, top, 61) == 0, dim

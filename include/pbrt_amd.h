@@ -241,6 +241,18 @@ typedef struct pbrt_scene_flat {
      * wrinkled, windy, marble: tex_node_info kinds 7-11; their params [22..24] = octaves,
      * roughness, variation and [26] = marble scale) */
     const float *noise_perm;
+    /* SubsurfaceMaterial (materials.h:772-866): material_sss [n_materials] = its subsurface
+     * description or -1 (NULL when n_sss == 0; such a material is otherwise a dielectric);
+     * sss_params [n_sss][20] = mode (0 sigma_a / sigma_s, 1 reflectance / mfp), scale, eta,
+     * 1 - 2 FresnelMoment1(1 / eta), two spectra {kind (0 constant, 1 scale * sigmoid, 2
+     * piecewise-linear), value, c0, c1, c2, scale, pl_spectra index}, g, 0; sss_tables
+     * [n_sss][13064] = the BSSRDFTable (rho[100], radius[64], profile[100][64], rhoEff[100],
+     * profileCDF[100][64]); dims_per_depth: sampler dimensions per path depth (7, or 10 with
+     * subsurface scattering: samples.cpp:39-41) */
+    int n_sss, dims_per_depth;
+    const int32_t *material_sss;
+    const float *sss_params;
+    const float *sss_tables;
 } pbrt_scene_flat;
 
 typedef struct pbrt_render_params {
@@ -350,6 +362,12 @@ int pbrt_debug_check_rn_math(int device, uint64_t seed, int64_t n, int64_t *mism
  * permutations) by the kernels' 24-bit float-reciprocal digit loop against the 64-bit
  * restatement of util/lowdiscrepancy.h:115-134, for a = a0, a0 + step, ... < a1 (a1 <= 2^24);
  * returns the number of indices whose floats differ (bitwise), or -1 on error */
+/* The Catmull-Rom spline utilities of the tabulated BSSRDF (core/bssrdf.h; util/math.cpp:157-265,
+ * util/sampling.cpp:424-488), run on the host: op 0 CatmullRomWeights(nodes1, x[i]) -> out[n][6]
+ * = ok, offset, w0..w3; 1 InvertCatmullRom(nodes1, values, x[i]) -> out[n]; 3
+ * SampleCatmullRom2D(nodes1, nodes2, values[n1][n2], cdf[n1][n2], alpha = x[2i], u = x[2i+1]) */
+int pbrt_debug_catmull_rom(int op, const float *nodes1, int n1, const float *nodes2, int n2, const float *values,
+                           const float *cdf, const float *x, int n, float *out);
 int64_t pbrt_debug_halton_fastpath_mismatches(const pbrt_scene *scene, int dim, uint32_t a0, uint32_t a1,
                                               uint32_t step);
 int pbrt_debug_rgb_coeffs(float r, float g, float b, float *coeffs3);

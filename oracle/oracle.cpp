@@ -4783,6 +4783,276 @@ bool Scene::AlphaKilled(int prim, const TriIsect &ti, Vec o, Vec d) const {
     return (Float)(uint32_t)Murmur64A(buf, 24, 0) * 0x1p-32f > a;
 }
 
+// ---------------------------------------------------------------- subsurface scattering
+// SubsurfaceMaterial's TabulatedBSSRDF and the wavefront's SampleSubsurface
+// (wavefront/subsurface.cpp:18-206), restated: the BSSRDF table (ComputeBeamDiffusionBSSRDF,
+// bssrdf.cpp:26-155, with FresnelMoment1/2 util/scattering.cpp:10-31 and IntegrateCatmullRom
+// util/math.cpp:267-288), the spline utilities (CatmullRomWeights / InvertCatmullRom
+// util/math.cpp:157-265, SampleCatmullRom2D util/sampling.cpp:424-488, NewtonBisection
+// util/math.h:662-696) and TabulatedBSSRDF's Sr / PDF_Sr / SampleSr / SampleSp / PDF_Sp
+// (bssrdf.h:118-258).  The table is built here from (g, eta), independently of the product.
+namespace osss {
+constexpr int NRho = 100, NRad = 64, TableFloats = NRho + NRad + 2 * NRho * NRad + NRho;
+static Float FresnelMoment1(Float eta) {
+    Float eta2 = eta * eta, eta3 = eta2 * eta, eta4 = eta3 * eta, eta5 = eta4 * eta;
+    if (eta < 1) return 0.45966f - 1.73965f * eta + 3.37668f * eta2 - 3.904945 * eta3 + 2.49277f * eta4 - 0.68441f * eta5;
+    return -4.61686f + 11.1136f * eta - 10.4646f * eta2 + 5.11455f * eta3 - 1.27198f * eta4 + 0.12746f * eta5;
+}
+static Float FresnelMoment2(Float eta) {
+    Float eta2 = eta * eta, eta3 = eta2 * eta, eta4 = eta3 * eta, eta5 = eta4 * eta;
+    if (eta < 1) return 0.27614f - 0.87350f * eta + 1.12077f * eta2 - 0.65095f * eta3 + 0.07883f * eta4 + 0.04860f * eta5;
+    Float r_eta = 1 / eta, r_eta2 = r_eta * r_eta, r_eta3 = r_eta2 * r_eta;
+    return -547.033f + 45.3087f * r_eta3 - 218.725f * r_eta2 + 458.843f * r_eta + 404.557f * eta - 189.519f * eta2 +
+           54.9327f * eta3 - 9.00603f * eta4 + 0.63942f * eta5;
+}
+static Float SampleExp(Float u, Float a) { return -CRLog(1 - u) / a; }
+static Float BeamDiffusionMS(Float sigma_s, Float sigma_a, Float g, Float eta, Float r) {
+    const int nSamples = 100;
+    Float Ed = 0;
+    Float sigmap_s = sigma_s * (1 - g), sigmap_t = sigma_a + sigmap_s, rhop = sigmap_s / sigmap_t;
+    Float D_g = (2 * sigma_a + sigmap_s) / (3 * sigmap_t * sigmap_t);
+    Float sigma_tr = SafeSqrt(sigma_a / D_g);
+    Float fm1 = FresnelMoment1(eta), fm2 = FresnelMoment2(eta);
+    Float ze = -2 * D_g * (1 + 3 * fm2) / (1 - 2 * fm1);
+    Float cPhi = 0.25f * (1 - 2 * fm1), cE = 0.5f * (1 - 3 * fm2);
+    const Float Inv4Pi = 0.07957747154594766788f;
+    for (int i = 0; i < nSamples; ++i) {
+        Float zr = SampleExp((i + 0.5f) / nSamples, sigmap_t);
+        Float zv = -zr + 2 * ze;
+        Float dr = std::sqrt(Sqr(r) + Sqr(zr)), dv = std::sqrt(Sqr(r) + Sqr(zv));
+        Float phiD = Inv4Pi / D_g * (FastExp(-sigma_tr * dr) / dr - FastExp(-sigma_tr * dv) / dv);
+        Float EDn = Inv4Pi * (zr * (1 + sigma_tr * dr) * FastExp(-sigma_tr * dr) / (dr * dr * dr) -
+                              zv * (1 + sigma_tr * dv) * FastExp(-sigma_tr * dv) / (dv * dv * dv));
+        Float E = phiD * cPhi + EDn * cE;
+        Float kappa = 1 - FastExp(-2 * sigmap_t * (dr + zr));
+        Ed += kappa * rhop * rhop * E;
+    }
+    return Ed / nSamples;
+}
+static Float BeamDiffusionSS(Float sigma_s, Float sigma_a, Float g, Float eta, Float r) {
+    Float sigma_t = sigma_a + sigma_s, rho = sigma_s / sigma_t;
+    Float tCrit = r * SafeSqrt(Sqr(eta) - 1);
+    Float Ess = 0;
+    const int nSamples = 100;
+    for (int i = 0; i < nSamples; ++i) {
+        Float ti = tCrit + SampleExp((i + 0.5f) / nSamples, sigma_t);
+        Float d = std::sqrt(Sqr(r) + Sqr(ti));
+        Float cosTheta_o = ti / d;
+        Ess += rho * FastExp(-sigma_t * (d + tCrit)) / Sqr(d) * HenyeyGreenstein(cosTheta_o, g) *
+               (1 - FrDielectric(-cosTheta_o, eta)) * std::abs(cosTheta_o);
+    }
+    return Ess / nSamples;
+}
+static std::vector<float> Table(Float g, Float eta) {
+    std::vector<float> t(TableFloats, 0.f);
+    float *rho = t.data(), *rad = rho + NRho, *prof = rad + NRad, *rhoEff = prof + NRho * NRad, *cdf = rhoEff + NRho;
+    rad[0] = 0;
+    rad[1] = 2.5e-3f;
+    for (int i = 2; i < NRad; ++i) rad[i] = rad[i - 1] * 1.2f;
+    for (int i = 0; i < NRho; ++i) rho[i] = (1 - FastExp(-8 * i / (Float)(NRho - 1))) / (1 - FastExp(-8));
+    for (int i = 0; i < NRho; ++i) {
+        for (int j = 0; j < NRad; ++j)
+            prof[i * NRad + j] = 2 * Pi * rad[j] *
+                                 (BeamDiffusionSS(rho[i], 1 - rho[i], g, eta, rad[j]) + BeamDiffusionMS(rho[i], 1 - rho[i], g, eta, rad[j]));
+        // IntegrateCatmullRom
+        const float *f = prof + i * NRad;
+        float *c = cdf + i * NRad;
+        Float sum = 0;
+        c[0] = 0;
+        for (int k = 0; k < NRad - 1; ++k) {
+            Float x0 = rad[k], x1 = rad[k + 1], f0 = f[k], f1 = f[k + 1], width = x1 - x0;
+            Float d0 = k > 0 ? width * (f1 - f[k - 1]) / (x1 - rad[k - 1]) : f1 - f0;
+            Float d1 = k + 2 < NRad ? width * (f[k + 2] - f0) / (rad[k + 2] - x0) : f1 - f0;
+            sum += width * ((f0 + f1) / 2 + (d0 - d1) / 12);
+            c[k + 1] = sum;
+        }
+        rhoEff[i] = sum;
+    }
+    return t;
+}
+template <typename Pred>
+static int FindInterval(int sz, const Pred &pred) {
+    int size = sz - 2, first = 1;
+    while (size > 0) {
+        int half = size >> 1, middle = first + half;
+        bool r = pred(middle);
+        first = r ? middle + 1 : first;
+        size = r ? size - (half + 1) : half;
+    }
+    return std::max(0, std::min(first - 1, sz - 2));
+}
+static bool Weights(const float *nodes, int n, Float x, int *offset, Float w[4]) {
+    if (!(x >= nodes[0] && x <= nodes[n - 1])) return false;
+    int idx = FindInterval(n, [&](int i) { return nodes[i] <= x; });
+    *offset = idx - 1;
+    Float x0 = nodes[idx], x1 = nodes[idx + 1];
+    Float t = (x - x0) / (x1 - x0), t2 = t * t, t3 = t2 * t;
+    w[1] = 2 * t3 - 3 * t2 + 1;
+    w[2] = -2 * t3 + 3 * t2;
+    if (idx > 0) {
+        Float w0 = (t3 - 2 * t2 + t) * (x1 - x0) / (x1 - nodes[idx - 1]);
+        w[0] = -w0;
+        w[2] += w0;
+    } else {
+        Float w0 = t3 - 2 * t2 + t;
+        w[0] = 0;
+        w[1] -= w0;
+        w[2] += w0;
+    }
+    if (idx + 2 < n) {
+        Float w3 = (t3 - t2) * (x1 - x0) / (nodes[idx + 2] - x0);
+        w[1] -= w3;
+        w[3] = w3;
+    } else {
+        Float w3 = t3 - t2;
+        w[1] -= w3;
+        w[2] += w3;
+        w[3] = 0;
+    }
+    return true;
+}
+template <typename F>
+static Float Newton(F f) {
+    Float x0 = 0, x1 = 1;
+    const Float eps = 1e-6f;
+    std::pair<Float, Float> a = f(x0), b = f(x1);
+    if (std::abs(a.first) < eps) return x0;
+    if (std::abs(b.first) < eps) return x1;
+    bool startIsNegative = a.first < 0;
+    Float xMid = x0 + (x1 - x0) * -a.first / (b.first - a.first);
+    while (true) {
+        if (!(x0 < xMid && xMid < x1)) xMid = (x0 + x1) / 2;
+        std::pair<Float, Float> m = f(xMid);
+        if (startIsNegative == (m.first < 0)) x0 = xMid;
+        else x1 = xMid;
+        if ((x1 - x0) < eps || std::abs(m.first) < eps) return xMid;
+        xMid -= m.first / m.second;
+    }
+}
+static Float InvertCatmullRom(const float *x, const float *f, int n, Float u) {
+    if (!(u > f[0])) return x[0];
+    if (!(u < f[n - 1])) return x[n - 1];
+    int i = FindInterval(n, [&](int k) { return f[k] <= u; });
+    Float x0 = x[i], x1 = x[i + 1], f0 = f[i], f1 = f[i + 1], width = x1 - x0;
+    Float d0 = i > 0 ? width * (f1 - f[i - 1]) / (x1 - x[i - 1]) : f1 - f0;
+    Float d1 = i + 2 < n ? width * (f[i + 2] - f0) / (x[i + 2] - x0) : f1 - f0;
+    Float t = Newton([&](Float t) {
+        Float t2 = t * t, t3 = t2 * t;
+        Float Fhat = (2 * t3 - 3 * t2 + 1) * f0 + (-2 * t3 + 3 * t2) * f1 + (t3 - 2 * t2 + t) * d0 + (t3 - t2) * d1;
+        Float fhat = (6 * t2 - 6 * t) * f0 + (-6 * t2 + 6 * t) * f1 + (3 * t2 - 4 * t + 1) * d0 + (3 * t2 - 2 * t) * d1;
+        return std::make_pair(Fhat - u, fhat);
+    });
+    return x0 + t * width;
+}
+static Float SampleCatmullRom2D(const float *n1, int s1, const float *n2, int s2, const float *values, const float *cdf,
+                                Float alpha, Float u) {
+    int offset;
+    Float w[4];
+    if (!Weights(n1, s1, alpha, &offset, w)) return 0;
+    auto interp = [&](const float *a, int idx) {
+        Float v = 0;
+        for (int i = 0; i < 4; ++i)
+            if (w[i] != 0) v += a[(offset + i) * s2 + idx] * w[i];
+        return v;
+    };
+    Float maximum = interp(cdf, s2 - 1);
+    u *= maximum;
+    int idx = FindInterval(s2, [&](int i) { return interp(cdf, i) <= u; });
+    Float f0 = interp(values, idx), f1 = interp(values, idx + 1);
+    Float x0 = n2[idx], x1 = n2[idx + 1], width = x1 - x0, d0, d1;
+    u = (u - interp(cdf, idx)) / width;
+    d0 = idx > 0 ? width * (f1 - interp(values, idx - 1)) / (x1 - n2[idx - 1]) : f1 - f0;
+    d1 = idx + 2 < s2 ? width * (interp(values, idx + 2) - f0) / (n2[idx + 2] - x0) : f1 - f0;
+    Float t = Newton([&](Float t) {
+        // EvaluatePolynomial: FMA Horner
+        Float c3 = (1.f / 3.f) * (-2 * d0 - d1) + f1 - f0, c4 = 0.25f * (d0 + d1) + 0.5f * (f0 - f1);
+        Float Fhat = std::fma(t, std::fma(t, std::fma(t, std::fma(t, c4, c3), 0.5f * d0), f0), 0.f);
+        Float fhat = std::fma(t, std::fma(t, std::fma(t, d0 + d1 + 2 * (f0 - f1), -2 * d0 - d1 + 3 * (f1 - f0)), d0), f0);
+        return std::make_pair(Fhat - u, fhat);
+    });
+    return x0 + width * t;
+}
+struct BSSRDF {
+    const float *rho, *rad, *prof, *rhoEff, *cdf;
+    Vec po, ns;
+    Spectrum sigma_t, rhoS;
+    Spectrum Sr(Float r) const {
+        Spectrum out(0.f);
+        for (int i = 0; i < NS; ++i) {
+            Float rOptical = r * sigma_t[i];
+            int ro, rr;
+            Float rw[4], dw[4];
+            if (!Weights(rho, NRho, rhoS[i], &ro, rw) || !Weights(rad, NRad, rOptical, &rr, dw)) continue;
+            Float sr = 0;
+            for (int j = 0; j < 4; ++j)
+                for (int k = 0; k < 4; ++k)
+                    if (Float weight = rw[j] * dw[k]; weight != 0) sr += weight * prof[(ro + j) * NRad + rr + k];
+            if (rOptical != 0) sr /= 2 * Pi * rOptical;
+            out[i] = sr;
+        }
+        for (int i = 0; i < NS; ++i) out[i] = std::max<Float>(0, out[i] * (sigma_t[i] * sigma_t[i]));
+        return out;
+    }
+    Spectrum PdfSr(Float r) const {
+        Spectrum pdf(0.f);
+        for (int i = 0; i < NS; ++i) {
+            Float rOptical = r * sigma_t[i];
+            int ro, rr;
+            Float rw[4], dw[4];
+            if (!Weights(rho, NRho, rhoS[i], &ro, rw) || !Weights(rad, NRad, rOptical, &rr, dw)) continue;
+            Float sr = 0, re = 0;
+            for (int j = 0; j < 4; ++j)
+                if (rw[j] != 0) {
+                    re += rhoEff[ro + j] * rw[j];
+                    for (int k = 0; k < 4; ++k)
+                        if (dw[k] != 0) sr += prof[(ro + j) * NRad + rr + k] * rw[j] * dw[k];
+                }
+            if (rOptical != 0) sr /= 2 * Pi * rOptical;
+            pdf[i] = sr * (sigma_t[i] * sigma_t[i]) / re;
+        }
+        for (int i = 0; i < NS; ++i) pdf[i] = std::max<Float>(0, pdf[i]);
+        return pdf;
+    }
+    bool SampleSr(Float u, Float *r) const {
+        if (sigma_t[0] == 0) return false;
+        *r = SampleCatmullRom2D(rho, NRho, rad, NRad, prof, cdf, rhoS[0], u) / sigma_t[0];
+        return true;
+    }
+    bool SampleSp(Float u1, Float u20, Float u21, Vec *p0, Vec *p1) const {
+        Vec fx, fy, fz;
+        if (u1 < 0.25f) {
+            fx = ns;
+            CoordinateSystem(ns, &fy, &fz);
+        } else if (u1 < 0.5f) {
+            fy = ns;
+            CoordinateSystem(ns, &fz, &fx);
+        } else {
+            fz = ns;
+            CoordinateSystem(ns, &fx, &fy);
+        }
+        Float r, rMax;
+        if (!SampleSr(u20, &r)) return false;
+        Float phi = 2 * Pi * u21;
+        if (!SampleSr(0.999f, &rMax) || r >= rMax) return false;
+        Float l = 2 * std::sqrt(Sqr(rMax) - Sqr(r));
+        Vec pStart = po + (fx * CRCos(phi) + fy * CRSin(phi)) * r - fz * l / 2;
+        *p0 = pStart;
+        *p1 = pStart + fz * l;
+        return true;
+    }
+    Spectrum PdfSp(Vec pi, Vec ni) const {
+        Vec d = pi - po, x, y;
+        CoordinateSystem(ns, &x, &y);
+        Vec dl(Dot(d, x), Dot(d, y), Dot(d, ns)), nl(DotN(ni, x), DotN(ni, y), DotN(ni, ns));
+        Float rProj[3] = {std::sqrt(Sqr(dl.y) + Sqr(dl.z)), std::sqrt(Sqr(dl.z) + Sqr(dl.x)), std::sqrt(Sqr(dl.x) + Sqr(dl.y))};
+        Float axisProb[3] = {.25f, .25f, .5f};
+        Spectrum pdf(0.f);
+        for (int a = 0; a < 3; ++a) pdf = pdf + PdfSr(rProj[a]) * std::abs(nl[a]) * axisProb[a];
+        return pdf;
+    }
+};
+}  // namespace osss
+
 struct Renderer {
     std::vector<OEnvLight> envs;  // ImageInfiniteLights (flat inf_image)
     // the image light behind global light index li, or null
@@ -4797,6 +5067,7 @@ struct Renderer {
     Media M;
     PixelFilter filt;
     const pbrt_scene_flat *f;
+    std::vector<std::vector<float>> sssTables;  // osss::Table(g, eta) per subsurface material
 
     // TraceTransmittance (wavefront/intersect.h:164-274) up to the light point o + tMax d:
     // closest hits; a non-interface surface blocks (T_ray = 0); interfaces are crossed with
@@ -5261,14 +5532,20 @@ struct Renderer {
             int prim = S.Intersect(ro, rd, Infinity, &ti, false);
             Interaction si;
             if (prim >= 0) si = S.Interact(prim, ti, rd);
-            // GenerateRaySamples: dims 6 + 7 depth (path depth)
+            // GenerateRaySamples: dims 6 + 7 depth (path depth), 6 + 10 depth with subsurface
+            // materials, whose three subsurface dimensions follow (samples.cpp:29-66)
             AnySampler h2 = S.Sampler();
-            h2.Start(px, py, sampleIndex, 6 + 7 * depth);
+            h2.Start(px, py, sampleIndex, 6 + f->dims_per_depth * depth);
             Float dUc = h2.Get1D(), dU0, dU1;
             h2.Get2D(&dU0, &dU1);
             Float iUc = h2.Get1D(), iU0, iU1;
             h2.Get2D(&iU0, &iU1);
             Float rr = h2.Get1D();
+            Float sUc = 0, sU0 = 0, sU1 = 0;
+            if (f->n_sss > 0) {
+                sUc = h2.Get1D();
+                h2.Get2D(&sU0, &sU1);
+            }
             if (haveMedia && medium >= 0) {
                 // SampleMediumInteraction (wavefront/media.cpp:22-247)
                 const Float tHit = prim >= 0 ? ti.t : Infinity;
@@ -5448,7 +5725,7 @@ struct Renderer {
             Vec woL = toLocal(si.wo);
             const int flags = layered ? lay.Flags() : bx.Flags();
             Spectrum oldBeta = beta;
-            bool haveNext = false, nextSpecular = false;
+            bool haveNext = false, nextSpecular = false, toSss = false;
             Vec nextO, nextD;
             Spectrum nb;
             Spectrum nrl;
@@ -5470,6 +5747,8 @@ struct Renderer {
                 }
                 if (nb) {
                     haveNext = true;
+                    // a subsurface material's transmitted sample enters the BSSRDF stage
+                    toSss = (bs.flags & BxT) && f->material_sss && f->material_sss[mat] >= 0;
                     nextSpecular = bs.flags & BxSpecular;
                     nextO = OffsetRayOrigin(si.p, si.err, si.n, wi);
                     nextD = wi;
@@ -5542,6 +5821,174 @@ struct Renderer {
                         }
                     }
                 }
+            }
+            if (haveNext && toSss) {
+                // SampleSubsurface (wavefront/subsurface.cpp:18-206): GetBSSRDF, SampleSp with
+                // the subsurface samples, IntersectOneRandom over the probe segment, then the
+                // exit vertex's NormalizedFresnelBxDF: indirect ray and light sample
+                const int k = f->material_sss[mat];
+                const float *P = f->sss_params + 20 * k;
+                const float *T = sssTables[k].data();
+                osss::BSSRDF bd;
+                bd.rho = T;
+                bd.rad = T + osss::NRho;
+                bd.prof = bd.rad + osss::NRad;
+                bd.rhoEff = bd.prof + osss::NRho * osss::NRad;
+                bd.cdf = bd.rhoEff + osss::NRho;
+                bd.po = si.p;
+                bd.ns = si.ns;
+                auto specAt = [&](const float *q, Float lam) -> Float {
+                    const int kind = (int)q[0];
+                    if (kind == 0) return q[1];
+                    if (kind == 1) return q[5] * Sigmoid(q[2], q[3], q[4], lam);
+                    const int pl = (int)q[6], a = f->pl_offsets[pl];
+                    return PLEval(f->pl_lambda + a, f->pl_value + a, f->pl_offsets[pl + 1] - a, lam);
+                };
+                for (int i = 0; i < NS; ++i) {
+                    const Float lam = lambda.lambda[i];
+                    Float sa, ss;
+                    if (P[0] == 0) {
+                        sa = std::max<Float>(0, P[1] * specAt(P + 4, lam));
+                        ss = std::max<Float>(0, P[1] * specAt(P + 11, lam));
+                    } else {
+                        const Float mfree = std::max<Float>(0, P[1] * specAt(P + 11, lam));
+                        const Float rh = osss::InvertCatmullRom(bd.rho, bd.rhoEff, osss::NRho, Clamp(specAt(P + 4, lam), 0, 1));
+                        ss = rh / mfree;
+                        sa = (1 - rh) / mfree;
+                    }
+                    bd.sigma_t[i] = sa + ss;
+                    bd.rhoS[i] = bd.sigma_t[i] != 0 ? ss / bd.sigma_t[i] : 0;
+                }
+                Vec p0, p1;
+                if (!bd.SampleSp(sUc, sU0, sU1, &p0, &p1)) break;
+                const uint64_t hseed = HashFloats(p0.x, p0.y, p0.z, p1.x, p1.y, p1.z);
+                PCG32 wrs(hseed, Mix64(hseed));  // WeightedReservoirSampler::Seed: RNG::SetSequence
+                Float wsum = 0;
+                int chosen = -1;
+                TriIsect cti{};
+                Vec cdir;
+                Vec po = p0, pd = p1 - p0;
+                for (int it = 1; LengthSquared(pd) > 0 && it < 100; ++it) {
+                    TriIsect t2;
+                    const int hp = S.Intersect(po, pd, 1, &t2, false);
+                    if (hp < 0) break;
+                    const Interaction hi = S.Interact(hp, t2, pd);
+                    if (S.Material(hp) == mat) {
+                        wsum += 1;
+                        if (wrs.Uniform() < 1 / wsum) chosen = hp, cti = t2, cdir = pd;
+                    }
+                    pd = p1 - hi.p;
+                    po = OffsetRayOrigin(hi.p, hi.err, hi.n, pd);
+                }
+                if (chosen < 0 || !(wsum > 0)) break;
+                const Float resPdf = 1 / wsum;
+                const Interaction ex = S.Interact(chosen, cti, cdir);
+                const Spectrum Sp = bd.Sr(Length(bd.po - ex.p)), pdfSp = bd.PdfSp(ex.p, ex.n);
+                if (!Sp || !pdfSp) break;
+                const Float pr = resPdf * pdfSp[0];
+                const Spectrum betap = nb * Sp / pr;
+                const Spectrum ru2 = r_u * pdfSp / pdfSp[0];
+                const Float eta = P[2], fc = P[3];
+                Vec ex_ = Normalize(ex.dpdus), ez_ = ex.ns, ey_ = Cross(ez_, ex_);
+                auto toL = [&](Vec v) { return Vec(Dot(v, ex_), Dot(v, ey_), Dot(v, ez_)); };
+                const Vec woS = toL(ex.ns);
+                auto nfF = [&](Vec wiL) -> Float {  // NormalizedFresnelBxDF::f (bxdfs.h:1249-1261)
+                    if (!(woS.z * wiL.z > 0)) return 0;
+                    const Float fv = (1 - FrDielectric(wiL.z, eta)) / (fc * Pi);
+                    return fv * Sqr(eta);
+                };
+                auto nfPdf = [&](Vec wiL) -> Float { return woS.z * wiL.z > 0 ? std::abs(wiL.z) * InvPi : 0; };
+                bool haveNext2 = false;
+                Spectrum nb2, nrl2;
+                Vec nO, nD;
+                if (woS.z != 0) {
+                    Vec wiL = SampleCosineHemisphere(iU0, iU1);
+                    if (woS.z < 0) wiL.z *= -1;
+                    const Float fv = nfF(wiL), pv = nfPdf(wiL);
+                    if (fv != 0 && pv != 0 && wiL.z != 0) {
+                        const Vec wi = ex_ * wiL.x + ey_ * wiL.y + ez_ * wiL.z;
+                        Spectrum b = betap * fv * AbsDotN(ex.ns, wi) / pv;
+                        const Spectrum rl = ru2 / pv;
+                        const Spectrum rrBeta = b * nextEtaScale / ru2.Average();
+                        if (rrBeta.Max() < 1 && depth > 1) {
+                            const Float q = std::max<Float>(0, 1 - rrBeta.Max());
+                            if (rr < q) b = Spectrum(0.f);
+                            else b = b / (1 - q);
+                        }
+                        if (b) {
+                            haveNext2 = true;
+                            nb2 = b;
+                            nrl2 = rl;
+                            nO = OffsetRayOrigin(ex.p, ex.err, ex.n, wi);
+                            nD = wi;
+                        }
+                    }
+                }
+                // direct lighting from the exit point (LightSampleContext(pi, n, ns), no offset)
+                int li;
+                Float lpmf;
+                DeltaSample ds;
+                const bool sampledL = woS.z != 0 && lights.Sample(ex.p, ex.ns, dUc, &li, &lpmf);
+                const OEnvLight *E = sampledL ? EnvOf(li) : nullptr;
+                Float eu, ev, emap;
+                if (E) {
+                    if (E->Sample(dU0, dU1, &eu, &ev, &emap)) {
+                        const int kk = li - f->n_area_lights - f->n_point_spot;
+                        Vec wi = OEnvLight::Mul(E->m, OEnvLight::SquareToSphere(eu, ev));
+                        Vec lp = ex.p + wi * (2 * f->scene_radius);
+                        Spectrum Le = E->Le(eu, ev, lambda, f->dense_spectra + 311 * f->inf_spectrum[kk], f->inf_scale[kk]);
+                        const Float fv = nfF(toL(wi));
+                        if (Le && fv != 0) {
+                            Spectrum b2 = betap * fv * AbsDotN(ex.ns, wi);
+                            Float lightPDF = emap / (4 * Pi) * lpmf;
+                            Spectrum ru = ru2 * nfPdf(toL(wi)), rl = ru2 * lightPDF;
+                            Vec pf = OffsetRayOrigin(ex.p, ex.err, ex.n, lp - ex.p);
+                            shadow(pf, lp - pf, DotN(ex.n, lp - pf) > 0 ? mOut : mIn, b2 * Le, ru, rl);
+                        }
+                    }
+                } else if (sampledL && li >= f->n_area_lights && DeltaLi(li, ex.p, lambda, &ds)) {
+                    const Float fv = nfF(toL(ds.wi));
+                    if (fv != 0) {
+                        Spectrum b2 = betap * fv * AbsDotN(ex.ns, ds.wi);
+                        Spectrum ru = ru2 * 0.f, rl = ru2 * (1 * lpmf);
+                        Vec pf = OffsetRayOrigin(ex.p, ex.err, ex.n, ds.p - ex.p);
+                        shadow(pf, ds.p - pf, DotN(ex.n, ds.p - pf) > 0 ? mOut : mIn, b2 * ds.L, ru, rl);
+                    }
+                } else if (sampledL && li < f->n_area_lights) {
+                    ShapeSample ss;
+                    if (sampleArea(li, ex.p, ex.err, ex.n, ex.ns, dU0, dU1, &ss) && ss.pdf != 0 &&
+                        LengthSquared(ss.p - ex.p) != 0) {
+                        Vec wi = Normalize(ss.p - ex.p);
+                        const Spectrum Le = SampledAreaL(li, ss.n, wi, lambda, ss.uv);
+                        if (Le) {
+                            const Float fv = nfF(toL(wi));
+                            if (fv != 0) {
+                                Spectrum b2 = betap * fv * AbsDotN(ex.ns, wi);
+                                Float lightPDF = ss.pdf * lpmf;
+                                Spectrum ru = ru2 * nfPdf(toL(wi)), rl = ru2 * lightPDF;
+                                Vec pf = OffsetRayOrigin(ex.p, ex.err, ex.n, ss.p - ex.p);
+                                Vec pt = OffsetRayOrigin(ss.p, ss.err, ss.n, pf - ss.p);
+                                shadow(pf, pt - pf, DotN(ex.n, pt - pf) > 0 ? mOut : mIn, b2 * Le, ru, rl);
+                            }
+                        }
+                    }
+                }
+                if (!haveNext2) break;
+                beta = nb2;
+                r_u = ru2;
+                r_l = nrl2;
+                specularBounce = false;
+                anyNonSpecular = true;
+                etaScale = nextEtaScale;
+                prevP = ex.p;
+                prevErr = ex.err;
+                prevN = ex.n;
+                prevNs = ex.ns;
+                medium = DotN(ex.n, nD) > 0 ? mOut : mIn;
+                ro = nO;
+                rd = nD;
+                ++depth;
+                continue;
             }
             if (!haveNext) break;
             beta = nb;
@@ -5768,6 +6215,30 @@ struct Renderer {
 using namespace oracle;
 
 extern "C" {
+// the oracle's Catmull-Rom restatements (tests against tests/golden "catmull_rom"): op 0
+// CatmullRomWeights over nodes1 -> [n][6] ok offset w0..w3; 1 InvertCatmullRom(nodes1, values)
+// -> [n]; 2 IntegrateCatmullRom-free (unused); 3 SampleCatmullRom2D(x[2i] alpha, x[2i+1] u) -> [n]
+void oracle_catmull_rom(int op, const float *nodes1, int n1, const float *nodes2, int n2, const float *values,
+                        const float *cdf, const float *x, int n, float *out) {
+    for (int i = 0; i < n; ++i) {
+        if (op == 0) {
+            int off = 0;
+            Float w[4] = {0, 0, 0, 0};
+            const bool ok = osss::Weights(nodes1, n1, x[i], &off, w);
+            const float r[6] = {ok ? 1.f : 0.f, (float)(ok ? off : 0), w[0], w[1], w[2], w[3]};
+            std::copy(r, r + 6, out + 6 * i);
+        } else if (op == 1) {
+            out[i] = osss::InvertCatmullRom(nodes1, values, n1, x[i]);
+        } else if (op == 3) {
+            out[i] = osss::SampleCatmullRom2D(nodes1, n1, nodes2, n2, values, cdf, x[2 * i], x[2 * i + 1]);
+        }
+    }
+}
+// the oracle's own BSSRDF table for (g, eta) (osss::Table), kSssTableFloats floats
+void oracle_sss_table(float g, float eta, float *out) {
+    const std::vector<float> t = osss::Table(g, eta);
+    std::copy(t.begin(), t.end(), out);
+}
 
 // Transcendental mode of every later call (see CRSin): 0 = libm float (reference), 1 = CR
 void oracle_set_cr_math(int on) { g_mathMode = on ? 1 : 0; }
@@ -5872,6 +6343,7 @@ static int RenderRows(const pbrt_scene_flat *flat, const pbrt_scene_info *info, 
     r.M.f = flat;
     r.M.n = flat->n_media;
     r.filt.Init(flat->filter_type, info->filter_radius_x, info->filter_radius_y, flat->filter_a, flat->filter_b);
+    for (int k = 0; k < flat->n_sss; ++k) r.sssTables.push_back(osss::Table(flat->sss_params[20 * k + 18], flat->sss_params[20 * k + 2]));
     hostMath.Done();
     size_t npix = (size_t)info->xres * info->yres;
     std::atomic<int> next(0);

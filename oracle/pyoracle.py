@@ -34,6 +34,10 @@ def lib():
         _lib.oracle_sampler.argtypes = [ctypes.c_int] * 9 + [ctypes.c_void_p] * 3 + [ctypes.c_int] * 4 + [ctypes.c_void_p]
         _lib.oracle_rng.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]
         _lib.oracle_procedural.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 3 + [ctypes.c_int, ctypes.c_void_p]
+        _lib.oracle_sss_table.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_void_p]
+        _lib.oracle_catmull_rom.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                            ctypes.c_void_p]
         vp = ctypes.c_void_p
         _lib.oracle_warps.argtypes = [vp, vp, vp]
         _lib.oracle_spherical_triangle.argtypes = [vp, vp, vp, vp]
@@ -358,6 +362,27 @@ def rng(seq, advance):
     out = np.zeros(2, np.uint32)
     lib().oracle_rng(int(seq), int(advance), out.ctypes.data)
     return int(out[0]), int(out[1])
+
+
+SSS_TABLE_FLOATS = 100 + 64 + 2 * 100 * 64 + 100
+
+
+def sss_table(g, eta):
+    """The oracle's BSSRDF table for (g, eta): rho[100], radius[64], profile[100][64], rhoEff[100],
+    profileCDF[100][64] (ComputeBeamDiffusionBSSRDF restated)."""
+    out = np.zeros(SSS_TABLE_FLOATS, np.float32)
+    lib().oracle_sss_table(float(g), float(eta), out.ctypes.data)
+    return out
+
+
+def catmull_rom(op, nodes1, nodes2, values, cdf, x):
+    """The oracle's spline restatements: op 0 weights [n][6], 1 invert [n], 3 sample2d (x: [n][2])."""
+    a = [np.ascontiguousarray(v, np.float32) for v in (nodes1, nodes2, values, cdf, x)]
+    n = len(a[4]) // 2 if op == 3 else len(a[4])
+    out = np.zeros(n * 6 if op == 0 else n, np.float32)
+    lib().oracle_catmull_rom(op, a[0].ctypes.data, len(a[0]), a[1].ctypes.data, len(a[1]), a[2].ctypes.data,
+                             a[3].ctypes.data, a[4].ctypes.data, n, out.ctypes.data)
+    return out.reshape(-1, 6) if op == 0 else out
 
 
 def procedural(kind, perm, params4, in9):

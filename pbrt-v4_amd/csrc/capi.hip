@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/pbrt_amd.h"
+#include "core/bssrdf.h"
 #include "host/bvh.h"
 #include "host/image.h"
 #include "host/scene.h"
@@ -103,6 +104,31 @@ static void MediumTables(const SceneDesc &s, std::vector<int32_t> *info, std::ve
         for (int i = 0; i < 4; ++i)
             for (int j = 0; j < 4; ++j) params->push_back((float)inv[i][j]);
     }
+}
+
+// Subsurface tables (pbrt_scene_flat::material_sss / sss_params / sss_tables; the device
+// upload uses the same layout): per material its SubsurfaceDesc or -1, per desc kSssParams
+// floats {mode, scale, eta, fresnelC, a: kind value c0 c1 c2 scale pl, b: the same, g, 0} and
+// its kSssTableFloats table.  Empty when no material has subsurface scattering.
+static void SssTables(const SceneDesc &s, std::vector<int32_t> *matSss, std::vector<float> *params,
+                      std::vector<float> *tables) {
+    matSss->clear();
+    params->clear();
+    tables->clear();
+    if (s.sss.empty()) return;
+    for (const MaterialDesc &m : s.materials) matSss->push_back(m.sss);
+    auto spec = [&](const SssSpectrumDesc &q) {
+        params->insert(params->end(), {(float)q.kind, q.value, q.c0, q.c1, q.c2, q.scale, (float)q.pl});
+    };
+    for (const SubsurfaceDesc &d : s.sss) {
+        if ((int)d.table.size() != kSssTableFloats) throw Error("subsurface table has the wrong size");
+        params->insert(params->end(), {(float)d.mode, d.scale, d.eta, d.fresnelC});
+        spec(d.a);
+        spec(d.b);
+        params->insert(params->end(), {d.g, 0.f});
+        tables->insert(tables->end(), d.table.begin(), d.table.end());
+    }
+    static_assert(kSssParams == 20, "SubsurfaceDesc packing");
 }
 
 // Texture tables in the device layout (core/texture_eval.h), built on the host: uploaded by
@@ -268,7 +294,8 @@ struct pbrt_scene {
     // flattened copies for pbrt_scene_get_flat
     std::vector<float> verts, matCoeffs, lightScale, infScale, dense, sensor, nodeBounds, matParams, plLambda, plValue,
         mediumParams, mediumValues, matLayer;
-    std::vector<int32_t> mediumInfo;
+    std::vector<int32_t> mediumInfo, matSss;
+    std::vector<float> sssParams, sssTables;
     std::vector<int32_t> tris, lightPrim, lightSpectrum, lightTwoSided, infSpectrum, matConstant, nodeInfo, matType,
         matSpectra, plOffsets, infDistant, uniformOrder;
     std::vector<float> deltaLights, deltaImages, lightSpread, areaImages;
@@ -333,6 +360,7 @@ struct pbrt_scene {
             matSpectra.insert(matSpectra.end(), {m.etaSpec, m.kSpec});
         }
         MediumTables(s, &mediumInfo, &mediumParams, &mediumValues);
+        SssTables(s, &matSss, &sssParams, &sssTables);
         plOffsets.assign(1, 0);
         plLambda.clear();
         plValue.clear();
@@ -451,7 +479,9 @@ struct pbrt_context {
     bool hasSpread = false;
     DevBuf<float> deltaImg, lightImg;
     DevBuf<int> lightImgOff;
-    DevBuf<int> primOrig, matType, matSpectra, plOffsets;
+    DevBuf<int> primOrig, matType, matSpectra, plOffsets, matSss;
+    DevBuf<float> sssParams, sssTables, sssF;
+    DevBuf<int> sssI;
     DevBuf<float> matParams, plLambda, plValue, triShade, matLayer, dispL0;
     DevBuf<uint16_t> plIndex;
     DevBuf<int> dispTerm;
@@ -765,6 +795,16 @@ static void BuildDevice(pbrt_context *c) {
                                  (m.albedoConstant || grey) ? 1.f : 0.f, m.cAlphaX, m.cAlphaY, (float)m.ifaceEtaSpec});
         }
         c->matLayer.Upload(ml);
+        {
+            std::vector<int32_t> ms;
+            std::vector<float> sp, stb;
+            SssTables(s, &ms, &sp, &stb);
+            if (!ms.empty()) {
+                c->matSss.Upload(ms);
+                c->sssParams.Upload(sp);
+                c->sssTables.Upload(stb);
+            }
+        }
         c->matType.Upload(mt);
         c->matParams.Upload(mp);
         c->matSpectra.Upload(msp);
@@ -1024,6 +1064,9 @@ static void BuildDevice(pbrt_context *c) {
     if (S.dispersive && !s.media.empty())
         throw std::runtime_error("a dielectric with spectral eta (dispersion) together with participating media is not supported yet");
     c->volumetric = c->volumetric || S.dispersive;
+    // subsurface scattering: its r_u becomes spectral (subsurface.cpp:61), so the volumetric
+    // kernels (spectral r_u / r_l records) render it
+    c->volumetric = c->volumetric || !s.sss.empty();
     S.media.cameraMedium = s.cameraMedium;
     S.media.allGrey = 1;
     for (size_t m = 0; m < s.media.size(); ++m) {
@@ -1062,6 +1105,10 @@ static void BuildDevice(pbrt_context *c) {
     S.matConstant = c->matConstant.p;
     S.nMaterials = (int)s.materials.size();
     S.matType = c->matType.p;
+    S.matSss = s.sss.empty() ? nullptr : c->matSss.p;
+    S.sssParams = c->sssParams.p;
+    S.sssTables = c->sssTables.p;
+    S.dimsPerDepth = s.sss.empty() ? 7 : 10;  // samples.cpp:39-41
     S.matParams = (const float4 *)c->matParams.p;
     S.matSpectra = c->matSpectra.p;
     S.matLayer = (const float4 *)c->matLayer.p;
@@ -1557,6 +1604,39 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
             HIPCHECK(hipMemset(c->queueHoles.p, 0, sizeof(int)));
         }
         v.holes = c->queueHoles.p;
+        v.sss = SssRecords{};
+        if (!c->desc.sss.empty()) {
+            c->sssF.Alloc((size_t)(2 * 31 + 3 + 3 + 2 + 3 + 1) * NR);
+            c->sssI.Alloc((size_t)7 * NR);
+            float *sf = c->sssF.p;
+            int *si = c->sssI.p;
+            auto sF = [&](int k) {
+                float *r = sf;
+                sf += (size_t)k * NR;
+                return r;
+            };
+            auto sI = [&](int k) {
+                int *r = si;
+                si += (size_t)k * NR;
+                return r;
+            };
+            SssRecords &q = v.sss;
+            q.beta = sF(31);
+            q.ru = sF(31);
+            q.po = sF(3);
+            q.ns = sF(3);
+            q.lambda0 = sF(1);
+            q.etaScale = sF(1);
+            q.hitB = sF(3);
+            q.resPdf = sF(1);
+            q.mat = sI(1);
+            q.pixel = sI(1);
+            q.depth = sI(1);
+            q.mIn = sI(1);
+            q.mOut = sI(1);
+            q.flags = sI(1);
+            q.hitPrim = sI(1);
+        }
     }
     if (!c->devStats.p) {
         c->devStats.Alloc(kStatsSlots);
@@ -1974,6 +2054,11 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
         f->vdc_sobol_inv = sob.vdcInv.data();
     }
     f->material_type = scene->matType.data();
+    f->n_sss = (int)s.sss.size();
+    f->material_sss = s.sss.empty() ? nullptr : scene->matSss.data();
+    f->sss_params = s.sss.empty() ? nullptr : scene->sssParams.data();
+    f->sss_tables = s.sss.empty() ? nullptr : scene->sssTables.data();
+    f->dims_per_depth = s.sss.empty() ? 7 : 10;
     f->material_params = scene->matParams.data();
     f->material_layer = scene->matLayer.data();
     f->material_spectra = scene->matSpectra.data();
@@ -2317,6 +2402,27 @@ int pbrt_debug_check_rn_math(int device, uint64_t seed, int64_t n, int64_t *mism
     } catch (const std::exception &e) {
         return Fail(e.what());
     }
+}
+
+int pbrt_debug_catmull_rom(int op, const float *nodes1, int n1, const float *nodes2, int n2, const float *values,
+                           const float *cdf, const float *x, int n, float *out) {
+    if (!nodes1 || !x || !out || n < 0 || n1 < 2 || (op == 3 && (!nodes2 || n2 < 2 || !values || !cdf)) ||
+        (op == 1 && !values) || (op != 0 && op != 1 && op != 3))
+        return Fail("pbrt_debug_catmull_rom: bad arguments");
+    for (int i = 0; i < n; ++i) {
+        if (op == 0) {
+            int off = 0;
+            float w[4] = {0, 0, 0, 0};
+            const bool ok = CatmullRomWeights(nodes1, n1, x[i], &off, w);
+            const float r[6] = {ok ? 1.f : 0.f, (float)(ok ? off : 0), w[0], w[1], w[2], w[3]};
+            std::copy(r, r + 6, out + 6 * i);
+        } else if (op == 1) {
+            out[i] = InvertCatmullRom(nodes1, values, n1, x[i]);
+        } else {
+            out[i] = SampleCatmullRom2D(nodes1, n1, nodes2, n2, values, cdf, x[2 * i], x[2 * i + 1]);
+        }
+    }
+    return 0;
 }
 
 int64_t pbrt_debug_halton_fastpath_mismatches(const pbrt_scene *scene, int dim, uint32_t a0, uint32_t a1,

@@ -667,7 +667,7 @@ class Parser {
         // shading-normal perturbation (materials.cpp: GetFloatTextureOrNull("displacement"),
         // scene.cpp normal map cache: Image::Read(normalmap, ColorEncoding::Linear)), for the
         // diffuse, dielectric and conductor materials of the surface wavefront
-        if (type == "diffuse" || type == "dielectric" || type == "conductor") {
+        if (type == "diffuse" || type == "dielectric" || type == "conductor" || type == "subsurface") {
             if (Param *d = ps.Find("displacement")) {
                 MatTexPending &mp = PendingTex(ps.loc);
                 mp.hasDisp = true;
@@ -735,6 +735,85 @@ class Parser {
                 m.etaSpec = SpectrumParam(es, ps.loc);
             }
             Roughness(ps, &m);
+        } else if (type == "subsurface") {
+            // SubsurfaceMaterial::Create (materials.cpp:544-613): a DielectricBxDF(eta, roughness)
+            // at the surface and a TabulatedBSSRDF below it
+            m.type = kMatDielectric;
+            SubsurfaceDesc d;
+            d.g = (float)ps.GetFloat("g", 0.0f);
+            const std::string nm = ps.GetString("name", "");
+            auto unbounded = [&](float r, float g, float b) {
+                // RGBUnboundedSpectrum(sRGB, rgb) (util/spectrum.cpp:230-244)
+                SssSpectrumDesc q;
+                const float mx = std::max({r, g, b});
+                q.kind = 1;
+                q.scale = 2 * mx;
+                const auto c = q.scale ? RGBToSigmoidCoeffs(r / q.scale, g / q.scale, b / q.scale) : RGBToSigmoidCoeffs(0, 0, 0);
+                q.c0 = c[0], q.c1 = c[1], q.c2 = c[2];
+                return q;
+            };
+            // GetSpectrumTexture(name, SpectrumType) of a constant (no textures here yet)
+            auto param = [&](Param *p, bool albedo) {
+                if (p->type == "texture") throw Error(ps.loc + ": textured \"" + p->name + "\" for the subsurface material is not supported yet");
+                if (p->type == "rgb") {
+                    if (p->nums.size() != 3) throw Error(ps.loc + ": " + p->name + " needs 3 values");
+                    const float r = (float)p->nums[0], g = (float)p->nums[1], b = (float)p->nums[2];
+                    if (albedo) {
+                        if (r < 0 || r > 1 || g < 0 || g > 1 || b < 0 || b > 1)
+                            throw Error(ps.loc + ": RGB parameter \"" + p->name + "\" used as an albedo has > 1 component.");
+                        SssSpectrumDesc q;
+                        q.kind = 1;
+                        q.scale = 1;
+                        const auto c = RGBToSigmoidCoeffs(r, g, b);
+                        q.c0 = c[0], q.c1 = c[1], q.c2 = c[2];
+                        return q;
+                    }
+                    if (r < 0 || g < 0 || b < 0) throw Error(ps.loc + ": RGB parameter \"" + p->name + "\" has negative component.");
+                    return unbounded(r, g, b);
+                }
+                if (p->type == "spectrum") {
+                    SssSpectrumDesc q;
+                    q.kind = 2;
+                    q.pl = SpectrumParam(p, ps.loc);
+                    return q;
+                }
+                throw Error(ps.loc + ": \"" + p->type + " " + p->name + "\" is not supported for the subsurface material yet");
+            };
+            if (!nm.empty()) {
+                // GetMediumScatteringProperties (media.cpp:74-151, 160-165): measured sigma'_s and
+                // sigma_a in mm^-1 as RGBUnboundedSpectrum; g forced to 0
+                auto it = GetSpectralData().mediumPresets.find(nm);
+                if (it == GetSpectralData().mediumPresets.end()) throw Error(ps.loc + ": " + nm + ": named medium not found.");
+                if (d.g != 0) std::fprintf(stderr, "%s: Warning: Non-zero \"g\" ignored with named scattering coefficients.\n", ps.loc.c_str());
+                d.g = 0;
+                const auto &pv = it->second;
+                d.a = unbounded(pv[3], pv[4], pv[5]);
+                d.b = unbounded(pv[0], pv[1], pv[2]);
+            } else {
+                Param *sa = ps.Find("sigma_a"), *ss = ps.Find("sigma_s");
+                if (sa && !ss) throw Error(ps.loc + ": Provided \"sigma_a\" parameter without \"sigma_s\".");
+                if (ss && !sa) throw Error(ps.loc + ": Provided \"sigma_s\" parameter without \"sigma_a\".");
+                if (sa) {
+                    d.a = param(sa, false);
+                    d.b = param(ss, false);
+                } else if (Param *refl = ps.Find("reflectance")) {
+                    d.mode = 1;
+                    d.a = param(refl, true);
+                    if (Param *mfp = ps.Find("mfp")) d.b = param(mfp, false);
+                    else d.b.kind = 0, d.b.value = 1;  // ConstantSpectrum(1)
+                } else {
+                    d.a = unbounded(.0011f, .0024f, .014f);
+                    d.b = unbounded(2.55f, 3.21f, 3.77f);
+                }
+            }
+            d.scale = (float)ps.GetFloat("scale", 1.f);
+            d.eta = (float)ps.GetFloat("eta", 1.33f);
+            m.eta = d.eta;
+            Roughness(ps, &m);
+            d.fresnelC = 1 - 2 * FresnelMoment1(1 / d.eta);
+            d.table = ComputeBeamDiffusionTable(d.g, d.eta);
+            m.sss = (int)scene.sss.size();
+            scene.sss.push_back(std::move(d));
         } else if (type == "diffusetransmission") {
             // DiffuseTransmissionMaterial::Create (materials.cpp:620-645): reflectance and
             // transmittance default 0.25, scale 1; the transmittance rides in the albedo fields

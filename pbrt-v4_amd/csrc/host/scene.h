@@ -102,7 +102,29 @@ struct MaterialDesc {
     // bump / normal mapping (materials.h:86-160): the displacement's program and node, the
     // normal map's image (SceneDesc::images); -1 when absent
     int texDisp = -1, dispNode = -1, normalMap = -1;
+    // SubsurfaceMaterial: a dielectric-typed material (its DielectricBxDF from eta and the
+    // alphas) with SceneDesc::sss[sss] as its BSSRDF; -1 for every other material
+    int sss = -1;
     std::string name;
+};
+
+// SubsurfaceMaterial's BSSRDF parameters (materials.h:772-866, materials.cpp:544-613): one of
+// its four forms reduced to sigma_a / sigma_s (mode 0: named preset, given, or the defaults)
+// or reflectance / mfp (mode 1, SubsurfaceFromDiffuse per wavelength), each a constant
+// spectrum: kind 0 ConstantSpectrum(value), 1 scale * sigmoid(c0, c1, c2) (RGBUnbounded; an
+// RGBAlbedo reflectance with scale 1), 2 PiecewiseLinearSpectrum SceneDesc::plSpectra[pl].
+// The table is ComputeBeamDiffusionBSSRDF(g, eta) (host/bssrdf.cpp); fresnelC = 1 - 2
+// FresnelMoment1(1 / eta) for NormalizedFresnelBxDF.
+struct SssSpectrumDesc {
+    int kind = 0;
+    float value = 0, c0 = 0, c1 = 0, c2 = 0, scale = 1;
+    int pl = -1;
+};
+struct SubsurfaceDesc {
+    int mode = 0;
+    SssSpectrumDesc a, b;  // sigma_a, sigma_s | reflectance, mfp
+    float scale = 1, eta = 1.33f, g = 0, fresnelC = 0;
+    std::vector<float> table;
 };
 
 // ---- textures (textures.h / textures.cpp, util/mipmap.*, util/image.*) --------------------
@@ -329,6 +351,7 @@ struct SceneDesc {
     std::vector<AnalyticShapeDesc> shapes;  // spheres and disks
 
     std::vector<MaterialDesc> materials;
+    std::vector<SubsurfaceDesc> sss;  // MaterialDesc::sss
     std::vector<MediumDesc> media;
     int cameraMedium = -1;                          // -1: vacuum
     std::vector<std::array<int16_t, 2>> triMedium;  // {inside, outside}; empty if no media
@@ -460,5 +483,10 @@ PLSpectrumDesc NamedPiecewiseLinear(const std::string &name);
 // Hash / permutation (util/hash.h:19, util/math.h:728)
 uint64_t MurmurHash64A(const unsigned char *key, size_t len, uint64_t seed);
 const std::vector<int> &Primes();
+
+// host/bssrdf.cpp
+std::vector<float> ComputeBeamDiffusionTable(float g, float eta);
+float FresnelMoment1(float eta);
+float FresnelMoment2(float eta);
 
 }  // namespace pbrt_amd

@@ -54,7 +54,7 @@ struct ShadeLdsLayout {
 // bounds every shard, and the records need no more memory than an unsharded queue.
 constexpr int kShards = 8;
 constexpr int kCounterPad = 64;  // ints between counters (256 B)
-constexpr int kNumQueues = 7;
+constexpr int kNumQueues = 8;
 constexpr int kCntRay = 0, kCntMat = 1, kCntShadow = 2, kCntEscaped = 3, kCntEmissive = 4;
 // per-material-type queues (pbrt's MaterialEvalQueue per Material::Types, surfscatter.cpp:39-55):
 // diffuse uses kCntMat, dielectric kCntMat + 4, conductor kCntMat + 5
@@ -232,6 +232,15 @@ struct DeviceScene {
     // sampler: 0 Halton, 1 ZSobol, 2 independent, 3 stratified, 4 Sobol, 5 padded Sobol (core.h kSampler*)
     int samplerType;
     SamplerDesc samp;  // the last four (core.h GenericSampler)
+    // sampler dimensions per path depth: 7, or 10 when a material has subsurface scattering
+    // (samples.cpp:39-41: direct 3, indirect 4, subsurface 3)
+    int dimsPerDepth;
+    // SubsurfaceMaterial (materials.h:772-866): per material its SubsurfaceDesc index or -1
+    // (nullptr: no subsurface material); per desc kSssParams floats (volpath.hip SssParam*) and
+    // a kSssTableFloats BSSRDF table (core/bssrdf.h)
+    const int *matSss;
+    const float *sssParams;
+    const float *sssTables;
     ZSobolParams zs;
     const uint8_t (*zsPerms)[4];  // [24][4]
     const uint32_t *sobolM1;      // Sobol' dimension-1 matrix rows [52]
@@ -342,6 +351,17 @@ struct VolRecords {
 constexpr int kVRay = 0, kVSurf = 1, kVShadow = 2, kVMed = 3, kVScat = 4;
 constexpr int kVIface = 5;  // surface hits on Material "interface" (k_viface)
 constexpr int kVEsc = 6;    // escaped rays (k_vescaped)
+constexpr int kVSss = 7;    // transmitted rays into a subsurface material (k_vsss_probe / _scatter)
+constexpr int kSssParams = 20;
+// BSSRDF work items (GetBSSRDFAndProbeRayWorkItem + SubsurfaceScatterWorkItem,
+// wavefront/workitems.h:202-240), compacted: the entry point's state, then the probe's result
+struct SssRecords {
+    float *beta, *ru;          // [31][NR] after the entry BSDF sample and Russian roulette
+    float *po, *ns;            // [3][NR] entry point and shading normal (TabulatedBSSRDF)
+    float *lambda0, *etaScale; // [NR]
+    float *hitB, *resPdf;      // [3][NR] the reservoir's hit (barycentrics / shape coords), [NR]
+    int *mat, *pixel, *depth, *mIn, *mOut, *flags, *hitPrim;  // [NR] (flags: kUni* bits)
+};
 struct VolState {
     VolRecords rec[2];
     int *hitPrim;  // [NR] this iteration's closest hit (-1: none)
@@ -354,6 +374,7 @@ struct VolState {
     int *shPixel, *shMedium;   // [NR]
     int *shFlags;              // [NR] uniform-spectrum bits (volpath.hip kShUni*)
     int *holes;                // [1] queue-integrity diagnostic: unwritten queue slots found
+    SssRecords sss;            // allocated when a material has subsurface scattering
 };
 
 }  // namespace pbrt_amd

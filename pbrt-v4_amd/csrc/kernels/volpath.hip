@@ -26,6 +26,7 @@
 #define PBRT_VOL_EXPERIMENT 0  // timing experiments only (tools/exp_*.sh), never in the product
 #endif
 #include "common.h"
+#include "../core/bssrdf.h"
 
 namespace pbrt_amd {
 
@@ -477,7 +478,7 @@ __device__ inline VRaySamples RaySamplesAt(const DeviceScene &S, const PathState
     int px, py, sampleIndex;
     PixelOf(st, slot, &px, &py, &sampleIndex);
     px += S.px0;
-    const int d0 = 6 + 7 * depth;
+    const int d0 = 6 + S.dimsPerDepth * depth;
     VRaySamples r;
     if (S.samplerType >= kSamplerIndependent) {
         // the other samplers are stateful: every draw in pbrt's order, indirect.uc included
@@ -511,6 +512,36 @@ __device__ inline VRaySamples RaySamplesAt(const DeviceScene &S, const PathState
         r.rr = Get1D(S, h);
     }
     return r;
+}
+
+// The subsurface samples of a path depth (samples.cpp:56-61): dimensions d0 + 7..9 after the
+// seven direct / indirect ones
+__device__ inline void SssSamplesAt(const DeviceScene &S, const PathState &st, int slot, int depth, float *uc,
+                                    float *u0, float *u1) {
+    int px, py, sampleIndex;
+    PixelOf(st, slot, &px, &py, &sampleIndex);
+    px += S.px0;
+    const int d0 = 6 + S.dimsPerDepth * depth;
+    if (S.samplerType >= kSamplerIndependent) {
+        GenericSampler g;  // stateful: the seven draws before, in pbrt's order
+        g.Start(S.samp, px, py, sampleIndex, d0);
+        float a, b;
+        (void)g.Get1D(S.samp);
+        g.Get2D(S.samp, &a, &b);
+        (void)g.Get1D(S.samp);
+        g.Get2D(S.samp, &a, &b);
+        (void)g.Get1D(S.samp);
+        *uc = g.Get1D(S.samp);
+        g.Get2D(S.samp, u0, u1);
+    } else if (S.samplerType == 1) {
+        const uint64_t morton = ZSobolMortonIndex(S.zs, px, py, sampleIndex);
+        *uc = ZSobolGet1D(S.zs, morton, d0 + 7, S.zsPerms, S.sobolM1);
+        ZSobolGet2D(S.zs, morton, d0 + 8, S.zsPerms, S.sobolM1, u0, u1);
+    } else {
+        Halton h = StartPixelSample(S, px, py, sampleIndex, d0 + 7);
+        *uc = Get1D(S, h);
+        Get2D(S, h, u0, u1);
+    }
 }
 
 // Spectral record I/O (wavelength-major).  A spectrum whose 31 entries are equal is stored
@@ -1636,6 +1667,34 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
             nbUni &= FloatToBits(nb) == FloatToBits(fL[0]);
         }
         if (!nz) continue;
+        if (transmission && S.matSss && S.matSss[mat] >= 0) {
+            // a subsurface material's transmitted sample goes to the BSSRDF queue instead of
+            // the next iteration (surfscatter.cpp:225-232); beta after Russian roulette, r_u as
+            // it came in, the updated etaScale
+            const int js = shardBase + WavePush(&st.counters[CounterIndex(wf, kVSss, shard)], true);
+            const SssRecords &sr = v.sss;
+            bool bu = true;
+#pragma unroll 2
+            for (int i = 0; i < kNS; ++i) bu &= FloatToBits(fL[i * kBlock]) == FloatToBits(fL[0]);
+            sr.beta[js] = fL[0];
+            sr.ru[js] = ruIn.v0;
+#pragma unroll 2
+            for (int i = 1; i < kNS; ++i) {
+                if (!bu) sr.beta[(size_t)i * NR + js] = fL[i * kBlock];
+                if (!ruUni) sr.ru[(size_t)i * NR + js] = ruIn(i);
+            }
+            StoreV3(sr.po, NR, js, si.p);
+            StoreV3(sr.ns, NR, js, si.ns);
+            sr.lambda0[js] = lambda0;
+            sr.etaScale[js] = etaScale;
+            sr.mat[js] = mat;
+            sr.pixel[js] = slot;
+            sr.depth[js] = depth;
+            sr.mIn[js] = mIn;
+            sr.mOut[js] = mOut;
+            sr.flags[js] = (bu ? kUniBeta : 0) | (ruUni ? kUniRu : 0);
+            continue;
+        }
         const int jn = shardBase + WavePush(nextCnt, true);
         out.beta[jn] = fL[0];
         out.ru[jn] = ruIn.v0;
@@ -1662,6 +1721,259 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
         out.pixel[jn] = slot;
         out.depth[jn] = depth + 1;
         out.medium[jn] = DotN(si.n, wi) > 0 ? mOut : mIn;
+    }
+}
+
+// ------------------------------------------------------------------ subsurface scattering
+// WavefrontPathIntegrator::SampleSubsurface (wavefront/subsurface.cpp:18-206) in two stages:
+// k_vsss_probe samples the BSSRDF probe segment and traces it (the aggregate's
+// IntersectOneRandom, optix.cu:478-518), k_vsss_scatter turns the reservoir's hit into the exit
+// vertex (TabulatedBSSRDF::ProbeIntersectionToSample) and samples its NormalizedFresnelBxDF for
+// the indirect ray and a light for the shadow ray.  Their shadow rays join this iteration's
+// shadow queue (traced after them).
+
+// A subsurface spectrum parameter at wavelength lam (SubsurfaceDesc: kind 0 ConstantSpectrum,
+// 1 RGBUnbounded / RGBAlbedo scale * sigmoid, 2 PiecewiseLinearSpectrum)
+__device__ inline float SssSpectrumAt(const DeviceScene &S, const float *q, float lam) {
+    const int kind = (int)q[0];
+    if (kind == 0) return q[1];
+    if (kind == 1) return q[5] * SigmoidPolynomial(q[2], q[3], q[4], lam);
+    const int pl = (int)q[6], a = S.plOffsets[pl], na = S.plOffsets[pl + 1] - a;
+    return PiecewiseLinearEval(S.plLambda + a, S.plValue + a, na, lam);
+}
+// SubsurfaceMaterial::GetBSSRDF's sigma_a / sigma_s at one wavelength (materials.h:823-841),
+// as the TabulatedBSSRDF's sigma_t and rho
+__device__ inline SssCoeffs SssCoeffsAt(const DeviceScene &S, const float *P, const SssTable &t, float lam) {
+    float sa, ss;
+    if (P[0] == 0) {
+        const float a = P[1] * SssSpectrumAt(S, P + 4, lam), b = P[1] * SssSpectrumAt(S, P + 11, lam);
+        sa = a > 0 ? a : 0.f;  // ClampZero
+        ss = b > 0 ? b : 0.f;
+    } else {
+        const float m = P[1] * SssSpectrumAt(S, P + 11, lam);
+        const float mfree = m > 0 ? m : 0.f;
+        const float r = Clampf(SssSpectrumAt(S, P + 4, lam), 0, 1);
+        SssFromDiffuse(t, r, mfree, &sa, &ss);
+    }
+    return MakeSssCoeffs(sa, ss);
+}
+
+template <int TM>
+__global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_vsss_probe(DeviceScene S, PathState st, VolState v,
+                                                                            int wf) {
+    const QueueView q = LoadQueue(st, wf, kVSss);
+    if ((int)(blockIdx.x * blockDim.x) >= q.total) return;
+    extern __shared__ float4 dynLds[];
+    const SceneLds L = SetupSceneLds(S, dynLds);
+    const int NR = st.NR;
+    const SssRecords &r = v.sss;
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < q.total; j += gridDim.x * blockDim.x) {
+        const int e = QueueSlot(q, j);
+        r.hitPrim[e] = -1;
+        r.resPdf[e] = 0;
+        const int mat = r.mat[e], k = S.matSss[mat];
+        const float *P = S.sssParams + (size_t)kSssParams * k;
+        const SssTable t = SssTable::At(S.sssTables + (size_t)kSssTableFloats * k);
+        // GetBSSRDF + SampleSp with the subsurface samples (subsurface.cpp:24-42)
+        const SssCoeffs c0 = SssCoeffsAt(S, P, t, r.lambda0[e]);
+        float uc, u0, u1;
+        SssSamplesAt(S, st, r.pixel[e], r.depth[e], &uc, &u0, &u1);
+        V3 p0, p1;
+        if (!SssSampleSp(t, c0, LoadV3(r.po, NR, e), LoadV3(r.ns, NR, e), uc, u0, u1, &p0, &p1)) continue;
+        // IntersectOneRandom: closest hits from p0 towards p1 (tMax 1), each continued by
+        // SpawnRayTo(p1); hits on this material enter a weighted reservoir (weight 1) seeded
+        // with Hash(p0, p1)
+        const uint32_t hw[6] = {FloatToBits(p0.x), FloatToBits(p0.y), FloatToBits(p0.z),
+                                FloatToBits(p1.x), FloatToBits(p1.y), FloatToBits(p1.z)};
+        PCG32 rng;
+        rng.SetSequence(HashWords(hw, 6));
+        float wsum = 0;
+        int chosen = -1;
+        float cb0 = 0, cb1 = 0, cb2 = 0;
+        V3 o = p0, d = p1 - p0;
+        for (int depth = 1; LengthSquared(d) > 0 && depth < 100; ++depth) {
+            TriHit h;
+            const int prim = Traverse<false, TM>(S, L, o, d, 1.f, &h);
+            if (prim < 0) break;
+            V3 a, b, c;
+            PrimVerts(S, prim, &a, &b, &c);
+            const TriSurface si = SurfaceAt<true>(S, prim, a, b, c, h.b0, h.b1, h.b2);
+            if (S.primMaterial[prim] == mat) {
+                wsum += 1.f;
+                if (rng.Uniform() < 1.f / wsum) {
+                    chosen = prim;
+                    cb0 = h.b0, cb1 = h.b1, cb2 = h.b2;
+                }
+            }
+            d = p1 - si.p;
+            o = OffsetRayOrigin(si.p, si.pErr, si.n, d);
+        }
+        if (chosen >= 0 && wsum > 0) {
+            r.hitPrim[e] = chosen;
+            r.hitB[e] = cb0;
+            r.hitB[NR + e] = cb1;
+            r.hitB[2 * (size_t)NR + e] = cb2;
+            r.resPdf[e] = 1.f / wsum;  // SampleProbability: reservoirWeight / weightSum
+        }
+    }
+}
+
+template <bool Ext>
+__global__ void __launch_bounds__(kBlock) k_vsss_scatter(DeviceScene S0, PathState st, VolState v, int wf) {
+    const QueueView q = LoadQueue(st, wf, kVSss);
+    if ((int)(blockIdx.x * blockDim.x) >= q.total) return;
+    extern __shared__ float4 dynLds[];
+    DeviceScene S = S0;
+    (void)StageVolTables(S0, S, reinterpret_cast<char *>(dynLds));
+    const int NR = st.NR;
+    const SssRecords &r = v.sss;
+    const VolRecords &out = v.rec[(wf + 1) & 1];
+    const int shard = ProducerShard();
+    const int shardBase = shard * st.capS;
+    int *nextCnt = &st.counters[CounterIndex(wf + 1, kVRay, shard)];
+    int *shadowCnt = &st.counters[CounterIndex(wf, kVShadow, shard)];
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < q.total; j += gridDim.x * blockDim.x) {
+        const int e = QueueSlot(q, j);
+        const int prim = r.hitPrim[e];
+        const float resPdf = r.resPdf[e];
+        if (prim < 0 || resPdf == 0) continue;  // "if (w.reservoirPDF == 0) return"
+        const int mat = r.mat[e], k = S.matSss[mat];
+        const float *P = S.sssParams + (size_t)kSssParams * k;
+        const SssTable t = SssTable::At(S.sssTables + (size_t)kSssTableFloats * k);
+        const float lambda0 = r.lambda0[e];
+        const int slot = r.pixel[e], depth = r.depth[e], fl = r.flags[e];
+        const SpecIn betaIn(r.beta, NR, e, fl & kUniBeta), ruIn(r.ru, NR, e, fl & kUniRu);
+        V3 a, b, c;
+        PrimVerts(S, prim, &a, &b, &c);
+        const TriSurface si = SurfaceAt<Ext>(S, prim, a, b, c, r.hitB[e], r.hitB[NR + e], r.hitB[2 * (size_t)NR + e]);
+        // ProbeIntersectionToSample (bssrdf.h:305-312): Sp(pi) = Sr(|po - pi|), PDF_Sp(pi, n)
+        const V3 po = LoadV3(r.po, NR, e);
+        const float rDist = Distance(po, si.p);
+        const SssPdfGeom g = MakeSssPdfGeom(po, LoadV3(r.ns, NR, e), si.p, si.n);
+        // betap = beta Sp / (reservoirPDF pdf_0) and r_u pdf / pdf_0 (subsurface.cpp:60-62), written
+        // over the record's own (full-spectrum) beta and r_u: bp(i), ru(i) below
+        float *bpP = r.beta + e, *ruP = r.ru + e;
+        auto bp = [&](int i) -> float & { return bpP[(size_t)i * NR]; };
+        auto ru = [&](int i) -> float & { return ruP[(size_t)i * NR]; };
+        const float pdf0 = SssPdfSp(t, SssCoeffsAt(S, P, t, lambda0), g);
+        const float pr = resPdf * pdf0;
+        bool spAny = false, pdfAny = false;
+        {
+            SpectralIter it(lambda0);
+#pragma unroll 1
+            for (int i = 0; i < kNS; ++i, it.Next()) {
+                const SssCoeffs ci = SssCoeffsAt(S, P, t, it.lam);
+                const float sp = SssSrScaled(t, ci, rDist), pdf = SssPdfSp(t, ci, g);
+                spAny |= sp != 0;
+                pdfAny |= pdf != 0;
+                const float b = betaIn(i), u = ruIn(i);  // read before the slot is overwritten
+                bp(i) = b * sp / pr;
+                ru(i) = u * pdf / pdf0;
+            }
+        }
+        if (!spAny || !pdfAny) continue;
+        float rus = 0;
+#pragma unroll 1
+        for (int i = 0; i < kNS; ++i) rus = i == 0 ? ru(0) : rus + ru(i);
+        const float avgRu = rus / kNS;
+        // NormalizedFresnelBxDF(eta) in the frame of the exit's shading normal and dpdu, wo = ns
+        const float eta = P[2], fc = P[3];
+        const Frame frame = Frame::FromXZ(Normalize(si.dpdus), si.ns);
+        const V3 woL = frame.ToLocal(si.ns);
+        int mIn = r.mIn[e], mOut = r.mOut[e];
+        float dUc = 0, dU0 = 0, dU1 = 0;
+        {
+            const VRaySamples rs = RaySamplesAt(S, st, slot, depth, false);
+            dUc = rs.dUc, dU0 = rs.dU0, dU1 = rs.dU1;
+            // ---- indirect (subsurface.cpp:76-150): BSDF::Sample_f, RR (depth > 1), next ray
+            if (woL.z != 0) {
+                V3 wiL = SampleCosineHemisphere(rs.iU0, rs.iU1);
+                if (woL.z < 0) wiL.z *= -1;
+                const float f = NormalizedFresnelF(eta, fc, woL, wiL);
+                const float pdf = woL.z * wiL.z > 0 ? CosineHemispherePDF(fabsf(wiL.z)) : 0.f;
+                if (f != 0 && pdf != 0 && wiL.z != 0) {
+                    const V3 wi = frame.FromLocal(wiL);
+                    const float absdot = AbsDotN(si.ns, wi);
+                    const float etaScale = r.etaScale[e];
+                    float mx = -kInfinity;
+                    // the new beta in the record slots' order: computed into registers per wavelength
+                    bool nz = false;
+                    float q = 0;
+#pragma unroll 1
+                    for (int i = 0; i < kNS; ++i) mx = fmaxf(mx, bp(i) * f * absdot / pdf * etaScale / avgRu);
+                    const bool rrOn = mx < 1 && depth > 1;
+                    bool killed = false;
+                    if (rrOn) {
+                        q = fmaxf(0.f, 1 - mx);
+                        killed = rs.rr < q;
+                    }
+                    if (!killed) {
+                        float nb0 = 0;
+                        bool nbUni = true;
+#pragma unroll 1
+                        for (int i = 0; i < kNS; ++i) {
+                            float nb = bp(i) * f * absdot / pdf;
+                            if (rrOn) nb /= 1 - q;
+                            nz |= nb != 0;
+                            nb0 = i == 0 ? nb : nb0;
+                            nbUni &= FloatToBits(nb) == FloatToBits(nb0);
+                        }
+                        if (nz) {
+                            const int jn = shardBase + WavePush(nextCnt, true);
+                            bool ruUni = true;
+#pragma unroll 1
+                            for (int i = 0; i < kNS; ++i) ruUni &= FloatToBits(ru(i)) == FloatToBits(ru(0));
+#pragma unroll 1
+                            for (int i = 0; i < kNS; ++i) {
+                                float nb = bp(i) * f * absdot / pdf;
+                                if (rrOn) nb /= 1 - q;
+                                if (i == 0 || !nbUni) out.beta[(size_t)i * NR + jn] = nb;
+                                if (i == 0 || !ruUni) {
+                                    out.ru[(size_t)i * NR + jn] = ru(i);
+                                    out.rl[(size_t)i * NR + jn] = ru(i) / pdf;
+                                }
+                            }
+                            StoreV3(out.ray, NR, jn, OffsetRayOrigin(si.p, si.pErr, si.n, wi));
+                            StoreV3(out.ray + 3 * (size_t)NR, NR, jn, wi);
+                            StoreV3(out.prev, NR, jn, si.p);
+                            StoreV3(out.prev + 3 * (size_t)NR, NR, jn, si.pErr);
+                            StoreV3(out.prev + 6 * (size_t)NR, NR, jn, si.n);
+                            StoreV3(out.prev + 9 * (size_t)NR, NR, jn, si.ns);
+                            out.lambda0[jn] = lambda0;
+                            out.etaScale[jn] = etaScale;
+                            out.flags[jn] = 2 | (nbUni ? kUniBeta : 0) | (ruUni ? kUniRu | kUniRl : 0);
+                            out.pixel[jn] = slot;
+                            out.depth[jn] = depth + 1;
+                            out.medium[jn] = DotN(si.n, wi) > 0 ? mOut : mIn;
+                        }
+                    }
+                }
+            }
+        }
+        // ---- direct lighting (subsurface.cpp:152-203): the light sample from the exit point
+        AreaLightHit ls;
+        if (!SampleAreaLightAt<Ext>(S, si.p, si.n, si.ns, dUc, dU0, dU1, lambda0, &ls, si.pErr)) continue;
+        const V3 wi = ls.wi;
+        const V3 wiL = frame.ToLocal(wi);
+        if (woL.z == 0) continue;  // BSDF::f
+        const float f = NormalizedFresnelF(eta, fc, woL, wiL);
+        if (f == 0) continue;
+        const float absdot = AbsDotN(si.ns, wi);
+        const float lightPDF = ls.pdf;
+        const float bsdfPDF = ls.delta ? 0.f : (woL.z * wiL.z > 0 ? CosineHemispherePDF(fabsf(wiL.z)) : 0.f);
+        const V3 so = OffsetRayOrigin(si.p, si.pErr, si.n, ls.p - si.p);
+        const V3 pt = OffsetRayOrigin(ls.p, ls.pErr, ls.n, so - ls.p);
+        const V3 sd = pt - so;
+        float Ld[kNS], sru[kNS], srl[kNS];
+        SpectralIter it(lambda0);
+#pragma unroll
+        for (int i = 0; i < kNS; ++i, it.Next()) {
+            Ld[i] = bp(i) * f * absdot * ls.Le(S, DenseOffset(it.lam), it.lam);
+            srl[i] = ru(i) * lightPDF;
+            sru[i] = ru(i) * bsdfPDF;
+        }
+        const int js = shardBase + WavePush(shadowCnt, true);
+        WriteShadow(S, v, NR, js, ShadowOut{so, sd, DotN(si.n, sd) > 0 ? mOut : mIn}, Ld, sru, srl, lambda0, slot);
     }
 }
 
@@ -2484,6 +2796,7 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
         (void)hipMemsetAsync(v.shPixel, 0xff, sizeof(int) * (size_t)st.NR, s);
         (void)hipMemsetAsync(v.rec[(wf + 1) & 1].pixel, 0xff, sizeof(int) * (size_t)st.NR, s);
     }
+#define K_VSSS_PROBE(tm) k_vsss_probe<tm>
 #define VOL_REST(EXT) \
     if (wf == S.maxDepth) return hipGetLastError(); \
     if (S.matTypeMask & (1 << 3)) hipLaunchKernelGGL(k_viface<EXT>, gW, block, 0, s, S, st, v, wf); \
@@ -2491,6 +2804,10 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
         hipLaunchKernelGGL(k_vlayered<EXT>, gW, block, 0, s, S, st, v, wf); \
     QUEUE_CHECK(2); \
     hipLaunchKernelGGL(k_vscatter<EXT>, gW, block, 0, s, S, st, v, wf); \
+    if (S.matSss) { \
+        PBRT_LAUNCH_TRAVERSAL(S, K_VSSS_PROBE, gT, block, VolStackBytes(S), s, S, st, v, wf); \
+        hipLaunchKernelGGL(k_vsss_scatter<EXT>, gW, block, VolTablesLdsBytes(S), s, S, st, v, wf); \
+    } \
     QUEUE_CHECK(3);
 #define QUEUE_CHECK(stage)                                                                                          \
     if (qcheck)                                                                                                     \
@@ -2525,6 +2842,7 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
         VOL_REST(false);
     }
 #undef VOL_REST
+#undef K_VSSS_PROBE
     if (qcheck) {
         hipLaunchKernelGGL(k_queue_holes, dim3(64, kShards), block, 0, s, st.counters, wf + 1, kVRay,
                            v.rec[(wf + 1) & 1].pixel, st.capS, v.holes, 4);

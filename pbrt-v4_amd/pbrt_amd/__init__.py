@@ -106,6 +106,11 @@ class SceneFlat(ctypes.Structure):
         ("sobol_log2_scale", ctypes.c_int), ("sobol_matrices32", ctypes.POINTER(ctypes.c_uint32)),
         ("vdc_sobol", ctypes.POINTER(ctypes.c_uint64)), ("vdc_sobol_inv", ctypes.POINTER(ctypes.c_uint64)),
         ("noise_perm", ctypes.POINTER(ctypes.c_float)),
+        ("n_sss", ctypes.c_int),
+        ("dims_per_depth", ctypes.c_int),
+        ("material_sss", ctypes.POINTER(ctypes.c_int32)),
+        ("sss_params", ctypes.POINTER(ctypes.c_float)),
+        ("sss_tables", ctypes.POINTER(ctypes.c_float)),
     ]
 
 
@@ -133,7 +138,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_scene_get_info", "pbrt_scene_get_flat", "pbrt_device_count", "pbrt_context_create",
     "pbrt_context_free", "pbrt_render", "pbrt_synchronize", "pbrt_get_stats", "pbrt_reset_stats",
     "pbrt_film_clear", "pbrt_film_device_ptr", "pbrt_film_read", "pbrt_film_get_rgb", "pbrt_intersect",
-    "pbrt_debug_halton", "pbrt_debug_halton_fastpath_mismatches", "pbrt_debug_check_rn_math", "pbrt_debug_rgb_coeffs", "pbrt_debug_rgb2spec_column", "pbrt_debug_kernel_sections",
+    "pbrt_debug_halton", "pbrt_debug_halton_fastpath_mismatches", "pbrt_debug_catmull_rom", "pbrt_debug_check_rn_math", "pbrt_debug_rgb_coeffs", "pbrt_debug_rgb2spec_column", "pbrt_debug_kernel_sections",
     "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_sampler", "pbrt_debug_rng", "pbrt_debug_det_math", "pbrt_debug_procedural", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
     "pbrt_debug_named_spectrum", "pbrt_debug_bxdf", "pbrt_debug_layered", "pbrt_debug_triangle_shading", "pbrt_film_write_image",
     "pbrt_image_read_size", "pbrt_image_read", "pbrt_image_write", "pbrt_image_error", "pbrt_debug_filter_sample",
@@ -198,6 +203,8 @@ def _lib():
     lib.pbrt_get_kernel_stats.argtypes = [c.c_void_p, c.c_void_p, c.c_int, c.POINTER(c.c_int)]
     lib.pbrt_debug_halton.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_int]
     lib.pbrt_debug_halton.restype = c.c_float
+    lib.pbrt_debug_catmull_rom.argtypes = [c.c_int, c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_void_p, c.c_void_p,
+                                           c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_debug_halton_fastpath_mismatches.argtypes = [c.c_void_p, c.c_int, c.c_uint32, c.c_uint32, c.c_uint32]
     lib.pbrt_debug_halton_fastpath_mismatches.restype = c.c_int64
     lib.pbrt_debug_check_rn_math.argtypes = [c.c_int, c.c_uint64, c.c_int64, c.POINTER(c.c_int64),
@@ -479,6 +486,17 @@ def det_math(fn, a, b=None, device=-1):
     _check(_lib().pbrt_debug_det_math(device, DET_MATH_FNS.index(fn), a.ctypes.data, b.ctypes.data, len(a),
                                       out.ctypes.data))
     return out
+
+
+def catmull_rom(op, nodes1, nodes2, values, cdf, x):
+    """The product's Catmull-Rom spline utilities (core/bssrdf.h) on the host: op 0 weights
+    [n][6] (ok, offset, w0..w3), 1 InvertCatmullRom [n], 3 SampleCatmullRom2D (x: alpha, u pairs)."""
+    a = [np.ascontiguousarray(v, np.float32) for v in (nodes1, nodes2, values, cdf, x)]
+    n = len(a[4]) // 2 if op == 3 else len(a[4])
+    out = np.zeros(n * 6 if op == 0 else n, np.float32)
+    _check(_lib().pbrt_debug_catmull_rom(op, a[0].ctypes.data, len(a[0]), a[1].ctypes.data, len(a[1]),
+                                         a[2].ctypes.data, a[3].ctypes.data, a[4].ctypes.data, n, out.ctypes.data))
+    return out.reshape(-1, 6) if op == 0 else out
 
 
 def procedural(kind, params4, in9):

@@ -14,7 +14,7 @@
  *   pbrt_render
  *       WavefrontPathIntegrator::Render (wavefront/integrator.cpp:290-493) restricted to a
  *       set of film rows and a range of sample indices; asynchronous on the context stream.
- *   pbrt_intersect / pbrt_intersect_tr
+ *   pbrt_intersect / pbrt_intersect_tr / pbrt_intersect_one_random
  *       WavefrontAggregate::IntersectClosest / IntersectShadow / IntersectShadowTr
  *       (wavefront/integrator.h:32-54) over caller-owned device SoA ray buffers.
  *   pbrt_film_*
@@ -338,6 +338,15 @@ int pbrt_image_flip(const float *image, const float *reference, int width, int h
  * Asynchronous on the context stream (no host round trip): the results are valid after
  * pbrt_synchronize, or for work the caller orders after the context stream. */
 int pbrt_intersect(pbrt_context *ctx, const float *rays_dev, int n, int any_hit, int32_t *prim_dev, float *hit_dev);
+/* WavefrontAggregate::IntersectOneRandom (wavefront/integrator.h:53; gpu/aggregate.cpp:1811-1847,
+ * optix.cu:478-518): per caller segment segs_dev[6][n] (p0.xyz, p1.xyz) the closest hits from p0
+ * towards p1, each continued by SpawnRayTo(p1), reservoir-sampled among the hits on
+ * materials_dev[i] (the scene's material index) with pbrt's RNG seeding (Hash(p0, p1)) ->
+ * prim_dev[n] (triangle in the caller's numbering, n_triangles + k for shape k, or -1),
+ * hit_dev[3][n] (b0, b1, b2; a shape's coordinates), pdf_dev[n] (SampleProbability, 0: none).
+ * Device pointers, asynchronous on the context stream. */
+int pbrt_intersect_one_random(pbrt_context *ctx, const float *segs_dev, const int32_t *materials_dev, int n,
+                              int32_t *prim_dev, float *hit_dev, float *pdf_dev);
 /* WavefrontAggregate::IntersectShadowTr (wavefront/integrator.h:49-51; TraceTransmittance,
  * wavefront/intersect.h:164-274) over device SoA buffers: rays_dev [7][n] (o, d, tMax: the light
  * point is o + tMax d), medium_dev [n] the medium each ray starts in (NULL or -1: vacuum; indices

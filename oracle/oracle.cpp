@@ -5053,6 +5053,31 @@ struct BSSRDF {
 };
 }  // namespace osss
 
+// IntersectOneRandom (optix.cu:478-518): closest hits from p0 towards p1 (tMax 1), each
+// continued by SpawnRayTo(p1) up to 99 traces, reservoir-sampling the hits on material `mat`
+// (weight 1, RNG seeded with Hash(p0, p1)); -1 when none
+int ProbeOneRandom(const Scene &S, Vec p0, Vec p1, int mat, TriIsect *cti, Vec *cdir, Float *resPdf) {
+    const uint64_t hseed = HashFloats(p0.x, p0.y, p0.z, p1.x, p1.y, p1.z);
+    PCG32 wrs(hseed, Mix64(hseed));  // WeightedReservoirSampler::Seed: RNG::SetSequence
+    Float wsum = 0;
+    int chosen = -1;
+    Vec po = p0, pd = p1 - p0;
+    for (int it = 1; LengthSquared(pd) > 0 && it < 100; ++it) {
+        TriIsect t2;
+        const int hp = S.Intersect(po, pd, 1, &t2, false);
+        if (hp < 0) break;
+        const Interaction hi = S.Interact(hp, t2, pd);
+        if (S.Material(hp) == mat) {
+            wsum += 1;
+            if (wrs.Uniform() < 1 / wsum) chosen = hp, *cti = t2, *cdir = pd;
+        }
+        pd = p1 - hi.p;
+        po = OffsetRayOrigin(hi.p, hi.err, hi.n, pd);
+    }
+    *resPdf = chosen >= 0 && wsum > 0 ? 1 / wsum : 0;
+    return chosen >= 0 && wsum > 0 ? chosen : -1;
+}
+
 struct Renderer {
     std::vector<OEnvLight> envs;  // ImageInfiniteLights (flat inf_image)
     // the image light behind global light index li, or null
@@ -5861,27 +5886,11 @@ struct Renderer {
                 }
                 Vec p0, p1;
                 if (!bd.SampleSp(sUc, sU0, sU1, &p0, &p1)) break;
-                const uint64_t hseed = HashFloats(p0.x, p0.y, p0.z, p1.x, p1.y, p1.z);
-                PCG32 wrs(hseed, Mix64(hseed));  // WeightedReservoirSampler::Seed: RNG::SetSequence
-                Float wsum = 0;
-                int chosen = -1;
                 TriIsect cti{};
                 Vec cdir;
-                Vec po = p0, pd = p1 - p0;
-                for (int it = 1; LengthSquared(pd) > 0 && it < 100; ++it) {
-                    TriIsect t2;
-                    const int hp = S.Intersect(po, pd, 1, &t2, false);
-                    if (hp < 0) break;
-                    const Interaction hi = S.Interact(hp, t2, pd);
-                    if (S.Material(hp) == mat) {
-                        wsum += 1;
-                        if (wrs.Uniform() < 1 / wsum) chosen = hp, cti = t2, cdir = pd;
-                    }
-                    pd = p1 - hi.p;
-                    po = OffsetRayOrigin(hi.p, hi.err, hi.n, pd);
-                }
-                if (chosen < 0 || !(wsum > 0)) break;
-                const Float resPdf = 1 / wsum;
+                Float resPdf;
+                const int chosen = ProbeOneRandom(S, p0, p1, mat, &cti, &cdir, &resPdf);
+                if (chosen < 0) break;
                 const Interaction ex = S.Interact(chosen, cti, cdir);
                 const Spectrum Sp = bd.Sr(Length(bd.po - ex.p)), pdfSp = bd.PdfSp(ex.p, ex.n);
                 if (!Sp || !pdfSp) break;
@@ -6419,6 +6428,30 @@ int oracle_intersect_batch(const pbrt_scene_flat *flat, const pbrt_scene_info *i
             }
         });
     for (auto &t : pool) t.join();
+    return 0;
+}
+
+// IntersectOneRandom per segment segs[6][n] (p0, p1) with materials[n]: prim (original
+// numbering, -1), hit[3][n] (b0 b1 b2), pdf[n]
+int oracle_intersect_one_random(const pbrt_scene_flat *flat, const pbrt_scene_info *info, const float *segs,
+                                const int32_t *mats, int n, int32_t *prim, float *hit, float *pdf) {
+    Scene S;
+    S.Init(flat, info);
+    if (flat->n_tex_nodes > 0 && (!g_rgbTable || !g_ewaLut)) return -2;
+    OTextures tex;
+    tex.Init(flat, info->spp, info->xres, info->yres);
+    S.tex = &tex;
+    for (int i = 0; i < n; ++i) {
+        const Vec p0(segs[i], segs[n + i], segs[2 * n + i]), p1(segs[3 * n + i], segs[4 * n + i], segs[5 * n + i]);
+        TriIsect ti{0, 0, 0, 0};
+        Vec d;
+        Float pr = 0;
+        prim[i] = ProbeOneRandom(S, p0, p1, mats[i], &ti, &d, &pr);
+        hit[i] = prim[i] >= 0 ? ti.b0 : 0;
+        hit[n + i] = prim[i] >= 0 ? ti.b1 : 0;
+        hit[2 * n + i] = prim[i] >= 0 ? ti.b2 : 0;
+        pdf[i] = pr;
+    }
     return 0;
 }
 

@@ -252,6 +252,23 @@ def intersect(scene, rays, any_hit=False):
     return prim, hit
 
 
+def intersect_one_random(scene, segs, materials):
+    """IntersectOneRandom per probe segment: segs float32 [6, n] (p0, p1), materials int32 [n]
+    -> (prim int32 [n], hit float32 [3, n], pdf float32 [n])"""
+    info = scene.info
+    flat = scene.flat()
+    segs = np.ascontiguousarray(segs, dtype=np.float32)
+    mats = np.ascontiguousarray(materials, dtype=np.int32)
+    n = segs.shape[1]
+    prim = np.zeros(n, np.int32)
+    hit = np.zeros((3, n), np.float32)
+    pdf = np.zeros(n, np.float32)
+    vp = ctypes.c_void_p
+    lib().oracle_intersect_one_random(ctypes.byref(flat), ctypes.byref(info), vp(segs.ctypes.data), vp(mats.ctypes.data), n,
+                                      vp(prim.ctypes.data), vp(hit.ctypes.data), vp(pdf.ctypes.data))
+    return prim, hit, pdf
+
+
 def intersect_tr(scene, rays, medium, lambda0):
     """TraceTransmittance per ray (see pbrt_intersect_tr): rays float32 [7, n], medium int32 [n],
     lambda0 float32 [n] -> float32 [3, 31, n] (T_ray, r_u, r_l)."""

@@ -48,6 +48,8 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
                               hipStream_t s);
 void SetQueueCheck(int on);
 int TakeQueueHoles();
+hipError_t LaunchIntersectOneRandom(const DeviceScene &S, const float *segs, const int *mats, int n, int *prim,
+                                    float *hit, float *pdf, hipStream_t s);
 hipError_t LaunchIntersectTr(const DeviceScene &S, const float *rays, const int *medium, const float *lambda0, int n,
                              float *out, hipStream_t s);
 size_t VolTraversalStaticLds(int tm);
@@ -2363,6 +2365,20 @@ int pbrt_intersect(pbrt_context *ctx, const float *rays, int n, int anyHit, int3
         if ((int64_t)n * 7 > INT32_MAX) return Fail("ray batch too large");
         // asynchronous on the context stream; the kernel writes the scene's triangle numbering
         HIPCHECK(LaunchIntersectBatch(ctx->S, rays, n, anyHit, prim, hit, ctx->stream));
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_intersect_one_random(pbrt_context *ctx, const float *segs, const int32_t *materials, int n, int32_t *prim,
+                              float *hit, float *pdf) {
+    try {
+        if (!ctx || n < 0 || (n > 0 && (!segs || !materials || !prim || !hit || !pdf))) return Fail("bad arguments");
+        HIPCHECK(hipSetDevice(ctx->device));
+        if (n == 0) return 0;
+        if ((int64_t)n * 6 > INT32_MAX) return Fail("segment batch too large");
+        HIPCHECK(LaunchIntersectOneRandom(ctx->S, segs, materials, n, prim, hit, pdf, ctx->stream));
         return 0;
     } catch (const std::exception &e) {
         return Fail(e.what());

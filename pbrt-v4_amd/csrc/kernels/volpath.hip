@@ -1758,6 +1758,62 @@ __device__ inline SssCoeffs SssCoeffsAt(const DeviceScene &S, const float *P, co
     return MakeSssCoeffs(sa, ss);
 }
 
+// IntersectOneRandom for one probe segment (optix.cu:478-518): closest hits from p0 towards p1
+// (tMax 1), each continued by SpawnRayTo(p1) up to 99 traces; hits on material `mat` enter a
+// weighted reservoir (weight 1) seeded with Hash(p0, p1).  Returns the chosen leaf-order
+// primitive (-1: none) with its hit coordinates and SampleProbability.
+template <int TM>
+__device__ inline int ProbeOneRandom(const DeviceScene &S, const SceneLds &L, V3 p0, V3 p1, int mat, float *b0,
+                                     float *b1, float *b2, float *resPdf) {
+    const uint32_t hw[6] = {FloatToBits(p0.x), FloatToBits(p0.y), FloatToBits(p0.z),
+                            FloatToBits(p1.x), FloatToBits(p1.y), FloatToBits(p1.z)};
+    PCG32 rng;
+    rng.SetSequence(HashWords(hw, 6));
+    float wsum = 0;
+    int chosen = -1;
+    V3 o = p0, d = p1 - p0;
+    for (int depth = 1; LengthSquared(d) > 0 && depth < 100; ++depth) {
+        TriHit h;
+        const int prim = Traverse<false, TM>(S, L, o, d, 1.f, &h);
+        if (prim < 0) break;
+        V3 a, b, c;
+        PrimVerts(S, prim, &a, &b, &c);
+        const TriSurface si = SurfaceAt<true>(S, prim, a, b, c, h.b0, h.b1, h.b2);
+        if (S.primMaterial[prim] == mat) {
+            wsum += 1.f;
+            if (rng.Uniform() < 1.f / wsum) {
+                chosen = prim;
+                *b0 = h.b0, *b1 = h.b1, *b2 = h.b2;
+            }
+        }
+        d = p1 - si.p;
+        o = OffsetRayOrigin(si.p, si.pErr, si.n, d);
+    }
+    *resPdf = chosen >= 0 && wsum > 0 ? 1.f / wsum : 0.f;  // reservoirWeight / weightSum
+    return chosen >= 0 && wsum > 0 ? chosen : -1;
+}
+
+// The aggregate's IntersectOneRandom exposed on its own (integrator.h:53): caller segments
+// segs[6][n] (p0, p1) and materials[n] -> prim[n] (the caller's primitive numbering, -1),
+// hit[3][n] (b0 b1 b2), pdf[n]
+template <int TM>
+__global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_intersect_one_random(DeviceScene S, const float *segs,
+                                                                                     const int *mats, int n, int *outPrim,
+                                                                                     float *outHit, float *outPdf) {
+    extern __shared__ float4 dynLds[];
+    const SceneLds L = SetupSceneLds(S, dynLds);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const V3 p0(segs[i], segs[n + i], segs[2 * n + i]), p1(segs[3 * n + i], segs[4 * n + i], segs[5 * n + i]);
+        float b0 = 0, b1 = 0, b2 = 0, pdf = 0;
+        const int prim = ProbeOneRandom<TM>(S, L, p0, p1, mats[i], &b0, &b1, &b2, &pdf);
+        outPrim[i] = prim >= 0 ? S.primOrig[prim] : -1;  // the caller's numbering
+        outHit[i] = b0;
+        outHit[n + i] = b1;
+        outHit[2 * n + i] = b2;
+        outPdf[i] = pdf;
+    }
+}
+
 template <int TM>
 __global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_vsss_probe(DeviceScene S, PathState st, VolState v,
                                                                             int wf) {
@@ -1780,40 +1836,14 @@ __global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_vsss_probe(Devic
         SssSamplesAt(S, st, r.pixel[e], r.depth[e], &uc, &u0, &u1);
         V3 p0, p1;
         if (!SssSampleSp(t, c0, LoadV3(r.po, NR, e), LoadV3(r.ns, NR, e), uc, u0, u1, &p0, &p1)) continue;
-        // IntersectOneRandom: closest hits from p0 towards p1 (tMax 1), each continued by
-        // SpawnRayTo(p1); hits on this material enter a weighted reservoir (weight 1) seeded
-        // with Hash(p0, p1)
-        const uint32_t hw[6] = {FloatToBits(p0.x), FloatToBits(p0.y), FloatToBits(p0.z),
-                                FloatToBits(p1.x), FloatToBits(p1.y), FloatToBits(p1.z)};
-        PCG32 rng;
-        rng.SetSequence(HashWords(hw, 6));
-        float wsum = 0;
-        int chosen = -1;
-        float cb0 = 0, cb1 = 0, cb2 = 0;
-        V3 o = p0, d = p1 - p0;
-        for (int depth = 1; LengthSquared(d) > 0 && depth < 100; ++depth) {
-            TriHit h;
-            const int prim = Traverse<false, TM>(S, L, o, d, 1.f, &h);
-            if (prim < 0) break;
-            V3 a, b, c;
-            PrimVerts(S, prim, &a, &b, &c);
-            const TriSurface si = SurfaceAt<true>(S, prim, a, b, c, h.b0, h.b1, h.b2);
-            if (S.primMaterial[prim] == mat) {
-                wsum += 1.f;
-                if (rng.Uniform() < 1.f / wsum) {
-                    chosen = prim;
-                    cb0 = h.b0, cb1 = h.b1, cb2 = h.b2;
-                }
-            }
-            d = p1 - si.p;
-            o = OffsetRayOrigin(si.p, si.pErr, si.n, d);
-        }
-        if (chosen >= 0 && wsum > 0) {
+        float cb0 = 0, cb1 = 0, cb2 = 0, pdf = 0;
+        const int chosen = ProbeOneRandom<TM>(S, L, p0, p1, mat, &cb0, &cb1, &cb2, &pdf);
+        if (chosen >= 0) {
             r.hitPrim[e] = chosen;
             r.hitB[e] = cb0;
             r.hitB[NR + e] = cb1;
             r.hitB[2 * (size_t)NR + e] = cb2;
-            r.resPdf[e] = 1.f / wsum;  // SampleProbability: reservoirWeight / weightSum
+            r.resPdf[e] = pdf;
         }
     }
 }
@@ -2759,6 +2789,15 @@ hipError_t LaunchIntersectTr(const DeviceScene &S, const float *rays, const int 
 #define K_TR(tm) k_intersect_tr<tm>
     PBRT_LAUNCH_TRAVERSAL(S, K_TR, dim3(g), dim3(kBlock), VolStackBytes(S), s, S, rays, medium, lambda0, n, out);
 #undef K_TR
+    return hipGetLastError();
+}
+
+hipError_t LaunchIntersectOneRandom(const DeviceScene &S, const float *segs, const int *mats, int n, int *prim,
+                                    float *hit, float *pdf, hipStream_t s) {
+    const int g = std::max(1, std::min(4096, (n + kBlock - 1) / kBlock));
+#define K_OR(tm) k_intersect_one_random<tm>
+    PBRT_LAUNCH_TRAVERSAL(S, K_OR, dim3(g), dim3(kBlock), VolStackBytes(S), s, S, segs, mats, n, prim, hit, pdf);
+#undef K_OR
     return hipGetLastError();
 }
 

@@ -142,7 +142,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_sampler", "pbrt_debug_rng", "pbrt_debug_det_math", "pbrt_debug_procedural", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
     "pbrt_debug_named_spectrum", "pbrt_debug_bxdf", "pbrt_debug_layered", "pbrt_debug_triangle_shading", "pbrt_film_write_image",
     "pbrt_image_read_size", "pbrt_image_read", "pbrt_image_write", "pbrt_image_error", "pbrt_debug_filter_sample",
-    "pbrt_debug_bvh_stats", "pbrt_debug_light_bvh", "pbrt_intersect_tr", "pbrt_image_flip", "pbrt_set_kernel_profiling", "pbrt_get_kernel_stats",
+    "pbrt_debug_bvh_stats", "pbrt_debug_light_bvh", "pbrt_intersect_tr", "pbrt_intersect_one_random", "pbrt_image_flip", "pbrt_set_kernel_profiling", "pbrt_get_kernel_stats",
     "pbrt_debug_texture_eval",
     "pbrt_debug_env_eval",
     "pbrt_debug_shape_eval",
@@ -197,6 +197,8 @@ def _lib():
     lib.pbrt_debug_bvh_stats.argtypes = [c.c_void_p, c.c_void_p]
     lib.pbrt_image_flip.argtypes = [c.c_void_p, c.c_void_p, c.c_int, c.c_int, c.c_void_p]
     lib.pbrt_intersect_tr.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
+    lib.pbrt_intersect_one_random.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p, c.c_void_p,
+                                              c.c_void_p]
     lib.pbrt_set_kernel_profiling.argtypes = [c.c_void_p, c.c_int]
     lib.pbrt_debug_light_bvh.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_void_p, c.c_void_p, c.c_int,
                                          c.POINTER(c.c_int)]
@@ -680,6 +682,29 @@ class HIPAggregate:
                                         ctypes.c_void_p(out.data_ptr())))
         self.integrator.synchronize()
         return out[0], out[1], out[2]
+
+
+    def IntersectOneRandom(self, segs, materials):
+        """IntersectOneRandom (optix.cu:478-518) per probe segment: segs [6, n] float32 (p0, p1)
+        and materials [n] int32 device tensors -> (prim [n] int32, hit [3, n], pdf [n])."""
+        import torch
+        if not (segs.is_cuda and segs.dtype == torch.float32 and segs.dim() == 2 and segs.shape[0] == 6):
+            raise PbrtError("segs must be a float32 device tensor of shape [6, n]")
+        n = segs.shape[1]
+        segs = segs.contiguous()
+        materials = materials.to(device=segs.device, dtype=torch.int32).contiguous()
+        if materials.numel() != n:
+            raise PbrtError("materials needs one entry per segment")
+        prim = torch.empty(n, dtype=torch.int32, device=segs.device)
+        hit = torch.empty((3, n), dtype=torch.float32, device=segs.device)
+        pdf = torch.empty(n, dtype=torch.float32, device=segs.device)
+        torch.cuda.synchronize(segs.device)
+        _check(_lib().pbrt_intersect_one_random(self.integrator._h, ctypes.c_void_p(segs.data_ptr()),
+                                                ctypes.c_void_p(materials.data_ptr()), n,
+                                                ctypes.c_void_p(prim.data_ptr()), ctypes.c_void_p(hit.data_ptr()),
+                                                ctypes.c_void_p(pdf.data_ptr())))
+        self.integrator.synchronize()
+        return prim, hit, pdf
 
 
 def RenderWavefront(scene_path, device=0, **overrides):

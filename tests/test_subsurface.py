@@ -144,3 +144,58 @@ def test_subsurface_matches_oracle_gpu(pa, oracle, form):
     a, _ = gpu_rgb(pa, oracle, sc)
     frac, mr = check(a, oracle_rgb(oracle, sc))
     print(f"subsurface ({form}): {frac*100:.2f}% pixels within 1e-3, mean rel {mr:.2e}")
+
+
+def probe_segments(n=6000, seed=12):
+    """Probe-like segments: axis-aligned (the BSSRDF frames of the box's faces) and random ones
+    through the blob and the box"""
+    rng = np.random.default_rng(seed)
+    c = rng.uniform([-0.6, -0.1, -0.6], [1.2, 1.1, 0.6], (n, 3))
+    d = rng.normal(size=(n, 3))
+    ax = rng.integers(0, 3, n)
+    axis = np.zeros((n, 3))
+    axis[np.arange(n), ax] = rng.choice([-1, 1], n)
+    d[: n // 2] = axis[: n // 2]
+    d /= np.linalg.norm(d, axis=1)[:, None]
+    half = rng.uniform(0.05, 1.2, n)[:, None]
+    c = c - EYE  # render space: world minus the eye (cameraworld)
+    return np.concatenate([(c - d * half).T, (c + d * half).T]).astype(np.float32)
+
+
+EYE = np.array([0, 1.4, -3.2])
+
+
+def test_intersect_one_random_oracle_plausible(pa, oracle):
+    sc = pa.Scene.from_string(scene(FORMS["sigma"], BLOB + BOX), SCENES)
+    f = sc.flat()
+    ms = np.ctypeslib.as_array(f.material_sss, shape=(f.n_materials,))
+    mat = int(np.nonzero(ms >= 0)[0][0])
+    segs = probe_segments(2000)
+    prim, hit, pdf = oracle.intersect_one_random(sc, segs, np.full(segs.shape[1], mat, np.int32))
+    assert (prim >= 0).mean() > 0.15
+    assert set(np.unique(pdf[prim >= 0])) <= {1.0, 0.5, np.float32(1 / 3), 0.25, 0.2, np.float32(1 / 6)}
+    assert (pdf[prim < 0] == 0).all()
+
+
+@pytest.mark.gpu
+def test_intersect_one_random_matches_oracle_gpu(pa, oracle):
+    """pbrt_intersect_one_random (HIPAggregate::IntersectOneRandom) against the oracle's probe,
+    bit for bit: the chosen primitive, its hit coordinates and the reservoir probability."""
+    import torch
+    sc = pa.Scene.from_string(scene(FORMS["sigma"], BLOB + BOX), SCENES)
+    f = sc.flat()
+    ms = np.ctypeslib.as_array(f.material_sss, shape=(f.n_materials,))
+    mat = int(np.nonzero(ms >= 0)[0][0])
+    segs = probe_segments()
+    mats = np.full(segs.shape[1], mat, np.int32)
+    mats[::7] = 0  # the ground's material: its hits are the ones sampled
+    integ = pa.WavefrontPathIntegrator(sc, max_paths=1 << 12)
+    agg = pa.HIPAggregate(integ)
+    p, h, q = agg.IntersectOneRandom(torch.from_numpy(segs).cuda(), torch.from_numpy(mats).cuda())
+    p, h, q = p.cpu().numpy(), h.cpu().numpy(), q.cpu().numpy()
+    po, ho, qo = oracle.intersect_one_random(sc, segs, mats)
+    same = (p == po)
+    print(f"IntersectOneRandom: {same.mean()*100:.3f}% same primitive, {(po >= 0).mean()*100:.1f}% with a hit")
+    assert same.mean() >= 0.999
+    np.testing.assert_array_equal(q[same], qo[same])
+    np.testing.assert_array_equal(h[:, same & (p >= 0)], ho[:, same & (po >= 0)])

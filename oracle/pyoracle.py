@@ -204,8 +204,8 @@ def set_math_mode(mode):
 
 
 def math_eval(fn, a, b=None):
-    """The oracle's transcendental `fn` (sin cos asin acos atan2 log) in its current mode."""
-    names = ["sin", "cos", "asin", "acos", "atan2", "log"]
+    """The oracle's transcendental `fn` (sin cos asin acos atan2 log exp sinh) in its current mode."""
+    names = ["sin", "cos", "asin", "acos", "atan2", "log", "exp", "sinh"]
     a = np.ascontiguousarray(a, np.float32)
     b = np.ascontiguousarray(b if b is not None else np.zeros_like(a), np.float32)
     out = np.zeros_like(a)

@@ -2763,7 +2763,7 @@ int pbrt_debug_sampler(const pbrt_scene *scene, int px, int py, int sampleIndex,
 
 int pbrt_debug_det_math(int device, int fn, const float *a, const float *b, int n, float *out) {
     try {
-        if (!a || !b || !out || n < 0 || fn < 0 || fn > 7) return Fail("pbrt_debug_det_math: bad arguments");
+        if (!a || !b || !out || n < 0 || fn < 0 || fn > 9) return Fail("pbrt_debug_det_math: bad arguments");
         if (device < 0) {  // the same code compiled for the host
             for (int i = 0; i < n; ++i) {
                 float s, c;
@@ -2775,7 +2775,9 @@ int pbrt_debug_det_math(int device, int fn, const float *a, const float *b, int 
                 case 4: out[i] = detm::ATan2(a[i], b[i]); break;
                 case 5: out[i] = detm::Log(a[i]); break;
                 case 6: detm::SinCos(a[i], &s, &c); out[i] = s; break;
-                default: detm::SinCos(a[i], &s, &c); out[i] = c; break;
+                case 7: detm::SinCos(a[i], &s, &c); out[i] = c; break;
+                case 8: out[i] = detm::Exp(a[i]); break;
+                default: out[i] = detm::Sinh(a[i]); break;
                 }
             }
             return 0;

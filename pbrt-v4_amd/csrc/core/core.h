@@ -91,6 +91,8 @@ PHD float ASinf(float x) { return detm::ASin(x); }
 PHD float ACosf(float x) { return detm::ACos(x); }
 PHD float ATan2f(float y, float x) { return detm::ATan2(y, x); }
 PHD float Logf(float x) { return detm::Log(x); }
+PHD float Expf(float x) { return detm::Exp(x); }
+PHD float Sinhf(float x) { return detm::Sinh(x); }
 #else
 PHD float Sinf(float x) { return std::sin(x); }
 PHD float Cosf(float x) { return std::cos(x); }
@@ -102,6 +104,8 @@ PHD float ASinf(float x) { return std::asin(x); }
 PHD float ACosf(float x) { return std::acos(x); }
 PHD float ATan2f(float y, float x) { return std::atan2(y, x); }
 PHD float Logf(float x) { return std::log(x); }
+PHD float Expf(float x) { return std::exp(x); }
+PHD float Sinhf(float x) { return std::sinh(x); }
 #endif
 
 PHD float Sqr(float v) { return v * v; }

@@ -212,5 +212,32 @@ PHD float Log(float x) {
     return fmaf(fe, 0.693359375f, m + y);
 }
 
+// e^x (Cephes expf): n = round(x log2 e), r = x - n ln 2 in two parts, a degree-5 polynomial,
+// then 2^n as two exact-then-rounding scalings (subnormal results round once)
+PHD float Exp(float x) {
+    if (x != x) return x;
+    if (x > 88.72283935546875f) return __builtin_huge_valf();
+    if (x < -103.97208404541016f) return 0.f;
+    const float n = std::floor(fmaf(x, 1.44269502162933349609f, 0.5f));
+    float r = fmaf(n, -0.693359375f, x);
+    r = fmaf(n, 2.12194440e-4f, r);
+    float p = fmaf(r, 1.9875691500e-4f, 1.3981999507e-3f);
+    p = fmaf(r, p, 8.3334519073e-3f);
+    p = fmaf(r, p, 4.1665795894e-2f);
+    p = fmaf(r, p, 1.6666665459e-1f);
+    p = fmaf(r, p, 5.0000001201e-1f);
+    const float y = fmaf(p, r * r, r) + 1.f;
+    const int k = (int)n, k1 = k / 2, k2 = k - k1;
+    return y * FromBits((uint32_t)(k1 + 127) << 23) * FromBits((uint32_t)(k2 + 127) << 23);
+}
+// sinh x = (e^|x| - e^-|x|) / 2 with x's sign; x itself below 2^-12
+PHD float Sinh(float x) {
+    const float a = std::fabs(x);
+    if (a < 0x1p-12f) return x;
+    const float e = Exp(a);
+    const float s = (e - 1.f / e) * 0.5f;
+    return x < 0 ? -s : s;
+}
+
 }  // namespace detm
 }  // namespace pbrt_amd

@@ -1563,7 +1563,7 @@ __global__ void k_check_rn_math(uint64_t seed, int perThread, unsigned long long
     atomicAdd(&bad[0], ns);
 }
 // the device's portable transcendentals (core/detmath.h) on given inputs: fn 0 sin, 1 cos, 2 asin,
-// 3 acos, 4 atan2(a, b), 5 log, 6 sin of SinCosf, 7 cos of SinCosf
+// 3 acos, 4 atan2(a, b), 5 log, 6 sin of SinCosf, 7 cos of SinCosf, 8 exp, 9 sinh
 __device__ inline float DetMathEval(int fn, float a, float b) {
     float s, c;
     switch (fn) {
@@ -1574,7 +1574,9 @@ __device__ inline float DetMathEval(int fn, float a, float b) {
     case 4: return ATan2f(a, b);
     case 5: return Logf(a);
     case 6: SinCosf(a, &s, &c); return s;
-    default: SinCosf(a, &s, &c); return c;
+    case 7: SinCosf(a, &s, &c); return c;
+    case 8: return Expf(a);
+    default: return Sinhf(a);
     }
 }
 __global__ void k_det_math(int fn, const float *a, const float *b, int n, float *out) {

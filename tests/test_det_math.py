@@ -12,7 +12,7 @@ gpu/optix.cu:197-243; mix choices hashing the hit, materials.h:285-294).
 import numpy as np
 import pytest
 
-FNS = ["sin", "cos", "asin", "acos", "atan2", "log"]
+FNS = ["sin", "cos", "asin", "acos", "atan2", "log", "exp", "sinh"]
 
 
 def inputs(fn, n=400000, seed=7):
@@ -30,6 +30,14 @@ def inputs(fn, n=400000, seed=7):
                             [0.0, -0.0, 0.0, -0.0, 1.0, -1.0, np.inf, -np.inf]])
         b = np.concatenate([rng.uniform(-5, 5, n // 2), rng.normal(size=n // 4), rng.uniform(-1e-5, 1e-5, n // 4),
                             [1.0, 1.0, -1.0, -1.0, 0.0, -0.0, np.inf, -np.inf]])
+    elif fn == "exp":
+        a = np.concatenate([rng.uniform(-104, 89, n // 2), rng.uniform(-1, 1, n // 4), rng.uniform(-20, 0, n // 4),
+                            [0.0, -0.0, 1.0, -1.0, 88.7, -87.3, -100.0, -104.0, 89.0]])
+        b = np.zeros_like(a)
+    elif fn == "sinh":
+        a = np.concatenate([rng.uniform(0.1, 30, n // 2), rng.uniform(-30, -0.1, n // 4), rng.uniform(1, 10, n // 4),
+                            [0.0, -0.0, 1e-5, 0.5, 1.0, 10.0]])
+        b = np.zeros_like(a)
     else:  # log
         a = np.concatenate([np.exp(rng.uniform(-87, 88, n // 2)), rng.uniform(0.5, 2, n // 4), rng.uniform(0, 1, n // 4),
                             [1.0, 2.0, 0.5, 1e-40, 1e-45, 3e38]])
@@ -45,7 +53,7 @@ def ulp_error(got, ref64):
 
 
 REF64 = {"sin": np.sin, "cos": np.cos, "asin": lambda a: np.arcsin(np.clip(a, -1, 1)),
-         "acos": lambda a: np.arccos(np.clip(a, -1, 1)), "log": np.log}
+         "acos": lambda a: np.arccos(np.clip(a, -1, 1)), "log": np.log, "exp": np.exp, "sinh": np.sinh}
 
 
 @pytest.mark.parametrize("fn", FNS)
@@ -54,11 +62,14 @@ def test_det_math_accuracy(pa, fn):
     got = pa.det_math(fn, a, b)
     with np.errstate(divide="ignore", invalid="ignore"):
         ref = np.arctan2(a.astype(np.float64), b.astype(np.float64)) if fn == "atan2" else REF64[fn](a.astype(np.float64))
-    fin = np.isfinite(ref)
+        fin = np.isfinite(ref.astype(np.float32))  # exp past ~88.72 overflows float32
     assert np.array_equal(np.isfinite(got), fin)
     err = ulp_error(got[fin], ref[fin])
     print(f"{fn}: max {err.max():.3f} ulp, mean {err.mean():.4f}, {np.mean(err > 0.5) * 100:.1f}% not correctly rounded")
-    assert err.max() <= 3.0, (fn, err.max(), a[fin][np.argmax(err)])
+    # sinh = (e^x - e^-x) / 2 loses a few bits to cancellation below x ~ 0.5 (the hair BxDF
+    # evaluates it at 1 / v >= 1); elsewhere within 3 ulp
+    tol = 3.0 if fn != "sinh" else np.where(np.abs(a[fin]) >= 0.5, 3.0, 64.0)
+    assert (err <= tol).all(), (fn, err.max(), a[fin][np.argmax(err)])
 
 
 def test_det_math_special_values(pa):

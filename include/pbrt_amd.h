@@ -424,9 +424,15 @@ int pbrt_debug_zsobol(const pbrt_scene *scene, int px, int py, int sample_index,
 int pbrt_debug_sampler(const pbrt_scene *scene, int px, int py, int sample_index, int dim, float *out7);
 /* The kernels' portable transcendentals (core/detmath.h) on n inputs: fn 0 sin, 1 cos, 2 asin, 3
  * acos (inputs clamped to [-1, 1] as SafeASin / SafeACos), 4 atan2(a, b), 5 log, 6 / 7 the sin /
- * cos of SinCosf; on GPU `device`, or compiled for the host when device < 0 (the two must agree
+ * cos of SinCosf, 8 exp, 9 sinh; on GPU `device`, or compiled for the host when device < 0 (the two must agree
  * bit for bit, and the oracle's device-math mode with both) */
 int pbrt_debug_det_math(int device, int fn, const float *a, const float *b, int n, float *out);
+/* HairBxDF (bxdfs.h:1054-1152, bxdfs.cpp:279-573; the BxDF HairMaterial::GetBxDF builds,
+ * materials.h:380-404) on n queries of 16 floats {h, eta, beta_m, beta_n, alpha, sigma_a0, wo[3],
+ * wi[3], uc, u0, u1, slope} with sigma_a[i] = sigma_a0 + slope * i at the 31 wavelengths:
+ * out[68] per query = {f(wo, wi)[31], PDF(wo, wi), Sample_f ok, wi[3], pdf, f[31]} (zeros when
+ * BSDF::Sample_f returns {}).  On GPU `device`, or compiled for the host when device < 0. */
+int pbrt_debug_hair(int device, const float *in16, int n, float *out);
 /* The procedural textures' kernels code on the host (core/texture_eval.h): kind 0 FBm, 1
  * Turbulence (wrinkled), 2 windy, 3 InsidePolkaDot (in9[0..1] = s, t), 4 marble; params4 =
  * octaves, roughness, scale, variation; in9 per point = p, dpdx, dpdy; out6 per point = value

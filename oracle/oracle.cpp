@@ -191,6 +191,34 @@ static float Log(float x) {
     yv = std::fma(-0.5f, z, yv);
     return std::fma(fe, 0.693359375f, m + yv);
 }
+// detmath.h Exp / Sinh restated (Cephes expf; sinh from it)
+static float Exp(float x) {
+    if (x != x) return x;
+    if (x > 88.72283935546875f) return std::numeric_limits<float>::infinity();
+    if (x < -103.97208404541016f) return 0.f;
+    const float n = std::floor(std::fma(x, 1.44269502162933349609f, 0.5f));
+    float r = std::fma(n, -0.693359375f, x);
+    r = std::fma(n, 2.12194440e-4f, r);
+    float p = std::fma(r, 1.9875691500e-4f, 1.3981999507e-3f);
+    p = std::fma(r, p, 8.3334519073e-3f);
+    p = std::fma(r, p, 4.1665795894e-2f);
+    p = std::fma(r, p, 1.6666665459e-1f);
+    p = std::fma(r, p, 5.0000001201e-1f);
+    const float y = std::fma(p, r * r, r) + 1.f;
+    const int k = (int)n, k1 = k / 2, k2 = k - k1;
+    uint32_t b1 = (uint32_t)(k1 + 127) << 23, b2 = (uint32_t)(k2 + 127) << 23;
+    float s1, s2;
+    std::memcpy(&s1, &b1, 4);
+    std::memcpy(&s2, &b2, 4);
+    return y * s1 * s2;
+}
+static float Sinh(float x) {
+    const float a = std::abs(x);
+    if (a < 0x1p-12f) return x;
+    const float e = Exp(a);
+    const float s = (e - 1.f / e) * 0.5f;
+    return x < 0 ? -s : s;
+}
 }  // namespace dm
 static inline Float CRSin(Float x) {
     if (g_mathMode == 2) { float s, c; dm::SinCos(x, &s, &c); return s; }
@@ -199,6 +227,14 @@ static inline Float CRSin(Float x) {
 static inline Float CRCos(Float x) {
     if (g_mathMode == 2) { float s, c; dm::SinCos(x, &s, &c); return c; }
     return g_mathMode ? (Float)std::cos((double)x) : std::cos(x);
+}
+static inline Float CRExp(Float x) {
+    if (g_mathMode == 2) return dm::Exp(x);
+    return g_mathMode ? (Float)std::exp((double)x) : std::exp(x);
+}
+static inline Float CRSinh(Float x) {
+    if (g_mathMode == 2) return dm::Sinh(x);
+    return g_mathMode ? (Float)std::sinh((double)x) : std::sinh(x);
 }
 static inline Float CRLog(Float x) {
     if (g_mathMode == 2) return dm::Log(x);
@@ -2774,14 +2810,237 @@ static bool Refract(Vec wi, Vec n, Float eta, Float *etap, Vec *wt) {
 }
 static inline Vec Reflect(Vec wo, Vec n) { return -wo + 2 * Dot(wo, n) * n; }
 
+static Float FastExp(Float x);
+// HairBxDF (bxdfs.h:1054-1152, bxdfs.cpp:279-573) with the math helpers it calls (util/math.h:
+// 294-309 Pow, :490-502 Logistic, :794-816 I0 / LogI0; util/sampling.h:79-115 SampleDiscrete,
+// :256-278 SampleTrimmedLogistic), pMax = 3, every SampledSpectrum operation per wavelength.
+namespace ohair {
+constexpr int pMax = 3;
+template <int n> static inline Float Pow(Float v) {
+    if constexpr (n == 0) return 1;
+    else if constexpr (n == 1) return v;
+    else {
+        Float n2 = Pow<n / 2>(v);
+        return n2 * n2 * Pow<n & 1>(v);
+    }
+}
+static inline Float I0(Float x) {
+    Float val = 0, x2i = 1;
+    int64_t ifact = 1;
+    int i4 = 1;
+    for (int i = 0; i < 10; ++i) {
+        if (i > 1) ifact *= i;
+        val += x2i / (i4 * (ifact * ifact));
+        x2i *= x * x;
+        i4 *= 4;
+    }
+    return val;
+}
+static inline Float LogI0(Float x) {
+    if (x > 12) return x + 0.5f * (-CRLog(2 * Pi) + CRLog(1 / x) + 1 / (8 * x));
+    return CRLog(I0(x));
+}
+static inline Float Logistic(Float x, Float s) {
+    x = std::abs(x);
+    return CRExp(-x / s) / (s * Sqr(1 + CRExp(-x / s)));
+}
+static inline Float LogisticCDF(Float x, Float s) { return 1 / (1 + CRExp(-x / s)); }
+static inline Float TrimmedLogistic(Float x, Float s, Float a, Float b) {
+    return Logistic(x, s) / (LogisticCDF(b, s) - LogisticCDF(a, s));
+}
+static inline Float SampleTrimmedLogistic(Float u, Float s, Float a, Float b) {
+    auto P = [&](Float x) { return 1 / (1 + CRExp(-x / s)); };  // InvertLogisticSample
+    u = Lerp(u, P(a), P(b));
+    Float x = -s * CRLog(1 / u - 1);  // SampleLogistic
+    return Clamp(x, a, b);
+}
+static inline Float Mp(Float cosTheta_i, Float cosTheta_o, Float sinTheta_i, Float sinTheta_o, Float v) {
+    Float a = cosTheta_i * cosTheta_o / v, b = sinTheta_i * sinTheta_o / v;
+    Float mp = (v <= .1) ? (FastExp(LogI0(a) - b - 1 / v + 0.6931f + CRLog(1 / (2 * v))))
+                         : (FastExp(-b) * I0(a)) / (CRSinh(1 / v) * 2 * v);
+    return mp;
+}
+static inline Float Phi(int p, Float gamma_o, Float gamma_t) { return 2 * p * gamma_t - 2 * gamma_o + p * Pi; }
+static inline Float Np(Float phi, int p, Float s, Float gamma_o, Float gamma_t) {
+    Float dphi = phi - Phi(p, gamma_o, gamma_t);
+    while (dphi > Pi) dphi -= 2 * Pi;
+    while (dphi < -Pi) dphi += 2 * Pi;
+    return TrimmedLogistic(dphi, s, -Pi, Pi);
+}
+struct Hair {
+    Float h = 0, eta = 1.55f;
+    Spectrum sigma_a;
+    Float v[pMax + 1] = {}, s = 0;
+    Float sin2kAlpha[pMax] = {}, cos2kAlpha[pMax] = {};
+
+    void Init(Float h_, Float eta_, const Spectrum &sa, Float beta_m, Float beta_n, Float alpha) {
+        h = h_;
+        eta = eta_;
+        sigma_a = sa;
+        v[0] = Sqr(0.726f * beta_m + 0.812f * Sqr(beta_m) + 3.7f * Pow<20>(beta_m));
+        v[1] = .25 * v[0];
+        v[2] = 4 * v[0];
+        for (int p = 3; p <= pMax; ++p) v[p] = v[2];
+        static const Float SqrtPiOver8 = 0.626657069f;
+        s = SqrtPiOver8 * (0.265f * beta_n + 1.194f * Sqr(beta_n) + 5.372f * Pow<22>(beta_n));
+        sin2kAlpha[0] = CRSin((Pi / 180) * alpha);
+        cos2kAlpha[0] = SafeSqrt(1 - Sqr(sin2kAlpha[0]));
+        for (int i = 1; i < pMax; ++i) {
+            sin2kAlpha[i] = 2 * cos2kAlpha[i - 1] * sin2kAlpha[i - 1];
+            cos2kAlpha[i] = Sqr(cos2kAlpha[i - 1]) - Sqr(sin2kAlpha[i - 1]);
+        }
+    }
+    // Ap (bxdfs.h:1102-1124); ap[pMax] stays zero when 1 - T f is zero at every wavelength
+    void Ap(Float cosTheta_o, const Spectrum &T, Spectrum ap[pMax + 1]) const {
+        Float cosGamma_o = SafeSqrt(1 - Sqr(h));
+        Float cosTheta = cosTheta_o * cosGamma_o;
+        Float f = FrDielectric(cosTheta, eta);
+        for (int i = 0; i < NS; ++i) ap[0][i] = f;
+        for (int i = 0; i < NS; ++i) ap[1][i] = Sqr(1 - f) * T[i];
+        for (int p = 2; p < pMax; ++p)
+            for (int i = 0; i < NS; ++i) ap[p][i] = ap[p - 1][i] * T[i] * f;
+        bool any = false;
+        for (int i = 0; i < NS; ++i) any = any || (1 - T[i] * f) != 0;
+        for (int i = 0; i < NS; ++i) ap[pMax][i] = any ? ap[pMax - 1][i] * f * T[i] / (1 - T[i] * f) : 0.f;
+    }
+    void Tilt(int p, Float sinTheta_o, Float cosTheta_o, Float *sinThetap_o, Float *cosThetap_o) const {
+        if (p == 0) {
+            *sinThetap_o = sinTheta_o * cos2kAlpha[1] - cosTheta_o * sin2kAlpha[1];
+            *cosThetap_o = cosTheta_o * cos2kAlpha[1] + sinTheta_o * sin2kAlpha[1];
+        } else if (p == 1) {
+            *sinThetap_o = sinTheta_o * cos2kAlpha[0] + cosTheta_o * sin2kAlpha[0];
+            *cosThetap_o = cosTheta_o * cos2kAlpha[0] - sinTheta_o * sin2kAlpha[0];
+        } else if (p == 2) {
+            *sinThetap_o = sinTheta_o * cos2kAlpha[2] + cosTheta_o * sin2kAlpha[2];
+            *cosThetap_o = cosTheta_o * cos2kAlpha[2] - sinTheta_o * sin2kAlpha[2];
+        } else {
+            *sinThetap_o = sinTheta_o;
+            *cosThetap_o = cosTheta_o;
+        }
+        *cosThetap_o = std::abs(*cosThetap_o);
+    }
+    Spectrum f(Vec wo, Vec wi) const {
+        Float sinTheta_o = wo.x;
+        Float cosTheta_o = SafeSqrt(1 - Sqr(sinTheta_o));
+        Float phi_o = CRATan2(wo.z, wo.y);
+        Float gamma_o = SafeASin(h);
+        Float sinTheta_i = wi.x;
+        Float cosTheta_i = SafeSqrt(1 - Sqr(sinTheta_i));
+        Float phi_i = CRATan2(wi.z, wi.y);
+        Float sinTheta_t = sinTheta_o / eta;
+        Float cosTheta_t = SafeSqrt(1 - Sqr(sinTheta_t));
+        Float etap = SafeSqrt(Sqr(eta) - Sqr(sinTheta_o)) / cosTheta_o;
+        Float sinGamma_t = h / etap;
+        Float cosGamma_t = SafeSqrt(1 - Sqr(sinGamma_t));
+        Float gamma_t = SafeASin(sinGamma_t);
+        Spectrum T;
+        for (int i = 0; i < NS; ++i) T[i] = CRExp(-sigma_a[i] * (2 * cosGamma_t / cosTheta_t));
+        Float phi = phi_i - phi_o;
+        Spectrum ap[pMax + 1];
+        Ap(cosTheta_o, T, ap);
+        Spectrum fsum(0.f);
+        for (int p = 0; p < pMax; ++p) {
+            Float sinThetap_o, cosThetap_o;
+            Tilt(p, sinTheta_o, cosTheta_o, &sinThetap_o, &cosThetap_o);
+            Float m = Mp(cosTheta_i, cosThetap_o, sinTheta_i, sinThetap_o, v[p]);
+            Float n = Np(phi, p, s, gamma_o, gamma_t);
+            for (int i = 0; i < NS; ++i) fsum[i] += m * ap[p][i] * n;
+        }
+        Float m3 = Mp(cosTheta_i, cosTheta_o, sinTheta_i, sinTheta_o, v[pMax]);
+        for (int i = 0; i < NS; ++i) fsum[i] += m3 * ap[pMax][i] / (2 * Pi);
+        if (std::abs(wi.z) > 0)
+            for (int i = 0; i < NS; ++i) fsum[i] /= std::abs(wi.z);
+        return fsum;
+    }
+    void ApPDF(Float cosTheta_o, Float apPDF[pMax + 1]) const {
+        Float sinTheta_o = SafeSqrt(1 - Sqr(cosTheta_o));
+        Float sinTheta_t = sinTheta_o / eta;
+        Float cosTheta_t = SafeSqrt(1 - Sqr(sinTheta_t));
+        Float etap = SafeSqrt(Sqr(eta) - Sqr(sinTheta_o)) / cosTheta_o;
+        Float sinGamma_t = h / etap;
+        Float cosGamma_t = SafeSqrt(1 - Sqr(sinGamma_t));
+        Spectrum T;
+        for (int i = 0; i < NS; ++i) T[i] = CRExp(-sigma_a[i] * (2 * cosGamma_t / cosTheta_t));
+        Spectrum ap[pMax + 1];
+        Ap(cosTheta_o, T, ap);
+        Float sumY = 0;
+        for (int p = 0; p <= pMax; ++p) sumY += ap[p].Average();
+        for (int p = 0; p <= pMax; ++p) apPDF[p] = ap[p].Average() / sumY;
+    }
+    Float PdfSum(const Float apPDF[pMax + 1], Float sinTheta_o, Float cosTheta_o, Float sinTheta_i, Float cosTheta_i,
+                 Float dphi, Float gamma_o, Float gamma_t) const {
+        Float pdf = 0;
+        for (int p = 0; p < pMax; ++p) {
+            Float sinThetap_o, cosThetap_o;
+            Tilt(p, sinTheta_o, cosTheta_o, &sinThetap_o, &cosThetap_o);
+            pdf += Mp(cosTheta_i, cosThetap_o, sinTheta_i, sinThetap_o, v[p]) * apPDF[p] * Np(dphi, p, s, gamma_o, gamma_t);
+        }
+        pdf += Mp(cosTheta_i, cosTheta_o, sinTheta_i, sinTheta_o, v[pMax]) * apPDF[pMax] * (1 / (2 * Pi));
+        return pdf;
+    }
+    bool Sample_f(Vec wo, Float uc, Float u0, Float u1, BSDFSample *bs) const {
+        Float sinTheta_o = wo.x;
+        Float cosTheta_o = SafeSqrt(1 - Sqr(sinTheta_o));
+        Float phi_o = CRATan2(wo.z, wo.y);
+        Float gamma_o = SafeASin(h);
+        Float apPDF[pMax + 1];
+        ApPDF(cosTheta_o, apPDF);
+        // SampleDiscrete(apPDF, uc, nullptr, &uc)
+        Float sumWeights = 0;
+        for (int k = 0; k <= pMax; ++k) sumWeights += apPDF[k];
+        Float up = uc * sumWeights;
+        if (up == sumWeights) up = NextFloatDown(up);
+        int p = 0;
+        Float sum = 0;
+        while (p < pMax && sum + apPDF[p] <= up) sum += apPDF[p++];
+        uc = std::min((up - sum) / apPDF[p], OneMinusEpsilon);
+        Float sinThetap_o, cosThetap_o;
+        Tilt(p, sinTheta_o, cosTheta_o, &sinThetap_o, &cosThetap_o);
+        Float cosTheta = 1 + v[p] * CRLog(std::max<Float>(u0, 1e-5) + (1 - u0) * FastExp(-2 / v[p]));
+        Float sinTheta = SafeSqrt(1 - Sqr(cosTheta));
+        Float cosPhi = CRCos(2 * Pi * u1);
+        Float sinTheta_i = -cosTheta * sinThetap_o + sinTheta * cosPhi * cosThetap_o;
+        Float cosTheta_i = SafeSqrt(1 - Sqr(sinTheta_i));
+        Float etap = SafeSqrt(Sqr(eta) - Sqr(sinTheta_o)) / cosTheta_o;
+        Float sinGamma_t = h / etap;
+        Float gamma_t = SafeASin(sinGamma_t);
+        Float dphi;
+        if (p < pMax) dphi = Phi(p, gamma_o, gamma_t) + SampleTrimmedLogistic(uc, s, -Pi, Pi);
+        else dphi = 2 * Pi * uc;
+        Float phi_i = phi_o + dphi;
+        Vec wi(sinTheta_i, cosTheta_i * CRCos(phi_i), cosTheta_i * CRSin(phi_i));
+        Float pdf = PdfSum(apPDF, sinTheta_o, cosTheta_o, sinTheta_i, cosTheta_i, dphi, gamma_o, gamma_t);
+        *bs = BSDFSample{f(wo, wi), wi, pdf, BxR | BxGlossy, 1};
+        return true;
+    }
+    Float PDF(Vec wo, Vec wi) const {
+        Float sinTheta_o = wo.x;
+        Float cosTheta_o = SafeSqrt(1 - Sqr(sinTheta_o));
+        Float phi_o = CRATan2(wo.z, wo.y);
+        Float gamma_o = SafeASin(h);
+        Float sinTheta_i = wi.x;
+        Float cosTheta_i = SafeSqrt(1 - Sqr(sinTheta_i));
+        Float phi_i = CRATan2(wi.z, wi.y);
+        Float etap = SafeSqrt(eta * eta - Sqr(sinTheta_o)) / cosTheta_o;
+        Float sinGamma_t = h / etap;
+        Float gamma_t = SafeASin(sinGamma_t);
+        Float apPDF[pMax + 1];
+        ApPDF(cosTheta_o, apPDF);
+        return PdfSum(apPDF, sinTheta_o, cosTheta_o, sinTheta_i, cosTheta_i, phi_i - phi_o, gamma_o, gamma_t);
+    }
+};
+}  // namespace ohair
+
 struct BxDF {
-    int type = 0;  // 0 diffuse, 1 dielectric, 2 conductor, 6 thin dielectric, 7 diffuse transmission
+    int type = 0;  // 0 diffuse, 1 dielectric, 2 conductor, 6 thin dielectric, 7 diffuse transmission, 9 hair
     Spectrum R, Tt;  // Tt: DiffuseTransmissionBxDF's T
     Float eta = 1;
     TRDistribution mf;
     Spectrum etaS, kS;
+    ohair::Hair hair;
 
     int Flags() const {
+        if (type == 9) return BxR | BxGlossy;  // HairBxDF::Flags (bxdfs.h:1079)
         if (type == 0) return R ? (BxR | BxDiffuse) : 0;
         if (type == 6) return BxR | BxT | BxSpecular;  // ThinDielectricBxDF
         if (type == 7) return (R ? (BxR | BxDiffuse) : 0) | (Tt ? (BxT | BxDiffuse) : 0);
@@ -2795,6 +3054,7 @@ struct BxDF {
         return r;
     }
     bool Sample_f(Vec wo, Float uc, Float u0, Float u1, BSDFSample *bs, bool radiance = true, int sf = 3) const {
+        if (type == 9) return hair.Sample_f(wo, uc, u0, u1, bs);
         if (type == 7) {
             // DiffuseTransmissionBxDF::Sample_f (bxdfs.h:231-260)
             Float pr = (sf & 1) ? R.Max() : 0, pt = (sf & 2) ? Tt.Max() : 0;
@@ -2907,6 +3167,7 @@ struct BxDF {
         return true;
     }
     Spectrum f(Vec wo, Vec wi, bool radiance = true) const {
+        if (type == 9) return hair.f(wo, wi);
         if (type == 6) return Spectrum(0.f);
         if (type == 7) return SameHemisphere(wo, wi) ? R * InvPi : Tt * InvPi;
         if (type == 0) return SameHemisphere(wo, wi) ? R * InvPi : Spectrum(0.f);
@@ -2933,6 +3194,7 @@ struct BxDF {
         return Spectrum(ft);
     }
     Float PDF(Vec wo, Vec wi, int sf = 3) const {
+        if (type == 9) return hair.PDF(wo, wi);
         if (type == 6) return 0;
         if (type == 7) {
             Float pr = (sf & 1) ? R.Max() : 0, pt = (sf & 2) ? Tt.Max() : 0;
@@ -5378,6 +5640,34 @@ struct Renderer {
                 lay.top.mf.Regularize();
                 lay.bottom.mf.Regularize();
             }
+        } else if (bx.type == 9) {
+            // HairMaterial::GetBxDF (materials.h:380-404) of constant parameters; material_layer
+            // holds {mode, sigma_a | color: kind value c0 c1 c2 scale pl, eta, beta_m, beta_n, alpha}
+            const float *ml = f->material_layer + 12 * mat;
+            Float bm = std::max<Float>(1e-2, std::min<Float>(1.0, ml[9]));
+            Float bn = std::max<Float>(1e-2, std::min<Float>(1.0, ml[10]));
+            Float a = ml[11], e = ml[8];
+            Spectrum sig;
+            for (int i = 0; i < NS; ++i) {
+                const Float l = lambda.lambda[i];
+                const int kind = (int)ml[1];
+                Float q;
+                if (kind == 0) q = ml[2];
+                else if (kind == 1) q = ml[6] * Sigmoid(ml[3], ml[4], ml[5], l);
+                else {
+                    const int pl = (int)ml[7], o = f->pl_offsets[pl];
+                    q = PLEval(f->pl_lambda + o, f->pl_value + o, f->pl_offsets[pl + 1] - o, l);
+                }
+                if (ml[0] == 0) {
+                    sig[i] = std::max<Float>(0, q);  // ClampZero(sigma_a)
+                } else {
+                    // HairBxDF::SigmaAFromReflectance (bxdfs.cpp:564-573) of Clamp(color, 0, 1)
+                    Float c = Clamp(q, 0, 1);
+                    sig[i] = Sqr(CRLog(c) / (5.969f - 0.215f * bn + 2.532f * Sqr(bn) - 10.73f * ohair::Pow<3>(bn) +
+                                             5.574f * ohair::Pow<4>(bn) + 0.245f * ohair::Pow<5>(bn)));
+                }
+            }
+            bx.hair.Init(-1 + 2 * si.uv[1], e, sig, bm, bn, a);
         } else if (bx.type == 7) {
             // DiffuseTransmissionMaterial::GetBxDF (materials.h): Clamp(scale * R | T, 0, 1)
             const float *ml = f->material_layer + 12 * mat;
@@ -6243,6 +6533,33 @@ void oracle_catmull_rom(int op, const float *nodes1, int n1, const float *nodes2
         }
     }
 }
+// the oracle's HairBxDF (ohair::Hair) on queries laid out as pbrt_debug_hair's: in[16] {h, eta,
+// beta_m, beta_n, alpha, sigma_a0, wo, wi, uc, u0, u1, slope} -> out[68] {f[NS], PDF, ok, wi,
+// pdf, f[NS]}, in the current math mode
+void oracle_hair_eval(const float *in, int n, float *out) {
+    for (int k = 0; k < n; ++k) {
+        const float *q = in + 16 * k;
+        float *o = out + (2 * NS + 6) * k;
+        Spectrum sa;
+        for (int i = 0; i < NS; ++i) sa[i] = q[5] + q[15] * (float)i;
+        ohair::Hair h;
+        h.Init(q[0], q[1], sa, q[2], q[3], q[4]);
+        const Vec wo(q[6], q[7], q[8]), wi(q[9], q[10], q[11]);
+        const Spectrum fv = h.f(wo, wi);
+        for (int i = 0; i < NS; ++i) o[i] = fv[i];
+        o[NS] = h.PDF(wo, wi);
+        float *s = o + NS + 1;
+        std::fill(s, s + 5 + NS, 0.f);
+        BSDFSample bs;
+        // BSDF::Sample_f's checks (bsdf.h:89-116)
+        if (h.Sample_f(wo, q[12], q[13], q[14], &bs) && bs.f && bs.pdf != 0 && bs.wi.z != 0) {
+            s[0] = 1;
+            s[1] = bs.wi.x, s[2] = bs.wi.y, s[3] = bs.wi.z;
+            s[4] = bs.pdf;
+            for (int i = 0; i < NS; ++i) s[5 + i] = bs.f[i];
+        }
+    }
+}
 // the oracle's own BSSRDF table for (g, eta) (osss::Table), kSssTableFloats floats
 void oracle_sss_table(float g, float eta, float *out) {
     const std::vector<float> t = osss::Table(g, eta);
@@ -6262,6 +6579,8 @@ void oracle_math_eval(int fn, const float *a, const float *b, int n, float *out)
         case 2: out[i] = SafeASin(a[i]); break;
         case 3: out[i] = SafeACos(a[i]); break;
         case 4: out[i] = CRATan2(a[i], b[i]); break;
+        case 6: out[i] = CRExp(a[i]); break;
+        case 7: out[i] = CRSinh(a[i]); break;
         default: out[i] = CRLog(a[i]); break;
         }
     }

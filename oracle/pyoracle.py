@@ -48,6 +48,7 @@ def lib():
         _lib.oracle_named_spectrum.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, vp]
         _lib.oracle_bxdf.argtypes = [ctypes.c_int] + [vp] * 7
         _lib.oracle_layered.argtypes = [vp] * 8
+        _lib.oracle_hair_eval.argtypes = [vp, ctypes.c_int, vp]
         _lib.oracle_triangle_shading.argtypes = [vp] * 3 + [ctypes.c_int] + [vp] * 3
         _lib.oracle_render.argtypes = [vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, vp]
@@ -400,6 +401,15 @@ def catmull_rom(op, nodes1, nodes2, values, cdf, x):
     lib().oracle_catmull_rom(op, a[0].ctypes.data, len(a[0]), a[1].ctypes.data, len(a[1]), a[2].ctypes.data,
                              a[3].ctypes.data, a[4].ctypes.data, n, out.ctypes.data)
     return out.reshape(-1, 6) if op == 0 else out
+
+
+def hair_eval(queries):
+    """The oracle's HairBxDF (f, PDF, Sample_f) on [n][16] queries laid out as the product's
+    hair_eval -> [n][68], in the current math mode."""
+    q = np.ascontiguousarray(queries, np.float32).reshape(-1, 16)
+    out = np.zeros((len(q), 68), np.float32)
+    lib().oracle_hair_eval(q.ctypes.data, len(q), out.ctypes.data)
+    return out
 
 
 def procedural(kind, perm, params4, in9):

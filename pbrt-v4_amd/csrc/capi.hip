@@ -13,6 +13,7 @@
 
 #include "../../include/pbrt_amd.h"
 #include "core/bssrdf.h"
+#include "core/hair.h"
 #include "host/bvh.h"
 #include "host/image.h"
 #include "host/scene.h"
@@ -37,6 +38,7 @@ hipError_t LaunchShadow(const DeviceScene &S, const PathState &st, int depth, in
 hipError_t LaunchFilm(const DeviceScene &S, const PathState &st, int nSamples, hipStream_t s);
 hipError_t LaunchCheckRNMath(uint64_t seed, int blocks, int perThread, unsigned long long *bad, hipStream_t s);
 hipError_t LaunchDetMath(int fn, const float *a, const float *b, int n, float *out, hipStream_t s);
+hipError_t LaunchHairEval(const float *in, int n, float *out, hipStream_t s);
 hipError_t LaunchIntersectBatch(const DeviceScene &S, const float *rays, int n, int anyHit, int *outPrim,
                                 float *outHit, hipStream_t s);
 size_t SurfaceTraversalStaticLds(int tm);
@@ -106,6 +108,14 @@ static void MediumTables(const SceneDesc &s, std::vector<int32_t> *info, std::ve
         for (int i = 0; i < 4; ++i)
             for (int j = 0; j < 4; ++j) params->push_back((float)inv[i][j]);
     }
+}
+
+// A hair material's 12 per-material floats in the matLayer slot (k_vlayered, the oracle's
+// MakeBSDF): {mode, sigma_a | color: kind value c0 c1 c2 scale pl, eta, beta_m, beta_n, alpha}
+static void HairLayer(const MaterialDesc &m, std::vector<float> *out) {
+    const SssSpectrumDesc &q = m.hairSpec;
+    out->insert(out->end(), {(float)m.hairMode, (float)q.kind, q.value, q.c0, q.c1, q.c2, q.scale, (float)q.pl, m.eta,
+                             m.hairBetaM, m.hairBetaN, m.hairAlpha});
 }
 
 // Subsurface tables (pbrt_scene_flat::material_sss / sss_params / sss_tables; the device
@@ -353,8 +363,11 @@ struct pbrt_scene {
         matSpectra.clear();
         matLayer.clear();
         for (auto &m : s.materials) {
-            matLayer.insert(matLayer.end(), {m.thickness, m.g, (float)m.maxDepth, (float)m.nSamples, m.a0, m.a1, m.a2,
-                                             m.albedoValue, m.albedoConstant ? 1.f : 0.f, m.cAlphaX, m.cAlphaY, (float)m.ifaceEtaSpec});
+            if (m.type == kMatHair) HairLayer(m, &matLayer);
+            else
+                matLayer.insert(matLayer.end(), {m.thickness, m.g, (float)m.maxDepth, (float)m.nSamples, m.a0, m.a1, m.a2,
+                                                 m.albedoValue, m.albedoConstant ? 1.f : 0.f, m.cAlphaX, m.cAlphaY,
+                                                 (float)m.ifaceEtaSpec});
             matCoeffs.insert(matCoeffs.end(), {m.c0, m.c1, m.c2, m.constantValue});
             matConstant.push_back(m.constant ? 1 : 0);
             matType.push_back(m.type);
@@ -790,6 +803,10 @@ static void BuildDevice(pbrt_context *c) {
         if (pll.empty()) pll.push_back(0), plv.push_back(0);
         std::vector<float> ml;
         for (auto &m : s.materials) {
+            if (m.type == kMatHair) {
+                HairLayer(m, &ml);
+                continue;
+            }
             // grey layer albedo uploaded as a constant (same bits, as the reflectances above)
             const bool grey = !m.albedoConstant && m.a0 == 0 && m.a1 == 0;
             const float av = grey ? SigmoidPolynomial(0.f, 0.f, m.a2, 500.f) : m.albedoValue;
@@ -1058,7 +1075,7 @@ static void BuildDevice(pbrt_context *c) {
     c->volumetric = !s.media.empty() ||
                     std::any_of(s.materials.begin(), s.materials.end(), [](const MaterialDesc &m) {
                         return m.type == kMatInterface || m.type == kMatCoatedDiffuse || m.type == kMatCoatedConductor ||
-                               m.type == kMatThinDielectric || m.type == kMatDiffuseTransmission;
+                               m.type == kMatThinDielectric || m.type == kMatDiffuseTransmission || m.type == kMatHair;
                     });
     S.dispersive = std::any_of(s.materials.begin(), s.materials.end(),
                                [](const MaterialDesc &m) { return ((m.type == kMatDielectric || m.type == kMatThinDielectric) && m.etaSpec >= 0) || m.ifaceEtaSpec >= 0;
@@ -2790,6 +2807,27 @@ int pbrt_debug_det_math(int device, int fn, const float *a, const float *b, int 
         if (n > 0) {
             HIPCHECK(LaunchDetMath(fn, da.p, db.p, n, dout.p, nullptr));
             HIPCHECK(hipMemcpy(out, dout.p, (size_t)n * sizeof(float), hipMemcpyDeviceToHost));
+        }
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_debug_hair(int device, const float *in16, int n, float *out) {
+    try {
+        if (!in16 || !out || n < 0) return Fail("pbrt_debug_hair: bad arguments");
+        if (device < 0) {  // the same code compiled for the host (libm transcendentals)
+            for (int i = 0; i < n; ++i) HairDebugEval(in16 + (size_t)kHairDebugIn * i, out + (size_t)kHairDebugOut * i);
+            return 0;
+        }
+        HIPCHECK(hipSetDevice(device));
+        DevBuf<float> din, dout;
+        din.Upload(std::vector<float>(in16, in16 + (size_t)kHairDebugIn * n));
+        dout.Alloc((size_t)kHairDebugOut * n);
+        if (n > 0) {
+            HIPCHECK(LaunchHairEval(din.p, n, dout.p, nullptr));
+            HIPCHECK(hipMemcpy(out, dout.p, (size_t)kHairDebugOut * n * sizeof(float), hipMemcpyDeviceToHost));
         }
         return 0;
     } catch (const std::exception &e) {

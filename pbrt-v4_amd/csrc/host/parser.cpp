@@ -661,6 +661,46 @@ class Parser {
         }
     }
 
+    // RGBUnboundedSpectrum(sRGB, rgb) (util/spectrum.cpp:230-244) as a SssSpectrumDesc
+    static SssSpectrumDesc UnboundedRGB(float r, float g, float b) {
+        SssSpectrumDesc q;
+        const float mx = std::max({r, g, b});
+        q.kind = 1;
+        q.scale = 2 * mx;
+        const auto c = q.scale ? RGBToSigmoidCoeffs(r / q.scale, g / q.scale, b / q.scale) : RGBToSigmoidCoeffs(0, 0, 0);
+        q.c0 = c[0], q.c1 = c[1], q.c2 = c[2];
+        return q;
+    }
+    // GetSpectrumTexture(name, SpectrumType::Albedo | Unbounded) of a constant "rgb" or
+    // "spectrum" parameter (textured forms are refused)
+    SssSpectrumDesc ConstSpectrum(Param *p, bool albedo, const std::string &loc, const char *mat) {
+        if (p->type == "texture")
+            throw Error(loc + ": textured \"" + p->name + "\" for the " + mat + " material is not supported yet");
+        if (p->type == "rgb") {
+            if (p->nums.size() != 3) throw Error(loc + ": " + p->name + " needs 3 values");
+            const float r = (float)p->nums[0], g = (float)p->nums[1], b = (float)p->nums[2];
+            if (albedo) {
+                if (r < 0 || r > 1 || g < 0 || g > 1 || b < 0 || b > 1)
+                    throw Error(loc + ": RGB parameter \"" + p->name + "\" used as an albedo has > 1 component.");
+                SssSpectrumDesc q;
+                q.kind = 1;
+                q.scale = 1;
+                const auto c = RGBToSigmoidCoeffs(r, g, b);
+                q.c0 = c[0], q.c1 = c[1], q.c2 = c[2];
+                return q;
+            }
+            if (r < 0 || g < 0 || b < 0) throw Error(loc + ": RGB parameter \"" + p->name + "\" has negative component.");
+            return UnboundedRGB(r, g, b);
+        }
+        if (p->type == "spectrum") {
+            SssSpectrumDesc q;
+            q.kind = 2;
+            q.pl = SpectrumParam(p, loc);
+            return q;
+        }
+        throw Error(loc + ": \"" + p->type + " " + p->name + "\" is not supported for the " + mat + " material yet");
+    }
+
     int MakeMaterial(const std::string &type, ParamSet &ps, const std::string &name, const std::string &dir) {
         MaterialDesc m;
         m.name = name;
@@ -742,43 +782,8 @@ class Parser {
             SubsurfaceDesc d;
             d.g = (float)ps.GetFloat("g", 0.0f);
             const std::string nm = ps.GetString("name", "");
-            auto unbounded = [&](float r, float g, float b) {
-                // RGBUnboundedSpectrum(sRGB, rgb) (util/spectrum.cpp:230-244)
-                SssSpectrumDesc q;
-                const float mx = std::max({r, g, b});
-                q.kind = 1;
-                q.scale = 2 * mx;
-                const auto c = q.scale ? RGBToSigmoidCoeffs(r / q.scale, g / q.scale, b / q.scale) : RGBToSigmoidCoeffs(0, 0, 0);
-                q.c0 = c[0], q.c1 = c[1], q.c2 = c[2];
-                return q;
-            };
-            // GetSpectrumTexture(name, SpectrumType) of a constant (no textures here yet)
-            auto param = [&](Param *p, bool albedo) {
-                if (p->type == "texture") throw Error(ps.loc + ": textured \"" + p->name + "\" for the subsurface material is not supported yet");
-                if (p->type == "rgb") {
-                    if (p->nums.size() != 3) throw Error(ps.loc + ": " + p->name + " needs 3 values");
-                    const float r = (float)p->nums[0], g = (float)p->nums[1], b = (float)p->nums[2];
-                    if (albedo) {
-                        if (r < 0 || r > 1 || g < 0 || g > 1 || b < 0 || b > 1)
-                            throw Error(ps.loc + ": RGB parameter \"" + p->name + "\" used as an albedo has > 1 component.");
-                        SssSpectrumDesc q;
-                        q.kind = 1;
-                        q.scale = 1;
-                        const auto c = RGBToSigmoidCoeffs(r, g, b);
-                        q.c0 = c[0], q.c1 = c[1], q.c2 = c[2];
-                        return q;
-                    }
-                    if (r < 0 || g < 0 || b < 0) throw Error(ps.loc + ": RGB parameter \"" + p->name + "\" has negative component.");
-                    return unbounded(r, g, b);
-                }
-                if (p->type == "spectrum") {
-                    SssSpectrumDesc q;
-                    q.kind = 2;
-                    q.pl = SpectrumParam(p, ps.loc);
-                    return q;
-                }
-                throw Error(ps.loc + ": \"" + p->type + " " + p->name + "\" is not supported for the subsurface material yet");
-            };
+            auto unbounded = [](float r, float g, float b) { return UnboundedRGB(r, g, b); };
+            auto param = [&](Param *p, bool albedo) { return ConstSpectrum(p, albedo, ps.loc, "subsurface"); };
             if (!nm.empty()) {
                 // GetMediumScatteringProperties (media.cpp:74-151, 160-165): measured sigma'_s and
                 // sigma_a in mm^-1 as RGBUnboundedSpectrum; g forced to 0
@@ -814,6 +819,43 @@ class Parser {
             d.table = ComputeBeamDiffusionTable(d.g, d.eta);
             m.sss = (int)scene.sss.size();
             scene.sss.push_back(std::move(d));
+        } else if (type == "hair") {
+            // HairMaterial::Create (materials.cpp:135-184): sigma_a, else reflectance / color,
+            // else eumelanin / pheomelanin (SigmaAFromConcentration, bxdfs.cpp:553-562), else
+            // eumelanin 1.3; eta 1.55, beta_m .3, beta_n .3, alpha 2.  Constant parameters only.
+            m.type = kMatHair;
+            Param *sa = ps.Find("sigma_a"), *refl = ps.Find("reflectance");
+            if (!refl) refl = ps.Find("color");
+            Param *eu = ps.Find("eumelanin"), *ph = ps.Find("pheomelanin");
+            auto warn = [&](const char *what) { std::fprintf(stderr, "%s: Warning: %s\n", ps.loc.c_str(), what); };
+            auto constFloat = [&](Param *p) {
+                if (p->type != "float" || p->nums.empty())
+                    throw Error(ps.loc + ": \"" + p->type + " " + p->name + "\" for the hair material is not supported yet (constant floats only)");
+                return (float)p->nums[0];
+            };
+            if (sa) {
+                if (refl) warn("Ignoring \"reflectance\" parameter since \"sigma_a\" was provided.");
+                if (eu) warn("Ignoring \"eumelanin\" parameter since \"sigma_a\" was provided.");
+                if (ph) warn("Ignoring \"pheomelanin\" parameter since \"sigma_a\" was provided.");
+                m.hairMode = 0;
+                m.hairSpec = ConstSpectrum(sa, false, ps.loc, "hair");
+            } else if (refl) {
+                if (eu) warn("Ignoring \"eumelanin\" parameter since \"reflectance\" was provided.");
+                if (ph) warn("Ignoring \"pheomelanin\" parameter since \"reflectance\" was provided.");
+                m.hairMode = 1;
+                m.hairSpec = ConstSpectrum(refl, true, ps.loc, "hair");
+            } else {
+                // the concentrations' RGB sigma_a (ce, cp clamped at 0 by GetBxDF)
+                const float ce = eu ? std::max(0.f, constFloat(eu)) : (ph ? 0.f : 1.3f);
+                const float cp = ph ? std::max(0.f, constFloat(ph)) : 0.f;
+                m.hairMode = 0;
+                m.hairSpec = UnboundedRGB(ce * 0.419f + cp * 0.187f, ce * 0.697f + cp * 0.4f, ce * 1.37f + cp * 1.05f);
+            }
+            m.eta = 1.55f;
+            if (Param *e = ps.Find("eta")) m.eta = constFloat(e);
+            if (Param *b = ps.Find("beta_m")) m.hairBetaM = constFloat(b);
+            if (Param *b = ps.Find("beta_n")) m.hairBetaN = constFloat(b);
+            if (Param *a = ps.Find("alpha")) m.hairAlpha = constFloat(a);
         } else if (type == "diffusetransmission") {
             // DiffuseTransmissionMaterial::Create (materials.cpp:620-645): reflectance and
             // transmittance default 0.25, scale 1; the transmittance rides in the albedo fields

@@ -40,6 +40,8 @@ constexpr int kMatDiffuseTransmission = 7;  // DiffuseTransmissionBxDF (bxdfs.h:
 // MixMaterial (materials.h:271-350): resolved per hit to one of its two materials by the
 // closest-hit stage (wavefront/intersect.h:90-97); never shaded itself
 constexpr int kMatMix = 8;
+// HairMaterial (materials.h:353-427): HairBxDF (bxdfs.h:1054-1152), k_vlayered
+constexpr int kMatHair = 9;
 
 // Participating media (media.h:209-350, media.cpp:167-330).  Spectra are DenselySampled
 // 395..705 nm tables in SceneDesc::denseSpectra with pbrt's constructor scaling applied
@@ -72,6 +74,11 @@ struct MediumDesc {
     float sigmaScale = 0;
 };
 
+struct SssSpectrumDesc {
+    int kind = 0;
+    float value = 0, c0 = 0, c1 = 0, c2 = 0, scale = 1;
+    int pl = -1;
+};
 struct MaterialDesc {
     int type = kMatDiffuse;
     // diffuse reflectance / conductor "reflectance": sigmoid (c0,c1,c2) or a constant value
@@ -105,6 +112,12 @@ struct MaterialDesc {
     // SubsurfaceMaterial: a dielectric-typed material (its DielectricBxDF from eta and the
     // alphas) with SceneDesc::sss[sss] as its BSSRDF; -1 for every other material
     int sss = -1;
+    // HairMaterial (eta in `eta`): hairMode 0 sigma_a = ClampZero(hairSpec) (given, or the
+    // eumelanin / pheomelanin RGB), 1 sigma_a = SigmaAFromReflectance(Clamp(hairSpec, 0, 1));
+    // beta_m / beta_n are clamped to [0.01, 1] per hit as GetBxDF does
+    int hairMode = 0;
+    SssSpectrumDesc hairSpec;
+    float hairBetaM = .3f, hairBetaN = .3f, hairAlpha = 2.f;
     std::string name;
 };
 
@@ -115,11 +128,6 @@ struct MaterialDesc {
 // RGBAlbedo reflectance with scale 1), 2 PiecewiseLinearSpectrum SceneDesc::plSpectra[pl].
 // The table is ComputeBeamDiffusionBSSRDF(g, eta) (host/bssrdf.cpp); fresnelC = 1 - 2
 // FresnelMoment1(1 / eta) for NormalizedFresnelBxDF.
-struct SssSpectrumDesc {
-    int kind = 0;
-    float value = 0, c0 = 0, c1 = 0, c2 = 0, scale = 1;
-    int pl = -1;
-};
 struct SubsurfaceDesc {
     int mode = 0;
     SssSpectrumDesc a, b;  // sigma_a, sigma_s | reflectance, mfp

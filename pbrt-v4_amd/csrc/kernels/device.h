@@ -64,6 +64,7 @@ constexpr int kMatCoatedDiffuseT = 4, kMatCoatedConductorT = 5;  // layered (vol
 constexpr int kMatThinDielectricT = 6;                           // volumetric path only
 constexpr int kMatDiffuseTransmissionT = 7;                      // k_vlayered
 constexpr int kMatMixT = 8;  // MixMaterial: resolved per hit by k_closest<kClosestMix>
+constexpr int kMatHairT = 9;  // HairBxDF: k_vlayered (volumetric path only)
 PHD int MatCounter(int type) { return type == 0 ? kCntMat : kCntMat + 3 + type; }
 PHD int CounterIndex(int depth, int queue, int shard) {
     return ((depth * kNumQueues + queue) * kShards + shard) * kCounterPad;

@@ -27,6 +27,7 @@
 #endif
 #include "common.h"
 #include "../core/bssrdf.h"
+#include "../core/hair.h"
 
 namespace pbrt_amd {
 
@@ -1402,7 +1403,8 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
             }
         }
         if (last) continue;
-        if (mtypeHit == kMatCoatedDiffuseT || mtypeHit == kMatCoatedConductorT || mtypeHit == kMatDiffuseTransmissionT)
+        if (mtypeHit == kMatCoatedDiffuseT || mtypeHit == kMatCoatedConductorT || mtypeHit == kMatDiffuseTransmissionT ||
+            mtypeHit == kMatHairT)
             continue;  // k_vlayered
         const int mtype = DiffuseOnly ? 0 : mtypeHit;
         // ---- EvaluateMaterialAndBSDF (surfscatter.cpp:57-328) for this material type
@@ -2166,8 +2168,10 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
         if (prim < 0) continue;
         const int mat = VolHitMaterial(S, st, ri, prim);
         const int mtype = S.matType[mat];
-        if (mtype != kMatCoatedDiffuseT && mtype != kMatCoatedConductorT && mtype != kMatDiffuseTransmissionT) continue;
-        const bool dt = mtype == kMatDiffuseTransmissionT;
+        if (mtype != kMatCoatedDiffuseT && mtype != kMatCoatedConductorT && mtype != kMatDiffuseTransmissionT &&
+            mtype != kMatHairT)
+            continue;
+        const bool dt = mtype == kMatDiffuseTransmissionT, hair = mtype == kMatHairT;
         const float lambda0 = rec.lambda0[ri];
         const int slot = rec.pixel[ri];
         const int depth = rec.depth[ri], flags = rec.flags[ri], medium = rec.medium[ri];
@@ -2188,7 +2192,7 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
         const float4 L0 = S.matLayer[3 * mat], L1 = S.matLayer[3 * mat + 1], L2 = S.matLayer[3 * mat + 2];
         const bool conductor = mtype == kMatCoatedConductorT;
         float ieta = mp4.z;
-        if (L2.w >= 0) {  // spectral interface eta: eta(lambda_0), TerminateSecondary
+        if (!hair && L2.w >= 0) {  // spectral interface eta: eta(lambda_0), TerminateSecondary
             const int es = (int)L2.w, a = S.plOffsets[es], na = S.plOffsets[es + 1] - a;
             ieta = PiecewiseLinearEval(S.plLambda + a, S.plValue + a, na, lambda0);
             if (ieta == 0) ieta = 1;
@@ -2199,10 +2203,20 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
         LayerSpec sp;
         bool bottomNz = false, albNz = false;
         float prMax = 0, ptMax = 0;
+        // HairMaterial::GetBxDF (materials.h:380-404): beta_m / beta_n clamped to [0.01, 1],
+        // h = -1 + 2 v; sigma_a per wavelength into sp.a (matLayer: HairLayer's packing)
+        const float hairBm = fmaxf(1e-2f, fminf(1.f, L2.y)), hairBn = fmaxf(1e-2f, fminf(1.f, L2.z));
+        const float hairDen = HairReflectanceDenom(hairBn);
+        const float hq[7] = {L0.y, L0.z, L0.w, L1.x, L1.y, L1.z, L1.w};
         {
             SpectralIter it(lambda0);
 #pragma unroll 1
             for (int i = 0; i < kNS; ++i, it.Next()) {
+                if (hair) {
+                    const float q = SssSpectrumAt(S, hq, it.lam);
+                    sp.a[i] = L0.x == 0 ? (q > 0 ? q : 0.f) : HairSigmaAFromReflectance(Clampf(q, 0, 1), hairDen);
+                    continue;
+                }
                 if (dt) {
                     // DiffuseTransmissionMaterial::GetBxDF: Clamp(scale * R, 0, 1), likewise T
                     const float r = constant ? mc.w : SigmoidPolynomial(mc.x, mc.y, mc.z, it.lam);
@@ -2243,7 +2257,9 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
         const LayeredBxDF<LayerSpec> L{ieta,         trTop, trBot, conductor, fmaxf(L0.x, 1.17549435e-38f),
                                        Clampf(L0.y, -1, 1), albNz, (int)L0.z,  (int)L0.w, 0, sp, bottomNz};
         const DiffuseTransmission<LayerSpec> D{sp, prMax, ptMax};
-        const int bflags = dt ? D.Flags() : L.LayerFlags();
+        HairState H{};
+        if (hair) H = MakeHair(-1 + 2 * si.uv[1], L2.x, hairBm, hairBn, L2.w);
+        const int bflags = hair ? (kBxGlossy | kBxReflection) : dt ? D.Flags() : L.LayerFlags();
         const Frame frame = Frame::FromXZ(Normalize(si.dpdus), si.ns);
         const V3 woL = frame.ToLocal(wo3);
         float fo[kNS];
@@ -2257,13 +2273,17 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
             if (SampleAreaLightAt<Ext>(S, cp, si.n, si.ns, rs.dUc, rs.dU0, rs.dU1, lambda0, &ls, cpErr) && woL.z != 0) {
                 const V3 wi = ls.wi;
                 const V3 wiL = frame.ToLocal(wi);
-                if (dt) D.f(woL, wiL, fo);
+                if (hair) HairF(H, sp.a, woL, wiL, fo);
+                else if (dt) D.f(woL, wiL, fo);
                 else L.f(woL, wiL, true, fo);
                 bool fnz = false;
 #pragma unroll 1
                 for (int i = 0; i < kNS; ++i) fnz |= fo[i] != 0;
                 if (fnz) {
-                    const float bsdfPDF = ls.delta ? 0.f : dt ? D.PDF(woL, wiL) : L.PDF(woL, wiL, true);
+                    const float bsdfPDF = ls.delta ? 0.f
+                                          : hair ? HairPDF(H, sp.a, woL, wiL)
+                                          : dt   ? D.PDF(woL, wiL)
+                                                 : L.PDF(woL, wiL, true);
                     const float absdot = AbsDotN(si.ns, wi);
                     const V3 so = OffsetRayOrigin(si.p, si.pErr, si.n, ls.p - si.p);
                     const V3 pt = OffsetRayOrigin(ls.p, ls.pErr, ls.n, so - ls.p);
@@ -2303,7 +2323,11 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
         // ---- BSDF::Sample_f + RR + indirect ray (surfscatter.cpp:170-250)
         if (woL.z == 0) continue;
         LayerSample bs;
-        if (dt) {
+        if (hair) {
+            bs.pdfIsProportional = false;
+            bs.flags = kBxGlossy | kBxReflection;
+            bs.ok = HairSampleF(H, sp.a, woL, rs.iUc, rs.iU0, rs.iU1, &bs.wi, &bs.pdf, fo);
+        } else if (dt) {
             bs.pdfIsProportional = false;
             bs.ok = D.Sample_f(woL, rs.iUc, rs.iU0, rs.iU1, &bs.wi, &bs.pdf, &bs.flags, fo);
         } else {
@@ -2827,8 +2851,9 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
     if (S.media.allGrey && S.media.hasCloud) hipLaunchKernelGGL(k_vmedium_grey<true>, gW, block, 0, s, S, st, v, wf);
     else if (S.media.allGrey) hipLaunchKernelGGL(k_vmedium_grey<false>, gW, block, 0, s, S, st, v, wf);
     else hipLaunchKernelGGL(k_vmedium, gW, block, 0, s, S, st, v, wf);
-    const int other = ~((1 << kMatDiffuseT) | (1 << 3) | (1 << kMatCoatedDiffuseT) | (1 << kMatCoatedConductorT) |
-                        (1 << kMatDiffuseTransmissionT));
+    const int layeredTypes =
+        (1 << kMatCoatedDiffuseT) | (1 << kMatCoatedConductorT) | (1 << kMatDiffuseTransmissionT) | (1 << kMatHairT);
+    const int other = ~((1 << kMatDiffuseT) | (1 << 3) | layeredTypes);
     const size_t surfLds = VolTablesLdsBytes(S) + kNS * kBlock * sizeof(float);
     const bool qcheck = QueueCheckOn() && wf != S.maxDepth;
     if (qcheck) {
@@ -2839,7 +2864,7 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
 #define VOL_REST(EXT) \
     if (wf == S.maxDepth) return hipGetLastError(); \
     if (S.matTypeMask & (1 << 3)) hipLaunchKernelGGL(k_viface<EXT>, gW, block, 0, s, S, st, v, wf); \
-    if (S.matTypeMask & ((1 << kMatCoatedDiffuseT) | (1 << kMatCoatedConductorT) | (1 << kMatDiffuseTransmissionT))) \
+    if (S.matTypeMask & layeredTypes) \
         hipLaunchKernelGGL(k_vlayered<EXT>, gW, block, 0, s, S, st, v, wf); \
     QUEUE_CHECK(2); \
     hipLaunchKernelGGL(k_vscatter<EXT>, gW, block, 0, s, S, st, v, wf); \

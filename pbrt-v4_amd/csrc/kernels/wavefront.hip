@@ -14,6 +14,7 @@
 // are separate queues (one per material tag present).  Launches are grid-stride over the
 // device-side queue counters so the host never synchronises inside the render loop.
 #include "common.h"
+#include "../core/hair.h"
 
 namespace pbrt_amd {
 // Traversal LDS of one block (shared with volpath.hip): group stack (uint2 entries), cached
@@ -1585,6 +1586,15 @@ __global__ void k_det_math(int fn, const float *a, const float *b, int n, float 
 }
 hipError_t LaunchDetMath(int fn, const float *a, const float *b, int n, float *out, hipStream_t s) {
     hipLaunchKernelGGL(k_det_math, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, fn, a, b, n, out);
+    return hipGetLastError();
+}
+// HairBxDF f / PDF / Sample_f per query (core/hair.h HairDebugEval; pbrt_debug_hair)
+__global__ void k_hair_eval(const float *in, int n, float *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) HairDebugEval(in + (size_t)kHairDebugIn * i, out + (size_t)kHairDebugOut * i);
+}
+hipError_t LaunchHairEval(const float *in, int n, float *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_hair_eval, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, in, n, out);
     return hipGetLastError();
 }
 hipError_t LaunchCheckRNMath(uint64_t seed, int blocks, int perThread, unsigned long long *bad, hipStream_t s) {

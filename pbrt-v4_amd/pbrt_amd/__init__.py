@@ -139,7 +139,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_context_free", "pbrt_render", "pbrt_synchronize", "pbrt_get_stats", "pbrt_reset_stats",
     "pbrt_film_clear", "pbrt_film_device_ptr", "pbrt_film_read", "pbrt_film_get_rgb", "pbrt_intersect",
     "pbrt_debug_halton", "pbrt_debug_halton_fastpath_mismatches", "pbrt_debug_catmull_rom", "pbrt_debug_check_rn_math", "pbrt_debug_rgb_coeffs", "pbrt_debug_rgb2spec_column", "pbrt_debug_kernel_sections",
-    "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_sampler", "pbrt_debug_rng", "pbrt_debug_det_math", "pbrt_debug_procedural", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
+    "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_sampler", "pbrt_debug_rng", "pbrt_debug_det_math", "pbrt_debug_hair", "pbrt_debug_procedural", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
     "pbrt_debug_named_spectrum", "pbrt_debug_bxdf", "pbrt_debug_layered", "pbrt_debug_triangle_shading", "pbrt_film_write_image",
     "pbrt_image_read_size", "pbrt_image_read", "pbrt_image_write", "pbrt_image_error", "pbrt_debug_filter_sample",
     "pbrt_debug_bvh_stats", "pbrt_debug_light_bvh", "pbrt_intersect_tr", "pbrt_intersect_one_random", "pbrt_image_flip", "pbrt_set_kernel_profiling", "pbrt_get_kernel_stats",
@@ -218,6 +218,7 @@ def _lib():
     lib.pbrt_debug_sampler.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_int, c.POINTER(c.c_float)]
     lib.pbrt_debug_rng.argtypes = [c.c_uint64, c.c_uint64, c.POINTER(c.c_uint32)]
     lib.pbrt_debug_det_math.argtypes = [c.c_int, c.c_int, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
+    lib.pbrt_debug_hair.argtypes = [c.c_int, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_debug_procedural.argtypes = [c.c_int, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_debug_queue_counts.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_int]
     lib.pbrt_debug_trowbridge.argtypes = [c.c_void_p, c.c_void_p]
@@ -487,6 +488,19 @@ def det_math(fn, a, b=None, device=-1):
     out = np.zeros_like(a)
     _check(_lib().pbrt_debug_det_math(device, DET_MATH_FNS.index(fn), a.ctypes.data, b.ctypes.data, len(a),
                                       out.ctypes.data))
+    return out
+
+
+HAIR_IN, HAIR_OUT = 16, 68
+
+
+def hair_eval(queries, device=-1):
+    """HairBxDF f / PDF / Sample_f (core/hair.h) on [n][16] queries {h, eta, beta_m, beta_n,
+    alpha, sigma_a0, wo, wi, uc, u0, u1, slope} -> [n][68] {f[31], pdf, ok, wi', pdf', f'[31]}, on
+    GPU `device` or compiled for the host (device < 0): pbrt_debug_hair."""
+    q = np.ascontiguousarray(queries, np.float32).reshape(-1, HAIR_IN)
+    out = np.zeros((len(q), HAIR_OUT), np.float32)
+    _check(_lib().pbrt_debug_hair(device, q.ctypes.data, len(q), out.ctypes.data))
     return out
 
 

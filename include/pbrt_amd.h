@@ -109,7 +109,8 @@ typedef struct pbrt_scene_flat {
     const float *pl_lambda, *pl_value;
     int regularize;                   /* integrator "regularize" */
     /* shading attributes (TriangleMesh n / uv): per vertex, or NULL when no mesh has any;
-     * tri_shading[t] bit0 = triangle t uses vertex normals, bit1 = uv */
+     * tri_shading[t] bit0 = triangle t uses vertex normals, bit1 = uv, bit2 = tangents S
+     * (vertex_s below) */
     const float *vertex_normals;      /* [n_vertices][3] render space */
     const float *vertex_uv;           /* [n_vertices][2] */
     const uint8_t *tri_shading;       /* [n_triangles] */
@@ -253,6 +254,10 @@ typedef struct pbrt_scene_flat {
     const int32_t *material_sss;
     const float *sss_params;
     const float *sss_tables;
+    /* per-vertex shading tangents (TriangleMesh s, "vector3 S"), render space, or NULL; used by
+     * the triangles whose tri_shading bit2 is set (entries past the array are zero) */
+    const float *vertex_s;            /* [n_vertex_s][3] */
+    int n_vertex_s;
 } pbrt_scene_flat;
 
 typedef struct pbrt_render_params {

@@ -987,8 +987,8 @@ struct Interaction {
 
 // a mesh triangle's optional vertex normals and uv (TriangleMesh n / uv, util/mesh.h:23-46)
 struct TriAttr {
-    bool hasN = false, hasUV = false;
-    Vec n[3];
+    bool hasN = false, hasUV = false, hasS = false;
+    Vec n[3], s[3];
     Float uv[3][2] = {{0, 0}, {1, 0}, {1, 1}};
 };
 
@@ -1020,10 +1020,18 @@ static Interaction TriangleInteraction(Vec p0, Vec p1, Vec p2, bool flip, TriIse
     si.dpdv = dpdv;
     // Point2f uvHit = b0 * uv[0] + b1 * uv[1] + b2 * uv[2] (shapes.h:920)
     for (int k = 0; k < 2; ++k) si.uv[k] = ti.b0 * a.uv[0][k] + ti.b1 * a.uv[1][k] + ti.b2 * a.uv[2][k];
-    if (a.hasN) {
-        Vec ns = ti.b0 * a.n[0] + ti.b1 * a.n[1] + ti.b2 * a.n[2];
-        ns = LengthSquared(ns) > 0 ? Normalize(ns) : si.n;
-        Vec ss = si.dpdu, ts = Cross(ns, ss);
+    if (a.hasN || a.hasS) {
+        Vec ns = si.n;
+        if (a.hasN) {
+            ns = ti.b0 * a.n[0] + ti.b1 * a.n[1] + ti.b2 * a.n[2];
+            ns = LengthSquared(ns) > 0 ? Normalize(ns) : si.n;
+        }
+        Vec ss = si.dpdu;
+        if (a.hasS) {  // shapes.h:951-957
+            ss = ti.b0 * a.s[0] + ti.b1 * a.s[1] + ti.b2 * a.s[2];
+            if (LengthSquared(ss) == 0) ss = si.dpdu;
+        }
+        Vec ts = Cross(ns, ss);
         if (LengthSquared(ts) > 0) ss = Cross(ts, ns);
         else CoordinateSystem(ns, &ss, &ts);
         si.ns = ns;
@@ -1038,7 +1046,9 @@ static Interaction TriangleInteraction(Vec p0, Vec p1, Vec p2, bool flip, TriIse
         si.hasShadingDiff = true;
         const Vec dn1 = a.n[0] - a.n[2], dn2 = a.n[1] - a.n[2];
         const Float det = DifferenceOfProducts(duv02[0], duv12[1], duv02[1], duv12[0]);
-        if (std::abs(det) < 1e-9f) {
+        if (!a.hasN) {
+            // no vertex normals: dndu = dndv = 0
+        } else if (std::abs(det) < 1e-9f) {
             const Vec dn = Cross(a.n[2] - a.n[0], a.n[1] - a.n[0]);
             if (LengthSquared(dn) != 0) CoordinateSystem(dn, &si.dndus, &si.dndvs);
         } else {
@@ -1092,9 +1102,12 @@ struct Scene {
                 a.uv[k][0] = f->vertex_uv[2 * vi];
                 a.uv[k][1] = f->vertex_uv[2 * vi + 1];
             }
+            if ((bits & 4) && vi < f->n_vertex_s)
+                a.s[k] = Vec(f->vertex_s[3 * vi], f->vertex_s[3 * vi + 1], f->vertex_s[3 * vi + 2]);
         }
         a.hasN = bits & 1;
         a.hasUV = bits & 2;
+        a.hasS = bits & 4;
         return a;
     }
 

@@ -39,6 +39,7 @@ hipError_t LaunchFilm(const DeviceScene &S, const PathState &st, int nSamples, h
 hipError_t LaunchCheckRNMath(uint64_t seed, int blocks, int perThread, unsigned long long *bad, hipStream_t s);
 hipError_t LaunchDetMath(int fn, const float *a, const float *b, int n, float *out, hipStream_t s);
 hipError_t LaunchHairEval(const float *in, int n, float *out, hipStream_t s);
+hipError_t LaunchQueueOverflowCheck(const PathState &st, int nDepths, hipStream_t s);
 hipError_t LaunchIntersectBatch(const DeviceScene &S, const float *rays, int n, int anyHit, int *outPrim,
                                 float *outHit, hipStream_t s);
 size_t SurfaceTraversalStaticLds(int tm);
@@ -497,7 +498,7 @@ struct pbrt_context {
     DevBuf<int> primOrig, matType, matSpectra, plOffsets, matSss;
     DevBuf<float> sssParams, sssTables, sssF;
     DevBuf<int> sssI;
-    DevBuf<float> matParams, plLambda, plValue, triShade, matLayer, dispL0;
+    DevBuf<float> matParams, plLambda, plValue, triShade, triTangent, matLayer, dispL0;
     DevBuf<uint16_t> plIndex;
     DevBuf<int> dispTerm;
     DevBuf<uint8_t> primFlip;
@@ -768,6 +769,22 @@ static void BuildDevice(pbrt_context *c) {
             d[15] = s.vertUV[t[2]][1];
         }
         c->triShade.Upload(ts);
+    }
+    // shading tangents per leaf triangle (triShade bit2): s0 s1 s2 as float4
+    if (std::any_of(s.triShade.begin(), s.triShade.end(), [](uint8_t f) { return (f & 4) != 0; })) {
+        std::vector<float> tt((size_t)nt * 12, 0.f);
+        for (int i = 0; i < nt; ++i) {
+            const int o = b.triPrim[i];
+            if (!(s.triShade[o] & 4)) continue;
+            const auto &t = s.tris[o];
+            for (int k = 0; k < 3; ++k) {
+                const V3 v = t[k] < (int)s.vertS.size() ? s.vertS[t[k]] : V3(0, 0, 0);
+                tt[(size_t)i * 12 + 4 * k] = v.x;
+                tt[(size_t)i * 12 + 4 * k + 1] = v.y;
+                tt[(size_t)i * 12 + 4 * k + 2] = v.z;
+            }
+        }
+        c->triTangent.Upload(tt);
     }
     std::vector<float> mc;
     std::vector<int> mk;
@@ -1120,6 +1137,7 @@ static void BuildDevice(pbrt_context *c) {
     S.shapeNodes = c->shapeNodes.p;
     S.shapeN = c->shapeN.p;
     S.triShade = (const float4 *)c->triShade.p;
+    S.triTangent = (const float4 *)c->triTangent.p;
     S.matCoeffs = (const float4 *)c->matCoeffs.p;
     S.matConstant = c->matConstant.p;
     S.nMaterials = (int)s.materials.size();
@@ -1498,7 +1516,10 @@ static int64_t PathStateBytesPerPath(bool volumetric, bool dispersive, bool text
 static void AllocPaths(pbrt_context *c, int64_t N) {
     if (N <= c->maxPaths) return;
     const int nf = kPathFloats, ni = kPathInts;
-    const int64_t capS = ((N + kShards - 1) / kShards + 256 + 63) / 64 * 64;
+    // per-shard capacity: the fair share plus one 256-item chunk per producer kernel of a queue
+    // (a producer's block b pushes into shard b % kShards and its grid is a multiple of kShards,
+    // so each producer overshoots a shard's share by less than one chunk; up to kShards producers)
+    const int64_t capS = ((N + kShards - 1) / kShards + 256 * kShards + 63) / 64 * 64;
     const int64_t NR = capS * kShards;  // record stride
     // kernels index [k][NR] arrays with 32-bit k * NR for k <= 11 (spectral ones use size_t)
     if (NR > INT32_MAX / 12) throw Error("max_paths too large: " + std::to_string(N));
@@ -1780,6 +1801,7 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
                                     "it never wrote (iteration " + std::to_string(wf) + "); render aborted");
                     HIPCHECK(e);
                 }
+                HIPCHECK(LaunchQueueOverflowCheck(st, s.maxDepth + 2, c->stream));
                 {
                     StageTimer t(c, "Update film (k_film)", c->stream);
                     HIPCHECK(LaunchFilm(c->S, st, nS, c->stream));
@@ -1876,6 +1898,7 @@ static void RenderImpl(pbrt_context *c, const pbrt_render_params *p) {
                     HIPCHECK(LaunchShadow(c->S, st, depth, (int)nActive, c->stream));
                 }
             }
+            HIPCHECK(LaunchQueueOverflowCheck(st, s.maxDepth + 2, c->stream));
             {
                 StageTimer t(c, "Update film (k_film)", c->stream);
                 HIPCHECK(LaunchFilm(c->S, st, nS, c->stream));
@@ -2077,6 +2100,8 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
     f->material_sss = s.sss.empty() ? nullptr : scene->matSss.data();
     f->sss_params = s.sss.empty() ? nullptr : scene->sssParams.data();
     f->sss_tables = s.sss.empty() ? nullptr : scene->sssTables.data();
+    f->vertex_s = s.vertS.empty() ? nullptr : &s.vertS[0].x;
+    f->n_vertex_s = (int)s.vertS.size();
     f->dims_per_depth = s.sss.empty() ? 7 : 10;
     f->material_params = scene->matParams.data();
     f->material_layer = scene->matLayer.data();
@@ -2171,6 +2196,11 @@ int pbrt_synchronize(pbrt_context *ctx) {
         CollectStageEvents(ctx);
         unsigned long long ds[8];
         HIPCHECK(hipMemcpy(ds, ctx->devStats.p, sizeof ds, hipMemcpyDeviceToHost));
+        if (ds[kStatQueueOverflow]) {
+            HIPCHECK(hipMemset(ctx->devStats.p + kStatQueueOverflow, 0, sizeof(unsigned long long)));
+            return Fail("queue overflow: " + std::to_string(ds[kStatQueueOverflow]) +
+                        " queue shard(s) exceeded their capacity; the film of this render is invalid");
+        }
         ctx->stats.camera_rays = ds[0];
         ctx->stats.closest_rays = ds[1];
         ctx->stats.shadow_rays = ds[2];

@@ -538,9 +538,10 @@ PHD bool IntersectTriangle(V3 o, V3 dir, float tMax, V3 p0, V3 p1, V3 p2, TriHit
 // Per-triangle shading attributes of TriangleMesh (util/mesh.h:23-46): vertex normals and
 // uv, each optional (flags bit0 / bit1).
 struct TriShading {
-    int flags = 0;
+    int flags = 0;      // bit0 vertex normals, bit1 uv, bit2 shading tangents S
     V3 n0, n1, n2;
     float uv[3][2];
+    V3 s0, s1, s2;
 };
 struct TriSurface {
     V3 p, pErr, n, dpdu;
@@ -589,10 +590,17 @@ PHD TriSurface TriangleSurface(V3 p0, V3 p1, V3 p2, float b0, float b1, float b2
     s.dpdu = dpdu;
     s.ns = n;
     s.dpdus = dpdu;
-    if (sh && (sh->flags & 1)) {
-        V3 ns = b0 * sh->n0 + b1 * sh->n1 + b2 * sh->n2;
-        ns = LengthSquared(ns) > 0 ? Normalize(ns) : s.n;
+    if (sh && (sh->flags & 5)) {  // mesh->n || mesh->s (shapes.h:940-960)
+        V3 ns = s.n;
+        if (sh->flags & 1) {
+            ns = b0 * sh->n0 + b1 * sh->n1 + b2 * sh->n2;
+            ns = LengthSquared(ns) > 0 ? Normalize(ns) : s.n;
+        }
         V3 ss = s.dpdu;
+        if (sh->flags & 4) {
+            ss = b0 * sh->s0 + b1 * sh->s1 + b2 * sh->s2;
+            if (LengthSquared(ss) == 0) ss = s.dpdu;
+        }
         V3 ts = Cross(ns, ss);
         if (LengthSquared(ts) > 0) ss = Cross(ts, ns);
         else CoordinateSystem(ns, &ss, &ts);

@@ -330,6 +330,7 @@ class Parser {
         std::vector<int> idx;
         std::vector<float> uv;  // per vertex, 2 floats
         std::vector<V3> N;      // per vertex (object space)
+        std::vector<V3> S;      // per-vertex shading tangents (object space; trianglemesh "S")
         std::string insideMedium, outsideMedium;
         Mat4 renderFromObject;
         bool flip;
@@ -1239,7 +1240,19 @@ class Parser {
                 if (N->nums.size() != 3 * s.P.size()) throw Error(ps.loc + ": N count mismatch");
                 for (size_t i = 0; i < N->nums.size(); i += 3) s.N.push_back(V3(N->nums[i], N->nums[i + 1], N->nums[i + 2]));
             }
-            if (ps.Find("S")) throw Error(ps.loc + ": per-vertex shading tangents \"S\" are not supported yet");
+            // per-vertex shading tangents (shapes.cpp:408-413): a count mismatch is reported and
+            // the tangents discarded, as pbrt's Error() does
+            Param *Sp = ps.Find("S", "vector3");
+            if (!Sp) Sp = ps.Find("S", "vector");
+            if (Sp) {
+                if (Sp->nums.size() != 3 * s.P.size()) {
+                    std::fprintf(stderr, "%s: Error: Number of \"S\"s for triangle mesh must match \"P\"s. Discarding \"S\"s.\n",
+                                 ps.loc.c_str());
+                } else {
+                    for (size_t i = 0; i < Sp->nums.size(); i += 3)
+                        s.S.push_back(V3(Sp->nums[i], Sp->nums[i + 1], Sp->nums[i + 2]));
+                }
+            }
             ps.Find("faceIndices");
         } else if (type == "plymesh") {
             std::string f = ps.GetString("filename", "");
@@ -2089,7 +2102,12 @@ void Parser::Finish() {
         for (V3 p : s.P) scene.verts.push_back(XformPoint(rfo, p));
         // normals: renderFromObject(n) (inverse transpose), negated under ReverseOrientation
         // (TriangleMesh ctor, util/mesh.cpp:49-57); uv as given
-        const uint8_t shadeBits = (s.N.empty() ? 0 : 1) | (s.uv.empty() ? 0 : 2);
+        const uint8_t shadeBits = (s.N.empty() ? 0 : 1) | (s.uv.empty() ? 0 : 2) | (s.S.empty() ? 0 : 4);
+        // shading tangents: renderFromObject(s) as a vector, not flipped (util/mesh.cpp:58-63)
+        if (!s.S.empty() || !scene.vertS.empty()) {
+            scene.vertS.resize(base, V3(0, 0, 0));
+            for (size_t i = 0; i < s.P.size(); ++i) scene.vertS.push_back(s.S.empty() ? V3(0, 0, 0) : XformVector(rfo, s.S[i]));
+        }
         if (shadeBits || !scene.vertN.empty()) {
             scene.vertN.resize(base, V3(0, 0, 0));
             scene.vertUV.resize(base, {0.f, 0.f});
@@ -2990,12 +3008,24 @@ void Parser::ResolveTextures() {
     }
 }
 
+// bump / normal mapping on a mesh with shading tangents "S" would need its shading dpdv (the
+// bitangent), which the texture stage does not carry: refused
+static void CheckTangentFrames(const SceneDesc &s) {
+    for (size_t o = 0; o < s.triShade.size(); ++o)
+        if (s.triShade[o] & 4) {
+            const MaterialDesc &m = s.materials[s.triMaterial[o]];
+            if (m.texDisp >= 0 || m.normalMap >= 0)
+                throw Error("bump or normal mapping on a triangle mesh with shading tangents \"S\" is not supported yet");
+        }
+}
+
 SceneDesc LoadPbrtString(const std::string &text, const std::string &baseDir,
                          const std::map<std::string, std::string> &overrides) {
     SceneDesc s;
     Parser p(s, overrides);
     p.ParseString(text, "<string>", baseDir);
     p.Finish();
+    CheckTangentFrames(s);
     FinalizeScene(s);
     return s;
 }
@@ -3005,6 +3035,7 @@ SceneDesc LoadPbrtFile(const std::string &path, const std::map<std::string, std:
     Parser p(s, overrides);
     p.ParseFile(path);
     p.Finish();
+    CheckTangentFrames(s);
     FinalizeScene(s);
     return s;
 }

@@ -355,6 +355,7 @@ struct SceneDesc {
     // only for triangles whose triShade bit says so (bit0 normals, bit1 uv)
     std::vector<V3> vertN;                       // render space, reverseOrientation applied
     std::vector<std::array<float, 2>> vertUV;
+    std::vector<V3> vertS;  // per-vertex shading tangents, render space (triShade bit2)
     std::vector<uint8_t> triShade;
     std::vector<AnalyticShapeDesc> shapes;  // spheres and disks
 

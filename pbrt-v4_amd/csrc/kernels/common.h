@@ -905,6 +905,12 @@ __device__ inline bool LoadTriShading(const DeviceScene &S, int prim, TriShading
     sh->uv[1][1] = d.y;
     sh->uv[2][0] = d.z;
     sh->uv[2][1] = d.w;
+    if ((flags & 4) && S.triTangent) {
+        const float4 s0 = S.triTangent[3 * prim], s1 = S.triTangent[3 * prim + 1], s2 = S.triTangent[3 * prim + 2];
+        sh->s0 = V3(s0.x, s0.y, s0.z);
+        sh->s1 = V3(s1.x, s1.y, s1.z);
+        sh->s2 = V3(s2.x, s2.y, s2.z);
+    }
     return true;
 }
 

@@ -50,8 +50,10 @@ struct ShadeLdsLayout {
 // shard with its own counter on its own cache line.  Same-line atomics serialise at ~11 ns
 // each on MI355X (tools/microbench/atomics.hip); kShards lines take the queue appends off the
 // critical path.  Producer grids are multiples of kShards and grid-stride in 256-item
-// chunks, so shard s receives at most count/kShards + 256 items: capS = N/kShards + 256
-// bounds every shard, and the records need no more memory than an unsharded queue.
+// chunks, so one producer kernel gives shard s at most its count/kShards + 256 items; a queue
+// fed by several producers (surface, layered, medium, subsurface stages) can overshoot by one
+// chunk per producer, so capS = N/kShards + 256 kShards, and every pass ends with a check that
+// no shard overflowed (k_queue_overflow).
 constexpr int kShards = 8;
 constexpr int kCounterPad = 64;  // ints between counters (256 B)
 constexpr int kNumQueues = 8;
@@ -71,6 +73,7 @@ PHD int CounterIndex(int depth, int queue, int shard) {
 }
 // device stats slots: [0..7] ray counters, [16..47] per-section wave cycles (profiling build)
 constexpr int kStatsSlots = 48, kStatsSectionBase = 16;
+constexpr int kStatQueueOverflow = 4;  // stats slot: queue counters found above capS (k_queue_overflow)
 constexpr int kMaxStackSize = 32;  // traversal stack entries per lane (uint2: 64 KB of LDS per block)
 constexpr int kSceneLdsBudget = 16 * 1024;  // bytes of BVH nodes + triangles cached in LDS per block (at most)
 // Traversal kernels run 256-thread blocks at PBRT_TRAVERSAL_WAVES blocks (= waves per SIMD) per
@@ -142,6 +145,7 @@ struct DeviceScene {
     // per-triangle shading attributes (leaf order, 4 float4 each: n0|flags, n1|u0, n2|v0,
     // u1 v1 u2 v2), nullptr when no mesh has vertex normals or uv
     const float4 *triShade;
+    const float4 *triTangent;  // [3][nTris] shading tangents S (triShade bit2), or nullptr
     // materials
     const float4 *matCoeffs;  // c0, c1, c2, constant value
     const int *matConstant;

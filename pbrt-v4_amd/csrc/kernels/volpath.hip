@@ -2843,6 +2843,26 @@ hipError_t LaunchVolClosest(const DeviceScene &S, const PathState &st, const Vol
     }
     return hipGetLastError();
 }
+// TraceShadowRays (integrator.cpp:575-586) of iteration wf: the queued shadow rays, through
+// media when the scene has any
+static void LaunchVolShadows(const DeviceScene &S, const PathState &st, const VolState &v, int wf, dim3 gT,
+                             hipStream_t s) {
+    const dim3 block(kBlock);
+    if (S.media.allGrey && S.media.hasCloud) {
+#define K_VSHADOW_GREY(tm) k_vshadow_grey<tm, true>
+        PBRT_LAUNCH_TRAVERSAL(S, K_VSHADOW_GREY, gT, block, VolStackBytes(S), s, S, st, v, wf);
+#undef K_VSHADOW_GREY
+    } else if (S.media.allGrey) {
+#define K_VSHADOW_GREY(tm) k_vshadow_grey<tm, false>
+        PBRT_LAUNCH_TRAVERSAL(S, K_VSHADOW_GREY, gT, block, VolStackBytes(S), s, S, st, v, wf);
+#undef K_VSHADOW_GREY
+    } else {
+#define K_VSHADOW(tm) k_vshadow<tm>
+        PBRT_LAUNCH_TRAVERSAL(S, K_VSHADOW, gT, block, VolStackBytes(S), s, S, st, v, wf);
+#undef K_VSHADOW
+    }
+}
+
 // the rest of wavefront iteration wf after its closest-hit launch
 hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const VolState &v, int wf, int maxCount,
                               hipStream_t s) {
@@ -2869,6 +2889,10 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
     QUEUE_CHECK(2); \
     hipLaunchKernelGGL(k_vscatter<EXT>, gW, block, 0, s, S, st, v, wf); \
     if (S.matSss) { \
+        /* the shadow rays so far first, so the subsurface exits have the queue to themselves \
+           ("so that we have space for shadow rays for subsurface", integrator.cpp:427-431) */ \
+        LaunchVolShadows(S, st, v, wf, gT, s); \
+        (void)hipMemsetAsync(st.counters + CounterIndex(wf, kVShadow, 0), 0, sizeof(int) * kShards * kCounterPad, s); \
         PBRT_LAUNCH_TRAVERSAL(S, K_VSSS_PROBE, gT, block, VolStackBytes(S), s, S, st, v, wf); \
         hipLaunchKernelGGL(k_vsss_scatter<EXT>, gW, block, VolTablesLdsBytes(S), s, S, st, v, wf); \
     } \
@@ -2915,19 +2939,7 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
         if (h > 0) return hipErrorIllegalState;  // nothing consumes the unwritten records
     }
 #undef QUEUE_CHECK
-    if (S.media.allGrey && S.media.hasCloud) {
-#define K_VSHADOW_GREY(tm) k_vshadow_grey<tm, true>
-        PBRT_LAUNCH_TRAVERSAL(S, K_VSHADOW_GREY, gT, block, VolStackBytes(S), s, S, st, v, wf);
-#undef K_VSHADOW_GREY
-    } else if (S.media.allGrey) {
-#define K_VSHADOW_GREY(tm) k_vshadow_grey<tm, false>
-        PBRT_LAUNCH_TRAVERSAL(S, K_VSHADOW_GREY, gT, block, VolStackBytes(S), s, S, st, v, wf);
-#undef K_VSHADOW_GREY
-    } else {
-#define K_VSHADOW(tm) k_vshadow<tm>
-        PBRT_LAUNCH_TRAVERSAL(S, K_VSHADOW, gT, block, VolStackBytes(S), s, S, st, v, wf);
-#undef K_VSHADOW
-    }
+    LaunchVolShadows(S, st, v, wf, gT, s);
     return hipGetLastError();
 }
 

@@ -1588,6 +1588,21 @@ hipError_t LaunchDetMath(int fn, const float *a, const float *b, int n, float *o
     hipLaunchKernelGGL(k_det_math, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, fn, a, b, n, out);
     return hipGetLastError();
 }
+// A pass's queue-capacity check: a shard's count above capS means its producers wrote past the
+// shard into the next one (AllocPaths sizes the per-shard slack for kShards producer kernels of
+// one queue); st.stats[kStatQueueOverflow] counts such counters and pbrt_synchronize fails.  The
+// depth-0 ray queue keeps every camera ray in shard 0 and is exempt.
+__global__ void k_queue_overflow(PathState st, int nDepths) {
+    const int n = nDepths * kNumQueues * kShards;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        if (i < kShards) continue;  // depth 0, queue 0
+        if (st.counters[i * kCounterPad] > st.capS) atomicAdd(&st.stats[kStatQueueOverflow], 1ull);
+    }
+}
+hipError_t LaunchQueueOverflowCheck(const PathState &st, int nDepths, hipStream_t s) {
+    hipLaunchKernelGGL(k_queue_overflow, dim3(1), dim3(kBlock), 0, s, st, nDepths);
+    return hipGetLastError();
+}
 // HairBxDF f / PDF / Sample_f per query (core/hair.h HairDebugEval; pbrt_debug_hair)
 __global__ void k_hair_eval(const float *in, int n, float *out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;

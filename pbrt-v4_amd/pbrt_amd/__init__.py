@@ -111,6 +111,7 @@ class SceneFlat(ctypes.Structure):
         ("material_sss", ctypes.POINTER(ctypes.c_int32)),
         ("sss_params", ctypes.POINTER(ctypes.c_float)),
         ("sss_tables", ctypes.POINTER(ctypes.c_float)),
+        ("vertex_s", ctypes.POINTER(ctypes.c_float)), ("n_vertex_s", ctypes.c_int),
     ]
 
 

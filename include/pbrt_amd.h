@@ -196,7 +196,7 @@ typedef struct pbrt_scene_flat {
     const int32_t *material_mix;
     /* ImageInfiniteLight (lights.h:557-641): infinite-list entry j is an image light when
      * inf_image[j] >= 0 (its index here); per image light env_info [n_env][4] res (square),
-     * 0, 0, 0, env_xform [n_env][18] renderFromLight then its inverse (upper 3x3, row major),
+     * portal flag, 0, 0, env_xform [n_env][18] renderFromLight then its inverse (upper 3x3, row major),
      * and its linear R, G, B pixels (Image::GetChannel) at env_rgb + 3 * env_offset[k]
      * ([res][res][3], row y = v * res).  inf_spectrum / inf_scale hold the colour space's
      * illuminant and the light's scale. */
@@ -258,6 +258,9 @@ typedef struct pbrt_scene_flat {
      * the triangles whose tri_shading bit2 is set (entries past the array are zero) */
     const float *vertex_s;            /* [n_vertex_s][3] */
     int n_vertex_s;
+    /* PortalImageInfiniteLight: env_info[4k + 1] = 1 for a portal light, whose render-space
+     * portal corners are env_portal [n_env][4][3] (zeros for the others) */
+    const float *env_portal;
 } pbrt_scene_flat;
 
 typedef struct pbrt_render_params {
@@ -401,6 +404,12 @@ int pbrt_debug_texture_eval(const pbrt_scene *scene, int material, int slot, con
  * EqualAreaSquareToSphere(u, v)), PiecewiseConstant2D::PDF at that sample, PDF at u taken as a
  * point of [0,1]^2, 1 unused */
 int pbrt_debug_env_eval(const pbrt_scene *scene, int env, const float *dirs, const float *u, int n, float *out);
+/* PortalImageInfiniteLight `env` (lights.cpp:1140-1297) on the host: per query q8 = {p[3], d[3],
+ * u0, u1}: out16 = {Le(ray p, d) at 400 / 500 / 600 / 700 nm (light scale 1, illuminant 1),
+ * PDF_Li(p, d), SampleLi(p, u) ok, wi[3], pdf, the sample's Le at the four wavelengths,
+ * ImageBounds(p) ok, 0}; img (optional, res * res * 4 floats): the rectified image [res][res][3]
+ * then the windowed distribution's function [res][res] */
+int pbrt_debug_portal_eval(const pbrt_scene *scene, int env, const float *q8, int n, float *out16, float *img);
 /* EqualAreaSquareToSphere (to_sphere != 0: in[n][2] -> out[n][3]) or EqualAreaSphereToSquare
  * (in[n][3] -> out[n][2]) with the product's shared host/device code (util/math.cpp:292-361) */
 /* util/noise.cpp Noise / DNoise and CloudMedium::Density (media.h:493-517) as the media

@@ -212,6 +212,11 @@ static float Exp(float x) {
     std::memcpy(&s2, &b2, 4);
     return y * s1 * s2;
 }
+static float Tan(float x) {
+    float s, c;
+    SinCos(x, &s, &c);
+    return s / c;
+}
 static float Sinh(float x) {
     const float a = std::abs(x);
     if (a < 0x1p-12f) return x;
@@ -231,6 +236,10 @@ static inline Float CRCos(Float x) {
 static inline Float CRExp(Float x) {
     if (g_mathMode == 2) return dm::Exp(x);
     return g_mathMode ? (Float)std::exp((double)x) : std::exp(x);
+}
+static inline Float CRTan(Float x) {
+    if (g_mathMode == 2) return dm::Tan(x);
+    return g_mathMode ? (Float)std::tan((double)x) : std::tan(x);
 }
 static inline Float CRSinh(Float x) {
     if (g_mathMode == 2) return dm::Sinh(x);
@@ -4477,6 +4486,7 @@ struct OEnvLight {
             mf[v] = rows[v].integral;
         }
         marginal.Init(mf.data(), n, 0, 1);
+        if (f->env_info[4 * k + 1]) InitPortal(f, k);
     }
     static Vec Mul(const float *a, Vec v) {
         return Vec(a[0] * v.x + a[1] * v.y + a[2] * v.z, a[3] * v.x + a[4] * v.y + a[5] * v.z,
@@ -4544,6 +4554,194 @@ struct OEnvLight {
     Float PDF(Float u, Float v) const {
         int iu = std::clamp((int)(u * n), 0, n - 1), iv = std::clamp((int)(v * n), 0, n - 1);
         return rows[iv].func[iu] / marginal.integral;
+    }
+
+    // ---- PortalImageInfiniteLight (lights.h:644-744, lights.cpp:1140-1297)
+    bool portal = false;
+    Vec pc[4], fx, fy, fz;    // corners (render space), portalFrame = Frame::FromXY(p03, p01)
+    std::vector<float> prgb;  // the rectified image [n][n][3]
+    std::vector<Float> pfunc; // WindowedPiecewiseConstant2D's function
+    std::vector<double> psat; // ... and its SummedAreaTable
+    bool ImageFromRender(Vec wr, Float *u, Float *v, Float *duv_dw) const {
+        Vec w(Dot(wr, fx), Dot(wr, fy), Dot(wr, fz));
+        if (w.z <= 0) return false;
+        if (duv_dw) *duv_dw = Sqr(Pi) * (1 - Sqr(w.x)) * (1 - Sqr(w.y)) / w.z;
+        Float alpha = CRATan2(w.x, w.z), beta = CRATan2(w.y, w.z);
+        *u = Clamp((alpha + Pi / 2) / Pi, 0, 1);
+        *v = Clamp((beta + Pi / 2) / Pi, 0, 1);
+        return true;
+    }
+    Vec RenderFromImage(Float u, Float v, Float *duv_dw) const {
+        Float alpha = -Pi / 2 + u * Pi, beta = -Pi / 2 + v * Pi;
+        Float x = CRTan(alpha), y = CRTan(beta);
+        Vec w = Normalize(Vec(x, y, 1));
+        if (duv_dw) *duv_dw = Sqr(Pi) * (1 - Sqr(w.x)) * (1 - Sqr(w.y)) / w.z;
+        return fx * w.x + fy * w.y + fz * w.z;
+    }
+    bool ImageBounds(Vec p, Float b[4]) const {
+        Float u0, v0, u1, v1;
+        if (!ImageFromRender(Normalize(pc[0] - p), &u0, &v0, nullptr)) return false;
+        if (!ImageFromRender(Normalize(pc[2] - p), &u1, &v1, nullptr)) return false;
+        b[0] = std::min(u0, u1), b[1] = std::min(v0, v1), b[2] = std::max(u0, u1), b[3] = std::max(v0, v1);
+        return true;
+    }
+    Float SatInt(int x, int y) const {
+        if (x == 0 || y == 0) return 0;
+        x = std::min(x - 1, n - 1);
+        y = std::min(y - 1, n - 1);
+        return (Float)psat[(size_t)y * n + x];
+    }
+    Float SatLookup(Float x, Float y) const {
+        x *= n;
+        y *= n;
+        int x0 = (int)x, y0 = (int)y;
+        Float v00 = SatInt(x0, y0), v10 = SatInt(x0 + 1, y0), v01 = SatInt(x0, y0 + 1), v11 = SatInt(x0 + 1, y0 + 1);
+        Float dx = x - int(x), dy = y - int(y);
+        return (1 - dx) * (1 - dy) * v00 + (1 - dx) * dy * v01 + dx * (1 - dy) * v10 + dx * dy * v11;
+    }
+    Float Integral(Float x0, Float y0, Float x1, Float y1) const {
+        double s = (((double)SatLookup(x1, y1) - (double)SatLookup(x0, y1)) +
+                    ((double)SatLookup(x0, y0) - (double)SatLookup(x1, y0)));
+        return std::max<Float>(s / (n * n), 0);
+    }
+    Float FuncEval(Float u, Float v) const {
+        return pfunc[(size_t)std::min<int>(v * n, n - 1) * n + std::min<int>(u * n, n - 1)];
+    }
+    // SampleBisection (util/sampling.h:956-972), capped at 128 halvings as the product's
+    template <typename CDF>
+    Float Bisect(CDF P, Float u, Float mn, Float mx) const {
+        for (int it = 0; it < 128 && std::ceil(n * mx) - std::floor(n * mn) > 1; ++it) {
+            Float mid = (mn + mx) / 2;
+            if (P(mid) > u) mx = mid;
+            else mn = mid;
+        }
+        Float t = (u - P(mn)) / (P(mx) - P(mn));
+        return Clamp(Lerp(t, mn, mx), mn, mx);
+    }
+    bool WindowedSample(Float u0, Float u1, const Float b[4], Float *px, Float *py, Float *pdf) const {
+        if (Integral(b[0], b[1], b[2], b[3]) == 0) return false;
+        Float bInt = Integral(b[0], b[1], b[2], b[3]);
+        Float x = Bisect([&](Float t) { return Integral(b[0], b[1], t, b[3]) / bInt; }, u0, b[0], b[2]);
+        Float c0 = std::floor(x * n) / n, c1 = std::ceil(x * n) / n;
+        if (c0 == c1) c1 += 1.f / n;
+        if (Integral(c0, b[1], c1, b[3]) == 0) return false;
+        Float cInt = Integral(c0, b[1], c1, b[3]);
+        Float y = Bisect([&](Float t) { return Integral(c0, b[1], c1, t) / cInt; }, u1, b[1], b[3]);
+        *px = x;
+        *py = y;
+        *pdf = FuncEval(x, y) / bInt;
+        return true;
+    }
+    // ImageLookup: LookupNearestChannel (clamp wrap) of the rectified image, RGBIlluminantSpectrum
+    Spectrum RectLe(Float u, Float v, const Wavelengths &lambda, const float *illum, Float lightScale) const {
+        int x = std::clamp((int)(u * n), 0, n - 1), y = std::clamp((int)(v * n), 0, n - 1);
+        const float *px = prgb.data() + 3 * ((size_t)y * n + x);
+        Float c3[3] = {std::max<Float>(0, px[0]), std::max<Float>(0, px[1]), std::max<Float>(0, px[2])};
+        Float mx = std::max({c3[0], c3[1], c3[2]}), scale = 2 * mx, co[3];
+        if (scale) ORGBCoeffs(c3[0] / scale, c3[1] / scale, c3[2] / scale, co);
+        else ORGBCoeffs(0, 0, 0, co);
+        Spectrum s;
+        for (int i = 0; i < NS; ++i) s[i] = scale * Sigmoid(co[0], co[1], co[2], lambda.lambda[i]);
+        return (s * SampleDense(illum, lambda)) * lightScale;
+    }
+    // the rectification, sampling distribution and SAT (lights.cpp:1164-1211); Init runs it in
+    // the host's libm mode
+    void InitPortal(const pbrt_scene_flat *f, int k) {
+        portal = true;
+        const float *c = f->env_portal + 12 * k;
+        for (int i = 0; i < 4; ++i) pc[i] = Vec(c[3 * i], c[3 * i + 1], c[3 * i + 2]);
+        Vec p01 = Normalize(pc[1] - pc[0]), p03 = Normalize(pc[3] - pc[0]);
+        fx = p03;
+        fy = p01;
+        fz = Cross(p03, p01);
+        prgb.assign((size_t)n * n * 3, 0.f);
+        for (int y = 0; y < n; ++y)
+            for (int x = 0; x < n; ++x) {
+                Vec w = RenderFromImage((x + 0.5f) / n, (y + 0.5f) / n, nullptr);
+                w = Normalize(Mul(mi, w));
+                Float ue, ve;
+                SphereToSquare(w, &ue, &ve);
+                // Image::BilerpChannel with WrapMode::OctahedralSphere
+                Float fxp = ue * n - 0.5f, fyp = ve * n - 0.5f;
+                int xi = (int)std::floor(fxp), yi = (int)std::floor(fyp);
+                Float dx = fxp - xi, dy = fyp - yi;
+                auto get = [&](int px, int py, int ch) {
+                    if (px < 0) px = -px, py = n - 1 - py;
+                    else if (px >= n) px = 2 * n - 1 - px, py = n - 1 - py;
+                    if (py < 0) px = n - 1 - px, py = -py;
+                    else if (py >= n) px = n - 1 - px, py = 2 * n - 1 - py;
+                    if (n == 1) px = py = 0;
+                    return rgb[3 * ((size_t)py * n + px) + ch];
+                };
+                for (int ch = 0; ch < 3; ++ch)
+                    prgb[3 * ((size_t)y * n + x) + ch] =
+                        ((1 - dx) * (1 - dy) * get(xi, yi, ch) + dx * (1 - dy) * get(xi + 1, yi, ch) +
+                         (1 - dx) * dy * get(xi, yi + 1, ch) + dx * dy * get(xi + 1, yi + 1, ch));
+            }
+        pfunc.assign((size_t)n * n, 0);
+        for (int y = 0; y < n; ++y)
+            for (int x = 0; x < n; ++x) {
+                Float sum = 0;
+                for (int ch = 0; ch < 3; ++ch) sum += prgb[3 * ((size_t)y * n + x) + ch];
+                Float d;
+                (void)RenderFromImage((x + .5f) / n, (y + .5f) / n, &d);
+                pfunc[(size_t)y * n + x] = sum / 3 * d;
+            }
+        psat.assign((size_t)n * n, 0.);
+        auto S = [&](int x, int y) -> double & { return psat[(size_t)y * n + x]; };
+        auto F = [&](int x, int y) { return pfunc[(size_t)y * n + x]; };
+        S(0, 0) = F(0, 0);
+        for (int x = 1; x < n; ++x) S(x, 0) = F(x, 0) + S(x - 1, 0);
+        for (int y = 1; y < n; ++y) S(0, y) = F(0, y) + S(0, y - 1);
+        for (int y = 1; y < n; ++y)
+            for (int x = 1; x < n; ++x) S(x, y) = (F(x, y) + S(x - 1, y) + S(x, y - 1) - S(x - 1, y - 1));
+    }
+
+    // Light::SampleLi for either kind from the reference point p: direction, solid-angle pdf
+    // (mapPDF / (4 pi) for an ImageInfiniteLight) and radiance; false for {} or pdf 0
+    bool SampleLi(Vec p, Float u0, Float u1, const Wavelengths &lambda, const float *illum, Float scale, Vec *wi,
+                  Float *pdf, Spectrum *Le) const {
+        if (portal) {
+            Float b[4], uu, vv, mapPDF, duv_dw;
+            if (!ImageBounds(p, b) || !WindowedSample(u0, u1, b, &uu, &vv, &mapPDF)) return false;
+            *wi = RenderFromImage(uu, vv, &duv_dw);
+            if (duv_dw == 0) return false;
+            *pdf = mapPDF / duv_dw;
+            *Le = RectLe(uu, vv, lambda, illum, scale);
+            return *pdf != 0;
+        }
+        Float eu, ev, emap;
+        if (!Sample(u0, u1, &eu, &ev, &emap)) return false;
+        *wi = Mul(m, SquareToSphere(eu, ev));
+        *pdf = emap / (4 * Pi);
+        *Le = this->Le(eu, ev, lambda, illum, scale);
+        return true;
+    }
+    // Light::Le(ray) of an escaped ray (origin o, direction d)
+    Spectrum LeRay(Vec o, Vec d, const Wavelengths &lambda, const float *illum, Float scale) const {
+        if (portal) {
+            Float u, v, b[4];
+            if (!ImageFromRender(Normalize(d), &u, &v, nullptr) || !ImageBounds(o, b) || !(u >= b[0] && u <= b[2] && v >= b[1] && v <= b[3]))
+                return Spectrum(0.f);
+            return RectLe(u, v, lambda, illum, scale);
+        }
+        Float u, v;
+        SphereToSquare(Normalize(Mul(mi, d)), &u, &v);
+        return Le(u, v, lambda, illum, scale);
+    }
+    // Light::PDF_Li(ctx, w, allowIncompletePDF) from the previous vertex p
+    Float PdfLi(Vec p, Vec w) const {
+        if (portal) {
+            Float u, v, duv_dw, b[4];
+            if (!ImageFromRender(w, &u, &v, &duv_dw) || duv_dw == 0) return 0;
+            if (!ImageBounds(p, b)) return 0;
+            Float fi = Integral(b[0], b[1], b[2], b[3]);
+            if (fi == 0) return 0;
+            return (FuncEval(u, v) / fi) / duv_dw;
+        }
+        Float u, v;
+        SphereToSquare(Mul(mi, w), &u, &v);
+        return PDF(u, v) / (4 * Pi);
     }
 };
 
@@ -5930,18 +6128,19 @@ struct Renderer {
                     DeltaSample ds;
                     const bool sampledL = lights.Sample(pS, Vec(0, 0, 0), dUc, &li, &lpmf);
                     const OEnvLight *E = sampledL ? EnvOf(li) : nullptr;
-                    Float eu, ev, emap;
                     if (E) {
-                        // ImageInfiniteLight::SampleLi from the medium point (media.cpp:280-305)
-                        if (E->Sample(dU0, dU1, &eu, &ev, &emap)) {
-                            const int k = li - f->n_area_lights - f->n_point_spot;
-                            Vec wi = OEnvLight::Mul(E->m, OEnvLight::SquareToSphere(eu, ev));
+                        // ImageInfiniteLight / PortalImageInfiniteLight::SampleLi from the medium
+                        // point (media.cpp:280-305)
+                        const int k = li - f->n_area_lights - f->n_point_spot;
+                        Vec wi;
+                        Float epdf;
+                        Spectrum Le;
+                        if (E->SampleLi(pS, dU0, dU1, lambda, f->dense_spectra + 311 * f->inf_spectrum[k], f->inf_scale[k],
+                                        &wi, &epdf, &Le)) {
                             Vec lp = pS + wi * (2 * f->scene_radius);
-                            Spectrum Le =
-                                E->Le(eu, ev, lambda, f->dense_spectra + 311 * f->inf_spectrum[k], f->inf_scale[k]);
                             if (Le) {
                                 Float ph = HenyeyGreenstein(Dot(wo, wi), g);
-                                Float lightPDF = emap / (4 * Pi) * lpmf;
+                                Float lightPDF = epdf * lpmf;
                                 Spectrum ru = r_u * ph, rl = r_u * lightPDF;
                                 shadow(pS, lp - pS, medium, beta * ph * Le, ru, rl);
                             }
@@ -5997,9 +6196,7 @@ struct Renderer {
                     const float *illum = f->dense_spectra + 311 * f->inf_spectrum[k];
                     Spectrum Le;
                     if (E) {
-                        Float u, v;
-                        OEnvLight::SphereToSquare(Normalize(OEnvLight::Mul(E->mi, rd)), &u, &v);
-                        Le = E->Le(u, v, lambda, illum, f->inf_scale[k]);
+                        Le = E->LeRay(ro, rd, lambda, illum, f->inf_scale[k]);
                     } else {
                         Le = SampleDense(illum, lambda) * f->inf_scale[k];
                     }
@@ -6007,11 +6204,7 @@ struct Renderer {
                     if (depth == 0 || specularBounce) L = L + beta * Le / r_u.Average();
                     else {
                         Float pdfLi = 0;
-                        if (E) {
-                            Float u, v;
-                            OEnvLight::SphereToSquare(OEnvLight::Mul(E->mi, rd), &u, &v);
-                            pdfLi = E->PDF(u, v) / (4 * Pi);
-                        }
+                        if (E) pdfLi = E->PdfLi(prevP, rd);
                         Spectrum rl = r_l * lights.PMF(prevP, prevNs, gi) * pdfLi;
                         L = L + beta * Le / (r_u + rl).Average();
                     }
@@ -6093,20 +6286,22 @@ struct Renderer {
                 DeltaSample ds;
                 const bool sampledL = lights.Sample(cp, si.ns, dUc, &li, &lpmf);
                 const OEnvLight *E = sampledL ? EnvOf(li) : nullptr;
-                Float eu, ev, emap;
                 if (E) {
-                    // ImageInfiniteLight::SampleLi(allowIncompletePDF) (lights.h:594-618): a light
-                    // point 2 sceneRadius away without error bounds or normal
-                    if (E->Sample(dU0, dU1, &eu, &ev, &emap)) {
-                        const int k = li - f->n_area_lights - f->n_point_spot;
-                        Vec wi = OEnvLight::Mul(E->m, OEnvLight::SquareToSphere(eu, ev));
+                    // ImageInfiniteLight::SampleLi(allowIncompletePDF) (lights.h:594-618), or the
+                    // portal light's (lights.cpp:1257-1281): a light point 2 sceneRadius away
+                    // without error bounds or normal
+                    const int k = li - f->n_area_lights - f->n_point_spot;
+                    Vec wi;
+                    Float epdf;
+                    Spectrum Le;
+                    if (E->SampleLi(cp, dU0, dU1, lambda, f->dense_spectra + 311 * f->inf_spectrum[k], f->inf_scale[k], &wi,
+                                    &epdf, &Le)) {
                         Vec lp = cp + wi * (2 * f->scene_radius);
-                        Spectrum Le = E->Le(eu, ev, lambda, f->dense_spectra + 311 * f->inf_spectrum[k], f->inf_scale[k]);
                         Vec wiL = toLocal(wi);
                         Spectrum fv = woL.z == 0 ? Spectrum(0.f) : layered ? lay.f(woL, wiL, true) : bx.f(woL, wiL);
                         if (Le && fv) {
                             Spectrum b2 = oldBeta * fv * AbsDotN(si.ns, wi);
-                            Float lightPDF = emap / (4 * Pi) * lpmf;
+                            Float lightPDF = epdf * lpmf;
                             Float bsdfPDF = woL.z == 0 ? 0 : layered ? lay.PDF(woL, wiL, true) : bx.PDF(woL, wiL);
                             Spectrum ru = r_u * bsdfPDF, rl = r_u * lightPDF;
                             Vec pf = OffsetRayOrigin(si.p, si.err, si.n, lp - si.p);
@@ -6242,17 +6437,18 @@ struct Renderer {
                 DeltaSample ds;
                 const bool sampledL = woS.z != 0 && lights.Sample(ex.p, ex.ns, dUc, &li, &lpmf);
                 const OEnvLight *E = sampledL ? EnvOf(li) : nullptr;
-                Float eu, ev, emap;
                 if (E) {
-                    if (E->Sample(dU0, dU1, &eu, &ev, &emap)) {
-                        const int kk = li - f->n_area_lights - f->n_point_spot;
-                        Vec wi = OEnvLight::Mul(E->m, OEnvLight::SquareToSphere(eu, ev));
+                    const int kk = li - f->n_area_lights - f->n_point_spot;
+                    Vec wi;
+                    Float epdf;
+                    Spectrum Le;
+                    if (E->SampleLi(ex.p, dU0, dU1, lambda, f->dense_spectra + 311 * f->inf_spectrum[kk], f->inf_scale[kk],
+                                    &wi, &epdf, &Le)) {
                         Vec lp = ex.p + wi * (2 * f->scene_radius);
-                        Spectrum Le = E->Le(eu, ev, lambda, f->dense_spectra + 311 * f->inf_spectrum[kk], f->inf_scale[kk]);
                         const Float fv = nfF(toL(wi));
                         if (Le && fv != 0) {
                             Spectrum b2 = betap * fv * AbsDotN(ex.ns, wi);
-                            Float lightPDF = emap / (4 * Pi) * lpmf;
+                            Float lightPDF = epdf * lpmf;
                             Spectrum ru = ru2 * nfPdf(toL(wi)), rl = ru2 * lightPDF;
                             Vec pf = OffsetRayOrigin(ex.p, ex.err, ex.n, lp - ex.p);
                             shadow(pf, lp - pf, DotN(ex.n, lp - pf) > 0 ? mOut : mIn, b2 * Le, ru, rl);
@@ -6360,11 +6556,8 @@ struct Renderer {
                     Spectrum Le;
                     Float pdfLi = 0;
                     if (E) {
-                        Float u, v;
-                        OEnvLight::SphereToSquare(Normalize(OEnvLight::Mul(E->mi, rd)), &u, &v);
-                        Le = E->Le(u, v, lambda, illum, f->inf_scale[k]);
-                        OEnvLight::SphereToSquare(OEnvLight::Mul(E->mi, rd), &u, &v);
-                        pdfLi = E->PDF(u, v) / (4 * Pi);
+                        Le = E->LeRay(ro, rd, lambda, illum, f->inf_scale[k]);
+                        pdfLi = E->PdfLi(prevP, rd);
                     } else {
                         Le = SampleDense(illum, lambda) * f->inf_scale[k];
                     }
@@ -6438,13 +6631,10 @@ struct Renderer {
                     DeltaSample ds;
                     const OEnvLight *E = EnvOf(li);
                     if (E) {
-                        Float eu, ev, emap;
-                        if (E->Sample(u0, u1, &eu, &ev, &emap)) {
-                            const int k = li - f->n_area_lights - f->n_point_spot;
-                            wi = OEnvLight::Mul(E->m, OEnvLight::SquareToSphere(eu, ev));
+                        const int k = li - f->n_area_lights - f->n_point_spot;
+                        if (E->SampleLi(cp, u0, u1, lambda, f->dense_spectra + 311 * f->inf_spectrum[k], f->inf_scale[k], &wi,
+                                        &pdf, &Le)) {
                             pt = cp + wi * (2 * f->scene_radius);
-                            Le = E->Le(eu, ev, lambda, f->dense_spectra + 311 * f->inf_spectrum[k], f->inf_scale[k]);
-                            pdf = emap / (4 * Pi);
                             pf = OffsetRayOrigin(si.p, si.err, si.n, pt - si.p);
                         }
                     } else if (li >= f->n_area_lights) {
@@ -6928,6 +7118,60 @@ int oracle_env_eval(const pbrt_scene_flat *flat, int env, const float *dirs, con
         o[13] = E.PDF(su, sv);                // PiecewiseConstant2D::PDF at the sample
         o[14] = E.PDF(u[2 * i], u[2 * i + 1]);  // ... and at u taken as a point of [0,1]^2
         o[15] = 0;
+    }
+    return 0;
+}
+// PortalImageInfiniteLight queries laid out as pbrt_debug_portal_eval's: q[8] = {p, d, u0, u1}
+// -> out[16] = {Le(ray p, d) at 400/500/600/700 nm (light scale 1, illuminant 1), PDF_Li(p, d),
+// SampleLi ok, wi, pdf, sample Le at the four wavelengths, ImageBounds ok, 0}; img (optional):
+// the rectified image [res][res][3] then the distribution's function [res][res]
+int oracle_portal_eval(const pbrt_scene_flat *flat, int env, const float *q, int n, float *out, float *img) {
+    if (!g_rgbTable) return -2;
+    if (env < 0 || env >= flat->n_env || !flat->env_portal || !flat->env_info[4 * env + 1]) return -1;
+    OEnvLight E;
+    {
+        const int mode = g_mathMode;
+        if (mode == 2) g_mathMode = 0;  // construction is host work (libm)
+        E.Init(flat, env);
+        g_mathMode = mode;
+    }
+    static const float kLam[4] = {400.f, 500.f, 600.f, 700.f};
+    float one[311];
+    std::fill(one, one + 311, 1.f);
+    auto at4 = [&](auto &&fn, float *o) {
+        for (int k = 0; k < 4; ++k) {
+            Wavelengths L = Wavelengths::SampleUniform(0.f);
+            for (int j = 0; j < NS; ++j) L.lambda[j] = kLam[k];
+            o[k] = fn(L)[0];
+        }
+    };
+    for (int i = 0; i < n; ++i) {
+        const float *x = q + 8 * (size_t)i;
+        float *o = out + 16 * (size_t)i;
+        std::fill(o, o + 16, 0.f);
+        const Vec p(x[0], x[1], x[2]), d(x[3], x[4], x[5]);
+        at4([&](const Wavelengths &L) { return E.LeRay(p, d, L, one, 1.f); }, o);
+        o[4] = E.PdfLi(p, d);
+        Vec wi;
+        Float pdf;
+        Spectrum Le;
+        Wavelengths L0 = Wavelengths::SampleUniform(0.f);
+        if (E.SampleLi(p, x[6], x[7], L0, one, 1.f, &wi, &pdf, &Le)) {
+            o[5] = 1;
+            o[6] = wi.x, o[7] = wi.y, o[8] = wi.z;
+            o[9] = pdf;
+            Float b[4], uu, vv, mp;
+            E.ImageBounds(p, b);
+            E.WindowedSample(x[6], x[7], b, &uu, &vv, &mp);
+            at4([&](const Wavelengths &L) { return E.RectLe(uu, vv, L, one, 1.f); }, o + 10);
+        }
+        Float b[4];
+        o[14] = E.ImageBounds(p, b) ? 1.f : 0.f;
+    }
+    if (img) {
+        const size_t np = (size_t)E.n * E.n;
+        std::copy(E.prgb.begin(), E.prgb.end(), img);
+        for (size_t k = 0; k < np; ++k) img[3 * np + k] = E.pfunc[k];
     }
     return 0;
 }

@@ -49,6 +49,7 @@ def lib():
         _lib.oracle_bxdf.argtypes = [ctypes.c_int] + [vp] * 7
         _lib.oracle_layered.argtypes = [vp] * 8
         _lib.oracle_hair_eval.argtypes = [vp, ctypes.c_int, vp]
+        _lib.oracle_portal_eval.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, vp, vp]
         _lib.oracle_triangle_shading.argtypes = [vp] * 3 + [ctypes.c_int] + [vp] * 3
         _lib.oracle_render.argtypes = [vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, vp]
@@ -401,6 +402,23 @@ def catmull_rom(op, nodes1, nodes2, values, cdf, x):
     lib().oracle_catmull_rom(op, a[0].ctypes.data, len(a[0]), a[1].ctypes.data, len(a[1]), a[2].ctypes.data,
                              a[3].ctypes.data, a[4].ctypes.data, n, out.ctypes.data)
     return out.reshape(-1, 6) if op == 0 else out
+
+
+def portal_eval(scene, env, queries, res=0):
+    """The oracle's PortalImageInfiniteLight on [n][8] queries {p, d, u0, u1} -> [n][16] (see
+    oracle_portal_eval); with res > 0 also its rectified image [res][res][3] and function."""
+    f = scene.flat()
+    q = np.ascontiguousarray(queries, np.float32).reshape(-1, 8)
+    out = np.zeros((len(q), 16), np.float32)
+    img = np.zeros(res * res * 4, np.float32) if res else None
+    rc = lib().oracle_portal_eval(ctypes.byref(f), env, q.ctypes.data, len(q), out.ctypes.data,
+                                  img.ctypes.data if img is not None else None)
+    if rc != 0:
+        raise RuntimeError(f"oracle_portal_eval failed ({rc})")
+    if img is None:
+        return out
+    np_ = res * res
+    return out, img[:3 * np_].reshape(res, res, 3), img[3 * np_:].reshape(res, res)
 
 
 def hair_eval(queries):

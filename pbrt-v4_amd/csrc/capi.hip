@@ -290,8 +290,9 @@ static std::vector<EnvCoef> BuildEnvCoefs(const EnvLightDesc &e) {
     T.rgbCoeffs = tab.data() + 64;
     const size_t np = (size_t)e.res * e.res;
     std::vector<EnvCoef> out(np);
+    const std::vector<float> &rgb = e.portal ? e.rect : e.rgb;  // a portal light's rectified image
     for (size_t p = 0; p < np; ++p) {
-        const float r = std::max(0.f, e.rgb[3 * p]), g = std::max(0.f, e.rgb[3 * p + 1]), b = std::max(0.f, e.rgb[3 * p + 2]);
+        const float r = std::max(0.f, rgb[3 * p]), g = std::max(0.f, rgb[3 * p + 1]), b = std::max(0.f, rgb[3 * p + 2]);
         const float m = std::max(r, std::max(g, b));
         const float scale = 2 * m;
         float c[3];
@@ -315,7 +316,7 @@ struct pbrt_scene {
     std::vector<int32_t> lightImage;
     std::vector<int32_t> infImage, envInfo, shapeInfo, primAlpha;
     std::vector<float> shapeParams, shapeNormals;
-    std::vector<float> envXform, envRgb;
+    std::vector<float> envXform, envRgb, envPortal;
     std::vector<uint64_t> envOffset;
     TexTables tex;
     void Flatten() {
@@ -339,10 +340,12 @@ struct pbrt_scene {
         }
         envInfo.clear();
         envXform.clear();
+        envPortal.clear();
         envRgb.clear();
         envOffset.clear();
         for (const EnvLightDesc &e : s.envLights) {
-            envInfo.insert(envInfo.end(), {e.res, 0, 0, 0});
+            envInfo.insert(envInfo.end(), {e.res, e.portal ? 1 : 0, 0, 0});
+            for (int k = 0; k < 4; ++k) envPortal.insert(envPortal.end(), e.portalP[k], e.portalP[k] + 3);
             envXform.insert(envXform.end(), e.renderFromLight, e.renderFromLight + 9);
             envXform.insert(envXform.end(), e.lightFromRender, e.lightFromRender + 9);
             envOffset.push_back(envRgb.size() / 3);
@@ -536,6 +539,7 @@ struct pbrt_context {
     DevBuf<EnvCoef> envCoef;
     DevBuf<float> envDist;
     DevBuf<DeviceEnvLight> envLights;
+    DevBuf<float> portalTab;  // portal lights: SummedAreaTable values then function, per light
     DevBuf<int> queueHoles;       // VolState::holes
     DevBuf<int> matMix, hitMat;   // mix materials: {m0, m1, amount program} and resolved materials
     bool hasMix = false;
@@ -939,6 +943,17 @@ static void BuildDevice(pbrt_context *c) {
         }
         c->envCoef.Upload(coefs);
         c->envDist.Upload(dist);
+        // portal lights' windowed distributions: SummedAreaTable values and function
+        std::vector<float> ptab;
+        std::vector<size_t> poff;
+        for (const EnvLightDesc &e : s.envLights) {
+            poff.push_back(ptab.size());
+            if (!e.portal) continue;
+            ptab.insert(ptab.end(), e.portalSat.begin(), e.portalSat.end());
+            ptab.insert(ptab.end(), e.portalFunc.begin(), e.portalFunc.end());
+        }
+        if (ptab.empty()) ptab.push_back(0.f);
+        c->portalTab.Upload(ptab);
         for (size_t k = 0; k < s.envLights.size(); ++k) {
             const EnvLightDesc &e = s.envLights[k];
             DeviceEnvLight d{};
@@ -947,6 +962,14 @@ static void BuildDevice(pbrt_context *c) {
             d.res = e.res;
             d.coef = c->envCoef.p + offs[k].first;
             d.dist = FilterTableView{e.res, e.res, c->envDist.p + offs[k].second};
+            if (e.portal) {
+                d.portal = 1;
+                std::memcpy(d.pf, e.portalFrame, sizeof(d.pf));
+                std::memcpy(d.pc0, e.portalP[0], sizeof(d.pc0));
+                std::memcpy(d.pc2, e.portalP[2], sizeof(d.pc2));
+                d.sat = c->portalTab.p + poff[k];
+                d.func = d.sat + (size_t)e.res * e.res;
+            }
             els.push_back(d);
         }
         c->envLights.Upload(els);
@@ -1103,6 +1126,9 @@ static void BuildDevice(pbrt_context *c) {
     // subsurface scattering: its r_u becomes spectral (subsurface.cpp:61), so the volumetric
     // kernels (spectral r_u / r_l records) render it
     c->volumetric = c->volumetric || !s.sss.empty();
+    // portal lights: Le and PDF_Li depend on the ray origin and the previous vertex, which the
+    // volumetric records carry
+    c->volumetric = c->volumetric || std::any_of(s.envLights.begin(), s.envLights.end(), [](const EnvLightDesc &e) { return e.portal; });
     S.media.cameraMedium = s.cameraMedium;
     S.media.allGrey = 1;
     for (size_t m = 0; m < s.media.size(); ++m) {
@@ -2102,6 +2128,7 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
     f->sss_tables = s.sss.empty() ? nullptr : scene->sssTables.data();
     f->vertex_s = s.vertS.empty() ? nullptr : &s.vertS[0].x;
     f->n_vertex_s = (int)s.vertS.size();
+    f->env_portal = scene->envPortal.empty() ? nullptr : scene->envPortal.data();
     f->dims_per_depth = s.sss.empty() ? 7 : 10;
     f->material_params = scene->matParams.data();
     f->material_layer = scene->matLayer.data();
@@ -2606,6 +2633,56 @@ int pbrt_debug_texture_eval(const pbrt_scene *scene, int material, int slot, con
         }
         for (int i = 0; i < n; ++i)
             out[4 + i] = pg.simple ? SigmoidPolynomial(R[0], R[1], R[2], lambda[i]) : TexPhase2(T, pg, R, lambda[i]);
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_debug_portal_eval(const pbrt_scene *scene, int env, const float *q8, int n, float *out16, float *img) {
+    try {
+        if (!scene || !q8 || !out16) return Fail("null argument");
+        const SceneDesc &s = scene->desc;
+        if (env < 0 || env >= (int)s.envLights.size() || !s.envLights[env].portal) return Fail("not a portal light index");
+        const EnvLightDesc &e = s.envLights[env];
+        const std::vector<EnvCoef> coef = BuildEnvCoefs(e);
+        DeviceEnvLight E{};
+        std::memcpy(E.m, e.renderFromLight, sizeof(E.m));
+        std::memcpy(E.mi, e.lightFromRender, sizeof(E.mi));
+        E.res = e.res;
+        E.portal = 1;
+        E.coef = coef.data();
+        std::memcpy(E.pf, e.portalFrame, sizeof(E.pf));
+        std::memcpy(E.pc0, e.portalP[0], sizeof(E.pc0));
+        std::memcpy(E.pc2, e.portalP[2], sizeof(E.pc2));
+        E.sat = e.portalSat.data();
+        E.func = e.portalFunc.data();
+        static const float kLam[4] = {400.f, 500.f, 600.f, 700.f};
+        for (int i = 0; i < n; ++i) {
+            const float *x = q8 + 8 * (size_t)i;
+            float *o = out16 + 16 * (size_t)i;
+            std::fill(o, o + 16, 0.f);
+            const V3 p(x[0], x[1], x[2]), d(x[3], x[4], x[5]);
+            const EnvCoef c = PortalLeCoef(E, p, d);
+            for (int k = 0; k < 4; ++k) o[k] = EnvLe(c, 1.f, 1.f, kLam[k]);
+            o[4] = PortalPDFLi(E, p, d);
+            V3 wi;
+            float pdf;
+            EnvCoef sc;
+            if (PortalSampleLi(E, p, x[6], x[7], &wi, &pdf, &sc)) {
+                o[5] = 1;
+                o[6] = wi.x, o[7] = wi.y, o[8] = wi.z;
+                o[9] = pdf;
+                for (int k = 0; k < 4; ++k) o[10 + k] = EnvLe(sc, 1.f, 1.f, kLam[k]);
+            }
+            float b[4];
+            o[14] = PortalImageBounds(E, p, b) ? 1.f : 0.f;
+        }
+        if (img) {
+            const size_t np = (size_t)e.res * e.res;
+            std::copy(e.rect.begin(), e.rect.end(), img);
+            std::copy(e.portalFunc.begin(), e.portalFunc.end(), img + 3 * np);
+        }
         return 0;
     } catch (const std::exception &e) {
         return Fail(e.what());

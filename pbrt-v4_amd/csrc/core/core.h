@@ -93,6 +93,7 @@ PHD float ATan2f(float y, float x) { return detm::ATan2(y, x); }
 PHD float Logf(float x) { return detm::Log(x); }
 PHD float Expf(float x) { return detm::Exp(x); }
 PHD float Sinhf(float x) { return detm::Sinh(x); }
+PHD float Tanf(float x) { return detm::Tan(x); }
 #else
 PHD float Sinf(float x) { return std::sin(x); }
 PHD float Cosf(float x) { return std::cos(x); }
@@ -106,6 +107,7 @@ PHD float ATan2f(float y, float x) { return std::atan2(y, x); }
 PHD float Logf(float x) { return std::log(x); }
 PHD float Expf(float x) { return std::exp(x); }
 PHD float Sinhf(float x) { return std::sinh(x); }
+PHD float Tanf(float x) { return std::tan(x); }
 #endif
 
 PHD float Sqr(float v) { return v * v; }
@@ -1968,9 +1970,14 @@ struct alignas(16) EnvCoef {
 };
 struct DeviceEnvLight {
     float m[9], mi[9];
-    int res, pad;
+    int res, portal;  // portal != 0: a PortalImageInfiniteLight (coef: the rectified image's)
     const EnvCoef *coef;
-    FilterTableView dist;
+    FilterTableView dist;  // ImageInfiniteLight's compensated distribution
+    // PortalImageInfiniteLight: portalFrame's rows x, y, z (Frame::FromXY(p03, p01)), portal[0]
+    // and portal[2] in render space, the windowed distribution's summed-area table (Float
+    // values of its double sums, as SummedAreaTable::LookupInt returns them) and function
+    float pf[9], pc0[3], pc2[3];
+    const float *sat, *func;
 };
 PHD V3 MulM3(const float *m, V3 v) {
     return V3(m[0] * v.x + m[1] * v.y + m[2] * v.z, m[3] * v.x + m[4] * v.y + m[5] * v.z,
@@ -2020,6 +2027,143 @@ PHD float EnvPDF(const DeviceEnvLight &E, float u, float v) {
 // scale * ((c.w * rsp(lambda)) * illuminant(lambda))
 PHD float EnvLe(const EnvCoef &c, float lightScale, float illum, float lambda) {
     return lightScale * ((c.s * SigmoidPolynomial(c.c0, c.c1, c.c2, lambda)) * illum);
+}
+
+// ---------------------------------------------------------------- portal image infinite lights
+// PortalImageInfiniteLight (lights.h:644-744, lights.cpp:1140-1297): the environment map
+// rectified over the portal frame's angles (alpha, beta) = (atan2(x, z), atan2(y, z)), sampled
+// with a WindowedPiecewiseConstant2D (util/sampling.h:830-989) restricted to the portal's image
+// bounds as seen from the reference point.
+PHD bool PortalImageFromRender(const DeviceEnvLight &E, V3 wr, float *u, float *v, float *duv_dw) {
+    const V3 w(Dot(wr, V3(E.pf[0], E.pf[1], E.pf[2])), Dot(wr, V3(E.pf[3], E.pf[4], E.pf[5])),
+               Dot(wr, V3(E.pf[6], E.pf[7], E.pf[8])));
+    if (w.z <= 0) return false;
+    if (duv_dw) *duv_dw = Sqr(kPi) * (1 - Sqr(w.x)) * (1 - Sqr(w.y)) / w.z;
+    const float alpha = ATan2f(w.x, w.z), beta = ATan2f(w.y, w.z);
+    *u = Clampf((alpha + kPi / 2) / kPi, 0, 1);
+    *v = Clampf((beta + kPi / 2) / kPi, 0, 1);
+    return true;
+}
+PHD V3 PortalRenderFromImage(const float *pf, float u, float v, float *duv_dw) {
+    const float alpha = -kPi / 2 + u * kPi, beta = -kPi / 2 + v * kPi;
+    const float x = Tanf(alpha), y = Tanf(beta);
+    const V3 w = Normalize(V3(x, y, 1));
+    if (duv_dw) *duv_dw = Sqr(kPi) * (1 - Sqr(w.x)) * (1 - Sqr(w.y)) / w.z;
+    return V3(pf[0], pf[1], pf[2]) * w.x + V3(pf[3], pf[4], pf[5]) * w.y + V3(pf[6], pf[7], pf[8]) * w.z;
+}
+// ImageBounds(p): the image points of portal[0] and portal[2] seen from p, as Bounds2f
+// {pMin.x, pMin.y, pMax.x, pMax.y}
+PHD bool PortalImageBounds(const DeviceEnvLight &E, V3 p, float b[4]) {
+    float u0, v0, u1, v1;
+    if (!PortalImageFromRender(E, Normalize(V3(E.pc0[0], E.pc0[1], E.pc0[2]) - p), &u0, &v0, nullptr)) return false;
+    if (!PortalImageFromRender(E, Normalize(V3(E.pc2[0], E.pc2[1], E.pc2[2]) - p), &u1, &v1, nullptr)) return false;
+    b[0] = u1 < u0 ? u1 : u0;
+    b[1] = v1 < v0 ? v1 : v0;
+    b[2] = u0 < u1 ? u1 : u0;
+    b[3] = v0 < v1 ? v1 : v0;
+    return true;
+}
+// SummedAreaTable::LookupInt / Lookup / Integral (util/sampling.h:851-888)
+PHD float SatLookupInt(const DeviceEnvLight &E, int x, int y) {
+    if (x == 0 || y == 0) return 0;
+    x = x - 1 < E.res - 1 ? x - 1 : E.res - 1;
+    y = y - 1 < E.res - 1 ? y - 1 : E.res - 1;
+    return E.sat[(size_t)y * E.res + x];
+}
+PHD float SatLookup(const DeviceEnvLight &E, float x, float y) {
+    x *= E.res;
+    y *= E.res;
+    const int x0 = (int)x, y0 = (int)y;
+    const float v00 = SatLookupInt(E, x0, y0), v10 = SatLookupInt(E, x0 + 1, y0);
+    const float v01 = SatLookupInt(E, x0, y0 + 1), v11 = SatLookupInt(E, x0 + 1, y0 + 1);
+    const float dx = x - (float)(int)x, dy = y - (float)(int)y;
+    return (1 - dx) * (1 - dy) * v00 + (1 - dx) * dy * v01 + dx * (1 - dy) * v10 + dx * dy * v11;
+}
+PHD float SatIntegral(const DeviceEnvLight &E, float x0, float y0, float x1, float y1) {
+    const double s = (((double)SatLookup(E, x1, y1) - (double)SatLookup(E, x0, y1)) +
+                      ((double)SatLookup(E, x0, y0) - (double)SatLookup(E, x1, y0)));
+    const float r = (float)(s / (double)(E.res * E.res));
+    return r < 0 ? 0.f : r;
+}
+// WindowedPiecewiseConstant2D::Eval
+PHD float PortalFuncAt(const DeviceEnvLight &E, float u, float v) {
+    int x = (int)(u * E.res), y = (int)(v * E.res);
+    x = x < E.res - 1 ? x : E.res - 1;
+    y = y < E.res - 1 ? y : E.res - 1;
+    return E.func[(size_t)y * E.res + x];
+}
+// SampleBisection over the windowed marginal (Y false: x in [b0, b2] with y over [b1, b3]) or
+// conditional (Y true: y with x over the column bounds cx0, cx1); the loop is capped (pbrt has no
+// cap; it ends within ~log2(n) halvings)
+template <bool Y>
+PHD float PortalBisect(const DeviceEnvLight &E, const float b[4], float cx0, float cx1, float norm, float u, float mn,
+                       float mx) {
+    auto P = [&](float t) {
+        return (Y ? SatIntegral(E, cx0, b[1], cx1, t) : SatIntegral(E, b[0], b[1], t, b[3])) / norm;
+    };
+    const int n = E.res;
+    for (int it = 0; it < 128 && std::ceil(n * mx) - std::floor(n * mn) > 1; ++it) {
+        const float mid = (mn + mx) / 2;
+        if (P(mid) > u) mx = mid;
+        else mn = mid;
+    }
+    const float t = (u - P(mn)) / (P(mx) - P(mn));
+    return Clampf((1 - t) * mn + t * mx, mn, mx);
+}
+// WindowedPiecewiseConstant2D::Sample(u, b, &pdf); false for {}
+PHD bool PortalWindowedSample(const DeviceEnvLight &E, float u0, float u1, const float b[4], float *px, float *py,
+                              float *pdf) {
+    const float bInt = SatIntegral(E, b[0], b[1], b[2], b[3]);
+    if (bInt == 0) return false;
+    const float x = PortalBisect<false>(E, b, 0, 0, bInt, u0, b[0], b[2]);
+    const int nx = E.res;
+    const float cx0 = std::floor(x * nx) / nx;
+    float cx1 = std::ceil(x * nx) / nx;
+    if (cx0 == cx1) cx1 += 1.f / nx;
+    const float cInt = SatIntegral(E, cx0, b[1], cx1, b[3]);
+    if (cInt == 0) return false;
+    const float y = PortalBisect<true>(E, b, cx0, cx1, cInt, u1, b[1], b[3]);
+    *px = x;
+    *py = y;
+    *pdf = PortalFuncAt(E, x, y) / bInt;
+    return true;
+}
+// ImageLookup's pixel: Image::LookupNearestChannel(uv, c) with the default clamp wrap
+PHD EnvCoef PortalCoefAt(const DeviceEnvLight &E, float u, float v) {
+    int x = (int)(u * E.res), y = (int)(v * E.res);
+    x = x < 0 ? 0 : (x > E.res - 1 ? E.res - 1 : x);
+    y = y < 0 ? 0 : (y > E.res - 1 ? E.res - 1 : y);
+    return E.coef[(size_t)y * E.res + x];
+}
+// PortalImageInfiniteLight::SampleLi (lights.cpp:1257-1281); false for {} (or pdf 0)
+PHD bool PortalSampleLi(const DeviceEnvLight &E, V3 p, float u0, float u1, V3 *wi, float *pdf, EnvCoef *ec) {
+    float b[4];
+    if (!PortalImageBounds(E, p, b)) return false;
+    float uu, vv, mapPDF;
+    if (!PortalWindowedSample(E, u0, u1, b, &uu, &vv, &mapPDF)) return false;
+    float duv_dw;
+    *wi = PortalRenderFromImage(E.pf, uu, vv, &duv_dw);
+    if (duv_dw == 0) return false;
+    *pdf = mapPDF / duv_dw;
+    *ec = PortalCoefAt(E, uu, vv);
+    return *pdf != 0;
+}
+// PortalImageInfiniteLight::Le(ray) (lights.cpp:1239-1246): zero coefficients outside the
+// portal's bounds as seen from the ray origin
+PHD EnvCoef PortalLeCoef(const DeviceEnvLight &E, V3 o, V3 d) {
+    float u, v, b[4];
+    if (!PortalImageFromRender(E, Normalize(d), &u, &v, nullptr) || !PortalImageBounds(E, o, b) || !(u >= b[0] && u <= b[2] && v >= b[1] && v <= b[3]))
+        return EnvCoef{0, 0, 0, 0};
+    return PortalCoefAt(E, u, v);
+}
+// PortalImageInfiniteLight::PDF_Li(ctx, w) (lights.cpp:1283-1297) from the reference point p
+PHD float PortalPDFLi(const DeviceEnvLight &E, V3 p, V3 w) {
+    float u, v, duv_dw, b[4];
+    if (!PortalImageFromRender(E, w, &u, &v, &duv_dw) || duv_dw == 0) return 0;
+    if (!PortalImageBounds(E, p, b)) return 0;
+    const float fi = SatIntegral(E, b[0], b[1], b[2], b[3]);
+    if (fi == 0) return 0;
+    return (PortalFuncAt(E, u, v) / fi) / duv_dw;
 }
 
 // ---------------------------------------------------------------- cloud medium

@@ -230,6 +230,13 @@ PHD float Exp(float x) {
     const int k = (int)n, k1 = k / 2, k2 = k - k1;
     return y * FromBits((uint32_t)(k1 + 127) << 23) * FromBits((uint32_t)(k2 + 127) << 23);
 }
+// tan x = sin x / cos x from one shared argument reduction (within a few ulp of tanf away from
+// the poles; the portal light evaluates it on (-pi/2, pi/2))
+PHD float Tan(float x) {
+    float s, c;
+    SinCos(x, &s, &c);
+    return s / c;
+}
 // sinh x = (e^|x| - e^-|x|) / 2 with x's sign; x itself below 2^-12
 PHD float Sinh(float x) {
     const float a = std::fabs(x);

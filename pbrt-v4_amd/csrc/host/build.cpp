@@ -673,3 +673,84 @@ void BuildFilterTable(SceneDesc &s) {
 }
 
 }  // namespace pbrt_amd
+
+namespace pbrt_amd {
+// Image::BilerpChannel(uv, c, WrapMode::OctahedralSphere) (util/image.h:279-292, 96-125) of an
+// environment map's linear RGB
+static float BilerpOctahedral(const EnvLightDesc &e, float u, float v, int c) {
+    const int n = e.res;
+    const float x = u * n - 0.5f, y = v * n - 0.5f;
+    const int xi = (int)std::floor(x), yi = (int)std::floor(y);
+    const float dx = x - xi, dy = y - yi;
+    auto get = [&](int px, int py) {
+        if (px < 0) {
+            px = -px;
+            py = n - 1 - py;
+        } else if (px >= n) {
+            px = 2 * n - 1 - px;
+            py = n - 1 - py;
+        }
+        if (py < 0) {
+            px = n - 1 - px;
+            py = -py;
+        } else if (py >= n) {
+            px = n - 1 - px;
+            py = 2 * n - 1 - py;
+        }
+        if (n == 1) px = py = 0;
+        return e.rgb[((size_t)py * n + px) * 3 + c];
+    };
+    const float v0 = get(xi, yi), v1 = get(xi + 1, yi), v2 = get(xi, yi + 1), v3 = get(xi + 1, yi + 1);
+    return ((1 - dx) * (1 - dy) * v0 + dx * (1 - dy) * v1 + (1 - dx) * dy * v2 + dx * dy * v3);
+}
+
+// PortalImageInfiniteLight's constructor (lights.cpp:1140-1212): the portal frame
+// (Frame::FromXY(p03, p01)), the map rectified over the portal's (alpha, beta) angles (each
+// pixel centre's direction back through renderFromLight to the equal-area map, bilerped), the
+// sampling distribution (channel average times duv/dw at the pixel centre,
+// Image::GetSamplingDistribution) and its SummedAreaTable (double sums; the device keeps the
+// Float values LookupInt returns).  Host float arithmetic with libm, as the reference's CPU build.
+void BuildPortal(EnvLightDesc &e, const std::string &loc) {
+    auto P = [&](int k) { return V3(e.portalP[k][0], e.portalP[k][1], e.portalP[k][2]); };
+    const V3 p01 = Normalize(P(1) - P(0)), p12 = Normalize(P(2) - P(1));
+    const V3 p32 = Normalize(P(2) - P(3)), p03 = Normalize(P(3) - P(0));
+    if (std::abs(Dot(p01, p32) - 1) > .001 || std::abs(Dot(p12, p03) - 1) > .001 || std::abs(Dot(p01, p12)) > .001 ||
+        std::abs(Dot(p12, p32)) > .001 || std::abs(Dot(p32, p03)) > .001 || std::abs(Dot(p03, p01)) > .001)
+        std::fprintf(stderr, "%s: Error: Infinite light portal isn't a planar quadrilateral\n", loc.c_str());
+    const V3 z = Cross(p03, p01);
+    const float fr[9] = {p03.x, p03.y, p03.z, p01.x, p01.y, p01.z, z.x, z.y, z.z};
+    std::copy(fr, fr + 9, e.portalFrame);
+    const int n = e.res;
+    e.rect.assign((size_t)n * n * 3, 0.f);
+    for (int y = 0; y < n; ++y)
+        for (int x = 0; x < n; ++x) {
+            const float u = (x + 0.5f) / n, v = (y + 0.5f) / n;
+            V3 w = PortalRenderFromImage(e.portalFrame, u, v, nullptr);
+            w = Normalize(MulM3(e.lightFromRender, w));
+            float ue, ve;
+            EqualAreaSphereToSquare(w, &ue, &ve);
+            for (int c = 0; c < 3; ++c) e.rect[((size_t)y * n + x) * 3 + c] = BilerpOctahedral(e, ue, ve, c);
+        }
+    e.portalFunc.assign((size_t)n * n, 0.f);
+    for (int y = 0; y < n; ++y)
+        for (int x = 0; x < n; ++x) {
+            const float *c = &e.rect[((size_t)y * n + x) * 3];
+            float sum = 0;
+            for (int k = 0; k < 3; ++k) sum += c[k];
+            const float value = sum / 3;
+            float duv_dw;
+            (void)PortalRenderFromImage(e.portalFrame, (x + .5f) / n, (y + .5f) / n, &duv_dw);
+            e.portalFunc[(size_t)y * n + x] = value * duv_dw;
+        }
+    std::vector<double> sum((size_t)n * n);
+    auto S = [&](int x, int y) -> double & { return sum[(size_t)y * n + x]; };
+    auto F = [&](int x, int y) { return e.portalFunc[(size_t)y * n + x]; };
+    S(0, 0) = F(0, 0);
+    for (int x = 1; x < n; ++x) S(x, 0) = F(x, 0) + S(x - 1, 0);
+    for (int y = 1; y < n; ++y) S(0, y) = F(0, y) + S(0, y - 1);
+    for (int y = 1; y < n; ++y)
+        for (int x = 1; x < n; ++x) S(x, y) = (F(x, y) + S(x - 1, y) + S(x, y - 1) - S(x - 1, y - 1));
+    e.portalSat.resize(sum.size());
+    for (size_t i = 0; i < sum.size(); ++i) e.portalSat[i] = (float)sum[i];
+}
+}  // namespace pbrt_amd

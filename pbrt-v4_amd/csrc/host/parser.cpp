@@ -2336,9 +2336,13 @@ InfiniteLightDesc Parser::InfiniteLight(PendingLight &l) {
     InfiniteLightDesc il;
     float scale = (float)ps.GetFloat("scale", 1);
     const float E_v = (float)ps.GetFloat("illuminance", -1);
-    if (ps.Find("portal")) throw Error(ps.loc + ": portal infinite lights are not supported yet");
+    Param *portal = ps.Find("portal", "point3");
+    if (!portal) portal = ps.Find("portal", "point");
     std::string fn = ps.GetString("filename", "");
     if (L && !fn.empty()) throw Error(ps.loc + ": Can't specify both emission \"L\" and \"filename\" with ImageInfiniteLight");
+    if (portal && fn.empty()) throw Error(ps.loc + ": a portal infinite light with \"L\" (no \"filename\") is not supported yet");
+    if (portal && portal->nums.size() != 12)
+        throw Error(ps.loc + ": Expected 4 vertices for infinite light portal but given " + std::to_string(portal->nums.size() / 3));
     if (fn.empty()) {
         std::array<float, 311> dense = GetSpectralData().denseD65;
         float photometric = GetSpectralData().photometricD65;
@@ -2399,6 +2403,16 @@ InfiniteLightDesc Parser::InfiniteLight(PendingLight &l) {
             env.lightFromRender[3 * i + j] = (float)lfr[i][j];
         }
     env.filename = fn;
+    if (portal) {
+        // the portal's corners through RenderFromWorld only (lights.cpp:1683-1685)
+        for (int k = 0; k < 4; ++k) {
+            const V3 p = XformPoint(scene.camera.renderFromWorld,
+                                    V3((float)portal->nums[3 * k], (float)portal->nums[3 * k + 1], (float)portal->nums[3 * k + 2]));
+            env.portalP[k][0] = p.x, env.portalP[k][1] = p.y, env.portalP[k][2] = p.z;
+        }
+        env.portal = true;
+        BuildPortal(env, ps.loc);
+    }
     il.image = (int)scene.envLights.size();
     scene.envLights.push_back(std::move(env));
     ps.CheckUnused();

@@ -275,7 +275,15 @@ struct EnvLightDesc {
     float renderFromLight[9] = {};    // upper 3x3 of renderFromLight (row major)
     float lightFromRender[9] = {};    // upper 3x3 of its inverse (Transform::ApplyInverse)
     std::string filename;
+    // PortalImageInfiniteLight (lights.h:644-744): the portal's corners in render space, its
+    // frame (rows x, y, z), the rectified image [res][res][3] and its windowed sampling tables
+    // (the distribution's function and the SummedAreaTable's sums as Float), BuildPortal
+    bool portal = false;
+    float portalP[4][3] = {};
+    float portalFrame[9] = {};
+    std::vector<float> rect, portalFunc, portalSat;
 };
+void BuildPortal(EnvLightDesc &e, const std::string &loc);
 
 // PointLight / SpotLight / DistantLight (lights.h:200-300, 740-800; lights.cpp:192-276, 1376-1495)
 // in render space: deltaLights holds the point and spot lights first (light-BVH members, global

@@ -1135,6 +1135,24 @@ struct LiSample {
 // 2 sceneRadius away and the nearest pixel's radiance
 __device__ inline bool SampleEnvLi(const DeviceScene &S, int j, V3 cp, float u0, float u1, LiSample *ls) {
     const DeviceEnvLight &E = S.env[S.infImage[j]];
+    if (E.portal) {  // PortalImageInfiniteLight::SampleLi from the context point
+        V3 wi;
+        float pdf;
+        EnvCoef ec;
+        if (!PortalSampleLi(E, cp, u0, u1, &wi, &pdf, &ec)) return false;
+        ls->wi = wi;
+        ls->pdf = pdf;
+        ls->lp = cp + wi * (2 * S.sceneRadius);
+        ls->lpe = V3(0, 0, 0);
+        ls->ln = V3(0, 0, 0);
+        ls->scale = S.infScale[j];
+        ls->d2 = 1;
+        ls->spectrum = S.infSpectrum[j];
+        ls->delta = false;
+        ls->envLe = true;
+        ls->env = ec;
+        return true;
+    }
     float uu, vv, mapPDF;
     EnvSampleUV(E, u0, u1, &uu, &vv, &mapPDF);
     if (mapPDF == 0) return false;

@@ -2048,11 +2048,13 @@ __global__ void __launch_bounds__(kBlock) k_vescaped(DeviceScene S0, PathState s
                 // r_l * PMF * PDF_Li(allowIncompletePDF) joins the denominator
                 const DeviceEnvLight &E = S.env[S.infImage[k]];
                 const V3 rd = LoadV3(rec.ray + 3 * (size_t)NR, NR, ri);
-                const EnvCoef ec = EnvLeCoef(E, rd);
+                // a portal light's Le depends on the ray origin, its PDF_Li on the previous
+                // vertex (prevIntrCtx.p())
+                const EnvCoef ec = E.portal ? PortalLeCoef(E, LoadV3(rec.ray, NR, ri), rd) : EnvLeCoef(E, rd);
                 float eavg = avg;
                 if (!(depth == 0 || specularBounce)) {
                     const float pmf = LightPMF(S, V3(0, 0, 0), V3(0, 0, 0), S.nAreaLights + S.nPointSpot + k);
-                    const float pdf = EnvPDFLi(E, rd);
+                    const float pdf = E.portal ? PortalPDFLi(E, LoadV3(rec.prev, NR, ri), rd) : EnvPDFLi(E, rd);
                     float es = 0;
 #pragma unroll 1
                     for (int i = 0; i < kNS; ++i) {

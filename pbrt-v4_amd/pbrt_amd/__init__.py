@@ -112,6 +112,7 @@ class SceneFlat(ctypes.Structure):
         ("sss_params", ctypes.POINTER(ctypes.c_float)),
         ("sss_tables", ctypes.POINTER(ctypes.c_float)),
         ("vertex_s", ctypes.POINTER(ctypes.c_float)), ("n_vertex_s", ctypes.c_int),
+        ("env_portal", ctypes.POINTER(ctypes.c_float)),
     ]
 
 
@@ -140,7 +141,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_context_free", "pbrt_render", "pbrt_synchronize", "pbrt_get_stats", "pbrt_reset_stats",
     "pbrt_film_clear", "pbrt_film_device_ptr", "pbrt_film_read", "pbrt_film_get_rgb", "pbrt_intersect",
     "pbrt_debug_halton", "pbrt_debug_halton_fastpath_mismatches", "pbrt_debug_catmull_rom", "pbrt_debug_check_rn_math", "pbrt_debug_rgb_coeffs", "pbrt_debug_rgb2spec_column", "pbrt_debug_kernel_sections",
-    "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_sampler", "pbrt_debug_rng", "pbrt_debug_det_math", "pbrt_debug_hair", "pbrt_debug_procedural", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
+    "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_sampler", "pbrt_debug_rng", "pbrt_debug_det_math", "pbrt_debug_hair", "pbrt_debug_portal_eval", "pbrt_debug_procedural", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
     "pbrt_debug_named_spectrum", "pbrt_debug_bxdf", "pbrt_debug_layered", "pbrt_debug_triangle_shading", "pbrt_film_write_image",
     "pbrt_image_read_size", "pbrt_image_read", "pbrt_image_write", "pbrt_image_error", "pbrt_debug_filter_sample",
     "pbrt_debug_bvh_stats", "pbrt_debug_light_bvh", "pbrt_intersect_tr", "pbrt_intersect_one_random", "pbrt_image_flip", "pbrt_set_kernel_profiling", "pbrt_get_kernel_stats",
@@ -220,6 +221,7 @@ def _lib():
     lib.pbrt_debug_rng.argtypes = [c.c_uint64, c.c_uint64, c.POINTER(c.c_uint32)]
     lib.pbrt_debug_det_math.argtypes = [c.c_int, c.c_int, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_debug_hair.argtypes = [c.c_int, c.c_void_p, c.c_int, c.c_void_p]
+    lib.pbrt_debug_portal_eval.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_void_p, c.c_void_p]
     lib.pbrt_debug_procedural.argtypes = [c.c_int, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_debug_queue_counts.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_int]
     lib.pbrt_debug_trowbridge.argtypes = [c.c_void_p, c.c_void_p]
@@ -436,6 +438,20 @@ class Scene:
         out = np.zeros((len(d), 16), dtype=np.float32)
         _check(_lib().pbrt_debug_env_eval(self._h, env, d.ctypes.data, uu.ctypes.data, len(d), out.ctypes.data))
         return out
+
+    def portal_eval(self, env, queries, res=0):
+        """The product's PortalImageInfiniteLight on the host for [n][8] queries {p, d, u0, u1}
+        (pbrt_debug_portal_eval) -> [n][16]; with res > 0 also the rectified image [res][res][3]
+        and the windowed distribution's function [res][res]."""
+        q = np.ascontiguousarray(queries, dtype=np.float32).reshape(-1, 8)
+        out = np.zeros((len(q), 16), dtype=np.float32)
+        img = np.zeros(res * res * 4, np.float32) if res else None
+        _check(_lib().pbrt_debug_portal_eval(self._h, env, q.ctypes.data, len(q), out.ctypes.data,
+                                             img.ctypes.data if img is not None else None))
+        if img is None:
+            return out
+        n = res * res
+        return out, img[:3 * n].reshape(res, res, 3), img[3 * n:].reshape(res, res)
 
     def shape_eval(self, shape, rays, u):
         """The product's sphere / disk intersection, surface, sampling and pdf for rays[n][6]

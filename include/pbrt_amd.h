@@ -385,6 +385,9 @@ int pbrt_debug_check_rn_math(int device, uint64_t seed, int64_t n, int64_t *mism
  * SampleCatmullRom2D(nodes1, nodes2, values[n1][n2], cdf[n1][n2], alpha = x[2i], u = x[2i+1]) */
 int pbrt_debug_catmull_rom(int op, const float *nodes1, int n1, const float *nodes2, int n2, const float *values,
                            const float *cdf, const float *x, int n, float *out);
+/* The same utilities compiled for gfx950 and run on GPU `device` (one thread per query). */
+int pbrt_debug_catmull_rom_gpu(int device, int op, const float *nodes1, int n1, const float *nodes2, int n2,
+                               const float *values, const float *cdf, const float *x, int n, float *out);
 int64_t pbrt_debug_halton_fastpath_mismatches(const pbrt_scene *scene, int dim, uint32_t a0, uint32_t a1,
                                               uint32_t step);
 int pbrt_debug_rgb_coeffs(float r, float g, float b, float *coeffs3);

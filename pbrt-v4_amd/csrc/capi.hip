@@ -39,6 +39,8 @@ hipError_t LaunchFilm(const DeviceScene &S, const PathState &st, int nSamples, h
 hipError_t LaunchCheckRNMath(uint64_t seed, int blocks, int perThread, unsigned long long *bad, hipStream_t s);
 hipError_t LaunchDetMath(int fn, const float *a, const float *b, int n, float *out, hipStream_t s);
 hipError_t LaunchHairEval(const float *in, int n, float *out, hipStream_t s);
+hipError_t LaunchCatmullRom(int op, const float *nodes1, int n1, const float *nodes2, int n2, const float *values,
+                            const float *cdf, const float *x, int n, float *out, hipStream_t s);
 hipError_t LaunchQueueOverflowCheck(const PathState &st, int nDepths, hipStream_t s);
 hipError_t LaunchIntersectBatch(const DeviceScene &S, const float *rays, int n, int anyHit, int *outPrim,
                                 float *outHit, hipStream_t s);
@@ -2513,6 +2515,34 @@ int pbrt_debug_catmull_rom(int op, const float *nodes1, int n1, const float *nod
         }
     }
     return 0;
+}
+
+int pbrt_debug_catmull_rom_gpu(int device, int op, const float *nodes1, int n1, const float *nodes2, int n2,
+                               const float *values, const float *cdf, const float *x, int n, float *out) {
+    try {
+        if (!nodes1 || !x || !out || n < 0 || n1 < 2 || (op == 3 && (!nodes2 || n2 < 2 || !values || !cdf)) ||
+            (op == 1 && !values) || (op != 0 && op != 1 && op != 3))
+            return Fail("pbrt_debug_catmull_rom_gpu: bad arguments");
+        HIPCHECK(hipSetDevice(device));
+        DevBuf<float> dn1, dn2, dv, dc, dx, dout;
+        dn1.Upload(std::vector<float>(nodes1, nodes1 + n1));
+        dn2.Upload(op == 3 ? std::vector<float>(nodes2, nodes2 + n2) : std::vector<float>(1, 0.f));
+        // values: [n1][n2] for sample2d, [n1] for invert; cdf [n1][n2]
+        const size_t nv = op == 3 ? (size_t)n1 * n2 : (op == 1 ? (size_t)n1 : 1);
+        dv.Upload(values ? std::vector<float>(values, values + nv) : std::vector<float>(1, 0.f));
+        dc.Upload(op == 3 ? std::vector<float>(cdf, cdf + (size_t)n1 * n2) : std::vector<float>(1, 0.f));
+        const size_t nx = op == 3 ? 2 * (size_t)n : (size_t)n;
+        dx.Upload(std::vector<float>(x, x + std::max<size_t>(nx, 1)));
+        const size_t no = op == 0 ? 6 * (size_t)n : (size_t)n;
+        dout.Alloc(std::max<size_t>(no, 1));
+        if (n > 0) {
+            HIPCHECK(LaunchCatmullRom(op, dn1.p, n1, dn2.p, n2, dv.p, dc.p, dx.p, n, dout.p, nullptr));
+            HIPCHECK(hipMemcpy(out, dout.p, no * sizeof(float), hipMemcpyDeviceToHost));
+        }
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
 }
 
 int64_t pbrt_debug_halton_fastpath_mismatches(const pbrt_scene *scene, int dim, uint32_t a0, uint32_t a1,

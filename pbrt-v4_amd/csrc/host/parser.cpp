@@ -2139,6 +2139,7 @@ void Parser::Finish() {
         float lightScale = 1;
         bool twoSided = false;
         float power = -1;
+        float imageKe = 1;  // an image emitter's mean luminance (k_e before the area term)
         if (!s.areaLight.empty()) {
             ParamSet &ap = s.areaParams;
             Param *L = ap.Find("L");
@@ -2208,7 +2209,6 @@ void Parser::Finish() {
                     if (std::isnan(v)) throw Error(ap.loc + ": " + fn + ": image has not-a-number pixel values and so is not suitable as a light.");
                 }
                 if (im.nc < 3) throw Error(ap.loc + ": " + fn + ": Image provided to \"diffuse\" area light must have R, G, and B channels.");
-                if (power > 0) throw Error(ap.loc + ": \"power\" for image area lights is not supported yet");
                 if (s.kind == kShapeSphereT || s.kind == kShapeDiskT || s.kind == kShapeCylinderT || !s.quadIdx.empty())
                     throw Error(ap.loc + ": image area lights on spheres, disks, cylinders and bilinear patches are not supported yet");
                 AreaLightImage ai;
@@ -2217,6 +2217,18 @@ void Parser::Finish() {
                 ai.rgb.resize((size_t)3 * im.w * im.h);
                 for (size_t q = 0; q < (size_t)im.w * im.h; ++q)
                     for (int c = 0; c < 3; ++c) ai.rgb[3 * q + c] = im.v[q * im.nc + c];
+                if (power > 0) {
+                    // k_e of an image emitter: its mean luminance (the image colour space's
+                    // LuminanceVector, lights.cpp:945-957); the area and pi follow per shape
+                    const double(*xr)[3] = GetSpectralData().xyzFromRGB;
+                    const float lum[3] = {(float)xr[1][0], (float)xr[1][1], (float)xr[1][2]};
+                    float k = 0;
+                    for (int y = 0; y < im.h; ++y)
+                        for (int x = 0; x < im.w; ++x)
+                            for (int c = 0; c < 3; ++c) k += ai.rgb[3 * ((size_t)y * im.w + x) + c] * lum[c];
+                    k /= im.w * im.h;
+                    imageKe = k;
+                }
                 curSpread.image = (int)scene.areaLightImages.size();
                 scene.areaLightImages.push_back(std::move(ai));
             }
@@ -2261,8 +2273,9 @@ void Parser::Finish() {
                 l.area = 0.5f * Length(Cross(p1 - p0, p2 - p0));  // Triangle::Area (shapes.h)
                 if (power > 0) {
                     // lights.cpp:943-965: each triangle is its own DiffuseAreaLight, scaled so that
-                    // it emits phi_v: k_e = (twoSided ? 2 : 1) * Area * Pi
-                    float k_e = 1;
+                    // it emits phi_v: k_e = (twoSided ? 2 : 1) * Area * Pi (times an image's mean
+                    // luminance)
+                    float k_e = imageKe;
                     k_e *= (twoSided ? 2 : 1) * l.area * kPi;
                     l.scale *= power / k_e;
                 }

@@ -15,6 +15,7 @@
 // device-side queue counters so the host never synchronises inside the render loop.
 #include "common.h"
 #include "../core/hair.h"
+#include "../core/bssrdf.h"
 
 namespace pbrt_amd {
 // Traversal LDS of one block (shared with volpath.hip): group stack (uint2 entries), cached
@@ -1610,6 +1611,30 @@ __global__ void k_hair_eval(const float *in, int n, float *out) {
 }
 hipError_t LaunchHairEval(const float *in, int n, float *out, hipStream_t s) {
     hipLaunchKernelGGL(k_hair_eval, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, in, n, out);
+    return hipGetLastError();
+}
+// the Catmull-Rom spline utilities of the subsurface kernels (core/bssrdf.h) per query, as the
+// host entry pbrt_debug_catmull_rom computes them: op 0 weights [6], 1 invert, 3 sample2d
+__global__ void k_catmull_rom(int op, const float *nodes1, int n1, const float *nodes2, int n2, const float *values,
+                              const float *cdf, const float *x, int n, float *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (op == 0) {
+        int off = 0;
+        float w[4] = {0, 0, 0, 0};
+        const bool ok = CatmullRomWeights(nodes1, n1, x[i], &off, w);
+        const float r[6] = {ok ? 1.f : 0.f, (float)(ok ? off : 0), w[0], w[1], w[2], w[3]};
+        for (int k = 0; k < 6; ++k) out[6 * i + k] = r[k];
+    } else if (op == 1) {
+        out[i] = InvertCatmullRom(nodes1, values, n1, x[i]);
+    } else {
+        out[i] = SampleCatmullRom2D(nodes1, n1, nodes2, n2, values, cdf, x[2 * i], x[2 * i + 1]);
+    }
+}
+hipError_t LaunchCatmullRom(int op, const float *nodes1, int n1, const float *nodes2, int n2, const float *values,
+                            const float *cdf, const float *x, int n, float *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_catmull_rom, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, op, nodes1, n1, nodes2, n2,
+                       values, cdf, x, n, out);
     return hipGetLastError();
 }
 hipError_t LaunchCheckRNMath(uint64_t seed, int blocks, int perThread, unsigned long long *bad, hipStream_t s) {

@@ -141,7 +141,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_context_free", "pbrt_render", "pbrt_synchronize", "pbrt_get_stats", "pbrt_reset_stats",
     "pbrt_film_clear", "pbrt_film_device_ptr", "pbrt_film_read", "pbrt_film_get_rgb", "pbrt_intersect",
     "pbrt_debug_halton", "pbrt_debug_halton_fastpath_mismatches", "pbrt_debug_catmull_rom", "pbrt_debug_check_rn_math", "pbrt_debug_rgb_coeffs", "pbrt_debug_rgb2spec_column", "pbrt_debug_kernel_sections",
-    "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_sampler", "pbrt_debug_rng", "pbrt_debug_det_math", "pbrt_debug_hair", "pbrt_debug_portal_eval", "pbrt_debug_procedural", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
+    "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_sampler", "pbrt_debug_rng", "pbrt_debug_det_math", "pbrt_debug_hair", "pbrt_debug_catmull_rom_gpu", "pbrt_debug_portal_eval", "pbrt_debug_procedural", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
     "pbrt_debug_named_spectrum", "pbrt_debug_bxdf", "pbrt_debug_layered", "pbrt_debug_triangle_shading", "pbrt_film_write_image",
     "pbrt_image_read_size", "pbrt_image_read", "pbrt_image_write", "pbrt_image_error", "pbrt_debug_filter_sample",
     "pbrt_debug_bvh_stats", "pbrt_debug_light_bvh", "pbrt_intersect_tr", "pbrt_intersect_one_random", "pbrt_image_flip", "pbrt_set_kernel_profiling", "pbrt_get_kernel_stats",
@@ -221,6 +221,8 @@ def _lib():
     lib.pbrt_debug_rng.argtypes = [c.c_uint64, c.c_uint64, c.POINTER(c.c_uint32)]
     lib.pbrt_debug_det_math.argtypes = [c.c_int, c.c_int, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_debug_hair.argtypes = [c.c_int, c.c_void_p, c.c_int, c.c_void_p]
+    lib.pbrt_debug_catmull_rom_gpu.argtypes = [c.c_int, c.c_int, c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_void_p,
+                                               c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_debug_portal_eval.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_void_p, c.c_void_p]
     lib.pbrt_debug_procedural.argtypes = [c.c_int, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_debug_queue_counts.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_int]
@@ -521,14 +523,19 @@ def hair_eval(queries, device=-1):
     return out
 
 
-def catmull_rom(op, nodes1, nodes2, values, cdf, x):
-    """The product's Catmull-Rom spline utilities (core/bssrdf.h) on the host: op 0 weights
-    [n][6] (ok, offset, w0..w3), 1 InvertCatmullRom [n], 3 SampleCatmullRom2D (x: alpha, u pairs)."""
+def catmull_rom(op, nodes1, nodes2, values, cdf, x, device=-1):
+    """The product's Catmull-Rom spline utilities (core/bssrdf.h) on the host, or compiled for
+    gfx950 on GPU `device`: op 0 weights [n][6] (ok, offset, w0..w3), 1 InvertCatmullRom [n], 3
+    SampleCatmullRom2D (x: alpha, u pairs)."""
     a = [np.ascontiguousarray(v, np.float32) for v in (nodes1, nodes2, values, cdf, x)]
     n = len(a[4]) // 2 if op == 3 else len(a[4])
     out = np.zeros(n * 6 if op == 0 else n, np.float32)
-    _check(_lib().pbrt_debug_catmull_rom(op, a[0].ctypes.data, len(a[0]), a[1].ctypes.data, len(a[1]),
-                                         a[2].ctypes.data, a[3].ctypes.data, a[4].ctypes.data, n, out.ctypes.data))
+    args = (op, a[0].ctypes.data, len(a[0]), a[1].ctypes.data, len(a[1]), a[2].ctypes.data, a[3].ctypes.data,
+            a[4].ctypes.data, n, out.ctypes.data)
+    if device >= 0:
+        _check(_lib().pbrt_debug_catmull_rom_gpu(device, *args))
+    else:
+        _check(_lib().pbrt_debug_catmull_rom(*args))
     return out.reshape(-1, 6) if op == 0 else out
 
 

@@ -3,8 +3,8 @@ an emitter's radiance is scale * RGBIlluminantSpectrum(ClampZero(image.Bilerp((u
 at the hit's uv for emission and at the light sample's uv (Triangle::Sample's barycentric uv)
 for light sampling; the light BVH's phi is the image's mean channel value.
 
-* Loader: the image, its errors (with "L", a grey image, "power", non-triangle emitters, the
-  volumetric path).
+* Loader: the image, its errors (with "L", a grey image, non-triangle emitters, the volumetric
+  path); "power" normalises by the image's mean luminance (lights.cpp:943-965).
 * Known answers on the oracle: an all-white image emits "rgb L [1 1 1]" (the grey
   RGBIlluminantSpectrum is the illuminant itself) to the bilerp's last-bit rounding; a camera looking at a red-over-blue emitter
   sees red in the image's top half and blue in its bottom half (the v flip); a floor under a
@@ -54,7 +54,6 @@ def test_image_emitter_loader(pa, tmp_path):
 @pytest.mark.parametrize("emitter, msg", [
     ('AreaLightSource "diffuse" "string filename" "e.png" "rgb L" [1 1 1]', "Both"),
     ('AreaLightSource "diffuse" "string filename" "g.png"', "must have R, G, and B"),
-    ('AreaLightSource "diffuse" "string filename" "e.png" "float power" 10', "not supported yet"),
 ])
 def test_image_emitter_errors(pa, tmp_path, emitter, msg):
     png(tmp_path / "e.png", np.full((4, 4, 3), 200))
@@ -92,6 +91,19 @@ def test_white_image_equals_rgb_emitter(pa, oracle, tmp_path):
     # equal up to the bilerp's own rounding: its four weights sum to 1 within an ulp, so the
     # bilerped white is 1 +- 1 ulp where pbrt's would be too
     np.testing.assert_allclose(fa, fb, rtol=3e-7, atol=0)
+
+
+def test_image_emitter_power(pa, oracle, tmp_path):
+    """power: k_e = mean luminance x (twoSided ? 2 : 1) x area x pi, so a uniform image of any
+    level emits what "rgb L" [1 1 1] with the same power does (white: luminance 1)"""
+    png(tmp_path / "w.png", np.full((8, 8, 3), 255))
+    png(tmp_path / "h.png", np.full((8, 8, 3), 128))
+    films = [oracle.render(scene(pa, tmp_path, f'AreaLightSource "diffuse" {src} "float power" 20', single=True),
+                           threads=8) for src in ('"string filename" "w.png"', '"string filename" "h.png"', '"rgb L" [1 1 1]')]
+    assert films[0][:3].sum() > 0
+    # the luminance vector sums to 1 within a few ulp, and the bilerp rounds by an ulp
+    np.testing.assert_allclose(films[0], films[2], rtol=1e-5, atol=0)
+    np.testing.assert_allclose(films[1], films[2], rtol=1e-5, atol=0)
 
 
 def test_image_emitter_seen_directly(pa, oracle, tmp_path):

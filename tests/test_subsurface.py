@@ -146,6 +146,25 @@ def test_subsurface_matches_oracle_gpu(pa, oracle, form):
     print(f"subsurface ({form}): {frac*100:.2f}% pixels within 1e-3, mean rel {mr:.2e}")
 
 
+@pytest.mark.gpu
+def test_catmull_rom_gpu_equals_host(pa):
+    """the spline utilities compiled for gfx950 give the host build's bits on a real BSSRDF table
+    (weights over the albedos, InvertCatmullRom of rhoEff, SampleCatmullRom2D of the profile)"""
+    _, _, _, _, tab = flat_sss(pa, FORMS["reflectance"])
+    t = tab[0]
+    rho, rad, prof = t[:100], t[100:164], t[164:164 + 6400]
+    rhoEff, cdf = t[6564:6664], t[6664:6664 + 6400]
+    rng = np.random.default_rng(4)
+    n = 1 << 16
+    x = np.concatenate([rng.uniform(0, 1, n), rng.uniform(0.3, 0.99, n)]).astype(np.float32)
+    for op, args in ((0, (rho, rad, prof, cdf, x)), (1, (rho, rad, rhoEff, cdf, x)),
+                     (3, (rho, rad, prof, cdf, np.stack([rng.uniform(0, 1, n), rng.uniform(0, 1, n)], 1).ravel()))):
+        host = pa.catmull_rom(op, *args)
+        dev = pa.catmull_rom(op, *args, device=0)
+        bad = host.view(np.uint32) != dev.view(np.uint32)
+        assert not bad.any(), (op, int(bad.sum()), np.nonzero(bad.reshape(len(host), -1).any(axis=1))[0][:5])
+
+
 def probe_segments(n=6000, seed=12):
     """Probe-like segments: axis-aligned (the BSSRDF frames of the box's faces) and random ones
     through the blob and the box"""

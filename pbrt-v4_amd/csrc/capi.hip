@@ -1324,9 +1324,6 @@ static void BuildDevice(pbrt_context *c) {
             S.nImageAreaLights += l.image >= 0;
         }
         if (S.nImageAreaLights > 0) {
-            if (c->volumetric)
-                throw Error("image area lights together with the volumetric path (media, interface, layered, thin "
-                            "dielectric, diffuse transmission or dispersive materials) are not supported yet");
             c->lightImg.Upload(img);
             c->lightImgOff.Upload(lo);
             if (!S.tex.rgbZNodes) {

@@ -110,7 +110,10 @@ static void BuildHalton(SceneDesc &s) {
     s.haltonMultInverse[0] = multInv(s.haltonBaseScales[1], s.haltonBaseScales[0]);
     s.haltonMultInverse[1] = multInv(s.haltonBaseScales[0], s.haltonBaseScales[1]);
 
-    int maxDim = 7 * s.maxDepth + 6;  // 6 camera dims + 7 per bounce (wavefront/samples.cpp:39)
+    // 6 camera dims + 7 per bounce, 10 with subsurface scattering (wavefront/samples.cpp:39-41):
+    // pbrt's Halton sampler holds permutations for every dimension below PrimeTableSize, so none
+    // of a path's dimensions may wrap here either
+    int maxDim = (s.sss.empty() ? 7 : 10) * s.maxDepth + 6;
     maxDim = std::min(maxDim, 999);
     const std::vector<int> &primes = Primes();
     s.permTable.clear();

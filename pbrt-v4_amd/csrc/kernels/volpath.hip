@@ -539,7 +539,13 @@ __device__ inline void SssSamplesAt(const DeviceScene &S, const PathState &st, i
         *uc = ZSobolGet1D(S.zs, morton, d0 + 7, S.zsPerms, S.sobolM1);
         ZSobolGet2D(S.zs, morton, d0 + 8, S.zsPerms, S.sobolM1, u0, u1);
     } else {
-        Halton h = StartPixelSample(S, px, py, sampleIndex, d0 + 7);
+        // the stateful sampler's dimension after GenerateRaySamples' seven draws (Get1D, Get2D,
+        // Get1D, Get2D, Get1D with their wrap to dimension 2), then the subsurface draws
+        int d = d0;
+        auto g1 = [&] { d = (d >= S.nDims ? 2 : d) + 1; };
+        auto g2 = [&] { d = (d + 1 >= S.nDims ? 2 : d) + 2; };
+        g1(), g2(), g1(), g2(), g1();
+        Halton h = StartPixelSample(S, px, py, sampleIndex, d);
         *uc = Get1D(S, h);
         Get2D(S, h, u0, u1);
     }
@@ -1111,7 +1117,10 @@ __device__ inline bool SampleAreaLight(const DeviceScene &S, V3 refP, V3 refN, V
     int li;
     float lpmf;
     if (!SampleLight(S, refP, refNs, uc, &li, &lpmf)) return false;
-    if (li >= S.nAreaLights || (Ext && S.nShapes > 0 && __float_as_int(S.lights[li].v0.w) >= S.nTris)) {
+    // lights other than plain emitting triangles -- and image emitters, whose radiance is the
+    // image at the sample's uv -- through SampleLiSurface (common.h)
+    if (li >= S.nAreaLights || (Ext && S.nShapes > 0 && __float_as_int(S.lights[li].v0.w) >= S.nTris) ||
+        (Ext && S.nImageAreaLights > 0 && S.lightImgOff[li] >= 0)) {
         LiSample ls;
         if (!SampleLiSurface<false, false, Ext>(S, S.lights, li, refP, refN, refNs, u0, u1, &ls)) return false;
         const float rd2 = 1 / ls.d2;
@@ -1212,7 +1221,8 @@ __device__ inline bool SampleAreaLightAt(const DeviceScene &S, V3 refP, V3 refN,
     int li;
     float lpmf;
     if (!SampleLight(S, refP, refNs, uc, &li, &lpmf)) return false;
-    if (li >= S.nAreaLights || (Ext && S.nShapes > 0 && __float_as_int(S.lights[li].v0.w) >= S.nTris)) {
+    if (li >= S.nAreaLights || (Ext && S.nShapes > 0 && __float_as_int(S.lights[li].v0.w) >= S.nTris) ||
+        (Ext && S.nImageAreaLights > 0 && S.lightImgOff[li] >= 0)) {
         LiSample ls;
         if (!SampleLiSurface<false, false, Ext>(S, S.lights, li, refP, refN, refNs, u0, u1, &ls, refErr)) return false;
         out->p = ls.lp;
@@ -1398,8 +1408,19 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
                     ds = i == 0 ? dv : ds + dv;
                 }
                 const float avg = ds / kNS;
-                AddSpecToL(S, st, slot, lambda0,
-                           [&](int i, int off) { return betaIn(i) * (Ld.scale * DenseAt(S, Ld.spectrum, off)) / avg; });
+                if (Ext && S.nImageAreaLights > 0 && S.lightImgOff[light] >= 0) {
+                    // an image emitter: the image at the hit's uv (lights.h:460-467)
+                    const EnvCoef ec = AreaImageCoef(S, S.lightImgOff[light], si.uv[0], si.uv[1]);
+                    SpectralIter itL(lambda0);
+                    AddSpecToL(S, st, slot, lambda0, [&](int i, int off) {
+                        const float lam = itL.lam;
+                        itL.Next();
+                        return betaIn(i) * EnvLe(ec, Ld.scale, DenseAt(S, Ld.spectrum, off), lam) / avg;
+                    });
+                } else {
+                    AddSpecToL(S, st, slot, lambda0,
+                               [&](int i, int off) { return betaIn(i) * (Ld.scale * DenseAt(S, Ld.spectrum, off)) / avg; });
+                }
             }
         }
         if (last) continue;
@@ -2904,7 +2925,7 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
         hipLaunchKernelGGL(k_queue_holes, dim3(64, kShards), block, 0, s, st.counters, wf, kVShadow, v.shPixel,      \
                            st.capS, v.holes, stage);
     // Ext: analytic shapes or image lights in the scene (their paths compiled in)
-    if (S.nShapes > 0 || S.nEnv > 0 || S.nImageDelta > 0 || S.hasSpread) {
+    if (S.nShapes > 0 || S.nEnv > 0 || S.nImageDelta > 0 || S.hasSpread || S.nImageAreaLights > 0) {
         if (S.textured) {
             hipLaunchKernelGGL(k_vtexture<true>, gW, block, 0, s, S, st, v, wf);
             if (S.matTypeMask & other) hipLaunchKernelGGL((k_vsurface<false, true, true>), gW, block, surfLds, s, S, st, v, wf);

@@ -3,13 +3,12 @@ an emitter's radiance is scale * RGBIlluminantSpectrum(ClampZero(image.Bilerp((u
 at the hit's uv for emission and at the light sample's uv (Triangle::Sample's barycentric uv)
 for light sampling; the light BVH's phi is the image's mean channel value.
 
-* Loader: the image, its errors (with "L", a grey image, non-triangle emitters, the volumetric
-  path); "power" normalises by the image's mean luminance (lights.cpp:943-965).
+* Loader: the image, its errors (with "L", a grey image, non-triangle emitters); "power" normalises by the image's mean luminance (lights.cpp:943-965).
 * Known answers on the oracle: an all-white image emits "rgb L [1 1 1]" (the grey
   RGBIlluminantSpectrum is the illuminant itself) to the bilerp's last-bit rounding; a camera looking at a red-over-blue emitter
   sees red in the image's top half and blue in its bottom half (the v flip); a floor under a
   left-red / right-blue emitter is tinted accordingly on each side.
-* GPU film parity on an image emitter scene."""
+* GPU film parity on an image emitter scene, on the surface and the volumetric path."""
 import numpy as np
 import pytest
 
@@ -70,14 +69,23 @@ def test_image_emitter_on_sphere_refused(pa, tmp_path):
 
 
 @pytest.mark.gpu
-def test_image_emitter_refused_with_media(pa, tmp_path):
-    """BuildDevice (the device context) decides the volumetric path and refuses image emitters there"""
-    png(tmp_path / "e.png", np.full((4, 4, 3), 200))
-    extra = ('MakeNamedMedium "fog" "string type" "homogeneous"\nAttributeBegin\nMediumInterface "fog" ""\n'
-             'Material "interface"\nShape "sphere" "float radius" 0.3\nAttributeEnd\n')
-    sc = scene(pa, tmp_path, 'AreaLightSource "diffuse" "string filename" "e.png"', extra=extra)
-    with pytest.raises(pa.PbrtError, match="volumetric path"):
-        pa.WavefrontPathIntegrator(sc, max_paths=1 << 12)
+def test_image_emitter_with_media_matches_oracle_gpu(pa, oracle, tmp_path):
+    """an image emitter on the volumetric path (a fog ball puts the scene there): emission at the
+    hit's uv in k_vsurface, light samples at the sample's uv through SampleLiSurface"""
+    from test_gpu_media import check, gpu_rgb, oracle_rgb
+    img = np.zeros((8, 8, 3))
+    img[:, :4, 0] = 255
+    img[:, 4:, 2] = 255
+    img[2:6, 2:6, 1] = 200
+    png(tmp_path / "e.png", img)
+    extra = ('MakeNamedMedium "fog" "string type" "homogeneous" "rgb sigma_a" [0.1 0.1 0.1] "rgb sigma_s" [0.6 0.6 0.6]\n'
+             'AttributeBegin\nMediumInterface "fog" ""\nMaterial "interface"\nTranslate 0.4 0.6 0\n'
+             'Shape "sphere" "float radius" 0.5\nAttributeEnd\n')
+    sc = scene(pa, tmp_path, 'AreaLightSource "diffuse" "string filename" "e.png" "float scale" 3 "float power" 40',
+               extra=extra, spp=16)
+    a, _ = gpu_rgb(pa, oracle, sc)
+    frac, mr = check(a, oracle_rgb(oracle, sc))
+    print(f"image emitter with media: {frac*100:.2f}% pixels within 1e-3, mean rel {mr:.2e}")
 
 
 def test_white_image_equals_rgb_emitter(pa, oracle, tmp_path):

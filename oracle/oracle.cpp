@@ -1799,6 +1799,13 @@ struct OShape {
         w[2] = Length(Cross(p01 - p00, p11 - p01));
         w[3] = Length(Cross(p11 - p10, p11 - p01));
     }
+    // a sample's (s, t): the mesh uv lerp at parametric (u, v) when the patch has uv
+    void PatchST(Float u, Float v, Float st[2]) const {
+        st[0] = u;
+        st[1] = v;
+        if (flags & 4)
+            for (int j = 0; j < 2; ++j) st[j] = Lerp(u, Lerp(v, UV[0][j], UV[2][j]), Lerp(v, UV[1][j], UV[3][j]));
+    }
     // BilinearPatch::Sample(u) (shapes.cpp:1158-1217)
     bool PatchSampleArea(Float u0, Float u1, ShapeSample *ss) const {
         Float pdf = 1, u = u0, v = u1;
@@ -1814,6 +1821,7 @@ struct OShape {
         ss->n = PatchNormalAt(Normalize(Cross(dpdu, dpdv)), u, v);
         Point3fi(p, gamma(6) * (Abs(P[0]) + Abs(P[2]) + Abs(P[1]) + Abs(P[3])), &ss->p, &ss->err);
         ss->pdf = pdf / Length(Cross(dpdu, dpdv));
+        PatchST(u, v, ss->uv);
         return true;
     }
     // BilinearPatch::Sample(ctx, u) and PDF(ctx, wi) (shapes.cpp:1257-1372)
@@ -1846,6 +1854,7 @@ struct OShape {
         out->p = p;
         out->err = Vec(0, 0, 0);
         out->pdf = pdf;
+        PatchST(su, sv, out->uv);
         return true;
     }
     Float PatchPDF(Vec cp, Vec cpErr, Vec cn, Vec cns, Vec wi) const {
@@ -2105,6 +2114,14 @@ struct OShape {
         si.wo = Normalize(-rd);
         return si;
     }
+    // a sphere point's (phi / phiMax, (theta - thetaZMin) / (thetaZMax - thetaZMin)) (shapes.cpp:54-58)
+    void SphereUV(Vec pObj, Float uv[2]) const {
+        const Float theta = SafeACos(pObj.z / a);
+        Float ph = CRATan2(pObj.y, pObj.x);
+        if (ph < 0) ph += 2 * Pi;
+        uv[0] = ph / d;
+        uv[1] = (theta - e) / (g - e);
+    }
     // Sphere::Sample(u) / Disk::Sample(u): area measure
     ShapeSample SampleArea(Float u0, Float u1) const {
         ShapeSample ss;
@@ -2121,6 +2138,7 @@ struct OShape {
             ss.p = Vec(po[0].Mid(), po[1].Mid(), po[2].Mid());
             ss.err = Vec(po[0].Err(), po[1].Err(), po[2].Err());
             ss.n = n;
+            SphereUV(pObj, ss.uv);
         } else if (cylinder()) {  // Cylinder::Sample(u) (shapes.h:772-793)
             const Float z = Lerp(u0, b, c), ph = u1 * d;
             Vec pObj(a * CRCos(ph), a * CRSin(ph), z);
@@ -2136,9 +2154,17 @@ struct OShape {
             Vec n = Normalize(XN(r2o, Vec(pObj.x, pObj.y, 0)));
             if (flags & 1) n = -n;
             ss.n = n;
+            ss.uv[0] = ph / d;
+            ss.uv[1] = (pObj.z - b) / (c - b);
         } else {
             Float dx, dy;
             SampleUniformDiskConcentric(u0, u1, &dx, &dy);
+            // Disk::Sample(u)'s (u, v) (shapes.h:517-522)
+            Float dphi = CRATan2(dy, dx);
+            if (dphi < 0) dphi += 2 * Pi;
+            const Float rs = std::sqrt(Sqr(dx * b) + Sqr(dy * b));
+            ss.uv[0] = dphi / d;
+            ss.uv[1] = (b - rs) / (b - c);
             const OInterval pi[3] = {OInterval(dx * b), OInterval(dy * b), OInterval(a)};
             OInterval po[3];
             XPointI(o2r, pi, po);
@@ -2178,6 +2204,7 @@ struct OShape {
                 Point3fi(p, gamma(5) * Abs(p), &out->p, &out->err);
                 out->n = n;
                 out->pdf = 1 / (2 * Pi * omc);
+                SphereUV(XP(r2o, p), out->uv);  // (*objectFromRender)(p)
                 return true;
             }
         }

@@ -2473,6 +2473,17 @@ PHD void PatchUV(const DeviceShape &s, int k, float *u, float *v) {
     *u = s.o2r[2 * k];
     *v = s.o2r[2 * k + 1];
 }
+// a bilinear patch's texture coordinates at parametric (u, v): the mesh uv lerp when the patch
+// has uv (flags bit 2), else (u, v) itself
+PHD void PatchST(const DeviceShape &s, float uu, float vv, float st[2]) {
+    st[0] = uu;
+    st[1] = vv;
+    if (s.flags & 4) {
+        float a[4][2];
+        for (int k = 0; k < 4; ++k) PatchUV(s, k, &a[k][0], &a[k][1]);  // uv00 uv10 uv01 uv11
+        for (int j = 0; j < 2; ++j) st[j] = Lerpf(uu, Lerpf(vv, a[0][j], a[2][j]), Lerpf(vv, a[1][j], a[3][j]));
+    }
+}
 // BilinearPatch::InteractionFromIntersection (shapes.h:1396-1497) without dndu/dndv; N: the
 // four vertex normals (render space, 12 floats) when the mesh has them
 PHD TriSurface BilinearSurface(const DeviceShape &s, const float *N, float uu, float vv) {
@@ -2552,7 +2563,7 @@ PHD void PatchAreaWeights(const PatchVerts &P, float w[4]) {
 }
 // BilinearPatch::Sample(u) (shapes.cpp:1158-1217): area measure; false for {}
 PHD bool BilinearSampleArea(const DeviceShape &s, const float *N, float u0, float u1, V3 *pOut, V3 *pErr, V3 *nOut,
-                            float *pdfOut) {
+                            float *pdfOut, float *stOut = nullptr) {
     const PatchVerts P = PatchP(s);
     float pdf = 1, uu = u0, vv = u1;
     if (s.b == 0) {
@@ -2570,6 +2581,7 @@ PHD bool BilinearSampleArea(const DeviceShape &s, const float *N, float u0, floa
     const V3 pAbsSum = Abs(P.p00) + Abs(P.p01) + Abs(P.p10) + Abs(P.p11);
     ToPoint3fi(p, gamma(6) * pAbsSum, pOut, pErr);
     *pdfOut = pdf / Length(Cross(dpdu, dpdv));
+    if (stOut) PatchST(s, uu, vv, stOut);
     return true;
 }
 // SphericalQuadArea (util/vecmath.h:1648-1666)
@@ -2901,7 +2913,17 @@ PHD TriSurface ShapeSurface(const DeviceShape &s, V3 pHit, const float *N = null
 struct ShapeSamplePt {
     V3 p, pErr, n;
     float pdf;
+    float uv[2];  // the sample's (u, v): an image emitter's lookup (DiffuseAreaLight::L)
 };
+// a sphere point's (phi / phiMax, (theta - thetaZMin) / (thetaZMax - thetaZMin)) from its object
+// space position (shapes.cpp:54-58, shapes.h:351-357)
+PHD void SphereUV(const DeviceShape &s, V3 pObj, float uv[2]) {
+    const float theta = SafeACos(pObj.z / s.a);
+    float phi = ATan2f(pObj.y, pObj.x);
+    if (phi < 0) phi += 2 * kPi;
+    uv[0] = phi / s.d;
+    uv[1] = (theta - s.e) / (s.f - s.e);
+}
 // Sphere::Sample(u) / Disk::Sample(u) (shapes.cpp:42-62, shapes.h:509-525): area measure
 PHD ShapeSamplePt ShapeSampleArea(const DeviceShape &s, float u0, float u1) {
     ShapeSamplePt r;
@@ -2920,6 +2942,7 @@ PHD ShapeSamplePt ShapeSampleArea(const DeviceShape &s, float u0, float u1) {
                         ItvFromValueAndError(pObj.z, pObjError.z)};
         XfPointInexact(s.o2r, pi, &r.p, &r.pErr);
         r.n = n;
+        SphereUV(s, pObj, r.uv);
     } else if (s.kind == kShapeCylinderT) {
         // Cylinder::Sample(u) (shapes.h:772-793)
         const float radius = s.a, zMin = s.b, zMax = s.c, phiMax = s.d;
@@ -2937,6 +2960,8 @@ PHD ShapeSamplePt ShapeSampleArea(const DeviceShape &s, float u0, float u1) {
         V3 n = Normalize(XfNormal(s.r2o, V3(pObj.x, pObj.y, 0)));
         if (s.flags & 1) n = -n;
         r.n = n;
+        r.uv[0] = phi / phiMax;
+        r.uv[1] = (pObj.z - zMin) / (zMax - zMin);
     } else {
         const float height = s.a, radius = s.b;
         float dx, dy;
@@ -2948,6 +2973,12 @@ PHD ShapeSamplePt ShapeSampleArea(const DeviceShape &s, float u0, float u1) {
         V3 n = Normalize(XfNormal(s.r2o, V3(0, 0, 1)));
         if (s.flags & 1) n = -n;
         r.n = n;
+        // Disk::Sample(u)'s (u, v) (shapes.h:517-522)
+        float phi = ATan2f(dy, dx);
+        if (phi < 0) phi += 2 * kPi;
+        const float radiusSample = std::sqrt(Sqr(pObj.x) + Sqr(pObj.y));
+        r.uv[0] = phi / s.d;
+        r.uv[1] = (radius - radiusSample) / (radius - s.c);
     }
     r.pdf = 1 / ShapeArea(s);
     return r;
@@ -2963,7 +2994,7 @@ PHD bool ShapeSampleSolidAngle(const DeviceShape &s, V3 cp, V3 cpErr, V3 cn, flo
         const V3 v01 = Normalize(P.p01 - cp), v11 = Normalize(P.p11 - cp);
         if (s.b == 0 || SphericalQuadArea(v00, v10, v11, v01) <= 1e-4f) {
             ShapeSamplePt ss;
-            if (!BilinearSampleArea(s, N, u0, u1, &ss.p, &ss.pErr, &ss.n, &ss.pdf)) return false;
+            if (!BilinearSampleArea(s, N, u0, u1, &ss.p, &ss.pErr, &ss.n, &ss.pdf, ss.uv)) return false;
             V3 wi = ss.p - cp;
             if (LengthSquared(wi) == 0) return false;
             wi = Normalize(wi);
@@ -2989,6 +3020,7 @@ PHD bool ShapeSampleSolidAngle(const DeviceShape &s, V3 cp, V3 cpErr, V3 cn, flo
         out->p = p;
         out->pErr = V3(0, 0, 0);
         out->pdf = pdf;
+        PatchST(s, su, sv, out->uv);
         return true;
     }
     if (s.kind == kShapeSphereT) {
@@ -3024,6 +3056,7 @@ PHD bool ShapeSampleSolidAngle(const DeviceShape &s, V3 cp, V3 cpErr, V3 cn, flo
             ToPoint3fi(p, gamma(5) * Abs(p), &out->p, &out->pErr);  // Interaction(Point3fi(p, pError))
             out->n = n;
             out->pdf = 1 / (2 * kPi * oneMinusCosThetaMax);
+            SphereUV(s, XfPt(s.r2o, p), out->uv);  // (*objectFromRender)(p)
             return true;
         }
     }

@@ -322,6 +322,7 @@ class Parser {
     ParamSet cameraParams, filmParams, samplerParams, integratorParams, filterParams;
     std::string cameraType = "perspective", filmType = "rgb";
     bool inWorld = false;
+    float curImageKe = 1;  // the current shape's image-emitter k_e factor (power normalisation)
     struct PendingShape {
         int kind = 0;                 // 0 triangle mesh, kShapeSphereT, kShapeDiskT, kShapeBilinearT
         std::vector<int> quadIdx;     // bilinear patches: 4 vertex indices each (p00 p10 p01 p11)
@@ -1437,7 +1438,7 @@ class Parser {
             l.twoSided = twoSided;
             l.area = ShapeArea(d);
             if (power > 0) {
-                float k_e = 1;
+                float k_e = curImageKe;  // an image emitter's mean luminance, else 1
                 k_e *= (twoSided ? 2 : 1) * l.area * kPi;
                 l.scale *= power / k_e;
             }
@@ -1519,7 +1520,7 @@ class Parser {
                 l.twoSided = twoSided;
                 l.area = area;
                 if (power > 0) {
-                    float k_e = 1;
+                    float k_e = curImageKe;  // an image emitter's mean luminance, else 1
                     k_e *= (twoSided ? 2 : 1) * l.area * kPi;
                     l.scale *= power / k_e;
                 }
@@ -2209,8 +2210,6 @@ void Parser::Finish() {
                     if (std::isnan(v)) throw Error(ap.loc + ": " + fn + ": image has not-a-number pixel values and so is not suitable as a light.");
                 }
                 if (im.nc < 3) throw Error(ap.loc + ": " + fn + ": Image provided to \"diffuse\" area light must have R, G, and B channels.");
-                if (s.kind == kShapeSphereT || s.kind == kShapeDiskT || s.kind == kShapeCylinderT || !s.quadIdx.empty())
-                    throw Error(ap.loc + ": image area lights on spheres, disks, cylinders and bilinear patches are not supported yet");
                 AreaLightImage ai;
                 ai.w = im.w;
                 ai.h = im.h;
@@ -2245,6 +2244,7 @@ void Parser::Finish() {
                 (s.kind == kShapeSphereT || s.kind == kShapeCylinderT || !s.quadIdx.empty()))
                 throw Error(s.loc + ": bump and normal mapping on spheres, cylinders and bilinear patches are not supported yet");
         }
+        curImageKe = imageKe;
         if (s.kind == kShapeSphereT || s.kind == kShapeDiskT || s.kind == kShapeCylinderT) {
             AnalyticShape(s, rfo, mat, lightSpectrum, lightScale, twoSided, power, mediumOf);
             continue;

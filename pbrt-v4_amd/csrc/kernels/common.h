@@ -1243,7 +1243,7 @@ __device__ inline float SpreadFactor(float tanE, float norm, V3 n, V3 wi) {
 __device__ __attribute__((noinline)) bool SampleShapeLi(const DeviceShape *shapes, const float *shapeN, int k,
                                                        bool twoSided, float scale, int spectrum, V3 cp, V3 cpErr, V3 n,
                                                        V3 ns, float u0, float u1, LiSample *ls, float cosE = -1,
-                                                       float tanE = 0, float spreadNorm = 0) {
+                                                       float tanE = 0, float spreadNorm = 0, float *uvOut = nullptr) {
     ShapeSamplePt ss;
     if (!ShapeSampleSolidAngle(shapes[k], cp, cpErr, n, u0, u1, &ss, shapeN + 12 * (size_t)k, ns) || ss.pdf == 0 ||
         LengthSquared(ss.p - cp) == 0)
@@ -1264,6 +1264,7 @@ __device__ __attribute__((noinline)) bool SampleShapeLi(const DeviceShape *shape
     ls->spectrum = spectrum;
     ls->delta = false;
     ls->envLe = false;
+    if (uvOut) uvOut[0] = ss.uv[0], uvOut[1] = ss.uv[1];
     return true;
 }
 // Ext: analytic-shape emitters and image infinite lights may be sampled (false: their branches
@@ -1274,10 +1275,18 @@ __device__ inline bool SampleLiSurface(const DeviceScene &S, const DeviceAreaLig
     if (li < S.nAreaLights) {
         const DeviceAreaLight &Ld = lightsL[li];
         if constexpr (!Lean && Ext) {
-            if (S.nShapes > 0 && __float_as_int(Ld.v0.w) >= S.nTris)
-                return SampleShapeLi(S.shapes, S.shapeN, __float_as_int(Ld.v0.w) - S.nTris, Ld.twoSided, Ld.scale,
-                                     Ld.spectrum, cp, cpErr, n, ns, u0, u1, ls, Ld.v1.w, Ld.v2.w,
-                                     Ld.v1.w > 0 ? S.lightSpreadNorm[li] : 0.f);
+            if (S.nShapes > 0 && __float_as_int(Ld.v0.w) >= S.nTris) {
+                float suv[2];
+                if (!SampleShapeLi(S.shapes, S.shapeN, __float_as_int(Ld.v0.w) - S.nTris, Ld.twoSided, Ld.scale,
+                                   Ld.spectrum, cp, cpErr, n, ns, u0, u1, ls, Ld.v1.w, Ld.v2.w,
+                                   Ld.v1.w > 0 ? S.lightSpreadNorm[li] : 0.f, suv))
+                    return false;
+                if (S.nImageAreaLights > 0 && S.lightImgOff[li] >= 0) {  // an image emitter at the sample's uv
+                    ls->envLe = true;
+                    ls->env = AreaImageCoef(S, S.lightImgOff[li], suv[0], suv[1]);
+                }
+                return true;
+            }
         }
         V3 q0(Ld.v0.x, Ld.v0.y, Ld.v0.z), q1(Ld.v1.x, Ld.v1.y, Ld.v1.z), q2(Ld.v2.x, Ld.v2.y, Ld.v2.z);
         TriShading lsh;

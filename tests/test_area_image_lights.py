@@ -3,11 +3,13 @@ an emitter's radiance is scale * RGBIlluminantSpectrum(ClampZero(image.Bilerp((u
 at the hit's uv for emission and at the light sample's uv (Triangle::Sample's barycentric uv)
 for light sampling; the light BVH's phi is the image's mean channel value.
 
-* Loader: the image, its errors (with "L", a grey image, non-triangle emitters); "power" normalises by the image's mean luminance (lights.cpp:943-965).
+* Loader: the image, its errors (with "L", a grey image); "power" normalises by the image's mean luminance (lights.cpp:943-965).
 * Known answers on the oracle: an all-white image emits "rgb L [1 1 1]" (the grey
   RGBIlluminantSpectrum is the illuminant itself) to the bilerp's last-bit rounding; a camera looking at a red-over-blue emitter
   sees red in the image's top half and blue in its bottom half (the v flip); a floor under a
   left-red / right-blue emitter is tinted accordingly on each side.
+* Emitters on spheres, disks, cylinders and bilinear patches (the uv of their hits and of their
+  shape samples): white image == "rgb L" [1 1 1] on the oracle; GPU film parity.
 * GPU film parity on an image emitter scene, on the surface and the volumetric path."""
 import numpy as np
 import pytest
@@ -61,11 +63,57 @@ def test_image_emitter_errors(pa, tmp_path, emitter, msg):
         scene(pa, tmp_path, emitter)
 
 
-def test_image_emitter_on_sphere_refused(pa, tmp_path):
-    png(tmp_path / "e.png", np.full((4, 4, 3), 200))
-    with pytest.raises(pa.PbrtError, match="spheres"):
-        pa.Scene.from_string('Camera "perspective"\nWorldBegin\nAttributeBegin\n'
-                             'AreaLightSource "diffuse" "string filename" "e.png"\nShape "sphere"\nAttributeEnd\n', tmp_path)
+SHAPES = {
+    "sphere": 'Translate 0 2 0\nShape "sphere" "float radius" 0.6',
+    "disk": 'Translate 0 2 0\nRotate 90 1 0 0\nShape "disk" "float radius" 0.9 "float innerradius" 0.2',
+    "cylinder": 'Translate 0 1.6 0\nRotate 90 1 0 0\nShape "cylinder" "float radius" 0.4 "float zmin" -0.5 "float zmax" 0.5',
+    "patch": 'Shape "bilinearmesh" "point3 P" [-1 2 -1  1 2 -1  -1 2 1  1 2 1] "point2 uv" [0 0 1 0 0 1 1 1]',
+}
+
+
+def shape_scene(pa, tmp_path, shape, emitter, extra="", spp=8, res=40):
+    text = (f'LookAt 0 3 -4  0 0.5 0  0 1 0\nCamera "perspective" "float fov" 60\n'
+            f'Film "rgb" "integer xresolution" {res} "integer yresolution" {res}\n'
+            f'Sampler "halton" "integer pixelsamples" {spp}\nIntegrator "volpath" "integer maxdepth" 3\n'
+            'WorldBegin\n' + extra +
+            'Material "diffuse" "rgb reflectance" [0.5 0.5 0.5]\n'
+            'Shape "trianglemesh" "integer indices" [0 1 2 0 2 3] "point3 P" [-6 0 -6 6 0 -6 6 0 6 -6 0 6]\n'
+            f'AttributeBegin\n{emitter}\n{SHAPES[shape]}\nAttributeEnd\n')
+    return pa.Scene.from_string(text, tmp_path)
+
+
+@pytest.mark.parametrize("shape", list(SHAPES))
+def test_white_image_on_shape_equals_rgb_emitter(pa, oracle, tmp_path, shape):
+    """an image emitter on a sphere, disk, cylinder or patch: the (u, v) of its hits and of its
+    light samples look the image up; an all-white image emits "rgb L" [1 1 1]"""
+    png(tmp_path / "w.png", np.full((8, 8, 3), 255))
+    a = shape_scene(pa, tmp_path, shape, 'AreaLightSource "diffuse" "string filename" "w.png" "float scale" 2')
+    b = shape_scene(pa, tmp_path, shape, 'AreaLightSource "diffuse" "rgb L" [1 1 1] "float scale" 2')
+    fa, fb = oracle.render(a, threads=8), oracle.render(b, threads=8)
+    assert fa[:3].sum() > 0
+    np.testing.assert_allclose(fa, fb, rtol=3e-6, atol=0)
+
+
+IMG_EXTRA = ('MakeNamedMedium "fog" "string type" "homogeneous" "rgb sigma_a" [0.1 0.1 0.1] "rgb sigma_s" [0.6 0.6 0.6]\n'
+             'AttributeBegin\nMediumInterface "fog" ""\nMaterial "interface"\nTranslate 1.6 0.6 0\n'
+             'Shape "sphere" "float radius" 0.5\nAttributeEnd\n')
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", list(SHAPES))
+@pytest.mark.parametrize("medium", [False, True])
+def test_image_on_shape_matches_oracle_gpu(pa, oracle, tmp_path, shape, medium):
+    from test_gpu_media import check, gpu_rgb, oracle_rgb
+    img = np.zeros((8, 8, 3))
+    img[:, :4, 0] = 255
+    img[:, 4:, 2] = 255
+    img[2:6, 2:6, 1] = 200
+    png(tmp_path / "e.png", img)
+    sc = shape_scene(pa, tmp_path, shape, 'AreaLightSource "diffuse" "string filename" "e.png" "float power" 30 '
+                                          '"bool twosided" true', extra=IMG_EXTRA if medium else "", spp=16)
+    a, _ = gpu_rgb(pa, oracle, sc)
+    frac, mr = check(a, oracle_rgb(oracle, sc))
+    print(f"image emitter on {shape} (medium={medium}): {frac*100:.2f}% pixels within 1e-3, mean rel {mr:.2e}")
 
 
 @pytest.mark.gpu

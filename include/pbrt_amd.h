@@ -261,6 +261,10 @@ typedef struct pbrt_scene_flat {
     /* PortalImageInfiniteLight: env_info[4k + 1] = 1 for a portal light, whose render-space
      * portal corners are env_portal [n_env][4][3] (zeros for the others) */
     const float *env_portal;
+    /* MeasuredMaterial (materials.h:925-967, type 10): material_layer[12 * m] = its BRDF index;
+     * measured_files [n_measured] the resolved RGL tensor files (".bsdf") */
+    int n_measured;
+    const char *const *measured_files;
 } pbrt_scene_flat;
 
 typedef struct pbrt_render_params {
@@ -450,6 +454,10 @@ int pbrt_debug_det_math(int device, int fn, const float *a, const float *b, int 
  * out[68] per query = {f(wo, wi)[31], PDF(wo, wi), Sample_f ok, wi[3], pdf, f[31]} (zeros when
  * BSDF::Sample_f returns {}).  On GPU `device`, or compiled for the host when device < 0. */
 int pbrt_debug_hair(int device, const float *in16, int n, float *out);
+/* MeasuredBxDF (bxdfs.cpp:1003-1124) on the host over a loaded scene's measured BRDF `brdf`:
+ * per query in8 {wo xyz, wi xyz, u0, u1} (local frame) at the 31 wavelengths `lambda`; out
+ * [n][68] = f(wo, wi)[31], PDF(wo, wi), Sample_f ok, wi xyz, pdf, f[31] */
+int pbrt_debug_measured(const pbrt_scene *scene, int brdf, const float *in8, int n, const float *lambda, float *out);
 /* The procedural textures' kernels code on the host (core/texture_eval.h): kind 0 FBm, 1
  * Turbulence (wrinkled), 2 windy, 3 InsidePolkaDot (in9[0..1] = s, t), 4 marble; params4 =
  * octaves, roughness, scale, variation; in9 per point = p, dpdx, dpdy; out6 per point = value

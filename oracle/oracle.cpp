@@ -28,7 +28,10 @@
 #include <atomic>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
+#include <map>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -3080,6 +3083,324 @@ struct Hair {
 };
 }  // namespace ohair
 
+// ---- MeasuredBxDF (bxdfs.h:1154-1204, bxdfs.cpp:690-1124) and PiecewiseLinear2D
+// (util/sampling.h:1264-1749), restated over the oracle's own reader of the RGL tensor file
+namespace omeas {
+// one PiecewiseLinear2D<D>: resolution, parameter grids, per-slice tables
+struct Table {
+    int nx = 0, ny = 0, D = 0;
+    std::vector<float> params[3];
+    uint32_t strides[3] = {0, 0, 0};
+    std::vector<float> data, marginal, conditional;
+
+    void Build(const float *in, int xSize, int ySize, int dims, const std::vector<float> *pv, bool normalize,
+               bool cdf) {
+        nx = xSize, ny = ySize, D = dims;
+        uint32_t slices = 1;
+        for (int i = D - 1; i >= 0; --i) {
+            params[i] = pv[i];
+            strides[i] = pv[i].size() > 1 ? slices : 0;
+            slices *= (uint32_t)pv[i].size();
+        }
+        const size_t n = (size_t)nx * ny;
+        data.resize(slices * n);
+        if (cdf) {
+            marginal.resize((size_t)slices * ny);
+            conditional.resize(slices * n);
+        }
+        for (uint32_t s = 0; s < slices; ++s) {
+            const float *d = in + s * n;
+            float *o = data.data() + s * n;
+            if (cdf) {
+                float *cc = conditional.data() + s * n, *mc = marginal.data() + (size_t)s * ny;
+                for (int y = 0; y < ny; ++y) {
+                    double acc = 0;
+                    cc[(size_t)y * nx] = 0;
+                    for (int x = 0; x + 1 < nx; ++x) {
+                        const size_t i = (size_t)y * nx + x;
+                        acc += .5 * ((double)d[i] + (double)d[i + 1]);
+                        cc[i + 1] = (float)acc;
+                    }
+                }
+                double acc = 0;
+                mc[0] = 0;
+                for (int y = 0; y + 1 < ny; ++y) {
+                    acc += .5 * ((double)cc[(size_t)(y + 1) * nx - 1] + (double)cc[(size_t)(y + 2) * nx - 1]);
+                    mc[y + 1] = (float)acc;
+                }
+                const float norm = 1.f / mc[ny - 1];
+                for (size_t i = 0; i < n; ++i) cc[i] *= norm;
+                for (int i = 0; i < ny; ++i) mc[i] *= norm;
+                for (size_t i = 0; i < n; ++i) o[i] = d[i] * norm;
+            } else {
+                float norm = 1.f / ((float)(nx - 1) * (float)(ny - 1));
+                if (normalize) {
+                    double acc = 0;
+                    for (int y = 0; y + 1 < ny; ++y)
+                        for (int x = 0; x + 1 < nx; ++x) {
+                            const size_t i = (size_t)y * nx + x;
+                            acc += (double)(.25f * (d[i] + d[i + 1] + d[i + nx] + d[i + 1 + nx]));
+                        }
+                    norm = float(1.0 / acc);
+                }
+                for (size_t i = 0; i < n; ++i) o[i] = d[i] * norm;
+            }
+        }
+    }
+    // parameter weights (the loop heading Sample / Invert / Evaluate)
+    uint32_t Weights(const Float *param, Float *w) const {
+        uint32_t slice = 0;
+        for (int k = 0; k < D; ++k) {
+            const int np = (int)params[k].size();
+            if (np == 1) {
+                w[2 * k] = 1, w[2 * k + 1] = 0;
+                continue;
+            }
+            // FindInterval(np, params[k][i] <= param[k])
+            int lo = 0, hi = np - 2;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) / 2;
+                if (params[k][mid] <= param[k]) lo = mid;
+                else hi = mid - 1;
+            }
+            const Float p0 = params[k][lo], p1 = params[k][lo + 1];
+            w[2 * k + 1] = Clamp((param[k] - p0) / (p1 - p0), 0, 1);
+            w[2 * k] = 1 - w[2 * k + 1];
+            slice += strides[k] * (uint32_t)lo;
+        }
+        return slice;
+    }
+    // lookup<Dim>: nested blend, the last parameter outermost
+    Float At(const float *t, uint32_t i, uint32_t size, const Float *w, int dim) const {
+        if (dim == 0) return t[i];
+        const Float v0 = At(t, i, size, w, dim - 1), v1 = At(t, i + strides[dim - 1] * size, size, w, dim - 1);
+        return std::fma(v0, w[2 * dim - 2], v1 * w[2 * dim - 1]);
+    }
+    Float Evaluate(Float x, Float y, const Float *param) const {
+        Float w[6];
+        const uint32_t slice = Weights(param, w);
+        x *= (Float)(nx - 1);
+        y *= (Float)(ny - 1);
+        const int ix = std::min((int)x, nx - 2), iy = std::min((int)y, ny - 2);
+        const Float fx = x - (Float)ix, fy = y - (Float)iy, gx = 1 - fx, gy = 1 - fy;
+        const uint32_t size = (uint32_t)(nx * ny), i = (uint32_t)(ix + iy * nx) + (D ? slice * size : 0);
+        const float *t = data.data();
+        const Float v00 = At(t, i, size, w, D), v10 = At(t + 1, i, size, w, D), v01 = At(t + nx, i, size, w, D),
+                    v11 = At(t + nx + 1, i, size, w, D);
+        return std::fma(gy, std::fma(gx, v00, fx * v10), fy * std::fma(gx, v01, fx * v11)) *
+               ((Float)(nx - 1) * (Float)(ny - 1));
+    }
+    void Invert(Float x, Float y, const Float *param, Float *ox, Float *oy, Float *pdf) const {
+        Float w[6];
+        const uint32_t slice = Weights(param, w);
+        x *= (Float)(nx - 1);
+        y *= (Float)(ny - 1);
+        const int ix = std::min((int)x, nx - 2), iy = std::min((int)y, ny - 2);
+        x -= (Float)ix;
+        y -= (Float)iy;
+        const uint32_t size = (uint32_t)(nx * ny), base = D ? slice * size : 0;
+        uint32_t i = (uint32_t)(ix + iy * nx) + base;
+        const float *t = data.data(), *c = conditional.data();
+        const Float v00 = At(t, i, size, w, D), v10 = At(t + 1, i, size, w, D), v01 = At(t + nx, i, size, w, D),
+                    v11 = At(t + nx + 1, i, size, w, D);
+        const Float c0 = std::fma(1 - y, v00, y * v01), c1 = std::fma(1 - y, v10, y * v11);
+        *pdf = std::fma(1 - x, c0, x * c1) * ((Float)(nx - 1) * (Float)(ny - 1));
+        x *= c0 + .5f * x * (c1 - c0);
+        x += (1.f - y) * At(c, i, size, w, D) + y * At(c + nx, i, size, w, D);
+        i = (uint32_t)(iy * nx) + base;
+        const Float r0 = At(c, i + nx - 1, size, w, D), r1 = At(c, i + (2 * nx - 1), size, w, D);
+        x /= (1.f - y) * r0 + y * r1;
+        y *= r0 + .5f * y * (r1 - r0);
+        y += At(marginal.data(), (uint32_t)iy + (D ? slice * (uint32_t)ny : 0), (uint32_t)ny, w, D);
+        *ox = x, *oy = y;
+    }
+    void Sample(Float x, Float y, const Float *param, Float *ox, Float *oy, Float *pdf) const {
+        x = Clamp(x, 1 - OneMinusEpsilon, OneMinusEpsilon);
+        y = Clamp(y, 1 - OneMinusEpsilon, OneMinusEpsilon);
+        Float w[6];
+        const uint32_t slice = Weights(param, w);
+        const float *c = conditional.data(), *t = data.data();
+        const uint32_t mbase = D ? slice * (uint32_t)ny : 0;
+        // FindInterval over the marginal: last row whose CDF is below y
+        int lo = 0, hi = ny - 2;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) / 2;
+            if (At(marginal.data(), mbase + mid, (uint32_t)ny, w, D) < y) lo = mid;
+            else hi = mid - 1;
+        }
+        const int row = lo;
+        y -= At(marginal.data(), mbase + row, (uint32_t)ny, w, D);
+        const uint32_t size = (uint32_t)(nx * ny);
+        uint32_t off = (uint32_t)(row * nx) + (D ? slice * size : 0);
+        const Float r0 = At(c, off + nx - 1, size, w, D), r1 = At(c, off + (2 * nx - 1), size, w, D);
+        bool flat = std::abs(r0 - r1) < 1e-4f * (r0 + r1);
+        y = flat ? (2.f * y) : (r0 - std::sqrt(std::max<Float>(0, r0 * r0 - 2.f * y * (r0 - r1))));
+        y /= flat ? (r0 + r1) : (r0 - r1);
+        x *= (1.f - y) * r0 + y * r1;
+        auto cond = [&](int k) { return (1.f - y) * At(c, off + k, size, w, D) + y * At(c + nx, off + k, size, w, D); };
+        lo = 0, hi = nx - 2;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) / 2;
+            if (cond(mid) < x) lo = mid;
+            else hi = mid - 1;
+        }
+        const int col = lo;
+        x -= cond(col);
+        off += (uint32_t)col;
+        const Float v00 = At(t, off, size, w, D), v10 = At(t + 1, off, size, w, D), v01 = At(t + nx, off, size, w, D),
+                    v11 = At(t + nx + 1, off, size, w, D);
+        const Float c0 = std::fma(1.f - y, v00, y * v01), c1 = std::fma(1.f - y, v10, y * v11);
+        flat = std::abs(c0 - c1) < 1e-4f * (c0 + c1);
+        x = flat ? (2.f * x) : (c0 - std::sqrt(std::max<Float>(0, c0 * c0 - 2.f * x * (c0 - c1))));
+        x /= flat ? (c0 + c1) : (c0 - c1);
+        *ox = ((Float)col + x) * (1.f / (Float)(nx - 1));
+        *oy = ((Float)row + y) * (1.f / (Float)(ny - 1));
+        *pdf = ((1.f - x) * c0 + x * c1) * ((Float)(nx - 1) * (Float)(ny - 1));
+    }
+};
+
+struct Brdf {
+    bool isotropic = true;
+    Table ndf, sigma, vndf, luminance, spectra;
+};
+
+// the tensor file (bxdfs.cpp:734-816): "tensor_file\0", version 1.0, fields {name, ndim, dtype,
+// offset, shape}; only what MeasuredBxDFData::Create reads
+static bool Load(const char *path, Brdf *b) {
+    FILE *fp = std::fopen(path, "rb");
+    if (!fp) return false;
+    std::vector<uint8_t> bytes;
+    uint8_t buf[65536];
+    size_t got;
+    while ((got = std::fread(buf, 1, sizeof(buf), fp)) > 0) bytes.insert(bytes.end(), buf, buf + got);
+    std::fclose(fp);
+    if (bytes.size() < 18 || std::memcmp(bytes.data(), "tensor_file", 12) != 0) return false;
+    size_t pos = 14;
+    auto rd = [&](void *dst, size_t n) {
+        std::memcpy(dst, bytes.data() + pos, n);
+        pos += n;
+    };
+    uint32_t nf;
+    rd(&nf, 4);
+    struct F {
+        std::vector<size_t> shape;
+        const float *p;
+    };
+    std::map<std::string, F> fs;
+    for (uint32_t k = 0; k < nf; ++k) {
+        uint16_t len, nd;
+        uint8_t dt;
+        uint64_t off;
+        rd(&len, 2);
+        std::string name((const char *)bytes.data() + pos, len);
+        pos += len;
+        rd(&nd, 2);
+        rd(&dt, 1);
+        rd(&off, 8);
+        F f;
+        for (int j = 0; j < nd; ++j) {
+            uint64_t v;
+            rd(&v, 8);
+            f.shape.push_back((size_t)v);
+        }
+        f.p = (const float *)(bytes.data() + off);
+        fs[name] = f;
+    }
+    const F &phi = fs["phi_i"], &theta = fs["theta_i"], &wl = fs["wavelengths"];
+    std::vector<float> pv[3] = {std::vector<float>(phi.p, phi.p + phi.shape[0]),
+                                std::vector<float>(theta.p, theta.p + theta.shape[0]),
+                                std::vector<float>(wl.p, wl.p + wl.shape[0])};
+    b->isotropic = phi.shape[0] <= 2;
+    const F &nd = fs["ndf"], &sg = fs["sigma"], &vn = fs["vndf"], &lu = fs["luminance"], &sp = fs["spectra"];
+    b->ndf.Build(nd.p, (int)nd.shape[1], (int)nd.shape[0], 0, pv, false, false);
+    b->sigma.Build(sg.p, (int)sg.shape[1], (int)sg.shape[0], 0, pv, false, false);
+    b->vndf.Build(vn.p, (int)vn.shape[3], (int)vn.shape[2], 2, pv, true, true);
+    b->luminance.Build(lu.p, (int)lu.shape[3], (int)lu.shape[2], 2, pv, true, true);
+    b->spectra.Build(sp.p, (int)sp.shape[4], (int)sp.shape[3], 3, pv, false, false);
+    return true;
+}
+
+static inline Float Theta2u(Float t) { return std::sqrt(t * (2 / Pi)); }
+static inline Float Phi2u(Float p) { return p * (1 / (2 * Pi)) + .5f; }
+
+struct Measured {
+    const Brdf *b = nullptr;
+    Spectrum lambda;
+
+    Spectrum Fr(Float ux, Float uy, Float phi_o, Float theta_o) const {
+        Spectrum fr;
+        for (int i = 0; i < NS; ++i) {
+            const Float par[3] = {phi_o, theta_o, lambda[i]};
+            fr[i] = std::max<Float>(0, b->spectra.Evaluate(ux, uy, par));
+        }
+        return fr;
+    }
+    Spectrum f(Vec wo, Vec wi) const {
+        if (!SameHemisphere(wo, wi)) return Spectrum(0.f);
+        if (wo.z < 0) wo = -wo, wi = -wi;
+        Vec wm = wi + wo;
+        if (LengthSquared(wm) == 0) return Spectrum(0.f);
+        wm = Normalize(wm);
+        const Float theta_o = SafeACos(wo.z), phi_o = CRATan2(wo.y, wo.x);
+        const Float theta_m = SafeACos(wm.z), phi_m = CRATan2(wm.y, wm.x);
+        const Float uo[2] = {Theta2u(theta_o), Phi2u(phi_o)};
+        Float um[2] = {Theta2u(theta_m), Phi2u(b->isotropic ? (phi_m - phi_o) : phi_m)};
+        um[1] = um[1] - std::floor(um[1]);
+        const Float par[2] = {phi_o, theta_o};
+        Float ux, uy, unused;
+        b->vndf.Invert(um[0], um[1], par, &ux, &uy, &unused);
+        Spectrum fr = Fr(ux, uy, phi_o, theta_o);
+        const Float n = b->ndf.Evaluate(um[0], um[1], nullptr);
+        const Float den = 4 * b->sigma.Evaluate(uo[0], uo[1], nullptr) * wi.z;
+        for (int i = 0; i < NS; ++i) fr[i] = fr[i] * n / den;
+        return fr;
+    }
+    bool Sample_f(Vec wo, Float u0, Float u1, BSDFSample *bs) const {
+        bool flip = false;
+        if (wo.z <= 0) wo = -wo, flip = true;
+        const Float theta_o = SafeACos(wo.z), phi_o = CRATan2(wo.y, wo.x);
+        const Float par[2] = {phi_o, theta_o};
+        Float ux, uy, lumPdf, mx, my, pdf;
+        b->luminance.Sample(u0, u1, par, &ux, &uy, &lumPdf);
+        b->vndf.Sample(ux, uy, par, &mx, &my, &pdf);
+        Float phi_m = (2.f * my - 1.f) * Pi;
+        const Float theta_m = Sqr(mx) * (Pi / 2.f);
+        if (b->isotropic) phi_m += phi_o;
+        const Float sinTheta_m = CRSin(theta_m), cosTheta_m = CRCos(theta_m);
+        const Float st = Clamp(sinTheta_m, -1, 1);
+        const Vec wm(st * CRCos(phi_m), st * CRSin(phi_m), Clamp(cosTheta_m, -1, 1));
+        Vec wi = Reflect(wo, wm);
+        if (wi.z <= 0) return false;
+        Spectrum fr = Fr(ux, uy, phi_o, theta_o);
+        const Float s = b->ndf.Evaluate(mx, my, nullptr) /
+                        (4 * b->sigma.Evaluate(Theta2u(theta_o), Phi2u(phi_o), nullptr) * std::abs(wi.z));
+        for (int i = 0; i < NS; ++i) fr[i] *= s;
+        pdf /= 4 * Dot(wo, wm) * std::max<Float>(2 * Sqr(Pi) * mx * sinTheta_m, 1e-6f);
+        if (flip) wi = -wi;
+        *bs = BSDFSample{fr, wi, pdf * lumPdf, BxR | BxGlossy, 1};
+        return true;
+    }
+    Float PDF(Vec wo, Vec wi) const {
+        if (!SameHemisphere(wo, wi)) return 0;
+        if (wo.z < 0) wo = -wo, wi = -wi;
+        Vec wm = wi + wo;
+        if (LengthSquared(wm) == 0) return 0;
+        wm = Normalize(wm);
+        const Float theta_o = SafeACos(wo.z), phi_o = CRATan2(wo.y, wo.x);
+        const Float theta_m = SafeACos(wm.z), phi_m = CRATan2(wm.y, wm.x);
+        Float um[2] = {Theta2u(theta_m), Phi2u(b->isotropic ? (phi_m - phi_o) : phi_m)};
+        um[1] = um[1] - std::floor(um[1]);
+        const Float par[2] = {phi_o, theta_o};
+        Float sx, sy, vndfPdf;
+        b->vndf.Invert(um[0], um[1], par, &sx, &sy, &vndfPdf);
+        const Float pdf = b->luminance.Evaluate(sx, sy, par);
+        const Float sinTheta_m = std::sqrt(Sqr(wm.x) + Sqr(wm.y));
+        const Float jac = 4.f * Dot(wo, wm) * std::max<Float>(2 * Sqr(Pi) * um[0] * sinTheta_m, 1e-6f);
+        return vndfPdf * pdf / jac;
+    }
+};
+}  // namespace omeas
+
 struct BxDF {
     int type = 0;  // 0 diffuse, 1 dielectric, 2 conductor, 6 thin dielectric, 7 diffuse transmission, 9 hair
     Spectrum R, Tt;  // Tt: DiffuseTransmissionBxDF's T
@@ -3087,9 +3408,10 @@ struct BxDF {
     TRDistribution mf;
     Spectrum etaS, kS;
     ohair::Hair hair;
+    omeas::Measured meas;  // type 10
 
     int Flags() const {
-        if (type == 9) return BxR | BxGlossy;  // HairBxDF::Flags (bxdfs.h:1079)
+        if (type == 9 || type == 10) return BxR | BxGlossy;  // MeasuredBxDF::Flags (bxdfs.h:1176)  // HairBxDF::Flags (bxdfs.h:1079)
         if (type == 0) return R ? (BxR | BxDiffuse) : 0;
         if (type == 6) return BxR | BxT | BxSpecular;  // ThinDielectricBxDF
         if (type == 7) return (R ? (BxR | BxDiffuse) : 0) | (Tt ? (BxT | BxDiffuse) : 0);
@@ -3104,6 +3426,7 @@ struct BxDF {
     }
     bool Sample_f(Vec wo, Float uc, Float u0, Float u1, BSDFSample *bs, bool radiance = true, int sf = 3) const {
         if (type == 9) return hair.Sample_f(wo, uc, u0, u1, bs);
+        if (type == 10) return (sf & 1) && meas.Sample_f(wo, u0, u1, bs);
         if (type == 7) {
             // DiffuseTransmissionBxDF::Sample_f (bxdfs.h:231-260)
             Float pr = (sf & 1) ? R.Max() : 0, pt = (sf & 2) ? Tt.Max() : 0;
@@ -3217,6 +3540,7 @@ struct BxDF {
     }
     Spectrum f(Vec wo, Vec wi, bool radiance = true) const {
         if (type == 9) return hair.f(wo, wi);
+        if (type == 10) return meas.f(wo, wi);
         if (type == 6) return Spectrum(0.f);
         if (type == 7) return SameHemisphere(wo, wi) ? R * InvPi : Tt * InvPi;
         if (type == 0) return SameHemisphere(wo, wi) ? R * InvPi : Spectrum(0.f);
@@ -3244,6 +3568,7 @@ struct BxDF {
     }
     Float PDF(Vec wo, Vec wi, int sf = 3) const {
         if (type == 9) return hair.PDF(wo, wi);
+        if (type == 10) return (sf & 1) ? meas.PDF(wo, wi) : 0;
         if (type == 6) return 0;
         if (type == 7) {
             Float pr = (sf & 1) ? R.Max() : 0, pt = (sf & 2) ? Tt.Max() : 0;
@@ -5593,6 +5918,7 @@ struct Renderer {
     PixelFilter filt;
     const pbrt_scene_flat *f;
     std::vector<std::vector<float>> sssTables;  // osss::Table(g, eta) per subsurface material
+    std::vector<omeas::Brdf> measured;          // flat measured_files, read by the oracle itself
 
     // TraceTransmittance (wavefront/intersect.h:164-274) up to the light point o + tMax d:
     // closest hits; a non-interface surface blocks (T_ray = 0); interfaces are crossed with
@@ -5906,6 +6232,10 @@ struct Renderer {
                 }
             }
             bx.hair.Init(-1 + 2 * si.uv[1], e, sig, bm, bn, a);
+        } else if (bx.type == 10) {
+            // MeasuredMaterial::GetBxDF (materials.h:931-934): material_layer[0] = the BRDF
+            bx.meas.b = &measured[(int)f->material_layer[12 * mat]];
+            for (int i = 0; i < NS; ++i) bx.meas.lambda[i] = lambda.lambda[i];
         } else if (bx.type == 7) {
             // DiffuseTransmissionMaterial::GetBxDF (materials.h): Clamp(scale * R | T, 0, 1)
             const float *ml = f->material_layer + 12 * mat;
@@ -6790,6 +7120,33 @@ void oracle_hair_eval(const float *in, int n, float *out) {
         }
     }
 }
+// the oracle's MeasuredBxDF (omeas) read from `path`, on queries laid out as pbrt_debug_measured's:
+// in[8] {wo, wi, u0, u1} at the wavelengths lambda[NS] -> out[68] {f[NS], PDF, ok, wi, pdf, f[NS]}
+int oracle_measured_eval(const char *path, const float *in, int n, const float *lambda, float *out) {
+    omeas::Brdf b;
+    if (!omeas::Load(path, &b)) return -1;
+    omeas::Measured m;
+    m.b = &b;
+    for (int i = 0; i < NS; ++i) m.lambda[i] = lambda[i];
+    for (int k = 0; k < n; ++k) {
+        const float *q = in + 8 * k;
+        float *o = out + (2 * NS + 6) * k;
+        const Vec wo(q[0], q[1], q[2]), wi(q[3], q[4], q[5]);
+        const Spectrum fv = m.f(wo, wi);
+        for (int i = 0; i < NS; ++i) o[i] = fv[i];
+        o[NS] = m.PDF(wo, wi);
+        float *s = o + NS + 1;
+        std::fill(s, s + 5 + NS, 0.f);
+        BSDFSample bs;
+        if (m.Sample_f(wo, q[6], q[7], &bs)) {
+            s[0] = 1;
+            s[1] = bs.wi.x, s[2] = bs.wi.y, s[3] = bs.wi.z;
+            s[4] = bs.pdf;
+            for (int i = 0; i < NS; ++i) s[5 + i] = bs.f[i];
+        }
+    }
+    return 0;
+}
 // the oracle's own BSSRDF table for (g, eta) (osss::Table), kSssTableFloats floats
 void oracle_sss_table(float g, float eta, float *out) {
     const std::vector<float> t = osss::Table(g, eta);
@@ -6901,6 +7258,9 @@ static int RenderRows(const pbrt_scene_flat *flat, const pbrt_scene_info *info, 
     r.M.f = flat;
     r.M.n = flat->n_media;
     r.filt.Init(flat->filter_type, info->filter_radius_x, info->filter_radius_y, flat->filter_a, flat->filter_b);
+    r.measured.resize(flat->n_measured);
+    for (int k = 0; k < flat->n_measured; ++k)
+        if (!omeas::Load(flat->measured_files[k], &r.measured[k])) std::fprintf(stderr, "oracle: cannot read %s\n", flat->measured_files[k]);
     for (int k = 0; k < flat->n_sss; ++k) r.sssTables.push_back(osss::Table(flat->sss_params[20 * k + 18], flat->sss_params[20 * k + 2]));
     hostMath.Done();
     size_t npix = (size_t)info->xres * info->yres;

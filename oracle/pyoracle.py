@@ -49,6 +49,7 @@ def lib():
         _lib.oracle_bxdf.argtypes = [ctypes.c_int] + [vp] * 7
         _lib.oracle_layered.argtypes = [vp] * 8
         _lib.oracle_hair_eval.argtypes = [vp, ctypes.c_int, vp]
+        _lib.oracle_measured_eval.argtypes = [ctypes.c_char_p, vp, ctypes.c_int, vp, vp]
         _lib.oracle_portal_eval.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, vp, vp]
         _lib.oracle_triangle_shading.argtypes = [vp] * 3 + [ctypes.c_int] + [vp] * 3
         _lib.oracle_render.argtypes = [vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -427,6 +428,17 @@ def hair_eval(queries):
     q = np.ascontiguousarray(queries, np.float32).reshape(-1, 16)
     out = np.zeros((len(q), 68), np.float32)
     lib().oracle_hair_eval(q.ctypes.data, len(q), out.ctypes.data)
+    return out
+
+
+def measured_eval(path, queries, lambdas):
+    """The oracle's MeasuredBxDF read from the tensor file `path` (its own reader and
+    PiecewiseLinear2D) on [n][8] queries {wo, wi, u0, u1} -> [n][68], in the current math mode."""
+    q = np.ascontiguousarray(queries, np.float32).reshape(-1, 8)
+    lam = np.ascontiguousarray(lambdas, np.float32).reshape(31)
+    out = np.zeros((len(q), 68), np.float32)
+    if lib().oracle_measured_eval(str(path).encode(), q.ctypes.data, len(q), lam.ctypes.data, out.ctypes.data) != 0:
+        raise OSError(f"oracle: cannot read {path}")
     return out
 
 

@@ -14,6 +14,7 @@
 #include "../../include/pbrt_amd.h"
 #include "core/bssrdf.h"
 #include "core/hair.h"
+#include "core/measured.h"
 #include "host/bvh.h"
 #include "host/image.h"
 #include "host/scene.h"
@@ -319,6 +320,7 @@ struct pbrt_scene {
     std::vector<int32_t> infImage, envInfo, shapeInfo, primAlpha;
     std::vector<float> shapeParams, shapeNormals;
     std::vector<float> envXform, envRgb, envPortal;
+    mutable std::vector<const char *> measuredFiles;
     std::vector<uint64_t> envOffset;
     TexTables tex;
     void Flatten() {
@@ -370,6 +372,7 @@ struct pbrt_scene {
         matLayer.clear();
         for (auto &m : s.materials) {
             if (m.type == kMatHair) HairLayer(m, &matLayer);
+            else if (m.type == kMatMeasured) matLayer.insert(matLayer.end(), {(float)m.measured, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0});
             else
                 matLayer.insert(matLayer.end(), {m.thickness, m.g, (float)m.maxDepth, (float)m.nSamples, m.a0, m.a1, m.a2,
                                                  m.albedoValue, m.albedoConstant ? 1.f : 0.f, m.cAlphaX, m.cAlphaY,
@@ -542,6 +545,8 @@ struct pbrt_context {
     DevBuf<float> envDist;
     DevBuf<DeviceEnvLight> envLights;
     DevBuf<float> portalTab;  // portal lights: SummedAreaTable values then function, per light
+    DevBuf<int> measHdr;      // measured BRDFs: headers, then their tables
+    DevBuf<float> measData;
     DevBuf<int> queueHoles;       // VolState::holes
     DevBuf<int> matMix, hitMat;   // mix materials: {m0, m1, amount program} and resolved materials
     bool hasMix = false;
@@ -830,6 +835,10 @@ static void BuildDevice(pbrt_context *c) {
                 HairLayer(m, &ml);
                 continue;
             }
+            if (m.type == kMatMeasured) {  // the BRDF's index; its tables are measHdr / measData
+                ml.insert(ml.end(), {(float)m.measured, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0});
+                continue;
+            }
             // grey layer albedo uploaded as a constant (same bits, as the reflectances above)
             const bool grey = !m.albedoConstant && m.a0 == 0 && m.a1 == 0;
             const float av = grey ? SigmoidPolynomial(0.f, 0.f, m.a2, 500.f) : m.albedoValue;
@@ -837,6 +846,20 @@ static void BuildDevice(pbrt_context *c) {
                                  (m.albedoConstant || grey) ? 1.f : 0.f, m.cAlphaX, m.cAlphaY, (float)m.ifaceEtaSpec});
         }
         c->matLayer.Upload(ml);
+        {
+            std::vector<int> mh;
+            std::vector<float> md;
+            for (const MeasuredDesc &b : s.measured) {
+                std::vector<int> h = b.hdr;
+                if (md.size() > (size_t)INT32_MAX - b.blob.size()) throw Error("measured BRDFs too large");
+                h[7] = (int)md.size();
+                mh.insert(mh.end(), h.begin(), h.end());
+                md.insert(md.end(), b.blob.begin(), b.blob.end());
+            }
+            if (mh.empty()) mh.assign(kMeasHdr, 0), md.push_back(0.f);
+            c->measHdr.Upload(mh);
+            c->measData.Upload(md);
+        }
         {
             std::vector<int32_t> ms;
             std::vector<float> sp, stb;
@@ -1117,7 +1140,8 @@ static void BuildDevice(pbrt_context *c) {
     c->volumetric = !s.media.empty() ||
                     std::any_of(s.materials.begin(), s.materials.end(), [](const MaterialDesc &m) {
                         return m.type == kMatInterface || m.type == kMatCoatedDiffuse || m.type == kMatCoatedConductor ||
-                               m.type == kMatThinDielectric || m.type == kMatDiffuseTransmission || m.type == kMatHair;
+                               m.type == kMatThinDielectric || m.type == kMatDiffuseTransmission || m.type == kMatHair ||
+                               m.type == kMatMeasured;
                     });
     S.dispersive = std::any_of(s.materials.begin(), s.materials.end(),
                                [](const MaterialDesc &m) { return ((m.type == kMatDielectric || m.type == kMatThinDielectric) && m.etaSpec >= 0) || m.ifaceEtaSpec >= 0;
@@ -1166,6 +1190,8 @@ static void BuildDevice(pbrt_context *c) {
     S.shapeN = c->shapeN.p;
     S.triShade = (const float4 *)c->triShade.p;
     S.triTangent = (const float4 *)c->triTangent.p;
+    S.measHdr = c->measHdr.p;
+    S.measData = c->measData.p;
     S.matCoeffs = (const float4 *)c->matCoeffs.p;
     S.matConstant = c->matConstant.p;
     S.nMaterials = (int)s.materials.size();
@@ -1230,7 +1256,8 @@ static void BuildDevice(pbrt_context *c) {
             if (c->volumetric)
                 for (const MaterialDesc &m : s.materials)
                     if ((m.texDisp >= 0 || m.normalMap >= 0) &&
-                        (m.type == kMatCoatedDiffuse || m.type == kMatCoatedConductor || m.type == kMatDiffuseTransmission))
+                        (m.type == kMatCoatedDiffuse || m.type == kMatCoatedConductor || m.type == kMatDiffuseTransmission ||
+                         m.type == kMatMeasured))
                         throw Error("bump or normal mapping on layered or diffuse transmission materials together with "
                                     "the volumetric path is not supported yet");
             c->texNodes.Upload(tt.nodes);
@@ -2128,6 +2155,10 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
     f->vertex_s = s.vertS.empty() ? nullptr : &s.vertS[0].x;
     f->n_vertex_s = (int)s.vertS.size();
     f->env_portal = scene->envPortal.empty() ? nullptr : scene->envPortal.data();
+    scene->measuredFiles.clear();
+    for (const MeasuredDesc &b : s.measured) scene->measuredFiles.push_back(b.path.c_str());
+    f->n_measured = (int)s.measured.size();
+    f->measured_files = s.measured.empty() ? nullptr : scene->measuredFiles.data();
     f->dims_per_depth = s.sss.empty() ? 7 : 10;
     f->material_params = scene->matParams.data();
     f->material_layer = scene->matLayer.data();
@@ -2660,6 +2691,19 @@ int pbrt_debug_texture_eval(const pbrt_scene *scene, int material, int slot, con
         }
         for (int i = 0; i < n; ++i)
             out[4 + i] = pg.simple ? SigmoidPolynomial(R[0], R[1], R[2], lambda[i]) : TexPhase2(T, pg, R, lambda[i]);
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_debug_measured(const pbrt_scene *scene, int brdf, const float *in8, int n, const float *lambda, float *out) {
+    try {
+        if (!scene || !in8 || !lambda || !out || n < 0) return Fail("pbrt_debug_measured: bad arguments");
+        const SceneDesc &s = scene->desc;
+        if (brdf < 0 || brdf >= (int)s.measured.size()) return Fail("pbrt_debug_measured: not a measured BRDF index");
+        const MeasuredView m = MeasuredAt(s.measured[brdf].hdr.data(), s.measured[brdf].blob.data());
+        for (int i = 0; i < n; ++i) MeasuredDebugEval(m, in8 + (size_t)kMeasDebugIn * i, lambda, out + (size_t)kMeasDebugOut * i);
         return 0;
     } catch (const std::exception &e) {
         return Fail(e.what());

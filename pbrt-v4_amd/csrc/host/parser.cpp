@@ -858,6 +858,23 @@ class Parser {
             if (Param *b = ps.Find("beta_m")) m.hairBetaM = constFloat(b);
             if (Param *b = ps.Find("beta_n")) m.hairBetaN = constFloat(b);
             if (Param *a = ps.Find("alpha")) m.hairAlpha = constFloat(a);
+        } else if (type == "measured") {
+            // MeasuredMaterial::Create (materials.cpp:644-667): the resolved "filename", each
+            // file read once (MeasuredBxDF::BRDFDataFromFile's cache, bxdfs.cpp:995-1001)
+            m.type = kMatMeasured;
+            const std::string f = ps.GetString("filename", "");
+            if (f.empty()) throw Error(ps.loc + ": Filename must be provided for MeasuredMaterial");
+            const std::string path = (f[0] == '/') ? f : (dir.empty() ? f : dir + "/" + f);
+            for (size_t k = 0; k < scene.measured.size() && m.measured < 0; ++k)
+                if (scene.measured[k].path == path) m.measured = (int)k;
+            if (m.measured < 0) {
+                try {
+                    scene.measured.push_back(LoadMeasuredBRDF(path));
+                } catch (const std::exception &e) {
+                    throw Error(ps.loc + ": " + e.what());
+                }
+                m.measured = (int)scene.measured.size() - 1;
+            }
         } else if (type == "diffusetransmission") {
             // DiffuseTransmissionMaterial::Create (materials.cpp:620-645): reflectance and
             // transmittance default 0.25, scale 1; the transmittance rides in the albedo fields

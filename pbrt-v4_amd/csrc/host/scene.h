@@ -42,6 +42,7 @@ constexpr int kMatDiffuseTransmission = 7;  // DiffuseTransmissionBxDF (bxdfs.h:
 constexpr int kMatMix = 8;
 // HairMaterial (materials.h:353-427): HairBxDF (bxdfs.h:1054-1152), k_vlayered
 constexpr int kMatHair = 9;
+constexpr int kMatMeasured = 10;
 
 // Participating media (media.h:209-350, media.cpp:167-330).  Spectra are DenselySampled
 // 395..705 nm tables in SceneDesc::denseSpectra with pbrt's constructor scaling applied
@@ -118,6 +119,7 @@ struct MaterialDesc {
     int hairMode = 0;
     SssSpectrumDesc hairSpec;
     float hairBetaM = .3f, hairBetaN = .3f, hairAlpha = 2.f;
+    int measured = -1;  // MeasuredMaterial: its SceneDesc::measured entry
     std::string name;
 };
 
@@ -285,6 +287,15 @@ struct EnvLightDesc {
 };
 void BuildPortal(EnvLightDesc &e, const std::string &loc);
 
+// MeasuredBxDFData (bxdfs.cpp:865-1001): an RGL tensor file's tables as PiecewiseLinear2D's
+// constructor leaves them, in core/measured.h's layout (kMeasHdr header ints, float blob)
+struct MeasuredDesc {
+    std::string path;
+    std::vector<int> hdr;
+    std::vector<float> blob;
+};
+MeasuredDesc LoadMeasuredBRDF(const std::string &path);
+
 // PointLight / SpotLight / DistantLight (lights.h:200-300, 740-800; lights.cpp:192-276, 1376-1495)
 // in render space: deltaLights holds the point and spot lights first (light-BVH members, global
 // light index nAreaLights + i), then the distant lights (members of the infinite-light list)
@@ -369,6 +380,7 @@ struct SceneDesc {
 
     std::vector<MaterialDesc> materials;
     std::vector<SubsurfaceDesc> sss;  // MaterialDesc::sss
+    std::vector<MeasuredDesc> measured;  // MaterialDesc::measured (one per file)
     std::vector<MediumDesc> media;
     int cameraMedium = -1;                          // -1: vacuum
     std::vector<std::array<int16_t, 2>> triMedium;  // {inside, outside}; empty if no media

@@ -67,6 +67,7 @@ constexpr int kMatThinDielectricT = 6;                           // volumetric p
 constexpr int kMatDiffuseTransmissionT = 7;                      // k_vlayered
 constexpr int kMatMixT = 8;  // MixMaterial: resolved per hit by k_closest<kClosestMix>
 constexpr int kMatHairT = 9;  // HairBxDF: k_vlayered (volumetric path only)
+constexpr int kMatMeasuredT = 10;  // MeasuredBxDF: k_vlayered (volumetric path only)
 PHD int MatCounter(int type) { return type == 0 ? kCntMat : kCntMat + 3 + type; }
 PHD int CounterIndex(int depth, int queue, int shard) {
     return ((depth * kNumQueues + queue) * kShards + shard) * kCounterPad;
@@ -146,6 +147,9 @@ struct DeviceScene {
     // u1 v1 u2 v2), nullptr when no mesh has vertex normals or uv
     const float4 *triShade;
     const float4 *triTangent;  // [3][nTris] shading tangents S (triShade bit2), or nullptr
+    // measured BRDFs (core/measured.h): kMeasHdr ints each (hdr[7] = the BRDF's blob offset)
+    const int *measHdr;
+    const float *measData;
     // materials
     const float4 *matCoeffs;  // c0, c1, c2, constant value
     const int *matConstant;

@@ -28,6 +28,7 @@
 #include "common.h"
 #include "../core/bssrdf.h"
 #include "../core/hair.h"
+#include "../core/measured.h"
 
 namespace pbrt_amd {
 
@@ -1425,7 +1426,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
         }
         if (last) continue;
         if (mtypeHit == kMatCoatedDiffuseT || mtypeHit == kMatCoatedConductorT || mtypeHit == kMatDiffuseTransmissionT ||
-            mtypeHit == kMatHairT)
+            mtypeHit == kMatHairT || mtypeHit == kMatMeasuredT)
             continue;  // k_vlayered
         const int mtype = DiffuseOnly ? 0 : mtypeHit;
         // ---- EvaluateMaterialAndBSDF (surfscatter.cpp:57-328) for this material type
@@ -2192,9 +2193,9 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
         const int mat = VolHitMaterial(S, st, ri, prim);
         const int mtype = S.matType[mat];
         if (mtype != kMatCoatedDiffuseT && mtype != kMatCoatedConductorT && mtype != kMatDiffuseTransmissionT &&
-            mtype != kMatHairT)
+            mtype != kMatHairT && mtype != kMatMeasuredT)
             continue;
-        const bool dt = mtype == kMatDiffuseTransmissionT, hair = mtype == kMatHairT;
+        const bool dt = mtype == kMatDiffuseTransmissionT, hair = mtype == kMatHairT, meas = mtype == kMatMeasuredT;
         const float lambda0 = rec.lambda0[ri];
         const int slot = rec.pixel[ri];
         const int depth = rec.depth[ri], flags = rec.flags[ri], medium = rec.medium[ri];
@@ -2215,7 +2216,7 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
         const float4 L0 = S.matLayer[3 * mat], L1 = S.matLayer[3 * mat + 1], L2 = S.matLayer[3 * mat + 2];
         const bool conductor = mtype == kMatCoatedConductorT;
         float ieta = mp4.z;
-        if (!hair && L2.w >= 0) {  // spectral interface eta: eta(lambda_0), TerminateSecondary
+        if (!hair && !meas && L2.w >= 0) {  // spectral interface eta: eta(lambda_0), TerminateSecondary
             const int es = (int)L2.w, a = S.plOffsets[es], na = S.plOffsets[es + 1] - a;
             ieta = PiecewiseLinearEval(S.plLambda + a, S.plValue + a, na, lambda0);
             if (ieta == 0) ieta = 1;
@@ -2235,6 +2236,10 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
             SpectralIter it(lambda0);
 #pragma unroll 1
             for (int i = 0; i < kNS; ++i, it.Next()) {
+                if (meas) {  // MeasuredBxDF keeps the wavelengths (its spectra are per lambda)
+                    sp.b[i] = it.lam;
+                    continue;
+                }
                 if (hair) {
                     const float q = SssSpectrumAt(S, hq, it.lam);
                     sp.a[i] = L0.x == 0 ? (q > 0 ? q : 0.f) : HairSigmaAFromReflectance(Clampf(q, 0, 1), hairDen);
@@ -2282,7 +2287,13 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
         const DiffuseTransmission<LayerSpec> D{sp, prMax, ptMax};
         HairState H{};
         if (hair) H = MakeHair(-1 + 2 * si.uv[1], L2.x, hairBm, hairBn, L2.w);
-        const int bflags = hair ? (kBxGlossy | kBxReflection) : dt ? D.Flags() : L.LayerFlags();
+        // MeasuredMaterial::GetBxDF (materials.h:931-934): the BRDF's tables (matLayer: its index)
+        MeasuredView M{};
+        if (meas) {
+            const int *mh = S.measHdr + kMeasHdr * (int)L0.x;
+            M = MeasuredAt(mh, S.measData + mh[7]);
+        }
+        const int bflags = (hair || meas) ? (kBxGlossy | kBxReflection) : dt ? D.Flags() : L.LayerFlags();
         const Frame frame = Frame::FromXZ(Normalize(si.dpdus), si.ns);
         const V3 woL = frame.ToLocal(wo3);
         float fo[kNS];
@@ -2297,6 +2308,7 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
                 const V3 wi = ls.wi;
                 const V3 wiL = frame.ToLocal(wi);
                 if (hair) HairF(H, sp.a, woL, wiL, fo);
+                else if (meas) MeasuredF(M, woL, wiL, sp.b, fo);
                 else if (dt) D.f(woL, wiL, fo);
                 else L.f(woL, wiL, true, fo);
                 bool fnz = false;
@@ -2305,6 +2317,7 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
                 if (fnz) {
                     const float bsdfPDF = ls.delta ? 0.f
                                           : hair ? HairPDF(H, sp.a, woL, wiL)
+                                          : meas ? MeasuredPDF(M, woL, wiL)
                                           : dt   ? D.PDF(woL, wiL)
                                                  : L.PDF(woL, wiL, true);
                     const float absdot = AbsDotN(si.ns, wi);
@@ -2350,6 +2363,10 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
             bs.pdfIsProportional = false;
             bs.flags = kBxGlossy | kBxReflection;
             bs.ok = HairSampleF(H, sp.a, woL, rs.iUc, rs.iU0, rs.iU1, &bs.wi, &bs.pdf, fo);
+        } else if (meas) {
+            bs.pdfIsProportional = false;
+            bs.flags = kBxGlossy | kBxReflection;
+            bs.ok = MeasuredSampleF(M, woL, rs.iU0, rs.iU1, sp.b, &bs.wi, &bs.pdf, fo);
         } else if (dt) {
             bs.pdfIsProportional = false;
             bs.ok = D.Sample_f(woL, rs.iUc, rs.iU0, rs.iU1, &bs.wi, &bs.pdf, &bs.flags, fo);
@@ -2895,7 +2912,8 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
     else if (S.media.allGrey) hipLaunchKernelGGL(k_vmedium_grey<false>, gW, block, 0, s, S, st, v, wf);
     else hipLaunchKernelGGL(k_vmedium, gW, block, 0, s, S, st, v, wf);
     const int layeredTypes =
-        (1 << kMatCoatedDiffuseT) | (1 << kMatCoatedConductorT) | (1 << kMatDiffuseTransmissionT) | (1 << kMatHairT);
+        (1 << kMatCoatedDiffuseT) | (1 << kMatCoatedConductorT) | (1 << kMatDiffuseTransmissionT) | (1 << kMatHairT) |
+        (1 << kMatMeasuredT);
     const int other = ~((1 << kMatDiffuseT) | (1 << 3) | layeredTypes);
     const size_t surfLds = VolTablesLdsBytes(S) + kNS * kBlock * sizeof(float);
     const bool qcheck = QueueCheckOn() && wf != S.maxDepth;

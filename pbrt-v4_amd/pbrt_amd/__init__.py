@@ -113,6 +113,8 @@ class SceneFlat(ctypes.Structure):
         ("sss_tables", ctypes.POINTER(ctypes.c_float)),
         ("vertex_s", ctypes.POINTER(ctypes.c_float)), ("n_vertex_s", ctypes.c_int),
         ("env_portal", ctypes.POINTER(ctypes.c_float)),
+        ("n_measured", ctypes.c_int),
+        ("measured_files", ctypes.POINTER(ctypes.c_char_p)),
     ]
 
 
@@ -141,7 +143,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_context_free", "pbrt_render", "pbrt_synchronize", "pbrt_get_stats", "pbrt_reset_stats",
     "pbrt_film_clear", "pbrt_film_device_ptr", "pbrt_film_read", "pbrt_film_get_rgb", "pbrt_intersect",
     "pbrt_debug_halton", "pbrt_debug_halton_fastpath_mismatches", "pbrt_debug_catmull_rom", "pbrt_debug_check_rn_math", "pbrt_debug_rgb_coeffs", "pbrt_debug_rgb2spec_column", "pbrt_debug_kernel_sections",
-    "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_sampler", "pbrt_debug_rng", "pbrt_debug_det_math", "pbrt_debug_hair", "pbrt_debug_catmull_rom_gpu", "pbrt_debug_portal_eval", "pbrt_debug_procedural", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
+    "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_sampler", "pbrt_debug_rng", "pbrt_debug_det_math", "pbrt_debug_hair", "pbrt_debug_measured", "pbrt_debug_catmull_rom_gpu", "pbrt_debug_portal_eval", "pbrt_debug_procedural", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
     "pbrt_debug_named_spectrum", "pbrt_debug_bxdf", "pbrt_debug_layered", "pbrt_debug_triangle_shading", "pbrt_film_write_image",
     "pbrt_image_read_size", "pbrt_image_read", "pbrt_image_write", "pbrt_image_error", "pbrt_debug_filter_sample",
     "pbrt_debug_bvh_stats", "pbrt_debug_light_bvh", "pbrt_intersect_tr", "pbrt_intersect_one_random", "pbrt_image_flip", "pbrt_set_kernel_profiling", "pbrt_get_kernel_stats",
@@ -224,6 +226,7 @@ def _lib():
     lib.pbrt_debug_catmull_rom_gpu.argtypes = [c.c_int, c.c_int, c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_void_p,
                                                c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_debug_portal_eval.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_void_p, c.c_void_p]
+    lib.pbrt_debug_measured.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_void_p, c.c_void_p]
     lib.pbrt_debug_procedural.argtypes = [c.c_int, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_debug_queue_counts.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_int]
     lib.pbrt_debug_trowbridge.argtypes = [c.c_void_p, c.c_void_p]
@@ -439,6 +442,15 @@ class Scene:
         assert len(d) == len(uu)
         out = np.zeros((len(d), 16), dtype=np.float32)
         _check(_lib().pbrt_debug_env_eval(self._h, env, d.ctypes.data, uu.ctypes.data, len(d), out.ctypes.data))
+        return out
+
+    def measured_eval(self, brdf, queries, lambdas):
+        """The product's MeasuredBxDF on the host (pbrt_debug_measured) for [n][8] queries {wo, wi,
+        u0, u1} at 31 wavelengths -> [n][68]: f[31], PDF, Sample_f ok, wi, pdf, f[31]."""
+        q = np.ascontiguousarray(queries, dtype=np.float32).reshape(-1, 8)
+        lam = np.ascontiguousarray(lambdas, dtype=np.float32).reshape(31)
+        out = np.zeros((len(q), 68), dtype=np.float32)
+        _check(_lib().pbrt_debug_measured(self._h, brdf, q.ctypes.data, len(q), lam.ctypes.data, out.ctypes.data))
         return out
 
     def portal_eval(self, env, queries, res=0):

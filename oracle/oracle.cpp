@@ -54,215 +54,31 @@ static inline Float Sqr(Float x) { return x * x; }
 static inline Float Clamp(Float v, Float lo, Float hi) { return v < lo ? lo : (v > hi ? hi : v); }
 static inline Float Lerp(Float t, Float a, Float b) { return (1 - t) * a + t * b; }
 static inline Float SafeSqrt(Float x) { return std::sqrt(std::max<Float>(0.f, x)); }
-// Transcendentals, in one of three modes (oracle_set_math_mode):
-//   0 (default) libm's float functions, as the reference CPU build calls them (the component
-//     tests pin the oracle against the reference's goldens in this mode);
-//   2 "device math" (the GPU parity tests select it): the portable polynomials the GPU kernels
-//     evaluate (the product's
-//     core/detmath.h: Cody-Waite reduction + Cephes minimax polynomials, IEEE operations only),
-//     restated here, so every device decision that hashes or seeds from a ray's bits (medium RNG,
-//     wavefront/media.cpp:44; alpha tests, gpu/optix.cu:197-243; mix choices, materials.h:285-294)
-//     is reproduced bit for bit;
-//   1 correctly rounded (double evaluation, one rounding).
-// The three differ by an ulp or two per call (tests/test_det_math.py measures it).
+// Transcendentals, in one of two modes (oracle_set_math_mode):
+//   0 (default) libm's float functions, as the reference CPU build calls them.  This is also what
+//     the GPU kernels compute: their core/detmath.h restates glibc's sinf, cosf, expf, logf, asinf,
+//     acosf, atan2f, tanf and sinhf bit for bit (tools/detmath_exhaustive.cpp), so the GPU parity
+//     tests compare against this mode and device decisions that hash or seed from a ray's bits
+//     (medium RNG, wavefront/media.cpp:44; alpha tests, gpu/optix.cu:197-243; mix choices,
+//     materials.h:285-294) follow the oracle's;
+//   1 correctly rounded (double evaluation, one rounding), an ulp away from libm in a few per cent
+//     of calls: the sensitivity check of tests/test_gpu_media.py.
+// Mode 2 (round 5's restated device polynomials) is gone: it is mode 0 now.
 static int g_mathMode = 0;
-namespace dm {
-static inline uint32_t Bits(float f) {
-    uint32_t u;
-    std::memcpy(&u, &f, 4);
-    return u;
-}
-static const float kPiF = 0x1.921fb6p+1f, kPio2F = 0x1.921fb6p+0f, kPio4F = 0x1.921fb6p-1f;
-static const float kPiLo = -0x1.777a5cp-24f, kPio2Lo = -0x1.777a5cp-25f, kPio4Lo = -0x1.777a5cp-26f;
-// sin / cos: q = rint(x 2/pi), r = x - q pi/2 with a three-part pi/2 (double beyond |x| = 8192)
-static void SinCos(float x, float *s, float *c) {
-    if (!(std::fabs(x) <= 3.0e38f)) { *s = *c = x - x; return; }
-    if (x == 0.f) { *s = x; *c = 1.f; return; }
-    float r;
-    int q;
-    if (std::fabs(x) <= 8192.f) {
-        const float qf = std::rint(x * 0x1.45f306p-1f);
-        r = std::fma(-qf, 0x1.921fb6p+0f, x);
-        r = std::fma(-qf, -0x1.777a5cp-25f, r);
-        r = std::fma(-qf, -0x1.ee59dap-50f, r);
-        q = (int)qf & 3;
-    } else {
-        const double qd = std::rint((double)x * 0.63661977236758134308);
-        double t = std::fma(-qd, 0x1.921fb54442d18p+0, (double)x);
-        t = std::fma(-qd, 0x1.1a62633145c07p-54, t);
-        r = (float)t;
-        q = (int)(int64_t)qd & 3;
-    }
-    const float z = r * r;
-    float ps = std::fma(z, -1.9515295891e-4f, 8.3321608736e-3f);
-    ps = std::fma(z, ps, -1.6666654611e-1f);
-    const float sp = std::fma(r * z, ps, r);
-    float pc = std::fma(z, 2.443315711809948e-5f, -1.388731625493765e-3f);
-    pc = std::fma(z, pc, 4.166664568298827e-2f);
-    const float cp = std::fma(z * z, pc, std::fma(-0.5f, z, 1.f));
-    const float sv[4] = {sp, cp, -sp, -cp}, cv[4] = {cp, -sp, -cp, sp};
-    *s = sv[q];
-    *c = cv[q];
-}
-static float AsinP(float z, float s) {  // asin on [0, 1/2] in z = s^2
-    float p = std::fma(z, 4.2163199048e-2f, 2.4181311049e-2f);
-    p = std::fma(z, p, 4.5470025998e-2f);
-    p = std::fma(z, p, 7.4953002686e-2f);
-    p = std::fma(z, p, 1.6666752422e-1f);
-    return std::fma(z * s, p, s);
-}
-static float Asin(float x) {
-    const float a = std::fabs(x);
-    if (!(a <= 1.f)) return std::numeric_limits<float>::quiet_NaN();
-    float r;
-    if (a > 0.5f) {
-        const float z = 0.5f * (1.f - a);
-        r = kPio2F + (kPio2Lo - 2.f * AsinP(z, std::sqrt(z)));
-    } else {
-        r = AsinP(a * a, a);
-    }
-    return x < 0 ? -r : r;
-}
-static float Acos(float x) {
-    if (!(std::fabs(x) <= 1.f)) return std::numeric_limits<float>::quiet_NaN();
-    if (x < -0.5f) {
-        const float z = 0.5f * (1.f + x);
-        return kPiF + (kPiLo - 2.f * AsinP(z, std::sqrt(z)));
-    }
-    if (x > 0.5f) {
-        const float z = 0.5f * (1.f - x);
-        return 2.f * AsinP(z, std::sqrt(z));
-    }
-    return kPio2F + (kPio2Lo - AsinP(x * x, x));
-}
-static float Atan2(float y, float x) {
-    if (x != x || y != y) return x + y;
-    const float ax = std::fabs(x), ay = std::fabs(y);
-    const bool yneg = std::signbit(y), xneg = std::signbit(x);
-    float a;
-    if (ay == 0.f) {
-        a = xneg ? kPiF : 0.f;
-    } else if (ax == 0.f) {
-        a = kPio2F;
-    } else if (std::isinf(ax) || std::isinf(ay)) {
-        a = std::isinf(ax) && std::isinf(ay) ? (xneg ? 3.f * kPio4F : kPio4F) : std::isinf(ax) ? (xneg ? kPiF : 0.f) : kPio2F;
-    } else {
-        const bool swap = ay > ax;
-        float t = swap ? ax / ay : ay / ax;
-        const bool shift = t > 0.4142135623730950f;  // tan(pi/8): atan(t) = pi/4 + atan((t-1)/(t+1))
-        if (shift) t = (t - 1.f) / (t + 1.f);
-        const float z = t * t;
-        float p = std::fma(z, 8.05374449538e-2f, -1.38776856032e-1f);
-        p = std::fma(z, p, 1.99777106478e-1f);
-        p = std::fma(z, p, -3.33329491539e-1f);
-        a = std::fma(z * t, p, t);
-        if (shift) a = kPio4F + (kPio4Lo + a);
-        if (swap) a = kPio2F + (kPio2Lo - a);
-        if (xneg) a = kPiF + (kPiLo - a);
-    }
-    return yneg ? -a : a;
-}
-static float Log(float x) {
-    if (x != x || x < 0.f) return std::numeric_limits<float>::quiet_NaN();
-    if (x == 0.f) return -std::numeric_limits<float>::infinity();
-    if (std::isinf(x)) return x;
-    uint32_t u = Bits(x);
-    int e;
-    if ((u >> 23) == 0) {
-        u = Bits(x * 0x1p25f);
-        e = (int)(u >> 23) - 151;
-    } else {
-        e = (int)(u >> 23) - 126;
-    }
-    const uint32_t mb = (u & 0x007fffffu) | 0x3f000000u;
-    float m;
-    std::memcpy(&m, &mb, 4);
-    if (m < 0.707106781186547524f) {
-        e -= 1;
-        m = m + m - 1.f;
-    } else {
-        m = m - 1.f;
-    }
-    const float z = m * m;
-    const float c[9] = {7.0376836292e-2f, -1.1514610310e-1f, 1.1676998740e-1f, -1.2420140846e-1f, 1.4249322787e-1f,
-                        -1.6668057665e-1f, 2.0000714765e-1f, -2.4999993993e-1f, 3.3333331174e-1f};
-    float p = std::fma(m, c[0], c[1]);
-    for (int k = 2; k < 9; ++k) p = std::fma(m, p, c[k]);
-    float yv = p * m * z;
-    const float fe = (float)e;
-    yv = std::fma(fe, -2.12194440e-4f, yv);
-    yv = std::fma(-0.5f, z, yv);
-    return std::fma(fe, 0.693359375f, m + yv);
-}
-// detmath.h Exp / Sinh restated (Cephes expf; sinh from it)
-static float Exp(float x) {
-    if (x != x) return x;
-    if (x > 88.72283935546875f) return std::numeric_limits<float>::infinity();
-    if (x < -103.97208404541016f) return 0.f;
-    const float n = std::floor(std::fma(x, 1.44269502162933349609f, 0.5f));
-    float r = std::fma(n, -0.693359375f, x);
-    r = std::fma(n, 2.12194440e-4f, r);
-    float p = std::fma(r, 1.9875691500e-4f, 1.3981999507e-3f);
-    p = std::fma(r, p, 8.3334519073e-3f);
-    p = std::fma(r, p, 4.1665795894e-2f);
-    p = std::fma(r, p, 1.6666665459e-1f);
-    p = std::fma(r, p, 5.0000001201e-1f);
-    const float y = std::fma(p, r * r, r) + 1.f;
-    const int k = (int)n, k1 = k / 2, k2 = k - k1;
-    uint32_t b1 = (uint32_t)(k1 + 127) << 23, b2 = (uint32_t)(k2 + 127) << 23;
-    float s1, s2;
-    std::memcpy(&s1, &b1, 4);
-    std::memcpy(&s2, &b2, 4);
-    return y * s1 * s2;
-}
-static float Tan(float x) {
-    float s, c;
-    SinCos(x, &s, &c);
-    return s / c;
-}
-static float Sinh(float x) {
-    const float a = std::abs(x);
-    if (a < 0x1p-12f) return x;
-    const float e = Exp(a);
-    const float s = (e - 1.f / e) * 0.5f;
-    return x < 0 ? -s : s;
-}
-}  // namespace dm
-static inline Float CRSin(Float x) {
-    if (g_mathMode == 2) { float s, c; dm::SinCos(x, &s, &c); return s; }
-    return g_mathMode ? (Float)std::sin((double)x) : std::sin(x);
-}
-static inline Float CRCos(Float x) {
-    if (g_mathMode == 2) { float s, c; dm::SinCos(x, &s, &c); return c; }
-    return g_mathMode ? (Float)std::cos((double)x) : std::cos(x);
-}
-static inline Float CRExp(Float x) {
-    if (g_mathMode == 2) return dm::Exp(x);
-    return g_mathMode ? (Float)std::exp((double)x) : std::exp(x);
-}
-static inline Float CRTan(Float x) {
-    if (g_mathMode == 2) return dm::Tan(x);
-    return g_mathMode ? (Float)std::tan((double)x) : std::tan(x);
-}
-static inline Float CRSinh(Float x) {
-    if (g_mathMode == 2) return dm::Sinh(x);
-    return g_mathMode ? (Float)std::sinh((double)x) : std::sinh(x);
-}
-static inline Float CRLog(Float x) {
-    if (g_mathMode == 2) return dm::Log(x);
-    return g_mathMode ? (Float)std::log((double)x) : std::log(x);
-}
+static inline Float CRSin(Float x) { return g_mathMode == 1 ? (Float)std::sin((double)x) : std::sin(x); }
+static inline Float CRCos(Float x) { return g_mathMode == 1 ? (Float)std::cos((double)x) : std::cos(x); }
+static inline Float CRExp(Float x) { return g_mathMode == 1 ? (Float)std::exp((double)x) : std::exp(x); }
+static inline Float CRTan(Float x) { return g_mathMode == 1 ? (Float)std::tan((double)x) : std::tan(x); }
+static inline Float CRSinh(Float x) { return g_mathMode == 1 ? (Float)std::sinh((double)x) : std::sinh(x); }
+static inline Float CRLog(Float x) { return g_mathMode == 1 ? (Float)std::log((double)x) : std::log(x); }
 static inline Float CRATan2(Float y, Float x) {
-    if (g_mathMode == 2) return dm::Atan2(y, x);
-    return g_mathMode ? (Float)std::atan2((double)y, (double)x) : std::atan2(y, x);
+    return g_mathMode == 1 ? (Float)std::atan2((double)y, (double)x) : std::atan2(y, x);
 }
 static inline Float SafeASin(Float x) {
-    if (g_mathMode == 2) return dm::Asin(Clamp(x, -1, 1));
-    return g_mathMode ? (Float)std::asin((double)Clamp(x, -1, 1)) : std::asin(Clamp(x, -1, 1));
+    return g_mathMode == 1 ? (Float)std::asin((double)Clamp(x, -1, 1)) : std::asin(Clamp(x, -1, 1));
 }
 static inline Float SafeACos(Float x) {
-    if (g_mathMode == 2) return dm::Acos(Clamp(x, -1, 1));
-    return g_mathMode ? (Float)std::acos((double)Clamp(x, -1, 1)) : std::acos(Clamp(x, -1, 1));
+    return g_mathMode == 1 ? (Float)std::acos((double)Clamp(x, -1, 1)) : std::acos(Clamp(x, -1, 1));
 }
 static inline Float DifferenceOfProducts(Float a, Float b, Float c, Float d) {
     Float cd = c * d;
@@ -7157,7 +6973,8 @@ void oracle_sss_table(float g, float eta, float *out) {
 void oracle_set_cr_math(int on) { g_mathMode = on ? 1 : 0; }
 void oracle_set_math_mode(int mode) { g_mathMode = mode; }
 int oracle_get_math_mode(void) { return g_mathMode; }
-// the oracle's transcendentals in its current mode: fn 0 sin, 1 cos, 2 asin, 3 acos, 4 atan2(a, b), 5 log
+// the oracle's transcendentals in its current mode: fn 0 sin, 1 cos, 2 asin, 3 acos, 4 atan2(a, b), 5 log,
+// 6 exp, 7 sinh, 8 tan, 9 atan, 10 expm1
 void oracle_math_eval(int fn, const float *a, const float *b, int n, float *out) {
     for (int i = 0; i < n; ++i) {
         switch (fn) {
@@ -7168,6 +6985,9 @@ void oracle_math_eval(int fn, const float *a, const float *b, int n, float *out)
         case 4: out[i] = CRATan2(a[i], b[i]); break;
         case 6: out[i] = CRExp(a[i]); break;
         case 7: out[i] = CRSinh(a[i]); break;
+        case 8: out[i] = CRTan(a[i]); break;
+        case 9: out[i] = g_mathMode == 1 ? (Float)std::atan((double)a[i]) : std::atan(a[i]); break;
+        case 10: out[i] = g_mathMode == 1 ? (Float)std::expm1((double)a[i]) : std::expm1(a[i]); break;
         default: out[i] = CRLog(a[i]); break;
         }
     }
@@ -7194,7 +7014,7 @@ int oracle_intersect_tr(const pbrt_scene_flat *flat, const pbrt_scene_info *info
     // and only the per-sample work uses the device's polynomials.
     struct HostMath {
         int mode = g_mathMode;
-        HostMath() { if (mode == 2) g_mathMode = 0; }
+        HostMath() { if (mode != 0) g_mathMode = 0; }
         void Done() { g_mathMode = mode; }
         ~HostMath() { Done(); }
     } hostMath;
@@ -7242,7 +7062,7 @@ static int RenderRows(const pbrt_scene_flat *flat, const pbrt_scene_info *info, 
     // and only the per-sample work uses the device's polynomials.
     struct HostMath {
         int mode = g_mathMode;
-        HostMath() { if (mode == 2) g_mathMode = 0; }
+        HostMath() { if (mode != 0) g_mathMode = 0; }
         void Done() { g_mathMode = mode; }
         ~HostMath() { Done(); }
     } hostMath;
@@ -7518,7 +7338,7 @@ int oracle_portal_eval(const pbrt_scene_flat *flat, int env, const float *q, int
     OEnvLight E;
     {
         const int mode = g_mathMode;
-        if (mode == 2) g_mathMode = 0;  // construction is host work (libm)
+        if (mode != 0) g_mathMode = 0;  // construction is host work (libm)
         E.Init(flat, env);
         g_mathMode = mode;
     }

@@ -181,13 +181,13 @@ def image_level(scene, image, level):
     return buf, w.value, h.value
 
 
-MATH_LIBM, MATH_CR, MATH_DEVICE = 0, 1, 2
+MATH_LIBM, MATH_CR = 0, 1
 
 
 class math_mode:
     """Context manager: the oracle's transcendentals inside the block -- MATH_LIBM (its default:
-    libm float, as pbrt's CPU build), MATH_DEVICE (the device kernels' portable polynomials,
-    core/detmath.h, bit for bit: what GPU parity compares against) or MATH_CR (correctly rounded)."""
+    glibc's float functions, as pbrt's CPU build calls them, and what the device kernels' detmath.h
+    reproduces bit for bit) or MATH_CR (correctly rounded, for sensitivity checks)."""
 
     def __init__(self, mode):
         self.mode = mode
@@ -207,8 +207,9 @@ def set_math_mode(mode):
 
 
 def math_eval(fn, a, b=None):
-    """The oracle's transcendental `fn` (sin cos asin acos atan2 log exp sinh) in its current mode."""
-    names = ["sin", "cos", "asin", "acos", "atan2", "log", "exp", "sinh"]
+    """The oracle's transcendental `fn` (sin cos asin acos atan2 log exp sinh tan atan expm1) in its
+    current mode: libm's float functions (MATH_LIBM) or correctly rounded (MATH_CR)."""
+    names = ["sin", "cos", "asin", "acos", "atan2", "log", "exp", "sinh", "tan", "atan", "expm1"]
     a = np.ascontiguousarray(a, np.float32)
     b = np.ascontiguousarray(b if b is not None else np.zeros_like(a), np.float32)
     out = np.zeros_like(a)

@@ -2958,23 +2958,10 @@ int pbrt_debug_sampler(const pbrt_scene *scene, int px, int py, int sampleIndex,
 
 int pbrt_debug_det_math(int device, int fn, const float *a, const float *b, int n, float *out) {
     try {
-        if (!a || !b || !out || n < 0 || fn < 0 || fn > 9) return Fail("pbrt_debug_det_math: bad arguments");
+        if (!a || !b || !out || n < 0 || fn < 0 || fn >= detm::kNumEvalFns)
+            return Fail("pbrt_debug_det_math: bad arguments");
         if (device < 0) {  // the same code compiled for the host
-            for (int i = 0; i < n; ++i) {
-                float s, c;
-                switch (fn) {
-                case 0: out[i] = detm::Sin(a[i]); break;
-                case 1: out[i] = detm::Cos(a[i]); break;
-                case 2: out[i] = detm::ASin(std::fmin(std::fmax(a[i], -1.f), 1.f)); break;
-                case 3: out[i] = detm::ACos(std::fmin(std::fmax(a[i], -1.f), 1.f)); break;
-                case 4: out[i] = detm::ATan2(a[i], b[i]); break;
-                case 5: out[i] = detm::Log(a[i]); break;
-                case 6: detm::SinCos(a[i], &s, &c); out[i] = s; break;
-                case 7: detm::SinCos(a[i], &s, &c); out[i] = c; break;
-                case 8: out[i] = detm::Exp(a[i]); break;
-                default: out[i] = detm::Sinh(a[i]); break;
-                }
-            }
+            for (int i = 0; i < n; ++i) out[i] = detm::Eval(fn, a[i], b[i]);
             return 0;
         }
         HIPCHECK(hipSetDevice(device));

@@ -1566,24 +1566,9 @@ __global__ void k_check_rn_math(uint64_t seed, int perThread, unsigned long long
 }
 // the device's portable transcendentals (core/detmath.h) on given inputs: fn 0 sin, 1 cos, 2 asin,
 // 3 acos, 4 atan2(a, b), 5 log, 6 sin of SinCosf, 7 cos of SinCosf, 8 exp, 9 sinh
-__device__ inline float DetMathEval(int fn, float a, float b) {
-    float s, c;
-    switch (fn) {
-    case 0: return Sinf(a);
-    case 1: return Cosf(a);
-    case 2: return SafeASin(a);
-    case 3: return SafeACos(a);
-    case 4: return ATan2f(a, b);
-    case 5: return Logf(a);
-    case 6: SinCosf(a, &s, &c); return s;
-    case 7: SinCosf(a, &s, &c); return c;
-    case 8: return Expf(a);
-    default: return Sinhf(a);
-    }
-}
 __global__ void k_det_math(int fn, const float *a, const float *b, int n, float *out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) out[i] = DetMathEval(fn, a[i], b[i]);
+    if (i < n) out[i] = detm::Eval(fn, a[i], b[i]);
 }
 hipError_t LaunchDetMath(int fn, const float *a, const float *b, int n, float *out, hipStream_t s) {
     hipLaunchKernelGGL(k_det_math, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, fn, a, b, n, out);

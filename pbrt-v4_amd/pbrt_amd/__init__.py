@@ -508,7 +508,8 @@ def debug_rng(seq, advance):
     return int(out[0]), int(out[1])
 
 
-DET_MATH_FNS = ["sin", "cos", "asin", "acos", "atan2", "log", "sincos_sin", "sincos_cos", "exp", "sinh"]
+DET_MATH_FNS = ["sin", "cos", "asin", "acos", "atan2", "log", "sincos_sin", "sincos_cos", "exp", "sinh", "tan", "atan",
+                "expm1"]
 
 
 def det_math(fn, a, b=None, device=-1):

@@ -36,12 +36,13 @@ def oracle():
 
 
 @pytest.fixture(autouse=True)
-def _oracle_math_mode(request):
-    """GPU parity tests compare against the oracle in its device-math mode (the kernels' portable
-    transcendentals, core/detmath.h, reproduced bit for bit); every other test sees its libm mode,
-    in which the component tests pin it to the reference's goldens."""
+def _oracle_math_mode():
+    """Every test -- GPU parity included -- sees the oracle in its libm mode: glibc's float
+    transcendentals, as pbrt's CPU build calls them, in which the component tests pin it to the
+    reference's goldens.  The device kernels' core/detmath.h restates those functions bit for bit
+    (tools/detmath_exhaustive.cpp), so no separate device-math mode exists any more."""
     import pyoracle
-    pyoracle.set_math_mode(pyoracle.MATH_DEVICE if request.node.get_closest_marker("gpu") else pyoracle.MATH_LIBM)
+    pyoracle.set_math_mode(pyoracle.MATH_LIBM)
     yield
     pyoracle.set_math_mode(pyoracle.MATH_LIBM)
 

@@ -164,12 +164,13 @@ def test_c5_full_grid_runs(pa, oracle):
     check(a[40:48], b[40:48])
 
 
-def test_c5_small_statistical_vs_libm_oracle(pa, oracle):
-    """The device media kernels against the oracle in its libm mode (the reference CPU build's
-    float transcendentals, an ulp or two from the device's portable polynomials): paths that meet a
-    one-ulp difference decorrelate (the medium RNG hashes the ray's bits), so the check is
-    statistical -- the image mean within 4 sigma of the oracle's, sigma from the per-pixel
-    spread of 4 independent sample ranges -- and many pixels still agree to 1e-3."""
+def test_c5_small_vs_libm_oracle(pa, oracle):
+    """The device media kernels against the oracle in its libm mode -- the reference CPU build's
+    float transcendentals, which core/detmath.h reproduces bit for bit.  The medium RNG hashes each
+    ray's bits (wavefront/media.cpp:44), so a single last-ulp difference in any transcendental
+    upstream would decorrelate the path: per-pixel agreement at check_parity's bar is the test that
+    the device follows the reference's arithmetic.  Round 5's Cephes polynomials reached only 5.3 %
+    of pixels here; the image mean is also held within 4 sigma of the oracle's."""
     spp = 32
     sc = pa.Scene.from_string(c5_small_text(res=48, spp=spp), SCENES)
     gpu, _ = gpu_rgb(pa, oracle, sc)
@@ -184,10 +185,24 @@ def test_c5_small_statistical_vs_libm_oracle(pa, oracle):
     d = np.abs(gpu.mean(axis=(0, 1)) - ref.mean(axis=(0, 1)))
     assert (d <= 4 * sigma).all(), (d, sigma)
     same = (np.abs(gpu - ref) <= np.maximum(1e-3 * np.abs(ref), 1e-4)).all(axis=-1).mean()
-    # measured 5.3 %: a multi-bounce medium path meets many transcendentals, and the device's
-    # portable polynomials differ from libm's float functions in 10-20 % of calls
-    assert same >= 0.02, same
-    print(f"C5 small vs libm oracle: mean diff {d} (sigma {sigma}), {same*100:.1f}% pixels within 1e-3")
+    print(f"C5 small vs libm oracle: mean diff {d} (sigma {sigma}), {same*100:.2f}% pixels within 1e-3")
+    assert same >= 0.995, same
+
+
+def test_c5_small_cr_oracle_sensitivity(pa, oracle):
+    """The counter-check: against the oracle evaluating correctly rounded transcendentals (an ulp
+    from glibc in 1-16 % of calls) most C5 pixels decorrelate, so the libm agreement above is not
+    something any accurate math library would give."""
+    spp = 32
+    sc = pa.Scene.from_string(c5_small_text(res=48, spp=spp), SCENES)
+    gpu, _ = gpu_rgb(pa, oracle, sc)
+    f = sc.flat()
+    m = [f.output_rgb_from_sensor_rgb[i] for i in range(9)]
+    with oracle.math_mode(oracle.MATH_CR):
+        ref = oracle.film_to_rgb(oracle.render(sc, threads=16), m)
+    same = (np.abs(gpu - ref) <= np.maximum(1e-3 * np.abs(ref), 1e-4)).all(axis=-1).mean()
+    print(f"C5 small vs correctly rounded oracle: {same*100:.2f}% pixels within 1e-3")
+    assert same < 0.9, same
 
 
 @pytest.mark.parametrize("kind", ["homogeneous", "grid"])

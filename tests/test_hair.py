@@ -146,10 +146,11 @@ def test_hair_h_on_the_edge(pa, oracle):
 
 @pytest.mark.gpu
 def test_hair_gpu_matches_oracle_bitwise(pa, oracle):
-    """the BxDF compiled for gfx950 (detmath transcendentals) == the oracle's device-math mode"""
+    """the BxDF compiled for gfx950 (detmath transcendentals, glibc's bit for bit) == the oracle in
+    its libm mode"""
     q = np.concatenate([queries(1 << 16, 21, slope=0.05), queries(8192, 22, bm=0.08, bn=0.3), queries(4096, 23, h=0.0)])
     got = pa.hair_eval(q, device=0)
-    with oracle.math_mode(oracle.MATH_DEVICE):
+    with oracle.math_mode(oracle.MATH_LIBM):
         ref = oracle.hair_eval(q)
     bad = (got.view(np.uint32) != ref.view(np.uint32)).any(axis=1)
     assert not bad.any(), (bad.sum(), q[bad][:3], got[bad][:3, :8], ref[bad][:3, :8])

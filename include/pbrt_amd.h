@@ -265,6 +265,15 @@ typedef struct pbrt_scene_flat {
      * measured_files [n_measured] the resolved RGL tensor files (".bsdf") */
     int n_measured;
     const char *const *measured_files;
+    /* scene Options (BasicSceneBuilder::Option, scene.cpp:492-560) that change the hot path:
+     * bit 0 disablepixeljitter (samplers.h:807-812), bit 1 disablewavelengthjitter
+     * (wavefront/camera.cpp:55), bit 2 disabletexturefiltering (wavefront/surfscatter.cpp:77) */
+    int options;
+    /* multispectral basis image textures (tex_node_info flags bit 5, the fork's "basisfilename"):
+     * the node's table starts at tex_basis[params[22]], params[24] floats long, laid out as the
+     * reference's GPU basis array (textures.cpp:1148-1176): channels, basis length, int(offset),
+     * then each channel's basis values */
+    const float *tex_basis;
 } pbrt_scene_flat;
 
 typedef struct pbrt_render_params {
@@ -458,6 +467,16 @@ int pbrt_debug_hair(int device, const float *in16, int n, float *out);
  * per query in8 {wo xyz, wi xyz, u0, u1} (local frame) at the 31 wavelengths `lambda`; out
  * [n][68] = f(wo, wi)[31], PDF(wo, wi), Sample_f ok, wi xyz, pdf, f[31] */
 int pbrt_debug_measured(const pbrt_scene *scene, int brdf, const float *in8, int n, const float *lambda, float *out);
+/* PiecewiseLinear2D<dim> alone (util/sampling.h:1299-1749; dim 0 or 2, normalised, CDF iff cdf)
+ * over data [pr2[0]][pr2[1]][ys][xs] with parameter grids pv0 [pr2[0]], pv1 [pr2[1]] (dim 2); per
+ * query q6 = {u0, u1, px, py, p0, p1}: out7 = Sample(u, p) xy pdf, Invert(p_xy, p) xy pdf,
+ * Evaluate(p_xy, p) (Sample / Invert left 0 without a CDF).  The measured BxDF's tables. */
+int pbrt_debug_pl2d(int dim, int cdf, const float *data, int xs, int ys, const int *pr2, const float *pv0,
+                    const float *pv1, const float *q6, int n, float *out7);
+/* WindowedPiecewiseConstant2D alone (util/sampling.h:890-980) over func [res][res] (the portal
+ * light's sampling distribution): per query q8 = {u0, u1, window b0 b1 b2 b3, qx, qy}: out5 =
+ * Sample ok, x, y, pdf, PDF(q, b) */
+int pbrt_debug_windowed2d(const float *func, int res, const float *q8, int n, float *out5);
 /* The procedural textures' kernels code on the host (core/texture_eval.h): kind 0 FBm, 1
  * Turbulence (wrinkled), 2 windy, 3 InsidePolkaDot (in9[0..1] = s, t), 4 marble; params4 =
  * octaves, roughness, scale, variation; in9 per point = p, dpdx, dpdy; out6 per point = value
@@ -480,7 +499,8 @@ int pbrt_debug_triangle_shading(const float *p9, const float *n9, const float *u
                                 const float *u2, float *out15);
 /* GetNamedSpectrum(name)(lambda_i) for the metal / glass tables */
 int pbrt_debug_named_spectrum(const char *name, const float *lambda, int n, float *out);
-/* DielectricBxDF (type 1) / ConductorBxDF (type 2) in the shading frame: params3 = alpha_x
+/* DielectricBxDF (type 1) / ConductorBxDF (type 2) / this fork's RetroreflectiveBxDF (type 11,
+ * bxdfs.h:102-215) in the shading frame: params3 = alpha_x
  * alpha_y eta (alphas as the constructor leaves them); eta31 / k31 the conductor's sampled
  * spectra; u3 = uc u0 u1.  out70 = sample_ok wi3 pdf flags etap f_sample[31] f(wo,wi)[31]
  * PDF(wo,wi) (Sample_f / f / PDF of bxdfs.h:300-517, bxdfs.cpp:77-245) */

@@ -3282,7 +3282,13 @@ struct BxDF {
             *bs = BSDFSample{R * InvPi, wi, std::abs(wi.z) * InvPi, BxR | BxDiffuse, 1};
             return true;
         }
-        if (type == 2) {
+        if (type == 11 && mf.Smooth()) {
+            // RetroreflectiveBxDF::Sample_f (bxdfs.h:119-129): the smooth case sends wi = wo
+            Vec wi = wo;
+            *bs = BSDFSample{FrC(std::abs(wi.z)) / std::abs(wi.z), wi, 1, BxR | BxSpecular, 1};
+            return true;
+        }
+        if (type == 2 || type == 11) {  // the rough retroreflective sample is the conductor's (bxdfs.h:130-152)
             if (mf.Smooth()) {
                 Vec wi(-wo.x, -wo.y, wo.z);
                 *bs = BSDFSample{FrC(std::abs(wi.z)) / std::abs(wi.z), wi, 1, BxR | BxSpecular, 1};
@@ -3360,6 +3366,21 @@ struct BxDF {
         if (type == 6) return Spectrum(0.f);
         if (type == 7) return SameHemisphere(wo, wi) ? R * InvPi : Tt * InvPi;
         if (type == 0) return SameHemisphere(wo, wi) ? R * InvPi : Spectrum(0.f);
+        if (type == 11) {
+            // RetroreflectiveBxDF::f (bxdfs.h:155-178): a retro lobe about wo plus the conductor
+            // lobe, both scaled by 1 - (R_i - R_o)
+            if (!SameHemisphere(wo, wi) || mf.Smooth()) return Spectrum(0.f);
+            Float co = std::abs(wo.z), ci = std::abs(wi.z);
+            if (ci == 0 || co == 0) return Spectrum(0.f);
+            Vec wm = wo + wi, wmRetro = wo;
+            if (LengthSquared(wm) == 0) return Spectrum(0.f);
+            wm = Normalize(wm);
+            Float R_o = FrDielectric(Dot(wo, wm), 1.59f), R_i = FrDielectric(Dot(wi, wmRetro), 1.59f);
+            Spectrum F = FrC(AbsDot(wo, wm)), Fr = FrC(AbsDot(wi, wmRetro));
+            Spectrum retro = Fr * mf.D(wmRetro) * mf.G(wo, wi) / (4 * ci * co);
+            Float w = 1 - (R_i - R_o);
+            return retro * w + (F * mf.D(wm) * mf.G(wo, wi) / (4 * ci * co)) * w;
+        }
         if (type == 2) {
             if (!SameHemisphere(wo, wi) || mf.Smooth()) return Spectrum(0.f);
             Float co = std::abs(wo.z), ci = std::abs(wi.z);
@@ -3393,7 +3414,7 @@ struct BxDF {
         }
         if (type != 1 && !(sf & 1)) return 0;
         if (type == 0) return SameHemisphere(wo, wi) ? std::abs(wi.z) * InvPi : 0;
-        if (type == 2) {
+        if (type == 2 || type == 11) {  // RetroreflectiveBxDF::PDF is the conductor's (bxdfs.h:181-201)
             if (!SameHemisphere(wo, wi) || mf.Smooth()) return 0;
             Vec wm = wo + wi;
             if (LengthSquared(wm) == 0) return 0;
@@ -5004,7 +5025,7 @@ struct OTextures {
         fullRes[1] = yres;
         n = flat->n_tex_nodes;
         if (!n && !flat->n_images) return;  // normal maps are images without a texture node
-        sppScale = std::max<Float>(.125f, 1 / std::sqrt((Float)spp));
+        sppScale = (flat->options & 1) ? 1.f : std::max<Float>(.125f, 1 / std::sqrt((Float)spp));
         images.resize(flat->n_images);
         for (int i = 0; i < flat->n_images; ++i) {
             const int32_t *ri = flat->image_raw_info + 8 * i;
@@ -5127,6 +5148,10 @@ struct OTextures {
         c.n = si.n;
         c.u = si.uv[0];
         c.v = si.uv[1];
+        if (f->options & 4) {  // Option "disabletexturefiltering" (surfscatter.cpp:76-77)
+            c.dudx = c.dudy = c.dvdx = c.dvdy = 0;
+            return c;
+        }
         Vec dpdx, dpdy;
         DpDxy(si.p, si.n, &dpdx, &dpdy);
         Float ata00 = Dot(si.dpdu, si.dpdu), ata01 = Dot(si.dpdu, si.dpdv), ata11 = Dot(si.dpdv, si.dpdv);
@@ -5384,6 +5409,20 @@ struct OTextures {
             Map2D(node, c, st, dst);
             st[1] = 1 - st[1];
             images[in[5]].Filter(in[7], q[27], st[0], st[1], dst[0], dst[2], dst[1], dst[3], 3, rgb);
+            if (in[1] & 32) {
+                // GPUSpectrumImageTexture::Evaluate, the fork's multispectral basis branch
+                // (textures.h:655-679): sum_c basis[3 + i + c NS] (texel_c - int offset), the basis
+                // indexed by the wavelength sample i (clamped to the table), the texel unscaled
+                const float *tab = f->tex_basis + (int)q[22];
+                const int width = (int)q[24], nCh = (int)tab[0], off = (int)tab[2];
+                Spectrum s(0.f);
+                for (int ch = 0; ch < nCh; ++ch) {
+                    Spectrum b;
+                    for (int i = 0; i < NS; ++i) b[i] = tab[std::min(3 + i + ch * NS, width - 1)];
+                    s = b * (rgb[ch] - off) + s;
+                }
+                return s;
+            }
             for (int k = 0; k < 3; ++k) {
                 rgb[k] = q[26] * rgb[k];
                 rgb[k] = std::max<Float>(0, (in[1] & 8) ? 1 - rgb[k] : rgb[k]);
@@ -6105,7 +6144,7 @@ struct Renderer {
                     lambda.pdf[0] /= NS;
                 }
             }
-            if (bx.type == 2) {
+            if (bx.type == 2 || bx.type == 11) {  // conductor; retroreflective reads the same parameters
                 int es = f->material_spectra[2 * mat], ks = f->material_spectra[2 * mat + 1];
                 for (int i = 0; i < NS; ++i) {
                     Float l = lambda.lambda[i];
@@ -6135,8 +6174,11 @@ struct Renderer {
     }
     // The camera sample and ray of EvaluatePixelSample (cpu/integrators.cpp:228-242; the wavefront's
     // camera.cpp:31-80 draws the same dimensions): wavelengths, filter, time, lens, render-space ray
+    // Option "disablewavelengthjitter" (camera.cpp:55) and "disablepixeljitter" (GetCameraSample,
+    // samplers.h:807-812): the draws happen, their values are replaced
     void CameraRay(int px, int py, AnySampler &hs, Wavelengths &lambda, float *weight, Vec &ro, Vec &rd) const {
         Float lu = hs.Get1D();
+        if (f->options & 2) lu = 0.5f;
         lambda = Wavelengths::SampleUniform(lu);
         Float fx, fy;
         hs.Pixel2D(&fx, &fy);
@@ -6146,6 +6188,12 @@ struct Renderer {
         hs.Get1D();  // time
         Float l0, l1;
         hs.Get2D(&l0, &l1);
+        if (f->options & 1) {
+            pFilmX = px + 0.5f;
+            pFilmY = py + 0.5f;
+            l0 = l1 = 0.5f;
+            fw = 1;
+        }
         *weight = fw;
         Vec pCam = Xf(f->camera_from_raster, Vec(pFilmX, pFilmY, 0), true);
         ro = Vec(0, 0, 0);
@@ -6936,6 +6984,60 @@ void oracle_hair_eval(const float *in, int n, float *out) {
         }
     }
 }
+// PiecewiseLinear2D<dim> (util/sampling.h:1299-1749) alone, as pbrt_debug_pl2d: the table over
+// data [pr0][pr1][ys][xs] (dim 2; normalised, CDF iff cdf) and per query q[6] {u0, u1, px, py, p0, p1}
+// -> out[7] {Sample x, y, pdf, Invert x, y, pdf, Evaluate} (Sample / Invert zero without a CDF)
+int oracle_pl2d(int dim, int cdf, const float *data, int xs, int ys, const int *pr, const float *pv0,
+                const float *pv1, const float *q, int n, float *out) {
+    if ((dim != 0 && dim != 2) || xs < 2 || ys < 2) return -1;
+    std::vector<float> pv[3];
+    if (dim == 2) {
+        pv[0].assign(pv0, pv0 + pr[0]);
+        pv[1].assign(pv1, pv1 + pr[1]);
+    }
+    omeas::Table t;
+    t.Build(data, xs, ys, dim, pv, true, cdf != 0);
+    for (int k = 0; k < n; ++k) {
+        const float *x = q + 6 * k;
+        float *o = out + 7 * k;
+        std::fill(o, o + 7, 0.f);
+        const Float par[2] = {x[4], x[5]};
+        if (cdf) {
+            t.Sample(x[0], x[1], par, &o[0], &o[1], &o[2]);
+            t.Invert(x[2], x[3], par, &o[3], &o[4], &o[5]);
+        }
+        o[6] = t.Evaluate(x[2], x[3], par);
+    }
+    return 0;
+}
+// WindowedPiecewiseConstant2D (util/sampling.h:890-980) alone, as pbrt_debug_windowed2d: the
+// function f [n][n] with its SummedAreaTable; per query q[8] {u0, u1, b0, b1, b2, b3, qx, qy}
+// -> out[5] {ok, x, y, pdf, PDF(q, b)}
+int oracle_windowed2d(const float *f, int n, const float *q, int k, float *out) {
+    if (n < 1) return -1;
+    OEnvLight E;
+    E.n = n;
+    E.pfunc.assign(f, f + (size_t)n * n);
+    E.psat.assign((size_t)n * n, 0.);
+    auto S = [&](int x, int y) -> double & { return E.psat[(size_t)y * n + x]; };
+    auto F = [&](int x, int y) { return E.pfunc[(size_t)y * n + x]; };
+    S(0, 0) = F(0, 0);
+    for (int x = 1; x < n; ++x) S(x, 0) = F(x, 0) + S(x - 1, 0);
+    for (int y = 1; y < n; ++y) S(0, y) = F(0, y) + S(0, y - 1);
+    for (int y = 1; y < n; ++y)
+        for (int x = 1; x < n; ++x) S(x, y) = (F(x, y) + S(x - 1, y) + S(x, y - 1) - S(x - 1, y - 1));
+    for (int i = 0; i < k; ++i) {
+        const float *x = q + 8 * i;
+        float *o = out + 5 * i;
+        std::fill(o, o + 5, 0.f);
+        const Float b[4] = {x[2], x[3], x[4], x[5]};
+        Float px, py, pdf;
+        if (E.WindowedSample(x[0], x[1], b, &px, &py, &pdf)) o[0] = 1, o[1] = px, o[2] = py, o[3] = pdf;
+        const Float bi = E.Integral(b[0], b[1], b[2], b[3]);
+        o[4] = bi == 0 ? 0.f : E.FuncEval(x[6], x[7]) / bi;
+    }
+    return 0;
+}
 // the oracle's MeasuredBxDF (omeas) read from `path`, on queries laid out as pbrt_debug_measured's:
 // in[8] {wo, wi, u0, u1} at the wavelengths lambda[NS] -> out[68] {f[NS], PDF, ok, wi, pdf, f[NS]}
 int oracle_measured_eval(const char *path, const float *in, int n, const float *lambda, float *out) {
@@ -7249,10 +7351,13 @@ int oracle_texture_eval(const pbrt_scene_flat *flat, const pbrt_scene_info *info
         out[4] = t.EvalF(node, c);
         return 0;
     }
-    for (int i = 0; i < n; ++i) {
+    // the wavelengths in groups of NS, lambda[i] at sample index i % NS (a multispectral basis
+    // is indexed by the sample index)
+    for (int i0 = 0; i0 < n; i0 += NS) {
         Wavelengths L = Wavelengths::SampleUniform(0.f);
-        for (int k = 0; k < NS; ++k) L.lambda[k] = lambda[i];
-        out[4 + i] = t.EvalS(node, c, L)[0];
+        for (int k = 0; k < NS; ++k) L.lambda[k] = lambda[std::min(i0 + k, n - 1)];
+        const Spectrum v = t.EvalS(node, c, L);
+        for (int k = 0; k < NS && i0 + k < n; ++k) out[4 + i0 + k] = v[k];
     }
     return 0;
 }

@@ -51,6 +51,9 @@ def lib():
         _lib.oracle_hair_eval.argtypes = [vp, ctypes.c_int, vp]
         _lib.oracle_measured_eval.argtypes = [ctypes.c_char_p, vp, ctypes.c_int, vp, vp]
         _lib.oracle_portal_eval.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, vp, vp]
+        _lib.oracle_pl2d.argtypes = [ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int] + [vp] * 4 + [
+            ctypes.c_int, vp]
+        _lib.oracle_windowed2d.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, vp]
         _lib.oracle_triangle_shading.argtypes = [vp] * 3 + [ctypes.c_int] + [vp] * 3
         _lib.oracle_render.argtypes = [vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, vp]
@@ -440,6 +443,32 @@ def measured_eval(path, queries, lambdas):
     out = np.zeros((len(q), 68), np.float32)
     if lib().oracle_measured_eval(str(path).encode(), q.ctypes.data, len(q), lam.ctypes.data, out.ctypes.data) != 0:
         raise OSError(f"oracle: cannot read {path}")
+    return out
+
+
+def pl2d(dim, cdf, data, xs, ys, pr, pv0, pv1, queries):
+    """The oracle's PiecewiseLinear2D<dim> (normalised; CDF iff cdf) over data [pr0][pr1][ys][xs] on
+    [n][6] queries {u0, u1, px, py, p0, p1} -> [n][7] {Sample xy pdf, Invert xy pdf, Evaluate}."""
+    d = np.ascontiguousarray(data, np.float32)
+    pr = np.ascontiguousarray(pr, np.int32)
+    a0, a1 = np.ascontiguousarray(pv0, np.float32), np.ascontiguousarray(pv1, np.float32)
+    q = np.ascontiguousarray(queries, np.float32).reshape(-1, 6)
+    out = np.zeros((len(q), 7), np.float32)
+    if lib().oracle_pl2d(dim, cdf, d.ctypes.data, xs, ys, pr.ctypes.data, a0.ctypes.data, a1.ctypes.data,
+                         q.ctypes.data, len(q), out.ctypes.data) != 0:
+        raise ValueError("oracle_pl2d: bad table")
+    return out
+
+
+def windowed2d(func, queries):
+    """The oracle's WindowedPiecewiseConstant2D over func [n][n] on [k][8] queries
+    {u0, u1, b0, b1, b2, b3, qx, qy} -> [k][5] {ok, x, y, pdf, PDF(q, b)}."""
+    f = np.ascontiguousarray(func, np.float32)
+    n = int(round(np.sqrt(f.size)))
+    q = np.ascontiguousarray(queries, np.float32).reshape(-1, 8)
+    out = np.zeros((len(q), 5), np.float32)
+    if lib().oracle_windowed2d(f.ctypes.data, n, q.ctypes.data, len(q), out.ctypes.data) != 0:
+        raise ValueError("oracle_windowed2d: bad table")
     return out
 
 

@@ -167,14 +167,18 @@ struct TexTables {
     std::vector<float> nodeParams, specFlat, rawGamma;
     std::vector<uint8_t> rawData;
     std::vector<uint64_t> rawOffset;
+    std::vector<float> basis;  // multispectral basis tables (never empty: one pad entry)
 };
 static void BuildTexTables(const SceneDesc &s, TexTables *t) {
     *t = TexTables{};
+    t->basis = s.texBasis;
+    t->basis.push_back(0.f);
     for (size_t i = 0; i < s.textures.size(); ++i) {
         const TextureDesc &d = s.textures[i];
         DeviceTexNode n{};
         n.kind = d.kind;
-        n.flags = (d.spectrum ? 1 : 0) | (d.specType << 1) | (d.invert ? 8 : 0) | (d.mapping == kMap3D ? 16 : 0);
+        n.flags = (d.spectrum ? 1 : 0) | (d.specType << 1) | (d.invert ? 8 : 0) | (d.mapping == kMap3D ? 16 : 0) |
+                  (d.basis >= 0 ? kTexNodeBasis : 0);
         n.child0 = d.child[0];
         n.child1 = d.child[1];
         n.child2 = d.child[2];
@@ -189,6 +193,10 @@ static void BuildTexTables(const SceneDesc &s, TexTables *t) {
             for (int k = 0; k < 3; ++k) n.p[22 + k] = d.dir[k];
         n.p[26] = d.scale;
         n.p[27] = d.maxAniso;
+        if (d.basis >= 0) {  // the multispectral basis table: start in texBasis, length
+            n.p[22] = (float)d.basis;
+            n.p[24] = (float)d.basisWidth;
+        }
         if (d.kind >= kTexDots) {  // procedural: octaves, omega, variation (core/texture_eval.h)
             n.p[22] = (float)d.octaves;
             n.p[23] = d.omega;
@@ -260,7 +268,9 @@ static CameraDiff MakeCameraDiff(const SceneDesc &s) {
     c.minPosDy = V3(s.minPosDy[0], s.minPosDy[1], s.minPosDy[2]);
     c.minDirDx = V3(s.minDirDx[0], s.minDirDx[1], s.minDirDx[2]);
     c.minDirDy = V3(s.minDirDy[0], s.minDirDy[1], s.minDirDy[2]);
-    c.sppScale = std::max<float>(.125f, 1 / std::sqrt((float)s.spp));  // cameras.h:187-190
+    // cameras.h:187-190; Option "disablepixeljitter" takes the full pixel footprint
+    c.sppScale = (s.options & kOptNoPixelJitter) ? 1.f : std::max<float>(.125f, 1 / std::sqrt((float)s.spp));
+    c.noFilter = (s.options & kOptNoTextureFiltering) ? 1 : 0;  // surfscatter.cpp:77
     return c;
 }
 // a TexView over host copies (debug entry points; the device view points at DevBufs)
@@ -279,6 +289,7 @@ static TexView HostTexView(const TexTables &t) {
     v.rgbCoeffs = rgb.data() + 64;
     v.ewaLut = GetSpectralData().mipFilterLUT.data();
     v.noisePerm = GetSpectralData().noisePerm.data();
+    v.basis = t.basis.data();
     v.nProgs = (int)t.progs.size();
     v.nLuts = (int)t.images.size();
     return v;
@@ -532,7 +543,7 @@ struct pbrt_context {
     DevBuf<DeviceImage> texImages;
     DevBuf<DeviceImageLevel> texLevels;
     DevBuf<uint8_t> texData;
-    DevBuf<float> texLuts, rgbTable, ewaLut, noisePerm;
+    DevBuf<float> texLuts, rgbTable, ewaLut, noisePerm, texBasis;
     DevBuf<DeviceTexInstr> texInstrs;
     DevBuf<DeviceTexProgram> texProgs;
     DevBuf<int> matTex;
@@ -1141,7 +1152,7 @@ static void BuildDevice(pbrt_context *c) {
                     std::any_of(s.materials.begin(), s.materials.end(), [](const MaterialDesc &m) {
                         return m.type == kMatInterface || m.type == kMatCoatedDiffuse || m.type == kMatCoatedConductor ||
                                m.type == kMatThinDielectric || m.type == kMatDiffuseTransmission || m.type == kMatHair ||
-                               m.type == kMatMeasured;
+                               m.type == kMatMeasured || m.type == kMatRetroreflective;
                     });
     S.dispersive = std::any_of(s.materials.begin(), s.materials.end(),
                                [](const MaterialDesc &m) { return ((m.type == kMatDielectric || m.type == kMatThinDielectric) && m.etaSpec >= 0) || m.ifaceEtaSpec >= 0;
@@ -1284,6 +1295,8 @@ static void BuildDevice(pbrt_context *c) {
             S.tex.ewaLut = c->ewaLut.p;
             c->noisePerm.Upload(GetSpectralData().noisePerm);  // procedural textures' Perlin noise
             S.tex.noisePerm = c->noisePerm.p;
+            c->texBasis.Upload(tt.basis);
+            S.tex.basis = c->texBasis.p;
             S.tex.nProgs = (int)tt.progs.size();
             S.tex.nLuts = (int)tt.images.size();
             S.camDiff = MakeCameraDiff(s);
@@ -1379,6 +1392,7 @@ static void BuildDevice(pbrt_context *c) {
             S.renderFromCamera[4 * i + j] = (float)s.camera.renderFromCamera[i][j];
         }
     S.lensRadius = s.camera.lensRadius;
+    S.options = s.options;
     S.focalDistance = s.camera.focalDistance;
     S.xres = s.xres;
     S.yres = s.yres;
@@ -1572,7 +1586,9 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
     // (a producer's block b pushes into shard b % kShards and its grid is a multiple of kShards,
     // so each producer overshoots a shard's share by less than one chunk; up to kShards producers)
     const int64_t capS = ((N + kShards - 1) / kShards + 256 * kShards + 63) / 64 * 64;
-    const int64_t NR = capS * kShards;  // record stride
+    // record stride: the shards plus a trash area whose last slot takes the writes of a full
+    // shard (ShardSlot), so an overflow never lands in another shard or past the arrays
+    const int64_t NR = capS * kShards + kQueueTrash;
     // kernels index [k][NR] arrays with 32-bit k * NR for k <= 11 (spectral ones use size_t)
     if (NR > INT32_MAX / 12) throw Error("max_paths too large: " + std::to_string(N));
     // per pixel-sample arrays (L, filterW) use N; the rest NR (>= N)
@@ -2085,6 +2101,7 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
         f->tex_node_params = t.nodeParams.data();
         f->noise_perm = GetSpectralData().noisePerm.data();
         f->tex_node_spec = t.specFlat.data();
+        f->tex_basis = t.basis.data();
         f->image_info = t.imageInfo.data();
         f->image_levels = t.levelInfo.data();
         f->image_data = t.data.data();
@@ -2157,6 +2174,7 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
     f->env_portal = scene->envPortal.empty() ? nullptr : scene->envPortal.data();
     scene->measuredFiles.clear();
     for (const MeasuredDesc &b : s.measured) scene->measuredFiles.push_back(b.path.c_str());
+    f->options = s.options;
     f->n_measured = (int)s.measured.size();
     f->measured_files = s.measured.empty() ? nullptr : scene->measuredFiles.data();
     f->dims_per_depth = s.sss.empty() ? 7 : 10;
@@ -2690,7 +2708,85 @@ int pbrt_debug_texture_eval(const pbrt_scene *scene, int material, int slot, con
             return 0;
         }
         for (int i = 0; i < n; ++i)
-            out[4 + i] = pg.simple ? SigmoidPolynomial(R[0], R[1], R[2], lambda[i]) : TexPhase2(T, pg, R, lambda[i]);
+            out[4 + i] = pg.simple ? SigmoidPolynomial(R[0], R[1], R[2], lambda[i]) : TexPhase2(T, pg, R, lambda[i], i % kNSpectrumSamples);
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_debug_pl2d(int dim, int cdf, const float *data, int xs, int ys, const int *pr2, const float *pv0,
+                    const float *pv1, const float *q6, int n, float *out7) {
+    try {
+        if (!data || !q6 || !out7 || n < 0) return Fail("pbrt_debug_pl2d: null argument");
+        if (dim != 0 && dim != 2) return Fail("pbrt_debug_pl2d: dim must be 0 or 2");
+        if (xs < 2 || ys < 2) return Fail("pbrt_debug_pl2d: the table needs at least 2x2 values");
+        if (dim == 2 && (!pr2 || !pv0 || !pv1 || pr2[0] < 1 || pr2[1] < 1))
+            return Fail("pbrt_debug_pl2d: bad parameter grids");
+        std::vector<float> blob;
+        if (dim == 2) {
+            blob.assign(pv0, pv0 + pr2[0]);
+            blob.insert(blob.end(), pv1, pv1 + pr2[1]);
+        }
+        const uint32_t slices = dim == 2 ? (uint32_t)(pr2[0] * pr2[1]) : 1u;
+        int h[5];
+        BuildPL2D(data, xs, ys, slices, true, cdf != 0, &blob, h);
+        PL2D d{};
+        d.sx = h[0];
+        d.sy = h[1];
+        d.np = dim;
+        d.data = blob.data() + h[2];
+        d.marg = h[3] >= 0 ? blob.data() + h[3] : nullptr;
+        d.cond = h[4] >= 0 ? blob.data() + h[4] : nullptr;
+        // the parameter grids lead the blob (BuildPL2D appends after them)
+        for (int i = 0; i < 3; ++i) {
+            d.pn[i] = (dim == 2 && i < 2) ? pr2[i] : 1;
+            d.pv[i] = blob.data() + (dim == 2 && i == 1 ? pr2[0] : 0);
+        }
+        for (int k = 0; k < n; ++k) {
+            const float *x = q6 + 6 * (size_t)k;
+            float *o = out7 + 7 * (size_t)k;
+            std::fill(o, o + 7, 0.f);
+            const float par[2] = {x[4], x[5]};
+            if (dim == 0) {
+                if (cdf) {
+                    PLSample<0>(d, x[0], x[1], par, &o[0], &o[1], &o[2]);
+                    PLInvert<0>(d, x[2], x[3], par, &o[3], &o[4], &o[5]);
+                }
+                o[6] = PLEvaluate<0>(d, x[2], x[3], par);
+            } else {
+                if (cdf) {
+                    PLSample<2>(d, x[0], x[1], par, &o[0], &o[1], &o[2]);
+                    PLInvert<2>(d, x[2], x[3], par, &o[3], &o[4], &o[5]);
+                }
+                o[6] = PLEvaluate<2>(d, x[2], x[3], par);
+            }
+        }
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_debug_windowed2d(const float *func, int res, const float *q8, int n, float *out5) {
+    try {
+        if (!func || !q8 || !out5 || n < 0 || res < 1) return Fail("pbrt_debug_windowed2d: bad arguments");
+        const std::vector<float> f(func, func + (size_t)res * res);
+        const std::vector<float> sat = SummedAreaTable(f, res);
+        DeviceEnvLight E{};
+        E.res = res;
+        E.sat = sat.data();
+        E.func = f.data();
+        for (int k = 0; k < n; ++k) {
+            const float *x = q8 + 8 * (size_t)k;
+            float *o = out5 + 5 * (size_t)k;
+            std::fill(o, o + 5, 0.f);
+            const float b[4] = {x[2], x[3], x[4], x[5]};
+            float px, py, pdf;
+            if (PortalWindowedSample(E, x[0], x[1], b, &px, &py, &pdf)) o[0] = 1, o[1] = px, o[2] = py, o[3] = pdf;
+            const float bi = SatIntegral(E, b[0], b[1], b[2], b[3]);
+            o[4] = bi == 0 ? 0.f : PortalFuncAt(E, x[6], x[7]) / bi;
+        }
         return 0;
     } catch (const std::exception &e) {
         return Fail(e.what());
@@ -3107,8 +3203,10 @@ int pbrt_debug_named_spectrum(const char *name, const float *lambda, int n, floa
 int pbrt_debug_bxdf(int type, const float *params, const float *eta31, const float *k31, const float *wo3,
                     const float *wi3, const float *u3, float *out) {
     if (!params || !wo3 || !wi3 || !u3 || !out) return Fail("null argument");
-    if (type == kMatConductor && (!eta31 || !k31)) return Fail("conductor needs eta and k");
-    if (type != kMatDielectric && type != kMatConductor) return Fail("type must be 1 (dielectric) or 2 (conductor)");
+    if ((type == kMatConductor || type == kMatRetroreflective) && (!eta31 || !k31))
+        return Fail("conductor / retroreflective needs eta and k");
+    if (type != kMatDielectric && type != kMatConductor && type != kMatRetroreflective)
+        return Fail("type must be 1 (dielectric), 2 (conductor) or 11 (retroreflective)");
     const TrowbridgeReitz tr{params[0], params[1]};
     const float eta = params[2];
     const V3 wo(wo3[0], wo3[1], wo3[2]), wi(wi3[0], wi3[1], wi3[2]);
@@ -3124,6 +3222,17 @@ int pbrt_debug_bxdf(int type, const float *params, const float *eta31, const flo
         float f = DielectricEval(eta, tr, wo, wi, &pdf);
         for (int i = 0; i < kNSpectrumSamples; ++i) out[38 + i] = f;
         out[69] = pdf;
+    } else if (type == kMatRetroreflective) {
+        const ConductorTerms ct = RetroSample(tr, wo, u3[1], u3[2]);
+        if (ct.ok) {
+            const float v[7] = {1, ct.wi.x, ct.wi.y, ct.wi.z, ct.pdf, (float)(kBxReflection | (ct.specular ? kBxSpecular : kBxGlossy)), 1};
+            memcpy(out, v, sizeof v);
+            for (int i = 0; i < kNSpectrumSamples; ++i) out[7 + i] = ConductorF(ct, eta31[i], k31[i]);
+        }
+        const RetroTerms rt = RetroEval(tr, wo, wi);
+        if (rt.ok)
+            for (int i = 0; i < kNSpectrumSamples; ++i) out[38 + i] = RetroF(rt, eta31[i], k31[i]);
+        out[69] = RetroPDF(tr, wo, wi);
     } else {
         ConductorTerms ct = ConductorSample(tr, wo, u3[1], u3[2]);
         if (ct.ok) {

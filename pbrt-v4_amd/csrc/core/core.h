@@ -110,6 +110,11 @@ PHD float Sinhf(float x) { return std::sinh(x); }
 PHD float Tanf(float x) { return std::tan(x); }
 #endif
 
+// Scene Options (BasicSceneBuilder::Option, scene.cpp:492-560) that change the hot path
+constexpr int kOptNoPixelJitter = 1;       // GetCameraSample (samplers.h:807-812), Approximate_dp_dxy
+constexpr int kOptNoWavelengthJitter = 2;  // wavefront/camera.cpp:55
+constexpr int kOptNoTextureFiltering = 4;  // wavefront/surfscatter.cpp:77
+
 PHD float Sqr(float v) { return v * v; }
 PHD float Clampf(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
 PHD float Lerpf(float t, float a, float b) { return (1 - t) * a + t * b; }
@@ -1313,6 +1318,54 @@ PHD ConductorTerms ConductorEval(const TrowbridgeReitz &tr, V3 wo, V3 wi) {
     c = ConductorTerms{true, false, wi, tr.PDF(wo, wmf) / (4 * AbsDot(wo, wmf)), tr.D(wm), tr.G(wo, wi), cosTheta_i,
                        cosTheta_o, AbsDot(wo, wm)};
     return c;
+}
+
+// RetroreflectiveBxDF, this fork's material (bxdfs.h:102-215), kept with its quirks:
+//  * Sample_f: the smooth case returns wi = wo (FrComplex(|cos wi|) / |cos wi|, pdf 1); the rough
+//    case is ConductorBxDF's microfacet reflection sample with the conductor's f (no retro lobe);
+//  * f: (1 - (R_i - R_o)) times the sum of a retro lobe (D(wo), Fresnel at |wi . wo|) and the
+//    conductor lobe, R_o = FrDielectric(wo . wm, 1.59), R_i = FrDielectric(wi . wo, 1.59);
+//  * PDF: the conductor's, which ignores the retro lobe.
+PHD int RetroFlags(const TrowbridgeReitz &tr) { return kBxReflection | (tr.EffectivelySmooth() ? kBxSpecular : kBxGlossy); }
+PHD ConductorTerms RetroSample(const TrowbridgeReitz &tr, V3 wo, float u0, float u1) {
+    if (!tr.EffectivelySmooth()) return ConductorSample(tr, wo, u0, u1);
+    ConductorTerms c{true, true, wo, 1, 0, 0, AbsCosTheta(wo), 0, AbsCosTheta(wo)};
+    return c;
+}
+// f's wavelength-independent terms; ok = false: f = 0
+struct RetroTerms {
+    bool ok;
+    float w;                   // 1 - (R_i - R_o)
+    float Dr, Dm, G, denom;    // D(wo), D(wm), G(wo, wi), 4 cos_i cos_o
+    float cosRetro, cosM;      // FrComplex arguments |wi . wo|, |wo . wm|
+};
+PHD RetroTerms RetroEval(const TrowbridgeReitz &tr, V3 wo, V3 wi) {
+    RetroTerms t{false, 0, 0, 0, 0, 0, 0, 0};
+    if (!SameHemisphere(wo, wi) || tr.EffectivelySmooth()) return t;
+    const float cosTheta_o = AbsCosTheta(wo), cosTheta_i = AbsCosTheta(wi);
+    if (cosTheta_i == 0 || cosTheta_o == 0) return t;
+    V3 wm = wo + wi;
+    const V3 wmRetro = wo;
+    if (LengthSquared(wm) == 0) return t;
+    wm = Normalize(wm);
+    const float R_o = FrDielectric(Dot(wo, wm), 1.59f), R_i = FrDielectric(Dot(wi, wmRetro), 1.59f);
+    t = RetroTerms{true, 1 - (R_i - R_o), tr.D(wmRetro), tr.D(wm), tr.G(wo, wi), 4 * cosTheta_i * cosTheta_o,
+                   AbsDot(wi, wmRetro), AbsDot(wo, wm)};
+    return t;
+}
+// one wavelength of f: w * (D(wo) F_retro G / denom) + w * (D(wm) F G / denom), pbrt's order
+PHD float RetroF(const RetroTerms &t, float eta, float k) {
+    const float Fr = FrComplex(t.cosRetro, eta, k), F = FrComplex(t.cosM, eta, k);
+    const float retro = t.Dr * Fr * t.G / t.denom;
+    return t.w * retro + t.w * (t.Dm * F * t.G / t.denom);
+}
+// PDF (bxdfs.h:182-201): the conductor's microfacet reflection density
+PHD float RetroPDF(const TrowbridgeReitz &tr, V3 wo, V3 wi) {
+    if (!SameHemisphere(wo, wi) || tr.EffectivelySmooth()) return 0;
+    V3 wh = wo + wi;
+    if (LengthSquared(wh) == 0) return 0;
+    wh = FaceForward(Normalize(wh), V3(0, 0, 1));
+    return tr.PDF(wo, wh) / (4 * AbsDot(wo, wh));
 }
 
 // ---------------------------------------------------------------- ZSobol sampler

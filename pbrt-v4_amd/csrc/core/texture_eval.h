@@ -60,10 +60,13 @@ enum TexOp1 : int {
     kT1FMix = 6, kT1FDMix = 7, kT1SImage = 8, kT1BilerpW = 9,
     // procedural: FBm, Turbulence (wrinkled), windy (float textures), the polka-dot selector,
     // a float select by it, and marble's RGBAlbedoSpectrum coefficients (4 registers)
-    kT1FBm = 10, kT1Wrinkled = 11, kT1Windy = 12, kT1DotsW = 13, kT1FSel = 14, kT1Marble = 15
+    kT1FBm = 10, kT1Wrinkled = 11, kT1Windy = 12, kT1DotsW = 13, kT1FSel = 14, kT1Marble = 15,
+    kT1SBasisRGB = 16  // a basis image's raw filtered RGB (no scale, invert or clamp)
 };
 // phase-2 ops (per wavelength: value stack)
-enum TexOp2 : int { kT2Const = 0, kT2RGBReg = 1, kT2Scale = 2, kT2Mix = 3, kT2DMix = 4, kT2Bilerp = 5, kT2Sel = 6 };
+enum TexOp2 : int { kT2Const = 0, kT2RGBReg = 1, kT2Scale = 2, kT2Mix = 3, kT2DMix = 4, kT2Bilerp = 5, kT2Sel = 6,
+                    kT2Basis = 7 };
+constexpr int kTexNodeBasis = 32;  // DeviceTexNode::flags: an image texture with a multispectral basis
 constexpr int kTexMaxRegs = 16, kTexMaxStack = 8;
 
 struct TexView {
@@ -79,6 +82,7 @@ struct TexView {
     const float *rgbCoeffs;     // RGBToSpectrumTable data[3][64][64][64][3]
     const float *ewaLut;        // MIPFilterLUT[128]
     const float *noisePerm;     // util/noise.cpp NoisePerm[512] (procedural textures)
+    const float *basis;         // multispectral basis tables (SceneDesc::texBasis)
     int nProgs;
     int nLuts;                  // images (one 256-entry decode table each)
 };
@@ -95,7 +99,8 @@ struct CameraDiff {
     float cameraFromRender[12];  // 3x4 (renderFromCamera^-1)
     float renderFromCamera[9];   // upper 3x3
     V3 minPosDx, minPosDy, minDirDx, minDirDy;
-    float sppScale;              // max(.125, 1 / sqrt(spp))
+    float sppScale;              // max(.125, 1 / sqrt(spp)); 1 with Option "disablepixeljitter"
+    int noFilter;                // Option "disabletexturefiltering": no differentials
 };
 
 // Transform::ApplyInverse(Point3f) of a 3x4 inverse matrix (transform.h:387-398)
@@ -152,6 +157,10 @@ PHD bool IsFiniteF(float x) { return !std::isinf(x) && !std::isnan(x); }
 
 // surfscatter.cpp:74-104: screen-space (u,v) derivatives from dp/dx, dp/dy and dpdu, dpdv
 PHD void UVDerivatives(const CameraDiff &c, V3 p, V3 n, V3 dpdu, V3 dpdv, TexEvalCtx *ctx) {
+    if (c.noFilter) {  // dudx = dudy = dvdx = dvdy = 0 (surfscatter.cpp:76-77)
+        ctx->dudx = ctx->dudy = ctx->dvdx = ctx->dvdy = 0.f;
+        return;
+    }
     V3 dpdx, dpdy;
     ApproximateDpDxy(c, p, n, &dpdx, &dpdy);
     const float ata00 = Dot(dpdu, dpdu), ata01 = Dot(dpdu, dpdv), ata11 = Dot(dpdv, dpdv);
@@ -541,14 +550,21 @@ PHD float FloatImageEval(const TexView &T, const DeviceTexNode &nd, const TexEva
     return (nd.flags & 8) ? std::fmax(0.f, 1 - v) : v;
 }
 // SpectrumImageTexture::Evaluate's RGB (textures.cpp:386-397) reduced to the sigmoid
-// coefficients and scale of its RGBAlbedoSpectrum / RGBUnboundedSpectrum
+// coefficients and scale of its RGBAlbedoSpectrum / RGBUnboundedSpectrum.  basisRaw: a
+// multispectral basis image's texel instead, out[0..2] = the filtered RGB without scale or invert
+// (textures.h:660-670; one MipFilter instance for both, which keeps the callers' registers)
 template <bool AllowEWA = true>
-PHD void SpectrumImageCoeffs(const TexView &T, const DeviceTexNode &nd, const TexEvalCtx &c, float out[4]) {
+PHD void SpectrumImageCoeffs(const TexView &T, const DeviceTexNode &nd, const TexEvalCtx &c, float out[4],
+                             bool basisRaw = false) {
     TexCoord2 tc = MapST(nd, c);
     tc.t = 1 - tc.t;
     const DeviceImage im = T.images[nd.image];
     const MipVal<true> f =
         MipFilter<true, AllowEWA>(T, im, nd.filter, nd.p[27], tc.s, tc.t, tc.dsdx, tc.dtdx, tc.dsdy, tc.dtdy);
+    if (basisRaw) {
+        for (int i = 0; i < 3; ++i) out[i] = f.v[i];
+        return;
+    }
     const float sc = nd.p[26];
     float rgb[3] = {sc * f.v[0], sc * f.v[1], sc * f.v[2]};
     for (int i = 0; i < 3; ++i) rgb[i] = std::fmax(0.f, (nd.flags & 8) ? 1 - rgb[i] : rgb[i]);
@@ -703,7 +719,8 @@ PHD void TexPhase1(const TexView &T, const DeviceTexProgram &pg, const TexEvalCt
             R[a] = amt * t1 + (1 - amt) * t2;
             break;
         }
-        case kT1SImage: SpectrumImageCoeffs(T, nd, c, R + a); break;
+        case kT1SImage:
+        case kT1SBasisRGB: SpectrumImageCoeffs(T, nd, c, R + a, op == kT1SBasisRGB); break;
         case kT1FBm:
         case kT1Wrinkled:
         case kT1Windy: {
@@ -747,8 +764,26 @@ PHD float TexSpecConstAt(const DeviceTexSpec &s, float lambda) {
     return s.value;
 }
 
-// phase 2 at one wavelength: the spectrum texture's value, in pbrt's operation order
-PHD float TexPhase2(const TexView &T, const DeviceTexProgram &pg, const float *R, float lambda) {
+// GPUSpectrumImageTexture::Evaluate's basis branch (textures.h:655-679, the fork's multispectral
+// textures): s = sum over channels c of basis_c * (tex_c - offset), where basis_c at wavelength
+// sample i is the table's entry 3 + i + c * NSpectrumSamples (tex1D, clamp addressing: indexed by
+// the sample's position, not its wavelength), offset = int(table[2]), no scale
+PHD float BasisAt(const TexView &T, const DeviceTexNode &nd, const float *rgb, int wi) {
+    const float *tab = T.basis + (int)nd.p[22];
+    const int width = (int)nd.p[24];
+    const int nChannels = (int)tab[0], offset = (int)tab[2];
+    float s = 0;
+    for (int c = 0; c < nChannels; ++c) {
+        int k = 3 + wi + c * kNSpectrumSamples;
+        k = k < width ? k : width - 1;
+        s = tab[k] * (rgb[c] - (float)offset) + s;
+    }
+    return s;
+}
+
+// phase 2 at one wavelength (its sample index wi and value lambda): the spectrum texture's value,
+// in pbrt's operation order
+PHD float TexPhase2(const TexView &T, const DeviceTexProgram &pg, const float *R, float lambda, int wi) {
     float st[kTexMaxStack];
     int sp = 0;
     for (int k = 0; k < pg.n2; ++k) {
@@ -787,6 +822,7 @@ PHD float TexPhase2(const TexView &T, const DeviceTexProgram &pg, const float *R
             st[sp - 1] = R[a] != 0 ? tIn : tOut;
             break;
         }
+        case kT2Basis: st[sp++] = BasisAt(T, T.nodes[in.node], R + a, wi); break;
         case kT2Bilerp: {
             const float v3 = st[sp - 1], v2 = st[sp - 2], v1 = st[sp - 3], v0 = st[sp - 4];
             sp -= 3;

@@ -76,6 +76,8 @@ std::map<std::string, TensorField> ReadTensorFile(const std::string &path) {
     return fields;
 }
 
+}  // namespace
+
 // PiecewiseLinear2D<D>(data, xSize, ySize, paramRes, ..., normalize, buildCdf): appends the
 // density values (and the CDFs) to blob; h = {sx, sy, data, marginal, conditional}
 void BuildPL2D(const float *data, int xSize, int ySize, uint32_t slices, bool normalize, bool buildCdf,
@@ -141,8 +143,6 @@ void BuildPL2D(const float *data, int xSize, int ySize, uint32_t slices, bool no
     h[3] = append(marg);
     h[4] = append(cond);
 }
-
-}  // namespace
 
 MeasuredDesc LoadMeasuredBRDF(const std::string &path) {
     const auto tf = ReadTensorFile(path);

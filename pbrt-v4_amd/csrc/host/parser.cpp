@@ -19,6 +19,8 @@
 #include "texture.h"
 
 namespace pbrt_amd {
+// multispectral basis files (below, beside the texture instantiation)
+void ReadBasisFile(const std::string &path, const std::string &loc, std::vector<float> *out);
 // host/subdiv.cpp
 void LoopSubdivideMesh(int nLevels, const std::vector<int> &indices, const std::vector<V3> &p, std::vector<V3> *P,
                        std::vector<int> *tris, std::vector<V3> *N);
@@ -246,6 +248,7 @@ struct Param {
     std::vector<std::string> strs;
     std::vector<bool> bools;
     bool used = false;
+    bool attribute = false;  // from an Attribute directive: may go unused (scene.cpp:209-213)
 };
 struct ParamSet {
     std::vector<Param> params;
@@ -276,12 +279,23 @@ struct ParamSet {
     }
     void CheckUnused() const {
         for (auto &p : params)
-            if (!p.used) throw Error(loc + ": parameter \"" + p.type + " " + p.name + "\" is not supported");
+            if (!p.used && !p.attribute)
+                throw Error(loc + ": parameter \"" + p.type + " " + p.name + "\" is not supported");
     }
 };
+// ParameterDictionary(params, attributes) (paramdict.cpp:150-159): a directive's own parameters
+// first, then the graphics state's Attribute parameters of its target, latest first, so a lookup
+// finds the directive's value, else the most recent attribute
+static ParamSet WithAttributes(ParamSet own, const std::vector<Param> &attributes) {
+    for (auto it = attributes.rbegin(); it != attributes.rend(); ++it) own.params.push_back(*it);
+    return own;
+}
 
 struct GraphicsState {
     Mat4 ctm = Identity4();
+    // Attribute "shape" / "light" / "material" / "medium" / "texture" parameters (scene.cpp:189-215),
+    // scoped by AttributeBegin / AttributeEnd like the rest of the graphics state
+    std::vector<Param> shapeAttributes, lightAttributes, materialAttributes, mediumAttributes, textureAttributes;
     bool reverseOrientation = false;
     int material = -1;  // index into materials (-1 -> default diffuse)
     std::string areaLightName;
@@ -422,6 +436,62 @@ class Parser {
 
     static std::string Loc(const Token &t) { return t.file + ":" + std::to_string(t.line); }
 
+    // BasicSceneBuilder::Option (scene.cpp:492-560) with the wavefront integrator's refusals
+    // (wavefront/integrator.cpp:202-212)
+    enum { kRenderCamera = 0, kRenderCameraWorld = 1, kRenderWorld = 2 };
+    int renderSpace = kRenderCameraWorld;
+    bool optionSeedSet = false;
+    int optionSeed = 0;
+    void Option(const std::string &name, const Token &v, const std::string &loc) {
+        std::string n;  // normalizeArg (util/args.h:23-30)
+        for (unsigned char c : name)
+            if (c != '_' && c != '-') n += (char)std::tolower(c);
+        const std::string raw = v.isString ? "\"" + v.text + "\"" : v.text;  // the token as pbrt sees it
+        auto boolean = [&]() {
+            if (raw == "true") return true;
+            if (raw == "false") return false;
+            throw Error(loc + ": " + raw + ": expected \"true\" or \"false\" for option value");
+        };
+        auto quoted = [&]() {
+            if (!v.isString || v.text.empty()) throw Error(loc + ": " + raw + ": expected quoted string for option value");
+            return v.text;
+        };
+        if (n == "disablepixeljitter") {
+            scene.options = boolean() ? (scene.options | kOptNoPixelJitter) : (scene.options & ~kOptNoPixelJitter);
+        } else if (n == "disabletexturefiltering") {
+            scene.options = boolean() ? (scene.options | kOptNoTextureFiltering) : (scene.options & ~kOptNoTextureFiltering);
+        } else if (n == "disablewavelengthjitter") {
+            scene.options = boolean() ? (scene.options | kOptNoWavelengthJitter) : (scene.options & ~kOptNoWavelengthJitter);
+        } else if (n == "displacementedgescale") {
+            char *end = nullptr;
+            const double e = std::strtod(raw.c_str(), &end);
+            if (v.isString || end == raw.c_str() || *end) throw Error(loc + ": " + raw + ": expected floating-point option value");
+            scene.displacementEdgeScale = (float)e;  // only displaced meshes use it: refused at their Shape
+        } else if (n == "msereferenceimage") {
+            quoted();
+            throw Error(loc + ": The wavefront integrator does not support --mse-reference-image.");
+        } else if (n == "msereferenceout") {
+            quoted();  // the MSE output of a reference image, which the wavefront refuses anyway
+        } else if (n == "rendercoordsys") {
+            const std::string cs = quoted();
+            if (cs == "camera") renderSpace = kRenderCamera;
+            else if (cs == "cameraworld") renderSpace = kRenderCameraWorld;
+            else if (cs == "world") renderSpace = kRenderWorld;
+            else throw Error(loc + ": " + cs + ": unknown rendering coordinate system.");
+        } else if (n == "seed") {
+            optionSeedSet = true;
+            optionSeed = std::atoi(raw.c_str());
+        } else if (n == "forcediffuse") {
+            if (boolean()) throw Error(loc + ": The wavefront integrator does not support --force-diffuse.");
+        } else if (n == "pixelstats") {
+            if (boolean()) throw Error(loc + ": The wavefront integrator does not support --pixelstats.");
+        } else if (n == "wavefront") {
+            boolean();  // this library is the wavefront integrator either way
+        } else {
+            throw Error(loc + ": " + name + ": unknown option");
+        }
+    }
+
     double Num(const std::vector<Token> &toks, size_t &pos) {
         if (pos >= toks.size()) throw Error("unexpected end of file");
         const Token &t = toks[pos++];
@@ -541,16 +611,34 @@ class Parser {
             scene.integratorName = Str(toks, pos);
             integratorParams = Params(toks, pos);
             integratorParams.loc = loc;
-        } else if (d == "Accelerator" || d == "Option" || d == "ColorSpace" || d == "Attribute") {
-            if (d == "ColorSpace") {
-                std::string cs = Str(toks, pos);
-                if (cs != "srgb") throw Error(loc + ": only the srgb colour space is supported");
-            } else if (d == "Option") {
-                Str(toks, pos);
-                if (pos < toks.size()) ++pos;
-            } else {
-                Str(toks, pos);
-                Params(toks, pos);
+        } else if (d == "Accelerator") {
+            Str(toks, pos);
+            Params(toks, pos);  // the BVH8 build is the aggregate whatever is asked (gpu/aggregate.cpp)
+        } else if (d == "ColorSpace") {
+            std::string cs = Str(toks, pos);
+            if (cs != "srgb") throw Error(loc + ": only the srgb colour space is supported");
+        } else if (d == "Option") {
+            // parser.cpp:877-880: a quoted name, then one raw value token
+            std::string name = Str(toks, pos);
+            if (pos >= toks.size()) throw Error(loc + ": Option needs a value");
+            Option(name, toks[pos], loc);
+            ++pos;
+        } else if (d == "Attribute") {
+            // BasicSceneBuilder::Attribute (scene.cpp:189-215)
+            std::string target = Str(toks, pos);
+            ParamSet ps = Params(toks, pos);
+            std::vector<Param> *attrs = target == "shape"      ? &gs.shapeAttributes
+                                        : target == "light"    ? &gs.lightAttributes
+                                        : target == "material" ? &gs.materialAttributes
+                                        : target == "medium"   ? &gs.mediumAttributes
+                                        : target == "texture"  ? &gs.textureAttributes
+                                                               : nullptr;
+            if (!attrs)
+                throw Error(loc + ": Unknown attribute target \"" + target +
+                            "\". Must be \"shape\", \"light\", \"material\", \"medium\", or \"texture\".");
+            for (Param &p : ps.params) {
+                p.attribute = true;
+                attrs->push_back(p);
             }
         } else if (d == "WorldBegin") {
             inWorld = true;
@@ -571,12 +659,12 @@ class Parser {
             }
         } else if (d == "Material") {
             std::string type = Str(toks, pos);
-            ParamSet ps = Params(toks, pos);
+            ParamSet ps = WithAttributes(Params(toks, pos), gs.materialAttributes);
             ps.loc = loc;
             gs.material = MakeMaterial(type, ps, "", dir);
         } else if (d == "MakeNamedMaterial") {
             std::string name = Str(toks, pos);
-            ParamSet ps = Params(toks, pos);
+            ParamSet ps = WithAttributes(Params(toks, pos), gs.materialAttributes);
             ps.loc = loc;
             std::string type = ps.GetString("type", "");
             if (type.empty()) throw Error(loc + ": MakeNamedMaterial needs \"string type\"");
@@ -587,20 +675,20 @@ class Parser {
             gs.material = namedMaterials[name];
         } else if (d == "AreaLightSource") {
             gs.areaLightName = Str(toks, pos);
-            gs.areaLightParams = Params(toks, pos);
+            gs.areaLightParams = WithAttributes(Params(toks, pos), gs.lightAttributes);
             gs.areaLightParams.loc = loc;
             if (gs.areaLightName != "diffuse") throw Error(loc + ": unsupported area light " + gs.areaLightName);
         } else if (d == "LightSource") {
             PendingLight l;
             l.type = Str(toks, pos);
-            l.params = Params(toks, pos);
+            l.params = WithAttributes(Params(toks, pos), gs.lightAttributes);
             l.params.loc = loc;
             l.worldFromLight = gs.ctm;
             l.dir = dir;
             lights.push_back(std::move(l));
         } else if (d == "Shape") {
             std::string type = Str(toks, pos);
-            ParamSet ps = Params(toks, pos);
+            ParamSet ps = WithAttributes(Params(toks, pos), gs.shapeAttributes);
             ps.loc = loc;
             Shape(type, ps, dir);
         } else if (d == "Include" || d == "Import") {
@@ -610,7 +698,7 @@ class Parser {
         } else if (d == "MakeNamedMedium") {
             PendingMedium m;
             m.name = Str(toks, pos);
-            m.params = Params(toks, pos);
+            m.params = WithAttributes(Params(toks, pos), gs.mediumAttributes);
             m.params.loc = loc;
             m.type = m.params.GetString("type", "");
             if (m.type.empty()) throw Error(loc + ": MakeNamedMedium needs \"string type\"");
@@ -646,7 +734,7 @@ class Parser {
             t.name = Str(toks, pos);
             std::string type = Str(toks, pos);
             t.cls = Str(toks, pos);
-            t.params = Params(toks, pos);
+            t.params = WithAttributes(Params(toks, pos), gs.textureAttributes);
             t.params.loc = loc;
             if (type != "float" && type != "spectrum")
                 throw Error(loc + ": " + type + ": texture type unknown. Must be \"float\" or \"spectrum\".");
@@ -896,9 +984,14 @@ class Parser {
             } else if (Param *es = ps.Find("eta", "spectrum")) {
                 m.etaSpec = SpectrumParam(es, ps.loc);  // eta(lambda_0) + TerminateSecondary
             }
-        } else if (type == "conductor") {
-            // ConductorMaterial::Create (materials.cpp:217-251)
-            m.type = kMatConductor;
+        } else if (type == "conductor" || type == "retroreflective") {
+            // ConductorMaterial::Create (materials.cpp:217-251); RetroreflectiveMaterial::Create
+            // (materials.cpp:263-297) reads the same parameters for its RetroreflectiveBxDF
+            m.type = type == "conductor" ? kMatConductor : kMatRetroreflective;
+            if (m.type == kMatRetroreflective)
+                for (const Param &q : ps.params)
+                    if (q.type == "texture" && !q.attribute)
+                        throw Error(ps.loc + ": textured parameters of the retroreflective material are not supported yet");
             Param *eta = ps.Find("eta"), *k = ps.Find("k"), *refl = ps.Find("reflectance");
             if (refl && (eta || k))
                 throw Error(ps.loc + ": For the conductor material, both \"reflectance\" and \"eta\" and \"k\" can't be provided.");
@@ -1812,9 +1905,14 @@ void Parser::Finish() {
     }
     // ---- sampler
     scene.spp = samplerParams.GetInt("pixelsamples", 16);
-    scene.seed = samplerParams.GetInt("seed", 0);
+    // the sampler's "seed" defaults to Options->seed (samplers.cpp:73 etc.): --seed (the "seed"
+    // override), replaced by a scene's Option "seed" (scene.cpp:543-544), which is parsed later
+    {
+        int optionsSeed = overrides.count("seed") ? std::stoi(overrides.at("seed")) : 0;
+        if (optionSeedSet) optionsSeed = optionSeed;
+        scene.seed = samplerParams.GetInt("seed", optionsSeed);
+    }
     if (overrides.count("spp")) scene.spp = std::stoi(overrides.at("spp"));
-    if (overrides.count("seed")) scene.seed = std::stoi(overrides.at("seed"));
     if (scene.samplerName == "halton") {
         scene.samplerType = 0;
         if (samplerParams.GetString("randomization", "permutedigits") != "permutedigits")
@@ -1900,7 +1998,10 @@ void Parser::Finish() {
     {
         Mat4 worldFromCamera = Inverse4(cameraFromWorld);
         V3 pCam = XformPoint(worldFromCamera, V3(0, 0, 0));
-        Mat4 renderFromWorld = TranslateM(-(double)pCam.x, -(double)pCam.y, -(double)pCam.z);
+        // CameraTransform (cameras.cpp:43-73): Option "rendercoordsys" picks the rendering space
+        Mat4 renderFromWorld = renderSpace == kRenderCamera  ? cameraFromWorld
+                               : renderSpace == kRenderWorld ? Identity4()
+                                                             : TranslateM(-(double)pCam.x, -(double)pCam.y, -(double)pCam.z);
         scene.camera.renderFromWorld = renderFromWorld;
         scene.camera.renderFromCamera = Mul(renderFromWorld, worldFromCamera);
         double frame = cameraParams.GetFloat("frameaspectratio", double((float)scene.xres / (float)scene.yres));
@@ -2940,7 +3041,22 @@ int Parser::InstTex(const std::string &name, bool spectrum, int specType, const 
             return e == ".png";
         };
         const std::string enc = ps.GetString("encoding", hasPng(fn) ? "sRGB" : "linear");
-        if (ps.Find("basisfilename")) throw Error(ps.loc + ": multispectral basis textures are not supported");
+        const std::string basisFile = ps.GetString("basisfilename", "");
+        if (!basisFile.empty() && spectrum) {
+            // GPUSpectrumImageTexture::Create (textures.cpp:1148-1176); the reference opens the
+            // name as given (relative to the working directory); relative names here resolve
+            // against the scene file's directory, as "filename" does
+            std::string bf = basisFile;
+            if (bf[0] != '/' && !pt.dir.empty()) bf = pt.dir + "/" + bf;
+            t.basis = (int)scene.texBasis.size();
+            ReadBasisFile(bf, ps.loc, &scene.texBasis);
+            t.basisWidth = (int)scene.texBasis.size() - t.basis;
+            if (scene.texBasis[t.basis] == 0) {  // no channels: Evaluate's RGB branch (textures.h:680)
+                scene.texBasis.resize(t.basis);
+                t.basis = -1;
+                t.basisWidth = 0;
+            }
+        }  // FloatImageTexture reads the file but never uses it (textures.cpp:447-458)
         // the texture cache (textures.h:537-554): one pyramid per (file, encoding, wrap)
         int img = -1;
         for (size_t i = 0; i < scene.images.size(); ++i)
@@ -2952,6 +3068,8 @@ int Parser::InstTex(const std::string &name, bool spectrum, int specType, const 
             img = (int)scene.images.size() - 1;
         }
         t.image = img;
+        if (t.basis >= 0 && scene.images[img].nc < 3)
+            throw Error(ps.loc + ": a multispectral basis texture needs an RGB image (" + fn + ")");
         result = NewTexNode(t);
     } else {
         throw Error(ps.loc + ": \"" + c + "\": " + std::string(spectrum ? "spectrum" : "float") +
@@ -2961,6 +3079,132 @@ int Parser::InstTex(const std::string &name, bool spectrum, int specType, const 
     texInProgress.erase({name, spectrum});
     texInstances[key] = result;
     return result;
+}
+
+// ---- multispectral basis files: a JSON array of channels, each {"basis": [...], "offset": [...]}
+namespace {
+struct Json {
+    enum Kind { Null, Bool, Num, Str, Arr, Obj } kind = Null;
+    double num = 0;
+    std::string str;
+    std::vector<Json> arr;
+    std::vector<std::pair<std::string, Json>> obj;
+    const Json *Get(const std::string &k) const {
+        for (auto &kv : obj)
+            if (kv.first == k) return &kv.second;
+        return nullptr;
+    }
+};
+struct JsonReader {
+    const std::string &s;
+    size_t i = 0;
+    std::string where;
+    [[noreturn]] void Fail(const std::string &m) const {
+        throw Error(where + ": malformed JSON (" + m + ") at byte " + std::to_string(i));
+    }
+    void Ws() {
+        while (i < s.size() && std::isspace((unsigned char)s[i])) ++i;
+    }
+    Json Value(int depth = 0) {
+        if (depth > 64) Fail("nesting too deep");
+        Ws();
+        if (i >= s.size()) Fail("unexpected end");
+        Json v;
+        const char c = s[i];
+        if (c == '[') {
+            v.kind = Json::Arr;
+            ++i;
+            Ws();
+            if (i < s.size() && s[i] == ']') return ++i, v;
+            for (;;) {
+                v.arr.push_back(Value(depth + 1));
+                Ws();
+                if (i < s.size() && s[i] == ',') { ++i; continue; }
+                if (i < s.size() && s[i] == ']') { ++i; return v; }
+                Fail("expected , or ]");
+            }
+        }
+        if (c == '{') {
+            v.kind = Json::Obj;
+            ++i;
+            Ws();
+            if (i < s.size() && s[i] == '}') return ++i, v;
+            for (;;) {
+                Ws();
+                Json k = Value(depth + 1);
+                if (k.kind != Json::Str) Fail("object key must be a string");
+                Ws();
+                if (i >= s.size() || s[i] != ':') Fail("expected :");
+                ++i;
+                v.obj.emplace_back(k.str, Value(depth + 1));
+                Ws();
+                if (i < s.size() && s[i] == ',') { ++i; continue; }
+                if (i < s.size() && s[i] == '}') { ++i; return v; }
+                Fail("expected , or }");
+            }
+        }
+        if (c == '"') {
+            v.kind = Json::Str;
+            ++i;
+            while (i < s.size() && s[i] != '"') {
+                if (s[i] == '\\') ++i;
+                if (i < s.size()) v.str += s[i++];
+            }
+            if (i >= s.size()) Fail("unterminated string");
+            return ++i, v;
+        }
+        if (s.compare(i, 4, "true") == 0) return i += 4, v.kind = Json::Bool, v.num = 1, v;
+        if (s.compare(i, 5, "false") == 0) return i += 5, v.kind = Json::Bool, v;
+        if (s.compare(i, 4, "null") == 0) return i += 4, v;
+        char *end = nullptr;
+        v.num = std::strtod(s.c_str() + i, &end);
+        if (end == s.c_str() + i) Fail("unexpected character");
+        v.kind = Json::Num;
+        i = end - s.c_str();
+        return v;
+    }
+};
+}  // namespace
+// the basis array of GPUSpectrumImageTexture::Create (textures.cpp:1148-1176): channel count, the
+// first channel's basis length, int(first channel's offset[0]), then every channel's first
+// <length> basis values.  Refused: an unreadable or malformed file, a channel without a numeric
+// "basis" array of that length, a first channel without a numeric "offset"; more than 3 channels
+// (Evaluate reads an RGB texel, textures.h:664-671)
+void ReadBasisFile(const std::string &path, const std::string &loc, std::vector<float> *out) {
+    std::ifstream in(path);
+    if (!in) throw Error(loc + ": cannot open basis file " + path);
+    std::stringstream ss;
+    ss << in.rdbuf();
+    const std::string text = ss.str();
+    JsonReader rd{text, 0, path};
+    const Json j = rd.Value();
+    rd.Ws();
+    if (rd.i != text.size()) rd.Fail("trailing characters");
+    if (j.kind != Json::Arr) throw Error(path + ": a basis file is a JSON array of channels");
+    if (j.arr.size() > 3) throw Error(path + ": more than 3 basis channels (an RGB texel has 3)");
+    size_t elemSize = 0;
+    int offset = 0;
+    for (size_t c = 0; c < j.arr.size(); ++c) {
+        const Json &e = j.arr[c];
+        const Json *b = e.kind == Json::Obj ? e.Get("basis") : nullptr;
+        if (!b || b->kind != Json::Arr) throw Error(path + ": channel " + std::to_string(c) + " has no \"basis\" array");
+        if (c == 0) {
+            elemSize = b->arr.size();
+            const Json *o = e.Get("offset");
+            if (!o || o->kind != Json::Arr || o->arr.empty() || o->arr[0].kind != Json::Num)
+                throw Error(path + ": the first channel has no numeric \"offset\" array");
+            offset = (int)o->arr[0].num;  // int offset = elem["offset"][0]
+        }
+        if (b->arr.size() < elemSize)
+            throw Error(path + ": channel " + std::to_string(c) + "'s basis is shorter than the first channel's");
+        for (size_t k = 0; k < elemSize; ++k)
+            if (b->arr[k].kind != Json::Num) throw Error(path + ": non-numeric basis value");
+    }
+    out->push_back((float)j.arr.size());
+    out->push_back((float)elemSize);
+    out->push_back((float)offset);
+    for (const Json &e : j.arr)
+        for (size_t k = 0; k < elemSize; ++k) out->push_back((float)e.Get("basis")->arr[k].num);
 }
 
 // The shape's alpha texture (scene.cpp:1369-1384 getAlphaTexture): a named float texture, or a

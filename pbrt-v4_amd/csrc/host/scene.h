@@ -43,6 +43,8 @@ constexpr int kMatMix = 8;
 // HairMaterial (materials.h:353-427): HairBxDF (bxdfs.h:1054-1152), k_vlayered
 constexpr int kMatHair = 9;
 constexpr int kMatMeasured = 10;
+// RetroreflectiveMaterial (this fork, materials.h:553-627): conductor parameters, RetroreflectiveBxDF, k_vlayered
+constexpr int kMatRetroreflective = 11;
 
 // Participating media (media.h:209-350, media.cpp:167-330).  Spectra are DenselySampled
 // 395..705 nm tables in SceneDesc::denseSpectra with pbrt's constructor scaling applied
@@ -197,6 +199,11 @@ struct TextureDesc {
     // fbm / wrinkled / marble: "octaves", "roughness" (omega); marble "variation"
     int octaves = 8;
     float omega = .5f, variation = .2f;
+    // multispectral basis ("basisfilename", this fork's --zhenyi addition): offset of the
+    // texture's table in SceneDesc::texBasis, laid out as the reference's GPU basis array
+    // (textures.cpp:1148-1176): {channels, basis length, int(offset), basis values channel by
+    // channel}; -1 for an ordinary image
+    int basis = -1, basisWidth = 0;
 };
 
 // A texture expression compiled for the device (core.h TexEval*): phase 1 runs once per hit
@@ -286,6 +293,8 @@ struct EnvLightDesc {
     std::vector<float> rect, portalFunc, portalSat;
 };
 void BuildPortal(EnvLightDesc &e, const std::string &loc);
+// SummedAreaTable (util/sampling.h:834-848) of the n x n function f: double running sums as Float
+std::vector<float> SummedAreaTable(const std::vector<float> &f, int n);
 
 // MeasuredBxDFData (bxdfs.cpp:865-1001): an RGL tensor file's tables as PiecewiseLinear2D's
 // constructor leaves them, in core/measured.h's layout (kMeasHdr header ints, float blob)
@@ -295,6 +304,11 @@ struct MeasuredDesc {
     std::vector<float> blob;
 };
 MeasuredDesc LoadMeasuredBRDF(const std::string &path);
+// PiecewiseLinear2D's constructor (util/sampling.h:1299-1400) over `slices` tables of xSize x ySize:
+// appends data, marginal and conditional CDFs to blob; h = {xSize, ySize, data, marg, cond} offsets
+// (-1 without a CDF)
+void BuildPL2D(const float *data, int xSize, int ySize, uint32_t slices, bool normalize, bool buildCdf,
+               std::vector<float> *blob, int *h);
 
 // PointLight / SpotLight / DistantLight (lights.h:200-300, 740-800; lights.cpp:192-276, 1376-1495)
 // in render space: deltaLights holds the point and spot lights first (light-BVH members, global
@@ -337,6 +351,9 @@ struct LightBVHNodeDesc {
 };
 
 struct SceneDesc {
+    std::vector<float> texBasis;        // multispectral basis tables (TextureDesc::basis)
+    int options = 0;                    // kOpt* bits (core.h)
+    float displacementEdgeScale = 1;    // Option "displacementedgescale" (no displaced meshes here)
     // film / sampler / integrator
     int xres = 1280, yres = 720;
     int px0 = 0, px1 = 1280, py0 = 0, py1 = 720;  // pixel bounds

@@ -750,6 +750,12 @@ struct TexCompiler {
         switch (t.kind) {
         case kTexConstant: Emit2(kT2Const, 0, 0, node, 1); return;
         case kTexImage: {
+            if (t.basis >= 0) {  // multispectral basis: the raw RGB, then the per-sample basis sum
+                const int r = NewReg(3);
+                Emit1(kT1SBasisRGB, r, 0, 0, node);
+                Emit2(kT2Basis, r, 0, node, 1);
+                return;
+            }
             const int r = NewReg(4);
             Emit1(kT1SImage, r, 0, 0, node);
             Emit2(kT2RGBReg, r, t.specType == kSpecUnbounded ? 1 : 0, -1, 1);

@@ -50,6 +50,12 @@ constexpr float kInvWavelengthPDF = kLambdaMax - kLambdaMin;  // 1 / SampleUnifo
 #define SEC_BEGIN() (void)0
 #define SEC_MARK(st, k) (void)0
 #endif
+// The record slot of a producer's queue position pos in its shard: a full shard (pos >= capS; the
+// counter keeps counting, so the pass's k_queue_overflow check fails the render) sends the record
+// to the trash slot NR - 1 past every shard instead of into the next shard or past the arrays
+__device__ inline int ShardSlot(int shardBase, int pos, int capS, int NR) {
+    return pos < capS ? shardBase + pos : NR - 1;
+}
 __device__ inline int WavePush(int *counter, bool pred) {
     unsigned long long mask = __ballot(pred);
     if (mask == 0) return -1;
@@ -150,6 +156,7 @@ struct BlockQueues {
     int *gbase; // LDS [K]
     int *const *counters;
     int *const *queues;
+    int capS;
 
     __device__ void Init() {
         if (threadIdx.x < K) fill[threadIdx.x] = 0;
@@ -161,7 +168,8 @@ struct BlockQueues {
         __syncthreads();
         const int b = gbase[k];
         int *q = queues[k];
-        for (int i = threadIdx.x; i < n; i += blockDim.x) q[b + i] = buf[k * Cap + i];
+        for (int i = threadIdx.x; i < n; i += blockDim.x)
+            if (b + i < capS) q[b + i] = buf[k * Cap + i];  // a full shard drops (k_queue_overflow)
         __syncthreads();
         if (threadIdx.x == 0) fill[k] = 0;
         __syncthreads();
@@ -198,8 +206,9 @@ struct WaveQueues {
     int fill[K];
     int *const *counters;
     int *const *queues;
+    int capS;
 
-    __device__ WaveQueues(int *ldsAll, int *const *c, int *const *q) : counters(c), queues(q) {
+    __device__ WaveQueues(int *ldsAll, int *const *c, int *const *q, int cap) : counters(c), queues(q), capS(cap) {
         buf = ldsAll + (threadIdx.x >> 6) * (K * Cap);
 #pragma unroll
         for (int k = 0; k < K; ++k) fill[k] = 0;
@@ -211,7 +220,8 @@ struct WaveQueues {
         if (__lane_id() == 0) b = atomicAdd(counters[k], n);
         b = __shfl(b, 0);
         int *q = queues[k];
-        for (int i = __lane_id(); i < n; i += 64) q[b + i] = buf[k * Cap + i];
+        for (int i = __lane_id(); i < n; i += 64)
+            if (b + i < capS) q[b + i] = buf[k * Cap + i];  // a full shard drops (k_queue_overflow)
         fill[k] = 0;
     }
     __device__ void Append(const bool (&pred)[K], int value) {
@@ -243,7 +253,11 @@ __device__ inline QueueView LoadQueue(const PathState &st, int depth, int queue)
     v.capS = st.capS;
 #pragma unroll
     for (int s = 0; s < kShards; ++s) {
-        v.count[s] = st.counters[CounterIndex(depth, queue, s)];
+        // never more than a shard holds: an overflowing producer dropped the rest, and the pass
+        // fails at its k_queue_overflow check without reading past the shard.  The depth-0 ray
+        // queue is exempt: the camera stage keeps every path's ray in shard 0 (slot = path)
+        const int c = st.counters[CounterIndex(depth, queue, s)];
+        v.count[s] = (depth == 0 && queue == 0) ? c : min(c, st.capS);
         v.total += v.count[s];
     }
     return v;
@@ -1551,10 +1565,16 @@ __device__ inline void GenerateCameraRay(const DeviceScene &S, const PathState &
             Get2D(S, h, &l0, &l1);
         }
     }
+    if (S.options & kOptNoWavelengthJitter) lu = 0.5f;  // camera.cpp:55-56
     float lambda0 = Lerpf(lu, kLambdaMin, kLambdaMax);
     // Filter::Sample(GetPixel2D()) (samplers.h:797-813): offset and weight
     float fx, fy;
     FilterSample(S.filter, S.filterTab, pix0, pix1, &fx, &fy, filterWeight);
+    if (S.options & kOptNoPixelJitter) {  // samplers.h:807-812: pixel centre, lens centre, weight 1
+        fx = fy = 0.f;
+        *filterWeight = 1.f;
+        l0 = l1 = 0.5f;
+    }
     float pFilmX = px + fx + 0.5f, pFilmY = py + fy + 0.5f;
     // PerspectiveCamera::GenerateRay (cameras.cpp:433-456)
     V3 pCamera = XfPoint(S.cameraFromRaster, V3(pFilmX, pFilmY, 0));
@@ -1709,7 +1729,7 @@ __device__ inline void HitTextures(const DeviceScene &S, const PathState &st, in
             float R[kTexMaxRegs];
             TexPhase1(S.tex, pg, tc, R);
             for (SpectralIter it(lambda0s[ri]); it.i < kNSpectrumSamples; it.Next())
-                st.texR[(size_t)it.i * N + ri] = TexPhase2(S.tex, pg, R, it.lam);
+                st.texR[(size_t)it.i * N + ri] = TexPhase2(S.tex, pg, R, it.lam, it.i);
             st.texCoef[3 * (size_t)N + ri] = 1.f;
         }
     }

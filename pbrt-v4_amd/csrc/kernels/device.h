@@ -55,6 +55,7 @@ struct ShadeLdsLayout {
 // chunk per producer, so capS = N/kShards + 256 kShards, and every pass ends with a check that
 // no shard overflowed (k_queue_overflow).
 constexpr int kShards = 8;
+constexpr int kQueueTrash = 64;  // record slots past the shards (PathState::NR - 1: overflow writes)
 constexpr int kCounterPad = 64;  // ints between counters (256 B)
 constexpr int kNumQueues = 8;
 constexpr int kCntRay = 0, kCntMat = 1, kCntShadow = 2, kCntEscaped = 3, kCntEmissive = 4;
@@ -68,6 +69,7 @@ constexpr int kMatDiffuseTransmissionT = 7;                      // k_vlayered
 constexpr int kMatMixT = 8;  // MixMaterial: resolved per hit by k_closest<kClosestMix>
 constexpr int kMatHairT = 9;  // HairBxDF: k_vlayered (volumetric path only)
 constexpr int kMatMeasuredT = 10;  // MeasuredBxDF: k_vlayered (volumetric path only)
+constexpr int kMatRetroreflectiveT = 11;  // RetroreflectiveBxDF: k_vlayered (volumetric path only)
 PHD int MatCounter(int type) { return type == 0 ? kCntMat : kCntMat + 3 + type; }
 PHD int CounterIndex(int depth, int queue, int shard) {
     return ((depth * kNumQueues + queue) * kShards + shard) * kCounterPad;
@@ -220,6 +222,7 @@ struct DeviceScene {
     float cameraFromRaster[16];
     float renderFromCamera[16];
     float lensRadius, focalDistance;
+    int options;  // scene Options: kOptNoPixelJitter / kOptNoWavelengthJitter (camera rays)
     // film / filter
     int xres, yres, px0, px1, py0, py1;
     float filterRadiusX, filterRadiusY;

@@ -728,10 +728,10 @@ __global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_vclosest(DeviceS
         const int ps = WavePush(surfCnt, active && medium < 0 && !iface && !esc);
         const int pf = WavePush(ifaceCnt, active && iface);
         const int pe = WavePush(&st.counters[CounterIndex(wf, kVEsc, shard)], active && esc);
-        if (pm >= 0) v.medQ[shard * st.capS + pm] = ri;
-        if (ps >= 0) v.surfQ[shard * st.capS + ps] = ri;
-        if (pf >= 0) v.ifaceQ[shard * st.capS + pf] = ri;
-        if (pe >= 0) v.escQ[shard * st.capS + pe] = ri;
+        if (pm >= 0 && pm < st.capS) v.medQ[shard * st.capS + pm] = ri;
+        if (ps >= 0 && ps < st.capS) v.surfQ[shard * st.capS + ps] = ri;
+        if (pf >= 0 && pf < st.capS) v.ifaceQ[shard * st.capS + pf] = ri;
+        if (pe >= 0 && pe < st.capS) v.escQ[shard * st.capS + pe] = ri;
     }
 }
 
@@ -887,10 +887,10 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vmedium(DeviceScene 
         const int p1 = WavePush(scatCnt, toScat);
         const int p2 = WavePush(&st.counters[CounterIndex(wf, kVIface, shard)], iface);
         const int p3 = WavePush(&st.counters[CounterIndex(wf, kVEsc, shard)], esc);
-        if (p0 >= 0) v.surfQ[shard * st.capS + p0] = ri;
-        if (p1 >= 0) v.scatQ[shard * st.capS + p1] = ri;
-        if (p2 >= 0) v.ifaceQ[shard * st.capS + p2] = ri;
-        if (p3 >= 0) v.escQ[shard * st.capS + p3] = ri;
+        if (p0 >= 0 && p0 < st.capS) v.surfQ[shard * st.capS + p0] = ri;
+        if (p1 >= 0 && p1 < st.capS) v.scatQ[shard * st.capS + p1] = ri;
+        if (p2 >= 0 && p2 < st.capS) v.ifaceQ[shard * st.capS + p2] = ri;
+        if (p3 >= 0 && p3 < st.capS) v.escQ[shard * st.capS + p3] = ri;
     }
 }
 
@@ -1063,10 +1063,10 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_GREY_WAVES) k_vmedium_grey(De
         const int p1 = WavePush(scatCnt, toScat);
         const int p2 = WavePush(&st.counters[CounterIndex(wf, kVIface, shard)], iface);
         const int p3 = WavePush(&st.counters[CounterIndex(wf, kVEsc, shard)], esc);
-        if (p0 >= 0) v.surfQ[shard * st.capS + p0] = ri;
-        if (p1 >= 0) v.scatQ[shard * st.capS + p1] = ri;
-        if (p2 >= 0) v.ifaceQ[shard * st.capS + p2] = ri;
-        if (p3 >= 0) v.escQ[shard * st.capS + p3] = ri;
+        if (p0 >= 0 && p0 < st.capS) v.surfQ[shard * st.capS + p0] = ri;
+        if (p1 >= 0 && p1 < st.capS) v.scatQ[shard * st.capS + p1] = ri;
+        if (p2 >= 0 && p2 < st.capS) v.ifaceQ[shard * st.capS + p2] = ri;
+        if (p3 >= 0 && p3 < st.capS) v.escQ[shard * st.capS + p3] = ri;
     }
 }
 
@@ -1426,7 +1426,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
         }
         if (last) continue;
         if (mtypeHit == kMatCoatedDiffuseT || mtypeHit == kMatCoatedConductorT || mtypeHit == kMatDiffuseTransmissionT ||
-            mtypeHit == kMatHairT || mtypeHit == kMatMeasuredT)
+            mtypeHit == kMatHairT || mtypeHit == kMatMeasuredT || mtypeHit == kMatRetroreflectiveT)
             continue;  // k_vlayered
         const int mtype = DiffuseOnly ? 0 : mtypeHit;
         // ---- EvaluateMaterialAndBSDF (surfscatter.cpp:57-328) for this material type
@@ -1546,7 +1546,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
                     int js = -1;
                     if (mtype == 0 && S.media.allGrey) {
                         // f_i from LDS; Ld as its sensor sums + Ld_0 (kShRgb)
-                        js = shardBase + WavePush(shadowCnt, true);
+                        js = ShardSlot(shardBase, WavePush(shadowCnt, true), st.capS, st.NR);
                         SpectralIter it(lambda0);
                         SensorAcc acc;
                         float ld0 = 0;
@@ -1565,7 +1565,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
                         rgb = true;
                     } else if (mtype == 0) {
                         // f_i from LDS (nonzero somewhere: the flags pass), Ld straight to the queue
-                        js = shardBase + WavePush(shadowCnt, true);
+                        js = ShardSlot(shardBase, WavePush(shadowCnt, true), st.capS, st.NR);
                         SpectralIter it(lambda0);
                         float ld0 = 0;
 #pragma unroll 2
@@ -1588,7 +1588,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
                             ldUni &= FloatToBits(Ldv) == FloatToBits(fL[0]);
                         }
                         if (fnz) {
-                            js = shardBase + WavePush(shadowCnt, true);
+                            js = ShardSlot(shardBase, WavePush(shadowCnt, true), st.capS, st.NR);
                             v.shLd[js] = fL[0];
 #pragma unroll 2
                             for (int i = 1; i < kNS; ++i)
@@ -1695,7 +1695,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
             // a subsurface material's transmitted sample goes to the BSSRDF queue instead of
             // the next iteration (surfscatter.cpp:225-232); beta after Russian roulette, r_u as
             // it came in, the updated etaScale
-            const int js = shardBase + WavePush(&st.counters[CounterIndex(wf, kVSss, shard)], true);
+            const int js = ShardSlot(shardBase, WavePush(&st.counters[CounterIndex(wf, kVSss, shard)], true), st.capS, st.NR);
             const SssRecords &sr = v.sss;
             bool bu = true;
 #pragma unroll 2
@@ -1719,7 +1719,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
             sr.flags[js] = (bu ? kUniBeta : 0) | (ruUni ? kUniRu : 0);
             continue;
         }
-        const int jn = shardBase + WavePush(nextCnt, true);
+        const int jn = ShardSlot(shardBase, WavePush(nextCnt, true), st.capS, st.NR);
         out.beta[jn] = fL[0];
         out.ru[jn] = ruIn.v0;
         out.rl[jn] = ruIn.v0 / pdf;
@@ -1973,7 +1973,7 @@ __global__ void __launch_bounds__(kBlock) k_vsss_scatter(DeviceScene S0, PathSta
                             nbUni &= FloatToBits(nb) == FloatToBits(nb0);
                         }
                         if (nz) {
-                            const int jn = shardBase + WavePush(nextCnt, true);
+                            const int jn = ShardSlot(shardBase, WavePush(nextCnt, true), st.capS, st.NR);
                             bool ruUni = true;
 #pragma unroll 1
                             for (int i = 0; i < kNS; ++i) ruUni &= FloatToBits(ru(i)) == FloatToBits(ru(0));
@@ -2026,7 +2026,7 @@ __global__ void __launch_bounds__(kBlock) k_vsss_scatter(DeviceScene S0, PathSta
             srl[i] = ru(i) * lightPDF;
             sru[i] = ru(i) * bsdfPDF;
         }
-        const int js = shardBase + WavePush(shadowCnt, true);
+        const int js = ShardSlot(shardBase, WavePush(shadowCnt, true), st.capS, st.NR);
         WriteShadow(S, v, NR, js, ShadowOut{so, sd, DotN(si.n, sd) > 0 ? mOut : mIn}, Ld, sru, srl, lambda0, slot);
     }
 }
@@ -2134,7 +2134,7 @@ __global__ void __launch_bounds__(kBlock) k_viface(DeviceScene S, PathState st, 
         const TriSurface si = SurfaceAt<Ext>(S, prim, p0, p1, p2, b0, b1, b2);
         int mIn, mOut;
         MediaOf(S, prim, medium, &mIn, &mOut);
-        const int jn = shardBase + WavePush(nextCnt, true);
+        const int jn = ShardSlot(shardBase, WavePush(nextCnt, true), st.capS, st.NR);
         out.beta[jn] = betaIn.v0;
         out.ru[jn] = ruIn.v0;
         out.rl[jn] = rlIn.v0;
@@ -2193,9 +2193,10 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
         const int mat = VolHitMaterial(S, st, ri, prim);
         const int mtype = S.matType[mat];
         if (mtype != kMatCoatedDiffuseT && mtype != kMatCoatedConductorT && mtype != kMatDiffuseTransmissionT &&
-            mtype != kMatHairT && mtype != kMatMeasuredT)
+            mtype != kMatHairT && mtype != kMatMeasuredT && mtype != kMatRetroreflectiveT)
             continue;
         const bool dt = mtype == kMatDiffuseTransmissionT, hair = mtype == kMatHairT, meas = mtype == kMatMeasuredT;
+        const bool retro = mtype == kMatRetroreflectiveT;
         const float lambda0 = rec.lambda0[ri];
         const int slot = rec.pixel[ri];
         const int depth = rec.depth[ri], flags = rec.flags[ri], medium = rec.medium[ri];
@@ -2214,9 +2215,9 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
         const float4 mp4 = S.matParams[mat], mc = S.matCoeffs[mat];
         const bool constant = S.matConstant[mat] & 1;
         const float4 L0 = S.matLayer[3 * mat], L1 = S.matLayer[3 * mat + 1], L2 = S.matLayer[3 * mat + 2];
-        const bool conductor = mtype == kMatCoatedConductorT;
-        float ieta = mp4.z;
-        if (!hair && !meas && L2.w >= 0) {  // spectral interface eta: eta(lambda_0), TerminateSecondary
+        const bool conductor = mtype == kMatCoatedConductorT || retro;
+        float ieta = retro ? 1.f : mp4.z;  // RetroreflectiveMaterial::GetBxDF: eta and k as given
+        if (!hair && !meas && !retro && L2.w >= 0) {  // spectral interface eta: eta(lambda_0), TerminateSecondary
             const int es = (int)L2.w, a = S.plOffsets[es], na = S.plOffsets[es + 1] - a;
             ieta = PiecewiseLinearEval(S.plLambda + a, S.plValue + a, na, lambda0);
             if (ieta == 0) ieta = 1;
@@ -2278,6 +2279,7 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
             }
         }
         TrowbridgeReitz trTop{mp4.x, mp4.y}, trBot{L2.y, L2.z};
+        if (retro) trBot = trTop;  // the material's own (remapped, clamped) alphas
         if (S.regularize && (flags & 2)) {  // surfscatter.cpp:127-128, LayeredBxDF::Regularize
             trTop.Regularize();
             trBot.Regularize();
@@ -2293,7 +2295,7 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
             const int *mh = S.measHdr + kMeasHdr * (int)L0.x;
             M = MeasuredAt(mh, S.measData + mh[7]);
         }
-        const int bflags = (hair || meas) ? (kBxGlossy | kBxReflection) : dt ? D.Flags() : L.LayerFlags();
+        const int bflags = (hair || meas) ? (kBxGlossy | kBxReflection) : retro ? RetroFlags(trBot) : dt ? D.Flags() : L.LayerFlags();
         const Frame frame = Frame::FromXZ(Normalize(si.dpdus), si.ns);
         const V3 woL = frame.ToLocal(wo3);
         float fo[kNS];
@@ -2309,6 +2311,11 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
                 const V3 wiL = frame.ToLocal(wi);
                 if (hair) HairF(H, sp.a, woL, wiL, fo);
                 else if (meas) MeasuredF(M, woL, wiL, sp.b, fo);
+                else if (retro) {
+                    const RetroTerms rt = RetroEval(trBot, woL, wiL);
+#pragma unroll 1
+                    for (int i = 0; i < kNS; ++i) fo[i] = rt.ok ? RetroF(rt, sp.a[i], sp.b[i]) : 0.f;
+                }
                 else if (dt) D.f(woL, wiL, fo);
                 else L.f(woL, wiL, true, fo);
                 bool fnz = false;
@@ -2318,6 +2325,7 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
                     const float bsdfPDF = ls.delta ? 0.f
                                           : hair ? HairPDF(H, sp.a, woL, wiL)
                                           : meas ? MeasuredPDF(M, woL, wiL)
+                                          : retro ? RetroPDF(trBot, woL, wiL)
                                           : dt   ? D.PDF(woL, wiL)
                                                  : L.PDF(woL, wiL, true);
                     const float absdot = AbsDotN(si.ns, wi);
@@ -2332,7 +2340,7 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
                         fo[i] = betaIn(i) * fo[i] * absdot * Le;
                         ldUni &= FloatToBits(fo[i]) == FloatToBits(fo[0]);
                     }
-                    const int js = shardBase + WavePush(shadowCnt, true);
+                    const int js = ShardSlot(shardBase, WavePush(shadowCnt, true), st.capS, st.NR);
                     v.shLd[js] = fo[0];
 #pragma unroll 1
                     for (int i = 1; i < kNS; ++i)
@@ -2367,6 +2375,15 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
             bs.pdfIsProportional = false;
             bs.flags = kBxGlossy | kBxReflection;
             bs.ok = MeasuredSampleF(M, woL, rs.iU0, rs.iU1, sp.b, &bs.wi, &bs.pdf, fo);
+        } else if (retro) {
+            const ConductorTerms ct = RetroSample(trBot, woL, rs.iU0, rs.iU1);
+            bs.pdfIsProportional = false;
+            bs.flags = kBxReflection | (ct.specular ? kBxSpecular : kBxGlossy);
+            bs.ok = ct.ok;
+            bs.wi = ct.wi;
+            bs.pdf = ct.pdf;
+#pragma unroll 1
+            for (int i = 0; i < kNS; ++i) fo[i] = ct.ok ? ConductorF(ct, sp.a[i], sp.b[i]) : 0.f;
         } else if (dt) {
             bs.pdfIsProportional = false;
             bs.ok = D.Sample_f(woL, rs.iUc, rs.iU0, rs.iU1, &bs.wi, &bs.pdf, &bs.flags, fo);
@@ -2408,7 +2425,7 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
         }
         if (!nz) continue;
         const bool specular = bs.flags & kBxSpecular;
-        const int jn = shardBase + WavePush(nextCnt, true);
+        const int jn = ShardSlot(shardBase, WavePush(nextCnt, true), st.capS, st.NR);
         out.beta[jn] = fo[0];
         out.ru[jn] = ruIn.v0;
         out.rl[jn] = ruIn.v0 / pdfP;
@@ -2480,7 +2497,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vscatter(DeviceScene
                 so.d = ls.p - pS;
                 so.medium = medium;
                 const int pos = WavePush(shadowCnt, true);
-                WriteShadow(S, v, NR, shardBase + pos, so, Ld, sru, srl, lambda0, slot);
+                WriteShadow(S, v, NR, ShardSlot(shardBase, pos, st.capS, st.NR), so, Ld, sru, srl, lambda0, slot);
             }
         }
         // indirect: phase-function sample, RR, next ray at depth + 1
@@ -2505,7 +2522,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_WAVES) k_vscatter(DeviceScene
             for (int i = 0; i < kNS; ++i) beta[i] /= 1 - q;
         }
         const int pos = WavePush(nextCnt, true);
-        const int jn = shardBase + pos;
+        const int jn = ShardSlot(shardBase, pos, st.capS, st.NR);
         const VolRecords &out = v.rec[(wf + 1) & 1];
         int uni = StoreSpec(out.beta, NR, jn, beta) ? kUniBeta : 0;
         uni |= StoreSpec(out.ru, NR, jn, ru) ? kUniRu : 0;
@@ -2782,7 +2799,7 @@ __global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_vshadow_grey(Dev
 __global__ void k_queue_holes(const int *counters, int wf, int queue, const int *pixel, int capS, int *hole,
                               int stage) {
     const int shard = blockIdx.y;
-    const int n = counters[CounterIndex(wf, queue, shard)];
+    const int n = min(counters[CounterIndex(wf, queue, shard)], capS);  // past capS: k_queue_overflow
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         if (pixel[shard * capS + i] < 0) {
             const int k = atomicAdd(hole, 1);
@@ -2791,6 +2808,13 @@ __global__ void k_queue_holes(const int *counters, int wf, int queue, const int 
                        shard, i, n);
         }
     }
+}
+// One queue's shard counters against the shard capacity (k_queue_overflow's test), for a queue
+// whose counters are reset within the pass (the subsurface stage's shadow queue)
+__global__ void k_shard_overflow(PathState st, int depth, int queue) {
+    const int s = threadIdx.x;
+    if (s < kShards && st.counters[CounterIndex(depth, queue, s)] > st.capS)
+        atomicAdd(&st.stats[kStatQueueOverflow], 1ull);
 }
 static int g_queueCheck = -1;  // -1: PBRT_AMD_QUEUE_CHECK decides on first use
 static int g_holesFound = 0;   // holes the checks found since the last TakeQueueHoles (host)
@@ -2913,7 +2937,7 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
     else hipLaunchKernelGGL(k_vmedium, gW, block, 0, s, S, st, v, wf);
     const int layeredTypes =
         (1 << kMatCoatedDiffuseT) | (1 << kMatCoatedConductorT) | (1 << kMatDiffuseTransmissionT) | (1 << kMatHairT) |
-        (1 << kMatMeasuredT);
+        (1 << kMatMeasuredT) | (1 << kMatRetroreflectiveT);
     const int other = ~((1 << kMatDiffuseT) | (1 << 3) | layeredTypes);
     const size_t surfLds = VolTablesLdsBytes(S) + kNS * kBlock * sizeof(float);
     const bool qcheck = QueueCheckOn() && wf != S.maxDepth;
@@ -2932,8 +2956,14 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
     if (S.matSss) { \
         /* the shadow rays so far first, so the subsurface exits have the queue to themselves \
            ("so that we have space for shadow rays for subsurface", integrator.cpp:427-431) */ \
+        QUEUE_CHECK(5); \
         LaunchVolShadows(S, st, v, wf, gT, s); \
+        /* the counts are about to be reset: check them against the shard capacity now (the \
+           pass-end k_queue_overflow would see only the exits' counts) */ \
+        hipLaunchKernelGGL(k_shard_overflow, dim3(1), dim3(64), 0, s, st, wf, kVShadow); \
         (void)hipMemsetAsync(st.counters + CounterIndex(wf, kVShadow, 0), 0, sizeof(int) * kShards * kCounterPad, s); \
+        if (qcheck) /* the exits' slots start unwritten again (QUEUE_CHECK(3) finds holes) */ \
+            (void)hipMemsetAsync(v.shPixel, 0xff, sizeof(int) * (size_t)st.NR, s); \
         PBRT_LAUNCH_TRAVERSAL(S, K_VSSS_PROBE, gT, block, VolStackBytes(S), s, S, st, v, wf); \
         hipLaunchKernelGGL(k_vsss_scatter<EXT>, gW, block, VolTablesLdsBytes(S), s, S, st, v, wf); \
     } \

@@ -98,7 +98,7 @@ __global__ void __launch_bounds__(kBlock, TraversalWaves(TM))
         qCnt[2 + t] = &st.counters[CounterIndex(depth, MatCounter(t), shard)];
         qArr[2 + t] = st.matQ[t] + shard * st.capS;
     }
-    WaveQueues<kQ, kCap> queues(qBuf, qCnt, qArr);
+    WaveQueues<kQ, kCap> queues(qBuf, qCnt, qArr, st.capS);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         atomicAdd(&st.stats[1], (unsigned long long)count);
         if (timed) atomicAdd(&st.stats[3], (unsigned long long)count);  // rays of event-timed launches
@@ -328,7 +328,7 @@ __global__ void __launch_bounds__(kBlock) k_classify(DeviceScene S, PathState st
         qCnt[2 + t] = &st.counters[CounterIndex(depth, MatCounter(t), shard)];
         qArr[2 + t] = st.matQ[t] + shard * st.capS;
     }
-    WaveQueues<kQ, kCap> queues(qBuf, qCnt, qArr);
+    WaveQueues<kQ, kCap> queues(qBuf, qCnt, qArr, st.capS);
     for (int base = blockIdx.x * blockDim.x; base < rays.total; base += gridDim.x * blockDim.x) {
         const int j = base + threadIdx.x;
         const bool active = j < rays.total;
@@ -972,7 +972,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
         int pos[2];
         BlockPush<2>(cnt, pred, pos);
         if (pos[1] >= 0) {
-            const int j = shardBase + pos[1];
+            const int j = ShardSlot(shardBase, pos[1], st.capS, st.NR);
             st.shadowRay[j] = sOrg.x;
             st.shadowRay[N + j] = sOrg.y;
             st.shadowRay[2 * N + j] = sOrg.z;
@@ -985,7 +985,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_diffuse(Devi
             st.shadowPixel[j] = slot;
         }
         if (pos[0] >= 0) {
-            const int j = shardBase + pos[0];
+            const int j = ShardSlot(shardBase, pos[0], st.capS, st.NR);
             const float *bf = bfLds + threadIdx.x;
             if (rrDiv) {  // beta /= 1 - q (surfscatter.cpp:221)
                 const float rq = 1 / rrOmq;
@@ -1277,7 +1277,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
         int pos[2];
         BlockPush<2>(cnt, pred, pos);
         if (pos[1] >= 0) {
-            const int j = shardBase + pos[1];
+            const int j = ShardSlot(shardBase, pos[1], st.capS, st.NR);
             st.shadowRay[j] = sOrg.x;
             st.shadowRay[N + j] = sOrg.y;
             st.shadowRay[2 * N + j] = sOrg.z;
@@ -1290,7 +1290,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_SHADE_WAVES) k_shade_microfacet(D
             st.shadowPixel[j] = slot;
         }
         if (pos[0] >= 0) {
-            const int j = shardBase + pos[0];
+            const int j = ShardSlot(shardBase, pos[0], st.capS, st.NR);
 #pragma unroll 8
             for (int i = 0; i < kNSpectrumSamples; ++i) out.beta[(size_t)i * N + j] = bf[i * kBlock];
             out.ray[j] = nOrg.x;
@@ -1393,7 +1393,7 @@ __global__ void __launch_bounds__(kBlock) k_texture(DeviceScene S, PathState st,
                 float R[kTexMaxRegs];
                 TexPhase1(S.tex, pg, tc, R);
                 for (SpectralIter it(rec.lambda0[ri]); it.i < kNSpectrumSamples; it.Next())
-                    st.texR[(size_t)it.i * N + ri] = TexPhase2(S.tex, pg, R, it.lam);
+                    st.texR[(size_t)it.i * N + ri] = TexPhase2(S.tex, pg, R, it.lam, it.i);
                 st.texCoef[3 * (size_t)N + ri] = 1.f;
             }
         }

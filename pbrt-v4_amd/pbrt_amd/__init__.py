@@ -115,6 +115,8 @@ class SceneFlat(ctypes.Structure):
         ("env_portal", ctypes.POINTER(ctypes.c_float)),
         ("n_measured", ctypes.c_int),
         ("measured_files", ctypes.POINTER(ctypes.c_char_p)),
+        ("options", ctypes.c_int),
+        ("tex_basis", ctypes.POINTER(ctypes.c_float)),
     ]
 
 
@@ -152,6 +154,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_debug_shape_eval",
     "pbrt_debug_set_queue_check", "pbrt_debug_queue_holes",
     "pbrt_debug_equal_area", "pbrt_debug_cloud_density",
+    "pbrt_debug_pl2d", "pbrt_debug_windowed2d",
 ]
 
 _LIB = None
@@ -227,6 +230,9 @@ def _lib():
                                                c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_debug_portal_eval.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_void_p, c.c_void_p]
     lib.pbrt_debug_measured.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_void_p, c.c_void_p]
+    lib.pbrt_debug_pl2d.argtypes = [c.c_int, c.c_int, c.c_void_p, c.c_int, c.c_int] + [c.c_void_p] * 4 + [
+        c.c_int, c.c_void_p]
+    lib.pbrt_debug_windowed2d.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_debug_procedural.argtypes = [c.c_int, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_debug_queue_counts.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_int]
     lib.pbrt_debug_trowbridge.argtypes = [c.c_void_p, c.c_void_p]
@@ -342,6 +348,32 @@ def debug_bxdf(bxdf_type, params3, wo, wi, u3, eta31=None, k31=None):
     o = np.zeros(70, np.float32)
     _check(_lib().pbrt_debug_bxdf(int(bxdf_type), p.ctypes.data, e.ctypes.data, k.ctypes.data, a.ctypes.data,
                                   b.ctypes.data, u.ctypes.data, o.ctypes.data))
+    return o
+
+
+def debug_pl2d(dim, cdf, data, xs, ys, pr, pv0, pv1, queries):
+    """PiecewiseLinear2D<dim> on the host (pbrt_debug_pl2d): [n][6] queries {u0, u1, px, py, p0, p1}
+    -> [n][7] {Sample xy pdf, Invert xy pdf, Evaluate}."""
+    d = np.ascontiguousarray(data, np.float32)
+    p = np.ascontiguousarray(pr, np.int32)
+    a0, a1 = np.ascontiguousarray(pv0, np.float32), np.ascontiguousarray(pv1, np.float32)
+    q = np.ascontiguousarray(queries, np.float32).reshape(-1, 6)
+    o = np.zeros((len(q), 7), np.float32)
+    _check(_lib().pbrt_debug_pl2d(int(dim), int(cdf), d.ctypes.data, int(xs), int(ys), p.ctypes.data, a0.ctypes.data,
+                                  a1.ctypes.data, q.ctypes.data, len(q), o.ctypes.data))
+    return o
+
+
+def debug_windowed2d(func, queries):
+    """WindowedPiecewiseConstant2D on the host (pbrt_debug_windowed2d) over func [n][n]: [k][8]
+    queries {u0, u1, b0, b1, b2, b3, qx, qy} -> [k][5] {ok, x, y, pdf, PDF(q, b)}."""
+    f = np.ascontiguousarray(func, np.float32)
+    n = int(round(np.sqrt(f.size)))
+    if n * n != f.size:
+        raise ValueError("debug_windowed2d: func must be square")
+    q = np.ascontiguousarray(queries, np.float32).reshape(-1, 8)
+    o = np.zeros((len(q), 5), np.float32)
+    _check(_lib().pbrt_debug_windowed2d(f.ctypes.data, n, q.ctypes.data, len(q), o.ctypes.data))
     return o
 
 

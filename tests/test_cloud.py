@@ -10,7 +10,7 @@ Perlin-noise density over [p0, p1] with a homogeneous majorant.
 * Known answers on the oracle: with density 0 the cloud is empty above p.y = 0.5 (Density's
   altitude term is zero there), so a cloud box spanning y in [0.5, 1] is transparent in
   expectation; a cloud box dims what lies behind it.
-* GPU film parity on a cloud scene (the media kernels' transcendentals are the oracle's device-math polynomials:
+* GPU film parity on a cloud scene (the media kernels' transcendentals are glibc's, as the oracle's libm mode:
   bit-level agreement expected)."""
 import json
 

@@ -264,7 +264,7 @@ def test_env_volumetric_queues_have_no_holes_gpu(pa, oracle, name):
 def test_env_coated_and_medium_match_oracle_gpu(pa, oracle):
     """The volumetric kernels with an image light: a coated-diffuse floor (layered BSDF) and a
     homogeneous-medium box, NEE from surface and medium points and escaped-ray MIS.  The
-    oracle runs in its device-math mode (conftest), as for the other media tests."""
+    oracle runs in its libm mode (conftest), as for the other media tests."""
     from test_gpu_media import check, gpu_rgb, oracle_rgb
     from test_media import box
     text = SCENE.format(fn="env_sky.pfm").replace('Material "diffuse" "rgb reflectance" [0.6 0.5 0.4]',

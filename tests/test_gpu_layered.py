@@ -1,7 +1,7 @@
 """GPU parity of the layered materials and of dispersion (spectral dielectric eta) (k_vlayered in pbrt-v4_amd/csrc/kernels/volpath.hip over
 core.h's LayeredBxDF) against the oracle's independent restatement (oracle/oracle.cpp
 LayeredBxDF).  The walks' RNGs hash direction bits, so, as for media, both sides evaluate
-transcendentals as the oracle's device-math mode computes them (core/detmath.h).  Known answers of test_layered.py are
+transcendentals, glibc's bit for bit as the oracle's libm mode computes them (core/detmath.h).  Known answers of test_layered.py are
 repeated on the GPU image.  Tolerances as test_gpu_media.py."""
 import numpy as np
 import pytest

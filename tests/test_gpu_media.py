@@ -8,7 +8,7 @@ Per-sample parity holds by construction: both sides seed the medium RNG from the
 dimensions.  Because the seed hashes the ray's bits, one ulp anywhere upstream (a sin/cos in a
 direction sample, the log of a free-flight distance) would decorrelate the two paths; so the
 kernels evaluate every transcendental with portable polynomials (core/detmath.h) that the
-oracle restates in its device-math mode (selected for GPU tests by conftest), bit for bit.  Tolerance as test_gpu_parity.py.  Known answers (Beer-Lambert slab, emitting absorber, albedo-1
+oracle computes in its libm mode: core/detmath.h returns glibc's bits.  Tolerance as test_gpu_parity.py.  Known answers (Beer-Lambert slab, emitting absorber, albedo-1
 furnace) are checked on the GPU image itself."""
 import sys
 
@@ -33,7 +33,7 @@ def gpu_rgb(pa, oracle, sc, max_paths=1 << 20, **kw):
 
 
 def oracle_rgb(oracle, sc, **kw):
-    """The oracle in its device-math mode (conftest): the kernels' portable transcendentals"""
+    """The oracle in its libm mode (conftest): glibc's transcendentals, which the kernels reproduce"""
     f = sc.flat()
     film = oracle.render(sc, threads=16, **kw)
     return oracle.film_to_rgb(film, [f.output_rgb_from_sensor_rgb[i] for i in range(9)])

@@ -4,7 +4,7 @@ curves pbrt's wavefront aggregate dices to bilinear patches, h = -1 + 2 v across
 
 * BxDF level: the product's core/hair.h through pbrt_debug_hair against the oracle's ohair
   restatement -- host build (libm) == oracle libm mode bit for bit (CPU), GPU == oracle
-  device-math mode bit for bit (gpu);
+  libm mode bit for bit (gpu);
 * the reference's own HairBxDF tests (bsdfs_test.cpp:673-820): WhiteFurnace, WhiteFurnaceSampled,
   SamplingWeights, SamplingConsistency, HOnTheEdge -- on the product's host build and on the
   oracle (their thresholds; y(lambda) replaced by the wavelength average, sigma_a = 0 gives a

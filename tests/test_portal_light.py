@@ -8,7 +8,7 @@ on the ray origin / previous vertex, so portal scenes render on the volumetric k
   SampleLi) against the oracle's restatement, bit for bit in libm mode;
 * pbrt's loader errors; the portal light and the plain image light of the same map agree on a
   room lit through a window (the portal only changes the sampling);
-* GPU film parity against the oracle (device-math mode).
+* GPU film parity against the oracle (libm mode).
 """
 import numpy as np
 import pytest

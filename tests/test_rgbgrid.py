@@ -9,7 +9,7 @@ grid of sigmaScale * (max sigma_a + max sigma_s).
 * Loader: RGBGridMedium::Create's errors.
 * Known answer on the oracle: a grey RGB grid renders the same image as the uniform grid of
   density 1 with the same grey coefficients (equal in expectation, equal but for ulps here).
-* GPU film parity on an emitting, coloured RGB grid (device-math oracle, as the media kernels)."""
+* GPU film parity on an emitting, coloured RGB grid (libm oracle, as the media kernels)."""
 import numpy as np
 import pytest
 

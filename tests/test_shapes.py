@@ -179,7 +179,7 @@ def test_shapes_scene_matches_oracle_gpu(pa, oracle):
 @pytest.mark.gpu
 def test_shapes_volumetric_matches_oracle_gpu(pa, oracle):
     """The volumetric kernels: a medium-filled sphere (interface material) and a coated sphere
-    beside the emitters (oracle in its device-math mode, as the media tests)."""
+    beside the emitters (oracle in its libm mode, as the media tests)."""
     from test_gpu_media import check, gpu_rgb, oracle_rgb
     text = SHAPES.replace('Material "conductor" "float roughness" 0.1',
                           'Material "coateddiffuse" "rgb reflectance" [0.3 0.5 0.7] "float roughness" 0.1')

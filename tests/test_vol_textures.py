@@ -3,7 +3,7 @@ surface stage evaluates the same texEval calls and bump / normal mapping as the 
 (EvaluateMaterialAndBSDF, surfscatter.cpp:57-137).  k_vtexture evaluates them over the
 iteration's surface queue; k_vsurface<..., Tex> reads the results.  The oracle's volumetric
 integrator shares MakeBSDF and the mix resolution with its surface integrator, so the GPU film
-is checked against it (device-math oracle, as the media kernels).  Mix materials resolve at the
+is checked against it (libm oracle, as the media kernels).  Mix materials resolve at the
 closest hit (k_vclosest<TM, true>) there too."""
 import numpy as np
 import pytest

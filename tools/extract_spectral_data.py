@@ -89,6 +89,30 @@ def main():
     for name in ("xyz_to_srgb", "srgb_to_xyz"):
         data["opt_" + name] = numbers(array_body(opt, name))
         assert len(data["opt_" + name]) == 9
+    # the other gamuts rgb2spec_opt builds tables for (init_tables, :408-486): ACES2065-1 under its
+    # D60 illuminant, Rec.2020 and DCI-P3 under D65
+    body = array_body(opt, "cie_d60")
+    raw = [float(x) for x in re.findall(r"N\((" + NUM + r")\)", body)]
+    # cie_d60[CIE_SAMPLES] has 94 initialisers: C++ zero-fills the 95th (830 nm) entry
+    assert len(raw) == 94
+    raw.append(0.0)
+    div = float(re.search(r"#define N\(x\) \(x / (" + NUM + r")\)", opt[:opt.find("cie_d60[")][-200:]).group(1))
+    data["opt_cie_d60_raw"] = raw
+    data["opt_cie_d60_divisor"] = div
+    for g in ("aces2065_1", "rec2020", "dcip3"):
+        for name in ("xyz_to_" + g, g + "_to_xyz"):
+            data["opt_" + name] = numbers(array_body(opt, name))
+            assert len(data["opt_" + name]) == 9
+    # the normalised standard illuminants Spectra::Init registers (util/spectrum.cpp:2604-2650,
+    # 2689-2707: FromInterleaved(..., normalize = true)): "stdillum-*" and "illum-acesD60"
+    illums = {"stdillum-A": "CIE_Illum_A", "stdillum-D50": "CIE_Illum_D5000", "stdillum-D65": "CIE_Illum_D6500",
+              "illum-acesD60": "ACES_Illum_D60"}
+    for k in range(1, 13):
+        illums[f"stdillum-F{k}"] = f"CIE_Illum_F{k}"
+    for name, arr in illums.items():
+        vals = numbers(array_body(spec, arr))
+        assert len(vals) % 2 == 0 and len(vals) >= 4, (name, len(vals))
+        data["illum:" + name] = vals
     color = (REF / "util" / "color.cpp").read_text()
     m = re.search(r"Float\s+SRGBToLinearLUT\s*\[256\]\s*=\s*\{", color)
     body = color[m.end():color.index("}", m.end())]

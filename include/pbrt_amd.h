@@ -405,6 +405,19 @@ int64_t pbrt_debug_halton_fastpath_mismatches(const pbrt_scene *scene, int dim, 
                                               uint32_t step);
 int pbrt_debug_rgb_coeffs(float r, float g, float b, float *coeffs3);
 int pbrt_debug_rgb2spec_column(int maxc, int j, int i, float *out192);
+/* The RGB colour spaces (util/colorspace.cpp:83-105): pbrt_color_space_index maps a ColorSpace
+ * directive name (srgb, dci-p3, rec2020, aces2065-1; any case) to 0..3, or -1 (error set).
+ * pbrt_debug_color_space: info[338] = r, g, b, white chromaticities (8), XYZFromRGB (9),
+ * RGBFromXYZ (9), SpectrumToPhotometric(illuminant), the illuminant densely sampled at 395..705 */
+int pbrt_color_space_index(const char *name);
+int pbrt_debug_color_space(int cs, float *info338);
+/* RGB -> spectrum in colour space cs for n RGB triples at nl wavelengths: per triple
+ * out[3 + 3 nl] = the table's sigmoid coefficients of rgb, RGBAlbedoSpectrum(rgb)(lambda),
+ * RGBUnboundedSpectrum(s rgb)(lambda), RGBIlluminantSpectrum(s rgb)(lambda) with s = unboundedScale */
+int pbrt_debug_rgb_spectrum(int cs, const float *rgb3, int n, float unboundedScale, const float *lambda, int nl,
+                            float *out);
+/* Column (maxc, j, i) of colour space cs's RGBToSpectrumTable as rgb2spec_opt builds it (64 x 3) */
+int pbrt_debug_rgb2spec_column_cs(int cs, int maxc, int j, int i, float *out192);
 /* Texture evaluation of material `material`'s textured parameter (slot 0 reflectance, 1 u / 2 v
  * roughness) at a hit given as p, n, dpdu, dpdv (render space) and uv (14 floats), with the
  * product's shared host/device code (surfscatter.cpp:74-137, textures.h): out[0..3] = dudx,

@@ -1549,7 +1549,7 @@ static void BuildDevice(pbrt_context *c) {
         const char *rs = getenv("PBRT_AMD_RAY_SORT");
         c->rayBinning = !c->volumetric && (rs ? atoi(rs) != 0 : S.ldsTris == 0);
         const char *rk = getenv("PBRT_AMD_RAY_BIN_KEY");
-        S.rayBinMode = rk ? std::max(0, std::min(2, atoi(rk))) : 0;
+        S.rayBinMode = rk ? std::max(0, std::min(4, atoi(rk))) : 0;
         const char *xg = getenv("PBRT_AMD_XCD_GROUPS");
         S.xcdGroups = xg ? std::max(0, atoi(xg)) : 0;  // measured neutral on C4 (k_closest 7434 vs 7410 us)
     }
@@ -2412,7 +2412,34 @@ int pbrt_film_write_image(pbrt_context *ctx, const char *path, int writeFP16) {
             std::copy(rgb.begin() + ((size_t)(d.py0 + y) * d.xres + d.px0) * 3,
                       rgb.begin() + ((size_t)(d.py0 + y) * d.xres + d.px0 + w) * 3, crop.begin() + (size_t)y * w * 3);
         const int window[4] = {d.px0, d.py0, d.xres, d.yres};
-        WriteImage(path, crop.data(), w, h, writeFP16 != 0, window);
+        const float *chroma = nullptr;
+        float chroma8[8];
+        if (d.filmColorSpace != kColorSpaceSRGB) {
+            const ColorSpaceDesc &cs = GetColorSpace(d.filmColorSpace);
+            const std::string p(path);
+            const std::string ext = p.size() >= 4 ? p.substr(p.size() - 4) : p;
+            if (ext == ".exr" || ext == ".EXR") {
+                // Image::WriteEXR keeps the film's colour space and records its chromaticities
+                std::copy(cs.prim, cs.prim + 6, chroma8);
+                chroma8[6] = cs.w[0], chroma8[7] = cs.w[1];
+                chroma = chroma8;
+            } else {
+                // Image::Write (util/image.cpp:989-1005): PNG / PFM pixels are converted to sRGB by
+                // ConvertRGBColorSpace(film, sRGB) = sRGB.RGBFromXYZ * film.XYZFromRGB, Mul<RGB>
+                float m[3][3];
+                MulCompensated3(GetColorSpace(kColorSpaceSRGB).rgbFromXYZf, cs.xyzFromRGBf, m);
+                for (size_t q = 0; q < (size_t)w * h; ++q) {
+                    float *c = &crop[3 * q];
+                    float o[3];
+                    for (int i = 0; i < 3; ++i) {
+                        o[i] = 0;
+                        for (int j = 0; j < 3; ++j) o[i] += m[i][j] * c[j];
+                    }
+                    std::copy(o, o + 3, c);
+                }
+            }
+        }
+        WriteImage(path, crop.data(), w, h, writeFP16 != 0, window, chroma);
         return 0;
     } catch (const std::exception &e) {
         return Fail(e.what());
@@ -2979,6 +3006,82 @@ int pbrt_debug_equal_area(int to_sphere, const float *in, int n, float *out) {
         }
     }
     return 0;
+}
+
+int pbrt_debug_color_space(int cs, float *info) {
+    try {
+        if (!info) return Fail("null argument");
+        if (cs < 0 || cs >= kNumColorSpaces) return Fail("pbrt_debug_color_space: colour space index out of range");
+        const ColorSpaceDesc &c = GetColorSpace(cs);
+        float *o = info;
+        o = std::copy(c.prim, c.prim + 6, o);
+        o = std::copy(c.w, c.w + 2, o);
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) *o++ = c.xyzFromRGBf[i][j];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) *o++ = c.rgbFromXYZf[i][j];
+        *o++ = c.photometric;
+        std::copy(c.illuminant.begin(), c.illuminant.end(), o);
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_color_space_index(const char *name) {
+    if (!name) {
+        Fail("null argument");
+        return -1;
+    }
+    const int cs = ColorSpaceByName(name);
+    if (cs < 0) Fail(std::string(name) + ": color space unknown");
+    return cs;
+}
+
+int pbrt_debug_rgb_spectrum(int cs, const float *rgb3, int n, float unboundedScale, const float *lambda, int nl,
+                            float *out) {
+    try {
+        if (!rgb3 || !lambda || !out || n < 0 || nl < 0) return Fail("null argument");
+        if (cs < 0 || cs >= kNumColorSpaces) return Fail("pbrt_debug_rgb_spectrum: colour space index out of range");
+        const ColorSpaceDesc &c = GetColorSpace(cs);
+        const int stride = 3 + 3 * nl;
+        for (int k = 0; k < n; ++k) {
+            const float *x = rgb3 + 3 * (size_t)k;
+            float *o = out + (size_t)stride * k;
+            // RGBAlbedoSpectrum(cs, rgb): the table's coefficients of rgb itself
+            const auto a = RGBToSigmoidCoeffs(x[0], x[1], x[2], cs);
+            std::copy(a.begin(), a.end(), o);
+            // RGBUnboundedSpectrum / RGBIlluminantSpectrum(cs, unboundedScale * rgb): scale 2 max,
+            // the coefficients of rgb / scale; the illuminant is DenselySampled (nearest nm)
+            const float r = unboundedScale * x[0], g = unboundedScale * x[1], b = unboundedScale * x[2];
+            const float scale = 2 * std::max({r, g, b});
+            const auto u = scale ? RGBToSigmoidCoeffs(r / scale, g / scale, b / scale, cs) : RGBToSigmoidCoeffs(0, 0, 0, cs);
+            for (int i = 0; i < nl; ++i) {
+                const float l = lambda[i];
+                o[3 + i] = SigmoidPolynomial(a[0], a[1], a[2], l);
+                o[3 + nl + i] = scale * SigmoidPolynomial(u[0], u[1], u[2], l);
+                const int off = (int)std::lround(l) - 395;
+                const float ill = off >= 0 && off < 311 ? c.illuminant[off] : 0.f;
+                o[3 + 2 * nl + i] = scale * SigmoidPolynomial(u[0], u[1], u[2], l) * ill;
+            }
+        }
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_debug_rgb2spec_column_cs(int cs, int maxc, int j, int i, float *out) {
+    try {
+        if (!out) return Fail("null argument");
+        if (cs < 0 || cs >= kNumColorSpaces || maxc < 0 || maxc > 2 || j < 0 || j > 63 || i < 0 || i > 63)
+            return Fail("pbrt_debug_rgb2spec_column_cs: index out of range");
+        auto v = RGB2SpecColumn(maxc, j, i, cs);
+        std::copy(v.begin(), v.end(), out);
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
 }
 
 int pbrt_debug_rgb2spec_column(int maxc, int j, int i, float *out) {

@@ -177,7 +177,8 @@ struct Bytes {
 // win = {x0, y0, fullW, fullH}: the image covers the film's pixelBounds starting at (x0, y0) of a
 // fullW x fullH frame (Image::WriteEXR, util/image.cpp:1179-1200: displayWindow = full resolution,
 // dataWindow = pixelBounds; scanline y coordinates are absolute).
-static void WriteEXR(const std::string &path, const float *rgb, int w, int h, bool half, const int win[4]) {
+static void WriteEXR(const std::string &path, const float *rgb, int w, int h, bool half, const int win[4],
+                     const float *chroma8) {
     const int pt = half ? 1 : 2, bpc = half ? 2 : 4;  // pixel type HALF / FLOAT
     Bytes hdr;
     hdr.u32(20000630u);  // magic
@@ -193,6 +194,11 @@ static void WriteEXR(const std::string &path, const float *rgb, int w, int h, bo
         }
         ch.u8(0);
         hdr.attr("channels", "chlist", ch);
+    }
+    if (chroma8) {
+        Bytes v;
+        for (int i = 0; i < 8; ++i) v.f32(chroma8[i]);
+        hdr.attr("chromaticities", "chromaticities", v);
     }
     {
         Bytes v;
@@ -520,11 +526,12 @@ static void WritePNG(const std::string &path, const float *rgb, int w, int h) {
 }
 
 // ---------------------------------------------------------------- public
-void WriteImage(const std::string &path, const float *rgb, int w, int h, bool exrHalf, const int *window) {
+void WriteImage(const std::string &path, const float *rgb, int w, int h, bool exrHalf, const int *window,
+                const float *chroma8) {
     const std::string e = Ext(path);
     const int full[4] = {0, 0, w, h};
     if (e == "pfm") WritePFM(path, rgb, w, h);
-    else if (e == "exr") WriteEXR(path, rgb, w, h, exrHalf, window ? window : full);
+    else if (e == "exr") WriteEXR(path, rgb, w, h, exrHalf, window ? window : full, chroma8);
     else if (e == "png") WritePNG(path, rgb, w, h);
     else throw std::runtime_error(path + ": unsupported image format \"" + e + "\" (pfm, exr, png)");
 }

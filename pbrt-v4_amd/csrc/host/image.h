@@ -15,8 +15,10 @@ struct Image {
 // by extension: .pfm (float), .exr (half unless exrHalf = false), .png (8-bit sRGB).
 // window = {x0, y0, fullW, fullH}: rgb is the w x h pixelBounds region at (x0, y0) of a
 // fullW x fullH film; EXR records it as dataWindow inside displayWindow (null: whole frame).
+// chroma8 (EXR only): the r, g, b, white chromaticities written as the "chromaticities" attribute
+// (Image::WriteEXR writes them for a colour space other than sRGB, util/image.cpp:1231-1242)
 void WriteImage(const std::string &path, const float *rgb, int w, int h, bool exrHalf = true,
-                const int *window = nullptr);
+                const int *window = nullptr, const float *chroma8 = nullptr);
 Image ReadImage(const std::string &path);  // .pfm, .exr (uncompressed scanline)
 
 enum class ErrorMetric { MAE = 0, MSE = 1, MRSE = 2, FLIP = 3 };

@@ -249,10 +249,12 @@ struct Param {
     std::vector<bool> bools;
     bool used = false;
     bool attribute = false;  // from an Attribute directive: may go unused (scene.cpp:209-213)
+    int colorSpace = kColorSpaceSRGB;  // the graphics state's at parse time (ParsedParameter::colorSpace)
 };
 struct ParamSet {
     std::vector<Param> params;
     std::string loc;
+    int colorSpace = kColorSpaceSRGB;  // ParameterDictionary::ColorSpace(): the directive's graphics state
     Param *Find(const std::string &name, const std::string &type = "") {
         for (auto &p : params)
             if (p.name == name && (type.empty() || p.type == type)) {
@@ -301,6 +303,7 @@ struct GraphicsState {
     std::string areaLightName;
     ParamSet areaLightParams;
     std::string insideMedium, outsideMedium;  // MediumInterface ("" = vacuum)
+    int colorSpace = kColorSpaceSRGB;         // ColorSpace directive (scene.cpp:108-115)
 };
 
 class Parser {
@@ -508,10 +511,12 @@ class Parser {
     ParamSet Params(const std::vector<Token> &toks, size_t &pos) {
         ParamSet ps;
         ps.loc = pos > 0 ? Loc(toks[pos - 1]) : "";
+        ps.colorSpace = gs.colorSpace;
         while (pos < toks.size() && toks[pos].isString) {
             std::string decl = toks[pos].text;
             std::istringstream ds(decl);
             Param p;
+            p.colorSpace = gs.colorSpace;
             ds >> p.type >> p.name;
             if (p.name.empty()) break;  // a bare string: not a parameter declaration
             ++pos;
@@ -615,8 +620,11 @@ class Parser {
             Str(toks, pos);
             Params(toks, pos);  // the BVH8 build is the aggregate whatever is asked (gpu/aggregate.cpp)
         } else if (d == "ColorSpace") {
-            std::string cs = Str(toks, pos);
-            if (cs != "srgb") throw Error(loc + ": only the srgb colour space is supported");
+            // BasicSceneBuilder::ColorSpace (scene.cpp:108-115): RGBColorSpace::GetNamed
+            const std::string name = Str(toks, pos);
+            const int cs = ColorSpaceByName(name);
+            if (cs < 0) throw Error(loc + ": " + name + ": color space unknown");
+            gs.colorSpace = cs;
         } else if (d == "Option") {
             // parser.cpp:877-880: a quoted name, then one raw value token
             std::string name = Str(toks, pos);
@@ -751,13 +759,14 @@ class Parser {
         }
     }
 
-    // RGBUnboundedSpectrum(sRGB, rgb) (util/spectrum.cpp:230-244) as a SssSpectrumDesc
-    static SssSpectrumDesc UnboundedRGB(float r, float g, float b) {
+    // RGBUnboundedSpectrum(cs, rgb) (util/spectrum.cpp:230-244) as a SssSpectrumDesc
+    static SssSpectrumDesc UnboundedRGB(float r, float g, float b, int cs = kColorSpaceSRGB) {
         SssSpectrumDesc q;
         const float mx = std::max({r, g, b});
         q.kind = 1;
         q.scale = 2 * mx;
-        const auto c = q.scale ? RGBToSigmoidCoeffs(r / q.scale, g / q.scale, b / q.scale) : RGBToSigmoidCoeffs(0, 0, 0);
+        const auto c = q.scale ? RGBToSigmoidCoeffs(r / q.scale, g / q.scale, b / q.scale, cs)
+                               : RGBToSigmoidCoeffs(0, 0, 0, cs);
         q.c0 = c[0], q.c1 = c[1], q.c2 = c[2];
         return q;
     }
@@ -775,12 +784,12 @@ class Parser {
                 SssSpectrumDesc q;
                 q.kind = 1;
                 q.scale = 1;
-                const auto c = RGBToSigmoidCoeffs(r, g, b);
+                const auto c = RGBToSigmoidCoeffs(r, g, b, p->colorSpace);
                 q.c0 = c[0], q.c1 = c[1], q.c2 = c[2];
                 return q;
             }
             if (r < 0 || g < 0 || b < 0) throw Error(loc + ": RGB parameter \"" + p->name + "\" has negative component.");
-            return UnboundedRGB(r, g, b);
+            return UnboundedRGB(r, g, b, p->colorSpace);
         }
         if (p->type == "spectrum") {
             SssSpectrumDesc q;
@@ -821,7 +830,7 @@ class Parser {
                 float rgb[3] = {(float)r->nums[0], (float)r->nums[1], (float)r->nums[2]};
                 for (float v : rgb)
                     if (v < 0 || v > 1) throw Error(ps.loc + ": RGB reflectance must be in [0,1]");
-                auto c = RGBToSigmoidCoeffs(rgb[0], rgb[1], rgb[2]);
+                auto c = RGBToSigmoidCoeffs(rgb[0], rgb[1], rgb[2], r->colorSpace);
                 m.c0 = c[0];
                 m.c1 = c[1];
                 m.c2 = c[2];
@@ -1005,7 +1014,7 @@ class Parser {
                 float rgb[3] = {(float)refl->nums[0], (float)refl->nums[1], (float)refl->nums[2]};
                 for (float v : rgb)
                     if (v < 0 || v > 1) throw Error(ps.loc + ": RGB parameter \"reflectance\" used as an albedo has > 1 component.");
-                auto c = RGBToSigmoidCoeffs(rgb[0], rgb[1], rgb[2]);
+                auto c = RGBToSigmoidCoeffs(rgb[0], rgb[1], rgb[2], refl->colorSpace);
                 m.c0 = c[0];
                 m.c1 = c[1];
                 m.c2 = c[2];
@@ -1043,7 +1052,7 @@ class Parser {
                 float rgb[3] = {(float)refl->nums[0], (float)refl->nums[1], (float)refl->nums[2]};
                 for (float v : rgb)
                     if (v < 0 || v > 1) throw Error(ps.loc + ": RGB parameter \"reflectance\" used as an albedo has > 1 component.");
-                auto cf = RGBToSigmoidCoeffs(rgb[0], rgb[1], rgb[2]);
+                auto cf = RGBToSigmoidCoeffs(rgb[0], rgb[1], rgb[2], refl->colorSpace);
                 m.c0 = cf[0];
                 m.c1 = cf[1];
                 m.c2 = cf[2];
@@ -1068,7 +1077,7 @@ class Parser {
             float rgb[3] = {(float)r->nums[0], (float)r->nums[1], (float)r->nums[2]};
             for (float v : rgb)
                 if (v < 0 || v > 1) throw Error(loc + ": RGB " + r->name + " must be in [0,1]");
-            auto c = RGBToSigmoidCoeffs(rgb[0], rgb[1], rgb[2]);
+            auto c = RGBToSigmoidCoeffs(rgb[0], rgb[1], rgb[2], r->colorSpace);
             *constant = false;
             *c0 = c[0];
             *c1 = c[1];
@@ -1769,8 +1778,8 @@ static void BuildRGBGridMedium(ParamSet &ps, MediumDesc &m) {
             const float r = grids[k][3 * i], g = grids[k][3 * i + 1], b = grids[k][3 * i + 2];
             if (r < 0 || g < 0 || b < 0) throw Error(ps.loc + ": RGB grid medium value has a negative component.");
             const float scale = 2 * std::max({r, g, b});
-            const std::array<float, 3> c = scale ? RGBToSigmoidCoeffs(r / scale, g / scale, b / scale)
-                                                 : RGBToSigmoidCoeffs(0, 0, 0);
+            const std::array<float, 3> c = scale ? RGBToSigmoidCoeffs(r / scale, g / scale, b / scale, ps.colorSpace)
+                                                 : RGBToSigmoidCoeffs(0, 0, 0, ps.colorSpace);
             float *d = &m.density[(size_t)k * 4 * n + 4 * i];
             d[0] = c[0], d[1] = c[1], d[2] = c[2], d[3] = scale;
         }
@@ -1831,10 +1840,10 @@ static std::array<float, 311> MediumSpectrum(ParamSet &ps, const char *name, boo
         float r = (float)p->nums[0], g = (float)p->nums[1], b = (float)p->nums[2];
         if (r < 0 || g < 0 || b < 0) throw Error(ps.loc + ": RGB parameter \"" + std::string(name) + "\" has negative component.");
         if (illuminant) {
-            d = DenseRGBIlluminant(r, g, b);
-            if (photometric) *photometric = GetSpectralData().photometricD65;
+            d = DenseRGBIlluminant(r, g, b, p->colorSpace);
+            if (photometric) *photometric = GetColorSpace(p->colorSpace).photometric;
         } else {
-            d = DenseRGBUnbounded(r, g, b);
+            d = DenseRGBUnbounded(r, g, b, p->colorSpace);
         }
         return d;
     }
@@ -2042,22 +2051,24 @@ void Parser::Finish() {
     // ---- sensor / output colour space
     {
         // RGBFilm: outputRGBFromSensorRGB = colorSpace->RGBFromXYZ * sensor->XYZFromSensorRGB
-        const SpectralData &sd = GetSpectralData();
+        const ColorSpaceDesc &sd = GetColorSpace(filmParams.colorSpace);
+        scene.filmColorSpace = filmParams.colorSpace;
         PixelSensorDesc ps;
         try {
-            ps = BuildPixelSensor(scene.sensorName, scene.whiteBalance);
+            ps = BuildPixelSensor(scene.sensorName, scene.whiteBalance, filmParams.colorSpace);
         } catch (const Error &e) {
             throw Error(filmParams.loc + ": " + e.what());
         }
         scene.sensorX = ps.r;
         scene.sensorY = ps.g;
         scene.sensorZ = ps.b;
+        // film.cpp:505: the float SquareMatrix<3> product, one compensated dot per entry
+        float out[3][3];
+        MulCompensated3(sd.rgbFromXYZf, ps.xyzFromSensorRGB, out);
         for (int i = 0; i < 3; ++i)
             for (int j = 0; j < 3; ++j) {
                 scene.xyzFromSensorRGB[i][j] = ps.xyzFromSensorRGB[i][j];
-                double v = 0;
-                for (int k = 0; k < 3; ++k) v += sd.rgbFromXYZ[i][k] * ps.xyzFromSensorRGB[k][j];
-                scene.outputRGBFromSensorRGB[i][j] = v;
+                scene.outputRGBFromSensorRGB[i][j] = out[i][j];
             }
     }
     // ---- media (MakeNamedMedium -> HomogeneousMedium / GridMedium, media.cpp:167-330)
@@ -2119,7 +2130,7 @@ void Parser::Finish() {
             m.sigmaA = (int)scene.denseSpectra.size() - 1;
             scene.denseSpectra.push_back(zero);
             m.sigmaS = (int)scene.denseSpectra.size() - 1;
-            scene.denseSpectra.push_back(GetSpectralData().denseD65);
+            scene.denseSpectra.push_back(GetColorSpace(ps.colorSpace).illuminant);
             m.Le = (int)scene.denseSpectra.size() - 1;
             ps.Find("type");
             ps.CheckUnused();
@@ -2264,14 +2275,20 @@ void Parser::Finish() {
             Param *L = ap.Find("L");
             float rgb[3] = {0, 0, 0};
             std::array<float, 311> dense;
-            float photometric = GetSpectralData().photometricD65;
+            // DiffuseAreaLight::Create (lights.cpp:901-941): L defaults to the parameters' colour
+            // space illuminant, and scale /= its photometric integral (an image emitter's too;
+            // its pixels are RGBIlluminantSpectrum of the image's own colour space, sRGB here)
+            const ColorSpaceDesc &acs = GetColorSpace(L ? L->colorSpace : ap.colorSpace);
+            float photometric = acs.photometric;
             std::string spectrumKey;
+            bool image = false;
+            for (const Param &q : ap.params) image |= q.name == "filename" && q.type == "string";
             if (!L) {
-                dense = GetSpectralData().denseD65;  // colorSpace->illuminant
+                dense = image ? GetSpectralData().denseD65 : acs.illuminant;  // colorSpace->illuminant
             } else if (L->type == "rgb") {
                 if (L->nums.size() != 3) throw Error(ap.loc + ": L needs 3 values");
                 for (int i = 0; i < 3; ++i) rgb[i] = (float)L->nums[i];
-                dense = DenseRGBIlluminant(rgb[0], rgb[1], rgb[2]);
+                dense = DenseRGBIlluminant(rgb[0], rgb[1], rgb[2], L->colorSpace);
             } else if (L->type == "spectrum" && !L->nums.empty()) {
                 // PiecewiseLinearSpectrum from (lambda, value) pairs (paramdict.cpp:415-439)
                 dense = DensePiecewiseLinear(L->nums, ap.loc);
@@ -2290,7 +2307,8 @@ void Parser::Finish() {
                 throw Error(ap.loc + ": L of type " + L->type + " not supported");
             }
             std::string key = spectrumKey.empty() ? std::to_string(rgb[0]) + "," + std::to_string(rgb[1]) + "," +
-                                                        std::to_string(rgb[2]) + (L ? "" : "D65")
+                                                        std::to_string(rgb[2]) + (L ? "" : image ? "D65" : "illum") +
+                                                        "@" + acs.name
                                                   : spectrumKey;
             if (!spectrumCache.count(key)) {
                 scene.denseSpectra.push_back(dense);
@@ -2337,7 +2355,7 @@ void Parser::Finish() {
                 if (power > 0) {
                     // k_e of an image emitter: its mean luminance (the image colour space's
                     // LuminanceVector, lights.cpp:945-957); the area and pi follow per shape
-                    const double(*xr)[3] = GetSpectralData().xyzFromRGB;
+                    const float(*xr)[3] = GetColorSpace(kColorSpaceSRGB).xyzFromRGBf;  // the image's (sRGB) LuminanceVector
                     const float lum[3] = {(float)xr[1][0], (float)xr[1][1], (float)xr[1][2]};
                     float k = 0;
                     for (int y = 0; y < im.h; ++y)
@@ -2475,10 +2493,13 @@ InfiniteLightDesc Parser::InfiniteLight(PendingLight &l) {
     if (portal && portal->nums.size() != 12)
         throw Error(ps.loc + ": Expected 4 vertices for infinite light portal but given " + std::to_string(portal->nums.size() / 3));
     if (fn.empty()) {
-        std::array<float, 311> dense = GetSpectralData().denseD65;
-        float photometric = GetSpectralData().photometricD65;
+        // UniformInfiniteLight (lights.cpp:1559-1580): L defaults to the parameters' colour space
+        // illuminant; scale /= SpectrumToPhotometric(L)
+        const ColorSpaceDesc &lcs = GetColorSpace(L ? L->colorSpace : ps.colorSpace);
+        std::array<float, 311> dense = lcs.illuminant;
+        float photometric = lcs.photometric;
         if (L && L->type == "rgb" && L->nums.size() == 3)
-            dense = DenseRGBIlluminant((float)L->nums[0], (float)L->nums[1], (float)L->nums[2]);
+            dense = DenseRGBIlluminant((float)L->nums[0], (float)L->nums[1], (float)L->nums[2], L->colorSpace);
         else if (L && L->type == "spectrum" && !L->nums.empty()) {
             dense = DensePiecewiseLinear(L->nums, ps.loc);
             photometric = PhotometricOf(dense);
@@ -2509,7 +2530,7 @@ InfiniteLightDesc Parser::InfiniteLight(PendingLight &l) {
     if (E_v > 0) {
         // the upper hemisphere's illuminance of the map (lights.cpp:1651-1679): pixel centres
         // through EqualAreaSquareToSphere, luminance-weighted, cosine-weighted; scale *= E_v / it
-        const double(*xr)[3] = GetSpectralData().xyzFromRGB;
+        const float(*xr)[3] = GetColorSpace(kColorSpaceSRGB).xyzFromRGBf;  // the image's (sRGB) LuminanceVector
         const float lum[3] = {(float)xr[1][0], (float)xr[1][1], (float)xr[1][2]};
         float illuminance = 0;
         for (int y = 0; y < env.res; ++y) {
@@ -2614,7 +2635,7 @@ void Parser::ImageLight(PendingLight &l, const Mat4 &rfl, float sc, DeltaLightDe
             // the screen window, each pixel weighted by dw/dA = cos^3 of its direction (the
             // direction lightFromScreen gives a screen point is (x / invTan, y / invTan, 1)
             // normalised, evaluated here in double)
-            const double(*xr)[3] = GetSpectralData().xyzFromRGB;
+            const float(*xr)[3] = GetColorSpace(kColorSpaceSRGB).xyzFromRGBf;  // the image's (sRGB) LuminanceVector
             const float lum[3] = {(float)xr[1][0], (float)xr[1][1], (float)xr[1][2]};
             const float aspect = float(im.w) / float(im.h);
             const float x0 = aspect > 1 ? -aspect : -1, x1 = -x0, y0 = aspect > 1 ? -1 : -1 / aspect, y1 = -y0;
@@ -2664,10 +2685,14 @@ void Parser::DeltaLight(PendingLight &l, std::vector<DeltaLightDesc> &pointSpot,
     ParamSet &ps = l.params;
     const bool distant = l.type == "distant", projection = l.type == "projection";
     Param *I = projection ? nullptr : ps.Find(distant ? "L" : "I");
-    std::array<float, 311> dense = GetSpectralData().denseD65;
-    float photometric = GetSpectralData().photometricD65;
+    // I / L default to the parameters' colour space illuminant; a projection light's image is
+    // RGBIlluminantSpectrum of the image's colour space (sRGB) and divides by its illuminant's
+    // photometric integral (lights.cpp:470-478)
+    const ColorSpaceDesc &lcs = GetColorSpace(projection ? kColorSpaceSRGB : I ? I->colorSpace : ps.colorSpace);
+    std::array<float, 311> dense = lcs.illuminant;
+    float photometric = lcs.photometric;
     if (I && I->type == "rgb" && I->nums.size() == 3) {
-        dense = DenseRGBIlluminant((float)I->nums[0], (float)I->nums[1], (float)I->nums[2]);
+        dense = DenseRGBIlluminant((float)I->nums[0], (float)I->nums[1], (float)I->nums[2], I->colorSpace);
     } else if (I && I->type == "spectrum" && !I->nums.empty()) {
         dense = DensePiecewiseLinear(I->nums, ps.loc);
         photometric = PhotometricOf(dense);
@@ -2810,14 +2835,15 @@ TexSpectrumConst Parser::RGBConst(const Param *p, int specType, const std::strin
     if (specType == kSpecAlbedo) {
         if (r > 1 || g > 1 || b > 1)
             throw Error(loc + ": RGB parameter \"" + p->name + "\" used as an albedo has > 1 component.");
-        auto cf = RGBToSigmoidCoeffs(r, g, b);
+        auto cf = RGBToSigmoidCoeffs(r, g, b, p->colorSpace);
         c.c[0] = cf[0], c.c[1] = cf[1], c.c[2] = cf[2];
         c.scale = 1;
     } else if (specType == kSpecUnbounded) {
         // RGBUnboundedSpectrum (util/spectrum.cpp:240-244)
         const float m = std::max({r, g, b});
         c.scale = 2 * m;
-        auto cf = c.scale != 0 ? RGBToSigmoidCoeffs(r / c.scale, g / c.scale, b / c.scale) : RGBToSigmoidCoeffs(0, 0, 0);
+        auto cf = c.scale != 0 ? RGBToSigmoidCoeffs(r / c.scale, g / c.scale, b / c.scale, p->colorSpace)
+                               : RGBToSigmoidCoeffs(0, 0, 0, p->colorSpace);
         c.c[0] = cf[0], c.c[1] = cf[1], c.c[2] = cf[2];
     } else {
         throw Error(loc + ": illuminant spectrum textures are not supported");

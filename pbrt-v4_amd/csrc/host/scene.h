@@ -371,6 +371,7 @@ struct SceneDesc {
     std::vector<float> filterTable;
     float imagingRatio = 1;
     std::string sensorName = "cie1931";
+    int filmColorSpace = 0;                    // RGBFilm's colour space (the Film directive's graphics state)
     float whiteBalance = 0;                    // Film "whitebalance" (0: none)
     float maxComponentValue = kInfinity;       // RGBFilm::AddSample clamp (film.h:247-249)
     float xyzFromSensorRGB[3][3];              // PixelSensor::XYZFromSensorRGB
@@ -466,11 +467,36 @@ void BuildFilterTable(SceneDesc &s);
 extern const uint8_t kZSobolPermutations[24][4];
 
 // Spectral support (host)
+// The RGB colour spaces of RGBColorSpace::Init (util/colorspace.cpp:83-105), selected by the
+// ColorSpace directive (scene.cpp:108-115) and carried per parameter (ParsedParameter::colorSpace)
+enum ColorSpaceId { kColorSpaceSRGB = 0, kColorSpaceDCIP3 = 1, kColorSpaceRec2020 = 2, kColorSpaceACES = 3 };
+constexpr int kNumColorSpaces = 4;
+struct ColorSpaceDef {
+    const char *name;        // RGBColorSpace::GetNamed's (lower case)
+    double prim[6];          // r, g, b chromaticities (xy)
+    const char *illuminant;  // named illuminant spectrum
+};
+extern const ColorSpaceDef kColorSpaceDefs[kNumColorSpaces];
+struct ColorSpaceDesc {
+    std::string name;
+    float prim[6];                       // r, g, b (xy)
+    float w[2];                          // SpectrumToXYZ(illuminant).xy()
+    std::array<float, 311> illuminant;   // DenselySampledSpectrum(illuminant), 395..705
+    float photometric = 0;               // SpectrumToPhotometric(illuminant)
+    double xyzFromRGB[3][3], rgbFromXYZ[3][3];  // solved in double (the loader's historical form)
+    float xyzFromRGBf[3][3], rgbFromXYZf[3][3];  // pbrt's float arithmetic, bit for bit
+};
+const ColorSpaceDesc &GetColorSpace(int cs);
+// SquareMatrix<3> product as pbrt forms it (compensated InnerProduct per entry)
+void MulCompensated3(const float a[3][3], const float b[3][3], float r[3][3]);
+int ColorSpaceByName(const std::string &name);  // -1 when unknown
 struct SpectralData {
     std::vector<float> cieX, cieY, cieZ, cieLambda, d65Interleaved;
     std::vector<double> optX, optY, optZ, optD65Raw, optXyzToSrgb, optSrgbToXyz;
+    std::vector<double> optD60Raw, optXyzToRgb[kNumColorSpaces], optRgbToXyz[kNumColorSpaces];  // rgb2spec_opt gamuts
     std::map<std::string, std::vector<float>> named;  // interleaved (lambda, value) tables
-    double optD65Divisor = 1;
+    std::map<std::string, std::vector<float>> illuminants;  // stdillum-*, illum-acesD60 (normalised on use)
+    double optD65Divisor = 1, optD60Divisor = 1;
     std::array<float, 311> denseX, denseY, denseZ, denseD65;  // 395..705
     float photometricD65 = 0;                                  // SpectrumToPhotometric(D65)
     double rgbFromXYZ[3][3];
@@ -494,7 +520,7 @@ struct PixelSensorDesc {
     float xyzFromSensorRGB[3][3];
     std::array<float, 311> illum;  // the white-balance illuminant (zeros without one)
 };
-PixelSensorDesc BuildPixelSensor(const std::string &name, float whiteBalanceTemp);
+PixelSensorDesc BuildPixelSensor(const std::string &name, float whiteBalanceTemp, int cs = kColorSpaceSRGB);
 // BlackbodySpectrum(T)(lambda) (util/spectrum.h): normalised to 1 at Wien's peak
 float BlackbodyNormalized(float lambda, float T);
 // Spectra::D(T) (util/spectrum.cpp:2537-2570) densely sampled over 395..705
@@ -516,12 +542,13 @@ void SetDataDirectory(const std::string &dir);
 std::string GetDataDirectory();
 // RGB -> sigmoid coefficients through the 64^3 sRGB table (util/color.cpp:36-75); table
 // columns are generated on demand with the rgb2spec Gauss-Newton restatement.
-std::array<float, 3> RGBToSigmoidCoeffs(float r, float g, float b);
-// Column (maxc, yi, xi) of the 64^3 table as produced by cmd/rgb2spec_opt.cpp: 64 x 3 floats
-std::vector<float> RGB2SpecColumn(int maxc, int j, int i);
+std::array<float, 3> RGBToSigmoidCoeffs(float r, float g, float b, int cs = kColorSpaceSRGB);
+// Column (maxc, yi, xi) of colour space cs's 64^3 table as cmd/rgb2spec_opt.cpp produces it
+// (gamut sRGB / DCI_P3 / REC2020 / ACES2065_1): 64 x 3 floats
+std::vector<float> RGB2SpecColumn(int maxc, int j, int i, int cs = kColorSpaceSRGB);
 float RGB2SpecZNode(int k);
-std::array<float, 311> DenseRGBIlluminant(float r, float g, float b);
-std::array<float, 311> DenseRGBUnbounded(float r, float g, float b);
+std::array<float, 311> DenseRGBIlluminant(float r, float g, float b, int cs = kColorSpaceSRGB);
+std::array<float, 311> DenseRGBUnbounded(float r, float g, float b, int cs = kColorSpaceSRGB);
 // GetNamedSpectrum(name) for the metal / glass tables: PiecewiseLinearSpectrum::FromInterleaved
 // (samples, normalize = false), extended to Lambda_min - 1 / Lambda_max + 1 (spectrum.cpp:133-163)
 PLSpectrumDesc NamedPiecewiseLinear(const std::string &name);

@@ -56,6 +56,87 @@ static void Invert3(const double m[3][3], double r[3][3]) {
     r[2][2] = (m[0][0] * m[1][1] - m[0][1] * m[1][0]) * id;
 }
 
+// the four spaces RGBColorSpace::Init builds (util/colorspace.cpp:83-105): name, primaries
+// r, g, b (xy) and the named illuminant
+const ColorSpaceDef kColorSpaceDefs[kNumColorSpaces] = {
+    {"srgb", {.64, .33, .3, .6, .15, .06}, "stdillum-D65"},
+    {"dci-p3", {.68, .32, .265, .690, .15, .06}, "stdillum-D65"},
+    {"rec2020", {.708, .292, .170, .797, .131, .046}, "stdillum-D65"},
+    {"aces2065-1", {.7347, .2653, 0., 1., .0001, -.077}, "illum-acesD60"}};
+
+// PiecewiseLinearSpectrum::FromInterleaved(samples, normalize = true) (util/spectrum.cpp:133-163):
+// extended to Lambda_min - 1 / Lambda_max + 1, then scaled by CIE_Y_integral / InnerProduct(s, Y)
+static void NormalizedIlluminant(const SpectralData &d, const std::vector<float> &iv, std::vector<float> *lam,
+                                 std::vector<float> *val) {
+    lam->clear();
+    val->clear();
+    for (size_t i = 0; i + 1 < iv.size(); i += 2) {
+        lam->push_back(iv[i]);
+        val->push_back(iv[i + 1]);
+    }
+    if (lam->front() > kLambdaMin) {
+        lam->insert(lam->begin(), kLambdaMin - 1);
+        val->insert(val->begin(), val->front());
+    }
+    if (lam->back() < kLambdaMax) {
+        lam->push_back(kLambdaMax + 1);
+        val->push_back(val->back());
+    }
+    // InnerProduct(spec, &Spectra::Y()) over lambda = 395..705 in Float steps
+    float integral = 0;
+    for (float lambda = kLambdaMin; lambda <= kLambdaMax; ++lambda)
+        integral += PiecewiseLinearEval(*lam, *val, lambda) * d.denseY[DenseOffset(lambda)];
+    const float CIE_Y_integral = 106.856895f;
+    float s = CIE_Y_integral / integral;
+    for (float &v : *val) v *= s;
+}
+
+// SpectrumToPhotometric(illuminant): sum over Float lambda of Y(l) * s(l)
+static float PhotometricDense(const SpectralData &d, const std::array<float, 311> &s) {
+    float y = 0;
+    for (float lambda = kLambdaMin; lambda <= kLambdaMax; ++lambda)
+        y += d.denseY[DenseOffset(lambda)] * s[DenseOffset(lambda)];
+    return y;
+}
+
+// RGBColorSpace's constructor (util/colorspace.cpp:23-37) in double: W = SpectrumToXYZ(illuminant),
+// the primaries' XYZ (Y = 1), C = inverse(rgb) * W, XYZFromRGB = rgb * diag(C), RGBFromXYZ its inverse
+static void ColorSpaceMatrices(const SpectralData &d, const std::array<float, 311> &illum, const double prim[6],
+                               double xyzFromRGBOut[3][3], double rgbFromXYZOut[3][3]) {
+    double X = 0, Y = 0, Z = 0;
+    for (int l = 395; l <= 705; ++l) {
+        X += (double)d.denseX[l - 395] * illum[l - 395];
+        Y += (double)d.denseY[l - 395] * illum[l - 395];
+        Z += (double)d.denseZ[l - 395] * illum[l - 395];
+    }
+    const double CIE_Y_integral = 106.856895;
+    X /= CIE_Y_integral;
+    Y /= CIE_Y_integral;
+    Z /= CIE_Y_integral;
+    auto fromxyY = [](double x, double y, double out[3]) {
+        if (y == 0) {  // XYZ::FromxyY: a primary on y = 0 is black
+            out[0] = out[1] = out[2] = 0;
+            return;
+        }
+        out[0] = x / y;
+        out[1] = 1;
+        out[2] = (1 - x - y) / y;
+    };
+    double R[3], G[3], B[3];
+    fromxyY(prim[0], prim[1], R);
+    fromxyY(prim[2], prim[3], G);
+    fromxyY(prim[4], prim[5], B);
+    const double W[3] = {X, Y, Z};
+    double rgb[3][3] = {{R[0], G[0], B[0]}, {R[1], G[1], B[1]}, {R[2], G[2], B[2]}};
+    double inv[3][3];
+    Invert3(rgb, inv);
+    double C[3];
+    for (int i = 0; i < 3; ++i) C[i] = inv[i][0] * W[0] + inv[i][1] * W[1] + inv[i][2] * W[2];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) xyzFromRGBOut[i][j] = rgb[i][j] * C[j];
+    Invert3(xyzFromRGBOut, rgbFromXYZOut);
+}
+
 static SpectralData LoadSpectralData() {
     SpectralData d;
     std::string path = GetDataDirectory() + "/spectral_data.txt";
@@ -83,6 +164,14 @@ static SpectralData LoadSpectralData() {
         else if (name == "opt_cie_d65_divisor") d.optD65Divisor = v[0];
         else if (name == "opt_xyz_to_srgb") d.optXyzToSrgb = v;
         else if (name == "opt_srgb_to_xyz") d.optSrgbToXyz = v;
+        else if (name == "opt_cie_d60_raw") d.optD60Raw = v;
+        else if (name == "opt_cie_d60_divisor") d.optD60Divisor = v[0];
+        else if (name == "opt_xyz_to_dcip3") d.optXyzToRgb[kColorSpaceDCIP3] = v;
+        else if (name == "opt_dcip3_to_xyz") d.optRgbToXyz[kColorSpaceDCIP3] = v;
+        else if (name == "opt_xyz_to_rec2020") d.optXyzToRgb[kColorSpaceRec2020] = v;
+        else if (name == "opt_rec2020_to_xyz") d.optRgbToXyz[kColorSpaceRec2020] = v;
+        else if (name == "opt_xyz_to_aces2065_1") d.optXyzToRgb[kColorSpaceACES] = v;
+        else if (name == "opt_aces2065_1_to_xyz") d.optRgbToXyz[kColorSpaceACES] = v;
         else if (name == "MIPFilterLUT" && n == 128) {
             for (int i = 0; i < 128; ++i) d.mipFilterLUT[i] = (float)v[i];
             haveMipLUT = true;
@@ -91,6 +180,7 @@ static SpectralData LoadSpectralData() {
             haveSrgbLUT = true;
         }
         else if (name.rfind("named:", 0) == 0) tof(d.named[name.substr(6)]);
+        else if (name.rfind("illum:", 0) == 0) tof(d.illuminants[name.substr(6)]);
         else if (name.rfind("sensor:", 0) == 0) tof(d.sensors[name.substr(7)]);
         else if (name.rfind("swatch:", 0) == 0) {
             d.swatches.emplace_back();
@@ -121,80 +211,16 @@ static SpectralData LoadSpectralData() {
         d.denseY[l - 395] = PiecewiseLinearEval(d.cieLambda, d.cieY, (float)l);
         d.denseZ[l - 395] = PiecewiseLinearEval(d.cieLambda, d.cieZ, (float)l);
     }
+    d.optXyzToRgb[kColorSpaceSRGB] = d.optXyzToSrgb;
+    d.optRgbToXyz[kColorSpaceSRGB] = d.optSrgbToXyz;
     // stdillum-D65 = PiecewiseLinearSpectrum::FromInterleaved(CIE_Illum_D6500, normalize=true)
     std::vector<float> lam, val;
-    for (size_t i = 0; i + 1 < d.d65Interleaved.size(); i += 2) {
-        lam.push_back(d.d65Interleaved[i]);
-        val.push_back(d.d65Interleaved[i + 1]);
-    }
-    if (lam.front() > kLambdaMin) {
-        lam.insert(lam.begin(), kLambdaMin - 1);
-        val.insert(val.begin(), val.front());
-    }
-    if (lam.back() < kLambdaMax) {
-        lam.push_back(kLambdaMax + 1);
-        val.push_back(val.back());
-    }
-    {
-        // InnerProduct(spec, &Spectra::Y()) over lambda = 395..705 in Float steps
-        float integral = 0;
-        for (float lambda = kLambdaMin; lambda <= kLambdaMax; ++lambda)
-            integral += PiecewiseLinearEval(lam, val, lambda) * d.denseY[DenseOffset(lambda)];
-        const float CIE_Y_integral = 106.856895f;
-        float s = CIE_Y_integral / integral;
-        for (float &v : val) v *= s;
-    }
+    NormalizedIlluminant(d, d.d65Interleaved, &lam, &val);
     // RGBColorSpace::illuminant = DenselySampledSpectrum(stdillum-D65)
     for (int l = 395; l <= 705; ++l) d.denseD65[l - 395] = PiecewiseLinearEval(lam, val, (float)l);
-    // SpectrumToPhotometric(illuminant): sum over Float lambda of Y(l) * s(l)
-    {
-        float y = 0;
-        for (float lambda = kLambdaMin; lambda <= kLambdaMax; ++lambda)
-            y += d.denseY[DenseOffset(lambda)] * d.denseD65[DenseOffset(lambda)];
-        d.photometricD65 = y;
-    }
+    d.photometricD65 = PhotometricDense(d, d.denseD65);
     // sRGB colour space matrices (colorspace.cpp:25-38), in double
-    {
-        double X = 0, Y = 0, Z = 0;
-        for (int l = 395; l <= 705; ++l) {
-            X += (double)d.denseX[l - 395] * d.denseD65[l - 395];
-            Y += (double)d.denseY[l - 395] * d.denseD65[l - 395];
-            Z += (double)d.denseZ[l - 395] * d.denseD65[l - 395];
-        }
-        const double CIE_Y_integral = 106.856895;
-        X /= CIE_Y_integral;
-        Y /= CIE_Y_integral;
-        Z /= CIE_Y_integral;
-        double wx = X / (X + Y + Z), wy = Y / (X + Y + Z);
-        auto fromxyY = [](double x, double y, double out[3]) {
-            out[0] = x / y;
-            out[1] = 1;
-            out[2] = (1 - x - y) / y;
-        };
-        double R[3], G[3], B[3], W[3];
-        fromxyY(0.64, 0.33, R);
-        fromxyY(0.3, 0.6, G);
-        fromxyY(0.15, 0.06, B);
-        fromxyY(wx, wy, W);
-        W[0] *= Y;
-        W[1] *= Y;
-        W[2] *= Y;
-        // W.xy() then XYZ::FromxyY(w, Y=1)?  pbrt uses W directly: C = inv(rgb) * W
-        W[0] = X;
-        W[1] = Y;
-        W[2] = Z;
-        double rgb[3][3] = {{R[0], G[0], B[0]}, {R[1], G[1], B[1]}, {R[2], G[2], B[2]}};
-        double inv[3][3];
-        Invert3(rgb, inv);
-        double C[3];
-        for (int i = 0; i < 3; ++i) C[i] = inv[i][0] * W[0] + inv[i][1] * W[1] + inv[i][2] * W[2];
-        double xyzFromRGB[3][3];
-        for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j) xyzFromRGB[i][j] = rgb[i][j] * C[j];
-        Invert3(xyzFromRGB, d.rgbFromXYZ);
-        for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j) d.xyzFromRGB[i][j] = xyzFromRGB[i][j];
-    }
+    ColorSpaceMatrices(d, d.denseD65, kColorSpaceDefs[kColorSpaceSRGB].prim, d.xyzFromRGB, d.rgbFromXYZ);
     return d;
 }
 
@@ -226,26 +252,33 @@ double cie_interp(const double *data, double x) {  // rgb2spec_opt.cpp:248
     return (1.0 - weight) * data[offset] + weight * data[offset + 1];
 }
 
-const OptTables &GetOptTables() {
-    static std::once_flag once;
-    static OptTables *t = nullptr;
-    std::call_once(once, [] {
+// init_tables(gamut) (rgb2spec_opt.cpp:408-486) for one of the four colour spaces: ACES2065-1
+// integrates against its D60 table, the others against D65
+const OptTables &GetOptTables(int cs) {
+    static std::once_flag once[kNumColorSpaces];
+    static OptTables *tabs[kNumColorSpaces] = {};
+    std::call_once(once[cs], [cs] {
         const SpectralData &d = GetSpectralData();
-        t = new OptTables();
+        OptTables *t = new OptTables();
         memset(t, 0, sizeof(*t));
-        double d65[kCIESamples];
-        for (int i = 0; i < kCIESamples; ++i) d65[i] = d.optD65Raw[i] / d.optD65Divisor;
+        const bool d60 = cs == kColorSpaceACES;
+        const std::vector<double> &raw = d60 ? d.optD60Raw : d.optD65Raw;
+        const double div = d60 ? d.optD60Divisor : d.optD65Divisor;
+        if (raw.size() != kCIESamples || d.optXyzToRgb[cs].size() != 9 || d.optRgbToXyz[cs].size() != 9)
+            throw Error(std::string("spectral data has no rgb2spec tables for colour space ") + kColorSpaceDefs[cs].name);
+        double ill[kCIESamples];
+        for (int i = 0; i < kCIESamples; ++i) ill[i] = raw[i] / div;
         for (int i = 0; i < 3; ++i)
             for (int j = 0; j < 3; ++j) {
-                t->xyz_to_rgb[i][j] = d.optXyzToSrgb[3 * i + j];
-                t->rgb_to_xyz[i][j] = d.optSrgbToXyz[3 * i + j];
+                t->xyz_to_rgb[i][j] = d.optXyzToRgb[cs][3 * i + j];
+                t->rgb_to_xyz[i][j] = d.optRgbToXyz[cs][3 * i + j];
             }
         double h = (kCIEMax - kCIEMin) / (kFine - 1);
-        for (int i = 0; i < kFine; ++i) {  // init_tables, rgb2spec_opt.cpp:408-486
+        for (int i = 0; i < kFine; ++i) {
             double lambda = kCIEMin + i * h;
             double xyz[3] = {cie_interp(d.optX.data(), lambda), cie_interp(d.optY.data(), lambda),
                              cie_interp(d.optZ.data(), lambda)},
-                   I = cie_interp(d65, lambda);
+                   I = cie_interp(ill, lambda);
             double weight = 3.0 / 8.0 * h;
             if (i == 0 || i == kFine - 1)
                 ;
@@ -258,8 +291,9 @@ const OptTables &GetOptTables() {
                 for (int j = 0; j < 3; ++j) t->rgb_tbl[k][i] += t->xyz_to_rgb[k][j] * xyz[j] * I * weight;
             for (int k = 0; k < 3; ++k) t->whitepoint[k] += xyz[k] * I * weight;
         }
+        tabs[cs] = t;
     });
-    return *t;
+    return *tabs[cs];
 }
 
 void cie_lab(const OptTables &t, double *p) {
@@ -374,9 +408,9 @@ double smoothstep(double x) { return x * x * (3.0 - 2.0 * x); }
 
 float RGB2SpecZNode(int k) { return (float)smoothstep(smoothstep(k / double(kRes - 1))); }
 
-std::vector<float> RGB2SpecColumn(int l, int j, int i) {
+std::vector<float> RGB2SpecColumn(int l, int j, int i, int cs) {
     // rgb2spec_opt.cpp:825-875 for one (l, j, i): two warm-started chains over k
-    const OptTables &t = GetOptTables();
+    const OptTables &t = GetOptTables(cs);
     std::vector<float> out(kRes * 3);
     const double y = j / double(kRes - 1), x = i / double(kRes - 1);
     auto store = [&](int k, const double *coeffs) {
@@ -409,13 +443,13 @@ std::vector<float> RGB2SpecColumn(int l, int j, int i) {
     return out;
 }
 
-static const std::vector<float> &CachedColumn(int l, int j, int i) {
+static const std::vector<float> &CachedColumn(int l, int j, int i, int cs) {
     static std::mutex mu;
     static std::map<int, std::vector<float>> cache;
     std::lock_guard<std::mutex> lock(mu);
-    int key = (l * kRes + j) * kRes + i;
+    int key = ((cs * 3 + l) * kRes + j) * kRes + i;
     auto it = cache.find(key);
-    if (it == cache.end()) it = cache.emplace(key, RGB2SpecColumn(l, j, i)).first;
+    if (it == cache.end()) it = cache.emplace(key, RGB2SpecColumn(l, j, i, cs)).first;
     return it->second;
 }
 
@@ -437,7 +471,7 @@ const std::vector<float> &RGBToSpectrumTableData() {
                 const int probe[3][3] = {{0, 0, 0}, {1, kRes / 2, kRes / 3}, {2, kRes - 1, kRes - 2}};
                 for (int p = 0; ok && p < 3; ++p) {
                     const int l = probe[p][0], j = probe[p][1], i = probe[p][2];
-                    const std::vector<float> c = RGB2SpecColumn(l, j, i);
+                    const std::vector<float> c = RGB2SpecColumn(l, j, i, kColorSpaceSRGB);
                     for (int k = 0; ok && k < kRes; ++k)
                         for (int ci = 0; ci < 3; ++ci)
                             ok = ok && table[kRes + ((((size_t)l * kRes + k) * kRes + j) * kRes + i) * 3 + ci] ==
@@ -455,7 +489,7 @@ const std::vector<float> &RGBToSpectrumTableData() {
             th.emplace_back([&, t] {
                 for (int col = (int)t; col < nCols; col += (int)nt) {
                     const int l = col / (kRes * kRes), j = (col / kRes) % kRes, i = col % kRes;
-                    const std::vector<float> c = RGB2SpecColumn(l, j, i);
+                    const std::vector<float> c = RGB2SpecColumn(l, j, i, kColorSpaceSRGB);
                     for (int k = 0; k < kRes; ++k)
                         for (int ci = 0; ci < 3; ++ci)
                             table[kRes + ((((size_t)l * kRes + k) * kRes + j) * kRes + i) * 3 + ci] = c[3 * k + ci];
@@ -468,7 +502,7 @@ const std::vector<float> &RGBToSpectrumTableData() {
     return table;
 }
 
-std::array<float, 3> RGBToSigmoidCoeffs(float r, float g, float b) {
+std::array<float, 3> RGBToSigmoidCoeffs(float r, float g, float b, int cs) {
     // RGBColorSpace::ToRGBCoeffs -> RGBToSpectrumTable::operator() (util/color.cpp:36-75)
     float rgb[3] = {std::max(0.f, r), std::max(0.f, g), std::max(0.f, b)};
     if (rgb[0] == rgb[1] && rgb[1] == rgb[2])
@@ -495,7 +529,7 @@ std::array<float, 3> RGBToSigmoidCoeffs(float r, float g, float b) {
     std::array<float, 3> c;
     for (int ci = 0; ci < 3; ++ci) {
         auto co = [&](int ddx, int ddy, int ddz) {
-            const std::vector<float> &col = CachedColumn(maxc, yi + ddy, xi + ddx);
+            const std::vector<float> &col = CachedColumn(maxc, yi + ddy, xi + ddx, cs);
             return col[3 * (zi + ddz) + ci];
         };
         c[ci] = Lerpf(dz, Lerpf(dy, Lerpf(dx, co(0, 0, 0), co(1, 0, 0)), Lerpf(dx, co(0, 1, 0), co(1, 1, 0))),
@@ -504,27 +538,27 @@ std::array<float, 3> RGBToSigmoidCoeffs(float r, float g, float b) {
     return c;
 }
 
-std::array<float, 311> DenseRGBIlluminant(float r, float g, float b) {
-    // DenselySampledSpectrum(RGBIlluminantSpectrum(sRGB, rgb)) (util/spectrum.cpp:246-251)
-    const SpectralData &d = GetSpectralData();
+std::array<float, 311> DenseRGBIlluminant(float r, float g, float b, int cs) {
+    // DenselySampledSpectrum(RGBIlluminantSpectrum(cs, rgb)) (util/spectrum.cpp:246-251)
+    const std::array<float, 311> &ill = GetColorSpace(cs).illuminant;
     float m = std::max({r, g, b});
     float scale = 2 * m;
-    std::array<float, 3> c = scale ? RGBToSigmoidCoeffs(r / scale, g / scale, b / scale)
-                                   : RGBToSigmoidCoeffs(0, 0, 0);
+    std::array<float, 3> c = scale ? RGBToSigmoidCoeffs(r / scale, g / scale, b / scale, cs)
+                                   : RGBToSigmoidCoeffs(0, 0, 0, cs);
     std::array<float, 311> out;
     for (int l = 395; l <= 705; ++l) {
         float lambda = (float)l;
-        out[l - 395] = scale * SigmoidPolynomial(c[0], c[1], c[2], lambda) * d.denseD65[DenseOffset(lambda)];
+        out[l - 395] = scale * SigmoidPolynomial(c[0], c[1], c[2], lambda) * ill[DenseOffset(lambda)];
     }
     return out;
 }
 
-std::array<float, 311> DenseRGBUnbounded(float r, float g, float b) {
-    // DenselySampledSpectrum(RGBUnboundedSpectrum(sRGB, rgb)) (util/spectrum.cpp:230-244)
+std::array<float, 311> DenseRGBUnbounded(float r, float g, float b, int cs) {
+    // DenselySampledSpectrum(RGBUnboundedSpectrum(cs, rgb)) (util/spectrum.cpp:230-244)
     float m = std::max({r, g, b});
     float scale = 2 * m;
-    std::array<float, 3> c = scale ? RGBToSigmoidCoeffs(r / scale, g / scale, b / scale)
-                                   : RGBToSigmoidCoeffs(0, 0, 0);
+    std::array<float, 3> c = scale ? RGBToSigmoidCoeffs(r / scale, g / scale, b / scale, cs)
+                                   : RGBToSigmoidCoeffs(0, 0, 0, cs);
     std::array<float, 311> out;
     for (int l = 395; l <= 705; ++l) out[l - 395] = scale * SigmoidPolynomial(c[0], c[1], c[2], (float)l);
     return out;
@@ -533,10 +567,131 @@ std::array<float, 311> DenseRGBUnbounded(float r, float g, float b) {
 }  // namespace pbrt_amd
 
 namespace pbrt_amd {
+static void WhiteXY(const std::array<float, 311> &s, float *x, float *y);
+static bool Invert3f(const float m[3][3], float r[3][3]);
+
+// pbrt's InnerProduct(a, b, c, d, e, f) (util/math.h): TwoProd / TwoSum compensated, rounded once
+static float CompInner3(float a0, float b0, float a1, float b1, float a2, float b2) {
+    auto twoProd = [](float a, float b, float *err) {
+        const float ab = a * b;
+        *err = std::fma(a, b, -ab);
+        return ab;
+    };
+    auto twoSum = [](float a, float b, float *err) {
+        const float s = a + b, delta = s - a;
+        *err = (a - (s - delta)) + (b - delta);
+        return s;
+    };
+    float e2, e1, e0, es1, es0;
+    const float p2 = twoProd(a2, b2, &e2);  // innermost term: InnerProduct(a2, b2)
+    const float p1 = twoProd(a1, b1, &e1);
+    const float s1 = twoSum(p1, p2, &es1);
+    const float err1 = e1 + (e2 + es1);
+    const float p0 = twoProd(a0, b0, &e0);
+    const float s0 = twoSum(p0, s1, &es0);
+    const float err0 = e0 + (err1 + es0);
+    return s0 + err0;
+}
+void MulCompensated3(const float a[3][3], const float b[3][3], float r[3][3]) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) r[i][j] = CompInner3(a[i][0], b[0][j], a[i][1], b[1][j], a[i][2], b[2][j]);
+}
+
+// RGBColorSpace's constructor in pbrt's own float arithmetic (util/colorspace.cpp:23-37):
+// W = SpectrumToXYZ(illuminant) (float InnerProducts / CIE_Y_integral), XYZ::FromxyY of the
+// float primaries, C = Mul(Inverse(rgb), W), XYZFromRGB = rgb * Diag(C) (compensated products,
+// one rounding each), RGBFromXYZ = Inverse(XYZFromRGB) (cofactors by DifferenceOfProducts)
+static void ColorSpaceMatricesF(const SpectralData &d, const std::array<float, 311> &illum, const float prim[6],
+                                float xyzFromRGB[3][3], float rgbFromXYZ[3][3]) {
+    const float CIE_Y_integral = 106.856895f;
+    float X = 0, Y = 0, Z = 0;
+    for (float lambda = kLambdaMin; lambda <= kLambdaMax; ++lambda) {
+        const int o = DenseOffset(lambda);
+        X += d.denseX[o] * illum[o];
+        Y += d.denseY[o] * illum[o];
+        Z += d.denseZ[o] * illum[o];
+    }
+    const float W[3] = {X / CIE_Y_integral, Y / CIE_Y_integral, Z / CIE_Y_integral};
+    auto fromxyY = [](float x, float y, float o[3]) {
+        if (y == 0) {
+            o[0] = o[1] = o[2] = 0;
+            return;
+        }
+        o[0] = x * 1.f / y;
+        o[1] = 1.f;
+        o[2] = (1 - x - y) * 1.f / y;
+    };
+    float R[3], G[3], B[3];
+    fromxyY(prim[0], prim[1], R);
+    fromxyY(prim[2], prim[3], G);
+    fromxyY(prim[4], prim[5], B);
+    const float rgb[3][3] = {{R[0], G[0], B[0]}, {R[1], G[1], B[1]}, {R[2], G[2], B[2]}};
+    float inv[3][3];
+    if (!Invert3f(rgb, inv)) throw Error("colour space primaries are degenerate");
+    float C[3];
+    for (int i = 0; i < 3; ++i) {
+        C[i] = 0;
+        for (int j = 0; j < 3; ++j) C[i] += inv[i][j] * W[j];
+    }
+    const float diag[3][3] = {{C[0], 0, 0}, {0, C[1], 0}, {0, 0, C[2]}};
+    MulCompensated3(rgb, diag, xyzFromRGB);
+    if (!Invert3f(xyzFromRGB, rgbFromXYZ)) throw Error("colour space matrix is singular");
+}
+
+// RGBColorSpace::sRGB / DCI_P3 / Rec2020 / ACES2065_1 (util/colorspace.cpp:83-105): the
+// densely sampled named illuminant, its photometric integral, white point and matrices
+const ColorSpaceDesc &GetColorSpace(int cs) {
+    if (cs < 0 || cs >= kNumColorSpaces) throw Error("colour space index out of range");
+    static std::once_flag once;
+    static ColorSpaceDesc *spaces = nullptr;
+    std::call_once(once, [] {
+        const SpectralData &d = GetSpectralData();
+        spaces = new ColorSpaceDesc[kNumColorSpaces];
+        for (int k = 0; k < kNumColorSpaces; ++k) {
+            ColorSpaceDesc &c = spaces[k];
+            const ColorSpaceDef &def = kColorSpaceDefs[k];
+            c.name = def.name;
+            for (int i = 0; i < 6; ++i) c.prim[i] = (float)def.prim[i];
+            if (std::string(def.illuminant) == "stdillum-D65") {
+                c.illuminant = d.denseD65;
+            } else {
+                auto it = d.illuminants.find(def.illuminant);
+                if (it == d.illuminants.end())
+                    throw Error(std::string("spectral data lacks the illuminant ") + def.illuminant);
+                std::vector<float> lam, val;
+                NormalizedIlluminant(d, it->second, &lam, &val);
+                for (int l = 395; l <= 705; ++l) c.illuminant[l - 395] = PiecewiseLinearEval(lam, val, (float)l);
+            }
+            c.photometric = PhotometricDense(d, c.illuminant);
+            ColorSpaceMatrices(d, c.illuminant, def.prim, c.xyzFromRGB, c.rgbFromXYZ);
+            ColorSpaceMatricesF(d, c.illuminant, c.prim, c.xyzFromRGBf, c.rgbFromXYZf);
+            WhiteXY(c.illuminant, &c.w[0], &c.w[1]);
+        }
+    });
+    return spaces[cs];
+}
+
+int ColorSpaceByName(const std::string &n) {
+    std::string name = n;
+    std::transform(name.begin(), name.end(), name.begin(), ::tolower);  // RGBColorSpace::GetNamed
+    for (int k = 0; k < kNumColorSpaces; ++k)
+        if (name == kColorSpaceDefs[k].name) return k;
+    return -1;
+}
+
 PLSpectrumDesc NamedPiecewiseLinear(const std::string &name) {
-    const auto &named = GetSpectralData().named;
+    const SpectralData &sd = GetSpectralData();
+    const auto &named = sd.named;
     auto it = named.find(name);
-    if (it == named.end()) throw Error("unknown named spectrum \"" + name + "\" (spectrum files are not supported)");
+    if (it == named.end()) {
+        // the standard illuminants are registered normalised to luminance 1 (spectrum.cpp:2604-2650)
+        auto il = sd.illuminants.find(name);
+        if (il == sd.illuminants.end())
+            throw Error("unknown named spectrum \"" + name + "\" (spectrum files are not supported)");
+        PLSpectrumDesc d;
+        NormalizedIlluminant(sd, il->second, &d.lambda, &d.value);
+        return d;
+    }
     const std::vector<float> &v = it->second;
     PLSpectrumDesc d;
     if (v[0] > kLambdaMin) {
@@ -589,10 +744,11 @@ static float InnerDense(const std::array<float, 311> &f, const std::array<float,
     return s;
 }
 typedef std::array<std::array<float, 3>, 3> M3;
+// SquareMatrix<3> * SquareMatrix<3> (util/math.h:1487-1495): one compensated InnerProduct per entry
 static M3 Mul3(const M3 &a, const M3 &b) {
     M3 r{};
     for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) r[i][j] = (float)((double)a[i][0] * b[0][j] + (double)a[i][1] * b[1][j] + (double)a[i][2] * b[2][j]);
+        for (int j = 0; j < 3; ++j) r[i][j] = CompInner3(a[i][0], b[0][j], a[i][1], b[1][j], a[i][2], b[2][j]);
     return r;
 }
 // SpectrumToXYZ(s).xy() (util/color.cpp)
@@ -669,8 +825,9 @@ std::array<float, 311> DenseCIEDaylight(float temperature) {
     return DenseOf(d.cieSLambda, v);
 }
 
-PixelSensorDesc BuildPixelSensor(const std::string &name, float whiteBalanceTemp) {
+PixelSensorDesc BuildPixelSensor(const std::string &name, float whiteBalanceTemp, int csId) {
     const SpectralData &d = GetSpectralData();
+    const ColorSpaceDesc &cs = GetColorSpace(csId);
     PixelSensorDesc s{};
     // PixelSensor::Create: named sensors white-balance to 6500 K unless told otherwise
     if (name != "cie1931" && whiteBalanceTemp == 0) whiteBalanceTemp = 6500;
@@ -678,8 +835,7 @@ PixelSensorDesc BuildPixelSensor(const std::string &name, float whiteBalanceTemp
     s.illum.fill(0.f);
     if (haveIllum) s.illum = DenseCIEDaylight(whiteBalanceTemp);
     // the output colour space's white (RGBColorSpace ctor: SpectrumToXYZ(illuminant).xy())
-    float wx, wy;
-    WhiteXY(d.denseD65, &wx, &wy);
+    const float wx = cs.w[0], wy = cs.w[1];
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) s.xyzFromSensorRGB[i][j] = i == j ? 1.f : 0.f;
     if (name == "cie1931") {
@@ -721,10 +877,10 @@ PixelSensorDesc BuildPixelSensor(const std::string &name, float whiteBalanceTemp
             r3[0] += s.r[o] * rl * s.illum[o];
             r3[1] += s.g[o] * rl * s.illum[o];
             r3[2] += s.b[o] * rl * s.illum[o];
-            gx += d.denseY[o] * d.denseD65[o];
-            x3[0] += d.denseX[o] * rl * d.denseD65[o];
-            x3[1] += d.denseY[o] * rl * d.denseD65[o];
-            x3[2] += d.denseZ[o] * rl * d.denseD65[o];
+            gx += d.denseY[o] * cs.illuminant[o];
+            x3[0] += d.denseX[o] * rl * cs.illuminant[o];
+            x3[1] += d.denseY[o] * rl * cs.illuminant[o];
+            x3[2] += d.denseZ[o] * rl * cs.illuminant[o];
         }
         for (int c = 0; c < 3; ++c) {
             rgbCamera[i][c] = r3[c] / gi;
@@ -745,8 +901,7 @@ PixelSensorDesc BuildPixelSensor(const std::string &name, float whiteBalanceTemp
     if (!Invert3f(AtA, inv)) throw Error("Sensor XYZ from RGB matrix could not be solved.");
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j)
-            s.xyzFromSensorRGB[j][i] =
-                (float)((double)inv[i][0] * AtB[0][j] + (double)inv[i][1] * AtB[1][j] + (double)inv[i][2] * AtB[2][j]);
+            s.xyzFromSensorRGB[j][i] = CompInner3(inv[i][0], AtB[0][j], inv[i][1], AtB[1][j], inv[i][2], AtB[2][j]);
     return s;
 }
 }  // namespace pbrt_amd

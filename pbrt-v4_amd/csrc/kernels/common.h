@@ -1667,9 +1667,8 @@ __device__ __attribute__((noinline)) int ResolveMixMaterial(const DeviceScene &S
     }
     return mat;
 }
-// The texture stage of EvaluateMaterialAndBSDF for one hit on the volumetric path (k_vtexture;
-// k_texture keeps its own inline copy of the same body: built on this function it hung on the
-// GPU in tests/test_textures.py's textured Cornell box, cause not isolated): bump / normal mapping into st.texBump[depth & 1], the reflectance as
+// The texture stage of EvaluateMaterialAndBSDF for one hit (k_texture on the surface path,
+// k_vtexture on the volumetric one): bump / normal mapping into st.texBump[depth & 1], the reflectance as
 // sigmoid coefficients (texCoef[0..2], texCoef[3] = 0) or 31 values (texR, texCoef[3] = 1),
 // the roughness alphas into texCoef[4..5]; record ri, its hit barycentrics hitB[k * NR + ri]
 // and lambda0[ri] (read only for textured materials).

@@ -193,12 +193,57 @@ __global__ void __launch_bounds__(kBlock, TraversalWaves(TM))
 // and the shade kernels' beta reads -- keep their coalesced layout.  Films are unchanged (each
 // path's arithmetic is independent of the order rays are traced in).
 constexpr int kRayBins = 4096, kBinBlock = 1024, kBinItems = 4;
+// Treelet of the ray origin: point location from the root of the quantised tree, `levels`
+// steps down the first interior child whose box contains o; the key is the path of slots (3
+// bits per level, 0 below a stop).  Sibling treelets get adjacent keys, so bin order walks the
+// tree's subtrees in turn and a CU's rays share the HBM-resident nodes below the LDS top.
+__device__ inline int TreeletKey(const DeviceScene &S, const V3 &o, int levels) {
+    int node = 0, path = 0;
+    for (int l = 0; l < levels; ++l) {
+        int slot = 8, next = -1;
+        if (node >= 0) {
+            const float4 *q = S.qnodes + (size_t)node * S.qStride;
+            const float4 f0 = q[0], f1 = q[1], f2 = q[2], f3 = q[3], f4 = q[4];
+            const uint32_t eb = __float_as_uint(f0.w), imask = eb >> 24;
+            const float p[3] = {f0.x, f0.y, f0.z};
+            const float sc[3] = {__uint_as_float((eb & 0xffu) << 23), __uint_as_float(((eb >> 8) & 0xffu) << 23),
+                                 __uint_as_float(((eb >> 16) & 0xffu) << 23)};
+            const uint32_t qw[12] = {__float_as_uint(f2.x), __float_as_uint(f2.y), __float_as_uint(f2.z),
+                                     __float_as_uint(f2.w), __float_as_uint(f3.x), __float_as_uint(f3.y),
+                                     __float_as_uint(f3.z), __float_as_uint(f3.w), __float_as_uint(f4.x),
+                                     __float_as_uint(f4.y), __float_as_uint(f4.z), __float_as_uint(f4.w)};
+            for (int c = 0; c < 8 && slot == 8; ++c) {
+                if (!((imask >> c) & 1u)) continue;
+                const int g = c >> 2, k = c & 3;
+                bool in = true;
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    const float lo = fmaf((float)((qw[2 * a + g] >> (8 * k)) & 0xffu), sc[a], p[a]);
+                    const float hi = fmaf((float)((qw[6 + 2 * a + g] >> (8 * k)) & 0xffu), sc[a], p[a]);
+                    in = in && o[a] >= lo && o[a] <= hi;
+                }
+                if (in) {
+                    slot = c;
+                    next = __float_as_int(f1.x) + __popc(imask & ((1u << c) - 1u));
+                }
+            }
+        }
+        path = path << 3 | (slot & 7);
+        node = next;
+    }
+    return path;
+}
 __device__ inline int RayBinKey(const DeviceScene &S, const V3 &o, const V3 &d) {
     // S.rayBinMode: 0 = origin 8^3 x octant; 1 = origin 4^3 x direction 8x8 (octahedral);
-    // 2 = origin 2^3 x direction 32x16
+    // 2 = origin 2^3 x direction 32x16; 3 = origin treelet (3 levels) x octant; 4 = origin
+    // treelet (4 levels).  The treelet keys need the quantised tree (else mode 0).
     const int mode = S.rayBinMode;
-    const int cBits = mode == 0 ? 3 : (mode == 1 ? 2 : 1);
-    const float cScale = mode == 0 ? 1.f : (mode == 1 ? 0.5f : 0.25f);
+    if (mode >= 3 && S.compressed) {
+        if (mode == 4) return TreeletKey(S, o, 4);
+        return TreeletKey(S, o, 3) << 3 | (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
+    }
+    const int cBits = (mode == 0 || mode >= 3) ? 3 : (mode == 1 ? 2 : 1);
+    const float cScale = (mode == 0 || mode >= 3) ? 1.f : (mode == 1 ? 0.5f : 0.25f);
     const float cMax = (float)((1 << cBits) - 1);
     int c[3];
 #pragma unroll
@@ -210,7 +255,7 @@ __device__ inline int RayBinKey(const DeviceScene &S, const V3 &o, const V3 &d) 
     for (int b = 0; b < cBits; ++b)
 #pragma unroll
         for (int a = 0; a < 3; ++a) m |= ((c[a] >> b) & 1) << (3 * b + a);
-    if (mode == 0) return m << 3 | (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
+    if (mode == 0 || mode >= 3) return m << 3 | (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0);
     // octahedral direction cell
     const float l1 = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
     float x = l1 > 0 ? d.x / l1 : 0.f, y = l1 > 0 ? d.y / l1 : 0.f;
@@ -1333,7 +1378,6 @@ __global__ void __launch_bounds__(kBlock) k_texture(DeviceScene S, PathState st,
     __syncthreads();
     S.tex.rgbZNodes = zLds;
     if (nLut) S.tex.luts = lutLds;
-    const int N = st.NR;
     const PathRecords &rec = st.rec[depth & 1];
     const int *hitPrim = st.hitPrim[depth & 1];
     const float *hitB = st.hitB[depth & 1];
@@ -1341,72 +1385,7 @@ __global__ void __launch_bounds__(kBlock) k_texture(DeviceScene S, PathState st,
         const int ri = st.matQ[MT][QueueSlot(mats, qi)];
         const int prim = hitPrim[ri];
         const int mat = HitMaterial(S, st, depth, ri, prim);
-        const int4 mt = S.matTex[mat];
-        const int4 mb = S.hasBump ? S.matBump[mat] : make_int4(-1, -1, 0, 0);
-        if (mt.x < 0 && mt.y < 0 && !mb.z) continue;
-        V3 p0, p1, p2;
-        PrimVerts(S, prim, &p0, &p1, &p2);
-        const TriSurface surf = SurfaceAt<Ext>(S, prim, p0, p1, p2, hitB[ri], hitB[N + ri], hitB[2 * N + ri]);
-        const TexEvalCtx tc = HitTexCtx(S, surf);
-        if (mb.z) {
-            // bump / normal mapping (surfscatter.cpp:109-127): the perturbed shading normal and
-            // dpdu, per record, for the shade kernel and the next depth's emission MIS
-            BumpCtx bc;
-            bc.p = surf.p;
-            bc.n = surf.n;
-            bc.u = tc.u;
-            bc.v = tc.v;
-            bc.dudx = tc.dudx;
-            bc.dudy = tc.dudy;
-            bc.dvdx = tc.dvdx;
-            bc.dvdy = tc.dvdy;
-            bc.ns = surf.ns;
-            bc.dpdu = surf.dpdus;
-            if (prim < S.nTris) {
-                TriShading sh;
-                const bool has = LoadTriShading(S, prim, &sh);
-                TriangleShadingDiff(p0, p1, p2, has ? &sh : nullptr, surf, &bc.dpdv, &bc.dndu, &bc.dndv);
-            } else {  // a disk: shading = geometric frame, no normal derivatives
-                bc.dpdv = surf.dpdv;
-                bc.dndu = bc.dndv = V3(0, 0, 0);
-            }
-            V3 ns, dpdus;
-            BumpShading(bc, S.tex, mb.y, [&](const TexEvalCtx &c) { return TexFloatFast<Full>(S, mb.x, c); }, &ns, &dpdus);
-            float *tb = st.texBump[depth & 1];
-            tb[ri] = ns.x;
-            tb[(size_t)N + ri] = ns.y;
-            tb[2 * (size_t)N + ri] = ns.z;
-            tb[3 * (size_t)N + ri] = dpdus.x;
-            tb[4 * (size_t)N + ri] = dpdus.y;
-            tb[5 * (size_t)N + ri] = dpdus.z;
-        }
-        if (mt.x >= 0) {
-            const DeviceTexProgram pg = S.tex.progs[mt.x];
-            if (!Full || pg.simple) {
-                float c[4];
-                SpectrumImageCoeffs<Full>(S.tex, S.tex.nodes[S.tex.instrs[pg.p1].node], tc, c);
-                st.texCoef[ri] = c[0];
-                st.texCoef[(size_t)N + ri] = c[1];
-                st.texCoef[2 * (size_t)N + ri] = c[2];
-                st.texCoef[3 * (size_t)N + ri] = 0.f;
-            } else if constexpr (Full) {
-                float R[kTexMaxRegs];
-                TexPhase1(S.tex, pg, tc, R);
-                for (SpectralIter it(rec.lambda0[ri]); it.i < kNSpectrumSamples; it.Next())
-                    st.texR[(size_t)it.i * N + ri] = TexPhase2(S.tex, pg, R, it.lam, it.i);
-                st.texCoef[3 * (size_t)N + ri] = 1.f;
-            }
-        }
-        if (mt.y >= 0) {
-            float ur = TexFloatFast<Full>(S, mt.y, tc), vr = TexFloatFast<Full>(S, mt.z, tc);
-            if (mt.w) {
-                ur = RoughnessToAlpha(ur);
-                vr = RoughnessToAlpha(vr);
-            }
-            const TrowbridgeReitz t = TrowbridgeReitz::Make(ur, vr);
-            st.texCoef[4 * (size_t)N + ri] = t.ax;
-            st.texCoef[5 * (size_t)N + ri] = t.ay;
-        }
+        HitTextures<Full, Ext>(S, st, depth, ri, prim, mat, hitB, rec.lambda0);
     }
 }
 

@@ -155,6 +155,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_debug_set_queue_check", "pbrt_debug_queue_holes",
     "pbrt_debug_equal_area", "pbrt_debug_cloud_density",
     "pbrt_debug_pl2d", "pbrt_debug_windowed2d",
+    "pbrt_color_space_index", "pbrt_debug_color_space", "pbrt_debug_rgb_spectrum", "pbrt_debug_rgb2spec_column_cs",
 ]
 
 _LIB = None
@@ -233,6 +234,10 @@ def _lib():
     lib.pbrt_debug_pl2d.argtypes = [c.c_int, c.c_int, c.c_void_p, c.c_int, c.c_int] + [c.c_void_p] * 4 + [
         c.c_int, c.c_void_p]
     lib.pbrt_debug_windowed2d.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_void_p]
+    lib.pbrt_color_space_index.argtypes = [c.c_char_p]
+    lib.pbrt_debug_color_space.argtypes = [c.c_int, c.c_void_p]
+    lib.pbrt_debug_rgb_spectrum.argtypes = [c.c_int, c.c_void_p, c.c_int, c.c_float, c.c_void_p, c.c_int, c.c_void_p]
+    lib.pbrt_debug_rgb2spec_column_cs.argtypes = [c.c_int] * 4 + [c.c_void_p]
     lib.pbrt_debug_procedural.argtypes = [c.c_int, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_debug_queue_counts.argtypes = [c.c_void_p, c.POINTER(c.c_int32), c.c_int]
     lib.pbrt_debug_trowbridge.argtypes = [c.c_void_p, c.c_void_p]
@@ -362,6 +367,44 @@ def debug_pl2d(dim, cdf, data, xs, ys, pr, pv0, pv1, queries):
     _check(_lib().pbrt_debug_pl2d(int(dim), int(cdf), d.ctypes.data, int(xs), int(ys), p.ctypes.data, a0.ctypes.data,
                                   a1.ctypes.data, q.ctypes.data, len(q), o.ctypes.data))
     return o
+
+
+COLOR_SPACES = ("srgb", "dci-p3", "rec2020", "aces2065-1")
+
+
+def color_space_index(name):
+    """ColorSpace directive name -> index 0..3 (RGBColorSpace::GetNamed; raises when unknown)."""
+    k = _lib().pbrt_color_space_index(name.encode())
+    if k < 0:
+        raise PbrtError(_lib().pbrt_last_error().decode())
+    return k
+
+
+def debug_color_space(cs):
+    """One colour space's constants (pbrt_debug_color_space): dict of prim[6], w[2],
+    xyz_from_rgb / rgb_from_xyz [3][3], photometric, illuminant[311]."""
+    o = np.zeros(338, np.float32)
+    _check(_lib().pbrt_debug_color_space(int(cs), o.ctypes.data))
+    return {"prim": o[:6], "w": o[6:8], "xyz_from_rgb": o[8:17].reshape(3, 3), "rgb_from_xyz": o[17:26].reshape(3, 3),
+            "photometric": o[26], "illuminant": o[27:]}
+
+
+def debug_rgb_spectrum(cs, rgbs, lambdas, unbounded_scale=1.0):
+    """RGB -> spectrum in colour space cs (pbrt_debug_rgb_spectrum): [n][3 + 3 nl] rows of
+    coefficients, albedo(lambda), unbounded(s rgb)(lambda), illuminant(s rgb)(lambda)."""
+    x = np.ascontiguousarray(rgbs, np.float32).reshape(-1, 3)
+    lam = np.ascontiguousarray(lambdas, np.float32).ravel()
+    o = np.zeros((len(x), 3 + 3 * len(lam)), np.float32)
+    _check(_lib().pbrt_debug_rgb_spectrum(int(cs), x.ctypes.data, len(x), float(unbounded_scale), lam.ctypes.data,
+                                          len(lam), o.ctypes.data))
+    return o
+
+
+def debug_rgb2spec_column(cs, maxc, j, i):
+    """Column (maxc, j, i) of colour space cs's RGBToSpectrumTable: [64][3]."""
+    o = np.zeros(192, np.float32)
+    _check(_lib().pbrt_debug_rgb2spec_column_cs(int(cs), int(maxc), int(j), int(i), o.ctypes.data))
+    return o.reshape(64, 3)
 
 
 def debug_windowed2d(func, queries):

@@ -24,6 +24,7 @@ def per_dispatch(csv_path, counter, kernel="k_closest"):
 
 src, bench_path, dst = Path(sys.argv[1]), Path(sys.argv[2]), Path(sys.argv[3])
 head = sys.argv[4] if len(sys.argv) > 4 else "unknown"
+label = sys.argv[5] if len(sys.argv) > 5 else "C4: 9,994,244 triangles"
 fetch, n = per_dispatch(src / "fetch" / "run_counter_collection.csv", "FETCH_SIZE")
 write, _ = per_dispatch(src / "write" / "run_counter_collection.csv", "WRITE_SIZE")
 hit, _ = per_dispatch(src / "tcc" / "run_counter_collection.csv", "TCC_HIT_sum")
@@ -32,7 +33,7 @@ bench = json.loads(bench_path.read_text().strip().splitlines()[-1])
 rays = bench["roofline"]["rays_per_launch"]
 fetch_b, write_b = 2 * 1024 * fetch, 1024 * write
 rec = {
-    "kernel": "k_closest (C4: 9,994,244 triangles, quantised BVH8 nodes, 6 waves/SIMD, rays binned at depth >= 1)",
+    "kernel": f"k_closest ({label}, quantised BVH8 nodes, 6 waves/SIMD, rays binned at depth >= 1)",
     "head": head,
     "dispatches": n,
     "fetch_size_kb_mean": fetch,
@@ -50,8 +51,8 @@ rec = {
     "l2_hit_rate": round(hit / (hit + miss), 4),
     "mean_launch_us": bench["roofline"]["mean_launch_us"],
     "bench_value_msamples_s": bench["value"],
-    "note": ("PMC dispatches average all depths of one 1920x1080x128 render (4 passes x 6 depths); rays_per_launch "
-             "and the launch time are the bench line's event-timed first-pass launches"),
+    "note": ("PMC dispatches average all depths of one bench step's render; rays_per_launch and the launch time "
+             "are the bench line's event-timed launches"),
 }
 dst.write_text(json.dumps(rec, indent=1) + "\n")
 print(json.dumps(rec, indent=1))

@@ -1,4 +1,5 @@
-// C ABI and render driver of pbrt-v4_amd (declared in include/pbrt_amd.h).
+// C ABI and render driver of pbrt-v4_amd (declared in include/pbrt_amd.h; the component entry
+// points tests and tools use in include/pbrt_amd_debug.h).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -12,6 +13,7 @@
 #include <vector>
 
 #include "../../include/pbrt_amd.h"
+#include "../../include/pbrt_amd_debug.h"
 #include "core/bssrdf.h"
 #include "core/hair.h"
 #include "core/measured.h"

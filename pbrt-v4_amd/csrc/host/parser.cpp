@@ -804,9 +804,11 @@ class Parser {
         MaterialDesc m;
         m.name = name;
         // shading-normal perturbation (materials.cpp: GetFloatTextureOrNull("displacement"),
-        // scene.cpp normal map cache: Image::Read(normalmap, ColorEncoding::Linear)), for the
-        // diffuse, dielectric and conductor materials of the surface wavefront
-        if (type == "diffuse" || type == "dielectric" || type == "conductor" || type == "subsurface") {
+        // scene.cpp normal map cache: Image::Read(normalmap, ColorEncoding::Linear)): every
+        // material Create but hair's, interface's and mix's reads them (materials.cpp:51-664)
+        if (type == "diffuse" || type == "dielectric" || type == "conductor" || type == "subsurface" ||
+            type == "coateddiffuse" || type == "coatedconductor" || type == "diffusetransmission" ||
+            type == "measured" || type == "retroreflective" || type == "thindielectric") {
             if (Param *d = ps.Find("displacement")) {
                 MatTexPending &mp = PendingTex(ps.loc);
                 mp.hasDisp = true;
@@ -999,7 +1001,7 @@ class Parser {
             m.type = type == "conductor" ? kMatConductor : kMatRetroreflective;
             if (m.type == kMatRetroreflective)
                 for (const Param &q : ps.params)
-                    if (q.type == "texture" && !q.attribute)
+                    if (q.type == "texture" && !q.attribute && q.name != "displacement")
                         throw Error(ps.loc + ": textured parameters of the retroreflective material are not supported yet");
             Param *eta = ps.Find("eta"), *k = ps.Find("k"), *refl = ps.Find("reflectance");
             if (refl && (eta || k))
@@ -3273,7 +3275,9 @@ void Parser::ResolveTextures() {
             m.texAmount = CompileTexProgram(scene, node, false);
             continue;
         }
-        if (m.type != kMatDiffuse && m.type != kMatDielectric && m.type != kMatConductor)
+        // textured reflectance / roughness: diffuse, dielectric and conductor materials; bump and
+        // normal maps on every material that reads them (MakeMaterial)
+        if ((mp.hasRefl || mp.hasRough) && m.type != kMatDiffuse && m.type != kMatDielectric && m.type != kMatConductor)
             throw Error(mp.loc + ": textures are supported on diffuse, dielectric and conductor materials only");
         if (mp.hasDisp) {
             m.dispNode = FloatParamNode(&mp.disp, 0.f, mp.loc);

@@ -1672,9 +1672,14 @@ __device__ __attribute__((noinline)) int ResolveMixMaterial(const DeviceScene &S
 // sigmoid coefficients (texCoef[0..2], texCoef[3] = 0) or 31 values (texR, texCoef[3] = 1),
 // the roughness alphas into texCoef[4..5]; record ri, its hit barycentrics hitB[k * NR + ri]
 // and lambda0[ri] (read only for textured materials).
+// Always inlined: compiled as a call (s_swappc) from k_texture it hung the textured Cornell box
+// on the GPU (round 4 and again in round 6: tests/test_textures.py timed out in the first
+// closest-hit-to-shade pass), with k_texture<*, false, false>'s private segment grown from 108 to
+// 2012 B per lane (the kernel's modified DeviceScene argument spilled to scratch for the callee's
+// reference) and 56 more VGPRs; inlined, the kernels keep the inline copy's code and resources.
 template <bool Full, bool Ext>
-__device__ inline void HitTextures(const DeviceScene &S, const PathState &st, int depth, int ri, int prim, int mat,
-                                   const float *hitB, const float *lambda0s) {
+__device__ __forceinline__ void HitTextures(const DeviceScene &S, const PathState &st, int depth, int ri, int prim,
+                                            int mat, const float *hitB, const float *lambda0s) {
     const int N = st.NR;
     const int4 mt = S.matTex[mat];
     const int4 mb = S.hasBump ? S.matBump[mat] : make_int4(-1, -1, 0, 0);

@@ -2206,7 +2206,10 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
         const float b0 = v.hitB[ri], b1 = v.hitB[NR + ri], b2 = v.hitB[2 * NR + ri];
         V3 p0, p1, p2;
         PrimVerts(S, prim, &p0, &p1, &p2);
-        const TriSurface si = SurfaceAt<Ext>(S, prim, p0, p1, p2, b0, b1, b2);
+        TriSurface si = SurfaceAt<Ext>(S, prim, p0, p1, p2, b0, b1, b2);
+        // bump / normal mapping (surfscatter.cpp:109-127): k_vtexture's shading frame for this
+        // record (the BSDF frame, the light sample and the next vertex's MIS context use it)
+        if (S.hasBump) BumpedShading(S, st, wf, mat, ri, &si);
         const V3 wo3 = Normalize(-rd);
         int mIn, mOut;
         MediaOf(S, prim, medium, &mIn, &mOut);

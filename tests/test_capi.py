@@ -1,5 +1,6 @@
 """C ABI surface: the library loads without a GPU, exports every entry point declared in
-include/pbrt_amd.h, and the loader fails loudly on unsupported input (pbrt's ErrorExit)."""
+include/pbrt_amd.h (the renderer API) and include/pbrt_amd_debug.h (component entry points for
+tests and tools), and the loader fails loudly on unsupported input (pbrt's ErrorExit)."""
 import ctypes
 import re
 
@@ -8,9 +9,13 @@ import pytest
 from conftest import ROOT, SCENES
 
 
-def header_symbols():
-    text = (ROOT / "include" / "pbrt_amd.h").read_text()
+def header_symbols(names=("pbrt_amd.h", "pbrt_amd_debug.h")):
+    text = "".join((ROOT / "include" / n).read_text() for n in names)
     return sorted(set(re.findall(r"\b(pbrt_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_renderer_header_has_no_debug_entry_points():
+    assert not [s for s in header_symbols(("pbrt_amd.h",)) if s.startswith("pbrt_debug_")]
 
 
 def test_header_declares_python_symbol_list(pa):

@@ -1,0 +1,18 @@
+# Round-6 check: textured GPU tests (k_texture on the shared HitTextures) first, then the whole
+# -m gpu suite, the C2 4-wave shade A/B (lib/exp_w4.so: PBRT_SHADE_WAVES=4), and the C4 / C3
+# k_closest PMC records.  Stops at the first failure.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r6e
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_textures.py tests/test_vol_textures.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/tex.log 2>&1 || { echo "textured tests failed"; tail -15 $O/tex.log; exit 3; }
+tail -1 $O/tex.log
+bash tools/gpu_r6.sh r6e tests "" "" || exit $?
+for lib in libpbrt_amd exp_w4; do
+  PBRT_AMD_LIB=$PWD/pbrt-v4_amd/lib/$lib.so timeout -k 10 120 python -u tools/film_hash.py > $O/hash_$lib.log 2>&1 || { echo "hash $lib failed"; tail -3 $O/hash_$lib.log; exit 3; }
+  echo "$lib $(tail -1 $O/hash_$lib.log)"
+  PBRT_AMD_LIB=$PWD/pbrt-v4_amd/lib/$lib.so timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline > $O/c2_$lib.log 2>&1 || { echo "bench $lib failed"; tail -3 $O/c2_$lib.log; exit 3; }
+  tail -1 $O/c2_$lib.log | cut -c1-200
+done
+HEAD_SHA=${HEAD_SHA:-unknown} bash tools/gpu_r6_pmc.sh r6e "c4 c3"

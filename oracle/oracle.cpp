@@ -6067,11 +6067,16 @@ struct Renderer {
             Float bn = std::max<Float>(1e-2, std::min<Float>(1.0, ml[10]));
             Float a = ml[11], e = ml[8];
             Spectrum sig;
+            // a textured sigma_a / reflectance (texEval at the hit)
+            const int ht = f->material_tex ? f->material_tex[4 * mat] : -1;
+            Spectrum hq{};
+            if (ht >= 0) hq = tex.EvalS(ht, tex.Ctx(si), lambda);
             for (int i = 0; i < NS; ++i) {
                 const Float l = lambda.lambda[i];
                 const int kind = (int)ml[1];
                 Float q;
-                if (kind == 0) q = ml[2];
+                if (ht >= 0) q = hq[i];
+                else if (kind == 0) q = ml[2];
                 else if (kind == 1) q = ml[6] * Sigmoid(ml[3], ml[4], ml[5], l);
                 else {
                     const int pl = (int)ml[7], o = f->pl_offsets[pl];

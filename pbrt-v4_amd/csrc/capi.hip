@@ -1264,15 +1264,8 @@ static void BuildDevice(pbrt_context *c) {
         S.tex = TexView{};
         if (!s.texPrograms.empty() || S.hasBump) {
             // textures on the volumetric path: k_vtexture + k_vsurface<..., Tex> (diffuse,
-            // dielectric, conductor); mix materials resolve in k_vclosest<TM, true>; bump on
-            // layered materials stays surface-only
-            if (c->volumetric)
-                for (const MaterialDesc &m : s.materials)
-                    if ((m.texDisp >= 0 || m.normalMap >= 0) &&
-                        (m.type == kMatCoatedDiffuse || m.type == kMatCoatedConductor || m.type == kMatDiffuseTransmission ||
-                         m.type == kMatMeasured))
-                        throw Error("bump or normal mapping on layered or diffuse transmission materials together with "
-                                    "the volumetric path is not supported yet");
+            // dielectric, conductor) and k_vlayered (bump / normal maps, hair sigma_a and
+            // reflectance); mix materials resolve in k_vclosest<TM, true>
             c->texNodes.Upload(tt.nodes);
             c->texSpec.Upload(tt.spec);
             c->texImages.Upload(tt.images);

@@ -414,6 +414,7 @@ class Parser {
         std::string loc;
         bool hasRefl = false;
         Param refl;
+        int reflSpec = 0;  // kSpecAlbedo, or kSpecUnbounded (hair "sigma_a")
         bool hasRough = false;
         Param ur, vr;  // type "" = constant 0 (no parameter)
         bool remap = true;
@@ -934,17 +935,27 @@ class Parser {
                     throw Error(ps.loc + ": \"" + p->type + " " + p->name + "\" for the hair material is not supported yet (constant floats only)");
                 return (float)p->nums[0];
             };
+            // a textured sigma_a (Unbounded) or reflectance (Albedo) is evaluated per hit by the
+            // texture stage (GetSpectrumTexture, materials.cpp:135-160)
+            auto textured = [&](Param *p, int spec) {
+                MatTexPending &mp = PendingTex(ps.loc);
+                mp.hasRefl = true;
+                mp.refl = *p;
+                mp.reflSpec = spec;
+            };
             if (sa) {
                 if (refl) warn("Ignoring \"reflectance\" parameter since \"sigma_a\" was provided.");
                 if (eu) warn("Ignoring \"eumelanin\" parameter since \"sigma_a\" was provided.");
                 if (ph) warn("Ignoring \"pheomelanin\" parameter since \"sigma_a\" was provided.");
                 m.hairMode = 0;
-                m.hairSpec = ConstSpectrum(sa, false, ps.loc, "hair");
+                if (sa->type == "texture") textured(sa, kSpecUnbounded);
+                else m.hairSpec = ConstSpectrum(sa, false, ps.loc, "hair");
             } else if (refl) {
                 if (eu) warn("Ignoring \"eumelanin\" parameter since \"reflectance\" was provided.");
                 if (ph) warn("Ignoring \"pheomelanin\" parameter since \"reflectance\" was provided.");
                 m.hairMode = 1;
-                m.hairSpec = ConstSpectrum(refl, true, ps.loc, "hair");
+                if (refl->type == "texture") textured(refl, kSpecAlbedo);
+                else m.hairSpec = ConstSpectrum(refl, true, ps.loc, "hair");
             } else {
                 // the concentrations' RGB sigma_a (ce, cp clamped at 0 by GetBxDF)
                 const float ce = eu ? std::max(0.f, constFloat(eu)) : (ph ? 0.f : 1.3f);
@@ -3277,7 +3288,8 @@ void Parser::ResolveTextures() {
         }
         // textured reflectance / roughness: diffuse, dielectric and conductor materials; bump and
         // normal maps on every material that reads them (MakeMaterial)
-        if ((mp.hasRefl || mp.hasRough) && m.type != kMatDiffuse && m.type != kMatDielectric && m.type != kMatConductor)
+        if (((mp.hasRefl && m.type != kMatHair) || mp.hasRough) && m.type != kMatDiffuse && m.type != kMatDielectric &&
+            m.type != kMatConductor)
             throw Error(mp.loc + ": textures are supported on diffuse, dielectric and conductor materials only");
         if (mp.hasDisp) {
             m.dispNode = FloatParamNode(&mp.disp, 0.f, mp.loc);
@@ -3300,7 +3312,7 @@ void Parser::ResolveTextures() {
             m.normalMap = img;
         }
         if (mp.hasRefl) {
-            const int node = SpectrumParamNode(&mp.refl, kSpecAlbedo, 0.5f, mp.loc);
+            const int node = SpectrumParamNode(&mp.refl, mp.reflSpec, 0.5f, mp.loc);
             m.texReflectance = CompileTexProgram(scene, node, true);
         }
         if (mp.hasRough) {

@@ -2236,6 +2236,13 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
         const float hairBm = fmaxf(1e-2f, fminf(1.f, L2.y)), hairBn = fmaxf(1e-2f, fminf(1.f, L2.z));
         const float hairDen = HairReflectanceDenom(hairBn);
         const float hq[7] = {L0.y, L0.z, L0.w, L1.x, L1.y, L1.z, L1.w};
+        // a textured sigma_a / reflectance: k_vtexture's value for this record (sigmoid
+        // coefficients, or one value per wavelength)
+        const bool hairTex = hair && S.textured && S.matTex[mat].x >= 0;
+        const bool hairTexR = hairTex && st.texCoef[3 * (size_t)NR + ri] != 0;
+        const float4 hairTc = hairTex && !hairTexR ? make_float4(st.texCoef[ri], st.texCoef[(size_t)NR + ri],
+                                                                 st.texCoef[2 * (size_t)NR + ri], 0.f)
+                                                   : make_float4(0.f, 0.f, 0.f, 0.f);
         {
             SpectralIter it(lambda0);
 #pragma unroll 1
@@ -2245,7 +2252,9 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
                     continue;
                 }
                 if (hair) {
-                    const float q = SssSpectrumAt(S, hq, it.lam);
+                    const float q = !hairTex ? SssSpectrumAt(S, hq, it.lam)
+                                    : hairTexR ? st.texR[(size_t)i * NR + ri]
+                                               : SigmoidPolynomial(hairTc.x, hairTc.y, hairTc.z, it.lam);
                     sp.a[i] = L0.x == 0 ? (q > 0 ? q : 0.f) : HairSigmaAFromReflectance(Clampf(q, 0, 1), hairDen);
                     continue;
                 }

@@ -221,7 +221,7 @@ def test_hair_loader_forms(pa):
     ('Material "hair" "rgb reflectance" [1.2 0.5 0.5]', "albedo"),
     ('Material "hair" "rgb sigma_a" [-1 0.5 0.5]', "negative"),
     ('Texture "t" "float" "constant"\nMaterial "hair" "texture beta_m" "t"', "not supported"),
-    ('Texture "t" "spectrum" "checkerboard"\nMaterial "hair" "texture sigma_a" "t"', "not supported"),
+    ('Texture "t" "float" "constant"\nMaterial "hair" "texture eumelanin" "t"', "not supported"),
 ])
 def test_hair_loader_errors(pa, material, msg):
     with pytest.raises(pa.PbrtError, match=msg):
@@ -235,11 +235,38 @@ def test_hair_oracle_renders(pa, oracle):
     assert np.isfinite(img).all() and img.mean() > 0.01
 
 
+# textured sigma_a (Unbounded) and reflectance (Albedo): GetSpectrumTexture per hit
+# (materials.cpp:135-160, materials.h:380-404), evaluated by k_vtexture for k_vlayered
+TEX_REFL = ('Texture "c" "spectrum" "checkerboard" "float uscale" 6 "float vscale" 6 "rgb tex1" [0.8 0.5 0.3] '
+            '"rgb tex2" [0.25 0.2 0.1]\nMaterial "hair" "texture reflectance" "c" "float beta_n" 0.4')
+TEX_SIGMA = ('Texture "s" "spectrum" "checkerboard" "float uscale" 6 "float vscale" 6 "rgb tex1" [0.2 0.4 1.0] '
+             '"rgb tex2" [1.5 1.0 0.6]\nMaterial "hair" "texture sigma_a" "s"')
+
 FORMS = {
     "melanin": 'Material "hair" "float eumelanin" 0.8 "float pheomelanin" 0.3',
     "reflectance": 'Material "hair" "rgb reflectance" [0.8 0.55 0.3] "float beta_m" 0.25 "float beta_n" 0.4',
     "sigma_rough": 'Material "hair" "rgb sigma_a" [0.06 0.1 0.2] "float beta_m" 0.6 "float beta_n" 0.8 "float alpha" 0',
+    "tex_reflectance": TEX_REFL,
+    "tex_sigma_a": TEX_SIGMA,
 }
+
+
+@pytest.mark.parametrize("material, const", [
+    (TEX_REFL, 'Material "hair" "rgb reflectance" [0.8 0.5 0.3] "float beta_n" 0.4'),
+    (TEX_SIGMA, 'Material "hair" "rgb sigma_a" [0.2 0.4 1.0]'),
+])
+def test_textured_hair_oracle(pa, oracle, material, const):
+    """The textured forms load (the program in the material's texture slot), render finite,
+    and differ from the constant form that equals one of the checks."""
+    kw = dict(xresolution=24, yresolution=18, spp=8)
+    sc, sc0 = pa.Scene.from_string(scene(material), SCENES, **kw), pa.Scene.from_string(scene(const), SCENES, **kw)
+    f = sc.flat()
+    assert any(f.material_tex[4 * k] >= 0 for k in range(f.n_materials))
+    m = [f.output_rgb_from_sensor_rgb[i] for i in range(9)]
+    a = oracle.film_to_rgb(oracle.render(sc, threads=8), m)
+    b = oracle.film_to_rgb(oracle.render(sc0, threads=8), m)
+    assert np.isfinite(a).all() and a.mean() > 0.005
+    assert np.abs(a - b).mean() > 1e-4
 
 
 @pytest.mark.gpu

@@ -6593,6 +6593,10 @@ struct Renderer {
                     const int pl = (int)q[6], a = f->pl_offsets[pl];
                     return PLEval(f->pl_lambda + a, f->pl_value + a, f->pl_offsets[pl + 1] - a, lam);
                 };
+                // a textured reflectance: texEval at the entry (materials.h:823-841)
+                const int rt = f->material_tex ? f->material_tex[4 * mat] : -1;
+                Spectrum rTex{};
+                if (rt >= 0 && P[0] != 0) rTex = tex.EvalS(rt, tex.Ctx(si), lambda);
                 for (int i = 0; i < NS; ++i) {
                     const Float lam = lambda.lambda[i];
                     Float sa, ss;
@@ -6601,7 +6605,8 @@ struct Renderer {
                         ss = std::max<Float>(0, P[1] * specAt(P + 11, lam));
                     } else {
                         const Float mfree = std::max<Float>(0, P[1] * specAt(P + 11, lam));
-                        const Float rh = osss::InvertCatmullRom(bd.rho, bd.rhoEff, osss::NRho, Clamp(specAt(P + 4, lam), 0, 1));
+                        const Float refl = rt >= 0 ? rTex[i] : specAt(P + 4, lam);
+                        const Float rh = osss::InvertCatmullRom(bd.rho, bd.rhoEff, osss::NRho, Clamp(refl, 0, 1));
                         ss = rh / mfree;
                         sa = (1 - rh) / mfree;
                     }

@@ -1710,7 +1710,7 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
         v.sss = SssRecords{};
         if (!c->desc.sss.empty()) {
             c->sssF.Alloc((size_t)(2 * 31 + 3 + 3 + 2 + 3 + 1) * NR);
-            c->sssI.Alloc((size_t)7 * NR);
+            c->sssI.Alloc((size_t)8 * NR);
             float *sf = c->sssF.p;
             int *si = c->sssI.p;
             auto sF = [&](int k) {
@@ -1739,6 +1739,7 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
             q.mOut = sI(1);
             q.flags = sI(1);
             q.hitPrim = sI(1);
+            q.src = sI(1);
         }
     }
     if (!c->devStats.p) {

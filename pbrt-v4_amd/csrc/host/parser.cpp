@@ -905,7 +905,15 @@ class Parser {
                     d.b = param(ss, false);
                 } else if (Param *refl = ps.Find("reflectance")) {
                     d.mode = 1;
-                    d.a = param(refl, true);
+                    if (refl->type == "texture") {
+                        // evaluated per hit by the texture stage; k_vsss_* read it at the entry
+                        MatTexPending &mp = PendingTex(ps.loc);
+                        mp.hasRefl = true;
+                        mp.refl = *refl;
+                        mp.reflSpec = kSpecAlbedo;
+                    } else {
+                        d.a = param(refl, true);
+                    }
                     if (Param *mfp = ps.Find("mfp")) d.b = param(mfp, false);
                     else d.b.kind = 0, d.b.value = 1;  // ConstantSpectrum(1)
                 } else {

@@ -373,6 +373,7 @@ struct SssRecords {
     float *lambda0, *etaScale; // [NR]
     float *hitB, *resPdf;      // [3][NR] the reservoir's hit (barycentrics / shape coords), [NR]
     int *mat, *pixel, *depth, *mIn, *mOut, *flags, *hitPrim;  // [NR] (flags: kUni* bits)
+    int *src;  // [NR] the entry's record index in this iteration (its texture-stage results)
 };
 struct VolState {
     VolRecords rec[2];

@@ -1717,6 +1717,7 @@ __global__ void __launch_bounds__(kBlock, PBRT_VOL_SURF_WAVES) k_vsurface(Device
             sr.mIn[js] = mIn;
             sr.mOut[js] = mOut;
             sr.flags[js] = (bu ? kUniBeta : 0) | (ruUni ? kUniRu : 0);
+            sr.src[js] = ri;
             continue;
         }
         const int jn = ShardSlot(shardBase, WavePush(nextCnt, true), st.capS, st.NR);
@@ -1765,9 +1766,35 @@ __device__ inline float SssSpectrumAt(const DeviceScene &S, const float *q, floa
     const int pl = (int)q[6], a = S.plOffsets[pl], na = S.plOffsets[pl + 1] - a;
     return PiecewiseLinearEval(S.plLambda + a, S.plValue + a, na, lam);
 }
-// SubsurfaceMaterial::GetBSSRDF's sigma_a / sigma_s at one wavelength (materials.h:823-841),
-// as the TabulatedBSSRDF's sigma_t and rho
-__device__ inline SssCoeffs SssCoeffsAt(const DeviceScene &S, const float *P, const SssTable &t, float lam) {
+// A textured subsurface reflectance (materials.h:823-841 texEval(reflectance)): the texture
+// stage's value at the entry record src of this iteration, per wavelength index i (sigmoid
+// coefficients, or one value per wavelength); on == false: the material's constant form
+struct SssTexRefl {
+    bool on = false, perLambda = false;
+    float c0 = 0, c1 = 0, c2 = 0;
+    const float *r = nullptr;  // texR + src, stride NR
+    int NR = 0;
+    __device__ float At(int i, float lam) const {
+        return perLambda ? r[(size_t)i * NR] : SigmoidPolynomial(c0, c1, c2, lam);
+    }
+};
+__device__ inline SssTexRefl SssTexReflOf(const DeviceScene &S, const PathState &st, int mat, int src) {
+    SssTexRefl x;
+    if (!S.textured || S.matTex[mat].x < 0) return x;
+    const int NR = st.NR;
+    x.on = true;
+    x.perLambda = st.texCoef[3 * (size_t)NR + src] != 0;
+    x.c0 = st.texCoef[src];
+    x.c1 = st.texCoef[(size_t)NR + src];
+    x.c2 = st.texCoef[2 * (size_t)NR + src];
+    x.r = st.texR + src;
+    x.NR = NR;
+    return x;
+}
+// SubsurfaceMaterial::GetBSSRDF's sigma_a / sigma_s at wavelength index i, lam (materials.h:
+// 823-841), as the TabulatedBSSRDF's sigma_t and rho
+__device__ inline SssCoeffs SssCoeffsAt(const DeviceScene &S, const float *P, const SssTable &t, float lam,
+                                        const SssTexRefl &tex = SssTexRefl{}, int i = 0) {
     float sa, ss;
     if (P[0] == 0) {
         const float a = P[1] * SssSpectrumAt(S, P + 4, lam), b = P[1] * SssSpectrumAt(S, P + 11, lam);
@@ -1776,7 +1803,7 @@ __device__ inline SssCoeffs SssCoeffsAt(const DeviceScene &S, const float *P, co
     } else {
         const float m = P[1] * SssSpectrumAt(S, P + 11, lam);
         const float mfree = m > 0 ? m : 0.f;
-        const float r = Clampf(SssSpectrumAt(S, P + 4, lam), 0, 1);
+        const float r = Clampf(tex.on ? tex.At(i, lam) : SssSpectrumAt(S, P + 4, lam), 0, 1);
         SssFromDiffuse(t, r, mfree, &sa, &ss);
     }
     return MakeSssCoeffs(sa, ss);
@@ -1855,7 +1882,7 @@ __global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_vsss_probe(Devic
         const float *P = S.sssParams + (size_t)kSssParams * k;
         const SssTable t = SssTable::At(S.sssTables + (size_t)kSssTableFloats * k);
         // GetBSSRDF + SampleSp with the subsurface samples (subsurface.cpp:24-42)
-        const SssCoeffs c0 = SssCoeffsAt(S, P, t, r.lambda0[e]);
+        const SssCoeffs c0 = SssCoeffsAt(S, P, t, r.lambda0[e], SssTexReflOf(S, st, mat, r.src[e]), 0);
         float uc, u0, u1;
         SssSamplesAt(S, st, r.pixel[e], r.depth[e], &uc, &u0, &u1);
         V3 p0, p1;
@@ -1909,14 +1936,15 @@ __global__ void __launch_bounds__(kBlock) k_vsss_scatter(DeviceScene S0, PathSta
         float *bpP = r.beta + e, *ruP = r.ru + e;
         auto bp = [&](int i) -> float & { return bpP[(size_t)i * NR]; };
         auto ru = [&](int i) -> float & { return ruP[(size_t)i * NR]; };
-        const float pdf0 = SssPdfSp(t, SssCoeffsAt(S, P, t, lambda0), g);
+        const SssTexRefl tex = SssTexReflOf(S, st, mat, r.src[e]);
+        const float pdf0 = SssPdfSp(t, SssCoeffsAt(S, P, t, lambda0, tex, 0), g);
         const float pr = resPdf * pdf0;
         bool spAny = false, pdfAny = false;
         {
             SpectralIter it(lambda0);
 #pragma unroll 1
             for (int i = 0; i < kNS; ++i, it.Next()) {
-                const SssCoeffs ci = SssCoeffsAt(S, P, t, it.lam);
+                const SssCoeffs ci = SssCoeffsAt(S, P, t, it.lam, tex, i);
                 const float sp = SssSrScaled(t, ci, rDist), pdf = SssPdfSp(t, ci, g);
                 spAny |= sp != 0;
                 pdfAny |= pdf != 0;

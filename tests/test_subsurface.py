@@ -114,7 +114,10 @@ def test_subsurface_loader_forms(pa):
     ('Material "subsurface" "rgb sigma_s" [1 1 1]', 'without "sigma_a"'),
     ('Material "subsurface" "string name" "Nope"', "named medium not found"),
     ('Material "subsurface" "rgb reflectance" [1.2 0.5 0.5]', "albedo"),
-    ('Texture "t" "spectrum" "checkerboard"\nMaterial "subsurface" "texture reflectance" "t"', "not supported"),
+    ('Texture "t" "spectrum" "checkerboard"\nMaterial "subsurface" "rgb reflectance" [0.5 0.5 0.5] "texture mfp" "t"',
+     "not supported"),
+    ('Texture "t" "spectrum" "checkerboard"\nMaterial "subsurface" "texture sigma_a" "t" "rgb sigma_s" [1 1 1]',
+     "not supported"),
 ])
 def test_subsurface_loader_errors(pa, material, msg):
     with pytest.raises(pa.PbrtError, match=msg):
@@ -129,7 +132,28 @@ def test_subsurface_oracle_renders(pa, oracle):
     assert np.isfinite(img).all() and img.mean() > 0.01
 
 
+# a textured reflectance (GetBSSRDF's texEval(reflectance), materials.h:823-841): the texture stage
+# evaluates it at the entry hit and k_vsss_probe / k_vsss_scatter read it there
+TEX_REFL = ('Texture "t" "spectrum" "checkerboard" "float uscale" 4 "float vscale" 4 "rgb tex1" [0.9 0.6 0.4] '
+            '"rgb tex2" [0.3 0.5 0.8]\nMaterial "subsurface" "texture reflectance" "t" "rgb mfp" [0.08 0.06 0.05]')
+
+
+def test_textured_reflectance_oracle(pa, oracle):
+    kw = dict(xresolution=32, yresolution=24, spp=8)
+    a_sc = pa.Scene.from_string(scene(TEX_REFL, BLOB + BOX), SCENES, **kw)
+    b_sc = pa.Scene.from_string(scene('Material "subsurface" "rgb reflectance" [0.9 0.6 0.4] "rgb mfp" [0.08 0.06 0.05]',
+                                      BLOB + BOX), SCENES, **kw)
+    f = a_sc.flat()
+    assert any(f.material_tex[4 * k] >= 0 for k in range(f.n_materials))
+    m = [f.output_rgb_from_sensor_rgb[i] for i in range(9)]
+    a = oracle.film_to_rgb(oracle.render(a_sc, threads=8), m)
+    b = oracle.film_to_rgb(oracle.render(b_sc, threads=8), m)
+    assert np.isfinite(a).all() and a.mean() > 0.01
+    assert np.abs(a - b).mean() > 1e-4
+
+
 FORMS = {
+    "tex_reflectance": TEX_REFL,
     "sigma": 'Material "subsurface" "rgb sigma_a" [0.8 1.2 2.0] "rgb sigma_s" [20 16 10] "float scale" 3',
     "reflectance": 'Material "subsurface" "rgb reflectance" [0.85 0.55 0.35] "rgb mfp" [0.08 0.06 0.05] "float eta" 1.45',
     "named_rough": 'Material "subsurface" "string name" "Ketchup" "float scale" 40 "float roughness" 0.25',

@@ -845,18 +845,23 @@ struct BumpCtx {
     float u, v, dudx, dudy, dvdx, dvdy;
     V3 ns, dpdu, dpdv, dndu, dndv;
 };
-// SetShadingGeometry's shading dpdv (the bitangent ts) and dndu, dndv of a triangle hit
-// (Triangle::InteractionFromIntersection, shapes.h:961-1006): with vertex normals ts =
-// Cross(ns, ss) (CoordinateSystem when degenerate) rescaled with ss, and the normal
-// derivatives from the uv deltas (degenerate uv: CoordinateSystem of the normals' cross
-// product); without vertex normals the geometric dpdv and zero derivatives.
-PHD void TriangleShadingDiff(V3 p0, V3 p1, V3 p2, const TriShading *sh, const TriSurface &s, V3 *dpdvs, V3 *dndu,
-                             V3 *dndv) {
+// SetShadingGeometry's shading dpdv (the bitangent ts) and dndu, dndv of a triangle hit with
+// barycentrics b (Triangle::InteractionFromIntersection, shapes.h:940-1006): with vertex normals
+// or shading tangents ts = Cross(ns, ss), ss the interpolated S (the geometric dpdu without
+// one), CoordinateSystem when degenerate, rescaled with ss; the normal derivatives from the uv
+// deltas with vertex normals (degenerate uv: CoordinateSystem of the normals' cross product),
+// else zero; neither: the geometric dpdv and zero derivatives.
+PHD void TriangleShadingDiff(V3 p0, V3 p1, V3 p2, const TriShading *sh, const TriSurface &s, float b0, float b1,
+                             float b2, V3 *dpdvs, V3 *dndu, V3 *dndv) {
     *dpdvs = s.dpdv;
     *dndu = *dndv = V3(0, 0, 0);
-    if (!sh || !(sh->flags & 1)) return;
+    if (!sh || !(sh->flags & 5)) return;
     (void)p0, (void)p1, (void)p2;
     V3 ss = s.dpdu;
+    if (sh->flags & 4) {
+        ss = b0 * sh->s0 + b1 * sh->s1 + b2 * sh->s2;
+        if (LengthSquared(ss) == 0) ss = s.dpdu;
+    }
     V3 ts = Cross(s.ns, ss);
     if (LengthSquared(ts) > 0) ss = Cross(ts, s.ns);
     else CoordinateSystem(s.ns, &ss, &ts);
@@ -865,6 +870,7 @@ PHD void TriangleShadingDiff(V3 p0, V3 p1, V3 p2, const TriShading *sh, const Tr
         ts = ts / 1e8f;
     }
     *dpdvs = ts;
+    if (!(sh->flags & 1)) return;  // shading tangents without vertex normals: dndu = dndv = 0
     float uv[3][2] = {{0, 0}, {1, 0}, {1, 1}};
     if (sh->flags & 2)
         for (int k = 0; k < 3; ++k) uv[k][0] = sh->uv[k][0], uv[k][1] = sh->uv[k][1];

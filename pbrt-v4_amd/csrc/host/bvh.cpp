@@ -72,6 +72,7 @@ struct Builder2 {
                              [dim](const Prim &a, const Prim &b) { return a.centroid[dim] < b.centroid[dim]; });
             return mid;
         }
+        if (SahAllAxes()) return SplitAllAxes(start, end, nb, cb);
         constexpr int nBuckets = 12;
         int counts[nBuckets] = {0};
         Box bbox[nBuckets];
@@ -116,6 +117,74 @@ struct Builder2 {
             mid = (start + end) / 2;
             std::nth_element(&prims[start], &prims[mid], &prims[end - 1] + 1,
                              [dim](const Prim &a, const Prim &b) { return a.centroid[dim] < b.centroid[dim]; });
+        }
+        return mid;
+    }
+
+    // The binned SAH over all three axes (32 buckets each, default since round 6: C2 / C3
+    // k_closest -12 % / -14 %, profiles/r06_bvh_sah_ab.txt); PBRT_AMD_BVH_SAH=1 restores the
+    // centroid bounds' longest axis with 12 buckets (pbrt's BVHAggregate::buildRecursive)
+    static bool SahAllAxes() {
+        static const bool on = [] {
+            const char *e = std::getenv("PBRT_AMD_BVH_SAH");
+            return !(e && std::atoi(e) == 1);
+        }();
+        return on;
+    }
+    // the SAH's traversal cost against one triangle test (PBRT_AMD_BVH_CT, default 1/2)
+    static float TraversalCost() {
+        static const float ct = [] {
+            const char *e = std::getenv("PBRT_AMD_BVH_CT");
+            return e ? (float)std::atof(e) : 0.5f;
+        }();
+        return ct;
+    }
+    int SplitAllAxes(int start, int end, const Box &nb, const Box &cb) {
+        constexpr int nBuckets = 32;
+        const int n = end - start;
+        int bestDim = -1, bestBucket = -1;
+        float bestCost = kInfinity;
+        for (int dim = 0; dim < 3; ++dim) {
+            if (!(cb.mx[dim] > cb.mn[dim])) continue;
+            int counts[nBuckets] = {0};
+            Box bbox[nBuckets];
+            const float lo = cb.mn[dim], ext = cb.mx[dim] - cb.mn[dim];
+            for (int i = start; i < end; ++i) {
+                int b = (int)(nBuckets * ((prims[i].centroid[dim] - lo) / ext));
+                b = std::min(std::max(b, 0), nBuckets - 1);
+                counts[b]++;
+                bbox[b].Add(prims[i].box);
+            }
+            float costs[nBuckets - 1] = {};
+            int below = 0, above = 0;
+            Box bb, ba;
+            for (int i = 0; i < nBuckets - 1; ++i) {
+                bb.Add(bbox[i]);
+                below += counts[i];
+                costs[i] += below * bb.Area();
+            }
+            for (int i = nBuckets - 1; i >= 1; --i) {
+                ba.Add(bbox[i]);
+                above += counts[i];
+                costs[i - 1] += above * ba.Area();
+            }
+            for (int i = 0; i < nBuckets - 1; ++i)
+                if (costs[i] < bestCost) bestCost = costs[i], bestDim = dim, bestBucket = i;
+        }
+        const float cost = TraversalCost() + bestCost / nb.Area();
+        if (bestDim < 0 || !(n > maxLeaf || cost < (float)n)) return n > maxLeaf ? (start + end) / 2 : -1;
+        const float lo = cb.mn[bestDim], ext = cb.mx[bestDim] - cb.mn[bestDim];
+        auto bucketOf = [&](const Prim &p) {
+            const int b = (int)(nBuckets * ((p.centroid[bestDim] - lo) / ext));
+            return std::min(std::max(b, 0), nBuckets - 1);
+        };
+        Prim *pm = std::partition(&prims[start], &prims[end - 1] + 1, [&](const Prim &p) { return bucketOf(p) <= bestBucket; });
+        int mid = (int)(pm - &prims[0]);
+        if (mid == start || mid == end) {
+            mid = (start + end) / 2;
+            const int d = bestDim;
+            std::nth_element(&prims[start], &prims[mid], &prims[end - 1] + 1,
+                             [d](const Prim &a, const Prim &b) { return a.centroid[d] < b.centroid[d]; });
         }
         return mid;
     }

@@ -3346,24 +3346,12 @@ void Parser::ResolveTextures() {
     }
 }
 
-// bump / normal mapping on a mesh with shading tangents "S" would need its shading dpdv (the
-// bitangent), which the texture stage does not carry: refused
-static void CheckTangentFrames(const SceneDesc &s) {
-    for (size_t o = 0; o < s.triShade.size(); ++o)
-        if (s.triShade[o] & 4) {
-            const MaterialDesc &m = s.materials[s.triMaterial[o]];
-            if (m.texDisp >= 0 || m.normalMap >= 0)
-                throw Error("bump or normal mapping on a triangle mesh with shading tangents \"S\" is not supported yet");
-        }
-}
-
 SceneDesc LoadPbrtString(const std::string &text, const std::string &baseDir,
                          const std::map<std::string, std::string> &overrides) {
     SceneDesc s;
     Parser p(s, overrides);
     p.ParseString(text, "<string>", baseDir);
     p.Finish();
-    CheckTangentFrames(s);
     FinalizeScene(s);
     return s;
 }
@@ -3373,7 +3361,6 @@ SceneDesc LoadPbrtFile(const std::string &path, const std::map<std::string, std:
     Parser p(s, overrides);
     p.ParseFile(path);
     p.Finish();
-    CheckTangentFrames(s);
     FinalizeScene(s);
     return s;
 }

@@ -1705,7 +1705,8 @@ __device__ __forceinline__ void HitTextures(const DeviceScene &S, const PathStat
         if (prim < S.nTris) {
             TriShading sh;
             const bool has = LoadTriShading(S, prim, &sh);
-            TriangleShadingDiff(p0, p1, p2, has ? &sh : nullptr, surf, &bc.dpdv, &bc.dndu, &bc.dndv);
+            TriangleShadingDiff(p0, p1, p2, has ? &sh : nullptr, surf, hitB[ri], hitB[N + ri], hitB[2 * N + ri], &bc.dpdv,
+                                &bc.dndu, &bc.dndv);
         } else {  // a disk: shading = geometric frame, no normal derivatives
             bc.dpdv = surf.dpdv;
             bc.dndu = bc.dndv = V3(0, 0, 0);

@@ -165,6 +165,12 @@ int pbrt_debug_layered(const float *params12, const float *a31, const float *b31
  * triangles, tree depth, worst-case traversal stack entries, wide node bytes, quantised node
  * bytes, 0, 0 */
 int pbrt_debug_bvh_stats(const pbrt_scene *scene, int64_t *out8);
+/* Host traversal of the device BVH8 (builder: spatial = 1 spatial splits, 0 object splits,
+   -1 the environment's choice) for n rays (ox oy oz dx dy dz); writes the closest t (-1 for
+   a miss) and the original triangle index, and stats4 = {node visits, triangle tests, leaf
+   references, nodes}.  Checks the builders against a brute-force search without a GPU. */
+int pbrt_debug_bvh_trace(const pbrt_scene *scene, int spatial, const float *rays, int n, float *tOut, int *primOut,
+                         int64_t *stats4);
 /* BVHLightSampler::buildBVH (lightsamplers.cpp:135-238) as the loader runs it, over given
  * LightBounds lights13 [n][13] = pMin3 pMax3 w3 phi cosTheta_o cosTheta_e twoSided: nodes12
  * [n_nodes][12] decoded CompactLightBounds (pMin3 pMax3 w3 phi cosTheta_o cosTheta_e), info3

@@ -709,9 +709,12 @@ static void BuildDevice(pbrt_context *c) {
         throw Error("BVH needs a " + std::to_string(c->bvh.maxStack) + "-entry traversal stack (limit " +
                     std::to_string(kMaxStackSize) + ")");
     BVH8 &b = c->bvh;
-    int nt = (int)s.tris.size();
-    std::vector<int> origToLeaf(nt);
-    for (int i = 0; i < nt; ++i) origToLeaf[b.triPrim[i]] = i;
+    // leaf-order positions: with spatial splits (PBRT_AMD_BVH_SBVH) a triangle may sit at several,
+    // each carrying the same per-prim data, so a hit on any copy shades the same triangle; the
+    // light records name the first
+    int nt = (int)b.triPrim.size();
+    std::vector<int> origToLeaf(s.tris.size(), -1);
+    for (int i = nt - 1; i >= 0; --i) origToLeaf[b.triPrim[i]] = i;
     const int nsh = (int)s.shapes.size();
     std::vector<int> pm(nt + nsh), pl(nt + nsh), po(b.triPrim.begin(), b.triPrim.end());
     std::vector<uint8_t> pf(nt + nsh, 0);
@@ -3435,6 +3438,68 @@ int pbrt_debug_bvh_stats(const pbrt_scene *scene, int64_t *out8) {
                               (int64_t)(b.nodes.size() * sizeof(BVH8Node)), (int64_t)(b.qnodes.size() * sizeof(BVH8QNode)),
                               0, 0};
         memcpy(out8, v, sizeof v);
+        return 0;
+    } catch (const std::exception &e) {
+        return Fail(e.what());
+    }
+}
+
+int pbrt_debug_bvh_trace(const pbrt_scene *scene, int spatial, const float *rays, int n, float *tOut, int *primOut,
+                         int64_t *stats4) {
+    try {
+        if (!scene || !rays || n < 0 || !tOut || !primOut || !stats4) return Fail("null argument");
+        const BVH8 b = BuildBVH8(scene->desc.verts, scene->desc.tris, 4, spatial);
+        int64_t nodeVisits = 0, triTests = 0;
+        std::vector<int> stack;
+        for (int i = 0; i < n; ++i) {
+            const V3 o(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]), d(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
+            float tMax = kInfinity;
+            int hit = -1;
+            stack.assign(1, 0);
+            while (!stack.empty()) {
+                const int ni = stack.back();
+                stack.pop_back();
+                ++nodeVisits;
+                const BVH8Node &nd = b.nodes[ni];
+                for (int c = 0; c < 8; ++c) {
+                    if (!(nd.occ >> c & 1)) continue;
+                    // exact slab test in double precision (a box that misses part of its
+                    // triangle shows up as a missed hit against the brute-force answer)
+                    double t0 = 0, t1 = tMax;
+                    const double lo[3] = {nd.lox[c], nd.loy[c], nd.loz[c]}, hi[3] = {nd.hix[c], nd.hiy[c], nd.hiz[c]};
+                    const double oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z};
+                    bool in = true;
+                    for (int a = 0; a < 3 && in; ++a) {
+                        if (dd[a] == 0) {
+                            if (oo[a] < lo[a] || oo[a] > hi[a]) in = false;
+                            continue;
+                        }
+                        double ta = (lo[a] - oo[a]) / dd[a], tb = (hi[a] - oo[a]) / dd[a];
+                        if (ta > tb) std::swap(ta, tb);
+                        t0 = std::max(t0, ta), t1 = std::min(t1, tb);
+                        if (t0 > t1) in = false;
+                    }
+                    if (!in) continue;
+                    const int ref = b.childRef[ni][c];
+                    if (ref >= 0) {
+                        stack.push_back(ref);
+                        continue;
+                    }
+                    const int enc = ~ref, first = enc >> 3, count = (enc & 7) + 1;
+                    for (int k = first; k < first + count; ++k) {
+                        ++triTests;
+                        const float *v = &b.triVerts[(size_t)k * 12];
+                        TriHit h;
+                        if (IntersectTriangle(o, d, tMax, V3(v[0], v[1], v[2]), V3(v[4], v[5], v[6]), V3(v[8], v[9], v[10]), &h))
+                            tMax = h.t, hit = b.triPrim[k];
+                    }
+                }
+            }
+            tOut[i] = hit >= 0 ? tMax : -1.f;
+            primOut[i] = hit;
+        }
+        const int64_t v[4] = {nodeVisits, triTests, (int64_t)b.triPrim.size(), (int64_t)b.nodes.size()};
+        memcpy(stats4, v, sizeof v);
         return 0;
     } catch (const std::exception &e) {
         return Fail(e.what());

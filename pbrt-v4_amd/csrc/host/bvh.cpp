@@ -1,5 +1,6 @@
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <cmath>
 #include <future>
 #include <cstdlib>
@@ -66,6 +67,9 @@ struct Builder2 {
             return (start + end) / 2;  // all centroids coincide: split the list
         }
         int mid;
+        if (n == 2 && SahAllAxes() && PairLeaves() == 1) return SplitAllAxes(start, end, nb, cb);
+        if (n == 2 && PairLeaves() == 2 && prims[start].box.Area() + prims[start + 1].box.Area() >= 1.9f * nb.Area())
+            return -1;
         if (n <= 2) {
             mid = (start + end) / 2;
             std::nth_element(&prims[start], &prims[mid], &prims[end - 1] + 1,
@@ -130,6 +134,17 @@ struct Builder2 {
             return !(e && std::atoi(e) == 1);
         }();
         return on;
+    }
+    // Two triangles whose boxes nearly coincide (area sum >= 1.9x their union's: a quad's two
+    // halves) stay one leaf instead of always splitting (default, PBRT_AMD_BVH_PAIR=2; C2
+    // k_closest -6 %, C3 / C4 unchanged, profiles/r06_bvh_sah_ab.txt); =1 puts every pair to the
+    // SAH's leaf test (C4 -1 %), =0 always splits as pbrt's builder does
+    static int PairLeaves() {
+        static const int mode = [] {
+            const char *e = std::getenv("PBRT_AMD_BVH_PAIR");
+            return e ? std::atoi(e) : 2;
+        }();
+        return mode;
     }
     // the SAH's traversal cost against one triangle test (PBRT_AMD_BVH_CT, default 1/2)
     static float TraversalCost() {
@@ -248,6 +263,287 @@ std::vector<Node2> BuildParallel(std::vector<Prim> &prims, int start, int end, i
     out[0].right = append(r);
     return out;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Spatial-split BVH (PBRT_AMD_BVH_SBVH=1; Stich, Friedrich and Dietrich 2009, "Spatial Splits
+// in Bounding Volume Hierarchies").  Beside the object split, a node whose best object split
+// leaves children overlapping by more than alpha of the root's area also bins the node's
+// bounds into 32 slabs per axis, clips every triangle reference into the slabs it spans, and
+// may split along a slab plane, referencing a straddling triangle from both sides (or from one,
+// when "unsplitting" it is cheaper).  The traversal is unchanged: a leaf lists triangles, and
+// a triangle may appear in several leaves.  Clipped boxes are padded outward by a few ulps and
+// then intersected with the triangle's own box, so every box still holds its part of the
+// triangle, and the closest-hit result is the same triangle test over a different visit order.
+struct SpatialBuilder {
+    const std::vector<V3> &verts;
+    const std::vector<std::array<int, 3>> &tris;
+    int maxLeaf;
+    float minOverlap;  // alpha * root area
+    std::atomic<long long> *budget;  // references that may still be duplicated
+
+    static constexpr int kBins = 32;
+
+    struct Result {
+        std::vector<Node2> nodes;
+        std::vector<Prim> refs;  // leaf order
+    };
+
+    static float Axis(const V3 &v, int d) { return d == 0 ? v.x : d == 1 ? v.y : v.z; }
+    static void SetAxis(V3 &v, int d, float f) { (d == 0 ? v.x : d == 1 ? v.y : v.z) = f; }
+
+    static Box Intersect(const Box &a, const Box &b) {
+        Box r;
+        r.mn = V3(std::max(a.mn.x, b.mn.x), std::max(a.mn.y, b.mn.y), std::max(a.mn.z, b.mn.z));
+        r.mx = V3(std::min(a.mx.x, b.mx.x), std::min(a.mx.y, b.mx.y), std::min(a.mx.z, b.mx.z));
+        if (r.mn.x > r.mx.x || r.mn.y > r.mx.y || r.mn.z > r.mx.z) return Box{};
+        return r;
+    }
+
+    // box of the part of triangle t with lo <= p[d] <= hi, within the reference box rb
+    Box ClipBox(int t, int d, float lo, float hi, const Box &rb) const {
+        const V3 v[3] = {verts[tris[t][0]], verts[tris[t][1]], verts[tris[t][2]]};
+        Box b;
+        for (int e = 0; e < 3; ++e) {
+            const V3 a = v[e], c = v[(e + 1) % 3];
+            const float ad = Axis(a, d), cd = Axis(c, d);
+            if (ad >= lo && ad <= hi) b.Add(a);
+            for (float pl : {lo, hi}) {
+                if ((ad < pl && cd > pl) || (ad > pl && cd < pl)) {
+                    const float s = (pl - ad) / (cd - ad);
+                    V3 p = a + (c - a) * s;
+                    SetAxis(p, d, pl);
+                    b.Add(p);
+                }
+            }
+        }
+        if (b.Empty()) return b;
+        for (int k = 0; k < 3; ++k) {
+            if (k == d) continue;
+            const float m = std::max(std::fabs(Axis(rb.mn, k)), std::fabs(Axis(rb.mx, k)));
+            const float pad = m * 4.7683716e-7f + 1e-30f;  // 8 ulps of the box's magnitude
+            SetAxis(b.mn, k, Axis(b.mn, k) - pad);
+            SetAxis(b.mx, k, Axis(b.mx, k) + pad);
+        }
+        SetAxis(b.mn, d, std::max(Axis(b.mn, d), lo));
+        SetAxis(b.mx, d, std::min(Axis(b.mx, d), hi));
+        return Intersect(b, rb);
+    }
+
+    struct ObjectSplit {
+        int dim = -1, bucket = -1;
+        float cost = kInfinity;
+        Box left, right;
+    };
+
+    ObjectSplit BestObjectSplit(const std::vector<Prim> &refs, const Box &cb) const {
+        ObjectSplit best;
+        for (int dim = 0; dim < 3; ++dim) {
+            const float lo = Axis(cb.mn, dim), ext = Axis(cb.mx, dim) - lo;
+            if (!(ext > 0)) continue;
+            int counts[kBins] = {0};
+            Box bbox[kBins];
+            for (const Prim &p : refs) {
+                int b = (int)(kBins * ((Axis(p.centroid, dim) - lo) / ext));
+                b = std::min(std::max(b, 0), kBins - 1);
+                counts[b]++;
+                bbox[b].Add(p.box);
+            }
+            Box below[kBins];
+            Box acc;
+            for (int i = 0; i < kBins; ++i) acc.Add(bbox[i]), below[i] = acc;
+            int cntBelow[kBins];
+            int c = 0;
+            for (int i = 0; i < kBins; ++i) c += counts[i], cntBelow[i] = c;
+            Box above;
+            int cntAbove = 0;
+            for (int i = kBins - 1; i >= 1; --i) {
+                above.Add(bbox[i]);
+                cntAbove += counts[i];
+                const float cost = cntBelow[i - 1] * below[i - 1].Area() + cntAbove * above.Area();
+                if (cost < best.cost) {
+                    best.cost = cost, best.dim = dim, best.bucket = i - 1;
+                    best.left = below[i - 1], best.right = above;
+                }
+            }
+        }
+        return best;
+    }
+
+    struct SpatialSplit {
+        int dim = -1;
+        float plane = 0, cost = kInfinity;
+    };
+
+    SpatialSplit BestSpatialSplit(const std::vector<Prim> &refs, const Box &nb) const {
+        SpatialSplit best;
+        for (int dim = 0; dim < 3; ++dim) {
+            const float lo = Axis(nb.mn, dim), ext = Axis(nb.mx, dim) - lo;
+            if (!(ext > 0)) continue;
+            const float w = ext / kBins;
+            auto planeAt = [&](int i) { return i == kBins ? Axis(nb.mx, dim) : lo + w * i; };
+            auto binOf = [&](float x) { return std::min(std::max((int)((x - lo) / w), 0), kBins - 1); };
+            int enter[kBins] = {0}, exit_[kBins] = {0};
+            Box bbox[kBins];
+            for (const Prim &p : refs) {
+                int b0 = binOf(Axis(p.box.mn, dim)), b1 = binOf(Axis(p.box.mx, dim));
+                enter[b0]++, exit_[b1]++;
+                if (b0 == b1) {
+                    bbox[b0].Add(p.box);
+                    continue;
+                }
+                for (int b = b0; b <= b1; ++b) bbox[b].Add(ClipBox(p.index, dim, planeAt(b), planeAt(b + 1), p.box));
+            }
+            Box below[kBins];
+            Box acc;
+            int nl[kBins], c = 0;
+            for (int i = 0; i < kBins; ++i) acc.Add(bbox[i]), below[i] = acc, c += enter[i], nl[i] = c;
+            Box above;
+            int nr = 0;
+            for (int i = kBins - 1; i >= 1; --i) {
+                above.Add(bbox[i]);
+                nr += exit_[i];
+                const float cost = nl[i - 1] * below[i - 1].Area() + nr * above.Area();
+                if (cost < best.cost) best.cost = cost, best.dim = dim, best.plane = planeAt(i);
+            }
+        }
+        return best;
+    }
+
+    Result Leaf(std::vector<Prim> &&refs, const Box &nb) const {
+        Result r;
+        Node2 n;
+        n.box = nb;
+        n.first = 0;
+        n.count = (int)refs.size();
+        r.nodes.push_back(n);
+        r.refs = std::move(refs);
+        return r;
+    }
+
+    static Box BoundsOf(const std::vector<Prim> &refs, Box *cb) {
+        Box b;
+        *cb = Box{};
+        for (const Prim &p : refs) b.Add(p.box), cb->Add(p.centroid);
+        return b;
+    }
+
+    Result Build(std::vector<Prim> &&refs, int depth) const {
+        Box cb;
+        const Box nb = BoundsOf(refs, &cb);
+        const int n = (int)refs.size();
+        if (n == 1) return Leaf(std::move(refs), nb);
+        std::vector<Prim> L, R;
+        ObjectSplit os = BestObjectSplit(refs, cb);
+        float bestCost = os.cost;
+        SpatialSplit ss;
+        if (depth < 48 && budget->load(std::memory_order_relaxed) > 0 && Intersect(os.left, os.right).Area() > minOverlap) {
+            ss = BestSpatialSplit(refs, nb);
+            if (ss.cost < bestCost) bestCost = ss.cost;
+            else ss.dim = -1;
+        }
+        const float cost = Builder2::TraversalCost() + bestCost / nb.Area();
+        if (os.dim < 0 && ss.dim < 0) {
+            // all centroids coincide and no spatial split: a leaf, or halve the list
+            if (n <= maxLeaf) return Leaf(std::move(refs), nb);
+            L.assign(refs.begin(), refs.begin() + n / 2);
+            R.assign(refs.begin() + n / 2, refs.end());
+        } else if (!(n > maxLeaf || cost < (float)n)) {
+            return Leaf(std::move(refs), nb);
+        } else if (ss.dim >= 0) {
+            const int d = ss.dim;
+            const float pl = ss.plane;
+            // the children's boxes and counts before the straddlers, then each straddler goes
+            // left, right or both, whichever the SAH prefers (reference unsplitting)
+            Box bl, br;
+            std::vector<Prim> straddle;
+            for (Prim &p : refs) {
+                if (Axis(p.box.mx, d) <= pl) bl.Add(p.box), L.push_back(p);
+                else if (Axis(p.box.mn, d) >= pl) br.Add(p.box), R.push_back(p);
+                else straddle.push_back(p);
+            }
+            long long dup = 0;
+            for (Prim &p : straddle) {
+                const Box lb = ClipBox(p.index, d, -kInfinity, pl, p.box);
+                const Box rb = ClipBox(p.index, d, pl, kInfinity, p.box);
+                const float nL = (float)L.size(), nR = (float)R.size();
+                Box blS = bl, brS = br, blW = bl, brW = br;
+                blS.Add(lb), brS.Add(rb), blW.Add(p.box), brW.Add(p.box);
+                const float cSplit = blS.Area() * (nL + 1) + brS.Area() * (nR + 1);
+                const float cLeft = blW.Area() * (nL + 1) + br.Area() * nR;
+                const float cRight = bl.Area() * nL + brW.Area() * (nR + 1);
+                if (lb.Empty() || (!rb.Empty() && cRight <= cLeft && cRight <= cSplit)) {
+                    br = brW, R.push_back(p);
+                } else if (rb.Empty() || (cLeft <= cSplit)) {
+                    bl = blW, L.push_back(p);
+                } else {
+                    Prim a = p, b = p;
+                    a.box = lb, b.box = rb;
+                    a.centroid = (lb.mn + lb.mx) * 0.5f, b.centroid = (rb.mn + rb.mx) * 0.5f;
+                    bl = blS, br = brS;
+                    L.push_back(a), R.push_back(b);
+                    ++dup;
+                }
+            }
+            budget->fetch_sub(dup, std::memory_order_relaxed);
+            if (L.empty() || R.empty()) {  // degenerate: fall back to halving
+                std::vector<Prim> all = L.empty() ? std::move(R) : std::move(L);
+                L.assign(all.begin(), all.begin() + all.size() / 2);
+                R.assign(all.begin() + all.size() / 2, all.end());
+            }
+        } else {
+            const int d = os.dim;
+            const float lo = Axis(cb.mn, d), ext = Axis(cb.mx, d) - lo;
+            for (Prim &p : refs) {
+                int b = (int)(kBins * ((Axis(p.centroid, d) - lo) / ext));
+                b = std::min(std::max(b, 0), kBins - 1);
+                (b <= os.bucket ? L : R).push_back(p);
+            }
+            if (L.empty() || R.empty()) {
+                std::vector<Prim> all = L.empty() ? std::move(R) : std::move(L);
+                std::sort(all.begin(), all.end(), [d](const Prim &a, const Prim &b) { return Axis(a.centroid, d) < Axis(b.centroid, d); });
+                L.assign(all.begin(), all.begin() + all.size() / 2);
+                R.assign(all.begin() + all.size() / 2, all.end());
+            }
+        }
+        std::vector<Prim>().swap(refs);
+        Result l, r;
+        if (depth < 4 && L.size() + R.size() >= (1u << 16)) {
+            auto fl = std::async(std::launch::async, [&] { return Build(std::move(L), depth + 1); });
+            r = Build(std::move(R), depth + 1);
+            l = fl.get();
+        } else {
+            l = Build(std::move(L), depth + 1);
+            r = Build(std::move(R), depth + 1);
+        }
+        Result out;
+        out.nodes.reserve(1 + l.nodes.size() + r.nodes.size());
+        out.refs.reserve(l.refs.size() + r.refs.size());
+        Node2 root;
+        root.box = nb;
+        out.nodes.push_back(root);
+        auto append = [&](Result &sub) {
+            const int off = (int)out.nodes.size(), roff = (int)out.refs.size();
+            for (Node2 nd : sub.nodes) {
+                if (!nd.leaf()) nd.left += off, nd.right += off;
+                else nd.first += roff;
+                out.nodes.push_back(nd);
+            }
+            out.refs.insert(out.refs.end(), sub.refs.begin(), sub.refs.end());
+            return off;
+        };
+        out.nodes[0].left = append(l);
+        out.nodes[0].right = append(r);
+        return out;
+    }
+};
+
+static bool SpatialSplitsOn() {
+    static const bool on = [] {
+        const char *e = std::getenv("PBRT_AMD_BVH_SBVH");
+        return e && std::atoi(e) > 0;
+    }();
+    return on;
+}
 }  // namespace
 
 // Quantise every node of out.nodes into out.qnodes (same indices).
@@ -364,7 +660,7 @@ static void ReorderGroupsDepthFirst(BVH8 &out, const std::vector<int> &depth, in
     out.childRef.swap(refs);
 }
 
-BVH8 BuildBVH8(const std::vector<V3> &verts, const std::vector<std::array<int, 3>> &tris, int maxLeafPrims) {
+BVH8 BuildBVH8(const std::vector<V3> &verts, const std::vector<std::array<int, 3>> &tris, int maxLeafPrims, int spatial) {
     BVH8 out;
     std::vector<Prim> prims;
     prims.reserve(tris.size());
@@ -418,7 +714,17 @@ BVH8 BuildBVH8(const std::vector<V3> &verts, const std::vector<std::array<int, 3
     }
     maxLeafPrims = std::min(std::max(maxLeafPrims, 1), kMaxLeafPrims);
     Builder2 b{prims, {}, maxLeafPrims};
-    b.nodes = BuildParallel(prims, 0, (int)prims.size(), maxLeafPrims, 0);
+    if (spatial < 0 ? SpatialSplitsOn() : spatial > 0) {
+        // leaves index the builder's reference list, which replaces prims below
+        const Box rootBox = all;
+        std::atomic<long long> budget{(long long)prims.size()};  // at most 2x the references
+        SpatialBuilder sb{verts, tris, maxLeafPrims, 1e-5f * rootBox.Area(), &budget};
+        SpatialBuilder::Result r = sb.Build(std::move(prims), 0);
+        prims = std::move(r.refs);
+        b.nodes = std::move(r.nodes);
+    } else {
+        b.nodes = BuildParallel(prims, 0, (int)prims.size(), maxLeafPrims, 0);
+    }
 
     // collapse BVH2 -> BVH8 (greedy: open the child with the largest surface area)
     struct Work {

@@ -77,7 +77,9 @@ struct BVH8 {
     V3 boundsMin, boundsMax;
 };
 
+// spatial: 1 = spatial splits (a triangle may be listed by several leaves), 0 = object splits
+// only, -1 = PBRT_AMD_BVH_SBVH
 BVH8 BuildBVH8(const std::vector<V3> &verts, const std::vector<std::array<int, 3>> &tris,
-               int maxLeafPrims = kMaxLeafPrims);
+               int maxLeafPrims = kMaxLeafPrims, int spatial = -1);
 
 }  // namespace pbrt_amd

@@ -148,7 +148,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_debug_queue_counts", "pbrt_debug_zsobol", "pbrt_debug_sampler", "pbrt_debug_rng", "pbrt_debug_det_math", "pbrt_debug_hair", "pbrt_debug_measured", "pbrt_debug_catmull_rom_gpu", "pbrt_debug_portal_eval", "pbrt_debug_procedural", "pbrt_debug_trowbridge", "pbrt_debug_fresnel",
     "pbrt_debug_named_spectrum", "pbrt_debug_bxdf", "pbrt_debug_layered", "pbrt_debug_triangle_shading", "pbrt_film_write_image",
     "pbrt_image_read_size", "pbrt_image_read", "pbrt_image_write", "pbrt_image_error", "pbrt_debug_filter_sample",
-    "pbrt_debug_bvh_stats", "pbrt_debug_light_bvh", "pbrt_intersect_tr", "pbrt_intersect_one_random", "pbrt_image_flip", "pbrt_set_kernel_profiling", "pbrt_get_kernel_stats",
+    "pbrt_debug_bvh_stats", "pbrt_debug_bvh_trace", "pbrt_debug_light_bvh", "pbrt_intersect_tr", "pbrt_intersect_one_random", "pbrt_image_flip", "pbrt_set_kernel_profiling", "pbrt_get_kernel_stats",
     "pbrt_debug_texture_eval",
     "pbrt_debug_env_eval",
     "pbrt_debug_shape_eval",
@@ -203,6 +203,7 @@ def _lib():
     lib.pbrt_film_get_rgb.argtypes = [c.c_void_p, c.c_void_p]
     lib.pbrt_intersect.argtypes = [c.c_void_p, c.c_void_p, c.c_int, c.c_int, c.c_void_p, c.c_void_p]
     lib.pbrt_debug_bvh_stats.argtypes = [c.c_void_p, c.c_void_p]
+    lib.pbrt_debug_bvh_trace.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_void_p, c.c_void_p, c.c_void_p]
     lib.pbrt_image_flip.argtypes = [c.c_void_p, c.c_void_p, c.c_int, c.c_int, c.c_void_p]
     lib.pbrt_intersect_tr.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_intersect_one_random.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p, c.c_void_p,
@@ -497,6 +498,17 @@ class Scene:
         _check(_lib().pbrt_debug_bvh_stats(self._h, out))
         keys = ("nodes", "triangles", "depth", "max_stack", "wide_bytes", "quantised_bytes")
         return dict(zip(keys, list(out)[:6]))
+
+    def bvh_trace(self, rays, spatial=-1):
+        """Closest hits of rays (n x 6: origin, direction) by a host traversal of the device BVH8
+        (pbrt_debug_bvh_trace): (t, triangle, stats); t = -1 and triangle = -1 for a miss."""
+        r = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 6)
+        n = r.shape[0]
+        t = np.zeros(n, np.float32)
+        prim = np.zeros(n, np.int32)
+        st = (ctypes.c_int64 * 4)()
+        _check(_lib().pbrt_debug_bvh_trace(self._h, int(spatial), r.ctypes.data, n, t.ctypes.data, prim.ctypes.data, st))
+        return t, prim, dict(zip(("node_visits", "tri_tests", "references", "nodes"), list(st)))
 
     def texture_eval(self, material, slot, hit14, lambdas=()):
         """The product's texture evaluation of a material's textured parameter at a hit

@@ -13,7 +13,7 @@ import pbrt_amd as pa
 
 scene = sys.argv[1] if len(sys.argv) > 1 else "cornell"
 x, y, spp = (int(v) for v in sys.argv[2:5]) if len(sys.argv) > 4 else (320, 180, 16)
-if scene == "cornell":
+if scene in ("cornell", "c2"):
     sc = pa.load_scene(ROOT / "scenes" / "cornell-box.pbrt", xresolution=x, yresolution=y, spp=spp)
 elif scene == "c3":
     import gen_c3

@@ -190,6 +190,14 @@ int pbrt_debug_kernel_sections(pbrt_context *ctx, uint64_t *cycles, int n);
  * stops with an error before any stage reads it.
  * pbrt_debug_queue_holes returns the holes found since its last call and resets the count.
  * PBRT_AMD_QUEUE_CHECK=1 turns the check on from the environment. */
+/* The plymesh displacement of shapes.cpp:1436-1452 (TriQuadMesh::Displace, util/mesh.h:91-191:
+   quads to triangles, normals when n is null, refinement to edges below edgeLength in render
+   space, p += d n, normals recomputed) with a closed-form d (mode 0: 0.1 u - 0.05 v; mode 1:
+   0.25 p.y u + 0.125; mode 2: 0.1) in place of the texture.  counts2 = {vertices, triangles} of the result;
+   fails when they exceed capVerts / capTris. */
+int pbrt_debug_displace(const float *p, const float *uv, const float *n, int nVerts, const int *tri, int nTri,
+                        const int *quad, int nQuad, const float *renderFromObject16, float edgeLength, int mode,
+                        int capVerts, int capTris, float *pOut, float *nOut, float *uvOut, int *triOut, int *counts2);
 int pbrt_debug_set_queue_check(int on);
 int pbrt_debug_queue_holes(int *holes);
 

@@ -1,7 +1,9 @@
-// Geometry BVH for the device: binned-SAH binary build in the manner of pbrt's
-// BVHAggregate::buildRecursive (cpu/aggregates.cpp:192-387: 12 buckets, leaf cost =
-// primitive count, 1/2 traversal cost) collapsed into an 8-wide tree whose nodes are laid
-// out for wave64 traversal (one 256-byte node = 8 child boxes in SoA + 8 child refs).
+// Geometry BVH for the device: a binned-SAH binary build after pbrt's
+// BVHAggregate::buildRecursive (cpu/aggregates.cpp:192-387: leaf cost = primitive count, 1/2
+// traversal cost), binned over all three axes with 32 buckets (pbrt: the longest axis, 12) and
+// keeping quad halves as one leaf (bvh.cpp), optionally with spatial splits, collapsed into an
+// 8-wide tree whose nodes are laid out for wave64 traversal (one 256-byte node = 8 child boxes
+// in SoA + 8 child refs).
 #pragma once
 
 #include <array>

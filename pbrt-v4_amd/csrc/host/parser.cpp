@@ -14,6 +14,7 @@
 #include <set>
 #include <sstream>
 
+#include "displace.h"
 #include "ply.h"
 #include "scene.h"
 #include "texture.h"
@@ -359,8 +360,12 @@ class Parser {
         std::string dir;  // directory of the declaring file (an area light's "filename")
         bool hasAlpha = false;  // "float alpha" < 1 or "texture alpha" (scene.cpp:1369-1384)
         Param alpha;
+        bool hasDisp = false;  // plymesh "texture displacement", applied once textures resolve
+        Param disp;
+        float edgeLength = 1;
     };
     std::vector<PendingShape> shapes;
+    void DisplacePlyMeshes();
     std::map<std::string, int> alphaIds;  // alpha parameter -> SceneDesc::alphaTex entry
     int AlphaId(const PendingShape &s);
     // object instancing (scene.cpp:309-395): shapes of each ObjectBegin/End definition, and the
@@ -1399,8 +1404,17 @@ class Parser {
             std::string f = ps.GetString("filename", "");
             if (f.empty()) throw Error(ps.loc + ": plymesh needs \"string filename\"");
             std::string path = (f[0] == '/') ? f : (dir.empty() ? f : dir + "/" + f);
-            if (ps.Find("displacement")) throw Error(ps.loc + ": plymesh displacement is not supported yet");
-            ps.GetFloat("edgelength", 1);
+            // shapes.cpp:1422-1458: a displacement texture refines and displaces the mesh
+            // (DisplacePlyMeshes, once the textures are resolved)
+            s.edgeLength = (float)ps.GetFloat("edgelength", 1);
+            if (Param *dp = ps.Find("displacement")) {
+                if (dp->type != "texture")
+                    throw Error(ps.loc + ": \"" + dp->type + " displacement\": plymesh displacement must be a float texture");
+                if (!activeInstance.empty())
+                    throw Error(ps.loc + ": plymesh displacement inside ObjectBegin is not supported yet");
+                s.hasDisp = true;
+                s.disp = *dp;
+            }
             PlyMesh m;
             try {
                 m = ReadPly(path);
@@ -2241,8 +2255,9 @@ void Parser::Finish() {
     };
     scene.cameraMedium = mediumOf(cameraMediumName, "Camera");
 
-    // ---- object instances (flattened), then shapes -> render-space triangles; area lights in
-    // shape order
+    // ---- displaced plymeshes, object instances (flattened), then shapes -> render-space
+    // triangles; area lights in shape order
+    DisplacePlyMeshes();
     ResolveInstances();
     const Mat4 &renderFromWorld = scene.camera.renderFromWorld;
     std::map<std::string, int> spectrumCache;
@@ -3281,6 +3296,55 @@ int Parser::AlphaId(const PendingShape &s) {
     const int id = (int)scene.alphaTex.size() - 1;
     alphaIds[key] = id;
     return id;
+}
+
+// The plymesh displacement of shapes.cpp:1425-1458: TriQuadMesh::Displace (host/displace.cpp)
+// with the texture evaluated on the host by the product's texture code at each vertex's
+// object-space position and uv, with no differentials (TextureEvalContext{p, uv})
+void Parser::DisplacePlyMeshes() {
+    std::vector<std::pair<PendingShape *, int>> todo;
+    for (PendingShape &s : shapes)
+        if (s.hasDisp) {
+            const int node = FloatParamNode(&s.disp, 0.f, s.loc);
+            todo.push_back({&s, CompileTexProgram(scene, node, false)});
+        }
+    if (todo.empty()) return;
+    TexTables tt;
+    BuildTexTables(scene, &tt);
+    const TexView T = HostTexView(tt);
+    const Mat4 &renderFromWorld = scene.camera.renderFromWorld;
+    for (auto &[sp, prog] : todo) {
+        PendingShape &s = *sp;
+        DisplaceMesh m;
+        m.p = s.P;
+        m.n = s.N;
+        for (size_t i = 0; i + 1 < s.uv.size(); i += 2) m.uv.push_back({s.uv[i], s.uv[i + 1]});
+        m.tri = s.idx;
+        m.quad = s.quadIdx;
+        const Mat4 rfo = Mul(renderFromWorld, s.renderFromObject);
+        float rf[16];
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j) rf[4 * i + j] = (float)rfo[i][j];
+        try {
+            DisplaceTriQuadMesh(&m, rf, s.edgeLength, [&](V3 p, float u, float v) {
+                TexEvalCtx c{};
+                c.p = p;
+                c.n = V3(0, 0, 0);
+                c.u = u;
+                c.v = v;
+                return HostTexFloat(T, prog, c);
+            });
+        } catch (const std::runtime_error &e) {
+            throw Error(s.loc + ": " + e.what());
+        }
+        s.P = std::move(m.p);
+        s.N = std::move(m.n);
+        s.uv.clear();
+        for (const auto &t : m.uv) s.uv.insert(s.uv.end(), {t[0], t[1]});
+        s.idx = std::move(m.tri);
+        s.quadIdx.clear();
+        s.hasDisp = false;
+    }
 }
 
 void Parser::ResolveTextures() {

@@ -919,4 +919,123 @@ void ComputeCameraDifferentials(SceneDesc &s) {
     }
 }
 
+void BuildTexTables(const SceneDesc &s, TexTables *t) {
+    *t = TexTables{};
+    t->basis = s.texBasis;
+    t->basis.push_back(0.f);
+    for (size_t i = 0; i < s.textures.size(); ++i) {
+        const TextureDesc &d = s.textures[i];
+        DeviceTexNode n{};
+        n.kind = d.kind;
+        n.flags = (d.spectrum ? 1 : 0) | (d.specType << 1) | (d.invert ? 8 : 0) | (d.mapping == kMap3D ? 16 : 0) |
+                  (d.basis >= 0 ? kTexNodeBasis : 0);
+        n.child0 = d.child[0];
+        n.child1 = d.child[1];
+        n.child2 = d.child[2];
+        n.image = d.image;
+        n.mapping = d.mapping == kMap3D ? 0 : d.mapping;
+        n.filter = d.filter;
+        for (int k = 0; k < 12; ++k) n.p[k] = d.textureFromRender[k];
+        for (int k = 0; k < 3; ++k) n.p[12 + k] = d.vs[k], n.p[15 + k] = d.vt[k];
+        for (int k = 0; k < 4; ++k) n.p[18 + k] = d.map[k];
+        for (int k = 0; k < 4; ++k) n.p[22 + k] = d.fvalue[k];
+        if (d.kind == kTexDirectionMix)
+            for (int k = 0; k < 3; ++k) n.p[22 + k] = d.dir[k];
+        n.p[26] = d.scale;
+        n.p[27] = d.maxAniso;
+        if (d.basis >= 0) {  // the multispectral basis table: start in texBasis, length
+            n.p[22] = (float)d.basis;
+            n.p[24] = (float)d.basisWidth;
+        }
+        if (d.kind >= kTexDots) {  // procedural: octaves, omega, variation (core/texture_eval.h)
+            n.p[22] = (float)d.octaves;
+            n.p[23] = d.omega;
+            n.p[24] = d.variation;
+        }
+        t->nodes.push_back(n);
+        for (int k = 0; k < 4; ++k) {
+            const TexSpectrumConst &c = d.svalue[k];
+            t->spec.push_back(DeviceTexSpec{c.rgb ? 1.f : 0.f, c.value, c.c[0], c.c[1], c.c[2], c.scale, 0.f, 0.f});
+        }
+        t->nodeInfo.insert(t->nodeInfo.end(), {n.kind, n.flags, n.child0, n.child1, n.child2, n.image, n.mapping, n.filter});
+        t->nodeParams.insert(t->nodeParams.end(), n.p, n.p + 28);
+        for (int k = 0; k < 4; ++k) {
+            const DeviceTexSpec &q = t->spec[4 * i + k];
+            t->specFlat.insert(t->specFlat.end(), {q.rgb, q.value, q.c0, q.c1, q.c2, q.scale, 0.f, 0.f});
+        }
+    }
+    for (size_t i = 0; i < s.images.size(); ++i) {
+        const ImageDesc &im = s.images[i];
+        DeviceImage di{};
+        di.format = im.format;
+        di.nc = im.nc;
+        di.nLevels = (int)im.levelRes.size();
+        di.wrap = im.wrap;
+        di.levelBase = (int)t->levels.size();
+        di.lutBase = (int)(256 * i);
+        const uint64_t base = t->data.size();
+        t->data.insert(t->data.end(), im.data.begin(), im.data.end());
+        t->data.resize((t->data.size() + 15) & ~size_t(15));
+        for (size_t l = 0; l < im.levelRes.size(); ++l) {
+            const uint64_t off = base + im.levelOffset[l];
+            t->levels.push_back(DeviceImageLevel{im.levelRes[l][0], im.levelRes[l][1], (uint32_t)off, (uint32_t)(off >> 32)});
+            t->levelInfo.insert(t->levelInfo.end(), {im.levelRes[l][0], im.levelRes[l][1], (int32_t)(uint32_t)off,
+                                                     (int32_t)(uint32_t)(off >> 32)});
+        }
+        t->luts.insert(t->luts.end(), im.toLinear.begin(), im.toLinear.end());
+        t->images.push_back(di);
+        t->imageInfo.insert(t->imageInfo.end(), {di.format, di.nc, di.nLevels, di.wrap, di.levelBase, di.lutBase, 0, 0});
+        t->rawInfo.insert(t->rawInfo.end(), {im.rawW, im.rawH, im.format, im.nc, im.encoding, 0, 0, 0});
+        t->rawGamma.push_back(im.gamma);
+        t->rawOffset.push_back(t->rawData.size());
+        t->rawData.insert(t->rawData.end(), im.raw.begin(), im.raw.end());
+    }
+    for (const TexInstr &in : s.texInstrs)
+        t->instrs.push_back(DeviceTexInstr{in.op | (in.a << 8) | (in.b << 16) | (in.c << 24), in.node});
+    for (const TexProgram &pg : s.texPrograms) {
+        int simple = 0;
+        if (pg.spectrum && pg.n1 == 1 && pg.n2 == 1) {
+            const TexInstr &a = s.texInstrs[pg.p1], &b = s.texInstrs[pg.p2];
+            simple = a.op == kT1SImage && a.a == 0 && b.op == kT2RGBReg && b.a == 0 && b.b == 0;
+        }
+        t->progs.push_back(DeviceTexProgram{pg.p1, pg.n1, pg.p2, pg.n2, pg.result, pg.nRegs, simple, 0});
+    }
+    for (const MaterialDesc &m : s.materials) {
+        t->matTex.insert(t->matTex.end(), {m.texReflectance, m.texURough, m.texVRough, m.remapRoughness ? 1 : 0});
+        auto root = [&](int p) { return p >= 0 ? s.texPrograms[p].root : -1; };
+        t->matTexNode.insert(t->matTexNode.end(),
+                             {root(m.texReflectance), root(m.texURough), root(m.texVRough), m.remapRoughness ? 1 : 0});
+        t->matMixNode.insert(t->matMixNode.end(), {m.mixMat[0], m.mixMat[1], root(m.texAmount), 0});
+        t->matBumpNode.insert(t->matBumpNode.end(), {root(m.texDisp), m.normalMap});
+    }
+}
+// a TexView over host copies (debug entry points; the device view points at DevBufs)
+TexView HostTexView(const TexTables &t) {
+    const std::vector<float> &rgb = RGBToSpectrumTableData();
+    TexView v{};
+    v.nodes = t.nodes.data();
+    v.spec = t.spec.data();
+    v.images = t.images.data();
+    v.levels = t.levels.data();
+    v.data = t.data.data();
+    v.luts = t.luts.data();
+    v.instrs = t.instrs.data();
+    v.progs = t.progs.data();
+    v.rgbZNodes = rgb.data();
+    v.rgbCoeffs = rgb.data() + 64;
+    v.ewaLut = GetSpectralData().mipFilterLUT.data();
+    v.noisePerm = GetSpectralData().noisePerm.data();
+    v.basis = t.basis.data();
+    v.nProgs = (int)t.progs.size();
+    v.nLuts = (int)t.images.size();
+    return v;
+}
+
+float HostTexFloat(const TexView &T, int prog, const TexEvalCtx &c) {
+    float R[kTexMaxRegs];
+    const DeviceTexProgram pg = T.progs[prog];
+    TexPhase1(T, pg, c, R);
+    return R[pg.result];
+}
+
 }  // namespace pbrt_amd

@@ -3,6 +3,7 @@
 
 #include <array>
 #include <string>
+#include <vector>
 
 #include "scene.h"
 #include "../core/texture_eval.h"
@@ -47,6 +48,33 @@ struct LightImage {
 };
 LightImage LoadLightImage(const std::string &filename, const std::string &loc);
 // lowers texture node `node` (scene.textures) to a two-phase device program; returns its index
+// Texture tables in the device layout (core/texture_eval.h), built on the host: uploaded by
+// BuildDevice, viewed in place by the host debug entry points, handed to the oracle by
+// pbrt_scene_get_flat.
+struct TexTables {
+    std::vector<DeviceTexNode> nodes;
+    std::vector<DeviceTexSpec> spec;
+    std::vector<DeviceImage> images;
+    std::vector<DeviceImageLevel> levels;
+    std::vector<uint8_t> data;
+    std::vector<float> luts;
+    std::vector<DeviceTexInstr> instrs;
+    std::vector<DeviceTexProgram> progs;
+    std::vector<int32_t> matTex;      // [nMaterials][4] program indices + remap
+    std::vector<int32_t> matTexNode;  // [nMaterials][4] the programs' root nodes + remap (oracle)
+    std::vector<int32_t> matMixNode;  // [nMaterials][4] mix: material 0, 1, amount root node, 0
+    std::vector<int32_t> matBumpNode; // [nMaterials][2] displacement root node, normal map image
+    std::vector<int32_t> nodeInfo, imageInfo, levelInfo, rawInfo;
+    std::vector<float> nodeParams, specFlat, rawGamma;
+    std::vector<uint8_t> rawData;
+    std::vector<uint64_t> rawOffset;
+    std::vector<float> basis;  // multispectral basis tables (never empty: one pad entry)
+};
+void BuildTexTables(const SceneDesc &s, TexTables *t);
+// a TexView over host copies (the device view points at DevBufs)
+TexView HostTexView(const TexTables &t);
+// FloatTexture::Evaluate of compiled program prog on the host
+float HostTexFloat(const TexView &T, int prog, const TexEvalCtx &c);
 int CompileTexProgram(SceneDesc &s, int node, bool spectrum);
 // CameraBase::FindMinimumDifferentials and CameraFromRender (SceneDesc::minPosDx ...)
 void ComputeCameraDifferentials(SceneDesc &s);

@@ -769,6 +769,17 @@ constexpr int kTravShapes = 4;
 constexpr int TraversalWaves(int tm) {
     return (tm & 3) == kTravQuant ? PBRT_QUANT_TRAVERSAL_WAVES : PBRT_TRAVERSAL_WAVES;
 }
+// k_shadow with every node and triangle in LDS (and no shapes) fits 5 waves per SIMD without
+// spills (93 VGPRs) and gains from them; k_closest spills there and stays at 4
+// (profiles/r06_c2_traversal_waves_ab.txt: C2 k_shadow 416 -> 370 us, k_closest 726 -> 736 us)
+#ifndef PBRT_SHADOW_LDS_WAVES
+#define PBRT_SHADOW_LDS_WAVES 5
+#endif
+constexpr int ShadowWaves(int tm) { return tm == kTravLds ? PBRT_SHADOW_LDS_WAVES : TraversalWaves(tm); }
+#ifndef PBRT_CLOSEST_LDS_WAVES
+#define PBRT_CLOSEST_LDS_WAVES 4
+#endif
+constexpr int ClosestWaves(int tm) { return tm == kTravLds ? PBRT_CLOSEST_LDS_WAVES : TraversalWaves(tm); }
 inline int TraversalMode(const DeviceScene &S) {
     return (S.compressed ? kTravQuant : (S.ldsTris > 0 ? kTravLds : kTravWide)) |
            (S.nShapes > 0 || S.nAlpha > 0 ? kTravShapes : 0);

@@ -68,7 +68,7 @@ constexpr int kClosestMix = 4;
 // sorted: this depth's rays were binned (k_raybin_*): lane j traces st.raySort[j] and only
 // writes its hit record; k_classify then enqueues the hits in record order.
 template <int NMatQ_, int TM>
-__global__ void __launch_bounds__(kBlock, TraversalWaves(TM))
+__global__ void __launch_bounds__(kBlock, ClosestWaves(TM))
     k_closest(DeviceScene S, PathState st, int depth, int timed, int sorted) {
     constexpr bool kMix = NMatQ_ == kClosestMix;
     constexpr int NMatQ = kMix ? kNumMatTypes : NMatQ_;
@@ -1390,7 +1390,7 @@ __global__ void __launch_bounds__(kBlock) k_texture(DeviceScene S, PathState st,
 }
 
 template <int TM>
-__global__ void __launch_bounds__(kBlock, TraversalWaves(TM)) k_shadow(DeviceScene S, PathState st, int depth) {
+__global__ void __launch_bounds__(kBlock, ShadowWaves(TM)) k_shadow(DeviceScene S, PathState st, int depth) {
     const QueueView shadows = LoadQueue(st, depth, kCntShadow);
     ChunkWalk walk = XcdChunks(shadows.total, S.xcdGroups);
     if (walk.n >= walk.end) return;  // no work

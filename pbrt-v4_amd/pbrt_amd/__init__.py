@@ -154,7 +154,7 @@ EXPORTED_SYMBOLS = [
     "pbrt_debug_shape_eval",
     "pbrt_debug_set_queue_check", "pbrt_debug_queue_holes",
     "pbrt_debug_equal_area", "pbrt_debug_cloud_density",
-    "pbrt_debug_pl2d", "pbrt_debug_windowed2d",
+    "pbrt_debug_pl2d", "pbrt_debug_windowed2d", "pbrt_debug_displace",
     "pbrt_color_space_index", "pbrt_debug_color_space", "pbrt_debug_rgb_spectrum", "pbrt_debug_rgb2spec_column_cs",
 ]
 
@@ -232,6 +232,8 @@ def _lib():
                                                c.c_void_p, c.c_void_p, c.c_int, c.c_void_p]
     lib.pbrt_debug_portal_eval.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_void_p, c.c_void_p]
     lib.pbrt_debug_measured.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_void_p, c.c_void_p]
+    lib.pbrt_debug_displace.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_void_p, c.c_int,
+                                        c.c_void_p, c.c_float, c.c_int, c.c_int, c.c_int] + [c.c_void_p] * 5
     lib.pbrt_debug_pl2d.argtypes = [c.c_int, c.c_int, c.c_void_p, c.c_int, c.c_int] + [c.c_void_p] * 4 + [
         c.c_int, c.c_void_p]
     lib.pbrt_debug_windowed2d.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_void_p]
@@ -368,6 +370,27 @@ def debug_pl2d(dim, cdf, data, xs, ys, pr, pv0, pv1, queries):
     _check(_lib().pbrt_debug_pl2d(int(dim), int(cdf), d.ctypes.data, int(xs), int(ys), p.ctypes.data, a0.ctypes.data,
                                   a1.ctypes.data, q.ctypes.data, len(q), o.ctypes.data))
     return o
+
+
+def debug_displace(P, uv, N, tri, quad, render_from_object, edge_length, mode):
+    """The plymesh displacement (pbrt_debug_displace) with a closed-form displacement (mode 0:
+    0.1 u - 0.05 v, mode 1: 0.25 p.y u + 0.125, mode 2: 0.1): returns (P, N, uv, tri) of the refined mesh."""
+    p = np.ascontiguousarray(P, np.float32).reshape(-1, 3)
+    t = np.ascontiguousarray(uv, np.float32).reshape(-1, 2)
+    n = None if N is None or len(N) == 0 else np.ascontiguousarray(N, np.float32).reshape(-1, 3)
+    tr = np.ascontiguousarray(tri, np.int32).reshape(-1)
+    qd = np.ascontiguousarray(quad, np.int32).reshape(-1)
+    m = np.ascontiguousarray(render_from_object, np.float32).reshape(16)
+    cap_v, cap_t = 1 << 16, 1 << 17
+    po, no = np.zeros((cap_v, 3), np.float32), np.zeros((cap_v, 3), np.float32)
+    uo, to = np.zeros((cap_v, 2), np.float32), np.zeros((cap_t, 3), np.int32)
+    cnt = np.zeros(2, np.int32)
+    _check(_lib().pbrt_debug_displace(p.ctypes.data, t.ctypes.data, None if n is None else n.ctypes.data, len(p),
+                                      tr.ctypes.data, len(tr) // 3, qd.ctypes.data, len(qd) // 4, m.ctypes.data,
+                                      float(edge_length), int(mode), cap_v, cap_t, po.ctypes.data, no.ctypes.data,
+                                      uo.ctypes.data, to.ctypes.data, cnt.ctypes.data))
+    nv, nt = int(cnt[0]), int(cnt[1])
+    return po[:nv], no[:nv], uo[:nv], to[:nt]
 
 
 COLOR_SPACES = ("srgb", "dci-p3", "rec2020", "aces2065-1")

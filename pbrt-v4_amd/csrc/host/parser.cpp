@@ -1410,8 +1410,6 @@ class Parser {
             if (Param *dp = ps.Find("displacement")) {
                 if (dp->type != "texture")
                     throw Error(ps.loc + ": \"" + dp->type + " displacement\": plymesh displacement must be a float texture");
-                if (!activeInstance.empty())
-                    throw Error(ps.loc + ": plymesh displacement inside ObjectBegin is not supported yet");
                 s.hasDisp = true;
                 s.disp = *dp;
             }
@@ -3302,12 +3300,17 @@ int Parser::AlphaId(const PendingShape &s) {
 // with the texture evaluated on the host by the product's texture code at each vertex's
 // object-space position and uv, with no differentials (TextureEvalContext{p, uv})
 void Parser::DisplacePlyMeshes() {
+    // shapes of ObjectBegin definitions too, once, in their definition's render space (the
+    // instances then copy the displaced mesh, as pbrt's instanced primitives share it)
     std::vector<std::pair<PendingShape *, int>> todo;
-    for (PendingShape &s : shapes)
-        if (s.hasDisp) {
-            const int node = FloatParamNode(&s.disp, 0.f, s.loc);
-            todo.push_back({&s, CompileTexProgram(scene, node, false)});
-        }
+    auto add = [&](PendingShape &s) {
+        if (!s.hasDisp) return;
+        const int node = FloatParamNode(&s.disp, 0.f, s.loc);
+        todo.push_back({&s, CompileTexProgram(scene, node, false)});
+    };
+    for (PendingShape &s : shapes) add(s);
+    for (auto &def : instanceDefs)
+        for (PendingShape &s : def.second) add(s);
     if (todo.empty()) return;
     TexTables tt;
     BuildTexTables(scene, &tt);

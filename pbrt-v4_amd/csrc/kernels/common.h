@@ -769,15 +769,17 @@ constexpr int kTravShapes = 4;
 constexpr int TraversalWaves(int tm) {
     return (tm & 3) == kTravQuant ? PBRT_QUANT_TRAVERSAL_WAVES : PBRT_TRAVERSAL_WAVES;
 }
-// k_shadow with every node and triangle in LDS (and no shapes) fits 5 waves per SIMD without
-// spills (93 VGPRs) and gains from them; k_closest spills there and stays at 4
-// (profiles/r06_c2_traversal_waves_ab.txt: C2 k_shadow 416 -> 370 us, k_closest 726 -> 736 us)
+// With every node and triangle in LDS (and no shapes) the traversal kernels run 5 waves per
+// SIMD: k_shadow fits them without spills (93 VGPRs), k_closest with a few spilled VGPRs but
+// its full queue staging (kCap 256: LDS is no constraint at 5 blocks there); with the staging cut
+// to 64 entries it lost (profiles/r06_c2_traversal_waves_ab.txt: C2 k_shadow 416 -> 371 us,
+// k_closest 727 -> 707 us)
 #ifndef PBRT_SHADOW_LDS_WAVES
 #define PBRT_SHADOW_LDS_WAVES 5
 #endif
 constexpr int ShadowWaves(int tm) { return tm == kTravLds ? PBRT_SHADOW_LDS_WAVES : TraversalWaves(tm); }
 #ifndef PBRT_CLOSEST_LDS_WAVES
-#define PBRT_CLOSEST_LDS_WAVES 4
+#define PBRT_CLOSEST_LDS_WAVES 5
 #endif
 constexpr int ClosestWaves(int tm) { return tm == kTravLds ? PBRT_CLOSEST_LDS_WAVES : TraversalWaves(tm); }
 inline int TraversalMode(const DeviceScene &S) {

@@ -89,6 +89,7 @@ __global__ void __launch_bounds__(kBlock, ClosestWaves(TM))
     constexpr int kQ = 2 + NMatQ;
     // entries per wave and queue: small enough that the staging (12 / 10 KB per block) leaves
     // room for the group stack and the node cache at TraversalWaves(TM) blocks per CU
+    // (keyed on the wide / quantised modes' waves: the all-LDS mode keeps the full staging)
     constexpr int kCap = TraversalWaves(TM) > 4 ? 64 : (NMatQ == 1 ? 256 : 128);
     __shared__ int qBuf[(kBlock / 64) * kQ * kCap];
     int *qCnt[kQ] = {escCounter, emitCounter};

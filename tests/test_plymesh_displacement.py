@@ -107,3 +107,17 @@ def test_displaced_plymesh_matches_oracle_gpu(pa, oracle, tmp_path):
     a, _ = gpu_rgb(pa, oracle, sc)
     frac, mr = check(a, oracle_rgb(oracle, sc))
     print(f"displaced plymesh parity: {frac * 100:.3f}% pixels, mean rel {mr:.2e}")
+
+
+def test_instanced_displaced_plymesh(pa, tmp_path):
+    """A displaced plymesh inside ObjectBegin is refined once and each instance copies it."""
+    write_ply(tmp_path / "m.ply", GRID_P, GRID_F, UV=GRID_UV)
+    one = flat(scene(pa, tmp_path, 'Shape "plymesh" "string filename" "m.ply" "texture displacement" "d" '
+                                    '"float edgelength" 0.3'))
+    inst = ('ObjectBegin "g"\nShape "plymesh" "string filename" "m.ply" "texture displacement" "d" "float edgelength" 0.3\n'
+            'ObjectEnd\nObjectInstance "g"\nAttributeBegin\nTranslate 3 0 0\nObjectInstance "g"\nAttributeEnd\n')
+    v, t, n = flat(scene(pa, tmp_path, inst))
+    nt, nv = len(one[1]), len(one[0])
+    assert len(t) == 2 * nt and len(v) == 2 * nv
+    np.testing.assert_array_equal(v[:nv], one[0])
+    np.testing.assert_allclose(v[nv:] - v[:nv], np.tile([3, 0, 0], (nv, 1)), atol=1e-5)

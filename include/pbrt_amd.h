@@ -274,6 +274,11 @@ typedef struct pbrt_scene_flat {
      * reference's GPU basis array (textures.cpp:1148-1176): channels, basis length, int(offset),
      * then each channel's basis values */
     const float *tex_basis;
+    /* textured hair floats (GetFloatTexture, materials.cpp:135-184): per material the tex_node
+     * roots of eta, beta_m, beta_n, alpha, eumelanin, pheomelanin, or -1 for the material_layer
+     * constant; the concentrations are textured as a pair (sigma_a = SigmaAFromConcentration
+     * per hit); NULL when no hair material is textured */
+    const int32_t *material_hair_tex;
 } pbrt_scene_flat;
 
 typedef struct pbrt_render_params {

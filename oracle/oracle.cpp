@@ -6063,9 +6063,29 @@ struct Renderer {
             // HairMaterial::GetBxDF (materials.h:380-404) of constant parameters; material_layer
             // holds {mode, sigma_a | color: kind value c0 c1 c2 scale pl, eta, beta_m, beta_n, alpha}
             const float *ml = f->material_layer + 12 * mat;
-            Float bm = std::max<Float>(1e-2, std::min<Float>(1.0, ml[9]));
-            Float bn = std::max<Float>(1e-2, std::min<Float>(1.0, ml[10]));
-            Float a = ml[11], e = ml[8];
+            // textured eta / beta_m / beta_n / alpha, and eumelanin / pheomelanin as a pair
+            // (SigmaAFromConcentration, bxdfs.cpp:553-562: RGBUnboundedSpectrum of the RGB sum)
+            Float e = ml[8], bmIn = ml[9], bnIn = ml[10], a = ml[11];
+            const int32_t *hn = f->material_hair_tex ? f->material_hair_tex + 6 * mat : nullptr;
+            bool conc = false;
+            Float cScale = 0, cCo[3] = {0, 0, 0};
+            if (hn && (hn[0] >= 0 || hn[1] >= 0 || hn[2] >= 0 || hn[3] >= 0 || hn[4] >= 0)) {
+                const OTexCtx hc = tex.Ctx(si);
+                if (hn[0] >= 0) e = tex.EvalF(hn[0], hc);
+                if (hn[1] >= 0) bmIn = tex.EvalF(hn[1], hc);
+                if (hn[2] >= 0) bnIn = tex.EvalF(hn[2], hc);
+                if (hn[3] >= 0) a = tex.EvalF(hn[3], hc);
+                if (hn[4] >= 0) {
+                    const Float ce = std::max<Float>(0, tex.EvalF(hn[4], hc)), cp = std::max<Float>(0, tex.EvalF(hn[5], hc));
+                    const Float r = ce * 0.419f + cp * 0.187f, g = ce * 0.697f + cp * 0.4f, b = ce * 1.37f + cp * 1.05f;
+                    cScale = 2 * std::max({r, g, b});
+                    if (cScale != 0) ORGBCoeffs(r / cScale, g / cScale, b / cScale, cCo);
+                    else ORGBCoeffs(0, 0, 0, cCo);
+                    conc = true;
+                }
+            }
+            Float bm = std::max<Float>(1e-2, std::min<Float>(1.0, bmIn));
+            Float bn = std::max<Float>(1e-2, std::min<Float>(1.0, bnIn));
             Spectrum sig;
             // a textured sigma_a / reflectance (texEval at the hit)
             const int ht = f->material_tex ? f->material_tex[4 * mat] : -1;
@@ -6075,7 +6095,8 @@ struct Renderer {
                 const Float l = lambda.lambda[i];
                 const int kind = (int)ml[1];
                 Float q;
-                if (ht >= 0) q = hq[i];
+                if (conc) q = cScale * Sigmoid(cCo[0], cCo[1], cCo[2], l);
+                else if (ht >= 0) q = hq[i];
                 else if (kind == 0) q = ml[2];
                 else if (kind == 1) q = ml[6] * Sigmoid(ml[3], ml[4], ml[5], l);
                 else {

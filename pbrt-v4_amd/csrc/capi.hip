@@ -436,7 +436,7 @@ struct pbrt_context {
     DevBuf<float4> raySort;
     DevBuf<int> rayBins;
     bool texGeneral = false;      // some textured reflectance is not a single image leaf
-    DevBuf<int> matBump;
+    DevBuf<int> matBump, matHairTex;
     DevBuf<float> texBump;        // [2][6][NR] (bump / normal-mapped materials only)
     int texTypeMask = 0;          // bit t: some material of type t is textured
     int texFullMask = 0;          // bit t: ... with an expression beyond one non-EWA image leaf
@@ -1116,7 +1116,8 @@ static void BuildDevice(pbrt_context *c) {
             std::vector<bool> alphaOnly(s.texPrograms.size(), false);
             for (const auto &a : s.alphaTex) alphaOnly[a[1]] = true;
             for (const MaterialDesc &m : s.materials)
-                for (int p : {m.texReflectance, m.texURough, m.texVRough, m.texAmount, m.texDisp})
+                for (int p : {m.texReflectance, m.texURough, m.texVRough, m.texAmount, m.texDisp, m.texHair[0], m.texHair[1],
+                              m.texHair[2], m.texHair[3], m.texHair[4], m.texHair[5]})
                     if (p >= 0) alphaOnly[p] = false;
             S.textured = std::any_of(alphaOnly.begin(), alphaOnly.end(), [](bool a) { return !a; }) ? 1 : 0;
         }
@@ -1130,6 +1131,14 @@ static void BuildDevice(pbrt_context *c) {
         }
         if (S.hasBump) S.textured = 1;
         c->matBump.Upload(mb);
+        S.matHairTex = nullptr;
+        if (tt.anyHairTex) {
+            std::vector<int> mh;
+            for (const MaterialDesc &m : s.materials)
+                mh.insert(mh.end(), {m.texHair[0], m.texHair[1], m.texHair[2], m.texHair[3], m.texHair[4], m.texHair[5], -1, -1});
+            c->matHairTex.Upload(mh);
+            S.matHairTex = (const int4 *)c->matHairTex.p;
+        }
         S.matBump = S.hasBump ? (const int4 *)c->matBump.p : nullptr;
         S.tex = TexView{};
         if (!s.texPrograms.empty() || S.hasBump) {
@@ -1179,6 +1188,7 @@ static void BuildDevice(pbrt_context *c) {
             };
             for (const MaterialDesc &m : s.materials) {
                 if (m.texReflectance >= 0 && !tt.progs[m.texReflectance].simple) c->texGeneral = true;
+                if (m.texHair[4] >= 0) c->texGeneral = true;  // sigma_a from textured concentrations, per wavelength
                 if (m.texReflectance >= 0 || m.texURough >= 0 || m.texDisp >= 0 || m.normalMap >= 0)
                     c->texTypeMask |= 1 << m.type;
                 if (m.texDisp >= 0 && !leanProg(m.texDisp, false)) c->texFullMask |= 1 << m.type;
@@ -1441,7 +1451,7 @@ constexpr int kVolFloats = 330, kVolInts = 17;
 static int64_t PathStateBytesPerPath(bool volumetric, bool dispersive, bool textured = false, bool texGeneral = false,
                                      bool mix = false, bool bump = false) {
     return 4 * (kPathFloats + kPathInts) + (volumetric ? 4 * (kVolFloats + kVolInts) : 0) + (dispersive ? 16 : 0) +
-           (textured ? 24 : 0) + (texGeneral ? 124 : 0) + (mix ? 8 : 0) + (bump ? 48 : 0);
+           (textured ? 32 : 0) + (texGeneral ? 124 : 0) + (mix ? 8 : 0) + (bump ? 48 : 0);
 }
 
 static void AllocPaths(pbrt_context *c, int64_t N) {
@@ -1464,7 +1474,7 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
         c->dispTerm.Alloc((size_t)NR);
     }
     if (c->S.textured) {
-        c->texCoef.Alloc((size_t)6 * NR);
+        c->texCoef.Alloc((size_t)8 * NR);
         if (c->S.hasBump) c->texBump.Alloc((size_t)12 * NR);
         if (c->texGeneral) c->texR.Alloc((size_t)kNSpectrumSamples * NR);
     }
@@ -1979,6 +1989,7 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
         f->material_tex = t.matTexNode.data();
         f->material_mix = t.matMixNode.data();
         f->material_bump = t.matBumpNode.data();
+        f->material_hair_tex = t.anyHairTex ? t.matHairNode.data() : nullptr;
         for (int k = 0; k < 12; ++k) f->camera_from_render[k] = s.cameraFromRender[k];
         for (int k = 0; k < 3; ++k) {
             f->camera_min_diff[k] = s.minPosDx[k];

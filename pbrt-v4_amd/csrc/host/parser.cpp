@@ -428,6 +428,8 @@ class Parser {
         bool hasDisp = false;   // "displacement" (a float texture or constant)
         Param disp;
         std::string normalMap;  // "normalmap" image file
+        bool hasHair = false;   // hair: textured eta, beta_m, beta_n, alpha, eumelanin, pheomelanin
+        Param hair[6];          // type "" = not textured
     };
     std::vector<MatTexPending> matTexPending;
     void ResolveTextures();
@@ -945,7 +947,7 @@ class Parser {
             auto warn = [&](const char *what) { std::fprintf(stderr, "%s: Warning: %s\n", ps.loc.c_str(), what); };
             auto constFloat = [&](Param *p) {
                 if (p->type != "float" || p->nums.empty())
-                    throw Error(ps.loc + ": \"" + p->type + " " + p->name + "\" for the hair material is not supported yet (constant floats only)");
+                    throw Error(ps.loc + ": \"" + p->type + " " + p->name + "\" is not a float parameter of the hair material");
                 return (float)p->nums[0];
             };
             // a textured sigma_a (Unbounded) or reflectance (Albedo) is evaluated per hit by the
@@ -969,6 +971,14 @@ class Parser {
                 m.hairMode = 1;
                 if (refl->type == "texture") textured(refl, kSpecAlbedo);
                 else m.hairSpec = ConstSpectrum(refl, true, ps.loc, "hair");
+            } else if ((eu && eu->type == "texture") || (ph && ph->type == "texture")) {
+                // textured concentrations: sigma_a = SigmaAFromConcentration(ce, cp) per hit
+                // (materials.h:396-399), a missing concentration is 0
+                MatTexPending &mp = PendingTex(ps.loc);
+                mp.hasHair = true;
+                if (eu) mp.hair[4] = *eu;
+                if (ph) mp.hair[5] = *ph;
+                m.hairMode = 0;
             } else {
                 // the concentrations' RGB sigma_a (ce, cp clamped at 0 by GetBxDF)
                 const float ce = eu ? std::max(0.f, constFloat(eu)) : (ph ? 0.f : 1.3f);
@@ -977,10 +987,22 @@ class Parser {
                 m.hairSpec = UnboundedRGB(ce * 0.419f + cp * 0.187f, ce * 0.697f + cp * 0.4f, ce * 1.37f + cp * 1.05f);
             }
             m.eta = 1.55f;
-            if (Param *e = ps.Find("eta")) m.eta = constFloat(e);
-            if (Param *b = ps.Find("beta_m")) m.hairBetaM = constFloat(b);
-            if (Param *b = ps.Find("beta_n")) m.hairBetaN = constFloat(b);
-            if (Param *a = ps.Find("alpha")) m.hairAlpha = constFloat(a);
+            // eta, beta_m, beta_n, alpha: constants, or float textures evaluated per hit
+            auto hairFloat = [&](const char *name, int k, float *dst) {
+                Param *q = ps.Find(name);
+                if (!q) return;
+                if (q->type == "texture") {
+                    MatTexPending &mp = PendingTex(ps.loc);
+                    mp.hasHair = true;
+                    mp.hair[k] = *q;
+                } else {
+                    *dst = constFloat(q);
+                }
+            };
+            hairFloat("eta", 0, &m.eta);
+            hairFloat("beta_m", 1, &m.hairBetaM);
+            hairFloat("beta_n", 2, &m.hairBetaN);
+            hairFloat("alpha", 3, &m.hairAlpha);
         } else if (type == "measured") {
             // MeasuredMaterial::Create (materials.cpp:644-667): the resolved "filename", each
             // file read once (MeasuredBxDF::BRDFDataFromFile's cache, bxdfs.cpp:995-1001)
@@ -3315,6 +3337,9 @@ void Parser::DisplacePlyMeshes() {
     TexTables tt;
     BuildTexTables(scene, &tt);
     const TexView T = HostTexView(tt);
+    // the programs serve the load only: dropped afterwards (they were compiled last), so the
+    // device does not take the scene for a textured one
+    const size_t firstDispProg = (size_t)todo.front().second;
     const Mat4 &renderFromWorld = scene.camera.renderFromWorld;
     for (auto &[sp, prog] : todo) {
         PendingShape &s = *sp;
@@ -3348,6 +3373,7 @@ void Parser::DisplacePlyMeshes() {
         s.quadIdx.clear();
         s.hasDisp = false;
     }
+    scene.texPrograms.resize(firstDispProg);
 }
 
 void Parser::ResolveTextures() {
@@ -3389,6 +3415,14 @@ void Parser::ResolveTextures() {
         if (mp.hasRefl) {
             const int node = SpectrumParamNode(&mp.refl, mp.reflSpec, 0.5f, mp.loc);
             m.texReflectance = CompileTexProgram(scene, node, true);
+        }
+        if (mp.hasHair) {
+            const bool conc = !mp.hair[4].type.empty() || !mp.hair[5].type.empty();
+            for (int k = 0; k < 6; ++k) {
+                if (mp.hair[k].type.empty() && !(conc && k >= 4)) continue;
+                const int node = FloatParamNode(mp.hair[k].type.empty() ? nullptr : &mp.hair[k], 0.f, mp.loc);
+                m.texHair[k] = CompileTexProgram(scene, node, false);
+            }
         }
         if (mp.hasRough) {
             const int u = FloatParamNode(mp.ur.type.empty() ? nullptr : &mp.ur, 0.f, mp.loc);

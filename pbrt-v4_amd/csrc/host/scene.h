@@ -121,6 +121,10 @@ struct MaterialDesc {
     int hairMode = 0;
     SssSpectrumDesc hairSpec;
     float hairBetaM = .3f, hairBetaN = .3f, hairAlpha = 2.f;
+    // textured hair floats (GetFloatTexture, materials.cpp:135-184): programs for eta, beta_m,
+    // beta_n, alpha, eumelanin, pheomelanin (-1: the constant above); the concentrations are
+    // textured as a pair (a missing one is the constant 0), sigma_a then formed per hit
+    int texHair[6] = {-1, -1, -1, -1, -1, -1};
     int measured = -1;  // MeasuredMaterial: its SceneDesc::measured entry
     std::string name;
 };

@@ -1007,6 +1007,10 @@ void BuildTexTables(const SceneDesc &s, TexTables *t) {
                              {root(m.texReflectance), root(m.texURough), root(m.texVRough), m.remapRoughness ? 1 : 0});
         t->matMixNode.insert(t->matMixNode.end(), {m.mixMat[0], m.mixMat[1], root(m.texAmount), 0});
         t->matBumpNode.insert(t->matBumpNode.end(), {root(m.texDisp), m.normalMap});
+        for (int k = 0; k < 6; ++k) {
+            t->matHairNode.push_back(root(m.texHair[k]));
+            t->anyHairTex = t->anyHairTex || m.texHair[k] >= 0;
+        }
     }
 }
 // a TexView over host copies (debug entry points; the device view points at DevBufs)

@@ -64,6 +64,8 @@ struct TexTables {
     std::vector<int32_t> matTexNode;  // [nMaterials][4] the programs' root nodes + remap (oracle)
     std::vector<int32_t> matMixNode;  // [nMaterials][4] mix: material 0, 1, amount root node, 0
     std::vector<int32_t> matBumpNode; // [nMaterials][2] displacement root node, normal map image
+    std::vector<int32_t> matHairNode; // [nMaterials][6] hair eta beta_m beta_n alpha eumelanin pheomelanin root nodes
+    bool anyHairTex = false;
     std::vector<int32_t> nodeInfo, imageInfo, levelInfo, rawInfo;
     std::vector<float> nodeParams, specFlat, rawGamma;
     std::vector<uint8_t> rawData;

@@ -1683,20 +1683,26 @@ __device__ __attribute__((noinline)) int ResolveMixMaterial(const DeviceScene &S
 // The texture stage of EvaluateMaterialAndBSDF for one hit (k_texture on the surface path,
 // k_vtexture on the volumetric one): bump / normal mapping into st.texBump[depth & 1], the reflectance as
 // sigmoid coefficients (texCoef[0..2], texCoef[3] = 0) or 31 values (texR, texCoef[3] = 1),
-// the roughness alphas into texCoef[4..5]; record ri, its hit barycentrics hitB[k * NR + ri]
+// the roughness alphas into texCoef[4..5] (textured hair floats into texCoef[4..7]); record ri, its hit barycentrics hitB[k * NR + ri]
 // and lambda0[ri] (read only for textured materials).
 // Always inlined: compiled as a call (s_swappc) from k_texture it hung the textured Cornell box
 // on the GPU (round 4 and again in round 6: tests/test_textures.py timed out in the first
 // closest-hit-to-shade pass), with k_texture<*, false, false>'s private segment grown from 108 to
 // 2012 B per lane (the kernel's modified DeviceScene argument spilled to scratch for the callee's
 // reference) and 56 more VGPRs; inlined, the kernels keep the inline copy's code and resources.
-template <bool Full, bool Ext>
+// Hair: the textured hair floats are compiled in (k_vtexture's instantiation for scenes with
+// S.matHairTex; elsewhere the block would only cost registers)
+template <bool Full, bool Ext, bool Hair = false>
 __device__ __forceinline__ void HitTextures(const DeviceScene &S, const PathState &st, int depth, int ri, int prim,
                                             int mat, const float *hitB, const float *lambda0s) {
     const int N = st.NR;
     const int4 mt = S.matTex[mat];
     const int4 mb = S.hasBump ? S.matBump[mat] : make_int4(-1, -1, 0, 0);
-    if (mt.x < 0 && mt.y < 0 && !mb.z) return;
+    // textured hair floats (Full stages only): eta, beta_m, beta_n, alpha and the concentrations
+    const int4 h0 = Hair ? S.matHairTex[2 * mat] : make_int4(-1, -1, -1, -1);
+    const int h1 = Hair ? S.matHairTex[2 * mat + 1].x : -1;
+    const bool hairT = h0.x >= 0 || h0.y >= 0 || h0.z >= 0 || h0.w >= 0 || h1 >= 0;
+    if (mt.x < 0 && mt.y < 0 && !mb.z && !hairT) return;
     V3 p0, p1, p2;
     PrimVerts(S, prim, &p0, &p1, &p2);
     const TriSurface surf = SurfaceAt<Ext>(S, prim, p0, p1, p2, hitB[ri], hitB[N + ri], hitB[2 * N + ri]);
@@ -1760,6 +1766,29 @@ __device__ __forceinline__ void HitTextures(const DeviceScene &S, const PathStat
         const TrowbridgeReitz t = TrowbridgeReitz::Make(ur, vr);
         st.texCoef[4 * (size_t)N + ri] = t.ax;
         st.texCoef[5 * (size_t)N + ri] = t.ay;
+    }
+    if constexpr (Hair) {
+        if (hairT) {
+            // HairMaterial::GetBxDF's GetFloatTexture values (materials.h:380-404) into texCoef[4..7]
+            // (hair has no roughness slots); a textured eumelanin / pheomelanin pair becomes sigma_a
+            // = SigmaAFromConcentration(ce, cp) (bxdfs.cpp:553-562: the RGB sum as an
+            // RGBUnboundedSpectrum) per wavelength in texR, flagged by texCoef[3] = 1
+            const int hp[4] = {h0.x, h0.y, h0.z, h0.w};
+            for (int k = 0; k < 4; ++k)
+                if (hp[k] >= 0) st.texCoef[(4 + k) * (size_t)N + ri] = TexFloatFast<true>(S, hp[k], tc);
+            if (h1 >= 0) {
+                const int h1y = S.matHairTex[2 * mat + 1].y;
+                const float ce = fmaxf(0.f, TexFloatFast<true>(S, h1, tc)), cp = fmaxf(0.f, TexFloatFast<true>(S, h1y, tc));
+                const float r = ce * 0.419f + cp * 0.187f, g = ce * 0.697f + cp * 0.4f, b = ce * 1.37f + cp * 1.05f;
+                const float scale = 2 * fmaxf(r, fmaxf(g, b));
+                float c[3];
+                if (scale != 0) RGBToCoeffs(S.tex, r / scale, g / scale, b / scale, c);
+                else RGBToCoeffs(S.tex, 0.f, 0.f, 0.f, c);
+                for (SpectralIter it(lambda0s[ri]); it.i < kNSpectrumSamples; it.Next())
+                    st.texR[(size_t)it.i * N + ri] = scale * SigmoidPolynomial(c[0], c[1], c[2], it.lam);
+                st.texCoef[3 * (size_t)N + ri] = 1.f;
+            }
+        }
     }
 }
 }  // namespace pbrt_amd

@@ -272,6 +272,9 @@ struct DeviceScene {
     TexView tex;
     CameraDiff camDiff;
     const int4 *matTex;
+    // textured hair floats: per material 2 int4 of programs {eta, beta_m, beta_n, alpha},
+    // {eumelanin, pheomelanin, -, -} (-1: constant); nullptr when no hair is textured
+    const int4 *matHairTex;
     // MixMaterial: per material {material 0, material 1, amount program, 0}
     const int4 *matMix;
     // this struct's copy in device memory (static scene fields only): out-of-line functions
@@ -327,7 +330,7 @@ struct PathState {
     // textured materials (k_texture, before each shade launch), by record index: the hit's
     // reflectance as sigmoid coefficients c0 c1 c2 + a flag (1: the per-wavelength values are
     // in texR), then the TrowbridgeReitz alphas of a textured roughness; null when untextured
-    float *texCoef;     // [6][NR]
+    float *texCoef;     // [8][NR]
     float *texBump[2];  // by depth parity, [6][NR]: the bump / normal-mapped shading normal and
                         // dpdu of a record (null without such materials)
     float *texR;        // [31][NR] general reflectance expressions (null when none)

@@ -1307,7 +1307,7 @@ size_t VolTablesLdsBytes(const DeviceScene &S) {
 // The texture stage of the volumetric surface queue (EvaluateMaterialAndBSDF's texEval calls
 // and bump / normal mapping, surfscatter.cpp:74-137), as k_texture on the surface path: per
 // surface hit of this iteration the results k_vsurface<..., Tex> reads (HitTextures).
-template <bool Ext>
+template <bool Ext, bool Hair = false>
 __global__ void __launch_bounds__(kBlock) k_vtexture(DeviceScene S, PathState st, VolState v, int wf) {
     const QueueView surf = LoadQueue(st, wf, kVSurf);
     if ((int)(blockIdx.x * blockDim.x) >= surf.total) return;
@@ -1326,7 +1326,7 @@ __global__ void __launch_bounds__(kBlock) k_vtexture(DeviceScene S, PathState st
         if (prim < 0) continue;  // escaped
         const int mat = VolHitMaterial(S, st, ri, prim);
         if (S.matType[mat] == 3) continue;  // interfaces
-        HitTextures<true, Ext>(S, st, wf, ri, prim, mat, v.hitB, rec.lambda0);
+        HitTextures<true, Ext, Hair>(S, st, wf, ri, prim, mat, v.hitB, rec.lambda0);
     }
 }
 
@@ -2261,12 +2261,24 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
         float prMax = 0, ptMax = 0;
         // HairMaterial::GetBxDF (materials.h:380-404): beta_m / beta_n clamped to [0.01, 1],
         // h = -1 + 2 v; sigma_a per wavelength into sp.a (matLayer: HairLayer's packing)
-        const float hairBm = fmaxf(1e-2f, fminf(1.f, L2.y)), hairBn = fmaxf(1e-2f, fminf(1.f, L2.z));
+        // textured floats (eta, beta_m, beta_n, alpha): the texture stage's values in texCoef[4..7]
+        // (HitTextures); a textured concentration pair left sigma_a per wavelength in texR
+        float hairEta = L2.x, hairBmIn = L2.y, hairBnIn = L2.z, hairAlpha = L2.w;
+        bool hairConc = false;
+        if (hair && S.matHairTex) {
+            const int4 h0 = S.matHairTex[2 * mat];
+            if (h0.x >= 0) hairEta = st.texCoef[4 * (size_t)NR + ri];
+            if (h0.y >= 0) hairBmIn = st.texCoef[5 * (size_t)NR + ri];
+            if (h0.z >= 0) hairBnIn = st.texCoef[6 * (size_t)NR + ri];
+            if (h0.w >= 0) hairAlpha = st.texCoef[7 * (size_t)NR + ri];
+            hairConc = S.matHairTex[2 * mat + 1].x >= 0;
+        }
+        const float hairBm = fmaxf(1e-2f, fminf(1.f, hairBmIn)), hairBn = fmaxf(1e-2f, fminf(1.f, hairBnIn));
         const float hairDen = HairReflectanceDenom(hairBn);
         const float hq[7] = {L0.y, L0.z, L0.w, L1.x, L1.y, L1.z, L1.w};
         // a textured sigma_a / reflectance: k_vtexture's value for this record (sigmoid
         // coefficients, or one value per wavelength)
-        const bool hairTex = hair && S.textured && S.matTex[mat].x >= 0;
+        const bool hairTex = hair && S.textured && (S.matTex[mat].x >= 0 || hairConc);
         const bool hairTexR = hairTex && st.texCoef[3 * (size_t)NR + ri] != 0;
         const float4 hairTc = hairTex && !hairTexR ? make_float4(st.texCoef[ri], st.texCoef[(size_t)NR + ri],
                                                                  st.texCoef[2 * (size_t)NR + ri], 0.f)
@@ -2328,7 +2340,7 @@ __global__ void __launch_bounds__(kBlock) k_vlayered(DeviceScene S, PathState st
                                        Clampf(L0.y, -1, 1), albNz, (int)L0.z,  (int)L0.w, 0, sp, bottomNz};
         const DiffuseTransmission<LayerSpec> D{sp, prMax, ptMax};
         HairState H{};
-        if (hair) H = MakeHair(-1 + 2 * si.uv[1], L2.x, hairBm, hairBn, L2.w);
+        if (hair) H = MakeHair(-1 + 2 * si.uv[1], hairEta, hairBm, hairBn, hairAlpha);
         // MeasuredMaterial::GetBxDF (materials.h:931-934): the BRDF's tables (matLayer: its index)
         MeasuredView M{};
         if (meas) {
@@ -3015,7 +3027,8 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
     // Ext: analytic shapes or image lights in the scene (their paths compiled in)
     if (S.nShapes > 0 || S.nEnv > 0 || S.nImageDelta > 0 || S.hasSpread || S.nImageAreaLights > 0) {
         if (S.textured) {
-            hipLaunchKernelGGL(k_vtexture<true>, gW, block, 0, s, S, st, v, wf);
+            if (S.matHairTex) hipLaunchKernelGGL((k_vtexture<true, true>), gW, block, 0, s, S, st, v, wf);
+            else hipLaunchKernelGGL(k_vtexture<true>, gW, block, 0, s, S, st, v, wf);
             if (S.matTypeMask & other) hipLaunchKernelGGL((k_vsurface<false, true, true>), gW, block, surfLds, s, S, st, v, wf);
             else hipLaunchKernelGGL((k_vsurface<true, true, true>), gW, block, surfLds, s, S, st, v, wf);
         } else if (S.matTypeMask & other) {
@@ -3028,7 +3041,8 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
         VOL_REST(true);
     } else {
         if (S.textured) {
-            hipLaunchKernelGGL(k_vtexture<false>, gW, block, 0, s, S, st, v, wf);
+            if (S.matHairTex) hipLaunchKernelGGL((k_vtexture<false, true>), gW, block, 0, s, S, st, v, wf);
+            else hipLaunchKernelGGL(k_vtexture<false>, gW, block, 0, s, S, st, v, wf);
             if (S.matTypeMask & other) hipLaunchKernelGGL((k_vsurface<false, false, true>), gW, block, surfLds, s, S, st, v, wf);
             else hipLaunchKernelGGL((k_vsurface<true, false, true>), gW, block, surfLds, s, S, st, v, wf);
         } else if (S.matTypeMask & other) {

@@ -117,6 +117,7 @@ class SceneFlat(ctypes.Structure):
         ("measured_files", ctypes.POINTER(ctypes.c_char_p)),
         ("options", ctypes.c_int),
         ("tex_basis", ctypes.POINTER(ctypes.c_float)),
+        ("material_hair_tex", ctypes.POINTER(ctypes.c_int32)),
     ]
 
 

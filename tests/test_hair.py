@@ -220,8 +220,8 @@ def test_hair_loader_forms(pa):
 @pytest.mark.parametrize("material, msg", [
     ('Material "hair" "rgb reflectance" [1.2 0.5 0.5]', "albedo"),
     ('Material "hair" "rgb sigma_a" [-1 0.5 0.5]', "negative"),
-    ('Texture "t" "float" "constant"\nMaterial "hair" "texture beta_m" "t"', "not supported"),
-    ('Texture "t" "float" "constant"\nMaterial "hair" "texture eumelanin" "t"', "not supported"),
+    ('Material "hair" "rgb beta_m" [0.1 0.2 0.3]', "not a float parameter"),
+    ('Material "hair" "texture beta_m" "nope"', "nope"),
 ])
 def test_hair_loader_errors(pa, material, msg):
     with pytest.raises(pa.PbrtError, match=msg):
@@ -242,12 +242,26 @@ TEX_REFL = ('Texture "c" "spectrum" "checkerboard" "float uscale" 6 "float vscal
 TEX_SIGMA = ('Texture "s" "spectrum" "checkerboard" "float uscale" 6 "float vscale" 6 "rgb tex1" [0.2 0.4 1.0] '
              '"rgb tex2" [1.5 1.0 0.6]\nMaterial "hair" "texture sigma_a" "s"')
 
+# textured floats (GetFloatTexture, materials.cpp:135-184): beta_m / beta_n / alpha / eta per
+# hit, and the eumelanin / pheomelanin pair forming sigma_a per hit (SigmaAFromConcentration)
+TEX_FLOATS = ('Texture "bm" "float" "checkerboard" "float uscale" 6 "float vscale" 6 "float tex1" 0.15 "float tex2" 0.6\n'
+              'Texture "al" "float" "scale" "float tex" 3 "float scale" 0.5\n'
+              'Material "hair" "rgb sigma_a" [0.2 0.4 1.0] "texture beta_m" "bm" "texture beta_n" "bm" '
+              '"texture alpha" "al" "float eta" 1.5')
+TEX_MELANIN = ('Texture "eu" "float" "checkerboard" "float uscale" 6 "float vscale" 6 "float tex1" 0.3 "float tex2" 2.5\n'
+               'Material "hair" "texture eumelanin" "eu" "float pheomelanin" 0.4')
+TEX_ETA = ('Texture "e" "float" "checkerboard" "float uscale" 6 "float vscale" 6 "float tex1" 1.3 "float tex2" 1.9\n'
+           'Material "hair" "rgb reflectance" [0.8 0.55 0.3] "texture eta" "e"')
+
 FORMS = {
     "melanin": 'Material "hair" "float eumelanin" 0.8 "float pheomelanin" 0.3',
     "reflectance": 'Material "hair" "rgb reflectance" [0.8 0.55 0.3] "float beta_m" 0.25 "float beta_n" 0.4',
     "sigma_rough": 'Material "hair" "rgb sigma_a" [0.06 0.1 0.2] "float beta_m" 0.6 "float beta_n" 0.8 "float alpha" 0',
     "tex_reflectance": TEX_REFL,
     "tex_sigma_a": TEX_SIGMA,
+    "tex_floats": TEX_FLOATS,
+    "tex_melanin": TEX_MELANIN,
+    "tex_eta": TEX_ETA,
 }
 
 
@@ -277,3 +291,27 @@ def test_hair_matches_oracle_gpu(pa, oracle, form):
     a, _ = gpu_rgb(pa, oracle, sc)
     frac, mr = check(a, oracle_rgb(oracle, sc))
     print(f"hair ({form}): {frac*100:.2f}% pixels within 1e-3, mean rel {mr:.2e}")
+
+
+@pytest.mark.parametrize("material, const, slots", [
+    (TEX_FLOATS, 'Material "hair" "rgb sigma_a" [0.2 0.4 1.0] "float beta_m" 0.15 "float beta_n" 0.15 "float alpha" 1.5 '
+                 '"float eta" 1.5', (1, 2, 3)),
+    (TEX_MELANIN, 'Material "hair" "float eumelanin" 0.3 "float pheomelanin" 0.4', (4, 5)),
+    (TEX_ETA, 'Material "hair" "rgb reflectance" [0.8 0.55 0.3] "float eta" 1.3', (0,)),
+])
+def test_textured_hair_floats_oracle(pa, oracle, material, const, slots):
+    """Textured hair floats load into material_hair_tex (the other slots stay constants), render
+    finite, and differ from the constant form that equals one of the checks."""
+    kw = dict(xresolution=24, yresolution=18, spp=8)
+    sc, sc0 = pa.Scene.from_string(scene(material), SCENES, **kw), pa.Scene.from_string(scene(const), SCENES, **kw)
+    f = sc.flat()
+    mt = np.ctypeslib.as_array(f.material_type, shape=(f.n_materials,))
+    hair = int(np.flatnonzero(mt == 9)[0])
+    ht = np.ctypeslib.as_array(f.material_hair_tex, shape=(f.n_materials * 6,)).reshape(-1, 6)[hair]
+    assert [k for k in range(6) if ht[k] >= 0] == list(slots)
+    assert not sc0.flat().material_hair_tex
+    m = [f.output_rgb_from_sensor_rgb[i] for i in range(9)]
+    a = oracle.film_to_rgb(oracle.render(sc, threads=8), m)
+    b = oracle.film_to_rgb(oracle.render(sc0, threads=8), m)
+    assert np.isfinite(a).all() and a.mean() > 0.005
+    assert np.abs(a - b).mean() > 1e-4

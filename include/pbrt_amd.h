@@ -279,6 +279,10 @@ typedef struct pbrt_scene_flat {
      * constant; the concentrations are textured as a pair (sigma_a = SigmaAFromConcentration
      * per hit); NULL when no hair material is textured */
     const int32_t *material_hair_tex;
+    /* textured subsurface spectra (SubsurfaceMaterial::GetBSSRDF, materials.h:823-841): per
+     * material the tex_node roots of sigma_a and of sigma_s (sss mode 0) or mfp (mode 1),
+     * Unbounded, or -1 for the sss_params constant; NULL when none is textured */
+    const int32_t *material_sss_tex;
 } pbrt_scene_flat;
 
 typedef struct pbrt_render_params {

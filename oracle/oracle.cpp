@@ -6618,14 +6618,20 @@ struct Renderer {
                 const int rt = f->material_tex ? f->material_tex[4 * mat] : -1;
                 Spectrum rTex{};
                 if (rt >= 0 && P[0] != 0) rTex = tex.EvalS(rt, tex.Ctx(si), lambda);
+                // textured sigma_a, and sigma_s | mfp (Unbounded), the same way
+                const int sat = f->material_sss_tex ? f->material_sss_tex[2 * mat] : -1;
+                const int sbt = f->material_sss_tex ? f->material_sss_tex[2 * mat + 1] : -1;
+                Spectrum aTex{}, bTex{};
+                if (sat >= 0) aTex = tex.EvalS(sat, tex.Ctx(si), lambda);
+                if (sbt >= 0) bTex = tex.EvalS(sbt, tex.Ctx(si), lambda);
                 for (int i = 0; i < NS; ++i) {
                     const Float lam = lambda.lambda[i];
                     Float sa, ss;
                     if (P[0] == 0) {
-                        sa = std::max<Float>(0, P[1] * specAt(P + 4, lam));
-                        ss = std::max<Float>(0, P[1] * specAt(P + 11, lam));
+                        sa = std::max<Float>(0, P[1] * (sat >= 0 ? aTex[i] : specAt(P + 4, lam)));
+                        ss = std::max<Float>(0, P[1] * (sbt >= 0 ? bTex[i] : specAt(P + 11, lam)));
                     } else {
-                        const Float mfree = std::max<Float>(0, P[1] * specAt(P + 11, lam));
+                        const Float mfree = std::max<Float>(0, P[1] * (sbt >= 0 ? bTex[i] : specAt(P + 11, lam)));
                         const Float refl = rt >= 0 ? rTex[i] : specAt(P + 4, lam);
                         const Float rh = osss::InvertCatmullRom(bd.rho, bd.rhoEff, osss::NRho, Clamp(refl, 0, 1));
                         ss = rh / mfree;

@@ -416,7 +416,7 @@ struct pbrt_context {
     DevBuf<DeviceTexInstr> texInstrs;
     DevBuf<DeviceTexProgram> texProgs;
     DevBuf<int> matTex;
-    DevBuf<float> texCoef, texR;  // k_texture results (PathState::texCoef / texR)
+    DevBuf<float> texCoef, texR, texS;  // k_texture results (PathState::texCoef / texR / texS)
     DevBuf<int> infImage;
     DevBuf<DeviceShape> shapes;
     DevBuf<ShapeBVHNode> shapeNodes;
@@ -436,7 +436,7 @@ struct pbrt_context {
     DevBuf<float4> raySort;
     DevBuf<int> rayBins;
     bool texGeneral = false;      // some textured reflectance is not a single image leaf
-    DevBuf<int> matBump, matHairTex;
+    DevBuf<int> matBump, matHairTex, matSssTex;
     DevBuf<float> texBump;        // [2][6][NR] (bump / normal-mapped materials only)
     int texTypeMask = 0;          // bit t: some material of type t is textured
     int texFullMask = 0;          // bit t: ... with an expression beyond one non-EWA image leaf
@@ -1117,7 +1117,7 @@ static void BuildDevice(pbrt_context *c) {
             for (const auto &a : s.alphaTex) alphaOnly[a[1]] = true;
             for (const MaterialDesc &m : s.materials)
                 for (int p : {m.texReflectance, m.texURough, m.texVRough, m.texAmount, m.texDisp, m.texHair[0], m.texHair[1],
-                              m.texHair[2], m.texHair[3], m.texHair[4], m.texHair[5]})
+                              m.texHair[2], m.texHair[3], m.texHair[4], m.texHair[5], m.texSss[0], m.texSss[1]})
                     if (p >= 0) alphaOnly[p] = false;
             S.textured = std::any_of(alphaOnly.begin(), alphaOnly.end(), [](bool a) { return !a; }) ? 1 : 0;
         }
@@ -1138,6 +1138,13 @@ static void BuildDevice(pbrt_context *c) {
                 mh.insert(mh.end(), {m.texHair[0], m.texHair[1], m.texHair[2], m.texHair[3], m.texHair[4], m.texHair[5], -1, -1});
             c->matHairTex.Upload(mh);
             S.matHairTex = (const int4 *)c->matHairTex.p;
+        }
+        S.matSssTex = nullptr;
+        if (tt.anySssTex) {
+            std::vector<int> ms;
+            for (const MaterialDesc &m : s.materials) ms.insert(ms.end(), {m.texSss[0], m.texSss[1]});
+            c->matSssTex.Upload(ms);
+            S.matSssTex = (const int2 *)c->matSssTex.p;
         }
         S.matBump = S.hasBump ? (const int4 *)c->matBump.p : nullptr;
         S.tex = TexView{};
@@ -1449,9 +1456,9 @@ constexpr int kPathFloats = 101, kPathInts = 16;
 // depth, medium) = 8, hitPrim, 5 queues, shadow pixel + medium + flags = 17 ints
 constexpr int kVolFloats = 330, kVolInts = 17;
 static int64_t PathStateBytesPerPath(bool volumetric, bool dispersive, bool textured = false, bool texGeneral = false,
-                                     bool mix = false, bool bump = false) {
+                                     bool mix = false, bool bump = false, bool sssTex = false) {
     return 4 * (kPathFloats + kPathInts) + (volumetric ? 4 * (kVolFloats + kVolInts) : 0) + (dispersive ? 16 : 0) +
-           (textured ? 32 : 0) + (texGeneral ? 124 : 0) + (mix ? 8 : 0) + (bump ? 48 : 0);
+           (textured ? 32 : 0) + (texGeneral ? 124 : 0) + (mix ? 8 : 0) + (bump ? 48 : 0) + (sssTex ? 248 : 0);
 }
 
 static void AllocPaths(pbrt_context *c, int64_t N) {
@@ -1477,6 +1484,7 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
         c->texCoef.Alloc((size_t)8 * NR);
         if (c->S.hasBump) c->texBump.Alloc((size_t)12 * NR);
         if (c->texGeneral) c->texR.Alloc((size_t)kNSpectrumSamples * NR);
+        if (c->S.matSssTex) c->texS.Alloc((size_t)2 * kNSpectrumSamples * NR);
     }
     if (c->hasMix) c->hitMat.Alloc((size_t)2 * NR);
     if (c->rayBinning) {
@@ -1529,6 +1537,7 @@ static void AllocPaths(pbrt_context *c, int64_t N) {
     st.texBump[0] = c->S.hasBump ? c->texBump.p : nullptr;
     st.texBump[1] = c->S.hasBump ? c->texBump.p + (size_t)6 * NR : nullptr;
     st.texR = c->texR.p;
+    st.texS = c->texS.p;
     st.hitMat[0] = c->hasMix ? c->hitMat.p : nullptr;
     st.hitMat[1] = c->hasMix ? c->hitMat.p + NR : nullptr;
     st.raySort = c->rayBinning ? c->raySort.p : nullptr;
@@ -1990,6 +1999,7 @@ int pbrt_scene_get_flat(const pbrt_scene *scene, pbrt_scene_flat *f) {
         f->material_mix = t.matMixNode.data();
         f->material_bump = t.matBumpNode.data();
         f->material_hair_tex = t.anyHairTex ? t.matHairNode.data() : nullptr;
+        f->material_sss_tex = t.anySssTex ? t.matSssNode.data() : nullptr;
         for (int k = 0; k < 12; ++k) f->camera_from_render[k] = s.cameraFromRender[k];
         for (int k = 0; k < 3; ++k) {
             f->camera_min_diff[k] = s.minPosDx[k];
@@ -2107,7 +2117,7 @@ int pbrt_context_create(const pbrt_scene *scene, int device, int64_t maxPaths, p
             size_t freeB = 0, totalB = 0;
             HIPCHECK(hipMemGetInfo(&freeB, &totalB));
             const int64_t perPath = PathStateBytesPerPath(c->volumetric, c->S.dispersive, c->S.textured, c->texGeneral, c->hasMix,
-                                                       c->S.hasBump) +
+                                                       c->S.hasBump, c->S.matSssTex != nullptr) +
                                     (c->rayBinning ? 32 : 0);
             const int64_t fit = (int64_t)(freeB / 4 * 3) / perPath - kShards * 320;
             if (fit < 4096) throw Error("not enough free device memory for path state");

@@ -430,6 +430,8 @@ class Parser {
         std::string normalMap;  // "normalmap" image file
         bool hasHair = false;   // hair: textured eta, beta_m, beta_n, alpha, eumelanin, pheomelanin
         Param hair[6];          // type "" = not textured
+        bool hasSss = false;    // subsurface: textured sigma_a, and sigma_s or mfp (Unbounded)
+        Param sss[2];
     };
     std::vector<MatTexPending> matTexPending;
     void ResolveTextures();
@@ -907,9 +909,18 @@ class Parser {
                 Param *sa = ps.Find("sigma_a"), *ss = ps.Find("sigma_s");
                 if (sa && !ss) throw Error(ps.loc + ": Provided \"sigma_a\" parameter without \"sigma_s\".");
                 if (ss && !sa) throw Error(ps.loc + ": Provided \"sigma_s\" parameter without \"sigma_a\".");
+                // a textured sigma_a / sigma_s / mfp (GetSpectrumTextureOrNull, Unbounded) is
+                // evaluated per hit by the texture stage; k_vsss_* read it at the entry record
+                auto sssTex = [&](Param *q, int k) {
+                    MatTexPending &mp = PendingTex(ps.loc);
+                    mp.hasSss = true;
+                    mp.sss[k] = *q;
+                };
                 if (sa) {
-                    d.a = param(sa, false);
-                    d.b = param(ss, false);
+                    if (sa->type == "texture") sssTex(sa, 0);
+                    else d.a = param(sa, false);
+                    if (ss->type == "texture") sssTex(ss, 1);
+                    else d.b = param(ss, false);
                 } else if (Param *refl = ps.Find("reflectance")) {
                     d.mode = 1;
                     if (refl->type == "texture") {
@@ -921,8 +932,12 @@ class Parser {
                     } else {
                         d.a = param(refl, true);
                     }
-                    if (Param *mfp = ps.Find("mfp")) d.b = param(mfp, false);
-                    else d.b.kind = 0, d.b.value = 1;  // ConstantSpectrum(1)
+                    if (Param *mfp = ps.Find("mfp")) {
+                        if (mfp->type == "texture") sssTex(mfp, 1);
+                        else d.b = param(mfp, false);
+                    } else {
+                        d.b.kind = 0, d.b.value = 1;  // ConstantSpectrum(1)
+                    }
                 } else {
                     d.a = unbounded(.0011f, .0024f, .014f);
                     d.b = unbounded(2.55f, 3.21f, 3.77f);
@@ -3423,6 +3438,11 @@ void Parser::ResolveTextures() {
                 const int node = FloatParamNode(mp.hair[k].type.empty() ? nullptr : &mp.hair[k], 0.f, mp.loc);
                 m.texHair[k] = CompileTexProgram(scene, node, false);
             }
+        }
+        if (mp.hasSss) {
+            for (int k = 0; k < 2; ++k)
+                if (!mp.sss[k].type.empty())
+                    m.texSss[k] = CompileTexProgram(scene, SpectrumParamNode(&mp.sss[k], kSpecUnbounded, 1.f, mp.loc), true);
         }
         if (mp.hasRough) {
             const int u = FloatParamNode(mp.ur.type.empty() ? nullptr : &mp.ur, 0.f, mp.loc);

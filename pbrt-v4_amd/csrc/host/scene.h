@@ -125,6 +125,9 @@ struct MaterialDesc {
     // beta_n, alpha, eumelanin, pheomelanin (-1: the constant above); the concentrations are
     // textured as a pair (a missing one is the constant 0), sigma_a then formed per hit
     int texHair[6] = {-1, -1, -1, -1, -1, -1};
+    // textured subsurface spectra (materials.h:823-841, Unbounded): sigma_a, and sigma_s or mfp
+    // (-1: the SubsurfaceDesc constant)
+    int texSss[2] = {-1, -1};
     int measured = -1;  // MeasuredMaterial: its SceneDesc::measured entry
     std::string name;
 };

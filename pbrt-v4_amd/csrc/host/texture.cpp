@@ -1011,6 +1011,10 @@ void BuildTexTables(const SceneDesc &s, TexTables *t) {
             t->matHairNode.push_back(root(m.texHair[k]));
             t->anyHairTex = t->anyHairTex || m.texHair[k] >= 0;
         }
+        for (int k = 0; k < 2; ++k) {
+            t->matSssNode.push_back(root(m.texSss[k]));
+            t->anySssTex = t->anySssTex || m.texSss[k] >= 0;
+        }
     }
 }
 // a TexView over host copies (debug entry points; the device view points at DevBufs)

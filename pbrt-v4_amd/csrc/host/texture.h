@@ -66,6 +66,8 @@ struct TexTables {
     std::vector<int32_t> matBumpNode; // [nMaterials][2] displacement root node, normal map image
     std::vector<int32_t> matHairNode; // [nMaterials][6] hair eta beta_m beta_n alpha eumelanin pheomelanin root nodes
     bool anyHairTex = false;
+    std::vector<int32_t> matSssNode;  // [nMaterials][2] subsurface sigma_a, sigma_s | mfp root nodes
+    bool anySssTex = false;
     std::vector<int32_t> nodeInfo, imageInfo, levelInfo, rawInfo;
     std::vector<float> nodeParams, specFlat, rawGamma;
     std::vector<uint8_t> rawData;

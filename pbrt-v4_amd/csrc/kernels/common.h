@@ -1690,8 +1690,9 @@ __device__ __attribute__((noinline)) int ResolveMixMaterial(const DeviceScene &S
 // closest-hit-to-shade pass), with k_texture<*, false, false>'s private segment grown from 108 to
 // 2012 B per lane (the kernel's modified DeviceScene argument spilled to scratch for the callee's
 // reference) and 56 more VGPRs; inlined, the kernels keep the inline copy's code and resources.
-// Hair: the textured hair floats are compiled in (k_vtexture's instantiation for scenes with
-// S.matHairTex; elsewhere the block would only cost registers)
+// Hair: the textured hair floats and subsurface spectra are compiled in (k_vtexture's
+// instantiation for scenes with S.matHairTex or S.matSssTex; elsewhere the blocks would only
+// cost registers)
 template <bool Full, bool Ext, bool Hair = false>
 __device__ __forceinline__ void HitTextures(const DeviceScene &S, const PathState &st, int depth, int ri, int prim,
                                             int mat, const float *hitB, const float *lambda0s) {
@@ -1702,7 +1703,9 @@ __device__ __forceinline__ void HitTextures(const DeviceScene &S, const PathStat
     const int4 h0 = Hair ? S.matHairTex[2 * mat] : make_int4(-1, -1, -1, -1);
     const int h1 = Hair ? S.matHairTex[2 * mat + 1].x : -1;
     const bool hairT = h0.x >= 0 || h0.y >= 0 || h0.z >= 0 || h0.w >= 0 || h1 >= 0;
-    if (mt.x < 0 && mt.y < 0 && !mb.z && !hairT) return;
+    const int2 sx = Hair && S.matSssTex ? S.matSssTex[mat] : make_int2(-1, -1);
+    const bool sssT = sx.x >= 0 || sx.y >= 0;
+    if (mt.x < 0 && mt.y < 0 && !mb.z && !hairT && !sssT) return;
     V3 p0, p1, p2;
     PrimVerts(S, prim, &p0, &p1, &p2);
     const TriSurface surf = SurfaceAt<Ext>(S, prim, p0, p1, p2, hitB[ri], hitB[N + ri], hitB[2 * N + ri]);
@@ -1787,6 +1790,19 @@ __device__ __forceinline__ void HitTextures(const DeviceScene &S, const PathStat
                 for (SpectralIter it(lambda0s[ri]); it.i < kNSpectrumSamples; it.Next())
                     st.texR[(size_t)it.i * N + ri] = scale * SigmoidPolynomial(c[0], c[1], c[2], it.lam);
                 st.texCoef[3 * (size_t)N + ri] = 1.f;
+            }
+        }
+        if (sssT) {
+            // SubsurfaceMaterial's texEval(sigma_a | sigma_s | mfp, ctx, lambda) per wavelength
+            // (materials.h:823-841; Unbounded spectrum programs) into texS[k][i]
+            const int sp[2] = {sx.x, sx.y};
+            for (int k = 0; k < 2; ++k) {
+                if (sp[k] < 0) continue;
+                const DeviceTexProgram pg = S.tex.progs[sp[k]];
+                float R[kTexMaxRegs];
+                TexPhase1(S.tex, pg, tc, R);
+                for (SpectralIter it(lambda0s[ri]); it.i < kNSpectrumSamples; it.Next())
+                    st.texS[((size_t)k * kNSpectrumSamples + it.i) * N + ri] = TexPhase2(S.tex, pg, R, it.lam, it.i);
             }
         }
     }

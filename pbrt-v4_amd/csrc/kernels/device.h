@@ -275,6 +275,9 @@ struct DeviceScene {
     // textured hair floats: per material 2 int4 of programs {eta, beta_m, beta_n, alpha},
     // {eumelanin, pheomelanin, -, -} (-1: constant); nullptr when no hair is textured
     const int4 *matHairTex;
+    // textured subsurface spectra: per material {sigma_a, sigma_s | mfp} programs (-1: constant);
+    // nullptr when none is textured
+    const int2 *matSssTex;
     // MixMaterial: per material {material 0, material 1, amount program, 0}
     const int4 *matMix;
     // this struct's copy in device memory (static scene fields only): out-of-line functions
@@ -331,6 +334,7 @@ struct PathState {
     // reflectance as sigmoid coefficients c0 c1 c2 + a flag (1: the per-wavelength values are
     // in texR), then the TrowbridgeReitz alphas of a textured roughness; null when untextured
     float *texCoef;     // [8][NR]
+    float *texS;        // [2][31][NR] textured subsurface sigma_a, sigma_s | mfp per wavelength
     float *texBump[2];  // by depth parity, [6][NR]: the bump / normal-mapped shading normal and
                         // dpdu of a record (null without such materials)
     float *texR;        // [31][NR] general reflectance expressions (null when none)

@@ -1769,10 +1769,13 @@ __device__ inline float SssSpectrumAt(const DeviceScene &S, const float *q, floa
 // A textured subsurface reflectance (materials.h:823-841 texEval(reflectance)): the texture
 // stage's value at the entry record src of this iteration, per wavelength index i (sigmoid
 // coefficients, or one value per wavelength); on == false: the material's constant form
+// sa / sb: a textured sigma_a and sigma_s | mfp at the entry record (texS + src, stride NR per
+// wavelength; null: the constant)
 struct SssTexRefl {
     bool on = false, perLambda = false;
     float c0 = 0, c1 = 0, c2 = 0;
     const float *r = nullptr;  // texR + src, stride NR
+    const float *sa = nullptr, *sb = nullptr;
     int NR = 0;
     __device__ float At(int i, float lam) const {
         return perLambda ? r[(size_t)i * NR] : SigmoidPolynomial(c0, c1, c2, lam);
@@ -1780,8 +1783,15 @@ struct SssTexRefl {
 };
 __device__ inline SssTexRefl SssTexReflOf(const DeviceScene &S, const PathState &st, int mat, int src) {
     SssTexRefl x;
-    if (!S.textured || S.matTex[mat].x < 0) return x;
+    if (!S.textured) return x;
     const int NR = st.NR;
+    x.NR = NR;
+    if (S.matSssTex) {
+        const int2 p = S.matSssTex[mat];
+        if (p.x >= 0) x.sa = st.texS + src;
+        if (p.y >= 0) x.sb = st.texS + (size_t)kNSpectrumSamples * NR + src;
+    }
+    if (S.matTex[mat].x < 0) return x;
     x.on = true;
     x.perLambda = st.texCoef[3 * (size_t)NR + src] != 0;
     x.c0 = st.texCoef[src];
@@ -1797,11 +1807,12 @@ __device__ inline SssCoeffs SssCoeffsAt(const DeviceScene &S, const float *P, co
                                         const SssTexRefl &tex = SssTexRefl{}, int i = 0) {
     float sa, ss;
     if (P[0] == 0) {
-        const float a = P[1] * SssSpectrumAt(S, P + 4, lam), b = P[1] * SssSpectrumAt(S, P + 11, lam);
+        const float a = P[1] * (tex.sa ? tex.sa[(size_t)i * tex.NR] : SssSpectrumAt(S, P + 4, lam));
+        const float b = P[1] * (tex.sb ? tex.sb[(size_t)i * tex.NR] : SssSpectrumAt(S, P + 11, lam));
         sa = a > 0 ? a : 0.f;  // ClampZero
         ss = b > 0 ? b : 0.f;
     } else {
-        const float m = P[1] * SssSpectrumAt(S, P + 11, lam);
+        const float m = P[1] * (tex.sb ? tex.sb[(size_t)i * tex.NR] : SssSpectrumAt(S, P + 11, lam));
         const float mfree = m > 0 ? m : 0.f;
         const float r = Clampf(tex.on ? tex.At(i, lam) : SssSpectrumAt(S, P + 4, lam), 0, 1);
         SssFromDiffuse(t, r, mfree, &sa, &ss);
@@ -3027,7 +3038,7 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
     // Ext: analytic shapes or image lights in the scene (their paths compiled in)
     if (S.nShapes > 0 || S.nEnv > 0 || S.nImageDelta > 0 || S.hasSpread || S.nImageAreaLights > 0) {
         if (S.textured) {
-            if (S.matHairTex) hipLaunchKernelGGL((k_vtexture<true, true>), gW, block, 0, s, S, st, v, wf);
+            if (S.matHairTex || S.matSssTex) hipLaunchKernelGGL((k_vtexture<true, true>), gW, block, 0, s, S, st, v, wf);
             else hipLaunchKernelGGL(k_vtexture<true>, gW, block, 0, s, S, st, v, wf);
             if (S.matTypeMask & other) hipLaunchKernelGGL((k_vsurface<false, true, true>), gW, block, surfLds, s, S, st, v, wf);
             else hipLaunchKernelGGL((k_vsurface<true, true, true>), gW, block, surfLds, s, S, st, v, wf);
@@ -3041,7 +3052,7 @@ hipError_t LaunchVolIteration(const DeviceScene &S, const PathState &st, const V
         VOL_REST(true);
     } else {
         if (S.textured) {
-            if (S.matHairTex) hipLaunchKernelGGL((k_vtexture<false, true>), gW, block, 0, s, S, st, v, wf);
+            if (S.matHairTex || S.matSssTex) hipLaunchKernelGGL((k_vtexture<false, true>), gW, block, 0, s, S, st, v, wf);
             else hipLaunchKernelGGL(k_vtexture<false>, gW, block, 0, s, S, st, v, wf);
             if (S.matTypeMask & other) hipLaunchKernelGGL((k_vsurface<false, false, true>), gW, block, surfLds, s, S, st, v, wf);
             else hipLaunchKernelGGL((k_vsurface<true, false, true>), gW, block, surfLds, s, S, st, v, wf);

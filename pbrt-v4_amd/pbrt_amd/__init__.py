@@ -118,6 +118,7 @@ class SceneFlat(ctypes.Structure):
         ("options", ctypes.c_int),
         ("tex_basis", ctypes.POINTER(ctypes.c_float)),
         ("material_hair_tex", ctypes.POINTER(ctypes.c_int32)),
+        ("material_sss_tex", ctypes.POINTER(ctypes.c_int32)),
     ]
 
 

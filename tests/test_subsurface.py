@@ -114,10 +114,7 @@ def test_subsurface_loader_forms(pa):
     ('Material "subsurface" "rgb sigma_s" [1 1 1]', 'without "sigma_a"'),
     ('Material "subsurface" "string name" "Nope"', "named medium not found"),
     ('Material "subsurface" "rgb reflectance" [1.2 0.5 0.5]', "albedo"),
-    ('Texture "t" "spectrum" "checkerboard"\nMaterial "subsurface" "rgb reflectance" [0.5 0.5 0.5] "texture mfp" "t"',
-     "not supported"),
-    ('Texture "t" "spectrum" "checkerboard"\nMaterial "subsurface" "texture sigma_a" "t" "rgb sigma_s" [1 1 1]',
-     "not supported"),
+    ('Material "subsurface" "rgb reflectance" [0.5 0.5 0.5] "texture mfp" "nope"', "nope"),
 ])
 def test_subsurface_loader_errors(pa, material, msg):
     with pytest.raises(pa.PbrtError, match=msg):
@@ -152,8 +149,43 @@ def test_textured_reflectance_oracle(pa, oracle):
     assert np.abs(a - b).mean() > 1e-4
 
 
+# textured mfp (with a constant or a textured reflectance) and textured sigma_a / sigma_s
+# (GetSpectrumTextureOrNull, Unbounded; texEval per hit at the entry, materials.h:823-841)
+TEX_MFP = ('Texture "m" "spectrum" "checkerboard" "float uscale" 4 "float vscale" 4 "rgb tex1" [0.03 0.03 0.02] '
+           '"rgb tex2" [0.2 0.15 0.1]\nMaterial "subsurface" "rgb reflectance" [0.9 0.6 0.4] "texture mfp" "m"')
+TEX_BOTH = ('Texture "t" "spectrum" "checkerboard" "float uscale" 4 "float vscale" 4 "rgb tex1" [0.9 0.6 0.4] '
+            '"rgb tex2" [0.3 0.5 0.8]\nTexture "m" "spectrum" "scale" "rgb tex" [0.08 0.06 0.05] "float scale" 1.5\n'
+            'Material "subsurface" "texture reflectance" "t" "texture mfp" "m"')
+TEX_SIGMA = ('Texture "sa" "spectrum" "checkerboard" "float uscale" 4 "float vscale" 4 "rgb tex1" [0.8 1.2 2.0] '
+             '"rgb tex2" [3 2 1]\nMaterial "subsurface" "texture sigma_a" "sa" "rgb sigma_s" [20 16 10] "float scale" 3')
+
+
+@pytest.mark.parametrize("material, const, slots", [
+    (TEX_MFP, 'Material "subsurface" "rgb reflectance" [0.9 0.6 0.4] "rgb mfp" [0.03 0.03 0.02]', (1,)),
+    (TEX_SIGMA, 'Material "subsurface" "rgb sigma_a" [0.8 1.2 2.0] "rgb sigma_s" [20 16 10] "float scale" 3', (0,)),
+])
+def test_textured_sss_spectra_oracle(pa, oracle, material, const, slots):
+    """Textured sigma_a / sigma_s / mfp load into material_sss_tex, render finite, and differ
+    from the constant form that equals one of the checks."""
+    kw = dict(xresolution=32, yresolution=24, spp=8)
+    a_sc = pa.Scene.from_string(scene(material, BLOB + BOX), SCENES, **kw)
+    b_sc = pa.Scene.from_string(scene(const, BLOB + BOX), SCENES, **kw)
+    f = a_sc.flat()
+    st = np.ctypeslib.as_array(f.material_sss_tex, shape=(f.n_materials * 2,)).reshape(-1, 2)
+    assert sorted({k for row in st for k in range(2) if row[k] >= 0}) == list(slots)
+    assert not b_sc.flat().material_sss_tex
+    m = [f.output_rgb_from_sensor_rgb[i] for i in range(9)]
+    a = oracle.film_to_rgb(oracle.render(a_sc, threads=8), m)
+    b = oracle.film_to_rgb(oracle.render(b_sc, threads=8), m)
+    assert np.isfinite(a).all() and a.mean() > 0.01
+    assert np.abs(a - b).mean() > 1e-4
+
+
 FORMS = {
     "tex_reflectance": TEX_REFL,
+    "tex_mfp": TEX_MFP,
+    "tex_both": TEX_BOTH,
+    "tex_sigma": TEX_SIGMA,
     "sigma": 'Material "subsurface" "rgb sigma_a" [0.8 1.2 2.0] "rgb sigma_s" [20 16 10] "float scale" 3',
     "reflectance": 'Material "subsurface" "rgb reflectance" [0.85 0.55 0.35] "rgb mfp" [0.08 0.06 0.05] "float eta" 1.45',
     "named_rough": 'Material "subsurface" "string name" "Ketchup" "float scale" 40 "float roughness" 0.25',

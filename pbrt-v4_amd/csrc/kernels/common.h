@@ -1700,8 +1700,9 @@ __device__ __forceinline__ void HitTextures(const DeviceScene &S, const PathStat
     const int4 mt = S.matTex[mat];
     const int4 mb = S.hasBump ? S.matBump[mat] : make_int4(-1, -1, 0, 0);
     // textured hair floats (Full stages only): eta, beta_m, beta_n, alpha and the concentrations
-    const int4 h0 = Hair ? S.matHairTex[2 * mat] : make_int4(-1, -1, -1, -1);
-    const int h1 = Hair ? S.matHairTex[2 * mat + 1].x : -1;
+    // (the instantiation also serves scenes with textured subsurface spectra and no hair table)
+    const int4 h0 = Hair && S.matHairTex ? S.matHairTex[2 * mat] : make_int4(-1, -1, -1, -1);
+    const int h1 = Hair && S.matHairTex ? S.matHairTex[2 * mat + 1].x : -1;
     const bool hairT = h0.x >= 0 || h0.y >= 0 || h0.z >= 0 || h0.w >= 0 || h1 >= 0;
     const int2 sx = Hair && S.matSssTex ? S.matSssTex[mat] : make_int2(-1, -1);
     const bool sssT = sx.x >= 0 || sx.y >= 0;
